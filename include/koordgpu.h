@@ -1,0 +1,226 @@
+/*
+ * koordgpu.h — C ABI of the MI355X batch Filter/Score engine for koord-scheduler.
+ *
+ * This is the drop-in boundary. Everything that crosses it is a flat,
+ * pointer-free struct of int64 fields (cgo rule: no Go pointers inside), a caller-owned
+ * array, or an opaque engine handle. Device memory is owned by the engine.
+ *
+ * What each entry point replaces in the reference (all paths under /root/reference):
+ *
+ *   kg_engine_create        plugin construction: loadaware.New (pkg/scheduler/plugins/loadaware/load_aware.go:76-110)
+ *                           with LoadAwareSchedulingArgs (pkg/scheduler/apis/config/types.go:30-76, defaults
+ *                           v1beta2/defaults.go:76-99) + upstream NodeResourcesFit args + profile score weights
+ *                           (config/manager/scheduler-config.yaml:82-91).
+ *   kg_nodes_upsert         upstream scheduler-cache node add/update after the node transformer
+ *                           (pkg/util/transformer/node_transformer.go:40-75); NodeInfo.Allocatable.
+ *   kg_node_metrics_update  NodeMetric lister reads done per (pod,node) in LoadAware Filter/Score
+ *                           (load_aware.go:133,278) — hoisted to ingest.
+ *   kg_pods_add             assigned-pod informer add: upstream NodeInfo.AddPod + podAssignCache.OnAdd/assign
+ *                           (pkg/scheduler/plugins/loadaware/pod_assign_cache.go:53-68,82-88).
+ *   kg_pods_remove          pod delete / Unreserve / ForgetPod: NodeInfo.RemovePod + podAssignCache.unAssign
+ *                           (pod_assign_cache.go:70-80,102-117; load_aware.go:265-267).
+ *   kg_pods_schedule        the per-pod hot loop: upstream findNodesThatPassFilters + prioritizeNodes + selectHost +
+ *                           assume, reached in koordinator through Scheduler.SchedulePod interception
+ *                           (pkg/scheduler/frameworkext/framework_extender_factory.go:136-185) and
+ *                           FrameworkExtender.RunFilterPluginsWithNominatedPods / RunScorePlugins
+ *                           (framework_extender.go:204-258). Sequential FIFO semantics; assume applied on device.
+ *   kg_pods_evaluate        one pod against every node WITHOUT assume: per-node Filter status and per-plugin Score,
+ *                           i.e. RunFilterPlugins + RunScorePlugins for one pod (framework_extender.go:204-258) —
+ *                           also what --debug-scores prints (frameworkext/debug.go:61-108).
+ *   kg_last_error           error text for the last failing call on this thread (maps to framework.NewStatus(Error,…)).
+ *
+ * Units follow the reference's getResourceValue (load_aware/helper.go:146-151): cpu-like resources in
+ * milli-units (Quantity.MilliValue), everything else in Quantity.Value.  Quantities must be integral.
+ */
+#ifndef KOORDGPU_H_
+#define KOORDGPU_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KG_ABI_VERSION 1
+
+/* ---- resource slots (fixed order) ------------------------------------------------------- */
+enum {
+  KG_RES_CPU = 0,          /* cpu, milli-cores                                   */
+  KG_RES_MEMORY = 1,       /* memory, bytes                                      */
+  KG_RES_EPHEMERAL = 2,    /* ephemeral-storage, bytes                           */
+  KG_RES_BATCH_CPU = 3,    /* kubernetes.io/batch-cpu (Value)                    */
+  KG_RES_BATCH_MEMORY = 4, /* kubernetes.io/batch-memory (Value)                 */
+  KG_RES_MID_CPU = 5,      /* kubernetes.io/mid-cpu (Value)                      */
+  KG_RES_MID_MEMORY = 6,   /* kubernetes.io/mid-memory (Value)                   */
+  KG_RES_RESERVED7 = 7,
+  KG_RES_MAX = 8
+};
+
+/* koordinator priority classes (apis/extension/priority.go:29-35); the caller passes the result of
+ * extension.GetPodPriorityClassWithDefault (apis/extension/priority_utils.go:26-48). */
+enum { KG_PRIO_NONE = 0, KG_PRIO_PROD = 1, KG_PRIO_MID = 2, KG_PRIO_BATCH = 3, KG_PRIO_FREE = 4 };
+
+/* status codes: 0 ok, <0 error class (framework.Error on the Go side) */
+enum {
+  KG_OK = 0,
+  KG_E_INVALID = -1,     /* invalid argument / validation failure   */
+  KG_E_DEVICE = -2,      /* HIP runtime error                       */
+  KG_E_COLLECTIVE = -3,  /* RCCL error                              */
+  KG_E_NOMEM = -4,       /* allocation failure                      */
+  KG_E_UNSUPPORTED = -5  /* input outside the accelerated profile   */
+};
+
+/* per-node filter reasons written by kg_pods_evaluate (bit set = plugin rejected the node) */
+enum {
+  KG_REJECT_FIT_PODS = 1 << 0,      /* NodeResourcesFit: Too many pods                 */
+  KG_REJECT_FIT_CPU = 1 << 1,       /* NodeResourcesFit: Insufficient cpu              */
+  KG_REJECT_FIT_MEMORY = 1 << 2,    /* NodeResourcesFit: Insufficient memory           */
+  KG_REJECT_LOADAWARE = 1 << 3,     /* LoadAwareScheduling: usage exceed threshold     */
+  KG_REJECT_INVALID_NODE = 1 << 4   /* deleted / never-upserted slot                   */
+};
+
+/* node flags */
+enum {
+  KG_NODE_VALID = 1 << 0,
+  KG_NODE_HAS_RAW_ALLOCATABLE = 1 << 1,   /* node.koordinator.sh/raw-allocatable annotation present */
+  KG_NODE_HAS_CUSTOM_THRESHOLDS = 1 << 2  /* custom-usage-thresholds annotation parsed OK            */
+};
+
+/* pod flags */
+enum { KG_POD_DAEMONSET = 1 << 0 };
+
+/* Engine configuration: plugin args + profile weights + engine tuning.  All int64 for a padding-free
+ * layout.  A threshold/weight of 0 means "resource absent from the map". */
+typedef struct kg_config {
+  int64_t abi_version;                         /* must be KG_ABI_VERSION                              */
+  /* LoadAwareSchedulingArgs (config/types.go:30-76) */
+  int64_t la_filter_expired_node_metrics;      /* bool                                                */
+  int64_t la_node_metric_expiration_seconds;   /* <0 = nil                                            */
+  int64_t la_resource_weights[KG_RES_MAX];
+  int64_t la_usage_thresholds[KG_RES_MAX];
+  int64_t la_prod_usage_thresholds[KG_RES_MAX];
+  int64_t la_estimated_scaling_factors[KG_RES_MAX];
+  int64_t la_score_according_prod_usage;       /* bool                                                */
+  /* NodeResourcesFit (upstream) LeastAllocated scoring strategy resources */
+  int64_t fit_resource_weights[KG_RES_MAX];
+  /* profile: plugins enabled at the Filter / Score extension points and their Score weights */
+  int64_t fit_filter;                          /* NodeResourcesFit at Filter                          */
+  int64_t fit_score;                           /* NodeResourcesFit at Score                           */
+  int64_t la_filter;                           /* LoadAwareScheduling at Filter                       */
+  int64_t la_score;                            /* LoadAwareScheduling at Score                        */
+  int64_t weight_fit;
+  int64_t weight_loadaware;
+  /* engine tuning (0 = default) */
+  int64_t batch_pods;                          /* pods resolved per device round (B, 1..64)           */
+  int64_t pods_per_wave;                       /* pods one eval wave scores per round (1..B)          */
+  int64_t device_id;                           /* HIP device ordinal (-1 = current)                   */
+  int64_t reserved[8];
+} kg_config;
+
+/* One node (snapshot index = position given by the caller). */
+typedef struct kg_node {
+  int64_t allocatable[KG_RES_MAX];             /* NodeInfo.Allocatable                                */
+  int64_t allowed_pods;                        /* Allocatable.AllowedPodNumber                        */
+  int64_t flags;                               /* KG_NODE_*                                           */
+  int64_t raw_allocatable[KG_RES_MAX];         /* extension.GetNodeRawAllocatable (EstimateNode)      */
+  int64_t raw_allocatable_present[KG_RES_MAX]; /* key present in the annotation map                   */
+  int64_t custom_usage_thresholds[KG_RES_MAX]; /* extension.GetCustomUsageThresholds; -1 = absent      */
+  int64_t custom_prod_usage_thresholds[KG_RES_MAX];
+} kg_node;
+
+/* NodeMetric status summary for one node (apis/slo/v1alpha1/nodemetric_types.go:107-122). */
+typedef struct kg_node_metric {
+  int64_t present;                             /* lister Get succeeded                                */
+  int64_t has_node_metric;                     /* Status.NodeMetric != nil                            */
+  int64_t has_update_time;                     /* Status.UpdateTime != nil                            */
+  int64_t update_time_unix_nano;
+  int64_t node_usage[KG_RES_MAX];              /* Status.NodeMetric.NodeUsage (cpu milli)             */
+  int64_t node_usage_present[KG_RES_MAX];
+  int64_t pods_metric_count;                   /* len(Status.PodsMetric)                              */
+  int64_t prod_pods_usage[KG_RES_MAX];         /* Σ PodsMetric usage of prod pods (buildPodMetricMap  */
+                                               /* filterProdPod=true + sumPodUsages, helper.go:153-186) */
+} kg_node_metric;
+
+/* One pod, pre-decoded by the caller (PodRequestsAndLimits semantics, pkg/util/pod_resources_utils.go:48-64). */
+typedef struct kg_pod {
+  int64_t requests[KG_RES_MAX];
+  int64_t limits[KG_RES_MAX];
+  int64_t nonzero_requests[2];                 /* schedutil.GetNonzeroRequests: cpu milli, memory     */
+  int64_t priority_class;                      /* KG_PRIO_*                                           */
+  int64_t flags;                               /* KG_POD_*                                            */
+  int64_t reserved[2];
+} kg_pod;
+
+typedef struct kg_stats {
+  int64_t pods_scheduled;                      /* pods with a node                                    */
+  int64_t pods_unschedulable;
+  int64_t device_batches;                      /* eval+resolve rounds issued                          */
+  int64_t node_evaluations;                    /* Σ pods × nodes evaluated                            */
+  double seconds;                              /* wall time inside kg_pods_schedule                   */
+  double reserved[3];
+} kg_stats;
+
+typedef struct kg_engine kg_engine;
+
+/* Defaults: v1beta2.SetDefaults_LoadAwareSchedulingArgs (v1beta2/defaults.go:76-99), NodeResourcesFit
+ * LeastAllocated cpu:1 memory:1, Fit and LoadAware enabled with weight 1. */
+void kg_config_default(kg_config* cfg);
+
+/* n_ranks>1: the engine shards node evaluation over ranks (one process per GPU) and exchanges candidates with
+ * RCCL; `nccl_unique_id` is the 128-byte ncclUniqueId created on rank 0 and broadcast by the caller. */
+/* ncclGetUniqueId (128 bytes) — call on rank 0, broadcast to the other ranks out of band. */
+int kg_nccl_unique_id(void* out128);
+int kg_engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank, int n_ranks,
+                     const void* nccl_unique_id, kg_engine** out);
+void kg_engine_destroy(kg_engine* e);
+
+int kg_nodes_upsert(kg_engine* e, const kg_node* nodes, const int32_t* idx, int64_t n);
+int kg_nodes_delete(kg_engine* e, const int32_t* idx, int64_t n);
+int kg_node_metrics_update(kg_engine* e, const kg_node_metric* m, const int32_t* idx, int64_t n, int64_t now_unix_nano);
+
+int kg_pods_add(kg_engine* e, const kg_pod* pods, const int32_t* node_idx, int64_t n);
+int kg_pods_remove(kg_engine* e, const kg_pod* pods, const int32_t* node_idx, int64_t n);
+
+/* Schedules `n` pods in FIFO order. out_node_idx[i] = chosen node (-1 = unschedulable), out_score[i] = the
+ * weighted total score of that node. Each placement is assumed before the next pod is evaluated. */
+int kg_pods_schedule(kg_engine* e, const kg_pod* pods, int64_t n, int32_t* out_node_idx, int64_t* out_score,
+                     kg_stats* stats);
+
+/* Evaluates one pod on every node slot [0, n_nodes): reject bits (KG_REJECT_*), NodeResourcesFit score and
+ * LoadAwareScheduling score (unweighted, as the plugins' Score returns them). Any output may be NULL. */
+int kg_pods_evaluate(kg_engine* e, const kg_pod* pod, int32_t* out_reject, int64_t* out_fit_score,
+                     int64_t* out_loadaware_score);
+
+/* Split form of kg_pods_schedule for callers that keep the pod queue resident on the device:
+ * kg_pods_stage decodes + uploads a queue (replacing any staged queue); kg_pods_schedule_staged schedules
+ * queue entries [first, first+count) (device only, blocks until done); kg_results_fetch copies decisions back. */
+int kg_pods_stage(kg_engine* e, const kg_pod* pods, int64_t n);
+int kg_pods_schedule_staged(kg_engine* e, int64_t first, int64_t count, kg_stats* stats);
+int kg_results_fetch(kg_engine* e, int64_t first, int64_t count, int32_t* out_node_idx, int64_t* out_score);
+
+int64_t kg_engine_num_nodes(const kg_engine* e);
+/* Reads the DEVICE copy of the mutable node state: NodeInfo.Requested{cpu,mem}, NonZeroRequested{cpu,mem},
+ * pod count and the LoadAware estimated usage Σ EstimatePod over the assign cache (all pods / prod pods).
+ * Any output may be NULL. */
+int kg_nodes_read_state(kg_engine* e, int64_t* requested_cpu, int64_t* requested_mem, int64_t* nonzero_cpu,
+                        int64_t* nonzero_mem, int64_t* num_pods, int64_t* la_est_cpu, int64_t* la_est_mem,
+                        int64_t* la_est_prod_cpu, int64_t* la_est_prod_mem);
+
+/* Measurement hooks (bench.py): replays one device round's kernel `which` (0 = eval, 1 = resolve) `iters` times
+ * on the engine stream between HIP events, restoring state, and returns the mean duration in ms plus the
+ * algorithmic bytes that kernel must move per launch. Requires a staged queue. */
+int kg_bench_kernel(kg_engine* e, int which, int iters, double* avg_ms, double* algo_bytes);
+/* Debug: leastRequestedScore on the device for n (requested, capacity) pairs (exactness test of the
+ * division-free path). */
+int kg_debug_least_requested(kg_engine* e, const int64_t* requested, const int64_t* capacity, int64_t* out,
+                             int64_t n);
+
+const char* kg_last_error(void);
+int kg_abi_version(void);
+/* sizeof of the ABI structs (0 kg_config, 1 kg_node, 2 kg_node_metric, 3 kg_pod, 4 kg_stats) for binding checks. */
+int64_t kg_abi_struct_size(int which);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KOORDGPU_H_ */

@@ -1,0 +1,170 @@
+"""ctypes/numpy mirror of include/koordgpu.h.
+
+Every ABI struct is a run of int64 fields, so a numpy structured dtype with the same field order IS the C
+layout; arrays of nodes / metrics / pods are passed to the library as plain pointers (the same memory a
+cgo caller would hand over).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+RES_MAX = 8
+RES_CPU, RES_MEMORY, RES_EPHEMERAL, RES_BATCH_CPU, RES_BATCH_MEMORY, RES_MID_CPU, RES_MID_MEMORY = range(7)
+RESOURCE_SLOTS = {
+    "cpu": RES_CPU,
+    "memory": RES_MEMORY,
+    "ephemeral-storage": RES_EPHEMERAL,
+    "kubernetes.io/batch-cpu": RES_BATCH_CPU,
+    "kubernetes.io/batch-memory": RES_BATCH_MEMORY,
+    "kubernetes.io/mid-cpu": RES_MID_CPU,
+    "kubernetes.io/mid-memory": RES_MID_MEMORY,
+}
+
+PRIO_NONE, PRIO_PROD, PRIO_MID, PRIO_BATCH, PRIO_FREE = range(5)
+PRIORITY_CLASSES = {"": PRIO_NONE, "koord-prod": PRIO_PROD, "koord-mid": PRIO_MID,
+                    "koord-batch": PRIO_BATCH, "koord-free": PRIO_FREE}
+
+OK, E_INVALID, E_DEVICE, E_COLLECTIVE, E_NOMEM, E_UNSUPPORTED = 0, -1, -2, -3, -4, -5
+REJECT_FIT_PODS, REJECT_FIT_CPU, REJECT_FIT_MEMORY, REJECT_LOADAWARE, REJECT_INVALID_NODE = 1, 2, 4, 8, 16
+NODE_VALID, NODE_HAS_RAW_ALLOCATABLE, NODE_HAS_CUSTOM_THRESHOLDS = 1, 2, 4
+POD_DAEMONSET = 1
+ABI_VERSION = 1
+
+
+def _i64(name, n=None):
+    return (name, np.int64) if n is None else (name, np.int64, (n,))
+
+
+CONFIG_DTYPE = np.dtype([
+    _i64("abi_version"),
+    _i64("la_filter_expired_node_metrics"),
+    _i64("la_node_metric_expiration_seconds"),
+    _i64("la_resource_weights", RES_MAX),
+    _i64("la_usage_thresholds", RES_MAX),
+    _i64("la_prod_usage_thresholds", RES_MAX),
+    _i64("la_estimated_scaling_factors", RES_MAX),
+    _i64("la_score_according_prod_usage"),
+    _i64("fit_resource_weights", RES_MAX),
+    _i64("fit_filter"), _i64("fit_score"), _i64("la_filter"), _i64("la_score"),
+    _i64("weight_fit"), _i64("weight_loadaware"),
+    _i64("batch_pods"), _i64("pods_per_wave"), _i64("device_id"),
+    _i64("reserved", 8),
+])
+
+NODE_DTYPE = np.dtype([
+    _i64("allocatable", RES_MAX),
+    _i64("allowed_pods"),
+    _i64("flags"),
+    _i64("raw_allocatable", RES_MAX),
+    _i64("raw_allocatable_present", RES_MAX),
+    _i64("custom_usage_thresholds", RES_MAX),
+    _i64("custom_prod_usage_thresholds", RES_MAX),
+])
+
+METRIC_DTYPE = np.dtype([
+    _i64("present"), _i64("has_node_metric"), _i64("has_update_time"), _i64("update_time_unix_nano"),
+    _i64("node_usage", RES_MAX),
+    _i64("node_usage_present", RES_MAX),
+    _i64("pods_metric_count"),
+    _i64("prod_pods_usage", RES_MAX),
+])
+
+POD_DTYPE = np.dtype([
+    _i64("requests", RES_MAX),
+    _i64("limits", RES_MAX),
+    _i64("nonzero_requests", 2),
+    _i64("priority_class"),
+    _i64("flags"),
+    _i64("reserved", 2),
+])
+
+STATS_DTYPE = np.dtype([
+    _i64("pods_scheduled"), _i64("pods_unschedulable"), _i64("device_batches"), _i64("node_evaluations"),
+    ("seconds", np.float64), ("reserved", np.float64, (3,)),
+])
+
+STRUCT_DTYPES = {0: CONFIG_DTYPE, 1: NODE_DTYPE, 2: METRIC_DTYPE, 3: POD_DTYPE, 4: STATS_DTYPE}
+
+# Every symbol include/koordgpu.h declares (tests check the library exports all of them).
+EXPORTED_SYMBOLS = (
+    "kg_config_default", "kg_engine_create", "kg_engine_destroy", "kg_nodes_upsert", "kg_nodes_delete",
+    "kg_node_metrics_update", "kg_pods_add", "kg_pods_remove", "kg_pods_schedule", "kg_pods_evaluate",
+    "kg_pods_stage", "kg_pods_schedule_staged", "kg_results_fetch", "kg_engine_num_nodes",
+    "kg_nodes_read_state", "kg_bench_kernel", "kg_debug_least_requested", "kg_last_error", "kg_abi_version",
+    "kg_abi_struct_size", "kg_nccl_unique_id",
+)
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG_DIR, "libkoordgpu.so")
+
+_lib = None
+
+
+def ptr(a):
+    """Pointer to a numpy array's data (None for None)."""
+    if a is None:
+        return None
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+def load_library(path: str | None = None):
+    """Loads the in-tree engine library.  Fails loudly if it is missing: there is no CPU fallback."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise RuntimeError(f"koordgpu engine library not built: {p} (run `make -C koordinator_amd` "
+                           f"or __graft_entry__.build())")
+    lib = ctypes.CDLL(p, mode=ctypes.RTLD_GLOBAL)
+    vp, i64, i32, i = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int
+    sig = {
+        "kg_config_default": (None, [vp]),
+        "kg_engine_create": (i, [vp, i64, i, i, vp, ctypes.POINTER(vp)]),
+        "kg_engine_destroy": (None, [vp]),
+        "kg_nodes_upsert": (i, [vp, vp, vp, i64]),
+        "kg_nodes_delete": (i, [vp, vp, i64]),
+        "kg_node_metrics_update": (i, [vp, vp, vp, i64, i64]),
+        "kg_pods_add": (i, [vp, vp, vp, i64]),
+        "kg_pods_remove": (i, [vp, vp, vp, i64]),
+        "kg_pods_schedule": (i, [vp, vp, i64, vp, vp, vp]),
+        "kg_pods_evaluate": (i, [vp, vp, vp, vp, vp]),
+        "kg_pods_stage": (i, [vp, vp, i64]),
+        "kg_pods_schedule_staged": (i, [vp, i64, i64, vp]),
+        "kg_results_fetch": (i, [vp, i64, i64, vp, vp]),
+        "kg_engine_num_nodes": (i64, [vp]),
+        "kg_nodes_read_state": (i, [vp] + [vp] * 9),
+        "kg_bench_kernel": (i, [vp, i, i, vp, vp]),
+        "kg_debug_least_requested": (i, [vp, vp, vp, vp, i64]),
+        "kg_last_error": (ctypes.c_char_p, []),
+        "kg_abi_version": (i, []),
+        "kg_abi_struct_size": (i64, [i]),
+        "kg_nccl_unique_id": (i, [vp]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    if lib.kg_abi_version() != ABI_VERSION:
+        raise RuntimeError("koordgpu ABI version mismatch")
+    for which, dt in STRUCT_DTYPES.items():
+        if lib.kg_abi_struct_size(which) != dt.itemsize:
+            raise RuntimeError(f"ABI struct {which} size mismatch: C {lib.kg_abi_struct_size(which)} vs {dt.itemsize}")
+    if path is None:
+        _lib = lib
+    return lib
+
+
+class KoordGPUError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"koordgpu error {code}: {msg}")
+        self.code = code
+
+
+def check(lib, rc: int):
+    if rc != 0:
+        raise KoordGPUError(rc, lib.kg_last_error().decode(errors="replace"))
+    return rc

@@ -1,0 +1,1058 @@
+// engine.hip — koordgpu: MI355X batch Filter/Score engine behind the C ABI of include/koordgpu.h.
+//
+// Device algorithm: scheduling is sequential per pod (each placement is assumed before the
+// next pod is scored), but a placement changes exactly ONE node row.  The engine therefore works in rounds of
+// B queued pods:
+//   1. eval_round   — every (pod, node) pair of the round is scored against the round-start snapshot in one
+//                     wide, coalesced pass; per (pod, 256-node tile) only the top-R packed keys survive
+//                     (score-bit threshold select with wave ballots — no sort, no LDS).
+//   2. [RCCL]       — n_ranks>1: ncclAllGather of the candidate lists (nodes are sharded, state replicated).
+//   3. resolve_round — one wavefront replays the B pods in FIFO order: the best candidate not yet modified in
+//                     this round, vs. the exact re-score of the ≤B rows modified in this round (held in
+//                     registers).  If a tile's whole candidate list was modified and its unknown remainder could
+//                     still win, the round stops early and the rest of the pods go to the next round.
+// Result = exactly the sequential reference decision (proof sketch in DESIGN.md §3.3), ties → lowest index.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/koordgpu.h"
+#include "kernels.h"
+
+using namespace kg;
+
+namespace {
+
+constexpr int kNPT = 4;               // nodes per lane in an eval tile
+constexpr int kTile = kWave * kNPT;   // 256 nodes per tile
+constexpr int kR = 8;                 // candidates kept per (pod, tile)
+constexpr int kEvalWaves = 4;         // waves (tiles) per eval block
+constexpr int kMaxB = 64;             // modified rows are held one per lane of the resolver wave
+constexpr int64_t kMaxNodes = 1 << 20;  // resolver bitmap lives in LDS: N/8 bytes ≤ 128 KiB
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                      \
+  do {                                                                                     \
+    hipError_t e_ = (expr);                                                                \
+    if (e_ != hipSuccess) return fail(KG_E_DEVICE, "%s: %s", #expr, hipGetErrorString(e_)); \
+  } while (0)
+
+#define NCCL_TRY(expr)                                                                           \
+  do {                                                                                           \
+    ncclResult_t r_ = (expr);                                                                    \
+    if (r_ != ncclSuccess) return fail(KG_E_COLLECTIVE, "%s: %s", #expr, ncclGetErrorString(r_)); \
+  } while (0)
+
+// ------------------------------------------------------------------------------------------------
+// Kernels
+// ------------------------------------------------------------------------------------------------
+
+// One wave = one tile of kTile nodes (lane l holds nodes tile*kTile + j*64 + l, j < kNPT) × pods_per_wave pods.
+// Writes lists[(rank, pod, tile)][kR] = the top-kR keys of the tile (unordered, zero-padded).
+__global__ __launch_bounds__(kWave* kEvalWaves) void eval_round(DevTable T, const DevPod* __restrict__ pods,
+                                                                  const int64_t* __restrict__ cursor_p,
+                                                                  int64_t end, int B, int pods_per_wave,
+                                                                  int64_t node_base, int64_t n_local, int nt_local,
+                                                                  EvalParams P, uint64_t* __restrict__ lists) {
+  const int64_t cursor = *cursor_p;
+  if (cursor >= end) return;
+  const int nb = (end - cursor) < (int64_t)B ? (int)(end - cursor) : B;
+  const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
+  const int tile = blockIdx.x * kEvalWaves + wave;
+  const int p0 = blockIdx.y * pods_per_wave;
+  if (tile >= nt_local || p0 >= nb) return;
+  const int p1 = (p0 + pods_per_wave) < nb ? (p0 + pods_per_wave) : nb;
+
+  Row rows[kNPT];
+  bool in_range[kNPT];
+  uint32_t gidx[kNPT];
+#pragma unroll
+  for (int j = 0; j < kNPT; ++j) {
+    const int64_t local = (int64_t)tile * kTile + j * kWave + lane;
+    in_range[j] = local < n_local;
+    gidx[j] = (uint32_t)(node_base + local);
+    if (in_range[j]) rows[j] = load_row(T, node_base + local);
+    else rows[j].flags = 0;
+  }
+  const uint64_t lane_lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+
+  for (int pi = p0; pi < p1; ++pi) {
+    const DevPod p = pods[cursor + pi];
+    uint32_t tot[kNPT];
+    uint64_t fm[kNPT];
+    int nfeas = 0;
+#pragma unroll
+    for (int j = 0; j < kNPT; ++j) {
+      int64_t t = 0;
+      const bool ok = in_range[j] && eval_node(rows[j], p, P, t);
+      tot[j] = (uint32_t)t;
+      fm[j] = __ballot(ok);
+      nfeas += __popcll(fm[j]);
+    }
+    uint64_t sel[kNPT];
+    if (nfeas <= kR) {
+#pragma unroll
+      for (int j = 0; j < kNPT; ++j) sel[j] = fm[j];
+    } else {
+      // τ = largest score with count(score ≥ τ) ≥ kR, by one ballot per score bit.
+      uint32_t cur = 0;
+      for (int b = P.score_bits - 1; b >= 0; --b) {
+        const uint32_t c = cur | (1u << b);
+        int cnt = 0;
+#pragma unroll
+        for (int j = 0; j < kNPT; ++j) cnt += __popcll(__ballot(((fm[j] >> lane) & 1) && tot[j] >= c));
+        if (cnt >= kR) cur = c;
+      }
+      int need = kR;
+      uint64_t eq[kNPT];
+#pragma unroll
+      for (int j = 0; j < kNPT; ++j) {
+        const bool f = (fm[j] >> lane) & 1;
+        sel[j] = __ballot(f && tot[j] > cur);
+        eq[j] = __ballot(f && tot[j] == cur);
+        need -= __popcll(sel[j]);
+      }
+      // ties at τ: lowest node index first (register j, then lane)
+#pragma unroll
+      for (int j = 0; j < kNPT; ++j) {
+        uint64_t m = eq[j];
+        while (need > 0 && m) {
+          const uint64_t low = m & (~m + 1);
+          sel[j] |= low;
+          m ^= low;
+          --need;
+        }
+      }
+    }
+    uint64_t* out = lists + ((size_t)pi * nt_local + tile) * kR;
+    int base = 0;
+#pragma unroll
+    for (int j = 0; j < kNPT; ++j) {
+      if ((sel[j] >> lane) & 1) out[base + __popcll(sel[j] & lane_lt)] = make_key(tot[j], gidx[j]);
+      base += __popcll(sel[j]);
+    }
+    if (lane >= base && lane < kR) out[lane] = 0;
+  }
+}
+
+// Single wavefront: FIFO replay of the round. lane l < nM keeps modified row l in registers; an LDS bitmap
+// marks modified node indices.  Writes out_keys[cursor + j] (0 = unschedulable) and advances the cursor by the
+// number of pods whose decision is proven exact.
+__global__ __launch_bounds__(kWave) void resolve_round(DevTable T, const DevPod* __restrict__ pods,
+                                                        int64_t* __restrict__ cursor_p, int64_t end, int B,
+                                                        int n_ranks, int nt_local,
+                                                        const uint64_t* __restrict__ lists, EvalParams P,
+                                                        uint64_t* __restrict__ out_keys, int bitmap_words,
+                                                        int64_t* __restrict__ round_stats) {
+  extern __shared__ uint32_t bitmap[];
+  const int lane = threadIdx.x;
+  const int64_t cursor = *cursor_p;
+  if (cursor >= end) return;
+  const int nb = (end - cursor) < (int64_t)B ? (int)(end - cursor) : B;
+  for (int w = lane; w < bitmap_words; w += kWave) bitmap[w] = 0;
+  __syncthreads();
+
+  Row mrow;
+  mrow.flags = 0;
+  uint32_t midx = 0xFFFFFFFFu;
+  int nM = 0;
+  int consumed = 0;
+  const int nt_total = n_ranks * nt_local;
+  for (int j = 0; j < nb; ++j) {
+    const DevPod p = pods[cursor + j];
+    uint64_t best = 0, bound = 0;
+    for (int g = lane; g < nt_total; g += kWave) {
+      const int rk = g / nt_local, t = g - rk * nt_local;
+      const uint64_t* L = lists + (((size_t)rk * B + j) * nt_local + t) * kR;
+      uint64_t k[kR];
+#pragma unroll
+      for (int r = 0; r < kR; r += 2) {
+        const ulonglong2 v = *reinterpret_cast<const ulonglong2*>(L + r);
+        k[r] = v.x;
+        k[r + 1] = v.y;
+      }
+      uint64_t bu = 0, mn = ~0ull;
+      int cnt = 0;
+      bool any_unmod = false;
+#pragma unroll
+      for (int r = 0; r < kR; ++r) {
+        if (k[r]) {
+          ++cnt;
+          const uint32_t n = key_node(k[r]);
+          const bool mod = (bitmap[n >> 5] >> (n & 31)) & 1u;
+          if (!mod) {
+            any_unmod = true;
+            bu = k[r] > bu ? k[r] : bu;
+          }
+          mn = k[r] < mn ? k[r] : mn;
+        }
+      }
+      best = bu > best ? bu : best;
+      if (cnt == kR && !any_unmod) bound = mn > bound ? mn : bound;  // tile remainder unknown, keys < mn
+    }
+    if (lane < nM) {
+      int64_t t = 0;
+      if (eval_node(mrow, p, P, t)) {
+        const uint64_t kk = make_key(t, midx);
+        best = kk > best ? kk : best;
+      }
+    }
+    best = wave_max_u64(best);
+    bound = wave_max_u64(bound);
+    if (best < bound || (best == 0 && bound != 0)) break;  // decision not provable from this round's lists
+    if (lane == 0) out_keys[cursor + j] = best;
+    ++consumed;
+    if (best == 0) continue;  // unschedulable: no state change
+    const uint32_t w = key_node(best);
+    const uint64_t hit = __ballot(lane < nM && midx == w);
+    if (hit) {
+      if (lane == (int)__builtin_ctzll(hit)) apply_pod(mrow, p);
+    } else {
+      if (lane == nM) {
+        mrow = load_row(T, w);
+        midx = w;
+        apply_pod(mrow, p);
+      }
+      if (lane == 0) bitmap[w >> 5] |= 1u << (w & 31);
+      ++nM;
+      __syncthreads();
+    }
+  }
+  if (lane < nM) store_mutable(T, midx, mrow);
+  if (lane == 0) {
+    *cursor_p = cursor + consumed;
+    round_stats[0] += 1;
+    round_stats[1] += consumed;
+  }
+}
+
+// kg_pods_evaluate: one pod, every node, per-plugin outputs.
+__global__ void evaluate_pod(DevTable T, const DevPod* __restrict__ pod, int64_t n, EvalParams P,
+                             int32_t* __restrict__ reject, int64_t* __restrict__ fit, int64_t* __restrict__ la) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const Row r = load_row(T, i);
+  int64_t t = 0, fs = 0, ls = 0;
+  uint32_t rej = 0;
+  eval_node(r, *pod, P, t, &rej, &fs, &ls);
+  reject[i] = (int32_t)rej;
+  fit[i] = fs;
+  la[i] = ls;
+}
+
+// Scatter-add of mutable-column deltas (pod add/remove, NodeMetric usage changes).
+struct RowDelta {
+  int64_t idx;
+  int64_t d[9];  // req_cpu, req_mem, nz_cpu, nz_mem, num_pods, la_used_cpu, la_used_mem, la_pused_cpu, la_pused_mem
+};
+__global__ void apply_deltas(DevTable T, const RowDelta* __restrict__ d, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const RowDelta x = d[i];
+  const int64_t k = x.idx;
+  atomicAdd((unsigned long long*)&T.req_cpu[k], (unsigned long long)x.d[0]);
+  atomicAdd((unsigned long long*)&T.req_mem[k], (unsigned long long)x.d[1]);
+  atomicAdd((unsigned long long*)&T.nz_cpu[k], (unsigned long long)x.d[2]);
+  atomicAdd((unsigned long long*)&T.nz_mem[k], (unsigned long long)x.d[3]);
+  atomicAdd(&T.num_pods[k], (int32_t)x.d[4]);
+  atomicAdd((unsigned long long*)&T.la_used_cpu[k], (unsigned long long)x.d[5]);
+  atomicAdd((unsigned long long*)&T.la_used_mem[k], (unsigned long long)x.d[6]);
+  atomicAdd((unsigned long long*)&T.la_pused_cpu[k], (unsigned long long)x.d[7]);
+  atomicAdd((unsigned long long*)&T.la_pused_mem[k], (unsigned long long)x.d[8]);
+}
+
+__global__ void debug_least_requested(const int64_t* req, const int64_t* cap, int64_t* out, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = least_requested(req[i], cap[i]);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Host side
+// ------------------------------------------------------------------------------------------------
+
+template <typename T>
+struct DevBuf {
+  T* p = nullptr;
+  size_t n = 0;
+  int ensure(size_t want) {
+    if (want <= n) return 0;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+    if (hipMalloc(&p, std::max<size_t>(want, 1) * sizeof(T)) != hipSuccess) return fail(KG_E_NOMEM, "hipMalloc %zu", want);
+    n = want;
+    return 0;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+};
+
+int64_t bits_for(int64_t v) {
+  int b = 1;
+  while (b < 32 && (int64_t(1) << b) <= v) ++b;
+  return b;
+}
+
+}  // namespace
+
+struct kg_engine {
+  kg_config cfg;
+  int rank = 0, n_ranks = 1;
+  int device = 0;
+  hipStream_t stream = nullptr;
+  ncclComm_t comm = nullptr;
+  int64_t capacity = 0;
+  int64_t n_nodes = 0;  // highest upserted index + 1
+  EvalParams P{};
+  // host mirror of static / ingest state
+  std::vector<kg_node> nodes;
+  std::vector<kg_node_metric> metrics;
+  std::vector<int64_t> folded_usage;  // NodeUsage currently folded into la_used (2 per node)
+  std::vector<int64_t> now_of;        // metric ingest time per node
+  bool static_dirty = true;
+  // device
+  DevTable T{};
+  DevBuf<int64_t> cols64;
+  DevBuf<int32_t> cols32;
+  DevBuf<DevPod> pods;
+  int64_t n_staged = 0;
+  DevBuf<uint64_t> lists;
+  DevBuf<uint64_t> out_keys;
+  DevBuf<int64_t> cursor;  // [0] cursor, [1] rounds, [2] consumed
+  DevBuf<RowDelta> deltas;
+  DevBuf<int64_t> scratch64;
+  DevBuf<int32_t> scratch32;
+  std::vector<int64_t> h_static64;
+  std::vector<int32_t> h_static32;
+};
+
+namespace {
+
+int validate_config(const kg_config* c) {
+  if (!c) return fail(KG_E_INVALID, "config is NULL");
+  if (c->abi_version != KG_ABI_VERSION) return fail(KG_E_INVALID, "abi_version %lld != %d", (long long)c->abi_version, KG_ABI_VERSION);
+  for (int r = 2; r < KG_RES_MAX; ++r) {
+    if (c->fit_score && c->fit_resource_weights[r] != 0)
+      return fail(KG_E_UNSUPPORTED, "NodeResourcesFit scoring resource slot %d: only cpu/memory are accelerated", r);
+    if (c->la_score && c->la_resource_weights[r] != 0)
+      return fail(KG_E_UNSUPPORTED, "LoadAware resourceWeights slot %d: only cpu/memory are accelerated", r);
+  }
+  for (int r = 0; r < 2; ++r) {
+    if (c->fit_resource_weights[r] < 0 || c->fit_resource_weights[r] > 1000000) return fail(KG_E_INVALID, "fit weight out of range");
+    if (c->la_resource_weights[r] < 0 || c->la_resource_weights[r] > 1000000) return fail(KG_E_INVALID, "loadaware weight out of range");
+  }
+  if ((c->la_score || c->la_filter) && c->la_resource_weights[0] + c->la_resource_weights[1] <= 0)
+    return fail(KG_E_INVALID, "LoadAwareSchedulingArgs.resourceWeights must not be empty");
+  if (c->weight_fit < 0 || c->weight_fit > 1000000 || c->weight_loadaware < 0 || c->weight_loadaware > 1000000)
+    return fail(KG_E_INVALID, "plugin weight out of range");
+  if (c->batch_pods < 0 || c->batch_pods > kMaxB) return fail(KG_E_INVALID, "batch_pods must be in [1,%d]", kMaxB);
+  return 0;
+}
+
+// EstimateNode (estimator/default_estimator.go:110-129)
+int64_t estimate_node(const kg_node& n, int r) {
+  if ((n.flags & KG_NODE_HAS_RAW_ALLOCATABLE) && n.raw_allocatable_present[r]) return n.raw_allocatable[r];
+  return n.allocatable[r];
+}
+
+// isNodeMetricExpired (loadaware/helper.go:36-41)
+bool metric_expired(const kg_node_metric& m, int64_t exp_s, int64_t now) {
+  if (!m.present || !m.has_update_time) return true;
+  return exp_s > 0 && (now - m.update_time_unix_nano) >= exp_s * 1000000000LL;
+}
+
+int64_t milli_of(int r, int64_t v) { return r == KG_RES_CPU ? v : v * 1000; }
+
+// int64(math.Round(float64(used.MilliValue()) / float64(total.MilliValue()) * 100)) (load_aware.go:214,248)
+int64_t usage_percent(int r, int64_t used, int64_t total) {
+  volatile double q = (double)milli_of(r, used) / (double)milli_of(r, total);
+  volatile double pct = q * 100.0;
+  return (int64_t)std::round(pct);
+}
+
+// LoadAware Filter verdict for one node, for a non-prod (prod=false) or prod pod (load_aware.go:123-254).
+// Pod-invariant apart from {prod, daemonset}: Filter ignores estimated/assigned pods (":198 TODO").
+bool la_filter_pass(const kg_config& c, const kg_node& n, const kg_node_metric& m, int64_t now, bool prod) {
+  if (!m.present) return true;
+  if (c.la_filter_expired_node_metrics && c.la_node_metric_expiration_seconds >= 0 &&
+      metric_expired(m, c.la_node_metric_expiration_seconds, now))
+    return true;
+  const bool custom = (n.flags & KG_NODE_HAS_CUSTOM_THRESHOLDS) != 0;
+  int nc = 0, ncp = 0, nprod_args = 0;
+  for (int r = 0; r < KG_RES_MAX; ++r) {
+    nc += custom && n.custom_usage_thresholds[r] >= 0;
+    ncp += custom && n.custom_prod_usage_thresholds[r] >= 0;
+    nprod_args += c.la_prod_usage_thresholds[r] != 0;
+  }
+  auto thr = [&](int r) { return nc > 0 ? std::max<int64_t>(n.custom_usage_thresholds[r], 0) : c.la_usage_thresholds[r]; };
+  auto pthr = [&](int r) { return ncp > 0 ? std::max<int64_t>(n.custom_prod_usage_thresholds[r], 0) : c.la_prod_usage_thresholds[r]; };
+  if (prod && (ncp > 0 ? ncp : nprod_args) > 0) {  // filterProdUsage (load_aware.go:226-254)
+    if (m.pods_metric_count == 0) return true;
+    for (int r = 0; r < KG_RES_MAX; ++r) {
+      const int64_t t = pthr(r);
+      if (t == 0) continue;
+      const int64_t total = estimate_node(n, r);
+      if (total == 0) continue;
+      if (usage_percent(r, m.prod_pods_usage[r], total) >= t) return false;
+    }
+    return true;
+  }
+  if (!m.has_node_metric) return true;  // filterNodeUsage (load_aware.go:173-224)
+  for (int r = 0; r < KG_RES_MAX; ++r) {
+    const int64_t t = thr(r);
+    if (t == 0) continue;
+    const int64_t total = estimate_node(n, r);
+    if (total == 0) continue;
+    const int64_t used = m.node_usage_present[r] ? m.node_usage[r] : 0;
+    if (usage_percent(r, used, total) >= t) return false;
+  }
+  return true;
+}
+
+// TranslateResourceNameByPriorityClass (apis/extension/resource.go:53-58); -1 = "".
+int translate_resource(int64_t prio, int r) {
+  if (prio == KG_PRIO_PROD || prio == KG_PRIO_NONE) return r;
+  if (prio == KG_PRIO_BATCH) return r == KG_RES_CPU ? KG_RES_BATCH_CPU : (r == KG_RES_MEMORY ? KG_RES_BATCH_MEMORY : -1);
+  if (prio == KG_PRIO_MID) return r == KG_RES_CPU ? KG_RES_MID_CPU : (r == KG_RES_MEMORY ? KG_RES_MID_MEMORY : -1);
+  return -1;
+}
+
+// estimatedUsedByResource (estimator/default_estimator.go:73-108)
+int64_t estimate_resource(const kg_pod& p, int real, int64_t factor) {
+  const int64_t limit = real >= 0 ? p.limits[real] : 0;
+  const int64_t request = real >= 0 ? p.requests[real] : 0;
+  int64_t q = request;
+  if (limit > request) {
+    factor = 100;
+    q = limit;
+  }
+  if (q == 0) {
+    if (real == KG_RES_CPU || real == KG_RES_BATCH_CPU) return 250;                 // DefaultMilliCPURequest
+    if (real == KG_RES_MEMORY || real == KG_RES_BATCH_MEMORY) return 200LL << 20;   // DefaultMemoryRequest
+    return 0;
+  }
+  volatile double prod = (double)q * (double)factor;
+  int64_t est = (int64_t)std::round(prod / 100.0);
+  if (limit > 0 && est > limit) est = limit;
+  return est;
+}
+
+// EstimatePod (default_estimator.go:57-70) for the cpu/memory weight keys.
+void estimate_pod(const kg_config& c, const kg_pod& p, int64_t est[2]) {
+  for (int r = 0; r < 2; ++r) {
+    est[r] = 0;
+    if (c.la_resource_weights[r] == 0) continue;
+    est[r] = estimate_resource(p, translate_resource(p.priority_class, r), c.la_estimated_scaling_factors[r]);
+  }
+}
+
+int decode_pod(const kg_engine* e, const kg_pod& p, DevPod& d) {
+  const kg_config& c = e->cfg;
+  bool zero = true;
+  for (int r = 0; r < KG_RES_MAX; ++r) {
+    if (p.requests[r] < 0 || p.limits[r] < 0) return fail(KG_E_INVALID, "negative pod quantity");
+    zero &= p.requests[r] == 0;
+    if (c.fit_filter && r >= 2 && p.requests[r] != 0)
+      return fail(KG_E_UNSUPPORTED, "pod requests resource slot %d; accelerated NodeResourcesFit covers cpu/memory", r);
+  }
+  if (p.priority_class < KG_PRIO_NONE || p.priority_class > KG_PRIO_FREE) return fail(KG_E_INVALID, "priority_class");
+  d.req_cpu = p.requests[KG_RES_CPU];
+  d.req_mem = p.requests[KG_RES_MEMORY];
+  d.nz_cpu = p.nonzero_requests[0];
+  d.nz_mem = p.nonzero_requests[1];
+  int64_t est[2];
+  estimate_pod(c, p, est);
+  d.est_cpu = est[0];
+  d.est_mem = est[1];
+  d.flags = (zero ? P_ZERO_REQ : 0) | ((p.flags & KG_POD_DAEMONSET) ? P_DAEMONSET : 0) |
+            (p.priority_class == KG_PRIO_PROD ? P_PROD : 0) |
+            (p.priority_class == KG_PRIO_PROD && c.la_score_according_prod_usage ? P_LA_PROD_SCORE : 0);
+  d.pad = 0;
+  return 0;
+}
+
+// Static columns (alloc_cpu, alloc_mem, la_alloc_cpu, la_alloc_mem | alloc_pods, flags) from host mirror.
+uint32_t node_flags(const kg_engine* e, int64_t i) {
+  const kg_node& n = e->nodes[i];
+  if (!(n.flags & KG_NODE_VALID)) return 0;
+  const kg_node_metric& m = e->metrics[i];
+  const int64_t now = e->now_of[i];
+  uint32_t f = F_VALID;
+  const kg_config& c = e->cfg;
+  if (m.present && !(c.la_node_metric_expiration_seconds >= 0 && metric_expired(m, c.la_node_metric_expiration_seconds, now)))
+    f |= F_LA_SCORE;
+  if (la_filter_pass(c, n, m, now, false)) f |= F_LA_PASS;
+  if (la_filter_pass(c, n, m, now, true)) f |= F_LA_PASS_PROD;
+  return f;
+}
+
+int sync_static(kg_engine* e) {
+  if (!e->static_dirty) return 0;
+  const int64_t cap = e->capacity;
+  auto& h64 = e->h_static64;
+  auto& h32 = e->h_static32;
+  h64.assign(4 * cap, 0);
+  h32.assign(2 * cap, 0);
+  for (int64_t i = 0; i < e->n_nodes; ++i) {
+    const kg_node& n = e->nodes[i];
+    h64[0 * cap + i] = n.allocatable[KG_RES_CPU];
+    h64[1 * cap + i] = n.allocatable[KG_RES_MEMORY];
+    h64[2 * cap + i] = estimate_node(n, KG_RES_CPU);
+    h64[3 * cap + i] = estimate_node(n, KG_RES_MEMORY);
+    h32[0 * cap + i] = (int32_t)std::min<int64_t>(n.allowed_pods, INT32_MAX);
+    h32[1 * cap + i] = (int32_t)node_flags(e, i);
+  }
+  HIP_TRY(hipMemcpyAsync(e->T.alloc_cpu, &h64[0 * cap], cap * 8, hipMemcpyHostToDevice, e->stream));
+  HIP_TRY(hipMemcpyAsync(e->T.alloc_mem, &h64[1 * cap], cap * 8, hipMemcpyHostToDevice, e->stream));
+  HIP_TRY(hipMemcpyAsync(e->T.la_alloc_cpu, &h64[2 * cap], cap * 8, hipMemcpyHostToDevice, e->stream));
+  HIP_TRY(hipMemcpyAsync(e->T.la_alloc_mem, &h64[3 * cap], cap * 8, hipMemcpyHostToDevice, e->stream));
+  HIP_TRY(hipMemcpyAsync(e->T.alloc_pods, &h32[0 * cap], cap * 4, hipMemcpyHostToDevice, e->stream));
+  HIP_TRY(hipMemcpyAsync(e->T.flags, (uint32_t*)&h32[1 * cap], cap * 4, hipMemcpyHostToDevice, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  e->static_dirty = false;
+  return 0;
+}
+
+int push_deltas(kg_engine* e, const std::vector<RowDelta>& d) {
+  if (d.empty()) return 0;
+  if (int rc = e->deltas.ensure(d.size())) return rc;
+  HIP_TRY(hipMemcpyAsync(e->deltas.p, d.data(), d.size() * sizeof(RowDelta), hipMemcpyHostToDevice, e->stream));
+  const int64_t n = (int64_t)d.size();
+  apply_deltas<<<(unsigned)((n + 255) / 256), 256, 0, e->stream>>>(e->T, e->deltas.p, n);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  return 0;
+}
+
+// NodeUsage folded into la_used (non-prod view): load_aware.go:307-326 with an empty PodsMetric.
+void usage_for_score(const kg_node_metric& m, int64_t u[2]) {
+  for (int r = 0; r < 2; ++r) u[r] = (m.present && m.has_node_metric && m.node_usage_present[r]) ? m.node_usage[r] : 0;
+}
+
+struct RoundGeom {
+  int64_t N, shard, base, n_local;
+  int nt_local, B, ppw, bitmap_words;
+};
+
+RoundGeom geometry(const kg_engine* e) {
+  RoundGeom g;
+  g.N = e->n_nodes;
+  g.shard = (g.N + e->n_ranks - 1) / e->n_ranks;
+  g.base = std::min<int64_t>(g.N, (int64_t)e->rank * g.shard);
+  g.n_local = std::min<int64_t>(g.shard, g.N - g.base);
+  g.nt_local = (int)std::max<int64_t>(1, (g.shard + kTile - 1) / kTile);
+  g.B = (int)(e->cfg.batch_pods > 0 ? e->cfg.batch_pods : 32);
+  g.ppw = (int)(e->cfg.pods_per_wave > 0 ? std::min<int64_t>(e->cfg.pods_per_wave, g.B) : 2);
+  g.bitmap_words = (int)((std::max<int64_t>(g.N, 1) + 31) / 32);
+  return g;
+}
+
+int launch_round(kg_engine* e, const RoundGeom& g, int64_t end) {
+  uint64_t* my_lists = e->lists.p + (size_t)e->rank * g.B * g.nt_local * kR;
+  dim3 grid((g.nt_local + kEvalWaves - 1) / kEvalWaves, (g.B + g.ppw - 1) / g.ppw);
+  eval_round<<<grid, kWave * kEvalWaves, 0, e->stream>>>(e->T, e->pods.p, e->cursor.p, end, g.B, g.ppw, g.base,
+                                                          g.n_local, g.nt_local, e->P, my_lists);
+  HIP_TRY(hipGetLastError());
+  if (e->n_ranks > 1) {
+    const size_t cnt = (size_t)g.B * g.nt_local * kR;
+    NCCL_TRY(ncclAllGather(my_lists, e->lists.p, cnt, ncclUint64, e->comm, e->stream));
+  }
+  resolve_round<<<1, kWave, g.bitmap_words * 4, e->stream>>>(e->T, e->pods.p, e->cursor.p, end, g.B, e->n_ranks,
+                                                              g.nt_local, e->lists.p, e->P, e->out_keys.p,
+                                                              g.bitmap_words, e->cursor.p + 1);
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+int prepare_rounds(kg_engine* e, RoundGeom& g) {
+  if (int rc = sync_static(e)) return rc;
+  g = geometry(e);
+  if (g.N > kMaxNodes) return fail(KG_E_UNSUPPORTED, "n_nodes %lld > %lld", (long long)g.N, (long long)kMaxNodes);
+  if (int rc = e->lists.ensure((size_t)e->n_ranks * g.B * g.nt_local * kR)) return rc;
+  return 0;
+}
+
+double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------------
+// C ABI
+// ------------------------------------------------------------------------------------------------
+extern "C" {
+
+int kg_abi_version(void) { return KG_ABI_VERSION; }
+
+int64_t kg_abi_struct_size(int which) {
+  switch (which) {
+    case 0: return sizeof(kg_config);
+    case 1: return sizeof(kg_node);
+    case 2: return sizeof(kg_node_metric);
+    case 3: return sizeof(kg_pod);
+    case 4: return sizeof(kg_stats);
+  }
+  return -1;
+}
+const char* kg_last_error(void) { return g_err.c_str(); }
+
+void kg_config_default(kg_config* c) {
+  std::memset(c, 0, sizeof(*c));
+  c->abi_version = KG_ABI_VERSION;
+  // v1beta2.SetDefaults_LoadAwareSchedulingArgs (pkg/scheduler/apis/config/v1beta2/defaults.go:76-99, 30-48)
+  c->la_filter_expired_node_metrics = 1;
+  c->la_node_metric_expiration_seconds = 180;
+  c->la_resource_weights[KG_RES_CPU] = 1;
+  c->la_resource_weights[KG_RES_MEMORY] = 1;
+  c->la_usage_thresholds[KG_RES_CPU] = 65;
+  c->la_usage_thresholds[KG_RES_MEMORY] = 95;
+  c->la_estimated_scaling_factors[KG_RES_CPU] = 85;
+  c->la_estimated_scaling_factors[KG_RES_MEMORY] = 70;
+  // upstream NodeResourcesFit default scoring strategy: LeastAllocated, cpu:1 memory:1
+  c->fit_resource_weights[KG_RES_CPU] = 1;
+  c->fit_resource_weights[KG_RES_MEMORY] = 1;
+  c->fit_filter = c->fit_score = c->la_filter = c->la_score = 1;
+  c->weight_fit = 1;
+  c->weight_loadaware = 1;
+  c->batch_pods = 32;
+  c->pods_per_wave = 2;
+  c->device_id = -1;
+}
+
+int kg_nccl_unique_id(void* out128) {
+  if (!out128) return fail(KG_E_INVALID, "out is NULL");
+  ncclUniqueId id;
+  NCCL_TRY(ncclGetUniqueId(&id));
+  static_assert(sizeof(id) == 128, "ncclUniqueId size");
+  std::memcpy(out128, &id, sizeof(id));
+  return 0;
+}
+
+int kg_engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank, int n_ranks, const void* nccl_id,
+                     kg_engine** out) {
+  if (!out) return fail(KG_E_INVALID, "out is NULL");
+  *out = nullptr;
+  if (int rc = validate_config(cfg)) return rc;
+  if (capacity_nodes <= 0 || capacity_nodes > kMaxNodes) return fail(KG_E_INVALID, "capacity_nodes out of range");
+  if (n_ranks < 1 || rank < 0 || rank >= n_ranks) return fail(KG_E_INVALID, "rank/n_ranks");
+  if (n_ranks > 1 && !nccl_id) return fail(KG_E_INVALID, "nccl_unique_id required for n_ranks>1");
+  kg_engine* e = new kg_engine();
+  e->cfg = *cfg;
+  if (e->cfg.batch_pods == 0) e->cfg.batch_pods = 32;
+  e->rank = rank;
+  e->n_ranks = n_ranks;
+  const int64_t cap = ((capacity_nodes + kTile - 1) / kTile) * kTile;
+  e->capacity = cap;
+  auto bail = [&](int rc) {
+    kg_engine_destroy(e);
+    return rc;
+  };
+  if (cfg->device_id >= 0) {
+    if (hipSetDevice((int)cfg->device_id) != hipSuccess) return bail(fail(KG_E_DEVICE, "hipSetDevice(%lld)", (long long)cfg->device_id));
+  }
+  if (hipGetDevice(&e->device) != hipSuccess) return bail(fail(KG_E_DEVICE, "no HIP device"));
+  if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) return bail(fail(KG_E_DEVICE, "hipStreamCreate"));
+  if (int rc = e->cols64.ensure(12 * cap)) return bail(rc);
+  if (int rc = e->cols32.ensure(3 * cap)) return bail(rc);
+  if (hipMemset(e->cols64.p, 0, 12 * cap * 8) != hipSuccess || hipMemset(e->cols32.p, 0, 3 * cap * 4) != hipSuccess)
+    return bail(fail(KG_E_DEVICE, "hipMemset"));
+  int64_t* c64 = e->cols64.p;
+  e->T.alloc_cpu = c64 + 0 * cap;
+  e->T.alloc_mem = c64 + 1 * cap;
+  e->T.req_cpu = c64 + 2 * cap;
+  e->T.req_mem = c64 + 3 * cap;
+  e->T.nz_cpu = c64 + 4 * cap;
+  e->T.nz_mem = c64 + 5 * cap;
+  e->T.la_alloc_cpu = c64 + 6 * cap;
+  e->T.la_alloc_mem = c64 + 7 * cap;
+  e->T.la_used_cpu = c64 + 8 * cap;
+  e->T.la_used_mem = c64 + 9 * cap;
+  e->T.la_pused_cpu = c64 + 10 * cap;
+  e->T.la_pused_mem = c64 + 11 * cap;
+  e->T.alloc_pods = e->cols32.p + 0 * cap;
+  e->T.num_pods = e->cols32.p + 1 * cap;
+  e->T.flags = (uint32_t*)(e->cols32.p + 2 * cap);
+  if (int rc = e->cursor.ensure(4)) return bail(rc);
+  if (hipMemset(e->cursor.p, 0, 4 * 8) != hipSuccess) return bail(fail(KG_E_DEVICE, "hipMemset"));
+  e->nodes.assign(cap, kg_node{});
+  e->metrics.assign(cap, kg_node_metric{});
+  e->folded_usage.assign(2 * cap, 0);
+  e->now_of.assign(cap, 0);
+  // EvalParams
+  const kg_config& c = e->cfg;
+  e->P.fit_w_cpu = c.fit_resource_weights[KG_RES_CPU];
+  e->P.fit_w_mem = c.fit_resource_weights[KG_RES_MEMORY];
+  e->P.la_w_cpu = c.la_resource_weights[KG_RES_CPU];
+  e->P.la_w_mem = c.la_resource_weights[KG_RES_MEMORY];
+  e->P.la_wsum = std::max<int64_t>(1, e->P.la_w_cpu + e->P.la_w_mem);
+  e->P.weight_fit = c.weight_fit;
+  e->P.weight_la = c.weight_loadaware;
+  e->P.fit_filter = (int)(c.fit_filter != 0);
+  e->P.fit_score = (int)(c.fit_score != 0);
+  e->P.la_filter = (int)(c.la_filter != 0);
+  e->P.la_score = (int)(c.la_score != 0);
+  const int64_t max_total = 100 * ((c.fit_score ? c.weight_fit : 0) + (c.la_score ? c.weight_loadaware : 0));
+  e->P.score_bits = (int32_t)bits_for(max_total);
+  if (hipFuncSetAttribute((const void*)resolve_round, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)(kMaxNodes / 8)) != hipSuccess)
+    return bail(fail(KG_E_DEVICE, "hipFuncSetAttribute(resolve_round LDS)"));
+  if (n_ranks > 1) {
+    ncclUniqueId id;
+    std::memcpy(&id, nccl_id, sizeof(id));
+    if (ncclCommInitRank(&e->comm, n_ranks, id, rank) != ncclSuccess) return bail(fail(KG_E_COLLECTIVE, "ncclCommInitRank"));
+  }
+  *out = e;
+  return 0;
+}
+
+void kg_engine_destroy(kg_engine* e) {
+  if (!e) return;
+  if (e->stream) (void)hipStreamSynchronize(e->stream);
+  if (e->comm) ncclCommDestroy(e->comm);
+  e->cols64.release();
+  e->cols32.release();
+  e->pods.release();
+  e->lists.release();
+  e->out_keys.release();
+  e->cursor.release();
+  e->deltas.release();
+  e->scratch64.release();
+  e->scratch32.release();
+  if (e->stream) (void)hipStreamDestroy(e->stream);
+  delete e;
+}
+
+int64_t kg_engine_num_nodes(const kg_engine* e) { return e ? e->n_nodes : 0; }
+
+int kg_nodes_upsert(kg_engine* e, const kg_node* nodes, const int32_t* idx, int64_t n) {
+  if (!e || (n > 0 && (!nodes || !idx))) return fail(KG_E_INVALID, "null argument");
+  for (int64_t k = 0; k < n; ++k) {
+    const int64_t i = idx[k];
+    if (i < 0 || i >= e->capacity) return fail(KG_E_INVALID, "node index %lld outside capacity", (long long)i);
+    for (int r = 0; r < KG_RES_MAX; ++r)
+      if (nodes[k].allocatable[r] < 0 || nodes[k].allocatable[r] > (int64_t(1) << 56))
+        return fail(KG_E_INVALID, "allocatable out of range");
+  }
+  for (int64_t k = 0; k < n; ++k) {
+    const int64_t i = idx[k];
+    e->nodes[i] = nodes[k];
+    e->n_nodes = std::max<int64_t>(e->n_nodes, i + 1);
+  }
+  e->static_dirty = true;
+  return 0;
+}
+
+int kg_nodes_delete(kg_engine* e, const int32_t* idx, int64_t n) {
+  if (!e || (n > 0 && !idx)) return fail(KG_E_INVALID, "null argument");
+  for (int64_t k = 0; k < n; ++k) {
+    if (idx[k] < 0 || idx[k] >= e->capacity) return fail(KG_E_INVALID, "node index");
+    e->nodes[idx[k]].flags &= ~(int64_t)KG_NODE_VALID;
+  }
+  e->static_dirty = true;
+  return 0;
+}
+
+int kg_node_metrics_update(kg_engine* e, const kg_node_metric* m, const int32_t* idx, int64_t n, int64_t now) {
+  if (!e || (n > 0 && (!m || !idx))) return fail(KG_E_INVALID, "null argument");
+  for (int64_t k = 0; k < n; ++k) {
+    if (idx[k] < 0 || idx[k] >= e->capacity) return fail(KG_E_INVALID, "node index");
+    if (e->cfg.la_score && m[k].present && m[k].pods_metric_count != 0)
+      return fail(KG_E_UNSUPPORTED, "PodsMetric-based LoadAware scoring is not accelerated (node %d)", idx[k]);
+  }
+  std::vector<RowDelta> d;
+  d.reserve(n);
+  for (int64_t k = 0; k < n; ++k) {
+    const int64_t i = idx[k];
+    int64_t u[2];
+    usage_for_score(m[k], u);
+    RowDelta x{};
+    x.idx = i;
+    x.d[5] = u[0] - e->folded_usage[2 * i];
+    x.d[6] = u[1] - e->folded_usage[2 * i + 1];
+    e->folded_usage[2 * i] = u[0];
+    e->folded_usage[2 * i + 1] = u[1];
+    e->metrics[i] = m[k];
+    e->now_of[i] = now;
+    if (x.d[5] || x.d[6]) d.push_back(x);
+  }
+  e->static_dirty = true;
+  return push_deltas(e, d);
+}
+
+static int pods_delta(kg_engine* e, const kg_pod* pods, const int32_t* node_idx, int64_t n, int sign) {
+  if (!e || (n > 0 && (!pods || !node_idx))) return fail(KG_E_INVALID, "null argument");
+  std::vector<RowDelta> d(n);
+  for (int64_t k = 0; k < n; ++k) {
+    const int64_t i = node_idx[k];
+    if (i < 0 || i >= e->capacity) return fail(KG_E_INVALID, "node index %lld", (long long)i);
+    DevPod p;
+    if (int rc = decode_pod(e, pods[k], p)) return rc;
+    RowDelta& x = d[k];
+    x.idx = i;
+    x.d[0] = sign * p.req_cpu;
+    x.d[1] = sign * p.req_mem;
+    x.d[2] = sign * p.nz_cpu;
+    x.d[3] = sign * p.nz_mem;
+    x.d[4] = sign;
+    x.d[5] = sign * p.est_cpu;
+    x.d[6] = sign * p.est_mem;
+    x.d[7] = (p.flags & P_PROD) ? sign * p.est_cpu : 0;
+    x.d[8] = (p.flags & P_PROD) ? sign * p.est_mem : 0;
+  }
+  return push_deltas(e, d);
+}
+
+int kg_pods_add(kg_engine* e, const kg_pod* pods, const int32_t* node_idx, int64_t n) {
+  return pods_delta(e, pods, node_idx, n, +1);
+}
+int kg_pods_remove(kg_engine* e, const kg_pod* pods, const int32_t* node_idx, int64_t n) {
+  return pods_delta(e, pods, node_idx, n, -1);
+}
+
+int kg_pods_stage(kg_engine* e, const kg_pod* pods, int64_t n) {
+  if (!e || (n > 0 && !pods)) return fail(KG_E_INVALID, "null argument");
+  std::vector<DevPod> h(std::max<int64_t>(n, 1));
+  for (int64_t k = 0; k < n; ++k)
+    if (int rc = decode_pod(e, pods[k], h[k])) return rc;
+  if (int rc = e->pods.ensure(n + kMaxB)) return rc;
+  if (int rc = e->out_keys.ensure(n + kMaxB)) return rc;
+  if (n > 0) HIP_TRY(hipMemcpyAsync(e->pods.p, h.data(), n * sizeof(DevPod), hipMemcpyHostToDevice, e->stream));
+  HIP_TRY(hipMemsetAsync(e->out_keys.p, 0, (n + kMaxB) * 8, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  e->n_staged = n;
+  return 0;
+}
+
+int kg_pods_schedule_staged(kg_engine* e, int64_t first, int64_t count, kg_stats* stats) {
+  if (!e) return fail(KG_E_INVALID, "engine is NULL");
+  if (first < 0 || count < 0 || first + count > e->n_staged) return fail(KG_E_INVALID, "staged range");
+  const double t0 = now_s();
+  RoundGeom g;
+  if (int rc = prepare_rounds(e, g)) return rc;
+  const int64_t end = first + count;
+  const int64_t init[3] = {first, 0, 0};
+  int64_t host_stats[3] = {first, 0, 0};
+  HIP_TRY(hipMemcpyAsync(e->cursor.p, init, 3 * 8, hipMemcpyHostToDevice, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  int64_t cur = first;
+  int64_t launched = 0;
+  double avg = g.B;  // pods resolved per round, refined from the device counters
+  while (cur < end) {
+    const int64_t remaining = end - cur;
+    int64_t rounds = (int64_t)std::ceil(remaining / std::max(1.0, avg));
+    rounds = std::max<int64_t>(rounds, 1);
+    for (int64_t r = 0; r < rounds; ++r)
+      if (int rc = launch_round(e, g, end)) return rc;
+    launched += rounds;
+    HIP_TRY(hipMemcpyAsync(host_stats, e->cursor.p, 3 * 8, hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    cur = host_stats[0];
+    if (host_stats[1] > 0) avg = std::max(1.0, (double)host_stats[2] / (double)host_stats[1]);
+  }
+  if (stats) {
+    std::memset(stats, 0, sizeof(*stats));
+    stats->device_batches = host_stats[1];
+    stats->node_evaluations = count * g.N;
+    stats->seconds = now_s() - t0;
+  }
+  (void)launched;
+  return 0;
+}
+
+int kg_results_fetch(kg_engine* e, int64_t first, int64_t count, int32_t* out_node, int64_t* out_score) {
+  if (!e) return fail(KG_E_INVALID, "engine is NULL");
+  if (first < 0 || count < 0 || first + count > e->n_staged) return fail(KG_E_INVALID, "staged range");
+  std::vector<uint64_t> keys(std::max<int64_t>(count, 1));
+  if (count > 0) {
+    HIP_TRY(hipMemcpyAsync(keys.data(), e->out_keys.p + first, count * 8, hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+  }
+  for (int64_t i = 0; i < count; ++i) {
+    const uint64_t k = keys[i];
+    if (out_node) out_node[i] = k ? (int32_t)(0xFFFFFFFFu - (uint32_t)k) : -1;
+    if (out_score) out_score[i] = k ? (int64_t)(k >> 32) : 0;
+  }
+  return 0;
+}
+
+int kg_pods_schedule(kg_engine* e, const kg_pod* pods, int64_t n, int32_t* out_node, int64_t* out_score,
+                     kg_stats* stats) {
+  const double t0 = now_s();
+  if (int rc = kg_pods_stage(e, pods, n)) return rc;
+  if (int rc = kg_pods_schedule_staged(e, 0, n, stats)) return rc;
+  if (int rc = kg_results_fetch(e, 0, n, out_node, out_score)) return rc;
+  if (stats) {
+    stats->seconds = now_s() - t0;
+    for (int64_t i = 0; i < n; ++i) (out_node && out_node[i] >= 0) ? ++stats->pods_scheduled : ++stats->pods_unschedulable;
+  }
+  return 0;
+}
+
+int kg_pods_evaluate(kg_engine* e, const kg_pod* pod, int32_t* out_reject, int64_t* out_fit, int64_t* out_la) {
+  if (!e || !pod) return fail(KG_E_INVALID, "null argument");
+  if (int rc = sync_static(e)) return rc;
+  DevPod d;
+  if (int rc = decode_pod(e, *pod, d)) return rc;
+  const int64_t n = e->n_nodes;
+  if (n == 0) return 0;
+  if (int rc = e->scratch64.ensure(2 * n + 8)) return rc;
+  if (int rc = e->scratch32.ensure(n)) return rc;
+  DevPod* dp = reinterpret_cast<DevPod*>(e->scratch64.p + 2 * n);  // 56 B fits in the 8 spare int64s
+  HIP_TRY(hipMemcpyAsync(dp, &d, sizeof(d), hipMemcpyHostToDevice, e->stream));
+  evaluate_pod<<<(unsigned)((n + 255) / 256), 256, 0, e->stream>>>(e->T, dp, n, e->P, e->scratch32.p, e->scratch64.p,
+                                                                   e->scratch64.p + n);
+  HIP_TRY(hipGetLastError());
+  std::vector<int32_t> rej(n);
+  std::vector<int64_t> fs(n), ls(n);
+  HIP_TRY(hipMemcpyAsync(rej.data(), e->scratch32.p, n * 4, hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipMemcpyAsync(fs.data(), e->scratch64.p, n * 8, hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipMemcpyAsync(ls.data(), e->scratch64.p + n, n * 8, hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  // reject bits are only reported for enabled Filter plugins (eval_node checks P.*_filter)
+  if (out_reject) std::memcpy(out_reject, rej.data(), n * 4);
+  if (out_fit) std::memcpy(out_fit, fs.data(), n * 8);
+  if (out_la) std::memcpy(out_la, ls.data(), n * 8);
+  return 0;
+}
+
+int kg_nodes_read_state(kg_engine* e, int64_t* req_cpu, int64_t* req_mem, int64_t* nz_cpu, int64_t* nz_mem,
+                        int64_t* num_pods, int64_t* la_est_cpu, int64_t* la_est_mem, int64_t* la_pcpu,
+                        int64_t* la_pmem) {
+  if (!e) return fail(KG_E_INVALID, "engine is NULL");
+  const int64_t n = e->n_nodes;
+  if (n == 0) return 0;
+  auto get64 = [&](int64_t* dst, const int64_t* src) -> int {
+    if (dst) HIP_TRY(hipMemcpyAsync(dst, src, n * 8, hipMemcpyDeviceToHost, e->stream));
+    return 0;
+  };
+  if (int rc = get64(req_cpu, e->T.req_cpu)) return rc;
+  if (int rc = get64(req_mem, e->T.req_mem)) return rc;
+  if (int rc = get64(nz_cpu, e->T.nz_cpu)) return rc;
+  if (int rc = get64(nz_mem, e->T.nz_mem)) return rc;
+  if (int rc = get64(la_est_cpu, e->T.la_used_cpu)) return rc;
+  if (int rc = get64(la_est_mem, e->T.la_used_mem)) return rc;
+  if (int rc = get64(la_pcpu, e->T.la_pused_cpu)) return rc;
+  if (int rc = get64(la_pmem, e->T.la_pused_mem)) return rc;
+  std::vector<int32_t> np(n);
+  HIP_TRY(hipMemcpyAsync(np.data(), e->T.num_pods, n * 4, hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  if (num_pods)
+    for (int64_t i = 0; i < n; ++i) num_pods[i] = np[i];
+  // la_used folds NodeUsage in; report Σ estimates only
+  for (int64_t i = 0; i < n; ++i) {
+    if (la_est_cpu) la_est_cpu[i] -= e->folded_usage[2 * i];
+    if (la_est_mem) la_est_mem[i] -= e->folded_usage[2 * i + 1];
+  }
+  return 0;
+}
+
+int kg_bench_kernel(kg_engine* e, int which, int iters, double* avg_ms, double* algo_bytes) {
+  if (!e || iters <= 0) return fail(KG_E_INVALID, "bad argument");
+  if (e->n_staged <= 0) return fail(KG_E_INVALID, "stage a pod queue first");
+  RoundGeom g;
+  if (int rc = prepare_rounds(e, g)) return rc;
+  const int64_t end = std::min<int64_t>(e->n_staged, g.B);
+  // snapshot mutable columns so that replays of the resolver leave the table unchanged
+  const size_t bytes64 = (size_t)e->capacity * 8;
+  DevBuf<int64_t> save;
+  if (int rc = save.ensure(9 * e->capacity)) return rc;
+  int64_t* mut64[8] = {e->T.req_cpu, e->T.req_mem, e->T.nz_cpu, e->T.nz_mem,
+                       e->T.la_used_cpu, e->T.la_used_mem, e->T.la_pused_cpu, e->T.la_pused_mem};
+  for (int k = 0; k < 8; ++k)
+    HIP_TRY(hipMemcpyAsync(save.p + k * e->capacity, mut64[k], bytes64, hipMemcpyDeviceToDevice, e->stream));
+  HIP_TRY(hipMemcpyAsync(save.p + 8 * e->capacity, e->T.num_pods, e->capacity * 4, hipMemcpyDeviceToDevice, e->stream));
+  int64_t zero3[3] = {0, 0, 0};
+  HIP_TRY(hipMemcpyAsync(e->cursor.p, zero3, 24, hipMemcpyHostToDevice, e->stream));
+  // one real round so the lists are valid for the resolver replay, then undo its write-back
+  if (int rc = launch_round(e, g, end)) return rc;
+  for (int k = 0; k < 8; ++k)
+    HIP_TRY(hipMemcpyAsync(mut64[k], save.p + k * e->capacity, bytes64, hipMemcpyDeviceToDevice, e->stream));
+  HIP_TRY(hipMemcpyAsync(e->T.num_pods, save.p + 8 * e->capacity, e->capacity * 4, hipMemcpyDeviceToDevice, e->stream));
+  HIP_TRY(hipMemcpyAsync(e->cursor.p, zero3, 24, hipMemcpyHostToDevice, e->stream));
+  hipEvent_t a, b;
+  HIP_TRY(hipEventCreate(&a));
+  HIP_TRY(hipEventCreate(&b));
+  uint64_t* my_lists = e->lists.p + (size_t)e->rank * g.B * g.nt_local * kR;
+  dim3 grid((g.nt_local + kEvalWaves - 1) / kEvalWaves, (g.B + g.ppw - 1) / g.ppw);
+  float total_ms = 0.f;
+  for (int it = 0; it < iters; ++it) {
+    HIP_TRY(hipMemcpyAsync(e->cursor.p, zero3, 24, hipMemcpyHostToDevice, e->stream));
+    HIP_TRY(hipEventRecord(a, e->stream));
+    if (which == 0) {
+      eval_round<<<grid, kWave * kEvalWaves, 0, e->stream>>>(e->T, e->pods.p, e->cursor.p, end, g.B, g.ppw, g.base,
+                                                              g.n_local, g.nt_local, e->P, my_lists);
+    } else {
+      resolve_round<<<1, kWave, g.bitmap_words * 4, e->stream>>>(e->T, e->pods.p, e->cursor.p, end, g.B, e->n_ranks,
+                                                                  g.nt_local, e->lists.p, e->P, e->out_keys.p,
+                                                                  g.bitmap_words, e->cursor.p + 1);
+    }
+    HIP_TRY(hipEventRecord(b, e->stream));
+    HIP_TRY(hipEventSynchronize(b));
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, a, b));
+    total_ms += ms;
+    if (which == 1) {  // undo the resolver's write-back
+      for (int k = 0; k < 8; ++k)
+        HIP_TRY(hipMemcpyAsync(mut64[k], save.p + k * e->capacity, bytes64, hipMemcpyDeviceToDevice, e->stream));
+      HIP_TRY(hipMemcpyAsync(e->T.num_pods, save.p + 8 * e->capacity, e->capacity * 4, hipMemcpyDeviceToDevice, e->stream));
+    }
+  }
+  for (int k = 0; k < 8; ++k)
+    HIP_TRY(hipMemcpyAsync(mut64[k], save.p + k * e->capacity, bytes64, hipMemcpyDeviceToDevice, e->stream));
+  HIP_TRY(hipMemcpyAsync(e->T.num_pods, save.p + 8 * e->capacity, e->capacity * 4, hipMemcpyDeviceToDevice, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  (void)hipEventDestroy(a);
+  (void)hipEventDestroy(b);
+  save.release();
+  const int nb = (int)end;
+  if (avg_ms) *avg_ms = total_ms / iters;
+  if (algo_bytes) {
+    // eval: node columns read once per pod group (92 B/node: Fit 56 + LoadAware 32 + flags 4) + lists written;
+    // resolve: every rank's lists read once per pod + pod descriptors.
+    const double groups = std::ceil((double)nb / g.ppw);
+    const double list_bytes = (double)nb * g.nt_local * e->n_ranks * kR * 8;
+    if (which == 0) *algo_bytes = groups * (double)g.n_local * 92.0 + (double)nb * g.nt_local * kR * 8 + nb * 56.0;
+    else *algo_bytes = list_bytes + nb * 56.0;
+  }
+  return 0;
+}
+
+int kg_debug_least_requested(kg_engine* e, const int64_t* req, const int64_t* cap, int64_t* out, int64_t n) {
+  if (!e || n < 0 || (n > 0 && (!req || !cap || !out))) return fail(KG_E_INVALID, "bad argument");
+  if (n == 0) return 0;
+  DevBuf<int64_t> b;
+  if (int rc = b.ensure(3 * n)) return rc;
+  HIP_TRY(hipMemcpyAsync(b.p, req, n * 8, hipMemcpyHostToDevice, e->stream));
+  HIP_TRY(hipMemcpyAsync(b.p + n, cap, n * 8, hipMemcpyHostToDevice, e->stream));
+  debug_least_requested<<<(unsigned)((n + 255) / 256), 256, 0, e->stream>>>(b.p, b.p + n, b.p + 2 * n, n);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(out, b.p + 2 * n, n * 8, hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  b.release();
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,155 @@
+"""Python handle over the koordgpu C ABI (the same entry points a cgo binding would call)."""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import abi
+from .abi import check, ptr
+
+
+def default_config() -> np.ndarray:
+    """kg_config_default: v1beta2 LoadAwareSchedulingArgs defaults + NodeResourcesFit LeastAllocated cpu/mem."""
+    lib = abi.load_library()
+    cfg = np.zeros(1, dtype=abi.CONFIG_DTYPE)
+    lib.kg_config_default(ptr(cfg))
+    return cfg
+
+
+def nccl_unique_id() -> bytes:
+    """ncclGetUniqueId on this rank (rank 0 creates it; the caller broadcasts the 128 bytes)."""
+    lib = abi.load_library()
+    buf = ctypes.create_string_buffer(128)
+    check(lib, lib.kg_nccl_unique_id(ctypes.cast(buf, ctypes.c_void_p)))
+    return buf.raw
+
+
+class Engine:
+    """One engine = one rank's GPU-resident node table (replicated) + its evaluation shard."""
+
+    def __init__(self, config: np.ndarray, capacity: int, rank: int = 0, n_ranks: int = 1,
+                 nccl_id: bytes | None = None):
+        self.lib = abi.load_library()
+        self._cfg = np.array(config, dtype=abi.CONFIG_DTYPE).reshape(1)
+        h = ctypes.c_void_p()
+        idbuf = None
+        if nccl_id is not None:
+            idbuf = ctypes.create_string_buffer(bytes(nccl_id), 128)
+        check(self.lib, self.lib.kg_engine_create(ptr(self._cfg), int(capacity), int(rank), int(n_ranks),
+                                                  ctypes.cast(idbuf, ctypes.c_void_p) if idbuf else None,
+                                                  ctypes.byref(h)))
+        self.h = h
+        self.capacity = capacity
+
+    # -- lifecycle -------------------------------------------------------------------------------------
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.kg_engine_destroy(self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- informer-style deltas ------------------------------------------------------------------------
+    @staticmethod
+    def _idx(idx, n):
+        if idx is None:
+            idx = np.arange(n, dtype=np.int32)
+        return np.ascontiguousarray(idx, dtype=np.int32)
+
+    def upsert_nodes(self, nodes: np.ndarray, idx=None):
+        nodes = np.ascontiguousarray(nodes, dtype=abi.NODE_DTYPE)
+        idx = self._idx(idx, len(nodes))
+        check(self.lib, self.lib.kg_nodes_upsert(self.h, ptr(nodes), ptr(idx), len(nodes)))
+
+    def delete_nodes(self, idx):
+        idx = np.ascontiguousarray(idx, dtype=np.int32)
+        check(self.lib, self.lib.kg_nodes_delete(self.h, ptr(idx), len(idx)))
+
+    def update_metrics(self, metrics: np.ndarray, now_ns: int, idx=None):
+        metrics = np.ascontiguousarray(metrics, dtype=abi.METRIC_DTYPE)
+        idx = self._idx(idx, len(metrics))
+        check(self.lib, self.lib.kg_node_metrics_update(self.h, ptr(metrics), ptr(idx), len(metrics), int(now_ns)))
+
+    def add_pods(self, pods: np.ndarray, node_idx):
+        pods = np.ascontiguousarray(pods, dtype=abi.POD_DTYPE)
+        node_idx = np.ascontiguousarray(node_idx, dtype=np.int32)
+        check(self.lib, self.lib.kg_pods_add(self.h, ptr(pods), ptr(node_idx), len(pods)))
+
+    def remove_pods(self, pods: np.ndarray, node_idx):
+        pods = np.ascontiguousarray(pods, dtype=abi.POD_DTYPE)
+        node_idx = np.ascontiguousarray(node_idx, dtype=np.int32)
+        check(self.lib, self.lib.kg_pods_remove(self.h, ptr(pods), ptr(node_idx), len(pods)))
+
+    # -- hot path -----------------------------------------------------------------------------------------
+    def schedule(self, pods: np.ndarray):
+        """Sequential FIFO scheduling with assume; returns (node_idx[-1 = unschedulable], total_score, stats)."""
+        pods = np.ascontiguousarray(pods, dtype=abi.POD_DTYPE)
+        n = len(pods)
+        out_node = np.empty(n, dtype=np.int32)
+        out_score = np.empty(n, dtype=np.int64)
+        stats = np.zeros(1, dtype=abi.STATS_DTYPE)
+        check(self.lib, self.lib.kg_pods_schedule(self.h, ptr(pods), n, ptr(out_node), ptr(out_score), ptr(stats)))
+        return out_node, out_score, stats[0]
+
+    def stage(self, pods: np.ndarray):
+        pods = np.ascontiguousarray(pods, dtype=abi.POD_DTYPE)
+        check(self.lib, self.lib.kg_pods_stage(self.h, ptr(pods), len(pods)))
+
+    def schedule_staged(self, first: int, count: int):
+        stats = np.zeros(1, dtype=abi.STATS_DTYPE)
+        check(self.lib, self.lib.kg_pods_schedule_staged(self.h, int(first), int(count), ptr(stats)))
+        return stats[0]
+
+    def fetch(self, first: int, count: int):
+        out_node = np.empty(count, dtype=np.int32)
+        out_score = np.empty(count, dtype=np.int64)
+        check(self.lib, self.lib.kg_results_fetch(self.h, int(first), int(count), ptr(out_node), ptr(out_score)))
+        return out_node, out_score
+
+    def evaluate(self, pod: np.ndarray):
+        """Per-node reject bits, NodeResourcesFit score, LoadAwareScheduling score for one pod (no assume)."""
+        pod = np.ascontiguousarray(np.asarray(pod, dtype=abi.POD_DTYPE).reshape(1))
+        n = self.num_nodes
+        rej = np.zeros(n, dtype=np.int32)
+        fit = np.zeros(n, dtype=np.int64)
+        la = np.zeros(n, dtype=np.int64)
+        check(self.lib, self.lib.kg_pods_evaluate(self.h, ptr(pod), ptr(rej), ptr(fit), ptr(la)))
+        return rej, fit, la
+
+    # -- introspection -----------------------------------------------------------------------------------
+    @property
+    def num_nodes(self) -> int:
+        return int(self.lib.kg_engine_num_nodes(self.h))
+
+    def read_state(self) -> dict:
+        n = self.num_nodes
+        names = ("requested_cpu", "requested_mem", "nonzero_cpu", "nonzero_mem", "num_pods",
+                 "la_est_cpu", "la_est_mem", "la_est_prod_cpu", "la_est_prod_mem")
+        out = {k: np.zeros(n, dtype=np.int64) for k in names}
+        check(self.lib, self.lib.kg_nodes_read_state(self.h, *[ptr(out[k]) for k in names]))
+        return out
+
+    def bench_kernel(self, which: int, iters: int):
+        ms = ctypes.c_double()
+        by = ctypes.c_double()
+        check(self.lib, self.lib.kg_bench_kernel(self.h, int(which), int(iters), ctypes.byref(ms), ctypes.byref(by)))
+        return ms.value, by.value
+
+    def debug_least_requested(self, requested, capacity):
+        requested = np.ascontiguousarray(requested, dtype=np.int64)
+        capacity = np.ascontiguousarray(capacity, dtype=np.int64)
+        out = np.zeros(len(requested), dtype=np.int64)
+        check(self.lib, self.lib.kg_debug_least_requested(self.h, ptr(requested), ptr(capacity), ptr(out),
+                                                          len(requested)))
+        return out

@@ -1,0 +1,206 @@
+"""Host-side mirror of the reference's plugin surface for the accelerated path.
+
+The reference's Go host (koord-scheduler) cannot run here (no Go toolchain); this module is the host layer
+above the C ABI with the reference's names and argument meanings, so tests read like the reference's own:
+
+* ``LoadAwareSchedulingArgs`` — pkg/scheduler/apis/config/types.go:30-76, defaults v1beta2/defaults.go:76-99.
+* ``NodeResourcesFitArgs`` — upstream NodeResourcesFitArgs, scoringStrategy LeastAllocated.
+* ``Profile`` — the score plugin set + weights of a KubeSchedulerConfiguration profile
+  (config/manager/scheduler-config.yaml:82-91).
+* ``make_node / make_node_metric / make_pod`` — what the Go shim decodes from corev1.Node, NodeMetric and
+  corev1.Pod (allocatable, raw-allocatable and custom-usage-threshold annotations, PodRequestsAndLimits,
+  GetPodPriorityClassWithDefault).
+* ``Scheduler`` — SchedulePod for a FIFO queue (frameworkext SchedulePod interception,
+  framework_extender_factory.go:136-185), RunFilterPlugins / RunScorePlugins for one pod
+  (framework_extender.go:204-258), Reserve/Unreserve (kg_pods_add / kg_pods_remove).
+Status codes mirror framework.Code: Success, Unschedulable.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import abi
+from .engine import Engine
+from .quantity import resource_value
+
+SUCCESS, UNSCHEDULABLE = "Success", "Unschedulable"
+NODE_RESOURCES_FIT, LOAD_AWARE = "NodeResourcesFit", "LoadAwareScheduling"
+
+
+def _slots(d: dict | None, absent=0) -> np.ndarray:
+    out = np.full(abi.RES_MAX, absent, dtype=np.int64)
+    for k, v in (d or {}).items():
+        out[abi.RESOURCE_SLOTS[k]] = int(v)
+    return out
+
+
+@dataclass
+class LoadAwareSchedulingArgs:
+    filter_expired_node_metrics: bool = True
+    node_metric_expiration_seconds: int | None = 180
+    resource_weights: dict = field(default_factory=lambda: {"cpu": 1, "memory": 1})
+    usage_thresholds: dict = field(default_factory=lambda: {"cpu": 65, "memory": 95})
+    prod_usage_thresholds: dict = field(default_factory=dict)
+    score_according_prod_usage: bool = False
+    estimated_scaling_factors: dict = field(default_factory=lambda: {"cpu": 85, "memory": 70})
+
+
+@dataclass
+class NodeResourcesFitArgs:
+    scoring_resources: dict = field(default_factory=lambda: {"cpu": 1, "memory": 1})
+
+
+@dataclass
+class Profile:
+    filter: tuple = (NODE_RESOURCES_FIT, LOAD_AWARE)
+    score: dict = field(default_factory=lambda: {NODE_RESOURCES_FIT: 1, LOAD_AWARE: 1})
+
+
+def build_config(la: LoadAwareSchedulingArgs | None = None, fit: NodeResourcesFitArgs | None = None,
+                 profile: Profile | None = None, batch_pods: int = 32, pods_per_wave: int = 2,
+                 device_id: int = -1) -> np.ndarray:
+    la = la or LoadAwareSchedulingArgs()
+    fit = fit or NodeResourcesFitArgs()
+    profile = profile or Profile()
+    c = np.zeros(1, dtype=abi.CONFIG_DTYPE)
+    r = c[0]
+    r["abi_version"] = abi.ABI_VERSION
+    r["la_filter_expired_node_metrics"] = int(la.filter_expired_node_metrics)
+    r["la_node_metric_expiration_seconds"] = -1 if la.node_metric_expiration_seconds is None else la.node_metric_expiration_seconds
+    r["la_resource_weights"] = _slots(la.resource_weights)
+    r["la_usage_thresholds"] = _slots(la.usage_thresholds)
+    r["la_prod_usage_thresholds"] = _slots(la.prod_usage_thresholds)
+    r["la_estimated_scaling_factors"] = _slots(la.estimated_scaling_factors)
+    r["la_score_according_prod_usage"] = int(la.score_according_prod_usage)
+    r["fit_resource_weights"] = _slots(fit.scoring_resources)
+    r["fit_filter"] = int(NODE_RESOURCES_FIT in profile.filter)
+    r["la_filter"] = int(LOAD_AWARE in profile.filter)
+    r["fit_score"] = int(NODE_RESOURCES_FIT in profile.score)
+    r["la_score"] = int(LOAD_AWARE in profile.score)
+    r["weight_fit"] = int(profile.score.get(NODE_RESOURCES_FIT, 0))
+    r["weight_loadaware"] = int(profile.score.get(LOAD_AWARE, 0))
+    r["batch_pods"] = batch_pods
+    r["pods_per_wave"] = pods_per_wave
+    r["device_id"] = device_id
+    return c
+
+
+def _values(resources: dict | None) -> np.ndarray:
+    out = np.zeros(abi.RES_MAX, dtype=np.int64)
+    for k, v in (resources or {}).items():
+        out[abi.RESOURCE_SLOTS[k]] = resource_value(k, v)
+    return out
+
+
+def make_node(allocatable: dict, allowed_pods: int = 110, raw_allocatable: dict | None = None,
+              custom_usage_thresholds: dict | None = None, custom_prod_usage_thresholds: dict | None = None,
+              valid: bool = True) -> np.ndarray:
+    n = np.zeros(1, dtype=abi.NODE_DTYPE)
+    r = n[0]
+    r["allocatable"] = _values(allocatable)
+    r["allowed_pods"] = allowed_pods
+    flags = abi.NODE_VALID if valid else 0
+    if raw_allocatable:
+        flags |= abi.NODE_HAS_RAW_ALLOCATABLE
+        r["raw_allocatable"] = _values(raw_allocatable)
+        pres = np.zeros(abi.RES_MAX, dtype=np.int64)
+        for k in raw_allocatable:
+            pres[abi.RESOURCE_SLOTS[k]] = 1
+        r["raw_allocatable_present"] = pres
+    r["custom_usage_thresholds"] = _slots(custom_usage_thresholds, absent=-1)
+    r["custom_prod_usage_thresholds"] = _slots(custom_prod_usage_thresholds, absent=-1)
+    if custom_usage_thresholds or custom_prod_usage_thresholds:
+        flags |= abi.NODE_HAS_CUSTOM_THRESHOLDS
+    r["flags"] = flags
+    return n
+
+
+def make_node_metric(present: bool = True, update_time_ns: int | None = 0, node_usage: dict | None = None,
+                     prod_pods_usage: dict | None = None, pods_metric_count: int = 0) -> np.ndarray:
+    """NodeMetric status summary; node_usage=None means Status.NodeMetric == nil."""
+    m = np.zeros(1, dtype=abi.METRIC_DTYPE)
+    r = m[0]
+    r["present"] = int(present)
+    r["has_update_time"] = int(update_time_ns is not None)
+    r["update_time_unix_nano"] = update_time_ns or 0
+    if node_usage is not None:
+        r["has_node_metric"] = 1
+        r["node_usage"] = _values(node_usage)
+        pres = np.zeros(abi.RES_MAX, dtype=np.int64)
+        for k in node_usage:
+            pres[abi.RESOURCE_SLOTS[k]] = 1
+        r["node_usage_present"] = pres
+    r["pods_metric_count"] = pods_metric_count
+    r["prod_pods_usage"] = _values(prod_pods_usage)
+    return m
+
+
+def make_pod(requests: dict | None = None, limits: dict | None = None, priority_class: str = "",
+             daemonset: bool = False, nonzero: tuple | None = None) -> np.ndarray:
+    """One single-container pod. nonzero = schedutil.GetNonzeroRequests (100m / 200MiB defaults)."""
+    p = np.zeros(1, dtype=abi.POD_DTYPE)
+    r = p[0]
+    req = _values(requests)
+    r["requests"] = req
+    r["limits"] = _values(limits)
+    if nonzero is None:
+        nonzero = (req[abi.RES_CPU] or 100, req[abi.RES_MEMORY] or 200 * 1024 * 1024)
+    r["nonzero_requests"] = nonzero
+    r["priority_class"] = abi.PRIORITY_CLASSES[priority_class]
+    r["flags"] = abi.POD_DAEMONSET if daemonset else 0
+    return p
+
+
+@dataclass
+class ScheduleResult:
+    suggested_host: int          # node index, -1 = FitError (unschedulable)
+    score: int
+    evaluated_nodes: int
+    feasible_nodes: int = -1
+
+
+class Scheduler:
+    """SchedulePod / RunFilterPlugins / RunScorePlugins over the GPU engine."""
+
+    def __init__(self, config: np.ndarray, capacity: int, **kw):
+        self.config = config
+        self.engine = Engine(config, capacity, **kw)
+
+    def close(self):
+        self.engine.close()
+
+    def run_filter_plugins(self, pod: np.ndarray) -> dict:
+        rej, _, _ = self.engine.evaluate(pod)
+        c = self.config[0]
+        out = {}
+        if c["fit_filter"]:
+            out[NODE_RESOURCES_FIT] = np.where(rej & (abi.REJECT_FIT_PODS | abi.REJECT_FIT_CPU | abi.REJECT_FIT_MEMORY),
+                                               UNSCHEDULABLE, SUCCESS)
+        if c["la_filter"]:
+            out[LOAD_AWARE] = np.where(rej & abi.REJECT_LOADAWARE, UNSCHEDULABLE, SUCCESS)
+        return out
+
+    def run_score_plugins(self, pod: np.ndarray) -> dict:
+        _, fit, la = self.engine.evaluate(pod)
+        c = self.config[0]
+        out = {}
+        if c["fit_score"]:
+            out[NODE_RESOURCES_FIT] = fit
+        if c["la_score"]:
+            out[LOAD_AWARE] = la
+        return out
+
+    def schedule_pods(self, pods: np.ndarray):
+        return self.engine.schedule(pods)
+
+    def schedule_pod(self, pod: np.ndarray) -> ScheduleResult:
+        node, score, _ = self.engine.schedule(np.asarray(pod).reshape(1))
+        return ScheduleResult(int(node[0]), int(score[0]), self.engine.num_nodes)
+
+    def reserve(self, pod: np.ndarray, node_idx: int):
+        self.engine.add_pods(np.asarray(pod).reshape(1), [node_idx])
+
+    def unreserve(self, pod: np.ndarray, node_idx: int):
+        self.engine.remove_pods(np.asarray(pod).reshape(1), [node_idx])

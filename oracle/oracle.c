@@ -1,0 +1,386 @@
+/*
+ * oracle.c — plain-C restatement of the koord-scheduler Filter/Score/selectHost/assume path.
+ *
+ * TEST INFRASTRUCTURE ONLY (see oracle.h).  Build: oracle/Makefile (gcc -O2 -ffp-contract=off, no fast-math,
+ * so float64 expressions round exactly like Go's).  Every function cites the reference file:line it restates
+ * (paths relative to /root/reference).
+ */
+#define _GNU_SOURCE
+#include "oracle.h"
+
+#include <math.h>
+#include <pthread.h>
+#include <stdatomic.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sched.h>
+
+#define MAX_NODE_SCORE 100 /* framework.MaxNodeScore (k8s v1.24.15) */
+#define DEFAULT_MILLI_CPU_REQUEST 250LL                 /* estimator/default_estimator.go:36 */
+#define DEFAULT_MEMORY_REQUEST (200LL * 1024 * 1024)     /* estimator/default_estimator.go:38 */
+
+static int is_cpu_like(int r) { return r == KG_RES_CPU; }
+
+/* Quantity.MilliValue() of the value stored in slot r (cpu is stored in milli already). */
+static int64_t milli_of(int r, int64_t v) { return is_cpu_like(r) ? v : v * 1000; }
+
+/* apis/extension/resource.go:53-58 TranslateResourceNameByPriorityClass; -1 = "" (no such resource). */
+static int translate_resource(int64_t prio, int r) {
+  if (prio == KG_PRIO_PROD || prio == KG_PRIO_NONE) return r;
+  if (prio == KG_PRIO_BATCH) {
+    if (r == KG_RES_CPU) return KG_RES_BATCH_CPU;
+    if (r == KG_RES_MEMORY) return KG_RES_BATCH_MEMORY;
+    return -1;
+  }
+  if (prio == KG_PRIO_MID) {
+    if (r == KG_RES_CPU) return KG_RES_MID_CPU;
+    if (r == KG_RES_MEMORY) return KG_RES_MID_MEMORY;
+    return -1;
+  }
+  return -1; /* PriorityFree: ResourceNameMap has no entry → "" */
+}
+
+/* estimator/default_estimator.go:73-108 estimatedUsedByResource */
+int64_t or_estimated_used_by_resource(const kg_pod* pod, int real, int64_t scaling_factor) {
+  int64_t limit = real >= 0 ? pod->limits[real] : 0;
+  int64_t request = real >= 0 ? pod->requests[real] : 0;
+  int64_t q;
+  if (limit > request) { /* limitQuantity.Cmp(requestQuantity) > 0 */
+    scaling_factor = 100;
+    q = limit;
+  } else {
+    q = request;
+  }
+  if (q == 0) {
+    if (real == KG_RES_CPU || real == KG_RES_BATCH_CPU) return DEFAULT_MILLI_CPU_REQUEST;
+    if (real == KG_RES_MEMORY || real == KG_RES_BATCH_MEMORY) return DEFAULT_MEMORY_REQUEST;
+    return 0;
+  }
+  /* case cpu: MilliValue; default: Value — slot values already carry exactly that unit */
+  volatile double prod = (double)q * (double)scaling_factor; /* float64(q) * float64(f), rounded */
+  int64_t est = (int64_t)round(prod / 100.0);
+  if (limit > 0 && est > limit) est = limit;
+  return est;
+}
+
+/* estimator/default_estimator.go:57-70 estimatedPodUsed, for the weight keys cpu and memory */
+void or_estimate_pod(const kg_config* cfg, const kg_pod* pod, int64_t out[2]) {
+  for (int r = 0; r < 2; r++) {
+    out[r] = 0;
+    if (cfg->la_resource_weights[r] == 0) continue; /* only resources in ResourceWeights are estimated */
+    int real = translate_resource(pod->priority_class, r);
+    out[r] = or_estimated_used_by_resource(pod, real, cfg->la_estimated_scaling_factors[r]);
+  }
+}
+
+/* estimator/default_estimator.go:110-129 EstimateNode: raw-allocatable keys override node.Status.Allocatable */
+int64_t or_estimate_node(const kg_node* node, int r) {
+  if ((node->flags & KG_NODE_HAS_RAW_ALLOCATABLE) && node->raw_allocatable_present[r]) return node->raw_allocatable[r];
+  return node->allocatable[r];
+}
+
+/* loadaware/helper.go:36-41 isNodeMetricExpired */
+static int node_metric_expired(const kg_node_metric* m, int64_t expiration_seconds, int64_t now) {
+  if (!m->present || !m->has_update_time) return 1;
+  return expiration_seconds > 0 && (now - m->update_time_unix_nano) >= expiration_seconds * 1000000000LL;
+}
+
+/* loadaware/helper.go:102-140 generateUsageThresholdsFilterProfile (non-aggregated part). */
+/* Custom maps replace the args' maps when non-empty (len counts zero-valued keys; -1 = key absent).  Args
+ * maps encode "absent" as 0, which the threshold loop skips anyway (load_aware.go:186,235). */
+static void usage_threshold_profile(const kg_config* cfg, const kg_node* node, int64_t thr[KG_RES_MAX],
+                                    int64_t prod_thr[KG_RES_MAX], int* n_thr, int* n_prod) {
+  int custom = (node->flags & KG_NODE_HAS_CUSTOM_THRESHOLDS) != 0;
+  int nc = 0, ncp = 0, nargs = 0, nargs_prod = 0;
+  for (int r = 0; r < KG_RES_MAX; r++) {
+    if (custom && node->custom_usage_thresholds[r] >= 0) nc++;
+    if (custom && node->custom_prod_usage_thresholds[r] >= 0) ncp++;
+    if (cfg->la_usage_thresholds[r] != 0) nargs++;
+    if (cfg->la_prod_usage_thresholds[r] != 0) nargs_prod++;
+  }
+  for (int r = 0; r < KG_RES_MAX; r++) {
+    thr[r] = nc > 0 ? (node->custom_usage_thresholds[r] > 0 ? node->custom_usage_thresholds[r] : 0)
+                    : cfg->la_usage_thresholds[r];
+    prod_thr[r] = ncp > 0 ? (node->custom_prod_usage_thresholds[r] > 0 ? node->custom_prod_usage_thresholds[r] : 0)
+                          : cfg->la_prod_usage_thresholds[r];
+  }
+  *n_thr = nc > 0 ? nc : nargs;
+  *n_prod = ncp > 0 ? ncp : nargs_prod;
+}
+
+/* loadaware/load_aware.go:123-171 Filter (+ filterNodeUsage :173-224, filterProdUsage :226-254) */
+int or_loadaware_filter(const kg_config* cfg, const kg_node* node, const kg_node_metric* m, const kg_pod* pod,
+                        int64_t now) {
+  if (pod->flags & KG_POD_DAEMONSET) return 0;            /* :129-131 */
+  if (!m->present) return 0;                               /* :133-140 NotFound → skip */
+  if (cfg->la_filter_expired_node_metrics && cfg->la_node_metric_expiration_seconds >= 0 &&
+      node_metric_expired(m, cfg->la_node_metric_expiration_seconds, now))
+    return 0;                                              /* :144-147 */
+  int64_t thr[KG_RES_MAX], pthr[KG_RES_MAX];
+  int n_thr, n_prod;
+  usage_threshold_profile(cfg, node, thr, pthr, &n_thr, &n_prod);
+  if (n_prod > 0 && pod->priority_class == KG_PRIO_PROD) { /* :150-154 → filterProdUsage :226-254 */
+    if (m->pods_metric_count == 0) return 0;               /* :227-229 */
+    for (int r = 0; r < KG_RES_MAX; r++) {
+      if (pthr[r] == 0) continue;                          /* :235-237 */
+      int64_t total = or_estimate_node(node, r);
+      if (total == 0) continue;                            /* :243-246 */
+      volatile double q = (double)milli_of(r, m->prod_pods_usage[r]) / (double)milli_of(r, total);
+      volatile double pct = q * 100.0;
+      if ((int64_t)round(pct) >= pthr[r]) return 1;        /* :248-251 */
+    }
+    return 0;
+  }
+  if (n_thr == 0) return 0;
+  if (!m->has_node_metric) return 0;                       /* :174-176 */
+  for (int r = 0; r < KG_RES_MAX; r++) {                   /* :185-222 */
+    if (thr[r] == 0) continue;
+    int64_t total = or_estimate_node(node, r);
+    if (total == 0) continue;
+    int64_t used = m->node_usage_present[r] ? m->node_usage[r] : 0;
+    volatile double q = (double)milli_of(r, used) / (double)milli_of(r, total);
+    volatile double pct = q * 100.0;
+    int64_t usage = (int64_t)round(pct);
+    if (usage >= thr[r]) return 1;
+  }
+  return 0;
+}
+
+/* loadaware/load_aware.go:388-397 leastRequestedScore */
+int64_t or_least_requested_score(int64_t requested, int64_t capacity) {
+  if (capacity == 0) return 0;
+  if (requested > capacity) return 0;
+  return ((capacity - requested) * MAX_NODE_SCORE) / capacity;
+}
+
+/* loadaware/load_aware.go:269-335 Score (+ estimatedAssignedPodUsed :337-376, scorer :378-386).
+ * PodsMetric is empty in the restated profile (helper.go:153-156 → nil map), so every assigned pod is estimated
+ * (:354) and no pod usage is subtracted from NodeUsage (:317). */
+int64_t or_loadaware_score(const kg_config* cfg, const kg_node* node, const kg_node_metric* m,
+                           const or_node_state* st, const kg_pod* pod, int64_t now) {
+  if (!m->present) return 0;                                                          /* :278-284 */
+  if (cfg->la_node_metric_expiration_seconds >= 0 &&
+      node_metric_expired(m, cfg->la_node_metric_expiration_seconds, now))
+    return 0;                                                                         /* :287-289 */
+  if (m->pods_metric_count != 0) return -1;
+  int prod_pod = pod->priority_class == KG_PRIO_PROD && cfg->la_score_according_prod_usage; /* :291 */
+  int64_t est[2];
+  or_estimate_pod(cfg, pod, est);                                                     /* :294 */
+  int64_t used[2];
+  for (int r = 0; r < 2; r++) used[r] = est[r] + (prod_pod ? st->la_est_prod[r] : st->la_est_all[r]); /* :298-301 */
+  if (!prod_pod && m->has_node_metric) {                                              /* :307-326 */
+    for (int r = 0; r < 2; r++)
+      if (m->node_usage_present[r]) used[r] += m->node_usage[r];
+  }
+  int64_t node_score = 0, weight_sum = 0;                                             /* :378-386 */
+  for (int r = 0; r < 2; r++) {
+    int64_t w = cfg->la_resource_weights[r];
+    if (w == 0) continue;
+    node_score += or_least_requested_score(used[r], or_estimate_node(node, r)) * w;
+    weight_sum += w;
+  }
+  if (weight_sum == 0) return -1; /* Go would divide by zero; validation forbids it */
+  return node_score / weight_sum;
+}
+
+/* k8s v1.24.15 noderesources/fit.go fitsRequest (restated in-tree by reservation/plugin.go:433-482). */
+int or_fit_filter(const kg_node* node, const or_node_state* st, const kg_pod* pod) {
+  int reasons = 0;
+  if (st->num_pods + 1 > node->allowed_pods) reasons |= KG_REJECT_FIT_PODS;
+  int zero = 1;
+  for (int r = 0; r < KG_RES_MAX; r++) zero &= pod->requests[r] == 0;
+  if (zero) return reasons;
+  if (pod->requests[KG_RES_CPU] > node->allocatable[KG_RES_CPU] - st->requested[KG_RES_CPU])
+    reasons |= KG_REJECT_FIT_CPU;
+  if (pod->requests[KG_RES_MEMORY] > node->allocatable[KG_RES_MEMORY] - st->requested[KG_RES_MEMORY])
+    reasons |= KG_REJECT_FIT_MEMORY;
+  return reasons;
+}
+
+/* k8s v1.24.15 noderesources resource_allocation.go score + least_allocated.go leastResourceScorer with
+ * useRequested=false (NonZeroRequested); restated in-tree by nodenumaresource/scoring.go:191-230 and
+ * least_allocated.go:30-58.  Only cpu/memory keys (non-scalar) are restated. */
+int64_t or_fit_score(const kg_config* cfg, const kg_node* node, const or_node_state* st, const kg_pod* pod) {
+  int64_t node_score = 0, weight_sum = 0;
+  for (int r = 0; r < 2; r++) {
+    int64_t w = cfg->fit_resource_weights[r];
+    if (w == 0) continue;                           /* not a key of resourceToWeightMap */
+    int64_t alloc = node->allocatable[r];
+    if (alloc == 0) continue;                       /* "Only fill the extended resource entry when it's non-zero" */
+    int64_t req = st->nonzero[r] + pod->nonzero_requests[r];
+    node_score += or_least_requested_score(req, alloc) * w;
+    weight_sum += w;
+  }
+  if (weight_sum == 0) return 0;
+  return node_score / weight_sum;
+}
+
+/* upstream NodeInfo.AddPod/RemovePod + LoadAware Reserve/Unreserve → podAssignCache.assign/unAssign
+ * (load_aware.go:260-267, pod_assign_cache.go:53-80) with the estimate taken at Score time (:359). */
+void or_apply_pod(const kg_config* cfg, or_node_state* st, const kg_pod* pod, int sign) {
+  for (int r = 0; r < KG_RES_MAX; r++) st->requested[r] += sign * pod->requests[r];
+  st->nonzero[0] += sign * pod->nonzero_requests[0];
+  st->nonzero[1] += sign * pod->nonzero_requests[1];
+  st->num_pods += sign;
+  int64_t est[2];
+  or_estimate_pod(cfg, pod, est);
+  for (int r = 0; r < 2; r++) {
+    st->la_est_all[r] += sign * est[r];
+    if (pod->priority_class == KG_PRIO_PROD) st->la_est_prod[r] += sign * est[r];
+  }
+}
+
+void or_states_init(int64_t n_nodes, or_node_state* st) { memset(st, 0, sizeof(*st) * (size_t)n_nodes); }
+
+int or_states_add_pods(const kg_config* cfg, int64_t n_nodes, or_node_state* st, int64_t n, const kg_pod* pods,
+                       const int32_t* node_idx) {
+  for (int64_t i = 0; i < n; i++) {
+    if (node_idx[i] < 0 || node_idx[i] >= n_nodes) return KG_E_INVALID;
+    or_apply_pod(cfg, &st[node_idx[i]], &pods[i], +1);
+  }
+  return 0;
+}
+
+/* ---------------------------------------------------------------------------------------------------
+ * Scheduling loop.  Per pod: Filter pass over all nodes, Score pass over feasible nodes, weighted sum,
+ * selectHost with lowest-index tie-break, assume.  Parallel passes mirror the reference Parallelizer:
+ * 16 workers by default, chunk = max(1, min(sqrt(n), n/16+1)) (pkg/util/parallelize/parallelism.go:29-49).
+ * ------------------------------------------------------------------------------------------------- */
+typedef struct sched_ctx {
+  const kg_config* cfg;
+  int64_t n_nodes;
+  const kg_node* nodes;
+  const kg_node_metric* metrics;
+  or_node_state* st;
+  int64_t now;
+  const kg_pod* pod;
+  int32_t* feasible;      /* per node: 1 feasible, 0 not, -1 unsupported */
+  int64_t* total;         /* weighted score per node                     */
+  int64_t chunk;
+  atomic_long next;       /* work counter for the current phase          */
+  int phase;              /* 0 filter, 1 score                           */
+  int n_threads;
+  atomic_int arrive;
+  atomic_int generation;
+  atomic_int stop;
+} sched_ctx;
+
+static void eval_filter(sched_ctx* c, int64_t i) {
+  const kg_config* cfg = c->cfg;
+  if (!(c->nodes[i].flags & KG_NODE_VALID)) { c->feasible[i] = 0; return; }
+  int ok = 1;
+  if (cfg->fit_filter && or_fit_filter(&c->nodes[i], &c->st[i], c->pod) != 0) ok = 0;
+  if (ok && cfg->la_filter) {
+    int s = or_loadaware_filter(cfg, &c->nodes[i], &c->metrics[i], c->pod, c->now);
+    if (s < 0) { c->feasible[i] = -1; return; }
+    if (s != 0) ok = 0;
+  }
+  c->feasible[i] = ok;
+}
+
+static void eval_score(sched_ctx* c, int64_t i) {
+  const kg_config* cfg = c->cfg;
+  if (c->feasible[i] != 1) return;
+  int64_t t = 0;
+  if (cfg->fit_score) t += cfg->weight_fit * or_fit_score(cfg, &c->nodes[i], &c->st[i], c->pod);
+  if (cfg->la_score) {
+    int64_t s = or_loadaware_score(cfg, &c->nodes[i], &c->metrics[i], &c->st[i], c->pod, c->now);
+    if (s < 0) { c->feasible[i] = -1; return; }
+    t += cfg->weight_loadaware * s;
+  }
+  c->total[i] = t;
+}
+
+static void run_chunks(sched_ctx* c) {
+  for (;;) {
+    int64_t start = atomic_fetch_add(&c->next, c->chunk);
+    if (start >= c->n_nodes) break;
+    int64_t end = start + c->chunk < c->n_nodes ? start + c->chunk : c->n_nodes;
+    for (int64_t i = start; i < end; i++) {
+      if (c->phase == 0) eval_filter(c, i);
+      else eval_score(c, i);
+    }
+  }
+}
+
+/* sense-reversing barrier over n_threads (workers + the main thread) */
+static void barrier_wait(sched_ctx* c) {
+  int gen = atomic_load(&c->generation);
+  if (atomic_fetch_add(&c->arrive, 1) == c->n_threads - 1) {
+    atomic_store(&c->arrive, 0);
+    atomic_fetch_add(&c->generation, 1);
+  } else {
+    int spins = 0;
+    while (atomic_load(&c->generation) == gen) {
+      if (++spins > 256) { sched_yield(); spins = 0; }
+    }
+  }
+}
+
+static void* worker(void* arg) {
+  sched_ctx* c = (sched_ctx*)arg;
+  for (;;) {
+    barrier_wait(c); /* phase start */
+    if (atomic_load(&c->stop)) break;
+    run_chunks(c);
+    barrier_wait(c); /* phase end */
+  }
+  return NULL;
+}
+
+static void run_phase(sched_ctx* c, int phase) {
+  c->phase = phase;
+  atomic_store(&c->next, 0);
+  if (c->n_threads <= 1) { run_chunks(c); return; }
+  barrier_wait(c);
+  run_chunks(c);
+  barrier_wait(c);
+}
+
+int or_schedule(const kg_config* cfg, int64_t n_nodes, const kg_node* nodes, const kg_node_metric* metrics,
+                or_node_state* st, int64_t n_pods, const kg_pod* pods, int64_t now, int n_threads,
+                int32_t* out_node, int64_t* out_score) {
+  sched_ctx c;
+  memset(&c, 0, sizeof(c));
+  c.cfg = cfg; c.n_nodes = n_nodes; c.nodes = nodes; c.metrics = metrics; c.st = st; c.now = now;
+  c.feasible = (int32_t*)malloc(sizeof(int32_t) * (size_t)(n_nodes > 0 ? n_nodes : 1));
+  c.total = (int64_t*)malloc(sizeof(int64_t) * (size_t)(n_nodes > 0 ? n_nodes : 1));
+  if (!c.feasible || !c.total) { free(c.feasible); free(c.total); return KG_E_NOMEM; }
+  if (n_threads < 1) n_threads = 1;
+  c.n_threads = n_threads;
+  /* chunkSizeFor (parallelism.go:35-46) with parallelism = n_threads */
+  int64_t s = (int64_t)sqrt((double)n_nodes);
+  int64_t r = n_nodes / n_threads + 1;
+  if (s > r) s = r; else if (s < 1) s = 1;
+  c.chunk = s;
+  pthread_t* th = NULL;
+  if (n_threads > 1) {
+    th = (pthread_t*)malloc(sizeof(pthread_t) * (size_t)(n_threads - 1));
+    for (int t = 0; t < n_threads - 1; t++) pthread_create(&th[t], NULL, worker, &c);
+  }
+  int rc = 0;
+  for (int64_t p = 0; p < n_pods && rc == 0; p++) {
+    c.pod = &pods[p];
+    run_phase(&c, 0);
+    run_phase(&c, 1);
+    /* selectHost: max total, ties → lowest snapshot index (BASELINE determinism pin) */
+    int64_t best = -1, best_score = 0;
+    for (int64_t i = 0; i < n_nodes; i++) {
+      if (c.feasible[i] < 0) { rc = KG_E_UNSUPPORTED; break; }
+      if (c.feasible[i] == 1 && (best < 0 || c.total[i] > best_score)) { best = i; best_score = c.total[i]; }
+    }
+    if (rc) break;
+    out_node[p] = (int32_t)best;
+    out_score[p] = best >= 0 ? best_score : 0;
+    if (best >= 0) or_apply_pod(cfg, &st[best], &pods[p], +1); /* assume + Reserve */
+  }
+  if (n_threads > 1) {
+    atomic_store(&c.stop, 1);
+    barrier_wait(&c);
+    for (int t = 0; t < n_threads - 1; t++) pthread_join(th[t], NULL);
+    free(th);
+  }
+  free(c.feasible);
+  free(c.total);
+  return rc;
+}

@@ -1,0 +1,73 @@
+/*
+ * oracle.h — CPU restatement of the koord-scheduler Filter/Score hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing under koordinator_amd/ links, loads or calls this code; only tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg do, as the checker / CPU baseline.
+ *
+ * Pinning: the reference (Go 1.18 + k8s.io/kubernetes v1.24.15) cannot be built in this container (no Go
+ * toolchain, no module cache).  This restatement is pinned by golden vectors transcribed
+ * from the reference's own table-driven tests (tests/golden/, script tests/golden/make_golden.py).
+ * Upstream NodeResourcesFit Score (NonZeroRequested) is restated from k8s v1.24.15 resource_allocation.go /
+ * least_allocated.go and from the in-tree restatement nodenumaresource/least_allocated.go:30-58 +
+ * scoring.go:191-230: "parity unpinned" for the upstream part (no reference test exercises it).
+ *
+ * The data model is the engine ABI's (include/koordgpu.h): the oracle consumes exactly the same inputs.
+ */
+#ifndef KOORD_ORACLE_H_
+#define KOORD_ORACLE_H_
+#include <stdint.h>
+#include "../include/koordgpu.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* One mutable node row as the reference holds it across plugins. */
+typedef struct or_node_state {
+  int64_t requested[KG_RES_MAX];     /* upstream NodeInfo.Requested                          */
+  int64_t nonzero[2];                /* upstream NodeInfo.NonZeroRequested {MilliCPU, Memory} */
+  int64_t num_pods;                  /* len(NodeInfo.Pods)                                    */
+  int64_t la_est_all[2];             /* Σ EstimatePod over podAssignCache[node] (cpu, mem)    */
+  int64_t la_est_prod[2];            /* same, prod-priority pods only                         */
+} or_node_state;
+
+/* LoadAware estimator (estimator/default_estimator.go:57-108): out[0]=cpu, out[1]=memory. */
+void or_estimate_pod(const kg_config* cfg, const kg_pod* pod, int64_t out[2]);
+/* Estimator for one translated resource (estimatedUsedByResource, default_estimator.go:73-108). */
+int64_t or_estimated_used_by_resource(const kg_pod* pod, int real_res, int64_t scaling_factor);
+/* DefaultEstimator.EstimateNode (default_estimator.go:110-129): value of resource r. */
+int64_t or_estimate_node(const kg_node* node, int r);
+
+/* LoadAwareScheduling.Filter (load_aware.go:123-171): 0 = Success, 1 = Unschedulable, <0 = unsupported. */
+int or_loadaware_filter(const kg_config* cfg, const kg_node* node, const kg_node_metric* m, const kg_pod* pod,
+                        int64_t now_unix_nano);
+/* LoadAwareScheduling.Score (load_aware.go:269-335); returns <0 on unsupported input. */
+int64_t or_loadaware_score(const kg_config* cfg, const kg_node* node, const kg_node_metric* m,
+                           const or_node_state* st, const kg_pod* pod, int64_t now_unix_nano);
+/* Upstream NodeResourcesFit.Filter/fitsRequest: 0 ok, else KG_REJECT_* bits of the first failures. */
+int or_fit_filter(const kg_node* node, const or_node_state* st, const kg_pod* pod);
+/* Upstream NodeResourcesFit.Score, LeastAllocated over NonZeroRequested. */
+int64_t or_fit_score(const kg_config* cfg, const kg_node* node, const or_node_state* st, const kg_pod* pod);
+/* leastRequestedScore (loadaware/load_aware.go:388-397, nodenumaresource/least_allocated.go:49-58). */
+int64_t or_least_requested_score(int64_t requested, int64_t capacity);
+
+/* Assume/AddPod + podAssignCache.assign for one pod onto one node state. sign=+1 add, -1 remove. */
+void or_apply_pod(const kg_config* cfg, or_node_state* st, const kg_pod* pod, int sign);
+
+/* Sequential FIFO scheduling of `n_pods` over `n_nodes` (percentageOfNodesToScore=100, ties → lowest index).
+ * `st` is updated in place (assume).  n_threads>1 splits every per-pod Filter and Score pass over threads
+ * with the reference Parallelizer's chunking (pkg/util/parallelize/parallelism.go:29-49).
+ * Returns 0, or <0 if an input is outside the restated profile. */
+int or_schedule(const kg_config* cfg, int64_t n_nodes, const kg_node* nodes, const kg_node_metric* metrics,
+                or_node_state* st, int64_t n_pods, const kg_pod* pods, int64_t now_unix_nano, int n_threads,
+                int32_t* out_node, int64_t* out_score);
+
+/* Builds node states from pre-existing assigned pods (informer adds). */
+void or_states_init(int64_t n_nodes, or_node_state* st);
+int or_states_add_pods(const kg_config* cfg, int64_t n_nodes, or_node_state* st, int64_t n, const kg_pod* pods,
+                       const int32_t* node_idx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,127 @@
+"""ctypes binding of the CPU restatement (oracle/oracle.c).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg, as the
+checker or the timed CPU baseline — never by koordinator_amd/.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+from koordinator_amd import abi
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "build", "liboracle.so")
+
+OR_STATE_DTYPE = np.dtype([
+    ("requested", np.int64, (abi.RES_MAX,)),
+    ("nonzero", np.int64, (2,)),
+    ("num_pods", np.int64),
+    ("la_est_all", np.int64, (2,)),
+    ("la_est_prod", np.int64, (2,)),
+])
+
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        L = ctypes.CDLL(LIB)
+        vp, i64, i = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int
+        L.or_estimate_pod.argtypes = [vp, vp, vp]
+        L.or_estimate_node.argtypes = [vp, i]
+        L.or_estimate_node.restype = i64
+        L.or_loadaware_filter.argtypes = [vp, vp, vp, vp, i64]
+        L.or_loadaware_filter.restype = i
+        L.or_loadaware_score.argtypes = [vp, vp, vp, vp, vp, i64]
+        L.or_loadaware_score.restype = i64
+        L.or_fit_filter.argtypes = [vp, vp, vp]
+        L.or_fit_filter.restype = i
+        L.or_fit_score.argtypes = [vp, vp, vp, vp]
+        L.or_fit_score.restype = i64
+        L.or_least_requested_score.argtypes = [i64, i64]
+        L.or_least_requested_score.restype = i64
+        L.or_apply_pod.argtypes = [vp, vp, vp, i]
+        L.or_states_init.argtypes = [i64, vp]
+        L.or_states_add_pods.argtypes = [vp, i64, vp, i64, vp, vp]
+        L.or_states_add_pods.restype = i
+        L.or_schedule.argtypes = [vp, i64, vp, vp, vp, i64, vp, i64, i, vp, vp]
+        L.or_schedule.restype = i
+        _lib = L
+    return _lib
+
+
+p = abi.ptr
+
+
+def states(n: int) -> np.ndarray:
+    st = np.zeros(n, dtype=OR_STATE_DTYPE)
+    lib().or_states_init(n, p(st))
+    return st
+
+
+def add_pods(cfg, st, pods, node_idx):
+    pods = np.ascontiguousarray(pods, dtype=abi.POD_DTYPE)
+    node_idx = np.ascontiguousarray(node_idx, dtype=np.int32)
+    rc = lib().or_states_add_pods(p(cfg), len(st), p(st), len(pods), p(pods), p(node_idx))
+    assert rc == 0, rc
+
+
+def estimate_pod(cfg, pod) -> tuple:
+    out = np.zeros(2, dtype=np.int64)
+    lib().or_estimate_pod(p(cfg), p(np.ascontiguousarray(pod)), p(out))
+    return int(out[0]), int(out[1])
+
+
+def estimate_node(node, r: int) -> int:
+    return int(lib().or_estimate_node(p(np.ascontiguousarray(node)), r))
+
+
+def loadaware_filter(cfg, node, metric, pod, now_ns: int) -> int:
+    return int(lib().or_loadaware_filter(p(cfg), p(node), p(metric), p(pod), now_ns))
+
+
+def loadaware_score(cfg, node, metric, state, pod, now_ns: int) -> int:
+    return int(lib().or_loadaware_score(p(cfg), p(node), p(metric), p(state), p(pod), now_ns))
+
+
+def fit_filter(node, state, pod) -> int:
+    return int(lib().or_fit_filter(p(node), p(state), p(pod)))
+
+
+def fit_score(cfg, node, state, pod) -> int:
+    return int(lib().or_fit_score(p(cfg), p(node), p(state), p(pod)))
+
+
+def least_requested(requested: int, capacity: int) -> int:
+    return int(lib().or_least_requested_score(requested, capacity))
+
+
+def schedule(cfg, nodes, metrics, st, pods, now_ns: int, n_threads: int = 1):
+    """Sequential FIFO scheduling; mutates `st` (assume). Returns (node_idx, score)."""
+    pods = np.ascontiguousarray(pods, dtype=abi.POD_DTYPE)
+    out_node = np.empty(len(pods), dtype=np.int32)
+    out_score = np.empty(len(pods), dtype=np.int64)
+    rc = lib().or_schedule(p(cfg), len(nodes), p(nodes), p(metrics), p(st), len(pods), p(pods), now_ns,
+                           n_threads, p(out_node), p(out_score))
+    if rc != 0:
+        raise RuntimeError(f"oracle or_schedule failed: {rc}")
+    return out_node, out_score
+
+
+def schedule_cluster(cfg, cluster, pods, n_threads: int = 1):
+    st = states(cluster.n)
+    if len(cluster.existing_pods):
+        add_pods(cfg, st, cluster.existing_pods, cluster.existing_node)
+    node, score = schedule(cfg, cluster.nodes, cluster.metrics, st, pods, cluster.now_ns, n_threads)
+    return node, score, st

@@ -1,0 +1,87 @@
+"""Turns tests/golden/*.json cases into ABI records (config, node, metric, pods) — shared by the oracle and
+GPU parity tests."""
+import json
+import os
+
+import numpy as np
+
+from koordinator_amd import abi, framework
+from koordinator_amd.quantity import resource_value
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+NOW_NS = 1_800_000_000 * 10**9
+
+
+def load(name):
+    with open(os.path.join(GOLDEN, name)) as f:
+        return json.load(f)
+
+
+def cases(name, scope=("core",)):
+    d = load(name)
+    return [(d, c) for c in d["cases"] if c["scope"] in scope]
+
+
+def case_id(dc):
+    return dc[1]["name"].replace(" ", "_")
+
+
+def la_args(doc, case):
+    a = framework.LoadAwareSchedulingArgs()
+    if "filter_expired_node_metrics" in doc:
+        a.filter_expired_node_metrics = doc["filter_expired_node_metrics"]
+    args = case.get("args") or {}
+    if "usage_thresholds" in args:  # v1beta2 defaults only fill an EMPTY map
+        a.usage_thresholds = {k: v for k, v in args["usage_thresholds"].items()}
+    if "prod_usage_thresholds" in args:
+        a.prod_usage_thresholds = dict(args["prod_usage_thresholds"])
+    if "score_according_prod_usage" in args:
+        a.score_according_prod_usage = args["score_according_prod_usage"]
+    if "factors" in case:  # SetDefaults fills the missing scaling-factor keys (v1beta2/defaults.go:92-98)
+        f = {"cpu": 85, "memory": 70}
+        f.update(case["factors"])
+        a.estimated_scaling_factors = f
+    return a
+
+
+def config(doc, case, profile=None, **kw):
+    return framework.build_config(la=la_args(doc, case), profile=profile, **kw)
+
+
+def node(doc, case):
+    return framework.make_node(doc.get("node_allocatable", {}),
+                               custom_usage_thresholds=case.get("custom_usage_thresholds"),
+                               custom_prod_usage_thresholds=case.get("custom_prod_usage_thresholds"))
+
+
+def metric(case):
+    m = case.get("metric")
+    if m is None:
+        return framework.make_node_metric(present=False)
+    age = m.get("update_age_s", 0)
+    return framework.make_node_metric(
+        present=True, update_time_ns=None if age is None else NOW_NS - age * 10**9,
+        node_usage=m.get("node_usage"), prod_pods_usage=m.get("prod_pods_usage"),
+        pods_metric_count=m.get("pods_metric_count", len(m.get("pods_metric", []))))
+
+
+def pod(spec):
+    """A fixture pod; a nil/empty test pod is &corev1.Pod{} → koord-batch (BestEffort)."""
+    spec = spec or {}
+    requests = spec.get("requests") or {}
+    prio = spec.get("priority")
+    if prio is None:
+        prio = "koord-batch" if not requests else "koord-prod"  # Guaranteed/Burstable with no label → LS/LSR → prod
+    return framework.make_pod(requests=requests, limits=spec.get("limits"), priority_class=prio,
+                              daemonset=spec.get("daemonset", False))
+
+
+def assigned(case):
+    specs = case.get("assigned") or []
+    if not specs:
+        return np.zeros(0, dtype=abi.POD_DTYPE)
+    return np.concatenate([pod(s) for s in specs])
+
+
+def quantity_map(d):
+    return {k: resource_value(k, v) for k, v in d.items()}
