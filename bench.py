@@ -147,9 +147,8 @@ def main():
     placed = int((node_idx >= 0).sum())
 
     # per-kernel live timing (HIP events on the engine stream) for the roofline
-    eval_ms, eval_bytes = e.bench_kernel(0, args.kernel_iters)
-    res_ms, res_bytes = e.bench_kernel(1, args.kernel_iters)
-    kernels = {"eval_round": (eval_ms, eval_bytes), "resolve_round": (res_ms, res_bytes)}
+    kernels = {name: e.bench_kernel(which, args.kernel_iters)
+               for which, name in enumerate(("eval_round", "merge_round", "resolve_round"))}
     dom = max(kernels, key=lambda k: kernels[k][0])
     dom_ms, dom_bytes = kernels[dom]
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9

@@ -206,7 +206,7 @@ int kg_nodes_read_state(kg_engine* e, int64_t* requested_cpu, int64_t* requested
                         int64_t* nonzero_mem, int64_t* num_pods, int64_t* la_est_cpu, int64_t* la_est_mem,
                         int64_t* la_est_prod_cpu, int64_t* la_est_prod_mem);
 
-/* Measurement hooks (bench.py): replays one device round's kernel `which` (0 = eval, 1 = resolve) `iters` times
+/* Measurement hooks (bench.py): replays one device round's kernel `which` (0 = eval, 1 = merge, 2 = resolve) `iters` times
  * on the engine stream between HIP events, restoring state, and returns the mean duration in ms plus the
  * algorithmic bytes that kernel must move per launch. Requires a staged queue. */
 int kg_bench_kernel(kg_engine* e, int which, int iters, double* avg_ms, double* algo_bytes);
@@ -214,6 +214,11 @@ int kg_bench_kernel(kg_engine* e, int which, int iters, double* avg_ms, double* 
  * division-free path). */
 int kg_debug_least_requested(kg_engine* e, const int64_t* requested, const int64_t* capacity, int64_t* out,
                              int64_t n);
+
+/* Debug: evaluates every staged pod on every node with both device evaluation paths (the reference-shaped
+ * one used for modified rows and per-plugin output, and the hoisted-term one of the wide pass) and returns
+ * the number of (pod, node) pairs where feasibility or total score differ (must be 0). */
+int kg_debug_eval_paths(kg_engine* e, int64_t* mismatches);
 
 const char* kg_last_error(void);
 int kg_abi_version(void);

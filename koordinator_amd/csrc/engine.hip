@@ -36,6 +36,10 @@ constexpr int kTile = kWave * kNPT;   // 256 nodes per tile
 constexpr int kR = 8;                 // candidates kept per (pod, tile)
 constexpr int kEvalWaves = 4;         // waves (tiles) per eval block
 constexpr int kMaxB = 64;             // modified rows are held one per lane of the resolver wave
+constexpr int kC = 64;                // merged candidates per pod (> any modified-set size: kC > kMaxB - 1)
+constexpr int kCandStride = 72;       // per-pod record: kC keys, ub, padding to a 64-B multiple
+constexpr int kMergeThreads = 256;
+constexpr int kMergeChunks = 4;       // chunks of 8 keys per merge thread: ≤ 1024 tile lists = 262144 nodes per rank
 constexpr int64_t kMaxNodes = 1 << 20;  // resolver bitmap lives in LDS: N/8 bytes ≤ 128 KiB
 
 thread_local std::string g_err;
@@ -66,8 +70,9 @@ int fail(int code, const char* fmt, ...) {
 // Kernels
 // ------------------------------------------------------------------------------------------------
 
-// One wave = one tile of kTile nodes (lane l holds nodes tile*kTile + j*64 + l, j < kNPT) × pods_per_wave pods.
-// Writes lists[(rank, pod, tile)][kR] = the top-kR keys of the tile (unordered, zero-padded).
+// ---- round kernel 1: wide evaluation -------------------------------------------------------------
+// One wave = one tile of kTile nodes (lane l holds nodes tile*kTile + j*64 + l, j < kNPT) × pods_per_wave pods
+// of the round.  Writes lists[(pod, tile)][kR] = the tile's top-kR packed keys (unordered, zero-padded).
 __global__ __launch_bounds__(kWave* kEvalWaves) void eval_round(DevTable T, const DevPod* __restrict__ pods,
                                                                   const int64_t* __restrict__ cursor_p,
                                                                   int64_t end, int B, int pods_per_wave,
@@ -82,16 +87,18 @@ __global__ __launch_bounds__(kWave* kEvalWaves) void eval_round(DevTable T, cons
   if (tile >= nt_local || p0 >= nb) return;
   const int p1 = (p0 + pods_per_wave) < nb ? (p0 + pods_per_wave) : nb;
 
-  Row rows[kNPT];
-  bool in_range[kNPT];
+  EvalRow rows[kNPT];
   uint32_t gidx[kNPT];
 #pragma unroll
   for (int j = 0; j < kNPT; ++j) {
     const int64_t local = (int64_t)tile * kTile + j * kWave + lane;
-    in_range[j] = local < n_local;
     gidx[j] = (uint32_t)(node_base + local);
-    if (in_range[j]) rows[j] = load_row(T, node_base + local);
-    else rows[j].flags = 0;
+    if (local < n_local) {
+      rows[j] = make_eval_row(load_row(T, node_base + local), P);
+    } else {
+      rows[j] = EvalRow{};
+      rows[j].flags = 0;  // not F_VALID → never feasible
+    }
   }
   const uint64_t lane_lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
 
@@ -102,9 +109,8 @@ __global__ __launch_bounds__(kWave* kEvalWaves) void eval_round(DevTable T, cons
     int nfeas = 0;
 #pragma unroll
     for (int j = 0; j < kNPT; ++j) {
-      int64_t t = 0;
-      const bool ok = in_range[j] && eval_node(rows[j], p, P, t);
-      tot[j] = (uint32_t)t;
+      tot[j] = 0;
+      const bool ok = eval_fast(rows[j], p, P, tot[j]);
       fm[j] = __ballot(ok);
       nfeas += __popcll(fm[j]);
     }
@@ -113,7 +119,7 @@ __global__ __launch_bounds__(kWave* kEvalWaves) void eval_round(DevTable T, cons
 #pragma unroll
       for (int j = 0; j < kNPT; ++j) sel[j] = fm[j];
     } else {
-      // τ = largest score with count(score ≥ τ) ≥ kR, by one ballot per score bit.
+      // τ = largest score with count(score ≥ τ) ≥ kR, one ballot per score bit.
       uint32_t cur = 0;
       for (int b = P.score_bits - 1; b >= 0; --b) {
         const uint32_t c = cur | (1u << b);
@@ -154,13 +160,192 @@ __global__ __launch_bounds__(kWave* kEvalWaves) void eval_round(DevTable T, cons
   }
 }
 
-// Single wavefront: FIFO replay of the round. lane l < nM keeps modified row l in registers; an LDS bitmap
-// marks modified node indices.  Writes out_keys[cursor + j] (0 = unschedulable) and advances the cursor by the
-// number of pods whose decision is proven exact.
+// ---- round kernel 2: per-pod merge ------------------------------------------------------------------
+// One block per pod of the round: the kC largest keys of the union of the pod's candidate lists, sorted
+// descending (0-padded), plus a STRICT upper bound `ub` on every key left out (0 = nothing left out):
+//   ub = max(max_l ub_l, (kC+1)-th key of the union + 1), where a tile list's ub_l is its minimum when it is
+//   full (its unseen nodes all score lower) and a rank list carries its own ub in slot kC.
+// The kC-th key is found by an 8-bit radix select over the 64-bit keys (keys are unique: score<<32 | ~idx).
+template <bool RANK_LISTS>
+__global__ __launch_bounds__(kMergeThreads) void merge_round(const uint64_t* __restrict__ in, int64_t pod_stride,
+                                                             int64_t list_stride, int n_lists, int list_len,
+                                                             const int64_t* __restrict__ cursor_p, int64_t end,
+                                                             int B, uint64_t* __restrict__ out) {
+  __shared__ uint32_t hist[256];
+  __shared__ uint64_t sel[kC];
+  __shared__ uint64_t red64[kMergeThreads / kWave];
+  __shared__ uint32_t red32[kMergeThreads / kWave];
+  __shared__ uint64_t sh_prefix;
+  __shared__ uint32_t sh_target, sh_nsel;
+  const int64_t cursor = *cursor_p;
+  if (cursor >= end) return;
+  const int nb = (end - cursor) < (int64_t)B ? (int)(end - cursor) : B;
+  const int pod = blockIdx.x;
+  if (pod >= nb) return;
+  const int tid = threadIdx.x, lane = tid % kWave, wave = tid / kWave;
+  const uint64_t* base = in + (size_t)pod * pod_stride;
+
+  // Keys held in registers: thread t owns chunks c = t + kMergeThreads*i of 8 consecutive keys.
+  const int chunks_per_list = list_len / 8;
+  const int n_chunks = n_lists * chunks_per_list;
+  uint64_t k[kMergeChunks][8];
+  uint64_t ub_in = 0, kmax = 0;
+  uint32_t nz = 0;
+#pragma unroll
+  for (int i = 0; i < kMergeChunks; ++i) {
+    const int c = tid + kMergeThreads * i;
+    if (c < n_chunks) {
+      const int l = c / chunks_per_list, part = c - l * chunks_per_list;
+      const uint64_t* src = base + (size_t)l * list_stride + part * 8;
+#pragma unroll
+      for (int r = 0; r < 8; r += 2) {
+        const ulonglong2 v = *reinterpret_cast<const ulonglong2*>(src + r);
+        k[i][r] = v.x;
+        k[i][r + 1] = v.y;
+      }
+      if (RANK_LISTS) {
+        if (part == 0) {
+          const uint64_t u = base[(size_t)l * list_stride + kC];
+          ub_in = u > ub_in ? u : ub_in;
+        }
+      } else {
+        uint64_t mn = ~0ull;
+        int cnt = 0;
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          cnt += k[i][r] != 0;
+          mn = (k[i][r] && k[i][r] < mn) ? k[i][r] : mn;
+        }
+        if (cnt == 8) ub_in = mn > ub_in ? mn : ub_in;  // full tile list: unseen nodes < its minimum
+      }
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        nz += k[i][r] != 0;
+        kmax = k[i][r] > kmax ? k[i][r] : kmax;
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < 8; ++r) k[i][r] = 0;
+    }
+  }
+  // block reductions: Σ nz, max ub_in, max kmax
+  {
+    uint32_t s = nz;
+    for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off, kWave);
+    const uint64_t u = wave_max_u64(ub_in), m = wave_max_u64(kmax);
+    if (lane == 0) {
+      red32[wave] = s;
+      red64[wave] = u;
+      hist[wave] = (uint32_t)(m >> 32);
+      hist[8 + wave] = (uint32_t)m;
+    }
+    __syncthreads();
+    uint32_t tot = 0;
+    uint64_t ubm = 0, km = 0;
+    for (int w = 0; w < kMergeThreads / kWave; ++w) {
+      tot += red32[w];
+      ubm = red64[w] > ubm ? red64[w] : ubm;
+      const uint64_t mw = ((uint64_t)hist[w] << 32) | hist[8 + w];
+      km = mw > km ? mw : km;
+    }
+    nz = tot;
+    ub_in = ubm;
+    kmax = km;
+    __syncthreads();
+  }
+
+  uint64_t kth = 1;  // select every non-zero key when there are at most kC of them
+  if (nz > (uint32_t)kC) {
+    int top = 7;
+    while (top > 0 && ((kmax >> (8 * top)) & 0xFF) == 0) --top;  // bytes above kmax's leading byte are 0
+    uint64_t prefix = 0, pmask = 0;
+    uint32_t target = kC;
+    for (int byte = top; byte >= 0; --byte) {
+      const int shift = 8 * byte;
+      hist[tid] = 0;  // kMergeThreads == 256 bins
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < kMergeChunks; ++i)
+#pragma unroll
+        for (int r = 0; r < 8; ++r)
+          if (k[i][r] && (k[i][r] & pmask) == prefix) atomicAdd(&hist[(k[i][r] >> shift) & 0xFF], 1u);
+      __syncthreads();
+      if (wave == 0) {
+        // lane l holds bins 4l..4l+3; count of keys in bins above lane l's bins = suffix sum over higher lanes
+        uint32_t b[4], s = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          b[q] = hist[4 * lane + q];
+          s += b[q];
+        }
+        uint32_t incl = s;  // inclusive suffix sum over lanes ≥ l
+        for (int off = 1; off < kWave; off <<= 1) {
+          const uint32_t o = __shfl_down(incl, off, kWave);
+          if (lane + off < kWave) incl += o;
+        }
+        uint32_t above = incl - s;  // keys in bins of lanes > l
+#pragma unroll
+        for (int q = 3; q >= 0; --q) {
+          if (above < target && above + b[q] >= target) {
+            sh_prefix = prefix | ((uint64_t)(4 * lane + q) << shift);
+            sh_target = target - above;
+          }
+          above += b[q];
+        }
+      }
+      __syncthreads();
+      prefix = sh_prefix;
+      target = sh_target;
+      pmask |= 0xFFull << shift;
+      __syncthreads();
+    }
+    kth = prefix;
+  }
+  // compaction of the selected keys + the best key left out
+  if (tid == 0) sh_nsel = 0;
+  if (tid < kC) sel[tid] = 0;
+  __syncthreads();
+  uint64_t next = 0;
+#pragma unroll
+  for (int i = 0; i < kMergeChunks; ++i)
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const uint64_t v = k[i][r];
+      if (v >= kth && v) sel[atomicAdd(&sh_nsel, 1u)] = v;
+      else if (v) next = v > next ? v : next;
+    }
+  next = wave_max_u64(next);
+  if (lane == 0) red64[wave] = next;
+  __syncthreads();
+  uint64_t* o = out + (size_t)pod * kCandStride;
+  if (wave == 0) {
+    uint64_t nx = 0;
+    for (int w = 0; w < kMergeThreads / kWave; ++w) nx = red64[w] > nx ? red64[w] : nx;
+    // rank sort of the ≤ kC selected keys (unique): position = number of larger keys
+    const uint64_t v = sel[lane];
+    int rank = 0;
+    for (int q = 0; q < kC; ++q) rank += sel[q] > v;
+    const int n_sel = (int)sh_nsel;
+    if (lane < n_sel) o[rank] = v;
+    else o[lane] = 0;  // positions ≥ n_sel
+    if (lane == 0) {
+      const uint64_t ub_sel = nx ? nx + 1 : 0;
+      o[kC] = ub_in > ub_sel ? ub_in : ub_sel;
+    }
+  }
+}
+
+// ---- round kernel 3: FIFO resolve --------------------------------------------------------------------
+// One wavefront replays the round's pods in queue order against the merged candidates.  Lane l < nM keeps
+// modified row l in registers; an LDS bitmap marks modified node indices.  Per pod:
+//   e     = the best candidate not modified in this round (ballot + ctz over the sorted list);
+//   mbest = the exact re-score of the modified rows — skipped when the profile is monotone (assume never raises
+//           a node's key) and e is the pod's top candidate;
+//   valid iff max(e, mbest) ≥ ub: every node outside the list scores lower.  Otherwise the round ends here.
+// Writes out_keys[cursor + j] (0 = unschedulable), the modified rows back, and advances the cursor.
 __global__ __launch_bounds__(kWave) void resolve_round(DevTable T, const DevPod* __restrict__ pods,
                                                         int64_t* __restrict__ cursor_p, int64_t end, int B,
-                                                        int n_ranks, int nt_local,
-                                                        const uint64_t* __restrict__ lists, EvalParams P,
+                                                        const uint64_t* __restrict__ cand, EvalParams P,
                                                         uint64_t* __restrict__ out_keys, int bitmap_words,
                                                         int64_t* __restrict__ round_stats) {
   extern __shared__ uint32_t bitmap[];
@@ -176,52 +361,34 @@ __global__ __launch_bounds__(kWave) void resolve_round(DevTable T, const DevPod*
   uint32_t midx = 0xFFFFFFFFu;
   int nM = 0;
   int consumed = 0;
-  const int nt_total = n_ranks * nt_local;
+  uint64_t key_next = cand[lane];
+  uint64_t ub_next = cand[kC];
+  DevPod pod_next = pods[cursor];
   for (int j = 0; j < nb; ++j) {
-    const DevPod p = pods[cursor + j];
-    uint64_t best = 0, bound = 0;
-    for (int g = lane; g < nt_total; g += kWave) {
-      const int rk = g / nt_local, t = g - rk * nt_local;
-      const uint64_t* L = lists + (((size_t)rk * B + j) * nt_local + t) * kR;
-      uint64_t k[kR];
-#pragma unroll
-      for (int r = 0; r < kR; r += 2) {
-        const ulonglong2 v = *reinterpret_cast<const ulonglong2*>(L + r);
-        k[r] = v.x;
-        k[r + 1] = v.y;
-      }
-      uint64_t bu = 0, mn = ~0ull;
-      int cnt = 0;
-      bool any_unmod = false;
-#pragma unroll
-      for (int r = 0; r < kR; ++r) {
-        if (k[r]) {
-          ++cnt;
-          const uint32_t n = key_node(k[r]);
-          const bool mod = (bitmap[n >> 5] >> (n & 31)) & 1u;
-          if (!mod) {
-            any_unmod = true;
-            bu = k[r] > bu ? k[r] : bu;
-          }
-          mn = k[r] < mn ? k[r] : mn;
-        }
-      }
-      best = bu > best ? bu : best;
-      if (cnt == kR && !any_unmod) bound = mn > bound ? mn : bound;  // tile remainder unknown, keys < mn
+    const uint64_t key = key_next, ub = ub_next;
+    const DevPod p = pod_next;
+    if (j + 1 < nb) {  // prefetch the next pod's candidates and descriptor
+      key_next = cand[(size_t)(j + 1) * kCandStride + lane];
+      ub_next = cand[(size_t)(j + 1) * kCandStride + kC];
+      pod_next = pods[cursor + j + 1];
     }
-    if (lane < nM) {
+    const uint32_t node = key ? key_node(key) : 0;
+    const bool mod = key && ((bitmap[node >> 5] >> (node & 31)) & 1u);
+    const uint64_t um = __ballot(key != 0 && !mod);
+    const int pos = um ? (int)__builtin_ctzll(um) : kC;
+    const uint64_t e = um ? readlane_u64(key, pos) : 0;
+    uint64_t best = e;
+    if (nM > 0 && (!P.monotone || pos > 0)) {
+      uint64_t mk = 0;
       int64_t t = 0;
-      if (eval_node(mrow, p, P, t)) {
-        const uint64_t kk = make_key(t, midx);
-        best = kk > best ? kk : best;
-      }
+      if (lane < nM && eval_node(mrow, p, P, t)) mk = make_key(t, midx);
+      const uint64_t mbest = wave_max_u64_dpp(mk);
+      best = mbest > best ? mbest : best;
     }
-    best = wave_max_u64(best);
-    bound = wave_max_u64(bound);
-    if (best < bound || (best == 0 && bound != 0)) break;  // decision not provable from this round's lists
+    if (best < ub) break;  // an unseen node could still win: leave this pod to the next round
     if (lane == 0) out_keys[cursor + j] = best;
     ++consumed;
-    if (best == 0) continue;  // unschedulable: no state change
+    if (best == 0) continue;  // unschedulable (ub == 0: no feasible node anywhere)
     const uint32_t w = key_node(best);
     const uint64_t hit = __ballot(lane < nM && midx == w);
     if (hit) {
@@ -278,6 +445,24 @@ __global__ void apply_deltas(DevTable T, const RowDelta* __restrict__ d, int64_t
   atomicAdd((unsigned long long*)&T.la_used_mem[k], (unsigned long long)x.d[6]);
   atomicAdd((unsigned long long*)&T.la_pused_cpu[k], (unsigned long long)x.d[7]);
   atomicAdd((unsigned long long*)&T.la_pused_mem[k], (unsigned long long)x.d[8]);
+}
+
+// Both evaluation paths on every (pod, node): eval_node (reference-shaped) vs eval_fast (hoisted terms).
+__global__ void debug_eval_paths(DevTable T, const DevPod* __restrict__ pods, int64_t n_pods, int64_t n,
+                                 EvalParams P, unsigned long long* __restrict__ mismatches) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const Row r = load_row(T, i);
+  const EvalRow er = make_eval_row(r, P);
+  unsigned long long bad = 0;
+  for (int64_t k = 0; k < n_pods; ++k) {
+    int64_t t1 = 0;
+    uint32_t t2 = 0;
+    const bool f1 = eval_node(r, pods[k], P, t1);
+    const bool f2 = eval_fast(er, pods[k], P, t2);
+    bad += (f1 != f2) || (f1 && (uint32_t)t1 != t2);
+  }
+  if (bad) atomicAdd(mismatches, bad);
 }
 
 __global__ void debug_least_requested(const int64_t* req, const int64_t* cap, int64_t* out, int64_t n) {
@@ -338,7 +523,9 @@ struct kg_engine {
   DevBuf<int32_t> cols32;
   DevBuf<DevPod> pods;
   int64_t n_staged = 0;
-  DevBuf<uint64_t> lists;
+  DevBuf<uint64_t> lists;     // [B][nt_local][kR] tile candidate lists (this rank)
+  DevBuf<uint64_t> gathered;  // [n_ranks][B][kCandStride] per-rank merged records (n_ranks > 1)
+  DevBuf<uint64_t> cand;      // [B][kCandStride] final merged candidates
   DevBuf<uint64_t> out_keys;
   DevBuf<int64_t> cursor;  // [0] cursor, [1] rounds, [2] consumed
   DevBuf<RowDelta> deltas;
@@ -569,19 +756,45 @@ RoundGeom geometry(const kg_engine* e) {
   return g;
 }
 
+dim3 eval_grid(const RoundGeom& g) {
+  return dim3((unsigned)((g.nt_local + kEvalWaves - 1) / kEvalWaves), (unsigned)((g.B + g.ppw - 1) / g.ppw));
+}
+
+void launch_eval(kg_engine* e, const RoundGeom& g, int64_t end) {
+  eval_round<<<eval_grid(g), kWave * kEvalWaves, 0, e->stream>>>(e->T, e->pods.p, e->cursor.p, end, g.B, g.ppw,
+                                                                  g.base, g.n_local, g.nt_local, e->P, e->lists.p);
+}
+
+// local merge: this rank's tile lists → per-pod record (single rank: the final candidates)
+void launch_merge_local(kg_engine* e, const RoundGeom& g, int64_t end) {
+  uint64_t* dst = e->n_ranks > 1 ? e->gathered.p + (size_t)e->rank * g.B * kCandStride : e->cand.p;
+  merge_round<false><<<g.B, kMergeThreads, 0, e->stream>>>(e->lists.p, (int64_t)g.nt_local * kR, kR, g.nt_local, kR,
+                                                           e->cursor.p, end, g.B, dst);
+}
+
+void launch_merge_ranks(kg_engine* e, const RoundGeom& g, int64_t end) {
+  merge_round<true><<<g.B, kMergeThreads, 0, e->stream>>>(e->gathered.p, kCandStride, (int64_t)g.B * kCandStride,
+                                                          e->n_ranks, kC, e->cursor.p, end, g.B, e->cand.p);
+}
+
+void launch_resolve(kg_engine* e, const RoundGeom& g, int64_t end) {
+  resolve_round<<<1, kWave, g.bitmap_words * 4, e->stream>>>(e->T, e->pods.p, e->cursor.p, end, g.B, e->cand.p,
+                                                              e->P, e->out_keys.p, g.bitmap_words, e->cursor.p + 1);
+}
+
 int launch_round(kg_engine* e, const RoundGeom& g, int64_t end) {
-  uint64_t* my_lists = e->lists.p + (size_t)e->rank * g.B * g.nt_local * kR;
-  dim3 grid((g.nt_local + kEvalWaves - 1) / kEvalWaves, (g.B + g.ppw - 1) / g.ppw);
-  eval_round<<<grid, kWave * kEvalWaves, 0, e->stream>>>(e->T, e->pods.p, e->cursor.p, end, g.B, g.ppw, g.base,
-                                                          g.n_local, g.nt_local, e->P, my_lists);
+  launch_eval(e, g, end);
+  HIP_TRY(hipGetLastError());
+  launch_merge_local(e, g, end);
   HIP_TRY(hipGetLastError());
   if (e->n_ranks > 1) {
-    const size_t cnt = (size_t)g.B * g.nt_local * kR;
-    NCCL_TRY(ncclAllGather(my_lists, e->lists.p, cnt, ncclUint64, e->comm, e->stream));
+    const size_t cnt = (size_t)g.B * kCandStride;
+    uint64_t* mine = e->gathered.p + (size_t)e->rank * cnt;
+    NCCL_TRY(ncclAllGather(mine, e->gathered.p, cnt, ncclUint64, e->comm, e->stream));
+    launch_merge_ranks(e, g, end);
+    HIP_TRY(hipGetLastError());
   }
-  resolve_round<<<1, kWave, g.bitmap_words * 4, e->stream>>>(e->T, e->pods.p, e->cursor.p, end, g.B, e->n_ranks,
-                                                              g.nt_local, e->lists.p, e->P, e->out_keys.p,
-                                                              g.bitmap_words, e->cursor.p + 1);
+  launch_resolve(e, g, end);
   HIP_TRY(hipGetLastError());
   return 0;
 }
@@ -590,7 +803,13 @@ int prepare_rounds(kg_engine* e, RoundGeom& g) {
   if (int rc = sync_static(e)) return rc;
   g = geometry(e);
   if (g.N > kMaxNodes) return fail(KG_E_UNSUPPORTED, "n_nodes %lld > %lld", (long long)g.N, (long long)kMaxNodes);
-  if (int rc = e->lists.ensure((size_t)e->n_ranks * g.B * g.nt_local * kR)) return rc;
+  if (g.nt_local > kMergeThreads * kMergeChunks)
+    return fail(KG_E_UNSUPPORTED, "%lld nodes per rank exceed one merge block (%d)", (long long)g.shard,
+                kMergeThreads * kMergeChunks * kTile);
+  if (int rc = e->lists.ensure((size_t)g.B * g.nt_local * kR)) return rc;
+  if (int rc = e->cand.ensure((size_t)g.B * kCandStride)) return rc;
+  if (e->n_ranks > 1)
+    if (int rc = e->gathered.ensure((size_t)e->n_ranks * g.B * kCandStride)) return rc;
   return 0;
 }
 
@@ -716,6 +935,8 @@ int kg_engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank, int
   e->P.la_score = (int)(c.la_score != 0);
   const int64_t max_total = 100 * ((c.fit_score ? c.weight_fit : 0) + (c.la_score ? c.weight_loadaware : 0));
   e->P.score_bits = (int32_t)bits_for(max_total);
+  e->P.monotone = 1;  // NodeResourcesFit + LoadAwareScheduling: assume only lowers a node's key
+  e->P.inv_la_wsum = 1.0f / (float)e->P.la_wsum;
   if (hipFuncSetAttribute((const void*)resolve_round, hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)(kMaxNodes / 8)) != hipSuccess)
     return bail(fail(KG_E_DEVICE, "hipFuncSetAttribute(resolve_round LDS)"));
@@ -736,6 +957,8 @@ void kg_engine_destroy(kg_engine* e) {
   e->cols32.release();
   e->pods.release();
   e->lists.release();
+  e->gathered.release();
+  e->cand.release();
   e->out_keys.release();
   e->cursor.release();
   e->deltas.release();
@@ -970,73 +1193,82 @@ int kg_nodes_read_state(kg_engine* e, int64_t* req_cpu, int64_t* req_mem, int64_
 }
 
 int kg_bench_kernel(kg_engine* e, int which, int iters, double* avg_ms, double* algo_bytes) {
-  if (!e || iters <= 0) return fail(KG_E_INVALID, "bad argument");
+  if (!e || iters <= 0 || which < 0 || which > 2) return fail(KG_E_INVALID, "bad argument");
   if (e->n_staged <= 0) return fail(KG_E_INVALID, "stage a pod queue first");
   RoundGeom g;
   if (int rc = prepare_rounds(e, g)) return rc;
   const int64_t end = std::min<int64_t>(e->n_staged, g.B);
-  // snapshot mutable columns so that replays of the resolver leave the table unchanged
+  // snapshot the mutable columns: the resolver writes rows back, replays must start from the same state
   const size_t bytes64 = (size_t)e->capacity * 8;
   DevBuf<int64_t> save;
   if (int rc = save.ensure(9 * e->capacity)) return rc;
   int64_t* mut64[8] = {e->T.req_cpu, e->T.req_mem, e->T.nz_cpu, e->T.nz_mem,
                        e->T.la_used_cpu, e->T.la_used_mem, e->T.la_pused_cpu, e->T.la_pused_mem};
-  for (int k = 0; k < 8; ++k)
-    HIP_TRY(hipMemcpyAsync(save.p + k * e->capacity, mut64[k], bytes64, hipMemcpyDeviceToDevice, e->stream));
-  HIP_TRY(hipMemcpyAsync(save.p + 8 * e->capacity, e->T.num_pods, e->capacity * 4, hipMemcpyDeviceToDevice, e->stream));
-  int64_t zero3[3] = {0, 0, 0};
+  auto snapshot = [&](bool restore) -> int {
+    for (int k = 0; k < 8; ++k) {
+      int64_t* a = save.p + k * e->capacity;
+      HIP_TRY(hipMemcpyAsync(restore ? mut64[k] : a, restore ? a : mut64[k], bytes64, hipMemcpyDeviceToDevice, e->stream));
+    }
+    int32_t* a = (int32_t*)(save.p + 8 * e->capacity);
+    HIP_TRY(hipMemcpyAsync(restore ? e->T.num_pods : a, restore ? a : e->T.num_pods, e->capacity * 4,
+                           hipMemcpyDeviceToDevice, e->stream));
+    return 0;
+  };
+  static const int64_t zero3[3] = {0, 0, 0};
+  if (int rc = snapshot(false)) return rc;
   HIP_TRY(hipMemcpyAsync(e->cursor.p, zero3, 24, hipMemcpyHostToDevice, e->stream));
-  // one real round so the lists are valid for the resolver replay, then undo its write-back
-  if (int rc = launch_round(e, g, end)) return rc;
-  for (int k = 0; k < 8; ++k)
-    HIP_TRY(hipMemcpyAsync(mut64[k], save.p + k * e->capacity, bytes64, hipMemcpyDeviceToDevice, e->stream));
-  HIP_TRY(hipMemcpyAsync(e->T.num_pods, save.p + 8 * e->capacity, e->capacity * 4, hipMemcpyDeviceToDevice, e->stream));
-  HIP_TRY(hipMemcpyAsync(e->cursor.p, zero3, 24, hipMemcpyHostToDevice, e->stream));
+  if (int rc = launch_round(e, g, end)) return rc;  // one real round: valid lists and candidates to replay on
+  if (int rc = snapshot(true)) return rc;
   hipEvent_t a, b;
   HIP_TRY(hipEventCreate(&a));
   HIP_TRY(hipEventCreate(&b));
-  uint64_t* my_lists = e->lists.p + (size_t)e->rank * g.B * g.nt_local * kR;
-  dim3 grid((g.nt_local + kEvalWaves - 1) / kEvalWaves, (g.B + g.ppw - 1) / g.ppw);
   float total_ms = 0.f;
   for (int it = 0; it < iters; ++it) {
     HIP_TRY(hipMemcpyAsync(e->cursor.p, zero3, 24, hipMemcpyHostToDevice, e->stream));
     HIP_TRY(hipEventRecord(a, e->stream));
-    if (which == 0) {
-      eval_round<<<grid, kWave * kEvalWaves, 0, e->stream>>>(e->T, e->pods.p, e->cursor.p, end, g.B, g.ppw, g.base,
-                                                              g.n_local, g.nt_local, e->P, my_lists);
-    } else {
-      resolve_round<<<1, kWave, g.bitmap_words * 4, e->stream>>>(e->T, e->pods.p, e->cursor.p, end, g.B, e->n_ranks,
-                                                                  g.nt_local, e->lists.p, e->P, e->out_keys.p,
-                                                                  g.bitmap_words, e->cursor.p + 1);
-    }
+    if (which == 0) launch_eval(e, g, end);
+    else if (which == 1) launch_merge_local(e, g, end);
+    else launch_resolve(e, g, end);
+    HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(b, e->stream));
     HIP_TRY(hipEventSynchronize(b));
     float ms = 0.f;
     HIP_TRY(hipEventElapsedTime(&ms, a, b));
     total_ms += ms;
-    if (which == 1) {  // undo the resolver's write-back
-      for (int k = 0; k < 8; ++k)
-        HIP_TRY(hipMemcpyAsync(mut64[k], save.p + k * e->capacity, bytes64, hipMemcpyDeviceToDevice, e->stream));
-      HIP_TRY(hipMemcpyAsync(e->T.num_pods, save.p + 8 * e->capacity, e->capacity * 4, hipMemcpyDeviceToDevice, e->stream));
-    }
+    if (which == 2)
+      if (int rc = snapshot(true)) return rc;
   }
-  for (int k = 0; k < 8; ++k)
-    HIP_TRY(hipMemcpyAsync(mut64[k], save.p + k * e->capacity, bytes64, hipMemcpyDeviceToDevice, e->stream));
-  HIP_TRY(hipMemcpyAsync(e->T.num_pods, save.p + 8 * e->capacity, e->capacity * 4, hipMemcpyDeviceToDevice, e->stream));
   HIP_TRY(hipStreamSynchronize(e->stream));
   (void)hipEventDestroy(a);
   (void)hipEventDestroy(b);
   save.release();
-  const int nb = (int)end;
+  const double nb = (double)end;
   if (avg_ms) *avg_ms = total_ms / iters;
   if (algo_bytes) {
-    // eval: node columns read once per pod group (92 B/node: Fit 56 + LoadAware 32 + flags 4) + lists written;
-    // resolve: every rank's lists read once per pod + pod descriptors.
-    const double groups = std::ceil((double)nb / g.ppw);
-    const double list_bytes = (double)nb * g.nt_local * e->n_ranks * kR * 8;
-    if (which == 0) *algo_bytes = groups * (double)g.n_local * 92.0 + (double)nb * g.nt_local * kR * 8 + nb * 56.0;
-    else *algo_bytes = list_bytes + nb * 56.0;
+    // eval: SURVEY §8(d) per-evaluation bytes (Fit 56 B + LoadAware 36 B = 92 B per node) × pods × nodes,
+    //       + the candidate lists written;  merge: lists read + records written;  resolve: records + pods read.
+    if (which == 0) *algo_bytes = nb * (double)g.n_local * 92.0 + nb * g.nt_local * kR * 8.0 + nb * 56.0;
+    else if (which == 1) *algo_bytes = nb * g.nt_local * kR * 8.0 + nb * kCandStride * 8.0;
+    else *algo_bytes = nb * kCandStride * 8.0 + nb * 56.0;
   }
+  return 0;
+}
+
+int kg_debug_eval_paths(kg_engine* e, int64_t* mismatches) {
+  if (!e || !mismatches) return fail(KG_E_INVALID, "bad argument");
+  if (int rc = sync_static(e)) return rc;
+  if (e->n_staged <= 0) return fail(KG_E_INVALID, "stage a pod queue first");
+  DevBuf<int64_t> b;
+  if (int rc = b.ensure(1)) return rc;
+  HIP_TRY(hipMemsetAsync(b.p, 0, 8, e->stream));
+  const int64_t n = e->n_nodes;
+  if (n > 0)
+    debug_eval_paths<<<(unsigned)((n + 255) / 256), 256, 0, e->stream>>>(e->T, e->pods.p, e->n_staged, n, e->P,
+                                                                         (unsigned long long*)b.p);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(mismatches, b.p, 8, hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  b.release();
   return 0;
 }
 

@@ -54,7 +54,9 @@ struct EvalParams {
   int64_t weight_fit, weight_la;
   int32_t fit_filter, fit_score, la_filter, la_score;
   int32_t score_bits;  // bit width of the largest possible weighted total
-  int32_t pad;
+  int32_t monotone;    // every enabled plugin's key can only drop when a pod is assumed (Fit, LoadAware)
+  float inv_la_wsum;
+  int32_t pad2;
 };
 
 struct Row {
@@ -202,6 +204,138 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
     v = o > v ? o : v;
   }
   return v;
+}
+
+// DPP max-reduction over the wave (gfx9 row_shr 1/2/4/8, row_bcast 15/31): result valid in lane 63,
+// returned wave-uniform via readlane.  Lanes whose DPP source is out of row read the identity 0.
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ uint64_t dpp_u64(uint64_t v) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)v, CTRL, ROW_MASK, 0xf, false);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(v >> 32), CTRL, ROW_MASK, 0xf, false);
+  return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t wave_max_u64_dpp(uint64_t v) {
+  uint64_t w;
+  w = dpp_u64<0x111, 0xf>(v); v = w > v ? w : v;  // row_shr:1
+  w = dpp_u64<0x112, 0xf>(v); v = w > v ? w : v;  // row_shr:2
+  w = dpp_u64<0x114, 0xf>(v); v = w > v ? w : v;  // row_shr:4
+  w = dpp_u64<0x118, 0xf>(v); v = w > v ? w : v;  // row_shr:8
+  w = dpp_u64<0x142, 0xa>(v); v = w > v ? w : v;  // row_bcast:15
+  w = dpp_u64<0x143, 0xc>(v); v = w > v ? w : v;  // row_bcast:31
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, 63);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), 63);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+__device__ __forceinline__ uint64_t readlane_u64(uint64_t v, int lane) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, lane);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), lane);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+}  // namespace kg
+
+namespace kg {
+
+// ---------------------------------------------------------------------------------------------------
+// Wide-pass evaluation with per-node terms hoisted out of the per-pod loop.  Must agree bit-for-bit with
+// eval_node (checked on the device by kg_debug_eval_paths).
+// ---------------------------------------------------------------------------------------------------
+struct EvalRow {
+  int64_t free_cpu, free_mem;          // Allocatable - Requested                 (fitsRequest)
+  int64_t alloc_cpu, alloc_mem;        // LeastAllocated capacity
+  int64_t fnz_cpu, fnz_mem;            // Allocatable - NonZeroRequested
+  int64_t la_alloc_cpu, la_alloc_mem;  // EstimateNode
+  int64_t la_free_cpu, la_free_mem;    // la_alloc - la_used      (non-prod view)
+  int64_t la_pfree_cpu, la_pfree_mem;  // la_alloc - la_pused     (prod view)
+  float inv_cpu, inv_mem, la_inv_cpu, la_inv_mem;  // 100 / capacity
+  float inv_fit_ws;                    // 1 / Σ fit weights of resources with non-zero allocatable
+  int32_t fit_ws;
+  int32_t pods_left;                   // AllowedPodNumber - len(Pods) - 1  (fits iff ≥ 0)
+  uint32_t flags;
+};
+
+__device__ __forceinline__ float i64_to_f32(int64_t x) {  // x ≥ 0; ~1 ulp, enough for a ±1 quotient estimate
+  const uint64_t u = (uint64_t)x;
+  return fmaf((float)(uint32_t)(u >> 32), 4294967296.0f, (float)(uint32_t)u);
+}
+
+__device__ __forceinline__ float inv100(int64_t cap) { return cap > 0 ? 100.0f / i64_to_f32(cap) : 0.0f; }
+
+__device__ __forceinline__ EvalRow make_eval_row(const Row& r, const EvalParams& P) {
+  EvalRow e;
+  e.free_cpu = r.alloc_cpu - r.req_cpu;
+  e.free_mem = r.alloc_mem - r.req_mem;
+  e.alloc_cpu = r.alloc_cpu;
+  e.alloc_mem = r.alloc_mem;
+  e.fnz_cpu = r.alloc_cpu - r.nz_cpu;
+  e.fnz_mem = r.alloc_mem - r.nz_mem;
+  e.la_alloc_cpu = r.la_alloc_cpu;
+  e.la_alloc_mem = r.la_alloc_mem;
+  e.la_free_cpu = r.la_alloc_cpu - r.la_used_cpu;
+  e.la_free_mem = r.la_alloc_mem - r.la_used_mem;
+  e.la_pfree_cpu = r.la_alloc_cpu - r.la_pused_cpu;
+  e.la_pfree_mem = r.la_alloc_mem - r.la_pused_mem;
+  e.inv_cpu = inv100(r.alloc_cpu);
+  e.inv_mem = inv100(r.alloc_mem);
+  e.la_inv_cpu = inv100(r.la_alloc_cpu);
+  e.la_inv_mem = inv100(r.la_alloc_mem);
+  int32_t ws = 0;
+  if (P.fit_w_cpu && r.alloc_cpu != 0) ws += (int32_t)P.fit_w_cpu;
+  if (P.fit_w_mem && r.alloc_mem != 0) ws += (int32_t)P.fit_w_mem;
+  e.fit_ws = ws;
+  e.inv_fit_ws = ws ? 1.0f / (float)ws : 0.0f;
+  e.pods_left = r.alloc_pods - r.num_pods - 1;
+  e.flags = r.flags;
+  return e;
+}
+
+// leastRequestedScore with x = capacity - requested precomputed: ((x * 100) / capacity), 0 if x < 0.
+__device__ __forceinline__ int64_t lrs_x(int64_t x, int64_t cap, float inv) {
+  if (cap == 0 || x < 0) return 0;
+  const int64_t num = x * 100;
+  if (x > cap) return num / cap;  // requested < 0: outside [0,100], exact slow path
+  int q = (int)(i64_to_f32(x) * inv);
+  q = q < 0 ? 0 : (q > 100 ? 100 : q);
+  const int64_t t = (int64_t)q * cap;
+  if (t > num) --q;
+  else if (t + cap <= num) ++q;
+  return q;
+}
+
+// s / w for 0 ≤ s ≤ 100·w (w ≤ 2·10⁶, so s < 2^28 is exact in f32's integer range + one correction step)
+__device__ __forceinline__ int32_t div_est(int32_t s, int32_t w, float inv_w) {
+  int q = (int)((float)s * inv_w);
+  const int32_t t = q * w;
+  if (t > s) --q;
+  else if (t + w <= s) ++q;
+  return q;
+}
+
+__device__ __forceinline__ bool eval_fast(const EvalRow& n, const DevPod& p, const EvalParams& P, uint32_t& total) {
+  bool ok = (n.flags & F_VALID) != 0;
+  if (P.fit_filter) {
+    ok &= n.pods_left >= 0;
+    if (!(p.flags & P_ZERO_REQ)) ok &= (p.req_cpu <= n.free_cpu) & (p.req_mem <= n.free_mem);
+  }
+  if (P.la_filter && !(p.flags & P_DAEMONSET)) ok &= (n.flags & ((p.flags & P_PROD) ? F_LA_PASS_PROD : F_LA_PASS)) != 0;
+  if (!ok) return false;
+  int32_t t = 0;
+  if (P.fit_score && n.fit_ws) {
+    int32_t s = 0;
+    if (P.fit_w_cpu) s += (int32_t)lrs_x(n.fnz_cpu - p.nz_cpu, n.alloc_cpu, n.inv_cpu) * (int32_t)P.fit_w_cpu;
+    if (P.fit_w_mem) s += (int32_t)lrs_x(n.fnz_mem - p.nz_mem, n.alloc_mem, n.inv_mem) * (int32_t)P.fit_w_mem;
+    t += div_est(s, n.fit_ws, n.inv_fit_ws) * (int32_t)P.weight_fit;
+  }
+  if (P.la_score && (n.flags & F_LA_SCORE)) {
+    const bool prodv = (p.flags & P_LA_PROD_SCORE) != 0;
+    int32_t s = 0;
+    if (P.la_w_cpu) s += (int32_t)lrs_x((prodv ? n.la_pfree_cpu : n.la_free_cpu) - p.est_cpu, n.la_alloc_cpu, n.la_inv_cpu) * (int32_t)P.la_w_cpu;
+    if (P.la_w_mem) s += (int32_t)lrs_x((prodv ? n.la_pfree_mem : n.la_free_mem) - p.est_mem, n.la_alloc_mem, n.la_inv_mem) * (int32_t)P.la_w_mem;
+    t += div_est(s, (int32_t)P.la_wsum, P.inv_la_wsum) * (int32_t)P.weight_la;
+  }
+  total = (uint32_t)t;
+  return true;
 }
 
 }  // namespace kg

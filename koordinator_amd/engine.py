@@ -146,6 +146,11 @@ class Engine:
         check(self.lib, self.lib.kg_bench_kernel(self.h, int(which), int(iters), ctypes.byref(ms), ctypes.byref(by)))
         return ms.value, by.value
 
+    def debug_eval_paths(self) -> int:
+        out = np.zeros(1, dtype=np.int64)
+        check(self.lib, self.lib.kg_debug_eval_paths(self.h, ptr(out)))
+        return int(out[0])
+
     def debug_least_requested(self, requested, capacity):
         requested = np.ascontiguousarray(requested, dtype=np.int64)
         capacity = np.ascontiguousarray(capacity, dtype=np.int64)

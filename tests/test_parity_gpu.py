@@ -265,3 +265,24 @@ def test_c2_scale_properties():
     np.testing.assert_array_equal(st["requested_cpu"], (base + add).astype(np.int64))
     assert (st["requested_cpu"] <= cl.nodes["allocatable"][:, 0]).all()
     assert (st["num_pods"] <= 110).all()
+
+
+def test_eval_paths_agree():
+    """The wide pass's hoisted-term evaluation equals the reference-shaped one on every (pod, node)."""
+    for la, prof in [(framework.LoadAwareSchedulingArgs(), framework.Profile()),
+                     (framework.LoadAwareSchedulingArgs(resource_weights={"cpu": 7, "memory": 3},
+                                                        score_according_prod_usage=True),
+                      framework.Profile(score={framework.NODE_RESOURCES_FIT: 3, framework.LOAD_AWARE: 11}))]:
+        cfg = framework.build_config(la=la, profile=prof)
+        cl = synth.make_cluster(3000, seed=91, invalid_frac=0.05)
+        cl.nodes["raw_allocatable"][::4, :2] = cl.nodes["allocatable"][::4, :2] // 2
+        cl.nodes["raw_allocatable_present"][::4, :2] = 1
+        cl.nodes["flags"][::4] |= abi.NODE_HAS_RAW_ALLOCATABLE
+        cl.nodes["allocatable"][::17, abi.RES_MEMORY] = 0
+        with _engine(cfg, cl) as e:
+            e.schedule(synth.make_pods(2000, seed=92))  # mutate the table
+            p = synth.make_pods(200, seed=93)
+            p["requests"][::9] = 0
+            p["flags"][::5] = abi.POD_DAEMONSET
+            e.stage(p)
+            assert e.debug_eval_paths() == 0
