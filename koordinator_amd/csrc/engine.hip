@@ -40,7 +40,7 @@ constexpr int kC = 64;                // merged candidates per pod (> any modifi
 constexpr int kCandStride = 72;       // per-pod record: kC keys, ub, padding to a 64-B multiple
 constexpr int kMergeThreads = 256;
 constexpr int kMergeChunks = 4;       // chunks of 8 keys per merge thread: ≤ 1024 tile lists = 262144 nodes per rank
-constexpr int64_t kMaxNodes = 1 << 20;  // resolver bitmap lives in LDS: N/8 bytes ≤ 128 KiB
+constexpr int64_t kMaxNodes = 3 << 18;  // resolver LDS: N/8-byte bitmap (≤ 96 KiB) + the round's records (≤ 40 KiB)
 
 thread_local std::string g_err;
 
@@ -172,7 +172,7 @@ __global__ __launch_bounds__(kMergeThreads) void merge_round(const uint64_t* __r
                                                              const int64_t* __restrict__ cursor_p, int64_t end,
                                                              int B, uint64_t* __restrict__ out) {
   __shared__ uint32_t hist[256];
-  __shared__ uint64_t sel[kC];
+  __shared__ __attribute__((aligned(16))) uint64_t sel[kC];
   __shared__ uint64_t red64[kMergeThreads / kWave];
   __shared__ uint32_t red32[kMergeThreads / kWave];
   __shared__ uint64_t sh_prefix;
@@ -230,9 +230,8 @@ __global__ __launch_bounds__(kMergeThreads) void merge_round(const uint64_t* __r
   }
   // block reductions: Σ nz, max ub_in, max kmax
   {
-    uint32_t s = nz;
-    for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off, kWave);
-    const uint64_t u = wave_max_u64(ub_in), m = wave_max_u64(kmax);
+    const uint32_t s = wave_sum_u32(nz);
+    const uint64_t u = wave_max_u64_dpp(ub_in), m = wave_max_u64_dpp(kmax);
     if (lane == 0) {
       red32[wave] = s;
       red64[wave] = u;
@@ -271,23 +270,18 @@ __global__ __launch_bounds__(kMergeThreads) void merge_round(const uint64_t* __r
           if (k[i][r] && (k[i][r] & pmask) == prefix) atomicAdd(&hist[(k[i][r] >> shift) & 0xFF], 1u);
       __syncthreads();
       if (wave == 0) {
-        // lane l holds bins 4l..4l+3; count of keys in bins above lane l's bins = suffix sum over higher lanes
+        // lane l holds digits 255-4l .. 252-4l (descending); keys with a higher digit sit in lanes < l
         uint32_t b[4], s = 0;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          b[q] = hist[4 * lane + q];
+          b[q] = hist[255 - 4 * lane - q];
           s += b[q];
         }
-        uint32_t incl = s;  // inclusive suffix sum over lanes ≥ l
-        for (int off = 1; off < kWave; off <<= 1) {
-          const uint32_t o = __shfl_down(incl, off, kWave);
-          if (lane + off < kWave) incl += o;
-        }
-        uint32_t above = incl - s;  // keys in bins of lanes > l
+        uint32_t above = wave_prefix_sum_u32(s) - s;
 #pragma unroll
-        for (int q = 3; q >= 0; --q) {
+        for (int q = 0; q < 4; ++q) {
           if (above < target && above + b[q] >= target) {
-            sh_prefix = prefix | ((uint64_t)(4 * lane + q) << shift);
+            sh_prefix = prefix | ((uint64_t)(255 - 4 * lane - q) << shift);
             sh_target = target - above;
           }
           above += b[q];
@@ -314,7 +308,7 @@ __global__ __launch_bounds__(kMergeThreads) void merge_round(const uint64_t* __r
       if (v >= kth && v) sel[atomicAdd(&sh_nsel, 1u)] = v;
       else if (v) next = v > next ? v : next;
     }
-  next = wave_max_u64(next);
+  next = wave_max_u64_dpp(next);
   if (lane == 0) red64[wave] = next;
   __syncthreads();
   uint64_t* o = out + (size_t)pod * kCandStride;
@@ -324,7 +318,12 @@ __global__ __launch_bounds__(kMergeThreads) void merge_round(const uint64_t* __r
     // rank sort of the ≤ kC selected keys (unique): position = number of larger keys
     const uint64_t v = sel[lane];
     int rank = 0;
-    for (int q = 0; q < kC; ++q) rank += sel[q] > v;
+    const ulonglong2* s2 = reinterpret_cast<const ulonglong2*>(sel);
+#pragma unroll
+    for (int q = 0; q < kC / 2; ++q) {
+      const ulonglong2 x = s2[q];  // broadcast LDS reads, all issued back to back
+      rank += (x.x > v) + (x.y > v);
+    }
     const int n_sel = (int)sh_nsel;
     if (lane < n_sel) o[rank] = v;
     else o[lane] = 0;  // positions ≥ n_sel
@@ -336,42 +335,80 @@ __global__ __launch_bounds__(kMergeThreads) void merge_round(const uint64_t* __r
 }
 
 // ---- round kernel 3: FIFO resolve --------------------------------------------------------------------
-// One wavefront replays the round's pods in queue order against the merged candidates.  Lane l < nM keeps
-// modified row l in registers; an LDS bitmap marks modified node indices.  Per pod:
+// One wavefront replays the round's pods in queue order against the merged candidates.  The round's candidate
+// records and pod descriptors are staged into LDS once (a single global-latency wait); the per-pod loop then
+// touches only LDS and registers.  Lane l < nM owns modified row l: its base row (loaded from HBM when the node
+// first wins, consumed lazily) plus the sum of the pods assumed onto it this round.  Per pod:
 //   e     = the best candidate not modified in this round (ballot + ctz over the sorted list);
 //   mbest = the exact re-score of the modified rows — skipped when the profile is monotone (assume never raises
 //           a node's key) and e is the pod's top candidate;
-//   valid iff max(e, mbest) ≥ ub: every node outside the list scores lower.  Otherwise the round ends here.
+//   valid iff max(e, mbest) ≥ ub (every node outside the list scores lower); otherwise the round ends here.
 // Writes out_keys[cursor + j] (0 = unschedulable), the modified rows back, and advances the cursor.
+struct PodDelta {
+  int64_t req_cpu, req_mem, nz_cpu, nz_mem, est_cpu, est_mem, pest_cpu, pest_mem;
+  int32_t pods;
+};
+
+__device__ __forceinline__ void add_delta(PodDelta& d, const DevPod& p) {
+  d.req_cpu += p.req_cpu;
+  d.req_mem += p.req_mem;
+  d.nz_cpu += p.nz_cpu;
+  d.nz_mem += p.nz_mem;
+  d.est_cpu += p.est_cpu;
+  d.est_mem += p.est_mem;
+  if (p.flags & P_PROD) {
+    d.pest_cpu += p.est_cpu;
+    d.pest_mem += p.est_mem;
+  }
+  d.pods += 1;
+}
+
+__device__ __forceinline__ Row with_delta(Row r, const PodDelta& d) {
+  r.req_cpu += d.req_cpu;
+  r.req_mem += d.req_mem;
+  r.nz_cpu += d.nz_cpu;
+  r.nz_mem += d.nz_mem;
+  r.la_used_cpu += d.est_cpu;
+  r.la_used_mem += d.est_mem;
+  r.la_pused_cpu += d.pest_cpu;
+  r.la_pused_mem += d.pest_mem;
+  r.num_pods += d.pods;
+  return r;
+}
+
 __global__ __launch_bounds__(kWave) void resolve_round(DevTable T, const DevPod* __restrict__ pods,
                                                         int64_t* __restrict__ cursor_p, int64_t end, int B,
                                                         const uint64_t* __restrict__ cand, EvalParams P,
                                                         uint64_t* __restrict__ out_keys, int bitmap_words,
                                                         int64_t* __restrict__ round_stats) {
-  extern __shared__ uint32_t bitmap[];
+  extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
   const int lane = threadIdx.x;
   const int64_t cursor = *cursor_p;
   if (cursor >= end) return;
   const int nb = (end - cursor) < (int64_t)B ? (int)(end - cursor) : B;
-  for (int w = lane; w < bitmap_words; w += kWave) bitmap[w] = 0;
+  uint64_t* s_cand = smem;                                              // [nb][kCandStride]
+  DevPod* s_pods = reinterpret_cast<DevPod*>(smem + (size_t)B * kCandStride);  // [nb]
+  uint32_t* bitmap = reinterpret_cast<uint32_t*>(smem + (size_t)B * kCandStride + (size_t)B * 7);
+  {
+    const ulonglong2* src = reinterpret_cast<const ulonglong2*>(cand);
+    ulonglong2* dst = reinterpret_cast<ulonglong2*>(s_cand);
+    for (int i = lane; i < nb * kCandStride / 2; i += kWave) dst[i] = src[i];
+    const uint64_t* ps = reinterpret_cast<const uint64_t*>(pods + cursor);
+    uint64_t* pd = reinterpret_cast<uint64_t*>(s_pods);
+    for (int i = lane; i < nb * 7; i += kWave) pd[i] = ps[i];
+    for (int w = lane; w < bitmap_words; w += kWave) bitmap[w] = 0;
+  }
   __syncthreads();
 
   Row mrow;
   mrow.flags = 0;
+  PodDelta dl = {};
   uint32_t midx = 0xFFFFFFFFu;
   int nM = 0;
   int consumed = 0;
-  uint64_t key_next = cand[lane];
-  uint64_t ub_next = cand[kC];
-  DevPod pod_next = pods[cursor];
   for (int j = 0; j < nb; ++j) {
-    const uint64_t key = key_next, ub = ub_next;
-    const DevPod p = pod_next;
-    if (j + 1 < nb) {  // prefetch the next pod's candidates and descriptor
-      key_next = cand[(size_t)(j + 1) * kCandStride + lane];
-      ub_next = cand[(size_t)(j + 1) * kCandStride + kC];
-      pod_next = pods[cursor + j + 1];
-    }
+    const uint64_t key = s_cand[(size_t)j * kCandStride + lane];
+    const uint64_t ub = s_cand[(size_t)j * kCandStride + kC];
     const uint32_t node = key ? key_node(key) : 0;
     const bool mod = key && ((bitmap[node >> 5] >> (node & 31)) & 1u);
     const uint64_t um = __ballot(key != 0 && !mod);
@@ -379,9 +416,10 @@ __global__ __launch_bounds__(kWave) void resolve_round(DevTable T, const DevPod*
     const uint64_t e = um ? readlane_u64(key, pos) : 0;
     uint64_t best = e;
     if (nM > 0 && (!P.monotone || pos > 0)) {
+      const DevPod p = s_pods[j];
       uint64_t mk = 0;
       int64_t t = 0;
-      if (lane < nM && eval_node(mrow, p, P, t)) mk = make_key(t, midx);
+      if (lane < nM && eval_node(with_delta(mrow, dl), p, P, t)) mk = make_key(t, midx);
       const uint64_t mbest = wave_max_u64_dpp(mk);
       best = mbest > best ? mbest : best;
     }
@@ -391,20 +429,21 @@ __global__ __launch_bounds__(kWave) void resolve_round(DevTable T, const DevPod*
     if (best == 0) continue;  // unschedulable (ub == 0: no feasible node anywhere)
     const uint32_t w = key_node(best);
     const uint64_t hit = __ballot(lane < nM && midx == w);
-    if (hit) {
-      if (lane == (int)__builtin_ctzll(hit)) apply_pod(mrow, p);
-    } else {
-      if (lane == nM) {
-        mrow = load_row(T, w);
+    const int owner = hit ? (int)__builtin_ctzll(hit) : nM;
+    if (lane == owner) {
+      if (!hit) {
+        mrow = load_row(T, w);  // consumed lazily: the fast path never waits for it
         midx = w;
-        apply_pod(mrow, p);
       }
+      add_delta(dl, s_pods[j]);
+    }
+    if (!hit) {
       if (lane == 0) bitmap[w >> 5] |= 1u << (w & 31);
       ++nM;
-      __syncthreads();
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // order the LDS bitmap write before later reads
     }
   }
-  if (lane < nM) store_mutable(T, midx, mrow);
+  if (lane < nM) store_mutable(T, midx, with_delta(mrow, dl));
   if (lane == 0) {
     *cursor_p = cursor + consumed;
     round_stats[0] += 1;
@@ -756,6 +795,10 @@ RoundGeom geometry(const kg_engine* e) {
   return g;
 }
 
+size_t resolve_lds_bytes(const RoundGeom& g) {
+  return (size_t)g.B * kCandStride * 8 + (size_t)g.B * sizeof(DevPod) + (size_t)g.bitmap_words * 4;
+}
+
 dim3 eval_grid(const RoundGeom& g) {
   return dim3((unsigned)((g.nt_local + kEvalWaves - 1) / kEvalWaves), (unsigned)((g.B + g.ppw - 1) / g.ppw));
 }
@@ -778,7 +821,7 @@ void launch_merge_ranks(kg_engine* e, const RoundGeom& g, int64_t end) {
 }
 
 void launch_resolve(kg_engine* e, const RoundGeom& g, int64_t end) {
-  resolve_round<<<1, kWave, g.bitmap_words * 4, e->stream>>>(e->T, e->pods.p, e->cursor.p, end, g.B, e->cand.p,
+  resolve_round<<<1, kWave, resolve_lds_bytes(g), e->stream>>>(e->T, e->pods.p, e->cursor.p, end, g.B, e->cand.p,
                                                               e->P, e->out_keys.p, g.bitmap_words, e->cursor.p + 1);
 }
 
@@ -938,7 +981,7 @@ int kg_engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank, int
   e->P.monotone = 1;  // NodeResourcesFit + LoadAwareScheduling: assume only lowers a node's key
   e->P.inv_la_wsum = 1.0f / (float)e->P.la_wsum;
   if (hipFuncSetAttribute((const void*)resolve_round, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)(kMaxNodes / 8)) != hipSuccess)
+                          (int)(kMaxNodes / 8 + kMaxB * (kCandStride * 8 + sizeof(DevPod)))) != hipSuccess)
     return bail(fail(KG_E_DEVICE, "hipFuncSetAttribute(resolve_round LDS)"));
   if (n_ranks > 1) {
     ncclUniqueId id;

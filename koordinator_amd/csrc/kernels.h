@@ -227,6 +227,24 @@ __device__ __forceinline__ uint64_t wave_max_u64_dpp(uint64_t v) {
   return ((uint64_t)hi << 32) | lo;
 }
 
+// Inclusive prefix sum over the wave in lane order (DPP row_shr 1/2/4/8 + row_bcast 15/31).
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROW_MASK, 0xf, false);
+}
+__device__ __forceinline__ uint32_t wave_prefix_sum_u32(uint32_t v) {
+  v += dpp_u32<0x111, 0xf>(v);
+  v += dpp_u32<0x112, 0xf>(v);
+  v += dpp_u32<0x114, 0xf>(v);
+  v += dpp_u32<0x118, 0xf>(v);
+  v += dpp_u32<0x142, 0xa>(v);
+  v += dpp_u32<0x143, 0xc>(v);
+  return v;
+}
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)wave_prefix_sum_u32(v), 63);
+}
+
 __device__ __forceinline__ uint64_t readlane_u64(uint64_t v, int lane) {
   const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, lane);
   const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), lane);
