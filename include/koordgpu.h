@@ -220,6 +220,9 @@ int kg_debug_least_requested(kg_engine* e, const int64_t* requested, const int64
  * the number of (pod, node) pairs where feasibility or total score differ (must be 0). */
 int kg_debug_eval_paths(kg_engine* e, int64_t* mismatches);
 
+/* Diagnostic builds (-DKG_STAMPS) only: copies the in-kernel (s_memtime, s_memrealtime) stamps, uint64[4][32][2]. */
+int kg_debug_stamps(kg_engine* e, uint64_t* out);
+
 const char* kg_last_error(void);
 int kg_abi_version(void);
 /* sizeof of the ABI structs (0 kg_config, 1 kg_node, 2 kg_node_metric, 3 kg_pod, 4 kg_stats) for binding checks. */

@@ -94,11 +94,11 @@ EXPORTED_SYMBOLS = (
     "kg_node_metrics_update", "kg_pods_add", "kg_pods_remove", "kg_pods_schedule", "kg_pods_evaluate",
     "kg_pods_stage", "kg_pods_schedule_staged", "kg_results_fetch", "kg_engine_num_nodes",
     "kg_nodes_read_state", "kg_bench_kernel", "kg_debug_least_requested", "kg_last_error", "kg_abi_version",
-    "kg_abi_struct_size", "kg_nccl_unique_id", "kg_debug_eval_paths",
+    "kg_abi_struct_size", "kg_nccl_unique_id", "kg_debug_eval_paths", "kg_debug_stamps",
 )
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG_DIR, "libkoordgpu.so")
+LIB_PATH = os.environ.get("KOORDGPU_LIB") or os.path.join(PKG_DIR, "libkoordgpu.so")
 
 _lib = None
 
@@ -144,6 +144,7 @@ def load_library(path: str | None = None):
         "kg_abi_struct_size": (i64, [i]),
         "kg_nccl_unique_id": (i, [vp]),
         "kg_debug_eval_paths": (i, [vp, vp]),
+        "kg_debug_stamps": (i, [vp, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)

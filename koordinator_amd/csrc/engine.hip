@@ -78,11 +78,13 @@ __global__ __launch_bounds__(kWave* kEvalWaves) void eval_round(DevTable T, cons
                                                                   int64_t end, int B, int pods_per_wave,
                                                                   int64_t node_base, int64_t n_local, int nt_local,
                                                                   EvalParams P, uint64_t* __restrict__ lists) {
+  KG_STAMP(0, 0);
   const int64_t cursor = *cursor_p;
   if (cursor >= end) return;
   const int nb = (end - cursor) < (int64_t)B ? (int)(end - cursor) : B;
   const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
   const int tile = blockIdx.x * kEvalWaves + wave;
+  KG_STAMP(0, 1);
   const int p0 = blockIdx.y * pods_per_wave;
   if (tile >= nt_local || p0 >= nb) return;
   const int p1 = (p0 + pods_per_wave) < nb ? (p0 + pods_per_wave) : nb;
@@ -104,16 +106,34 @@ __global__ __launch_bounds__(kWave* kEvalWaves) void eval_round(DevTable T, cons
 
   for (int pi = p0; pi < p1; ++pi) {
     const DevPod p = pods[cursor + pi];
+    KG_STAMP(0, 2 + 4 * (pi - p0));
     uint32_t tot[kNPT];
+    bool okv[kNPT];
+    bool rare = false;
+#pragma unroll
+    for (int j = 0; j < kNPT; ++j) {
+      tot[j] = 0;
+      okv[j] = eval_fast(rows[j], p, P, tot[j], rare);
+    }
+    if (__ballot(rare)) {  // negative Requested somewhere in the tile: exact reference-shaped path
+#pragma unroll
+      for (int j = 0; j < kNPT; ++j) {
+        const int64_t local = (int64_t)tile * kTile + j * kWave + lane;
+        if (local < n_local) {
+          int64_t t = 0;
+          okv[j] = eval_node(load_row(T, node_base + local), p, P, t);
+          tot[j] = (uint32_t)t;
+        }
+      }
+    }
     uint64_t fm[kNPT];
     int nfeas = 0;
 #pragma unroll
     for (int j = 0; j < kNPT; ++j) {
-      tot[j] = 0;
-      const bool ok = eval_fast(rows[j], p, P, tot[j]);
-      fm[j] = __ballot(ok);
+      fm[j] = __ballot(okv[j]);
       nfeas += __popcll(fm[j]);
     }
+    KG_STAMP(0, 3 + 4 * (pi - p0));
     uint64_t sel[kNPT];
     if (nfeas <= kR) {
 #pragma unroll
@@ -150,6 +170,7 @@ __global__ __launch_bounds__(kWave* kEvalWaves) void eval_round(DevTable T, cons
       }
     }
     uint64_t* out = lists + ((size_t)pi * nt_local + tile) * kR;
+    KG_STAMP(0, 4 + 4 * (pi - p0));
     int base = 0;
 #pragma unroll
     for (int j = 0; j < kNPT; ++j) {
@@ -158,6 +179,7 @@ __global__ __launch_bounds__(kWave* kEvalWaves) void eval_round(DevTable T, cons
     }
     if (lane >= base && lane < kR) out[lane] = 0;
   }
+  KG_STAMP(0, 31);
 }
 
 // ---- round kernel 2: per-pod merge ------------------------------------------------------------------
@@ -171,6 +193,7 @@ __global__ __launch_bounds__(kMergeThreads) void merge_round(const uint64_t* __r
                                                              int64_t list_stride, int n_lists, int list_len,
                                                              const int64_t* __restrict__ cursor_p, int64_t end,
                                                              int B, uint64_t* __restrict__ out) {
+  KG_STAMP(1, 0);
   __shared__ uint32_t hist[256];
   __shared__ __attribute__((aligned(16))) uint64_t sel[kC];
   __shared__ uint64_t red64[kMergeThreads / kWave];
@@ -184,6 +207,7 @@ __global__ __launch_bounds__(kMergeThreads) void merge_round(const uint64_t* __r
   if (pod >= nb) return;
   const int tid = threadIdx.x, lane = tid % kWave, wave = tid / kWave;
   const uint64_t* base = in + (size_t)pod * pod_stride;
+  KG_STAMP(1, 1);
 
   // Keys held in registers: thread t owns chunks c = t + kMergeThreads*i of 8 consecutive keys.
   const int chunks_per_list = list_len / 8;
@@ -229,6 +253,7 @@ __global__ __launch_bounds__(kMergeThreads) void merge_round(const uint64_t* __r
     }
   }
   // block reductions: Σ nz, max ub_in, max kmax
+  KG_STAMP(1, 2);
   {
     const uint32_t s = wave_sum_u32(nz);
     const uint64_t u = wave_max_u64_dpp(ub_in), m = wave_max_u64_dpp(kmax);
@@ -252,6 +277,7 @@ __global__ __launch_bounds__(kMergeThreads) void merge_round(const uint64_t* __r
     kmax = km;
     __syncthreads();
   }
+  KG_STAMP(1, 3);
 
   uint64_t kth = 1;  // select every non-zero key when there are at most kC of them
   if (nz > (uint32_t)kC) {
@@ -292,25 +318,45 @@ __global__ __launch_bounds__(kMergeThreads) void merge_round(const uint64_t* __r
       target = sh_target;
       pmask |= 0xFFull << shift;
       __syncthreads();
+      KG_STAMP(1, 4 + byte);
     }
     kth = prefix;
   }
-  // compaction of the selected keys + the best key left out
-  if (tid == 0) sh_nsel = 0;
-  if (tid < kC) sel[tid] = 0;
-  __syncthreads();
+  // compaction of the selected keys (block prefix sum of per-thread counts) + the best key left out
+  uint32_t mycnt = 0;
   uint64_t next = 0;
 #pragma unroll
   for (int i = 0; i < kMergeChunks; ++i)
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
       const uint64_t v = k[i][r];
-      if (v >= kth && v) sel[atomicAdd(&sh_nsel, 1u)] = v;
-      else if (v) next = v > next ? v : next;
+      mycnt += (v >= kth) & (v != 0);
+      if (v && v < kth) next = v > next ? v : next;
     }
+  const uint32_t incl = wave_prefix_sum_u32(mycnt);
   next = wave_max_u64_dpp(next);
+  if (lane == kWave - 1) red32[wave] = incl;
   if (lane == 0) red64[wave] = next;
+  if (tid < kC) sel[tid] = 0;
   __syncthreads();
+  {
+    uint32_t off = incl - mycnt;
+    for (int w = 0; w < wave; ++w) off += red32[w];
+#pragma unroll
+    for (int i = 0; i < kMergeChunks; ++i)
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const uint64_t v = k[i][r];
+        if (v >= kth && v) sel[off++] = v;
+      }
+    if (tid == 0) {
+      uint32_t t = 0;
+      for (int w = 0; w < kMergeThreads / kWave; ++w) t += red32[w];
+      sh_nsel = t;
+    }
+  }
+  __syncthreads();
+  KG_STAMP(1, 13);
   uint64_t* o = out + (size_t)pod * kCandStride;
   if (wave == 0) {
     uint64_t nx = 0;
@@ -332,13 +378,15 @@ __global__ __launch_bounds__(kMergeThreads) void merge_round(const uint64_t* __r
       o[kC] = ub_in > ub_sel ? ub_in : ub_sel;
     }
   }
+  KG_STAMP(1, 14);
 }
 
 // ---- round kernel 3: FIFO resolve --------------------------------------------------------------------
-// One wavefront replays the round's pods in queue order against the merged candidates.  The round's candidate
-// records and pod descriptors are staged into LDS once (a single global-latency wait); the per-pod loop then
-// touches only LDS and registers.  Lane l < nM owns modified row l: its base row (loaded from HBM when the node
-// first wins, consumed lazily) plus the sum of the pods assumed onto it this round.  Per pod:
+// One wavefront replays the round's pods in queue order against the merged candidates.  Prologue (one
+// global-latency wait): the round's candidate records and pod descriptors are copied HBM→LDS by LDS-DMA, and
+// the rows of every pod's two best candidates are gathered into LDS.  The per-pod loop then touches only LDS
+// and registers.  Lane l < nM owns modified row l: base row, the sum of pods assumed onto it this round, and
+// its hoisted EvalRow (rebuilt only after the row changes).  Per pod:
 //   e     = the best candidate not modified in this round (ballot + ctz over the sorted list);
 //   mbest = the exact re-score of the modified rows — skipped when the profile is monotone (assume never raises
 //           a node's key) and e is the pod's top candidate;
@@ -376,34 +424,85 @@ __device__ __forceinline__ Row with_delta(Row r, const PodDelta& d) {
   return r;
 }
 
+constexpr int kRowWords = 16;  // a Row staged in LDS: 12 int64 + (alloc_pods | num_pods << 32) + flags + pad
+
+__device__ __forceinline__ void row_to_lds(uint64_t* d, const Row& r) {
+  d[0] = r.alloc_cpu; d[1] = r.alloc_mem; d[2] = r.req_cpu; d[3] = r.req_mem; d[4] = r.nz_cpu; d[5] = r.nz_mem;
+  d[6] = r.la_alloc_cpu; d[7] = r.la_alloc_mem; d[8] = r.la_used_cpu; d[9] = r.la_used_mem;
+  d[10] = r.la_pused_cpu; d[11] = r.la_pused_mem;
+  d[12] = (uint64_t)(uint32_t)r.alloc_pods | ((uint64_t)(uint32_t)r.num_pods << 32);
+  d[13] = r.flags;
+}
+
+__device__ __forceinline__ Row row_from_lds(const uint64_t* d) {
+  Row r;
+  r.alloc_cpu = d[0]; r.alloc_mem = d[1]; r.req_cpu = d[2]; r.req_mem = d[3]; r.nz_cpu = d[4]; r.nz_mem = d[5];
+  r.la_alloc_cpu = d[6]; r.la_alloc_mem = d[7]; r.la_used_cpu = d[8]; r.la_used_mem = d[9];
+  r.la_pused_cpu = d[10]; r.la_pused_mem = d[11];
+  r.alloc_pods = (int32_t)(uint32_t)d[12];
+  r.num_pods = (int32_t)(uint32_t)(d[12] >> 32);
+  r.flags = (uint32_t)d[13];
+  return r;
+}
+
+typedef __attribute__((address_space(3))) void* lds_void_ptr;
+typedef const __attribute__((address_space(1))) void* global_cvoid_ptr;
+
 __global__ __launch_bounds__(kWave) void resolve_round(DevTable T, const DevPod* __restrict__ pods,
                                                         int64_t* __restrict__ cursor_p, int64_t end, int B,
                                                         const uint64_t* __restrict__ cand, EvalParams P,
                                                         uint64_t* __restrict__ out_keys, int bitmap_words,
                                                         int64_t* __restrict__ round_stats) {
   extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
+  KG_STAMP(2, 0);
   const int lane = threadIdx.x;
   const int64_t cursor = *cursor_p;
   if (cursor >= end) return;
   const int nb = (end - cursor) < (int64_t)B ? (int)(end - cursor) : B;
-  uint64_t* s_cand = smem;                                              // [nb][kCandStride]
-  DevPod* s_pods = reinterpret_cast<DevPod*>(smem + (size_t)B * kCandStride);  // [nb]
-  uint32_t* bitmap = reinterpret_cast<uint32_t*>(smem + (size_t)B * kCandStride + (size_t)B * 7);
+  uint64_t* s_cand = smem;                                            // [B][kCandStride]
+  uint64_t* s_podw = s_cand + (size_t)B * kCandStride;                // [B] DevPod (8 words)
+  uint64_t* s_rows = s_podw + (size_t)B * 8;                          // [2B][kRowWords]
+  uint32_t* bitmap = reinterpret_cast<uint32_t*>(s_rows + (size_t)2 * B * kRowWords);
+  // prologue: LDS-DMA of records + pods, gather of the two best candidates' rows per pod, bitmap clear
   {
-    const ulonglong2* src = reinterpret_cast<const ulonglong2*>(cand);
-    ulonglong2* dst = reinterpret_cast<ulonglong2*>(s_cand);
-    for (int i = lane; i < nb * kCandStride / 2; i += kWave) dst[i] = src[i];
-    const uint64_t* ps = reinterpret_cast<const uint64_t*>(pods + cursor);
-    uint64_t* pd = reinterpret_cast<uint64_t*>(s_pods);
-    for (int i = lane; i < nb * 7; i += kWave) pd[i] = ps[i];
-    for (int w = lane; w < bitmap_words; w += kWave) bitmap[w] = 0;
+    const int n16 = nb * kCandStride / 2;
+    for (int it = 0; it * kWave < n16; ++it) {
+      const int idx = it * kWave + lane;
+      if (idx < n16)
+        __builtin_amdgcn_global_load_lds((global_cvoid_ptr)(cand + 2 * (size_t)idx), (lds_void_ptr)(s_cand + 2 * (size_t)it * kWave),
+                                         16, 0, 0);
+    }
+    const uint64_t* pw = reinterpret_cast<const uint64_t*>(pods + cursor);
+    const int p16 = nb * 4;
+    for (int it = 0; it * kWave < p16; ++it) {
+      const int idx = it * kWave + lane;
+      if (idx < p16)
+        __builtin_amdgcn_global_load_lds((global_cvoid_ptr)(pw + 2 * (size_t)idx), (lds_void_ptr)(s_podw + 2 * (size_t)it * kWave),
+                                         16, 0, 0);
+    }
   }
+  uint32_t staged = 0xFFFFFFFFu;  // node whose row this lane staged (lane l < 2nb: pod l/2, position l%2)
+  if (lane < 2 * nb) {
+    const uint64_t k = cand[(size_t)(lane >> 1) * kCandStride + (lane & 1)];
+    if (k) {
+      staged = key_node(k);
+      row_to_lds(s_rows + (size_t)lane * kRowWords, load_row(T, staged));
+    }
+  }
+  for (int w = lane; w < bitmap_words; w += kWave) bitmap[w] = 0;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  KG_STAMP(2, 1);
 
+  const DevPod* s_pods = reinterpret_cast<const DevPod*>(s_podw);
   Row mrow;
   mrow.flags = 0;
   PodDelta dl = {};
+  EvalRow er;
+  er.flags = 0;
+  bool er_valid = false;
   uint32_t midx = 0xFFFFFFFFu;
+  uint64_t my_out = 0;
   int nM = 0;
   int consumed = 0;
   for (int j = 0; j < nb; ++j) {
@@ -418,37 +517,56 @@ __global__ __launch_bounds__(kWave) void resolve_round(DevTable T, const DevPod*
     if (nM > 0 && (!P.monotone || pos > 0)) {
       const DevPod p = s_pods[j];
       uint64_t mk = 0;
-      int64_t t = 0;
-      if (lane < nM && eval_node(with_delta(mrow, dl), p, P, t)) mk = make_key(t, midx);
+      if (lane < nM) {
+        if (!er_valid) {
+          er = make_eval_row(with_delta(mrow, dl), P);
+          er_valid = true;
+        }
+        uint32_t t = 0;
+        bool rare = false;
+        bool ok = eval_fast(er, p, P, t, rare);
+        if (rare) {
+          int64_t t64 = 0;
+          ok = eval_node(with_delta(mrow, dl), p, P, t64);
+          t = (uint32_t)t64;
+        }
+        if (ok) mk = make_key(t, midx);
+      }
       const uint64_t mbest = wave_max_u64_dpp(mk);
       best = mbest > best ? mbest : best;
     }
     if (best < ub) break;  // an unseen node could still win: leave this pod to the next round
-    if (lane == 0) out_keys[cursor + j] = best;
+    if (lane == j) my_out = best;
     ++consumed;
     if (best == 0) continue;  // unschedulable (ub == 0: no feasible node anywhere)
     const uint32_t w = key_node(best);
     const uint64_t hit = __ballot(lane < nM && midx == w);
     const int owner = hit ? (int)__builtin_ctzll(hit) : nM;
+    const uint64_t st = hit ? 0 : __ballot(staged == w);
     if (lane == owner) {
       if (!hit) {
-        mrow = load_row(T, w);  // consumed lazily: the fast path never waits for it
+        mrow = st ? row_from_lds(s_rows + (size_t)__builtin_ctzll(st) * kRowWords) : load_row(T, w);
         midx = w;
       }
       add_delta(dl, s_pods[j]);
+      er_valid = false;
     }
     if (!hit) {
       if (lane == 0) bitmap[w >> 5] |= 1u << (w & 31);
       ++nM;
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // order the LDS bitmap write before later reads
+      asm volatile("" ::: "memory");  // LDS ops of one wave are in order; keep the compiler from reordering
     }
+    if (j < 28) KG_STAMP(2, 2 + j);
   }
   if (lane < nM) store_mutable(T, midx, with_delta(mrow, dl));
+  if (lane < consumed) out_keys[cursor + lane] = my_out;
+  KG_STAMP(2, 30);
   if (lane == 0) {
     *cursor_p = cursor + consumed;
     round_stats[0] += 1;
     round_stats[1] += consumed;
   }
+  KG_STAMP(2, 31);
 }
 
 // kg_pods_evaluate: one pod, every node, per-plugin outputs.
@@ -498,8 +616,9 @@ __global__ void debug_eval_paths(DevTable T, const DevPod* __restrict__ pods, in
     int64_t t1 = 0;
     uint32_t t2 = 0;
     const bool f1 = eval_node(r, pods[k], P, t1);
-    const bool f2 = eval_fast(er, pods[k], P, t2);
-    bad += (f1 != f2) || (f1 && (uint32_t)t1 != t2);
+    bool rare = false;
+    const bool f2 = eval_fast(er, pods[k], P, t2, rare);
+    bad += !rare && ((f1 != f2) || (f1 && (uint32_t)t1 != t2));
   }
   if (bad) atomicAdd(mismatches, bad);
 }
@@ -716,6 +835,7 @@ int decode_pod(const kg_engine* e, const kg_pod& p, DevPod& d) {
             (p.priority_class == KG_PRIO_PROD ? P_PROD : 0) |
             (p.priority_class == KG_PRIO_PROD && c.la_score_according_prod_usage ? P_LA_PROD_SCORE : 0);
   d.pad = 0;
+  d.pad2 = 0;
   return 0;
 }
 
@@ -796,7 +916,7 @@ RoundGeom geometry(const kg_engine* e) {
 }
 
 size_t resolve_lds_bytes(const RoundGeom& g) {
-  return (size_t)g.B * kCandStride * 8 + (size_t)g.B * sizeof(DevPod) + (size_t)g.bitmap_words * 4;
+  return ((size_t)g.B * kCandStride + (size_t)g.B * 8 + (size_t)2 * g.B * kRowWords) * 8 + (size_t)g.bitmap_words * 4;
 }
 
 dim3 eval_grid(const RoundGeom& g) {
@@ -981,7 +1101,7 @@ int kg_engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank, int
   e->P.monotone = 1;  // NodeResourcesFit + LoadAwareScheduling: assume only lowers a node's key
   e->P.inv_la_wsum = 1.0f / (float)e->P.la_wsum;
   if (hipFuncSetAttribute((const void*)resolve_round, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)(kMaxNodes / 8 + kMaxB * (kCandStride * 8 + sizeof(DevPod)))) != hipSuccess)
+                          (int)(kMaxNodes / 8 + kMaxB * (kCandStride + 8 + 2 * kRowWords) * 8)) != hipSuccess)
     return bail(fail(KG_E_DEVICE, "hipFuncSetAttribute(resolve_round LDS)"));
   if (n_ranks > 1) {
     ncclUniqueId id;
@@ -1186,7 +1306,7 @@ int kg_pods_evaluate(kg_engine* e, const kg_pod* pod, int32_t* out_reject, int64
   if (n == 0) return 0;
   if (int rc = e->scratch64.ensure(2 * n + 8)) return rc;
   if (int rc = e->scratch32.ensure(n)) return rc;
-  DevPod* dp = reinterpret_cast<DevPod*>(e->scratch64.p + 2 * n);  // 56 B fits in the 8 spare int64s
+  DevPod* dp = reinterpret_cast<DevPod*>(e->scratch64.p + 2 * n);  // 64 B = the 8 spare int64s
   HIP_TRY(hipMemcpyAsync(dp, &d, sizeof(d), hipMemcpyHostToDevice, e->stream));
   evaluate_pod<<<(unsigned)((n + 255) / 256), 256, 0, e->stream>>>(e->T, dp, n, e->P, e->scratch32.p, e->scratch64.p,
                                                                    e->scratch64.p + n);
@@ -1290,9 +1410,9 @@ int kg_bench_kernel(kg_engine* e, int which, int iters, double* avg_ms, double* 
   if (algo_bytes) {
     // eval: SURVEY §8(d) per-evaluation bytes (Fit 56 B + LoadAware 36 B = 92 B per node) × pods × nodes,
     //       + the candidate lists written;  merge: lists read + records written;  resolve: records + pods read.
-    if (which == 0) *algo_bytes = nb * (double)g.n_local * 92.0 + nb * g.nt_local * kR * 8.0 + nb * 56.0;
+    if (which == 0) *algo_bytes = nb * (double)g.n_local * 92.0 + nb * g.nt_local * kR * 8.0 + nb * 64.0;
     else if (which == 1) *algo_bytes = nb * g.nt_local * kR * 8.0 + nb * kCandStride * 8.0;
-    else *algo_bytes = nb * kCandStride * 8.0 + nb * 56.0;
+    else *algo_bytes = nb * kCandStride * 8.0 + nb * 64.0;
   }
   return 0;
 }
@@ -1313,6 +1433,19 @@ int kg_debug_eval_paths(kg_engine* e, int64_t* mismatches) {
   HIP_TRY(hipStreamSynchronize(e->stream));
   b.release();
   return 0;
+}
+
+int kg_debug_stamps(kg_engine* e, uint64_t* out) {
+#ifdef KG_STAMPS
+  if (!e || !out) return fail(KG_E_INVALID, "bad argument");
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(kg::g_stamps), sizeof(kg::g_stamps), 0, hipMemcpyDeviceToHost));
+  return 0;
+#else
+  (void)e;
+  (void)out;
+  return fail(KG_E_UNSUPPORTED, "not a -DKG_STAMPS diagnostic build");
+#endif
 }
 
 int kg_debug_least_requested(kg_engine* e, const int64_t* req, const int64_t* cap, int64_t* out, int64_t n) {

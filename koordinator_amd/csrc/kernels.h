@@ -16,6 +16,24 @@ namespace kg {
 
 constexpr int kWave = 64;
 
+// Diagnostic build only (-DKG_STAMPS): block 0 / lane 0 records (s_memtime, s_memrealtime) pairs at named
+// points of each kernel into a device array read back by kg_debug_stamps.  No stamp executes in the product
+// build (the macro expands to nothing).
+#ifdef KG_STAMPS
+__device__ unsigned long long g_stamps[4][32][2];
+#define KG_STAMP(kern, point)                                                                  \
+  do {                                                                                         \
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {                              \
+      g_stamps[kern][point][0] = __builtin_amdgcn_s_memtime();                                 \
+      g_stamps[kern][point][1] = __builtin_amdgcn_s_memrealtime();                             \
+    }                                                                                          \
+  } while (0)
+#else
+#define KG_STAMP(kern, point) \
+  do {                        \
+  } while (0)
+#endif
+
 // node flags (device)
 constexpr uint32_t F_VALID = 1u << 0;
 constexpr uint32_t F_LA_SCORE = 1u << 1;      // NodeMetric present and not expired: LoadAware scores it
@@ -45,8 +63,9 @@ struct DevPod {
   int64_t est_cpu, est_mem;
   uint32_t flags;
   uint32_t pad;
+  int64_t pad2;  // 64 B: 16-B aligned for LDS-DMA
 };
-static_assert(sizeof(DevPod) == 56, "DevPod layout");
+static_assert(sizeof(DevPod) == 64, "DevPod layout");
 
 struct EvalParams {
   int64_t fit_w_cpu, fit_w_mem;
@@ -308,52 +327,59 @@ __device__ __forceinline__ EvalRow make_eval_row(const Row& r, const EvalParams&
   return e;
 }
 
-// leastRequestedScore with x = capacity - requested precomputed: ((x * 100) / capacity), 0 if x < 0.
-__device__ __forceinline__ int64_t lrs_x(int64_t x, int64_t cap, float inv) {
-  if (cap == 0 || x < 0) return 0;
+// leastRequestedScore with x = capacity - requested precomputed: ((x * 100) / capacity), 0 when x < 0 or
+// capacity == 0.  Branch-free; exact for 0 ≤ x ≤ capacity (the estimate is within ±1 and one int64
+// multiply-compare corrects it).  x > capacity (a negative Requested) is flagged `rare` for the exact path.
+__device__ __forceinline__ int32_t lrs_x(int64_t x, int64_t cap, float inv, bool& rare) {
   const int64_t num = x * 100;
-  if (x > cap) return num / cap;  // requested < 0: outside [0,100], exact slow path
-  int q = (int)(i64_to_f32(x) * inv);
+  int q = (int)(i64_to_f32(x > 0 ? x : 0) * inv);
   q = q < 0 ? 0 : (q > 100 ? 100 : q);
   const int64_t t = (int64_t)q * cap;
-  if (t > num) --q;
-  else if (t + cap <= num) ++q;
-  return q;
+  q -= (int)(t > num);
+  q += (int)(t + cap <= num);
+  rare |= x > cap;
+  return (cap == 0 || x < 0) ? 0 : q;
 }
 
 // s / w for 0 ≤ s ≤ 100·w (w ≤ 2·10⁶, so s < 2^28 is exact in f32's integer range + one correction step)
 __device__ __forceinline__ int32_t div_est(int32_t s, int32_t w, float inv_w) {
   int q = (int)((float)s * inv_w);
   const int32_t t = q * w;
-  if (t > s) --q;
-  else if (t + w <= s) ++q;
+  q -= (int)(t > s);
+  q += (int)(t + w <= s);
   return q;
 }
 
-__device__ __forceinline__ bool eval_fast(const EvalRow& n, const DevPod& p, const EvalParams& P, uint32_t& total) {
+// Branch-free fused Filter + Score on hoisted terms.  Returns feasibility; sets `rare` when an input lies
+// outside the fast path's domain (a negative Requested) — the caller then re-evaluates with eval_node.
+__device__ __forceinline__ bool eval_fast(const EvalRow& n, const DevPod& p, const EvalParams& P, uint32_t& total,
+                                          bool& rare) {
   bool ok = (n.flags & F_VALID) != 0;
   if (P.fit_filter) {
     ok &= n.pods_left >= 0;
     if (!(p.flags & P_ZERO_REQ)) ok &= (p.req_cpu <= n.free_cpu) & (p.req_mem <= n.free_mem);
   }
   if (P.la_filter && !(p.flags & P_DAEMONSET)) ok &= (n.flags & ((p.flags & P_PROD) ? F_LA_PASS_PROD : F_LA_PASS)) != 0;
-  if (!ok) return false;
   int32_t t = 0;
-  if (P.fit_score && n.fit_ws) {
+  if (P.fit_score) {
     int32_t s = 0;
-    if (P.fit_w_cpu) s += (int32_t)lrs_x(n.fnz_cpu - p.nz_cpu, n.alloc_cpu, n.inv_cpu) * (int32_t)P.fit_w_cpu;
-    if (P.fit_w_mem) s += (int32_t)lrs_x(n.fnz_mem - p.nz_mem, n.alloc_mem, n.inv_mem) * (int32_t)P.fit_w_mem;
-    t += div_est(s, n.fit_ws, n.inv_fit_ws) * (int32_t)P.weight_fit;
+    const int32_t qc = lrs_x(n.fnz_cpu - p.nz_cpu, n.alloc_cpu, n.inv_cpu, rare);
+    const int32_t qm = lrs_x(n.fnz_mem - p.nz_mem, n.alloc_mem, n.inv_mem, rare);
+    if (P.fit_w_cpu) s += qc * (int32_t)P.fit_w_cpu;
+    if (P.fit_w_mem) s += qm * (int32_t)P.fit_w_mem;
+    t += n.fit_ws ? div_est(s, n.fit_ws, n.inv_fit_ws) * (int32_t)P.weight_fit : 0;
   }
-  if (P.la_score && (n.flags & F_LA_SCORE)) {
+  if (P.la_score) {
     const bool prodv = (p.flags & P_LA_PROD_SCORE) != 0;
+    const int32_t qc = lrs_x((prodv ? n.la_pfree_cpu : n.la_free_cpu) - p.est_cpu, n.la_alloc_cpu, n.la_inv_cpu, rare);
+    const int32_t qm = lrs_x((prodv ? n.la_pfree_mem : n.la_free_mem) - p.est_mem, n.la_alloc_mem, n.la_inv_mem, rare);
     int32_t s = 0;
-    if (P.la_w_cpu) s += (int32_t)lrs_x((prodv ? n.la_pfree_cpu : n.la_free_cpu) - p.est_cpu, n.la_alloc_cpu, n.la_inv_cpu) * (int32_t)P.la_w_cpu;
-    if (P.la_w_mem) s += (int32_t)lrs_x((prodv ? n.la_pfree_mem : n.la_free_mem) - p.est_mem, n.la_alloc_mem, n.la_inv_mem) * (int32_t)P.la_w_mem;
-    t += div_est(s, (int32_t)P.la_wsum, P.inv_la_wsum) * (int32_t)P.weight_la;
+    if (P.la_w_cpu) s += qc * (int32_t)P.la_w_cpu;
+    if (P.la_w_mem) s += qm * (int32_t)P.la_w_mem;
+    t += (n.flags & F_LA_SCORE) ? div_est(s, (int32_t)P.la_wsum, P.inv_la_wsum) * (int32_t)P.weight_la : 0;
   }
   total = (uint32_t)t;
-  return true;
+  return ok;
 }
 
 }  // namespace kg
