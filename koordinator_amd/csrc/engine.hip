@@ -495,70 +495,95 @@ __global__ __launch_bounds__(kWave) void resolve_round(DevTable T, const DevPod*
   KG_STAMP(2, 1);
 
   const DevPod* s_pods = reinterpret_cast<const DevPod*>(s_podw);
+  // lane state (lane < nM): the modified node, where its base row lives (staged LDS slot, or `mrow` loaded from
+  // HBM), the pods assumed onto it this round, and its hoisted EvalRow once materialised.
+  uint32_t midx = 0xFFFFFFFFu;
+  int slot = -1;
   Row mrow;
   mrow.flags = 0;
   PodDelta dl = {};
   EvalRow er;
   er.flags = 0;
   bool er_valid = false;
-  uint32_t midx = 0xFFFFFFFFu;
   uint64_t my_out = 0;
   int nM = 0;
   int consumed = 0;
+  uint64_t key_n = s_cand[lane];
+  uint64_t ub_n = s_cand[kC];
   for (int j = 0; j < nb; ++j) {
-    const uint64_t key = s_cand[(size_t)j * kCandStride + lane];
-    const uint64_t ub = s_cand[(size_t)j * kCandStride + kC];
-    const uint32_t node = key ? key_node(key) : 0;
-    const bool mod = key && ((bitmap[node >> 5] >> (node & 31)) & 1u);
-    const uint64_t um = __ballot(key != 0 && !mod);
+    const uint64_t key = key_n, ub = ub_n;
+    const int jn = j + 1 < nb ? j + 1 : j;  // software prefetch of the next pod's list (branch-free)
+    key_n = s_cand[(size_t)jn * kCandStride + lane];
+    ub_n = s_cand[(size_t)jn * kCandStride + kC];
+    const uint32_t node = key ? key_node(key) : 0u;
+    const uint32_t word = bitmap[node >> 5];
+    const bool unmod = key != 0 && !((word >> (node & 31)) & 1u);
+    const uint64_t um = __ballot(unmod);
     const int pos = um ? (int)__builtin_ctzll(um) : kC;
     const uint64_t e = um ? readlane_u64(key, pos) : 0;
+    const DevPod p = s_pods[j];
     uint64_t best = e;
-    if (nM > 0 && (!P.monotone || pos > 0)) {
-      const DevPod p = s_pods[j];
+    if (nM > 0 && (!P.monotone || pos > 0)) {  // slow path: re-score this round's modified rows
       uint64_t mk = 0;
       if (lane < nM) {
         if (!er_valid) {
-          er = make_eval_row(with_delta(mrow, dl), P);
+          const Row base = slot >= 0 ? row_from_lds(s_rows + (size_t)slot * kRowWords) : mrow;
+          er = make_eval_row(with_delta(base, dl), P);
           er_valid = true;
         }
         uint32_t t = 0;
         bool rare = false;
         bool ok = eval_fast(er, p, P, t, rare);
         if (rare) {
+          const Row base = slot >= 0 ? row_from_lds(s_rows + (size_t)slot * kRowWords) : mrow;
           int64_t t64 = 0;
-          ok = eval_node(with_delta(mrow, dl), p, P, t64);
+          ok = eval_node(with_delta(base, dl), p, P, t64);
           t = (uint32_t)t64;
         }
-        if (ok) mk = make_key(t, midx);
+        mk = ok ? make_key(t, midx) : 0;
       }
       const uint64_t mbest = wave_max_u64_dpp(mk);
       best = mbest > best ? mbest : best;
     }
     if (best < ub) break;  // an unseen node could still win: leave this pod to the next round
-    if (lane == j) my_out = best;
+    my_out = lane == j ? best : my_out;
     ++consumed;
     if (best == 0) continue;  // unschedulable (ub == 0: no feasible node anywhere)
     const uint32_t w = key_node(best);
     const uint64_t hit = __ballot(lane < nM && midx == w);
     const int owner = hit ? (int)__builtin_ctzll(hit) : nM;
-    const uint64_t st = hit ? 0 : __ballot(staged == w);
-    if (lane == owner) {
-      if (!hit) {
-        mrow = st ? row_from_lds(s_rows + (size_t)__builtin_ctzll(st) * kRowWords) : load_row(T, w);
-        midx = w;
-      }
-      add_delta(dl, s_pods[j]);
-      er_valid = false;
-    }
+    const bool me = lane == owner;
     if (!hit) {
-      if (lane == 0) bitmap[w >> 5] |= 1u << (w & 31);
+      const uint64_t st = __ballot(staged == w);
+      if (me) {
+        midx = w;
+        slot = st ? (int)__builtin_ctzll(st) : -1;
+        if (!st) mrow = load_row(T, w);  // not staged (rare): HBM load, consumed lazily
+        er_valid = false;
+      }
+      if (lane == 0) atomicOr(&bitmap[w >> 5], 1u << (w & 31));
       ++nM;
-      asm volatile("" ::: "memory");  // LDS ops of one wave are in order; keep the compiler from reordering
     }
-    if (j < 28) KG_STAMP(2, 2 + j);
+    // assume: accumulate the pod on the owner lane; keep a materialised EvalRow current incrementally
+    const int64_t prod = (p.flags & P_PROD) ? 1 : 0;
+    if (me) {
+      add_delta(dl, p);
+      er.free_cpu -= p.req_cpu;
+      er.free_mem -= p.req_mem;
+      er.fnz_cpu -= p.nz_cpu;
+      er.fnz_mem -= p.nz_mem;
+      er.la_free_cpu -= p.est_cpu;
+      er.la_free_mem -= p.est_mem;
+      er.la_pfree_cpu -= prod * p.est_cpu;
+      er.la_pfree_mem -= prod * p.est_mem;
+      er.pods_left -= 1;
+    }
+    if (j == 0 || j == 15 || j == 31) KG_STAMP(2, 2 + j / 8);
   }
-  if (lane < nM) store_mutable(T, midx, with_delta(mrow, dl));
+  if (lane < nM) {
+    const Row base = slot >= 0 ? row_from_lds(s_rows + (size_t)slot * kRowWords) : mrow;
+    store_mutable(T, midx, with_delta(base, dl));
+  }
   if (lane < consumed) out_keys[cursor + lane] = my_out;
   KG_STAMP(2, 30);
   if (lane == 0) {
