@@ -37,10 +37,13 @@ constexpr int kR = 8;                 // candidates kept per (pod, tile)
 constexpr int kEvalWaves = 4;         // waves (tiles) per eval block
 constexpr int kMaxB = 64;             // modified rows are held one per lane of the resolver wave
 constexpr int kC = 64;                // merged candidates per pod (> any modified-set size: kC > kMaxB - 1)
-constexpr int kCandStride = 72;       // per-pod record: kC keys, ub, padding to a 64-B multiple
+constexpr int kStaged = 3;            // hoisted rows of each pod's best candidates shipped with its record
+constexpr int kRecRows = 72;          // record layout (uint64 words): [0,kC) keys, [kC] ub, [72, 72+3·17) rows
+constexpr int kCandStride = 128;      // per-pod record: 1 KiB (a 16-B multiple, for LDS-DMA)
 constexpr int kMergeThreads = 256;
 constexpr int kMergeChunks = 4;       // chunks of 8 keys per merge thread: ≤ 1024 tile lists = 262144 nodes per rank
-constexpr int64_t kMaxNodes = 3 << 18;  // resolver LDS: N/8-byte bitmap (≤ 96 KiB) + the round's records (≤ 40 KiB)
+constexpr int64_t kMaxNodes = 1 << 19;  // resolver LDS: N/8-byte bitmap (≤ 64 KiB) + the round's records (≤ 64 KiB)
+static_assert(kRecRows + kStaged * kEvalRowWords <= kCandStride, "record layout");
 
 thread_local std::string g_err;
 
@@ -66,6 +69,9 @@ int fail(int code, const char* fmt, ...) {
     if (r_ != ncclSuccess) return fail(KG_E_COLLECTIVE, "%s: %s", #expr, ncclGetErrorString(r_)); \
   } while (0)
 
+typedef __attribute__((address_space(3))) void* lds_void_ptr;
+typedef const __attribute__((address_space(1))) void* global_cvoid_ptr;
+
 // ------------------------------------------------------------------------------------------------
 // Kernels
 // ------------------------------------------------------------------------------------------------
@@ -73,6 +79,7 @@ int fail(int code, const char* fmt, ...) {
 // ---- round kernel 1: wide evaluation -------------------------------------------------------------
 // One wave = one tile of kTile nodes (lane l holds nodes tile*kTile + j*64 + l, j < kNPT) × pods_per_wave pods
 // of the round.  Writes lists[(pod, tile)][kR] = the tile's top-kR packed keys (unordered, zero-padded).
+template <int PF>
 __global__ __launch_bounds__(kWave* kEvalWaves) void eval_round(DevTable T, const DevPod* __restrict__ pods,
                                                                   const int64_t* __restrict__ cursor_p,
                                                                   int64_t end, int B, int pods_per_wave,
@@ -113,7 +120,7 @@ __global__ __launch_bounds__(kWave* kEvalWaves) void eval_round(DevTable T, cons
 #pragma unroll
     for (int j = 0; j < kNPT; ++j) {
       tot[j] = 0;
-      okv[j] = eval_fast(rows[j], p, P, tot[j], rare);
+      okv[j] = eval_fast<PF>(rows[j], p, P, tot[j], rare);
     }
     if (__ballot(rare)) {  // negative Requested somewhere in the tile: exact reference-shaped path
 #pragma unroll
@@ -145,16 +152,15 @@ __global__ __launch_bounds__(kWave* kEvalWaves) void eval_round(DevTable T, cons
         const uint32_t c = cur | (1u << b);
         int cnt = 0;
 #pragma unroll
-        for (int j = 0; j < kNPT; ++j) cnt += __popcll(__ballot(((fm[j] >> lane) & 1) && tot[j] >= c));
+        for (int j = 0; j < kNPT; ++j) cnt += __popcll(__ballot(okv[j] && tot[j] >= c));
         if (cnt >= kR) cur = c;
       }
       int need = kR;
       uint64_t eq[kNPT];
 #pragma unroll
       for (int j = 0; j < kNPT; ++j) {
-        const bool f = (fm[j] >> lane) & 1;
-        sel[j] = __ballot(f && tot[j] > cur);
-        eq[j] = __ballot(f && tot[j] == cur);
+        sel[j] = __ballot(okv[j] && tot[j] > cur);
+        eq[j] = __ballot(okv[j] && tot[j] == cur);
         need -= __popcll(sel[j]);
       }
       // ties at τ: lowest node index first (register j, then lane)
@@ -169,8 +175,8 @@ __global__ __launch_bounds__(kWave* kEvalWaves) void eval_round(DevTable T, cons
         }
       }
     }
-    uint64_t* out = lists + ((size_t)pi * nt_local + tile) * kR;
     KG_STAMP(0, 4 + 4 * (pi - p0));
+    uint64_t* out = lists + ((size_t)pi * nt_local + tile) * kR;
     int base = 0;
 #pragma unroll
     for (int j = 0; j < kNPT; ++j) {
@@ -188,18 +194,21 @@ __global__ __launch_bounds__(kWave* kEvalWaves) void eval_round(DevTable T, cons
 //   ub = max(max_l ub_l, (kC+1)-th key of the union + 1), where a tile list's ub_l is its minimum when it is
 //   full (its unseen nodes all score lower) and a rank list carries its own ub in slot kC.
 // The kC-th key is found by an 8-bit radix select over the 64-bit keys (keys are unique: score<<32 | ~idx).
+// The record also carries the hoisted rows of the kStaged best candidates, read from this rank's replica of
+// the node table, so that the resolver never waits on HBM for a likely winner.
 template <bool RANK_LISTS>
-__global__ __launch_bounds__(kMergeThreads) void merge_round(const uint64_t* __restrict__ in, int64_t pod_stride,
+__global__ __launch_bounds__(kMergeThreads) void merge_round(DevTable T, EvalParams P,
+                                                             const uint64_t* __restrict__ in, int64_t pod_stride,
                                                              int64_t list_stride, int n_lists, int list_len,
                                                              const int64_t* __restrict__ cursor_p, int64_t end,
                                                              int B, uint64_t* __restrict__ out) {
-  KG_STAMP(1, 0);
   __shared__ uint32_t hist[256];
   __shared__ __attribute__((aligned(16))) uint64_t sel[kC];
   __shared__ uint64_t red64[kMergeThreads / kWave];
   __shared__ uint32_t red32[kMergeThreads / kWave];
   __shared__ uint64_t sh_prefix;
   __shared__ uint32_t sh_target, sh_nsel;
+  KG_STAMP(1, 0);
   const int64_t cursor = *cursor_p;
   if (cursor >= end) return;
   const int nb = (end - cursor) < (int64_t)B ? (int)(end - cursor) : B;
@@ -252,8 +261,8 @@ __global__ __launch_bounds__(kMergeThreads) void merge_round(const uint64_t* __r
       for (int r = 0; r < 8; ++r) k[i][r] = 0;
     }
   }
-  // block reductions: Σ nz, max ub_in, max kmax
   KG_STAMP(1, 2);
+  // block reductions: Σ nz, max ub_in, max kmax
   {
     const uint32_t s = wave_sum_u32(nz);
     const uint64_t u = wave_max_u64_dpp(ub_in), m = wave_max_u64_dpp(kmax);
@@ -317,7 +326,6 @@ __global__ __launch_bounds__(kMergeThreads) void merge_round(const uint64_t* __r
       prefix = sh_prefix;
       target = sh_target;
       pmask |= 0xFFull << shift;
-      __syncthreads();
       KG_STAMP(1, 4 + byte);
     }
     kth = prefix;
@@ -377,16 +385,24 @@ __global__ __launch_bounds__(kMergeThreads) void merge_round(const uint64_t* __r
       const uint64_t ub_sel = nx ? nx + 1 : 0;
       o[kC] = ub_in > ub_sel ? ub_in : ub_sel;
     }
+    // hoisted rows of the kStaged best candidates (the resolver's likely winners)
+    if (lane < n_sel && rank < kStaged) {
+      const EvalRow er = make_eval_row(load_row(T, key_node(v)), P);
+      const uint64_t* src = reinterpret_cast<const uint64_t*>(&er);
+      uint64_t* dst = o + kRecRows + rank * kEvalRowWords;
+#pragma unroll
+      for (int w = 0; w < kEvalRowWords; ++w) dst[w] = src[w];
+    }
   }
   KG_STAMP(1, 14);
 }
 
 // ---- round kernel 3: FIFO resolve --------------------------------------------------------------------
 // One wavefront replays the round's pods in queue order against the merged candidates.  Prologue (one
-// global-latency wait): the round's candidate records and pod descriptors are copied HBM→LDS by LDS-DMA, and
-// the rows of every pod's two best candidates are gathered into LDS.  The per-pod loop then touches only LDS
-// and registers.  Lane l < nM owns modified row l: base row, the sum of pods assumed onto it this round, and
-// its hoisted EvalRow (rebuilt only after the row changes).  Per pod:
+// global-latency wait): the round's records (candidate keys, bound, hoisted rows of the best candidates) and
+// pod descriptors are copied HBM→LDS by LDS-DMA.  The per-pod loop then touches only LDS and registers.
+// Lane l < nM owns modified node l as a hoisted EvalRow kept current by assume_on (or, when the node was not
+// staged, a base Row loading from HBM plus the pods assumed since, materialised on first use).  Per pod:
 //   e     = the best candidate not modified in this round (ballot + ctz over the sorted list);
 //   mbest = the exact re-score of the modified rows — skipped when the profile is monotone (assume never raises
 //           a node's key) and e is the pod's top candidate;
@@ -398,16 +414,15 @@ struct PodDelta {
 };
 
 __device__ __forceinline__ void add_delta(PodDelta& d, const DevPod& p) {
+  const int64_t prod = (p.flags & P_PROD) ? 1 : 0;
   d.req_cpu += p.req_cpu;
   d.req_mem += p.req_mem;
   d.nz_cpu += p.nz_cpu;
   d.nz_mem += p.nz_mem;
   d.est_cpu += p.est_cpu;
   d.est_mem += p.est_mem;
-  if (p.flags & P_PROD) {
-    d.pest_cpu += p.est_cpu;
-    d.pest_mem += p.est_mem;
-  }
+  d.pest_cpu += prod * p.est_cpu;
+  d.pest_mem += prod * p.est_mem;
   d.pods += 1;
 }
 
@@ -424,30 +439,7 @@ __device__ __forceinline__ Row with_delta(Row r, const PodDelta& d) {
   return r;
 }
 
-constexpr int kRowWords = 16;  // a Row staged in LDS: 12 int64 + (alloc_pods | num_pods << 32) + flags + pad
-
-__device__ __forceinline__ void row_to_lds(uint64_t* d, const Row& r) {
-  d[0] = r.alloc_cpu; d[1] = r.alloc_mem; d[2] = r.req_cpu; d[3] = r.req_mem; d[4] = r.nz_cpu; d[5] = r.nz_mem;
-  d[6] = r.la_alloc_cpu; d[7] = r.la_alloc_mem; d[8] = r.la_used_cpu; d[9] = r.la_used_mem;
-  d[10] = r.la_pused_cpu; d[11] = r.la_pused_mem;
-  d[12] = (uint64_t)(uint32_t)r.alloc_pods | ((uint64_t)(uint32_t)r.num_pods << 32);
-  d[13] = r.flags;
-}
-
-__device__ __forceinline__ Row row_from_lds(const uint64_t* d) {
-  Row r;
-  r.alloc_cpu = d[0]; r.alloc_mem = d[1]; r.req_cpu = d[2]; r.req_mem = d[3]; r.nz_cpu = d[4]; r.nz_mem = d[5];
-  r.la_alloc_cpu = d[6]; r.la_alloc_mem = d[7]; r.la_used_cpu = d[8]; r.la_used_mem = d[9];
-  r.la_pused_cpu = d[10]; r.la_pused_mem = d[11];
-  r.alloc_pods = (int32_t)(uint32_t)d[12];
-  r.num_pods = (int32_t)(uint32_t)(d[12] >> 32);
-  r.flags = (uint32_t)d[13];
-  return r;
-}
-
-typedef __attribute__((address_space(3))) void* lds_void_ptr;
-typedef const __attribute__((address_space(1))) void* global_cvoid_ptr;
-
+template <int PF>
 __global__ __launch_bounds__(kWave) void resolve_round(DevTable T, const DevPod* __restrict__ pods,
                                                         int64_t* __restrict__ cursor_p, int64_t end, int B,
                                                         const uint64_t* __restrict__ cand, EvalParams P,
@@ -461,50 +453,43 @@ __global__ __launch_bounds__(kWave) void resolve_round(DevTable T, const DevPod*
   const int nb = (end - cursor) < (int64_t)B ? (int)(end - cursor) : B;
   uint64_t* s_cand = smem;                                            // [B][kCandStride]
   uint64_t* s_podw = s_cand + (size_t)B * kCandStride;                // [B] DevPod (8 words)
-  uint64_t* s_rows = s_podw + (size_t)B * 8;                          // [2B][kRowWords]
-  uint32_t* bitmap = reinterpret_cast<uint32_t*>(s_rows + (size_t)2 * B * kRowWords);
-  // prologue: LDS-DMA of records + pods, gather of the two best candidates' rows per pod, bitmap clear
-  {
+  uint32_t* bitmap = reinterpret_cast<uint32_t*>(s_podw + (size_t)B * 8);
+  {  // prologue: LDS-DMA of records + pods, bitmap clear
     const int n16 = nb * kCandStride / 2;
     for (int it = 0; it * kWave < n16; ++it) {
       const int idx = it * kWave + lane;
       if (idx < n16)
-        __builtin_amdgcn_global_load_lds((global_cvoid_ptr)(cand + 2 * (size_t)idx), (lds_void_ptr)(s_cand + 2 * (size_t)it * kWave),
-                                         16, 0, 0);
+        __builtin_amdgcn_global_load_lds((global_cvoid_ptr)(cand + 2 * (size_t)idx),
+                                         (lds_void_ptr)(s_cand + 2 * (size_t)it * kWave), 16, 0, 0);
     }
     const uint64_t* pw = reinterpret_cast<const uint64_t*>(pods + cursor);
     const int p16 = nb * 4;
     for (int it = 0; it * kWave < p16; ++it) {
       const int idx = it * kWave + lane;
       if (idx < p16)
-        __builtin_amdgcn_global_load_lds((global_cvoid_ptr)(pw + 2 * (size_t)idx), (lds_void_ptr)(s_podw + 2 * (size_t)it * kWave),
-                                         16, 0, 0);
+        __builtin_amdgcn_global_load_lds((global_cvoid_ptr)(pw + 2 * (size_t)idx),
+                                         (lds_void_ptr)(s_podw + 2 * (size_t)it * kWave), 16, 0, 0);
     }
+    for (int w = lane; w < bitmap_words; w += kWave) bitmap[w] = 0;
   }
-  uint32_t staged = 0xFFFFFFFFu;  // node whose row this lane staged (lane l < 2nb: pod l/2, position l%2)
-  if (lane < 2 * nb) {
-    const uint64_t k = cand[(size_t)(lane >> 1) * kCandStride + (lane & 1)];
-    if (k) {
-      staged = key_node(k);
-      row_to_lds(s_rows + (size_t)lane * kRowWords, load_row(T, staged));
-    }
-  }
-  for (int w = lane; w < bitmap_words; w += kWave) bitmap[w] = 0;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   KG_STAMP(2, 1);
-
+  // lane l < kStaged·nb: node whose hoisted row sits in record l / kStaged, slot l % kStaged
+  uint32_t staged = 0xFFFFFFFFu;
+  if (lane < kStaged * nb) {
+    const uint64_t kk = s_cand[(size_t)(lane / kStaged) * kCandStride + (lane % kStaged)];
+    staged = kk ? key_node(kk) : 0xFFFFFFFFu;
+  }
   const DevPod* s_pods = reinterpret_cast<const DevPod*>(s_podw);
-  // lane state (lane < nM): the modified node, where its base row lives (staged LDS slot, or `mrow` loaded from
-  // HBM), the pods assumed onto it this round, and its hoisted EvalRow once materialised.
+
   uint32_t midx = 0xFFFFFFFFu;
-  int slot = -1;
+  EvalRow er;
+  er.flags = 0;
+  bool er_valid = false;  // false: base row `mrow` (HBM load in flight) + `dl` not yet materialised
   Row mrow;
   mrow.flags = 0;
   PodDelta dl = {};
-  EvalRow er;
-  er.flags = 0;
-  bool er_valid = false;
   uint64_t my_out = 0;
   int nM = 0;
   int consumed = 0;
@@ -526,18 +511,16 @@ __global__ __launch_bounds__(kWave) void resolve_round(DevTable T, const DevPod*
     if (nM > 0 && (!P.monotone || pos > 0)) {  // slow path: re-score this round's modified rows
       uint64_t mk = 0;
       if (lane < nM) {
-        if (!er_valid) {
-          const Row base = slot >= 0 ? row_from_lds(s_rows + (size_t)slot * kRowWords) : mrow;
-          er = make_eval_row(with_delta(base, dl), P);
+        if (!er_valid) {  // non-staged winner: materialise from the HBM row + the pods assumed since
+          er = make_eval_row(with_delta(mrow, dl), P);
           er_valid = true;
         }
         uint32_t t = 0;
         bool rare = false;
-        bool ok = eval_fast(er, p, P, t, rare);
+        bool ok = eval_fast<PF>(er, p, P, t, rare);
         if (rare) {
-          const Row base = slot >= 0 ? row_from_lds(s_rows + (size_t)slot * kRowWords) : mrow;
           int64_t t64 = 0;
-          ok = eval_node(with_delta(base, dl), p, P, t64);
+          ok = eval_node(row_of(er), p, P, t64);
           t = (uint32_t)t64;
         }
         mk = ok ? make_key(t, midx) : 0;
@@ -557,32 +540,31 @@ __global__ __launch_bounds__(kWave) void resolve_round(DevTable T, const DevPod*
       const uint64_t st = __ballot(staged == w);
       if (me) {
         midx = w;
-        slot = st ? (int)__builtin_ctzll(st) : -1;
-        if (!st) mrow = load_row(T, w);  // not staged (rare): HBM load, consumed lazily
-        er_valid = false;
+        if (st) {
+          const int sl = (int)__builtin_ctzll(st);
+          const uint64_t* src = s_cand + (size_t)(sl / kStaged) * kCandStride + kRecRows + (sl % kStaged) * kEvalRowWords;
+          uint64_t* dst = reinterpret_cast<uint64_t*>(&er);
+#pragma unroll
+          for (int q = 0; q < kEvalRowWords; ++q) dst[q] = src[q];
+          er_valid = true;
+        } else {
+          mrow = load_row(T, w);  // not staged (rare): HBM load, consumed lazily
+          dl = PodDelta{};
+          er_valid = false;
+        }
       }
       if (lane == 0) atomicOr(&bitmap[w >> 5], 1u << (w & 31));
       ++nM;
     }
-    // assume: accumulate the pod on the owner lane; keep a materialised EvalRow current incrementally
-    const int64_t prod = (p.flags & P_PROD) ? 1 : 0;
-    if (me) {
-      add_delta(dl, p);
-      er.free_cpu -= p.req_cpu;
-      er.free_mem -= p.req_mem;
-      er.fnz_cpu -= p.nz_cpu;
-      er.fnz_mem -= p.nz_mem;
-      er.la_free_cpu -= p.est_cpu;
-      er.la_free_mem -= p.est_mem;
-      er.la_pfree_cpu -= prod * p.est_cpu;
-      er.la_pfree_mem -= prod * p.est_mem;
-      er.pods_left -= 1;
+    if (me) {  // assume the pod on the owner's row
+      if (er_valid) assume_on(er, p);
+      else add_delta(dl, p);
     }
     if (j == 0 || j == 15 || j == 31) KG_STAMP(2, 2 + j / 8);
   }
   if (lane < nM) {
-    const Row base = slot >= 0 ? row_from_lds(s_rows + (size_t)slot * kRowWords) : mrow;
-    store_mutable(T, midx, with_delta(base, dl));
+    if (er_valid) store_eval_row(T, midx, er);
+    else store_mutable(T, midx, with_delta(mrow, dl));
   }
   if (lane < consumed) out_keys[cursor + lane] = my_out;
   KG_STAMP(2, 30);
@@ -629,6 +611,21 @@ __global__ void apply_deltas(DevTable T, const RowDelta* __restrict__ d, int64_t
   atomicAdd((unsigned long long*)&T.la_pused_mem[k], (unsigned long long)x.d[8]);
 }
 
+__device__ __forceinline__ bool eval_fast_rt(const EvalRow& n, const DevPod& p, const EvalParams& P, uint32_t& t,
+                                             bool& rare) {
+  const int pf = (P.fit_filter ? PF_FIT_FILTER : 0) | (P.fit_score ? PF_FIT_SCORE : 0) |
+                 (P.la_filter ? PF_LA_FILTER : 0) | (P.la_score ? PF_LA_SCORE : 0);
+  switch (pf) {
+#define KG_CASE(X) \
+  case X:          \
+    return eval_fast<X>(n, p, P, t, rare);
+    KG_CASE(0) KG_CASE(1) KG_CASE(2) KG_CASE(3) KG_CASE(4) KG_CASE(5) KG_CASE(6) KG_CASE(7)
+    KG_CASE(8) KG_CASE(9) KG_CASE(10) KG_CASE(11) KG_CASE(12) KG_CASE(13) KG_CASE(14) KG_CASE(15)
+#undef KG_CASE
+  }
+  return false;
+}
+
 // Both evaluation paths on every (pod, node): eval_node (reference-shaped) vs eval_fast (hoisted terms).
 __global__ void debug_eval_paths(DevTable T, const DevPod* __restrict__ pods, int64_t n_pods, int64_t n,
                                  EvalParams P, unsigned long long* __restrict__ mismatches) {
@@ -642,7 +639,7 @@ __global__ void debug_eval_paths(DevTable T, const DevPod* __restrict__ pods, in
     uint32_t t2 = 0;
     const bool f1 = eval_node(r, pods[k], P, t1);
     bool rare = false;
-    const bool f2 = eval_fast(er, pods[k], P, t2, rare);
+    const bool f2 = eval_fast_rt(er, pods[k], P, t2, rare);
     bad += !rare && ((f1 != f2) || (f1 && (uint32_t)t1 != t2));
   }
   if (bad) atomicAdd(mismatches, bad);
@@ -885,7 +882,9 @@ int sync_static(kg_engine* e) {
   auto& h64 = e->h_static64;
   auto& h32 = e->h_static32;
   h64.assign(4 * cap, 0);
-  h32.assign(2 * cap, 0);
+  h32.assign(6 * cap, 0);
+  // 100 / capacity in f32: only an estimate of leastRequestedScore's quotient (corrected exactly on device)
+  auto inv100 = [](int64_t c) -> float { return c > 0 ? (float)(100.0 / (double)c) : 0.0f; };
   for (int64_t i = 0; i < e->n_nodes; ++i) {
     const kg_node& n = e->nodes[i];
     h64[0 * cap + i] = n.allocatable[KG_RES_CPU];
@@ -894,6 +893,9 @@ int sync_static(kg_engine* e) {
     h64[3 * cap + i] = estimate_node(n, KG_RES_MEMORY);
     h32[0 * cap + i] = (int32_t)std::min<int64_t>(n.allowed_pods, INT32_MAX);
     h32[1 * cap + i] = (int32_t)node_flags(e, i);
+    const float f[4] = {inv100(h64[0 * cap + i]), inv100(h64[1 * cap + i]), inv100(h64[2 * cap + i]),
+                        inv100(h64[3 * cap + i])};
+    for (int q = 0; q < 4; ++q) std::memcpy(&h32[(2 + q) * cap + i], &f[q], 4);
   }
   HIP_TRY(hipMemcpyAsync(e->T.alloc_cpu, &h64[0 * cap], cap * 8, hipMemcpyHostToDevice, e->stream));
   HIP_TRY(hipMemcpyAsync(e->T.alloc_mem, &h64[1 * cap], cap * 8, hipMemcpyHostToDevice, e->stream));
@@ -901,6 +903,7 @@ int sync_static(kg_engine* e) {
   HIP_TRY(hipMemcpyAsync(e->T.la_alloc_mem, &h64[3 * cap], cap * 8, hipMemcpyHostToDevice, e->stream));
   HIP_TRY(hipMemcpyAsync(e->T.alloc_pods, &h32[0 * cap], cap * 4, hipMemcpyHostToDevice, e->stream));
   HIP_TRY(hipMemcpyAsync(e->T.flags, (uint32_t*)&h32[1 * cap], cap * 4, hipMemcpyHostToDevice, e->stream));
+  HIP_TRY(hipMemcpyAsync(e->T.inv, &h32[2 * cap], 4 * cap * 4, hipMemcpyHostToDevice, e->stream));
   HIP_TRY(hipStreamSynchronize(e->stream));
   e->static_dirty = false;
   return 0;
@@ -941,33 +944,53 @@ RoundGeom geometry(const kg_engine* e) {
 }
 
 size_t resolve_lds_bytes(const RoundGeom& g) {
-  return ((size_t)g.B * kCandStride + (size_t)g.B * 8 + (size_t)2 * g.B * kRowWords) * 8 + (size_t)g.bitmap_words * 4;
+  return ((size_t)g.B * kCandStride + (size_t)g.B * 8) * 8 + (size_t)g.bitmap_words * 4;
 }
 
 dim3 eval_grid(const RoundGeom& g) {
   return dim3((unsigned)((g.nt_local + kEvalWaves - 1) / kEvalWaves), (unsigned)((g.B + g.ppw - 1) / g.ppw));
 }
 
+int profile_bits(const EvalParams& P) {
+  return (P.fit_filter ? PF_FIT_FILTER : 0) | (P.fit_score ? PF_FIT_SCORE : 0) | (P.la_filter ? PF_LA_FILTER : 0) |
+         (P.la_score ? PF_LA_SCORE : 0);
+}
+
+#define KG_PF_SWITCH(pf, CALL)                                                                   \
+  switch (pf) {                                                                                  \
+    case 0: CALL(0); break;   case 1: CALL(1); break;   case 2: CALL(2); break;   case 3: CALL(3); break;     \
+    case 4: CALL(4); break;   case 5: CALL(5); break;   case 6: CALL(6); break;   case 7: CALL(7); break;     \
+    case 8: CALL(8); break;   case 9: CALL(9); break;   case 10: CALL(10); break; case 11: CALL(11); break;   \
+    case 12: CALL(12); break; case 13: CALL(13); break; case 14: CALL(14); break; case 15: CALL(15); break;   \
+  }
+
 void launch_eval(kg_engine* e, const RoundGeom& g, int64_t end) {
-  eval_round<<<eval_grid(g), kWave * kEvalWaves, 0, e->stream>>>(e->T, e->pods.p, e->cursor.p, end, g.B, g.ppw,
-                                                                  g.base, g.n_local, g.nt_local, e->P, e->lists.p);
+#define KG_EVAL(X)                                                                                                \
+  eval_round<X><<<eval_grid(g), kWave * kEvalWaves, 0, e->stream>>>(e->T, e->pods.p, e->cursor.p, end, g.B, g.ppw, \
+                                                                     g.base, g.n_local, g.nt_local, e->P, e->lists.p)
+  KG_PF_SWITCH(profile_bits(e->P), KG_EVAL)
+#undef KG_EVAL
 }
 
 // local merge: this rank's tile lists → per-pod record (single rank: the final candidates)
 void launch_merge_local(kg_engine* e, const RoundGeom& g, int64_t end) {
   uint64_t* dst = e->n_ranks > 1 ? e->gathered.p + (size_t)e->rank * g.B * kCandStride : e->cand.p;
-  merge_round<false><<<g.B, kMergeThreads, 0, e->stream>>>(e->lists.p, (int64_t)g.nt_local * kR, kR, g.nt_local, kR,
-                                                           e->cursor.p, end, g.B, dst);
+  merge_round<false><<<g.B, kMergeThreads, 0, e->stream>>>(e->T, e->P, e->lists.p, (int64_t)g.nt_local * kR, kR,
+                                                           g.nt_local, kR, e->cursor.p, end, g.B, dst);
 }
 
 void launch_merge_ranks(kg_engine* e, const RoundGeom& g, int64_t end) {
-  merge_round<true><<<g.B, kMergeThreads, 0, e->stream>>>(e->gathered.p, kCandStride, (int64_t)g.B * kCandStride,
-                                                          e->n_ranks, kC, e->cursor.p, end, g.B, e->cand.p);
+  merge_round<true><<<g.B, kMergeThreads, 0, e->stream>>>(e->T, e->P, e->gathered.p, kCandStride,
+                                                          (int64_t)g.B * kCandStride, e->n_ranks, kC, e->cursor.p,
+                                                          end, g.B, e->cand.p);
 }
 
 void launch_resolve(kg_engine* e, const RoundGeom& g, int64_t end) {
-  resolve_round<<<1, kWave, resolve_lds_bytes(g), e->stream>>>(e->T, e->pods.p, e->cursor.p, end, g.B, e->cand.p,
-                                                              e->P, e->out_keys.p, g.bitmap_words, e->cursor.p + 1);
+#define KG_RESOLVE(X)                                                                                               \
+  resolve_round<X><<<1, kWave, resolve_lds_bytes(g), e->stream>>>(e->T, e->pods.p, e->cursor.p, end, g.B, e->cand.p, \
+                                                                 e->P, e->out_keys.p, g.bitmap_words, e->cursor.p + 1)
+  KG_PF_SWITCH(profile_bits(e->P), KG_RESOLVE)
+#undef KG_RESOLVE
 }
 
 int launch_round(kg_engine* e, const RoundGeom& g, int64_t end) {
@@ -1083,8 +1106,8 @@ int kg_engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank, int
   if (hipGetDevice(&e->device) != hipSuccess) return bail(fail(KG_E_DEVICE, "no HIP device"));
   if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) return bail(fail(KG_E_DEVICE, "hipStreamCreate"));
   if (int rc = e->cols64.ensure(12 * cap)) return bail(rc);
-  if (int rc = e->cols32.ensure(3 * cap)) return bail(rc);
-  if (hipMemset(e->cols64.p, 0, 12 * cap * 8) != hipSuccess || hipMemset(e->cols32.p, 0, 3 * cap * 4) != hipSuccess)
+  if (int rc = e->cols32.ensure(7 * cap)) return bail(rc);  // alloc_pods, num_pods, flags, inv[4] (f32)
+  if (hipMemset(e->cols64.p, 0, 12 * cap * 8) != hipSuccess || hipMemset(e->cols32.p, 0, 7 * cap * 4) != hipSuccess)
     return bail(fail(KG_E_DEVICE, "hipMemset"));
   int64_t* c64 = e->cols64.p;
   e->T.alloc_cpu = c64 + 0 * cap;
@@ -1102,6 +1125,8 @@ int kg_engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank, int
   e->T.alloc_pods = e->cols32.p + 0 * cap;
   e->T.num_pods = e->cols32.p + 1 * cap;
   e->T.flags = (uint32_t*)(e->cols32.p + 2 * cap);
+  e->T.inv = (float*)(e->cols32.p + 3 * cap);
+  e->T.cap = cap;
   if (int rc = e->cursor.ensure(4)) return bail(rc);
   if (hipMemset(e->cursor.p, 0, 4 * 8) != hipSuccess) return bail(fail(KG_E_DEVICE, "hipMemset"));
   e->nodes.assign(cap, kg_node{});
@@ -1125,9 +1150,22 @@ int kg_engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank, int
   e->P.score_bits = (int32_t)bits_for(max_total);
   e->P.monotone = 1;  // NodeResourcesFit + LoadAwareScheduling: assume only lowers a node's key
   e->P.inv_la_wsum = 1.0f / (float)e->P.la_wsum;
-  if (hipFuncSetAttribute((const void*)resolve_round, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)(kMaxNodes / 8 + kMaxB * (kCandStride + 8 + 2 * kRowWords) * 8)) != hipSuccess)
-    return bail(fail(KG_E_DEVICE, "hipFuncSetAttribute(resolve_round LDS)"));
+  {
+    const float wc = (float)e->P.fit_w_cpu, wm = (float)e->P.fit_w_mem;
+    e->P.inv_fit_ws[0] = 0.0f;
+    e->P.inv_fit_ws[1] = wc > 0 ? 1.0f / wc : 0.0f;
+    e->P.inv_fit_ws[2] = wm > 0 ? 1.0f / wm : 0.0f;
+    e->P.inv_fit_ws[3] = wc + wm > 0 ? 1.0f / (wc + wm) : 0.0f;
+  }
+  {
+    const int lds = (int)(kMaxNodes / 8 + (size_t)kMaxB * (kCandStride + 8) * 8);
+    hipError_t fe = hipSuccess;
+#define KG_ATTR(X) \
+  fe = hipFuncSetAttribute((const void*)resolve_round<X>, hipFuncAttributeMaxDynamicSharedMemorySize, lds)
+    KG_PF_SWITCH(profile_bits(e->P), KG_ATTR)
+#undef KG_ATTR
+    if (fe != hipSuccess) return bail(fail(KG_E_DEVICE, "hipFuncSetAttribute(resolve_round LDS)"));
+  }
   if (n_ranks > 1) {
     ncclUniqueId id;
     std::memcpy(&id, nccl_id, sizeof(id));

@@ -2,12 +2,14 @@
 //
 // Node state lives in HBM as structure-of-arrays (one column per field, int64 like the reference's
 // framework.Resource fields), replicated on every rank.  A pod is pre-decoded on the host into DevPod
-// (requests, non-zero requests, LoadAware estimate, flags).  eval_node() is the fused body of
+// (requests, non-zero requests, LoadAware estimate, flags).  eval_node() is the fused, reference-shaped body of
 //   upstream NodeResourcesFit.Filter (fitsRequest)       — restated in-tree: reservation/plugin.go:433-482
-//   LoadAwareScheduling.Filter                            — load_aware.go:123-171 (threshold bit precomputed)
+//   LoadAwareScheduling.Filter                            — load_aware.go:123-171 (threshold verdict precomputed)
 //   upstream NodeResourcesFit.Score (LeastAllocated, NonZeroRequested) — nodenumaresource/scoring.go:191-230
 //   LoadAwareScheduling.Score                             — load_aware.go:269-335, scorer :378-397
 //   weighted sum over plugins                             — upstream RunScorePlugins (framework_extender.go:236-258)
+// eval_fast<PF>() is the same function on hoisted per-node terms, specialised at compile time on the profile
+// (PF bits) and branch-free in the pod flags; the two are checked equal on the device (kg_debug_eval_paths).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -21,18 +23,21 @@ constexpr int kWave = 64;
 // build (the macro expands to nothing).
 #ifdef KG_STAMPS
 __device__ unsigned long long g_stamps[4][32][2];
-#define KG_STAMP(kern, point)                                                                  \
-  do {                                                                                         \
-    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {                              \
-      g_stamps[kern][point][0] = __builtin_amdgcn_s_memtime();                                 \
-      g_stamps[kern][point][1] = __builtin_amdgcn_s_memrealtime();                             \
-    }                                                                                          \
+#define KG_STAMP(kern, point)                                                      \
+  do {                                                                             \
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {                  \
+      g_stamps[kern][point][0] = __builtin_amdgcn_s_memtime();                     \
+      g_stamps[kern][point][1] = __builtin_amdgcn_s_memrealtime();                 \
+    }                                                                              \
   } while (0)
 #else
 #define KG_STAMP(kern, point) \
   do {                        \
   } while (0)
 #endif
+
+// profile bits (compile-time specialisation of the evaluation kernels)
+constexpr int PF_FIT_FILTER = 1, PF_FIT_SCORE = 2, PF_LA_FILTER = 4, PF_LA_SCORE = 8;
 
 // node flags (device)
 constexpr uint32_t F_VALID = 1u << 0;
@@ -55,6 +60,8 @@ struct DevTable {
   int64_t *la_pused_cpu, *la_pused_mem;  // Σ EstimatePod(assigned prod pods)      (mutable)
   int32_t *alloc_pods, *num_pods;        // AllowedPodNumber, len(Pods)    (num_pods mutable)
   uint32_t *flags;
+  float *inv;                            // [4][cap]: 100/alloc_cpu, 100/alloc_mem, 100/la_alloc_cpu, 100/la_alloc_mem
+  int64_t cap;                           // column stride of `inv`
 };
 
 struct DevPod {
@@ -75,6 +82,7 @@ struct EvalParams {
   int32_t score_bits;  // bit width of the largest possible weighted total
   int32_t monotone;    // every enabled plugin's key can only drop when a pod is assumed (Fit, LoadAware)
   float inv_la_wsum;
+  float inv_fit_ws[4];  // 1 / Σ fit weights, indexed by (alloc_cpu != 0) | (alloc_mem != 0) << 1
   int32_t pad2;
 };
 
@@ -83,6 +91,7 @@ struct Row {
   int64_t la_alloc_cpu, la_alloc_mem, la_used_cpu, la_used_mem, la_pused_cpu, la_pused_mem;
   int32_t alloc_pods, num_pods;
   uint32_t flags;
+  float inv_cpu, inv_mem, la_inv_cpu, la_inv_mem;
 };
 
 __device__ __forceinline__ Row load_row(const DevTable& T, int64_t i) {
@@ -102,6 +111,10 @@ __device__ __forceinline__ Row load_row(const DevTable& T, int64_t i) {
   r.alloc_pods = T.alloc_pods[i];
   r.num_pods = T.num_pods[i];
   r.flags = T.flags[i];
+  r.inv_cpu = T.inv[i];
+  r.inv_mem = T.inv[T.cap + i];
+  r.la_inv_cpu = T.inv[2 * T.cap + i];
+  r.la_inv_mem = T.inv[3 * T.cap + i];
   return r;
 }
 
@@ -117,31 +130,14 @@ __device__ __forceinline__ void store_mutable(const DevTable& T, int64_t i, cons
   T.num_pods[i] = r.num_pods;
 }
 
-// assume(pod) on a row: upstream NodeInfo.AddPod + LoadAware Reserve → podAssignCache.assign
-// (load_aware.go:260-263; the estimate is EstimatePod, counted because PodsMetric has no entry for it).
-__device__ __forceinline__ void apply_pod(Row& r, const DevPod& p) {
-  r.req_cpu += p.req_cpu;
-  r.req_mem += p.req_mem;
-  r.nz_cpu += p.nz_cpu;
-  r.nz_mem += p.nz_mem;
-  r.num_pods += 1;
-  r.la_used_cpu += p.est_cpu;
-  r.la_used_mem += p.est_mem;
-  if (p.flags & P_PROD) {
-    r.la_pused_cpu += p.est_cpu;
-    r.la_pused_mem += p.est_mem;
-  }
-}
-
 // leastRequestedScore (load_aware.go:388-397; nodenumaresource/least_allocated.go:49-58):
 //   capacity == 0 → 0; requested > capacity → 0; else ((capacity - requested) * 100) / capacity.
-// The quotient lies in [0,100] whenever 0 <= requested <= capacity, so a float estimate is off by at most one
-// and one exact int64 multiply-compare fixes it: no 64-bit integer division on the hot path.
+// Reference-shaped form (exact integer division when outside [0,100]).
 __device__ __forceinline__ int64_t least_requested(int64_t requested, int64_t capacity) {
   if (capacity == 0 || requested > capacity) return 0;
   const int64_t x = capacity - requested;
   const int64_t num = x * 100;
-  if (requested < 0) return num / capacity;  // outside the [0,100] range: exact slow path
+  if (requested < 0) return num / capacity;
   int q = (int)(((float)x * 100.0f) / (float)capacity);
   q = q < 0 ? 0 : (q > 100 ? 100 : q);
   const int64_t t = (int64_t)q * capacity;
@@ -157,8 +153,8 @@ __device__ __forceinline__ int64_t div_small(int64_t s, int64_t w) {
   return s / w;
 }
 
-// Fused Filter + Score of one node for one pod. Returns false when any enabled Filter rejects the node;
-// otherwise writes the weighted total Σ_p weight_p · score_p.
+// Reference-shaped fused Filter + Score of one node for one pod (runtime profile).  Returns false when any
+// enabled Filter rejects the node; otherwise writes the weighted total Σ_p weight_p · score_p.
 __device__ __forceinline__ bool eval_node(const Row& n, const DevPod& p, const EvalParams& P, int64_t& total,
                                           uint32_t* reject = nullptr, int64_t* fit_out = nullptr,
                                           int64_t* la_out = nullptr) {
@@ -216,15 +212,9 @@ __device__ __forceinline__ uint64_t make_key(int64_t total, uint32_t node) {
 }
 __device__ __forceinline__ uint32_t key_node(uint64_t k) { return 0xFFFFFFFFu - (uint32_t)k; }
 
-__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) {
-    const uint64_t o = __shfl_xor(v, off, kWave);
-    v = o > v ? o : v;
-  }
-  return v;
-}
-
+// ---------------------------------------------------------------------------------------------------
+// wave primitives
+// ---------------------------------------------------------------------------------------------------
 // DPP max-reduction over the wave (gfx9 row_shr 1/2/4/8, row_bcast 15/31): result valid in lane 63,
 // returned wave-uniform via readlane.  Lanes whose DPP source is out of row read the identity 0.
 template <int CTRL, int ROW_MASK>
@@ -270,13 +260,8 @@ __device__ __forceinline__ uint64_t readlane_u64(uint64_t v, int lane) {
   return ((uint64_t)hi << 32) | lo;
 }
 
-}  // namespace kg
-
-namespace kg {
-
 // ---------------------------------------------------------------------------------------------------
-// Wide-pass evaluation with per-node terms hoisted out of the per-pod loop.  Must agree bit-for-bit with
-// eval_node (checked on the device by kg_debug_eval_paths).
+// Wide-pass evaluation on hoisted per-node terms (no division: capacities' reciprocals are static columns).
 // ---------------------------------------------------------------------------------------------------
 struct EvalRow {
   int64_t free_cpu, free_mem;          // Allocatable - Requested                 (fitsRequest)
@@ -289,15 +274,17 @@ struct EvalRow {
   float inv_fit_ws;                    // 1 / Σ fit weights of resources with non-zero allocatable
   int32_t fit_ws;
   int32_t pods_left;                   // AllowedPodNumber - len(Pods) - 1  (fits iff ≥ 0)
+  int32_t alloc_pods;
   uint32_t flags;
+  uint32_t pad;
 };
+static_assert(sizeof(EvalRow) == 136, "EvalRow layout");
+constexpr int kEvalRowWords = 17;  // 136 B in uint64 words
 
 __device__ __forceinline__ float i64_to_f32(int64_t x) {  // x ≥ 0; ~1 ulp, enough for a ±1 quotient estimate
   const uint64_t u = (uint64_t)x;
   return fmaf((float)(uint32_t)(u >> 32), 4294967296.0f, (float)(uint32_t)u);
 }
-
-__device__ __forceinline__ float inv100(int64_t cap) { return cap > 0 ? 100.0f / i64_to_f32(cap) : 0.0f; }
 
 __device__ __forceinline__ EvalRow make_eval_row(const Row& r, const EvalParams& P) {
   EvalRow e;
@@ -313,18 +300,70 @@ __device__ __forceinline__ EvalRow make_eval_row(const Row& r, const EvalParams&
   e.la_free_mem = r.la_alloc_mem - r.la_used_mem;
   e.la_pfree_cpu = r.la_alloc_cpu - r.la_pused_cpu;
   e.la_pfree_mem = r.la_alloc_mem - r.la_pused_mem;
-  e.inv_cpu = inv100(r.alloc_cpu);
-  e.inv_mem = inv100(r.alloc_mem);
-  e.la_inv_cpu = inv100(r.la_alloc_cpu);
-  e.la_inv_mem = inv100(r.la_alloc_mem);
-  int32_t ws = 0;
-  if (P.fit_w_cpu && r.alloc_cpu != 0) ws += (int32_t)P.fit_w_cpu;
-  if (P.fit_w_mem && r.alloc_mem != 0) ws += (int32_t)P.fit_w_mem;
-  e.fit_ws = ws;
-  e.inv_fit_ws = ws ? 1.0f / (float)ws : 0.0f;
+  e.inv_cpu = r.inv_cpu;
+  e.inv_mem = r.inv_mem;
+  e.la_inv_cpu = r.la_inv_cpu;
+  e.la_inv_mem = r.la_inv_mem;
+  const bool hc = P.fit_w_cpu && r.alloc_cpu != 0, hm = P.fit_w_mem && r.alloc_mem != 0;
+  e.fit_ws = (hc ? (int32_t)P.fit_w_cpu : 0) + (hm ? (int32_t)P.fit_w_mem : 0);
+  e.inv_fit_ws = hc ? (hm ? P.inv_fit_ws[3] : P.inv_fit_ws[1]) : (hm ? P.inv_fit_ws[2] : 0.0f);
   e.pods_left = r.alloc_pods - r.num_pods - 1;
+  e.alloc_pods = r.alloc_pods;
   e.flags = r.flags;
+  e.pad = 0;
   return e;
+}
+
+// assume(pod) on a hoisted row: upstream NodeInfo.AddPod + LoadAware Reserve → podAssignCache.assign
+// (load_aware.go:260-263).  Capacities and reciprocals are unchanged; only the free terms move.
+__device__ __forceinline__ void assume_on(EvalRow& e, const DevPod& p) {
+  const int64_t prod = (p.flags & P_PROD) ? 1 : 0;
+  e.free_cpu -= p.req_cpu;
+  e.free_mem -= p.req_mem;
+  e.fnz_cpu -= p.nz_cpu;
+  e.fnz_mem -= p.nz_mem;
+  e.la_free_cpu -= p.est_cpu;
+  e.la_free_mem -= p.est_mem;
+  e.la_pfree_cpu -= prod * p.est_cpu;
+  e.la_pfree_mem -= prod * p.est_mem;
+  e.pods_left -= 1;
+}
+
+// Mutable columns recovered from a hoisted row (inverse of make_eval_row).
+__device__ __forceinline__ void store_eval_row(const DevTable& T, int64_t i, const EvalRow& e) {
+  T.req_cpu[i] = e.alloc_cpu - e.free_cpu;
+  T.req_mem[i] = e.alloc_mem - e.free_mem;
+  T.nz_cpu[i] = e.alloc_cpu - e.fnz_cpu;
+  T.nz_mem[i] = e.alloc_mem - e.fnz_mem;
+  T.la_used_cpu[i] = e.la_alloc_cpu - e.la_free_cpu;
+  T.la_used_mem[i] = e.la_alloc_mem - e.la_free_mem;
+  T.la_pused_cpu[i] = e.la_alloc_cpu - e.la_pfree_cpu;
+  T.la_pused_mem[i] = e.la_alloc_mem - e.la_pfree_mem;
+  T.num_pods[i] = e.alloc_pods - e.pods_left - 1;
+}
+
+__device__ __forceinline__ Row row_of(const EvalRow& e) {  // the reference-shaped row behind a hoisted one
+  Row r;
+  r.alloc_cpu = e.alloc_cpu;
+  r.alloc_mem = e.alloc_mem;
+  r.req_cpu = e.alloc_cpu - e.free_cpu;
+  r.req_mem = e.alloc_mem - e.free_mem;
+  r.nz_cpu = e.alloc_cpu - e.fnz_cpu;
+  r.nz_mem = e.alloc_mem - e.fnz_mem;
+  r.la_alloc_cpu = e.la_alloc_cpu;
+  r.la_alloc_mem = e.la_alloc_mem;
+  r.la_used_cpu = e.la_alloc_cpu - e.la_free_cpu;
+  r.la_used_mem = e.la_alloc_mem - e.la_free_mem;
+  r.la_pused_cpu = e.la_alloc_cpu - e.la_pfree_cpu;
+  r.la_pused_mem = e.la_alloc_mem - e.la_pfree_mem;
+  r.alloc_pods = e.alloc_pods;
+  r.num_pods = e.alloc_pods - e.pods_left - 1;
+  r.flags = e.flags;
+  r.inv_cpu = e.inv_cpu;
+  r.inv_mem = e.inv_mem;
+  r.la_inv_cpu = e.la_inv_cpu;
+  r.la_inv_mem = e.la_inv_mem;
+  return r;
 }
 
 // leastRequestedScore with x = capacity - requested precomputed: ((x * 100) / capacity), 0 when x < 0 or
@@ -350,33 +389,39 @@ __device__ __forceinline__ int32_t div_est(int32_t s, int32_t w, float inv_w) {
   return q;
 }
 
-// Branch-free fused Filter + Score on hoisted terms.  Returns feasibility; sets `rare` when an input lies
-// outside the fast path's domain (a negative Requested) — the caller then re-evaluates with eval_node.
+// Branch-free fused Filter + Score on hoisted terms, specialised on the profile PF.  Returns feasibility;
+// sets `rare` when an input lies outside the fast path's domain (a negative Requested) — the caller then
+// re-evaluates with eval_node.
+template <int PF>
 __device__ __forceinline__ bool eval_fast(const EvalRow& n, const DevPod& p, const EvalParams& P, uint32_t& total,
                                           bool& rare) {
+  const uint32_t pf = p.flags;
   bool ok = (n.flags & F_VALID) != 0;
-  if (P.fit_filter) {
-    ok &= n.pods_left >= 0;
-    if (!(p.flags & P_ZERO_REQ)) ok &= (p.req_cpu <= n.free_cpu) & (p.req_mem <= n.free_mem);
+  if constexpr ((PF & PF_FIT_FILTER) != 0) {
+    const bool fits = (p.req_cpu <= n.free_cpu) & (p.req_mem <= n.free_mem);
+    ok = ok & (n.pods_left >= 0) & (((pf & P_ZERO_REQ) != 0) | fits);
   }
-  if (P.la_filter && !(p.flags & P_DAEMONSET)) ok &= (n.flags & ((p.flags & P_PROD) ? F_LA_PASS_PROD : F_LA_PASS)) != 0;
+  if constexpr ((PF & PF_LA_FILTER) != 0) {
+    const uint32_t passbit = (pf & P_PROD) ? F_LA_PASS_PROD : F_LA_PASS;
+    ok = ok & (((pf & P_DAEMONSET) != 0) | ((n.flags & passbit) != 0));
+  }
   int32_t t = 0;
-  if (P.fit_score) {
-    int32_t s = 0;
+  if constexpr ((PF & PF_FIT_SCORE) != 0) {
     const int32_t qc = lrs_x(n.fnz_cpu - p.nz_cpu, n.alloc_cpu, n.inv_cpu, rare);
     const int32_t qm = lrs_x(n.fnz_mem - p.nz_mem, n.alloc_mem, n.inv_mem, rare);
-    if (P.fit_w_cpu) s += qc * (int32_t)P.fit_w_cpu;
-    if (P.fit_w_mem) s += qm * (int32_t)P.fit_w_mem;
-    t += n.fit_ws ? div_est(s, n.fit_ws, n.inv_fit_ws) * (int32_t)P.weight_fit : 0;
+    const int32_t s = qc * (int32_t)P.fit_w_cpu + qm * (int32_t)P.fit_w_mem;
+    const int32_t f = div_est(s, n.fit_ws, n.inv_fit_ws);
+    t += (n.fit_ws ? f : 0) * (int32_t)P.weight_fit;
   }
-  if (P.la_score) {
-    const bool prodv = (p.flags & P_LA_PROD_SCORE) != 0;
-    const int32_t qc = lrs_x((prodv ? n.la_pfree_cpu : n.la_free_cpu) - p.est_cpu, n.la_alloc_cpu, n.la_inv_cpu, rare);
-    const int32_t qm = lrs_x((prodv ? n.la_pfree_mem : n.la_free_mem) - p.est_mem, n.la_alloc_mem, n.la_inv_mem, rare);
-    int32_t s = 0;
-    if (P.la_w_cpu) s += qc * (int32_t)P.la_w_cpu;
-    if (P.la_w_mem) s += qm * (int32_t)P.la_w_mem;
-    t += (n.flags & F_LA_SCORE) ? div_est(s, (int32_t)P.la_wsum, P.inv_la_wsum) * (int32_t)P.weight_la : 0;
+  if constexpr ((PF & PF_LA_SCORE) != 0) {
+    const bool prodv = (pf & P_LA_PROD_SCORE) != 0;
+    const int64_t fc = prodv ? n.la_pfree_cpu : n.la_free_cpu;
+    const int64_t fm = prodv ? n.la_pfree_mem : n.la_free_mem;
+    const int32_t qc = lrs_x(fc - p.est_cpu, n.la_alloc_cpu, n.la_inv_cpu, rare);
+    const int32_t qm = lrs_x(fm - p.est_mem, n.la_alloc_mem, n.la_inv_mem, rare);
+    const int32_t s = qc * (int32_t)P.la_w_cpu + qm * (int32_t)P.la_w_mem;
+    const int32_t l = div_est(s, (int32_t)P.la_wsum, P.inv_la_wsum);
+    t += ((n.flags & F_LA_SCORE) ? l : 0) * (int32_t)P.weight_la;
   }
   total = (uint32_t)t;
   return ok;
