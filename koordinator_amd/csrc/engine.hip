@@ -388,10 +388,11 @@ __global__ __launch_bounds__(kMergeThreads) void merge_round(DevTable T, EvalPar
     // hoisted rows of the kStaged best candidates (the resolver's likely winners)
     if (lane < n_sel && rank < kStaged) {
       const EvalRow er = make_eval_row(load_row(T, key_node(v)), P);
-      const uint64_t* src = reinterpret_cast<const uint64_t*>(&er);
+      uint64_t words[kEvalRowWords];
+      __builtin_memcpy(words, &er, sizeof(er));  // well-defined type punning (no strict-aliasing hazard)
       uint64_t* dst = o + kRecRows + rank * kEvalRowWords;
 #pragma unroll
-      for (int w = 0; w < kEvalRowWords; ++w) dst[w] = src[w];
+      for (int w = 0; w < kEvalRowWords; ++w) dst[w] = words[w];
     }
   }
   KG_STAMP(1, 14);
@@ -475,11 +476,18 @@ __global__ __launch_bounds__(kWave) void resolve_round(DevTable T, const DevPod*
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   KG_STAMP(2, 1);
-  // lane l < kStaged·nb: node whose hoisted row sits in record l / kStaged, slot l % kStaged
-  uint32_t staged = 0xFFFFFFFFu;
-  if (lane < kStaged * nb) {
-    const uint64_t kk = s_cand[(size_t)(lane / kStaged) * kCandStride + (lane % kStaged)];
-    staged = kk ? key_node(kk) : 0xFFFFFFFFu;
+  // staged[q] on lane l: node whose hoisted row sits at staged slot s = q·64 + l (record s / kStaged,
+  // position s % kStaged of that pod's list)
+  constexpr int kSlotsPerLane = (kStaged * kMaxB + kWave - 1) / kWave;
+  uint32_t staged[kSlotsPerLane];
+#pragma unroll
+  for (int q = 0; q < kSlotsPerLane; ++q) {
+    const int sl = q * kWave + lane;
+    staged[q] = 0xFFFFFFFFu;
+    if (sl < kStaged * nb) {
+      const uint64_t kk = s_cand[(size_t)(sl / kStaged) * kCandStride + (sl % kStaged)];
+      staged[q] = kk ? key_node(kk) : 0xFFFFFFFFu;
+    }
   }
   const DevPod* s_pods = reinterpret_cast<const DevPod*>(s_podw);
 
@@ -537,15 +545,20 @@ __global__ __launch_bounds__(kWave) void resolve_round(DevTable T, const DevPod*
     const int owner = hit ? (int)__builtin_ctzll(hit) : nM;
     const bool me = lane == owner;
     if (!hit) {
-      const uint64_t st = __ballot(staged == w);
+      int sl = -1;
+#pragma unroll
+      for (int q = 0; q < kSlotsPerLane; ++q) {
+        const uint64_t b = __ballot(staged[q] == w);
+        if (sl < 0 && b) sl = q * kWave + (int)__builtin_ctzll(b);
+      }
       if (me) {
         midx = w;
-        if (st) {
-          const int sl = (int)__builtin_ctzll(st);
+        if (sl >= 0) {
           const uint64_t* src = s_cand + (size_t)(sl / kStaged) * kCandStride + kRecRows + (sl % kStaged) * kEvalRowWords;
-          uint64_t* dst = reinterpret_cast<uint64_t*>(&er);
+          uint64_t words[kEvalRowWords];
 #pragma unroll
-          for (int q = 0; q < kEvalRowWords; ++q) dst[q] = src[q];
+          for (int q = 0; q < kEvalRowWords; ++q) words[q] = src[q];
+          __builtin_memcpy(&er, words, sizeof(er));  // well-defined type punning
           er_valid = true;
         } else {
           mrow = load_row(T, w);  // not staged (rare): HBM load, consumed lazily
