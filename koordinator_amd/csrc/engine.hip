@@ -492,9 +492,12 @@ __global__ __launch_bounds__(kWave) void resolve_round(DevTable T, const DevPod*
   const DevPod* s_pods = reinterpret_cast<const DevPod*>(s_podw);
 
   uint32_t midx = 0xFFFFFFFFu;
+  // lane state (lane < nM): rsrc ≥ 0 → base hoisted row at staged slot rsrc (LDS), rsrc == -1 → base Row `mrow`
+  // (HBM load in flight); `dl` = pods assumed since the base; `er` = materialised current row when er_valid.
+  int rsrc = -1;
   EvalRow er;
   er.flags = 0;
-  bool er_valid = false;  // false: base row `mrow` (HBM load in flight) + `dl` not yet materialised
+  bool er_valid = false;
   Row mrow;
   mrow.flags = 0;
   PodDelta dl = {};
@@ -503,24 +506,36 @@ __global__ __launch_bounds__(kWave) void resolve_round(DevTable T, const DevPod*
   int consumed = 0;
   uint64_t key_n = s_cand[lane];
   uint64_t ub_n = s_cand[kC];
+  DevPod p_n = s_pods[0];
   for (int j = 0; j < nb; ++j) {
     const uint64_t key = key_n, ub = ub_n;
-    const int jn = j + 1 < nb ? j + 1 : j;  // software prefetch of the next pod's list (branch-free)
+    const DevPod p = p_n;
+    const int jn = j + 1 < nb ? j + 1 : j;  // software prefetch of the next pod (branch-free)
     key_n = s_cand[(size_t)jn * kCandStride + lane];
     ub_n = s_cand[(size_t)jn * kCandStride + kC];
-    const uint32_t node = key ? key_node(key) : 0u;
-    const uint32_t word = bitmap[node >> 5];
-    const bool unmod = key != 0 && !((word >> (node & 31)) & 1u);
+    p_n = s_pods[jn];
+    const uint32_t node = key_node(key);  // key 0 → node 0xFFFFFFFF: masked below, word index clamped
+    const uint32_t word = bitmap[(key ? node : 0u) >> 5];
+    const bool unmod = (key != 0) & !((word >> (node & 31)) & 1u);
     const uint64_t um = __ballot(unmod);
     const int pos = um ? (int)__builtin_ctzll(um) : kC;
     const uint64_t e = um ? readlane_u64(key, pos) : 0;
-    const DevPod p = s_pods[j];
     uint64_t best = e;
     if (nM > 0 && (!P.monotone || pos > 0)) {  // slow path: re-score this round's modified rows
       uint64_t mk = 0;
       if (lane < nM) {
-        if (!er_valid) {  // non-staged winner: materialise from the HBM row + the pods assumed since
-          er = make_eval_row(with_delta(mrow, dl), P);
+        if (!er_valid) {  // materialise: staged hoisted row (LDS) or HBM row, plus the pods assumed since
+          if (rsrc >= 0) {
+            const uint64_t* src = s_cand + (size_t)(rsrc / kStaged) * kCandStride + kRecRows +
+                                  (rsrc % kStaged) * kEvalRowWords;
+            uint64_t words[kEvalRowWords];
+#pragma unroll
+            for (int q = 0; q < kEvalRowWords; ++q) words[q] = src[q];
+            __builtin_memcpy(&er, words, sizeof(er));
+            er = make_eval_row(with_delta(row_of(er), dl), P);
+          } else {
+            er = make_eval_row(with_delta(mrow, dl), P);
+          }
           er_valid = true;
         }
         uint32_t t = 0;
@@ -541,7 +556,7 @@ __global__ __launch_bounds__(kWave) void resolve_round(DevTable T, const DevPod*
     ++consumed;
     if (best == 0) continue;  // unschedulable (ub == 0: no feasible node anywhere)
     const uint32_t w = key_node(best);
-    const uint64_t hit = __ballot(lane < nM && midx == w);
+    const uint64_t hit = __ballot((lane < nM) & (midx == w));
     const int owner = hit ? (int)__builtin_ctzll(hit) : nM;
     const bool me = lane == owner;
     if (!hit) {
@@ -553,31 +568,34 @@ __global__ __launch_bounds__(kWave) void resolve_round(DevTable T, const DevPod*
       }
       if (me) {
         midx = w;
-        if (sl >= 0) {
-          const uint64_t* src = s_cand + (size_t)(sl / kStaged) * kCandStride + kRecRows + (sl % kStaged) * kEvalRowWords;
-          uint64_t words[kEvalRowWords];
-#pragma unroll
-          for (int q = 0; q < kEvalRowWords; ++q) words[q] = src[q];
-          __builtin_memcpy(&er, words, sizeof(er));  // well-defined type punning
-          er_valid = true;
-        } else {
-          mrow = load_row(T, w);  // not staged (rare): HBM load, consumed lazily
-          dl = PodDelta{};
-          er_valid = false;
-        }
+        rsrc = sl;
+        dl = PodDelta{};
+        er_valid = false;
+        if (sl < 0) mrow = load_row(T, w);  // not staged (rare): HBM load, consumed lazily
       }
       if (lane == 0) atomicOr(&bitmap[w >> 5], 1u << (w & 31));
       ++nM;
     }
     if (me) {  // assume the pod on the owner's row
       if (er_valid) assume_on(er, p);
-      else add_delta(dl, p);
+      add_delta(dl, p);
     }
     if (j == 0 || j == 15 || j == 31) KG_STAMP(2, 2 + j / 8);
   }
   if (lane < nM) {
-    if (er_valid) store_eval_row(T, midx, er);
-    else store_mutable(T, midx, with_delta(mrow, dl));
+    if (er_valid) {
+      store_eval_row(T, midx, er);
+    } else if (rsrc >= 0) {
+      const uint64_t* src = s_cand + (size_t)(rsrc / kStaged) * kCandStride + kRecRows + (rsrc % kStaged) * kEvalRowWords;
+      uint64_t words[kEvalRowWords];
+#pragma unroll
+      for (int q = 0; q < kEvalRowWords; ++q) words[q] = src[q];
+      EvalRow base;
+      __builtin_memcpy(&base, words, sizeof(base));
+      store_mutable(T, midx, with_delta(row_of(base), dl));
+    } else {
+      store_mutable(T, midx, with_delta(mrow, dl));
+    }
   }
   if (lane < consumed) out_keys[cursor + lane] = my_out;
   KG_STAMP(2, 30);
