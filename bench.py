@@ -140,6 +140,8 @@ def main():
     for k in range(args.steps):
         st = e.schedule_staged(k * args.pods_per_step, args.pods_per_step)
         rounds += int(st["device_batches"])
+        if d.rank == 0:
+            print(f"[bench] step {k + 1}/{args.steps} done", file=sys.stderr, flush=True)
     t1 = time.perf_counter()
     d.barrier()
     elapsed = d.max(t1 - t0)
@@ -169,6 +171,7 @@ def main():
 
     cpu = None
     if d.rank == 0 and d.world == 1 and not args.no_cpu_baseline:
+        print("[bench] cpu baseline sample", file=sys.stderr, flush=True)
         m, dt = cpu_baseline(cfg, cluster, pods, args.cpu_seconds, args.cpu_threads)
         cpu = {"value": m / dt, "unit": "pods/s", "cores": args.cpu_threads, "kind": "port",
                "sample": f"first {m} pods of the same queue after a 64-pod probe, {cluster.n} nodes, "

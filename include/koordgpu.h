@@ -214,6 +214,11 @@ int kg_bench_kernel(kg_engine* e, int which, int iters, double* avg_ms, double* 
  * division-free path). */
 int kg_debug_least_requested(kg_engine* e, const int64_t* requested, const int64_t* capacity, int64_t* out,
                              int64_t n);
+/* Debug: the wide pass's division-free leastRequestedScore on n (requested, capacity) pairs — the 32-bit
+ * cpu-term routine into out_cpu and the f64 memory-term routine into out_mem (-1 where a pair lies outside
+ * that routine's exact domain; the engine sends such rows to the exact path). */
+int kg_debug_fast_lrs(kg_engine* e, const int64_t* requested, const int64_t* capacity, int64_t* out_cpu,
+                      int64_t* out_mem, int64_t n);
 
 /* Debug: evaluates every staged pod on every node with both device evaluation paths (the reference-shaped
  * one used for modified rows and per-plugin output, and the hoisted-term one of the wide pass) and returns

@@ -94,7 +94,7 @@ EXPORTED_SYMBOLS = (
     "kg_node_metrics_update", "kg_pods_add", "kg_pods_remove", "kg_pods_schedule", "kg_pods_evaluate",
     "kg_pods_stage", "kg_pods_schedule_staged", "kg_results_fetch", "kg_engine_num_nodes",
     "kg_nodes_read_state", "kg_bench_kernel", "kg_debug_least_requested", "kg_last_error", "kg_abi_version",
-    "kg_abi_struct_size", "kg_nccl_unique_id", "kg_debug_eval_paths", "kg_debug_stamps",
+    "kg_abi_struct_size", "kg_nccl_unique_id", "kg_debug_eval_paths", "kg_debug_stamps", "kg_debug_fast_lrs",
 )
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
@@ -145,6 +145,7 @@ def load_library(path: str | None = None):
         "kg_nccl_unique_id": (i, [vp]),
         "kg_debug_eval_paths": (i, [vp, vp]),
         "kg_debug_stamps": (i, [vp, vp]),
+        "kg_debug_fast_lrs": (i, [vp, vp, vp, vp, vp, i64]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)

@@ -42,6 +42,7 @@ constexpr int kRecRows = 72;          // record layout (uint64 words): [0,kC) ke
 constexpr int kCandStride = 128;      // per-pod record: 1 KiB (a 16-B multiple, for LDS-DMA)
 constexpr int kMergeThreads = 256;
 constexpr int kMergeChunks = 4;       // chunks of 8 keys per merge thread: ≤ 1024 tile lists = 262144 nodes per rank
+constexpr double kAlgoBytesPerNode = 76.0;  // SURVEY §8(d) b_node for C1-C3: Fit 56 B + LoadAware 20 B
 constexpr int64_t kMaxNodes = 1 << 19;  // resolver LDS: N/8-byte bitmap (≤ 64 KiB) + the round's records (≤ 64 KiB)
 static_assert(kRecRows + kStaged * kEvalRowWords <= kCandStride, "record layout");
 
@@ -90,9 +91,15 @@ __global__ __launch_bounds__(kWave* kEvalWaves) void eval_round(DevTable T, cons
   if (cursor >= end) return;
   const int nb = (end - cursor) < (int64_t)B ? (int)(end - cursor) : B;
   const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
-  const int tile = blockIdx.x * kEvalWaves + wave;
+  // XCD-aware swizzle (bijective for any grid size): the blocks of one tile group — one per pod group — get
+  // consecutive ids on the same XCD label, so the group's node rows come from HBM once and from that XCD's
+  // L2 for the other pod groups (the straight grid spread them over all 8 L2s: ~12x the table per launch).
+  const int n_pg = (B + pods_per_wave - 1) / pods_per_wave;
+  const uint32_t nwg = gridDim.x, bid = blockIdx.x, xcd = bid % 8u, q = nwg / 8u, r = nwg % 8u;
+  const uint32_t wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8u;
+  const int tile = (int)(wgid / (uint32_t)n_pg) * kEvalWaves + wave;
   KG_STAMP(0, 1);
-  const int p0 = blockIdx.y * pods_per_wave;
+  const int p0 = (int)(wgid % (uint32_t)n_pg) * pods_per_wave;
   if (tile >= nt_local || p0 >= nb) return;
   const int p1 = (p0 + pods_per_wave) < nb ? (p0 + pods_per_wave) : nb;
 
@@ -122,7 +129,13 @@ __global__ __launch_bounds__(kWave* kEvalWaves) void eval_round(DevTable T, cons
       tot[j] = 0;
       okv[j] = eval_fast<PF>(rows[j], p, P, tot[j], rare);
     }
-    if (__ballot(rare)) {  // negative Requested somewhere in the tile: exact reference-shaped path
+#ifdef KG_STAMPS
+    if (lane == 0) {
+      atomicAdd(&g_stamps[3][0][0], 1ull);
+      if (__ballot(rare)) atomicAdd(&g_stamps[3][0][1], 1ull);
+    }
+#endif
+    if (__ballot(rare)) {  // a row outside eval_fast's exact domain in the tile: exact reference-shaped path
 #pragma unroll
       for (int j = 0; j < kNPT; ++j) {
         const int64_t local = (int64_t)tile * kTile + j * kWave + lane;
@@ -453,8 +466,8 @@ __global__ __launch_bounds__(kWave) void resolve_round(DevTable T, const DevPod*
   if (cursor >= end) return;
   const int nb = (end - cursor) < (int64_t)B ? (int)(end - cursor) : B;
   uint64_t* s_cand = smem;                                            // [B][kCandStride]
-  uint64_t* s_podw = s_cand + (size_t)B * kCandStride;                // [B] DevPod (8 words)
-  uint32_t* bitmap = reinterpret_cast<uint32_t*>(s_podw + (size_t)B * 8);
+  uint64_t* s_podw = s_cand + (size_t)B * kCandStride;                // [B] DevPod (kPodWords words)
+  uint32_t* bitmap = reinterpret_cast<uint32_t*>(s_podw + (size_t)B * kPodWords);
   {  // prologue: LDS-DMA of records + pods, bitmap clear
     const int n16 = nb * kCandStride / 2;
     for (int it = 0; it * kWave < n16; ++it) {
@@ -464,7 +477,7 @@ __global__ __launch_bounds__(kWave) void resolve_round(DevTable T, const DevPod*
                                          (lds_void_ptr)(s_cand + 2 * (size_t)it * kWave), 16, 0, 0);
     }
     const uint64_t* pw = reinterpret_cast<const uint64_t*>(pods + cursor);
-    const int p16 = nb * 4;
+    const int p16 = nb * kPodWords / 2;
     for (int it = 0; it * kWave < p16; ++it) {
       const int idx = it * kWave + lane;
       if (idx < p16)
@@ -577,7 +590,7 @@ __global__ __launch_bounds__(kWave) void resolve_round(DevTable T, const DevPod*
       ++nM;
     }
     if (me) {  // assume the pod on the owner's row
-      if (er_valid) assume_on(er, p);
+      if (er_valid) assume_on(er, p, P);
       add_delta(dl, p);
     }
     if (j == 0 || j == 15 || j == 31) KG_STAMP(2, 2 + j / 8);
@@ -681,6 +694,16 @@ __global__ void debug_least_requested(const int64_t* req, const int64_t* cap, in
   if (i < n) out[i] = least_requested(req[i], cap[i]);
 }
 
+__global__ void debug_fast_lrs(const int64_t* req, const int64_t* cap, int64_t* out_cpu, int64_t* out_mem, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t c = cap[i], fr = c - req[i];
+  // reciprocals exactly as sync_static computes the static columns (correctly rounded f64 division)
+  const double invd = c > 0 ? 100.0 / (double)c : 0.0;
+  out_cpu[i] = cpu_dom(c, fr) ? lrs_cpu((int32_t)fr, (int32_t)c, (float)invd) : -1;
+  out_mem[i] = mem_dom(c, fr) ? lrs_mem((double)fr, (double)c, invd) : -1;
+}
+
 // ------------------------------------------------------------------------------------------------
 // Host side
 // ------------------------------------------------------------------------------------------------
@@ -744,6 +767,7 @@ struct kg_engine {
   DevBuf<int32_t> scratch32;
   std::vector<int64_t> h_static64;
   std::vector<int32_t> h_static32;
+  std::vector<double> h_static_f64;
 };
 
 namespace {
@@ -884,11 +908,15 @@ int decode_pod(const kg_engine* e, const kg_pod& p, DevPod& d) {
   estimate_pod(c, p, est);
   d.est_cpu = est[0];
   d.est_mem = est[1];
+  d.nz_mem_d = (double)d.nz_mem;
+  d.est_mem_d = (double)d.est_mem;
+  d.nz_cpu32 = (int32_t)std::min<int64_t>(d.nz_cpu, kPodCpu32Max);
+  d.est_cpu32 = (int32_t)std::min<int64_t>(d.est_cpu, kPodCpu32Max);
   d.flags = (zero ? P_ZERO_REQ : 0) | ((p.flags & KG_POD_DAEMONSET) ? P_DAEMONSET : 0) |
             (p.priority_class == KG_PRIO_PROD ? P_PROD : 0) |
             (p.priority_class == KG_PRIO_PROD && c.la_score_according_prod_usage ? P_LA_PROD_SCORE : 0);
   d.pad = 0;
-  d.pad2 = 0;
+  d.pad2[0] = d.pad2[1] = 0;
   return 0;
 }
 
@@ -913,9 +941,13 @@ int sync_static(kg_engine* e) {
   auto& h64 = e->h_static64;
   auto& h32 = e->h_static32;
   h64.assign(4 * cap, 0);
-  h32.assign(6 * cap, 0);
-  // 100 / capacity in f32: only an estimate of leastRequestedScore's quotient (corrected exactly on device)
+  h32.assign(4 * cap, 0);
+  auto& hd = e->h_static_f64;
+  hd.assign(2 * cap, 0.0);
+  // 100 / capacity: only estimates of leastRequestedScore's quotient (corrected exactly on device); f32 for the
+  // cpu terms, f64 (correctly rounded) for the memory terms
   auto inv100 = [](int64_t c) -> float { return c > 0 ? (float)(100.0 / (double)c) : 0.0f; };
+  auto inv100d = [](int64_t c) -> double { return c > 0 ? 100.0 / (double)c : 0.0; };
   for (int64_t i = 0; i < e->n_nodes; ++i) {
     const kg_node& n = e->nodes[i];
     h64[0 * cap + i] = n.allocatable[KG_RES_CPU];
@@ -924,9 +956,10 @@ int sync_static(kg_engine* e) {
     h64[3 * cap + i] = estimate_node(n, KG_RES_MEMORY);
     h32[0 * cap + i] = (int32_t)std::min<int64_t>(n.allowed_pods, INT32_MAX);
     h32[1 * cap + i] = (int32_t)node_flags(e, i);
-    const float f[4] = {inv100(h64[0 * cap + i]), inv100(h64[1 * cap + i]), inv100(h64[2 * cap + i]),
-                        inv100(h64[3 * cap + i])};
-    for (int q = 0; q < 4; ++q) std::memcpy(&h32[(2 + q) * cap + i], &f[q], 4);
+    const float f[2] = {inv100(h64[0 * cap + i]), inv100(h64[2 * cap + i])};
+    for (int q = 0; q < 2; ++q) std::memcpy(&h32[(2 + q) * cap + i], &f[q], 4);
+    hd[0 * cap + i] = inv100d(h64[1 * cap + i]);
+    hd[1 * cap + i] = inv100d(h64[3 * cap + i]);
   }
   HIP_TRY(hipMemcpyAsync(e->T.alloc_cpu, &h64[0 * cap], cap * 8, hipMemcpyHostToDevice, e->stream));
   HIP_TRY(hipMemcpyAsync(e->T.alloc_mem, &h64[1 * cap], cap * 8, hipMemcpyHostToDevice, e->stream));
@@ -934,7 +967,8 @@ int sync_static(kg_engine* e) {
   HIP_TRY(hipMemcpyAsync(e->T.la_alloc_mem, &h64[3 * cap], cap * 8, hipMemcpyHostToDevice, e->stream));
   HIP_TRY(hipMemcpyAsync(e->T.alloc_pods, &h32[0 * cap], cap * 4, hipMemcpyHostToDevice, e->stream));
   HIP_TRY(hipMemcpyAsync(e->T.flags, (uint32_t*)&h32[1 * cap], cap * 4, hipMemcpyHostToDevice, e->stream));
-  HIP_TRY(hipMemcpyAsync(e->T.inv, &h32[2 * cap], 4 * cap * 4, hipMemcpyHostToDevice, e->stream));
+  HIP_TRY(hipMemcpyAsync(e->T.inv_cpu, &h32[2 * cap], 2 * cap * 4, hipMemcpyHostToDevice, e->stream));
+  HIP_TRY(hipMemcpyAsync(e->T.inv_mem, hd.data(), 2 * cap * 8, hipMemcpyHostToDevice, e->stream));
   HIP_TRY(hipStreamSynchronize(e->stream));
   e->static_dirty = false;
   return 0;
@@ -975,11 +1009,12 @@ RoundGeom geometry(const kg_engine* e) {
 }
 
 size_t resolve_lds_bytes(const RoundGeom& g) {
-  return ((size_t)g.B * kCandStride + (size_t)g.B * 8) * 8 + (size_t)g.bitmap_words * 4;
+  return ((size_t)g.B * kCandStride + (size_t)g.B * kPodWords) * 8 + (size_t)g.bitmap_words * 4;
 }
 
 dim3 eval_grid(const RoundGeom& g) {
-  return dim3((unsigned)((g.nt_local + kEvalWaves - 1) / kEvalWaves), (unsigned)((g.B + g.ppw - 1) / g.ppw));
+  // 1-D grid: tile groups × pod groups, swizzled over XCDs inside eval_round
+  return dim3((unsigned)(((g.nt_local + kEvalWaves - 1) / kEvalWaves) * ((g.B + g.ppw - 1) / g.ppw)));
 }
 
 int profile_bits(const EvalParams& P) {
@@ -1136,9 +1171,9 @@ int kg_engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank, int
   }
   if (hipGetDevice(&e->device) != hipSuccess) return bail(fail(KG_E_DEVICE, "no HIP device"));
   if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) return bail(fail(KG_E_DEVICE, "hipStreamCreate"));
-  if (int rc = e->cols64.ensure(12 * cap)) return bail(rc);
-  if (int rc = e->cols32.ensure(7 * cap)) return bail(rc);  // alloc_pods, num_pods, flags, inv[4] (f32)
-  if (hipMemset(e->cols64.p, 0, 12 * cap * 8) != hipSuccess || hipMemset(e->cols32.p, 0, 7 * cap * 4) != hipSuccess)
+  if (int rc = e->cols64.ensure(14 * cap)) return bail(rc);  // 12 int64 columns + inv_mem[2] (f64)
+  if (int rc = e->cols32.ensure(5 * cap)) return bail(rc);   // alloc_pods, num_pods, flags, inv_cpu[2] (f32)
+  if (hipMemset(e->cols64.p, 0, 14 * cap * 8) != hipSuccess || hipMemset(e->cols32.p, 0, 5 * cap * 4) != hipSuccess)
     return bail(fail(KG_E_DEVICE, "hipMemset"));
   int64_t* c64 = e->cols64.p;
   e->T.alloc_cpu = c64 + 0 * cap;
@@ -1156,7 +1191,8 @@ int kg_engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank, int
   e->T.alloc_pods = e->cols32.p + 0 * cap;
   e->T.num_pods = e->cols32.p + 1 * cap;
   e->T.flags = (uint32_t*)(e->cols32.p + 2 * cap);
-  e->T.inv = (float*)(e->cols32.p + 3 * cap);
+  e->T.inv_cpu = (float*)(e->cols32.p + 3 * cap);
+  e->T.inv_mem = (double*)(e->cols64.p + 12 * cap);
   e->T.cap = cap;
   if (int rc = e->cursor.ensure(4)) return bail(rc);
   if (hipMemset(e->cursor.p, 0, 4 * 8) != hipSuccess) return bail(fail(KG_E_DEVICE, "hipMemset"));
@@ -1189,7 +1225,7 @@ int kg_engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank, int
     e->P.inv_fit_ws[3] = wc + wm > 0 ? 1.0f / (wc + wm) : 0.0f;
   }
   {
-    const int lds = (int)(kMaxNodes / 8 + (size_t)kMaxB * (kCandStride + 8) * 8);
+    const int lds = (int)(kMaxNodes / 8 + (size_t)kMaxB * (kCandStride + kPodWords) * 8);
     hipError_t fe = hipSuccess;
 #define KG_ATTR(X) \
   fe = hipFuncSetAttribute((const void*)resolve_round<X>, hipFuncAttributeMaxDynamicSharedMemorySize, lds)
@@ -1398,9 +1434,9 @@ int kg_pods_evaluate(kg_engine* e, const kg_pod* pod, int32_t* out_reject, int64
   if (int rc = decode_pod(e, *pod, d)) return rc;
   const int64_t n = e->n_nodes;
   if (n == 0) return 0;
-  if (int rc = e->scratch64.ensure(2 * n + 8)) return rc;
+  if (int rc = e->scratch64.ensure(2 * n + kPodWords)) return rc;
   if (int rc = e->scratch32.ensure(n)) return rc;
-  DevPod* dp = reinterpret_cast<DevPod*>(e->scratch64.p + 2 * n);  // 64 B = the 8 spare int64s
+  DevPod* dp = reinterpret_cast<DevPod*>(e->scratch64.p + 2 * n);  // the kPodWords spare int64s
   HIP_TRY(hipMemcpyAsync(dp, &d, sizeof(d), hipMemcpyHostToDevice, e->stream));
   evaluate_pod<<<(unsigned)((n + 255) / 256), 256, 0, e->stream>>>(e->T, dp, n, e->P, e->scratch32.p, e->scratch64.p,
                                                                    e->scratch64.p + n);
@@ -1502,9 +1538,9 @@ int kg_bench_kernel(kg_engine* e, int which, int iters, double* avg_ms, double* 
   const double nb = (double)end;
   if (avg_ms) *avg_ms = total_ms / iters;
   if (algo_bytes) {
-    // eval: SURVEY §8(d) per-evaluation bytes (Fit 56 B + LoadAware 36 B = 92 B per node) × pods × nodes,
+    // eval: SURVEY §8(d) per-evaluation bytes (Fit 56 B + LoadAware 20 B = 76 B per node) × pods × nodes,
     //       + the candidate lists written;  merge: lists read + records written;  resolve: records + pods read.
-    if (which == 0) *algo_bytes = nb * (double)g.n_local * 92.0 + nb * g.nt_local * kR * 8.0 + nb * 64.0;
+    if (which == 0) *algo_bytes = nb * (double)g.n_local * kAlgoBytesPerNode + nb * g.nt_local * kR * 8.0 + nb * 64.0;
     else if (which == 1) *algo_bytes = nb * g.nt_local * kR * 8.0 + nb * kCandStride * 8.0;
     else *algo_bytes = nb * kCandStride * 8.0 + nb * 64.0;
   }
@@ -1552,6 +1588,23 @@ int kg_debug_least_requested(kg_engine* e, const int64_t* req, const int64_t* ca
   debug_least_requested<<<(unsigned)((n + 255) / 256), 256, 0, e->stream>>>(b.p, b.p + n, b.p + 2 * n, n);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpyAsync(out, b.p + 2 * n, n * 8, hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  b.release();
+  return 0;
+}
+
+int kg_debug_fast_lrs(kg_engine* e, const int64_t* req, const int64_t* cap, int64_t* out_cpu, int64_t* out_mem,
+                      int64_t n) {
+  if (!e || n < 0 || (n > 0 && (!req || !cap || !out_cpu || !out_mem))) return fail(KG_E_INVALID, "bad argument");
+  if (n == 0) return 0;
+  DevBuf<int64_t> b;
+  if (int rc = b.ensure(4 * n)) return rc;
+  HIP_TRY(hipMemcpyAsync(b.p, req, n * 8, hipMemcpyHostToDevice, e->stream));
+  HIP_TRY(hipMemcpyAsync(b.p + n, cap, n * 8, hipMemcpyHostToDevice, e->stream));
+  debug_fast_lrs<<<(unsigned)((n + 255) / 256), 256, 0, e->stream>>>(b.p, b.p + n, b.p + 2 * n, b.p + 3 * n, n);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(out_cpu, b.p + 2 * n, n * 8, hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipMemcpyAsync(out_mem, b.p + 3 * n, n * 8, hipMemcpyDeviceToHost, e->stream));
   HIP_TRY(hipStreamSynchronize(e->stream));
   b.release();
   return 0;

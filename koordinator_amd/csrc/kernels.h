@@ -44,6 +44,7 @@ constexpr uint32_t F_VALID = 1u << 0;
 constexpr uint32_t F_LA_SCORE = 1u << 1;      // NodeMetric present and not expired: LoadAware scores it
 constexpr uint32_t F_LA_PASS = 1u << 2;       // LoadAware Filter verdict for a non-prod pod
 constexpr uint32_t F_LA_PASS_PROD = 1u << 3;  // LoadAware Filter verdict for a prod pod
+constexpr uint32_t F_RARE = 1u << 4;          // EvalRow only: a score input lies outside eval_fast's exact domain
 
 // pod flags (device)
 constexpr uint32_t P_ZERO_REQ = 1u << 0;      // every request zero → fitsRequest skips resource checks
@@ -60,19 +61,23 @@ struct DevTable {
   int64_t *la_pused_cpu, *la_pused_mem;  // Σ EstimatePod(assigned prod pods)      (mutable)
   int32_t *alloc_pods, *num_pods;        // AllowedPodNumber, len(Pods)    (num_pods mutable)
   uint32_t *flags;
-  float *inv;                            // [4][cap]: 100/alloc_cpu, 100/alloc_mem, 100/la_alloc_cpu, 100/la_alloc_mem
-  int64_t cap;                           // column stride of `inv`
+  float *inv_cpu;                        // [2][cap]: 100/alloc_cpu, 100/la_alloc_cpu        (f32 estimates)
+  double *inv_mem;                       // [2][cap]: 100/alloc_mem, 100/la_alloc_mem        (f64 estimates)
+  int64_t cap;                           // column stride of the reciprocal columns
 };
 
 struct DevPod {
   int64_t req_cpu, req_mem;
   int64_t nz_cpu, nz_mem;
   int64_t est_cpu, est_mem;
+  double nz_mem_d, est_mem_d;  // the same quantities as f64 (exact below 2^53) for the memory score terms
+  int32_t nz_cpu32, est_cpu32; // min(·, 2^30) for the 32-bit cpu score terms
   uint32_t flags;
   uint32_t pad;
-  int64_t pad2;  // 64 B: 16-B aligned for LDS-DMA
+  int64_t pad2[2];  // 96 B: a 16-B multiple for LDS-DMA
 };
-static_assert(sizeof(DevPod) == 64, "DevPod layout");
+static_assert(sizeof(DevPod) == 96, "DevPod layout");
+constexpr int kPodWords = (int)(sizeof(DevPod) / 8);
 
 struct EvalParams {
   int64_t fit_w_cpu, fit_w_mem;
@@ -91,7 +96,8 @@ struct Row {
   int64_t la_alloc_cpu, la_alloc_mem, la_used_cpu, la_used_mem, la_pused_cpu, la_pused_mem;
   int32_t alloc_pods, num_pods;
   uint32_t flags;
-  float inv_cpu, inv_mem, la_inv_cpu, la_inv_mem;
+  float inv_cpu, la_inv_cpu;
+  double inv_mem, la_inv_mem;
 };
 
 __device__ __forceinline__ Row load_row(const DevTable& T, int64_t i) {
@@ -111,10 +117,10 @@ __device__ __forceinline__ Row load_row(const DevTable& T, int64_t i) {
   r.alloc_pods = T.alloc_pods[i];
   r.num_pods = T.num_pods[i];
   r.flags = T.flags[i];
-  r.inv_cpu = T.inv[i];
-  r.inv_mem = T.inv[T.cap + i];
-  r.la_inv_cpu = T.inv[2 * T.cap + i];
-  r.la_inv_mem = T.inv[3 * T.cap + i];
+  r.inv_cpu = T.inv_cpu[i];
+  r.la_inv_cpu = T.inv_cpu[T.cap + i];
+  r.inv_mem = T.inv_mem[i];
+  r.la_inv_mem = T.inv_mem[T.cap + i];
   return r;
 }
 
@@ -263,27 +269,55 @@ __device__ __forceinline__ uint64_t readlane_u64(uint64_t v, int lane) {
 // ---------------------------------------------------------------------------------------------------
 // Wide-pass evaluation on hoisted per-node terms (no division: capacities' reciprocals are static columns).
 // ---------------------------------------------------------------------------------------------------
+// Domain of eval_fast's exact arithmetic (outside it the row carries F_RARE and the exact path runs):
+//   cpu    : 0 < capacity < 2^24 millicores, -2^30 ≤ free ≤ capacity   → 32-bit terms, 24-bit multiplies
+//   memory : 0 < capacity < 2^45 bytes,     -2^52 < free ≤ capacity   → f64 terms, every product < 2^53
+constexpr int64_t kCpuCapMax = 1ll << 24, kCpuFreeMin = -(1ll << 30);
+constexpr int64_t kMemCapMax = 1ll << 45, kMemFreeMin = -(1ll << 52);
+constexpr int64_t kPodCpu32Max = 1ll << 30;
+
 struct EvalRow {
-  int64_t free_cpu, free_mem;          // Allocatable - Requested                 (fitsRequest)
-  int64_t alloc_cpu, alloc_mem;        // LeastAllocated capacity
-  int64_t fnz_cpu, fnz_mem;            // Allocatable - NonZeroRequested
-  int64_t la_alloc_cpu, la_alloc_mem;  // EstimateNode
-  int64_t la_free_cpu, la_free_mem;    // la_alloc - la_used      (non-prod view)
-  int64_t la_pfree_cpu, la_pfree_mem;  // la_alloc - la_pused     (prod view)
-  float inv_cpu, inv_mem, la_inv_cpu, la_inv_mem;  // 100 / capacity
+  int64_t free_cpu, free_mem;                                     // Allocatable - Requested (fitsRequest)
+  int64_t alloc_cpu, fnz_cpu, la_alloc_cpu, la_free_cpu, la_pfree_cpu;  // cpu terms (low dword on the fast path)
+  double alloc_mem, fnz_mem, la_alloc_mem, la_free_mem, la_pfree_mem;   // memory terms, exact integers in f64
+  double inv_mem, la_inv_mem;                                     // 100 / capacity (f64 estimate)
+  float inv_cpu, la_inv_cpu;                                      // 100 / capacity (f32 estimate)
   float inv_fit_ws;                    // 1 / Σ fit weights of resources with non-zero allocatable
   int32_t fit_ws;
   int32_t pods_left;                   // AllowedPodNumber - len(Pods) - 1  (fits iff ≥ 0)
   int32_t alloc_pods;
-  uint32_t flags;
+  uint32_t flags;                      // node flags | F_RARE
   uint32_t pad;
 };
-static_assert(sizeof(EvalRow) == 136, "EvalRow layout");
-constexpr int kEvalRowWords = 17;  // 136 B in uint64 words
+static_assert(sizeof(EvalRow) == 144, "EvalRow layout");
+constexpr int kEvalRowWords = 18;  // 144 B in uint64 words
 
 __device__ __forceinline__ float i64_to_f32(int64_t x) {  // x ≥ 0; ~1 ulp, enough for a ±1 quotient estimate
   const uint64_t u = (uint64_t)x;
   return fmaf((float)(uint32_t)(u >> 32), 4294967296.0f, (float)(uint32_t)u);
+}
+
+__device__ __forceinline__ bool cpu_dom(int64_t cap, int64_t fr) {
+  return cap > 0 && cap < kCpuCapMax && fr >= kCpuFreeMin && fr <= cap;
+}
+__device__ __forceinline__ bool mem_dom(int64_t cap, int64_t fr) {
+  return cap > 0 && cap < kMemCapMax && fr > kMemFreeMin && fr <= cap;
+}
+
+// F_RARE for the free terms the profile scores (a pure function of the row; recomputed after each assume).
+__device__ __forceinline__ uint32_t rare_bit(const EvalRow& e, const EvalParams& P) {
+  bool ok = true;
+  if (P.fit_score) {
+    if (P.fit_w_cpu) ok &= cpu_dom(e.alloc_cpu, e.fnz_cpu);
+    if (P.fit_w_mem) ok &= mem_dom((int64_t)e.alloc_mem, (int64_t)e.fnz_mem);
+  }
+  if (P.la_score && (e.flags & F_LA_SCORE)) {
+    if (P.la_w_cpu) ok &= cpu_dom(e.la_alloc_cpu, e.la_free_cpu) & cpu_dom(e.la_alloc_cpu, e.la_pfree_cpu);
+    if (P.la_w_mem)
+      ok &= mem_dom((int64_t)e.la_alloc_mem, (int64_t)e.la_free_mem) &
+            mem_dom((int64_t)e.la_alloc_mem, (int64_t)e.la_pfree_mem);
+  }
+  return ok ? 0u : F_RARE;
 }
 
 __device__ __forceinline__ EvalRow make_eval_row(const Row& r, const EvalParams& P) {
@@ -291,19 +325,19 @@ __device__ __forceinline__ EvalRow make_eval_row(const Row& r, const EvalParams&
   e.free_cpu = r.alloc_cpu - r.req_cpu;
   e.free_mem = r.alloc_mem - r.req_mem;
   e.alloc_cpu = r.alloc_cpu;
-  e.alloc_mem = r.alloc_mem;
   e.fnz_cpu = r.alloc_cpu - r.nz_cpu;
-  e.fnz_mem = r.alloc_mem - r.nz_mem;
   e.la_alloc_cpu = r.la_alloc_cpu;
-  e.la_alloc_mem = r.la_alloc_mem;
   e.la_free_cpu = r.la_alloc_cpu - r.la_used_cpu;
-  e.la_free_mem = r.la_alloc_mem - r.la_used_mem;
   e.la_pfree_cpu = r.la_alloc_cpu - r.la_pused_cpu;
-  e.la_pfree_mem = r.la_alloc_mem - r.la_pused_mem;
-  e.inv_cpu = r.inv_cpu;
+  e.alloc_mem = (double)r.alloc_mem;
+  e.fnz_mem = (double)(r.alloc_mem - r.nz_mem);
+  e.la_alloc_mem = (double)r.la_alloc_mem;
+  e.la_free_mem = (double)(r.la_alloc_mem - r.la_used_mem);
+  e.la_pfree_mem = (double)(r.la_alloc_mem - r.la_pused_mem);
   e.inv_mem = r.inv_mem;
-  e.la_inv_cpu = r.la_inv_cpu;
   e.la_inv_mem = r.la_inv_mem;
+  e.inv_cpu = r.inv_cpu;
+  e.la_inv_cpu = r.la_inv_cpu;
   const bool hc = P.fit_w_cpu && r.alloc_cpu != 0, hm = P.fit_w_mem && r.alloc_mem != 0;
   e.fit_ws = (hc ? (int32_t)P.fit_w_cpu : 0) + (hm ? (int32_t)P.fit_w_mem : 0);
   e.inv_fit_ws = hc ? (hm ? P.inv_fit_ws[3] : P.inv_fit_ws[1]) : (hm ? P.inv_fit_ws[2] : 0.0f);
@@ -311,54 +345,59 @@ __device__ __forceinline__ EvalRow make_eval_row(const Row& r, const EvalParams&
   e.alloc_pods = r.alloc_pods;
   e.flags = r.flags;
   e.pad = 0;
+  // the f64 memory terms are exact only inside the domain; outside it the exact path re-reads the table
+  e.flags |= rare_bit(e, P);
   return e;
 }
 
 // assume(pod) on a hoisted row: upstream NodeInfo.AddPod + LoadAware Reserve → podAssignCache.assign
 // (load_aware.go:260-263).  Capacities and reciprocals are unchanged; only the free terms move.
-__device__ __forceinline__ void assume_on(EvalRow& e, const DevPod& p) {
-  const int64_t prod = (p.flags & P_PROD) ? 1 : 0;
+__device__ __forceinline__ void assume_on(EvalRow& e, const DevPod& p, const EvalParams& P) {
+  const bool prod = (p.flags & P_PROD) != 0;
   e.free_cpu -= p.req_cpu;
   e.free_mem -= p.req_mem;
   e.fnz_cpu -= p.nz_cpu;
-  e.fnz_mem -= p.nz_mem;
+  e.fnz_mem -= p.nz_mem_d;
   e.la_free_cpu -= p.est_cpu;
-  e.la_free_mem -= p.est_mem;
-  e.la_pfree_cpu -= prod * p.est_cpu;
-  e.la_pfree_mem -= prod * p.est_mem;
+  e.la_free_mem -= p.est_mem_d;
+  e.la_pfree_cpu -= prod ? p.est_cpu : 0;
+  e.la_pfree_mem -= prod ? p.est_mem_d : 0.0;
   e.pods_left -= 1;
+  e.flags = (e.flags & ~F_RARE) | rare_bit(e, P);
 }
 
-// Mutable columns recovered from a hoisted row (inverse of make_eval_row).
+// Mutable columns recovered from a hoisted row (inverse of make_eval_row; exact inside the domain).
 __device__ __forceinline__ void store_eval_row(const DevTable& T, int64_t i, const EvalRow& e) {
+  const int64_t am = (int64_t)e.alloc_mem, lam = (int64_t)e.la_alloc_mem;
   T.req_cpu[i] = e.alloc_cpu - e.free_cpu;
-  T.req_mem[i] = e.alloc_mem - e.free_mem;
+  T.req_mem[i] = am - e.free_mem;
   T.nz_cpu[i] = e.alloc_cpu - e.fnz_cpu;
-  T.nz_mem[i] = e.alloc_mem - e.fnz_mem;
+  T.nz_mem[i] = am - (int64_t)e.fnz_mem;
   T.la_used_cpu[i] = e.la_alloc_cpu - e.la_free_cpu;
-  T.la_used_mem[i] = e.la_alloc_mem - e.la_free_mem;
+  T.la_used_mem[i] = lam - (int64_t)e.la_free_mem;
   T.la_pused_cpu[i] = e.la_alloc_cpu - e.la_pfree_cpu;
-  T.la_pused_mem[i] = e.la_alloc_mem - e.la_pfree_mem;
+  T.la_pused_mem[i] = lam - (int64_t)e.la_pfree_mem;
   T.num_pods[i] = e.alloc_pods - e.pods_left - 1;
 }
 
 __device__ __forceinline__ Row row_of(const EvalRow& e) {  // the reference-shaped row behind a hoisted one
   Row r;
+  const int64_t am = (int64_t)e.alloc_mem, lam = (int64_t)e.la_alloc_mem;
   r.alloc_cpu = e.alloc_cpu;
-  r.alloc_mem = e.alloc_mem;
+  r.alloc_mem = am;
   r.req_cpu = e.alloc_cpu - e.free_cpu;
-  r.req_mem = e.alloc_mem - e.free_mem;
+  r.req_mem = am - e.free_mem;
   r.nz_cpu = e.alloc_cpu - e.fnz_cpu;
-  r.nz_mem = e.alloc_mem - e.fnz_mem;
+  r.nz_mem = am - (int64_t)e.fnz_mem;
   r.la_alloc_cpu = e.la_alloc_cpu;
-  r.la_alloc_mem = e.la_alloc_mem;
+  r.la_alloc_mem = lam;
   r.la_used_cpu = e.la_alloc_cpu - e.la_free_cpu;
-  r.la_used_mem = e.la_alloc_mem - e.la_free_mem;
+  r.la_used_mem = lam - (int64_t)e.la_free_mem;
   r.la_pused_cpu = e.la_alloc_cpu - e.la_pfree_cpu;
-  r.la_pused_mem = e.la_alloc_mem - e.la_pfree_mem;
+  r.la_pused_mem = lam - (int64_t)e.la_pfree_mem;
   r.alloc_pods = e.alloc_pods;
   r.num_pods = e.alloc_pods - e.pods_left - 1;
-  r.flags = e.flags;
+  r.flags = e.flags & ~F_RARE;
   r.inv_cpu = e.inv_cpu;
   r.inv_mem = e.inv_mem;
   r.la_inv_cpu = e.la_inv_cpu;
@@ -366,32 +405,52 @@ __device__ __forceinline__ Row row_of(const EvalRow& e) {  // the reference-shap
   return r;
 }
 
-// leastRequestedScore with x = capacity - requested precomputed: ((x * 100) / capacity), 0 when x < 0 or
-// capacity == 0.  Branch-free; exact for 0 ≤ x ≤ capacity (the estimate is within ±1 and one int64
-// multiply-compare corrects it).  x > capacity (a negative Requested) is flagged `rare` for the exact path.
-__device__ __forceinline__ int32_t lrs_x(int64_t x, int64_t cap, float inv, bool& rare) {
-  const int64_t num = x * 100;
-  int q = (int)(i64_to_f32(x > 0 ? x : 0) * inv);
-  q = q < 0 ? 0 : (q > 100 ? 100 : q);
-  const int64_t t = (int64_t)q * cap;
+// leastRequestedScore ((x · 100) / capacity, x = capacity - requested; 0 when x < 0) on the fast path.
+// cpu (32-bit): the f32 quotient is within ±1 (relative error ≤ 3·2^-24 on a value ≤ 100); one 24-bit
+// multiply-compare each way corrects it — q·cap and 100·x stay below 2^31 inside the domain.
+__device__ __forceinline__ int32_t lrs_cpu(int32_t x, int32_t cap, float inv) {
+  const int32_t xc = x < 0 ? 0 : x;  // x < 0 scores 0, and so does xc = 0 (cap > 0 in the domain)
+  int q = (int)((float)xc * inv);
+  const int32_t t = (int32_t)__umul24((uint32_t)q, (uint32_t)cap);
+  const int32_t num = (int32_t)__umul24((uint32_t)xc, 100u);
   q -= (int)(t > num);
   q += (int)(t + cap <= num);
-  rare |= x > cap;
-  return (cap == 0 || x < 0) ? 0 : q;
+  return q;
+}
+// memory (f64): x·inv has absolute error ≤ 100·2^-52 < 1/cap (cap < 2^45), so trunc() is exact unless the
+// quotient is an integer k and the estimate lands just below it: one exact f64 compare (q+1)·cap ≤ 100·x
+// (every value < 2^52) lifts it.
+__device__ __forceinline__ int32_t lrs_mem(double x, double cap, double inv) {
+  const double xc = __builtin_fmax(x, 0.0);  // as lrs_cpu: x < 0 → 0
+  int q = (int)(xc * inv);
+  const double t = __builtin_fma((double)q, cap, cap);
+  q += (int)(t <= xc * 100.0);
+  return q;
 }
 
-// s / w for 0 ≤ s ≤ 100·w (w ≤ 2·10⁶, so s < 2^28 is exact in f32's integer range + one correction step)
+// s / w for 0 ≤ s ≤ 100·w, w ≤ 2·10⁶ (validate_config): f32 estimate + one correction step, 24-bit multiplies.
 __device__ __forceinline__ int32_t div_est(int32_t s, int32_t w, float inv_w) {
   int q = (int)((float)s * inv_w);
-  const int32_t t = q * w;
+  const int32_t t = (int32_t)__umul24((uint32_t)q, (uint32_t)w);
   q -= (int)(t > s);
   q += (int)(t + w <= s);
   return q;
 }
 
+// Value selects the optimiser cannot turn into a select of field ADDRESSES: that rewrite (select of two loads
+// → load of a selected address) would keep a whole EvalRow array in scratch memory instead of registers.
+__device__ __forceinline__ int64_t pick(bool c, int64_t a, int64_t b) {
+  asm("" : "+v"(a), "+v"(b));
+  return c ? b : a;
+}
+__device__ __forceinline__ double pick(bool c, double a, double b) {
+  asm("" : "+v"(a), "+v"(b));
+  return c ? b : a;
+}
+
 // Branch-free fused Filter + Score on hoisted terms, specialised on the profile PF.  Returns feasibility;
-// sets `rare` when an input lies outside the fast path's domain (a negative Requested) — the caller then
-// re-evaluates with eval_node.
+// sets `rare` when the row lies outside the fast path's exact domain (F_RARE) — the caller then re-evaluates
+// with eval_node.
 template <int PF>
 __device__ __forceinline__ bool eval_fast(const EvalRow& n, const DevPod& p, const EvalParams& P, uint32_t& total,
                                           bool& rare) {
@@ -405,25 +464,28 @@ __device__ __forceinline__ bool eval_fast(const EvalRow& n, const DevPod& p, con
     const uint32_t passbit = (pf & P_PROD) ? F_LA_PASS_PROD : F_LA_PASS;
     ok = ok & (((pf & P_DAEMONSET) != 0) | ((n.flags & passbit) != 0));
   }
-  int32_t t = 0;
+  uint32_t t = 0;
+  if constexpr ((PF & (PF_FIT_SCORE | PF_LA_SCORE)) != 0) rare |= (n.flags & F_RARE) != 0;
   if constexpr ((PF & PF_FIT_SCORE) != 0) {
-    const int32_t qc = lrs_x(n.fnz_cpu - p.nz_cpu, n.alloc_cpu, n.inv_cpu, rare);
-    const int32_t qm = lrs_x(n.fnz_mem - p.nz_mem, n.alloc_mem, n.inv_mem, rare);
-    const int32_t s = qc * (int32_t)P.fit_w_cpu + qm * (int32_t)P.fit_w_mem;
+    const int32_t qc = lrs_cpu((int32_t)n.fnz_cpu - p.nz_cpu32, (int32_t)n.alloc_cpu, n.inv_cpu);
+    const int32_t qm = lrs_mem(n.fnz_mem - p.nz_mem_d, n.alloc_mem, n.inv_mem);
+    const int32_t s = (int32_t)(__umul24((uint32_t)qc, (uint32_t)P.fit_w_cpu) +
+                                __umul24((uint32_t)qm, (uint32_t)P.fit_w_mem));
     const int32_t f = div_est(s, n.fit_ws, n.inv_fit_ws);
-    t += (n.fit_ws ? f : 0) * (int32_t)P.weight_fit;
+    t += __umul24((uint32_t)(n.fit_ws ? f : 0), (uint32_t)P.weight_fit);
   }
   if constexpr ((PF & PF_LA_SCORE) != 0) {
     const bool prodv = (pf & P_LA_PROD_SCORE) != 0;
-    const int64_t fc = prodv ? n.la_pfree_cpu : n.la_free_cpu;
-    const int64_t fm = prodv ? n.la_pfree_mem : n.la_free_mem;
-    const int32_t qc = lrs_x(fc - p.est_cpu, n.la_alloc_cpu, n.la_inv_cpu, rare);
-    const int32_t qm = lrs_x(fm - p.est_mem, n.la_alloc_mem, n.la_inv_mem, rare);
-    const int32_t s = qc * (int32_t)P.la_w_cpu + qm * (int32_t)P.la_w_mem;
+    const int32_t fc = (int32_t)pick(prodv, n.la_free_cpu, n.la_pfree_cpu);
+    const double fm = pick(prodv, n.la_free_mem, n.la_pfree_mem);
+    const int32_t qc = lrs_cpu(fc - p.est_cpu32, (int32_t)n.la_alloc_cpu, n.la_inv_cpu);
+    const int32_t qm = lrs_mem(fm - p.est_mem_d, n.la_alloc_mem, n.la_inv_mem);
+    const int32_t s = (int32_t)(__umul24((uint32_t)qc, (uint32_t)P.la_w_cpu) +
+                                __umul24((uint32_t)qm, (uint32_t)P.la_w_mem));
     const int32_t l = div_est(s, (int32_t)P.la_wsum, P.inv_la_wsum);
-    t += ((n.flags & F_LA_SCORE) ? l : 0) * (int32_t)P.weight_la;
+    t += __umul24((uint32_t)((n.flags & F_LA_SCORE) ? l : 0), (uint32_t)P.weight_la);
   }
-  total = (uint32_t)t;
+  total = t;
   return ok;
 }
 

@@ -158,3 +158,13 @@ class Engine:
         check(self.lib, self.lib.kg_debug_least_requested(self.h, ptr(requested), ptr(capacity), ptr(out),
                                                           len(requested)))
         return out
+
+    def debug_fast_lrs(self, requested, capacity):
+        """(cpu-routine, memory-routine) leastRequestedScore of the wide pass; -1 outside a routine's domain."""
+        requested = np.ascontiguousarray(requested, dtype=np.int64)
+        capacity = np.ascontiguousarray(capacity, dtype=np.int64)
+        oc = np.zeros(len(requested), dtype=np.int64)
+        om = np.zeros(len(requested), dtype=np.int64)
+        check(self.lib, self.lib.kg_debug_fast_lrs(self.h, ptr(requested), ptr(capacity), ptr(oc), ptr(om),
+                                                   len(requested)))
+        return oc, om

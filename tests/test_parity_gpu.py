@@ -101,6 +101,35 @@ def test_least_requested_exact():
     np.testing.assert_array_equal(got, want)
 
 
+def _lrs_exact(req, cap):
+    # leastRequestedScore (load_aware.go:388-397) in exact integer arithmetic (Python ints)
+    return np.array([0 if (c == 0 or r > c) else ((c - r) * 100) // c for r, c in zip(req.tolist(), cap.tolist())])
+
+
+@pytest.mark.parametrize("cap_hi,name", [(1 << 24, "cpu"), (1 << 45, "mem")])
+def test_fast_lrs_exact(cap_hi, name):
+    """The wide pass's division-free quotient routines equal the exact quotient on their whole domain: random
+    pairs, every exact-integer quotient boundary ±1, the capacity edge, and small capacities."""
+    rng = np.random.default_rng(11 if name == "cpu" else 12)
+    caps = np.concatenate([rng.integers(1, cap_hi, 30000), rng.integers(1, 4096, 5000),
+                           np.array([1, 2, 3, 7, 100, 1000, 96000, cap_hi - 1, cap_hi - 2, (cap_hi - 1) // 3])])
+    caps = caps[caps < cap_hi]
+    k = rng.integers(0, 101, len(caps))
+    edge = caps - (caps * k + 99) // 100          # smallest requested with quotient ≥ 100 - k … boundaries
+    reqs = np.concatenate([np.floor(caps * rng.random(len(caps))).astype(np.int64), edge, edge + 1, edge - 1,
+                           caps, caps - 1, np.zeros_like(caps), caps + 5, caps * 2])
+    capv = np.tile(caps, 9)
+    with Engine(framework.build_config(), 1) as e:
+        oc, om = e.debug_fast_lrs(reqs, capv)
+    got = oc if name == "cpu" else om
+    free = capv - reqs
+    lo = -(1 << 30) if name == "cpu" else -(1 << 52) + 1
+    dom = (capv > 0) & (capv < cap_hi) & (free >= lo) & (free <= capv)
+    assert dom.sum() > 0.8 * len(dom)
+    assert np.all(got[~dom] == -1)
+    np.testing.assert_array_equal(got[dom], _lrs_exact(reqs[dom], capv[dom]))
+
+
 # ---------------------------------------------------------------------------------------------------
 # synthetic clusters: placements + final state vs oracle
 # ---------------------------------------------------------------------------------------------------
