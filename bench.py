@@ -43,6 +43,8 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel-iters", type=int, default=50)
+    ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "r01", "traffic_c3.json"),
+                    help="PMC summary (scripts/pmc_summary.py) of the same workload: per-launch HBM bytes")
     ap.add_argument("--check", type=int, default=0, help="verify the first N placements against the oracle")
     return ap.parse_args()
 
@@ -103,6 +105,20 @@ def cpu_baseline(cfg, cluster, pods, budget_s, threads):
     oracle.schedule(cfg, cluster.nodes, cluster.metrics, st, pods[probe:probe + m], cluster.now_ns, threads)
     dt = time.perf_counter() - t0
     return m, dt
+
+
+def pmc_traffic(path, kernel, nodes, batch, ppw):
+    """Per-launch HBM bytes of `kernel` (FETCH_SIZE x2 + WRITE_SIZE, gfx950-corrected by scripts/pmc_summary.py)
+    from a committed rocprofv3 --pmc summary, if it was collected on this exact workload geometry."""
+    try:
+        with open(path) as fh:
+            d = json.load(fh)
+    except (OSError, ValueError):
+        return None, None
+    m = d.get("_meta", {})
+    if (m.get("nodes"), m.get("batch_pods"), m.get("pods_per_wave")) != (nodes, batch, ppw) or kernel not in d:
+        return None, None
+    return d[kernel]["traffic_bytes"], os.path.relpath(path, ROOT)
 
 
 def main():
@@ -179,6 +195,8 @@ def main():
                          f"host nproc={os.cpu_count()}",
                "node_evals_per_sec": m * cluster.n / dt}
 
+    traffic, traffic_src = (pmc_traffic(args.traffic_file, dom, cluster.n, args.batch, args.pods_per_wave)
+                            if d.world == 1 else (None, None))
     if d.rank == 0:
         pods_s = total / elapsed
         out = {
@@ -202,7 +220,8 @@ def main():
             "placed": placed,
             "device_rounds": rounds,
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "traffic_source": traffic_src,
                          "kernels_ms": {k: v[0] for k, v in kernels.items()},
                          "algo_bytes": {k: v[1] for k, v in kernels.items()}},
             "cpu_baseline": cpu,

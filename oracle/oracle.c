@@ -384,3 +384,26 @@ int or_schedule(const kg_config* cfg, int64_t n_nodes, const kg_node* nodes, con
   free(c.total);
   return rc;
 }
+
+int or_node_keys(const kg_config* cfg, const kg_node* nodes, const kg_node_metric* metrics,
+                 const or_node_state* st, const kg_pod* pod, int64_t now, int64_t lo, int64_t hi,
+                 uint64_t* out_keys) {
+  sched_ctx c;
+  memset(&c, 0, sizeof(c));
+  c.cfg = cfg; c.nodes = nodes; c.metrics = metrics; c.st = (or_node_state*)st; c.now = now; c.pod = pod;
+  c.feasible = (int32_t*)calloc((size_t)(hi > 0 ? hi : 1), sizeof(int32_t)); /* indexed by node, like or_schedule */
+  c.total = (int64_t*)calloc((size_t)(hi > 0 ? hi : 1), sizeof(int64_t));
+  if (!c.feasible || !c.total) { free(c.feasible); free(c.total); return KG_E_NOMEM; }
+  int rc = 0;
+  for (int64_t i = lo; i < hi && rc == 0; i++) {
+    eval_filter(&c, i);
+    if (c.feasible[i] == 1) eval_score(&c, i);
+    if (c.feasible[i] < 0) { rc = KG_E_UNSUPPORTED; break; }
+    out_keys[i - lo] = c.feasible[i] == 1
+                           ? (((uint64_t)(uint32_t)c.total[i] << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)i))
+                           : 0;
+  }
+  free(c.feasible);
+  free(c.total);
+  return rc;
+}

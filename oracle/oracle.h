@@ -62,6 +62,13 @@ int or_schedule(const kg_config* cfg, int64_t n_nodes, const kg_node* nodes, con
                 or_node_state* st, int64_t n_pods, const kg_pod* pods, int64_t now_unix_nano, int n_threads,
                 int32_t* out_node, int64_t* out_score);
 
+/* Packed selection keys of one pod on nodes [lo, hi): (total << 32) | (0xFFFFFFFF - idx), 0 = filtered out —
+ * the same Filter + Score + weighted sum as or_schedule, single-threaded, no assume.  Used by the
+ * round-protocol model (tests/round_model.py).  Returns <0 if an input is outside the restated profile. */
+int or_node_keys(const kg_config* cfg, const kg_node* nodes, const kg_node_metric* metrics,
+                 const or_node_state* st, const kg_pod* pod, int64_t now_unix_nano, int64_t lo, int64_t hi,
+                 uint64_t* out_keys);
+
 /* Builds node states from pre-existing assigned pods (informer adds). */
 void or_states_init(int64_t n_nodes, or_node_state* st);
 int or_states_add_pods(const kg_config* cfg, int64_t n_nodes, or_node_state* st, int64_t n, const kg_pod* pods,

@@ -57,6 +57,8 @@ def lib():
         L.or_states_add_pods.restype = i
         L.or_schedule.argtypes = [vp, i64, vp, vp, vp, i64, vp, i64, i, vp, vp]
         L.or_schedule.restype = i
+        L.or_node_keys.argtypes = [vp, vp, vp, vp, vp, i64, i64, i64, vp]
+        L.or_node_keys.restype = i
         _lib = L
     return _lib
 
@@ -117,6 +119,22 @@ def schedule(cfg, nodes, metrics, st, pods, now_ns: int, n_threads: int = 1):
     if rc != 0:
         raise RuntimeError(f"oracle or_schedule failed: {rc}")
     return out_node, out_score
+
+
+def node_keys(cfg, nodes, metrics, st, pod, now_ns: int, lo: int, hi: int) -> np.ndarray:
+    """Packed keys (total << 32 | ~idx, 0 = filtered out) of one pod on nodes [lo, hi), current `st`."""
+    out = np.zeros(max(hi - lo, 0), dtype=np.uint64)
+    pod = np.ascontiguousarray(np.asarray(pod, dtype=abi.POD_DTYPE).reshape(1))
+    rc = lib().or_node_keys(p(cfg), p(nodes), p(metrics), p(st), p(pod), now_ns, lo, hi, p(out))
+    if rc != 0:
+        raise RuntimeError(f"oracle or_node_keys failed: {rc}")
+    return out
+
+
+def apply_pod(cfg, st, pod, node: int, sign: int = 1):
+    """assume (+1) / forget (-1) of one pod on node `node` of `st` (or_apply_pod)."""
+    pod = np.ascontiguousarray(np.asarray(pod, dtype=abi.POD_DTYPE).reshape(1))
+    lib().or_apply_pod(p(cfg), p(st[node:node + 1]), p(pod), sign)
 
 
 def schedule_cluster(cfg, cluster, pods, n_threads: int = 1):
