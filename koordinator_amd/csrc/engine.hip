@@ -43,6 +43,7 @@ constexpr int kCandStride = 128;      // per-pod record: 1 KiB (a 16-B multiple,
 constexpr int kMergeThreads = 256;
 constexpr int kMergeChunks = 4;       // chunks of 8 keys per merge thread: ≤ 1024 tile lists = 262144 nodes per rank
 constexpr double kAlgoBytesPerNode = 76.0;  // SURVEY §8(d) b_node for C1-C3: Fit 56 B + LoadAware 20 B
+constexpr int64_t kMaxBatchRounds = 256;  // rounds launched between two host synchronisations
 constexpr int64_t kMaxNodes = 1 << 19;  // resolver LDS: N/8-byte bitmap (≤ 64 KiB) + the round's records (≤ 64 KiB)
 static_assert(kRecRows + kStaged * kEvalRowWords <= kCandStride, "record layout");
 
@@ -78,72 +79,67 @@ typedef const __attribute__((address_space(1))) void* global_cvoid_ptr;
 // ------------------------------------------------------------------------------------------------
 
 // ---- round kernel 1: wide evaluation -------------------------------------------------------------
-// One wave = one tile of kTile nodes (lane l holds nodes tile*kTile + j*64 + l, j < kNPT) × pods_per_wave pods
-// of the round.  Writes lists[(pod, tile)][kR] = the tile's top-kR packed keys (unordered, zero-padded).
+// One wave = one tile of kTile nodes (lane l holds nodes tile*kTile + j*64 + l, j < kNPT, as HotRows in
+// registers) × pods_per_wave pods of the round [first, first + nb).  Writes lists[(pod, tile)][kR] = the
+// tile's top-kR packed keys (ascending node order, zero-padded).  The table may be mid-update by the previous
+// round's resolver (pipelining): every column load is a single aligned 8-/4-byte load, so a
+// row reads as a mix of pre- and post-assume columns, whose key is ≥ the row's current key (monotone profile);
+// the resolver re-scores those rows exactly.  `poison` ≠ 0: an earlier round of this batch stopped early, so
+// this round's pods are not the next ones — nothing to do.
 template <int PF>
 __global__ __launch_bounds__(kWave* kEvalWaves) void eval_round(DevTable T, const DevPod* __restrict__ pods,
-                                                                  const int64_t* __restrict__ cursor_p,
-                                                                  int64_t end, int B, int pods_per_wave,
+                                                                  int64_t first, int nb, int pods_per_wave,
                                                                   int64_t node_base, int64_t n_local, int nt_local,
-                                                                  EvalParams P, uint64_t* __restrict__ lists) {
+                                                                  EvalParams P, uint64_t* __restrict__ lists,
+                                                                  const int32_t* __restrict__ poison) {
   KG_STAMP(0, 0);
-  const int64_t cursor = *cursor_p;
-  if (cursor >= end) return;
-  const int nb = (end - cursor) < (int64_t)B ? (int)(end - cursor) : B;
+  if (*poison) return;
   const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
   // XCD-aware swizzle (bijective for any grid size): the blocks of one tile group — one per pod group — get
   // consecutive ids on the same XCD label, so the group's node rows come from HBM once and from that XCD's
   // L2 for the other pod groups (the straight grid spread them over all 8 L2s: ~12x the table per launch).
-  const int n_pg = (B + pods_per_wave - 1) / pods_per_wave;
+  const int n_pg = (nb + pods_per_wave - 1) / pods_per_wave;
   const uint32_t nwg = gridDim.x, bid = blockIdx.x, xcd = bid % 8u, q = nwg / 8u, r = nwg % 8u;
   const uint32_t wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8u;
   const int tile = (int)(wgid / (uint32_t)n_pg) * kEvalWaves + wave;
-  KG_STAMP(0, 1);
   const int p0 = (int)(wgid % (uint32_t)n_pg) * pods_per_wave;
   if (tile >= nt_local || p0 >= nb) return;
   const int p1 = (p0 + pods_per_wave) < nb ? (p0 + pods_per_wave) : nb;
 
-  EvalRow rows[kNPT];
+  HotRow rows[kNPT];
   uint32_t gidx[kNPT];
+  bool rare = false;
 #pragma unroll
   for (int j = 0; j < kNPT; ++j) {
     const int64_t local = (int64_t)tile * kTile + j * kWave + lane;
     gidx[j] = (uint32_t)(node_base + local);
     if (local < n_local) {
-      rows[j] = make_eval_row(load_row(T, node_base + local), P);
+      rows[j] = load_hot<PF>(T, node_base + local, P);
+      rare |= (rows[j].flags & F_RARE) != 0;
     } else {
-      rows[j] = EvalRow{};
+      rows[j] = HotRow{};
       rows[j].flags = 0;  // not F_VALID → never feasible
     }
   }
+  KG_STAMP(0, 1);
+  // a row outside eval_hot's exact domain anywhere in the tile: the whole tile takes the exact path
+  const bool exact_tile = __ballot(rare) != 0;
   const uint64_t lane_lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
 
   for (int pi = p0; pi < p1; ++pi) {
-    const DevPod p = pods[cursor + pi];
-    KG_STAMP(0, 2 + 4 * (pi - p0));
+    const DevPod p = pods[first + pi];
     uint32_t tot[kNPT];
     bool okv[kNPT];
-    bool rare = false;
+    if (!exact_tile) {
 #pragma unroll
-    for (int j = 0; j < kNPT; ++j) {
-      tot[j] = 0;
-      okv[j] = eval_fast<PF>(rows[j], p, P, tot[j], rare);
-    }
-#ifdef KG_STAMPS
-    if (lane == 0) {
-      atomicAdd(&g_stamps[3][0][0], 1ull);
-      if (__ballot(rare)) atomicAdd(&g_stamps[3][0][1], 1ull);
-    }
-#endif
-    if (__ballot(rare)) {  // a row outside eval_fast's exact domain in the tile: exact reference-shaped path
+      for (int j = 0; j < kNPT; ++j) okv[j] = eval_hot<PF>(rows[j], p, P, tot[j]);
+    } else {
 #pragma unroll
       for (int j = 0; j < kNPT; ++j) {
         const int64_t local = (int64_t)tile * kTile + j * kWave + lane;
-        if (local < n_local) {
-          int64_t t = 0;
-          okv[j] = eval_node(load_row(T, node_base + local), p, P, t);
-          tot[j] = (uint32_t)t;
-        }
+        int64_t t = 0;
+        okv[j] = local < n_local && eval_node(load_row(T, node_base + local), p, P, t);
+        tot[j] = (uint32_t)t;
       }
     }
     uint64_t fm[kNPT];
@@ -153,7 +149,6 @@ __global__ __launch_bounds__(kWave* kEvalWaves) void eval_round(DevTable T, cons
       fm[j] = __ballot(okv[j]);
       nfeas += __popcll(fm[j]);
     }
-    KG_STAMP(0, 3 + 4 * (pi - p0));
     uint64_t sel[kNPT];
     if (nfeas <= kR) {
 #pragma unroll
@@ -188,7 +183,6 @@ __global__ __launch_bounds__(kWave* kEvalWaves) void eval_round(DevTable T, cons
         }
       }
     }
-    KG_STAMP(0, 4 + 4 * (pi - p0));
     uint64_t* out = lists + ((size_t)pi * nt_local + tile) * kR;
     int base = 0;
 #pragma unroll
@@ -204,34 +198,53 @@ __global__ __launch_bounds__(kWave* kEvalWaves) void eval_round(DevTable T, cons
 // ---- round kernel 2: per-pod merge ------------------------------------------------------------------
 // One block per pod of the round: the kC largest keys of the union of the pod's candidate lists, sorted
 // descending (0-padded), plus a STRICT upper bound `ub` on every key left out (0 = nothing left out):
-//   ub = max(max_l ub_l, (kC+1)-th key of the union + 1), where a tile list's ub_l is its minimum when it is
-//   full (its unseen nodes all score lower) and a rank list carries its own ub in slot kC.
-// The kC-th key is found by an 8-bit radix select over the 64-bit keys (keys are unique: score<<32 | ~idx).
+//   ub = max(max_l ub_l, largest key left out + 1), where a tile list's ub_l is its minimum when it is full
+//   (its unseen nodes all score lower) and a rank list carries its own ub in slot kC.
+// Selection: keys are unique (score << 32 | ~idx) and the lists, read in order, enumerate nodes in ascending
+// index within each score (tile lists: ascending node order; rank lists: descending keys of contiguous shards).
+// So the top kC = every key with score > τ plus the first `need` keys with score == τ in list order, where τ
+// is the largest score with count(score ≥ τ) ≥ kC: one LDS histogram of the scores (score_bits ≤ kHistBits)
+// and two block scans.  Wider score ranges use an 8-bit radix select over the whole key.
 // The record also carries the hoisted rows of the kStaged best candidates, read from this rank's replica of
 // the node table, so that the resolver never waits on HBM for a likely winner.
+constexpr int kHistBits = 10;
+
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* red, int lane, int wave, uint32_t& total) {
+  const uint32_t incl = wave_prefix_sum_u32(v);
+  if (lane == kWave - 1) red[wave] = incl;
+  __syncthreads();
+  uint32_t off = incl - v, tot = 0;
+#pragma unroll
+  for (int w = 0; w < kMergeThreads / kWave; ++w) {
+    off += w < wave ? red[w] : 0u;
+    tot += red[w];
+  }
+  __syncthreads();
+  total = tot;
+  return off;
+}
+
 template <bool RANK_LISTS>
 __global__ __launch_bounds__(kMergeThreads) void merge_round(DevTable T, EvalParams P,
                                                              const uint64_t* __restrict__ in, int64_t pod_stride,
                                                              int64_t list_stride, int n_lists, int list_len,
-                                                             const int64_t* __restrict__ cursor_p, int64_t end,
-                                                             int B, uint64_t* __restrict__ out) {
-  __shared__ uint32_t hist[256];
+                                                             int nb, const int32_t* __restrict__ poison,
+                                                             uint64_t* __restrict__ out) {
+  __shared__ uint32_t hist[1 << kHistBits];
   __shared__ __attribute__((aligned(16))) uint64_t sel[kC];
   __shared__ uint64_t red64[kMergeThreads / kWave];
   __shared__ uint32_t red32[kMergeThreads / kWave];
   __shared__ uint64_t sh_prefix;
-  __shared__ uint32_t sh_target, sh_nsel;
+  __shared__ uint32_t sh_target;
   KG_STAMP(1, 0);
-  const int64_t cursor = *cursor_p;
-  if (cursor >= end) return;
-  const int nb = (end - cursor) < (int64_t)B ? (int)(end - cursor) : B;
+  if (*poison) return;
   const int pod = blockIdx.x;
   if (pod >= nb) return;
   const int tid = threadIdx.x, lane = tid % kWave, wave = tid / kWave;
   const uint64_t* base = in + (size_t)pod * pod_stride;
-  KG_STAMP(1, 1);
 
-  // Keys held in registers: thread t owns chunks c = t + kMergeThreads*i of 8 consecutive keys.
+  // Keys held in registers: thread t owns chunks c = t + kMergeThreads*i of 8 consecutive keys (chunk order
+  // = list order = ascending node index within a score).
   const int chunks_per_list = list_len / 8;
   const int n_chunks = n_lists * chunks_per_list;
   uint64_t k[kMergeChunks][8];
@@ -274,16 +287,18 @@ __global__ __launch_bounds__(kMergeThreads) void merge_round(DevTable T, EvalPar
       for (int r = 0; r < 8; ++r) k[i][r] = 0;
     }
   }
-  KG_STAMP(1, 2);
+  const bool hist_path = P.score_bits <= kHistBits;
+  if (hist_path)
+    for (int b = tid; b < (1 << kHistBits); b += kMergeThreads) hist[b] = 0;
+  KG_STAMP(1, 1);
   // block reductions: Σ nz, max ub_in, max kmax
   {
     const uint32_t s = wave_sum_u32(nz);
-    const uint64_t u = wave_max_u64_dpp(ub_in), m = wave_max_u64_dpp(kmax);
+    const uint64_t u = wave_max_key(ub_in), m = wave_max_key(kmax);
     if (lane == 0) {
       red32[wave] = s;
       red64[wave] = u;
-      hist[wave] = (uint32_t)(m >> 32);
-      hist[8 + wave] = (uint32_t)m;
+      sel[wave] = m;
     }
     __syncthreads();
     uint32_t tot = 0;
@@ -291,18 +306,51 @@ __global__ __launch_bounds__(kMergeThreads) void merge_round(DevTable T, EvalPar
     for (int w = 0; w < kMergeThreads / kWave; ++w) {
       tot += red32[w];
       ubm = red64[w] > ubm ? red64[w] : ubm;
-      const uint64_t mw = ((uint64_t)hist[w] << 32) | hist[8 + w];
-      km = mw > km ? mw : km;
+      km = sel[w] > km ? sel[w] : km;
     }
     nz = tot;
     ub_in = ubm;
     kmax = km;
     __syncthreads();
   }
-  KG_STAMP(1, 3);
+  KG_STAMP(1, 2);
 
+  // selection predicate: key ≥ kth, and for the histogram path score > tau || (score == tau && tie rank < need)
   uint64_t kth = 1;  // select every non-zero key when there are at most kC of them
-  if (nz > (uint32_t)kC) {
+  uint32_t tau = 0, need = 0;
+  bool use_tau = false;
+  if (nz > (uint32_t)kC && hist_path) {
+#pragma unroll
+    for (int i = 0; i < kMergeChunks; ++i)
+#pragma unroll
+      for (int r = 0; r < 8; ++r)
+        if (k[i][r]) atomicAdd(&hist[(uint32_t)(k[i][r] >> 32)], 1u);
+    __syncthreads();
+    if (wave == 0) {
+      // lane l holds bins top-16l .. top-16l-15 (descending); τ = the bin where the count from the top reaches kC
+      constexpr int kPer = (1 << kHistBits) / kWave;
+      uint32_t b[kPer], s = 0;
+#pragma unroll
+      for (int q = 0; q < kPer; ++q) {
+        b[q] = hist[(1 << kHistBits) - 1 - kPer * lane - q];
+        s += b[q];
+      }
+      uint32_t above = wave_prefix_sum_u32(s) - s;
+#pragma unroll
+      for (int q = 0; q < kPer; ++q) {
+        if (above < (uint32_t)kC && above + b[q] >= (uint32_t)kC) {
+          sh_prefix = (uint64_t)((1 << kHistBits) - 1 - kPer * lane - q);
+          sh_target = (uint32_t)kC - above;  // keys needed from the τ bin
+        }
+        above += b[q];
+      }
+    }
+    __syncthreads();
+    tau = (uint32_t)sh_prefix;
+    need = sh_target;
+    use_tau = true;
+    KG_STAMP(1, 3);
+  } else if (nz > (uint32_t)kC) {
     int top = 7;
     while (top > 0 && ((kmax >> (8 * top)) & 0xFF) == 0) --top;  // bytes above kmax's leading byte are 0
     uint64_t prefix = 0, pmask = 0;
@@ -339,43 +387,63 @@ __global__ __launch_bounds__(kMergeThreads) void merge_round(DevTable T, EvalPar
       prefix = sh_prefix;
       target = sh_target;
       pmask |= 0xFFull << shift;
-      KG_STAMP(1, 4 + byte);
     }
     kth = prefix;
   }
-  // compaction of the selected keys (block prefix sum of per-thread counts) + the best key left out
+  // tie ranks at τ in list order (chunk c = t + 256·i: i-major, then thread), 16-bit fields per chunk pair
+  uint32_t tie_base[kMergeChunks] = {0, 0, 0, 0};
+  if (use_tau) {
+    uint32_t c01 = 0, c23 = 0;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      c01 += ((k[0][r] >> 32) == tau && k[0][r]) + (((k[1][r] >> 32) == tau && k[1][r]) << 16);
+      c23 += ((k[2][r] >> 32) == tau && k[2][r]) + (((k[3][r] >> 32) == tau && k[3][r]) << 16);
+    }
+    uint32_t t01, t23;
+    const uint32_t o01 = block_excl_scan(c01, red32, lane, wave, t01);
+    const uint32_t o23 = block_excl_scan(c23, red32, lane, wave, t23);
+    const uint32_t T0 = t01 & 0xFFFF, T1 = t01 >> 16, T2 = t23 & 0xFFFF;
+    tie_base[0] = o01 & 0xFFFF;
+    tie_base[1] = T0 + (o01 >> 16);
+    tie_base[2] = T0 + T1 + (o23 & 0xFFFF);
+    tie_base[3] = T0 + T1 + T2 + (o23 >> 16);
+  }
+  // selection + compaction + the best key left out
   uint32_t mycnt = 0;
   uint64_t next = 0;
+  uint32_t selmask[kMergeChunks];
 #pragma unroll
-  for (int i = 0; i < kMergeChunks; ++i)
+  for (int i = 0; i < kMergeChunks; ++i) {
+    uint32_t m = 0, tr = tie_base[i];
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
       const uint64_t v = k[i][r];
-      mycnt += (v >= kth) & (v != 0);
-      if (v && v < kth) next = v > next ? v : next;
+      bool s;
+      if (use_tau) {
+        const uint32_t sc = (uint32_t)(v >> 32);
+        const bool tie = v && sc == tau;
+        s = v && (sc > tau || (tie && tr < need));
+        tr += tie;
+      } else {
+        s = v && v >= kth;
+      }
+      m |= (uint32_t)s << r;
+      if (v && !s) next = v > next ? v : next;
     }
-  const uint32_t incl = wave_prefix_sum_u32(mycnt);
-  next = wave_max_u64_dpp(next);
-  if (lane == kWave - 1) red32[wave] = incl;
+    selmask[i] = m;
+    mycnt += __popc(m);
+  }
+  uint32_t n_sel;
+  uint32_t off = block_excl_scan(mycnt, red32, lane, wave, n_sel);
+  next = wave_max_key(next);
   if (lane == 0) red64[wave] = next;
   if (tid < kC) sel[tid] = 0;
   __syncthreads();
-  {
-    uint32_t off = incl - mycnt;
-    for (int w = 0; w < wave; ++w) off += red32[w];
 #pragma unroll
-    for (int i = 0; i < kMergeChunks; ++i)
+  for (int i = 0; i < kMergeChunks; ++i)
 #pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        const uint64_t v = k[i][r];
-        if (v >= kth && v) sel[off++] = v;
-      }
-    if (tid == 0) {
-      uint32_t t = 0;
-      for (int w = 0; w < kMergeThreads / kWave; ++w) t += red32[w];
-      sh_nsel = t;
-    }
-  }
+    for (int r = 0; r < 8; ++r)
+      if ((selmask[i] >> r) & 1) sel[off++] = k[i][r];
   __syncthreads();
   KG_STAMP(1, 13);
   uint64_t* o = out + (size_t)pod * kCandStride;
@@ -391,15 +459,14 @@ __global__ __launch_bounds__(kMergeThreads) void merge_round(DevTable T, EvalPar
       const ulonglong2 x = s2[q];  // broadcast LDS reads, all issued back to back
       rank += (x.x > v) + (x.y > v);
     }
-    const int n_sel = (int)sh_nsel;
-    if (lane < n_sel) o[rank] = v;
+    if (lane < (int)n_sel) o[rank] = v;
     else o[lane] = 0;  // positions ≥ n_sel
     if (lane == 0) {
       const uint64_t ub_sel = nx ? nx + 1 : 0;
       o[kC] = ub_in > ub_sel ? ub_in : ub_sel;
     }
     // hoisted rows of the kStaged best candidates (the resolver's likely winners)
-    if (lane < n_sel && rank < kStaged) {
+    if (lane < (int)n_sel && rank < kStaged) {
       const EvalRow er = make_eval_row(load_row(T, key_node(v)), P);
       uint64_t words[kEvalRowWords];
       __builtin_memcpy(words, &er, sizeof(er));  // well-defined type punning (no strict-aliasing hazard)
@@ -412,16 +479,20 @@ __global__ __launch_bounds__(kMergeThreads) void merge_round(DevTable T, EvalPar
 }
 
 // ---- round kernel 3: FIFO resolve --------------------------------------------------------------------
-// One wavefront replays the round's pods in queue order against the merged candidates.  Prologue (one
-// global-latency wait): the round's records (candidate keys, bound, hoisted rows of the best candidates) and
-// pod descriptors are copied HBM→LDS by LDS-DMA.  The per-pod loop then touches only LDS and registers.
+// One wavefront replays the round's pods [first, first + nb) in queue order against the merged candidates.
+// Prologue (one global-latency wait): the round's records (candidate keys, bound, hoisted rows of the best
+// candidates) and pod descriptors are copied HBM→LDS by LDS-DMA, and the rows the PREVIOUS round modified
+// (`prev_mod`, pipelined rounds: this round was evaluated on the table before they changed) are loaded as
+// modified lanes.  The per-pod loop then touches only LDS and registers.
 // Lane l < nM owns modified node l as a hoisted EvalRow kept current by assume_on (or, when the node was not
-// staged, a base Row loading from HBM plus the pods assumed since, materialised on first use).  Per pod:
-//   e     = the best candidate not modified in this round (ballot + ctz over the sorted list);
+// staged, a base Row plus the pods assumed since, materialised on first use).  Per pod:
+//   e     = the best candidate not modified (bitmap word prefetched one pod ahead, patched with the last winner);
 //   mbest = the exact re-score of the modified rows — skipped when the profile is monotone (assume never raises
-//           a node's key) and e is the pod's top candidate;
-//   valid iff max(e, mbest) ≥ ub (every node outside the list scores lower); otherwise the round ends here.
-// Writes out_keys[cursor + j] (0 = unschedulable), the modified rows back, and advances the cursor.
+//           a node's key, and a mid-update row reads ≥ its current key) and e is the pod's top candidate;
+//   valid iff max(e, mbest) ≥ ub (every node outside the list scores lower); otherwise the round ends here and
+//   sets `poison`, so the rest of the batch (evaluated for later pods) is skipped until the host re-syncs.
+// Writes out_keys[first + j] (0 = unschedulable), the rows modified in this round back to the table and into
+// `my_mod` ([0] = count, then node ids), and advances the cursor ctl[0].
 struct PodDelta {
   int64_t req_cpu, req_mem, nz_cpu, nz_mem, est_cpu, est_mem, pest_cpu, pest_mem;
   int32_t pods;
@@ -453,22 +524,40 @@ __device__ __forceinline__ Row with_delta(Row r, const PodDelta& d) {
   return r;
 }
 
+__device__ __forceinline__ EvalRow staged_row(const uint64_t* s_cand, int slot) {
+  const uint64_t* src = s_cand + (size_t)(slot / kStaged) * kCandStride + kRecRows + (slot % kStaged) * kEvalRowWords;
+  uint64_t words[kEvalRowWords];
+#pragma unroll
+  for (int q = 0; q < kEvalRowWords; ++q) words[q] = src[q];
+  EvalRow er;
+  __builtin_memcpy(&er, words, sizeof(er));
+  return er;
+}
+
 template <int PF>
 __global__ __launch_bounds__(kWave) void resolve_round(DevTable T, const DevPod* __restrict__ pods,
-                                                        int64_t* __restrict__ cursor_p, int64_t end, int B,
+                                                        int64_t* __restrict__ ctl, int64_t first, int nb,
                                                         const uint64_t* __restrict__ cand, EvalParams P,
                                                         uint64_t* __restrict__ out_keys, int bitmap_words,
-                                                        int64_t* __restrict__ round_stats) {
+                                                        const int32_t* __restrict__ prev_mod,
+                                                        int32_t* __restrict__ my_mod, int32_t* __restrict__ poison) {
   extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
   KG_STAMP(2, 0);
   const int lane = threadIdx.x;
-  const int64_t cursor = *cursor_p;
-  if (cursor >= end) return;
-  const int nb = (end - cursor) < (int64_t)B ? (int)(end - cursor) : B;
-  uint64_t* s_cand = smem;                                            // [B][kCandStride]
-  uint64_t* s_podw = s_cand + (size_t)B * kCandStride;                // [B] DevPod (kPodWords words)
-  uint32_t* bitmap = reinterpret_cast<uint32_t*>(s_podw + (size_t)B * kPodWords);
-  {  // prologue: LDS-DMA of records + pods, bitmap clear
+  if (*poison || ctl[0] != first || nb <= 0) return;
+  uint64_t* s_cand = smem;                                            // [nb][kCandStride]
+  uint64_t* s_podw = s_cand + (size_t)nb * kCandStride;               // [nb] DevPod (kPodWords words)
+  uint32_t* bitmap = reinterpret_cast<uint32_t*>(s_podw + (size_t)nb * kPodWords);
+  // previous round's modified rows (exact current state: the previous resolver wrote them back)
+  const int n_prev = prev_mod ? prev_mod[0] : 0;
+  uint32_t midx = 0xFFFFFFFFu;
+  Row mrow;
+  mrow.flags = 0;
+  if (lane < n_prev) {
+    midx = (uint32_t)prev_mod[1 + lane];
+    mrow = load_row(T, midx);
+  }
+  {  // prologue: LDS-DMA of records + pods, bitmap clear (16-B stores)
     const int n16 = nb * kCandStride / 2;
     for (int it = 0; it * kWave < n16; ++it) {
       const int idx = it * kWave + lane;
@@ -476,7 +565,7 @@ __global__ __launch_bounds__(kWave) void resolve_round(DevTable T, const DevPod*
         __builtin_amdgcn_global_load_lds((global_cvoid_ptr)(cand + 2 * (size_t)idx),
                                          (lds_void_ptr)(s_cand + 2 * (size_t)it * kWave), 16, 0, 0);
     }
-    const uint64_t* pw = reinterpret_cast<const uint64_t*>(pods + cursor);
+    const uint64_t* pw = reinterpret_cast<const uint64_t*>(pods + first);
     const int p16 = nb * kPodWords / 2;
     for (int it = 0; it * kWave < p16; ++it) {
       const int idx = it * kWave + lane;
@@ -484,9 +573,13 @@ __global__ __launch_bounds__(kWave) void resolve_round(DevTable T, const DevPod*
         __builtin_amdgcn_global_load_lds((global_cvoid_ptr)(pw + 2 * (size_t)idx),
                                          (lds_void_ptr)(s_podw + 2 * (size_t)it * kWave), 16, 0, 0);
     }
-    for (int w = lane; w < bitmap_words; w += kWave) bitmap[w] = 0;
+    uint4* b4 = reinterpret_cast<uint4*>(bitmap);
+    for (int w = lane; w < bitmap_words / 4; w += kWave) b4[w] = make_uint4(0, 0, 0, 0);
+    for (int w = (bitmap_words / 4) * 4 + lane; w < bitmap_words; w += kWave) bitmap[w] = 0;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (lane < n_prev) atomicOr(&bitmap[midx >> 5], 1u << (midx & 31));
   __syncthreads();
   KG_STAMP(2, 1);
   // staged[q] on lane l: node whose hoisted row sits at staged slot s = q·64 + l (record s / kStaged,
@@ -504,51 +597,43 @@ __global__ __launch_bounds__(kWave) void resolve_round(DevTable T, const DevPod*
   }
   const DevPod* s_pods = reinterpret_cast<const DevPod*>(s_podw);
 
-  uint32_t midx = 0xFFFFFFFFu;
-  // lane state (lane < nM): rsrc ≥ 0 → base hoisted row at staged slot rsrc (LDS), rsrc == -1 → base Row `mrow`
-  // (HBM load in flight); `dl` = pods assumed since the base; `er` = materialised current row when er_valid.
+  // lane state (lane < nM): rsrc ≥ 0 → base hoisted row at staged slot rsrc (LDS), rsrc == -1 → base Row `mrow`;
+  // `dl` = pods assumed since the base; `er` = materialised current row when er_valid; `touched` = modified
+  // in this round (written back at the end)
   int rsrc = -1;
   EvalRow er;
   er.flags = 0;
-  bool er_valid = false;
-  Row mrow;
-  mrow.flags = 0;
+  bool er_valid = false, touched = false;
   PodDelta dl = {};
   uint64_t my_out = 0;
-  int nM = 0;
+  int nM = n_prev;
   int consumed = 0;
+  uint32_t last_w = 0xFFFFFFFFu;
   uint64_t key_n = s_cand[lane];
   uint64_t ub_n = s_cand[kC];
   DevPod p_n = s_pods[0];
+  uint32_t word_n = bitmap[key_n ? key_node(key_n) >> 5 : 0u];
   for (int j = 0; j < nb; ++j) {
     const uint64_t key = key_n, ub = ub_n;
     const DevPod p = p_n;
+    const uint32_t word = word_n;
     const int jn = j + 1 < nb ? j + 1 : j;  // software prefetch of the next pod (branch-free)
     key_n = s_cand[(size_t)jn * kCandStride + lane];
     ub_n = s_cand[(size_t)jn * kCandStride + kC];
     p_n = s_pods[jn];
-    const uint32_t node = key_node(key);  // key 0 → node 0xFFFFFFFF: masked below, word index clamped
-    const uint32_t word = bitmap[(key ? node : 0u) >> 5];
-    const bool unmod = (key != 0) & !((word >> (node & 31)) & 1u);
+    const uint32_t node = key_node(key);  // key 0 → node 0xFFFFFFFF: masked below
+    // the prefetched word predates the previous pod's bitmap update: patch with its winner
+    const bool unmod = (key != 0) & !((word >> (node & 31)) & 1u) & (node != last_w);
+    word_n = bitmap[key_n ? key_node(key_n) >> 5 : 0u];
     const uint64_t um = __ballot(unmod);
     const int pos = um ? (int)__builtin_ctzll(um) : kC;
     const uint64_t e = um ? readlane_u64(key, pos) : 0;
     uint64_t best = e;
-    if (nM > 0 && (!P.monotone || pos > 0)) {  // slow path: re-score this round's modified rows
+    if (nM > 0 && (!P.monotone || pos > 0)) {  // slow path: re-score the modified rows
       uint64_t mk = 0;
       if (lane < nM) {
-        if (!er_valid) {  // materialise: staged hoisted row (LDS) or HBM row, plus the pods assumed since
-          if (rsrc >= 0) {
-            const uint64_t* src = s_cand + (size_t)(rsrc / kStaged) * kCandStride + kRecRows +
-                                  (rsrc % kStaged) * kEvalRowWords;
-            uint64_t words[kEvalRowWords];
-#pragma unroll
-            for (int q = 0; q < kEvalRowWords; ++q) words[q] = src[q];
-            __builtin_memcpy(&er, words, sizeof(er));
-            er = make_eval_row(with_delta(row_of(er), dl), P);
-          } else {
-            er = make_eval_row(with_delta(mrow, dl), P);
-          }
+        if (!er_valid) {  // materialise: staged hoisted row (LDS) or the base Row, plus the pods assumed since
+          er = make_eval_row(with_delta(rsrc >= 0 ? row_of(staged_row(s_cand, rsrc)) : mrow, dl), P);
           er_valid = true;
         }
         uint32_t t = 0;
@@ -561,14 +646,18 @@ __global__ __launch_bounds__(kWave) void resolve_round(DevTable T, const DevPod*
         }
         mk = ok ? make_key(t, midx) : 0;
       }
-      const uint64_t mbest = wave_max_u64_dpp(mk);
+      const uint64_t mbest = wave_max_key(mk);
       best = mbest > best ? mbest : best;
     }
     if (best < ub) break;  // an unseen node could still win: leave this pod to the next round
     my_out = lane == j ? best : my_out;
     ++consumed;
-    if (best == 0) continue;  // unschedulable (ub == 0: no feasible node anywhere)
+    if (best == 0) {  // unschedulable (ub == 0: no feasible node anywhere)
+      last_w = 0xFFFFFFFFu;
+      continue;
+    }
     const uint32_t w = key_node(best);
+    last_w = w;
     const uint64_t hit = __ballot((lane < nM) & (midx == w));
     const int owner = hit ? (int)__builtin_ctzll(hit) : nM;
     const bool me = lane == owner;
@@ -592,30 +681,25 @@ __global__ __launch_bounds__(kWave) void resolve_round(DevTable T, const DevPod*
     if (me) {  // assume the pod on the owner's row
       if (er_valid) assume_on(er, p, P);
       add_delta(dl, p);
+      touched = true;
     }
     if (j == 0 || j == 15 || j == 31) KG_STAMP(2, 2 + j / 8);
   }
-  if (lane < nM) {
-    if (er_valid) {
-      store_eval_row(T, midx, er);
-    } else if (rsrc >= 0) {
-      const uint64_t* src = s_cand + (size_t)(rsrc / kStaged) * kCandStride + kRecRows + (rsrc % kStaged) * kEvalRowWords;
-      uint64_t words[kEvalRowWords];
-#pragma unroll
-      for (int q = 0; q < kEvalRowWords; ++q) words[q] = src[q];
-      EvalRow base;
-      __builtin_memcpy(&base, words, sizeof(base));
-      store_mutable(T, midx, with_delta(row_of(base), dl));
-    } else {
-      store_mutable(T, midx, with_delta(mrow, dl));
-    }
+  if (touched) {
+    if (er_valid) store_eval_row(T, midx, er);
+    else store_mutable(T, midx, with_delta(rsrc >= 0 ? row_of(staged_row(s_cand, rsrc)) : mrow, dl));
   }
-  if (lane < consumed) out_keys[cursor + lane] = my_out;
+  const uint64_t tm = __ballot(touched);
+  const uint64_t lane_lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  if (touched) my_mod[1 + __popcll(tm & lane_lt)] = (int32_t)midx;
+  if (lane < consumed) out_keys[first + lane] = my_out;
   KG_STAMP(2, 30);
   if (lane == 0) {
-    *cursor_p = cursor + consumed;
-    round_stats[0] += 1;
-    round_stats[1] += consumed;
+    my_mod[0] = __popcll(tm);
+    ctl[0] = first + consumed;
+    ctl[1] += 1;
+    ctl[2] += consumed;
+    if (consumed < nb) *poison = 1;
   }
   KG_STAMP(2, 31);
 }
@@ -655,6 +739,24 @@ __global__ void apply_deltas(DevTable T, const RowDelta* __restrict__ d, int64_t
   atomicAdd((unsigned long long*)&T.la_pused_mem[k], (unsigned long long)x.d[8]);
 }
 
+__device__ __forceinline__ bool eval_hot_rt(const DevTable& T, int64_t i, const DevPod& p, const EvalParams& P,
+                                            uint32_t& t, bool& rare) {
+  const int pf = (P.fit_filter ? PF_FIT_FILTER : 0) | (P.fit_score ? PF_FIT_SCORE : 0) |
+                 (P.la_filter ? PF_LA_FILTER : 0) | (P.la_score ? PF_LA_SCORE : 0);
+  switch (pf) {
+#define KG_CASE(X)                                   \
+  case X: {                                          \
+    const HotRow h = load_hot<X>(T, i, P);           \
+    rare = (h.flags & F_RARE) != 0;                  \
+    return eval_hot<X>(h, p, P, t);                  \
+  }
+    KG_CASE(0) KG_CASE(1) KG_CASE(2) KG_CASE(3) KG_CASE(4) KG_CASE(5) KG_CASE(6) KG_CASE(7)
+    KG_CASE(8) KG_CASE(9) KG_CASE(10) KG_CASE(11) KG_CASE(12) KG_CASE(13) KG_CASE(14) KG_CASE(15)
+#undef KG_CASE
+  }
+  return false;
+}
+
 __device__ __forceinline__ bool eval_fast_rt(const EvalRow& n, const DevPod& p, const EvalParams& P, uint32_t& t,
                                              bool& rare) {
   const int pf = (P.fit_filter ? PF_FIT_FILTER : 0) | (P.fit_score ? PF_FIT_SCORE : 0) |
@@ -685,6 +787,10 @@ __global__ void debug_eval_paths(DevTable T, const DevPod* __restrict__ pods, in
     bool rare = false;
     const bool f2 = eval_fast_rt(er, pods[k], P, t2, rare);
     bad += !rare && ((f1 != f2) || (f1 && (uint32_t)t1 != t2));
+    uint32_t t3 = 0;
+    bool rare3 = false;
+    const bool f3 = eval_hot_rt(T, i, pods[k], P, t3, rare3);
+    bad += !rare3 && ((f1 != f3) || (f1 && (uint32_t)t1 != t3));
   }
   if (bad) atomicAdd(mismatches, bad);
 }
@@ -757,11 +863,14 @@ struct kg_engine {
   DevBuf<int32_t> cols32;
   DevBuf<DevPod> pods;
   int64_t n_staged = 0;
-  DevBuf<uint64_t> lists;     // [B][nt_local][kR] tile candidate lists (this rank)
+  DevBuf<uint64_t> lists;     // [2][B][nt_local][kR] tile candidate lists (this rank), by round parity
   DevBuf<uint64_t> gathered;  // [n_ranks][B][kCandStride] per-rank merged records (n_ranks > 1)
   DevBuf<uint64_t> cand;      // [B][kCandStride] final merged candidates
   DevBuf<uint64_t> out_keys;
-  DevBuf<int64_t> cursor;  // [0] cursor, [1] rounds, [2] consumed
+  DevBuf<int64_t> cursor;     // [0] cursor, [1] rounds, [2] consumed, [3] poison (int32 in its low word)
+  DevBuf<int32_t> modlists;   // [2][1 + kMaxB]: rows each round modified ([0] = count), by round parity
+  hipStream_t stream_r = nullptr;  // merge + exchange + resolve (high priority); `stream` runs eval + ingest
+  hipEvent_t ev_eval[2] = {nullptr, nullptr}, ev_res[2] = {nullptr, nullptr};
   DevBuf<RowDelta> deltas;
   DevBuf<int64_t> scratch64;
   DevBuf<int32_t> scratch32;
@@ -912,11 +1021,12 @@ int decode_pod(const kg_engine* e, const kg_pod& p, DevPod& d) {
   d.est_mem_d = (double)d.est_mem;
   d.nz_cpu32 = (int32_t)std::min<int64_t>(d.nz_cpu, kPodCpu32Max);
   d.est_cpu32 = (int32_t)std::min<int64_t>(d.est_cpu, kPodCpu32Max);
+  d.req_cpu32 = (int32_t)std::min<int64_t>(d.req_cpu, kFreeCpuAbs + 1);
+  d.req_mem_d = (double)std::min<int64_t>(d.req_mem, int64_t(1) << 53);
   d.flags = (zero ? P_ZERO_REQ : 0) | ((p.flags & KG_POD_DAEMONSET) ? P_DAEMONSET : 0) |
             (p.priority_class == KG_PRIO_PROD ? P_PROD : 0) |
             (p.priority_class == KG_PRIO_PROD && c.la_score_according_prod_usage ? P_LA_PROD_SCORE : 0);
   d.pad = 0;
-  d.pad2[0] = d.pad2[1] = 0;
   return 0;
 }
 
@@ -993,6 +1103,7 @@ void usage_for_score(const kg_node_metric& m, int64_t u[2]) {
 struct RoundGeom {
   int64_t N, shard, base, n_local;
   int nt_local, B, ppw, bitmap_words;
+  bool pipelined;  // eval(r+1) overlaps resolve(r): needs ≤ 2B-1 modified rows per round within one wave (B ≤ 32)
 };
 
 RoundGeom geometry(const kg_engine* e) {
@@ -1004,17 +1115,18 @@ RoundGeom geometry(const kg_engine* e) {
   g.nt_local = (int)std::max<int64_t>(1, (g.shard + kTile - 1) / kTile);
   g.B = (int)(e->cfg.batch_pods > 0 ? e->cfg.batch_pods : 32);
   g.ppw = (int)(e->cfg.pods_per_wave > 0 ? std::min<int64_t>(e->cfg.pods_per_wave, g.B) : 2);
-  g.bitmap_words = (int)((std::max<int64_t>(g.N, 1) + 31) / 32);
+  g.bitmap_words = (int)(((std::max<int64_t>(g.N, 1) + 127) / 128) * 4);  // whole 16-B stores
+  g.pipelined = 2 * g.B - 1 <= kWave && e->P.monotone;
   return g;
 }
 
-size_t resolve_lds_bytes(const RoundGeom& g) {
-  return ((size_t)g.B * kCandStride + (size_t)g.B * kPodWords) * 8 + (size_t)g.bitmap_words * 4;
+size_t resolve_lds_bytes(const RoundGeom& g, int nb) {
+  return ((size_t)nb * kCandStride + (size_t)nb * kPodWords) * 8 + (size_t)g.bitmap_words * 4;
 }
 
-dim3 eval_grid(const RoundGeom& g) {
+dim3 eval_grid(const RoundGeom& g, int nb) {
   // 1-D grid: tile groups × pod groups, swizzled over XCDs inside eval_round
-  return dim3((unsigned)(((g.nt_local + kEvalWaves - 1) / kEvalWaves) * ((g.B + g.ppw - 1) / g.ppw)));
+  return dim3((unsigned)(((g.nt_local + kEvalWaves - 1) / kEvalWaves) * ((nb + g.ppw - 1) / g.ppw)));
 }
 
 int profile_bits(const EvalParams& P) {
@@ -1030,49 +1142,84 @@ int profile_bits(const EvalParams& P) {
     case 12: CALL(12); break; case 13: CALL(13); break; case 14: CALL(14); break; case 15: CALL(15); break;   \
   }
 
-void launch_eval(kg_engine* e, const RoundGeom& g, int64_t end) {
-#define KG_EVAL(X)                                                                                                \
-  eval_round<X><<<eval_grid(g), kWave * kEvalWaves, 0, e->stream>>>(e->T, e->pods.p, e->cursor.p, end, g.B, g.ppw, \
-                                                                     g.base, g.n_local, g.nt_local, e->P, e->lists.p)
+int32_t* poison_ptr(kg_engine* e) { return reinterpret_cast<int32_t*>(e->cursor.p + 3); }
+uint64_t* lists_slot(kg_engine* e, const RoundGeom& g, int slot) {
+  return e->lists.p + (size_t)slot * g.B * g.nt_local * kR;
+}
+
+void launch_eval(kg_engine* e, const RoundGeom& g, int64_t first, int nb, int slot, hipStream_t st) {
+#define KG_EVAL(X)                                                                                        \
+  eval_round<X><<<eval_grid(g, nb), kWave * kEvalWaves, 0, st>>>(e->T, e->pods.p, first, nb, g.ppw, g.base, \
+                                                                 g.n_local, g.nt_local, e->P,             \
+                                                                 lists_slot(e, g, slot), poison_ptr(e))
   KG_PF_SWITCH(profile_bits(e->P), KG_EVAL)
 #undef KG_EVAL
 }
 
 // local merge: this rank's tile lists → per-pod record (single rank: the final candidates)
-void launch_merge_local(kg_engine* e, const RoundGeom& g, int64_t end) {
+void launch_merge_local(kg_engine* e, const RoundGeom& g, int nb, int slot, hipStream_t st) {
   uint64_t* dst = e->n_ranks > 1 ? e->gathered.p + (size_t)e->rank * g.B * kCandStride : e->cand.p;
-  merge_round<false><<<g.B, kMergeThreads, 0, e->stream>>>(e->T, e->P, e->lists.p, (int64_t)g.nt_local * kR, kR,
-                                                           g.nt_local, kR, e->cursor.p, end, g.B, dst);
+  merge_round<false><<<nb, kMergeThreads, 0, st>>>(e->T, e->P, lists_slot(e, g, slot), (int64_t)g.nt_local * kR,
+                                                   kR, g.nt_local, kR, nb, poison_ptr(e), dst);
 }
 
-void launch_merge_ranks(kg_engine* e, const RoundGeom& g, int64_t end) {
-  merge_round<true><<<g.B, kMergeThreads, 0, e->stream>>>(e->T, e->P, e->gathered.p, kCandStride,
-                                                          (int64_t)g.B * kCandStride, e->n_ranks, kC, e->cursor.p,
-                                                          end, g.B, e->cand.p);
+void launch_merge_ranks(kg_engine* e, const RoundGeom& g, int nb, hipStream_t st) {
+  merge_round<true><<<nb, kMergeThreads, 0, st>>>(e->T, e->P, e->gathered.p, kCandStride,
+                                                  (int64_t)g.B * kCandStride, e->n_ranks, kC, nb, poison_ptr(e),
+                                                  e->cand.p);
 }
 
-void launch_resolve(kg_engine* e, const RoundGeom& g, int64_t end) {
-#define KG_RESOLVE(X)                                                                                               \
-  resolve_round<X><<<1, kWave, resolve_lds_bytes(g), e->stream>>>(e->T, e->pods.p, e->cursor.p, end, g.B, e->cand.p, \
-                                                                 e->P, e->out_keys.p, g.bitmap_words, e->cursor.p + 1)
+void launch_resolve(kg_engine* e, const RoundGeom& g, int64_t first, int nb, int prev_slot, int slot,
+                    hipStream_t st) {
+  const int32_t* prev = prev_slot >= 0 ? e->modlists.p + (size_t)prev_slot * (1 + kMaxB) : nullptr;
+  int32_t* mine = e->modlists.p + (size_t)slot * (1 + kMaxB);
+#define KG_RESOLVE(X)                                                                                            \
+  resolve_round<X><<<1, kWave, resolve_lds_bytes(g, nb), st>>>(e->T, e->pods.p, e->cursor.p, first, nb, e->cand.p, \
+                                                               e->P, e->out_keys.p, g.bitmap_words, prev, mine,  \
+                                                               poison_ptr(e))
   KG_PF_SWITCH(profile_bits(e->P), KG_RESOLVE)
 #undef KG_RESOLVE
 }
 
-int launch_round(kg_engine* e, const RoundGeom& g, int64_t end) {
-  launch_eval(e, g, end);
-  HIP_TRY(hipGetLastError());
-  launch_merge_local(e, g, end);
+// merge → [all-gather + merge of the rank records] → resolve of one round, on stream st
+int launch_tail(kg_engine* e, const RoundGeom& g, int64_t first, int nb, int prev_slot, int slot, hipStream_t st) {
+  launch_merge_local(e, g, nb, slot, st);
   HIP_TRY(hipGetLastError());
   if (e->n_ranks > 1) {
     const size_t cnt = (size_t)g.B * kCandStride;
     uint64_t* mine = e->gathered.p + (size_t)e->rank * cnt;
-    NCCL_TRY(ncclAllGather(mine, e->gathered.p, cnt, ncclUint64, e->comm, e->stream));
-    launch_merge_ranks(e, g, end);
+    NCCL_TRY(ncclAllGather(mine, e->gathered.p, cnt, ncclUint64, e->comm, st));
+    launch_merge_ranks(e, g, nb, st);
     HIP_TRY(hipGetLastError());
   }
-  launch_resolve(e, g, end);
+  launch_resolve(e, g, first, nb, prev_slot, slot, st);
   HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+// One batch of rounds over pods [cur, end), pipelined when the geometry allows it:
+//   stream E: eval(r) after resolve(r-2) (pipelined) / resolve(r-1);
+//   stream R: merge(r) after eval(r), [RCCL], resolve(r) with round r-1's modified rows as modified lanes.
+// The first round of a batch starts from a fully written table (the host synchronised), so it has no
+// previous-round rows.  Returns after both streams drained.
+int run_batch(kg_engine* e, const RoundGeom& g, int64_t cur, int64_t end, int64_t n_rounds) {
+  HIP_TRY(hipMemsetAsync(poison_ptr(e), 0, 4, e->stream));
+  const int lag = g.pipelined ? 2 : 1;
+  for (int64_t r = 0; r < n_rounds; ++r) {
+    const int64_t first = cur + r * g.B;
+    const int nb = (int)std::min<int64_t>(g.B, end - first);
+    const int slot = (int)(r & 1);
+    if (r >= lag) HIP_TRY(hipStreamWaitEvent(e->stream, e->ev_res[(r - lag) & 1], 0));
+    launch_eval(e, g, first, nb, slot, e->stream);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(e->ev_eval[slot], e->stream));
+    HIP_TRY(hipStreamWaitEvent(e->stream_r, e->ev_eval[slot], 0));
+    const int prev_slot = (g.pipelined && r > 0) ? (int)((r - 1) & 1) : -1;
+    if (int rc = launch_tail(e, g, first, nb, prev_slot, slot, e->stream_r)) return rc;
+    HIP_TRY(hipEventRecord(e->ev_res[slot], e->stream_r));
+  }
+  HIP_TRY(hipStreamSynchronize(e->stream_r));
+  HIP_TRY(hipStreamSynchronize(e->stream));
   return 0;
 }
 
@@ -1083,7 +1230,7 @@ int prepare_rounds(kg_engine* e, RoundGeom& g) {
   if (g.nt_local > kMergeThreads * kMergeChunks)
     return fail(KG_E_UNSUPPORTED, "%lld nodes per rank exceed one merge block (%d)", (long long)g.shard,
                 kMergeThreads * kMergeChunks * kTile);
-  if (int rc = e->lists.ensure((size_t)g.B * g.nt_local * kR)) return rc;
+  if (int rc = e->lists.ensure((size_t)2 * g.B * g.nt_local * kR)) return rc;
   if (int rc = e->cand.ensure((size_t)g.B * kCandStride)) return rc;
   if (e->n_ranks > 1)
     if (int rc = e->gathered.ensure((size_t)e->n_ranks * g.B * kCandStride)) return rc;
@@ -1171,6 +1318,16 @@ int kg_engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank, int
   }
   if (hipGetDevice(&e->device) != hipSuccess) return bail(fail(KG_E_DEVICE, "no HIP device"));
   if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) return bail(fail(KG_E_DEVICE, "hipStreamCreate"));
+  {  // the serial merge → resolve chain gets the device's highest stream priority over the wide eval pass
+    int lo = 0, hi = 0;
+    if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess ||
+        hipStreamCreateWithPriority(&e->stream_r, hipStreamNonBlocking, hi) != hipSuccess)
+      return bail(fail(KG_E_DEVICE, "hipStreamCreateWithPriority"));
+    for (int k = 0; k < 2; ++k)
+      if (hipEventCreateWithFlags(&e->ev_eval[k], hipEventDisableTiming) != hipSuccess ||
+          hipEventCreateWithFlags(&e->ev_res[k], hipEventDisableTiming) != hipSuccess)
+        return bail(fail(KG_E_DEVICE, "hipEventCreate"));
+  }
   if (int rc = e->cols64.ensure(14 * cap)) return bail(rc);  // 12 int64 columns + inv_mem[2] (f64)
   if (int rc = e->cols32.ensure(5 * cap)) return bail(rc);   // alloc_pods, num_pods, flags, inv_cpu[2] (f32)
   if (hipMemset(e->cols64.p, 0, 14 * cap * 8) != hipSuccess || hipMemset(e->cols32.p, 0, 5 * cap * 4) != hipSuccess)
@@ -1196,6 +1353,8 @@ int kg_engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank, int
   e->T.cap = cap;
   if (int rc = e->cursor.ensure(4)) return bail(rc);
   if (hipMemset(e->cursor.p, 0, 4 * 8) != hipSuccess) return bail(fail(KG_E_DEVICE, "hipMemset"));
+  if (int rc = e->modlists.ensure(2 * (1 + kMaxB))) return bail(rc);
+  if (hipMemset(e->modlists.p, 0, 2 * (1 + kMaxB) * 4) != hipSuccess) return bail(fail(KG_E_DEVICE, "hipMemset"));
   e->nodes.assign(cap, kg_node{});
   e->metrics.assign(cap, kg_node_metric{});
   e->folded_usage.assign(2 * cap, 0);
@@ -1217,6 +1376,7 @@ int kg_engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank, int
   e->P.score_bits = (int32_t)bits_for(max_total);
   e->P.monotone = 1;  // NodeResourcesFit + LoadAwareScheduling: assume only lowers a node's key
   e->P.inv_la_wsum = 1.0f / (float)e->P.la_wsum;
+  e->P.fit_wsum32 = (int32_t)(e->P.fit_w_cpu + e->P.fit_w_mem);
   {
     const float wc = (float)e->P.fit_w_cpu, wm = (float)e->P.fit_w_mem;
     e->P.inv_fit_ws[0] = 0.0f;
@@ -1245,6 +1405,7 @@ int kg_engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank, int
 void kg_engine_destroy(kg_engine* e) {
   if (!e) return;
   if (e->stream) (void)hipStreamSynchronize(e->stream);
+  if (e->stream_r) (void)hipStreamSynchronize(e->stream_r);
   if (e->comm) ncclCommDestroy(e->comm);
   e->cols64.release();
   e->cols32.release();
@@ -1254,6 +1415,12 @@ void kg_engine_destroy(kg_engine* e) {
   e->cand.release();
   e->out_keys.release();
   e->cursor.release();
+  e->modlists.release();
+  for (int k = 0; k < 2; ++k) {
+    if (e->ev_eval[k]) (void)hipEventDestroy(e->ev_eval[k]);
+    if (e->ev_res[k]) (void)hipEventDestroy(e->ev_res[k]);
+  }
+  if (e->stream_r) (void)hipStreamDestroy(e->stream_r);
   e->deltas.release();
   e->scratch64.release();
   e->scratch32.release();
@@ -1369,24 +1536,17 @@ int kg_pods_schedule_staged(kg_engine* e, int64_t first, int64_t count, kg_stats
   RoundGeom g;
   if (int rc = prepare_rounds(e, g)) return rc;
   const int64_t end = first + count;
-  const int64_t init[3] = {first, 0, 0};
+  const int64_t init[4] = {first, 0, 0, 0};
   int64_t host_stats[3] = {first, 0, 0};
-  HIP_TRY(hipMemcpyAsync(e->cursor.p, init, 3 * 8, hipMemcpyHostToDevice, e->stream));
+  HIP_TRY(hipMemcpyAsync(e->cursor.p, init, 4 * 8, hipMemcpyHostToDevice, e->stream));
   HIP_TRY(hipStreamSynchronize(e->stream));
   int64_t cur = first;
-  int64_t launched = 0;
-  double avg = g.B;  // pods resolved per round, refined from the device counters
   while (cur < end) {
-    const int64_t remaining = end - cur;
-    int64_t rounds = (int64_t)std::ceil(remaining / std::max(1.0, avg));
-    rounds = std::max<int64_t>(rounds, 1);
-    for (int64_t r = 0; r < rounds; ++r)
-      if (int rc = launch_round(e, g, end)) return rc;
-    launched += rounds;
-    HIP_TRY(hipMemcpyAsync(host_stats, e->cursor.p, 3 * 8, hipMemcpyDeviceToHost, e->stream));
-    HIP_TRY(hipStreamSynchronize(e->stream));
+    // a round that stops early poisons the rest of its batch; the next batch restarts from the device cursor
+    const int64_t n_rounds = std::min<int64_t>((end - cur + g.B - 1) / g.B, kMaxBatchRounds);
+    if (int rc = run_batch(e, g, cur, end, n_rounds)) return rc;
+    HIP_TRY(hipMemcpy(host_stats, e->cursor.p, 3 * 8, hipMemcpyDeviceToHost));
     cur = host_stats[0];
-    if (host_stats[1] > 0) avg = std::max(1.0, (double)host_stats[2] / (double)host_stats[1]);
   }
   if (stats) {
     std::memset(stats, 0, sizeof(*stats));
@@ -1394,7 +1554,6 @@ int kg_pods_schedule_staged(kg_engine* e, int64_t first, int64_t count, kg_stats
     stats->node_evaluations = count * g.N;
     stats->seconds = now_s() - t0;
   }
-  (void)launched;
   return 0;
 }
 
@@ -1507,21 +1666,22 @@ int kg_bench_kernel(kg_engine* e, int which, int iters, double* avg_ms, double* 
                            hipMemcpyDeviceToDevice, e->stream));
     return 0;
   };
-  static const int64_t zero3[3] = {0, 0, 0};
+  static const int64_t zero4[4] = {0, 0, 0, 0};
+  const int nb = (int)end;
   if (int rc = snapshot(false)) return rc;
-  HIP_TRY(hipMemcpyAsync(e->cursor.p, zero3, 24, hipMemcpyHostToDevice, e->stream));
-  if (int rc = launch_round(e, g, end)) return rc;  // one real round: valid lists and candidates to replay on
+  HIP_TRY(hipMemcpyAsync(e->cursor.p, zero4, 32, hipMemcpyHostToDevice, e->stream));
+  if (int rc = run_batch(e, g, 0, end, 1)) return rc;  // one real round: valid lists and candidates to replay on
   if (int rc = snapshot(true)) return rc;
   hipEvent_t a, b;
   HIP_TRY(hipEventCreate(&a));
   HIP_TRY(hipEventCreate(&b));
   float total_ms = 0.f;
   for (int it = 0; it < iters; ++it) {
-    HIP_TRY(hipMemcpyAsync(e->cursor.p, zero3, 24, hipMemcpyHostToDevice, e->stream));
+    HIP_TRY(hipMemcpyAsync(e->cursor.p, zero4, 32, hipMemcpyHostToDevice, e->stream));
     HIP_TRY(hipEventRecord(a, e->stream));
-    if (which == 0) launch_eval(e, g, end);
-    else if (which == 1) launch_merge_local(e, g, end);
-    else launch_resolve(e, g, end);
+    if (which == 0) launch_eval(e, g, 0, nb, 0, e->stream);
+    else if (which == 1) launch_merge_local(e, g, nb, 0, e->stream);
+    else launch_resolve(e, g, 0, nb, -1, 0, e->stream);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(b, e->stream));
     HIP_TRY(hipEventSynchronize(b));
@@ -1535,14 +1695,14 @@ int kg_bench_kernel(kg_engine* e, int which, int iters, double* avg_ms, double* 
   (void)hipEventDestroy(a);
   (void)hipEventDestroy(b);
   save.release();
-  const double nb = (double)end;
+  const double nbd = (double)end;
   if (avg_ms) *avg_ms = total_ms / iters;
   if (algo_bytes) {
     // eval: SURVEY §8(d) per-evaluation bytes (Fit 56 B + LoadAware 20 B = 76 B per node) × pods × nodes,
     //       + the candidate lists written;  merge: lists read + records written;  resolve: records + pods read.
-    if (which == 0) *algo_bytes = nb * (double)g.n_local * kAlgoBytesPerNode + nb * g.nt_local * kR * 8.0 + nb * 64.0;
-    else if (which == 1) *algo_bytes = nb * g.nt_local * kR * 8.0 + nb * kCandStride * 8.0;
-    else *algo_bytes = nb * kCandStride * 8.0 + nb * 64.0;
+    if (which == 0) *algo_bytes = nbd * (double)g.n_local * kAlgoBytesPerNode + nbd * g.nt_local * kR * 8.0 + nbd * 96.0;
+    else if (which == 1) *algo_bytes = nbd * g.nt_local * kR * 8.0 + nbd * kCandStride * 8.0;
+    else *algo_bytes = nbd * kCandStride * 8.0 + nbd * 96.0;
   }
   return 0;
 }

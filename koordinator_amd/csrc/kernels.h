@@ -71,10 +71,11 @@ struct DevPod {
   int64_t nz_cpu, nz_mem;
   int64_t est_cpu, est_mem;
   double nz_mem_d, est_mem_d;  // the same quantities as f64 (exact below 2^53) for the memory score terms
+  double req_mem_d;            // min(req_mem, 2^53) for the f64 filter compare of the wide pass
   int32_t nz_cpu32, est_cpu32; // min(·, 2^30) for the 32-bit cpu score terms
+  int32_t req_cpu32;           // min(req_cpu, 2^30 + 1) for the 32-bit filter compare of the wide pass
   uint32_t flags;
-  uint32_t pad;
-  int64_t pad2[2];  // 96 B: a 16-B multiple for LDS-DMA
+  int64_t pad;  // 96 B: a 16-B multiple for LDS-DMA
 };
 static_assert(sizeof(DevPod) == 96, "DevPod layout");
 constexpr int kPodWords = (int)(sizeof(DevPod) / 8);
@@ -88,7 +89,7 @@ struct EvalParams {
   int32_t monotone;    // every enabled plugin's key can only drop when a pod is assumed (Fit, LoadAware)
   float inv_la_wsum;
   float inv_fit_ws[4];  // 1 / Σ fit weights, indexed by (alloc_cpu != 0) | (alloc_mem != 0) << 1
-  int32_t pad2;
+  int32_t fit_wsum32;   // Σ fit weights (cpu + memory)
 };
 
 struct Row {
@@ -443,6 +444,10 @@ __device__ __forceinline__ int64_t pick(bool c, int64_t a, int64_t b) {
   asm("" : "+v"(a), "+v"(b));
   return c ? b : a;
 }
+__device__ __forceinline__ int32_t pick(bool c, int32_t a, int32_t b) {
+  asm("" : "+v"(a), "+v"(b));
+  return c ? b : a;
+}
 __device__ __forceinline__ double pick(bool c, double a, double b) {
   asm("" : "+v"(a), "+v"(b));
   return c ? b : a;
@@ -487,6 +492,123 @@ __device__ __forceinline__ bool eval_fast(const EvalRow& n, const DevPod& p, con
   }
   total = t;
   return ok;
+}
+
+// ---------------------------------------------------------------------------------------------------
+// Wide-pass row (eval_round): the hoisted terms of one node in the narrowest exact types — cpu terms in
+// 32-bit lanes, memory terms as exact f64 integers, pod-count fit folded into the flags.  ~23 VGPRs per node
+// (EvalRow: 36) so a lane can hold 4 nodes at 4 waves/SIMD.  F_RARE marks a row outside the exact domain of
+// eval_hot (a pure function of the node, so it is decided once per tile, not per pod).
+// ---------------------------------------------------------------------------------------------------
+constexpr uint32_t F_PODS_OK = 1u << 5;  // HotRow only: F_VALID && len(Pods) + 1 <= AllowedPodNumber
+constexpr int64_t kFreeCpuAbs = 1ll << 30;  // |Allocatable - Requested| cpu bound of the 32-bit filter compare
+constexpr int64_t kFreeMemAbs = 1ll << 52;  // |Allocatable - Requested| memory bound of the f64 filter compare
+
+struct HotRow {
+  int32_t free_cpu, fnz_cpu, alloc_cpu, la_free_cpu, la_pfree_cpu, la_alloc_cpu;
+  float inv_cpu, la_inv_cpu;
+  double free_mem, fnz_mem, alloc_mem, inv_mem, la_free_mem, la_pfree_mem, la_alloc_mem, la_inv_mem;
+  uint32_t flags;
+};
+
+template <int PF>
+__device__ __forceinline__ HotRow load_hot(const DevTable& T, int64_t i, const EvalParams& P) {
+  HotRow h;
+  const uint32_t fl = T.flags[i];
+  const int64_t ac = T.alloc_cpu[i], am = T.alloc_mem[i];
+  const int64_t fc = ac - T.req_cpu[i], fm = am - T.req_mem[i];
+  const int64_t fnc = ac - T.nz_cpu[i], fnm = am - T.nz_mem[i];
+  const int64_t lac = T.la_alloc_cpu[i], lam = T.la_alloc_mem[i];
+  const int64_t lfc = lac - T.la_used_cpu[i], lfm = lam - T.la_used_mem[i];
+  const int64_t lpc = lac - T.la_pused_cpu[i], lpm = lam - T.la_pused_mem[i];
+  const bool pods_ok = T.num_pods[i] + 1 <= T.alloc_pods[i];
+  bool ok = true;
+  if constexpr ((PF & PF_FIT_FILTER) != 0) ok &= (fc >= -kFreeCpuAbs) & (fc <= kFreeCpuAbs) & (fm > -kFreeMemAbs) & (fm < kFreeMemAbs);
+  if constexpr ((PF & PF_FIT_SCORE) != 0) {
+    if (P.fit_w_cpu) ok &= cpu_dom(ac, fnc);
+    if (P.fit_w_mem) ok &= mem_dom(am, fnm);
+  }
+  if constexpr ((PF & PF_LA_SCORE) != 0) {
+    if (fl & F_LA_SCORE) {
+      if (P.la_w_cpu) ok &= cpu_dom(lac, lfc) && cpu_dom(lac, lpc);
+      if (P.la_w_mem) ok &= mem_dom(lam, lfm) && mem_dom(lam, lpm);
+    }
+  }
+  h.free_cpu = (int32_t)fc;
+  h.fnz_cpu = (int32_t)fnc;
+  h.alloc_cpu = (int32_t)ac;
+  h.la_free_cpu = (int32_t)lfc;
+  h.la_pfree_cpu = (int32_t)lpc;
+  h.la_alloc_cpu = (int32_t)lac;
+  h.inv_cpu = T.inv_cpu[i];
+  h.la_inv_cpu = T.inv_cpu[T.cap + i];
+  h.free_mem = (double)fm;
+  h.fnz_mem = (double)fnm;
+  h.alloc_mem = (double)am;
+  h.inv_mem = T.inv_mem[i];
+  h.la_free_mem = (double)lfm;
+  h.la_pfree_mem = (double)lpm;
+  h.la_alloc_mem = (double)lam;
+  h.la_inv_mem = T.inv_mem[T.cap + i];
+  h.flags = (fl & ~(F_RARE | F_PODS_OK)) | ((fl & F_VALID) && pods_ok ? F_PODS_OK : 0u) | (ok ? 0u : F_RARE);
+  return h;
+}
+
+// eval_hot<PF>: eval_fast on a HotRow (caller guarantees !(flags & F_RARE)).  The pod's request/estimate
+// quantities come pre-narrowed in DevPod: req_cpu32 = min(req_cpu, 2^30 + 1) (any larger request fails the
+// 32-bit compare exactly as the int64 one does, since |free_cpu| ≤ 2^30), req_mem_d = min(req_mem, 2^53).
+template <int PF>
+__device__ __forceinline__ bool eval_hot(const HotRow& n, const DevPod& p, const EvalParams& P, uint32_t& total) {
+  const uint32_t pf = p.flags;
+  bool ok = (n.flags & F_VALID) != 0;
+  if constexpr ((PF & PF_FIT_FILTER) != 0) {
+    const bool fits = (p.req_cpu32 <= n.free_cpu) & (p.req_mem_d <= n.free_mem);
+    ok = ((n.flags & F_PODS_OK) != 0) & (((pf & P_ZERO_REQ) != 0) | fits);
+  }
+  if constexpr ((PF & PF_LA_FILTER) != 0) {
+    const uint32_t passbit = (pf & P_PROD) ? F_LA_PASS_PROD : F_LA_PASS;
+    ok = ok & (((pf & P_DAEMONSET) != 0) | ((n.flags & passbit) != 0));
+  }
+  uint32_t t = 0;
+  if constexpr ((PF & PF_FIT_SCORE) != 0) {
+    const int32_t qc = lrs_cpu(n.fnz_cpu - p.nz_cpu32, n.alloc_cpu, n.inv_cpu);
+    const int32_t qm = lrs_mem(n.fnz_mem - p.nz_mem_d, n.alloc_mem, n.inv_mem);
+    const int32_t s = (int32_t)(__umul24((uint32_t)qc, (uint32_t)P.fit_w_cpu) +
+                                __umul24((uint32_t)qm, (uint32_t)P.fit_w_mem));
+    // inside the domain every weighted resource has allocatable > 0: Σ weights is the profile constant
+    const int32_t f = div_est(s, P.fit_wsum32, P.inv_fit_ws[3]);
+    t += __umul24((uint32_t)(P.fit_wsum32 ? f : 0), (uint32_t)P.weight_fit);
+  }
+  if constexpr ((PF & PF_LA_SCORE) != 0) {
+    const bool prodv = (pf & P_LA_PROD_SCORE) != 0;
+    const int32_t fc = pick(prodv, n.la_free_cpu, n.la_pfree_cpu);
+    const double fm = pick(prodv, n.la_free_mem, n.la_pfree_mem);
+    const int32_t qc = lrs_cpu(fc - p.est_cpu32, n.la_alloc_cpu, n.la_inv_cpu);
+    const int32_t qm = lrs_mem(fm - p.est_mem_d, n.la_alloc_mem, n.la_inv_mem);
+    const int32_t s = (int32_t)(__umul24((uint32_t)qc, (uint32_t)P.la_w_cpu) +
+                                __umul24((uint32_t)qm, (uint32_t)P.la_w_mem));
+    const int32_t l = div_est(s, (int32_t)P.la_wsum, P.inv_la_wsum);
+    t += __umul24((uint32_t)((n.flags & F_LA_SCORE) ? l : 0), (uint32_t)P.weight_la);
+  }
+  total = t;
+  return ok;
+}
+
+// Wave max of a packed 64-bit key in two 32-bit DPP max scans (high word, then the low word among the lanes
+// holding the high maximum).  Returns the wave-uniform maximum.
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+  v = max(v, dpp_u32<0x111, 0xf>(v));  // row_shr:1
+  v = max(v, dpp_u32<0x112, 0xf>(v));  // row_shr:2
+  v = max(v, dpp_u32<0x114, 0xf>(v));  // row_shr:4
+  v = max(v, dpp_u32<0x118, 0xf>(v));  // row_shr:8
+  v = max(v, dpp_u32<0x142, 0xa>(v));  // row_bcast:15
+  v = max(v, dpp_u32<0x143, 0xc>(v));  // row_bcast:31
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+__device__ __forceinline__ uint64_t wave_max_key(uint64_t k) {
+  const uint32_t hi = wave_max_u32((uint32_t)(k >> 32));
+  const uint32_t lo = wave_max_u32((uint32_t)(k >> 32) == hi ? (uint32_t)k : 0u);
+  return ((uint64_t)hi << 32) | lo;
 }
 
 }  // namespace kg
