@@ -43,7 +43,8 @@ constexpr int kCandStride = 128;      // per-pod record: 1 KiB (a 16-B multiple,
 constexpr int kMergeThreads = 256;
 constexpr int kMergeChunks = 4;       // chunks of 8 keys per merge thread: ≤ 1024 tile lists = 262144 nodes per rank
 constexpr double kAlgoBytesPerNode = 76.0;  // SURVEY §8(d) b_node for C1-C3: Fit 56 B + LoadAware 20 B
-constexpr int64_t kMaxBatchRounds = 256;  // rounds launched between two host synchronisations
+constexpr int64_t kMaxBatchRounds = 256;
+constexpr int64_t kSpinLimit = 1 << 25;  // resolver chain wait: ~2 s of s_sleep(2) before reporting an error  // rounds launched between two host synchronisations
 constexpr int64_t kMaxNodes = 1 << 19;  // resolver LDS: N/8-byte bitmap (≤ 64 KiB) + the round's records (≤ 64 KiB)
 static_assert(kRecRows + kStaged * kEvalRowWords <= kCandStride, "record layout");
 
@@ -534,30 +535,31 @@ __device__ __forceinline__ EvalRow staged_row(const uint64_t* s_cand, int slot) 
   return er;
 }
 
+// End of a resolver: every store of this wave visible device-wide, then ctl[4] = seq (agent-scope release) for
+// the next round's resolver, which may already be resident on the other round stream.
+__device__ __forceinline__ void publish_round(int64_t* ctl, int64_t seq) {
+  __threadfence();
+  if (threadIdx.x == 0) __hip_atomic_store(&ctl[4], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 template <int PF>
 __global__ __launch_bounds__(kWave) void resolve_round(DevTable T, const DevPod* __restrict__ pods,
                                                         int64_t* __restrict__ ctl, int64_t first, int nb,
                                                         const uint64_t* __restrict__ cand, EvalParams P,
                                                         uint64_t* __restrict__ out_keys, int bitmap_words,
                                                         const int32_t* __restrict__ prev_mod,
-                                                        int32_t* __restrict__ my_mod, int32_t* __restrict__ poison) {
+                                                        int32_t* __restrict__ my_mod, int32_t* __restrict__ poison,
+                                                        int64_t seq, int wait) {
   extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
   KG_STAMP(2, 0);
   const int lane = threadIdx.x;
-  if (*poison || ctl[0] != first || nb <= 0) return;
+  // the serial chain outranks the wide pass's waves when they share a SIMD
+  __builtin_amdgcn_s_setprio(3);
   uint64_t* s_cand = smem;                                            // [nb][kCandStride]
   uint64_t* s_podw = s_cand + (size_t)nb * kCandStride;               // [nb] DevPod (kPodWords words)
   uint32_t* bitmap = reinterpret_cast<uint32_t*>(s_podw + (size_t)nb * kPodWords);
-  // previous round's modified rows (exact current state: the previous resolver wrote them back)
-  const int n_prev = prev_mod ? prev_mod[0] : 0;
-  uint32_t midx = 0xFFFFFFFFu;
-  Row mrow;
-  mrow.flags = 0;
-  if (lane < n_prev) {
-    midx = (uint32_t)prev_mod[1 + lane];
-    mrow = load_row(T, midx);
-  }
-  {  // prologue: LDS-DMA of records + pods, bitmap clear (16-B stores)
+  {  // prologue, independent of the previous round: LDS-DMA of this round's records (merged on this stream)
+     // + pods, bitmap clear (16-B stores)
     const int n16 = nb * kCandStride / 2;
     for (int it = 0; it * kWave < n16; ++it) {
       const int idx = it * kWave + lane;
@@ -576,6 +578,39 @@ __global__ __launch_bounds__(kWave) void resolve_round(DevTable T, const DevPod*
     uint4* b4 = reinterpret_cast<uint4*>(bitmap);
     for (int w = lane; w < bitmap_words / 4; w += kWave) b4[w] = make_uint4(0, 0, 0, 0);
     for (int w = (bitmap_words / 4) * 4 + lane; w < bitmap_words; w += kWave) bitmap[w] = 0;
+  }
+  // Chain on the previous round's resolver (the other round stream): its rows, cursor, poison and modified-row
+  // list are published with an agent-scope release of ctl[4] = its sequence number.  Bounded spin: a missing
+  // predecessor reports an error instead of hanging the device.
+  int timed_out = 0;
+  if (wait) {
+    if (lane == 0) {
+      int64_t it = 0;
+      while (__hip_atomic_load(&ctl[4], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < seq - 1) {
+        __builtin_amdgcn_s_sleep(2);
+        if (++it > kSpinLimit) {
+          timed_out = 1;
+          break;
+        }
+      }
+    }
+    timed_out = __builtin_amdgcn_readfirstlane(timed_out);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
+  if (timed_out || *poison || ctl[0] != first) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the LDS-DMA lands before the wave retires
+    if (lane == 0 && timed_out) ctl[5] = 1;
+    publish_round(ctl, seq);
+    return;
+  }
+  // previous round's modified rows (exact current state: the previous resolver wrote them back)
+  const int n_prev = prev_mod ? prev_mod[0] : 0;
+  uint32_t midx = 0xFFFFFFFFu;
+  Row mrow;
+  mrow.flags = 0;
+  if (lane < n_prev) {
+    midx = (uint32_t)prev_mod[1 + lane];
+    mrow = load_row(T, midx);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -701,6 +736,7 @@ __global__ __launch_bounds__(kWave) void resolve_round(DevTable T, const DevPod*
     ctl[2] += consumed;
     if (consumed < nb) *poison = 1;
   }
+  publish_round(ctl, seq);
   KG_STAMP(2, 31);
 }
 
@@ -864,13 +900,16 @@ struct kg_engine {
   DevBuf<DevPod> pods;
   int64_t n_staged = 0;
   DevBuf<uint64_t> lists;     // [2][B][nt_local][kR] tile candidate lists (this rank), by round parity
-  DevBuf<uint64_t> gathered;  // [n_ranks][B][kCandStride] per-rank merged records (n_ranks > 1)
-  DevBuf<uint64_t> cand;      // [B][kCandStride] final merged candidates
+  DevBuf<uint64_t> gathered;  // [2][n_ranks][B][kCandStride] per-rank merged records (n_ranks > 1), by round parity
+  DevBuf<uint64_t> cand;      // [2][B][kCandStride] final merged candidates, by round parity
   DevBuf<uint64_t> out_keys;
-  DevBuf<int64_t> cursor;     // [0] cursor, [1] rounds, [2] consumed, [3] poison (int32 in its low word)
+  DevBuf<int64_t> cursor;     // [0] cursor, [1] rounds, [2] consumed, [3] poison (int32 in its low word),
+                              // [4] last published resolver sequence, [5] device error (chain wait timed out)
   DevBuf<int32_t> modlists;   // [2][1 + kMaxB]: rows each round modified ([0] = count), by round parity
-  hipStream_t stream_r = nullptr;  // merge + exchange + resolve (high priority); `stream` runs eval + ingest
-  hipEvent_t ev_eval[2] = {nullptr, nullptr}, ev_res[2] = {nullptr, nullptr};
+  // round r runs on rs[r & 1] (eval → merge → [RCCL on comms[r & 1]] → resolve); `stream` runs ingest
+  hipStream_t rs[2] = {nullptr, nullptr};
+  ncclComm_t comm2 = nullptr;
+  hipEvent_t ev_res[2] = {nullptr, nullptr};
   DevBuf<RowDelta> deltas;
   DevBuf<int64_t> scratch64;
   DevBuf<int32_t> scratch32;
@@ -1157,69 +1196,78 @@ void launch_eval(kg_engine* e, const RoundGeom& g, int64_t first, int nb, int sl
 }
 
 // local merge: this rank's tile lists → per-pod record (single rank: the final candidates)
+uint64_t* cand_slot(kg_engine* e, const RoundGeom& g, int slot) { return e->cand.p + (size_t)slot * g.B * kCandStride; }
+uint64_t* gathered_slot(kg_engine* e, const RoundGeom& g, int slot) {
+  return e->gathered.p + (size_t)slot * e->n_ranks * g.B * kCandStride;
+}
+
 void launch_merge_local(kg_engine* e, const RoundGeom& g, int nb, int slot, hipStream_t st) {
-  uint64_t* dst = e->n_ranks > 1 ? e->gathered.p + (size_t)e->rank * g.B * kCandStride : e->cand.p;
+  uint64_t* dst = e->n_ranks > 1 ? gathered_slot(e, g, slot) + (size_t)e->rank * g.B * kCandStride : cand_slot(e, g, slot);
   merge_round<false><<<nb, kMergeThreads, 0, st>>>(e->T, e->P, lists_slot(e, g, slot), (int64_t)g.nt_local * kR,
                                                    kR, g.nt_local, kR, nb, poison_ptr(e), dst);
 }
 
-void launch_merge_ranks(kg_engine* e, const RoundGeom& g, int nb, hipStream_t st) {
-  merge_round<true><<<nb, kMergeThreads, 0, st>>>(e->T, e->P, e->gathered.p, kCandStride,
+void launch_merge_ranks(kg_engine* e, const RoundGeom& g, int nb, int slot, hipStream_t st) {
+  merge_round<true><<<nb, kMergeThreads, 0, st>>>(e->T, e->P, gathered_slot(e, g, slot), kCandStride,
                                                   (int64_t)g.B * kCandStride, e->n_ranks, kC, nb, poison_ptr(e),
-                                                  e->cand.p);
+                                                  cand_slot(e, g, slot));
 }
 
 void launch_resolve(kg_engine* e, const RoundGeom& g, int64_t first, int nb, int prev_slot, int slot,
-                    hipStream_t st) {
+                    int64_t seq, int wait, hipStream_t st) {
   const int32_t* prev = prev_slot >= 0 ? e->modlists.p + (size_t)prev_slot * (1 + kMaxB) : nullptr;
   int32_t* mine = e->modlists.p + (size_t)slot * (1 + kMaxB);
 #define KG_RESOLVE(X)                                                                                            \
-  resolve_round<X><<<1, kWave, resolve_lds_bytes(g, nb), st>>>(e->T, e->pods.p, e->cursor.p, first, nb, e->cand.p, \
+  resolve_round<X><<<1, kWave, resolve_lds_bytes(g, nb), st>>>(e->T, e->pods.p, e->cursor.p, first, nb,              \
+                                                               cand_slot(e, g, slot),                             \
                                                                e->P, e->out_keys.p, g.bitmap_words, prev, mine,  \
-                                                               poison_ptr(e))
+                                                               poison_ptr(e), seq, wait)
   KG_PF_SWITCH(profile_bits(e->P), KG_RESOLVE)
 #undef KG_RESOLVE
 }
 
-// merge → [all-gather + merge of the rank records] → resolve of one round, on stream st
-int launch_tail(kg_engine* e, const RoundGeom& g, int64_t first, int nb, int prev_slot, int slot, hipStream_t st) {
+// merge → [all-gather + merge of the rank records] of one round, on stream st
+int launch_merge(kg_engine* e, const RoundGeom& g, int nb, int slot, hipStream_t st) {
   launch_merge_local(e, g, nb, slot, st);
   HIP_TRY(hipGetLastError());
   if (e->n_ranks > 1) {
     const size_t cnt = (size_t)g.B * kCandStride;
-    uint64_t* mine = e->gathered.p + (size_t)e->rank * cnt;
-    NCCL_TRY(ncclAllGather(mine, e->gathered.p, cnt, ncclUint64, e->comm, st));
-    launch_merge_ranks(e, g, nb, st);
+    uint64_t* all = gathered_slot(e, g, slot);
+    NCCL_TRY(ncclAllGather(all + (size_t)e->rank * cnt, all, cnt, ncclUint64, slot ? e->comm2 : e->comm, st));
+    launch_merge_ranks(e, g, nb, slot, st);
     HIP_TRY(hipGetLastError());
   }
-  launch_resolve(e, g, first, nb, prev_slot, slot, st);
-  HIP_TRY(hipGetLastError());
   return 0;
 }
 
-// One batch of rounds over pods [cur, end), pipelined when the geometry allows it:
-//   stream E: eval(r) after resolve(r-2) (pipelined) / resolve(r-1);
-//   stream R: merge(r) after eval(r), [RCCL], resolve(r) with round r-1's modified rows as modified lanes.
-// The first round of a batch starts from a fully written table (the host synchronised), so it has no
-// previous-round rows.  Returns after both streams drained.
+// One batch of rounds over pods [cur, end).  Round r runs on stream rs[r & 1]: eval(r) → merge(r) →
+// [RCCL all-gather on that stream's communicator] → resolve(r), the resolve waiting on resolve(r-1) (the
+// other stream).  Stream order makes eval(r) start right after resolve(r-2), so it overlaps resolve(r-1)
+// (the pipelined protocol: round r-1's rows are modified lanes of resolve(r)); merge(r) also runs off the
+// serial resolve chain.  Unpipelined geometries (B > 32) put every round on rs[0].  The first round of a
+// batch starts from a fully written table (the host synchronised), so it has no previous-round rows.
 int run_batch(kg_engine* e, const RoundGeom& g, int64_t cur, int64_t end, int64_t n_rounds) {
-  HIP_TRY(hipMemsetAsync(poison_ptr(e), 0, 4, e->stream));
-  const int lag = g.pipelined ? 2 : 1;
+  HIP_TRY(hipMemsetAsync(e->cursor.p + 3, 0, 3 * 8, e->rs[0]));  // poison, resolver sequence, device error
+  if (g.pipelined) {  // rs[1] must not start round 1 before that reset
+    HIP_TRY(hipEventRecord(e->ev_res[1], e->rs[0]));
+    HIP_TRY(hipStreamWaitEvent(e->rs[1], e->ev_res[1], 0));
+  }
   for (int64_t r = 0; r < n_rounds; ++r) {
     const int64_t first = cur + r * g.B;
     const int nb = (int)std::min<int64_t>(g.B, end - first);
     const int slot = (int)(r & 1);
-    if (r >= lag) HIP_TRY(hipStreamWaitEvent(e->stream, e->ev_res[(r - lag) & 1], 0));
-    launch_eval(e, g, first, nb, slot, e->stream);
+    hipStream_t st = g.pipelined ? e->rs[slot] : e->rs[0];
+    launch_eval(e, g, first, nb, slot, st);
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipEventRecord(e->ev_eval[slot], e->stream));
-    HIP_TRY(hipStreamWaitEvent(e->stream_r, e->ev_eval[slot], 0));
+    if (int rc = launch_merge(e, g, nb, slot, st)) return rc;
+    // pipelined: resolve(r) chains on resolve(r-1) through the device sequence word (resolve_round), so its
+    // launch and prologue overlap the previous resolver instead of waiting for a cross-stream event
     const int prev_slot = (g.pipelined && r > 0) ? (int)((r - 1) & 1) : -1;
-    if (int rc = launch_tail(e, g, first, nb, prev_slot, slot, e->stream_r)) return rc;
-    HIP_TRY(hipEventRecord(e->ev_res[slot], e->stream_r));
+    launch_resolve(e, g, first, nb, prev_slot, slot, r + 1, g.pipelined && r > 0, st);
+    HIP_TRY(hipGetLastError());
   }
-  HIP_TRY(hipStreamSynchronize(e->stream_r));
-  HIP_TRY(hipStreamSynchronize(e->stream));
+  HIP_TRY(hipStreamSynchronize(e->rs[0]));
+  HIP_TRY(hipStreamSynchronize(e->rs[1]));
   return 0;
 }
 
@@ -1231,9 +1279,9 @@ int prepare_rounds(kg_engine* e, RoundGeom& g) {
     return fail(KG_E_UNSUPPORTED, "%lld nodes per rank exceed one merge block (%d)", (long long)g.shard,
                 kMergeThreads * kMergeChunks * kTile);
   if (int rc = e->lists.ensure((size_t)2 * g.B * g.nt_local * kR)) return rc;
-  if (int rc = e->cand.ensure((size_t)g.B * kCandStride)) return rc;
+  if (int rc = e->cand.ensure((size_t)2 * g.B * kCandStride)) return rc;
   if (e->n_ranks > 1)
-    if (int rc = e->gathered.ensure((size_t)e->n_ranks * g.B * kCandStride)) return rc;
+    if (int rc = e->gathered.ensure((size_t)2 * e->n_ranks * g.B * kCandStride)) return rc;
   return 0;
 }
 
@@ -1318,15 +1366,15 @@ int kg_engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank, int
   }
   if (hipGetDevice(&e->device) != hipSuccess) return bail(fail(KG_E_DEVICE, "no HIP device"));
   if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) return bail(fail(KG_E_DEVICE, "hipStreamCreate"));
-  {  // the serial merge → resolve chain gets the device's highest stream priority over the wide eval pass
+  {  // round streams at the device's highest priority (the serial resolve chain runs on them)
     int lo = 0, hi = 0;
-    if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess ||
-        hipStreamCreateWithPriority(&e->stream_r, hipStreamNonBlocking, hi) != hipSuccess)
-      return bail(fail(KG_E_DEVICE, "hipStreamCreateWithPriority"));
-    for (int k = 0; k < 2; ++k)
-      if (hipEventCreateWithFlags(&e->ev_eval[k], hipEventDisableTiming) != hipSuccess ||
-          hipEventCreateWithFlags(&e->ev_res[k], hipEventDisableTiming) != hipSuccess)
+    if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) return bail(fail(KG_E_DEVICE, "hipDeviceGetStreamPriorityRange"));
+    for (int k = 0; k < 2; ++k) {
+      if (hipStreamCreateWithPriority(&e->rs[k], hipStreamNonBlocking, hi) != hipSuccess)
+        return bail(fail(KG_E_DEVICE, "hipStreamCreateWithPriority"));
+      if (hipEventCreateWithFlags(&e->ev_res[k], hipEventDisableTiming) != hipSuccess)
         return bail(fail(KG_E_DEVICE, "hipEventCreate"));
+    }
   }
   if (int rc = e->cols64.ensure(14 * cap)) return bail(rc);  // 12 int64 columns + inv_mem[2] (f64)
   if (int rc = e->cols32.ensure(5 * cap)) return bail(rc);   // alloc_pods, num_pods, flags, inv_cpu[2] (f32)
@@ -1351,8 +1399,8 @@ int kg_engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank, int
   e->T.inv_cpu = (float*)(e->cols32.p + 3 * cap);
   e->T.inv_mem = (double*)(e->cols64.p + 12 * cap);
   e->T.cap = cap;
-  if (int rc = e->cursor.ensure(4)) return bail(rc);
-  if (hipMemset(e->cursor.p, 0, 4 * 8) != hipSuccess) return bail(fail(KG_E_DEVICE, "hipMemset"));
+  if (int rc = e->cursor.ensure(8)) return bail(rc);
+  if (hipMemset(e->cursor.p, 0, 8 * 8) != hipSuccess) return bail(fail(KG_E_DEVICE, "hipMemset"));
   if (int rc = e->modlists.ensure(2 * (1 + kMaxB))) return bail(rc);
   if (hipMemset(e->modlists.p, 0, 2 * (1 + kMaxB) * 4) != hipSuccess) return bail(fail(KG_E_DEVICE, "hipMemset"));
   e->nodes.assign(cap, kg_node{});
@@ -1397,6 +1445,9 @@ int kg_engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank, int
     ncclUniqueId id;
     std::memcpy(&id, nccl_id, sizeof(id));
     if (ncclCommInitRank(&e->comm, n_ranks, id, rank) != ncclSuccess) return bail(fail(KG_E_COLLECTIVE, "ncclCommInitRank"));
+    // a second communicator for the odd-round stream: collectives of one communicator never run concurrently
+    if (ncclCommSplit(e->comm, 0, rank, &e->comm2, nullptr) != ncclSuccess)
+      return bail(fail(KG_E_COLLECTIVE, "ncclCommSplit"));
   }
   *out = e;
   return 0;
@@ -1405,7 +1456,9 @@ int kg_engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank, int
 void kg_engine_destroy(kg_engine* e) {
   if (!e) return;
   if (e->stream) (void)hipStreamSynchronize(e->stream);
-  if (e->stream_r) (void)hipStreamSynchronize(e->stream_r);
+  for (int k = 0; k < 2; ++k)
+    if (e->rs[k]) (void)hipStreamSynchronize(e->rs[k]);
+  if (e->comm2) ncclCommDestroy(e->comm2);
   if (e->comm) ncclCommDestroy(e->comm);
   e->cols64.release();
   e->cols32.release();
@@ -1417,10 +1470,9 @@ void kg_engine_destroy(kg_engine* e) {
   e->cursor.release();
   e->modlists.release();
   for (int k = 0; k < 2; ++k) {
-    if (e->ev_eval[k]) (void)hipEventDestroy(e->ev_eval[k]);
     if (e->ev_res[k]) (void)hipEventDestroy(e->ev_res[k]);
+    if (e->rs[k]) (void)hipStreamDestroy(e->rs[k]);
   }
-  if (e->stream_r) (void)hipStreamDestroy(e->stream_r);
   e->deltas.release();
   e->scratch64.release();
   e->scratch32.release();
@@ -1536,16 +1588,17 @@ int kg_pods_schedule_staged(kg_engine* e, int64_t first, int64_t count, kg_stats
   RoundGeom g;
   if (int rc = prepare_rounds(e, g)) return rc;
   const int64_t end = first + count;
-  const int64_t init[4] = {first, 0, 0, 0};
-  int64_t host_stats[3] = {first, 0, 0};
-  HIP_TRY(hipMemcpyAsync(e->cursor.p, init, 4 * 8, hipMemcpyHostToDevice, e->stream));
+  const int64_t init[6] = {first, 0, 0, 0, 0, 0};
+  int64_t host_stats[6] = {first, 0, 0, 0, 0, 0};
+  HIP_TRY(hipMemcpyAsync(e->cursor.p, init, 6 * 8, hipMemcpyHostToDevice, e->stream));
   HIP_TRY(hipStreamSynchronize(e->stream));
   int64_t cur = first;
   while (cur < end) {
     // a round that stops early poisons the rest of its batch; the next batch restarts from the device cursor
     const int64_t n_rounds = std::min<int64_t>((end - cur + g.B - 1) / g.B, kMaxBatchRounds);
     if (int rc = run_batch(e, g, cur, end, n_rounds)) return rc;
-    HIP_TRY(hipMemcpy(host_stats, e->cursor.p, 3 * 8, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(host_stats, e->cursor.p, 6 * 8, hipMemcpyDeviceToHost));
+    if (host_stats[5]) return fail(KG_E_DEVICE, "resolver chain wait timed out (round sequence %lld)", (long long)host_stats[4]);
     cur = host_stats[0];
   }
   if (stats) {
@@ -1666,10 +1719,10 @@ int kg_bench_kernel(kg_engine* e, int which, int iters, double* avg_ms, double* 
                            hipMemcpyDeviceToDevice, e->stream));
     return 0;
   };
-  static const int64_t zero4[4] = {0, 0, 0, 0};
+  static const int64_t zero4[6] = {0, 0, 0, 0, 0, 0};
   const int nb = (int)end;
   if (int rc = snapshot(false)) return rc;
-  HIP_TRY(hipMemcpyAsync(e->cursor.p, zero4, 32, hipMemcpyHostToDevice, e->stream));
+  HIP_TRY(hipMemcpyAsync(e->cursor.p, zero4, 48, hipMemcpyHostToDevice, e->stream));
   if (int rc = run_batch(e, g, 0, end, 1)) return rc;  // one real round: valid lists and candidates to replay on
   if (int rc = snapshot(true)) return rc;
   hipEvent_t a, b;
@@ -1677,11 +1730,11 @@ int kg_bench_kernel(kg_engine* e, int which, int iters, double* avg_ms, double* 
   HIP_TRY(hipEventCreate(&b));
   float total_ms = 0.f;
   for (int it = 0; it < iters; ++it) {
-    HIP_TRY(hipMemcpyAsync(e->cursor.p, zero4, 32, hipMemcpyHostToDevice, e->stream));
+    HIP_TRY(hipMemcpyAsync(e->cursor.p, zero4, 48, hipMemcpyHostToDevice, e->stream));
     HIP_TRY(hipEventRecord(a, e->stream));
     if (which == 0) launch_eval(e, g, 0, nb, 0, e->stream);
     else if (which == 1) launch_merge_local(e, g, nb, 0, e->stream);
-    else launch_resolve(e, g, 0, nb, -1, 0, e->stream);
+    else launch_resolve(e, g, 0, nb, -1, 0, 1, 0, e->stream);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(b, e->stream));
     HIP_TRY(hipEventSynchronize(b));

@@ -18,8 +18,8 @@ with Engine(cfg, n) as e:
     e.schedule(pods)
     st = np.zeros((4, 32, 2), dtype=np.uint64)
     abi.check(e.lib, e.lib.kg_debug_stamps(e.h, abi.ptr(st)))
-print(f"eval wave-pods: {int(st[3, 0, 0])}, exact-path fallbacks: {int(st[3, 0, 1])}")
-st[3, 0] = 0
+pass
+pass
 for k, name in enumerate(("eval", "merge", "resolve")):
     pts = [(i, int(st[k, i, 0]), int(st[k, i, 1])) for i in range(32) if st[k, i, 0]]
     if not pts:
