@@ -38,7 +38,7 @@ def parse():
     ap.add_argument("--nodes", type=int, default=100_000)
     ap.add_argument("--pods-per-step", type=int, default=100_000)
     ap.add_argument("--batch", type=int, default=32)
-    ap.add_argument("--pods-per-wave", type=int, default=2)
+    ap.add_argument("--pods-per-wave", type=int, default=8)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")

@@ -87,6 +87,84 @@ typedef const __attribute__((address_space(1))) void* global_cvoid_ptr;
 // row reads as a mix of pre- and post-assume columns, whose key is ≥ the row's current key (monotone profile);
 // the resolver re-scores those rows exactly.  `poison` ≠ 0: an earlier round of this batch stopped early, so
 // this round's pods are not the next ones — nothing to do.
+// Per (pod, tile): the tile's top-kR packed keys from v[j] = feasible ? total + 1 : 0 (one value per node, so a
+// compare needs no feasibility mask).  τ = the largest v with count(v ≥ τ) ≥ kR, one ballot per value bit;
+// ties at τ go to the lowest node index (register j, then lane).  Writes the list in ascending node order.
+__device__ __forceinline__ void select_write(const uint32_t (&v)[kNPT], const uint32_t (&gidx)[kNPT], int vbits,
+                                             uint64_t* __restrict__ out, int lane) {
+  uint64_t fm[kNPT], sel[kNPT];
+  int nfeas = 0;
+#pragma unroll
+  for (int j = 0; j < kNPT; ++j) {
+    fm[j] = __ballot(v[j] != 0);
+    nfeas += __popcll(fm[j]);
+  }
+  if (nfeas <= kR) {
+#pragma unroll
+    for (int j = 0; j < kNPT; ++j) sel[j] = fm[j];
+  } else {
+    uint32_t cur = 0;
+    for (int b = vbits - 1; b >= 0; --b) {
+      const uint32_t c = cur | (1u << b);
+      int cnt = 0;
+#pragma unroll
+      for (int j = 0; j < kNPT; ++j) cnt += __popcll(__ballot(v[j] >= c));
+      if (cnt >= kR) cur = c;
+    }
+    int need = kR;
+    uint64_t eq[kNPT];
+#pragma unroll
+    for (int j = 0; j < kNPT; ++j) {
+      sel[j] = __ballot(v[j] > cur);
+      eq[j] = __ballot(v[j] == cur);
+      need -= __popcll(sel[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < kNPT; ++j) {
+      uint64_t m = eq[j];
+      while (need > 0 && m) {
+        const uint64_t low = m & (~m + 1);
+        sel[j] |= low;
+        m ^= low;
+        --need;
+      }
+    }
+  }
+  const uint64_t lane_lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  int base = 0;
+#pragma unroll
+  for (int j = 0; j < kNPT; ++j) {
+    if ((sel[j] >> lane) & 1) out[base + __popcll(sel[j] & lane_lt)] = make_key(v[j] - 1, gidx[j]);
+    base += __popcll(sel[j]);
+  }
+  if (lane >= base && lane < kR) out[lane] = 0;
+}
+
+// A tile holding a row outside eval_hot's exact domain: the reference-shaped int64 path for every pod (rare).
+// The row index is laundered inside the loop so the compiler cannot hoist the 19 column addresses out of it
+// (they would stay live across the wide loop and halve its occupancy).
+__device__ __forceinline__ void eval_tile_exact(const DevTable& T, const DevPod* __restrict__ pods, int64_t first,
+                                             int p0, int p1, int tile, int64_t node_base, int64_t n_local,
+                                             int nt_local, const EvalParams& P, uint64_t* __restrict__ lists,
+                                             int vbits) {
+  const int lane = threadIdx.x % kWave;
+  uint32_t gidx[kNPT];
+#pragma unroll
+  for (int j = 0; j < kNPT; ++j) gidx[j] = (uint32_t)(node_base + (int64_t)tile * kTile + j * kWave + lane);
+  for (int pi = p0; pi < p1; ++pi) {
+    const DevPod p = pods[first + pi];
+    uint32_t v[kNPT];
+#pragma unroll
+    for (int j = 0; j < kNPT; ++j) {
+      int64_t local = (int64_t)tile * kTile + j * kWave + lane;
+      asm volatile("" : "+v"(local));
+      int64_t t = 0;
+      v[j] = (local < n_local && eval_node(load_row(T, node_base + local), p, P, t)) ? (uint32_t)t + 1u : 0u;
+    }
+    select_write(v, gidx, vbits, lists + ((size_t)pi * nt_local + tile) * kR, lane);
+  }
+}
+
 template <int PF>
 __global__ __launch_bounds__(kWave* kEvalWaves) void eval_round(DevTable T, const DevPod* __restrict__ pods,
                                                                   int64_t first, int nb, int pods_per_wave,
@@ -106,6 +184,7 @@ __global__ __launch_bounds__(kWave* kEvalWaves) void eval_round(DevTable T, cons
   const int p0 = (int)(wgid % (uint32_t)n_pg) * pods_per_wave;
   if (tile >= nt_local || p0 >= nb) return;
   const int p1 = (p0 + pods_per_wave) < nb ? (p0 + pods_per_wave) : nb;
+  const int vbits = P.score_bits + 1;  // v = total + 1 ≤ 2^score_bits
 
   HotRow rows[kNPT];
   uint32_t gidx[kNPT];
@@ -124,74 +203,19 @@ __global__ __launch_bounds__(kWave* kEvalWaves) void eval_round(DevTable T, cons
   }
   KG_STAMP(0, 1);
   // a row outside eval_hot's exact domain anywhere in the tile: the whole tile takes the exact path
-  const bool exact_tile = __ballot(rare) != 0;
-  const uint64_t lane_lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-
+  if (__ballot(rare)) {
+    eval_tile_exact(T, pods, first, p0, p1, tile, node_base, n_local, nt_local, P, lists, vbits);
+    return;
+  }
   for (int pi = p0; pi < p1; ++pi) {
     const DevPod p = pods[first + pi];
-    uint32_t tot[kNPT];
-    bool okv[kNPT];
-    if (!exact_tile) {
-#pragma unroll
-      for (int j = 0; j < kNPT; ++j) okv[j] = eval_hot<PF>(rows[j], p, P, tot[j]);
-    } else {
-#pragma unroll
-      for (int j = 0; j < kNPT; ++j) {
-        const int64_t local = (int64_t)tile * kTile + j * kWave + lane;
-        int64_t t = 0;
-        okv[j] = local < n_local && eval_node(load_row(T, node_base + local), p, P, t);
-        tot[j] = (uint32_t)t;
-      }
-    }
-    uint64_t fm[kNPT];
-    int nfeas = 0;
+    uint32_t v[kNPT];
 #pragma unroll
     for (int j = 0; j < kNPT; ++j) {
-      fm[j] = __ballot(okv[j]);
-      nfeas += __popcll(fm[j]);
+      uint32_t t = 0;
+      v[j] = eval_hot<PF>(rows[j], p, P, t) ? t + 1u : 0u;
     }
-    uint64_t sel[kNPT];
-    if (nfeas <= kR) {
-#pragma unroll
-      for (int j = 0; j < kNPT; ++j) sel[j] = fm[j];
-    } else {
-      // τ = largest score with count(score ≥ τ) ≥ kR, one ballot per score bit.
-      uint32_t cur = 0;
-      for (int b = P.score_bits - 1; b >= 0; --b) {
-        const uint32_t c = cur | (1u << b);
-        int cnt = 0;
-#pragma unroll
-        for (int j = 0; j < kNPT; ++j) cnt += __popcll(__ballot(okv[j] && tot[j] >= c));
-        if (cnt >= kR) cur = c;
-      }
-      int need = kR;
-      uint64_t eq[kNPT];
-#pragma unroll
-      for (int j = 0; j < kNPT; ++j) {
-        sel[j] = __ballot(okv[j] && tot[j] > cur);
-        eq[j] = __ballot(okv[j] && tot[j] == cur);
-        need -= __popcll(sel[j]);
-      }
-      // ties at τ: lowest node index first (register j, then lane)
-#pragma unroll
-      for (int j = 0; j < kNPT; ++j) {
-        uint64_t m = eq[j];
-        while (need > 0 && m) {
-          const uint64_t low = m & (~m + 1);
-          sel[j] |= low;
-          m ^= low;
-          --need;
-        }
-      }
-    }
-    uint64_t* out = lists + ((size_t)pi * nt_local + tile) * kR;
-    int base = 0;
-#pragma unroll
-    for (int j = 0; j < kNPT; ++j) {
-      if ((sel[j] >> lane) & 1) out[base + __popcll(sel[j] & lane_lt)] = make_key(tot[j], gidx[j]);
-      base += __popcll(sel[j]);
-    }
-    if (lane >= base && lane < kR) out[lane] = 0;
+    select_write(v, gidx, vbits, lists + ((size_t)pi * nt_local + tile) * kR, lane);
   }
   KG_STAMP(0, 31);
 }
@@ -778,7 +802,8 @@ __global__ void apply_deltas(DevTable T, const RowDelta* __restrict__ d, int64_t
 __device__ __forceinline__ bool eval_hot_rt(const DevTable& T, int64_t i, const DevPod& p, const EvalParams& P,
                                             uint32_t& t, bool& rare) {
   const int pf = (P.fit_filter ? PF_FIT_FILTER : 0) | (P.fit_score ? PF_FIT_SCORE : 0) |
-                 (P.la_filter ? PF_LA_FILTER : 0) | (P.la_score ? PF_LA_SCORE : 0);
+                 (P.la_filter ? PF_LA_FILTER : 0) | (P.la_score ? PF_LA_SCORE : 0) |
+                 (P.la_score && P.la_prod_score ? PF_LA_PROD : 0);
   switch (pf) {
 #define KG_CASE(X)                                   \
   case X: {                                          \
@@ -788,6 +813,7 @@ __device__ __forceinline__ bool eval_hot_rt(const DevTable& T, int64_t i, const 
   }
     KG_CASE(0) KG_CASE(1) KG_CASE(2) KG_CASE(3) KG_CASE(4) KG_CASE(5) KG_CASE(6) KG_CASE(7)
     KG_CASE(8) KG_CASE(9) KG_CASE(10) KG_CASE(11) KG_CASE(12) KG_CASE(13) KG_CASE(14) KG_CASE(15)
+    KG_CASE(24) KG_CASE(25) KG_CASE(26) KG_CASE(27) KG_CASE(28) KG_CASE(29) KG_CASE(30) KG_CASE(31)
 #undef KG_CASE
   }
   return false;
@@ -1153,7 +1179,7 @@ RoundGeom geometry(const kg_engine* e) {
   g.n_local = std::min<int64_t>(g.shard, g.N - g.base);
   g.nt_local = (int)std::max<int64_t>(1, (g.shard + kTile - 1) / kTile);
   g.B = (int)(e->cfg.batch_pods > 0 ? e->cfg.batch_pods : 32);
-  g.ppw = (int)(e->cfg.pods_per_wave > 0 ? std::min<int64_t>(e->cfg.pods_per_wave, g.B) : 2);
+  g.ppw = (int)(e->cfg.pods_per_wave > 0 ? std::min<int64_t>(e->cfg.pods_per_wave, g.B) : 8);
   g.bitmap_words = (int)(((std::max<int64_t>(g.N, 1) + 127) / 128) * 4);  // whole 16-B stores
   g.pipelined = 2 * g.B - 1 <= kWave && e->P.monotone;
   return g;
@@ -1170,7 +1196,7 @@ dim3 eval_grid(const RoundGeom& g, int nb) {
 
 int profile_bits(const EvalParams& P) {
   return (P.fit_filter ? PF_FIT_FILTER : 0) | (P.fit_score ? PF_FIT_SCORE : 0) | (P.la_filter ? PF_LA_FILTER : 0) |
-         (P.la_score ? PF_LA_SCORE : 0);
+         (P.la_score ? PF_LA_SCORE : 0) | (P.la_score && P.la_prod_score ? PF_LA_PROD : 0);
 }
 
 #define KG_PF_SWITCH(pf, CALL)                                                                   \
@@ -1179,6 +1205,8 @@ int profile_bits(const EvalParams& P) {
     case 4: CALL(4); break;   case 5: CALL(5); break;   case 6: CALL(6); break;   case 7: CALL(7); break;     \
     case 8: CALL(8); break;   case 9: CALL(9); break;   case 10: CALL(10); break; case 11: CALL(11); break;   \
     case 12: CALL(12); break; case 13: CALL(13); break; case 14: CALL(14); break; case 15: CALL(15); break;   \
+    case 24: CALL(24); break; case 25: CALL(25); break; case 26: CALL(26); break; case 27: CALL(27); break;   \
+    case 28: CALL(28); break; case 29: CALL(29); break; case 30: CALL(30); break; case 31: CALL(31); break;   \
   }
 
 int32_t* poison_ptr(kg_engine* e) { return reinterpret_cast<int32_t*>(e->cursor.p + 3); }
@@ -1329,7 +1357,7 @@ void kg_config_default(kg_config* c) {
   c->weight_fit = 1;
   c->weight_loadaware = 1;
   c->batch_pods = 32;
-  c->pods_per_wave = 2;
+  c->pods_per_wave = 8;
   c->device_id = -1;
 }
 
@@ -1425,6 +1453,7 @@ int kg_engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank, int
   e->P.monotone = 1;  // NodeResourcesFit + LoadAwareScheduling: assume only lowers a node's key
   e->P.inv_la_wsum = 1.0f / (float)e->P.la_wsum;
   e->P.fit_wsum32 = (int32_t)(e->P.fit_w_cpu + e->P.fit_w_mem);
+  e->P.la_prod_score = (int32_t)(c.la_score_according_prod_usage != 0);
   {
     const float wc = (float)e->P.fit_w_cpu, wm = (float)e->P.fit_w_mem;
     e->P.inv_fit_ws[0] = 0.0f;

@@ -38,6 +38,7 @@ __device__ unsigned long long g_stamps[4][32][2];
 
 // profile bits (compile-time specialisation of the evaluation kernels)
 constexpr int PF_FIT_FILTER = 1, PF_FIT_SCORE = 2, PF_LA_FILTER = 4, PF_LA_SCORE = 8;
+constexpr int PF_LA_PROD = 16;  // LoadAware ScoreAccordingProdUsage: prod pods score on the prod-usage terms
 
 // node flags (device)
 constexpr uint32_t F_VALID = 1u << 0;
@@ -90,6 +91,8 @@ struct EvalParams {
   float inv_la_wsum;
   float inv_fit_ws[4];  // 1 / Σ fit weights, indexed by (alloc_cpu != 0) | (alloc_mem != 0) << 1
   int32_t fit_wsum32;   // Σ fit weights (cpu + memory)
+  int32_t la_prod_score;  // LoadAwareSchedulingArgs.ScoreAccordingProdUsage
+  int32_t pad3;
 };
 
 struct Row {
@@ -520,7 +523,8 @@ __device__ __forceinline__ HotRow load_hot(const DevTable& T, int64_t i, const E
   const int64_t fnc = ac - T.nz_cpu[i], fnm = am - T.nz_mem[i];
   const int64_t lac = T.la_alloc_cpu[i], lam = T.la_alloc_mem[i];
   const int64_t lfc = lac - T.la_used_cpu[i], lfm = lam - T.la_used_mem[i];
-  const int64_t lpc = lac - T.la_pused_cpu[i], lpm = lam - T.la_pused_mem[i];
+  constexpr bool kProd = (PF & PF_LA_PROD) != 0;
+  const int64_t lpc = kProd ? lac - T.la_pused_cpu[i] : 0, lpm = kProd ? lam - T.la_pused_mem[i] : 0;
   const bool pods_ok = T.num_pods[i] + 1 <= T.alloc_pods[i];
   bool ok = true;
   if constexpr ((PF & PF_FIT_FILTER) != 0) ok &= (fc >= -kFreeCpuAbs) & (fc <= kFreeCpuAbs) & (fm > -kFreeMemAbs) & (fm < kFreeMemAbs);
@@ -530,8 +534,8 @@ __device__ __forceinline__ HotRow load_hot(const DevTable& T, int64_t i, const E
   }
   if constexpr ((PF & PF_LA_SCORE) != 0) {
     if (fl & F_LA_SCORE) {
-      if (P.la_w_cpu) ok &= cpu_dom(lac, lfc) && cpu_dom(lac, lpc);
-      if (P.la_w_mem) ok &= mem_dom(lam, lfm) && mem_dom(lam, lpm);
+      if (P.la_w_cpu) ok &= cpu_dom(lac, lfc) && (!kProd || cpu_dom(lac, lpc));
+      if (P.la_w_mem) ok &= mem_dom(lam, lfm) && (!kProd || mem_dom(lam, lpm));
     }
   }
   h.free_cpu = (int32_t)fc;
@@ -580,9 +584,13 @@ __device__ __forceinline__ bool eval_hot(const HotRow& n, const DevPod& p, const
     t += __umul24((uint32_t)(P.fit_wsum32 ? f : 0), (uint32_t)P.weight_fit);
   }
   if constexpr ((PF & PF_LA_SCORE) != 0) {
-    const bool prodv = (pf & P_LA_PROD_SCORE) != 0;
-    const int32_t fc = pick(prodv, n.la_free_cpu, n.la_pfree_cpu);
-    const double fm = pick(prodv, n.la_free_mem, n.la_pfree_mem);
+    int32_t fc = n.la_free_cpu;
+    double fm = n.la_free_mem;
+    if constexpr ((PF & PF_LA_PROD) != 0) {
+      const bool prodv = (pf & P_LA_PROD_SCORE) != 0;
+      fc = pick(prodv, n.la_free_cpu, n.la_pfree_cpu);
+      fm = pick(prodv, n.la_free_mem, n.la_pfree_mem);
+    }
     const int32_t qc = lrs_cpu(fc - p.est_cpu32, n.la_alloc_cpu, n.la_inv_cpu);
     const int32_t qm = lrs_mem(fm - p.est_mem_d, n.la_alloc_mem, n.la_inv_mem);
     const int32_t s = (int32_t)(__umul24((uint32_t)qc, (uint32_t)P.la_w_cpu) +

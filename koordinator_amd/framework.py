@@ -59,7 +59,7 @@ class Profile:
 
 
 def build_config(la: LoadAwareSchedulingArgs | None = None, fit: NodeResourcesFitArgs | None = None,
-                 profile: Profile | None = None, batch_pods: int = 32, pods_per_wave: int = 2,
+                 profile: Profile | None = None, batch_pods: int = 32, pods_per_wave: int = 8,
                  device_id: int = -1) -> np.ndarray:
     la = la or LoadAwareSchedulingArgs()
     fit = fit or NodeResourcesFitArgs()
