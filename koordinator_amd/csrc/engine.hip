@@ -737,9 +737,9 @@ __global__ __launch_bounds__(kWave) void resolve_round(DevTable T, const DevPod*
       if (lane == 0) atomicOr(&bitmap[w >> 5], 1u << (w & 31));
       ++nM;
     }
-    if (me) {  // assume the pod on the owner's row
+    if (me) {  // assume the pod on the owner's row (the delta only matters while the row is not materialised)
       if (er_valid) assume_on(er, p, P);
-      add_delta(dl, p);
+      else add_delta(dl, p);
       touched = true;
     }
     if (j == 0 || j == 15 || j == 31) KG_STAMP(2, 2 + j / 8);
