@@ -167,7 +167,9 @@ def main():
     # per-kernel live timing (HIP events on the engine stream) for the roofline
     kernels = {name: e.bench_kernel(which, args.kernel_iters)
                for which, name in enumerate(("eval_round", "merge_round", "resolve_round"))}
-    dom = max(kernels, key=lambda k: kernels[k][0])
+    # roofline kernel: the wide pass, the only kernel whose work scales with node evaluations (SURVEY §8d's
+    # 76 B per evaluation); merge and the single-wave FIFO resolver are latency-bound per round
+    dom = "eval_round"
     dom_ms, dom_bytes = kernels[dom]
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
 
