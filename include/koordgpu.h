@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define KG_ABI_VERSION 1
+#define KG_ABI_VERSION 2
 
 /* ---- resource slots (fixed order) ------------------------------------------------------- */
 enum {
@@ -60,6 +60,21 @@ enum {
  * extension.GetPodPriorityClassWithDefault (apis/extension/priority_utils.go:26-48). */
 enum { KG_PRIO_NONE = 0, KG_PRIO_PROD = 1, KG_PRIO_MID = 2, KG_PRIO_BATCH = 3, KG_PRIO_FREE = 4 };
 
+/* NodeNUMAResource vocabulary (apis/extension/numa_aware.go:89-144, apis/extension/qos.go:23-28) */
+enum { KG_QOS_NONE = 0, KG_QOS_LSE = 1, KG_QOS_LSR = 2, KG_QOS_LS = 3, KG_QOS_BE = 4, KG_QOS_SYSTEM = 5 };
+/* CPUBindPolicy: "" / Default / FullPCPUs / SpreadByPCPUs / ConstrainedBurst */
+enum { KG_BIND_NONE = 0, KG_BIND_DEFAULT = 1, KG_BIND_FULL_PCPUS = 2, KG_BIND_SPREAD_BY_PCPUS = 3,
+       KG_BIND_CONSTRAINED_BURST = 4 };
+/* NodeCPUBindPolicy label (or kubelet static policy with full-pcpus-only) */
+enum { KG_NODE_BIND_NONE = 0, KG_NODE_BIND_FULL_PCPUS_ONLY = 1, KG_NODE_BIND_SPREAD_BY_PCPUS = 2 };
+/* NUMATopologyPolicy (node label, else NodeResourceTopology) */
+enum { KG_NUMA_POLICY_NONE = 0, KG_NUMA_POLICY_BEST_EFFORT = 1, KG_NUMA_POLICY_RESTRICTED = 2,
+       KG_NUMA_POLICY_SINGLE_NUMA_NODE = 3 };
+/* ScoringStrategy type / NUMAAllocateStrategy */
+enum { KG_STRATEGY_LEAST_ALLOCATED = 0, KG_STRATEGY_MOST_ALLOCATED = 1 };
+#define KG_MAX_NUMA 4
+#define KG_MAX_CPUS 256
+
 /* status codes: 0 ok, <0 error class (framework.Error on the Go side) */
 enum {
   KG_OK = 0,
@@ -76,7 +91,8 @@ enum {
   KG_REJECT_FIT_CPU = 1 << 1,       /* NodeResourcesFit: Insufficient cpu              */
   KG_REJECT_FIT_MEMORY = 1 << 2,    /* NodeResourcesFit: Insufficient memory           */
   KG_REJECT_LOADAWARE = 1 << 3,     /* LoadAwareScheduling: usage exceed threshold     */
-  KG_REJECT_INVALID_NODE = 1 << 4   /* deleted / never-upserted slot                   */
+  KG_REJECT_INVALID_NODE = 1 << 4,  /* deleted / never-upserted slot                   */
+  KG_REJECT_NUMA = 1 << 5           /* NodeNUMAResource (topology, cpuset, NUMA admit) */
 };
 
 /* node flags */
@@ -110,6 +126,15 @@ typedef struct kg_config {
   int64_t la_score;                            /* LoadAwareScheduling at Score                        */
   int64_t weight_fit;
   int64_t weight_loadaware;
+  /* NodeNUMAResourceArgs (config/types.go; defaults v1beta2/defaults.go:101-137) + profile */
+  int64_t numa_filter;                         /* NodeNUMAResource at Filter                          */
+  int64_t numa_score;                          /* NodeNUMAResource at Score                           */
+  int64_t weight_numa;
+  int64_t numa_default_cpu_bind_policy;        /* KG_BIND_* (default FullPCPUs)                       */
+  int64_t numa_scoring_strategy;               /* ScoringStrategy.Type: KG_STRATEGY_*                 */
+  int64_t numa_scoring_weights[2];             /* ScoringStrategy.Resources: cpu, memory              */
+  int64_t numa_numa_scoring_strategy;          /* NUMAScoringStrategy.Type (also the default NUMA     */
+  int64_t numa_numa_scoring_weights[2];        /* allocate strategy, util.go:26-32)                   */
   /* engine tuning (0 = default) */
   int64_t batch_pods;                          /* pods resolved per device round (B, 1..64)           */
   int64_t pods_per_wave;                       /* pods one eval wave scores per round (1..B)          */
@@ -148,8 +173,31 @@ typedef struct kg_pod {
   int64_t nonzero_requests[2];                 /* schedutil.GetNonzeroRequests: cpu milli, memory     */
   int64_t priority_class;                      /* KG_PRIO_*                                           */
   int64_t flags;                               /* KG_POD_*                                            */
-  int64_t reserved[2];
+  int64_t qos;                                 /* extension.GetPodQoSClassRaw: KG_QOS_*               */
+  int64_t required_cpu_bind_policy;            /* ResourceSpec annotation: KG_BIND_*                  */
+  int64_t preferred_cpu_bind_policy;           /* ResourceSpec annotation: KG_BIND_*                  */
+  int64_t reserved[3];
 } kg_pod;
+
+/* NodeNUMAResource view of one node: TopologyOptions (topology_options.go:40-48, from the
+ * NodeResourceTopology) + the NodeAllocation built from already-bound pods (node_allocation.go:32-38).
+ * The CPU topology is described in buildCPUTopology numbering (socket-major, then NUMA node, core, thread:
+ * cpu = ((socket·nodes_per_socket + node)·cores_per_node + core)·cpus_per_core + thread) with ≤ 256 CPUs and
+ * ≤ 4 NUMA nodes; NUMA zone i of the NRT is NUMA node i. */
+typedef struct kg_node_numa {
+  int64_t has_topology;                        /* CPUTopology reported                                */
+  int64_t sockets, nodes_per_socket, cores_per_node, cpus_per_core;
+  int64_t numa_policy;                         /* KG_NUMA_POLICY_* (label over NRT policy, util.go:51-57) */
+  int64_t node_cpu_bind_policy;                /* KG_NODE_BIND_* (extension.GetNodeCPUBindPolicy)      */
+  int64_t numa_allocate_strategy;              /* node label KG_STRATEGY_*, -1 = plugin default       */
+  int64_t num_numa;                            /* NUMANodeResources zones (0 = none)                  */
+  int64_t numa_cpu[KG_MAX_NUMA];               /* zone allocatable cpu (milli)                        */
+  int64_t numa_mem[KG_MAX_NUMA];               /* zone allocatable memory (bytes)                     */
+  uint64_t reserved_cpus[KG_MAX_CPUS / 64];    /* TopologyOptions.ReservedCPUs                        */
+  uint64_t allocated_cpus[KG_MAX_CPUS / 64];   /* NodeAllocation.allocatedCPUs (maxRefCount 1)        */
+  int64_t numa_alloc_cpu[KG_MAX_NUMA];         /* NodeAllocation.allocatedResources: cpu (milli)      */
+  int64_t numa_alloc_mem[KG_MAX_NUMA];         /*                                   memory (bytes)    */
+} kg_node_numa;
 
 typedef struct kg_stats {
   int64_t pods_scheduled;                      /* pods with a node                                    */
@@ -230,7 +278,8 @@ int kg_debug_stamps(kg_engine* e, uint64_t* out);
 
 const char* kg_last_error(void);
 int kg_abi_version(void);
-/* sizeof of the ABI structs (0 kg_config, 1 kg_node, 2 kg_node_metric, 3 kg_pod, 4 kg_stats) for binding checks. */
+/* sizeof of the ABI structs (0 kg_config, 1 kg_node, 2 kg_node_metric, 3 kg_pod, 4 kg_stats, 5 kg_node_numa) for
+ * binding checks. */
 int64_t kg_abi_struct_size(int which);
 
 #ifdef __cplusplus

@@ -31,7 +31,14 @@ OK, E_INVALID, E_DEVICE, E_COLLECTIVE, E_NOMEM, E_UNSUPPORTED = 0, -1, -2, -3, -
 REJECT_FIT_PODS, REJECT_FIT_CPU, REJECT_FIT_MEMORY, REJECT_LOADAWARE, REJECT_INVALID_NODE = 1, 2, 4, 8, 16
 NODE_VALID, NODE_HAS_RAW_ALLOCATABLE, NODE_HAS_CUSTOM_THRESHOLDS = 1, 2, 4
 POD_DAEMONSET = 1
-ABI_VERSION = 1
+ABI_VERSION = 2
+MAX_NUMA, MAX_CPUS = 4, 256
+QOS = {"": 0, "LSE": 1, "LSR": 2, "LS": 3, "BE": 4, "SYSTEM": 5}
+BIND = {"": 0, "Default": 1, "FullPCPUs": 2, "SpreadByPCPUs": 3, "ConstrainedBurst": 4}
+NODE_BIND = {"": 0, "None": 0, "FullPCPUsOnly": 1, "SpreadByPCPUs": 2}
+NUMA_POLICY = {"": 0, "BestEffort": 1, "Restricted": 2, "SingleNUMANode": 3}
+STRATEGY = {"LeastAllocated": 0, "MostAllocated": 1}
+REJECT_NUMA = 32
 
 
 def _i64(name, n=None):
@@ -50,6 +57,9 @@ CONFIG_DTYPE = np.dtype([
     _i64("fit_resource_weights", RES_MAX),
     _i64("fit_filter"), _i64("fit_score"), _i64("la_filter"), _i64("la_score"),
     _i64("weight_fit"), _i64("weight_loadaware"),
+    _i64("numa_filter"), _i64("numa_score"), _i64("weight_numa"), _i64("numa_default_cpu_bind_policy"),
+    _i64("numa_scoring_strategy"), _i64("numa_scoring_weights", 2),
+    _i64("numa_numa_scoring_strategy"), _i64("numa_numa_scoring_weights", 2),
     _i64("batch_pods"), _i64("pods_per_wave"), _i64("device_id"),
     _i64("reserved", 8),
 ])
@@ -78,7 +88,16 @@ POD_DTYPE = np.dtype([
     _i64("nonzero_requests", 2),
     _i64("priority_class"),
     _i64("flags"),
-    _i64("reserved", 2),
+    _i64("qos"), _i64("required_cpu_bind_policy"), _i64("preferred_cpu_bind_policy"),
+    _i64("reserved", 3),
+])
+
+NODE_NUMA_DTYPE = np.dtype([
+    _i64("has_topology"), _i64("sockets"), _i64("nodes_per_socket"), _i64("cores_per_node"), _i64("cpus_per_core"),
+    _i64("numa_policy"), _i64("node_cpu_bind_policy"), _i64("numa_allocate_strategy"), _i64("num_numa"),
+    _i64("numa_cpu", MAX_NUMA), _i64("numa_mem", MAX_NUMA),
+    ("reserved_cpus", np.uint64, (MAX_CPUS // 64,)), ("allocated_cpus", np.uint64, (MAX_CPUS // 64,)),
+    _i64("numa_alloc_cpu", MAX_NUMA), _i64("numa_alloc_mem", MAX_NUMA),
 ])
 
 STATS_DTYPE = np.dtype([
@@ -86,7 +105,7 @@ STATS_DTYPE = np.dtype([
     ("seconds", np.float64), ("reserved", np.float64, (3,)),
 ])
 
-STRUCT_DTYPES = {0: CONFIG_DTYPE, 1: NODE_DTYPE, 2: METRIC_DTYPE, 3: POD_DTYPE, 4: STATS_DTYPE}
+STRUCT_DTYPES = {0: CONFIG_DTYPE, 1: NODE_DTYPE, 2: METRIC_DTYPE, 3: POD_DTYPE, 4: STATS_DTYPE, 5: NODE_NUMA_DTYPE}
 
 # Every symbol include/koordgpu.h declares (tests check the library exports all of them).
 EXPORTED_SYMBOLS = (

@@ -1333,6 +1333,7 @@ int64_t kg_abi_struct_size(int which) {
     case 2: return sizeof(kg_node_metric);
     case 3: return sizeof(kg_pod);
     case 4: return sizeof(kg_stats);
+    case 5: return sizeof(kg_node_numa);
   }
   return -1;
 }
@@ -1356,6 +1357,14 @@ void kg_config_default(kg_config* c) {
   c->fit_filter = c->fit_score = c->la_filter = c->la_score = 1;
   c->weight_fit = 1;
   c->weight_loadaware = 1;
+  // v1beta2.SetDefaults_NodeNUMAResourceArgs (defaults.go:101-137): FullPCPUs, LeastAllocated cpu:1 memory:1 for
+  // both the node and the NUMA scoring strategies; the plugin is off unless the profile enables it
+  c->weight_numa = 1;
+  c->numa_default_cpu_bind_policy = KG_BIND_FULL_PCPUS;
+  c->numa_scoring_strategy = KG_STRATEGY_LEAST_ALLOCATED;
+  c->numa_scoring_weights[0] = c->numa_scoring_weights[1] = 1;
+  c->numa_numa_scoring_strategy = KG_STRATEGY_LEAST_ALLOCATED;
+  c->numa_numa_scoring_weights[0] = c->numa_numa_scoring_weights[1] = 1;
   c->batch_pods = 32;
   c->pods_per_wave = 8;
   c->device_id = -1;

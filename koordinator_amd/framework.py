@@ -26,7 +26,7 @@ from .engine import Engine
 from .quantity import resource_value
 
 SUCCESS, UNSCHEDULABLE = "Success", "Unschedulable"
-NODE_RESOURCES_FIT, LOAD_AWARE = "NodeResourcesFit", "LoadAwareScheduling"
+NODE_RESOURCES_FIT, LOAD_AWARE, NODE_NUMA_RESOURCE = "NodeResourcesFit", "LoadAwareScheduling", "NodeNUMAResource"
 
 
 def _slots(d: dict | None, absent=0) -> np.ndarray:
@@ -53,6 +53,16 @@ class NodeResourcesFitArgs:
 
 
 @dataclass
+class NodeNUMAResourceArgs:
+    """pkg/scheduler/apis/config/types.go NodeNUMAResourceArgs; defaults v1beta2/defaults.go:101-137."""
+    default_cpu_bind_policy: str = "FullPCPUs"
+    scoring_strategy: str = "LeastAllocated"
+    scoring_resources: dict = field(default_factory=lambda: {"cpu": 1, "memory": 1})
+    numa_scoring_strategy: str = "LeastAllocated"
+    numa_scoring_resources: dict = field(default_factory=lambda: {"cpu": 1, "memory": 1})
+
+
+@dataclass
 class Profile:
     filter: tuple = (NODE_RESOURCES_FIT, LOAD_AWARE)
     score: dict = field(default_factory=lambda: {NODE_RESOURCES_FIT: 1, LOAD_AWARE: 1})
@@ -60,10 +70,11 @@ class Profile:
 
 def build_config(la: LoadAwareSchedulingArgs | None = None, fit: NodeResourcesFitArgs | None = None,
                  profile: Profile | None = None, batch_pods: int = 32, pods_per_wave: int = 8,
-                 device_id: int = -1) -> np.ndarray:
+                 device_id: int = -1, numa: NodeNUMAResourceArgs | None = None) -> np.ndarray:
     la = la or LoadAwareSchedulingArgs()
     fit = fit or NodeResourcesFitArgs()
     profile = profile or Profile()
+    numa = numa or NodeNUMAResourceArgs()
     c = np.zeros(1, dtype=abi.CONFIG_DTYPE)
     r = c[0]
     r["abi_version"] = abi.ABI_VERSION
@@ -84,6 +95,15 @@ def build_config(la: LoadAwareSchedulingArgs | None = None, fit: NodeResourcesFi
     r["batch_pods"] = batch_pods
     r["pods_per_wave"] = pods_per_wave
     r["device_id"] = device_id
+    r["numa_filter"] = int(NODE_NUMA_RESOURCE in profile.filter)
+    r["numa_score"] = int(NODE_NUMA_RESOURCE in profile.score)
+    r["weight_numa"] = int(profile.score.get(NODE_NUMA_RESOURCE, 0))
+    r["numa_default_cpu_bind_policy"] = abi.BIND[numa.default_cpu_bind_policy]
+    r["numa_scoring_strategy"] = abi.STRATEGY[numa.scoring_strategy]
+    r["numa_scoring_weights"] = [numa.scoring_resources.get("cpu", 0), numa.scoring_resources.get("memory", 0)]
+    r["numa_numa_scoring_strategy"] = abi.STRATEGY[numa.numa_scoring_strategy]
+    r["numa_numa_scoring_weights"] = [numa.numa_scoring_resources.get("cpu", 0),
+                                      numa.numa_scoring_resources.get("memory", 0)]
     return c
 
 
@@ -137,9 +157,52 @@ def make_node_metric(present: bool = True, update_time_ns: int | None = 0, node_
     return m
 
 
+def make_node_numa(sockets: int = 0, nodes_per_socket: int = 1, cores_per_node: int = 0, cpus_per_core: int = 2,
+                   numa_policy: str = "", node_cpu_bind_policy: str = "", numa_allocate_strategy: str | None = None,
+                   numa_resources: list | None = None, reserved_cpus=(), allocated_cpus=(),
+                   numa_allocated: dict | None = None) -> np.ndarray:
+    """NodeNUMAResource view of a node: the NodeResourceTopology's CPU topology (buildCPUTopology numbering),
+    policies and zones, and the NodeAllocation of already-bound pods. numa_resources = [{"cpu": .., "memory": ..}]
+    per NUMA zone; numa_allocated = {zone: {"cpu": .., "memory": ..}}."""
+    n = np.zeros(1, dtype=abi.NODE_NUMA_DTYPE)
+    r = n[0]
+    r["has_topology"] = int(sockets > 0)
+    r["sockets"], r["nodes_per_socket"], r["cores_per_node"], r["cpus_per_core"] = (
+        sockets, nodes_per_socket, cores_per_node, cpus_per_core)
+    r["numa_policy"] = abi.NUMA_POLICY[numa_policy]
+    r["node_cpu_bind_policy"] = abi.NODE_BIND[node_cpu_bind_policy]
+    r["numa_allocate_strategy"] = -1 if numa_allocate_strategy is None else abi.STRATEGY[numa_allocate_strategy]
+    zones = numa_resources or []
+    r["num_numa"] = len(zones)
+    for i, z in enumerate(zones):
+        r["numa_cpu"][i] = resource_value("cpu", z.get("cpu", 0))
+        r["numa_mem"][i] = resource_value("memory", z.get("memory", 0))
+    for name, cpus in (("reserved_cpus", reserved_cpus), ("allocated_cpus", allocated_cpus)):
+        w = np.zeros(abi.MAX_CPUS // 64, dtype=np.uint64)
+        for c in cpus:
+            w[c // 64] |= np.uint64(1) << np.uint64(c % 64)
+        r[name] = w
+    for i, res in (numa_allocated or {}).items():
+        r["numa_alloc_cpu"][i] = resource_value("cpu", res.get("cpu", 0))
+        r["numa_alloc_mem"][i] = resource_value("memory", res.get("memory", 0))
+    return n
+
+
+def cpuset_of(words) -> list:
+    """The cpu ids of a 256-bit mask (uint64[4])."""
+    out = []
+    for w, v in enumerate(np.asarray(words, dtype=np.uint64).tolist()):
+        for b in range(64):
+            if (v >> b) & 1:
+                out.append(64 * w + b)
+    return out
+
+
 def make_pod(requests: dict | None = None, limits: dict | None = None, priority_class: str = "",
-             daemonset: bool = False, nonzero: tuple | None = None) -> np.ndarray:
-    """One single-container pod. nonzero = schedutil.GetNonzeroRequests (100m / 200MiB defaults)."""
+             daemonset: bool = False, nonzero: tuple | None = None, qos: str = "",
+             required_cpu_bind_policy: str = "", preferred_cpu_bind_policy: str = "") -> np.ndarray:
+    """One single-container pod. nonzero = schedutil.GetNonzeroRequests (100m / 200MiB defaults); qos = the
+    koordinator.sh/qosClass label; *_cpu_bind_policy = the scheduling.koordinator.sh/resource-spec annotation."""
     p = np.zeros(1, dtype=abi.POD_DTYPE)
     r = p[0]
     req = _values(requests)
@@ -150,6 +213,9 @@ def make_pod(requests: dict | None = None, limits: dict | None = None, priority_
     r["nonzero_requests"] = nonzero
     r["priority_class"] = abi.PRIORITY_CLASSES[priority_class]
     r["flags"] = abi.POD_DAEMONSET if daemonset else 0
+    r["qos"] = abi.QOS[qos]
+    r["required_cpu_bind_policy"] = abi.BIND[required_cpu_bind_policy]
+    r["preferred_cpu_bind_policy"] = abi.BIND[preferred_cpu_bind_policy]
     return p
 
 

@@ -1,0 +1,81 @@
+/*
+ * numa.h — CPU restatement of koord-scheduler's NodeNUMAResource plugin (TEST INFRASTRUCTURE ONLY, like
+ * oracle.h).  Implementation and reference citations: numa.c.
+ */
+#ifndef KG_ORACLE_NUMA_H_
+#define KG_ORACLE_NUMA_H_
+
+#include <stdint.h>
+
+#include "../include/koordgpu.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OR_CPUSET_WORDS (KG_MAX_CPUS / 64)
+
+typedef struct {
+  uint64_t w[OR_CPUSET_WORDS];
+} or_cpuset;
+
+/* CPUTopology in buildCPUTopologyForTest numbering (cpu_accumulator_test.go:30-57) */
+typedef struct {
+  int num_sockets, num_nodes, num_cores, num_cpus;
+  int cpus_per_core, cores_per_node, nodes_per_socket;
+  or_cpuset all;
+} or_topology;
+
+/* One node's NodeNUMAResource state: TopologyOptions + NodeAllocation (maxRefCount 1). */
+typedef struct {
+  int has_topology, valid_topology;
+  or_topology topo;
+  int numa_policy, node_cpu_bind_policy, numa_allocate_strategy;
+  int num_numa;
+  int64_t numa_cpu[KG_MAX_NUMA], numa_mem[KG_MAX_NUMA];
+  or_cpuset reserved;
+  /* mutable */
+  or_cpuset allocated;
+  int64_t numa_alloc_cpu[KG_MAX_NUMA], numa_alloc_mem[KG_MAX_NUMA];
+  int numa_alloc_present[KG_MAX_NUMA]; /* allocatedResources[numa] exists */
+} or_numa_node;
+
+/* NodeNUMAResource preFilterState (plugin.go:177-186, PreFilter :220-270) */
+typedef struct {
+  int skip, prefilter_error;
+  int request_cpu_bind;
+  int required_policy, preferred_policy; /* KG_BIND_* */
+  int num_cpus_needed;
+  int64_t req_cpu, req_mem; /* PodRequestsAndLimits cpu (milli) / memory */
+} or_numa_pod;
+
+/* the affinity the topology manager stores for a node (store.SetAffinity, manager.go:73) */
+typedef struct {
+  int nil;       /* NUMANodeAffinity == nil */
+  uint32_t mask;
+  int preferred;
+  int64_t score;
+} or_hint;
+
+void or_topology_build(or_topology* t, int sockets, int nodes_per_socket, int cores_per_node, int cpus_per_core);
+int or_take_cpus(const or_topology* t, or_cpuset available, int needed, int bind_policy, int strategy,
+                 or_cpuset* out);
+or_cpuset or_filter_required(const or_topology* t, or_cpuset available, int policy);
+
+void or_numa_node_init(or_numa_node* n, const kg_node_numa* src);
+void or_numa_pod_init(const kg_config* cfg, const kg_pod* pod, or_numa_pod* out);
+
+/* Filter (plugin.go:276-334).  Returns 1 when the node passes; writes the stored affinity. */
+int or_numa_filter(const kg_config* cfg, const or_numa_node* n, const or_numa_pod* p, or_hint* affinity);
+/* Score (scoring.go:55-120) with the affinity Filter stored; req/alloc = NodeInfo.Requested/Allocatable. */
+int64_t or_numa_score(const kg_config* cfg, const or_numa_node* n, const or_numa_pod* p, const or_hint* affinity,
+                      int64_t node_req_cpu, int64_t node_req_mem, int64_t node_alloc_cpu, int64_t node_alloc_mem);
+/* Reserve (plugin.go:375-415): Allocate with the stored affinity, then Update.  Returns 0 (and the cpuset in
+ * *cpus) or -1 when the allocation fails (the pod is not placed). */
+int or_numa_reserve(const kg_config* cfg, or_numa_node* n, const or_numa_pod* p, const or_hint* affinity,
+                    or_cpuset* cpus);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

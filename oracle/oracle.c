@@ -7,6 +7,7 @@
  */
 #define _GNU_SOURCE
 #include "oracle.h"
+#include "numa.h"
 
 #include <math.h>
 #include <pthread.h>
@@ -254,6 +255,9 @@ typedef struct sched_ctx {
   or_node_state* st;
   int64_t now;
   const kg_pod* pod;
+  or_numa_node* numa;     /* per node NodeNUMAResource state (NULL: plugin not in the profile) */
+  or_numa_pod numa_pod;   /* the pod's NodeNUMAResource preFilterState                          */
+  or_hint* affinity;      /* per node: the topology manager's stored affinity (Filter → Score/Reserve) */
   int32_t* feasible;      /* per node: 1 feasible, 0 not, -1 unsupported */
   int64_t* total;         /* weighted score per node                     */
   int64_t chunk;
@@ -275,6 +279,8 @@ static void eval_filter(sched_ctx* c, int64_t i) {
     if (s < 0) { c->feasible[i] = -1; return; }
     if (s != 0) ok = 0;
   }
+  if (c->numa) c->affinity[i] = (or_hint){1, 0, 0, 0};
+  if (ok && cfg->numa_filter && c->numa && !or_numa_filter(cfg, &c->numa[i], &c->numa_pod, &c->affinity[i])) ok = 0;
   c->feasible[i] = ok;
 }
 
@@ -288,6 +294,10 @@ static void eval_score(sched_ctx* c, int64_t i) {
     if (s < 0) { c->feasible[i] = -1; return; }
     t += cfg->weight_loadaware * s;
   }
+  if (cfg->numa_score && c->numa)
+    t += cfg->weight_numa * or_numa_score(cfg, &c->numa[i], &c->numa_pod, &c->affinity[i], c->st[i].requested[KG_RES_CPU],
+                                          c->st[i].requested[KG_RES_MEMORY], c->nodes[i].allocatable[KG_RES_CPU],
+                                          c->nodes[i].allocatable[KG_RES_MEMORY]);
   c->total[i] = t;
 }
 
@@ -340,9 +350,19 @@ static void run_phase(sched_ctx* c, int phase) {
 int or_schedule(const kg_config* cfg, int64_t n_nodes, const kg_node* nodes, const kg_node_metric* metrics,
                 or_node_state* st, int64_t n_pods, const kg_pod* pods, int64_t now, int n_threads,
                 int32_t* out_node, int64_t* out_score) {
+  return or_schedule_numa(cfg, n_nodes, nodes, metrics, st, NULL, n_pods, pods, now, n_threads, out_node, out_score);
+}
+
+int or_schedule_numa(const kg_config* cfg, int64_t n_nodes, const kg_node* nodes, const kg_node_metric* metrics,
+                     or_node_state* st, void* numa_states, int64_t n_pods, const kg_pod* pods, int64_t now,
+                     int n_threads, int32_t* out_node, int64_t* out_score) {
+  or_numa_node* numa = (or_numa_node*)numa_states;
   sched_ctx c;
   memset(&c, 0, sizeof(c));
   c.cfg = cfg; c.n_nodes = n_nodes; c.nodes = nodes; c.metrics = metrics; c.st = st; c.now = now;
+  const int numa_on = numa && (cfg->numa_filter || cfg->numa_score);
+  c.numa = numa_on ? numa : NULL;
+  c.affinity = numa_on ? (or_hint*)calloc((size_t)(n_nodes > 0 ? n_nodes : 1), sizeof(or_hint)) : NULL;
   c.feasible = (int32_t*)malloc(sizeof(int32_t) * (size_t)(n_nodes > 0 ? n_nodes : 1));
   c.total = (int64_t*)malloc(sizeof(int64_t) * (size_t)(n_nodes > 0 ? n_nodes : 1));
   if (!c.feasible || !c.total) { free(c.feasible); free(c.total); return KG_E_NOMEM; }
@@ -361,6 +381,7 @@ int or_schedule(const kg_config* cfg, int64_t n_nodes, const kg_node* nodes, con
   int rc = 0;
   for (int64_t p = 0; p < n_pods && rc == 0; p++) {
     c.pod = &pods[p];
+    if (c.numa) or_numa_pod_init(cfg, c.pod, &c.numa_pod);
     run_phase(&c, 0);
     run_phase(&c, 1);
     /* selectHost: max total, ties → lowest snapshot index (BASELINE determinism pin) */
@@ -370,6 +391,12 @@ int or_schedule(const kg_config* cfg, int64_t n_nodes, const kg_node* nodes, con
       if (c.feasible[i] == 1 && (best < 0 || c.total[i] > best_score)) { best = i; best_score = c.total[i]; }
     }
     if (rc) break;
+    /* Reserve: NodeNUMAResource allocates the cpuset / NUMA resources; a failure un-assumes the pod
+     * (RunReservePluginsUnreserve + ForgetPod): it is not placed this cycle */
+    if (best >= 0 && c.numa) {
+      or_cpuset cpus;
+      if (or_numa_reserve(cfg, &c.numa[best], &c.numa_pod, &c.affinity[best], &cpus) != 0) best = -1;
+    }
     out_node[p] = (int32_t)best;
     out_score[p] = best >= 0 ? best_score : 0;
     if (best >= 0) or_apply_pod(cfg, &st[best], &pods[p], +1); /* assume + Reserve */
@@ -382,6 +409,7 @@ int or_schedule(const kg_config* cfg, int64_t n_nodes, const kg_node* nodes, con
   }
   free(c.feasible);
   free(c.total);
+  free(c.affinity);
   return rc;
 }
 

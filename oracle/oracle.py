@@ -59,6 +59,17 @@ def lib():
         L.or_schedule.restype = i
         L.or_node_keys.argtypes = [vp, vp, vp, vp, vp, i64, i64, i64, vp]
         L.or_node_keys.restype = i
+        L.or_schedule_numa.argtypes = [vp, i64, vp, vp, vp, vp, i64, vp, i64, i, vp, vp]
+        L.or_schedule_numa.restype = i
+        L.or_numa_state_size.restype = i64
+        L.or_numa_states_init.argtypes = [vp, i64, vp]
+        L.or_numa_state_read.argtypes = [vp, i64, vp, vp, vp]
+        L.or_take_cpus_flat.argtypes = [i, i, i, i, vp, i, i, i, vp]
+        L.or_take_cpus_flat.restype = i
+        L.or_numa_eval_flat.argtypes = [vp, vp, vp, i64, i64, i64, i64, vp, vp]
+        L.or_numa_eval_flat.restype = i
+        L.or_numa_reserve_flat.argtypes = [vp, vp, vp, vp]
+        L.or_numa_reserve_flat.restype = i
         _lib = L
     return _lib
 
@@ -135,6 +146,66 @@ def apply_pod(cfg, st, pod, node: int, sign: int = 1):
     """assume (+1) / forget (-1) of one pod on node `node` of `st` (or_apply_pod)."""
     pod = np.ascontiguousarray(np.asarray(pod, dtype=abi.POD_DTYPE).reshape(1))
     lib().or_apply_pod(p(cfg), p(st[node:node + 1]), p(pod), sign)
+
+
+def numa_states(nodes_numa: np.ndarray) -> np.ndarray:
+    """Per-node NodeNUMAResource state (numa.c or_numa_node) from kg_node_numa rows."""
+    nodes_numa = np.ascontiguousarray(nodes_numa, dtype=abi.NODE_NUMA_DTYPE)
+    size = int(lib().or_numa_state_size())
+    buf = np.zeros(max(len(nodes_numa), 1) * size, dtype=np.uint8)
+    lib().or_numa_states_init(p(nodes_numa), len(nodes_numa), p(buf))
+    return buf
+
+
+def numa_state_read(buf: np.ndarray, n: int):
+    """(allocated cpu masks uint64[n,4], per-NUMA allocated cpu int64[n,4], memory int64[n,4])."""
+    alloc = np.zeros((n, abi.MAX_CPUS // 64), dtype=np.uint64)
+    cpu = np.zeros((n, abi.MAX_NUMA), dtype=np.int64)
+    mem = np.zeros((n, abi.MAX_NUMA), dtype=np.int64)
+    for i in range(n):
+        lib().or_numa_state_read(p(buf), i, p(alloc[i]), p(cpu[i]), p(mem[i]))
+    return alloc, cpu, mem
+
+
+def schedule_numa(cfg, nodes, metrics, st, numa_buf, pods, now_ns: int, n_threads: int = 1):
+    """or_schedule with the NodeNUMAResource plugin; mutates `st` and `numa_buf`."""
+    pods = np.ascontiguousarray(pods, dtype=abi.POD_DTYPE)
+    out_node = np.empty(len(pods), dtype=np.int32)
+    out_score = np.empty(len(pods), dtype=np.int64)
+    rc = lib().or_schedule_numa(p(cfg), len(nodes), p(nodes), p(metrics), p(st), p(numa_buf), len(pods), p(pods),
+                                now_ns, n_threads, p(out_node), p(out_score))
+    if rc != 0:
+        raise RuntimeError(f"oracle or_schedule_numa failed: {rc}")
+    return out_node, out_score
+
+
+def take_cpus(topology, available, needed: int, bind_policy: str, strategy: str):
+    """takeCPUs on buildCPUTopologyForTest(*topology); returns the cpu list or None on error."""
+    words = np.zeros(abi.MAX_CPUS // 64, dtype=np.uint64)
+    for c in available:
+        words[c // 64] |= np.uint64(1) << np.uint64(c % 64)
+    out = np.zeros(abi.MAX_CPUS // 64, dtype=np.uint64)
+    rc = lib().or_take_cpus_flat(*topology, p(words), needed, abi.BIND[bind_policy], abi.STRATEGY[strategy], p(out))
+    if rc != 0:
+        return None
+    return [64 * w + b for w in range(len(out)) for b in range(64) if (int(out[w]) >> b) & 1]
+
+
+def numa_eval(cfg, node_numa, pod, node_requested=(0, 0), node_allocatable=(0, 0)):
+    """(passes Filter, Score, stored affinity mask or -1 for nil) of one pod on one node."""
+    score = np.zeros(1, dtype=np.int64)
+    mask = np.zeros(1, dtype=np.int64)
+    ok = lib().or_numa_eval_flat(p(cfg), p(np.ascontiguousarray(node_numa)), p(np.ascontiguousarray(pod)),
+                                 int(node_requested[0]), int(node_requested[1]), int(node_allocatable[0]),
+                                 int(node_allocatable[1]), p(score), p(mask))
+    return bool(ok), int(score[0]), int(mask[0])
+
+
+def numa_reserve(cfg, node_numa, pod):
+    """Reserve of one pod on one node: (0 / -1, chosen cpu list)."""
+    out = np.zeros(abi.MAX_CPUS // 64, dtype=np.uint64)
+    rc = lib().or_numa_reserve_flat(p(cfg), p(np.ascontiguousarray(node_numa)), p(np.ascontiguousarray(pod)), p(out))
+    return rc, [64 * w + b for w in range(len(out)) for b in range(64) if (int(out[w]) >> b) & 1]
 
 
 def schedule_cluster(cfg, cluster, pods, n_threads: int = 1):
