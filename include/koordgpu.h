@@ -254,6 +254,21 @@ int kg_nodes_read_state(kg_engine* e, int64_t* requested_cpu, int64_t* requested
                         int64_t* nonzero_mem, int64_t* num_pods, int64_t* la_est_cpu, int64_t* la_est_mem,
                         int64_t* la_est_prod_cpu, int64_t* la_est_prod_mem);
 
+/* NodeNUMAResource (engines whose profile enables it): the TopologyOptions + NodeAllocation of nodes idx[0..n)
+ * (replaces each node's NUMA state; node_allocation.go:32-38, topology_options.go:40-48 — fed by the NRT and
+ * pod informers, topology_eventhandler.go:62-113 / pod_eventhandler.go:94-136). */
+int kg_nodes_numa_upsert(kg_engine* e, const kg_node_numa* numa, const int32_t* idx, int64_t n);
+/* Reads the DEVICE NodeAllocation: allocated cpus (4 words per node), per-NUMA allocated cpu / memory
+ * (KG_MAX_NUMA per node). Any output may be NULL. */
+int kg_nodes_read_numa(kg_engine* e, uint64_t* allocated_cpus, int64_t* numa_alloc_cpu, int64_t* numa_alloc_mem);
+/* The cpuset NodeNUMAResource Reserve allocated to staged pods [first, first+count): 4 uint64 words per pod,
+ * empty for pods without a cpuset (the resource-status annotation PreBind writes, plugin.go:427-463). */
+int kg_results_fetch_cpusets(kg_engine* e, int64_t first, int64_t count, uint64_t* out_cpusets);
+/* NodeNUMAResource Filter + Score of one pod on every node slot, the plugin alone: out_pass 1/0, the plugin's
+ * unweighted score (0 where Filter rejects) and the affinity the topology manager stores (NUMA mask, -1 = nil). */
+int kg_pods_evaluate_numa(kg_engine* e, const kg_pod* pod, int32_t* out_pass, int64_t* out_score,
+                          int64_t* out_affinity);
+
 /* Measurement hooks (bench.py): replays one device round's kernel `which` (0 = eval, 1 = merge, 2 = resolve) `iters` times
  * on the engine stream between HIP events, restoring state, and returns the mean duration in ms plus the
  * algorithmic bytes that kernel must move per launch. Requires a staged queue. */

@@ -114,6 +114,7 @@ EXPORTED_SYMBOLS = (
     "kg_pods_stage", "kg_pods_schedule_staged", "kg_results_fetch", "kg_engine_num_nodes",
     "kg_nodes_read_state", "kg_bench_kernel", "kg_debug_least_requested", "kg_last_error", "kg_abi_version",
     "kg_abi_struct_size", "kg_nccl_unique_id", "kg_debug_eval_paths", "kg_debug_stamps", "kg_debug_fast_lrs",
+    "kg_nodes_numa_upsert", "kg_nodes_read_numa", "kg_results_fetch_cpusets", "kg_pods_evaluate_numa",
 )
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
@@ -165,6 +166,10 @@ def load_library(path: str | None = None):
         "kg_debug_eval_paths": (i, [vp, vp]),
         "kg_debug_stamps": (i, [vp, vp]),
         "kg_debug_fast_lrs": (i, [vp, vp, vp, vp, vp, i64]),
+        "kg_nodes_numa_upsert": (i, [vp, vp, vp, i64]),
+        "kg_nodes_read_numa": (i, [vp, vp, vp, vp]),
+        "kg_results_fetch_cpusets": (i, [vp, i64, i64, vp]),
+        "kg_pods_evaluate_numa": (i, [vp, vp, vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)

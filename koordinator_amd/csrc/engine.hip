@@ -26,6 +26,7 @@
 
 #include "../../include/koordgpu.h"
 #include "kernels.h"
+#include "numa_dev.h"
 
 using namespace kg;
 
@@ -764,6 +765,229 @@ __global__ __launch_bounds__(kWave) void resolve_round(DevTable T, const DevPod*
   KG_STAMP(2, 31);
 }
 
+// ---- NodeNUMAResource profiles (config C4) --------------------------------------------
+// NUMA state per node: static TopologyOptions (NumaStatic, 128 B) + NodeAllocation (NumaMut, 96 B), AoS so
+// one node's state is two contiguous lines.  The NUMA plugin is not monotone (Reserve moves cpus between
+// NUMA nodes and the hint search can raise a score), so these profiles run unpipelined rounds and the
+// resolver re-scores every modified row for every pod.
+struct NumaTable {
+  const NumaStatic* __restrict__ s;
+  NumaMut* __restrict__ m;
+};
+
+// Reference-shaped Fit + LoadAware (eval_node) + NodeNUMAResource Filter/Score of one node for one pod.
+__device__ __forceinline__ bool eval_node_numa(const Row& r, const NumaStatic& ns, const NumaMut& nm, const DevPod& p,
+                                               const NumaPod& np, const EvalParams& P, const NumaParams& NP,
+                                               int64_t& total) {
+  int64_t t = 0;
+  if (!eval_node(r, p, P, t)) return false;
+  int64_t sc = 0;
+  NumaHint aff;
+  if (!numa_eval(ns, nm, np, NP, r.req_cpu, r.req_mem, r.alloc_cpu, r.alloc_mem, sc, aff)) return false;
+  total = t + (NP.score ? sc * NP.weight : 0);
+  return true;
+}
+
+__global__ __launch_bounds__(kWave* kEvalWaves) void eval_round_numa(DevTable T, NumaTable NT,
+                                                                       const DevPod* __restrict__ pods,
+                                                                       const NumaPod* __restrict__ npods,
+                                                                       int64_t first, int nb, int pods_per_wave,
+                                                                       int64_t node_base, int64_t n_local,
+                                                                       int nt_local, EvalParams P, NumaParams NP,
+                                                                       uint64_t* __restrict__ lists,
+                                                                       const int32_t* __restrict__ poison) {
+  if (*poison) return;
+  const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
+  const int n_pg = (nb + pods_per_wave - 1) / pods_per_wave;
+  const uint32_t nwg = gridDim.x, bid = blockIdx.x, xcd = bid % 8u, q = nwg / 8u, r = nwg % 8u;
+  const uint32_t wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8u;
+  const int tile = (int)(wgid / (uint32_t)n_pg) * kEvalWaves + wave;
+  const int p0 = (int)(wgid % (uint32_t)n_pg) * pods_per_wave;
+  if (tile >= nt_local || p0 >= nb) return;
+  const int p1 = (p0 + pods_per_wave) < nb ? (p0 + pods_per_wave) : nb;
+  const int vbits = P.score_bits + 1;
+  uint32_t gidx[kNPT];
+#pragma unroll
+  for (int j = 0; j < kNPT; ++j) gidx[j] = (uint32_t)(node_base + (int64_t)tile * kTile + j * kWave + lane);
+  for (int pi = p0; pi < p1; ++pi) {
+    const DevPod p = pods[first + pi];
+    const NumaPod np = npods[first + pi];
+    uint32_t v[kNPT];
+#pragma unroll
+    for (int j = 0; j < kNPT; ++j) {
+      int64_t local = (int64_t)tile * kTile + j * kWave + lane;
+      asm volatile("" : "+v"(local));
+      v[j] = 0;
+      if (local < n_local) {
+        const int64_t i = node_base + local;
+        const NumaStatic ns = NT.s[i];
+        const NumaMut nm = NT.m[i];
+        int64_t t = 0;
+        if (eval_node_numa(load_row(T, i), ns, nm, p, np, P, NP, t)) v[j] = (uint32_t)t + 1u;
+      }
+    }
+    select_write(v, gidx, vbits, lists + ((size_t)pi * nt_local + tile) * kR, lane);
+  }
+}
+
+// Single-wave FIFO resolver of a NUMA round (unpipelined).  Lane l < nM owns modified node l: its Row in
+// registers, its NUMA state in LDS slot l.  Per pod: e = best unmodified candidate, mbest = exact re-score of
+// every modified row; best < ub ends the round early (as resolve_round).  The winner's owner lane runs
+// Reserve — the NUMA allocation with the exact cpuset (cpu accumulator); a failed Reserve leaves the pod
+// unplaced (RunReservePluginsUnreserve) and the node unchanged.
+constexpr int kNumaStaticWords = (int)(sizeof(NumaStatic) / 8), kNumaMutWords = (int)(sizeof(NumaMut) / 8);
+constexpr int kNumaPodWords = (int)(sizeof(NumaPod) / 8);
+
+__global__ __launch_bounds__(kWave) void resolve_round_numa(DevTable T, NumaTable NT, const DevPod* __restrict__ pods,
+                                                             const NumaPod* __restrict__ npods,
+                                                             int64_t* __restrict__ ctl, int64_t first, int nb,
+                                                             const uint64_t* __restrict__ cand, EvalParams P,
+                                                             NumaParams NP, uint64_t* __restrict__ out_keys,
+                                                             uint64_t* __restrict__ out_cpus, int bitmap_words,
+                                                             int32_t* __restrict__ poison, int64_t seq) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
+  const int lane = threadIdx.x;
+  uint64_t* s_cand = smem;                                    // [nb][kCandStride]
+  uint64_t* s_podw = s_cand + (size_t)nb * kCandStride;       // [nb] DevPod
+  uint64_t* s_npw = s_podw + (size_t)nb * kPodWords;          // [nb] NumaPod
+  uint64_t* s_nsw = s_npw + (size_t)nb * kNumaPodWords;       // [kWave] NumaStatic of the modified rows
+  uint64_t* s_nmw = s_nsw + (size_t)kWave * kNumaStaticWords; // [kWave] NumaMut of the modified rows
+  uint32_t* bitmap = reinterpret_cast<uint32_t*>(s_nmw + (size_t)kWave * kNumaMutWords);
+  for (int w = lane; w < nb * kCandStride; w += kWave) s_cand[w] = cand[w];
+  {
+    const uint64_t* pw = reinterpret_cast<const uint64_t*>(pods + first);
+    for (int w = lane; w < nb * kPodWords; w += kWave) s_podw[w] = pw[w];
+    const uint64_t* nw = reinterpret_cast<const uint64_t*>(npods + first);
+    for (int w = lane; w < nb * kNumaPodWords; w += kWave) s_npw[w] = nw[w];
+  }
+  for (int w = lane; w < bitmap_words; w += kWave) bitmap[w] = 0;
+  __syncthreads();
+  if (*poison || ctl[0] != first) {
+    publish_round(ctl, seq);
+    return;
+  }
+  const DevPod* s_pods = reinterpret_cast<const DevPod*>(s_podw);
+  const NumaPod* s_np = reinterpret_cast<const NumaPod*>(s_npw);
+  NumaStatic* s_ns = reinterpret_cast<NumaStatic*>(s_nsw);
+  NumaMut* s_nm = reinterpret_cast<NumaMut*>(s_nmw);
+  uint32_t midx = 0xFFFFFFFFu;
+  Row mrow;
+  mrow.flags = 0;
+  bool touched = false;
+  uint64_t my_out = 0;
+  int nM = 0, consumed = 0;
+  for (int j = 0; j < nb; ++j) {
+    const uint64_t key = s_cand[(size_t)j * kCandStride + lane];
+    const uint64_t ub = s_cand[(size_t)j * kCandStride + kC];
+    const DevPod p = s_pods[j];
+    const NumaPod np = s_np[j];
+    const uint32_t node = key_node(key);
+    const bool unmod = (key != 0) && !((bitmap[node >> 5] >> (node & 31)) & 1u);
+    const uint64_t um = __ballot(unmod);
+    const int pos = um ? (int)__builtin_ctzll(um) : kC;
+    uint64_t best = um ? readlane_u64(key, pos) : 0;
+    if (nM > 0) {
+      uint64_t mk = 0;
+      if (lane < nM) {
+        int64_t t = 0;
+        if (eval_node_numa(mrow, s_ns[lane], s_nm[lane], p, np, P, NP, t)) mk = make_key(t, midx);
+      }
+      const uint64_t mbest = wave_max_key(mk);
+      best = mbest > best ? mbest : best;
+    }
+    if (best < ub) break;
+    ++consumed;
+    if (best == 0) {
+      my_out = lane == j ? 0 : my_out;
+      continue;
+    }
+    const uint32_t w = key_node(best);
+    const uint64_t hit = __ballot((lane < nM) & (midx == w));
+    const int owner = hit ? (int)__builtin_ctzll(hit) : nM;
+    if (!hit) {
+      if (lane == owner) {
+        midx = w;
+        mrow = load_row(T, w);
+        s_ns[owner] = NT.s[w];
+        s_nm[owner] = NT.m[w];
+      }
+      if (lane == 0) bitmap[w >> 5] |= 1u << (w & 31);
+      ++nM;
+    }
+    __syncthreads();
+    int placed = 0;
+    if (lane == owner) {  // Reserve with the affinity Filter stores (recomputed on the same state)
+      const Topo tp = make_topo(s_ns[lane]);
+      NumaHint aff{0, 1, 0, 0};
+      if (NP.filter) (void)numa_filter(tp, s_ns[lane], s_nm[lane], np, NP, aff);
+      CpuSet cpus;
+      NumaMut nm = s_nm[lane];
+      if (numa_reserve(tp, s_ns[lane], nm, np, NP, aff, cpus)) {
+        placed = 1;
+        s_nm[lane] = nm;
+        mrow.req_cpu += p.req_cpu;  // assume: NodeInfo.AddPod + LoadAware assign cache
+        mrow.req_mem += p.req_mem;
+        mrow.nz_cpu += p.nz_cpu;
+        mrow.nz_mem += p.nz_mem;
+        mrow.la_used_cpu += p.est_cpu;
+        mrow.la_used_mem += p.est_mem;
+        if (p.flags & P_PROD) {
+          mrow.la_pused_cpu += p.est_cpu;
+          mrow.la_pused_mem += p.est_mem;
+        }
+        mrow.num_pods += 1;
+        touched = true;
+#pragma unroll
+        for (int q = 0; q < kCpuWords; ++q) out_cpus[(size_t)(first + j) * kCpuWords + q] = cpus.w[q];
+      }
+    }
+    placed = __builtin_amdgcn_readlane(placed, owner);
+    my_out = lane == j ? (placed ? best : 0) : my_out;
+    __syncthreads();
+  }
+  if (touched) {
+    store_mutable(T, midx, mrow);
+    NT.m[midx] = s_nm[lane];
+  }
+  if (lane < consumed) out_keys[first + lane] = my_out;
+  if (lane == 0) {
+    ctl[0] = first + consumed;
+    ctl[1] += 1;
+    ctl[2] += consumed;
+    if (consumed < nb) *poison = 1;
+  }
+  publish_round(ctl, seq);
+}
+
+// kg_pods_evaluate_numa: NodeNUMAResource Filter + Score of one pod on every node (the plugin alone)
+__global__ void evaluate_pod_numa(DevTable T, NumaTable NT, const DevPod* __restrict__ pod,
+                                  const NumaPod* __restrict__ npod, int64_t n, NumaParams NP,
+                                  int32_t* __restrict__ pass, int64_t* __restrict__ score,
+                                  int64_t* __restrict__ affinity) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const Row r = load_row(T, i);
+  NumaParams q = NP;
+  q.filter = 1;
+  q.score = 1;
+  int64_t sc = 0;
+  NumaHint aff;
+  const bool ok = numa_eval(NT.s[i], NT.m[i], *npod, q, r.req_cpu, r.req_mem, r.alloc_cpu, r.alloc_mem, sc, aff);
+  pass[i] = ok ? 1 : 0;
+  score[i] = ok ? sc : 0;
+  affinity[i] = aff.nil ? -1 : (int64_t)aff.mask;
+}
+
+// Scatter of upserted NUMA rows (static + NodeAllocation)
+__global__ void scatter_numa(NumaTable NT, const NumaStatic* __restrict__ s, const NumaMut* __restrict__ m,
+                             const int32_t* __restrict__ idx, int64_t n) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const int64_t i = idx[k];
+  const_cast<NumaStatic*>(NT.s)[i] = s[k];
+  NT.m[i] = m[k];
+}
+
 // kg_pods_evaluate: one pod, every node, per-plugin outputs.
 __global__ void evaluate_pod(DevTable T, const DevPod* __restrict__ pod, int64_t n, EvalParams P,
                              int32_t* __restrict__ reject, int64_t* __restrict__ fit, int64_t* __restrict__ la) {
@@ -942,6 +1166,13 @@ struct kg_engine {
   std::vector<int64_t> h_static64;
   std::vector<int32_t> h_static32;
   std::vector<double> h_static_f64;
+  // NodeNUMAResource (profile enables it): per-node state, per-pod preFilterState, Reserve's cpusets
+  bool numa_on = false;
+  NumaParams NP{};
+  DevBuf<NumaStatic> numa_s;
+  DevBuf<NumaMut> numa_m;
+  DevBuf<NumaPod> npods;
+  DevBuf<uint64_t> out_cpus;  // [staged + kMaxB][4]
 };
 
 namespace {
@@ -964,6 +1195,19 @@ int validate_config(const kg_config* c) {
   if (c->weight_fit < 0 || c->weight_fit > 1000000 || c->weight_loadaware < 0 || c->weight_loadaware > 1000000)
     return fail(KG_E_INVALID, "plugin weight out of range");
   if (c->batch_pods < 0 || c->batch_pods > kMaxB) return fail(KG_E_INVALID, "batch_pods must be in [1,%d]", kMaxB);
+  if (c->numa_filter || c->numa_score) {
+    if (c->weight_numa < 0 || c->weight_numa > 1000000) return fail(KG_E_INVALID, "NodeNUMAResource weight out of range");
+    if ((c->numa_scoring_strategy != KG_STRATEGY_LEAST_ALLOCATED && c->numa_scoring_strategy != KG_STRATEGY_MOST_ALLOCATED) ||
+        (c->numa_numa_scoring_strategy != KG_STRATEGY_LEAST_ALLOCATED &&
+         c->numa_numa_scoring_strategy != KG_STRATEGY_MOST_ALLOCATED))
+      return fail(KG_E_UNSUPPORTED, "NodeNUMAResource scoring strategy: LeastAllocated / MostAllocated");
+    for (int r = 0; r < 2; ++r)
+      if (c->numa_scoring_weights[r] < 0 || c->numa_scoring_weights[r] > 1000000 || c->numa_numa_scoring_weights[r] < 0 ||
+          c->numa_numa_scoring_weights[r] > 1000000)
+        return fail(KG_E_INVALID, "NodeNUMAResource scoring weight out of range");
+    if (c->numa_default_cpu_bind_policy < KG_BIND_NONE || c->numa_default_cpu_bind_policy > KG_BIND_CONSTRAINED_BURST)
+      return fail(KG_E_INVALID, "DefaultCPUBindPolicy");
+  }
   return 0;
 }
 
@@ -1095,6 +1339,84 @@ int decode_pod(const kg_engine* e, const kg_pod& p, DevPod& d) {
   return 0;
 }
 
+// NodeNUMAResource preFilterState (plugin.go:220-270; AllowUseCPUSet util.go:42-49)
+int decode_numa_pod(const kg_config& c, const kg_pod& p, NumaPod& d) {
+  std::memset(&d, 0, sizeof(d));
+  if (p.qos < KG_QOS_NONE || p.qos > KG_QOS_SYSTEM) return fail(KG_E_INVALID, "pod qos");
+  if (p.required_cpu_bind_policy < KG_BIND_NONE || p.required_cpu_bind_policy > KG_BIND_CONSTRAINED_BURST ||
+      p.preferred_cpu_bind_policy < KG_BIND_NONE || p.preferred_cpu_bind_policy > KG_BIND_CONSTRAINED_BURST)
+    return fail(KG_E_INVALID, "pod cpu bind policy");
+  d.req_cpu = p.requests[KG_RES_CPU];
+  d.req_mem = p.requests[KG_RES_MEMORY];
+  bool zero = true;
+  for (int r = 0; r < KG_RES_MAX; ++r) zero &= p.requests[r] == 0;
+  if (zero) {
+    d.skip = 1;
+    return 0;
+  }
+  if (!((p.qos == KG_QOS_LSE || p.qos == KG_QOS_LSR) && p.priority_class == KG_PRIO_PROD)) return 0;
+  int bind = (int)p.preferred_cpu_bind_policy;
+  if (bind == KG_BIND_NONE || bind == KG_BIND_DEFAULT) bind = (int)c.numa_default_cpu_bind_policy;
+  int required = (int)p.required_cpu_bind_policy;
+  if (required == KG_BIND_DEFAULT) required = (int)c.numa_default_cpu_bind_policy;
+  if (required != KG_BIND_NONE) bind = required;
+  if (bind == KG_BIND_FULL_PCPUS || bind == KG_BIND_SPREAD_BY_PCPUS) {
+    if (d.req_cpu % 1000 != 0) {  // "the requested CPUs must be integer": every node rejects
+      d.prefilter_error = 1;
+      return 0;
+    }
+    if (d.req_cpu > 0) {
+      d.cpu_bind = 1;
+      d.required = required;
+      d.preferred = bind;
+      d.needed = (int32_t)std::min<int64_t>(d.req_cpu / 1000, 1 << 20);
+    }
+  }
+  return 0;
+}
+
+// TopologyOptions + NodeAllocation of one node → device rows
+int decode_node_numa(const kg_node_numa& n, NumaStatic& s, NumaMut& m) {
+  std::memset(&s, 0, sizeof(s));
+  std::memset(&m, 0, sizeof(m));
+  if (n.num_numa < 0 || n.num_numa > KG_MAX_NUMA) return fail(KG_E_UNSUPPORTED, "num_numa %lld > %d", (long long)n.num_numa, KG_MAX_NUMA);
+  if (n.numa_policy < KG_NUMA_POLICY_NONE || n.numa_policy > KG_NUMA_POLICY_SINGLE_NUMA_NODE) return fail(KG_E_INVALID, "numa_policy");
+  if (n.node_cpu_bind_policy < KG_NODE_BIND_NONE || n.node_cpu_bind_policy > KG_NODE_BIND_SPREAD_BY_PCPUS)
+    return fail(KG_E_INVALID, "node_cpu_bind_policy");
+  if (n.numa_allocate_strategy < -1 || n.numa_allocate_strategy > KG_STRATEGY_MOST_ALLOCATED)
+    return fail(KG_E_INVALID, "numa_allocate_strategy");
+  if (n.has_topology) {
+    if (n.sockets < 0 || n.nodes_per_socket < 0 || n.cores_per_node < 0 || n.cpus_per_core < 0)
+      return fail(KG_E_INVALID, "negative topology");
+    const int64_t cpus = n.sockets * n.nodes_per_socket * n.cores_per_node * n.cpus_per_core;
+    if (cpus > KG_MAX_CPUS || n.sockets > 8 || n.sockets * n.nodes_per_socket > 8)
+      return fail(KG_E_UNSUPPORTED, "cpu topology beyond %d cpus / 8 NUMA nodes", KG_MAX_CPUS);
+    if (n.cpus_per_core > 2) return fail(KG_E_UNSUPPORTED, "cpus_per_core %lld > 2", (long long)n.cpus_per_core);
+    s.sockets = (int32_t)n.sockets;
+    s.nps = (int32_t)n.nodes_per_socket;
+    s.cpn = (int32_t)n.cores_per_node;
+    s.cpc = (int32_t)n.cpus_per_core;
+    s.valid = cpus > 0 ? 1 : 0;  // CPUTopology.IsValid: every count non-zero
+  }
+  s.policy = (int32_t)n.numa_policy;
+  s.node_bind = (int32_t)n.node_cpu_bind_policy;
+  s.strategy = (int32_t)n.numa_allocate_strategy;
+  s.num_numa = (int32_t)n.num_numa;
+  for (int i = 0; i < KG_MAX_NUMA; ++i) {
+    if (n.numa_cpu[i] < 0 || n.numa_mem[i] < 0 || n.numa_alloc_cpu[i] < 0 || n.numa_alloc_mem[i] < 0)
+      return fail(KG_E_INVALID, "negative NUMA quantity");
+    s.numa_cpu[i] = i < n.num_numa ? n.numa_cpu[i] : 0;
+    s.numa_mem[i] = i < n.num_numa ? n.numa_mem[i] : 0;
+    m.alloc_cpu[i] = i < n.num_numa ? n.numa_alloc_cpu[i] : 0;
+    m.alloc_mem[i] = i < n.num_numa ? n.numa_alloc_mem[i] : 0;
+  }
+  for (int w = 0; w < KG_MAX_CPUS / 64; ++w) {
+    s.reserved[w] = n.reserved_cpus[w];
+    m.allocated[w] = n.allocated_cpus[w];
+  }
+  return 0;
+}
+
 // Static columns (alloc_cpu, alloc_mem, la_alloc_cpu, la_alloc_mem | alloc_pods, flags) from host mirror.
 uint32_t node_flags(const kg_engine* e, int64_t i) {
   const kg_node& n = e->nodes[i];
@@ -1188,6 +1510,11 @@ RoundGeom geometry(const kg_engine* e) {
 size_t resolve_lds_bytes(const RoundGeom& g, int nb) {
   return ((size_t)nb * kCandStride + (size_t)nb * kPodWords) * 8 + (size_t)g.bitmap_words * 4;
 }
+size_t resolve_numa_lds_bytes(const RoundGeom& g, int nb) {
+  return ((size_t)nb * (kCandStride + kPodWords + kNumaPodWords) + (size_t)kWave * (kNumaStaticWords + kNumaMutWords)) * 8 +
+         (size_t)g.bitmap_words * 4;
+}
+NumaTable numa_table(kg_engine* e) { return NumaTable{e->numa_s.p, e->numa_m.p}; }
 
 dim3 eval_grid(const RoundGeom& g, int nb) {
   // 1-D grid: tile groups × pod groups, swizzled over XCDs inside eval_round
@@ -1215,6 +1542,12 @@ uint64_t* lists_slot(kg_engine* e, const RoundGeom& g, int slot) {
 }
 
 void launch_eval(kg_engine* e, const RoundGeom& g, int64_t first, int nb, int slot, hipStream_t st) {
+  if (e->numa_on) {
+    eval_round_numa<<<eval_grid(g, nb), kWave * kEvalWaves, 0, st>>>(e->T, numa_table(e), e->pods.p, e->npods.p, first, nb,
+                                                                      g.ppw, g.base, g.n_local, g.nt_local, e->P,
+                                                                      e->NP, lists_slot(e, g, slot), poison_ptr(e));
+    return;
+  }
 #define KG_EVAL(X)                                                                                        \
   eval_round<X><<<eval_grid(g, nb), kWave * kEvalWaves, 0, st>>>(e->T, e->pods.p, first, nb, g.ppw, g.base, \
                                                                  g.n_local, g.nt_local, e->P,             \
@@ -1243,6 +1576,13 @@ void launch_merge_ranks(kg_engine* e, const RoundGeom& g, int nb, int slot, hipS
 
 void launch_resolve(kg_engine* e, const RoundGeom& g, int64_t first, int nb, int prev_slot, int slot,
                     int64_t seq, int wait, hipStream_t st) {
+  if (e->numa_on) {
+    resolve_round_numa<<<1, kWave, resolve_numa_lds_bytes(g, nb), st>>>(e->T, numa_table(e), e->pods.p, e->npods.p,
+                                                                        e->cursor.p, first, nb, cand_slot(e, g, slot),
+                                                                        e->P, e->NP, e->out_keys.p, e->out_cpus.p,
+                                                                        g.bitmap_words, poison_ptr(e), seq);
+    return;
+  }
   const int32_t* prev = prev_slot >= 0 ? e->modlists.p + (size_t)prev_slot * (1 + kMaxB) : nullptr;
   int32_t* mine = e->modlists.p + (size_t)slot * (1 + kMaxB);
 #define KG_RESOLVE(X)                                                                                            \
@@ -1457,9 +1797,34 @@ int kg_engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank, int
   e->P.fit_score = (int)(c.fit_score != 0);
   e->P.la_filter = (int)(c.la_filter != 0);
   e->P.la_score = (int)(c.la_score != 0);
-  const int64_t max_total = 100 * ((c.fit_score ? c.weight_fit : 0) + (c.la_score ? c.weight_loadaware : 0));
+  e->numa_on = c.numa_filter || c.numa_score;
+  const int64_t max_total = 100 * ((c.fit_score ? c.weight_fit : 0) + (c.la_score ? c.weight_loadaware : 0) +
+                                   (c.numa_score ? c.weight_numa : 0));
   e->P.score_bits = (int32_t)bits_for(max_total);
-  e->P.monotone = 1;  // NodeResourcesFit + LoadAwareScheduling: assume only lowers a node's key
+  // NodeResourcesFit + LoadAwareScheduling: assume only lowers a node's key; NodeNUMAResource does not
+  e->P.monotone = e->numa_on ? 0 : 1;
+  e->NP.filter = (int32_t)(c.numa_filter != 0);
+  e->NP.score = (int32_t)(c.numa_score != 0);
+  e->NP.weight = (int32_t)c.weight_numa;
+  e->NP.node_strategy = (int32_t)c.numa_scoring_strategy;
+  e->NP.numa_strategy = (int32_t)c.numa_numa_scoring_strategy;
+  e->NP.w_cpu = (int32_t)c.numa_scoring_weights[0];
+  e->NP.w_mem = (int32_t)c.numa_scoring_weights[1];
+  e->NP.nw_cpu = (int32_t)c.numa_numa_scoring_weights[0];
+  e->NP.nw_mem = (int32_t)c.numa_numa_scoring_weights[1];
+  // GetDefaultNUMAAllocateStrategy (util.go:26-32): MostAllocated iff the NUMA scoring strategy is
+  e->NP.default_alloc_strategy = c.numa_numa_scoring_strategy == KG_STRATEGY_MOST_ALLOCATED ? 1 : 0;
+  if (e->numa_on) {
+    if (int rc = e->numa_s.ensure(cap)) return bail(rc);
+    if (int rc = e->numa_m.ensure(cap)) return bail(rc);
+    if (hipMemset(e->numa_s.p, 0, cap * sizeof(NumaStatic)) != hipSuccess ||
+        hipMemset(e->numa_m.p, 0, cap * sizeof(NumaMut)) != hipSuccess)
+      return bail(fail(KG_E_DEVICE, "hipMemset"));
+    const int lds = (int)(kMaxNodes / 8 + ((size_t)kMaxB * (kCandStride + kPodWords + kNumaPodWords) +
+                                           (size_t)kWave * (kNumaStaticWords + kNumaMutWords)) * 8);
+    if (hipFuncSetAttribute((const void*)resolve_round_numa, hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess)
+      return bail(fail(KG_E_DEVICE, "hipFuncSetAttribute(resolve_round_numa LDS)"));
+  }
   e->P.inv_la_wsum = 1.0f / (float)e->P.la_wsum;
   e->P.fit_wsum32 = (int32_t)(e->P.fit_w_cpu + e->P.fit_w_mem);
   e->P.la_prod_score = (int32_t)(c.la_score_according_prod_usage != 0);
@@ -1512,6 +1877,10 @@ void kg_engine_destroy(kg_engine* e) {
     if (e->rs[k]) (void)hipStreamDestroy(e->rs[k]);
   }
   e->deltas.release();
+  e->numa_s.release();
+  e->numa_m.release();
+  e->npods.release();
+  e->out_cpus.release();
   e->scratch64.release();
   e->scratch32.release();
   if (e->stream) (void)hipStreamDestroy(e->stream);
@@ -1614,6 +1983,16 @@ int kg_pods_stage(kg_engine* e, const kg_pod* pods, int64_t n) {
   if (int rc = e->out_keys.ensure(n + kMaxB)) return rc;
   if (n > 0) HIP_TRY(hipMemcpyAsync(e->pods.p, h.data(), n * sizeof(DevPod), hipMemcpyHostToDevice, e->stream));
   HIP_TRY(hipMemsetAsync(e->out_keys.p, 0, (n + kMaxB) * 8, e->stream));
+  std::vector<NumaPod> hn;
+  if (e->numa_on) {
+    hn.resize(std::max<int64_t>(n, 1));
+    for (int64_t k = 0; k < n; ++k)
+      if (int rc = decode_numa_pod(e->cfg, pods[k], hn[k])) return rc;
+    if (int rc = e->npods.ensure(n + kMaxB)) return rc;
+    if (int rc = e->out_cpus.ensure((n + kMaxB) * kCpuWords)) return rc;
+    if (n > 0) HIP_TRY(hipMemcpyAsync(e->npods.p, hn.data(), n * sizeof(NumaPod), hipMemcpyHostToDevice, e->stream));
+    HIP_TRY(hipMemsetAsync(e->out_cpus.p, 0, (n + kMaxB) * kCpuWords * 8, e->stream));
+  }
   HIP_TRY(hipStreamSynchronize(e->stream));
   e->n_staged = n;
   return 0;
@@ -1735,6 +2114,97 @@ int kg_nodes_read_state(kg_engine* e, int64_t* req_cpu, int64_t* req_mem, int64_
   return 0;
 }
 
+int kg_nodes_numa_upsert(kg_engine* e, const kg_node_numa* numa, const int32_t* idx, int64_t n) {
+  if (!e || (n > 0 && (!numa || !idx))) return fail(KG_E_INVALID, "null argument");
+  if (!e->numa_on) return fail(KG_E_INVALID, "the profile does not enable NodeNUMAResource");
+  if (n == 0) return 0;
+  std::vector<NumaStatic> hs(n);
+  std::vector<NumaMut> hm(n);
+  for (int64_t k = 0; k < n; ++k) {
+    if (idx[k] < 0 || idx[k] >= e->capacity) return fail(KG_E_INVALID, "node index %d outside capacity", idx[k]);
+    if (int rc = decode_node_numa(numa[k], hs[k], hm[k])) return rc;
+  }
+  DevBuf<uint8_t> b;
+  const size_t bytes = n * (sizeof(NumaStatic) + sizeof(NumaMut) + 4);
+  if (int rc = b.ensure(bytes)) return rc;
+  NumaStatic* ds = reinterpret_cast<NumaStatic*>(b.p);
+  NumaMut* dm = reinterpret_cast<NumaMut*>(b.p + n * sizeof(NumaStatic));
+  int32_t* di = reinterpret_cast<int32_t*>(b.p + n * (sizeof(NumaStatic) + sizeof(NumaMut)));
+  HIP_TRY(hipMemcpyAsync(ds, hs.data(), n * sizeof(NumaStatic), hipMemcpyHostToDevice, e->stream));
+  HIP_TRY(hipMemcpyAsync(dm, hm.data(), n * sizeof(NumaMut), hipMemcpyHostToDevice, e->stream));
+  HIP_TRY(hipMemcpyAsync(di, idx, n * 4, hipMemcpyHostToDevice, e->stream));
+  scatter_numa<<<(unsigned)((n + 255) / 256), 256, 0, e->stream>>>(numa_table(e), ds, dm, di, n);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  b.release();
+  return 0;
+}
+
+int kg_nodes_read_numa(kg_engine* e, uint64_t* allocated_cpus, int64_t* numa_alloc_cpu, int64_t* numa_alloc_mem) {
+  if (!e) return fail(KG_E_INVALID, "engine is NULL");
+  if (!e->numa_on) return fail(KG_E_INVALID, "the profile does not enable NodeNUMAResource");
+  const int64_t n = e->n_nodes;
+  if (n == 0) return 0;
+  std::vector<NumaMut> hm(n);
+  HIP_TRY(hipMemcpyAsync(hm.data(), e->numa_m.p, n * sizeof(NumaMut), hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  for (int64_t i = 0; i < n; ++i)
+    for (int k = 0; k < 4; ++k) {
+      if (allocated_cpus) allocated_cpus[i * 4 + k] = hm[i].allocated[k];
+      if (numa_alloc_cpu) numa_alloc_cpu[i * 4 + k] = hm[i].alloc_cpu[k];
+      if (numa_alloc_mem) numa_alloc_mem[i * 4 + k] = hm[i].alloc_mem[k];
+    }
+  return 0;
+}
+
+int kg_results_fetch_cpusets(kg_engine* e, int64_t first, int64_t count, uint64_t* out_cpusets) {
+  if (!e || (count > 0 && !out_cpusets)) return fail(KG_E_INVALID, "null argument");
+  if (first < 0 || count < 0 || first + count > e->n_staged) return fail(KG_E_INVALID, "staged range");
+  if (!e->numa_on) {
+    std::memset(out_cpusets, 0, (size_t)count * kCpuWords * 8);
+    return 0;
+  }
+  if (count > 0) {
+    HIP_TRY(hipMemcpyAsync(out_cpusets, e->out_cpus.p + first * kCpuWords, count * kCpuWords * 8, hipMemcpyDeviceToHost,
+                           e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+  }
+  return 0;
+}
+
+int kg_pods_evaluate_numa(kg_engine* e, const kg_pod* pod, int32_t* out_pass, int64_t* out_score,
+                          int64_t* out_affinity) {
+  if (!e || !pod) return fail(KG_E_INVALID, "null argument");
+  if (!e->numa_on) return fail(KG_E_INVALID, "the profile does not enable NodeNUMAResource");
+  if (int rc = sync_static(e)) return rc;
+  DevPod d;
+  NumaPod np;
+  if (int rc = decode_pod(e, *pod, d)) return rc;
+  if (int rc = decode_numa_pod(e->cfg, *pod, np)) return rc;
+  const int64_t n = e->n_nodes;
+  if (n == 0) return 0;
+  if (int rc = e->scratch64.ensure(2 * n + kPodWords + kNumaPodWords)) return rc;
+  if (int rc = e->scratch32.ensure(n)) return rc;
+  DevPod* dp = reinterpret_cast<DevPod*>(e->scratch64.p + 2 * n);
+  NumaPod* dn = reinterpret_cast<NumaPod*>(e->scratch64.p + 2 * n + kPodWords);
+  HIP_TRY(hipMemcpyAsync(dp, &d, sizeof(d), hipMemcpyHostToDevice, e->stream));
+  HIP_TRY(hipMemcpyAsync(dn, &np, sizeof(np), hipMemcpyHostToDevice, e->stream));
+  evaluate_pod_numa<<<(unsigned)((n + 255) / 256), 256, 0, e->stream>>>(e->T, numa_table(e), dp, dn, n, e->NP,
+                                                                        e->scratch32.p, e->scratch64.p,
+                                                                        e->scratch64.p + n);
+  HIP_TRY(hipGetLastError());
+  std::vector<int32_t> ps(n);
+  std::vector<int64_t> sc(n), af(n);
+  HIP_TRY(hipMemcpyAsync(ps.data(), e->scratch32.p, n * 4, hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipMemcpyAsync(sc.data(), e->scratch64.p, n * 8, hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipMemcpyAsync(af.data(), e->scratch64.p + n, n * 8, hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  if (out_pass) std::memcpy(out_pass, ps.data(), n * 4);
+  if (out_score) std::memcpy(out_score, sc.data(), n * 8);
+  if (out_affinity) std::memcpy(out_affinity, af.data(), n * 8);
+  return 0;
+}
+
 int kg_bench_kernel(kg_engine* e, int which, int iters, double* avg_ms, double* algo_bytes) {
   if (!e || iters <= 0 || which < 0 || which > 2) return fail(KG_E_INVALID, "bad argument");
   if (e->n_staged <= 0) return fail(KG_E_INVALID, "stage a pod queue first");
@@ -1744,7 +2214,7 @@ int kg_bench_kernel(kg_engine* e, int which, int iters, double* avg_ms, double* 
   // snapshot the mutable columns: the resolver writes rows back, replays must start from the same state
   const size_t bytes64 = (size_t)e->capacity * 8;
   DevBuf<int64_t> save;
-  if (int rc = save.ensure(9 * e->capacity)) return rc;
+  if (int rc = save.ensure((9 + (e->numa_on ? sizeof(NumaMut) / 8 : 0)) * e->capacity)) return rc;
   int64_t* mut64[8] = {e->T.req_cpu, e->T.req_mem, e->T.nz_cpu, e->T.nz_mem,
                        e->T.la_used_cpu, e->T.la_used_mem, e->T.la_pused_cpu, e->T.la_pused_mem};
   auto snapshot = [&](bool restore) -> int {
@@ -1755,6 +2225,11 @@ int kg_bench_kernel(kg_engine* e, int which, int iters, double* avg_ms, double* 
     int32_t* a = (int32_t*)(save.p + 8 * e->capacity);
     HIP_TRY(hipMemcpyAsync(restore ? e->T.num_pods : a, restore ? a : e->T.num_pods, e->capacity * 4,
                            hipMemcpyDeviceToDevice, e->stream));
+    if (e->numa_on) {
+      NumaMut* m = reinterpret_cast<NumaMut*>(save.p + 9 * e->capacity);
+      HIP_TRY(hipMemcpyAsync(restore ? e->numa_m.p : m, restore ? m : e->numa_m.p, e->capacity * sizeof(NumaMut),
+                             hipMemcpyDeviceToDevice, e->stream));
+    }
     return 0;
   };
   static const int64_t zero4[6] = {0, 0, 0, 0, 0, 0};

@@ -316,9 +316,9 @@ __device__ __forceinline__ uint32_t rare_bit(const EvalRow& e, const EvalParams&
     if (P.fit_w_mem) ok &= mem_dom((int64_t)e.alloc_mem, (int64_t)e.fnz_mem);
   }
   if (P.la_score && (e.flags & F_LA_SCORE)) {
-    if (P.la_w_cpu) ok &= cpu_dom(e.la_alloc_cpu, e.la_free_cpu) & cpu_dom(e.la_alloc_cpu, e.la_pfree_cpu);
+    if (P.la_w_cpu) ok &= cpu_dom(e.la_alloc_cpu, e.la_free_cpu) && cpu_dom(e.la_alloc_cpu, e.la_pfree_cpu);
     if (P.la_w_mem)
-      ok &= mem_dom((int64_t)e.la_alloc_mem, (int64_t)e.la_free_mem) &
+      ok &= mem_dom((int64_t)e.la_alloc_mem, (int64_t)e.la_free_mem) &&
             mem_dom((int64_t)e.la_alloc_mem, (int64_t)e.la_pfree_mem);
   }
   return ok ? 0u : F_RARE;

@@ -1,0 +1,834 @@
+// numa_dev.h — NodeNUMAResource on the device: per-(pod, node) Filter + Score (topology hints, topology-manager
+// merge, Allocate feasibility) for the wide pass and the resolver, and the winner's Reserve (exact cpuset via
+// the cpu accumulator) for the resolver.  Restates (paths under /root/reference/pkg/scheduler):
+//   plugins/nodenumaresource/plugin.go        Filter :276-334, Reserve :375-415, getPreferredCPUBindPolicy :556-576
+//   plugins/nodenumaresource/scoring.go       Score :55-120, calculateAllocatableAndRequested :122-168
+//   plugins/nodenumaresource/resource_manager.go  hints :122-169/:418-532, Allocate :171-360, required :534-589
+//   plugins/nodenumaresource/node_allocation.go   getAvailableCPUs :133-153, NUMA resources :155-177
+//   plugins/nodenumaresource/cpu_accumulator.go   takeCPUs :87-232 and the sorted free lists :371-822
+//   frameworkext/topologymanager/policy*.go   mergeFilteredHints + best-effort / restricted / single-numa-node
+// CPU sets are 256-bit masks in buildCPUTopology numbering (cpu = ((socket·nps + node)·cpn + core)·cpc + t), so a
+// NUMA node, a socket and a core are contiguous cpu ranges.  Scope: ≤ 4 NUMA nodes, cpus per core 1 or 2,
+// maxRefCount 1, no amplification, no reservations, exclusive policy None (validated at ingest).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "kernels.h"
+
+namespace kg {
+
+constexpr int kNumaMax = 4;
+constexpr int kCpuWords = 4;
+
+// static per-node NUMA data (ingest), 136 B
+struct NumaStatic {
+  uint64_t reserved[kCpuWords];
+  int64_t numa_cpu[kNumaMax], numa_mem[kNumaMax];
+  int32_t sockets, nps, cpn, cpc;  // topology (0 sockets = none)
+  int32_t valid;                   // CPUTopology present and IsValid()
+  int32_t policy;                  // KG_NUMA_POLICY_*
+  int32_t node_bind;               // KG_NODE_BIND_*
+  int32_t strategy;                // -1 = plugin default, else KG_STRATEGY_*
+  int32_t num_numa;
+  int32_t pad;
+};
+static_assert(sizeof(NumaStatic) == 136, "NumaStatic layout");
+
+// mutable per-node NUMA state (NodeAllocation)
+struct NumaMut {
+  uint64_t allocated[kCpuWords];
+  int64_t alloc_cpu[kNumaMax], alloc_mem[kNumaMax];
+};
+static_assert(sizeof(NumaMut) == 96, "NumaMut layout");
+
+// per-pod NodeNUMAResource preFilterState (decoded on the host: plugin.go:220-270)
+struct NumaPod {
+  int64_t req_cpu, req_mem;
+  int32_t skip, prefilter_error, cpu_bind, required;  // required/preferred: KG_BIND_*
+  int32_t preferred, needed;
+  int32_t pad[2];
+};
+static_assert(sizeof(NumaPod) == 48, "NumaPod layout");
+
+struct NumaParams {
+  int32_t filter, score, weight;
+  int32_t node_strategy, numa_strategy;  // ScoringStrategy / NUMAScoringStrategy types
+  int32_t w_cpu, w_mem, nw_cpu, nw_mem;
+  int32_t default_alloc_strategy;
+};
+
+struct CpuSet {
+  uint64_t w[kCpuWords];
+};
+
+__device__ __forceinline__ CpuSet cs_zero() { return CpuSet{{0, 0, 0, 0}}; }
+__device__ __forceinline__ int cs_count(const CpuSet& s) {
+  return __popcll(s.w[0]) + __popcll(s.w[1]) + __popcll(s.w[2]) + __popcll(s.w[3]);
+}
+__device__ __forceinline__ bool cs_has(const CpuSet& s, int c) { return (s.w[c >> 6] >> (c & 63)) & 1ull; }
+__device__ __forceinline__ void cs_set(CpuSet& s, int c) { s.w[c >> 6] |= 1ull << (c & 63); }
+__device__ __forceinline__ void cs_clr(CpuSet& s, int c) { s.w[c >> 6] &= ~(1ull << (c & 63)); }
+// cpus [lo, hi)
+__device__ __forceinline__ CpuSet cs_range(int lo, int hi) {
+  CpuSet s;
+#pragma unroll
+  for (int w = 0; w < kCpuWords; ++w) {
+    const int a = lo - 64 * w, b = hi - 64 * w;
+    const uint64_t hiMask = b >= 64 ? ~0ull : (b <= 0 ? 0ull : ((1ull << b) - 1));
+    const uint64_t loMask = a <= 0 ? ~0ull : (a >= 64 ? 0ull : ~((1ull << a) - 1));
+    s.w[w] = hiMask & loMask;
+  }
+  return s;
+}
+__device__ __forceinline__ CpuSet cs_and(CpuSet a, const CpuSet& b) {
+#pragma unroll
+  for (int w = 0; w < kCpuWords; ++w) a.w[w] &= b.w[w];
+  return a;
+}
+__device__ __forceinline__ CpuSet cs_andnot(CpuSet a, const CpuSet& b) {
+#pragma unroll
+  for (int w = 0; w < kCpuWords; ++w) a.w[w] &= ~b.w[w];
+  return a;
+}
+__device__ __forceinline__ CpuSet cs_or(CpuSet a, const CpuSet& b) {
+#pragma unroll
+  for (int w = 0; w < kCpuWords; ++w) a.w[w] |= b.w[w];
+  return a;
+}
+
+struct Topo {
+  int sockets, nps, cpn, cpc, nodes, cores, cpus;
+  __device__ int core_of(int c) const { return c / cpc; }
+  __device__ int node_of(int c) const { return c / (cpc * cpn); }
+  __device__ int socket_of(int c) const { return c / (cpc * cpn * nps); }
+  __device__ int per_node() const { return cpc * cpn; }
+  __device__ int per_socket() const { return cpc * cpn * nps; }
+  __device__ CpuSet all() const { return cs_range(0, cpus); }
+  __device__ CpuSet node_cpus(int n) const { return cs_range(n * per_node(), (n + 1) * per_node()); }
+  __device__ CpuSet socket_cpus(int s) const { return cs_range(s * per_socket(), (s + 1) * per_socket()); }
+};
+
+__device__ __forceinline__ Topo make_topo(const NumaStatic& s) {
+  Topo t;
+  t.sockets = s.sockets;
+  t.nps = s.nps;
+  t.cpn = s.cpn;
+  t.cpc = s.cpc > 0 ? s.cpc : 1;
+  t.nodes = s.sockets * s.nps;
+  t.cores = t.nodes * s.cpn;
+  t.cpus = t.cores * t.cpc;
+  return t;
+}
+
+// even-position bits (the first cpu of every 2-cpu core)
+constexpr uint64_t kEven = 0x5555555555555555ull;
+
+// cpus of cores whose every cpu is in s (cpc 1: s itself)
+__device__ __forceinline__ CpuSet full_core_cpus(const Topo& t, const CpuSet& s) {
+  if (t.cpc == 1) return s;
+  CpuSet r;
+#pragma unroll
+  for (int w = 0; w < kCpuWords; ++w) {
+    const uint64_t f = s.w[w] & (s.w[w] >> 1) & kEven;
+    r.w[w] = f | (f << 1);
+  }
+  return r;
+}
+// the first (lowest) cpu of every core with a cpu in s
+__device__ __forceinline__ CpuSet first_cpu_per_core(const Topo& t, const CpuSet& s) {
+  if (t.cpc == 1) return s;
+  CpuSet r;
+#pragma unroll
+  for (int w = 0; w < kCpuWords; ++w) {
+    const uint64_t ev = s.w[w] & kEven, od = s.w[w] & ~kEven;
+    r.w[w] = ev | (od & ~(ev << 1));
+  }
+  return r;
+}
+
+// filterCPUsByRequiredCPUBindPolicy (resource_manager.go:534-566)
+__device__ __forceinline__ CpuSet filter_required(const Topo& t, const CpuSet& avail, int policy) {
+  if (policy == 2 /*FullPCPUs*/) return full_core_cpus(t, avail);
+  if (policy == 3 /*SpreadByPCPUs*/) return first_cpu_per_core(t, avail);
+  return avail;
+}
+
+// the lowest k cpus of s (k ≤ |s|)
+__device__ __forceinline__ CpuSet lowest_k(CpuSet s, int k) {
+  CpuSet r = cs_zero();
+  for (int w = 0; w < kCpuWords && k > 0; ++w) {
+    uint64_t v = s.w[w];
+    const int c = __popcll(v);
+    if (c <= k) {
+      r.w[w] = v;
+      k -= c;
+    } else {
+      while (k > 0) {
+        const uint64_t low = v & (~v + 1);
+        r.w[w] |= low;
+        v ^= low;
+        --k;
+      }
+    }
+  }
+  return r;
+}
+
+__device__ __forceinline__ bool better_free(int strategy, int a, int b) { return strategy == 1 ? a < b : a > b; }
+
+// ---------------------------------------------------------------------------------------------------------
+// takeCPUs (cpu_accumulator.go:87-232), single thread, on masks.  Returns false on "not enough cpus".
+// ---------------------------------------------------------------------------------------------------------
+struct Acc {
+  Topo t;
+  CpuSet avail;  // allocatableCPUs
+  CpuSet result;
+  int needed, strategy;
+  __device__ void take(const CpuSet& s) {
+    result = cs_or(result, s);
+    avail = cs_andnot(avail, s);
+    needed -= cs_count(s);
+  }
+};
+
+// groups (NUMA nodes or sockets) of a cpu mask, ordered as freeCoresInNode/Socket(full=true) order them:
+// (group free count, [socket free for nodes], id).  Returns the group count; ids in order.
+__device__ __forceinline__ int order_groups(const Acc& a, bool by_node, const CpuSet& sel, int* ids, int* cnt) {
+  const int ng = by_node ? a.t.nodes : a.t.sockets;
+  int n = 0;
+  for (int g = 0; g < ng && g < 8; ++g) {
+    const CpuSet in = cs_and(sel, by_node ? a.t.node_cpus(g) : a.t.socket_cpus(g));
+    const int c = cs_count(in);
+    if (c == 0) continue;
+    ids[n] = g;
+    cnt[n] = c;
+    ++n;
+  }
+  for (int i = 0; i < n; ++i) {  // selection sort on a total order
+    int best = i;
+    for (int j = i + 1; j < n; ++j) {
+      bool before;
+      if (cnt[j] != cnt[best]) before = better_free(a.strategy, cnt[j], cnt[best]);
+      else if (by_node) {
+        const int sj = cs_count(cs_and(a.avail, a.t.socket_cpus(ids[j] / a.t.nps)));
+        const int sb = cs_count(cs_and(a.avail, a.t.socket_cpus(ids[best] / a.t.nps)));
+        before = sj != sb ? better_free(a.strategy, sj, sb) : ids[j] < ids[best];
+      } else {
+        before = ids[j] < ids[best];
+      }
+      if (before) best = j;
+    }
+    const int ti = ids[i], tc = cnt[i];
+    ids[i] = ids[best];
+    cnt[i] = cnt[best];
+    ids[best] = ti;
+    cnt[best] = tc;
+  }
+  return n;
+}
+
+// first k cpus of a group list where cores are ordered (free count desc, id) and cpus ascending (cpc ≤ 2:
+// full cores then single-cpu cores, each ascending)
+__device__ __forceinline__ CpuSet first_k_cores_order(const Topo& t, const CpuSet& s, int k) {
+  const CpuSet full = full_core_cpus(t, s);
+  const int nf = cs_count(full);
+  if (k <= nf) return lowest_k(full, k);
+  return cs_or(full, lowest_k(cs_andnot(s, full), k - nf));
+}
+
+// spreadCPUs over an ascending cpu list: the first cpu of every core (ascending), then the rest (ascending);
+// returns the first k
+__device__ __forceinline__ CpuSet spread_first_k(const Topo& t, const CpuSet& s, int k) {
+  const CpuSet first = first_cpu_per_core(t, s);
+  const int nf = cs_count(first);
+  if (k <= nf) return lowest_k(first, k);
+  return cs_or(first, lowest_k(cs_andnot(s, first), k - nf));
+}
+
+__device__ inline bool take_cpus(const Topo& t, const CpuSet& available, int needed, int bind, int strategy,
+                                 CpuSet& out) {
+  Acc a;
+  a.t = t;
+  a.avail = cs_and(available, t.all());
+  a.result = cs_zero();
+  a.needed = needed;
+  a.strategy = strategy;
+  out = cs_zero();
+  if (a.needed < 1) return true;
+  if (a.needed > cs_count(a.avail)) return false;
+  const bool full = bind == 2;
+  int ids[8], cnt[8];
+  if (full || t.cpc == 1) {
+    if (a.needed <= t.per_node()) {
+      const CpuSet fc = full_core_cpus(t, a.avail);
+      const int ng = order_groups(a, true, fc, ids, cnt);
+      for (int g = 0; g < ng; ++g)
+        if (cnt[g] >= a.needed) {
+          a.take(lowest_k(cs_and(fc, t.node_cpus(ids[g])), a.needed));
+          out = a.result;
+          return true;
+        }
+    }
+    if (a.needed <= t.per_socket()) {
+      const CpuSet fc = full_core_cpus(t, a.avail);
+      const int ng = order_groups(a, false, fc, ids, cnt);
+      for (int g = 0; g < ng; ++g)
+        if (cnt[g] >= a.needed) {
+          a.take(lowest_k(cs_and(fc, t.socket_cpus(ids[g])), a.needed));
+          out = a.result;
+          return true;
+        }
+    }
+    {
+      const CpuSet fc = full_core_cpus(t, a.avail);
+      int ng = order_groups(a, false, fc, ids, cnt);
+      // stable sort by full-core cpu count, most first
+      for (int i = 1; i < ng; ++i)
+        for (int j = i; j > 0 && cnt[j - 1] < cnt[j]; --j) {
+          const int ti = ids[j], tc = cnt[j];
+          ids[j] = ids[j - 1];
+          cnt[j] = cnt[j - 1];
+          ids[j - 1] = ti;
+          cnt[j - 1] = tc;
+        }
+      int uid[8], ucnt[8], nu = 0;
+      for (int g = 0; g < ng; ++g) {
+        if (a.needed < cnt[g]) {
+          uid[nu] = ids[g];
+          ucnt[nu++] = cnt[g];
+        } else {
+          a.take(cs_and(fc, t.socket_cpus(ids[g])));
+          if (a.needed < 1) {
+            out = a.result;
+            return true;
+          }
+        }
+      }
+      if (a.needed >= t.cpc) {
+        for (int i = 1; i < nu; ++i)  // stable, fewest first
+          for (int j = i; j > 0 && ucnt[j - 1] > ucnt[j]; --j) {
+            const int ti = uid[j], tc = ucnt[j];
+            uid[j] = uid[j - 1];
+            ucnt[j] = ucnt[j - 1];
+            uid[j - 1] = ti;
+            ucnt[j - 1] = tc;
+          }
+        for (int g = 0; g < nu; ++g) {
+          CpuSet list = cs_and(fc, t.socket_cpus(uid[g]));  // the group's full-core cpus, ascending
+          while (cs_count(list) > 0) {
+            const CpuSet chunk = lowest_k(list, t.cpc);
+            list = cs_andnot(list, chunk);
+            a.take(chunk);
+            if (a.needed < 1) {
+              out = a.result;
+              return true;
+            }
+            if (a.needed < t.cpc) break;
+          }
+        }
+      }
+    }
+  }
+  if (!full) {
+    if (a.needed <= t.per_node()) {
+      for (int fe = 0; fe < 2; ++fe) {
+        // freeCPUsInNode: nodes by (node free, socket free, id) on the unreduced counts; with
+        // filterExclusive each list keeps one cpu per core
+        const int ng = order_groups(a, true, a.avail, ids, cnt);
+        for (int g = 0; g < ng; ++g) {
+          const CpuSet in = cs_and(a.avail, t.node_cpus(ids[g]));
+          const CpuSet lst = fe == 0 ? first_cpu_per_core(t, in) : in;
+          if (cs_count(lst) >= a.needed) {
+            a.take(fe == 0 ? lowest_k(lst, a.needed) : spread_first_k(t, lst, a.needed));
+            out = a.result;
+            return true;
+          }
+        }
+      }
+    }
+    if (a.needed <= t.per_socket()) {
+      for (int fe = 0; fe < 2; ++fe) {
+        // freeCPUsInSocket: sockets by (length of the (reduced) list, id)
+        int sid[8], scnt[8], ns = 0;
+        for (int s = 0; s < t.sockets && s < 8; ++s) {
+          const CpuSet in = cs_and(a.avail, t.socket_cpus(s));
+          const CpuSet lst = fe == 0 ? first_cpu_per_core(t, in) : in;
+          const int c = cs_count(lst);
+          if (cs_count(in) == 0) continue;
+          sid[ns] = s;
+          scnt[ns++] = c;
+        }
+        for (int i = 0; i < ns; ++i) {
+          int best = i;
+          for (int j = i + 1; j < ns; ++j)
+            if (scnt[j] != scnt[best] ? better_free(a.strategy, scnt[j], scnt[best]) : sid[j] < sid[best]) best = j;
+          const int ti = sid[i], tc = scnt[i];
+          sid[i] = sid[best];
+          scnt[i] = scnt[best];
+          sid[best] = ti;
+          scnt[best] = tc;
+        }
+        for (int g = 0; g < ns; ++g) {
+          const CpuSet in = cs_and(a.avail, t.socket_cpus(sid[g]));
+          const CpuSet lst = fe == 0 ? first_cpu_per_core(t, in) : in;
+          if (scnt[g] >= a.needed) {
+            a.take(fe == 0 ? lowest_k(lst, a.needed) : spread_first_k(t, lst, a.needed));
+            out = a.result;
+            return true;
+          }
+        }
+      }
+    }
+  }
+  // freeCPUs: cores by (socket colo desc, socket free, node free, core free asc, socket, core), then spread;
+  // take one by one.  Classes of (socket, node) share the first three keys; inside a run of equal classes
+  // single-free cores come before full ones, each by core id (= (socket, core) order in this numbering).
+  {
+    int nid[8], nn = 0;
+    for (int n = 0; n < t.nodes && n < 8; ++n)
+      if (cs_count(cs_and(a.avail, t.node_cpus(n))) > 0) nid[nn++] = n;
+    int colo[8], sfree[8], nfree[8];
+    for (int i = 0; i < nn; ++i) {
+      const int s = nid[i] / t.nps;
+      colo[i] = cs_count(cs_and(a.result, t.socket_cpus(s)));
+      sfree[i] = cs_count(cs_and(a.avail, t.socket_cpus(s)));
+      nfree[i] = cs_count(cs_and(a.avail, t.node_cpus(nid[i])));
+    }
+    for (int i = 0; i < nn; ++i) {  // order the nodes by the class keys, then id
+      int best = i;
+      for (int j = i + 1; j < nn; ++j) {
+        bool before;
+        if (colo[j] != colo[best]) before = colo[j] > colo[best];
+        else if (sfree[j] != sfree[best]) before = better_free(a.strategy, sfree[j], sfree[best]);
+        else if (nfree[j] != nfree[best]) before = better_free(a.strategy, nfree[j], nfree[best]);
+        else before = nid[j] < nid[best];
+        if (before) best = j;
+      }
+      int tmp;
+      tmp = nid[i]; nid[i] = nid[best]; nid[best] = tmp;
+      tmp = colo[i]; colo[i] = colo[best]; colo[best] = tmp;
+      tmp = sfree[i]; sfree[i] = sfree[best]; sfree[best] = tmp;
+      tmp = nfree[i]; nfree[i] = nfree[best]; nfree[best] = tmp;
+    }
+    // the ordered cpu list, as a sequence of masks to read in ascending order
+    CpuSet seq[16];
+    int nseq = 0;
+    for (int i = 0; i < nn;) {
+      int j = i;
+      CpuSet run = cs_zero();
+      while (j < nn && colo[j] == colo[i] && sfree[j] == sfree[i] && nfree[j] == nfree[i]) {
+        run = cs_or(run, cs_and(a.avail, t.node_cpus(nid[j])));
+        ++j;
+      }
+      const CpuSet fc = full_core_cpus(t, run);
+      seq[nseq++] = cs_andnot(run, fc);  // single-free cores first
+      seq[nseq++] = fc;
+      i = j;
+    }
+    // spreadCPUs over the concatenated list: first pass takes the first cpu of each core, second the rest
+    for (int pass = 0; pass < 2; ++pass)
+      for (int k = 0; k < nseq; ++k) {
+        const CpuSet part = pass == 0 ? first_cpu_per_core(t, seq[k]) : cs_andnot(seq[k], first_cpu_per_core(t, seq[k]));
+        const int c = cs_count(part);
+        if (c == 0) continue;
+        const int take = c < a.needed ? c : a.needed;
+        a.take(lowest_k(part, take));
+        if (a.needed < 1) {
+          out = a.result;
+          return true;
+        }
+      }
+  }
+  out = cs_zero();
+  return false;
+}
+
+// ---------------------------------------------------------------------------------------------------------
+// Filter / Score / Reserve
+// ---------------------------------------------------------------------------------------------------------
+struct NumaHint {
+  uint32_t mask;
+  int nil, preferred, score;
+};
+
+// IterateBitMasks order over ≤ 4 NUMA nodes (size, then lexicographic bit lists), one nibble per mask
+__device__ __forceinline__ uint32_t mask_at(int k) {
+  // 1,2,4,8 | 3,5,9,6,10,12 | 7,11,13,14 | 15
+  constexpr uint64_t order = (1ull << 0) | (2ull << 4) | (4ull << 8) | (8ull << 12) | (3ull << 16) | (5ull << 20) |
+                             (9ull << 24) | (6ull << 28) | (10ull << 32) | (12ull << 36) | (7ull << 40) |
+                             (11ull << 44) | (13ull << 48) | (14ull << 52) | (15ull << 56);
+  return (uint32_t)((order >> (4 * k)) & 15ull);
+}
+
+// getPreferredCPUBindPolicy (plugin.go:556-576); -1: getResourceOptions fails (topology missing / invalid)
+__device__ __forceinline__ int numa_pref_bind(const NumaStatic& s, int preferred) {
+  if (!s.valid) return -1;
+  if (s.node_bind == 2 /*SpreadByPCPUs*/) return 3;
+  if (s.node_bind == 1 /*FullPCPUsOnly*/) return 2;
+  return preferred;
+}
+
+__device__ __forceinline__ int64_t most_requested64(int64_t requested, int64_t capacity) {
+  if (capacity == 0) return 0;
+  if (requested > capacity) requested = capacity;
+  return (requested * 100) / capacity;
+}
+
+// resourceAllocationScorer.score (scoring.go:191-230) over cpu + memory with least/mostResourceScorer
+__device__ __forceinline__ int64_t numa_scorer(int strategy, int32_t w_cpu, int32_t w_mem, int64_t req_c, int64_t req_m,
+                                               int64_t alloc_c, int64_t alloc_m, int64_t pod_c, int64_t pod_m) {
+  int64_t s = 0, ws = 0;
+  if (w_cpu != 0 && alloc_c != 0) {
+    s += (strategy == 1 ? most_requested64(req_c + pod_c, alloc_c) : least_requested(req_c + pod_c, alloc_c)) * w_cpu;
+    ws += w_cpu;
+  }
+  if (w_mem != 0 && alloc_m != 0) {
+    s += (strategy == 1 ? most_requested64(req_m + pod_m, alloc_m) : least_requested(req_m + pod_m, alloc_m)) * w_mem;
+    ws += w_mem;
+  }
+  return ws ? s / ws : 0;
+}
+
+__device__ __forceinline__ CpuSet numa_available_cpus(const Topo& t, const NumaStatic& s, const NumaMut& m) {
+  CpuSet a = t.all();
+#pragma unroll
+  for (int w = 0; w < kCpuWords; ++w) a.w[w] &= ~(m.allocated[w] | s.reserved[w]);
+  return a;
+}
+
+// One provider list of the topology manager: either a single "don't care" (nil) hint, or hints over the
+// masks of a set of enumeration positions; `empty` = no hint at all
+struct HintList {
+  uint32_t set;  // positions k (mask_at(k)) in enumeration order
+  int nil, nil_pref, empty, min_size;
+};
+
+__device__ __forceinline__ int sc_at(uint64_t lo, uint64_t hi, int k) {
+  return k < 9 ? (int)((lo >> (7 * k)) & 127u) : (int)((hi >> (7 * (k - 9))) & 127u);
+}
+
+// mergeFilteredHints (policy.go:127-185) over the permutations of ≤ 2 lists (the last varies fastest)
+__device__ inline NumaHint merge_hints(uint32_t def, const HintList* L, int nl, uint64_t sc_lo, uint64_t sc_hi) {
+  NumaHint best{def, 0, 0, 0};
+  for (int i = 0; i < nl; ++i)
+    if (L[i].empty) return best;
+  const uint32_t s0 = L[0].nil ? 1u : L[0].set;
+  const uint32_t s1 = nl > 1 ? (L[1].nil ? 1u : L[1].set) : 1u;
+  for (uint32_t a = s0; a; a &= a - 1) {
+    const int ka = __builtin_ctz(a);
+    const bool nila = L[0].nil;
+    const uint32_t ma = nila ? def : mask_at(ka);
+    const bool pa = nila ? L[0].nil_pref : __popc(ma) == L[0].min_size;
+    for (uint32_t b = s1; b; b &= b - 1) {
+      const int kb = __builtin_ctz(b);
+      const bool nilb = nl > 1 ? L[1].nil : true;
+      const uint32_t mb = nilb ? def : mask_at(kb);
+      const bool pb = nl > 1 ? (nilb ? L[1].nil_pref : __popc(mb) == L[1].min_size) : true;
+      const uint32_t merged = def & ma & mb;
+      if (merged == 0) continue;
+      const int preferred = pa && pb;
+      int score = 0;
+      if (!nila && ma == merged) score = sc_at(sc_lo, sc_hi, ka);
+      if (nl > 1 && !nilb && mb == merged && sc_at(sc_lo, sc_hi, kb) > score) score = sc_at(sc_lo, sc_hi, kb);
+      const int pm = __popc(merged), pbst = __popc(best.mask);
+      if (preferred && !best.preferred) {
+        best = NumaHint{merged, 0, 1, score};
+      } else if (!preferred && best.preferred) {
+      } else {
+        const bool narrower = pm == pbst ? merged < best.mask : pm < pbst;
+        if (!narrower) {
+          if (pm == pbst && score > best.score) best = NumaHint{merged, 0, preferred, score};
+        } else {
+          best = NumaHint{merged, 0, preferred, score};
+        }
+      }
+    }
+  }
+  return best;
+}
+
+// Topology-manager Admit for the NodeNUMAResource provider alone (manager.go:58-100, policy_*.go) with the
+// hints of generateResourceHints (resource_manager.go:418-532).  Returns admit; writes the best hint.
+__device__ inline bool numa_admit(const Topo& t, const NumaStatic& s, const NumaMut& m, const NumaPod& p,
+                                  const NumaParams& NP, NumaHint& best) {
+  const int nn = s.num_numa;
+  const uint32_t def = (1u << nn) - 1u;
+  const int bind = numa_pref_bind(s, p.preferred);
+  HintList L[2];
+  int nl = 0;
+  uint64_t sc_lo = 0, sc_hi = 0;
+  const bool req_c = p.req_cpu > 0, req_m = p.req_mem > 0;
+  if (bind < 0 || (!req_c && !req_m)) {
+    L[0] = HintList{0, 1, 1, 0, 0};
+    nl = 1;
+  } else {
+    int64_t av_cpu[kNumaMax], av_mem[kNumaMax];
+    const CpuSet avail = numa_available_cpus(t, s, m);
+    for (int i = 0; i < kNumaMax; ++i) {
+      if (i >= nn) {
+        av_cpu[i] = av_mem[i] = 0;
+        continue;
+      }
+      const int64_t ac = s.numa_cpu[i] - m.alloc_cpu[i], am = s.numa_mem[i] - m.alloc_mem[i];
+      av_cpu[i] = ac > 0 ? ac : 0;
+      av_mem[i] = am > 0 ? am : 0;
+      if (p.cpu_bind && p.required != 0 && av_cpu[i] != 0) {  // trimNUMANodeResources (:140-169)
+        CpuSet in = cs_and(avail, t.node_cpus(i));
+        if ((int64_t)cs_count(in) * 1000 >= av_cpu[i]) in = filter_required(t, in, bind);
+        const int64_t c = (int64_t)cs_count(in) * 1000;
+        if (c < av_cpu[i]) av_cpu[i] = c;
+      }
+    }
+    uint32_t hc = 0, hm = 0;
+    int min_c = nn, min_m = nn;
+    const int nmask = (1 << nn) - 1;  // masks of ≤ nn bits: the first (2^nn - 1) positions restricted to def
+    for (int k = 0; k < 15; ++k) {
+      const uint32_t mk = mask_at(k);
+      if (mk & ~def) continue;
+      int64_t a_c = 0, a_m = 0, tot_c = 0, tot_m = 0;
+      for (int i = 0; i < nn; ++i)
+        if ((mk >> i) & 1u) {
+          a_c += av_cpu[i];
+          a_m += av_mem[i];
+          tot_c += s.numa_cpu[i];
+          tot_m += s.numa_mem[i];
+        }
+      const int64_t rq_c = tot_c - a_c > 0 ? tot_c - a_c : 0, rq_m = tot_m - a_m > 0 ? tot_m - a_m : 0;
+      const int64_t sc = numa_scorer(NP.numa_strategy, NP.nw_cpu, NP.nw_mem, rq_c, rq_m, tot_c, tot_m, p.req_cpu,
+                                     p.req_mem);
+      if (k < 9) sc_lo |= (uint64_t)sc << (7 * k);
+      else sc_hi |= (uint64_t)sc << (7 * (k - 9));
+      const int cnt = __popc(mk);
+      if (req_m && tot_m >= p.req_mem) {
+        if (cnt < min_m) min_m = cnt;
+        if (a_m >= p.req_mem) hm |= 1u << k;
+      }
+      if (req_c && tot_c >= p.req_cpu) {
+        if (cnt < min_c) min_c = cnt;
+        if (a_c >= p.req_cpu) hc |= 1u << k;
+      }
+    }
+    (void)nmask;
+    // filterProvidersHints (policy.go:94-125): resources in sorted-name order (cpu, memory); a present but
+    // empty list becomes one non-preferred "don't care" hint
+    if (req_c) L[nl++] = hc ? HintList{hc, 0, 0, 0, min_c} : HintList{0, 1, 0, 0, 0};
+    if (req_m) L[nl++] = hm ? HintList{hm, 0, 0, 0, min_m} : HintList{0, 1, 0, 0, 0};
+  }
+  if (s.policy == 3 /*SingleNUMANode*/) {
+    // filterSingleNumaHints: "don't care" hints that are preferred, and preferred single-NUMA hints
+    for (int i = 0; i < nl; ++i) {
+      if (L[i].nil) {
+        if (!L[i].nil_pref) L[i].empty = 1;
+      } else {
+        uint32_t keep = 0;
+        for (uint32_t b = L[i].set; b; b &= b - 1) {
+          const int k = __builtin_ctz(b);
+          if (__popc(mask_at(k)) == 1 && 1 == L[i].min_size) keep |= 1u << k;
+        }
+        L[i].set = keep;
+        if (!keep) L[i].empty = 1;
+      }
+    }
+    best = merge_hints(def, L, nl, sc_lo, sc_hi);
+    if (!best.nil && best.mask == def) best = NumaHint{0, 1, best.preferred, 0};
+    return best.preferred != 0;
+  }
+  best = merge_hints(def, L, nl, sc_lo, sc_hi);
+  if (s.policy == 2 /*Restricted*/) return best.preferred != 0;
+  return true;  // BestEffort
+}
+
+struct NumaAlloc {
+  int n;
+  int numa[kNumaMax];
+  int64_t cpu[kNumaMax], mem[kNumaMax];
+};
+
+// allocateResourcesByHint (resource_manager.go:195-250); false on insufficient NUMA resources
+__device__ __forceinline__ bool alloc_by_hint(const NumaStatic& s, const NumaMut& m, const NumaPod& p,
+                                              uint32_t mask, NumaAlloc& res) {
+  res.n = 0;
+  if (s.num_numa == 0) return false;
+  int64_t rq_c = p.req_cpu, rq_m = p.req_mem;
+  const bool key_c = p.req_cpu > 0, key_m = p.req_mem > 0;
+  for (int i = 0; i < s.num_numa; ++i) {
+    if (!((mask >> i) & 1u)) continue;
+    int64_t ac = 0, am = 0;
+    if (key_c) {
+      const int64_t av = s.numa_cpu[i] - m.alloc_cpu[i] > 0 ? s.numa_cpu[i] - m.alloc_cpu[i] : 0;
+      ac = rq_c < av ? rq_c : av;
+      rq_c -= ac;
+    }
+    if (key_m) {
+      const int64_t av = s.numa_mem[i] - m.alloc_mem[i] > 0 ? s.numa_mem[i] - m.alloc_mem[i] : 0;
+      am = rq_m < av ? rq_m : av;
+      rq_m -= am;
+    }
+    if (ac != 0 || am != 0) {
+      res.numa[res.n] = i;
+      res.cpu[res.n] = ac;
+      res.mem[res.n] = am;
+      ++res.n;
+    }
+    if (rq_c == 0 && rq_m == 0) break;
+  }
+  return !((key_c && rq_c != 0) || (key_m && rq_m != 0));
+}
+
+// resourceManager.Allocate (resource_manager.go:171-360).  EXACT=false: feasibility from counts only (the
+// per-NUMA takes of allocateCPUSet never fail and a FullPCPUs take of k cpus from full-core lists is whole
+// cores iff k is a multiple of cpus-per-core, so satisfiedRequiredCPUBindPolicy reduces to that parity);
+// EXACT=true: the cpuset itself (cpu accumulator), for Reserve.
+template <bool EXACT>
+__device__ inline bool numa_allocate(const Topo& t, const NumaStatic& s, const NumaMut& m, const NumaPod& p,
+                                     const NumaHint& h, int strategy, NumaAlloc& res, CpuSet& cpus) {
+  res.n = 0;
+  cpus = cs_zero();
+  const int bind = numa_pref_bind(s, p.preferred);
+  if (bind < 0) return false;
+  if (!h.nil && !alloc_by_hint(s, m, p, h.mask, res)) return false;
+  if (!p.cpu_bind) return true;
+  CpuSet avail = numa_available_cpus(t, s, m);
+  const bool required = p.required != 0;
+  if (required) avail = filter_required(t, avail, bind);
+  if (cs_count(avail) < p.needed) return false;
+  const bool whole = required && bind == 2 && t.cpc > 1;  // satisfiedRequired(FullPCPUs) needs whole cores
+  int needed = p.needed;
+  if (res.n > 0) {
+    int got = 0;
+    for (int k = 0; k < res.n; ++k) {
+      const CpuSet in = cs_and(avail, t.node_cpus(res.numa[k]));
+      int num = cs_count(in);
+      const int want = (int)(res.cpu[k] / 1000);
+      if (want < num) num = want;
+      if (whole && num % t.cpc != 0) return false;
+      if (EXACT) {
+        CpuSet one;
+        if (!take_cpus(t, in, num, bind, strategy, one)) return false;
+        cpus = cs_or(cpus, one);
+      }
+      got += num;
+    }
+    if (got != needed) return false;
+    return true;
+  }
+  if (whole && needed % t.cpc != 0) return false;
+  if (EXACT) {
+    if (!take_cpus(t, avail, needed, bind, strategy, cpus)) return false;
+    if (required) {  // satisfiedRequiredCPUBindPolicy (:568-589), exact
+      if (bind == 2 && t.cpc > 1 && cs_count(full_core_cpus(t, cpus)) != cs_count(cpus)) return false;
+      if (bind == 3 && cs_count(first_cpu_per_core(t, cpus)) != cs_count(cpus)) return false;
+    }
+  }
+  return true;
+}
+
+__device__ __forceinline__ int numa_alloc_strategy(const NumaStatic& s, const NumaParams& NP) {
+  return s.strategy >= 0 ? s.strategy : NP.default_alloc_strategy;
+}
+
+__device__ __forceinline__ bool skip_the_node(const NumaPod& p, int policy) {
+  return p.skip || (!p.cpu_bind && policy == 0);
+}
+
+// NodeNUMAResource.Filter (plugin.go:276-334); writes the affinity the topology manager stores
+__device__ inline bool numa_filter(const Topo& t, const NumaStatic& s, const NumaMut& m, const NumaPod& p,
+                                   const NumaParams& NP, NumaHint& aff) {
+  aff = NumaHint{0, 1, 0, 0};
+  if (p.prefilter_error) return false;
+  if (skip_the_node(p, s.policy)) return true;
+  const int strategy = numa_alloc_strategy(s, NP);
+  NumaAlloc res;
+  CpuSet cpus;
+  if (p.cpu_bind) {
+    if (!s.valid) return false;
+    const bool full_only = s.node_bind == 1;
+    if (full_only || p.required == 2) {
+      if (p.needed % t.cpc != 0) return false;                                   // SMT alignment
+      if (full_only && (p.required != 2 || p.preferred != 2)) return false;  // required FullPCPUs policy
+    }
+    if (p.required != 0 && s.policy == 0) {
+      const NumaHint none{0, 1, 0, 0};
+      if (!numa_allocate<false>(t, s, m, p, none, strategy, res, cpus)) return false;
+    }
+  }
+  if (s.policy != 0) {
+    if (s.num_numa == 0) return false;
+    NumaHint best;
+    if (!numa_admit(t, s, m, p, NP, best)) return false;
+    aff = best;
+    if (!numa_allocate<false>(t, s, m, p, best, strategy, res, cpus)) return false;
+  }
+  return true;
+}
+
+// NodeNUMAResource.Score (scoring.go:55-168) with the stored affinity; node_* = NodeInfo.Requested/Allocatable
+__device__ inline int64_t numa_score(const Topo& t, const NumaStatic& s, const NumaMut& m, const NumaPod& p,
+                                     const NumaParams& NP, const NumaHint& aff, int64_t node_req_cpu,
+                                     int64_t node_req_mem, int64_t node_alloc_cpu, int64_t node_alloc_mem) {
+  if (skip_the_node(p, s.policy)) {
+    if (p.skip) return 0;
+    if (numa_pref_bind(s, p.preferred) < 0) return 0;  // scoreWithAmplifiedCPUs: getResourceOptions
+    return numa_scorer(NP.node_strategy, NP.w_cpu, NP.w_mem, node_req_cpu, node_req_mem, node_alloc_cpu,
+                       node_alloc_mem, p.req_cpu, p.req_mem);
+  }
+  if (p.cpu_bind && !s.valid) return 0;
+  NumaAlloc res;
+  CpuSet cpus;
+  if (!numa_allocate<false>(t, s, m, p, aff, numa_alloc_strategy(s, NP), res, cpus)) return 0;
+  int64_t ac, am, rc, rm;
+  if (res.n > 0) {
+    ac = am = rc = rm = 0;
+    for (int k = 0; k < res.n; ++k) {
+      const int i = res.numa[k];
+      rc += m.alloc_cpu[i];
+      rm += m.alloc_mem[i];
+      ac += s.numa_cpu[i];
+      am += s.numa_mem[i];
+    }
+  } else {
+    ac = node_alloc_cpu;
+    am = node_alloc_mem;
+    rc = node_req_cpu;
+    rm = node_req_mem;
+  }
+  // a cpuset pod: requested cpu = |allocated cpus| · 1000 (needed ≥ 1 whenever cpu_bind)
+  if (p.cpu_bind) {
+    const CpuSet alloc{{m.allocated[0], m.allocated[1], m.allocated[2], m.allocated[3]}};
+    rc = (int64_t)cs_count(alloc) * 1000;
+  }
+  return numa_scorer(NP.node_strategy, NP.w_cpu, NP.w_mem, rc, rm, ac, am, p.req_cpu, p.req_mem);
+}
+
+// NodeNUMAResource.Reserve (plugin.go:375-415) → Allocate (exact cpuset) → addPodAllocation
+// (node_allocation.go:76-103).  False: the allocation fails and the pod is not placed.
+__device__ inline bool numa_reserve(const Topo& t, const NumaStatic& s, NumaMut& m, const NumaPod& p,
+                                    const NumaParams& NP, const NumaHint& aff, CpuSet& cpus) {
+  cpus = cs_zero();
+  if (skip_the_node(p, s.policy)) return true;
+  if (p.cpu_bind && !s.valid) return false;
+  NumaAlloc res;
+  if (!numa_allocate<true>(t, s, m, p, aff, numa_alloc_strategy(s, NP), res, cpus)) return false;
+#pragma unroll
+  for (int w = 0; w < kCpuWords; ++w) m.allocated[w] |= cpus.w[w];
+  for (int k = 0; k < res.n; ++k) {
+    m.alloc_cpu[res.numa[k]] += res.cpu[k];
+    m.alloc_mem[res.numa[k]] += res.mem[k];
+  }
+  return true;
+}
+
+// Filter (when the profile has it) + Score of one node: feasibility and the unweighted plugin score
+__device__ inline bool numa_eval(const NumaStatic& s, const NumaMut& m, const NumaPod& p, const NumaParams& NP,
+                                 int64_t node_req_cpu, int64_t node_req_mem, int64_t node_alloc_cpu,
+                                 int64_t node_alloc_mem, int64_t& score, NumaHint& aff) {
+  const Topo t = make_topo(s);
+  aff = NumaHint{0, 1, 0, 0};
+  score = 0;
+  if (NP.filter && !numa_filter(t, s, m, p, NP, aff)) return false;
+  if (NP.score) score = numa_score(t, s, m, p, NP, aff, node_req_cpu, node_req_mem, node_alloc_cpu, node_alloc_mem);
+  return true;
+}
+
+}  // namespace kg

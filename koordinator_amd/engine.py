@@ -91,6 +91,12 @@ class Engine:
         node_idx = np.ascontiguousarray(node_idx, dtype=np.int32)
         check(self.lib, self.lib.kg_pods_remove(self.h, ptr(pods), ptr(node_idx), len(pods)))
 
+    def upsert_numa(self, node_numa: np.ndarray, idx=None):
+        """NodeNUMAResource state (TopologyOptions + NodeAllocation) of nodes `idx` (kg_nodes_numa_upsert)."""
+        node_numa = np.ascontiguousarray(node_numa, dtype=abi.NODE_NUMA_DTYPE)
+        idx = self._idx(idx, len(node_numa))
+        check(self.lib, self.lib.kg_nodes_numa_upsert(self.h, ptr(node_numa), ptr(idx), len(node_numa)))
+
     # -- hot path -----------------------------------------------------------------------------------------
     def schedule(self, pods: np.ndarray):
         """Sequential FIFO scheduling with assume; returns (node_idx[-1 = unschedulable], total_score, stats)."""
@@ -127,6 +133,22 @@ class Engine:
         check(self.lib, self.lib.kg_pods_evaluate(self.h, ptr(pod), ptr(rej), ptr(fit), ptr(la)))
         return rej, fit, la
 
+    def evaluate_numa(self, pod: np.ndarray):
+        """NodeNUMAResource alone on every node: (passes Filter, Score, stored affinity mask or -1 for nil)."""
+        pod = np.ascontiguousarray(np.asarray(pod, dtype=abi.POD_DTYPE).reshape(1))
+        n = self.num_nodes
+        ok = np.zeros(n, dtype=np.int32)
+        sc = np.zeros(n, dtype=np.int64)
+        af = np.zeros(n, dtype=np.int64)
+        check(self.lib, self.lib.kg_pods_evaluate_numa(self.h, ptr(pod), ptr(ok), ptr(sc), ptr(af)))
+        return ok, sc, af
+
+    def fetch_cpusets(self, first: int, count: int) -> np.ndarray:
+        """uint64[count, 4]: the cpuset NodeNUMAResource Reserve allocated to each staged pod (empty = none)."""
+        out = np.zeros((count, abi.MAX_CPUS // 64), dtype=np.uint64)
+        check(self.lib, self.lib.kg_results_fetch_cpusets(self.h, int(first), int(count), ptr(out)))
+        return out
+
     # -- introspection -----------------------------------------------------------------------------------
     @property
     def num_nodes(self) -> int:
@@ -139,6 +161,15 @@ class Engine:
         out = {k: np.zeros(n, dtype=np.int64) for k in names}
         check(self.lib, self.lib.kg_nodes_read_state(self.h, *[ptr(out[k]) for k in names]))
         return out
+
+    def read_numa(self):
+        """(allocated cpus uint64[n,4], per-NUMA allocated cpu int64[n,4], memory int64[n,4]) from the device."""
+        n = self.num_nodes
+        alloc = np.zeros((n, abi.MAX_CPUS // 64), dtype=np.uint64)
+        cpu = np.zeros((n, abi.MAX_NUMA), dtype=np.int64)
+        mem = np.zeros((n, abi.MAX_NUMA), dtype=np.int64)
+        check(self.lib, self.lib.kg_nodes_read_numa(self.h, ptr(alloc), ptr(cpu), ptr(mem)))
+        return alloc, cpu, mem
 
     def bench_kernel(self, which: int, iters: int):
         ms = ctypes.c_double()

@@ -121,3 +121,117 @@ def load_into(engine, cluster: Cluster):
     engine.update_metrics(cluster.metrics, cluster.now_ns)
     if len(cluster.existing_pods):
         engine.add_pods(cluster.existing_pods, cluster.existing_node)
+
+
+# ---- config C4: NodeNUMAResource cpuset / NUMA topology (2-socket 256-cpu nodes, LSR/LSE pods) --------------
+def make_numa_cluster(n_nodes: int, seed: int = BASE_SEED + 4) -> tuple:
+    """(Cluster, kg_node_numa[n]) for config C4.  Every node: 2 sockets, 256 cpus (SMT-2) in buildCPUTopology
+    numbering — 80 % as 1 NUMA node per socket × 64 cores, 20 % as 2 NUMA nodes per socket × 32 cores — with
+    1 TiB of memory split evenly over the NUMA zones.  NodeAllocation: 0–40 % of the cores held by bound
+    cpuset pods (whole cores at random positions) + 0–40 % of each zone's memory; 20 % of nodes reserve cpus
+    0-1.  NUMA policy none 50 % / BestEffort 20 % / Restricted 15 % / SingleNUMANode 15 %; node cpu-bind
+    policy FullPCPUsOnly 10 % / SpreadByPCPUs 5 %; NUMA allocate strategy label Least 10 % / Most 10 %.
+    Bound pods also count in NodeInfo.Requested (plus 0–10 % non-cpuset cpu).  NodeMetric as make_cluster."""
+    rng = np.random.default_rng(seed)
+    n = n_nodes
+    nodes = np.zeros(n, dtype=abi.NODE_DTYPE)
+    nodes["allocatable"][:, abi.RES_CPU] = 256_000
+    nodes["allocatable"][:, abi.RES_MEMORY] = 1024 * GI
+    nodes["allowed_pods"] = 250
+    nodes["flags"] = abi.NODE_VALID
+    nodes["custom_usage_thresholds"] = -1
+    nodes["custom_prod_usage_thresholds"] = -1
+    numa = np.zeros(n, dtype=abi.NODE_NUMA_DTYPE)
+    four = rng.random(n) < 0.2
+    numa["has_topology"] = 1
+    numa["sockets"] = 2
+    numa["nodes_per_socket"] = np.where(four, 2, 1)
+    numa["cores_per_node"] = np.where(four, 32, 64)
+    numa["cpus_per_core"] = 2
+    u = rng.random(n)
+    numa["numa_policy"] = np.select([u < 0.5, u < 0.7, u < 0.85], [abi.NUMA_POLICY[""], abi.NUMA_POLICY["BestEffort"],
+                                    abi.NUMA_POLICY["Restricted"]], abi.NUMA_POLICY["SingleNUMANode"])
+    u = rng.random(n)
+    numa["node_cpu_bind_policy"] = np.select([u < 0.10, u < 0.15], [abi.NODE_BIND["FullPCPUsOnly"],
+                                             abi.NODE_BIND["SpreadByPCPUs"]], abi.NODE_BIND[""])
+    u = rng.random(n)
+    numa["numa_allocate_strategy"] = np.select([u < 0.1, u < 0.2], [abi.STRATEGY["LeastAllocated"],
+                                               abi.STRATEGY["MostAllocated"]], -1)
+    zones = np.where(four, 4, 2)
+    numa["num_numa"] = zones
+    req_cpu = np.zeros(n, dtype=np.int64)
+    req_mem = np.zeros(n, dtype=np.int64)
+    for i in range(n):
+        z = int(zones[i])
+        zmem = 1024 * GI // z
+        numa["numa_cpu"][i, :z] = 256_000 // z
+        numa["numa_mem"][i, :z] = zmem
+        held = rng.random(128) < rng.random() * 0.4        # cores held by bound cpuset pods
+        cpus = np.flatnonzero(np.repeat(held, 2))
+        words = np.zeros(4, dtype=np.uint64)
+        for c in cpus:
+            words[c // 64] |= np.uint64(1) << np.uint64(c % 64)
+        numa["allocated_cpus"][i] = words
+        per_zone = np.bincount(cpus // (256 // z), minlength=z)[:z] * 1000
+        numa["numa_alloc_cpu"][i, :z] = per_zone
+        zm = (np.floor(rng.random(z) * 0.4 * zmem / MI).astype(np.int64)) * MI
+        numa["numa_alloc_mem"][i, :z] = zm
+        if rng.random() < 0.2:
+            numa["reserved_cpus"][i, 0] = np.uint64(3) if not (int(words[0]) & 3) else np.uint64(0)
+        req_cpu[i] = int(per_zone.sum()) + int(rng.random() * 0.1 * 256_000)
+        req_mem[i] = int(zm.sum())
+    ex = np.zeros(n, dtype=abi.POD_DTYPE)
+    ex["requests"][:, abi.RES_CPU] = req_cpu
+    ex["requests"][:, abi.RES_MEMORY] = req_mem
+    ex["limits"] = ex["requests"]
+    ex["nonzero_requests"][:, 0] = np.maximum(req_cpu, 100)
+    ex["nonzero_requests"][:, 1] = np.maximum(req_mem, 200 * MI)
+    ex["priority_class"] = abi.PRIO_PROD
+    keep = (req_cpu > 0) | (req_mem > 0)
+    now = T0_NS + 10 * 10**9
+    metrics = np.zeros(n, dtype=abi.METRIC_DTYPE)
+    has = rng.random(n) < 0.95
+    metrics["present"] = has
+    metrics["has_update_time"] = has
+    metrics["has_node_metric"] = has
+    metrics["update_time_unix_nano"] = np.where(has, T0_NS, 0)
+    metrics["node_usage"][:, abi.RES_CPU] = np.where(has, np.floor(rng.random(n) * 0.6 * 256_000), 0).astype(np.int64)
+    metrics["node_usage"][:, abi.RES_MEMORY] = (np.where(has, np.floor(rng.random(n) * 0.9 * 1024 * GI / MI), 0)
+                                                .astype(np.int64) * MI)
+    metrics["node_usage_present"][:, abi.RES_CPU] = has
+    metrics["node_usage_present"][:, abi.RES_MEMORY] = has
+    cluster = Cluster(nodes, metrics, ex[keep], np.flatnonzero(keep).astype(np.int32), now)
+    return cluster, numa
+
+
+def make_numa_pods(n_pods: int, seed: int = BASE_SEED + 5) -> np.ndarray:
+    """Config C4 queue: 60 % LSR and 10 % LSE koord-prod pods with whole-core cpu requests {1,2,3,4,8,16} (cpu
+    bind: required FullPCPUs 20 %, preferred SpreadByPCPUs 20 %, else the default FullPCPUs), 25 % LS koord-prod
+    and 4 % BE koord-batch pods with fractional cpu, 1 % zero-request pods; memory 256Mi–32Gi."""
+    rng = np.random.default_rng(seed)
+    p = np.zeros(n_pods, dtype=abi.POD_DTYPE)
+    u = rng.random(n_pods)
+    cpuset = u < 0.7
+    cores = rng.choice(np.array([1, 2, 3, 4, 8, 16], dtype=np.int64), n_pods)
+    frac = rng.choice(np.array([250, 500, 1500, 2000, 4000], dtype=np.int64), n_pods)
+    cpu = np.where(cpuset, cores * 1000, frac)
+    mem = rng.choice(np.array([256, 1024, 4096, 8192, 16384, 32768], dtype=np.int64), n_pods) * MI
+    zero = (u >= 0.99)
+    cpu[zero] = 0
+    mem[zero] = 0
+    p["requests"][:, abi.RES_CPU] = cpu
+    p["requests"][:, abi.RES_MEMORY] = mem
+    p["limits"] = p["requests"]
+    p["nonzero_requests"][:, 0] = np.where(cpu > 0, cpu, 100)
+    p["nonzero_requests"][:, 1] = np.where(mem > 0, mem, 200 * MI)
+    p["priority_class"] = np.where((u >= 0.95) & (u < 0.99), abi.PRIO_BATCH, abi.PRIO_PROD)
+    p["qos"] = np.select([u < 0.6, u < 0.7, u < 0.95], [abi.QOS["LSR"], abi.QOS["LSE"], abi.QOS["LS"]], abi.QOS["BE"])
+    b = rng.random(n_pods)
+    p["required_cpu_bind_policy"] = np.where(cpuset & (b < 0.2), abi.BIND["FullPCPUs"], abi.BIND[""])
+    p["preferred_cpu_bind_policy"] = np.where(cpuset & (b >= 0.2) & (b < 0.4), abi.BIND["SpreadByPCPUs"], abi.BIND[""])
+    return p
+
+
+def load_numa_into(engine, cluster: Cluster, numa: np.ndarray):
+    load_into(engine, cluster)
+    engine.upsert_numa(numa)

@@ -316,7 +316,7 @@ static void insertion_sort_len(list_t* g, int n, int desc) { /* stable (sort.Sli
 /* takeCPUs (:87-232).  0 and the set, or -1 ("not enough cpus" / "failed to allocate cpus"). */
 int or_take_cpus(const or_topology* t, or_cpuset available, int needed, int bind_policy, int strategy,
                  or_cpuset* out) {
-  static list_t groups[KG_MAX_CPUS], unsat[KG_MAX_CPUS];
+  static _Thread_local list_t groups[KG_MAX_CPUS], unsat[KG_MAX_CPUS]; /* per scheduling thread */
   acc_t a;
   a.t = t;
   a.allocatable = cs_and(available, t->all);

@@ -350,12 +350,13 @@ static void run_phase(sched_ctx* c, int phase) {
 int or_schedule(const kg_config* cfg, int64_t n_nodes, const kg_node* nodes, const kg_node_metric* metrics,
                 or_node_state* st, int64_t n_pods, const kg_pod* pods, int64_t now, int n_threads,
                 int32_t* out_node, int64_t* out_score) {
-  return or_schedule_numa(cfg, n_nodes, nodes, metrics, st, NULL, n_pods, pods, now, n_threads, out_node, out_score);
+  return or_schedule_numa(cfg, n_nodes, nodes, metrics, st, NULL, n_pods, pods, now, n_threads, out_node, out_score,
+                          NULL);
 }
 
 int or_schedule_numa(const kg_config* cfg, int64_t n_nodes, const kg_node* nodes, const kg_node_metric* metrics,
                      or_node_state* st, void* numa_states, int64_t n_pods, const kg_pod* pods, int64_t now,
-                     int n_threads, int32_t* out_node, int64_t* out_score) {
+                     int n_threads, int32_t* out_node, int64_t* out_score, uint64_t* out_cpus) {
   or_numa_node* numa = (or_numa_node*)numa_states;
   sched_ctx c;
   memset(&c, 0, sizeof(c));
@@ -393,10 +394,13 @@ int or_schedule_numa(const kg_config* cfg, int64_t n_nodes, const kg_node* nodes
     if (rc) break;
     /* Reserve: NodeNUMAResource allocates the cpuset / NUMA resources; a failure un-assumes the pod
      * (RunReservePluginsUnreserve + ForgetPod): it is not placed this cycle */
+    or_cpuset cpus;
+    memset(&cpus, 0, sizeof(cpus));
     if (best >= 0 && c.numa) {
-      or_cpuset cpus;
       if (or_numa_reserve(cfg, &c.numa[best], &c.numa_pod, &c.affinity[best], &cpus) != 0) best = -1;
     }
+    if (out_cpus)
+      for (int w = 0; w < OR_CPUSET_WORDS; w++) out_cpus[p * OR_CPUSET_WORDS + w] = cpus.w[w];
     out_node[p] = (int32_t)best;
     out_score[p] = best >= 0 ? best_score : 0;
     if (best >= 0) or_apply_pod(cfg, &st[best], &pods[p], +1); /* assume + Reserve */

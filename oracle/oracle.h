@@ -69,10 +69,11 @@ int or_node_keys(const kg_config* cfg, const kg_node* nodes, const kg_node_metri
                  const or_node_state* st, const kg_pod* pod, int64_t now_unix_nano, int64_t lo, int64_t hi,
                  uint64_t* out_keys);
 
-/* or_schedule with the NodeNUMAResource plugin: `numa` = per-node state (numa.h), updated by Reserve. */
+/* or_schedule with the NodeNUMAResource plugin: `numa` = per-node state (numa.h), updated by Reserve;
+ * out_cpus (nullable) = the cpuset Reserve allocated to each pod, KG_MAX_CPUS/64 words per pod. */
 int or_schedule_numa(const kg_config* cfg, int64_t n_nodes, const kg_node* nodes, const kg_node_metric* metrics,
                      or_node_state* st, void* numa, int64_t n_pods, const kg_pod* pods, int64_t now_unix_nano,
-                     int n_threads, int32_t* out_node, int64_t* out_score);
+                     int n_threads, int32_t* out_node, int64_t* out_score, uint64_t* out_cpus);
 
 /* Builds node states from pre-existing assigned pods (informer adds). */
 void or_states_init(int64_t n_nodes, or_node_state* st);

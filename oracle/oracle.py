@@ -59,7 +59,7 @@ def lib():
         L.or_schedule.restype = i
         L.or_node_keys.argtypes = [vp, vp, vp, vp, vp, i64, i64, i64, vp]
         L.or_node_keys.restype = i
-        L.or_schedule_numa.argtypes = [vp, i64, vp, vp, vp, vp, i64, vp, i64, i, vp, vp]
+        L.or_schedule_numa.argtypes = [vp, i64, vp, vp, vp, vp, i64, vp, i64, i, vp, vp, vp]
         L.or_schedule_numa.restype = i
         L.or_numa_state_size.restype = i64
         L.or_numa_states_init.argtypes = [vp, i64, vp]
@@ -167,15 +167,19 @@ def numa_state_read(buf: np.ndarray, n: int):
     return alloc, cpu, mem
 
 
-def schedule_numa(cfg, nodes, metrics, st, numa_buf, pods, now_ns: int, n_threads: int = 1):
-    """or_schedule with the NodeNUMAResource plugin; mutates `st` and `numa_buf`."""
+def schedule_numa(cfg, nodes, metrics, st, numa_buf, pods, now_ns: int, n_threads: int = 1, with_cpusets=False):
+    """or_schedule with the NodeNUMAResource plugin; mutates `st` and `numa_buf`.  Returns (node, score) or,
+    with_cpusets, (node, score, uint64[n_pods, 4] cpuset Reserve allocated to each pod)."""
     pods = np.ascontiguousarray(pods, dtype=abi.POD_DTYPE)
     out_node = np.empty(len(pods), dtype=np.int32)
     out_score = np.empty(len(pods), dtype=np.int64)
+    cpus = np.zeros((max(len(pods), 1), abi.MAX_CPUS // 64), dtype=np.uint64)
     rc = lib().or_schedule_numa(p(cfg), len(nodes), p(nodes), p(metrics), p(st), p(numa_buf), len(pods), p(pods),
-                                now_ns, n_threads, p(out_node), p(out_score))
+                                now_ns, n_threads, p(out_node), p(out_score), p(cpus))
     if rc != 0:
         raise RuntimeError(f"oracle or_schedule_numa failed: {rc}")
+    if with_cpusets:
+        return out_node, out_score, cpus[:len(pods)]
     return out_node, out_score
 
 
