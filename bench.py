@@ -35,8 +35,11 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--nodes", type=int, default=100_000)
-    ap.add_argument("--pods-per-step", type=int, default=100_000)
+    ap.add_argument("--workload", choices=("c3", "c4"), default="c3",
+                    help="c3: Fit+LoadAware at 100k nodes (the BASELINE metric); c4: + NodeNUMAResource cpuset/NUMA "
+                         "on 2-socket 256-cpu nodes")
+    ap.add_argument("--nodes", type=int, default=None, help="default 100k (c3) / 10k (c4)")
+    ap.add_argument("--pods-per-step", type=int, default=None, help="default 100k (c3) / 10k (c4)")
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--pods-per-wave", type=int, default=8)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU baseline sample")
@@ -91,18 +94,26 @@ class Dist:
             self.dist.destroy_process_group()
 
 
-def cpu_baseline(cfg, cluster, pods, budget_s, threads):
-    """Oracle (C restatement of the same Go algorithm, oracle/oracle.c) on this host, bounded sample."""
+def cpu_baseline(cfg, cluster, pods, budget_s, threads, numa=None):
+    """Oracle (C restatement of the same Go algorithm, oracle/oracle.c [+ numa.c]) on this host, bounded sample."""
     from oracle import oracle
     st = oracle.states(cluster.n)
     oracle.add_pods(cfg, st, cluster.existing_pods, cluster.existing_node)
+    buf = oracle.numa_states(numa) if numa is not None else None
+
+    def run(p):
+        if buf is None:
+            oracle.schedule(cfg, cluster.nodes, cluster.metrics, st, p, cluster.now_ns, threads)
+        else:
+            oracle.schedule_numa(cfg, cluster.nodes, cluster.metrics, st, buf, p, cluster.now_ns, threads)
+
     probe = 64
     t0 = time.perf_counter()
-    oracle.schedule(cfg, cluster.nodes, cluster.metrics, st, pods[:probe], cluster.now_ns, threads)
+    run(pods[:probe])
     per_pod = (time.perf_counter() - t0) / probe
     m = int(min(len(pods) - probe, max(probe, budget_s / max(per_pod, 1e-9))))
     t0 = time.perf_counter()
-    oracle.schedule(cfg, cluster.nodes, cluster.metrics, st, pods[probe:probe + m], cluster.now_ns, threads)
+    run(pods[probe:probe + m])
     dt = time.perf_counter() - t0
     return m, dt
 
@@ -130,20 +141,37 @@ def main():
     nccl_id = None
     if d.world > 1:
         nccl_id = d.bcast_bytes(nccl_unique_id() if d.rank == 0 else None)
-    cfg = framework.build_config(batch_pods=args.batch, pods_per_wave=args.pods_per_wave, device_id=d.local_rank)
-    seed = synth.BASE_SEED + 3
-    cluster = synth.make_cluster(args.nodes, seed=seed)
+    c4 = args.workload == "c4"
+    args.nodes = args.nodes or (10_000 if c4 else 100_000)
+    args.pods_per_step = args.pods_per_step or (10_000 if c4 else 100_000)
+    F = framework
+    profile = (F.Profile(filter=(F.NODE_RESOURCES_FIT, F.LOAD_AWARE, F.NODE_NUMA_RESOURCE),
+                         score={F.NODE_RESOURCES_FIT: 1, F.LOAD_AWARE: 1, F.NODE_NUMA_RESOURCE: 1}) if c4 else None)
+    cfg = framework.build_config(batch_pods=args.batch, pods_per_wave=args.pods_per_wave, device_id=d.local_rank,
+                                 profile=profile)
+    numa = None
+    if c4:
+        seed = synth.BASE_SEED + 4
+        cluster, numa = synth.make_numa_cluster(args.nodes, seed=seed)
+        make_pods = synth.make_numa_pods
+    else:
+        seed = synth.BASE_SEED + 3
+        cluster = synth.make_cluster(args.nodes, seed=seed)
+        make_pods = synth.make_pods
     total = args.steps * args.pods_per_step
-    pods = synth.make_pods(total, seed=seed + 1)
+    pods = make_pods(total, seed=seed + 1)
 
     def engine():
         e = Engine(cfg, cluster.n, rank=d.rank, n_ranks=d.world, nccl_id=nccl_id)
-        synth.load_into(e, cluster)
+        if c4:
+            synth.load_numa_into(e, cluster, numa)
+        else:
+            synth.load_into(e, cluster)
         return e
 
     # warmup on a throw-away engine (same cluster, different pods): code objects, caches, RCCL channels
     if args.warmup > 0:
-        wp = synth.make_pods(args.warmup * min(args.pods_per_step, 20_000), seed=seed + 7)
+        wp = make_pods(args.warmup * min(args.pods_per_step, 20_000), seed=seed + 7)
         with engine() as ew:
             ew.stage(wp)
             ew.schedule_staged(0, len(wp))
@@ -184,25 +212,33 @@ def main():
     check = None
     if args.check and d.rank == 0:
         from oracle import oracle
-        on, _, _ = oracle.schedule_cluster(cfg, cluster, pods[: args.check], n_threads=args.cpu_threads)
+        if c4:
+            st = oracle.states(cluster.n)
+            oracle.add_pods(cfg, st, cluster.existing_pods, cluster.existing_node)
+            on, _ = oracle.schedule_numa(cfg, cluster.nodes, cluster.metrics, st, oracle.numa_states(numa),
+                                         pods[: args.check], cluster.now_ns, args.cpu_threads)
+        else:
+            on, _, _ = oracle.schedule_cluster(cfg, cluster, pods[: args.check], n_threads=args.cpu_threads)
         check = bool(np.array_equal(on, node_idx[: args.check]))
 
     cpu = None
     if d.rank == 0 and d.world == 1 and not args.no_cpu_baseline:
         print("[bench] cpu baseline sample", file=sys.stderr, flush=True)
-        m, dt = cpu_baseline(cfg, cluster, pods, args.cpu_seconds, args.cpu_threads)
+        m, dt = cpu_baseline(cfg, cluster, pods, args.cpu_seconds, args.cpu_threads, numa)
         cpu = {"value": m / dt, "unit": "pods/s", "cores": args.cpu_threads, "kind": "port",
                "sample": f"first {m} pods of the same queue after a 64-pod probe, {cluster.n} nodes, "
-                         f"oracle/oracle.c or_schedule, {args.cpu_threads} threads (Parallelizer chunking), "
+                         f"oracle/oracle.c {'or_schedule_numa' if c4 else 'or_schedule'}, {args.cpu_threads} threads "
+                         f"(Parallelizer chunking), "
                          f"host nproc={os.cpu_count()}",
                "node_evals_per_sec": m * cluster.n / dt}
 
     traffic, traffic_src = (pmc_traffic(args.traffic_file, dom, cluster.n, args.batch, args.pods_per_wave)
-                            if d.world == 1 else (None, None))
+                            if d.world == 1 and not c4 else (None, None))
     if d.rank == 0:
         pods_s = total / elapsed
         out = {
-            "metric": "pods scheduled/sec at 100k nodes (node-evals/sec alongside)",
+            "metric": ("pods scheduled/sec, NodeNUMAResource cpuset/NUMA profile (node-evals/sec alongside)" if c4
+                       else "pods scheduled/sec at 100k nodes (node-evals/sec alongside)"),
             "value": pods_s,
             "unit": "pods/s",
             "n_gpus": d.world,
@@ -214,8 +250,10 @@ def main():
             "vs_baseline": None,
             "dtype": "int64",
             "data": "synthetic (SURVEY §8d generator, seed %d)" % seed,
-            "config": {"workload": "C3 cluster: %d nodes, %d-pod FIFO queue, NodeResourcesFit+LoadAwareScheduling, "
-                                   "%d pods per step" % (cluster.n, total, args.pods_per_step),
+            "config": {"workload": ("C4 cluster: %d 2-socket 256-cpu nodes, %d-pod FIFO queue (70%% cpuset LSR/LSE), "
+                                    "NodeResourcesFit+LoadAwareScheduling+NodeNUMAResource, %d pods per step" if c4 else
+                                    "C3 cluster: %d nodes, %d-pod FIFO queue, NodeResourcesFit+LoadAwareScheduling, "
+                                    "%d pods per step") % (cluster.n, total, args.pods_per_step),
                        "nodes": cluster.n, "pods": total, "batch_pods": args.batch,
                        "parallelism": "node-sharded x%d (replicated table, RCCL all-gather)" % d.world},
             "node_evals_per_sec": pods_s * cluster.n,

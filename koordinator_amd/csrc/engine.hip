@@ -776,17 +776,21 @@ struct NumaTable {
 };
 
 // Reference-shaped Fit + LoadAware (eval_node) + NodeNUMAResource Filter/Score of one node for one pod.
-__device__ __forceinline__ bool eval_node_numa(const Row& r, const NumaStatic& ns, const NumaMut& nm, const DevPod& p,
-                                               const NumaPod& np, const EvalParams& P, const NumaParams& NP,
-                                               int64_t& total) {
+__device__ __forceinline__ bool eval_node_numa(const Row& r, const NumaView& nv, const DevPod& p, const NumaPod& np,
+                                               const EvalParams& P, const NumaParams& NP, int64_t& total) {
   int64_t t = 0;
   if (!eval_node(r, p, P, t)) return false;
   int64_t sc = 0;
   NumaHint aff;
-  if (!numa_eval(ns, nm, np, NP, r.req_cpu, r.req_mem, r.alloc_cpu, r.alloc_mem, sc, aff)) return false;
+  if (!numa_eval(nv, np, NP, r.req_cpu, r.req_mem, r.alloc_cpu, r.alloc_mem, sc, aff)) return false;
   total = t + (NP.score ? sc * NP.weight : 0);
   return true;
 }
+
+// Wide pass of a NUMA round.  Same tiles, pod groups and candidate lists as eval_round; each lane takes its
+// kNPT nodes one at a time (Row + NumaView hoisted out of the pod loop) and parks the per-pod values in LDS,
+// then the per-pod top-kR selects run as in eval_round.  pods_per_wave ≤ kNumaPpw (host clamps).
+constexpr int kNumaPpw = 8;
 
 __global__ __launch_bounds__(kWave* kEvalWaves) void eval_round_numa(DevTable T, NumaTable NT,
                                                                        const DevPod* __restrict__ pods,
@@ -796,6 +800,7 @@ __global__ __launch_bounds__(kWave* kEvalWaves) void eval_round_numa(DevTable T,
                                                                        int nt_local, EvalParams P, NumaParams NP,
                                                                        uint64_t* __restrict__ lists,
                                                                        const int32_t* __restrict__ poison) {
+  __shared__ uint32_t s_v[kEvalWaves][kNumaPpw][kNPT][kWave];
   if (*poison) return;
   const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
   const int n_pg = (nb + pods_per_wave - 1) / pods_per_wave;
@@ -806,26 +811,47 @@ __global__ __launch_bounds__(kWave* kEvalWaves) void eval_round_numa(DevTable T,
   if (tile >= nt_local || p0 >= nb) return;
   const int p1 = (p0 + pods_per_wave) < nb ? (p0 + pods_per_wave) : nb;
   const int vbits = P.score_bits + 1;
+  for (int j = 0; j < kNPT; ++j) {
+    int64_t local = (int64_t)tile * kTile + j * kWave + lane;
+    asm volatile("" : "+v"(local));
+    const bool in = local < n_local;
+    // phase 1: Fit + LoadAware (the Row is dead afterwards but for the four NodeInfo terms NUMA reads)
+    int64_t rq_c = 0, rq_m = 0, al_c = 0, al_m = 0;
+    {
+      Row row;
+      row.flags = 0;
+      if (in) row = load_row(T, node_base + local);
+      for (int pi = p0; pi < p1; ++pi) {
+        const DevPod p = pods[first + pi];
+        int64_t t = 0;
+        s_v[wave][pi - p0][j][lane] = (in && eval_node(row, p, P, t)) ? (uint32_t)t + 1u : 0u;
+      }
+      rq_c = row.req_cpu;
+      rq_m = row.req_mem;
+      al_c = row.alloc_cpu;
+      al_m = row.alloc_mem;
+    }
+    // phase 2: NodeNUMAResource on the pods Fit/LoadAware kept
+    if (in) {
+      const NumaView nv = make_view(NT.s + node_base + local, NT.m + node_base + local, NP);
+      for (int pi = p0; pi < p1; ++pi) {
+        const uint32_t v0 = s_v[wave][pi - p0][j][lane];
+        if (v0 == 0) continue;
+        const NumaPod np = npods[first + pi];
+        int64_t sc = 0;
+        NumaHint aff;
+        const bool ok = numa_eval(nv, np, NP, rq_c, rq_m, al_c, al_m, sc, aff);
+        s_v[wave][pi - p0][j][lane] = ok ? v0 + (uint32_t)(NP.score ? sc * NP.weight : 0) : 0u;
+      }
+    }
+  }
   uint32_t gidx[kNPT];
 #pragma unroll
   for (int j = 0; j < kNPT; ++j) gidx[j] = (uint32_t)(node_base + (int64_t)tile * kTile + j * kWave + lane);
   for (int pi = p0; pi < p1; ++pi) {
-    const DevPod p = pods[first + pi];
-    const NumaPod np = npods[first + pi];
     uint32_t v[kNPT];
 #pragma unroll
-    for (int j = 0; j < kNPT; ++j) {
-      int64_t local = (int64_t)tile * kTile + j * kWave + lane;
-      asm volatile("" : "+v"(local));
-      v[j] = 0;
-      if (local < n_local) {
-        const int64_t i = node_base + local;
-        const NumaStatic ns = NT.s[i];
-        const NumaMut nm = NT.m[i];
-        int64_t t = 0;
-        if (eval_node_numa(load_row(T, i), ns, nm, p, np, P, NP, t)) v[j] = (uint32_t)t + 1u;
-      }
-    }
+    for (int j = 0; j < kNPT; ++j) v[j] = s_v[wave][pi - p0][j][lane];
     select_write(v, gidx, vbits, lists + ((size_t)pi * nt_local + tile) * kR, lane);
   }
 }
@@ -873,6 +899,7 @@ __global__ __launch_bounds__(kWave) void resolve_round_numa(DevTable T, NumaTabl
   uint32_t midx = 0xFFFFFFFFu;
   Row mrow;
   mrow.flags = 0;
+  NumaView mv;
   bool touched = false;
   uint64_t my_out = 0;
   int nM = 0, consumed = 0;
@@ -890,7 +917,7 @@ __global__ __launch_bounds__(kWave) void resolve_round_numa(DevTable T, NumaTabl
       uint64_t mk = 0;
       if (lane < nM) {
         int64_t t = 0;
-        if (eval_node_numa(mrow, s_ns[lane], s_nm[lane], p, np, P, NP, t)) mk = make_key(t, midx);
+        if (eval_node_numa(mrow, mv, p, np, P, NP, t)) mk = make_key(t, midx);
       }
       const uint64_t mbest = wave_max_key(mk);
       best = mbest > best ? mbest : best;
@@ -908,8 +935,11 @@ __global__ __launch_bounds__(kWave) void resolve_round_numa(DevTable T, NumaTabl
       if (lane == owner) {
         midx = w;
         mrow = load_row(T, w);
-        s_ns[owner] = NT.s[w];
-        s_nm[owner] = NT.m[w];
+        const NumaStatic ns = NT.s[w];
+        const NumaMut nm = NT.m[w];
+        s_ns[owner] = ns;
+        s_nm[owner] = nm;
+        mv = make_view(&s_ns[owner], &s_nm[owner], NP);
       }
       if (lane == 0) bitmap[w >> 5] |= 1u << (w & 31);
       ++nM;
@@ -917,14 +947,15 @@ __global__ __launch_bounds__(kWave) void resolve_round_numa(DevTable T, NumaTabl
     __syncthreads();
     int placed = 0;
     if (lane == owner) {  // Reserve with the affinity Filter stores (recomputed on the same state)
-      const Topo tp = make_topo(s_ns[lane]);
       NumaHint aff{0, 1, 0, 0};
-      if (NP.filter) (void)numa_filter(tp, s_ns[lane], s_nm[lane], np, NP, aff);
+      if (NP.filter) (void)numa_filter(mv, np, NP, aff);
       CpuSet cpus;
+      const NumaStatic ns = s_ns[lane];
       NumaMut nm = s_nm[lane];
-      if (numa_reserve(tp, s_ns[lane], nm, np, NP, aff, cpus)) {
+      if (numa_reserve(ns, nm, mv, np, aff, cpus)) {
         placed = 1;
         s_nm[lane] = nm;
+        mv = make_view(&s_ns[lane], &s_nm[lane], NP);
         mrow.req_cpu += p.req_cpu;  // assume: NodeInfo.AddPod + LoadAware assign cache
         mrow.req_mem += p.req_mem;
         mrow.nz_cpu += p.nz_cpu;
@@ -972,7 +1003,8 @@ __global__ void evaluate_pod_numa(DevTable T, NumaTable NT, const DevPod* __rest
   q.score = 1;
   int64_t sc = 0;
   NumaHint aff;
-  const bool ok = numa_eval(NT.s[i], NT.m[i], *npod, q, r.req_cpu, r.req_mem, r.alloc_cpu, r.alloc_mem, sc, aff);
+  const NumaView nv = make_view(NT.s + i, NT.m + i, q);
+  const bool ok = numa_eval(nv, *npod, q, r.req_cpu, r.req_mem, r.alloc_cpu, r.alloc_mem, sc, aff);
   pass[i] = ok ? 1 : 0;
   score[i] = ok ? sc : 0;
   affinity[i] = aff.nil ? -1 : (int64_t)aff.mask;
@@ -1504,6 +1536,7 @@ RoundGeom geometry(const kg_engine* e) {
   g.ppw = (int)(e->cfg.pods_per_wave > 0 ? std::min<int64_t>(e->cfg.pods_per_wave, g.B) : 8);
   g.bitmap_words = (int)(((std::max<int64_t>(g.N, 1) + 127) / 128) * 4);  // whole 16-B stores
   g.pipelined = 2 * g.B - 1 <= kWave && e->P.monotone;
+  if (e->numa_on) g.ppw = std::min(g.ppw, kNumaPpw);  // eval_round_numa parks ≤ kNumaPpw pods' values in LDS
   return g;
 }
 
@@ -2266,7 +2299,9 @@ int kg_bench_kernel(kg_engine* e, int which, int iters, double* avg_ms, double* 
   if (algo_bytes) {
     // eval: SURVEY §8(d) per-evaluation bytes (Fit 56 B + LoadAware 20 B = 76 B per node) × pods × nodes,
     //       + the candidate lists written;  merge: lists read + records written;  resolve: records + pods read.
-    if (which == 0) *algo_bytes = nbd * (double)g.n_local * kAlgoBytesPerNode + nbd * g.nt_local * kR * 8.0 + nbd * 96.0;
+    // NUMA profiles add the node's NumaStatic + NumaMut (232 B) to every evaluation
+    const double per_node = kAlgoBytesPerNode + (e->numa_on ? (double)(sizeof(NumaStatic) + sizeof(NumaMut)) : 0.0);
+    if (which == 0) *algo_bytes = nbd * (double)g.n_local * per_node + nbd * g.nt_local * kR * 8.0 + nbd * 96.0;
     else if (which == 1) *algo_bytes = nbd * g.nt_local * kR * 8.0 + nbd * kCandStride * 8.0;
     else *algo_bytes = nbd * kCandStride * 8.0 + nbd * 96.0;
   }

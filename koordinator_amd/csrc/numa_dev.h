@@ -246,7 +246,7 @@ __device__ __forceinline__ CpuSet spread_first_k(const Topo& t, const CpuSet& s,
   return cs_or(first, lowest_k(cs_andnot(s, first), k - nf));
 }
 
-__device__ inline bool take_cpus(const Topo& t, const CpuSet& available, int needed, int bind, int strategy,
+__device__ __noinline__ bool take_cpus(const Topo& t, const CpuSet& available, int needed, int bind, int strategy,
                                  CpuSet& out) {
   Acc a;
   a.t = t;
@@ -461,14 +461,6 @@ __device__ __forceinline__ uint32_t mask_at(int k) {
   return (uint32_t)((order >> (4 * k)) & 15ull);
 }
 
-// getPreferredCPUBindPolicy (plugin.go:556-576); -1: getResourceOptions fails (topology missing / invalid)
-__device__ __forceinline__ int numa_pref_bind(const NumaStatic& s, int preferred) {
-  if (!s.valid) return -1;
-  if (s.node_bind == 2 /*SpreadByPCPUs*/) return 3;
-  if (s.node_bind == 1 /*FullPCPUsOnly*/) return 2;
-  return preferred;
-}
-
 __device__ __forceinline__ int64_t most_requested64(int64_t requested, int64_t capacity) {
   if (capacity == 0) return 0;
   if (requested > capacity) requested = capacity;
@@ -487,7 +479,7 @@ __device__ __forceinline__ int64_t numa_scorer(int strategy, int32_t w_cpu, int3
     s += (strategy == 1 ? most_requested64(req_m + pod_m, alloc_m) : least_requested(req_m + pod_m, alloc_m)) * w_mem;
     ws += w_mem;
   }
-  return ws ? s / ws : 0;
+  return ws ? div_small(s, ws) : 0;
 }
 
 __device__ __forceinline__ CpuSet numa_available_cpus(const Topo& t, const NumaStatic& s, const NumaMut& m) {
@@ -497,8 +489,84 @@ __device__ __forceinline__ CpuSet numa_available_cpus(const Topo& t, const NumaS
   return a;
 }
 
-// One provider list of the topology manager: either a single "don't care" (nil) hint, or hints over the
-// masks of a set of enumeration positions; `empty` = no hint at all
+// ---------------------------------------------------------------------------------------------------------
+// Pod-independent view of one node (recomputed when its NodeAllocation changes): every quantity Filter and
+// Score read, as counts.  Per NUMA node i: the available cpus (getAvailableCPUs ∩ NUMA node i) raw, reduced
+// to whole free cores (filterCPUsByRequiredCPUBindPolicy FullPCPUs) and to one cpu per core (SpreadByPCPUs).
+// Every array is indexed only by unrolled compile-time indices, so the view lives in registers.
+// ---------------------------------------------------------------------------------------------------------
+struct NumaView {
+  int32_t valid, policy, node_bind, cpc, nn, strategy, n_alloc;
+  int32_t cnt[3][kNumaMax];  // [kind: 0 raw, 1 full cores, 2 one per core][NUMA node]
+  int32_t tot[3];
+  int64_t numa_cpu[kNumaMax], numa_mem[kNumaMax], alloc_cpu[kNumaMax], alloc_mem[kNumaMax];
+};
+
+// which count a cpu-bind policy reads (filterCPUsByRequiredCPUBindPolicy only reduces for FullPCPUs / Spread)
+__device__ __forceinline__ int kind_of(int bind) { return bind == 2 ? 1 : (bind == 3 ? 2 : 0); }
+// (value selects laundered as in kernels.h pick(): a select of the three loads must not become a load of a
+// selected address, which would move the whole view to scratch)
+__device__ __forceinline__ int32_t sel3(int kind, int32_t a, int32_t b, int32_t c) {
+  asm("" : "+v"(a), "+v"(b), "+v"(c));
+  return kind == 1 ? b : (kind == 2 ? c : a);
+}
+__device__ __forceinline__ int32_t cnt_at(const NumaView& v, int kind, int i) {
+  return sel3(kind, v.cnt[0][i], v.cnt[1][i], v.cnt[2][i]);
+}
+__device__ __forceinline__ int32_t tot_at(const NumaView& v, int kind) { return sel3(kind, v.tot[0], v.tot[1], v.tot[2]); }
+
+__device__ __forceinline__ NumaView make_view(const NumaStatic* __restrict__ s, const NumaMut* __restrict__ m,
+                                              const NumaParams& NP) {
+  NumaView v;
+  Topo t;
+  t.sockets = s->sockets;
+  t.nps = s->nps;
+  t.cpn = s->cpn;
+  t.cpc = s->cpc > 0 ? s->cpc : 1;
+  t.nodes = t.sockets * t.nps;
+  t.cores = t.nodes * t.cpn;
+  t.cpus = t.cores * t.cpc;
+  v.valid = s->valid;
+  v.policy = s->policy;
+  v.node_bind = s->node_bind;
+  v.cpc = t.cpc;
+  v.nn = s->num_numa;
+  v.strategy = s->strategy >= 0 ? s->strategy : NP.default_alloc_strategy;
+  CpuSet alloc, avail = t.all();
+#pragma unroll
+  for (int w = 0; w < kCpuWords; ++w) {
+    alloc.w[w] = m->allocated[w];
+    avail.w[w] &= ~(alloc.w[w] | s->reserved[w]);
+  }
+  v.n_alloc = cs_count(alloc);
+  const CpuSet full = full_core_cpus(t, avail), spread = first_cpu_per_core(t, avail);
+  v.tot[0] = cs_count(avail);
+  v.tot[1] = cs_count(full);
+  v.tot[2] = cs_count(spread);
+#pragma unroll
+  for (int i = 0; i < kNumaMax; ++i) {
+    const CpuSet nc = t.node_cpus(i);
+    v.cnt[0][i] = cs_count(cs_and(avail, nc));
+    v.cnt[1][i] = cs_count(cs_and(full, nc));
+    v.cnt[2][i] = cs_count(cs_and(spread, nc));
+    v.numa_cpu[i] = s->numa_cpu[i];
+    v.numa_mem[i] = s->numa_mem[i];
+    v.alloc_cpu[i] = m->alloc_cpu[i];
+    v.alloc_mem[i] = m->alloc_mem[i];
+  }
+  return v;
+}
+
+// getPreferredCPUBindPolicy (plugin.go:556-576); -1: getResourceOptions fails (topology missing / invalid)
+__device__ __forceinline__ int numa_pref_bind(const NumaView& v, int preferred) {
+  if (!v.valid) return -1;
+  if (v.node_bind == 2 /*SpreadByPCPUs*/) return 3;
+  if (v.node_bind == 1 /*FullPCPUsOnly*/) return 2;
+  return preferred;
+}
+
+// One provider list of the topology manager: a single "don't care" (nil) hint, or hints over the masks of a
+// set of enumeration positions; `empty` = no hint at all
 struct HintList {
   uint32_t set;  // positions k (mask_at(k)) in enumeration order
   int nil, nil_pref, empty, min_size;
@@ -509,28 +577,31 @@ __device__ __forceinline__ int sc_at(uint64_t lo, uint64_t hi, int k) {
 }
 
 // mergeFilteredHints (policy.go:127-185) over the permutations of ≤ 2 lists (the last varies fastest)
-__device__ inline NumaHint merge_hints(uint32_t def, const HintList* L, int nl, uint64_t sc_lo, uint64_t sc_hi) {
+__device__ __forceinline__ NumaHint merge_hints(uint32_t def, const HintList L0, const HintList L1, int nl,
+                                                uint64_t sc_lo, uint64_t sc_hi) {
   NumaHint best{def, 0, 0, 0};
-  for (int i = 0; i < nl; ++i)
-    if (L[i].empty) return best;
-  const uint32_t s0 = L[0].nil ? 1u : L[0].set;
-  const uint32_t s1 = nl > 1 ? (L[1].nil ? 1u : L[1].set) : 1u;
+  if (L0.empty || (nl > 1 && L1.empty)) return best;
+  const uint32_t s0 = L0.nil ? 1u : L0.set;
+  const uint32_t s1 = nl > 1 ? (L1.nil ? 1u : L1.set) : 1u;
+  const bool nilb = nl > 1 ? L1.nil != 0 : true;
   for (uint32_t a = s0; a; a &= a - 1) {
     const int ka = __builtin_ctz(a);
-    const bool nila = L[0].nil;
-    const uint32_t ma = nila ? def : mask_at(ka);
-    const bool pa = nila ? L[0].nil_pref : __popc(ma) == L[0].min_size;
+    const uint32_t ma = L0.nil ? def : mask_at(ka);
+    const bool pa = L0.nil ? L0.nil_pref != 0 : __popc(ma) == L0.min_size;
+    const int sa = L0.nil ? 0 : sc_at(sc_lo, sc_hi, ka);
     for (uint32_t b = s1; b; b &= b - 1) {
       const int kb = __builtin_ctz(b);
-      const bool nilb = nl > 1 ? L[1].nil : true;
       const uint32_t mb = nilb ? def : mask_at(kb);
-      const bool pb = nl > 1 ? (nilb ? L[1].nil_pref : __popc(mb) == L[1].min_size) : true;
+      const bool pb = nl > 1 ? (nilb ? L1.nil_pref != 0 : __popc(mb) == L1.min_size) : true;
       const uint32_t merged = def & ma & mb;
       if (merged == 0) continue;
       const int preferred = pa && pb;
       int score = 0;
-      if (!nila && ma == merged) score = sc_at(sc_lo, sc_hi, ka);
-      if (nl > 1 && !nilb && mb == merged && sc_at(sc_lo, sc_hi, kb) > score) score = sc_at(sc_lo, sc_hi, kb);
+      if (!L0.nil && ma == merged) score = sa;
+      if (!nilb && mb == merged) {
+        const int sb = sc_at(sc_lo, sc_hi, kb);
+        if (sb > score) score = sb;
+      }
       const int pm = __popc(merged), pbst = __popc(best.mask);
       if (preferred && !best.preferred) {
         best = NumaHint{merged, 0, 1, score};
@@ -548,51 +619,62 @@ __device__ inline NumaHint merge_hints(uint32_t def, const HintList* L, int nl, 
   return best;
 }
 
+__device__ __forceinline__ HintList single_numa_only(HintList L) {
+  // filterSingleNumaHints: "don't care" hints that are preferred, and preferred single-NUMA hints
+  if (L.nil) {
+    if (!L.nil_pref) L.empty = 1;
+    return L;
+  }
+  uint32_t keep = 0;
+  if (L.min_size == 1)
+    for (uint32_t b = L.set; b; b &= b - 1) {
+      const int k = __builtin_ctz(b);
+      if (__popc(mask_at(k)) == 1) keep |= 1u << k;
+    }
+  L.set = keep;
+  if (!keep) L.empty = 1;
+  return L;
+}
+
 // Topology-manager Admit for the NodeNUMAResource provider alone (manager.go:58-100, policy_*.go) with the
 // hints of generateResourceHints (resource_manager.go:418-532).  Returns admit; writes the best hint.
-__device__ inline bool numa_admit(const Topo& t, const NumaStatic& s, const NumaMut& m, const NumaPod& p,
-                                  const NumaParams& NP, NumaHint& best) {
-  const int nn = s.num_numa;
+__device__ __forceinline__ bool numa_admit(const NumaView& v, const NumaPod& p, const NumaParams& NP, NumaHint& best) {
+  const int nn = v.nn;
   const uint32_t def = (1u << nn) - 1u;
-  const int bind = numa_pref_bind(s, p.preferred);
-  HintList L[2];
-  int nl = 0;
+  const int bind = numa_pref_bind(v, p.preferred);
+  HintList L0{0, 1, 1, 0, 0}, L1{0, 1, 1, 0, 0};
+  int nl = 1;
   uint64_t sc_lo = 0, sc_hi = 0;
   const bool req_c = p.req_cpu > 0, req_m = p.req_mem > 0;
-  if (bind < 0 || (!req_c && !req_m)) {
-    L[0] = HintList{0, 1, 1, 0, 0};
-    nl = 1;
-  } else {
+  if (bind >= 0 && (req_c || req_m)) {
     int64_t av_cpu[kNumaMax], av_mem[kNumaMax];
-    const CpuSet avail = numa_available_cpus(t, s, m);
+    const bool trim = p.cpu_bind && p.required != 0;
+    const int kind = kind_of(bind);
+#pragma unroll
     for (int i = 0; i < kNumaMax; ++i) {
-      if (i >= nn) {
-        av_cpu[i] = av_mem[i] = 0;
-        continue;
-      }
-      const int64_t ac = s.numa_cpu[i] - m.alloc_cpu[i], am = s.numa_mem[i] - m.alloc_mem[i];
-      av_cpu[i] = ac > 0 ? ac : 0;
-      av_mem[i] = am > 0 ? am : 0;
-      if (p.cpu_bind && p.required != 0 && av_cpu[i] != 0) {  // trimNUMANodeResources (:140-169)
-        CpuSet in = cs_and(avail, t.node_cpus(i));
-        if ((int64_t)cs_count(in) * 1000 >= av_cpu[i]) in = filter_required(t, in, bind);
-        const int64_t c = (int64_t)cs_count(in) * 1000;
+      const int64_t ac = v.numa_cpu[i] - v.alloc_cpu[i], am = v.numa_mem[i] - v.alloc_mem[i];
+      av_cpu[i] = i < nn && ac > 0 ? ac : 0;
+      av_mem[i] = i < nn && am > 0 ? am : 0;
+      if (trim && av_cpu[i] != 0) {  // trimNUMANodeResources (:140-169)
+        const int64_t raw = (int64_t)v.cnt[0][i] * 1000;
+        const int64_t c = raw >= av_cpu[i] ? (int64_t)cnt_at(v, kind, i) * 1000 : raw;
         if (c < av_cpu[i]) av_cpu[i] = c;
       }
     }
     uint32_t hc = 0, hm = 0;
     int min_c = nn, min_m = nn;
-    const int nmask = (1 << nn) - 1;  // masks of ≤ nn bits: the first (2^nn - 1) positions restricted to def
+#pragma unroll 1
     for (int k = 0; k < 15; ++k) {
       const uint32_t mk = mask_at(k);
       if (mk & ~def) continue;
       int64_t a_c = 0, a_m = 0, tot_c = 0, tot_m = 0;
-      for (int i = 0; i < nn; ++i)
+#pragma unroll
+      for (int i = 0; i < kNumaMax; ++i)
         if ((mk >> i) & 1u) {
           a_c += av_cpu[i];
           a_m += av_mem[i];
-          tot_c += s.numa_cpu[i];
-          tot_m += s.numa_mem[i];
+          tot_c += v.numa_cpu[i];
+          tot_m += v.numa_mem[i];
         }
       const int64_t rq_c = tot_c - a_c > 0 ? tot_c - a_c : 0, rq_m = tot_m - a_m > 0 ? tot_m - a_m : 0;
       const int64_t sc = numa_scorer(NP.numa_strategy, NP.nw_cpu, NP.nw_mem, rq_c, rq_m, tot_c, tot_m, p.req_cpu,
@@ -609,123 +691,97 @@ __device__ inline bool numa_admit(const Topo& t, const NumaStatic& s, const Numa
         if (a_c >= p.req_cpu) hc |= 1u << k;
       }
     }
-    (void)nmask;
     // filterProvidersHints (policy.go:94-125): resources in sorted-name order (cpu, memory); a present but
     // empty list becomes one non-preferred "don't care" hint
-    if (req_c) L[nl++] = hc ? HintList{hc, 0, 0, 0, min_c} : HintList{0, 1, 0, 0, 0};
-    if (req_m) L[nl++] = hm ? HintList{hm, 0, 0, 0, min_m} : HintList{0, 1, 0, 0, 0};
-  }
-  if (s.policy == 3 /*SingleNUMANode*/) {
-    // filterSingleNumaHints: "don't care" hints that are preferred, and preferred single-NUMA hints
-    for (int i = 0; i < nl; ++i) {
-      if (L[i].nil) {
-        if (!L[i].nil_pref) L[i].empty = 1;
-      } else {
-        uint32_t keep = 0;
-        for (uint32_t b = L[i].set; b; b &= b - 1) {
-          const int k = __builtin_ctz(b);
-          if (__popc(mask_at(k)) == 1 && 1 == L[i].min_size) keep |= 1u << k;
-        }
-        L[i].set = keep;
-        if (!keep) L[i].empty = 1;
+    const HintList lc = hc ? HintList{hc, 0, 0, 0, min_c} : HintList{0, 1, 0, 0, 0};
+    const HintList lm = hm ? HintList{hm, 0, 0, 0, min_m} : HintList{0, 1, 0, 0, 0};
+    if (req_c) {
+      L0 = lc;
+      if (req_m) {
+        L1 = lm;
+        nl = 2;
       }
+    } else {
+      L0 = lm;
     }
-    best = merge_hints(def, L, nl, sc_lo, sc_hi);
+  }
+  if (v.policy == 3 /*SingleNUMANode*/) {
+    best = merge_hints(def, single_numa_only(L0), single_numa_only(L1), nl, sc_lo, sc_hi);
     if (!best.nil && best.mask == def) best = NumaHint{0, 1, best.preferred, 0};
     return best.preferred != 0;
   }
-  best = merge_hints(def, L, nl, sc_lo, sc_hi);
-  if (s.policy == 2 /*Restricted*/) return best.preferred != 0;
+  best = merge_hints(def, L0, L1, nl, sc_lo, sc_hi);
+  if (v.policy == 2 /*Restricted*/) return best.preferred != 0;
   return true;  // BestEffort
 }
 
+// allocateResourcesByHint (resource_manager.go:195-250): per NUMA node i (ascending within the hint) the cpu /
+// memory taken; `res` = bit i when NUMA node i got an entry.  False on insufficient NUMA resources.
 struct NumaAlloc {
-  int n;
-  int numa[kNumaMax];
+  uint32_t res;
   int64_t cpu[kNumaMax], mem[kNumaMax];
 };
 
-// allocateResourcesByHint (resource_manager.go:195-250); false on insufficient NUMA resources
-__device__ __forceinline__ bool alloc_by_hint(const NumaStatic& s, const NumaMut& m, const NumaPod& p,
-                                              uint32_t mask, NumaAlloc& res) {
-  res.n = 0;
-  if (s.num_numa == 0) return false;
+__device__ __forceinline__ bool alloc_by_hint(const NumaView& v, const NumaPod& p, uint32_t mask, NumaAlloc& a) {
+  a.res = 0;
+#pragma unroll
+  for (int i = 0; i < kNumaMax; ++i) a.cpu[i] = a.mem[i] = 0;
+  if (v.nn == 0) return false;
   int64_t rq_c = p.req_cpu, rq_m = p.req_mem;
   const bool key_c = p.req_cpu > 0, key_m = p.req_mem > 0;
-  for (int i = 0; i < s.num_numa; ++i) {
-    if (!((mask >> i) & 1u)) continue;
+  bool done = false;
+#pragma unroll
+  for (int i = 0; i < kNumaMax; ++i) {
+    if (done || i >= v.nn || !((mask >> i) & 1u)) continue;
     int64_t ac = 0, am = 0;
     if (key_c) {
-      const int64_t av = s.numa_cpu[i] - m.alloc_cpu[i] > 0 ? s.numa_cpu[i] - m.alloc_cpu[i] : 0;
+      const int64_t av = v.numa_cpu[i] - v.alloc_cpu[i] > 0 ? v.numa_cpu[i] - v.alloc_cpu[i] : 0;
       ac = rq_c < av ? rq_c : av;
       rq_c -= ac;
     }
     if (key_m) {
-      const int64_t av = s.numa_mem[i] - m.alloc_mem[i] > 0 ? s.numa_mem[i] - m.alloc_mem[i] : 0;
+      const int64_t av = v.numa_mem[i] - v.alloc_mem[i] > 0 ? v.numa_mem[i] - v.alloc_mem[i] : 0;
       am = rq_m < av ? rq_m : av;
       rq_m -= am;
     }
     if (ac != 0 || am != 0) {
-      res.numa[res.n] = i;
-      res.cpu[res.n] = ac;
-      res.mem[res.n] = am;
-      ++res.n;
+      a.res |= 1u << i;
+      a.cpu[i] = ac;
+      a.mem[i] = am;
     }
-    if (rq_c == 0 && rq_m == 0) break;
+    if (rq_c == 0 && rq_m == 0) done = true;
   }
   return !((key_c && rq_c != 0) || (key_m && rq_m != 0));
 }
 
-// resourceManager.Allocate (resource_manager.go:171-360).  EXACT=false: feasibility from counts only (the
-// per-NUMA takes of allocateCPUSet never fail and a FullPCPUs take of k cpus from full-core lists is whole
-// cores iff k is a multiple of cpus-per-core, so satisfiedRequiredCPUBindPolicy reduces to that parity);
-// EXACT=true: the cpuset itself (cpu accumulator), for Reserve.
-template <bool EXACT>
-__device__ inline bool numa_allocate(const Topo& t, const NumaStatic& s, const NumaMut& m, const NumaPod& p,
-                                     const NumaHint& h, int strategy, NumaAlloc& res, CpuSet& cpus) {
-  res.n = 0;
-  cpus = cs_zero();
-  const int bind = numa_pref_bind(s, p.preferred);
+// resourceManager.Allocate feasibility (resource_manager.go:171-360) from counts: the per-NUMA takes of
+// allocateCPUSet never fail, and a FullPCPUs take of k cpus from whole-core lists is whole cores iff k is a
+// multiple of cpus-per-core, so satisfiedRequiredCPUBindPolicy reduces to that parity.
+__device__ __forceinline__ bool numa_feasible(const NumaView& v, const NumaPod& p, const NumaHint& h, NumaAlloc& a) {
+  a.res = 0;
+  const int bind = numa_pref_bind(v, p.preferred);
   if (bind < 0) return false;
-  if (!h.nil && !alloc_by_hint(s, m, p, h.mask, res)) return false;
+  if (!h.nil && !alloc_by_hint(v, p, h.mask, a)) return false;
   if (!p.cpu_bind) return true;
-  CpuSet avail = numa_available_cpus(t, s, m);
   const bool required = p.required != 0;
-  if (required) avail = filter_required(t, avail, bind);
-  if (cs_count(avail) < p.needed) return false;
-  const bool whole = required && bind == 2 && t.cpc > 1;  // satisfiedRequired(FullPCPUs) needs whole cores
-  int needed = p.needed;
-  if (res.n > 0) {
+  const int kind = required ? kind_of(bind) : 0;
+  if (tot_at(v, kind) < p.needed) return false;
+  const bool whole = required && bind == 2 && v.cpc > 1;
+  if (a.res) {
     int got = 0;
-    for (int k = 0; k < res.n; ++k) {
-      const CpuSet in = cs_and(avail, t.node_cpus(res.numa[k]));
-      int num = cs_count(in);
-      const int want = (int)(res.cpu[k] / 1000);
+    bool ok = true;
+#pragma unroll
+    for (int i = 0; i < kNumaMax; ++i) {
+      if (!((a.res >> i) & 1u)) continue;
+      int num = cnt_at(v, kind, i);
+      const int want = (int)(a.cpu[i] / 1000);
       if (want < num) num = want;
-      if (whole && num % t.cpc != 0) return false;
-      if (EXACT) {
-        CpuSet one;
-        if (!take_cpus(t, in, num, bind, strategy, one)) return false;
-        cpus = cs_or(cpus, one);
-      }
+      ok &= !(whole && (num % v.cpc) != 0);
       got += num;
     }
-    if (got != needed) return false;
-    return true;
+    return ok && got == p.needed;
   }
-  if (whole && needed % t.cpc != 0) return false;
-  if (EXACT) {
-    if (!take_cpus(t, avail, needed, bind, strategy, cpus)) return false;
-    if (required) {  // satisfiedRequiredCPUBindPolicy (:568-589), exact
-      if (bind == 2 && t.cpc > 1 && cs_count(full_core_cpus(t, cpus)) != cs_count(cpus)) return false;
-      if (bind == 3 && cs_count(first_cpu_per_core(t, cpus)) != cs_count(cpus)) return false;
-    }
-  }
-  return true;
-}
-
-__device__ __forceinline__ int numa_alloc_strategy(const NumaStatic& s, const NumaParams& NP) {
-  return s.strategy >= 0 ? s.strategy : NP.default_alloc_strategy;
+  return !(whole && p.needed % v.cpc != 0);
 }
 
 __device__ __forceinline__ bool skip_the_node(const NumaPod& p, int policy) {
@@ -733,101 +789,112 @@ __device__ __forceinline__ bool skip_the_node(const NumaPod& p, int policy) {
 }
 
 // NodeNUMAResource.Filter (plugin.go:276-334); writes the affinity the topology manager stores
-__device__ inline bool numa_filter(const Topo& t, const NumaStatic& s, const NumaMut& m, const NumaPod& p,
-                                   const NumaParams& NP, NumaHint& aff) {
+__device__ __forceinline__ bool numa_filter(const NumaView& v, const NumaPod& p, const NumaParams& NP, NumaHint& aff) {
   aff = NumaHint{0, 1, 0, 0};
   if (p.prefilter_error) return false;
-  if (skip_the_node(p, s.policy)) return true;
-  const int strategy = numa_alloc_strategy(s, NP);
-  NumaAlloc res;
-  CpuSet cpus;
+  if (skip_the_node(p, v.policy)) return true;
+  NumaAlloc a;
   if (p.cpu_bind) {
-    if (!s.valid) return false;
-    const bool full_only = s.node_bind == 1;
+    if (!v.valid) return false;
+    const bool full_only = v.node_bind == 1;
     if (full_only || p.required == 2) {
-      if (p.needed % t.cpc != 0) return false;                                   // SMT alignment
+      if (p.needed % v.cpc != 0) return false;                                // SMT alignment
       if (full_only && (p.required != 2 || p.preferred != 2)) return false;  // required FullPCPUs policy
     }
-    if (p.required != 0 && s.policy == 0) {
-      const NumaHint none{0, 1, 0, 0};
-      if (!numa_allocate<false>(t, s, m, p, none, strategy, res, cpus)) return false;
-    }
+    if (p.required != 0 && v.policy == 0 && !numa_feasible(v, p, NumaHint{0, 1, 0, 0}, a)) return false;
   }
-  if (s.policy != 0) {
-    if (s.num_numa == 0) return false;
+  if (v.policy != 0) {
+    if (v.nn == 0) return false;
     NumaHint best;
-    if (!numa_admit(t, s, m, p, NP, best)) return false;
+    if (!numa_admit(v, p, NP, best)) return false;
     aff = best;
-    if (!numa_allocate<false>(t, s, m, p, best, strategy, res, cpus)) return false;
+    if (!numa_feasible(v, p, best, a)) return false;
   }
   return true;
 }
 
 // NodeNUMAResource.Score (scoring.go:55-168) with the stored affinity; node_* = NodeInfo.Requested/Allocatable
-__device__ inline int64_t numa_score(const Topo& t, const NumaStatic& s, const NumaMut& m, const NumaPod& p,
-                                     const NumaParams& NP, const NumaHint& aff, int64_t node_req_cpu,
-                                     int64_t node_req_mem, int64_t node_alloc_cpu, int64_t node_alloc_mem) {
-  if (skip_the_node(p, s.policy)) {
+__device__ __forceinline__ int64_t numa_score(const NumaView& v, const NumaPod& p, const NumaParams& NP,
+                                              const NumaHint& aff, int64_t node_req_cpu, int64_t node_req_mem,
+                                              int64_t node_alloc_cpu, int64_t node_alloc_mem) {
+  if (skip_the_node(p, v.policy)) {
     if (p.skip) return 0;
-    if (numa_pref_bind(s, p.preferred) < 0) return 0;  // scoreWithAmplifiedCPUs: getResourceOptions
+    if (numa_pref_bind(v, p.preferred) < 0) return 0;  // scoreWithAmplifiedCPUs: getResourceOptions
     return numa_scorer(NP.node_strategy, NP.w_cpu, NP.w_mem, node_req_cpu, node_req_mem, node_alloc_cpu,
                        node_alloc_mem, p.req_cpu, p.req_mem);
   }
-  if (p.cpu_bind && !s.valid) return 0;
-  NumaAlloc res;
-  CpuSet cpus;
-  if (!numa_allocate<false>(t, s, m, p, aff, numa_alloc_strategy(s, NP), res, cpus)) return 0;
-  int64_t ac, am, rc, rm;
-  if (res.n > 0) {
+  if (p.cpu_bind && !v.valid) return 0;
+  NumaAlloc a;
+  if (!numa_feasible(v, p, aff, a)) return 0;
+  int64_t ac = node_alloc_cpu, am = node_alloc_mem, rc = node_req_cpu, rm = node_req_mem;
+  if (a.res) {  // calculateAllocatableAndRequested (:122-168): the hint's NUMA nodes
     ac = am = rc = rm = 0;
-    for (int k = 0; k < res.n; ++k) {
-      const int i = res.numa[k];
-      rc += m.alloc_cpu[i];
-      rm += m.alloc_mem[i];
-      ac += s.numa_cpu[i];
-      am += s.numa_mem[i];
-    }
-  } else {
-    ac = node_alloc_cpu;
-    am = node_alloc_mem;
-    rc = node_req_cpu;
-    rm = node_req_mem;
+#pragma unroll
+    for (int i = 0; i < kNumaMax; ++i)
+      if ((a.res >> i) & 1u) {
+        rc += v.alloc_cpu[i];
+        rm += v.alloc_mem[i];
+        ac += v.numa_cpu[i];
+        am += v.numa_mem[i];
+      }
   }
   // a cpuset pod: requested cpu = |allocated cpus| · 1000 (needed ≥ 1 whenever cpu_bind)
-  if (p.cpu_bind) {
-    const CpuSet alloc{{m.allocated[0], m.allocated[1], m.allocated[2], m.allocated[3]}};
-    rc = (int64_t)cs_count(alloc) * 1000;
-  }
+  if (p.cpu_bind) rc = (int64_t)v.n_alloc * 1000;
   return numa_scorer(NP.node_strategy, NP.w_cpu, NP.w_mem, rc, rm, ac, am, p.req_cpu, p.req_mem);
 }
 
-// NodeNUMAResource.Reserve (plugin.go:375-415) → Allocate (exact cpuset) → addPodAllocation
-// (node_allocation.go:76-103).  False: the allocation fails and the pod is not placed.
-__device__ inline bool numa_reserve(const Topo& t, const NumaStatic& s, NumaMut& m, const NumaPod& p,
-                                    const NumaParams& NP, const NumaHint& aff, CpuSet& cpus) {
-  cpus = cs_zero();
-  if (skip_the_node(p, s.policy)) return true;
-  if (p.cpu_bind && !s.valid) return false;
-  NumaAlloc res;
-  if (!numa_allocate<true>(t, s, m, p, aff, numa_alloc_strategy(s, NP), res, cpus)) return false;
-#pragma unroll
-  for (int w = 0; w < kCpuWords; ++w) m.allocated[w] |= cpus.w[w];
-  for (int k = 0; k < res.n; ++k) {
-    m.alloc_cpu[res.numa[k]] += res.cpu[k];
-    m.alloc_mem[res.numa[k]] += res.mem[k];
-  }
+// Filter (when the profile has it) + Score of one node: feasibility and the unweighted plugin score
+__device__ __forceinline__ bool numa_eval(const NumaView& v, const NumaPod& p, const NumaParams& NP,
+                                          int64_t node_req_cpu, int64_t node_req_mem, int64_t node_alloc_cpu,
+                                          int64_t node_alloc_mem, int64_t& score, NumaHint& aff) {
+  aff = NumaHint{0, 1, 0, 0};
+  score = 0;
+  if (NP.filter && !numa_filter(v, p, NP, aff)) return false;
+  if (NP.score) score = numa_score(v, p, NP, aff, node_req_cpu, node_req_mem, node_alloc_cpu, node_alloc_mem);
   return true;
 }
 
-// Filter (when the profile has it) + Score of one node: feasibility and the unweighted plugin score
-__device__ inline bool numa_eval(const NumaStatic& s, const NumaMut& m, const NumaPod& p, const NumaParams& NP,
-                                 int64_t node_req_cpu, int64_t node_req_mem, int64_t node_alloc_cpu,
-                                 int64_t node_alloc_mem, int64_t& score, NumaHint& aff) {
-  const Topo t = make_topo(s);
-  aff = NumaHint{0, 1, 0, 0};
-  score = 0;
-  if (NP.filter && !numa_filter(t, s, m, p, NP, aff)) return false;
-  if (NP.score) score = numa_score(t, s, m, p, NP, aff, node_req_cpu, node_req_mem, node_alloc_cpu, node_alloc_mem);
+// NodeNUMAResource.Reserve (plugin.go:375-415) → Allocate with the exact cpuset (cpu accumulator) →
+// addPodAllocation (node_allocation.go:76-103).  False: the allocation fails and the pod is not placed.
+__device__ __noinline__ bool numa_reserve(const NumaStatic& s, NumaMut& m, const NumaView& v, const NumaPod& p,
+                                    const NumaHint& aff, CpuSet& cpus) {
+  cpus = cs_zero();
+  if (skip_the_node(p, v.policy)) return true;
+  if (p.cpu_bind && !v.valid) return false;
+  NumaAlloc a;
+  if (!numa_feasible(v, p, aff, a)) return false;
+  if (p.cpu_bind) {  // allocateCPUSet (:273-360), exact
+    const Topo t = make_topo(s);
+    const int bind = numa_pref_bind(v, p.preferred);
+    CpuSet avail = numa_available_cpus(t, s, m);
+    if (p.required != 0) avail = filter_required(t, avail, bind);
+    if (a.res) {
+      for (int i = 0; i < kNumaMax; ++i) {
+        if (!((a.res >> i) & 1u)) continue;
+        const CpuSet in = cs_and(avail, t.node_cpus(i));
+        int num = cs_count(in);
+        const int want = (int)(a.cpu[i] / 1000);
+        if (want < num) num = want;
+        CpuSet one;
+        if (!take_cpus(t, in, num, bind, v.strategy, one)) return false;
+        cpus = cs_or(cpus, one);
+      }
+    } else if (!take_cpus(t, avail, p.needed, bind, v.strategy, cpus)) {
+      return false;
+    }
+    if (p.required != 0) {  // satisfiedRequiredCPUBindPolicy (:568-589), exact
+      if (bind == 2 && t.cpc > 1 && cs_count(full_core_cpus(t, cpus)) != cs_count(cpus)) return false;
+      if (bind == 3 && cs_count(first_cpu_per_core(t, cpus)) != cs_count(cpus)) return false;
+    }
+  }
+#pragma unroll
+  for (int w = 0; w < kCpuWords; ++w) m.allocated[w] |= cpus.w[w];
+#pragma unroll
+  for (int i = 0; i < kNumaMax; ++i)
+    if ((a.res >> i) & 1u) {
+      m.alloc_cpu[i] += a.cpu[i];
+      m.alloc_mem[i] += a.mem[i];
+    }
   return true;
 }
 
