@@ -41,7 +41,7 @@ def parse():
     ap.add_argument("--nodes", type=int, default=None, help="default 100k (c3) / 10k (c4)")
     ap.add_argument("--pods-per-step", type=int, default=None, help="default 100k (c3) / 10k (c4)")
     ap.add_argument("--batch", type=int, default=32)
-    ap.add_argument("--pods-per-wave", type=int, default=8)
+    ap.add_argument("--pods-per-wave", type=int, default=None, help="default 8 (c3) / 1 (c4)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -144,6 +144,7 @@ def main():
     c4 = args.workload == "c4"
     args.nodes = args.nodes or (10_000 if c4 else 100_000)
     args.pods_per_step = args.pods_per_step or (10_000 if c4 else 100_000)
+    args.pods_per_wave = args.pods_per_wave or (1 if c4 else 8)  # C4 sweep: profiles/r01/c4_sweep.txt
     F = framework
     profile = (F.Profile(filter=(F.NODE_RESOURCES_FIT, F.LOAD_AWARE, F.NODE_NUMA_RESOURCE),
                          score={F.NODE_RESOURCES_FIT: 1, F.LOAD_AWARE: 1, F.NODE_NUMA_RESOURCE: 1}) if c4 else None)
