@@ -35,7 +35,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--workload", choices=("c3", "c4"), default="c3",
+    ap.add_argument("--workload", choices=("c3", "c4", "c5"), default="c3",
                     help="c3: Fit+LoadAware at 100k nodes (the BASELINE metric); c4: + NodeNUMAResource cpuset/NUMA "
                          "on 2-socket 256-cpu nodes")
     ap.add_argument("--nodes", type=int, default=None, help="default 100k (c3) / 10k (c4)")
@@ -94,15 +94,19 @@ class Dist:
             self.dist.destroy_process_group()
 
 
-def cpu_baseline(cfg, cluster, pods, budget_s, threads, numa=None):
-    """Oracle (C restatement of the same Go algorithm, oracle/oracle.c [+ numa.c]) on this host, bounded sample."""
+def cpu_baseline(cfg, cluster, pods, budget_s, threads, numa=None, devices=None):
+    """Oracle (C restatement of the same Go algorithm, oracle/oracle.c [+ numa.c / deviceshare.c]) on this host,
+    bounded sample."""
     from oracle import oracle
     st = oracle.states(cluster.n)
     oracle.add_pods(cfg, st, cluster.existing_pods, cluster.existing_node)
     buf = oracle.numa_states(numa) if numa is not None else None
+    dev = devices.copy() if devices is not None else None
 
     def run(p):
-        if buf is None:
+        if dev is not None:
+            oracle.schedule_full(cfg, cluster.nodes, cluster.metrics, st, p, cluster.now_ns, threads, devices=dev)
+        elif buf is None:
             oracle.schedule(cfg, cluster.nodes, cluster.metrics, st, p, cluster.now_ns, threads)
         else:
             oracle.schedule_numa(cfg, cluster.nodes, cluster.metrics, st, buf, p, cluster.now_ns, threads)
@@ -142,19 +146,29 @@ def main():
     if d.world > 1:
         nccl_id = d.bcast_bytes(nccl_unique_id() if d.rank == 0 else None)
     c4 = args.workload == "c4"
-    args.nodes = args.nodes or (10_000 if c4 else 100_000)
-    args.pods_per_step = args.pods_per_step or (10_000 if c4 else 100_000)
+    c5 = args.workload == "c5"
+    args.nodes = args.nodes or (10_000 if c4 else (50_000 if c5 else 100_000))
+    args.pods_per_step = args.pods_per_step or (10_000 if (c4 or c5) else 100_000)
     args.pods_per_wave = args.pods_per_wave or (1 if c4 else 8)  # C4 sweep: profiles/r01/c4_sweep.txt
     F = framework
-    profile = (F.Profile(filter=(F.NODE_RESOURCES_FIT, F.LOAD_AWARE, F.NODE_NUMA_RESOURCE),
-                         score={F.NODE_RESOURCES_FIT: 1, F.LOAD_AWARE: 1, F.NODE_NUMA_RESOURCE: 1}) if c4 else None)
+    profile = None
+    if c4:
+        profile = F.Profile(filter=(F.NODE_RESOURCES_FIT, F.LOAD_AWARE, F.NODE_NUMA_RESOURCE),
+                            score={F.NODE_RESOURCES_FIT: 1, F.LOAD_AWARE: 1, F.NODE_NUMA_RESOURCE: 1})
+    elif c5:  # shipped weights: DeviceShare 1 (config/manager/scheduler-config.yaml:82-91)
+        profile = F.Profile(filter=(F.NODE_RESOURCES_FIT, F.LOAD_AWARE, F.DEVICE_SHARE),
+                            score={F.NODE_RESOURCES_FIT: 1, F.LOAD_AWARE: 1, F.DEVICE_SHARE: 1})
     cfg = framework.build_config(batch_pods=args.batch, pods_per_wave=args.pods_per_wave, device_id=d.local_rank,
                                  profile=profile)
-    numa = None
+    numa = devices = None
     if c4:
         seed = synth.BASE_SEED + 4
         cluster, numa = synth.make_numa_cluster(args.nodes, seed=seed)
         make_pods = synth.make_numa_pods
+    elif c5:
+        seed = synth.BASE_SEED + 6
+        cluster, devices = synth.make_gpu_cluster(args.nodes, seed=seed)
+        make_pods = synth.make_gpu_pods
     else:
         seed = synth.BASE_SEED + 3
         cluster = synth.make_cluster(args.nodes, seed=seed)
@@ -166,6 +180,8 @@ def main():
         e = Engine(cfg, cluster.n, rank=d.rank, n_ranks=d.world, nccl_id=nccl_id)
         if c4:
             synth.load_numa_into(e, cluster, numa)
+        elif c5:
+            synth.load_gpu_into(e, cluster, devices)
         else:
             synth.load_into(e, cluster)
         return e
@@ -194,8 +210,8 @@ def main():
     placed = int((node_idx >= 0).sum())
 
     # per-kernel live timing (HIP events on the engine stream) for the roofline
-    kernels = {name: e.bench_kernel(which, args.kernel_iters)
-               for which, name in enumerate(("eval_round", "merge_round", "resolve_round"))}
+    names = ("eval_round", "merge_round", "resolve_round") + (("ds_max_round", "ds_norm_reduce") if c5 else ())
+    kernels = {name: e.bench_kernel(which, args.kernel_iters) for which, name in enumerate(names)}
     # roofline kernel: the wide pass, the only kernel whose work scales with node evaluations (SURVEY §8d's
     # 76 B per evaluation); merge and the single-wave FIFO resolver are latency-bound per round
     dom = "eval_round"
@@ -213,7 +229,12 @@ def main():
     check = None
     if args.check and d.rank == 0:
         from oracle import oracle
-        if c4:
+        if c5:
+            st = oracle.states(cluster.n)
+            oracle.add_pods(cfg, st, cluster.existing_pods, cluster.existing_node)
+            on, _, _, _ = oracle.schedule_full(cfg, cluster.nodes, cluster.metrics, st, pods[: args.check],
+                                               cluster.now_ns, args.cpu_threads, devices=devices.copy())
+        elif c4:
             st = oracle.states(cluster.n)
             oracle.add_pods(cfg, st, cluster.existing_pods, cluster.existing_node)
             on, _ = oracle.schedule_numa(cfg, cluster.nodes, cluster.metrics, st, oracle.numa_states(numa),
@@ -225,21 +246,23 @@ def main():
     cpu = None
     if d.rank == 0 and d.world == 1 and not args.no_cpu_baseline:
         print("[bench] cpu baseline sample", file=sys.stderr, flush=True)
-        m, dt = cpu_baseline(cfg, cluster, pods, args.cpu_seconds, args.cpu_threads, numa)
+        m, dt = cpu_baseline(cfg, cluster, pods, args.cpu_seconds, args.cpu_threads, numa, devices)
         cpu = {"value": m / dt, "unit": "pods/s", "cores": args.cpu_threads, "kind": "port",
                "sample": f"first {m} pods of the same queue after a 64-pod probe, {cluster.n} nodes, "
-                         f"oracle/oracle.c {'or_schedule_numa' if c4 else 'or_schedule'}, {args.cpu_threads} threads "
+                         f"oracle/oracle.c {'or_schedule_numa' if c4 else ('or_schedule_full' if c5 else 'or_schedule')}, "
+                         f"{args.cpu_threads} threads "
                          f"(Parallelizer chunking), "
                          f"host nproc={os.cpu_count()}",
                "node_evals_per_sec": m * cluster.n / dt}
 
     traffic, traffic_src = (pmc_traffic(args.traffic_file, dom, cluster.n, args.batch, args.pods_per_wave)
-                            if d.world == 1 and not c4 else (None, None))
+                            if d.world == 1 and not (c4 or c5) else (None, None))
     if d.rank == 0:
         pods_s = total / elapsed
         out = {
             "metric": ("pods scheduled/sec, NodeNUMAResource cpuset/NUMA profile (node-evals/sec alongside)" if c4
-                       else "pods scheduled/sec at 100k nodes (node-evals/sec alongside)"),
+                       else ("pods scheduled/sec, DeviceShare GPU-share profile (node-evals/sec alongside)" if c5
+                             else "pods scheduled/sec at 100k nodes (node-evals/sec alongside)")),
             "value": pods_s,
             "unit": "pods/s",
             "n_gpus": d.world,
@@ -253,8 +276,10 @@ def main():
             "data": "synthetic (SURVEY §8d generator, seed %d)" % seed,
             "config": {"workload": ("C4 cluster: %d 2-socket 256-cpu nodes, %d-pod FIFO queue (70%% cpuset LSR/LSE), "
                                     "NodeResourcesFit+LoadAwareScheduling+NodeNUMAResource, %d pods per step" if c4 else
-                                    "C3 cluster: %d nodes, %d-pod FIFO queue, NodeResourcesFit+LoadAwareScheduling, "
-                                    "%d pods per step") % (cluster.n, total, args.pods_per_step),
+                                    ("C5 (DeviceShare part): %d nodes x 8 GPUs, %d-pod FIFO queue (30%% GPU-share), "
+                                     "NodeResourcesFit+LoadAwareScheduling+DeviceShare, %d pods per step" if c5 else
+                                     "C3 cluster: %d nodes, %d-pod FIFO queue, NodeResourcesFit+LoadAwareScheduling, "
+                                     "%d pods per step")) % (cluster.n, total, args.pods_per_step),
                        "nodes": cluster.n, "pods": total, "batch_pods": args.batch,
                        "parallelism": "node-sharded x%d (replicated table, RCCL all-gather)" % d.world},
             "node_evals_per_sec": pods_s * cluster.n,

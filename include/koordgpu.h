@@ -27,6 +27,10 @@
  *   kg_pods_evaluate        one pod against every node WITHOUT assume: per-node Filter status and per-plugin Score,
  *                           i.e. RunFilterPlugins + RunScorePlugins for one pod (framework_extender.go:204-258) —
  *                           also what --debug-scores prints (frameworkext/debug.go:61-108).
+ *   kg_nodes_device_upsert  DeviceShare nodeDeviceCache.updateNodeDevice (deviceshare/device_cache.go:485-523) + the
+ *                           assigned-pod informer's updateCacheUsed (device_cache.go:124-135, eventhandler_pod.go).
+ *   kg_pods_evaluate_device DeviceShare Filter + Score for one pod on every node (deviceshare/plugin.go:280-330,
+ *                           scoring.go:34-89).
  *   kg_last_error           error text for the last failing call on this thread (maps to framework.NewStatus(Error,…)).
  *
  * Units follow the reference's getResourceValue (load_aware/helper.go:146-151): cpu-like resources in
@@ -41,7 +45,7 @@
 extern "C" {
 #endif
 
-#define KG_ABI_VERSION 2
+#define KG_ABI_VERSION 3
 
 /* ---- resource slots (fixed order) ------------------------------------------------------- */
 enum {
@@ -75,6 +79,20 @@ enum { KG_STRATEGY_LEAST_ALLOCATED = 0, KG_STRATEGY_MOST_ALLOCATED = 1 };
 #define KG_MAX_NUMA 4
 #define KG_MAX_CPUS 256
 
+/* DeviceShare: device resources a pod may request (deviceshare/utils.go:46-56, apis/extension/resource.go) */
+enum {
+  KG_DEV_NVIDIA_GPU = 0,        /* nvidia.com/gpu (count)                              */
+  KG_DEV_HYGON_DCU = 1,         /* dcu.com/gpu (count)                                 */
+  KG_DEV_KOORD_GPU = 2,         /* koordinator.sh/gpu (percentage)                     */
+  KG_DEV_GPU_CORE = 3,          /* koordinator.sh/gpu-core (percentage)                */
+  KG_DEV_GPU_MEMORY = 4,        /* koordinator.sh/gpu-memory (bytes)                   */
+  KG_DEV_GPU_MEMORY_RATIO = 5,  /* koordinator.sh/gpu-memory-ratio (percentage)        */
+  KG_DEV_FPGA = 6,              /* koordinator.sh/fpga (not accelerated)               */
+  KG_DEV_RDMA = 7,              /* koordinator.sh/rdma (not accelerated)               */
+  KG_DEV_RES_MAX = 8
+};
+#define KG_MAX_MINORS 8         /* GPU minors per node */
+
 /* status codes: 0 ok, <0 error class (framework.Error on the Go side) */
 enum {
   KG_OK = 0,
@@ -92,7 +110,8 @@ enum {
   KG_REJECT_FIT_MEMORY = 1 << 2,    /* NodeResourcesFit: Insufficient memory           */
   KG_REJECT_LOADAWARE = 1 << 3,     /* LoadAwareScheduling: usage exceed threshold     */
   KG_REJECT_INVALID_NODE = 1 << 4,  /* deleted / never-upserted slot                   */
-  KG_REJECT_NUMA = 1 << 5           /* NodeNUMAResource (topology, cpuset, NUMA admit) */
+  KG_REJECT_NUMA = 1 << 5,          /* NodeNUMAResource (topology, cpuset, NUMA admit) */
+  KG_REJECT_DEVICE = 1 << 6         /* DeviceShare (Insufficient gpu devices)          */
 };
 
 /* node flags */
@@ -135,6 +154,14 @@ typedef struct kg_config {
   int64_t numa_scoring_weights[2];             /* ScoringStrategy.Resources: cpu, memory              */
   int64_t numa_numa_scoring_strategy;          /* NUMAScoringStrategy.Type (also the default NUMA     */
   int64_t numa_numa_scoring_weights[2];        /* allocate strategy, util.go:26-32)                   */
+  /* DeviceShareArgs (config/types.go; defaults v1beta2/defaults.go:187-208) + profile.  ScoringStrategy.Resources
+   * weights over the GPU resources: gpu-core, gpu-memory, gpu-memory-ratio (default 0, 0, 1; rdma/fpga weights
+   * only touch RDMA/FPGA devices, which are not accelerated). */
+  int64_t ds_filter;                           /* DeviceShare at Filter                               */
+  int64_t ds_score;                            /* DeviceShare at Score (NormalizeScore: DefaultNormalizeScore) */
+  int64_t weight_deviceshare;
+  int64_t ds_scoring_strategy;                 /* KG_STRATEGY_* (LeastAllocated only is accelerated)  */
+  int64_t ds_scoring_weights[3];               /* gpu-core, gpu-memory, gpu-memory-ratio              */
   /* engine tuning (0 = default) */
   int64_t batch_pods;                          /* pods resolved per device round (B, 1..64)           */
   int64_t pods_per_wave;                       /* pods one eval wave scores per round (1..B)          */
@@ -176,8 +203,21 @@ typedef struct kg_pod {
   int64_t qos;                                 /* extension.GetPodQoSClassRaw: KG_QOS_*               */
   int64_t required_cpu_bind_policy;            /* ResourceSpec annotation: KG_BIND_*                  */
   int64_t preferred_cpu_bind_policy;           /* ResourceSpec annotation: KG_BIND_*                  */
+  int64_t device_requests[KG_DEV_RES_MAX];     /* PodRequestsAndLimits of the device resources (KG_DEV_*) */
   int64_t reserved[3];
 } kg_pod;
+
+/* DeviceShare view of one node's GPUs: the Device object's GPU entries (deviceshare/device_cache.go:505-523:
+ * an unhealthy device has empty resources) + nodeDevice.deviceUsed from the pods already bound there.
+ * has_device = 0: no Device object for the node (the plugin passes such nodes; NodeResourcesFit on the
+ * device extended resources, whose allocatable is then 0, rejects device pods). */
+typedef struct kg_node_device {
+  int64_t has_device;
+  int64_t present[KG_MAX_MINORS];              /* a GPU DeviceInfo with this minor exists             */
+  int64_t healthy[KG_MAX_MINORS];
+  int64_t total_core[KG_MAX_MINORS], total_memory[KG_MAX_MINORS], total_ratio[KG_MAX_MINORS];
+  int64_t used_core[KG_MAX_MINORS], used_memory[KG_MAX_MINORS], used_ratio[KG_MAX_MINORS];
+} kg_node_device;
 
 /* NodeNUMAResource view of one node: TopologyOptions (topology_options.go:40-48, from the
  * NodeResourceTopology) + the NodeAllocation built from already-bound pods (node_allocation.go:32-38).
@@ -269,6 +309,18 @@ int kg_results_fetch_cpusets(kg_engine* e, int64_t first, int64_t count, uint64_
 int kg_pods_evaluate_numa(kg_engine* e, const kg_pod* pod, int32_t* out_pass, int64_t* out_score,
                           int64_t* out_affinity);
 
+/* DeviceShare (engines whose profile enables it): the GPU devices of nodes idx[0..n) (replaces each node's
+ * device state). */
+int kg_nodes_device_upsert(kg_engine* e, const kg_node_device* dev, const int32_t* idx, int64_t n);
+/* Reads the DEVICE nodeDevice.deviceUsed of every node: KG_MAX_MINORS values per node for each output. */
+int kg_nodes_read_device(kg_engine* e, int64_t* used_core, int64_t* used_memory, int64_t* used_ratio);
+/* The GPU minors DeviceShare Reserve allocated to staged pods [first, first+count): a bitmask per pod (0 = none);
+ * every chosen minor received the pod's per-instance request (CalcDesiredRequestsAndCount). */
+int kg_results_fetch_devices(kg_engine* e, int64_t first, int64_t count, int32_t* out_minor_mask);
+/* DeviceShare Filter + Score of one pod on every node slot, the plugin alone: out_pass 1/0 and the raw
+ * (un-normalized) score, 0 where Filter rejects. */
+int kg_pods_evaluate_device(kg_engine* e, const kg_pod* pod, int32_t* out_pass, int64_t* out_score);
+
 /* Measurement hooks (bench.py): replays one device round's kernel `which` (0 = eval, 1 = merge, 2 = resolve) `iters` times
  * on the engine stream between HIP events, restoring state, and returns the mean duration in ms plus the
  * algorithmic bytes that kernel must move per launch. Requires a staged queue. */
@@ -293,7 +345,8 @@ int kg_debug_stamps(kg_engine* e, uint64_t* out);
 
 const char* kg_last_error(void);
 int kg_abi_version(void);
-/* sizeof of the ABI structs (0 kg_config, 1 kg_node, 2 kg_node_metric, 3 kg_pod, 4 kg_stats, 5 kg_node_numa) for
+/* sizeof of the ABI structs (0 kg_config, 1 kg_node, 2 kg_node_metric, 3 kg_pod, 4 kg_stats, 5 kg_node_numa,
+ * 6 kg_node_device) for
  * binding checks. */
 int64_t kg_abi_struct_size(int which);
 

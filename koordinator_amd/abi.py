@@ -31,7 +31,7 @@ OK, E_INVALID, E_DEVICE, E_COLLECTIVE, E_NOMEM, E_UNSUPPORTED = 0, -1, -2, -3, -
 REJECT_FIT_PODS, REJECT_FIT_CPU, REJECT_FIT_MEMORY, REJECT_LOADAWARE, REJECT_INVALID_NODE = 1, 2, 4, 8, 16
 NODE_VALID, NODE_HAS_RAW_ALLOCATABLE, NODE_HAS_CUSTOM_THRESHOLDS = 1, 2, 4
 POD_DAEMONSET = 1
-ABI_VERSION = 2
+ABI_VERSION = 3
 MAX_NUMA, MAX_CPUS = 4, 256
 QOS = {"": 0, "LSE": 1, "LSR": 2, "LS": 3, "BE": 4, "SYSTEM": 5}
 BIND = {"": 0, "Default": 1, "FullPCPUs": 2, "SpreadByPCPUs": 3, "ConstrainedBurst": 4}
@@ -39,6 +39,17 @@ NODE_BIND = {"": 0, "None": 0, "FullPCPUsOnly": 1, "SpreadByPCPUs": 2}
 NUMA_POLICY = {"": 0, "BestEffort": 1, "Restricted": 2, "SingleNUMANode": 3}
 STRATEGY = {"LeastAllocated": 0, "MostAllocated": 1}
 REJECT_NUMA = 32
+REJECT_DEVICE = 64
+# DeviceShare device resources (KG_DEV_*)
+DEV_RES_MAX, MAX_MINORS = 8, 8
+DEV_NVIDIA_GPU, DEV_HYGON_DCU, DEV_KOORD_GPU, DEV_GPU_CORE, DEV_GPU_MEMORY, DEV_GPU_MEMORY_RATIO, DEV_FPGA, DEV_RDMA = \
+    range(8)
+DEVICE_RESOURCE_SLOTS = {
+    "nvidia.com/gpu": DEV_NVIDIA_GPU, "dcu.com/gpu": DEV_HYGON_DCU, "koordinator.sh/gpu": DEV_KOORD_GPU,
+    "koordinator.sh/gpu-core": DEV_GPU_CORE, "koordinator.sh/gpu-memory": DEV_GPU_MEMORY,
+    "koordinator.sh/gpu-memory-ratio": DEV_GPU_MEMORY_RATIO, "koordinator.sh/fpga": DEV_FPGA,
+    "koordinator.sh/rdma": DEV_RDMA,
+}
 
 
 def _i64(name, n=None):
@@ -60,6 +71,8 @@ CONFIG_DTYPE = np.dtype([
     _i64("numa_filter"), _i64("numa_score"), _i64("weight_numa"), _i64("numa_default_cpu_bind_policy"),
     _i64("numa_scoring_strategy"), _i64("numa_scoring_weights", 2),
     _i64("numa_numa_scoring_strategy"), _i64("numa_numa_scoring_weights", 2),
+    _i64("ds_filter"), _i64("ds_score"), _i64("weight_deviceshare"), _i64("ds_scoring_strategy"),
+    _i64("ds_scoring_weights", 3),
     _i64("batch_pods"), _i64("pods_per_wave"), _i64("device_id"),
     _i64("reserved", 8),
 ])
@@ -89,7 +102,14 @@ POD_DTYPE = np.dtype([
     _i64("priority_class"),
     _i64("flags"),
     _i64("qos"), _i64("required_cpu_bind_policy"), _i64("preferred_cpu_bind_policy"),
+    _i64("device_requests", DEV_RES_MAX),
     _i64("reserved", 3),
+])
+
+NODE_DEVICE_DTYPE = np.dtype([
+    _i64("has_device"), _i64("present", MAX_MINORS), _i64("healthy", MAX_MINORS),
+    _i64("total_core", MAX_MINORS), _i64("total_memory", MAX_MINORS), _i64("total_ratio", MAX_MINORS),
+    _i64("used_core", MAX_MINORS), _i64("used_memory", MAX_MINORS), _i64("used_ratio", MAX_MINORS),
 ])
 
 NODE_NUMA_DTYPE = np.dtype([
@@ -105,7 +125,8 @@ STATS_DTYPE = np.dtype([
     ("seconds", np.float64), ("reserved", np.float64, (3,)),
 ])
 
-STRUCT_DTYPES = {0: CONFIG_DTYPE, 1: NODE_DTYPE, 2: METRIC_DTYPE, 3: POD_DTYPE, 4: STATS_DTYPE, 5: NODE_NUMA_DTYPE}
+STRUCT_DTYPES = {0: CONFIG_DTYPE, 1: NODE_DTYPE, 2: METRIC_DTYPE, 3: POD_DTYPE, 4: STATS_DTYPE, 5: NODE_NUMA_DTYPE,
+                 6: NODE_DEVICE_DTYPE}
 
 # Every symbol include/koordgpu.h declares (tests check the library exports all of them).
 EXPORTED_SYMBOLS = (
@@ -115,6 +136,7 @@ EXPORTED_SYMBOLS = (
     "kg_nodes_read_state", "kg_bench_kernel", "kg_debug_least_requested", "kg_last_error", "kg_abi_version",
     "kg_abi_struct_size", "kg_nccl_unique_id", "kg_debug_eval_paths", "kg_debug_stamps", "kg_debug_fast_lrs",
     "kg_nodes_numa_upsert", "kg_nodes_read_numa", "kg_results_fetch_cpusets", "kg_pods_evaluate_numa",
+    "kg_nodes_device_upsert", "kg_nodes_read_device", "kg_results_fetch_devices", "kg_pods_evaluate_device",
 )
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
@@ -170,6 +192,10 @@ def load_library(path: str | None = None):
         "kg_nodes_read_numa": (i, [vp, vp, vp, vp]),
         "kg_results_fetch_cpusets": (i, [vp, i64, i64, vp]),
         "kg_pods_evaluate_numa": (i, [vp, vp, vp, vp, vp]),
+        "kg_nodes_device_upsert": (i, [vp, vp, vp, i64]),
+        "kg_nodes_read_device": (i, [vp, vp, vp, vp]),
+        "kg_results_fetch_devices": (i, [vp, i64, i64, vp]),
+        "kg_pods_evaluate_device": (i, [vp, vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)

@@ -27,6 +27,7 @@
 #include "../../include/koordgpu.h"
 #include "kernels.h"
 #include "numa_dev.h"
+#include "ds_dev.h"
 
 using namespace kg;
 
@@ -1020,6 +1021,369 @@ __global__ void scatter_numa(NumaTable NT, const NumaStatic* __restrict__ s, con
   NT.m[i] = m[k];
 }
 
+// ---- DeviceShare profiles (config C5) -------------------------------------------------------
+// DeviceShare's Score is normalized per pod (DefaultNormalizeScore: 100·s / max over the feasible nodes), so a
+// node's key depends on the maximum M over the whole cluster.  Per round:
+//   ds_max_round   — every (pod, tile): max raw DeviceShare score over the tile's feasible nodes + how many hold it
+//   ds_norm_reduce — per pod: M = max over tiles, c = #feasible nodes with raw == M (round-start snapshot)
+//   eval_round_ds  — keys with that M (Fit + LoadAware + w·normalized DeviceShare), top-kR per tile
+//   merge_round    — as for the other profiles
+//   resolve_round_ds — FIFO replay; pod j keeps M_j = M only if an unmodified node or a modified row still holds
+//                    M (counts of round-start holders among the modified rows); otherwise the round ends there.
+// Rounds are unpipelined and driven by the device cursor: every kernel reads its first pod from ctl[0], so an
+// early stop just makes the next round start at the cursor (no poison, no host round trip).
+constexpr int kDsPpw = 8;
+
+struct DsTable {
+  DsNode* __restrict__ d;
+};
+
+__device__ __forceinline__ bool ds_round_range(const int64_t* ctl, int64_t end, int B, int64_t& first, int& nb) {
+  first = ctl[0];
+  const int64_t left = end - first;
+  nb = left < B ? (int)left : B;
+  return nb > 0;
+}
+
+__global__ __launch_bounds__(kWave* kEvalWaves) void ds_max_round(DevTable T, DsTable DT,
+                                                                   const DevPod* __restrict__ pods,
+                                                                   const DsPod* __restrict__ dpods,
+                                                                   const int64_t* __restrict__ ctl, int64_t end,
+                                                                   int B, int pods_per_wave, int64_t n_local,
+                                                                   int nt_local, EvalParams P, DsParams DP,
+                                                                   uint64_t* __restrict__ dsmax) {
+  int64_t first;
+  int nb;
+  if (!ds_round_range(ctl, end, B, first, nb)) return;
+  const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
+  const int n_pg = (B + pods_per_wave - 1) / pods_per_wave;
+  const uint32_t nwg = gridDim.x, bid = blockIdx.x, xcd = bid % 8u, q = nwg / 8u, r = nwg % 8u;
+  const uint32_t wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8u;
+  const int tile = (int)(wgid / (uint32_t)n_pg) * kEvalWaves + wave;
+  const int p0 = (int)(wgid % (uint32_t)n_pg) * pods_per_wave;
+  if (tile >= nt_local || p0 >= nb) return;
+  const int np = ((p0 + pods_per_wave) < nb ? (p0 + pods_per_wave) : nb) - p0;
+  uint32_t mx[kDsPpw], cnt[kDsPpw];
+#pragma unroll
+  for (int k = 0; k < kDsPpw; ++k) mx[k] = 0, cnt[k] = 0;
+  for (int j = 0; j < kNPT; ++j) {
+    const int64_t i = (int64_t)tile * kTile + j * kWave + lane;
+    if (i >= n_local) break;
+    const Row row = load_row(T, i);
+    const DsNode d = DT.d[i];
+#pragma unroll
+    for (int k = 0; k < kDsPpw; ++k) {
+      if (k >= np) break;
+      int64_t t = 0, raw = 0;
+      if (eval_node(row, pods[first + p0 + k], P, t) && ds_eval(d, dpods[first + p0 + k], DP, raw)) {
+        const uint32_t v = (uint32_t)raw + 1u;  // +1: a feasible node with raw 0 still counts
+        cnt[k] = v > mx[k] ? 1u : cnt[k] + (v == mx[k] ? 1u : 0u);
+        mx[k] = v > mx[k] ? v : mx[k];
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < kDsPpw; ++k) {
+    if (k >= np) break;
+    const uint32_t m = wave_max_u32(mx[k]);
+    const uint32_t c = wave_sum_u32(mx[k] == m ? cnt[k] : 0u);
+    if (lane == 0) dsmax[(size_t)(p0 + k) * nt_local + tile] = ((uint64_t)m << 32) | c;
+  }
+}
+
+// per pod: (M + 1) << 32 | c over the tiles (0: no feasible node)
+__global__ __launch_bounds__(256) void ds_norm_reduce(const int64_t* __restrict__ ctl, int64_t end, int B,
+                                                      const uint64_t* __restrict__ dsmax, int nt_local,
+                                                      uint64_t* __restrict__ dsnorm) {
+  __shared__ uint32_t s_m[256 / kWave], s_c[256 / kWave];
+  int64_t first;
+  int nb;
+  if (!ds_round_range(ctl, end, B, first, nb)) return;
+  const int pod = blockIdx.x;
+  if (pod >= nb) return;
+  const int tid = threadIdx.x, lane = tid % kWave, wave = tid / kWave;
+  uint32_t m = 0, c = 0;
+  for (int t = tid; t < nt_local; t += 256) {
+    const uint64_t v = dsmax[(size_t)pod * nt_local + t];
+    const uint32_t vm = (uint32_t)(v >> 32), vc = (uint32_t)v;
+    c = vm > m ? vc : c + (vm == m ? vc : 0u);
+    m = vm > m ? vm : m;
+  }
+  const uint32_t wm = wave_max_u32(m);
+  const uint32_t wc = wave_sum_u32(m == wm ? c : 0u);
+  if (lane == 0) s_m[wave] = wm, s_c[wave] = wc;
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t M = 0, C = 0;
+    for (int w = 0; w < 256 / kWave; ++w) {
+      C = s_m[w] > M ? s_c[w] : C + (s_m[w] == M ? s_c[w] : 0u);
+      M = s_m[w] > M ? s_m[w] : M;
+    }
+    dsnorm[pod] = ((uint64_t)M << 32) | C;
+  }
+}
+
+__global__ __launch_bounds__(kWave* kEvalWaves) void eval_round_ds(DevTable T, DsTable DT,
+                                                                    const DevPod* __restrict__ pods,
+                                                                    const DsPod* __restrict__ dpods,
+                                                                    const int64_t* __restrict__ ctl, int64_t end,
+                                                                    int B, int pods_per_wave, int64_t n_local,
+                                                                    int nt_local, EvalParams P, DsParams DP,
+                                                                    const uint64_t* __restrict__ dsnorm,
+                                                                    uint64_t* __restrict__ lists) {
+  int64_t first;
+  int nb;
+  if (!ds_round_range(ctl, end, B, first, nb)) return;
+  const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
+  const int n_pg = (B + pods_per_wave - 1) / pods_per_wave;
+  const uint32_t nwg = gridDim.x, bid = blockIdx.x, xcd = bid % 8u, q = nwg / 8u, r = nwg % 8u;
+  const uint32_t wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8u;
+  const int tile = (int)(wgid / (uint32_t)n_pg) * kEvalWaves + wave;
+  const int p0 = (int)(wgid % (uint32_t)n_pg) * pods_per_wave;
+  if (tile >= nt_local || p0 >= nb) return;
+  const int np = ((p0 + pods_per_wave) < nb ? (p0 + pods_per_wave) : nb) - p0;
+  const int vbits = P.score_bits + 1;
+  uint32_t M[kDsPpw];
+#pragma unroll
+  for (int k = 0; k < kDsPpw; ++k) {
+    const uint32_t mm = k < np ? (uint32_t)(dsnorm[p0 + k] >> 32) : 0u;
+    M[k] = mm ? mm - 1u : 0u;
+  }
+  uint32_t v[kDsPpw][kNPT];
+  uint32_t gidx[kNPT];
+#pragma unroll
+  for (int j = 0; j < kNPT; ++j) {
+    const int64_t i = (int64_t)tile * kTile + j * kWave + lane;
+    gidx[j] = (uint32_t)i;
+    const bool in = i < n_local;
+    Row row;
+    row.flags = 0;
+    DsNode d;
+    if (in) {
+      row = load_row(T, i);
+      d = DT.d[i];
+    }
+#pragma unroll
+    for (int k = 0; k < kDsPpw; ++k) {
+      v[k][j] = 0u;
+      if (k >= np || !in) continue;
+      int64_t t = 0, raw = 0;
+      if (eval_node(row, pods[first + p0 + k], P, t) && ds_eval(d, dpods[first + p0 + k], DP, raw))
+        v[k][j] = (uint32_t)(t + (DP.score ? DP.weight * ds_normalized(raw, M[k]) : 0)) + 1u;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < kDsPpw; ++k) {
+    if (k >= np) break;
+    select_write(v[k], gidx, vbits, lists + ((size_t)(p0 + k) * nt_local + tile) * kR, lane);
+  }
+}
+
+// Single-wave FIFO resolver of a DeviceShare round.  Lane l < nM owns modified node l: its Row in registers and
+// its DsNode in LDS, plus the round-start copies of both (what the wide passes saw).
+constexpr int kDsNodeWords = (int)(sizeof(DsNode) / 8), kDsPodWords = (int)(sizeof(DsPod) / 8);
+
+__global__ __launch_bounds__(kWave) void resolve_round_ds(DevTable T, DsTable DT, const DevPod* __restrict__ pods,
+                                                           const DsPod* __restrict__ dpods,
+                                                           int64_t* __restrict__ ctl, int64_t end, int B,
+                                                           const uint64_t* __restrict__ cand,
+                                                           const uint64_t* __restrict__ dsnorm, EvalParams P,
+                                                           DsParams DP, uint64_t* __restrict__ out_keys,
+                                                           int32_t* __restrict__ out_minors, int bitmap_words) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
+  const int lane = threadIdx.x;
+  int64_t first;
+  int nb;
+  if (!ds_round_range(ctl, end, B, first, nb)) return;
+  uint64_t* s_cand = smem;                                  // [nb][kCandStride]
+  uint64_t* s_podw = s_cand + (size_t)nb * kCandStride;     // [nb] DevPod
+  uint64_t* s_dpw = s_podw + (size_t)nb * kPodWords;        // [nb] DsPod
+  uint64_t* s_cur = s_dpw + (size_t)nb * kDsPodWords;       // [kWave] DsNode, current
+  uint64_t* s_rs = s_cur + (size_t)kWave * kDsNodeWords;    // [kWave] DsNode, round start
+  uint64_t* s_stg = s_rs + (size_t)kWave * kDsNodeWords;    // [nb] DsNode of each pod's top candidate
+  Row* s_srow = reinterpret_cast<Row*>(s_stg + (size_t)nb * kDsNodeWords);  // [nb] its Row
+  uint32_t* bitmap = reinterpret_cast<uint32_t*>(s_srow + nb);
+  for (int w = lane; w < nb * kCandStride; w += kWave) s_cand[w] = cand[w];
+  {
+    const uint64_t* pw = reinterpret_cast<const uint64_t*>(pods + first);
+    for (int w = lane; w < nb * kPodWords; w += kWave) s_podw[w] = pw[w];
+    const uint64_t* dw = reinterpret_cast<const uint64_t*>(dpods + first);
+    for (int w = lane; w < nb * kDsPodWords; w += kWave) s_dpw[w] = dw[w];
+  }
+  for (int w = lane; w < bitmap_words; w += kWave) bitmap[w] = 0;
+  // stage the round-start row of every pod's top candidate (the usual winner): a first assume onto it then
+  // reads LDS instead of waiting on HBM inside the serial loop
+  uint32_t stg_node = 0xFFFFFFFFu;
+  const uint64_t my_nrm = lane < nb ? dsnorm[lane] : 0;  // pod `lane`'s (M + 1, holders), read by readlane
+  if (lane < nb) {
+    const uint64_t k0 = cand[(size_t)lane * kCandStride];
+    if (k0 != 0) {
+      stg_node = key_node(k0);
+      s_srow[lane] = load_row(T, stg_node);
+      reinterpret_cast<DsNode*>(s_stg)[lane] = DT.d[stg_node];
+    }
+  }
+  __syncthreads();
+  const DevPod* s_pods = reinterpret_cast<const DevPod*>(s_podw);
+  const DsPod* s_dp = reinterpret_cast<const DsPod*>(s_dpw);
+  DsNode* s_dc = reinterpret_cast<DsNode*>(s_cur);
+  DsNode* s_dr = reinterpret_cast<DsNode*>(s_rs);
+  uint32_t midx = 0xFFFFFFFFu;
+  Row mrow, rrow;
+  mrow.flags = 0;
+  rrow.flags = 0;
+  bool touched = false;
+  uint64_t my_out = 0;
+  int32_t my_minors = 0;
+  int nM = 0, consumed = 0;
+  for (int j = 0; j < nb; ++j) {
+    const uint64_t key = s_cand[(size_t)j * kCandStride + lane];
+    const uint64_t ub = s_cand[(size_t)j * kCandStride + kC];
+    const DevPod p = s_pods[j];
+    const DsPod dp = s_dp[j];
+    const uint64_t nrm = readlane_u64(my_nrm, j);
+    const uint32_t Mrs = (uint32_t)(nrm >> 32), Crs = (uint32_t)nrm;  // Mrs = max raw + 1 (0: no feasible node)
+    // M_j: the round-start max survives while an unmodified node or a modified row still holds it.  At most nM
+    // holders can have been modified, so with more than nM holders nothing needs re-scoring.
+    bool cf = false, have_cur = false;
+    int64_t ct = 0, craw = 0;
+    if (DP.score && Mrs > 0 && Crs <= (uint32_t)nM) {
+      bool rf = false;
+      int64_t rt = 0, rraw = 0;
+      if (lane < nM) rf = eval_node(rrow, p, P, rt) && ds_eval(s_dr[lane], dp, DP, rraw);
+      const uint32_t lost = (uint32_t)__popcll(__ballot(rf && (uint32_t)rraw + 1u == Mrs));
+      if (lost >= Crs) {
+        if (lane < nM) cf = eval_node(mrow, p, P, ct) && ds_eval(s_dc[lane], dp, DP, craw);
+        have_cur = true;
+        const uint32_t cm = wave_max_u32(cf ? (uint32_t)craw + 1u : 0u);
+        if (cm != Mrs) break;  // the normalization changed: every key of the round's lists is stale
+      }
+    }
+    const uint32_t Mj = Mrs ? Mrs - 1u : 0u;
+    const uint32_t node = key_node(key);
+    const bool unmod = (key != 0) && !((bitmap[node >> 5] >> (node & 31)) & 1u);
+    const uint64_t um = __ballot(unmod);
+    const int pos = um ? (int)__builtin_ctzll(um) : kC;
+    uint64_t best = um ? readlane_u64(key, pos) : 0;
+    // With M_j = the round-start M every plugin term is monotone (an assume only lowers a node's key), so a
+    // modified row can only beat the best unmodified candidate when that is not the pod's overall top key.
+    if (nM > 0 && pos != 0) {
+      if (!have_cur && lane < nM) cf = eval_node(mrow, p, P, ct) && ds_eval(s_dc[lane], dp, DP, craw);
+      const uint64_t mk = cf ? make_key(ct + (DP.score ? DP.weight * ds_normalized(craw, Mj) : 0), midx) : 0;
+      const uint64_t mbest = wave_max_key(mk);
+      best = mbest > best ? mbest : best;
+    }
+    if (best < ub) break;
+    ++consumed;
+    if (best == 0) {
+      my_out = lane == j ? 0 : my_out;
+      my_minors = lane == j ? 0 : my_minors;
+      continue;
+    }
+    const uint32_t w = key_node(best);
+    const uint64_t hit = __ballot((lane < nM) & (midx == w));
+    const int owner = hit ? (int)__builtin_ctzll(hit) : nM;
+    if (!hit) {
+      const uint64_t sh = __ballot(stg_node == w);  // a pod whose top candidate is w staged its row
+      const int src = sh ? (int)__builtin_ctzll(sh) : -1;
+      if (lane == owner) {
+        midx = w;
+        const DsNode dn = src >= 0 ? reinterpret_cast<const DsNode*>(s_stg)[src] : DT.d[w];
+        mrow = src >= 0 ? s_srow[src] : load_row(T, w);
+        rrow = mrow;
+        s_dc[owner] = dn;
+        s_dr[owner] = dn;
+      }
+      if (lane == 0) bitmap[w >> 5] |= 1u << (w & 31);
+      ++nM;
+    }
+    __syncthreads();
+    // Reserve: DeviceShare allocates the minors (wave-parallel: lane m scores minor m of the winner's row), then
+    // the assume.  A failed Reserve leaves the pod unplaced and the node unchanged.
+    int placed = 0, minors = 0;
+    {
+      DsNode& dn = s_dc[owner];
+      if (dp.skip || !dn.has_device) {
+        placed = 1;
+      } else if (!dp.error) {
+        const DsInst in = ds_instance(dn, dp);
+        if (in.ok) {
+          bool fit = false, nz = false;
+          const int64_t sc = lane < kMinors ? ds_minor(dn, lane, in, DP, fit, nz) : 0;
+          fit &= lane < kMinors;
+          const uint64_t fits = __ballot(fit);
+          if (__ballot(nz && lane < kMinors) != 0 && __popcll(fits) >= in.count) {
+            uint32_t taken = 0;
+            for (int k = 0; k < in.count; ++k) {  // (score desc, minor asc): max of score << 4 | (15 - minor)
+              const bool cand = fit && !((taken >> (lane & 31)) & 1u);
+              const uint32_t v = cand ? ((uint32_t)sc << 4) | (uint32_t)(15 - lane) : 0u;
+              taken |= 1u << (15 - (int)(wave_max_u32(v) & 15u));
+            }
+            if (lane < kMinors && ((taken >> lane) & 1u)) {
+              dn.ucore[lane] += (int32_t)in.core;
+              dn.uratio[lane] += (int32_t)in.ratio;
+              dn.umem[lane] += in.mem;
+            }
+            placed = 1;
+            minors = (int)taken;
+          }
+        }
+      }
+    }
+    if (placed && lane == owner) {
+      mrow.req_cpu += p.req_cpu;  // NodeInfo.AddPod + LoadAware assign cache
+      mrow.req_mem += p.req_mem;
+      mrow.nz_cpu += p.nz_cpu;
+      mrow.nz_mem += p.nz_mem;
+      mrow.la_used_cpu += p.est_cpu;
+      mrow.la_used_mem += p.est_mem;
+      if (p.flags & P_PROD) {
+        mrow.la_pused_cpu += p.est_cpu;
+        mrow.la_pused_mem += p.est_mem;
+      }
+      mrow.num_pods += 1;
+      touched = true;
+    }
+    placed = __builtin_amdgcn_readlane(placed, owner);
+    minors = __builtin_amdgcn_readlane(minors, owner);
+    my_out = lane == j ? (placed ? best : 0) : my_out;
+    my_minors = lane == j ? (placed ? minors : 0) : my_minors;
+    __syncthreads();
+  }
+  if (touched) {
+    store_mutable(T, midx, mrow);
+    DT.d[midx] = s_dc[lane];
+  }
+  if (lane < consumed) {
+    out_keys[first + lane] = my_out;
+    out_minors[first + lane] = my_minors;
+  }
+  __threadfence();
+  if (lane == 0) {
+    ctl[0] = first + consumed;
+    ctl[1] += 1;
+    ctl[2] += consumed;
+  }
+}
+
+// kg_pods_evaluate_device: DeviceShare Filter + raw Score of one pod on every node (the plugin alone)
+__global__ void evaluate_pod_ds(DsTable DT, const DsPod* __restrict__ pod, int64_t n, DsParams DP,
+                                int32_t* __restrict__ pass, int64_t* __restrict__ score) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  int64_t raw = 0;
+  const bool ok = ds_eval(DT.d[i], *pod, DP, raw);
+  pass[i] = ok ? 1 : 0;
+  score[i] = ok ? raw : 0;
+}
+
+// Scatter of upserted device rows
+__global__ void scatter_ds(DsTable DT, const DsNode* __restrict__ s, const int32_t* __restrict__ idx, int64_t n) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  DT.d[idx[k]] = s[k];
+}
+
 // kg_pods_evaluate: one pod, every node, per-plugin outputs.
 __global__ void evaluate_pod(DevTable T, const DevPod* __restrict__ pod, int64_t n, EvalParams P,
                              int32_t* __restrict__ reject, int64_t* __restrict__ fit, int64_t* __restrict__ la) {
@@ -1205,6 +1569,15 @@ struct kg_engine {
   DevBuf<NumaMut> numa_m;
   DevBuf<NumaPod> npods;
   DevBuf<uint64_t> out_cpus;  // [staged + kMaxB][4]
+  // DeviceShare (profile enables it): per-node GPU state, per-pod preFilterState, Reserve's minors, round scratch
+  bool ds_on = false;
+  DsParams DP{};
+  DevBuf<DsNode> ds_d;
+  std::vector<DsNode> ds_host;
+  DevBuf<DsPod> dpods;
+  DevBuf<int32_t> out_minors;  // [staged + kMaxB]
+  DevBuf<uint64_t> dsmax;      // [B][nt_local]
+  DevBuf<uint64_t> dsnorm;     // [B]
 };
 
 namespace {
@@ -1227,6 +1600,17 @@ int validate_config(const kg_config* c) {
   if (c->weight_fit < 0 || c->weight_fit > 1000000 || c->weight_loadaware < 0 || c->weight_loadaware > 1000000)
     return fail(KG_E_INVALID, "plugin weight out of range");
   if (c->batch_pods < 0 || c->batch_pods > kMaxB) return fail(KG_E_INVALID, "batch_pods must be in [1,%d]", kMaxB);
+  if (c->ds_filter || c->ds_score) {
+    if (c->weight_deviceshare < 0 || c->weight_deviceshare > 1000000) return fail(KG_E_INVALID, "DeviceShare weight out of range");
+    if (c->ds_scoring_strategy != KG_STRATEGY_LEAST_ALLOCATED)
+      return fail(KG_E_UNSUPPORTED, "DeviceShare scoring strategy: LeastAllocated only is accelerated");
+    for (int r = 0; r < 3; ++r)
+      if (c->ds_scoring_weights[r] < 0 || c->ds_scoring_weights[r] > 1000000) return fail(KG_E_INVALID, "DeviceShare scoring weight");
+    if (c->ds_score && !c->ds_filter)
+      return fail(KG_E_UNSUPPORTED, "DeviceShare at Score needs DeviceShare at Filter (Score errors on unfiltered nodes)");
+    if (c->numa_filter || c->numa_score) return fail(KG_E_UNSUPPORTED, "NodeNUMAResource + DeviceShare in one profile");
+    if (c->batch_pods > 32) return fail(KG_E_UNSUPPORTED, "DeviceShare profiles: batch_pods <= 32");
+  }
   if (c->numa_filter || c->numa_score) {
     if (c->weight_numa < 0 || c->weight_numa > 1000000) return fail(KG_E_INVALID, "NodeNUMAResource weight out of range");
     if ((c->numa_scoring_strategy != KG_STRATEGY_LEAST_ALLOCATED && c->numa_scoring_strategy != KG_STRATEGY_MOST_ALLOCATED) ||
@@ -1449,6 +1833,75 @@ int decode_node_numa(const kg_node_numa& n, NumaStatic& s, NumaMut& m) {
   return 0;
 }
 
+// DeviceShare preFilterState for the GPU type: GetPodDeviceRequests (deviceshare/utils.go:232-252) =
+// RemoveZeros → Mask(GPU names) → ValidateDeviceRequest (:158-179, percentage units :151-156) →
+// ConvertDeviceRequest (:181-192 with the mapper table :92-149).
+int decode_ds_pod(const kg_pod& p, DsPod& d) {
+  std::memset(&d, 0, sizeof(d));
+  const int64_t* q = p.device_requests;
+  for (int r = 0; r < KG_DEV_RES_MAX; ++r)
+    if (q[r] < 0) return fail(KG_E_INVALID, "negative device request");
+  if (q[KG_DEV_FPGA] || q[KG_DEV_RDMA]) return fail(KG_E_UNSUPPORTED, "FPGA / RDMA device requests are not accelerated");
+  enum { NV = 1, DCU = 2, KG = 4, CORE = 8, MEM = 16, RATIO = 32 };
+  unsigned comb = 0;
+  for (int r = 0; r < 6; ++r)
+    if (q[r]) comb |= 1u << r;  // KG_DEV_* order = flag order
+  if (!comb) {
+    d.skip = 1;
+    return 0;
+  }
+  auto pct_ok = [](int64_t v) { return !(v > 100 && v % 100 != 0); };
+  if ((q[KG_DEV_KOORD_GPU] && !pct_ok(q[KG_DEV_KOORD_GPU])) || (q[KG_DEV_GPU_CORE] && !pct_ok(q[KG_DEV_GPU_CORE])) ||
+      (q[KG_DEV_GPU_MEMORY_RATIO] && !pct_ok(q[KG_DEV_GPU_MEMORY_RATIO]))) {
+    d.error = 1;
+    return 0;
+  }
+  if (q[KG_DEV_NVIDIA_GPU] > (1 << 20) || q[KG_DEV_HYGON_DCU] > (1 << 20) || q[KG_DEV_KOORD_GPU] > (1 << 27) ||
+      q[KG_DEV_GPU_CORE] > (1 << 27) || q[KG_DEV_GPU_MEMORY_RATIO] > (1 << 27) || q[KG_DEV_GPU_MEMORY] > (1ll << 50))
+    return fail(KG_E_UNSUPPORTED, "device request beyond the accelerated range");
+  switch (comb) {
+    case NV: d.core = d.ratio = q[KG_DEV_NVIDIA_GPU] * 100; break;
+    case DCU: d.core = d.ratio = q[KG_DEV_HYGON_DCU] * 100; break;
+    case KG: d.core = d.ratio = q[KG_DEV_KOORD_GPU]; break;
+    case MEM: d.mem = q[KG_DEV_GPU_MEMORY]; d.has_mem = 1; break;
+    case RATIO: d.ratio = q[KG_DEV_GPU_MEMORY_RATIO]; break;
+    case CORE | MEM: d.core = q[KG_DEV_GPU_CORE]; d.mem = q[KG_DEV_GPU_MEMORY]; d.has_mem = 1; break;
+    case CORE | RATIO: d.core = q[KG_DEV_GPU_CORE]; d.ratio = q[KG_DEV_GPU_MEMORY_RATIO]; break;
+    default: d.error = 1;  // "invalid resource device requests"
+  }
+  return 0;
+}
+
+// One node's Device object + deviceUsed → device row (buildDeviceResources, device_cache.go:505-523)
+int decode_node_device(const kg_node_device& n, DsNode& d) {
+  std::memset(&d, 0, sizeof(d));
+  d.first = -1;
+  d.has_device = n.has_device ? 1 : 0;
+  if (!n.has_device) return 0;
+  for (int m = 0; m < KG_MAX_MINORS; ++m) {
+    if (!n.present[m]) continue;
+    const int64_t v[6] = {n.total_core[m], n.total_ratio[m], n.used_core[m], n.used_ratio[m], n.total_memory[m], n.used_memory[m]};
+    for (int k = 0; k < 6; ++k) {
+      if (v[k] < 0) return fail(KG_E_INVALID, "negative device quantity");
+      if (v[k] >= (k < 4 ? (1ll << 30) : (1ll << 50))) return fail(KG_E_UNSUPPORTED, "device quantity beyond the accelerated range");
+    }
+    d.present |= 1 << m;
+    if (n.healthy[m]) {
+      d.tcore[m] = (int32_t)n.total_core[m];
+      d.tratio[m] = (int32_t)n.total_ratio[m];
+      d.tmem[m] = n.total_memory[m];
+    }
+    d.ucore[m] = (int32_t)n.used_core[m];
+    d.uratio[m] = (int32_t)n.used_ratio[m];
+    d.umem[m] = n.used_memory[m];
+    if (d.first < 0 && (d.tcore[m] || d.tratio[m] || d.tmem[m])) {
+      if (d.tmem[m] == 0) return fail(KG_E_UNSUPPORTED, "first healthy GPU without gpu-memory (fillGPUTotalMem divides by it)");
+      d.first = m;
+    }
+  }
+  return 0;
+}
+
 // Static columns (alloc_cpu, alloc_mem, la_alloc_cpu, la_alloc_mem | alloc_pods, flags) from host mirror.
 uint32_t node_flags(const kg_engine* e, int64_t i) {
   const kg_node& n = e->nodes[i];
@@ -1537,6 +1990,7 @@ RoundGeom geometry(const kg_engine* e) {
   g.bitmap_words = (int)(((std::max<int64_t>(g.N, 1) + 127) / 128) * 4);  // whole 16-B stores
   g.pipelined = 2 * g.B - 1 <= kWave && e->P.monotone;
   if (e->numa_on) g.ppw = std::min(g.ppw, kNumaPpw);  // eval_round_numa parks ≤ kNumaPpw pods' values in LDS
+  if (e->ds_on) g.ppw = std::min(g.ppw, kDsPpw);      // the DeviceShare passes keep ≤ kDsPpw pods in registers
   return g;
 }
 
@@ -1672,6 +2126,41 @@ int run_batch(kg_engine* e, const RoundGeom& g, int64_t cur, int64_t end, int64_
   return 0;
 }
 
+// ---- DeviceShare rounds: cursor-driven, unpipelined, all on rs[0] ----
+size_t resolve_ds_lds_bytes(const RoundGeom& g, int nb) {
+  return ((size_t)nb * (kCandStride + kPodWords + kDsPodWords + kDsNodeWords) + (size_t)2 * kWave * kDsNodeWords) * 8 +
+         (size_t)nb * sizeof(Row) + (size_t)g.bitmap_words * 4;
+}
+
+void launch_round_ds(kg_engine* e, const RoundGeom& g, int64_t end, hipStream_t st, int which = -1) {
+  const DsTable DT{e->ds_d.p};
+  const dim3 grid = eval_grid(g, g.B);
+  if (which < 0 || which == 3)
+    ds_max_round<<<grid, kWave * kEvalWaves, 0, st>>>(e->T, DT, e->pods.p, e->dpods.p, e->cursor.p, end, g.B, g.ppw,
+                                                       g.n_local, g.nt_local, e->P, e->DP, e->dsmax.p);
+  if (which < 0 || which == 4)
+    ds_norm_reduce<<<g.B, 256, 0, st>>>(e->cursor.p, end, g.B, e->dsmax.p, g.nt_local, e->dsnorm.p);
+  if (which < 0 || which == 0)
+    eval_round_ds<<<grid, kWave * kEvalWaves, 0, st>>>(e->T, DT, e->pods.p, e->dpods.p, e->cursor.p, end, g.B, g.ppw,
+                                                        g.n_local, g.nt_local, e->P, e->DP, e->dsnorm.p,
+                                                        lists_slot(e, g, 0));
+  if (which < 0 || which == 1) launch_merge_local(e, g, g.B, 0, st);
+  if (which < 0 || which == 2)
+    resolve_round_ds<<<1, kWave, resolve_ds_lds_bytes(g, g.B), st>>>(e->T, DT, e->pods.p, e->dpods.p, e->cursor.p,
+                                                                     end, g.B, cand_slot(e, g, 0), e->dsnorm.p, e->P,
+                                                                     e->DP, e->out_keys.p, e->out_minors.p,
+                                                                     g.bitmap_words);
+}
+
+int run_batch_ds(kg_engine* e, const RoundGeom& g, int64_t end, int64_t n_rounds) {
+  for (int64_t r = 0; r < n_rounds; ++r) {
+    launch_round_ds(e, g, end, e->rs[0]);
+    HIP_TRY(hipGetLastError());
+  }
+  HIP_TRY(hipStreamSynchronize(e->rs[0]));
+  return 0;
+}
+
 int prepare_rounds(kg_engine* e, RoundGeom& g) {
   if (int rc = sync_static(e)) return rc;
   g = geometry(e);
@@ -1683,6 +2172,10 @@ int prepare_rounds(kg_engine* e, RoundGeom& g) {
   if (int rc = e->cand.ensure((size_t)2 * g.B * kCandStride)) return rc;
   if (e->n_ranks > 1)
     if (int rc = e->gathered.ensure((size_t)2 * e->n_ranks * g.B * kCandStride)) return rc;
+  if (e->ds_on) {
+    if (int rc = e->dsmax.ensure((size_t)g.B * g.nt_local)) return rc;
+    if (int rc = e->dsnorm.ensure((size_t)g.B)) return rc;
+  }
   return 0;
 }
 
@@ -1707,6 +2200,7 @@ int64_t kg_abi_struct_size(int which) {
     case 3: return sizeof(kg_pod);
     case 4: return sizeof(kg_stats);
     case 5: return sizeof(kg_node_numa);
+    case 6: return sizeof(kg_node_device);
   }
   return -1;
 }
@@ -1831,11 +2325,30 @@ int kg_engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank, int
   e->P.la_filter = (int)(c.la_filter != 0);
   e->P.la_score = (int)(c.la_score != 0);
   e->numa_on = c.numa_filter || c.numa_score;
+  e->ds_on = c.ds_filter || c.ds_score;
+  if (e->ds_on && n_ranks > 1) return bail(fail(KG_E_UNSUPPORTED, "DeviceShare profiles run on one rank"));
   const int64_t max_total = 100 * ((c.fit_score ? c.weight_fit : 0) + (c.la_score ? c.weight_loadaware : 0) +
-                                   (c.numa_score ? c.weight_numa : 0));
+                                   (c.numa_score ? c.weight_numa : 0) + (c.ds_score ? c.weight_deviceshare : 0));
   e->P.score_bits = (int32_t)bits_for(max_total);
   // NodeResourcesFit + LoadAwareScheduling: assume only lowers a node's key; NodeNUMAResource does not
-  e->P.monotone = e->numa_on ? 0 : 1;
+  e->P.monotone = (e->numa_on || e->ds_on) ? 0 : 1;  // DeviceShare: normalization couples every node's key
+  e->DP.filter = (int32_t)(c.ds_filter != 0);
+  e->DP.score = (int32_t)(c.ds_score != 0);
+  e->DP.weight = (int32_t)c.weight_deviceshare;
+  e->DP.w_core = (int32_t)c.ds_scoring_weights[0];
+  e->DP.w_mem = (int32_t)c.ds_scoring_weights[1];
+  e->DP.w_ratio = (int32_t)c.ds_scoring_weights[2];
+  if (e->ds_on) {
+    if (int rc = e->ds_d.ensure(cap)) return bail(rc);
+    e->ds_host.assign(cap, DsNode{});
+    for (auto& d : e->ds_host) d.first = -1;
+    if (hipMemcpy(e->ds_d.p, e->ds_host.data(), cap * sizeof(DsNode), hipMemcpyHostToDevice) != hipSuccess)
+      return bail(fail(KG_E_DEVICE, "hipMemcpy"));
+    const int lds = (int)(kMaxNodes / 8 + ((size_t)32 * (kCandStride + kPodWords + kDsPodWords + kDsNodeWords) +
+                                           (size_t)2 * kWave * kDsNodeWords) * 8 + 32 * sizeof(Row));
+    if (hipFuncSetAttribute((const void*)resolve_round_ds, hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess)
+      return bail(fail(KG_E_DEVICE, "hipFuncSetAttribute(resolve_round_ds LDS)"));
+  }
   e->NP.filter = (int32_t)(c.numa_filter != 0);
   e->NP.score = (int32_t)(c.numa_score != 0);
   e->NP.weight = (int32_t)c.weight_numa;
@@ -1914,6 +2427,11 @@ void kg_engine_destroy(kg_engine* e) {
   e->numa_m.release();
   e->npods.release();
   e->out_cpus.release();
+  e->ds_d.release();
+  e->dpods.release();
+  e->out_minors.release();
+  e->dsmax.release();
+  e->dsnorm.release();
   e->scratch64.release();
   e->scratch32.release();
   if (e->stream) (void)hipStreamDestroy(e->stream);
@@ -2026,6 +2544,22 @@ int kg_pods_stage(kg_engine* e, const kg_pod* pods, int64_t n) {
     if (n > 0) HIP_TRY(hipMemcpyAsync(e->npods.p, hn.data(), n * sizeof(NumaPod), hipMemcpyHostToDevice, e->stream));
     HIP_TRY(hipMemsetAsync(e->out_cpus.p, 0, (n + kMaxB) * kCpuWords * 8, e->stream));
   }
+  std::vector<DsPod> hd;
+  if (e->ds_on) {
+    hd.resize(std::max<int64_t>(n, 1));
+    for (int64_t k = 0; k < n; ++k)
+      if (int rc = decode_ds_pod(pods[k], hd[k])) return rc;
+    if (int rc = e->dpods.ensure(n + kMaxB)) return rc;
+    if (int rc = e->out_minors.ensure(n + kMaxB)) return rc;
+    if (n > 0) HIP_TRY(hipMemcpyAsync(e->dpods.p, hd.data(), n * sizeof(DsPod), hipMemcpyHostToDevice, e->stream));
+    HIP_TRY(hipMemsetAsync(e->out_minors.p, 0, (n + kMaxB) * 4, e->stream));
+  } else {
+    for (int64_t k = 0; k < n; ++k)
+      for (int r = 0; r < KG_DEV_RES_MAX; ++r)
+        if (pods[k].device_requests[r] != 0 && e->cfg.fit_filter)
+          return fail(KG_E_UNSUPPORTED, "pod %lld requests devices; the profile has no DeviceShare (NodeResourcesFit on "
+                      "device resources is not accelerated)", (long long)k);
+  }
   HIP_TRY(hipStreamSynchronize(e->stream));
   e->n_staged = n;
   return 0;
@@ -2045,8 +2579,9 @@ int kg_pods_schedule_staged(kg_engine* e, int64_t first, int64_t count, kg_stats
   int64_t cur = first;
   while (cur < end) {
     // a round that stops early poisons the rest of its batch; the next batch restarts from the device cursor
+    // (DeviceShare rounds read the cursor themselves: an early stop only shortens that round)
     const int64_t n_rounds = std::min<int64_t>((end - cur + g.B - 1) / g.B, kMaxBatchRounds);
-    if (int rc = run_batch(e, g, cur, end, n_rounds)) return rc;
+    if (int rc = e->ds_on ? run_batch_ds(e, g, end, n_rounds) : run_batch(e, g, cur, end, n_rounds)) return rc;
     HIP_TRY(hipMemcpy(host_stats, e->cursor.p, 6 * 8, hipMemcpyDeviceToHost));
     if (host_stats[5]) return fail(KG_E_DEVICE, "resolver chain wait timed out (round sequence %lld)", (long long)host_stats[4]);
     cur = host_stats[0];
@@ -2238,8 +2773,85 @@ int kg_pods_evaluate_numa(kg_engine* e, const kg_pod* pod, int32_t* out_pass, in
   return 0;
 }
 
+int kg_nodes_device_upsert(kg_engine* e, const kg_node_device* dev, const int32_t* idx, int64_t n) {
+  if (!e || (n > 0 && (!dev || !idx))) return fail(KG_E_INVALID, "null argument");
+  if (!e->ds_on) return fail(KG_E_INVALID, "the profile does not enable DeviceShare");
+  if (n == 0) return 0;
+  std::vector<DsNode> h(n);
+  for (int64_t k = 0; k < n; ++k) {
+    if (idx[k] < 0 || idx[k] >= e->capacity) return fail(KG_E_INVALID, "node index %d outside capacity", idx[k]);
+    if (int rc = decode_node_device(dev[k], h[k])) return rc;
+  }
+  DevBuf<uint8_t> b;
+  if (int rc = b.ensure(n * (sizeof(DsNode) + 4))) return rc;
+  DsNode* dd = reinterpret_cast<DsNode*>(b.p);
+  int32_t* di = reinterpret_cast<int32_t*>(b.p + n * sizeof(DsNode));
+  HIP_TRY(hipMemcpyAsync(dd, h.data(), n * sizeof(DsNode), hipMemcpyHostToDevice, e->stream));
+  HIP_TRY(hipMemcpyAsync(di, idx, n * 4, hipMemcpyHostToDevice, e->stream));
+  scatter_ds<<<(unsigned)((n + 255) / 256), 256, 0, e->stream>>>(DsTable{e->ds_d.p}, dd, di, n);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  b.release();
+  return 0;
+}
+
+int kg_nodes_read_device(kg_engine* e, int64_t* used_core, int64_t* used_memory, int64_t* used_ratio) {
+  if (!e) return fail(KG_E_INVALID, "engine is NULL");
+  if (!e->ds_on) return fail(KG_E_INVALID, "the profile does not enable DeviceShare");
+  const int64_t n = e->n_nodes;
+  if (n == 0) return 0;
+  std::vector<DsNode> h(n);
+  HIP_TRY(hipMemcpyAsync(h.data(), e->ds_d.p, n * sizeof(DsNode), hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  for (int64_t i = 0; i < n; ++i)
+    for (int m = 0; m < KG_MAX_MINORS; ++m) {
+      if (used_core) used_core[i * KG_MAX_MINORS + m] = h[i].ucore[m];
+      if (used_memory) used_memory[i * KG_MAX_MINORS + m] = h[i].umem[m];
+      if (used_ratio) used_ratio[i * KG_MAX_MINORS + m] = h[i].uratio[m];
+    }
+  return 0;
+}
+
+int kg_results_fetch_devices(kg_engine* e, int64_t first, int64_t count, int32_t* out_minor_mask) {
+  if (!e || (count > 0 && !out_minor_mask)) return fail(KG_E_INVALID, "null argument");
+  if (first < 0 || count < 0 || first + count > e->n_staged) return fail(KG_E_INVALID, "staged range");
+  if (!e->ds_on) {
+    std::memset(out_minor_mask, 0, (size_t)count * 4);
+    return 0;
+  }
+  if (count > 0) {
+    HIP_TRY(hipMemcpyAsync(out_minor_mask, e->out_minors.p + first, count * 4, hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+  }
+  return 0;
+}
+
+int kg_pods_evaluate_device(kg_engine* e, const kg_pod* pod, int32_t* out_pass, int64_t* out_score) {
+  if (!e || !pod) return fail(KG_E_INVALID, "null argument");
+  if (!e->ds_on) return fail(KG_E_INVALID, "the profile does not enable DeviceShare");
+  DsPod dp;
+  if (int rc = decode_ds_pod(*pod, dp)) return rc;
+  const int64_t n = e->n_nodes;
+  if (n == 0) return 0;
+  if (int rc = e->scratch64.ensure(n + kDsPodWords)) return rc;
+  if (int rc = e->scratch32.ensure(n)) return rc;
+  DsPod* d = reinterpret_cast<DsPod*>(e->scratch64.p + n);
+  HIP_TRY(hipMemcpyAsync(d, &dp, sizeof(dp), hipMemcpyHostToDevice, e->stream));
+  evaluate_pod_ds<<<(unsigned)((n + 255) / 256), 256, 0, e->stream>>>(DsTable{e->ds_d.p}, d, n, e->DP, e->scratch32.p,
+                                                                      e->scratch64.p);
+  HIP_TRY(hipGetLastError());
+  std::vector<int32_t> ps(n);
+  std::vector<int64_t> sc(n);
+  HIP_TRY(hipMemcpyAsync(ps.data(), e->scratch32.p, n * 4, hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipMemcpyAsync(sc.data(), e->scratch64.p, n * 8, hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  if (out_pass) std::memcpy(out_pass, ps.data(), n * 4);
+  if (out_score) std::memcpy(out_score, sc.data(), n * 8);
+  return 0;
+}
+
 int kg_bench_kernel(kg_engine* e, int which, int iters, double* avg_ms, double* algo_bytes) {
-  if (!e || iters <= 0 || which < 0 || which > 2) return fail(KG_E_INVALID, "bad argument");
+  if (!e || iters <= 0 || which < 0 || which > (e && e->ds_on ? 4 : 2)) return fail(KG_E_INVALID, "bad argument");
   if (e->n_staged <= 0) return fail(KG_E_INVALID, "stage a pod queue first");
   RoundGeom g;
   if (int rc = prepare_rounds(e, g)) return rc;
@@ -2247,7 +2859,9 @@ int kg_bench_kernel(kg_engine* e, int which, int iters, double* avg_ms, double* 
   // snapshot the mutable columns: the resolver writes rows back, replays must start from the same state
   const size_t bytes64 = (size_t)e->capacity * 8;
   DevBuf<int64_t> save;
-  if (int rc = save.ensure((9 + (e->numa_on ? sizeof(NumaMut) / 8 : 0)) * e->capacity)) return rc;
+  if (int rc = save.ensure((9 + (e->numa_on ? sizeof(NumaMut) / 8 : 0) + (e->ds_on ? sizeof(DsNode) / 8 : 0)) *
+                           e->capacity))
+    return rc;
   int64_t* mut64[8] = {e->T.req_cpu, e->T.req_mem, e->T.nz_cpu, e->T.nz_mem,
                        e->T.la_used_cpu, e->T.la_used_mem, e->T.la_pused_cpu, e->T.la_pused_mem};
   auto snapshot = [&](bool restore) -> int {
@@ -2263,13 +2877,20 @@ int kg_bench_kernel(kg_engine* e, int which, int iters, double* avg_ms, double* 
       HIP_TRY(hipMemcpyAsync(restore ? e->numa_m.p : m, restore ? m : e->numa_m.p, e->capacity * sizeof(NumaMut),
                              hipMemcpyDeviceToDevice, e->stream));
     }
+    if (e->ds_on) {
+      DsNode* m = reinterpret_cast<DsNode*>(save.p + 9 * e->capacity);
+      HIP_TRY(hipMemcpyAsync(restore ? e->ds_d.p : m, restore ? m : e->ds_d.p, e->capacity * sizeof(DsNode),
+                             hipMemcpyDeviceToDevice, e->stream));
+    }
     return 0;
   };
   static const int64_t zero4[6] = {0, 0, 0, 0, 0, 0};
   const int nb = (int)end;
   if (int rc = snapshot(false)) return rc;
   HIP_TRY(hipMemcpyAsync(e->cursor.p, zero4, 48, hipMemcpyHostToDevice, e->stream));
-  if (int rc = run_batch(e, g, 0, end, 1)) return rc;  // one real round: valid lists and candidates to replay on
+  // one real round: valid lists and candidates to replay on
+  if (int rc = e->ds_on ? (launch_round_ds(e, g, end, e->stream), 0) : run_batch(e, g, 0, end, 1)) return rc;
+  HIP_TRY(hipGetLastError());
   if (int rc = snapshot(true)) return rc;
   hipEvent_t a, b;
   HIP_TRY(hipEventCreate(&a));
@@ -2278,7 +2899,8 @@ int kg_bench_kernel(kg_engine* e, int which, int iters, double* avg_ms, double* 
   for (int it = 0; it < iters; ++it) {
     HIP_TRY(hipMemcpyAsync(e->cursor.p, zero4, 48, hipMemcpyHostToDevice, e->stream));
     HIP_TRY(hipEventRecord(a, e->stream));
-    if (which == 0) launch_eval(e, g, 0, nb, 0, e->stream);
+    if (e->ds_on) launch_round_ds(e, g, end, e->stream, which);
+    else if (which == 0) launch_eval(e, g, 0, nb, 0, e->stream);
     else if (which == 1) launch_merge_local(e, g, nb, 0, e->stream);
     else launch_resolve(e, g, 0, nb, -1, 0, 1, 0, e->stream);
     HIP_TRY(hipGetLastError());
@@ -2300,8 +2922,11 @@ int kg_bench_kernel(kg_engine* e, int which, int iters, double* avg_ms, double* 
     // eval: SURVEY §8(d) per-evaluation bytes (Fit 56 B + LoadAware 20 B = 76 B per node) × pods × nodes,
     //       + the candidate lists written;  merge: lists read + records written;  resolve: records + pods read.
     // NUMA profiles add the node's NumaStatic + NumaMut (232 B) to every evaluation
-    const double per_node = kAlgoBytesPerNode + (e->numa_on ? (double)(sizeof(NumaStatic) + sizeof(NumaMut)) : 0.0);
-    if (which == 0) *algo_bytes = nbd * (double)g.n_local * per_node + nbd * g.nt_local * kR * 8.0 + nbd * 96.0;
+    const double per_node = kAlgoBytesPerNode + (e->numa_on ? (double)(sizeof(NumaStatic) + sizeof(NumaMut)) : 0.0) +
+                            (e->ds_on ? (double)sizeof(DsNode) : 0.0);
+    if (which == 3) *algo_bytes = nbd * (double)g.n_local * per_node + nbd * g.nt_local * 8.0;
+    else if (which == 4) *algo_bytes = nbd * g.nt_local * 8.0 + nbd * 8.0;
+    else if (which == 0) *algo_bytes = nbd * (double)g.n_local * per_node + nbd * g.nt_local * kR * 8.0 + nbd * 96.0;
     else if (which == 1) *algo_bytes = nbd * g.nt_local * kR * 8.0 + nbd * kCandStride * 8.0;
     else *algo_bytes = nbd * kCandStride * 8.0 + nbd * 96.0;
   }

@@ -97,6 +97,12 @@ class Engine:
         idx = self._idx(idx, len(node_numa))
         check(self.lib, self.lib.kg_nodes_numa_upsert(self.h, ptr(node_numa), ptr(idx), len(node_numa)))
 
+    def upsert_devices(self, node_device: np.ndarray, idx=None):
+        """DeviceShare GPU state (Device object + deviceUsed) of nodes `idx` (kg_nodes_device_upsert)."""
+        node_device = np.ascontiguousarray(node_device, dtype=abi.NODE_DEVICE_DTYPE)
+        idx = self._idx(idx, len(node_device))
+        check(self.lib, self.lib.kg_nodes_device_upsert(self.h, ptr(node_device), ptr(idx), len(node_device)))
+
     # -- hot path -----------------------------------------------------------------------------------------
     def schedule(self, pods: np.ndarray):
         """Sequential FIFO scheduling with assume; returns (node_idx[-1 = unschedulable], total_score, stats)."""
@@ -142,6 +148,28 @@ class Engine:
         af = np.zeros(n, dtype=np.int64)
         check(self.lib, self.lib.kg_pods_evaluate_numa(self.h, ptr(pod), ptr(ok), ptr(sc), ptr(af)))
         return ok, sc, af
+
+    def evaluate_device(self, pod: np.ndarray):
+        """DeviceShare alone on every node: (passes Filter, raw Score before NormalizeScore)."""
+        pod = np.ascontiguousarray(np.asarray(pod, dtype=abi.POD_DTYPE).reshape(1))
+        n = self.num_nodes
+        ok = np.zeros(n, dtype=np.int32)
+        sc = np.zeros(n, dtype=np.int64)
+        check(self.lib, self.lib.kg_pods_evaluate_device(self.h, ptr(pod), ptr(ok), ptr(sc)))
+        return ok, sc
+
+    def fetch_devices(self, first: int, count: int) -> np.ndarray:
+        """int32[count]: the GPU minor bitmask DeviceShare Reserve allocated to each staged pod (0 = none)."""
+        out = np.zeros(count, dtype=np.int32)
+        check(self.lib, self.lib.kg_results_fetch_devices(self.h, int(first), int(count), ptr(out)))
+        return out
+
+    def read_devices(self):
+        """(used core, used memory, used ratio), int64[n, 8] each, from the device."""
+        n = self.num_nodes
+        out = [np.zeros((n, abi.MAX_MINORS), dtype=np.int64) for _ in range(3)]
+        check(self.lib, self.lib.kg_nodes_read_device(self.h, *[ptr(o) for o in out]))
+        return tuple(out)
 
     def fetch_cpusets(self, first: int, count: int) -> np.ndarray:
         """uint64[count, 4]: the cpuset NodeNUMAResource Reserve allocated to each staged pod (empty = none)."""

@@ -27,6 +27,7 @@ from .quantity import resource_value
 
 SUCCESS, UNSCHEDULABLE = "Success", "Unschedulable"
 NODE_RESOURCES_FIT, LOAD_AWARE, NODE_NUMA_RESOURCE = "NodeResourcesFit", "LoadAwareScheduling", "NodeNUMAResource"
+DEVICE_SHARE = "DeviceShare"
 
 
 def _slots(d: dict | None, absent=0) -> np.ndarray:
@@ -63,6 +64,15 @@ class NodeNUMAResourceArgs:
 
 
 @dataclass
+class DeviceShareArgs:
+    """pkg/scheduler/apis/config/types.go DeviceShareArgs; defaults v1beta2/defaults.go:187-208 (LeastAllocated on
+    gpu-memory-ratio / rdma / fpga, weight 1 — rdma and fpga weights only touch RDMA / FPGA devices)."""
+    scoring_strategy: str = "LeastAllocated"
+    scoring_resources: dict = field(default_factory=lambda: {"koordinator.sh/gpu-memory-ratio": 1,
+                                                             "koordinator.sh/rdma": 1, "koordinator.sh/fpga": 1})
+
+
+@dataclass
 class Profile:
     filter: tuple = (NODE_RESOURCES_FIT, LOAD_AWARE)
     score: dict = field(default_factory=lambda: {NODE_RESOURCES_FIT: 1, LOAD_AWARE: 1})
@@ -70,11 +80,13 @@ class Profile:
 
 def build_config(la: LoadAwareSchedulingArgs | None = None, fit: NodeResourcesFitArgs | None = None,
                  profile: Profile | None = None, batch_pods: int = 32, pods_per_wave: int = 8,
-                 device_id: int = -1, numa: NodeNUMAResourceArgs | None = None) -> np.ndarray:
+                 device_id: int = -1, numa: NodeNUMAResourceArgs | None = None,
+                 deviceshare: DeviceShareArgs | None = None) -> np.ndarray:
     la = la or LoadAwareSchedulingArgs()
     fit = fit or NodeResourcesFitArgs()
     profile = profile or Profile()
     numa = numa or NodeNUMAResourceArgs()
+    ds = deviceshare or DeviceShareArgs()
     c = np.zeros(1, dtype=abi.CONFIG_DTYPE)
     r = c[0]
     r["abi_version"] = abi.ABI_VERSION
@@ -104,6 +116,13 @@ def build_config(la: LoadAwareSchedulingArgs | None = None, fit: NodeResourcesFi
     r["numa_numa_scoring_strategy"] = abi.STRATEGY[numa.numa_scoring_strategy]
     r["numa_numa_scoring_weights"] = [numa.numa_scoring_resources.get("cpu", 0),
                                       numa.numa_scoring_resources.get("memory", 0)]
+    r["ds_filter"] = int(DEVICE_SHARE in profile.filter)
+    r["ds_score"] = int(DEVICE_SHARE in profile.score)
+    r["weight_deviceshare"] = int(profile.score.get(DEVICE_SHARE, 0))
+    r["ds_scoring_strategy"] = abi.STRATEGY[ds.scoring_strategy]
+    r["ds_scoring_weights"] = [ds.scoring_resources.get("koordinator.sh/gpu-core", 0),
+                               ds.scoring_resources.get("koordinator.sh/gpu-memory", 0),
+                               ds.scoring_resources.get("koordinator.sh/gpu-memory-ratio", 0)]
     return c
 
 
@@ -198,9 +217,26 @@ def cpuset_of(words) -> list:
     return out
 
 
+def make_node_device(gpus: list | None = None, has_device: bool = True) -> np.ndarray:
+    """DeviceShare view of one node: gpus = [{"minor": m, "healthy": True, "total": {core, memory, ratio},
+    "used": {core, memory, ratio}}, ...] in koordinator.sh/gpu-* units (core / ratio percent, memory bytes)."""
+    d = np.zeros(1, dtype=abi.NODE_DEVICE_DTYPE)
+    r = d[0]
+    r["has_device"] = int(has_device)
+    for g in gpus or []:
+        m = int(g["minor"])
+        r["present"][m] = 1
+        r["healthy"][m] = int(g.get("healthy", True))
+        t, u = g.get("total", {}), g.get("used", {})
+        r["total_core"][m], r["total_memory"][m], r["total_ratio"][m] = t.get("core", 0), t.get("memory", 0), t.get("ratio", 0)
+        r["used_core"][m], r["used_memory"][m], r["used_ratio"][m] = u.get("core", 0), u.get("memory", 0), u.get("ratio", 0)
+    return d
+
+
 def make_pod(requests: dict | None = None, limits: dict | None = None, priority_class: str = "",
              daemonset: bool = False, nonzero: tuple | None = None, qos: str = "",
-             required_cpu_bind_policy: str = "", preferred_cpu_bind_policy: str = "") -> np.ndarray:
+             required_cpu_bind_policy: str = "", preferred_cpu_bind_policy: str = "",
+             devices: dict | None = None) -> np.ndarray:
     """One single-container pod. nonzero = schedutil.GetNonzeroRequests (100m / 200MiB defaults); qos = the
     koordinator.sh/qosClass label; *_cpu_bind_policy = the scheduling.koordinator.sh/resource-spec annotation."""
     p = np.zeros(1, dtype=abi.POD_DTYPE)
@@ -216,6 +252,8 @@ def make_pod(requests: dict | None = None, limits: dict | None = None, priority_
     r["qos"] = abi.QOS[qos]
     r["required_cpu_bind_policy"] = abi.BIND[required_cpu_bind_policy]
     r["preferred_cpu_bind_policy"] = abi.BIND[preferred_cpu_bind_policy]
+    for k, v in (devices or {}).items():  # device resources: PodRequestsAndLimits of e.g. koordinator.sh/gpu-core
+        r["device_requests"][abi.DEVICE_RESOURCE_SLOTS[k]] = int(v)
     return p
 
 

@@ -235,3 +235,53 @@ def make_numa_pods(n_pods: int, seed: int = BASE_SEED + 5) -> np.ndarray:
 def load_numa_into(engine, cluster: Cluster, numa: np.ndarray):
     load_into(engine, cluster)
     engine.upsert_numa(numa)
+
+
+# ---- config C5 (DeviceShare part): GPU nodes, GPU-sharing pods ------------------------------------------------
+GPU_MEM = 80 * GI
+
+
+def make_gpu_cluster(n_nodes: int, seed: int = BASE_SEED + 6) -> tuple:
+    """(Cluster, kg_node_device[n]) for config C5's DeviceShare part: make_cluster's nodes and NodeMetrics, each
+    node with 8 GPUs (gpu-core 100, gpu-memory-ratio 100, gpu-memory 80 GiB) of which 0–60 % (in steps of 5)
+    is used per minor; 1 % of the GPUs unhealthy, 1 % of the nodes without a Device object."""
+    cluster = make_cluster(n_nodes, seed=seed)
+    rng = np.random.default_rng(seed + 1000)
+    n = n_nodes
+    dev = np.zeros(n, dtype=abi.NODE_DEVICE_DTYPE)
+    dev["has_device"] = rng.random(n) >= 0.01
+    dev["present"] = 1
+    dev["healthy"] = rng.random((n, abi.MAX_MINORS)) >= 0.01
+    dev["total_core"] = 100
+    dev["total_ratio"] = 100
+    dev["total_memory"] = GPU_MEM
+    used = rng.integers(0, 13, size=(n, abi.MAX_MINORS)) * 5
+    dev["used_core"] = used
+    dev["used_ratio"] = used
+    dev["used_memory"] = used * GPU_MEM // 100
+    for f in ("present", "healthy", "total_core", "total_ratio", "total_memory", "used_core", "used_ratio", "used_memory"):
+        dev[f][dev["has_device"] == 0] = 0  # no Device object: no device state at all
+    return cluster, dev
+
+
+def make_gpu_pods(n_pods: int, seed: int = BASE_SEED + 7) -> np.ndarray:
+    """Config C5 queue: make_pods' cpu/memory pods, 30 % of them also requesting GPU share — gpu-memory-ratio
+    ∈ {25, 50, 100, 200} with the same gpu-core (70 %), gpu-memory-ratio alone (20 %) or gpu-memory bytes (10 %)."""
+    p = make_pods(n_pods, seed=seed)
+    rng = np.random.default_rng(seed + 1000)
+    gpu = rng.random(n_pods) < 0.3
+    ratio = rng.choice(np.array([25, 50, 100, 200], dtype=np.int64), n_pods)
+    kind = rng.random(n_pods)
+    dr = p["device_requests"]
+    core_ratio = gpu & (kind < 0.7)
+    ratio_only = gpu & (kind >= 0.7) & (kind < 0.9)
+    mem_only = gpu & (kind >= 0.9)
+    dr[:, abi.DEV_GPU_CORE] = np.where(core_ratio, ratio, 0)
+    dr[:, abi.DEV_GPU_MEMORY_RATIO] = np.where(core_ratio | ratio_only, ratio, 0)
+    dr[:, abi.DEV_GPU_MEMORY] = np.where(mem_only, ratio * GPU_MEM // 100, 0)
+    return p
+
+
+def load_gpu_into(engine, cluster: Cluster, dev: np.ndarray):
+    load_into(engine, cluster)
+    engine.upsert_devices(dev)

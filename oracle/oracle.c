@@ -8,6 +8,7 @@
 #define _GNU_SOURCE
 #include "oracle.h"
 #include "numa.h"
+#include "deviceshare.h"
 
 #include <math.h>
 #include <pthread.h>
@@ -258,6 +259,9 @@ typedef struct sched_ctx {
   or_numa_node* numa;     /* per node NodeNUMAResource state (NULL: plugin not in the profile) */
   or_numa_pod numa_pod;   /* the pod's NodeNUMAResource preFilterState                          */
   or_hint* affinity;      /* per node: the topology manager's stored affinity (Filter → Score/Reserve) */
+  kg_node_device* dev;    /* per node DeviceShare state (NULL: plugin not in the profile)       */
+  or_ds_pod ds_pod;       /* the pod's DeviceShare preFilterState                               */
+  int64_t* ds_raw;        /* per node: DeviceShare Score before NormalizeScore                  */
   int32_t* feasible;      /* per node: 1 feasible, 0 not, -1 unsupported */
   int64_t* total;         /* weighted score per node                     */
   int64_t chunk;
@@ -281,6 +285,7 @@ static void eval_filter(sched_ctx* c, int64_t i) {
   }
   if (c->numa) c->affinity[i] = (or_hint){1, 0, 0, 0};
   if (ok && cfg->numa_filter && c->numa && !or_numa_filter(cfg, &c->numa[i], &c->numa_pod, &c->affinity[i])) ok = 0;
+  if (ok && cfg->ds_filter && c->dev && !or_ds_filter(&c->dev[i], &c->ds_pod)) ok = 0;
   c->feasible[i] = ok;
 }
 
@@ -298,6 +303,8 @@ static void eval_score(sched_ctx* c, int64_t i) {
     t += cfg->weight_numa * or_numa_score(cfg, &c->numa[i], &c->numa_pod, &c->affinity[i], c->st[i].requested[KG_RES_CPU],
                                           c->st[i].requested[KG_RES_MEMORY], c->nodes[i].allocatable[KG_RES_CPU],
                                           c->nodes[i].allocatable[KG_RES_MEMORY]);
+  if (c->dev) c->ds_raw[i] = cfg->ds_score ? or_ds_score(&c->dev[i], &c->ds_pod, (int)cfg->ds_scoring_strategy,
+                                                         cfg->ds_scoring_weights) : 0;
   c->total[i] = t;
 }
 
@@ -357,6 +364,14 @@ int or_schedule(const kg_config* cfg, int64_t n_nodes, const kg_node* nodes, con
 int or_schedule_numa(const kg_config* cfg, int64_t n_nodes, const kg_node* nodes, const kg_node_metric* metrics,
                      or_node_state* st, void* numa_states, int64_t n_pods, const kg_pod* pods, int64_t now,
                      int n_threads, int32_t* out_node, int64_t* out_score, uint64_t* out_cpus) {
+  return or_schedule_full(cfg, n_nodes, nodes, metrics, st, numa_states, NULL, n_pods, pods, now, n_threads, out_node,
+                          out_score, out_cpus, NULL);
+}
+
+int or_schedule_full(const kg_config* cfg, int64_t n_nodes, const kg_node* nodes, const kg_node_metric* metrics,
+                     or_node_state* st, void* numa_states, kg_node_device* dev, int64_t n_pods, const kg_pod* pods,
+                     int64_t now, int n_threads, int32_t* out_node, int64_t* out_score, uint64_t* out_cpus,
+                     int32_t* out_minors) {
   or_numa_node* numa = (or_numa_node*)numa_states;
   sched_ctx c;
   memset(&c, 0, sizeof(c));
@@ -364,6 +379,9 @@ int or_schedule_numa(const kg_config* cfg, int64_t n_nodes, const kg_node* nodes
   const int numa_on = numa && (cfg->numa_filter || cfg->numa_score);
   c.numa = numa_on ? numa : NULL;
   c.affinity = numa_on ? (or_hint*)calloc((size_t)(n_nodes > 0 ? n_nodes : 1), sizeof(or_hint)) : NULL;
+  const int ds_on = dev && (cfg->ds_filter || cfg->ds_score);
+  c.dev = ds_on ? dev : NULL;
+  c.ds_raw = ds_on ? (int64_t*)calloc((size_t)(n_nodes > 0 ? n_nodes : 1), sizeof(int64_t)) : NULL;
   c.feasible = (int32_t*)malloc(sizeof(int32_t) * (size_t)(n_nodes > 0 ? n_nodes : 1));
   c.total = (int64_t*)malloc(sizeof(int64_t) * (size_t)(n_nodes > 0 ? n_nodes : 1));
   if (!c.feasible || !c.total) { free(c.feasible); free(c.total); return KG_E_NOMEM; }
@@ -383,8 +401,22 @@ int or_schedule_numa(const kg_config* cfg, int64_t n_nodes, const kg_node* nodes
   for (int64_t p = 0; p < n_pods && rc == 0; p++) {
     c.pod = &pods[p];
     if (c.numa) or_numa_pod_init(cfg, c.pod, &c.numa_pod);
+    if (c.dev) {
+      or_ds_pod_init(c.pod, &c.ds_pod);
+      if (c.ds_pod.unsupported) { rc = KG_E_UNSUPPORTED; break; }
+    }
     run_phase(&c, 0);
     run_phase(&c, 1);
+    if (c.dev && cfg->ds_score) {
+      /* RunScorePlugins: DeviceShare NormalizeScore = DefaultNormalizeScore over the feasible nodes' scores,
+       * then × weight (scoring.go:95-97) */
+      int64_t mx = 0;
+      for (int64_t i = 0; i < n_nodes; i++)
+        if (c.feasible[i] == 1 && c.ds_raw[i] > mx) mx = c.ds_raw[i];
+      if (mx > 0)
+        for (int64_t i = 0; i < n_nodes; i++)
+          if (c.feasible[i] == 1) c.total[i] += cfg->weight_deviceshare * (100 * c.ds_raw[i] / mx);
+    }
     /* selectHost: max total, ties → lowest snapshot index (BASELINE determinism pin) */
     int64_t best = -1, best_score = 0;
     for (int64_t i = 0; i < n_nodes; i++) {
@@ -399,6 +431,12 @@ int or_schedule_numa(const kg_config* cfg, int64_t n_nodes, const kg_node* nodes
     if (best >= 0 && c.numa) {
       if (or_numa_reserve(cfg, &c.numa[best], &c.numa_pod, &c.affinity[best], &cpus) != 0) best = -1;
     }
+    int32_t minors = 0;
+    if (best >= 0 && c.dev) {
+      minors = or_ds_reserve(&c.dev[best], &c.ds_pod, (int)cfg->ds_scoring_strategy, cfg->ds_scoring_weights);
+      if (minors < 0) { minors = 0; best = -1; }
+    }
+    if (out_minors) out_minors[p] = minors;
     if (out_cpus)
       for (int w = 0; w < OR_CPUSET_WORDS; w++) out_cpus[p * OR_CPUSET_WORDS + w] = cpus.w[w];
     out_node[p] = (int32_t)best;
@@ -414,6 +452,7 @@ int or_schedule_numa(const kg_config* cfg, int64_t n_nodes, const kg_node* nodes
   free(c.feasible);
   free(c.total);
   free(c.affinity);
+  free(c.ds_raw);
   return rc;
 }
 

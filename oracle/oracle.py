@@ -70,8 +70,72 @@ def lib():
         L.or_numa_eval_flat.restype = i
         L.or_numa_reserve_flat.argtypes = [vp, vp, vp, vp]
         L.or_numa_reserve_flat.restype = i
+        L.or_schedule_full.argtypes = [vp, i64, vp, vp, vp, vp, vp, i64, vp, i64, i, vp, vp, vp, vp]
+        L.or_schedule_full.restype = i
+        L.or_ds_pod_init.argtypes = [vp, vp]
+        L.or_ds_pod_init.restype = i
+        L.or_ds_filter.argtypes = [vp, vp]
+        L.or_ds_filter.restype = i
+        L.or_ds_score.argtypes = [vp, vp, i, vp]
+        L.or_ds_score.restype = i64
+        L.or_ds_reserve.argtypes = [vp, vp, i, vp]
+        L.or_ds_reserve.restype = ctypes.c_int32
+        L.or_ds_memory_bytes_to_ratio.argtypes = [i64, i64]
+        L.or_ds_memory_bytes_to_ratio.restype = i64
+        L.or_ds_memory_ratio_to_bytes.argtypes = [i64, i64]
+        L.or_ds_memory_ratio_to_bytes.restype = i64
+        L.or_ds_instance_flat.argtypes = [vp, vp, vp]
+        L.or_ds_instance_flat.restype = i
         _lib = L
     return _lib
+
+
+DS_POD_DTYPE = np.dtype([("skip", np.int32), ("error", np.int32), ("unsupported", np.int32), ("has_mem", np.int32),
+                         ("core", np.int64), ("mem", np.int64), ("ratio", np.int64)])
+
+
+def ds_pod(pod) -> np.ndarray:
+    """DeviceShare preFilterState of one kg_pod (or_ds_pod_init)."""
+    out = np.zeros(1, dtype=DS_POD_DTYPE)
+    lib().or_ds_pod_init(p(np.ascontiguousarray(np.asarray(pod, dtype=abi.POD_DTYPE).reshape(1))), p(out))
+    return out
+
+
+def ds_instance(dev, pod):
+    """CalcDesiredRequestsAndCount on one node: None (Insufficient gpu devices) or (count, core, mem, ratio)."""
+    out = np.zeros(4, dtype=np.int64)
+    ok = lib().or_ds_instance_flat(p(np.ascontiguousarray(dev)), p(ds_pod(pod)), p(out))
+    return tuple(int(x) for x in out) if ok else None
+
+
+def ds_filter(dev, pod) -> bool:
+    return bool(lib().or_ds_filter(p(np.ascontiguousarray(dev)), p(ds_pod(pod))))
+
+
+def ds_score(cfg, dev, pod) -> int:
+    w = np.ascontiguousarray(cfg["ds_scoring_weights"].reshape(3), dtype=np.int64)
+    return int(lib().or_ds_score(p(np.ascontiguousarray(dev)), p(ds_pod(pod)), int(cfg["ds_scoring_strategy"]), p(w)))
+
+
+def ds_reserve(cfg, dev, pod) -> int:
+    """Reserve on one node (mutates `dev`, a 1-element NODE_DEVICE array): minor bitmask, 0 none, -1 failure."""
+    w = np.ascontiguousarray(cfg["ds_scoring_weights"].reshape(3), dtype=np.int64)
+    return int(lib().or_ds_reserve(p(dev), p(ds_pod(pod)), int(cfg["ds_scoring_strategy"]), p(w)))
+
+
+def schedule_full(cfg, nodes, metrics, st, pods, now_ns: int, n_threads: int = 1, numa_buf=None, devices=None):
+    """Sequential FIFO scheduling with the optional NodeNUMAResource / DeviceShare states (both mutated).
+    Returns (node, score, cpusets uint64[n, 4], GPU minor masks int32[n])."""
+    pods = np.ascontiguousarray(pods, dtype=abi.POD_DTYPE)
+    out_node = np.empty(len(pods), dtype=np.int32)
+    out_score = np.empty(len(pods), dtype=np.int64)
+    cpus = np.zeros((max(len(pods), 1), abi.MAX_CPUS // 64), dtype=np.uint64)
+    minors = np.zeros(max(len(pods), 1), dtype=np.int32)
+    rc = lib().or_schedule_full(p(cfg), len(nodes), p(nodes), p(metrics), p(st), p(numa_buf), p(devices), len(pods),
+                                p(pods), now_ns, n_threads, p(out_node), p(out_score), p(cpus), p(minors))
+    if rc != 0:
+        raise RuntimeError(f"oracle or_schedule_full failed: {rc}")
+    return out_node, out_score, cpus[:len(pods)], minors[:len(pods)]
 
 
 p = abi.ptr
