@@ -31,6 +31,9 @@
  *                           assigned-pod informer's updateCacheUsed (device_cache.go:124-135, eventhandler_pod.go).
  *   kg_pods_evaluate_device DeviceShare Filter + Score for one pod on every node (deviceshare/plugin.go:280-330,
  *                           scoring.go:34-89).
+ *   kg_quotas_set           ElasticQuota PreFilter/Reserve state: per quota used / non-preemptible used (QuotaInfo,
+ *                           elasticquota/core/quota_info.go) and usedLimit (getQuotaInfoUsedLimit: runtime or max,
+ *                           elasticquota/plugin_helper.go:237-246) + min, as the Go GroupQuotaManager holds them.
  *   kg_last_error           error text for the last failing call on this thread (maps to framework.NewStatus(Error,…)).
  *
  * Units follow the reference's getResourceValue (load_aware/helper.go:146-151): cpu-like resources in
@@ -122,7 +125,11 @@ enum {
 };
 
 /* pod flags */
-enum { KG_POD_DAEMONSET = 1 << 0 };
+enum {
+  KG_POD_DAEMONSET = 1 << 0,
+  KG_POD_NON_PREEMPTIBLE = 1 << 1   /* extension.IsPodNonPreemptible (ElasticQuota min check) */
+};
+#define KG_MAX_QUOTAS 64
 
 /* Engine configuration: plugin args + profile weights + engine tuning.  All int64 for a padding-free
  * layout.  A threshold/weight of 0 means "resource absent from the map". */
@@ -204,8 +211,21 @@ typedef struct kg_pod {
   int64_t required_cpu_bind_policy;            /* ResourceSpec annotation: KG_BIND_*                  */
   int64_t preferred_cpu_bind_policy;           /* ResourceSpec annotation: KG_BIND_*                  */
   int64_t device_requests[KG_DEV_RES_MAX];     /* PodRequestsAndLimits of the device resources (KG_DEV_*) */
-  int64_t reserved[3];
+  int64_t quota_id;                            /* 1 + index into the kg_quotas_set table; 0 = no ElasticQuota */
+  int64_t reserved[2];
 } kg_pod;
+
+/* One ElasticQuota as the plugin's PreFilter snapshot sees it (plugin.go:211-256): cpu (milli) and memory (bytes).
+ * used_limit = runtime when EnableRuntimeQuota else max (getQuotaInfoUsedLimit).  Runtime is refreshed from the
+ * quota tree's requests, which Reserve does not change, so it is fixed for a batch.  A limit / min of -1 = the
+ * resource is absent from that ResourceList: quotav1.LessThanOrEqual only compares keys of its second argument,
+ * so an absent key does not constrain. */
+typedef struct kg_quota {
+  int64_t used[2];
+  int64_t non_preemptible_used[2];
+  int64_t used_limit[2];
+  int64_t min[2];
+} kg_quota;
 
 /* DeviceShare view of one node's GPUs: the Device object's GPU entries (deviceshare/device_cache.go:505-523:
  * an unhealthy device has empty resources) + nodeDevice.deviceUsed from the pods already bound there.
@@ -321,6 +341,14 @@ int kg_results_fetch_devices(kg_engine* e, int64_t first, int64_t count, int32_t
  * (un-normalized) score, 0 where Filter rejects. */
 int kg_pods_evaluate_device(kg_engine* e, const kg_pod* pod, int32_t* out_pass, int64_t* out_score);
 
+/* ElasticQuota admission (engines whose pods carry quota_id): replaces the quota table (n ≤ KG_MAX_QUOTAS).
+ * Every scheduled pod runs PreFilter's check (used + request ≤ used_limit over the pod's cpu/memory requests; for
+ * non-preemptible pods also non_preemptible_used + request ≤ min) before its node search, and a placed pod is
+ * charged (ReservePod → updatePodUsedNoLock, core/group_quota_manager.go:613-648,791-797). */
+int kg_quotas_set(kg_engine* e, const kg_quota* quotas, int64_t n);
+/* Reads the DEVICE quota table back (used / non_preemptible_used after the batches so far). */
+int kg_quotas_read(kg_engine* e, kg_quota* out, int64_t n);
+
 /* Measurement hooks (bench.py): replays one device round's kernel `which` (0 = eval, 1 = merge, 2 = resolve) `iters` times
  * on the engine stream between HIP events, restoring state, and returns the mean duration in ms plus the
  * algorithmic bytes that kernel must move per launch. Requires a staged queue. */
@@ -346,7 +374,7 @@ int kg_debug_stamps(kg_engine* e, uint64_t* out);
 const char* kg_last_error(void);
 int kg_abi_version(void);
 /* sizeof of the ABI structs (0 kg_config, 1 kg_node, 2 kg_node_metric, 3 kg_pod, 4 kg_stats, 5 kg_node_numa,
- * 6 kg_node_device) for
+ * 6 kg_node_device, 7 kg_quota) for
  * binding checks. */
 int64_t kg_abi_struct_size(int which);
 

@@ -575,7 +575,7 @@ __global__ __launch_bounds__(kWave) void resolve_round(DevTable T, const DevPod*
                                                         uint64_t* __restrict__ out_keys, int bitmap_words,
                                                         const int32_t* __restrict__ prev_mod,
                                                         int32_t* __restrict__ my_mod, int32_t* __restrict__ poison,
-                                                        int64_t seq, int wait) {
+                                                        int64_t seq, int wait, DevQuota* __restrict__ quotas, int nq) {
   extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
   KG_STAMP(2, 0);
   const int lane = threadIdx.x;
@@ -642,6 +642,7 @@ __global__ __launch_bounds__(kWave) void resolve_round(DevTable T, const DevPod*
   __syncthreads();
   if (lane < n_prev) atomicOr(&bitmap[midx >> 5], 1u << (midx & 31));
   __syncthreads();
+  DevQuota ql = quota_load(quotas, nq, lane);  // after the chain wait: the previous resolver's charges are visible
   KG_STAMP(2, 1);
   // staged[q] on lane l: node whose hoisted row sits at staged slot s = q·64 + l (record s / kStaged,
   // position s % kStaged of that pod's list)
@@ -686,6 +687,12 @@ __global__ __launch_bounds__(kWave) void resolve_round(DevTable T, const DevPod*
     // the prefetched word predates the previous pod's bitmap update: patch with its winner
     const bool unmod = (key != 0) & !((word >> (node & 31)) & 1u) & (node != last_w);
     word_n = bitmap[key_n ? key_node(key_n) >> 5 : 0u];
+    if (nq > 0 && !quota_admit(ql, p)) {  // ElasticQuota PreFilter rejects: Unschedulable, no node search
+      my_out = lane == j ? 0 : my_out;
+      ++consumed;
+      last_w = 0xFFFFFFFFu;
+      continue;
+    }
     const uint64_t um = __ballot(unmod);
     const int pos = um ? (int)__builtin_ctzll(um) : kC;
     const uint64_t e = um ? readlane_u64(key, pos) : 0;
@@ -744,6 +751,7 @@ __global__ __launch_bounds__(kWave) void resolve_round(DevTable T, const DevPod*
       else add_delta(dl, p);
       touched = true;
     }
+    if (nq > 0) quota_charge(ql, p, lane);  // ElasticQuota Reserve
     if (j == 0 || j == 15 || j == 31) KG_STAMP(2, 2 + j / 8);
   }
   if (touched) {
@@ -754,6 +762,7 @@ __global__ __launch_bounds__(kWave) void resolve_round(DevTable T, const DevPod*
   const uint64_t lane_lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   if (touched) my_mod[1 + __popcll(tm & lane_lt)] = (int32_t)midx;
   if (lane < consumed) out_keys[first + lane] = my_out;
+  if (lane < nq) quotas[lane] = ql;
   KG_STAMP(2, 30);
   if (lane == 0) {
     my_mod[0] = __popcll(tm);
@@ -871,7 +880,8 @@ __global__ __launch_bounds__(kWave) void resolve_round_numa(DevTable T, NumaTabl
                                                              const uint64_t* __restrict__ cand, EvalParams P,
                                                              NumaParams NP, uint64_t* __restrict__ out_keys,
                                                              uint64_t* __restrict__ out_cpus, int bitmap_words,
-                                                             int32_t* __restrict__ poison, int64_t seq) {
+                                                             int32_t* __restrict__ poison, int64_t seq,
+                                                             DevQuota* __restrict__ quotas, int nq) {
   extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
   const int lane = threadIdx.x;
   uint64_t* s_cand = smem;                                    // [nb][kCandStride]
@@ -904,11 +914,17 @@ __global__ __launch_bounds__(kWave) void resolve_round_numa(DevTable T, NumaTabl
   bool touched = false;
   uint64_t my_out = 0;
   int nM = 0, consumed = 0;
+  DevQuota ql = quota_load(quotas, nq, lane);
   for (int j = 0; j < nb; ++j) {
     const uint64_t key = s_cand[(size_t)j * kCandStride + lane];
     const uint64_t ub = s_cand[(size_t)j * kCandStride + kC];
     const DevPod p = s_pods[j];
     const NumaPod np = s_np[j];
+    if (nq > 0 && !quota_admit(ql, p)) {  // ElasticQuota PreFilter rejects
+      my_out = lane == j ? 0 : my_out;
+      ++consumed;
+      continue;
+    }
     const uint32_t node = key_node(key);
     const bool unmod = (key != 0) && !((bitmap[node >> 5] >> (node & 31)) & 1u);
     const uint64_t um = __ballot(unmod);
@@ -974,6 +990,7 @@ __global__ __launch_bounds__(kWave) void resolve_round_numa(DevTable T, NumaTabl
       }
     }
     placed = __builtin_amdgcn_readlane(placed, owner);
+    if (placed && nq > 0) quota_charge(ql, p, lane);
     my_out = lane == j ? (placed ? best : 0) : my_out;
     __syncthreads();
   }
@@ -982,6 +999,7 @@ __global__ __launch_bounds__(kWave) void resolve_round_numa(DevTable T, NumaTabl
     NT.m[midx] = s_nm[lane];
   }
   if (lane < consumed) out_keys[first + lane] = my_out;
+  if (lane < nq) quotas[lane] = ql;
   if (lane == 0) {
     ctl[0] = first + consumed;
     ctl[1] += 1;
@@ -1189,7 +1207,8 @@ __global__ __launch_bounds__(kWave) void resolve_round_ds(DevTable T, DsTable DT
                                                            const uint64_t* __restrict__ cand,
                                                            const uint64_t* __restrict__ dsnorm, EvalParams P,
                                                            DsParams DP, uint64_t* __restrict__ out_keys,
-                                                           int32_t* __restrict__ out_minors, int bitmap_words) {
+                                                           int32_t* __restrict__ out_minors, int bitmap_words,
+                                                           DevQuota* __restrict__ quotas, int nq) {
   extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
   const int lane = threadIdx.x;
   int64_t first;
@@ -1236,11 +1255,18 @@ __global__ __launch_bounds__(kWave) void resolve_round_ds(DevTable T, DsTable DT
   uint64_t my_out = 0;
   int32_t my_minors = 0;
   int nM = 0, consumed = 0;
+  DevQuota ql = quota_load(quotas, nq, lane);
   for (int j = 0; j < nb; ++j) {
     const uint64_t key = s_cand[(size_t)j * kCandStride + lane];
     const uint64_t ub = s_cand[(size_t)j * kCandStride + kC];
     const DevPod p = s_pods[j];
     const DsPod dp = s_dp[j];
+    if (nq > 0 && !quota_admit(ql, p)) {  // ElasticQuota PreFilter rejects
+      my_out = lane == j ? 0 : my_out;
+      my_minors = lane == j ? 0 : my_minors;
+      ++consumed;
+      continue;
+    }
     const uint64_t nrm = readlane_u64(my_nrm, j);
     const uint32_t Mrs = (uint32_t)(nrm >> 32), Crs = (uint32_t)nrm;  // Mrs = max raw + 1 (0: no feasible node)
     // M_j: the round-start max survives while an unmodified node or a modified row still holds it.  At most nM
@@ -1346,6 +1372,7 @@ __global__ __launch_bounds__(kWave) void resolve_round_ds(DevTable T, DsTable DT
     }
     placed = __builtin_amdgcn_readlane(placed, owner);
     minors = __builtin_amdgcn_readlane(minors, owner);
+    if (placed && nq > 0) quota_charge(ql, p, lane);
     my_out = lane == j ? (placed ? best : 0) : my_out;
     my_minors = lane == j ? (placed ? minors : 0) : my_minors;
     __syncthreads();
@@ -1358,6 +1385,7 @@ __global__ __launch_bounds__(kWave) void resolve_round_ds(DevTable T, DsTable DT
     out_keys[first + lane] = my_out;
     out_minors[first + lane] = my_minors;
   }
+  if (lane < nq) quotas[lane] = ql;
   __threadfence();
   if (lane == 0) {
     ctl[0] = first + consumed;
@@ -1578,6 +1606,9 @@ struct kg_engine {
   DevBuf<int32_t> out_minors;  // [staged + kMaxB]
   DevBuf<uint64_t> dsmax;      // [B][nt_local]
   DevBuf<uint64_t> dsnorm;     // [B]
+  // ElasticQuota admission table (kg_quotas_set)
+  DevBuf<DevQuota> quotas;     // [KG_MAX_QUOTAS]
+  int nq = 0;
 };
 
 namespace {
@@ -1752,6 +1783,8 @@ int decode_pod(const kg_engine* e, const kg_pod& p, DevPod& d) {
             (p.priority_class == KG_PRIO_PROD ? P_PROD : 0) |
             (p.priority_class == KG_PRIO_PROD && c.la_score_according_prod_usage ? P_LA_PROD_SCORE : 0);
   d.pad = 0;
+  d.quota = (int32_t)std::min<int64_t>(std::max<int64_t>(p.quota_id, 0), 1 << 20) - 1;
+  if (p.flags & KG_POD_NON_PREEMPTIBLE) d.flags |= P_NONPREEMPT;
   return 0;
 }
 
@@ -2067,7 +2100,8 @@ void launch_resolve(kg_engine* e, const RoundGeom& g, int64_t first, int nb, int
     resolve_round_numa<<<1, kWave, resolve_numa_lds_bytes(g, nb), st>>>(e->T, numa_table(e), e->pods.p, e->npods.p,
                                                                         e->cursor.p, first, nb, cand_slot(e, g, slot),
                                                                         e->P, e->NP, e->out_keys.p, e->out_cpus.p,
-                                                                        g.bitmap_words, poison_ptr(e), seq);
+                                                                        g.bitmap_words, poison_ptr(e), seq, e->quotas.p,
+                                                                        e->nq);
     return;
   }
   const int32_t* prev = prev_slot >= 0 ? e->modlists.p + (size_t)prev_slot * (1 + kMaxB) : nullptr;
@@ -2076,7 +2110,7 @@ void launch_resolve(kg_engine* e, const RoundGeom& g, int64_t first, int nb, int
   resolve_round<X><<<1, kWave, resolve_lds_bytes(g, nb), st>>>(e->T, e->pods.p, e->cursor.p, first, nb,              \
                                                                cand_slot(e, g, slot),                             \
                                                                e->P, e->out_keys.p, g.bitmap_words, prev, mine,  \
-                                                               poison_ptr(e), seq, wait)
+                                                               poison_ptr(e), seq, wait, e->quotas.p, e->nq)
   KG_PF_SWITCH(profile_bits(e->P), KG_RESOLVE)
 #undef KG_RESOLVE
 }
@@ -2149,7 +2183,7 @@ void launch_round_ds(kg_engine* e, const RoundGeom& g, int64_t end, hipStream_t 
     resolve_round_ds<<<1, kWave, resolve_ds_lds_bytes(g, g.B), st>>>(e->T, DT, e->pods.p, e->dpods.p, e->cursor.p,
                                                                      end, g.B, cand_slot(e, g, 0), e->dsnorm.p, e->P,
                                                                      e->DP, e->out_keys.p, e->out_minors.p,
-                                                                     g.bitmap_words);
+                                                                     g.bitmap_words, e->quotas.p, e->nq);
 }
 
 int run_batch_ds(kg_engine* e, const RoundGeom& g, int64_t end, int64_t n_rounds) {
@@ -2201,6 +2235,7 @@ int64_t kg_abi_struct_size(int which) {
     case 4: return sizeof(kg_stats);
     case 5: return sizeof(kg_node_numa);
     case 6: return sizeof(kg_node_device);
+    case 7: return sizeof(kg_quota);
   }
   return -1;
 }
@@ -2428,6 +2463,7 @@ void kg_engine_destroy(kg_engine* e) {
   e->npods.release();
   e->out_cpus.release();
   e->ds_d.release();
+  e->quotas.release();
   e->dpods.release();
   e->out_minors.release();
   e->dsmax.release();
@@ -2527,6 +2563,16 @@ int kg_pods_remove(kg_engine* e, const kg_pod* pods, const int32_t* node_idx, in
 
 int kg_pods_stage(kg_engine* e, const kg_pod* pods, int64_t n) {
   if (!e || (n > 0 && !pods)) return fail(KG_E_INVALID, "null argument");
+  for (int64_t k = 0; k < n; ++k) {
+    if (pods[k].quota_id < 0 || pods[k].quota_id > e->nq)
+      return fail(KG_E_INVALID, "pod %lld: quota_id %lld outside the quota table (%d quotas)", (long long)k,
+                  (long long)pods[k].quota_id, e->nq);
+    if (pods[k].quota_id > 0)
+      for (int r = 0; r < KG_DEV_RES_MAX; ++r)
+        if (pods[k].device_requests[r] != 0)
+          return fail(KG_E_UNSUPPORTED, "pod %lld: ElasticQuota admission covers cpu/memory; device requests in a "
+                      "quota are not accelerated", (long long)k);
+  }
   std::vector<DevPod> h(std::max<int64_t>(n, 1));
   for (int64_t k = 0; k < n; ++k)
     if (int rc = decode_pod(e, pods[k], h[k])) return rc;
@@ -2847,6 +2893,43 @@ int kg_pods_evaluate_device(kg_engine* e, const kg_pod* pod, int32_t* out_pass, 
   HIP_TRY(hipStreamSynchronize(e->stream));
   if (out_pass) std::memcpy(out_pass, ps.data(), n * 4);
   if (out_score) std::memcpy(out_score, sc.data(), n * 8);
+  return 0;
+}
+
+int kg_quotas_set(kg_engine* e, const kg_quota* quotas, int64_t n) {
+  if (!e || (n > 0 && !quotas)) return fail(KG_E_INVALID, "null argument");
+  if (n < 0 || n > KG_MAX_QUOTAS) return fail(KG_E_UNSUPPORTED, "%lld quotas > %d", (long long)n, KG_MAX_QUOTAS);
+  std::vector<DevQuota> h(std::max<int64_t>(n, 1));
+  for (int64_t k = 0; k < n; ++k) {
+    const kg_quota& q = quotas[k];
+    for (int r = 0; r < 2; ++r)
+      if (q.used[r] < 0 || q.non_preemptible_used[r] < 0 || q.used_limit[r] < -1 || q.min[r] < -1 ||
+          q.used[r] > (1ll << 60) || q.used_limit[r] > (1ll << 60) || q.min[r] > (1ll << 60) ||
+          q.non_preemptible_used[r] > (1ll << 60))
+        return fail(KG_E_INVALID, "quota %lld: quantity out of range", (long long)k);
+    h[k] = DevQuota{q.used[0], q.used[1], q.non_preemptible_used[0], q.non_preemptible_used[1], q.used_limit[0],
+                    q.used_limit[1], q.min[0], q.min[1]};
+  }
+  if (int rc = e->quotas.ensure(KG_MAX_QUOTAS)) return rc;
+  if (n > 0) {
+    HIP_TRY(hipMemcpyAsync(e->quotas.p, h.data(), n * sizeof(DevQuota), hipMemcpyHostToDevice, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+  }
+  e->nq = (int)n;
+  return 0;
+}
+
+int kg_quotas_read(kg_engine* e, kg_quota* out, int64_t n) {
+  if (!e || (n > 0 && !out)) return fail(KG_E_INVALID, "null argument");
+  if (n != e->nq) return fail(KG_E_INVALID, "the quota table holds %d quotas", e->nq);
+  if (n == 0) return 0;
+  std::vector<DevQuota> h(n);
+  HIP_TRY(hipMemcpyAsync(h.data(), e->quotas.p, n * sizeof(DevQuota), hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  for (int64_t k = 0; k < n; ++k) {
+    const DevQuota& d = h[k];
+    out[k] = kg_quota{{d.used_c, d.used_m}, {d.np_c, d.np_m}, {d.lim_c, d.lim_m}, {d.min_c, d.min_m}};
+  }
   return 0;
 }
 

@@ -52,6 +52,7 @@ constexpr uint32_t P_ZERO_REQ = 1u << 0;      // every request zero → fitsRequ
 constexpr uint32_t P_DAEMONSET = 1u << 1;     // LoadAware Filter bypass (load_aware.go:129-131)
 constexpr uint32_t P_PROD = 1u << 2;          // priority class koord-prod
 constexpr uint32_t P_LA_PROD_SCORE = 1u << 3; // prod && ScoreAccordingProdUsage (load_aware.go:291)
+constexpr uint32_t P_NONPREEMPT = 1u << 4;    // extension.IsPodNonPreemptible (ElasticQuota min check)
 
 struct DevTable {
   int64_t *alloc_cpu, *alloc_mem;        // NodeInfo.Allocatable
@@ -76,7 +77,8 @@ struct DevPod {
   int32_t nz_cpu32, est_cpu32; // min(·, 2^30) for the 32-bit cpu score terms
   int32_t req_cpu32;           // min(req_cpu, 2^30 + 1) for the 32-bit filter compare of the wide pass
   uint32_t flags;
-  int64_t pad;  // 96 B: a 16-B multiple for LDS-DMA
+  int32_t quota;  // ElasticQuota table index, -1 = none
+  int32_t pad;    // 96 B: a 16-B multiple for LDS-DMA
 };
 static_assert(sizeof(DevPod) == 96, "DevPod layout");
 constexpr int kPodWords = (int)(sizeof(DevPod) / 8);
@@ -617,6 +619,48 @@ __device__ __forceinline__ uint64_t wave_max_key(uint64_t k) {
   const uint32_t hi = wave_max_u32((uint32_t)(k >> 32));
   const uint32_t lo = wave_max_u32((uint32_t)(k >> 32) == hi ? (uint32_t)k : 0u);
   return ((uint64_t)hi << 32) | lo;
+}
+
+// ---------------------------------------------------------------------------------------------------
+// ElasticQuota admission inside the FIFO resolvers (elasticquota/plugin.go:211-256 PreFilter, :332-346 Reserve).
+// Quota q lives in lane q of the resolver wave (≤ 64 quotas); a pod's PreFilter check reads it by readlane and a
+// placed pod is charged by that lane, so pod j+1's check sees pod j's Reserve, as in the reference.
+// ---------------------------------------------------------------------------------------------------
+struct DevQuota {
+  int64_t used_c, used_m, np_c, np_m, lim_c, lim_m, min_c, min_m;
+};
+
+__device__ __forceinline__ DevQuota quota_load(const DevQuota* __restrict__ q, int nq, int lane) {
+  DevQuota r{0, 0, 0, 0, 0, 0, 0, 0};
+  if (lane < nq) r = q[lane];
+  return r;
+}
+
+// quotav1.LessThanOrEqual(Mask(Add(request, used), ResourceNames(request)), limit) over cpu / memory (wave-uniform);
+// a limit < 0 is a key absent from the limit list, which LessThanOrEqual does not compare
+__device__ __forceinline__ bool quota_admit(const DevQuota& ql, const DevPod& p) {
+  if (p.quota < 0) return true;
+  const int q = p.quota;
+  const int64_t uc = (int64_t)readlane_u64((uint64_t)ql.used_c, q), um = (int64_t)readlane_u64((uint64_t)ql.used_m, q);
+  const int64_t lc = (int64_t)readlane_u64((uint64_t)ql.lim_c, q), lm = (int64_t)readlane_u64((uint64_t)ql.lim_m, q);
+  bool ok = (p.req_cpu == 0 || lc < 0 || uc + p.req_cpu <= lc) && (p.req_mem == 0 || lm < 0 || um + p.req_mem <= lm);
+  if (p.flags & P_NONPREEMPT) {
+    const int64_t nc = (int64_t)readlane_u64((uint64_t)ql.np_c, q), nm = (int64_t)readlane_u64((uint64_t)ql.np_m, q);
+    const int64_t mc = (int64_t)readlane_u64((uint64_t)ql.min_c, q), mm = (int64_t)readlane_u64((uint64_t)ql.min_m, q);
+    ok = ok && (p.req_cpu == 0 || mc < 0 || nc + p.req_cpu <= mc) && (p.req_mem == 0 || mm < 0 || nm + p.req_mem <= mm);
+  }
+  return ok;
+}
+
+// GroupQuotaManager.ReservePod → updatePodUsedNoLock (core/group_quota_manager.go:613-648, 791-797)
+__device__ __forceinline__ void quota_charge(DevQuota& ql, const DevPod& p, int lane) {
+  if (p.quota != lane) return;
+  ql.used_c += p.req_cpu;
+  ql.used_m += p.req_mem;
+  if (p.flags & P_NONPREEMPT) {
+    ql.np_c += p.req_cpu;
+    ql.np_m += p.req_mem;
+  }
 }
 
 }  // namespace kg

@@ -103,6 +103,16 @@ class Engine:
         idx = self._idx(idx, len(node_device))
         check(self.lib, self.lib.kg_nodes_device_upsert(self.h, ptr(node_device), ptr(idx), len(node_device)))
 
+    def set_quotas(self, quotas: np.ndarray):
+        """ElasticQuota table (kg_quotas_set): pods' quota_id = 1 + index."""
+        quotas = np.ascontiguousarray(quotas, dtype=abi.QUOTA_DTYPE)
+        check(self.lib, self.lib.kg_quotas_set(self.h, ptr(quotas), len(quotas)))
+
+    def read_quotas(self, n: int) -> np.ndarray:
+        out = np.zeros(n, dtype=abi.QUOTA_DTYPE)
+        check(self.lib, self.lib.kg_quotas_read(self.h, ptr(out), n))
+        return out
+
     # -- hot path -----------------------------------------------------------------------------------------
     def schedule(self, pods: np.ndarray):
         """Sequential FIFO scheduling with assume; returns (node_idx[-1 = unschedulable], total_score, stats)."""

@@ -233,10 +233,23 @@ def make_node_device(gpus: list | None = None, has_device: bool = True) -> np.nd
     return d
 
 
+def make_quota(used_limit: dict | None = None, used: dict | None = None, min: dict | None = None,
+               non_preemptible_used: dict | None = None) -> np.ndarray:
+    """One ElasticQuota (kg_quota): {"cpu": milli, "memory": bytes} lists; a key absent from used_limit / min does
+    not constrain (quotav1.LessThanOrEqual compares only the limit's keys)."""
+    q = np.zeros(1, dtype=abi.QUOTA_DTYPE)
+    r = q[0]
+    for f, d, absent in (("used", used, 0), ("non_preemptible_used", non_preemptible_used, 0),
+                         ("used_limit", used_limit, -1), ("min", min, -1)):
+        d = d or {}
+        r[f] = [int(d.get("cpu", absent)), int(d.get("memory", absent))]
+    return q
+
+
 def make_pod(requests: dict | None = None, limits: dict | None = None, priority_class: str = "",
              daemonset: bool = False, nonzero: tuple | None = None, qos: str = "",
              required_cpu_bind_policy: str = "", preferred_cpu_bind_policy: str = "",
-             devices: dict | None = None) -> np.ndarray:
+             devices: dict | None = None, quota_id: int = 0, non_preemptible: bool = False) -> np.ndarray:
     """One single-container pod. nonzero = schedutil.GetNonzeroRequests (100m / 200MiB defaults); qos = the
     koordinator.sh/qosClass label; *_cpu_bind_policy = the scheduling.koordinator.sh/resource-spec annotation."""
     p = np.zeros(1, dtype=abi.POD_DTYPE)
@@ -248,7 +261,8 @@ def make_pod(requests: dict | None = None, limits: dict | None = None, priority_
         nonzero = (req[abi.RES_CPU] or 100, req[abi.RES_MEMORY] or 200 * 1024 * 1024)
     r["nonzero_requests"] = nonzero
     r["priority_class"] = abi.PRIORITY_CLASSES[priority_class]
-    r["flags"] = abi.POD_DAEMONSET if daemonset else 0
+    r["flags"] = (abi.POD_DAEMONSET if daemonset else 0) | (abi.POD_NON_PREEMPTIBLE if non_preemptible else 0)
+    r["quota_id"] = quota_id  # 1 + index into the ElasticQuota table (0: the pod has no quota)
     r["qos"] = abi.QOS[qos]
     r["required_cpu_bind_policy"] = abi.BIND[required_cpu_bind_policy]
     r["preferred_cpu_bind_policy"] = abi.BIND[preferred_cpu_bind_policy]

@@ -364,14 +364,38 @@ int or_schedule(const kg_config* cfg, int64_t n_nodes, const kg_node* nodes, con
 int or_schedule_numa(const kg_config* cfg, int64_t n_nodes, const kg_node* nodes, const kg_node_metric* metrics,
                      or_node_state* st, void* numa_states, int64_t n_pods, const kg_pod* pods, int64_t now,
                      int n_threads, int32_t* out_node, int64_t* out_score, uint64_t* out_cpus) {
-  return or_schedule_full(cfg, n_nodes, nodes, metrics, st, numa_states, NULL, n_pods, pods, now, n_threads, out_node,
-                          out_score, out_cpus, NULL);
+  return or_schedule_full(cfg, n_nodes, nodes, metrics, st, numa_states, NULL, NULL, 0, n_pods, pods, now, n_threads,
+                          out_node, out_score, out_cpus, NULL);
+}
+
+/* ElasticQuota PreFilter (elasticquota/plugin.go:211-256): Mask(Add(request, used), ResourceNames(request)) ≤
+ * usedLimit, and for non-preemptible pods (extension.IsPodNonPreemptible) the same against min with the
+ * non-preemptible used.  Resource names = the pod's non-zero cpu / memory requests. */
+static int quota_admit(const kg_quota* q, const kg_pod* p) {
+  const int64_t rc = p->requests[KG_RES_CPU], rm = p->requests[KG_RES_MEMORY];
+  /* quotav1.LessThanOrEqual(a, b) walks the keys of b and compares those a has: a limit of -1 (absent) is free */
+  int ok = (rc == 0 || q->used_limit[0] < 0 || q->used[0] + rc <= q->used_limit[0]) &&
+           (rm == 0 || q->used_limit[1] < 0 || q->used[1] + rm <= q->used_limit[1]);
+  if (p->flags & KG_POD_NON_PREEMPTIBLE)
+    ok = ok && (rc == 0 || q->min[0] < 0 || q->non_preemptible_used[0] + rc <= q->min[0]) &&
+         (rm == 0 || q->min[1] < 0 || q->non_preemptible_used[1] + rm <= q->min[1]);
+  return ok;
+}
+
+/* Reserve → GroupQuotaManager.ReservePod → updatePodUsedNoLock (core/group_quota_manager.go:613-648, 791-797) */
+static void quota_charge(kg_quota* q, const kg_pod* p) {
+  q->used[0] += p->requests[KG_RES_CPU];
+  q->used[1] += p->requests[KG_RES_MEMORY];
+  if (p->flags & KG_POD_NON_PREEMPTIBLE) {
+    q->non_preemptible_used[0] += p->requests[KG_RES_CPU];
+    q->non_preemptible_used[1] += p->requests[KG_RES_MEMORY];
+  }
 }
 
 int or_schedule_full(const kg_config* cfg, int64_t n_nodes, const kg_node* nodes, const kg_node_metric* metrics,
-                     or_node_state* st, void* numa_states, kg_node_device* dev, int64_t n_pods, const kg_pod* pods,
-                     int64_t now, int n_threads, int32_t* out_node, int64_t* out_score, uint64_t* out_cpus,
-                     int32_t* out_minors) {
+                     or_node_state* st, void* numa_states, kg_node_device* dev, kg_quota* quotas, int64_t n_quotas,
+                     int64_t n_pods, const kg_pod* pods, int64_t now, int n_threads, int32_t* out_node,
+                     int64_t* out_score, uint64_t* out_cpus, int32_t* out_minors) {
   or_numa_node* numa = (or_numa_node*)numa_states;
   sched_ctx c;
   memset(&c, 0, sizeof(c));
@@ -400,6 +424,19 @@ int or_schedule_full(const kg_config* cfg, int64_t n_nodes, const kg_node* nodes
   int rc = 0;
   for (int64_t p = 0; p < n_pods && rc == 0; p++) {
     c.pod = &pods[p];
+    kg_quota* quota = NULL;
+    if (pods[p].quota_id > 0) {
+      if (pods[p].quota_id > n_quotas) { rc = KG_E_INVALID; break; }
+      quota = &quotas[pods[p].quota_id - 1];
+      if (!quota_admit(quota, &pods[p])) { /* PreFilter Unschedulable: no node search, nothing reserved */
+        out_node[p] = -1;
+        out_score[p] = 0;
+        if (out_minors) out_minors[p] = 0;
+        if (out_cpus)
+          for (int w = 0; w < OR_CPUSET_WORDS; w++) out_cpus[p * OR_CPUSET_WORDS + w] = 0;
+        continue;
+      }
+    }
     if (c.numa) or_numa_pod_init(cfg, c.pod, &c.numa_pod);
     if (c.dev) {
       or_ds_pod_init(c.pod, &c.ds_pod);
@@ -442,6 +479,7 @@ int or_schedule_full(const kg_config* cfg, int64_t n_nodes, const kg_node* nodes
     out_node[p] = (int32_t)best;
     out_score[p] = best >= 0 ? best_score : 0;
     if (best >= 0) or_apply_pod(cfg, &st[best], &pods[p], +1); /* assume + Reserve */
+    if (best >= 0 && quota) quota_charge(quota, &pods[p]);
   }
   if (n_threads > 1) {
     atomic_store(&c.stop, 1);

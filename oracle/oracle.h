@@ -75,12 +75,13 @@ int or_schedule_numa(const kg_config* cfg, int64_t n_nodes, const kg_node* nodes
                      or_node_state* st, void* numa, int64_t n_pods, const kg_pod* pods, int64_t now_unix_nano,
                      int n_threads, int32_t* out_node, int64_t* out_score, uint64_t* out_cpus);
 
-/* The full profile: optional NodeNUMAResource state (`numa`, NULL = off) and DeviceShare state (`dev`, NULL =
- * off; updated by Reserve), out_minors (nullable) = the GPU minor bitmask DeviceShare Reserve allocated. */
+/* The full profile: optional NodeNUMAResource state (`numa`, NULL = off), DeviceShare state (`dev`, NULL = off;
+ * updated by Reserve) and ElasticQuota table (`quotas`, pods' quota_id index it; admission before the node search,
+ * charged on placement), out_minors (nullable) = the GPU minor bitmask DeviceShare Reserve allocated. */
 int or_schedule_full(const kg_config* cfg, int64_t n_nodes, const kg_node* nodes, const kg_node_metric* metrics,
-                     or_node_state* st, void* numa, kg_node_device* dev, int64_t n_pods, const kg_pod* pods,
-                     int64_t now_unix_nano, int n_threads, int32_t* out_node, int64_t* out_score, uint64_t* out_cpus,
-                     int32_t* out_minors);
+                     or_node_state* st, void* numa, kg_node_device* dev, kg_quota* quotas, int64_t n_quotas,
+                     int64_t n_pods, const kg_pod* pods, int64_t now_unix_nano, int n_threads, int32_t* out_node,
+                     int64_t* out_score, uint64_t* out_cpus, int32_t* out_minors);
 
 /* Builds node states from pre-existing assigned pods (informer adds). */
 void or_states_init(int64_t n_nodes, or_node_state* st);

@@ -70,7 +70,7 @@ def lib():
         L.or_numa_eval_flat.restype = i
         L.or_numa_reserve_flat.argtypes = [vp, vp, vp, vp]
         L.or_numa_reserve_flat.restype = i
-        L.or_schedule_full.argtypes = [vp, i64, vp, vp, vp, vp, vp, i64, vp, i64, i, vp, vp, vp, vp]
+        L.or_schedule_full.argtypes = [vp, i64, vp, vp, vp, vp, vp, vp, i64, i64, vp, i64, i, vp, vp, vp, vp]
         L.or_schedule_full.restype = i
         L.or_ds_pod_init.argtypes = [vp, vp]
         L.or_ds_pod_init.restype = i
@@ -123,16 +123,18 @@ def ds_reserve(cfg, dev, pod) -> int:
     return int(lib().or_ds_reserve(p(dev), p(ds_pod(pod)), int(cfg["ds_scoring_strategy"]), p(w)))
 
 
-def schedule_full(cfg, nodes, metrics, st, pods, now_ns: int, n_threads: int = 1, numa_buf=None, devices=None):
-    """Sequential FIFO scheduling with the optional NodeNUMAResource / DeviceShare states (both mutated).
-    Returns (node, score, cpusets uint64[n, 4], GPU minor masks int32[n])."""
+def schedule_full(cfg, nodes, metrics, st, pods, now_ns: int, n_threads: int = 1, numa_buf=None, devices=None,
+                  quotas=None):
+    """Sequential FIFO scheduling with the optional NodeNUMAResource / DeviceShare states and ElasticQuota table
+    (all mutated).  Returns (node, score, cpusets uint64[n, 4], GPU minor masks int32[n])."""
     pods = np.ascontiguousarray(pods, dtype=abi.POD_DTYPE)
     out_node = np.empty(len(pods), dtype=np.int32)
     out_score = np.empty(len(pods), dtype=np.int64)
     cpus = np.zeros((max(len(pods), 1), abi.MAX_CPUS // 64), dtype=np.uint64)
     minors = np.zeros(max(len(pods), 1), dtype=np.int32)
-    rc = lib().or_schedule_full(p(cfg), len(nodes), p(nodes), p(metrics), p(st), p(numa_buf), p(devices), len(pods),
-                                p(pods), now_ns, n_threads, p(out_node), p(out_score), p(cpus), p(minors))
+    nq = 0 if quotas is None else len(quotas)
+    rc = lib().or_schedule_full(p(cfg), len(nodes), p(nodes), p(metrics), p(st), p(numa_buf), p(devices), p(quotas), nq,
+                                len(pods), p(pods), now_ns, n_threads, p(out_node), p(out_score), p(cpus), p(minors))
     if rc != 0:
         raise RuntimeError(f"oracle or_schedule_full failed: {rc}")
     return out_node, out_score, cpus[:len(pods)], minors[:len(pods)]
