@@ -797,9 +797,11 @@ __device__ __forceinline__ bool eval_node_numa(const Row& r, const NumaView& nv,
   return true;
 }
 
-// Wide pass of a NUMA round.  Same tiles, pod groups and candidate lists as eval_round; each lane takes its
-// kNPT nodes one at a time (Row + NumaView hoisted out of the pod loop) and parks the per-pod values in LDS,
-// then the per-pod top-kR selects run as in eval_round.  pods_per_wave ≤ kNumaPpw (host clamps).
+// Wide pass of a NUMA round.  One block per (256-node tile, pod group): wave w evaluates node row j = w of the tile
+// (lane l → node tile·256 + w·64 + l) for the group's pods, Fit + LoadAware first, then NodeNUMAResource on the
+// pods that survived, parking the values in LDS; after a barrier the waves split the group's pods for the
+// per-pod top-kR selects of eval_round.  numa_eval is long and divergent, so one node per lane (4x the waves of
+// a 4-nodes-per-lane tile) keeps the serial path of a wave short.  pods_per_wave ≤ kNumaPpw (host clamps).
 constexpr int kNumaPpw = 8;
 
 __global__ __launch_bounds__(kWave* kEvalWaves) void eval_round_numa(DevTable T, NumaTable NT,
@@ -810,58 +812,58 @@ __global__ __launch_bounds__(kWave* kEvalWaves) void eval_round_numa(DevTable T,
                                                                        int nt_local, EvalParams P, NumaParams NP,
                                                                        uint64_t* __restrict__ lists,
                                                                        const int32_t* __restrict__ poison) {
-  __shared__ uint32_t s_v[kEvalWaves][kNumaPpw][kNPT][kWave];
+  __shared__ uint32_t s_v[kNumaPpw][kNPT][kWave];
   if (*poison) return;
   const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
   const int n_pg = (nb + pods_per_wave - 1) / pods_per_wave;
   const uint32_t nwg = gridDim.x, bid = blockIdx.x, xcd = bid % 8u, q = nwg / 8u, r = nwg % 8u;
   const uint32_t wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8u;
-  const int tile = (int)(wgid / (uint32_t)n_pg) * kEvalWaves + wave;
+  const int tile = (int)(wgid / (uint32_t)n_pg);
   const int p0 = (int)(wgid % (uint32_t)n_pg) * pods_per_wave;
-  if (tile >= nt_local || p0 >= nb) return;
+  if (tile >= nt_local || p0 >= nb) return;  // block-uniform
   const int p1 = (p0 + pods_per_wave) < nb ? (p0 + pods_per_wave) : nb;
   const int vbits = P.score_bits + 1;
-  for (int j = 0; j < kNPT; ++j) {
-    int64_t local = (int64_t)tile * kTile + j * kWave + lane;
-    asm volatile("" : "+v"(local));
-    const bool in = local < n_local;
-    // phase 1: Fit + LoadAware (the Row is dead afterwards but for the four NodeInfo terms NUMA reads)
-    int64_t rq_c = 0, rq_m = 0, al_c = 0, al_m = 0;
-    {
-      Row row;
-      row.flags = 0;
-      if (in) row = load_row(T, node_base + local);
-      for (int pi = p0; pi < p1; ++pi) {
-        const DevPod p = pods[first + pi];
-        int64_t t = 0;
-        s_v[wave][pi - p0][j][lane] = (in && eval_node(row, p, P, t)) ? (uint32_t)t + 1u : 0u;
-      }
-      rq_c = row.req_cpu;
-      rq_m = row.req_mem;
-      al_c = row.alloc_cpu;
-      al_m = row.alloc_mem;
+  const int j = wave;
+  int64_t local = (int64_t)tile * kTile + j * kWave + lane;
+  asm volatile("" : "+v"(local));
+  const bool in = local < n_local;
+  // phase 1: Fit + LoadAware (the Row is dead afterwards but for the four NodeInfo terms NUMA reads)
+  int64_t rq_c = 0, rq_m = 0, al_c = 0, al_m = 0;
+  {
+    Row row;
+    row.flags = 0;
+    if (in) row = load_row(T, node_base + local);
+    for (int pi = p0; pi < p1; ++pi) {
+      const DevPod p = pods[first + pi];
+      int64_t t = 0;
+      s_v[pi - p0][j][lane] = (in && eval_node(row, p, P, t)) ? (uint32_t)t + 1u : 0u;
     }
-    // phase 2: NodeNUMAResource on the pods Fit/LoadAware kept
-    if (in) {
-      const NumaView nv = make_view(NT.s + node_base + local, NT.m + node_base + local, NP);
-      for (int pi = p0; pi < p1; ++pi) {
-        const uint32_t v0 = s_v[wave][pi - p0][j][lane];
-        if (v0 == 0) continue;
-        const NumaPod np = npods[first + pi];
-        int64_t sc = 0;
-        NumaHint aff;
-        const bool ok = numa_eval(nv, np, NP, rq_c, rq_m, al_c, al_m, sc, aff);
-        s_v[wave][pi - p0][j][lane] = ok ? v0 + (uint32_t)(NP.score ? sc * NP.weight : 0) : 0u;
-      }
+    rq_c = row.req_cpu;
+    rq_m = row.req_mem;
+    al_c = row.alloc_cpu;
+    al_m = row.alloc_mem;
+  }
+  // phase 2: NodeNUMAResource on the pods Fit/LoadAware kept
+  if (in) {
+    const NumaView nv = make_view(NT.s + node_base + local, NT.m + node_base + local, NP);
+    for (int pi = p0; pi < p1; ++pi) {
+      const uint32_t v0 = s_v[pi - p0][j][lane];
+      if (v0 == 0) continue;
+      const NumaPod np = npods[first + pi];
+      int64_t sc = 0;
+      NumaHint aff;
+      const bool ok = numa_eval(nv, np, NP, rq_c, rq_m, al_c, al_m, sc, aff);
+      s_v[pi - p0][j][lane] = ok ? v0 + (uint32_t)(NP.score ? sc * NP.weight : 0) : 0u;
     }
   }
+  __syncthreads();
   uint32_t gidx[kNPT];
 #pragma unroll
-  for (int j = 0; j < kNPT; ++j) gidx[j] = (uint32_t)(node_base + (int64_t)tile * kTile + j * kWave + lane);
-  for (int pi = p0; pi < p1; ++pi) {
+  for (int jj = 0; jj < kNPT; ++jj) gidx[jj] = (uint32_t)(node_base + (int64_t)tile * kTile + jj * kWave + lane);
+  for (int pi = p0 + wave; pi < p1; pi += kEvalWaves) {
     uint32_t v[kNPT];
 #pragma unroll
-    for (int j = 0; j < kNPT; ++j) v[j] = s_v[wave][pi - p0][j][lane];
+    for (int jj = 0; jj < kNPT; ++jj) v[jj] = s_v[pi - p0][jj][lane];
     select_write(v, gidx, vbits, lists + ((size_t)pi * nt_local + tile) * kR, lane);
   }
 }
@@ -2062,8 +2064,9 @@ uint64_t* lists_slot(kg_engine* e, const RoundGeom& g, int slot) {
 }
 
 void launch_eval(kg_engine* e, const RoundGeom& g, int64_t first, int nb, int slot, hipStream_t st) {
-  if (e->numa_on) {
-    eval_round_numa<<<eval_grid(g, nb), kWave * kEvalWaves, 0, st>>>(e->T, numa_table(e), e->pods.p, e->npods.p, first, nb,
+  if (e->numa_on) {  // one block per (tile, pod group)
+    const dim3 grid((unsigned)(g.nt_local * ((nb + g.ppw - 1) / g.ppw)));
+    eval_round_numa<<<grid, kWave * kEvalWaves, 0, st>>>(e->T, numa_table(e), e->pods.p, e->npods.p, first, nb,
                                                                       g.ppw, g.base, g.n_local, g.nt_local, e->P,
                                                                       e->NP, lists_slot(e, g, slot), poison_ptr(e));
     return;

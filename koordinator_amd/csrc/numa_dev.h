@@ -461,23 +461,44 @@ __device__ __forceinline__ uint32_t mask_at(int k) {
   return (uint32_t)((order >> (4 * k)) & 15ull);
 }
 
+// mostRequestedScore (most_allocated.go:50-62): (min(requested, capacity) · 100) / capacity, division-free like
+// least_requested (kernels.h): a float quotient estimate corrected by one exact int64 compare each way.
 __device__ __forceinline__ int64_t most_requested64(int64_t requested, int64_t capacity) {
   if (capacity == 0) return 0;
   if (requested > capacity) requested = capacity;
-  return (requested * 100) / capacity;
+  const int64_t num = requested * 100;
+  if (requested < 0) return num / capacity;
+  int q = (int)(((float)requested * 100.0f) / (float)capacity);
+  q = q < 0 ? 0 : (q > 100 ? 100 : q);
+  const int64_t t = (int64_t)q * capacity;
+  if (t > num) q -= 1;
+  else if (t + capacity <= num) q += 1;
+  return q;
 }
 
-// resourceAllocationScorer.score (scoring.go:191-230) over cpu + memory with least/mostResourceScorer
+// resourceAllocationScorer.score (scoring.go:191-230) over cpu + memory with least/mostResourceScorer.  The
+// strategy is a profile constant: an explicit branch keeps the unused scorer out of the instruction stream.
 __device__ __forceinline__ int64_t numa_scorer(int strategy, int32_t w_cpu, int32_t w_mem, int64_t req_c, int64_t req_m,
                                                int64_t alloc_c, int64_t alloc_m, int64_t pod_c, int64_t pod_m) {
   int64_t s = 0, ws = 0;
-  if (w_cpu != 0 && alloc_c != 0) {
-    s += (strategy == 1 ? most_requested64(req_c + pod_c, alloc_c) : least_requested(req_c + pod_c, alloc_c)) * w_cpu;
-    ws += w_cpu;
-  }
-  if (w_mem != 0 && alloc_m != 0) {
-    s += (strategy == 1 ? most_requested64(req_m + pod_m, alloc_m) : least_requested(req_m + pod_m, alloc_m)) * w_mem;
-    ws += w_mem;
+  if (strategy == 1) {
+    if (w_cpu != 0 && alloc_c != 0) {
+      s += most_requested64(req_c + pod_c, alloc_c) * w_cpu;
+      ws += w_cpu;
+    }
+    if (w_mem != 0 && alloc_m != 0) {
+      s += most_requested64(req_m + pod_m, alloc_m) * w_mem;
+      ws += w_mem;
+    }
+  } else {
+    if (w_cpu != 0 && alloc_c != 0) {
+      s += least_requested(req_c + pod_c, alloc_c) * w_cpu;
+      ws += w_cpu;
+    }
+    if (w_mem != 0 && alloc_m != 0) {
+      s += least_requested(req_m + pod_m, alloc_m) * w_mem;
+      ws += w_mem;
+    }
   }
   return ws ? div_small(s, ws) : 0;
 }
