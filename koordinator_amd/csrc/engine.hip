@@ -568,7 +568,7 @@ __device__ __forceinline__ void publish_round(int64_t* ctl, int64_t seq) {
   if (threadIdx.x == 0) __hip_atomic_store(&ctl[4], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <int PF>
+template <int PF, bool QUOTA>
 __global__ __launch_bounds__(kWave) void resolve_round(DevTable T, const DevPod* __restrict__ pods,
                                                         int64_t* __restrict__ ctl, int64_t first, int nb,
                                                         const uint64_t* __restrict__ cand, EvalParams P,
@@ -642,7 +642,8 @@ __global__ __launch_bounds__(kWave) void resolve_round(DevTable T, const DevPod*
   __syncthreads();
   if (lane < n_prev) atomicOr(&bitmap[midx >> 5], 1u << (midx & 31));
   __syncthreads();
-  DevQuota ql = quota_load(quotas, nq, lane);  // after the chain wait: the previous resolver's charges are visible
+  // ElasticQuota table (QUOTA instantiation only), after the chain wait: the previous resolver's charges are visible
+  DevQuota ql = QUOTA ? quota_load(quotas, nq, lane) : DevQuota{0, 0, 0, 0, 0, 0, 0, 0};
   KG_STAMP(2, 1);
   // staged[q] on lane l: node whose hoisted row sits at staged slot s = q·64 + l (record s / kStaged,
   // position s % kStaged of that pod's list)
@@ -687,7 +688,7 @@ __global__ __launch_bounds__(kWave) void resolve_round(DevTable T, const DevPod*
     // the prefetched word predates the previous pod's bitmap update: patch with its winner
     const bool unmod = (key != 0) & !((word >> (node & 31)) & 1u) & (node != last_w);
     word_n = bitmap[key_n ? key_node(key_n) >> 5 : 0u];
-    if (nq > 0 && !quota_admit(ql, p)) {  // ElasticQuota PreFilter rejects: Unschedulable, no node search
+    if (QUOTA && !quota_admit(ql, p)) {  // ElasticQuota PreFilter rejects: Unschedulable, no node search
       my_out = lane == j ? 0 : my_out;
       ++consumed;
       last_w = 0xFFFFFFFFu;
@@ -751,7 +752,7 @@ __global__ __launch_bounds__(kWave) void resolve_round(DevTable T, const DevPod*
       else add_delta(dl, p);
       touched = true;
     }
-    if (nq > 0) quota_charge(ql, p, lane);  // ElasticQuota Reserve
+    if (QUOTA) quota_charge(ql, p, lane);  // ElasticQuota Reserve
     if (j == 0 || j == 15 || j == 31) KG_STAMP(2, 2 + j / 8);
   }
   if (touched) {
@@ -762,7 +763,7 @@ __global__ __launch_bounds__(kWave) void resolve_round(DevTable T, const DevPod*
   const uint64_t lane_lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   if (touched) my_mod[1 + __popcll(tm & lane_lt)] = (int32_t)midx;
   if (lane < consumed) out_keys[first + lane] = my_out;
-  if (lane < nq) quotas[lane] = ql;
+  if (QUOTA && lane < nq) quotas[lane] = ql;
   KG_STAMP(2, 30);
   if (lane == 0) {
     my_mod[0] = __popcll(tm);
@@ -2109,12 +2110,20 @@ void launch_resolve(kg_engine* e, const RoundGeom& g, int64_t first, int nb, int
   }
   const int32_t* prev = prev_slot >= 0 ? e->modlists.p + (size_t)prev_slot * (1 + kMaxB) : nullptr;
   int32_t* mine = e->modlists.p + (size_t)slot * (1 + kMaxB);
-#define KG_RESOLVE(X)                                                                                            \
-  resolve_round<X><<<1, kWave, resolve_lds_bytes(g, nb), st>>>(e->T, e->pods.p, e->cursor.p, first, nb,              \
-                                                               cand_slot(e, g, slot),                             \
-                                                               e->P, e->out_keys.p, g.bitmap_words, prev, mine,  \
-                                                               poison_ptr(e), seq, wait, e->quotas.p, e->nq)
-  KG_PF_SWITCH(profile_bits(e->P), KG_RESOLVE)
+#define KG_RESOLVE_T(X, Q)                                                                                       \
+  resolve_round<X, Q><<<1, kWave, resolve_lds_bytes(g, nb), st>>>(e->T, e->pods.p, e->cursor.p, first, nb,           \
+                                                                  cand_slot(e, g, slot), e->P, e->out_keys.p,       \
+                                                                  g.bitmap_words, prev, mine, poison_ptr(e), seq,   \
+                                                                  wait, e->quotas.p, e->nq)
+#define KG_RESOLVE(X) KG_RESOLVE_T(X, false)
+#define KG_RESOLVE_Q(X) KG_RESOLVE_T(X, true)
+  if (e->nq > 0) {
+    KG_PF_SWITCH(profile_bits(e->P), KG_RESOLVE_Q)
+  } else {
+    KG_PF_SWITCH(profile_bits(e->P), KG_RESOLVE)
+  }
+#undef KG_RESOLVE_Q
+#undef KG_RESOLVE_T
 #undef KG_RESOLVE
 }
 
@@ -2422,8 +2431,10 @@ int kg_engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank, int
   {
     const int lds = (int)(kMaxNodes / 8 + (size_t)kMaxB * (kCandStride + kPodWords) * 8);
     hipError_t fe = hipSuccess;
-#define KG_ATTR(X) \
-  fe = hipFuncSetAttribute((const void*)resolve_round<X>, hipFuncAttributeMaxDynamicSharedMemorySize, lds)
+#define KG_ATTR(X)                                                                                           \
+  fe = hipFuncSetAttribute((const void*)resolve_round<X, false>, hipFuncAttributeMaxDynamicSharedMemorySize, lds); \
+  if (fe == hipSuccess)                                                                                      \
+    fe = hipFuncSetAttribute((const void*)resolve_round<X, true>, hipFuncAttributeMaxDynamicSharedMemorySize, lds)
     KG_PF_SWITCH(profile_bits(e->P), KG_ATTR)
 #undef KG_ATTR
     if (fe != hipSuccess) return bail(fail(KG_E_DEVICE, "hipFuncSetAttribute(resolve_round LDS)"));
