@@ -41,7 +41,7 @@ def parse():
     ap.add_argument("--nodes", type=int, default=None, help="default 100k (c3) / 10k (c4)")
     ap.add_argument("--pods-per-step", type=int, default=None, help="default 100k (c3) / 10k (c4)")
     ap.add_argument("--batch", type=int, default=None, help="default 32 (c3, c5) / 16 (c4)")
-    ap.add_argument("--pods-per-wave", type=int, default=None, help="default 8 (c3) / 1 (c4)")
+    ap.add_argument("--pods-per-wave", type=int, default=None, help="default 8 (c3) / 1 (c4) / 4 (c5)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -149,7 +149,8 @@ def main():
     c5 = args.workload == "c5"
     args.nodes = args.nodes or (10_000 if c4 else (50_000 if c5 else 100_000))
     args.pods_per_step = args.pods_per_step or (10_000 if (c4 or c5) else 100_000)
-    args.pods_per_wave = args.pods_per_wave or (1 if c4 else 8)  # C4 sweep: profiles/r01/c4_sweep.txt
+    # geometry sweeps: profiles/r01/c4_sweep.txt, c5_sweep.txt
+    args.pods_per_wave = args.pods_per_wave or (1 if c4 else (4 if c5 else 8))
     args.batch = args.batch or (16 if c4 else 32)
     F = framework
     profile = None

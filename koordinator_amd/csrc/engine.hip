@@ -1242,7 +1242,7 @@ __global__ __launch_bounds__(kWave) void resolve_round_ds(DevTable T, DsTable DT
     if (k0 != 0) {
       stg_node = key_node(k0);
       s_srow[lane] = load_row(T, stg_node);
-      reinterpret_cast<DsNode*>(s_stg)[lane] = DT.d[stg_node];
+      __builtin_memcpy(reinterpret_cast<DsNode*>(s_stg) + lane, DT.d + stg_node, sizeof(DsNode));
     }
   }
   __syncthreads();
@@ -1315,13 +1315,13 @@ __global__ __launch_bounds__(kWave) void resolve_round_ds(DevTable T, DsTable DT
     if (!hit) {
       const uint64_t sh = __ballot(stg_node == w);  // a pod whose top candidate is w staged its row
       const int src = sh ? (int)__builtin_ctzll(sh) : -1;
-      if (lane == owner) {
+      if (lane == owner) {  // copy the row straight into the lane's LDS slots (memcpy: alias-safe, no private copy)
         midx = w;
-        const DsNode dn = src >= 0 ? reinterpret_cast<const DsNode*>(s_stg)[src] : DT.d[w];
+        const DsNode* from = src >= 0 ? reinterpret_cast<const DsNode*>(s_stg) + src : DT.d + w;
         mrow = src >= 0 ? s_srow[src] : load_row(T, w);
+        __builtin_memcpy(&s_dc[owner], from, sizeof(DsNode));
+        __builtin_memcpy(&s_dr[owner], from, sizeof(DsNode));
         rrow = mrow;
-        s_dc[owner] = dn;
-        s_dr[owner] = dn;
       }
       if (lane == 0) bitmap[w >> 5] |= 1u << (w & 31);
       ++nM;
@@ -1382,7 +1382,7 @@ __global__ __launch_bounds__(kWave) void resolve_round_ds(DevTable T, DsTable DT
   }
   if (touched) {
     store_mutable(T, midx, mrow);
-    DT.d[midx] = s_dc[lane];
+    __builtin_memcpy(DT.d + midx, &s_dc[lane], sizeof(DsNode));
   }
   if (lane < consumed) {
     out_keys[first + lane] = my_out;
