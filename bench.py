@@ -216,7 +216,8 @@ def main():
     kernels = {name: e.bench_kernel(which, args.kernel_iters) for which, name in enumerate(names)}
     # roofline kernel: the wide pass, the only kernel whose work scales with node evaluations (SURVEY §8d's
     # 76 B per evaluation); merge and the single-wave FIFO resolver are latency-bound per round
-    dom = "eval_round"
+    # (C5: ds_max_round is the DeviceShare profile's full evaluation; eval_round_ds only normalizes its output)
+    dom = "ds_max_round" if c5 else "eval_round"
     dom_ms, dom_bytes = kernels[dom]
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
 

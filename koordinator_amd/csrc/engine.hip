@@ -1072,7 +1072,8 @@ __global__ __launch_bounds__(kWave* kEvalWaves) void ds_max_round(DevTable T, Ds
                                                                    const int64_t* __restrict__ ctl, int64_t end,
                                                                    int B, int pods_per_wave, int64_t n_local,
                                                                    int nt_local, EvalParams P, DsParams DP,
-                                                                   uint64_t* __restrict__ dsmax) {
+                                                                   uint64_t* __restrict__ dsmax,
+                                                                   uint32_t* __restrict__ dsval) {
   int64_t first;
   int nb;
   if (!ds_round_range(ctl, end, B, first, nb)) return;
@@ -1096,11 +1097,14 @@ __global__ __launch_bounds__(kWave* kEvalWaves) void ds_max_round(DevTable T, Ds
     for (int k = 0; k < kDsPpw; ++k) {
       if (k >= np) break;
       int64_t t = 0, raw = 0;
+      uint32_t packed = 0;
       if (eval_node(row, pods[first + p0 + k], P, t) && ds_eval(d, dpods[first + p0 + k], DP, raw)) {
         const uint32_t v = (uint32_t)raw + 1u;  // +1: a feasible node with raw 0 still counts
         cnt[k] = v > mx[k] ? 1u : cnt[k] + (v == mx[k] ? 1u : 0u);
         mx[k] = v > mx[k] ? v : mx[k];
+        packed = (((uint32_t)t << 8) | (uint32_t)raw) + 1u;  // t < 2^23 (host check), raw ≤ 100
       }
+      dsval[(size_t)(p0 + k) * ((size_t)nt_local * kTile) + i] = packed;  // eval_round_ds reads this back
     }
   }
 #pragma unroll
@@ -1144,14 +1148,14 @@ __global__ __launch_bounds__(256) void ds_norm_reduce(const int64_t* __restrict_
   }
 }
 
-__global__ __launch_bounds__(kWave* kEvalWaves) void eval_round_ds(DevTable T, DsTable DT,
-                                                                    const DevPod* __restrict__ pods,
-                                                                    const DsPod* __restrict__ dpods,
-                                                                    const int64_t* __restrict__ ctl, int64_t end,
+__global__ __launch_bounds__(kWave* kEvalWaves) void eval_round_ds(const int64_t* __restrict__ ctl, int64_t end,
                                                                     int B, int pods_per_wave, int64_t n_local,
                                                                     int nt_local, EvalParams P, DsParams DP,
                                                                     const uint64_t* __restrict__ dsnorm,
+                                                                    const uint32_t* __restrict__ dsval,
                                                                     uint64_t* __restrict__ lists) {
+  // ds_max_round left every (pod, node)'s Fit + LoadAware total and raw DeviceShare score packed in dsval
+  // ((t << 8 | raw) + 1, 0 = filtered out): this pass only normalizes with M and selects.
   int64_t first;
   int nb;
   if (!ds_round_range(ctl, end, B, first, nb)) return;
@@ -1164,39 +1168,21 @@ __global__ __launch_bounds__(kWave* kEvalWaves) void eval_round_ds(DevTable T, D
   if (tile >= nt_local || p0 >= nb) return;
   const int np = ((p0 + pods_per_wave) < nb ? (p0 + pods_per_wave) : nb) - p0;
   const int vbits = P.score_bits + 1;
-  uint32_t M[kDsPpw];
-#pragma unroll
-  for (int k = 0; k < kDsPpw; ++k) {
-    const uint32_t mm = k < np ? (uint32_t)(dsnorm[p0 + k] >> 32) : 0u;
-    M[k] = mm ? mm - 1u : 0u;
-  }
-  uint32_t v[kDsPpw][kNPT];
+  const size_t stride = (size_t)nt_local * kTile;
   uint32_t gidx[kNPT];
 #pragma unroll
-  for (int j = 0; j < kNPT; ++j) {
-    const int64_t i = (int64_t)tile * kTile + j * kWave + lane;
-    gidx[j] = (uint32_t)i;
-    const bool in = i < n_local;
-    Row row;
-    row.flags = 0;
-    DsNode d;
-    if (in) {
-      row = load_row(T, i);
-      d = DT.d[i];
-    }
+  for (int j = 0; j < kNPT; ++j) gidx[j] = (uint32_t)((int64_t)tile * kTile + j * kWave + lane);
+  for (int k = 0; k < np; ++k) {
+    const uint32_t mm = (uint32_t)(dsnorm[p0 + k] >> 32);
+    const uint32_t M = mm ? mm - 1u : 0u;
+    uint32_t v[kNPT];
 #pragma unroll
-    for (int k = 0; k < kDsPpw; ++k) {
-      v[k][j] = 0u;
-      if (k >= np || !in) continue;
-      int64_t t = 0, raw = 0;
-      if (eval_node(row, pods[first + p0 + k], P, t) && ds_eval(d, dpods[first + p0 + k], DP, raw))
-        v[k][j] = (uint32_t)(t + (DP.score ? DP.weight * ds_normalized(raw, M[k]) : 0)) + 1u;
+    for (int j = 0; j < kNPT; ++j) {
+      const uint32_t pk = (int64_t)gidx[j] < n_local ? dsval[(size_t)(p0 + k) * stride + gidx[j]] : 0u;
+      const uint32_t t = (pk - 1u) >> 8, raw = (pk - 1u) & 255u;
+      v[j] = pk ? t + (DP.score ? (uint32_t)(DP.weight * ds_normalized(raw, M)) : 0u) + 1u : 0u;
     }
-  }
-#pragma unroll
-  for (int k = 0; k < kDsPpw; ++k) {
-    if (k >= np) break;
-    select_write(v[k], gidx, vbits, lists + ((size_t)(p0 + k) * nt_local + tile) * kR, lane);
+    select_write(v, gidx, vbits, lists + ((size_t)(p0 + k) * nt_local + tile) * kR, lane);
   }
 }
 
@@ -1609,6 +1595,7 @@ struct kg_engine {
   DevBuf<int32_t> out_minors;  // [staged + kMaxB]
   DevBuf<uint64_t> dsmax;      // [B][nt_local]
   DevBuf<uint64_t> dsnorm;     // [B]
+  DevBuf<uint32_t> dsval;      // [B][nt_local·256]: packed (Fit+LoadAware total, raw DeviceShare) per (pod, node)
   // ElasticQuota admission table (kg_quotas_set)
   DevBuf<DevQuota> quotas;     // [KG_MAX_QUOTAS]
   int nq = 0;
@@ -1644,6 +1631,8 @@ int validate_config(const kg_config* c) {
       return fail(KG_E_UNSUPPORTED, "DeviceShare at Score needs DeviceShare at Filter (Score errors on unfiltered nodes)");
     if (c->numa_filter || c->numa_score) return fail(KG_E_UNSUPPORTED, "NodeNUMAResource + DeviceShare in one profile");
     if (c->batch_pods > 32) return fail(KG_E_UNSUPPORTED, "DeviceShare profiles: batch_pods <= 32");
+    if (100 * ((c->fit_score ? c->weight_fit : 0) + (c->la_score ? c->weight_loadaware : 0)) >= (1 << 23))
+      return fail(KG_E_UNSUPPORTED, "DeviceShare profiles: Fit + LoadAware weights must keep totals below 2^23");
   }
   if (c->numa_filter || c->numa_score) {
     if (c->weight_numa < 0 || c->weight_numa > 1000000) return fail(KG_E_INVALID, "NodeNUMAResource weight out of range");
@@ -2183,13 +2172,12 @@ void launch_round_ds(kg_engine* e, const RoundGeom& g, int64_t end, hipStream_t 
   const dim3 grid = eval_grid(g, g.B);
   if (which < 0 || which == 3)
     ds_max_round<<<grid, kWave * kEvalWaves, 0, st>>>(e->T, DT, e->pods.p, e->dpods.p, e->cursor.p, end, g.B, g.ppw,
-                                                       g.n_local, g.nt_local, e->P, e->DP, e->dsmax.p);
+                                                       g.n_local, g.nt_local, e->P, e->DP, e->dsmax.p, e->dsval.p);
   if (which < 0 || which == 4)
     ds_norm_reduce<<<g.B, 256, 0, st>>>(e->cursor.p, end, g.B, e->dsmax.p, g.nt_local, e->dsnorm.p);
   if (which < 0 || which == 0)
-    eval_round_ds<<<grid, kWave * kEvalWaves, 0, st>>>(e->T, DT, e->pods.p, e->dpods.p, e->cursor.p, end, g.B, g.ppw,
-                                                        g.n_local, g.nt_local, e->P, e->DP, e->dsnorm.p,
-                                                        lists_slot(e, g, 0));
+    eval_round_ds<<<grid, kWave * kEvalWaves, 0, st>>>(e->cursor.p, end, g.B, g.ppw, g.n_local, g.nt_local, e->P,
+                                                        e->DP, e->dsnorm.p, e->dsval.p, lists_slot(e, g, 0));
   if (which < 0 || which == 1) launch_merge_local(e, g, g.B, 0, st);
   if (which < 0 || which == 2)
     resolve_round_ds<<<1, kWave, resolve_ds_lds_bytes(g, g.B), st>>>(e->T, DT, e->pods.p, e->dpods.p, e->cursor.p,
@@ -2221,6 +2209,7 @@ int prepare_rounds(kg_engine* e, RoundGeom& g) {
   if (e->ds_on) {
     if (int rc = e->dsmax.ensure((size_t)g.B * g.nt_local)) return rc;
     if (int rc = e->dsnorm.ensure((size_t)g.B)) return rc;
+    if (int rc = e->dsval.ensure((size_t)g.B * g.nt_local * kTile)) return rc;
   }
   return 0;
 }
@@ -2482,6 +2471,7 @@ void kg_engine_destroy(kg_engine* e) {
   e->out_minors.release();
   e->dsmax.release();
   e->dsnorm.release();
+  e->dsval.release();
   e->scratch64.release();
   e->scratch32.release();
   if (e->stream) (void)hipStreamDestroy(e->stream);
@@ -3021,7 +3011,9 @@ int kg_bench_kernel(kg_engine* e, int which, int iters, double* avg_ms, double* 
     // NUMA profiles add the node's NumaStatic + NumaMut (232 B) to every evaluation
     const double per_node = kAlgoBytesPerNode + (e->numa_on ? (double)(sizeof(NumaStatic) + sizeof(NumaMut)) : 0.0) +
                             (e->ds_on ? (double)sizeof(DsNode) : 0.0);
-    if (which == 3) *algo_bytes = nbd * (double)g.n_local * per_node + nbd * g.nt_local * 8.0;
+    if (which == 3) *algo_bytes = nbd * (double)g.n_local * (per_node + 4.0) + nbd * g.nt_local * 8.0;  // + dsval
+    else if (which == 0 && e->ds_on)  // eval_round_ds reads the packed values ds_max_round left, writes the lists
+      *algo_bytes = nbd * (double)g.n_local * 4.0 + nbd * g.nt_local * kR * 8.0;
     else if (which == 4) *algo_bytes = nbd * g.nt_local * 8.0 + nbd * 8.0;
     else if (which == 0) *algo_bytes = nbd * (double)g.n_local * per_node + nbd * g.nt_local * kR * 8.0 + nbd * 96.0;
     else if (which == 1) *algo_bytes = nbd * g.nt_local * kR * 8.0 + nbd * kCandStride * 8.0;
