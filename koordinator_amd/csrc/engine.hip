@@ -1194,7 +1194,9 @@ __global__ __launch_bounds__(kWave) void resolve_round_ds(DevTable T, DsTable DT
                                                            const DsPod* __restrict__ dpods,
                                                            int64_t* __restrict__ ctl, int64_t end, int B,
                                                            const uint64_t* __restrict__ cand,
-                                                           const uint64_t* __restrict__ dsnorm, EvalParams P,
+                                                           const uint64_t* __restrict__ dsnorm,
+                                                           const uint32_t* __restrict__ dsval, int64_t dsval_stride,
+                                                           EvalParams P,
                                                            DsParams DP, uint64_t* __restrict__ out_keys,
                                                            int32_t* __restrict__ out_minors, int bitmap_words,
                                                            DevQuota* __restrict__ quotas, int nq) {
@@ -1207,8 +1209,7 @@ __global__ __launch_bounds__(kWave) void resolve_round_ds(DevTable T, DsTable DT
   uint64_t* s_podw = s_cand + (size_t)nb * kCandStride;     // [nb] DevPod
   uint64_t* s_dpw = s_podw + (size_t)nb * kPodWords;        // [nb] DsPod
   uint64_t* s_cur = s_dpw + (size_t)nb * kDsPodWords;       // [kWave] DsNode, current
-  uint64_t* s_rs = s_cur + (size_t)kWave * kDsNodeWords;    // [kWave] DsNode, round start
-  uint64_t* s_stg = s_rs + (size_t)kWave * kDsNodeWords;    // [nb] DsNode of each pod's top candidate
+  uint64_t* s_stg = s_cur + (size_t)kWave * kDsNodeWords;   // [nb] DsNode of each pod's top candidate
   Row* s_srow = reinterpret_cast<Row*>(s_stg + (size_t)nb * kDsNodeWords);  // [nb] its Row
   uint32_t* bitmap = reinterpret_cast<uint32_t*>(s_srow + nb);
   for (int w = lane; w < nb * kCandStride; w += kWave) s_cand[w] = cand[w];
@@ -1235,11 +1236,9 @@ __global__ __launch_bounds__(kWave) void resolve_round_ds(DevTable T, DsTable DT
   const DevPod* s_pods = reinterpret_cast<const DevPod*>(s_podw);
   const DsPod* s_dp = reinterpret_cast<const DsPod*>(s_dpw);
   DsNode* s_dc = reinterpret_cast<DsNode*>(s_cur);
-  DsNode* s_dr = reinterpret_cast<DsNode*>(s_rs);
   uint32_t midx = 0xFFFFFFFFu;
-  Row mrow, rrow;
+  Row mrow;
   mrow.flags = 0;
-  rrow.flags = 0;
   bool touched = false;
   uint64_t my_out = 0;
   int32_t my_minors = 0;
@@ -1259,13 +1258,14 @@ __global__ __launch_bounds__(kWave) void resolve_round_ds(DevTable T, DsTable DT
     const uint64_t nrm = readlane_u64(my_nrm, j);
     const uint32_t Mrs = (uint32_t)(nrm >> 32), Crs = (uint32_t)nrm;  // Mrs = max raw + 1 (0: no feasible node)
     // M_j: the round-start max survives while an unmodified node or a modified row still holds it.  At most nM
-    // holders can have been modified, so with more than nM holders nothing needs re-scoring.
+    // holders can have been modified, so with more than nM holders nothing needs checking.  A modified row's
+    // round-start value for pod j is what ds_max_round packed for it (dsval): no re-score.
     bool cf = false, have_cur = false;
     int64_t ct = 0, craw = 0;
     if (DP.score && Mrs > 0 && Crs <= (uint32_t)nM) {
-      bool rf = false;
-      int64_t rt = 0, rraw = 0;
-      if (lane < nM) rf = eval_node(rrow, p, P, rt) && ds_eval(s_dr[lane], dp, DP, rraw);
+      const uint32_t pk = lane < nM ? dsval[(size_t)j * dsval_stride + midx] : 0u;
+      const bool rf = pk != 0;
+      const int64_t rraw = (int64_t)((pk - 1u) & 255u);
       const uint32_t lost = (uint32_t)__popcll(__ballot(rf && (uint32_t)rraw + 1u == Mrs));
       if (lost >= Crs) {
         if (lane < nM) cf = eval_node(mrow, p, P, ct) && ds_eval(s_dc[lane], dp, DP, craw);
@@ -1306,8 +1306,6 @@ __global__ __launch_bounds__(kWave) void resolve_round_ds(DevTable T, DsTable DT
         const DsNode* from = src >= 0 ? reinterpret_cast<const DsNode*>(s_stg) + src : DT.d + w;
         mrow = src >= 0 ? s_srow[src] : load_row(T, w);
         __builtin_memcpy(&s_dc[owner], from, sizeof(DsNode));
-        __builtin_memcpy(&s_dr[owner], from, sizeof(DsNode));
-        rrow = mrow;
       }
       if (lane == 0) bitmap[w >> 5] |= 1u << (w & 31);
       ++nM;
@@ -2163,7 +2161,7 @@ int run_batch(kg_engine* e, const RoundGeom& g, int64_t cur, int64_t end, int64_
 
 // ---- DeviceShare rounds: cursor-driven, unpipelined, all on rs[0] ----
 size_t resolve_ds_lds_bytes(const RoundGeom& g, int nb) {
-  return ((size_t)nb * (kCandStride + kPodWords + kDsPodWords + kDsNodeWords) + (size_t)2 * kWave * kDsNodeWords) * 8 +
+  return ((size_t)nb * (kCandStride + kPodWords + kDsPodWords + kDsNodeWords) + (size_t)kWave * kDsNodeWords) * 8 +
          (size_t)nb * sizeof(Row) + (size_t)g.bitmap_words * 4;
 }
 
@@ -2181,7 +2179,8 @@ void launch_round_ds(kg_engine* e, const RoundGeom& g, int64_t end, hipStream_t 
   if (which < 0 || which == 1) launch_merge_local(e, g, g.B, 0, st);
   if (which < 0 || which == 2)
     resolve_round_ds<<<1, kWave, resolve_ds_lds_bytes(g, g.B), st>>>(e->T, DT, e->pods.p, e->dpods.p, e->cursor.p,
-                                                                     end, g.B, cand_slot(e, g, 0), e->dsnorm.p, e->P,
+                                                                     end, g.B, cand_slot(e, g, 0), e->dsnorm.p,
+                                                                     e->dsval.p, (int64_t)g.nt_local * kTile, e->P,
                                                                      e->DP, e->out_keys.p, e->out_minors.p,
                                                                      g.bitmap_words, e->quotas.p, e->nq);
 }
@@ -2381,7 +2380,7 @@ int kg_engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank, int
     if (hipMemcpy(e->ds_d.p, e->ds_host.data(), cap * sizeof(DsNode), hipMemcpyHostToDevice) != hipSuccess)
       return bail(fail(KG_E_DEVICE, "hipMemcpy"));
     const int lds = (int)(kMaxNodes / 8 + ((size_t)32 * (kCandStride + kPodWords + kDsPodWords + kDsNodeWords) +
-                                           (size_t)2 * kWave * kDsNodeWords) * 8 + 32 * sizeof(Row));
+                                           (size_t)kWave * kDsNodeWords) * 8 + 32 * sizeof(Row));
     if (hipFuncSetAttribute((const void*)resolve_round_ds, hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess)
       return bail(fail(KG_E_DEVICE, "hipFuncSetAttribute(resolve_round_ds LDS)"));
   }
