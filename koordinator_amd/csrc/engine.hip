@@ -1066,6 +1066,7 @@ __device__ __forceinline__ bool ds_round_range(const int64_t* ctl, int64_t end, 
   return nb > 0;
 }
 
+template <int PF>
 __global__ __launch_bounds__(kWave* kEvalWaves) void ds_max_round(DevTable T, DsTable DT,
                                                                    const DevPod* __restrict__ pods,
                                                                    const DsPod* __restrict__ dpods,
@@ -1091,14 +1092,29 @@ __global__ __launch_bounds__(kWave* kEvalWaves) void ds_max_round(DevTable T, Ds
   for (int j = 0; j < kNPT; ++j) {
     const int64_t i = (int64_t)tile * kTile + j * kWave + lane;
     if (i >= n_local) break;
-    const Row row = load_row(T, i);
+    // Fit + LoadAware on the compact hoisted row of the C3 wide pass (eval_hot); a row outside its exact
+    // domain (F_RARE) sends this node row of the wave to the reference-shaped eval_node
+    const HotRow h = load_hot<PF>(T, i, P);
+    const bool rare = __ballot((h.flags & F_RARE) != 0) != 0;
+    Row row;
+    row.flags = 0;
+    if (rare) row = load_row(T, i);
     const DsNode d = DT.d[i];
 #pragma unroll
     for (int k = 0; k < kDsPpw; ++k) {
       if (k >= np) break;
       int64_t t = 0, raw = 0;
       uint32_t packed = 0;
-      if (eval_node(row, pods[first + p0 + k], P, t) && ds_eval(d, dpods[first + p0 + k], DP, raw)) {
+      const DevPod& pod = pods[first + p0 + k];
+      bool ok;
+      if (rare) {
+        ok = eval_node(row, pod, P, t);
+      } else {
+        uint32_t t32 = 0;
+        ok = eval_hot<PF>(h, pod, P, t32);
+        t = t32;
+      }
+      if (ok && ds_eval(d, dpods[first + p0 + k], DP, raw)) {
         const uint32_t v = (uint32_t)raw + 1u;  // +1: a feasible node with raw 0 still counts
         cnt[k] = v > mx[k] ? 1u : cnt[k] + (v == mx[k] ? 1u : 0u);
         mx[k] = v > mx[k] ? v : mx[k];
@@ -2168,9 +2184,13 @@ size_t resolve_ds_lds_bytes(const RoundGeom& g, int nb) {
 void launch_round_ds(kg_engine* e, const RoundGeom& g, int64_t end, hipStream_t st, int which = -1) {
   const DsTable DT{e->ds_d.p};
   const dim3 grid = eval_grid(g, g.B);
-  if (which < 0 || which == 3)
-    ds_max_round<<<grid, kWave * kEvalWaves, 0, st>>>(e->T, DT, e->pods.p, e->dpods.p, e->cursor.p, end, g.B, g.ppw,
-                                                       g.n_local, g.nt_local, e->P, e->DP, e->dsmax.p, e->dsval.p);
+  if (which < 0 || which == 3) {
+#define KG_DSMAX(X)                                                                                             \
+  ds_max_round<X><<<grid, kWave * kEvalWaves, 0, st>>>(e->T, DT, e->pods.p, e->dpods.p, e->cursor.p, end, g.B, g.ppw, \
+                                                       g.n_local, g.nt_local, e->P, e->DP, e->dsmax.p, e->dsval.p)
+    KG_PF_SWITCH(profile_bits(e->P), KG_DSMAX)
+#undef KG_DSMAX
+  }
   if (which < 0 || which == 4)
     ds_norm_reduce<<<g.B, 256, 0, st>>>(e->cursor.p, end, g.B, e->dsmax.p, g.nt_local, e->dsnorm.p);
   if (which < 0 || which == 0)
