@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define KG_ABI_VERSION 3
+#define KG_ABI_VERSION 4
 
 /* ---- resource slots (fixed order) ------------------------------------------------------- */
 enum {
@@ -127,7 +127,9 @@ enum {
 /* pod flags */
 enum {
   KG_POD_DAEMONSET = 1 << 0,
-  KG_POD_NON_PREEMPTIBLE = 1 << 1   /* extension.IsPodNonPreemptible (ElasticQuota min check) */
+  KG_POD_NON_PREEMPTIBLE = 1 << 1,  /* extension.IsPodNonPreemptible (ElasticQuota min check) */
+  KG_POD_RESERVE = 1 << 2           /* a reservation's reserve pod (kg_pods_add): NodeInfo only — the LoadAware
+                                       assign cache is fed by the pod informer, which never sees it */
 };
 #define KG_MAX_QUOTAS 64
 
@@ -173,7 +175,11 @@ typedef struct kg_config {
   int64_t batch_pods;                          /* pods resolved per device round (B, 1..64)           */
   int64_t pods_per_wave;                       /* pods one eval wave scores per round (1..B)          */
   int64_t device_id;                           /* HIP device ordinal (-1 = current)                   */
-  int64_t reserved[8];
+  /* Reservation (reservation/plugin.go:318-559, scoring.go:42-203; weight scheduler-config.yaml:90-91) */
+  int64_t reservation_filter;                  /* Reservation at Filter (+ BeforePreFilter restore)   */
+  int64_t reservation_score;                   /* Reservation at PreScore/Score (NormalizeScore: DefaultNormalizeScore) */
+  int64_t weight_reservation;
+  int64_t reserved[5];
 } kg_config;
 
 /* One node (snapshot index = position given by the caller). */
@@ -212,8 +218,36 @@ typedef struct kg_pod {
   int64_t preferred_cpu_bind_policy;           /* ResourceSpec annotation: KG_BIND_*                  */
   int64_t device_requests[KG_DEV_RES_MAX];     /* PodRequestsAndLimits of the device resources (KG_DEV_*) */
   int64_t quota_id;                            /* 1 + index into the kg_quotas_set table; 0 = no ElasticQuota */
-  int64_t reserved[2];
+  int64_t reservation_owner;                   /* owner group the caller decoded from the pod against every   */
+                                               /* ReservationInfo.Match (reservation_info.go:231-236,        */
+                                               /* MatchReservationOwners pkg/util/reservation:389-410); 0 = none */
+  int64_t reservation_flags;                   /* KG_POD_RSV_*                                        */
 } kg_pod;
+
+/* pod reservation flags */
+enum {
+  KG_POD_RSV_AFFINITY = 1 << 0   /* GetRequiredReservationAffinity != nil: must allocate from a reservation */
+};
+
+/* Reservation slots of one node as reservationCache holds them (frameworkext/reservation_info.go:79-99,
+ * reservation/cache.go:56-61).  The reserve pods stay in NodeInfo (kg_pods_add: requests = allocatable), as the
+ * reference's scheduler cache keeps them.  Policies: reservation allocate policy (Default / Aligned / Restricted). */
+#define KG_MAX_RSV_SLOTS 4
+enum { KG_RSV_POLICY_DEFAULT = 0, KG_RSV_POLICY_ALIGNED = 1, KG_RSV_POLICY_RESTRICTED = 2 };
+typedef struct kg_node_reservations {
+  int64_t n;                                   /* slots in use (0..KG_MAX_RSV_SLOTS), by reservation index    */
+  int64_t owner[KG_MAX_RSV_SLOTS];             /* owner group a pod's reservation_owner must equal            */
+  int64_t allocatable_cpu[KG_MAX_RSV_SLOTS];   /* ReservationInfo.Allocatable (milli; both > 0)               */
+  int64_t allocatable_mem[KG_MAX_RSV_SLOTS];
+  int64_t allocated_cpu[KG_MAX_RSV_SLOTS];     /* ReservationInfo.Allocated (Σ assigned pods' requests)       */
+  int64_t allocated_mem[KG_MAX_RSV_SLOTS];
+  int64_t assigned[KG_MAX_RSV_SLOTS];          /* len(AssignedPods)                                            */
+  int64_t order[KG_MAX_RSV_SLOTS];             /* LabelReservationOrder value (0 = absent; < 2^31)             */
+  int64_t policy[KG_MAX_RSV_SLOTS];            /* KG_RSV_POLICY_*                                             */
+  int64_t allocate_once[KG_MAX_RSV_SLOTS];     /* IsAllocateOnce                                               */
+  int64_t available[KG_MAX_RSV_SLOTS];         /* IsAvailable && ParseError == nil                             */
+  int64_t unschedulable[KG_MAX_RSV_SLOTS];     /* IsUnschedulable                                              */
+} kg_node_reservations;
 
 /* One ElasticQuota as the plugin's PreFilter snapshot sees it (plugin.go:211-256): cpu (milli) and memory (bytes).
  * used_limit = runtime when EnableRuntimeQuota else max (getQuotaInfoUsedLimit).  Runtime is refreshed from the
@@ -341,6 +375,15 @@ int kg_results_fetch_devices(kg_engine* e, int64_t first, int64_t count, int32_t
  * (un-normalized) score, 0 where Filter rejects. */
 int kg_pods_evaluate_device(kg_engine* e, const kg_pod* pod, int32_t* out_pass, int64_t* out_score);
 
+/* Reservation (engines whose profile enables it): the reservation slots of nodes idx[0..n) (replaces each node's
+ * slots; fed by the reservation informer, eventhandlers/reservation_handler.go).  The Reservation profile runs
+ * one FIFO pod per device pass (BeforePreFilter restore + Filter + PreScore/nominate + Score + NormalizeScore). */
+int kg_nodes_reservation_upsert(kg_engine* e, const kg_node_reservations* r, const int32_t* idx, int64_t n);
+/* Reads the DEVICE reservation slots: allocated cpu / memory and assigned count, KG_MAX_RSV_SLOTS per node. */
+int kg_nodes_read_reservations(kg_engine* e, int64_t* allocated_cpu, int64_t* allocated_mem, int64_t* assigned);
+/* The reservation slot Reserve assumed each staged pod [first, first+count) into (-1 = none). */
+int kg_results_fetch_reservations(kg_engine* e, int64_t first, int64_t count, int32_t* out_slot);
+
 /* ElasticQuota admission (engines whose pods carry quota_id): replaces the quota table (n ≤ KG_MAX_QUOTAS).
  * Every scheduled pod runs PreFilter's check (used + request ≤ used_limit over the pod's cpu/memory requests; for
  * non-preemptible pods also non_preemptible_used + request ≤ min) before its node search, and a placed pod is
@@ -374,7 +417,7 @@ int kg_debug_stamps(kg_engine* e, uint64_t* out);
 const char* kg_last_error(void);
 int kg_abi_version(void);
 /* sizeof of the ABI structs (0 kg_config, 1 kg_node, 2 kg_node_metric, 3 kg_pod, 4 kg_stats, 5 kg_node_numa,
- * 6 kg_node_device, 7 kg_quota) for
+ * 6 kg_node_device, 7 kg_quota, 8 kg_node_reservations) for
  * binding checks. */
 int64_t kg_abi_struct_size(int which);
 

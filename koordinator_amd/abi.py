@@ -30,9 +30,12 @@ PRIORITY_CLASSES = {"": PRIO_NONE, "koord-prod": PRIO_PROD, "koord-mid": PRIO_MI
 OK, E_INVALID, E_DEVICE, E_COLLECTIVE, E_NOMEM, E_UNSUPPORTED = 0, -1, -2, -3, -4, -5
 REJECT_FIT_PODS, REJECT_FIT_CPU, REJECT_FIT_MEMORY, REJECT_LOADAWARE, REJECT_INVALID_NODE = 1, 2, 4, 8, 16
 NODE_VALID, NODE_HAS_RAW_ALLOCATABLE, NODE_HAS_CUSTOM_THRESHOLDS = 1, 2, 4
-POD_DAEMONSET, POD_NON_PREEMPTIBLE = 1, 2
+POD_DAEMONSET, POD_NON_PREEMPTIBLE, POD_RESERVE = 1, 2, 4
 MAX_QUOTAS = 64
-ABI_VERSION = 3
+ABI_VERSION = 4
+MAX_RSV_SLOTS = 4
+RSV_POLICY = {"Default": 0, "Aligned": 1, "Restricted": 2}
+POD_RSV_AFFINITY = 1
 MAX_NUMA, MAX_CPUS = 4, 256
 QOS = {"": 0, "LSE": 1, "LSR": 2, "LS": 3, "BE": 4, "SYSTEM": 5}
 BIND = {"": 0, "Default": 1, "FullPCPUs": 2, "SpreadByPCPUs": 3, "ConstrainedBurst": 4}
@@ -75,7 +78,8 @@ CONFIG_DTYPE = np.dtype([
     _i64("ds_filter"), _i64("ds_score"), _i64("weight_deviceshare"), _i64("ds_scoring_strategy"),
     _i64("ds_scoring_weights", 3),
     _i64("batch_pods"), _i64("pods_per_wave"), _i64("device_id"),
-    _i64("reserved", 8),
+    _i64("reservation_filter"), _i64("reservation_score"), _i64("weight_reservation"),
+    _i64("reserved", 5),
 ])
 
 NODE_DTYPE = np.dtype([
@@ -105,8 +109,12 @@ POD_DTYPE = np.dtype([
     _i64("qos"), _i64("required_cpu_bind_policy"), _i64("preferred_cpu_bind_policy"),
     _i64("device_requests", DEV_RES_MAX),
     _i64("quota_id"),
-    _i64("reserved", 2),
+    _i64("reservation_owner"), _i64("reservation_flags"),
 ])
+
+NODE_RSV_DTYPE = np.dtype([_i64("n")] + [_i64(f, MAX_RSV_SLOTS) for f in (
+    "owner", "allocatable_cpu", "allocatable_mem", "allocated_cpu", "allocated_mem", "assigned", "order", "policy",
+    "allocate_once", "available", "unschedulable")])
 
 QUOTA_DTYPE = np.dtype([_i64("used", 2), _i64("non_preemptible_used", 2), _i64("used_limit", 2), _i64("min", 2)])
 
@@ -130,7 +138,7 @@ STATS_DTYPE = np.dtype([
 ])
 
 STRUCT_DTYPES = {0: CONFIG_DTYPE, 1: NODE_DTYPE, 2: METRIC_DTYPE, 3: POD_DTYPE, 4: STATS_DTYPE, 5: NODE_NUMA_DTYPE,
-                 6: NODE_DEVICE_DTYPE, 7: QUOTA_DTYPE}
+                 6: NODE_DEVICE_DTYPE, 7: QUOTA_DTYPE, 8: NODE_RSV_DTYPE}
 
 # Every symbol include/koordgpu.h declares (tests check the library exports all of them).
 EXPORTED_SYMBOLS = (
@@ -141,7 +149,8 @@ EXPORTED_SYMBOLS = (
     "kg_abi_struct_size", "kg_nccl_unique_id", "kg_debug_eval_paths", "kg_debug_stamps", "kg_debug_fast_lrs",
     "kg_nodes_numa_upsert", "kg_nodes_read_numa", "kg_results_fetch_cpusets", "kg_pods_evaluate_numa",
     "kg_nodes_device_upsert", "kg_nodes_read_device", "kg_results_fetch_devices", "kg_pods_evaluate_device",
-    "kg_quotas_set", "kg_quotas_read",
+    "kg_quotas_set", "kg_quotas_read", "kg_nodes_reservation_upsert", "kg_nodes_read_reservations",
+    "kg_results_fetch_reservations",
 )
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
@@ -203,6 +212,9 @@ def load_library(path: str | None = None):
         "kg_pods_evaluate_device": (i, [vp, vp, vp, vp]),
         "kg_quotas_set": (i, [vp, vp, i64]),
         "kg_quotas_read": (i, [vp, vp, i64]),
+        "kg_nodes_reservation_upsert": (i, [vp, vp, vp, i64]),
+        "kg_nodes_read_reservations": (i, [vp, vp, vp, vp]),
+        "kg_results_fetch_reservations": (i, [vp, i64, i64, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)

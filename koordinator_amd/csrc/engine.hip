@@ -28,6 +28,7 @@
 #include "kernels.h"
 #include "numa_dev.h"
 #include "ds_dev.h"
+#include "rsv_dev.h"
 
 using namespace kg;
 
@@ -1613,6 +1614,15 @@ struct kg_engine {
   // ElasticQuota admission table (kg_quotas_set)
   DevBuf<DevQuota> quotas;     // [KG_MAX_QUOTAS]
   int nq = 0;
+  // Reservation (profile enables it): per-node slots, per-pod owner/affinity, Reserve's slots, pass scratch
+  bool rsv_on = false;
+  RsvParams RP{};
+  DevBuf<RsvNode> rsv_d;
+  DevBuf<int32_t> rsv_nd;       // slots in use per node
+  DevBuf<RsvPod> rpods;
+  DevBuf<int32_t> out_rslot;    // [staged + kMaxB]
+  DevBuf<uint64_t> rsv_val;     // [capacity] packed per-node pass-1 values
+  DevBuf<unsigned long long> rsv_ws;  // [4]
 };
 
 namespace {
@@ -1635,6 +1645,11 @@ int validate_config(const kg_config* c) {
   if (c->weight_fit < 0 || c->weight_fit > 1000000 || c->weight_loadaware < 0 || c->weight_loadaware > 1000000)
     return fail(KG_E_INVALID, "plugin weight out of range");
   if (c->batch_pods < 0 || c->batch_pods > kMaxB) return fail(KG_E_INVALID, "batch_pods must be in [1,%d]", kMaxB);
+  if (c->reservation_filter || c->reservation_score) {
+    if (c->weight_reservation < 0 || c->weight_reservation > 1000000) return fail(KG_E_INVALID, "Reservation weight out of range");
+    if (c->numa_filter || c->numa_score || c->ds_filter || c->ds_score)
+      return fail(KG_E_UNSUPPORTED, "Reservation with NodeNUMAResource / DeviceShare in one profile is not accelerated");
+  }
   if (c->ds_filter || c->ds_score) {
     if (c->weight_deviceshare < 0 || c->weight_deviceshare > 1000000) return fail(KG_E_INVALID, "DeviceShare weight out of range");
     if (c->ds_scoring_strategy != KG_STRATEGY_LEAST_ALLOCATED)
@@ -2237,6 +2252,75 @@ double now_s() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
+
+// Reservation profile: one FIFO pod per device pass (rsv_eval → rsv_select → rsv_apply), kRsvGroup passes per
+// hipGraph launch.  The pod index lives in the device cursor ws[3]; passes past `end` are no-ops.
+constexpr int kRsvGroup = 32;
+int run_rsv(kg_engine* e, int64_t first, int64_t count, kg_stats* stats, double t0) {
+  if (int rc = sync_static(e)) return rc;
+  const int64_t n = e->n_nodes, end = first + count;
+  if (count > 0 && n > 0) {
+    const unsigned blocks = (unsigned)((n + 255) / 256);
+    const unsigned long long init[4] = {0, 0, 0, (unsigned long long)first};
+    HIP_TRY(hipMemcpyAsync(e->rsv_ws.p, init, 32, hipMemcpyHostToDevice, e->stream));
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t exec = nullptr;
+    HIP_TRY(hipStreamBeginCapture(e->stream, hipStreamCaptureModeThreadLocal));
+    for (int g = 0; g < kRsvGroup; ++g) {
+      rsv_eval<<<blocks, 256, 0, e->stream>>>(e->T, e->rsv_d.p, e->rsv_nd.p, e->pods.p, e->rpods.p, end, n, e->P,
+                                               e->RP, e->rsv_val.p, e->rsv_ws.p);
+      rsv_select<<<blocks, 256, 0, e->stream>>>(e->rsv_val.p, end, n, e->RP, e->rsv_ws.p);
+      rsv_apply<<<1, 1, 0, e->stream>>>(e->T, e->rsv_d.p, e->rsv_val.p, e->pods.p, end, e->out_keys.p,
+                                        e->out_rslot.p, e->rsv_ws.p);
+    }
+    const hipError_t ce = hipStreamEndCapture(e->stream, &graph);
+    if (ce != hipSuccess) return fail(KG_E_DEVICE, "hipStreamEndCapture: %s", hipGetErrorString(ce));
+    hipError_t ge = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+    for (int64_t c = 0; ge == hipSuccess && c < count; c += kRsvGroup) ge = hipGraphLaunch(exec, e->stream);
+    if (ge == hipSuccess) ge = hipStreamSynchronize(e->stream);
+    if (exec) (void)hipGraphExecDestroy(exec);
+    (void)hipGraphDestroy(graph);
+    if (ge != hipSuccess) return fail(KG_E_DEVICE, "reservation pass graph: %s", hipGetErrorString(ge));
+  } else if (count > 0) {
+    HIP_TRY(hipMemsetAsync(e->out_keys.p + first, 0, count * 8, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+  }
+  if (stats) {
+    std::memset(stats, 0, sizeof(*stats));
+    stats->device_batches = (count + kRsvGroup - 1) / kRsvGroup;
+    stats->node_evaluations = count * n;
+    stats->seconds = now_s() - t0;
+  }
+  return 0;
+}
+
+int decode_node_rsv(const kg_node_reservations& r, RsvNode& d, int32_t& ns) {
+  std::memset(&d, 0, sizeof(d));
+  if (r.n < 0 || r.n > KG_MAX_RSV_SLOTS) return fail(KG_E_INVALID, "reservation slot count %lld", (long long)r.n);
+  ns = (int32_t)r.n;
+  for (int s = 0; s < ns; ++s) {
+    if (r.allocatable_cpu[s] <= 0 || r.allocatable_mem[s] <= 0 || r.allocatable_cpu[s] > (int64_t(1) << 40) ||
+        r.allocatable_mem[s] > (int64_t(1) << 46))
+      return fail(KG_E_UNSUPPORTED, "reservation slot %d: allocatable cpu and memory must be in (0, 2^40] / (0, 2^46]", s);
+    if (r.allocated_cpu[s] < 0 || r.allocated_mem[s] < 0 || r.allocated_cpu[s] > (int64_t(1) << 40) ||
+        r.allocated_mem[s] > (int64_t(1) << 46) || r.assigned[s] < 0 || r.assigned[s] > INT32_MAX / 2)
+      return fail(KG_E_INVALID, "reservation slot %d: allocated / assigned out of range", s);
+    if (r.order[s] < 0 || r.order[s] >= INT32_MAX) return fail(KG_E_UNSUPPORTED, "reservation slot %d: order outside [0, 2^31-1)", s);
+    if (r.owner[s] < 0 || r.owner[s] > INT32_MAX) return fail(KG_E_INVALID, "reservation slot %d: owner outside [0, 2^31)", s);
+    if (r.policy[s] < KG_RSV_POLICY_DEFAULT || r.policy[s] > KG_RSV_POLICY_RESTRICTED) return fail(KG_E_INVALID, "reservation policy");
+    d.alloc_cpu[s] = r.allocatable_cpu[s];
+    d.alloc_mem[s] = r.allocatable_mem[s];
+    d.allocd_cpu[s] = r.allocated_cpu[s];
+    d.allocd_mem[s] = r.allocated_mem[s];
+    d.owner[s] = (int32_t)r.owner[s];
+    d.assigned[s] = (int32_t)r.assigned[s];
+    d.order[s] = (int32_t)r.order[s];
+    d.meta[s] = (r.available[s] ? RS_AVAIL : 0u) | (r.allocate_once[s] ? RS_ONCE : 0u) |
+                (r.unschedulable[s] ? RS_UNSCHED : 0u) | ((uint32_t)r.policy[s] << 4);
+  }
+  return 0;
+}
+
 }  // namespace
 
 // ------------------------------------------------------------------------------------------------
@@ -2256,6 +2340,7 @@ int64_t kg_abi_struct_size(int which) {
     case 5: return sizeof(kg_node_numa);
     case 6: return sizeof(kg_node_device);
     case 7: return sizeof(kg_quota);
+    case 8: return sizeof(kg_node_reservations);
   }
   return -1;
 }
@@ -2382,11 +2467,25 @@ int kg_engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank, int
   e->numa_on = c.numa_filter || c.numa_score;
   e->ds_on = c.ds_filter || c.ds_score;
   if (e->ds_on && n_ranks > 1) return bail(fail(KG_E_UNSUPPORTED, "DeviceShare profiles run on one rank"));
+  e->rsv_on = c.reservation_filter || c.reservation_score;
+  if (e->rsv_on && n_ranks > 1) return bail(fail(KG_E_UNSUPPORTED, "Reservation profiles run on one rank"));
+  e->RP.filter = (int32_t)(c.reservation_filter != 0);
+  e->RP.score = (int32_t)(c.reservation_score != 0);
+  e->RP.weight = (int32_t)c.weight_reservation;
+  if (e->rsv_on) {
+    if (int rc = e->rsv_d.ensure(cap)) return bail(rc);
+    if (int rc = e->rsv_nd.ensure(cap)) return bail(rc);
+    if (int rc = e->rsv_val.ensure(cap)) return bail(rc);
+    if (int rc = e->rsv_ws.ensure(4)) return bail(rc);
+    if (hipMemset(e->rsv_nd.p, 0, cap * 4) != hipSuccess || hipMemset(e->rsv_ws.p, 0, 32) != hipSuccess)
+      return bail(fail(KG_E_DEVICE, "hipMemset"));
+  }
   const int64_t max_total = 100 * ((c.fit_score ? c.weight_fit : 0) + (c.la_score ? c.weight_loadaware : 0) +
-                                   (c.numa_score ? c.weight_numa : 0) + (c.ds_score ? c.weight_deviceshare : 0));
+                                   (c.numa_score ? c.weight_numa : 0) + (c.ds_score ? c.weight_deviceshare : 0) +
+                                   (c.reservation_score ? c.weight_reservation : 0));
   e->P.score_bits = (int32_t)bits_for(max_total);
   // NodeResourcesFit + LoadAwareScheduling: assume only lowers a node's key; NodeNUMAResource does not
-  e->P.monotone = (e->numa_on || e->ds_on) ? 0 : 1;  // DeviceShare: normalization couples every node's key
+  e->P.monotone = (e->numa_on || e->ds_on || e->rsv_on) ? 0 : 1;  // DeviceShare: normalization couples every node's key
   e->DP.filter = (int32_t)(c.ds_filter != 0);
   e->DP.score = (int32_t)(c.ds_score != 0);
   e->DP.weight = (int32_t)c.weight_deviceshare;
@@ -2491,6 +2590,12 @@ void kg_engine_destroy(kg_engine* e) {
   e->dsmax.release();
   e->dsnorm.release();
   e->dsval.release();
+  e->rsv_d.release();
+  e->rsv_nd.release();
+  e->rpods.release();
+  e->out_rslot.release();
+  e->rsv_val.release();
+  e->rsv_ws.release();
   e->scratch64.release();
   e->scratch32.release();
   if (e->stream) (void)hipStreamDestroy(e->stream);
@@ -2569,10 +2674,11 @@ static int pods_delta(kg_engine* e, const kg_pod* pods, const int32_t* node_idx,
     x.d[2] = sign * p.nz_cpu;
     x.d[3] = sign * p.nz_mem;
     x.d[4] = sign;
-    x.d[5] = sign * p.est_cpu;
-    x.d[6] = sign * p.est_mem;
-    x.d[7] = (p.flags & P_PROD) ? sign * p.est_cpu : 0;
-    x.d[8] = (p.flags & P_PROD) ? sign * p.est_mem : 0;
+    const int64_t la = (pods[k].flags & KG_POD_RESERVE) ? 0 : sign;  // reserve pods: not in the assign cache
+    x.d[5] = la * p.est_cpu;
+    x.d[6] = la * p.est_mem;
+    x.d[7] = (p.flags & P_PROD) ? la * p.est_cpu : 0;
+    x.d[8] = (p.flags & P_PROD) ? la * p.est_mem : 0;
   }
   return push_deltas(e, d);
 }
@@ -2629,6 +2735,20 @@ int kg_pods_stage(kg_engine* e, const kg_pod* pods, int64_t n) {
           return fail(KG_E_UNSUPPORTED, "pod %lld requests devices; the profile has no DeviceShare (NodeResourcesFit on "
                       "device resources is not accelerated)", (long long)k);
   }
+  if (e->rsv_on) {
+    std::vector<RsvPod> hr(std::max<int64_t>(n, 1));
+    for (int64_t k = 0; k < n; ++k) {
+      if (pods[k].quota_id > 0) return fail(KG_E_UNSUPPORTED, "pod %lld: ElasticQuota with Reservation is not accelerated", (long long)k);
+      if (pods[k].reservation_owner < 0 || pods[k].reservation_owner > INT32_MAX)
+        return fail(KG_E_INVALID, "pod %lld: reservation_owner outside [0, 2^31)", (long long)k);
+      hr[k].owner = (int32_t)pods[k].reservation_owner;
+      hr[k].flags = (pods[k].reservation_flags & KG_POD_RSV_AFFINITY) ? RP_AFFINITY : 0u;
+    }
+    if (int rc = e->rpods.ensure(n + kMaxB)) return rc;
+    if (int rc = e->out_rslot.ensure(n + kMaxB)) return rc;
+    if (n > 0) HIP_TRY(hipMemcpyAsync(e->rpods.p, hr.data(), n * sizeof(RsvPod), hipMemcpyHostToDevice, e->stream));
+    HIP_TRY(hipMemsetAsync(e->out_rslot.p, 0xff, (n + kMaxB) * 4, e->stream));
+  }
   HIP_TRY(hipStreamSynchronize(e->stream));
   e->n_staged = n;
   return 0;
@@ -2638,6 +2758,7 @@ int kg_pods_schedule_staged(kg_engine* e, int64_t first, int64_t count, kg_stats
   if (!e) return fail(KG_E_INVALID, "engine is NULL");
   if (first < 0 || count < 0 || first + count > e->n_staged) return fail(KG_E_INVALID, "staged range");
   const double t0 = now_s();
+  if (e->rsv_on) return run_rsv(e, first, count, stats, t0);
   RoundGeom g;
   if (int rc = prepare_rounds(e, g)) return rc;
   const int64_t end = first + count;
@@ -3101,6 +3222,65 @@ int kg_debug_fast_lrs(kg_engine* e, const int64_t* req, const int64_t* cap, int6
   HIP_TRY(hipMemcpyAsync(out_mem, b.p + 3 * n, n * 8, hipMemcpyDeviceToHost, e->stream));
   HIP_TRY(hipStreamSynchronize(e->stream));
   b.release();
+  return 0;
+}
+
+int kg_nodes_reservation_upsert(kg_engine* e, const kg_node_reservations* r, const int32_t* idx, int64_t n) {
+  if (!e || (n > 0 && (!r || !idx))) return fail(KG_E_INVALID, "null argument");
+  if (!e->rsv_on) return fail(KG_E_INVALID, "the profile does not enable Reservation");
+  if (n == 0) return 0;
+  std::vector<RsvNode> h(n);
+  std::vector<int32_t> hn(n);
+  for (int64_t k = 0; k < n; ++k) {
+    if (idx[k] < 0 || idx[k] >= e->capacity) return fail(KG_E_INVALID, "node index %d outside capacity", idx[k]);
+    if (int rc = decode_node_rsv(r[k], h[k], hn[k])) return rc;
+  }
+  DevBuf<uint8_t> b;
+  if (int rc = b.ensure(n * (sizeof(RsvNode) + 8))) return rc;
+  RsvNode* dd = reinterpret_cast<RsvNode*>(b.p);
+  int32_t* dn = reinterpret_cast<int32_t*>(b.p + n * sizeof(RsvNode));
+  int32_t* di = dn + n;
+  HIP_TRY(hipMemcpyAsync(dd, h.data(), n * sizeof(RsvNode), hipMemcpyHostToDevice, e->stream));
+  HIP_TRY(hipMemcpyAsync(dn, hn.data(), n * 4, hipMemcpyHostToDevice, e->stream));
+  HIP_TRY(hipMemcpyAsync(di, idx, n * 4, hipMemcpyHostToDevice, e->stream));
+  scatter_rsv<<<(unsigned)((n + 255) / 256), 256, 0, e->stream>>>(e->rsv_d.p, e->rsv_nd.p, dd, dn, di, n);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  b.release();
+  return 0;
+}
+
+int kg_nodes_read_reservations(kg_engine* e, int64_t* allocated_cpu, int64_t* allocated_mem, int64_t* assigned) {
+  if (!e) return fail(KG_E_INVALID, "engine is NULL");
+  if (!e->rsv_on) return fail(KG_E_INVALID, "the profile does not enable Reservation");
+  const int64_t n = e->n_nodes;
+  if (n == 0) return 0;
+  std::vector<RsvNode> h(n);
+  std::vector<int32_t> hn(n);
+  HIP_TRY(hipMemcpyAsync(h.data(), e->rsv_d.p, n * sizeof(RsvNode), hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipMemcpyAsync(hn.data(), e->rsv_nd.p, n * 4, hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  for (int64_t i = 0; i < n; ++i)
+    for (int s = 0; s < KG_MAX_RSV_SLOTS; ++s) {
+      const bool on = s < hn[i];
+      if (allocated_cpu) allocated_cpu[i * KG_MAX_RSV_SLOTS + s] = on ? h[i].allocd_cpu[s] : 0;
+      if (allocated_mem) allocated_mem[i * KG_MAX_RSV_SLOTS + s] = on ? h[i].allocd_mem[s] : 0;
+      if (assigned) assigned[i * KG_MAX_RSV_SLOTS + s] = on ? h[i].assigned[s] : 0;
+    }
+  return 0;
+}
+
+int kg_results_fetch_reservations(kg_engine* e, int64_t first, int64_t count, int32_t* out_slot) {
+  if (!e || (count > 0 && !out_slot)) return fail(KG_E_INVALID, "null argument");
+  if (first < 0 || count < 0 || first + count > e->n_staged) return fail(KG_E_INVALID, "staged range");
+  if (!e->rsv_on) {
+    for (int64_t i = 0; i < count; ++i) out_slot[i] = -1;
+    return 0;
+  }
+  if (count > 0) {
+    HIP_TRY(hipMemcpyAsync(out_slot, e->out_rslot.p + first, count * 4, hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+  }
   return 0;
 }
 

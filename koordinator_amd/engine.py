@@ -103,6 +103,25 @@ class Engine:
         idx = self._idx(idx, len(node_device))
         check(self.lib, self.lib.kg_nodes_device_upsert(self.h, ptr(node_device), ptr(idx), len(node_device)))
 
+    def upsert_reservations(self, node_rsv: np.ndarray, idx=None):
+        """Reservation slots of nodes `idx` (kg_nodes_reservation_upsert)."""
+        node_rsv = np.ascontiguousarray(node_rsv, dtype=abi.NODE_RSV_DTYPE)
+        idx = self._idx(idx, len(node_rsv))
+        check(self.lib, self.lib.kg_nodes_reservation_upsert(self.h, ptr(node_rsv), ptr(idx), len(node_rsv)))
+
+    def read_reservations(self):
+        """(allocated cpu, allocated memory, assigned), int64[n, KG_MAX_RSV_SLOTS] each, from the device."""
+        n = self.num_nodes
+        out = [np.zeros((n, abi.MAX_RSV_SLOTS), dtype=np.int64) for _ in range(3)]
+        check(self.lib, self.lib.kg_nodes_read_reservations(self.h, *[ptr(o) for o in out]))
+        return tuple(out)
+
+    def fetch_reservations(self, first: int, count: int) -> np.ndarray:
+        """int32[count]: the reservation slot Reserve assumed each staged pod into (-1 = none)."""
+        out = np.zeros(count, dtype=np.int32)
+        check(self.lib, self.lib.kg_results_fetch_reservations(self.h, int(first), int(count), ptr(out)))
+        return out
+
     def set_quotas(self, quotas: np.ndarray):
         """ElasticQuota table (kg_quotas_set): pods' quota_id = 1 + index."""
         quotas = np.ascontiguousarray(quotas, dtype=abi.QUOTA_DTYPE)

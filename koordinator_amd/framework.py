@@ -28,6 +28,7 @@ from .quantity import resource_value
 SUCCESS, UNSCHEDULABLE = "Success", "Unschedulable"
 NODE_RESOURCES_FIT, LOAD_AWARE, NODE_NUMA_RESOURCE = "NodeResourcesFit", "LoadAwareScheduling", "NodeNUMAResource"
 DEVICE_SHARE = "DeviceShare"
+RESERVATION = "Reservation"
 
 
 def _slots(d: dict | None, absent=0) -> np.ndarray:
@@ -119,6 +120,9 @@ def build_config(la: LoadAwareSchedulingArgs | None = None, fit: NodeResourcesFi
     r["ds_filter"] = int(DEVICE_SHARE in profile.filter)
     r["ds_score"] = int(DEVICE_SHARE in profile.score)
     r["weight_deviceshare"] = int(profile.score.get(DEVICE_SHARE, 0))
+    r["reservation_filter"] = int(RESERVATION in profile.filter)
+    r["reservation_score"] = int(RESERVATION in profile.score)
+    r["weight_reservation"] = int(profile.score.get(RESERVATION, 0))
     r["ds_scoring_strategy"] = abi.STRATEGY[ds.scoring_strategy]
     r["ds_scoring_weights"] = [ds.scoring_resources.get("koordinator.sh/gpu-core", 0),
                                ds.scoring_resources.get("koordinator.sh/gpu-memory", 0),

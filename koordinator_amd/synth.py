@@ -285,3 +285,76 @@ def make_gpu_pods(n_pods: int, seed: int = BASE_SEED + 7) -> np.ndarray:
 def load_gpu_into(engine, cluster: Cluster, dev: np.ndarray):
     load_into(engine, cluster)
     engine.upsert_devices(dev)
+
+
+# ---- config C5: Reservation matching (50k nodes; 0–4 reservations on 30 % of nodes, owner label selectors) -----
+N_OWNERS = 64
+
+
+def make_rsv_cluster(n_nodes: int, seed: int = BASE_SEED + 8) -> tuple:
+    """(Cluster, kg_node_reservations[n]) for config C5's Reservation part: make_cluster's nodes, 30 % of them with
+    1–4 Available reservations (cpu {2,4,8,16} cores, memory {4..64} GiB, owner group 1..64, 40 % carrying an
+    order label, policy Default 60 % / Aligned 20 % / Restricted 20 %, 20 % AllocateOnce).  Each reservation's
+    reserve pod sits in NodeInfo (requests = allocatable, KG_POD_RESERVE) and 0–2 pods are already assigned to it
+    (in NodeInfo and the LoadAware assign cache, accounted in Allocated)."""
+    cluster = make_cluster(n_nodes, seed=seed)
+    rng = np.random.default_rng(seed + 1000)
+    n = n_nodes
+    rsv = np.zeros(n, dtype=abi.NODE_RSV_DTYPE)
+    has = rng.random(n) < 0.3
+    rsv["n"] = np.where(has, rng.integers(1, abi.MAX_RSV_SLOTS + 1, n), 0)
+    S = abi.MAX_RSV_SLOTS
+    cpu = rng.choice(np.array([2, 4, 8, 16], dtype=np.int64), (n, S)) * 1000
+    mem = rng.choice(np.array([4, 8, 16, 32, 64], dtype=np.int64), (n, S)) * GI
+    on = np.arange(S)[None, :] < rsv["n"][:, None]
+    rsv["allocatable_cpu"] = np.where(on, cpu, 0)
+    rsv["allocatable_mem"] = np.where(on, mem, 0)
+    rsv["owner"] = np.where(on, rng.integers(1, N_OWNERS + 1, (n, S)), 0)
+    rsv["order"] = np.where(on & (rng.random((n, S)) < 0.4), rng.integers(1, 1000, (n, S)), 0)
+    u = rng.random((n, S))
+    rsv["policy"] = np.where(on, np.where(u < 0.6, 0, np.where(u < 0.8, 1, 2)), 0)
+    rsv["allocate_once"] = on & (rng.random((n, S)) < 0.2)
+    rsv["available"] = on
+    # pods already assigned to reservations: 0–2 per reservation, each a quarter of it
+    k = np.where(on, rng.integers(0, 3, (n, S)), 0)
+    k = np.where(rsv["allocate_once"].astype(bool), np.minimum(k, 1), k)
+    rsv["assigned"] = k
+    rsv["allocated_cpu"] = k * (cpu // 4) * on
+    rsv["allocated_mem"] = k * (mem // 4) * on
+    extra_pods, extra_node = [], []
+    ii, ss = np.nonzero(on)
+    for i, s in zip(ii.tolist(), ss.tolist()):
+        rp = np.zeros(1, dtype=abi.POD_DTYPE)[0]
+        rp["requests"][abi.RES_CPU] = rp["limits"][abi.RES_CPU] = rp["nonzero_requests"][0] = cpu[i, s]
+        rp["requests"][abi.RES_MEMORY] = rp["limits"][abi.RES_MEMORY] = rp["nonzero_requests"][1] = mem[i, s]
+        rp["priority_class"] = abi.PRIO_PROD
+        rp["flags"] = abi.POD_RESERVE
+        extra_pods.append(rp)
+        extra_node.append(i)
+        for _ in range(int(k[i, s])):
+            ap = np.zeros(1, dtype=abi.POD_DTYPE)[0]
+            ap["requests"][abi.RES_CPU] = ap["limits"][abi.RES_CPU] = ap["nonzero_requests"][0] = cpu[i, s] // 4
+            ap["requests"][abi.RES_MEMORY] = ap["limits"][abi.RES_MEMORY] = ap["nonzero_requests"][1] = mem[i, s] // 4
+            ap["priority_class"] = abi.PRIO_PROD
+            extra_pods.append(ap)
+            extra_node.append(i)
+    if extra_pods:
+        cluster.existing_pods = np.concatenate([cluster.existing_pods, np.array(extra_pods, dtype=abi.POD_DTYPE)])
+        cluster.existing_node = np.concatenate([cluster.existing_node, np.array(extra_node, dtype=np.int32)])
+    return cluster, rsv
+
+
+def make_rsv_pods(n_pods: int, seed: int = BASE_SEED + 9) -> np.ndarray:
+    """Config C5 Reservation queue: make_pods' pods, 20 % owned by a reservation owner group (matching label
+    selectors), a quarter of those with a required reservation affinity."""
+    p = make_pods(n_pods, seed=seed)
+    rng = np.random.default_rng(seed + 1000)
+    owned = rng.random(n_pods) < 0.2
+    p["reservation_owner"] = np.where(owned, rng.integers(1, N_OWNERS + 1, n_pods), 0)
+    p["reservation_flags"] = np.where(owned & (rng.random(n_pods) < 0.25), abi.POD_RSV_AFFINITY, 0)
+    return p
+
+
+def load_rsv_into(engine, cluster: Cluster, rsv: np.ndarray):
+    load_into(engine, cluster)
+    engine.upsert_reservations(rsv)

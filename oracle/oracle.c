@@ -224,6 +224,7 @@ void or_apply_pod(const kg_config* cfg, or_node_state* st, const kg_pod* pod, in
   st->nonzero[0] += sign * pod->nonzero_requests[0];
   st->nonzero[1] += sign * pod->nonzero_requests[1];
   st->num_pods += sign;
+  if (pod->flags & KG_POD_RESERVE) return; /* reserve pods never reach podAssignCache (pod informer only) */
   int64_t est[2];
   or_estimate_pod(cfg, pod, est);
   for (int r = 0; r < 2; r++) {

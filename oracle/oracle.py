@@ -86,6 +86,10 @@ def lib():
         L.or_ds_memory_ratio_to_bytes.restype = i64
         L.or_ds_instance_flat.argtypes = [vp, vp, vp]
         L.or_ds_instance_flat.restype = i
+        L.or_schedule_resv.argtypes = [vp, i64, vp, vp, vp, vp, i64, vp, i64, vp, vp, vp]
+        L.or_schedule_resv.restype = i
+        L.or_rsv_case_flat.argtypes = [vp, i64, vp, i64, vp, vp, i, vp, vp]
+        L.or_rsv_case_flat.restype = None
         _lib = L
     return _lib
 
@@ -141,6 +145,31 @@ def schedule_full(cfg, nodes, metrics, st, pods, now_ns: int, n_threads: int = 1
 
 
 p = abi.ptr
+
+
+def schedule_resv(cfg, nodes, metrics, st, rsv, pods, now_ns: int):
+    """Sequential FIFO scheduling with NodeResourcesFit + LoadAware + Reservation (st, rsv mutated).
+    Returns (node, score, slot) — slot = the reservation each pod was assumed into (-1 = none)."""
+    pods = np.ascontiguousarray(pods, dtype=abi.POD_DTYPE)
+    n = max(len(pods), 1)
+    out_node, out_score, out_slot = (np.empty(n, dtype=np.int32), np.empty(n, dtype=np.int64),
+                                     np.empty(n, dtype=np.int32))
+    rc = lib().or_schedule_resv(p(cfg), len(nodes), p(nodes), p(metrics), p(st), p(rsv), len(pods), p(pods), now_ns,
+                                p(out_node), p(out_score), p(out_slot))
+    if rc != 0:
+        raise RuntimeError(f"oracle or_schedule_resv failed: {rc}")
+    return out_node[:len(pods)], out_score[:len(pods)], out_slot[:len(pods)]
+
+
+def rsv_case(pod, allowed_pods, alloc, num_pods, pod_requested, r_allocated, has_state, rsv):
+    """One node's Reservation Filter / nomination / Score with an explicit nodeReservationState, every slot in
+    `matched` (how reservation/*_test.go build their states).  Returns (filter_pass, nominated_slot, score)."""
+    out = np.zeros(3, dtype=np.int64)
+    a = lambda v: np.ascontiguousarray(v, dtype=np.int64)
+    lib().or_rsv_case_flat(p(np.ascontiguousarray(np.asarray(pod, dtype=abi.POD_DTYPE).reshape(1))), allowed_pods,
+                           p(a(alloc)), num_pods, p(a(pod_requested)), p(a(r_allocated)), int(has_state),
+                           p(np.ascontiguousarray(np.asarray(rsv, dtype=abi.NODE_RSV_DTYPE).reshape(1))), p(out))
+    return int(out[0]), int(out[1]), int(out[2])
 
 
 def states(n: int) -> np.ndarray:

@@ -1,0 +1,266 @@
+/*
+ * reservation.c — CPU restatement of the Reservation plugin (TEST INFRASTRUCTURE ONLY; see reservation.h).
+ * Resources are cpu (milli) and memory (bytes); reservations always reserve both (ResourceNames = {cpu, memory}).
+ */
+#include "reservation.h"
+
+#include <stdlib.h>
+#include <string.h>
+
+static int slot_usable(const kg_node_reservations* r, int s) {
+  /* forEachAvailableReservationOnNode + IsAvailable/ParseError + AllocateOnce skip (transformer.go:101-110) */
+  if (!r->available[s]) return 0;
+  if (r->allocate_once[s] && r->assigned[s] > 0) return 0;
+  return 1;
+}
+
+static int pod_matches(const kg_pod* pod, const kg_node_reservations* r, int s) {
+  /* ReservationInfo.Match → MatchReservationOwners (reservation_info.go:231-236) decoded to an owner group;
+   * !IsUnschedulable (transformer.go:112); the affinity selector matches every reservation of the owner group */
+  return pod->reservation_owner != 0 && r->owner[s] == pod->reservation_owner && !r->unschedulable[s];
+}
+
+static int64_t sub_nn(int64_t a, int64_t b) { return a - b > 0 ? a - b : 0; } /* SubtractWithNonNegativeResult */
+
+void or_rsv_restore(const kg_node_reservations* r, const or_node_state* st, const kg_pod* pod, or_rsv_node* out) {
+  memset(out, 0, sizeof(*out));
+  out->requested[0] = st->requested[KG_RES_CPU];
+  out->requested[1] = st->requested[KG_RES_MEMORY];
+  out->nonzero[0] = st->nonzero[0];
+  out->nonzero[1] = st->nonzero[1];
+  out->num_pods = st->num_pods;
+  if (!r) return;
+  int32_t unmatched[KG_MAX_RSV_SLOTS];
+  int n_unmatched = 0;
+  for (int s = 0; s < (int)r->n; s++) {
+    if (!slot_usable(r, s)) continue;
+    if (pod_matches(pod, r, s)) out->matched[out->n_matched++] = s;
+    else if (r->assigned[s] > 0) unmatched[n_unmatched++] = s;
+  }
+  if (out->n_matched == 0 && n_unmatched == 0) return;
+  /* reservationAffinity != nil && no matched: the node is not processed (transformer.go:134-136) */
+  if ((pod->reservation_flags & KG_POD_RSV_AFFINITY) && out->n_matched == 0) return;
+  out->has_state = 1;
+  /* restoreUnmatchedReservations (transformer.go:265-291): the reserve pod (requests = allocatable, both keys
+   * present so NonZero = requests) leaves; its remainder returns when non-zero */
+  for (int k = 0; k < n_unmatched; k++) {
+    const int s = unmatched[k];
+    out->requested[0] -= r->allocatable_cpu[s];
+    out->requested[1] -= r->allocatable_mem[s];
+    out->nonzero[0] -= r->allocatable_cpu[s];
+    out->nonzero[1] -= r->allocatable_mem[s];
+    const int64_t rc = sub_nn(r->allocatable_cpu[s], r->allocated_cpu[s]);
+    const int64_t rm = sub_nn(r->allocatable_mem[s], r->allocated_mem[s]);
+    if (rc != 0 || rm != 0) {
+      out->requested[0] += rc;
+      out->requested[1] += rm;
+      out->nonzero[0] += rc; /* keys present (explicit zero) → GetNonzeroRequests keeps the value */
+      out->nonzero[1] += rm;
+    }
+  }
+  out->pod_requested[0] = out->requested[0];
+  out->pod_requested[1] = out->requested[1];
+  /* restoreMatchedReservation (transformer.go:240-263): NodeInfo.RemovePod(reserve pod) */
+  for (int k = 0; k < out->n_matched; k++) {
+    const int s = out->matched[k];
+    out->requested[0] -= r->allocatable_cpu[s];
+    out->requested[1] -= r->allocatable_mem[s];
+    out->nonzero[0] -= r->allocatable_cpu[s];
+    out->nonzero[1] -= r->allocatable_mem[s];
+    out->num_pods -= 1;
+    out->r_allocated[0] += r->allocated_cpu[s];
+    out->r_allocated[1] += r->allocated_mem[s];
+  }
+}
+
+int or_rsv_fits_node(const kg_pod* pod, int64_t allowed_pods, const int64_t alloc[2], const or_rsv_node* ns,
+                     const kg_node_reservations* r, int s) {
+  if (ns->num_pods - ns->n_matched + 1 > allowed_pods) return 0;
+  const int64_t pc = pod->requests[KG_RES_CPU], pm = pod->requests[KG_RES_MEMORY];
+  if (pc == 0 && pm == 0) return 1;
+  int64_t rc = 0, rm = 0;
+  if (s >= 0) {
+    rc = sub_nn(r->allocatable_cpu[s], r->allocated_cpu[s]);
+    rm = sub_nn(r->allocatable_mem[s], r->allocated_mem[s]);
+  }
+  if (pc > alloc[0] - (ns->pod_requested[0] - rc - ns->r_allocated[0])) return 0;
+  if (pm > alloc[1] - (ns->pod_requested[1] - rm - ns->r_allocated[1])) return 0;
+  return 1;
+}
+
+int or_rsv_filter_with(const kg_pod* pod, int64_t allowed_pods, const int64_t alloc[2], const or_rsv_node* ns,
+                       const kg_node_reservations* r, const int32_t* slots, int n_slots, int required) {
+  const int64_t pc = pod->requests[KG_RES_CPU], pm = pod->requests[KG_RES_MEMORY];
+  int satisfied = 0;
+  for (int k = 0; k < n_slots && !satisfied; k++) {
+    const int s = slots[k];
+    if (pc == 0 && pm == 0) continue; /* Intersection(ResourceNames, pod request names) empty */
+    const int fits = or_rsv_fits_node(pod, allowed_pods, alloc, ns, r, s);
+    if (r->policy[s] == KG_RSV_POLICY_RESTRICTED) {
+      const int64_t rc = sub_nn(r->allocatable_cpu[s], r->allocated_cpu[s]);
+      const int64_t rm = sub_nn(r->allocatable_mem[s], r->allocated_mem[s]);
+      if (pc <= rc && pm <= rm && fits) satisfied = 1;
+    } else if (fits) {
+      satisfied = 1;
+    }
+  }
+  return (!satisfied && required) ? 0 : 1;
+}
+
+int or_rsv_filter(const kg_pod* pod, int64_t allowed_pods, const int64_t alloc[2], const or_rsv_node* ns,
+                  const kg_node_reservations* r) {
+  const int required = (pod->reservation_flags & KG_POD_RSV_AFFINITY) != 0;
+  if (ns->n_matched == 0 || !ns->has_state) return required ? 0 : 1;
+  return or_rsv_filter_with(pod, allowed_pods, alloc, ns, r, ns->matched, ns->n_matched, required);
+}
+
+int64_t or_rsv_score_slot(const kg_pod* pod, const kg_node_reservations* r, int s) {
+  const int64_t req[2] = {pod->requests[KG_RES_CPU] + r->allocated_cpu[s],
+                          pod->requests[KG_RES_MEMORY] + r->allocated_mem[s]};
+  const int64_t cap[2] = {r->allocatable_cpu[s], r->allocatable_mem[s]};
+  int64_t w = 0, sc = 0;
+  for (int k = 0; k < 2; k++) {
+    if (cap[k] == 0) continue; /* RemoveZeros */
+    w++;
+    if (req[k] <= cap[k]) sc += 100 * req[k] / cap[k]; /* MaxNodeScore · MilliValue / MilliValue */
+  }
+  return w > 0 ? sc / w : 0;
+}
+
+int64_t or_rsv_node_order(const or_rsv_node* ns, const kg_node_reservations* r) {
+  int64_t best = INT64_MAX;
+  for (int k = 0; k < ns->n_matched; k++) {
+    const int64_t o = r->order[ns->matched[k]];
+    if (o != 0 && best > o) best = o;
+  }
+  return best;
+}
+
+int or_rsv_nominate(const kg_pod* pod, int64_t allowed_pods, const int64_t alloc[2], const or_rsv_node* ns,
+                    const kg_node_reservations* r) {
+  if (!ns->has_state || ns->n_matched == 0) return -1;
+  int32_t cand[KG_MAX_RSV_SLOTS];
+  int n = 0;
+  for (int k = 0; k < ns->n_matched; k++) {
+    const int s = ns->matched[k];
+    /* FilterReservation (plugin.go:492-519): AllocateOnce already excluded; filterWithReservations([s], true) */
+    const int32_t one = s;
+    if (or_rsv_filter_with(pod, allowed_pods, alloc, ns, r, &one, 1, 1)) cand[n++] = s;
+  }
+  if (n == 0) return -1;
+  int64_t best_order = INT64_MAX;
+  int pick = -1;
+  for (int k = 0; k < n; k++) {
+    const int64_t o = r->order[cand[k]];
+    if (o != 0 && best_order > o) { best_order = o; pick = cand[k]; }
+  }
+  if (pick >= 0) return pick;
+  int64_t best = -1;
+  for (int k = 0; k < n; k++) {
+    const int64_t sc = or_rsv_score_slot(pod, r, cand[k]);
+    if (sc > best) { best = sc; pick = cand[k]; } /* sort.Slice unstable → pinned: lowest slot on ties */
+  }
+  return pick;
+}
+
+void or_rsv_case_flat(const kg_pod* pod, int64_t allowed_pods, const int64_t alloc[2], int64_t num_pods,
+                      const int64_t pod_requested[2], const int64_t r_allocated[2], int has_state,
+                      const kg_node_reservations* r, int64_t* out) {
+  or_rsv_node ns;
+  memset(&ns, 0, sizeof(ns));
+  ns.has_state = has_state;
+  for (int s = 0; s < (int)r->n; s++) ns.matched[ns.n_matched++] = s; /* the tests place every slot in matched */
+  ns.num_pods = num_pods;
+  for (int k = 0; k < 2; k++) { ns.pod_requested[k] = pod_requested[k]; ns.r_allocated[k] = r_allocated[k]; }
+  out[0] = or_rsv_filter(pod, allowed_pods, alloc, &ns, r);
+  const int nom = or_rsv_nominate(pod, allowed_pods, alloc, &ns, r);
+  out[1] = nom;
+  out[2] = nom >= 0 ? or_rsv_score_slot(pod, r, nom) : 0;
+}
+
+int or_schedule_resv(const kg_config* cfg, int64_t n_nodes, const kg_node* nodes, const kg_node_metric* metrics,
+                     or_node_state* st, kg_node_reservations* rsv, int64_t n_pods, const kg_pod* pods, int64_t now,
+                     int32_t* out_node, int64_t* out_score, int32_t* out_slot) {
+  const size_t nn = (size_t)(n_nodes > 0 ? n_nodes : 1);
+  int8_t* feas = (int8_t*)malloc(nn);
+  int64_t* base = (int64_t*)malloc(nn * sizeof(int64_t));
+  int64_t* raw = (int64_t*)malloc(nn * sizeof(int64_t));
+  int64_t* order = (int64_t*)malloc(nn * sizeof(int64_t));
+  int32_t* nom = (int32_t*)malloc(nn * sizeof(int32_t));
+  if (!feas || !base || !raw || !order || !nom) {
+    free(feas); free(base); free(raw); free(order); free(nom);
+    return KG_E_NOMEM;
+  }
+  int rc = 0;
+  for (int64_t p = 0; p < n_pods && rc == 0; p++) {
+    const kg_pod* pod = &pods[p];
+    for (int64_t i = 0; i < n_nodes; i++) {
+      feas[i] = 0;
+      const kg_node* nd = &nodes[i];
+      if (!(nd->flags & KG_NODE_VALID)) continue;
+      or_rsv_node ns;
+      or_rsv_restore(cfg->reservation_filter || cfg->reservation_score ? &rsv[i] : NULL, &st[i], pod, &ns);
+      or_node_state rs = st[i];
+      rs.requested[KG_RES_CPU] = ns.requested[0];
+      rs.requested[KG_RES_MEMORY] = ns.requested[1];
+      rs.nonzero[0] = ns.nonzero[0];
+      rs.nonzero[1] = ns.nonzero[1];
+      rs.num_pods = ns.num_pods;
+      const int64_t alloc[2] = {nd->allocatable[KG_RES_CPU], nd->allocatable[KG_RES_MEMORY]};
+      if (cfg->fit_filter && or_fit_filter(nd, &rs, pod) != 0) continue;
+      if (cfg->la_filter) {
+        const int f = or_loadaware_filter(cfg, nd, &metrics[i], pod, now);
+        if (f < 0) { rc = f; break; }
+        if (f != 0) continue;
+      }
+      if (cfg->reservation_filter && !or_rsv_filter(pod, nd->allowed_pods, alloc, &ns, &rsv[i])) continue;
+      feas[i] = 1;
+      int64_t t = 0;
+      if (cfg->fit_score) t += cfg->weight_fit * or_fit_score(cfg, nd, &rs, pod);
+      if (cfg->la_score) {
+        const int64_t s = or_loadaware_score(cfg, nd, &metrics[i], &st[i], pod, now);
+        if (s < 0) { rc = (int)s; break; }
+        t += cfg->weight_loadaware * s;
+      }
+      base[i] = t;
+      nom[i] = or_rsv_nominate(pod, nd->allowed_pods, alloc, &ns, &rsv[i]);
+      raw[i] = nom[i] >= 0 ? or_rsv_score_slot(pod, &rsv[i], nom[i]) : 0;
+      order[i] = ns.has_state ? or_rsv_node_order(&ns, &rsv[i]) : INT64_MAX;
+    }
+    if (rc) break;
+    /* PreScore preferredNode (scoring.go:89-99): smallest order, first (lowest index) feasible node */
+    int64_t pref = -1, best_order = INT64_MAX;
+    for (int64_t i = 0; i < n_nodes; i++)
+      if (feas[i] && order[i] != 0 && best_order > order[i]) { best_order = order[i]; pref = i; }
+    int64_t mx = 0;
+    for (int64_t i = 0; i < n_nodes; i++) {
+      if (!feas[i]) continue;
+      const int64_t s = (i == pref) ? 1000 : raw[i]; /* mostPreferredScore */
+      raw[i] = s;
+      if (s > mx) mx = s;
+    }
+    int64_t win = -1, win_total = -1;
+    for (int64_t i = 0; i < n_nodes; i++) {
+      if (!feas[i]) continue;
+      int64_t t = base[i];
+      if (cfg->reservation_score && mx > 0) t += cfg->weight_reservation * (100 * raw[i] / mx);
+      if (t > win_total) { win_total = t; win = i; }
+    }
+    out_node[p] = (int32_t)win;
+    out_score[p] = win >= 0 ? win_total : 0;
+    if (out_slot) out_slot[p] = -1;
+    if (win >= 0) {
+      or_apply_pod(cfg, &st[win], pod, 1);
+      if ((cfg->reservation_filter || cfg->reservation_score) && nom[win] >= 0) {
+        /* Reserve → reservationCache.assumePod → AddAssignedPod (reservation_info.go:317-326) */
+        kg_node_reservations* r = &rsv[win];
+        r->allocated_cpu[nom[win]] += pod->requests[KG_RES_CPU];
+        r->allocated_mem[nom[win]] += pod->requests[KG_RES_MEMORY];
+        r->assigned[nom[win]] += 1;
+        if (out_slot) out_slot[p] = nom[win];
+      }
+    }
+  }
+  free(feas); free(base); free(raw); free(order); free(nom);
+  return rc;
+}

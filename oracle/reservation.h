@@ -1,0 +1,71 @@
+/*
+ * reservation.h — CPU restatement of the Reservation plugin on the hot path (SURVEY §8a A15–A18).
+ *
+ * TEST INFRASTRUCTURE ONLY (see oracle.h): tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg use it
+ * as the checker / CPU baseline; nothing under koordinator_amd/ links or calls it.
+ *
+ * Pinning: golden cases transcribed from reservation/scoring_test.go (TestScore :40, TestPreScore nomination
+ * :392-729) and plugin_test.go (Test_filterWithReservations :670) into tests/golden/reservation.json
+ * (script tests/golden/make_golden_resv.py).  The BeforePreFilter restore arithmetic (transformer.go:49-346)
+ * and the full-cycle composition (Filter → PreScore → Score → NormalizeScore → Reserve) are restated from the
+ * source; no reference test drives the whole cycle on a cluster, so those parts are "parity unpinned" beyond
+ * the per-function cases.
+ */
+#ifndef KOORD_ORACLE_RESERVATION_H_
+#define KOORD_ORACLE_RESERVATION_H_
+#include <stdint.h>
+#include "../include/koordgpu.h"
+#include "oracle.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* nodeReservationState (transformer.go:180-187) of one (pod, node) plus the restored NodeInfo fields. */
+typedef struct or_rsv_node {
+  int32_t has_state;                 /* the node is in state.nodeReservationStates                         */
+  int32_t n_matched;
+  int32_t matched[KG_MAX_RSV_SLOTS]; /* slot indices, reservation order                                     */
+  int64_t pod_requested[2];          /* Requested after the unmatched trim (cpu milli, memory)              */
+  int64_t r_allocated[2];            /* Σ matched Allocated                                                 */
+  int64_t requested[2], nonzero[2];  /* restored NodeInfo.Requested / NonZeroRequested                      */
+  int64_t num_pods;                  /* restored len(NodeInfo.Pods)                                         */
+} or_rsv_node;
+
+/* BeforePreFilter for one node (transformer.go:100-189). */
+void or_rsv_restore(const kg_node_reservations* r, const or_node_state* st, const kg_pod* pod, or_rsv_node* out);
+/* fitsNode (plugin.go:433-482) with rInfo = slot s (s < 0: nil), preemptible = 0. */
+int or_rsv_fits_node(const kg_pod* pod, int64_t allowed_pods, const int64_t alloc[2], const or_rsv_node* ns,
+                     const kg_node_reservations* r, int s);
+/* filterWithReservations over the given slots (plugin.go:384-428): 1 = Success, 0 = Unschedulable. */
+int or_rsv_filter_with(const kg_pod* pod, int64_t allowed_pods, const int64_t alloc[2], const or_rsv_node* ns,
+                       const kg_node_reservations* r, const int32_t* slots, int n_slots, int required);
+/* Filter for a non-reserve pod (plugin.go:357-378, preemption maps empty). */
+int or_rsv_filter(const kg_pod* pod, int64_t allowed_pods, const int64_t alloc[2], const or_rsv_node* ns,
+                  const kg_node_reservations* r);
+/* scoreReservation (scoring.go:183-203) of slot s. */
+int64_t or_rsv_score_slot(const kg_pod* pod, const kg_node_reservations* r, int s);
+/* NominateReservation (nominator.go:76-134) with FilterReservation (plugin.go:492-519) as the only reservation
+ * filter and ScoreReservation as the only reservation scorer; ties on score → lowest slot.  Returns slot or -1. */
+int or_rsv_nominate(const kg_pod* pod, int64_t allowed_pods, const int64_t alloc[2], const or_rsv_node* ns,
+                    const kg_node_reservations* r);
+/* findMostPreferredReservationByOrder over the matched slots (scoring.go:162-181): INT64_MAX if none. */
+int64_t or_rsv_node_order(const or_rsv_node* ns, const kg_node_reservations* r);
+
+/* Sequential FIFO scheduling with NodeResourcesFit + LoadAwareScheduling + Reservation (one pod at a time,
+ * ties → lowest index).  `st` and `rsv` are updated by Reserve; out_slot (nullable) = the slot each pod was
+ * assumed into (-1 = none). */
+int or_schedule_resv(const kg_config* cfg, int64_t n_nodes, const kg_node* nodes, const kg_node_metric* metrics,
+                     or_node_state* st, kg_node_reservations* rsv, int64_t n_pods, const kg_pod* pods, int64_t now,
+                     int32_t* out_node, int64_t* out_score, int32_t* out_slot);
+
+/* Golden-case entry (flat): explicit nodeReservationState (pod_requested, r_allocated, restored pod count) as the
+ * reference tests build it.  out[0] = filter pass, out[1] = nominated slot, out[2] = Score (before normalize). */
+void or_rsv_case_flat(const kg_pod* pod, int64_t allowed_pods, const int64_t alloc[2], int64_t num_pods,
+                      const int64_t pod_requested[2], const int64_t r_allocated[2], int has_state,
+                      const kg_node_reservations* r, int64_t* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,50 @@
+"""Reservation scheduling loop of the oracle (or_schedule_resv) — CPU checks of its composition: with the plugin
+off it is the Fit + LoadAware loop; with it on, placements land in reservations and Reserve's bookkeeping adds up."""
+import numpy as np
+
+from koordinator_amd import abi, framework as F, synth
+from oracle import oracle
+
+PROFILE = F.Profile(filter=(F.NODE_RESOURCES_FIT, F.LOAD_AWARE, F.RESERVATION),
+                    score={F.NODE_RESOURCES_FIT: 1, F.LOAD_AWARE: 1, F.RESERVATION: 5000})
+BASE = F.Profile(filter=(F.NODE_RESOURCES_FIT, F.LOAD_AWARE), score={F.NODE_RESOURCES_FIT: 1, F.LOAD_AWARE: 1})
+
+
+def run(cfg, cluster, rsv, pods):
+    st = oracle.states(cluster.n)
+    oracle.add_pods(cfg, st, cluster.existing_pods, cluster.existing_node)
+    r = rsv.copy()
+    node, score, slot = oracle.schedule_resv(cfg, cluster.nodes, cluster.metrics, st, r, pods, cluster.now_ns)
+    return node, score, slot, st, r
+
+
+def test_plugin_off_equals_fit_loadaware_loop():
+    cluster, rsv = synth.make_rsv_cluster(300, seed=5)
+    pods = synth.make_rsv_pods(400, seed=6)
+    cfg = F.build_config(profile=BASE)
+    node, score, slot, _, _ = run(cfg, cluster, rsv, pods)
+    st = oracle.states(cluster.n)
+    oracle.add_pods(cfg, st, cluster.existing_pods, cluster.existing_node)
+    wn, ws, _, _ = oracle.schedule_full(cfg, cluster.nodes, cluster.metrics, st, pods, cluster.now_ns, 1)
+    assert np.array_equal(node, wn) and np.array_equal(score, ws)
+    assert (slot == -1).all()
+
+
+def test_reserve_bookkeeping_and_affinity():
+    cluster, rsv = synth.make_rsv_cluster(300, seed=7)
+    pods = synth.make_rsv_pods(600, seed=8)
+    cfg = F.build_config(profile=PROFILE)
+    node, score, slot, st, r = run(cfg, cluster, rsv, pods)
+    assert (slot >= 0).sum() > 10  # owned pods land in their reservations (weight 5000)
+    for j in np.nonzero(slot >= 0)[0]:
+        i, s = node[j], slot[j]
+        assert pods[j]["reservation_owner"] == rsv[i]["owner"][s]
+    got = r["allocated_cpu"] - rsv["allocated_cpu"]
+    want = np.zeros_like(got)
+    np.add.at(want, (node[slot >= 0], slot[slot >= 0]), pods["requests"][slot >= 0, abi.RES_CPU])
+    assert np.array_equal(got, want)
+    assert np.array_equal(r["assigned"] - rsv["assigned"],
+                          np.bincount(node[slot >= 0] * abi.MAX_RSV_SLOTS + slot[slot >= 0],
+                                      minlength=cluster.n * abi.MAX_RSV_SLOTS).reshape(cluster.n, -1))
+    aff = (pods["reservation_flags"] & abi.POD_RSV_AFFINITY) != 0
+    assert ((slot >= 0) | (node < 0))[aff].all()  # required affinity: placed only through a reservation
