@@ -35,7 +35,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--workload", choices=("c3", "c4", "c5"), default="c3",
+    ap.add_argument("--workload", choices=("c3", "c4", "c5", "c5r"), default="c3",
                     help="c3: Fit+LoadAware at 100k nodes (the BASELINE metric); c4: + NodeNUMAResource cpuset/NUMA "
                          "on 2-socket 256-cpu nodes")
     ap.add_argument("--nodes", type=int, default=None, help="default 100k (c3) / 10k (c4)")
@@ -94,7 +94,7 @@ class Dist:
             self.dist.destroy_process_group()
 
 
-def cpu_baseline(cfg, cluster, pods, budget_s, threads, numa=None, devices=None):
+def cpu_baseline(cfg, cluster, pods, budget_s, threads, numa=None, devices=None, rsv=None):
     """Oracle (C restatement of the same Go algorithm, oracle/oracle.c [+ numa.c / deviceshare.c]) on this host,
     bounded sample."""
     from oracle import oracle
@@ -102,9 +102,12 @@ def cpu_baseline(cfg, cluster, pods, budget_s, threads, numa=None, devices=None)
     oracle.add_pods(cfg, st, cluster.existing_pods, cluster.existing_node)
     buf = oracle.numa_states(numa) if numa is not None else None
     dev = devices.copy() if devices is not None else None
+    rs = rsv.copy() if rsv is not None else None
 
     def run(p):
-        if dev is not None:
+        if rs is not None:  # or_schedule_resv is single-threaded
+            oracle.schedule_resv(cfg, cluster.nodes, cluster.metrics, st, rs, p, cluster.now_ns)
+        elif dev is not None:
             oracle.schedule_full(cfg, cluster.nodes, cluster.metrics, st, p, cluster.now_ns, threads, devices=dev)
         elif buf is None:
             oracle.schedule(cfg, cluster.nodes, cluster.metrics, st, p, cluster.now_ns, threads)
@@ -147,8 +150,9 @@ def main():
         nccl_id = d.bcast_bytes(nccl_unique_id() if d.rank == 0 else None)
     c4 = args.workload == "c4"
     c5 = args.workload == "c5"
-    args.nodes = args.nodes or (10_000 if c4 else (50_000 if c5 else 100_000))
-    args.pods_per_step = args.pods_per_step or (10_000 if (c4 or c5) else 100_000)
+    c5r = args.workload == "c5r"
+    args.nodes = args.nodes or (10_000 if c4 else (50_000 if (c5 or c5r) else 100_000))
+    args.pods_per_step = args.pods_per_step or (10_000 if (c4 or c5 or c5r) else 100_000)
     # geometry sweeps: profiles/r01/c4_sweep.txt, c5_sweep.txt
     args.pods_per_wave = args.pods_per_wave or (1 if c4 else (4 if c5 else 8))
     args.batch = args.batch or (16 if c4 else 32)
@@ -160,9 +164,12 @@ def main():
     elif c5:  # shipped weights: DeviceShare 1 (config/manager/scheduler-config.yaml:82-91)
         profile = F.Profile(filter=(F.NODE_RESOURCES_FIT, F.LOAD_AWARE, F.DEVICE_SHARE),
                             score={F.NODE_RESOURCES_FIT: 1, F.LOAD_AWARE: 1, F.DEVICE_SHARE: 1})
+    elif c5r:  # shipped weights: Reservation 5000 (config/manager/scheduler-config.yaml:90-91)
+        profile = F.Profile(filter=(F.NODE_RESOURCES_FIT, F.LOAD_AWARE, F.RESERVATION),
+                            score={F.NODE_RESOURCES_FIT: 1, F.LOAD_AWARE: 1, F.RESERVATION: 5000})
     cfg = framework.build_config(batch_pods=args.batch, pods_per_wave=args.pods_per_wave, device_id=d.local_rank,
                                  profile=profile)
-    numa = devices = None
+    numa = devices = rsv = None
     if c4:
         seed = synth.BASE_SEED + 4
         cluster, numa = synth.make_numa_cluster(args.nodes, seed=seed)
@@ -171,6 +178,10 @@ def main():
         seed = synth.BASE_SEED + 6
         cluster, devices = synth.make_gpu_cluster(args.nodes, seed=seed)
         make_pods = synth.make_gpu_pods
+    elif c5r:
+        seed = synth.BASE_SEED + 8
+        cluster, rsv = synth.make_rsv_cluster(args.nodes, seed=seed)
+        make_pods = synth.make_rsv_pods
     else:
         seed = synth.BASE_SEED + 3
         cluster = synth.make_cluster(args.nodes, seed=seed)
@@ -184,6 +195,8 @@ def main():
             synth.load_numa_into(e, cluster, numa)
         elif c5:
             synth.load_gpu_into(e, cluster, devices)
+        elif c5r:
+            synth.load_rsv_into(e, cluster, rsv)
         else:
             synth.load_into(e, cluster)
         return e
@@ -212,12 +225,14 @@ def main():
     placed = int((node_idx >= 0).sum())
 
     # per-kernel live timing (HIP events on the engine stream) for the roofline
-    names = ("eval_round", "merge_round", "resolve_round") + (("ds_max_round", "ds_norm_reduce") if c5 else ())
+    names = (("rsv_eval", "rsv_select") if c5r else
+             ("eval_round", "merge_round", "resolve_round") + (("ds_max_round", "ds_norm_reduce") if c5 else ()))
     kernels = {name: e.bench_kernel(which, args.kernel_iters) for which, name in enumerate(names)}
     # roofline kernel: the wide pass, the only kernel whose work scales with node evaluations (SURVEY §8d's
     # 76 B per evaluation); merge and the single-wave FIFO resolver are latency-bound per round
     # (C5: ds_max_round is the DeviceShare profile's full evaluation; eval_round_ds only normalizes its output)
-    dom = "ds_max_round" if c5 else "eval_round"
+    # (C5 Reservation: rsv_eval is the per-pod wide pass; rsv_select re-reads 8 B per node, rsv_apply is one lane)
+    dom = "ds_max_round" if c5 else ("rsv_eval" if c5r else "eval_round")
     dom_ms, dom_bytes = kernels[dom]
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
 
@@ -232,7 +247,12 @@ def main():
     check = None
     if args.check and d.rank == 0:
         from oracle import oracle
-        if c5:
+        if c5r:
+            st = oracle.states(cluster.n)
+            oracle.add_pods(cfg, st, cluster.existing_pods, cluster.existing_node)
+            on, _, _ = oracle.schedule_resv(cfg, cluster.nodes, cluster.metrics, st, rsv.copy(), pods[: args.check],
+                                            cluster.now_ns)
+        elif c5:
             st = oracle.states(cluster.n)
             oracle.add_pods(cfg, st, cluster.existing_pods, cluster.existing_node)
             on, _, _, _ = oracle.schedule_full(cfg, cluster.nodes, cluster.metrics, st, pods[: args.check],
@@ -249,12 +269,13 @@ def main():
     cpu = None
     if d.rank == 0 and d.world == 1 and not args.no_cpu_baseline:
         print("[bench] cpu baseline sample", file=sys.stderr, flush=True)
-        m, dt = cpu_baseline(cfg, cluster, pods, args.cpu_seconds, args.cpu_threads, numa, devices)
-        cpu = {"value": m / dt, "unit": "pods/s", "cores": args.cpu_threads, "kind": "port",
+        m, dt = cpu_baseline(cfg, cluster, pods, args.cpu_seconds, args.cpu_threads, numa, devices, rsv)
+        threads = 1 if c5r else args.cpu_threads
+        cpu = {"value": m / dt, "unit": "pods/s", "cores": threads, "kind": "port",
                "sample": f"first {m} pods of the same queue after a 64-pod probe, {cluster.n} nodes, "
-                         f"oracle/oracle.c {'or_schedule_numa' if c4 else ('or_schedule_full' if c5 else 'or_schedule')}, "
-                         f"{args.cpu_threads} threads "
-                         f"(Parallelizer chunking), "
+                         f"oracle/{'reservation.c or_schedule_resv' if c5r else 'oracle.c ' + ('or_schedule_numa' if c4 else ('or_schedule_full' if c5 else 'or_schedule'))}, "
+                         f"{threads} thread(s) "
+                         f"{'(single-threaded loop)' if c5r else '(Parallelizer chunking)'}, "
                          f"host nproc={os.cpu_count()}",
                "node_evals_per_sec": m * cluster.n / dt}
 
@@ -264,7 +285,8 @@ def main():
         pods_s = total / elapsed
         out = {
             "metric": ("pods scheduled/sec, NodeNUMAResource cpuset/NUMA profile (node-evals/sec alongside)" if c4
-                       else ("pods scheduled/sec, DeviceShare GPU-share profile (node-evals/sec alongside)" if c5
+                       else ("pods scheduled/sec, Reservation profile (node-evals/sec alongside)" if c5r else
+                             "pods scheduled/sec, DeviceShare GPU-share profile (node-evals/sec alongside)" if c5
                              else "pods scheduled/sec at 100k nodes (node-evals/sec alongside)")),
             "value": pods_s,
             "unit": "pods/s",
@@ -279,11 +301,14 @@ def main():
             "data": "synthetic (SURVEY §8d generator, seed %d)" % seed,
             "config": {"workload": ("C4 cluster: %d 2-socket 256-cpu nodes, %d-pod FIFO queue (70%% cpuset LSR/LSE), "
                                     "NodeResourcesFit+LoadAwareScheduling+NodeNUMAResource, %d pods per step" if c4 else
-                                    ("C5 (DeviceShare part): %d nodes x 8 GPUs, %d-pod FIFO queue (30%% GPU-share), "
+                                    ("C5 (Reservation part): %d nodes (30%% with 1-4 reservations), %d-pod FIFO queue "
+                                     "(20%% reservation-owned), NodeResourcesFit+LoadAwareScheduling+Reservation (w 5000), "
+                                     "one pod per device pass, %d pods per step" if c5r else
+                                     "C5 (DeviceShare part): %d nodes x 8 GPUs, %d-pod FIFO queue (30%% GPU-share), "
                                      "NodeResourcesFit+LoadAwareScheduling+DeviceShare, %d pods per step" if c5 else
                                      "C3 cluster: %d nodes, %d-pod FIFO queue, NodeResourcesFit+LoadAwareScheduling, "
                                      "%d pods per step")) % (cluster.n, total, args.pods_per_step),
-                       "nodes": cluster.n, "pods": total, "batch_pods": args.batch,
+                       "nodes": cluster.n, "pods": total, "batch_pods": 1 if c5r else args.batch,
                        "parallelism": "node-sharded x%d (replicated table, RCCL all-gather)" % d.world},
             "node_evals_per_sec": pods_s * cluster.n,
             "placed": placed,

@@ -20,6 +20,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -1622,7 +1623,8 @@ struct kg_engine {
   DevBuf<RsvPod> rpods;
   DevBuf<int32_t> out_rslot;    // [staged + kMaxB]
   DevBuf<uint64_t> rsv_val;     // [capacity] packed per-node pass-1 values
-  DevBuf<unsigned long long> rsv_ws;  // [4]
+  DevBuf<unsigned long long> rsv_ws;  // [4]: [3] = pod cursor
+  DevBuf<uint64_t> rsv_part;    // [3][blocks] per-block partials (preferred-node key, max raw, max key)
 };
 
 namespace {
@@ -2260,18 +2262,32 @@ int run_rsv(kg_engine* e, int64_t first, int64_t count, kg_stats* stats, double 
   if (int rc = sync_static(e)) return rc;
   const int64_t n = e->n_nodes, end = first + count;
   if (count > 0 && n > 0) {
-    const unsigned blocks = (unsigned)((n + 255) / 256);
+    const unsigned blocks = (unsigned)((n + kRsvThreads - 1) / kRsvThreads);
     const unsigned long long init[4] = {0, 0, 0, (unsigned long long)first};
     HIP_TRY(hipMemcpyAsync(e->rsv_ws.p, init, 32, hipMemcpyHostToDevice, e->stream));
+    // KG_RSV_NO_GRAPH=1: plain stream launches (profilers whose kernel tracing does not follow graph launches)
+    static const bool no_graph = std::getenv("KG_RSV_NO_GRAPH") && std::getenv("KG_RSV_NO_GRAPH")[0] == '1';
+    if (no_graph) {
+      for (int64_t c = 0; c < count; ++c) {
+        rsv_eval<<<blocks, kRsvThreads, 0, e->stream>>>(e->T, e->rsv_d.p, e->rsv_nd.p, e->pods.p, e->rpods.p, end, n,
+                                                         e->P, e->RP, e->rsv_val.p, e->rsv_part.p, e->rsv_ws.p);
+        rsv_select<<<blocks, kRsvThreads, 0, e->stream>>>(e->rsv_val.p, end, n, e->RP, e->rsv_part.p, e->rsv_ws.p);
+        rsv_apply<<<1, kWave, 0, e->stream>>>(e->T, e->rsv_d.p, e->rsv_val.p, e->pods.p, end, (int)blocks,
+                                              e->rsv_part.p, e->out_keys.p, e->out_rslot.p, e->rsv_ws.p);
+      }
+      HIP_TRY(hipGetLastError());
+      HIP_TRY(hipStreamSynchronize(e->stream));
+    }
     hipGraph_t graph = nullptr;
     hipGraphExec_t exec = nullptr;
+    if (!no_graph) {
     HIP_TRY(hipStreamBeginCapture(e->stream, hipStreamCaptureModeThreadLocal));
     for (int g = 0; g < kRsvGroup; ++g) {
-      rsv_eval<<<blocks, 256, 0, e->stream>>>(e->T, e->rsv_d.p, e->rsv_nd.p, e->pods.p, e->rpods.p, end, n, e->P,
-                                               e->RP, e->rsv_val.p, e->rsv_ws.p);
-      rsv_select<<<blocks, 256, 0, e->stream>>>(e->rsv_val.p, end, n, e->RP, e->rsv_ws.p);
-      rsv_apply<<<1, 1, 0, e->stream>>>(e->T, e->rsv_d.p, e->rsv_val.p, e->pods.p, end, e->out_keys.p,
-                                        e->out_rslot.p, e->rsv_ws.p);
+      rsv_eval<<<blocks, kRsvThreads, 0, e->stream>>>(e->T, e->rsv_d.p, e->rsv_nd.p, e->pods.p, e->rpods.p, end, n,
+                                                       e->P, e->RP, e->rsv_val.p, e->rsv_part.p, e->rsv_ws.p);
+      rsv_select<<<blocks, kRsvThreads, 0, e->stream>>>(e->rsv_val.p, end, n, e->RP, e->rsv_part.p, e->rsv_ws.p);
+      rsv_apply<<<1, kWave, 0, e->stream>>>(e->T, e->rsv_d.p, e->rsv_val.p, e->pods.p, end, (int)blocks,
+                                            e->rsv_part.p, e->out_keys.p, e->out_rslot.p, e->rsv_ws.p);
     }
     const hipError_t ce = hipStreamEndCapture(e->stream, &graph);
     if (ce != hipSuccess) return fail(KG_E_DEVICE, "hipStreamEndCapture: %s", hipGetErrorString(ce));
@@ -2281,6 +2297,7 @@ int run_rsv(kg_engine* e, int64_t first, int64_t count, kg_stats* stats, double 
     if (exec) (void)hipGraphExecDestroy(exec);
     (void)hipGraphDestroy(graph);
     if (ge != hipSuccess) return fail(KG_E_DEVICE, "reservation pass graph: %s", hipGetErrorString(ge));
+    }
   } else if (count > 0) {
     HIP_TRY(hipMemsetAsync(e->out_keys.p + first, 0, count * 8, e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
@@ -2477,6 +2494,7 @@ int kg_engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank, int
     if (int rc = e->rsv_nd.ensure(cap)) return bail(rc);
     if (int rc = e->rsv_val.ensure(cap)) return bail(rc);
     if (int rc = e->rsv_ws.ensure(4)) return bail(rc);
+    if (int rc = e->rsv_part.ensure(3 * ((cap + kRsvThreads - 1) / kRsvThreads) + 3)) return bail(rc);
     if (hipMemset(e->rsv_nd.p, 0, cap * 4) != hipSuccess || hipMemset(e->rsv_ws.p, 0, 32) != hipSuccess)
       return bail(fail(KG_E_DEVICE, "hipMemset"));
   }
@@ -2596,6 +2614,7 @@ void kg_engine_destroy(kg_engine* e) {
   e->out_rslot.release();
   e->rsv_val.release();
   e->rsv_ws.release();
+  e->rsv_part.release();
   e->scratch64.release();
   e->scratch32.release();
   if (e->stream) (void)hipStreamDestroy(e->stream);
@@ -3077,7 +3096,57 @@ int kg_quotas_read(kg_engine* e, kg_quota* out, int64_t n) {
   return 0;
 }
 
+// Reservation profile: which 0 = rsv_eval, 1 = rsv_select, replayed on the first staged pod (neither kernel
+// changes node state; the cursor words are reset afterwards).  Algorithmic bytes of rsv_eval per launch: SURVEY
+// §8d's 76 B of Fit + LoadAware columns per node, the 4-B slot count and the 8-B packed value written, plus the
+// 192-B slot record of every node that has reservations; rsv_select reads the 8-B packed value per node.
+static int bench_rsv(kg_engine* e, int which, int iters, double* avg_ms, double* algo_bytes) {
+  if (iters <= 0 || which < 0 || which > 1) return fail(KG_E_INVALID, "bad argument");
+  if (e->n_staged <= 0) return fail(KG_E_INVALID, "stage a pod queue first");
+  if (int rc = sync_static(e)) return rc;
+  const int64_t n = e->n_nodes;
+  if (n <= 0) return fail(KG_E_INVALID, "no nodes");
+  std::vector<int32_t> hn(n);
+  HIP_TRY(hipMemcpy(hn.data(), e->rsv_nd.p, n * 4, hipMemcpyDeviceToHost));
+  int64_t with_slots = 0;
+  for (int64_t i = 0; i < n; ++i) with_slots += hn[i] > 0;
+  const unsigned blocks = (unsigned)((n + kRsvThreads - 1) / kRsvThreads);
+  const unsigned long long zero[4] = {0, 0, 0, 0};
+  HIP_TRY(hipMemcpyAsync(e->rsv_ws.p, zero, 32, hipMemcpyHostToDevice, e->stream));
+  auto launch = [&]() {
+    if (which == 0)
+      rsv_eval<<<blocks, kRsvThreads, 0, e->stream>>>(e->T, e->rsv_d.p, e->rsv_nd.p, e->pods.p, e->rpods.p,
+                                                       e->n_staged, n, e->P, e->RP, e->rsv_val.p, e->rsv_part.p,
+                                                       e->rsv_ws.p);
+    else
+      rsv_select<<<blocks, kRsvThreads, 0, e->stream>>>(e->rsv_val.p, e->n_staged, n, e->RP, e->rsv_part.p,
+                                                         e->rsv_ws.p);
+  };
+  if (which == 1)  // rsv_select needs the packed values and partials of a real pass
+    rsv_eval<<<blocks, kRsvThreads, 0, e->stream>>>(e->T, e->rsv_d.p, e->rsv_nd.p, e->pods.p, e->rpods.p,
+                                                     e->n_staged, n, e->P, e->RP, e->rsv_val.p, e->rsv_part.p,
+                                                     e->rsv_ws.p);
+  launch();  // warm
+  hipEvent_t a, b;
+  HIP_TRY(hipEventCreate(&a));
+  HIP_TRY(hipEventCreate(&b));
+  HIP_TRY(hipEventRecord(a, e->stream));
+  for (int k = 0; k < iters; ++k) launch();
+  HIP_TRY(hipEventRecord(b, e->stream));
+  HIP_TRY(hipEventSynchronize(b));
+  float ms = 0;
+  HIP_TRY(hipEventElapsedTime(&ms, a, b));
+  (void)hipEventDestroy(a);
+  (void)hipEventDestroy(b);
+  HIP_TRY(hipMemcpyAsync(e->rsv_ws.p, zero, 32, hipMemcpyHostToDevice, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  if (avg_ms) *avg_ms = ms / iters;
+  if (algo_bytes) *algo_bytes = which == 0 ? (double)n * (76 + 4 + 8) + (double)with_slots * sizeof(RsvNode) : (double)n * 8;
+  return 0;
+}
+
 int kg_bench_kernel(kg_engine* e, int which, int iters, double* avg_ms, double* algo_bytes) {
+  if (e && e->rsv_on) return bench_rsv(e, which, iters, avg_ms, algo_bytes);
   if (!e || iters <= 0 || which < 0 || which > (e && e->ds_on ? 4 : 2)) return fail(KG_E_INVALID, "bad argument");
   if (e->n_staged <= 0) return fail(KG_E_INVALID, "stage a pod queue first");
   RoundGeom g;

@@ -36,8 +36,7 @@ struct RsvParams {
   int32_t filter, score, weight, pad;
 };
 
-// ws words: [0] ~min(order << 32 | node) over feasible nodes with an order label (0 = none), [1] max raw Score,
-// [2] max selection key, [3] pod cursor
+// ws words: [3] = pod cursor (the others are unused)
 struct RsvOut {
   bool feas;
   int64_t base;   // Fit + LoadAware weighted total
@@ -77,7 +76,9 @@ __device__ __forceinline__ RsvOut rsv_eval_node(const DevTable& T, const RsvNode
   if (ns > 0) {
     rn = RN[i];
     uint32_t um = 0;
-    for (int s = 0; s < ns; ++s) {
+    #pragma unroll
+    for (int s = 0; s < kRsvSlots; ++s) {
+      if (s >= ns) break;
       const uint32_t m = rn.meta[s];
       if (!(m & RS_AVAIL) || ((m & RS_ONCE) && rn.assigned[s] > 0)) continue;  // transformer.go:101-110
       if (rp.owner != 0 && rn.owner[s] == rp.owner && !(m & RS_UNSCHED)) mm |= 1u << s;
@@ -85,7 +86,8 @@ __device__ __forceinline__ RsvOut rsv_eval_node(const DevTable& T, const RsvNode
     }
     has_state = (mm | um) != 0 && !((rp.flags & RP_AFFINITY) && mm == 0);  // transformer.go:127-136
     if (has_state) {
-      for (int s = 0; s < ns; ++s)
+#pragma unroll
+      for (int s = 0; s < kRsvSlots; ++s)
         if (um >> s & 1) {  // restoreUnmatchedReservations (transformer.go:265-291)
           r.req_cpu -= rn.alloc_cpu[s];
           r.req_mem -= rn.alloc_mem[s];
@@ -101,7 +103,8 @@ __device__ __forceinline__ RsvOut rsv_eval_node(const DevTable& T, const RsvNode
         }
       pr_c = r.req_cpu;
       pr_m = r.req_mem;
-      for (int s = 0; s < ns; ++s)
+#pragma unroll
+      for (int s = 0; s < kRsvSlots; ++s)
         if (mm >> s & 1) {  // restoreMatchedReservation: NodeInfo.RemovePod(reserve pod) (transformer.go:240-263)
           r.req_cpu -= rn.alloc_cpu[s];
           r.req_mem -= rn.alloc_mem[s];
@@ -121,7 +124,8 @@ __device__ __forceinline__ RsvOut rsv_eval_node(const DevTable& T, const RsvNode
   uint32_t sat = 0;
   if (has_state && !zero) {
     const bool pods_ok = !(r.num_pods - nm + 1 > r.alloc_pods);
-    for (int s = 0; s < ns; ++s) {
+#pragma unroll
+    for (int s = 0; s < kRsvSlots; ++s) {
       if (!(mm >> s & 1)) continue;
       const int64_t rc = rsv_nn(rn.alloc_cpu[s], rn.allocd_cpu[s]), rm = rsv_nn(rn.alloc_mem[s], rn.allocd_mem[s]);
       bool fits = pods_ok && !(p.req_cpu > r.alloc_cpu - (pr_c - rc - ra_c)) &&
@@ -137,7 +141,8 @@ __device__ __forceinline__ RsvOut rsv_eval_node(const DevTable& T, const RsvNode
     // PreScore node order over matched (scoring.go:66, 162-181); nomination over FilterReservation-passing slots
     int32_t best_all = 0x7fffffff, best_sat = 0x7fffffff;
     int pick = -1;
-    for (int s = 0; s < ns; ++s) {
+#pragma unroll
+    for (int s = 0; s < kRsvSlots; ++s) {
       if (!(mm >> s & 1)) continue;
       const int32_t od = rn.order[s];
       if (od != 0 && best_all > od) best_all = od;
@@ -149,7 +154,8 @@ __device__ __forceinline__ RsvOut rsv_eval_node(const DevTable& T, const RsvNode
     o.order = best_all;
     if (pick < 0) {
       int32_t best = -1;
-      for (int s = 0; s < ns; ++s)
+#pragma unroll
+      for (int s = 0; s < kRsvSlots; ++s)
         if (sat >> s & 1) {
           const int32_t sc = rsv_score_slot(rn, s, p);
           if (sc > best) {  // prioritizeReservations + sort (unstable; pinned: lowest slot on ties)
@@ -159,23 +165,51 @@ __device__ __forceinline__ RsvOut rsv_eval_node(const DevTable& T, const RsvNode
         }
     }
     o.nom = pick;
-    o.raw = pick >= 0 ? rsv_score_slot(rn, pick, p) : 0;
+    int32_t raw = 0;
+#pragma unroll
+    for (int s = 0; s < kRsvSlots; ++s)
+      if (s == pick) raw = rsv_score_slot(rn, s, p);
+    o.raw = raw;
   }
   return o;
 }
 
-// Pass 1: per-node Filter + Fit/LoadAware total + nominated slot and raw Score; wave-reduced preferred-node key and
-// max raw Score into ws[0], ws[1].  val[i] = (base << 32) | raw << 8 | feasible << 7 | (nom + 1), 0 = filtered.
-__global__ __launch_bounds__(256) void rsv_eval(DevTable T, const RsvNode* __restrict__ RN,
-                                                const int32_t* __restrict__ rsv_n, const DevPod* __restrict__ pods,
-                                                const RsvPod* __restrict__ rpods, int64_t end, int64_t n,
-                                                EvalParams P, RsvParams RP, uint64_t* __restrict__ val,
-                                                unsigned long long* __restrict__ ws) {
+constexpr int kRsvThreads = 128;  // 2 waves per block: ≥ 2 blocks per CU at 50k nodes
+
+// Block max of a u64 over its waves (DPP wave max, then LDS); result valid in thread 0.
+__device__ __forceinline__ uint64_t rsv_block_max(uint64_t v, uint64_t* s_red) {
+  v = wave_max_u64_dpp(v);
+  const int w = threadIdx.x / kWave;
+  if ((threadIdx.x & (kWave - 1)) == 0) s_red[w] = v;
+  __syncthreads();
+  if (threadIdx.x == 0)
+    for (int k = 1; k < kRsvThreads / kWave; ++k) v = s_red[k] > v ? s_red[k] : v;
+  return v;
+}
+
+// Max over `nb` per-block partials, computed by one wave (every lane returns it).
+__device__ __forceinline__ uint64_t rsv_partials_max(const uint64_t* __restrict__ part, int nb) {
+  uint64_t v = 0;
+  for (int k = threadIdx.x & (kWave - 1); k < nb; k += kWave) v = part[k] > v ? part[k] : v;
+  return wave_max_u64_dpp(v);
+}
+
+// Pass 1: per-node Filter + Fit/LoadAware total + nominated slot and raw Score.  val[i] = (base << 32) |
+// raw << 8 | feasible << 7 | (nom + 1), 0 = filtered.  Per-block partials (no same-address atomics):
+// part[b] = max ~(order << 32 | node) over feasible nodes with an order label (PreScore preferred node, 0 = none),
+// part[nb + b] = max raw Score.
+__global__ __launch_bounds__(kRsvThreads) void rsv_eval(DevTable T, const RsvNode* __restrict__ RN,
+                                                        const int32_t* __restrict__ rsv_n,
+                                                        const DevPod* __restrict__ pods,
+                                                        const RsvPod* __restrict__ rpods, int64_t end, int64_t n,
+                                                        EvalParams P, RsvParams RP, uint64_t* __restrict__ val,
+                                                        uint64_t* __restrict__ part,
+                                                        const unsigned long long* __restrict__ ws) {
+  __shared__ uint64_t s_red[kRsvThreads / kWave];
   const int64_t j = (int64_t)ws[3];
   if (j >= end) return;  // uniform across the grid
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  uint64_t pk = 0;
-  uint32_t rawv = 0;
+  uint64_t pk = 0, rawv = 0;
   if (i < n) {
     const DevPod p = pods[j];
     const RsvPod rp = rpods[j];
@@ -184,26 +218,33 @@ __global__ __launch_bounds__(256) void rsv_eval(DevTable T, const RsvNode* __res
     if (o.feas) {
       v = ((uint64_t)(uint32_t)o.base << 32) | ((uint64_t)(uint32_t)o.raw << 8) | (1ull << 7) | (uint64_t)(o.nom + 1);
       if (o.order != 0x7fffffff) pk = ~(((uint64_t)(uint32_t)o.order << 32) | (uint64_t)(uint32_t)i);
-      rawv = (uint32_t)o.raw;
+      rawv = (uint64_t)(uint32_t)o.raw;
     }
     val[i] = v;
   }
-  pk = wave_max_u64_dpp(pk);
-  rawv = wave_max_u32(rawv);
-  if ((threadIdx.x & (kWave - 1)) == 0) {
-    if (pk) atomicMax(&ws[0], (unsigned long long)pk);
-    if (rawv) atomicMax(&ws[1], (unsigned long long)rawv);
+  const int nb = gridDim.x;
+  pk = rsv_block_max(pk, s_red);
+  __syncthreads();
+  rawv = rsv_block_max(rawv, s_red);
+  if (threadIdx.x == 0) {
+    part[blockIdx.x] = pk;
+    part[nb + blockIdx.x] = rawv;
   }
 }
 
-// Pass 2: PreScore preferred node (1000), DefaultNormalizeScore over the feasible nodes, × weight, packed argmax.
-__global__ __launch_bounds__(256) void rsv_select(const uint64_t* __restrict__ val, int64_t end, int64_t n,
-                                                  RsvParams RP, unsigned long long* __restrict__ ws) {
+// Pass 2: PreScore preferred node (1000), DefaultNormalizeScore over the feasible nodes, × weight, packed key;
+// part[2 nb + b] = the block's max key.
+__global__ __launch_bounds__(kRsvThreads) void rsv_select(const uint64_t* __restrict__ val, int64_t end, int64_t n,
+                                                          RsvParams RP, uint64_t* __restrict__ part,
+                                                          const unsigned long long* __restrict__ ws) {
+  __shared__ uint64_t s_red[kRsvThreads / kWave];
   if ((int64_t)ws[3] >= end) return;
+  const int nb = gridDim.x;
+  const uint64_t pk = rsv_partials_max(part, nb);
+  const uint64_t mraw = rsv_partials_max(part + nb, nb);
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint64_t pk = ws[0];
   const int64_t pref = pk ? (int64_t)(uint32_t)(~pk) : -1;
-  const int64_t mx = pk ? (ws[1] > 1000 ? (int64_t)ws[1] : 1000) : (int64_t)ws[1];
+  const int64_t mx = pk ? (mraw > 1000 ? (int64_t)mraw : 1000) : (int64_t)mraw;
   uint64_t key = 0;
   if (i < n) {
     const uint64_t v = val[i];
@@ -214,18 +255,22 @@ __global__ __launch_bounds__(256) void rsv_select(const uint64_t* __restrict__ v
       key = make_key(t, (uint32_t)i);
     }
   }
-  key = wave_max_key(key);
-  if ((threadIdx.x & (kWave - 1)) == 0 && key) atomicMax(&ws[2], (unsigned long long)key);
+  key = rsv_block_max(key, s_red);
+  if (threadIdx.x == 0) part[2 * nb + blockIdx.x] = key;
 }
 
-// Pass 3 (one lane): Reserve — assume on the winner row (NodeInfo + LoadAware assign cache) and
-// reservationCache.assumePod on its nominated slot (reservation_info.go:317-326); advance the cursor.
-__global__ void rsv_apply(DevTable T, RsvNode* __restrict__ RN, const uint64_t* __restrict__ val,
-                          const DevPod* __restrict__ pods, int64_t end, uint64_t* __restrict__ out_keys,
-                          int32_t* __restrict__ out_slot, unsigned long long* __restrict__ ws) {
+// Pass 3 (one wave): the winner = max over the block keys; lane 0 runs Reserve — assume on the winner row
+// (NodeInfo + LoadAware assign cache) and reservationCache.assumePod on its nominated slot
+// (reservation_info.go:317-326) — and advances the cursor.
+__global__ __launch_bounds__(kWave) void rsv_apply(DevTable T, RsvNode* __restrict__ RN,
+                                                   const uint64_t* __restrict__ val, const DevPod* __restrict__ pods,
+                                                   int64_t end, int nb, const uint64_t* __restrict__ part,
+                                                   uint64_t* __restrict__ out_keys, int32_t* __restrict__ out_slot,
+                                                   unsigned long long* __restrict__ ws) {
   const int64_t j = (int64_t)ws[3];
   if (j >= end) return;
-  const uint64_t k = ws[2];
+  const uint64_t k = rsv_partials_max(part + 2 * nb, nb);
+  if (threadIdx.x != 0) return;
   int32_t slot = -1;
   if (k) {
     const int64_t w = (int64_t)key_node(k);
@@ -251,9 +296,6 @@ __global__ void rsv_apply(DevTable T, RsvNode* __restrict__ RN, const uint64_t* 
   }
   out_keys[j] = k;
   out_slot[j] = slot;
-  ws[0] = 0;
-  ws[1] = 0;
-  ws[2] = 0;
   ws[3] = (unsigned long long)(j + 1);
 }
 
