@@ -2255,8 +2255,8 @@ double now_s() {
 }
 
 
-// Reservation profile: one FIFO pod per device pass (rsv_eval → rsv_select → rsv_apply), kRsvGroup passes per
-// hipGraph launch.  The pod index lives in the device cursor ws[3]; passes past `end` are no-ops.
+// Reservation profile: one FIFO pod per device pass (rsv_eval → rsv_select; Reserve in the next rsv_eval),
+// kRsvGroup passes + the group-closing rsv_apply per hipGraph launch.  The pod index lives in the device cursor ws[3]; passes past `end` are no-ops.
 constexpr int kRsvGroup = 32;
 int run_rsv(kg_engine* e, int64_t first, int64_t count, kg_stats* stats, double t0) {
   if (int rc = sync_static(e)) return rc;
@@ -2265,38 +2265,35 @@ int run_rsv(kg_engine* e, int64_t first, int64_t count, kg_stats* stats, double 
     const unsigned blocks = (unsigned)((n + kRsvThreads - 1) / kRsvThreads);
     const unsigned long long init[4] = {0, 0, 0, (unsigned long long)first};
     HIP_TRY(hipMemcpyAsync(e->rsv_ws.p, init, 32, hipMemcpyHostToDevice, e->stream));
+    auto issue_group = [&]() {
+      for (int g = 0; g < kRsvGroup; ++g) {
+        rsv_eval<<<blocks, kRsvThreads, 0, e->stream>>>(e->T, e->rsv_d.p, e->rsv_nd.p, e->pods.p, e->rpods.p, end, n, g,
+                                                         e->P, e->RP, e->rsv_val.p, e->rsv_part.p, e->out_keys.p,
+                                                         e->out_rslot.p, e->rsv_ws.p);
+        rsv_select<<<blocks, kRsvThreads, 0, e->stream>>>(e->rsv_val.p, end, n, g, e->RP, e->rsv_part.p, e->rsv_ws.p);
+      }
+      rsv_apply<<<1, kWave, 0, e->stream>>>(e->T, e->rsv_d.p, e->rsv_val.p, e->pods.p, end, (int)blocks, kRsvGroup - 1,
+                                            e->rsv_part.p, e->out_keys.p, e->out_rslot.p, e->rsv_ws.p);
+    };
     // KG_RSV_NO_GRAPH=1: plain stream launches (profilers whose kernel tracing does not follow graph launches)
     static const bool no_graph = std::getenv("KG_RSV_NO_GRAPH") && std::getenv("KG_RSV_NO_GRAPH")[0] == '1';
     if (no_graph) {
-      for (int64_t c = 0; c < count; ++c) {
-        rsv_eval<<<blocks, kRsvThreads, 0, e->stream>>>(e->T, e->rsv_d.p, e->rsv_nd.p, e->pods.p, e->rpods.p, end, n,
-                                                         e->P, e->RP, e->rsv_val.p, e->rsv_part.p, e->rsv_ws.p);
-        rsv_select<<<blocks, kRsvThreads, 0, e->stream>>>(e->rsv_val.p, end, n, e->RP, e->rsv_part.p, e->rsv_ws.p);
-        rsv_apply<<<1, kWave, 0, e->stream>>>(e->T, e->rsv_d.p, e->rsv_val.p, e->pods.p, end, (int)blocks,
-                                              e->rsv_part.p, e->out_keys.p, e->out_rslot.p, e->rsv_ws.p);
-      }
+      for (int64_t c = 0; c < count; c += kRsvGroup) issue_group();
       HIP_TRY(hipGetLastError());
       HIP_TRY(hipStreamSynchronize(e->stream));
-    }
-    hipGraph_t graph = nullptr;
-    hipGraphExec_t exec = nullptr;
-    if (!no_graph) {
-    HIP_TRY(hipStreamBeginCapture(e->stream, hipStreamCaptureModeThreadLocal));
-    for (int g = 0; g < kRsvGroup; ++g) {
-      rsv_eval<<<blocks, kRsvThreads, 0, e->stream>>>(e->T, e->rsv_d.p, e->rsv_nd.p, e->pods.p, e->rpods.p, end, n,
-                                                       e->P, e->RP, e->rsv_val.p, e->rsv_part.p, e->rsv_ws.p);
-      rsv_select<<<blocks, kRsvThreads, 0, e->stream>>>(e->rsv_val.p, end, n, e->RP, e->rsv_part.p, e->rsv_ws.p);
-      rsv_apply<<<1, kWave, 0, e->stream>>>(e->T, e->rsv_d.p, e->rsv_val.p, e->pods.p, end, (int)blocks,
-                                            e->rsv_part.p, e->out_keys.p, e->out_rslot.p, e->rsv_ws.p);
-    }
-    const hipError_t ce = hipStreamEndCapture(e->stream, &graph);
-    if (ce != hipSuccess) return fail(KG_E_DEVICE, "hipStreamEndCapture: %s", hipGetErrorString(ce));
-    hipError_t ge = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
-    for (int64_t c = 0; ge == hipSuccess && c < count; c += kRsvGroup) ge = hipGraphLaunch(exec, e->stream);
-    if (ge == hipSuccess) ge = hipStreamSynchronize(e->stream);
-    if (exec) (void)hipGraphExecDestroy(exec);
-    (void)hipGraphDestroy(graph);
-    if (ge != hipSuccess) return fail(KG_E_DEVICE, "reservation pass graph: %s", hipGetErrorString(ge));
+    } else {
+      hipGraph_t graph = nullptr;
+      hipGraphExec_t exec = nullptr;
+      HIP_TRY(hipStreamBeginCapture(e->stream, hipStreamCaptureModeThreadLocal));
+      issue_group();
+      const hipError_t ce = hipStreamEndCapture(e->stream, &graph);
+      if (ce != hipSuccess) return fail(KG_E_DEVICE, "hipStreamEndCapture: %s", hipGetErrorString(ce));
+      hipError_t ge = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+      for (int64_t c = 0; ge == hipSuccess && c < count; c += kRsvGroup) ge = hipGraphLaunch(exec, e->stream);
+      if (ge == hipSuccess) ge = hipStreamSynchronize(e->stream);
+      if (exec) (void)hipGraphExecDestroy(exec);
+      (void)hipGraphDestroy(graph);
+      if (ge != hipSuccess) return fail(KG_E_DEVICE, "reservation pass graph: %s", hipGetErrorString(ge));
     }
   } else if (count > 0) {
     HIP_TRY(hipMemsetAsync(e->out_keys.p + first, 0, count * 8, e->stream));
@@ -3116,16 +3113,16 @@ static int bench_rsv(kg_engine* e, int which, int iters, double* avg_ms, double*
   auto launch = [&]() {
     if (which == 0)
       rsv_eval<<<blocks, kRsvThreads, 0, e->stream>>>(e->T, e->rsv_d.p, e->rsv_nd.p, e->pods.p, e->rpods.p,
-                                                       e->n_staged, n, e->P, e->RP, e->rsv_val.p, e->rsv_part.p,
-                                                       e->rsv_ws.p);
+                                                       e->n_staged, n, 0, e->P, e->RP, e->rsv_val.p, e->rsv_part.p,
+                                                       e->out_keys.p, e->out_rslot.p, e->rsv_ws.p);
     else
-      rsv_select<<<blocks, kRsvThreads, 0, e->stream>>>(e->rsv_val.p, e->n_staged, n, e->RP, e->rsv_part.p,
+      rsv_select<<<blocks, kRsvThreads, 0, e->stream>>>(e->rsv_val.p, e->n_staged, n, 0, e->RP, e->rsv_part.p,
                                                          e->rsv_ws.p);
   };
   if (which == 1)  // rsv_select needs the packed values and partials of a real pass
     rsv_eval<<<blocks, kRsvThreads, 0, e->stream>>>(e->T, e->rsv_d.p, e->rsv_nd.p, e->pods.p, e->rpods.p,
-                                                     e->n_staged, n, e->P, e->RP, e->rsv_val.p, e->rsv_part.p,
-                                                     e->rsv_ws.p);
+                                                     e->n_staged, n, 0, e->P, e->RP, e->rsv_val.p, e->rsv_part.p,
+                                                     e->out_keys.p, e->out_rslot.p, e->rsv_ws.p);
   launch();  // warm
   hipEvent_t a, b;
   HIP_TRY(hipEventCreate(&a));

@@ -4,8 +4,9 @@
 // (nominator.go:76-134) and Score (scoring.go:103-203) with the PreScore preferred node, DefaultNormalizeScore,
 // then Reserve (plugin.go:521-559).
 //
-// One pod per pass, three kernels (HBM-bound wide pass, normalise + argmax pass, one-lane Reserve), captured in a
-// hipGraph per group of pods; the pod index is read from a device cursor that the Reserve kernel advances.
+// One pod per pass, two kernels (wide pass, normalise + argmax pass); pod j's Reserve runs in pod j+1's wide-pass
+// prologue by the thread owning the winner row.  A group of kRsvGroup pods is captured in one hipGraph, closed by
+// a one-wave kernel that reserves the group's last pod and advances the device cursor.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -36,7 +37,7 @@ struct RsvParams {
   int32_t filter, score, weight, pad;
 };
 
-// ws words: [3] = pod cursor (the others are unused)
+// ws words: [3] = cursor: the first pod of the current group (the others are unused)
 struct RsvOut {
   bool feas;
   int64_t base;   // Fit + LoadAware weighted total
@@ -194,21 +195,60 @@ __device__ __forceinline__ uint64_t rsv_partials_max(const uint64_t* __restrict_
   return wave_max_u64_dpp(v);
 }
 
-// Pass 1: per-node Filter + Fit/LoadAware total + nominated slot and raw Score.  val[i] = (base << 32) |
-// raw << 8 | feasible << 7 | (nom + 1), 0 = filtered.  Per-block partials (no same-address atomics):
-// part[b] = max ~(order << 32 | node) over feasible nodes with an order label (PreScore preferred node, 0 = none),
-// part[nb + b] = max raw Score.
-__global__ __launch_bounds__(kRsvThreads) void rsv_eval(DevTable T, const RsvNode* __restrict__ RN,
+// Reserve of pod j on its winner row w (NodeInfo + LoadAware assign cache) and reservationCache.assumePod on the
+// slot nominated there (reservation_info.go:317-326).  Called by the one thread that owns row w.
+__device__ __forceinline__ int32_t rsv_reserve(const DevTable& T, RsvNode* __restrict__ RN, int64_t w, uint64_t v,
+                                               const DevPod& p) {
+  Row r = load_row(T, w);
+  const int64_t prod = (p.flags & P_PROD) ? 1 : 0;
+  r.req_cpu += p.req_cpu;
+  r.req_mem += p.req_mem;
+  r.nz_cpu += p.nz_cpu;
+  r.nz_mem += p.nz_mem;
+  r.la_used_cpu += p.est_cpu;
+  r.la_used_mem += p.est_mem;
+  r.la_pused_cpu += prod * p.est_cpu;
+  r.la_pused_mem += prod * p.est_mem;
+  r.num_pods += 1;
+  store_mutable(T, w, r);
+  const int32_t slot = (int32_t)(v & 7) - 1;
+  if (slot >= 0) {
+    RN[w].allocd_cpu[slot] += p.req_cpu;
+    RN[w].allocd_mem[slot] += p.req_mem;
+    RN[w].assigned[slot] += 1;
+  }
+  return slot;
+}
+
+// Pass 1 for pod j = cursor + g: first the Reserve of pod j - 1 (g > 0; its winner is the max of the previous
+// rsv_select's block keys — the thread owning that row applies it, so no separate launch), then per-node Filter +
+// Fit/LoadAware total + nominated slot and raw Score.  val[i] = (base << 32) | raw << 8 | feasible << 7 | (nom + 1),
+// 0 = filtered.  Per-block partials (no same-address atomics): part[b] = max ~(order << 32 | node) over feasible
+// nodes with an order label (PreScore preferred node, 0 = none), part[nb + b] = max raw Score.
+__global__ __launch_bounds__(kRsvThreads) void rsv_eval(DevTable T, RsvNode* __restrict__ RN,
                                                         const int32_t* __restrict__ rsv_n,
                                                         const DevPod* __restrict__ pods,
                                                         const RsvPod* __restrict__ rpods, int64_t end, int64_t n,
-                                                        EvalParams P, RsvParams RP, uint64_t* __restrict__ val,
-                                                        uint64_t* __restrict__ part,
+                                                        int g, EvalParams P, RsvParams RP, uint64_t* __restrict__ val,
+                                                        uint64_t* __restrict__ part, uint64_t* __restrict__ out_keys,
+                                                        int32_t* __restrict__ out_slot,
                                                         const unsigned long long* __restrict__ ws) {
   __shared__ uint64_t s_red[kRsvThreads / kWave];
-  const int64_t j = (int64_t)ws[3];
-  if (j >= end) return;  // uniform across the grid
+  const int64_t j = (int64_t)ws[3] + g;
+  if (j - 1 >= end || (g == 0 && j >= end)) return;  // uniform across the grid
+  const int nb = gridDim.x;
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g > 0) {  // Reserve of pod j - 1
+    const uint64_t k = rsv_partials_max(part + 2 * nb, nb);
+    const int64_t w = k ? (int64_t)key_node(k) : -1;
+    if (i == w || (w < 0 && i == 0)) {
+      int32_t slot = -1;
+      if (w >= 0) slot = rsv_reserve(T, RN, w, val[w], pods[j - 1]);
+      out_keys[j - 1] = k;
+      out_slot[j - 1] = slot;
+    }
+    if (j >= end) return;
+  }
   uint64_t pk = 0, rawv = 0;
   if (i < n) {
     const DevPod p = pods[j];
@@ -222,7 +262,7 @@ __global__ __launch_bounds__(kRsvThreads) void rsv_eval(DevTable T, const RsvNod
     }
     val[i] = v;
   }
-  const int nb = gridDim.x;
+  __syncthreads();  // part[2nb..] (read above) is not rewritten here, but keep the block's LDS use ordered
   pk = rsv_block_max(pk, s_red);
   __syncthreads();
   rawv = rsv_block_max(rawv, s_red);
@@ -235,10 +275,10 @@ __global__ __launch_bounds__(kRsvThreads) void rsv_eval(DevTable T, const RsvNod
 // Pass 2: PreScore preferred node (1000), DefaultNormalizeScore over the feasible nodes, × weight, packed key;
 // part[2 nb + b] = the block's max key.
 __global__ __launch_bounds__(kRsvThreads) void rsv_select(const uint64_t* __restrict__ val, int64_t end, int64_t n,
-                                                          RsvParams RP, uint64_t* __restrict__ part,
+                                                          int g, RsvParams RP, uint64_t* __restrict__ part,
                                                           const unsigned long long* __restrict__ ws) {
   __shared__ uint64_t s_red[kRsvThreads / kWave];
-  if ((int64_t)ws[3] >= end) return;
+  if ((int64_t)ws[3] + g >= end) return;
   const int nb = gridDim.x;
   const uint64_t pk = rsv_partials_max(part, nb);
   const uint64_t mraw = rsv_partials_max(part + nb, nb);
@@ -259,44 +299,28 @@ __global__ __launch_bounds__(kRsvThreads) void rsv_select(const uint64_t* __rest
   if (threadIdx.x == 0) part[2 * nb + blockIdx.x] = key;
 }
 
-// Pass 3 (one wave): the winner = max over the block keys; lane 0 runs Reserve — assume on the winner row
-// (NodeInfo + LoadAware assign cache) and reservationCache.assumePod on its nominated slot
-// (reservation_info.go:317-326) — and advances the cursor.
+// End of a group of kRsvGroup pods (one wave): Reserve of the group's last pod (cursor + g_last) and the cursor
+// advance.  Pods past `end` are skipped.
 __global__ __launch_bounds__(kWave) void rsv_apply(DevTable T, RsvNode* __restrict__ RN,
                                                    const uint64_t* __restrict__ val, const DevPod* __restrict__ pods,
-                                                   int64_t end, int nb, const uint64_t* __restrict__ part,
+                                                   int64_t end, int nb, int g_last, const uint64_t* __restrict__ part,
                                                    uint64_t* __restrict__ out_keys, int32_t* __restrict__ out_slot,
                                                    unsigned long long* __restrict__ ws) {
-  const int64_t j = (int64_t)ws[3];
-  if (j >= end) return;
-  const uint64_t k = rsv_partials_max(part + 2 * nb, nb);
+  const int64_t base = (int64_t)ws[3];
+  const int64_t j = base + g_last;
+  if (base >= end) return;
+  const uint64_t k = j < end ? rsv_partials_max(part + 2 * nb, nb) : 0;
   if (threadIdx.x != 0) return;
-  int32_t slot = -1;
-  if (k) {
-    const int64_t w = (int64_t)key_node(k);
-    const DevPod p = pods[j];
-    Row r = load_row(T, w);
-    const int64_t prod = (p.flags & P_PROD) ? 1 : 0;
-    r.req_cpu += p.req_cpu;
-    r.req_mem += p.req_mem;
-    r.nz_cpu += p.nz_cpu;
-    r.nz_mem += p.nz_mem;
-    r.la_used_cpu += p.est_cpu;
-    r.la_used_mem += p.est_mem;
-    r.la_pused_cpu += prod * p.est_cpu;
-    r.la_pused_mem += prod * p.est_mem;
-    r.num_pods += 1;
-    store_mutable(T, w, r);
-    slot = (int32_t)(val[w] & 7) - 1;
-    if (slot >= 0) {
-      RN[w].allocd_cpu[slot] += p.req_cpu;
-      RN[w].allocd_mem[slot] += p.req_mem;
-      RN[w].assigned[slot] += 1;
+  if (j < end) {
+    int32_t slot = -1;
+    if (k) {
+      const int64_t w = (int64_t)key_node(k);
+      slot = rsv_reserve(T, RN, w, val[w], pods[j]);
     }
+    out_keys[j] = k;
+    out_slot[j] = slot;
   }
-  out_keys[j] = k;
-  out_slot[j] = slot;
-  ws[3] = (unsigned long long)(j + 1);
+  ws[3] = (unsigned long long)(base + g_last + 1);
 }
 
 __global__ void scatter_rsv(RsvNode* __restrict__ RN, int32_t* __restrict__ rsv_n, const RsvNode* __restrict__ s,
