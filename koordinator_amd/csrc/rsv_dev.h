@@ -175,7 +175,7 @@ __device__ __forceinline__ RsvOut rsv_eval_node(const DevTable& T, const RsvNode
   return o;
 }
 
-constexpr int kRsvThreads = 128;  // 2 waves per block: ≥ 2 blocks per CU at 50k nodes
+constexpr int kRsvThreads = 256;  // 4 waves per block: fewer block partials to reduce per pass
 
 // Block max of a u64 over its waves (DPP wave max, then LDS); result valid in thread 0.
 __device__ __forceinline__ uint64_t rsv_block_max(uint64_t v, uint64_t* s_red) {
