@@ -8,6 +8,14 @@ percentageOfNodesToScore=100, ties → lowest index.  One step = scheduling `--p
 schedules the whole 1M-pod queue of config 3.  Inputs are resident in HBM before the timed region (nodes
 ingested, pod queue staged); PCIe-inclusive timing of kg_pods_schedule is reported separately.
 
+Other workloads (--workload): c1 (500 nodes, 5k pods: the reference's CPU-runnable case), c4 (NodeNUMAResource),
+c5 (Reservation + DeviceShare + ElasticQuota, 50k nodes), c5ds / c5r (its DeviceShare / Reservation halves).
+
+After the timed region: (1) `--profile-pods` more queued pods are scheduled with live kernel timing (HIP events
+bracketing every launch on its own stream, kg_profile_enable) — the roofline's kernel time; (2) the first
+`--check` placements are compared with the oracle (bit-exact); (3) the CPU baseline (the oracle, the same
+algorithm in C) is timed on a bounded sample with 16 threads and with 1 thread.
+
 N>1 (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): the node table is replicated
 and its evaluation sharded over ranks; candidate lists are exchanged with RCCL all-gather over xGMI.  Total
 work is fixed as N grows → "scaling": "strong".
@@ -28,6 +36,16 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+B_NODE = 76.0          # SURVEY §8d b_node for Fit + LoadAware: bytes of node columns one evaluation reads
+
+# workload → (nodes, pods per step, batch, pods per wave, default check)
+WORKLOADS = {
+    "c1": (500, 5_000, 32, 8, 5_000),
+    "c3": (100_000, 100_000, 32, 8, 10_000),
+    "c4": (10_000, 10_000, 16, 1, 2_000),
+    "c5ds": (50_000, 10_000, 32, 4, 2_000),
+    "c5r": (50_000, 10_000, 32, 4, 2_000),
+}
 
 
 def parse():
@@ -35,20 +53,21 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--workload", choices=("c3", "c4", "c5", "c5r"), default="c3",
-                    help="c3: Fit+LoadAware at 100k nodes (the BASELINE metric); c4: + NodeNUMAResource cpuset/NUMA "
-                         "on 2-socket 256-cpu nodes")
-    ap.add_argument("--nodes", type=int, default=None, help="default 100k (c3) / 10k (c4)")
-    ap.add_argument("--pods-per-step", type=int, default=None, help="default 100k (c3) / 10k (c4)")
-    ap.add_argument("--batch", type=int, default=None, help="default 32 (c3, c5) / 16 (c4)")
-    ap.add_argument("--pods-per-wave", type=int, default=None, help="default 8 (c3) / 1 (c4) / 4 (c5)")
-    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU baseline sample")
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c3")
+    ap.add_argument("--nodes", type=int, default=None)
+    ap.add_argument("--pods-per-step", type=int, default=None)
+    ap.add_argument("--batch", type=int, default=None)
+    ap.add_argument("--pods-per-wave", type=int, default=None)
+    ap.add_argument("--depth", type=int, default=0, help="pipeline depth (rounds in flight; 0 = engine default)")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of each CPU baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--kernel-iters", type=int, default=50)
-    ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "r01", "traffic_c3.json"),
+    ap.add_argument("--kernel-iters", type=int, default=20)
+    ap.add_argument("--profile-pods", type=int, default=None, help="pods scheduled with live kernel timing after "
+                    "the timed region (default min(pods per step, 20k))")
+    ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "r02", "traffic_c3.json"),
                     help="PMC summary (scripts/pmc_summary.py) of the same workload: per-launch HBM bytes")
-    ap.add_argument("--check", type=int, default=0, help="verify the first N placements against the oracle")
+    ap.add_argument("--check", type=int, default=None, help="verify the first N placements against the oracle")
     return ap.parse_args()
 
 
@@ -94,38 +113,76 @@ class Dist:
             self.dist.destroy_process_group()
 
 
-def cpu_baseline(cfg, cluster, pods, budget_s, threads, numa=None, devices=None, rsv=None):
-    """Oracle (C restatement of the same Go algorithm, oracle/oracle.c [+ numa.c / deviceshare.c]) on this host,
-    bounded sample."""
-    from oracle import oracle
-    st = oracle.states(cluster.n)
-    oracle.add_pods(cfg, st, cluster.existing_pods, cluster.existing_node)
-    buf = oracle.numa_states(numa) if numa is not None else None
-    dev = devices.copy() if devices is not None else None
-    rs = rsv.copy() if rsv is not None else None
+class Work:
+    """One workload: cluster, per-plugin node state, queue generator, engine loader and the oracle run."""
 
-    def run(p):
-        if rs is not None:  # or_schedule_resv is single-threaded
-            oracle.schedule_resv(cfg, cluster.nodes, cluster.metrics, st, rs, p, cluster.now_ns)
-        elif dev is not None:
-            oracle.schedule_full(cfg, cluster.nodes, cluster.metrics, st, p, cluster.now_ns, threads, devices=dev)
-        elif buf is None:
-            oracle.schedule(cfg, cluster.nodes, cluster.metrics, st, p, cluster.now_ns, threads)
+    def __init__(self, name, nodes, cfg):
+        from koordinator_amd import synth
+        self.name, self.cfg = name, cfg
+        self.numa = self.devices = self.rsv = None
+        S = synth
+        if name == "c4":
+            self.seed = S.BASE_SEED + 4
+            self.cluster, self.numa = S.make_numa_cluster(nodes, seed=self.seed)
+            self.make_pods = S.make_numa_pods
+        elif name == "c5ds":
+            self.seed = S.BASE_SEED + 6
+            self.cluster, self.devices = S.make_gpu_cluster(nodes, seed=self.seed)
+            self.make_pods = S.make_gpu_pods
+        elif name == "c5r":
+            self.seed = S.BASE_SEED + 8
+            self.cluster, self.rsv = S.make_rsv_cluster(nodes, seed=self.seed)
+            self.make_pods = S.make_rsv_pods
+        else:  # c1, c3: Fit + LoadAware
+            self.seed = S.BASE_SEED + (1 if name == "c1" else 3)
+            self.cluster = S.make_cluster(nodes, seed=self.seed)
+            self.make_pods = S.make_pods
+
+    def load(self, e):
+        from koordinator_amd import synth
+        if self.numa is not None:
+            synth.load_numa_into(e, self.cluster, self.numa)
+        elif self.devices is not None:
+            synth.load_gpu_into(e, self.cluster, self.devices)
+        elif self.rsv is not None:
+            synth.load_rsv_into(e, self.cluster, self.rsv)
         else:
-            oracle.schedule_numa(cfg, cluster.nodes, cluster.metrics, st, buf, p, cluster.now_ns, threads)
+            synth.load_into(e, self.cluster)
 
-    probe = 64
+    def oracle_run(self, pods, threads):
+        """(node idx, oracle name) of the oracle's sequential FIFO run over `pods` from the initial state."""
+        from oracle import oracle
+        cl, cfg = self.cluster, self.cfg
+        st = oracle.states(cl.n)
+        oracle.add_pods(cfg, st, cl.existing_pods, cl.existing_node)
+        if self.rsv is not None:
+            on, _, _ = oracle.schedule_resv(cfg, cl.nodes, cl.metrics, st, self.rsv.copy(), pods, cl.now_ns)
+            return on, "oracle/reservation.c or_schedule_resv (single-threaded loop)"
+        if self.devices is not None:
+            on, _, _, _ = oracle.schedule_full(cfg, cl.nodes, cl.metrics, st, pods, cl.now_ns, threads,
+                                               devices=self.devices.copy())
+            return on, "oracle/oracle.c or_schedule_full (Parallelizer chunking)"
+        if self.numa is not None:
+            on, _ = oracle.schedule_numa(cfg, cl.nodes, cl.metrics, st, oracle.numa_states(self.numa), pods,
+                                         cl.now_ns, threads)
+            return on, "oracle/oracle.c or_schedule_numa (Parallelizer chunking)"
+        on, _ = oracle.schedule(cfg, cl.nodes, cl.metrics, st, pods, cl.now_ns, threads)
+        return on, "oracle/oracle.c or_schedule (Parallelizer chunking)"
+
+
+def cpu_sample(work, pods, budget_s, threads):
+    """Oracle on this host over a bounded prefix of the queue: (pods, seconds, description)."""
+    probe = min(64, len(pods))
     t0 = time.perf_counter()
-    run(pods[:probe])
+    work.oracle_run(pods[:probe], threads)
     per_pod = (time.perf_counter() - t0) / probe
-    m = int(min(len(pods) - probe, max(probe, budget_s / max(per_pod, 1e-9))))
+    m = int(min(len(pods), max(probe, budget_s / max(per_pod, 1e-9))))
     t0 = time.perf_counter()
-    run(pods[probe:probe + m])
-    dt = time.perf_counter() - t0
-    return m, dt
+    _, desc = work.oracle_run(pods[:m], threads)
+    return m, time.perf_counter() - t0, desc
 
 
-def pmc_traffic(path, kernel, nodes, batch, ppw):
+def pmc_traffic(path, kernel, nodes, batch, ppw, depth):
     """Per-launch HBM bytes of `kernel` (FETCH_SIZE x2 + WRITE_SIZE, gfx950-corrected by scripts/pmc_summary.py)
     from a committed rocprofv3 --pmc summary, if it was collected on this exact workload geometry."""
     try:
@@ -134,7 +191,8 @@ def pmc_traffic(path, kernel, nodes, batch, ppw):
     except (OSError, ValueError):
         return None, None
     m = d.get("_meta", {})
-    if (m.get("nodes"), m.get("batch_pods"), m.get("pods_per_wave")) != (nodes, batch, ppw) or kernel not in d:
+    if (m.get("nodes"), m.get("batch_pods"), m.get("pods_per_wave"), m.get("depth")) != (nodes, batch, ppw, depth) \
+            or kernel not in d:
         return None, None
     return d[kernel]["traffic_bytes"], os.path.relpath(path, ROOT)
 
@@ -142,68 +200,48 @@ def pmc_traffic(path, kernel, nodes, batch, ppw):
 def main():
     args = parse()
     d = Dist(args.gpus)
-    from koordinator_amd import Engine, framework, synth
+    from koordinator_amd import Engine, framework
     from koordinator_amd.engine import nccl_unique_id
 
     nccl_id = None
     if d.world > 1:
         nccl_id = d.bcast_bytes(nccl_unique_id() if d.rank == 0 else None)
-    c4 = args.workload == "c4"
-    c5 = args.workload == "c5"
-    c5r = args.workload == "c5r"
-    args.nodes = args.nodes or (10_000 if c4 else (50_000 if (c5 or c5r) else 100_000))
-    args.pods_per_step = args.pods_per_step or (10_000 if (c4 or c5 or c5r) else 100_000)
-    # geometry sweeps: profiles/r01/c4_sweep.txt, c5_sweep.txt
-    args.pods_per_wave = args.pods_per_wave or (1 if c4 else (4 if c5 else 8))
-    args.batch = args.batch or (16 if c4 else 32)
+    wl = args.workload
+    nodes0, pps0, b0, ppw0, check0 = WORKLOADS[wl]
+    args.nodes = args.nodes or nodes0
+    args.pods_per_step = args.pods_per_step or pps0
+    args.batch = args.batch or b0
+    args.pods_per_wave = args.pods_per_wave or ppw0
+    args.check = check0 if args.check is None else args.check
+    if wl == "c1" and args.steps == 10:
+        args.steps = 1  # the whole 5k-pod queue of config 1
     F = framework
     profile = None
-    if c4:
+    if wl == "c4":
         profile = F.Profile(filter=(F.NODE_RESOURCES_FIT, F.LOAD_AWARE, F.NODE_NUMA_RESOURCE),
                             score={F.NODE_RESOURCES_FIT: 1, F.LOAD_AWARE: 1, F.NODE_NUMA_RESOURCE: 1})
-    elif c5:  # shipped weights: DeviceShare 1 (config/manager/scheduler-config.yaml:82-91)
+    elif wl == "c5ds":  # shipped weights: DeviceShare 1 (config/manager/scheduler-config.yaml:82-91)
         profile = F.Profile(filter=(F.NODE_RESOURCES_FIT, F.LOAD_AWARE, F.DEVICE_SHARE),
                             score={F.NODE_RESOURCES_FIT: 1, F.LOAD_AWARE: 1, F.DEVICE_SHARE: 1})
-    elif c5r:  # shipped weights: Reservation 5000 (config/manager/scheduler-config.yaml:90-91)
+    elif wl == "c5r":  # shipped weights: Reservation 5000 (config/manager/scheduler-config.yaml:90-91)
         profile = F.Profile(filter=(F.NODE_RESOURCES_FIT, F.LOAD_AWARE, F.RESERVATION),
                             score={F.NODE_RESOURCES_FIT: 1, F.LOAD_AWARE: 1, F.RESERVATION: 5000})
     cfg = framework.build_config(batch_pods=args.batch, pods_per_wave=args.pods_per_wave, device_id=d.local_rank,
-                                 profile=profile)
-    numa = devices = rsv = None
-    if c4:
-        seed = synth.BASE_SEED + 4
-        cluster, numa = synth.make_numa_cluster(args.nodes, seed=seed)
-        make_pods = synth.make_numa_pods
-    elif c5:
-        seed = synth.BASE_SEED + 6
-        cluster, devices = synth.make_gpu_cluster(args.nodes, seed=seed)
-        make_pods = synth.make_gpu_pods
-    elif c5r:
-        seed = synth.BASE_SEED + 8
-        cluster, rsv = synth.make_rsv_cluster(args.nodes, seed=seed)
-        make_pods = synth.make_rsv_pods
-    else:
-        seed = synth.BASE_SEED + 3
-        cluster = synth.make_cluster(args.nodes, seed=seed)
-        make_pods = synth.make_pods
+                                 profile=profile, pipeline_depth=args.depth)
+    work = Work(wl, args.nodes, cfg)
+    cluster = work.cluster
     total = args.steps * args.pods_per_step
-    pods = make_pods(total, seed=seed + 1)
+    n_prof = args.profile_pods if args.profile_pods is not None else min(args.pods_per_step, 20_000)
+    pods = work.make_pods(total + n_prof, seed=work.seed + 1)
 
     def engine():
         e = Engine(cfg, cluster.n, rank=d.rank, n_ranks=d.world, nccl_id=nccl_id)
-        if c4:
-            synth.load_numa_into(e, cluster, numa)
-        elif c5:
-            synth.load_gpu_into(e, cluster, devices)
-        elif c5r:
-            synth.load_rsv_into(e, cluster, rsv)
-        else:
-            synth.load_into(e, cluster)
+        work.load(e)
         return e
 
     # warmup on a throw-away engine (same cluster, different pods): code objects, caches, RCCL channels
     if args.warmup > 0:
-        wp = make_pods(args.warmup * min(args.pods_per_step, 20_000), seed=seed + 7)
+        wp = work.make_pods(args.warmup * min(args.pods_per_step, 20_000), seed=work.seed + 7)
         with engine() as ew:
             ew.stage(wp)
             ew.schedule_staged(0, len(wp))
@@ -224,17 +262,34 @@ def main():
     node_idx, score = e.fetch(0, total)
     placed = int((node_idx >= 0).sum())
 
-    # per-kernel live timing (HIP events on the engine stream) for the roofline
-    names = (("rsv_eval", "rsv_select") if c5r else
-             ("eval_round", "merge_round", "resolve_round") + (("ds_max_round", "ds_norm_reduce") if c5 else ()))
-    kernels = {name: e.bench_kernel(which, args.kernel_iters) for which, name in enumerate(names)}
-    # roofline kernel: the wide pass, the only kernel whose work scales with node evaluations (SURVEY §8d's
-    # 76 B per evaluation); merge and the single-wave FIFO resolver are latency-bound per round
-    # (C5: ds_max_round is the DeviceShare profile's full evaluation; eval_round_ds only normalizes its output)
-    # (C5 Reservation: rsv_eval is the per-pod wide pass; rsv_select re-reads 8 B per node, rsv_apply is one lane)
-    dom = "ds_max_round" if c5 else ("rsv_eval" if c5r else "eval_round")
-    dom_ms, dom_bytes = kernels[dom]
-    achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
+    # live kernel timing on the real pipelined runner, continuing the same queue (outside the timed region)
+    live = {}
+    if n_prof > 0:
+        e.profile(True)
+        e.schedule_staged(total, n_prof)
+        live = {k: {"avg_ms": ms / n, "launches": n} for k, (ms, n) in e.profile_read().items()}
+        e.profile(False)
+    # isolated replays of one round's kernels (warm caches, no concurrency) for comparison
+    names = (("rsv_eval", "rsv_select") if wl == "c5r" else
+             ("eval_round", "merge_round", "resolve_round") + (("ds_max_round", "ds_norm_reduce") if wl == "c5ds" else ()))
+    isolated = {name: e.bench_kernel(which, args.kernel_iters) for which, name in enumerate(names)}
+
+    # roofline kernel: the wide pass — the only kernel whose work scales with node evaluations.  One launch
+    # processes the round's B pods against every node row of this rank's shard, reading each row once:
+    # algorithmic bytes = rows × b_node + the candidate lists written + the pods read.
+    dom = {"c5ds": "ds_max_round", "c5r": "rsv_eval"}.get(wl, "eval_round")
+    n_local = -(-cluster.n // d.world)
+    nt = max(1, -(-n_local // 256))
+    B = 1 if wl == "c5r" else args.batch
+    if wl == "c5ds":  # ds_max_round also reads the 272-B GPU row and writes a 4-B packed value per (pod, node)
+        algo = n_local * (B_NODE + 272.0) + B * n_local * 4.0 + B * nt * 8.0
+    elif wl == "c5r":  # rsv_eval (one pod per pass): _, isolated replay reports its own accounting
+        algo = isolated["rsv_eval"][1]
+    else:
+        algo = n_local * B_NODE + B * nt * 8 * 8.0 + B * 96.0
+    dom_ms = live.get(dom, {}).get("avg_ms") or isolated[dom][0]
+    achieved = algo / (dom_ms * 1e-3) / 1e9
+    per_eval = B * n_local * B_NODE / (dom_ms * 1e-3) / 1e9  # §8d per-evaluation accounting (one table read per pod)
 
     # PCIe-inclusive path (host pods in, host decisions out) on a fresh engine, one step
     pcie = None
@@ -246,48 +301,45 @@ def main():
 
     check = None
     if args.check and d.rank == 0:
-        from oracle import oracle
-        if c5r:
-            st = oracle.states(cluster.n)
-            oracle.add_pods(cfg, st, cluster.existing_pods, cluster.existing_node)
-            on, _, _ = oracle.schedule_resv(cfg, cluster.nodes, cluster.metrics, st, rsv.copy(), pods[: args.check],
-                                            cluster.now_ns)
-        elif c5:
-            st = oracle.states(cluster.n)
-            oracle.add_pods(cfg, st, cluster.existing_pods, cluster.existing_node)
-            on, _, _, _ = oracle.schedule_full(cfg, cluster.nodes, cluster.metrics, st, pods[: args.check],
-                                               cluster.now_ns, args.cpu_threads, devices=devices.copy())
-        elif c4:
-            st = oracle.states(cluster.n)
-            oracle.add_pods(cfg, st, cluster.existing_pods, cluster.existing_node)
-            on, _ = oracle.schedule_numa(cfg, cluster.nodes, cluster.metrics, st, oracle.numa_states(numa),
-                                         pods[: args.check], cluster.now_ns, args.cpu_threads)
-        else:
-            on, _, _ = oracle.schedule_cluster(cfg, cluster, pods[: args.check], n_threads=args.cpu_threads)
-        check = bool(np.array_equal(on, node_idx[: args.check]))
+        nchk = min(args.check, total)
+        print(f"[bench] oracle check of the first {nchk} placements", file=sys.stderr, flush=True)
+        on, _ = work.oracle_run(pods[:nchk], args.cpu_threads)
+        check = bool(np.array_equal(on, node_idx[:nchk]))
 
     cpu = None
     if d.rank == 0 and d.world == 1 and not args.no_cpu_baseline:
-        print("[bench] cpu baseline sample", file=sys.stderr, flush=True)
-        m, dt = cpu_baseline(cfg, cluster, pods, args.cpu_seconds, args.cpu_threads, numa, devices, rsv)
-        threads = 1 if c5r else args.cpu_threads
+        print("[bench] cpu baseline samples", file=sys.stderr, flush=True)
+        threads = 1 if wl == "c5r" else args.cpu_threads
+        m, dt, desc = cpu_sample(work, pods[:total], args.cpu_seconds, threads)
+        m1, dt1, _ = cpu_sample(work, pods[:total], args.cpu_seconds / 3, 1)
         cpu = {"value": m / dt, "unit": "pods/s", "cores": threads, "kind": "port",
-               "sample": f"first {m} pods of the same queue after a 64-pod probe, {cluster.n} nodes, "
-                         f"oracle/{'reservation.c or_schedule_resv' if c5r else 'oracle.c ' + ('or_schedule_numa' if c4 else ('or_schedule_full' if c5 else 'or_schedule'))}, "
-                         f"{threads} thread(s) "
-                         f"{'(single-threaded loop)' if c5r else '(Parallelizer chunking)'}, "
-                         f"host nproc={os.cpu_count()}",
-               "node_evals_per_sec": m * cluster.n / dt}
+               "sample": f"first {m} pods of the same queue, {cluster.n} nodes, {desc}, {threads} thread(s); "
+                         f"host nproc={os.cpu_count()} (the GPU box's CPU share is 16 threads per GPU)",
+               "node_evals_per_sec": m * cluster.n / dt,
+               "single_thread": {"value": m1 / dt1, "sample_pods": m1}}
 
-    traffic, traffic_src = (pmc_traffic(args.traffic_file, dom, cluster.n, args.batch, args.pods_per_wave)
-                            if d.world == 1 and not (c4 or c5) else (None, None))
+    traffic, traffic_src = (pmc_traffic(args.traffic_file, dom, cluster.n, args.batch, args.pods_per_wave,
+                                        args.depth) if d.world == 1 else (None, None))
     if d.rank == 0:
         pods_s = total / elapsed
+        desc = {
+            "c1": "C1 cluster: %d nodes, %d-pod FIFO queue, NodeResourcesFit+LoadAwareScheduling, %d pods per step",
+            "c3": "C3 cluster: %d nodes, %d-pod FIFO queue, NodeResourcesFit+LoadAwareScheduling, %d pods per step",
+            "c4": "C4 cluster: %d 2-socket 256-cpu nodes (node count: builder's choice, BASELINE names none), "
+                  "%d-pod FIFO queue (70%% cpuset LSR/LSE), NodeResourcesFit+LoadAwareScheduling+NodeNUMAResource, "
+                  "%d pods per step",
+            "c5ds": "C5 (DeviceShare part): %d nodes x 8 GPUs, %d-pod FIFO queue (30%% GPU-share), "
+                    "NodeResourcesFit+LoadAwareScheduling+DeviceShare, %d pods per step",
+            "c5r": "C5 (Reservation part): %d nodes (30%% with 1-4 reservations), %d-pod FIFO queue (20%% "
+                   "reservation-owned), NodeResourcesFit+LoadAwareScheduling+Reservation (w 5000), one pod per device "
+                   "pass, %d pods per step",
+        }[wl] % (cluster.n, total, args.pods_per_step)
         out = {
-            "metric": ("pods scheduled/sec, NodeNUMAResource cpuset/NUMA profile (node-evals/sec alongside)" if c4
-                       else ("pods scheduled/sec, Reservation profile (node-evals/sec alongside)" if c5r else
-                             "pods scheduled/sec, DeviceShare GPU-share profile (node-evals/sec alongside)" if c5
-                             else "pods scheduled/sec at 100k nodes (node-evals/sec alongside)")),
+            "metric": {"c3": "pods scheduled/sec at 100k nodes (node-evals/sec alongside)",
+                       "c1": "pods scheduled/sec, config 1 (500 nodes; node-evals/sec alongside)",
+                       "c4": "pods scheduled/sec, NodeNUMAResource cpuset/NUMA profile (node-evals/sec alongside)",
+                       "c5ds": "pods scheduled/sec, DeviceShare GPU-share profile (node-evals/sec alongside)",
+                       "c5r": "pods scheduled/sec, Reservation profile (node-evals/sec alongside)"}[wl],
             "value": pods_s,
             "unit": "pods/s",
             "n_gpus": d.world,
@@ -298,29 +350,26 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "int64",
-            "data": "synthetic (SURVEY §8d generator, seed %d)" % seed,
-            "config": {"workload": ("C4 cluster: %d 2-socket 256-cpu nodes, %d-pod FIFO queue (70%% cpuset LSR/LSE), "
-                                    "NodeResourcesFit+LoadAwareScheduling+NodeNUMAResource, %d pods per step" if c4 else
-                                    ("C5 (Reservation part): %d nodes (30%% with 1-4 reservations), %d-pod FIFO queue "
-                                     "(20%% reservation-owned), NodeResourcesFit+LoadAwareScheduling+Reservation (w 5000), "
-                                     "one pod per device pass, %d pods per step" if c5r else
-                                     "C5 (DeviceShare part): %d nodes x 8 GPUs, %d-pod FIFO queue (30%% GPU-share), "
-                                     "NodeResourcesFit+LoadAwareScheduling+DeviceShare, %d pods per step" if c5 else
-                                     "C3 cluster: %d nodes, %d-pod FIFO queue, NodeResourcesFit+LoadAwareScheduling, "
-                                     "%d pods per step")) % (cluster.n, total, args.pods_per_step),
-                       "nodes": cluster.n, "pods": total, "batch_pods": 1 if c5r else args.batch,
+            "data": "synthetic (SURVEY §8d generator, seed %d)" % work.seed,
+            "config": {"workload": desc, "nodes": cluster.n, "pods": total, "batch_pods": B,
+                       "pods_per_wave": args.pods_per_wave, "pipeline_depth": args.depth or "default",
                        "parallelism": "node-sharded x%d (replicated table, RCCL all-gather)" % d.world},
             "node_evals_per_sec": pods_s * cluster.n,
             "placed": placed,
             "device_rounds": rounds,
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "traffic_source": traffic_src,
-                         "kernels_ms": {k: v[0] for k, v in kernels.items()},
-                         "algo_bytes": {k: v[1] for k, v in kernels.items()}},
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
+                         "kernel_ms": dom_ms, "algo_bytes_per_launch": algo,
+                         "timing": "live HIP events around every launch of %d extra queued pods (kg_profile_enable)"
+                                   % n_prof if dom in live else "isolated replay (kg_bench_kernel)",
+                         "per_evaluation_rate_gbs": per_eval,
+                         "live_ms": {k: v["avg_ms"] for k, v in live.items()},
+                         "live_launches": {k: v["launches"] for k, v in live.items()},
+                         "isolated_ms": {k: v[0] for k, v in isolated.items()}},
             "cpu_baseline": cpu,
             "pcie_inclusive_pods_per_sec": pcie,
             "oracle_check": check,
+            "oracle_check_pods": min(args.check, total) if args.check else 0,
         }
         print(json.dumps(out), flush=True)
     e.close()

@@ -179,7 +179,8 @@ typedef struct kg_config {
   int64_t reservation_filter;                  /* Reservation at Filter (+ BeforePreFilter restore)   */
   int64_t reservation_score;                   /* Reservation at PreScore/Score (NormalizeScore: DefaultNormalizeScore) */
   int64_t weight_reservation;
-  int64_t reserved[5];
+  int64_t pipeline_depth;                      /* rounds in flight (1..4; 0 = default 2) for monotone profiles  */
+  int64_t reserved[4];
 } kg_config;
 
 /* One node (snapshot index = position given by the caller). */
@@ -392,6 +393,17 @@ int kg_quotas_set(kg_engine* e, const kg_quota* quotas, int64_t n);
 /* Reads the DEVICE quota table back (used / non_preemptible_used after the batches so far). */
 int kg_quotas_read(kg_engine* e, kg_quota* out, int64_t n);
 
+/* Live kernel timing of the real (pipelined) round runners: with profiling on, every launch of kind k
+ * (KG_PROF_*) is bracketed by HIP events on its own stream; kg_profile_read returns the summed event time (ms)
+ * and the launch count per kind since kg_profile_enable.  Adds two event records per launch: not for the timed
+ * region of a benchmark. */
+enum {
+  KG_PROF_EVAL = 0, KG_PROF_MERGE = 1, KG_PROF_RESOLVE = 2, KG_PROF_DS_MAX = 3, KG_PROF_DS_NORM = 4,
+  KG_PROF_RSV_EVAL = 5, KG_PROF_RSV_SELECT = 6, KG_PROF_RSV_APPLY = 7, KG_PROF_KINDS = 16
+};
+int kg_profile_enable(kg_engine* e, int on);
+int kg_profile_read(kg_engine* e, double* ms_total, int64_t* launches);
+
 /* Measurement hooks (bench.py): replays one device round's kernel `which` (0 = eval, 1 = merge, 2 = resolve) `iters` times
  * on the engine stream between HIP events, restoring state, and returns the mean duration in ms plus the
  * algorithmic bytes that kernel must move per launch. Requires a staged queue. */
@@ -411,7 +423,8 @@ int kg_debug_fast_lrs(kg_engine* e, const int64_t* requested, const int64_t* cap
  * the number of (pod, node) pairs where feasibility or total score differ (must be 0). */
 int kg_debug_eval_paths(kg_engine* e, int64_t* mismatches);
 
-/* Diagnostic builds (-DKG_STAMPS) only: copies the in-kernel (s_memtime, s_memrealtime) stamps, uint64[4][32][2]. */
+/* Diagnostic builds (-DKG_STAMPS) only: copies the in-kernel (s_memtime, s_memrealtime) stamps, uint64[4][32][2],
+ * then the last resolver launch's per-pod (s_memtime, path bits), uint64[64][2]. */
 int kg_debug_stamps(kg_engine* e, uint64_t* out);
 
 const char* kg_last_error(void);

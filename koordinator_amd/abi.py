@@ -36,6 +36,9 @@ ABI_VERSION = 4
 MAX_RSV_SLOTS = 4
 RSV_POLICY = {"Default": 0, "Aligned": 1, "Restricted": 2}
 POD_RSV_AFFINITY = 1
+PROF_KINDS = 16
+PROF_NAMES = {0: "eval_round", 1: "merge_round", 2: "resolve_round", 3: "ds_max_round", 4: "ds_norm_reduce",
+              5: "rsv_eval", 6: "rsv_select", 7: "rsv_apply"}
 MAX_NUMA, MAX_CPUS = 4, 256
 QOS = {"": 0, "LSE": 1, "LSR": 2, "LS": 3, "BE": 4, "SYSTEM": 5}
 BIND = {"": 0, "Default": 1, "FullPCPUs": 2, "SpreadByPCPUs": 3, "ConstrainedBurst": 4}
@@ -79,7 +82,7 @@ CONFIG_DTYPE = np.dtype([
     _i64("ds_scoring_weights", 3),
     _i64("batch_pods"), _i64("pods_per_wave"), _i64("device_id"),
     _i64("reservation_filter"), _i64("reservation_score"), _i64("weight_reservation"),
-    _i64("reserved", 5),
+    _i64("pipeline_depth"), _i64("reserved", 4),
 ])
 
 NODE_DTYPE = np.dtype([
@@ -150,7 +153,7 @@ EXPORTED_SYMBOLS = (
     "kg_nodes_numa_upsert", "kg_nodes_read_numa", "kg_results_fetch_cpusets", "kg_pods_evaluate_numa",
     "kg_nodes_device_upsert", "kg_nodes_read_device", "kg_results_fetch_devices", "kg_pods_evaluate_device",
     "kg_quotas_set", "kg_quotas_read", "kg_nodes_reservation_upsert", "kg_nodes_read_reservations",
-    "kg_results_fetch_reservations",
+    "kg_results_fetch_reservations", "kg_profile_enable", "kg_profile_read",
 )
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
@@ -215,6 +218,8 @@ def load_library(path: str | None = None):
         "kg_nodes_reservation_upsert": (i, [vp, vp, vp, i64]),
         "kg_nodes_read_reservations": (i, [vp, vp, vp, vp]),
         "kg_results_fetch_reservations": (i, [vp, i64, i64, vp]),
+        "kg_profile_enable": (i, [vp, i]),
+        "kg_profile_read": (i, [vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)

@@ -507,26 +507,81 @@ __global__ __launch_bounds__(kMergeThreads) void merge_round(DevTable T, EvalPar
   KG_STAMP(1, 14);
 }
 
-// ---- round kernel 3: FIFO resolve --------------------------------------------------------------------
+// ---- round kernel 3: FIFO resolve (one wavefront, modified rows in registers) ---------------------------
 // One wavefront replays the round's pods [first, first + nb) in queue order against the merged candidates.
-// Prologue (one global-latency wait): the round's records (candidate keys, bound, hoisted rows of the best
-// candidates) and pod descriptors are copied HBM→LDS by LDS-DMA, and the rows the PREVIOUS round modified
-// (`prev_mod`, pipelined rounds: this round was evaluated on the table before they changed) are loaded as
-// modified lanes.  The per-pod loop then touches only LDS and registers.
-// Lane l < nM owns modified node l as a hoisted EvalRow kept current by assume_on (or, when the node was not
-// staged, a base Row plus the pods assumed since, materialised on first use).  Per pod:
-//   e     = the best candidate not modified (bitmap word prefetched one pod ahead, patched with the last winner);
-//   mbest = the exact re-score of the modified rows — skipped when the profile is monotone (assume never raises
-//           a node's key, and a mid-update row reads ≥ its current key) and e is the pod's top candidate;
-//   valid iff max(e, mbest) ≥ ub (every node outside the list scores lower); otherwise the round ends here and
-//   sets `poison`, so the rest of the batch (evaluated for later pods) is skipped until the host re-syncs.
-// Writes out_keys[first + j] (0 = unschedulable), the rows modified in this round back to the table and into
-// `my_mod` ([0] = count, then node ids), and advances the cursor ctl[0].
+// The "modified set" of pod j = every node assumed by an earlier pod of this round or by the n_prev rounds before
+// it that were still resolving when this round was evaluated (pipelining depth D: this round's eval read the table
+// right after resolve(r - D), so rows of rounds r-D+1 .. r-1 may have been read mid-update).  Modified rows live
+// in registers: slot s = bank·64 + lane holds node m[bank] as a hoisted EvalRow kept current by assume_on (two
+// banks: ≤ 128 rows).  Per pod j, for a monotone profile (Fit, LoadAware: an assume only lowers a node's key; a
+// row read as a mix of pre- and post-assume columns reads ≥ its current key):
+//   e     = the best listed candidate not modified (its key is exact);
+//   mbest = the exact re-score of every modified row — skipped when e is the pod's top candidate (every modified
+//           node then reads ≤ its listed key < e);
+//   best  = max(e, mbest) is the sequential answer when best ≥ ub (every unlisted node's key < ub).  Otherwise an
+//           unseen node could still win: the round ends before pod j and sets `poison` (the rest of the batch,
+//           evaluated for later pods, is skipped until the host restarts from the cursor).
+// The next pod's candidate keys, pod record and modified-bitmap word are prefetched while pod j resolves (the
+// prefetched word is patched with pod j's winner).  Rows of earlier rounds are loaded once, after the chain wait;
+// a node listed by two earlier rounds keeps its first slot (LDS hash), the duplicate becomes an infeasible hole.
+// Writes out_keys[first + j] (0 = unschedulable), the touched rows back to the table and into this round's
+// modified-row list (modlists[slot]), and advances the cursor ctl[0].
+constexpr int kMaxDepth = 4;          // pipelined rounds in flight (streams)
+constexpr int kMaxMod = 2 * kWave;    // modified-row slots: two register banks
+constexpr int kModHash = 512;         // node → slot hash for de-duplicating earlier rounds' lists
+constexpr int kModListStride = 1 + kMaxB;  // [count, node ids...] per round slot
+
+__device__ __forceinline__ uint32_t mod_hash(uint32_t node) { return (node * 2654435761u) >> (32 - 9); }
+static_assert(kModHash == 512, "hash width");
+
+// insert node → slot; returns the slot already holding node when present
+__device__ __forceinline__ int mod_insert(uint32_t* h, uint32_t node, int slot) {
+  const uint32_t v = ((node + 1u) << 8) | (uint32_t)slot;
+  uint32_t i = mod_hash(node);
+  for (int it = 0; it < kModHash; ++it) {
+    const uint32_t prev = atomicCAS(&h[i], 0u, v);
+    if (prev == 0u) return slot;
+    if ((prev >> 8) == node + 1u) return (int)(prev & 0xFFu);
+    i = (i + 1u) & (kModHash - 1);
+  }
+  return -1;
+}
+
+// End of a resolver: every store of this wave visible device-wide, then ctl[4] = seq (agent-scope release) for
+// the next round's resolver, which may already be resident on another round stream.
+__device__ __forceinline__ void publish_round(int64_t* ctl, int64_t seq) {
+  __threadfence();
+  if (threadIdx.x == 0) __hip_atomic_store(&ctl[4], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// exact key of one modified row for pod p (0 = filtered out)
+template <int PF>
+__device__ __forceinline__ uint64_t mod_key(const EvalRow& er, uint32_t node, const DevPod& p, const EvalParams& P) {
+  uint32_t t = 0;
+  bool rare = false;
+  bool ok = eval_fast<PF>(er, p, P, t, rare);
+  if (rare) {
+    int64_t t64 = 0;
+    ok = eval_node(row_of(er), p, P, t64);
+    t = (uint32_t)t64;
+  }
+  return ok ? make_key(t, node) : 0;
+}
+
+__device__ __forceinline__ EvalRow lds_row(const uint64_t* src) {
+  uint64_t w[kEvalRowWords];
+#pragma unroll
+  for (int q = 0; q < kEvalRowWords; ++q) w[q] = src[q];
+  EvalRow er;
+  __builtin_memcpy(&er, w, sizeof(er));
+  return er;
+}
+
+// Σ of the pods assumed onto a row since its base state (NodeInfo.AddPod + podAssignCache.assign terms)
 struct PodDelta {
   int64_t req_cpu, req_mem, nz_cpu, nz_mem, est_cpu, est_mem, pest_cpu, pest_mem;
   int32_t pods;
 };
-
 __device__ __forceinline__ void add_delta(PodDelta& d, const DevPod& p) {
   const int64_t prod = (p.flags & P_PROD) ? 1 : 0;
   d.req_cpu += p.req_cpu;
@@ -539,7 +594,6 @@ __device__ __forceinline__ void add_delta(PodDelta& d, const DevPod& p) {
   d.pest_mem += prod * p.est_mem;
   d.pods += 1;
 }
-
 __device__ __forceinline__ Row with_delta(Row r, const PodDelta& d) {
   r.req_cpu += d.req_cpu;
   r.req_mem += d.req_mem;
@@ -553,21 +607,101 @@ __device__ __forceinline__ Row with_delta(Row r, const PodDelta& d) {
   return r;
 }
 
-__device__ __forceinline__ EvalRow staged_row(const uint64_t* s_cand, int slot) {
-  const uint64_t* src = s_cand + (size_t)(slot / kStaged) * kCandStride + kRecRows + (slot % kStaged) * kEvalRowWords;
-  uint64_t words[kEvalRowWords];
-#pragma unroll
-  for (int q = 0; q < kEvalRowWords; ++q) words[q] = src[q];
+// One modified row held by a lane: its hoisted EvalRow (from a merge record's shipped rows, or converted from HBM)
+// + the pods assumed since it was last brought up to date.  The assume on the serial chain is a few adds into
+// `dl`; the row absorbs them (apply_delta) only when a later pod has to re-score it.
+constexpr uint32_t kNoNode = 0xFFFFFFFFu;
+struct LaneRow {
+  uint32_t node;
+  bool pending, touched;
   EvalRow er;
-  __builtin_memcpy(&er, words, sizeof(er));
-  return er;
+  PodDelta dl;   // assumed since `er` was last brought up to date
+  PodDelta tot;  // assumed in this round (written back exactly: int64 adds onto the table columns)
+};
+__device__ __forceinline__ void lane_row_init(LaneRow& L) {
+  L.node = kNoNode;
+  L.pending = false;
+  L.touched = false;
+  L.er.flags = 0;
+  L.dl = PodDelta{};
+  L.tot = PodDelta{};
+}
+// assume of Σ dl on a hoisted row: the free terms drop (capacities and reciprocals unchanged), so the exact domain
+// of eval_fast can only be left through the lower bounds of the free terms the profile scores
+__device__ __forceinline__ void apply_delta(EvalRow& e, const PodDelta& d, const EvalParams& P) {
+  e.free_cpu -= d.req_cpu;
+  e.free_mem -= d.req_mem;
+  e.fnz_cpu -= d.nz_cpu;
+  e.fnz_mem -= (double)d.nz_mem;
+  e.la_free_cpu -= d.est_cpu;
+  e.la_free_mem -= (double)d.est_mem;
+  e.la_pfree_cpu -= d.pest_cpu;
+  e.la_pfree_mem -= (double)d.pest_mem;
+  e.pods_left -= d.pods;
+  bool out = false;
+  if (P.fit_score) out |= (P.fit_w_cpu && e.fnz_cpu < kCpuFreeMin) | (P.fit_w_mem && !(e.fnz_mem > (double)kMemFreeMin));
+  if (P.la_score && (e.flags & F_LA_SCORE)) {
+    out |= P.la_w_cpu && (e.la_free_cpu < kCpuFreeMin || e.la_pfree_cpu < kCpuFreeMin);
+    out |= P.la_w_mem && (!(e.la_free_mem > (double)kMemFreeMin) || !(e.la_pfree_mem > (double)kMemFreeMin));
+  }
+  if (out) e.flags |= F_RARE;
+}
+// a new modified row for winner w of pod j, listed at position pos of its record
+__device__ __forceinline__ void lane_row_new(LaneRow& L, const DevTable& T, const uint64_t* s_cand, uint32_t w, int j,
+                                             int pos, const DevPod& p, const EvalParams& P) {
+  L.node = w;
+  if (pos < kStaged) L.er = lds_row(s_cand + (size_t)j * kCandStride + kRecRows + pos * kEvalRowWords);
+  else L.er = make_eval_row(load_row(T, w), P);  // beyond the shipped rows (rare): HBM
+  L.dl = PodDelta{};
+  add_delta(L.dl, p);
+  L.tot = L.dl;
+  L.pending = true;
+  L.touched = true;
+}
+__device__ __forceinline__ void lane_row_assume(LaneRow& L, const DevPod& p) {
+  add_delta(L.dl, p);
+  add_delta(L.tot, p);
+  L.pending = true;
+  L.touched = true;
+}
+// write-back of a touched row: this round's Σ onto the table columns (no other writer: the earlier rounds'
+// resolvers are done, later rounds' resolvers wait for this one; concurrent wide passes read mixed columns)
+__device__ __forceinline__ void lane_row_store(const LaneRow& L, const DevTable& T) {
+  if (!L.touched) return;
+  const int64_t i = L.node;
+  auto add = [](int64_t* a, int64_t v) { atomicAdd(reinterpret_cast<unsigned long long*>(a), (unsigned long long)v); };
+  add(&T.req_cpu[i], L.tot.req_cpu);
+  add(&T.req_mem[i], L.tot.req_mem);
+  add(&T.nz_cpu[i], L.tot.nz_cpu);
+  add(&T.nz_mem[i], L.tot.nz_mem);
+  add(&T.la_used_cpu[i], L.tot.est_cpu);
+  add(&T.la_used_mem[i], L.tot.est_mem);
+  add(&T.la_pused_cpu[i], L.tot.pest_cpu);
+  add(&T.la_pused_mem[i], L.tot.pest_mem);
+  atomicAdd(&T.num_pods[i], L.tot.pods);
+}
+__device__ __forceinline__ void lane_row_sync(LaneRow& L, const EvalParams& P) {
+  if (L.pending) {
+    apply_delta(L.er, L.dl, P);
+    L.dl = PodDelta{};
+    L.pending = false;
+  }
+}
+template <int PF>
+__device__ __forceinline__ uint64_t lane_row_key(LaneRow& L, const DevPod& p, const EvalParams& P) {
+  if (L.node == kNoNode) return 0;
+  lane_row_sync(L, P);
+  return mod_key<PF>(L.er, L.node, p, P);
 }
 
-// End of a resolver: every store of this wave visible device-wide, then ctl[4] = seq (agent-scope release) for
-// the next round's resolver, which may already be resident on the other round stream.
-__device__ __forceinline__ void publish_round(int64_t* ctl, int64_t seq) {
-  __threadfence();
-  if (threadIdx.x == 0) __hip_atomic_store(&ctl[4], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+// wave max of packed keys: one 32-bit DPP max when (score, node) fit 13 + 19 bits, else the two-word form
+__device__ __forceinline__ uint64_t wave_max_modkey(uint64_t k, bool narrow) {
+  if (narrow) {
+    const uint32_t k32 = k ? (uint32_t)((k >> 32) << 19) | (0x7FFFFu - key_node(k)) : 0u;
+    const uint32_t m = wave_max_u32(k32);
+    return m ? make_key((int64_t)(m >> 19), 0x7FFFFu - (m & 0x7FFFFu)) : 0;
+  }
+  return wave_max_key(k);
 }
 
 template <int PF, bool QUOTA>
@@ -575,9 +709,9 @@ __global__ __launch_bounds__(kWave) void resolve_round(DevTable T, const DevPod*
                                                         int64_t* __restrict__ ctl, int64_t first, int nb,
                                                         const uint64_t* __restrict__ cand, EvalParams P,
                                                         uint64_t* __restrict__ out_keys, int bitmap_words,
-                                                        const int32_t* __restrict__ prev_mod,
-                                                        int32_t* __restrict__ my_mod, int32_t* __restrict__ poison,
-                                                        int64_t seq, int wait, DevQuota* __restrict__ quotas, int nq) {
+                                                        int32_t* __restrict__ modlists, int slot, int depth,
+                                                        int n_prev, int32_t* __restrict__ poison, int64_t seq,
+                                                        int wait, DevQuota* __restrict__ quotas, int nq) {
   extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
   KG_STAMP(2, 0);
   const int lane = threadIdx.x;
@@ -585,9 +719,11 @@ __global__ __launch_bounds__(kWave) void resolve_round(DevTable T, const DevPod*
   __builtin_amdgcn_s_setprio(3);
   uint64_t* s_cand = smem;                                            // [nb][kCandStride]
   uint64_t* s_podw = s_cand + (size_t)nb * kCandStride;               // [nb] DevPod (kPodWords words)
-  uint32_t* bitmap = reinterpret_cast<uint32_t*>(s_podw + (size_t)nb * kPodWords);
+  uint32_t* s_hash = reinterpret_cast<uint32_t*>(s_podw + (size_t)nb * kPodWords);  // [kModHash]
+  uint32_t* s_prevn = s_hash + kModHash;                              // [kMaxMod] earlier rounds' nodes
+  uint32_t* bitmap = s_prevn + kMaxMod;                               // [bitmap_words]
   {  // prologue, independent of the previous round: LDS-DMA of this round's records (merged on this stream)
-     // + pods, bitmap clear (16-B stores)
+     // + pods, bitmap / hash clears (16-B stores)
     const int n16 = nb * kCandStride / 2;
     for (int it = 0; it * kWave < n16; ++it) {
       const int idx = it * kWave + lane;
@@ -606,8 +742,10 @@ __global__ __launch_bounds__(kWave) void resolve_round(DevTable T, const DevPod*
     uint4* b4 = reinterpret_cast<uint4*>(bitmap);
     for (int w = lane; w < bitmap_words / 4; w += kWave) b4[w] = make_uint4(0, 0, 0, 0);
     for (int w = (bitmap_words / 4) * 4 + lane; w < bitmap_words; w += kWave) bitmap[w] = 0;
+    uint4* h4 = reinterpret_cast<uint4*>(s_hash);
+    for (int w = lane; w < kModHash / 4; w += kWave) h4[w] = make_uint4(0, 0, 0, 0);
   }
-  // Chain on the previous round's resolver (the other round stream): its rows, cursor, poison and modified-row
+  // Chain on the previous round's resolver (another round stream): its rows, cursor, poison and modified-row
   // list are published with an agent-scope release of ctl[4] = its sequence number.  Bounded spin: a missing
   // predecessor reports an error instead of hanging the device.
   int timed_out = 0;
@@ -615,7 +753,7 @@ __global__ __launch_bounds__(kWave) void resolve_round(DevTable T, const DevPod*
     if (lane == 0) {
       int64_t it = 0;
       while (__hip_atomic_load(&ctl[4], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < seq - 1) {
-        __builtin_amdgcn_s_sleep(2);
+        __builtin_amdgcn_s_sleep(1);
         if (++it > kSpinLimit) {
           timed_out = 1;
           break;
@@ -625,60 +763,59 @@ __global__ __launch_bounds__(kWave) void resolve_round(DevTable T, const DevPod*
     timed_out = __builtin_amdgcn_readfirstlane(timed_out);
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   }
+  KG_STAMP(2, 1);
   if (timed_out || *poison || ctl[0] != first) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the LDS-DMA lands before the wave retires
     if (lane == 0 && timed_out) ctl[5] = 1;
     publish_round(ctl, seq);
     return;
   }
-  // previous round's modified rows (exact current state: the previous resolver wrote them back)
-  const int n_prev = prev_mod ? prev_mod[0] : 0;
-  uint32_t midx = 0xFFFFFFFFu;
-  Row mrow;
-  mrow.flags = 0;
-  if (lane < n_prev) {
-    midx = (uint32_t)prev_mod[1 + lane];
-    mrow = load_row(T, midx);
+  // rows the n_prev previous rounds modified: slots [0, nM) of the register banks (slot s: lane s % 64, bank s / 64)
+  LaneRow R0, R1;
+  lane_row_init(R0);
+  lane_row_init(R1);
+  int nM = 0;
+  for (int d = 1; d <= n_prev; ++d) {  // concatenate the lists in LDS, then slot s → lane s % 64, bank s / 64
+    const int32_t* ml = modlists + (size_t)(((slot - d) % depth + depth) % depth) * kModListStride;
+    const int c = ml[0];
+    for (int t = lane; t < c; t += kWave) s_prevn[nM + t] = (uint32_t)ml[1 + t];
+    nM += c;
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (lane < n_prev) atomicOr(&bitmap[midx >> 5], 1u << (midx & 31));
+  if (lane < nM) {
+    const uint32_t node = s_prevn[lane];
+    if (mod_insert(s_hash, node, lane) == lane) {
+      R0.node = node;
+      R0.er = make_eval_row(load_row(T, node), P);
+      atomicOr(&bitmap[node >> 5], 1u << (node & 31));
+    }
+  }
+  if (kWave + lane < nM) {
+    const uint32_t node = s_prevn[kWave + lane];
+    if (mod_insert(s_hash, node, kWave + lane) == kWave + lane) {
+      R1.node = node;
+      R1.er = make_eval_row(load_row(T, node), P);
+      atomicOr(&bitmap[node >> 5], 1u << (node & 31));
+    }
+  }
+  const bool narrow = P.score_bits <= 13;  // packed keys fit 32 bits (node < 2^19 = kMaxNodes)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // LDS-DMA of records and pods (+ the rows above)
   __syncthreads();
   // ElasticQuota table (QUOTA instantiation only), after the chain wait: the previous resolver's charges are visible
   DevQuota ql = QUOTA ? quota_load(quotas, nq, lane) : DevQuota{0, 0, 0, 0, 0, 0, 0, 0};
-  KG_STAMP(2, 1);
-  // staged[q] on lane l: node whose hoisted row sits at staged slot s = q·64 + l (record s / kStaged,
-  // position s % kStaged of that pod's list)
-  constexpr int kSlotsPerLane = (kStaged * kMaxB + kWave - 1) / kWave;
-  uint32_t staged[kSlotsPerLane];
-#pragma unroll
-  for (int q = 0; q < kSlotsPerLane; ++q) {
-    const int sl = q * kWave + lane;
-    staged[q] = 0xFFFFFFFFu;
-    if (sl < kStaged * nb) {
-      const uint64_t kk = s_cand[(size_t)(sl / kStaged) * kCandStride + (sl % kStaged)];
-      staged[q] = kk ? key_node(kk) : 0xFFFFFFFFu;
-    }
-  }
+  KG_STAMP(2, 2);
   const DevPod* s_pods = reinterpret_cast<const DevPod*>(s_podw);
-
-  // lane state (lane < nM): rsrc ≥ 0 → base hoisted row at staged slot rsrc (LDS), rsrc == -1 → base Row `mrow`;
-  // `dl` = pods assumed since the base; `er` = materialised current row when er_valid; `touched` = modified
-  // in this round (written back at the end)
-  int rsrc = -1;
-  EvalRow er;
-  er.flags = 0;
-  bool er_valid = false, touched = false;
-  PodDelta dl = {};
   uint64_t my_out = 0;
-  int nM = n_prev;
-  int consumed = 0;
-  uint32_t last_w = 0xFFFFFFFFu;
+  int consumed = 0, n_slow = 0;
+  uint32_t last_w = kNoNode;
   uint64_t key_n = s_cand[lane];
   uint64_t ub_n = s_cand[kC];
   DevPod p_n = s_pods[0];
   uint32_t word_n = bitmap[key_n ? key_node(key_n) >> 5 : 0u];
+  uint32_t diag = 0;
   for (int j = 0; j < nb; ++j) {
+    KG_POD_DIAG(j, diag);
+    diag = 0;
     const uint64_t key = key_n, ub = ub_n;
     const DevPod p = p_n;
     const uint32_t word = word_n;
@@ -693,85 +830,78 @@ __global__ __launch_bounds__(kWave) void resolve_round(DevTable T, const DevPod*
     if (QUOTA && !quota_admit(ql, p)) {  // ElasticQuota PreFilter rejects: Unschedulable, no node search
       my_out = lane == j ? 0 : my_out;
       ++consumed;
-      last_w = 0xFFFFFFFFu;
+      last_w = kNoNode;
       continue;
     }
     const uint64_t um = __ballot(unmod);
     const int pos = um ? (int)__builtin_ctzll(um) : kC;
-    const uint64_t e = um ? readlane_u64(key, pos) : 0;
-    uint64_t best = e;
-    if (nM > 0 && (!P.monotone || pos > 0)) {  // slow path: re-score the modified rows
-      uint64_t mk = 0;
-      if (lane < nM) {
-        if (!er_valid) {  // materialise: staged hoisted row (LDS) or the base Row, plus the pods assumed since
-          er = make_eval_row(with_delta(rsrc >= 0 ? row_of(staged_row(s_cand, rsrc)) : mrow, dl), P);
-          er_valid = true;
-        }
-        uint32_t t = 0;
-        bool rare = false;
-        bool ok = eval_fast<PF>(er, p, P, t, rare);
-        if (rare) {
-          int64_t t64 = 0;
-          ok = eval_node(row_of(er), p, P, t64);
-          t = (uint32_t)t64;
-        }
-        mk = ok ? make_key(t, midx) : 0;
+    uint64_t best = um ? readlane_u64(key, pos) : 0;
+    diag = (uint32_t)pos << 8;
+    if (nM > 0 && pos > 0) {  // a modified node is listed above e: re-score the modified rows exactly
+      ++n_slow;
+      diag |= 1;
+      // only the modified nodes listed above e can beat it (a modified node reads ≤ its listed key; unlisted < ub):
+      // lanes whose row is one of the candidates at positions < pos re-score it, the others sit out
+      bool a0 = false, a1 = false;
+      for (int q = 0; q < pos; ++q) {
+        const uint32_t c = key_node(readlane_u64(key, q));
+        a0 |= R0.node == c;
+        a1 |= R1.node == c;
       }
-      const uint64_t mbest = wave_max_key(mk);
+      uint64_t mk = 0;
+      if (__ballot(a0)) mk = a0 ? lane_row_key<PF>(R0, p, P) : 0;
+      if (__ballot(a1)) {
+        const uint64_t k1 = a1 ? lane_row_key<PF>(R1, p, P) : 0;
+        mk = k1 > mk ? k1 : mk;
+      }
+      const uint64_t mbest = wave_max_modkey(mk, narrow);
       best = mbest > best ? mbest : best;
     }
     if (best < ub) break;  // an unseen node could still win: leave this pod to the next round
     my_out = lane == j ? best : my_out;
     ++consumed;
     if (best == 0) {  // unschedulable (ub == 0: no feasible node anywhere)
-      last_w = 0xFFFFFFFFu;
+      last_w = kNoNode;
       continue;
     }
     const uint32_t w = key_node(best);
     last_w = w;
-    const uint64_t hit = __ballot((lane < nM) & (midx == w));
-    const int owner = hit ? (int)__builtin_ctzll(hit) : nM;
-    const bool me = lane == owner;
-    if (!hit) {
-      int sl = -1;
-#pragma unroll
-      for (int q = 0; q < kSlotsPerLane; ++q) {
-        const uint64_t b = __ballot(staged[q] == w);
-        if (sl < 0 && b) sl = q * kWave + (int)__builtin_ctzll(b);
+    const uint64_t h0 = __ballot(R0.node == w), h1 = __ballot(R1.node == w);
+    if (h0 | h1) {  // assume onto the modified row: NodeInfo.AddPod + LoadAware Reserve (podAssignCache.assign)
+      if (h0) {
+        if (lane == (int)__builtin_ctzll(h0)) lane_row_assume(R0, p);
+      } else if (lane == (int)__builtin_ctzll(h1)) {
+        lane_row_assume(R1, p);
       }
-      if (me) {
-        midx = w;
-        rsrc = sl;
-        dl = PodDelta{};
-        er_valid = false;
-        if (sl < 0) mrow = load_row(T, w);  // not staged (rare): HBM load, consumed lazily
+    } else {  // w = e, unmodified: a new slot based on its row shipped in the record (HBM beyond the staged rows)
+      diag |= 2;
+      const int s = nM++;
+      if (lane == (s & (kWave - 1))) {
+        if (s < kWave) lane_row_new(R0, T, s_cand, w, j, pos, p, P);
+        else lane_row_new(R1, T, s_cand, w, j, pos, p, P);
+        atomicOr(&bitmap[w >> 5], 1u << (w & 31));
       }
-      if (lane == 0) atomicOr(&bitmap[w >> 5], 1u << (w & 31));
-      ++nM;
-    }
-    if (me) {  // assume the pod on the owner's row (the delta only matters while the row is not materialised)
-      if (er_valid) assume_on(er, p, P);
-      else add_delta(dl, p);
-      touched = true;
     }
     if (QUOTA) quota_charge(ql, p, lane);  // ElasticQuota Reserve
-    if (j == 0 || j == 15 || j == 31) KG_STAMP(2, 2 + j / 8);
   }
-  if (touched) {
-    if (er_valid) store_eval_row(T, midx, er);
-    else store_mutable(T, midx, with_delta(rsrc >= 0 ? row_of(staged_row(s_cand, rsrc)) : mrow, dl));
-  }
-  const uint64_t tm = __ballot(touched);
+  KG_STAMP(2, 30);
+  KG_POD_DIAG(consumed, diag);
+  // write-back of the touched rows + this round's modified-row list
+  lane_row_store(R0, T);
+  lane_row_store(R1, T);
+  int32_t* my_mod = modlists + (size_t)slot * kModListStride;
   const uint64_t lane_lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  if (touched) my_mod[1 + __popcll(tm & lane_lt)] = (int32_t)midx;
+  const uint64_t b0 = __ballot(R0.touched), b1 = __ballot(R1.touched);
+  if (R0.touched) my_mod[1 + __popcll(b0 & lane_lt)] = (int32_t)R0.node;
+  if (R1.touched) my_mod[1 + __popcll(b0) + __popcll(b1 & lane_lt)] = (int32_t)R1.node;
   if (lane < consumed) out_keys[first + lane] = my_out;
   if (QUOTA && lane < nq) quotas[lane] = ql;
-  KG_STAMP(2, 30);
   if (lane == 0) {
-    my_mod[0] = __popcll(tm);
+    my_mod[0] = __popcll(b0) + __popcll(b1);
     ctl[0] = first + consumed;
     ctl[1] += 1;
     ctl[2] += consumed;
+    ctl[6] += n_slow;  // diagnostics: pods that re-scored modified rows
     if (consumed < nb) *poison = 1;
   }
   publish_round(ctl, seq);
@@ -1578,17 +1708,17 @@ struct kg_engine {
   DevBuf<int32_t> cols32;
   DevBuf<DevPod> pods;
   int64_t n_staged = 0;
-  DevBuf<uint64_t> lists;     // [2][B][nt_local][kR] tile candidate lists (this rank), by round parity
-  DevBuf<uint64_t> gathered;  // [2][n_ranks][B][kCandStride] per-rank merged records (n_ranks > 1), by round parity
-  DevBuf<uint64_t> cand;      // [2][B][kCandStride] final merged candidates, by round parity
+  DevBuf<uint64_t> lists;     // [D][B][nt_local][kR] tile candidate lists (this rank), by round slot r % D
+  DevBuf<uint64_t> gathered;  // [D][n_ranks][B][kCandStride] per-rank merged records (n_ranks > 1), by round slot
+  DevBuf<uint64_t> cand;      // [D][B][kCandStride] final merged candidates, by round slot
   DevBuf<uint64_t> out_keys;
   DevBuf<int64_t> cursor;     // [0] cursor, [1] rounds, [2] consumed, [3] poison (int32 in its low word),
                               // [4] last published resolver sequence, [5] device error (chain wait timed out)
-  DevBuf<int32_t> modlists;   // [2][1 + kMaxB]: rows each round modified ([0] = count), by round parity
-  // round r runs on rs[r & 1] (eval → merge → [RCCL on comms[r & 1]] → resolve); `stream` runs ingest
-  hipStream_t rs[2] = {nullptr, nullptr};
-  ncclComm_t comm2 = nullptr;
-  hipEvent_t ev_res[2] = {nullptr, nullptr};
+  DevBuf<int32_t> modlists;   // [kMaxDepth][kModListStride]: rows each round modified ([0] = count), by round slot
+  // round r runs on rs[r % D] (eval → merge → [RCCL on comms[r % D]] → resolve); `stream` runs ingest
+  hipStream_t rs[kMaxDepth] = {};
+  ncclComm_t comms[kMaxDepth] = {};  // comms[0] = comm; one communicator per round stream
+  hipEvent_t ev_res[kMaxDepth] = {};
   DevBuf<RowDelta> deltas;
   DevBuf<int64_t> scratch64;
   DevBuf<int32_t> scratch32;
@@ -1625,9 +1755,51 @@ struct kg_engine {
   DevBuf<uint64_t> rsv_val;     // [capacity] packed per-node pass-1 values
   DevBuf<unsigned long long> rsv_ws;  // [4]: [3] = pod cursor
   DevBuf<uint64_t> rsv_part;    // [3][blocks] per-block partials (preferred-node key, max raw, max key)
+  // live kernel timing (kg_profile_enable): HIP event pairs around every launch of the round runners, on the
+  // launch's own stream, folded into per-kind totals after each batch synchronises
+  bool prof_on = false;
+  std::vector<hipEvent_t> prof_pool;
+  size_t prof_used = 0;
+  struct ProfRec {
+    int kind;
+    size_t a, b;  // prof_pool indices of the begin / end events
+  };
+  std::vector<ProfRec> prof_recs;
+  double prof_ms[KG_PROF_KINDS] = {};
+  int64_t prof_n[KG_PROF_KINDS] = {};
 };
 
 namespace {
+
+// ---- live kernel timing (kg_profile_enable) ----
+constexpr size_t kNoProf = ~size_t(0);
+size_t prof_mark(kg_engine* e, hipStream_t st) {
+  if (e->prof_used == e->prof_pool.size()) {
+    hipEvent_t ev = nullptr;
+    if (hipEventCreate(&ev) != hipSuccess) return kNoProf;
+    e->prof_pool.push_back(ev);
+  }
+  const size_t i = e->prof_used++;
+  return hipEventRecord(e->prof_pool[i], st) == hipSuccess ? i : kNoProf;
+}
+size_t prof_begin(kg_engine* e, hipStream_t st) { return e->prof_on ? prof_mark(e, st) : kNoProf; }
+void prof_end(kg_engine* e, int kind, size_t a, hipStream_t st) {
+  if (a == kNoProf) return;
+  const size_t b = prof_mark(e, st);
+  if (b != kNoProf) e->prof_recs.push_back({kind, a, b});
+}
+// after the streams of the recorded launches have synchronised
+int prof_collect(kg_engine* e) {
+  for (const auto& r : e->prof_recs) {
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, e->prof_pool[r.a], e->prof_pool[r.b]));
+    e->prof_ms[r.kind] += ms;
+    e->prof_n[r.kind] += 1;
+  }
+  e->prof_recs.clear();
+  e->prof_used = 0;
+  return 0;
+}
 
 int validate_config(const kg_config* c) {
   if (!c) return fail(KG_E_INVALID, "config is NULL");
@@ -2031,7 +2203,7 @@ void usage_for_score(const kg_node_metric& m, int64_t u[2]) {
 struct RoundGeom {
   int64_t N, shard, base, n_local;
   int nt_local, B, ppw, bitmap_words;
-  bool pipelined;  // eval(r+1) overlaps resolve(r): needs ≤ 2B-1 modified rows per round within one wave (B ≤ 32)
+  int depth;  // rounds in flight: eval(r) reads the table right after resolve(r - depth) (1 = unpipelined)
 };
 
 RoundGeom geometry(const kg_engine* e) {
@@ -2044,15 +2216,21 @@ RoundGeom geometry(const kg_engine* e) {
   g.B = (int)(e->cfg.batch_pods > 0 ? e->cfg.batch_pods : 32);
   g.ppw = (int)(e->cfg.pods_per_wave > 0 ? std::min<int64_t>(e->cfg.pods_per_wave, g.B) : 8);
   g.bitmap_words = (int)(((std::max<int64_t>(g.N, 1) + 127) / 128) * 4);  // whole 16-B stores
-  g.pipelined = 2 * g.B - 1 <= kWave && e->P.monotone;
+  // pipelining needs the monotone profile (a row read mid-update reads ≥ its current key) and depth·B modified-row
+  // slots in the resolver; several ranks keep one communicator per round stream
+  int d = (int)(e->cfg.pipeline_depth > 0 ? e->cfg.pipeline_depth : 2);
+  d = std::min(d, kMaxDepth);
+  while (d > 1 && d * g.B > kMaxMod) --d;
+  g.depth = e->P.monotone ? d : 1;
   if (e->numa_on) g.ppw = std::min(g.ppw, kNumaPpw);  // eval_round_numa parks ≤ kNumaPpw pods' values in LDS
   if (e->ds_on) g.ppw = std::min(g.ppw, kDsPpw);      // the DeviceShare passes keep ≤ kDsPpw pods in registers
   return g;
 }
 
 size_t resolve_lds_bytes(const RoundGeom& g, int nb) {
-  return ((size_t)nb * kCandStride + (size_t)nb * kPodWords) * 8 + (size_t)g.bitmap_words * 4;
+  return (size_t)nb * (kCandStride + kPodWords) * 8 + (size_t)(kModHash + kMaxMod) * 4 + (size_t)g.bitmap_words * 4;
 }
+constexpr size_t kMaxLds = 160 * 1024;
 size_t resolve_numa_lds_bytes(const RoundGeom& g, int nb) {
   return ((size_t)nb * (kCandStride + kPodWords + kNumaPodWords) + (size_t)kWave * (kNumaStaticWords + kNumaMutWords)) * 8 +
          (size_t)g.bitmap_words * 4;
@@ -2118,7 +2296,7 @@ void launch_merge_ranks(kg_engine* e, const RoundGeom& g, int nb, int slot, hipS
                                                   cand_slot(e, g, slot));
 }
 
-void launch_resolve(kg_engine* e, const RoundGeom& g, int64_t first, int nb, int prev_slot, int slot,
+void launch_resolve(kg_engine* e, const RoundGeom& g, int64_t first, int nb, int slot, int n_prev,
                     int64_t seq, int wait, hipStream_t st) {
   if (e->numa_on) {
     resolve_round_numa<<<1, kWave, resolve_numa_lds_bytes(g, nb), st>>>(e->T, numa_table(e), e->pods.p, e->npods.p,
@@ -2128,13 +2306,12 @@ void launch_resolve(kg_engine* e, const RoundGeom& g, int64_t first, int nb, int
                                                                         e->nq);
     return;
   }
-  const int32_t* prev = prev_slot >= 0 ? e->modlists.p + (size_t)prev_slot * (1 + kMaxB) : nullptr;
-  int32_t* mine = e->modlists.p + (size_t)slot * (1 + kMaxB);
 #define KG_RESOLVE_T(X, Q)                                                                                       \
   resolve_round<X, Q><<<1, kWave, resolve_lds_bytes(g, nb), st>>>(e->T, e->pods.p, e->cursor.p, first, nb,           \
                                                                   cand_slot(e, g, slot), e->P, e->out_keys.p,       \
-                                                                  g.bitmap_words, prev, mine, poison_ptr(e), seq,   \
-                                                                  wait, e->quotas.p, e->nq)
+                                                                  g.bitmap_words, e->modlists.p, slot, g.depth,     \
+                                                                  n_prev, poison_ptr(e), seq, wait, e->quotas.p,    \
+                                                                  e->nq)
 #define KG_RESOLVE(X) KG_RESOLVE_T(X, false)
 #define KG_RESOLVE_Q(X) KG_RESOLVE_T(X, true)
   if (e->nq > 0) {
@@ -2154,42 +2331,47 @@ int launch_merge(kg_engine* e, const RoundGeom& g, int nb, int slot, hipStream_t
   if (e->n_ranks > 1) {
     const size_t cnt = (size_t)g.B * kCandStride;
     uint64_t* all = gathered_slot(e, g, slot);
-    NCCL_TRY(ncclAllGather(all + (size_t)e->rank * cnt, all, cnt, ncclUint64, slot ? e->comm2 : e->comm, st));
+    NCCL_TRY(ncclAllGather(all + (size_t)e->rank * cnt, all, cnt, ncclUint64, e->comms[slot], st));
     launch_merge_ranks(e, g, nb, slot, st);
     HIP_TRY(hipGetLastError());
   }
   return 0;
 }
 
-// One batch of rounds over pods [cur, end).  Round r runs on stream rs[r & 1]: eval(r) → merge(r) →
-// [RCCL all-gather on that stream's communicator] → resolve(r), the resolve waiting on resolve(r-1) (the
-// other stream).  Stream order makes eval(r) start right after resolve(r-2), so it overlaps resolve(r-1)
-// (the pipelined protocol: round r-1's rows are modified lanes of resolve(r)); merge(r) also runs off the
-// serial resolve chain.  Unpipelined geometries (B > 32) put every round on rs[0].  The first round of a
-// batch starts from a fully written table (the host synchronised), so it has no previous-round rows.
+// One batch of rounds over pods [cur, end).  Round r runs on stream rs[r % D]: eval(r) → merge(r) →
+// [RCCL all-gather on that stream's communicator] → resolve(r), the resolve waiting on resolve(r-1) (another
+// stream) through the device sequence word, so its launch and prologue overlap the previous resolver instead of
+// waiting on a cross-stream event.  Stream order makes eval(r) start right after resolve(r-D): it overlaps
+// resolve(r-D+1 .. r-1), whose rows resolve(r) treats as modified; merge(r) also runs off the
+// serial chain.  The first round of a batch starts from a fully written table (the host synchronised), so it has
+// no previous-round rows.
 int run_batch(kg_engine* e, const RoundGeom& g, int64_t cur, int64_t end, int64_t n_rounds) {
+  const int D = g.depth;
   HIP_TRY(hipMemsetAsync(e->cursor.p + 3, 0, 3 * 8, e->rs[0]));  // poison, resolver sequence, device error
-  if (g.pipelined) {  // rs[1] must not start round 1 before that reset
-    HIP_TRY(hipEventRecord(e->ev_res[1], e->rs[0]));
-    HIP_TRY(hipStreamWaitEvent(e->rs[1], e->ev_res[1], 0));
+  if (D > 1) {  // the other round streams must not start before that reset
+    HIP_TRY(hipEventRecord(e->ev_res[0], e->rs[0]));
+    for (int k = 1; k < D; ++k) HIP_TRY(hipStreamWaitEvent(e->rs[k], e->ev_res[0], 0));
   }
   for (int64_t r = 0; r < n_rounds; ++r) {
     const int64_t first = cur + r * g.B;
     const int nb = (int)std::min<int64_t>(g.B, end - first);
-    const int slot = (int)(r & 1);
-    hipStream_t st = g.pipelined ? e->rs[slot] : e->rs[0];
+    const int slot = (int)(r % D);
+    hipStream_t st = e->rs[slot];
+    size_t t = prof_begin(e, st);
     launch_eval(e, g, first, nb, slot, st);
     HIP_TRY(hipGetLastError());
+    prof_end(e, KG_PROF_EVAL, t, st);
+    t = prof_begin(e, st);
     if (int rc = launch_merge(e, g, nb, slot, st)) return rc;
-    // pipelined: resolve(r) chains on resolve(r-1) through the device sequence word (resolve_round), so its
-    // launch and prologue overlap the previous resolver instead of waiting for a cross-stream event
-    const int prev_slot = (g.pipelined && r > 0) ? (int)((r - 1) & 1) : -1;
-    launch_resolve(e, g, first, nb, prev_slot, slot, r + 1, g.pipelined && r > 0, st);
+    prof_end(e, KG_PROF_MERGE, t, st);
+    const int n_prev = (int)std::min<int64_t>(r, D - 1);
+    t = prof_begin(e, st);
+    launch_resolve(e, g, first, nb, slot, n_prev, r + 1, D > 1 && r > 0, st);
     HIP_TRY(hipGetLastError());
+    prof_end(e, KG_PROF_RESOLVE, t, st);
   }
-  HIP_TRY(hipStreamSynchronize(e->rs[0]));
-  HIP_TRY(hipStreamSynchronize(e->rs[1]));
-  return 0;
+  for (int k = 0; k < D; ++k) HIP_TRY(hipStreamSynchronize(e->rs[k]));
+  return prof_collect(e);
 }
 
 // ---- DeviceShare rounds: cursor-driven, unpipelined, all on rs[0] ----
@@ -2201,25 +2383,41 @@ size_t resolve_ds_lds_bytes(const RoundGeom& g, int nb) {
 void launch_round_ds(kg_engine* e, const RoundGeom& g, int64_t end, hipStream_t st, int which = -1) {
   const DsTable DT{e->ds_d.p};
   const dim3 grid = eval_grid(g, g.B);
+  size_t t;
   if (which < 0 || which == 3) {
+    t = prof_begin(e, st);
 #define KG_DSMAX(X)                                                                                             \
   ds_max_round<X><<<grid, kWave * kEvalWaves, 0, st>>>(e->T, DT, e->pods.p, e->dpods.p, e->cursor.p, end, g.B, g.ppw, \
                                                        g.n_local, g.nt_local, e->P, e->DP, e->dsmax.p, e->dsval.p)
     KG_PF_SWITCH(profile_bits(e->P), KG_DSMAX)
 #undef KG_DSMAX
+    prof_end(e, KG_PROF_DS_MAX, t, st);
   }
-  if (which < 0 || which == 4)
+  if (which < 0 || which == 4) {
+    t = prof_begin(e, st);
     ds_norm_reduce<<<g.B, 256, 0, st>>>(e->cursor.p, end, g.B, e->dsmax.p, g.nt_local, e->dsnorm.p);
-  if (which < 0 || which == 0)
+    prof_end(e, KG_PROF_DS_NORM, t, st);
+  }
+  if (which < 0 || which == 0) {
+    t = prof_begin(e, st);
     eval_round_ds<<<grid, kWave * kEvalWaves, 0, st>>>(e->cursor.p, end, g.B, g.ppw, g.n_local, g.nt_local, e->P,
                                                         e->DP, e->dsnorm.p, e->dsval.p, lists_slot(e, g, 0));
-  if (which < 0 || which == 1) launch_merge_local(e, g, g.B, 0, st);
-  if (which < 0 || which == 2)
+    prof_end(e, KG_PROF_EVAL, t, st);
+  }
+  if (which < 0 || which == 1) {
+    t = prof_begin(e, st);
+    launch_merge_local(e, g, g.B, 0, st);
+    prof_end(e, KG_PROF_MERGE, t, st);
+  }
+  if (which < 0 || which == 2) {
+    t = prof_begin(e, st);
     resolve_round_ds<<<1, kWave, resolve_ds_lds_bytes(g, g.B), st>>>(e->T, DT, e->pods.p, e->dpods.p, e->cursor.p,
                                                                      end, g.B, cand_slot(e, g, 0), e->dsnorm.p,
                                                                      e->dsval.p, (int64_t)g.nt_local * kTile, e->P,
                                                                      e->DP, e->out_keys.p, e->out_minors.p,
                                                                      g.bitmap_words, e->quotas.p, e->nq);
+    prof_end(e, KG_PROF_RESOLVE, t, st);
+  }
 }
 
 int run_batch_ds(kg_engine* e, const RoundGeom& g, int64_t end, int64_t n_rounds) {
@@ -2228,7 +2426,7 @@ int run_batch_ds(kg_engine* e, const RoundGeom& g, int64_t end, int64_t n_rounds
     HIP_TRY(hipGetLastError());
   }
   HIP_TRY(hipStreamSynchronize(e->rs[0]));
-  return 0;
+  return prof_collect(e);
 }
 
 int prepare_rounds(kg_engine* e, RoundGeom& g) {
@@ -2238,10 +2436,14 @@ int prepare_rounds(kg_engine* e, RoundGeom& g) {
   if (g.nt_local > kMergeThreads * kMergeChunks)
     return fail(KG_E_UNSUPPORTED, "%lld nodes per rank exceed one merge block (%d)", (long long)g.shard,
                 kMergeThreads * kMergeChunks * kTile);
-  if (int rc = e->lists.ensure((size_t)2 * g.B * g.nt_local * kR)) return rc;
-  if (int rc = e->cand.ensure((size_t)2 * g.B * kCandStride)) return rc;
+  if (!e->numa_on && !e->ds_on && resolve_lds_bytes(g, g.B) > kMaxLds)
+    return fail(KG_E_UNSUPPORTED, "resolver LDS %zu B > %zu B: fewer nodes or a smaller batch_pods",
+                resolve_lds_bytes(g, g.B), kMaxLds);
+  const size_t D = (size_t)g.depth;
+  if (int rc = e->lists.ensure(D * g.B * g.nt_local * kR)) return rc;
+  if (int rc = e->cand.ensure(D * g.B * kCandStride)) return rc;
   if (e->n_ranks > 1)
-    if (int rc = e->gathered.ensure((size_t)2 * e->n_ranks * g.B * kCandStride)) return rc;
+    if (int rc = e->gathered.ensure(D * e->n_ranks * g.B * kCandStride)) return rc;
   if (e->ds_on) {
     if (int rc = e->dsmax.ensure((size_t)g.B * g.nt_local)) return rc;
     if (int rc = e->dsnorm.ensure((size_t)g.B)) return rc;
@@ -2267,20 +2469,28 @@ int run_rsv(kg_engine* e, int64_t first, int64_t count, kg_stats* stats, double 
     HIP_TRY(hipMemcpyAsync(e->rsv_ws.p, init, 32, hipMemcpyHostToDevice, e->stream));
     auto issue_group = [&]() {
       for (int g = 0; g < kRsvGroup; ++g) {
+        size_t t = prof_begin(e, e->stream);
         rsv_eval<<<blocks, kRsvThreads, 0, e->stream>>>(e->T, e->rsv_d.p, e->rsv_nd.p, e->pods.p, e->rpods.p, end, n, g,
                                                          e->P, e->RP, e->rsv_val.p, e->rsv_part.p, e->out_keys.p,
                                                          e->out_rslot.p, e->rsv_ws.p);
+        prof_end(e, KG_PROF_RSV_EVAL, t, e->stream);
+        t = prof_begin(e, e->stream);
         rsv_select<<<blocks, kRsvThreads, 0, e->stream>>>(e->rsv_val.p, end, n, g, e->RP, e->rsv_part.p, e->rsv_ws.p);
+        prof_end(e, KG_PROF_RSV_SELECT, t, e->stream);
       }
+      size_t t = prof_begin(e, e->stream);
       rsv_apply<<<1, kWave, 0, e->stream>>>(e->T, e->rsv_d.p, e->rsv_val.p, e->pods.p, end, (int)blocks, kRsvGroup - 1,
                                             e->rsv_part.p, e->out_keys.p, e->out_rslot.p, e->rsv_ws.p);
+      prof_end(e, KG_PROF_RSV_APPLY, t, e->stream);
     };
-    // KG_RSV_NO_GRAPH=1: plain stream launches (profilers whose kernel tracing does not follow graph launches)
+    // KG_RSV_NO_GRAPH=1: plain stream launches (profilers whose kernel tracing does not follow graph launches);
+    // live kernel timing also uses plain launches (its events bracket each launch)
     static const bool no_graph = std::getenv("KG_RSV_NO_GRAPH") && std::getenv("KG_RSV_NO_GRAPH")[0] == '1';
-    if (no_graph) {
+    if (no_graph || e->prof_on) {
       for (int64_t c = 0; c < count; c += kRsvGroup) issue_group();
       HIP_TRY(hipGetLastError());
       HIP_TRY(hipStreamSynchronize(e->stream));
+      if (int rc = prof_collect(e)) return rc;
     } else {
       hipGraph_t graph = nullptr;
       hipGraphExec_t exec = nullptr;
@@ -2427,7 +2637,7 @@ int kg_engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank, int
   {  // round streams at the device's highest priority (the serial resolve chain runs on them)
     int lo = 0, hi = 0;
     if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) return bail(fail(KG_E_DEVICE, "hipDeviceGetStreamPriorityRange"));
-    for (int k = 0; k < 2; ++k) {
+    for (int k = 0; k < kMaxDepth; ++k) {
       if (hipStreamCreateWithPriority(&e->rs[k], hipStreamNonBlocking, hi) != hipSuccess)
         return bail(fail(KG_E_DEVICE, "hipStreamCreateWithPriority"));
       if (hipEventCreateWithFlags(&e->ev_res[k], hipEventDisableTiming) != hipSuccess)
@@ -2459,8 +2669,8 @@ int kg_engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank, int
   e->T.cap = cap;
   if (int rc = e->cursor.ensure(8)) return bail(rc);
   if (hipMemset(e->cursor.p, 0, 8 * 8) != hipSuccess) return bail(fail(KG_E_DEVICE, "hipMemset"));
-  if (int rc = e->modlists.ensure(2 * (1 + kMaxB))) return bail(rc);
-  if (hipMemset(e->modlists.p, 0, 2 * (1 + kMaxB) * 4) != hipSuccess) return bail(fail(KG_E_DEVICE, "hipMemset"));
+  if (int rc = e->modlists.ensure(kMaxDepth * kModListStride)) return bail(rc);
+  if (hipMemset(e->modlists.p, 0, kMaxDepth * kModListStride * 4) != hipSuccess) return bail(fail(KG_E_DEVICE, "hipMemset"));
   e->nodes.assign(cap, kg_node{});
   e->metrics.assign(cap, kg_node_metric{});
   e->folded_usage.assign(2 * cap, 0);
@@ -2551,7 +2761,7 @@ int kg_engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank, int
     e->P.inv_fit_ws[3] = wc + wm > 0 ? 1.0f / (wc + wm) : 0.0f;
   }
   {
-    const int lds = (int)(kMaxNodes / 8 + (size_t)kMaxB * (kCandStride + kPodWords) * 8);
+    const int lds = (int)kMaxLds;
     hipError_t fe = hipSuccess;
 #define KG_ATTR(X)                                                                                           \
   fe = hipFuncSetAttribute((const void*)resolve_round<X, false>, hipFuncAttributeMaxDynamicSharedMemorySize, lds); \
@@ -2565,9 +2775,11 @@ int kg_engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank, int
     ncclUniqueId id;
     std::memcpy(&id, nccl_id, sizeof(id));
     if (ncclCommInitRank(&e->comm, n_ranks, id, rank) != ncclSuccess) return bail(fail(KG_E_COLLECTIVE, "ncclCommInitRank"));
-    // a second communicator for the odd-round stream: collectives of one communicator never run concurrently
-    if (ncclCommSplit(e->comm, 0, rank, &e->comm2, nullptr) != ncclSuccess)
-      return bail(fail(KG_E_COLLECTIVE, "ncclCommSplit"));
+    // one communicator per round stream: collectives of one communicator never run concurrently
+    e->comms[0] = e->comm;
+    for (int k = 1; k < kMaxDepth; ++k)
+      if (ncclCommSplit(e->comm, 0, rank, &e->comms[k], nullptr) != ncclSuccess)
+        return bail(fail(KG_E_COLLECTIVE, "ncclCommSplit"));
   }
   *out = e;
   return 0;
@@ -2576,10 +2788,12 @@ int kg_engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank, int
 void kg_engine_destroy(kg_engine* e) {
   if (!e) return;
   if (e->stream) (void)hipStreamSynchronize(e->stream);
-  for (int k = 0; k < 2; ++k)
+  for (int k = 0; k < kMaxDepth; ++k)
     if (e->rs[k]) (void)hipStreamSynchronize(e->rs[k]);
-  if (e->comm2) ncclCommDestroy(e->comm2);
+  for (int k = 1; k < kMaxDepth; ++k)
+    if (e->comms[k]) ncclCommDestroy(e->comms[k]);
   if (e->comm) ncclCommDestroy(e->comm);
+  for (hipEvent_t ev : e->prof_pool) (void)hipEventDestroy(ev);
   e->cols64.release();
   e->cols32.release();
   e->pods.release();
@@ -2589,7 +2803,7 @@ void kg_engine_destroy(kg_engine* e) {
   e->out_keys.release();
   e->cursor.release();
   e->modlists.release();
-  for (int k = 0; k < 2; ++k) {
+  for (int k = 0; k < kMaxDepth; ++k) {
     if (e->ev_res[k]) (void)hipEventDestroy(e->ev_res[k]);
     if (e->rs[k]) (void)hipStreamDestroy(e->rs[k]);
   }
@@ -2778,9 +2992,9 @@ int kg_pods_schedule_staged(kg_engine* e, int64_t first, int64_t count, kg_stats
   RoundGeom g;
   if (int rc = prepare_rounds(e, g)) return rc;
   const int64_t end = first + count;
-  const int64_t init[6] = {first, 0, 0, 0, 0, 0};
-  int64_t host_stats[6] = {first, 0, 0, 0, 0, 0};
-  HIP_TRY(hipMemcpyAsync(e->cursor.p, init, 6 * 8, hipMemcpyHostToDevice, e->stream));
+  const int64_t init[8] = {first, 0, 0, 0, 0, 0, 0, 0};
+  int64_t host_stats[8] = {first, 0, 0, 0, 0, 0, 0, 0};
+  HIP_TRY(hipMemcpyAsync(e->cursor.p, init, 8 * 8, hipMemcpyHostToDevice, e->stream));
   HIP_TRY(hipStreamSynchronize(e->stream));
   int64_t cur = first;
   while (cur < end) {
@@ -2788,13 +3002,15 @@ int kg_pods_schedule_staged(kg_engine* e, int64_t first, int64_t count, kg_stats
     // (DeviceShare rounds read the cursor themselves: an early stop only shortens that round)
     const int64_t n_rounds = std::min<int64_t>((end - cur + g.B - 1) / g.B, kMaxBatchRounds);
     if (int rc = e->ds_on ? run_batch_ds(e, g, end, n_rounds) : run_batch(e, g, cur, end, n_rounds)) return rc;
-    HIP_TRY(hipMemcpy(host_stats, e->cursor.p, 6 * 8, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(host_stats, e->cursor.p, 8 * 8, hipMemcpyDeviceToHost));
     if (host_stats[5]) return fail(KG_E_DEVICE, "resolver chain wait timed out (round sequence %lld)", (long long)host_stats[4]);
     cur = host_stats[0];
   }
   if (stats) {
     std::memset(stats, 0, sizeof(*stats));
     stats->device_batches = host_stats[1];
+    stats->reserved[0] = (double)host_stats[6];  // diagnostics: slow-path pods, speculation steps (resolve_round)
+    stats->reserved[1] = (double)host_stats[7];
     stats->node_evaluations = count * g.N;
     stats->seconds = now_s() - t0;
   }
@@ -3195,7 +3411,7 @@ int kg_bench_kernel(kg_engine* e, int which, int iters, double* avg_ms, double* 
     if (e->ds_on) launch_round_ds(e, g, end, e->stream, which);
     else if (which == 0) launch_eval(e, g, 0, nb, 0, e->stream);
     else if (which == 1) launch_merge_local(e, g, nb, 0, e->stream);
-    else launch_resolve(e, g, 0, nb, -1, 0, 1, 0, e->stream);
+    else launch_resolve(e, g, 0, nb, 0, 0, 1, 0, e->stream);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(b, e->stream));
     HIP_TRY(hipEventSynchronize(b));
@@ -3228,6 +3444,24 @@ int kg_bench_kernel(kg_engine* e, int which, int iters, double* avg_ms, double* 
   return 0;
 }
 
+int kg_profile_enable(kg_engine* e, int on) {
+  if (!e) return fail(KG_E_INVALID, "engine is NULL");
+  e->prof_on = on != 0;
+  for (int k = 0; k < KG_PROF_KINDS; ++k) e->prof_ms[k] = 0.0, e->prof_n[k] = 0;
+  e->prof_recs.clear();
+  e->prof_used = 0;
+  return 0;
+}
+
+int kg_profile_read(kg_engine* e, double* ms_total, int64_t* launches) {
+  if (!e) return fail(KG_E_INVALID, "engine is NULL");
+  for (int k = 0; k < KG_PROF_KINDS; ++k) {
+    if (ms_total) ms_total[k] = e->prof_ms[k];
+    if (launches) launches[k] = e->prof_n[k];
+  }
+  return 0;
+}
+
 int kg_debug_eval_paths(kg_engine* e, int64_t* mismatches) {
   if (!e || !mismatches) return fail(KG_E_INVALID, "bad argument");
   if (int rc = sync_static(e)) return rc;
@@ -3251,6 +3485,8 @@ int kg_debug_stamps(kg_engine* e, uint64_t* out) {
   if (!e || !out) return fail(KG_E_INVALID, "bad argument");
   HIP_TRY(hipStreamSynchronize(e->stream));
   HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(kg::g_stamps), sizeof(kg::g_stamps), 0, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpyFromSymbol(out + 4 * 32 * 2, HIP_SYMBOL(kg::g_pod_diag), sizeof(kg::g_pod_diag), 0,
+                              hipMemcpyDeviceToHost));
   return 0;
 #else
   (void)e;

@@ -30,7 +30,19 @@ __device__ unsigned long long g_stamps[4][32][2];
       g_stamps[kern][point][1] = __builtin_amdgcn_s_memrealtime();                 \
     }                                                                              \
   } while (0)
+// per-pod diagnostics of the last resolver launch: cycle stamp + path bits
+__device__ unsigned long long g_pod_diag[64][2];
+#define KG_POD_DIAG(j, bits)                                                       \
+  do {                                                                             \
+    if (threadIdx.x == 0 && (j) < 64) {                                            \
+      g_pod_diag[j][0] = __builtin_amdgcn_s_memtime();                             \
+      g_pod_diag[j][1] = (bits);                                                   \
+    }                                                                              \
+  } while (0)
 #else
+#define KG_POD_DIAG(j, bits) \
+  do {                       \
+  } while (0)
 #define KG_STAMP(kern, point) \
   do {                        \
   } while (0)

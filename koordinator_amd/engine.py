@@ -234,6 +234,17 @@ class Engine:
         check(self.lib, self.lib.kg_bench_kernel(self.h, int(which), int(iters), ctypes.byref(ms), ctypes.byref(by)))
         return ms.value, by.value
 
+    def profile(self, on: bool = True):
+        """Live kernel timing of the round runners (kg_profile_enable): resets the accumulators."""
+        check(self.lib, self.lib.kg_profile_enable(self.h, int(on)))
+
+    def profile_read(self) -> dict:
+        """{kernel name: (summed event ms, launches)} since profile() (kg_profile_read)."""
+        ms = np.zeros(abi.PROF_KINDS, dtype=np.float64)
+        n = np.zeros(abi.PROF_KINDS, dtype=np.int64)
+        check(self.lib, self.lib.kg_profile_read(self.h, ptr(ms), ptr(n)))
+        return {name: (float(ms[k]), int(n[k])) for k, name in abi.PROF_NAMES.items() if n[k] > 0}
+
     def debug_eval_paths(self) -> int:
         out = np.zeros(1, dtype=np.int64)
         check(self.lib, self.lib.kg_debug_eval_paths(self.h, ptr(out)))

@@ -82,7 +82,7 @@ class Profile:
 def build_config(la: LoadAwareSchedulingArgs | None = None, fit: NodeResourcesFitArgs | None = None,
                  profile: Profile | None = None, batch_pods: int = 32, pods_per_wave: int = 8,
                  device_id: int = -1, numa: NodeNUMAResourceArgs | None = None,
-                 deviceshare: DeviceShareArgs | None = None) -> np.ndarray:
+                 deviceshare: DeviceShareArgs | None = None, pipeline_depth: int = 0) -> np.ndarray:
     la = la or LoadAwareSchedulingArgs()
     fit = fit or NodeResourcesFitArgs()
     profile = profile or Profile()
@@ -108,6 +108,7 @@ def build_config(la: LoadAwareSchedulingArgs | None = None, fit: NodeResourcesFi
     r["batch_pods"] = batch_pods
     r["pods_per_wave"] = pods_per_wave
     r["device_id"] = device_id
+    r["pipeline_depth"] = pipeline_depth
     r["numa_filter"] = int(NODE_NUMA_RESOURCE in profile.filter)
     r["numa_score"] = int(NODE_NUMA_RESOURCE in profile.score)
     r["weight_numa"] = int(profile.score.get(NODE_NUMA_RESOURCE, 0))

@@ -19,7 +19,9 @@ from collections import defaultdict
 
 
 def short(name: str) -> str:
-    for k in ("eval_round", "merge_round", "resolve_round", "evaluate_pod", "apply_deltas"):
+    for k in ("ds_max_round", "ds_norm_reduce", "eval_round_numa", "eval_round_ds", "resolve_round_numa",
+              "resolve_round_ds", "eval_round", "merge_round", "resolve_round", "rsv_eval", "rsv_select", "rsv_apply",
+              "evaluate_pod", "apply_deltas"):
         if k in name:
             return k
     return name[:60]
@@ -44,6 +46,7 @@ def pmc(d: str, counter: str):
 
 def main():
     d = sys.argv[1]
+    meta = json.loads(sys.argv[2]) if len(sys.argv) > 2 else None  # workload geometry, matched by bench.py
     for f in glob.glob(os.path.join(d, "trace", "**", "*kernel_stats.csv"), recursive=True):
         print(f"-- kernel stats ({os.path.relpath(f, d)})")
         with open(f) as fh:
@@ -61,6 +64,8 @@ def main():
         out[k] = {"fetch_bytes": fb, "write_bytes": wb, "traffic_bytes": fb + wb,
                   "launches": max(fetch.get(k, (0, 0))[1], write.get(k, (0, 0))[1])}
         print(f"  {k:16s} fetch={fb/1e6:10.3f} MB write={wb/1e6:10.3f} MB launches={out[k]['launches']}")
+    if meta:
+        out["_meta"] = meta
     with open(os.path.join(d, "traffic.json"), "w") as fh:
         json.dump(out, fh, indent=1)
 

@@ -150,6 +150,22 @@ def test_schedule_parity_round_shapes(batch, ppw):
     _parity(cfg, cl, pods)
 
 
+@pytest.mark.parametrize("depth,batch", [(1, 32), (2, 32), (3, 32), (4, 32), (2, 64), (3, 48), (4, 13)])
+def test_schedule_parity_pipeline_depths(depth, batch):
+    """Rounds in flight (eval(r) reads the table right after resolve(r - depth)): every depth and batch shape
+    gives the sequential result, including a tie-heavy cluster where most pods take the speculative resolver's
+    slow path."""
+    cfg = framework.build_config(batch_pods=batch, pods_per_wave=8, pipeline_depth=depth)
+    _parity(cfg, synth.make_cluster(1500, seed=23), synth.make_pods(4000, seed=24))
+    n = 300
+    nodes = np.concatenate([framework.make_node({"cpu": "16", "memory": "64Gi"}) for _ in range(n)])
+    metrics = np.concatenate([framework.make_node_metric(update_time_ns=synth.T0_NS,
+                                                         node_usage={"cpu": "1", "memory": "1Gi"}) for _ in range(n)])
+    cl = synth.Cluster(nodes, metrics, np.zeros(0, dtype=abi.POD_DTYPE), np.zeros(0, dtype=np.int32),
+                       synth.T0_NS + 10**9)
+    _parity(cfg, cl, synth.make_pods(2500, seed=25))
+
+
 def test_schedule_parity_profile_variants():
     cl = synth.make_cluster(800, seed=31)
     pods = synth.make_pods(2000, seed=32)
@@ -315,3 +331,39 @@ def test_eval_paths_agree():
             p["flags"][::5] = abi.POD_DAEMONSET
             e.stage(p)
             assert e.debug_eval_paths() == 0
+
+
+@pytest.mark.slow
+def test_c3_full_size():
+    """BASELINE config 3 on one GPU at full size: the 100k-node cluster and 1M-pod queue bench.py times (same
+    seeds, same default geometry).  Bit-exact vs the oracle on the first 10k pods; over the whole queue the
+    size-independent properties: the unpipelined B=1 device path (trivially sequential) agrees on a 20k prefix,
+    requested resources are conserved (initial + Σ placed requests), and every placement is feasible (no node over
+    its cpu / memory allocatable or pod count)."""
+    cfg = framework.build_config()
+    cl = synth.make_cluster(100_000, seed=synth.BASE_SEED + 3)
+    pods = synth.make_pods(1_000_000, seed=synth.BASE_SEED + 4)
+    on, _, _ = oracle.schedule_cluster(cfg, cl, pods[:10_000], n_threads=16)
+    with _engine(cfg, cl) as e:
+        e.stage(pods)
+        for s in range(0, len(pods), 100_000):
+            e.schedule_staged(s, 100_000)
+        g, sc = e.fetch(0, len(pods))
+        st = e.read_state()
+    mism = np.nonzero(g[:10_000] != on)[0]
+    assert mism.size == 0, f"first mismatch at pod {mism[:5]}"
+    with _engine(framework.build_config(batch_pods=1, pods_per_wave=1, pipeline_depth=1), cl) as e1:
+        g1, s1, _ = e1.schedule(pods[:20_000])
+    np.testing.assert_array_equal(g[:20_000], g1)
+    np.testing.assert_array_equal(sc[:20_000], s1)
+    placed = g >= 0
+    assert placed.sum() > 900_000
+    for r, col in ((abi.RES_CPU, "requested_cpu"), (abi.RES_MEMORY, "requested_mem")):
+        base = np.bincount(cl.existing_node, weights=cl.existing_pods["requests"][:, r].astype(np.float64),
+                           minlength=cl.n)
+        add = np.bincount(g[placed], weights=pods["requests"][placed, r].astype(np.float64), minlength=cl.n)
+        np.testing.assert_array_equal(st[col], (base + add).astype(np.int64))
+        assert (st[col] <= cl.nodes["allocatable"][:, r]).all()
+    assert (st["num_pods"] <= cl.nodes["allowed_pods"]).all()
+    np.testing.assert_array_equal(st["num_pods"], np.bincount(cl.existing_node, minlength=cl.n) +
+                                  np.bincount(g[placed], minlength=cl.n))
