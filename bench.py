@@ -43,6 +43,7 @@ WORKLOADS = {
     "c1": (500, 5_000, 32, 8, 5_000),
     "c3": (100_000, 100_000, 32, 8, 10_000),
     "c4": (10_000, 10_000, 16, 1, 2_000),
+    "c5": (50_000, 10_000, 32, 4, 2_000),
     "c5ds": (50_000, 10_000, 32, 4, 2_000),
     "c5r": (50_000, 10_000, 32, 4, 2_000),
 }
@@ -119,9 +120,13 @@ class Work:
     def __init__(self, name, nodes, cfg):
         from koordinator_amd import synth
         self.name, self.cfg = name, cfg
-        self.numa = self.devices = self.rsv = None
+        self.numa = self.devices = self.rsv = self.quotas = None
         S = synth
-        if name == "c4":
+        if name == "c5":
+            self.seed = S.BASE_SEED + 10
+            self.cluster, self.devices, self.rsv = S.make_c5_cluster(nodes, seed=self.seed)
+            self.make_pods = S.make_c5_pods
+        elif name == "c4":
             self.seed = S.BASE_SEED + 4
             self.cluster, self.numa = S.make_numa_cluster(nodes, seed=self.seed)
             self.make_pods = S.make_numa_pods
@@ -138,9 +143,17 @@ class Work:
             self.cluster = S.make_cluster(nodes, seed=self.seed)
             self.make_pods = S.make_pods
 
+    def set_queue(self, pods):
+        """ElasticQuota groups sized on the queue's demand (C5: 16 groups whose limits run out mid-queue)."""
+        from koordinator_amd import synth
+        if self.name == "c5":
+            self.quotas = synth.make_c5_quotas(pods, seed=self.seed + 2)
+
     def load(self, e):
         from koordinator_amd import synth
-        if self.numa is not None:
+        if self.name == "c5":
+            synth.load_c5_into(e, self.cluster, self.devices, self.rsv, self.quotas)
+        elif self.numa is not None:
             synth.load_numa_into(e, self.cluster, self.numa)
         elif self.devices is not None:
             synth.load_gpu_into(e, self.cluster, self.devices)
@@ -156,8 +169,11 @@ class Work:
         st = oracle.states(cl.n)
         oracle.add_pods(cfg, st, cl.existing_pods, cl.existing_node)
         if self.rsv is not None:
-            on, _, _ = oracle.schedule_resv(cfg, cl.nodes, cl.metrics, st, self.rsv.copy(), pods, cl.now_ns)
-            return on, "oracle/reservation.c or_schedule_resv (single-threaded loop)"
+            on, _, _ = oracle.schedule_resv(cfg, cl.nodes, cl.metrics, st, self.rsv.copy(), pods, cl.now_ns,
+                                            devices=None if self.devices is None else self.devices.copy(),
+                                            quotas=None if self.quotas is None else self.quotas.copy(),
+                                            n_threads=threads)
+            return on, "oracle/reservation.c or_schedule_resv_full (Parallelizer chunking)"
         if self.devices is not None:
             on, _, _, _ = oracle.schedule_full(cfg, cl.nodes, cl.metrics, st, pods, cl.now_ns, threads,
                                                devices=self.devices.copy())
@@ -223,6 +239,9 @@ def main():
     elif wl == "c5ds":  # shipped weights: DeviceShare 1 (config/manager/scheduler-config.yaml:82-91)
         profile = F.Profile(filter=(F.NODE_RESOURCES_FIT, F.LOAD_AWARE, F.DEVICE_SHARE),
                             score={F.NODE_RESOURCES_FIT: 1, F.LOAD_AWARE: 1, F.DEVICE_SHARE: 1})
+    elif wl == "c5":  # one profile: Reservation 5000, DeviceShare 1, ElasticQuota admission (PreFilter only)
+        profile = F.Profile(filter=(F.NODE_RESOURCES_FIT, F.LOAD_AWARE, F.RESERVATION, F.DEVICE_SHARE),
+                            score={F.NODE_RESOURCES_FIT: 1, F.LOAD_AWARE: 1, F.RESERVATION: 5000, F.DEVICE_SHARE: 1})
     elif wl == "c5r":  # shipped weights: Reservation 5000 (config/manager/scheduler-config.yaml:90-91)
         profile = F.Profile(filter=(F.NODE_RESOURCES_FIT, F.LOAD_AWARE, F.RESERVATION),
                             score={F.NODE_RESOURCES_FIT: 1, F.LOAD_AWARE: 1, F.RESERVATION: 5000})
@@ -233,6 +252,7 @@ def main():
     total = args.steps * args.pods_per_step
     n_prof = args.profile_pods if args.profile_pods is not None else min(args.pods_per_step, 20_000)
     pods = work.make_pods(total + n_prof, seed=work.seed + 1)
+    work.set_queue(pods)
 
     def engine():
         e = Engine(cfg, cluster.n, rank=d.rank, n_ranks=d.world, nccl_id=nccl_id)
@@ -270,21 +290,25 @@ def main():
         live = {k: {"avg_ms": ms / n, "launches": n} for k, (ms, n) in e.profile_read().items()}
         e.profile(False)
     # isolated replays of one round's kernels (warm caches, no concurrency) for comparison
-    names = (("rsv_eval", "rsv_select") if wl == "c5r" else
+    rsv_path = wl in ("c5r", "c5")
+    names = (("rsv_eval", "rsv_select") if rsv_path else
              ("eval_round", "merge_round", "resolve_round") + (("ds_max_round", "ds_norm_reduce") if wl == "c5ds" else ()))
     isolated = {name: e.bench_kernel(which, args.kernel_iters) for which, name in enumerate(names)}
 
     # roofline kernel: the wide pass — the only kernel whose work scales with node evaluations.  One launch
     # processes the round's B pods against every node row of this rank's shard, reading each row once:
     # algorithmic bytes = rows × b_node + the candidate lists written + the pods read.
-    dom = {"c5ds": "ds_max_round", "c5r": "rsv_eval"}.get(wl, "eval_round")
+    dom = {"c5ds": "ds_max_round", "c5r": "rsv_eval", "c5": "rsv_eval"}.get(wl, "eval_round")
     n_local = -(-cluster.n // d.world)
     nt = max(1, -(-n_local // 256))
-    B = 1 if wl == "c5r" else args.batch
+    B = 1 if rsv_path else args.batch
     if wl == "c5ds":  # ds_max_round also reads the 272-B GPU row and writes a 4-B packed value per (pod, node)
         algo = n_local * (B_NODE + 272.0) + B * n_local * 4.0 + B * nt * 8.0
-    elif wl == "c5r":  # rsv_eval (one pod per pass): _, isolated replay reports its own accounting
-        algo = isolated["rsv_eval"][1]
+    elif rsv_path:  # rsv_eval, one pod per pass: node columns + rsv_n + packed value per node, the 192-B slot rows of
+        # nodes holding reservations, and the 272-B GPU row per node for the device pods among the profiled ones
+        prof_pods = pods[total:total + n_prof] if n_prof > 0 else pods[:1]
+        frac_dev = float(prof_pods["device_requests"].any(axis=1).mean()) if work.devices is not None else 0.0
+        algo = n_local * (B_NODE + 4 + 8) + int((work.rsv["n"] > 0).sum()) * 192.0 + frac_dev * n_local * 272.0
     else:
         algo = n_local * B_NODE + B * nt * 8 * 8.0 + B * 96.0
     dom_ms = live.get(dom, {}).get("avg_ms") or isolated[dom][0]
@@ -309,7 +333,7 @@ def main():
     cpu = None
     if d.rank == 0 and d.world == 1 and not args.no_cpu_baseline:
         print("[bench] cpu baseline samples", file=sys.stderr, flush=True)
-        threads = 1 if wl == "c5r" else args.cpu_threads
+        threads = args.cpu_threads
         m, dt, desc = cpu_sample(work, pods[:total], args.cpu_seconds, threads)
         m1, dt1, _ = cpu_sample(work, pods[:total], args.cpu_seconds / 3, 1)
         cpu = {"value": m / dt, "unit": "pods/s", "cores": threads, "kind": "port",
@@ -330,6 +354,10 @@ def main():
                   "%d pods per step",
             "c5ds": "C5 (DeviceShare part): %d nodes x 8 GPUs, %d-pod FIFO queue (30%% GPU-share), "
                     "NodeResourcesFit+LoadAwareScheduling+DeviceShare, %d pods per step",
+            "c5": "C5 (one profile): %d nodes x 8 GPUs (30%% with 1-4 cpu/memory reservations, 64 owner groups), "
+                  "%d-pod FIFO queue (30%% GPU-share, 20%% reservation-owned, 80%% in 16 ElasticQuota groups), "
+                  "NodeResourcesFit+LoadAwareScheduling+Reservation (w 5000)+DeviceShare+ElasticQuota admission, "
+                  "one pod per device pass, %d pods per step",
             "c5r": "C5 (Reservation part): %d nodes (30%% with 1-4 reservations), %d-pod FIFO queue (20%% "
                    "reservation-owned), NodeResourcesFit+LoadAwareScheduling+Reservation (w 5000), one pod per device "
                    "pass, %d pods per step",
@@ -339,7 +367,9 @@ def main():
                        "c1": "pods scheduled/sec, config 1 (500 nodes; node-evals/sec alongside)",
                        "c4": "pods scheduled/sec, NodeNUMAResource cpuset/NUMA profile (node-evals/sec alongside)",
                        "c5ds": "pods scheduled/sec, DeviceShare GPU-share profile (node-evals/sec alongside)",
-                       "c5r": "pods scheduled/sec, Reservation profile (node-evals/sec alongside)"}[wl],
+                       "c5r": "pods scheduled/sec, Reservation profile (node-evals/sec alongside)",
+                       "c5": "pods scheduled/sec, Reservation+DeviceShare+ElasticQuota profile (node-evals/sec "
+                             "alongside)"}[wl],
             "value": pods_s,
             "unit": "pods/s",
             "n_gpus": d.world,

@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define KG_ABI_VERSION 4
+#define KG_ABI_VERSION 5
 
 /* ---- resource slots (fixed order) ------------------------------------------------------- */
 enum {
@@ -128,8 +128,15 @@ enum {
 enum {
   KG_POD_DAEMONSET = 1 << 0,
   KG_POD_NON_PREEMPTIBLE = 1 << 1,  /* extension.IsPodNonPreemptible (ElasticQuota min check) */
-  KG_POD_RESERVE = 1 << 2           /* a reservation's reserve pod (kg_pods_add): NodeInfo only — the LoadAware
+  KG_POD_RESERVE = 1 << 2,          /* a reservation's reserve pod (kg_pods_add): NodeInfo only — the LoadAware
                                        assign cache is fed by the pod informer, which never sees it */
+  /* request-key presence (PodRequestsAndLimits keys, even when zero): with KG_POD_REQUEST_KEYS set the next two bits
+   * say whether the cpu / memory keys exist; without it a key exists iff its request is non-zero.  Only
+   * filterWithReservations looks at keys (Intersection(rInfo.ResourceNames, pod request names),
+   * reservation/plugin.go:392-395). */
+  KG_POD_REQUEST_KEYS = 1 << 3,
+  KG_POD_CPU_KEY = 1 << 4,
+  KG_POD_MEM_KEY = 1 << 5
 };
 #define KG_MAX_QUOTAS 64
 
@@ -219,9 +226,11 @@ typedef struct kg_pod {
   int64_t preferred_cpu_bind_policy;           /* ResourceSpec annotation: KG_BIND_*                  */
   int64_t device_requests[KG_DEV_RES_MAX];     /* PodRequestsAndLimits of the device resources (KG_DEV_*) */
   int64_t quota_id;                            /* 1 + index into the kg_quotas_set table; 0 = no ElasticQuota */
-  int64_t reservation_owner;                   /* owner group the caller decoded from the pod against every   */
-                                               /* ReservationInfo.Match (reservation_info.go:231-236,        */
-                                               /* MatchReservationOwners pkg/util/reservation:389-410); 0 = none */
+  int64_t reservation_owner_mask;              /* bit g set: the pod matches the owners of reservation owner  */
+                                               /* group g (kg_node_reservations.owner), as the caller decoded  */
+                                               /* ReservationInfo.Match (reservation_info.go:231-236,          */
+                                               /* MatchReservationOwners pkg/util/reservation:389-410) once per */
+                                               /* distinct owner spec; 0 = matches none                         */
   int64_t reservation_flags;                   /* KG_POD_RSV_*                                        */
 } kg_pod;
 
@@ -231,14 +240,19 @@ enum {
 };
 
 /* Reservation slots of one node as reservationCache holds them (frameworkext/reservation_info.go:79-99,
- * reservation/cache.go:56-61).  The reserve pods stay in NodeInfo (kg_pods_add: requests = allocatable), as the
- * reference's scheduler cache keeps them.  Policies: reservation allocate policy (Default / Aligned / Restricted). */
+ * reservation/cache.go:56-61).  The reserve pods stay in NodeInfo (kg_pods_add: requests = allocatable, non-zero
+ * requests = schedutil.GetNonzeroRequests of them, i.e. 100m / 200MiB for an absent key), as the reference's
+ * scheduler cache keeps them.  Owners: reservations with the same owner spec (ObjectRef / Controller /
+ * LabelSelector list) share an owner group 0..63; a pod carries the bitmask of the groups it matches.  An allocatable
+ * of 0 = the resource is absent from ReservationInfo.Allocatable (cpu-only / memory-only reservations).  Policies:
+ * reservation allocate policy (Default / Aligned / Restricted). */
+#define KG_MAX_OWNER_GROUPS 64
 #define KG_MAX_RSV_SLOTS 4
 enum { KG_RSV_POLICY_DEFAULT = 0, KG_RSV_POLICY_ALIGNED = 1, KG_RSV_POLICY_RESTRICTED = 2 };
 typedef struct kg_node_reservations {
   int64_t n;                                   /* slots in use (0..KG_MAX_RSV_SLOTS), by reservation index    */
-  int64_t owner[KG_MAX_RSV_SLOTS];             /* owner group a pod's reservation_owner must equal            */
-  int64_t allocatable_cpu[KG_MAX_RSV_SLOTS];   /* ReservationInfo.Allocatable (milli; both > 0)               */
+  int64_t owner[KG_MAX_RSV_SLOTS];             /* owner group 0..63 (bit of kg_pod.reservation_owner_mask)    */
+  int64_t allocatable_cpu[KG_MAX_RSV_SLOTS];   /* ReservationInfo.Allocatable (milli / bytes; 0 = absent)     */
   int64_t allocatable_mem[KG_MAX_RSV_SLOTS];
   int64_t allocated_cpu[KG_MAX_RSV_SLOTS];     /* ReservationInfo.Allocated (Σ assigned pods' requests)       */
   int64_t allocated_mem[KG_MAX_RSV_SLOTS];
@@ -250,16 +264,19 @@ typedef struct kg_node_reservations {
   int64_t unschedulable[KG_MAX_RSV_SLOTS];     /* IsUnschedulable                                              */
 } kg_node_reservations;
 
-/* One ElasticQuota as the plugin's PreFilter snapshot sees it (plugin.go:211-256): cpu (milli) and memory (bytes).
- * used_limit = runtime when EnableRuntimeQuota else max (getQuotaInfoUsedLimit).  Runtime is refreshed from the
- * quota tree's requests, which Reserve does not change, so it is fixed for a batch.  A limit / min of -1 = the
- * resource is absent from that ResourceList: quotav1.LessThanOrEqual only compares keys of its second argument,
- * so an absent key does not constrain. */
+/* One ElasticQuota as the plugin's PreFilter snapshot sees it (plugin.go:211-256) over KG_QUOTA_RES resources: cpu
+ * (milli), memory (bytes), then the device resources of kg_pod.device_requests[0..5] (nvidia.com/gpu, dcu.com/gpu,
+ * koordinator.sh/gpu, gpu-core, gpu-memory, gpu-memory-ratio) — the pod's quota request is PodRequestsAndLimits
+ * over all of them.  used_limit = runtime when EnableRuntimeQuota else max (getQuotaInfoUsedLimit).  Runtime is
+ * refreshed from the quota tree's requests, which Reserve does not change, so it is fixed for a batch.  A limit /
+ * min of -1 = the resource is absent from that ResourceList: quotav1.LessThanOrEqual only compares keys of its
+ * second argument, so an absent key does not constrain. */
+#define KG_QUOTA_RES 8
 typedef struct kg_quota {
-  int64_t used[2];
-  int64_t non_preemptible_used[2];
-  int64_t used_limit[2];
-  int64_t min[2];
+  int64_t used[KG_QUOTA_RES];
+  int64_t non_preemptible_used[KG_QUOTA_RES];
+  int64_t used_limit[KG_QUOTA_RES];
+  int64_t min[KG_QUOTA_RES];
 } kg_quota;
 
 /* DeviceShare view of one node's GPUs: the Device object's GPU entries (deviceshare/device_cache.go:505-523:

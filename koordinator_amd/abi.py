@@ -31,8 +31,11 @@ OK, E_INVALID, E_DEVICE, E_COLLECTIVE, E_NOMEM, E_UNSUPPORTED = 0, -1, -2, -3, -
 REJECT_FIT_PODS, REJECT_FIT_CPU, REJECT_FIT_MEMORY, REJECT_LOADAWARE, REJECT_INVALID_NODE = 1, 2, 4, 8, 16
 NODE_VALID, NODE_HAS_RAW_ALLOCATABLE, NODE_HAS_CUSTOM_THRESHOLDS = 1, 2, 4
 POD_DAEMONSET, POD_NON_PREEMPTIBLE, POD_RESERVE = 1, 2, 4
+POD_REQUEST_KEYS, POD_CPU_KEY, POD_MEM_KEY = 8, 16, 32
+MAX_OWNER_GROUPS = 64
+QUOTA_RES = 8
 MAX_QUOTAS = 64
-ABI_VERSION = 4
+ABI_VERSION = 5
 MAX_RSV_SLOTS = 4
 RSV_POLICY = {"Default": 0, "Aligned": 1, "Restricted": 2}
 POD_RSV_AFFINITY = 1
@@ -112,14 +115,15 @@ POD_DTYPE = np.dtype([
     _i64("qos"), _i64("required_cpu_bind_policy"), _i64("preferred_cpu_bind_policy"),
     _i64("device_requests", DEV_RES_MAX),
     _i64("quota_id"),
-    _i64("reservation_owner"), _i64("reservation_flags"),
+    _i64("reservation_owner_mask"), _i64("reservation_flags"),
 ])
 
 NODE_RSV_DTYPE = np.dtype([_i64("n")] + [_i64(f, MAX_RSV_SLOTS) for f in (
     "owner", "allocatable_cpu", "allocatable_mem", "allocated_cpu", "allocated_mem", "assigned", "order", "policy",
     "allocate_once", "available", "unschedulable")])
 
-QUOTA_DTYPE = np.dtype([_i64("used", 2), _i64("non_preemptible_used", 2), _i64("used_limit", 2), _i64("min", 2)])
+QUOTA_DTYPE = np.dtype([_i64("used", QUOTA_RES), _i64("non_preemptible_used", QUOTA_RES), _i64("used_limit", QUOTA_RES),
+                        _i64("min", QUOTA_RES)])
 
 NODE_DEVICE_DTYPE = np.dtype([
     _i64("has_device"), _i64("present", MAX_MINORS), _i64("healthy", MAX_MINORS),

@@ -495,7 +495,9 @@ __global__ __launch_bounds__(kMergeThreads) void merge_round(DevTable T, EvalPar
       o[kC] = ub_in > ub_sel ? ub_in : ub_sel;
     }
     // hoisted rows of the kStaged best candidates (the resolver's likely winners)
-    if (lane < (int)n_sel && rank < kStaged) {
+    // (DeviceShare rounds merge all B pod slots, the ones past the round's pods holding stale lists: a node index
+    // outside the table is never dereferenced)
+    if (lane < (int)n_sel && rank < kStaged && key_node(v) < (uint32_t)T.cap) {
       const EvalRow er = make_eval_row(load_row(T, key_node(v)), P);
       uint64_t words[kEvalRowWords];
       __builtin_memcpy(words, &er, sizeof(er));  // well-defined type punning (no strict-aliasing hazard)
@@ -711,7 +713,7 @@ __global__ __launch_bounds__(kWave) void resolve_round(DevTable T, const DevPod*
                                                         uint64_t* __restrict__ out_keys, int bitmap_words,
                                                         int32_t* __restrict__ modlists, int slot, int depth,
                                                         int n_prev, int32_t* __restrict__ poison, int64_t seq,
-                                                        int wait, DevQuota* __restrict__ quotas, int nq) {
+                                                        int wait, QuotaRow* __restrict__ quotas, int nq) {
   extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
   KG_STAMP(2, 0);
   const int lane = threadIdx.x;
@@ -895,7 +897,7 @@ __global__ __launch_bounds__(kWave) void resolve_round(DevTable T, const DevPod*
   if (R0.touched) my_mod[1 + __popcll(b0 & lane_lt)] = (int32_t)R0.node;
   if (R1.touched) my_mod[1 + __popcll(b0) + __popcll(b1 & lane_lt)] = (int32_t)R1.node;
   if (lane < consumed) out_keys[first + lane] = my_out;
-  if (QUOTA && lane < nq) quotas[lane] = ql;
+  if (QUOTA) quota_store(quotas, nq, lane, ql);
   if (lane == 0) {
     my_mod[0] = __popcll(b0) + __popcll(b1);
     ctl[0] = first + consumed;
@@ -1016,7 +1018,7 @@ __global__ __launch_bounds__(kWave) void resolve_round_numa(DevTable T, NumaTabl
                                                              NumaParams NP, uint64_t* __restrict__ out_keys,
                                                              uint64_t* __restrict__ out_cpus, int bitmap_words,
                                                              int32_t* __restrict__ poison, int64_t seq,
-                                                             DevQuota* __restrict__ quotas, int nq) {
+                                                             QuotaRow* __restrict__ quotas, int nq) {
   extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
   const int lane = threadIdx.x;
   uint64_t* s_cand = smem;                                    // [nb][kCandStride]
@@ -1134,7 +1136,7 @@ __global__ __launch_bounds__(kWave) void resolve_round_numa(DevTable T, NumaTabl
     NT.m[midx] = s_nm[lane];
   }
   if (lane < consumed) out_keys[first + lane] = my_out;
-  if (lane < nq) quotas[lane] = ql;
+  quota_store(quotas, nq, lane, ql);
   if (lane == 0) {
     ctl[0] = first + consumed;
     ctl[1] += 1;
@@ -1347,7 +1349,8 @@ __global__ __launch_bounds__(kWave) void resolve_round_ds(DevTable T, DsTable DT
                                                            EvalParams P,
                                                            DsParams DP, uint64_t* __restrict__ out_keys,
                                                            int32_t* __restrict__ out_minors, int bitmap_words,
-                                                           DevQuota* __restrict__ quotas, int nq) {
+                                                           QuotaRow* __restrict__ quotas, int nq,
+                                                           const int64_t* __restrict__ qdev) {
   extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
   const int lane = threadIdx.x;
   int64_t first;
@@ -1358,7 +1361,9 @@ __global__ __launch_bounds__(kWave) void resolve_round_ds(DevTable T, DsTable DT
   uint64_t* s_dpw = s_podw + (size_t)nb * kPodWords;        // [nb] DsPod
   uint64_t* s_cur = s_dpw + (size_t)nb * kDsPodWords;       // [kWave] DsNode, current
   uint64_t* s_stg = s_cur + (size_t)kWave * kDsNodeWords;   // [nb] DsNode of each pod's top candidate
-  Row* s_srow = reinterpret_cast<Row*>(s_stg + (size_t)nb * kDsNodeWords);  // [nb] its Row
+  QuotaRow* s_q = reinterpret_cast<QuotaRow*>(s_stg + (size_t)nb * kDsNodeWords);  // [nq] quota rows
+  int64_t* s_qdev = reinterpret_cast<int64_t*>(s_q + nq);   // [nb][kQuotaRes] device quota requests
+  Row* s_srow = reinterpret_cast<Row*>(s_qdev + (size_t)nb * kQuotaRes);  // [nb] its Row
   uint32_t* bitmap = reinterpret_cast<uint32_t*>(s_srow + nb);
   for (int w = lane; w < nb * kCandStride; w += kWave) s_cand[w] = cand[w];
   {
@@ -1366,6 +1371,12 @@ __global__ __launch_bounds__(kWave) void resolve_round_ds(DevTable T, DsTable DT
     for (int w = lane; w < nb * kPodWords; w += kWave) s_podw[w] = pw[w];
     const uint64_t* dw = reinterpret_cast<const uint64_t*>(dpods + first);
     for (int w = lane; w < nb * kDsPodWords; w += kWave) s_dpw[w] = dw[w];
+    if (nq > 0) {  // ElasticQuota rows (cpu, memory, device resources) + the pods' device requests
+      const uint64_t* qw = reinterpret_cast<const uint64_t*>(quotas);
+      uint64_t* sq = reinterpret_cast<uint64_t*>(s_q);
+      for (int w = lane; w < nq * (int)(sizeof(QuotaRow) / 8); w += kWave) sq[w] = qw[w];
+      for (int w = lane; w < nb * kQuotaRes; w += kWave) s_qdev[w] = qdev[(size_t)first * kQuotaRes + w];
+    }
   }
   for (int w = lane; w < bitmap_words; w += kWave) bitmap[w] = 0;
   // stage the round-start row of every pod's top candidate (the usual winner): a first assume onto it then
@@ -1391,13 +1402,14 @@ __global__ __launch_bounds__(kWave) void resolve_round_ds(DevTable T, DsTable DT
   uint64_t my_out = 0;
   int32_t my_minors = 0;
   int nM = 0, consumed = 0;
-  DevQuota ql = quota_load(quotas, nq, lane);
   for (int j = 0; j < nb; ++j) {
     const uint64_t key = s_cand[(size_t)j * kCandStride + lane];
     const uint64_t ub = s_cand[(size_t)j * kCandStride + kC];
     const DevPod p = s_pods[j];
     const DsPod dp = s_dp[j];
-    if (nq > 0 && !quota_admit(ql, p)) {  // ElasticQuota PreFilter rejects
+    QuotaReq qr;
+    if (p.quota >= 0) qr = quota_req(p, s_qdev + (size_t)j * kQuotaRes);
+    if (p.quota >= 0 && !quota_row_admit(s_q[p.quota], qr, (p.flags & P_NONPREEMPT) != 0)) {  // PreFilter rejects
       my_out = lane == j ? 0 : my_out;
       my_minors = lane == j ? 0 : my_minors;
       ++consumed;
@@ -1507,7 +1519,7 @@ __global__ __launch_bounds__(kWave) void resolve_round_ds(DevTable T, DsTable DT
     }
     placed = __builtin_amdgcn_readlane(placed, owner);
     minors = __builtin_amdgcn_readlane(minors, owner);
-    if (placed && nq > 0) quota_charge(ql, p, lane);
+    if (placed && p.quota >= 0 && lane == 0) quota_row_charge(s_q[p.quota], qr, (p.flags & P_NONPREEMPT) != 0);
     my_out = lane == j ? (placed ? best : 0) : my_out;
     my_minors = lane == j ? (placed ? minors : 0) : my_minors;
     __syncthreads();
@@ -1520,7 +1532,11 @@ __global__ __launch_bounds__(kWave) void resolve_round_ds(DevTable T, DsTable DT
     out_keys[first + lane] = my_out;
     out_minors[first + lane] = my_minors;
   }
-  if (lane < nq) quotas[lane] = ql;
+  if (nq > 0) {
+    const uint64_t* sq = reinterpret_cast<const uint64_t*>(s_q);
+    uint64_t* qw = reinterpret_cast<uint64_t*>(quotas);
+    for (int w = lane; w < nq * (int)(sizeof(QuotaRow) / 8); w += kWave) qw[w] = sq[w];
+  }
   __threadfence();
   if (lane == 0) {
     ctl[0] = first + consumed;
@@ -1743,7 +1759,8 @@ struct kg_engine {
   DevBuf<uint64_t> dsnorm;     // [B]
   DevBuf<uint32_t> dsval;      // [B][nt_local·256]: packed (Fit+LoadAware total, raw DeviceShare) per (pod, node)
   // ElasticQuota admission table (kg_quotas_set)
-  DevBuf<DevQuota> quotas;     // [KG_MAX_QUOTAS]
+  DevBuf<QuotaRow> quotas;     // [KG_MAX_QUOTAS] full kg_quota rows (cpu, memory, device resources)
+  DevBuf<int64_t> qdev;        // [staged + kMaxB][kQuotaRes]: the pod's device requests (quota dims 2..7)
   int nq = 0;
   // Reservation (profile enables it): per-node slots, per-pod owner/affinity, Reserve's slots, pass scratch
   bool rsv_on = false;
@@ -1754,7 +1771,7 @@ struct kg_engine {
   DevBuf<int32_t> out_rslot;    // [staged + kMaxB]
   DevBuf<uint64_t> rsv_val;     // [capacity] packed per-node pass-1 values
   DevBuf<unsigned long long> rsv_ws;  // [4]: [3] = pod cursor
-  DevBuf<uint64_t> rsv_part;    // [3][blocks] per-block partials (preferred-node key, max raw, max key)
+  DevBuf<uint64_t> rsv_part;    // [4][blocks] per-block partials (preferred-node key, max raw, max key, max ds raw)
   // live kernel timing (kg_profile_enable): HIP event pairs around every launch of the round runners, on the
   // launch's own stream, folded into per-kind totals after each batch synchronises
   bool prof_on = false;
@@ -1821,8 +1838,8 @@ int validate_config(const kg_config* c) {
   if (c->batch_pods < 0 || c->batch_pods > kMaxB) return fail(KG_E_INVALID, "batch_pods must be in [1,%d]", kMaxB);
   if (c->reservation_filter || c->reservation_score) {
     if (c->weight_reservation < 0 || c->weight_reservation > 1000000) return fail(KG_E_INVALID, "Reservation weight out of range");
-    if (c->numa_filter || c->numa_score || c->ds_filter || c->ds_score)
-      return fail(KG_E_UNSUPPORTED, "Reservation with NodeNUMAResource / DeviceShare in one profile is not accelerated");
+    if (c->numa_filter || c->numa_score)
+      return fail(KG_E_UNSUPPORTED, "Reservation with NodeNUMAResource in one profile is not accelerated");
   }
   if (c->ds_filter || c->ds_score) {
     if (c->weight_deviceshare < 0 || c->weight_deviceshare > 1000000) return fail(KG_E_INVALID, "DeviceShare weight out of range");
@@ -1980,6 +1997,12 @@ int decode_pod(const kg_engine* e, const kg_pod& p, DevPod& d) {
   d.pad = 0;
   d.quota = (int32_t)std::min<int64_t>(std::max<int64_t>(p.quota_id, 0), 1 << 20) - 1;
   if (p.flags & KG_POD_NON_PREEMPTIBLE) d.flags |= P_NONPREEMPT;
+  // request-key presence (PodRequestsAndLimits keys): explicit with KG_POD_REQUEST_KEYS, else by value
+  const bool kc = (p.flags & KG_POD_REQUEST_KEYS) ? (p.flags & KG_POD_CPU_KEY) != 0 : d.req_cpu != 0;
+  const bool km = (p.flags & KG_POD_REQUEST_KEYS) ? (p.flags & KG_POD_MEM_KEY) != 0 : d.req_mem != 0;
+  d.flags |= (kc ? P_CPU_KEY : 0u) | (km ? P_MEM_KEY : 0u);
+  for (int r = 0; r < KG_QUOTA_RES - 2; ++r)
+    if (p.device_requests[r] != 0) d.flags |= P_QDEV;
   return 0;
 }
 
@@ -2375,9 +2398,9 @@ int run_batch(kg_engine* e, const RoundGeom& g, int64_t cur, int64_t end, int64_
 }
 
 // ---- DeviceShare rounds: cursor-driven, unpipelined, all on rs[0] ----
-size_t resolve_ds_lds_bytes(const RoundGeom& g, int nb) {
-  return ((size_t)nb * (kCandStride + kPodWords + kDsPodWords + kDsNodeWords) + (size_t)kWave * kDsNodeWords) * 8 +
-         (size_t)nb * sizeof(Row) + (size_t)g.bitmap_words * 4;
+size_t resolve_ds_lds_bytes(const RoundGeom& g, int nb, int nq) {
+  return ((size_t)nb * (kCandStride + kPodWords + kDsPodWords + kDsNodeWords + kQuotaRes) + (size_t)kWave * kDsNodeWords) * 8 +
+         (size_t)nq * sizeof(QuotaRow) + (size_t)nb * sizeof(Row) + (size_t)g.bitmap_words * 4;
 }
 
 void launch_round_ds(kg_engine* e, const RoundGeom& g, int64_t end, hipStream_t st, int which = -1) {
@@ -2411,11 +2434,13 @@ void launch_round_ds(kg_engine* e, const RoundGeom& g, int64_t end, hipStream_t 
   }
   if (which < 0 || which == 2) {
     t = prof_begin(e, st);
-    resolve_round_ds<<<1, kWave, resolve_ds_lds_bytes(g, g.B), st>>>(e->T, DT, e->pods.p, e->dpods.p, e->cursor.p,
-                                                                     end, g.B, cand_slot(e, g, 0), e->dsnorm.p,
-                                                                     e->dsval.p, (int64_t)g.nt_local * kTile, e->P,
-                                                                     e->DP, e->out_keys.p, e->out_minors.p,
-                                                                     g.bitmap_words, e->quotas.p, e->nq);
+    resolve_round_ds<<<1, kWave, resolve_ds_lds_bytes(g, g.B, e->nq), st>>>(e->T, DT, e->pods.p, e->dpods.p,
+                                                                            e->cursor.p, end, g.B, cand_slot(e, g, 0),
+                                                                            e->dsnorm.p, e->dsval.p,
+                                                                            (int64_t)g.nt_local * kTile, e->P, e->DP,
+                                                                            e->out_keys.p, e->out_minors.p,
+                                                                            g.bitmap_words, e->quotas.p, e->nq,
+                                                                            e->qdev.p);
     prof_end(e, KG_PROF_RESOLVE, t, st);
   }
 }
@@ -2440,7 +2465,10 @@ int prepare_rounds(kg_engine* e, RoundGeom& g) {
     return fail(KG_E_UNSUPPORTED, "resolver LDS %zu B > %zu B: fewer nodes or a smaller batch_pods",
                 resolve_lds_bytes(g, g.B), kMaxLds);
   const size_t D = (size_t)g.depth;
+  const size_t lists_n = e->lists.n;
   if (int rc = e->lists.ensure(D * g.B * g.nt_local * kR)) return rc;
+  if (e->lists.n != lists_n)  // fresh lists hold no keys (DeviceShare rounds merge every one of the B slots)
+    HIP_TRY(hipMemsetAsync(e->lists.p, 0, e->lists.n * 8, e->stream));
   if (int rc = e->cand.ensure(D * g.B * kCandStride)) return rc;
   if (e->n_ranks > 1)
     if (int rc = e->gathered.ensure(D * e->n_ranks * g.B * kCandStride)) return rc;
@@ -2460,27 +2488,41 @@ double now_s() {
 // Reservation profile: one FIFO pod per device pass (rsv_eval → rsv_select; Reserve in the next rsv_eval),
 // kRsvGroup passes + the group-closing rsv_apply per hipGraph launch.  The pod index lives in the device cursor ws[3]; passes past `end` are no-ops.
 constexpr int kRsvGroup = 32;
+RsvExt rsv_ext(kg_engine* e) {
+  RsvExt X;
+  X.ds = e->ds_on ? e->ds_d.p : nullptr;
+  X.dpods = e->ds_on ? e->dpods.p : nullptr;
+  X.DP = e->DP;
+  X.quotas = e->quotas.p;
+  X.qdev = e->qdev.p;
+  X.out_minors = e->ds_on ? e->out_minors.p : nullptr;
+  X.nq = e->nq;
+  return X;
+}
+
 int run_rsv(kg_engine* e, int64_t first, int64_t count, kg_stats* stats, double t0) {
   if (int rc = sync_static(e)) return rc;
   const int64_t n = e->n_nodes, end = first + count;
   if (count > 0 && n > 0) {
     const unsigned blocks = (unsigned)((n + kRsvThreads - 1) / kRsvThreads);
+    const RsvExt X = rsv_ext(e);
     const unsigned long long init[4] = {0, 0, 0, (unsigned long long)first};
     HIP_TRY(hipMemcpyAsync(e->rsv_ws.p, init, 32, hipMemcpyHostToDevice, e->stream));
     auto issue_group = [&]() {
       for (int g = 0; g < kRsvGroup; ++g) {
         size_t t = prof_begin(e, e->stream);
         rsv_eval<<<blocks, kRsvThreads, 0, e->stream>>>(e->T, e->rsv_d.p, e->rsv_nd.p, e->pods.p, e->rpods.p, end, n, g,
-                                                         e->P, e->RP, e->rsv_val.p, e->rsv_part.p, e->out_keys.p,
+                                                         e->P, e->RP, X, e->rsv_val.p, e->rsv_part.p, e->out_keys.p,
                                                          e->out_rslot.p, e->rsv_ws.p);
         prof_end(e, KG_PROF_RSV_EVAL, t, e->stream);
         t = prof_begin(e, e->stream);
-        rsv_select<<<blocks, kRsvThreads, 0, e->stream>>>(e->rsv_val.p, end, n, g, e->RP, e->rsv_part.p, e->rsv_ws.p);
+        rsv_select<<<blocks, kRsvThreads, 0, e->stream>>>(e->rsv_val.p, e->pods.p, end, n, g, e->RP, X, e->rsv_part.p,
+                                                           e->rsv_ws.p);
         prof_end(e, KG_PROF_RSV_SELECT, t, e->stream);
       }
       size_t t = prof_begin(e, e->stream);
       rsv_apply<<<1, kWave, 0, e->stream>>>(e->T, e->rsv_d.p, e->rsv_val.p, e->pods.p, end, (int)blocks, kRsvGroup - 1,
-                                            e->rsv_part.p, e->out_keys.p, e->out_rslot.p, e->rsv_ws.p);
+                                            X, e->rsv_part.p, e->out_keys.p, e->out_rslot.p, e->rsv_ws.p);
       prof_end(e, KG_PROF_RSV_APPLY, t, e->stream);
     };
     // KG_RSV_NO_GRAPH=1: plain stream launches (profilers whose kernel tracing does not follow graph launches);
@@ -2523,14 +2565,15 @@ int decode_node_rsv(const kg_node_reservations& r, RsvNode& d, int32_t& ns) {
   if (r.n < 0 || r.n > KG_MAX_RSV_SLOTS) return fail(KG_E_INVALID, "reservation slot count %lld", (long long)r.n);
   ns = (int32_t)r.n;
   for (int s = 0; s < ns; ++s) {
-    if (r.allocatable_cpu[s] <= 0 || r.allocatable_mem[s] <= 0 || r.allocatable_cpu[s] > (int64_t(1) << 40) ||
+    if (r.allocatable_cpu[s] < 0 || r.allocatable_mem[s] < 0 || r.allocatable_cpu[s] > (int64_t(1) << 40) ||
         r.allocatable_mem[s] > (int64_t(1) << 46))
-      return fail(KG_E_UNSUPPORTED, "reservation slot %d: allocatable cpu and memory must be in (0, 2^40] / (0, 2^46]", s);
+      return fail(KG_E_UNSUPPORTED, "reservation slot %d: allocatable cpu / memory outside [0, 2^40] / [0, 2^46]", s);
     if (r.allocated_cpu[s] < 0 || r.allocated_mem[s] < 0 || r.allocated_cpu[s] > (int64_t(1) << 40) ||
         r.allocated_mem[s] > (int64_t(1) << 46) || r.assigned[s] < 0 || r.assigned[s] > INT32_MAX / 2)
       return fail(KG_E_INVALID, "reservation slot %d: allocated / assigned out of range", s);
     if (r.order[s] < 0 || r.order[s] >= INT32_MAX) return fail(KG_E_UNSUPPORTED, "reservation slot %d: order outside [0, 2^31-1)", s);
-    if (r.owner[s] < 0 || r.owner[s] > INT32_MAX) return fail(KG_E_INVALID, "reservation slot %d: owner outside [0, 2^31)", s);
+    if (r.owner[s] < 0 || r.owner[s] >= KG_MAX_OWNER_GROUPS)
+      return fail(KG_E_UNSUPPORTED, "reservation slot %d: owner group outside [0, %d)", s, KG_MAX_OWNER_GROUPS);
     if (r.policy[s] < KG_RSV_POLICY_DEFAULT || r.policy[s] > KG_RSV_POLICY_RESTRICTED) return fail(KG_E_INVALID, "reservation policy");
     d.alloc_cpu[s] = r.allocatable_cpu[s];
     d.alloc_mem[s] = r.allocatable_mem[s];
@@ -2701,7 +2744,7 @@ int kg_engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank, int
     if (int rc = e->rsv_nd.ensure(cap)) return bail(rc);
     if (int rc = e->rsv_val.ensure(cap)) return bail(rc);
     if (int rc = e->rsv_ws.ensure(4)) return bail(rc);
-    if (int rc = e->rsv_part.ensure(3 * ((cap + kRsvThreads - 1) / kRsvThreads) + 3)) return bail(rc);
+    if (int rc = e->rsv_part.ensure(4 * ((cap + kRsvThreads - 1) / kRsvThreads) + 4)) return bail(rc);
     if (hipMemset(e->rsv_nd.p, 0, cap * 4) != hipSuccess || hipMemset(e->rsv_ws.p, 0, 32) != hipSuccess)
       return bail(fail(KG_E_DEVICE, "hipMemset"));
   }
@@ -2723,8 +2766,9 @@ int kg_engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank, int
     for (auto& d : e->ds_host) d.first = -1;
     if (hipMemcpy(e->ds_d.p, e->ds_host.data(), cap * sizeof(DsNode), hipMemcpyHostToDevice) != hipSuccess)
       return bail(fail(KG_E_DEVICE, "hipMemcpy"));
-    const int lds = (int)(kMaxNodes / 8 + ((size_t)32 * (kCandStride + kPodWords + kDsPodWords + kDsNodeWords) +
-                                           (size_t)kWave * kDsNodeWords) * 8 + 32 * sizeof(Row));
+    const int lds = (int)(kMaxNodes / 8 + ((size_t)32 * (kCandStride + kPodWords + kDsPodWords + kDsNodeWords + kQuotaRes) +
+                                           (size_t)kWave * kDsNodeWords) * 8 + KG_MAX_QUOTAS * sizeof(QuotaRow) +
+                          32 * sizeof(Row));
     if (hipFuncSetAttribute((const void*)resolve_round_ds, hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess)
       return bail(fail(KG_E_DEVICE, "hipFuncSetAttribute(resolve_round_ds LDS)"));
   }
@@ -2814,6 +2858,7 @@ void kg_engine_destroy(kg_engine* e) {
   e->out_cpus.release();
   e->ds_d.release();
   e->quotas.release();
+  e->qdev.release();
   e->dpods.release();
   e->out_minors.release();
   e->dsmax.release();
@@ -2926,11 +2971,6 @@ int kg_pods_stage(kg_engine* e, const kg_pod* pods, int64_t n) {
     if (pods[k].quota_id < 0 || pods[k].quota_id > e->nq)
       return fail(KG_E_INVALID, "pod %lld: quota_id %lld outside the quota table (%d quotas)", (long long)k,
                   (long long)pods[k].quota_id, e->nq);
-    if (pods[k].quota_id > 0)
-      for (int r = 0; r < KG_DEV_RES_MAX; ++r)
-        if (pods[k].device_requests[r] != 0)
-          return fail(KG_E_UNSUPPORTED, "pod %lld: ElasticQuota admission covers cpu/memory; device requests in a "
-                      "quota are not accelerated", (long long)k);
   }
   std::vector<DevPod> h(std::max<int64_t>(n, 1));
   for (int64_t k = 0; k < n; ++k)
@@ -2938,6 +2978,13 @@ int kg_pods_stage(kg_engine* e, const kg_pod* pods, int64_t n) {
   if (int rc = e->pods.ensure(n + kMaxB)) return rc;
   if (int rc = e->out_keys.ensure(n + kMaxB)) return rc;
   if (n > 0) HIP_TRY(hipMemcpyAsync(e->pods.p, h.data(), n * sizeof(DevPod), hipMemcpyHostToDevice, e->stream));
+  if (e->ds_on || e->rsv_on) {  // the pods' device requests as ElasticQuota dims (cpu, memory, 6 device resources)
+    std::vector<int64_t> hq((size_t)std::max<int64_t>(n, 1) * kQuotaRes, 0);
+    for (int64_t k = 0; k < n; ++k)
+      for (int r = 0; r < KG_QUOTA_RES - 2; ++r) hq[(size_t)k * kQuotaRes + r] = pods[k].device_requests[r];
+    if (int rc = e->qdev.ensure((size_t)(n + kMaxB) * kQuotaRes)) return rc;
+    if (n > 0) HIP_TRY(hipMemcpyAsync(e->qdev.p, hq.data(), (size_t)n * kQuotaRes * 8, hipMemcpyHostToDevice, e->stream));
+  }
   HIP_TRY(hipMemsetAsync(e->out_keys.p, 0, (n + kMaxB) * 8, e->stream));
   std::vector<NumaPod> hn;
   if (e->numa_on) {
@@ -2968,11 +3015,9 @@ int kg_pods_stage(kg_engine* e, const kg_pod* pods, int64_t n) {
   if (e->rsv_on) {
     std::vector<RsvPod> hr(std::max<int64_t>(n, 1));
     for (int64_t k = 0; k < n; ++k) {
-      if (pods[k].quota_id > 0) return fail(KG_E_UNSUPPORTED, "pod %lld: ElasticQuota with Reservation is not accelerated", (long long)k);
-      if (pods[k].reservation_owner < 0 || pods[k].reservation_owner > INT32_MAX)
-        return fail(KG_E_INVALID, "pod %lld: reservation_owner outside [0, 2^31)", (long long)k);
-      hr[k].owner = (int32_t)pods[k].reservation_owner;
+      hr[k].owner_mask = (uint64_t)pods[k].reservation_owner_mask;
       hr[k].flags = (pods[k].reservation_flags & KG_POD_RSV_AFFINITY) ? RP_AFFINITY : 0u;
+      hr[k].pad = 0;
     }
     if (int rc = e->rpods.ensure(n + kMaxB)) return rc;
     if (int rc = e->out_rslot.ensure(n + kMaxB)) return rc;
@@ -3275,20 +3320,18 @@ int kg_pods_evaluate_device(kg_engine* e, const kg_pod* pod, int32_t* out_pass, 
 int kg_quotas_set(kg_engine* e, const kg_quota* quotas, int64_t n) {
   if (!e || (n > 0 && !quotas)) return fail(KG_E_INVALID, "null argument");
   if (n < 0 || n > KG_MAX_QUOTAS) return fail(KG_E_UNSUPPORTED, "%lld quotas > %d", (long long)n, KG_MAX_QUOTAS);
-  std::vector<DevQuota> h(std::max<int64_t>(n, 1));
+  static_assert(sizeof(kg_quota) == sizeof(QuotaRow), "kg_quota is the device row");
   for (int64_t k = 0; k < n; ++k) {
     const kg_quota& q = quotas[k];
-    for (int r = 0; r < 2; ++r)
+    for (int r = 0; r < KG_QUOTA_RES; ++r)
       if (q.used[r] < 0 || q.non_preemptible_used[r] < 0 || q.used_limit[r] < -1 || q.min[r] < -1 ||
           q.used[r] > (1ll << 60) || q.used_limit[r] > (1ll << 60) || q.min[r] > (1ll << 60) ||
           q.non_preemptible_used[r] > (1ll << 60))
         return fail(KG_E_INVALID, "quota %lld: quantity out of range", (long long)k);
-    h[k] = DevQuota{q.used[0], q.used[1], q.non_preemptible_used[0], q.non_preemptible_used[1], q.used_limit[0],
-                    q.used_limit[1], q.min[0], q.min[1]};
   }
   if (int rc = e->quotas.ensure(KG_MAX_QUOTAS)) return rc;
   if (n > 0) {
-    HIP_TRY(hipMemcpyAsync(e->quotas.p, h.data(), n * sizeof(DevQuota), hipMemcpyHostToDevice, e->stream));
+    HIP_TRY(hipMemcpyAsync(e->quotas.p, quotas, n * sizeof(QuotaRow), hipMemcpyHostToDevice, e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
   }
   e->nq = (int)n;
@@ -3299,13 +3342,8 @@ int kg_quotas_read(kg_engine* e, kg_quota* out, int64_t n) {
   if (!e || (n > 0 && !out)) return fail(KG_E_INVALID, "null argument");
   if (n != e->nq) return fail(KG_E_INVALID, "the quota table holds %d quotas", e->nq);
   if (n == 0) return 0;
-  std::vector<DevQuota> h(n);
-  HIP_TRY(hipMemcpyAsync(h.data(), e->quotas.p, n * sizeof(DevQuota), hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipMemcpyAsync(out, e->quotas.p, n * sizeof(QuotaRow), hipMemcpyDeviceToHost, e->stream));
   HIP_TRY(hipStreamSynchronize(e->stream));
-  for (int64_t k = 0; k < n; ++k) {
-    const DevQuota& d = h[k];
-    out[k] = kg_quota{{d.used_c, d.used_m}, {d.np_c, d.np_m}, {d.lim_c, d.lim_m}, {d.min_c, d.min_m}};
-  }
   return 0;
 }
 
@@ -3326,18 +3364,19 @@ static int bench_rsv(kg_engine* e, int which, int iters, double* avg_ms, double*
   const unsigned blocks = (unsigned)((n + kRsvThreads - 1) / kRsvThreads);
   const unsigned long long zero[4] = {0, 0, 0, 0};
   HIP_TRY(hipMemcpyAsync(e->rsv_ws.p, zero, 32, hipMemcpyHostToDevice, e->stream));
+  const RsvExt X = rsv_ext(e);
   auto launch = [&]() {
     if (which == 0)
       rsv_eval<<<blocks, kRsvThreads, 0, e->stream>>>(e->T, e->rsv_d.p, e->rsv_nd.p, e->pods.p, e->rpods.p,
-                                                       e->n_staged, n, 0, e->P, e->RP, e->rsv_val.p, e->rsv_part.p,
+                                                       e->n_staged, n, 0, e->P, e->RP, X, e->rsv_val.p, e->rsv_part.p,
                                                        e->out_keys.p, e->out_rslot.p, e->rsv_ws.p);
     else
-      rsv_select<<<blocks, kRsvThreads, 0, e->stream>>>(e->rsv_val.p, e->n_staged, n, 0, e->RP, e->rsv_part.p,
+      rsv_select<<<blocks, kRsvThreads, 0, e->stream>>>(e->rsv_val.p, e->pods.p, e->n_staged, n, 0, e->RP, X, e->rsv_part.p,
                                                          e->rsv_ws.p);
   };
   if (which == 1)  // rsv_select needs the packed values and partials of a real pass
     rsv_eval<<<blocks, kRsvThreads, 0, e->stream>>>(e->T, e->rsv_d.p, e->rsv_nd.p, e->pods.p, e->rpods.p,
-                                                     e->n_staged, n, 0, e->P, e->RP, e->rsv_val.p, e->rsv_part.p,
+                                                     e->n_staged, n, 0, e->P, e->RP, X, e->rsv_val.p, e->rsv_part.p,
                                                      e->out_keys.p, e->out_rslot.p, e->rsv_ws.p);
   launch();  // warm
   hipEvent_t a, b;
@@ -3354,7 +3393,18 @@ static int bench_rsv(kg_engine* e, int which, int iters, double* avg_ms, double*
   HIP_TRY(hipMemcpyAsync(e->rsv_ws.p, zero, 32, hipMemcpyHostToDevice, e->stream));
   HIP_TRY(hipStreamSynchronize(e->stream));
   if (avg_ms) *avg_ms = ms / iters;
-  if (algo_bytes) *algo_bytes = which == 0 ? (double)n * (76 + 4 + 8) + (double)with_slots * sizeof(RsvNode) : (double)n * 8;
+  // rsv_eval: the Fit/LoadAware columns, rsv_n and the packed value per node, the slot rows of nodes holding
+  // reservations and — for a device pod in a DeviceShare profile — the 272-B GPU row of every node
+  bool dev_pod = false;
+  if (e->ds_on) {
+    DsPod d0;
+    HIP_TRY(hipMemcpy(&d0, e->dpods.p, sizeof(DsPod), hipMemcpyDeviceToHost));
+    dev_pod = !d0.skip;
+  }
+  if (algo_bytes)
+    *algo_bytes = which == 0 ? (double)n * (76 + 4 + 8) + (double)with_slots * sizeof(RsvNode) +
+                                   (dev_pod ? (double)n * sizeof(DsNode) : 0.0)
+                             : (double)n * 8;
   return 0;
 }
 

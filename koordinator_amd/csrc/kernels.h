@@ -65,6 +65,9 @@ constexpr uint32_t P_DAEMONSET = 1u << 1;     // LoadAware Filter bypass (load_a
 constexpr uint32_t P_PROD = 1u << 2;          // priority class koord-prod
 constexpr uint32_t P_LA_PROD_SCORE = 1u << 3; // prod && ScoreAccordingProdUsage (load_aware.go:291)
 constexpr uint32_t P_NONPREEMPT = 1u << 4;    // extension.IsPodNonPreemptible (ElasticQuota min check)
+constexpr uint32_t P_CPU_KEY = 1u << 5;       // cpu is a key of the pod's requests (PodRequestsAndLimits)
+constexpr uint32_t P_MEM_KEY = 1u << 6;       // memory is a key of the pod's requests
+constexpr uint32_t P_QDEV = 1u << 7;          // the pod requests device resources (quota dims 2.. are keys)
 
 struct DevTable {
   int64_t *alloc_cpu, *alloc_mem;        // NodeInfo.Allocatable
@@ -635,31 +638,50 @@ __device__ __forceinline__ uint64_t wave_max_key(uint64_t k) {
 
 // ---------------------------------------------------------------------------------------------------
 // ElasticQuota admission inside the FIFO resolvers (elasticquota/plugin.go:211-256 PreFilter, :332-346 Reserve).
-// Quota q lives in lane q of the resolver wave (≤ 64 quotas); a pod's PreFilter check reads it by readlane and a
-// placed pod is charged by that lane, so pod j+1's check sees pod j's Reserve, as in the reference.
+// The quota table in HBM holds KG_QUOTA_RES resources per quota (cpu, memory, then the 6 device resources of
+// kg_pod.device_requests).  The lane-based resolvers (Fit + LoadAware, NodeNUMAResource) only see pods without
+// device requests, so they keep quota q's cpu / memory part in lane q (DevQuota) and leave the device dims as they
+// are; pod j+1's check reads it by readlane and a placed pod is charged by that lane, so pod j+1's check sees pod j's
+// Reserve, as in the reference.  The DeviceShare / Reservation resolvers use the full rows (QuotaRow).
 // ---------------------------------------------------------------------------------------------------
+constexpr int kQuotaRes = 8;
+struct QuotaRow {  // one kg_quota on the device (same field order, int64)
+  int64_t used[kQuotaRes], np[kQuotaRes], lim[kQuotaRes], min[kQuotaRes];
+};
+static_assert(sizeof(QuotaRow) == 256, "QuotaRow layout");
+
 struct DevQuota {
   int64_t used_c, used_m, np_c, np_m, lim_c, lim_m, min_c, min_m;
 };
 
-__device__ __forceinline__ DevQuota quota_load(const DevQuota* __restrict__ q, int nq, int lane) {
+__device__ __forceinline__ DevQuota quota_load(const QuotaRow* __restrict__ q, int nq, int lane) {
   DevQuota r{0, 0, 0, 0, 0, 0, 0, 0};
-  if (lane < nq) r = q[lane];
+  if (lane < nq) {
+    const QuotaRow& x = q[lane];
+    r = DevQuota{x.used[0], x.used[1], x.np[0], x.np[1], x.lim[0], x.lim[1], x.min[0], x.min[1]};
+  }
   return r;
 }
+__device__ __forceinline__ void quota_store(QuotaRow* __restrict__ q, int nq, int lane, const DevQuota& r) {
+  if (lane < nq) {
+    QuotaRow& x = q[lane];
+    x.used[0] = r.used_c, x.used[1] = r.used_m, x.np[0] = r.np_c, x.np[1] = r.np_m;
+  }
+}
 
-// quotav1.LessThanOrEqual(Mask(Add(request, used), ResourceNames(request)), limit) over cpu / memory (wave-uniform);
-// a limit < 0 is a key absent from the limit list, which LessThanOrEqual does not compare
+// quotav1.LessThanOrEqual(Mask(Add(request, used), ResourceNames(request)), limit) over cpu / memory (wave-uniform):
+// only the pod's request keys are compared, and only where the limit has the key (a limit < 0 is absent)
 __device__ __forceinline__ bool quota_admit(const DevQuota& ql, const DevPod& p) {
   if (p.quota < 0) return true;
   const int q = p.quota;
+  const bool kc = (p.flags & P_CPU_KEY) != 0, km = (p.flags & P_MEM_KEY) != 0;
   const int64_t uc = (int64_t)readlane_u64((uint64_t)ql.used_c, q), um = (int64_t)readlane_u64((uint64_t)ql.used_m, q);
   const int64_t lc = (int64_t)readlane_u64((uint64_t)ql.lim_c, q), lm = (int64_t)readlane_u64((uint64_t)ql.lim_m, q);
-  bool ok = (p.req_cpu == 0 || lc < 0 || uc + p.req_cpu <= lc) && (p.req_mem == 0 || lm < 0 || um + p.req_mem <= lm);
+  bool ok = (!kc || lc < 0 || uc + p.req_cpu <= lc) && (!km || lm < 0 || um + p.req_mem <= lm);
   if (p.flags & P_NONPREEMPT) {
     const int64_t nc = (int64_t)readlane_u64((uint64_t)ql.np_c, q), nm = (int64_t)readlane_u64((uint64_t)ql.np_m, q);
     const int64_t mc = (int64_t)readlane_u64((uint64_t)ql.min_c, q), mm = (int64_t)readlane_u64((uint64_t)ql.min_m, q);
-    ok = ok && (p.req_cpu == 0 || mc < 0 || nc + p.req_cpu <= mc) && (p.req_mem == 0 || mm < 0 || nm + p.req_mem <= mm);
+    ok = ok && (!kc || mc < 0 || nc + p.req_cpu <= mc) && (!km || mm < 0 || nm + p.req_mem <= mm);
   }
   return ok;
 }
@@ -672,6 +694,45 @@ __device__ __forceinline__ void quota_charge(DevQuota& ql, const DevPod& p, int 
   if (p.flags & P_NONPREEMPT) {
     ql.np_c += p.req_cpu;
     ql.np_m += p.req_mem;
+  }
+}
+
+// Full-row forms (device requests included): the pod's request over the quota resources is (cpu, memory,
+// dev[0..5]) with key flags; `add` (nullable) = earlier usage not yet in the row.
+struct QuotaReq {
+  int64_t r[kQuotaRes];
+  uint32_t keys;  // bit d: resource d is a key of the pod's requests
+};
+__device__ __forceinline__ QuotaReq quota_req(const DevPod& p, const int64_t* __restrict__ dev6) {
+  QuotaReq q;
+  q.r[0] = p.req_cpu;
+  q.r[1] = p.req_mem;
+  q.keys = ((p.flags & P_CPU_KEY) ? 1u : 0u) | ((p.flags & P_MEM_KEY) ? 2u : 0u);
+#pragma unroll
+  for (int d = 0; d < kQuotaRes - 2; ++d) {
+    q.r[2 + d] = (p.flags & P_QDEV) ? dev6[d] : 0;
+    q.keys |= q.r[2 + d] != 0 ? (1u << (2 + d)) : 0u;
+  }
+  return q;
+}
+__device__ __forceinline__ bool quota_row_admit(const QuotaRow& Q, const QuotaReq& rq, bool nonpreempt,
+                                                const int64_t* add_used = nullptr, const int64_t* add_np = nullptr) {
+  // add_used / add_np (nullable): usage of earlier placements not yet charged into the row
+  bool ok = true;
+#pragma unroll
+  for (int d = 0; d < kQuotaRes; ++d) {
+    if (!((rq.keys >> d) & 1u)) continue;
+    const int64_t au = add_used ? add_used[d] : 0, an = add_np ? add_np[d] : 0;
+    if (Q.lim[d] >= 0 && Q.used[d] + au + rq.r[d] > Q.lim[d]) ok = false;
+    if (nonpreempt && Q.min[d] >= 0 && Q.np[d] + an + rq.r[d] > Q.min[d]) ok = false;
+  }
+  return ok;
+}
+__device__ __forceinline__ void quota_row_charge(QuotaRow& Q, const QuotaReq& rq, bool nonpreempt) {
+#pragma unroll
+  for (int d = 0; d < kQuotaRes; ++d) {
+    Q.used[d] += rq.r[d];
+    if (nonpreempt) Q.np[d] += rq.r[d];
   }
 }
 

@@ -1,17 +1,25 @@
-// Reservation plugin on the device (SURVEY §8a A15–A18): per-node reservation slots in HBM and the per-pod
-// pass that restores NodeInfo for matched / unmatched reservations (BeforePreFilter, transformer.go:49-346), runs
-// NodeResourcesFit + LoadAware on the restored row, the Reservation Filter (plugin.go:357-428), the nomination
-// (nominator.go:76-134) and Score (scoring.go:103-203) with the PreScore preferred node, DefaultNormalizeScore,
-// then Reserve (plugin.go:521-559).
+// Reservation plugin on the device (SURVEY §8a A15–A18), composed with DeviceShare (A19–A21) and ElasticQuota
+// admission (A24) for config C5: per-node reservation slots in HBM and the per-pod pass that restores NodeInfo for
+// matched / unmatched reservations (BeforePreFilter, transformer.go:49-346), runs NodeResourcesFit + LoadAware on the
+// restored row, the Reservation Filter (plugin.go:357-428), the DeviceShare Filter (deviceshare/plugin.go:280-330),
+// the nomination (nominator.go:76-134) and both Scores (reservation/scoring.go:103-203, deviceshare/scoring.go:34-89)
+// with the PreScore preferred node and DefaultNormalizeScore, then Reserve (reservation/plugin.go:521-559,
+// deviceshare/plugin.go:385-438, elasticquota/plugin.go:332-346).
 //
 // One pod per pass, two kernels (wide pass, normalise + argmax pass); pod j's Reserve runs in pod j+1's wide-pass
 // prologue by the thread owning the winner row.  A group of kRsvGroup pods is captured in one hipGraph, closed by
 // a one-wave kernel that reserves the group's last pod and advances the device cursor.
+//
+// Reservations here hold cpu / memory (an allocatable of 0 = the key is absent).  DeviceShare restores device state
+// only for reservations whose reserve pod holds devices (deviceshare/reservation.go:132-150), so for these it keeps
+// no reservation state: its Filter / Score are the node-level ones, and its FilterReservation rejects every
+// reservation for a pod that requests devices (plugin.go:462-486) — such a pod is never nominated into one.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "../../include/koordgpu.h"
+#include "ds_dev.h"
 #include "kernels.h"
 
 namespace kg {
@@ -19,34 +27,54 @@ namespace kg {
 constexpr int kRsvSlots = KG_MAX_RSV_SLOTS;
 constexpr uint32_t RS_AVAIL = 1u << 0, RS_ONCE = 1u << 1, RS_UNSCHED = 1u << 2;  // policy in bits 4..5
 constexpr uint32_t RP_AFFINITY = 1u << 0;
+constexpr int64_t kDefaultMilliCpu = 100, kDefaultMemory = 200ll << 20;  // schedutil.GetNonzeroRequests defaults
 
 struct RsvNode {  // 192 B: one node's slots, read only for nodes with slots (rsv_n[i] > 0)
-  int64_t alloc_cpu[kRsvSlots], alloc_mem[kRsvSlots];
-  int64_t allocd_cpu[kRsvSlots], allocd_mem[kRsvSlots];
-  int32_t owner[kRsvSlots], assigned[kRsvSlots], order[kRsvSlots];
+  int64_t alloc_cpu[kRsvSlots], alloc_mem[kRsvSlots];    // ReservationInfo.Allocatable (0 = key absent)
+  int64_t allocd_cpu[kRsvSlots], allocd_mem[kRsvSlots];  // ReservationInfo.Allocated
+  int32_t owner[kRsvSlots], assigned[kRsvSlots], order[kRsvSlots];  // owner group 0..63
   uint32_t meta[kRsvSlots];
 };
 static_assert(sizeof(RsvNode) == 192, "RsvNode layout");
 
 struct RsvPod {
-  int32_t owner;
+  uint64_t owner_mask;  // bit g: the pod matches the owners of owner group g
   uint32_t flags;
+  uint32_t pad;
 };
 
 struct RsvParams {
   int32_t filter, score, weight, pad;
 };
 
-// ws words: [3] = cursor: the first pod of the current group (the others are unused)
+// DeviceShare + ElasticQuota context of the C5 pass (ds = nullptr: no DeviceShare in the profile; nq = 0: no quotas)
+struct RsvExt {
+  const DsNode* __restrict__ ds;       // [cap] node devices (deviceUsed updated by Reserve)
+  const DsPod* __restrict__ dpods;     // [pods] DeviceShare preFilterState
+  DsParams DP;
+  QuotaRow* __restrict__ quotas;       // [nq]
+  const int64_t* __restrict__ qdev;    // [pods][kQuotaRes] device requests (quota dims 2..7)
+  int32_t* __restrict__ out_minors;    // [pods]
+  int nq;
+};
+
 struct RsvOut {
   bool feas;
   int64_t base;   // Fit + LoadAware weighted total
   int32_t raw;    // Reservation Score of the nominated slot (0 = none)
   int32_t nom;    // nominated slot, -1 = none
   int32_t order;  // findMostPreferredReservationByOrder over matched (INT32_MAX = none)
+  int32_t dsraw;  // DeviceShare raw Score
 };
 
 __device__ __forceinline__ int64_t rsv_nn(int64_t a, int64_t b) { return a - b > 0 ? a - b : 0; }
+// GetNonzeroRequests of the reserve pod (requests = Allocatable): an absent key takes the default
+__device__ __forceinline__ int64_t rsv_nz_cpu(const RsvNode& rn, int s) {
+  return rn.alloc_cpu[s] > 0 ? rn.alloc_cpu[s] : kDefaultMilliCpu;
+}
+__device__ __forceinline__ int64_t rsv_nz_mem(const RsvNode& rn, int s) {
+  return rn.alloc_mem[s] > 0 ? rn.alloc_mem[s] : kDefaultMemory;
+}
 
 // scoreReservation (scoring.go:183-203): MostAllocated over the reservation's non-zero allocatable.
 __device__ __forceinline__ int32_t rsv_score_slot(const RsvNode& rn, int s, const DevPod& p) {
@@ -65,10 +93,11 @@ __device__ __forceinline__ int32_t rsv_score_slot(const RsvNode& rn, int s, cons
 
 __device__ __forceinline__ RsvOut rsv_eval_node(const DevTable& T, const RsvNode* __restrict__ RN,
                                                 const int32_t* __restrict__ rsv_n, int64_t i, const DevPod& p,
-                                                const RsvPod& rp, const EvalParams& P, const RsvParams& RP) {
+                                                const RsvPod& rp, const EvalParams& P, const RsvParams& RP,
+                                                const RsvExt& X, const DsPod* dp) {
   Row r = load_row(T, i);
   const int ns = rsv_n[i];
-  RsvOut o{false, 0, 0, -1, 0x7fffffff};
+  RsvOut o{false, 0, 0, -1, 0x7fffffff, 0};
   uint32_t mm = 0;  // matched slots
   int nm = 0;
   int64_t pr_c = 0, pr_m = 0, ra_c = 0, ra_m = 0;
@@ -77,12 +106,13 @@ __device__ __forceinline__ RsvOut rsv_eval_node(const DevTable& T, const RsvNode
   if (ns > 0) {
     rn = RN[i];
     uint32_t um = 0;
-    #pragma unroll
+#pragma unroll
     for (int s = 0; s < kRsvSlots; ++s) {
       if (s >= ns) break;
       const uint32_t m = rn.meta[s];
       if (!(m & RS_AVAIL) || ((m & RS_ONCE) && rn.assigned[s] > 0)) continue;  // transformer.go:101-110
-      if (rp.owner != 0 && rn.owner[s] == rp.owner && !(m & RS_UNSCHED)) mm |= 1u << s;
+      // ReservationInfo.Match → MatchReservationOwners, decoded per owner group into the pod's mask
+      if (((rp.owner_mask >> (rn.owner[s] & 63)) & 1u) && !(m & RS_UNSCHED)) mm |= 1u << s;
       else if (rn.assigned[s] > 0) um |= 1u << s;
     }
     has_state = (mm | um) != 0 && !((rp.flags & RP_AFFINITY) && mm == 0);  // transformer.go:127-136
@@ -92,14 +122,14 @@ __device__ __forceinline__ RsvOut rsv_eval_node(const DevTable& T, const RsvNode
         if (um >> s & 1) {  // restoreUnmatchedReservations (transformer.go:265-291)
           r.req_cpu -= rn.alloc_cpu[s];
           r.req_mem -= rn.alloc_mem[s];
-          r.nz_cpu -= rn.alloc_cpu[s];
-          r.nz_mem -= rn.alloc_mem[s];
+          r.nz_cpu -= rsv_nz_cpu(rn, s);
+          r.nz_mem -= rsv_nz_mem(rn, s);
           const int64_t rc = rsv_nn(rn.alloc_cpu[s], rn.allocd_cpu[s]), rm = rsv_nn(rn.alloc_mem[s], rn.allocd_mem[s]);
-          if (rc != 0 || rm != 0) {
+          if (rc != 0 || rm != 0) {  // the remainder pod carries the reservation's keys
             r.req_cpu += rc;
             r.req_mem += rm;
-            r.nz_cpu += rc;
-            r.nz_mem += rm;
+            r.nz_cpu += rn.alloc_cpu[s] > 0 ? rc : kDefaultMilliCpu;
+            r.nz_mem += rn.alloc_mem[s] > 0 ? rm : kDefaultMemory;
           }
         }
       pr_c = r.req_cpu;
@@ -109,8 +139,8 @@ __device__ __forceinline__ RsvOut rsv_eval_node(const DevTable& T, const RsvNode
         if (mm >> s & 1) {  // restoreMatchedReservation: NodeInfo.RemovePod(reserve pod) (transformer.go:240-263)
           r.req_cpu -= rn.alloc_cpu[s];
           r.req_mem -= rn.alloc_mem[s];
-          r.nz_cpu -= rn.alloc_cpu[s];
-          r.nz_mem -= rn.alloc_mem[s];
+          r.nz_cpu -= rsv_nz_cpu(rn, s);
+          r.nz_mem -= rsv_nz_mem(rn, s);
           r.num_pods -= 1;
           ra_c += rn.allocd_cpu[s];
           ra_m += rn.allocd_mem[s];
@@ -121,23 +151,34 @@ __device__ __forceinline__ RsvOut rsv_eval_node(const DevTable& T, const RsvNode
   int64_t t = 0;
   if (!eval_node(r, p, P, t)) return o;  // NodeResourcesFit + LoadAware on the restored NodeInfo
   // satisfied(s): filterWithReservations([s]) (plugin.go:384-428) with fitsNode (:433-482), preemptible = 0
-  const bool zero = p.req_cpu == 0 && p.req_mem == 0;
+  const bool kc = (p.flags & P_CPU_KEY) != 0, km = (p.flags & P_MEM_KEY) != 0;
   uint32_t sat = 0;
-  if (has_state && !zero) {
+  if (has_state) {
     const bool pods_ok = !(r.num_pods - nm + 1 > r.alloc_pods);
+    const bool zero = p.req_cpu == 0 && p.req_mem == 0;  // fitsNode: a zero request fits
 #pragma unroll
     for (int s = 0; s < kRsvSlots; ++s) {
       if (!(mm >> s & 1)) continue;
+      const bool hc = rn.alloc_cpu[s] > 0, hm = rn.alloc_mem[s] > 0;
+      if (!((kc && hc) || (km && hm))) continue;  // Intersection(rInfo.ResourceNames, pod request names) empty
       const int64_t rc = rsv_nn(rn.alloc_cpu[s], rn.allocd_cpu[s]), rm = rsv_nn(rn.alloc_mem[s], rn.allocd_mem[s]);
-      bool fits = pods_ok && !(p.req_cpu > r.alloc_cpu - (pr_c - rc - ra_c)) &&
-                  !(p.req_mem > r.alloc_mem - (pr_m - rm - ra_m));
-      if (((rn.meta[s] >> 4) & 3) == KG_RSV_POLICY_RESTRICTED) fits = fits && p.req_cpu <= rc && p.req_mem <= rm;
+      bool fits = pods_ok && (zero || (!(p.req_cpu > r.alloc_cpu - (pr_c - rc - ra_c)) &&
+                                       !(p.req_mem > r.alloc_mem - (pr_m - rm - ra_m))));
+      if (((rn.meta[s] >> 4) & 3) == KG_RSV_POLICY_RESTRICTED)  // LessThanOrEqual(podRequests, rRemained)
+        fits = fits && (!hc || !kc || p.req_cpu <= rc) && (!hm || !km || p.req_mem <= rm);
       if (fits) sat |= 1u << s;
     }
   }
   if (RP.filter && (rp.flags & RP_AFFINITY) && sat == 0) return o;  // plugin.go:361-364, 423-426
+  int64_t dsraw = 0;
+  if (X.ds && dp && !dp->skip) {  // DeviceShare Filter + raw Score (node level: no device-holding reservations)
+    if (!ds_eval(X.ds[i], *dp, X.DP, dsraw)) return o;
+    // DeviceShare.FilterReservation rejects every reservation for a pod that requests devices
+    if (X.DP.filter) sat = 0;
+  }
   o.feas = true;
   o.base = t;
+  o.dsraw = X.DP.score ? (int32_t)dsraw : 0;
   if (has_state) {
     // PreScore node order over matched (scoring.go:66, 162-181); nomination over FilterReservation-passing slots
     int32_t best_all = 0x7fffffff, best_sat = 0x7fffffff;
@@ -195,10 +236,65 @@ __device__ __forceinline__ uint64_t rsv_partials_max(const uint64_t* __restrict_
   return wave_max_u64_dpp(v);
 }
 
-// Reserve of pod j on its winner row w (NodeInfo + LoadAware assign cache) and reservationCache.assumePod on the
-// slot nominated there (reservation_info.go:317-326).  Called by the one thread that owns row w.
-__device__ __forceinline__ int32_t rsv_reserve(const DevTable& T, RsvNode* __restrict__ RN, int64_t w, uint64_t v,
-                                               const DevPod& p) {
+// DeviceShare Reserve on one node (one thread): the first `count` fitting minors in (score desc, minor asc) order
+// (defaultAllocateDevices device_allocator.go:384-454 + sortDeviceResourcesByMinor device_resources.go:187-208),
+// then nodeDevice.updateCacheUsed (device_cache.go:124-135).  Returns the minor mask, -1 if no allocation.
+__device__ __forceinline__ int32_t rsv_ds_reserve(DsNode& dn, const DsPod& dp, const DsParams& DP) {
+  if (dp.skip || !dn.has_device) return 0;
+  if (dp.error) return -1;
+  const DsInst in = ds_instance(dn, dp);
+  if (!in.ok) return -1;
+  int64_t sc[kMinors];
+  uint32_t fit = 0;
+  bool any = false;
+#pragma unroll
+  for (int m = 0; m < kMinors; ++m) {
+    bool f = false, nz = false;
+    sc[m] = ds_minor(dn, m, in, DP, f, nz);
+    any |= nz;
+    fit |= f ? (1u << m) : 0u;
+  }
+  if (!any || __popc(fit) < in.count) return -1;
+  uint32_t taken = 0;
+  for (int k = 0; k < in.count; ++k) {
+    int best = -1;
+#pragma unroll
+    for (int m = 0; m < kMinors; ++m)
+      if (((fit & ~taken) >> m) & 1u)
+        if (best < 0 || sc[m] > sc[best]) best = m;
+    taken |= 1u << best;
+  }
+#pragma unroll
+  for (int m = 0; m < kMinors; ++m)
+    if ((taken >> m) & 1u) {
+      dn.ucore[m] += (int32_t)in.core;
+      dn.uratio[m] += (int32_t)in.ratio;
+      dn.umem[m] += in.mem;
+    }
+  return (int32_t)taken;
+}
+
+__device__ __forceinline__ void rsv_quota_charge(const RsvExt& X, const DevPod& p, int64_t j) {
+  if (X.nq == 0 || p.quota < 0) return;
+  quota_row_charge(X.quotas[p.quota], quota_req(p, X.qdev + (size_t)j * kQuotaRes), (p.flags & P_NONPREEMPT) != 0);
+}
+
+// Reserve of pod j on its winner row w: DeviceShare first (a failure un-assumes the pod: nothing is placed), then
+// NodeInfo + LoadAware assign cache and reservationCache.assumePod on the slot nominated there
+// (reservation_info.go:317-326).  Called by the one thread that owns row w.  Returns false when not placed.
+__device__ __forceinline__ bool rsv_reserve(const DevTable& T, RsvNode* __restrict__ RN, int64_t w, uint64_t v,
+                                            const DevPod& p, const RsvExt& X, int64_t j, int32_t& slot_out) {
+  slot_out = -1;
+  if (X.ds) {
+    DsNode dn = X.ds[w];
+    const int32_t minors = rsv_ds_reserve(dn, X.dpods[j], X.DP);
+    if (minors < 0) {
+      X.out_minors[j] = 0;
+      return false;
+    }
+    if (minors) const_cast<DsNode*>(X.ds)[w] = dn;
+    X.out_minors[j] = minors;
+  }
   Row r = load_row(T, w);
   const int64_t prod = (p.flags & P_PROD) ? 1 : 0;
   r.req_cpu += p.req_cpu;
@@ -217,71 +313,115 @@ __device__ __forceinline__ int32_t rsv_reserve(const DevTable& T, RsvNode* __res
     RN[w].allocd_mem[slot] += p.req_mem;
     RN[w].assigned[slot] += 1;
   }
-  return slot;
+  slot_out = slot;
+  return true;
 }
 
 // Pass 1 for pod j = cursor + g: first the Reserve of pod j - 1 (g > 0; its winner is the max of the previous
 // rsv_select's block keys — the thread owning that row applies it, so no separate launch), then per-node Filter +
-// Fit/LoadAware total + nominated slot and raw Score.  val[i] = (base << 32) | raw << 8 | feasible << 7 | (nom + 1),
-// 0 = filtered.  Per-block partials (no same-address atomics): part[b] = max ~(order << 32 | node) over feasible
-// nodes with an order label (PreScore preferred node, 0 = none), part[nb + b] = max raw Score.
+// Fit/LoadAware total + nominated slot and raw Scores.  val[i] = base << 32 | dsraw << 16 | raw << 8 | feasible << 7 |
+// (nom + 1), 0 = filtered.  Per-block partials (no same-address atomics): part[b] = max ~(order << 32 | node) over
+// feasible nodes with an order label (PreScore preferred node, 0 = none), part[nb + b] = max raw Reservation Score,
+// part[3 nb + b] = max raw DeviceShare Score.
+// ElasticQuota: pod j's PreFilter must see the Reserve of every earlier pod.  The quota rows hold the charges of
+// pods < j - 1 (pod j - 2 was charged by rsv_select(j - 1)); pod j - 1's charge is added here explicitly when it was
+// placed (g > 0; a group's last pod is charged by rsv_apply itself), and written into the rows by rsv_select(j), when
+// no pass reads them (ws[0] = j tags it).
 __global__ __launch_bounds__(kRsvThreads) void rsv_eval(DevTable T, RsvNode* __restrict__ RN,
                                                         const int32_t* __restrict__ rsv_n,
                                                         const DevPod* __restrict__ pods,
                                                         const RsvPod* __restrict__ rpods, int64_t end, int64_t n,
-                                                        int g, EvalParams P, RsvParams RP, uint64_t* __restrict__ val,
-                                                        uint64_t* __restrict__ part, uint64_t* __restrict__ out_keys,
-                                                        int32_t* __restrict__ out_slot,
-                                                        const unsigned long long* __restrict__ ws) {
+                                                        int g, EvalParams P, RsvParams RP, RsvExt X,
+                                                        uint64_t* __restrict__ val, uint64_t* __restrict__ part,
+                                                        uint64_t* __restrict__ out_keys, int32_t* __restrict__ out_slot,
+                                                        unsigned long long* __restrict__ ws) {
   __shared__ uint64_t s_red[kRsvThreads / kWave];
+  __shared__ int s_admit;
   const int64_t j = (int64_t)ws[3] + g;
   if (j - 1 >= end || (g == 0 && j >= end)) return;  // uniform across the grid
   const int nb = gridDim.x;
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  bool prev_placed = false;
   if (g > 0) {  // Reserve of pod j - 1
     const uint64_t k = rsv_partials_max(part + 2 * nb, nb);
     const int64_t w = k ? (int64_t)key_node(k) : -1;
     if (i == w || (w < 0 && i == 0)) {
       int32_t slot = -1;
-      if (w >= 0) slot = rsv_reserve(T, RN, w, val[w], pods[j - 1]);
-      out_keys[j - 1] = k;
+      bool placed = false;
+      if (w >= 0) placed = rsv_reserve(T, RN, w, val[w], pods[j - 1], X, j - 1, slot);
+      out_keys[j - 1] = placed ? k : 0;
       out_slot[j - 1] = slot;
+      if (placed && X.nq > 0 && pods[j - 1].quota >= 0) {
+        if (j >= end) rsv_quota_charge(X, pods[j - 1], j - 1);  // no later pass charges it
+        else ws[0] = (unsigned long long)j;                     // rsv_select(j) charges it
+      }
     }
     if (j >= end) return;
+    prev_placed = k != 0;  // (a DeviceShare Reserve failure leaves it unplaced: only the ds dims could disagree)
   }
-  uint64_t pk = 0, rawv = 0;
+  const DevPod p = pods[j];
+  if (threadIdx.x == 0) {  // ElasticQuota PreFilter of pod j (the same verdict in every block)
+    int ok = 1;
+    if (X.nq > 0 && p.quota >= 0) {
+      const QuotaReq rq = quota_req(p, X.qdev + (size_t)j * kQuotaRes);
+      int64_t au[kQuotaRes] = {}, an[kQuotaRes] = {};
+      if (prev_placed) {
+        const DevPod pp = pods[j - 1];
+        if (pp.quota == p.quota) {
+          const QuotaReq pr = quota_req(pp, X.qdev + (size_t)(j - 1) * kQuotaRes);
+          const bool npp = (pp.flags & P_NONPREEMPT) != 0;
+#pragma unroll
+          for (int d = 0; d < kQuotaRes; ++d) au[d] = pr.r[d], an[d] = npp ? pr.r[d] : 0;
+        }
+      }
+      ok = quota_row_admit(X.quotas[p.quota], rq, (p.flags & P_NONPREEMPT) != 0, au, an) ? 1 : 0;
+    }
+    s_admit = ok;
+  }
+  uint64_t pk = 0, rawv = 0, dsv = 0;
+  uint64_t v = 0;
   if (i < n) {
-    const DevPod p = pods[j];
     const RsvPod rp = rpods[j];
-    const RsvOut o = rsv_eval_node(T, RN, rsv_n, i, p, rp, P, RP);
-    uint64_t v = 0;
+    const DsPod* dp = X.ds ? &X.dpods[j] : nullptr;
+    const RsvOut o = rsv_eval_node(T, RN, rsv_n, i, p, rp, P, RP, X, dp);
     if (o.feas) {
-      v = ((uint64_t)(uint32_t)o.base << 32) | ((uint64_t)(uint32_t)o.raw << 8) | (1ull << 7) | (uint64_t)(o.nom + 1);
+      v = ((uint64_t)(uint32_t)o.base << 32) | ((uint64_t)(uint32_t)o.dsraw << 16) |
+          ((uint64_t)(uint32_t)o.raw << 8) | (1ull << 7) | (uint64_t)(o.nom + 1);
       if (o.order != 0x7fffffff) pk = ~(((uint64_t)(uint32_t)o.order << 32) | (uint64_t)(uint32_t)i);
       rawv = (uint64_t)(uint32_t)o.raw;
+      dsv = (uint64_t)(uint32_t)o.dsraw;
     }
-    val[i] = v;
   }
-  __syncthreads();  // part[2nb..] (read above) is not rewritten here, but keep the block's LDS use ordered
+  __syncthreads();
+  if (!s_admit) v = 0, pk = 0, rawv = 0, dsv = 0;  // PreFilter Unschedulable: no node is feasible
+  if (i < n) val[i] = v;
   pk = rsv_block_max(pk, s_red);
   __syncthreads();
   rawv = rsv_block_max(rawv, s_red);
+  __syncthreads();
+  dsv = rsv_block_max(dsv, s_red);
   if (threadIdx.x == 0) {
     part[blockIdx.x] = pk;
     part[nb + blockIdx.x] = rawv;
+    part[3 * nb + blockIdx.x] = dsv;
   }
 }
 
-// Pass 2: PreScore preferred node (1000), DefaultNormalizeScore over the feasible nodes, × weight, packed key;
-// part[2 nb + b] = the block's max key.
-__global__ __launch_bounds__(kRsvThreads) void rsv_select(const uint64_t* __restrict__ val, int64_t end, int64_t n,
-                                                          int g, RsvParams RP, uint64_t* __restrict__ part,
-                                                          const unsigned long long* __restrict__ ws) {
+// Pass 2: PreScore preferred node (1000), DefaultNormalizeScore of both plugins over the feasible nodes, × weights,
+// packed key; part[2 nb + b] = the block's max key.  Block 0 also charges pod j - 1's quota (tagged ws[0] = j).
+__global__ __launch_bounds__(kRsvThreads) void rsv_select(const uint64_t* __restrict__ val, const DevPod* __restrict__ pods,
+                                                          int64_t end, int64_t n, int g, RsvParams RP, RsvExt X,
+                                                          uint64_t* __restrict__ part,
+                                                          unsigned long long* __restrict__ ws) {
   __shared__ uint64_t s_red[kRsvThreads / kWave];
-  if ((int64_t)ws[3] + g >= end) return;
+  const int64_t j = (int64_t)ws[3] + g;
+  if (j >= end) return;
   const int nb = gridDim.x;
+  if (blockIdx.x == 0 && threadIdx.x == 0 && X.nq > 0 && g > 0 && ws[0] == (unsigned long long)j)
+    rsv_quota_charge(X, pods[j - 1], j - 1);
   const uint64_t pk = rsv_partials_max(part, nb);
   const uint64_t mraw = rsv_partials_max(part + nb, nb);
+  const uint64_t mds = X.ds ? rsv_partials_max(part + 3 * nb, nb) : 0;
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t pref = pk ? (int64_t)(uint32_t)(~pk) : -1;
   const int64_t mx = pk ? (mraw > 1000 ? (int64_t)mraw : 1000) : (int64_t)mraw;
@@ -292,6 +432,7 @@ __global__ __launch_bounds__(kRsvThreads) void rsv_select(const uint64_t* __rest
       const int64_t raw = (i == pref) ? 1000 : (int64_t)((v >> 8) & 0xff);  // mostPreferredScore
       int64_t t = (int64_t)(v >> 32);
       if (RP.score && mx > 0) t += (int64_t)RP.weight * (100 * raw / mx);
+      if (X.DP.score && mds > 0) t += (int64_t)X.DP.weight * (100 * (int64_t)((v >> 16) & 0xff) / (int64_t)mds);
       key = make_key(t, (uint32_t)i);
     }
   }
@@ -299,11 +440,12 @@ __global__ __launch_bounds__(kRsvThreads) void rsv_select(const uint64_t* __rest
   if (threadIdx.x == 0) part[2 * nb + blockIdx.x] = key;
 }
 
-// End of a group of kRsvGroup pods (one wave): Reserve of the group's last pod (cursor + g_last) and the cursor
-// advance.  Pods past `end` are skipped.
+// End of a group of kRsvGroup pods (one wave): Reserve of the group's last pod (cursor + g_last) with its quota
+// charge, and the cursor advance.  Pods past `end` are skipped.
 __global__ __launch_bounds__(kWave) void rsv_apply(DevTable T, RsvNode* __restrict__ RN,
                                                    const uint64_t* __restrict__ val, const DevPod* __restrict__ pods,
-                                                   int64_t end, int nb, int g_last, const uint64_t* __restrict__ part,
+                                                   int64_t end, int nb, int g_last, RsvExt X,
+                                                   const uint64_t* __restrict__ part,
                                                    uint64_t* __restrict__ out_keys, int32_t* __restrict__ out_slot,
                                                    unsigned long long* __restrict__ ws) {
   const int64_t base = (int64_t)ws[3];
@@ -313,12 +455,14 @@ __global__ __launch_bounds__(kWave) void rsv_apply(DevTable T, RsvNode* __restri
   if (threadIdx.x != 0) return;
   if (j < end) {
     int32_t slot = -1;
+    bool placed = false;
     if (k) {
       const int64_t w = (int64_t)key_node(k);
-      slot = rsv_reserve(T, RN, w, val[w], pods[j]);
+      placed = rsv_reserve(T, RN, w, val[w], pods[j], X, j, slot);
     }
-    out_keys[j] = k;
+    out_keys[j] = placed ? k : 0;
     out_slot[j] = slot;
+    if (placed) rsv_quota_charge(X, pods[j], j);
   }
   ws[3] = (unsigned long long)(base + g_last + 1);
 }

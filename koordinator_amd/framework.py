@@ -238,16 +238,21 @@ def make_node_device(gpus: list | None = None, has_device: bool = True) -> np.nd
     return d
 
 
+QUOTA_RESOURCES = ("cpu", "memory", "nvidia.com/gpu", "dcu.com/gpu", "koordinator.sh/gpu", "koordinator.sh/gpu-core",
+                   "koordinator.sh/gpu-memory", "koordinator.sh/gpu-memory-ratio")
+
+
 def make_quota(used_limit: dict | None = None, used: dict | None = None, min: dict | None = None,
                non_preemptible_used: dict | None = None) -> np.ndarray:
-    """One ElasticQuota (kg_quota): {"cpu": milli, "memory": bytes} lists; a key absent from used_limit / min does
-    not constrain (quotav1.LessThanOrEqual compares only the limit's keys)."""
+    """One ElasticQuota (kg_quota) over QUOTA_RESOURCES: {"cpu": milli, "memory": bytes, "koordinator.sh/gpu-core":
+    .., ...} lists; a key absent from used_limit / min does not constrain (quotav1.LessThanOrEqual compares only the
+    limit's keys)."""
     q = np.zeros(1, dtype=abi.QUOTA_DTYPE)
     r = q[0]
     for f, d, absent in (("used", used, 0), ("non_preemptible_used", non_preemptible_used, 0),
                          ("used_limit", used_limit, -1), ("min", min, -1)):
         d = d or {}
-        r[f] = [int(d.get("cpu", absent)), int(d.get("memory", absent))]
+        r[f] = [int(d.get(k, absent)) for k in QUOTA_RESOURCES]
     return q
 
 

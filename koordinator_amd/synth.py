@@ -288,16 +288,17 @@ def load_gpu_into(engine, cluster: Cluster, dev: np.ndarray):
 
 
 # ---- config C5: Reservation matching (50k nodes; 0–4 reservations on 30 % of nodes, owner label selectors) -----
-N_OWNERS = 64
+N_OWNERS = 64  # owner groups (reservations sharing an owner spec); a pod carries the bitmask of the groups it matches
 
 
-def make_rsv_cluster(n_nodes: int, seed: int = BASE_SEED + 8) -> tuple:
-    """(Cluster, kg_node_reservations[n]) for config C5's Reservation part: make_cluster's nodes, 30 % of them with
-    1–4 Available reservations (cpu {2,4,8,16} cores, memory {4..64} GiB, owner group 1..64, 40 % carrying an
-    order label, policy Default 60 % / Aligned 20 % / Restricted 20 %, 20 % AllocateOnce).  Each reservation's
-    reserve pod sits in NodeInfo (requests = allocatable, KG_POD_RESERVE) and 0–2 pods are already assigned to it
-    (in NodeInfo and the LoadAware assign cache, accounted in Allocated)."""
-    cluster = make_cluster(n_nodes, seed=seed)
+def make_rsv_cluster(n_nodes: int, seed: int = BASE_SEED + 8, cluster: Cluster | None = None) -> tuple:
+    """(Cluster, kg_node_reservations[n]) for config C5's Reservation part: make_cluster's nodes (or `cluster`), 30 %
+    of them with 1–4 Available reservations (cpu {2,4,8,16} cores, memory {4..64} GiB — 8 % of them cpu-only and 4 %
+    memory-only —, owner group 0..63, 40 % carrying an order label, policy Default 60 % / Aligned 20 % / Restricted
+    20 %, 20 % AllocateOnce).  Each reservation's reserve pod sits in NodeInfo (requests = allocatable, an absent key's
+    non-zero request = the 100m / 200MiB default, KG_POD_RESERVE) and 0–2 pods are already assigned to it (in NodeInfo
+    and the LoadAware assign cache, accounted in Allocated)."""
+    cluster = cluster if cluster is not None else make_cluster(n_nodes, seed=seed)
     rng = np.random.default_rng(seed + 1000)
     n = n_nodes
     rsv = np.zeros(n, dtype=abi.NODE_RSV_DTYPE)
@@ -306,10 +307,13 @@ def make_rsv_cluster(n_nodes: int, seed: int = BASE_SEED + 8) -> tuple:
     S = abi.MAX_RSV_SLOTS
     cpu = rng.choice(np.array([2, 4, 8, 16], dtype=np.int64), (n, S)) * 1000
     mem = rng.choice(np.array([4, 8, 16, 32, 64], dtype=np.int64), (n, S)) * GI
+    kind = rng.random((n, S))
+    cpu = np.where(kind >= 0.96, 0, cpu)                  # memory-only
+    mem = np.where((kind >= 0.88) & (kind < 0.96), 0, mem)  # cpu-only
     on = np.arange(S)[None, :] < rsv["n"][:, None]
     rsv["allocatable_cpu"] = np.where(on, cpu, 0)
     rsv["allocatable_mem"] = np.where(on, mem, 0)
-    rsv["owner"] = np.where(on, rng.integers(1, N_OWNERS + 1, (n, S)), 0)
+    rsv["owner"] = np.where(on, rng.integers(0, N_OWNERS, (n, S)), 0)
     rsv["order"] = np.where(on & (rng.random((n, S)) < 0.4), rng.integers(1, 1000, (n, S)), 0)
     u = rng.random((n, S))
     rsv["policy"] = np.where(on, np.where(u < 0.6, 0, np.where(u < 0.8, 1, 2)), 0)
@@ -325,16 +329,19 @@ def make_rsv_cluster(n_nodes: int, seed: int = BASE_SEED + 8) -> tuple:
     ii, ss = np.nonzero(on)
     for i, s in zip(ii.tolist(), ss.tolist()):
         rp = np.zeros(1, dtype=abi.POD_DTYPE)[0]
-        rp["requests"][abi.RES_CPU] = rp["limits"][abi.RES_CPU] = rp["nonzero_requests"][0] = cpu[i, s]
-        rp["requests"][abi.RES_MEMORY] = rp["limits"][abi.RES_MEMORY] = rp["nonzero_requests"][1] = mem[i, s]
+        rp["requests"][abi.RES_CPU] = rp["limits"][abi.RES_CPU] = cpu[i, s]
+        rp["requests"][abi.RES_MEMORY] = rp["limits"][abi.RES_MEMORY] = mem[i, s]
+        rp["nonzero_requests"][0] = cpu[i, s] if cpu[i, s] else 100
+        rp["nonzero_requests"][1] = mem[i, s] if mem[i, s] else 200 * MI
         rp["priority_class"] = abi.PRIO_PROD
         rp["flags"] = abi.POD_RESERVE
         extra_pods.append(rp)
         extra_node.append(i)
         for _ in range(int(k[i, s])):
             ap = np.zeros(1, dtype=abi.POD_DTYPE)[0]
-            ap["requests"][abi.RES_CPU] = ap["limits"][abi.RES_CPU] = ap["nonzero_requests"][0] = cpu[i, s] // 4
-            ap["requests"][abi.RES_MEMORY] = ap["limits"][abi.RES_MEMORY] = ap["nonzero_requests"][1] = mem[i, s] // 4
+            ac, am = (cpu[i, s] or 4000) // 4, (mem[i, s] or 8 * GI) // 4
+            ap["requests"][abi.RES_CPU] = ap["limits"][abi.RES_CPU] = ap["nonzero_requests"][0] = ac
+            ap["requests"][abi.RES_MEMORY] = ap["limits"][abi.RES_MEMORY] = ap["nonzero_requests"][1] = am
             ap["priority_class"] = abi.PRIO_PROD
             extra_pods.append(ap)
             extra_node.append(i)
@@ -344,13 +351,23 @@ def make_rsv_cluster(n_nodes: int, seed: int = BASE_SEED + 8) -> tuple:
     return cluster, rsv
 
 
-def make_rsv_pods(n_pods: int, seed: int = BASE_SEED + 9) -> np.ndarray:
-    """Config C5 Reservation queue: make_pods' pods, 20 % owned by a reservation owner group (matching label
-    selectors), a quarter of those with a required reservation affinity."""
-    p = make_pods(n_pods, seed=seed)
+def owner_masks(rng, n_pods: int, frac: float = 0.2, n_groups: int = N_OWNERS) -> np.ndarray:
+    """Owner-group bitmasks for a queue: `frac` of the pods match one group, a quarter of those a second one."""
+    owned = rng.random(n_pods) < frac
+    g1 = rng.integers(0, n_groups, n_pods)
+    g2 = rng.integers(0, n_groups, n_pods)
+    two = owned & (rng.random(n_pods) < 0.25)
+    m = np.where(owned, np.left_shift(np.int64(1), g1), 0)
+    return (m | np.where(two, np.left_shift(np.int64(1), g2), 0)).astype(np.int64)
+
+
+def make_rsv_pods(n_pods: int, seed: int = BASE_SEED + 9, base: np.ndarray | None = None) -> np.ndarray:
+    """Config C5 Reservation queue: make_pods' pods (or `base`), 20 % owned (matching one owner group's label
+    selectors, a quarter of them a second group's), a quarter of those with a required reservation affinity."""
+    p = make_pods(n_pods, seed=seed) if base is None else base
     rng = np.random.default_rng(seed + 1000)
-    owned = rng.random(n_pods) < 0.2
-    p["reservation_owner"] = np.where(owned, rng.integers(1, N_OWNERS + 1, n_pods), 0)
+    p["reservation_owner_mask"] = owner_masks(rng, n_pods)
+    owned = p["reservation_owner_mask"] != 0
     p["reservation_flags"] = np.where(owned & (rng.random(n_pods) < 0.25), abi.POD_RSV_AFFINITY, 0)
     return p
 
@@ -358,3 +375,56 @@ def make_rsv_pods(n_pods: int, seed: int = BASE_SEED + 9) -> np.ndarray:
 def load_rsv_into(engine, cluster: Cluster, rsv: np.ndarray):
     load_into(engine, cluster)
     engine.upsert_reservations(rsv)
+
+
+# ---- config C5 (one profile): Reservation + DeviceShare + ElasticQuota ------------------------------------------
+N_QUOTAS = 16
+
+
+def make_c5_cluster(n_nodes: int, seed: int = BASE_SEED + 10) -> tuple:
+    """(Cluster, kg_node_device[n], kg_node_reservations[n]) for config C5 as one profile: make_gpu_cluster's GPU nodes
+    with make_rsv_cluster's reservations on top (cpu / memory reservations; the reserve pods in NodeInfo)."""
+    cluster, dev = make_gpu_cluster(n_nodes, seed=seed)
+    cluster, rsv = make_rsv_cluster(n_nodes, seed=seed + 1, cluster=cluster)
+    return cluster, dev, rsv
+
+
+def make_c5_pods(n_pods: int, seed: int = BASE_SEED + 11) -> np.ndarray:
+    """Config C5 queue: make_gpu_pods (30 % GPU-share) with make_rsv_pods' owner masks / affinities (20 % owned) and
+    N_QUOTAS ElasticQuota groups (80 % of the pods in one)."""
+    p = make_rsv_pods(n_pods, seed=seed + 1, base=make_gpu_pods(n_pods, seed=seed))
+    rng = np.random.default_rng(seed + 2000)
+    p["quota_id"] = np.where(rng.random(n_pods) < 0.8, rng.integers(1, N_QUOTAS + 1, n_pods), 0)
+    return p
+
+
+def make_c5_quotas(pods: np.ndarray, seed: int = BASE_SEED + 12, n_quotas: int = N_QUOTAS,
+                   share: float = 1.0) -> np.ndarray:
+    """kg_quota[n_quotas] whose limits run out during the queue: used_limit ≈ U(0.3, 1.2) · `share` of each
+    quota's total demand on cpu / memory / gpu-core / gpu-memory-ratio (gpu-memory absent 50 %), min = 1/4 of it."""
+    rng = np.random.default_rng(seed)
+    q = np.zeros(n_quotas, dtype=abi.QUOTA_DTYPE)
+    q["used_limit"] = -1
+    q["min"] = -1
+    req = np.zeros((len(pods), abi.QUOTA_RES), dtype=np.int64)
+    req[:, 0] = pods["requests"][:, abi.RES_CPU]
+    req[:, 1] = pods["requests"][:, abi.RES_MEMORY]
+    req[:, 2:] = pods["device_requests"][:, :abi.QUOTA_RES - 2]
+    for k in range(n_quotas):
+        mine = pods["quota_id"] == k + 1
+        demand = req[mine].sum(axis=0)
+        for d in (0, 1, 2 + abi.DEV_GPU_CORE, 2 + abi.DEV_GPU_MEMORY_RATIO, 2 + abi.DEV_GPU_MEMORY):
+            if d == 2 + abi.DEV_GPU_MEMORY and rng.random() < 0.5:
+                continue
+            lim = int(demand[d] * share * rng.uniform(0.3, 1.2))
+            q["used_limit"][k, d] = lim
+            q["min"][k, d] = lim // 4
+    return q
+
+
+def load_c5_into(engine, cluster: Cluster, dev: np.ndarray, rsv: np.ndarray, quotas: np.ndarray | None = None):
+    load_into(engine, cluster)
+    engine.upsert_devices(dev)
+    engine.upsert_reservations(rsv)
+    if quotas is not None:
+        engine.set_quotas(quotas)

@@ -369,27 +369,44 @@ int or_schedule_numa(const kg_config* cfg, int64_t n_nodes, const kg_node* nodes
                           out_node, out_score, out_cpus, NULL);
 }
 
+/* The pod's quota request over the KG_QUOTA_RES resources (PodRequestsAndLimits: cpu, memory, the device
+ * resources) and which of them are keys of it: cpu / memory per the request-key flags, devices by value. */
+static void quota_request(const kg_pod* p, int64_t req[KG_QUOTA_RES], int key[KG_QUOTA_RES]) {
+  req[0] = p->requests[KG_RES_CPU];
+  req[1] = p->requests[KG_RES_MEMORY];
+  key[0] = or_pod_cpu_key(p);
+  key[1] = or_pod_mem_key(p);
+  for (int k = 0; k < KG_QUOTA_RES - 2; k++) {
+    req[2 + k] = p->device_requests[k];
+    key[2 + k] = p->device_requests[k] != 0;
+  }
+}
+
 /* ElasticQuota PreFilter (elasticquota/plugin.go:211-256): Mask(Add(request, used), ResourceNames(request)) ≤
  * usedLimit, and for non-preemptible pods (extension.IsPodNonPreemptible) the same against min with the
- * non-preemptible used.  Resource names = the pod's non-zero cpu / memory requests. */
-static int quota_admit(const kg_quota* q, const kg_pod* p) {
-  const int64_t rc = p->requests[KG_RES_CPU], rm = p->requests[KG_RES_MEMORY];
+ * non-preemptible used. */
+int or_quota_admit(const kg_quota* q, const kg_pod* p) {
+  int64_t req[KG_QUOTA_RES];
+  int key[KG_QUOTA_RES];
+  quota_request(p, req, key);
   /* quotav1.LessThanOrEqual(a, b) walks the keys of b and compares those a has: a limit of -1 (absent) is free */
-  int ok = (rc == 0 || q->used_limit[0] < 0 || q->used[0] + rc <= q->used_limit[0]) &&
-           (rm == 0 || q->used_limit[1] < 0 || q->used[1] + rm <= q->used_limit[1]);
+  int ok = 1;
+  for (int d = 0; d < KG_QUOTA_RES; d++)
+    if (key[d] && q->used_limit[d] >= 0 && q->used[d] + req[d] > q->used_limit[d]) ok = 0;
   if (p->flags & KG_POD_NON_PREEMPTIBLE)
-    ok = ok && (rc == 0 || q->min[0] < 0 || q->non_preemptible_used[0] + rc <= q->min[0]) &&
-         (rm == 0 || q->min[1] < 0 || q->non_preemptible_used[1] + rm <= q->min[1]);
+    for (int d = 0; d < KG_QUOTA_RES; d++)
+      if (key[d] && q->min[d] >= 0 && q->non_preemptible_used[d] + req[d] > q->min[d]) ok = 0;
   return ok;
 }
 
 /* Reserve → GroupQuotaManager.ReservePod → updatePodUsedNoLock (core/group_quota_manager.go:613-648, 791-797) */
-static void quota_charge(kg_quota* q, const kg_pod* p) {
-  q->used[0] += p->requests[KG_RES_CPU];
-  q->used[1] += p->requests[KG_RES_MEMORY];
-  if (p->flags & KG_POD_NON_PREEMPTIBLE) {
-    q->non_preemptible_used[0] += p->requests[KG_RES_CPU];
-    q->non_preemptible_used[1] += p->requests[KG_RES_MEMORY];
+void or_quota_charge(kg_quota* q, const kg_pod* p) {
+  int64_t req[KG_QUOTA_RES];
+  int key[KG_QUOTA_RES];
+  quota_request(p, req, key);
+  for (int d = 0; d < KG_QUOTA_RES; d++) {
+    q->used[d] += req[d];
+    if (p->flags & KG_POD_NON_PREEMPTIBLE) q->non_preemptible_used[d] += req[d];
   }
 }
 
@@ -429,7 +446,7 @@ int or_schedule_full(const kg_config* cfg, int64_t n_nodes, const kg_node* nodes
     if (pods[p].quota_id > 0) {
       if (pods[p].quota_id > n_quotas) { rc = KG_E_INVALID; break; }
       quota = &quotas[pods[p].quota_id - 1];
-      if (!quota_admit(quota, &pods[p])) { /* PreFilter Unschedulable: no node search, nothing reserved */
+      if (!or_quota_admit(quota, &pods[p])) { /* PreFilter Unschedulable: no node search, nothing reserved */
         out_node[p] = -1;
         out_score[p] = 0;
         if (out_minors) out_minors[p] = 0;
@@ -480,7 +497,7 @@ int or_schedule_full(const kg_config* cfg, int64_t n_nodes, const kg_node* nodes
     out_node[p] = (int32_t)best;
     out_score[p] = best >= 0 ? best_score : 0;
     if (best >= 0) or_apply_pod(cfg, &st[best], &pods[p], +1); /* assume + Reserve */
-    if (best >= 0 && quota) quota_charge(quota, &pods[p]);
+    if (best >= 0 && quota) or_quota_charge(quota, &pods[p]);
   }
   if (n_threads > 1) {
     atomic_store(&c.stop, 1);

@@ -85,6 +85,16 @@ int or_schedule_full(const kg_config* cfg, int64_t n_nodes, const kg_node* nodes
 
 /* Builds node states from pre-existing assigned pods (informer adds). */
 void or_states_init(int64_t n_nodes, or_node_state* st);
+/* request-key presence of a pod (KG_POD_REQUEST_KEYS; else a key exists iff the request is non-zero) */
+static inline int or_pod_cpu_key(const kg_pod* p) {
+  return (p->flags & KG_POD_REQUEST_KEYS) ? (p->flags & KG_POD_CPU_KEY) != 0 : p->requests[KG_RES_CPU] != 0;
+}
+static inline int or_pod_mem_key(const kg_pod* p) {
+  return (p->flags & KG_POD_REQUEST_KEYS) ? (p->flags & KG_POD_MEM_KEY) != 0 : p->requests[KG_RES_MEMORY] != 0;
+}
+/* ElasticQuota PreFilter admission / Reserve charge of one pod (KG_QUOTA_RES resources) */
+int or_quota_admit(const kg_quota* q, const kg_pod* p);
+void or_quota_charge(kg_quota* q, const kg_pod* p);
 int or_states_add_pods(const kg_config* cfg, int64_t n_nodes, or_node_state* st, int64_t n, const kg_pod* pods,
                        const int32_t* node_idx);
 

@@ -88,6 +88,10 @@ def lib():
         L.or_ds_instance_flat.restype = i
         L.or_schedule_resv.argtypes = [vp, i64, vp, vp, vp, vp, i64, vp, i64, vp, vp, vp]
         L.or_schedule_resv.restype = i
+        L.or_schedule_resv_full.argtypes = [vp, i64, vp, vp, vp, vp, vp, vp, i64, i64, vp, i64, i, vp, vp, vp, vp]
+        L.or_schedule_resv_full.restype = i
+        L.or_quota_admit.argtypes = [vp, vp]
+        L.or_quota_admit.restype = i
         L.or_rsv_case_flat.argtypes = [vp, i64, vp, i64, vp, vp, i, vp, vp]
         L.or_rsv_case_flat.restype = None
         _lib = L
@@ -147,18 +151,29 @@ def schedule_full(cfg, nodes, metrics, st, pods, now_ns: int, n_threads: int = 1
 p = abi.ptr
 
 
-def schedule_resv(cfg, nodes, metrics, st, rsv, pods, now_ns: int):
-    """Sequential FIFO scheduling with NodeResourcesFit + LoadAware + Reservation (st, rsv mutated).
-    Returns (node, score, slot) — slot = the reservation each pod was assumed into (-1 = none)."""
+def schedule_resv(cfg, nodes, metrics, st, rsv, pods, now_ns: int, devices=None, quotas=None, n_threads: int = 1,
+                  with_minors: bool = False):
+    """Sequential FIFO scheduling with NodeResourcesFit + LoadAware + Reservation [+ DeviceShare + ElasticQuota]
+    (st, rsv, devices, quotas mutated; the node loop of each pod on n_threads threads).  Returns (node, score, slot)
+    — slot = the reservation each pod was assumed into (-1 = none) — and, with_minors, DeviceShare's minor masks."""
     pods = np.ascontiguousarray(pods, dtype=abi.POD_DTYPE)
     n = max(len(pods), 1)
-    out_node, out_score, out_slot = (np.empty(n, dtype=np.int32), np.empty(n, dtype=np.int64),
-                                     np.empty(n, dtype=np.int32))
-    rc = lib().or_schedule_resv(p(cfg), len(nodes), p(nodes), p(metrics), p(st), p(rsv), len(pods), p(pods), now_ns,
-                                p(out_node), p(out_score), p(out_slot))
+    out_node, out_score, out_slot, out_minors = (np.empty(n, dtype=np.int32), np.empty(n, dtype=np.int64),
+                                                 np.empty(n, dtype=np.int32), np.zeros(n, dtype=np.int32))
+    nq = 0 if quotas is None else len(quotas)
+    rc = lib().or_schedule_resv_full(p(cfg), len(nodes), p(nodes), p(metrics), p(st), p(rsv), p(devices), p(quotas),
+                                     nq, len(pods), p(pods), now_ns, n_threads, p(out_node), p(out_score), p(out_slot),
+                                     p(out_minors))
     if rc != 0:
-        raise RuntimeError(f"oracle or_schedule_resv failed: {rc}")
-    return out_node[:len(pods)], out_score[:len(pods)], out_slot[:len(pods)]
+        raise RuntimeError(f"oracle or_schedule_resv_full failed: {rc}")
+    out = (out_node[:len(pods)], out_score[:len(pods)], out_slot[:len(pods)])
+    return out + (out_minors[:len(pods)],) if with_minors else out
+
+
+def quota_admit(quota, pod) -> bool:
+    """ElasticQuota PreFilter admission of one pod against one quota (or_quota_admit)."""
+    return bool(lib().or_quota_admit(p(np.ascontiguousarray(np.asarray(quota, dtype=abi.QUOTA_DTYPE).reshape(1))),
+                                     p(np.ascontiguousarray(np.asarray(pod, dtype=abi.POD_DTYPE).reshape(1)))))
 
 
 def rsv_case(pod, allowed_pods, alloc, num_pods, pod_requested, r_allocated, has_state, rsv):

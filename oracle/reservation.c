@@ -1,11 +1,18 @@
 /*
  * reservation.c — CPU restatement of the Reservation plugin (TEST INFRASTRUCTURE ONLY; see reservation.h).
- * Resources are cpu (milli) and memory (bytes); reservations always reserve both (ResourceNames = {cpu, memory}).
+ * Resources are cpu (milli) and memory (bytes); a reservation's allocatable of 0 means the key is absent
+ * (ResourceNames ⊆ {cpu, memory}: cpu-only and memory-only reservations).
  */
 #include "reservation.h"
 
+#include <math.h>
 #include <stdlib.h>
 #include <string.h>
+
+#include "deviceshare.h"
+
+#define OR_DEFAULT_MILLI_CPU 100LL             /* schedutil.DefaultMilliCPURequest */
+#define OR_DEFAULT_MEMORY (200LL * 1024 * 1024) /* schedutil.DefaultMemoryRequest   */
 
 static int slot_usable(const kg_node_reservations* r, int s) {
   /* forEachAvailableReservationOnNode + IsAvailable/ParseError + AllocateOnce skip (transformer.go:101-110) */
@@ -15,9 +22,19 @@ static int slot_usable(const kg_node_reservations* r, int s) {
 }
 
 static int pod_matches(const kg_pod* pod, const kg_node_reservations* r, int s) {
-  /* ReservationInfo.Match → MatchReservationOwners (reservation_info.go:231-236) decoded to an owner group;
-   * !IsUnschedulable (transformer.go:112); the affinity selector matches every reservation of the owner group */
-  return pod->reservation_owner != 0 && r->owner[s] == pod->reservation_owner && !r->unschedulable[s];
+  /* ReservationInfo.Match → MatchReservationOwners (reservation_info.go:231-236) decoded per owner group: bit g of
+   * the pod's mask; !IsUnschedulable (transformer.go:112); the affinity selector matches every reservation of the
+   * owner group */
+  const int64_t g = r->owner[s];
+  return g >= 0 && g < KG_MAX_OWNER_GROUPS && (((uint64_t)pod->reservation_owner_mask >> g) & 1u) && !r->unschedulable[s];
+}
+
+/* GetNonzeroRequests of the reserve pod (requests = Allocatable): an absent key takes the default */
+static int64_t nz_cpu_of(const kg_node_reservations* r, int s) {
+  return r->allocatable_cpu[s] > 0 ? r->allocatable_cpu[s] : OR_DEFAULT_MILLI_CPU;
+}
+static int64_t nz_mem_of(const kg_node_reservations* r, int s) {
+  return r->allocatable_mem[s] > 0 ? r->allocatable_mem[s] : OR_DEFAULT_MEMORY;
 }
 
 static int64_t sub_nn(int64_t a, int64_t b) { return a - b > 0 ? a - b : 0; } /* SubtractWithNonNegativeResult */
@@ -47,15 +64,17 @@ void or_rsv_restore(const kg_node_reservations* r, const or_node_state* st, cons
     const int s = unmatched[k];
     out->requested[0] -= r->allocatable_cpu[s];
     out->requested[1] -= r->allocatable_mem[s];
-    out->nonzero[0] -= r->allocatable_cpu[s];
-    out->nonzero[1] -= r->allocatable_mem[s];
+    out->nonzero[0] -= nz_cpu_of(r, s);
+    out->nonzero[1] -= nz_mem_of(r, s);
     const int64_t rc = sub_nn(r->allocatable_cpu[s], r->allocated_cpu[s]);
     const int64_t rm = sub_nn(r->allocatable_mem[s], r->allocated_mem[s]);
     if (rc != 0 || rm != 0) {
+      /* the remainder pod's requests carry the reservation's keys (even a zero value): a present key keeps its
+       * value in GetNonzeroRequests, an absent one takes the default */
       out->requested[0] += rc;
       out->requested[1] += rm;
-      out->nonzero[0] += rc; /* keys present (explicit zero) → GetNonzeroRequests keeps the value */
-      out->nonzero[1] += rm;
+      out->nonzero[0] += r->allocatable_cpu[s] > 0 ? rc : OR_DEFAULT_MILLI_CPU;
+      out->nonzero[1] += r->allocatable_mem[s] > 0 ? rm : OR_DEFAULT_MEMORY;
     }
   }
   out->pod_requested[0] = out->requested[0];
@@ -65,8 +84,8 @@ void or_rsv_restore(const kg_node_reservations* r, const or_node_state* st, cons
     const int s = out->matched[k];
     out->requested[0] -= r->allocatable_cpu[s];
     out->requested[1] -= r->allocatable_mem[s];
-    out->nonzero[0] -= r->allocatable_cpu[s];
-    out->nonzero[1] -= r->allocatable_mem[s];
+    out->nonzero[0] -= nz_cpu_of(r, s);
+    out->nonzero[1] -= nz_mem_of(r, s);
     out->num_pods -= 1;
     out->r_allocated[0] += r->allocated_cpu[s];
     out->r_allocated[1] += r->allocated_mem[s];
@@ -91,15 +110,18 @@ int or_rsv_fits_node(const kg_pod* pod, int64_t allowed_pods, const int64_t allo
 int or_rsv_filter_with(const kg_pod* pod, int64_t allowed_pods, const int64_t alloc[2], const or_rsv_node* ns,
                        const kg_node_reservations* r, const int32_t* slots, int n_slots, int required) {
   const int64_t pc = pod->requests[KG_RES_CPU], pm = pod->requests[KG_RES_MEMORY];
+  const int kc = or_pod_cpu_key(pod), km = or_pod_mem_key(pod);
   int satisfied = 0;
   for (int k = 0; k < n_slots && !satisfied; k++) {
     const int s = slots[k];
-    if (pc == 0 && pm == 0) continue; /* Intersection(ResourceNames, pod request names) empty */
+    const int hc = r->allocatable_cpu[s] > 0, hm = r->allocatable_mem[s] > 0;
+    if (!((kc && hc) || (km && hm))) continue; /* Intersection(ResourceNames, pod request names) empty */
     const int fits = or_rsv_fits_node(pod, allowed_pods, alloc, ns, r, s);
     if (r->policy[s] == KG_RSV_POLICY_RESTRICTED) {
+      /* LessThanOrEqual(podRequests, rRemained): the reservation's keys the pod requests */
       const int64_t rc = sub_nn(r->allocatable_cpu[s], r->allocated_cpu[s]);
       const int64_t rm = sub_nn(r->allocatable_mem[s], r->allocated_mem[s]);
-      if (pc <= rc && pm <= rm && fits) satisfied = 1;
+      if ((!hc || !kc || pc <= rc) && (!hm || !km || pm <= rm) && fits) satisfied = 1;
     } else if (fits) {
       satisfied = 1;
     }
@@ -181,25 +203,67 @@ void or_rsv_case_flat(const kg_pod* pod, int64_t allowed_pods, const int64_t all
 int or_schedule_resv(const kg_config* cfg, int64_t n_nodes, const kg_node* nodes, const kg_node_metric* metrics,
                      or_node_state* st, kg_node_reservations* rsv, int64_t n_pods, const kg_pod* pods, int64_t now,
                      int32_t* out_node, int64_t* out_score, int32_t* out_slot) {
+  return or_schedule_resv_full(cfg, n_nodes, nodes, metrics, st, rsv, NULL, NULL, 0, n_pods, pods, now, 1, out_node,
+                               out_score, out_slot, NULL);
+}
+
+int or_schedule_resv_full(const kg_config* cfg, int64_t n_nodes, const kg_node* nodes, const kg_node_metric* metrics,
+                          or_node_state* st, kg_node_reservations* rsv, kg_node_device* dev, kg_quota* quotas,
+                          int64_t n_quotas, int64_t n_pods, const kg_pod* pods, int64_t now, int n_threads,
+                          int32_t* out_node, int64_t* out_score, int32_t* out_slot, int32_t* out_minors) {
   const size_t nn = (size_t)(n_nodes > 0 ? n_nodes : 1);
   int8_t* feas = (int8_t*)malloc(nn);
   int64_t* base = (int64_t*)malloc(nn * sizeof(int64_t));
   int64_t* raw = (int64_t*)malloc(nn * sizeof(int64_t));
+  int64_t* dsraw = (int64_t*)malloc(nn * sizeof(int64_t));
   int64_t* order = (int64_t*)malloc(nn * sizeof(int64_t));
   int32_t* nom = (int32_t*)malloc(nn * sizeof(int32_t));
-  if (!feas || !base || !raw || !order || !nom) {
-    free(feas); free(base); free(raw); free(order); free(nom);
+  if (!feas || !base || !raw || !dsraw || !order || !nom) {
+    free(feas); free(base); free(raw); free(dsraw); free(order); free(nom);
     return KG_E_NOMEM;
   }
+  const int rsv_on = cfg->reservation_filter || cfg->reservation_score;
+  const int ds_on = dev && (cfg->ds_filter || cfg->ds_score);
+  if (n_threads < 1) n_threads = 1;
+  /* chunkSizeFor (pkg/util/parallelize/parallelism.go:35-46) with parallelism = n_threads */
+  int64_t chunk = (int64_t)sqrt((double)n_nodes), lim = n_nodes / n_threads + 1;
+  if (chunk > lim) chunk = lim;
+  if (chunk < 1) chunk = 1;
   int rc = 0;
   for (int64_t p = 0; p < n_pods && rc == 0; p++) {
     const kg_pod* pod = &pods[p];
+    if (out_slot) out_slot[p] = -1;
+    if (out_minors) out_minors[p] = 0;
+    /* ElasticQuota PreFilter: a rejected pod is Unschedulable without a node search */
+    kg_quota* quota = NULL;
+    if (pod->quota_id > 0) {
+      if (pod->quota_id > n_quotas || !quotas) { rc = KG_E_INVALID; break; }
+      quota = &quotas[pod->quota_id - 1];
+      if (!or_quota_admit(quota, pod)) {
+        out_node[p] = -1;
+        out_score[p] = 0;
+        continue;
+      }
+    }
+    or_ds_pod dsp;
+    memset(&dsp, 0, sizeof(dsp));
+    dsp.skip = 1;
+    if (ds_on) {
+      or_ds_pod_init(pod, &dsp);
+      if (dsp.unsupported) { rc = KG_E_UNSUPPORTED; break; }
+    }
+    /* DeviceShare.FilterReservation (deviceshare/plugin.go:462-486): a pod with device requests can only use a
+     * reservation DeviceShare restored device state for; the reservations here hold none, so it is rejected and no
+     * reservation is nominated for such a pod (NominateReservation skips failing reservations, nominator.go:99-105) */
+    const int ds_blocks_nomination = ds_on && cfg->ds_filter && !dsp.skip;
+    int err = 0;
+#pragma omp parallel for schedule(dynamic, chunk) num_threads(n_threads)
     for (int64_t i = 0; i < n_nodes; i++) {
       feas[i] = 0;
       const kg_node* nd = &nodes[i];
       if (!(nd->flags & KG_NODE_VALID)) continue;
       or_rsv_node ns;
-      or_rsv_restore(cfg->reservation_filter || cfg->reservation_score ? &rsv[i] : NULL, &st[i], pod, &ns);
+      or_rsv_restore(rsv_on ? &rsv[i] : NULL, &st[i], pod, &ns);
       or_node_state rs = st[i];
       rs.requested[KG_RES_CPU] = ns.requested[0];
       rs.requested[KG_RES_MEMORY] = ns.requested[1];
@@ -210,48 +274,60 @@ int or_schedule_resv(const kg_config* cfg, int64_t n_nodes, const kg_node* nodes
       if (cfg->fit_filter && or_fit_filter(nd, &rs, pod) != 0) continue;
       if (cfg->la_filter) {
         const int f = or_loadaware_filter(cfg, nd, &metrics[i], pod, now);
-        if (f < 0) { rc = f; break; }
+        if (f < 0) { err = f; continue; }
         if (f != 0) continue;
       }
       if (cfg->reservation_filter && !or_rsv_filter(pod, nd->allowed_pods, alloc, &ns, &rsv[i])) continue;
+      if (ds_on && cfg->ds_filter && !or_ds_filter(&dev[i], &dsp)) continue;
       feas[i] = 1;
       int64_t t = 0;
       if (cfg->fit_score) t += cfg->weight_fit * or_fit_score(cfg, nd, &rs, pod);
       if (cfg->la_score) {
-        const int64_t s = or_loadaware_score(cfg, nd, &metrics[i], &st[i], pod, now);
-        if (s < 0) { rc = (int)s; break; }
-        t += cfg->weight_loadaware * s;
+        const int64_t sc = or_loadaware_score(cfg, nd, &metrics[i], &st[i], pod, now);
+        if (sc < 0) { err = (int)sc; continue; }
+        t += cfg->weight_loadaware * sc;
       }
       base[i] = t;
-      nom[i] = or_rsv_nominate(pod, nd->allowed_pods, alloc, &ns, &rsv[i]);
+      nom[i] = (rsv_on && !ds_blocks_nomination) ? or_rsv_nominate(pod, nd->allowed_pods, alloc, &ns, &rsv[i]) : -1;
       raw[i] = nom[i] >= 0 ? or_rsv_score_slot(pod, &rsv[i], nom[i]) : 0;
       order[i] = ns.has_state ? or_rsv_node_order(&ns, &rsv[i]) : INT64_MAX;
+      dsraw[i] = (ds_on && cfg->ds_score && !dsp.skip)
+                     ? or_ds_score(&dev[i], &dsp, (int)cfg->ds_scoring_strategy, cfg->ds_scoring_weights) : 0;
     }
-    if (rc) break;
+    if (err) { rc = err; break; }
     /* PreScore preferredNode (scoring.go:89-99): smallest order, first (lowest index) feasible node */
     int64_t pref = -1, best_order = INT64_MAX;
     for (int64_t i = 0; i < n_nodes; i++)
       if (feas[i] && order[i] != 0 && best_order > order[i]) { best_order = order[i]; pref = i; }
-    int64_t mx = 0;
+    int64_t mx = 0, mds = 0;
     for (int64_t i = 0; i < n_nodes; i++) {
       if (!feas[i]) continue;
-      const int64_t s = (i == pref) ? 1000 : raw[i]; /* mostPreferredScore */
-      raw[i] = s;
-      if (s > mx) mx = s;
+      const int64_t sc = (i == pref) ? 1000 : raw[i]; /* mostPreferredScore */
+      raw[i] = sc;
+      if (sc > mx) mx = sc;
+      if (dsraw[i] > mds) mds = dsraw[i];
     }
+    /* RunScorePlugins: DefaultNormalizeScore (Reservation scoring.go:126-131, DeviceShare scoring.go:95-97) × weight */
     int64_t win = -1, win_total = -1;
     for (int64_t i = 0; i < n_nodes; i++) {
       if (!feas[i]) continue;
       int64_t t = base[i];
       if (cfg->reservation_score && mx > 0) t += cfg->weight_reservation * (100 * raw[i] / mx);
+      if (ds_on && cfg->ds_score && mds > 0) t += cfg->weight_deviceshare * (100 * dsraw[i] / mds);
       if (t > win_total) { win_total = t; win = i; }
+    }
+    /* Reserve: DeviceShare allocates the minors first; a failure un-assumes the pod (Unreserve) */
+    int32_t minors = 0;
+    if (win >= 0 && ds_on && !dsp.skip) {
+      minors = or_ds_reserve(&dev[win], &dsp, (int)cfg->ds_scoring_strategy, cfg->ds_scoring_weights);
+      if (minors < 0) { minors = 0; win = -1; }
     }
     out_node[p] = (int32_t)win;
     out_score[p] = win >= 0 ? win_total : 0;
-    if (out_slot) out_slot[p] = -1;
+    if (out_minors) out_minors[p] = minors;
     if (win >= 0) {
       or_apply_pod(cfg, &st[win], pod, 1);
-      if ((cfg->reservation_filter || cfg->reservation_score) && nom[win] >= 0) {
+      if (rsv_on && nom[win] >= 0) {
         /* Reserve → reservationCache.assumePod → AddAssignedPod (reservation_info.go:317-326) */
         kg_node_reservations* r = &rsv[win];
         r->allocated_cpu[nom[win]] += pod->requests[KG_RES_CPU];
@@ -259,8 +335,9 @@ int or_schedule_resv(const kg_config* cfg, int64_t n_nodes, const kg_node* nodes
         r->assigned[nom[win]] += 1;
         if (out_slot) out_slot[p] = nom[win];
       }
+      if (quota) or_quota_charge(quota, pod);
     }
   }
-  free(feas); free(base); free(raw); free(order); free(nom);
+  free(feas); free(base); free(raw); free(dsraw); free(order); free(nom);
   return rc;
 }

@@ -115,11 +115,14 @@ def test_quotas_with_deviceshare_profile():
     cluster, dev = synth.make_gpu_cluster(400, seed=5)
     pods = synth.make_gpu_pods(1500, seed=6)
     rng = np.random.default_rng(9)
-    cpu_only = ~pods["device_requests"].any(axis=1)
-    pods["quota_id"] = np.where(cpu_only & (rng.random(len(pods)) < 0.7), rng.integers(1, 5, len(pods)), 0)
+    pods["quota_id"] = np.where(rng.random(len(pods)) < 0.7, rng.integers(1, 5, len(pods)), 0)
     quotas = np.zeros(4, dtype=abi.QUOTA_DTYPE)
-    quotas["used_limit"] = [[200_000, 400 << 30], [100_000, -1], [300_000, 200 << 30], [50_000, 100 << 30]]
+    quotas["used_limit"] = -1
     quotas["min"] = -1
+    quotas["used_limit"][:, :2] = [[200_000, 400 << 30], [100_000, -1], [300_000, 200 << 30], [50_000, 100 << 30]]
+    core, ratio = 2 + abi.DEV_GPU_CORE, 2 + abi.DEV_GPU_MEMORY_RATIO  # device pods are admitted on their GPU keys too
+    quotas["used_limit"][:, core] = [4000, 1500, -1, 800]
+    quotas["used_limit"][:, ratio] = [4000, -1, 2500, 800]
     prof = F.Profile(filter=(F.NODE_RESOURCES_FIT, F.LOAD_AWARE, F.DEVICE_SHARE),
                      score={F.NODE_RESOURCES_FIT: 1, F.LOAD_AWARE: 1, F.DEVICE_SHARE: 1})
     cfg = F.build_config(profile=prof)
@@ -136,3 +139,4 @@ def test_quotas_with_deviceshare_profile():
         got_q = e.read_quotas(len(quotas))
     assert np.array_equal(node, want) and np.array_equal(minors, want_minors)
     assert np.array_equal(got_q, q)
+    assert (want < 0).any() and (minors != 0).any()

@@ -18,7 +18,7 @@ def rsv_row(slots):
     for s, d in enumerate(slots):
         for k, v in d.items():
             r[k][s] = v
-        r["owner"][s] = 1
+        r["owner"][s] = 0
         r["available"][s] = 1
     return r
 
@@ -27,7 +27,7 @@ def rsv_row(slots):
 def test_reservation_golden(case):
     pod = np.zeros(1, dtype=abi.POD_DTYPE)[0]
     pod["requests"][0], pod["requests"][1] = case["pod"]
-    pod["reservation_owner"] = 1
+    pod["reservation_owner_mask"] = 1
     pod["reservation_flags"] = abi.POD_RSV_AFFINITY if case.get("affinity") else 0
     ok, nom, score = oracle.rsv_case(pod, case["allowed_pods"], case["alloc"], case["num_pods"],
                                      case["pod_requested"], case["r_allocated"], case["has_state"],

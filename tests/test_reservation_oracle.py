@@ -38,7 +38,7 @@ def test_reserve_bookkeeping_and_affinity():
     assert (slot >= 0).sum() > 10  # owned pods land in their reservations (weight 5000)
     for j in np.nonzero(slot >= 0)[0]:
         i, s = node[j], slot[j]
-        assert pods[j]["reservation_owner"] == rsv[i]["owner"][s]
+        assert (int(pods[j]["reservation_owner_mask"]) >> int(rsv[i]["owner"][s])) & 1
     got = r["allocated_cpu"] - rsv["allocated_cpu"]
     want = np.zeros_like(got)
     np.add.at(want, (node[slot >= 0], slot[slot >= 0]), pods["requests"][slot >= 0, abi.RES_CPU])
