@@ -66,8 +66,9 @@ def parse():
     ap.add_argument("--kernel-iters", type=int, default=20)
     ap.add_argument("--profile-pods", type=int, default=None, help="pods scheduled with live kernel timing after "
                     "the timed region (default min(pods per step, 20k))")
-    ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "r02", "traffic_c3.json"),
-                    help="PMC summary (scripts/pmc_summary.py) of the same workload: per-launch HBM bytes")
+    ap.add_argument("--traffic-file", default=None,
+                    help="PMC summary (scripts/pmc_summary.py) of the same workload: per-launch HBM bytes "
+                         "(default profiles/r02/traffic_<workload>.json)")
     ap.add_argument("--check", type=int, default=None, help="verify the first N placements against the oracle")
     return ap.parse_args()
 
@@ -342,8 +343,10 @@ def main():
                "node_evals_per_sec": m * cluster.n / dt,
                "single_thread": {"value": m1 / dt1, "sample_pods": m1}}
 
-    traffic, traffic_src = (pmc_traffic(args.traffic_file, dom, cluster.n, args.batch, args.pods_per_wave,
-                                        args.depth) if d.world == 1 else (None, None))
+    tfile = args.traffic_file or os.path.join(ROOT, "profiles", "r02", f"traffic_{wl}.json")
+    pmc_name = "eval_round_numa" if wl == "c4" else dom  # live timing folds every wide pass under "eval_round"
+    traffic, traffic_src = (pmc_traffic(tfile, pmc_name, cluster.n, args.batch, args.pods_per_wave, args.depth)
+                            if d.world == 1 else (None, None))
     if d.rank == 0:
         pods_s = total / elapsed
         desc = {
@@ -393,6 +396,8 @@ def main():
                          "timing": "live HIP events around every launch of %d extra queued pods (kg_profile_enable)"
                                    % n_prof if dom in live else "isolated replay (kg_bench_kernel)",
                          "per_evaluation_rate_gbs": per_eval,
+                         "traffic_rate_gbs": traffic / (dom_ms * 1e-3) / 1e9 if traffic else None,
+                         "traffic_frac": traffic / (dom_ms * 1e-3) / 1e9 / HBM_PEAK_GBS if traffic else None,
                          "live_ms": {k: v["avg_ms"] for k, v in live.items()},
                          "live_launches": {k: v["launches"] for k, v in live.items()},
                          "isolated_ms": {k: v[0] for k, v in isolated.items()}},

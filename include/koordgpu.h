@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define KG_ABI_VERSION 5
+#define KG_ABI_VERSION 6
 
 /* ---- resource slots (fixed order) ------------------------------------------------------- */
 enum {
@@ -333,6 +333,18 @@ int kg_nccl_unique_id(void* out128);
 int kg_engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank, int n_ranks,
                      const void* nccl_unique_id, kg_engine** out);
 void kg_engine_destroy(kg_engine* e);
+
+/* Test hook (not a product path): n_ranks engines in ONE process, usually on one device, exchanging their
+ * per-round candidate records (and DeviceShare's per-round maxima) by device copies ordered with HIP events
+ * instead of RCCL, which runs one rank per device.  Every other step — the sharded wide pass, the rank-record
+ * merge (merge_round over n_ranks records), the replicated resolver — is the multi-rank engine itself.  Each
+ * rank's engine must be driven from its own host thread with the same calls in the same order (a host barrier
+ * pairs the ranks' exchanges; it fails with KG_E_COLLECTIVE after 60 s without a peer). */
+typedef struct kg_loopback kg_loopback;
+int kg_loopback_create(int n_ranks, kg_loopback** out);
+void kg_loopback_destroy(kg_loopback* lb);
+int kg_engine_create_loopback(const kg_config* cfg, int64_t capacity_nodes, int rank, int n_ranks, kg_loopback* lb,
+                              kg_engine** out);
 
 int kg_nodes_upsert(kg_engine* e, const kg_node* nodes, const int32_t* idx, int64_t n);
 int kg_nodes_delete(kg_engine* e, const int32_t* idx, int64_t n);

@@ -35,7 +35,7 @@ POD_REQUEST_KEYS, POD_CPU_KEY, POD_MEM_KEY = 8, 16, 32
 MAX_OWNER_GROUPS = 64
 QUOTA_RES = 8
 MAX_QUOTAS = 64
-ABI_VERSION = 5
+ABI_VERSION = 6
 MAX_RSV_SLOTS = 4
 RSV_POLICY = {"Default": 0, "Aligned": 1, "Restricted": 2}
 POD_RSV_AFFINITY = 1
@@ -157,7 +157,8 @@ EXPORTED_SYMBOLS = (
     "kg_nodes_numa_upsert", "kg_nodes_read_numa", "kg_results_fetch_cpusets", "kg_pods_evaluate_numa",
     "kg_nodes_device_upsert", "kg_nodes_read_device", "kg_results_fetch_devices", "kg_pods_evaluate_device",
     "kg_quotas_set", "kg_quotas_read", "kg_nodes_reservation_upsert", "kg_nodes_read_reservations",
-    "kg_results_fetch_reservations", "kg_profile_enable", "kg_profile_read",
+    "kg_results_fetch_reservations", "kg_profile_enable", "kg_profile_read", "kg_loopback_create",
+    "kg_loopback_destroy", "kg_engine_create_loopback",
 )
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
@@ -224,6 +225,9 @@ def load_library(path: str | None = None):
         "kg_results_fetch_reservations": (i, [vp, i64, i64, vp]),
         "kg_profile_enable": (i, [vp, i]),
         "kg_profile_read": (i, [vp, vp, vp]),
+        "kg_loopback_create": (i, [i, ctypes.POINTER(vp)]),
+        "kg_loopback_destroy": (None, [vp]),
+        "kg_engine_create_loopback": (i, [vp, i64, i, i, vp, ctypes.POINTER(vp)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)

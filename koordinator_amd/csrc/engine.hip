@@ -18,6 +18,8 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <condition_variable>
+#include <mutex>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -1205,9 +1207,9 @@ __global__ __launch_bounds__(kWave* kEvalWaves) void ds_max_round(DevTable T, Ds
                                                                    const DevPod* __restrict__ pods,
                                                                    const DsPod* __restrict__ dpods,
                                                                    const int64_t* __restrict__ ctl, int64_t end,
-                                                                   int B, int pods_per_wave, int64_t n_local,
-                                                                   int nt_local, EvalParams P, DsParams DP,
-                                                                   uint64_t* __restrict__ dsmax,
+                                                                   int B, int pods_per_wave, int64_t base,
+                                                                   int64_t n_local, int nt_local, EvalParams P,
+                                                                   DsParams DP, uint64_t* __restrict__ dsmax,
                                                                    uint32_t* __restrict__ dsval) {
   int64_t first;
   int nb;
@@ -1224,16 +1226,16 @@ __global__ __launch_bounds__(kWave* kEvalWaves) void ds_max_round(DevTable T, Ds
 #pragma unroll
   for (int k = 0; k < kDsPpw; ++k) mx[k] = 0, cnt[k] = 0;
   for (int j = 0; j < kNPT; ++j) {
-    const int64_t i = (int64_t)tile * kTile + j * kWave + lane;
+    const int64_t i = (int64_t)tile * kTile + j * kWave + lane;  // shard-local; the node is base + i
     if (i >= n_local) break;
     // Fit + LoadAware on the compact hoisted row of the C3 wide pass (eval_hot); a row outside its exact
     // domain (F_RARE) sends this node row of the wave to the reference-shaped eval_node
-    const HotRow h = load_hot<PF>(T, i, P);
+    const HotRow h = load_hot<PF>(T, base + i, P);
     const bool rare = __ballot((h.flags & F_RARE) != 0) != 0;
     Row row;
     row.flags = 0;
-    if (rare) row = load_row(T, i);
-    const DsNode d = DT.d[i];
+    if (rare) row = load_row(T, base + i);
+    const DsNode d = DT.d[base + i];
 #pragma unroll
     for (int k = 0; k < kDsPpw; ++k) {
       if (k >= np) break;
@@ -1298,8 +1300,29 @@ __global__ __launch_bounds__(256) void ds_norm_reduce(const int64_t* __restrict_
   }
 }
 
+// several ranks: the global (M + 1, holders) per pod from the ranks' (all-gathered) shard values — the max of M,
+// the holders summed over the ranks that hold it
+__global__ __launch_bounds__(kMaxB) void ds_norm_combine(const int64_t* __restrict__ ctl, int64_t end, int B,
+                                                         const uint64_t* __restrict__ all, int n_ranks,
+                                                         uint64_t* __restrict__ dsnorm) {
+  int64_t first;
+  int nb;
+  if (!ds_round_range(ctl, end, B, first, nb)) return;
+  const int pod = threadIdx.x;
+  if (pod >= nb) return;
+  uint32_t M = 0, C = 0;
+  for (int r = 0; r < n_ranks; ++r) {
+    const uint64_t v = all[(size_t)r * B + pod];
+    const uint32_t vm = (uint32_t)(v >> 32), vc = (uint32_t)v;
+    C = vm > M ? vc : C + (vm == M ? vc : 0u);
+    M = vm > M ? vm : M;
+  }
+  dsnorm[pod] = ((uint64_t)M << 32) | C;
+}
+
 __global__ __launch_bounds__(kWave* kEvalWaves) void eval_round_ds(const int64_t* __restrict__ ctl, int64_t end,
-                                                                    int B, int pods_per_wave, int64_t n_local,
+                                                                    int B, int pods_per_wave, int64_t base,
+                                                                    int64_t n_local,
                                                                     int nt_local, EvalParams P, DsParams DP,
                                                                     const uint64_t* __restrict__ dsnorm,
                                                                     const uint32_t* __restrict__ dsval,
@@ -1319,16 +1342,19 @@ __global__ __launch_bounds__(kWave* kEvalWaves) void eval_round_ds(const int64_t
   const int np = ((p0 + pods_per_wave) < nb ? (p0 + pods_per_wave) : nb) - p0;
   const int vbits = P.score_bits + 1;
   const size_t stride = (size_t)nt_local * kTile;
-  uint32_t gidx[kNPT];
+  uint32_t gidx[kNPT], lidx[kNPT];  // global node index (the key), shard-local index (dsval)
 #pragma unroll
-  for (int j = 0; j < kNPT; ++j) gidx[j] = (uint32_t)((int64_t)tile * kTile + j * kWave + lane);
+  for (int j = 0; j < kNPT; ++j) {
+    lidx[j] = (uint32_t)((int64_t)tile * kTile + j * kWave + lane);
+    gidx[j] = (uint32_t)(base + lidx[j]);
+  }
   for (int k = 0; k < np; ++k) {
     const uint32_t mm = (uint32_t)(dsnorm[p0 + k] >> 32);
     const uint32_t M = mm ? mm - 1u : 0u;
     uint32_t v[kNPT];
 #pragma unroll
     for (int j = 0; j < kNPT; ++j) {
-      const uint32_t pk = (int64_t)gidx[j] < n_local ? dsval[(size_t)(p0 + k) * stride + gidx[j]] : 0u;
+      const uint32_t pk = (int64_t)lidx[j] < n_local ? dsval[(size_t)(p0 + k) * stride + lidx[j]] : 0u;
       const uint32_t t = (pk - 1u) >> 8, raw = (pk - 1u) & 255u;
       v[j] = pk ? t + (DP.score ? (uint32_t)(DP.weight * ds_normalized(raw, M)) : 0u) + 1u : 0u;
     }
@@ -1350,7 +1376,9 @@ __global__ __launch_bounds__(kWave) void resolve_round_ds(DevTable T, DsTable DT
                                                            DsParams DP, uint64_t* __restrict__ out_keys,
                                                            int32_t* __restrict__ out_minors, int bitmap_words,
                                                            QuotaRow* __restrict__ quotas, int nq,
-                                                           const int64_t* __restrict__ qdev) {
+                                                           const int64_t* __restrict__ qdev, int sharded) {
+  // sharded (several ranks): dsval holds only this rank's shard, so a modified row's round-start value is
+  // re-evaluated from its round-start Row / DsNode copies (s_r0 / s_d0) instead of read from dsval
   extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
   const int lane = threadIdx.x;
   int64_t first;
@@ -1364,7 +1392,9 @@ __global__ __launch_bounds__(kWave) void resolve_round_ds(DevTable T, DsTable DT
   QuotaRow* s_q = reinterpret_cast<QuotaRow*>(s_stg + (size_t)nb * kDsNodeWords);  // [nq] quota rows
   int64_t* s_qdev = reinterpret_cast<int64_t*>(s_q + nq);   // [nb][kQuotaRes] device quota requests
   Row* s_srow = reinterpret_cast<Row*>(s_qdev + (size_t)nb * kQuotaRes);  // [nb] its Row
-  uint32_t* bitmap = reinterpret_cast<uint32_t*>(s_srow + nb);
+  DsNode* s_d0 = reinterpret_cast<DsNode*>(s_srow + nb);    // sharded: [kWave] round-start DsNode per modified lane
+  Row* s_r0 = reinterpret_cast<Row*>(s_d0 + (sharded ? kWave : 0));  // sharded: [kWave] round-start Row
+  uint32_t* bitmap = reinterpret_cast<uint32_t*>(s_r0 + (sharded ? kWave : 0));
   for (int w = lane; w < nb * kCandStride; w += kWave) s_cand[w] = cand[w];
   {
     const uint64_t* pw = reinterpret_cast<const uint64_t*>(pods + first);
@@ -1423,7 +1453,15 @@ __global__ __launch_bounds__(kWave) void resolve_round_ds(DevTable T, DsTable DT
     bool cf = false, have_cur = false;
     int64_t ct = 0, craw = 0;
     if (DP.score && Mrs > 0 && Crs <= (uint32_t)nM) {
-      const uint32_t pk = lane < nM ? dsval[(size_t)j * dsval_stride + midx] : 0u;
+      uint32_t pk = 0;
+      if (lane < nM) {
+        if (sharded) {
+          int64_t t0 = 0, raw0 = 0;
+          pk = (eval_node(s_r0[lane], p, P, t0) && ds_eval(s_d0[lane], dp, DP, raw0)) ? (uint32_t)raw0 + 1u : 0u;
+        } else {
+          pk = dsval[(size_t)j * dsval_stride + midx];
+        }
+      }
       const bool rf = pk != 0;
       const int64_t rraw = (int64_t)((pk - 1u) & 255u);
       const uint32_t lost = (uint32_t)__popcll(__ballot(rf && (uint32_t)rraw + 1u == Mrs));
@@ -1466,6 +1504,10 @@ __global__ __launch_bounds__(kWave) void resolve_round_ds(DevTable T, DsTable DT
         const DsNode* from = src >= 0 ? reinterpret_cast<const DsNode*>(s_stg) + src : DT.d + w;
         mrow = src >= 0 ? s_srow[src] : load_row(T, w);
         __builtin_memcpy(&s_dc[owner], from, sizeof(DsNode));
+        if (sharded) {
+          s_r0[owner] = mrow;
+          __builtin_memcpy(&s_d0[owner], from, sizeof(DsNode));
+        }
       }
       if (lane == 0) bitmap[w >> 5] |= 1u << (w & 31);
       ++nM;
@@ -1703,9 +1745,25 @@ int64_t bits_for(int64_t v) {
 
 }  // namespace
 
+// In-process rank group (test hook, kg_engine_create_loopback): the ranks' exchange buffers and events, and a
+// host barrier that pairs their exchanges call by call.
+struct kg_loopback {
+  int n = 0;
+  std::mutex mu;
+  std::condition_variable cv;
+  int arrived = 0;
+  uint64_t gen = 0;
+  bool failed = false;
+  std::vector<kg_engine*> ranks;
+  std::vector<const uint64_t*> buf;  // this exchange: each rank's buffer holding its record at [rank · cnt]
+  std::vector<hipEvent_t> ready, done;
+};
+
 struct kg_engine {
   kg_config cfg;
   int rank = 0, n_ranks = 1;
+  kg_loopback* lb = nullptr;  // test hook: exchanges through device copies instead of RCCL
+  hipEvent_t lb_ready = nullptr, lb_done = nullptr;
   int device = 0;
   hipStream_t stream = nullptr;
   ncclComm_t comm = nullptr;
@@ -1757,6 +1815,7 @@ struct kg_engine {
   DevBuf<int32_t> out_minors;  // [staged + kMaxB]
   DevBuf<uint64_t> dsmax;      // [B][nt_local]
   DevBuf<uint64_t> dsnorm;     // [B]
+  DevBuf<uint64_t> dsnorm_all; // [n_ranks][B]: every rank's shard maxima (several ranks)
   DevBuf<uint32_t> dsval;      // [B][nt_local·256]: packed (Fit+LoadAware total, raw DeviceShare) per (pod, node)
   // ElasticQuota admission table (kg_quotas_set)
   DevBuf<QuotaRow> quotas;     // [KG_MAX_QUOTAS] full kg_quota rows (cpu, memory, device resources)
@@ -2347,6 +2406,48 @@ void launch_resolve(kg_engine* e, const RoundGeom& g, int64_t first, int nb, int
 #undef KG_RESOLVE
 }
 
+int lb_barrier(kg_loopback* lb) {
+  std::unique_lock<std::mutex> lk(lb->mu);
+  const uint64_t g = lb->gen;
+  if (lb->failed) return fail(KG_E_COLLECTIVE, "loopback group failed");
+  if (++lb->arrived == lb->n) {
+    lb->arrived = 0;
+    ++lb->gen;
+    lb->cv.notify_all();
+    return 0;
+  }
+  if (!lb->cv.wait_for(lk, std::chrono::seconds(60), [&] { return lb->gen != g || lb->failed; })) {
+    lb->failed = true;
+    lb->cv.notify_all();
+    return fail(KG_E_COLLECTIVE, "loopback exchange: a peer rank did not arrive within 60 s");
+  }
+  return lb->failed ? fail(KG_E_COLLECTIVE, "loopback group failed") : 0;
+}
+
+// All-gather of `cnt` words per rank in `all` ([n_ranks][cnt], this rank's part already written on stream st):
+// ncclAllGather over RCCL, or — loopback test hook — device copies from the peers' buffers, ordered by events.
+int rank_allgather(kg_engine* e, uint64_t* all, size_t cnt, int slot, hipStream_t st) {
+  if (!e->lb) {
+    NCCL_TRY(ncclAllGather(all + (size_t)e->rank * cnt, all, cnt, ncclUint64, e->comms[slot], st));
+    return 0;
+  }
+  kg_loopback* lb = e->lb;
+  HIP_TRY(hipEventRecord(e->lb_ready, st));
+  lb->buf[e->rank] = all;
+  if (int rc = lb_barrier(lb)) return rc;
+  for (int q = 0; q < lb->n; ++q) {
+    if (q == e->rank) continue;
+    HIP_TRY(hipStreamWaitEvent(st, lb->ready[q], 0));
+    HIP_TRY(hipMemcpyAsync(all + (size_t)q * cnt, lb->buf[q] + (size_t)q * cnt, cnt * 8, hipMemcpyDeviceToDevice, st));
+  }
+  HIP_TRY(hipEventRecord(e->lb_done, st));
+  if (int rc = lb_barrier(lb)) return rc;
+  // a peer's later writes into its buffer (same stream as its reads of it) wait for this rank's copies
+  for (int q = 0; q < lb->n; ++q)
+    if (q != e->rank) HIP_TRY(hipStreamWaitEvent(st, lb->done[q], 0));
+  return 0;
+}
+
 // merge → [all-gather + merge of the rank records] of one round, on stream st
 int launch_merge(kg_engine* e, const RoundGeom& g, int nb, int slot, hipStream_t st) {
   launch_merge_local(e, g, nb, slot, st);
@@ -2354,7 +2455,7 @@ int launch_merge(kg_engine* e, const RoundGeom& g, int nb, int slot, hipStream_t
   if (e->n_ranks > 1) {
     const size_t cnt = (size_t)g.B * kCandStride;
     uint64_t* all = gathered_slot(e, g, slot);
-    NCCL_TRY(ncclAllGather(all + (size_t)e->rank * cnt, all, cnt, ncclUint64, e->comms[slot], st));
+    if (int rc = rank_allgather(e, all, cnt, slot, st)) return rc;
     launch_merge_ranks(e, g, nb, slot, st);
     HIP_TRY(hipGetLastError());
   }
@@ -2398,56 +2499,65 @@ int run_batch(kg_engine* e, const RoundGeom& g, int64_t cur, int64_t end, int64_
 }
 
 // ---- DeviceShare rounds: cursor-driven, unpipelined, all on rs[0] ----
-size_t resolve_ds_lds_bytes(const RoundGeom& g, int nb, int nq) {
+size_t resolve_ds_lds_bytes(const RoundGeom& g, int nb, int nq, bool sharded) {
   return ((size_t)nb * (kCandStride + kPodWords + kDsPodWords + kDsNodeWords + kQuotaRes) + (size_t)kWave * kDsNodeWords) * 8 +
-         (size_t)nq * sizeof(QuotaRow) + (size_t)nb * sizeof(Row) + (size_t)g.bitmap_words * 4;
+         (size_t)nq * sizeof(QuotaRow) + (size_t)nb * sizeof(Row) +
+         (sharded ? (size_t)kWave * (sizeof(DsNode) + sizeof(Row)) : 0) + (size_t)g.bitmap_words * 4;
 }
 
-void launch_round_ds(kg_engine* e, const RoundGeom& g, int64_t end, hipStream_t st, int which = -1) {
+int launch_round_ds(kg_engine* e, const RoundGeom& g, int64_t end, hipStream_t st, int which = -1) {
   const DsTable DT{e->ds_d.p};
+  const bool sharded = e->n_ranks > 1;
   const dim3 grid = eval_grid(g, g.B);
   size_t t;
   if (which < 0 || which == 3) {
     t = prof_begin(e, st);
 #define KG_DSMAX(X)                                                                                             \
   ds_max_round<X><<<grid, kWave * kEvalWaves, 0, st>>>(e->T, DT, e->pods.p, e->dpods.p, e->cursor.p, end, g.B, g.ppw, \
-                                                       g.n_local, g.nt_local, e->P, e->DP, e->dsmax.p, e->dsval.p)
+                                                       g.base, g.n_local, g.nt_local, e->P, e->DP, e->dsmax.p,     \
+                                                       e->dsval.p)
     KG_PF_SWITCH(profile_bits(e->P), KG_DSMAX)
 #undef KG_DSMAX
     prof_end(e, KG_PROF_DS_MAX, t, st);
   }
   if (which < 0 || which == 4) {
     t = prof_begin(e, st);
-    ds_norm_reduce<<<g.B, 256, 0, st>>>(e->cursor.p, end, g.B, e->dsmax.p, g.nt_local, e->dsnorm.p);
+    uint64_t* mine = sharded ? e->dsnorm_all.p + (size_t)e->rank * g.B : e->dsnorm.p;
+    ds_norm_reduce<<<g.B, 256, 0, st>>>(e->cursor.p, end, g.B, e->dsmax.p, g.nt_local, mine);
+    if (sharded) {  // the per-pod normalization maxima over every rank's shard
+      if (int rc = rank_allgather(e, e->dsnorm_all.p, (size_t)g.B, 0, st)) return rc;
+      ds_norm_combine<<<1, kMaxB, 0, st>>>(e->cursor.p, end, g.B, e->dsnorm_all.p, e->n_ranks, e->dsnorm.p);
+    }
     prof_end(e, KG_PROF_DS_NORM, t, st);
   }
   if (which < 0 || which == 0) {
     t = prof_begin(e, st);
-    eval_round_ds<<<grid, kWave * kEvalWaves, 0, st>>>(e->cursor.p, end, g.B, g.ppw, g.n_local, g.nt_local, e->P,
-                                                        e->DP, e->dsnorm.p, e->dsval.p, lists_slot(e, g, 0));
+    eval_round_ds<<<grid, kWave * kEvalWaves, 0, st>>>(e->cursor.p, end, g.B, g.ppw, g.base, g.n_local, g.nt_local,
+                                                        e->P, e->DP, e->dsnorm.p, e->dsval.p, lists_slot(e, g, 0));
     prof_end(e, KG_PROF_EVAL, t, st);
   }
   if (which < 0 || which == 1) {
     t = prof_begin(e, st);
-    launch_merge_local(e, g, g.B, 0, st);
+    if (int rc = launch_merge(e, g, g.B, 0, st)) return rc;
     prof_end(e, KG_PROF_MERGE, t, st);
   }
   if (which < 0 || which == 2) {
     t = prof_begin(e, st);
-    resolve_round_ds<<<1, kWave, resolve_ds_lds_bytes(g, g.B, e->nq), st>>>(e->T, DT, e->pods.p, e->dpods.p,
+    resolve_round_ds<<<1, kWave, resolve_ds_lds_bytes(g, g.B, e->nq, sharded), st>>>(e->T, DT, e->pods.p, e->dpods.p,
                                                                             e->cursor.p, end, g.B, cand_slot(e, g, 0),
                                                                             e->dsnorm.p, e->dsval.p,
                                                                             (int64_t)g.nt_local * kTile, e->P, e->DP,
                                                                             e->out_keys.p, e->out_minors.p,
                                                                             g.bitmap_words, e->quotas.p, e->nq,
-                                                                            e->qdev.p);
+                                                                            e->qdev.p, (int)sharded);
     prof_end(e, KG_PROF_RESOLVE, t, st);
   }
+  return 0;
 }
 
 int run_batch_ds(kg_engine* e, const RoundGeom& g, int64_t end, int64_t n_rounds) {
   for (int64_t r = 0; r < n_rounds; ++r) {
-    launch_round_ds(e, g, end, e->rs[0]);
+    if (int rc = launch_round_ds(e, g, end, e->rs[0])) return rc;
     HIP_TRY(hipGetLastError());
   }
   HIP_TRY(hipStreamSynchronize(e->rs[0]));
@@ -2461,6 +2571,9 @@ int prepare_rounds(kg_engine* e, RoundGeom& g) {
   if (g.nt_local > kMergeThreads * kMergeChunks)
     return fail(KG_E_UNSUPPORTED, "%lld nodes per rank exceed one merge block (%d)", (long long)g.shard,
                 kMergeThreads * kMergeChunks * kTile);
+  if (e->ds_on && resolve_ds_lds_bytes(g, g.B, e->nq, e->n_ranks > 1) > kMaxLds)
+    return fail(KG_E_UNSUPPORTED, "DeviceShare resolver LDS %zu B > %zu B: fewer nodes or a smaller batch_pods",
+                resolve_ds_lds_bytes(g, g.B, e->nq, e->n_ranks > 1), kMaxLds);
   if (!e->numa_on && !e->ds_on && resolve_lds_bytes(g, g.B) > kMaxLds)
     return fail(KG_E_UNSUPPORTED, "resolver LDS %zu B > %zu B: fewer nodes or a smaller batch_pods",
                 resolve_lds_bytes(g, g.B), kMaxLds);
@@ -2475,6 +2588,8 @@ int prepare_rounds(kg_engine* e, RoundGeom& g) {
   if (e->ds_on) {
     if (int rc = e->dsmax.ensure((size_t)g.B * g.nt_local)) return rc;
     if (int rc = e->dsnorm.ensure((size_t)g.B)) return rc;
+    if (e->n_ranks > 1)
+      if (int rc = e->dsnorm_all.ensure((size_t)e->n_ranks * g.B)) return rc;
     if (int rc = e->dsval.ensure((size_t)g.B * g.nt_local * kTile)) return rc;
   }
   return 0;
@@ -2653,14 +2768,19 @@ int kg_nccl_unique_id(void* out128) {
   return 0;
 }
 
-int kg_engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank, int n_ranks, const void* nccl_id,
-                     kg_engine** out) {
+static int engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank, int n_ranks, const void* nccl_id,
+                         kg_loopback* lb, kg_engine** out) {
   if (!out) return fail(KG_E_INVALID, "out is NULL");
   *out = nullptr;
   if (int rc = validate_config(cfg)) return rc;
   if (capacity_nodes <= 0 || capacity_nodes > kMaxNodes) return fail(KG_E_INVALID, "capacity_nodes out of range");
   if (n_ranks < 1 || rank < 0 || rank >= n_ranks) return fail(KG_E_INVALID, "rank/n_ranks");
-  if (n_ranks > 1 && !nccl_id) return fail(KG_E_INVALID, "nccl_unique_id required for n_ranks>1");
+  if (n_ranks > 1 && !nccl_id && !lb) return fail(KG_E_INVALID, "nccl_unique_id required for n_ranks>1");
+  if (lb) {
+    std::lock_guard<std::mutex> lk(lb->mu);
+    if (lb->n != n_ranks) return fail(KG_E_INVALID, "loopback group of %d ranks, engine n_ranks %d", lb->n, n_ranks);
+    if (lb->ranks[rank]) return fail(KG_E_INVALID, "loopback rank %d already has an engine", rank);
+  }
   kg_engine* e = new kg_engine();
   e->cfg = *cfg;
   if (e->cfg.batch_pods == 0) e->cfg.batch_pods = 32;
@@ -2733,7 +2853,6 @@ int kg_engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank, int
   e->P.la_score = (int)(c.la_score != 0);
   e->numa_on = c.numa_filter || c.numa_score;
   e->ds_on = c.ds_filter || c.ds_score;
-  if (e->ds_on && n_ranks > 1) return bail(fail(KG_E_UNSUPPORTED, "DeviceShare profiles run on one rank"));
   e->rsv_on = c.reservation_filter || c.reservation_score;
   if (e->rsv_on && n_ranks > 1) return bail(fail(KG_E_UNSUPPORTED, "Reservation profiles run on one rank"));
   e->RP.filter = (int32_t)(c.reservation_filter != 0);
@@ -2768,8 +2887,9 @@ int kg_engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank, int
       return bail(fail(KG_E_DEVICE, "hipMemcpy"));
     const int lds = (int)(kMaxNodes / 8 + ((size_t)32 * (kCandStride + kPodWords + kDsPodWords + kDsNodeWords + kQuotaRes) +
                                            (size_t)kWave * kDsNodeWords) * 8 + KG_MAX_QUOTAS * sizeof(QuotaRow) +
-                          32 * sizeof(Row));
-    if (hipFuncSetAttribute((const void*)resolve_round_ds, hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess)
+                          32 * sizeof(Row) + (size_t)kWave * (sizeof(DsNode) + sizeof(Row)));
+    const int lds_cap = (int)std::min<size_t>((size_t)lds, 160 * 1024);  // prepare_rounds checks the real need
+    if (hipFuncSetAttribute((const void*)resolve_round_ds, hipFuncAttributeMaxDynamicSharedMemorySize, lds_cap) != hipSuccess)
       return bail(fail(KG_E_DEVICE, "hipFuncSetAttribute(resolve_round_ds LDS)"));
   }
   e->NP.filter = (int32_t)(c.numa_filter != 0);
@@ -2815,7 +2935,16 @@ int kg_engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank, int
 #undef KG_ATTR
     if (fe != hipSuccess) return bail(fail(KG_E_DEVICE, "hipFuncSetAttribute(resolve_round LDS)"));
   }
-  if (n_ranks > 1) {
+  if (lb) {
+    if (hipEventCreateWithFlags(&e->lb_ready, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&e->lb_done, hipEventDisableTiming) != hipSuccess)
+      return bail(fail(KG_E_DEVICE, "hipEventCreate"));
+    std::lock_guard<std::mutex> lk(lb->mu);
+    e->lb = lb;
+    lb->ranks[rank] = e;
+    lb->ready[rank] = e->lb_ready;
+    lb->done[rank] = e->lb_done;
+  } else if (n_ranks > 1) {
     ncclUniqueId id;
     std::memcpy(&id, nccl_id, sizeof(id));
     if (ncclCommInitRank(&e->comm, n_ranks, id, rank) != ncclSuccess) return bail(fail(KG_E_COLLECTIVE, "ncclCommInitRank"));
@@ -2829,11 +2958,43 @@ int kg_engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank, int
   return 0;
 }
 
+int kg_engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank, int n_ranks, const void* nccl_id,
+                     kg_engine** out) {
+  return engine_create(cfg, capacity_nodes, rank, n_ranks, nccl_id, nullptr, out);
+}
+
+int kg_loopback_create(int n_ranks, kg_loopback** out) {
+  if (!out || n_ranks < 1 || n_ranks > 64) return fail(KG_E_INVALID, "n_ranks in [1, 64]");
+  kg_loopback* lb = new kg_loopback();
+  lb->n = n_ranks;
+  lb->ranks.assign(n_ranks, nullptr);
+  lb->buf.assign(n_ranks, nullptr);
+  lb->ready.assign(n_ranks, nullptr);
+  lb->done.assign(n_ranks, nullptr);
+  *out = lb;
+  return 0;
+}
+
+void kg_loopback_destroy(kg_loopback* lb) { delete lb; }
+
+int kg_engine_create_loopback(const kg_config* cfg, int64_t capacity_nodes, int rank, int n_ranks, kg_loopback* lb,
+                              kg_engine** out) {
+  if (!lb) return fail(KG_E_INVALID, "loopback group is NULL");
+  return engine_create(cfg, capacity_nodes, rank, n_ranks, nullptr, lb, out);
+}
+
 void kg_engine_destroy(kg_engine* e) {
   if (!e) return;
+  if (e->lb) {
+    std::lock_guard<std::mutex> lk(e->lb->mu);
+    e->lb->ranks[e->rank] = nullptr;
+    e->lb->ready[e->rank] = e->lb->done[e->rank] = nullptr;
+  }
   if (e->stream) (void)hipStreamSynchronize(e->stream);
   for (int k = 0; k < kMaxDepth; ++k)
     if (e->rs[k]) (void)hipStreamSynchronize(e->rs[k]);
+  if (e->lb_ready) (void)hipEventDestroy(e->lb_ready);
+  if (e->lb_done) (void)hipEventDestroy(e->lb_done);
   for (int k = 1; k < kMaxDepth; ++k)
     if (e->comms[k]) ncclCommDestroy(e->comms[k]);
   if (e->comm) ncclCommDestroy(e->comm);
@@ -2863,6 +3024,7 @@ void kg_engine_destroy(kg_engine* e) {
   e->out_minors.release();
   e->dsmax.release();
   e->dsnorm.release();
+  e->dsnorm_all.release();
   e->dsval.release();
   e->rsv_d.release();
   e->rsv_nd.release();
@@ -3448,7 +3610,7 @@ int kg_bench_kernel(kg_engine* e, int which, int iters, double* avg_ms, double* 
   if (int rc = snapshot(false)) return rc;
   HIP_TRY(hipMemcpyAsync(e->cursor.p, zero4, 48, hipMemcpyHostToDevice, e->stream));
   // one real round: valid lists and candidates to replay on
-  if (int rc = e->ds_on ? (launch_round_ds(e, g, end, e->stream), 0) : run_batch(e, g, 0, end, 1)) return rc;
+  if (int rc = e->ds_on ? launch_round_ds(e, g, end, e->stream) : run_batch(e, g, 0, end, 1)) return rc;
   HIP_TRY(hipGetLastError());
   if (int rc = snapshot(true)) return rc;
   hipEvent_t a, b;
@@ -3458,7 +3620,9 @@ int kg_bench_kernel(kg_engine* e, int which, int iters, double* avg_ms, double* 
   for (int it = 0; it < iters; ++it) {
     HIP_TRY(hipMemcpyAsync(e->cursor.p, zero4, 48, hipMemcpyHostToDevice, e->stream));
     HIP_TRY(hipEventRecord(a, e->stream));
-    if (e->ds_on) launch_round_ds(e, g, end, e->stream, which);
+    if (e->ds_on) {
+      if (int rc = launch_round_ds(e, g, end, e->stream, which)) return rc;
+    }
     else if (which == 0) launch_eval(e, g, 0, nb, 0, e->stream);
     else if (which == 1) launch_merge_local(e, g, nb, 0, e->stream);
     else launch_resolve(e, g, 0, nb, 0, 0, 1, 0, e->stream);

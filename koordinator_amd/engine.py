@@ -25,20 +25,46 @@ def nccl_unique_id() -> bytes:
     return buf.raw
 
 
+class Loopback:
+    """kg_loopback (test hook): n ranks' engines in one process exchanging their round records by device copies
+    instead of RCCL.  Drive each rank's engine from its own thread (ctypes releases the GIL in the calls)."""
+
+    def __init__(self, n_ranks: int):
+        self.lib = abi.load_library()
+        h = ctypes.c_void_p()
+        check(self.lib, self.lib.kg_loopback_create(int(n_ranks), ctypes.byref(h)))
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.kg_loopback_destroy(self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
 class Engine:
     """One engine = one rank's GPU-resident node table (replicated) + its evaluation shard."""
 
     def __init__(self, config: np.ndarray, capacity: int, rank: int = 0, n_ranks: int = 1,
-                 nccl_id: bytes | None = None):
+                 nccl_id: bytes | None = None, loopback: Loopback | None = None):
         self.lib = abi.load_library()
         self._cfg = np.array(config, dtype=abi.CONFIG_DTYPE).reshape(1)
         h = ctypes.c_void_p()
         idbuf = None
         if nccl_id is not None:
             idbuf = ctypes.create_string_buffer(bytes(nccl_id), 128)
-        check(self.lib, self.lib.kg_engine_create(ptr(self._cfg), int(capacity), int(rank), int(n_ranks),
-                                                  ctypes.cast(idbuf, ctypes.c_void_p) if idbuf else None,
-                                                  ctypes.byref(h)))
+        if loopback is not None:
+            check(self.lib, self.lib.kg_engine_create_loopback(ptr(self._cfg), int(capacity), int(rank), int(n_ranks),
+                                                               loopback.h, ctypes.byref(h)))
+        else:
+            check(self.lib, self.lib.kg_engine_create(ptr(self._cfg), int(capacity), int(rank), int(n_ranks),
+                                                      ctypes.cast(idbuf, ctypes.c_void_p) if idbuf else None,
+                                                      ctypes.byref(h)))
         self.h = h
         self.capacity = capacity
 
