@@ -352,6 +352,19 @@ int kg_node_metrics_update(kg_engine* e, const kg_node_metric* m, const int32_t*
 
 int kg_pods_add(kg_engine* e, const kg_pod* pods, const int32_t* node_idx, int64_t n);
 int kg_pods_remove(kg_engine* e, const kg_pod* pods, const int32_t* node_idx, int64_t n);
+/* The framework's Unreserve (RunReservePluginsUnreserve after a failed Permit / PreBind / Bind) of staged pods
+ * [first, first+count) that kg_pods_schedule_staged placed, `mask` (nullable, count bytes) selecting them: every
+ * enabled plugin releases what its Reserve took — NodeInfo.RemovePod + the LoadAware assign cache
+ * (loadaware/pod_assign_cache.go:119-131), the NodeNUMAResource cpuset and NUMA resources
+ * (nodenumaresource/plugin.go:417-425), the DeviceShare GPU minors (deviceshare/plugin.go:440-455), the
+ * reservation assume (reservation/plugin.go:561-583) and the ElasticQuota charge (elasticquota/plugin.go:348-360).
+ * The pods' decisions are cleared (fetch → -1); a pod is released at most once. */
+int kg_pods_unreserve(kg_engine* e, int64_t first, int64_t count, const uint8_t* mask);
+/* The scheduler clock isNodeMetricExpired reads (loadaware/helper.go:36-41, time.Since on every Filter/Score):
+ * now_unix_nano > 0 fixes it; 0 = the host's real-time clock, read at every schedule / evaluate call; < 0 (the
+ * default) = the newest now passed to kg_node_metrics_update.  Nodes whose metric expires or revives between calls
+ * are re-flagged before the next call evaluates them. */
+int kg_engine_set_clock(kg_engine* e, int64_t now_unix_nano);
 
 /* Schedules `n` pods in FIFO order. out_node_idx[i] = chosen node (-1 = unschedulable), out_score[i] = the
  * weighted total score of that node. Each placement is assumed before the next pod is evaluated. */

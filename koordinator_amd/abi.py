@@ -158,7 +158,7 @@ EXPORTED_SYMBOLS = (
     "kg_nodes_device_upsert", "kg_nodes_read_device", "kg_results_fetch_devices", "kg_pods_evaluate_device",
     "kg_quotas_set", "kg_quotas_read", "kg_nodes_reservation_upsert", "kg_nodes_read_reservations",
     "kg_results_fetch_reservations", "kg_profile_enable", "kg_profile_read", "kg_loopback_create",
-    "kg_loopback_destroy", "kg_engine_create_loopback",
+    "kg_loopback_destroy", "kg_engine_create_loopback", "kg_pods_unreserve", "kg_engine_set_clock",
 )
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
@@ -228,6 +228,8 @@ def load_library(path: str | None = None):
         "kg_loopback_create": (i, [i, ctypes.POINTER(vp)]),
         "kg_loopback_destroy": (None, [vp]),
         "kg_engine_create_loopback": (i, [vp, i64, i, i, vp, ctypes.POINTER(vp)]),
+        "kg_pods_unreserve": (i, [vp, i64, i64, vp]),
+        "kg_engine_set_clock": (i, [vp, i64]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)

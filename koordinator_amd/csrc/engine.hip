@@ -1018,7 +1018,8 @@ __global__ __launch_bounds__(kWave) void resolve_round_numa(DevTable T, NumaTabl
                                                              int64_t* __restrict__ ctl, int64_t first, int nb,
                                                              const uint64_t* __restrict__ cand, EvalParams P,
                                                              NumaParams NP, uint64_t* __restrict__ out_keys,
-                                                             uint64_t* __restrict__ out_cpus, int bitmap_words,
+                                                             uint64_t* __restrict__ out_cpus,
+                                                             int64_t* __restrict__ out_nrec, int bitmap_words,
                                                              int32_t* __restrict__ poison, int64_t seq,
                                                              QuotaRow* __restrict__ quotas, int nq) {
   extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
@@ -1106,9 +1107,10 @@ __global__ __launch_bounds__(kWave) void resolve_round_numa(DevTable T, NumaTabl
       NumaHint aff{0, 1, 0, 0};
       if (NP.filter) (void)numa_filter(mv, np, NP, aff);
       CpuSet cpus;
+      NumaAlloc rec;
       const NumaStatic ns = s_ns[lane];
       NumaMut nm = s_nm[lane];
-      if (numa_reserve(ns, nm, mv, np, aff, cpus)) {
+      if (numa_reserve(ns, nm, mv, np, aff, cpus, rec)) {
         placed = 1;
         s_nm[lane] = nm;
         mv = make_view(&s_ns[lane], &s_nm[lane], NP);
@@ -1126,6 +1128,13 @@ __global__ __launch_bounds__(kWave) void resolve_round_numa(DevTable T, NumaTabl
         touched = true;
 #pragma unroll
         for (int q = 0; q < kCpuWords; ++q) out_cpus[(size_t)(first + j) * kCpuWords + q] = cpus.w[q];
+        int64_t* r = out_nrec + (size_t)(first + j) * kNumaRecWords;
+        r[0] = rec.res;
+#pragma unroll
+        for (int i = 0; i < kNumaMax; ++i) {
+          r[1 + i] = ((rec.res >> i) & 1u) ? rec.cpu[i] : 0;
+          r[1 + kNumaMax + i] = ((rec.res >> i) & 1u) ? rec.mem[i] : 0;
+        }
       }
     }
     placed = __builtin_amdgcn_readlane(placed, owner);
@@ -1624,6 +1633,81 @@ struct RowDelta {
   int64_t idx;
   int64_t d[9];  // req_cpu, req_mem, nz_cpu, nz_mem, num_pods, la_used_cpu, la_used_mem, la_pused_cpu, la_pused_mem
 };
+// The framework's Unreserve of placed staged pods idx[0..n) (kg_pods_unreserve), one thread in queue order: NodeInfo
+// + the LoadAware assign cache, NodeNUMAResource Release, DeviceShare updateCacheUsed(add=false), Reservation
+// forgetPod, ElasticQuota UnreservePod.  Each pod's decision is cleared, so a second Unreserve is a no-op.
+__global__ void unreserve_pods(DevTable T, const DevPod* __restrict__ pods, const int64_t* __restrict__ idx, int64_t n,
+                               uint64_t* __restrict__ out_keys, NumaMut* __restrict__ nm, uint64_t* __restrict__ out_cpus,
+                               int64_t* __restrict__ out_nrec, DsNode* __restrict__ ds, const DsPod* __restrict__ dpods,
+                               int32_t* __restrict__ out_minors, RsvNode* __restrict__ RN, int32_t* __restrict__ out_rslot,
+                               QuotaRow* __restrict__ quotas, int nq, const int64_t* __restrict__ qdev) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  for (int64_t k = 0; k < n; ++k) {
+    const int64_t j = idx[k];
+    const uint64_t key = out_keys[j];
+    if (key == 0) continue;
+    const uint32_t w = key_node(key);
+    const DevPod p = pods[j];
+    Row r = load_row(T, w);  // NodeInfo.RemovePod + podAssignCache.unAssign (pod_assign_cache.go:119-131)
+    const int64_t prod = (p.flags & P_PROD) ? 1 : 0;
+    r.req_cpu -= p.req_cpu;
+    r.req_mem -= p.req_mem;
+    r.nz_cpu -= p.nz_cpu;
+    r.nz_mem -= p.nz_mem;
+    r.la_used_cpu -= p.est_cpu;
+    r.la_used_mem -= p.est_mem;
+    r.la_pused_cpu -= prod * p.est_cpu;
+    r.la_pused_mem -= prod * p.est_mem;
+    r.num_pods -= 1;
+    store_mutable(T, w, r);
+    if (nm) {  // nodenumaresource/plugin.go:417-425
+      uint64_t* c = out_cpus + (size_t)j * kCpuWords;
+      int64_t* rec = out_nrec + (size_t)j * kNumaRecWords;
+      NumaMut m = nm[w];
+      numa_release(m, c, rec);
+      nm[w] = m;
+      for (int q = 0; q < kCpuWords; ++q) c[q] = 0;
+      for (int q = 0; q < kNumaRecWords; ++q) rec[q] = 0;
+    }
+    if (ds && out_minors[j]) {  // deviceshare/plugin.go:440-455, SubtractWithNonNegativeResult per minor
+      const DsPod dp = dpods[j];
+      DsNode dn = ds[w];
+      if (!dp.skip && !dp.error && dn.has_device) {
+        const DsInst in = ds_instance(dn, dp);
+        for (int m = 0; m < kMinors; ++m) {
+          if (!((out_minors[j] >> m) & 1)) continue;
+          const int64_t c = dn.ucore[m] - in.core, q = dn.uratio[m] - in.ratio, b = dn.umem[m] - in.mem;
+          dn.ucore[m] = (int32_t)(c > 0 ? c : 0);
+          dn.uratio[m] = (int32_t)(q > 0 ? q : 0);
+          dn.umem[m] = b > 0 ? b : 0;
+        }
+        ds[w] = dn;
+      }
+      out_minors[j] = 0;
+    }
+    if (RN && out_rslot[j] >= 0) {  // reservation/plugin.go:561-583 → RemoveAssignedPod (reservation_info.go:328-339)
+      const int s = out_rslot[j];
+      RsvNode& rn = RN[w];
+      if (rn.assigned[s] > 0) {
+        if (rn.alloc_cpu[s] > 0) rn.allocd_cpu[s] = rn.allocd_cpu[s] > p.req_cpu ? rn.allocd_cpu[s] - p.req_cpu : 0;
+        if (rn.alloc_mem[s] > 0) rn.allocd_mem[s] = rn.allocd_mem[s] > p.req_mem ? rn.allocd_mem[s] - p.req_mem : 0;
+        rn.assigned[s] -= 1;
+      }
+      out_rslot[j] = -1;
+    }
+    if (nq > 0 && p.quota >= 0) {  // elasticquota/plugin.go:348-360 → UnreservePod (addUsedNonNegativeNoLock)
+      const QuotaReq rq = quota_req(p, qdev ? qdev + (size_t)j * kQuotaRes : nullptr);
+      QuotaRow& Q = quotas[p.quota];
+      const bool np = (p.flags & P_NONPREEMPT) != 0;
+      for (int d = 0; d < kQuotaRes; ++d) {
+        Q.used[d] = Q.used[d] > rq.r[d] ? Q.used[d] - rq.r[d] : 0;
+        if (np) Q.np[d] = Q.np[d] > rq.r[d] ? Q.np[d] - rq.r[d] : 0;
+      }
+    }
+    out_keys[j] = 0;
+  }
+}
+
 __global__ void apply_deltas(DevTable T, const RowDelta* __restrict__ d, int64_t n) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -1776,6 +1860,11 @@ struct kg_engine {
   std::vector<int64_t> folded_usage;  // NodeUsage currently folded into la_used (2 per node)
   std::vector<int64_t> now_of;        // metric ingest time per node
   bool static_dirty = true;
+  // scheduler clock for isNodeMetricExpired (kg_engine_set_clock): 0 = the newest now given to
+  // kg_node_metrics_update, 1 = fixed, 2 = the host's real-time clock at every call
+  int clock_mode = 0;
+  int64_t clock_fixed = 0, clock_metrics = 0, clock_now = 0;
+  DevBuf<int64_t> uidx;  // kg_pods_unreserve: staged pod indices
   // device
   DevTable T{};
   DevBuf<int64_t> cols64;
@@ -1806,6 +1895,7 @@ struct kg_engine {
   DevBuf<NumaMut> numa_m;
   DevBuf<NumaPod> npods;
   DevBuf<uint64_t> out_cpus;  // [staged + kMaxB][4]
+  DevBuf<int64_t> out_nrec;   // [staged + kMaxB][kNumaRecWords]: each pod's NUMA allocation (for Unreserve)
   // DeviceShare (profile enables it): per-node GPU state, per-pod preFilterState, Reserve's minors, round scratch
   bool ds_on = false;
   DsParams DP{};
@@ -2217,7 +2307,7 @@ uint32_t node_flags(const kg_engine* e, int64_t i) {
   const kg_node& n = e->nodes[i];
   if (!(n.flags & KG_NODE_VALID)) return 0;
   const kg_node_metric& m = e->metrics[i];
-  const int64_t now = e->now_of[i];
+  const int64_t now = e->clock_now;  // isNodeMetricExpired: time.Since(updateTime) at this scheduling call
   uint32_t f = F_VALID;
   const kg_config& c = e->cfg;
   if (m.present && !(c.la_node_metric_expiration_seconds >= 0 && metric_expired(m, c.la_node_metric_expiration_seconds, now)))
@@ -2227,7 +2317,31 @@ uint32_t node_flags(const kg_engine* e, int64_t i) {
   return f;
 }
 
+int64_t clock_read(const kg_engine* e) {
+  if (e->clock_mode == 1) return e->clock_fixed;
+  if (e->clock_mode == 2)
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::system_clock::now().time_since_epoch()).count();
+  return e->clock_metrics;
+}
+
+// Moves the scheduler clock to this call's now: the static flags are rebuilt only when some node's
+// isNodeMetricExpired verdict (loadaware/helper.go:36-41) differs between the old and the new now.
+void clock_refresh(kg_engine* e) {
+  const int64_t now = clock_read(e);
+  if (now == e->clock_now) return;
+  const int64_t exp_s = e->cfg.la_node_metric_expiration_seconds;
+  bool flip = false;
+  for (int64_t i = 0; i < e->n_nodes && !flip && exp_s > 0; ++i) {
+    const kg_node_metric& m = e->metrics[i];
+    if (m.present && m.has_update_time)
+      flip = metric_expired(m, exp_s, now) != metric_expired(m, exp_s, e->clock_now);
+  }
+  e->clock_now = now;
+  if (flip) e->static_dirty = true;
+}
+
 int sync_static(kg_engine* e) {
+  clock_refresh(e);
   if (!e->static_dirty) return 0;
   const int64_t cap = e->capacity;
   auto& h64 = e->h_static64;
@@ -2384,6 +2498,7 @@ void launch_resolve(kg_engine* e, const RoundGeom& g, int64_t first, int nb, int
     resolve_round_numa<<<1, kWave, resolve_numa_lds_bytes(g, nb), st>>>(e->T, numa_table(e), e->pods.p, e->npods.p,
                                                                         e->cursor.p, first, nb, cand_slot(e, g, slot),
                                                                         e->P, e->NP, e->out_keys.p, e->out_cpus.p,
+                                                                        e->out_nrec.p,
                                                                         g.bitmap_words, poison_ptr(e), seq, e->quotas.p,
                                                                         e->nq);
     return;
@@ -3017,6 +3132,7 @@ void kg_engine_destroy(kg_engine* e) {
   e->numa_m.release();
   e->npods.release();
   e->out_cpus.release();
+  e->out_nrec.release();
   e->ds_d.release();
   e->quotas.release();
   e->qdev.release();
@@ -3035,6 +3151,7 @@ void kg_engine_destroy(kg_engine* e) {
   e->rsv_part.release();
   e->scratch64.release();
   e->scratch32.release();
+  e->uidx.release();
   if (e->stream) (void)hipStreamDestroy(e->stream);
   delete e;
 }
@@ -3090,6 +3207,7 @@ int kg_node_metrics_update(kg_engine* e, const kg_node_metric* m, const int32_t*
     e->folded_usage[2 * i + 1] = u[1];
     e->metrics[i] = m[k];
     e->now_of[i] = now;
+    e->clock_metrics = std::max(e->clock_metrics, now);
     if (x.d[5] || x.d[6]) d.push_back(x);
   }
   e->static_dirty = true;
@@ -3127,6 +3245,32 @@ int kg_pods_remove(kg_engine* e, const kg_pod* pods, const int32_t* node_idx, in
   return pods_delta(e, pods, node_idx, n, -1);
 }
 
+int kg_pods_unreserve(kg_engine* e, int64_t first, int64_t count, const uint8_t* mask) {
+  if (!e) return fail(KG_E_INVALID, "engine is NULL");
+  if (first < 0 || count < 0 || first + count > e->n_staged) return fail(KG_E_INVALID, "staged range");
+  std::vector<int64_t> idx;
+  for (int64_t k = 0; k < count; ++k)
+    if (!mask || mask[k]) idx.push_back(first + k);
+  if (idx.empty()) return 0;
+  if (int rc = e->uidx.ensure(idx.size())) return rc;
+  HIP_TRY(hipMemcpyAsync(e->uidx.p, idx.data(), idx.size() * 8, hipMemcpyHostToDevice, e->stream));
+  unreserve_pods<<<1, 1, 0, e->stream>>>(e->T, e->pods.p, e->uidx.p, (int64_t)idx.size(), e->out_keys.p,
+                                        e->numa_on ? e->numa_m.p : nullptr, e->out_cpus.p, e->out_nrec.p,
+                                        e->ds_on ? e->ds_d.p : nullptr, e->dpods.p, e->out_minors.p,
+                                        e->rsv_on ? e->rsv_d.p : nullptr, e->out_rslot.p, e->quotas.p, e->nq,
+                                        (e->ds_on || e->rsv_on) ? e->qdev.p : nullptr);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  return 0;
+}
+
+int kg_engine_set_clock(kg_engine* e, int64_t now_unix_nano) {
+  if (!e) return fail(KG_E_INVALID, "engine is NULL");
+  e->clock_mode = now_unix_nano > 0 ? 1 : now_unix_nano == 0 ? 2 : 0;
+  e->clock_fixed = now_unix_nano > 0 ? now_unix_nano : 0;
+  return 0;
+}
+
 int kg_pods_stage(kg_engine* e, const kg_pod* pods, int64_t n) {
   if (!e || (n > 0 && !pods)) return fail(KG_E_INVALID, "null argument");
   for (int64_t k = 0; k < n; ++k) {
@@ -3157,6 +3301,8 @@ int kg_pods_stage(kg_engine* e, const kg_pod* pods, int64_t n) {
     if (int rc = e->out_cpus.ensure((n + kMaxB) * kCpuWords)) return rc;
     if (n > 0) HIP_TRY(hipMemcpyAsync(e->npods.p, hn.data(), n * sizeof(NumaPod), hipMemcpyHostToDevice, e->stream));
     HIP_TRY(hipMemsetAsync(e->out_cpus.p, 0, (n + kMaxB) * kCpuWords * 8, e->stream));
+    if (int rc = e->out_nrec.ensure((n + kMaxB) * kNumaRecWords)) return rc;
+    HIP_TRY(hipMemsetAsync(e->out_nrec.p, 0, (n + kMaxB) * kNumaRecWords * 8, e->stream));
   }
   std::vector<DsPod> hd;
   if (e->ds_on) {

@@ -878,8 +878,9 @@ __device__ __forceinline__ bool numa_eval(const NumaView& v, const NumaPod& p, c
 // NodeNUMAResource.Reserve (plugin.go:375-415) → Allocate with the exact cpuset (cpu accumulator) →
 // addPodAllocation (node_allocation.go:76-103).  False: the allocation fails and the pod is not placed.
 __device__ __noinline__ bool numa_reserve(const NumaStatic& s, NumaMut& m, const NumaView& v, const NumaPod& p,
-                                    const NumaHint& aff, CpuSet& cpus) {
+                                    const NumaHint& aff, CpuSet& cpus, NumaAlloc& rec) {
   cpus = cs_zero();
+  rec.res = 0;  // the PodAllocation's NUMANodeResources, kept for Release (node_allocation.go:105-131)
   if (skip_the_node(p, v.policy)) return true;
   if (p.cpu_bind && !v.valid) return false;
   NumaAlloc a;
@@ -916,7 +917,25 @@ __device__ __noinline__ bool numa_reserve(const NumaStatic& s, NumaMut& m, const
       m.alloc_cpu[i] += a.cpu[i];
       m.alloc_mem[i] += a.mem[i];
     }
+  rec = a;
   return true;
+}
+
+// per-pod NUMA allocation record (kg_pods_unreserve): [0] NUMA-node mask, [1 + i] cpu, [1 + kNumaMax + i] memory
+constexpr int kNumaRecWords = 1 + 2 * kNumaMax;
+
+// resourceManager.Release → NodeAllocation.release (node_allocation.go:105-131): the pod's cpus leave the
+// allocated set (maxRefCount 1), its NUMANodeResources are subtracted with a non-negative result
+__device__ __forceinline__ void numa_release(NumaMut& m, const uint64_t* cpus, const int64_t* rec) {
+#pragma unroll
+  for (int w = 0; w < kCpuWords; ++w) m.allocated[w] &= ~cpus[w];
+#pragma unroll
+  for (int i = 0; i < kNumaMax; ++i)
+    if ((rec[0] >> i) & 1) {
+      const int64_t c = m.alloc_cpu[i] - rec[1 + i], mm = m.alloc_mem[i] - rec[1 + kNumaMax + i];
+      m.alloc_cpu[i] = c > 0 ? c : 0;
+      m.alloc_mem[i] = mm > 0 ? mm : 0;
+    }
 }
 
 }  // namespace kg

@@ -308,9 +308,9 @@ __device__ __forceinline__ bool rsv_reserve(const DevTable& T, RsvNode* __restri
   r.num_pods += 1;
   store_mutable(T, w, r);
   const int32_t slot = (int32_t)(v & 7) - 1;
-  if (slot >= 0) {
-    RN[w].allocd_cpu[slot] += p.req_cpu;
-    RN[w].allocd_mem[slot] += p.req_mem;
+  if (slot >= 0) {  // Allocated += quotav1.Mask(requests, ResourceNames): only the reservation's keys (0 = absent)
+    if (RN[w].alloc_cpu[slot] > 0) RN[w].allocd_cpu[slot] += p.req_cpu;
+    if (RN[w].alloc_mem[slot] > 0) RN[w].allocd_mem[slot] += p.req_mem;
     RN[w].assigned[slot] += 1;
   }
   slot_out = slot;

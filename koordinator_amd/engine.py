@@ -117,6 +117,17 @@ class Engine:
         node_idx = np.ascontiguousarray(node_idx, dtype=np.int32)
         check(self.lib, self.lib.kg_pods_remove(self.h, ptr(pods), ptr(node_idx), len(pods)))
 
+    def unreserve(self, first: int, count: int, mask=None):
+        """kg_pods_unreserve: the framework's Unreserve of staged pods [first, first+count) (mask selects them)."""
+        m = None if mask is None else np.ascontiguousarray(mask, dtype=np.uint8)
+        if m is not None and len(m) != count:
+            raise ValueError("mask length != count")
+        check(self.lib, self.lib.kg_pods_unreserve(self.h, int(first), int(count), ptr(m)))
+
+    def set_clock(self, now_ns: int):
+        """kg_engine_set_clock: > 0 fixed, 0 real time, < 0 the newest metrics update time."""
+        check(self.lib, self.lib.kg_engine_set_clock(self.h, int(now_ns)))
+
     def upsert_numa(self, node_numa: np.ndarray, idx=None):
         """NodeNUMAResource state (TopologyOptions + NodeAllocation) of nodes `idx` (kg_nodes_numa_upsert)."""
         node_numa = np.ascontiguousarray(node_numa, dtype=abi.NODE_NUMA_DTYPE)

@@ -200,6 +200,18 @@ int32_t or_ds_reserve(kg_node_device* d, const or_ds_pod* p, int strategy, const
   return mask;
 }
 
+void or_ds_release(kg_node_device* d, const or_ds_pod* p, int32_t minors) {
+  if (p->skip || !d->has_device || p->error) return;
+  const or_ds_inst in = or_ds_instance(d, p); /* the per-instance request Reserve added (node totals only) */
+  for (int m = 0; m < KG_MAX_MINORS; m++) {
+    if (!(minors >> m & 1)) continue;
+    /* updateDeviceUsed(add=false): quotav1.SubtractWithNonNegativeResult(used, allocation.Resources) */
+    d->used_core[m] = d->used_core[m] - in.core > 0 ? d->used_core[m] - in.core : 0;
+    d->used_memory[m] = d->used_memory[m] - in.mem > 0 ? d->used_memory[m] - in.mem : 0;
+    d->used_ratio[m] = d->used_ratio[m] - in.ratio > 0 ? d->used_ratio[m] - in.ratio : 0;
+  }
+}
+
 void or_default_normalize(int64_t* s, int64_t n) {
   int64_t mx = 0;
   for (int64_t i = 0; i < n; i++)

@@ -44,6 +44,8 @@ int or_ds_pod_init(const kg_pod* pod, or_ds_pod* out);
 int64_t or_ds_memory_bytes_to_ratio(int64_t bytes, int64_t total_memory);
 int64_t or_ds_memory_ratio_to_bytes(int64_t ratio, int64_t total_memory);
 or_ds_inst or_ds_instance(const kg_node_device* d, const or_ds_pod* p);
+/* Unreserve (plugin.go:440-455): each minor of `minors` gives the pod's per-instance request back */
+void or_ds_release(kg_node_device* d, const or_ds_pod* p, int32_t minors);
 /* Filter: 1 pass, 0 reject.  A node without a Device object rejects device pods (NodeResourcesFit on the device
  * extended resources, whose allocatable is then 0). */
 int or_ds_filter(const kg_node_device* d, const or_ds_pod* p);

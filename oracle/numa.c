@@ -920,8 +920,9 @@ int64_t or_numa_score(const kg_config* cfg, const or_numa_node* n, const or_numa
 }
 
 int or_numa_reserve(const kg_config* cfg, or_numa_node* n, const or_numa_pod* p, const or_hint* affinity,
-                    or_cpuset* cpus) {
+                    or_cpuset* cpus, int64_t* alloc) {
   *cpus = cs_empty();
+  if (alloc) memset(alloc, 0, sizeof(int64_t) * OR_NUMA_ALLOC_WORDS);
   if (skip_the_node(p, n->numa_policy)) return 0;
   if (p->request_cpu_bind && (!n->has_topology || !n->valid_topology)) return -1;
   numa_alloc res;
@@ -933,8 +934,25 @@ int or_numa_reserve(const kg_config* cfg, or_numa_node* n, const or_numa_pod* p,
     n->numa_alloc_cpu[i] += res.cpu[k];
     n->numa_alloc_mem[i] += res.mem[k];
     n->numa_alloc_present[i] = 1;
+    if (alloc) { /* the PodAllocation's NUMANodeResources, kept for Release */
+      alloc[0] |= (int64_t)1 << i;
+      alloc[1 + i] += res.cpu[k];
+      alloc[1 + KG_MAX_NUMA + i] += res.mem[k];
+    }
   }
   return 0;
+}
+
+/* resourceManager.Release → NodeAllocation.release (node_allocation.go:105-131): the pod's cpus leave the
+ * allocated set (maxRefCount 1) and its NUMANodeResources are subtracted (SubtractWithNonNegativeResult). */
+void or_numa_release(or_numa_node* n, const or_cpuset* cpus, const int64_t* alloc) {
+  for (int w = 0; w < OR_CPUSET_WORDS; w++) n->allocated.w[w] &= ~cpus->w[w];
+  for (int i = 0; i < KG_MAX_NUMA; i++) {
+    if (!((alloc[0] >> i) & 1)) continue;
+    n->numa_alloc_cpu[i] = n->numa_alloc_cpu[i] - alloc[1 + i] > 0 ? n->numa_alloc_cpu[i] - alloc[1 + i] : 0;
+    const int64_t m = alloc[1 + KG_MAX_NUMA + i];
+    n->numa_alloc_mem[i] = n->numa_alloc_mem[i] - m > 0 ? n->numa_alloc_mem[i] - m : 0;
+  }
 }
 
 /* ---------------------------------------------------------------------------------------------------- */
@@ -992,7 +1010,7 @@ int or_numa_reserve_flat(const kg_config* cfg, const kg_node_numa* node, const k
   or_hint h;
   or_numa_filter(cfg, &n, &p, &h);
   or_cpuset cs;
-  const int rc = or_numa_reserve(cfg, &n, &p, &h, &cs);
+  const int rc = or_numa_reserve(cfg, &n, &p, &h, &cs, NULL);
   for (int w = 0; w < OR_CPUSET_WORDS; w++) cpuset[w] = cs.w[w];
   return rc;
 }

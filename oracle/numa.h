@@ -72,8 +72,11 @@ int64_t or_numa_score(const kg_config* cfg, const or_numa_node* n, const or_numa
                       int64_t node_req_cpu, int64_t node_req_mem, int64_t node_alloc_cpu, int64_t node_alloc_mem);
 /* Reserve (plugin.go:375-415): Allocate with the stored affinity, then Update.  Returns 0 (and the cpuset in
  * *cpus) or -1 when the allocation fails (the pod is not placed). */
+/* the per-pod NUMA allocation record: [0] NUMA-node bitmask, [1 + i] cpu and [1 + KG_MAX_NUMA + i] memory on NUMA i */
+#define OR_NUMA_ALLOC_WORDS (1 + 2 * KG_MAX_NUMA)
 int or_numa_reserve(const kg_config* cfg, or_numa_node* n, const or_numa_pod* p, const or_hint* affinity,
-                    or_cpuset* cpus);
+                    or_cpuset* cpus, int64_t* alloc);
+void or_numa_release(or_numa_node* n, const or_cpuset* cpus, const int64_t* alloc);
 
 #ifdef __cplusplus
 }

@@ -9,6 +9,7 @@
 #include "oracle.h"
 #include "numa.h"
 #include "deviceshare.h"
+#include "reservation.h"
 
 #include <math.h>
 #include <pthread.h>
@@ -366,7 +367,7 @@ int or_schedule_numa(const kg_config* cfg, int64_t n_nodes, const kg_node* nodes
                      or_node_state* st, void* numa_states, int64_t n_pods, const kg_pod* pods, int64_t now,
                      int n_threads, int32_t* out_node, int64_t* out_score, uint64_t* out_cpus) {
   return or_schedule_full(cfg, n_nodes, nodes, metrics, st, numa_states, NULL, NULL, 0, n_pods, pods, now, n_threads,
-                          out_node, out_score, out_cpus, NULL);
+                          out_node, out_score, out_cpus, NULL, NULL);
 }
 
 /* The pod's quota request over the KG_QUOTA_RES resources (PodRequestsAndLimits: cpu, memory, the device
@@ -410,10 +411,41 @@ void or_quota_charge(kg_quota* q, const kg_pod* p) {
   }
 }
 
+int or_unreserve(const kg_config* cfg, or_node_state* st, void* numa_states, kg_node_device* dev,
+                 kg_node_reservations* rsv, kg_quota* quotas, int64_t n_quotas, const kg_pod* pod, int32_t node,
+                 const uint64_t* cpus, const int64_t* numa_alloc, int32_t minors, int32_t slot) {
+  if (node < 0) return 0;
+  if (pod->quota_id > n_quotas) return KG_E_INVALID;
+  or_apply_pod(cfg, &st[node], pod, -1); /* NodeInfo.RemovePod + podAssignCache.unAssign */
+  if (numa_states && (cfg->numa_filter || cfg->numa_score) && cpus && numa_alloc) {
+    or_cpuset cs;
+    for (int w = 0; w < OR_CPUSET_WORDS; w++) cs.w[w] = cpus[w];
+    or_numa_release(&((or_numa_node*)numa_states)[node], &cs, numa_alloc); /* nodenumaresource/plugin.go:417-425 */
+  }
+  if (dev && (cfg->ds_filter || cfg->ds_score) && minors) { /* deviceshare/plugin.go:440-455 */
+    or_ds_pod dsp;
+    if (or_ds_pod_init(pod, &dsp) != 0) return KG_E_INVALID;
+    or_ds_release(&dev[node], &dsp, minors);
+  }
+  if (rsv && slot >= 0) or_rsv_forget(&rsv[node], slot, pod); /* reservation/plugin.go:561-583 */
+  if (quotas && pod->quota_id > 0) { /* elasticquota/plugin.go:348-360 → UnreservePod (addUsedNonNegativeNoLock) */
+    kg_quota* q = &quotas[pod->quota_id - 1];
+    int64_t req[KG_QUOTA_RES];
+    int key[KG_QUOTA_RES];
+    quota_request(pod, req, key);
+    for (int d = 0; d < KG_QUOTA_RES; d++) {
+      q->used[d] = q->used[d] - req[d] > 0 ? q->used[d] - req[d] : 0;
+      if (pod->flags & KG_POD_NON_PREEMPTIBLE)
+        q->non_preemptible_used[d] = q->non_preemptible_used[d] - req[d] > 0 ? q->non_preemptible_used[d] - req[d] : 0;
+    }
+  }
+  return 0;
+}
+
 int or_schedule_full(const kg_config* cfg, int64_t n_nodes, const kg_node* nodes, const kg_node_metric* metrics,
                      or_node_state* st, void* numa_states, kg_node_device* dev, kg_quota* quotas, int64_t n_quotas,
                      int64_t n_pods, const kg_pod* pods, int64_t now, int n_threads, int32_t* out_node,
-                     int64_t* out_score, uint64_t* out_cpus, int32_t* out_minors) {
+                     int64_t* out_score, uint64_t* out_cpus, int32_t* out_minors, int64_t* out_numa) {
   or_numa_node* numa = (or_numa_node*)numa_states;
   sched_ctx c;
   memset(&c, 0, sizeof(c));
@@ -452,6 +484,7 @@ int or_schedule_full(const kg_config* cfg, int64_t n_nodes, const kg_node* nodes
         if (out_minors) out_minors[p] = 0;
         if (out_cpus)
           for (int w = 0; w < OR_CPUSET_WORDS; w++) out_cpus[p * OR_CPUSET_WORDS + w] = 0;
+        if (out_numa) memset(&out_numa[p * OR_NUMA_ALLOC_WORDS], 0, sizeof(int64_t) * OR_NUMA_ALLOC_WORDS);
         continue;
       }
     }
@@ -483,9 +516,11 @@ int or_schedule_full(const kg_config* cfg, int64_t n_nodes, const kg_node* nodes
      * (RunReservePluginsUnreserve + ForgetPod): it is not placed this cycle */
     or_cpuset cpus;
     memset(&cpus, 0, sizeof(cpus));
+    int64_t nalloc[OR_NUMA_ALLOC_WORDS] = {0};
     if (best >= 0 && c.numa) {
-      if (or_numa_reserve(cfg, &c.numa[best], &c.numa_pod, &c.affinity[best], &cpus) != 0) best = -1;
+      if (or_numa_reserve(cfg, &c.numa[best], &c.numa_pod, &c.affinity[best], &cpus, nalloc) != 0) best = -1;
     }
+    if (out_numa) memcpy(&out_numa[p * OR_NUMA_ALLOC_WORDS], nalloc, sizeof(nalloc));
     int32_t minors = 0;
     if (best >= 0 && c.dev) {
       minors = or_ds_reserve(&c.dev[best], &c.ds_pod, (int)cfg->ds_scoring_strategy, cfg->ds_scoring_weights);

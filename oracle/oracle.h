@@ -81,7 +81,16 @@ int or_schedule_numa(const kg_config* cfg, int64_t n_nodes, const kg_node* nodes
 int or_schedule_full(const kg_config* cfg, int64_t n_nodes, const kg_node* nodes, const kg_node_metric* metrics,
                      or_node_state* st, void* numa, kg_node_device* dev, kg_quota* quotas, int64_t n_quotas,
                      int64_t n_pods, const kg_pod* pods, int64_t now_unix_nano, int n_threads, int32_t* out_node,
-                     int64_t* out_score, uint64_t* out_cpus, int32_t* out_minors);
+                     int64_t* out_score, uint64_t* out_cpus, int32_t* out_minors, int64_t* out_numa);
+
+/* The framework's Unreserve of one pod Reserve placed on `node` (RunReservePluginsUnreserve: every enabled plugin
+ * in turn; each state pointer may be NULL when its plugin is off): NodeInfo.RemovePod + the LoadAware assign cache,
+ * NodeNUMAResource Release of its cpuset / NUMA resources (`cpus`, `numa_alloc` = the OR_NUMA_ALLOC_WORDS record
+ * Reserve produced), DeviceShare updateCacheUsed(add=false) on the `minors` it allocated, Reservation
+ * forgetPod from reservation `slot` (-1 none) and ElasticQuota UnreservePod. */
+int or_unreserve(const kg_config* cfg, or_node_state* st, void* numa, kg_node_device* dev, kg_node_reservations* rsv,
+                 kg_quota* quotas, int64_t n_quotas, const kg_pod* pod, int32_t node, const uint64_t* cpus,
+                 const int64_t* numa_alloc, int32_t minors, int32_t slot);
 
 /* Builds node states from pre-existing assigned pods (informer adds). */
 void or_states_init(int64_t n_nodes, or_node_state* st);

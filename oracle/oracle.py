@@ -70,7 +70,9 @@ def lib():
         L.or_numa_eval_flat.restype = i
         L.or_numa_reserve_flat.argtypes = [vp, vp, vp, vp]
         L.or_numa_reserve_flat.restype = i
-        L.or_schedule_full.argtypes = [vp, i64, vp, vp, vp, vp, vp, vp, i64, i64, vp, i64, i, vp, vp, vp, vp]
+        L.or_schedule_full.argtypes = [vp, i64, vp, vp, vp, vp, vp, vp, i64, i64, vp, i64, i, vp, vp, vp, vp, vp]
+        L.or_unreserve.argtypes = [vp, vp, vp, vp, vp, vp, i64, vp, i, vp, vp, i, i]
+        L.or_unreserve.restype = i
         L.or_schedule_full.restype = i
         L.or_ds_pod_init.argtypes = [vp, vp]
         L.or_ds_pod_init.restype = i
@@ -131,21 +133,41 @@ def ds_reserve(cfg, dev, pod) -> int:
     return int(lib().or_ds_reserve(p(dev), p(ds_pod(pod)), int(cfg["ds_scoring_strategy"]), p(w)))
 
 
+NUMA_ALLOC_WORDS = 1 + 2 * abi.MAX_NUMA  # per-pod NUMA allocation record (oracle/numa.h OR_NUMA_ALLOC_WORDS)
+
+
 def schedule_full(cfg, nodes, metrics, st, pods, now_ns: int, n_threads: int = 1, numa_buf=None, devices=None,
-                  quotas=None):
+                  quotas=None, with_numa_alloc: bool = False):
     """Sequential FIFO scheduling with the optional NodeNUMAResource / DeviceShare states and ElasticQuota table
-    (all mutated).  Returns (node, score, cpusets uint64[n, 4], GPU minor masks int32[n])."""
+    (all mutated).  Returns (node, score, cpusets uint64[n, 4], GPU minor masks int32[n]) and, with_numa_alloc,
+    each pod's NUMA allocation record int64[n, NUMA_ALLOC_WORDS]."""
     pods = np.ascontiguousarray(pods, dtype=abi.POD_DTYPE)
     out_node = np.empty(len(pods), dtype=np.int32)
     out_score = np.empty(len(pods), dtype=np.int64)
     cpus = np.zeros((max(len(pods), 1), abi.MAX_CPUS // 64), dtype=np.uint64)
     minors = np.zeros(max(len(pods), 1), dtype=np.int32)
+    nalloc = np.zeros((max(len(pods), 1), NUMA_ALLOC_WORDS), dtype=np.int64)
     nq = 0 if quotas is None else len(quotas)
     rc = lib().or_schedule_full(p(cfg), len(nodes), p(nodes), p(metrics), p(st), p(numa_buf), p(devices), p(quotas), nq,
-                                len(pods), p(pods), now_ns, n_threads, p(out_node), p(out_score), p(cpus), p(minors))
+                                len(pods), p(pods), now_ns, n_threads, p(out_node), p(out_score), p(cpus), p(minors),
+                                p(nalloc))
     if rc != 0:
         raise RuntimeError(f"oracle or_schedule_full failed: {rc}")
-    return out_node, out_score, cpus[:len(pods)], minors[:len(pods)]
+    out = (out_node, out_score, cpus[:len(pods)], minors[:len(pods)])
+    return out + (nalloc[:len(pods)],) if with_numa_alloc else out
+
+
+def unreserve(cfg, st, pod, node: int, numa_buf=None, devices=None, rsv=None, quotas=None, cpus=None,
+              numa_alloc=None, minors: int = 0, slot: int = -1):
+    """The framework's Unreserve of one placed pod (or_unreserve; every state given is mutated)."""
+    pod = np.ascontiguousarray(np.asarray(pod, dtype=abi.POD_DTYPE).reshape(1))
+    cp = None if cpus is None else np.ascontiguousarray(cpus, dtype=np.uint64)
+    na = None if numa_alloc is None else np.ascontiguousarray(numa_alloc, dtype=np.int64)
+    nq = 0 if quotas is None else len(quotas)
+    rc = lib().or_unreserve(p(cfg), p(st), p(numa_buf), p(devices), p(rsv), p(quotas), nq, p(pod), int(node), p(cp),
+                            p(na), int(minors), int(slot))
+    if rc != 0:
+        raise RuntimeError(f"oracle or_unreserve failed: {rc}")
 
 
 p = abi.ptr

@@ -92,6 +92,15 @@ void or_rsv_restore(const kg_node_reservations* r, const or_node_state* st, cons
   }
 }
 
+/* reservationCache.forgetPod → ReservationInfo.RemoveAssignedPod (reservation_info.go:328-339): Allocated −=
+ * Mask(requests, ResourceNames) with a non-negative result, and the pod leaves AssignedPods */
+void or_rsv_forget(kg_node_reservations* r, int s, const kg_pod* pod) {
+  if (s < 0 || s >= (int)r->n || r->assigned[s] <= 0) return;
+  if (r->allocatable_cpu[s] > 0) r->allocated_cpu[s] = sub_nn(r->allocated_cpu[s], pod->requests[KG_RES_CPU]);
+  if (r->allocatable_mem[s] > 0) r->allocated_mem[s] = sub_nn(r->allocated_mem[s], pod->requests[KG_RES_MEMORY]);
+  r->assigned[s] -= 1;
+}
+
 int or_rsv_fits_node(const kg_pod* pod, int64_t allowed_pods, const int64_t alloc[2], const or_rsv_node* ns,
                      const kg_node_reservations* r, int s) {
   if (ns->num_pods - ns->n_matched + 1 > allowed_pods) return 0;
@@ -330,9 +339,11 @@ int or_schedule_resv_full(const kg_config* cfg, int64_t n_nodes, const kg_node* 
       if (rsv_on && nom[win] >= 0) {
         /* Reserve → reservationCache.assumePod → AddAssignedPod (reservation_info.go:317-326) */
         kg_node_reservations* r = &rsv[win];
-        r->allocated_cpu[nom[win]] += pod->requests[KG_RES_CPU];
-        r->allocated_mem[nom[win]] += pod->requests[KG_RES_MEMORY];
-        r->assigned[nom[win]] += 1;
+        const int s = nom[win];
+        /* Allocated += quotav1.Mask(requests, ResourceNames): only the reservation's own keys (0 = absent) */
+        if (r->allocatable_cpu[s] > 0) r->allocated_cpu[s] += pod->requests[KG_RES_CPU];
+        if (r->allocatable_mem[s] > 0) r->allocated_mem[s] += pod->requests[KG_RES_MEMORY];
+        r->assigned[s] += 1;
         if (out_slot) out_slot[p] = nom[win];
       }
       if (quota) or_quota_charge(quota, pod);

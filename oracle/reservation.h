@@ -33,6 +33,7 @@ typedef struct or_rsv_node {
 } or_rsv_node;
 
 /* BeforePreFilter for one node (transformer.go:100-189). */
+void or_rsv_forget(kg_node_reservations* r, int s, const kg_pod* pod);
 void or_rsv_restore(const kg_node_reservations* r, const or_node_state* st, const kg_pod* pod, or_rsv_node* out);
 /* fitsNode (plugin.go:433-482) with rInfo = slot s (s < 0: nil), preemptible = 0. */
 int or_rsv_fits_node(const kg_pod* pod, int64_t allowed_pods, const int64_t alloc[2], const or_rsv_node* ns,

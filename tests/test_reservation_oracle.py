@@ -42,6 +42,7 @@ def test_reserve_bookkeeping_and_affinity():
     got = r["allocated_cpu"] - rsv["allocated_cpu"]
     want = np.zeros_like(got)
     np.add.at(want, (node[slot >= 0], slot[slot >= 0]), pods["requests"][slot >= 0, abi.RES_CPU])
+    want *= rsv["allocatable_cpu"] > 0  # Allocated += Mask(requests, ResourceNames): memory-only keeps cpu absent
     assert np.array_equal(got, want)
     assert np.array_equal(r["assigned"] - rsv["assigned"],
                           np.bincount(node[slot >= 0] * abi.MAX_RSV_SLOTS + slot[slot >= 0],
