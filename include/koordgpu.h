@@ -309,6 +309,9 @@ typedef struct kg_node_numa {
   uint64_t allocated_cpus[KG_MAX_CPUS / 64];   /* NodeAllocation.allocatedCPUs (maxRefCount 1)        */
   int64_t numa_alloc_cpu[KG_MAX_NUMA];         /* NodeAllocation.allocatedResources: cpu (milli)      */
   int64_t numa_alloc_mem[KG_MAX_NUMA];         /*                                   memory (bytes)    */
+  /* node.koordinator.sh/resource-amplification-ratio cpu (extension.Ratio, ≤ 1 = none).  numa_cpu above is the
+   * zone cpu AFTER amplifyNUMANodeResources (util.go:63-84), node allocatable cpu the amplified one. */
+  double cpu_amplification_ratio;
 } kg_node_numa;
 
 typedef struct kg_stats {

@@ -136,7 +136,7 @@ NODE_NUMA_DTYPE = np.dtype([
     _i64("numa_policy"), _i64("node_cpu_bind_policy"), _i64("numa_allocate_strategy"), _i64("num_numa"),
     _i64("numa_cpu", MAX_NUMA), _i64("numa_mem", MAX_NUMA),
     ("reserved_cpus", np.uint64, (MAX_CPUS // 64,)), ("allocated_cpus", np.uint64, (MAX_CPUS // 64,)),
-    _i64("numa_alloc_cpu", MAX_NUMA), _i64("numa_alloc_mem", MAX_NUMA),
+    _i64("numa_alloc_cpu", MAX_NUMA), _i64("numa_alloc_mem", MAX_NUMA), ("cpu_amplification_ratio", np.float64),
 ])
 
 STATS_DTYPE = np.dtype([

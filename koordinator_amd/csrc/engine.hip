@@ -1105,7 +1105,7 @@ __global__ __launch_bounds__(kWave) void resolve_round_numa(DevTable T, NumaTabl
     int placed = 0;
     if (lane == owner) {  // Reserve with the affinity Filter stores (recomputed on the same state)
       NumaHint aff{0, 1, 0, 0};
-      if (NP.filter) (void)numa_filter(mv, np, NP, aff);
+      if (NP.filter) (void)numa_filter(mv, np, NP, aff, mrow.req_cpu, mrow.alloc_cpu);
       CpuSet cpus;
       NumaAlloc rec;
       const NumaStatic ns = s_ns[lane];
@@ -2225,7 +2225,11 @@ int decode_node_numa(const kg_node_numa& n, NumaStatic& s, NumaMut& m) {
     s.numa_mem[i] = i < n.num_numa ? n.numa_mem[i] : 0;
     m.alloc_cpu[i] = i < n.num_numa ? n.numa_alloc_cpu[i] : 0;
     m.alloc_mem[i] = i < n.num_numa ? n.numa_alloc_mem[i] : 0;
+    if (m.alloc_cpu[i] != 0 || m.alloc_mem[i] != 0) m.present |= 1u << i;
   }
+  if (!(n.cpu_amplification_ratio >= 0.0) || n.cpu_amplification_ratio > 1000.0)
+    return fail(KG_E_INVALID, "cpu_amplification_ratio outside [0, 1000]");
+  s.cpu_amp = n.cpu_amplification_ratio;
   for (int w = 0; w < KG_MAX_CPUS / 64; ++w) {
     s.reserved[w] = n.reserved_cpus[w];
     m.allocated[w] = n.allocated_cpus[w];

@@ -21,7 +21,7 @@ namespace kg {
 constexpr int kNumaMax = 4;
 constexpr int kCpuWords = 4;
 
-// static per-node NUMA data (ingest), 136 B
+// static per-node NUMA data (ingest), 144 B
 struct NumaStatic {
   uint64_t reserved[kCpuWords];
   int64_t numa_cpu[kNumaMax], numa_mem[kNumaMax];
@@ -32,15 +32,23 @@ struct NumaStatic {
   int32_t strategy;                // -1 = plugin default, else KG_STRATEGY_*
   int32_t num_numa;
   int32_t pad;
+  double cpu_amp;                  // cpu amplification ratio (≤ 1 = none)
 };
-static_assert(sizeof(NumaStatic) == 136, "NumaStatic layout");
+static_assert(sizeof(NumaStatic) == 144, "NumaStatic layout");
 
 // mutable per-node NUMA state (NodeAllocation)
 struct NumaMut {
   uint64_t allocated[kCpuWords];
   int64_t alloc_cpu[kNumaMax], alloc_mem[kNumaMax];
+  uint32_t present;  // bit i: allocatedResources[i] exists (an allocation ever landed on NUMA node i)
+  uint32_t pad;
 };
-static_assert(sizeof(NumaMut) == 96, "NumaMut layout");
+static_assert(sizeof(NumaMut) == 104, "NumaMut layout");
+
+// extension.Amplify (apis/extension/node_resource_amplification.go:170-175): ceil in float64, as Go
+__device__ __forceinline__ int64_t amplify(int64_t origin, double ratio) {
+  return ratio > 1.0 ? (int64_t)__builtin_ceil((double)origin * ratio) : origin;
+}
 
 // per-pod NodeNUMAResource preFilterState (decoded on the host: plugin.go:220-270)
 struct NumaPod {
@@ -517,6 +525,7 @@ __device__ __forceinline__ CpuSet numa_available_cpus(const Topo& t, const NumaS
 // Every array is indexed only by unrolled compile-time indices, so the view lives in registers.
 // ---------------------------------------------------------------------------------------------------------
 struct NumaView {
+  double amp;  // cpu amplification ratio (≤ 1 = none)
   int32_t valid, policy, node_bind, cpc, nn, strategy, n_alloc;
   int32_t cnt[3][kNumaMax];  // [kind: 0 raw, 1 full cores, 2 one per core][NUMA node]
   int32_t tot[3];
@@ -547,6 +556,7 @@ __device__ __forceinline__ NumaView make_view(const NumaStatic* __restrict__ s, 
   t.nodes = t.sockets * t.nps;
   t.cores = t.nodes * t.cpn;
   t.cpus = t.cores * t.cpc;
+  v.amp = s->cpu_amp;
   v.valid = s->valid;
   v.policy = s->policy;
   v.node_bind = s->node_bind;
@@ -572,10 +582,20 @@ __device__ __forceinline__ NumaView make_view(const NumaStatic* __restrict__ s, 
     v.cnt[2][i] = cs_count(cs_and(spread, nc));
     v.numa_cpu[i] = s->numa_cpu[i];
     v.numa_mem[i] = s->numa_mem[i];
-    v.alloc_cpu[i] = m->alloc_cpu[i];
-    v.alloc_mem[i] = m->alloc_mem[i];
+    // getAvailableNUMANodeResources (node_allocation.go:155-177): with a cpu ratio > 1 the cpuset part of an
+    // allocatedResources entry (allocated cpus on NUMA node i × 1000) counts amplified
+    const bool present = (m->present >> i) & 1u;
+    const int64_t sets = (int64_t)cs_count(cs_and(alloc, nc)) * 1000;
+    v.alloc_cpu[i] = present ? m->alloc_cpu[i] - sets + amplify(sets, v.amp) : 0;
+    v.alloc_mem[i] = present ? m->alloc_mem[i] : 0;
   }
   return v;
+}
+
+// getResourceOptions (plugin.go:470-510): a cpu-bind pod's cpu request amplified by the node's ratio
+// (AmplifyResourceList), for the hints, the NUMA allocation and the score
+__device__ __forceinline__ int64_t opt_cpu(const NumaView& v, const NumaPod& p) {
+  return p.cpu_bind ? amplify(p.req_cpu, v.amp) : p.req_cpu;
 }
 
 // getPreferredCPUBindPolicy (plugin.go:556-576); -1: getResourceOptions fails (topology missing / invalid)
@@ -667,6 +687,7 @@ __device__ __forceinline__ bool numa_admit(const NumaView& v, const NumaPod& p, 
   int nl = 1;
   uint64_t sc_lo = 0, sc_hi = 0;
   const bool req_c = p.req_cpu > 0, req_m = p.req_mem > 0;
+  const int64_t rqc = opt_cpu(v, p);
   if (bind >= 0 && (req_c || req_m)) {
     int64_t av_cpu[kNumaMax], av_mem[kNumaMax];
     const bool trim = p.cpu_bind && p.required != 0;
@@ -698,8 +719,7 @@ __device__ __forceinline__ bool numa_admit(const NumaView& v, const NumaPod& p, 
           tot_m += v.numa_mem[i];
         }
       const int64_t rq_c = tot_c - a_c > 0 ? tot_c - a_c : 0, rq_m = tot_m - a_m > 0 ? tot_m - a_m : 0;
-      const int64_t sc = numa_scorer(NP.numa_strategy, NP.nw_cpu, NP.nw_mem, rq_c, rq_m, tot_c, tot_m, p.req_cpu,
-                                     p.req_mem);
+      const int64_t sc = numa_scorer(NP.numa_strategy, NP.nw_cpu, NP.nw_mem, rq_c, rq_m, tot_c, tot_m, rqc, p.req_mem);
       if (k < 9) sc_lo |= (uint64_t)sc << (7 * k);
       else sc_hi |= (uint64_t)sc << (7 * (k - 9));
       const int cnt = __popc(mk);
@@ -707,9 +727,9 @@ __device__ __forceinline__ bool numa_admit(const NumaView& v, const NumaPod& p, 
         if (cnt < min_m) min_m = cnt;
         if (a_m >= p.req_mem) hm |= 1u << k;
       }
-      if (req_c && tot_c >= p.req_cpu) {
+      if (req_c && tot_c >= rqc) {
         if (cnt < min_c) min_c = cnt;
-        if (a_c >= p.req_cpu) hc |= 1u << k;
+        if (a_c >= rqc) hc |= 1u << k;
       }
     }
     // filterProvidersHints (policy.go:94-125): resources in sorted-name order (cpu, memory); a present but
@@ -748,7 +768,7 @@ __device__ __forceinline__ bool alloc_by_hint(const NumaView& v, const NumaPod& 
 #pragma unroll
   for (int i = 0; i < kNumaMax; ++i) a.cpu[i] = a.mem[i] = 0;
   if (v.nn == 0) return false;
-  int64_t rq_c = p.req_cpu, rq_m = p.req_mem;
+  int64_t rq_c = opt_cpu(v, p), rq_m = p.req_mem;
   const bool key_c = p.req_cpu > 0, key_m = p.req_mem > 0;
   bool done = false;
 #pragma unroll
@@ -810,9 +830,17 @@ __device__ __forceinline__ bool skip_the_node(const NumaPod& p, int policy) {
 }
 
 // NodeNUMAResource.Filter (plugin.go:276-334); writes the affinity the topology manager stores
-__device__ __forceinline__ bool numa_filter(const NumaView& v, const NumaPod& p, const NumaParams& NP, NumaHint& aff) {
+__device__ __forceinline__ bool numa_filter(const NumaView& v, const NumaPod& p, const NumaParams& NP, NumaHint& aff,
+                                            int64_t node_req_cpu, int64_t node_alloc_cpu) {
   aff = NumaHint{0, 1, 0, 0};
   if (p.prefilter_error) return false;
+  if (p.req_cpu != 0 && v.amp > 1.0) {  // filterAmplifiedCPUs (plugin.go:336-373)
+    const int64_t pod = opt_cpu(v, p);
+    const int64_t am = v.valid ? (int64_t)v.n_alloc * 1000 : 0;  // GetAvailableCPUs needs a valid topology
+    int64_t req = node_req_cpu;
+    if (req >= am && am > 0) req = req - am + amplify(am, v.amp);
+    if (pod > node_alloc_cpu - req) return false;  // ErrInsufficientAmplifiedCPU
+  }
   if (skip_the_node(p, v.policy)) return true;
   NumaAlloc a;
   if (p.cpu_bind) {
@@ -841,7 +869,12 @@ __device__ __forceinline__ int64_t numa_score(const NumaView& v, const NumaPod& 
   if (skip_the_node(p, v.policy)) {
     if (p.skip) return 0;
     if (numa_pref_bind(v, p.preferred) < 0) return 0;  // scoreWithAmplifiedCPUs: getResourceOptions
-    return numa_scorer(NP.node_strategy, NP.w_cpu, NP.w_mem, node_req_cpu, node_req_mem, node_alloc_cpu,
+    int64_t rc = node_req_cpu;
+    if (p.req_cpu != 0 && v.amp > 1.0) {  // the cpuset part of Requested counts amplified (scoring.go:95-120)
+      const int64_t am = (int64_t)v.n_alloc * 1000;
+      rc = rc - am + amplify(am, v.amp);
+    }
+    return numa_scorer(NP.node_strategy, NP.w_cpu, NP.w_mem, rc, node_req_mem, node_alloc_cpu,
                        node_alloc_mem, p.req_cpu, p.req_mem);
   }
   if (p.cpu_bind && !v.valid) return 0;
@@ -859,9 +892,9 @@ __device__ __forceinline__ int64_t numa_score(const NumaView& v, const NumaPod& 
         am += v.numa_mem[i];
       }
   }
-  // a cpuset pod: requested cpu = |allocated cpus| · 1000 (needed ≥ 1 whenever cpu_bind)
-  if (p.cpu_bind) rc = (int64_t)v.n_alloc * 1000;
-  return numa_scorer(NP.node_strategy, NP.w_cpu, NP.w_mem, rc, rm, ac, am, p.req_cpu, p.req_mem);
+  // a cpuset pod: requested cpu = Amplify(|allocated cpus| · 1000) (needed ≥ 1 whenever cpu_bind)
+  if (p.cpu_bind) rc = amplify((int64_t)v.n_alloc * 1000, v.amp);
+  return numa_scorer(NP.node_strategy, NP.w_cpu, NP.w_mem, rc, rm, ac, am, opt_cpu(v, p), p.req_mem);
 }
 
 // Filter (when the profile has it) + Score of one node: feasibility and the unweighted plugin score
@@ -870,7 +903,7 @@ __device__ __forceinline__ bool numa_eval(const NumaView& v, const NumaPod& p, c
                                           int64_t node_alloc_mem, int64_t& score, NumaHint& aff) {
   aff = NumaHint{0, 1, 0, 0};
   score = 0;
-  if (NP.filter && !numa_filter(v, p, NP, aff)) return false;
+  if (NP.filter && !numa_filter(v, p, NP, aff, node_req_cpu, node_alloc_cpu)) return false;
   if (NP.score) score = numa_score(v, p, NP, aff, node_req_cpu, node_req_mem, node_alloc_cpu, node_alloc_mem);
   return true;
 }
@@ -917,6 +950,7 @@ __device__ __noinline__ bool numa_reserve(const NumaStatic& s, NumaMut& m, const
       m.alloc_cpu[i] += a.cpu[i];
       m.alloc_mem[i] += a.mem[i];
     }
+  m.present |= a.res;
   rec = a;
   return true;
 }

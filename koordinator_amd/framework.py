@@ -184,10 +184,11 @@ def make_node_metric(present: bool = True, update_time_ns: int | None = 0, node_
 def make_node_numa(sockets: int = 0, nodes_per_socket: int = 1, cores_per_node: int = 0, cpus_per_core: int = 2,
                    numa_policy: str = "", node_cpu_bind_policy: str = "", numa_allocate_strategy: str | None = None,
                    numa_resources: list | None = None, reserved_cpus=(), allocated_cpus=(),
-                   numa_allocated: dict | None = None) -> np.ndarray:
+                   numa_allocated: dict | None = None, cpu_amplification_ratio: float = 0.0) -> np.ndarray:
     """NodeNUMAResource view of a node: the NodeResourceTopology's CPU topology (buildCPUTopology numbering),
     policies and zones, and the NodeAllocation of already-bound pods. numa_resources = [{"cpu": .., "memory": ..}]
-    per NUMA zone; numa_allocated = {zone: {"cpu": .., "memory": ..}}."""
+    per NUMA zone; numa_allocated = {zone: {"cpu": .., "memory": ..}}; cpu_amplification_ratio = the node's
+    node.koordinator.sh/resource-amplification-ratio cpu (≤ 1 none; zone cpu is given amplified)."""
     n = np.zeros(1, dtype=abi.NODE_NUMA_DTYPE)
     r = n[0]
     r["has_topology"] = int(sockets > 0)
@@ -209,6 +210,7 @@ def make_node_numa(sockets: int = 0, nodes_per_socket: int = 1, cores_per_node: 
     for i, res in (numa_allocated or {}).items():
         r["numa_alloc_cpu"][i] = resource_value("cpu", res.get("cpu", 0))
         r["numa_alloc_mem"][i] = resource_value("memory", res.get("memory", 0))
+    r["cpu_amplification_ratio"] = cpu_amplification_ratio
     return n
 
 

@@ -287,6 +287,24 @@ def load_gpu_into(engine, cluster: Cluster, dev: np.ndarray):
     engine.upsert_devices(dev)
 
 
+def amplify_numa_cluster(cluster: Cluster, numa: np.ndarray, frac: float = 0.3, seed: int = BASE_SEED + 5):
+    """CPU amplification (node.koordinator.sh/resource-amplification-ratio cpu ∈ {1.5, 2.0, 2.5}) on `frac` of
+    make_numa_cluster's nodes, as the NodeResource controller leaves them: node allocatable cpu and each NUMA zone's
+    cpu amplified (Amplify: ceil in float64, apis/extension/node_resource_amplification.go:170-175), the bound
+    cpuset pods' NUMA allocations unchanged.  In place; returns the ratios."""
+    rng = np.random.default_rng(seed)
+    n = cluster.n
+    on = rng.random(n) < frac
+    ratio = np.where(on, rng.choice(np.array([1.5, 2.0, 2.5]), n), 0.0)
+    amp = lambda v, r: np.where(r > 1, np.ceil(v.astype(np.float64) * r), v).astype(np.int64)
+    cores = cluster.nodes["allocatable"][:, abi.RES_CPU] // 1000
+    cluster.nodes["allocatable"][:, abi.RES_CPU] = amp(cores, ratio) * 1000
+    zc = numa["numa_cpu"] // 1000
+    numa["numa_cpu"] = amp(zc, ratio[:, None]) * 1000
+    numa["cpu_amplification_ratio"] = ratio
+    return ratio
+
+
 # ---- config C5: Reservation matching (50k nodes; 0–4 reservations on 30 % of nodes, owner label selectors) -----
 N_OWNERS = 64  # owner groups (reservations sharing an owner spec); a pod carries the bitmask of the groups it matches
 

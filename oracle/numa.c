@@ -23,6 +23,8 @@
  */
 #include "numa.h"
 
+#include <math.h>
+
 #include <string.h>
 
 #define MAX_NODE_SCORE 100
@@ -464,6 +466,7 @@ void or_numa_node_init(or_numa_node* n, const kg_node_numa* s) {
   n->node_cpu_bind_policy = (int)s->node_cpu_bind_policy;
   n->numa_allocate_strategy = (int)s->numa_allocate_strategy;
   n->num_numa = (int)s->num_numa;
+  n->cpu_amp = s->cpu_amplification_ratio;
   for (int i = 0; i < KG_MAX_NUMA; i++) {
     n->numa_cpu[i] = s->numa_cpu[i];
     n->numa_mem[i] = s->numa_mem[i];
@@ -532,10 +535,35 @@ static or_cpuset available_cpus(const or_numa_node* n) {
   return cs_andnot(cs_andnot(n->topo.all, n->allocated), n->reserved);
 }
 
-/* getAvailableNUMANodeResources (node_allocation.go:155-177), no amplification / reusable resources */
+/* extension.Amplify (apis/extension/node_resource_amplification.go:170-175) */
+static int64_t amplify(int64_t origin, double ratio) {
+  if (ratio <= 1) return origin;
+  return (int64_t)ceil((double)origin * ratio);
+}
+
+/* getResourceOptions (plugin.go:470-510): a cpu-bind pod's cpu request is amplified by the node's cpu ratio
+ * (AmplifyResourceList) for the hints, the NUMA allocation and the score */
+static int64_t opt_req_cpu(const or_numa_node* n, const or_numa_pod* p) {
+  return (p->request_cpu_bind && n->cpu_amp > 1) ? amplify(p->req_cpu, n->cpu_amp) : p->req_cpu;
+}
+
+/* allocatedResources[i] cpu as getAvailableNUMANodeResources sees it (node_allocation.go:155-177): with a cpu
+ * ratio > 1 the cpuset part (allocated cpus on NUMA node i × 1000) counts amplified; 0 when no entry */
+static int64_t numa_allocated_cpu(const or_numa_node* n, int i) {
+  if (!n->numa_alloc_present[i]) return 0;
+  int64_t c = n->numa_alloc_cpu[i];
+  if (n->cpu_amp > 1) {
+    const or_cpuset in = cs_and(n->allocated, cpus_in_numa(&n->topo, i));
+    const int64_t sets = (int64_t)cs_size(&in) * 1000;
+    c = c - sets + amplify(sets, n->cpu_amp);
+  }
+  return c;
+}
+
+/* getAvailableNUMANodeResources (node_allocation.go:155-177), no reusable resources (no reservations) */
 static void numa_available(const or_numa_node* n, int64_t avail_cpu[], int64_t avail_mem[]) {
   for (int i = 0; i < n->num_numa; i++) {
-    const int64_t ac = n->numa_alloc_present[i] ? n->numa_alloc_cpu[i] : 0;
+    const int64_t ac = numa_allocated_cpu(n, i);
     const int64_t am = n->numa_alloc_present[i] ? n->numa_alloc_mem[i] : 0;
     avail_cpu[i] = n->numa_cpu[i] - ac > 0 ? n->numa_cpu[i] - ac : 0;
     avail_mem[i] = n->numa_mem[i] - am > 0 ? n->numa_mem[i] - am : 0;
@@ -640,7 +668,8 @@ static int numa_hints(const kg_config* cfg, const or_numa_node* n, const or_numa
         tot_m += n->numa_mem[i];
       }
     const int64_t rq_c = tot_c - av_c > 0 ? tot_c - av_c : 0, rq_m = tot_m - av_m > 0 ? tot_m - av_m : 0;
-    const int64_t score = scorer((int)cfg->numa_numa_scoring_strategy, wn, rq_c, rq_m, tot_c, tot_m, p->req_cpu, p->req_mem);
+    const int64_t score = scorer((int)cfg->numa_numa_scoring_strategy, wn, rq_c, rq_m, tot_c, tot_m, opt_req_cpu(n, p),
+                                 p->req_mem);
     const int cnt = __builtin_popcount(m);
     /* generateHints(mask, ..., memory) then (..., cpu): total ≥ request gates the min affinity size, free ≥
      * request gates the hint */
@@ -651,9 +680,9 @@ static int numa_hints(const kg_config* cfg, const or_numa_node* n, const or_numa
         hm->h[hm->n++] = h;
       }
     }
-    if (req_c && tot_c >= p->req_cpu) {
+    if (req_c && tot_c >= opt_req_cpu(n, p)) {
       if (cnt < min_c) min_c = cnt;
-      if (av_c >= p->req_cpu) {
+      if (av_c >= opt_req_cpu(n, p)) {
         or_hint h = {0, m, 0, score};
         hc->h[hc->n++] = h;
       }
@@ -782,7 +811,7 @@ static int allocate(const kg_config* cfg, const or_numa_node* n, const or_numa_p
     if (n->num_numa == 0) return -1;
     int64_t avail_cpu[KG_MAX_NUMA], avail_mem[KG_MAX_NUMA];
     numa_available(n, avail_cpu, avail_mem);
-    int64_t rq_c = p->req_cpu, rq_m = p->req_mem;
+    int64_t rq_c = opt_req_cpu(n, p), rq_m = p->req_mem;
     const int key_c = p->req_cpu > 0, key_m = p->req_mem > 0;
     int inter_c = 0, inter_m = 0;
     for (int i = 0; i < n->num_numa; i++) {
@@ -844,10 +873,18 @@ static int allocate(const kg_config* cfg, const or_numa_node* n, const or_numa_p
 /* ---------------------------------------------------------------------------------------------------- */
 /* plugin extension points                                                                                */
 /* ---------------------------------------------------------------------------------------------------- */
-int or_numa_filter(const kg_config* cfg, const or_numa_node* n, const or_numa_pod* p, or_hint* affinity) {
+int or_numa_filter(const kg_config* cfg, const or_numa_node* n, const or_numa_pod* p, or_hint* affinity,
+                   int64_t node_req_cpu, int64_t node_alloc_cpu) {
   *affinity = (or_hint){1, 0, 0, 0};
   if (p->prefilter_error) return 0;
-  /* filterAmplifiedCPUs: no amplification → pass */
+  if (p->req_cpu != 0 && n->cpu_amp > 1) { /* filterAmplifiedCPUs (plugin.go:336-373) */
+    const int64_t pod = p->request_cpu_bind ? amplify(p->req_cpu, n->cpu_amp) : p->req_cpu;
+    /* GetAvailableCPUs fails without a valid topology: no allocated cpus */
+    const int64_t am = (n->has_topology && n->valid_topology) ? (int64_t)cs_size(&n->allocated) * 1000 : 0;
+    int64_t req = node_req_cpu;
+    if (req >= am && am > 0) req = req - am + amplify(am, n->cpu_amp);
+    if (pod > node_alloc_cpu - req) return 0; /* ErrInsufficientAmplifiedCPU */
+  }
   const int policy = n->numa_policy;
   if (skip_the_node(p, policy)) return 1;
   if (p->request_cpu_bind) {
@@ -890,7 +927,12 @@ int64_t or_numa_score(const kg_config* cfg, const or_numa_node* n, const or_numa
     if (p->skip) return 0;
     /* scoreWithAmplifiedCPUs (:95-120): getResourceOptions needs a valid topology */
     if (preferred_bind(n, p->preferred_policy) < 0) return 0;
-    return scorer(strategy, w, node_req_cpu, node_req_mem, node_alloc_cpu, node_alloc_mem, p->req_cpu, p->req_mem);
+    int64_t rc = node_req_cpu;
+    if (p->req_cpu != 0 && n->cpu_amp > 1) { /* the cpuset part of Requested counts amplified */
+      const int64_t am = (int64_t)cs_size(&n->allocated) * 1000;
+      rc = rc - am + amplify(am, n->cpu_amp);
+    }
+    return scorer(strategy, w, rc, node_req_mem, node_alloc_cpu, node_alloc_mem, p->req_cpu, p->req_mem);
   }
   if (p->request_cpu_bind && (!n->has_topology || !n->valid_topology)) return 0;
   numa_alloc res;
@@ -903,7 +945,7 @@ int64_t or_numa_score(const kg_config* cfg, const or_numa_node* n, const or_numa
     for (int k = 0; k < res.n; k++) {
       const int i = res.numa[k];
       if (n->numa_alloc_present[i]) {
-        req_c += n->numa_alloc_cpu[i];
+        req_c += numa_allocated_cpu(n, i);
         req_m += n->numa_alloc_mem[i];
       }
       alloc_c += n->numa_cpu[i];
@@ -915,8 +957,8 @@ int64_t or_numa_score(const kg_config* cfg, const or_numa_node* n, const or_numa
     req_c = node_req_cpu;
     req_m = node_req_mem;
   }
-  if (cs_size(&cpus) > 0) req_c = (int64_t)cs_size(&n->allocated) * 1000;
-  return scorer(strategy, w, req_c, req_m, alloc_c, alloc_m, p->req_cpu, p->req_mem);
+  if (cs_size(&cpus) > 0) req_c = amplify((int64_t)cs_size(&n->allocated) * 1000, n->cpu_amp);
+  return scorer(strategy, w, req_c, req_m, alloc_c, alloc_m, opt_req_cpu(n, p), p->req_mem);
 }
 
 int or_numa_reserve(const kg_config* cfg, or_numa_node* n, const or_numa_pod* p, const or_hint* affinity,
@@ -995,7 +1037,7 @@ int or_numa_eval_flat(const kg_config* cfg, const kg_node_numa* node, const kg_p
   or_numa_pod p;
   or_numa_pod_init(cfg, pod, &p);
   or_hint h;
-  const int ok = or_numa_filter(cfg, &n, &p, &h);
+  const int ok = or_numa_filter(cfg, &n, &p, &h, node_req_cpu, node_alloc_cpu);
   *affinity_mask = h.nil ? -1 : (int64_t)h.mask;
   *score = ok ? or_numa_score(cfg, &n, &p, &h, node_req_cpu, node_req_mem, node_alloc_cpu, node_alloc_mem) : 0;
   return ok;
@@ -1008,7 +1050,7 @@ int or_numa_reserve_flat(const kg_config* cfg, const kg_node_numa* node, const k
   or_numa_pod p;
   or_numa_pod_init(cfg, pod, &p);
   or_hint h;
-  or_numa_filter(cfg, &n, &p, &h);
+  or_numa_filter(cfg, &n, &p, &h, 0, INT64_MAX / 4);
   or_cpuset cs;
   const int rc = or_numa_reserve(cfg, &n, &p, &h, &cs, NULL);
   for (int w = 0; w < OR_CPUSET_WORDS; w++) cpuset[w] = cs.w[w];

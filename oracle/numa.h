@@ -33,6 +33,7 @@ typedef struct {
   int numa_policy, node_cpu_bind_policy, numa_allocate_strategy;
   int num_numa;
   int64_t numa_cpu[KG_MAX_NUMA], numa_mem[KG_MAX_NUMA];
+  double cpu_amp; /* cpu amplification ratio (≤ 1 = none) */
   or_cpuset reserved;
   /* mutable */
   or_cpuset allocated;
@@ -65,8 +66,10 @@ or_cpuset or_filter_required(const or_topology* t, or_cpuset available, int poli
 void or_numa_node_init(or_numa_node* n, const kg_node_numa* src);
 void or_numa_pod_init(const kg_config* cfg, const kg_pod* pod, or_numa_pod* out);
 
-/* Filter (plugin.go:276-334).  Returns 1 when the node passes; writes the stored affinity. */
-int or_numa_filter(const kg_config* cfg, const or_numa_node* n, const or_numa_pod* p, or_hint* affinity);
+/* Filter (plugin.go:276-334; filterAmplifiedCPUs :336-373 reads NodeInfo.Requested / Allocatable cpu).  Returns 1
+ * when the node passes; writes the stored affinity. */
+int or_numa_filter(const kg_config* cfg, const or_numa_node* n, const or_numa_pod* p, or_hint* affinity,
+                   int64_t node_req_cpu, int64_t node_alloc_cpu);
 /* Score (scoring.go:55-120) with the affinity Filter stored; req/alloc = NodeInfo.Requested/Allocatable. */
 int64_t or_numa_score(const kg_config* cfg, const or_numa_node* n, const or_numa_pod* p, const or_hint* affinity,
                       int64_t node_req_cpu, int64_t node_req_mem, int64_t node_alloc_cpu, int64_t node_alloc_mem);

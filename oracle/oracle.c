@@ -286,7 +286,9 @@ static void eval_filter(sched_ctx* c, int64_t i) {
     if (s != 0) ok = 0;
   }
   if (c->numa) c->affinity[i] = (or_hint){1, 0, 0, 0};
-  if (ok && cfg->numa_filter && c->numa && !or_numa_filter(cfg, &c->numa[i], &c->numa_pod, &c->affinity[i])) ok = 0;
+  if (ok && cfg->numa_filter && c->numa && !or_numa_filter(cfg, &c->numa[i], &c->numa_pod, &c->affinity[i],
+                                                            c->st[i].requested[KG_RES_CPU],
+                                                            c->nodes[i].allocatable[KG_RES_CPU])) ok = 0;
   if (ok && cfg->ds_filter && c->dev && !or_ds_filter(&c->dev[i], &c->ds_pod)) ok = 0;
   c->feasible[i] = ok;
 }
