@@ -80,6 +80,11 @@ enum { KG_NUMA_POLICY_NONE = 0, KG_NUMA_POLICY_BEST_EFFORT = 1, KG_NUMA_POLICY_R
 /* ScoringStrategy type / NUMAAllocateStrategy */
 enum { KG_STRATEGY_LEAST_ALLOCATED = 0, KG_STRATEGY_MOST_ALLOCATED = 1 };
 #define KG_MAX_NUMA 4
+/* NodeMetric AggregatedNodeUsages (apis/slo/v1alpha1/nodemetric_types.go): ≤ KG_MAX_AGG durations, each with the
+ * KG_AGG_TYPES percentile kinds of extension.AggregationType (apis/extension/constants.go:45-54) */
+#define KG_MAX_AGG 4
+#define KG_AGG_TYPES 5
+enum { KG_AGG_NONE = 0, KG_AGG_AVG = 1, KG_AGG_P50 = 2, KG_AGG_P90 = 3, KG_AGG_P95 = 4, KG_AGG_P99 = 5 };
 #define KG_MAX_CPUS 256
 
 /* DeviceShare: device resources a pod may request (deviceshare/utils.go:46-56, apis/extension/resource.go) */
@@ -187,6 +192,12 @@ typedef struct kg_config {
   int64_t reservation_score;                   /* Reservation at PreScore/Score (NormalizeScore: DefaultNormalizeScore) */
   int64_t weight_reservation;
   int64_t pipeline_depth;                      /* rounds in flight (1..4; 0 = default 2) for monotone profiles  */
+  /* LoadAwareSchedulingArgs.Aggregated (config/types.go:56-76): percentile usage for Filter / Score */
+  int64_t la_agg_usage_thresholds[KG_RES_MAX]; /* Aggregated.UsageThresholds (0 = absent)            */
+  int64_t la_agg_usage_type;                   /* UsageAggregationType KG_AGG_* (0 = "")              */
+  int64_t la_agg_usage_duration_ns;            /* UsageAggregatedDuration (0 = the longest recorded) */
+  int64_t la_agg_score_type;                   /* ScoreAggregationType KG_AGG_* (0 = "")              */
+  int64_t la_agg_score_duration_ns;            /* ScoreAggregatedDuration (0 = the longest recorded) */
   int64_t reserved[4];
 } kg_config;
 
@@ -199,6 +210,10 @@ typedef struct kg_node {
   int64_t raw_allocatable_present[KG_RES_MAX]; /* key present in the annotation map                   */
   int64_t custom_usage_thresholds[KG_RES_MAX]; /* extension.GetCustomUsageThresholds; -1 = absent      */
   int64_t custom_prod_usage_thresholds[KG_RES_MAX];
+  /* the annotation's CustomUsageThresholds.AggregatedUsage (apis/extension/load_aware.go:40-50) */
+  int64_t custom_agg_thresholds[KG_RES_MAX];   /* UsageThresholds; -1 = absent                        */
+  int64_t custom_agg_type;                     /* UsageAggregationType KG_AGG_* (0 = "")              */
+  int64_t custom_agg_duration_ns;              /* UsageAggregatedDuration (0 = nil / the longest)    */
 } kg_node;
 
 /* NodeMetric status summary for one node (apis/slo/v1alpha1/nodemetric_types.go:107-122). */
@@ -212,6 +227,10 @@ typedef struct kg_node_metric {
   int64_t pods_metric_count;                   /* len(Status.PodsMetric)                              */
   int64_t prod_pods_usage[KG_RES_MAX];         /* Σ PodsMetric usage of prod pods (buildPodMetricMap  */
                                                /* filterProdPod=true + sumPodUsages, helper.go:153-186) */
+  int64_t agg_count;                           /* len(Status.NodeMetric.AggregatedNodeUsages)         */
+  int64_t agg_duration_ns[KG_MAX_AGG];         /* AggregatedUsage.Duration                            */
+  int64_t agg_usage[KG_MAX_AGG][KG_AGG_TYPES][2];  /* Usage[type] cpu (milli) / memory (bytes)       */
+  int64_t agg_present[KG_MAX_AGG][KG_AGG_TYPES];   /* bit r: resource r in that ResourceList (0 = empty) */
 } kg_node_metric;
 
 /* One pod, pre-decoded by the caller (PodRequestsAndLimits semantics, pkg/util/pod_resources_utils.go:48-64). */

@@ -85,7 +85,10 @@ CONFIG_DTYPE = np.dtype([
     _i64("ds_scoring_weights", 3),
     _i64("batch_pods"), _i64("pods_per_wave"), _i64("device_id"),
     _i64("reservation_filter"), _i64("reservation_score"), _i64("weight_reservation"),
-    _i64("pipeline_depth"), _i64("reserved", 4),
+    _i64("pipeline_depth"),
+    _i64("la_agg_usage_thresholds", RES_MAX), _i64("la_agg_usage_type"), _i64("la_agg_usage_duration_ns"),
+    _i64("la_agg_score_type"), _i64("la_agg_score_duration_ns"),
+    _i64("reserved", 4),
 ])
 
 NODE_DTYPE = np.dtype([
@@ -96,6 +99,7 @@ NODE_DTYPE = np.dtype([
     _i64("raw_allocatable_present", RES_MAX),
     _i64("custom_usage_thresholds", RES_MAX),
     _i64("custom_prod_usage_thresholds", RES_MAX),
+    _i64("custom_agg_thresholds", RES_MAX), _i64("custom_agg_type"), _i64("custom_agg_duration_ns"),
 ])
 
 METRIC_DTYPE = np.dtype([
@@ -104,7 +108,9 @@ METRIC_DTYPE = np.dtype([
     _i64("node_usage_present", RES_MAX),
     _i64("pods_metric_count"),
     _i64("prod_pods_usage", RES_MAX),
+    _i64("agg_count"), _i64("agg_duration_ns", 4), ("agg_usage", np.int64, (4, 5, 2)), ("agg_present", np.int64, (4, 5)),
 ])
+AGG_TYPES = {"": 0, "avg": 1, "p50": 2, "p90": 3, "p95": 4, "p99": 5}
 
 POD_DTYPE = np.dtype([
     _i64("requests", RES_MAX),

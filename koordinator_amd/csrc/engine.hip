@@ -1985,6 +1985,9 @@ int validate_config(const kg_config* c) {
   if (c->weight_fit < 0 || c->weight_fit > 1000000 || c->weight_loadaware < 0 || c->weight_loadaware > 1000000)
     return fail(KG_E_INVALID, "plugin weight out of range");
   if (c->batch_pods < 0 || c->batch_pods > kMaxB) return fail(KG_E_INVALID, "batch_pods must be in [1,%d]", kMaxB);
+  if (c->la_agg_usage_type < KG_AGG_NONE || c->la_agg_usage_type > KG_AGG_P99 || c->la_agg_score_type < KG_AGG_NONE ||
+      c->la_agg_score_type > KG_AGG_P99 || c->la_agg_usage_duration_ns < 0 || c->la_agg_score_duration_ns < 0)
+    return fail(KG_E_INVALID, "LoadAwareSchedulingArgs.Aggregated: aggregation type / duration");
   if (c->reservation_filter || c->reservation_score) {
     if (c->weight_reservation < 0 || c->weight_reservation > 1000000) return fail(KG_E_INVALID, "Reservation weight out of range");
     if (c->numa_filter || c->numa_score)
@@ -2042,6 +2045,49 @@ int64_t usage_percent(int r, int64_t used, int64_t total) {
 
 // LoadAware Filter verdict for one node, for a non-prod (prod=false) or prod pod (load_aware.go:123-254).
 // Pod-invariant apart from {prod, daemonset}: Filter ignores estimated/assigned pods (":198 TODO").
+// getTargetAggregatedUsage (loadaware/helper.go:58-92): the AggregatedNodeUsages entry whose Usage[type] is
+// read, -1 = nil (no NodeMetric, no entries, or the chosen entry's map is empty)
+int agg_index(const kg_node_metric& m, int64_t dur_ns, int64_t type) {
+  if (!m.has_node_metric || m.agg_count <= 0 || type < 1 || type > KG_AGG_TYPES) return -1;
+  const int n = (int)std::min<int64_t>(m.agg_count, KG_MAX_AGG);
+  if (dur_ns == 0) {  // no period: the longest one recorded (the first of equals)
+    int64_t maxd = 0;
+    int maxi = 0;
+    for (int i = 0; i < n; ++i)
+      if (m.agg_duration_ns[i] > maxd) maxd = m.agg_duration_ns[i], maxi = i;
+    return m.agg_present[maxi][type - 1] ? maxi : -1;
+  }
+  for (int i = 0; i < n; ++i)
+    if (m.agg_duration_ns[i] == dur_ns && m.agg_present[i][type - 1]) return i;
+  return -1;
+}
+int64_t agg_value(const kg_node_metric& m, int i, int64_t type, int r) {
+  return (r < 2 && ((m.agg_present[i][type - 1] >> r) & 1)) ? m.agg_usage[i][type - 1][r] : 0;
+}
+
+// generateUsageThresholdsFilterProfile's AggregatedUsage (helper.go:102-140): the node annotation's when complete,
+// else the args' when filterWithAggregation.  False = nil.
+bool agg_filter_profile(const kg_config& c, const kg_node& n, int64_t thr[KG_RES_MAX], int64_t& type, int64_t& dur) {
+  int nargs = 0, ncust = 0;
+  for (int r = 0; r < KG_RES_MAX; ++r) {
+    nargs += c.la_agg_usage_thresholds[r] != 0;
+    ncust += n.custom_agg_thresholds[r] >= 0;
+  }
+  if ((n.flags & KG_NODE_HAS_CUSTOM_THRESHOLDS) && ncust > 0 && n.custom_agg_type != KG_AGG_NONE) {
+    for (int r = 0; r < KG_RES_MAX; ++r) thr[r] = std::max<int64_t>(n.custom_agg_thresholds[r], 0);
+    type = n.custom_agg_type;
+    dur = n.custom_agg_duration_ns;
+    return true;
+  }
+  if (nargs > 0 && c.la_agg_usage_type != KG_AGG_NONE) {
+    for (int r = 0; r < KG_RES_MAX; ++r) thr[r] = c.la_agg_usage_thresholds[r];
+    type = c.la_agg_usage_type;
+    dur = c.la_agg_usage_duration_ns;
+    return true;
+  }
+  return false;
+}
+
 bool la_filter_pass(const kg_config& c, const kg_node& n, const kg_node_metric& m, int64_t now, bool prod) {
   if (!m.present) return true;
   if (c.la_filter_expired_node_metrics && c.la_node_metric_expiration_seconds >= 0 &&
@@ -2067,13 +2113,17 @@ bool la_filter_pass(const kg_config& c, const kg_node& n, const kg_node_metric& 
     }
     return true;
   }
+  int64_t athr[KG_RES_MAX], atype = 0, adur = 0;
+  const bool agg = agg_filter_profile(c, n, athr, atype, adur);
   if (!m.has_node_metric) return true;  // filterNodeUsage (load_aware.go:173-224)
+  const int ai = agg ? agg_index(m, adur, atype) : -1;
   for (int r = 0; r < KG_RES_MAX; ++r) {
-    const int64_t t = thr(r);
+    const int64_t t = agg ? athr[r] : thr(r);
     if (t == 0) continue;
     const int64_t total = estimate_node(n, r);
     if (total == 0) continue;
-    const int64_t used = m.node_usage_present[r] ? m.node_usage[r] : 0;
+    if (agg && ai < 0) continue;  // aggregated usage nil
+    const int64_t used = agg ? agg_value(m, ai, atype, r) : (m.node_usage_present[r] ? m.node_usage[r] : 0);
     if (usage_percent(r, used, total) >= t) return false;
   }
   return true;
@@ -2395,8 +2445,14 @@ int push_deltas(kg_engine* e, const std::vector<RowDelta>& d) {
   return 0;
 }
 
-// NodeUsage folded into la_used (non-prod view): load_aware.go:307-326 with an empty PodsMetric.
-void usage_for_score(const kg_node_metric& m, int64_t u[2]) {
+// NodeUsage folded into la_used (non-prod view): load_aware.go:307-326 with an empty PodsMetric — the aggregated
+// usage of ScoreAggregationType when scoreWithAggregation (nil: no node usage at all).
+void usage_for_score(const kg_config& c, const kg_node_metric& m, int64_t u[2]) {
+  if (c.la_agg_score_type != KG_AGG_NONE) {
+    const int i = m.present ? agg_index(m, c.la_agg_score_duration_ns, c.la_agg_score_type) : -1;
+    for (int r = 0; r < 2; ++r) u[r] = i >= 0 ? agg_value(m, i, c.la_agg_score_type, r) : 0;
+    return;
+  }
   for (int r = 0; r < 2; ++r) u[r] = (m.present && m.has_node_metric && m.node_usage_present[r]) ? m.node_usage[r] : 0;
 }
 
@@ -3202,7 +3258,7 @@ int kg_node_metrics_update(kg_engine* e, const kg_node_metric* m, const int32_t*
   for (int64_t k = 0; k < n; ++k) {
     const int64_t i = idx[k];
     int64_t u[2];
-    usage_for_score(m[k], u);
+    usage_for_score(e->cfg, m[k], u);
     RowDelta x{};
     x.idx = i;
     x.d[5] = u[0] - e->folded_usage[2 * i];

@@ -47,6 +47,9 @@ class LoadAwareSchedulingArgs:
     prod_usage_thresholds: dict = field(default_factory=dict)
     score_according_prod_usage: bool = False
     estimated_scaling_factors: dict = field(default_factory=lambda: {"cpu": 85, "memory": 70})
+    # Aggregated (config/types.go:56-76): usage_thresholds / usage_type ("p95", ...) / usage_duration_s for Filter,
+    # score_type / score_duration_s for Score; duration 0 = the longest period recorded
+    aggregated: dict | None = None
 
 
 @dataclass
@@ -98,6 +101,12 @@ def build_config(la: LoadAwareSchedulingArgs | None = None, fit: NodeResourcesFi
     r["la_prod_usage_thresholds"] = _slots(la.prod_usage_thresholds)
     r["la_estimated_scaling_factors"] = _slots(la.estimated_scaling_factors)
     r["la_score_according_prod_usage"] = int(la.score_according_prod_usage)
+    agg = la.aggregated or {}
+    r["la_agg_usage_thresholds"] = _slots(agg.get("usage_thresholds"))
+    r["la_agg_usage_type"] = abi.AGG_TYPES[agg.get("usage_type", "")]
+    r["la_agg_usage_duration_ns"] = int(agg.get("usage_duration_s", 0) * 10**9)
+    r["la_agg_score_type"] = abi.AGG_TYPES[agg.get("score_type", "")]
+    r["la_agg_score_duration_ns"] = int(agg.get("score_duration_s", 0) * 10**9)
     r["fit_resource_weights"] = _slots(fit.scoring_resources)
     r["fit_filter"] = int(NODE_RESOURCES_FIT in profile.filter)
     r["la_filter"] = int(LOAD_AWARE in profile.filter)
@@ -140,7 +149,8 @@ def _values(resources: dict | None) -> np.ndarray:
 
 def make_node(allocatable: dict, allowed_pods: int = 110, raw_allocatable: dict | None = None,
               custom_usage_thresholds: dict | None = None, custom_prod_usage_thresholds: dict | None = None,
-              valid: bool = True) -> np.ndarray:
+              valid: bool = True, custom_aggregated: dict | None = None) -> np.ndarray:
+    """custom_aggregated = the annotation's AggregatedUsage {usage_thresholds, usage_type, usage_duration_s}."""
     n = np.zeros(1, dtype=abi.NODE_DTYPE)
     r = n[0]
     r["allocatable"] = _values(allocatable)
@@ -155,15 +165,21 @@ def make_node(allocatable: dict, allowed_pods: int = 110, raw_allocatable: dict 
         r["raw_allocatable_present"] = pres
     r["custom_usage_thresholds"] = _slots(custom_usage_thresholds, absent=-1)
     r["custom_prod_usage_thresholds"] = _slots(custom_prod_usage_thresholds, absent=-1)
-    if custom_usage_thresholds or custom_prod_usage_thresholds:
+    ca = custom_aggregated or {}
+    r["custom_agg_thresholds"] = _slots(ca.get("usage_thresholds"), absent=-1)
+    r["custom_agg_type"] = abi.AGG_TYPES[ca.get("usage_type", "")]
+    r["custom_agg_duration_ns"] = int(ca.get("usage_duration_s", 0) * 10**9)
+    if custom_usage_thresholds or custom_prod_usage_thresholds or custom_aggregated:
         flags |= abi.NODE_HAS_CUSTOM_THRESHOLDS
     r["flags"] = flags
     return n
 
 
 def make_node_metric(present: bool = True, update_time_ns: int | None = 0, node_usage: dict | None = None,
-                     prod_pods_usage: dict | None = None, pods_metric_count: int = 0) -> np.ndarray:
-    """NodeMetric status summary; node_usage=None means Status.NodeMetric == nil."""
+                     prod_pods_usage: dict | None = None, pods_metric_count: int = 0,
+                     aggregated: list | None = None) -> np.ndarray:
+    """NodeMetric status summary; node_usage=None means Status.NodeMetric == nil.  aggregated = the
+    AggregatedNodeUsages [{"duration_s": .., "p95": {"cpu": .., "memory": ..}, ...}]."""
     m = np.zeros(1, dtype=abi.METRIC_DTYPE)
     r = m[0]
     r["present"] = int(present)
@@ -178,6 +194,20 @@ def make_node_metric(present: bool = True, update_time_ns: int | None = 0, node_
         r["node_usage_present"] = pres
     r["pods_metric_count"] = pods_metric_count
     r["prod_pods_usage"] = _values(prod_pods_usage)
+    aggs = aggregated or []
+    if len(aggs) > 4:
+        raise ValueError("at most 4 AggregatedNodeUsages")
+    r["agg_count"] = len(aggs)
+    for i, a in enumerate(aggs):
+        r["agg_duration_ns"][i] = int(a.get("duration_s", 0) * 10**9)
+        for name, t in abi.AGG_TYPES.items():
+            if t == 0 or name not in a:
+                continue
+            for k, v in a[name].items():
+                slot = abi.RESOURCE_SLOTS[k]
+                if slot < 2:
+                    r["agg_usage"][i, t - 1, slot] = resource_value(k, v)
+                    r["agg_present"][i, t - 1] |= 1 << slot
     return m
 
 

@@ -111,6 +111,50 @@ static void usage_threshold_profile(const kg_config* cfg, const kg_node* node, i
   *n_prod = ncp > 0 ? ncp : nargs_prod;
 }
 
+/* loadaware/helper.go:58-92 getTargetAggregatedUsage: index of the AggregatedNodeUsages entry read, -1 = nil */
+static int target_aggregated(const kg_node_metric* m, int64_t dur_ns, int64_t type) {
+  if (!m->has_node_metric || m->agg_count <= 0 || type < 1 || type > KG_AGG_TYPES) return -1;
+  const int n = m->agg_count < KG_MAX_AGG ? (int)m->agg_count : KG_MAX_AGG;
+  if (dur_ns == 0) { /* "the maximum period recorded by NodeMetrics will be used by default" */
+    int64_t max_d = 0;
+    int max_i = 0;
+    for (int i = 0; i < n; i++)
+      if (m->agg_duration_ns[i] > max_d) { max_d = m->agg_duration_ns[i]; max_i = i; }
+    return m->agg_present[max_i][type - 1] ? max_i : -1; /* len(usage.ResourceList) > 0 */
+  }
+  for (int i = 0; i < n; i++)
+    if (m->agg_duration_ns[i] == dur_ns && m->agg_present[i][type - 1]) return i;
+  return -1;
+}
+
+static int64_t aggregated_value(const kg_node_metric* m, int i, int64_t type, int r) {
+  return (r < 2 && ((m->agg_present[i][type - 1] >> r) & 1)) ? m->agg_usage[i][type - 1][r] : 0;
+}
+
+/* generateUsageThresholdsFilterProfile's AggregatedUsage (helper.go:102-140): the annotation's when it has
+ * thresholds and a type, else the args' when filterWithAggregation (helper.go:94-96).  Returns 0 for nil. */
+static int aggregated_filter_profile(const kg_config* cfg, const kg_node* node, int64_t thr[KG_RES_MAX],
+                                     int64_t* type, int64_t* dur) {
+  int nargs = 0, ncust = 0;
+  for (int r = 0; r < KG_RES_MAX; r++) {
+    if (cfg->la_agg_usage_thresholds[r] != 0) nargs++;
+    if (node->custom_agg_thresholds[r] >= 0) ncust++;
+  }
+  if ((node->flags & KG_NODE_HAS_CUSTOM_THRESHOLDS) && ncust > 0 && node->custom_agg_type != KG_AGG_NONE) {
+    for (int r = 0; r < KG_RES_MAX; r++) thr[r] = node->custom_agg_thresholds[r] > 0 ? node->custom_agg_thresholds[r] : 0;
+    *type = node->custom_agg_type;
+    *dur = node->custom_agg_duration_ns;
+    return 1;
+  }
+  if (nargs > 0 && cfg->la_agg_usage_type != KG_AGG_NONE) {
+    for (int r = 0; r < KG_RES_MAX; r++) thr[r] = cfg->la_agg_usage_thresholds[r];
+    *type = cfg->la_agg_usage_type;
+    *dur = cfg->la_agg_usage_duration_ns;
+    return 1;
+  }
+  return 0;
+}
+
 /* loadaware/load_aware.go:123-171 Filter (+ filterNodeUsage :173-224, filterProdUsage :226-254) */
 int or_loadaware_filter(const kg_config* cfg, const kg_node* node, const kg_node_metric* m, const kg_pod* pod,
                         int64_t now) {
@@ -134,13 +178,22 @@ int or_loadaware_filter(const kg_config* cfg, const kg_node* node, const kg_node
     }
     return 0;
   }
+  int64_t athr[KG_RES_MAX], atype = 0, adur = 0;
+  const int agg = aggregated_filter_profile(cfg, node, athr, &atype, &adur); /* :157-161 */
+  if (agg) {
+    n_thr = 0;
+    for (int r = 0; r < KG_RES_MAX; r++) n_thr += athr[r] != 0;
+    for (int r = 0; r < KG_RES_MAX; r++) thr[r] = athr[r];
+  }
   if (n_thr == 0) return 0;
   if (!m->has_node_metric) return 0;                       /* :174-176 */
+  const int ai = agg ? target_aggregated(m, adur, atype) : -1;
   for (int r = 0; r < KG_RES_MAX; r++) {                   /* :185-222 */
     if (thr[r] == 0) continue;
     int64_t total = or_estimate_node(node, r);
     if (total == 0) continue;
-    int64_t used = m->node_usage_present[r] ? m->node_usage[r] : 0;
+    if (agg && ai < 0) continue;                           /* :198-209 nodeUsage == nil */
+    int64_t used = agg ? aggregated_value(m, ai, atype, r) : (m->node_usage_present[r] ? m->node_usage[r] : 0);
     volatile double q = (double)milli_of(r, used) / (double)milli_of(r, total);
     volatile double pct = q * 100.0;
     int64_t usage = (int64_t)round(pct);
@@ -172,8 +225,14 @@ int64_t or_loadaware_score(const kg_config* cfg, const kg_node* node, const kg_n
   int64_t used[2];
   for (int r = 0; r < 2; r++) used[r] = est[r] + (prod_pod ? st->la_est_prod[r] : st->la_est_all[r]); /* :298-301 */
   if (!prod_pod && m->has_node_metric) {                                              /* :307-326 */
-    for (int r = 0; r < 2; r++)
-      if (m->node_usage_present[r]) used[r] += m->node_usage[r];
+    if (cfg->la_agg_score_type != KG_AGG_NONE) { /* scoreWithAggregation: the aggregated usage, nil → none */
+      const int i = target_aggregated(m, cfg->la_agg_score_duration_ns, cfg->la_agg_score_type);
+      if (i >= 0)
+        for (int r = 0; r < 2; r++) used[r] += aggregated_value(m, i, cfg->la_agg_score_type, r);
+    } else {
+      for (int r = 0; r < 2; r++)
+        if (m->node_usage_present[r]) used[r] += m->node_usage[r];
+    }
   }
   int64_t node_score = 0, weight_sum = 0;                                             /* :378-386 */
   for (int r = 0; r < 2; r++) {

@@ -11,8 +11,8 @@ Conventions for the LoadAware cases (load_aware_test.go harness :806-908 for Fil
 * Filter harness sets FilterExpiredNodeMetrics=false (:807); Score harness keeps the defaults (expiration 180s);
 * a nil test pod is &corev1.Pod{} (:573-576), whose default priority class is koord-batch (BestEffort → BE,
   apis/extension/priority_utils.go:26-48 + qos_utils.go);
-* scope "core" = restated and accelerated now; scope "next" = needs aggregated usages or PodsMetric-based
-  estimation — kept for completeness, skipped with a reason by the tests.
+* scope "core" = restated and accelerated now (aggregated percentile usages included); scope "next" = needs
+  PodsMetric-based estimation — kept for completeness, skipped with a reason by the tests.
 
 Run: python tests/golden/make_golden.py   (rewrites the JSON files next to this script)
 """
@@ -30,7 +30,7 @@ FILTER_CASES = [
     dict(name="filter node missing NodeMetrics", line=305, metric=None, want="Success"),
     dict(name="filter exceed cpu usage", line=310, metric=dict(update_age_s=0, node_usage={"cpu": "70", "memory": "256Gi"}),
          want="Unschedulable"),
-    dict(name="filter exceed p95 cpu usage", line=338, scope="next",
+    dict(name="filter exceed p95 cpu usage", line=338,
          args=dict(aggregated=dict(usage_thresholds={"cpu": 60}, type="p95", duration="5m")),
          metric=dict(update_age_s=0, node_usage={"cpu": "30", "memory": "100Gi"},
                      aggregated=[dict(duration="5m", p95={"cpu": "70", "memory": "256Gi"})]),
@@ -40,7 +40,7 @@ FILTER_CASES = [
     dict(name="filter exceed memory usage by custom usage thresholds", line=414,
          custom_usage_thresholds={"memory": 60},
          metric=dict(update_age_s=0, node_usage={"cpu": "30", "memory": "316Gi"}), want="Unschedulable"),
-    dict(name="filter exceed p95 cpu usage by custom usage", line=445, scope="next",
+    dict(name="filter exceed p95 cpu usage by custom usage", line=445,
          custom_aggregated=dict(usage_thresholds={"cpu": 60}, type="p95", duration="5m"),
          metric=dict(update_age_s=0, node_usage={"cpu": "30", "memory": "100Gi"},
                      aggregated=[dict(duration="5m", p95={"cpu": "70", "memory": "256Gi"})]),
@@ -86,13 +86,13 @@ SCORE_CASES = [
     dict(name="score node missing NodeMetrics", line=991, pod=dict(requests=G, limits=G), metric=None, want=0),
     dict(name="score load node", line=1020, pod=dict(requests=G, limits=G),
          metric=dict(update_age_s=0, node_usage={"cpu": "32", "memory": "10Gi"}), want=72),
-    dict(name="score load node with p95", line=1072, scope="next", pod=dict(requests=G, limits=G),
+    dict(name="score load node with p95", line=1072, pod=dict(requests=G, limits=G),
          args=dict(score_aggregated=dict(type="p95", duration="5m")),
          metric=dict(update_age_s=0, node_usage={"cpu": "0", "memory": "0Gi"},
-                     aggregated=[dict(duration="5m", p50={"cpu": "32", "memory": "10Gi"},
-                                      p95={"cpu": "50", "memory": "70Gi"})]),
+                     aggregated=[dict(duration="5m", p95={"cpu": "32", "memory": "10Gi"},
+                                      p99={"cpu": "50", "memory": "70Gi"})]),
          want=72),
-    dict(name="score load node with p95 but have not reported usage", line=1147, scope="next",
+    dict(name="score load node with p95 but have not reported usage", line=1147,
          pod=dict(requests=G, limits=G), args=dict(score_aggregated=dict(type="p95", duration="5m")),
          metric=dict(update_age_s=0, node_usage={"cpu": "0", "memory": "0Gi"}), want=90),
     dict(name="score load node with p95 but have not reported usage and have assigned pods", line=1203, scope="next",

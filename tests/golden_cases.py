@@ -37,6 +37,15 @@ def la_args(doc, case):
         a.prod_usage_thresholds = dict(args["prod_usage_thresholds"])
     if "score_according_prod_usage" in args:
         a.score_according_prod_usage = args["score_according_prod_usage"]
+    agg = {}
+    if "aggregated" in args:  # LoadAwareSchedulingAggregatedArgs for Filter
+        g = args["aggregated"]
+        agg.update(usage_thresholds=dict(g["usage_thresholds"]), usage_type=g["type"],
+                   usage_duration_s=duration_s(g.get("duration")))
+    if "score_aggregated" in args:
+        g = args["score_aggregated"]
+        agg.update(score_type=g["type"], score_duration_s=duration_s(g.get("duration")))
+    a.aggregated = agg or None
     if "factors" in case:  # SetDefaults fills the missing scaling-factor keys (v1beta2/defaults.go:92-98)
         f = {"cpu": 85, "memory": 70}
         f.update(case["factors"])
@@ -48,10 +57,21 @@ def config(doc, case, profile=None, **kw):
     return framework.build_config(la=la_args(doc, case), profile=profile, **kw)
 
 
+def duration_s(d) -> int:
+    """metav1.Duration strings of the fixtures ("5m", "30s", "1h"); None → 0 (nil)."""
+    if not d:
+        return 0
+    return int(d[:-1]) * {"s": 1, "m": 60, "h": 3600}[d[-1]]
+
+
 def node(doc, case):
+    ca = case.get("custom_aggregated")
+    custom_agg = None if ca is None else dict(usage_thresholds=dict(ca["usage_thresholds"]), usage_type=ca["type"],
+                                              usage_duration_s=duration_s(ca.get("duration")))
     return framework.make_node(doc.get("node_allocatable", {}),
                                custom_usage_thresholds=case.get("custom_usage_thresholds"),
-                               custom_prod_usage_thresholds=case.get("custom_prod_usage_thresholds"))
+                               custom_prod_usage_thresholds=case.get("custom_prod_usage_thresholds"),
+                               custom_aggregated=custom_agg)
 
 
 def metric(case):
@@ -62,7 +82,9 @@ def metric(case):
     return framework.make_node_metric(
         present=True, update_time_ns=None if age is None else NOW_NS - age * 10**9,
         node_usage=m.get("node_usage"), prod_pods_usage=m.get("prod_pods_usage"),
-        pods_metric_count=m.get("pods_metric_count", len(m.get("pods_metric", []))))
+        pods_metric_count=m.get("pods_metric_count", len(m.get("pods_metric", []))),
+        aggregated=[dict({k: v for k, v in a.items() if k != "duration"}, duration_s=duration_s(a.get("duration")))
+                    for a in m.get("aggregated", [])])
 
 
 def pod(spec):
