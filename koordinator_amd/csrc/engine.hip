@@ -558,15 +558,24 @@ __device__ __forceinline__ void publish_round(int64_t* ctl, int64_t seq) {
   if (threadIdx.x == 0) __hip_atomic_store(&ctl[4], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// exact key of one modified row for pod p (0 = filtered out)
+// exact key of one modified row for pod p (0 = filtered out).  A row outside eval_fast's domain takes the
+// reference-shaped eval_node with the EvalParams copy in LDS behind an opaque pointer: its runtime weight / flag
+// tests then stay inside the (rare) branch instead of being hoisted as loop-invariant scalar masks that crowd the
+// resolver's scalar registers.
+constexpr int kParWords = (int)((sizeof(EvalParams) + 7) / 8);
 template <int PF>
-__device__ __forceinline__ uint64_t mod_key(const EvalRow& er, uint32_t node, const DevPod& p, const EvalParams& P) {
+__device__ __forceinline__ uint64_t mod_key(const EvalRow& er, uint32_t node, const DevPod& p, const EvalParams& P,
+                                            const uint64_t* s_par) {
   uint32_t t = 0;
   bool rare = false;
   bool ok = eval_fast<PF>(er, p, P, t, rare);
   if (rare) {
+    const uint64_t* q = s_par;
+    asm volatile("" : "+v"(q));
+    EvalParams Pr;
+    __builtin_memcpy(&Pr, q, sizeof(Pr));
     int64_t t64 = 0;
-    ok = eval_node(row_of(er), p, P, t64);
+    ok = eval_node(row_of(er), p, Pr, t64);
     t = (uint32_t)t64;
   }
   return ok ? make_key(t, node) : 0;
@@ -581,121 +590,52 @@ __device__ __forceinline__ EvalRow lds_row(const uint64_t* src) {
   return er;
 }
 
-// Σ of the pods assumed onto a row since its base state (NodeInfo.AddPod + podAssignCache.assign terms)
-struct PodDelta {
-  int64_t req_cpu, req_mem, nz_cpu, nz_mem, est_cpu, est_mem, pest_cpu, pest_mem;
-  int32_t pods;
-};
-__device__ __forceinline__ void add_delta(PodDelta& d, const DevPod& p) {
-  const int64_t prod = (p.flags & P_PROD) ? 1 : 0;
-  d.req_cpu += p.req_cpu;
-  d.req_mem += p.req_mem;
-  d.nz_cpu += p.nz_cpu;
-  d.nz_mem += p.nz_mem;
-  d.est_cpu += p.est_cpu;
-  d.est_mem += p.est_mem;
-  d.pest_cpu += prod * p.est_cpu;
-  d.pest_mem += prod * p.est_mem;
-  d.pods += 1;
-}
-__device__ __forceinline__ Row with_delta(Row r, const PodDelta& d) {
-  r.req_cpu += d.req_cpu;
-  r.req_mem += d.req_mem;
-  r.nz_cpu += d.nz_cpu;
-  r.nz_mem += d.nz_mem;
-  r.la_used_cpu += d.est_cpu;
-  r.la_used_mem += d.est_mem;
-  r.la_pused_cpu += d.pest_cpu;
-  r.la_pused_mem += d.pest_mem;
-  r.num_pods += d.pods;
-  return r;
-}
-
-// One modified row held by a lane: its hoisted EvalRow (from a merge record's shipped rows, or converted from HBM)
-// + the pods assumed since it was last brought up to date.  The assume on the serial chain is a few adds into
-// `dl`; the row absorbs them (apply_delta) only when a later pod has to re-score it.
+// One modified row held by a lane: its node and hoisted terms, kept current by assume_mod on every placement (the
+// owner lane only).  A node that wins while unmodified takes a new slot lazily: `pend` = (j << 8) | pos records the
+// placing pod j and the winner's position in pod j's record, and the row is brought in (shipped record row, or HBM
+// beyond the staged rows) and assumed only when a later pod has to re-score the modified rows — all pending lanes
+// at once (mod_row_settle).  The table write-back happens once per round, per placed pod (epilogue atomics).
 constexpr uint32_t kNoNode = 0xFFFFFFFFu;
-struct LaneRow {
+struct ModRow {
   uint32_t node;
-  bool pending, touched;
+  int32_t pend;  // -1: er is current
   EvalRow er;
-  PodDelta dl;   // assumed since `er` was last brought up to date
-  PodDelta tot;  // assumed in this round (written back exactly: int64 adds onto the table columns)
 };
-__device__ __forceinline__ void lane_row_init(LaneRow& L) {
-  L.node = kNoNode;
-  L.pending = false;
-  L.touched = false;
-  L.er.flags = 0;
-  L.dl = PodDelta{};
-  L.tot = PodDelta{};
-}
-// assume of Σ dl on a hoisted row: the free terms drop (capacities and reciprocals unchanged), so the exact domain
-// of eval_fast can only be left through the lower bounds of the free terms the profile scores
-__device__ __forceinline__ void apply_delta(EvalRow& e, const PodDelta& d, const EvalParams& P) {
-  e.free_cpu -= d.req_cpu;
-  e.free_mem -= d.req_mem;
-  e.fnz_cpu -= d.nz_cpu;
-  e.fnz_mem -= (double)d.nz_mem;
-  e.la_free_cpu -= d.est_cpu;
-  e.la_free_mem -= (double)d.est_mem;
-  e.la_pfree_cpu -= d.pest_cpu;
-  e.la_pfree_mem -= (double)d.pest_mem;
-  e.pods_left -= d.pods;
-  bool out = false;
-  if (P.fit_score) out |= (P.fit_w_cpu && e.fnz_cpu < kCpuFreeMin) | (P.fit_w_mem && !(e.fnz_mem > (double)kMemFreeMin));
-  if (P.la_score && (e.flags & F_LA_SCORE)) {
-    out |= P.la_w_cpu && (e.la_free_cpu < kCpuFreeMin || e.la_pfree_cpu < kCpuFreeMin);
-    out |= P.la_w_mem && (!(e.la_free_mem > (double)kMemFreeMin) || !(e.la_pfree_mem > (double)kMemFreeMin));
-  }
-  if (out) e.flags |= F_RARE;
-}
-// a new modified row for winner w of pod j, listed at position pos of its record
-__device__ __forceinline__ void lane_row_new(LaneRow& L, const DevTable& T, const uint64_t* s_cand, uint32_t w, int j,
-                                             int pos, const DevPod& p, const EvalParams& P) {
-  L.node = w;
-  if (pos < kStaged) L.er = lds_row(s_cand + (size_t)j * kCandStride + kRecRows + pos * kEvalRowWords);
-  else L.er = make_eval_row(load_row(T, w), P);  // beyond the shipped rows (rare): HBM
-  L.dl = PodDelta{};
-  add_delta(L.dl, p);
-  L.tot = L.dl;
-  L.pending = true;
-  L.touched = true;
-}
-__device__ __forceinline__ void lane_row_assume(LaneRow& L, const DevPod& p) {
-  add_delta(L.dl, p);
-  add_delta(L.tot, p);
-  L.pending = true;
-  L.touched = true;
-}
-// write-back of a touched row: this round's Σ onto the table columns (no other writer: the earlier rounds'
-// resolvers are done, later rounds' resolvers wait for this one; concurrent wide passes read mixed columns)
-__device__ __forceinline__ void lane_row_store(const LaneRow& L, const DevTable& T) {
-  if (!L.touched) return;
-  const int64_t i = L.node;
-  auto add = [](int64_t* a, int64_t v) { atomicAdd(reinterpret_cast<unsigned long long*>(a), (unsigned long long)v); };
-  add(&T.req_cpu[i], L.tot.req_cpu);
-  add(&T.req_mem[i], L.tot.req_mem);
-  add(&T.nz_cpu[i], L.tot.nz_cpu);
-  add(&T.nz_mem[i], L.tot.nz_mem);
-  add(&T.la_used_cpu[i], L.tot.est_cpu);
-  add(&T.la_used_mem[i], L.tot.est_mem);
-  add(&T.la_pused_cpu[i], L.tot.pest_cpu);
-  add(&T.la_pused_mem[i], L.tot.pest_mem);
-  atomicAdd(&T.num_pods[i], L.tot.pods);
-}
-__device__ __forceinline__ void lane_row_sync(LaneRow& L, const EvalParams& P) {
-  if (L.pending) {
-    apply_delta(L.er, L.dl, P);
-    L.dl = PodDelta{};
-    L.pending = false;
-  }
+__device__ __forceinline__ void mod_row_init(ModRow& m) {
+  m.node = kNoNode;
+  m.pend = -1;
+  m.er.flags = 0;
 }
 template <int PF>
-__device__ __forceinline__ uint64_t lane_row_key(LaneRow& L, const DevPod& p, const EvalParams& P) {
-  if (L.node == kNoNode) return 0;
-  lane_row_sync(L, P);
-  return mod_key<PF>(L.er, L.node, p, P);
+__device__ __forceinline__ uint64_t mod_row_key(const ModRow& m, const DevPod& p, const EvalParams& P,
+                                                const uint64_t* s_par) {
+  return m.node == kNoNode ? 0 : mod_key<PF>(m.er, m.node, p, P, s_par);
+}
+
+// assume(pod) on a modified row (NodeInfo.AddPod + LoadAware Reserve → podAssignCache.assign): only the free terms
+// move, and only downwards, so eval_fast's exact domain can be left only through the lower bounds of the free terms
+// the profile scores (the same test as rare_bit's, without its capacity compares or f64 → int64 conversions).
+template <int PF>
+__device__ __forceinline__ void assume_mod(EvalRow& e, const DevPod& p, const EvalParams& P) {
+  const bool prod = (p.flags & P_PROD) != 0;
+  e.free_cpu -= p.req_cpu;
+  e.free_mem -= p.req_mem;
+  e.fnz_cpu -= p.nz_cpu;
+  e.fnz_mem -= p.nz_mem_d;
+  e.la_free_cpu -= p.est_cpu;
+  e.la_free_mem -= p.est_mem_d;
+  e.la_pfree_cpu -= prod ? p.est_cpu : 0;
+  e.la_pfree_mem -= prod ? p.est_mem_d : 0.0;
+  e.pods_left -= 1;
+  bool out = false;
+  // (whatever the weights: F_RARE only sends the row to the exact path, so marking it for a zero-weight term is safe)
+  if constexpr ((PF & PF_FIT_SCORE) != 0) out |= (e.fnz_cpu < kCpuFreeMin) | !(e.fnz_mem > (double)kMemFreeMin);
+  if constexpr ((PF & PF_LA_SCORE) != 0) {
+    if (e.flags & F_LA_SCORE)
+      out |= (e.la_free_cpu < kCpuFreeMin) | (e.la_pfree_cpu < kCpuFreeMin) | !(e.la_free_mem > (double)kMemFreeMin) |
+             !(e.la_pfree_mem > (double)kMemFreeMin);
+  }
+  if (out) e.flags |= F_RARE;
 }
 
 // wave max of packed keys: one 32-bit DPP max when (score, node) fit 13 + 19 bits, else the two-word form
@@ -708,8 +648,71 @@ __device__ __forceinline__ uint64_t wave_max_modkey(uint64_t k, bool narrow) {
   return wave_max_key(k);
 }
 
+// Round write-back: lane j < consumed adds placed pod j's NodeInfo.AddPod + podAssignCache.assign terms onto its
+// winner's columns (int64 atomics: several pods of the round may share a winner; no other writer — earlier rounds'
+// resolvers are done, later ones wait for this one; concurrent wide passes read mixed columns).
+__device__ __forceinline__ void writeback_pod(const DevTable& T, uint32_t node, const DevPod& p) {
+  const int64_t i = node;
+  const int64_t prod = (p.flags & P_PROD) ? 1 : 0;
+  auto add = [](int64_t* a, int64_t v) { atomicAdd(reinterpret_cast<unsigned long long*>(a), (unsigned long long)v); };
+  add(&T.req_cpu[i], p.req_cpu);
+  add(&T.req_mem[i], p.req_mem);
+  add(&T.nz_cpu[i], p.nz_cpu);
+  add(&T.nz_mem[i], p.nz_mem);
+  add(&T.la_used_cpu[i], p.est_cpu);
+  add(&T.la_used_mem[i], p.est_mem);
+  if (prod) {
+    add(&T.la_pused_cpu[i], p.est_cpu);
+    add(&T.la_pused_mem[i], p.est_mem);
+  }
+  atomicAdd(&T.num_pods[i], 1);
+}
+
+// The node table's columns are carved from two allocations (kg_engine: cols64 = 12 int64 columns + inv_mem[2],
+// cols32 = alloc_pods, num_pods, flags, inv_cpu[2]), so a DevTable is (c64, c32, cap).  The single-wave resolvers
+// rebuild it where a column is touched: the bases pass through an opaque asm so the 19 derived column addresses are
+// not kept live in scalar registers across the per-pod loop (they spilled, costing v_readlane on the serial chain).
+__device__ __forceinline__ DevTable table_at(const DevTable& T0) {
+  int64_t* c64 = T0.alloc_cpu;
+  int32_t* c32 = T0.alloc_pods;
+  int64_t cap = T0.cap;
+  asm volatile("" : "+s"(c64), "+s"(c32), "+s"(cap));
+  DevTable T;
+  T.alloc_cpu = c64 + 0 * cap;
+  T.alloc_mem = c64 + 1 * cap;
+  T.req_cpu = c64 + 2 * cap;
+  T.req_mem = c64 + 3 * cap;
+  T.nz_cpu = c64 + 4 * cap;
+  T.nz_mem = c64 + 5 * cap;
+  T.la_alloc_cpu = c64 + 6 * cap;
+  T.la_alloc_mem = c64 + 7 * cap;
+  T.la_used_cpu = c64 + 8 * cap;
+  T.la_used_mem = c64 + 9 * cap;
+  T.la_pused_cpu = c64 + 10 * cap;
+  T.la_pused_mem = c64 + 11 * cap;
+  T.inv_mem = reinterpret_cast<double*>(c64 + 12 * cap);
+  T.alloc_pods = c32 + 0 * cap;
+  T.num_pods = c32 + 1 * cap;
+  T.flags = reinterpret_cast<uint32_t*>(c32 + 2 * cap);
+  T.inv_cpu = reinterpret_cast<float*>(c32 + 3 * cap);
+  T.cap = cap;
+  return T;
+}
+
+template <int PF>
+__device__ __forceinline__ void mod_row_settle(ModRow& R, const uint64_t* s_cand, const DevPod* s_pods, const DevTable& T0,
+                                               const EvalParams& P) {
+  if (R.pend >= 0) {
+    const int pj = R.pend >> 8, ppos = R.pend & 0xFF;
+    if (ppos < kStaged) R.er = lds_row(s_cand + (size_t)pj * kCandStride + kRecRows + ppos * kEvalRowWords);
+    else R.er = make_eval_row(load_row(table_at(T0), R.node), P);
+    assume_mod<PF>(R.er, s_pods[pj], P);
+    R.pend = -1;
+  }
+}
+
 template <int PF, bool QUOTA>
-__global__ __launch_bounds__(kWave) void resolve_round(DevTable T, const DevPod* __restrict__ pods,
+__global__ __launch_bounds__(kWave) void resolve_round(DevTable T0, const DevPod* __restrict__ pods,
                                                         int64_t* __restrict__ ctl, int64_t first, int nb,
                                                         const uint64_t* __restrict__ cand, EvalParams P,
                                                         uint64_t* __restrict__ out_keys, int bitmap_words,
@@ -723,9 +726,17 @@ __global__ __launch_bounds__(kWave) void resolve_round(DevTable T, const DevPod*
   __builtin_amdgcn_s_setprio(3);
   uint64_t* s_cand = smem;                                            // [nb][kCandStride]
   uint64_t* s_podw = s_cand + (size_t)nb * kCandStride;               // [nb] DevPod (kPodWords words)
-  uint32_t* s_hash = reinterpret_cast<uint32_t*>(s_podw + (size_t)nb * kPodWords);  // [kModHash]
+  uint64_t* s_par = s_podw + (size_t)nb * kPodWords;                  // [kParWords] EvalParams (rare-path copy)
+  uint32_t* s_hash = reinterpret_cast<uint32_t*>(s_par + kParWords);  // [kModHash]
   uint32_t* s_prevn = s_hash + kModHash;                              // [kMaxMod] earlier rounds' nodes
   uint32_t* bitmap = s_prevn + kMaxMod;                               // [bitmap_words]
+  {
+    uint64_t pw[kParWords] = {};
+    __builtin_memcpy(pw, &P, sizeof(P));
+#pragma unroll
+    for (int q = 0; q < kParWords; ++q)
+      if (lane == q) s_par[q] = pw[q];
+  }
   {  // prologue, independent of the previous round: LDS-DMA of this round's records (merged on this stream)
      // + pods, bitmap / hash clears (16-B stores)
     const int n16 = nb * kCandStride / 2;
@@ -775,9 +786,9 @@ __global__ __launch_bounds__(kWave) void resolve_round(DevTable T, const DevPod*
     return;
   }
   // rows the n_prev previous rounds modified: slots [0, nM) of the register banks (slot s: lane s % 64, bank s / 64)
-  LaneRow R0, R1;
-  lane_row_init(R0);
-  lane_row_init(R1);
+  ModRow R0, R1;
+  mod_row_init(R0);
+  mod_row_init(R1);
   int nM = 0;
   for (int d = 1; d <= n_prev; ++d) {  // concatenate the lists in LDS, then slot s → lane s % 64, bank s / 64
     const int32_t* ml = modlists + (size_t)(((slot - d) % depth + depth) % depth) * kModListStride;
@@ -790,7 +801,7 @@ __global__ __launch_bounds__(kWave) void resolve_round(DevTable T, const DevPod*
     const uint32_t node = s_prevn[lane];
     if (mod_insert(s_hash, node, lane) == lane) {
       R0.node = node;
-      R0.er = make_eval_row(load_row(T, node), P);
+      R0.er = make_eval_row(load_row(table_at(T0), node), P);
       atomicOr(&bitmap[node >> 5], 1u << (node & 31));
     }
   }
@@ -798,7 +809,7 @@ __global__ __launch_bounds__(kWave) void resolve_round(DevTable T, const DevPod*
     const uint32_t node = s_prevn[kWave + lane];
     if (mod_insert(s_hash, node, kWave + lane) == kWave + lane) {
       R1.node = node;
-      R1.er = make_eval_row(load_row(T, node), P);
+      R1.er = make_eval_row(load_row(table_at(T0), node), P);
       atomicOr(&bitmap[node >> 5], 1u << (node & 31));
     }
   }
@@ -812,96 +823,110 @@ __global__ __launch_bounds__(kWave) void resolve_round(DevTable T, const DevPod*
   uint64_t my_out = 0;
   int consumed = 0, n_slow = 0;
   uint32_t last_w = kNoNode;
-  uint64_t key_n = s_cand[lane];
-  uint64_t ub_n = s_cand[kC];
-  DevPod p_n = s_pods[0];
-  uint32_t word_n = bitmap[key_n ? key_node(key_n) >> 5 : 0u];
+  // software pipeline: pod j's key / ub / record and bitmap word are in registers when pod j starts; pod j+1's key
+  // was loaded one pod earlier, so its bitmap word issues without waiting on LDS (it misses pod j's own winner,
+  // which the next pod patches with last_w)
+  uint64_t key = s_cand[lane];
+  uint64_t ub = s_cand[kC];
+  // pod records come through the scalar cache (wave-uniform, straight into scalar registers; no LDS round trip and
+  // no v_readfirstlane on the chain); the LDS copy serves the lane-parallel epilogue
+  typedef const __attribute__((address_space(4))) uint64_t* const_u64_ptr;  // constant address space: s_load
+  const const_u64_ptr gpods = (const_u64_ptr)(uintptr_t)(pods + first);
+  auto pod_at = [&](int q) {
+    uint64_t w[kPodWords];
+#pragma unroll
+    for (int k = 0; k < kPodWords; ++k) w[k] = gpods[(size_t)q * kPodWords + k];
+    DevPod d;
+    __builtin_memcpy(&d, w, sizeof(d));
+    return d;
+  };
+
+  uint32_t word = bitmap[key ? key_node(key) >> 5 : 0u];
+  uint64_t key_n = s_cand[(size_t)(nb > 1 ? 1 : 0) * kCandStride + lane];
   uint32_t diag = 0;
   for (int j = 0; j < nb; ++j) {
     KG_POD_DIAG(j, diag);
     diag = 0;
-    const uint64_t key = key_n, ub = ub_n;
-    const DevPod p = p_n;
-    const uint32_t word = word_n;
-    const int jn = j + 1 < nb ? j + 1 : j;  // software prefetch of the next pod (branch-free)
-    key_n = s_cand[(size_t)jn * kCandStride + lane];
-    ub_n = s_cand[(size_t)jn * kCandStride + kC];
-    p_n = s_pods[jn];
+    const int j1 = j + 1 < nb ? j + 1 : j, j2 = j + 2 < nb ? j + 2 : j1;
+    const uint32_t word_n = bitmap[key_n ? key_node(key_n) >> 5 : 0u];
+    const uint64_t ub_n = s_cand[(size_t)j1 * kCandStride + kC];
+    const uint64_t key_nn = s_cand[(size_t)j2 * kCandStride + lane];
+    const DevPod p = pod_at(j);  // scalar cache: the queue is read in order, so the line is usually warm
     const uint32_t node = key_node(key);  // key 0 → node 0xFFFFFFFF: masked below
-    // the prefetched word predates the previous pod's bitmap update: patch with its winner
     const bool unmod = (key != 0) & !((word >> (node & 31)) & 1u) & (node != last_w);
-    word_n = bitmap[key_n ? key_node(key_n) >> 5 : 0u];
-    if (QUOTA && !quota_admit(ql, p)) {  // ElasticQuota PreFilter rejects: Unschedulable, no node search
+    bool placed = false;
+    uint32_t w = kNoNode;
+    if (!QUOTA || quota_admit(ql, p)) {  // ElasticQuota PreFilter rejects: Unschedulable, no node search
+      const uint64_t um = __ballot(unmod);
+      const int pos = um ? (int)__builtin_ctzll(um) : kC;
+      uint64_t best = um ? readlane_u64(key, pos) : 0;
+      diag = (uint32_t)pos << 8;
+      KG_POD_SUB(j, 0);
+      bool from_mod = false;
+      if (nM > 0 && pos > 0) {  // a modified node is listed above e: re-score the modified rows exactly
+        ++n_slow;
+        diag |= 1;
+        mod_row_settle<PF>(R0, s_cand, s_pods, T0, P);
+        uint64_t mk = mod_row_key<PF>(R0, p, P, s_par);
+        if (nM > kWave) {
+          mod_row_settle<PF>(R1, s_cand, s_pods, T0, P);
+          const uint64_t k1 = mod_row_key<PF>(R1, p, P, s_par);
+          mk = k1 > mk ? k1 : mk;
+        }
+        const uint64_t mbest = wave_max_modkey(mk, narrow);
+        from_mod = mbest > best;
+        best = from_mod ? mbest : best;
+      }
+      if (best < ub) break;  // an unseen node could still win: leave this pod to the next round
+      KG_POD_SUB(j, 1);
+      my_out = lane == j ? best : my_out;
+      if (best != 0) {  // 0: unschedulable (ub == 0: no feasible node anywhere)
+        placed = true;
+        w = key_node(best);
+        // assume (NodeInfo.AddPod + LoadAware Reserve: podAssignCache.assign): onto the winner's settled row when it
+        // is a modified node, else a new pending slot (e, at position pos of pod j's record)
+        if (from_mod) {
+          if (R0.node == w) assume_mod<PF>(R0.er, p, P);
+          if (R1.node == w) assume_mod<PF>(R1.er, p, P);
+        } else {
+          diag |= 2;
+          const int sl = nM++;
+          const int pend = (j << 8) | pos;
+          if (sl < kWave) {
+            if (lane == sl) R0.node = w, R0.pend = pend;
+          } else if (lane == sl - kWave) {
+            R1.node = w, R1.pend = pend;
+          }
+          if (lane == (sl & (kWave - 1))) atomicOr(&bitmap[w >> 5], 1u << (w & 31));
+        }
+        KG_POD_SUB(j, 2);
+      }
+    } else {
       my_out = lane == j ? 0 : my_out;
-      ++consumed;
-      last_w = kNoNode;
-      continue;
     }
-    const uint64_t um = __ballot(unmod);
-    const int pos = um ? (int)__builtin_ctzll(um) : kC;
-    uint64_t best = um ? readlane_u64(key, pos) : 0;
-    diag = (uint32_t)pos << 8;
-    if (nM > 0 && pos > 0) {  // a modified node is listed above e: re-score the modified rows exactly
-      ++n_slow;
-      diag |= 1;
-      // only the modified nodes listed above e can beat it (a modified node reads ≤ its listed key; unlisted < ub):
-      // lanes whose row is one of the candidates at positions < pos re-score it, the others sit out
-      bool a0 = false, a1 = false;
-      for (int q = 0; q < pos; ++q) {
-        const uint32_t c = key_node(readlane_u64(key, q));
-        a0 |= R0.node == c;
-        a1 |= R1.node == c;
-      }
-      uint64_t mk = 0;
-      if (__ballot(a0)) mk = a0 ? lane_row_key<PF>(R0, p, P) : 0;
-      if (__ballot(a1)) {
-        const uint64_t k1 = a1 ? lane_row_key<PF>(R1, p, P) : 0;
-        mk = k1 > mk ? k1 : mk;
-      }
-      const uint64_t mbest = wave_max_modkey(mk, narrow);
-      best = mbest > best ? mbest : best;
-    }
-    if (best < ub) break;  // an unseen node could still win: leave this pod to the next round
-    my_out = lane == j ? best : my_out;
+    if (QUOTA && placed) quota_charge(ql, p, lane);  // ElasticQuota Reserve
     ++consumed;
-    if (best == 0) {  // unschedulable (ub == 0: no feasible node anywhere)
-      last_w = kNoNode;
-      continue;
-    }
-    const uint32_t w = key_node(best);
     last_w = w;
-    const uint64_t h0 = __ballot(R0.node == w), h1 = __ballot(R1.node == w);
-    if (h0 | h1) {  // assume onto the modified row: NodeInfo.AddPod + LoadAware Reserve (podAssignCache.assign)
-      if (h0) {
-        if (lane == (int)__builtin_ctzll(h0)) lane_row_assume(R0, p);
-      } else if (lane == (int)__builtin_ctzll(h1)) {
-        lane_row_assume(R1, p);
-      }
-    } else {  // w = e, unmodified: a new slot based on its row shipped in the record (HBM beyond the staged rows)
-      diag |= 2;
-      const int s = nM++;
-      if (lane == (s & (kWave - 1))) {
-        if (s < kWave) lane_row_new(R0, T, s_cand, w, j, pos, p, P);
-        else lane_row_new(R1, T, s_cand, w, j, pos, p, P);
-        atomicOr(&bitmap[w >> 5], 1u << (w & 31));
-      }
-    }
-    if (QUOTA) quota_charge(ql, p, lane);  // ElasticQuota Reserve
+    key = key_n;
+    key_n = key_nn;
+    ub = ub_n;
+    word = word_n;
   }
   KG_STAMP(2, 30);
   KG_POD_DIAG(consumed, diag);
-  // write-back of the touched rows + this round's modified-row list
-  lane_row_store(R0, T);
-  lane_row_store(R1, T);
+  // write-back: each placed pod's terms onto its winner + this round's modified-row list (winners, duplicates
+  // allowed: the next resolver's hash keeps one slot per node)
+  const bool mine = lane < consumed && my_out != 0;
+  const uint32_t my_node = mine ? key_node(my_out) : kNoNode;
+  if (mine) writeback_pod(table_at(T0), my_node, s_pods[lane]);
   int32_t* my_mod = modlists + (size_t)slot * kModListStride;
   const uint64_t lane_lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  const uint64_t b0 = __ballot(R0.touched), b1 = __ballot(R1.touched);
-  if (R0.touched) my_mod[1 + __popcll(b0 & lane_lt)] = (int32_t)R0.node;
-  if (R1.touched) my_mod[1 + __popcll(b0) + __popcll(b1 & lane_lt)] = (int32_t)R1.node;
+  const uint64_t bm = __ballot(mine);
+  if (mine) my_mod[1 + __popcll(bm & lane_lt)] = (int32_t)my_node;
   if (lane < consumed) out_keys[first + lane] = my_out;
   if (QUOTA) quota_store(quotas, nq, lane, ql);
   if (lane == 0) {
-    my_mod[0] = __popcll(b0) + __popcll(b1);
+    my_mod[0] = __popcll(bm);
     ctl[0] = first + consumed;
     ctl[1] += 1;
     ctl[2] += consumed;
@@ -2484,7 +2509,8 @@ RoundGeom geometry(const kg_engine* e) {
 }
 
 size_t resolve_lds_bytes(const RoundGeom& g, int nb) {
-  return (size_t)nb * (kCandStride + kPodWords) * 8 + (size_t)(kModHash + kMaxMod) * 4 + (size_t)g.bitmap_words * 4;
+  return ((size_t)nb * (kCandStride + kPodWords) + kParWords) * 8 + (size_t)(kModHash + kMaxMod) * 4 +
+         (size_t)g.bitmap_words * 4;
 }
 constexpr size_t kMaxLds = 160 * 1024;
 size_t resolve_numa_lds_bytes(const RoundGeom& g, int nb) {
@@ -2503,8 +2529,16 @@ int profile_bits(const EvalParams& P) {
          (P.la_score ? PF_LA_SCORE : 0) | (P.la_score && P.la_prod_score ? PF_LA_PROD : 0);
 }
 
+#ifdef KG_DEV_PF  // iteration builds only (make dev): one profile instantiated, every other one refused at run time
+#define KG_PF_SWITCH(pf, CALL) \
+  if ((pf) == KG_DEV_PF) {     \
+    CALL(KG_DEV_PF);           \
+  } else {                     \
+    std::abort();              \
+  }
+#else
 #define KG_PF_SWITCH(pf, CALL)                                                                   \
-  switch (pf) {                                                                                  \
+  switch (pf) {                                                                                \
     case 0: CALL(0); break;   case 1: CALL(1); break;   case 2: CALL(2); break;   case 3: CALL(3); break;     \
     case 4: CALL(4); break;   case 5: CALL(5); break;   case 6: CALL(6); break;   case 7: CALL(7); break;     \
     case 8: CALL(8); break;   case 9: CALL(9); break;   case 10: CALL(10); break; case 11: CALL(11); break;   \
@@ -2512,6 +2546,7 @@ int profile_bits(const EvalParams& P) {
     case 24: CALL(24); break; case 25: CALL(25); break; case 26: CALL(26); break; case 27: CALL(27); break;   \
     case 28: CALL(28); break; case 29: CALL(29); break; case 30: CALL(30); break; case 31: CALL(31); break;   \
   }
+#endif
 
 int32_t* poison_ptr(kg_engine* e) { return reinterpret_cast<int32_t*>(e->cursor.p + 3); }
 uint64_t* lists_slot(kg_engine* e, const RoundGeom& g, int slot) {

@@ -31,7 +31,7 @@ __device__ unsigned long long g_stamps[4][32][2];
     }                                                                              \
   } while (0)
 // per-pod diagnostics of the last resolver launch: cycle stamp + path bits
-__device__ unsigned long long g_pod_diag[64][2];
+__device__ unsigned long long g_pod_diag[64][6];
 #define KG_POD_DIAG(j, bits)                                                       \
   do {                                                                             \
     if (threadIdx.x == 0 && (j) < 64) {                                            \
@@ -39,9 +39,17 @@ __device__ unsigned long long g_pod_diag[64][2];
       g_pod_diag[j][1] = (bits);                                                   \
     }                                                                              \
   } while (0)
+// sub-phase stamp k (0..3) of pod j
+#define KG_POD_SUB(j, k)                                                           \
+  do {                                                                             \
+    if (threadIdx.x == 0 && (j) < 64) g_pod_diag[j][2 + (k)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
 #else
 #define KG_POD_DIAG(j, bits) \
   do {                       \
+  } while (0)
+#define KG_POD_SUB(j, k) \
+  do {                   \
   } while (0)
 #define KG_STAMP(kern, point) \
   do {                        \

@@ -4,7 +4,7 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-os.environ["KOORDGPU_LIB"] = os.path.join(ROOT, "koordinator_amd", "libkoordgpu_stamps.so")
+os.environ["KOORDGPU_LIB"] = os.path.join(ROOT, "koordinator_amd", os.environ.get("STAMPS_LIB", "libkoordgpu_stamps.so"))
 sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 
@@ -23,10 +23,10 @@ with Engine(cfg, n) as e:
     e.profile(True)
     st = e.schedule_staged(0, npods)
     prof = e.profile_read()
-    buf = np.zeros(4 * 32 * 2 + 64 * 2, dtype=np.uint64)
+    buf = np.zeros(4 * 32 * 2 + 64 * 6, dtype=np.uint64)
     abi.check(e.lib, e.lib.kg_debug_stamps(e.h, abi.ptr(buf)))
     stamps = buf[:256].reshape(4, 32, 2)
-    diag = buf[256:].reshape(64, 2)
+    diag = buf[256:256 + 384].reshape(64, 6)
 print(f"nodes={n} pods={npods} depth={depth} batch={batch}: rounds={int(st['device_batches'])} "
       f"slow={st['reserved'][0]:.0f} steps={st['reserved'][1]:.0f} seconds={st['seconds']:.4f} "
       f"pods/s={npods / st['seconds']:.0f}")
@@ -49,5 +49,6 @@ for j in range(64):
     if not c:
         break
     if prev is not None:
-        print(f"  pod {j - 1:2d}: {c - prev:6d} cyc pos={b >> 8:2d} slow={b & 1} new={(b >> 1) & 1}")
+        sub = " ".join(f"{int(diag[j - 1, 2 + k]) - prev if diag[j - 1, 2 + k] else -1:5d}" for k in range(4))
+        print(f"  pod {j - 1:2d}: {c - prev:6d} cyc pos={b >> 8:2d} slow={b & 1} new={(b >> 1) & 1}  sub {sub}")
     prev = c
