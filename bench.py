@@ -62,6 +62,7 @@ def parse():
     ap.add_argument("--depth", type=int, default=0, help="pipeline depth (rounds in flight; 0 = engine default)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of each CPU baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-nproc", action="store_true", help="also time the oracle with os.cpu_count() threads")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel-iters", type=int, default=20)
     ap.add_argument("--profile-pods", type=int, default=None, help="pods scheduled with live kernel timing after "
@@ -342,6 +343,10 @@ def main():
                          f"host nproc={os.cpu_count()} (the GPU box's CPU share is 16 threads per GPU)",
                "node_evals_per_sec": m * cluster.n / dt,
                "single_thread": {"value": m1 / dt1, "sample_pods": m1}}
+        nproc = os.cpu_count() or threads
+        if args.cpu_nproc and nproc > threads:  # §8d: the Parallelizer widened to every host thread as well
+            mn, dtn, _ = cpu_sample(work, pods[:total], args.cpu_seconds / 2, nproc)
+            cpu["nproc_threads"] = {"value": mn / dtn, "threads": nproc, "sample_pods": mn}
 
     tfile = args.traffic_file or os.path.join(ROOT, "profiles", "r02", f"traffic_{wl}.json")
     pmc_name = "eval_round_numa" if wl == "c4" else dom  # live timing folds every wide pass under "eval_round"
