@@ -1944,7 +1944,10 @@ struct kg_engine {
   DevBuf<RsvPod> rpods;
   DevBuf<int32_t> out_rslot;    // [staged + kMaxB]
   DevBuf<uint64_t> rsv_val;     // [capacity] packed per-node pass-1 values
-  DevBuf<unsigned long long> rsv_ws;  // [4]: [3] = pod cursor
+  DevBuf<unsigned long long> rsv_ws;  // [8]: [3] = pod cursor, [4] = the call's end (graph launches)
+  // the instantiated reservation group graph, reused while its launch arguments are unchanged
+  hipGraphExec_t rsv_exec = nullptr;
+  std::vector<unsigned char> rsv_exec_sig;
   DevBuf<uint64_t> rsv_part;    // [4][blocks] per-block partials (preferred-node key, max raw, max key, max ds raw)
   // live kernel timing (kg_profile_enable): HIP event pairs around every launch of the round runners, on the
   // launch's own stream, folded into per-kind totals after each batch synchronises
@@ -2831,45 +2834,70 @@ int run_rsv(kg_engine* e, int64_t first, int64_t count, kg_stats* stats, double 
   if (count > 0 && n > 0) {
     const unsigned blocks = (unsigned)((n + kRsvThreads - 1) / kRsvThreads);
     const RsvExt X = rsv_ext(e);
-    const unsigned long long init[4] = {0, 0, 0, (unsigned long long)first};
-    HIP_TRY(hipMemcpyAsync(e->rsv_ws.p, init, 32, hipMemcpyHostToDevice, e->stream));
-    auto issue_group = [&]() {
-      for (int g = 0; g < kRsvGroup; ++g) {
+    const unsigned long long init[5] = {0, 0, 0, (unsigned long long)first, (unsigned long long)end};
+    HIP_TRY(hipMemcpyAsync(e->rsv_ws.p, init, sizeof(init), hipMemcpyHostToDevice, e->stream));
+    // `end_arg` < 0: the kernels read the call's end from the workspace (a graph stays valid across calls);
+    // `passes` < kRsvGroup: a short call issues exactly its passes, no empty ones
+    auto issue_group = [&](int64_t end_arg, int passes) {
+      for (int g = 0; g < passes; ++g) {
         size_t t = prof_begin(e, e->stream);
-        rsv_eval<<<blocks, kRsvThreads, 0, e->stream>>>(e->T, e->rsv_d.p, e->rsv_nd.p, e->pods.p, e->rpods.p, end, n, g,
-                                                         e->P, e->RP, X, e->rsv_val.p, e->rsv_part.p, e->out_keys.p,
+        rsv_eval<<<blocks, kRsvThreads, 0, e->stream>>>(e->T, e->rsv_d.p, e->rsv_nd.p, e->pods.p, e->rpods.p, end_arg, n,
+                                                         g, e->P, e->RP, X, e->rsv_val.p, e->rsv_part.p, e->out_keys.p,
                                                          e->out_rslot.p, e->rsv_ws.p);
         prof_end(e, KG_PROF_RSV_EVAL, t, e->stream);
         t = prof_begin(e, e->stream);
-        rsv_select<<<blocks, kRsvThreads, 0, e->stream>>>(e->rsv_val.p, e->pods.p, end, n, g, e->RP, X, e->rsv_part.p,
+        rsv_select<<<blocks, kRsvThreads, 0, e->stream>>>(e->rsv_val.p, e->pods.p, end_arg, n, g, e->RP, X, e->rsv_part.p,
                                                            e->rsv_ws.p);
         prof_end(e, KG_PROF_RSV_SELECT, t, e->stream);
       }
       size_t t = prof_begin(e, e->stream);
-      rsv_apply<<<1, kWave, 0, e->stream>>>(e->T, e->rsv_d.p, e->rsv_val.p, e->pods.p, end, (int)blocks, kRsvGroup - 1,
+      rsv_apply<<<1, kWave, 0, e->stream>>>(e->T, e->rsv_d.p, e->rsv_val.p, e->pods.p, end_arg, (int)blocks, passes - 1,
                                             X, e->rsv_part.p, e->out_keys.p, e->out_rslot.p, e->rsv_ws.p);
       prof_end(e, KG_PROF_RSV_APPLY, t, e->stream);
     };
     // KG_RSV_NO_GRAPH=1: plain stream launches (profilers whose kernel tracing does not follow graph launches);
     // live kernel timing also uses plain launches (its events bracket each launch)
     static const bool no_graph = std::getenv("KG_RSV_NO_GRAPH") && std::getenv("KG_RSV_NO_GRAPH")[0] == '1';
-    if (no_graph || e->prof_on) {
-      for (int64_t c = 0; c < count; c += kRsvGroup) issue_group();
+    if (no_graph || e->prof_on || count < kRsvGroup) {
+      for (int64_t c = 0; c < count; c += kRsvGroup) issue_group(end, (int)std::min<int64_t>(kRsvGroup, count - c));
       HIP_TRY(hipGetLastError());
       HIP_TRY(hipStreamSynchronize(e->stream));
-      if (int rc = prof_collect(e)) return rc;
+      if (e->prof_on)
+        if (int rc = prof_collect(e)) return rc;
     } else {
-      hipGraph_t graph = nullptr;
-      hipGraphExec_t exec = nullptr;
-      HIP_TRY(hipStreamBeginCapture(e->stream, hipStreamCaptureModeThreadLocal));
-      issue_group();
-      const hipError_t ce = hipStreamEndCapture(e->stream, &graph);
-      if (ce != hipSuccess) return fail(KG_E_DEVICE, "hipStreamEndCapture: %s", hipGetErrorString(ce));
-      hipError_t ge = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
-      for (int64_t c = 0; ge == hipSuccess && c < count; c += kRsvGroup) ge = hipGraphLaunch(exec, e->stream);
+      // the group graph is keyed on its launch arguments (table / buffer pointers, sizes, profile parameters)
+      std::vector<unsigned char> sig;
+      auto put = [&](const void* q, size_t len) {
+        const unsigned char* b = static_cast<const unsigned char*>(q);
+        sig.insert(sig.end(), b, b + len);
+      };
+      put(&e->T, sizeof(e->T));
+      const void* ptrs[] = {e->rsv_d.p, e->rsv_nd.p, e->pods.p, e->rpods.p, e->rsv_val.p, e->rsv_part.p,
+                            e->out_keys.p, e->out_rslot.p, e->rsv_ws.p};
+      put(ptrs, sizeof(ptrs));
+      put(&n, sizeof(n));
+      put(&e->P, sizeof(e->P));
+      put(&e->RP, sizeof(e->RP));
+      put(&X, sizeof(X));
+      if (!e->rsv_exec || sig != e->rsv_exec_sig) {
+        if (e->rsv_exec) (void)hipGraphExecDestroy(e->rsv_exec);
+        e->rsv_exec = nullptr;
+        hipGraph_t graph = nullptr;
+        HIP_TRY(hipStreamBeginCapture(e->stream, hipStreamCaptureModeThreadLocal));
+        issue_group(-1, kRsvGroup);
+        const hipError_t ce = hipStreamEndCapture(e->stream, &graph);
+        if (ce != hipSuccess) return fail(KG_E_DEVICE, "hipStreamEndCapture: %s", hipGetErrorString(ce));
+        const hipError_t ie = hipGraphInstantiate(&e->rsv_exec, graph, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(graph);
+        if (ie != hipSuccess) {
+          e->rsv_exec = nullptr;
+          return fail(KG_E_DEVICE, "reservation pass graph: %s", hipGetErrorString(ie));
+        }
+        e->rsv_exec_sig = sig;
+      }
+      hipError_t ge = hipSuccess;
+      for (int64_t c = 0; ge == hipSuccess && c < count; c += kRsvGroup) ge = hipGraphLaunch(e->rsv_exec, e->stream);
       if (ge == hipSuccess) ge = hipStreamSynchronize(e->stream);
-      if (exec) (void)hipGraphExecDestroy(exec);
-      (void)hipGraphDestroy(graph);
       if (ge != hipSuccess) return fail(KG_E_DEVICE, "reservation pass graph: %s", hipGetErrorString(ge));
     }
   } else if (count > 0) {
@@ -3072,9 +3100,9 @@ static int engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank,
     if (int rc = e->rsv_d.ensure(cap)) return bail(rc);
     if (int rc = e->rsv_nd.ensure(cap)) return bail(rc);
     if (int rc = e->rsv_val.ensure(cap)) return bail(rc);
-    if (int rc = e->rsv_ws.ensure(4)) return bail(rc);
+    if (int rc = e->rsv_ws.ensure(8)) return bail(rc);
     if (int rc = e->rsv_part.ensure(4 * ((cap + kRsvThreads - 1) / kRsvThreads) + 4)) return bail(rc);
-    if (hipMemset(e->rsv_nd.p, 0, cap * 4) != hipSuccess || hipMemset(e->rsv_ws.p, 0, 32) != hipSuccess)
+    if (hipMemset(e->rsv_nd.p, 0, cap * 4) != hipSuccess || hipMemset(e->rsv_ws.p, 0, 64) != hipSuccess)
       return bail(fail(KG_E_DEVICE, "hipMemset"));
   }
   const int64_t max_total = 100 * ((c.fit_score ? c.weight_fit : 0) + (c.la_score ? c.weight_loadaware : 0) +
@@ -3242,6 +3270,8 @@ void kg_engine_destroy(kg_engine* e) {
   e->rpods.release();
   e->out_rslot.release();
   e->rsv_val.release();
+  if (e->rsv_exec) (void)hipGraphExecDestroy(e->rsv_exec);
+  e->rsv_exec = nullptr;
   e->rsv_ws.release();
   e->rsv_part.release();
   e->scratch64.release();

@@ -337,6 +337,7 @@ __global__ __launch_bounds__(kRsvThreads) void rsv_eval(DevTable T, RsvNode* __r
                                                         unsigned long long* __restrict__ ws) {
   __shared__ uint64_t s_red[kRsvThreads / kWave];
   __shared__ int s_admit;
+  if (end < 0) end = (int64_t)ws[4];  // graph launches: the call's end lives in the workspace
   const int64_t j = (int64_t)ws[3] + g;
   if (j - 1 >= end || (g == 0 && j >= end)) return;  // uniform across the grid
   const int nb = gridDim.x;
@@ -414,6 +415,7 @@ __global__ __launch_bounds__(kRsvThreads) void rsv_select(const uint64_t* __rest
                                                           uint64_t* __restrict__ part,
                                                           unsigned long long* __restrict__ ws) {
   __shared__ uint64_t s_red[kRsvThreads / kWave];
+  if (end < 0) end = (int64_t)ws[4];
   const int64_t j = (int64_t)ws[3] + g;
   if (j >= end) return;
   const int nb = gridDim.x;
@@ -448,6 +450,7 @@ __global__ __launch_bounds__(kWave) void rsv_apply(DevTable T, RsvNode* __restri
                                                    const uint64_t* __restrict__ part,
                                                    uint64_t* __restrict__ out_keys, int32_t* __restrict__ out_slot,
                                                    unsigned long long* __restrict__ ws) {
+  if (end < 0) end = (int64_t)ws[4];
   const int64_t base = (int64_t)ws[3];
   const int64_t j = base + g_last;
   if (base >= end) return;
