@@ -119,7 +119,9 @@ enum {
   KG_REJECT_LOADAWARE = 1 << 3,     /* LoadAwareScheduling: usage exceed threshold     */
   KG_REJECT_INVALID_NODE = 1 << 4,  /* deleted / never-upserted slot                   */
   KG_REJECT_NUMA = 1 << 5,          /* NodeNUMAResource (topology, cpuset, NUMA admit) */
-  KG_REJECT_DEVICE = 1 << 6         /* DeviceShare (Insufficient gpu devices)          */
+  KG_REJECT_DEVICE = 1 << 6,        /* DeviceShare (Insufficient gpu devices)          */
+  KG_REJECT_FIT_OTHER = 1 << 7      /* NodeResourcesFit: Insufficient ephemeral-storage / a scalar resource
+                                       (KG_RES_EPHEMERAL .. KG_RES_MID_MEMORY; reservation/plugin.go:469-479) */
 };
 
 /* node flags */

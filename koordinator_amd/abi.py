@@ -50,6 +50,7 @@ NUMA_POLICY = {"": 0, "BestEffort": 1, "Restricted": 2, "SingleNUMANode": 3}
 STRATEGY = {"LeastAllocated": 0, "MostAllocated": 1}
 REJECT_NUMA = 32
 REJECT_DEVICE = 64
+REJECT_FIT_OTHER = 128  # NodeResourcesFit: ephemeral-storage / a scalar resource (RES_EPHEMERAL .. RES_MID_MEMORY)
 # DeviceShare device resources (KG_DEV_*)
 DEV_RES_MAX, MAX_MINORS = 8, 8
 DEV_NVIDIA_GPU, DEV_HYGON_DCU, DEV_KOORD_GPU, DEV_GPU_CORE, DEV_GPU_MEMORY, DEV_GPU_MEMORY_RATIO, DEV_FPGA, DEV_RDMA = \

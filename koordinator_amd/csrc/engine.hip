@@ -152,7 +152,7 @@ __device__ __forceinline__ void select_write(const uint32_t (&v)[kNPT], const ui
 __device__ __forceinline__ void eval_tile_exact(const DevTable& T, const DevPod* __restrict__ pods, int64_t first,
                                              int p0, int p1, int tile, int64_t node_base, int64_t n_local,
                                              int nt_local, const EvalParams& P, uint64_t* __restrict__ lists,
-                                             int vbits) {
+                                             int vbits, const int64_t* __restrict__ paux) {
   const int lane = threadIdx.x % kWave;
   uint32_t gidx[kNPT];
 #pragma unroll
@@ -166,6 +166,8 @@ __device__ __forceinline__ void eval_tile_exact(const DevTable& T, const DevPod*
       asm volatile("" : "+v"(local));
       int64_t t = 0;
       v[j] = (local < n_local && eval_node(load_row(T, node_base + local), p, P, t)) ? (uint32_t)t + 1u : 0u;
+      if (P.fit_filter && (p.flags & P_AUX) && v[j] && !aux_fits(T, node_base + local, paux + (size_t)(first + pi) * kAux))
+        v[j] = 0;
     }
     select_write(v, gidx, vbits, lists + ((size_t)pi * nt_local + tile) * kR, lane);
   }
@@ -176,7 +178,8 @@ __global__ __launch_bounds__(kWave* kEvalWaves) void eval_round(DevTable T, cons
                                                                   int64_t first, int nb, int pods_per_wave,
                                                                   int64_t node_base, int64_t n_local, int nt_local,
                                                                   EvalParams P, uint64_t* __restrict__ lists,
-                                                                  const int32_t* __restrict__ poison) {
+                                                                  const int32_t* __restrict__ poison,
+                                                                  const int64_t* __restrict__ paux) {
   KG_STAMP(0, 0);
   if (*poison) return;
   const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
@@ -210,7 +213,7 @@ __global__ __launch_bounds__(kWave* kEvalWaves) void eval_round(DevTable T, cons
   KG_STAMP(0, 1);
   // a row outside eval_hot's exact domain anywhere in the tile: the whole tile takes the exact path
   if (__ballot(rare)) {
-    eval_tile_exact(T, pods, first, p0, p1, tile, node_base, n_local, nt_local, P, lists, vbits);
+    eval_tile_exact(T, pods, first, p0, p1, tile, node_base, n_local, nt_local, P, lists, vbits, paux);
     return;
   }
   for (int pi = p0; pi < p1; ++pi) {
@@ -221,7 +224,19 @@ __global__ __launch_bounds__(kWave* kEvalWaves) void eval_round(DevTable T, cons
       uint32_t t = 0;
       v[j] = eval_hot<PF>(rows[j], p, P, t) ? t + 1u : 0u;
     }
+    if constexpr ((PF & PF_FIT_FILTER) != 0) {  // ephemeral-storage / scalar requests: the Allocatable-Requested columns
+      if (p.flags & P_AUX) {
+        const int64_t* rq = paux + (size_t)(first + pi) * kAux;
+#pragma unroll
+        for (int j = 0; j < kNPT; ++j)
+          if (v[j] && !aux_fits(T, gidx[j], rq)) v[j] = 0;
+      }
+    }
+#ifdef KG_EXP_NOSELECT  // timing experiment only (wrong lists): the wide pass without its per-tile select
+    if (lane < kR) lists[((size_t)pi * nt_local + tile) * kR + lane] = make_key(v[0] + v[1] + v[2] + v[3], gidx[0]);
+#else
     select_write(v, gidx, vbits, lists + ((size_t)pi * nt_local + tile) * kR, lane);
+#endif
   }
   KG_STAMP(0, 31);
 }
@@ -651,7 +666,8 @@ __device__ __forceinline__ uint64_t wave_max_modkey(uint64_t k, bool narrow) {
 // Round write-back: lane j < consumed adds placed pod j's NodeInfo.AddPod + podAssignCache.assign terms onto its
 // winner's columns (int64 atomics: several pods of the round may share a winner; no other writer — earlier rounds'
 // resolvers are done, later ones wait for this one; concurrent wide passes read mixed columns).
-__device__ __forceinline__ void writeback_pod(const DevTable& T, uint32_t node, const DevPod& p) {
+__device__ __forceinline__ void writeback_pod(const DevTable& T, uint32_t node, const DevPod& p,
+                                              const int64_t* __restrict__ rq) {
   const int64_t i = node;
   const int64_t prod = (p.flags & P_PROD) ? 1 : 0;
   auto add = [](int64_t* a, int64_t v) { atomicAdd(reinterpret_cast<unsigned long long*>(a), (unsigned long long)v); };
@@ -666,6 +682,30 @@ __device__ __forceinline__ void writeback_pod(const DevTable& T, uint32_t node, 
     add(&T.la_pused_mem[i], p.est_mem);
   }
   atomicAdd(&T.num_pods[i], 1);
+  if (p.flags & P_AUX)
+#pragma unroll
+    for (int r = 0; r < kAux; ++r)
+      if (rq[r]) add(&T.aux[(size_t)(kAux + r) * T.cap + i], rq[r]);
+}
+
+// fitsRequest over the kAux resources on a modified row: the round-start Requested (the table; this round's
+// placements are written back only by the epilogue) plus every earlier placement of this round on that node
+__device__ __forceinline__ bool mod_aux_fits(const DevTable& T, uint32_t node, const int64_t* __restrict__ rq, int j,
+                                             uint64_t my_out, const DevPod* s_pods, const int64_t* __restrict__ prq) {
+  int64_t add[kAux] = {0, 0, 0, 0, 0};
+  for (int q = 0; q < j; ++q) {
+    const uint64_t k = readlane_u64(my_out, q);
+    if (k == 0 || !(s_pods[q].flags & P_AUX)) continue;
+    if (key_node(k) == node)
+#pragma unroll
+      for (int r = 0; r < kAux; ++r) add[r] += prq[(size_t)q * kAux + r];
+  }
+  bool ok = true;
+#pragma unroll
+  for (int r = 0; r < kAux; ++r)
+    if (rq[r] != 0)
+      ok &= !(rq[r] > T.aux[(size_t)r * T.cap + node] - (T.aux[(size_t)(kAux + r) * T.cap + node] + add[r]));
+  return ok;
 }
 
 // The node table's columns are carved from two allocations (kg_engine: cols64 = 12 int64 columns + inv_mem[2],
@@ -691,6 +731,7 @@ __device__ __forceinline__ DevTable table_at(const DevTable& T0) {
   T.la_pused_cpu = c64 + 10 * cap;
   T.la_pused_mem = c64 + 11 * cap;
   T.inv_mem = reinterpret_cast<double*>(c64 + 12 * cap);
+  T.aux = c64 + 14 * cap;
   T.alloc_pods = c32 + 0 * cap;
   T.num_pods = c32 + 1 * cap;
   T.flags = reinterpret_cast<uint32_t*>(c32 + 2 * cap);
@@ -718,7 +759,8 @@ __global__ __launch_bounds__(kWave) void resolve_round(DevTable T0, const DevPod
                                                         uint64_t* __restrict__ out_keys, int bitmap_words,
                                                         int32_t* __restrict__ modlists, int slot, int depth,
                                                         int n_prev, int32_t* __restrict__ poison, int64_t seq,
-                                                        int wait, QuotaRow* __restrict__ quotas, int nq) {
+                                                        int wait, QuotaRow* __restrict__ quotas, int nq,
+                                                        const int64_t* __restrict__ paux) {
   extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
   KG_STAMP(2, 0);
   const int lane = threadIdx.x;
@@ -866,11 +908,17 @@ __global__ __launch_bounds__(kWave) void resolve_round(DevTable T0, const DevPod
       if (nM > 0 && pos > 0) {  // a modified node is listed above e: re-score the modified rows exactly
         ++n_slow;
         diag |= 1;
+        const bool aux = (PF & PF_FIT_FILTER) && (p.flags & P_AUX);  // ephemeral-storage / scalar requests
+        const int64_t* rq = paux + (size_t)(first + j) * kAux;
         mod_row_settle<PF>(R0, s_cand, s_pods, T0, P);
         uint64_t mk = mod_row_key<PF>(R0, p, P, s_par);
+        if (aux && mk && !mod_aux_fits(table_at(T0), R0.node, rq, j, my_out, s_pods, paux + (size_t)first * kAux))
+          mk = 0;
         if (nM > kWave) {
           mod_row_settle<PF>(R1, s_cand, s_pods, T0, P);
-          const uint64_t k1 = mod_row_key<PF>(R1, p, P, s_par);
+          uint64_t k1 = mod_row_key<PF>(R1, p, P, s_par);
+          if (aux && k1 && !mod_aux_fits(table_at(T0), R1.node, rq, j, my_out, s_pods, paux + (size_t)first * kAux))
+            k1 = 0;
           mk = k1 > mk ? k1 : mk;
         }
         const uint64_t mbest = wave_max_modkey(mk, narrow);
@@ -918,7 +966,7 @@ __global__ __launch_bounds__(kWave) void resolve_round(DevTable T0, const DevPod
   // allowed: the next resolver's hash keeps one slot per node)
   const bool mine = lane < consumed && my_out != 0;
   const uint32_t my_node = mine ? key_node(my_out) : kNoNode;
-  if (mine) writeback_pod(table_at(T0), my_node, s_pods[lane]);
+  if (mine) writeback_pod(table_at(T0), my_node, s_pods[lane], paux + (size_t)(first + lane) * kAux);
   int32_t* my_mod = modlists + (size_t)slot * kModListStride;
   const uint64_t lane_lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   const uint64_t bm = __ballot(mine);
@@ -1641,13 +1689,15 @@ __global__ void scatter_ds(DsTable DT, const DsNode* __restrict__ s, const int32
 
 // kg_pods_evaluate: one pod, every node, per-plugin outputs.
 __global__ void evaluate_pod(DevTable T, const DevPod* __restrict__ pod, int64_t n, EvalParams P,
-                             int32_t* __restrict__ reject, int64_t* __restrict__ fit, int64_t* __restrict__ la) {
+                             int32_t* __restrict__ reject, int64_t* __restrict__ fit, int64_t* __restrict__ la,
+                             const int64_t* __restrict__ aux_req) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const Row r = load_row(T, i);
   int64_t t = 0, fs = 0, ls = 0;
   uint32_t rej = 0;
   eval_node(r, *pod, P, t, &rej, &fs, &ls);
+  if (P.fit_filter && (pod->flags & P_AUX) && (r.flags & F_VALID) && !aux_fits(T, i, aux_req)) rej |= 1u << 7;
   reject[i] = (int32_t)rej;
   fit[i] = fs;
   la[i] = ls;
@@ -1657,6 +1707,7 @@ __global__ void evaluate_pod(DevTable T, const DevPod* __restrict__ pod, int64_t
 struct RowDelta {
   int64_t idx;
   int64_t d[9];  // req_cpu, req_mem, nz_cpu, nz_mem, num_pods, la_used_cpu, la_used_mem, la_pused_cpu, la_pused_mem
+  int64_t aux[kAux];  // Requested of the kAux resources
 };
 // The framework's Unreserve of placed staged pods idx[0..n) (kg_pods_unreserve), one thread in queue order: NodeInfo
 // + the LoadAware assign cache, NodeNUMAResource Release, DeviceShare updateCacheUsed(add=false), Reservation
@@ -1665,7 +1716,8 @@ __global__ void unreserve_pods(DevTable T, const DevPod* __restrict__ pods, cons
                                uint64_t* __restrict__ out_keys, NumaMut* __restrict__ nm, uint64_t* __restrict__ out_cpus,
                                int64_t* __restrict__ out_nrec, DsNode* __restrict__ ds, const DsPod* __restrict__ dpods,
                                int32_t* __restrict__ out_minors, RsvNode* __restrict__ RN, int32_t* __restrict__ out_rslot,
-                               QuotaRow* __restrict__ quotas, int nq, const int64_t* __restrict__ qdev) {
+                               QuotaRow* __restrict__ quotas, int nq, const int64_t* __restrict__ qdev,
+                               const int64_t* __restrict__ paux) {
   if (blockIdx.x != 0 || threadIdx.x != 0) return;
   for (int64_t k = 0; k < n; ++k) {
     const int64_t j = idx[k];
@@ -1685,6 +1737,8 @@ __global__ void unreserve_pods(DevTable T, const DevPod* __restrict__ pods, cons
     r.la_pused_mem -= prod * p.est_mem;
     r.num_pods -= 1;
     store_mutable(T, w, r);
+    if (p.flags & P_AUX)  // ephemeral-storage / scalar Requested
+      for (int q = 0; q < kAux; ++q) T.aux[(size_t)(kAux + q) * T.cap + w] -= paux[(size_t)j * kAux + q];
     if (nm) {  // nodenumaresource/plugin.go:417-425
       uint64_t* c = out_cpus + (size_t)j * kCpuWords;
       int64_t* rec = out_nrec + (size_t)j * kNumaRecWords;
@@ -1747,6 +1801,9 @@ __global__ void apply_deltas(DevTable T, const RowDelta* __restrict__ d, int64_t
   atomicAdd((unsigned long long*)&T.la_used_mem[k], (unsigned long long)x.d[6]);
   atomicAdd((unsigned long long*)&T.la_pused_cpu[k], (unsigned long long)x.d[7]);
   atomicAdd((unsigned long long*)&T.la_pused_mem[k], (unsigned long long)x.d[8]);
+#pragma unroll
+  for (int r = 0; r < kAux; ++r)
+    if (x.aux[r]) atomicAdd((unsigned long long*)&T.aux[(size_t)(kAux + r) * T.cap + k], (unsigned long long)x.aux[r]);
 }
 
 __device__ __forceinline__ bool eval_hot_rt(const DevTable& T, int64_t i, const DevPod& p, const EvalParams& P,
@@ -1893,6 +1950,9 @@ struct kg_engine {
   // device
   DevTable T{};
   DevBuf<int64_t> cols64;
+  std::vector<int64_t> h_aux;  // staging of the kAux Allocatable columns
+  DevBuf<int64_t> paux;        // [pods][kAux] the staged pods' requests of the kAux resources
+  DevBuf<int64_t> paux1;       // [kAux] the pod of a kg_pods_evaluate call
   DevBuf<int32_t> cols32;
   DevBuf<DevPod> pods;
   int64_t n_staged = 0;
@@ -2200,8 +2260,11 @@ int decode_pod(const kg_engine* e, const kg_pod& p, DevPod& d) {
   for (int r = 0; r < KG_RES_MAX; ++r) {
     if (p.requests[r] < 0 || p.limits[r] < 0) return fail(KG_E_INVALID, "negative pod quantity");
     zero &= p.requests[r] == 0;
-    if (c.fit_filter && r >= 2 && p.requests[r] != 0)
-      return fail(KG_E_UNSUPPORTED, "pod requests resource slot %d; accelerated NodeResourcesFit covers cpu/memory", r);
+    if (c.fit_filter && r >= kAuxFirst + kAux && p.requests[r] != 0)
+      return fail(KG_E_UNSUPPORTED, "pod requests resource slot %d outside the accelerated NodeResourcesFit set", r);
+    if (c.fit_filter && r >= kAuxFirst && p.requests[r] != 0 && (e->numa_on || e->ds_on || e->rsv_on))
+      return fail(KG_E_UNSUPPORTED, "pod requests ephemeral-storage / a scalar resource (slot %d): accelerated in the "
+                  "NodeResourcesFit + LoadAware profiles only", r);
   }
   if (p.priority_class < KG_PRIO_NONE || p.priority_class > KG_PRIO_FREE) return fail(KG_E_INVALID, "priority_class");
   d.req_cpu = p.requests[KG_RES_CPU];
@@ -2230,6 +2293,8 @@ int decode_pod(const kg_engine* e, const kg_pod& p, DevPod& d) {
   d.flags |= (kc ? P_CPU_KEY : 0u) | (km ? P_MEM_KEY : 0u);
   for (int r = 0; r < KG_QUOTA_RES - 2; ++r)
     if (p.device_requests[r] != 0) d.flags |= P_QDEV;
+  for (int r = 0; r < kAux; ++r)
+    if (c.fit_filter && p.requests[kAuxFirst + r] != 0) d.flags |= P_AUX;
   return 0;
 }
 
@@ -2457,6 +2522,13 @@ int sync_static(kg_engine* e) {
   HIP_TRY(hipMemcpyAsync(e->T.flags, (uint32_t*)&h32[1 * cap], cap * 4, hipMemcpyHostToDevice, e->stream));
   HIP_TRY(hipMemcpyAsync(e->T.inv_cpu, &h32[2 * cap], 2 * cap * 4, hipMemcpyHostToDevice, e->stream));
   HIP_TRY(hipMemcpyAsync(e->T.inv_mem, hd.data(), 2 * cap * 8, hipMemcpyHostToDevice, e->stream));
+  {  // Allocatable of the NodeResourcesFit-only resources (ephemeral-storage, batch / mid cpu / memory)
+    auto& ha = e->h_aux;
+    ha.assign((size_t)kAux * cap, 0);
+    for (int64_t i = 0; i < e->n_nodes; ++i)
+      for (int r = 0; r < kAux; ++r) ha[(size_t)r * cap + i] = e->nodes[i].allocatable[kAuxFirst + r];
+    HIP_TRY(hipMemcpyAsync(e->T.aux, ha.data(), (size_t)kAux * cap * 8, hipMemcpyHostToDevice, e->stream));
+  }
   HIP_TRY(hipStreamSynchronize(e->stream));
   e->static_dirty = false;
   return 0;
@@ -2567,7 +2639,7 @@ void launch_eval(kg_engine* e, const RoundGeom& g, int64_t first, int nb, int sl
 #define KG_EVAL(X)                                                                                        \
   eval_round<X><<<eval_grid(g, nb), kWave * kEvalWaves, 0, st>>>(e->T, e->pods.p, first, nb, g.ppw, g.base, \
                                                                  g.n_local, g.nt_local, e->P,             \
-                                                                 lists_slot(e, g, slot), poison_ptr(e))
+                                                                 lists_slot(e, g, slot), poison_ptr(e), e->paux.p)
   KG_PF_SWITCH(profile_bits(e->P), KG_EVAL)
 #undef KG_EVAL
 }
@@ -2606,7 +2678,7 @@ void launch_resolve(kg_engine* e, const RoundGeom& g, int64_t first, int nb, int
                                                                   cand_slot(e, g, slot), e->P, e->out_keys.p,       \
                                                                   g.bitmap_words, e->modlists.p, slot, g.depth,     \
                                                                   n_prev, poison_ptr(e), seq, wait, e->quotas.p,    \
-                                                                  e->nq)
+                                                                  e->nq, e->paux.p)
 #define KG_RESOLVE(X) KG_RESOLVE_T(X, false)
 #define KG_RESOLVE_Q(X) KG_RESOLVE_T(X, true)
   if (e->nq > 0) {
@@ -3045,9 +3117,10 @@ static int engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank,
         return bail(fail(KG_E_DEVICE, "hipEventCreate"));
     }
   }
-  if (int rc = e->cols64.ensure(14 * cap)) return bail(rc);  // 12 int64 columns + inv_mem[2] (f64)
+  // 12 int64 columns + inv_mem[2] (f64) + the kAux resources' Allocatable / Requested
+  if (int rc = e->cols64.ensure((14 + 2 * kAux) * cap)) return bail(rc);
   if (int rc = e->cols32.ensure(5 * cap)) return bail(rc);   // alloc_pods, num_pods, flags, inv_cpu[2] (f32)
-  if (hipMemset(e->cols64.p, 0, 14 * cap * 8) != hipSuccess || hipMemset(e->cols32.p, 0, 5 * cap * 4) != hipSuccess)
+  if (hipMemset(e->cols64.p, 0, (14 + 2 * kAux) * cap * 8) != hipSuccess || hipMemset(e->cols32.p, 0, 5 * cap * 4) != hipSuccess)
     return bail(fail(KG_E_DEVICE, "hipMemset"));
   int64_t* c64 = e->cols64.p;
   e->T.alloc_cpu = c64 + 0 * cap;
@@ -3067,6 +3140,7 @@ static int engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank,
   e->T.flags = (uint32_t*)(e->cols32.p + 2 * cap);
   e->T.inv_cpu = (float*)(e->cols32.p + 3 * cap);
   e->T.inv_mem = (double*)(e->cols64.p + 12 * cap);
+  e->T.aux = e->cols64.p + 14 * cap;
   e->T.cap = cap;
   if (int rc = e->cursor.ensure(8)) return bail(rc);
   if (hipMemset(e->cursor.p, 0, 8 * 8) != hipSuccess) return bail(fail(KG_E_DEVICE, "hipMemset"));
@@ -3238,6 +3312,8 @@ void kg_engine_destroy(kg_engine* e) {
   if (e->comm) ncclCommDestroy(e->comm);
   for (hipEvent_t ev : e->prof_pool) (void)hipEventDestroy(ev);
   e->cols64.release();
+  e->paux.release();
+  e->paux1.release();
   e->cols32.release();
   e->pods.release();
   e->lists.release();
@@ -3359,6 +3435,7 @@ static int pods_delta(kg_engine* e, const kg_pod* pods, const int32_t* node_idx,
     x.d[6] = la * p.est_mem;
     x.d[7] = (p.flags & P_PROD) ? la * p.est_cpu : 0;
     x.d[8] = (p.flags & P_PROD) ? la * p.est_mem : 0;
+    for (int r = 0; r < kAux; ++r) x.aux[r] = sign * pods[k].requests[kAuxFirst + r];
   }
   return push_deltas(e, d);
 }
@@ -3383,7 +3460,7 @@ int kg_pods_unreserve(kg_engine* e, int64_t first, int64_t count, const uint8_t*
                                         e->numa_on ? e->numa_m.p : nullptr, e->out_cpus.p, e->out_nrec.p,
                                         e->ds_on ? e->ds_d.p : nullptr, e->dpods.p, e->out_minors.p,
                                         e->rsv_on ? e->rsv_d.p : nullptr, e->out_rslot.p, e->quotas.p, e->nq,
-                                        (e->ds_on || e->rsv_on) ? e->qdev.p : nullptr);
+                                        (e->ds_on || e->rsv_on) ? e->qdev.p : nullptr, e->paux.p);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(e->stream));
   return 0;
@@ -3409,6 +3486,13 @@ int kg_pods_stage(kg_engine* e, const kg_pod* pods, int64_t n) {
   if (int rc = e->pods.ensure(n + kMaxB)) return rc;
   if (int rc = e->out_keys.ensure(n + kMaxB)) return rc;
   if (n > 0) HIP_TRY(hipMemcpyAsync(e->pods.p, h.data(), n * sizeof(DevPod), hipMemcpyHostToDevice, e->stream));
+  {  // the kAux requests (NodeResourcesFit Filter of ephemeral-storage / scalar resources)
+    std::vector<int64_t> ha((size_t)std::max<int64_t>(n, 1) * kAux, 0);
+    for (int64_t k = 0; k < n; ++k)
+      for (int r = 0; r < kAux; ++r) ha[(size_t)k * kAux + r] = pods[k].requests[kAuxFirst + r];
+    if (int rc = e->paux.ensure((size_t)(n + kMaxB) * kAux)) return rc;
+    if (n > 0) HIP_TRY(hipMemcpyAsync(e->paux.p, ha.data(), (size_t)n * kAux * 8, hipMemcpyHostToDevice, e->stream));
+  }
   if (e->ds_on || e->rsv_on) {  // the pods' device requests as ElasticQuota dims (cpu, memory, 6 device resources)
     std::vector<int64_t> hq((size_t)std::max<int64_t>(n, 1) * kQuotaRes, 0);
     for (int64_t k = 0; k < n; ++k)
@@ -3535,8 +3619,10 @@ int kg_pods_evaluate(kg_engine* e, const kg_pod* pod, int32_t* out_reject, int64
   if (int rc = e->scratch32.ensure(n)) return rc;
   DevPod* dp = reinterpret_cast<DevPod*>(e->scratch64.p + 2 * n);  // the kPodWords spare int64s
   HIP_TRY(hipMemcpyAsync(dp, &d, sizeof(d), hipMemcpyHostToDevice, e->stream));
+  if (int rc = e->paux1.ensure(kAux)) return rc;
+  HIP_TRY(hipMemcpyAsync(e->paux1.p, &pod->requests[kAuxFirst], kAux * 8, hipMemcpyHostToDevice, e->stream));
   evaluate_pod<<<(unsigned)((n + 255) / 256), 256, 0, e->stream>>>(e->T, dp, n, e->P, e->scratch32.p, e->scratch64.p,
-                                                                   e->scratch64.p + n);
+                                                                   e->scratch64.p + n, e->paux1.p);
   HIP_TRY(hipGetLastError());
   std::vector<int32_t> rej(n);
   std::vector<int64_t> fs(n), ls(n);

@@ -76,6 +76,13 @@ constexpr uint32_t P_NONPREEMPT = 1u << 4;    // extension.IsPodNonPreemptible (
 constexpr uint32_t P_CPU_KEY = 1u << 5;       // cpu is a key of the pod's requests (PodRequestsAndLimits)
 constexpr uint32_t P_MEM_KEY = 1u << 6;       // memory is a key of the pod's requests
 constexpr uint32_t P_QDEV = 1u << 7;          // the pod requests device resources (quota dims 2.. are keys)
+constexpr uint32_t P_AUX = 1u << 8;           // the pod requests ephemeral-storage or a scalar resource (kAux slots)
+
+// NodeResourcesFit-only resources (kg_pod / kg_node slots KG_RES_EPHEMERAL .. KG_RES_MID_MEMORY): ephemeral-storage
+// and the batch / mid cpu / memory extended resources.  Filter only (fitsRequest, reservation/plugin.go:469-479):
+// per node an Allocatable and a Requested column each; a pod carries its requests in a side array (pod_aux).
+constexpr int kAux = 5;
+constexpr int kAuxFirst = 2;
 
 struct DevTable {
   int64_t *alloc_cpu, *alloc_mem;        // NodeInfo.Allocatable
@@ -88,6 +95,7 @@ struct DevTable {
   uint32_t *flags;
   float *inv_cpu;                        // [2][cap]: 100/alloc_cpu, 100/la_alloc_cpu        (f32 estimates)
   double *inv_mem;                       // [2][cap]: 100/alloc_mem, 100/la_alloc_mem        (f64 estimates)
+  int64_t *aux;                          // [2 * kAux][cap]: Allocatable, then Requested, of the kAux resources
   int64_t cap;                           // column stride of the reciprocal columns
 };
 
@@ -238,6 +246,16 @@ __device__ __forceinline__ bool eval_node(const Row& n, const DevPod& p, const E
   if (la_out) *la_out = ls;
   total = t;
   return rej == 0;
+}
+
+// fitsRequest over the kAux resources for a pod requesting some of them (req: kAux values, 0 = not requested):
+// `request > Allocatable - Requested` rejects (reservation/plugin.go:469-479)
+__device__ __forceinline__ bool aux_fits(const DevTable& T, int64_t i, const int64_t* __restrict__ req) {
+  bool ok = true;
+#pragma unroll
+  for (int r = 0; r < kAux; ++r)
+    if (req[r] != 0) ok &= !(req[r] > T.aux[(size_t)r * T.cap + i] - T.aux[(size_t)(kAux + r) * T.cap + i]);
+  return ok;
 }
 
 // Packed selection key: higher total wins, then LOWER node index (BASELINE pin replacing selectHost's

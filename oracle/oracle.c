@@ -256,6 +256,12 @@ int or_fit_filter(const kg_node* node, const or_node_state* st, const kg_pod* po
     reasons |= KG_REJECT_FIT_CPU;
   if (pod->requests[KG_RES_MEMORY] > node->allocatable[KG_RES_MEMORY] - st->requested[KG_RES_MEMORY])
     reasons |= KG_REJECT_FIT_MEMORY;
+  /* ephemeral-storage and the scalar (batch / mid cpu / memory) resources the pod requests
+   * (reservation/plugin.go:469-479: EphemeralStorage, then `for rName, rQuant := range podRequest.ScalarResources`).
+   * A resource the pod does not request (0) is not compared: the engine keeps no per-pod key set for these. */
+  for (int r = KG_RES_EPHEMERAL; r <= KG_RES_MID_MEMORY; r++)
+    if (pod->requests[r] != 0 && pod->requests[r] > node->allocatable[r] - st->requested[r])
+      reasons |= KG_REJECT_FIT_OTHER;
   return reasons;
 }
 

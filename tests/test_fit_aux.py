@@ -1,0 +1,161 @@
+"""NodeResourcesFit Filter over ephemeral-storage and the scalar (batch / mid cpu / memory) resources.
+
+fitsRequest (restated in-tree at reservation/plugin.go:433-482) compares, beyond cpu / memory / pod count,
+`EphemeralStorage > Allocatable - Requested` and, for every scalar resource in the pod's request,
+`rQuant > Allocatable.ScalarResources[r] - Requested.ScalarResources[r]`.  The engine holds an Allocatable and a
+Requested column per resource (kAux), checks them for pods that request any of them (P_AUX) in the wide pass, in the
+resolver's re-score of modified rows (round-start Requested + this round's earlier placements on the row) and in
+kg_pods_evaluate (KG_REJECT_FIT_OTHER), and moves Requested on assume / kg_pods_add / kg_pods_remove / Unreserve.
+
+Parity unpinned beyond the restated comparison: no reference test drives these resources through a cluster.  One
+documented divergence: a resource the pod does not request (0) is not compared, so a node whose ephemeral-storage
+Requested exceeds its Allocatable still admits pods without an ephemeral request (the reference compares 0 > negative
+and rejects them); the synthetic clusters never overcommit."""
+import numpy as np
+import pytest
+
+from koordinator_amd import Engine, abi, framework as F, synth
+from oracle import oracle
+
+GI = 1 << 30
+AUX = (abi.RES_EPHEMERAL, abi.RES_BATCH_CPU, abi.RES_BATCH_MEMORY, abi.RES_MID_CPU, abi.RES_MID_MEMORY)
+
+
+def _aux_cluster(n, seed):
+    """C2-style cluster where 70 % of nodes expose ephemeral-storage and batch / mid resources, and the existing
+    pods already hold a share of them."""
+    rng = np.random.default_rng(seed)
+    cl = synth.make_cluster(n, seed=seed)
+    has = rng.random(n) < 0.7
+    cl.nodes["allocatable"][:, abi.RES_EPHEMERAL] = np.where(has, rng.choice([100, 200, 400], n) * GI, 0)
+    cl.nodes["allocatable"][:, abi.RES_BATCH_CPU] = np.where(has, rng.integers(4, 40, n) * 1000, 0)
+    cl.nodes["allocatable"][:, abi.RES_BATCH_MEMORY] = np.where(has, rng.integers(8, 80, n) * GI, 0)
+    cl.nodes["allocatable"][:, abi.RES_MID_CPU] = np.where(rng.random(n) < 0.5, rng.integers(2, 20, n) * 1000, 0)
+    cl.nodes["allocatable"][:, abi.RES_MID_MEMORY] = np.where(rng.random(n) < 0.5, rng.integers(4, 40, n) * GI, 0)
+    ex = cl.existing_pods
+    m = len(ex)
+    k = rng.random(m) < 0.3
+    node_has = has[cl.existing_node]
+    ex["requests"][:, abi.RES_EPHEMERAL] = np.where(k & node_has, rng.choice([1, 5, 20], m) * GI, 0)
+    return cl
+
+
+def _aux_pods(n, seed, frac=0.35):
+    rng = np.random.default_rng(seed)
+    pods = synth.make_pods(n, seed=seed)
+    k = rng.random(n) < frac
+    which = rng.integers(0, 3, n)
+    pods["requests"][:, abi.RES_EPHEMERAL] = np.where(k & (which == 0), rng.choice([10, 50, 150, 500], n) * GI, 0)
+    pods["requests"][:, abi.RES_BATCH_CPU] = np.where(k & (which == 1), rng.choice([1000, 4000, 8000], n), 0)
+    pods["requests"][:, abi.RES_BATCH_MEMORY] = np.where(k & (which == 1), rng.choice([2, 8, 16], n) * GI, 0)
+    pods["requests"][:, abi.RES_MID_CPU] = np.where(k & (which == 2), rng.choice([500, 2000], n), 0)
+    return pods
+
+
+def _state_from_pods(n, cfg, cluster):
+    st = oracle.states(n)
+    oracle.add_pods(cfg, st, cluster.existing_pods, cluster.existing_node)
+    return st
+
+
+# ---- CPU: the oracle's comparison --------------------------------------------------------------------------------
+def test_oracle_fit_filter_aux_resources():
+    cfg = F.build_config()
+    node = np.zeros(1, dtype=abi.NODE_DTYPE)
+    node["allocatable"][0, abi.RES_CPU] = 8000
+    node["allocatable"][0, abi.RES_MEMORY] = 16 * GI
+    node["allocatable"][0, abi.RES_EPHEMERAL] = 100 * GI
+    node["allocatable"][0, abi.RES_BATCH_CPU] = 4000
+    node["allowed_pods"] = 110
+    node["flags"] = abi.NODE_VALID
+    st = oracle.states(1)
+    held = np.zeros(1, dtype=abi.POD_DTYPE)
+    held["requests"][0, abi.RES_CPU] = 1000
+    held["requests"][0, abi.RES_EPHEMERAL] = 90 * GI
+    held["requests"][0, abi.RES_BATCH_CPU] = 3000
+    oracle.add_pods(cfg, st, held, np.zeros(1, dtype=np.int32))
+
+    def pod(eph=0, bcpu=0, mcpu=0):
+        p = np.zeros(1, dtype=abi.POD_DTYPE)
+        p["requests"][0, abi.RES_CPU] = 500
+        p["requests"][0, abi.RES_MEMORY] = GI
+        p["requests"][0, abi.RES_EPHEMERAL] = eph
+        p["requests"][0, abi.RES_BATCH_CPU] = bcpu
+        p["requests"][0, abi.RES_MID_CPU] = mcpu
+        return p
+
+    assert oracle.fit_filter(node, st, pod()) == 0
+    assert oracle.fit_filter(node, st, pod(eph=10 * GI)) == 0          # 10 Gi ≤ 100 - 90
+    assert oracle.fit_filter(node, st, pod(eph=11 * GI)) == abi.REJECT_FIT_OTHER
+    assert oracle.fit_filter(node, st, pod(bcpu=1000)) == 0
+    assert oracle.fit_filter(node, st, pod(bcpu=1001)) == abi.REJECT_FIT_OTHER
+    assert oracle.fit_filter(node, st, pod(mcpu=1)) == abi.REJECT_FIT_OTHER  # node has no mid-cpu
+
+
+def test_oracle_aux_queue_differs_from_cpu_memory_only():
+    """The aux requests change placements on this cluster (so the GPU parity below exercises the new columns)."""
+    cfg = F.build_config()
+    cl = _aux_cluster(300, seed=811)
+    pods = _aux_pods(2000, seed=812)
+    on, _, _ = oracle.schedule_cluster(cfg, cl, pods, n_threads=4)
+    plain = pods.copy()
+    for r in AUX:
+        plain["requests"][:, r] = 0
+    on2, _, _ = oracle.schedule_cluster(cfg, cl, plain, n_threads=4)
+    assert (on != on2).sum() > 50
+    assert (on < 0).sum() > 0  # some aux requests fit nowhere
+
+
+# ---- GPU: bit-exact against the oracle ---------------------------------------------------------------------------
+@pytest.mark.gpu
+@pytest.mark.parametrize("n_nodes,n_pods,batch", [(300, 3000, 32), (2000, 6000, 32), (257, 2000, 13)])
+def test_gpu_aux_parity(n_nodes, n_pods, batch):
+    cfg = F.build_config(batch_pods=batch)
+    cl = _aux_cluster(n_nodes, seed=820 + n_nodes)
+    pods = _aux_pods(n_pods, seed=821 + n_nodes)
+    on, os_, st = oracle.schedule_cluster(cfg, cl, pods, n_threads=4)
+    with Engine(cfg, cl.n) as e:
+        synth.load_into(e, cl)
+        gn, gs, _ = e.schedule(pods)
+        bad = np.nonzero(gn != on)[0]
+        assert bad.size == 0, f"first mismatch at pod {bad[:5]}: gpu {gn[bad[:5]]} oracle {on[bad[:5]]}"
+        np.testing.assert_array_equal(gs, os_)
+        # the engine's aux Requested after the queue: an extra probe pod per node sees the same verdicts
+        probe = _aux_pods(40, seed=899, frac=1.0)
+        for k in range(len(probe)):
+            q = probe[k:k + 1]
+            rej, _, _ = e.evaluate(q)
+            want = np.array([oracle.fit_filter(cl.nodes[i:i + 1], st[i:i + 1], q) for i in range(cl.n)])
+            got = rej & (abi.REJECT_FIT_PODS | abi.REJECT_FIT_CPU | abi.REJECT_FIT_MEMORY | abi.REJECT_FIT_OTHER)
+            np.testing.assert_array_equal(got, want)
+
+
+@pytest.mark.gpu
+def test_gpu_aux_unreserve_and_remove():
+    """Unreserve and pod-delete deltas move the aux Requested columns like the oracle's Unreserve / RemovePod."""
+    cfg = F.build_config()
+    cl = _aux_cluster(400, seed=830)
+    pods = _aux_pods(1500, seed=831, frac=0.6)
+    st = _state_from_pods(cl.n, cfg, cl)
+    with Engine(cfg, cl.n) as e:
+        synth.load_into(e, cl)
+        e.stage(pods)
+        e.schedule_staged(0, 1000)
+        gn, _ = e.fetch(0, 1000)
+        on, _ = oracle.schedule(cfg, cl.nodes, cl.metrics, st, pods[:1000], cl.now_ns, 4)
+        np.testing.assert_array_equal(gn, on)
+        mask = np.zeros(1000, dtype=np.uint8)
+        mask[::3] = 1
+        e.unreserve(0, 1000, mask)
+        # pod delete of some pre-existing pods through kg_pods_remove
+        e.remove_pods(cl.existing_pods[:200], cl.existing_node[:200])
+        # the oracle's state after both: the existing pods left + the placed pods not unreserved
+        rm = oracle.states(cl.n)
+        keep = np.ones(len(cl.existing_pods), dtype=bool)
+        keep[:200] = False
+        oracle.add_pods(cfg, rm, cl.existing_pods[keep], cl.existing_node[keep])
+        placed = np.nonzero((on >= 0) & (mask == 0))[0]
+        oracle.add_pods(cfg, rm, pods[placed], on[placed])
+        gn2 = e.schedule(pods[1000:])[0]
+        on2, _ = oracle.schedule(cfg, cl.nodes, cl.metrics, rm, pods[1000:], cl.now_ns, 4)
+        np.testing.assert_array_equal(gn2, on2)
