@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define KG_ABI_VERSION 6
+#define KG_ABI_VERSION 7
 
 /* ---- resource slots (fixed order) ------------------------------------------------------- */
 enum {
@@ -233,7 +233,19 @@ typedef struct kg_node_metric {
   int64_t agg_duration_ns[KG_MAX_AGG];         /* AggregatedUsage.Duration                            */
   int64_t agg_usage[KG_MAX_AGG][KG_AGG_TYPES][2];  /* Usage[type] cpu (milli) / memory (bytes)       */
   int64_t agg_present[KG_MAX_AGG][KG_AGG_TYPES];   /* bit r: resource r in that ResourceList (0 = empty) */
+  int64_t report_interval_ns;                  /* Spec.CollectPolicy.ReportIntervalSeconds (0 = default 60 s,
+                                                  getNodeMetricReportInterval, loadaware/helper.go:43-48) */
 } kg_node_metric;
+
+/* One entry of NodeMetric.Status.PodsMetric (PodMetricInfo) as buildPodMetricMap (loadaware/helper.go:153-170)
+ * reads it: the pod's identity, its usage (cpu milli / memory bytes) and whether the pod is prod priority
+ * (GetPodPriorityClassWithDefault == koord-prod, for the ScoreAccordingProdUsage view). */
+typedef struct kg_pod_metric {
+  int64_t uid;                                 /* the pod's identity (same value as kg_pod.uid)        */
+  int64_t usage[2];                            /* PodUsage cpu (milli), memory (bytes)                 */
+  int64_t usage_present;                       /* bit r: resource r is a key of PodUsage               */
+  int64_t prod;                                /* the pod's priority class is koord-prod               */
+} kg_pod_metric;
 
 /* One pod, pre-decoded by the caller (PodRequestsAndLimits semantics, pkg/util/pod_resources_utils.go:48-64). */
 typedef struct kg_pod {
@@ -253,6 +265,9 @@ typedef struct kg_pod {
                                                /* MatchReservationOwners pkg/util/reservation:389-410) once per */
                                                /* distinct owner spec; 0 = matches none                         */
   int64_t reservation_flags;                   /* KG_POD_RSV_*                                        */
+  int64_t uid;                                 /* the pod's identity (matches kg_pod_metric.uid; 0 = none)  */
+  int64_t assign_time_unix_nano;               /* kg_pods_add: the podAssignCache timestamp of the pod  */
+                                               /* (pod_assign_cache.go:62-66); scheduled pods take the engine clock */
 } kg_pod;
 
 /* pod reservation flags */
@@ -373,6 +388,12 @@ int kg_engine_create_loopback(const kg_config* cfg, int64_t capacity_nodes, int 
 int kg_nodes_upsert(kg_engine* e, const kg_node* nodes, const int32_t* idx, int64_t n);
 int kg_nodes_delete(kg_engine* e, const int32_t* idx, int64_t n);
 int kg_node_metrics_update(kg_engine* e, const kg_node_metric* m, const int32_t* idx, int64_t n, int64_t now_unix_nano);
+/* NodeMetric.Status.PodsMetric of one node (replaces the node's list; informer delta, like kg_node_metrics_update).
+ * LoadAware Score then follows estimatedAssignedPodUsed / sumPodUsages (load_aware.go:283-376): an assigned pod whose
+ * usage is reported and who was assigned before the metric's update time (and not within the report interval) counts
+ * through NodeUsage; the others are estimated as max(EstimatePod, reported usage), and their reported usage is taken
+ * out of NodeUsage (or, for a prod pod under ScoreAccordingProdUsage, the prod pods' reported usages replace it). */
+int kg_node_pods_metric_set(kg_engine* e, int32_t node_idx, const kg_pod_metric* m, int64_t n);
 
 int kg_pods_add(kg_engine* e, const kg_pod* pods, const int32_t* node_idx, int64_t n);
 int kg_pods_remove(kg_engine* e, const kg_pod* pods, const int32_t* node_idx, int64_t n);
@@ -496,7 +517,7 @@ int kg_debug_stamps(kg_engine* e, uint64_t* out);
 const char* kg_last_error(void);
 int kg_abi_version(void);
 /* sizeof of the ABI structs (0 kg_config, 1 kg_node, 2 kg_node_metric, 3 kg_pod, 4 kg_stats, 5 kg_node_numa,
- * 6 kg_node_device, 7 kg_quota, 8 kg_node_reservations) for
+ * 6 kg_node_device, 7 kg_quota, 8 kg_node_reservations, 9 kg_pod_metric) for
  * binding checks. */
 int64_t kg_abi_struct_size(int which);
 

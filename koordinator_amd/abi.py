@@ -35,7 +35,7 @@ POD_REQUEST_KEYS, POD_CPU_KEY, POD_MEM_KEY = 8, 16, 32
 MAX_OWNER_GROUPS = 64
 QUOTA_RES = 8
 MAX_QUOTAS = 64
-ABI_VERSION = 6
+ABI_VERSION = 7
 MAX_RSV_SLOTS = 4
 RSV_POLICY = {"Default": 0, "Aligned": 1, "Restricted": 2}
 POD_RSV_AFFINITY = 1
@@ -110,7 +110,9 @@ METRIC_DTYPE = np.dtype([
     _i64("pods_metric_count"),
     _i64("prod_pods_usage", RES_MAX),
     _i64("agg_count"), _i64("agg_duration_ns", 4), ("agg_usage", np.int64, (4, 5, 2)), ("agg_present", np.int64, (4, 5)),
+    _i64("report_interval_ns"),
 ])
+POD_METRIC_DTYPE = np.dtype([_i64("uid"), _i64("usage", 2), _i64("usage_present"), _i64("prod")])
 AGG_TYPES = {"": 0, "avg": 1, "p50": 2, "p90": 3, "p95": 4, "p99": 5}
 
 POD_DTYPE = np.dtype([
@@ -123,6 +125,7 @@ POD_DTYPE = np.dtype([
     _i64("device_requests", DEV_RES_MAX),
     _i64("quota_id"),
     _i64("reservation_owner_mask"), _i64("reservation_flags"),
+    _i64("uid"), _i64("assign_time_unix_nano"),
 ])
 
 NODE_RSV_DTYPE = np.dtype([_i64("n")] + [_i64(f, MAX_RSV_SLOTS) for f in (
@@ -152,7 +155,7 @@ STATS_DTYPE = np.dtype([
 ])
 
 STRUCT_DTYPES = {0: CONFIG_DTYPE, 1: NODE_DTYPE, 2: METRIC_DTYPE, 3: POD_DTYPE, 4: STATS_DTYPE, 5: NODE_NUMA_DTYPE,
-                 6: NODE_DEVICE_DTYPE, 7: QUOTA_DTYPE, 8: NODE_RSV_DTYPE}
+                 6: NODE_DEVICE_DTYPE, 7: QUOTA_DTYPE, 8: NODE_RSV_DTYPE, 9: POD_METRIC_DTYPE}
 
 # Every symbol include/koordgpu.h declares (tests check the library exports all of them).
 EXPORTED_SYMBOLS = (
@@ -166,6 +169,7 @@ EXPORTED_SYMBOLS = (
     "kg_quotas_set", "kg_quotas_read", "kg_nodes_reservation_upsert", "kg_nodes_read_reservations",
     "kg_results_fetch_reservations", "kg_profile_enable", "kg_profile_read", "kg_loopback_create",
     "kg_loopback_destroy", "kg_engine_create_loopback", "kg_pods_unreserve", "kg_engine_set_clock",
+    "kg_node_pods_metric_set",
 )
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
@@ -199,6 +203,7 @@ def load_library(path: str | None = None):
         "kg_nodes_upsert": (i, [vp, vp, vp, i64]),
         "kg_nodes_delete": (i, [vp, vp, i64]),
         "kg_node_metrics_update": (i, [vp, vp, vp, i64, i64]),
+        "kg_node_pods_metric_set": (i, [vp, i, vp, i64]),
         "kg_pods_add": (i, [vp, vp, vp, i64]),
         "kg_pods_remove": (i, [vp, vp, vp, i64]),
         "kg_pods_schedule": (i, [vp, vp, i64, vp, vp, vp]),

@@ -1939,7 +1939,27 @@ struct kg_engine {
   // host mirror of static / ingest state
   std::vector<kg_node> nodes;
   std::vector<kg_node_metric> metrics;
-  std::vector<int64_t> folded_usage;  // NodeUsage currently folded into la_used (2 per node)
+  std::vector<int64_t> folded_usage;  // node-level term currently folded into la_used (2 per node): NodeUsage, or with
+                                      // PodsMetric NodeUsage minus the estimated pods' usage + the pods' corrections
+  std::vector<int64_t> folded_prod;   // the same for la_pused (the ScoreAccordingProdUsage view), 2 per node
+  // podAssignCache mirror (pod_assign_cache.go:35-45) and NodeMetric.Status.PodsMetric per node: the PodsMetric
+  // LoadAware Score terms (load_aware.go:283-376) are host-side functions of these, folded into la_used / la_pused
+  struct AssignedPod {
+    int64_t uid, time, est[2];
+    int32_t prod;
+  };
+  struct PodMetricRec {
+    int64_t uid, usage[2], present;
+    int32_t prod;
+  };
+  std::vector<std::vector<AssignedPod>> assigned;
+  std::vector<std::vector<PodMetricRec>> pmetrics;
+  int64_t pm_nodes = 0;                  // nodes with a non-empty PodsMetric list
+  std::vector<AssignedPod> staged_info;  // the staged pods' (uid, est, prod) for the mirror
+  struct PendingPlace {
+    int64_t first, count, time;
+  };
+  std::vector<PendingPlace> pending_place;  // scheduled staged ranges not yet in the mirror (flush_placements)
   std::vector<int64_t> now_of;        // metric ingest time per node
   bool static_dirty = true;
   // scheduler clock for isNodeMetricExpired (kg_engine_set_clock): 0 = the newest now given to
@@ -2556,6 +2576,97 @@ void usage_for_score(const kg_config& c, const kg_node_metric& m, int64_t u[2]) 
   for (int r = 0; r < 2; ++r) u[r] = (m.present && m.has_node_metric && m.node_usage_present[r]) ? m.node_usage[r] : 0;
 }
 
+// The node-level LoadAware Score terms with PodsMetric (load_aware.go:283-376), relative to what the device adds per
+// assigned pod (its EstimatePod): out[0..1] = the non-prod view folded into la_used, out[2..3] = the prod view
+// (ScoreAccordingProdUsage) folded into la_pused.  An assigned pod is estimated when its usage is not reported,
+// or it was assigned after the metric's update time, or within the report interval before it, or the aggregated
+// score usage is missing (estimatedAssignedPodUsed :337-376); it then counts max(EstimatePod, reported usage) and its
+// reported usage leaves NodeUsage when NodeUsage covers it (:307-326); otherwise its usage is already in NodeUsage
+// (non-prod view) or in the prod pods' reported usages (prod view), and its EstimatePod is taken back out.
+void la_node_terms(const kg_engine* e, int64_t i, int64_t out[4]) {
+  const kg_config& c = e->cfg;
+  const kg_node_metric& m = e->metrics[i];
+  int64_t u[2];
+  usage_for_score(c, m, u);
+  const auto& pm = e->pmetrics[i];
+  out[0] = u[0], out[1] = u[1], out[2] = 0, out[3] = 0;
+  if (pm.empty() || !m.present) return;  // nil podMetrics: every assigned pod is estimated (:355)
+  const int64_t upd = m.has_update_time ? m.update_time_unix_nano : INT64_MIN;  // zero time: before every assign
+  const int64_t interval = m.report_interval_ns > 0 ? m.report_interval_ns : 60ll * 1000000000ll;
+  const bool agg_nil = c.la_agg_score_type != KG_AGG_NONE && agg_index(m, c.la_agg_score_duration_ns, c.la_agg_score_type) < 0;
+  for (int view = 0; view < 2; ++view) {  // 0: all pods (non-prod), 1: prod pods only (buildPodMetricMap filterProdPod)
+    int64_t corr[2] = {0, 0}, est_usage[2] = {0, 0}, act_usage[2] = {0, 0};
+    std::vector<char> estimated(pm.size(), 0);
+    for (const auto& a : e->assigned[i]) {
+      if (view == 1 && !a.prod) continue;
+      int hit = -1;
+      if (a.uid != 0)
+        for (size_t q = 0; q < pm.size(); ++q)
+          if (pm[q].uid == a.uid && (view == 0 || pm[q].prod)) {
+            hit = (int)q;
+            break;
+          }
+      const bool reported = hit >= 0 && pm[hit].present != 0;
+      const bool missed = a.time > upd;
+      const bool in_interval = a.time < upd && upd - a.time < interval;
+      if (!reported || missed || in_interval || agg_nil) {
+        for (int r = 0; r < 2; ++r) {
+          int64_t v = a.est[r];
+          if (reported && ((pm[hit].present >> r) & 1) && pm[hit].usage[r] > v) v = pm[hit].usage[r];
+          corr[r] += v - a.est[r];
+        }
+        if (hit >= 0) estimated[hit] = 1;
+      } else {
+        for (int r = 0; r < 2; ++r) corr[r] -= a.est[r];
+      }
+    }
+    for (size_t q = 0; q < pm.size(); ++q) {  // sumPodUsages (helper.go:172-186)
+      if (view == 1 && !pm[q].prod) continue;
+      for (int r = 0; r < 2; ++r) {
+        if (!((pm[q].present >> r) & 1)) continue;
+        (estimated[q] ? est_usage : act_usage)[r] += pm[q].usage[r];
+      }
+    }
+    if (view == 0) {
+      for (int r = 0; r < 2; ++r) {
+        int64_t nu = u[r];
+        if (est_usage[r] != 0 && nu >= est_usage[r]) nu -= est_usage[r];
+        out[r] = nu + corr[r];
+      }
+    } else {
+      for (int r = 0; r < 2; ++r) out[2 + r] = act_usage[r] + corr[r];
+    }
+  }
+}
+
+// Re-folds node i's LoadAware terms into la_used / la_pused (a delta against what is folded now)
+void la_refold(kg_engine* e, int64_t i, std::vector<RowDelta>& d) {
+  int64_t t[4];
+  la_node_terms(e, i, t);
+  RowDelta x{};
+  x.idx = i;
+  x.d[5] = t[0] - e->folded_usage[2 * i];
+  x.d[6] = t[1] - e->folded_usage[2 * i + 1];
+  x.d[7] = t[2] - e->folded_prod[2 * i];
+  x.d[8] = t[3] - e->folded_prod[2 * i + 1];
+  e->folded_usage[2 * i] = t[0];
+  e->folded_usage[2 * i + 1] = t[1];
+  e->folded_prod[2 * i] = t[2];
+  e->folded_prod[2 * i + 1] = t[3];
+  if (x.d[5] || x.d[6] || x.d[7] || x.d[8]) d.push_back(x);
+}
+
+// podAssignCache mirror: assign (Reserve / informer add) and unAssign (Unreserve / delete) of one pod
+void mirror_assign(kg_engine* e, int64_t i, const kg_engine::AssignedPod& a) { e->assigned[i].push_back(a); }
+void mirror_unassign(kg_engine* e, int64_t i, int64_t uid, const int64_t est[2]) {
+  auto& v = e->assigned[i];
+  for (size_t q = 0; q < v.size(); ++q)
+    if ((uid != 0 && v[q].uid == uid) || (uid == 0 && v[q].uid == 0 && v[q].est[0] == est[0] && v[q].est[1] == est[1])) {
+      v.erase(v.begin() + (long)q);
+      return;
+    }
+}
+
 struct RoundGeom {
   int64_t N, shard, base, n_local;
   int nt_local, B, ppw, bitmap_words;
@@ -3033,6 +3144,7 @@ int64_t kg_abi_struct_size(int which) {
     case 6: return sizeof(kg_node_device);
     case 7: return sizeof(kg_quota);
     case 8: return sizeof(kg_node_reservations);
+    case 9: return sizeof(kg_pod_metric);
   }
   return -1;
 }
@@ -3149,6 +3261,9 @@ static int engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank,
   e->nodes.assign(cap, kg_node{});
   e->metrics.assign(cap, kg_node_metric{});
   e->folded_usage.assign(2 * cap, 0);
+  e->folded_prod.assign(2 * cap, 0);
+  e->assigned.assign(cap, {});
+  e->pmetrics.assign(cap, {});
   e->now_of.assign(cap, 0);
   // EvalParams
   const kg_config& c = e->cfg;
@@ -3387,29 +3502,39 @@ int kg_nodes_delete(kg_engine* e, const int32_t* idx, int64_t n) {
   return 0;
 }
 
+static int flush_placements(kg_engine* e);
+
+int kg_node_pods_metric_set(kg_engine* e, int32_t node_idx, const kg_pod_metric* m, int64_t n) {
+  if (!e || (n > 0 && !m)) return fail(KG_E_INVALID, "null argument");
+  if (node_idx < 0 || node_idx >= e->capacity) return fail(KG_E_INVALID, "node index");
+  if (int rc = flush_placements(e)) return rc;
+  auto& v = e->pmetrics[node_idx];
+  const bool was = !v.empty();
+  v.clear();
+  for (int64_t k = 0; k < n; ++k)
+    v.push_back(kg_engine::PodMetricRec{m[k].uid, {m[k].usage[0], m[k].usage[1]}, m[k].usage_present & 3,
+                                        m[k].prod ? 1 : 0});
+  e->pm_nodes += (int64_t)(!v.empty()) - (int64_t)was;
+  std::vector<RowDelta> d;
+  la_refold(e, node_idx, d);
+  return push_deltas(e, d);
+}
+
 int kg_node_metrics_update(kg_engine* e, const kg_node_metric* m, const int32_t* idx, int64_t n, int64_t now) {
   if (!e || (n > 0 && (!m || !idx))) return fail(KG_E_INVALID, "null argument");
   for (int64_t k = 0; k < n; ++k) {
     if (idx[k] < 0 || idx[k] >= e->capacity) return fail(KG_E_INVALID, "node index");
-    if (e->cfg.la_score && m[k].present && m[k].pods_metric_count != 0)
-      return fail(KG_E_UNSUPPORTED, "PodsMetric-based LoadAware scoring is not accelerated (node %d)", idx[k]);
   }
+  if (e->pm_nodes > 0)
+    if (int rc = flush_placements(e)) return rc;
   std::vector<RowDelta> d;
   d.reserve(n);
   for (int64_t k = 0; k < n; ++k) {
     const int64_t i = idx[k];
-    int64_t u[2];
-    usage_for_score(e->cfg, m[k], u);
-    RowDelta x{};
-    x.idx = i;
-    x.d[5] = u[0] - e->folded_usage[2 * i];
-    x.d[6] = u[1] - e->folded_usage[2 * i + 1];
-    e->folded_usage[2 * i] = u[0];
-    e->folded_usage[2 * i + 1] = u[1];
     e->metrics[i] = m[k];
     e->now_of[i] = now;
     e->clock_metrics = std::max(e->clock_metrics, now);
-    if (x.d[5] || x.d[6]) d.push_back(x);
+    la_refold(e, i, d);
   }
   e->static_dirty = true;
   return push_deltas(e, d);
@@ -3417,6 +3542,8 @@ int kg_node_metrics_update(kg_engine* e, const kg_node_metric* m, const int32_t*
 
 static int pods_delta(kg_engine* e, const kg_pod* pods, const int32_t* node_idx, int64_t n, int sign) {
   if (!e || (n > 0 && (!pods || !node_idx))) return fail(KG_E_INVALID, "null argument");
+  if (sign < 0)  // a delete may name a pod this engine placed
+    if (int rc = flush_placements(e)) return rc;
   std::vector<RowDelta> d(n);
   for (int64_t k = 0; k < n; ++k) {
     const int64_t i = node_idx[k];
@@ -3436,6 +3563,22 @@ static int pods_delta(kg_engine* e, const kg_pod* pods, const int32_t* node_idx,
     x.d[7] = (p.flags & P_PROD) ? la * p.est_cpu : 0;
     x.d[8] = (p.flags & P_PROD) ? la * p.est_mem : 0;
     for (int r = 0; r < kAux; ++r) x.aux[r] = sign * pods[k].requests[kAuxFirst + r];
+    if (la) {  // the podAssignCache mirror (reserve pods are not in the assign cache)
+      const int64_t est[2] = {p.est_cpu, p.est_mem};
+      if (sign > 0)
+        mirror_assign(e, i, kg_engine::AssignedPod{pods[k].uid, pods[k].assign_time_unix_nano, {est[0], est[1]},
+                                                   (p.flags & P_PROD) ? 1 : 0});
+      else
+        mirror_unassign(e, i, pods[k].uid, est);
+    }
+  }
+  if (e->pm_nodes > 0) {  // the PodsMetric terms of the touched nodes
+    std::vector<char> seen((size_t)e->capacity, 0);
+    for (int64_t k = 0; k < n; ++k) {
+      const int64_t i = node_idx[k];
+      if (!seen[i] && !e->pmetrics[i].empty()) la_refold(e, i, d);
+      seen[i] = 1;
+    }
   }
   return push_deltas(e, d);
 }
@@ -3454,6 +3597,20 @@ int kg_pods_unreserve(kg_engine* e, int64_t first, int64_t count, const uint8_t*
   for (int64_t k = 0; k < count; ++k)
     if (!mask || mask[k]) idx.push_back(first + k);
   if (idx.empty()) return 0;
+  if (int rc = flush_placements(e)) return rc;
+  {  // podAssignCache.unAssign of the placed ones, then the PodsMetric terms of their nodes
+    std::vector<uint64_t> keys((size_t)count);
+    HIP_TRY(hipMemcpy(keys.data(), e->out_keys.p + first, count * 8, hipMemcpyDeviceToHost));
+    std::vector<RowDelta> d;
+    for (int64_t j : idx) {
+      const uint64_t key = keys[j - first];
+      if (!key) continue;
+      const int64_t i = (int64_t)(0xFFFFFFFFu - (uint32_t)key);
+      mirror_unassign(e, i, e->staged_info[j].uid, e->staged_info[j].est);
+      if (!e->pmetrics[i].empty()) la_refold(e, i, d);
+    }
+    if (int rc = push_deltas(e, d)) return rc;
+  }
   if (int rc = e->uidx.ensure(idx.size())) return rc;
   HIP_TRY(hipMemcpyAsync(e->uidx.p, idx.data(), idx.size() * 8, hipMemcpyHostToDevice, e->stream));
   unreserve_pods<<<1, 1, 0, e->stream>>>(e->T, e->pods.p, e->uidx.p, (int64_t)idx.size(), e->out_keys.p,
@@ -3483,6 +3640,10 @@ int kg_pods_stage(kg_engine* e, const kg_pod* pods, int64_t n) {
   std::vector<DevPod> h(std::max<int64_t>(n, 1));
   for (int64_t k = 0; k < n; ++k)
     if (int rc = decode_pod(e, pods[k], h[k])) return rc;
+  if (int rc = flush_placements(e)) return rc;  // before the staged queue is replaced
+  e->staged_info.resize((size_t)n);
+  for (int64_t k = 0; k < n; ++k)
+    e->staged_info[k] = kg_engine::AssignedPod{pods[k].uid, 0, {h[k].est_cpu, h[k].est_mem}, (h[k].flags & P_PROD) ? 1 : 0};
   if (int rc = e->pods.ensure(n + kMaxB)) return rc;
   if (int rc = e->out_keys.ensure(n + kMaxB)) return rc;
   if (n > 0) HIP_TRY(hipMemcpyAsync(e->pods.p, h.data(), n * sizeof(DevPod), hipMemcpyHostToDevice, e->stream));
@@ -3546,7 +3707,35 @@ int kg_pods_stage(kg_engine* e, const kg_pod* pods, int64_t n) {
   return 0;
 }
 
+static int schedule_staged_impl(kg_engine* e, int64_t first, int64_t count, kg_stats* stats);
+// the placed pods enter the podAssignCache mirror (LoadAware Reserve → assign, timestamp = the engine clock; a pod
+// placed under the default clock, the newest NodeMetric update, is taken as assigned just after it)
+// Reserve → podAssignCache.assign (load_aware.go:260-263) of the pods a schedule call placed.  The mirror only
+// feeds the PodsMetric terms, so the placed ranges are recorded and read back lazily: right away when some node
+// reports PodsMetric, otherwise before the next call that reads or rewrites the mirror or the staged queue.
+static int flush_placements(kg_engine* e) {
+  std::vector<uint64_t> keys;
+  for (const auto& r : e->pending_place) {
+    keys.resize((size_t)r.count);
+    HIP_TRY(hipMemcpy(keys.data(), e->out_keys.p + r.first, r.count * 8, hipMemcpyDeviceToHost));
+    for (int64_t k = 0; k < r.count; ++k) {
+      if (!keys[k]) continue;
+      kg_engine::AssignedPod a = e->staged_info[r.first + k];
+      a.time = r.time;
+      mirror_assign(e, (int64_t)(0xFFFFFFFFu - (uint32_t)keys[k]), a);
+    }
+  }
+  e->pending_place.clear();
+  return 0;
+}
 int kg_pods_schedule_staged(kg_engine* e, int64_t first, int64_t count, kg_stats* stats) {
+  if (int rc = schedule_staged_impl(e, first, count, stats)) return rc;
+  if (count == 0) return 0;
+  // the assign time: after this call's clock (clock mode 0 keeps the newest metric time, so +1 ns = after it)
+  e->pending_place.push_back({first, count, e->clock_now + (e->clock_mode == 0 ? 1 : 0)});
+  return e->pm_nodes > 0 ? flush_placements(e) : 0;
+}
+static int schedule_staged_impl(kg_engine* e, int64_t first, int64_t count, kg_stats* stats) {
   if (!e) return fail(KG_E_INVALID, "engine is NULL");
   if (first < 0 || count < 0 || first + count > e->n_staged) return fail(KG_E_INVALID, "staged range");
   const double t0 = now_s();
@@ -3664,6 +3853,8 @@ int kg_nodes_read_state(kg_engine* e, int64_t* req_cpu, int64_t* req_mem, int64_
   for (int64_t i = 0; i < n; ++i) {
     if (la_est_cpu) la_est_cpu[i] -= e->folded_usage[2 * i];
     if (la_est_mem) la_est_mem[i] -= e->folded_usage[2 * i + 1];
+    if (la_pcpu) la_pcpu[i] -= e->folded_prod[2 * i];
+    if (la_pmem) la_pmem[i] -= e->folded_prod[2 * i + 1];
   }
   return 0;
 }

@@ -107,6 +107,12 @@ class Engine:
         idx = self._idx(idx, len(metrics))
         check(self.lib, self.lib.kg_node_metrics_update(self.h, ptr(metrics), ptr(idx), len(metrics), int(now_ns)))
 
+    def set_pods_metric(self, node: int, entries: np.ndarray):
+        """kg_node_pods_metric_set: NodeMetric.Status.PodsMetric of one node (POD_METRIC_DTYPE rows)."""
+        entries = np.ascontiguousarray(entries, dtype=abi.POD_METRIC_DTYPE)
+        check(self.lib, self.lib.kg_node_pods_metric_set(self.h, int(node), ptr(entries) if len(entries) else None,
+                                                          len(entries)))
+
     def add_pods(self, pods: np.ndarray, node_idx):
         pods = np.ascontiguousarray(pods, dtype=abi.POD_DTYPE)
         node_idx = np.ascontiguousarray(node_idx, dtype=np.int32)

@@ -177,7 +177,7 @@ def make_node(allocatable: dict, allowed_pods: int = 110, raw_allocatable: dict 
 
 def make_node_metric(present: bool = True, update_time_ns: int | None = 0, node_usage: dict | None = None,
                      prod_pods_usage: dict | None = None, pods_metric_count: int = 0,
-                     aggregated: list | None = None) -> np.ndarray:
+                     aggregated: list | None = None, report_interval_ns: int = 0) -> np.ndarray:
     """NodeMetric status summary; node_usage=None means Status.NodeMetric == nil.  aggregated = the
     AggregatedNodeUsages [{"duration_s": .., "p95": {"cpu": .., "memory": ..}, ...}]."""
     m = np.zeros(1, dtype=abi.METRIC_DTYPE)
@@ -193,6 +193,7 @@ def make_node_metric(present: bool = True, update_time_ns: int | None = 0, node_
             pres[abi.RESOURCE_SLOTS[k]] = 1
         r["node_usage_present"] = pres
     r["pods_metric_count"] = pods_metric_count
+    r["report_interval_ns"] = report_interval_ns  # CollectPolicy.ReportIntervalSeconds; 0 = the 60 s default
     r["prod_pods_usage"] = _values(prod_pods_usage)
     aggs = aggregated or []
     if len(aggs) > 4:

@@ -209,22 +209,96 @@ int64_t or_least_requested_score(int64_t requested, int64_t capacity) {
   return ((capacity - requested) * MAX_NODE_SCORE) / capacity;
 }
 
+/* NodeUsage (or the aggregated score usage) of the all-pods view, per resource present: load_aware.go:307-320 */
+static void score_node_usage(const kg_config* cfg, const kg_node_metric* m, int64_t u[2], int present[2]) {
+  u[0] = u[1] = 0;
+  present[0] = present[1] = 0;
+  if (!m->has_node_metric) return;
+  if (cfg->la_agg_score_type != KG_AGG_NONE) {
+    const int i = target_aggregated(m, cfg->la_agg_score_duration_ns, cfg->la_agg_score_type);
+    if (i < 0) return;
+    for (int r = 0; r < 2; r++) {
+      u[r] = aggregated_value(m, i, cfg->la_agg_score_type, r);
+      present[r] = 1;
+    }
+    return;
+  }
+  for (int r = 0; r < 2; r++)
+    if (m->node_usage_present[r]) {
+      u[r] = m->node_usage[r];
+      present[r] = 1;
+    }
+}
+
+/* estimatedAssignedPodUsed (load_aware.go:337-376), sumPodUsages (helper.go:172-186) and the two views of
+ * Score (:296-326).  view 1 = buildPodMetricMap with filterProdPod and the prod-filtered assign cache. */
+void or_la_node_terms(const kg_config* cfg, const kg_node_metric* m, const kg_pod_metric* pm, int64_t n_pm,
+                      const or_assigned* as, int64_t n_as, int64_t out[4]) {
+  int64_t nu[2];
+  int present[2];
+  score_node_usage(cfg, m, nu, present);
+  const int64_t upd = m->has_update_time ? m->update_time_unix_nano : INT64_MIN;
+  const int64_t interval = m->report_interval_ns > 0 ? m->report_interval_ns : 60LL * 1000000000LL; /* helper.go:43-48 */
+  const int agg_nil = cfg->la_agg_score_type != KG_AGG_NONE &&
+                      target_aggregated(m, cfg->la_agg_score_duration_ns, cfg->la_agg_score_type) < 0;
+  for (int view = 0; view < 2; view++) {
+    int64_t used[2] = {0, 0};       /* Σ over estimated pods of (counted value − EstimatePod) − Σ non-estimated EstimatePod */
+    int64_t est_pods_usage[2] = {0, 0}, pods_usage[2] = {0, 0};
+    char estimated[256] = {0};
+    for (int64_t a = 0; a < n_as; a++) {
+      if (view == 1 && !as[a].prod) continue;                                          /* :350-352 */
+      int64_t hit = -1;
+      for (int64_t q = 0; as[a].uid != 0 && q < n_pm && q < 256; q++)
+        if (pm[q].uid == as[a].uid && (view == 0 || pm[q].prod)) { hit = q; break; }   /* podMetrics[podName] */
+      const int has_usage = hit >= 0 && (pm[hit].usage_present & 3) != 0;              /* len(podUsage) != 0 */
+      const int missed = as[a].time > upd;                                             /* helper.go:50-52 */
+      const int still = as[a].time < upd && upd - as[a].time < interval;               /* helper.go:54-56 */
+      if (!has_usage || missed || still || agg_nil) {                                  /* :355-359 */
+        for (int r = 0; r < 2; r++) {
+          int64_t v = as[a].est[r];
+          if (hit >= 0 && ((pm[hit].usage_present >> r) & 1) && pm[hit].usage[r] > v) v = pm[hit].usage[r]; /* :364-369 */
+          used[r] += v - as[a].est[r];
+        }
+        if (hit >= 0) estimated[hit] = 1;                                              /* estimatedPods.Insert */
+      } else {
+        for (int r = 0; r < 2; r++) used[r] -= as[a].est[r];  /* counted through the reported usages instead */
+      }
+    }
+    for (int64_t q = 0; q < n_pm && q < 256; q++) {
+      if (view == 1 && !pm[q].prod) continue;
+      for (int r = 0; r < 2; r++)
+        if ((pm[q].usage_present >> r) & 1) (estimated[q] ? est_pods_usage : pods_usage)[r] += pm[q].usage[r];
+    }
+    if (view == 1) {                                                                   /* :302-305 */
+      for (int r = 0; r < 2; r++) out[2 + r] = pods_usage[r] + used[r];
+    } else {                                                                           /* :306-326 */
+      for (int r = 0; r < 2; r++) {
+        int64_t q = nu[r];
+        if (present[r] && est_pods_usage[r] != 0 && q >= est_pods_usage[r]) q -= est_pods_usage[r];
+        out[r] = (present[r] ? q : 0) + used[r];
+      }
+    }
+  }
+}
+
 /* loadaware/load_aware.go:269-335 Score (+ estimatedAssignedPodUsed :337-376, scorer :378-386).
- * PodsMetric is empty in the restated profile (helper.go:153-156 → nil map), so every assigned pod is estimated
- * (:354) and no pod usage is subtracted from NodeUsage (:317). */
+ * Without PodsMetric (helper.go:153-156 → nil map) every assigned pod is estimated (:354) and no pod usage is
+ * subtracted from NodeUsage (:317); with it, the state carries or_la_node_terms. */
 int64_t or_loadaware_score(const kg_config* cfg, const kg_node* node, const kg_node_metric* m,
                            const or_node_state* st, const kg_pod* pod, int64_t now) {
   if (!m->present) return 0;                                                          /* :278-284 */
   if (cfg->la_node_metric_expiration_seconds >= 0 &&
       node_metric_expired(m, cfg->la_node_metric_expiration_seconds, now))
     return 0;                                                                         /* :287-289 */
-  if (m->pods_metric_count != 0) return -1;
+  if (m->pods_metric_count != 0 && !st->has_la_term) return -1;
   int prod_pod = pod->priority_class == KG_PRIO_PROD && cfg->la_score_according_prod_usage; /* :291 */
   int64_t est[2];
   or_estimate_pod(cfg, pod, est);                                                     /* :294 */
   int64_t used[2];
   for (int r = 0; r < 2; r++) used[r] = est[r] + (prod_pod ? st->la_est_prod[r] : st->la_est_all[r]); /* :298-301 */
-  if (!prod_pod && m->has_node_metric) {                                              /* :307-326 */
+  if (st->has_la_term) {
+    for (int r = 0; r < 2; r++) used[r] += st->la_term[(prod_pod ? 2 : 0) + r];
+  } else if (!prod_pod && m->has_node_metric) {                                       /* :307-326 */
     if (cfg->la_agg_score_type != KG_AGG_NONE) { /* scoreWithAggregation: the aggregated usage, nil → none */
       const int i = target_aggregated(m, cfg->la_agg_score_duration_ns, cfg->la_agg_score_type);
       if (i >= 0)

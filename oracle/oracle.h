@@ -29,7 +29,20 @@ typedef struct or_node_state {
   int64_t num_pods;                  /* len(NodeInfo.Pods)                                    */
   int64_t la_est_all[2];             /* Σ EstimatePod over podAssignCache[node] (cpu, mem)    */
   int64_t la_est_prod[2];            /* same, prod-priority pods only                         */
+  /* PodsMetric present (or_la_node_terms): the node-level LoadAware Score terms beside Σ EstimatePod —
+   * [0..1] the all-pods view (replaces NodeUsage), [2..3] the prod view (ScoreAccordingProdUsage) */
+  int64_t la_term[4];
+  int64_t has_la_term;
 } or_node_state;
+
+/* One podAssignCache entry (pod_assign_cache.go:35-45) as the LoadAware PodsMetric terms read it. */
+typedef struct or_assigned {
+  int64_t uid, time, est[2], prod;
+} or_assigned;
+/* estimatedAssignedPodUsed + sumPodUsages + the NodeUsage subtraction (load_aware.go:283-376, helper.go:153-186):
+ * out[0..1] = the node-level used terms of the all-pods view beside Σ EstimatePod(assigned), out[2..3] the prod view. */
+void or_la_node_terms(const kg_config* cfg, const kg_node_metric* m, const kg_pod_metric* pm, int64_t n_pm,
+                      const or_assigned* as, int64_t n_as, int64_t out[4]);
 
 /* LoadAware estimator (estimator/default_estimator.go:57-108): out[0]=cpu, out[1]=memory. */
 void or_estimate_pod(const kg_config* cfg, const kg_pod* pod, int64_t out[2]);

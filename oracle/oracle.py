@@ -22,7 +22,10 @@ OR_STATE_DTYPE = np.dtype([
     ("num_pods", np.int64),
     ("la_est_all", np.int64, (2,)),
     ("la_est_prod", np.int64, (2,)),
+    ("la_term", np.int64, (4,)),
+    ("has_la_term", np.int64),
 ])
+OR_ASSIGNED_DTYPE = np.dtype([("uid", np.int64), ("time", np.int64), ("est", np.int64, (2,)), ("prod", np.int64)])
 
 _lib = None
 
@@ -39,6 +42,8 @@ def lib():
         L = ctypes.CDLL(LIB)
         vp, i64, i = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int
         L.or_estimate_pod.argtypes = [vp, vp, vp]
+        L.or_la_node_terms.argtypes = [vp, vp, vp, ctypes.c_int64, vp, ctypes.c_int64, vp]
+        L.or_la_node_terms.restype = None
         L.or_estimate_node.argtypes = [vp, i]
         L.or_estimate_node.restype = i64
         L.or_loadaware_filter.argtypes = [vp, vp, vp, vp, i64]
@@ -238,6 +243,21 @@ def loadaware_filter(cfg, node, metric, pod, now_ns: int) -> int:
 
 def loadaware_score(cfg, node, metric, state, pod, now_ns: int) -> int:
     return int(lib().or_loadaware_score(p(cfg), p(node), p(metric), p(state), p(pod), now_ns))
+
+
+def la_node_terms(cfg, metric, pods_metric, assigned) -> np.ndarray:
+    """or_la_node_terms: the PodsMetric LoadAware Score terms of one node ([0..1] all pods, [2..3] prod view)."""
+    pm = np.ascontiguousarray(pods_metric, dtype=abi.POD_METRIC_DTYPE)
+    a = np.ascontiguousarray(assigned, dtype=OR_ASSIGNED_DTYPE)
+    out = np.zeros(4, dtype=np.int64)
+    lib().or_la_node_terms(p(cfg), p(np.ascontiguousarray(np.asarray(metric, dtype=abi.METRIC_DTYPE).reshape(1))),
+                           p(pm) if len(pm) else None, len(pm), p(a) if len(a) else None, len(a), p(out))
+    return out
+
+
+def set_la_terms(st, i: int, terms):
+    st["la_term"][i] = terms
+    st["has_la_term"][i] = 1
 
 
 def fit_filter(node, state, pod) -> int:

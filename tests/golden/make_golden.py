@@ -11,8 +11,11 @@ Conventions for the LoadAware cases (load_aware_test.go harness :806-908 for Fil
 * Filter harness sets FilterExpiredNodeMetrics=false (:807); Score harness keeps the defaults (expiration 180s);
 * a nil test pod is &corev1.Pod{} (:573-576), whose default priority class is koord-batch (BestEffort → BE,
   apis/extension/priority_utils.go:26-48 + qos_utils.go);
-* scope "core" = restated and accelerated now (aggregated percentile usages included); scope "next" = needs
-  PodsMetric-based estimation — kept for completeness, skipped with a reason by the tests.
+* scope "core" = restated and accelerated now (aggregated percentile usages and the PodsMetric-based estimation of
+  assigned pods included); scope "next" = kept for completeness, skipped with a reason by the tests (none left);
+* an assigned pod's "name" matches NodeMetric.Status.PodsMetric entries by namespace/name; its timestamp is taken
+  before the metric's UpdateTime (the Go literal evaluates assignedPod first), so age 0 = 1 ns before the update;
+* "report_interval_s" = NodeMetric.Spec.CollectPolicy.ReportIntervalSeconds.
 
 Run: python tests/golden/make_golden.py   (rewrites the JSON files next to this script)
 """
@@ -95,10 +98,10 @@ SCORE_CASES = [
     dict(name="score load node with p95 but have not reported usage", line=1147,
          pod=dict(requests=G, limits=G), args=dict(score_aggregated=dict(type="p95", duration="5m")),
          metric=dict(update_age_s=0, node_usage={"cpu": "0", "memory": "0Gi"}), want=90),
-    dict(name="score load node with p95 but have not reported usage and have assigned pods", line=1203, scope="next",
+    dict(name="score load node with p95 but have not reported usage and have assigned pods", line=1203,
          pod=dict(requests=G, limits=G), args=dict(score_aggregated=dict(type="p95", duration="5m")),
-         assigned=[dict(requests=G, limits=G, age_s=600)],
-         metric=dict(update_age_s=0, node_usage={"cpu": "0", "memory": "0Gi"},
+         assigned=[dict(name="assigned-pod-1", requests=G, limits=G, age_s=600)],
+         metric=dict(update_age_s=0, report_interval_s=60, node_usage={"cpu": "0", "memory": "0Gi"},
                      pods_metric=[dict(name="assigned-pod-1", usage={"cpu": "1", "memory": "1Gi"})]),
          want=81),
     dict(name="score load node with just assigned pod", line=1300, pod=dict(requests=G, limits=G),
@@ -115,11 +118,11 @@ SCORE_CASES = [
                   requests={"kubernetes.io/batch-cpu": "16000", "kubernetes.io/batch-memory": "32Gi"},
                   limits={"kubernetes.io/batch-cpu": "16000", "kubernetes.io/batch-memory": "32Gi"}),
          metric=dict(update_age_s=0), want=90),
-    dict(name="score prod Pod", line=1588, scope="next", args=dict(score_according_prod_usage=True),
+    dict(name="score prod Pod", line=1588, args=dict(score_according_prod_usage=True),
          pod=dict(priority="koord-prod", requests={"cpu": "16000", "memory": "32Gi"},
                   limits={"cpu": "16000", "memory": "32Gi"}),
-         assigned=[dict(priority="koord-prod", requests=G, limits=G, age_s=0)],
-         metric=dict(update_age_s=0, pods_metric=[dict(name="assign-prod-pod-1", usage={"cpu": "30", "memory": "100Gi"})]),
+         assigned=[dict(name="assign-prod-pod-1", priority="koord-prod", requests=G, limits=G, age_s=0)],
+         metric=dict(update_age_s=0, report_interval_s=60, pods_metric=[dict(name="assign-prod-pod-1", usage={"cpu": "30", "memory": "100Gi"})]),
          want=38),
     dict(name="score request less than limit", line=1676,
          pod=dict(requests={"cpu": "8", "memory": "16Gi"}, limits=G), metric=dict(update_age_s=0), want=88),

@@ -2,6 +2,7 @@
 GPU parity tests."""
 import json
 import os
+import zlib
 
 import numpy as np
 
@@ -83,6 +84,7 @@ def metric(case):
         present=True, update_time_ns=None if age is None else NOW_NS - age * 10**9,
         node_usage=m.get("node_usage"), prod_pods_usage=m.get("prod_pods_usage"),
         pods_metric_count=m.get("pods_metric_count", len(m.get("pods_metric", []))),
+        report_interval_ns=m.get("report_interval_s", 0) * 10**9,
         aggregated=[dict({k: v for k, v in a.items() if k != "duration"}, duration_s=duration_s(a.get("duration")))
                     for a in m.get("aggregated", [])])
 
@@ -98,12 +100,56 @@ def pod(spec):
                               daemonset=spec.get("daemonset", False))
 
 
+def uid_of(name: str) -> int:
+    """A stable nonzero pod uid for namespace "default" + name (the fixtures match PodsMetric entries by name)."""
+    return zlib.crc32(("default/" + name).encode()) + 1
+
+
 def assigned(case):
+    """The case's assigned pods with uid and assign time (1 ns before NOW - age: the Go literal reads time.Now()
+    for podAssignInfo.timestamp before the NodeMetric's UpdateTime)."""
     specs = case.get("assigned") or []
     if not specs:
         return np.zeros(0, dtype=abi.POD_DTYPE)
-    return np.concatenate([pod(s) for s in specs])
+    out = np.concatenate([pod(s) for s in specs])
+    for k, s in enumerate(specs):
+        out[k]["uid"] = uid_of(s["name"]) if "name" in s else 0
+        out[k]["assign_time_unix_nano"] = NOW_NS - int(s.get("age_s", 0)) * 10**9 - 1
+    return out
+
+
+def pods_metric(case):
+    """NodeMetric.Status.PodsMetric as POD_METRIC_DTYPE rows.  buildPodMetricMap (loadaware/helper.go:153-170) drops
+    entries whose pod the lister does not know and sets prod from the listed pod's priority."""
+    m = case.get("metric") or {}
+    a = assigned(case)
+    by_uid = {int(r["uid"]): r for r in a}
+    rows = []
+    for e in m.get("pods_metric", []):
+        u = uid_of(e["name"])
+        if u not in by_uid:
+            continue
+        r = np.zeros(1, dtype=abi.POD_METRIC_DTYPE)
+        q = quantity_map(e.get("usage", {}))
+        r[0]["uid"] = u
+        r[0]["usage"] = (q.get("cpu", 0), q.get("memory", 0))
+        r[0]["usage_present"] = ("cpu" in q) | (("memory" in q) << 1)  # bit r: resource r reported
+        r[0]["prod"] = int(by_uid[u]["priority_class"] == abi.PRIO_PROD)
+        rows.append(r)
+    return np.concatenate(rows) if rows else np.zeros(0, dtype=abi.POD_METRIC_DTYPE)
 
 
 def quantity_map(d):
     return {k: resource_value(k, v) for k, v in d.items()}
+
+
+def oracle_assigned(cfg, pods):
+    """The oracle's record of assigned pods (uid, assign time, EstimatePod, prod) — the engine's mirror."""
+    from oracle import oracle
+    out = np.zeros(len(pods), dtype=oracle.OR_ASSIGNED_DTYPE)
+    for k in range(len(pods)):
+        out[k]["uid"] = pods[k]["uid"]
+        out[k]["time"] = pods[k]["assign_time_unix_nano"]
+        out[k]["est"] = oracle.estimate_pod(cfg, pods[k:k + 1])
+        out[k]["prod"] = int(pods[k]["priority_class"] == abi.PRIO_PROD)
+    return out

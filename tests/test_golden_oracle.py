@@ -47,16 +47,22 @@ def test_loadaware_score(dc):
     a = G.assigned(case)
     if len(a):
         oracle.add_pods(cfg, st, a, np.zeros(len(a), dtype=np.int32))
-    got = oracle.loadaware_score(cfg, G.node(doc, case), G.metric(case), st, G.pod(case.get("pod")), G.NOW_NS)
+    m = G.metric(case)
+    pm = G.pods_metric(case)
+    if len(pm):  # PodsMetric reported: the estimated / actual usage terms of the assigned pods
+        oracle.set_la_terms(st, 0, oracle.la_node_terms(cfg, m, pm, G.oracle_assigned(cfg, a)))
+    got = oracle.loadaware_score(cfg, G.node(doc, case), m, st, G.pod(case.get("pod")), G.NOW_NS)
     assert got == case["want"], case["source_line"]
 
 
-def test_next_scope_cases_are_recorded():
-    """The out-of-scope reference cases (PodsMetric-based estimation) stay in the fixtures, not silently dropped;
-    the aggregated-usage cases moved into scope (4 of the original 6)."""
+def test_every_reference_case_is_in_scope():
+    """The aggregated-usage cases (round 1) and the PodsMetric-based estimation cases (round 2, load_aware_test.go
+    :1203 and :1588) moved into scope: no fixture is skipped any more."""
     nxt = [c["name"] for f in ("loadaware_filter.json", "loadaware_score.json")
            for c in G.load(f)["cases"] if c["scope"] == "next"]
-    assert len(nxt) == 2, nxt
+    assert nxt == [], nxt
+    lines = {int(c["source_line"].rsplit(":", 1)[1]) for c in G.load("loadaware_score.json")["cases"]}
+    assert {1203, 1588} <= lines
 
 
 @pytest.mark.parametrize("req,cap,want", [(0, 0, 0), (5, 0, 0), (11, 10, 0), (10, 10, 0), (0, 10, 100),

@@ -54,6 +54,9 @@ def _one_node_engine(doc, case, profile):
     a = G.assigned(case)
     if len(a):
         e.add_pods(a, np.zeros(len(a), dtype=np.int32))
+    pm = G.pods_metric(case)
+    if len(pm):  # NodeMetric.Status.PodsMetric (load_aware_test.go:1203, :1588)
+        e.set_pods_metric(0, pm)
     return e
 
 
