@@ -996,12 +996,13 @@ struct NumaTable {
 };
 
 // Reference-shaped Fit + LoadAware (eval_node) + NodeNUMAResource Filter/Score of one node for one pod.
+// `aff` = the affinity NodeNUMAResource.Filter stores (valid when this returns true).
 __device__ __forceinline__ bool eval_node_numa(const Row& r, const NumaView& nv, const DevPod& p, const NumaPod& np,
-                                               const EvalParams& P, const NumaParams& NP, int64_t& total) {
+                                               const EvalParams& P, const NumaParams& NP, int64_t& total,
+                                               NumaHint& aff) {
   int64_t t = 0;
   if (!eval_node(r, p, P, t)) return false;
   int64_t sc = 0;
-  NumaHint aff;
   if (!numa_eval(nv, np, NP, r.req_cpu, r.req_mem, r.alloc_cpu, r.alloc_mem, sc, aff)) return false;
   total = t + (NP.score ? sc * NP.weight : 0);
   return true;
@@ -1133,6 +1134,7 @@ __global__ __launch_bounds__(kWave) void resolve_round_numa(DevTable T, NumaTabl
     const uint64_t ub = s_cand[(size_t)j * kCandStride + kC];
     const DevPod p = s_pods[j];
     const NumaPod np = s_np[j];
+    KG_POD_DIAG(j, (uint64_t)nM);
     if (nq > 0 && !quota_admit(ql, p)) {  // ElasticQuota PreFilter rejects
       my_out = lane == j ? 0 : my_out;
       ++consumed;
@@ -1143,15 +1145,17 @@ __global__ __launch_bounds__(kWave) void resolve_round_numa(DevTable T, NumaTabl
     const uint64_t um = __ballot(unmod);
     const int pos = um ? (int)__builtin_ctzll(um) : kC;
     uint64_t best = um ? readlane_u64(key, pos) : 0;
+    NumaHint maff{0, 1, 0, 0};  // the affinity of this lane's modified row (Reserve reuses it when it wins)
     if (nM > 0) {
       uint64_t mk = 0;
       if (lane < nM) {
         int64_t t = 0;
-        if (eval_node_numa(mrow, mv, p, np, P, NP, t)) mk = make_key(t, midx);
+        if (eval_node_numa(mrow, mv, p, np, P, NP, t, maff)) mk = make_key(t, midx);
       }
       const uint64_t mbest = wave_max_key(mk);
       best = mbest > best ? mbest : best;
     }
+    KG_POD_SUB(j, 0);
     if (best < ub) break;
     ++consumed;
     if (best == 0) {
@@ -1175,10 +1179,17 @@ __global__ __launch_bounds__(kWave) void resolve_round_numa(DevTable T, NumaTabl
       ++nM;
     }
     __syncthreads();
+    KG_POD_SUB(j, 1);
     int placed = 0;
-    if (lane == owner) {  // Reserve with the affinity Filter stores (recomputed on the same state)
-      NumaHint aff{0, 1, 0, 0};
-      if (NP.filter) (void)numa_filter(mv, np, NP, aff, mrow.req_cpu, mrow.alloc_cpu);
+    if (lane == owner) {  // Reserve with the affinity Filter stores (a fresh row's is computed on its state)
+      NumaHint aff = maff;
+      if (!hit) {
+        aff = NumaHint{0, 1, 0, 0};
+        if (NP.filter) (void)numa_filter(mv, np, NP, aff, mrow.req_cpu, mrow.alloc_cpu);
+      }
+#ifdef KG_STAMPS
+      if (j < 64) g_pod_diag[j][5] = __builtin_amdgcn_s_memtime();
+#endif
       CpuSet cpus;
       NumaAlloc rec;
       const NumaStatic ns = s_ns[lane];
@@ -1211,6 +1222,7 @@ __global__ __launch_bounds__(kWave) void resolve_round_numa(DevTable T, NumaTabl
       }
     }
     placed = __builtin_amdgcn_readlane(placed, owner);
+    KG_POD_SUB(j, 2);
     if (placed && nq > 0) quota_charge(ql, p, lane);
     my_out = lane == j ? (placed ? best : 0) : my_out;
     __syncthreads();

@@ -617,7 +617,19 @@ __device__ __forceinline__ int sc_at(uint64_t lo, uint64_t hi, int k) {
   return k < 9 ? (int)((lo >> (7 * k)) & 127u) : (int)((hi >> (7 * (k - 9))) & 127u);
 }
 
-// mergeFilteredHints (policy.go:127-185) over the permutations of ≤ 2 lists (the last varies fastest)
+// positions of a list's preferred hints: generateResourceHints marks a mask preferred iff its size is the
+// list's minimum; mask_at enumerates by size, so a size class is a contiguous run of positions
+__device__ __forceinline__ uint32_t preferred_positions(const HintList& L) {
+  if (L.nil) return L.nil_pref ? 1u : 0u;
+  const uint32_t cls = L.min_size == 1 ? 0x000Fu : L.min_size == 2 ? 0x03F0u : L.min_size == 3 ? 0x3C00u : 0x4000u;
+  return L.set & cls;
+}
+
+// mergeFilteredHints (policy.go:127-185) over the permutations of ≤ 2 lists (the last varies fastest).
+// Exact pruning: the first preferred permutation with a non-empty merge always replaces a non-preferred best,
+// and after it no non-preferred one can; so when any preferred permutation merges non-empty the result is the
+// same fold restricted to the preferred permutations (≤ 6 × 6 of them instead of ≤ 15 × 15), in the same order.
+// Only when none does (every merge among them empty, so none changed the best) are all permutations folded.
 __device__ __forceinline__ NumaHint merge_hints(uint32_t def, const HintList L0, const HintList L1, int nl,
                                                 uint64_t sc_lo, uint64_t sc_hi) {
   NumaHint best{def, 0, 0, 0};
@@ -625,37 +637,43 @@ __device__ __forceinline__ NumaHint merge_hints(uint32_t def, const HintList L0,
   const uint32_t s0 = L0.nil ? 1u : L0.set;
   const uint32_t s1 = nl > 1 ? (L1.nil ? 1u : L1.set) : 1u;
   const bool nilb = nl > 1 ? L1.nil != 0 : true;
-  for (uint32_t a = s0; a; a &= a - 1) {
-    const int ka = __builtin_ctz(a);
-    const uint32_t ma = L0.nil ? def : mask_at(ka);
-    const bool pa = L0.nil ? L0.nil_pref != 0 : __popc(ma) == L0.min_size;
-    const int sa = L0.nil ? 0 : sc_at(sc_lo, sc_hi, ka);
-    for (uint32_t b = s1; b; b &= b - 1) {
-      const int kb = __builtin_ctz(b);
-      const uint32_t mb = nilb ? def : mask_at(kb);
-      const bool pb = nl > 1 ? (nilb ? L1.nil_pref != 0 : __popc(mb) == L1.min_size) : true;
-      const uint32_t merged = def & ma & mb;
-      if (merged == 0) continue;
-      const int preferred = pa && pb;
-      int score = 0;
-      if (!L0.nil && ma == merged) score = sa;
-      if (!nilb && mb == merged) {
-        const int sb = sc_at(sc_lo, sc_hi, kb);
-        if (sb > score) score = sb;
-      }
-      const int pm = __popc(merged), pbst = __popc(best.mask);
-      if (preferred && !best.preferred) {
-        best = NumaHint{merged, 0, 1, score};
-      } else if (!preferred && best.preferred) {
-      } else {
-        const bool narrower = pm == pbst ? merged < best.mask : pm < pbst;
-        if (!narrower) {
-          if (pm == pbst && score > best.score) best = NumaHint{merged, 0, preferred, score};
+  const uint32_t q0 = preferred_positions(L0), q1 = nl > 1 ? preferred_positions(L1) : 1u;
+#pragma unroll 1
+  for (int pass = 0; pass < 2; ++pass) {
+    const uint32_t t0 = pass == 0 ? q0 : s0, t1 = pass == 0 ? q1 : s1;
+    for (uint32_t a = t0; a; a &= a - 1) {
+      const int ka = __builtin_ctz(a);
+      const uint32_t ma = L0.nil ? def : mask_at(ka);
+      const bool pa = L0.nil ? L0.nil_pref != 0 : __popc(ma) == L0.min_size;
+      const int sa = L0.nil ? 0 : sc_at(sc_lo, sc_hi, ka);
+      for (uint32_t b = t1; b; b &= b - 1) {
+        const int kb = __builtin_ctz(b);
+        const uint32_t mb = nilb ? def : mask_at(kb);
+        const bool pb = nl > 1 ? (nilb ? L1.nil_pref != 0 : __popc(mb) == L1.min_size) : true;
+        const uint32_t merged = def & ma & mb;
+        if (merged == 0) continue;
+        const int preferred = pa && pb;
+        int score = 0;
+        if (!L0.nil && ma == merged) score = sa;
+        if (!nilb && mb == merged) {
+          const int sb = sc_at(sc_lo, sc_hi, kb);
+          if (sb > score) score = sb;
+        }
+        const int pm = __popc(merged), pbst = __popc(best.mask);
+        if (preferred && !best.preferred) {
+          best = NumaHint{merged, 0, 1, score};
+        } else if (!preferred && best.preferred) {
         } else {
-          best = NumaHint{merged, 0, preferred, score};
+          const bool narrower = pm == pbst ? merged < best.mask : pm < pbst;
+          if (!narrower) {
+            if (pm == pbst && score > best.score) best = NumaHint{merged, 0, preferred, score};
+          } else {
+            best = NumaHint{merged, 0, preferred, score};
+          }
         }
       }
     }
+    if (best.preferred) break;
   }
   return best;
 }

@@ -38,6 +38,6 @@ for j in range(64):
     if not c:
         break
     if prev is not None:
-        sub = " ".join(f"{int(diag[j - 1, 2 + k]) - prev if diag[j - 1, 2 + k] else -1:7d}" for k in range(3))
-        print(f"  pod {j - 1:2d}: {c - prev:7d} cyc nM={int(diag[j - 1, 1]):2d}  sub {sub}")
+        sub = " ".join(f"{int(diag[j - 1, 2 + k]) - prev if diag[j - 1, 2 + k] else -1:7d}" for k in range(3))  # rescored / winner ready / reserved
+        print(f"  pod {j - 1:2d}: {c - prev:7d} cyc nM={int(diag[j - 1, 1]):2d}  sub {sub}  filt {int(diag[j - 1, 5]) - prev if diag[j - 1, 5] else -1:7d}")
     prev = c
