@@ -613,10 +613,6 @@ struct HintList {
   int nil, nil_pref, empty, min_size;
 };
 
-__device__ __forceinline__ int sc_at(uint64_t lo, uint64_t hi, int k) {
-  return k < 9 ? (int)((lo >> (7 * k)) & 127u) : (int)((hi >> (7 * (k - 9))) & 127u);
-}
-
 // positions of a list's preferred hints: generateResourceHints marks a mask preferred iff its size is the
 // list's minimum; mask_at enumerates by size, so a size class is a contiguous run of positions
 __device__ __forceinline__ uint32_t preferred_positions(const HintList& L) {
@@ -630,8 +626,9 @@ __device__ __forceinline__ uint32_t preferred_positions(const HintList& L) {
 // and after it no non-preferred one can; so when any preferred permutation merges non-empty the result is the
 // same fold restricted to the preferred permutations (≤ 6 × 6 of them instead of ≤ 15 × 15), in the same order.
 // Only when none does (every merge among them empty, so none changed the best) are all permutations folded.
+template <typename ScoreOf>
 __device__ __forceinline__ NumaHint merge_hints(uint32_t def, const HintList L0, const HintList L1, int nl,
-                                                uint64_t sc_lo, uint64_t sc_hi) {
+                                                const ScoreOf& score_of) {
   NumaHint best{def, 0, 0, 0};
   if (L0.empty || (nl > 1 && L1.empty)) return best;
   const uint32_t s0 = L0.nil ? 1u : L0.set;
@@ -645,7 +642,6 @@ __device__ __forceinline__ NumaHint merge_hints(uint32_t def, const HintList L0,
       const int ka = __builtin_ctz(a);
       const uint32_t ma = L0.nil ? def : mask_at(ka);
       const bool pa = L0.nil ? L0.nil_pref != 0 : __popc(ma) == L0.min_size;
-      const int sa = L0.nil ? 0 : sc_at(sc_lo, sc_hi, ka);
       for (uint32_t b = t1; b; b &= b - 1) {
         const int kb = __builtin_ctz(b);
         const uint32_t mb = nilb ? def : mask_at(kb);
@@ -653,12 +649,9 @@ __device__ __forceinline__ NumaHint merge_hints(uint32_t def, const HintList L0,
         const uint32_t merged = def & ma & mb;
         if (merged == 0) continue;
         const int preferred = pa && pb;
-        int score = 0;
-        if (!L0.nil && ma == merged) score = sa;
-        if (!nilb && mb == merged) {
-          const int sb = sc_at(sc_lo, sc_hi, kb);
-          if (sb > score) score = sb;
-        }
+        // a hint's score is its mask's (generateResourceHints), so the permutation's is that of the merged mask
+        // when some hint equals it — computed only then
+        const int score = ((!L0.nil && ma == merged) || (!nilb && mb == merged)) ? score_of(merged) : 0;
         const int pm = __popc(merged), pbst = __popc(best.mask);
         if (preferred && !best.preferred) {
           best = NumaHint{merged, 0, 1, score};
@@ -703,11 +696,27 @@ __device__ __forceinline__ bool numa_admit(const NumaView& v, const NumaPod& p, 
   const int bind = numa_pref_bind(v, p.preferred);
   HintList L0{0, 1, 1, 0, 0}, L1{0, 1, 1, 0, 0};
   int nl = 1;
-  uint64_t sc_lo = 0, sc_hi = 0;
   const bool req_c = p.req_cpu > 0, req_m = p.req_mem > 0;
   const int64_t rqc = opt_cpu(v, p);
+  int64_t av_cpu[kNumaMax], av_mem[kNumaMax];
+#pragma unroll
+  for (int i = 0; i < kNumaMax; ++i) av_cpu[i] = av_mem[i] = 0;
+  // the score of a hint mask (resource_manager.go:479-500: scorer over the mask's NUMA nodes), computed lazily
+  // by the merge for the masks it actually compares
+  const auto score_of = [&](uint32_t mk) -> int {
+    int64_t a_c = 0, a_m = 0, tot_c = 0, tot_m = 0;
+#pragma unroll
+    for (int i = 0; i < kNumaMax; ++i)
+      if ((mk >> i) & 1u) {
+        a_c += av_cpu[i];
+        a_m += av_mem[i];
+        tot_c += v.numa_cpu[i];
+        tot_m += v.numa_mem[i];
+      }
+    const int64_t rq_c = tot_c - a_c > 0 ? tot_c - a_c : 0, rq_m = tot_m - a_m > 0 ? tot_m - a_m : 0;
+    return (int)numa_scorer(NP.numa_strategy, NP.nw_cpu, NP.nw_mem, rq_c, rq_m, tot_c, tot_m, rqc, p.req_mem);
+  };
   if (bind >= 0 && (req_c || req_m)) {
-    int64_t av_cpu[kNumaMax], av_mem[kNumaMax];
     const bool trim = p.cpu_bind && p.required != 0;
     const int kind = kind_of(bind);
 #pragma unroll
@@ -736,10 +745,6 @@ __device__ __forceinline__ bool numa_admit(const NumaView& v, const NumaPod& p, 
           tot_c += v.numa_cpu[i];
           tot_m += v.numa_mem[i];
         }
-      const int64_t rq_c = tot_c - a_c > 0 ? tot_c - a_c : 0, rq_m = tot_m - a_m > 0 ? tot_m - a_m : 0;
-      const int64_t sc = numa_scorer(NP.numa_strategy, NP.nw_cpu, NP.nw_mem, rq_c, rq_m, tot_c, tot_m, rqc, p.req_mem);
-      if (k < 9) sc_lo |= (uint64_t)sc << (7 * k);
-      else sc_hi |= (uint64_t)sc << (7 * (k - 9));
       const int cnt = __popc(mk);
       if (req_m && tot_m >= p.req_mem) {
         if (cnt < min_m) min_m = cnt;
@@ -764,12 +769,14 @@ __device__ __forceinline__ bool numa_admit(const NumaView& v, const NumaPod& p, 
       L0 = lm;
     }
   }
-  if (v.policy == 3 /*SingleNUMANode*/) {
-    best = merge_hints(def, single_numa_only(L0), single_numa_only(L1), nl, sc_lo, sc_hi);
+  // one merge for every policy (lanes of one wave hold nodes of different policies: a single inlined merge
+  // keeps the divergent path to one copy)
+  const bool single = v.policy == 3 /*SingleNUMANode*/;
+  best = merge_hints(def, single ? single_numa_only(L0) : L0, single ? single_numa_only(L1) : L1, nl, score_of);
+  if (single) {
     if (!best.nil && best.mask == def) best = NumaHint{0, 1, best.preferred, 0};
     return best.preferred != 0;
   }
-  best = merge_hints(def, L0, L1, nl, sc_lo, sc_hi);
   if (v.policy == 2 /*Restricted*/) return best.preferred != 0;
   return true;  // BestEffort
 }
@@ -848,8 +855,12 @@ __device__ __forceinline__ bool skip_the_node(const NumaPod& p, int policy) {
 }
 
 // NodeNUMAResource.Filter (plugin.go:276-334); writes the affinity the topology manager stores
+// `fa` / `fa_ok`: when Filter passes and has run Allocate feasibility for the affinity it stores, that
+// allocation (Score runs the same check on the same state and reuses it)
 __device__ __forceinline__ bool numa_filter(const NumaView& v, const NumaPod& p, const NumaParams& NP, NumaHint& aff,
-                                            int64_t node_req_cpu, int64_t node_alloc_cpu) {
+                                            int64_t node_req_cpu, int64_t node_alloc_cpu, NumaAlloc& fa,
+                                            bool& fa_ok) {
+  fa_ok = false;
   aff = NumaHint{0, 1, 0, 0};
   if (p.prefilter_error) return false;
   if (p.req_cpu != 0 && v.amp > 1.0) {  // filterAmplifiedCPUs (plugin.go:336-373)
@@ -860,7 +871,6 @@ __device__ __forceinline__ bool numa_filter(const NumaView& v, const NumaPod& p,
     if (pod > node_alloc_cpu - req) return false;  // ErrInsufficientAmplifiedCPU
   }
   if (skip_the_node(p, v.policy)) return true;
-  NumaAlloc a;
   if (p.cpu_bind) {
     if (!v.valid) return false;
     const bool full_only = v.node_bind == 1;
@@ -868,51 +878,65 @@ __device__ __forceinline__ bool numa_filter(const NumaView& v, const NumaPod& p,
       if (p.needed % v.cpc != 0) return false;                                // SMT alignment
       if (full_only && (p.required != 2 || p.preferred != 2)) return false;  // required FullPCPUs policy
     }
-    if (p.required != 0 && v.policy == 0 && !numa_feasible(v, p, NumaHint{0, 1, 0, 0}, a)) return false;
   }
+  // Allocate feasibility runs once: on "don't care" for a required cpu-bind pod without a NUMA policy, on the
+  // admitted hint otherwise (the two cases exclude each other)
+  bool feas = p.cpu_bind && p.required != 0 && v.policy == 0;
   if (v.policy != 0) {
     if (v.nn == 0) return false;
     NumaHint best;
     if (!numa_admit(v, p, NP, best)) return false;
     aff = best;
-    if (!numa_feasible(v, p, best, a)) return false;
+    feas = true;
+  }
+  if (feas) {
+    if (!numa_feasible(v, p, aff, fa)) return false;
+    fa_ok = true;
   }
   return true;
+}
+__device__ __forceinline__ bool numa_filter(const NumaView& v, const NumaPod& p, const NumaParams& NP, NumaHint& aff,
+                                            int64_t node_req_cpu, int64_t node_alloc_cpu) {
+  NumaAlloc fa;
+  bool fa_ok;
+  return numa_filter(v, p, NP, aff, node_req_cpu, node_alloc_cpu, fa, fa_ok);
 }
 
 // NodeNUMAResource.Score (scoring.go:55-168) with the stored affinity; node_* = NodeInfo.Requested/Allocatable
 __device__ __forceinline__ int64_t numa_score(const NumaView& v, const NumaPod& p, const NumaParams& NP,
                                               const NumaHint& aff, int64_t node_req_cpu, int64_t node_req_mem,
-                                              int64_t node_alloc_cpu, int64_t node_alloc_mem) {
+                                              int64_t node_alloc_cpu, int64_t node_alloc_mem,
+                                              const NumaAlloc* known = nullptr) {
+  // both branches end in one scorer call (a single inlined copy on the divergent path)
+  int64_t ac = node_alloc_cpu, am = node_alloc_mem, rc = node_req_cpu, rm = node_req_mem, pc = p.req_cpu;
   if (skip_the_node(p, v.policy)) {
     if (p.skip) return 0;
     if (numa_pref_bind(v, p.preferred) < 0) return 0;  // scoreWithAmplifiedCPUs: getResourceOptions
-    int64_t rc = node_req_cpu;
     if (p.req_cpu != 0 && v.amp > 1.0) {  // the cpuset part of Requested counts amplified (scoring.go:95-120)
-      const int64_t am = (int64_t)v.n_alloc * 1000;
-      rc = rc - am + amplify(am, v.amp);
+      const int64_t an = (int64_t)v.n_alloc * 1000;
+      rc = rc - an + amplify(an, v.amp);
     }
-    return numa_scorer(NP.node_strategy, NP.w_cpu, NP.w_mem, rc, node_req_mem, node_alloc_cpu,
-                       node_alloc_mem, p.req_cpu, p.req_mem);
-  }
-  if (p.cpu_bind && !v.valid) return 0;
-  NumaAlloc a;
-  if (!numa_feasible(v, p, aff, a)) return 0;
-  int64_t ac = node_alloc_cpu, am = node_alloc_mem, rc = node_req_cpu, rm = node_req_mem;
-  if (a.res) {  // calculateAllocatableAndRequested (:122-168): the hint's NUMA nodes
-    ac = am = rc = rm = 0;
+  } else {
+    if (p.cpu_bind && !v.valid) return 0;
+    NumaAlloc a;
+    if (known) a = *known;
+    else if (!numa_feasible(v, p, aff, a)) return 0;
+    if (a.res) {  // calculateAllocatableAndRequested (:122-168): the hint's NUMA nodes
+      ac = am = rc = rm = 0;
 #pragma unroll
-    for (int i = 0; i < kNumaMax; ++i)
-      if ((a.res >> i) & 1u) {
-        rc += v.alloc_cpu[i];
-        rm += v.alloc_mem[i];
-        ac += v.numa_cpu[i];
-        am += v.numa_mem[i];
-      }
+      for (int i = 0; i < kNumaMax; ++i)
+        if ((a.res >> i) & 1u) {
+          rc += v.alloc_cpu[i];
+          rm += v.alloc_mem[i];
+          ac += v.numa_cpu[i];
+          am += v.numa_mem[i];
+        }
+    }
+    // a cpuset pod: requested cpu = Amplify(|allocated cpus| · 1000) (needed ≥ 1 whenever cpu_bind)
+    if (p.cpu_bind) rc = amplify((int64_t)v.n_alloc * 1000, v.amp);
+    pc = opt_cpu(v, p);
   }
-  // a cpuset pod: requested cpu = Amplify(|allocated cpus| · 1000) (needed ≥ 1 whenever cpu_bind)
-  if (p.cpu_bind) rc = amplify((int64_t)v.n_alloc * 1000, v.amp);
-  return numa_scorer(NP.node_strategy, NP.w_cpu, NP.w_mem, rc, rm, ac, am, opt_cpu(v, p), p.req_mem);
+  return numa_scorer(NP.node_strategy, NP.w_cpu, NP.w_mem, rc, rm, ac, am, pc, p.req_mem);
 }
 
 // Filter (when the profile has it) + Score of one node: feasibility and the unweighted plugin score
@@ -921,8 +945,11 @@ __device__ __forceinline__ bool numa_eval(const NumaView& v, const NumaPod& p, c
                                           int64_t node_alloc_mem, int64_t& score, NumaHint& aff) {
   aff = NumaHint{0, 1, 0, 0};
   score = 0;
-  if (NP.filter && !numa_filter(v, p, NP, aff, node_req_cpu, node_alloc_cpu)) return false;
-  if (NP.score) score = numa_score(v, p, NP, aff, node_req_cpu, node_req_mem, node_alloc_cpu, node_alloc_mem);
+  NumaAlloc fa;
+  bool fa_ok = false;
+  if (NP.filter && !numa_filter(v, p, NP, aff, node_req_cpu, node_alloc_cpu, fa, fa_ok)) return false;
+  if (NP.score)
+    score = numa_score(v, p, NP, aff, node_req_cpu, node_req_mem, node_alloc_cpu, node_alloc_mem, fa_ok ? &fa : nullptr);
   return true;
 }
 
