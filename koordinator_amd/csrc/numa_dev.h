@@ -9,7 +9,7 @@
 //   frameworkext/topologymanager/policy*.go   mergeFilteredHints + best-effort / restricted / single-numa-node
 // CPU sets are 256-bit masks in buildCPUTopology numbering (cpu = ((socket·nps + node)·cpn + core)·cpc + t), so a
 // NUMA node, a socket and a core are contiguous cpu ranges.  Scope: ≤ 4 NUMA nodes, cpus per core 1 or 2,
-// maxRefCount 1, no amplification, no reservations, exclusive policy None (validated at ingest).
+// maxRefCount 1, no reservations, exclusive policy None (validated at ingest); cpu amplification included.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -200,40 +200,55 @@ struct Acc {
   }
 };
 
-// groups (NUMA nodes or sockets) of a cpu mask, ordered as freeCoresInNode/Socket(full=true) order them:
-// (group free count, [socket free for nodes], id).  Returns the group count; ids in order.
-__device__ __forceinline__ int order_groups(const Acc& a, bool by_node, const CpuSet& sel, int* ids, int* cnt) {
+// Group orders as sorted packed keys (ascending key = the reference's order; ids make every key unique, so the
+// order is total): ≤ 8 groups sorted by a fixed network on compile-time indices, so the lists live in registers.
+constexpr uint64_t kNoGroup = ~0ull;
+__device__ __forceinline__ void cswap(uint64_t& a, uint64_t& b) {
+  const uint64_t lo = a < b ? a : b, hi = a < b ? b : a;
+  a = lo;
+  b = hi;
+}
+// Batcher odd-even merge sort of 8 keys (19 comparators)
+__device__ __forceinline__ void sort8(uint64_t* k) {
+  cswap(k[0], k[1]); cswap(k[2], k[3]); cswap(k[4], k[5]); cswap(k[6], k[7]);
+  cswap(k[0], k[2]); cswap(k[1], k[3]); cswap(k[4], k[6]); cswap(k[5], k[7]);
+  cswap(k[1], k[2]); cswap(k[5], k[6]);
+  cswap(k[0], k[4]); cswap(k[1], k[5]); cswap(k[2], k[6]); cswap(k[3], k[7]);
+  cswap(k[2], k[4]); cswap(k[3], k[5]);
+  cswap(k[1], k[2]); cswap(k[3], k[4]); cswap(k[5], k[6]);
+}
+// a free count as a key field: better_free first (MostAllocated: fewer free first, else more free first)
+__device__ __forceinline__ uint64_t free_field(int strategy, int c) {
+  return strategy == 1 ? (uint64_t)c : (uint64_t)(0xFFFF - c);
+}
+// k[g] for a run-time g without a dynamically indexed (scratch) array: a select chain over the 8 registers
+__device__ __forceinline__ uint64_t kat(const uint64_t* k, int g) {
+  uint64_t v = kNoGroup;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v = g == i ? k[i] : v;
+  return v;
+}
+__device__ __forceinline__ int key_id(uint64_t k) { return (int)(k & 0xFFu); }
+__device__ __forceinline__ int key_free(int strategy, uint64_t k) {
+  const int f = (int)((k >> 32) & 0xFFFFu);
+  return strategy == 1 ? f : 0xFFFF - f;
+}
+
+// groups (NUMA nodes or sockets) with cpus in `sel`, ordered as freeCoresInNode/Socket(full=true) order them:
+// (group free count, [socket free count for nodes], id)
+__device__ __forceinline__ void order_groups(const Acc& a, bool by_node, const CpuSet& sel, uint64_t* k) {
   const int ng = by_node ? a.t.nodes : a.t.sockets;
-  int n = 0;
-  for (int g = 0; g < ng && g < 8; ++g) {
-    const CpuSet in = cs_and(sel, by_node ? a.t.node_cpus(g) : a.t.socket_cpus(g));
-    const int c = cs_count(in);
+#pragma unroll
+  for (int g = 0; g < 8; ++g) {
+    k[g] = kNoGroup;
+    if (g >= ng) continue;
+    const int c = cs_count(cs_and(sel, by_node ? a.t.node_cpus(g) : a.t.socket_cpus(g)));
     if (c == 0) continue;
-    ids[n] = g;
-    cnt[n] = c;
-    ++n;
+    uint64_t key = free_field(a.strategy, c) << 32 | (uint64_t)g;
+    if (by_node) key |= free_field(a.strategy, cs_count(cs_and(a.avail, a.t.socket_cpus(g / a.t.nps)))) << 16;
+    k[g] = key;
   }
-  for (int i = 0; i < n; ++i) {  // selection sort on a total order
-    int best = i;
-    for (int j = i + 1; j < n; ++j) {
-      bool before;
-      if (cnt[j] != cnt[best]) before = better_free(a.strategy, cnt[j], cnt[best]);
-      else if (by_node) {
-        const int sj = cs_count(cs_and(a.avail, a.t.socket_cpus(ids[j] / a.t.nps)));
-        const int sb = cs_count(cs_and(a.avail, a.t.socket_cpus(ids[best] / a.t.nps)));
-        before = sj != sb ? better_free(a.strategy, sj, sb) : ids[j] < ids[best];
-      } else {
-        before = ids[j] < ids[best];
-      }
-      if (before) best = j;
-    }
-    const int ti = ids[i], tc = cnt[i];
-    ids[i] = ids[best];
-    cnt[i] = cnt[best];
-    ids[best] = ti;
-    cnt[best] = tc;
-  }
-  return n;
+  sort8(k);
 }
 
 // first k cpus of a group list where cores are ordered (free count desc, id) and cpus ascending (cpc ≤ 2:
@@ -266,47 +281,52 @@ __device__ __noinline__ bool take_cpus(const Topo& t, const CpuSet& available, i
   if (a.needed < 1) return true;
   if (a.needed > cs_count(a.avail)) return false;
   const bool full = bind == 2;
-  int ids[8], cnt[8];
+  uint64_t k[8];
   if (full || t.cpc == 1) {
     if (a.needed <= t.per_node()) {
       const CpuSet fc = full_core_cpus(t, a.avail);
-      const int ng = order_groups(a, true, fc, ids, cnt);
-      for (int g = 0; g < ng; ++g)
-        if (cnt[g] >= a.needed) {
-          a.take(lowest_k(cs_and(fc, t.node_cpus(ids[g])), a.needed));
+      order_groups(a, true, fc, k);
+      for (int g = 0; g < 8; ++g) {
+        const uint64_t kg = kat(k, g);
+        if (kg != kNoGroup && key_free(a.strategy, kg) >= a.needed) {
+          a.take(lowest_k(cs_and(fc, t.node_cpus(key_id(kg))), a.needed));
           out = a.result;
           return true;
         }
+      }
     }
     if (a.needed <= t.per_socket()) {
       const CpuSet fc = full_core_cpus(t, a.avail);
-      const int ng = order_groups(a, false, fc, ids, cnt);
-      for (int g = 0; g < ng; ++g)
-        if (cnt[g] >= a.needed) {
-          a.take(lowest_k(cs_and(fc, t.socket_cpus(ids[g])), a.needed));
+      order_groups(a, false, fc, k);
+      for (int g = 0; g < 8; ++g) {
+        const uint64_t kg = kat(k, g);
+        if (kg != kNoGroup && key_free(a.strategy, kg) >= a.needed) {
+          a.take(lowest_k(cs_and(fc, t.socket_cpus(key_id(kg))), a.needed));
           out = a.result;
           return true;
         }
+      }
     }
     {
+      // sockets by (full-core cpu count desc, id): order_groups re-sorted stably by count, most first
       const CpuSet fc = full_core_cpus(t, a.avail);
-      int ng = order_groups(a, false, fc, ids, cnt);
-      // stable sort by full-core cpu count, most first
-      for (int i = 1; i < ng; ++i)
-        for (int j = i; j > 0 && cnt[j - 1] < cnt[j]; --j) {
-          const int ti = ids[j], tc = cnt[j];
-          ids[j] = ids[j - 1];
-          cnt[j] = cnt[j - 1];
-          ids[j - 1] = ti;
-          cnt[j - 1] = tc;
-        }
-      int uid[8], ucnt[8], nu = 0;
-      for (int g = 0; g < ng; ++g) {
-        if (a.needed < cnt[g]) {
-          uid[nu] = ids[g];
-          ucnt[nu++] = cnt[g];
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        k[s] = kNoGroup;
+        if (s >= t.sockets) continue;
+        const int c = cs_count(cs_and(fc, t.socket_cpus(s)));
+        if (c > 0) k[s] = (uint64_t)(0xFFFF - c) << 32 | (uint64_t)s;
+      }
+      sort8(k);
+      uint32_t um = 0;  // sockets the request does not fill, kept for the core-by-core pass
+      for (int g = 0; g < 8; ++g) {
+        const uint64_t kg = kat(k, g);
+        if (kg == kNoGroup) continue;
+        const int id = key_id(kg), c = 0xFFFF - (int)((kg >> 32) & 0xFFFFu);
+        if (a.needed < c) {
+          um |= 1u << id;
         } else {
-          a.take(cs_and(fc, t.socket_cpus(ids[g])));
+          a.take(cs_and(fc, t.socket_cpus(id)));
           if (a.needed < 1) {
             out = a.result;
             return true;
@@ -314,16 +334,15 @@ __device__ __noinline__ bool take_cpus(const Topo& t, const CpuSet& available, i
         }
       }
       if (a.needed >= t.cpc) {
-        for (int i = 1; i < nu; ++i)  // stable, fewest first
-          for (int j = i; j > 0 && ucnt[j - 1] > ucnt[j]; --j) {
-            const int ti = uid[j], tc = ucnt[j];
-            uid[j] = uid[j - 1];
-            ucnt[j] = ucnt[j - 1];
-            uid[j - 1] = ti;
-            ucnt[j - 1] = tc;
-          }
-        for (int g = 0; g < nu; ++g) {
-          CpuSet list = cs_and(fc, t.socket_cpus(uid[g]));  // the group's full-core cpus, ascending
+        // those sockets by (count, id) ascending: the list above re-sorted stably, fewest first
+#pragma unroll
+        for (int s = 0; s < 8; ++s)
+          k[s] = ((um >> s) & 1u) ? (uint64_t)cs_count(cs_and(fc, t.socket_cpus(s))) << 32 | (uint64_t)s : kNoGroup;
+        sort8(k);
+        for (int g = 0; g < 8; ++g) {
+          const uint64_t kg = kat(k, g);
+          if (kg == kNoGroup) continue;
+          CpuSet list = cs_and(fc, t.socket_cpus(key_id(kg)));  // the group's full-core cpus, ascending
           while (cs_count(list) > 0) {
             const CpuSet chunk = lowest_k(list, t.cpc);
             list = cs_andnot(list, chunk);
@@ -343,9 +362,11 @@ __device__ __noinline__ bool take_cpus(const Topo& t, const CpuSet& available, i
       for (int fe = 0; fe < 2; ++fe) {
         // freeCPUsInNode: nodes by (node free, socket free, id) on the unreduced counts; with
         // filterExclusive each list keeps one cpu per core
-        const int ng = order_groups(a, true, a.avail, ids, cnt);
-        for (int g = 0; g < ng; ++g) {
-          const CpuSet in = cs_and(a.avail, t.node_cpus(ids[g]));
+        order_groups(a, true, a.avail, k);
+        for (int g = 0; g < 8; ++g) {
+          const uint64_t kg = kat(k, g);
+          if (kg == kNoGroup) continue;
+          const CpuSet in = cs_and(a.avail, t.node_cpus(key_id(kg)));
           const CpuSet lst = fe == 0 ? first_cpu_per_core(t, in) : in;
           if (cs_count(lst) >= a.needed) {
             a.take(fe == 0 ? lowest_k(lst, a.needed) : spread_first_k(t, lst, a.needed));
@@ -358,29 +379,22 @@ __device__ __noinline__ bool take_cpus(const Topo& t, const CpuSet& available, i
     if (a.needed <= t.per_socket()) {
       for (int fe = 0; fe < 2; ++fe) {
         // freeCPUsInSocket: sockets by (length of the (reduced) list, id)
-        int sid[8], scnt[8], ns = 0;
-        for (int s = 0; s < t.sockets && s < 8; ++s) {
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+          k[s] = kNoGroup;
+          if (s >= t.sockets) continue;
           const CpuSet in = cs_and(a.avail, t.socket_cpus(s));
-          const CpuSet lst = fe == 0 ? first_cpu_per_core(t, in) : in;
-          const int c = cs_count(lst);
           if (cs_count(in) == 0) continue;
-          sid[ns] = s;
-          scnt[ns++] = c;
-        }
-        for (int i = 0; i < ns; ++i) {
-          int best = i;
-          for (int j = i + 1; j < ns; ++j)
-            if (scnt[j] != scnt[best] ? better_free(a.strategy, scnt[j], scnt[best]) : sid[j] < sid[best]) best = j;
-          const int ti = sid[i], tc = scnt[i];
-          sid[i] = sid[best];
-          scnt[i] = scnt[best];
-          sid[best] = ti;
-          scnt[best] = tc;
-        }
-        for (int g = 0; g < ns; ++g) {
-          const CpuSet in = cs_and(a.avail, t.socket_cpus(sid[g]));
           const CpuSet lst = fe == 0 ? first_cpu_per_core(t, in) : in;
-          if (scnt[g] >= a.needed) {
+          k[s] = free_field(a.strategy, cs_count(lst)) << 32 | (uint64_t)s;
+        }
+        sort8(k);
+        for (int g = 0; g < 8; ++g) {
+          const uint64_t kg = kat(k, g);
+          if (kg == kNoGroup) continue;
+          if (key_free(a.strategy, kg) >= a.needed) {
+            const CpuSet in = cs_and(a.avail, t.socket_cpus(key_id(kg)));
+            const CpuSet lst = fe == 0 ? first_cpu_per_core(t, in) : in;
             a.take(fe == 0 ? lowest_k(lst, a.needed) : spread_first_k(t, lst, a.needed));
             out = a.result;
             return true;
@@ -393,60 +407,48 @@ __device__ __noinline__ bool take_cpus(const Topo& t, const CpuSet& available, i
   // take one by one.  Classes of (socket, node) share the first three keys; inside a run of equal classes
   // single-free cores come before full ones, each by core id (= (socket, core) order in this numbering).
   {
-    int nid[8], nn = 0;
-    for (int n = 0; n < t.nodes && n < 8; ++n)
-      if (cs_count(cs_and(a.avail, t.node_cpus(n))) > 0) nid[nn++] = n;
-    int colo[8], sfree[8], nfree[8];
-    for (int i = 0; i < nn; ++i) {
-      const int s = nid[i] / t.nps;
-      colo[i] = cs_count(cs_and(a.result, t.socket_cpus(s)));
-      sfree[i] = cs_count(cs_and(a.avail, t.socket_cpus(s)));
-      nfree[i] = cs_count(cs_and(a.avail, t.node_cpus(nid[i])));
+#pragma unroll
+    for (int n = 0; n < 8; ++n) {
+      k[n] = kNoGroup;
+      if (n >= t.nodes) continue;
+      const int nf = cs_count(cs_and(a.avail, t.node_cpus(n)));
+      if (nf == 0) continue;
+      const int s = n / t.nps;
+      const int colo = cs_count(cs_and(a.result, t.socket_cpus(s)));
+      const int sf = cs_count(cs_and(a.avail, t.socket_cpus(s)));
+      k[n] = (uint64_t)(0xFFFF - colo) << 48 | free_field(a.strategy, sf) << 32 | free_field(a.strategy, nf) << 16 |
+             (uint64_t)n;
     }
-    for (int i = 0; i < nn; ++i) {  // order the nodes by the class keys, then id
-      int best = i;
-      for (int j = i + 1; j < nn; ++j) {
-        bool before;
-        if (colo[j] != colo[best]) before = colo[j] > colo[best];
-        else if (sfree[j] != sfree[best]) before = better_free(a.strategy, sfree[j], sfree[best]);
-        else if (nfree[j] != nfree[best]) before = better_free(a.strategy, nfree[j], nfree[best]);
-        else before = nid[j] < nid[best];
-        if (before) best = j;
-      }
-      int tmp;
-      tmp = nid[i]; nid[i] = nid[best]; nid[best] = tmp;
-      tmp = colo[i]; colo[i] = colo[best]; colo[best] = tmp;
-      tmp = sfree[i]; sfree[i] = sfree[best]; sfree[best] = tmp;
-      tmp = nfree[i]; nfree[i] = nfree[best]; nfree[best] = tmp;
-    }
-    // the ordered cpu list, as a sequence of masks to read in ascending order
-    CpuSet seq[16];
-    int nseq = 0;
-    for (int i = 0; i < nn;) {
-      int j = i;
-      CpuSet run = cs_zero();
-      while (j < nn && colo[j] == colo[i] && sfree[j] == sfree[i] && nfree[j] == nfree[i]) {
-        run = cs_or(run, cs_and(a.avail, t.node_cpus(nid[j])));
-        ++j;
-      }
-      const CpuSet fc = full_core_cpus(t, run);
-      seq[nseq++] = cs_andnot(run, fc);  // single-free cores first
-      seq[nseq++] = fc;
-      i = j;
-    }
+    sort8(k);
+    // the ordered cpu list as runs of equal class (key >> 16), each read as [single-free cores, full cores] in
+    // ascending cpu order; the node masks are taken before any cpu is
+    const CpuSet avail0 = a.avail;
     // spreadCPUs over the concatenated list: first pass takes the first cpu of each core, second the rest
-    for (int pass = 0; pass < 2; ++pass)
-      for (int k = 0; k < nseq; ++k) {
-        const CpuSet part = pass == 0 ? first_cpu_per_core(t, seq[k]) : cs_andnot(seq[k], first_cpu_per_core(t, seq[k]));
-        const int c = cs_count(part);
-        if (c == 0) continue;
-        const int take = c < a.needed ? c : a.needed;
-        a.take(lowest_k(part, take));
-        if (a.needed < 1) {
-          out = a.result;
-          return true;
+    for (int pass = 0; pass < 2; ++pass) {
+      CpuSet run = cs_zero();
+      for (int r = 0; r < 8; ++r) {
+        const uint64_t kr = kat(k, r);
+        if (kr == kNoGroup) continue;
+        run = cs_or(run, cs_and(avail0, t.node_cpus(key_id(kr))));
+        const uint64_t nxt = kat(k, r + 1);  // kNoGroup past the end
+        if (nxt != kNoGroup && (nxt >> 16) == (kr >> 16)) continue;
+        const CpuSet fc = full_core_cpus(t, run);
+        const CpuSet parts[2] = {cs_andnot(run, fc), fc};
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const CpuSet first = first_cpu_per_core(t, parts[q]);
+          const CpuSet part = pass == 0 ? first : cs_andnot(parts[q], first);
+          const int c = cs_count(part);
+          if (c == 0) continue;
+          a.take(lowest_k(part, c < a.needed ? c : a.needed));
+          if (a.needed < 1) {
+            out = a.result;
+            return true;
+          }
         }
+        run = cs_zero();
       }
+    }
   }
   out = cs_zero();
   return false;
