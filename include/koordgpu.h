@@ -511,7 +511,8 @@ int kg_debug_fast_lrs(kg_engine* e, const int64_t* requested, const int64_t* cap
 int kg_debug_eval_paths(kg_engine* e, int64_t* mismatches);
 
 /* Diagnostic builds (-DKG_STAMPS) only: copies the in-kernel (s_memtime, s_memrealtime) stamps, uint64[4][32][2],
- * then the last resolver launch's per-pod (s_memtime, path bits), uint64[64][2]. */
+ * then the last resolver launch's per-pod (s_memtime, path bits, sub-phase stamps), uint64[64][6], then the NUMA
+ * hint-merge counters (merges, all-permutation fallback passes), uint64[2]: 258 + 384 words in all. */
 int kg_debug_stamps(kg_engine* e, uint64_t* out);
 
 const char* kg_last_error(void);

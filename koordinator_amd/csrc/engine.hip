@@ -4261,6 +4261,8 @@ int kg_debug_stamps(kg_engine* e, uint64_t* out) {
   HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(kg::g_stamps), sizeof(kg::g_stamps), 0, hipMemcpyDeviceToHost));
   HIP_TRY(hipMemcpyFromSymbol(out + 4 * 32 * 2, HIP_SYMBOL(kg::g_pod_diag), sizeof(kg::g_pod_diag), 0,
                               hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpyFromSymbol(out + 4 * 32 * 2 + 64 * 6, HIP_SYMBOL(kg::g_merge_count), sizeof(kg::g_merge_count), 0,
+                              hipMemcpyDeviceToHost));
   return 0;
 #else
   (void)e;

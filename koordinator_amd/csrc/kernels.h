@@ -39,12 +39,21 @@ __device__ unsigned long long g_pod_diag[64][6];
       g_pod_diag[j][1] = (bits);                                                   \
     }                                                                              \
   } while (0)
+// NUMA hint merges and the ones that needed the all-permutation fallback pass (diagnostic counters)
+__device__ unsigned long long g_merge_count[2];
+#define KG_COUNT(i)                                                                \
+  do {                                                                             \
+    atomicAdd(&g_merge_count[i], 1ull);                                            \
+  } while (0)
 // sub-phase stamp k (0..3) of pod j
 #define KG_POD_SUB(j, k)                                                           \
   do {                                                                             \
     if (threadIdx.x == 0 && (j) < 64) g_pod_diag[j][2 + (k)] = __builtin_amdgcn_s_memtime(); \
   } while (0)
 #else
+#define KG_COUNT(i) \
+  do {              \
+  } while (0)
 #define KG_POD_DIAG(j, bits) \
   do {                       \
   } while (0)

@@ -637,8 +637,10 @@ __device__ __forceinline__ NumaHint merge_hints(uint32_t def, const HintList L0,
   const uint32_t s1 = nl > 1 ? (L1.nil ? 1u : L1.set) : 1u;
   const bool nilb = nl > 1 ? L1.nil != 0 : true;
   const uint32_t q0 = preferred_positions(L0), q1 = nl > 1 ? preferred_positions(L1) : 1u;
+  KG_COUNT(0);
 #pragma unroll 1
   for (int pass = 0; pass < 2; ++pass) {
+    if (pass == 1) KG_COUNT(1);
     const uint32_t t0 = pass == 0 ? q0 : s0, t1 = pass == 0 ? q1 : s1;
     for (uint32_t a = t0; a; a &= a - 1) {
       const int ka = __builtin_ctz(a);
@@ -734,7 +736,7 @@ __device__ __forceinline__ bool numa_admit(const NumaView& v, const NumaPod& p, 
     }
     uint32_t hc = 0, hm = 0;
     int min_c = nn, min_m = nn;
-#pragma unroll 1
+#pragma unroll  // constant masks: each subset sum is a fixed 0-3 adds
     for (int k = 0; k < 15; ++k) {
       const uint32_t mk = mask_at(k);
       if (mk & ~def) continue;

@@ -23,7 +23,7 @@ with Engine(cfg, n) as e:
     e.profile(True)
     st = e.schedule_staged(0, npods)
     prof = e.profile_read()
-    buf = np.zeros(4 * 32 * 2 + 64 * 6, dtype=np.uint64)
+    buf = np.zeros(4 * 32 * 2 + 64 * 6 + 2, dtype=np.uint64)
     abi.check(e.lib, e.lib.kg_debug_stamps(e.h, abi.ptr(buf)))
     stamps = buf[:256].reshape(4, 32, 2)
     diag = buf[256:256 + 384].reshape(64, 6)

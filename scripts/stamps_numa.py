@@ -25,12 +25,15 @@ with Engine(cfg, n) as e:
     e.profile(True)
     st = e.schedule_staged(0, npods)
     prof = e.profile_read()
-    buf = np.zeros(4 * 32 * 2 + 64 * 6, dtype=np.uint64)
+    buf = np.zeros(4 * 32 * 2 + 64 * 6 + 2, dtype=np.uint64)
     abi.check(e.lib, e.lib.kg_debug_stamps(e.h, abi.ptr(buf)))
     diag = buf[256:256 + 384].reshape(64, 6)
 print(f"nodes={n} pods={npods} batch={batch}: rounds={int(st['device_batches'])} seconds={st['seconds']:.4f} "
       f"pods/s={npods / st['seconds']:.0f}")
 print("live:", {k: (round(ms / c * 1e3, 2), c) for k, (ms, c) in prof.items()})
+merges, fallbacks = int(buf[-2]), int(buf[-1])
+print(f"NUMA hint merges: {merges}, all-permutation fallback passes: {fallbacks} "
+      f"({100.0 * fallbacks / max(merges, 1):.2f} %)")
 print("== resolver per pod (last launch): cycles; nM; sub: rescored / winner row ready / reserved")
 prev = None
 for j in range(64):
