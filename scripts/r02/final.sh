@@ -13,6 +13,7 @@ run() {  # name timeout cmd...
   echo "$name rc=$rc"; tail -n 2 "$OUT/$name.log" | cut -c1-300
   [ $rc -eq 0 ] || exit $rc
 }
+run smoke 300 python3 -u -c "import __graft_entry__ as g; g.smoke(); print(\"smoke ok\")"
 run tests 900 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread
 run bench_c4 600 python3 -u bench.py --workload c4
 run bench_c3 600 python3 -u bench.py
