@@ -1145,12 +1145,23 @@ __global__ __launch_bounds__(kWave) void resolve_round_numa(DevTable T, NumaTabl
     const uint64_t um = __ballot(unmod);
     const int pos = um ? (int)__builtin_ctzll(um) : kC;
     uint64_t best = um ? readlane_u64(key, pos) : 0;
-    NumaHint maff{0, 1, 0, 0};  // the affinity of this lane's modified row (Reserve reuses it when it wins)
-    if (nM > 0) {
+    // The best unmodified candidate e wins unless a modified row beats it: its row is brought into the spare slot
+    // nM before the re-score, so its Filter (the affinity Reserve needs) runs alongside the modified rows' instead
+    // of after the search on one lane.  Slot nM only becomes a modified row if e wins.
+    if (um && lane == nM) {
+      const uint32_t en = key_node(best);
+      midx = en;
+      mrow = load_row(T, en);
+      s_ns[nM] = NT.s[en];
+      s_nm[nM] = NT.m[en];
+      mv = make_view(&s_ns[nM], &s_nm[nM], NP);
+    }
+    NumaHint maff{0, 1, 0, 0};  // the affinity of this lane's row (Reserve reuses it when the row wins)
+    if (nM > 0 || um) {
       uint64_t mk = 0;
-      if (lane < nM) {
+      if (lane < nM || (um && lane == nM)) {
         int64_t t = 0;
-        if (eval_node_numa(mrow, mv, p, np, P, NP, t, maff)) mk = make_key(t, midx);
+        if (eval_node_numa(mrow, mv, p, np, P, NP, t, maff) && lane < nM) mk = make_key(t, midx);
       }
       const uint64_t mbest = wave_max_key(mk);
       best = mbest > best ? mbest : best;
@@ -1165,28 +1176,15 @@ __global__ __launch_bounds__(kWave) void resolve_round_numa(DevTable T, NumaTabl
     const uint32_t w = key_node(best);
     const uint64_t hit = __ballot((lane < nM) & (midx == w));
     const int owner = hit ? (int)__builtin_ctzll(hit) : nM;
-    if (!hit) {
-      if (lane == owner) {
-        midx = w;
-        mrow = load_row(T, w);
-        const NumaStatic ns = NT.s[w];
-        const NumaMut nm = NT.m[w];
-        s_ns[owner] = ns;
-        s_nm[owner] = nm;
-        mv = make_view(&s_ns[owner], &s_nm[owner], NP);
-      }
+    if (!hit) {  // w = e, already in slot nM = owner (with its affinity)
       if (lane == 0) bitmap[w >> 5] |= 1u << (w & 31);
       ++nM;
     }
     __syncthreads();
     KG_POD_SUB(j, 1);
     int placed = 0;
-    if (lane == owner) {  // Reserve with the affinity Filter stores (a fresh row's is computed on its state)
-      NumaHint aff = maff;
-      if (!hit) {
-        aff = NumaHint{0, 1, 0, 0};
-        if (NP.filter) (void)numa_filter(mv, np, NP, aff, mrow.req_cpu, mrow.alloc_cpu);
-      }
+    if (lane == owner) {  // Reserve with the affinity Filter stored on the winner's row this pod
+      const NumaHint aff = maff;
 #ifdef KG_STAMPS
       if (j < 64) g_pod_diag[j][5] = __builtin_amdgcn_s_memtime();
 #endif
