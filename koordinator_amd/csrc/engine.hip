@@ -1797,6 +1797,14 @@ __global__ void unreserve_pods(DevTable T, const DevPod* __restrict__ pods, cons
   }
 }
 
+// F_EPH_OVER of every node from its ephemeral-storage Allocatable / Requested columns (aux slot 0)
+__global__ void refresh_eph_flags(DevTable T, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const bool over = T.aux[(size_t)kAux * T.cap + i] > T.aux[i];
+  T.flags[i] = (T.flags[i] & ~F_EPH_OVER) | (over ? F_EPH_OVER : 0u);
+}
+
 __global__ void apply_deltas(DevTable T, const RowDelta* __restrict__ d, int64_t n) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -1972,6 +1980,9 @@ struct kg_engine {
   std::vector<PendingPlace> pending_place;  // scheduled staged ranges not yet in the mirror (flush_placements)
   std::vector<int64_t> now_of;        // metric ingest time per node
   bool static_dirty = true;
+  // F_EPH_OVER (ephemeral-storage Requested > Allocatable) must be recomputed on the device: eph_any once any
+  // ephemeral Requested delta was pushed, eph_dirty until the flags column has been refreshed since
+  bool eph_any = false, eph_dirty = false;
   // scheduler clock for isNodeMetricExpired (kg_engine_set_clock): 0 = the newest now given to
   // kg_node_metrics_update, 1 = fixed, 2 = the host's real-time clock at every call
   int clock_mode = 0;
@@ -2517,9 +2528,20 @@ void clock_refresh(kg_engine* e) {
   if (flip) e->static_dirty = true;
 }
 
+int refresh_eph(kg_engine* e) {
+  if (!e->eph_dirty) return 0;
+  e->eph_dirty = false;
+  if (e->n_nodes == 0) return 0;
+  refresh_eph_flags<<<(unsigned)((e->n_nodes + 255) / 256), 256, 0, e->stream>>>(e->T, e->n_nodes);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  return 0;
+}
+
 int sync_static(kg_engine* e) {
   clock_refresh(e);
-  if (!e->static_dirty) return 0;
+  if (!e->static_dirty) return refresh_eph(e);
+  e->eph_dirty |= e->eph_any;  // the flags column below is rewritten without F_EPH_OVER
   const int64_t cap = e->capacity;
   auto& h64 = e->h_static64;
   auto& h32 = e->h_static32;
@@ -2561,7 +2583,7 @@ int sync_static(kg_engine* e) {
   }
   HIP_TRY(hipStreamSynchronize(e->stream));
   e->static_dirty = false;
-  return 0;
+  return refresh_eph(e);
 }
 
 int push_deltas(kg_engine* e, const std::vector<RowDelta>& d) {
@@ -3573,6 +3595,7 @@ static int pods_delta(kg_engine* e, const kg_pod* pods, const int32_t* node_idx,
     x.d[7] = (p.flags & P_PROD) ? la * p.est_cpu : 0;
     x.d[8] = (p.flags & P_PROD) ? la * p.est_mem : 0;
     for (int r = 0; r < kAux; ++r) x.aux[r] = sign * pods[k].requests[kAuxFirst + r];
+    if (x.aux[0] != 0) e->eph_any = e->eph_dirty = true;
     if (la) {  // the podAssignCache mirror (reserve pods are not in the assign cache)
       const int64_t est[2] = {p.est_cpu, p.est_mem};
       if (sign > 0)
@@ -3630,6 +3653,7 @@ int kg_pods_unreserve(kg_engine* e, int64_t first, int64_t count, const uint8_t*
                                         (e->ds_on || e->rsv_on) ? e->qdev.p : nullptr, e->paux.p);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(e->stream));
+  e->eph_dirty |= e->eph_any;  // a release may end an ephemeral-storage overcommit
   return 0;
 }
 

@@ -75,6 +75,10 @@ constexpr uint32_t F_LA_SCORE = 1u << 1;      // NodeMetric present and not expi
 constexpr uint32_t F_LA_PASS = 1u << 2;       // LoadAware Filter verdict for a non-prod pod
 constexpr uint32_t F_LA_PASS_PROD = 1u << 3;  // LoadAware Filter verdict for a prod pod
 constexpr uint32_t F_RARE = 1u << 4;          // EvalRow only: a score input lies outside eval_fast's exact domain
+// ephemeral-storage Requested > Allocatable: fitsRequest compares EphemeralStorage for EVERY pod with a non-zero request
+// (reservation/plugin.go:469-471: 0 > Allocatable - Requested rejects).  Scheduling never sets it (a placed request fits
+// the free amount), so only host deltas (kg_pods_add / remove / unreserve, node upserts) move it: refresh_eph_flags.
+constexpr uint32_t F_EPH_OVER = 1u << 6;
 
 // pod flags (device)
 constexpr uint32_t P_ZERO_REQ = 1u << 0;      // every request zero → fitsRequest skips resource checks
@@ -217,6 +221,7 @@ __device__ __forceinline__ bool eval_node(const Row& n, const DevPod& p, const E
     if (!(p.flags & P_ZERO_REQ)) {
       if (p.req_cpu > n.alloc_cpu - n.req_cpu) rej |= 1u << 1;
       if (p.req_mem > n.alloc_mem - n.req_mem) rej |= 1u << 2;
+      if (n.flags & F_EPH_OVER) rej |= 1u << 7;
     }
   }
   if (P.la_filter && !(p.flags & P_DAEMONSET)) {
@@ -517,7 +522,7 @@ __device__ __forceinline__ bool eval_fast(const EvalRow& n, const DevPod& p, con
   const uint32_t pf = p.flags;
   bool ok = (n.flags & F_VALID) != 0;
   if constexpr ((PF & PF_FIT_FILTER) != 0) {
-    const bool fits = (p.req_cpu <= n.free_cpu) & (p.req_mem <= n.free_mem);
+    const bool fits = (p.req_cpu <= n.free_cpu) & (p.req_mem <= n.free_mem) & !(n.flags & F_EPH_OVER);
     ok = ok & (n.pods_left >= 0) & (((pf & P_ZERO_REQ) != 0) | fits);
   }
   if constexpr ((PF & PF_LA_FILTER) != 0) {
@@ -618,7 +623,7 @@ __device__ __forceinline__ bool eval_hot(const HotRow& n, const DevPod& p, const
   const uint32_t pf = p.flags;
   bool ok = (n.flags & F_VALID) != 0;
   if constexpr ((PF & PF_FIT_FILTER) != 0) {
-    const bool fits = (p.req_cpu32 <= n.free_cpu) & (p.req_mem_d <= n.free_mem);
+    const bool fits = (p.req_cpu32 <= n.free_cpu) & (p.req_mem_d <= n.free_mem) & !(n.flags & F_EPH_OVER);
     ok = ((n.flags & F_PODS_OK) != 0) & (((pf & P_ZERO_REQ) != 0) | fits);
   }
   if constexpr ((PF & PF_LA_FILTER) != 0) {

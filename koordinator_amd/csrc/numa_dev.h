@@ -797,7 +797,9 @@ __device__ __forceinline__ bool alloc_by_hint(const NumaView& v, const NumaPod& 
 #pragma unroll
   for (int i = 0; i < kNumaMax; ++i) a.cpu[i] = a.mem[i] = 0;
   if (v.nn == 0) return false;
-  int64_t rq_c = opt_cpu(v, p), rq_m = p.req_mem;
+  // a cpu-bind pod splits its ORIGINAL requests (resource_manager.go:205-210, options.originalRequests), never the
+  // amplified ones the hints and Score use; other pods' requests are not amplified at all
+  int64_t rq_c = p.req_cpu, rq_m = p.req_mem;
   const bool key_c = p.req_cpu > 0, key_m = p.req_mem > 0;
   bool done = false;
 #pragma unroll

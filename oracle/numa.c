@@ -17,7 +17,7 @@
  *   pkg/scheduler/frameworkext/topologymanager/{manager.go :58-111, policy.go :65-224, policy_best_effort.go,
  *                                               policy_restricted.go, policy_single_numa_node.go}
  *   pkg/util/bitmask/bitmask.go                                 IterateBitMasks :206-222, IsNarrowerThan :146-151
- * Scope: maxRefCount 1, no CPU amplification (ratio ≤ 1), no reservations (preferred CPUs empty),
+ * Scope: maxRefCount 1, CPU amplification included, no reservations (preferred CPUs empty),
  * CPU exclusive policy None, ≤ 4 NUMA nodes, ≤ 256 CPUs.  Go map iteration never decides a result here: every
  * accumulator sort ends on an ID, and the hint providers' resources are taken in sorted-name order (cpu, memory).
  */
@@ -811,7 +811,9 @@ static int allocate(const kg_config* cfg, const or_numa_node* n, const or_numa_p
     if (n->num_numa == 0) return -1;
     int64_t avail_cpu[KG_MAX_NUMA], avail_mem[KG_MAX_NUMA];
     numa_available(n, avail_cpu, avail_mem);
-    int64_t rq_c = opt_req_cpu(n, p), rq_m = p->req_mem;
+    /* a cpu-bind pod splits its ORIGINAL (un-amplified) requests (:205-210: options.originalRequests); any other
+     * pod's requests are never amplified, so the plain request is right for both */
+    int64_t rq_c = p->req_cpu, rq_m = p->req_mem;
     const int key_c = p->req_cpu > 0, key_m = p->req_mem > 0;
     int inter_c = 0, inter_m = 0;
     for (int i = 0; i < n->num_numa; i++) {

@@ -244,11 +244,12 @@ void or_la_node_terms(const kg_config* cfg, const kg_node_metric* m, const kg_po
   for (int view = 0; view < 2; view++) {
     int64_t used[2] = {0, 0};       /* Σ over estimated pods of (counted value − EstimatePod) − Σ non-estimated EstimatePod */
     int64_t est_pods_usage[2] = {0, 0}, pods_usage[2] = {0, 0};
-    char estimated[256] = {0};
+    char* estimated = (char*)calloc(n_pm > 0 ? (size_t)n_pm : 1, 1); /* estimatedPods, indexed like pm */
+    if (!estimated) return;
     for (int64_t a = 0; a < n_as; a++) {
       if (view == 1 && !as[a].prod) continue;                                          /* :350-352 */
       int64_t hit = -1;
-      for (int64_t q = 0; as[a].uid != 0 && q < n_pm && q < 256; q++)
+      for (int64_t q = 0; as[a].uid != 0 && q < n_pm; q++)
         if (pm[q].uid == as[a].uid && (view == 0 || pm[q].prod)) { hit = q; break; }   /* podMetrics[podName] */
       const int has_usage = hit >= 0 && (pm[hit].usage_present & 3) != 0;              /* len(podUsage) != 0 */
       const int missed = as[a].time > upd;                                             /* helper.go:50-52 */
@@ -264,11 +265,12 @@ void or_la_node_terms(const kg_config* cfg, const kg_node_metric* m, const kg_po
         for (int r = 0; r < 2; r++) used[r] -= as[a].est[r];  /* counted through the reported usages instead */
       }
     }
-    for (int64_t q = 0; q < n_pm && q < 256; q++) {
+    for (int64_t q = 0; q < n_pm; q++) {
       if (view == 1 && !pm[q].prod) continue;
       for (int r = 0; r < 2; r++)
         if ((pm[q].usage_present >> r) & 1) (estimated[q] ? est_pods_usage : pods_usage)[r] += pm[q].usage[r];
     }
+    free(estimated);
     if (view == 1) {                                                                   /* :302-305 */
       for (int r = 0; r < 2; r++) out[2 + r] = pods_usage[r] + used[r];
     } else {                                                                           /* :306-326 */
@@ -330,10 +332,13 @@ int or_fit_filter(const kg_node* node, const or_node_state* st, const kg_pod* po
     reasons |= KG_REJECT_FIT_CPU;
   if (pod->requests[KG_RES_MEMORY] > node->allocatable[KG_RES_MEMORY] - st->requested[KG_RES_MEMORY])
     reasons |= KG_REJECT_FIT_MEMORY;
-  /* ephemeral-storage and the scalar (batch / mid cpu / memory) resources the pod requests
-   * (reservation/plugin.go:469-479: EphemeralStorage, then `for rName, rQuant := range podRequest.ScalarResources`).
-   * A resource the pod does not request (0) is not compared: the engine keeps no per-pod key set for these. */
-  for (int r = KG_RES_EPHEMERAL; r <= KG_RES_MID_MEMORY; r++)
+  /* ephemeral-storage for every pod with a non-zero request (reservation/plugin.go:469-471: compared unconditionally,
+   * so an overcommitted node rejects a pod without an ephemeral request too), then the scalar (batch / mid cpu /
+   * memory) resources the pod requests (:472-479 `for rName, rQuant := range podRequest.ScalarResources`): a scalar
+   * the pod does not request (0) is not a key of its request map. */
+  if (pod->requests[KG_RES_EPHEMERAL] > node->allocatable[KG_RES_EPHEMERAL] - st->requested[KG_RES_EPHEMERAL])
+    reasons |= KG_REJECT_FIT_OTHER;
+  for (int r = KG_RES_EPHEMERAL + 1; r <= KG_RES_MID_MEMORY; r++)
     if (pod->requests[r] != 0 && pod->requests[r] > node->allocatable[r] - st->requested[r])
       reasons |= KG_REJECT_FIT_OTHER;
   return reasons;

@@ -266,7 +266,7 @@ int or_schedule_resv_full(const kg_config* cfg, int64_t n_nodes, const kg_node* 
      * reservation is nominated for such a pod (NominateReservation skips failing reservations, nominator.go:99-105) */
     const int ds_blocks_nomination = ds_on && cfg->ds_filter && !dsp.skip;
     int err = 0;
-#pragma omp parallel for schedule(dynamic, chunk) num_threads(n_threads)
+#pragma omp parallel for schedule(dynamic, chunk) num_threads(n_threads) reduction(min : err)
     for (int64_t i = 0; i < n_nodes; i++) {
       feas[i] = 0;
       const kg_node* nd = &nodes[i];

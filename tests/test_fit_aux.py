@@ -7,10 +7,11 @@ Requested column per resource (kAux), checks them for pods that request any of t
 resolver's re-score of modified rows (round-start Requested + this round's earlier placements on the row) and in
 kg_pods_evaluate (KG_REJECT_FIT_OTHER), and moves Requested on assume / kg_pods_add / kg_pods_remove / Unreserve.
 
-Parity unpinned beyond the restated comparison: no reference test drives these resources through a cluster.  One
-documented divergence: a resource the pod does not request (0) is not compared, so a node whose ephemeral-storage
-Requested exceeds its Allocatable still admits pods without an ephemeral request (the reference compares 0 > negative
-and rejects them); the synthetic clusters never overcommit."""
+Parity unpinned beyond the restated comparison: no reference test drives these resources through a cluster.
+Ephemeral-storage is compared for every pod with a non-zero request (reservation/plugin.go:469-471), so a node whose
+ephemeral Requested exceeds its Allocatable (bound pods added over it) rejects pods without an ephemeral request too:
+the device keeps that verdict as a node flag (F_EPH_OVER), refreshed after every host delta.  A scalar resource the
+pod does not request is not a key of its request map and is not compared."""
 import numpy as np
 import pytest
 
@@ -159,3 +160,44 @@ def test_gpu_aux_unreserve_and_remove():
         gn2 = e.schedule(pods[1000:])[0]
         on2, _ = oracle.schedule(cfg, cl.nodes, cl.metrics, rm, pods[1000:], cl.now_ns, 4)
         np.testing.assert_array_equal(gn2, on2)
+
+
+def _overcommit_case():
+    """Two identical nodes with 10Gi ephemeral-storage; node 0 is overcommitted by a bound pod asking 20Gi.  A plain
+    cpu / memory pod (no ephemeral request) must skip node 0: 0 > 10Gi - 20Gi (reservation/plugin.go:469-471)."""
+    cfg = F.build_config(profile=F.Profile(filter=(F.NODE_RESOURCES_FIT,), score={F.NODE_RESOURCES_FIT: 1}))
+    nodes = np.concatenate([F.make_node({"cpu": "32", "memory": str(64 * GI), "ephemeral-storage": str(10 * GI)})] * 2)
+    metrics = np.concatenate([F.make_node_metric(present=False)] * 2)
+    bound = F.make_pod({"cpu": "1", "memory": str(GI), "ephemeral-storage": str(20 * GI)})
+    pod = F.make_pod({"cpu": "1", "memory": str(GI)})
+    zero = F.make_pod({})
+    return cfg, nodes, metrics, bound, pod, zero
+
+
+def test_ephemeral_overcommit_oracle():
+    cfg, nodes, metrics, bound, pod, zero = _overcommit_case()
+    st = oracle.states(2)
+    oracle.add_pods(cfg, st, bound, np.zeros(1, np.int32))
+    assert oracle.fit_filter(nodes[0:1], st[0:1], pod) == abi.REJECT_FIT_OTHER
+    assert oracle.fit_filter(nodes[0:1], st[0:1], zero) == 0  # a zero request skips every resource compare
+    assert oracle.fit_filter(nodes[1:2], st[1:2], pod) == 0
+
+
+@pytest.mark.gpu
+def test_ephemeral_overcommit_device():
+    cfg, nodes, metrics, bound, pod, zero = _overcommit_case()
+    with Engine(cfg, 2) as e:
+        e.upsert_nodes(nodes)
+        e.update_metrics(metrics, 0)
+        e.add_pods(bound, np.zeros(1, np.int32))
+        rej, _, _ = e.evaluate(pod)
+        assert rej.tolist() == [abi.REJECT_FIT_OTHER, 0]
+        rej, _, _ = e.evaluate(zero)
+        assert rej.tolist() == [0, 0]
+        # load node 1 so that LeastAllocated would prefer node 0 if it were feasible
+        e.add_pods(F.make_pod({"cpu": "16", "memory": str(32 * GI)}), np.ones(1, np.int32))
+        got, _, _ = e.schedule(np.concatenate([pod] * 3))
+        assert got.tolist() == [1, 1, 1]
+        e.remove_pods(bound, np.zeros(1, np.int32))  # the overcommit ends: node 0 (emptier) wins again
+        got, _, _ = e.schedule(pod)
+        assert got.tolist() == [0]

@@ -124,3 +124,48 @@ def test_evaluate_numa_amplified_matches_oracle():
                                         (st["requested"][i, abi.RES_CPU], st["requested"][i, abi.RES_MEMORY]),
                                         (alloc[i, abi.RES_CPU], alloc[i, abi.RES_MEMORY]))
                 assert (bool(ok[i]), int(sc[i]), int(af[i])) == want, (k, i)
+
+
+def _cpubind_amplified_case():
+    """One 32-cpu node (2 sockets x 1 NUMA x 8 cores x 2 threads) at cpu ratio 2, SingleNUMANode policy, and an LSR
+    pod asking 4 cpus: the hints see the amplified 8000m, the per-NUMA split takes the ORIGINAL 4000m
+    (resource_manager.go:205-210), so the pod is placed with 4 cpus and NUMA node 0 records 4000m."""
+    cfg = F.build_config(profile=PROFILE)
+    zones = [{"cpu": "32", "memory": str(64 << 30)}] * 2
+    nn = F.make_node_numa(2, 1, 8, 2, numa_policy="SingleNUMANode", numa_resources=zones, cpu_amplification_ratio=2.0)
+    node = F.make_node({"cpu": "64", "memory": str(128 << 30)})
+    metric = F.make_node_metric(present=False)
+    pod = F.make_pod({"cpu": "4", "memory": str(1 << 30)}, priority_class="koord-prod", qos="LSR")
+    return cfg, nn, node, metric, pod
+
+
+def test_cpubind_amplified_split_oracle():
+    cfg, nn, node, metric, pod = _cpubind_amplified_case()
+    st = oracle.states(1)
+    buf = oracle.numa_states(nn)
+    got, _, cpus, _, nalloc = oracle.schedule_full(cfg, node, metric, st, pod, 0, 1, numa_buf=buf,
+                                                   with_numa_alloc=True)
+    assert got[0] == 0
+    assert len(F.cpuset_of(cpus[0])) == 4
+    _, c, m = oracle.numa_state_read(buf, 1)
+    assert c[0].tolist() == [4000, 0, 0, 0] and m[0].tolist() == [1 << 30, 0, 0, 0]
+    oracle.unreserve(cfg, st, pod, 0, numa_buf=buf, cpus=cpus[0], numa_alloc=nalloc[0])
+    a, c, m = oracle.numa_state_read(buf, 1)
+    assert not a.any() and not c.any() and not m.any()
+
+
+@pytest.mark.gpu
+def test_cpubind_amplified_split_device():
+    cfg, nn, node, metric, pod = _cpubind_amplified_case()
+    with Engine(cfg, 1) as e:
+        e.upsert_nodes(node)
+        e.update_metrics(metric, 0)
+        e.upsert_numa(nn)
+        got, _, _ = e.schedule(pod)
+        assert got[0] == 0
+        assert len(F.cpuset_of(e.fetch_cpusets(0, 1)[0])) == 4
+        _, c, m = e.read_numa()
+        assert c[0].tolist() == [4000, 0, 0, 0] and m[0].tolist() == [1 << 30, 0, 0, 0]
+        e.unreserve(0, 1)
+        a, c, m = e.read_numa()
+        assert not a.any() and not c.any() and not m.any()
