@@ -447,7 +447,8 @@ int kg_nodes_read_numa(kg_engine* e, uint64_t* allocated_cpus, int64_t* numa_all
  * empty for pods without a cpuset (the resource-status annotation PreBind writes, plugin.go:427-463). */
 int kg_results_fetch_cpusets(kg_engine* e, int64_t first, int64_t count, uint64_t* out_cpusets);
 /* NodeNUMAResource Filter + Score of one pod on every node slot, the plugin alone: out_pass 1/0, the plugin's
- * unweighted score (0 where Filter rejects) and the affinity the topology manager stores (NUMA mask, -1 = nil). */
+ * unweighted score (0 where Filter rejects) and the affinity the topology manager stores (NUMA mask, -1 = nil).
+ * Filter runs only when the profile enables the plugin at Filter; otherwise Score sees no stored affinity. */
 int kg_pods_evaluate_numa(kg_engine* e, const kg_pod* pod, int32_t* out_pass, int64_t* out_score,
                           int64_t* out_affinity);
 
@@ -471,6 +472,18 @@ int kg_nodes_reservation_upsert(kg_engine* e, const kg_node_reservations* r, con
 int kg_nodes_read_reservations(kg_engine* e, int64_t* allocated_cpu, int64_t* allocated_mem, int64_t* assigned);
 /* The reservation slot Reserve assumed each staged pod [first, first+count) into (-1 = none). */
 int kg_results_fetch_reservations(kg_engine* e, int64_t first, int64_t count, int32_t* out_slot);
+
+/* The exact pass's evaluation of one pod on every node slot (profiles with Reservation, or NodeNUMAResource together
+ * with DeviceShare): BeforePreFilter restore (reservation/transformer.go:49-346), every enabled Filter on the restored
+ * NodeInfo, the nomination (nominator.go:76-134) and the raw Scores, exactly as kg_pods_schedule evaluates the pod —
+ * what frameworkext's --debug-scores prints for it (frameworkext/debug.go:61-108).  KG_RSV_EVAL_WORDS int64 per node:
+ * [0] pass, [1] nominated slot (-1 none), [2] raw Reservation score of it, [3] a nodeReservationState exists (the node
+ * was restored), [4] the matched slots (bit s), [5..9] the restored NodeInfo Requested cpu / memory, NonZeroRequested
+ * cpu / memory, pod count, [10..11] nodeReservationState.podRequested cpu / memory, [12] the weighted total of the
+ * non-normalized plugins (Fit, LoadAware, NodeNUMAResource), [13] raw DeviceShare score, [14] the smallest
+ * reservation-order label among the matched slots (0 none), [15] reserved. */
+#define KG_RSV_EVAL_WORDS 16
+int kg_pods_evaluate_reservation(kg_engine* e, const kg_pod* pod, int64_t* out);
 
 /* ElasticQuota admission (engines whose pods carry quota_id): replaces the quota table (n ≤ KG_MAX_QUOTAS).
  * Every scheduled pod runs PreFilter's check (used + request ≤ used_limit over the pod's cpu/memory requests; for
@@ -504,6 +517,16 @@ int kg_debug_least_requested(kg_engine* e, const int64_t* requested, const int64
  * that routine's exact domain; the engine sends such rows to the exact path). */
 int kg_debug_fast_lrs(kg_engine* e, const int64_t* requested, const int64_t* capacity, int64_t* out_cpu,
                       int64_t* out_mem, int64_t n);
+
+/* Debug: the device topology-manager policy merge — Policy.Merge + canAdmitPodResult over ≤ 2 filtered provider lists
+ * (frameworkext/topologymanager/policy.go:127-185 mergeFilteredHints, policy_best_effort.go:43-48,
+ * policy_restricted.go:41-46, policy_single_numa_node.go:38-77) — exactly the code NodeNUMAResource Filter runs, on n
+ * caller-given cases of KG_DBG_MERGE_WORDS int64: policy (KG_NUMA_POLICY_*), NUMA node count (1..4), list count
+ * (1..2), then per list {hint positions, preferred positions, nil, nil preferred, empty} (positions index the
+ * IterateBitMasks order 1,2,4,8,3,5,9,6,10,12,7,11,13,14,15), then the hint score of each mask 0..15.
+ * out: 8 int64 per case = admit, nil, mask, preferred, score. */
+#define KG_DBG_MERGE_WORDS 32
+int kg_debug_numa_merge(kg_engine* e, const int64_t* cases, int64_t n, int64_t* out);
 
 /* Debug: evaluates every staged pod on every node with both device evaluation paths (the reference-shaped
  * one used for modified rows and per-plugin output, and the hoisted-term one of the wide pass) and returns

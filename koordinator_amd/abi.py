@@ -50,6 +50,8 @@ NUMA_POLICY = {"": 0, "BestEffort": 1, "Restricted": 2, "SingleNUMANode": 3}
 STRATEGY = {"LeastAllocated": 0, "MostAllocated": 1}
 REJECT_NUMA = 32
 REJECT_DEVICE = 64
+RSV_EVAL_WORDS = 16  # KG_RSV_EVAL_WORDS: kg_pods_evaluate_reservation per node
+DBG_MERGE_WORDS = 32  # KG_DBG_MERGE_WORDS: one kg_debug_numa_merge case
 REJECT_FIT_OTHER = 128  # NodeResourcesFit: ephemeral-storage / a scalar resource (RES_EPHEMERAL .. RES_MID_MEMORY)
 # DeviceShare device resources (KG_DEV_*)
 DEV_RES_MAX, MAX_MINORS = 8, 8
@@ -169,7 +171,7 @@ EXPORTED_SYMBOLS = (
     "kg_quotas_set", "kg_quotas_read", "kg_nodes_reservation_upsert", "kg_nodes_read_reservations",
     "kg_results_fetch_reservations", "kg_profile_enable", "kg_profile_read", "kg_loopback_create",
     "kg_loopback_destroy", "kg_engine_create_loopback", "kg_pods_unreserve", "kg_engine_set_clock",
-    "kg_node_pods_metric_set",
+    "kg_node_pods_metric_set", "kg_debug_numa_merge", "kg_pods_evaluate_reservation",
 )
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
@@ -242,6 +244,8 @@ def load_library(path: str | None = None):
         "kg_engine_create_loopback": (i, [vp, i64, i, i, vp, ctypes.POINTER(vp)]),
         "kg_pods_unreserve": (i, [vp, i64, i64, vp]),
         "kg_engine_set_clock": (i, [vp, i64]),
+        "kg_debug_numa_merge": (i, [vp, vp, i64, vp]),
+        "kg_pods_evaluate_reservation": (i, [vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)

@@ -10,7 +10,9 @@
 // The pod's request is decoded on the host (GetPodDeviceRequests → ValidateDeviceRequest → ConvertDeviceRequest,
 // utils.go:158-252); the per-node part (fillGPUTotalMem needs the node's GPU memory) runs here.
 // Scope: GPU devices without hints, joint allocation, VFs, NUMA affinity, reservations or preemption;
-// ScoringStrategy LeastAllocated (the monotone one: an assume only lowers a node's score).
+// ScoringStrategy LeastAllocated or MostAllocated (the latter is not monotone: an assume raises the node's score,
+// which the round resolver handles by re-scoring its modified rows for every pod and ending a round when one of them
+// raises the normalization max).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -44,6 +46,8 @@ static_assert(sizeof(DsPod) == 48, "DsPod layout");
 struct DsParams {
   int32_t filter, score, weight;
   int32_t w_core, w_mem, w_ratio;  // ScoringStrategy.Resources weights
+  int32_t most;                    // ScoringStrategy.Type MostAllocated (mostResourceScorer, scoring.go:281-304)
+  int32_t pad;
 };
 
 struct DsInst {
@@ -84,12 +88,12 @@ __device__ __forceinline__ DsInst ds_instance(const DsNode& d, const DsPod& p) {
 
 __device__ __forceinline__ int64_t ds_sub0(int64_t a, int64_t b) { return a - b > 0 ? a - b : 0; }
 
-// one resource term of leastResourceScorer over (total, free, request) (scoring.go:183-203, 254-279)
+// one resource term of least/mostResourceScorer over (total, free, request) (scoring.go:183-203, 254-304)
 __device__ __forceinline__ void ds_term(int64_t w, int64_t total, int64_t free_, int64_t req, int64_t& num,
-                                        int64_t& ws) {
+                                        int64_t& ws, bool most) {
   if (w == 0 || total == 0) return;
   const int64_t rq = total >= free_ ? total - free_ + req : total;
-  num += least_requested(rq, total) * w;
+  num += (most ? most_requested64(rq, total) : least_requested(rq, total)) * w;
   ws += w;
 }
 
@@ -121,9 +125,10 @@ __device__ __forceinline__ bool ds_eval(const DsNode& d, const DsPod& p, const D
   }
   if (!any || nfit < in.count) return false;
   int64_t num = 0, ws = 0;
-  ds_term(P.w_core, Tc, Fc, in.core, num, ws);
-  ds_term(P.w_mem, Tm, Fm, in.mem, num, ws);
-  ds_term(P.w_ratio, Tr, Fr, in.ratio, num, ws);
+  const bool most = P.most != 0;
+  ds_term(P.w_core, Tc, Fc, in.core, num, ws, most);
+  ds_term(P.w_mem, Tm, Fm, in.mem, num, ws, most);
+  ds_term(P.w_ratio, Tr, Fr, in.ratio, num, ws, most);
   raw = ws ? div_small(num, ws) : 0;
   return true;
 }
@@ -139,9 +144,10 @@ __device__ __forceinline__ int64_t ds_minor(const DsNode& d, int m, const DsInst
   nonzero = (fc | fr | fm) != 0;
   fits = nonzero && ((d.present >> m) & 1) && in.core <= fc && in.mem <= fm && in.ratio <= fr;
   int64_t num = 0, ws = 0;
-  ds_term(P.w_core, d.tcore[m], fc, in.core, num, ws);
-  ds_term(P.w_mem, d.tmem[m], fm, in.mem, num, ws);
-  ds_term(P.w_ratio, d.tratio[m], fr, in.ratio, num, ws);
+  const bool most = P.most != 0;
+  ds_term(P.w_core, d.tcore[m], fc, in.core, num, ws, most);
+  ds_term(P.w_mem, d.tmem[m], fm, in.mem, num, ws, most);
+  ds_term(P.w_ratio, d.tratio[m], fr, in.ratio, num, ws, most);
   return ws ? div_small(num, ws) : 0;
 }
 

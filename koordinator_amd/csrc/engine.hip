@@ -1248,8 +1248,7 @@ __global__ void evaluate_pod_numa(DevTable T, NumaTable NT, const DevPod* __rest
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const Row r = load_row(T, i);
-  NumaParams q = NP;
-  q.filter = 1;
+  NumaParams q = NP;  // Filter only when the profile runs it (a Score-only profile scores the nil affinity)
   q.score = 1;
   int64_t sc = 0;
   NumaHint aff;
@@ -1542,9 +1541,12 @@ __global__ __launch_bounds__(kWave) void resolve_round_ds(DevTable T, DsTable DT
     // M_j: the round-start max survives while an unmodified node or a modified row still holds it.  At most nM
     // holders can have been modified, so with more than nM holders nothing needs checking.  A modified row's
     // round-start value for pod j is what ds_max_round packed for it (dsval): no re-score.
+    // MostAllocated: an assume RAISES the node's raw score, so a modified row can also lift the max above M — the
+    // modified rows are re-scored for every pod and the round ends when their max exceeds the round-start M.
+    const bool most = DP.most != 0;
     bool cf = false, have_cur = false;
     int64_t ct = 0, craw = 0;
-    if (DP.score && Mrs > 0 && Crs <= (uint32_t)nM) {
+    if (DP.score && Mrs > 0 && (most ? nM > 0 : Crs <= (uint32_t)nM)) {
       uint32_t pk = 0;
       if (lane < nM) {
         if (sharded) {
@@ -1557,11 +1559,12 @@ __global__ __launch_bounds__(kWave) void resolve_round_ds(DevTable T, DsTable DT
       const bool rf = pk != 0;
       const int64_t rraw = (int64_t)((pk - 1u) & 255u);
       const uint32_t lost = (uint32_t)__popcll(__ballot(rf && (uint32_t)rraw + 1u == Mrs));
-      if (lost >= Crs) {
+      if (most || lost >= Crs) {
         if (lane < nM) cf = eval_node(mrow, p, P, ct) && ds_eval(s_dc[lane], dp, DP, craw);
         have_cur = true;
         const uint32_t cm = wave_max_u32(cf ? (uint32_t)craw + 1u : 0u);
-        if (cm != Mrs) break;  // the normalization changed: every key of the round's lists is stale
+        // the normalization changed: every key of the round's lists is stale
+        if (cm > Mrs || (lost >= Crs && cm != Mrs)) break;
       }
     }
     const uint32_t Mj = Mrs ? Mrs - 1u : 0u;
@@ -1572,7 +1575,7 @@ __global__ __launch_bounds__(kWave) void resolve_round_ds(DevTable T, DsTable DT
     uint64_t best = um ? readlane_u64(key, pos) : 0;
     // With M_j = the round-start M every plugin term is monotone (an assume only lowers a node's key), so a
     // modified row can only beat the best unmodified candidate when that is not the pod's overall top key.
-    if (nM > 0 && pos != 0) {
+    if (nM > 0 && (pos != 0 || most)) {
       if (!have_cur && lane < nM) cf = eval_node(mrow, p, P, ct) && ds_eval(s_dc[lane], dp, DP, craw);
       const uint64_t mk = cf ? make_key(ct + (DP.score ? DP.weight * ds_normalized(craw, Mj) : 0), midx) : 0;
       const uint64_t mbest = wave_max_key(mk);
@@ -1688,6 +1691,30 @@ __global__ void evaluate_pod_ds(DsTable DT, const DsPod* __restrict__ pod, int64
   const bool ok = ds_eval(DT.d[i], *pod, DP, raw);
   pass[i] = ok ? 1 : 0;
   score[i] = ok ? raw : 0;
+}
+
+// kg_pods_evaluate_reservation: the exact pass's per-node evaluation of one pod (restore, every Filter, nomination,
+// raw Scores) with the restore's state; KG_RSV_EVAL_WORDS int64 per node
+__global__ void evaluate_pod_rsv(DevTable T, const RsvNode* __restrict__ RN, const int32_t* __restrict__ rsv_n,
+                                 const DevPod* __restrict__ pod, const RsvPod* __restrict__ rpod,
+                                 const DsPod* __restrict__ dpod, const NumaPod* __restrict__ npod, int64_t n,
+                                 EvalParams P, RsvParams RP, RsvExt X, int64_t* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  RsvDbg d;
+  const RsvOut o = rsv_eval_node(T, RN, rsv_n, i, *pod, *rpod, P, RP, X, dpod, npod, &d);
+  int64_t* w = out + (size_t)i * KG_RSV_EVAL_WORDS;
+  w[0] = o.feas ? 1 : 0;
+  w[1] = o.feas ? o.nom : -1;
+  w[2] = o.feas ? o.raw : 0;
+  w[3] = d.has_state;
+  w[4] = d.matched;
+  w[5] = d.req_cpu, w[6] = d.req_mem, w[7] = d.nz_cpu, w[8] = d.nz_mem, w[9] = d.num_pods;
+  w[10] = d.pod_req_cpu, w[11] = d.pod_req_mem;
+  w[12] = o.feas ? o.base : 0;
+  w[13] = o.feas ? o.dsraw : 0;
+  w[14] = o.order == 0x7fffffff ? 0 : o.order;
+  w[15] = 0;
 }
 
 // Scatter of upserted device rows
@@ -1882,6 +1909,31 @@ __global__ void debug_eval_paths(DevTable T, const DevPod* __restrict__ pods, in
   if (bad) atomicAdd(mismatches, bad);
 }
 
+// kg_debug_numa_merge: one case per thread through policy_merge, the merge numa_admit runs.  Case layout
+// (KG_DBG_MERGE_WORDS int64): policy, NUMA node count, list count (1..2), then per list {positions, preferred
+// positions, nil, nil preferred, empty}, then the hint score of each mask 0..15.  Out: admit, nil, mask, preferred,
+// score (8 words per case).
+__global__ void debug_numa_merge(const int64_t* __restrict__ in, int64_t n, int64_t* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t* c = in + (size_t)i * KG_DBG_MERGE_WORDS;
+  HintList L[2];
+#pragma unroll
+  for (int l = 0; l < 2; ++l)
+    L[l] = HintList{(uint32_t)c[3 + 5 * l], (uint32_t)c[4 + 5 * l], (int)c[5 + 5 * l], (int)c[6 + 5 * l],
+                    (int)c[7 + 5 * l]};
+  const int64_t* sc = c + 13;
+  const auto score_of = [&](uint32_t m) -> int { return (int)sc[m & 15u]; };
+  NumaHint best;
+  const bool admit = policy_merge((int)c[0], (1u << (int)c[1]) - 1u, L[0], L[1], (int)c[2], score_of, best);
+  int64_t* o = out + (size_t)i * 8;
+  o[0] = admit;
+  o[1] = best.nil;
+  o[2] = best.mask;
+  o[3] = best.preferred;
+  o[4] = best.score;
+}
+
 __global__ void debug_least_requested(const int64_t* req, const int64_t* cap, int64_t* out, int64_t n) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) out[i] = least_requested(req[i], cap[i]);
@@ -2039,6 +2091,10 @@ struct kg_engine {
   int nq = 0;
   // Reservation (profile enables it): per-node slots, per-pod owner/affinity, Reserve's slots, pass scratch
   bool rsv_on = false;
+  // the per-pod exact pass (rsv_eval / rsv_select / rsv_apply) runs the profile: Reservation, or NodeNUMAResource
+  // together with DeviceShare (the reference's shipped profile, config/manager/scheduler-config.yaml:66-117)
+  bool exact_on = false;
+  DevBuf<uint32_t> numa_aff;  // exact pass: the NUMA affinity Filter stored per node for the pass's pod
   RsvParams RP{};
   DevBuf<RsvNode> rsv_d;
   DevBuf<int32_t> rsv_nd;       // slots in use per node
@@ -2119,18 +2175,15 @@ int validate_config(const kg_config* c) {
     return fail(KG_E_INVALID, "LoadAwareSchedulingArgs.Aggregated: aggregation type / duration");
   if (c->reservation_filter || c->reservation_score) {
     if (c->weight_reservation < 0 || c->weight_reservation > 1000000) return fail(KG_E_INVALID, "Reservation weight out of range");
-    if (c->numa_filter || c->numa_score)
-      return fail(KG_E_UNSUPPORTED, "Reservation with NodeNUMAResource in one profile is not accelerated");
   }
   if (c->ds_filter || c->ds_score) {
     if (c->weight_deviceshare < 0 || c->weight_deviceshare > 1000000) return fail(KG_E_INVALID, "DeviceShare weight out of range");
-    if (c->ds_scoring_strategy != KG_STRATEGY_LEAST_ALLOCATED)
-      return fail(KG_E_UNSUPPORTED, "DeviceShare scoring strategy: LeastAllocated only is accelerated");
+    if (c->ds_scoring_strategy != KG_STRATEGY_LEAST_ALLOCATED && c->ds_scoring_strategy != KG_STRATEGY_MOST_ALLOCATED)
+      return fail(KG_E_UNSUPPORTED, "DeviceShare scoring strategy: LeastAllocated / MostAllocated");
     for (int r = 0; r < 3; ++r)
       if (c->ds_scoring_weights[r] < 0 || c->ds_scoring_weights[r] > 1000000) return fail(KG_E_INVALID, "DeviceShare scoring weight");
     if (c->ds_score && !c->ds_filter)
       return fail(KG_E_UNSUPPORTED, "DeviceShare at Score needs DeviceShare at Filter (Score errors on unfiltered nodes)");
-    if (c->numa_filter || c->numa_score) return fail(KG_E_UNSUPPORTED, "NodeNUMAResource + DeviceShare in one profile");
     if (c->batch_pods > 32) return fail(KG_E_UNSUPPORTED, "DeviceShare profiles: batch_pods <= 32");
     if (100 * ((c->fit_score ? c->weight_fit : 0) + (c->la_score ? c->weight_loadaware : 0)) >= (1 << 23))
       return fail(KG_E_UNSUPPORTED, "DeviceShare profiles: Fit + LoadAware weights must keep totals below 2^23");
@@ -3040,6 +3093,13 @@ RsvExt rsv_ext(kg_engine* e) {
   X.qdev = e->qdev.p;
   X.out_minors = e->ds_on ? e->out_minors.p : nullptr;
   X.nq = e->nq;
+  X.ns = e->numa_on ? e->numa_s.p : nullptr;
+  X.nm = e->numa_on ? e->numa_m.p : nullptr;
+  X.npods = e->numa_on ? e->npods.p : nullptr;
+  X.NP = e->NP;
+  X.aff = e->numa_on ? e->numa_aff.p : nullptr;
+  X.out_cpus = e->numa_on ? e->out_cpus.p : nullptr;
+  X.out_nrec = e->numa_on ? e->out_nrec.p : nullptr;
   return X;
 }
 
@@ -3313,11 +3373,15 @@ static int engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank,
   e->numa_on = c.numa_filter || c.numa_score;
   e->ds_on = c.ds_filter || c.ds_score;
   e->rsv_on = c.reservation_filter || c.reservation_score;
-  if (e->rsv_on && n_ranks > 1) return bail(fail(KG_E_UNSUPPORTED, "Reservation profiles run on one rank"));
+  e->exact_on = e->rsv_on || (e->numa_on && e->ds_on);
+  if (e->exact_on && n_ranks > 1)
+    return bail(fail(KG_E_UNSUPPORTED, "Reservation / NodeNUMAResource + DeviceShare profiles run on one rank"));
   e->RP.filter = (int32_t)(c.reservation_filter != 0);
   e->RP.score = (int32_t)(c.reservation_score != 0);
   e->RP.weight = (int32_t)c.weight_reservation;
-  if (e->rsv_on) {
+  if (e->exact_on) {
+    if (e->numa_on)
+      if (int rc = e->numa_aff.ensure(cap)) return bail(rc);
     if (int rc = e->rsv_d.ensure(cap)) return bail(rc);
     if (int rc = e->rsv_nd.ensure(cap)) return bail(rc);
     if (int rc = e->rsv_val.ensure(cap)) return bail(rc);
@@ -3338,6 +3402,7 @@ static int engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank,
   e->DP.w_core = (int32_t)c.ds_scoring_weights[0];
   e->DP.w_mem = (int32_t)c.ds_scoring_weights[1];
   e->DP.w_ratio = (int32_t)c.ds_scoring_weights[2];
+  e->DP.most = (int32_t)(c.ds_scoring_strategy == KG_STRATEGY_MOST_ALLOCATED);
   if (e->ds_on) {
     if (int rc = e->ds_d.ensure(cap)) return bail(rc);
     e->ds_host.assign(cap, DsNode{});
@@ -3724,7 +3789,7 @@ int kg_pods_stage(kg_engine* e, const kg_pod* pods, int64_t n) {
           return fail(KG_E_UNSUPPORTED, "pod %lld requests devices; the profile has no DeviceShare (NodeResourcesFit on "
                       "device resources is not accelerated)", (long long)k);
   }
-  if (e->rsv_on) {
+  if (e->exact_on) {
     std::vector<RsvPod> hr(std::max<int64_t>(n, 1));
     for (int64_t k = 0; k < n; ++k) {
       hr[k].owner_mask = (uint64_t)pods[k].reservation_owner_mask;
@@ -3773,7 +3838,7 @@ static int schedule_staged_impl(kg_engine* e, int64_t first, int64_t count, kg_s
   if (!e) return fail(KG_E_INVALID, "engine is NULL");
   if (first < 0 || count < 0 || first + count > e->n_staged) return fail(KG_E_INVALID, "staged range");
   const double t0 = now_s();
-  if (e->rsv_on) return run_rsv(e, first, count, stats, t0);
+  if (e->exact_on) return run_rsv(e, first, count, stats, t0);
   RoundGeom g;
   if (int rc = prepare_rounds(e, g)) return rc;
   const int64_t end = first + count;
@@ -4145,15 +4210,17 @@ static int bench_rsv(kg_engine* e, int which, int iters, double* avg_ms, double*
     HIP_TRY(hipMemcpy(&d0, e->dpods.p, sizeof(DsPod), hipMemcpyDeviceToHost));
     dev_pod = !d0.skip;
   }
+  // NodeNUMAResource: the NumaStatic + NodeAllocation rows and the stored affinity of every node
   if (algo_bytes)
     *algo_bytes = which == 0 ? (double)n * (76 + 4 + 8) + (double)with_slots * sizeof(RsvNode) +
-                                   (dev_pod ? (double)n * sizeof(DsNode) : 0.0)
+                                   (dev_pod ? (double)n * sizeof(DsNode) : 0.0) +
+                                   (e->numa_on ? (double)n * (sizeof(NumaStatic) + sizeof(NumaMut) + 4) : 0.0)
                              : (double)n * 8;
   return 0;
 }
 
 int kg_bench_kernel(kg_engine* e, int which, int iters, double* avg_ms, double* algo_bytes) {
-  if (e && e->rsv_on) return bench_rsv(e, which, iters, avg_ms, algo_bytes);
+  if (e && e->exact_on) return bench_rsv(e, which, iters, avg_ms, algo_bytes);
   if (!e || iters <= 0 || which < 0 || which > (e && e->ds_on ? 4 : 2)) return fail(KG_E_INVALID, "bad argument");
   if (e->n_staged <= 0) return fail(KG_E_INVALID, "stage a pod queue first");
   RoundGeom g;
@@ -4293,6 +4360,25 @@ int kg_debug_stamps(kg_engine* e, uint64_t* out) {
 #endif
 }
 
+int kg_debug_numa_merge(kg_engine* e, const int64_t* cases, int64_t n, int64_t* out) {
+  if (!e || (n > 0 && (!cases || !out))) return fail(KG_E_INVALID, "null argument");
+  if (n <= 0) return 0;
+  for (int64_t i = 0; i < n; ++i) {
+    const int64_t* c = cases + (size_t)i * KG_DBG_MERGE_WORDS;
+    if (c[0] < 0 || c[0] > 3 || c[1] < 1 || c[1] > kNumaMax || c[2] < 1 || c[2] > 2)
+      return fail(KG_E_INVALID, "merge case %lld: policy / NUMA count / list count", (long long)i);
+  }
+  DevBuf<int64_t> din, dout;
+  if (int rc = din.ensure((size_t)n * KG_DBG_MERGE_WORDS)) return rc;
+  if (int rc = dout.ensure((size_t)n * 8)) return rc;
+  HIP_TRY(hipMemcpy(din.p, cases, (size_t)n * KG_DBG_MERGE_WORDS * 8, hipMemcpyHostToDevice));
+  debug_numa_merge<<<(unsigned)((n + 63) / 64), 64, 0, e->stream>>>(din.p, n, dout.p);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  HIP_TRY(hipMemcpy(out, dout.p, (size_t)n * 8 * 8, hipMemcpyDeviceToHost));
+  return 0;
+}
+
 int kg_debug_least_requested(kg_engine* e, const int64_t* req, const int64_t* cap, int64_t* out, int64_t n) {
   if (!e || n < 0 || (n > 0 && (!req || !cap || !out))) return fail(KG_E_INVALID, "bad argument");
   if (n == 0) return 0;
@@ -4367,6 +4453,45 @@ int kg_nodes_read_reservations(kg_engine* e, int64_t* allocated_cpu, int64_t* al
       if (allocated_mem) allocated_mem[i * KG_MAX_RSV_SLOTS + s] = on ? h[i].allocd_mem[s] : 0;
       if (assigned) assigned[i * KG_MAX_RSV_SLOTS + s] = on ? h[i].assigned[s] : 0;
     }
+  return 0;
+}
+
+int kg_pods_evaluate_reservation(kg_engine* e, const kg_pod* pod, int64_t* out) {
+  if (!e || !pod || !out) return fail(KG_E_INVALID, "null argument");
+  if (!e->exact_on) return fail(KG_E_INVALID, "the profile does not run the exact pass (Reservation or NUMA + DeviceShare)");
+  if (int rc = sync_static(e)) return rc;
+  DevPod d;
+  if (int rc = decode_pod(e, *pod, d)) return rc;
+  RsvPod rp{(uint64_t)pod->reservation_owner_mask, (pod->reservation_flags & KG_POD_RSV_AFFINITY) ? RP_AFFINITY : 0u, 0};
+  DsPod dsp{};
+  dsp.skip = 1;
+  if (e->ds_on)
+    if (int rc = decode_ds_pod(*pod, dsp)) return rc;
+  NumaPod np{};
+  if (e->numa_on)
+    if (int rc = decode_numa_pod(e->cfg, *pod, np)) return rc;
+  const int64_t n = e->n_nodes;
+  if (n == 0) return 0;
+  const int64_t words = (int64_t)KG_RSV_EVAL_WORDS * n;
+  const int64_t pw = kPodWords + (int64_t)(sizeof(RsvPod) / 8) + kDsPodWords + kNumaPodWords;
+  if (int rc = e->scratch64.ensure(words + pw)) return rc;
+  DevPod* gp = reinterpret_cast<DevPod*>(e->scratch64.p + words);
+  RsvPod* gr = reinterpret_cast<RsvPod*>(e->scratch64.p + words + kPodWords);
+  DsPod* gd = reinterpret_cast<DsPod*>(e->scratch64.p + words + kPodWords + sizeof(RsvPod) / 8);
+  NumaPod* gn = reinterpret_cast<NumaPod*>(e->scratch64.p + words + kPodWords + sizeof(RsvPod) / 8 + kDsPodWords);
+  HIP_TRY(hipMemcpyAsync(gp, &d, sizeof(d), hipMemcpyHostToDevice, e->stream));
+  HIP_TRY(hipMemcpyAsync(gr, &rp, sizeof(rp), hipMemcpyHostToDevice, e->stream));
+  HIP_TRY(hipMemcpyAsync(gd, &dsp, sizeof(dsp), hipMemcpyHostToDevice, e->stream));
+  HIP_TRY(hipMemcpyAsync(gn, &np, sizeof(np), hipMemcpyHostToDevice, e->stream));
+  RsvExt X = rsv_ext(e);
+  X.aff = nullptr;  // no pass affinity store: this is not a scheduling pass
+  evaluate_pod_rsv<<<(unsigned)((n + 255) / 256), 256, 0, e->stream>>>(e->T, e->rsv_d.p, e->rsv_nd.p, gp, gr,
+                                                                       e->ds_on ? gd : nullptr,
+                                                                       e->numa_on ? gn : nullptr, n, e->P, e->RP, X,
+                                                                       e->scratch64.p);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(out, e->scratch64.p, words * 8, hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
   return 0;
 }
 

@@ -202,6 +202,21 @@ __device__ __forceinline__ int64_t least_requested(int64_t requested, int64_t ca
   return q;
 }
 
+// mostRequestedScore (nodenumaresource/most_allocated.go:50-62, deviceshare/scoring.go:294-304): (min(requested, capacity) · 100) / capacity, division-free like
+// least_requested (kernels.h): a float quotient estimate corrected by one exact int64 compare each way.
+__device__ __forceinline__ int64_t most_requested64(int64_t requested, int64_t capacity) {
+  if (capacity == 0) return 0;
+  if (requested > capacity) requested = capacity;
+  const int64_t num = requested * 100;
+  if (requested < 0) return num / capacity;
+  int q = (int)(((float)requested * 100.0f) / (float)capacity);
+  q = q < 0 ? 0 : (q > 100 ? 100 : q);
+  const int64_t t = (int64_t)q * capacity;
+  if (t > num) q -= 1;
+  else if (t + capacity <= num) q += 1;
+  return q;
+}
+
 // s / w for the per-plugin weight sums: 32-bit unsigned division whenever both fit (always, for validated
 // weights ≤ 1e6), exact int64 truncating division otherwise (Go semantics).
 __device__ __forceinline__ int64_t div_small(int64_t s, int64_t w) {

@@ -471,21 +471,6 @@ __device__ __forceinline__ uint32_t mask_at(int k) {
   return (uint32_t)((order >> (4 * k)) & 15ull);
 }
 
-// mostRequestedScore (most_allocated.go:50-62): (min(requested, capacity) · 100) / capacity, division-free like
-// least_requested (kernels.h): a float quotient estimate corrected by one exact int64 compare each way.
-__device__ __forceinline__ int64_t most_requested64(int64_t requested, int64_t capacity) {
-  if (capacity == 0) return 0;
-  if (requested > capacity) requested = capacity;
-  const int64_t num = requested * 100;
-  if (requested < 0) return num / capacity;
-  int q = (int)(((float)requested * 100.0f) / (float)capacity);
-  q = q < 0 ? 0 : (q > 100 ? 100 : q);
-  const int64_t t = (int64_t)q * capacity;
-  if (t > num) q -= 1;
-  else if (t + capacity <= num) q += 1;
-  return q;
-}
-
 // resourceAllocationScorer.score (scoring.go:191-230) over cpu + memory with least/mostResourceScorer.  The
 // strategy is a profile constant: an explicit branch keeps the unused scorer out of the instruction stream.
 __device__ __forceinline__ int64_t numa_scorer(int strategy, int32_t w_cpu, int32_t w_mem, int64_t req_c, int64_t req_m,
@@ -609,18 +594,23 @@ __device__ __forceinline__ int numa_pref_bind(const NumaView& v, int preferred) 
 }
 
 // One provider list of the topology manager: a single "don't care" (nil) hint, or hints over the masks of a
-// set of enumeration positions; `empty` = no hint at all
+// set of enumeration positions, each preferred or not; `empty` = no hint at all
 struct HintList {
-  uint32_t set;  // positions k (mask_at(k)) in enumeration order
-  int nil, nil_pref, empty, min_size;
+  uint32_t set;   // positions k (mask_at(k)) in enumeration order
+  uint32_t pref;  // positions whose hint is preferred
+  int nil, nil_pref, empty;
 };
 
-// positions of a list's preferred hints: generateResourceHints marks a mask preferred iff its size is the
-// list's minimum; mask_at enumerates by size, so a size class is a contiguous run of positions
+// enumeration positions of the masks of one size: mask_at enumerates by size, so a size class is a contiguous run
+// (generateResourceHints marks a mask preferred iff its size is the list's minimum, resource_manager.go:511-525)
+__device__ __forceinline__ uint32_t size_class(int size) {
+  return size == 1 ? 0x000Fu : size == 2 ? 0x03F0u : size == 3 ? 0x3C00u : 0x4000u;
+}
+
+// positions of a list's preferred hints
 __device__ __forceinline__ uint32_t preferred_positions(const HintList& L) {
   if (L.nil) return L.nil_pref ? 1u : 0u;
-  const uint32_t cls = L.min_size == 1 ? 0x000Fu : L.min_size == 2 ? 0x03F0u : L.min_size == 3 ? 0x3C00u : 0x4000u;
-  return L.set & cls;
+  return L.set & L.pref;
 }
 
 // mergeFilteredHints (policy.go:127-185) over the permutations of ≤ 2 lists (the last varies fastest).
@@ -645,11 +635,11 @@ __device__ __forceinline__ NumaHint merge_hints(uint32_t def, const HintList L0,
     for (uint32_t a = t0; a; a &= a - 1) {
       const int ka = __builtin_ctz(a);
       const uint32_t ma = L0.nil ? def : mask_at(ka);
-      const bool pa = L0.nil ? L0.nil_pref != 0 : __popc(ma) == L0.min_size;
+      const bool pa = L0.nil ? L0.nil_pref != 0 : ((L0.pref >> ka) & 1u) != 0;
       for (uint32_t b = t1; b; b &= b - 1) {
         const int kb = __builtin_ctz(b);
         const uint32_t mb = nilb ? def : mask_at(kb);
-        const bool pb = nl > 1 ? (nilb ? L1.nil_pref != 0 : __popc(mb) == L1.min_size) : true;
+        const bool pb = nl > 1 ? (nilb ? L1.nil_pref != 0 : ((L1.pref >> kb) & 1u) != 0) : true;
         const uint32_t merged = def & ma & mb;
         if (merged == 0) continue;
         const int preferred = pa && pb;
@@ -681,15 +671,26 @@ __device__ __forceinline__ HintList single_numa_only(HintList L) {
     if (!L.nil_pref) L.empty = 1;
     return L;
   }
-  uint32_t keep = 0;
-  if (L.min_size == 1)
-    for (uint32_t b = L.set; b; b &= b - 1) {
-      const int k = __builtin_ctz(b);
-      if (__popc(mask_at(k)) == 1) keep |= 1u << k;
-    }
+  const uint32_t keep = L.set & L.pref & size_class(1);  // positions 0..3 are the single-NUMA masks
   L.set = keep;
   if (!keep) L.empty = 1;
   return L;
+}
+
+// Policy.Merge + canAdmitPodResult (policy_best_effort.go:43-48, policy_restricted.go:41-46,
+// policy_single_numa_node.go:62-77) over ≤ 2 provider lists.  One merge for every policy (lanes of one wave hold
+// nodes of different policies: a single inlined merge keeps the divergent path to one copy).
+template <typename ScoreOf>
+__device__ __forceinline__ bool policy_merge(int policy, uint32_t def, const HintList& L0, const HintList& L1, int nl,
+                                             const ScoreOf& score_of, NumaHint& best) {
+  const bool single = policy == 3 /*SingleNUMANode*/;
+  best = merge_hints(def, single ? single_numa_only(L0) : L0, single ? single_numa_only(L1) : L1, nl, score_of);
+  if (single) {
+    if (!best.nil && best.mask == def) best = NumaHint{0, 1, best.preferred, 0};
+    return best.preferred != 0;
+  }
+  if (policy == 2 /*Restricted*/) return best.preferred != 0;
+  return true;  // BestEffort
 }
 
 // Topology-manager Admit for the NodeNUMAResource provider alone (manager.go:58-100, policy_*.go) with the
@@ -698,7 +699,7 @@ __device__ __forceinline__ bool numa_admit(const NumaView& v, const NumaPod& p, 
   const int nn = v.nn;
   const uint32_t def = (1u << nn) - 1u;
   const int bind = numa_pref_bind(v, p.preferred);
-  HintList L0{0, 1, 1, 0, 0}, L1{0, 1, 1, 0, 0};
+  HintList L0{0, 0, 1, 1, 0}, L1{0, 0, 1, 1, 0};
   int nl = 1;
   const bool req_c = p.req_cpu > 0, req_m = p.req_mem > 0;
   const int64_t rqc = opt_cpu(v, p);
@@ -761,8 +762,8 @@ __device__ __forceinline__ bool numa_admit(const NumaView& v, const NumaPod& p, 
     }
     // filterProvidersHints (policy.go:94-125): resources in sorted-name order (cpu, memory); a present but
     // empty list becomes one non-preferred "don't care" hint
-    const HintList lc = hc ? HintList{hc, 0, 0, 0, min_c} : HintList{0, 1, 0, 0, 0};
-    const HintList lm = hm ? HintList{hm, 0, 0, 0, min_m} : HintList{0, 1, 0, 0, 0};
+    const HintList lc = hc ? HintList{hc, size_class(min_c), 0, 0, 0} : HintList{0, 0, 1, 0, 0};
+    const HintList lm = hm ? HintList{hm, size_class(min_m), 0, 0, 0} : HintList{0, 0, 1, 0, 0};
     if (req_c) {
       L0 = lc;
       if (req_m) {
@@ -773,16 +774,7 @@ __device__ __forceinline__ bool numa_admit(const NumaView& v, const NumaPod& p, 
       L0 = lm;
     }
   }
-  // one merge for every policy (lanes of one wave hold nodes of different policies: a single inlined merge
-  // keeps the divergent path to one copy)
-  const bool single = v.policy == 3 /*SingleNUMANode*/;
-  best = merge_hints(def, single ? single_numa_only(L0) : L0, single ? single_numa_only(L1) : L1, nl, score_of);
-  if (single) {
-    if (!best.nil && best.mask == def) best = NumaHint{0, 1, best.preferred, 0};
-    return best.preferred != 0;
-  }
-  if (v.policy == 2 /*Restricted*/) return best.preferred != 0;
-  return true;  // BestEffort
+  return policy_merge(v.policy, def, L0, L1, nl, score_of, best);
 }
 
 // allocateResourcesByHint (resource_manager.go:195-250): per NUMA node i (ascending within the hint) the cpu /

@@ -10,6 +10,14 @@
 // prologue by the thread owning the winner row.  A group of kRsvGroup pods is captured in one hipGraph, closed by
 // a one-wave kernel that reserves the group's last pod and advances the device cursor.
 //
+// (r3) The same pass is the engine's exact path for every plugin combination the round engines do not cover, in
+// particular the reference's shipped profile (config/manager/scheduler-config.yaml:66-117: LoadAwareScheduling +
+// NodeNUMAResource + DeviceShare + Reservation [+ ElasticQuota]): NodeNUMAResource Filter + Score run per node on the
+// restored NodeInfo (nodenumaresource/plugin.go:276-334, scoring.go:55-93) and its Reserve (plugin.go:375-415, the
+// exact cpuset) runs in the winner's owner thread before DeviceShare's, in the profile's Reserve order; a later
+// Reserve failure leaves the earlier plugins' state untouched (RunReservePluginsUnreserve).  Reserve pods hold no
+// cpuset here, so NodeNUMAResource's RestoreReservation (nodenumaresource/reservation.go) has nothing to restore.
+//
 // Reservations here hold cpu / memory (an allocatable of 0 = the key is absent).  DeviceShare restores device state
 // only for reservations whose reserve pod holds devices (deviceshare/reservation.go:132-150), so for these it keeps
 // no reservation state: its Filter / Score are the node-level ones, and its FilterReservation rejects every
@@ -21,6 +29,7 @@
 #include "../../include/koordgpu.h"
 #include "ds_dev.h"
 #include "kernels.h"
+#include "numa_dev.h"
 
 namespace kg {
 
@@ -56,6 +65,14 @@ struct RsvExt {
   const int64_t* __restrict__ qdev;    // [pods][kQuotaRes] device requests (quota dims 2..7)
   int32_t* __restrict__ out_minors;    // [pods]
   int nq;
+  // NodeNUMAResource (ns = nullptr: not in the profile)
+  const NumaStatic* __restrict__ ns;   // [cap] TopologyOptions
+  NumaMut* __restrict__ nm;            // [cap] NodeAllocation (Reserve updates it)
+  const NumaPod* __restrict__ npods;   // [pods] preFilterState
+  NumaParams NP;
+  uint32_t* __restrict__ aff;          // [cap] the affinity NUMA Filter stored for the pass's pod: mask | nil << 8
+  uint64_t* __restrict__ out_cpus;     // [pods][kCpuWords] the cpuset Reserve allocated
+  int64_t* __restrict__ out_nrec;      // [pods][kNumaRecWords] the pod's NUMA allocation record
 };
 
 struct RsvOut {
@@ -91,10 +108,19 @@ __device__ __forceinline__ int32_t rsv_score_slot(const RsvNode& rn, int s, cons
   return w ? (int32_t)(sc / w) : 0;
 }
 
+// Per-node outputs kg_pods_evaluate_reservation reports besides RsvOut (nullptr in the scheduling pass)
+struct RsvDbg {
+  uint32_t matched;       // the slots in nodeReservationState.matched
+  int32_t has_state;      // a nodeReservationState exists (BeforePreFilter restored the node)
+  int64_t req_cpu, req_mem, nz_cpu, nz_mem, num_pods;  // the restored NodeInfo
+  int64_t pod_req_cpu, pod_req_mem;                    // nodeReservationState.podRequested
+};
+
 __device__ __forceinline__ RsvOut rsv_eval_node(const DevTable& T, const RsvNode* __restrict__ RN,
                                                 const int32_t* __restrict__ rsv_n, int64_t i, const DevPod& p,
                                                 const RsvPod& rp, const EvalParams& P, const RsvParams& RP,
-                                                const RsvExt& X, const DsPod* dp) {
+                                                const RsvExt& X, const DsPod* dp, const NumaPod* np = nullptr,
+                                                RsvDbg* dbg = nullptr) {
   Row r = load_row(T, i);
   const int ns = rsv_n[i];
   RsvOut o{false, 0, 0, -1, 0x7fffffff, 0};
@@ -148,6 +174,13 @@ __device__ __forceinline__ RsvOut rsv_eval_node(const DevTable& T, const RsvNode
         }
     }
   }
+  if (dbg) {
+    dbg->matched = mm;
+    dbg->has_state = has_state ? 1 : 0;
+    dbg->req_cpu = r.req_cpu, dbg->req_mem = r.req_mem, dbg->nz_cpu = r.nz_cpu, dbg->nz_mem = r.nz_mem;
+    dbg->num_pods = r.num_pods;
+    dbg->pod_req_cpu = has_state ? pr_c : 0, dbg->pod_req_mem = has_state ? pr_m : 0;
+  }
   int64_t t = 0;
   if (!eval_node(r, p, P, t)) return o;  // NodeResourcesFit + LoadAware on the restored NodeInfo
   // satisfied(s): filterWithReservations([s]) (plugin.go:384-428) with fitsNode (:433-482), preemptible = 0
@@ -175,6 +208,14 @@ __device__ __forceinline__ RsvOut rsv_eval_node(const DevTable& T, const RsvNode
     if (!ds_eval(X.ds[i], *dp, X.DP, dsraw)) return o;
     // DeviceShare.FilterReservation rejects every reservation for a pod that requests devices
     if (X.DP.filter) sat = 0;
+  }
+  if (X.ns && np) {  // NodeNUMAResource Filter + Score on the restored NodeInfo; Reserve reuses the stored affinity
+    const NumaView nv = make_view(X.ns + i, X.nm + i, X.NP);
+    int64_t sc = 0;
+    NumaHint aff;
+    if (!numa_eval(nv, *np, X.NP, r.req_cpu, r.req_mem, r.alloc_cpu, r.alloc_mem, sc, aff)) return o;
+    if (X.NP.score) t += sc * X.NP.weight;
+    if (X.aff) X.aff[i] = aff.nil ? 0x100u : aff.mask;
   }
   o.feas = true;
   o.base = t;
@@ -285,6 +326,23 @@ __device__ __forceinline__ void rsv_quota_charge(const RsvExt& X, const DevPod& 
 __device__ __forceinline__ bool rsv_reserve(const DevTable& T, RsvNode* __restrict__ RN, int64_t w, uint64_t v,
                                             const DevPod& p, const RsvExt& X, int64_t j, int32_t& slot_out) {
   slot_out = -1;
+  // NodeNUMAResource Reserve first (the profile's Reserve order), computed on copies: nothing is committed unless
+  // every Reserve succeeds
+  NumaMut nmw;
+  CpuSet cpus = cs_zero();
+  NumaAlloc rec;
+  rec.res = 0;
+  if (X.ns) {
+    const NumaStatic nsw = X.ns[w];
+    nmw = X.nm[w];
+    const NumaView nv = make_view(&nsw, &nmw, X.NP);
+    const uint32_t a = X.aff[w];
+    const NumaHint aff{a & 0xFFu, (int)((a >> 8) & 1u), 0, 0};
+    if (!numa_reserve(nsw, nmw, nv, X.npods[j], aff, cpus, rec)) {
+      if (X.out_minors) X.out_minors[j] = 0;
+      return false;
+    }
+  }
   if (X.ds) {
     DsNode dn = X.ds[w];
     const int32_t minors = rsv_ds_reserve(dn, X.dpods[j], X.DP);
@@ -294,6 +352,18 @@ __device__ __forceinline__ bool rsv_reserve(const DevTable& T, RsvNode* __restri
     }
     if (minors) const_cast<DsNode*>(X.ds)[w] = dn;
     X.out_minors[j] = minors;
+  }
+  if (X.ns) {
+    X.nm[w] = nmw;
+#pragma unroll
+    for (int q = 0; q < kCpuWords; ++q) X.out_cpus[(size_t)j * kCpuWords + q] = cpus.w[q];
+    int64_t* r = X.out_nrec + (size_t)j * kNumaRecWords;
+    r[0] = rec.res;
+#pragma unroll
+    for (int k = 0; k < kNumaMax; ++k) {
+      r[1 + k] = ((rec.res >> k) & 1u) ? rec.cpu[k] : 0;
+      r[1 + kNumaMax + k] = ((rec.res >> k) & 1u) ? rec.mem[k] : 0;
+    }
   }
   Row r = load_row(T, w);
   const int64_t prod = (p.flags & P_PROD) ? 1 : 0;
@@ -384,7 +454,8 @@ __global__ __launch_bounds__(kRsvThreads) void rsv_eval(DevTable T, RsvNode* __r
   if (i < n) {
     const RsvPod rp = rpods[j];
     const DsPod* dp = X.ds ? &X.dpods[j] : nullptr;
-    const RsvOut o = rsv_eval_node(T, RN, rsv_n, i, p, rp, P, RP, X, dp);
+    const NumaPod* np = X.ns ? &X.npods[j] : nullptr;
+    const RsvOut o = rsv_eval_node(T, RN, rsv_n, i, p, rp, P, RP, X, dp, np);
     if (o.feas) {
       v = ((uint64_t)(uint32_t)o.base << 32) | ((uint64_t)(uint32_t)o.dsraw << 16) |
           ((uint64_t)(uint32_t)o.raw << 8) | (1ull << 7) | (uint64_t)(o.nom + 1);

@@ -293,6 +293,27 @@ class Engine:
         check(self.lib, self.lib.kg_debug_eval_paths(self.h, ptr(out)))
         return int(out[0])
 
+    def evaluate_reservation(self, pod: np.ndarray) -> dict:
+        """The exact pass's evaluation of one pod on every node (kg_pods_evaluate_reservation): per node pass,
+        nominated slot, raw Reservation score, restore state (has_state, matched slots, restored Requested /
+        NonZeroRequested / pod count, podRequested), the non-normalized weighted total and the raw DeviceShare score."""
+        pod = np.ascontiguousarray(np.asarray(pod, dtype=abi.POD_DTYPE).reshape(1))
+        n = self.num_nodes
+        out = np.zeros((max(n, 1), abi.RSV_EVAL_WORDS), dtype=np.int64)
+        check(self.lib, self.lib.kg_pods_evaluate_reservation(self.h, ptr(pod), ptr(out)))
+        out = out[:n]
+        names = ("pass", "nominated", "score", "has_state", "matched", "requested_cpu", "requested_mem", "nonzero_cpu",
+                 "nonzero_mem", "num_pods", "pod_requested_cpu", "pod_requested_mem", "base", "ds_raw", "order")
+        return {k: out[:, q] for q, k in enumerate(names)}
+
+    def debug_numa_merge(self, cases: np.ndarray) -> np.ndarray:
+        """The device topology-manager policy merge on int64[n, DBG_MERGE_WORDS] cases (kg_debug_numa_merge);
+        returns int64[n, 8]: admit, nil, mask, preferred, score."""
+        cases = np.ascontiguousarray(cases, dtype=np.int64).reshape(-1, abi.DBG_MERGE_WORDS)
+        out = np.zeros((len(cases), 8), dtype=np.int64)
+        check(self.lib, self.lib.kg_debug_numa_merge(self.h, ptr(cases), len(cases), ptr(out)))
+        return out
+
     def debug_least_requested(self, requested, capacity):
         requested = np.ascontiguousarray(requested, dtype=np.int64)
         capacity = np.ascontiguousarray(capacity, dtype=np.int64)

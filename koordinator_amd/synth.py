@@ -246,7 +246,13 @@ def make_gpu_cluster(n_nodes: int, seed: int = BASE_SEED + 6) -> tuple:
     node with 8 GPUs (gpu-core 100, gpu-memory-ratio 100, gpu-memory 80 GiB) of which 0–60 % (in steps of 5)
     is used per minor; 1 % of the GPUs unhealthy, 1 % of the nodes without a Device object."""
     cluster = make_cluster(n_nodes, seed=seed)
-    rng = np.random.default_rng(seed + 1000)
+    return cluster, make_node_devices(n_nodes, seed=seed + 1000)
+
+
+def make_node_devices(n_nodes: int, seed: int) -> np.ndarray:
+    """kg_node_device[n]: 8 GPUs per node (gpu-core 100, gpu-memory-ratio 100, gpu-memory 80 GiB), 0–60 % (steps of 5)
+    used per minor, 1 % of the GPUs unhealthy, 1 % of the nodes without a Device object."""
+    rng = np.random.default_rng(seed)
     n = n_nodes
     dev = np.zeros(n, dtype=abi.NODE_DEVICE_DTYPE)
     dev["has_device"] = rng.random(n) >= 0.01
@@ -261,13 +267,14 @@ def make_gpu_cluster(n_nodes: int, seed: int = BASE_SEED + 6) -> tuple:
     dev["used_memory"] = used * GPU_MEM // 100
     for f in ("present", "healthy", "total_core", "total_ratio", "total_memory", "used_core", "used_ratio", "used_memory"):
         dev[f][dev["has_device"] == 0] = 0  # no Device object: no device state at all
-    return cluster, dev
+    return dev
 
 
-def make_gpu_pods(n_pods: int, seed: int = BASE_SEED + 7) -> np.ndarray:
-    """Config C5 queue: make_pods' cpu/memory pods, 30 % of them also requesting GPU share — gpu-memory-ratio
-    ∈ {25, 50, 100, 200} with the same gpu-core (70 %), gpu-memory-ratio alone (20 %) or gpu-memory bytes (10 %)."""
-    p = make_pods(n_pods, seed=seed)
+def make_gpu_pods(n_pods: int, seed: int = BASE_SEED + 7, base: np.ndarray | None = None) -> np.ndarray:
+    """Config C5 queue: make_pods' cpu/memory pods (or `base`), 30 % of them also requesting GPU share —
+    gpu-memory-ratio ∈ {25, 50, 100, 200} with the same gpu-core (70 %), gpu-memory-ratio alone (20 %) or gpu-memory
+    bytes (10 %)."""
+    p = make_pods(n_pods, seed=seed) if base is None else base
     rng = np.random.default_rng(seed + 1000)
     gpu = rng.random(n_pods) < 0.3
     ratio = rng.choice(np.array([25, 50, 100, 200], dtype=np.int64), n_pods)
@@ -442,6 +449,39 @@ def make_c5_quotas(pods: np.ndarray, seed: int = BASE_SEED + 12, n_quotas: int =
 
 def load_c5_into(engine, cluster: Cluster, dev: np.ndarray, rsv: np.ndarray, quotas: np.ndarray | None = None):
     load_into(engine, cluster)
+    engine.upsert_devices(dev)
+    engine.upsert_reservations(rsv)
+    if quotas is not None:
+        engine.set_quotas(quotas)
+
+
+# ---- the reference's shipped profile (config/manager/scheduler-config.yaml:66-117): LoadAwareScheduling +
+# NodeNUMAResource + DeviceShare + Reservation (+ the upstream NodeResourcesFit) with ElasticQuota admission ------------
+def make_shipped_cluster(n_nodes: int, seed: int = BASE_SEED + 13) -> tuple:
+    """(Cluster, kg_node_numa[n], kg_node_device[n], kg_node_reservations[n]): make_numa_cluster's 2-socket 256-cpu
+    nodes (NUMA policies, bound cpuset pods, NodeMetrics), each with make_node_devices' 8 GPUs, and make_rsv_cluster's
+    cpu / memory reservations on 30 % of them (reserve pods in NodeInfo, no cpuset)."""
+    cluster, numa = make_numa_cluster(n_nodes, seed=seed)
+    dev = make_node_devices(n_nodes, seed=seed + 1000)
+    cluster, rsv = make_rsv_cluster(n_nodes, seed=seed + 1, cluster=cluster)
+    return cluster, numa, dev, rsv
+
+
+def make_shipped_pods(n_pods: int, seed: int = BASE_SEED + 14) -> np.ndarray:
+    """The shipped profile's queue: make_numa_pods' LSR / LSE cpuset and LS / BE pods, 30 % also requesting GPU share
+    (make_gpu_pods), 20 % owned by reservation owner groups (make_rsv_pods) and 80 % in one of N_QUOTAS quotas."""
+    p = make_numa_pods(n_pods, seed=seed)
+    p = make_gpu_pods(n_pods, seed=seed + 1, base=p)
+    p = make_rsv_pods(n_pods, seed=seed + 2, base=p)
+    rng = np.random.default_rng(seed + 3000)
+    p["quota_id"] = np.where(rng.random(n_pods) < 0.8, rng.integers(1, N_QUOTAS + 1, n_pods), 0)
+    return p
+
+
+def load_shipped_into(engine, cluster: Cluster, numa: np.ndarray, dev: np.ndarray, rsv: np.ndarray,
+                      quotas: np.ndarray | None = None):
+    load_into(engine, cluster)
+    engine.upsert_numa(numa)
     engine.upsert_devices(dev)
     engine.upsert_reservations(rsv)
     if quotas is not None:

@@ -742,6 +742,32 @@ static or_hint merge_filtered(uint32_t def, hint_list* lists, int nl) {
   return best;
 }
 
+/* filterSingleNumaHints (policy_single_numa_node.go:38-53): keep "don't care" and single-NUMA hints, preferred only */
+static void single_numa_filter(hint_list* lists, int nl) {
+  for (int i = 0; i < nl; i++) {
+    int k = 0;
+    for (int j = 0; j < lists[i].n; j++) {
+      const or_hint h = lists[i].h[j];
+      if ((h.nil && h.preferred) || (!h.nil && __builtin_popcount(h.mask) == 1 && h.preferred)) lists[i].h[k++] = h;
+    }
+    lists[i].n = k;
+  }
+}
+
+/* Policy.Merge + canAdmitPodResult over filtered provider lists (policy_best_effort.go:43-48,
+ * policy_restricted.go:41-46, policy_single_numa_node.go:62-77).  Returns admit. */
+static int policy_merge_lists(int policy, uint32_t def, hint_list* lists, int nl, or_hint* best) {
+  if (policy == KG_NUMA_POLICY_SINGLE_NUMA_NODE) {
+    single_numa_filter(lists, nl);
+    *best = merge_filtered(def, lists, nl);
+    if (!best->nil && best->mask == def) *best = (or_hint){1, 0, best->preferred, 0};
+    return best->preferred;
+  }
+  *best = merge_filtered(def, lists, nl);
+  if (policy == KG_NUMA_POLICY_RESTRICTED) return best->preferred;
+  return 1; /* best-effort */
+}
+
 /* Policy.Merge for the NodeNUMAResource provider alone (manager.go:82-100; policy_*.go).  Returns admit. */
 static int policy_merge(const or_numa_node* n, int hints_ok, hint_list* hc, int has_c, hint_list* hm, int has_m,
                         or_hint* best) {
@@ -772,23 +798,7 @@ static int policy_merge(const or_numa_node* n, int hints_ok, hint_list* hc, int 
       nl++;
     }
   }
-  if (n->numa_policy == KG_NUMA_POLICY_SINGLE_NUMA_NODE) {
-    /* filterSingleNumaHints: keep "don't care" and single-NUMA hints, preferred only */
-    for (int i = 0; i < nl; i++) {
-      int k = 0;
-      for (int j = 0; j < lists[i].n; j++) {
-        const or_hint h = lists[i].h[j];
-        if ((h.nil && h.preferred) || (!h.nil && __builtin_popcount(h.mask) == 1 && h.preferred)) lists[i].h[k++] = h;
-      }
-      lists[i].n = k;
-    }
-    *best = merge_filtered(def, lists, nl);
-    if (!best->nil && best->mask == def) *best = (or_hint){1, 0, best->preferred, 0};
-    return best->preferred;
-  }
-  *best = merge_filtered(def, lists, nl);
-  if (n->numa_policy == KG_NUMA_POLICY_RESTRICTED) return best->preferred;
-  return 1; /* best-effort */
+  return policy_merge_lists(n->numa_policy, def, lists, nl, best);
 }
 
 /* ---------------------------------------------------------------------------------------------------- */
@@ -1038,8 +1048,8 @@ int or_numa_eval_flat(const kg_config* cfg, const kg_node_numa* node, const kg_p
   or_numa_node_init(&n, node);
   or_numa_pod p;
   or_numa_pod_init(cfg, pod, &p);
-  or_hint h;
-  const int ok = or_numa_filter(cfg, &n, &p, &h, node_req_cpu, node_alloc_cpu);
+  or_hint h = {1, 0, 0, 0};  /* no Filter in the profile: Score reads no stored affinity (nil) */
+  const int ok = cfg->numa_filter ? or_numa_filter(cfg, &n, &p, &h, node_req_cpu, node_alloc_cpu) : 1;
   *affinity_mask = h.nil ? -1 : (int64_t)h.mask;
   *score = ok ? or_numa_score(cfg, &n, &p, &h, node_req_cpu, node_req_mem, node_alloc_cpu, node_alloc_mem) : 0;
   return ok;
@@ -1057,4 +1067,52 @@ int or_numa_reserve_flat(const kg_config* cfg, const kg_node_numa* node, const k
   const int rc = or_numa_reserve(cfg, &n, &p, &h, &cs, NULL);
   for (int w = 0; w < OR_CPUSET_WORDS; w++) cpuset[w] = cs.w[w];
   return rc;
+}
+
+/* Test hook: Policy.Merge on caller-given filtered provider lists (filterProvidersHints already applied: nl lists,
+ * counts[i] hints each, hints[4 * (16 * i + j)] = {nil, mask, preferred, score}).  out = {admit, nil, mask,
+ * preferred, score}.  Pins mergeFilteredHints + the policies with the reference's topologymanager test tables. */
+int or_debug_policy_merge(int policy, int num_numa, int nl, const int32_t* counts, const int64_t* hints, int64_t* out) {
+  if (nl < 0 || nl > 8) return -1;
+  hint_list lists[8];
+  for (int i = 0; i < nl; i++) {
+    if (counts[i] < 0 || counts[i] > 16) return -1;
+    lists[i].n = counts[i];
+    for (int j = 0; j < counts[i]; j++) {
+      const int64_t* h = hints + 4 * (16 * i + j);
+      lists[i].h[j] = (or_hint){(int)h[0], (uint32_t)h[1], (int)h[2], h[3]};
+    }
+  }
+  or_hint best;
+  const int admit = policy_merge_lists(policy, (1u << num_numa) - 1u, lists, nl, &best);
+  out[0] = admit;
+  out[1] = best.nil;
+  out[2] = best.mask;
+  out[3] = best.preferred;
+  out[4] = best.score;
+  return 0;
+}
+
+/* Test hook: filterSingleNumaHints on caller-given lists (same encoding); writes the filtered counts and hints. */
+int or_debug_single_numa_filter(int nl, const int32_t* counts, const int64_t* hints, int32_t* out_counts,
+                                int64_t* out_hints) {
+  if (nl < 0 || nl > 8) return -1;
+  hint_list lists[8];
+  for (int i = 0; i < nl; i++) {
+    if (counts[i] < 0 || counts[i] > 16) return -1;
+    lists[i].n = counts[i];
+    for (int j = 0; j < counts[i]; j++) {
+      const int64_t* h = hints + 4 * (16 * i + j);
+      lists[i].h[j] = (or_hint){(int)h[0], (uint32_t)h[1], (int)h[2], h[3]};
+    }
+  }
+  single_numa_filter(lists, nl);
+  for (int i = 0; i < nl; i++) {
+    out_counts[i] = lists[i].n;
+    for (int j = 0; j < lists[i].n; j++) {
+      int64_t* h = out_hints + 4 * (16 * i + j);
+      h[0] = lists[i].h[j].nil, h[1] = lists[i].h[j].mask, h[2] = lists[i].h[j].preferred, h[3] = lists[i].h[j].score;
+    }
+  }
+  return 0;
 }

@@ -663,15 +663,26 @@ int or_schedule_full(const kg_config* cfg, int64_t n_nodes, const kg_node* nodes
     or_cpuset cpus;
     memset(&cpus, 0, sizeof(cpus));
     int64_t nalloc[OR_NUMA_ALLOC_WORDS] = {0};
+    or_numa_node numa_save;
     if (best >= 0 && c.numa) {
+      numa_save = c.numa[best];
       if (or_numa_reserve(cfg, &c.numa[best], &c.numa_pod, &c.affinity[best], &cpus, nalloc) != 0) best = -1;
     }
-    if (out_numa) memcpy(&out_numa[p * OR_NUMA_ALLOC_WORDS], nalloc, sizeof(nalloc));
     int32_t minors = 0;
     if (best >= 0 && c.dev) {
       minors = or_ds_reserve(&c.dev[best], &c.ds_pod, (int)cfg->ds_scoring_strategy, cfg->ds_scoring_weights);
-      if (minors < 0) { minors = 0; best = -1; }
+      if (minors < 0) {
+        /* DeviceShare Reserve failed: RunReservePluginsUnreserve releases NodeNUMAResource's allocation too */
+        minors = 0;
+        if (c.numa) {
+          c.numa[best] = numa_save;
+          memset(&cpus, 0, sizeof(cpus));
+          memset(nalloc, 0, sizeof(nalloc));
+        }
+        best = -1;
+      }
     }
+    if (out_numa) memcpy(&out_numa[p * OR_NUMA_ALLOC_WORDS], nalloc, sizeof(nalloc));
     if (out_minors) out_minors[p] = minors;
     if (out_cpus)
       for (int w = 0; w < OR_CPUSET_WORDS; w++) out_cpus[p * OR_CPUSET_WORDS + w] = cpus.w[w];

@@ -95,7 +95,8 @@ def lib():
         L.or_ds_instance_flat.restype = i
         L.or_schedule_resv.argtypes = [vp, i64, vp, vp, vp, vp, i64, vp, i64, vp, vp, vp]
         L.or_schedule_resv.restype = i
-        L.or_schedule_resv_full.argtypes = [vp, i64, vp, vp, vp, vp, vp, vp, i64, i64, vp, i64, i, vp, vp, vp, vp]
+        L.or_schedule_resv_full.argtypes = [vp, i64, vp, vp, vp, vp, vp, vp, i64, i64, vp, i64, i, vp, vp, vp, vp,
+                                            vp, vp, vp]
         L.or_schedule_resv_full.restype = i
         L.or_quota_admit.argtypes = [vp, vp]
         L.or_quota_admit.restype = i
@@ -179,22 +180,30 @@ p = abi.ptr
 
 
 def schedule_resv(cfg, nodes, metrics, st, rsv, pods, now_ns: int, devices=None, quotas=None, n_threads: int = 1,
-                  with_minors: bool = False):
-    """Sequential FIFO scheduling with NodeResourcesFit + LoadAware + Reservation [+ DeviceShare + ElasticQuota]
-    (st, rsv, devices, quotas mutated; the node loop of each pod on n_threads threads).  Returns (node, score, slot)
-    — slot = the reservation each pod was assumed into (-1 = none) — and, with_minors, DeviceShare's minor masks."""
+                  with_minors: bool = False, numa_buf=None, with_numa: bool = False):
+    """Sequential FIFO scheduling through the per-pod exact loop: NodeResourcesFit + LoadAware + Reservation
+    [+ DeviceShare + NodeNUMAResource + ElasticQuota] (st, rsv, devices, numa_buf, quotas mutated; the node loop of each
+    pod on n_threads threads).  Returns (node, score, slot) — slot = the reservation each pod was assumed into (-1 =
+    none) — then, with_minors, DeviceShare's minor masks and, with_numa, the cpusets uint64[n, 4] and NUMA allocation
+    records int64[n, NUMA_ALLOC_WORDS] NodeNUMAResource Reserve made."""
     pods = np.ascontiguousarray(pods, dtype=abi.POD_DTYPE)
     n = max(len(pods), 1)
     out_node, out_score, out_slot, out_minors = (np.empty(n, dtype=np.int32), np.empty(n, dtype=np.int64),
                                                  np.empty(n, dtype=np.int32), np.zeros(n, dtype=np.int32))
+    cpus = np.zeros((n, abi.MAX_CPUS // 64), dtype=np.uint64)
+    nalloc = np.zeros((n, NUMA_ALLOC_WORDS), dtype=np.int64)
     nq = 0 if quotas is None else len(quotas)
     rc = lib().or_schedule_resv_full(p(cfg), len(nodes), p(nodes), p(metrics), p(st), p(rsv), p(devices), p(quotas),
                                      nq, len(pods), p(pods), now_ns, n_threads, p(out_node), p(out_score), p(out_slot),
-                                     p(out_minors))
+                                     p(out_minors), p(numa_buf), p(cpus), p(nalloc))
     if rc != 0:
         raise RuntimeError(f"oracle or_schedule_resv_full failed: {rc}")
     out = (out_node[:len(pods)], out_score[:len(pods)], out_slot[:len(pods)])
-    return out + (out_minors[:len(pods)],) if with_minors else out
+    if with_minors:
+        out = out + (out_minors[:len(pods)],)
+    if with_numa:
+        out = out + (cpus[:len(pods)], nalloc[:len(pods)])
+    return out
 
 
 def quota_admit(quota, pod) -> bool:
@@ -212,6 +221,17 @@ def rsv_case(pod, allowed_pods, alloc, num_pods, pod_requested, r_allocated, has
                            p(a(alloc)), num_pods, p(a(pod_requested)), p(a(r_allocated)), int(has_state),
                            p(np.ascontiguousarray(np.asarray(rsv, dtype=abi.NODE_RSV_DTYPE).reshape(1))), p(out))
     return int(out[0]), int(out[1]), int(out[2])
+
+
+def rsv_restore(rsv, st, pod) -> dict:
+    """BeforePreFilter's restore of one node (or_rsv_restore_flat)."""
+    out = np.zeros(11, dtype=np.int64)
+    lib().or_rsv_restore_flat(p(np.ascontiguousarray(np.asarray(rsv, dtype=abi.NODE_RSV_DTYPE).reshape(1))),
+                              p(np.ascontiguousarray(st[:1])),
+                              p(np.ascontiguousarray(np.asarray(pod, dtype=abi.POD_DTYPE).reshape(1))), p(out))
+    names = ("has_state", "matched", "requested_cpu", "requested_mem", "nonzero_cpu", "nonzero_mem", "num_pods",
+             "pod_requested_cpu", "pod_requested_mem", "r_allocated_cpu", "r_allocated_mem")
+    return {k: int(v) for k, v in zip(names, out)}
 
 
 def states(n: int) -> np.ndarray:
@@ -370,3 +390,43 @@ def schedule_cluster(cfg, cluster, pods, n_threads: int = 1):
         add_pods(cfg, st, cluster.existing_pods, cluster.existing_node)
     node, score = schedule(cfg, cluster.nodes, cluster.metrics, st, pods, cluster.now_ns, n_threads)
     return node, score, st
+
+
+MERGE_POLICY = {"best-effort": 1, "restricted": 2, "single-numa-node": 3}
+
+
+def _hint_arrays(lists):
+    """Flat (counts int32[nl], hints int64[nl, 16, 4]) of hint lists [[mask bits or None, preferred, score?], ...]."""
+    counts = np.zeros(max(len(lists), 1), dtype=np.int32)
+    hints = np.zeros((max(len(lists), 1), 16, 4), dtype=np.int64)
+    for i, l in enumerate(lists):
+        counts[i] = len(l)
+        for j, h in enumerate(l):
+            bits = h[0]
+            hints[i, j] = (1 if bits is None else 0, 0 if bits is None else sum(1 << b for b in bits), int(bool(h[1])),
+                           h[2] if len(h) > 2 else 0)
+    return counts, hints
+
+
+def policy_merge(policy: str, num_numa: int, lists):
+    """Policy.Merge + canAdmitPodResult on filtered provider lists (or_debug_policy_merge):
+    (admit, mask bits or None, preferred, score)."""
+    counts, hints = _hint_arrays(lists)
+    out = np.zeros(5, dtype=np.int64)
+    rc = lib().or_debug_policy_merge(MERGE_POLICY[policy], num_numa, len(lists), p(counts), p(hints), p(out))
+    if rc != 0:
+        raise RuntimeError("or_debug_policy_merge failed")
+    bits = None if out[1] else [b for b in range(8) if (int(out[2]) >> b) & 1]
+    return bool(out[0]), bits, bool(out[3]), int(out[4])
+
+
+def single_numa_filter(lists):
+    """filterSingleNumaHints (or_debug_single_numa_filter): the filtered lists."""
+    counts, hints = _hint_arrays(lists)
+    oc = np.zeros_like(counts)
+    oh = np.zeros_like(hints)
+    rc = lib().or_debug_single_numa_filter(len(lists), p(counts), p(hints), p(oc), p(oh))
+    if rc != 0:
+        raise RuntimeError("or_debug_single_numa_filter failed")
+    return [[[None if oh[i, j, 0] else [b for b in range(8) if (int(oh[i, j, 1]) >> b) & 1], bool(oh[i, j, 2])]
+             for j in range(oc[i])] for i in range(len(lists))]

@@ -4,6 +4,7 @@
  * (ResourceNames ⊆ {cpu, memory}: cpu-only and memory-only reservations).
  */
 #include "reservation.h"
+#include "numa.h"
 
 #include <math.h>
 #include <stdlib.h>
@@ -213,14 +214,19 @@ int or_schedule_resv(const kg_config* cfg, int64_t n_nodes, const kg_node* nodes
                      or_node_state* st, kg_node_reservations* rsv, int64_t n_pods, const kg_pod* pods, int64_t now,
                      int32_t* out_node, int64_t* out_score, int32_t* out_slot) {
   return or_schedule_resv_full(cfg, n_nodes, nodes, metrics, st, rsv, NULL, NULL, 0, n_pods, pods, now, 1, out_node,
-                               out_score, out_slot, NULL);
+                               out_score, out_slot, NULL, NULL, NULL, NULL);
 }
 
 int or_schedule_resv_full(const kg_config* cfg, int64_t n_nodes, const kg_node* nodes, const kg_node_metric* metrics,
                           or_node_state* st, kg_node_reservations* rsv, kg_node_device* dev, kg_quota* quotas,
                           int64_t n_quotas, int64_t n_pods, const kg_pod* pods, int64_t now, int n_threads,
-                          int32_t* out_node, int64_t* out_score, int32_t* out_slot, int32_t* out_minors) {
+                          int32_t* out_node, int64_t* out_score, int32_t* out_slot, int32_t* out_minors,
+                          void* numa_states, uint64_t* out_cpus, int64_t* out_numa) {
   const size_t nn = (size_t)(n_nodes > 0 ? n_nodes : 1);
+  or_numa_node* numa = (or_numa_node*)numa_states;
+  const int numa_on = numa && (cfg->numa_filter || cfg->numa_score);
+  or_hint* aff = numa_on ? (or_hint*)calloc(nn, sizeof(or_hint)) : NULL;
+  if (numa_on && !aff) return KG_E_NOMEM;
   int8_t* feas = (int8_t*)malloc(nn);
   int64_t* base = (int64_t*)malloc(nn * sizeof(int64_t));
   int64_t* raw = (int64_t*)malloc(nn * sizeof(int64_t));
@@ -228,7 +234,7 @@ int or_schedule_resv_full(const kg_config* cfg, int64_t n_nodes, const kg_node* 
   int64_t* order = (int64_t*)malloc(nn * sizeof(int64_t));
   int32_t* nom = (int32_t*)malloc(nn * sizeof(int32_t));
   if (!feas || !base || !raw || !dsraw || !order || !nom) {
-    free(feas); free(base); free(raw); free(dsraw); free(order); free(nom);
+    free(feas); free(base); free(raw); free(dsraw); free(order); free(nom); free(aff);
     return KG_E_NOMEM;
   }
   const int rsv_on = cfg->reservation_filter || cfg->reservation_score;
@@ -243,6 +249,8 @@ int or_schedule_resv_full(const kg_config* cfg, int64_t n_nodes, const kg_node* 
     const kg_pod* pod = &pods[p];
     if (out_slot) out_slot[p] = -1;
     if (out_minors) out_minors[p] = 0;
+    if (out_cpus) memset(&out_cpus[p * OR_CPUSET_WORDS], 0, sizeof(uint64_t) * OR_CPUSET_WORDS);
+    if (out_numa) memset(&out_numa[p * OR_NUMA_ALLOC_WORDS], 0, sizeof(int64_t) * OR_NUMA_ALLOC_WORDS);
     /* ElasticQuota PreFilter: a rejected pod is Unschedulable without a node search */
     kg_quota* quota = NULL;
     if (pod->quota_id > 0) {
@@ -265,6 +273,8 @@ int or_schedule_resv_full(const kg_config* cfg, int64_t n_nodes, const kg_node* 
      * reservation DeviceShare restored device state for; the reservations here hold none, so it is rejected and no
      * reservation is nominated for such a pod (NominateReservation skips failing reservations, nominator.go:99-105) */
     const int ds_blocks_nomination = ds_on && cfg->ds_filter && !dsp.skip;
+    or_numa_pod npod;
+    if (numa_on) or_numa_pod_init(cfg, pod, &npod);
     int err = 0;
 #pragma omp parallel for schedule(dynamic, chunk) num_threads(n_threads) reduction(min : err)
     for (int64_t i = 0; i < n_nodes; i++) {
@@ -288,6 +298,14 @@ int or_schedule_resv_full(const kg_config* cfg, int64_t n_nodes, const kg_node* 
       }
       if (cfg->reservation_filter && !or_rsv_filter(pod, nd->allowed_pods, alloc, &ns, &rsv[i])) continue;
       if (ds_on && cfg->ds_filter && !or_ds_filter(&dev[i], &dsp)) continue;
+      /* NodeNUMAResource Filter (nodenumaresource/plugin.go:276-334) on the restored NodeInfo; the reserve pods hold
+       * no cpuset, so its RestoreReservation (nodenumaresource/reservation.go) restores nothing */
+      if (numa_on) {
+        aff[i] = (or_hint){1, 0, 0, 0};
+        if (cfg->numa_filter &&
+            !or_numa_filter(cfg, &numa[i], &npod, &aff[i], rs.requested[KG_RES_CPU], nd->allocatable[KG_RES_CPU]))
+          continue;
+      }
       feas[i] = 1;
       int64_t t = 0;
       if (cfg->fit_score) t += cfg->weight_fit * or_fit_score(cfg, nd, &rs, pod);
@@ -296,6 +314,10 @@ int or_schedule_resv_full(const kg_config* cfg, int64_t n_nodes, const kg_node* 
         if (sc < 0) { err = (int)sc; continue; }
         t += cfg->weight_loadaware * sc;
       }
+      if (numa_on && cfg->numa_score) /* scoring.go:55-93 on the restored NodeInfo with the stored affinity */
+        t += cfg->weight_numa * or_numa_score(cfg, &numa[i], &npod, &aff[i], rs.requested[KG_RES_CPU],
+                                              rs.requested[KG_RES_MEMORY], nd->allocatable[KG_RES_CPU],
+                                              nd->allocatable[KG_RES_MEMORY]);
       base[i] = t;
       nom[i] = (rsv_on && !ds_blocks_nomination) ? or_rsv_nominate(pod, nd->allowed_pods, alloc, &ns, &rsv[i]) : -1;
       raw[i] = nom[i] >= 0 ? or_rsv_score_slot(pod, &rsv[i], nom[i]) : 0;
@@ -325,12 +347,31 @@ int or_schedule_resv_full(const kg_config* cfg, int64_t n_nodes, const kg_node* 
       if (ds_on && cfg->ds_score && mds > 0) t += cfg->weight_deviceshare * (100 * dsraw[i] / mds);
       if (t > win_total) { win_total = t; win = i; }
     }
-    /* Reserve: DeviceShare allocates the minors first; a failure un-assumes the pod (Unreserve) */
+    /* Reserve in the profile's order (scheduler-config.yaml:92-98): NodeNUMAResource (the exact cpuset), then
+     * DeviceShare (the minors); any failure un-assumes the pod and RunReservePluginsUnreserve releases what the earlier
+     * plugins took (nodenumaresource/plugin.go:417-425), so nothing stays placed */
+    or_numa_node numa_save;
+    or_cpuset cpus;
+    memset(&cpus, 0, sizeof(cpus));
+    int64_t nalloc[OR_NUMA_ALLOC_WORDS] = {0};
+    if (win >= 0 && numa_on) {
+      numa_save = numa[win];
+      if (or_numa_reserve(cfg, &numa[win], &npod, &aff[win], &cpus, nalloc) != 0) {
+        numa[win] = numa_save;
+        win = -1;
+      }
+    }
     int32_t minors = 0;
     if (win >= 0 && ds_on && !dsp.skip) {
       minors = or_ds_reserve(&dev[win], &dsp, (int)cfg->ds_scoring_strategy, cfg->ds_scoring_weights);
-      if (minors < 0) { minors = 0; win = -1; }
+      if (minors < 0) {
+        minors = 0;
+        if (numa_on) numa[win] = numa_save;
+        win = -1;
+      }
     }
+    if (win >= 0 && out_cpus) memcpy(&out_cpus[p * OR_CPUSET_WORDS], cpus.w, sizeof(uint64_t) * OR_CPUSET_WORDS);
+    if (win >= 0 && out_numa) memcpy(&out_numa[p * OR_NUMA_ALLOC_WORDS], nalloc, sizeof(nalloc));
     out_node[p] = (int32_t)win;
     out_score[p] = win >= 0 ? win_total : 0;
     if (out_minors) out_minors[p] = minors;
@@ -349,6 +390,23 @@ int or_schedule_resv_full(const kg_config* cfg, int64_t n_nodes, const kg_node* 
       if (quota) or_quota_charge(quota, pod);
     }
   }
-  free(feas); free(base); free(raw); free(dsraw); free(order); free(nom);
+  free(feas); free(base); free(raw); free(dsraw); free(order); free(nom); free(aff);
   return rc;
+}
+
+/* Test hook: BeforePreFilter's restore of one node (or_rsv_restore) as flat values: [0] has_state, [1] matched slot
+ * mask, [2..3] restored Requested cpu / memory, [4..5] NonZeroRequested, [6] pod count, [7..8] podRequested,
+ * [9..10] Σ matched Allocated.  Pins transformer.go's restore with transformer_test.go's tables. */
+void or_rsv_restore_flat(const kg_node_reservations* r, const or_node_state* st, const kg_pod* pod, int64_t* out) {
+  or_rsv_node ns;
+  or_rsv_restore(r, st, pod, &ns);
+  int64_t m = 0;
+  for (int k = 0; k < ns.n_matched; k++) m |= 1LL << ns.matched[k];
+  out[0] = ns.has_state;
+  out[1] = m;
+  out[2] = ns.requested[0], out[3] = ns.requested[1];
+  out[4] = ns.nonzero[0], out[5] = ns.nonzero[1];
+  out[6] = ns.num_pods;
+  out[7] = ns.pod_requested[0], out[8] = ns.pod_requested[1];
+  out[9] = ns.r_allocated[0], out[10] = ns.r_allocated[1];
 }

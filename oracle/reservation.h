@@ -66,13 +66,16 @@ int or_schedule_resv(const kg_config* cfg, int64_t n_nodes, const kg_node* nodes
 int or_schedule_resv_full(const kg_config* cfg, int64_t n_nodes, const kg_node* nodes, const kg_node_metric* metrics,
                           or_node_state* st, kg_node_reservations* rsv, kg_node_device* dev, kg_quota* quotas,
                           int64_t n_quotas, int64_t n_pods, const kg_pod* pods, int64_t now, int n_threads,
-                          int32_t* out_node, int64_t* out_score, int32_t* out_slot, int32_t* out_minors);
+                          int32_t* out_node, int64_t* out_score, int32_t* out_slot, int32_t* out_minors,
+                          void* numa_states, uint64_t* out_cpus, int64_t* out_numa);
 
 /* Golden-case entry (flat): explicit nodeReservationState (pod_requested, r_allocated, restored pod count) as the
  * reference tests build it.  out[0] = filter pass, out[1] = nominated slot, out[2] = Score (before normalize). */
 void or_rsv_case_flat(const kg_pod* pod, int64_t allowed_pods, const int64_t alloc[2], int64_t num_pods,
                       const int64_t pod_requested[2], const int64_t r_allocated[2], int has_state,
                       const kg_node_reservations* r, int64_t* out);
+
+void or_rsv_restore_flat(const kg_node_reservations* r, const or_node_state* st, const kg_pod* pod, int64_t* out);
 
 #ifdef __cplusplus
 }

@@ -52,9 +52,51 @@ CASES = [
          slots=[dict(slot(6, 0), policy=2)], has_state=1, pod_requested=[30000, 24 * GI], **NODE32, want_pass=0),
 ]
 
+# nominator_test.go TestNominateReservation (:40-283): the nominated reservation of one node whose state matches every
+# listed reservation; node Status empty, pod 2C4G (`reservations` order = slot order).  "reserve pod" (:169) is out of
+# scope: reserve pods themselves are scheduled on the Go path.
+CASES += [
+    dict(ref="nominator_test.go:121 node without reservations", pod=[2000, 4 * GI], slots=[], has_state=0, **EMPTY_NODE,
+         want_nominated=-1),
+    dict(ref="nominator_test.go:126 preferred reservation", pod=[2000, 4 * GI],
+         slots=[dict(slot(2, 4), order=100), slot(2, 4)], has_state=1, **EMPTY_NODE, want_nominated=0),
+    dict(ref="nominator_test.go:224 allocated reservation", pod=[2000, 4 * GI],
+         slots=[R4C8G, slot(2, 4, allocated=(2000, 4 * GI))], has_state=1, **EMPTY_NODE, want_nominated=0),
+    dict(ref="nominator_test.go:253 matched reservations", pod=[2000, 4 * GI], slots=[R4C8G, R2C4G], has_state=1,
+         **EMPTY_NODE, want_nominated=1),
+]
+
+# BeforePreFilter's restore (transformer.go:49-346): one node, its bound pods (cpu cores, memory GiB; "reserve" = a
+# reservation's reserve pod) and reservation slots, the pod's owner-group mask / required-affinity flag, and the
+# restored node (transformer_test.go assertions).  Owner groups: the caller decodes ReservationInfo.Match — and, when
+# the pod has a reservation affinity, the affinity selector over the reservation's labels (matchReservation,
+# transformer.go:348-372) — into the pod's mask.  Test_matchReservation (:348) exercises only that caller-side label
+# matching and is not an engine case.
+RESTORE = [
+    dict(ref="transformer_test.go:41 TestRestoreReservation", node=[32, 64],
+         pods=[[4, 8, 0], [8, 16, 0], [12, 24, 1], [8, 16, 1], [4, 8, 0]],
+         slots=[dict(slot(12, 24, allocated=(4000, 8 * GI)), owner=1, assigned=1, allocate_once=0),
+                dict(slot(8, 16), owner=0, allocate_once=1)],
+         mask=1, affinity=0,
+         want=dict(has_state=1, matched=0b10, requested_cpu=24000, requested_mem=48 * GI, nonzero_cpu=24000,
+                   nonzero_mem=48 * GI, num_pods=4, pod_requested_cpu=32000, pod_requested_mem=64 * GI)),
+    dict(ref="transformer_test.go:510 pod has no reservation affinity", node=[32, 64], pods=[[8, 16, 1]],
+         slots=[dict(slot(8, 16), owner=0, allocate_once=1)], mask=1, affinity=0, want=dict(has_state=1)),
+    dict(ref="transformer_test.go:514 pod has reservation affinity and matched", node=[32, 64], pods=[[8, 16, 1]],
+         slots=[dict(slot(8, 16), owner=0, allocate_once=1)], mask=1, affinity=1, want=dict(has_state=1)),
+    dict(ref="transformer_test.go:533 pod has reservation affinity but failed to match", node=[32, 64],
+         pods=[[8, 16, 1]], slots=[dict(slot(8, 16), owner=0, allocate_once=1)], mask=0, affinity=1,
+         want=dict(has_state=0)),
+]
+
 if __name__ == "__main__":
     out = os.path.join(os.path.dirname(os.path.abspath(__file__)), "reservation.json")
     with open(out, "w") as f:
-        json.dump({"source": "hhyasdf/koordinator pkg/scheduler/plugins/reservation tests", "cases": CASES}, f,
-                  indent=1)
+        json.dump({"source": "hhyasdf/koordinator pkg/scheduler/plugins/reservation tests", "cases": CASES,
+                   "restore": RESTORE,
+                   "skipped": [{"ref": "nominator_test.go:110 reserve pod",
+                                "reason": "scheduling a reserve pod stays on the Go path"},
+                               {"ref": "transformer_test.go:348 Test_matchReservation",
+                                "reason": "caller-side label-selector matching (decoded into reservation_owner_mask)"}]},
+                  f, indent=1)
     print(f"wrote {len(CASES)} cases to {out}")

@@ -29,11 +29,6 @@ def _engine_one(cfg, dev):
 def test_golden_score_device(c):
     cfg = TG.case_config(c)
     dev, pod = TG.node_device(c["node"]), TG.case_pod(c)
-    if c["strategy"] == "MostAllocated":  # not monotone: the engine refuses the profile instead of guessing
-        with pytest.raises(KoordGPUError) as ei:
-            Engine(cfg, 1)
-        assert ei.value.code == abi.E_UNSUPPORTED
-        return
     with _engine_one(cfg, dev) as e:
         ok, sc = e.evaluate_device(pod)
     assert bool(ok[0]) == c["want_filter"], c["source"]
@@ -41,7 +36,15 @@ def test_golden_score_device(c):
         assert int(sc[0]) == c["want_score"], c["source"]
 
 
-@pytest.mark.parametrize("c", [c for c in TG._cases(("reserve",)) if c["strategy"] != "MostAllocated"], ids=TG._id)
+@pytest.mark.parametrize("c", TG._cases(("filter",)), ids=TG._id)
+def test_golden_filter_device(c):
+    dev, pod = TG.node_device(c["node"]), TG.case_pod(c)
+    with _engine_one(TG.case_config(c), dev) as e:
+        ok, _ = e.evaluate_device(pod)
+    assert bool(ok[0]) == c["want_filter"], c["source"]
+
+
+@pytest.mark.parametrize("c", TG._cases(("reserve",)), ids=TG._id)
 def test_golden_reserve_device(c):
     cfg = TG.case_config(c)
     if not c.get("strategy"):
@@ -132,6 +135,17 @@ def test_schedule_parity_weights_and_filter_only():
                  F.Profile(filter=(F.NODE_RESOURCES_FIT, F.LOAD_AWARE, F.DEVICE_SHARE),
                            score={F.NODE_RESOURCES_FIT: 2, F.LOAD_AWARE: 1, F.DEVICE_SHARE: 7})):
         _check(F.build_config(profile=prof), cluster, dev, pods)
+
+
+@pytest.mark.parametrize("batch,ppw,seed", [(32, 8, 1), (16, 4, 2), (1, 1, 3)])
+def test_schedule_parity_most_allocated(batch, ppw, seed):
+    """MostAllocated (scoring.go:281-304): an assume raises the node's DeviceShare score, so a modified row can lift
+    the normalization max: the resolver re-scores modified rows for every pod and ends the round when it rises."""
+    cluster, dev = synth.make_gpu_cluster(400, seed=300 + seed)
+    pods = synth.make_gpu_pods(2000, seed=400 + seed)
+    args = F.DeviceShareArgs(scoring_strategy="MostAllocated")
+    prof = F.Profile(filter=PROFILE.filter, score={F.NODE_RESOURCES_FIT: 1, F.LOAD_AWARE: 1, F.DEVICE_SHARE: 5})
+    _check(F.build_config(profile=prof, deviceshare=args, batch_pods=batch, pods_per_wave=ppw), cluster, dev, pods)
 
 
 def test_scoring_weights_over_core_and_memory():

@@ -50,6 +50,12 @@ def test_golden_score(c):
         assert oracle.ds_score(cfg[0], dev, pod) == c["want_score"], c["source"]
 
 
+@pytest.mark.parametrize("c", _cases(("filter",)), ids=_id)
+def test_golden_filter(c):
+    dev, pod = node_device(c["node"]), case_pod(c)
+    assert oracle.ds_filter(dev, pod) == c["want_filter"], c["source"]
+
+
 @pytest.mark.parametrize("c", _cases(("reserve",)), ids=_id)
 def test_golden_reserve(c):
     cfg = case_config(c)

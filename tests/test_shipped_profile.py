@@ -1,0 +1,218 @@
+"""The reference's shipped koord-scheduler profile as ONE accelerated profile (config/manager/scheduler-config.yaml:66-117):
+NodeResourcesFit (upstream default) + LoadAwareScheduling + NodeNUMAResource + DeviceShare + Reservation at Filter and
+Score (weights 1 / 1 / 1 / 1 / 5000), with ElasticQuota admission — SURVEY §8a A0–A24 together.
+
+The engine runs it through its per-pod exact pass (rsv_dev.h): BeforePreFilter restore, every Filter on the restored
+NodeInfo, NodeNUMAResource's topology-manager admit and Score, DeviceShare and Reservation raw scores normalized over the
+feasible nodes, the lowest-index argmax, then Reserve in the profile's order (NodeNUMAResource's exact cpuset, then
+DeviceShare's minors, then the reservation / NodeInfo assume and the quota charge; a failing Reserve un-assumes the pod and
+releases what the earlier plugins took).  The oracle runs the same composition (oracle/reservation.c
+or_schedule_resv_full with NUMA).  Out of scope, refused or kept on the Go path: reserve pods holding cpusets or GPUs
+(NodeNUMAResource / DeviceShare RestoreReservation), several ranks.
+
+Bar: bit-exact — placement, weighted total, reservation slot, GPU minor mask, cpuset, NUMA allocation record, and the
+final NodeInfo / NodeAllocation / deviceUsed / reservation / quota state."""
+import numpy as np
+import pytest
+
+from koordinator_amd import Engine, abi, framework as F, synth
+from oracle import oracle
+
+PROFILE = F.Profile(filter=(F.NODE_RESOURCES_FIT, F.LOAD_AWARE, F.NODE_NUMA_RESOURCE, F.DEVICE_SHARE, F.RESERVATION),
+                    score={F.NODE_RESOURCES_FIT: 1, F.LOAD_AWARE: 1, F.NODE_NUMA_RESOURCE: 1, F.DEVICE_SHARE: 1,
+                           F.RESERVATION: 5000})
+# the shipped LoadAwareSchedulingArgs (scheduler-config.yaml:29-46)
+SHIPPED_LA = F.LoadAwareSchedulingArgs(filter_expired_node_metrics=False, node_metric_expiration_seconds=300)
+
+
+def config(**kw):
+    return F.build_config(profile=kw.pop("profile", PROFILE), la=SHIPPED_LA, **kw)
+
+
+def workload(n_nodes, n_pods, seed, share=1.0):
+    cluster, numa, dev, rsv = synth.make_shipped_cluster(n_nodes, seed=seed)
+    pods = synth.make_shipped_pods(n_pods, seed=seed + 50)
+    quotas = synth.make_c5_quotas(pods, seed=seed + 60, share=share)
+    return cluster, numa, dev, rsv, pods, quotas
+
+
+def oracle_run(cfg, cluster, numa, dev, rsv, pods, quotas, n_threads=8):
+    st = oracle.states(cluster.n)
+    oracle.add_pods(cfg, st, cluster.existing_pods, cluster.existing_node)
+    buf = oracle.numa_states(numa)
+    r, d, q = rsv.copy(), dev.copy(), None if quotas is None else quotas.copy()
+    node, score, slot, minors, cpus, nalloc = oracle.schedule_resv(cfg, cluster.nodes, cluster.metrics, st, r, pods,
+                                                                   cluster.now_ns, devices=d, quotas=q,
+                                                                   n_threads=n_threads, with_minors=True,
+                                                                   numa_buf=buf, with_numa=True)
+    return dict(node=node, score=score, slot=slot, minors=minors, cpus=cpus, nalloc=nalloc, st=st, numa=buf, rsv=r,
+                dev=d, quotas=q)
+
+
+def test_oracle_composition():
+    cluster, numa, dev, rsv, pods, quotas = workload(400, 1500, 11)
+    w = oracle_run(config(), cluster, numa, dev, rsv, pods, quotas)
+    node, slot, minors, cpus = w["node"], w["slot"], w["minors"], w["cpus"]
+    placed = node >= 0
+    device_pod = pods["device_requests"].any(axis=1)
+    assert placed.mean() > 0.5
+    assert (slot[device_pod] == -1).all()  # DeviceShare FilterReservation: no device pod nominates
+    assert ((minors != 0) == (device_pod & placed)).all()
+    assert (cpus.any(axis=1) & device_pod).any() and (slot >= 0).sum() > 10  # cpuset + GPU pods; reservation pods
+    assert not cpus[~placed].any()
+
+
+def test_oracle_loops_agree_without_reservations():
+    """With no reservation slots and Reservation out of the profile, the exact loop equals the round loop's
+    composition of NodeNUMAResource + DeviceShare + ElasticQuota (or_schedule_full)."""
+    cluster, numa, dev, rsv, pods, quotas = workload(300, 800, 12)
+    prof = F.Profile(filter=PROFILE.filter[:-1], score={k: v for k, v in PROFILE.score.items() if k != F.RESERVATION})
+    cfg = config(profile=prof)
+    rsv[:] = np.zeros(1, dtype=abi.NODE_RSV_DTYPE)
+    a = oracle_run(cfg, cluster, numa, dev, rsv, pods, quotas)
+    st = oracle.states(cluster.n)
+    oracle.add_pods(cfg, st, cluster.existing_pods, cluster.existing_node)
+    buf, d, q = oracle.numa_states(numa), dev.copy(), quotas.copy()
+    node, score, cpus, minors, nalloc = oracle.schedule_full(cfg, cluster.nodes, cluster.metrics, st, pods,
+                                                             cluster.now_ns, 8, numa_buf=buf, devices=d, quotas=q,
+                                                             with_numa_alloc=True)
+    assert np.array_equal(node, a["node"]) and np.array_equal(score, a["score"])
+    assert np.array_equal(cpus, a["cpus"]) and np.array_equal(minors, a["minors"])
+    assert np.array_equal(nalloc, a["nalloc"]) and np.array_equal(buf, a["numa"])
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# device parity
+# ---------------------------------------------------------------------------------------------------------------
+def engine_run(cfg, cluster, numa, dev, rsv, pods, quotas, chunks=1):
+    with Engine(cfg, cluster.n) as e:
+        synth.load_shipped_into(e, cluster, numa, dev, rsv, quotas)
+        e.stage(pods)
+        bounds = np.linspace(0, len(pods), chunks + 1).astype(int)
+        for a, b in zip(bounds[:-1], bounds[1:]):
+            e.schedule_staged(int(a), int(b - a))
+        out = dict(zip(("node", "score"), e.fetch(0, len(pods))))
+        out["slot"] = e.fetch_reservations(0, len(pods))
+        out["minors"] = e.fetch_devices(0, len(pods))
+        out["cpus"] = e.fetch_cpusets(0, len(pods))
+        out["state"] = e.read_state()
+        out["numa"] = e.read_numa()
+        out["used"] = e.read_devices()
+        out["rsv"] = e.read_reservations()
+        out["quotas"] = e.read_quotas(len(quotas)) if quotas is not None else None
+    return out
+
+
+def check(cfg, cluster, numa, dev, rsv, pods, quotas, chunks=1):
+    w = oracle_run(cfg, cluster, numa, dev, rsv, pods, quotas)
+    g = engine_run(cfg, cluster, numa, dev, rsv, pods, quotas, chunks)
+    bad = np.flatnonzero((g["node"] != w["node"]) | (g["score"] != w["score"]) | (g["slot"] != w["slot"]))
+    assert bad.size == 0, (f"first mismatch at pod {bad[0]}: gpu ({g['node'][bad[0]]}, {g['score'][bad[0]]}, "
+                           f"{g['slot'][bad[0]]}) oracle ({w['node'][bad[0]]}, {w['score'][bad[0]]}, {w['slot'][bad[0]]})")
+    assert np.array_equal(g["minors"], w["minors"])
+    assert np.array_equal(g["cpus"], w["cpus"])
+    ga, gc, gm = g["numa"]
+    wa, wc, wm = oracle.numa_state_read(w["numa"], cluster.n)
+    assert np.array_equal(ga, wa) and np.array_equal(gc, wc) and np.array_equal(gm, wm)
+    uc, um, ur = g["used"]
+    assert np.array_equal(uc, w["dev"]["used_core"]) and np.array_equal(ur, w["dev"]["used_ratio"])
+    assert np.array_equal(um, w["dev"]["used_memory"])
+    ac, am, asg = g["rsv"]
+    on = np.arange(abi.MAX_RSV_SLOTS)[None, :] < w["rsv"]["n"][:, None]
+    assert np.array_equal(ac, np.where(on, w["rsv"]["allocated_cpu"], 0))
+    assert np.array_equal(am, np.where(on, w["rsv"]["allocated_mem"], 0))
+    assert np.array_equal(asg, np.where(on, w["rsv"]["assigned"], 0))
+    st = w["st"]
+    assert np.array_equal(g["state"]["requested_cpu"], st["requested"][:, abi.RES_CPU])
+    assert np.array_equal(g["state"]["requested_mem"], st["requested"][:, abi.RES_MEMORY])
+    assert np.array_equal(g["state"]["num_pods"], st["num_pods"])
+    if quotas is not None:
+        assert np.array_equal(g["quotas"]["used"], w["quotas"]["used"])
+        assert np.array_equal(g["quotas"]["non_preemptible_used"], w["quotas"]["non_preemptible_used"])
+    return g, w
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n_nodes,n_pods,seed,chunks", [(1500, 1500, 1, 2), (60, 900, 2, 3), (777, 1200, 3, 1)])
+def test_shipped_profile_parity(n_nodes, n_pods, seed, chunks):
+    cluster, numa, dev, rsv, pods, quotas = workload(n_nodes, n_pods, 100 + seed)
+    g, _ = check(config(), cluster, numa, dev, rsv, pods, quotas, chunks)
+    placed = g["node"] >= 0
+    assert placed.any() and (g["slot"] >= 0).any() and g["cpus"].any() and (g["minors"] != 0).any()
+
+
+@pytest.mark.gpu
+def test_shipped_profile_parity_10k_nodes():
+    cluster, numa, dev, rsv, pods, quotas = workload(10_000, 600, 131)
+    check(config(), cluster, numa, dev, rsv, pods, quotas, 1)
+
+
+@pytest.mark.gpu
+def test_numa_deviceshare_without_reservation():
+    """NodeNUMAResource + DeviceShare (no Reservation) also runs on the exact pass; MostAllocated on both plugins."""
+    cluster, numa, dev, rsv, pods, quotas = workload(800, 1000, 141)
+    rsv[:] = np.zeros(1, dtype=abi.NODE_RSV_DTYPE)
+    prof = F.Profile(filter=PROFILE.filter[:-1], score={k: v for k, v in PROFILE.score.items() if k != F.RESERVATION})
+    numa_args = F.NodeNUMAResourceArgs(scoring_strategy="MostAllocated")
+    ds_args = F.DeviceShareArgs(scoring_strategy="MostAllocated")
+    check(config(profile=prof, numa=numa_args, deviceshare=ds_args), cluster, numa, dev, rsv, pods, None)
+
+
+@pytest.mark.gpu
+def test_shipped_unreserve_matches_oracle():
+    """The framework's Unreserve of half the placed pods releases every plugin's state (cpuset, NUMA resources, minors,
+    reservation assume, quota charge, NodeInfo) exactly as the oracle's or_unreserve; the next batch then places alike."""
+    cfg = config()
+    cluster, numa, dev, rsv, pods, quotas = workload(500, 900, 151)
+    first, second = pods[:600], pods[600:]
+    w = oracle_run(cfg, cluster, numa, dev, rsv, first, quotas)
+    mask = (np.arange(len(first)) % 2 == 0) & (w["node"] >= 0)
+    for j in np.flatnonzero(mask):
+        oracle.unreserve(cfg, w["st"], first[j], int(w["node"][j]), numa_buf=w["numa"], devices=w["dev"], rsv=w["rsv"],
+                         quotas=w["quotas"], cpus=w["cpus"][j], numa_alloc=w["nalloc"][j], minors=int(w["minors"][j]),
+                         slot=int(w["slot"][j]))
+    node2, score2, slot2, minors2, cpus2, _ = oracle.schedule_resv(cfg, cluster.nodes, cluster.metrics, w["st"], w["rsv"],
+                                                                  second, cluster.now_ns, devices=w["dev"],
+                                                                  quotas=w["quotas"], n_threads=8, with_minors=True,
+                                                                  numa_buf=w["numa"], with_numa=True)
+    with Engine(cfg, cluster.n) as e:
+        synth.load_shipped_into(e, cluster, numa, dev, rsv, quotas)
+        e.stage(first)
+        e.schedule_staged(0, len(first))
+        e.unreserve(0, len(first), mask.astype(np.uint8))
+        ga, gc, gm = e.read_numa()
+        wa, wc, wm = oracle.numa_state_read(w["numa"], cluster.n)
+        assert np.array_equal(ga, wa) and np.array_equal(gc, wc) and np.array_equal(gm, wm)
+        assert np.array_equal(e.read_quotas(len(quotas))["used"], w["quotas"]["used"])
+        e.stage(second)
+        e.schedule_staged(0, len(second))
+        node, score = e.fetch(0, len(second))
+        assert np.array_equal(node, node2) and np.array_equal(score, score2)
+        assert np.array_equal(e.fetch_reservations(0, len(second)), slot2)
+        assert np.array_equal(e.fetch_devices(0, len(second)), minors2)
+        assert np.array_equal(e.fetch_cpusets(0, len(second)), cpus2)
+
+
+@pytest.mark.gpu
+def test_evaluate_reservation_matches_oracle_loop_first_pod():
+    """kg_pods_evaluate_reservation reports, for the first pod, the same feasible set and totals the scheduling pass
+    uses: the argmax of its normalized totals is the pod's placement."""
+    cluster, numa, dev, rsv, pods, quotas = workload(600, 1, 161)
+    cfg = config()
+    w = oracle_run(cfg, cluster, numa, dev, rsv, pods, None)
+    with Engine(cfg, cluster.n) as e:
+        synth.load_shipped_into(e, cluster, numa, dev, rsv)
+        ev = e.evaluate_reservation(pods[0])
+    feas = ev["pass"] == 1
+    if not feas.any():
+        assert w["node"][0] == -1
+        return
+    raw = np.where(feas, ev["score"], 0)
+    order = np.where(feas & (ev["order"] > 0), ev["order"], np.iinfo(np.int64).max)
+    pref = int(np.argmin(order)) if (order < np.iinfo(np.int64).max).any() else -1
+    if pref >= 0:
+        raw[pref] = 1000
+    mx, mds = raw.max(), np.where(feas, ev["ds_raw"], 0).max()
+    total = ev["base"] + (5000 * (100 * raw // mx) if mx > 0 else 0) + (100 * ev["ds_raw"] // mds if mds > 0 else 0)
+    total = np.where(feas, total, -1)
+    assert int(np.argmax(total)) == w["node"][0] and int(total.max()) == w["score"][0]
