@@ -8,8 +8,14 @@ percentageOfNodesToScore=100, ties → lowest index.  One step = scheduling `--p
 schedules the whole 1M-pod queue of config 3.  Inputs are resident in HBM before the timed region (nodes
 ingested, pod queue staged); PCIe-inclusive timing of kg_pods_schedule is reported separately.
 
-Other workloads (--workload): c1 (500 nodes, 5k pods: the reference's CPU-runnable case), c4 (NodeNUMAResource),
-c5 (Reservation + DeviceShare + ElasticQuota, 50k nodes), c5ds / c5r (its DeviceShare / Reservation halves).
+Other workloads (--workload): c1 (500 nodes, 5k pods: the reference's CPU-runnable case), c2 (10k nodes, 100k pods),
+c4 (NodeNUMAResource), c5 (Reservation + DeviceShare + ElasticQuota, 50k nodes), c5ds / c5r (its DeviceShare /
+Reservation halves), shipped (the reference's shipped profile, config/manager/scheduler-config.yaml:66-117:
+LoadAware + NodeNUMAResource + DeviceShare + Reservation + ElasticQuota on 256-cpu NUMA nodes with 8 GPUs).
+
+Single-pod calls (the drop-in's scheduleOne, framework_extender_factory.go:156-185): after the timed region
+`--single-pod-calls` more queued pods are scheduled one kg_pods_schedule_staged call each, and the same number through
+kg_pods_schedule (host pod in, host decision out); p50 / p99 microseconds per call are reported.
 
 After the timed region: (1) `--profile-pods` more queued pods are scheduled with live kernel timing (HIP events
 bracketing every launch on its own stream, kg_profile_enable) — the roofline's kernel time; (2) the first
@@ -41,11 +47,13 @@ B_NODE = 76.0          # SURVEY §8d b_node for Fit + LoadAware: bytes of node c
 # workload → (nodes, pods per step, batch, pods per wave, default check)
 WORKLOADS = {
     "c1": (500, 5_000, 32, 8, 5_000),
+    "c2": (10_000, 10_000, 32, 8, 10_000),
     "c3": (100_000, 100_000, 32, 8, 10_000),
     "c4": (10_000, 10_000, 16, 1, 2_000),
     "c5": (50_000, 10_000, 32, 4, 2_000),
     "c5ds": (50_000, 10_000, 32, 4, 2_000),
     "c5r": (50_000, 10_000, 32, 4, 2_000),
+    "shipped": (50_000, 5_000, 32, 4, 1_000),
 }
 
 
@@ -71,6 +79,8 @@ def parse():
                     help="PMC summary (scripts/pmc_summary.py) of the same workload: per-launch HBM bytes "
                          "(default profiles/r02/traffic_<workload>.json)")
     ap.add_argument("--check", type=int, default=None, help="verify the first N placements against the oracle")
+    ap.add_argument("--single-pod-calls", type=int, default=200, help="single-pod scheduling calls timed one by one "
+                    "after the timed region (0 = skip)")
     return ap.parse_args()
 
 
@@ -128,6 +138,10 @@ class Work:
             self.seed = S.BASE_SEED + 10
             self.cluster, self.devices, self.rsv = S.make_c5_cluster(nodes, seed=self.seed)
             self.make_pods = S.make_c5_pods
+        elif name == "shipped":
+            self.seed = S.BASE_SEED + 13
+            self.cluster, self.numa, self.devices, self.rsv = S.make_shipped_cluster(nodes, seed=self.seed)
+            self.make_pods = S.make_shipped_pods
         elif name == "c4":
             self.seed = S.BASE_SEED + 4
             self.cluster, self.numa = S.make_numa_cluster(nodes, seed=self.seed)
@@ -148,12 +162,14 @@ class Work:
     def set_queue(self, pods):
         """ElasticQuota groups sized on the queue's demand (C5: 16 groups whose limits run out mid-queue)."""
         from koordinator_amd import synth
-        if self.name == "c5":
+        if self.name in ("c5", "shipped"):
             self.quotas = synth.make_c5_quotas(pods, seed=self.seed + 2)
 
     def load(self, e):
         from koordinator_amd import synth
-        if self.name == "c5":
+        if self.name == "shipped":
+            synth.load_shipped_into(e, self.cluster, self.numa, self.devices, self.rsv, self.quotas)
+        elif self.name == "c5":
             synth.load_c5_into(e, self.cluster, self.devices, self.rsv, self.quotas)
         elif self.numa is not None:
             synth.load_numa_into(e, self.cluster, self.numa)
@@ -174,7 +190,8 @@ class Work:
             on, _, _ = oracle.schedule_resv(cfg, cl.nodes, cl.metrics, st, self.rsv.copy(), pods, cl.now_ns,
                                             devices=None if self.devices is None else self.devices.copy(),
                                             quotas=None if self.quotas is None else self.quotas.copy(),
-                                            n_threads=threads)
+                                            n_threads=threads,
+                                            numa_buf=None if self.numa is None else oracle.numa_states(self.numa))
             return on, "oracle/reservation.c or_schedule_resv_full (Parallelizer chunking)"
         if self.devices is not None:
             on, _, _, _ = oracle.schedule_full(cfg, cl.nodes, cl.metrics, st, pods, cl.now_ns, threads,
@@ -247,13 +264,21 @@ def main():
     elif wl == "c5r":  # shipped weights: Reservation 5000 (config/manager/scheduler-config.yaml:90-91)
         profile = F.Profile(filter=(F.NODE_RESOURCES_FIT, F.LOAD_AWARE, F.RESERVATION),
                             score={F.NODE_RESOURCES_FIT: 1, F.LOAD_AWARE: 1, F.RESERVATION: 5000})
+    la = None
+    if wl == "shipped":  # config/manager/scheduler-config.yaml:29-117: plugins, weights and LoadAware args
+        profile = F.Profile(filter=(F.NODE_RESOURCES_FIT, F.LOAD_AWARE, F.NODE_NUMA_RESOURCE, F.DEVICE_SHARE,
+                                    F.RESERVATION),
+                            score={F.NODE_RESOURCES_FIT: 1, F.LOAD_AWARE: 1, F.NODE_NUMA_RESOURCE: 1, F.DEVICE_SHARE: 1,
+                                   F.RESERVATION: 5000})
+        la = F.LoadAwareSchedulingArgs(filter_expired_node_metrics=False, node_metric_expiration_seconds=300)
     cfg = framework.build_config(batch_pods=args.batch, pods_per_wave=args.pods_per_wave, device_id=d.local_rank,
-                                 profile=profile, pipeline_depth=args.depth)
+                                 profile=profile, pipeline_depth=args.depth, la=la)
     work = Work(wl, args.nodes, cfg)
     cluster = work.cluster
     total = args.steps * args.pods_per_step
     n_prof = args.profile_pods if args.profile_pods is not None else min(args.pods_per_step, 20_000)
-    pods = work.make_pods(total + n_prof, seed=work.seed + 1)
+    n_single = args.single_pod_calls if d.world == 1 else 0
+    pods = work.make_pods(total + n_prof + n_single, seed=work.seed + 1)
     work.set_queue(pods)
 
     def engine():
@@ -291,8 +316,31 @@ def main():
         e.schedule_staged(total, n_prof)
         live = {k: {"avg_ms": ms / n, "launches": n} for k, (ms, n) in e.profile_read().items()}
         e.profile(False)
+    # the drop-in's per-pod call (scheduleOne): single-pod kg_pods_schedule_staged calls continuing the queue, and the
+    # same pods again through kg_pods_schedule (host record in, host decision out) on a fresh engine
+    single = None
+    if n_single > 0:
+        lat = []
+        base = total + n_prof
+        for j in range(n_single):
+            tt = time.perf_counter()
+            e.schedule_staged(base + j, 1)
+            lat.append(time.perf_counter() - tt)
+        lat = np.array(lat) * 1e6
+        single = {"staged_p50_us": float(np.percentile(lat, 50)), "staged_p99_us": float(np.percentile(lat, 99)),
+                  "calls": n_single}
+        with engine() as es:
+            lat2 = []
+            for j in range(n_single):
+                tt = time.perf_counter()
+                es.schedule(pods[base + j:base + j + 1])
+                lat2.append(time.perf_counter() - tt)
+        lat2 = np.array(lat2) * 1e6
+        single.update({"host_p50_us": float(np.percentile(lat2, 50)), "host_p99_us": float(np.percentile(lat2, 99)),
+                       "note": "kg_pods_schedule_staged(count=1) continuing the staged queue after the timed region; "
+                               "kg_pods_schedule(1 host pod) on a fresh engine: decode + upload + schedule + result"})
     # isolated replays of one round's kernels (warm caches, no concurrency) for comparison
-    rsv_path = wl in ("c5r", "c5")
+    rsv_path = wl in ("c5r", "c5", "shipped")
     names = (("rsv_eval", "rsv_select") if rsv_path else
              ("eval_round", "merge_round", "resolve_round") + (("ds_max_round", "ds_norm_reduce") if wl == "c5ds" else ()))
     isolated = {name: e.bench_kernel(which, args.kernel_iters) for which, name in enumerate(names)}
@@ -300,7 +348,7 @@ def main():
     # roofline kernel: the wide pass — the only kernel whose work scales with node evaluations.  One launch
     # processes the round's B pods against every node row of this rank's shard, reading each row once:
     # algorithmic bytes = rows × b_node + the candidate lists written + the pods read.
-    dom = {"c5ds": "ds_max_round", "c5r": "rsv_eval", "c5": "rsv_eval"}.get(wl, "eval_round")
+    dom = {"c5ds": "ds_max_round", "c5r": "rsv_eval", "c5": "rsv_eval", "shipped": "rsv_eval"}.get(wl, "eval_round")
     n_local = -(-cluster.n // d.world)
     nt = max(1, -(-n_local // 256))
     B = 1 if rsv_path else args.batch
@@ -311,6 +359,8 @@ def main():
         prof_pods = pods[total:total + n_prof] if n_prof > 0 else pods[:1]
         frac_dev = float(prof_pods["device_requests"].any(axis=1).mean()) if work.devices is not None else 0.0
         algo = n_local * (B_NODE + 4 + 8) + int((work.rsv["n"] > 0).sum()) * 192.0 + frac_dev * n_local * 272.0
+        if work.numa is not None:  # NumaStatic (144 B) + NodeAllocation (104 B) rows and the stored affinity (4 B)
+            algo += n_local * (144.0 + 104.0 + 4.0)
     else:
         algo = n_local * B_NODE + B * nt * 8 * 8.0 + B * 96.0
     dom_ms = live.get(dom, {}).get("avg_ms") or isolated[dom][0]
@@ -356,6 +406,12 @@ def main():
         pods_s = total / elapsed
         desc = {
             "c1": "C1 cluster: %d nodes, %d-pod FIFO queue, NodeResourcesFit+LoadAwareScheduling, %d pods per step",
+            "c2": "C2 cluster: %d nodes, %d-pod FIFO queue, NodeResourcesFit+LoadAwareScheduling, %d pods per step",
+            "shipped": "shipped profile (config/manager/scheduler-config.yaml:66-117): %d 2-socket 256-cpu NUMA nodes x "
+                       "8 GPUs (30%% with 1-4 cpu/memory reservations), %d-pod FIFO queue (70%% cpuset LSR/LSE, 30%% "
+                       "GPU-share, 20%% reservation-owned, 80%% in 16 ElasticQuota groups), NodeResourcesFit+"
+                       "LoadAwareScheduling+NodeNUMAResource+DeviceShare+Reservation (w 1/1/1/1/5000)+ElasticQuota, "
+                       "one pod per device pass, %d pods per step",
             "c3": "C3 cluster: %d nodes, %d-pod FIFO queue, NodeResourcesFit+LoadAwareScheduling, %d pods per step",
             "c4": "C4 cluster: %d 2-socket 256-cpu nodes (node count: builder's choice, BASELINE names none), "
                   "%d-pod FIFO queue (70%% cpuset LSR/LSE), NodeResourcesFit+LoadAwareScheduling+NodeNUMAResource, "
@@ -373,6 +429,8 @@ def main():
         out = {
             "metric": {"c3": "pods scheduled/sec at 100k nodes (node-evals/sec alongside)",
                        "c1": "pods scheduled/sec, config 1 (500 nodes; node-evals/sec alongside)",
+                       "c2": "pods scheduled/sec, config 2 (10k nodes; node-evals/sec alongside)",
+                       "shipped": "pods scheduled/sec, the shipped koord-scheduler profile (node-evals/sec alongside)",
                        "c4": "pods scheduled/sec, NodeNUMAResource cpuset/NUMA profile (node-evals/sec alongside)",
                        "c5ds": "pods scheduled/sec, DeviceShare GPU-share profile (node-evals/sec alongside)",
                        "c5r": "pods scheduled/sec, Reservation profile (node-evals/sec alongside)",
@@ -408,6 +466,7 @@ def main():
                          "isolated_ms": {k: v[0] for k, v in isolated.items()}},
             "cpu_baseline": cpu,
             "pcie_inclusive_pods_per_sec": pcie,
+            "single_pod_call": single,
             "oracle_check": check,
             "oracle_check_pods": min(args.check, total) if args.check else 0,
         }

@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define KG_ABI_VERSION 7
+#define KG_ABI_VERSION 8
 
 /* ---- resource slots (fixed order) ------------------------------------------------------- */
 enum {

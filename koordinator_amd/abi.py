@@ -35,7 +35,7 @@ POD_REQUEST_KEYS, POD_CPU_KEY, POD_MEM_KEY = 8, 16, 32
 MAX_OWNER_GROUPS = 64
 QUOTA_RES = 8
 MAX_QUOTAS = 64
-ABI_VERSION = 7
+ABI_VERSION = 8
 MAX_RSV_SLOTS = 4
 RSV_POLICY = {"Default": 0, "Aligned": 1, "Restricted": 2}
 POD_RSV_AFFINITY = 1

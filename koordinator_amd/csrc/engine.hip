@@ -2035,6 +2035,7 @@ struct kg_engine {
   // F_EPH_OVER (ephemeral-storage Requested > Allocatable) must be recomputed on the device: eph_any once any
   // ephemeral Requested delta was pushed, eph_dirty until the flags column has been refreshed since
   bool eph_any = false, eph_dirty = false;
+  int64_t rounds_ahead = 256;  // rounds one host batch launches (adapted to how often rounds stop early)
   // scheduler clock for isNodeMetricExpired (kg_engine_set_clock): 0 = the newest now given to
   // kg_node_metrics_update, 1 = fixed, 2 = the host's real-time clock at every call
   int clock_mode = 0;
@@ -2103,8 +2104,10 @@ struct kg_engine {
   DevBuf<uint64_t> rsv_val;     // [capacity] packed per-node pass-1 values
   DevBuf<unsigned long long> rsv_ws;  // [8]: [3] = pod cursor, [4] = the call's end (graph launches)
   // the instantiated reservation group graph, reused while its launch arguments are unchanged
-  hipGraphExec_t rsv_exec = nullptr;
+  hipGraphExec_t rsv_exec = nullptr;   // a group of kRsvGroup passes + rsv_apply
   std::vector<unsigned char> rsv_exec_sig;
+  hipGraphExec_t rsv_exec1 = nullptr;  // one pass + rsv_apply (single-pod calls)
+  std::vector<unsigned char> rsv_exec1_sig;
   DevBuf<uint64_t> rsv_part;    // [4][blocks] per-block partials (preferred-node key, max raw, max key, max ds raw)
   // live kernel timing (kg_profile_enable): HIP event pairs around every launch of the round runners, on the
   // launch's own stream, folded into per-kind totals after each batch synchronises
@@ -2356,7 +2359,7 @@ int decode_pod(const kg_engine* e, const kg_pod& p, DevPod& d) {
     zero &= p.requests[r] == 0;
     if (c.fit_filter && r >= kAuxFirst + kAux && p.requests[r] != 0)
       return fail(KG_E_UNSUPPORTED, "pod requests resource slot %d outside the accelerated NodeResourcesFit set", r);
-    if (c.fit_filter && r >= kAuxFirst && p.requests[r] != 0 && (e->numa_on || e->ds_on || e->rsv_on))
+    if (c.fit_filter && r >= kAuxFirst && p.requests[r] != 0 && (e->numa_on || e->ds_on) && !e->exact_on)
       return fail(KG_E_UNSUPPORTED, "pod requests ephemeral-storage / a scalar resource (slot %d): accelerated in the "
                   "NodeResourcesFit + LoadAware profiles only", r);
   }
@@ -3084,6 +3087,7 @@ double now_s() {
 // Reservation profile: one FIFO pod per device pass (rsv_eval → rsv_select; Reserve in the next rsv_eval),
 // kRsvGroup passes + the group-closing rsv_apply per hipGraph launch.  The pod index lives in the device cursor ws[3]; passes past `end` are no-ops.
 constexpr int kRsvGroup = 32;
+constexpr int64_t kExactSmall = 2;  // schedule calls of at most this many pods take the exact pass (single-pod path)
 RsvExt rsv_ext(kg_engine* e) {
   RsvExt X;
   X.ds = e->ds_on ? e->ds_d.p : nullptr;
@@ -3100,6 +3104,7 @@ RsvExt rsv_ext(kg_engine* e) {
   X.aff = e->numa_on ? e->numa_aff.p : nullptr;
   X.out_cpus = e->numa_on ? e->out_cpus.p : nullptr;
   X.out_nrec = e->numa_on ? e->out_nrec.p : nullptr;
+  X.paux = e->paux.p;
   return X;
 }
 
@@ -3133,14 +3138,9 @@ int run_rsv(kg_engine* e, int64_t first, int64_t count, kg_stats* stats, double 
     // KG_RSV_NO_GRAPH=1: plain stream launches (profilers whose kernel tracing does not follow graph launches);
     // live kernel timing also uses plain launches (its events bracket each launch)
     static const bool no_graph = std::getenv("KG_RSV_NO_GRAPH") && std::getenv("KG_RSV_NO_GRAPH")[0] == '1';
-    if (no_graph || e->prof_on || count < kRsvGroup) {
-      for (int64_t c = 0; c < count; c += kRsvGroup) issue_group(end, (int)std::min<int64_t>(kRsvGroup, count - c));
-      HIP_TRY(hipGetLastError());
-      HIP_TRY(hipStreamSynchronize(e->stream));
-      if (e->prof_on)
-        if (int rc = prof_collect(e)) return rc;
-    } else {
-      // the group graph is keyed on its launch arguments (table / buffer pointers, sizes, profile parameters)
+    // graphs of `passes` passes (kRsvGroup, or 1 for single-pod calls), keyed on their launch arguments (table /
+    // buffer pointers, sizes, profile parameters) and re-instantiated when one changes
+    auto graph = [&](int passes, hipGraphExec_t& exec, std::vector<unsigned char>& exec_sig) -> int {
       std::vector<unsigned char> sig;
       auto put = [&](const void* q, size_t len) {
         const unsigned char* b = static_cast<const unsigned char*>(q);
@@ -3154,26 +3154,43 @@ int run_rsv(kg_engine* e, int64_t first, int64_t count, kg_stats* stats, double 
       put(&e->P, sizeof(e->P));
       put(&e->RP, sizeof(e->RP));
       put(&X, sizeof(X));
-      if (!e->rsv_exec || sig != e->rsv_exec_sig) {
-        if (e->rsv_exec) (void)hipGraphExecDestroy(e->rsv_exec);
-        e->rsv_exec = nullptr;
-        hipGraph_t graph = nullptr;
-        HIP_TRY(hipStreamBeginCapture(e->stream, hipStreamCaptureModeThreadLocal));
-        issue_group(-1, kRsvGroup);
-        const hipError_t ce = hipStreamEndCapture(e->stream, &graph);
-        if (ce != hipSuccess) return fail(KG_E_DEVICE, "hipStreamEndCapture: %s", hipGetErrorString(ce));
-        const hipError_t ie = hipGraphInstantiate(&e->rsv_exec, graph, nullptr, nullptr, 0);
-        (void)hipGraphDestroy(graph);
-        if (ie != hipSuccess) {
-          e->rsv_exec = nullptr;
-          return fail(KG_E_DEVICE, "reservation pass graph: %s", hipGetErrorString(ie));
-        }
-        e->rsv_exec_sig = sig;
+      if (exec && sig == exec_sig) return 0;
+      if (exec) (void)hipGraphExecDestroy(exec);
+      exec = nullptr;
+      hipGraph_t gr = nullptr;
+      HIP_TRY(hipStreamBeginCapture(e->stream, hipStreamCaptureModeThreadLocal));
+      issue_group(-1, passes);
+      const hipError_t ce = hipStreamEndCapture(e->stream, &gr);
+      if (ce != hipSuccess) return fail(KG_E_DEVICE, "hipStreamEndCapture: %s", hipGetErrorString(ce));
+      const hipError_t ie = hipGraphInstantiate(&exec, gr, nullptr, nullptr, 0);
+      (void)hipGraphDestroy(gr);
+      if (ie != hipSuccess) {
+        exec = nullptr;
+        return fail(KG_E_DEVICE, "exact pass graph: %s", hipGetErrorString(ie));
       }
+      exec_sig = sig;
+      return 0;
+    };
+    if (no_graph || e->prof_on || (count > 1 && count < kRsvGroup)) {
+      for (int64_t c = 0; c < count; c += kRsvGroup) issue_group(end, (int)std::min<int64_t>(kRsvGroup, count - c));
+      HIP_TRY(hipGetLastError());
+      HIP_TRY(hipStreamSynchronize(e->stream));
+      if (e->prof_on)
+        if (int rc = prof_collect(e)) return rc;
+    } else {
+      hipGraphExec_t ex = nullptr;
+      if (count == 1) {
+        if (int rc = graph(1, e->rsv_exec1, e->rsv_exec1_sig)) return rc;
+        ex = e->rsv_exec1;
+      } else {
+        if (int rc = graph(kRsvGroup, e->rsv_exec, e->rsv_exec_sig)) return rc;
+        ex = e->rsv_exec;
+      }
+      const int64_t per = count == 1 ? 1 : kRsvGroup;
       hipError_t ge = hipSuccess;
-      for (int64_t c = 0; ge == hipSuccess && c < count; c += kRsvGroup) ge = hipGraphLaunch(e->rsv_exec, e->stream);
+      for (int64_t c = 0; ge == hipSuccess && c < count; c += per) ge = hipGraphLaunch(ex, e->stream);
       if (ge == hipSuccess) ge = hipStreamSynchronize(e->stream);
-      if (ge != hipSuccess) return fail(KG_E_DEVICE, "reservation pass graph: %s", hipGetErrorString(ge));
+      if (ge != hipSuccess) return fail(KG_E_DEVICE, "exact pass graph: %s", hipGetErrorString(ge));
     }
   } else if (count > 0) {
     HIP_TRY(hipMemsetAsync(e->out_keys.p + first, 0, count * 8, e->stream));
@@ -3379,7 +3396,7 @@ static int engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank,
   e->RP.filter = (int32_t)(c.reservation_filter != 0);
   e->RP.score = (int32_t)(c.reservation_score != 0);
   e->RP.weight = (int32_t)c.weight_reservation;
-  if (e->exact_on) {
+  {  // the exact pass's tables: its profiles, and single-pod calls of every profile (schedule_staged_impl)
     if (e->numa_on)
       if (int rc = e->numa_aff.ensure(cap)) return bail(rc);
     if (int rc = e->rsv_d.ensure(cap)) return bail(rc);
@@ -3789,7 +3806,7 @@ int kg_pods_stage(kg_engine* e, const kg_pod* pods, int64_t n) {
           return fail(KG_E_UNSUPPORTED, "pod %lld requests devices; the profile has no DeviceShare (NodeResourcesFit on "
                       "device resources is not accelerated)", (long long)k);
   }
-  if (e->exact_on) {
+  {  // exact-pass records (the Reservation view of every pod; single-pod calls of any profile use the pass)
     std::vector<RsvPod> hr(std::max<int64_t>(n, 1));
     for (int64_t k = 0; k < n; ++k) {
       hr[k].owner_mask = (uint64_t)pods[k].reservation_owner_mask;
@@ -3838,7 +3855,9 @@ static int schedule_staged_impl(kg_engine* e, int64_t first, int64_t count, kg_s
   if (!e) return fail(KG_E_INVALID, "engine is NULL");
   if (first < 0 || count < 0 || first + count > e->n_staged) return fail(KG_E_INVALID, "staged range");
   const double t0 = now_s();
-  if (e->exact_on) return run_rsv(e, first, count, stats, t0);
+  // the exact per-pod pass: its profiles, and calls of at most kExactSmall pods of any profile (the drop-in's per-pod
+  // scheduleOne): one pass costs less than a round's eval + merge + resolve when a round would hold one pod
+  if (e->exact_on || (count <= kExactSmall && e->n_ranks == 1)) return run_rsv(e, first, count, stats, t0);
   RoundGeom g;
   if (int rc = prepare_rounds(e, g)) return rc;
   const int64_t end = first + count;
@@ -3849,11 +3868,19 @@ static int schedule_staged_impl(kg_engine* e, int64_t first, int64_t count, kg_s
   int64_t cur = first;
   while (cur < end) {
     // a round that stops early poisons the rest of its batch; the next batch restarts from the device cursor
-    // (DeviceShare rounds read the cursor themselves: an early stop only shortens that round)
-    const int64_t n_rounds = std::min<int64_t>((end - cur + g.B - 1) / g.B, kMaxBatchRounds);
+    // (DeviceShare rounds read the cursor themselves: an early stop only shortens that round).  The batch launches
+    // at most rounds_ahead rounds: halved towards the rounds that ran before a stop when rounds stop early (small
+    // clusters), doubled back when a batch completes, so a stop wastes few poisoned launches.
+    const int64_t n_rounds = std::min<int64_t>({(end - cur + g.B - 1) / g.B, kMaxBatchRounds, e->rounds_ahead});
+    const int64_t ran0 = host_stats[1];
     if (int rc = e->ds_on ? run_batch_ds(e, g, end, n_rounds) : run_batch(e, g, cur, end, n_rounds)) return rc;
     HIP_TRY(hipMemcpy(host_stats, e->cursor.p, 8 * 8, hipMemcpyDeviceToHost));
     if (host_stats[5]) return fail(KG_E_DEVICE, "resolver chain wait timed out (round sequence %lld)", (long long)host_stats[4]);
+    const bool stopped = host_stats[0] < std::min<int64_t>(end, cur + n_rounds * g.B);
+    const int64_t ran = host_stats[1] - ran0;
+    if (!e->ds_on)  // DeviceShare rounds are cursor-driven: a stop never poisons the rest of the batch
+      e->rounds_ahead = stopped ? std::max<int64_t>(2, std::min<int64_t>(e->rounds_ahead, 2 * ran))
+                                : std::min<int64_t>(kMaxBatchRounds, 2 * e->rounds_ahead);
     cur = host_stats[0];
   }
   if (stats) {

@@ -73,6 +73,8 @@ struct RsvExt {
   uint32_t* __restrict__ aff;          // [cap] the affinity NUMA Filter stored for the pass's pod: mask | nil << 8
   uint64_t* __restrict__ out_cpus;     // [pods][kCpuWords] the cpuset Reserve allocated
   int64_t* __restrict__ out_nrec;      // [pods][kNumaRecWords] the pod's NUMA allocation record
+  // NodeResourcesFit over ephemeral-storage / scalar resources (P_AUX pods): [pods][kAux] requests
+  const int64_t* __restrict__ paux;
 };
 
 struct RsvOut {
@@ -120,7 +122,7 @@ __device__ __forceinline__ RsvOut rsv_eval_node(const DevTable& T, const RsvNode
                                                 const int32_t* __restrict__ rsv_n, int64_t i, const DevPod& p,
                                                 const RsvPod& rp, const EvalParams& P, const RsvParams& RP,
                                                 const RsvExt& X, const DsPod* dp, const NumaPod* np = nullptr,
-                                                RsvDbg* dbg = nullptr) {
+                                                RsvDbg* dbg = nullptr, const int64_t* aux_req = nullptr) {
   Row r = load_row(T, i);
   const int ns = rsv_n[i];
   RsvOut o{false, 0, 0, -1, 0x7fffffff, 0};
@@ -183,6 +185,8 @@ __device__ __forceinline__ RsvOut rsv_eval_node(const DevTable& T, const RsvNode
   }
   int64_t t = 0;
   if (!eval_node(r, p, P, t)) return o;  // NodeResourcesFit + LoadAware on the restored NodeInfo
+  // fitsRequest over ephemeral-storage and the scalar resources the pod requests (reservation/plugin.go:469-479)
+  if (aux_req && P.fit_filter && !aux_fits(T, i, aux_req)) return o;
   // satisfied(s): filterWithReservations([s]) (plugin.go:384-428) with fitsNode (:433-482), preemptible = 0
   const bool kc = (p.flags & P_CPU_KEY) != 0, km = (p.flags & P_MEM_KEY) != 0;
   uint32_t sat = 0;
@@ -367,6 +371,9 @@ __device__ __forceinline__ bool rsv_reserve(const DevTable& T, RsvNode* __restri
   }
   Row r = load_row(T, w);
   const int64_t prod = (p.flags & P_PROD) ? 1 : 0;
+  if (X.paux && (p.flags & P_AUX))  // NodeInfo.Requested of ephemeral-storage / the scalar resources
+#pragma unroll
+    for (int q = 0; q < kAux; ++q) T.aux[(size_t)(kAux + q) * T.cap + w] += X.paux[(size_t)j * kAux + q];
   r.req_cpu += p.req_cpu;
   r.req_mem += p.req_mem;
   r.nz_cpu += p.nz_cpu;
@@ -455,7 +462,8 @@ __global__ __launch_bounds__(kRsvThreads) void rsv_eval(DevTable T, RsvNode* __r
     const RsvPod rp = rpods[j];
     const DsPod* dp = X.ds ? &X.dpods[j] : nullptr;
     const NumaPod* np = X.ns ? &X.npods[j] : nullptr;
-    const RsvOut o = rsv_eval_node(T, RN, rsv_n, i, p, rp, P, RP, X, dp, np);
+    const int64_t* aux = (X.paux && (p.flags & P_AUX)) ? X.paux + (size_t)j * kAux : nullptr;
+    const RsvOut o = rsv_eval_node(T, RN, rsv_n, i, p, rp, P, RP, X, dp, np, nullptr, aux);
     if (o.feas) {
       v = ((uint64_t)(uint32_t)o.base << 32) | ((uint64_t)(uint32_t)o.dsraw << 16) |
           ((uint64_t)(uint32_t)o.raw << 8) | (1ull << 7) | (uint64_t)(o.nom + 1);

@@ -85,8 +85,15 @@ def test_oracle_loops_agree_without_reservations():
 # device parity
 # ---------------------------------------------------------------------------------------------------------------
 def engine_run(cfg, cluster, numa, dev, rsv, pods, quotas, chunks=1):
+    rsv_on = bool(cfg[0]["reservation_filter"] or cfg[0]["reservation_score"])
     with Engine(cfg, cluster.n) as e:
-        synth.load_shipped_into(e, cluster, numa, dev, rsv, quotas)
+        if rsv_on:
+            synth.load_shipped_into(e, cluster, numa, dev, rsv, quotas)
+        else:  # a profile without Reservation holds no reservation table
+            synth.load_numa_into(e, cluster, numa)
+            e.upsert_devices(dev)
+            if quotas is not None:
+                e.set_quotas(quotas)
         e.stage(pods)
         bounds = np.linspace(0, len(pods), chunks + 1).astype(int)
         for a, b in zip(bounds[:-1], bounds[1:]):
@@ -98,7 +105,8 @@ def engine_run(cfg, cluster, numa, dev, rsv, pods, quotas, chunks=1):
         out["state"] = e.read_state()
         out["numa"] = e.read_numa()
         out["used"] = e.read_devices()
-        out["rsv"] = e.read_reservations()
+        z = np.zeros((cluster.n, abi.MAX_RSV_SLOTS), dtype=np.int64)
+        out["rsv"] = e.read_reservations() if rsv_on else (z, z, z)
         out["quotas"] = e.read_quotas(len(quotas)) if quotas is not None else None
     return out
 
@@ -155,6 +163,7 @@ def test_numa_deviceshare_without_reservation():
     prof = F.Profile(filter=PROFILE.filter[:-1], score={k: v for k, v in PROFILE.score.items() if k != F.RESERVATION})
     numa_args = F.NodeNUMAResourceArgs(scoring_strategy="MostAllocated")
     ds_args = F.DeviceShareArgs(scoring_strategy="MostAllocated")
+    pods["quota_id"] = 0
     check(config(profile=prof, numa=numa_args, deviceshare=ds_args), cluster, numa, dev, rsv, pods, None)
 
 
@@ -171,6 +180,8 @@ def test_shipped_unreserve_matches_oracle():
         oracle.unreserve(cfg, w["st"], first[j], int(w["node"][j]), numa_buf=w["numa"], devices=w["dev"], rsv=w["rsv"],
                          quotas=w["quotas"], cpus=w["cpus"][j], numa_alloc=w["nalloc"][j], minors=int(w["minors"][j]),
                          slot=int(w["slot"][j]))
+    after_numa = oracle.numa_state_read(w["numa"], cluster.n)
+    after_used = w["quotas"]["used"].copy()
     node2, score2, slot2, minors2, cpus2, _ = oracle.schedule_resv(cfg, cluster.nodes, cluster.metrics, w["st"], w["rsv"],
                                                                   second, cluster.now_ns, devices=w["dev"],
                                                                   quotas=w["quotas"], n_threads=8, with_minors=True,
@@ -181,9 +192,9 @@ def test_shipped_unreserve_matches_oracle():
         e.schedule_staged(0, len(first))
         e.unreserve(0, len(first), mask.astype(np.uint8))
         ga, gc, gm = e.read_numa()
-        wa, wc, wm = oracle.numa_state_read(w["numa"], cluster.n)
+        wa, wc, wm = after_numa
         assert np.array_equal(ga, wa) and np.array_equal(gc, wc) and np.array_equal(gm, wm)
-        assert np.array_equal(e.read_quotas(len(quotas))["used"], w["quotas"]["used"])
+        assert np.array_equal(e.read_quotas(len(quotas))["used"], after_used)
         e.stage(second)
         e.schedule_staged(0, len(second))
         node, score = e.fetch(0, len(second))
@@ -198,6 +209,7 @@ def test_evaluate_reservation_matches_oracle_loop_first_pod():
     """kg_pods_evaluate_reservation reports, for the first pod, the same feasible set and totals the scheduling pass
     uses: the argmax of its normalized totals is the pod's placement."""
     cluster, numa, dev, rsv, pods, quotas = workload(600, 1, 161)
+    pods["quota_id"] = 0
     cfg = config()
     w = oracle_run(cfg, cluster, numa, dev, rsv, pods, None)
     with Engine(cfg, cluster.n) as e:
