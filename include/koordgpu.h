@@ -200,6 +200,17 @@ typedef struct kg_config {
   int64_t la_agg_usage_duration_ns;            /* UsageAggregatedDuration (0 = the longest recorded) */
   int64_t la_agg_score_type;                   /* ScoreAggregationType KG_AGG_* (0 = "")              */
   int64_t la_agg_score_duration_ns;            /* ScoreAggregatedDuration (0 = the longest recorded) */
+  /* upstream default plugins of a stock profile (k8s v1.24.15 pkg/scheduler/framework/plugins, not vendored; restated
+   * as published — see DESIGN.md §3.13).  Evaluated on the exact per-pod pass.  Weights default 1 upstream. */
+  int64_t taint_filter;                        /* TaintToleration at Filter (NoSchedule / NoExecute taints)      */
+  int64_t taint_score;                         /* TaintToleration at Score (PreferNoSchedule; reverse-normalized) */
+  int64_t weight_taint;
+  int64_t affinity_filter;                     /* NodeAffinity at Filter (nodeSelector + required terms)         */
+  int64_t affinity_score;                      /* NodeAffinity at Score (preferred terms; normalized)            */
+  int64_t weight_affinity;
+  int64_t balanced_score;                      /* NodeResourcesBalancedAllocation at Score                       */
+  int64_t weight_balanced;
+  int64_t balanced_resources;                  /* bit r: resource r (cpu 0, memory 1) is in its Resources list   */
   int64_t reserved[4];
 } kg_config;
 
@@ -247,6 +258,9 @@ typedef struct kg_pod_metric {
   int64_t prod;                                /* the pod's priority class is koord-prod               */
 } kg_pod_metric;
 
+/* Node affinity terms a pod may carry (more: the pod stays on the Go path) */
+#define KG_MAX_AFF_TERMS 4
+
 /* One pod, pre-decoded by the caller (PodRequestsAndLimits semantics, pkg/util/pod_resources_utils.go:48-64). */
 typedef struct kg_pod {
   int64_t requests[KG_RES_MAX];
@@ -268,6 +282,15 @@ typedef struct kg_pod {
   int64_t uid;                                 /* the pod's identity (matches kg_pod_metric.uid; 0 = none)  */
   int64_t assign_time_unix_nano;               /* kg_pods_add: the podAssignCache timestamp of the pod  */
                                                /* (pod_assign_cache.go:62-66); scheduled pods take the engine clock */
+  /* TaintToleration / NodeAffinity (ABI 8), over the caller's taint and predicate tables (kg_node_predicates): */
+  uint64_t tolerated_taints;                   /* bit t: the pod's tolerations tolerate taint t                 */
+  uint64_t node_selector;                      /* predicates pod.Spec.NodeSelector requires (all must hold)     */
+  int64_t n_required_terms;                    /* required NodeSelectorTerms (0 = no required node affinity)   */
+  uint64_t required_terms[KG_MAX_AFF_TERMS];   /* term k holds iff every listed predicate holds (0 = empty term: */
+                                               /* matches no node)                                             */
+  int64_t n_preferred_terms;                   /* preferred PreferredSchedulingTerms                            */
+  uint64_t preferred_terms[KG_MAX_AFF_TERMS];
+  int64_t preferred_weights[KG_MAX_AFF_TERMS];
 } kg_pod;
 
 /* pod reservation flags */
@@ -349,6 +372,16 @@ typedef struct kg_node_numa {
    * zone cpu AFTER amplifyNUMANodeResources (util.go:63-84), node allocatable cpu the amplified one. */
   double cpu_amplification_ratio;
 } kg_node_numa;
+
+/* Node-side view for TaintToleration / NodeAffinity (ABI 8).  The caller keeps two dense tables: up to 64 distinct
+ * taints (key, value, effect) and up to 64 distinct node-selector predicates (a NodeSelectorRequirement — key, operator,
+ * values — or a MatchFields requirement, or one nodeSelector key=value pair), and evaluates them on each node's
+ * labels / name when the node or the tables change (label matching is string work; the device combines the bits). */
+typedef struct kg_node_predicates {
+  uint64_t predicates;                         /* bit k: predicate k holds on the node                          */
+  uint64_t taints_hard;                        /* the node's taints with effect NoSchedule or NoExecute         */
+  uint64_t taints_soft;                        /* the node's taints with effect PreferNoSchedule                */
+} kg_node_predicates;
 
 typedef struct kg_stats {
   int64_t pods_scheduled;                      /* pods with a node                                    */
@@ -468,6 +501,9 @@ int kg_pods_evaluate_device(kg_engine* e, const kg_pod* pod, int32_t* out_pass, 
  * slots; fed by the reservation informer, eventhandlers/reservation_handler.go).  The Reservation profile runs
  * one FIFO pod per device pass (BeforePreFilter restore + Filter + PreScore/nominate + Score + NormalizeScore). */
 int kg_nodes_reservation_upsert(kg_engine* e, const kg_node_reservations* r, const int32_t* idx, int64_t n);
+/* TaintToleration / NodeAffinity node view of nodes idx[0..n) (replaces each node's predicates and taints; fed by the
+ * node informer after the caller re-evaluates its predicate / taint tables on the node's labels and taints). */
+int kg_nodes_predicates_upsert(kg_engine* e, const kg_node_predicates* p, const int32_t* idx, int64_t n);
 /* Reads the DEVICE reservation slots: allocated cpu / memory and assigned count, KG_MAX_RSV_SLOTS per node. */
 int kg_nodes_read_reservations(kg_engine* e, int64_t* allocated_cpu, int64_t* allocated_mem, int64_t* assigned);
 /* The reservation slot Reserve assumed each staged pod [first, first+count) into (-1 = none). */
@@ -541,7 +577,7 @@ int kg_debug_stamps(kg_engine* e, uint64_t* out);
 const char* kg_last_error(void);
 int kg_abi_version(void);
 /* sizeof of the ABI structs (0 kg_config, 1 kg_node, 2 kg_node_metric, 3 kg_pod, 4 kg_stats, 5 kg_node_numa,
- * 6 kg_node_device, 7 kg_quota, 8 kg_node_reservations, 9 kg_pod_metric) for
+ * 6 kg_node_device, 7 kg_quota, 8 kg_node_reservations, 9 kg_pod_metric, 10 kg_node_predicates) for
  * binding checks. */
 int64_t kg_abi_struct_size(int which);
 

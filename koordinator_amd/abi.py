@@ -55,6 +55,7 @@ DBG_MERGE_WORDS = 32  # KG_DBG_MERGE_WORDS: one kg_debug_numa_merge case
 REJECT_FIT_OTHER = 128  # NodeResourcesFit: ephemeral-storage / a scalar resource (RES_EPHEMERAL .. RES_MID_MEMORY)
 # DeviceShare device resources (KG_DEV_*)
 DEV_RES_MAX, MAX_MINORS = 8, 8
+MAX_AFF_TERMS = 4  # KG_MAX_AFF_TERMS
 DEV_NVIDIA_GPU, DEV_HYGON_DCU, DEV_KOORD_GPU, DEV_GPU_CORE, DEV_GPU_MEMORY, DEV_GPU_MEMORY_RATIO, DEV_FPGA, DEV_RDMA = \
     range(8)
 DEVICE_RESOURCE_SLOTS = {
@@ -91,6 +92,9 @@ CONFIG_DTYPE = np.dtype([
     _i64("pipeline_depth"),
     _i64("la_agg_usage_thresholds", RES_MAX), _i64("la_agg_usage_type"), _i64("la_agg_usage_duration_ns"),
     _i64("la_agg_score_type"), _i64("la_agg_score_duration_ns"),
+    _i64("taint_filter"), _i64("taint_score"), _i64("weight_taint"),
+    _i64("affinity_filter"), _i64("affinity_score"), _i64("weight_affinity"),
+    _i64("balanced_score"), _i64("weight_balanced"), _i64("balanced_resources"),
     _i64("reserved", 4),
 ])
 
@@ -128,7 +132,11 @@ POD_DTYPE = np.dtype([
     _i64("quota_id"),
     _i64("reservation_owner_mask"), _i64("reservation_flags"),
     _i64("uid"), _i64("assign_time_unix_nano"),
+    ("tolerated_taints", np.uint64), ("node_selector", np.uint64),
+    _i64("n_required_terms"), ("required_terms", np.uint64, (MAX_AFF_TERMS,)),
+    _i64("n_preferred_terms"), ("preferred_terms", np.uint64, (MAX_AFF_TERMS,)), _i64("preferred_weights", MAX_AFF_TERMS),
 ])
+NODE_PRED_DTYPE = np.dtype([("predicates", np.uint64), ("taints_hard", np.uint64), ("taints_soft", np.uint64)])
 
 NODE_RSV_DTYPE = np.dtype([_i64("n")] + [_i64(f, MAX_RSV_SLOTS) for f in (
     "owner", "allocatable_cpu", "allocatable_mem", "allocated_cpu", "allocated_mem", "assigned", "order", "policy",
@@ -157,7 +165,7 @@ STATS_DTYPE = np.dtype([
 ])
 
 STRUCT_DTYPES = {0: CONFIG_DTYPE, 1: NODE_DTYPE, 2: METRIC_DTYPE, 3: POD_DTYPE, 4: STATS_DTYPE, 5: NODE_NUMA_DTYPE,
-                 6: NODE_DEVICE_DTYPE, 7: QUOTA_DTYPE, 8: NODE_RSV_DTYPE, 9: POD_METRIC_DTYPE}
+                 6: NODE_DEVICE_DTYPE, 7: QUOTA_DTYPE, 8: NODE_RSV_DTYPE, 9: POD_METRIC_DTYPE, 10: NODE_PRED_DTYPE}
 
 # Every symbol include/koordgpu.h declares (tests check the library exports all of them).
 EXPORTED_SYMBOLS = (
@@ -171,7 +179,7 @@ EXPORTED_SYMBOLS = (
     "kg_quotas_set", "kg_quotas_read", "kg_nodes_reservation_upsert", "kg_nodes_read_reservations",
     "kg_results_fetch_reservations", "kg_profile_enable", "kg_profile_read", "kg_loopback_create",
     "kg_loopback_destroy", "kg_engine_create_loopback", "kg_pods_unreserve", "kg_engine_set_clock",
-    "kg_node_pods_metric_set", "kg_debug_numa_merge", "kg_pods_evaluate_reservation",
+    "kg_node_pods_metric_set", "kg_debug_numa_merge", "kg_pods_evaluate_reservation", "kg_nodes_predicates_upsert",
 )
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
@@ -246,6 +254,7 @@ def load_library(path: str | None = None):
         "kg_engine_set_clock": (i, [vp, i64]),
         "kg_debug_numa_merge": (i, [vp, vp, i64, vp]),
         "kg_pods_evaluate_reservation": (i, [vp, vp, vp]),
+        "kg_nodes_predicates_upsert": (i, [vp, vp, vp, i64]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)

@@ -1718,6 +1718,13 @@ __global__ void evaluate_pod_rsv(DevTable T, const RsvNode* __restrict__ RN, con
 }
 
 // Scatter of upserted device rows
+template <typename Rec>
+__global__ void scatter_rows(Rec* __restrict__ dst, const Rec* __restrict__ src, const int32_t* __restrict__ idx,
+                             int64_t n) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < n) dst[idx[k]] = src[k];
+}
+
 __global__ void scatter_ds(DsTable DT, const DsNode* __restrict__ s, const int32_t* __restrict__ idx, int64_t n) {
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= n) return;
@@ -2108,7 +2115,14 @@ struct kg_engine {
   std::vector<unsigned char> rsv_exec_sig;
   hipGraphExec_t rsv_exec1 = nullptr;  // one pass + rsv_apply (single-pod calls)
   std::vector<unsigned char> rsv_exec1_sig;
-  DevBuf<uint64_t> rsv_part;    // [4][blocks] per-block partials (preferred-node key, max raw, max key, max ds raw)
+  DevBuf<uint64_t> rsv_part;    // [6][blocks] per-block partials (preferred-node key, max raw, max key, max ds raw,
+                                // max taint count, max affinity sum)
+  // TaintToleration / NodeAffinity / NodeResourcesBalancedAllocation (exact pass)
+  bool def_on = false, def_score = false;
+  DefParams DF{};
+  DevBuf<NodePred> npred;       // [cap] kg_node_predicates
+  DevBuf<DefPod> defpods;       // [staged + kMaxB]
+  DevBuf<uint32_t> rsv_val2;    // [cap] raw taint count << 24 | raw affinity sum (their Scores on)
   // live kernel timing (kg_profile_enable): HIP event pairs around every launch of the round runners, on the
   // launch's own stream, folded into per-kind totals after each batch synchronises
   bool prof_on = false;
@@ -2176,6 +2190,11 @@ int validate_config(const kg_config* c) {
   if (c->la_agg_usage_type < KG_AGG_NONE || c->la_agg_usage_type > KG_AGG_P99 || c->la_agg_score_type < KG_AGG_NONE ||
       c->la_agg_score_type > KG_AGG_P99 || c->la_agg_usage_duration_ns < 0 || c->la_agg_score_duration_ns < 0)
     return fail(KG_E_INVALID, "LoadAwareSchedulingArgs.Aggregated: aggregation type / duration");
+  if (c->weight_taint < 0 || c->weight_taint > 1000000 || c->weight_affinity < 0 || c->weight_affinity > 1000000 ||
+      c->weight_balanced < 0 || c->weight_balanced > 1000000)
+    return fail(KG_E_INVALID, "TaintToleration / NodeAffinity / NodeResourcesBalancedAllocation weight out of range");
+  if (c->balanced_score && (c->balanced_resources & ~3ll))
+    return fail(KG_E_UNSUPPORTED, "NodeResourcesBalancedAllocation resources: cpu / memory are accelerated");
   if (c->reservation_filter || c->reservation_score) {
     if (c->weight_reservation < 0 || c->weight_reservation > 1000000) return fail(KG_E_INVALID, "Reservation weight out of range");
   }
@@ -2480,6 +2499,28 @@ int decode_node_numa(const kg_node_numa& n, NumaStatic& s, NumaMut& m) {
 // DeviceShare preFilterState for the GPU type: GetPodDeviceRequests (deviceshare/utils.go:232-252) =
 // RemoveZeros → Mask(GPU names) → ValidateDeviceRequest (:158-179, percentage units :151-156) →
 // ConvertDeviceRequest (:181-192 with the mapper table :92-149).
+// TaintToleration / NodeAffinity view of one pod (k: its index, for the error)
+int decode_def_pod(const kg_pod& p, DefPod& d, int64_t k) {
+  d = DefPod{};
+  if (p.n_required_terms < 0 || p.n_required_terms > kAffTerms || p.n_preferred_terms < 0 ||
+      p.n_preferred_terms > kAffTerms)
+    return fail(KG_E_UNSUPPORTED, "pod %lld: more than %d node affinity terms (the pod stays on the Go path)",
+                (long long)k, kAffTerms);
+  d.tol = p.tolerated_taints;
+  d.sel = p.node_selector;
+  d.nreq = (int32_t)p.n_required_terms;
+  d.npref = (int32_t)p.n_preferred_terms;
+  for (int t = 0; t < kAffTerms; ++t) {
+    d.req[t] = t < d.nreq ? p.required_terms[t] : 0;
+    d.pref[t] = t < d.npref ? p.preferred_terms[t] : 0;
+    if (t < d.npref && (p.preferred_weights[t] < 0 || p.preferred_weights[t] > 100))
+      return fail(KG_E_INVALID, "pod %lld: preferred term weight %lld outside [0, 100]", (long long)k,
+                  (long long)p.preferred_weights[t]);
+    d.w[t] = t < d.npref ? (int32_t)p.preferred_weights[t] : 0;
+  }
+  return 0;
+}
+
 int decode_ds_pod(const kg_pod& p, DsPod& d) {
   std::memset(&d, 0, sizeof(d));
   const int64_t* q = p.device_requests;
@@ -3105,6 +3146,10 @@ RsvExt rsv_ext(kg_engine* e) {
   X.out_cpus = e->numa_on ? e->out_cpus.p : nullptr;
   X.out_nrec = e->numa_on ? e->out_nrec.p : nullptr;
   X.paux = e->paux.p;
+  X.pred = e->def_on ? e->npred.p : nullptr;
+  X.defp = e->def_on ? e->defpods.p : nullptr;
+  X.DF = e->DF;
+  X.val2 = e->def_score ? e->rsv_val2.p : nullptr;
   return X;
 }
 
@@ -3254,6 +3299,7 @@ int64_t kg_abi_struct_size(int which) {
     case 7: return sizeof(kg_quota);
     case 8: return sizeof(kg_node_reservations);
     case 9: return sizeof(kg_pod_metric);
+    case 10: return sizeof(kg_node_predicates);
   }
   return -1;
 }
@@ -3390,9 +3436,22 @@ static int engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank,
   e->numa_on = c.numa_filter || c.numa_score;
   e->ds_on = c.ds_filter || c.ds_score;
   e->rsv_on = c.reservation_filter || c.reservation_score;
-  e->exact_on = e->rsv_on || (e->numa_on && e->ds_on);
+  e->def_on = c.taint_filter || c.taint_score || c.affinity_filter || c.affinity_score || c.balanced_score;
+  e->def_score = c.taint_score || c.affinity_score;
+  e->exact_on = e->rsv_on || (e->numa_on && e->ds_on) || e->def_on;
   if (e->exact_on && n_ranks > 1)
-    return bail(fail(KG_E_UNSUPPORTED, "Reservation / NodeNUMAResource + DeviceShare profiles run on one rank"));
+    return bail(fail(KG_E_UNSUPPORTED, "Reservation / NodeNUMAResource + DeviceShare / TaintToleration / NodeAffinity / "
+                                       "BalancedAllocation profiles run on one rank"));
+  e->DF = DefParams{(int32_t)(c.taint_filter != 0), (int32_t)(c.taint_score != 0), (int32_t)c.weight_taint,
+                    (int32_t)(c.affinity_filter != 0), (int32_t)(c.affinity_score != 0), (int32_t)c.weight_affinity,
+                    (int32_t)(c.balanced_score != 0), (int32_t)c.weight_balanced,
+                    (int32_t)(c.balanced_resources & 1), (int32_t)((c.balanced_resources >> 1) & 1)};
+  if (e->def_on) {
+    if (int rc = e->npred.ensure(cap)) return bail(rc);
+    if (hipMemset(e->npred.p, 0, cap * sizeof(NodePred)) != hipSuccess) return bail(fail(KG_E_DEVICE, "hipMemset"));
+    if (e->def_score)
+      if (int rc = e->rsv_val2.ensure(cap)) return bail(rc);
+  }
   e->RP.filter = (int32_t)(c.reservation_filter != 0);
   e->RP.score = (int32_t)(c.reservation_score != 0);
   e->RP.weight = (int32_t)c.weight_reservation;
@@ -3403,13 +3462,15 @@ static int engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank,
     if (int rc = e->rsv_nd.ensure(cap)) return bail(rc);
     if (int rc = e->rsv_val.ensure(cap)) return bail(rc);
     if (int rc = e->rsv_ws.ensure(8)) return bail(rc);
-    if (int rc = e->rsv_part.ensure(4 * ((cap + kRsvThreads - 1) / kRsvThreads) + 4)) return bail(rc);
+    if (int rc = e->rsv_part.ensure(6 * ((cap + kRsvThreads - 1) / kRsvThreads) + 4)) return bail(rc);
     if (hipMemset(e->rsv_nd.p, 0, cap * 4) != hipSuccess || hipMemset(e->rsv_ws.p, 0, 64) != hipSuccess)
       return bail(fail(KG_E_DEVICE, "hipMemset"));
   }
   const int64_t max_total = 100 * ((c.fit_score ? c.weight_fit : 0) + (c.la_score ? c.weight_loadaware : 0) +
                                    (c.numa_score ? c.weight_numa : 0) + (c.ds_score ? c.weight_deviceshare : 0) +
-                                   (c.reservation_score ? c.weight_reservation : 0));
+                                   (c.reservation_score ? c.weight_reservation : 0) +
+                                   (c.taint_score ? c.weight_taint : 0) + (c.affinity_score ? c.weight_affinity : 0) +
+                                   (c.balanced_score ? c.weight_balanced : 0));
   e->P.score_bits = (int32_t)bits_for(max_total);
   // NodeResourcesFit + LoadAwareScheduling: assume only lowers a node's key; NodeNUMAResource does not
   e->P.monotone = (e->numa_on || e->ds_on || e->rsv_on) ? 0 : 1;  // DeviceShare: normalization couples every node's key
@@ -3579,6 +3640,9 @@ void kg_engine_destroy(kg_engine* e) {
   e->rsv_exec = nullptr;
   e->rsv_ws.release();
   e->rsv_part.release();
+  e->npred.release();
+  e->defpods.release();
+  e->rsv_val2.release();
   e->scratch64.release();
   e->scratch32.release();
   e->uidx.release();
@@ -3805,6 +3869,13 @@ int kg_pods_stage(kg_engine* e, const kg_pod* pods, int64_t n) {
         if (pods[k].device_requests[r] != 0 && e->cfg.fit_filter)
           return fail(KG_E_UNSUPPORTED, "pod %lld requests devices; the profile has no DeviceShare (NodeResourcesFit on "
                       "device resources is not accelerated)", (long long)k);
+  }
+  if (e->def_on) {  // TaintToleration / NodeAffinity view of the pods
+    std::vector<DefPod> hf(std::max<int64_t>(n, 1));
+    for (int64_t k = 0; k < n; ++k)
+      if (int rc = decode_def_pod(pods[k], hf[k], k)) return rc;
+    if (int rc = e->defpods.ensure(n + kMaxB)) return rc;
+    if (n > 0) HIP_TRY(hipMemcpyAsync(e->defpods.p, hf.data(), n * sizeof(DefPod), hipMemcpyHostToDevice, e->stream));
   }
   {  // exact-pass records (the Reservation view of every pod; single-pod calls of any profile use the pass)
     std::vector<RsvPod> hr(std::max<int64_t>(n, 1));
@@ -4433,6 +4504,25 @@ int kg_debug_fast_lrs(kg_engine* e, const int64_t* req, const int64_t* cap, int6
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpyAsync(out_cpu, b.p + 2 * n, n * 8, hipMemcpyDeviceToHost, e->stream));
   HIP_TRY(hipMemcpyAsync(out_mem, b.p + 3 * n, n * 8, hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  b.release();
+  return 0;
+}
+
+int kg_nodes_predicates_upsert(kg_engine* e, const kg_node_predicates* p, const int32_t* idx, int64_t n) {
+  if (!e || (n > 0 && (!p || !idx))) return fail(KG_E_INVALID, "null argument");
+  if (!e->def_on) return fail(KG_E_INVALID, "the profile enables none of TaintToleration / NodeAffinity / BalancedAllocation");
+  if (n == 0) return 0;
+  for (int64_t k = 0; k < n; ++k)
+    if (idx[k] < 0 || idx[k] >= e->capacity) return fail(KG_E_INVALID, "node index %d outside capacity", idx[k]);
+  DevBuf<uint8_t> b;
+  if (int rc = b.ensure(n * (sizeof(NodePred) + 4))) return rc;
+  NodePred* dp = reinterpret_cast<NodePred*>(b.p);
+  int32_t* di = reinterpret_cast<int32_t*>(b.p + n * sizeof(NodePred));
+  HIP_TRY(hipMemcpyAsync(dp, p, n * sizeof(NodePred), hipMemcpyHostToDevice, e->stream));
+  HIP_TRY(hipMemcpyAsync(di, idx, n * 4, hipMemcpyHostToDevice, e->stream));
+  scatter_rows<NodePred><<<(unsigned)((n + 255) / 256), 256, 0, e->stream>>>(e->npred.p, dp, di, n);
+  HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(e->stream));
   b.release();
   return 0;

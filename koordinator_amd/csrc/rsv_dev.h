@@ -27,6 +27,7 @@
 #include <stdint.h>
 
 #include "../../include/koordgpu.h"
+#include "defaults_dev.h"
 #include "ds_dev.h"
 #include "kernels.h"
 #include "numa_dev.h"
@@ -75,6 +76,11 @@ struct RsvExt {
   int64_t* __restrict__ out_nrec;      // [pods][kNumaRecWords] the pod's NUMA allocation record
   // NodeResourcesFit over ephemeral-storage / scalar resources (P_AUX pods): [pods][kAux] requests
   const int64_t* __restrict__ paux;
+  // TaintToleration / NodeAffinity / NodeResourcesBalancedAllocation (defp = nullptr: none in the profile)
+  const NodePred* __restrict__ pred;   // [cap]
+  const DefPod* __restrict__ defp;     // [pods]
+  DefParams DF;
+  uint32_t* __restrict__ val2;         // [cap] raw TaintToleration count << 24 | raw NodeAffinity sum (scores on)
 };
 
 struct RsvOut {
@@ -84,6 +90,8 @@ struct RsvOut {
   int32_t nom;    // nominated slot, -1 = none
   int32_t order;  // findMostPreferredReservationByOrder over matched (INT32_MAX = none)
   int32_t dsraw;  // DeviceShare raw Score
+  int32_t tcnt;   // TaintToleration raw Score (intolerable PreferNoSchedule taints)
+  int32_t asum;   // NodeAffinity raw Score
 };
 
 __device__ __forceinline__ int64_t rsv_nn(int64_t a, int64_t b) { return a - b > 0 ? a - b : 0; }
@@ -122,10 +130,16 @@ __device__ __forceinline__ RsvOut rsv_eval_node(const DevTable& T, const RsvNode
                                                 const int32_t* __restrict__ rsv_n, int64_t i, const DevPod& p,
                                                 const RsvPod& rp, const EvalParams& P, const RsvParams& RP,
                                                 const RsvExt& X, const DsPod* dp, const NumaPod* np = nullptr,
-                                                RsvDbg* dbg = nullptr, const int64_t* aux_req = nullptr) {
+                                                RsvDbg* dbg = nullptr, const int64_t* aux_req = nullptr,
+                                                const DefPod* df = nullptr) {
+  RsvOut o{false, 0, 0, -1, 0x7fffffff, 0, 0, 0};
+  NodePred npd{0, 0, 0};
+  if (df) {  // TaintToleration / NodeAffinity Filter: node-static, so first
+    npd = X.pred[i];
+    if (!dbg && !defaults_filter(npd, *df, X.DF)) return o;
+  }
   Row r = load_row(T, i);
   const int ns = rsv_n[i];
-  RsvOut o{false, 0, 0, -1, 0x7fffffff, 0};
   uint32_t mm = 0;  // matched slots
   int nm = 0;
   int64_t pr_c = 0, pr_m = 0, ra_c = 0, ra_m = 0;
@@ -183,6 +197,7 @@ __device__ __forceinline__ RsvOut rsv_eval_node(const DevTable& T, const RsvNode
     dbg->num_pods = r.num_pods;
     dbg->pod_req_cpu = has_state ? pr_c : 0, dbg->pod_req_mem = has_state ? pr_m : 0;
   }
+  if (dbg && df && !defaults_filter(npd, *df, X.DF)) return o;
   int64_t t = 0;
   if (!eval_node(r, p, P, t)) return o;  // NodeResourcesFit + LoadAware on the restored NodeInfo
   // fitsRequest over ephemeral-storage and the scalar resources the pod requests (reservation/plugin.go:469-479)
@@ -220,6 +235,11 @@ __device__ __forceinline__ RsvOut rsv_eval_node(const DevTable& T, const RsvNode
     if (!numa_eval(nv, *np, X.NP, r.req_cpu, r.req_mem, r.alloc_cpu, r.alloc_mem, sc, aff)) return o;
     if (X.NP.score) t += sc * X.NP.weight;
     if (X.aff) X.aff[i] = aff.nil ? 0x100u : aff.mask;
+  }
+  if (df) {  // BalancedAllocation on the restored NodeInfo; the two normalised raw Scores
+    if (X.DF.bal) t += X.DF.w_bal * balanced_score(r.alloc_cpu, r.alloc_mem, r.req_cpu, r.req_mem, p.req_cpu, p.req_mem, X.DF);
+    o.tcnt = X.DF.taint_score ? taint_raw(npd, *df) : 0;
+    o.asum = X.DF.aff_score ? affinity_raw(npd, *df) : 0;
   }
   o.feas = true;
   o.base = t;
@@ -456,34 +476,46 @@ __global__ __launch_bounds__(kRsvThreads) void rsv_eval(DevTable T, RsvNode* __r
     }
     s_admit = ok;
   }
-  uint64_t pk = 0, rawv = 0, dsv = 0;
+  uint64_t pk = 0, rawv = 0, dsv = 0, tv = 0, av = 0;
   uint64_t v = 0;
   if (i < n) {
     const RsvPod rp = rpods[j];
     const DsPod* dp = X.ds ? &X.dpods[j] : nullptr;
     const NumaPod* np = X.ns ? &X.npods[j] : nullptr;
     const int64_t* aux = (X.paux && (p.flags & P_AUX)) ? X.paux + (size_t)j * kAux : nullptr;
-    const RsvOut o = rsv_eval_node(T, RN, rsv_n, i, p, rp, P, RP, X, dp, np, nullptr, aux);
+    const DefPod* df = X.defp ? &X.defp[j] : nullptr;
+    const RsvOut o = rsv_eval_node(T, RN, rsv_n, i, p, rp, P, RP, X, dp, np, nullptr, aux, df);
     if (o.feas) {
       v = ((uint64_t)(uint32_t)o.base << 32) | ((uint64_t)(uint32_t)o.dsraw << 16) |
           ((uint64_t)(uint32_t)o.raw << 8) | (1ull << 7) | (uint64_t)(o.nom + 1);
       if (o.order != 0x7fffffff) pk = ~(((uint64_t)(uint32_t)o.order << 32) | (uint64_t)(uint32_t)i);
       rawv = (uint64_t)(uint32_t)o.raw;
       dsv = (uint64_t)(uint32_t)o.dsraw;
+      tv = (uint64_t)(uint32_t)o.tcnt;
+      av = (uint64_t)(uint32_t)o.asum;
     }
   }
   __syncthreads();
-  if (!s_admit) v = 0, pk = 0, rawv = 0, dsv = 0;  // PreFilter Unschedulable: no node is feasible
+  if (!s_admit) v = 0, pk = 0, rawv = 0, dsv = 0, tv = 0, av = 0;  // PreFilter Unschedulable: no node is feasible
   if (i < n) val[i] = v;
+  const bool dscore = X.val2 != nullptr;  // TaintToleration / NodeAffinity Score in the profile
+  if (dscore && i < n) X.val2[i] = (uint32_t)(tv << 24 | av);
   pk = rsv_block_max(pk, s_red);
   __syncthreads();
   rawv = rsv_block_max(rawv, s_red);
   __syncthreads();
   dsv = rsv_block_max(dsv, s_red);
+  if (dscore) {
+    __syncthreads();
+    tv = rsv_block_max(tv, s_red);
+    __syncthreads();
+    av = rsv_block_max(av, s_red);
+  }
   if (threadIdx.x == 0) {
     part[blockIdx.x] = pk;
     part[nb + blockIdx.x] = rawv;
     part[3 * nb + blockIdx.x] = dsv;
+    if (dscore) part[4 * nb + blockIdx.x] = tv, part[5 * nb + blockIdx.x] = av;
   }
 }
 
@@ -503,6 +535,8 @@ __global__ __launch_bounds__(kRsvThreads) void rsv_select(const uint64_t* __rest
   const uint64_t pk = rsv_partials_max(part, nb);
   const uint64_t mraw = rsv_partials_max(part + nb, nb);
   const uint64_t mds = X.ds ? rsv_partials_max(part + 3 * nb, nb) : 0;
+  const int64_t mt = X.val2 ? (int64_t)rsv_partials_max(part + 4 * nb, nb) : 0;
+  const int64_t ma = X.val2 ? (int64_t)rsv_partials_max(part + 5 * nb, nb) : 0;
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t pref = pk ? (int64_t)(uint32_t)(~pk) : -1;
   const int64_t mx = pk ? (mraw > 1000 ? (int64_t)mraw : 1000) : (int64_t)mraw;
@@ -514,6 +548,11 @@ __global__ __launch_bounds__(kRsvThreads) void rsv_select(const uint64_t* __rest
       int64_t t = (int64_t)(v >> 32);
       if (RP.score && mx > 0) t += (int64_t)RP.weight * (100 * raw / mx);
       if (X.DP.score && mds > 0) t += (int64_t)X.DP.weight * (100 * (int64_t)((v >> 16) & 0xff) / (int64_t)mds);
+      if (X.val2) {
+        const uint32_t v2 = X.val2[i];
+        if (X.DF.taint_score) t += (int64_t)X.DF.w_taint * normalize_default(v2 >> 24, mt, true);
+        if (X.DF.aff_score) t += (int64_t)X.DF.w_aff * normalize_default(v2 & 0xFFFFFFu, ma, false);
+      }
       key = make_key(t, (uint32_t)i);
     }
   }

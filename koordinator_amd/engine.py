@@ -152,6 +152,13 @@ class Engine:
         idx = self._idx(idx, len(node_rsv))
         check(self.lib, self.lib.kg_nodes_reservation_upsert(self.h, ptr(node_rsv), ptr(idx), len(node_rsv)))
 
+    def upsert_predicates(self, preds: np.ndarray, idx=None):
+        """TaintToleration / NodeAffinity node rows of nodes `idx` (kg_nodes_predicates_upsert; NODE_PRED_DTYPE, see
+        koordinator_amd/predicates.py)."""
+        preds = np.ascontiguousarray(preds, dtype=abi.NODE_PRED_DTYPE)
+        idx = self._idx(idx, len(preds))
+        check(self.lib, self.lib.kg_nodes_predicates_upsert(self.h, ptr(preds), ptr(idx), len(preds)))
+
     def read_reservations(self):
         """(allocated cpu, allocated memory, assigned), int64[n, KG_MAX_RSV_SLOTS] each, from the device."""
         n = self.num_nodes

@@ -29,6 +29,9 @@ SUCCESS, UNSCHEDULABLE = "Success", "Unschedulable"
 NODE_RESOURCES_FIT, LOAD_AWARE, NODE_NUMA_RESOURCE = "NodeResourcesFit", "LoadAwareScheduling", "NodeNUMAResource"
 DEVICE_SHARE = "DeviceShare"
 RESERVATION = "Reservation"
+# upstream default plugins a stock profile keeps (k8s v1.24.15 v1beta2 defaults: Score weight 1 each)
+TAINT_TOLERATION, NODE_AFFINITY = "TaintToleration", "NodeAffinity"
+BALANCED_ALLOCATION = "NodeResourcesBalancedAllocation"
 
 
 def _slots(d: dict | None, absent=0) -> np.ndarray:
@@ -85,7 +88,10 @@ class Profile:
 def build_config(la: LoadAwareSchedulingArgs | None = None, fit: NodeResourcesFitArgs | None = None,
                  profile: Profile | None = None, batch_pods: int = 32, pods_per_wave: int = 8,
                  device_id: int = -1, numa: NodeNUMAResourceArgs | None = None,
-                 deviceshare: DeviceShareArgs | None = None, pipeline_depth: int = 0) -> np.ndarray:
+                 deviceshare: DeviceShareArgs | None = None, pipeline_depth: int = 0,
+                 balanced_resources: tuple = ("cpu", "memory")) -> np.ndarray:
+    """kg_config of a profile.  balanced_resources: NodeResourcesBalancedAllocationArgs.resources (v1beta2 default
+    cpu + memory, weight 1 each; the weights do not enter the two-resource std)."""
     la = la or LoadAwareSchedulingArgs()
     fit = fit or NodeResourcesFitArgs()
     profile = profile or Profile()
@@ -133,6 +139,15 @@ def build_config(la: LoadAwareSchedulingArgs | None = None, fit: NodeResourcesFi
     r["reservation_filter"] = int(RESERVATION in profile.filter)
     r["reservation_score"] = int(RESERVATION in profile.score)
     r["weight_reservation"] = int(profile.score.get(RESERVATION, 0))
+    r["taint_filter"] = int(TAINT_TOLERATION in profile.filter)
+    r["taint_score"] = int(TAINT_TOLERATION in profile.score)
+    r["weight_taint"] = int(profile.score.get(TAINT_TOLERATION, 0))
+    r["affinity_filter"] = int(NODE_AFFINITY in profile.filter)
+    r["affinity_score"] = int(NODE_AFFINITY in profile.score)
+    r["weight_affinity"] = int(profile.score.get(NODE_AFFINITY, 0))
+    r["balanced_score"] = int(BALANCED_ALLOCATION in profile.score)
+    r["weight_balanced"] = int(profile.score.get(BALANCED_ALLOCATION, 0))
+    r["balanced_resources"] = sum({"cpu": 1, "memory": 2}.get(k, 1 << 8) for k in balanced_resources)
     r["ds_scoring_strategy"] = abi.STRATEGY[ds.scoring_strategy]
     r["ds_scoring_weights"] = [ds.scoring_resources.get("koordinator.sh/gpu-core", 0),
                                ds.scoring_resources.get("koordinator.sh/gpu-memory", 0),

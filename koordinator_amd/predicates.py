@@ -1,0 +1,169 @@
+"""Host-side compiler of node labels / taints and pod tolerations / node affinity into the engine's bitmasks
+(kg_node_predicates and the kg_pod TaintToleration / NodeAffinity fields, ABI 8).
+
+The Go shim keeps two dense tables per scheduler: the distinct taints (key, value, effect) of the cluster's nodes
+and the distinct node-selector predicates the queued pods use — a NodeSelectorRequirement (key, operator, values),
+a MatchFields requirement on metadata.name, or one pod.Spec.NodeSelector key=value pair.  Each node row holds
+which predicates hold on the node's labels and which taints it carries; each pod holds which taints its
+tolerations tolerate and its terms as predicate masks.  The device then evaluates the plugins as bit arithmetic
+(koordinator_amd/csrc/defaults_dev.h).
+
+Matching restates upstream semantics (k8s.io/kubernetes v1.24.15, k8s.io/component-helpers v0.24.15 — neither
+vendored in the reference):
+* Toleration.ToleratesTaint (core/v1/toleration.go): an effect, if set, must equal the taint's; a key, if set, must
+  equal the taint's; operator Exists tolerates any value, Equal (or empty) needs the same value.
+* nodeaffinity.NodeSelector (component-helpers/scheduling/corev1/nodeaffinity): terms are ORed, requirements of a
+  term ANDed, a term with no requirements matches nothing; label operators In / NotIn / Exists / DoesNotExist /
+  Gt / Lt (labels.Requirement.Matches: NotIn and DoesNotExist hold when the key is absent, Gt / Lt parse both sides
+  as int64 and fail on a parse error); MatchFields only on metadata.name with In / NotIn.
+* pod.Spec.NodeSelector: labels.SelectorFromSet — every key present with the same value.
+A requirement that does not parse (unknown operator, Gt / Lt without exactly one integer value, a field other than
+metadata.name) makes its term fail to match — the lazy-error selector skips such terms — so it compiles to a
+predicate that holds on no node.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import abi
+
+NO_SCHEDULE, PREFER_NO_SCHEDULE, NO_EXECUTE = "NoSchedule", "PreferNoSchedule", "NoExecute"
+MAX_IDS = 64
+
+
+def _parse_int(s):
+    try:
+        return int(s, 10)
+    except (TypeError, ValueError):
+        return None
+
+
+class PredicateTable:
+    """The caller's taint and predicate id tables (at most 64 each)."""
+
+    def __init__(self):
+        self.taints: list[tuple] = []
+        self.preds: list[tuple] = []
+        self._taint_id: dict = {}
+        self._pred_id: dict = {}
+
+    # ---- interning ----
+    def taint_id(self, key: str, value: str, effect: str) -> int:
+        t = (key, value or "", effect)
+        if t not in self._taint_id:
+            if len(self.taints) == MAX_IDS:
+                raise OverflowError("more than 64 distinct taints: the pods stay on the Go path")
+            self._taint_id[t] = len(self.taints)
+            self.taints.append(t)
+        return self._taint_id[t]
+
+    def pred_id(self, kind: str, key: str, op: str, values=()) -> int:
+        p = (kind, key, op, tuple(values or ()))
+        if p not in self._pred_id:
+            if len(self.preds) == MAX_IDS:
+                raise OverflowError("more than 64 distinct node-selector predicates: the pods stay on the Go path")
+            self._pred_id[p] = len(self.preds)
+            self.preds.append(p)
+        return self._pred_id[p]
+
+    # ---- predicate evaluation (per node update) ----
+    @staticmethod
+    def _holds(pred, labels: dict, name: str) -> bool:
+        kind, key, op, values = pred
+        if kind == "field":
+            if key != "metadata.name" or op not in ("In", "NotIn"):
+                return False
+            return (name in values) == (op == "In")
+        has = key in labels
+        v = labels.get(key)
+        if op == "In":
+            return has and v in values
+        if op == "NotIn":
+            return not has or v not in values
+        if op == "Exists":
+            return has
+        if op == "DoesNotExist":
+            return not has
+        if op in ("Gt", "Lt"):
+            if not has or len(values) != 1:
+                return False
+            a, b = _parse_int(v), _parse_int(values[0])
+            if a is None or b is None:
+                return False
+            return a > b if op == "Gt" else a < b
+        return False  # unknown operator: the term never matches
+
+    def node_row(self, labels: dict | None = None, taints: list | None = None, name: str = "") -> np.ndarray:
+        """kg_node_predicates of one node: labels {key: value}, taints [{key, value, effect}]."""
+        labels = labels or {}
+        r = np.zeros(1, dtype=abi.NODE_PRED_DTYPE)
+        m = 0
+        for k, pr in enumerate(self.preds):
+            if self._holds(pr, labels, name):
+                m |= 1 << k
+        hard = soft = 0
+        for t in taints or ():
+            eff = t["effect"]
+            bit = 1 << self.taint_id(t["key"], t.get("value", ""), eff)
+            if eff == PREFER_NO_SCHEDULE:
+                soft |= bit
+            elif eff in (NO_SCHEDULE, NO_EXECUTE):
+                hard |= bit
+        r["predicates"], r["taints_hard"], r["taints_soft"] = m, hard, soft
+        return r
+
+    # ---- pods (per staging: evaluated against the taints interned so far) ----
+    @staticmethod
+    def tolerates(tol: dict, taint: tuple) -> bool:
+        key, value, effect = taint
+        if tol.get("effect") and tol["effect"] != effect:
+            return False
+        if tol.get("key") and tol["key"] != key:
+            return False
+        op = tol.get("operator") or "Equal"
+        if op == "Exists":
+            return True
+        if op == "Equal":
+            return (tol.get("value") or "") == value
+        return False
+
+    def _term_mask(self, term: dict) -> int:
+        m = 0
+        for req in term.get("matchExpressions") or ():
+            m |= 1 << self.pred_id("label", req["key"], req["operator"], req.get("values"))
+        for req in term.get("matchFields") or ():
+            m |= 1 << self.pred_id("field", req["key"], req["operator"], req.get("values"))
+        return m
+
+    def fill_pod(self, pod: np.ndarray, tolerations=None, node_selector: dict | None = None,
+                 required_terms: list | None = None, preferred: list | None = None) -> np.ndarray:
+        """Fills one kg_pod row's TaintToleration / NodeAffinity fields (in place; returns it).
+        required_terms: the NodeSelectorTerms of requiredDuringScheduling (None = not set; [] = set with no terms,
+        which matches no node); preferred: [(weight, term)]."""
+        row = pod[0] if pod.shape else pod
+        tol = 0
+        for t_id, taint in enumerate(self.taints):
+            if any(self.tolerates(t, taint) for t in tolerations or ()):
+                tol |= 1 << t_id
+        sel = 0
+        for k, v in (node_selector or {}).items():
+            sel |= 1 << self.pred_id("label", k, "In", (v,))
+        row["tolerated_taints"] = tol
+        row["node_selector"] = sel
+        if required_terms is not None:
+            if len(required_terms) > abi.MAX_AFF_TERMS:
+                raise OverflowError("more than 4 required terms: the pod stays on the Go path")
+            terms = [self._term_mask(t) for t in required_terms] or [0]  # no terms: one never-matching term
+            row["n_required_terms"] = len(terms)
+            row["required_terms"][:] = 0
+            row["required_terms"][:len(terms)] = terms
+        pref = preferred or []
+        if len(pref) > abi.MAX_AFF_TERMS:
+            raise OverflowError("more than 4 preferred terms: the pod stays on the Go path")
+        row["n_preferred_terms"] = len(pref)
+        row["preferred_terms"][:] = 0
+        row["preferred_weights"][:] = 0
+        for k, (w, term) in enumerate(pref):
+            row["preferred_terms"][k] = self._term_mask(term)
+            row["preferred_weights"][k] = w
+        return pod

@@ -486,3 +486,66 @@ def load_shipped_into(engine, cluster: Cluster, numa: np.ndarray, dev: np.ndarra
     engine.upsert_reservations(rsv)
     if quotas is not None:
         engine.set_quotas(quotas)
+
+
+def make_predicates(n_nodes: int, pods: np.ndarray, seed: int = BASE_SEED + 15) -> tuple:
+    """Node labels / taints and pod tolerations / nodeSelector / node affinity for TaintToleration + NodeAffinity
+    (compiled through koordinator_amd.predicates).  Fills `pods` in place; returns (table, NODE_PRED_DTYPE[n_nodes])."""
+    from .predicates import PredicateTable, NO_SCHEDULE, NO_EXECUTE, PREFER_NO_SCHEDULE
+    rng = np.random.default_rng(seed)
+    zones, pools = ["z0", "z1", "z2", "z3"], ["general", "compute", "memory"]
+    labels, taints = [], []
+    for i in range(n_nodes):
+        lb = {"topology.kubernetes.io/zone": zones[rng.integers(4)], "pool": pools[rng.integers(3)],
+              "rack": str(int(rng.integers(20)))}
+        if rng.random() < 0.3:
+            lb["ssd"] = "true"
+        labels.append(lb)
+        ts = []
+        u = rng.random()
+        if u < 0.12:
+            ts.append({"key": "dedicated", "value": ["infra", "batch"][rng.integers(2)], "effect": NO_SCHEDULE})
+        elif u < 0.16:
+            ts.append({"key": "maintenance", "value": "", "effect": NO_EXECUTE})
+        for k in ("spot", "noisy", "legacy"):
+            if rng.random() < 0.2:
+                ts.append({"key": k, "value": "true", "effect": PREFER_NO_SCHEDULE})
+        taints.append(ts)
+    table = PredicateTable()
+    for ts in taints:  # intern the cluster's taints first: pods' tolerated masks cover them
+        for t in ts:
+            table.taint_id(t["key"], t.get("value", ""), t["effect"])
+    expr = lambda k, op, v=None: {"key": k, "operator": op, **({"values": v} if v is not None else {})}
+    for j in range(len(pods)):
+        tol = []
+        u = rng.random()
+        if u < 0.15:
+            tol.append({"key": "dedicated", "operator": "Equal", "value": "batch", "effect": NO_SCHEDULE})
+        elif u < 0.2:
+            tol.append({"operator": "Exists"})  # tolerates everything
+        if rng.random() < 0.4:
+            tol.append({"key": ["spot", "noisy", "legacy"][rng.integers(3)], "operator": "Exists"})
+        sel = {"pool": pools[rng.integers(3)]} if rng.random() < 0.2 else None
+        req = None
+        u = rng.random()
+        if u < 0.25:
+            req = [{"matchExpressions": [expr("topology.kubernetes.io/zone", "In", list(rng.choice(zones, 2,
+                                                                                                  replace=False)))]}]
+            if rng.random() < 0.5:
+                req.append({"matchExpressions": [expr("rack", "Gt", [["4", "9", "14"][rng.integers(3)]]),
+                                                 expr("ssd", "Exists")]})
+        elif u < 0.3:
+            req = [{"matchExpressions": [expr("pool", "NotIn", ["memory"]), expr("ssd", "DoesNotExist")]}]
+        pref = []
+        if rng.random() < 0.5:
+            for _ in range(int(rng.integers(1, 4))):
+                c = rng.integers(4)
+                term = ({"matchExpressions": [expr("ssd", "Exists")]} if c == 0 else
+                        {"matchExpressions": [expr("topology.kubernetes.io/zone", "In", [zones[rng.integers(4)]])]}
+                        if c == 1 else
+                        {"matchExpressions": [expr("rack", "Lt", [["5", "10", "15"][rng.integers(3)]])]} if c == 2 else
+                        {"matchExpressions": [expr("pool", "In", ["compute"]), expr("ssd", "Exists")]})
+                pref.append((int(rng.integers(1, 101)), term))
+        table.fill_pod(pods[j:j + 1], tolerations=tol, node_selector=sel, required_terms=req, preferred=pref)
+    rows = np.concatenate([table.node_row(labels[i], taints[i], name=f"node-{i}") for i in range(n_nodes)])
+    return table, rows

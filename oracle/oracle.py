@@ -96,12 +96,20 @@ def lib():
         L.or_schedule_resv.argtypes = [vp, i64, vp, vp, vp, vp, i64, vp, i64, vp, vp, vp]
         L.or_schedule_resv.restype = i
         L.or_schedule_resv_full.argtypes = [vp, i64, vp, vp, vp, vp, vp, vp, i64, i64, vp, i64, i, vp, vp, vp, vp,
-                                            vp, vp, vp]
+                                            vp, vp, vp, vp]
         L.or_schedule_resv_full.restype = i
         L.or_quota_admit.argtypes = [vp, vp]
         L.or_quota_admit.restype = i
         L.or_rsv_case_flat.argtypes = [vp, i64, vp, i64, vp, vp, i, vp, vp]
         L.or_rsv_case_flat.restype = None
+        for f, res in (("or_taint_filter", i), ("or_taint_count", i64), ("or_affinity_filter", i),
+                       ("or_affinity_sum", i64)):
+            getattr(L, f).argtypes = [vp, vp]
+            getattr(L, f).restype = res
+        L.or_balanced_score.argtypes = [i64] * 7
+        L.or_balanced_score.restype = i64
+        L.or_normalize_default.argtypes = [i64, i64, i]
+        L.or_normalize_default.restype = i64
         _lib = L
     return _lib
 
@@ -180,9 +188,10 @@ p = abi.ptr
 
 
 def schedule_resv(cfg, nodes, metrics, st, rsv, pods, now_ns: int, devices=None, quotas=None, n_threads: int = 1,
-                  with_minors: bool = False, numa_buf=None, with_numa: bool = False):
+                  with_minors: bool = False, numa_buf=None, with_numa: bool = False, preds=None):
     """Sequential FIFO scheduling through the per-pod exact loop: NodeResourcesFit + LoadAware + Reservation
-    [+ DeviceShare + NodeNUMAResource + ElasticQuota] (st, rsv, devices, numa_buf, quotas mutated; the node loop of each
+    [+ DeviceShare + NodeNUMAResource + ElasticQuota + TaintToleration / NodeAffinity over `preds` (NODE_PRED_DTYPE
+    rows) + BalancedAllocation] (st, rsv, devices, numa_buf, quotas mutated; the node loop of each
     pod on n_threads threads).  Returns (node, score, slot) — slot = the reservation each pod was assumed into (-1 =
     none) — then, with_minors, DeviceShare's minor masks and, with_numa, the cpusets uint64[n, 4] and NUMA allocation
     records int64[n, NUMA_ALLOC_WORDS] NodeNUMAResource Reserve made."""
@@ -195,7 +204,8 @@ def schedule_resv(cfg, nodes, metrics, st, rsv, pods, now_ns: int, devices=None,
     nq = 0 if quotas is None else len(quotas)
     rc = lib().or_schedule_resv_full(p(cfg), len(nodes), p(nodes), p(metrics), p(st), p(rsv), p(devices), p(quotas),
                                      nq, len(pods), p(pods), now_ns, n_threads, p(out_node), p(out_score), p(out_slot),
-                                     p(out_minors), p(numa_buf), p(cpus), p(nalloc))
+                                     p(out_minors), p(numa_buf), p(cpus), p(nalloc),
+                                     p(None if preds is None else np.ascontiguousarray(preds, dtype=abi.NODE_PRED_DTYPE)))
     if rc != 0:
         raise RuntimeError(f"oracle or_schedule_resv_full failed: {rc}")
     out = (out_node[:len(pods)], out_score[:len(pods)], out_slot[:len(pods)])
@@ -430,3 +440,26 @@ def single_numa_filter(lists):
         raise RuntimeError("or_debug_single_numa_filter failed")
     return [[[None if oh[i, j, 0] else [b for b in range(8) if (int(oh[i, j, 1]) >> b) & 1], bool(oh[i, j, 2])]
              for j in range(oc[i])] for i in range(len(lists))]
+
+
+def _pred_pod(pred, pod):
+    n = np.ascontiguousarray(np.asarray(pred, dtype=abi.NODE_PRED_DTYPE).reshape(1))
+    q = np.ascontiguousarray(np.asarray(pod, dtype=abi.POD_DTYPE).reshape(1))
+    return n, q
+
+
+def default_plugins(pred, pod) -> dict:
+    """TaintToleration / NodeAffinity of one (node, pod) (oracle/defaults.c): filter verdicts and raw Scores."""
+    n, q = _pred_pod(pred, pod)
+    L = lib()
+    return {"taint_filter": bool(L.or_taint_filter(p(n), p(q))), "taint_count": int(L.or_taint_count(p(n), p(q))),
+            "affinity_filter": bool(L.or_affinity_filter(p(n), p(q))),
+            "affinity_sum": int(L.or_affinity_sum(p(n), p(q)))}
+
+
+def balanced_score(alloc_cpu, alloc_mem, req_cpu, req_mem, pod_cpu, pod_mem, resources=3) -> int:
+    return int(lib().or_balanced_score(alloc_cpu, alloc_mem, req_cpu, req_mem, pod_cpu, pod_mem, resources))
+
+
+def normalize_default(score, max_count, reverse) -> int:
+    return int(lib().or_normalize_default(score, max_count, int(bool(reverse))))

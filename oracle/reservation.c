@@ -4,6 +4,8 @@
  * (ResourceNames ⊆ {cpu, memory}: cpu-only and memory-only reservations).
  */
 #include "reservation.h"
+
+#include "defaults.h"
 #include "numa.h"
 
 #include <math.h>
@@ -214,14 +216,14 @@ int or_schedule_resv(const kg_config* cfg, int64_t n_nodes, const kg_node* nodes
                      or_node_state* st, kg_node_reservations* rsv, int64_t n_pods, const kg_pod* pods, int64_t now,
                      int32_t* out_node, int64_t* out_score, int32_t* out_slot) {
   return or_schedule_resv_full(cfg, n_nodes, nodes, metrics, st, rsv, NULL, NULL, 0, n_pods, pods, now, 1, out_node,
-                               out_score, out_slot, NULL, NULL, NULL, NULL);
+                               out_score, out_slot, NULL, NULL, NULL, NULL, NULL);
 }
 
 int or_schedule_resv_full(const kg_config* cfg, int64_t n_nodes, const kg_node* nodes, const kg_node_metric* metrics,
                           or_node_state* st, kg_node_reservations* rsv, kg_node_device* dev, kg_quota* quotas,
                           int64_t n_quotas, int64_t n_pods, const kg_pod* pods, int64_t now, int n_threads,
                           int32_t* out_node, int64_t* out_score, int32_t* out_slot, int32_t* out_minors,
-                          void* numa_states, uint64_t* out_cpus, int64_t* out_numa) {
+                          void* numa_states, uint64_t* out_cpus, int64_t* out_numa, const kg_node_predicates* preds) {
   const size_t nn = (size_t)(n_nodes > 0 ? n_nodes : 1);
   or_numa_node* numa = (or_numa_node*)numa_states;
   const int numa_on = numa && (cfg->numa_filter || cfg->numa_score);
@@ -233,10 +235,14 @@ int or_schedule_resv_full(const kg_config* cfg, int64_t n_nodes, const kg_node* 
   int64_t* dsraw = (int64_t*)malloc(nn * sizeof(int64_t));
   int64_t* order = (int64_t*)malloc(nn * sizeof(int64_t));
   int32_t* nom = (int32_t*)malloc(nn * sizeof(int32_t));
-  if (!feas || !base || !raw || !dsraw || !order || !nom) {
-    free(feas); free(base); free(raw); free(dsraw); free(order); free(nom); free(aff);
+  int64_t* tcnt = (int64_t*)calloc(nn, sizeof(int64_t));
+  int64_t* asum = (int64_t*)calloc(nn, sizeof(int64_t));
+  if (!feas || !base || !raw || !dsraw || !order || !nom || !tcnt || !asum) {
+    free(feas); free(base); free(raw); free(dsraw); free(order); free(nom); free(aff); free(tcnt); free(asum);
     return KG_E_NOMEM;
   }
+  /* TaintToleration / NodeAffinity / BalancedAllocation (defaults.c); a NULL table = no predicates, no taints */
+  const kg_node_predicates zero_pred = {0, 0, 0};
   const int rsv_on = cfg->reservation_filter || cfg->reservation_score;
   const int ds_on = dev && (cfg->ds_filter || cfg->ds_score);
   if (n_threads < 1) n_threads = 1;
@@ -281,6 +287,9 @@ int or_schedule_resv_full(const kg_config* cfg, int64_t n_nodes, const kg_node* 
       feas[i] = 0;
       const kg_node* nd = &nodes[i];
       if (!(nd->flags & KG_NODE_VALID)) continue;
+      const kg_node_predicates* np = preds ? &preds[i] : &zero_pred;
+      if (cfg->taint_filter && !or_taint_filter(np, pod)) continue;
+      if (cfg->affinity_filter && !or_affinity_filter(np, pod)) continue;
       or_rsv_node ns;
       or_rsv_restore(rsv_on ? &rsv[i] : NULL, &st[i], pod, &ns);
       or_node_state rs = st[i];
@@ -318,6 +327,13 @@ int or_schedule_resv_full(const kg_config* cfg, int64_t n_nodes, const kg_node* 
         t += cfg->weight_numa * or_numa_score(cfg, &numa[i], &npod, &aff[i], rs.requested[KG_RES_CPU],
                                               rs.requested[KG_RES_MEMORY], nd->allocatable[KG_RES_CPU],
                                               nd->allocatable[KG_RES_MEMORY]);
+      if (cfg->balanced_score)
+        t += cfg->weight_balanced * or_balanced_score(nd->allocatable[KG_RES_CPU], nd->allocatable[KG_RES_MEMORY],
+                                                      rs.requested[KG_RES_CPU], rs.requested[KG_RES_MEMORY],
+                                                      pod->requests[KG_RES_CPU], pod->requests[KG_RES_MEMORY],
+                                                      cfg->balanced_resources);
+      tcnt[i] = cfg->taint_score ? or_taint_count(np, pod) : 0;
+      asum[i] = cfg->affinity_score ? or_affinity_sum(np, pod) : 0;
       base[i] = t;
       nom[i] = (rsv_on && !ds_blocks_nomination) ? or_rsv_nominate(pod, nd->allowed_pods, alloc, &ns, &rsv[i]) : -1;
       raw[i] = nom[i] >= 0 ? or_rsv_score_slot(pod, &rsv[i], nom[i]) : 0;
@@ -330,9 +346,11 @@ int or_schedule_resv_full(const kg_config* cfg, int64_t n_nodes, const kg_node* 
     int64_t pref = -1, best_order = INT64_MAX;
     for (int64_t i = 0; i < n_nodes; i++)
       if (feas[i] && order[i] != 0 && best_order > order[i]) { best_order = order[i]; pref = i; }
-    int64_t mx = 0, mds = 0;
+    int64_t mx = 0, mds = 0, mt = 0, ma = 0;
     for (int64_t i = 0; i < n_nodes; i++) {
       if (!feas[i]) continue;
+      if (tcnt[i] > mt) mt = tcnt[i];
+      if (asum[i] > ma) ma = asum[i];
       const int64_t sc = (i == pref) ? 1000 : raw[i]; /* mostPreferredScore */
       raw[i] = sc;
       if (sc > mx) mx = sc;
@@ -345,6 +363,9 @@ int or_schedule_resv_full(const kg_config* cfg, int64_t n_nodes, const kg_node* 
       int64_t t = base[i];
       if (cfg->reservation_score && mx > 0) t += cfg->weight_reservation * (100 * raw[i] / mx);
       if (ds_on && cfg->ds_score && mds > 0) t += cfg->weight_deviceshare * (100 * dsraw[i] / mds);
+      /* TaintToleration NormalizeScore (reverse) and NodeAffinity NormalizeScore × weight */
+      if (cfg->taint_score) t += cfg->weight_taint * or_normalize_default(tcnt[i], mt, 1);
+      if (cfg->affinity_score) t += cfg->weight_affinity * or_normalize_default(asum[i], ma, 0);
       if (t > win_total) { win_total = t; win = i; }
     }
     /* Reserve in the profile's order (scheduler-config.yaml:92-98): NodeNUMAResource (the exact cpuset), then
@@ -390,7 +411,7 @@ int or_schedule_resv_full(const kg_config* cfg, int64_t n_nodes, const kg_node* 
       if (quota) or_quota_charge(quota, pod);
     }
   }
-  free(feas); free(base); free(raw); free(dsraw); free(order); free(nom); free(aff);
+  free(feas); free(base); free(raw); free(dsraw); free(order); free(nom); free(aff); free(tcnt); free(asum);
   return rc;
 }
 
