@@ -1718,6 +1718,8 @@ __global__ void evaluate_pod_rsv(DevTable T, const RsvNode* __restrict__ RN, con
 }
 
 // Scatter of upserted device rows
+#include "xr_dev.h"
+
 template <typename Rec>
 __global__ void scatter_rows(Rec* __restrict__ dst, const Rec* __restrict__ src, const int32_t* __restrict__ idx,
                              int64_t n) {
@@ -2123,6 +2125,18 @@ struct kg_engine {
   DevBuf<NodePred> npred;       // [cap] kg_node_predicates
   DevBuf<DefPod> defpods;       // [staged + kMaxB]
   DevBuf<uint32_t> rsv_val2;    // [cap] raw taint count << 24 | raw affinity sum (their Scores on)
+  // batched exact rounds (xr_dev.h): kXrPods pods per round
+  bool xr_on = true;            // KG_EXACT_ROUNDS=0: one pod per pass only
+  DevBuf<uint64_t> xr_val;      // [kXrPods][cap]
+  DevBuf<uint32_t> xr_val2;     // [kXrPods][cap] (TaintToleration / NodeAffinity Scores on)
+  DevBuf<uint32_t> xr_aff;      // [kXrPods][cap] (NodeNUMAResource on)
+  DevBuf<uint64_t> xr_part;     // [kXrPods][tiles][kXrNorm]
+  DevBuf<uint64_t> xr_norm_d;   // [kXrPods][kXrNorm]
+  DevBuf<uint64_t> xr_lists;    // [kXrPods][tiles][kR]
+  DevBuf<uint64_t> xr_cand;     // [kXrPods][kCandStride]
+  hipGraphExec_t xr_exec = nullptr;  // kXrGraphRounds rounds
+  std::vector<unsigned char> xr_exec_sig;
+  double xr_avg = kXrPods;      // pods a round consumed on average (sizes the launches between host checks)
   // live kernel timing (kg_profile_enable): HIP event pairs around every launch of the round runners, on the
   // launch's own stream, folded into per-kind totals after each batch synchronises
   bool prof_on = false;
@@ -3250,6 +3264,115 @@ int run_rsv(kg_engine* e, int64_t first, int64_t count, kg_stats* stats, double 
   return 0;
 }
 
+// Batched exact rounds (xr_dev.h): rounds of kXrPods pods, kXrGraphRounds rounds per hipGraph launch; the host
+// launches about as many rounds as the pods left need at the recent consumption rate, then checks the cursor.
+constexpr int kXrGraphRounds = 4;
+constexpr int64_t kXrMin = 8;  // schedule calls of fewer pods run one pod per pass
+int run_xr(kg_engine* e, int64_t first, int64_t count, kg_stats* stats, double t0) {
+  if (int rc = sync_static(e)) return rc;
+  const int64_t n = e->n_nodes, end = first + count;
+  const int nt = (int)((n + kTile - 1) / kTile);
+  const int64_t stride = e->capacity;
+  const RsvExt X = rsv_ext(e);
+  const unsigned long long init[8] = {0, 0, 0, (unsigned long long)first, (unsigned long long)end, 0, 0, 0};
+  HIP_TRY(hipMemcpyAsync(e->rsv_ws.p, init, sizeof(init), hipMemcpyHostToDevice, e->stream));
+  const unsigned eval_blocks = (unsigned)(((nt + kEvalWaves - 1) / kEvalWaves) * (kXrPods / kXrPpw));
+  const int vbits = e->P.score_bits + 1;
+  const int bitmap_words = (int)((n + 31) / 32);
+  const size_t lds = (size_t)kXrPods * (kC + 1) * 8 + (size_t)bitmap_words * 4;
+  const int32_t* poison = reinterpret_cast<const int32_t*>(e->rsv_ws.p + 7);  // stays 0
+  uint64_t* val = e->xr_val.p;
+  uint32_t* val2 = e->def_score ? e->xr_val2.p : nullptr;
+  uint32_t* affk = e->numa_on ? e->xr_aff.p : nullptr;
+  auto issue_round = [&]() {
+    size_t t = prof_begin(e, e->stream);
+    xr_eval<<<eval_blocks, kWave * kEvalWaves, 0, e->stream>>>(e->T, e->rsv_d.p, e->rsv_nd.p, e->pods.p, e->rpods.p, n, nt,
+                                                             stride, e->P, e->RP, X, val, val2, affk, e->xr_part.p,
+                                                             e->rsv_ws.p);
+    prof_end(e, KG_PROF_RSV_EVAL, t, e->stream);
+    t = prof_begin(e, e->stream);
+    xr_norm<<<kXrPods, 256, 0, e->stream>>>(e->xr_part.p, nt, e->xr_norm_d.p, e->rsv_ws.p);
+    xr_select<<<eval_blocks, kWave * kEvalWaves, 0, e->stream>>>(val, val2, n, nt, stride, vbits, e->RP, X,
+                                                               e->xr_norm_d.p, e->xr_lists.p, e->rsv_ws.p);
+    merge_round<false><<<kXrPods, kMergeThreads, 0, e->stream>>>(e->T, e->P, e->xr_lists.p, (int64_t)nt * kR, kR, nt,
+                                                                 kR, kXrPods, poison, e->xr_cand.p);
+    prof_end(e, KG_PROF_RSV_SELECT, t, e->stream);
+    t = prof_begin(e, e->stream);
+    xr_resolve<<<1, kWave, lds, e->stream>>>(e->T, e->rsv_d.p, e->rsv_nd.p, e->pods.p, e->rpods.p, stride, e->P, e->RP, X,
+                                             val, val2, affk, e->xr_norm_d.p, e->xr_cand.p, bitmap_words,
+                                             e->out_keys.p, e->out_rslot.p, e->rsv_ws.p);
+    prof_end(e, KG_PROF_RSV_APPLY, t, e->stream);
+  };
+  static const bool no_graph = std::getenv("KG_RSV_NO_GRAPH") && std::getenv("KG_RSV_NO_GRAPH")[0] == '1';
+  if (!no_graph && !e->prof_on) {  // the instantiated graph of kXrGraphRounds rounds, keyed on its launch arguments
+    std::vector<unsigned char> sig;
+    auto put = [&](const void* q, size_t len) {
+      const unsigned char* b = static_cast<const unsigned char*>(q);
+      sig.insert(sig.end(), b, b + len);
+    };
+    put(&e->T, sizeof(e->T));
+    const void* ptrs[] = {e->rsv_d.p, e->rsv_nd.p, e->pods.p, e->rpods.p, val, val2, affk, e->xr_part.p,
+                          e->xr_norm_d.p, e->xr_lists.p, e->xr_cand.p, e->out_keys.p, e->out_rslot.p, e->rsv_ws.p};
+    put(ptrs, sizeof(ptrs));
+    put(&n, sizeof(n));
+    put(&e->P, sizeof(e->P));
+    put(&e->RP, sizeof(e->RP));
+    put(&X, sizeof(X));
+    if (!e->xr_exec || sig != e->xr_exec_sig) {
+      if (e->xr_exec) (void)hipGraphExecDestroy(e->xr_exec);
+      e->xr_exec = nullptr;
+      hipGraph_t gr = nullptr;
+      HIP_TRY(hipStreamBeginCapture(e->stream, hipStreamCaptureModeThreadLocal));
+      for (int r = 0; r < kXrGraphRounds; ++r) issue_round();
+      const hipError_t ce = hipStreamEndCapture(e->stream, &gr);
+      if (ce != hipSuccess) return fail(KG_E_DEVICE, "hipStreamEndCapture: %s", hipGetErrorString(ce));
+      const hipError_t ie = hipGraphInstantiate(&e->xr_exec, gr, nullptr, nullptr, 0);
+      (void)hipGraphDestroy(gr);
+      if (ie != hipSuccess) {
+        e->xr_exec = nullptr;
+        return fail(KG_E_DEVICE, "exact rounds graph: %s", hipGetErrorString(ie));
+      }
+      e->xr_exec_sig = sig;
+    }
+  }
+  int64_t cursor = first, launched = 0;
+  unsigned long long ws[8];
+  while (cursor < end) {
+    // rounds for the pods left at the recent rate (at least one graph), then one check of the cursor
+    const double per = std::max(1.0, e->xr_avg);
+    int64_t rounds = (int64_t)std::ceil((double)(end - cursor) / per);
+    rounds = std::max<int64_t>(1, std::min<int64_t>(rounds, kMaxBatchRounds));
+    if (e->xr_exec && !e->prof_on) {
+      const int64_t graphs = (rounds + kXrGraphRounds - 1) / kXrGraphRounds;
+      for (int64_t g = 0; g < graphs; ++g) {
+        const hipError_t ge = hipGraphLaunch(e->xr_exec, e->stream);
+        if (ge != hipSuccess) return fail(KG_E_DEVICE, "exact rounds graph: %s", hipGetErrorString(ge));
+      }
+      rounds = graphs * kXrGraphRounds;
+    } else {
+      for (int64_t r = 0; r < rounds; ++r) issue_round();
+      HIP_TRY(hipGetLastError());
+    }
+    launched += rounds;
+    HIP_TRY(hipMemcpyAsync(ws, e->rsv_ws.p, sizeof(ws), hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    if (e->prof_on)
+      if (int rc = prof_collect(e)) return rc;
+    const int64_t c = (int64_t)ws[3];
+    if (c <= cursor) return fail(KG_E_DEVICE, "exact rounds made no progress at pod %lld", (long long)cursor);
+    cursor = c;
+    if (ws[5] > 0) e->xr_avg = 0.5 * e->xr_avg + 0.5 * ((double)ws[6] / (double)ws[5]);
+  }
+  if (stats) {
+    std::memset(stats, 0, sizeof(*stats));
+    stats->device_batches = (int64_t)ws[5];
+    stats->node_evaluations = (int64_t)ws[5] * kXrPods * n;
+    stats->seconds = now_s() - t0;
+  }
+  (void)launched;
+  return 0;
+}
+
 int decode_node_rsv(const kg_node_reservations& r, RsvNode& d, int32_t& ns) {
   std::memset(&d, 0, sizeof(d));
   if (r.n < 0 || r.n > KG_MAX_RSV_SLOTS) return fail(KG_E_INVALID, "reservation slot count %lld", (long long)r.n);
@@ -3466,6 +3589,24 @@ static int engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank,
     if (hipMemset(e->rsv_nd.p, 0, cap * 4) != hipSuccess || hipMemset(e->rsv_ws.p, 0, 64) != hipSuccess)
       return bail(fail(KG_E_DEVICE, "hipMemset"));
   }
+  {
+    const char* xr = std::getenv("KG_EXACT_ROUNDS");
+    e->xr_on = !(xr && xr[0] == '0');
+  }
+  if (e->exact_on && e->xr_on) {  // batched exact rounds
+    const size_t nt = (size_t)((cap + kTile - 1) / kTile);
+    if (int rc = e->xr_val.ensure((size_t)kXrPods * cap)) return bail(rc);
+    if (e->def_score)
+      if (int rc = e->xr_val2.ensure((size_t)kXrPods * cap)) return bail(rc);
+    if (e->numa_on)
+      if (int rc = e->xr_aff.ensure((size_t)kXrPods * cap)) return bail(rc);
+    if (int rc = e->xr_part.ensure((size_t)kXrPods * nt * kXrNorm)) return bail(rc);
+    if (int rc = e->xr_norm_d.ensure((size_t)kXrPods * kXrNorm)) return bail(rc);
+    if (int rc = e->xr_lists.ensure((size_t)kXrPods * nt * kR)) return bail(rc);
+    if (int rc = e->xr_cand.ensure((size_t)kXrPods * kCandStride)) return bail(rc);
+    if (hipMemset(e->xr_lists.p, 0, (size_t)kXrPods * nt * kR * 8) != hipSuccess)
+      return bail(fail(KG_E_DEVICE, "hipMemset"));
+  }
   const int64_t max_total = 100 * ((c.fit_score ? c.weight_fit : 0) + (c.la_score ? c.weight_loadaware : 0) +
                                    (c.numa_score ? c.weight_numa : 0) + (c.ds_score ? c.weight_deviceshare : 0) +
                                    (c.reservation_score ? c.weight_reservation : 0) +
@@ -3638,6 +3779,17 @@ void kg_engine_destroy(kg_engine* e) {
   e->rsv_val.release();
   if (e->rsv_exec) (void)hipGraphExecDestroy(e->rsv_exec);
   e->rsv_exec = nullptr;
+  if (e->rsv_exec1) (void)hipGraphExecDestroy(e->rsv_exec1);
+  e->rsv_exec1 = nullptr;
+  if (e->xr_exec) (void)hipGraphExecDestroy(e->xr_exec);
+  e->xr_exec = nullptr;
+  e->xr_val.release();
+  e->xr_val2.release();
+  e->xr_aff.release();
+  e->xr_part.release();
+  e->xr_norm_d.release();
+  e->xr_lists.release();
+  e->xr_cand.release();
   e->rsv_ws.release();
   e->rsv_part.release();
   e->npred.release();
@@ -3928,6 +4080,7 @@ static int schedule_staged_impl(kg_engine* e, int64_t first, int64_t count, kg_s
   const double t0 = now_s();
   // the exact per-pod pass: its profiles, and calls of at most kExactSmall pods of any profile (the drop-in's per-pod
   // scheduleOne): one pass costs less than a round's eval + merge + resolve when a round would hold one pod
+  if (e->exact_on && e->xr_on && count >= kXrMin && e->n_nodes > 0) return run_xr(e, first, count, stats, t0);
   if (e->exact_on || (count <= kExactSmall && e->n_ranks == 1)) return run_rsv(e, first, count, stats, t0);
   RoundGeom g;
   if (int rc = prepare_rounds(e, g)) return rc;

@@ -281,6 +281,16 @@ __device__ __forceinline__ RsvOut rsv_eval_node(const DevTable& T, const RsvNode
   return o;
 }
 
+// pass-1 value of a feasible node: base << 32 | dsraw << 16 | raw << 8 | feasible << 7 | (nom + 1)
+__device__ __forceinline__ uint64_t rsv_pack(const RsvOut& o) {
+  return ((uint64_t)(uint32_t)o.base << 32) | ((uint64_t)(uint32_t)o.dsraw << 16) | ((uint64_t)(uint32_t)o.raw << 8) |
+         (1ull << 7) | (uint64_t)(o.nom + 1);
+}
+// PreScore preferred-node key of a feasible node with an order label: max = smallest order, then lowest index
+__device__ __forceinline__ uint64_t rsv_pref_key(const RsvOut& o, uint32_t i) {
+  return o.order != 0x7fffffff ? ~(((uint64_t)(uint32_t)o.order << 32) | (uint64_t)i) : 0ull;
+}
+
 constexpr int kRsvThreads = 256;  // 4 waves per block: fewer block partials to reduce per pass
 
 // Block max of a u64 over its waves (DPP wave max, then LDS); result valid in thread 0.
@@ -486,9 +496,8 @@ __global__ __launch_bounds__(kRsvThreads) void rsv_eval(DevTable T, RsvNode* __r
     const DefPod* df = X.defp ? &X.defp[j] : nullptr;
     const RsvOut o = rsv_eval_node(T, RN, rsv_n, i, p, rp, P, RP, X, dp, np, nullptr, aux, df);
     if (o.feas) {
-      v = ((uint64_t)(uint32_t)o.base << 32) | ((uint64_t)(uint32_t)o.dsraw << 16) |
-          ((uint64_t)(uint32_t)o.raw << 8) | (1ull << 7) | (uint64_t)(o.nom + 1);
-      if (o.order != 0x7fffffff) pk = ~(((uint64_t)(uint32_t)o.order << 32) | (uint64_t)(uint32_t)i);
+      v = rsv_pack(o);
+      pk = rsv_pref_key(o, (uint32_t)i);
       rawv = (uint64_t)(uint32_t)o.raw;
       dsv = (uint64_t)(uint32_t)o.dsraw;
       tv = (uint64_t)(uint32_t)o.tcnt;
@@ -519,6 +528,20 @@ __global__ __launch_bounds__(kRsvThreads) void rsv_eval(DevTable T, RsvNode* __r
   }
 }
 
+// The weighted total of one feasible node from its pass-1 value: PreScore preferred node (1000), DefaultNormalizeScore
+// of the Reservation / DeviceShare / TaintToleration / NodeAffinity raw Scores against the feasible nodes' maxima
+// (mx already max(raw, 1000) when a preferred node exists), × weights.  Shared by rsv_select and the batched rounds.
+__device__ __forceinline__ int64_t rsv_total(uint64_t v, uint32_t v2, bool is_pref, int64_t mx, int64_t mds,
+                                             int64_t mt, int64_t ma, const RsvParams& RP, const RsvExt& X) {
+  const int64_t raw = is_pref ? 1000 : (int64_t)((v >> 8) & 0xff);  // mostPreferredScore
+  int64_t t = (int64_t)(v >> 32);
+  if (RP.score && mx > 0) t += (int64_t)RP.weight * (100 * raw / mx);
+  if (X.DP.score && mds > 0) t += (int64_t)X.DP.weight * (100 * (int64_t)((v >> 16) & 0xff) / mds);
+  if (X.DF.taint_score) t += (int64_t)X.DF.w_taint * normalize_default(v2 >> 24, mt, true);
+  if (X.DF.aff_score) t += (int64_t)X.DF.w_aff * normalize_default(v2 & 0xFFFFFFu, ma, false);
+  return t;
+}
+
 // Pass 2: PreScore preferred node (1000), DefaultNormalizeScore of both plugins over the feasible nodes, × weights,
 // packed key; part[2 nb + b] = the block's max key.  Block 0 also charges pod j - 1's quota (tagged ws[0] = j).
 __global__ __launch_bounds__(kRsvThreads) void rsv_select(const uint64_t* __restrict__ val, const DevPod* __restrict__ pods,
@@ -544,16 +567,8 @@ __global__ __launch_bounds__(kRsvThreads) void rsv_select(const uint64_t* __rest
   if (i < n) {
     const uint64_t v = val[i];
     if (v & (1ull << 7)) {
-      const int64_t raw = (i == pref) ? 1000 : (int64_t)((v >> 8) & 0xff);  // mostPreferredScore
-      int64_t t = (int64_t)(v >> 32);
-      if (RP.score && mx > 0) t += (int64_t)RP.weight * (100 * raw / mx);
-      if (X.DP.score && mds > 0) t += (int64_t)X.DP.weight * (100 * (int64_t)((v >> 16) & 0xff) / (int64_t)mds);
-      if (X.val2) {
-        const uint32_t v2 = X.val2[i];
-        if (X.DF.taint_score) t += (int64_t)X.DF.w_taint * normalize_default(v2 >> 24, mt, true);
-        if (X.DF.aff_score) t += (int64_t)X.DF.w_aff * normalize_default(v2 & 0xFFFFFFu, ma, false);
-      }
-      key = make_key(t, (uint32_t)i);
+      const uint32_t v2 = X.val2 ? X.val2[i] : 0u;
+      key = make_key(rsv_total(v, v2, i == pref, mx, (int64_t)mds, mt, ma, RP, X), (uint32_t)i);
     }
   }
   key = rsv_block_max(key, s_red);

@@ -1,0 +1,356 @@
+// Batched exact rounds (SURVEY §8a A15–A24 on the profiles the per-pod exact pass runs: Reservation, the shipped
+// NodeNUMAResource + DeviceShare profile, the upstream defaults): kXrPods FIFO pods per round instead of one pod per
+// device pass.  Included by engine.hip inside its kernel namespace (uses kTile / kNPT / kR / select_write).
+//
+// A round over pods [c, c + nb), c = the device cursor ws[3]:
+//   xr_eval    every (pod, node) of the round through rsv_eval_node on the round-start state (BeforePreFilter restore,
+//              every Filter, the un-normalised totals and raw Scores): val[k][i] (rsv_pack), val2[k][i] (raw
+//              TaintToleration / NodeAffinity), aff[k][i] (the NUMA affinity Reserve needs), and per (pod, tile) the
+//              PreScore preferred-node key and, per normalised Score, (max + 1, holders);
+//   xr_norm    per pod: the round-start maxima and holder counts over all nodes;
+//   xr_select  per (pod, tile): the weighted totals with the round-start maxima (rsv_total, as rsv_select) → top-kR;
+//   merge      merge_round: per pod the kC best keys + ub (a strict bound on every key left out);
+//   xr_resolve one wave replays the pods in order (ElasticQuota PreFilter, winner, Reserve).  Lane l owns the l-th
+//              row modified in this round and re-runs pod j on it (the exact current key).  The round-start keys
+//              of unmodified rows stay exact while the normalisation of pod j is unchanged, so pod j is resolved
+//              iff: no modified row raises a maximum or, having been a holder of it, lowers it when every holder
+//              was modified (the holder count says so); the preferred node neither moves nor changes; and the best
+//              candidate is ≥ ub.  Otherwise the round stops before pod j and the next round starts there.
+// The first pod of a round always resolves (nothing modified yet), so every round makes progress.
+#pragma once
+
+constexpr int kXrPods = 32;      // pods per round (< kWave: one modified row per resolver lane)
+constexpr int kXrPpw = 8;        // pods per eval / select wave
+constexpr int kXrNorm = 5;       // per-pod statistics: preferred key, raw Reservation, DeviceShare, taint, affinity
+static_assert(kXrPods < kWave, "resolver lanes");
+
+__device__ __forceinline__ bool xr_range(const unsigned long long* __restrict__ ws, int64_t& first, int& nb) {
+  first = (int64_t)ws[3];
+  const int64_t left = (int64_t)ws[4] - first;
+  nb = left < kXrPods ? (int)left : kXrPods;
+  return nb > 0;
+}
+
+// (max + 1, count) of one statistic over a wave; v = value + 1 (0 = infeasible)
+__device__ __forceinline__ uint64_t xr_wave_maxcount(uint32_t m, uint32_t c) {
+  const uint32_t wm = wave_max_u32(m);
+  const uint32_t wc = wave_sum_u32(m == wm ? c : 0u);
+  return ((uint64_t)wm << 32) | wc;
+}
+__device__ __forceinline__ void xr_acc(uint32_t v, uint32_t& m, uint32_t& c) {
+  c = v > m ? 1u : c + (v == m && v != 0 ? 1u : 0u);
+  m = v > m ? v : m;
+}
+__device__ __forceinline__ void xr_tile_coords(int n_pg, int& tile, int& p0) {
+  const int wave = threadIdx.x / kWave;
+  const uint32_t nwg = gridDim.x, bid = blockIdx.x, xcd = bid % 8u, q = nwg / 8u, r = nwg % 8u;
+  const uint32_t wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8u;  // XCD-aware swizzle
+  tile = (int)(wgid / (uint32_t)n_pg) * kEvalWaves + wave;
+  p0 = (int)(wgid % (uint32_t)n_pg) * kXrPpw;
+}
+
+__global__ __launch_bounds__(kWave* kEvalWaves) void xr_eval(DevTable T, const RsvNode* __restrict__ RN,
+                                                             const int32_t* __restrict__ rsv_n,
+                                                             const DevPod* __restrict__ pods,
+                                                             const RsvPod* __restrict__ rpods, int64_t n, int nt,
+                                                             int64_t stride, EvalParams P, RsvParams RP, RsvExt X,
+                                                             uint64_t* __restrict__ val, uint32_t* __restrict__ val2,
+                                                             uint32_t* __restrict__ affk, uint64_t* __restrict__ part,
+                                                             const unsigned long long* __restrict__ ws) {
+  int64_t first;
+  int nb;
+  if (!xr_range(ws, first, nb)) return;
+  int tile, p0;
+  xr_tile_coords(kXrPods / kXrPpw, tile, p0);
+  if (tile >= nt || p0 >= nb) return;
+  const int lane = threadIdx.x % kWave;
+  const int p1 = p0 + kXrPpw < nb ? p0 + kXrPpw : nb;
+  for (int k = p0; k < p1; ++k) {
+    const int64_t j = first + k;
+    const DevPod p = pods[j];
+    const RsvPod rp = rpods[j];
+    const DsPod* dp = X.ds ? &X.dpods[j] : nullptr;
+    const NumaPod* np = X.ns ? &X.npods[j] : nullptr;
+    const int64_t* aux = (X.paux && (p.flags & P_AUX)) ? X.paux + (size_t)j * kAux : nullptr;
+    const DefPod* df = X.defp ? &X.defp[j] : nullptr;
+    RsvExt Xk = X;
+    Xk.aff = X.aff ? affk + (size_t)k * stride : nullptr;  // rsv_eval_node stores the NUMA affinity per node
+    uint64_t pk = 0;
+    uint32_t m[4] = {0, 0, 0, 0}, c[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int q = 0; q < kNPT; ++q) {
+      int64_t i = (int64_t)tile * kTile + q * kWave + lane;
+      asm volatile("" : "+v"(i));  // keep the per-node addresses inside the loop (register pressure)
+      if (i >= n) break;
+      const RsvOut o = rsv_eval_node(T, RN, rsv_n, i, p, rp, P, RP, Xk, dp, np, nullptr, aux, df);
+      uint64_t v = 0;
+      uint32_t v2 = 0;
+      if (o.feas) {
+        v = rsv_pack(o);
+        v2 = ((uint32_t)o.tcnt << 24) | (uint32_t)o.asum;
+        const uint64_t k2 = rsv_pref_key(o, (uint32_t)i);
+        pk = k2 > pk ? k2 : pk;
+        xr_acc((uint32_t)o.raw + 1u, m[0], c[0]);
+        xr_acc((uint32_t)o.dsraw + 1u, m[1], c[1]);
+        xr_acc((uint32_t)o.tcnt + 1u, m[2], c[2]);
+        xr_acc((uint32_t)o.asum + 1u, m[3], c[3]);
+      }
+      val[(size_t)k * stride + i] = v;
+      if (val2) val2[(size_t)k * stride + i] = v2;
+    }
+    pk = wave_max_u64_dpp(pk);
+    uint64_t s[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) s[q] = xr_wave_maxcount(m[q], c[q]);
+    if (lane == 0) {
+      uint64_t* o = part + ((size_t)k * nt + tile) * kXrNorm;
+      o[0] = pk;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) o[1 + q] = s[q];
+    }
+  }
+}
+
+// one block per pod: norm[k] = {preferred key, (M + 1) << 32 | holders for raw, ds, taint, affinity}
+__global__ __launch_bounds__(256) void xr_norm(const uint64_t* __restrict__ part, int nt,
+                                               uint64_t* __restrict__ norm, const unsigned long long* __restrict__ ws) {
+  __shared__ uint64_t s_v[256 / kWave][kXrNorm];
+  int64_t first;
+  int nb;
+  if (!xr_range(ws, first, nb)) return;
+  const int k = blockIdx.x;
+  if (k >= nb) return;
+  const int tid = threadIdx.x, lane = tid % kWave, wave = tid / kWave;
+  uint64_t pk = 0;
+  uint32_t m[4] = {0, 0, 0, 0}, c[4] = {0, 0, 0, 0};
+  for (int t = tid; t < nt; t += 256) {
+    const uint64_t* o = part + ((size_t)k * nt + t) * kXrNorm;
+    pk = o[0] > pk ? o[0] : pk;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t vm = (uint32_t)(o[1 + q] >> 32), vc = (uint32_t)o[1 + q];
+      c[q] = vm > m[q] ? vc : c[q] + (vm == m[q] ? vc : 0u);
+      m[q] = vm > m[q] ? vm : m[q];
+    }
+  }
+  pk = wave_max_u64_dpp(pk);
+  uint64_t s[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) s[q] = xr_wave_maxcount(m[q], c[q]);
+  if (lane == 0) {
+    s_v[wave][0] = pk;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) s_v[wave][1 + q] = s[q];
+  }
+  __syncthreads();
+  if (tid < kXrNorm) {
+    uint64_t r = 0;
+    if (tid == 0) {
+      for (int w = 0; w < 256 / kWave; ++w) r = s_v[w][0] > r ? s_v[w][0] : r;
+    } else {
+      uint32_t M = 0, C = 0;
+      for (int w = 0; w < 256 / kWave; ++w) {
+        const uint32_t vm = (uint32_t)(s_v[w][tid] >> 32), vc = (uint32_t)s_v[w][tid];
+        C = vm > M ? vc : C + (vm == M ? vc : 0u);
+        M = vm > M ? vm : M;
+      }
+      r = ((uint64_t)M << 32) | C;
+    }
+    norm[(size_t)k * kXrNorm + tid] = r;
+  }
+}
+
+struct XrNorms {
+  int64_t pref;             // the PreScore preferred node (-1 = none)
+  int64_t mx, mds, mt, ma;  // the normalisation maxima rsv_total takes
+};
+__device__ __forceinline__ XrNorms xr_norms(const uint64_t* __restrict__ nk) {
+  auto mval = [](uint64_t e) -> int64_t { return (e >> 32) ? (int64_t)(e >> 32) - 1 : 0; };
+  XrNorms r;
+  const uint64_t pk = nk[0];
+  const int64_t mraw = mval(nk[1]);
+  r.pref = pk ? (int64_t)(uint32_t)(~pk) : -1;
+  r.mx = pk ? (mraw > 1000 ? mraw : 1000) : mraw;
+  r.mds = mval(nk[2]);
+  r.mt = mval(nk[3]);
+  r.ma = mval(nk[4]);
+  return r;
+}
+
+__global__ __launch_bounds__(kWave* kEvalWaves) void xr_select(const uint64_t* __restrict__ val,
+                                                               const uint32_t* __restrict__ val2, int64_t n, int nt,
+                                                               int64_t stride, int vbits, RsvParams RP, RsvExt X,
+                                                               const uint64_t* __restrict__ norm,
+                                                               uint64_t* __restrict__ lists,
+                                                               const unsigned long long* __restrict__ ws) {
+  int64_t first;
+  int nb;
+  if (!xr_range(ws, first, nb)) return;
+  int tile, p0;
+  xr_tile_coords(kXrPods / kXrPpw, tile, p0);
+  if (tile >= nt || p0 >= nb) return;
+  const int lane = threadIdx.x % kWave;
+  const int p1 = p0 + kXrPpw < nb ? p0 + kXrPpw : nb;
+  uint32_t gidx[kNPT];
+#pragma unroll
+  for (int q = 0; q < kNPT; ++q) gidx[q] = (uint32_t)((int64_t)tile * kTile + q * kWave + lane);
+  for (int k = p0; k < p1; ++k) {
+    const XrNorms N = xr_norms(norm + (size_t)k * kXrNorm);
+    uint32_t v[kNPT];
+#pragma unroll
+    for (int q = 0; q < kNPT; ++q) {
+      const int64_t i = gidx[q];
+      const uint64_t pv = i < n ? val[(size_t)k * stride + i] : 0;
+      v[q] = 0;
+      if (pv & (1ull << 7)) {
+        const uint32_t pv2 = val2 ? val2[(size_t)k * stride + i] : 0u;
+        v[q] = (uint32_t)rsv_total(pv, pv2, i == N.pref, N.mx, N.mds, N.mt, N.ma, RP, X) + 1u;
+      }
+    }
+    select_write(v, gidx, vbits, lists + ((size_t)k * nt + tile) * kR, lane);
+  }
+}
+
+// One wave: the round's FIFO replay (see the header).  Dynamic LDS: the pods' candidate records [nb][kC + 1] and the
+// modified-node bitmap.
+__global__ __launch_bounds__(kWave) void xr_resolve(DevTable T, RsvNode* __restrict__ RN,
+                                                    const int32_t* __restrict__ rsv_n,
+                                                    const DevPod* __restrict__ pods,
+                                                    const RsvPod* __restrict__ rpods, int64_t stride,
+                                                    EvalParams P, RsvParams RP, RsvExt X,
+                                                    const uint64_t* __restrict__ val, const uint32_t* __restrict__ val2,
+                                                    const uint32_t* __restrict__ affk,
+                                                    const uint64_t* __restrict__ norm,
+                                                    const uint64_t* __restrict__ cand, int bitmap_words,
+                                                    uint64_t* __restrict__ out_keys, int32_t* __restrict__ out_slot,
+                                                    unsigned long long* __restrict__ ws) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
+  int64_t first;
+  int nb;
+  if (!xr_range(ws, first, nb)) return;
+  const int lane = threadIdx.x;
+  uint64_t* s_cand = smem;  // [nb][kC + 1]
+  uint32_t* bitmap = reinterpret_cast<uint32_t*>(s_cand + (size_t)nb * (kC + 1));
+  for (int w = lane; w < nb * (kC + 1); w += kWave) s_cand[w] = cand[(size_t)(w / (kC + 1)) * kCandStride + w % (kC + 1)];
+  for (int w = lane; w < bitmap_words; w += kWave) bitmap[w] = 0;
+  __syncthreads();
+  uint32_t midx = 0xFFFFFFFFu;  // the modified row this lane owns
+  int nM = 0, consumed = 0;
+  const bool dscore = val2 != nullptr;
+  for (int j = 0; j < nb; ++j) {
+    const int64_t jj = first + j;
+    const DevPod p = pods[jj];
+    // ElasticQuota PreFilter against every earlier Reserve (lane 0 owns the quota rows)
+    int admit = 1;
+    QuotaReq qr;
+    if (X.nq > 0 && p.quota >= 0) {
+      qr = quota_req(p, X.qdev + (size_t)jj * kQuotaRes);
+      if (lane == 0) admit = quota_row_admit(X.quotas[p.quota], qr, (p.flags & P_NONPREEMPT) != 0) ? 1 : 0;
+      admit = __builtin_amdgcn_readfirstlane(admit);
+    }
+    if (!admit) {
+      if (lane == 0) {
+        out_keys[jj] = 0;
+        out_slot[jj] = -1;
+        if (X.out_minors) X.out_minors[jj] = 0;
+      }
+      ++consumed;
+      continue;
+    }
+    // pod j on the modified rows: the exact current values, next to the round-start ones
+    const RsvPod rp = rpods[jj];
+    const DsPod* dp = X.ds ? &X.dpods[jj] : nullptr;
+    const NumaPod* np = X.ns ? &X.npods[jj] : nullptr;
+    const int64_t* aux = (X.paux && (p.flags & P_AUX)) ? X.paux + (size_t)jj * kAux : nullptr;
+    const DefPod* df = X.defp ? &X.defp[jj] : nullptr;
+    RsvOut cur{false, 0, 0, -1, 0x7fffffff, 0, 0, 0};
+    uint64_t ov = 0, cv = 0;
+    uint32_t ov2 = 0, cv2 = 0;
+    if (lane < nM) {
+      cur = rsv_eval_node(T, RN, rsv_n, midx, p, rp, P, RP, X, dp, np, nullptr, aux, df);  // X.aff[midx] = pod j's
+      if (cur.feas) cv = rsv_pack(cur), cv2 = ((uint32_t)cur.tcnt << 24) | (uint32_t)cur.asum;
+      ov = val[(size_t)j * stride + midx];
+      ov2 = dscore ? val2[(size_t)j * stride + midx] : 0u;
+    }
+    const uint64_t* nk = norm + (size_t)j * kXrNorm;
+    bool stop = false;
+    {  // the normalisation of pod j must equal the round's
+      const bool of = (ov >> 7) & 1, cf = cur.feas;
+      const uint32_t oval[4] = {(uint32_t)((ov >> 8) & 0xff), (uint32_t)((ov >> 16) & 0xff), ov2 >> 24, ov2 & 0xFFFFFFu};
+      const uint32_t cval[4] = {(uint32_t)cur.raw, (uint32_t)cur.dsraw, (uint32_t)cur.tcnt, (uint32_t)cur.asum};
+      const bool used[4] = {RP.score != 0, X.DP.score != 0, X.DF.taint_score != 0, X.DF.aff_score != 0};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (!used[q]) continue;
+        const uint32_t Menc = (uint32_t)(nk[1 + q] >> 32), C = (uint32_t)nk[1 + q];
+        const uint32_t oe = (lane < nM && of) ? oval[q] + 1u : 0u, ce = (lane < nM && cf) ? cval[q] + 1u : 0u;
+        const uint32_t lost = (uint32_t)__popcll(__ballot(oe != 0 && oe == Menc));
+        const uint32_t cm = wave_max_u32(ce);
+        if (cm > Menc || (lost >= C && cm != Menc)) stop = true;
+      }
+      if (RP.score) {  // the preferred node (smallest order label) must stay where it is, with the same order
+        const uint64_t PK = nk[0];
+        const uint64_t ck = (lane < nM && cf) ? rsv_pref_key(cur, midx) : 0ull;
+        const uint64_t mk = wave_max_key(ck);
+        const uint32_t pn = (uint32_t)(~PK);
+        const bool holder_mod = PK != 0 && ((bitmap[pn >> 5] >> (pn & 31)) & 1u);
+        if (mk > PK || (holder_mod && mk != PK)) stop = true;
+      }
+    }
+    if (stop) break;
+    const XrNorms N = xr_norms(nk);
+    const uint64_t mkey = (lane < nM && cur.feas)
+                              ? make_key(rsv_total(cv, cv2, (int64_t)midx == N.pref, N.mx, N.mds, N.mt, N.ma, RP, X), midx)
+                              : 0ull;
+    const uint64_t mbest = wave_max_key(mkey);
+    const uint64_t key = lane < kC ? s_cand[(size_t)j * (kC + 1) + lane] : 0ull;
+    const uint32_t kn = key_node(key);
+    const bool unmod = key != 0 && !((bitmap[kn >> 5] >> (kn & 31)) & 1u);
+    const uint64_t um = __ballot(unmod);
+    uint64_t best = um ? readlane_u64(key, (int)__builtin_ctzll(um)) : 0ull;
+    best = mbest > best ? mbest : best;
+    if (best < s_cand[(size_t)j * (kC + 1) + kC]) break;  // an unlisted node could win
+    ++consumed;
+    if (best == 0) {
+      if (lane == 0) {
+        out_keys[jj] = 0;
+        out_slot[jj] = -1;
+        if (X.out_minors) X.out_minors[jj] = 0;
+      }
+      continue;
+    }
+    const uint32_t w = key_node(best);
+    const uint64_t hit = __ballot(lane < nM && midx == w);
+    const int owner = hit ? (int)__builtin_ctzll(hit) : nM;
+    if (!hit) {
+      if (lane == 0) bitmap[w >> 5] |= 1u << (w & 31);
+      ++nM;
+    }
+    int placed = 0, slot = -1;
+    if (lane == owner) {
+      uint64_t v = cv;
+      if (!hit) {  // an unmodified winner: its round-start value, and its NUMA affinity for pod j
+        midx = w;
+        v = val[(size_t)j * stride + w];
+        if (X.aff) X.aff[w] = affk[(size_t)j * stride + w];
+      }
+      int32_t s = -1;
+      placed = rsv_reserve(T, RN, w, v, p, X, jj, s) ? 1 : 0;
+      slot = s;
+    }
+    placed = __builtin_amdgcn_readlane(placed, owner);
+    slot = __builtin_amdgcn_readlane(slot, owner);
+    if (lane == 0) {
+      out_keys[jj] = placed ? best : 0;
+      out_slot[jj] = slot;
+      if (placed && X.nq > 0 && p.quota >= 0) quota_row_charge(X.quotas[p.quota], qr, (p.flags & P_NONPREEMPT) != 0);
+    }
+    __syncthreads();
+  }
+  __threadfence();
+  if (lane == 0) {
+    ws[3] = (unsigned long long)(first + consumed);
+    ws[5] += 1;
+    ws[6] += (unsigned long long)consumed;
+  }
+}
