@@ -886,6 +886,7 @@ __global__ __launch_bounds__(kWave) void resolve_round(DevTable T0, const DevPod
   uint32_t word = bitmap[key ? key_node(key) >> 5 : 0u];
   uint64_t key_n = s_cand[(size_t)(nb > 1 ? 1 : 0) * kCandStride + lane];
   uint32_t diag = 0;
+  (void)diag;  // read by the KG_STAMPS build only
   for (int j = 0; j < nb; ++j) {
     KG_POD_DIAG(j, diag);
     diag = 0;
@@ -2613,6 +2614,9 @@ uint32_t node_flags(const kg_engine* e, int64_t i) {
     f |= F_LA_SCORE;
   if (la_filter_pass(c, n, m, now, false)) f |= F_LA_PASS;
   if (la_filter_pass(c, n, m, now, true)) f |= F_LA_PASS_PROD;
+  if (estimate_node(n, KG_RES_CPU) == n.allocatable[KG_RES_CPU] &&
+      estimate_node(n, KG_RES_MEMORY) == n.allocatable[KG_RES_MEMORY])
+    f |= F_LA_ALLOC_EQ;
   return f;
 }
 
@@ -3277,6 +3281,7 @@ int run_xr(kg_engine* e, int64_t first, int64_t count, kg_stats* stats, double t
   const unsigned long long init[8] = {0, 0, 0, (unsigned long long)first, (unsigned long long)end, 0, 0, 0};
   HIP_TRY(hipMemcpyAsync(e->rsv_ws.p, init, sizeof(init), hipMemcpyHostToDevice, e->stream));
   const unsigned eval_blocks = (unsigned)(((nt + kEvalWaves - 1) / kEvalWaves) * (kXrPods / kXrPpw));
+  const unsigned xr_eval_blocks = (unsigned)nt * (kXrPods / kXrEvalPpw);
   const int vbits = e->P.score_bits + 1;
   const int bitmap_words = (int)((n + 31) / 32);
   const size_t lds = (size_t)kXrPods * (kC + 1) * 8 + (size_t)bitmap_words * 4;
@@ -3286,7 +3291,7 @@ int run_xr(kg_engine* e, int64_t first, int64_t count, kg_stats* stats, double t
   uint32_t* affk = e->numa_on ? e->xr_aff.p : nullptr;
   auto issue_round = [&]() {
     size_t t = prof_begin(e, e->stream);
-    xr_eval<<<eval_blocks, kWave * kEvalWaves, 0, e->stream>>>(e->T, e->rsv_d.p, e->rsv_nd.p, e->pods.p, e->rpods.p, n, nt,
+    xr_eval<<<xr_eval_blocks, kTile, 0, e->stream>>>(e->T, e->rsv_d.p, e->rsv_nd.p, e->pods.p, e->rpods.p, n, nt,
                                                              stride, e->P, e->RP, X, val, val2, affk, e->xr_part.p,
                                                              e->rsv_ws.p);
     prof_end(e, KG_PROF_RSV_EVAL, t, e->stream);

@@ -79,6 +79,9 @@ constexpr uint32_t F_RARE = 1u << 4;          // EvalRow only: a score input lie
 // (reservation/plugin.go:469-471: 0 > Allocatable - Requested rejects).  Scheduling never sets it (a placed request fits
 // the free amount), so only host deltas (kg_pods_add / remove / unreserve, node upserts) move it: refresh_eph_flags.
 constexpr uint32_t F_EPH_OVER = 1u << 6;
+// EstimateNode == Allocatable for cpu and memory (no raw-allocatable annotation: default_estimator.go:110-129): the wide
+// pass then takes LoadAware's capacity from the Fit columns instead of reading la_alloc_cpu / la_alloc_mem
+constexpr uint32_t F_LA_ALLOC_EQ = 1u << 7;
 
 // pod flags (device)
 constexpr uint32_t P_ZERO_REQ = 1u << 0;      // every request zero → fitsRequest skips resource checks
@@ -586,6 +589,12 @@ struct HotRow {
   uint32_t flags;
 };
 
+// 100 / capacity as the host's ingest writes the reciprocal columns (sync_static: IEEE double division, then the cpu
+// estimate rounded to f32), computed where a tile's rows are hoisted so that the wide pass does not read those
+// columns (24 B per node); the values are bit-identical to the columns the resolvers read.
+__device__ __forceinline__ float inv100_f32(int64_t c) { return c > 0 ? (float)(100.0 / (double)c) : 0.0f; }
+__device__ __forceinline__ double inv100_f64(int64_t c) { return c > 0 ? 100.0 / (double)c : 0.0; }
+
 template <int PF>
 __device__ __forceinline__ HotRow load_hot(const DevTable& T, int64_t i, const EvalParams& P) {
   HotRow h;
@@ -593,10 +602,14 @@ __device__ __forceinline__ HotRow load_hot(const DevTable& T, int64_t i, const E
   const int64_t ac = T.alloc_cpu[i], am = T.alloc_mem[i];
   const int64_t fc = ac - T.req_cpu[i], fm = am - T.req_mem[i];
   const int64_t fnc = ac - T.nz_cpu[i], fnm = am - T.nz_mem[i];
-  const int64_t lac = T.la_alloc_cpu[i], lam = T.la_alloc_mem[i];
-  const int64_t lfc = lac - T.la_used_cpu[i], lfm = lam - T.la_used_mem[i];
+  // LoadAware terms only for rows it scores; capacity from the Fit columns when EstimateNode == Allocatable
+  constexpr bool kLa = (PF & PF_LA_SCORE) != 0;
+  const bool la_row = kLa && (fl & F_LA_SCORE) != 0, la_eq = (fl & F_LA_ALLOC_EQ) != 0;
+  const int64_t lac = !la_row ? 0 : la_eq ? ac : T.la_alloc_cpu[i];
+  const int64_t lam = !la_row ? 0 : la_eq ? am : T.la_alloc_mem[i];
+  const int64_t lfc = la_row ? lac - T.la_used_cpu[i] : 0, lfm = la_row ? lam - T.la_used_mem[i] : 0;
   constexpr bool kProd = (PF & PF_LA_PROD) != 0;
-  const int64_t lpc = kProd ? lac - T.la_pused_cpu[i] : 0, lpm = kProd ? lam - T.la_pused_mem[i] : 0;
+  const int64_t lpc = kProd && la_row ? lac - T.la_pused_cpu[i] : 0, lpm = kProd && la_row ? lam - T.la_pused_mem[i] : 0;
   const bool pods_ok = T.num_pods[i] + 1 <= T.alloc_pods[i];
   bool ok = true;
   if constexpr ((PF & PF_FIT_FILTER) != 0) ok &= (fc >= -kFreeCpuAbs) & (fc <= kFreeCpuAbs) & (fm > -kFreeMemAbs) & (fm < kFreeMemAbs);
@@ -616,16 +629,17 @@ __device__ __forceinline__ HotRow load_hot(const DevTable& T, int64_t i, const E
   h.la_free_cpu = (int32_t)lfc;
   h.la_pfree_cpu = (int32_t)lpc;
   h.la_alloc_cpu = (int32_t)lac;
-  h.inv_cpu = T.inv_cpu[i];
-  h.la_inv_cpu = T.inv_cpu[T.cap + i];
+  constexpr bool kFitS = (PF & PF_FIT_SCORE) != 0;
+  h.inv_cpu = kFitS ? inv100_f32(ac) : 0.0f;
+  h.la_inv_cpu = la_row ? inv100_f32(lac) : 0.0f;
   h.free_mem = (double)fm;
   h.fnz_mem = (double)fnm;
   h.alloc_mem = (double)am;
-  h.inv_mem = T.inv_mem[i];
+  h.inv_mem = kFitS ? inv100_f64(am) : 0.0;
   h.la_free_mem = (double)lfm;
   h.la_pfree_mem = (double)lpm;
   h.la_alloc_mem = (double)lam;
-  h.la_inv_mem = T.inv_mem[T.cap + i];
+  h.la_inv_mem = la_row ? inv100_f64(lam) : 0.0;
   h.flags = (fl & ~(F_RARE | F_PODS_OK)) | ((fl & F_VALID) && pods_ok ? F_PODS_OK : 0u) | (ok ? 0u : F_RARE);
   return h;
 }

@@ -49,51 +49,54 @@ __device__ __forceinline__ void xr_tile_coords(int n_pg, int& tile, int& p0) {
   p0 = (int)(wgid % (uint32_t)n_pg) * kXrPpw;
 }
 
-__global__ __launch_bounds__(kWave* kEvalWaves) void xr_eval(DevTable T, const RsvNode* __restrict__ RN,
-                                                             const int32_t* __restrict__ rsv_n,
-                                                             const DevPod* __restrict__ pods,
-                                                             const RsvPod* __restrict__ rpods, int64_t n, int nt,
-                                                             int64_t stride, EvalParams P, RsvParams RP, RsvExt X,
-                                                             uint64_t* __restrict__ val, uint32_t* __restrict__ val2,
-                                                             uint32_t* __restrict__ affk, uint64_t* __restrict__ part,
-                                                             const unsigned long long* __restrict__ ws) {
+// One block per (256-node tile, group of kXrEvalPpw pods), one node per thread: rsv_eval_node is long and divergent
+// (NUMA hints, DeviceShare minors, reservation slots), so the parallelism is in the (pod, node) pairs, not in several
+// nodes per lane (a 50k-node round then had < 1 wave per SIMD).  The per-(pod, tile) statistics are combined over the
+// block's waves in LDS.
+constexpr int kXrEvalPpw = 2;
+__global__ __launch_bounds__(kTile) void xr_eval(DevTable T, const RsvNode* __restrict__ RN,
+                                                 const int32_t* __restrict__ rsv_n, const DevPod* __restrict__ pods,
+                                                 const RsvPod* __restrict__ rpods, int64_t n, int nt, int64_t stride,
+                                                 EvalParams P, RsvParams RP, RsvExt X, uint64_t* __restrict__ val,
+                                                 uint32_t* __restrict__ val2, uint32_t* __restrict__ affk,
+                                                 uint64_t* __restrict__ part,
+                                                 const unsigned long long* __restrict__ ws) {
+  __shared__ uint64_t s_st[kTile / kWave][kXrNorm];
   int64_t first;
   int nb;
   if (!xr_range(ws, first, nb)) return;
-  int tile, p0;
-  xr_tile_coords(kXrPods / kXrPpw, tile, p0);
-  if (tile >= nt || p0 >= nb) return;
-  const int lane = threadIdx.x % kWave;
-  const int p1 = p0 + kXrPpw < nb ? p0 + kXrPpw : nb;
+  constexpr int n_pg = kXrPods / kXrEvalPpw;
+  const uint32_t nwg = gridDim.x, bid = blockIdx.x, xcd = bid % 8u, q8 = nwg / 8u, r8 = nwg % 8u;
+  const uint32_t wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8u;  // XCD-aware swizzle
+  const int tile = (int)(wgid / (uint32_t)n_pg), p0 = (int)(wgid % (uint32_t)n_pg) * kXrEvalPpw;
+  if (tile >= nt || p0 >= nb) return;  // block-uniform
+  const int tid = threadIdx.x, lane = tid % kWave, wave = tid / kWave;
+  const int p1 = p0 + kXrEvalPpw < nb ? p0 + kXrEvalPpw : nb;
+  const int64_t i = (int64_t)tile * kTile + tid;
   for (int k = p0; k < p1; ++k) {
     const int64_t j = first + k;
-    const DevPod p = pods[j];
-    const RsvPod rp = rpods[j];
-    const DsPod* dp = X.ds ? &X.dpods[j] : nullptr;
-    const NumaPod* np = X.ns ? &X.npods[j] : nullptr;
-    const int64_t* aux = (X.paux && (p.flags & P_AUX)) ? X.paux + (size_t)j * kAux : nullptr;
-    const DefPod* df = X.defp ? &X.defp[j] : nullptr;
-    RsvExt Xk = X;
-    Xk.aff = X.aff ? affk + (size_t)k * stride : nullptr;  // rsv_eval_node stores the NUMA affinity per node
     uint64_t pk = 0;
-    uint32_t m[4] = {0, 0, 0, 0}, c[4] = {0, 0, 0, 0};
-#pragma unroll
-    for (int q = 0; q < kNPT; ++q) {
-      int64_t i = (int64_t)tile * kTile + q * kWave + lane;
-      asm volatile("" : "+v"(i));  // keep the per-node addresses inside the loop (register pressure)
-      if (i >= n) break;
+    uint32_t m[4] = {0, 0, 0, 0};
+    if (i < n) {
+      const DevPod p = pods[j];
+      const RsvPod rp = rpods[j];
+      const DsPod* dp = X.ds ? &X.dpods[j] : nullptr;
+      const NumaPod* np = X.ns ? &X.npods[j] : nullptr;
+      const int64_t* aux = (X.paux && (p.flags & P_AUX)) ? X.paux + (size_t)j * kAux : nullptr;
+      const DefPod* df = X.defp ? &X.defp[j] : nullptr;
+      RsvExt Xk = X;
+      Xk.aff = X.aff ? affk + (size_t)k * stride : nullptr;  // rsv_eval_node stores the NUMA affinity per node
       const RsvOut o = rsv_eval_node(T, RN, rsv_n, i, p, rp, P, RP, Xk, dp, np, nullptr, aux, df);
       uint64_t v = 0;
       uint32_t v2 = 0;
       if (o.feas) {
         v = rsv_pack(o);
         v2 = ((uint32_t)o.tcnt << 24) | (uint32_t)o.asum;
-        const uint64_t k2 = rsv_pref_key(o, (uint32_t)i);
-        pk = k2 > pk ? k2 : pk;
-        xr_acc((uint32_t)o.raw + 1u, m[0], c[0]);
-        xr_acc((uint32_t)o.dsraw + 1u, m[1], c[1]);
-        xr_acc((uint32_t)o.tcnt + 1u, m[2], c[2]);
-        xr_acc((uint32_t)o.asum + 1u, m[3], c[3]);
+        pk = rsv_pref_key(o, (uint32_t)i);
+        m[0] = (uint32_t)o.raw + 1u;
+        m[1] = (uint32_t)o.dsraw + 1u;
+        m[2] = (uint32_t)o.tcnt + 1u;
+        m[3] = (uint32_t)o.asum + 1u;
       }
       val[(size_t)k * stride + i] = v;
       if (val2) val2[(size_t)k * stride + i] = v2;
@@ -101,13 +104,29 @@ __global__ __launch_bounds__(kWave* kEvalWaves) void xr_eval(DevTable T, const R
     pk = wave_max_u64_dpp(pk);
     uint64_t s[4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) s[q] = xr_wave_maxcount(m[q], c[q]);
+    for (int q = 0; q < 4; ++q) s[q] = xr_wave_maxcount(m[q], m[q] != 0 ? 1u : 0u);
     if (lane == 0) {
-      uint64_t* o = part + ((size_t)k * nt + tile) * kXrNorm;
-      o[0] = pk;
+      s_st[wave][0] = pk;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) o[1 + q] = s[q];
+      for (int q = 0; q < 4; ++q) s_st[wave][1 + q] = s[q];
     }
+    __syncthreads();
+    if (tid < kXrNorm) {  // thread q combines statistic q over the block's waves
+      uint64_t r = 0;
+      if (tid == 0) {
+        for (int w = 0; w < kTile / kWave; ++w) r = s_st[w][0] > r ? s_st[w][0] : r;
+      } else {
+        uint32_t M = 0, C = 0;
+        for (int w = 0; w < kTile / kWave; ++w) {
+          const uint32_t vm = (uint32_t)(s_st[w][tid] >> 32), vc = (uint32_t)s_st[w][tid];
+          C = vm > M ? vc : C + (vm == M ? vc : 0u);
+          M = vm > M ? vm : M;
+        }
+        r = ((uint64_t)M << 32) | C;
+      }
+      part[((size_t)k * nt + tile) * kXrNorm + tid] = r;
+    }
+    __syncthreads();
   }
 }
 
@@ -238,6 +257,7 @@ __global__ __launch_bounds__(kWave) void xr_resolve(DevTable T, RsvNode* __restr
   int nM = 0, consumed = 0;
   const bool dscore = val2 != nullptr;
   for (int j = 0; j < nb; ++j) {
+    KG_POD_DIAG(j, (uint32_t)nM);
     const int64_t jj = first + j;
     const DevPod p = pods[jj];
     // ElasticQuota PreFilter against every earlier Reserve (lane 0 owns the quota rows)
@@ -272,6 +292,7 @@ __global__ __launch_bounds__(kWave) void xr_resolve(DevTable T, RsvNode* __restr
       ov = val[(size_t)j * stride + midx];
       ov2 = dscore ? val2[(size_t)j * stride + midx] : 0u;
     }
+    KG_POD_SUB(j, 0);
     const uint64_t* nk = norm + (size_t)j * kXrNorm;
     bool stop = false;
     {  // the normalisation of pod j must equal the round's
@@ -298,6 +319,7 @@ __global__ __launch_bounds__(kWave) void xr_resolve(DevTable T, RsvNode* __restr
       }
     }
     if (stop) break;
+    KG_POD_SUB(j, 1);
     const XrNorms N = xr_norms(nk);
     const uint64_t mkey = (lane < nM && cur.feas)
                               ? make_key(rsv_total(cv, cv2, (int64_t)midx == N.pref, N.mx, N.mds, N.mt, N.ma, RP, X), midx)
@@ -326,6 +348,7 @@ __global__ __launch_bounds__(kWave) void xr_resolve(DevTable T, RsvNode* __restr
       if (lane == 0) bitmap[w >> 5] |= 1u << (w & 31);
       ++nM;
     }
+    KG_POD_SUB(j, 2);
     int placed = 0, slot = -1;
     if (lane == owner) {
       uint64_t v = cv;
@@ -339,6 +362,7 @@ __global__ __launch_bounds__(kWave) void xr_resolve(DevTable T, RsvNode* __restr
       slot = s;
     }
     placed = __builtin_amdgcn_readlane(placed, owner);
+    KG_POD_SUB(j, 3);
     slot = __builtin_amdgcn_readlane(slot, owner);
     if (lane == 0) {
       out_keys[jj] = placed ? best : 0;
@@ -347,6 +371,7 @@ __global__ __launch_bounds__(kWave) void xr_resolve(DevTable T, RsvNode* __restr
     }
     __syncthreads();
   }
+  KG_POD_DIAG(consumed, 0u);
   __threadfence();
   if (lane == 0) {
     ws[3] = (unsigned long long)(first + consumed);
