@@ -418,6 +418,16 @@ void kg_loopback_destroy(kg_loopback* lb);
 int kg_engine_create_loopback(const kg_config* cfg, int64_t capacity_nodes, int rank, int n_ranks, kg_loopback* lb,
                               kg_engine** out);
 
+/* Host-collective rank (test hook / RCCL-less deployments): a multi-rank engine whose per-round exchanges go through
+ * the caller's all-gather instead of RCCL — e.g. torch.distributed gloo across processes.  `exchange` receives this
+ * rank's `bytes` (host memory, already copied back from the device) and must fill `recv` with every rank's part in
+ * rank order ([n_ranks][bytes]); it returns 0 on success.  The engine synchronises the round's stream around each
+ * exchange, so this path is slow; every other step is the multi-rank engine itself.  Every rank must make the same
+ * engine calls in the same order, as with RCCL. */
+typedef int (*kg_exchange_fn)(void* user, const void* send, void* recv, int64_t bytes);
+int kg_engine_create_hosted(const kg_config* cfg, int64_t capacity_nodes, int rank, int n_ranks,
+                            kg_exchange_fn exchange, void* user, kg_engine** out);
+
 int kg_nodes_upsert(kg_engine* e, const kg_node* nodes, const int32_t* idx, int64_t n);
 int kg_nodes_delete(kg_engine* e, const int32_t* idx, int64_t n);
 int kg_node_metrics_update(kg_engine* e, const kg_node_metric* m, const int32_t* idx, int64_t n, int64_t now_unix_nano);

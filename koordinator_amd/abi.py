@@ -180,7 +180,11 @@ EXPORTED_SYMBOLS = (
     "kg_results_fetch_reservations", "kg_profile_enable", "kg_profile_read", "kg_loopback_create",
     "kg_loopback_destroy", "kg_engine_create_loopback", "kg_pods_unreserve", "kg_engine_set_clock",
     "kg_node_pods_metric_set", "kg_debug_numa_merge", "kg_pods_evaluate_reservation", "kg_nodes_predicates_upsert",
+    "kg_engine_create_hosted",
 )
+
+# int (*kg_exchange_fn)(void* user, const void* send, void* recv, int64_t bytes)
+EXCHANGE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64)
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("KOORDGPU_LIB") or os.path.join(PKG_DIR, "libkoordgpu.so")
@@ -255,6 +259,7 @@ def load_library(path: str | None = None):
         "kg_debug_numa_merge": (i, [vp, vp, i64, vp]),
         "kg_pods_evaluate_reservation": (i, [vp, vp, vp]),
         "kg_nodes_predicates_upsert": (i, [vp, vp, vp, i64]),
+        "kg_engine_create_hosted": (i, [vp, i64, i, i, EXCHANGE_FN, vp, ctypes.POINTER(vp)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)

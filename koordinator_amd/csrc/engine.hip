@@ -2009,6 +2009,9 @@ struct kg_engine {
   kg_config cfg;
   int rank = 0, n_ranks = 1;
   kg_loopback* lb = nullptr;  // test hook: exchanges through device copies instead of RCCL
+  kg_exchange_fn xfn = nullptr;  // host collective (kg_engine_create_hosted): exchanges through the caller
+  void* xuser = nullptr;
+  std::vector<uint64_t> xsend, xrecv;
   hipEvent_t lb_ready = nullptr, lb_done = nullptr;
   int device = 0;
   hipStream_t stream = nullptr;
@@ -2970,6 +2973,17 @@ int lb_barrier(kg_loopback* lb) {
 // All-gather of `cnt` words per rank in `all` ([n_ranks][cnt], this rank's part already written on stream st):
 // ncclAllGather over RCCL, or — loopback test hook — device copies from the peers' buffers, ordered by events.
 int rank_allgather(kg_engine* e, uint64_t* all, size_t cnt, int slot, hipStream_t st) {
+  if (e->xfn) {  // host collective: this rank's part back to the host, the caller's all-gather, every part up again
+    e->xsend.resize(cnt);
+    e->xrecv.resize(cnt * (size_t)e->n_ranks);
+    HIP_TRY(hipMemcpyAsync(e->xsend.data(), all + (size_t)e->rank * cnt, cnt * 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    if (int rc = e->xfn(e->xuser, e->xsend.data(), e->xrecv.data(), (int64_t)(cnt * 8)))
+      return fail(KG_E_COLLECTIVE, "host exchange returned %d", rc);
+    HIP_TRY(hipMemcpyAsync(all, e->xrecv.data(), cnt * 8 * (size_t)e->n_ranks, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipStreamSynchronize(st));  // the host buffers are reused by the next exchange
+    return 0;
+  }
   if (!e->lb) {
     NCCL_TRY(ncclAllGather(all + (size_t)e->rank * cnt, all, cnt, ncclUint64, e->comms[slot], st));
     return 0;
@@ -3474,13 +3488,13 @@ int kg_nccl_unique_id(void* out128) {
 }
 
 static int engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank, int n_ranks, const void* nccl_id,
-                         kg_loopback* lb, kg_engine** out) {
+                         kg_loopback* lb, kg_engine** out, kg_exchange_fn xfn = nullptr, void* xuser = nullptr) {
   if (!out) return fail(KG_E_INVALID, "out is NULL");
   *out = nullptr;
   if (int rc = validate_config(cfg)) return rc;
   if (capacity_nodes <= 0 || capacity_nodes > kMaxNodes) return fail(KG_E_INVALID, "capacity_nodes out of range");
   if (n_ranks < 1 || rank < 0 || rank >= n_ranks) return fail(KG_E_INVALID, "rank/n_ranks");
-  if (n_ranks > 1 && !nccl_id && !lb) return fail(KG_E_INVALID, "nccl_unique_id required for n_ranks>1");
+  if (n_ranks > 1 && !nccl_id && !lb && !xfn) return fail(KG_E_INVALID, "nccl_unique_id required for n_ranks>1");
   if (lb) {
     std::lock_guard<std::mutex> lk(lb->mu);
     if (lb->n != n_ranks) return fail(KG_E_INVALID, "loopback group of %d ranks, engine n_ranks %d", lb->n, n_ranks);
@@ -3692,6 +3706,9 @@ static int engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank,
     lb->ranks[rank] = e;
     lb->ready[rank] = e->lb_ready;
     lb->done[rank] = e->lb_done;
+  } else if (xfn) {
+    e->xfn = xfn;
+    e->xuser = xuser;
   } else if (n_ranks > 1) {
     ncclUniqueId id;
     std::memcpy(&id, nccl_id, sizeof(id));
@@ -3724,6 +3741,12 @@ int kg_loopback_create(int n_ranks, kg_loopback** out) {
 }
 
 void kg_loopback_destroy(kg_loopback* lb) { delete lb; }
+
+int kg_engine_create_hosted(const kg_config* cfg, int64_t capacity_nodes, int rank, int n_ranks,
+                            kg_exchange_fn exchange, void* user, kg_engine** out) {
+  if (!exchange) return fail(KG_E_INVALID, "exchange function is NULL");
+  return engine_create(cfg, capacity_nodes, rank, n_ranks, nullptr, nullptr, out, exchange, user);
+}
 
 int kg_engine_create_loopback(const kg_config* cfg, int64_t capacity_nodes, int rank, int n_ranks, kg_loopback* lb,
                               kg_engine** out) {

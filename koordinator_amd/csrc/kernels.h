@@ -589,11 +589,14 @@ struct HotRow {
   uint32_t flags;
 };
 
-// 100 / capacity as the host's ingest writes the reciprocal columns (sync_static: IEEE double division, then the cpu
-// estimate rounded to f32), computed where a tile's rows are hoisted so that the wide pass does not read those
-// columns (24 B per node); the values are bit-identical to the columns the resolvers read.
-__device__ __forceinline__ float inv100_f32(int64_t c) { return c > 0 ? (float)(100.0 / (double)c) : 0.0f; }
-__device__ __forceinline__ double inv100_f64(int64_t c) { return c > 0 ? 100.0 / (double)c : 0.0; }
+// 100 / capacity for the cpu terms from v_rcp_f32 (≤ 2 ulp), computed where a tile's rows are hoisted so that the
+// wide pass does not read the f32 reciprocal columns: lrs_cpu needs only an estimate within ±1 of the quotient (its
+// 24-bit multiply-compare corrects it both ways; relative error ≤ 2^-22 on a value ≤ 100), and inside the domain the
+// capacity is < 2^24, so (float)c is exact.  The f64 memory reciprocals stay columns: lrs_mem's one-sided correction
+// needs them correctly rounded, and an in-kernel IEEE division per node cost the pass ~10 % (measured).
+__device__ __forceinline__ float inv100_f32(int64_t c) {
+  return c > 0 ? 100.0f * __builtin_amdgcn_rcpf((float)c) : 0.0f;
+}
 
 template <int PF>
 __device__ __forceinline__ HotRow load_hot(const DevTable& T, int64_t i, const EvalParams& P) {
@@ -635,11 +638,11 @@ __device__ __forceinline__ HotRow load_hot(const DevTable& T, int64_t i, const E
   h.free_mem = (double)fm;
   h.fnz_mem = (double)fnm;
   h.alloc_mem = (double)am;
-  h.inv_mem = kFitS ? inv100_f64(am) : 0.0;
+  h.inv_mem = kFitS ? T.inv_mem[i] : 0.0;
   h.la_free_mem = (double)lfm;
   h.la_pfree_mem = (double)lpm;
   h.la_alloc_mem = (double)lam;
-  h.la_inv_mem = la_row ? inv100_f64(lam) : 0.0;
+  h.la_inv_mem = la_row ? T.inv_mem[T.cap + i] : 0.0;
   h.flags = (fl & ~(F_RARE | F_PODS_OK)) | ((fl & F_VALID) && pods_ok ? F_PODS_OK : 0u) | (ok ? 0u : F_RARE);
   return h;
 }

@@ -47,18 +47,45 @@ class Loopback:
         self.close()
 
 
+class HostExchange:
+    """kg_engine_create_hosted's exchange over a caller-side all-gather: `allgather(send: bytes-like uint8 array)`
+    returns the n_ranks parts concatenated in rank order — e.g. torch.distributed.all_gather on gloo CPU tensors,
+    so that several processes run the engine's multi-rank round path without RCCL."""
+
+    def __init__(self, allgather):
+        self.allgather = allgather
+        self.error = None
+
+        def _fn(user, send, recv, nbytes):
+            try:
+                buf = np.ctypeslib.as_array(ctypes.cast(send, ctypes.POINTER(ctypes.c_uint8)), shape=(int(nbytes),))
+                out = np.ascontiguousarray(self.allgather(buf.copy()), dtype=np.uint8).reshape(-1)
+                ctypes.memmove(recv, out.ctypes.data, out.nbytes)
+                return 0
+            except Exception as exc:  # reported through the engine's KG_E_COLLECTIVE
+                self.error = exc
+                return 1
+
+        self.fn = abi.EXCHANGE_FN(_fn)  # kept alive as long as the engine
+
+
 class Engine:
     """One engine = one rank's GPU-resident node table (replicated) + its evaluation shard."""
 
     def __init__(self, config: np.ndarray, capacity: int, rank: int = 0, n_ranks: int = 1,
-                 nccl_id: bytes | None = None, loopback: Loopback | None = None):
+                 nccl_id: bytes | None = None, loopback: Loopback | None = None,
+                 exchange: HostExchange | None = None):
         self.lib = abi.load_library()
         self._cfg = np.array(config, dtype=abi.CONFIG_DTYPE).reshape(1)
         h = ctypes.c_void_p()
         idbuf = None
         if nccl_id is not None:
             idbuf = ctypes.create_string_buffer(bytes(nccl_id), 128)
-        if loopback is not None:
+        self._exchange = exchange
+        if exchange is not None:
+            check(self.lib, self.lib.kg_engine_create_hosted(ptr(self._cfg), int(capacity), int(rank), int(n_ranks),
+                                                             exchange.fn, None, ctypes.byref(h)))
+        elif loopback is not None:
             check(self.lib, self.lib.kg_engine_create_loopback(ptr(self._cfg), int(capacity), int(rank), int(n_ranks),
                                                                loopback.h, ctypes.byref(h)))
         else:
