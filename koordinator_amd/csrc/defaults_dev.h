@@ -96,7 +96,7 @@ __device__ __forceinline__ int64_t balanced_score(int64_t alloc_cpu, int64_t all
 // DefaultNormalizeScore (helper/normalize_score.go) of one node's raw score against the feasible nodes' maximum
 __device__ __forceinline__ int64_t normalize_default(int64_t raw, int64_t mx, bool reverse) {
   if (mx == 0) return reverse ? 100 : raw;
-  const int64_t s = 100 * raw / mx;
+  const int64_t s = div_small(100 * raw, mx);
   return reverse ? 100 - s : s;
 }
 

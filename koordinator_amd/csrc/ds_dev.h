@@ -75,9 +75,14 @@ __device__ __forceinline__ DsInst ds_instance(const DsNode& d, const DsPod& p) {
   if (ratio > 100 && ratio % 100 == 0) {
     const int64_t n = ratio / 100;
     in.count = (int32_t)n;
-    core /= n;
-    mem /= n;
-    ratio /= n;
+    // x / n for 0 ≤ x < 2^52 and n ≥ 2: trunc of the correctly rounded f64 quotient is exact (a quotient just
+    // below an integer k is ≤ k - 1/n, far more than an ulp below it), and avoids three 64-bit divide expansions
+    auto qdiv = [](int64_t x, int64_t d) -> int64_t {
+      return (x >= 0 && x < (1ll << 52)) ? (int64_t)((double)x / (double)d) : x / d;
+    };
+    core = qdiv(core, n);
+    mem = qdiv(mem, n);
+    ratio = qdiv(ratio, n);
   }
   in.ok = 1;
   in.core = core;

@@ -3282,6 +3282,18 @@ int run_rsv(kg_engine* e, int64_t first, int64_t count, kg_stats* stats, double 
   return 0;
 }
 
+#define KG_XF_SWITCH(xf, CALL)    \
+  switch (xf) {                   \
+    case 0: CALL(0); break;       \
+    case 1: CALL(1); break;       \
+    case 2: CALL(2); break;       \
+    case 3: CALL(3); break;       \
+    case 4: CALL(4); break;       \
+    case 5: CALL(5); break;       \
+    case 6: CALL(6); break;       \
+    default: CALL(7); break;      \
+  }
+
 // Batched exact rounds (xr_dev.h): rounds of kXrPods pods, kXrGraphRounds rounds per hipGraph launch; the host
 // launches about as many rounds as the pods left need at the recent consumption rate, then checks the cursor.
 constexpr int kXrGraphRounds = 4;
@@ -3298,16 +3310,21 @@ int run_xr(kg_engine* e, int64_t first, int64_t count, kg_stats* stats, double t
   const unsigned xr_eval_blocks = (unsigned)nt * (kXrPods / kXrEvalPpw);
   const int vbits = e->P.score_bits + 1;
   const int bitmap_words = (int)((n + 31) / 32);
-  const size_t lds = (size_t)kXrPods * (kC + 1) * 8 + (size_t)bitmap_words * 4;
+  const int xf = (X.ns ? XF_NUMA : 0) | (X.ds ? XF_DS : 0) | (X.defp ? XF_DEF : 0);
+  const size_t lds = xr_resolve_lds_bytes(xf, X.nq, X.paux != nullptr, bitmap_words);
+  if (lds > 160 * 1024) return fail(KG_E_UNSUPPORTED, "exact rounds: %zu B of LDS for %lld nodes", lds, (long long)n);
   const int32_t* poison = reinterpret_cast<const int32_t*>(e->rsv_ws.p + 7);  // stays 0
   uint64_t* val = e->xr_val.p;
   uint32_t* val2 = e->def_score ? e->xr_val2.p : nullptr;
   uint32_t* affk = e->numa_on ? e->xr_aff.p : nullptr;
   auto issue_round = [&]() {
     size_t t = prof_begin(e, e->stream);
-    xr_eval<<<xr_eval_blocks, kTile, 0, e->stream>>>(e->T, e->rsv_d.p, e->rsv_nd.p, e->pods.p, e->rpods.p, n, nt,
-                                                             stride, e->P, e->RP, X, val, val2, affk, e->xr_part.p,
-                                                             e->rsv_ws.p);
+#define KG_XR_EVAL(XF)                                                                                        \
+  xr_eval<XF><<<xr_eval_blocks, kTile, 0, e->stream>>>(e->T, e->rsv_d.p, e->rsv_nd.p, e->pods.p, e->rpods.p, n, nt, \
+                                                       stride, e->P, e->RP, X, val, val2, affk, e->xr_part.p,     \
+                                                       e->rsv_ws.p)
+    KG_XF_SWITCH(xf, KG_XR_EVAL);
+#undef KG_XR_EVAL
     prof_end(e, KG_PROF_RSV_EVAL, t, e->stream);
     t = prof_begin(e, e->stream);
     xr_norm<<<kXrPods, 256, 0, e->stream>>>(e->xr_part.p, nt, e->xr_norm_d.p, e->rsv_ws.p);
@@ -3317,9 +3334,12 @@ int run_xr(kg_engine* e, int64_t first, int64_t count, kg_stats* stats, double t
                                                                  kR, kXrPods, poison, e->xr_cand.p);
     prof_end(e, KG_PROF_RSV_SELECT, t, e->stream);
     t = prof_begin(e, e->stream);
-    xr_resolve<<<1, kWave, lds, e->stream>>>(e->T, e->rsv_d.p, e->rsv_nd.p, e->pods.p, e->rpods.p, stride, e->P, e->RP, X,
-                                             val, val2, affk, e->xr_norm_d.p, e->xr_cand.p, bitmap_words,
-                                             e->out_keys.p, e->out_rslot.p, e->rsv_ws.p);
+#define KG_XR_RESOLVE(XF)                                                                                      \
+  xr_resolve<XF><<<1, kWave, lds, e->stream>>>(e->T, e->rsv_d.p, e->rsv_nd.p, e->pods.p, e->rpods.p, stride, e->P, \
+                                               e->RP, X, val, val2, affk, e->xr_norm_d.p, e->xr_cand.p,          \
+                                               bitmap_words, e->out_keys.p, e->out_rslot.p, e->rsv_ws.p)
+    KG_XF_SWITCH(xf, KG_XR_RESOLVE);
+#undef KG_XR_RESOLVE
     prof_end(e, KG_PROF_RSV_APPLY, t, e->stream);
   };
   static const bool no_graph = std::getenv("KG_RSV_NO_GRAPH") && std::getenv("KG_RSV_NO_GRAPH")[0] == '1';
@@ -3581,9 +3601,10 @@ static int engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank,
   e->def_on = c.taint_filter || c.taint_score || c.affinity_filter || c.affinity_score || c.balanced_score;
   e->def_score = c.taint_score || c.affinity_score;
   e->exact_on = e->rsv_on || (e->numa_on && e->ds_on) || e->def_on;
-  if (e->exact_on && n_ranks > 1)
-    return bail(fail(KG_E_UNSUPPORTED, "Reservation / NodeNUMAResource + DeviceShare / TaintToleration / NodeAffinity / "
-                                       "BalancedAllocation profiles run on one rank"));
+  // Exact profiles (Reservation, NodeNUMAResource + DeviceShare, the upstream defaults) on several ranks run as
+  // replicas: every rank evaluates its full replica of the table and resolves the same FIFO order, so no exchange is
+  // needed and every rank holds the same placements (the exact rounds' stop rule reads the round-start
+  // values of the modified rows, which a node-sharded pass would hold on another rank only).
   e->DF = DefParams{(int32_t)(c.taint_filter != 0), (int32_t)(c.taint_score != 0), (int32_t)c.weight_taint,
                     (int32_t)(c.affinity_filter != 0), (int32_t)(c.affinity_score != 0), (int32_t)c.weight_affinity,
                     (int32_t)(c.balanced_score != 0), (int32_t)c.weight_balanced,
@@ -3625,6 +3646,12 @@ static int engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank,
     if (int rc = e->xr_cand.ensure((size_t)kXrPods * kCandStride)) return bail(rc);
     if (hipMemset(e->xr_lists.p, 0, (size_t)kXrPods * nt * kR * 8) != hipSuccess)
       return bail(fail(KG_E_DEVICE, "hipMemset"));
+    hipError_t fe = hipSuccess;
+#define KG_XR_ATTR(XF) \
+  fe = hipFuncSetAttribute((const void*)xr_resolve<XF>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024)
+    for (int xf = 0; xf < 8 && fe == hipSuccess; ++xf) KG_XF_SWITCH(xf, KG_XR_ATTR);
+#undef KG_XR_ATTR
+    if (fe != hipSuccess) return bail(fail(KG_E_DEVICE, "hipFuncSetAttribute(xr_resolve LDS)"));
   }
   const int64_t max_total = 100 * ((c.fit_score ? c.weight_fit : 0) + (c.la_score ? c.weight_loadaware : 0) +
                                    (c.numa_score ? c.weight_numa : 0) + (c.ds_score ? c.weight_deviceshare : 0) +

@@ -197,7 +197,9 @@ __device__ __forceinline__ int64_t least_requested(int64_t requested, int64_t ca
   const int64_t x = capacity - requested;
   const int64_t num = x * 100;
   if (requested < 0) return num / capacity;
-  int q = (int)(((float)x * 100.0f) / (float)capacity);
+  // quotient estimate from v_rcp_f32 (relative error ≤ 2^-21 on a value ≤ 100: within ±1 of the exact quotient,
+  // which the two int64 compares then restore — no IEEE division sequence)
+  int q = (int)(((float)x * 100.0f) * __builtin_amdgcn_rcpf((float)capacity));
   q = q < 0 ? 0 : (q > 100 ? 100 : q);
   const int64_t t = (int64_t)q * capacity;
   if (t > num) q -= 1;
@@ -212,7 +214,7 @@ __device__ __forceinline__ int64_t most_requested64(int64_t requested, int64_t c
   if (requested > capacity) requested = capacity;
   const int64_t num = requested * 100;
   if (requested < 0) return num / capacity;
-  int q = (int)(((float)requested * 100.0f) / (float)capacity);
+  int q = (int)(((float)requested * 100.0f) * __builtin_amdgcn_rcpf((float)capacity));  // as least_requested
   q = q < 0 ? 0 : (q > 100 ? 100 : q);
   const int64_t t = (int64_t)q * capacity;
   if (t > num) q -= 1;

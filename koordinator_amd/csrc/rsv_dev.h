@@ -103,19 +103,22 @@ __device__ __forceinline__ int64_t rsv_nz_mem(const RsvNode& rn, int s) {
   return rn.alloc_mem[s] > 0 ? rn.alloc_mem[s] : kDefaultMemory;
 }
 
-// scoreReservation (scoring.go:183-203): MostAllocated over the reservation's non-zero allocatable.
+// scoreReservation (scoring.go:183-203): MostAllocated over the reservation's non-zero allocatable.  Division-free:
+// 100·r / a for 0 ≤ r ≤ a is most_requested64 (float estimate + one exact int64 correction each way), and Σ / #r
+// divides by 1 or 2 (a non-negative sum: a shift).
 __device__ __forceinline__ int32_t rsv_score_slot(const RsvNode& rn, int s, const DevPod& p) {
   const int64_t rc = p.req_cpu + rn.allocd_cpu[s], rm = p.req_mem + rn.allocd_mem[s];
   int64_t w = 0, sc = 0;
   if (rn.alloc_cpu[s] != 0) {
     ++w;
-    if (rc <= rn.alloc_cpu[s]) sc += 100 * rc / rn.alloc_cpu[s];
+    if (rc <= rn.alloc_cpu[s]) sc += rc >= 0 ? most_requested64(rc, rn.alloc_cpu[s]) : 100 * rc / rn.alloc_cpu[s];
   }
   if (rn.alloc_mem[s] != 0) {
     ++w;
-    if (rm <= rn.alloc_mem[s]) sc += 100 * rm / rn.alloc_mem[s];
+    if (rm <= rn.alloc_mem[s]) sc += rm >= 0 ? most_requested64(rm, rn.alloc_mem[s]) : 100 * rm / rn.alloc_mem[s];
   }
-  return w ? (int32_t)(sc / w) : 0;
+  if (w == 2) return (int32_t)(sc >= 0 ? sc >> 1 : sc / 2);
+  return (int32_t)sc;
 }
 
 // Per-node outputs kg_pods_evaluate_reservation reports besides RsvOut (nullptr in the scheduling pass)
@@ -259,14 +262,17 @@ __device__ __forceinline__ RsvOut rsv_eval_node(const DevTable& T, const RsvNode
       }
     }
     o.order = best_all;
+    // every satisfied slot's score once (the nominated slot's is its raw Reservation Score)
+    int32_t ssc[kRsvSlots];
+#pragma unroll
+    for (int s = 0; s < kRsvSlots; ++s) ssc[s] = (sat >> s & 1) ? rsv_score_slot(rn, s, p) : 0;
     if (pick < 0) {
       int32_t best = -1;
 #pragma unroll
       for (int s = 0; s < kRsvSlots; ++s)
         if (sat >> s & 1) {
-          const int32_t sc = rsv_score_slot(rn, s, p);
-          if (sc > best) {  // prioritizeReservations + sort (unstable; pinned: lowest slot on ties)
-            best = sc;
+          if (ssc[s] > best) {  // prioritizeReservations + sort (unstable; pinned: lowest slot on ties)
+            best = ssc[s];
             pick = s;
           }
         }
@@ -275,7 +281,7 @@ __device__ __forceinline__ RsvOut rsv_eval_node(const DevTable& T, const RsvNode
     int32_t raw = 0;
 #pragma unroll
     for (int s = 0; s < kRsvSlots; ++s)
-      if (s == pick) raw = rsv_score_slot(rn, s, p);
+      if (s == pick) raw = ssc[s];
     o.raw = raw;
   }
   return o;
@@ -357,6 +363,7 @@ __device__ __forceinline__ void rsv_quota_charge(const RsvExt& X, const DevPod& 
 // Reserve of pod j on its winner row w: DeviceShare first (a failure un-assumes the pod: nothing is placed), then
 // NodeInfo + LoadAware assign cache and reservationCache.assumePod on the slot nominated there
 // (reservation_info.go:317-326).  Called by the one thread that owns row w.  Returns false when not placed.
+template <bool NUMA = true, bool DS = true>  // compile-time: the profile's plugins (batched exact rounds)
 __device__ __forceinline__ bool rsv_reserve(const DevTable& T, RsvNode* __restrict__ RN, int64_t w, uint64_t v,
                                             const DevPod& p, const RsvExt& X, int64_t j, int32_t& slot_out) {
   slot_out = -1;
@@ -366,7 +373,7 @@ __device__ __forceinline__ bool rsv_reserve(const DevTable& T, RsvNode* __restri
   CpuSet cpus = cs_zero();
   NumaAlloc rec;
   rec.res = 0;
-  if (X.ns) {
+  if (NUMA && X.ns) {
     const NumaStatic nsw = X.ns[w];
     nmw = X.nm[w];
     const NumaView nv = make_view(&nsw, &nmw, X.NP);
@@ -377,7 +384,7 @@ __device__ __forceinline__ bool rsv_reserve(const DevTable& T, RsvNode* __restri
       return false;
     }
   }
-  if (X.ds) {
+  if (DS && X.ds) {
     DsNode dn = X.ds[w];
     const int32_t minors = rsv_ds_reserve(dn, X.dpods[j], X.DP);
     if (minors < 0) {
@@ -387,7 +394,7 @@ __device__ __forceinline__ bool rsv_reserve(const DevTable& T, RsvNode* __restri
     if (minors) const_cast<DsNode*>(X.ds)[w] = dn;
     X.out_minors[j] = minors;
   }
-  if (X.ns) {
+  if (NUMA && X.ns) {
     X.nm[w] = nmw;
 #pragma unroll
     for (int q = 0; q < kCpuWords; ++q) X.out_cpus[(size_t)j * kCpuWords + q] = cpus.w[q];
@@ -535,8 +542,8 @@ __device__ __forceinline__ int64_t rsv_total(uint64_t v, uint32_t v2, bool is_pr
                                              int64_t mt, int64_t ma, const RsvParams& RP, const RsvExt& X) {
   const int64_t raw = is_pref ? 1000 : (int64_t)((v >> 8) & 0xff);  // mostPreferredScore
   int64_t t = (int64_t)(v >> 32);
-  if (RP.score && mx > 0) t += (int64_t)RP.weight * (100 * raw / mx);
-  if (X.DP.score && mds > 0) t += (int64_t)X.DP.weight * (100 * (int64_t)((v >> 16) & 0xff) / mds);
+  if (RP.score && mx > 0) t += (int64_t)RP.weight * div_small(100 * raw, mx);
+  if (X.DP.score && mds > 0) t += (int64_t)X.DP.weight * div_small(100 * (int64_t)((v >> 16) & 0xff), mds);
   if (X.DF.taint_score) t += (int64_t)X.DF.w_taint * normalize_default(v2 >> 24, mt, true);
   if (X.DF.aff_score) t += (int64_t)X.DF.w_aff * normalize_default(v2 & 0xFFFFFFu, ma, false);
   return t;

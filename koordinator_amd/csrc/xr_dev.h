@@ -22,6 +22,9 @@
 constexpr int kXrPods = 32;      // pods per round (< kWave: one modified row per resolver lane)
 constexpr int kXrPpw = 8;        // pods per eval / select wave
 constexpr int kXrNorm = 5;       // per-pod statistics: preferred key, raw Reservation, DeviceShare, taint, affinity
+// Exact-round features (compile-time: the kernels carry only the plugins the profile enables, so the Fit /
+// LoadAware / Reservation-only variants keep their registers, and none spills for code it never runs)
+constexpr int XF_NUMA = 1, XF_DS = 2, XF_DEF = 4;
 static_assert(kXrPods < kWave, "resolver lanes");
 
 __device__ __forceinline__ bool xr_range(const unsigned long long* __restrict__ ws, int64_t& first, int& nb) {
@@ -54,6 +57,7 @@ __device__ __forceinline__ void xr_tile_coords(int n_pg, int& tile, int& p0) {
 // nodes per lane (a 50k-node round then had < 1 wave per SIMD).  The per-(pod, tile) statistics are combined over the
 // block's waves in LDS.
 constexpr int kXrEvalPpw = 2;
+template <int XF>
 __global__ __launch_bounds__(kTile) void xr_eval(DevTable T, const RsvNode* __restrict__ RN,
                                                  const int32_t* __restrict__ rsv_n, const DevPod* __restrict__ pods,
                                                  const RsvPod* __restrict__ rpods, int64_t n, int nt, int64_t stride,
@@ -80,10 +84,10 @@ __global__ __launch_bounds__(kTile) void xr_eval(DevTable T, const RsvNode* __re
     if (i < n) {
       const DevPod p = pods[j];
       const RsvPod rp = rpods[j];
-      const DsPod* dp = X.ds ? &X.dpods[j] : nullptr;
-      const NumaPod* np = X.ns ? &X.npods[j] : nullptr;
+      const DsPod* dp = (XF & XF_DS) ? &X.dpods[j] : nullptr;
+      const NumaPod* np = (XF & XF_NUMA) ? &X.npods[j] : nullptr;
       const int64_t* aux = (X.paux && (p.flags & P_AUX)) ? X.paux + (size_t)j * kAux : nullptr;
-      const DefPod* df = X.defp ? &X.defp[j] : nullptr;
+      const DefPod* df = (XF & XF_DEF) ? &X.defp[j] : nullptr;
       RsvExt Xk = X;
       Xk.aff = X.aff ? affk + (size_t)k * stride : nullptr;  // rsv_eval_node stores the NUMA affinity per node
       const RsvOut o = rsv_eval_node(T, RN, rsv_n, i, p, rp, P, RP, Xk, dp, np, nullptr, aux, df);
@@ -230,8 +234,24 @@ __global__ __launch_bounds__(kWave* kEvalWaves) void xr_select(const uint64_t* _
   }
 }
 
-// One wave: the round's FIFO replay (see the header).  Dynamic LDS: the pods' candidate records [nb][kC + 1] and the
-// modified-node bitmap.
+constexpr int kRsvPodWords = (int)(sizeof(RsvPod) / 8), kDefPodWords = (int)((sizeof(DefPod) + 7) / 8);
+
+// LDS bytes of xr_resolve: the records, the pods' staged per-plugin records, the quota rows, the modified bitmap
+__host__ __device__ inline size_t xr_resolve_lds_bytes(int XF, int nq, bool aux, int bitmap_words) {
+  size_t w = (size_t)kXrPods * (kC + 1) + (size_t)kXrPods * (kPodWords + kRsvPodWords);
+  if (XF & XF_DS) w += (size_t)kXrPods * kDsPodWords;
+  if (XF & XF_NUMA) w += (size_t)kXrPods * kNumaPodWords;
+  if (XF & XF_DEF) w += (size_t)kXrPods * kDefPodWords;
+  if (aux) w += (size_t)kXrPods * kAux;
+  if (nq > 0) w += (size_t)nq * (sizeof(QuotaRow) / 8) + (size_t)kXrPods * kQuotaRes;
+  return w * 8 + (size_t)bitmap_words * 4;
+}
+
+// One wave: the round's FIFO replay (see the header).  Dynamic LDS: the pods' candidate records [nb][kC + 1], the
+// round's pods and their per-plugin records (DevPod, RsvPod, DsPod, NumaPod, DefPod, aux requests), the ElasticQuota
+// rows (admitted / charged in LDS, written back at the end) and the modified-node bitmap — one bulk load, so the
+// per-pod chain touches global memory only for the modified rows and the Reserve.
+template <int XF>
 __global__ __launch_bounds__(kWave) void xr_resolve(DevTable T, RsvNode* __restrict__ RN,
                                                     const int32_t* __restrict__ rsv_n,
                                                     const DevPod* __restrict__ pods,
@@ -244,28 +264,79 @@ __global__ __launch_bounds__(kWave) void xr_resolve(DevTable T, RsvNode* __restr
                                                     uint64_t* __restrict__ out_keys, int32_t* __restrict__ out_slot,
                                                     unsigned long long* __restrict__ ws) {
   extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
+  constexpr bool kNuma = (XF & XF_NUMA) != 0, kDs = (XF & XF_DS) != 0, kDef = (XF & XF_DEF) != 0;
   int64_t first;
   int nb;
   if (!xr_range(ws, first, nb)) return;
   const int lane = threadIdx.x;
-  uint64_t* s_cand = smem;  // [nb][kC + 1]
-  uint32_t* bitmap = reinterpret_cast<uint32_t*>(s_cand + (size_t)nb * (kC + 1));
-  for (int w = lane; w < nb * (kC + 1); w += kWave) s_cand[w] = cand[(size_t)(w / (kC + 1)) * kCandStride + w % (kC + 1)];
-  for (int w = lane; w < bitmap_words; w += kWave) bitmap[w] = 0;
+  const int nq = X.nq;
+  const bool has_aux = X.paux != nullptr;
+  uint64_t* s_cand = smem;                                        // [kXrPods][kC + 1]
+  uint64_t* s_podw = s_cand + (size_t)kXrPods * (kC + 1);         // [kXrPods][kPodWords]
+  uint64_t* s_rpw = s_podw + (size_t)kXrPods * kPodWords;         // [kXrPods][kRsvPodWords]
+  uint64_t* s_next = s_rpw + (size_t)kXrPods * kRsvPodWords;
+  uint64_t* s_dpw = s_next;                                        // [kXrPods][kDsPodWords]      (DS)
+  if (kDs) s_next += (size_t)kXrPods * kDsPodWords;
+  uint64_t* s_npw = s_next;                                        // [kXrPods][kNumaPodWords]    (NUMA)
+  if (kNuma) s_next += (size_t)kXrPods * kNumaPodWords;
+  uint64_t* s_dfw = s_next;                                        // [kXrPods][kDefPodWords]     (defaults)
+  if (kDef) s_next += (size_t)kXrPods * kDefPodWords;
+  int64_t* s_aux = reinterpret_cast<int64_t*>(s_next);             // [kXrPods][kAux]             (aux requests)
+  if (has_aux) s_next += (size_t)kXrPods * kAux;
+  QuotaRow* s_q = reinterpret_cast<QuotaRow*>(s_next);             // [nq]
+  int64_t* s_qdev = reinterpret_cast<int64_t*>(s_q + nq);          // [kXrPods][kQuotaRes]
+  if (nq > 0) s_next += (size_t)nq * (sizeof(QuotaRow) / 8) + (size_t)kXrPods * kQuotaRes;
+  uint32_t* bitmap = reinterpret_cast<uint32_t*>(s_next);
+  {  // one bulk load of everything the per-pod chain reads
+    for (int w = lane; w < nb * (kC + 1); w += kWave) s_cand[w] = cand[(size_t)(w / (kC + 1)) * kCandStride + w % (kC + 1)];
+    auto stage = [&](uint64_t* dst, const void* src, int words) {
+      const uint64_t* g = reinterpret_cast<const uint64_t*>(src);
+      for (int w = lane; w < nb * words; w += kWave) dst[w] = g[(size_t)first * words + w];
+    };
+    stage(s_podw, pods, kPodWords);
+    stage(s_rpw, rpods, kRsvPodWords);
+    if (kDs) stage(s_dpw, X.dpods, kDsPodWords);
+    if (kNuma) stage(s_npw, X.npods, kNumaPodWords);
+    if (kDef) {  // DefPod is 104 B: byte-exact copy of the nb records
+      const uint32_t* g = reinterpret_cast<const uint32_t*>(X.defp + first);
+      uint32_t* d = reinterpret_cast<uint32_t*>(s_dfw);
+      constexpr int kW = (int)(sizeof(DefPod) / 4);
+      for (int w = lane; w < nb * kW; w += kWave) d[(w / kW) * (kDefPodWords * 2) + w % kW] = g[w];
+    }
+    if (has_aux) {
+      for (int w = lane; w < nb * kAux; w += kWave) s_aux[w] = X.paux[(size_t)first * kAux + w];
+    }
+    if (nq > 0) {
+      const uint64_t* qw = reinterpret_cast<const uint64_t*>(X.quotas);
+      uint64_t* sq = reinterpret_cast<uint64_t*>(s_q);
+      for (int w = lane; w < nq * (int)(sizeof(QuotaRow) / 8); w += kWave) sq[w] = qw[w];
+      for (int w = lane; w < nb * kQuotaRes; w += kWave) s_qdev[w] = X.qdev[(size_t)first * kQuotaRes + w];
+    }
+    for (int w = lane; w < bitmap_words; w += kWave) bitmap[w] = 0;
+  }
   __syncthreads();
+  const DevPod* s_pods = reinterpret_cast<const DevPod*>(s_podw);
+  const RsvPod* s_rpods = reinterpret_cast<const RsvPod*>(s_rpw);
   uint32_t midx = 0xFFFFFFFFu;  // the modified row this lane owns
   int nM = 0, consumed = 0;
   const bool dscore = val2 != nullptr;
   for (int j = 0; j < nb; ++j) {
     KG_POD_DIAG(j, (uint32_t)nM);
     const int64_t jj = first + j;
-    const DevPod p = pods[jj];
-    // ElasticQuota PreFilter against every earlier Reserve (lane 0 owns the quota rows)
+    const DevPod p = s_pods[j];
+    // the round-start values of this lane's modified row, issued before the pod's own evaluation
+    uint64_t ov = 0;
+    uint32_t ov2 = 0;
+    if (lane < nM) {
+      ov = val[(size_t)j * stride + midx];
+      ov2 = dscore ? val2[(size_t)j * stride + midx] : 0u;
+    }
+    // ElasticQuota PreFilter against every earlier Reserve (lane 0 owns the LDS quota rows)
     int admit = 1;
     QuotaReq qr;
-    if (X.nq > 0 && p.quota >= 0) {
-      qr = quota_req(p, X.qdev + (size_t)jj * kQuotaRes);
-      if (lane == 0) admit = quota_row_admit(X.quotas[p.quota], qr, (p.flags & P_NONPREEMPT) != 0) ? 1 : 0;
+    if (nq > 0 && p.quota >= 0) {
+      qr = quota_req(p, s_qdev + (size_t)j * kQuotaRes);
+      if (lane == 0) admit = quota_row_admit(s_q[p.quota], qr, (p.flags & P_NONPREEMPT) != 0) ? 1 : 0;
       admit = __builtin_amdgcn_readfirstlane(admit);
     }
     if (!admit) {
@@ -278,44 +349,42 @@ __global__ __launch_bounds__(kWave) void xr_resolve(DevTable T, RsvNode* __restr
       continue;
     }
     // pod j on the modified rows: the exact current values, next to the round-start ones
-    const RsvPod rp = rpods[jj];
-    const DsPod* dp = X.ds ? &X.dpods[jj] : nullptr;
-    const NumaPod* np = X.ns ? &X.npods[jj] : nullptr;
-    const int64_t* aux = (X.paux && (p.flags & P_AUX)) ? X.paux + (size_t)jj * kAux : nullptr;
-    const DefPod* df = X.defp ? &X.defp[jj] : nullptr;
+    const RsvPod rp = s_rpods[j];
+    const DsPod* dp = kDs ? reinterpret_cast<const DsPod*>(s_dpw + (size_t)j * kDsPodWords) : nullptr;
+    const NumaPod* np = kNuma ? reinterpret_cast<const NumaPod*>(s_npw + (size_t)j * kNumaPodWords) : nullptr;
+    const int64_t* aux = (has_aux && (p.flags & P_AUX)) ? s_aux + (size_t)j * kAux : nullptr;
+    const DefPod* df = kDef ? reinterpret_cast<const DefPod*>(s_dfw + (size_t)j * kDefPodWords) : nullptr;
     RsvOut cur{false, 0, 0, -1, 0x7fffffff, 0, 0, 0};
-    uint64_t ov = 0, cv = 0;
-    uint32_t ov2 = 0, cv2 = 0;
+    uint64_t cv = 0;
+    uint32_t cv2 = 0;
     if (lane < nM) {
       cur = rsv_eval_node(T, RN, rsv_n, midx, p, rp, P, RP, X, dp, np, nullptr, aux, df);  // X.aff[midx] = pod j's
       if (cur.feas) cv = rsv_pack(cur), cv2 = ((uint32_t)cur.tcnt << 24) | (uint32_t)cur.asum;
-      ov = val[(size_t)j * stride + midx];
-      ov2 = dscore ? val2[(size_t)j * stride + midx] : 0u;
     }
     KG_POD_SUB(j, 0);
     const uint64_t* nk = norm + (size_t)j * kXrNorm;
     bool stop = false;
-    {  // the normalisation of pod j must equal the round's
+    if (nM > 0) {  // the normalisation of pod j must equal the round's (ballots only: no wave reductions)
       const bool of = (ov >> 7) & 1, cf = cur.feas;
       const uint32_t oval[4] = {(uint32_t)((ov >> 8) & 0xff), (uint32_t)((ov >> 16) & 0xff), ov2 >> 24, ov2 & 0xFFFFFFu};
       const uint32_t cval[4] = {(uint32_t)cur.raw, (uint32_t)cur.dsraw, (uint32_t)cur.tcnt, (uint32_t)cur.asum};
-      const bool used[4] = {RP.score != 0, X.DP.score != 0, X.DF.taint_score != 0, X.DF.aff_score != 0};
+      const bool used[4] = {RP.score != 0, kDs && X.DP.score != 0, kDef && X.DF.taint_score != 0,
+                            kDef && X.DF.aff_score != 0};
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         if (!used[q]) continue;
         const uint32_t Menc = (uint32_t)(nk[1 + q] >> 32), C = (uint32_t)nk[1 + q];
         const uint32_t oe = (lane < nM && of) ? oval[q] + 1u : 0u, ce = (lane < nM && cf) ? cval[q] + 1u : 0u;
         const uint32_t lost = (uint32_t)__popcll(__ballot(oe != 0 && oe == Menc));
-        const uint32_t cm = wave_max_u32(ce);
-        if (cm > Menc || (lost >= C && cm != Menc)) stop = true;
+        // max over the modified rows > M, or every holder modified and none holds M any more
+        if (__ballot(ce > Menc) || (lost >= C && !__ballot(ce == Menc))) stop = true;
       }
       if (RP.score) {  // the preferred node (smallest order label) must stay where it is, with the same order
         const uint64_t PK = nk[0];
         const uint64_t ck = (lane < nM && cf) ? rsv_pref_key(cur, midx) : 0ull;
-        const uint64_t mk = wave_max_key(ck);
         const uint32_t pn = (uint32_t)(~PK);
         const bool holder_mod = PK != 0 && ((bitmap[pn >> 5] >> (pn & 31)) & 1u);
-        if (mk > PK || (holder_mod && mk != PK)) stop = true;
+        if (__ballot(ck > PK) || (holder_mod && !__ballot(ck == PK))) stop = true;
       }
     }
     if (stop) break;
@@ -324,7 +393,7 @@ __global__ __launch_bounds__(kWave) void xr_resolve(DevTable T, RsvNode* __restr
     const uint64_t mkey = (lane < nM && cur.feas)
                               ? make_key(rsv_total(cv, cv2, (int64_t)midx == N.pref, N.mx, N.mds, N.mt, N.ma, RP, X), midx)
                               : 0ull;
-    const uint64_t mbest = wave_max_key(mkey);
+    const uint64_t mbest = nM > 0 ? wave_max_key(mkey) : 0ull;
     const uint64_t key = lane < kC ? s_cand[(size_t)j * (kC + 1) + lane] : 0ull;
     const uint32_t kn = key_node(key);
     const bool unmod = key != 0 && !((bitmap[kn >> 5] >> (kn & 31)) & 1u);
@@ -355,10 +424,10 @@ __global__ __launch_bounds__(kWave) void xr_resolve(DevTable T, RsvNode* __restr
       if (!hit) {  // an unmodified winner: its round-start value, and its NUMA affinity for pod j
         midx = w;
         v = val[(size_t)j * stride + w];
-        if (X.aff) X.aff[w] = affk[(size_t)j * stride + w];
+        if (kNuma && X.aff) X.aff[w] = affk[(size_t)j * stride + w];
       }
       int32_t s = -1;
-      placed = rsv_reserve(T, RN, w, v, p, X, jj, s) ? 1 : 0;
+      placed = rsv_reserve<kNuma, kDs>(T, RN, w, v, p, X, jj, s) ? 1 : 0;
       slot = s;
     }
     placed = __builtin_amdgcn_readlane(placed, owner);
@@ -367,9 +436,15 @@ __global__ __launch_bounds__(kWave) void xr_resolve(DevTable T, RsvNode* __restr
     if (lane == 0) {
       out_keys[jj] = placed ? best : 0;
       out_slot[jj] = slot;
-      if (placed && X.nq > 0 && p.quota >= 0) quota_row_charge(X.quotas[p.quota], qr, (p.flags & P_NONPREEMPT) != 0);
+      if (placed && nq > 0 && p.quota >= 0) quota_row_charge(s_q[p.quota], qr, (p.flags & P_NONPREEMPT) != 0);
     }
     __syncthreads();
+  }
+  if (nq > 0) {  // the charged quota rows back to the table
+    __syncthreads();
+    const uint64_t* sq = reinterpret_cast<const uint64_t*>(s_q);
+    uint64_t* qw = reinterpret_cast<uint64_t*>(X.quotas);
+    for (int w = lane; w < nq * (int)(sizeof(QuotaRow) / 8); w += kWave) qw[w] = sq[w];
   }
   KG_POD_DIAG(consumed, 0u);
   __threadfence();

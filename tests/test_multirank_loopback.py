@@ -138,3 +138,32 @@ def test_deviceshare_ranks():
         minors, (uc, um, ur) = out[r][3]
         assert np.array_equal(minors, want_minors), r
         assert np.array_equal(uc, d["used_core"]) and np.array_equal(ur, d["used_ratio"]), r
+
+
+C5_PROFILE = F.Profile(filter=(F.NODE_RESOURCES_FIT, F.LOAD_AWARE, F.RESERVATION, F.DEVICE_SHARE),
+                       score={F.NODE_RESOURCES_FIT: 1, F.LOAD_AWARE: 1, F.RESERVATION: 5000, F.DEVICE_SHARE: 1})
+
+
+def test_reservation_profile_ranks_replicated():
+    """C5 as one profile (Reservation + DeviceShare + ElasticQuota) on 2 ranks: the exact profiles run as replicas
+    (every rank evaluates its full table and resolves the same FIFO order), so every rank's placements,
+    reservation slots, GPU minors and quota charges equal the oracle's."""
+    cfg = F.build_config(profile=C5_PROFILE)
+    cluster, dev, rsv = synth.make_c5_cluster(2000, seed=961)
+    pods = synth.make_c5_pods(1500, seed=962)
+    quotas = synth.make_c5_quotas(pods, seed=963)
+    st = oracle.states(cluster.n)
+    oracle.add_pods(cfg, st, cluster.existing_pods, cluster.existing_node)
+    r, d, q = rsv.copy(), dev.copy(), quotas.copy()
+    want, want_score, want_slot, want_minors = oracle.schedule_resv(cfg, cluster.nodes, cluster.metrics, st, r, pods,
+                                                                    cluster.now_ns, devices=d, quotas=q, n_threads=8,
+                                                                    with_minors=True)
+    out = run_ranks(cfg, 2, cluster.n, lambda e: synth.load_c5_into(e, cluster, dev, rsv, quotas), pods, chunks=2,
+                    fetch=lambda e: (e.fetch_reservations(0, len(pods)), e.fetch_devices(0, len(pods)),
+                                     e.read_quotas(len(quotas))))
+    same_on_every_rank(out, want, want_score, st)
+    for rk in range(2):
+        slot, minors, qq = out[rk][3]
+        assert np.array_equal(slot, want_slot), rk
+        assert np.array_equal(minors, want_minors), rk
+        assert np.array_equal(qq, q), rk
