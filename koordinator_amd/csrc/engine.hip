@@ -4658,6 +4658,8 @@ int kg_debug_stamps(kg_engine* e, uint64_t* out) {
                               hipMemcpyDeviceToHost));
   HIP_TRY(hipMemcpyFromSymbol(out + 4 * 32 * 2 + 64 * 6, HIP_SYMBOL(kg::g_merge_count), sizeof(kg::g_merge_count), 0,
                               hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpyFromSymbol(out + 4 * 32 * 2 + 64 * 6 + 2, HIP_SYMBOL(kg::g_lane_diag), sizeof(kg::g_lane_diag), 0,
+                              hipMemcpyDeviceToHost));
   return 0;
 #else
   (void)e;

@@ -50,7 +50,16 @@ __device__ unsigned long long g_merge_count[2];
   do {                                                                             \
     if (threadIdx.x == 0 && (j) < 64) g_pod_diag[j][2 + (k)] = __builtin_amdgcn_s_memtime(); \
   } while (0)
+// stamp k (0..7) of pod j taken by whichever lane executes it (e.g. the owner lane inside a Reserve)
+__device__ unsigned long long g_lane_diag[64][8];
+#define KG_LANE_SUB(j, k)                                                          \
+  do {                                                                             \
+    if ((j) >= 0 && (j) < 64) g_lane_diag[j][k] = __builtin_amdgcn_s_memtime();    \
+  } while (0)
 #else
+#define KG_LANE_SUB(j, k) \
+  do {                    \
+  } while (0)
 #define KG_COUNT(i) \
   do {              \
   } while (0)

@@ -365,8 +365,11 @@ __device__ __forceinline__ void rsv_quota_charge(const RsvExt& X, const DevPod& 
 // (reservation_info.go:317-326).  Called by the one thread that owns row w.  Returns false when not placed.
 template <bool NUMA = true, bool DS = true>  // compile-time: the profile's plugins (batched exact rounds)
 __device__ __forceinline__ bool rsv_reserve(const DevTable& T, RsvNode* __restrict__ RN, int64_t w, uint64_t v,
-                                            const DevPod& p, const RsvExt& X, int64_t j, int32_t& slot_out) {
+                                            const DevPod& p, const RsvExt& X, int64_t j, int32_t& slot_out,
+                                            int diag_j = -1) {
+  (void)diag_j;  // KG_STAMPS builds: the round-local pod index of the lane stamps
   slot_out = -1;
+  KG_LANE_SUB(diag_j, 0);
   // NodeNUMAResource Reserve first (the profile's Reserve order), computed on copies: nothing is committed unless
   // every Reserve succeeds
   NumaMut nmw;
@@ -384,9 +387,11 @@ __device__ __forceinline__ bool rsv_reserve(const DevTable& T, RsvNode* __restri
       return false;
     }
   }
+  KG_LANE_SUB(diag_j, 1);
   if (DS && X.ds) {
     DsNode dn = X.ds[w];
     const int32_t minors = rsv_ds_reserve(dn, X.dpods[j], X.DP);
+    KG_LANE_SUB(diag_j, 2);
     if (minors < 0) {
       X.out_minors[j] = 0;
       return false;
@@ -406,6 +411,7 @@ __device__ __forceinline__ bool rsv_reserve(const DevTable& T, RsvNode* __restri
       r[1 + kNumaMax + k] = ((rec.res >> k) & 1u) ? rec.mem[k] : 0;
     }
   }
+  KG_LANE_SUB(diag_j, 3);
   Row r = load_row(T, w);
   const int64_t prod = (p.flags & P_PROD) ? 1 : 0;
   if (X.paux && (p.flags & P_AUX))  // NodeInfo.Requested of ephemeral-storage / the scalar resources
@@ -421,6 +427,7 @@ __device__ __forceinline__ bool rsv_reserve(const DevTable& T, RsvNode* __restri
   r.la_pused_mem += prod * p.est_mem;
   r.num_pods += 1;
   store_mutable(T, w, r);
+  KG_LANE_SUB(diag_j, 4);
   const int32_t slot = (int32_t)(v & 7) - 1;
   if (slot >= 0) {  // Allocated += quotav1.Mask(requests, ResourceNames): only the reservation's keys (0 = absent)
     if (RN[w].alloc_cpu[slot] > 0) RN[w].allocd_cpu[slot] += p.req_cpu;
@@ -428,6 +435,7 @@ __device__ __forceinline__ bool rsv_reserve(const DevTable& T, RsvNode* __restri
     RN[w].assigned[slot] += 1;
   }
   slot_out = slot;
+  KG_LANE_SUB(diag_j, 5);
   return true;
 }
 

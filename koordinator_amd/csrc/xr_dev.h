@@ -20,7 +20,7 @@
 #pragma once
 
 constexpr int kXrPods = 32;      // pods per round (< kWave: one modified row per resolver lane)
-constexpr int kXrPpw = 8;        // pods per eval / select wave
+constexpr int kXrPpw = 2;        // pods per select wave (4 x 2 = 8 waves per tile group: enough waves to fill the chip)
 constexpr int kXrNorm = 5;       // per-pod statistics: preferred key, raw Reservation, DeviceShare, taint, affinity
 // Exact-round features (compile-time: the kernels carry only the plugins the profile enables, so the Fit /
 // LoadAware / Reservation-only variants keep their registers, and none spills for code it never runs)
@@ -427,7 +427,7 @@ __global__ __launch_bounds__(kWave) void xr_resolve(DevTable T, RsvNode* __restr
         if (kNuma && X.aff) X.aff[w] = affk[(size_t)j * stride + w];
       }
       int32_t s = -1;
-      placed = rsv_reserve<kNuma, kDs>(T, RN, w, v, p, X, jj, s) ? 1 : 0;
+      placed = rsv_reserve<kNuma, kDs>(T, RN, w, v, p, X, jj, s, j) ? 1 : 0;
       slot = s;
     }
     placed = __builtin_amdgcn_readlane(placed, owner);

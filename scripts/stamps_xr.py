@@ -35,9 +35,10 @@ with Engine(cfg, work.cluster.n) as e:
     e.profile(True)
     st = e.schedule_staged(0, npods)
     prof = e.profile_read()
-    buf = np.zeros(4 * 32 * 2 + 64 * 6 + 2, dtype=np.uint64)
+    buf = np.zeros(4 * 32 * 2 + 64 * 6 + 2 + 64 * 8, dtype=np.uint64)
     abi.check(e.lib, e.lib.kg_debug_stamps(e.h, abi.ptr(buf)))
     diag = buf[256:256 + 384].reshape(64, 6)
+    lane = buf[256 + 384 + 2:].reshape(64, 8)
 print(f"{wl} nodes={n} pods={npods}: rounds={int(st['device_batches'])} seconds={st['seconds']:.4f} "
       f"pods/s={npods / st['seconds']:.0f}")
 print("live:", {k: (round(ms / c * 1e3, 2), c) for k, (ms, c) in prof.items()})
@@ -51,5 +52,6 @@ for j in range(64):
     if prev is not None:
         pc = int(diag[j - 1, 0])
         sub = " ".join(f"{int(diag[j - 1, 2 + k]) - pc if diag[j - 1, 2 + k] else -1:6d}" for k in range(4))
-        print(f"  pod {j - 1:2d}: {c - prev:7d} cyc nM={int(diag[j - 1, 1]):2d}  sub {sub}")
+        rs = " ".join(f"{int(lane[j - 1, k]) - pc if lane[j - 1, k] else -1:6d}" for k in range(6))
+        print(f"  pod {j - 1:2d}: {c - prev:7d} cyc nM={int(diag[j - 1, 1]):2d}  sub {sub}  reserve {rs}")
     prev = c
