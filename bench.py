@@ -398,7 +398,9 @@ def main():
             mn, dtn, _ = cpu_sample(work, pods[:total], args.cpu_seconds / 2, nproc)
             cpu["nproc_threads"] = {"value": mn / dtn, "threads": nproc, "sample_pods": mn}
 
-    tfile = args.traffic_file or os.path.join(ROOT, "profiles", "r02", f"traffic_{wl}.json")
+    tfile = args.traffic_file or next((f for f in (os.path.join(ROOT, "profiles", r, f"traffic_{wl}.json")
+                                                   for r in ("r03", "r02")) if os.path.exists(f)),
+                                      os.path.join(ROOT, "profiles", "r02", f"traffic_{wl}.json"))
     pmc_name = "eval_round_numa" if wl == "c4" else dom  # live timing folds every wide pass under "eval_round"
     traffic, traffic_src = (pmc_traffic(tfile, pmc_name, cluster.n, args.batch, args.pods_per_wave, args.depth)
                             if d.world == 1 else (None, None))

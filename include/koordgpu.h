@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define KG_ABI_VERSION 8
+#define KG_ABI_VERSION 9
 
 /* ---- resource slots (fixed order) ------------------------------------------------------- */
 enum {
@@ -70,6 +70,8 @@ enum { KG_PRIO_NONE = 0, KG_PRIO_PROD = 1, KG_PRIO_MID = 2, KG_PRIO_BATCH = 3, K
 /* NodeNUMAResource vocabulary (apis/extension/numa_aware.go:89-144, apis/extension/qos.go:23-28) */
 enum { KG_QOS_NONE = 0, KG_QOS_LSE = 1, KG_QOS_LSR = 2, KG_QOS_LS = 3, KG_QOS_BE = 4, KG_QOS_SYSTEM = 5 };
 /* CPUBindPolicy: "" / Default / FullPCPUs / SpreadByPCPUs / ConstrainedBurst */
+/* CPUExclusivePolicy (apis/scheduling/config types; ResourceSpec.PreferredCPUExclusivePolicy, plugin.go:261) */
+enum { KG_EXCL_NONE = 0, KG_EXCL_PCPU_LEVEL = 1, KG_EXCL_NUMA_NODE_LEVEL = 2 };
 enum { KG_BIND_NONE = 0, KG_BIND_DEFAULT = 1, KG_BIND_FULL_PCPUS = 2, KG_BIND_SPREAD_BY_PCPUS = 3,
        KG_BIND_CONSTRAINED_BURST = 4 };
 /* NodeCPUBindPolicy label (or kubelet static policy with full-pcpus-only) */
@@ -291,6 +293,10 @@ typedef struct kg_pod {
   int64_t n_preferred_terms;                   /* preferred PreferredSchedulingTerms                            */
   uint64_t preferred_terms[KG_MAX_AFF_TERMS];
   int64_t preferred_weights[KG_MAX_AFF_TERMS];
+  /* (ABI 9) ResourceSpec.PreferredCPUExclusivePolicy (KG_EXCL_*): cpuAccumulator's filterExclusive passes keep the
+   * pod off the cores (PCPULevel) / NUMA nodes (NUMANodeLevel) that hold cpus of pods with the same policy
+   * (cpu_accumulator.go:247-330), and Reserve records the pod's cpus with it (node_allocation.go:68-90) */
+  int64_t preferred_cpu_exclusive_policy;
 } kg_pod;
 
 /* pod reservation flags */
@@ -371,6 +377,10 @@ typedef struct kg_node_numa {
   /* node.koordinator.sh/resource-amplification-ratio cpu (extension.Ratio, ≤ 1 = none).  numa_cpu above is the
    * zone cpu AFTER amplifyNUMANodeResources (util.go:63-84), node allocatable cpu the amplified one. */
   double cpu_amplification_ratio;
+  /* (ABI 9) NodeAllocation.allocatedCPUs whose CPUInfo.ExclusivePolicy is PCPULevel / NUMANodeLevel (the policy of
+   * the pod holding them; subsets of allocated_cpus) */
+  uint64_t exclusive_pcpu_cpus[KG_MAX_CPUS / 64];
+  uint64_t exclusive_numa_cpus[KG_MAX_CPUS / 64];
 } kg_node_numa;
 
 /* Node-side view for TaintToleration / NodeAffinity (ABI 8).  The caller keeps two dense tables: up to 64 distinct

@@ -35,7 +35,7 @@ POD_REQUEST_KEYS, POD_CPU_KEY, POD_MEM_KEY = 8, 16, 32
 MAX_OWNER_GROUPS = 64
 QUOTA_RES = 8
 MAX_QUOTAS = 64
-ABI_VERSION = 8
+ABI_VERSION = 9
 MAX_RSV_SLOTS = 4
 RSV_POLICY = {"Default": 0, "Aligned": 1, "Restricted": 2}
 POD_RSV_AFFINITY = 1
@@ -45,6 +45,7 @@ PROF_NAMES = {0: "eval_round", 1: "merge_round", 2: "resolve_round", 3: "ds_max_
 MAX_NUMA, MAX_CPUS = 4, 256
 QOS = {"": 0, "LSE": 1, "LSR": 2, "LS": 3, "BE": 4, "SYSTEM": 5}
 BIND = {"": 0, "Default": 1, "FullPCPUs": 2, "SpreadByPCPUs": 3, "ConstrainedBurst": 4}
+EXCL = {"": 0, "None": 0, "PCPULevel": 1, "NUMANodeLevel": 2}  # CPUExclusivePolicy
 NODE_BIND = {"": 0, "None": 0, "FullPCPUsOnly": 1, "SpreadByPCPUs": 2}
 NUMA_POLICY = {"": 0, "BestEffort": 1, "Restricted": 2, "SingleNUMANode": 3}
 STRATEGY = {"LeastAllocated": 0, "MostAllocated": 1}
@@ -135,6 +136,7 @@ POD_DTYPE = np.dtype([
     ("tolerated_taints", np.uint64), ("node_selector", np.uint64),
     _i64("n_required_terms"), ("required_terms", np.uint64, (MAX_AFF_TERMS,)),
     _i64("n_preferred_terms"), ("preferred_terms", np.uint64, (MAX_AFF_TERMS,)), _i64("preferred_weights", MAX_AFF_TERMS),
+    _i64("preferred_cpu_exclusive_policy"),
 ])
 NODE_PRED_DTYPE = np.dtype([("predicates", np.uint64), ("taints_hard", np.uint64), ("taints_soft", np.uint64)])
 
@@ -157,6 +159,7 @@ NODE_NUMA_DTYPE = np.dtype([
     _i64("numa_cpu", MAX_NUMA), _i64("numa_mem", MAX_NUMA),
     ("reserved_cpus", np.uint64, (MAX_CPUS // 64,)), ("allocated_cpus", np.uint64, (MAX_CPUS // 64,)),
     _i64("numa_alloc_cpu", MAX_NUMA), _i64("numa_alloc_mem", MAX_NUMA), ("cpu_amplification_ratio", np.float64),
+    ("exclusive_pcpu_cpus", np.uint64, (MAX_CPUS // 64,)), ("exclusive_numa_cpus", np.uint64, (MAX_CPUS // 64,)),
 ])
 
 STATS_DTYPE = np.dtype([

@@ -2439,6 +2439,8 @@ int decode_numa_pod(const kg_config& c, const kg_pod& p, NumaPod& d) {
   if (p.required_cpu_bind_policy < KG_BIND_NONE || p.required_cpu_bind_policy > KG_BIND_CONSTRAINED_BURST ||
       p.preferred_cpu_bind_policy < KG_BIND_NONE || p.preferred_cpu_bind_policy > KG_BIND_CONSTRAINED_BURST)
     return fail(KG_E_INVALID, "pod cpu bind policy");
+  if (p.preferred_cpu_exclusive_policy < KG_EXCL_NONE || p.preferred_cpu_exclusive_policy > KG_EXCL_NUMA_NODE_LEVEL)
+    return fail(KG_E_INVALID, "pod cpu exclusive policy");
   d.req_cpu = p.requests[KG_RES_CPU];
   d.req_mem = p.requests[KG_RES_MEMORY];
   bool zero = true;
@@ -2463,6 +2465,7 @@ int decode_numa_pod(const kg_config& c, const kg_pod& p, NumaPod& d) {
       d.required = required;
       d.preferred = bind;
       d.needed = (int32_t)std::min<int64_t>(d.req_cpu / 1000, 1 << 20);
+      d.excl = (int32_t)p.preferred_cpu_exclusive_policy;  // plugin.go:261
     }
   }
   return 0;
@@ -2510,6 +2513,8 @@ int decode_node_numa(const kg_node_numa& n, NumaStatic& s, NumaMut& m) {
   for (int w = 0; w < KG_MAX_CPUS / 64; ++w) {
     s.reserved[w] = n.reserved_cpus[w];
     m.allocated[w] = n.allocated_cpus[w];
+    m.excl_pcpu[w] = n.exclusive_pcpu_cpus[w] & n.allocated_cpus[w];
+    m.excl_numa[w] = n.exclusive_numa_cpus[w] & n.allocated_cpus[w];
   }
   return 0;
 }

@@ -42,8 +42,11 @@ struct NumaMut {
   int64_t alloc_cpu[kNumaMax], alloc_mem[kNumaMax];
   uint32_t present;  // bit i: allocatedResources[i] exists (an allocation ever landed on NUMA node i)
   uint32_t pad;
+  // allocated cpus whose CPUInfo.ExclusivePolicy is PCPULevel / NUMANodeLevel (read by Reserve only; past the
+  // fields Filter / Score read, so the wide pass touches the same lines as without them)
+  uint64_t excl_pcpu[kCpuWords], excl_numa[kCpuWords];
 };
-static_assert(sizeof(NumaMut) == 104, "NumaMut layout");
+static_assert(sizeof(NumaMut) == 168, "NumaMut layout");
 
 // extension.Amplify (apis/extension/node_resource_amplification.go:170-175): ceil in float64, as Go
 __device__ __forceinline__ int64_t amplify(int64_t origin, double ratio) {
@@ -55,7 +58,8 @@ struct NumaPod {
   int64_t req_cpu, req_mem;
   int32_t skip, prefilter_error, cpu_bind, required;  // required/preferred: KG_BIND_*
   int32_t preferred, needed;
-  int32_t pad[2];
+  int32_t excl;  // preferredCPUExclusivePolicy (KG_EXCL_*)
+  int32_t pad;
 };
 static_assert(sizeof(NumaPod) == 48, "NumaPod layout");
 
@@ -188,15 +192,43 @@ __device__ __forceinline__ bool better_free(int strategy, int a, int b) { return
 // ---------------------------------------------------------------------------------------------------------
 // takeCPUs (cpu_accumulator.go:87-232), single thread, on masks.  Returns false on "not enough cpus".
 // ---------------------------------------------------------------------------------------------------------
+// every cpu of the cores with a cpu in s (cpc ≤ 2)
+__device__ __forceinline__ CpuSet expand_cores(const Topo& t, const CpuSet& s) {
+  if (t.cpc == 1) return s;
+  CpuSet r;
+#pragma unroll
+  for (int w = 0; w < kCpuWords; ++w) {
+    const uint64_t e = (s.w[w] | (s.w[w] >> 1)) & kEven;
+    r.w[w] = e | (e << 1);
+  }
+  return r;
+}
+
 struct Acc {
   Topo t;
   CpuSet avail;  // allocatableCPUs
   CpuSet result;
   int needed, strategy;
+  int excl;      // the pod's CPUExclusivePolicy (KG_EXCL_*)
+  CpuSet seed;   // the node's allocated cpus holding that policy (newCPUAccumulator, cpu_accumulator.go:256-264)
   __device__ void take(const CpuSet& s) {
     result = cs_or(result, s);
     avail = cs_andnot(avail, s);
     needed -= cs_count(s);
+  }
+  // the cpus a filterExclusive pass skips (isCPUExclusivePCPULevel / NUMANodeLevel, :318-330): every cpu of a core
+  // (PCPULevel) or NUMA node (NUMANodeLevel) holding a seed cpu or a cpu this call took (take() grows the sets,
+  // :290-304); pcpu / numa: the levels the calling list filters (freeCoresInNode NUMA only, freeCPUsInSocket PCPU
+  // only, freeCPUsInNode / freeCPUs both)
+  __device__ CpuSet excluded(bool pcpu, bool numa) const {
+    if (!((excl == KG_EXCL_PCPU_LEVEL && pcpu) || (excl == KG_EXCL_NUMA_NODE_LEVEL && numa))) return cs_zero();
+    const CpuSet held = cs_or(seed, result);
+    if (excl == KG_EXCL_PCPU_LEVEL) return expand_cores(t, held);
+    CpuSet r = cs_zero();
+#pragma unroll
+    for (int n = 0; n < 8; ++n)
+      if (n < t.nodes && cs_count(cs_and(held, t.node_cpus(n))) > 0) r = cs_or(r, t.node_cpus(n));
+    return r;
   }
 };
 
@@ -236,7 +268,9 @@ __device__ __forceinline__ int key_free(int strategy, uint64_t k) {
 
 // groups (NUMA nodes or sockets) with cpus in `sel`, ordered as freeCoresInNode/Socket(full=true) order them:
 // (group free count, [socket free count for nodes], id)
-__device__ __forceinline__ void order_groups(const Acc& a, bool by_node, const CpuSet& sel, uint64_t* k) {
+// (av: the allocatable cpus the list counts socket free scores over — filterExclusive passes drop the exclusive ones)
+__device__ __forceinline__ void order_groups(const Acc& a, bool by_node, const CpuSet& sel, const CpuSet& av,
+                                             uint64_t* k) {
   const int ng = by_node ? a.t.nodes : a.t.sockets;
 #pragma unroll
   for (int g = 0; g < 8; ++g) {
@@ -245,7 +279,7 @@ __device__ __forceinline__ void order_groups(const Acc& a, bool by_node, const C
     const int c = cs_count(cs_and(sel, by_node ? a.t.node_cpus(g) : a.t.socket_cpus(g)));
     if (c == 0) continue;
     uint64_t key = free_field(a.strategy, c) << 32 | (uint64_t)g;
-    if (by_node) key |= free_field(a.strategy, cs_count(cs_and(a.avail, a.t.socket_cpus(g / a.t.nps)))) << 16;
+    if (by_node) key |= free_field(a.strategy, cs_count(cs_and(av, a.t.socket_cpus(g / a.t.nps)))) << 16;
     k[g] = key;
   }
   sort8(k);
@@ -270,13 +304,15 @@ __device__ __forceinline__ CpuSet spread_first_k(const Topo& t, const CpuSet& s,
 }
 
 __device__ __noinline__ bool take_cpus(const Topo& t, const CpuSet& available, int needed, int bind, int strategy,
-                                 CpuSet& out) {
+                                 CpuSet& out, int excl, const CpuSet& seed) {
   Acc a;
   a.t = t;
   a.avail = cs_and(available, t.all());
   a.result = cs_zero();
   a.needed = needed;
   a.strategy = strategy;
+  a.excl = excl;
+  a.seed = seed;
   out = cs_zero();
   if (a.needed < 1) return true;
   if (a.needed > cs_count(a.avail)) return false;
@@ -284,20 +320,24 @@ __device__ __noinline__ bool take_cpus(const Topo& t, const CpuSet& available, i
   uint64_t k[8];
   if (full || t.cpc == 1) {
     if (a.needed <= t.per_node()) {
-      const CpuSet fc = full_core_cpus(t, a.avail);
-      order_groups(a, true, fc, k);
-      for (int g = 0; g < 8; ++g) {
-        const uint64_t kg = kat(k, g);
-        if (kg != kNoGroup && key_free(a.strategy, kg) >= a.needed) {
-          a.take(lowest_k(cs_and(fc, t.node_cpus(key_id(kg))), a.needed));
-          out = a.result;
-          return true;
+      // freeCoresInNode(true, filterExclusive) for filterExclusive true, false (the same list unless NUMANodeLevel)
+      for (int fe = 0; fe < (a.excl == KG_EXCL_NUMA_NODE_LEVEL ? 2 : 1); ++fe) {
+        const CpuSet av = fe == 0 ? cs_andnot(a.avail, a.excluded(false, true)) : a.avail;
+        const CpuSet fc = full_core_cpus(t, av);
+        order_groups(a, true, fc, av, k);
+        for (int g = 0; g < 8; ++g) {
+          const uint64_t kg = kat(k, g);
+          if (kg != kNoGroup && key_free(a.strategy, kg) >= a.needed) {
+            a.take(lowest_k(cs_and(fc, t.node_cpus(key_id(kg))), a.needed));
+            out = a.result;
+            return true;
+          }
         }
       }
     }
     if (a.needed <= t.per_socket()) {
       const CpuSet fc = full_core_cpus(t, a.avail);
-      order_groups(a, false, fc, k);
+      order_groups(a, false, fc, a.avail, k);
       for (int g = 0; g < 8; ++g) {
         const uint64_t kg = kat(k, g);
         if (kg != kNoGroup && key_free(a.strategy, kg) >= a.needed) {
@@ -361,12 +401,13 @@ __device__ __noinline__ bool take_cpus(const Topo& t, const CpuSet& available, i
     if (a.needed <= t.per_node()) {
       for (int fe = 0; fe < 2; ++fe) {
         // freeCPUsInNode: nodes by (node free, socket free, id) on the unreduced counts; with
-        // filterExclusive each list keeps one cpu per core
-        order_groups(a, true, a.avail, k);
+        // filterExclusive the exclusive cpus are skipped and each list keeps one cpu per core
+        const CpuSet av = fe == 0 ? cs_andnot(a.avail, a.excluded(true, true)) : a.avail;
+        order_groups(a, true, av, av, k);
         for (int g = 0; g < 8; ++g) {
           const uint64_t kg = kat(k, g);
           if (kg == kNoGroup) continue;
-          const CpuSet in = cs_and(a.avail, t.node_cpus(key_id(kg)));
+          const CpuSet in = cs_and(av, t.node_cpus(key_id(kg)));
           const CpuSet lst = fe == 0 ? first_cpu_per_core(t, in) : in;
           if (cs_count(lst) >= a.needed) {
             a.take(fe == 0 ? lowest_k(lst, a.needed) : spread_first_k(t, lst, a.needed));
@@ -378,12 +419,13 @@ __device__ __noinline__ bool take_cpus(const Topo& t, const CpuSet& available, i
     }
     if (a.needed <= t.per_socket()) {
       for (int fe = 0; fe < 2; ++fe) {
-        // freeCPUsInSocket: sockets by (length of the (reduced) list, id)
+        // freeCPUsInSocket: sockets by (length of the (reduced) list, id); filterExclusive skips PCPU-level cpus
+        const CpuSet av = fe == 0 ? cs_andnot(a.avail, a.excluded(true, false)) : a.avail;
 #pragma unroll
         for (int s = 0; s < 8; ++s) {
           k[s] = kNoGroup;
           if (s >= t.sockets) continue;
-          const CpuSet in = cs_and(a.avail, t.socket_cpus(s));
+          const CpuSet in = cs_and(av, t.socket_cpus(s));
           if (cs_count(in) == 0) continue;
           const CpuSet lst = fe == 0 ? first_cpu_per_core(t, in) : in;
           k[s] = free_field(a.strategy, cs_count(lst)) << 32 | (uint64_t)s;
@@ -393,7 +435,7 @@ __device__ __noinline__ bool take_cpus(const Topo& t, const CpuSet& available, i
           const uint64_t kg = kat(k, g);
           if (kg == kNoGroup) continue;
           if (key_free(a.strategy, kg) >= a.needed) {
-            const CpuSet in = cs_and(a.avail, t.socket_cpus(key_id(kg)));
+            const CpuSet in = cs_and(av, t.socket_cpus(key_id(kg)));
             const CpuSet lst = fe == 0 ? first_cpu_per_core(t, in) : in;
             a.take(fe == 0 ? lowest_k(lst, a.needed) : spread_first_k(t, lst, a.needed));
             out = a.result;
@@ -406,23 +448,26 @@ __device__ __noinline__ bool take_cpus(const Topo& t, const CpuSet& available, i
   // freeCPUs: cores by (socket colo desc, socket free, node free, core free asc, socket, core), then spread;
   // take one by one.  Classes of (socket, node) share the first three keys; inside a run of equal classes
   // single-free cores come before full ones, each by core id (= (socket, core) order in this numbering).
-  {
+  // filterExclusive true, then false: without an exclusive policy the first list is every free cpu, so the second
+  // has nothing left
+  for (int fe = 0; fe < (a.excl != KG_EXCL_NONE ? 2 : 1); ++fe) {
+    const CpuSet av = fe == 0 ? cs_andnot(a.avail, a.excluded(true, true)) : a.avail;
 #pragma unroll
     for (int n = 0; n < 8; ++n) {
       k[n] = kNoGroup;
       if (n >= t.nodes) continue;
-      const int nf = cs_count(cs_and(a.avail, t.node_cpus(n)));
+      const int nf = cs_count(cs_and(av, t.node_cpus(n)));
       if (nf == 0) continue;
       const int s = n / t.nps;
       const int colo = cs_count(cs_and(a.result, t.socket_cpus(s)));
-      const int sf = cs_count(cs_and(a.avail, t.socket_cpus(s)));
+      const int sf = cs_count(cs_and(av, t.socket_cpus(s)));
       k[n] = (uint64_t)(0xFFFF - colo) << 48 | free_field(a.strategy, sf) << 32 | free_field(a.strategy, nf) << 16 |
              (uint64_t)n;
     }
     sort8(k);
     // the ordered cpu list as runs of equal class (key >> 16), each read as [single-free cores, full cores] in
     // ascending cpu order; the node masks are taken before any cpu is
-    const CpuSet avail0 = a.avail;
+    const CpuSet avail0 = av;
     // spreadCPUs over the concatenated list: first pass takes the first cpu of each core, second the rest
     for (int pass = 0; pass < 2; ++pass) {
       CpuSet run = cs_zero();
@@ -966,6 +1011,10 @@ __device__ __noinline__ bool numa_reserve(const NumaStatic& s, NumaMut& m, const
     const int bind = numa_pref_bind(v, p.preferred);
     CpuSet avail = numa_available_cpus(t, s, m);
     if (p.required != 0) avail = filter_required(t, avail, bind);
+    CpuSet seed = cs_zero();  // the allocated cpus holding the pod's exclusive policy
+#pragma unroll
+    for (int w = 0; w < kCpuWords; ++w)
+      seed.w[w] = p.excl == KG_EXCL_PCPU_LEVEL ? m.excl_pcpu[w] : p.excl == KG_EXCL_NUMA_NODE_LEVEL ? m.excl_numa[w] : 0;
     if (a.res) {
       for (int i = 0; i < kNumaMax; ++i) {
         if (!((a.res >> i) & 1u)) continue;
@@ -974,10 +1023,10 @@ __device__ __noinline__ bool numa_reserve(const NumaStatic& s, NumaMut& m, const
         const int want = (int)(a.cpu[i] / 1000);
         if (want < num) num = want;
         CpuSet one;
-        if (!take_cpus(t, in, num, bind, v.strategy, one)) return false;
+        if (!take_cpus(t, in, num, bind, v.strategy, one, p.excl, seed)) return false;
         cpus = cs_or(cpus, one);
       }
-    } else if (!take_cpus(t, avail, p.needed, bind, v.strategy, cpus)) {
+    } else if (!take_cpus(t, avail, p.needed, bind, v.strategy, cpus, p.excl, seed)) {
       return false;
     }
     if (p.required != 0) {  // satisfiedRequiredCPUBindPolicy (:568-589), exact
@@ -986,7 +1035,12 @@ __device__ __noinline__ bool numa_reserve(const NumaStatic& s, NumaMut& m, const
     }
   }
 #pragma unroll
-  for (int w = 0; w < kCpuWords; ++w) m.allocated[w] |= cpus.w[w];
+  for (int w = 0; w < kCpuWords; ++w) {
+    m.allocated[w] |= cpus.w[w];
+    // addPodAllocation: the pod's cpus carry its exclusive policy (node_allocation.go:82-90)
+    m.excl_pcpu[w] = (m.excl_pcpu[w] & ~cpus.w[w]) | (p.excl == KG_EXCL_PCPU_LEVEL ? cpus.w[w] : 0ull);
+    m.excl_numa[w] = (m.excl_numa[w] & ~cpus.w[w]) | (p.excl == KG_EXCL_NUMA_NODE_LEVEL ? cpus.w[w] : 0ull);
+  }
 #pragma unroll
   for (int i = 0; i < kNumaMax; ++i)
     if ((a.res >> i) & 1u) {
@@ -1005,7 +1059,11 @@ constexpr int kNumaRecWords = 1 + 2 * kNumaMax;
 // allocated set (maxRefCount 1), its NUMANodeResources are subtracted with a non-negative result
 __device__ __forceinline__ void numa_release(NumaMut& m, const uint64_t* cpus, const int64_t* rec) {
 #pragma unroll
-  for (int w = 0; w < kCpuWords; ++w) m.allocated[w] &= ~cpus[w];
+  for (int w = 0; w < kCpuWords; ++w) {
+    m.allocated[w] &= ~cpus[w];
+    m.excl_pcpu[w] &= ~cpus[w];  // RefCount 0: the CPUInfo and its policy are deleted
+    m.excl_numa[w] &= ~cpus[w];
+  }
 #pragma unroll
   for (int i = 0; i < kNumaMax; ++i)
     if ((rec[0] >> i) & 1) {

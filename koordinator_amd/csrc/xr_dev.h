@@ -247,6 +247,119 @@ __host__ __device__ inline size_t xr_resolve_lds_bytes(int XF, int nq, bool aux,
   return w * 8 + (size_t)bitmap_words * 4;
 }
 
+// Wave-cooperative Reserve of pod j on its winner row w (every lane calls it with the same w, v, j; `owner` holds row
+// w): NodeNUMAResource Reserve on copies (owner lane), then DeviceShare's minor choice with one lane per minor —
+// score and fit of minor m on lane m, the (score desc, minor asc) rank from the other lanes, the first `count` fitting
+// minors taken (defaultAllocateDevices, device_allocator.go:384-454; sortDeviceResourcesByMinor,
+// device_resources.go:187-208) and their deviceUsed updated by their lanes (updateCacheUsed, device_cache.go:124-135) —
+// then the commits on the owner lane (NUMA NodeAllocation, NodeInfo + LoadAware assign cache, reservationCache
+// assumePod).  The same Reserve as rsv_reserve, with the ~1.5 k-instruction per-minor scoring off the single lane.
+template <bool NUMA, bool DS>
+__device__ __forceinline__ bool xr_reserve(const DevTable& T, RsvNode* __restrict__ RN, int64_t w, uint64_t v,
+                                           const DevPod& p, const RsvExt& X, int64_t j, int owner, int32_t& slot_out,
+                                           int diag_j) {
+  (void)diag_j;
+  const int lane = threadIdx.x;
+  slot_out = -1;
+  KG_LANE_SUB(diag_j, 0);
+  NumaMut nmw;
+  CpuSet cpus = cs_zero();
+  NumaAlloc rec;
+  rec.res = 0;
+  if (NUMA && X.ns) {
+    int ok = 1;
+    if (lane == owner) {
+      const NumaStatic nsw = X.ns[w];
+      nmw = X.nm[w];
+      const NumaView nv = make_view(&nsw, &nmw, X.NP);
+      const uint32_t a = X.aff[w];
+      const NumaHint aff{a & 0xFFu, (int)((a >> 8) & 1u), 0, 0};
+      ok = numa_reserve(nsw, nmw, nv, X.npods[j], aff, cpus, rec) ? 1 : 0;
+    }
+    ok = __builtin_amdgcn_readlane(ok, owner);
+    if (!ok) {
+      if (lane == 0 && X.out_minors) X.out_minors[j] = 0;
+      return false;
+    }
+  }
+  KG_LANE_SUB(diag_j, 1);
+  if (DS && X.ds) {
+    const DsPod dp = X.dpods[j];
+    const DsNode& d = X.ds[w];
+    int32_t minors = 0;
+    bool failed = false;
+    if (!dp.skip && d.has_device) {
+      const DsInst in = dp.error ? DsInst{0, 0, 0, 0, 0} : ds_instance(d, dp);
+      bool f = false, nz = false;
+      int64_t sc = 0;
+      if (in.ok && lane < kMinors) sc = ds_minor(d, lane, in, X.DP, f, nz);
+      const uint64_t anym = __ballot(nz), fitm = __ballot(f);
+      failed = !in.ok || anym == 0 || __popcll(fitm) < in.count;
+      if (!failed) {
+        int rank = 0;
+#pragma unroll
+        for (int q = 0; q < kMinors; ++q) {
+          const int64_t sq = (int64_t)readlane_u64((uint64_t)sc, q);
+          rank += (((fitm >> q) & 1ull) != 0) && (sq > sc || (sq == sc && q < lane)) ? 1 : 0;
+        }
+        const uint64_t taken = __ballot(f && rank < in.count);
+        if ((taken >> lane) & 1ull) {
+          DsNode* dw = const_cast<DsNode*>(X.ds) + w;
+          dw->ucore[lane] += (int32_t)in.core;
+          dw->uratio[lane] += (int32_t)in.ratio;
+          dw->umem[lane] += in.mem;
+        }
+        minors = (int32_t)taken;
+      }
+    }
+    if (lane == 0) X.out_minors[j] = failed ? 0 : minors;
+    if (failed) return false;
+    __threadfence_block();  // the owner lane re-reads this row's deviceUsed for later pods
+  }
+  KG_LANE_SUB(diag_j, 2);
+  int32_t slot = -1;
+  if (lane == owner) {
+    if (NUMA && X.ns) {
+      X.nm[w] = nmw;
+#pragma unroll
+      for (int q = 0; q < kCpuWords; ++q) X.out_cpus[(size_t)j * kCpuWords + q] = cpus.w[q];
+      int64_t* r = X.out_nrec + (size_t)j * kNumaRecWords;
+      r[0] = rec.res;
+#pragma unroll
+      for (int k = 0; k < kNumaMax; ++k) {
+        r[1 + k] = ((rec.res >> k) & 1u) ? rec.cpu[k] : 0;
+        r[1 + kNumaMax + k] = ((rec.res >> k) & 1u) ? rec.mem[k] : 0;
+      }
+    }
+    KG_LANE_SUB(diag_j, 3);
+    Row r = load_row(T, w);
+    const int64_t prod = (p.flags & P_PROD) ? 1 : 0;
+    if (X.paux && (p.flags & P_AUX))  // NodeInfo.Requested of ephemeral-storage / the scalar resources
+#pragma unroll
+      for (int q = 0; q < kAux; ++q) T.aux[(size_t)(kAux + q) * T.cap + w] += X.paux[(size_t)j * kAux + q];
+    r.req_cpu += p.req_cpu;
+    r.req_mem += p.req_mem;
+    r.nz_cpu += p.nz_cpu;
+    r.nz_mem += p.nz_mem;
+    r.la_used_cpu += p.est_cpu;
+    r.la_used_mem += p.est_mem;
+    r.la_pused_cpu += prod * p.est_cpu;
+    r.la_pused_mem += prod * p.est_mem;
+    r.num_pods += 1;
+    store_mutable(T, w, r);
+    KG_LANE_SUB(diag_j, 4);
+    slot = (int32_t)(v & 7) - 1;
+    if (slot >= 0) {  // Allocated += quotav1.Mask(requests, ResourceNames): only the reservation's keys (0 = absent)
+      if (RN[w].alloc_cpu[slot] > 0) RN[w].allocd_cpu[slot] += p.req_cpu;
+      if (RN[w].alloc_mem[slot] > 0) RN[w].allocd_mem[slot] += p.req_mem;
+      RN[w].assigned[slot] += 1;
+    }
+    KG_LANE_SUB(diag_j, 5);
+  }
+  slot_out = __builtin_amdgcn_readlane(slot, owner);
+  return true;
+}
+
 // One wave: the round's FIFO replay (see the header).  Dynamic LDS: the pods' candidate records [nb][kC + 1], the
 // round's pods and their per-plugin records (DevPod, RsvPod, DsPod, NumaPod, DefPod, aux requests), the ElasticQuota
 // rows (admitted / charged in LDS, written back at the end) and the modified-node bitmap — one bulk load, so the
@@ -418,21 +531,16 @@ __global__ __launch_bounds__(kWave) void xr_resolve(DevTable T, RsvNode* __restr
       ++nM;
     }
     KG_POD_SUB(j, 2);
-    int placed = 0, slot = -1;
-    if (lane == owner) {
-      uint64_t v = cv;
-      if (!hit) {  // an unmodified winner: its round-start value, and its NUMA affinity for pod j
-        midx = w;
-        v = val[(size_t)j * stride + w];
-        if (kNuma && X.aff) X.aff[w] = affk[(size_t)j * stride + w];
-      }
-      int32_t s = -1;
-      placed = rsv_reserve<kNuma, kDs>(T, RN, w, v, p, X, jj, s, j) ? 1 : 0;
-      slot = s;
+    uint64_t v = cv;
+    if (lane == owner && !hit) {  // an unmodified winner: its round-start value, and its NUMA affinity for pod j
+      midx = w;
+      v = val[(size_t)j * stride + w];
+      if (kNuma && X.aff) X.aff[w] = affk[(size_t)j * stride + w];
     }
-    placed = __builtin_amdgcn_readlane(placed, owner);
+    v = readlane_u64(v, owner);
+    int32_t slot = -1;
+    const bool placed = xr_reserve<kNuma, kDs>(T, RN, w, v, p, X, jj, owner, slot, j);
     KG_POD_SUB(j, 3);
-    slot = __builtin_amdgcn_readlane(slot, owner);
     if (lane == 0) {
       out_keys[jj] = placed ? best : 0;
       out_slot[jj] = slot;

@@ -230,11 +230,13 @@ def make_node_metric(present: bool = True, update_time_ns: int | None = 0, node_
 def make_node_numa(sockets: int = 0, nodes_per_socket: int = 1, cores_per_node: int = 0, cpus_per_core: int = 2,
                    numa_policy: str = "", node_cpu_bind_policy: str = "", numa_allocate_strategy: str | None = None,
                    numa_resources: list | None = None, reserved_cpus=(), allocated_cpus=(),
-                   numa_allocated: dict | None = None, cpu_amplification_ratio: float = 0.0) -> np.ndarray:
+                   numa_allocated: dict | None = None, cpu_amplification_ratio: float = 0.0,
+                   exclusive_pcpu_cpus=(), exclusive_numa_cpus=()) -> np.ndarray:
     """NodeNUMAResource view of a node: the NodeResourceTopology's CPU topology (buildCPUTopology numbering),
     policies and zones, and the NodeAllocation of already-bound pods. numa_resources = [{"cpu": .., "memory": ..}]
     per NUMA zone; numa_allocated = {zone: {"cpu": .., "memory": ..}}; cpu_amplification_ratio = the node's
-    node.koordinator.sh/resource-amplification-ratio cpu (≤ 1 none; zone cpu is given amplified)."""
+    node.koordinator.sh/resource-amplification-ratio cpu (≤ 1 none; zone cpu is given amplified);
+    exclusive_{pcpu,numa}_cpus = the allocated cpus whose holder's CPUExclusivePolicy is PCPULevel / NUMANodeLevel."""
     n = np.zeros(1, dtype=abi.NODE_NUMA_DTYPE)
     r = n[0]
     r["has_topology"] = int(sockets > 0)
@@ -248,7 +250,8 @@ def make_node_numa(sockets: int = 0, nodes_per_socket: int = 1, cores_per_node: 
     for i, z in enumerate(zones):
         r["numa_cpu"][i] = resource_value("cpu", z.get("cpu", 0))
         r["numa_mem"][i] = resource_value("memory", z.get("memory", 0))
-    for name, cpus in (("reserved_cpus", reserved_cpus), ("allocated_cpus", allocated_cpus)):
+    for name, cpus in (("reserved_cpus", reserved_cpus), ("allocated_cpus", allocated_cpus),
+                       ("exclusive_pcpu_cpus", exclusive_pcpu_cpus), ("exclusive_numa_cpus", exclusive_numa_cpus)):
         w = np.zeros(abi.MAX_CPUS // 64, dtype=np.uint64)
         for c in cpus:
             w[c // 64] |= np.uint64(1) << np.uint64(c % 64)
@@ -307,9 +310,11 @@ def make_quota(used_limit: dict | None = None, used: dict | None = None, min: di
 def make_pod(requests: dict | None = None, limits: dict | None = None, priority_class: str = "",
              daemonset: bool = False, nonzero: tuple | None = None, qos: str = "",
              required_cpu_bind_policy: str = "", preferred_cpu_bind_policy: str = "",
-             devices: dict | None = None, quota_id: int = 0, non_preemptible: bool = False) -> np.ndarray:
+             devices: dict | None = None, quota_id: int = 0, non_preemptible: bool = False,
+             preferred_cpu_exclusive_policy: str = "") -> np.ndarray:
     """One single-container pod. nonzero = schedutil.GetNonzeroRequests (100m / 200MiB defaults); qos = the
-    koordinator.sh/qosClass label; *_cpu_bind_policy = the scheduling.koordinator.sh/resource-spec annotation."""
+    koordinator.sh/qosClass label; *_cpu_bind_policy / preferred_cpu_exclusive_policy = the
+    scheduling.koordinator.sh/resource-spec annotation."""
     p = np.zeros(1, dtype=abi.POD_DTYPE)
     r = p[0]
     req = _values(requests)
@@ -324,6 +329,7 @@ def make_pod(requests: dict | None = None, limits: dict | None = None, priority_
     r["qos"] = abi.QOS[qos]
     r["required_cpu_bind_policy"] = abi.BIND[required_cpu_bind_policy]
     r["preferred_cpu_bind_policy"] = abi.BIND[preferred_cpu_bind_policy]
+    r["preferred_cpu_exclusive_policy"] = abi.EXCL[preferred_cpu_exclusive_policy]
     for k, v in (devices or {}).items():  # device resources: PodRequestsAndLimits of e.g. koordinator.sh/gpu-core
         r["device_requests"][abi.DEVICE_RESOURCE_SLOTS[k]] = int(v)
     return p

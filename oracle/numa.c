@@ -17,8 +17,8 @@
  *   pkg/scheduler/frameworkext/topologymanager/{manager.go :58-111, policy.go :65-224, policy_best_effort.go,
  *                                               policy_restricted.go, policy_single_numa_node.go}
  *   pkg/util/bitmask/bitmask.go                                 IterateBitMasks :206-222, IsNarrowerThan :146-151
- * Scope: maxRefCount 1, CPU amplification included, no reservations (preferred CPUs empty),
- * CPU exclusive policy None, ≤ 4 NUMA nodes, ≤ 256 CPUs.  Go map iteration never decides a result here: every
+ * Scope: maxRefCount 1, CPU amplification included, CPU exclusive policies (PCPULevel / NUMANodeLevel,
+ * cpu_accumulator.go:247-330), no reservations (preferred CPUs empty), ≤ 4 NUMA nodes, ≤ 256 CPUs.  Go map iteration never decides a result here: every
  * accumulator sort ends on an ID, and the hint providers' resources are taken in sorted-name order (cpu, memory).
  */
 #include "numa.h"
@@ -90,7 +90,7 @@ static or_cpuset cpus_in_numa(const or_topology* t, int numa) {
 }
 
 /* ---------------------------------------------------------------------------------------------------- */
-/* cpuAccumulator (cpu_accumulator.go:234-822), maxRefCount 1, exclusive policy None                     */
+/* cpuAccumulator (cpu_accumulator.go:234-822), maxRefCount 1                                            */
 /* ---------------------------------------------------------------------------------------------------- */
 typedef struct {
   const or_topology* t;
@@ -98,7 +98,35 @@ typedef struct {
   int needed;
   int strategy;
   or_cpuset result;
+  int excl_policy;     /* KG_EXCL_* of the pod (a.exclusivePolicy) */
+  or_cpuset excl_seed; /* allocated cpus holding that policy (newCPUAccumulator :256-264) */
 } acc_t;
+
+/* The cpus a filterExclusive pass skips (isCPUExclusivePCPULevel / isCPUExclusiveNUMANodeLevel :318-330): every cpu
+ * of a core (PCPULevel) or NUMA node (NUMANodeLevel) in exclusiveInCores / exclusiveInNUMANodes — seeded from the
+ * allocated cpus holding the pod's policy and grown by every take() of this call (:290-304).  `pcpu` / `numa`:
+ * whether the calling list filters on that level (freeCoresInNode: NUMA only; freeCPUsInSocket: PCPU only;
+ * freeCPUsInNode / freeCPUs: both). */
+static or_cpuset acc_excluded(const acc_t* a, int pcpu, int numa) {
+  or_cpuset r = cs_empty();
+  const int pol = a->excl_policy;
+  if (!((pol == KG_EXCL_PCPU_LEVEL && pcpu) || (pol == KG_EXCL_NUMA_NODE_LEVEL && numa))) return r;
+  const or_cpuset held = cs_or(a->excl_seed, a->result);
+  const or_topology* t = a->t;
+  for (int c = 0; c < t->num_cpus; c++) {
+    if (!cs_has(&held, c)) continue;
+    if (pol == KG_EXCL_PCPU_LEVEL) {
+      const int core = core_of(t, c);
+      for (int q = 0; q < t->num_cpus; q++)
+        if (core_of(t, q) == core) cs_add(&r, q);
+    } else {
+      const int node = node_of(t, c);
+      for (int q = 0; q < t->num_cpus; q++)
+        if (node_of(t, q) == node) cs_add(&r, q);
+    }
+  }
+  return r;
+}
 
 typedef struct {
   int n;
@@ -141,12 +169,14 @@ static void swap_groups(list_t* g, int* gid, int i, int j) {
 /* freeCoresInNode(filterFullFreeCore, _) / freeCoresInSocket(filterFullFreeCore) (:371-527): per group (NUMA
  * node or socket) the cpus of its (full) free cores, cores by (free count desc, id), cpus ascending; groups by
  * (group free, [socket free for nodes], id). */
-static int free_cores_in(const acc_t* a, int by_node, int full, list_t* out) {
+static int free_cores_in(const acc_t* a, int by_node, int full, int filter_excl, list_t* out) {
   const or_topology* t = a->t;
   const int ng = by_node ? t->num_nodes : t->num_sockets;
+  /* freeCoresInNode(_, filterExclusive) skips NUMA-level exclusive cpus (:377); freeCoresInSocket never filters */
+  const or_cpuset alloc = (by_node && filter_excl) ? cs_andnot(a->allocatable, acc_excluded(a, 0, 1)) : a->allocatable;
   int socket_free[KG_MAX_CPUS] = {0}, core_cnt[KG_MAX_CPUS] = {0};
   for (int c = 0; c < t->num_cpus; c++)
-    if (cs_has(&a->allocatable, c)) {
+    if (cs_has(&alloc, c)) {
       core_cnt[core_of(t, c)]++;
       socket_free[socket_of(t, c)]++;
     }
@@ -160,7 +190,7 @@ static int free_cores_in(const acc_t* a, int by_node, int full, list_t* out) {
       for (int core = 0; core < t->num_cores; core++) {
         if (core_cnt[core] != cnt) continue;
         int cpus[KG_MAX_CPUS];
-        const int k = core_cpus(t, &a->allocatable, core, cpus);
+        const int k = core_cpus(t, &alloc, core, cpus);
         const int grp = by_node ? node_of(t, cpus[0]) : socket_of(t, cpus[0]);
         if (grp != g) continue;
         for (int i = 0; i < k; i++) l.v[l.n++] = cpus[i];
@@ -194,9 +224,12 @@ static int free_cores_in(const acc_t* a, int by_node, int full, list_t* out) {
 static int free_cpus_in(const acc_t* a, int by_node, int extract, list_t* out) {
   const or_topology* t = a->t;
   const int ng = by_node ? t->num_nodes : t->num_sockets;
+  /* filterExclusive (= extract): freeCPUsInNode skips PCPU- and NUMA-level exclusive cpus (:535), freeCPUsInSocket
+   * PCPU-level ones (:612), before counting */
+  const or_cpuset alloc = extract ? cs_andnot(a->allocatable, acc_excluded(a, 1, by_node)) : a->allocatable;
   int node_free[KG_MAX_CPUS] = {0}, socket_free[KG_MAX_CPUS] = {0};
   for (int c = 0; c < t->num_cpus; c++)
-    if (cs_has(&a->allocatable, c)) {
+    if (cs_has(&alloc, c)) {
       node_free[node_of(t, c)]++;
       socket_free[socket_of(t, c)]++;
     }
@@ -206,7 +239,7 @@ static int free_cpus_in(const acc_t* a, int by_node, int extract, list_t* out) {
     l.n = 0;
     int last_core = -1;
     for (int c = 0; c < t->num_cpus; c++)
-      if (cs_has(&a->allocatable, c) && (by_node ? node_of(t, c) : socket_of(t, c)) == g) {
+      if (cs_has(&alloc, c) && (by_node ? node_of(t, c) : socket_of(t, c)) == g) {
         if (extract && core_of(t, c) == last_core) continue;
         last_core = core_of(t, c);
         l.v[l.n++] = c;
@@ -237,12 +270,14 @@ static int free_cpus_in(const acc_t* a, int by_node, int extract, list_t* out) {
 
 /* freeCPUs (:666-774): every free cpu; cores by (socket colo desc, socket free, node free, core free asc,
  * socket asc, core asc), cpus ascending within a core. */
-static void free_cpus_all(const acc_t* a, list_t* out) {
+static void free_cpus_all(const acc_t* a, int filter_excl, list_t* out) {
   const or_topology* t = a->t;
+  /* freeCPUs(filterExclusive) skips PCPU- and NUMA-level exclusive cpus (:674) */
+  const or_cpuset alloc = filter_excl ? cs_andnot(a->allocatable, acc_excluded(a, 1, 1)) : a->allocatable;
   int node_free[KG_MAX_CPUS] = {0}, socket_free[KG_MAX_CPUS] = {0}, core_cnt[KG_MAX_CPUS] = {0};
   int socket_colo[KG_MAX_CPUS] = {0};
   for (int c = 0; c < t->num_cpus; c++) {
-    if (cs_has(&a->allocatable, c)) {
+    if (cs_has(&alloc, c)) {
       node_free[node_of(t, c)]++;
       socket_free[socket_of(t, c)]++;
       core_cnt[core_of(t, c)]++;
@@ -275,7 +310,7 @@ static void free_cpus_all(const acc_t* a, list_t* out) {
   out->n = 0;
   for (int i = 0; i < n; i++) {
     int cpus[KG_MAX_CPUS];
-    const int k = core_cpus(t, &a->allocatable, cores[i], cpus);
+    const int k = core_cpus(t, &alloc, cores[i], cpus);
     for (int q = 0; q < k; q++) out->v[out->n++] = cpus[q];
   }
 }
@@ -318,6 +353,11 @@ static void insertion_sort_len(list_t* g, int n, int desc) { /* stable (sort.Sli
 /* takeCPUs (:87-232).  0 and the set, or -1 ("not enough cpus" / "failed to allocate cpus"). */
 int or_take_cpus(const or_topology* t, or_cpuset available, int needed, int bind_policy, int strategy,
                  or_cpuset* out) {
+  return or_take_cpus_ex(t, available, needed, bind_policy, strategy, KG_EXCL_NONE, cs_empty(), out);
+}
+
+int or_take_cpus_ex(const or_topology* t, or_cpuset available, int needed, int bind_policy, int strategy,
+                    int excl_policy, or_cpuset excl_seed, or_cpuset* out) {
   static _Thread_local list_t groups[KG_MAX_CPUS], unsat[KG_MAX_CPUS]; /* per scheduling thread */
   acc_t a;
   a.t = t;
@@ -325,6 +365,8 @@ int or_take_cpus(const or_topology* t, or_cpuset available, int needed, int bind
   a.needed = needed;
   a.strategy = strategy;
   a.result = cs_empty();
+  a.excl_policy = excl_policy;
+  a.excl_seed = excl_seed;
   *out = cs_empty();
   if (acc_satisfied(&a)) return 0;
   if (acc_failed(&a)) return -1;
@@ -332,8 +374,8 @@ int or_take_cpus(const or_topology* t, or_cpuset available, int needed, int bind
   const int full = bind_policy == KG_BIND_FULL_PCPUS;
   if (full || cpc == 1) {
     if (a.needed <= cpus_per_node(t)) {
-      for (int fe = 0; fe < 2; fe++) { /* filterExclusive true, false: the same without exclusive policies */
-        const int ng = free_cores_in(&a, 1, 1, groups);
+      for (int fe = 0; fe < 2; fe++) { /* filterExclusive true, then false */
+        const int ng = free_cores_in(&a, 1, 1, fe == 0, groups);
         for (int g = 0; g < ng; g++)
           if (groups[g].n >= a.needed) {
             acc_take(&a, groups[g].v, a.needed);
@@ -343,7 +385,7 @@ int or_take_cpus(const or_topology* t, or_cpuset available, int needed, int bind
       }
     }
     if (a.needed <= cpus_per_socket(t)) {
-      const int ng = free_cores_in(&a, 0, 1, groups);
+      const int ng = free_cores_in(&a, 0, 1, 0, groups);
       for (int g = 0; g < ng; g++)
         if (groups[g].n >= a.needed) {
           acc_take(&a, groups[g].v, a.needed);
@@ -351,7 +393,7 @@ int or_take_cpus(const or_topology* t, or_cpuset available, int needed, int bind
           return 0;
         }
     }
-    int ng = free_cores_in(&a, 0, 1, groups);
+    int ng = free_cores_in(&a, 0, 1, 0, groups);
     insertion_sort_len(groups, ng, 1);
     int nu = 0;
     for (int g = 0; g < ng; g++) {
@@ -407,7 +449,7 @@ int or_take_cpus(const or_topology* t, or_cpuset available, int needed, int bind
   }
   for (int fe = 0; fe < 2; fe++) {
     list_t l;
-    free_cpus_all(&a, &l);
+    free_cpus_all(&a, fe == 0, &l);
     spread_cpus(&a, &l);
     for (int i = 0; i < l.n; i++) {
       if (acc_needs(&a, 1)) acc_take(&a, &l.v[i], 1);
@@ -477,6 +519,8 @@ void or_numa_node_init(or_numa_node* n, const kg_node_numa* s) {
   for (int i = 0; i < OR_CPUSET_WORDS; i++) {
     n->reserved.w[i] = s->reserved_cpus[i];
     n->allocated.w[i] = s->allocated_cpus[i];
+    n->excl_pcpu.w[i] = s->exclusive_pcpu_cpus[i] & s->allocated_cpus[i];
+    n->excl_numa.w[i] = s->exclusive_numa_cpus[i] & s->allocated_cpus[i];
   }
 }
 
@@ -508,6 +552,7 @@ void or_numa_pod_init(const kg_config* cfg, const kg_pod* pod, or_numa_pod* p) {
       p->required_policy = required;
       p->preferred_policy = bind;
       p->num_cpus_needed = (int)(p->req_cpu / 1000);
+      p->excl_policy = (int)pod->preferred_cpu_exclusive_policy; /* plugin.go:261 */
     }
   }
 }
@@ -810,6 +855,13 @@ typedef struct {
   int64_t cpu[KG_MAX_NUMA], mem[KG_MAX_NUMA];
 } numa_alloc;
 
+/* the node's allocated cpus holding the pod's exclusive policy (GetAvailableCPUs' allocatedCPUs → newCPUAccumulator) */
+static or_cpuset excl_seed(const or_numa_node* n, const or_numa_pod* p) {
+  if (p->excl_policy == KG_EXCL_PCPU_LEVEL) return n->excl_pcpu;
+  if (p->excl_policy == KG_EXCL_NUMA_NODE_LEVEL) return n->excl_numa;
+  return cs_empty();
+}
+
 static int allocate(const kg_config* cfg, const or_numa_node* n, const or_numa_pod* p, const or_hint* hint,
                     numa_alloc* res, or_cpuset* cpus) {
   res->n = 0;
@@ -865,7 +917,8 @@ static int allocate(const kg_config* cfg, const or_numa_node* n, const or_numa_p
         const int node_need = (int)(res->cpu[k] / 1000);
         if (node_need < num) num = node_need;
         or_cpuset got;
-        if (or_take_cpus(&n->topo, in_node, num, bind, strategy, &got) != 0) return -1;
+        if (or_take_cpus_ex(&n->topo, in_node, num, bind, strategy, p->excl_policy, excl_seed(n, p), &got) != 0)
+          return -1;
         result = cs_or(result, got);
       }
       needed -= cs_size(&result);
@@ -873,7 +926,9 @@ static int allocate(const kg_config* cfg, const or_numa_node* n, const or_numa_p
     }
     if (needed > 0) {
       or_cpuset got;
-      if (or_take_cpus(&n->topo, cs_andnot(avail, result), needed, bind, strategy, &got) != 0) return -1;
+      if (or_take_cpus_ex(&n->topo, cs_andnot(avail, result), needed, bind, strategy, p->excl_policy,
+                          excl_seed(n, p), &got) != 0)
+        return -1;
       result = cs_or(result, got);
     }
     if (required && !satisfied_required(&n->topo, result, bind)) return -1;
@@ -981,8 +1036,12 @@ int or_numa_reserve(const kg_config* cfg, or_numa_node* n, const or_numa_pod* p,
   if (p->request_cpu_bind && (!n->has_topology || !n->valid_topology)) return -1;
   numa_alloc res;
   if (allocate(cfg, n, p, affinity, &res, cpus) != 0) return -1;
-  /* resourceManager.Update → addPodAllocation (node_allocation.go:76-103) */
+  /* resourceManager.Update → addPodAllocation (node_allocation.go:76-103): the pod's cpus carry its exclusive policy */
   n->allocated = cs_or(n->allocated, *cpus);
+  n->excl_pcpu = cs_andnot(n->excl_pcpu, *cpus);
+  n->excl_numa = cs_andnot(n->excl_numa, *cpus);
+  if (p->excl_policy == KG_EXCL_PCPU_LEVEL) n->excl_pcpu = cs_or(n->excl_pcpu, *cpus);
+  if (p->excl_policy == KG_EXCL_NUMA_NODE_LEVEL) n->excl_numa = cs_or(n->excl_numa, *cpus);
   for (int k = 0; k < res.n; k++) {
     const int i = res.numa[k];
     n->numa_alloc_cpu[i] += res.cpu[k];
@@ -1000,7 +1059,11 @@ int or_numa_reserve(const kg_config* cfg, or_numa_node* n, const or_numa_pod* p,
 /* resourceManager.Release → NodeAllocation.release (node_allocation.go:105-131): the pod's cpus leave the
  * allocated set (maxRefCount 1) and its NUMANodeResources are subtracted (SubtractWithNonNegativeResult). */
 void or_numa_release(or_numa_node* n, const or_cpuset* cpus, const int64_t* alloc) {
-  for (int w = 0; w < OR_CPUSET_WORDS; w++) n->allocated.w[w] &= ~cpus->w[w];
+  for (int w = 0; w < OR_CPUSET_WORDS; w++) {
+    n->allocated.w[w] &= ~cpus->w[w];
+    n->excl_pcpu.w[w] &= ~cpus->w[w]; /* RefCount 0: the CPUInfo (and its policy) is deleted */
+    n->excl_numa.w[w] &= ~cpus->w[w];
+  }
   for (int i = 0; i < KG_MAX_NUMA; i++) {
     if (!((alloc[0] >> i) & 1)) continue;
     n->numa_alloc_cpu[i] = n->numa_alloc_cpu[i] - alloc[1 + i] > 0 ? n->numa_alloc_cpu[i] - alloc[1 + i] : 0;
@@ -1035,6 +1098,21 @@ int or_take_cpus_flat(int sockets, int nodes_per_socket, int cores_per_node, int
   or_cpuset a, r;
   for (int w = 0; w < OR_CPUSET_WORDS; w++) a.w[w] = available[w];
   const int rc = or_take_cpus(&t, a, needed, bind_policy, strategy, &r);
+  for (int w = 0; w < OR_CPUSET_WORDS; w++) out[w] = r.w[w];
+  return rc;
+}
+
+int or_take_cpus_excl_flat(int sockets, int nodes_per_socket, int cores_per_node, int cpus_per_core,
+                           const uint64_t* available, int needed, int bind_policy, int strategy, int excl_policy,
+                           const uint64_t* excl_seed, uint64_t* out) {
+  or_topology t;
+  or_topology_build(&t, sockets, nodes_per_socket, cores_per_node, cpus_per_core);
+  or_cpuset a, seed, r;
+  for (int w = 0; w < OR_CPUSET_WORDS; w++) {
+    a.w[w] = available[w];
+    seed.w[w] = excl_seed[w];
+  }
+  const int rc = or_take_cpus_ex(&t, a, needed, bind_policy, strategy, excl_policy, seed, &r);
   for (int w = 0; w < OR_CPUSET_WORDS; w++) out[w] = r.w[w];
   return rc;
 }

@@ -37,6 +37,7 @@ typedef struct {
   or_cpuset reserved;
   /* mutable */
   or_cpuset allocated;
+  or_cpuset excl_pcpu, excl_numa; /* allocated cpus whose CPUInfo.ExclusivePolicy is PCPULevel / NUMANodeLevel */
   int64_t numa_alloc_cpu[KG_MAX_NUMA], numa_alloc_mem[KG_MAX_NUMA];
   int numa_alloc_present[KG_MAX_NUMA]; /* allocatedResources[numa] exists */
 } or_numa_node;
@@ -47,6 +48,7 @@ typedef struct {
   int request_cpu_bind;
   int required_policy, preferred_policy; /* KG_BIND_* */
   int num_cpus_needed;
+  int excl_policy;          /* preferredCPUExclusivePolicy (KG_EXCL_*) */
   int64_t req_cpu, req_mem; /* PodRequestsAndLimits cpu (milli) / memory */
 } or_numa_pod;
 
@@ -61,6 +63,9 @@ typedef struct {
 void or_topology_build(or_topology* t, int sockets, int nodes_per_socket, int cores_per_node, int cpus_per_core);
 int or_take_cpus(const or_topology* t, or_cpuset available, int needed, int bind_policy, int strategy,
                  or_cpuset* out);
+/* takeCPUs with a CPUExclusivePolicy: excl_seed = the node's allocated cpus holding that policy */
+int or_take_cpus_ex(const or_topology* t, or_cpuset available, int needed, int bind_policy, int strategy,
+                    int excl_policy, or_cpuset excl_seed, or_cpuset* out);
 or_cpuset or_filter_required(const or_topology* t, or_cpuset available, int policy);
 
 void or_numa_node_init(or_numa_node* n, const kg_node_numa* src);

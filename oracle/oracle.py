@@ -71,6 +71,8 @@ def lib():
         L.or_numa_state_read.argtypes = [vp, i64, vp, vp, vp]
         L.or_take_cpus_flat.argtypes = [i, i, i, i, vp, i, i, i, vp]
         L.or_take_cpus_flat.restype = i
+        L.or_take_cpus_excl_flat.argtypes = [i, i, i, i, vp, i, i, i, i, vp, vp]
+        L.or_take_cpus_excl_flat.restype = i
         L.or_numa_eval_flat.argtypes = [vp, vp, vp, i64, i64, i64, i64, vp, vp]
         L.or_numa_eval_flat.restype = i
         L.or_numa_reserve_flat.argtypes = [vp, vp, vp, vp]
@@ -365,13 +367,25 @@ def schedule_numa(cfg, nodes, metrics, st, numa_buf, pods, now_ns: int, n_thread
     return out_node, out_score
 
 
-def take_cpus(topology, available, needed: int, bind_policy: str, strategy: str):
-    """takeCPUs on buildCPUTopologyForTest(*topology); returns the cpu list or None on error."""
+def _cpu_words(cpus):
     words = np.zeros(abi.MAX_CPUS // 64, dtype=np.uint64)
-    for c in available:
+    for c in cpus:
         words[c // 64] |= np.uint64(1) << np.uint64(c % 64)
+    return words
+
+
+def take_cpus(topology, available, needed: int, bind_policy: str, strategy: str, exclusive_policy: str = "",
+              exclusive_cpus=()):
+    """takeCPUs on buildCPUTopologyForTest(*topology); returns the cpu list or None on error.  exclusive_policy =
+    the pod's CPUExclusivePolicy, exclusive_cpus = the allocated cpus holding that policy."""
+    words = _cpu_words(available)
     out = np.zeros(abi.MAX_CPUS // 64, dtype=np.uint64)
-    rc = lib().or_take_cpus_flat(*topology, p(words), needed, abi.BIND[bind_policy], abi.STRATEGY[strategy], p(out))
+    if exclusive_policy:
+        rc = lib().or_take_cpus_excl_flat(*topology, p(words), needed, abi.BIND[bind_policy], abi.STRATEGY[strategy],
+                                          abi.EXCL[exclusive_policy], p(_cpu_words(exclusive_cpus)), p(out))
+    else:
+        rc = lib().or_take_cpus_flat(*topology, p(words), needed, abi.BIND[bind_policy], abi.STRATEGY[strategy],
+                                     p(out))
     if rc != 0:
         return None
     return [64 * w + b for w in range(len(out)) for b in range(64) if (int(out[w]) >> b) & 1]

@@ -3,6 +3,7 @@ table-driven tests (paths under /root/reference/pkg/scheduler/plugins/nodenumare
 
 * numa_take_cpus.json  cpu_accumulator_test.go TestTakeFullPCPUs (:59-173, NUMAMostAllocated),
                        TestTakeFullPCPUsWithNUMALeastAllocated (:175-289), TestTakeSpreadByPCPUs (:301-362).
+* numa_take_cpus_exclusive.json  TestTakeCPUsWithExclusivePolicy (:435-558): PCPULevel / NUMANodeLevel / None.
                        topology = buildCPUTopologyForTest(sockets, nodesPerSocket, coresPerNode, cpusPerCore).
 * numa_filter.json     plugin_test.go TestPlugin_Filter (:548-816): the cases expressible as a pod (state written
                        by PreFilter; 96 cpu / 512Gi node; zones = CPUsPerNode cores + 32Gi each, :779-786).
@@ -167,8 +168,41 @@ AFFINITY = [
 ]
 
 
+# TestTakeCPUsWithExclusivePolicy (:435-558): allocatedExclusiveCPUs are allocated (not available) and hold
+# allocatedExclusivePolicy (default PCPULevel, :530-534); the pod's exclusivePolicy defaults to PCPULevel (:538-540),
+# bindPolicy to SpreadByPCPUs (:541-543); maxRefCount 1; NUMAMostAllocated (:547).
+EXCL = [
+    dict(line=448, name="allocate cpus on full-free socket with PCPULevel", topo=[2, 1, 4, 2], alloc=[0, 2],
+         alloc_policy="PCPULevel", excl="PCPULevel", policy="SpreadByPCPUs", need=4, want=[8, 10, 12, 14]),
+    dict(line=456, name="allocate overlapped cpus with PCPULevel", topo=[2, 1, 4, 2], alloc=[],
+         alloc_policy="PCPULevel", excl="PCPULevel", policy="SpreadByPCPUs", need=10,
+         want=[0, 1, 2, 3, 4, 6, 8, 10, 12, 14]),
+    dict(line=463, name="allocate cpus on large-size partially-allocated socket with PCPULevel", topo=[2, 1, 8, 2],
+         alloc=[0, 2], alloc_policy="PCPULevel", excl="PCPULevel", policy="SpreadByPCPUs", need=4,
+         want=[4, 6, 8, 10]),
+    dict(line=471, name="allocate cpus with none exclusive policy", topo=[2, 1, 8, 2], alloc=[0, 2],
+         alloc_policy="PCPULevel", excl="None", policy="SpreadByPCPUs", need=4, want=[1, 3, 4, 6]),
+    dict(line=480, name="allocate cpus on full-free socket with NUMANodeLevel", topo=[2, 1, 4, 2], alloc=[0, 2],
+         alloc_policy="NUMANodeLevel", excl="NUMANodeLevel", policy="SpreadByPCPUs", need=4, want=[8, 10, 12, 14]),
+    dict(line=490, name="allocate cpus on partially-allocated socket without NUMANodeLevel", topo=[2, 1, 4, 2],
+         alloc=[0, 2], alloc_policy="NUMANodeLevel", excl="None", policy="SpreadByPCPUs", need=4,
+         want=[1, 3, 4, 6]),
+    dict(line=500, name="allocate cpus on full-free socket with NUMANodeLevel with PCPUs", topo=[2, 1, 4, 2],
+         alloc=[0, 2], alloc_policy="NUMANodeLevel", excl="NUMANodeLevel", policy="FullPCPUs", need=4,
+         want=[8, 9, 10, 11]),
+    dict(line=511, name="allocate cpus on partially-allocated socket without NUMANodeLevel with PCPUs",
+         topo=[2, 1, 4, 2], alloc=[0, 2], alloc_policy="NUMANodeLevel", excl="None", policy="FullPCPUs", need=4,
+         want=[4, 5, 6, 7]),
+]
+for c in EXCL:
+    c["strategy"] = "MostAllocated"
+
+
 def main():
     docs = {
+        "numa_take_cpus_exclusive.json": dict(source=ACC, harness="takeCPUs(topology, 1, available, allocated with "
+                                                                  "alloc_policy, need, policy, excl, NUMAMostAllocated)",
+                                              cases=EXCL),
         "numa_take_cpus.json": dict(source=ACC, harness="takeCPUs(topology, 1, available, allocated, need, policy, "
                                                         "CPUExclusivePolicyNone, strategy)", cases=TAKE),
         "numa_filter.json": dict(source=PLG, harness="TestPlugin_Filter :744-815", cases=FILTER),

@@ -31,6 +31,20 @@ def test_take_cpus(dc):
     assert got == sorted(c["want"]), c["source_line"]
 
 
+@pytest.mark.parametrize("dc", _cases("numa_take_cpus_exclusive.json"), ids=_id)
+def test_take_cpus_exclusive(dc):
+    """TestTakeCPUsWithExclusivePolicy: the pod's exclusive policy filters the cores / NUMA nodes holding cpus of
+    the same policy; the allocated cpus hold alloc_policy."""
+    _, c = dc
+    s, n, k, t = c["topo"]
+    total = s * n * k * t
+    avail = [x for x in range(total) if x not in set(c["alloc"])]
+    seed = c["alloc"] if c["alloc_policy"] == c["excl"] else []
+    got = oracle.take_cpus(tuple(c["topo"]), avail, c["need"], c["policy"], c["strategy"],
+                           exclusive_policy=c["excl"], exclusive_cpus=seed)
+    assert got == sorted(c["want"]), c["source_line"]
+
+
 def filter_case(c):
     """(config, kg_node_numa, kg_pod) of one TestPlugin_Filter case."""
     cfg = framework.build_config(profile=NUMA_PROFILE)

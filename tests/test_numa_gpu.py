@@ -89,6 +89,20 @@ def test_golden_take_cpus_device(dc):
     assert node == 0 and cpus == sorted(c["want"]), c["source_line"]
 
 
+@pytest.mark.parametrize("dc", TG._cases("numa_take_cpus_exclusive.json"), ids=TG._id)
+def test_golden_take_cpus_exclusive_device(dc):
+    """TestTakeCPUsWithExclusivePolicy through Reserve: the allocated cpus hold alloc_policy on the node
+    (kg_node_numa.exclusive_*_cpus), the pod prefers the case's exclusive and bind policies."""
+    _, c = dc
+    cfg = F.build_config(profile=TG.NUMA_PROFILE)
+    ex = {"exclusive_pcpu_cpus": c["alloc"]} if c["alloc_policy"] == "PCPULevel" else {"exclusive_numa_cpus": c["alloc"]}
+    nn = F.make_node_numa(*c["topo"], numa_allocate_strategy=c["strategy"], allocated_cpus=c["alloc"], **ex)
+    pod = F.make_pod({"cpu": str(c["need"])}, priority_class="koord-prod", qos="LSR",
+                     preferred_cpu_bind_policy=c["policy"], preferred_cpu_exclusive_policy=c["excl"])
+    node, cpus = _schedule_one(cfg, nn, pod)
+    assert node == 0 and cpus == sorted(c["want"]), c["source_line"]
+
+
 @pytest.mark.parametrize("dc", TG._cases("numa_reserve.json"), ids=TG._id)
 def test_golden_reserve_device(dc):
     _, c = dc
@@ -180,3 +194,36 @@ def test_numa_upsert_requires_profile():
     with Engine(cfg, 4) as e:
         with pytest.raises(abi.KoordGPUError):
             e.upsert_numa(F.make_node_numa(2, 1, 4, 2))
+
+
+def _with_exclusive(numa, pods, seed):
+    """Marks half of every node's allocated cpus as held by PCPULevel / NUMANodeLevel pods and gives 30 % / 20 % of the
+    queue those preferred exclusive policies (the rest None)."""
+    rng = np.random.default_rng(seed)
+    numa = numa.copy()
+    for i in range(len(numa)):
+        alloc = F.cpuset_of(numa[i]["allocated_cpus"])
+        pick = rng.random(len(alloc))
+        for name, lo, hi in (("exclusive_pcpu_cpus", 0.0, 0.3), ("exclusive_numa_cpus", 0.3, 0.5)):
+            w = np.zeros(abi.MAX_CPUS // 64, dtype=np.uint64)
+            for c, u in zip(alloc, pick):
+                if lo <= u < hi:
+                    w[c // 64] |= np.uint64(1) << np.uint64(c % 64)
+            numa[i][name] = w
+    pods = pods.copy()
+    u = rng.random(len(pods))
+    pods["preferred_cpu_exclusive_policy"] = np.where(u < 0.3, 1, np.where(u < 0.5, 2, 0))
+    return numa, pods
+
+
+@pytest.mark.parametrize("batch", [16, 1])
+def test_c4_exclusive_policies_parity(batch):
+    """C4 with CPU exclusive policies (cpu_accumulator.go:247-330): bit-exact placements, cpusets and NodeAllocation
+    against the oracle, the masks carried across Reserve."""
+    cfg = F.build_config(profile=FULL_PROFILE, batch_pods=batch, pods_per_wave=min(8, batch))
+    cluster, numa = synth.make_numa_cluster(500, seed=synth.BASE_SEED + 46)
+    pods = synth.make_numa_pods(2000 if batch > 1 else 300, seed=synth.BASE_SEED + 47)
+    numa, pods = _with_exclusive(numa, pods, 48)
+    node, cpus = _numa_parity(cfg, cluster, numa, pods)
+    assert (node >= 0).mean() > 0.5
+    assert (cpus != 0).any()
