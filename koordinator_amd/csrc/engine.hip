@@ -912,7 +912,9 @@ __global__ __launch_bounds__(kWave) void resolve_round(DevTable T0, const DevPod
         const bool aux = (PF & PF_FIT_FILTER) && (p.flags & P_AUX);  // ephemeral-storage / scalar requests
         const int64_t* rq = paux + (size_t)(first + j) * kAux;
         mod_row_settle<PF>(R0, s_cand, s_pods, T0, P);
+        if (lane == 0) KG_LANE_SUB(j, 0);
         uint64_t mk = mod_row_key<PF>(R0, p, P, s_par);
+        if (lane == 0) KG_LANE_SUB(j, 1);
         if (aux && mk && !mod_aux_fits(table_at(T0), R0.node, rq, j, my_out, s_pods, paux + (size_t)first * kAux))
           mk = 0;
         if (nM > kWave) {
@@ -922,7 +924,9 @@ __global__ __launch_bounds__(kWave) void resolve_round(DevTable T0, const DevPod
             k1 = 0;
           mk = k1 > mk ? k1 : mk;
         }
+        if (lane == 0) KG_LANE_SUB(j, 2);
         const uint64_t mbest = wave_max_modkey(mk, narrow);
+        if (lane == 0) KG_LANE_SUB(j, 3);
         from_mod = mbest > best;
         best = from_mod ? mbest : best;
       }

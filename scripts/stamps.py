@@ -23,10 +23,11 @@ with Engine(cfg, n) as e:
     e.profile(True)
     st = e.schedule_staged(0, npods)
     prof = e.profile_read()
-    buf = np.zeros(4 * 32 * 2 + 64 * 6 + 2, dtype=np.uint64)
+    buf = np.zeros(4 * 32 * 2 + 64 * 6 + 2 + 64 * 8, dtype=np.uint64)
     abi.check(e.lib, e.lib.kg_debug_stamps(e.h, abi.ptr(buf)))
     stamps = buf[:256].reshape(4, 32, 2)
     diag = buf[256:256 + 384].reshape(64, 6)
+    lane = buf[256 + 384 + 2:].reshape(64, 8)
 print(f"nodes={n} pods={npods} depth={depth} batch={batch}: rounds={int(st['device_batches'])} "
       f"slow={st['reserved'][0]:.0f} steps={st['reserved'][1]:.0f} seconds={st['seconds']:.4f} "
       f"pods/s={npods / st['seconds']:.0f}")
@@ -50,5 +51,7 @@ for j in range(64):
         break
     if prev is not None:
         sub = " ".join(f"{int(diag[j - 1, 2 + k]) - prev if diag[j - 1, 2 + k] else -1:5d}" for k in range(4))
-        print(f"  pod {j - 1:2d}: {c - prev:6d} cyc pos={b >> 8:2d} slow={b & 1} new={(b >> 1) & 1}  sub {sub}")
+        ls = " ".join(f"{int(lane[j - 1, k]) - prev if lane[j - 1, k] > prev else -1:5d}" for k in range(4))
+        print(f"  pod {j - 1:2d}: {c - prev:6d} cyc pos={b >> 8:2d} slow={b & 1} new={(b >> 1) & 1}  sub {sub}"
+              f"  slow-path [settled, keyed, aux, max] {ls}")
     prev = c
