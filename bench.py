@@ -72,6 +72,7 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-nproc", action="store_true", help="also time the oracle with os.cpu_count() threads")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-pcie", action="store_true", help="skip the PCIe-inclusive fresh-engine step (profiling runs)")
     ap.add_argument("--kernel-iters", type=int, default=20)
     ap.add_argument("--profile-pods", type=int, default=None, help="pods scheduled with live kernel timing after "
                     "the timed region (default min(pods per step, 20k))")
@@ -369,7 +370,7 @@ def main():
 
     # PCIe-inclusive path (host pods in, host decisions out) on a fresh engine, one step
     pcie = None
-    if d.world == 1:
+    if d.world == 1 and not args.no_pcie:
         with engine() as ep:
             tt = time.perf_counter()
             ep.schedule(pods[: args.pods_per_step])
