@@ -1153,6 +1153,7 @@ __global__ __launch_bounds__(kWave) void resolve_round_numa(DevTable T, NumaTabl
     // The best unmodified candidate e wins unless a modified row beats it: its row is brought into the spare slot
     // nM before the re-score, so its Filter (the affinity Reserve needs) runs alongside the modified rows' instead
     // of after the search on one lane.  Slot nM only becomes a modified row if e wins.
+    if (lane == 0) KG_LANE_SUB(j, 0);
     if (um && lane == nM) {
       const uint32_t en = key_node(best);
       midx = en;
@@ -1161,6 +1162,7 @@ __global__ __launch_bounds__(kWave) void resolve_round_numa(DevTable T, NumaTabl
       s_nm[nM] = NT.m[en];
       mv = make_view(&s_ns[nM], &s_nm[nM], NP);
     }
+    if (lane == 0) KG_LANE_SUB(j, 1);
     NumaHint maff{0, 1, 0, 0};  // the affinity of this lane's row (Reserve reuses it when the row wins)
     if (nM > 0 || um) {
       uint64_t mk = 0;
@@ -1168,6 +1170,7 @@ __global__ __launch_bounds__(kWave) void resolve_round_numa(DevTable T, NumaTabl
         int64_t t = 0;
         if (eval_node_numa(mrow, mv, p, np, P, NP, t, maff) && lane < nM) mk = make_key(t, midx);
       }
+      if (lane == 0) KG_LANE_SUB(j, 2);
       const uint64_t mbest = wave_max_key(mk);
       best = mbest > best ? mbest : best;
     }
@@ -1188,17 +1191,23 @@ __global__ __launch_bounds__(kWave) void resolve_round_numa(DevTable T, NumaTabl
     __syncthreads();
     KG_POD_SUB(j, 1);
     int placed = 0;
-    if (lane == owner) {  // Reserve with the affinity Filter stored on the winner's row this pod
-      const NumaHint aff = maff;
+    {  // Reserve with the affinity Filter stored on the winner's row this pod, run wave-uniformly on the owner's
+       // row (LDS slot `owner`): scalar mask arithmetic, the owner lane commits
+      const NumaHint aff{(uint32_t)__builtin_amdgcn_readlane((int)maff.mask, owner),
+                         __builtin_amdgcn_readlane(maff.nil, owner), __builtin_amdgcn_readlane(maff.preferred, owner),
+                         __builtin_amdgcn_readlane(maff.score, owner)};
 #ifdef KG_STAMPS
-      if (j < 64) g_pod_diag[j][5] = __builtin_amdgcn_s_memtime();
+      if (j < 64 && lane == 0) g_pod_diag[j][5] = __builtin_amdgcn_s_memtime();
 #endif
       CpuSet cpus;
       NumaAlloc rec;
-      const NumaStatic ns = s_ns[lane];
-      NumaMut nm = s_nm[lane];
-      if (numa_reserve(ns, nm, mv, np, aff, cpus, rec)) {
-        placed = 1;
+      const NumaStatic ns = s_ns[owner];
+      NumaMut nm = s_nm[owner];
+      const NumaView ov = make_view(&ns, &nm, NP);
+      if (lane == 0) KG_LANE_SUB(j, 3);
+      placed = numa_reserve(ns, nm, ov, np, aff, cpus, rec) ? 1 : 0;
+      if (lane == 0) KG_LANE_SUB(j, 4);
+      if (placed && lane == owner) {
         s_nm[lane] = nm;
         mv = make_view(&s_ns[lane], &s_nm[lane], NP);
         mrow.req_cpu += p.req_cpu;  // assume: NodeInfo.AddPod + LoadAware assign cache
@@ -1224,7 +1233,6 @@ __global__ __launch_bounds__(kWave) void resolve_round_numa(DevTable T, NumaTabl
         }
       }
     }
-    placed = __builtin_amdgcn_readlane(placed, owner);
     KG_POD_SUB(j, 2);
     if (placed && nq > 0) quota_charge(ql, p, lane);
     my_out = lane == j ? (placed ? best : 0) : my_out;

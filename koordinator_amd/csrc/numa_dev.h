@@ -303,8 +303,11 @@ __device__ __forceinline__ CpuSet spread_first_k(const Topo& t, const CpuSet& s,
   return cs_or(first, lowest_k(cs_andnot(s, first), k - nf));
 }
 
-__device__ __noinline__ bool take_cpus(const Topo& t, const CpuSet& available, int needed, int bind, int strategy,
-                                 CpuSet& out, int excl, const CpuSet& seed) {
+// Inlined into callers that run it wave-uniformly (every lane with the same node and pod): the masks, counts and group
+// keys then live in scalar registers and the branches are scalar (s_and_b64 / s_bcnt1 / s_cselect), instead of one
+// active lane issuing the 64-bit mask arithmetic as vector instructions through a call frame in scratch.
+__device__ __forceinline__ bool take_cpus(const Topo& t, const CpuSet& available, int needed, int bind, int strategy,
+                                          CpuSet& out, int excl, const CpuSet& seed) {
   Acc a;
   a.t = t;
   a.avail = cs_and(available, t.all());
@@ -998,8 +1001,9 @@ __device__ __forceinline__ bool numa_eval(const NumaView& v, const NumaPod& p, c
 
 // NodeNUMAResource.Reserve (plugin.go:375-415) → Allocate with the exact cpuset (cpu accumulator) →
 // addPodAllocation (node_allocation.go:76-103).  False: the allocation fails and the pod is not placed.
-__device__ __noinline__ bool numa_reserve(const NumaStatic& s, NumaMut& m, const NumaView& v, const NumaPod& p,
-                                    const NumaHint& aff, CpuSet& cpus, NumaAlloc& rec) {
+// (inlined: the resolvers call it wave-uniformly, see take_cpus)
+__device__ __forceinline__ bool numa_reserve(const NumaStatic& s, NumaMut& m, const NumaView& v, const NumaPod& p,
+                                             const NumaHint& aff, CpuSet& cpus, NumaAlloc& rec) {
   cpus = cs_zero();
   rec.res = 0;  // the PodAllocation's NUMANodeResources, kept for Release (node_allocation.go:105-131)
   if (skip_the_node(p, v.policy)) return true;
@@ -1015,19 +1019,20 @@ __device__ __noinline__ bool numa_reserve(const NumaStatic& s, NumaMut& m, const
 #pragma unroll
     for (int w = 0; w < kCpuWords; ++w)
       seed.w[w] = p.excl == KG_EXCL_PCPU_LEVEL ? m.excl_pcpu[w] : p.excl == KG_EXCL_NUMA_NODE_LEVEL ? m.excl_numa[w] : 0;
-    if (a.res) {
-      for (int i = 0; i < kNumaMax; ++i) {
-        if (!((a.res >> i) & 1u)) continue;
-        const CpuSet in = cs_and(avail, t.node_cpus(i));
-        int num = cs_count(in);
+    // per NUMA node of the hint (ascending), or once over every available cpu: one inlined take_cpus
+    const int parts = a.res ? kNumaMax : 1;
+    for (int i = 0; i < parts; ++i) {
+      if (a.res && !((a.res >> i) & 1u)) continue;
+      const CpuSet in = a.res ? cs_and(avail, t.node_cpus(i)) : avail;
+      int num = p.needed;
+      if (a.res) {
+        num = cs_count(in);
         const int want = (int)(a.cpu[i] / 1000);
         if (want < num) num = want;
-        CpuSet one;
-        if (!take_cpus(t, in, num, bind, v.strategy, one, p.excl, seed)) return false;
-        cpus = cs_or(cpus, one);
       }
-    } else if (!take_cpus(t, avail, p.needed, bind, v.strategy, cpus, p.excl, seed)) {
-      return false;
+      CpuSet one;
+      if (!take_cpus(t, in, num, bind, v.strategy, one, p.excl, seed)) return false;
+      cpus = cs_or(cpus, one);
     }
     if (p.required != 0) {  // satisfiedRequiredCPUBindPolicy (:568-589), exact
       if (bind == 2 && t.cpc > 1 && cs_count(full_core_cpus(t, cpus)) != cs_count(cpus)) return false;

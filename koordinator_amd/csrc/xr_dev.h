@@ -267,16 +267,13 @@ __device__ __forceinline__ bool xr_reserve(const DevTable& T, RsvNode* __restric
   NumaAlloc rec;
   rec.res = 0;
   if (NUMA && X.ns) {
-    int ok = 1;
-    if (lane == owner) {
-      const NumaStatic nsw = X.ns[w];
-      nmw = X.nm[w];
-      const NumaView nv = make_view(&nsw, &nmw, X.NP);
-      const uint32_t a = X.aff[w];
-      const NumaHint aff{a & 0xFFu, (int)((a >> 8) & 1u), 0, 0};
-      ok = numa_reserve(nsw, nmw, nv, X.npods[j], aff, cpus, rec) ? 1 : 0;
-    }
-    ok = __builtin_amdgcn_readlane(ok, owner);
+    // every lane runs the NUMA Reserve on the same row (uniform loads): scalar mask arithmetic (take_cpus)
+    const NumaStatic nsw = X.ns[w];
+    nmw = X.nm[w];
+    const NumaView nv = make_view(&nsw, &nmw, X.NP);
+    const uint32_t a = X.aff[w];
+    const NumaHint aff{a & 0xFFu, (int)((a >> 8) & 1u), 0, 0};
+    const bool ok = numa_reserve(nsw, nmw, nv, X.npods[j], aff, cpus, rec);
     if (!ok) {
       if (lane == 0 && X.out_minors) X.out_minors[j] = 0;
       return false;

@@ -25,13 +25,14 @@ with Engine(cfg, n) as e:
     e.profile(True)
     st = e.schedule_staged(0, npods)
     prof = e.profile_read()
-    buf = np.zeros(4 * 32 * 2 + 64 * 6 + 2, dtype=np.uint64)
+    buf = np.zeros(4 * 32 * 2 + 64 * 6 + 2 + 64 * 8, dtype=np.uint64)  # + the lane stamps kg_debug_stamps also copies
     abi.check(e.lib, e.lib.kg_debug_stamps(e.h, abi.ptr(buf)))
     diag = buf[256:256 + 384].reshape(64, 6)
+    lane = buf[256 + 384 + 2:].reshape(64, 8)
 print(f"nodes={n} pods={npods} batch={batch}: rounds={int(st['device_batches'])} seconds={st['seconds']:.4f} "
       f"pods/s={npods / st['seconds']:.0f}")
 print("live:", {k: (round(ms / c * 1e3, 2), c) for k, (ms, c) in prof.items()})
-merges, fallbacks = int(buf[-2]), int(buf[-1])
+merges, fallbacks = int(buf[256 + 384]), int(buf[256 + 384 + 1])
 print(f"NUMA hint merges: {merges}, all-permutation fallback passes: {fallbacks} "
       f"({100.0 * fallbacks / max(merges, 1):.2f} %)")
 print("== resolver per pod (last launch): cycles; nM; sub: rescored / winner row ready / reserved")
@@ -42,5 +43,7 @@ for j in range(64):
         break
     if prev is not None:
         sub = " ".join(f"{int(diag[j - 1, 2 + k]) - prev if diag[j - 1, 2 + k] else -1:7d}" for k in range(3))  # rescored / winner ready / reserved
-        print(f"  pod {j - 1:2d}: {c - prev:7d} cyc nM={int(diag[j - 1, 1]):2d}  sub {sub}  filt {int(diag[j - 1, 5]) - prev if diag[j - 1, 5] else -1:7d}")
+        ls = " ".join(f"{int(lane[j - 1, k]) - prev if lane[j - 1, k] else -1:7d}" for k in range(5))
+        print(f"  pod {j - 1:2d}: {c - prev:7d} cyc nM={int(diag[j - 1, 1]):2d}  sub {sub}  filt "
+              f"{int(diag[j - 1, 5]) - prev if diag[j - 1, 5] else -1:7d}  lanes [e row loaded, rescored, reserve in, out] {ls}")
     prev = c
