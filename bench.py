@@ -225,12 +225,12 @@ def pmc_traffic(path, kernel, nodes, batch, ppw, depth):
         with open(path) as fh:
             d = json.load(fh)
     except (OSError, ValueError):
-        return None, None
+        return None, None, None
     m = d.get("_meta", {})
     if (m.get("nodes"), m.get("batch_pods"), m.get("pods_per_wave"), m.get("depth")) != (nodes, batch, ppw, depth) \
             or kernel not in d:
-        return None, None
-    return d[kernel]["traffic_bytes"], os.path.relpath(path, ROOT)
+        return None, None, None
+    return d[kernel]["traffic_bytes"], os.path.relpath(path, ROOT), d[kernel].get("rocprof_avg_ns")
 
 
 def main():
@@ -403,8 +403,8 @@ def main():
                                                    for r in ("r03", "r02")) if os.path.exists(f)),
                                       os.path.join(ROOT, "profiles", "r02", f"traffic_{wl}.json"))
     pmc_name = "eval_round_numa" if wl == "c4" else dom  # live timing folds every wide pass under "eval_round"
-    traffic, traffic_src = (pmc_traffic(tfile, pmc_name, cluster.n, args.batch, args.pods_per_wave, args.depth)
-                            if d.world == 1 else (None, None))
+    traffic, traffic_src, rocprof_ns = (pmc_traffic(tfile, pmc_name, cluster.n, args.batch, args.pods_per_wave,
+                                                    args.depth) if d.world == 1 else (None, None, None))
     if d.rank == 0:
         pods_s = total / elapsed
         desc = {
@@ -464,6 +464,10 @@ def main():
                          "per_evaluation_rate_gbs": per_eval,
                          "traffic_rate_gbs": traffic / (dom_ms * 1e-3) / 1e9 if traffic else None,
                          "traffic_frac": traffic / (dom_ms * 1e-3) / 1e9 / HBM_PEAK_GBS if traffic else None,
+                         # the same kernel's rocprof average (trace pass of the committed PMC command): live
+                         # events also hold the command processor's dispatch of each launch
+                         "rocprof_kernel_ms": rocprof_ns / 1e6 if rocprof_ns else None,
+                         "frac_rocprof": algo / (rocprof_ns * 1e-9) / 1e9 / HBM_PEAK_GBS if rocprof_ns else None,
                          "live_ms": {k: v["avg_ms"] for k, v in live.items()},
                          "live_launches": {k: v["launches"] for k, v in live.items()},
                          "isolated_ms": {k: v[0] for k, v in isolated.items()}},

@@ -47,10 +47,13 @@ def pmc(d: str, counter: str):
 def main():
     d = sys.argv[1]
     meta = json.loads(sys.argv[2]) if len(sys.argv) > 2 else None  # workload geometry, matched by bench.py
+    avg_ns = {}  # rocprof average duration per kernel, from the trace pass of the same command
     for f in glob.glob(os.path.join(d, "trace", "**", "*kernel_stats.csv"), recursive=True):
         print(f"-- kernel stats ({os.path.relpath(f, d)})")
         with open(f) as fh:
             rows = list(csv.DictReader(fh))
+        for r in rows:
+            avg_ns.setdefault(short(r["Name"]), float(r["AverageNs"]))
         for r in rows[:12]:
             print(f"  {short(r['Name']):16s} calls={r['Calls']:>8s} avg={float(r['AverageNs'])/1e3:9.2f} us "
                   f"total={float(r['TotalDurationNs'])/1e6:9.2f} ms  {float(r['Percentage']):6.2f}%")
@@ -63,6 +66,8 @@ def main():
         wb = write.get(k, (0.0, 0))[0] * 1024
         out[k] = {"fetch_bytes": fb, "write_bytes": wb, "traffic_bytes": fb + wb,
                   "launches": max(fetch.get(k, (0, 0))[1], write.get(k, (0, 0))[1])}
+        if k in avg_ns:
+            out[k]["rocprof_avg_ns"] = avg_ns[k]
         print(f"  {k:16s} fetch={fb/1e6:10.3f} MB write={wb/1e6:10.3f} MB launches={out[k]['launches']}")
     if meta:
         out["_meta"] = meta

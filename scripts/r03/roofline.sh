@@ -8,7 +8,7 @@ export TMPDIR=/tmp
 wl=${WL:-c3}
 OUT=gpurun_out/r03/roofline_$wl
 rm -rf $OUT; mkdir -p $OUT
-SHORT="--workload $wl --steps 1 --pods-per-step ${PODS:-8000} --warmup 0 --no-cpu-baseline --check 0 --profile-pods 0 --kernel-iters 2 --single-pod-calls 0 --no-pcie"
+SHORT="--workload $wl --steps 1 --pods-per-step ${PODS:-8000} --warmup 0 --no-cpu-baseline --check 0 --profile-pods ${PROFPODS:-8000} --kernel-iters 2 --single-pod-calls 0 --no-pcie"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python3 -u bench.py $SHORT > $OUT/trace.log 2>&1
 rc=$?; echo "trace rc=$rc"; [ $rc -eq 0 ] || { tail -5 $OUT/trace.log; exit $rc; }
 # heartbeat: a PMC pass serialises every dispatch and writes its CSV only at exit
