@@ -198,16 +198,25 @@ __global__ __launch_bounds__(kWave* kEvalWaves) void eval_round(DevTable T, cons
   HotRow rows[kNPT];
   uint32_t gidx[kNPT];
   bool rare = false;
+  {  // every column load of the tile's rows issued before any is used (a row past the shard reads the shard's last
+     // row and is masked invalid): one wait for the tile instead of a wait per conditional load
+    HotCols c[kNPT];
+    int64_t ii[kNPT];
 #pragma unroll
-  for (int j = 0; j < kNPT; ++j) {
-    const int64_t local = (int64_t)tile * kTile + j * kWave + lane;
-    gidx[j] = (uint32_t)(node_base + local);
-    if (local < n_local) {
-      rows[j] = load_hot<PF>(T, node_base + local, P);
+    for (int j = 0; j < kNPT; ++j) {
+      const int64_t local = (int64_t)tile * kTile + j * kWave + lane;
+      gidx[j] = (uint32_t)(node_base + local);
+      ii[j] = node_base + (local < n_local ? local : n_local - 1);
+      load_hot_cols<PF>(T, ii[j], c[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < kNPT; ++j) load_hot_la_alloc<PF>(T, ii[j], c[j]);
+#pragma unroll
+    for (int j = 0; j < kNPT; ++j) {
+      const int64_t local = (int64_t)tile * kTile + j * kWave + lane;
+      rows[j] = hot_from_cols<PF>(c[j], P);
+      if (local >= n_local) rows[j].flags = 0;  // not F_VALID → never feasible
       rare |= (rows[j].flags & F_RARE) != 0;
-    } else {
-      rows[j] = HotRow{};
-      rows[j].flags = 0;  // not F_VALID → never feasible
     }
   }
   KG_STAMP(0, 1);
@@ -1965,10 +1974,16 @@ __global__ void debug_fast_lrs(const int64_t* req, const int64_t* cap, int64_t* 
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const int64_t c = cap[i], fr = c - req[i];
-  // reciprocals exactly as sync_static computes the static columns (correctly rounded f64 division)
+  // the wide pass's in-kernel estimates (load_hot), and for memory also the correctly rounded column value the exact
+  // paths use: both must give the same quotient (-2 flags a disagreement)
   const double invd = c > 0 ? 100.0 / (double)c : 0.0;
-  out_cpu[i] = cpu_dom(c, fr) ? lrs_cpu((int32_t)fr, (int32_t)c, (float)invd) : -1;
-  out_mem[i] = mem_dom(c, fr) ? lrs_mem((double)fr, (double)c, invd) : -1;
+  out_cpu[i] = cpu_dom(c, fr) ? lrs_cpu((int32_t)fr, (int32_t)c, inv100_f32(c)) : -1;
+  if (mem_dom(c, fr)) {
+    const int32_t a = lrs_mem((double)fr, (double)c, inv100_f64(c)), b = lrs_mem((double)fr, (double)c, invd);
+    out_mem[i] = a == b ? a : -2;
+  } else {
+    out_mem[i] = -1;
+  }
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -507,14 +507,16 @@ __device__ __forceinline__ int32_t lrs_cpu(int32_t x, int32_t cap, float inv) {
   q += (int)(t + cap <= num);
   return q;
 }
-// memory (f64): x·inv has absolute error ≤ 100·2^-52 < 1/cap (cap < 2^45), so trunc() is exact unless the
-// quotient is an integer k and the estimate lands just below it: one exact f64 compare (q+1)·cap ≤ 100·x
-// (every value < 2^52) lifts it.
+// memory (f64): any reciprocal estimate with relative error ≪ 2^-40 puts x·inv within ±1 of the quotient (a value
+// ≤ 100); one exact f64 compare each way corrects it — q·cap, (q+1)·cap and 100·x are integers below 2^52.  The wide
+// pass feeds it inv100_f64 (v_rcp_f64 + one Newton step, no column read); the exact paths the correctly rounded
+// column value.
 __device__ __forceinline__ int32_t lrs_mem(double x, double cap, double inv) {
   const double xc = __builtin_fmax(x, 0.0);  // as lrs_cpu: x < 0 → 0
   int q = (int)(xc * inv);
-  const double t = __builtin_fma((double)q, cap, cap);
-  q += (int)(t <= xc * 100.0);
+  const double num = xc * 100.0, t = (double)q * cap;
+  q -= (int)(t > num);
+  q += (int)(t + cap <= num);
   return q;
 }
 
@@ -603,28 +605,74 @@ struct HotRow {
 // 100 / capacity for the cpu terms from v_rcp_f32 (≤ 2 ulp), computed where a tile's rows are hoisted so that the
 // wide pass does not read the f32 reciprocal columns: lrs_cpu needs only an estimate within ±1 of the quotient (its
 // 24-bit multiply-compare corrects it both ways; relative error ≤ 2^-22 on a value ≤ 100), and inside the domain the
-// capacity is < 2^24, so (float)c is exact.  The f64 memory reciprocals stay columns: lrs_mem's one-sided correction
-// needs them correctly rounded, and an in-kernel IEEE division per node cost the pass ~10 % (measured).
+// capacity is < 2^24, so (float)c is exact.  (r3) The memory reciprocals likewise (inv100_f64): lrs_mem corrects both
+// ways, so the f64 columns are read only by the exact paths.
 __device__ __forceinline__ float inv100_f32(int64_t c) {
   return c > 0 ? 100.0f * __builtin_amdgcn_rcpf((float)c) : 0.0f;
 }
+// 100 / capacity for the memory terms: v_rcp_f64 refined by one Newton step (relative error far below 2^-40, which is
+// all lrs_mem's two-way correction needs), so the wide pass does not read the f64 reciprocal columns either
+__device__ __forceinline__ double inv100_f64(int64_t c) {
+  if (c <= 0) return 0.0;
+  const double d = (double)c;
+  const double r0 = __builtin_amdgcn_rcp(d);
+  return 100.0 * __builtin_fma(r0, __builtin_fma(-d, r0, 1.0), r0);
+}
 
+// The columns of one hot row, loaded without branches (every load unconditional, or from a selected column), so that
+// a tile's rows are all in flight at once: the wide pass waits once for its rows instead of once per conditional load
+// (r3: the branchy loads compiled to ~3 waits per row, ~half of a wave's life parked on vmcnt).
+struct HotCols {
+  uint32_t fl;
+  int32_t np, ap;
+  int64_t ac, am, rc, rm, nc, nm, luc, lum, lpc, lpm, lac, lam;
+};
 template <int PF>
-__device__ __forceinline__ HotRow load_hot(const DevTable& T, int64_t i, const EvalParams& P) {
+__device__ __forceinline__ void load_hot_cols(const DevTable& T, int64_t i, HotCols& c) {
+  constexpr bool kLa = (PF & PF_LA_SCORE) != 0, kProd = (PF & PF_LA_PROD) != 0;
+  c.fl = T.flags[i];
+  c.ac = T.alloc_cpu[i];
+  c.am = T.alloc_mem[i];
+  c.rc = T.req_cpu[i];
+  c.rm = T.req_mem[i];
+  c.nc = T.nz_cpu[i];
+  c.nm = T.nz_mem[i];
+  c.np = T.num_pods[i];
+  c.ap = T.alloc_pods[i];
+  c.luc = kLa ? T.la_used_cpu[i] : 0;
+  c.lum = kLa ? T.la_used_mem[i] : 0;
+  c.lpc = kProd ? T.la_pused_cpu[i] : 0;
+  c.lpm = kProd ? T.la_pused_mem[i] : 0;
+}
+// EstimateNode capacity: the Fit column again (a cache hit) when F_LA_ALLOC_EQ, else the LoadAware column — one load
+// from a selected column, after the flags
+template <int PF>
+__device__ __forceinline__ void load_hot_la_alloc(const DevTable& T, int64_t i, HotCols& c) {
+  if constexpr ((PF & PF_LA_SCORE) != 0) {
+    const bool eq = (c.fl & F_LA_ALLOC_EQ) != 0;
+    const int64_t* cc = eq ? T.alloc_cpu : T.la_alloc_cpu;
+    const int64_t* cm = eq ? T.alloc_mem : T.la_alloc_mem;
+    c.lac = cc[i];
+    c.lam = cm[i];
+  } else {
+    c.lac = c.lam = 0;
+  }
+}
+template <int PF>
+__device__ __forceinline__ HotRow hot_from_cols(const HotCols& c, const EvalParams& P) {
   HotRow h;
-  const uint32_t fl = T.flags[i];
-  const int64_t ac = T.alloc_cpu[i], am = T.alloc_mem[i];
-  const int64_t fc = ac - T.req_cpu[i], fm = am - T.req_mem[i];
-  const int64_t fnc = ac - T.nz_cpu[i], fnm = am - T.nz_mem[i];
-  // LoadAware terms only for rows it scores; capacity from the Fit columns when EstimateNode == Allocatable
+  const uint32_t fl = c.fl;
+  const int64_t ac = c.ac, am = c.am;
+  const int64_t fc = ac - c.rc, fm = am - c.rm;
+  const int64_t fnc = ac - c.nc, fnm = am - c.nm;
+  // LoadAware terms only for rows it scores
   constexpr bool kLa = (PF & PF_LA_SCORE) != 0;
   const bool la_row = kLa && (fl & F_LA_SCORE) != 0, la_eq = (fl & F_LA_ALLOC_EQ) != 0;
-  const int64_t lac = !la_row ? 0 : la_eq ? ac : T.la_alloc_cpu[i];
-  const int64_t lam = !la_row ? 0 : la_eq ? am : T.la_alloc_mem[i];
-  const int64_t lfc = la_row ? lac - T.la_used_cpu[i] : 0, lfm = la_row ? lam - T.la_used_mem[i] : 0;
+  const int64_t lac = la_row ? c.lac : 0, lam = la_row ? c.lam : 0;
+  const int64_t lfc = la_row ? lac - c.luc : 0, lfm = la_row ? lam - c.lum : 0;
   constexpr bool kProd = (PF & PF_LA_PROD) != 0;
-  const int64_t lpc = kProd && la_row ? lac - T.la_pused_cpu[i] : 0, lpm = kProd && la_row ? lam - T.la_pused_mem[i] : 0;
-  const bool pods_ok = T.num_pods[i] + 1 <= T.alloc_pods[i];
+  const int64_t lpc = kProd && la_row ? lac - c.lpc : 0, lpm = kProd && la_row ? lam - c.lpm : 0;
+  const bool pods_ok = c.np + 1 <= c.ap;
   bool ok = true;
   if constexpr ((PF & PF_FIT_FILTER) != 0) ok &= (fc >= -kFreeCpuAbs) & (fc <= kFreeCpuAbs) & (fm > -kFreeMemAbs) & (fm < kFreeMemAbs);
   if constexpr ((PF & PF_FIT_SCORE) != 0) {
@@ -649,13 +697,20 @@ __device__ __forceinline__ HotRow load_hot(const DevTable& T, int64_t i, const E
   h.free_mem = (double)fm;
   h.fnz_mem = (double)fnm;
   h.alloc_mem = (double)am;
-  h.inv_mem = kFitS ? T.inv_mem[i] : 0.0;
+  h.inv_mem = kFitS ? inv100_f64(am) : 0.0;
   h.la_free_mem = (double)lfm;
   h.la_pfree_mem = (double)lpm;
   h.la_alloc_mem = (double)lam;
-  h.la_inv_mem = la_row ? T.inv_mem[T.cap + i] : 0.0;
+  h.la_inv_mem = !la_row ? 0.0 : (kFitS && la_eq) ? h.inv_mem : inv100_f64(lam);
   h.flags = (fl & ~(F_RARE | F_PODS_OK)) | ((fl & F_VALID) && pods_ok ? F_PODS_OK : 0u) | (ok ? 0u : F_RARE);
   return h;
+}
+template <int PF>
+__device__ __forceinline__ HotRow load_hot(const DevTable& T, int64_t i, const EvalParams& P) {
+  HotCols c;
+  load_hot_cols<PF>(T, i, c);
+  load_hot_la_alloc<PF>(T, i, c);
+  return hot_from_cols<PF>(c, P);
 }
 
 // eval_hot<PF>: eval_fast on a HotRow (caller guarantees !(flags & F_RARE)).  The pod's request/estimate

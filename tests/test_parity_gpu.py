@@ -115,7 +115,10 @@ def test_fast_lrs_exact(cap_hi, name):
     pairs, every exact-integer quotient boundary ±1, the capacity edge, and small capacities."""
     rng = np.random.default_rng(11 if name == "cpu" else 12)
     caps = np.concatenate([rng.integers(1, cap_hi, 30000), rng.integers(1, 4096, 5000),
-                           np.array([1, 2, 3, 7, 100, 1000, 96000, cap_hi - 1, cap_hi - 2, (cap_hi - 1) // 3])])
+                           np.array([1, 2, 3, 7, 100, 1000, 96000, cap_hi - 1, cap_hi - 2, (cap_hi - 1) // 3]),
+                           # node-sized memory capacities (GiB multiples, a few bytes off them)
+                           np.array([g << 30 for g in (1, 3, 16, 255, 256, 1024, 4095)] +
+                                    [(g << 30) + d for g in (7, 512) for d in (-1, 1, 4095)], dtype=np.int64)])
     caps = caps[caps < cap_hi]
     k = rng.integers(0, 101, len(caps))
     edge = caps - (caps * k + 99) // 100          # smallest requested with quotient ≥ 100 - k … boundaries
