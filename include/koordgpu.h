@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define KG_ABI_VERSION 9
+#define KG_ABI_VERSION 10
 
 /* ---- resource slots (fixed order) ------------------------------------------------------- */
 enum {
@@ -213,7 +213,9 @@ typedef struct kg_config {
   int64_t balanced_score;                      /* NodeResourcesBalancedAllocation at Score                       */
   int64_t weight_balanced;
   int64_t balanced_resources;                  /* bit r: resource r (cpu 0, memory 1) is in its Resources list   */
-  int64_t reserved[4];
+  int64_t image_score;                         /* (ABI 10) ImageLocality at Score (no NormalizeScore)            */
+  int64_t weight_image;
+  int64_t reserved[2];
 } kg_config;
 
 /* One node (snapshot index = position given by the caller). */
@@ -262,6 +264,8 @@ typedef struct kg_pod_metric {
 
 /* Node affinity terms a pod may carry (more: the pod stays on the Go path) */
 #define KG_MAX_AFF_TERMS 4
+/* Containers an ImageLocality pod may carry (more: the pod stays on the Go path) */
+#define KG_MAX_CONTAINERS 8
 
 /* One pod, pre-decoded by the caller (PodRequestsAndLimits semantics, pkg/util/pod_resources_utils.go:48-64). */
 typedef struct kg_pod {
@@ -297,6 +301,13 @@ typedef struct kg_pod {
    * pod off the cores (PCPULevel) / NUMA nodes (NUMANodeLevel) that hold cpus of pods with the same policy
    * (cpu_accumulator.go:247-330), and Reserve records the pod's cpus with it (node_allocation.go:68-90) */
   int64_t preferred_cpu_exclusive_policy;
+  /* (ABI 10) ImageLocality (k8s v1.24.15 imagelocality/image_locality.go, not vendored): the pod's containers
+   * (pod.Spec.Containers, len ≤ KG_MAX_CONTAINERS) — per container the bit of its normalized image name in the caller's
+   * image table (kg_node_predicates.images; -1: no node holds the image) and that image's scaledImageScore, which is
+   * node-independent: int64(float64(ImageStateSummary.Size) * float64(NumNodes) / float64(totalNumNodes)) */
+  int64_t n_containers;
+  int64_t container_image_bit[KG_MAX_CONTAINERS];
+  int64_t container_image_score[KG_MAX_CONTAINERS];
 } kg_pod;
 
 /* pod reservation flags */
@@ -391,6 +402,8 @@ typedef struct kg_node_predicates {
   uint64_t predicates;                         /* bit k: predicate k holds on the node                          */
   uint64_t taints_hard;                        /* the node's taints with effect NoSchedule or NoExecute         */
   uint64_t taints_soft;                        /* the node's taints with effect PreferNoSchedule                */
+  uint64_t images;                             /* (ABI 10) bit i: NodeInfo.ImageStates holds image i of the     */
+                                               /* caller's image table (the ≤ 64 images queued pods reference) */
 } kg_node_predicates;
 
 typedef struct kg_stats {

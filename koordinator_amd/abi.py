@@ -35,7 +35,7 @@ POD_REQUEST_KEYS, POD_CPU_KEY, POD_MEM_KEY = 8, 16, 32
 MAX_OWNER_GROUPS = 64
 QUOTA_RES = 8
 MAX_QUOTAS = 64
-ABI_VERSION = 9
+ABI_VERSION = 10
 MAX_RSV_SLOTS = 4
 RSV_POLICY = {"Default": 0, "Aligned": 1, "Restricted": 2}
 POD_RSV_AFFINITY = 1
@@ -57,6 +57,7 @@ REJECT_FIT_OTHER = 128  # NodeResourcesFit: ephemeral-storage / a scalar resourc
 # DeviceShare device resources (KG_DEV_*)
 DEV_RES_MAX, MAX_MINORS = 8, 8
 MAX_AFF_TERMS = 4  # KG_MAX_AFF_TERMS
+MAX_CONTAINERS = 8  # KG_MAX_CONTAINERS
 DEV_NVIDIA_GPU, DEV_HYGON_DCU, DEV_KOORD_GPU, DEV_GPU_CORE, DEV_GPU_MEMORY, DEV_GPU_MEMORY_RATIO, DEV_FPGA, DEV_RDMA = \
     range(8)
 DEVICE_RESOURCE_SLOTS = {
@@ -96,7 +97,8 @@ CONFIG_DTYPE = np.dtype([
     _i64("taint_filter"), _i64("taint_score"), _i64("weight_taint"),
     _i64("affinity_filter"), _i64("affinity_score"), _i64("weight_affinity"),
     _i64("balanced_score"), _i64("weight_balanced"), _i64("balanced_resources"),
-    _i64("reserved", 4),
+    _i64("image_score"), _i64("weight_image"),
+    _i64("reserved", 2),
 ])
 
 NODE_DTYPE = np.dtype([
@@ -137,8 +139,10 @@ POD_DTYPE = np.dtype([
     _i64("n_required_terms"), ("required_terms", np.uint64, (MAX_AFF_TERMS,)),
     _i64("n_preferred_terms"), ("preferred_terms", np.uint64, (MAX_AFF_TERMS,)), _i64("preferred_weights", MAX_AFF_TERMS),
     _i64("preferred_cpu_exclusive_policy"),
+    _i64("n_containers"), _i64("container_image_bit", MAX_CONTAINERS), _i64("container_image_score", MAX_CONTAINERS),
 ])
-NODE_PRED_DTYPE = np.dtype([("predicates", np.uint64), ("taints_hard", np.uint64), ("taints_soft", np.uint64)])
+NODE_PRED_DTYPE = np.dtype([("predicates", np.uint64), ("taints_hard", np.uint64), ("taints_soft", np.uint64),
+                            ("images", np.uint64)])
 
 NODE_RSV_DTYPE = np.dtype([_i64("n")] + [_i64(f, MAX_RSV_SLOTS) for f in (
     "owner", "allocatable_cpu", "allocatable_mem", "allocated_cpu", "allocated_mem", "assigned", "order", "policy",

@@ -8,6 +8,9 @@
 //   nodeaffinity/node_affinity.go         Filter: RequiredNodeAffinity.Match (nodeSelector AND any required term);
 //                                         Score: Σ weights of matching preferred terms,
 //                                         NormalizeScore = DefaultNormalizeScore(MaxNodeScore, reverse = false)
+//   imagelocality/image_locality.go       Score: calculatePriority(sumImageScores(node, pod.Spec.Containers), #containers)
+//                                         with minThreshold 23 MiB, maxThreshold 1000 MiB × #containers; no NormalizeScore.
+//                                         scaledImageScore is node-independent: the caller passes it per container.
 //   noderesources/balanced_allocation.go  Score (useRequested = true): fraction_r = float64(Requested_r + podRequest_r)
 //   + resource_allocation.go              / float64(Allocatable_r) capped at 1 over the configured resources with a
 //                                         non-zero Allocatable; std = |f_cpu − f_mem| / 2 for two of them, 0 for
@@ -24,22 +27,29 @@ namespace kg {
 
 constexpr int kAffTerms = KG_MAX_AFF_TERMS;
 
-struct NodePred {  // 24 B per node (kg_node_predicates)
-  uint64_t pred, hard, soft;
+struct NodePred {  // 32 B per node (kg_node_predicates)
+  uint64_t pred, hard, soft, images;
 };
 static_assert(sizeof(NodePred) == sizeof(kg_node_predicates), "NodePred layout");
 
-struct DefPod {  // 104 B per staged pod; the pass broadcasts one
+constexpr int kContainers = KG_MAX_CONTAINERS;
+struct DefPod {  // 184 B per staged pod; the pass broadcasts one
   uint64_t tol, sel;
   uint64_t req[kAffTerms], pref[kAffTerms];
   int32_t w[kAffTerms];
   int32_t nreq, npref;
+  // ImageLocality: the distinct image bits of the pod's containers with Σ scaledImageScore over the containers using
+  // each (a container's image counts once per container, sumImageScores), and len(pod.Spec.Containers)
+  int64_t img_w[kContainers];
+  uint8_t img_bit[kContainers];
+  int32_t nimg, ncont;
 };
 
 struct DefParams {
   int32_t taint_filter, taint_score, w_taint;
   int32_t aff_filter, aff_score, w_aff;
   int32_t bal, w_bal, bal_cpu, bal_mem;
+  int32_t img, w_img;
 };
 
 // nodeSelectorTerm.match: every requirement of the term holds; a term without requirements matches no node
@@ -91,6 +101,21 @@ __device__ __forceinline__ int64_t balanced_score(int64_t alloc_cpu, int64_t all
   }
   const double std = n == 2 ? fabs((f[0] - f[1]) / 2.0) : 0.0;
   return (int64_t)((1.0 - std) * 100.0);
+}
+
+// ImageLocality Score: calculatePriority(sumImageScores, numContainers) — Σ over the pod's containers whose image the
+// node holds of scaledImageScore, clamped to [minThreshold, maxThreshold], MaxNodeScore · (sum − min) / (max − min)
+// in int64 (Go truncation; both operands non-negative except with 0 containers, where the numerator is 0)
+constexpr int64_t kImgMB = 1024 * 1024, kImgMin = 23 * kImgMB, kImgMaxPerContainer = 1000 * kImgMB;
+__device__ __forceinline__ int64_t image_score(const NodePred& n, const DefPod& d) {
+  int64_t sum = 0;
+#pragma unroll
+  for (int k = 0; k < kContainers; ++k)
+    if (k < d.nimg && ((n.images >> d.img_bit[k]) & 1ull)) sum += d.img_w[k];
+  const int64_t mx = kImgMaxPerContainer * d.ncont;
+  sum = sum < kImgMin ? kImgMin : (sum > mx ? mx : sum);
+  const int64_t num = 100 * (sum - kImgMin), den = mx - kImgMin;
+  return num == 0 ? 0 : num / den;
 }
 
 // DefaultNormalizeScore (helper/normalize_score.go) of one node's raw score against the feasible nodes' maximum

@@ -2236,8 +2236,9 @@ int validate_config(const kg_config* c) {
       c->la_agg_score_type > KG_AGG_P99 || c->la_agg_usage_duration_ns < 0 || c->la_agg_score_duration_ns < 0)
     return fail(KG_E_INVALID, "LoadAwareSchedulingArgs.Aggregated: aggregation type / duration");
   if (c->weight_taint < 0 || c->weight_taint > 1000000 || c->weight_affinity < 0 || c->weight_affinity > 1000000 ||
-      c->weight_balanced < 0 || c->weight_balanced > 1000000)
-    return fail(KG_E_INVALID, "TaintToleration / NodeAffinity / NodeResourcesBalancedAllocation weight out of range");
+      c->weight_balanced < 0 || c->weight_balanced > 1000000 || c->weight_image < 0 || c->weight_image > 1000000)
+    return fail(KG_E_INVALID,
+                "TaintToleration / NodeAffinity / NodeResourcesBalancedAllocation / ImageLocality weight out of range");
   if (c->balanced_score && (c->balanced_resources & ~3ll))
     return fail(KG_E_UNSUPPORTED, "NodeResourcesBalancedAllocation resources: cpu / memory are accelerated");
   if (c->reservation_filter || c->reservation_score) {
@@ -2567,6 +2568,25 @@ int decode_def_pod(const kg_pod& p, DefPod& d, int64_t k) {
       return fail(KG_E_INVALID, "pod %lld: preferred term weight %lld outside [0, 100]", (long long)k,
                   (long long)p.preferred_weights[t]);
     d.w[t] = t < d.npref ? (int32_t)p.preferred_weights[t] : 0;
+  }
+  // ImageLocality: containers grouped by image bit (sumImageScores adds an image once per container using it)
+  if (p.n_containers < 0 || p.n_containers > kContainers)
+    return fail(KG_E_UNSUPPORTED, "pod %lld: more than %d containers for ImageLocality (the pod stays on the Go path)",
+                (long long)k, kContainers);
+  d.ncont = (int32_t)p.n_containers;
+  for (int c = 0; c < d.ncont; ++c) {
+    const int64_t b = p.container_image_bit[c], w = p.container_image_score[c];
+    if (b < -1 || b > 63 || w < 0)
+      return fail(KG_E_INVALID, "pod %lld: container %d image bit %lld / score %lld out of range", (long long)k, c,
+                  (long long)b, (long long)w);
+    if (b < 0) continue;  // no node holds the image
+    int at = 0;
+    while (at < d.nimg && d.img_bit[at] != (uint8_t)b) ++at;
+    if (at == d.nimg) {
+      d.img_bit[d.nimg] = (uint8_t)b;
+      d.img_w[d.nimg++] = 0;
+    }
+    d.img_w[at] += w;
   }
   return 0;
 }
@@ -3630,7 +3650,7 @@ static int engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank,
   e->numa_on = c.numa_filter || c.numa_score;
   e->ds_on = c.ds_filter || c.ds_score;
   e->rsv_on = c.reservation_filter || c.reservation_score;
-  e->def_on = c.taint_filter || c.taint_score || c.affinity_filter || c.affinity_score || c.balanced_score;
+  e->def_on = c.taint_filter || c.taint_score || c.affinity_filter || c.affinity_score || c.balanced_score || c.image_score;
   e->def_score = c.taint_score || c.affinity_score;
   e->exact_on = e->rsv_on || (e->numa_on && e->ds_on) || e->def_on;
   // Exact profiles (Reservation, NodeNUMAResource + DeviceShare, the upstream defaults) on several ranks run as
@@ -3640,7 +3660,8 @@ static int engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank,
   e->DF = DefParams{(int32_t)(c.taint_filter != 0), (int32_t)(c.taint_score != 0), (int32_t)c.weight_taint,
                     (int32_t)(c.affinity_filter != 0), (int32_t)(c.affinity_score != 0), (int32_t)c.weight_affinity,
                     (int32_t)(c.balanced_score != 0), (int32_t)c.weight_balanced,
-                    (int32_t)(c.balanced_resources & 1), (int32_t)((c.balanced_resources >> 1) & 1)};
+                    (int32_t)(c.balanced_resources & 1), (int32_t)((c.balanced_resources >> 1) & 1),
+                    (int32_t)(c.image_score != 0), (int32_t)c.weight_image};
   if (e->def_on) {
     if (int rc = e->npred.ensure(cap)) return bail(rc);
     if (hipMemset(e->npred.p, 0, cap * sizeof(NodePred)) != hipSuccess) return bail(fail(KG_E_DEVICE, "hipMemset"));
@@ -3689,7 +3710,7 @@ static int engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank,
                                    (c.numa_score ? c.weight_numa : 0) + (c.ds_score ? c.weight_deviceshare : 0) +
                                    (c.reservation_score ? c.weight_reservation : 0) +
                                    (c.taint_score ? c.weight_taint : 0) + (c.affinity_score ? c.weight_affinity : 0) +
-                                   (c.balanced_score ? c.weight_balanced : 0));
+                                   (c.balanced_score ? c.weight_balanced : 0) + (c.image_score ? c.weight_image : 0));
   e->P.score_bits = (int32_t)bits_for(max_total);
   // NodeResourcesFit + LoadAwareScheduling: assume only lowers a node's key; NodeNUMAResource does not
   e->P.monotone = (e->numa_on || e->ds_on || e->rsv_on) ? 0 : 1;  // DeviceShare: normalization couples every node's key

@@ -136,7 +136,7 @@ __device__ __forceinline__ RsvOut rsv_eval_node(const DevTable& T, const RsvNode
                                                 RsvDbg* dbg = nullptr, const int64_t* aux_req = nullptr,
                                                 const DefPod* df = nullptr) {
   RsvOut o{false, 0, 0, -1, 0x7fffffff, 0, 0, 0};
-  NodePred npd{0, 0, 0};
+  NodePred npd{0, 0, 0, 0};
   if (df) {  // TaintToleration / NodeAffinity Filter: node-static, so first
     npd = X.pred[i];
     if (!dbg && !defaults_filter(npd, *df, X.DF)) return o;
@@ -241,6 +241,7 @@ __device__ __forceinline__ RsvOut rsv_eval_node(const DevTable& T, const RsvNode
   }
   if (df) {  // BalancedAllocation on the restored NodeInfo; the two normalised raw Scores
     if (X.DF.bal) t += X.DF.w_bal * balanced_score(r.alloc_cpu, r.alloc_mem, r.req_cpu, r.req_mem, p.req_cpu, p.req_mem, X.DF);
+    if (X.DF.img) t += X.DF.w_img * image_score(npd, *df);
     o.tcnt = X.DF.taint_score ? taint_raw(npd, *df) : 0;
     o.asum = X.DF.aff_score ? affinity_raw(npd, *df) : 0;
   }

@@ -32,6 +32,7 @@ RESERVATION = "Reservation"
 # upstream default plugins a stock profile keeps (k8s v1.24.15 v1beta2 defaults: Score weight 1 each)
 TAINT_TOLERATION, NODE_AFFINITY = "TaintToleration", "NodeAffinity"
 BALANCED_ALLOCATION = "NodeResourcesBalancedAllocation"
+IMAGE_LOCALITY = "ImageLocality"
 
 
 def _slots(d: dict | None, absent=0) -> np.ndarray:
@@ -148,6 +149,8 @@ def build_config(la: LoadAwareSchedulingArgs | None = None, fit: NodeResourcesFi
     r["balanced_score"] = int(BALANCED_ALLOCATION in profile.score)
     r["weight_balanced"] = int(profile.score.get(BALANCED_ALLOCATION, 0))
     r["balanced_resources"] = sum({"cpu": 1, "memory": 2}.get(k, 1 << 8) for k in balanced_resources)
+    r["image_score"] = int(IMAGE_LOCALITY in profile.score)
+    r["weight_image"] = int(profile.score.get(IMAGE_LOCALITY, 0))
     r["ds_scoring_strategy"] = abi.STRATEGY[ds.scoring_strategy]
     r["ds_scoring_weights"] = [ds.scoring_resources.get("koordinator.sh/gpu-core", 0),
                                ds.scoring_resources.get("koordinator.sh/gpu-memory", 0),

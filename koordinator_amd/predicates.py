@@ -1,5 +1,6 @@
 """Host-side compiler of node labels / taints and pod tolerations / node affinity into the engine's bitmasks
-(kg_node_predicates and the kg_pod TaintToleration / NodeAffinity fields, ABI 8).
+(kg_node_predicates and the kg_pod TaintToleration / NodeAffinity fields, ABI 8), and of node images / pod
+containers into the ImageLocality fields (ABI 10, ImageTable).
 
 The Go shim keeps two dense tables per scheduler: the distinct taints (key, value, effect) of the cluster's nodes
 and the distinct node-selector predicates the queued pods use — a NodeSelectorRequirement (key, operator, values),
@@ -167,3 +168,66 @@ class PredicateTable:
             row["preferred_terms"][k] = self._term_mask(term)
             row["preferred_weights"][k] = w
         return pod
+
+
+def normalized_image_name(name: str) -> str:
+    """imagelocality normalizedImageName (v1.24.15): no tag after the last '/' → ':latest' appended."""
+    return name if name.rfind(":") > name.rfind("/") else name + ":latest"
+
+
+class ImageTable:
+    """The caller's ImageLocality view.  The scheduler cache keeps, per image name of any node's status, the size first
+    recorded and the set of nodes listing it (cache.addNodeImageStates); a node's ImageStates holds the names its own
+    status lists.  Bits go to the images the queued pods use and some node holds (at most 64); scaledImageScore =
+    int64(float64(size) * float64(numNodes) / float64(totalNumNodes)) is the same on every node, so it travels with
+    the pod and the device only tests node bits."""
+
+    def __init__(self, node_images: list):
+        """node_images[i]: node i's status images as [(names, size_bytes)], in snapshot order."""
+        self.total = len(node_images)
+        self.size: dict = {}
+        self.nodes: dict = {}
+        self.node_names = []
+        for i, imgs in enumerate(node_images):
+            names = set()
+            for img_names, size in imgs or ():
+                for nm in img_names:
+                    if nm not in self.size:
+                        self.size[nm] = int(size)
+                        self.nodes[nm] = set()
+                    self.nodes[nm].add(i)
+                    names.add(nm)
+            self.node_names.append(names)
+        self.bits: dict = {}
+
+    def scaled(self, name: str) -> int:
+        spread = float(len(self.nodes[name])) / float(self.total)
+        return int(float(self.size[name]) * spread)
+
+    def fill_pod(self, pod: np.ndarray, containers: list) -> np.ndarray:
+        """The pod's ImageLocality fields from its container images (in place; returns it)."""
+        row = pod[0] if pod.shape else pod
+        if len(containers) > abi.MAX_CONTAINERS:
+            raise OverflowError("more than 8 containers: the pod stays on the Go path")
+        row["n_containers"] = len(containers)
+        row["container_image_bit"][:] = -1
+        row["container_image_score"][:] = 0
+        for c, image in enumerate(containers):
+            nm = normalized_image_name(image)
+            if nm not in self.size:
+                continue  # no node lists it: never in an ImageStates map
+            if nm not in self.bits:
+                if len(self.bits) == MAX_IDS:
+                    raise OverflowError("more than 64 distinct pod images: the pods stay on the Go path")
+                self.bits[nm] = len(self.bits)
+            row["container_image_bit"][c] = self.bits[nm]
+            row["container_image_score"][c] = self.scaled(nm)
+        return pod
+
+    def node_mask(self, i: int) -> int:
+        """kg_node_predicates.images of node i over the bits assigned so far."""
+        m = 0
+        for nm, b in self.bits.items():
+            if nm in self.node_names[i]:
+                m |= 1 << b
+        return m

@@ -549,3 +549,33 @@ def make_predicates(n_nodes: int, pods: np.ndarray, seed: int = BASE_SEED + 15) 
         table.fill_pod(pods[j:j + 1], tolerations=tol, node_selector=sel, required_terms=req, preferred=pref)
     rows = np.concatenate([table.node_row(labels[i], taints[i], name=f"node-{i}") for i in range(n_nodes)])
     return table, rows
+
+
+def make_images(n_nodes: int, pods: np.ndarray, preds: np.ndarray, seed: int = BASE_SEED + 16):
+    """Node images and pod containers for ImageLocality (compiled through koordinator_amd.predicates.ImageTable):
+    a 40-image catalog (50 MiB - 2 GiB, some listed under two names), 5-15 images per node, 1-3 containers per pod
+    (untagged names resolve to ':latest'; 5 % name an image no node holds).  Fills `pods` and preds["images"] in
+    place; returns the table."""
+    from .predicates import ImageTable
+    rng = np.random.default_rng(seed)
+    mib = 1024 * 1024
+    catalog = []
+    for k in range(40):
+        names = [f"registry.local/app-{k}:v{k % 3}"] + ([f"registry.local/app-{k}:latest"] if k % 4 == 0 else [])
+        catalog.append((names, int(rng.integers(50, 2048)) * mib + int(rng.integers(0, mib))))
+    node_images = []
+    for _ in range(n_nodes):
+        pick = rng.choice(len(catalog), int(rng.integers(5, 16)), replace=False)
+        node_images.append([catalog[int(c)] for c in pick])
+    table = ImageTable(node_images)
+    for j in range(len(pods)):
+        cont = []
+        for _ in range(int(rng.integers(1, 4))):
+            if rng.random() < 0.05:
+                cont.append("registry.local/unknown:v9")
+            else:
+                k = int(rng.integers(40))
+                cont.append(f"registry.local/app-{k}" if k % 4 == 0 and rng.random() < 0.5 else catalog[k][0][0])
+        table.fill_pod(pods[j:j + 1], cont)
+    preds["images"] = [table.node_mask(i) for i in range(n_nodes)]
+    return table

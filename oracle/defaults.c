@@ -67,6 +67,22 @@ int64_t or_balanced_score(int64_t alloc_cpu, int64_t alloc_mem, int64_t req_cpu,
   return (int64_t)((1 - std) * (double)100);
 }
 
+/* imagelocality/image_locality.go (v1.24.15): sumImageScores over pod.Spec.Containers — a container whose normalized
+ * image the node holds adds its image's scaledImageScore (int64(float64(size) * spread), node-independent, computed
+ * by the caller) — then calculatePriority: clamp to [23 MiB, 1000 MiB × #containers],
+ * MaxNodeScore * (sum - minThreshold) / (maxThreshold - minThreshold) in int64. */
+int64_t or_image_score(const kg_node_predicates* n, const kg_pod* pod) {
+  const int64_t mb = 1024 * 1024, min_t = 23 * mb, max_t = 1000 * mb * pod->n_containers;
+  int64_t sum = 0;
+  for (int64_t c = 0; c < pod->n_containers; c++) {
+    const int64_t b = pod->container_image_bit[c];
+    if (b >= 0 && ((n->images >> b) & 1u)) sum += pod->container_image_score[c];
+  }
+  if (sum < min_t) sum = min_t;
+  else if (sum > max_t) sum = max_t;
+  return 100 * (sum - min_t) / (max_t - min_t);
+}
+
 /* helper/normalize_score.go DefaultNormalizeScore */
 int64_t or_normalize_default(int64_t score, int64_t max_count, int reverse) {
   if (max_count == 0) return reverse ? 100 : score;

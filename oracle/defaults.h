@@ -34,6 +34,7 @@ int or_affinity_filter(const kg_node_predicates* n, const kg_pod* pod);
 int64_t or_affinity_sum(const kg_node_predicates* n, const kg_pod* pod);
 /* BalancedAllocation Score (useRequested = true) from Allocatable, Requested and the pod's request of cpu / memory;
  * `resources` bit 0 = cpu, bit 1 = memory listed. */
+int64_t or_image_score(const kg_node_predicates* n, const kg_pod* pod);
 int64_t or_balanced_score(int64_t alloc_cpu, int64_t alloc_mem, int64_t req_cpu, int64_t req_mem, int64_t pod_cpu,
                           int64_t pod_mem, int64_t resources);
 /* DefaultNormalizeScore(MaxNodeScore, reverse) of one score against the maximum over the scored nodes. */

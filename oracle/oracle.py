@@ -105,7 +105,7 @@ def lib():
         L.or_rsv_case_flat.argtypes = [vp, i64, vp, i64, vp, vp, i, vp, vp]
         L.or_rsv_case_flat.restype = None
         for f, res in (("or_taint_filter", i), ("or_taint_count", i64), ("or_affinity_filter", i),
-                       ("or_affinity_sum", i64)):
+                       ("or_affinity_sum", i64), ("or_image_score", i64)):
             getattr(L, f).argtypes = [vp, vp]
             getattr(L, f).restype = res
         L.or_balanced_score.argtypes = [i64] * 7
@@ -468,7 +468,7 @@ def default_plugins(pred, pod) -> dict:
     L = lib()
     return {"taint_filter": bool(L.or_taint_filter(p(n), p(q))), "taint_count": int(L.or_taint_count(p(n), p(q))),
             "affinity_filter": bool(L.or_affinity_filter(p(n), p(q))),
-            "affinity_sum": int(L.or_affinity_sum(p(n), p(q)))}
+            "affinity_sum": int(L.or_affinity_sum(p(n), p(q))), "image_score": int(L.or_image_score(p(n), p(q)))}
 
 
 def balanced_score(alloc_cpu, alloc_mem, req_cpu, req_mem, pod_cpu, pod_mem, resources=3) -> int:

@@ -332,6 +332,7 @@ int or_schedule_resv_full(const kg_config* cfg, int64_t n_nodes, const kg_node* 
                                                       rs.requested[KG_RES_CPU], rs.requested[KG_RES_MEMORY],
                                                       pod->requests[KG_RES_CPU], pod->requests[KG_RES_MEMORY],
                                                       cfg->balanced_resources);
+      if (cfg->image_score) t += cfg->weight_image * or_image_score(np, pod);
       tcnt[i] = cfg->taint_score ? or_taint_count(np, pod) : 0;
       asum[i] = cfg->affinity_score ? or_affinity_sum(np, pod) : 0;
       base[i] = t;

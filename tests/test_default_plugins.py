@@ -322,3 +322,94 @@ def test_shipped_profile_with_stock_defaults():
     assert np.array_equal(node, want[0]) and np.array_equal(score, want[1])
     assert np.array_equal(slot, want[2]) and np.array_equal(minors, want[3]) and np.array_equal(cpus, want[4])
     assert (node >= 0).mean() > 0.4
+
+
+# ---- ImageLocality (ABI 10): image_locality.go restated; cases hand-derived from the published v1.24 formula ----
+MIB = 1024 * 1024
+
+
+def _go_image_priority(sum_scores, n_containers):
+    """calculatePriority with Go int64 semantics (operands non-negative here, so // is Go's truncation)."""
+    lo, hi = 23 * MIB, 1000 * MIB * n_containers
+    s = lo if sum_scores < lo else (hi if sum_scores > hi else sum_scores)
+    return 100 * (s - lo) // (hi - lo) if hi != lo else 0
+
+
+def test_normalized_image_name():
+    from koordinator_amd.predicates import normalized_image_name as nn
+    assert nn("nginx") == "nginx:latest"
+    assert nn("nginx:1.2") == "nginx:1.2"
+    assert nn("host:5000/nginx") == "host:5000/nginx:latest"  # a registry port is not a tag
+    assert nn("host:5000/nginx:1.2") == "host:5000/nginx:1.2"
+
+
+@pytest.mark.parametrize("node_images,containers,want", [
+    # one container, its 300 MiB image on one of two nodes: spread 0.5 → 150 MiB → 100·127/977 = 12 on node 0
+    ([[(["img/a:v1"], 300 * MIB)], []], ["img/a:v1"], [12, 0]),
+    # below minThreshold (23 MiB) scores 0 even where the image is present
+    ([[(["img/a:v1"], 40 * MIB)], []], ["img/a:v1"], [0, 0]),
+    # a 2 GiB image on both nodes: clamped to maxThreshold → 100
+    ([[(["img/b:v1"], 2048 * MIB)], [(["img/b:v1"], 2048 * MIB)]], ["img/b:v1"], [100, 100]),
+    # two containers: maxThreshold doubles; the same image twice counts twice
+    ([[(["img/b:v1"], 1000 * MIB)], [(["img/b:v1"], 1000 * MIB)]], ["img/b:v1", "img/b:v1"], [100, 100]),
+    ([[(["img/b:v1"], 1000 * MIB)], [(["img/c:v1"], 500 * MIB)]], ["img/b:v1", "img/c:v1"],
+     [_go_image_priority(500 * MIB, 2), _go_image_priority(250 * MIB, 2)]),
+    # an untagged container image resolves to ':latest', which a node lists under a second name
+    ([[(["img/d:v2", "img/d:latest"], 600 * MIB)], []], ["img/d"], [_go_image_priority(300 * MIB, 1), 0]),
+    # no node holds the image
+    ([[(["img/a:v1"], 300 * MIB)], []], ["img/zzz:v1"], [0, 0]),
+])
+def test_image_locality_cases(node_images, containers, want):
+    from koordinator_amd.predicates import ImageTable
+    t = ImageTable(node_images)
+    pod = t.fill_pod(_pod(), containers)
+    rows = np.zeros(len(node_images), dtype=abi.NODE_PRED_DTYPE)
+    rows["images"] = [t.node_mask(i) for i in range(len(node_images))]
+    got = [oracle.default_plugins(rows[i], pod)["image_score"] for i in range(len(node_images))]
+    assert got == want
+
+
+def test_image_locality_random_vs_python():
+    """The oracle's restatement against an independent Python one over the synthetic image world."""
+    cluster = synth.make_cluster(300, seed=71)
+    pods = synth.make_pods(400, seed=72)
+    preds = np.zeros(cluster.n, dtype=abi.NODE_PRED_DTYPE)
+    table = synth.make_images(cluster.n, pods, preds, seed=73)
+    for j in range(0, len(pods), 7):
+        for i in range(0, cluster.n, 11):
+            s = 0
+            for c in range(int(pods[j]["n_containers"])):
+                b = int(pods[j]["container_image_bit"][c])
+                if b >= 0 and (int(preds[i]["images"]) >> b) & 1:
+                    s += int(pods[j]["container_image_score"][c])
+            want = _go_image_priority(s, int(pods[j]["n_containers"]))
+            assert oracle.default_plugins(preds[i], pods[j])["image_score"] == want
+    assert len(table.bits) > 20
+
+
+IMAGE_PROFILE = F.Profile(filter=STOCK.filter, score=dict(STOCK.score, **{F.IMAGE_LOCALITY: 1}))
+
+
+def test_oracle_image_locality_moves_placements():
+    cluster, pods, preds = _world(400, 600, 81)
+    synth.make_images(cluster.n, pods, preds, seed=82)
+    n0, _, _ = _oracle(F.build_config(profile=STOCK), cluster, pods, preds)
+    n1, _, _ = _oracle(F.build_config(profile=IMAGE_PROFILE), cluster, pods, preds)
+    assert (n0 != n1).mean() > 0.1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", ["stock_plus_image", "image_only"])
+def test_device_image_locality_matches_oracle(variant):
+    prof = IMAGE_PROFILE if variant == "stock_plus_image" else F.Profile(
+        filter=(F.NODE_RESOURCES_FIT,), score={F.NODE_RESOURCES_FIT: 1, F.IMAGE_LOCALITY: 2})
+    cfg = F.build_config(profile=prof)
+    cluster, pods, preds = _world(2500, 900, 91)
+    synth.make_images(cluster.n, pods, preds, seed=92)
+    want, want_score, _ = _oracle(cfg, cluster, pods, preds)
+    with Engine(cfg, cluster.n) as e:
+        synth.load_into(e, cluster)
+        e.upsert_predicates(preds)
+        node, score = e.schedule(pods)[:2]
+    assert np.array_equal(node, want) and np.array_equal(score, want_score)
+    assert (node >= 0).mean() > 0.5
