@@ -607,6 +607,12 @@ int kg_debug_eval_paths(kg_engine* e, int64_t* mismatches);
  * hint-merge counters (merges, all-permutation fallback passes), uint64[2]: 258 + 384 words in all. */
 int kg_debug_stamps(kg_engine* e, uint64_t* out);
 
+/* Debug: the RCCL calls a multi-rank engine makes (ncclGetUniqueId, ncclCommInitRank, ncclCommSplit, ncclAllGather on
+ * a HIP stream), on a one-rank communicator of device `device_id`, gathering n uint64 words: 0 when the gathered
+ * words equal the sent ones.  A one-GPU box cannot run two RCCL ranks; this checks the library path the driver's
+ * multi-GPU run takes. */
+int kg_debug_rccl_selftest(int device_id, int64_t n);
+
 const char* kg_last_error(void);
 int kg_abi_version(void);
 /* sizeof of the ABI structs (0 kg_config, 1 kg_node, 2 kg_node_metric, 3 kg_pod, 4 kg_stats, 5 kg_node_numa,

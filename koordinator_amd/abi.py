@@ -180,7 +180,8 @@ EXPORTED_SYMBOLS = (
     "kg_node_metrics_update", "kg_pods_add", "kg_pods_remove", "kg_pods_schedule", "kg_pods_evaluate",
     "kg_pods_stage", "kg_pods_schedule_staged", "kg_results_fetch", "kg_engine_num_nodes",
     "kg_nodes_read_state", "kg_bench_kernel", "kg_debug_least_requested", "kg_last_error", "kg_abi_version",
-    "kg_abi_struct_size", "kg_nccl_unique_id", "kg_debug_eval_paths", "kg_debug_stamps", "kg_debug_fast_lrs",
+    "kg_abi_struct_size", "kg_nccl_unique_id", "kg_debug_rccl_selftest", "kg_debug_eval_paths", "kg_debug_stamps",
+    "kg_debug_fast_lrs",
     "kg_nodes_numa_upsert", "kg_nodes_read_numa", "kg_results_fetch_cpusets", "kg_pods_evaluate_numa",
     "kg_nodes_device_upsert", "kg_nodes_read_device", "kg_results_fetch_devices", "kg_pods_evaluate_device",
     "kg_quotas_set", "kg_quotas_read", "kg_nodes_reservation_upsert", "kg_nodes_read_reservations",
@@ -240,6 +241,7 @@ def load_library(path: str | None = None):
         "kg_abi_version": (i, []),
         "kg_abi_struct_size": (i64, [i]),
         "kg_nccl_unique_id": (i, [vp]),
+        "kg_debug_rccl_selftest": (i, [i, i64]),
         "kg_debug_eval_paths": (i, [vp, vp]),
         "kg_debug_stamps": (i, [vp, vp]),
         "kg_debug_fast_lrs": (i, [vp, vp, vp, vp, vp, i64]),

@@ -3550,6 +3550,38 @@ void kg_config_default(kg_config* c) {
   c->device_id = -1;
 }
 
+int kg_debug_rccl_selftest(int device_id, int64_t n) {
+  if (n < 1 || n > (1 << 24)) return fail(KG_E_INVALID, "n in [1, 2^24]");
+  HIP_TRY(hipSetDevice(device_id));
+  ncclUniqueId id;
+  NCCL_TRY(ncclGetUniqueId(&id));
+  ncclComm_t c = nullptr, c2 = nullptr;
+  if (ncclCommInitRank(&c, 1, id, 0) != ncclSuccess) return fail(KG_E_COLLECTIVE, "ncclCommInitRank");
+  int rc = 0;
+  hipStream_t st = nullptr;
+  uint64_t *in = nullptr, *out = nullptr;
+  std::vector<uint64_t> h(n), g(n);
+  for (int64_t i = 0; i < n; ++i) h[i] = 0x9E3779B97F4A7C15ull * (uint64_t)(i + 1);
+  if (ncclCommSplit(c, 0, 0, &c2, nullptr) != ncclSuccess) rc = fail(KG_E_COLLECTIVE, "ncclCommSplit");
+  if (!rc && (hipStreamCreate(&st) != hipSuccess || hipMalloc(&in, n * 8) != hipSuccess ||
+              hipMalloc(&out, n * 8) != hipSuccess))
+    rc = fail(KG_E_DEVICE, "stream / buffers");
+  if (!rc && (hipMemcpy(in, h.data(), n * 8, hipMemcpyHostToDevice) != hipSuccess ||
+              hipMemset(out, 0, n * 8) != hipSuccess))
+    rc = fail(KG_E_DEVICE, "upload");
+  if (!rc && ncclAllGather(in, out, (size_t)n, ncclUint64, c2, st) != ncclSuccess)
+    rc = fail(KG_E_COLLECTIVE, "ncclAllGather");
+  if (!rc && (hipStreamSynchronize(st) != hipSuccess || hipMemcpy(g.data(), out, n * 8, hipMemcpyDeviceToHost) != hipSuccess))
+    rc = fail(KG_E_DEVICE, "download");
+  if (!rc && g != h) rc = fail(KG_E_COLLECTIVE, "ncclAllGather returned different words");
+  if (out) (void)hipFree(out);
+  if (in) (void)hipFree(in);
+  if (st) (void)hipStreamDestroy(st);
+  if (c2) ncclCommDestroy(c2);
+  ncclCommDestroy(c);
+  return rc;
+}
+
 int kg_nccl_unique_id(void* out128) {
   if (!out128) return fail(KG_E_INVALID, "out is NULL");
   ncclUniqueId id;
