@@ -129,6 +129,7 @@ struct RsvDbg {
   int64_t pod_req_cpu, pod_req_mem;                    // nodeReservationState.podRequested
 };
 
+template <bool kSlotsInRegs = true>  // false: the slot record is read where used (the wide exact pass, register-bound)
 __device__ __forceinline__ RsvOut rsv_eval_node(const DevTable& T, const RsvNode* __restrict__ RN,
                                                 const int32_t* __restrict__ rsv_n, int64_t i, const DevPod& p,
                                                 const RsvPod& rp, const EvalParams& P, const RsvParams& RP,
@@ -147,9 +148,13 @@ __device__ __forceinline__ RsvOut rsv_eval_node(const DevTable& T, const RsvNode
   int nm = 0;
   int64_t pr_c = 0, pr_m = 0, ra_c = 0, ra_m = 0;
   bool has_state = false;
-  RsvNode rn;
+  // xr_eval reads the slot record where used instead of copying it: a 192-B copy live across the Fit / NUMA /
+  // DeviceShare evaluation cost that pass a wave per SIMD (shipped profile: 256 VGPRs + AGPR spills → 239, occupancy
+  // 1 → 2); the single-wave resolvers keep the copy (one batch of loads on their serial path)
+  RsvNode rn_copy;
+  if (kSlotsInRegs && ns > 0) rn_copy = RN[i];
+  const RsvNode& rn = kSlotsInRegs ? rn_copy : RN[i];
   if (ns > 0) {
-    rn = RN[i];
     uint32_t um = 0;
 #pragma unroll
     for (int s = 0; s < kRsvSlots; ++s) {

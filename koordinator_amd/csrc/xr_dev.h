@@ -90,7 +90,7 @@ __global__ __launch_bounds__(kTile) void xr_eval(DevTable T, const RsvNode* __re
       const DefPod* df = (XF & XF_DEF) ? &X.defp[j] : nullptr;
       RsvExt Xk = X;
       Xk.aff = X.aff ? affk + (size_t)k * stride : nullptr;  // rsv_eval_node stores the NUMA affinity per node
-      const RsvOut o = rsv_eval_node(T, RN, rsv_n, i, p, rp, P, RP, Xk, dp, np, nullptr, aux, df);
+      const RsvOut o = rsv_eval_node<false>(T, RN, rsv_n, i, p, rp, P, RP, Xk, dp, np, nullptr, aux, df);
       uint64_t v = 0;
       uint32_t v2 = 0;
       if (o.feas) {
