@@ -355,13 +355,19 @@ def main():
     B = 1 if rsv_path else args.batch
     if wl == "c5ds":  # ds_max_round also reads the 272-B GPU row and writes a 4-B packed value per (pod, node)
         algo = n_local * (B_NODE + 272.0) + B * n_local * 4.0 + B * nt * 8.0
-    elif rsv_path:  # rsv_eval, one pod per pass: node columns + rsv_n + packed value per node, the 192-B slot rows of
-        # nodes holding reservations, and the 272-B GPU row per node for the device pods among the profiled ones
+    elif rsv_path:  # the exact wide pass (xr_eval, live time folded under "rsv_eval"): one launch scores the round's
+        # pods (kXrPods = 32, or fewer) against every node.  Per launch: the node columns + rsv_n once, the 192-B slot
+        # rows of nodes holding reservations, the 272-B GPU row per node when the round has device pods, the NUMA rows
+        # (NumaStatic 144 B + NodeAllocation 104 B), and per (pod, node) the 8-B packed value (+ 4-B NUMA affinity)
+        ev = live.get("rsv_eval", {})
+        pods_per_launch = (n_prof / ev["launches"]) if ev.get("launches") else 1.0
         prof_pods = pods[total:total + n_prof] if n_prof > 0 else pods[:1]
-        frac_dev = float(prof_pods["device_requests"].any(axis=1).mean()) if work.devices is not None else 0.0
-        algo = n_local * (B_NODE + 4 + 8) + int((work.rsv["n"] > 0).sum()) * 192.0 + frac_dev * n_local * 272.0
-        if work.numa is not None:  # NumaStatic (144 B) + NodeAllocation (104 B) rows and the stored affinity (4 B)
-            algo += n_local * (144.0 + 104.0 + 4.0)
+        has_dev = work.devices is not None and bool(prof_pods["device_requests"].any())
+        algo = n_local * (B_NODE + 4) + int((work.rsv["n"] > 0).sum()) * 192.0 + (n_local * 272.0 if has_dev else 0.0)
+        algo += pods_per_launch * n_local * 8.0
+        if work.numa is not None:
+            algo += n_local * (144.0 + 104.0) + pods_per_launch * n_local * 4.0
+        B = pods_per_launch
     else:
         algo = n_local * B_NODE + B * nt * 8 * 8.0 + B * 96.0
     dom_ms = live.get(dom, {}).get("avg_ms") or isolated[dom][0]
@@ -402,7 +408,8 @@ def main():
     tfile = args.traffic_file or next((f for f in (os.path.join(ROOT, "profiles", r, f"traffic_{wl}.json")
                                                    for r in ("r03", "r02")) if os.path.exists(f)),
                                       os.path.join(ROOT, "profiles", "r02", f"traffic_{wl}.json"))
-    pmc_name = "eval_round_numa" if wl == "c4" else dom  # live timing folds every wide pass under "eval_round"
+    # live timing folds every wide pass under one name: the kernel rocprof sees
+    pmc_name = {"c4": "eval_round_numa", "c5": "xr_eval", "c5r": "xr_eval", "shipped": "xr_eval"}.get(wl, dom)
     traffic, traffic_src, rocprof_ns = (pmc_traffic(tfile, pmc_name, cluster.n, args.batch, args.pods_per_wave,
                                                     args.depth) if d.world == 1 else (None, None, None))
     if d.rank == 0:
@@ -450,7 +457,7 @@ def main():
             "vs_baseline": None,
             "dtype": "int64",
             "data": "synthetic (SURVEY §8d generator, seed %d)" % work.seed,
-            "config": {"workload": desc, "nodes": cluster.n, "pods": total, "batch_pods": B,
+            "config": {"workload": desc, "nodes": cluster.n, "pods": total, "batch_pods": args.batch,
                        "pods_per_wave": args.pods_per_wave, "pipeline_depth": args.depth or "default",
                        "parallelism": "node-sharded x%d (replicated table, RCCL all-gather)" % d.world},
             "node_evals_per_sec": pods_s * cluster.n,
@@ -461,7 +468,7 @@ def main():
                          "kernel_ms": dom_ms, "algo_bytes_per_launch": algo,
                          "timing": "live HIP events around every launch of %d extra queued pods (kg_profile_enable)"
                                    % n_prof if dom in live else "isolated replay (kg_bench_kernel)",
-                         "per_evaluation_rate_gbs": per_eval,
+                         "per_evaluation_rate_gbs": per_eval, "pods_per_launch": B,
                          "traffic_rate_gbs": traffic / (dom_ms * 1e-3) / 1e9 if traffic else None,
                          "traffic_frac": traffic / (dom_ms * 1e-3) / 1e9 / HBM_PEAK_GBS if traffic else None,
                          # the same kernel's rocprof average (trace pass of the committed PMC command): live

@@ -127,6 +127,10 @@ __device__ __forceinline__ bool ds_eval(const DsNode& d, const DsPod& p, const D
     Fc += fc;
     Fr += fr;
     Fm += fm;
+    // half the minors consumed before the other half is loaded (the accumulators pass through an opaque asm with a
+    // memory clobber): xr_eval<DeviceShare> 214 → 164 VGPRs, a third wave per SIMD
+    if (m == kMinors / 2 - 1)
+      asm volatile("" : "+v"(Tc), "+v"(Tr), "+v"(Tm), "+v"(Fc), "+v"(Fr), "+v"(Fm), "+v"(nfit) : : "memory");
   }
   if (!any || nfit < in.count) return false;
   int64_t num = 0, ws = 0;

@@ -19,7 +19,7 @@ from collections import defaultdict
 
 
 def short(name: str) -> str:
-    for k in ("ds_max_round", "ds_norm_reduce", "eval_round_numa", "eval_round_ds", "resolve_round_numa",
+    for k in ("xr_eval", "xr_norm", "xr_select", "xr_resolve", "ds_max_round", "ds_norm_reduce", "eval_round_numa", "eval_round_ds", "resolve_round_numa",
               "resolve_round_ds", "eval_round", "merge_round", "resolve_round", "rsv_eval", "rsv_select", "rsv_apply",
               "evaluate_pod", "apply_deltas"):
         if k in name:

@@ -17,7 +17,7 @@ run() {  # name timeout cmd...
 [ -n "$NOTESTS" ] || run tests 900 python -u -m pytest tests -q -m gpu --timeout 300 --timeout-method thread
 run smoke 300 python3 -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')"
 run bench_c3 400 python3 -u bench.py
-for w in ${BENCHES:-c2 c1 c5 shipped c4}; do
+for w in ${BENCHES:-c2 c1 c5 c5r shipped c4}; do
   run bench_$w 400 python3 -u bench.py --workload $w --steps 5 --cpu-seconds 4 --single-pod-calls 20
 done
 [ -n "$NOROOF" ] || WL=c3 bash scripts/r03/roofline.sh
