@@ -242,7 +242,7 @@ int or_schedule_resv_full(const kg_config* cfg, int64_t n_nodes, const kg_node* 
     return KG_E_NOMEM;
   }
   /* TaintToleration / NodeAffinity / BalancedAllocation (defaults.c); a NULL table = no predicates, no taints */
-  const kg_node_predicates zero_pred = {0, 0, 0};
+  const kg_node_predicates zero_pred = {0, 0, 0, 0};
   const int rsv_on = cfg->reservation_filter || cfg->reservation_score;
   const int ds_on = dev && (cfg->ds_filter || cfg->ds_score);
   if (n_threads < 1) n_threads = 1;
