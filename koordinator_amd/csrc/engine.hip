@@ -1212,7 +1212,18 @@ __global__ __launch_bounds__(kWave) void resolve_round_numa(DevTable T, NumaTabl
       NumaAlloc rec;
       const NumaStatic ns = s_ns[owner];
       NumaMut nm = s_nm[owner];
-      const NumaView ov = make_view(&ns, &nm, NP);
+      // the owner lane's view of its row is current (built when the row entered its slot, rebuilt after each of its
+      // Reserves): read it across lanes instead of rebuilding it (a view build is ~5 k cycles)
+      NumaView ov;
+      {
+        constexpr int kVw = (int)(sizeof(NumaView) / 4);
+        static_assert(sizeof(NumaView) % 4 == 0, "NumaView in dwords");
+        uint32_t vw[kVw];
+        __builtin_memcpy(vw, &mv, sizeof(mv));
+#pragma unroll
+        for (int q = 0; q < kVw; ++q) vw[q] = (uint32_t)__builtin_amdgcn_readlane((int)vw[q], owner);
+        __builtin_memcpy(&ov, vw, sizeof(ov));
+      }
       if (lane == 0) KG_LANE_SUB(j, 3);
       placed = numa_reserve(ns, nm, ov, np, aff, cpus, rec) ? 1 : 0;
       if (lane == 0) KG_LANE_SUB(j, 4);
