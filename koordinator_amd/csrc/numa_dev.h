@@ -609,18 +609,54 @@ __device__ __forceinline__ NumaView make_view(const NumaStatic* __restrict__ s, 
   v.tot[0] = cs_count(avail);
   v.tot[1] = cs_count(full);
   v.tot[2] = cs_count(spread);
+  int32_t acnt[kNumaMax];  // allocated cpus per NUMA node
+  const int pn = t.per_node();
+  if (pn > 0 && (pn & 63) == 0) {
+    // NUMA nodes of whole 64-cpu words (e.g. 64 / 128 cpus per node): per-word popcounts summed per node, instead of
+    // building each node's range mask (a view is rebuilt per pod on the resolvers' serial path)
+    const int wpn = pn >> 6;
+    int32_t pa[kCpuWords], pf[kCpuWords], ps[kCpuWords], pl[kCpuWords];
+#pragma unroll
+    for (int w = 0; w < kCpuWords; ++w) {
+      pa[w] = __popcll(avail.w[w]);
+      pf[w] = __popcll(full.w[w]);
+      ps[w] = __popcll(spread.w[w]);
+      pl[w] = __popcll(alloc.w[w]);
+    }
+#pragma unroll
+    for (int i = 0; i < kNumaMax; ++i) {
+      int32_t c0 = 0, c1 = 0, c2 = 0, cl = 0;
+#pragma unroll
+      for (int w = 0; w < kCpuWords; ++w) {
+        const bool in = w >= i * wpn && w < (i + 1) * wpn;
+        c0 += in ? pa[w] : 0;
+        c1 += in ? pf[w] : 0;
+        c2 += in ? ps[w] : 0;
+        cl += in ? pl[w] : 0;
+      }
+      v.cnt[0][i] = c0;
+      v.cnt[1][i] = c1;
+      v.cnt[2][i] = c2;
+      acnt[i] = cl;
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < kNumaMax; ++i) {
+      const CpuSet nc = t.node_cpus(i);
+      v.cnt[0][i] = cs_count(cs_and(avail, nc));
+      v.cnt[1][i] = cs_count(cs_and(full, nc));
+      v.cnt[2][i] = cs_count(cs_and(spread, nc));
+      acnt[i] = cs_count(cs_and(alloc, nc));
+    }
+  }
 #pragma unroll
   for (int i = 0; i < kNumaMax; ++i) {
-    const CpuSet nc = t.node_cpus(i);
-    v.cnt[0][i] = cs_count(cs_and(avail, nc));
-    v.cnt[1][i] = cs_count(cs_and(full, nc));
-    v.cnt[2][i] = cs_count(cs_and(spread, nc));
     v.numa_cpu[i] = s->numa_cpu[i];
     v.numa_mem[i] = s->numa_mem[i];
     // getAvailableNUMANodeResources (node_allocation.go:155-177): with a cpu ratio > 1 the cpuset part of an
     // allocatedResources entry (allocated cpus on NUMA node i × 1000) counts amplified
     const bool present = (m->present >> i) & 1u;
-    const int64_t sets = (int64_t)cs_count(cs_and(alloc, nc)) * 1000;
+    const int64_t sets = (int64_t)acnt[i] * 1000;
     v.alloc_cpu[i] = present ? m->alloc_cpu[i] - sets + amplify(sets, v.amp) : 0;
     v.alloc_mem[i] = present ? m->alloc_mem[i] : 0;
   }
