@@ -2001,6 +2001,13 @@ __global__ void debug_fast_lrs(const int64_t* req, const int64_t* cap, int64_t* 
 // Host side
 // ------------------------------------------------------------------------------------------------
 
+// KG_DEBUG_POISON=1 (debug runs only): every fresh device buffer is filled with 0xA5 bytes before use, so a read of
+// memory the engine never wrote shows up as a wrong answer instead of inheriting a freed buffer's old contents.
+bool debug_poison() {
+  const char* v = std::getenv("KG_DEBUG_POISON");
+  return v && v[0] == '1';
+}
+
 template <typename T>
 struct DevBuf {
   T* p = nullptr;
@@ -2012,6 +2019,8 @@ struct DevBuf {
     n = 0;
     if (hipMalloc(&p, std::max<size_t>(want, 1) * sizeof(T)) != hipSuccess) return fail(KG_E_NOMEM, "hipMalloc %zu", want);
     n = want;
+    if (debug_poison() && (hipMemset(p, 0xA5, n * sizeof(T)) != hipSuccess || hipDeviceSynchronize() != hipSuccess))
+      return fail(KG_E_DEVICE, "poison fill");
     return 0;
   }
   void release() {
@@ -3202,7 +3211,9 @@ int prepare_rounds(kg_engine* e, RoundGeom& g) {
   if (int rc = e->lists.ensure(D * g.B * g.nt_local * kR)) return rc;
   if (e->lists.n != lists_n)  // fresh lists hold no keys (DeviceShare rounds merge every one of the B slots)
     HIP_TRY(hipMemsetAsync(e->lists.p, 0, e->lists.n * 8, e->stream));
+  const size_t cand_n = e->cand.n;
   if (int rc = e->cand.ensure(D * g.B * kCandStride)) return rc;
+  if (e->cand.n != cand_n) HIP_TRY(hipMemsetAsync(e->cand.p, 0, e->cand.n * 8, e->stream));
   if (e->n_ranks > 1)
     if (int rc = e->gathered.ensure(D * e->n_ranks * g.B * kCandStride)) return rc;
   if (e->ds_on) {
@@ -3644,7 +3655,7 @@ static int engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank,
   // 12 int64 columns + inv_mem[2] (f64) + the kAux resources' Allocatable / Requested
   if (int rc = e->cols64.ensure((14 + 2 * kAux) * cap)) return bail(rc);
   if (int rc = e->cols32.ensure(5 * cap)) return bail(rc);   // alloc_pods, num_pods, flags, inv_cpu[2] (f32)
-  if (hipMemset(e->cols64.p, 0, (14 + 2 * kAux) * cap * 8) != hipSuccess || hipMemset(e->cols32.p, 0, 5 * cap * 4) != hipSuccess)
+  if (hipMemsetAsync(e->cols64.p, 0, (14 + 2 * kAux) * cap * 8, e->stream) != hipSuccess || hipMemsetAsync(e->cols32.p, 0, 5 * cap * 4, e->stream) != hipSuccess)
     return bail(fail(KG_E_DEVICE, "hipMemset"));
   int64_t* c64 = e->cols64.p;
   e->T.alloc_cpu = c64 + 0 * cap;
@@ -3667,9 +3678,9 @@ static int engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank,
   e->T.aux = e->cols64.p + 14 * cap;
   e->T.cap = cap;
   if (int rc = e->cursor.ensure(8)) return bail(rc);
-  if (hipMemset(e->cursor.p, 0, 8 * 8) != hipSuccess) return bail(fail(KG_E_DEVICE, "hipMemset"));
+  if (hipMemsetAsync(e->cursor.p, 0, 8 * 8, e->stream) != hipSuccess) return bail(fail(KG_E_DEVICE, "hipMemset"));
   if (int rc = e->modlists.ensure(kMaxDepth * kModListStride)) return bail(rc);
-  if (hipMemset(e->modlists.p, 0, kMaxDepth * kModListStride * 4) != hipSuccess) return bail(fail(KG_E_DEVICE, "hipMemset"));
+  if (hipMemsetAsync(e->modlists.p, 0, kMaxDepth * kModListStride * 4, e->stream) != hipSuccess) return bail(fail(KG_E_DEVICE, "hipMemset"));
   e->nodes.assign(cap, kg_node{});
   e->metrics.assign(cap, kg_node_metric{});
   e->folded_usage.assign(2 * cap, 0);
@@ -3707,7 +3718,7 @@ static int engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank,
                     (int32_t)(c.image_score != 0), (int32_t)c.weight_image};
   if (e->def_on) {
     if (int rc = e->npred.ensure(cap)) return bail(rc);
-    if (hipMemset(e->npred.p, 0, cap * sizeof(NodePred)) != hipSuccess) return bail(fail(KG_E_DEVICE, "hipMemset"));
+    if (hipMemsetAsync(e->npred.p, 0, cap * sizeof(NodePred), e->stream) != hipSuccess) return bail(fail(KG_E_DEVICE, "hipMemset"));
     if (e->def_score)
       if (int rc = e->rsv_val2.ensure(cap)) return bail(rc);
   }
@@ -3722,7 +3733,7 @@ static int engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank,
     if (int rc = e->rsv_val.ensure(cap)) return bail(rc);
     if (int rc = e->rsv_ws.ensure(8)) return bail(rc);
     if (int rc = e->rsv_part.ensure(6 * ((cap + kRsvThreads - 1) / kRsvThreads) + 4)) return bail(rc);
-    if (hipMemset(e->rsv_nd.p, 0, cap * 4) != hipSuccess || hipMemset(e->rsv_ws.p, 0, 64) != hipSuccess)
+    if (hipMemsetAsync(e->rsv_nd.p, 0, cap * 4, e->stream) != hipSuccess || hipMemsetAsync(e->rsv_ws.p, 0, 64, e->stream) != hipSuccess)
       return bail(fail(KG_E_DEVICE, "hipMemset"));
   }
   {
@@ -3740,7 +3751,7 @@ static int engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank,
     if (int rc = e->xr_norm_d.ensure((size_t)kXrPods * kXrNorm)) return bail(rc);
     if (int rc = e->xr_lists.ensure((size_t)kXrPods * nt * kR)) return bail(rc);
     if (int rc = e->xr_cand.ensure((size_t)kXrPods * kCandStride)) return bail(rc);
-    if (hipMemset(e->xr_lists.p, 0, (size_t)kXrPods * nt * kR * 8) != hipSuccess)
+    if (hipMemsetAsync(e->xr_lists.p, 0, (size_t)kXrPods * nt * kR * 8, e->stream) != hipSuccess)
       return bail(fail(KG_E_DEVICE, "hipMemset"));
     hipError_t fe = hipSuccess;
 #define KG_XR_ATTR(XF) \
@@ -3768,7 +3779,7 @@ static int engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank,
     if (int rc = e->ds_d.ensure(cap)) return bail(rc);
     e->ds_host.assign(cap, DsNode{});
     for (auto& d : e->ds_host) d.first = -1;
-    if (hipMemcpy(e->ds_d.p, e->ds_host.data(), cap * sizeof(DsNode), hipMemcpyHostToDevice) != hipSuccess)
+    if (hipMemcpyAsync(e->ds_d.p, e->ds_host.data(), cap * sizeof(DsNode), hipMemcpyHostToDevice, e->stream) != hipSuccess)
       return bail(fail(KG_E_DEVICE, "hipMemcpy"));
     const int lds = (int)(kMaxNodes / 8 + ((size_t)32 * (kCandStride + kPodWords + kDsPodWords + kDsNodeWords + kQuotaRes) +
                                            (size_t)kWave * kDsNodeWords) * 8 + KG_MAX_QUOTAS * sizeof(QuotaRow) +
@@ -3791,8 +3802,8 @@ static int engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank,
   if (e->numa_on) {
     if (int rc = e->numa_s.ensure(cap)) return bail(rc);
     if (int rc = e->numa_m.ensure(cap)) return bail(rc);
-    if (hipMemset(e->numa_s.p, 0, cap * sizeof(NumaStatic)) != hipSuccess ||
-        hipMemset(e->numa_m.p, 0, cap * sizeof(NumaMut)) != hipSuccess)
+    if (hipMemsetAsync(e->numa_s.p, 0, cap * sizeof(NumaStatic), e->stream) != hipSuccess ||
+        hipMemsetAsync(e->numa_m.p, 0, cap * sizeof(NumaMut), e->stream) != hipSuccess)
       return bail(fail(KG_E_DEVICE, "hipMemset"));
     const int lds = (int)(kMaxNodes / 8 + ((size_t)kMaxB * (kCandStride + kPodWords + kNumaPodWords) +
                                            (size_t)kWave * (kNumaStaticWords + kNumaMutWords)) * 8);
@@ -3842,6 +3853,11 @@ static int engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank,
       if (ncclCommSplit(e->comm, 0, rank, &e->comms[k], nullptr) != ncclSuccess)
         return bail(fail(KG_E_COLLECTIVE, "ncclCommSplit"));
   }
+  // Every initialisation above is ordered on e->stream and complete before the first ingest call.  (r4) They were
+  // null-stream hipMemset calls: the engine's streams are non-blocking, so nothing ordered the first ingest deltas
+  // (apply_deltas on e->stream) after the table's zero fill, and on some boxes the fill landed after the NodeMetric
+  // deltas — the node usage vanished from la_used (GPUTEST_r03, test_schedule_parity_round_shapes[16-4]).
+  if (hipStreamSynchronize(e->stream) != hipSuccess) return bail(fail(KG_E_DEVICE, "engine initialisation"));
   *out = e;
   return 0;
 }

@@ -156,6 +156,34 @@ def test_schedule_parity_round_shapes(batch, ppw):
     _parity(cfg, cl, pods)
 
 
+@pytest.mark.parametrize("depth", [1, 2])
+def test_fresh_engine_after_destroy_poisoned(depth, monkeypatch):
+    """Regression (GPUTEST_r03: round_shapes[16-4] placed pod 0 on node 230 instead of 277 on the driver's box).
+    Cause: the engine's zero fill of the node table ran as null-stream hipMemset calls, which the engine's
+    non-blocking streams do not order against, so on some boxes the fill landed after the first NodeMetric deltas and
+    the node usage vanished from la_used (the box's placements equal the oracle's with NodeUsage = 0).  The fill is now
+    stream-ordered and synchronised before kg_engine_create returns.  This runs the failing shape on an engine created
+    right after another one was destroyed, with every fresh device buffer poison-filled (KG_DEBUG_POISON), so a read of
+    memory the engine never wrote would show as a wrong answer; ingest follows creation with no host delay."""
+    cl = synth.make_cluster(900, seed=21)
+    pods = synth.make_pods(2500, seed=22)
+    cfg = framework.build_config(batch_pods=16, pods_per_wave=4, pipeline_depth=depth)
+    on, os_, st = oracle.schedule_cluster(cfg, cl, pods, n_threads=4)
+    with _engine(framework.build_config(batch_pods=3, pods_per_wave=1), cl) as e0:
+        e0.schedule(pods)
+    monkeypatch.setenv("KG_DEBUG_POISON", "1")
+    e = Engine(cfg, cl.n)
+    try:
+        synth.load_into(e, cl)
+        gn, gs, _ = e.schedule(pods)
+        mism = np.nonzero(gn != on)[0]
+        assert mism.size == 0, f"first mismatch at pod {mism[:5]}: gpu {gn[mism[:5]]} oracle {on[mism[:5]]}"
+        np.testing.assert_array_equal(gs, os_)
+        _assert_state_equal(e, st)
+    finally:
+        e.close()
+
+
 @pytest.mark.parametrize("depth,batch", [(1, 32), (2, 32), (3, 32), (4, 32), (2, 64), (3, 48), (4, 13)])
 def test_schedule_parity_pipeline_depths(depth, batch):
     """Rounds in flight (eval(r) reads the table right after resolve(r - depth)): every depth and batch shape
