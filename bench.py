@@ -299,9 +299,11 @@ def main():
     d.barrier()
     t0 = time.perf_counter()
     rounds = 0
+    active_s = 0.0  # resolvers' in-kernel active time (after the chain wait; s_memrealtime), round profiles
     for k in range(args.steps):
         st = e.schedule_staged(k * args.pods_per_step, args.pods_per_step)
         rounds += int(st["device_batches"])
+        active_s += float(st["reserved"][2])
         if d.rank == 0:
             print(f"[bench] step {k + 1}/{args.steps} done", file=sys.stderr, flush=True)
     t1 = time.perf_counter()
@@ -412,6 +414,31 @@ def main():
     pmc_name = {"c4": "eval_round_numa", "c5": "xr_eval", "c5r": "xr_eval", "shipped": "xr_eval"}.get(wl, dom)
     traffic, traffic_src, rocprof_ns = (pmc_traffic(tfile, pmc_name, cluster.n, args.batch, args.pods_per_wave,
                                                     args.depth) if d.world == 1 else (None, None, None))
+    # period decomposition of the round pipeline (Fit + LoadAware / DeviceShare round profiles): per round, the serial
+    # resolver's active time (its own s_memrealtime stamps, after the chain wait) against the wall-clock period, and the
+    # wide pass + merge stream (live HIP events) against the depth rounds it overlaps
+    period = None
+    if not rsv_path and rounds > 0:
+        per = elapsed / rounds
+        ev_ms = live.get("eval_round", {}).get("avg_ms") or live.get("ds_max_round", {}).get("avg_ms")
+        mg_ms = live.get("merge_round", {}).get("avg_ms")
+        depth = args.depth or (1 if wl == "c4" or wl == "c5ds" else 2)
+        res_us = active_s / rounds * 1e6
+        # the resolver's algorithmic bytes per launch: the round's records and pods (LDS-DMA) + the rows it writes back
+        res_bytes = B * (1024.0 + 96.0) + B * 80.0
+        period = {"us_per_round": per * 1e6, "pods_per_round": total / rounds,
+                  "resolver_active_us": res_us if active_s > 0 else None,
+                  "resolver_share": active_s / elapsed if active_s > 0 else None,
+                  "eval_us": ev_ms * 1e3 if ev_ms else None, "merge_us": mg_ms * 1e3 if mg_ms else None,
+                  "depth": depth,
+                  "eval_stream_share": ((ev_ms or 0) + (mg_ms or 0)) * 1e-3 / (depth * per) if ev_ms else None,
+                  "dominant": ("resolver" if active_s > 0 and active_s / elapsed >= ((ev_ms or 0) + (mg_ms or 0)) * 1e-3
+                               / (depth * per) else "eval_stream"),
+                  "resolver_roofline": ({"algo_bytes_per_launch": res_bytes,
+                                         "frac": res_bytes / (res_us * 1e-6) / 1e9 / HBM_PEAK_GBS}
+                                        if active_s > 0 else None),
+                  "note": "resolver_share = in-kernel active time / wall time of the timed steps (the serial chain "
+                          "sets the period when it is near 1); eval_stream_share = (eval + merge) / (depth x period)"}
     if d.rank == 0:
         pods_s = total / elapsed
         desc = {
@@ -477,7 +504,8 @@ def main():
                          "frac_rocprof": algo / (rocprof_ns * 1e-9) / 1e9 / HBM_PEAK_GBS if rocprof_ns else None,
                          "live_ms": {k: v["avg_ms"] for k, v in live.items()},
                          "live_launches": {k: v["launches"] for k, v in live.items()},
-                         "isolated_ms": {k: v[0] for k, v in isolated.items()}},
+                         "isolated_ms": {k: v[0] for k, v in isolated.items()},
+                         "period": period},
             "cpu_baseline": cpu,
             "pcie_inclusive_pods_per_sec": pcie,
             "single_pod_call": single,

@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define KG_ABI_VERSION 10
+#define KG_ABI_VERSION 11
 
 /* ---- resource slots (fixed order) ------------------------------------------------------- */
 enum {
@@ -145,7 +145,11 @@ enum {
    * reservation/plugin.go:392-395). */
   KG_POD_REQUEST_KEYS = 1 << 3,
   KG_POD_CPU_KEY = 1 << 4,
-  KG_POD_MEM_KEY = 1 << 5
+  KG_POD_MEM_KEY = 1 << 5,
+  /* (ABI 11) tolerated_taints was compiled against the first taint_count taints of the caller's taint table; without
+   * it the mask does not depend on the table (no tolerations, or a toleration with no key, operator Exists and no
+   * effect, for which the caller passes all ones) */
+  KG_POD_TAINT_TABLE = 1 << 6
 };
 #define KG_MAX_QUOTAS 64
 
@@ -308,6 +312,10 @@ typedef struct kg_pod {
   int64_t n_containers;
   int64_t container_image_bit[KG_MAX_CONTAINERS];
   int64_t container_image_score[KG_MAX_CONTAINERS];
+  /* (ABI 11) with KG_POD_TAINT_TABLE: the number of taints of the caller's taint table tolerated_taints was compiled
+   * against (taint ids < taint_count are decided).  kg_pods_schedule* refuses a staged queue holding a pod compiled
+   * against fewer taints than some valid node row carries (KG_E_INVALID: re-stage the pods). */
+  int64_t taint_count;
 } kg_pod;
 
 /* pod reservation flags */
@@ -404,6 +412,11 @@ typedef struct kg_node_predicates {
   uint64_t taints_soft;                        /* the node's taints with effect PreferNoSchedule                */
   uint64_t images;                             /* (ABI 10) bit i: NodeInfo.ImageStates holds image i of the     */
                                                /* caller's image table (the ≤ 64 images queued pods reference) */
+  /* (ABI 11) the sizes of the caller's predicate and image tables this row was compiled against: predicate ids <
+   * predicate_count and image ids < image_count are decided.  kg_pods_schedule* refuses a staged queue that
+   * references a predicate or image id some valid node row was not compiled for (KG_E_INVALID: re-send the rows). */
+  int64_t predicate_count;
+  int64_t image_count;
 } kg_node_predicates;
 
 typedef struct kg_stats {

@@ -32,10 +32,11 @@ REJECT_FIT_PODS, REJECT_FIT_CPU, REJECT_FIT_MEMORY, REJECT_LOADAWARE, REJECT_INV
 NODE_VALID, NODE_HAS_RAW_ALLOCATABLE, NODE_HAS_CUSTOM_THRESHOLDS = 1, 2, 4
 POD_DAEMONSET, POD_NON_PREEMPTIBLE, POD_RESERVE = 1, 2, 4
 POD_REQUEST_KEYS, POD_CPU_KEY, POD_MEM_KEY = 8, 16, 32
+POD_TAINT_TABLE = 64
 MAX_OWNER_GROUPS = 64
 QUOTA_RES = 8
 MAX_QUOTAS = 64
-ABI_VERSION = 10
+ABI_VERSION = 11
 MAX_RSV_SLOTS = 4
 RSV_POLICY = {"Default": 0, "Aligned": 1, "Restricted": 2}
 POD_RSV_AFFINITY = 1
@@ -140,9 +141,11 @@ POD_DTYPE = np.dtype([
     _i64("n_preferred_terms"), ("preferred_terms", np.uint64, (MAX_AFF_TERMS,)), _i64("preferred_weights", MAX_AFF_TERMS),
     _i64("preferred_cpu_exclusive_policy"),
     _i64("n_containers"), _i64("container_image_bit", MAX_CONTAINERS), _i64("container_image_score", MAX_CONTAINERS),
+    _i64("taint_count"),
 ])
 NODE_PRED_DTYPE = np.dtype([("predicates", np.uint64), ("taints_hard", np.uint64), ("taints_soft", np.uint64),
-                            ("images", np.uint64)])
+                            ("images", np.uint64), _i64("predicate_count"), _i64("image_count")])
+
 
 NODE_RSV_DTYPE = np.dtype([_i64("n")] + [_i64(f, MAX_RSV_SLOTS) for f in (
     "owner", "allocatable_cpu", "allocatable_mem", "allocated_cpu", "allocated_mem", "assigned", "order", "policy",

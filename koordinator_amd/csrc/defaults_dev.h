@@ -27,10 +27,9 @@ namespace kg {
 
 constexpr int kAffTerms = KG_MAX_AFF_TERMS;
 
-struct NodePred {  // 32 B per node (kg_node_predicates)
+struct NodePred {  // 32 B per node (the masks of kg_node_predicates; its ABI 11 table sizes stay on the host)
   uint64_t pred, hard, soft, images;
 };
-static_assert(sizeof(NodePred) == sizeof(kg_node_predicates), "NodePred layout");
 
 constexpr int kContainers = KG_MAX_CONTAINERS;
 struct DefPod {  // 184 B per staged pod; the pass broadcasts one

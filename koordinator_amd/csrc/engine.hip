@@ -999,6 +999,582 @@ __global__ __launch_bounds__(kWave) void resolve_round(DevTable T0, const DevPod
   KG_STAMP(2, 31);
 }
 
+// ---- round kernel 3 (r4): FIFO resolve with look-ahead helper waves (monotone profiles) ----------------------
+// One workgroup: the chain wave, a keeper wave and kHelpers helper waves.  resolve_round above did everything on one
+// wave, so every pod's re-score of the modified rows (~190 VALU instructions at one instruction per 4 cycles) and its
+// assume sat on the serial chain.  Here the chain only decides; the re-score moves to helpers that work kLag pods
+// ahead, and the assume to the keeper:
+//   helper(j), on the table after pods ≤ j − kLag (the winners the chain has published by then), scores pod j on
+//   every modified row (lane = slot) and on its listed candidates, and hands the chain the kTop best keys T_j of
+//   {listed candidates not modified by then} ∪ {modified rows}, each with where its row lives in LDS.
+//   chain step j: S = the winners of pods j − kLag + 1 .. j − 1 (≤ kLag − 1 nodes, the only rows that can have
+//   changed since helper(j)'s snapshot).  c* = the first entry of T_j not in S: every node outside S holds its
+//   snapshot key, and T_j is the top of those, so c* is their maximum (|S| < kTop, so some entry lies outside S).
+//   A node of S can only have lost score since the snapshot (monotone profile), so only the S nodes listed in T_j
+//   above c* need an exact re-score — on the chain's current copy of their rows.  best = max(c*, those); best < ub
+//   stops the round as before (ub bounds every node outside the pod's record, modified or not).
+// The chain publishes, per pod, the winner and its slot; the keeper applies the pod's assume to the slot's row (its
+// own register copy, lane = slot) and publishes the row's new state; each helper advances its own register copy of
+// the rows to its lag from those states, and the chain reads them only to re-score a recent winner (rare: ~5 % of C3
+// pods).
+constexpr int kHelpers = 5;                        // helper waves
+constexpr int kLag = kHelpers + 1;                 // helper(j) scores pod j on the table after pods ≤ j − kLag
+constexpr int kTop = kLag;                         // candidates per pod handed to the chain (> |S| = kLag − 1)
+constexpr int kMwThreads = kWave * (2 + kHelpers);  // the chain, the keeper, the helpers
+constexpr uint32_t kTopMod = 0x80000000u;  // s_topx: a modified row (its slot in the low bits); otherwise the LDS
+                                           // word offset of the candidate's round-start EvalRow
+constexpr int64_t kMwSpin = 1 << 24;       // bounded in-workgroup waits (an error instead of a hang on a bug)
+
+struct MwLayout {  // dynamic LDS carve; u64 arrays (word offsets), then u32 arrays (offsets from the u32 base)
+  uint32_t cand, podw, par, prow, toprow, state, top, u64_end;
+  uint32_t topx, win, wslot, nsl, ready, slot_node, slot_row, hash, prevn, sctl, u32_end;
+};
+__host__ __device__ inline MwLayout mw_layout(int nb) {
+  MwLayout L;
+  L.cand = 0;
+  L.podw = L.cand + (uint32_t)nb * kCandStride;
+  L.par = L.podw + (uint32_t)nb * kPodWords;
+  L.prow = L.par + kParWords;                          // earlier rounds' rows (slots < nP)
+  // slots of earlier rounds ≤ (depth − 1) · batch ≤ kMaxMod − nb (RoundGeom keeps depth · batch ≤ kMaxMod)
+  L.toprow = L.prow + (uint32_t)(kMaxMod - nb) * kEvalRowWords;  // rows of listed candidates past the staged ones
+  L.state = L.toprow + (uint32_t)nb * kTop * kEvalRowWords;  // the winner's row after pod j's assume
+  L.top = L.state + (uint32_t)nb * kEvalRowWords;
+  L.u64_end = L.top + (uint32_t)nb * kTop;
+  L.topx = 0;
+  L.win = L.topx + (uint32_t)nb * kTop;
+  L.wslot = L.win + (uint32_t)nb;
+  L.nsl = L.wslot + (uint32_t)nb;    // slots in use after pod j
+  L.ready = L.nsl + (uint32_t)nb;    // helper(j) done
+  L.slot_node = L.ready + (uint32_t)nb;
+  L.slot_row = L.slot_node + kMaxMod;   // LDS word offset of the slot's round-start row
+  L.hash = L.slot_row + kMaxMod;
+  L.prevn = L.hash + kModHash;
+  L.sctl = L.prevn + kMaxMod;  // [0] pods published, [1] chain ended, [2] abort, [3] nP, [4] error, [5] states kept
+  L.u32_end = L.sctl + 8;
+  return L;
+}
+inline size_t mw_lds_bytes(int nb) {
+  const MwLayout L = mw_layout(nb);
+  return (size_t)L.u64_end * 8 + (size_t)L.u32_end * 4;
+}
+
+__device__ __forceinline__ uint32_t lds_ld(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ uint32_t lds_acq(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_rel(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ int mod_lookup(const uint32_t* h, uint32_t node) {
+  uint32_t i = mod_hash(node);
+  for (int it = 0; it < kModHash; ++it) {
+    const uint32_t v = lds_ld(&h[i]);
+    if (v == 0u) return -1;
+    if ((v >> 8) == node + 1u) return (int)(v & 0xFFu);
+    i = (i + 1u) & (kModHash - 1);
+  }
+  return -1;
+}
+__device__ __forceinline__ void lds_put_row(uint64_t* dst, const EvalRow& er) {
+  uint64_t w[kEvalRowWords];
+  __builtin_memcpy(w, &er, sizeof(er));
+#pragma unroll
+  for (int q = 0; q < kEvalRowWords; ++q) dst[q] = w[q];
+}
+// fitsRequest over the kAux resources on a modified row whose state includes this round's pods ≤ upto (published
+// winners in `win`)
+__device__ __forceinline__ bool mw_aux_fits(const DevTable& T, uint32_t node, const int64_t* __restrict__ rq, int upto,
+                                            const uint32_t* win, const DevPod* s_pods, const int64_t* __restrict__ prq) {
+  int64_t add[kAux] = {0, 0, 0, 0, 0};
+  for (int q = 0; q <= upto; ++q) {
+    if (lds_ld(&win[q]) != node || !(s_pods[q].flags & P_AUX)) continue;
+#pragma unroll
+    for (int r = 0; r < kAux; ++r) add[r] += prq[(size_t)q * kAux + r];
+  }
+  bool ok = true;
+#pragma unroll
+  for (int r = 0; r < kAux; ++r)
+    if (rq[r] != 0) ok &= !(rq[r] > T.aux[(size_t)r * T.cap + node] - (T.aux[(size_t)(kAux + r) * T.cap + node] + add[r]));
+  return ok;
+}
+
+template <int PF, bool QUOTA>
+__global__ __launch_bounds__(kMwThreads) void resolve_mw(DevTable T0, const DevPod* __restrict__ pods,
+                                                         int64_t* __restrict__ ctl, int64_t first, int nb,
+                                                         const uint64_t* __restrict__ cand, EvalParams P,
+                                                         uint64_t* __restrict__ out_keys,
+                                                         int32_t* __restrict__ modlists, int slot, int depth,
+                                                         int n_prev, int32_t* __restrict__ poison, int64_t seq,
+                                                         int wait, QuotaRow* __restrict__ quotas, int nq,
+                                                         const int64_t* __restrict__ paux) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
+  KG_STAMP(2, 0);
+  const MwLayout L = mw_layout(nb);
+  const int tid = threadIdx.x, lane = tid % kWave, wave = tid / kWave;
+  if (wave == 0) __builtin_amdgcn_s_setprio(3);  // the chain first, then its helpers, then any wide-pass wave
+  else __builtin_amdgcn_s_setprio(2);
+  uint64_t* s_cand = smem + L.cand;
+  uint64_t* s_par = smem + L.par;
+  uint32_t* b32 = reinterpret_cast<uint32_t*>(smem + L.u64_end);
+  uint32_t* s_topx = b32 + L.topx;
+  uint32_t* s_win = b32 + L.win;
+  uint32_t* s_wslot = b32 + L.wslot;
+  uint32_t* s_nsl = b32 + L.nsl;
+  uint32_t* s_ready = b32 + L.ready;
+  uint32_t* s_slot_node = b32 + L.slot_node;
+  uint32_t* s_slot_row = b32 + L.slot_row;
+  uint32_t* s_hash = b32 + L.hash;
+  uint32_t* s_prevn = b32 + L.prevn;
+  uint32_t* s_ctl = b32 + L.sctl;
+  const DevPod* s_pods = reinterpret_cast<const DevPod*>(smem + L.podw);
+  if (tid < kParWords) {
+    uint64_t pw[kParWords] = {};
+    __builtin_memcpy(pw, &P, sizeof(P));
+#pragma unroll
+    for (int q = 0; q < kParWords; ++q)
+      if (tid == q) s_par[q] = pw[q];
+  }
+  {  // prologue, independent of the previous round: LDS-DMA of the records and pods, flag / hash clears
+    const int n16 = nb * kCandStride / 2;
+    for (int it = 0; it * kMwThreads < n16; ++it) {
+      const int idx = it * kMwThreads + tid;
+      if (idx < n16)
+        __builtin_amdgcn_global_load_lds((global_cvoid_ptr)(cand + 2 * (size_t)idx),
+                                         (lds_void_ptr)(s_cand + 2 * ((size_t)it * kMwThreads + wave * kWave)), 16, 0, 0);
+    }
+    const uint64_t* pw = reinterpret_cast<const uint64_t*>(pods + first);
+    const int p16 = nb * kPodWords / 2;
+    for (int it = 0; it * kMwThreads < p16; ++it) {
+      const int idx = it * kMwThreads + tid;
+      if (idx < p16)
+        __builtin_amdgcn_global_load_lds((global_cvoid_ptr)(pw + 2 * (size_t)idx),
+                                         (lds_void_ptr)(smem + L.podw + 2 * ((size_t)it * kMwThreads + wave * kWave)), 16, 0, 0);
+    }
+    for (int w = tid; w < kModHash; w += kMwThreads) s_hash[w] = 0u;
+    for (int w = tid; w < nb; w += kMwThreads) s_ready[w] = 0u;
+    if (tid < 8) s_ctl[tid] = 0u;
+  }
+  // chain on the previous round's resolver (as resolve_round)
+  if (wave == 0) {
+    int timed_out = 0;
+    if (wait) {
+      if (lane == 0) {
+        int64_t it = 0;
+        while (__hip_atomic_load(&ctl[4], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < seq - 1) {
+          __builtin_amdgcn_s_sleep(1);
+          if (++it > kSpinLimit) {
+            timed_out = 1;
+            break;
+          }
+        }
+      }
+      timed_out = __builtin_amdgcn_readfirstlane(timed_out);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+    KG_STAMP(2, 1);
+    const int abort_ = timed_out || *poison || ctl[0] != first;
+    if (abort_ && lane == 0 && timed_out) ctl[5] = 1;
+    int nM = 0;
+    if (!abort_) {  // rows the n_prev previous rounds modified: slots [0, nP), rows read after the chain wait
+      for (int d = 1; d <= n_prev; ++d) {
+        const int32_t* ml = modlists + (size_t)(((slot - d) % depth + depth) % depth) * kModListStride;
+        const int c = ml[0];
+        for (int t = lane; t < c; t += kWave) s_prevn[nM + t] = (uint32_t)ml[1 + t];
+        nM += c;
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    for (int s = lane; s < nM; s += kWave) {
+      const uint32_t node = s_prevn[s];
+      const bool mine = mod_insert(s_hash, node, s) == s;  // a node listed by two earlier rounds keeps its first slot
+      s_slot_node[s] = mine ? node : kNoNode;
+      s_slot_row[s] = L.prow + (uint32_t)s * kEvalRowWords;
+      if (mine) lds_put_row(smem + L.prow + (size_t)s * kEvalRowWords, make_eval_row(load_row(table_at(T0), node), P));
+    }
+    if (lane == 0) {
+      s_ctl[2] = (uint32_t)abort_;
+      s_ctl[3] = (uint32_t)nM;
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // LDS-DMA of records and pods (+ the rows above)
+  __syncthreads();
+  if (s_ctl[2]) {
+    if (wave == 0) publish_round(ctl, seq);
+    return;
+  }
+  KG_STAMP(2, 2);
+  const uint64_t t_active = __builtin_amdgcn_s_memrealtime();  // the period decomposition's resolver time
+  const int nP = (int)s_ctl[3];
+  const bool narrow = P.score_bits <= 13;  // packed keys fit 32 bits (node < 2^19 = kMaxNodes)
+  const int64_t* prq0 = paux + (size_t)first * kAux;
+
+  if (wave >= 2) {
+    // ---------------- helper waves: pods j ≡ wave − 2 (mod kHelpers) ----------------
+    // The wave keeps its own copy of the modified rows at its snapshot (lane = slot, two banks), advanced by the
+    // winners the chain publishes: a winner's row after its pod is read from s_state by its owner lane alone, so a
+    // pod costs the LDS a few single-lane row reads instead of a 64-lane one (which saturated the CU's LDS pipe).
+    int seen = nP;  // slots this wave has entered into the node → slot hash
+    int applied = -1;  // pods whose placement this wave's rows include
+    ModRow H0, H1;
+    mod_row_init(H0);
+    mod_row_init(H1);
+    if (lane < nP && s_slot_node[lane] != kNoNode) {
+      H0.node = s_slot_node[lane];
+      H0.er = lds_row(smem + L.prow + (size_t)lane * kEvalRowWords);
+    }
+    if (kWave + lane < nP && s_slot_node[kWave + lane] != kNoNode) {
+      H1.node = s_slot_node[kWave + lane];
+      H1.er = lds_row(smem + L.prow + (size_t)(kWave + lane) * kEvalRowWords);
+    }
+    for (int j = wave - 2; j < nb; j += kHelpers) {
+      const int lag = j - kLag;
+      // the snapshot needs the keeper's states of pods ≤ lag (the chain has then published them too)
+      uint32_t kept = lds_acq(&s_ctl[5]);
+      bool gone = false;
+      for (int64_t it = 0; (int)kept < lag + 1; ++it) {
+        if (lds_acq(&s_ctl[1]) && (int)lds_acq(&s_ctl[0]) < lag + 1) {  // the chain ended before pod lag
+          gone = true;
+          break;
+        }
+        if (it > kMwSpin) {
+          if (lane == 0) s_ctl[4] = 1u;  // waited too long: the round reports an error
+          gone = true;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+        kept = lds_acq(&s_ctl[5]);
+      }
+      if (gone) break;
+      if (lane == 0) KG_LANE_SUB(j, 0);
+      for (int k = applied + 1; k <= lag; ++k) {  // advance the snapshot to pods ≤ lag
+        const uint32_t wk = s_win[k];
+        if (wk == kNoNode) continue;
+        const int sk = (int)s_wslot[k];
+        if (sk < kWave) {
+          if (lane == sk) H0.node = wk, H0.er = lds_row(smem + L.state + (size_t)k * kEvalRowWords);
+        } else if (lane == sk - kWave) {
+          H1.node = wk, H1.er = lds_row(smem + L.state + (size_t)k * kEvalRowWords);
+        }
+      }
+      applied = lag > applied ? lag : applied;
+      if (lane == 0) KG_LANE_SUB(j, 1);
+      const int nSl = lag >= 0 ? (int)s_nsl[lag] : nP;
+      for (int s = seen + lane; s < nSl; s += kWave) mod_insert(s_hash, s_slot_node[s], s);
+      seen = nSl > seen ? nSl : seen;
+      const DevPod p = s_pods[j];
+      const bool aux = (PF & PF_FIT_FILTER) && (p.flags & P_AUX);
+      const int64_t* rq = paux + (size_t)(first + j) * kAux;
+      // the pod's listed candidates not modified at the snapshot (in key order: lane = record position)
+      const uint64_t key = s_cand[(size_t)j * kCandStride + lane];
+      bool modl = false;
+      if (key) {
+        const int sl = mod_lookup(s_hash, key_node(key));
+        modl = sl >= 0 && sl < nSl;
+      }
+      const uint64_t um0 = __ballot(key != 0 && !modl);
+      // lane i < kTop: the i-th of them; past the record's staged rows its round-start row comes from HBM, issued
+      // now so that the load overlaps the modified rows' scoring below
+      int my_lpos = -1;
+      {
+        uint64_t u = um0;
+#pragma unroll
+        for (int i = 0; i < kTop; ++i) {
+          const int pos = u ? (int)__builtin_ctzll(u) : -1;
+          u &= u - 1;
+          if (lane == i) my_lpos = pos;
+        }
+      }
+      const uint64_t my_lkey = __shfl(key, my_lpos >= 0 ? my_lpos : 0);  // every lane takes part in the permute
+      const uint32_t my_lnode = key_node(my_lkey);
+      const bool my_hbm = my_lpos >= kStaged;
+      Row hr;
+      if (my_hbm) hr = load_row(table_at(T0), my_lnode);
+      // every modified row at the snapshot (after pods ≤ lag)
+      uint64_t mk[2] = {0, 0};
+      mk[0] = mod_row_key<PF>(H0, p, P, s_par);
+      if (aux && mk[0] && !mw_aux_fits(table_at(T0), H0.node, rq, lag, s_win, s_pods, prq0)) mk[0] = 0;
+      if (nSl > kWave) {
+        mk[1] = mod_row_key<PF>(H1, p, P, s_par);
+        if (aux && mk[1] && !mw_aux_fits(table_at(T0), H1.node, rq, lag, s_win, s_pods, prq0)) mk[1] = 0;
+      }
+      // T_j = the kTop best of the two descending sequences
+      uint64_t um = um0;
+      uint64_t tk_l = 0;
+      uint32_t tx_l = 0;
+      int n_listed = 0;  // listed entries taken so far (the n-th is lane n's my_lpos)
+      uint64_t mrest = mk[0] > mk[1] ? mk[0] : mk[1];
+      uint64_t mtop = wave_max_modkey(mrest, narrow);
+#pragma unroll
+      for (int i = 0; i < kTop; ++i) {
+        const int lpos = um ? (int)__builtin_ctzll(um) : -1;
+        const uint64_t lkey = lpos >= 0 ? readlane_u64(key, lpos) : 0;
+        uint64_t tkey;
+        uint32_t tx;
+        if (lkey == 0 && mtop == 0) {
+          tkey = 0;
+          tx = 0;
+        } else if (lkey > mtop) {
+          tkey = lkey;
+          um &= um - 1;
+          tx = lpos < kStaged ? L.cand + (uint32_t)j * kCandStride + kRecRows + (uint32_t)lpos * kEvalRowWords
+                              : L.toprow + (uint32_t)(j * kTop + n_listed) * kEvalRowWords;
+          ++n_listed;
+        } else {
+          tkey = mtop;
+          const uint64_t b0 = __ballot(mk[0] == mtop), b1 = __ballot(mk[1] == mtop);
+          const int sl = b0 ? (int)__builtin_ctzll(b0) : kWave + (int)__builtin_ctzll(b1);
+          tx = kTopMod | (uint32_t)sl;
+          if (lane == (sl & (kWave - 1))) {
+            if (sl < kWave) mk[0] = 0;
+            else mk[1] = 0;
+          }
+          mrest = mk[0] > mk[1] ? mk[0] : mk[1];
+          mtop = i + 1 < kTop ? wave_max_modkey(mrest, narrow) : 0;
+        }
+        if (lane == i) {
+          tk_l = tkey;
+          tx_l = tx;
+        }
+      }
+      if (lane == 0) KG_LANE_SUB(j, 2);
+      if (my_hbm && lane < n_listed)  // a listed entry of T_j past the staged rows: its row from the early load
+        lds_put_row(smem + L.toprow + (size_t)(j * kTop + lane) * kEvalRowWords, make_eval_row(hr, P));
+      if (lane < kTop) {
+        smem[L.top + (size_t)j * kTop + lane] = tk_l;
+        s_topx[j * kTop + lane] = tx_l;
+      }
+      if (lane == 0) lds_rel(&s_ready[j], 1u);
+      if (lane == 0) KG_LANE_SUB(j, 3);
+    }
+    return;
+  }
+
+  if (wave == 1) {
+    // ---------------- the keeper wave: the modified rows' states behind the chain ----------------
+    // For each pod the chain has published, the winner's slot takes the pod's assume (NodeInfo.AddPod + LoadAware
+    // Reserve → podAssignCache.assign) on its owner lane, and the row's new state goes to s_state[k]; helpers read
+    // their snapshots from it, the chain only when it re-scores a recent winner.
+    ModRow K0, K1;
+    mod_row_init(K0);
+    mod_row_init(K1);
+    if (lane < nP && s_slot_node[lane] != kNoNode) {
+      K0.node = s_slot_node[lane];
+      K0.er = lds_row(smem + L.prow + (size_t)lane * kEvalRowWords);
+    }
+    if (kWave + lane < nP && s_slot_node[kWave + lane] != kNoNode) {
+      K1.node = s_slot_node[kWave + lane];
+      K1.er = lds_row(smem + L.prow + (size_t)(kWave + lane) * kEvalRowWords);
+    }
+    int known = nP;  // slots this wave holds (created in order by the chain)
+    for (int k = 0; k < nb; ++k) {
+      uint32_t done = lds_acq(&s_ctl[0]);
+      for (int64_t it = 0; (int)done <= k; ++it) {
+        if (lds_acq(&s_ctl[1]) || it > kMwSpin) break;
+        __builtin_amdgcn_s_sleep(1);
+        done = lds_acq(&s_ctl[0]);
+      }
+      if ((int)done <= k) {
+        if (!lds_acq(&s_ctl[1]) && lane == 0) s_ctl[4] = 1u;
+        break;
+      }
+      const uint32_t wk = s_win[k];
+      if (wk != kNoNode) {
+        const int sk = (int)s_wslot[k];
+        const DevPod p = s_pods[k];
+        if (sk >= known) {  // a new slot: its round-start row
+          const uint32_t off = s_slot_row[sk];
+          if (sk < kWave) {
+            if (lane == sk) K0.node = wk, K0.er = lds_row(smem + off);
+          } else if (lane == sk - kWave) {
+            K1.node = wk, K1.er = lds_row(smem + off);
+          }
+          known = sk + 1;
+        }
+        if (sk < kWave) {
+          if (lane == sk) {
+            assume_mod<PF>(K0.er, p, P);
+            lds_put_row(smem + L.state + (size_t)k * kEvalRowWords, K0.er);
+          }
+        } else if (lane == sk - kWave) {
+          assume_mod<PF>(K1.er, p, P);
+          lds_put_row(smem + L.state + (size_t)k * kEvalRowWords, K1.er);
+        }
+      }
+      if (lane == 0) lds_rel(&s_ctl[5], (uint32_t)(k + 1));
+    }
+    return;
+  }
+
+  // ---------------- the chain wave ----------------
+  DevQuota ql = QUOTA ? quota_load(quotas, nq, lane) : DevQuota{0, 0, 0, 0, 0, 0, 0, 0};
+  uint32_t rw[kLag - 1];  // winners of the kLag − 1 previous pods (kNoNode: none), oldest first
+  int rsl[kLag - 1];      // their slots
+#pragma unroll
+  for (int k = 0; k < kLag - 1; ++k) rw[k] = kNoNode, rsl[k] = -1;
+  uint64_t my_out = 0;
+  int consumed = 0, n_slow = 0, n_wait = 0, nS = nP, err = 0;
+  // pod j's inputs are read during pod j − 1 (after its decision, before its publication): the helper's flag and T_j
+  // in one LDS round trip — a wave's LDS reads are served in order, so T_j read after a set flag holds what the helper
+  // wrote before it released the flag; a flag still clear is re-polled at pod j
+  uint32_t rdy_n = lds_ld(&s_ready[0]);
+  asm volatile("" ::: "memory");
+  uint64_t tk_n = lane < kTop ? smem[L.top + lane] : 0;
+  uint32_t tx_n = lane < kTop ? s_topx[lane] : 0u;
+  uint64_t ub_n = s_cand[kC];
+  DevPod p_n = s_pods[0];
+  for (int j = 0; j < nb; ++j) {
+    KG_POD_DIAG(j, (uint32_t)n_wait);
+    const uint32_t rdy = rdy_n;
+    uint64_t tk = tk_n;
+    uint32_t tx = tx_n;
+    const uint64_t ub = ub_n;
+    const DevPod p = p_n;
+    if (rdy == 0u) {
+      ++n_wait;
+      int64_t it = 0;
+      while (lds_acq(&s_ready[j]) == 0u && ++it < kMwSpin) __builtin_amdgcn_s_sleep(0);
+      if (it >= kMwSpin || lds_acq(&s_ctl[4])) {
+        err = 1;
+        break;
+      }
+      tk = lane < kTop ? smem[L.top + (size_t)j * kTop + lane] : 0;
+      tx = lane < kTop ? s_topx[j * kTop + lane] : 0u;
+    }
+    bool placed = false;
+    uint32_t w = kNoNode;
+    int wsl = -1;
+    if (!QUOTA || quota_admit(ql, p)) {  // ElasticQuota PreFilter rejects: Unschedulable, no node search
+      const uint32_t tn = key_node(tk);
+      bool inS = false;
+#pragma unroll
+      for (int k = 0; k < kLag - 1; ++k) inS |= tn == rw[k];
+      inS &= tk != 0;
+      const uint64_t okm = __ballot(tk != 0 && !inS);
+      const int pos = okm ? (int)__builtin_ctzll(okm) : kTop;
+      uint64_t best = okm ? readlane_u64(tk, pos) : 0;
+      uint64_t above = __ballot(inS && lane < pos);
+      KG_POD_SUB(j, 0);
+      bool from_s = false;
+      if (above) {  // recent winners listed above c*: re-score them exactly on their current rows (rare)
+        ++n_slow;
+        {  // the keeper has published the states of pods < j
+          int64_t it = 0;
+          while ((int)lds_acq(&s_ctl[5]) < j && ++it < kMwSpin) __builtin_amdgcn_s_sleep(0);
+          if (it >= kMwSpin) {
+            err = 1;
+            break;
+          }
+        }
+        // lane k < kLag − 1: window entry k (pod j − kLag + 1 + k); its state is the node's current row when no later
+        // entry placed the same node
+        uint32_t nd = kNoNode;
+        bool last = true;
+#pragma unroll
+        for (int k = 0; k < kLag - 1; ++k) {
+          if (lane == k) nd = rw[k];
+          if (lane < k && nd == rw[k]) last = false;
+        }
+        bool want = false;
+        while (above) {
+          const int b = (int)__builtin_ctzll(above);
+          above &= above - 1;
+          want |= nd == (uint32_t)__builtin_amdgcn_readlane((int)tn, b);
+        }
+        want &= lane < kLag - 1 && nd != kNoNode && last;
+        uint64_t mkv = 0;
+        if (want) {
+          const int step = j - (kLag - 1) + lane;
+          const EvalRow er = lds_row(smem + L.state + (size_t)step * kEvalRowWords);
+          mkv = mod_key<PF>(er, nd, p, P, s_par);
+          const bool aux = (PF & PF_FIT_FILTER) && (p.flags & P_AUX);
+          if (aux && mkv && !mod_aux_fits(table_at(T0), nd, paux + (size_t)(first + j) * kAux, j, my_out, s_pods, prq0))
+            mkv = 0;
+        }
+        const uint64_t mbest = wave_max_modkey(mkv, narrow);
+        from_s = mbest > best;
+        best = from_s ? mbest : best;
+      }
+      if (best < ub) break;  // an unseen node could still win: leave this pod to the next round
+      KG_POD_SUB(j, 1);
+      my_out = lane == j ? best : my_out;
+      if (best != 0) {  // 0: unschedulable (ub == 0: no feasible node anywhere)
+        placed = true;
+        w = key_node(best);
+        if (from_s) {  // the slot of the last window entry that placed w
+#pragma unroll
+          for (int k = 0; k < kLag - 1; ++k) wsl = rw[k] == w ? rsl[k] : wsl;
+        } else {
+          const uint32_t cx = (uint32_t)__builtin_amdgcn_readlane((int)tx, pos);
+          if (cx & kTopMod) {
+            wsl = (int)(cx & 0xFFu);
+          } else {  // a node first modified now: a new slot (the keeper loads its round-start row from LDS)
+            wsl = nS++;
+            if (lane == 0) {
+              s_slot_node[wsl] = w;
+              s_slot_row[wsl] = cx;
+            }
+          }
+        }
+      }
+    } else {
+      my_out = lane == j ? 0 : my_out;
+    }
+    KG_POD_SUB(j, 2);
+    if (QUOTA && placed) quota_charge(ql, p, lane);  // ElasticQuota Reserve
+    if (j + 1 < nb) {  // pod j + 1's inputs (see above)
+      rdy_n = lds_ld(&s_ready[j + 1]);
+      asm volatile("" ::: "memory");
+      tk_n = lane < kTop ? smem[L.top + (size_t)(j + 1) * kTop + lane] : 0;
+      tx_n = lane < kTop ? s_topx[(j + 1) * kTop + lane] : 0u;
+      ub_n = s_cand[(size_t)(j + 1) * kCandStride + kC];
+      p_n = s_pods[j + 1];
+    }
+    if (lane == 0) {
+      s_win[j] = w;
+      s_wslot[j] = (uint32_t)wsl;
+      s_nsl[j] = (uint32_t)nS;
+      lds_rel(&s_ctl[0], (uint32_t)(j + 1));
+    }
+    KG_POD_SUB(j, 3);
+    ++consumed;
+#pragma unroll
+    for (int k = 0; k + 1 < kLag - 1; ++k) rw[k] = rw[k + 1], rsl[k] = rsl[k + 1];
+    rw[kLag - 2] = w;
+    rsl[kLag - 2] = wsl;
+  }
+  if (lane == 0) lds_rel(&s_ctl[1], 1u);  // the helpers stop waiting
+  KG_STAMP(2, 30);
+  // write-back (as resolve_round): each placed pod's terms onto its winner + this round's modified-row list
+  const bool mine = !err && lane < consumed && my_out != 0;
+  const uint32_t my_node = mine ? key_node(my_out) : kNoNode;
+  if (mine) writeback_pod(table_at(T0), my_node, s_pods[lane], paux + (size_t)(first + lane) * kAux);
+  int32_t* my_mod = modlists + (size_t)slot * kModListStride;
+  const uint64_t lane_lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  const uint64_t bm = __ballot(mine);
+  if (mine) my_mod[1 + __popcll(bm & lane_lt)] = (int32_t)my_node;
+  if (!err && lane < consumed) out_keys[first + lane] = my_out;
+  if (QUOTA && !err) quota_store(quotas, nq, lane, ql);
+  if (lane == 0) {
+    my_mod[0] = __popcll(bm);
+    if (err) {
+      ctl[5] = 1;  // reported as a device error by the host
+      *poison = 1;
+    } else {
+      ctl[0] = first + consumed;
+      ctl[1] += 1;
+      ctl[2] += consumed;
+      ctl[6] += n_slow;  // diagnostics: pods that re-scored recent winners on the chain
+      ctl[7] += n_wait;  // diagnostics: pods the chain waited for its helper
+      if (consumed < nb) *poison = 1;
+    }
+    ctl[8] += (int64_t)(__builtin_amdgcn_s_memrealtime() - t_active);
+  }
+  publish_round(ctl, seq);
+  KG_STAMP(2, 31);
+}
+
 // ---- NodeNUMAResource profiles (config C4) --------------------------------------------
 // NUMA state per node: static TopologyOptions (NumaStatic, 128 B) + NodeAllocation (NumaMut, 96 B), AoS so
 // one node's state is two contiguous lines.  The NUMA plugin is not monotone (Reserve moves cpus between
@@ -2115,7 +2691,9 @@ struct kg_engine {
   DevBuf<uint64_t> cand;      // [D][B][kCandStride] final merged candidates, by round slot
   DevBuf<uint64_t> out_keys;
   DevBuf<int64_t> cursor;     // [0] cursor, [1] rounds, [2] consumed, [3] poison (int32 in its low word),
-                              // [4] last published resolver sequence, [5] device error (chain wait timed out)
+                              // [4] last published resolver sequence, [5] device error (chain wait timed out),
+                              // [6] pods re-scored on the chain, [7] chain waits on a helper, [8] resolver active
+                              // time (s_memrealtime ticks)
   DevBuf<int32_t> modlists;   // [kMaxDepth][kModListStride]: rows each round modified ([0] = count), by round slot
   // round r runs on rs[r % D] (eval → merge → [RCCL on comms[r % D]] → resolve); `stream` runs ingest
   hipStream_t rs[kMaxDepth] = {};
@@ -2174,6 +2752,13 @@ struct kg_engine {
   bool def_on = false, def_score = false;
   DefParams DF{};
   DevBuf<NodePred> npred;       // [cap] kg_node_predicates
+  // (ABI 11) what the node rows and the staged queue were compiled against (the caller's tables only grow): per node
+  // the highest taint id it carries + 1, and the predicate / image table sizes its row decides; per staged queue the
+  // fewest taints a pod's tolerations were compiled against and the highest predicate / image id + 1 it references
+  std::vector<int16_t> np_taint_top, np_pred_cnt, np_img_cnt;
+  bool np_dirty = true;
+  int64_t np_taint_top_max = 0, np_pred_cnt_min = 64, np_img_cnt_min = 64;
+  int64_t sq_taint_min = 64, sq_pred_top = 0, sq_img_top = 0;
   DevBuf<DefPod> defpods;       // [staged + kMaxB]
   DevBuf<uint32_t> rsv_val2;    // [cap] raw taint count << 24 | raw affinity sum (their Scores on)
   // batched exact rounds (xr_dev.h): kXrPods pods per round
@@ -2995,6 +3580,12 @@ void launch_merge_ranks(kg_engine* e, const RoundGeom& g, int nb, int slot, hipS
                                                   cand_slot(e, g, slot));
 }
 
+// KG_RESOLVER=1wave: the single-wave resolve_round (A/B measurements only; the look-ahead resolver is the default)
+bool resolver_one_wave() {
+  static const bool on = std::getenv("KG_RESOLVER") && std::string(std::getenv("KG_RESOLVER")) == "1wave";
+  return on;
+}
+
 void launch_resolve(kg_engine* e, const RoundGeom& g, int64_t first, int nb, int slot, int n_prev,
                     int64_t seq, int wait, hipStream_t st) {
   if (e->numa_on) {
@@ -3014,11 +3605,27 @@ void launch_resolve(kg_engine* e, const RoundGeom& g, int64_t first, int nb, int
                                                                   e->nq, e->paux.p)
 #define KG_RESOLVE(X) KG_RESOLVE_T(X, false)
 #define KG_RESOLVE_Q(X) KG_RESOLVE_T(X, true)
-  if (e->nq > 0) {
+#define KG_RESOLVE_MW_T(X, Q)                                                                                   \
+  resolve_mw<X, Q><<<1, kMwThreads, mw_lds_bytes(nb), st>>>(e->T, e->pods.p, e->cursor.p, first, nb,              \
+                                                            cand_slot(e, g, slot), e->P, e->out_keys.p,         \
+                                                            e->modlists.p, slot, g.depth, n_prev, poison_ptr(e), \
+                                                            seq, wait, e->quotas.p, e->nq, e->paux.p)
+#define KG_RESOLVE_MW(X) KG_RESOLVE_MW_T(X, false)
+#define KG_RESOLVE_MW_Q(X) KG_RESOLVE_MW_T(X, true)
+  if (!resolver_one_wave()) {
+    if (e->nq > 0) {
+      KG_PF_SWITCH(profile_bits(e->P), KG_RESOLVE_MW_Q)
+    } else {
+      KG_PF_SWITCH(profile_bits(e->P), KG_RESOLVE_MW)
+    }
+  } else if (e->nq > 0) {
     KG_PF_SWITCH(profile_bits(e->P), KG_RESOLVE_Q)
   } else {
     KG_PF_SWITCH(profile_bits(e->P), KG_RESOLVE)
   }
+#undef KG_RESOLVE_MW_Q
+#undef KG_RESOLVE_MW
+#undef KG_RESOLVE_MW_T
 #undef KG_RESOLVE_Q
 #undef KG_RESOLVE_T
 #undef KG_RESOLVE
@@ -3206,6 +3813,8 @@ int prepare_rounds(kg_engine* e, RoundGeom& g) {
   if (!e->numa_on && !e->ds_on && resolve_lds_bytes(g, g.B) > kMaxLds)
     return fail(KG_E_UNSUPPORTED, "resolver LDS %zu B > %zu B: fewer nodes or a smaller batch_pods",
                 resolve_lds_bytes(g, g.B), kMaxLds);
+  if (!e->numa_on && !e->ds_on && mw_lds_bytes(g.B) > kMaxLds)
+    return fail(KG_E_UNSUPPORTED, "resolver LDS %zu B > %zu B: a smaller batch_pods", mw_lds_bytes(g.B), kMaxLds);
   const size_t D = (size_t)g.depth;
   const size_t lists_n = e->lists.n;
   if (int rc = e->lists.ensure(D * g.B * g.nt_local * kR)) return rc;
@@ -3677,8 +4286,8 @@ static int engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank,
   e->T.inv_mem = (double*)(e->cols64.p + 12 * cap);
   e->T.aux = e->cols64.p + 14 * cap;
   e->T.cap = cap;
-  if (int rc = e->cursor.ensure(8)) return bail(rc);
-  if (hipMemsetAsync(e->cursor.p, 0, 8 * 8, e->stream) != hipSuccess) return bail(fail(KG_E_DEVICE, "hipMemset"));
+  if (int rc = e->cursor.ensure(16)) return bail(rc);
+  if (hipMemsetAsync(e->cursor.p, 0, 16 * 8, e->stream) != hipSuccess) return bail(fail(KG_E_DEVICE, "hipMemset"));
   if (int rc = e->modlists.ensure(kMaxDepth * kModListStride)) return bail(rc);
   if (hipMemsetAsync(e->modlists.p, 0, kMaxDepth * kModListStride * 4, e->stream) != hipSuccess) return bail(fail(KG_E_DEVICE, "hipMemset"));
   e->nodes.assign(cap, kg_node{});
@@ -3719,6 +4328,9 @@ static int engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank,
   if (e->def_on) {
     if (int rc = e->npred.ensure(cap)) return bail(rc);
     if (hipMemsetAsync(e->npred.p, 0, cap * sizeof(NodePred), e->stream) != hipSuccess) return bail(fail(KG_E_DEVICE, "hipMemset"));
+    e->np_taint_top.assign(cap, 0);
+    e->np_pred_cnt.assign(cap, 0);
+    e->np_img_cnt.assign(cap, 0);
     if (e->def_score)
       if (int rc = e->rsv_val2.ensure(cap)) return bail(rc);
   }
@@ -3826,7 +4438,11 @@ static int engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank,
 #define KG_ATTR(X)                                                                                           \
   fe = hipFuncSetAttribute((const void*)resolve_round<X, false>, hipFuncAttributeMaxDynamicSharedMemorySize, lds); \
   if (fe == hipSuccess)                                                                                      \
-    fe = hipFuncSetAttribute((const void*)resolve_round<X, true>, hipFuncAttributeMaxDynamicSharedMemorySize, lds)
+    fe = hipFuncSetAttribute((const void*)resolve_round<X, true>, hipFuncAttributeMaxDynamicSharedMemorySize, lds); \
+  if (fe == hipSuccess)                                                                                      \
+    fe = hipFuncSetAttribute((const void*)resolve_mw<X, false>, hipFuncAttributeMaxDynamicSharedMemorySize, lds); \
+  if (fe == hipSuccess)                                                                                      \
+    fe = hipFuncSetAttribute((const void*)resolve_mw<X, true>, hipFuncAttributeMaxDynamicSharedMemorySize, lds)
     KG_PF_SWITCH(profile_bits(e->P), KG_ATTR)
 #undef KG_ATTR
     if (fe != hipSuccess) return bail(fail(KG_E_DEVICE, "hipFuncSetAttribute(resolve_round LDS)"));
@@ -3986,6 +4602,7 @@ int kg_nodes_upsert(kg_engine* e, const kg_node* nodes, const int32_t* idx, int6
     e->n_nodes = std::max<int64_t>(e->n_nodes, i + 1);
   }
   e->static_dirty = true;
+  e->np_dirty = true;
   return 0;
 }
 
@@ -3996,6 +4613,7 @@ int kg_nodes_delete(kg_engine* e, const int32_t* idx, int64_t n) {
     e->nodes[idx[k]].flags &= ~(int64_t)KG_NODE_VALID;
   }
   e->static_dirty = true;
+  e->np_dirty = true;
   return 0;
 }
 
@@ -4193,6 +4811,25 @@ int kg_pods_stage(kg_engine* e, const kg_pod* pods, int64_t n) {
     std::vector<DefPod> hf(std::max<int64_t>(n, 1));
     for (int64_t k = 0; k < n; ++k)
       if (int rc = decode_def_pod(pods[k], hf[k], k)) return rc;
+    int64_t tmin = 64, ptop = 0, itop = 0;  // what the queue was compiled against (ABI 11)
+    for (int64_t k = 0; k < n; ++k) {
+      const kg_pod& q = pods[k];
+      if (q.flags & KG_POD_TAINT_TABLE) {
+        if (q.taint_count < 0 || q.taint_count > 64) return fail(KG_E_INVALID, "pod %lld: taint_count", (long long)k);
+        tmin = std::min<int64_t>(tmin, q.taint_count);
+      }
+      uint64_t used = q.node_selector;
+      for (int t = 0; t < KG_MAX_AFF_TERMS; ++t) {
+        if (t < q.n_required_terms) used |= q.required_terms[t];
+        if (t < q.n_preferred_terms) used |= q.preferred_terms[t];
+      }
+      ptop = std::max<int64_t>(ptop, used ? 64 - __builtin_clzll(used) : 0);
+      for (int c = 0; c < KG_MAX_CONTAINERS && c < q.n_containers; ++c)
+        itop = std::max<int64_t>(itop, q.container_image_bit[c] + 1);
+    }
+    e->sq_taint_min = tmin;
+    e->sq_pred_top = ptop;
+    e->sq_img_top = itop;
     if (int rc = e->defpods.ensure(n + kMaxB)) return rc;
     if (n > 0) HIP_TRY(hipMemcpyAsync(e->defpods.p, hf.data(), n * sizeof(DefPod), hipMemcpyHostToDevice, e->stream));
   }
@@ -4241,9 +4878,38 @@ int kg_pods_schedule_staged(kg_engine* e, int64_t first, int64_t count, kg_stats
   e->pending_place.push_back({first, count, e->clock_now + (e->clock_mode == 0 ? 1 : 0)});
   return e->pm_nodes > 0 ? flush_placements(e) : 0;
 }
+// (ABI 11) the caller's taint / predicate / image tables only grow; rows compiled before an id existed leave it
+// undecided, so a schedule call is refused when the staged queue and the valid node rows disagree on what was compiled
+static int check_predicate_tables(kg_engine* e) {
+  if (!e->def_on) return 0;
+  if (e->np_dirty) {
+    int64_t tt = 0, pc = 64, ic = 64;
+    for (int64_t i = 0; i < e->n_nodes; ++i) {
+      if (!(e->nodes[i].flags & KG_NODE_VALID)) continue;
+      tt = std::max<int64_t>(tt, e->np_taint_top[i]);
+      pc = std::min<int64_t>(pc, e->np_pred_cnt[i]);
+      ic = std::min<int64_t>(ic, e->np_img_cnt[i]);
+    }
+    e->np_taint_top_max = tt, e->np_pred_cnt_min = pc, e->np_img_cnt_min = ic;
+    e->np_dirty = false;
+  }
+  if (e->np_taint_top_max > e->sq_taint_min)
+    return fail(KG_E_INVALID, "TaintToleration: a node row carries taint %lld but a staged pod's tolerations were compiled "
+                "against %lld taints: re-stage the pods", (long long)e->np_taint_top_max - 1, (long long)e->sq_taint_min);
+  if (e->sq_pred_top > e->np_pred_cnt_min)
+    return fail(KG_E_INVALID, "NodeAffinity: the staged pods use predicate %lld but a node row was compiled against %lld "
+                "predicates: re-send the node rows", (long long)e->sq_pred_top - 1, (long long)e->np_pred_cnt_min);
+  if (e->sq_img_top > e->np_img_cnt_min)
+    return fail(KG_E_INVALID, "ImageLocality: the staged pods use image %lld but a node row was compiled against %lld "
+                "images: re-send the node rows", (long long)e->sq_img_top - 1, (long long)e->np_img_cnt_min);
+  return 0;
+}
+
 static int schedule_staged_impl(kg_engine* e, int64_t first, int64_t count, kg_stats* stats) {
   if (!e) return fail(KG_E_INVALID, "engine is NULL");
   if (first < 0 || count < 0 || first + count > e->n_staged) return fail(KG_E_INVALID, "staged range");
+  if (count > 0)
+    if (int rc = check_predicate_tables(e)) return rc;
   const double t0 = now_s();
   // the exact per-pod pass: its profiles, and calls of at most kExactSmall pods of any profile (the drop-in's per-pod
   // scheduleOne): one pass costs less than a round's eval + merge + resolve when a round would hold one pod
@@ -4252,9 +4918,9 @@ static int schedule_staged_impl(kg_engine* e, int64_t first, int64_t count, kg_s
   RoundGeom g;
   if (int rc = prepare_rounds(e, g)) return rc;
   const int64_t end = first + count;
-  const int64_t init[8] = {first, 0, 0, 0, 0, 0, 0, 0};
-  int64_t host_stats[8] = {first, 0, 0, 0, 0, 0, 0, 0};
-  HIP_TRY(hipMemcpyAsync(e->cursor.p, init, 8 * 8, hipMemcpyHostToDevice, e->stream));
+  const int64_t init[16] = {first};
+  int64_t host_stats[16] = {first};
+  HIP_TRY(hipMemcpyAsync(e->cursor.p, init, 16 * 8, hipMemcpyHostToDevice, e->stream));
   HIP_TRY(hipStreamSynchronize(e->stream));
   int64_t cur = first;
   while (cur < end) {
@@ -4265,7 +4931,7 @@ static int schedule_staged_impl(kg_engine* e, int64_t first, int64_t count, kg_s
     const int64_t n_rounds = std::min<int64_t>({(end - cur + g.B - 1) / g.B, kMaxBatchRounds, e->rounds_ahead});
     const int64_t ran0 = host_stats[1];
     if (int rc = e->ds_on ? run_batch_ds(e, g, end, n_rounds) : run_batch(e, g, cur, end, n_rounds)) return rc;
-    HIP_TRY(hipMemcpy(host_stats, e->cursor.p, 8 * 8, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(host_stats, e->cursor.p, 16 * 8, hipMemcpyDeviceToHost));
     if (host_stats[5]) return fail(KG_E_DEVICE, "resolver chain wait timed out (round sequence %lld)", (long long)host_stats[4]);
     const bool stopped = host_stats[0] < std::min<int64_t>(end, cur + n_rounds * g.B);
     const int64_t ran = host_stats[1] - ran0;
@@ -4279,6 +4945,8 @@ static int schedule_staged_impl(kg_engine* e, int64_t first, int64_t count, kg_s
     stats->device_batches = host_stats[1];
     stats->reserved[0] = (double)host_stats[6];  // diagnostics: slow-path pods, speculation steps (resolve_round)
     stats->reserved[1] = (double)host_stats[7];
+    stats->reserved[2] = (double)host_stats[8] * 1e-8;  // resolvers' active time (s_memrealtime, 100 MHz): after the
+                                                         // chain wait to the publish, summed over the call's rounds
     stats->node_evaluations = count * g.N;
     stats->seconds = now_s() - t0;
   }
@@ -4837,11 +5505,23 @@ int kg_nodes_predicates_upsert(kg_engine* e, const kg_node_predicates* p, const 
   if (n == 0) return 0;
   for (int64_t k = 0; k < n; ++k)
     if (idx[k] < 0 || idx[k] >= e->capacity) return fail(KG_E_INVALID, "node index %d outside capacity", idx[k]);
+  std::vector<NodePred> h((size_t)n);
+  for (int64_t k = 0; k < n; ++k) {
+    if (p[k].predicate_count < 0 || p[k].predicate_count > 64 || p[k].image_count < 0 || p[k].image_count > 64)
+      return fail(KG_E_INVALID, "node row %lld: predicate_count / image_count outside [0, 64]", (long long)k);
+    h[k] = NodePred{p[k].predicates, p[k].taints_hard, p[k].taints_soft, p[k].images};
+    const uint64_t t = p[k].taints_hard | p[k].taints_soft;
+    const int i = idx[k];
+    e->np_taint_top[i] = (int16_t)(t ? 64 - __builtin_clzll(t) : 0);
+    e->np_pred_cnt[i] = (int16_t)p[k].predicate_count;
+    e->np_img_cnt[i] = (int16_t)p[k].image_count;
+  }
+  e->np_dirty = true;
   DevBuf<uint8_t> b;
   if (int rc = b.ensure(n * (sizeof(NodePred) + 4))) return rc;
   NodePred* dp = reinterpret_cast<NodePred*>(b.p);
   int32_t* di = reinterpret_cast<int32_t*>(b.p + n * sizeof(NodePred));
-  HIP_TRY(hipMemcpyAsync(dp, p, n * sizeof(NodePred), hipMemcpyHostToDevice, e->stream));
+  HIP_TRY(hipMemcpyAsync(dp, h.data(), n * sizeof(NodePred), hipMemcpyHostToDevice, e->stream));
   HIP_TRY(hipMemcpyAsync(di, idx, n * 4, hipMemcpyHostToDevice, e->stream));
   scatter_rows<NodePred><<<(unsigned)((n + 255) / 256), 256, 0, e->stream>>>(e->npred.p, dp, di, n);
   HIP_TRY(hipGetLastError());

@@ -271,6 +271,9 @@ __device__ __forceinline__ bool xr_reserve(const DevTable& T, RsvNode* __restric
     const NumaStatic nsw = X.ns[w];
     nmw = X.nm[w];
     const NumaView nv = make_view(&nsw, &nmw, X.NP);
+    // X.aff[w] was stored by one lane (the owner's hand-off of pod j's affinity, or rsv_eval_node on a modified row)
+    // and is read here by every lane: a workgroup-scope fence orders that store before these loads
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
     const uint32_t a = X.aff[w];
     const NumaHint aff{a & 0xFFu, (int)((a >> 8) & 1u), 0, 0};
     const bool ok = numa_reserve(nsw, nmw, nv, X.npods[j], aff, cpus, rec);

@@ -32,15 +32,27 @@ NO_SCHEDULE, PREFER_NO_SCHEDULE, NO_EXECUTE = "NoSchedule", "PreferNoSchedule", 
 MAX_IDS = 64
 
 
+_INT64_MIN, _INT64_MAX = -(1 << 63), (1 << 63) - 1
+
+
 def _parse_int(s):
-    try:
-        return int(s, 10)
-    except (TypeError, ValueError):
+    """strconv.ParseInt(s, 10, 64) as labels.Requirement.Matches uses it for Gt / Lt: an optional sign and decimal
+    digits only (no underscores, spaces or '0x'), within int64; anything else is a parse error (None)."""
+    if not isinstance(s, str) or not s:
         return None
+    body = s[1:] if s[0] in "+-" else s
+    if not body or not all("0" <= ch <= "9" for ch in body):
+        return None
+    v = int(s, 10)
+    return v if _INT64_MIN <= v <= _INT64_MAX else None
 
 
 class PredicateTable:
-    """The caller's taint and predicate id tables (at most 64 each)."""
+    """The caller's taint and predicate id tables (at most 64 each).  The tables only grow, and a row compiled earlier
+    stays right for the ids that existed then: a node row decides the predicates interned before it (predicate_count),
+    a pod's tolerated mask the taints interned before it (taint_count, KG_POD_TAINT_TABLE).  The engine refuses a
+    schedule call whose queue references a predicate some node row was compiled without, or whose node rows carry a
+    taint some pod was compiled without (ABI 11): re-send the node rows / re-stage the pods after the table grows."""
 
     def __init__(self):
         self.taints: list[tuple] = []
@@ -111,6 +123,7 @@ class PredicateTable:
             elif eff in (NO_SCHEDULE, NO_EXECUTE):
                 hard |= bit
         r["predicates"], r["taints_hard"], r["taints_soft"] = m, hard, soft
+        r["predicate_count"] = len(self.preds)  # ABI 11: predicates interned later are undecided on this row
         return r
 
     # ---- pods (per staging: evaluated against the taints interned so far) ----
@@ -142,10 +155,19 @@ class PredicateTable:
         required_terms: the NodeSelectorTerms of requiredDuringScheduling (None = not set; [] = set with no terms,
         which matches no node); preferred: [(weight, term)]."""
         row = pod[0] if pod.shape else pod
-        tol = 0
-        for t_id, taint in enumerate(self.taints):
-            if any(self.tolerates(t, taint) for t in tolerations or ()):
-                tol |= 1 << t_id
+        tols = list(tolerations or ())
+        flags = int(row["flags"]) & ~abi.POD_TAINT_TABLE
+        if any(not t.get("key") and t.get("operator") == "Exists" and not t.get("effect") for t in tols):
+            tol = (1 << 64) - 1  # tolerates every taint, including ones interned later
+        else:
+            tol = 0
+            for t_id, taint in enumerate(self.taints):
+                if any(self.tolerates(t, taint) for t in tols):
+                    tol |= 1 << t_id
+            if tols:  # decided for the taints interned so far only (ABI 11: the engine checks it against node rows)
+                flags |= abi.POD_TAINT_TABLE
+                row["taint_count"] = len(self.taints)
+        row["flags"] = flags
         sel = 0
         for k, v in (node_selector or {}).items():
             sel |= 1 << self.pred_id("label", k, "In", (v,))
@@ -224,8 +246,12 @@ class ImageTable:
             row["container_image_score"][c] = self.scaled(nm)
         return pod
 
+    def image_count(self) -> int:
+        """kg_node_predicates.image_count of a row whose mask node_mask() computes now (ABI 11)."""
+        return len(self.bits)
+
     def node_mask(self, i: int) -> int:
-        """kg_node_predicates.images of node i over the bits assigned so far."""
+        """kg_node_predicates.images of node i over the bits assigned so far (decided for ids < image_count())."""
         m = 0
         for nm, b in self.bits.items():
             if nm in self.node_names[i]:

@@ -578,4 +578,5 @@ def make_images(n_nodes: int, pods: np.ndarray, preds: np.ndarray, seed: int = B
                 cont.append(f"registry.local/app-{k}" if k % 4 == 0 and rng.random() < 0.5 else catalog[k][0][0])
         table.fill_pod(pods[j:j + 1], cont)
     preds["images"] = [table.node_mask(i) for i in range(n_nodes)]
+    preds["image_count"] = table.image_count()
     return table

@@ -43,6 +43,16 @@ def _pod():
     ({}, E("a", "Lt", ["9"]), False),
     ({"a": "-3"}, E("a", "Lt", ["2"]), True),
     ({"a": "1"}, E("a", "Bogus", ["1"]), False),  # unknown operator
+    # strconv.ParseInt(s, 10, 64): no underscores, spaces or hex; int64 range
+    ({"a": "1_0"}, E("a", "Gt", ["9"]), False),
+    ({"a": "10"}, E("a", "Gt", ["0_9"]), False),
+    ({"a": " 10"}, E("a", "Gt", ["9"]), False),
+    ({"a": "0x10"}, E("a", "Gt", ["9"]), False),
+    ({"a": "+10"}, E("a", "Gt", ["9"]), True),
+    ({"a": "99999999999999999999"}, E("a", "Gt", ["9"]), False),  # 20 digits: out of int64
+    ({"a": "9223372036854775807"}, E("a", "Gt", ["9"]), True),
+    ({"a": "-9223372036854775808"}, E("a", "Lt", ["0"]), True),
+    ({"a": "-9223372036854775809"}, E("a", "Lt", ["0"]), False),
 ])
 def test_requirement_operators(labels, req, want):
     t = PredicateTable()
@@ -298,6 +308,47 @@ def test_single_pod_calls_and_predicate_updates():
 
 
 @pytest.mark.gpu
+def test_table_growth_refused_until_recompiled():
+    """ABI 11: the caller's taint / predicate tables only grow, and a row compiled before an id existed
+    leaves it undecided.  A node row carrying a taint the staged pods' tolerations were not compiled against, or a
+    staged pod using a predicate the node rows were not compiled against, makes the schedule call fail loudly until
+    the pods are re-staged / the rows re-sent; a tolerate-all pod (no key, Exists, no effect) holds for any taint."""
+    cfg = F.build_config(profile=STOCK)
+    cluster = synth.make_cluster(500, seed=61)
+    pods = synth.make_pods(200, seed=62)
+    table, preds = synth.make_predicates(500, pods, seed=63)
+    assert ((pods["flags"] & abi.POD_TAINT_TABLE) != 0).any()
+    assert (pods["tolerated_taints"] == np.uint64((1 << 64) - 1)).any()  # tolerate-all pods, no table flag
+    with Engine(cfg, cluster.n) as e:
+        synth.load_into(e, cluster)
+        e.upsert_predicates(preds)
+        e.stage(pods)
+        e.schedule_staged(0, 50)
+        t_new = table.taint_id("fresh", "x", NO_SCHEDULE)  # a node gains a taint the pods were not compiled against
+        row = preds[7:8].copy()
+        row["taints_hard"] |= np.uint64(1 << t_new)
+        e.upsert_predicates(row, np.array([7], dtype=np.int32))
+        with pytest.raises(abi.KoordGPUError, match="re-stage"):
+            e.schedule_staged(50, 10)
+        pods2 = pods.copy()  # re-compiled: no toleration of these pods names "fresh"
+        dep = (pods2["flags"] & abi.POD_TAINT_TABLE) != 0
+        pods2["taint_count"][dep] = len(table.taints)
+        e.stage(pods2)
+        e.schedule_staged(50, 10)
+        extra = pods2[60:61].copy()  # a pod interns a predicate the node rows were not compiled against
+        table.fill_pod(extra, node_selector={"fresh-label": "y"})
+        e.stage(np.concatenate([pods2[:60], extra]))
+        with pytest.raises(abi.KoordGPUError, match="re-send the node rows"):
+            e.schedule_staged(60, 1)
+        rows2 = preds.copy()  # no node has the label: recompiled rows decide the predicate as not holding
+        rows2["taints_hard"][7] = row["taints_hard"][0]
+        rows2["predicate_count"] = len(table.preds)
+        e.upsert_predicates(rows2)
+        node, _, _ = e.schedule(extra)
+        assert node[0] == -1
+
+
+@pytest.mark.gpu
 def test_shipped_profile_with_stock_defaults():
     """The shipped koord profile plus the upstream defaults a v1beta2 profile keeps (weights 1)."""
     import test_shipped_profile as S
@@ -365,6 +416,7 @@ def test_image_locality_cases(node_images, containers, want):
     pod = t.fill_pod(_pod(), containers)
     rows = np.zeros(len(node_images), dtype=abi.NODE_PRED_DTYPE)
     rows["images"] = [t.node_mask(i) for i in range(len(node_images))]
+    rows["image_count"] = t.image_count()
     got = [oracle.default_plugins(rows[i], pod)["image_score"] for i in range(len(node_images))]
     assert got == want
 
