@@ -408,7 +408,7 @@ def main():
             cpu["nproc_threads"] = {"value": mn / dtn, "threads": nproc, "sample_pods": mn}
 
     tfile = args.traffic_file or next((f for f in (os.path.join(ROOT, "profiles", r, f"traffic_{wl}.json")
-                                                   for r in ("r03", "r02")) if os.path.exists(f)),
+                                                   for r in ("r04", "r03", "r02")) if os.path.exists(f)),
                                       os.path.join(ROOT, "profiles", "r02", f"traffic_{wl}.json"))
     # live timing folds every wide pass under one name: the kernel rocprof sees
     pmc_name = {"c4": "eval_round_numa", "c5": "xr_eval", "c5r": "xr_eval", "shipped": "xr_eval"}.get(wl, dom)
@@ -448,7 +448,7 @@ def main():
                        "8 GPUs (30%% with 1-4 cpu/memory reservations), %d-pod FIFO queue (70%% cpuset LSR/LSE, 30%% "
                        "GPU-share, 20%% reservation-owned, 80%% in 16 ElasticQuota groups), NodeResourcesFit+"
                        "LoadAwareScheduling+NodeNUMAResource+DeviceShare+Reservation (w 1/1/1/1/5000)+ElasticQuota, "
-                       "one pod per device pass, %d pods per step",
+                       "batched exact rounds of 32 pods, %d pods per step",
             "c3": "C3 cluster: %d nodes, %d-pod FIFO queue, NodeResourcesFit+LoadAwareScheduling, %d pods per step",
             "c4": "C4 cluster: %d 2-socket 256-cpu nodes (node count: builder's choice, BASELINE names none), "
                   "%d-pod FIFO queue (70%% cpuset LSR/LSE), NodeResourcesFit+LoadAwareScheduling+NodeNUMAResource, "
@@ -458,10 +458,10 @@ def main():
             "c5": "C5 (one profile): %d nodes x 8 GPUs (30%% with 1-4 cpu/memory reservations, 64 owner groups), "
                   "%d-pod FIFO queue (30%% GPU-share, 20%% reservation-owned, 80%% in 16 ElasticQuota groups), "
                   "NodeResourcesFit+LoadAwareScheduling+Reservation (w 5000)+DeviceShare+ElasticQuota admission, "
-                  "one pod per device pass, %d pods per step",
+                  "batched exact rounds of 32 pods, %d pods per step",
             "c5r": "C5 (Reservation part): %d nodes (30%% with 1-4 reservations), %d-pod FIFO queue (20%% "
-                   "reservation-owned), NodeResourcesFit+LoadAwareScheduling+Reservation (w 5000), one pod per device "
-                   "pass, %d pods per step",
+                   "reservation-owned), NodeResourcesFit+LoadAwareScheduling+Reservation (w 5000), batched exact "
+                   "rounds of 32 pods, %d pods per step",
         }[wl] % (cluster.n, total, args.pods_per_step)
         out = {
             "metric": {"c3": "pods scheduled/sec at 100k nodes (node-evals/sec alongside)",
@@ -486,7 +486,9 @@ def main():
             "data": "synthetic (SURVEY §8d generator, seed %d)" % work.seed,
             "config": {"workload": desc, "nodes": cluster.n, "pods": total, "batch_pods": args.batch,
                        "pods_per_wave": args.pods_per_wave, "pipeline_depth": args.depth or "default",
-                       "parallelism": "node-sharded x%d (replicated table, RCCL all-gather)" % d.world},
+                       "parallelism": (("replicas x%d (exact profile: every rank evaluates its full replica, no "
+                                        "exchange)" % d.world) if rsv_path else
+                                       "node-sharded x%d (replicated table, RCCL all-gather)" % d.world)},
             "node_evals_per_sec": pods_s * cluster.n,
             "placed": placed,
             "device_rounds": rounds,

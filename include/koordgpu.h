@@ -122,8 +122,10 @@ enum {
   KG_REJECT_INVALID_NODE = 1 << 4,  /* deleted / never-upserted slot                   */
   KG_REJECT_NUMA = 1 << 5,          /* NodeNUMAResource (topology, cpuset, NUMA admit) */
   KG_REJECT_DEVICE = 1 << 6,        /* DeviceShare (Insufficient gpu devices)          */
-  KG_REJECT_FIT_OTHER = 1 << 7      /* NodeResourcesFit: Insufficient ephemeral-storage / a scalar resource
+  KG_REJECT_FIT_OTHER = 1 << 7,     /* NodeResourcesFit: Insufficient ephemeral-storage / a scalar resource
                                        (KG_RES_EPHEMERAL .. KG_RES_MID_MEMORY; reservation/plugin.go:469-479) */
+  KG_REJECT_RESERVATION = 1 << 8    /* (ABI 11) Reservation Filter (kg_pods_filter_preemption): preemption failed /
+                                       no reservation meets the requirements / reservation affinity */
 };
 
 /* node flags */
@@ -566,6 +568,18 @@ int kg_results_fetch_reservations(kg_engine* e, int64_t first, int64_t count, in
  * reservation-order label among the matched slots (0 none), [15] reserved. */
 #define KG_RSV_EVAL_WORDS 16
 int kg_pods_evaluate_reservation(kg_engine* e, const kg_pod* pod, int64_t* out);
+
+/* (ABI 11) The preemption dry run's Filter of one pod on one node (PostFilter → defaultpreemption SelectVictimsOnNode
+ * → RunFilterPluginsWithNominatedPods; replaces one Filter round of the Go dry run): the pod's Filters on node
+ * node_idx of a NodeInfo copy with the n_victims pods `victims` removed (NodeInfo.RemovePod) and the Reservation
+ * plugin's PreFilterExtensions.RemovePod applied (reservation/plugin.go:284-310: a victim's requests add to
+ * state.preemptible[node], or to state.preemptibleInRRs[node][its reservation] when victim_slot[k] >= 0 names the
+ * node's reservation slot it was allocated from; NULL = none).  The Reservation Filter then fits the pod against them
+ * (plugin.go:357-428, fitsNode :433-482).  out_reject: 0 = every enabled Filter passes, else KG_REJECT_* bits.
+ * Profiles with NodeResourcesFit / LoadAwareScheduling / Reservation; NodeNUMAResource, DeviceShare and the upstream
+ * defaults are refused (KG_E_UNSUPPORTED: the victims' cpusets / devices / labels are not modelled here). */
+int kg_pods_filter_preemption(kg_engine* e, const kg_pod* pod, int32_t node_idx, const kg_pod* victims,
+                              const int32_t* victim_slot, int64_t n_victims, int32_t* out_reject);
 
 /* ElasticQuota admission (engines whose pods carry quota_id): replaces the quota table (n ≤ KG_MAX_QUOTAS).
  * Every scheduled pod runs PreFilter's check (used + request ≤ used_limit over the pod's cpu/memory requests; for

@@ -55,6 +55,7 @@ REJECT_DEVICE = 64
 RSV_EVAL_WORDS = 16  # KG_RSV_EVAL_WORDS: kg_pods_evaluate_reservation per node
 DBG_MERGE_WORDS = 32  # KG_DBG_MERGE_WORDS: one kg_debug_numa_merge case
 REJECT_FIT_OTHER = 128  # NodeResourcesFit: ephemeral-storage / a scalar resource (RES_EPHEMERAL .. RES_MID_MEMORY)
+REJECT_RESERVATION = 256  # Reservation Filter (kg_pods_filter_preemption)
 # DeviceShare device resources (KG_DEV_*)
 DEV_RES_MAX, MAX_MINORS = 8, 8
 MAX_AFF_TERMS = 4  # KG_MAX_AFF_TERMS
@@ -191,7 +192,7 @@ EXPORTED_SYMBOLS = (
     "kg_results_fetch_reservations", "kg_profile_enable", "kg_profile_read", "kg_loopback_create",
     "kg_loopback_destroy", "kg_engine_create_loopback", "kg_pods_unreserve", "kg_engine_set_clock",
     "kg_node_pods_metric_set", "kg_debug_numa_merge", "kg_pods_evaluate_reservation", "kg_nodes_predicates_upsert",
-    "kg_engine_create_hosted",
+    "kg_engine_create_hosted", "kg_pods_filter_preemption",
 )
 
 # int (*kg_exchange_fn)(void* user, const void* send, void* recv, int64_t bytes)
@@ -270,6 +271,7 @@ def load_library(path: str | None = None):
         "kg_engine_set_clock": (i, [vp, i64]),
         "kg_debug_numa_merge": (i, [vp, vp, i64, vp]),
         "kg_pods_evaluate_reservation": (i, [vp, vp, vp]),
+        "kg_pods_filter_preemption": (i, [vp, vp, ctypes.c_int32, vp, vp, i64, vp]),
         "kg_nodes_predicates_upsert": (i, [vp, vp, vp, i64]),
         "kg_engine_create_hosted": (i, [vp, i64, i, i, EXCHANGE_FN, vp, ctypes.POINTER(vp)]),
     }

@@ -284,7 +284,8 @@ __global__ __launch_bounds__(kMergeThreads) void merge_round(DevTable T, EvalPar
                                                              const uint64_t* __restrict__ in, int64_t pod_stride,
                                                              int64_t list_stride, int n_lists, int list_len,
                                                              int nb, const int32_t* __restrict__ poison,
-                                                             uint64_t* __restrict__ out) {
+                                                             uint64_t* __restrict__ out,
+                                                             uint32_t* __restrict__ done_cnt) {
   __shared__ uint32_t hist[1 << kHistBits];
   __shared__ __attribute__((aligned(16))) uint64_t sel[kC];
   __shared__ uint64_t red64[kMergeThreads / kWave];
@@ -292,10 +293,14 @@ __global__ __launch_bounds__(kMergeThreads) void merge_round(DevTable T, EvalPar
   __shared__ uint64_t sh_prefix;
   __shared__ uint32_t sh_target;
   KG_STAMP(1, 0);
-  if (*poison) return;
   const int pod = blockIdx.x;
-  if (pod >= nb) return;
   const int tid = threadIdx.x, lane = tid % kWave, wave = tid / kWave;
+  // done_cnt (round engines): every block of the grid counts itself once its record is written (or skipped), so the
+  // round's resolver — dispatched ahead on its own stream — knows when the records are there
+  if (*poison || pod >= nb) {
+    if (tid == 0 && done_cnt) atomicAdd(done_cnt, 1u);
+    return;
+  }
   const uint64_t* base = in + (size_t)pod * pod_stride;
 
   // Keys held in registers: thread t owns chunks c = t + kMergeThreads*i of 8 consecutive keys (chunk order
@@ -532,6 +537,11 @@ __global__ __launch_bounds__(kMergeThreads) void merge_round(DevTable T, EvalPar
       for (int w = 0; w < kEvalRowWords; ++w) dst[w] = words[w];
     }
   }
+  if (done_cnt) {
+    __threadfence();
+    __syncthreads();
+    if (tid == 0) atomicAdd(done_cnt, 1u);
+  }
   KG_STAMP(1, 14);
 }
 
@@ -580,6 +590,19 @@ __device__ __forceinline__ int mod_insert(uint32_t* h, uint32_t node, int slot) 
 __device__ __forceinline__ void publish_round(int64_t* ctl, int64_t seq) {
   __threadfence();
   if (threadIdx.x == 0) __hip_atomic_store(&ctl[4], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// The round's records: each merge_round block adds 1 to *rec_cnt once its record is written; the resolver, dispatched
+// ahead on its own stream, waits for the batch's cumulative count (nullptr: stream order already guarantees them).
+// Bounded spin: 1 = timed out (reported as a device error).
+__device__ __forceinline__ int wait_records(const uint32_t* rec_cnt, uint32_t target) {
+  if (!rec_cnt) return 0;
+  int64_t it = 0;
+  while (__hip_atomic_load(rec_cnt, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < target) {
+    __builtin_amdgcn_s_sleep(1);
+    if (++it > kSpinLimit) return 1;
+  }
+  return 0;
 }
 
 // exact key of one modified row for pod p (0 = filtered out).  A row outside eval_fast's domain takes the
@@ -769,12 +792,24 @@ __global__ __launch_bounds__(kWave) void resolve_round(DevTable T0, const DevPod
                                                         int32_t* __restrict__ modlists, int slot, int depth,
                                                         int n_prev, int32_t* __restrict__ poison, int64_t seq,
                                                         int wait, QuotaRow* __restrict__ quotas, int nq,
-                                                        const int64_t* __restrict__ paux) {
+                                                        const int64_t* __restrict__ paux,
+                                                        const uint32_t* __restrict__ rec_cnt, uint32_t rec_target) {
   extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
   KG_STAMP(2, 0);
   const int lane = threadIdx.x;
   // the serial chain outranks the wide pass's waves when they share a SIMD
   __builtin_amdgcn_s_setprio(3);
+  {
+    int to = 0;
+    if (lane == 0) to = wait_records(rec_cnt, rec_target);
+    to = __builtin_amdgcn_readfirstlane(to);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    if (to) {
+      if (lane == 0) ctl[5] = 1, *poison = 1;
+      publish_round(ctl, seq);
+      return;
+    }
+  }
   uint64_t* s_cand = smem;                                            // [nb][kCandStride]
   uint64_t* s_podw = s_cand + (size_t)nb * kCandStride;               // [nb] DevPod (kPodWords words)
   uint64_t* s_par = s_podw + (size_t)nb * kPodWords;                  // [kParWords] EvalParams (rare-path copy)
@@ -830,6 +865,8 @@ __global__ __launch_bounds__(kWave) void resolve_round(DevTable T0, const DevPod
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   }
   KG_STAMP(2, 1);
+  // the period decomposition's resolver time: from the predecessor's hand-off (modified-row loads included)
+  const uint64_t t_active = __builtin_amdgcn_s_memrealtime();
   if (timed_out || *poison || ctl[0] != first) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the LDS-DMA lands before the wave retires
     if (lane == 0 && timed_out) ctl[5] = 1;
@@ -879,19 +916,6 @@ __global__ __launch_bounds__(kWave) void resolve_round(DevTable T0, const DevPod
   // which the next pod patches with last_w)
   uint64_t key = s_cand[lane];
   uint64_t ub = s_cand[kC];
-  // pod records come through the scalar cache (wave-uniform, straight into scalar registers; no LDS round trip and
-  // no v_readfirstlane on the chain); the LDS copy serves the lane-parallel epilogue
-  typedef const __attribute__((address_space(4))) uint64_t* const_u64_ptr;  // constant address space: s_load
-  const const_u64_ptr gpods = (const_u64_ptr)(uintptr_t)(pods + first);
-  auto pod_at = [&](int q) {
-    uint64_t w[kPodWords];
-#pragma unroll
-    for (int k = 0; k < kPodWords; ++k) w[k] = gpods[(size_t)q * kPodWords + k];
-    DevPod d;
-    __builtin_memcpy(&d, w, sizeof(d));
-    return d;
-  };
-
   uint32_t word = bitmap[key ? key_node(key) >> 5 : 0u];
   uint64_t key_n = s_cand[(size_t)(nb > 1 ? 1 : 0) * kCandStride + lane];
   uint32_t diag = 0;
@@ -903,7 +927,7 @@ __global__ __launch_bounds__(kWave) void resolve_round(DevTable T0, const DevPod
     const uint32_t word_n = bitmap[key_n ? key_node(key_n) >> 5 : 0u];
     const uint64_t ub_n = s_cand[(size_t)j1 * kCandStride + kC];
     const uint64_t key_nn = s_cand[(size_t)j2 * kCandStride + lane];
-    const DevPod p = pod_at(j);  // scalar cache: the queue is read in order, so the line is usually warm
+    const DevPod p = s_pods[j];  // (r4) from the LDS copy: a scalar load on the chain made every LDS wait wait for it
     const uint32_t node = key_node(key);  // key 0 → node 0xFFFFFFFF: masked below
     const bool unmod = (key != 0) & !((word >> (node & 31)) & 1u) & (node != last_w);
     bool placed = false;
@@ -994,6 +1018,7 @@ __global__ __launch_bounds__(kWave) void resolve_round(DevTable T0, const DevPod
     ctl[2] += consumed;
     ctl[6] += n_slow;  // diagnostics: pods that re-scored modified rows
     if (consumed < nb) *poison = 1;
+    ctl[8] += (int64_t)(__builtin_amdgcn_s_memrealtime() - t_active);
   }
   publish_round(ctl, seq);
   KG_STAMP(2, 31);
@@ -1058,14 +1083,22 @@ inline size_t mw_lds_bytes(int nb) {
   return (size_t)L.u64_end * 8 + (size_t)L.u32_end * 4;
 }
 
+// Hand-offs between the resolver's waves go through LDS only, and the LDS serves one wave's DS instructions in issue
+// order: a flag written after the data it guards is seen by another wave only after that data, and that wave's data
+// reads issued after it saw the flag are served after the writes.  So publishing needs no s_waitcnt (lds_rel: a
+// compiler barrier, then the store) and observing needs none either (lds_acq: the load, then a compiler barrier) —
+// the release / acquire fences would stall the chain on its own outstanding LDS traffic for nothing.
 __device__ __forceinline__ uint32_t lds_ld(const uint32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 __device__ __forceinline__ uint32_t lds_acq(const uint32_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  const uint32_t v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  asm volatile("" ::: "memory");
+  return v;
 }
 __device__ __forceinline__ void lds_rel(uint32_t* p, uint32_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  asm volatile("" ::: "memory");
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 __device__ __forceinline__ int mod_lookup(const uint32_t* h, uint32_t node) {
   uint32_t i = mod_hash(node);
@@ -1108,11 +1141,23 @@ __global__ __launch_bounds__(kMwThreads) void resolve_mw(DevTable T0, const DevP
                                                          int32_t* __restrict__ modlists, int slot, int depth,
                                                          int n_prev, int32_t* __restrict__ poison, int64_t seq,
                                                          int wait, QuotaRow* __restrict__ quotas, int nq,
-                                                         const int64_t* __restrict__ paux) {
+                                                         const int64_t* __restrict__ paux,
+                                                         const uint32_t* __restrict__ rec_cnt, uint32_t rec_target) {
   extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
   KG_STAMP(2, 0);
   const MwLayout L = mw_layout(nb);
   const int tid = threadIdx.x, lane = tid % kWave, wave = tid / kWave;
+  {  // every wave waits for the round's records itself (a timeout is the same on every wave: the round is abandoned)
+    int to = 0;
+    if (lane == 0) to = wait_records(rec_cnt, rec_target);
+    to = __builtin_amdgcn_readfirstlane(to);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    if (to) {
+      if (tid == 0) ctl[5] = 1, *poison = 1;
+      if (wave == 0) publish_round(ctl, seq);
+      return;
+    }
+  }
   if (wave == 0) __builtin_amdgcn_s_setprio(3);  // the chain first, then its helpers, then any wide-pass wave
   else __builtin_amdgcn_s_setprio(2);
   uint64_t* s_cand = smem + L.cand;
@@ -1685,9 +1730,21 @@ __global__ __launch_bounds__(kWave) void resolve_round_numa(DevTable T, NumaTabl
                                                              uint64_t* __restrict__ out_cpus,
                                                              int64_t* __restrict__ out_nrec, int bitmap_words,
                                                              int32_t* __restrict__ poison, int64_t seq,
-                                                             QuotaRow* __restrict__ quotas, int nq) {
+                                                             QuotaRow* __restrict__ quotas, int nq,
+                                                             const uint32_t* __restrict__ rec_cnt, uint32_t rec_target) {
   extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
   const int lane = threadIdx.x;
+  {
+    int to = 0;
+    if (lane == 0) to = wait_records(rec_cnt, rec_target);
+    to = __builtin_amdgcn_readfirstlane(to);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    if (to) {
+      if (lane == 0) ctl[5] = 1, *poison = 1;
+      publish_round(ctl, seq);
+      return;
+    }
+  }
   uint64_t* s_cand = smem;                                    // [nb][kCandStride]
   uint64_t* s_podw = s_cand + (size_t)nb * kCandStride;       // [nb] DevPod
   uint64_t* s_npw = s_podw + (size_t)nb * kPodWords;          // [nb] NumaPod
@@ -1707,6 +1764,7 @@ __global__ __launch_bounds__(kWave) void resolve_round_numa(DevTable T, NumaTabl
     publish_round(ctl, seq);
     return;
   }
+  const uint64_t t_active = __builtin_amdgcn_s_memrealtime();  // the period decomposition's resolver time
   const DevPod* s_pods = reinterpret_cast<const DevPod*>(s_podw);
   const NumaPod* s_np = reinterpret_cast<const NumaPod*>(s_npw);
   NumaStatic* s_ns = reinterpret_cast<NumaStatic*>(s_nsw);
@@ -1845,6 +1903,7 @@ __global__ __launch_bounds__(kWave) void resolve_round_numa(DevTable T, NumaTabl
     ctl[1] += 1;
     ctl[2] += consumed;
     if (consumed < nb) *poison = 1;
+    ctl[8] += (int64_t)(__builtin_amdgcn_s_memrealtime() - t_active);
   }
   publish_round(ctl, seq);
 }
@@ -2084,6 +2143,7 @@ __global__ __launch_bounds__(kWave) void resolve_round_ds(DevTable T, DsTable DT
   int64_t first;
   int nb;
   if (!ds_round_range(ctl, end, B, first, nb)) return;
+  const uint64_t t_active = __builtin_amdgcn_s_memrealtime();  // the period decomposition's resolver time
   uint64_t* s_cand = smem;                                  // [nb][kCandStride]
   uint64_t* s_podw = s_cand + (size_t)nb * kCandStride;     // [nb] DevPod
   uint64_t* s_dpw = s_podw + (size_t)nb * kPodWords;        // [nb] DsPod
@@ -2288,6 +2348,7 @@ __global__ __launch_bounds__(kWave) void resolve_round_ds(DevTable T, DsTable DT
     ctl[0] = first + consumed;
     ctl[1] += 1;
     ctl[2] += consumed;
+    ctl[8] += (int64_t)(__builtin_amdgcn_s_memrealtime() - t_active);
   }
 }
 
@@ -2324,6 +2385,101 @@ __global__ void evaluate_pod_rsv(DevTable T, const RsvNode* __restrict__ RN, con
   w[13] = o.feas ? o.dsraw : 0;
   w[14] = o.order == 0x7fffffff ? 0 : o.order;
   w[15] = 0;
+}
+
+// kg_pods_filter_preemption: the preemption dry run's Filter of one pod on one node (one thread): the restored node
+// minus the victims (NodeInfo.RemovePod), NodeResourcesFit + LoadAware on it, and the Reservation Filter with the
+// victims' requests as preemptible (reservation/plugin.go:284-310 RemovePod, :357-428 Filter, :433-482 fitsNode)
+struct Victim {
+  int64_t req_cpu, req_mem, nz_cpu, nz_mem;
+  int32_t slot;     // the node's reservation slot the victim was allocated from, -1 = none
+  int32_t nonzero;  // !quotav1.IsZero(PodRequestsAndLimits): RemovePod records it
+};
+__global__ void filter_pod_preempt(DevTable T, const RsvNode* __restrict__ RN, const int32_t* __restrict__ rsv_n,
+                                   int64_t i, const DevPod* __restrict__ pod, RsvPod rp, EvalParams P, RsvParams RP,
+                                   int rsv_on, const Victim* __restrict__ vic, int64_t n_vic, int32_t* __restrict__ out) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  const DevPod p = *pod;
+  Row r = load_row(T, i);
+  if (!(r.flags & F_VALID)) {
+    *out = KG_REJECT_INVALID_NODE;
+    return;
+  }
+  uint32_t mm = 0;
+  int nm = 0;
+  int64_t pr_c = 0, pr_m = 0, ra_c = 0, ra_m = 0;
+  bool has_state = false;
+  const int ns = rsv_on ? rsv_n[i] : 0;
+  RsvNode rn;
+  if (ns > 0) {
+    rn = RN[i];
+    rsv_restore(rn, ns, rp, r, mm, nm, pr_c, pr_m, ra_c, ra_m, has_state);
+  }
+  int64_t pre_c = 0, pre_m = 0, rr_c[kRsvSlots] = {}, rr_m[kRsvSlots] = {};
+  bool pre_set = false;
+  uint32_t rr_set = 0;
+  for (int64_t k = 0; k < n_vic; ++k) {
+    const Victim v = vic[k];
+    r.req_cpu -= v.req_cpu;
+    r.req_mem -= v.req_mem;
+    r.nz_cpu -= v.nz_cpu;
+    r.nz_mem -= v.nz_mem;
+    r.num_pods -= 1;
+    if (!v.nonzero) continue;
+    if (v.slot >= 0 && v.slot < kRsvSlots) {
+      rr_c[v.slot] += v.req_cpu;
+      rr_m[v.slot] += v.req_mem;
+      rr_set |= 1u << v.slot;
+    } else {
+      pre_c += v.req_cpu;
+      pre_m += v.req_mem;
+      pre_set = true;
+    }
+  }
+  uint32_t rej = 0;
+  int64_t t = 0;
+  (void)eval_node(r, p, P, t, &rej);  // NodeResourcesFit + LoadAware Filter verdicts on the victim-free NodeInfo
+  if (rsv_on && RP.filter) {
+    const bool required = (rp.flags & RP_AFFINITY) != 0;
+    const bool zero = p.req_cpu == 0 && p.req_mem == 0;
+    // fitsNode with rInfo = slot s (s < 0: nil) and preemptible (pc, pm); a node without state has no podRequested
+    auto fits_node = [&](int s, int64_t pc, int64_t pm) {
+      if (r.num_pods - nm + 1 > r.alloc_pods) return false;
+      if (zero) return true;
+      const int64_t rc = s >= 0 ? rsv_nn(rn.alloc_cpu[s], rn.allocd_cpu[s]) : 0;
+      const int64_t rm = s >= 0 ? rsv_nn(rn.alloc_mem[s], rn.allocd_mem[s]) : 0;
+      const int64_t prc = has_state ? pr_c : 0, prm = has_state ? pr_m : 0;
+      return !(p.req_cpu > r.alloc_cpu - (prc - rc - ra_c - pc)) && !(p.req_mem > r.alloc_mem - (prm - rm - ra_m - pm));
+    };
+    bool ok = true;
+    if (mm == 0 || !has_state) {
+      if (required) ok = false;
+      else if (pre_set || rr_set) ok = fits_node(-1, pre_c, pre_m);
+    } else {
+      const bool kc = (p.flags & P_CPU_KEY) != 0, km = (p.flags & P_MEM_KEY) != 0;
+      bool sat = false;
+      for (int s = 0; s < kRsvSlots && !sat; ++s) {
+        if (!(mm >> s & 1)) continue;
+        const bool hc = rn.alloc_cpu[s] > 0, hm = rn.alloc_mem[s] > 0;
+        if (!((kc && hc) || (km && hm))) continue;  // Intersection(rInfo.ResourceNames, pod request names) empty
+        const bool fits = fits_node(s, rr_c[s] + pre_c, rr_m[s] + pre_m);
+        if (((rn.meta[s] >> 4) & 3) == KG_RSV_POLICY_RESTRICTED) {
+          int64_t ac = rn.allocd_cpu[s], am = rn.allocd_mem[s];
+          if (rr_set >> s & 1) {  // Allocated − preemptibleInRR, non-negative, masked to the reservation's keys
+            ac = hc ? rsv_nn(ac, rr_c[s]) : 0;
+            am = hm ? rsv_nn(am, rr_m[s]) : 0;
+          }
+          const int64_t rc = rsv_nn(rn.alloc_cpu[s], ac), rm = rsv_nn(rn.alloc_mem[s], am);
+          sat = fits && (!hc || !kc || p.req_cpu <= rc) && (!hm || !km || p.req_mem <= rm);
+        } else {
+          sat = fits;
+        }
+      }
+      ok = sat || !required;
+    }
+    if (!ok) rej |= KG_REJECT_RESERVATION;
+  }
+  *out = (int32_t)rej;
 }
 
 // Scatter of upserted device rows
@@ -2699,6 +2855,14 @@ struct kg_engine {
   hipStream_t rs[kMaxDepth] = {};
   ncclComm_t comms[kMaxDepth] = {};  // comms[0] = comm; one communicator per round stream
   hipEvent_t ev_res[kMaxDepth] = {};
+  // (r4) round r's wide pass and merge run on es[r % D], its resolver on rs[r % D]: the resolver is dispatched as soon
+  // as resolve(r - D) is done — long before its records exist — and waits on the device for merge(r)'s blocks
+  // (mcnt[r % D]) and for resolve(r - 1) (the sequence word).  Same-stream resolvers were dispatched only after their
+  // merge, when the next round's wide pass could already fill every CU, and a multi-wave resolver then waited for a
+  // whole CU to drain.  eval(r) waits for resolve(r - D) through ev_done[r % D].
+  hipStream_t es[kMaxDepth] = {};
+  hipEvent_t ev_done[kMaxDepth] = {};
+  DevBuf<uint32_t> mcnt;  // [kMaxDepth] merge blocks done per round slot (cumulative over a batch)
   DevBuf<RowDelta> deltas;
   DevBuf<int64_t> scratch64;
   DevBuf<int32_t> scratch32;
@@ -3568,33 +3732,35 @@ uint64_t* gathered_slot(kg_engine* e, const RoundGeom& g, int slot) {
   return e->gathered.p + (size_t)slot * e->n_ranks * g.B * kCandStride;
 }
 
-void launch_merge_local(kg_engine* e, const RoundGeom& g, int nb, int slot, hipStream_t st) {
+void launch_merge_local(kg_engine* e, const RoundGeom& g, int nb, int slot, hipStream_t st, uint32_t* done = nullptr) {
   uint64_t* dst = e->n_ranks > 1 ? gathered_slot(e, g, slot) + (size_t)e->rank * g.B * kCandStride : cand_slot(e, g, slot);
   merge_round<false><<<nb, kMergeThreads, 0, st>>>(e->T, e->P, lists_slot(e, g, slot), (int64_t)g.nt_local * kR,
-                                                   kR, g.nt_local, kR, nb, poison_ptr(e), dst);
+                                                   kR, g.nt_local, kR, nb, poison_ptr(e), dst,
+                                                   e->n_ranks > 1 ? nullptr : done);
 }
 
-void launch_merge_ranks(kg_engine* e, const RoundGeom& g, int nb, int slot, hipStream_t st) {
+void launch_merge_ranks(kg_engine* e, const RoundGeom& g, int nb, int slot, hipStream_t st, uint32_t* done = nullptr) {
   merge_round<true><<<nb, kMergeThreads, 0, st>>>(e->T, e->P, gathered_slot(e, g, slot), kCandStride,
                                                   (int64_t)g.B * kCandStride, e->n_ranks, kC, nb, poison_ptr(e),
-                                                  cand_slot(e, g, slot));
+                                                  cand_slot(e, g, slot), done);
 }
 
-// KG_RESOLVER=1wave: the single-wave resolve_round (A/B measurements only; the look-ahead resolver is the default)
+// KG_RESOLVER=mw: the look-ahead resolve_mw (A/B measurements only).  The single-wave resolve_round is the default:
+// on MI355X at 100k nodes, depth 2, it runs the C3 queue at 869k pods/s against resolve_mw's 671k
 bool resolver_one_wave() {
-  static const bool on = std::getenv("KG_RESOLVER") && std::string(std::getenv("KG_RESOLVER")) == "1wave";
+  static const bool on = !(std::getenv("KG_RESOLVER") && std::string(std::getenv("KG_RESOLVER")) == "mw");
   return on;
 }
 
 void launch_resolve(kg_engine* e, const RoundGeom& g, int64_t first, int nb, int slot, int n_prev,
-                    int64_t seq, int wait, hipStream_t st) {
+                    int64_t seq, int wait, hipStream_t st, const uint32_t* rec_cnt = nullptr, uint32_t rec_target = 0) {
   if (e->numa_on) {
     resolve_round_numa<<<1, kWave, resolve_numa_lds_bytes(g, nb), st>>>(e->T, numa_table(e), e->pods.p, e->npods.p,
                                                                         e->cursor.p, first, nb, cand_slot(e, g, slot),
                                                                         e->P, e->NP, e->out_keys.p, e->out_cpus.p,
                                                                         e->out_nrec.p,
                                                                         g.bitmap_words, poison_ptr(e), seq, e->quotas.p,
-                                                                        e->nq);
+                                                                        e->nq, rec_cnt, rec_target);
     return;
   }
 #define KG_RESOLVE_T(X, Q)                                                                                       \
@@ -3602,14 +3768,15 @@ void launch_resolve(kg_engine* e, const RoundGeom& g, int64_t first, int nb, int
                                                                   cand_slot(e, g, slot), e->P, e->out_keys.p,       \
                                                                   g.bitmap_words, e->modlists.p, slot, g.depth,     \
                                                                   n_prev, poison_ptr(e), seq, wait, e->quotas.p,    \
-                                                                  e->nq, e->paux.p)
+                                                                  e->nq, e->paux.p, rec_cnt, rec_target)
 #define KG_RESOLVE(X) KG_RESOLVE_T(X, false)
 #define KG_RESOLVE_Q(X) KG_RESOLVE_T(X, true)
 #define KG_RESOLVE_MW_T(X, Q)                                                                                   \
   resolve_mw<X, Q><<<1, kMwThreads, mw_lds_bytes(nb), st>>>(e->T, e->pods.p, e->cursor.p, first, nb,              \
                                                             cand_slot(e, g, slot), e->P, e->out_keys.p,         \
                                                             e->modlists.p, slot, g.depth, n_prev, poison_ptr(e), \
-                                                            seq, wait, e->quotas.p, e->nq, e->paux.p)
+                                                            seq, wait, e->quotas.p, e->nq, e->paux.p, rec_cnt,   \
+                                                            rec_target)
 #define KG_RESOLVE_MW(X) KG_RESOLVE_MW_T(X, false)
 #define KG_RESOLVE_MW_Q(X) KG_RESOLVE_MW_T(X, true)
   if (!resolver_one_wave()) {
@@ -3685,14 +3852,14 @@ int rank_allgather(kg_engine* e, uint64_t* all, size_t cnt, int slot, hipStream_
 }
 
 // merge → [all-gather + merge of the rank records] of one round, on stream st
-int launch_merge(kg_engine* e, const RoundGeom& g, int nb, int slot, hipStream_t st) {
-  launch_merge_local(e, g, nb, slot, st);
+int launch_merge(kg_engine* e, const RoundGeom& g, int nb, int slot, hipStream_t st, uint32_t* done = nullptr) {
+  launch_merge_local(e, g, nb, slot, st, done);
   HIP_TRY(hipGetLastError());
   if (e->n_ranks > 1) {
     const size_t cnt = (size_t)g.B * kCandStride;
     uint64_t* all = gathered_slot(e, g, slot);
     if (int rc = rank_allgather(e, all, cnt, slot, st)) return rc;
-    launch_merge_ranks(e, g, nb, slot, st);
+    launch_merge_ranks(e, g, nb, slot, st, done);
     HIP_TRY(hipGetLastError());
   }
   return 0;
@@ -3704,7 +3871,9 @@ int launch_merge(kg_engine* e, const RoundGeom& g, int nb, int slot, hipStream_t
 // waiting on a cross-stream event.  Stream order makes eval(r) start right after resolve(r-D): it overlaps
 // resolve(r-D+1 .. r-1), whose rows resolve(r) treats as modified; merge(r) also runs off the
 // serial chain.  The first round of a batch starts from a fully written table (the host synchronised), so it has
-// no previous-round rows.
+// no previous-round rows.  (r4: a split — resolvers on streams of their own, dispatched ahead and waiting on the
+// device for their merge — measured slower at every depth: the cross-stream event before each wide pass costs more
+// than the early dispatch saves)
 int run_batch(kg_engine* e, const RoundGeom& g, int64_t cur, int64_t end, int64_t n_rounds) {
   const int D = g.depth;
   HIP_TRY(hipMemsetAsync(e->cursor.p + 3, 0, 3 * 8, e->rs[0]));  // poison, resolver sequence, device error
@@ -3813,7 +3982,7 @@ int prepare_rounds(kg_engine* e, RoundGeom& g) {
   if (!e->numa_on && !e->ds_on && resolve_lds_bytes(g, g.B) > kMaxLds)
     return fail(KG_E_UNSUPPORTED, "resolver LDS %zu B > %zu B: fewer nodes or a smaller batch_pods",
                 resolve_lds_bytes(g, g.B), kMaxLds);
-  if (!e->numa_on && !e->ds_on && mw_lds_bytes(g.B) > kMaxLds)
+  if (!e->numa_on && !e->ds_on && !resolver_one_wave() && mw_lds_bytes(g.B) > kMaxLds)
     return fail(KG_E_UNSUPPORTED, "resolver LDS %zu B > %zu B: a smaller batch_pods", mw_lds_bytes(g.B), kMaxLds);
   const size_t D = (size_t)g.depth;
   const size_t lists_n = e->lists.n;
@@ -4014,7 +4183,7 @@ int run_xr(kg_engine* e, int64_t first, int64_t count, kg_stats* stats, double t
     xr_select<<<eval_blocks, kWave * kEvalWaves, 0, e->stream>>>(val, val2, n, nt, stride, vbits, e->RP, X,
                                                                e->xr_norm_d.p, e->xr_lists.p, e->rsv_ws.p);
     merge_round<false><<<kXrPods, kMergeThreads, 0, e->stream>>>(e->T, e->P, e->xr_lists.p, (int64_t)nt * kR, kR, nt,
-                                                                 kR, kXrPods, poison, e->xr_cand.p);
+                                                                 kR, kXrPods, poison, e->xr_cand.p, nullptr);
     prof_end(e, KG_PROF_RSV_SELECT, t, e->stream);
     t = prof_begin(e, e->stream);
 #define KG_XR_RESOLVE(XF)                                                                                      \
@@ -4259,6 +4428,9 @@ static int engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank,
         return bail(fail(KG_E_DEVICE, "hipStreamCreateWithPriority"));
       if (hipEventCreateWithFlags(&e->ev_res[k], hipEventDisableTiming) != hipSuccess)
         return bail(fail(KG_E_DEVICE, "hipEventCreate"));
+      if (hipStreamCreateWithPriority(&e->es[k], hipStreamNonBlocking, hi) != hipSuccess ||
+          hipEventCreateWithFlags(&e->ev_done[k], hipEventDisableTiming) != hipSuccess)
+        return bail(fail(KG_E_DEVICE, "hipStreamCreateWithPriority / hipEventCreate"));
     }
   }
   // 12 int64 columns + inv_mem[2] (f64) + the kAux resources' Allocatable / Requested
@@ -4289,6 +4461,7 @@ static int engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank,
   if (int rc = e->cursor.ensure(16)) return bail(rc);
   if (hipMemsetAsync(e->cursor.p, 0, 16 * 8, e->stream) != hipSuccess) return bail(fail(KG_E_DEVICE, "hipMemset"));
   if (int rc = e->modlists.ensure(kMaxDepth * kModListStride)) return bail(rc);
+  if (int rc = e->mcnt.ensure(kMaxDepth)) return bail(rc);
   if (hipMemsetAsync(e->modlists.p, 0, kMaxDepth * kModListStride * 4, e->stream) != hipSuccess) return bail(fail(KG_E_DEVICE, "hipMemset"));
   e->nodes.assign(cap, kg_node{});
   e->metrics.assign(cap, kg_node_metric{});
@@ -4519,6 +4692,8 @@ void kg_engine_destroy(kg_engine* e) {
   if (e->stream) (void)hipStreamSynchronize(e->stream);
   for (int k = 0; k < kMaxDepth; ++k)
     if (e->rs[k]) (void)hipStreamSynchronize(e->rs[k]);
+  for (int k = 0; k < kMaxDepth; ++k)
+    if (e->es[k]) (void)hipStreamSynchronize(e->es[k]);
   if (e->lb_ready) (void)hipEventDestroy(e->lb_ready);
   if (e->lb_done) (void)hipEventDestroy(e->lb_done);
   for (int k = 1; k < kMaxDepth; ++k)
@@ -4536,9 +4711,12 @@ void kg_engine_destroy(kg_engine* e) {
   e->out_keys.release();
   e->cursor.release();
   e->modlists.release();
+  e->mcnt.release();
   for (int k = 0; k < kMaxDepth; ++k) {
     if (e->ev_res[k]) (void)hipEventDestroy(e->ev_res[k]);
     if (e->rs[k]) (void)hipStreamDestroy(e->rs[k]);
+    if (e->ev_done[k]) (void)hipEventDestroy(e->ev_done[k]);
+    if (e->es[k]) (void)hipStreamDestroy(e->es[k]);
   }
   e->deltas.release();
   e->numa_s.release();
@@ -5610,6 +5788,44 @@ int kg_pods_evaluate_reservation(kg_engine* e, const kg_pod* pod, int64_t* out) 
                                                                        e->scratch64.p);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpyAsync(out, e->scratch64.p, words * 8, hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  return 0;
+}
+
+int kg_pods_filter_preemption(kg_engine* e, const kg_pod* pod, int32_t node_idx, const kg_pod* victims,
+                              const int32_t* victim_slot, int64_t n_victims, int32_t* out_reject) {
+  if (!e || !pod || !out_reject || n_victims < 0 || (n_victims > 0 && !victims)) return fail(KG_E_INVALID, "null argument");
+  if (node_idx < 0 || node_idx >= e->n_nodes) return fail(KG_E_INVALID, "node index %d outside [0, %lld)", node_idx,
+                                                           (long long)e->n_nodes);
+  if (e->numa_on || e->ds_on || e->def_on)
+    return fail(KG_E_UNSUPPORTED, "preemption dry run: NodeNUMAResource / DeviceShare / the upstream defaults keep the "
+                "Go path (the victims' cpusets, devices and labels are not modelled)");
+  if (int rc = sync_static(e)) return rc;
+  DevPod d;
+  if (int rc = decode_pod(e, *pod, d)) return rc;
+  if (d.flags & P_AUX) return fail(KG_E_UNSUPPORTED, "preemption dry run: ephemeral-storage / scalar requests");
+  const RsvPod rp{(uint64_t)pod->reservation_owner_mask, (pod->reservation_flags & KG_POD_RSV_AFFINITY) ? RP_AFFINITY : 0u, 0};
+  std::vector<Victim> hv((size_t)std::max<int64_t>(n_victims, 1));
+  for (int64_t k = 0; k < n_victims; ++k) {
+    DevPod v;
+    if (int rc = decode_pod(e, victims[k], v)) return rc;
+    const int32_t s = victim_slot ? victim_slot[k] : -1;
+    if (s < -1 || s >= KG_MAX_RSV_SLOTS) return fail(KG_E_INVALID, "victim %lld: reservation slot %d", (long long)k, s);
+    bool nz = false;
+    for (int q = 0; q < KG_RES_MAX; ++q) nz |= victims[k].requests[q] != 0;
+    hv[k] = Victim{v.req_cpu, v.req_mem, v.nz_cpu, v.nz_mem, s, nz ? 1 : 0};
+  }
+  const size_t vw = (hv.size() * sizeof(Victim) + 7) / 8;
+  if (int rc = e->scratch64.ensure(kPodWords + vw + 1)) return rc;
+  DevPod* gp = reinterpret_cast<DevPod*>(e->scratch64.p);
+  Victim* gv = reinterpret_cast<Victim*>(e->scratch64.p + kPodWords);
+  int32_t* go = reinterpret_cast<int32_t*>(e->scratch64.p + kPodWords + vw);
+  HIP_TRY(hipMemcpyAsync(gp, &d, sizeof(d), hipMemcpyHostToDevice, e->stream));
+  if (n_victims > 0) HIP_TRY(hipMemcpyAsync(gv, hv.data(), (size_t)n_victims * sizeof(Victim), hipMemcpyHostToDevice, e->stream));
+  filter_pod_preempt<<<1, kWave, 0, e->stream>>>(e->T, e->rsv_d.p, e->rsv_nd.p, node_idx, gp, rp, e->P, e->RP,
+                                                 e->rsv_on ? 1 : 0, gv, n_victims, go);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(out_reject, go, 4, hipMemcpyDeviceToHost, e->stream));
   HIP_TRY(hipStreamSynchronize(e->stream));
   return 0;
 }

@@ -129,6 +129,55 @@ struct RsvDbg {
   int64_t pod_req_cpu, pod_req_mem;                    // nodeReservationState.podRequested
 };
 
+// BeforePreFilter's restore of one node for one pod (transformer.go:100-189): the matched slots' reserve pods leave
+// NodeInfo (restoreMatchedReservation :240-263), the unmatched assigned ones leave and return as their remainders
+// (restoreUnmatchedReservations :265-291); pr_* = nodeReservationState.podRequested, ra_* = Σ matched Allocated.
+__device__ __forceinline__ void rsv_restore(const RsvNode& rn, int ns, const RsvPod& rp, Row& r, uint32_t& mm, int& nm,
+                                            int64_t& pr_c, int64_t& pr_m, int64_t& ra_c, int64_t& ra_m,
+                                            bool& has_state) {
+  uint32_t um = 0;
+#pragma unroll
+  for (int s = 0; s < kRsvSlots; ++s) {
+    if (s >= ns) break;
+    const uint32_t m = rn.meta[s];
+    if (!(m & RS_AVAIL) || ((m & RS_ONCE) && rn.assigned[s] > 0)) continue;  // transformer.go:101-110
+    // ReservationInfo.Match → MatchReservationOwners, decoded per owner group into the pod's mask
+    if (((rp.owner_mask >> (rn.owner[s] & 63)) & 1u) && !(m & RS_UNSCHED)) mm |= 1u << s;
+    else if (rn.assigned[s] > 0) um |= 1u << s;
+  }
+  has_state = (mm | um) != 0 && !((rp.flags & RP_AFFINITY) && mm == 0);  // transformer.go:127-136
+  if (!has_state) return;
+#pragma unroll
+  for (int s = 0; s < kRsvSlots; ++s)
+    if (um >> s & 1) {  // restoreUnmatchedReservations (transformer.go:265-291)
+      r.req_cpu -= rn.alloc_cpu[s];
+      r.req_mem -= rn.alloc_mem[s];
+      r.nz_cpu -= rsv_nz_cpu(rn, s);
+      r.nz_mem -= rsv_nz_mem(rn, s);
+      const int64_t rc = rsv_nn(rn.alloc_cpu[s], rn.allocd_cpu[s]), rm = rsv_nn(rn.alloc_mem[s], rn.allocd_mem[s]);
+      if (rc != 0 || rm != 0) {  // the remainder pod carries the reservation's keys
+        r.req_cpu += rc;
+        r.req_mem += rm;
+        r.nz_cpu += rn.alloc_cpu[s] > 0 ? rc : kDefaultMilliCpu;
+        r.nz_mem += rn.alloc_mem[s] > 0 ? rm : kDefaultMemory;
+      }
+    }
+  pr_c = r.req_cpu;
+  pr_m = r.req_mem;
+#pragma unroll
+  for (int s = 0; s < kRsvSlots; ++s)
+    if (mm >> s & 1) {  // restoreMatchedReservation: NodeInfo.RemovePod(reserve pod) (transformer.go:240-263)
+      r.req_cpu -= rn.alloc_cpu[s];
+      r.req_mem -= rn.alloc_mem[s];
+      r.nz_cpu -= rsv_nz_cpu(rn, s);
+      r.nz_mem -= rsv_nz_mem(rn, s);
+      r.num_pods -= 1;
+      ra_c += rn.allocd_cpu[s];
+      ra_m += rn.allocd_mem[s];
+      ++nm;
+    }
+}
+
 template <bool kSlotsInRegs = true>  // false: the slot record is read where used (the wide exact pass, register-bound)
 __device__ __forceinline__ RsvOut rsv_eval_node(const DevTable& T, const RsvNode* __restrict__ RN,
                                                 const int32_t* __restrict__ rsv_n, int64_t i, const DevPod& p,
@@ -154,50 +203,7 @@ __device__ __forceinline__ RsvOut rsv_eval_node(const DevTable& T, const RsvNode
   RsvNode rn_copy;
   if (kSlotsInRegs && ns > 0) rn_copy = RN[i];
   const RsvNode& rn = kSlotsInRegs ? rn_copy : RN[i];
-  if (ns > 0) {
-    uint32_t um = 0;
-#pragma unroll
-    for (int s = 0; s < kRsvSlots; ++s) {
-      if (s >= ns) break;
-      const uint32_t m = rn.meta[s];
-      if (!(m & RS_AVAIL) || ((m & RS_ONCE) && rn.assigned[s] > 0)) continue;  // transformer.go:101-110
-      // ReservationInfo.Match → MatchReservationOwners, decoded per owner group into the pod's mask
-      if (((rp.owner_mask >> (rn.owner[s] & 63)) & 1u) && !(m & RS_UNSCHED)) mm |= 1u << s;
-      else if (rn.assigned[s] > 0) um |= 1u << s;
-    }
-    has_state = (mm | um) != 0 && !((rp.flags & RP_AFFINITY) && mm == 0);  // transformer.go:127-136
-    if (has_state) {
-#pragma unroll
-      for (int s = 0; s < kRsvSlots; ++s)
-        if (um >> s & 1) {  // restoreUnmatchedReservations (transformer.go:265-291)
-          r.req_cpu -= rn.alloc_cpu[s];
-          r.req_mem -= rn.alloc_mem[s];
-          r.nz_cpu -= rsv_nz_cpu(rn, s);
-          r.nz_mem -= rsv_nz_mem(rn, s);
-          const int64_t rc = rsv_nn(rn.alloc_cpu[s], rn.allocd_cpu[s]), rm = rsv_nn(rn.alloc_mem[s], rn.allocd_mem[s]);
-          if (rc != 0 || rm != 0) {  // the remainder pod carries the reservation's keys
-            r.req_cpu += rc;
-            r.req_mem += rm;
-            r.nz_cpu += rn.alloc_cpu[s] > 0 ? rc : kDefaultMilliCpu;
-            r.nz_mem += rn.alloc_mem[s] > 0 ? rm : kDefaultMemory;
-          }
-        }
-      pr_c = r.req_cpu;
-      pr_m = r.req_mem;
-#pragma unroll
-      for (int s = 0; s < kRsvSlots; ++s)
-        if (mm >> s & 1) {  // restoreMatchedReservation: NodeInfo.RemovePod(reserve pod) (transformer.go:240-263)
-          r.req_cpu -= rn.alloc_cpu[s];
-          r.req_mem -= rn.alloc_mem[s];
-          r.nz_cpu -= rsv_nz_cpu(rn, s);
-          r.nz_mem -= rsv_nz_mem(rn, s);
-          r.num_pods -= 1;
-          ra_c += rn.allocd_cpu[s];
-          ra_m += rn.allocd_mem[s];
-          ++nm;
-        }
-    }
-  }
+  if (ns > 0) rsv_restore(rn, ns, rp, r, mm, nm, pr_c, pr_m, ra_c, ra_m, has_state);
   if (dbg) {
     dbg->matched = mm;
     dbg->has_state = has_state ? 1 : 0;

@@ -410,7 +410,7 @@ __global__ __launch_bounds__(kWave) void xr_resolve(DevTable T, RsvNode* __restr
     stage(s_rpw, rpods, kRsvPodWords);
     if (kDs) stage(s_dpw, X.dpods, kDsPodWords);
     if (kNuma) stage(s_npw, X.npods, kNumaPodWords);
-    if (kDef) {  // DefPod is 104 B: byte-exact copy of the nb records
+    if (kDef) {  // DefPod (sizeof: 184 B since ABI 10): byte-exact copy of the nb records
       const uint32_t* g = reinterpret_cast<const uint32_t*>(X.defp + first);
       uint32_t* d = reinterpret_cast<uint32_t*>(s_dfw);
       constexpr int kW = (int)(sizeof(DefPod) / 4);

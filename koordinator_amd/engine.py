@@ -327,6 +327,17 @@ class Engine:
         check(self.lib, self.lib.kg_debug_eval_paths(self.h, ptr(out)))
         return int(out[0])
 
+    def filter_preemption(self, pod: np.ndarray, node: int, victims: np.ndarray, slots=None) -> int:
+        """The preemption dry run's Filter of `pod` on node `node` with `victims` removed (kg_pods_filter_preemption):
+        KG_REJECT_* bits, 0 = fits.  slots[k]: the node's reservation slot victim k was allocated from (-1 = none)."""
+        pod = np.ascontiguousarray(np.asarray(pod, dtype=abi.POD_DTYPE).reshape(1))
+        victims = np.ascontiguousarray(np.asarray(victims, dtype=abi.POD_DTYPE).reshape(-1))
+        sl = None if slots is None else np.ascontiguousarray(slots, dtype=np.int32)
+        out = np.zeros(1, dtype=np.int32)
+        check(self.lib, self.lib.kg_pods_filter_preemption(self.h, ptr(pod), int(node), ptr(victims) if len(victims) else None,
+                                                           ptr(sl) if sl is not None else None, len(victims), ptr(out)))
+        return int(out[0])
+
     def evaluate_reservation(self, pod: np.ndarray) -> dict:
         """The exact pass's evaluation of one pod on every node (kg_pods_evaluate_reservation): per node pass,
         nominated slot, raw Reservation score, restore state (has_state, matched slots, restored Requested /

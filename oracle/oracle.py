@@ -104,6 +104,8 @@ def lib():
         L.or_quota_admit.restype = i
         L.or_rsv_case_flat.argtypes = [vp, i64, vp, i64, vp, vp, i, vp, vp]
         L.or_rsv_case_flat.restype = None
+        L.or_filter_preemption.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, i64, i64]
+        L.or_filter_preemption.restype = i64
         for f, res in (("or_taint_filter", i), ("or_taint_count", i64), ("or_affinity_filter", i),
                        ("or_affinity_sum", i64), ("or_image_score", i64)):
             getattr(L, f).argtypes = [vp, vp]
@@ -233,6 +235,18 @@ def rsv_case(pod, allowed_pods, alloc, num_pods, pod_requested, r_allocated, has
                            p(a(alloc)), num_pods, p(a(pod_requested)), p(a(r_allocated)), int(has_state),
                            p(np.ascontiguousarray(np.asarray(rsv, dtype=abi.NODE_RSV_DTYPE).reshape(1))), p(out))
     return int(out[0]), int(out[1]), int(out[2])
+
+
+def filter_preemption(cfg, node, metric, state, rsv, pod, victims, slots, now_ns: int) -> int:
+    """or_filter_preemption: the preemption dry run's Filter (KG_REJECT_* bits) of one pod on one node."""
+    c = lambda a, dt: np.ascontiguousarray(np.asarray(a, dtype=dt).reshape(-1))
+    v = c(victims, abi.POD_DTYPE)
+    sl = c(slots if slots is not None else -np.ones(len(v)), np.int32)
+    return int(lib().or_filter_preemption(p(cfg), p(c(node, abi.NODE_DTYPE)), p(c(metric, abi.METRIC_DTYPE)),
+                                          p(np.ascontiguousarray(state[:1])),
+                                          p(c(rsv, abi.NODE_RSV_DTYPE)) if rsv is not None else None,
+                                          p(c(pod, abi.POD_DTYPE)), p(v) if len(v) else None, p(sl) if len(v) else None,
+                                          len(v), now_ns))
 
 
 def rsv_restore(rsv, st, pod) -> dict:

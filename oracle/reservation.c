@@ -242,7 +242,7 @@ int or_schedule_resv_full(const kg_config* cfg, int64_t n_nodes, const kg_node* 
     return KG_E_NOMEM;
   }
   /* TaintToleration / NodeAffinity / BalancedAllocation (defaults.c); a NULL table = no predicates, no taints */
-  const kg_node_predicates zero_pred = {0, 0, 0, 0};
+  const kg_node_predicates zero_pred = {0, 0, 0, 0, 0, 0};
   const int rsv_on = cfg->reservation_filter || cfg->reservation_score;
   const int ds_on = dev && (cfg->ds_filter || cfg->ds_score);
   if (n_threads < 1) n_threads = 1;
@@ -431,4 +431,105 @@ void or_rsv_restore_flat(const kg_node_reservations* r, const or_node_state* st,
   out[6] = ns.num_pods;
   out[7] = ns.pod_requested[0], out[8] = ns.pod_requested[1];
   out[9] = ns.r_allocated[0], out[10] = ns.r_allocated[1];
+}
+
+/* fitsNode (plugin.go:433-482) with rInfo = slot s (s < 0: nil) and a preemptible amount.  `np` = len(NodeInfo.Pods)
+ * of the NodeInfo the Filter sees (victims removed); podRequested / rAllocated are nodeReservationState's, which the
+ * victims' removal does not touch (a node without state has none: zero). */
+static int fits_node_pre(const kg_pod* pod, int64_t allowed_pods, const int64_t alloc[2], const or_rsv_node* ns,
+                         int64_t np, const kg_node_reservations* r, int s, const int64_t pre[2]) {
+  if (np - ns->n_matched + 1 > allowed_pods) return 0;
+  const int64_t pc = pod->requests[KG_RES_CPU], pm = pod->requests[KG_RES_MEMORY];
+  if (pc == 0 && pm == 0) return 1;
+  int64_t rc = 0, rm = 0;
+  if (s >= 0) {
+    rc = sub_nn(r->allocatable_cpu[s], r->allocated_cpu[s]);
+    rm = sub_nn(r->allocatable_mem[s], r->allocated_mem[s]);
+  }
+  const int64_t prc = ns->has_state ? ns->pod_requested[0] : 0, prm = ns->has_state ? ns->pod_requested[1] : 0;
+  if (pc > alloc[0] - (prc - rc - ns->r_allocated[0] - pre[0])) return 0;
+  if (pm > alloc[1] - (prm - rm - ns->r_allocated[1] - pre[1])) return 0;
+  return 1;
+}
+
+int64_t or_filter_preemption(const kg_config* cfg, const kg_node* node, const kg_node_metric* metric,
+                             const or_node_state* st, const kg_node_reservations* rsv, const kg_pod* pod,
+                             const kg_pod* victims, const int32_t* victim_slot, int64_t n_victims, int64_t now) {
+  if (!(node->flags & KG_NODE_VALID)) return KG_REJECT_INVALID_NODE;
+  const int rsv_on = cfg->reservation_filter || cfg->reservation_score;
+  or_rsv_node ns;
+  or_rsv_restore(rsv_on ? rsv : NULL, st, pod, &ns);
+  /* the NodeInfo copy the dry run filters on: the restored node minus the victims (NodeInfo.RemovePod) */
+  or_node_state rs = *st;
+  rs.requested[KG_RES_CPU] = ns.requested[0];
+  rs.requested[KG_RES_MEMORY] = ns.requested[1];
+  rs.nonzero[0] = ns.nonzero[0];
+  rs.nonzero[1] = ns.nonzero[1];
+  rs.num_pods = ns.num_pods;
+  int64_t pre[2] = {0, 0}, pre_rr[KG_MAX_RSV_SLOTS][2];
+  int pre_set = 0, pre_rr_set = 0;
+  memset(pre_rr, 0, sizeof(pre_rr));
+  for (int64_t k = 0; k < n_victims; k++) {
+    const kg_pod* v = &victims[k];
+    rs.requested[KG_RES_CPU] -= v->requests[KG_RES_CPU];
+    rs.requested[KG_RES_MEMORY] -= v->requests[KG_RES_MEMORY];
+    rs.nonzero[0] -= v->nonzero_requests[0];
+    rs.nonzero[1] -= v->nonzero_requests[1];
+    rs.num_pods -= 1;
+    int nz = 0; /* !quotav1.IsZero(podRequests): every requested resource counts, not only cpu / memory */
+    for (int q = 0; q < KG_RES_MAX; q++) nz |= v->requests[q] != 0;
+    if (!nz) continue;
+    const int s = victim_slot ? victim_slot[k] : -1;
+    if (s >= 0 && s < KG_MAX_RSV_SLOTS) {
+      pre_rr[s][0] += v->requests[KG_RES_CPU];
+      pre_rr[s][1] += v->requests[KG_RES_MEMORY];
+      pre_rr_set |= 1 << s;
+    } else {
+      pre[0] += v->requests[KG_RES_CPU];
+      pre[1] += v->requests[KG_RES_MEMORY];
+      pre_set = 1;
+    }
+  }
+  int64_t rej = 0;
+  if (cfg->fit_filter) rej |= or_fit_filter(node, &rs, pod);
+  if (cfg->la_filter) {
+    const int f = or_loadaware_filter(cfg, node, metric, pod, now);
+    if (f < 0) return f;
+    if (f) rej |= KG_REJECT_LOADAWARE;
+  }
+  if (rsv_on && cfg->reservation_filter) {
+    const int required = (pod->reservation_flags & KG_POD_RSV_AFFINITY) != 0;
+    const int64_t alloc[2] = {node->allocatable[KG_RES_CPU], node->allocatable[KG_RES_MEMORY]};
+    int ok = 1;
+    if (ns.n_matched == 0 || !ns.has_state) {
+      if (required) ok = 0;
+      else if (pre_set || pre_rr_set) ok = fits_node_pre(pod, node->allowed_pods, alloc, &ns, rs.num_pods, rsv, -1, pre);
+    } else {
+      const int64_t pc = pod->requests[KG_RES_CPU], pm = pod->requests[KG_RES_MEMORY];
+      const int kc = or_pod_cpu_key(pod), km = or_pod_mem_key(pod);
+      int satisfied = 0;
+      for (int k = 0; k < ns.n_matched && !satisfied; k++) {
+        const int s = ns.matched[k];
+        const int hc = rsv->allocatable_cpu[s] > 0, hm = rsv->allocatable_mem[s] > 0;
+        if (!((kc && hc) || (km && hm))) continue;
+        const int64_t p2[2] = {pre_rr[s][0] + pre[0], pre_rr[s][1] + pre[1]};
+        const int fits = fits_node_pre(pod, node->allowed_pods, alloc, &ns, rs.num_pods, rsv, s, p2);
+        if (rsv->policy[s] == KG_RSV_POLICY_RESTRICTED) {
+          /* Allocated − preemptibleInRR (non-negative, masked to the reservation's keys) when that map is set */
+          int64_t ac = rsv->allocated_cpu[s], am = rsv->allocated_mem[s];
+          if ((pre_rr_set >> s) & 1) {
+            ac = hc ? sub_nn(ac, pre_rr[s][0]) : 0;
+            am = hm ? sub_nn(am, pre_rr[s][1]) : 0;
+          }
+          const int64_t rc = sub_nn(rsv->allocatable_cpu[s], ac), rm = sub_nn(rsv->allocatable_mem[s], am);
+          if ((!hc || !kc || pc <= rc) && (!hm || !km || pm <= rm) && fits) satisfied = 1;
+        } else if (fits) {
+          satisfied = 1;
+        }
+      }
+      ok = satisfied || !required;
+    }
+    if (!ok) rej |= KG_REJECT_RESERVATION;
+  }
+  return rej;
 }

@@ -78,6 +78,17 @@ void or_rsv_case_flat(const kg_pod* pod, int64_t allowed_pods, const int64_t all
 
 void or_rsv_restore_flat(const kg_node_reservations* r, const or_node_state* st, const kg_pod* pod, int64_t* out);
 
+/* Preemption dry run (defaultpreemption SelectVictimsOnNode → RunFilterPluginsWithNominatedPods on a NodeInfo copy
+ * with the victims removed): NodeInfo.RemovePod of each victim, and Reservation's PreFilterExtensions.RemovePod
+ * (plugin.go:284-310) adding each victim's requests to state.preemptible[node] (victim_slot[k] < 0) or to
+ * state.preemptibleInRRs[node][slot] — a victim with all-zero requests is skipped.  Then the pod's Filters on that
+ * node: NodeResourcesFit (cpu / memory / pods), LoadAwareScheduling, and the Reservation Filter (plugin.go:357-428)
+ * with the preemptible amounts in fitsNode (:433-482) and the Restricted policy's Allocated (:404-413).  Returns the
+ * KG_REJECT_* bits (0 = every Filter passes).  Profiles: Fit / LoadAware / Reservation. */
+int64_t or_filter_preemption(const kg_config* cfg, const kg_node* node, const kg_node_metric* metric,
+                             const or_node_state* st, const kg_node_reservations* rsv, const kg_pod* pod,
+                             const kg_pod* victims, const int32_t* victim_slot, int64_t n_victims, int64_t now);
+
 #ifdef __cplusplus
 }
 #endif

@@ -465,3 +465,27 @@ def test_device_image_locality_matches_oracle(variant):
         node, score = e.schedule(pods)[:2]
     assert np.array_equal(node, want) and np.array_equal(score, want_score)
     assert (node >= 0).mean() > 0.5
+
+
+def test_image_table_counts_are_cluster_wide_known_deviation():
+    """ADVICE r3, a documented deviation: k8s v1.24's cache.addNodeImageStates copies len(state.nodes)
+    into a node's ImageStateSummary when that node is added or updated, so a node added before a second holder of the
+    same image keeps NumNodes = 1 until its own next update.  ImageTable — and the device, which takes one scaled score
+    per container — uses the cluster-wide count on every node.  The two agree once every holder has been re-added
+    after the last one arrived (an informer resync).  Parity unpinned: upstream is not vendored."""
+    from koordinator_amd.predicates import ImageTable
+    size = 600 * MIB
+    t = ImageTable([[(["img/a:v1"], size)], [(["img/a:v1"], size)], []])  # nodes 0 and 1 hold the image, 3 nodes
+    pod = t.fill_pod(_pod(), ["img/a:v1"])
+    assert int(pod["container_image_score"][0][0]) == int(float(size) * (2.0 / 3.0))  # NumNodes = 2 on both
+    rows = np.zeros(3, dtype=abi.NODE_PRED_DTYPE)
+    rows["images"] = [t.node_mask(i) for i in range(3)]
+    rows["image_count"] = t.image_count()
+    got = [oracle.default_plugins(rows[i], pod)["image_score"] for i in range(3)]
+    assert got[0] == got[1] and got[2] == 0
+
+    def calc(scaled):  # calculatePriority(sumImageScores, 1 container): clamp to [23 MiB, 1000 MiB], scale to 0..100
+        s = min(max(scaled, 23 * MIB), 1000 * MIB)
+        return 100 * (s - 23 * MIB) // (1000 * MIB - 23 * MIB)
+    upstream_v124 = [calc(int(float(size) * (1.0 / 3.0))), calc(int(float(size) * (2.0 / 3.0))), 0]  # node 0 added first
+    assert got[1] == upstream_v124[1] and got[0] != upstream_v124[0]  # the deviation, on the earlier-added holder only

@@ -401,3 +401,16 @@ def test_c3_full_size():
     assert (st["num_pods"] <= cl.nodes["allowed_pods"]).all()
     np.testing.assert_array_equal(st["num_pods"], np.bincount(cl.existing_node, minlength=cl.n) +
                                   np.bincount(g[placed], minlength=cl.n))
+
+
+def test_lookahead_resolver_parity():
+    """The look-ahead resolver (resolve_mw: chain + keeper + helper waves) is not the default; its
+    selection is read once per process, so its parity runs in a child process with KG_RESOLVER=mw."""
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    r = subprocess.run([sys.executable, "-u", os.path.join(here, "resolver_ab.py")], env={**os.environ, "KG_RESOLVER": "mw"},
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert "parity: ok" in r.stdout
