@@ -151,8 +151,8 @@ __device__ __forceinline__ void select_write(const uint32_t (&v)[kNPT], const ui
 // (they would stay live across the wide loop and halve its occupancy).
 __device__ __forceinline__ void eval_tile_exact(const DevTable& T, const DevPod* __restrict__ pods, int64_t first,
                                              int p0, int p1, int tile, int64_t node_base, int64_t n_local,
-                                             int nt_local, const EvalParams& P, uint64_t* __restrict__ lists,
-                                             int vbits, const int64_t* __restrict__ paux) {
+                                             const EvalParams& P, uint64_t* __restrict__ out, int vbits,
+                                             const int64_t* __restrict__ paux) {
   const int lane = threadIdx.x % kWave;
   uint32_t gidx[kNPT];
 #pragma unroll
@@ -169,7 +169,65 @@ __device__ __forceinline__ void eval_tile_exact(const DevTable& T, const DevPod*
       if (P.fit_filter && (p.flags & P_AUX) && v[j] && !aux_fits(T, node_base + local, paux + (size_t)(first + pi) * kAux))
         v[j] = 0;
     }
-    select_write(v, gidx, vbits, lists + ((size_t)pi * nt_local + tile) * kR, lane);
+    select_write(v, gidx, vbits, out + (size_t)(pi - p0) * kR, lane);
+  }
+}
+
+// one wave's tile for pods [p0, p1): its kR best packed keys per pod into out[(pi - p0) * kR ..]
+template <int PF>
+__device__ __forceinline__ void eval_tile(const DevTable& T, const DevPod* __restrict__ pods, int64_t first, int p0,
+                                          int p1, int tile, int64_t node_base, int64_t n_local, const EvalParams& P,
+                                          uint64_t* __restrict__ out, int vbits, const int64_t* __restrict__ paux,
+                                          int lane) {
+
+  HotRow rows[kNPT];
+  uint32_t gidx[kNPT];
+  bool rare = false;
+  {  // every column load of the tile's rows issued before any is used (a row past the shard reads the shard's last
+     // row — row 0 for an empty shard — and is masked invalid): one wait for the tile instead of a wait per
+     // conditional load
+    HotCols c[kNPT];
+    int64_t ii[kNPT];
+#pragma unroll
+    for (int j = 0; j < kNPT; ++j) {
+      const int64_t local = (int64_t)tile * kTile + j * kWave + lane;
+      gidx[j] = (uint32_t)(node_base + local);
+      ii[j] = local < n_local ? node_base + local : (n_local > 0 ? node_base + n_local - 1 : 0);
+      load_hot_cols<PF>(T, ii[j], c[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < kNPT; ++j) load_hot_la_alloc<PF>(T, ii[j], c[j]);
+#pragma unroll
+    for (int j = 0; j < kNPT; ++j) {
+      const int64_t local = (int64_t)tile * kTile + j * kWave + lane;
+      rows[j] = hot_from_cols<PF>(c[j], P);
+      if (local >= n_local) rows[j].flags = 0;  // not F_VALID → never feasible
+      rare |= (rows[j].flags & F_RARE) != 0;
+    }
+  }
+  KG_STAMP(0, 1);
+  // a row outside eval_hot's exact domain anywhere in the tile: the whole tile takes the exact path
+  if (__ballot(rare)) {
+    eval_tile_exact(T, pods, first, p0, p1, tile, node_base, n_local, P, out, vbits, paux);
+    return;
+  }
+  for (int pi = p0; pi < p1; ++pi) {
+    const DevPod p = pods[first + pi];
+    uint32_t v[kNPT];
+#pragma unroll
+    for (int j = 0; j < kNPT; ++j) {
+      uint32_t t = 0;
+      v[j] = eval_hot<PF>(rows[j], p, P, t) ? t + 1u : 0u;
+    }
+    if constexpr ((PF & PF_FIT_FILTER) != 0) {  // ephemeral-storage / scalar requests: the Allocatable-Requested columns
+      if (p.flags & P_AUX) {
+        const int64_t* rq = paux + (size_t)(first + pi) * kAux;
+#pragma unroll
+        for (int j = 0; j < kNPT; ++j)
+          if (v[j] && !aux_fits(T, gidx[j], rq)) v[j] = 0;
+      }
+    }
+    select_write(v, gidx, vbits, out + (size_t)(pi - p0) * kR, lane);
   }
 }
 
@@ -189,63 +247,40 @@ __global__ __launch_bounds__(kWave* kEvalWaves) void eval_round(DevTable T, cons
   const int n_pg = (nb + pods_per_wave - 1) / pods_per_wave;
   const uint32_t nwg = gridDim.x, bid = blockIdx.x, xcd = bid % 8u, q = nwg / 8u, r = nwg % 8u;
   const uint32_t wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8u;
-  const int tile = (int)(wgid / (uint32_t)n_pg) * kEvalWaves + wave;
+  const int tile0 = (int)(wgid / (uint32_t)n_pg) * kEvalWaves, tile = tile0 + wave;
   const int p0 = (int)(wgid % (uint32_t)n_pg) * pods_per_wave;
-  if (tile >= nt_local || p0 >= nb) return;
+  if (tile0 >= nt_local || p0 >= nb) return;  // block-uniform
   const int p1 = (p0 + pods_per_wave) < nb ? (p0 + pods_per_wave) : nb;
   const int vbits = P.score_bits + 1;  // v = total + 1 ≤ 2^score_bits
-
-  HotRow rows[kNPT];
-  uint32_t gidx[kNPT];
-  bool rare = false;
-  {  // every column load of the tile's rows issued before any is used (a row past the shard reads the shard's last
-     // row and is masked invalid): one wait for the tile instead of a wait per conditional load
-    HotCols c[kNPT];
-    int64_t ii[kNPT];
+  // (r4) each wave's per-pod tile top-kR goes to LDS; the block then combines its kEvalWaves tiles into one
+  // top-kR list per (pod, tile group) — a quarter of the candidate lists for the merge to read and rank
+  extern __shared__ __attribute__((aligned(16))) uint64_t s_lists[];  // [kEvalWaves][pods_per_wave][kR]
+  uint64_t* my_l = s_lists + (size_t)wave * pods_per_wave * kR;
+  if (tile < nt_local) eval_tile<PF>(T, pods, first, p0, p1, tile, node_base, n_local, P, my_l, vbits, paux, lane);
+  else
+    for (int q = lane; q < (p1 - p0) * kR; q += kWave) my_l[q] = 0;
+  __syncthreads();
+  // group list = the kR largest of the block's kEvalWaves·kR keys, in descending key order (within one score:
+  // ascending node index, as the merge's tie rule reads lists); a full group list's minimum bounds every key the
+  // block left out, as a full tile list's did (a full tile list's kR keys are all in the union)
+  const int ng_local = (nt_local + kEvalWaves - 1) / kEvalWaves, grp = tile0 / kEvalWaves;
+  static_assert(kEvalWaves * kR <= kWave, "one key per lane");
+  for (int pl = wave; pl < p1 - p0; pl += kEvalWaves) {
+    const uint64_t key = lane < kEvalWaves * kR ? s_lists[((size_t)(lane / kR) * pods_per_wave + pl) * kR + lane % kR] : 0;
+    int rank = 0;
 #pragma unroll
-    for (int j = 0; j < kNPT; ++j) {
-      const int64_t local = (int64_t)tile * kTile + j * kWave + lane;
-      gidx[j] = (uint32_t)(node_base + local);
-      ii[j] = node_base + (local < n_local ? local : n_local - 1);
-      load_hot_cols<PF>(T, ii[j], c[j]);
-    }
+    for (int w = 0; w < kEvalWaves; ++w) {
+      const ulonglong2* l2 = reinterpret_cast<const ulonglong2*>(s_lists + ((size_t)w * pods_per_wave + pl) * kR);
 #pragma unroll
-    for (int j = 0; j < kNPT; ++j) load_hot_la_alloc<PF>(T, ii[j], c[j]);
-#pragma unroll
-    for (int j = 0; j < kNPT; ++j) {
-      const int64_t local = (int64_t)tile * kTile + j * kWave + lane;
-      rows[j] = hot_from_cols<PF>(c[j], P);
-      if (local >= n_local) rows[j].flags = 0;  // not F_VALID → never feasible
-      rare |= (rows[j].flags & F_RARE) != 0;
-    }
-  }
-  KG_STAMP(0, 1);
-  // a row outside eval_hot's exact domain anywhere in the tile: the whole tile takes the exact path
-  if (__ballot(rare)) {
-    eval_tile_exact(T, pods, first, p0, p1, tile, node_base, n_local, nt_local, P, lists, vbits, paux);
-    return;
-  }
-  for (int pi = p0; pi < p1; ++pi) {
-    const DevPod p = pods[first + pi];
-    uint32_t v[kNPT];
-#pragma unroll
-    for (int j = 0; j < kNPT; ++j) {
-      uint32_t t = 0;
-      v[j] = eval_hot<PF>(rows[j], p, P, t) ? t + 1u : 0u;
-    }
-    if constexpr ((PF & PF_FIT_FILTER) != 0) {  // ephemeral-storage / scalar requests: the Allocatable-Requested columns
-      if (p.flags & P_AUX) {
-        const int64_t* rq = paux + (size_t)(first + pi) * kAux;
-#pragma unroll
-        for (int j = 0; j < kNPT; ++j)
-          if (v[j] && !aux_fits(T, gidx[j], rq)) v[j] = 0;
+      for (int q = 0; q < kR / 2; ++q) {
+        const ulonglong2 x = l2[q];  // broadcast LDS reads
+        rank += (x.x > key) + (x.y > key);
       }
     }
-#ifdef KG_EXP_NOSELECT  // timing experiment only (wrong lists): the wide pass without its per-tile select
-    if (lane < kR) lists[((size_t)pi * nt_local + tile) * kR + lane] = make_key(v[0] + v[1] + v[2] + v[3], gidx[0]);
-#else
-    select_write(v, gidx, vbits, lists + ((size_t)pi * nt_local + tile) * kR, lane);
-#endif
+    const int nnz = __popcll(__ballot(key != 0));
+    uint64_t* out = lists + ((size_t)(p0 + pl) * ng_local + grp) * kR;
+    if (key != 0 && rank < kR) out[rank] = key;
+    if (lane >= nnz && lane < kR) out[lane] = 0;
   }
   KG_STAMP(0, 31);
 }
@@ -3676,6 +3711,7 @@ size_t resolve_numa_lds_bytes(const RoundGeom& g, int nb) {
 }
 NumaTable numa_table(kg_engine* e) { return NumaTable{e->numa_s.p, e->numa_m.p}; }
 
+size_t eval_lds_bytes(const RoundGeom& g) { return (size_t)kEvalWaves * g.ppw * kR * 8; }
 dim3 eval_grid(const RoundGeom& g, int nb) {
   // 1-D grid: tile groups × pod groups, swizzled over XCDs inside eval_round
   return dim3((unsigned)(((g.nt_local + kEvalWaves - 1) / kEvalWaves) * ((nb + g.ppw - 1) / g.ppw)));
@@ -3719,11 +3755,18 @@ void launch_eval(kg_engine* e, const RoundGeom& g, int64_t first, int nb, int sl
     return;
   }
 #define KG_EVAL(X)                                                                                        \
-  eval_round<X><<<eval_grid(g, nb), kWave * kEvalWaves, 0, st>>>(e->T, e->pods.p, first, nb, g.ppw, g.base, \
+  eval_round<X><<<eval_grid(g, nb), kWave * kEvalWaves, eval_lds_bytes(g), st>>>(e->T, e->pods.p, first, nb,   \
+                                                                                g.ppw, g.base,                   \
                                                                  g.n_local, g.nt_local, e->P,             \
                                                                  lists_slot(e, g, slot), poison_ptr(e), e->paux.p)
   KG_PF_SWITCH(profile_bits(e->P), KG_EVAL)
 #undef KG_EVAL
+}
+
+// candidate lists per pod of the round's wide pass: eval_round writes one per tile group of kEvalWaves tiles, the
+// NUMA and DeviceShare passes one per tile
+int eval_lists(kg_engine* e, const RoundGeom& g) {
+  return (e->numa_on || e->ds_on) ? g.nt_local : (g.nt_local + kEvalWaves - 1) / kEvalWaves;
 }
 
 // local merge: this rank's tile lists → per-pod record (single rank: the final candidates)
@@ -3734,8 +3777,9 @@ uint64_t* gathered_slot(kg_engine* e, const RoundGeom& g, int slot) {
 
 void launch_merge_local(kg_engine* e, const RoundGeom& g, int nb, int slot, hipStream_t st, uint32_t* done = nullptr) {
   uint64_t* dst = e->n_ranks > 1 ? gathered_slot(e, g, slot) + (size_t)e->rank * g.B * kCandStride : cand_slot(e, g, slot);
-  merge_round<false><<<nb, kMergeThreads, 0, st>>>(e->T, e->P, lists_slot(e, g, slot), (int64_t)g.nt_local * kR,
-                                                   kR, g.nt_local, kR, nb, poison_ptr(e), dst,
+  const int nl = eval_lists(e, g);
+  merge_round<false><<<nb, kMergeThreads, 0, st>>>(e->T, e->P, lists_slot(e, g, slot), (int64_t)nl * kR, kR, nl, kR,
+                                                   nb, poison_ptr(e), dst,
                                                    e->n_ranks > 1 ? nullptr : done);
 }
 
