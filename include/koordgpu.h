@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define KG_ABI_VERSION 11
+#define KG_ABI_VERSION 12
 
 /* ---- resource slots (fixed order) ------------------------------------------------------- */
 enum {
@@ -124,8 +124,11 @@ enum {
   KG_REJECT_DEVICE = 1 << 6,        /* DeviceShare (Insufficient gpu devices)          */
   KG_REJECT_FIT_OTHER = 1 << 7,     /* NodeResourcesFit: Insufficient ephemeral-storage / a scalar resource
                                        (KG_RES_EPHEMERAL .. KG_RES_MID_MEMORY; reservation/plugin.go:469-479) */
-  KG_REJECT_RESERVATION = 1 << 8    /* (ABI 11) Reservation Filter (kg_pods_filter_preemption): preemption failed /
+  KG_REJECT_RESERVATION = 1 << 8,   /* (ABI 11) Reservation Filter (kg_pods_filter_preemption): preemption failed /
                                        no reservation meets the requirements / reservation affinity */
+  KG_REJECT_SPREAD = 1 << 9,        /* (ABI 12) PodTopologySpread: DoNotSchedule constraint's skew exceeded   */
+  KG_REJECT_INTERPOD = 1 << 10      /* (ABI 12) InterPodAffinity: affinity / anti-affinity / existing pods'
+                                       anti-affinity rules not matched                                          */
 };
 
 /* node flags */
@@ -221,6 +224,16 @@ typedef struct kg_config {
   int64_t balanced_resources;                  /* bit r: resource r (cpu 0, memory 1) is in its Resources list   */
   int64_t image_score;                         /* (ABI 10) ImageLocality at Score (no NormalizeScore)            */
   int64_t weight_image;
+  /* (ABI 12) PodTopologySpread and InterPodAffinity with topologyKey kubernetes.io/hostname (k8s v1.24.15
+   * podtopologyspread/{filtering,scoring}.go, interpodaffinity/{filtering,scoring}.go; not vendored — DESIGN.md §3.15).
+   * Evaluated on the exact per-pod pass, one pod per pass.  Upstream default weights: 2 and 1. */
+  int64_t spread_filter;                       /* PodTopologySpread at Filter (DoNotSchedule constraint)         */
+  int64_t spread_score;                        /* PodTopologySpread at Score (ScheduleAnyway; its NormalizeScore) */
+  int64_t weight_spread;
+  int64_t interpod_filter;                     /* InterPodAffinity at Filter                                     */
+  int64_t interpod_score;                      /* InterPodAffinity at Score (min-max NormalizeScore)             */
+  int64_t weight_interpod;
+  int64_t hard_pod_affinity_weight;            /* InterPodAffinityArgs.HardPodAffinityWeight (default 1)         */
   int64_t reserved[2];
 } kg_config;
 
@@ -272,6 +285,8 @@ typedef struct kg_pod_metric {
 #define KG_MAX_AFF_TERMS 4
 /* Containers an ImageLocality pod may carry (more: the pod stays on the Go path) */
 #define KG_MAX_CONTAINERS 8
+#define KG_MAX_MATCH_GROUPS 16   /* (ABI 12) PodTopologySpread / InterPodAffinity match groups */
+#define KG_MAX_POD_PREFERRED 4   /* (ABI 12) preferred pod (anti-)affinity terms per pod */
 
 /* One pod, pre-decoded by the caller (PodRequestsAndLimits semantics, pkg/util/pod_resources_utils.go:48-64). */
 typedef struct kg_pod {
@@ -318,6 +333,24 @@ typedef struct kg_pod {
    * against (taint ids < taint_count are decided).  kg_pods_schedule* refuses a staged queue holding a pod compiled
    * against fewer taints than some valid node row carries (KG_E_INVALID: re-stage the pods). */
   int64_t taint_count;
+  /* (ABI 12) PodTopologySpread / InterPodAffinity, topologyKey kubernetes.io/hostname only, over the caller's table of
+   * match groups (≤ KG_MAX_MATCH_GROUPS).  A group is a label selector with its namespace set (a spread constraint's
+   * selector in the pod's namespace; an affinity term's selector and namespaces), or the conjunction of a pod's
+   * required pod-affinity terms.  Group ids below are 1 + index, 0 = none.  The same fields describe the pod both when
+   * it is scheduled and when it sits on a node (kg_pods_add, or placed by the engine): the engine keeps per node the
+   * number of pods matching each group, of required anti-affinity terms of each group, and the symmetric weights. */
+  int64_t match_groups;                        /* bit k: the pod (labels, namespace) matches group k             */
+  int64_t spread_hard_group;                   /* the DoNotSchedule hostname constraint's group (0 = none)       */
+  int64_t spread_hard_max_skew;
+  int64_t spread_soft_group;                   /* the ScheduleAnyway hostname constraint's group (0 = none); a   */
+  int64_t spread_soft_max_skew;                /* pod without constraints passes the system default one here     */
+  int64_t pod_affinity_group;                  /* the conjunction of its required pod-affinity terms (0 = none)  */
+  int64_t pod_affinity_terms;                  /* bit k: a required pod-affinity term of group k (symmetric      */
+                                               /* score of later pods: HardPodAffinityWeight)                    */
+  int64_t pod_anti_affinity;                   /* bit k: a required pod-anti-affinity term of group k            */
+  int64_t n_pod_preferred;                     /* preferred pod (anti-)affinity terms (≤ KG_MAX_POD_PREFERRED)   */
+  int64_t pod_preferred_group[KG_MAX_POD_PREFERRED];
+  int64_t pod_preferred_weight[KG_MAX_POD_PREFERRED];  /* + affinity weight, − anti-affinity weight           */
 } kg_pod;
 
 /* pod reservation flags */
@@ -580,6 +613,13 @@ int kg_pods_evaluate_reservation(kg_engine* e, const kg_pod* pod, int64_t* out);
  * defaults are refused (KG_E_UNSUPPORTED: the victims' cpusets / devices / labels are not modelled here). */
 int kg_pods_filter_preemption(kg_engine* e, const kg_pod* pod, int32_t node_idx, const kg_pod* victims,
                               const int32_t* victim_slot, int64_t n_victims, int32_t* out_reject);
+
+/* (ABI 12) PodTopologySpread / InterPodAffinity state (engines whose profile enables either): per node and match
+ * group k, [n][k] layout of KG_MAX_MATCH_GROUPS int32 each — pods matching group k (countPodsMatchSelector),
+ * required anti-affinity terms of group k held by the node's pods (existingAntiAffinityCounts), and the symmetric
+ * score weight of the node's pods' terms of group k (processExistingPod: preferred ± weight, required affinity ×
+ * HardPodAffinityWeight).  Maintained from kg_pods_add / kg_pods_remove, Reserve and Unreserve. */
+int kg_nodes_read_pod_groups(kg_engine* e, int32_t* match_count, int32_t* anti_count, int32_t* sym_weight);
 
 /* ElasticQuota admission (engines whose pods carry quota_id): replaces the quota table (n ≤ KG_MAX_QUOTAS).
  * Every scheduled pod runs PreFilter's check (used + request ≤ used_limit over the pod's cpu/memory requests; for

@@ -36,7 +36,7 @@ POD_TAINT_TABLE = 64
 MAX_OWNER_GROUPS = 64
 QUOTA_RES = 8
 MAX_QUOTAS = 64
-ABI_VERSION = 11
+ABI_VERSION = 12
 MAX_RSV_SLOTS = 4
 RSV_POLICY = {"Default": 0, "Aligned": 1, "Restricted": 2}
 POD_RSV_AFFINITY = 1
@@ -56,10 +56,14 @@ RSV_EVAL_WORDS = 16  # KG_RSV_EVAL_WORDS: kg_pods_evaluate_reservation per node
 DBG_MERGE_WORDS = 32  # KG_DBG_MERGE_WORDS: one kg_debug_numa_merge case
 REJECT_FIT_OTHER = 128  # NodeResourcesFit: ephemeral-storage / a scalar resource (RES_EPHEMERAL .. RES_MID_MEMORY)
 REJECT_RESERVATION = 256  # Reservation Filter (kg_pods_filter_preemption)
+REJECT_SPREAD = 512  # (ABI 12) PodTopologySpread
+REJECT_INTERPOD = 1024  # (ABI 12) InterPodAffinity
 # DeviceShare device resources (KG_DEV_*)
 DEV_RES_MAX, MAX_MINORS = 8, 8
 MAX_AFF_TERMS = 4  # KG_MAX_AFF_TERMS
 MAX_CONTAINERS = 8  # KG_MAX_CONTAINERS
+MAX_MATCH_GROUPS = 16  # KG_MAX_MATCH_GROUPS (ABI 12)
+MAX_POD_PREFERRED = 4  # KG_MAX_POD_PREFERRED (ABI 12)
 DEV_NVIDIA_GPU, DEV_HYGON_DCU, DEV_KOORD_GPU, DEV_GPU_CORE, DEV_GPU_MEMORY, DEV_GPU_MEMORY_RATIO, DEV_FPGA, DEV_RDMA = \
     range(8)
 DEVICE_RESOURCE_SLOTS = {
@@ -100,6 +104,8 @@ CONFIG_DTYPE = np.dtype([
     _i64("affinity_filter"), _i64("affinity_score"), _i64("weight_affinity"),
     _i64("balanced_score"), _i64("weight_balanced"), _i64("balanced_resources"),
     _i64("image_score"), _i64("weight_image"),
+    _i64("spread_filter"), _i64("spread_score"), _i64("weight_spread"),
+    _i64("interpod_filter"), _i64("interpod_score"), _i64("weight_interpod"), _i64("hard_pod_affinity_weight"),
     _i64("reserved", 2),
 ])
 
@@ -143,6 +149,10 @@ POD_DTYPE = np.dtype([
     _i64("preferred_cpu_exclusive_policy"),
     _i64("n_containers"), _i64("container_image_bit", MAX_CONTAINERS), _i64("container_image_score", MAX_CONTAINERS),
     _i64("taint_count"),
+    _i64("match_groups"), _i64("spread_hard_group"), _i64("spread_hard_max_skew"), _i64("spread_soft_group"),
+    _i64("spread_soft_max_skew"), _i64("pod_affinity_group"), _i64("pod_affinity_terms"), _i64("pod_anti_affinity"),
+    _i64("n_pod_preferred"), _i64("pod_preferred_group", MAX_POD_PREFERRED),
+    _i64("pod_preferred_weight", MAX_POD_PREFERRED),
 ])
 NODE_PRED_DTYPE = np.dtype([("predicates", np.uint64), ("taints_hard", np.uint64), ("taints_soft", np.uint64),
                             ("images", np.uint64), _i64("predicate_count"), _i64("image_count")])
@@ -192,7 +202,7 @@ EXPORTED_SYMBOLS = (
     "kg_results_fetch_reservations", "kg_profile_enable", "kg_profile_read", "kg_loopback_create",
     "kg_loopback_destroy", "kg_engine_create_loopback", "kg_pods_unreserve", "kg_engine_set_clock",
     "kg_node_pods_metric_set", "kg_debug_numa_merge", "kg_pods_evaluate_reservation", "kg_nodes_predicates_upsert",
-    "kg_engine_create_hosted", "kg_pods_filter_preemption",
+    "kg_engine_create_hosted", "kg_pods_filter_preemption", "kg_nodes_read_pod_groups",
 )
 
 # int (*kg_exchange_fn)(void* user, const void* send, void* recv, int64_t bytes)
@@ -272,6 +282,7 @@ def load_library(path: str | None = None):
         "kg_debug_numa_merge": (i, [vp, vp, i64, vp]),
         "kg_pods_evaluate_reservation": (i, [vp, vp, vp]),
         "kg_pods_filter_preemption": (i, [vp, vp, ctypes.c_int32, vp, vp, i64, vp]),
+        "kg_nodes_read_pod_groups": (i, [vp, vp, vp, vp]),
         "kg_nodes_predicates_upsert": (i, [vp, vp, vp, i64]),
         "kg_engine_create_hosted": (i, [vp, i64, i, i, EXCHANGE_FN, vp, ctypes.POINTER(vp)]),
     }

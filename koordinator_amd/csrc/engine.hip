@@ -2563,7 +2563,8 @@ __global__ void unreserve_pods(DevTable T, const DevPod* __restrict__ pods, cons
                                int64_t* __restrict__ out_nrec, DsNode* __restrict__ ds, const DsPod* __restrict__ dpods,
                                int32_t* __restrict__ out_minors, RsvNode* __restrict__ RN, int32_t* __restrict__ out_rslot,
                                QuotaRow* __restrict__ quotas, int nq, const int64_t* __restrict__ qdev,
-                               const int64_t* __restrict__ paux) {
+                               const int64_t* __restrict__ paux, GroupTable G, const GroupPod* __restrict__ gpods,
+                               int hard_w) {
   if (blockIdx.x != 0 || threadIdx.x != 0) return;
   for (int64_t k = 0; k < n; ++k) {
     const int64_t j = idx[k];
@@ -2583,6 +2584,7 @@ __global__ void unreserve_pods(DevTable T, const DevPod* __restrict__ pods, cons
     r.la_pused_mem -= prod * p.est_mem;
     r.num_pods -= 1;
     store_mutable(T, w, r);
+    if (gpods) group_apply(G, w, gpods[j], -1, hard_w);  // the node's pod-group counters
     if (p.flags & P_AUX)  // ephemeral-storage / scalar Requested
       for (int q = 0; q < kAux; ++q) T.aux[(size_t)(kAux + q) * T.cap + w] -= paux[(size_t)j * kAux + q];
     if (nm) {  // nodenumaresource/plugin.go:417-425
@@ -2945,8 +2947,9 @@ struct kg_engine {
   std::vector<unsigned char> rsv_exec_sig;
   hipGraphExec_t rsv_exec1 = nullptr;  // one pass + rsv_apply (single-pod calls)
   std::vector<unsigned char> rsv_exec1_sig;
-  DevBuf<uint64_t> rsv_part;    // [6][blocks] per-block partials (preferred-node key, max raw, max key, max ds raw,
-                                // max taint count, max affinity sum)
+  DevBuf<uint64_t> rsv_part;    // [13][blocks] per-block partials (preferred-node key, max raw, max key, max ds raw,
+                                // max taint count, max affinity sum; (ABI 12) group_pre's min match / total, the
+                                // filtered-node count and the spread count / InterPodAffinity raw extremes)
   // TaintToleration / NodeAffinity / NodeResourcesBalancedAllocation (exact pass)
   bool def_on = false, def_score = false;
   DefParams DF{};
@@ -2960,6 +2963,15 @@ struct kg_engine {
   int64_t sq_taint_min = 64, sq_pred_top = 0, sq_img_top = 0;
   DevBuf<DefPod> defpods;       // [staged + kMaxB]
   DevBuf<uint32_t> rsv_val2;    // [cap] raw taint count << 24 | raw affinity sum (their Scores on)
+  // (ABI 12) PodTopologySpread / InterPodAffinity, hostname key (groups_dev.h): one pod per exact pass
+  bool grp_on = false;
+  GroupParams GP{};
+  DevBuf<int32_t> grp_d;        // [3][kGroups][cap] per-node group counters
+  DevBuf<GroupPod> gpods;       // [staged + kMaxB]
+  DevBuf<double> logw;          // [cap + 1] log(F + 2)
+  DevBuf<uint64_t> gval;        // [cap] InterPodAffinity raw << 32 | spread count
+  DevBuf<GroupPod> gdelta;      // kg_pods_add / kg_pods_remove: the pods' group view, their nodes and signs
+  DevBuf<int32_t> gdelta_ns;
   // batched exact rounds (xr_dev.h): kXrPods pods per round
   bool xr_on = true;            // KG_EXACT_ROUNDS=0: one pod per pass only
   DevBuf<uint64_t> xr_val;      // [kXrPods][cap]
@@ -3043,6 +3055,10 @@ int validate_config(const kg_config* c) {
       c->weight_balanced < 0 || c->weight_balanced > 1000000 || c->weight_image < 0 || c->weight_image > 1000000)
     return fail(KG_E_INVALID,
                 "TaintToleration / NodeAffinity / NodeResourcesBalancedAllocation / ImageLocality weight out of range");
+  if (c->weight_spread < 0 || c->weight_spread > 1000000 || c->weight_interpod < 0 || c->weight_interpod > 1000000)
+    return fail(KG_E_INVALID, "PodTopologySpread / InterPodAffinity weight out of range");
+  if ((c->interpod_filter || c->interpod_score) && (c->hard_pod_affinity_weight < 0 || c->hard_pod_affinity_weight > 100))
+    return fail(KG_E_INVALID, "InterPodAffinityArgs.HardPodAffinityWeight must be in [0, 100]");
   if (c->balanced_score && (c->balanced_resources & ~3ll))
     return fail(KG_E_UNSUPPORTED, "NodeResourcesBalancedAllocation resources: cpu / memory are accelerated");
   if (c->reservation_filter || c->reservation_score) {
@@ -3391,6 +3407,46 @@ int decode_def_pod(const kg_pod& p, DefPod& d, int64_t k) {
       d.img_w[d.nimg++] = 0;
     }
     d.img_w[at] += w;
+  }
+  return 0;
+}
+
+// (ABI 12) PodTopologySpread / InterPodAffinity view of one pod (groups 1-based in the ABI)
+int decode_group_pod(const kg_pod& p, GroupPod& d, int64_t k) {
+  d = GroupPod{};
+  auto grp = [&](int64_t g, int32_t& out, const char* what) -> int {
+    if (g < 0 || g > kGroups) return fail(KG_E_INVALID, "pod %lld: %s group %lld outside [0, %d]", (long long)k, what,
+                                          (long long)g, kGroups);
+    out = (int32_t)g - 1;
+    return 0;
+  };
+  const uint64_t all = kGroups >= 64 ? ~0ull : ((1ull << kGroups) - 1);
+  if (((uint64_t)p.match_groups | (uint64_t)p.pod_affinity_terms | (uint64_t)p.pod_anti_affinity) & ~all)
+    return fail(KG_E_INVALID, "pod %lld: a group bit beyond %d", (long long)k, kGroups);
+  d.match = (uint32_t)p.match_groups;
+  d.aff_terms = (uint32_t)p.pod_affinity_terms;
+  d.anti = (uint32_t)p.pod_anti_affinity;
+  if (int rc = grp(p.spread_hard_group, d.hard, "spread (DoNotSchedule)")) return rc;
+  if (int rc = grp(p.spread_soft_group, d.soft, "spread (ScheduleAnyway)")) return rc;
+  if (int rc = grp(p.pod_affinity_group, d.req, "pod affinity")) return rc;
+  if ((d.hard >= 0 && p.spread_hard_max_skew < 1) || (d.soft >= 0 && p.spread_soft_max_skew < 1) ||
+      p.spread_hard_max_skew > INT32_MAX || p.spread_soft_max_skew > INT32_MAX)
+    return fail(KG_E_INVALID, "pod %lld: maxSkew must be >= 1", (long long)k);
+  d.hard_skew = (int32_t)p.spread_hard_max_skew;
+  d.soft_skew = (int32_t)p.spread_soft_max_skew;
+  if (p.n_pod_preferred < 0 || p.n_pod_preferred > kPodPref)
+    return fail(KG_E_UNSUPPORTED, "pod %lld: more than %d preferred pod (anti-)affinity terms (the pod stays on the Go "
+                "path)", (long long)k, kPodPref);
+  d.npref = (int32_t)p.n_pod_preferred;
+  for (int t = 0; t < d.npref; ++t) {
+    int32_t g = -1;
+    if (int rc = grp(p.pod_preferred_group[t], g, "preferred term")) return rc;
+    const int64_t w = p.pod_preferred_weight[t];
+    if (g < 0 || w < -100 || w > 100 || w == 0)
+      return fail(KG_E_INVALID, "pod %lld: preferred term %d: group %lld weight %lld (weights in [1, 100], negative for "
+                  "anti-affinity)", (long long)k, t, (long long)p.pod_preferred_group[t], (long long)w);
+    d.pref_g[t] = g;
+    d.pref_w[t] = (int32_t)w;
   }
   return 0;
 }
@@ -4078,6 +4134,11 @@ RsvExt rsv_ext(kg_engine* e) {
   X.defp = e->def_on ? e->defpods.p : nullptr;
   X.DF = e->DF;
   X.val2 = e->def_score ? e->rsv_val2.p : nullptr;
+  X.G = GroupTable{e->grp_d.p, e->capacity};
+  X.gpods = e->grp_on ? e->gpods.p : nullptr;
+  X.GP = e->GP;
+  X.logw = e->logw.p;
+  X.gval = e->gval.p;
   return X;
 }
 
@@ -4094,6 +4155,9 @@ int run_rsv(kg_engine* e, int64_t first, int64_t count, kg_stats* stats, double 
     auto issue_group = [&](int64_t end_arg, int passes) {
       for (int g = 0; g < passes; ++g) {
         size_t t = prof_begin(e, e->stream);
+        if (e->grp_on)  // Reserve of the previous pod + the group reductions this pod's Filters need
+          group_pre<<<blocks, kRsvThreads, 0, e->stream>>>(e->T, e->rsv_d.p, e->pods.p, end_arg, n, g, X, e->rsv_val.p,
+                                                           e->rsv_part.p, e->out_keys.p, e->out_rslot.p, e->rsv_ws.p);
         rsv_eval<<<blocks, kRsvThreads, 0, e->stream>>>(e->T, e->rsv_d.p, e->rsv_nd.p, e->pods.p, e->rpods.p, end_arg, n,
                                                          g, e->P, e->RP, X, e->rsv_val.p, e->rsv_part.p, e->out_keys.p,
                                                          e->out_rslot.p, e->rsv_ws.p);
@@ -4392,6 +4456,10 @@ void kg_config_default(kg_config* c) {
   c->batch_pods = 32;
   c->pods_per_wave = 8;
   c->device_id = -1;
+  // (ABI 12) upstream v1beta2 defaults: PodTopologySpread weight 2, InterPodAffinity weight 1, HardPodAffinityWeight 1
+  c->weight_spread = 2;
+  c->weight_interpod = 1;
+  c->hard_pod_affinity_weight = 1;
 }
 
 int kg_debug_rccl_selftest(int device_id, int64_t n) {
@@ -4530,7 +4598,10 @@ static int engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank,
   e->numa_on = c.numa_filter || c.numa_score;
   e->ds_on = c.ds_filter || c.ds_score;
   e->rsv_on = c.reservation_filter || c.reservation_score;
-  e->def_on = c.taint_filter || c.taint_score || c.affinity_filter || c.affinity_score || c.balanced_score || c.image_score;
+  e->grp_on = c.spread_filter || c.spread_score || c.interpod_filter || c.interpod_score;
+  // (the group plugins read the pods' nodeSelector / required node affinity: the predicate tables come with them)
+  e->def_on = c.taint_filter || c.taint_score || c.affinity_filter || c.affinity_score || c.balanced_score ||
+              c.image_score || e->grp_on;
   e->def_score = c.taint_score || c.affinity_score;
   e->exact_on = e->rsv_on || (e->numa_on && e->ds_on) || e->def_on;
   // Exact profiles (Reservation, NodeNUMAResource + DeviceShare, the upstream defaults) on several ranks run as
@@ -4551,6 +4622,20 @@ static int engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank,
     if (e->def_score)
       if (int rc = e->rsv_val2.ensure(cap)) return bail(rc);
   }
+  e->GP = GroupParams{(int32_t)(c.spread_filter != 0), (int32_t)(c.spread_score != 0), (int32_t)c.weight_spread,
+                      (int32_t)(c.interpod_filter != 0), (int32_t)(c.interpod_score != 0), (int32_t)c.weight_interpod,
+                      (int32_t)c.hard_pod_affinity_weight, 0};
+  if (e->grp_on) {
+    if (int rc = e->grp_d.ensure((size_t)3 * kGroups * cap)) return bail(rc);
+    if (int rc = e->logw.ensure(cap + 1)) return bail(rc);
+    if (int rc = e->gval.ensure(cap)) return bail(rc);
+    std::vector<double> lw((size_t)cap + 1);
+    for (int64_t f = 0; f <= cap; ++f) lw[f] = std::log((double)(f + 2));  // TopologyNormalizingWeight
+    if (hipMemsetAsync(e->grp_d.p, 0, (size_t)3 * kGroups * cap * 4, e->stream) != hipSuccess ||
+        hipMemcpyAsync(e->logw.p, lw.data(), lw.size() * 8, hipMemcpyHostToDevice, e->stream) != hipSuccess ||
+        hipStreamSynchronize(e->stream) != hipSuccess)
+      return bail(fail(KG_E_DEVICE, "group tables"));
+  }
   e->RP.filter = (int32_t)(c.reservation_filter != 0);
   e->RP.score = (int32_t)(c.reservation_score != 0);
   e->RP.weight = (int32_t)c.weight_reservation;
@@ -4561,7 +4646,7 @@ static int engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank,
     if (int rc = e->rsv_nd.ensure(cap)) return bail(rc);
     if (int rc = e->rsv_val.ensure(cap)) return bail(rc);
     if (int rc = e->rsv_ws.ensure(8)) return bail(rc);
-    if (int rc = e->rsv_part.ensure(6 * ((cap + kRsvThreads - 1) / kRsvThreads) + 4)) return bail(rc);
+    if (int rc = e->rsv_part.ensure(13 * ((cap + kRsvThreads - 1) / kRsvThreads) + 4)) return bail(rc);
     if (hipMemsetAsync(e->rsv_nd.p, 0, cap * 4, e->stream) != hipSuccess || hipMemsetAsync(e->rsv_ws.p, 0, 64, e->stream) != hipSuccess)
       return bail(fail(KG_E_DEVICE, "hipMemset"));
   }
@@ -4593,7 +4678,8 @@ static int engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank,
                                    (c.numa_score ? c.weight_numa : 0) + (c.ds_score ? c.weight_deviceshare : 0) +
                                    (c.reservation_score ? c.weight_reservation : 0) +
                                    (c.taint_score ? c.weight_taint : 0) + (c.affinity_score ? c.weight_affinity : 0) +
-                                   (c.balanced_score ? c.weight_balanced : 0) + (c.image_score ? c.weight_image : 0));
+                                   (c.balanced_score ? c.weight_balanced : 0) + (c.image_score ? c.weight_image : 0) +
+                                   (c.spread_score ? c.weight_spread : 0) + (c.interpod_score ? c.weight_interpod : 0));
   e->P.score_bits = (int32_t)bits_for(max_total);
   // NodeResourcesFit + LoadAwareScheduling: assume only lowers a node's key; NodeNUMAResource does not
   e->P.monotone = (e->numa_on || e->ds_on || e->rsv_on) ? 0 : 1;  // DeviceShare: normalization couples every node's key
@@ -4800,6 +4886,12 @@ void kg_engine_destroy(kg_engine* e) {
   e->npred.release();
   e->defpods.release();
   e->rsv_val2.release();
+  e->grp_d.release();
+  e->gpods.release();
+  e->logw.release();
+  e->gval.release();
+  e->gdelta.release();
+  e->gdelta_ns.release();
   e->scratch64.release();
   e->scratch32.release();
   e->uidx.release();
@@ -4910,6 +5002,23 @@ static int pods_delta(kg_engine* e, const kg_pod* pods, const int32_t* node_idx,
         mirror_unassign(e, i, pods[k].uid, est);
     }
   }
+  if (e->grp_on && n > 0) {  // the nodes' pod-group counters (NodeInfo.AddPod / RemovePod of the pods' labels / terms)
+    std::vector<GroupPod> hg((size_t)n);
+    std::vector<int32_t> hn((size_t)(2 * n));
+    for (int64_t k = 0; k < n; ++k) {
+      if (int rc = decode_group_pod(pods[k], hg[k], k)) return rc;
+      hn[k] = (int32_t)node_idx[k];
+      hn[n + k] = sign;
+    }
+    if (int rc = e->gdelta.ensure(n)) return rc;
+    if (int rc = e->gdelta_ns.ensure(2 * n)) return rc;
+    HIP_TRY(hipMemcpyAsync(e->gdelta.p, hg.data(), n * sizeof(GroupPod), hipMemcpyHostToDevice, e->stream));
+    HIP_TRY(hipMemcpyAsync(e->gdelta_ns.p, hn.data(), 2 * n * 4, hipMemcpyHostToDevice, e->stream));
+    group_deltas<<<(unsigned)((n + 255) / 256), 256, 0, e->stream>>>(GroupTable{e->grp_d.p, e->capacity}, e->gdelta.p,
+                                                                      e->gdelta_ns.p, e->gdelta_ns.p + n, n, e->GP.hard_w);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(e->stream));
+  }
   if (e->pm_nodes > 0) {  // the PodsMetric terms of the touched nodes
     std::vector<char> seen((size_t)e->capacity, 0);
     for (int64_t k = 0; k < n; ++k) {
@@ -4955,7 +5064,9 @@ int kg_pods_unreserve(kg_engine* e, int64_t first, int64_t count, const uint8_t*
                                         e->numa_on ? e->numa_m.p : nullptr, e->out_cpus.p, e->out_nrec.p,
                                         e->ds_on ? e->ds_d.p : nullptr, e->dpods.p, e->out_minors.p,
                                         e->rsv_on ? e->rsv_d.p : nullptr, e->out_rslot.p, e->quotas.p, e->nq,
-                                        (e->ds_on || e->rsv_on) ? e->qdev.p : nullptr, e->paux.p);
+                                        (e->ds_on || e->rsv_on) ? e->qdev.p : nullptr, e->paux.p,
+                                        GroupTable{e->grp_d.p, e->capacity}, e->grp_on ? e->gpods.p : nullptr,
+                                        e->GP.hard_w);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(e->stream));
   e->eph_dirty |= e->eph_any;  // a release may end an ephemeral-storage overcommit
@@ -5055,6 +5166,13 @@ int kg_pods_stage(kg_engine* e, const kg_pod* pods, int64_t n) {
     if (int rc = e->defpods.ensure(n + kMaxB)) return rc;
     if (n > 0) HIP_TRY(hipMemcpyAsync(e->defpods.p, hf.data(), n * sizeof(DefPod), hipMemcpyHostToDevice, e->stream));
   }
+  if (e->grp_on) {  // PodTopologySpread / InterPodAffinity view of the pods
+    std::vector<GroupPod> hg(std::max<int64_t>(n, 1));
+    for (int64_t k = 0; k < n; ++k)
+      if (int rc = decode_group_pod(pods[k], hg[k], k)) return rc;
+    if (int rc = e->gpods.ensure(n + kMaxB)) return rc;
+    if (n > 0) HIP_TRY(hipMemcpyAsync(e->gpods.p, hg.data(), n * sizeof(GroupPod), hipMemcpyHostToDevice, e->stream));
+  }
   {  // exact-pass records (the Reservation view of every pod; single-pod calls of any profile use the pass)
     std::vector<RsvPod> hr(std::max<int64_t>(n, 1));
     for (int64_t k = 0; k < n; ++k) {
@@ -5135,7 +5253,9 @@ static int schedule_staged_impl(kg_engine* e, int64_t first, int64_t count, kg_s
   const double t0 = now_s();
   // the exact per-pod pass: its profiles, and calls of at most kExactSmall pods of any profile (the drop-in's per-pod
   // scheduleOne): one pass costs less than a round's eval + merge + resolve when a round would hold one pod
-  if (e->exact_on && e->xr_on && count >= kXrMin && e->n_nodes > 0) return run_xr(e, first, count, stats, t0);
+  // (PodTopologySpread / InterPodAffinity profiles: one pod per pass — the batched rounds' stop rules do not cover
+  // their cluster-wide minimum / count and min-max normalisation)
+  if (e->exact_on && e->xr_on && !e->grp_on && count >= kXrMin && e->n_nodes > 0) return run_xr(e, first, count, stats, t0);
   if (e->exact_on || (count <= kExactSmall && e->n_ranks == 1)) return run_rsv(e, first, count, stats, t0);
   RoundGeom g;
   if (int rc = prepare_rounds(e, g)) return rc;
@@ -5797,9 +5917,28 @@ int kg_nodes_read_reservations(kg_engine* e, int64_t* allocated_cpu, int64_t* al
   return 0;
 }
 
+int kg_nodes_read_pod_groups(kg_engine* e, int32_t* match_count, int32_t* anti_count, int32_t* sym_weight) {
+  if (!e) return fail(KG_E_INVALID, "engine is NULL");
+  if (!e->grp_on) return fail(KG_E_INVALID, "the profile enables neither PodTopologySpread nor InterPodAffinity");
+  const int64_t n = e->n_nodes, cap = e->capacity;
+  if (n == 0) return 0;
+  std::vector<int32_t> h((size_t)3 * kGroups * cap);
+  HIP_TRY(hipMemcpyAsync(h.data(), e->grp_d.p, h.size() * 4, hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  int32_t* outs[3] = {match_count, anti_count, sym_weight};
+  for (int a = 0; a < 3; ++a)
+    if (outs[a])
+      for (int64_t i = 0; i < n; ++i)
+        for (int k = 0; k < kGroups; ++k) outs[a][i * kGroups + k] = h[((size_t)a * kGroups + k) * cap + i];
+  return 0;
+}
+
 int kg_pods_evaluate_reservation(kg_engine* e, const kg_pod* pod, int64_t* out) {
   if (!e || !pod || !out) return fail(KG_E_INVALID, "null argument");
   if (!e->exact_on) return fail(KG_E_INVALID, "the profile does not run the exact pass (Reservation or NUMA + DeviceShare)");
+  if (e->grp_on)
+    return fail(KG_E_UNSUPPORTED, "kg_pods_evaluate_reservation: PodTopologySpread / InterPodAffinity need the pass's "
+                "cluster-wide reductions (use kg_pods_schedule)");
   if (int rc = sync_static(e)) return rc;
   DevPod d;
   if (int rc = decode_pod(e, *pod, d)) return rc;

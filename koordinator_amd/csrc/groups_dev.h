@@ -1,0 +1,146 @@
+// (ABI 12) PodTopologySpread and InterPodAffinity with topologyKey kubernetes.io/hostname on the exact per-pod pass
+// (SURVEY §8f-2).  The reference runs both from k8s.io/kubernetes v1.24.15 (not vendored), restated as published:
+//   podtopologyspread/common.go, filtering.go  PreFilter counts, per topology pair, the pods matching a DoNotSchedule
+//                                              constraint's selector in the pod's namespace over the nodes passing the
+//                                              pod's nodeSelector / required node affinity; Filter: matchNum +
+//                                              selfMatch − minMatchNum ≤ maxSkew (a node outside that set has no pair:
+//                                              matchNum 0).
+//   podtopologyspread/scoring.go               ScheduleAnyway: per node int64(cnt · log(size + 2) + maxSkew − 1), size
+//                                              = the filtered nodes (hostname); NormalizeScore MaxNodeScore · (max +
+//                                              min − s) / max, MaxNodeScore when max == 0 (also with no constraint).
+//   interpodaffinity/filtering.go              required affinity (count of pods matching all terms > 0, or no pod in
+//                                              the cluster matches them and the pod matches its own), required
+//                                              anti-affinity, existing pods' required anti-affinity.
+//   interpodaffinity/scoring.go                processExistingPod summed per node; NormalizeScore min–max in float64.
+// With the hostname key every node is its own topology domain, so the per-pair maps become per-node counters over the
+// caller's match groups (a label selector + namespaces, decided by the caller once per pod): an assume changes its
+// winner's counters only.  The globals a pod's Filter needs (the minimum match count over the eligible nodes, the
+// cluster-wide count of pods matching its required affinity) come from a reduction pass (group_pre) that runs after
+// the previous pod's Reserve; the Score normalisations reuse the exact pass's second kernel.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/koordgpu.h"
+#include "defaults_dev.h"
+#include "kernels.h"
+
+namespace kg {
+
+constexpr int kGroups = KG_MAX_MATCH_GROUPS;
+constexpr int kPodPref = KG_MAX_POD_PREFERRED;
+
+// per-node counters, structure of arrays [3][kGroups][cap] int32: pods matching group k, required anti-affinity
+// terms of group k on the node, Σ symmetric weights of the node's pods' terms of group k
+struct GroupTable {
+  int32_t* __restrict__ g;
+  int64_t cap;
+  __device__ __forceinline__ int32_t& cnt(int k, int64_t i) const { return g[(size_t)k * cap + i]; }
+  __device__ __forceinline__ int32_t& anti(int k, int64_t i) const { return g[(size_t)(kGroups + k) * cap + i]; }
+  __device__ __forceinline__ int32_t& symw(int k, int64_t i) const { return g[(size_t)(2 * kGroups + k) * cap + i]; }
+};
+
+struct GroupPod {  // 72 B per staged pod
+  uint32_t match, aff_terms, anti, pad;
+  int32_t hard, hard_skew;  // DoNotSchedule hostname constraint: group (-1 none), maxSkew
+  int32_t soft, soft_skew;  // ScheduleAnyway hostname constraint
+  int32_t req;              // conjunction group of the required pod-affinity terms (-1 none)
+  int32_t npref;
+  int32_t pref_g[kPodPref], pref_w[kPodPref];
+};
+
+struct GroupParams {
+  int32_t spread_filter, spread_score, w_spread;
+  int32_t ipa_filter, ipa_score, w_ipa;
+  int32_t hard_w;
+  int32_t pad;
+};
+
+// NodeInfo.AddPod / RemovePod (sign ±1) of a pod's group contributions on node i (atomics: the delta pass applies
+// several pods to one node at once; Reserve is one thread)
+__device__ __forceinline__ void group_apply(const GroupTable& G, int64_t i, const GroupPod& gp, int sign, int hard_w) {
+#pragma unroll
+  for (int k = 0; k < kGroups; ++k) {
+    if ((gp.match >> k) & 1u) atomicAdd(&G.cnt(k, i), sign);
+    if ((gp.anti >> k) & 1u) atomicAdd(&G.anti(k, i), sign);
+    if (hard_w > 0 && ((gp.aff_terms >> k) & 1u)) atomicAdd(&G.symw(k, i), sign * hard_w);
+  }
+  for (int t = 0; t < gp.npref; ++t) atomicAdd(&G.symw(gp.pref_g[t], i), sign * gp.pref_w[t]);
+}
+
+// PodMatchesNodeSelectorAndAffinityTerms: the pod's nodeSelector and required node affinity (the NodeAffinity Filter
+// without its profile switch); no predicate table = no node selector / affinity on the pod
+__device__ __forceinline__ bool node_affinity_match(const NodePred* pred, const DefPod* d, int64_t i) {
+  if (!pred || !d) return true;
+  const NodePred n = pred[i];
+  if ((n.pred & d->sel) != d->sel) return false;
+  if (d->nreq == 0) return true;
+  bool any = false;
+#pragma unroll
+  for (int k = 0; k < kAffTerms; ++k) any |= k < d->nreq && term_holds(n.pred, d->req[k]);
+  return any;
+}
+
+// Filters of both plugins on node i (true = feasible); min_match / total from group_pre
+__device__ __forceinline__ bool groups_filter(const GroupTable& G, int64_t i, const GroupPod& gp, const GroupParams& GP,
+                                              bool eligible, int64_t min_match, int64_t total) {
+  if (GP.spread_filter && gp.hard >= 0) {
+    const int64_t match = eligible ? G.cnt(gp.hard, i) : 0;
+    const int64_t self = (gp.match >> gp.hard) & 1u;
+    if (match + self - min_match > gp.hard_skew) return false;
+  }
+  if (GP.ipa_filter) {
+    if (gp.req >= 0 && G.cnt(gp.req, i) <= 0 && !(total == 0 && ((gp.match >> gp.req) & 1u))) return false;
+    for (int k = 0; k < kGroups; ++k) {
+      if (((gp.anti >> k) & 1u) && G.cnt(k, i) > 0) return false;
+      if (((gp.match >> k) & 1u) && G.anti(k, i) > 0) return false;
+    }
+  }
+  return true;
+}
+
+// InterPodAffinity raw Score on node i: the pod's preferred terms against the node's matching pods, plus the node's
+// pods' terms the pod matches
+__device__ __forceinline__ int32_t interpod_raw(const GroupTable& G, int64_t i, const GroupPod& gp) {
+  int32_t s = 0;
+  for (int t = 0; t < gp.npref; ++t) s += gp.pref_w[t] * G.cnt(gp.pref_g[t], i);
+  uint32_t m = gp.match;
+  while (m) {
+    const int k = __builtin_ctz(m);
+    m &= m - 1;
+    s += G.symw(k, i);
+  }
+  return s;
+}
+
+// PodTopologySpread raw Score of a count: int64(float64(cnt)·w + float64(maxSkew − 1)), w = log(F + 2) from the host's
+// table (the same libm as the checker); the product and the sum round separately (-ffp-contract=off)
+__device__ __forceinline__ int64_t spread_raw(int64_t cnt, const GroupPod& gp, double w) {
+  if (gp.soft < 0) return 0;
+  const double s = (double)cnt * w + (double)(gp.soft_skew - 1);
+  return (int64_t)s;
+}
+
+__device__ __forceinline__ int64_t spread_normalize(int64_t raw, int64_t mn, int64_t mx) {
+  return mx == 0 ? 100 : 100 * (mx + mn - raw) / mx;
+}
+
+__device__ __forceinline__ int64_t interpod_normalize(int64_t raw, int64_t mn, int64_t mx) {
+  const int64_t d = mx - mn;
+  return d <= 0 ? 0 : (int64_t)(100.0 * ((double)(raw - mn) / (double)d));
+}
+
+// order-preserving encodings for max-reductions of signed / min values
+__device__ __forceinline__ uint64_t enc_max_i32(int32_t v) { return (uint64_t)((int64_t)v + 0x80000000ll) + 1; }
+__device__ __forceinline__ int32_t dec_max_i32(uint64_t e) { return (int32_t)((int64_t)(e - 1) - 0x80000000ll); }
+__device__ __forceinline__ uint64_t enc_min_i32(int32_t v) { return 0x100000000ull - (uint64_t)((int64_t)v + 0x80000000ll); }
+__device__ __forceinline__ int32_t dec_min_i32(uint64_t e) { return (int32_t)((int64_t)(0x100000000ull - e) - 0x80000000ll); }
+
+__global__ void group_deltas(GroupTable G, const GroupPod* __restrict__ gp, const int32_t* __restrict__ node,
+                             const int32_t* __restrict__ sign, int64_t n, int hard_w) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  group_apply(G, node[k], gp[k], sign[k], hard_w);
+}
+
+}  // namespace kg

@@ -29,6 +29,7 @@
 #include "../../include/koordgpu.h"
 #include "defaults_dev.h"
 #include "ds_dev.h"
+#include "groups_dev.h"
 #include "kernels.h"
 #include "numa_dev.h"
 
@@ -81,6 +82,12 @@ struct RsvExt {
   const DefPod* __restrict__ defp;     // [pods]
   DefParams DF;
   uint32_t* __restrict__ val2;         // [cap] raw TaintToleration count << 24 | raw NodeAffinity sum (scores on)
+  // (ABI 12) PodTopologySpread / InterPodAffinity, hostname key (gpods = nullptr: neither in the profile)
+  GroupTable G;                        // per-node group counters
+  const GroupPod* __restrict__ gpods;  // [pods]
+  GroupParams GP;
+  const double* __restrict__ logw;     // [cap + 1]: log(F + 2), the host's libm
+  uint64_t* __restrict__ gval;         // [cap] InterPodAffinity raw << 32 | the spread constraint's count
 };
 
 struct RsvOut {
@@ -328,6 +335,22 @@ __device__ __forceinline__ uint64_t rsv_partials_max(const uint64_t* __restrict_
   for (int k = threadIdx.x & (kWave - 1); k < nb; k += kWave) v = part[k] > v ? part[k] : v;
   return wave_max_u64_dpp(v);
 }
+// Block sum (thread 0 holds it) and the sum of `nb` partials (every lane)
+__device__ __forceinline__ uint64_t rsv_block_sum(uint32_t v, uint64_t* s_red) {
+  v = wave_sum_u32(v);
+  const int w = threadIdx.x / kWave;
+  if ((threadIdx.x & (kWave - 1)) == 0) s_red[w] = v;
+  __syncthreads();
+  uint64_t t = 0;
+  if (threadIdx.x == 0)
+    for (int k = 0; k < kRsvThreads / kWave; ++k) t += s_red[k];
+  return t;
+}
+__device__ __forceinline__ uint64_t rsv_partials_sum(const uint64_t* __restrict__ part, int nb) {
+  uint32_t v = 0;
+  for (int k = threadIdx.x & (kWave - 1); k < nb; k += kWave) v += (uint32_t)part[k];
+  return wave_sum_u32(v);
+}
 
 // DeviceShare Reserve on one node (one thread): the first `count` fitting minors in (score desc, minor asc) order
 // (defaultAllocateDevices device_allocator.go:384-454 + sortDeviceResourcesByMinor device_resources.go:187-208),
@@ -439,6 +462,7 @@ __device__ __forceinline__ bool rsv_reserve(const DevTable& T, RsvNode* __restri
   r.la_pused_mem += prod * p.est_mem;
   r.num_pods += 1;
   store_mutable(T, w, r);
+  if (X.gpods) group_apply(X.G, w, X.gpods[j], +1, X.GP.hard_w);  // the node's pod-group counters
   KG_LANE_SUB(diag_j, 4);
   const int32_t slot = (int32_t)(v & 7) - 1;
   if (slot >= 0) {  // Allocated += quotav1.Mask(requests, ResourceNames): only the reservation's keys (0 = absent)
@@ -477,10 +501,10 @@ __global__ __launch_bounds__(kRsvThreads) void rsv_eval(DevTable T, RsvNode* __r
   const int nb = gridDim.x;
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   bool prev_placed = false;
-  if (g > 0) {  // Reserve of pod j - 1
+  if (g > 0) {  // Reserve of pod j - 1 (group profiles: group_pre ran it before this pass)
     const uint64_t k = rsv_partials_max(part + 2 * nb, nb);
     const int64_t w = k ? (int64_t)key_node(k) : -1;
-    if (i == w || (w < 0 && i == 0)) {
+    if (!X.gpods && (i == w || (w < 0 && i == 0))) {
       int32_t slot = -1;
       bool placed = false;
       if (w >= 0) placed = rsv_reserve(T, RN, w, val[w], pods[j - 1], X, j - 1, slot);
@@ -515,13 +539,29 @@ __global__ __launch_bounds__(kRsvThreads) void rsv_eval(DevTable T, RsvNode* __r
   }
   uint64_t pk = 0, rawv = 0, dsv = 0, tv = 0, av = 0;
   uint64_t v = 0;
+  int32_t scnt = 0, iraw = 0;  // PodTopologySpread count / InterPodAffinity raw Score of a feasible node
+  int64_t min_match = 0x7fffffff, total = 0;
+  GroupPod gp{};
+  if (X.gpods) {  // group_pre's reductions over the snapshot after pod j - 1's Reserve
+    gp = X.gpods[j];
+    const uint64_t e = rsv_partials_max(part + 6 * nb, nb);
+    if (e) min_match = dec_min_i32(e);
+    total = (int64_t)rsv_partials_sum(part + 7 * nb, nb);
+  }
   if (i < n) {
     const RsvPod rp = rpods[j];
     const DsPod* dp = X.ds ? &X.dpods[j] : nullptr;
     const NumaPod* np = X.ns ? &X.npods[j] : nullptr;
     const int64_t* aux = (X.paux && (p.flags & P_AUX)) ? X.paux + (size_t)j * kAux : nullptr;
     const DefPod* df = X.defp ? &X.defp[j] : nullptr;
-    const RsvOut o = rsv_eval_node(T, RN, rsv_n, i, p, rp, P, RP, X, dp, np, nullptr, aux, df);
+    RsvOut o = rsv_eval_node(T, RN, rsv_n, i, p, rp, P, RP, X, dp, np, nullptr, aux, df);
+    if (o.feas && X.gpods) {
+      o.feas = groups_filter(X.G, i, gp, X.GP, node_affinity_match(X.pred, df, i), min_match, total);
+      if (o.feas) {
+        scnt = gp.soft >= 0 ? X.G.cnt(gp.soft, i) : 0;
+        iraw = interpod_raw(X.G, i, gp);
+      }
+    }
     if (o.feas) {
       v = rsv_pack(o);
       pk = rsv_pref_key(o, (uint32_t)i);
@@ -536,6 +576,27 @@ __global__ __launch_bounds__(kRsvThreads) void rsv_eval(DevTable T, RsvNode* __r
   if (i < n) val[i] = v;
   const bool dscore = X.val2 != nullptr;  // TaintToleration / NodeAffinity Score in the profile
   if (dscore && i < n) X.val2[i] = (uint32_t)(tv << 24 | av);
+  if (X.gpods) {  // the NormalizeScore inputs of both plugins over the filtered nodes
+    const bool f = (v >> 7) & 1u;
+    if (i < n) X.gval[i] = ((uint64_t)(uint32_t)iraw << 32) | (uint32_t)scnt;
+    const uint64_t fc = rsv_block_sum(f ? 1u : 0u, s_red);
+    __syncthreads();
+    const uint64_t sx = rsv_block_max(f ? enc_max_i32(scnt) : 0, s_red);
+    __syncthreads();
+    const uint64_t sn = rsv_block_max(f ? enc_min_i32(scnt) : 0, s_red);
+    __syncthreads();
+    const uint64_t ix = rsv_block_max(f ? enc_max_i32(iraw) : 0, s_red);
+    __syncthreads();
+    const uint64_t in = rsv_block_max(f ? enc_min_i32(iraw) : 0, s_red);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      part[8 * nb + blockIdx.x] = fc;
+      part[9 * nb + blockIdx.x] = sx;
+      part[10 * nb + blockIdx.x] = sn;
+      part[11 * nb + blockIdx.x] = ix;
+      part[12 * nb + blockIdx.x] = in;
+    }
+  }
   pk = rsv_block_max(pk, s_red);
   __syncthreads();
   rawv = rsv_block_max(rawv, s_red);
@@ -590,16 +651,89 @@ __global__ __launch_bounds__(kRsvThreads) void rsv_select(const uint64_t* __rest
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t pref = pk ? (int64_t)(uint32_t)(~pk) : -1;
   const int64_t mx = pk ? (mraw > 1000 ? (int64_t)mraw : 1000) : (int64_t)mraw;
+  // PodTopologySpread / InterPodAffinity NormalizeScore over the filtered nodes (the raw spread score is monotone in
+  // the count, so its extremes are the extremes' scores)
+  GroupPod gp{};
+  double lw = 0;
+  int64_t smin = 0, smax = 0, imin = 0, imax = 0;
+  if (X.gpods) {
+    gp = X.gpods[j];
+    const int64_t F = (int64_t)rsv_partials_sum(part + 8 * nb, nb);
+    lw = X.logw[F < n ? F : n];
+    const uint64_t sx = rsv_partials_max(part + 9 * nb, nb), sn = rsv_partials_max(part + 10 * nb, nb);
+    const uint64_t ix = rsv_partials_max(part + 11 * nb, nb), in = rsv_partials_max(part + 12 * nb, nb);
+    smax = sx ? spread_raw(dec_max_i32(sx), gp, lw) : 0;
+    smin = sn ? spread_raw(dec_min_i32(sn), gp, lw) : 0;
+    imax = ix ? dec_max_i32(ix) : 0;
+    imin = in ? dec_min_i32(in) : 0;
+  }
   uint64_t key = 0;
   if (i < n) {
     const uint64_t v = val[i];
     if (v & (1ull << 7)) {
       const uint32_t v2 = X.val2 ? X.val2[i] : 0u;
-      key = make_key(rsv_total(v, v2, i == pref, mx, (int64_t)mds, mt, ma, RP, X), (uint32_t)i);
+      int64_t t = rsv_total(v, v2, i == pref, mx, (int64_t)mds, mt, ma, RP, X);
+      if (X.gpods) {
+        const uint64_t gv = X.gval[i];
+        if (X.GP.spread_score)
+          t += (int64_t)X.GP.w_spread * spread_normalize(spread_raw((int32_t)(uint32_t)gv, gp, lw), smin, smax);
+        if (X.GP.ipa_score) t += (int64_t)X.GP.w_ipa * interpod_normalize((int32_t)(gv >> 32), imin, imax);
+      }
+      key = make_key(t, (uint32_t)i);
     }
   }
   key = rsv_block_max(key, s_red);
   if (threadIdx.x == 0) part[2 * nb + blockIdx.x] = key;
+}
+
+// (ABI 12) Pass 0 of group profiles for pod j = cursor + g: the Reserve of pod j - 1 (as rsv_eval does without
+// groups: the thread owning the winner row), then the reductions pod j's Filters need over the snapshot after it:
+// part[6 nb + b] = min over the block's valid nodes passing the pod's nodeSelector / required node affinity of the
+// DoNotSchedule constraint's count (enc_min_i32; 0 = none: MaxInt32), part[7 nb + b] = Σ over valid nodes of pods
+// matching the required pod-affinity group.
+__global__ __launch_bounds__(kRsvThreads) void group_pre(DevTable T, RsvNode* __restrict__ RN,
+                                                         const DevPod* __restrict__ pods, int64_t end, int64_t n,
+                                                         int g, RsvExt X, const uint64_t* __restrict__ val,
+                                                         uint64_t* __restrict__ part, uint64_t* __restrict__ out_keys,
+                                                         int32_t* __restrict__ out_slot,
+                                                         unsigned long long* __restrict__ ws) {
+  __shared__ uint64_t s_red[kRsvThreads / kWave];
+  if (end < 0) end = (int64_t)ws[4];
+  const int64_t j = (int64_t)ws[3] + g;
+  if (j - 1 >= end || (g == 0 && j >= end)) return;  // uniform across the grid
+  const int nb = gridDim.x;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g > 0) {
+    const uint64_t k = rsv_partials_max(part + 2 * nb, nb);
+    const int64_t w = k ? (int64_t)key_node(k) : -1;
+    if (i == w || (w < 0 && i == 0)) {
+      int32_t slot = -1;
+      bool placed = false;
+      if (w >= 0) placed = rsv_reserve(T, RN, w, val[w], pods[j - 1], X, j - 1, slot);
+      out_keys[j - 1] = placed ? k : 0;
+      out_slot[j - 1] = slot;
+      if (placed && X.nq > 0 && pods[j - 1].quota >= 0) {
+        if (j >= end) rsv_quota_charge(X, pods[j - 1], j - 1);
+        else ws[0] = (unsigned long long)j;
+      }
+    }
+    if (j >= end) return;
+  }
+  const GroupPod gp = X.gpods[j];
+  uint64_t mn = 0;
+  uint32_t sm = 0;
+  if (i < n && (T.flags[i] & F_VALID)) {
+    if (X.GP.spread_filter && gp.hard >= 0 && node_affinity_match(X.pred, X.defp ? &X.defp[j] : nullptr, i))
+      mn = enc_min_i32(X.G.cnt(gp.hard, i));
+    if (X.GP.ipa_filter && gp.req >= 0) sm = (uint32_t)X.G.cnt(gp.req, i);
+  }
+  mn = rsv_block_max(mn, s_red);
+  __syncthreads();
+  const uint64_t st = rsv_block_sum(sm, s_red);
+  if (threadIdx.x == 0) {
+    part[6 * nb + blockIdx.x] = mn;
+    part[7 * nb + blockIdx.x] = st;
+  }
 }
 
 // End of a group of kRsvGroup pods (one wave): Reserve of the group's last pod (cursor + g_last) with its quota

@@ -33,6 +33,8 @@ RESERVATION = "Reservation"
 TAINT_TOLERATION, NODE_AFFINITY = "TaintToleration", "NodeAffinity"
 BALANCED_ALLOCATION = "NodeResourcesBalancedAllocation"
 IMAGE_LOCALITY = "ImageLocality"
+# (ABI 12) hostname-keyed PodTopologySpread (default weight 2) and InterPodAffinity (default weight 1)
+POD_TOPOLOGY_SPREAD, INTER_POD_AFFINITY = "PodTopologySpread", "InterPodAffinity"
 
 
 def _slots(d: dict | None, absent=0) -> np.ndarray:
@@ -90,9 +92,10 @@ def build_config(la: LoadAwareSchedulingArgs | None = None, fit: NodeResourcesFi
                  profile: Profile | None = None, batch_pods: int = 32, pods_per_wave: int = 8,
                  device_id: int = -1, numa: NodeNUMAResourceArgs | None = None,
                  deviceshare: DeviceShareArgs | None = None, pipeline_depth: int = 0,
-                 balanced_resources: tuple = ("cpu", "memory")) -> np.ndarray:
+                 balanced_resources: tuple = ("cpu", "memory"), hard_pod_affinity_weight: int = 1) -> np.ndarray:
     """kg_config of a profile.  balanced_resources: NodeResourcesBalancedAllocationArgs.resources (v1beta2 default
-    cpu + memory, weight 1 each; the weights do not enter the two-resource std)."""
+    cpu + memory, weight 1 each; the weights do not enter the two-resource std).  hard_pod_affinity_weight:
+    InterPodAffinityArgs.HardPodAffinityWeight (v1beta2 default 1)."""
     la = la or LoadAwareSchedulingArgs()
     fit = fit or NodeResourcesFitArgs()
     profile = profile or Profile()
@@ -151,6 +154,13 @@ def build_config(la: LoadAwareSchedulingArgs | None = None, fit: NodeResourcesFi
     r["balanced_resources"] = sum({"cpu": 1, "memory": 2}.get(k, 1 << 8) for k in balanced_resources)
     r["image_score"] = int(IMAGE_LOCALITY in profile.score)
     r["weight_image"] = int(profile.score.get(IMAGE_LOCALITY, 0))
+    r["spread_filter"] = int(POD_TOPOLOGY_SPREAD in profile.filter)
+    r["spread_score"] = int(POD_TOPOLOGY_SPREAD in profile.score)
+    r["weight_spread"] = int(profile.score.get(POD_TOPOLOGY_SPREAD, 0))
+    r["interpod_filter"] = int(INTER_POD_AFFINITY in profile.filter)
+    r["interpod_score"] = int(INTER_POD_AFFINITY in profile.score)
+    r["weight_interpod"] = int(profile.score.get(INTER_POD_AFFINITY, 0))
+    r["hard_pod_affinity_weight"] = hard_pod_affinity_weight
     r["ds_scoring_strategy"] = abi.STRATEGY[ds.scoring_strategy]
     r["ds_scoring_weights"] = [ds.scoring_resources.get("koordinator.sh/gpu-core", 0),
                                ds.scoring_resources.get("koordinator.sh/gpu-memory", 0),

@@ -257,3 +257,107 @@ class ImageTable:
             if nm in self.node_names[i]:
                 m |= 1 << b
         return m
+
+
+# ---- (ABI 12) PodTopologySpread / InterPodAffinity match groups ---------------------------------------------------
+def selector_matches(selector: dict | None, labels: dict) -> bool:
+    """metav1.LabelSelectorAsSelector(selector).Matches(labels): nil matches nothing, {} everything; matchLabels and
+    matchExpressions (In / NotIn / Exists / DoesNotExist) are ANDed."""
+    if selector is None:
+        return False
+    for k, v in (selector.get("matchLabels") or {}).items():
+        if labels.get(k) != v:
+            return False
+    for e in selector.get("matchExpressions") or ():
+        key, op, values = e["key"], e["operator"], tuple(e.get("values") or ())
+        has = key in labels
+        if op == "In" and not (has and labels[key] in values):
+            return False
+        if op == "NotIn" and has and labels[key] in values:
+            return False
+        if op == "Exists" and not has:
+            return False
+        if op == "DoesNotExist" and has:
+            return False
+        if op not in ("In", "NotIn", "Exists", "DoesNotExist"):
+            return False
+    return True
+
+
+HOSTNAME = "kubernetes.io/hostname"
+
+
+class PodGroupTable:
+    """The caller's match groups (≤ KG_MAX_MATCH_GROUPS): a label selector with its namespace set — a topology spread
+    constraint's selector in the pod's namespace (podtopologyspread/common.go countPodsMatchSelector), a pod-affinity
+    term's selector and namespaces (AffinityTerm.Matches; an empty namespace list means the term owner's namespace),
+    or the conjunction of a pod's required pod-affinity terms (updateWithAffinityTerms counts a pod only when it matches
+    all of them).  Register every group the cluster's pods and the queue use before filling pod rows: a row's
+    match_groups covers the groups registered when it was filled.  Only topologyKey kubernetes.io/hostname is
+    accelerated (another key raises NotImplementedError: the pod stays on the Go path)."""
+
+    def __init__(self):
+        self.groups: list[tuple] = []  # (kind, payload): ("sel", (selector_repr, namespaces)) / ("and", (gid, ...))
+        self._id: dict = {}
+        self._sel: list = []
+
+    def _intern(self, key, payload) -> int:
+        if key not in self._id:
+            if len(self.groups) == abi.MAX_MATCH_GROUPS:
+                raise OverflowError(f"more than {abi.MAX_MATCH_GROUPS} match groups: the pods stay on the Go path")
+            self._id[key] = len(self.groups)
+            self.groups.append(key)
+            self._sel.append(payload)
+        return self._id[key] + 1
+
+    def group(self, selector: dict | None, namespaces) -> int:
+        ns = frozenset(namespaces)
+        return self._intern(("sel", repr(selector), ns), ("sel", selector, ns))
+
+    def conjunction(self, gids) -> int:
+        gids = tuple(sorted(set(gids)))
+        return gids[0] if len(gids) == 1 else self._intern(("and", gids), ("and", gids, None))
+
+    def matches(self, gid: int, labels: dict, namespace: str) -> bool:
+        kind, a, b = self._sel[gid - 1]
+        if kind == "and":
+            return all(self.matches(g, labels, namespace) for g in a)
+        return namespace in b and selector_matches(a, labels)
+
+    def match_mask(self, labels: dict, namespace: str) -> int:
+        return sum(1 << (g - 1) for g in range(1, len(self.groups) + 1) if self.matches(g, labels, namespace))
+
+    def _term(self, t: dict, namespace: str) -> int:
+        if t.get("topologyKey", HOSTNAME) != HOSTNAME:
+            raise NotImplementedError("pod affinity topologyKey other than kubernetes.io/hostname")
+        return self.group(t.get("labelSelector"), t.get("namespaces") or (namespace,))
+
+    def fill_pod(self, pod: np.ndarray, labels: dict, namespace: str, spread=(), required_affinity=(),
+                 required_anti_affinity=(), preferred_affinity=(), preferred_anti_affinity=()) -> np.ndarray:
+        """The ABI 12 fields of one pod.  spread: [{maxSkew, whenUnsatisfiable, labelSelector, topologyKey}] (a pod
+        without constraints may pass the system default hostname one, maxSkew 3 ScheduleAnyway, with its owners'
+        selector); required_*: [{labelSelector, namespaces, topologyKey}]; preferred_*: [{weight, podAffinityTerm}]."""
+        r = pod[0] if pod.ndim else pod
+        hard = [c for c in spread if c.get("whenUnsatisfiable", "DoNotSchedule") == "DoNotSchedule"]
+        soft = [c for c in spread if c.get("whenUnsatisfiable") == "ScheduleAnyway"]
+        for c in spread:
+            if c.get("topologyKey", HOSTNAME) != HOSTNAME:
+                raise NotImplementedError("topology spread key other than kubernetes.io/hostname")
+        if len(hard) > 1 or len(soft) > 1:
+            raise ValueError("duplicate {topologyKey, whenUnsatisfiable} spread constraints")
+        for arr, (gk, sk) in ((hard, ("spread_hard_group", "spread_hard_max_skew")),
+                              (soft, ("spread_soft_group", "spread_soft_max_skew"))):
+            r[gk], r[sk] = (self.group(arr[0].get("labelSelector"), (namespace,)), arr[0]["maxSkew"]) if arr else (0, 0)
+        terms = [self._term(t, namespace) for t in required_affinity]
+        r["pod_affinity_terms"] = sum(1 << (g - 1) for g in set(terms))
+        r["pod_affinity_group"] = self.conjunction(terms) if terms else 0
+        r["pod_anti_affinity"] = sum(1 << (self._term(t, namespace) - 1) for t in required_anti_affinity)
+        pref = [(self._term(t["podAffinityTerm"], namespace), t["weight"]) for t in preferred_affinity]
+        pref += [(self._term(t["podAffinityTerm"], namespace), -t["weight"]) for t in preferred_anti_affinity]
+        if len(pref) > abi.MAX_POD_PREFERRED:
+            raise NotImplementedError(f"more than {abi.MAX_POD_PREFERRED} preferred pod affinity terms")
+        r["n_pod_preferred"] = len(pref)
+        for t, (g, w) in enumerate(pref):
+            r["pod_preferred_group"][t], r["pod_preferred_weight"][t] = g, w
+        r["match_groups"] = self.match_mask(labels, namespace)
+        return pod

@@ -580,3 +580,39 @@ def make_images(n_nodes: int, pods: np.ndarray, preds: np.ndarray, seed: int = B
     preds["images"] = [table.node_mask(i) for i in range(n_nodes)]
     preds["image_count"] = table.image_count()
     return table
+
+
+# ---- (ABI 12) PodTopologySpread / InterPodAffinity (hostname key) ------------------------------------------------
+def make_pod_groups(pods: np.ndarray, seed: int = BASE_SEED + 17, n_apps: int = 8) -> np.ndarray:
+    """Fills the ABI 12 group fields of `pods` in place, as PodGroupTable would compile them for a workload of n_apps
+    deployments (groups 1..n_apps: app=k in the namespace) in n_apps / 2 teams (groups n_apps+1..: team=t): every pod
+    matches its app and team; 40 % carry a DoNotSchedule hostname spread constraint on their app (maxSkew 1-3), 50 % a
+    ScheduleAnyway one (maxSkew 1-5), 15 % a required anti-affinity to their own app (one per node), 10 % a required
+    affinity to another team, 30 % one or two preferred (anti-)affinity terms (weights ±1..100)."""
+    rng = np.random.default_rng(seed)
+    n = len(pods)
+    n_teams = n_apps // 2
+    app = rng.integers(0, n_apps, n)
+    team = app // 2
+    pods["match_groups"] = (1 << app) | (1 << (n_apps + team))
+    hard = rng.random(n) < 0.4
+    pods["spread_hard_group"] = np.where(hard, app + 1, 0)
+    pods["spread_hard_max_skew"] = np.where(hard, rng.integers(1, 4, n), 0)
+    soft = rng.random(n) < 0.5
+    pods["spread_soft_group"] = np.where(soft, app + 1, 0)
+    pods["spread_soft_max_skew"] = np.where(soft, rng.integers(1, 6, n), 0)
+    anti = rng.random(n) < 0.15
+    pods["pod_anti_affinity"] = np.where(anti, 1 << app, 0)
+    aff = rng.random(n) < 0.10
+    other = (team + rng.integers(1, n_teams, n)) % n_teams
+    pods["pod_affinity_group"] = np.where(aff, n_apps + other + 1, 0)
+    pods["pod_affinity_terms"] = np.where(aff, 1 << (n_apps + other), 0)
+    npref = np.where(rng.random(n) < 0.3, rng.integers(1, 3, n), 0)
+    pods["n_pod_preferred"] = npref
+    for t in range(2):
+        on = npref > t
+        g = rng.integers(1, n_apps + n_teams + 1, n)
+        w = rng.integers(1, 101, n) * np.where(rng.random(n) < 0.4, -1, 1)
+        pods["pod_preferred_group"][:, t] = np.where(on, g, 0)
+        pods["pod_preferred_weight"][:, t] = np.where(on, w, 0)
+    return pods

@@ -89,3 +89,77 @@ int64_t or_normalize_default(int64_t score, int64_t max_count, int reverse) {
   int64_t s = 100 * score / max_count;
   return reverse ? 100 - s : s;
 }
+
+/* ---- (ABI 12) PodTopologySpread / InterPodAffinity, topologyKey kubernetes.io/hostname ---------------------------- */
+
+/* The counters a pod contributes to its node: countPodsMatchSelector (podtopologyspread/common.go, and the
+ * interpodaffinity PreFilter / PreScore matches of existing pods against the incoming pod's terms) counts it in every
+ * group it matches; its required anti-affinity terms feed existingAntiAffinityCounts (filtering.go
+ * getExistingAntiAffinityCounts); its terms matched by a later incoming pod feed that pod's topologyScore
+ * (scoring.go processExistingPod: required affinity × HardPodAffinityWeight when > 0, preferred ± weight). */
+void or_groups_apply(or_group_node* g, const kg_pod* pod, int sign, int64_t hard_weight) {
+  for (int k = 0; k < KG_MAX_MATCH_GROUPS; k++) {
+    if ((pod->match_groups >> k) & 1) g->cnt[k] += sign;
+    if ((pod->pod_anti_affinity >> k) & 1) g->anti[k] += sign;
+    if (hard_weight > 0 && ((pod->pod_affinity_terms >> k) & 1)) g->symw[k] += sign * (int32_t)hard_weight;
+  }
+  for (int64_t t = 0; t < pod->n_pod_preferred; t++) {
+    const int64_t k = pod->pod_preferred_group[t] - 1;
+    if (k >= 0 && k < KG_MAX_MATCH_GROUPS) g->symw[k] += sign * (int32_t)pod->pod_preferred_weight[t];
+  }
+}
+
+/* filtering.go Filter: skew = matchNum + selfMatchNum − minMatchNum (TpKeyToCriticalPaths[key][0], the minimum over
+ * the pairs PreFilter counted: nodes passing the pod's nodeSelector / required node affinity); a node outside that
+ * set has no pair, so its matchNum is 0.  selfMatchNum: the constraint's selector matches the pod's own labels. */
+int or_spread_filter(const or_group_node* g, const kg_pod* pod, int eligible, int64_t min_match) {
+  const int64_t k = pod->spread_hard_group - 1;
+  if (k < 0) return 1;
+  const int64_t match = eligible ? g->cnt[k] : 0;
+  const int64_t self = (pod->match_groups >> k) & 1;
+  return match + self - min_match <= pod->spread_hard_max_skew;
+}
+
+/* scoring.go: TopologyNormalizingWeight = log(size + 2) with size = len(filteredNodes) − len(IgnoredNodes) for the
+ * hostname key (no node lacks it); scoreForCount = float64(cnt)·weight + float64(maxSkew − 1), summed from 0 and
+ * truncated by int64() (no fused multiply-add: -ffp-contract=off). */
+int64_t or_spread_raw(int64_t cnt, const kg_pod* pod, int64_t n_feasible) {
+  if (pod->spread_soft_group <= 0) return 0;
+  const double w = log((double)(n_feasible + 2));
+  const double s = (double)cnt * w + (double)(pod->spread_soft_max_skew - 1);
+  return (int64_t)s;
+}
+
+int64_t or_spread_normalize(int64_t raw, int64_t mn, int64_t mx) {
+  if (mx == 0) return 100;
+  return 100 * (mx + mn - raw) / mx;
+}
+
+int or_interpod_filter(const or_group_node* g, const kg_pod* pod, const int64_t* total) {
+  const int64_t a = pod->pod_affinity_group - 1;
+  if (a >= 0 && g->cnt[a] <= 0) {  /* satisfyPodAffinity */
+    if (!(total[a] == 0 && ((pod->match_groups >> a) & 1))) return 0;
+  }
+  for (int k = 0; k < KG_MAX_MATCH_GROUPS; k++) {
+    if (((pod->pod_anti_affinity >> k) & 1) && g->cnt[k] > 0) return 0;  /* satisfyPodAntiAffinity */
+    if (((pod->match_groups >> k) & 1) && g->anti[k] > 0) return 0;      /* satisfyExistingPodsAntiAffinity */
+  }
+  return 1;
+}
+
+int64_t or_interpod_raw(const or_group_node* g, const kg_pod* pod) {
+  int64_t s = 0;
+  for (int64_t t = 0; t < pod->n_pod_preferred; t++) {
+    const int64_t k = pod->pod_preferred_group[t] - 1;
+    if (k >= 0 && k < KG_MAX_MATCH_GROUPS) s += pod->pod_preferred_weight[t] * (int64_t)g->cnt[k];
+  }
+  for (int k = 0; k < KG_MAX_MATCH_GROUPS; k++)
+    if ((pod->match_groups >> k) & 1) s += g->symw[k];
+  return s;
+}
+
+int64_t or_interpod_normalize(int64_t raw, int64_t mn, int64_t mx) {
+  const int64_t d = mx - mn;
+  if (d <= 0) return 0;
+  return (int64_t)(100.0 * ((double)(raw - mn) / (double)d));
+}

@@ -40,6 +40,34 @@ int64_t or_balanced_score(int64_t alloc_cpu, int64_t alloc_mem, int64_t req_cpu,
 /* DefaultNormalizeScore(MaxNodeScore, reverse) of one score against the maximum over the scored nodes. */
 int64_t or_normalize_default(int64_t score, int64_t max_count, int reverse);
 
+/* (ABI 12) PodTopologySpread / InterPodAffinity with topologyKey kubernetes.io/hostname (k8s v1.24.15
+ * podtopologyspread/{common,filtering,scoring}.go, interpodaffinity/{filtering,scoring}.go; not vendored, restated as
+ * published — "parity unpinned" beyond tests/test_pod_groups.py's hand-derived cases).  Each node is its own
+ * topology domain, so the plugins' per-domain maps become per-node counters over the caller's match groups. */
+typedef struct or_group_node {
+  int32_t cnt[KG_MAX_MATCH_GROUPS];   /* pods on the node matching group k (countPodsMatchSelector)        */
+  int32_t anti[KG_MAX_MATCH_GROUPS];  /* required anti-affinity terms of group k held by the node's pods   */
+  int32_t symw[KG_MAX_MATCH_GROUPS];  /* Σ symmetric weights of the node's pods' terms of group k          */
+} or_group_node;
+/* NodeInfo.AddPod / RemovePod of `pod` (sign ±1) on one node's counters. */
+void or_groups_apply(or_group_node* g, const kg_pod* pod, int sign, int64_t hard_weight);
+/* PodTopologySpread Filter (filtering.go Filter): matchNum (0 off the eligible set) + selfMatch − minMatchNum ≤
+ * maxSkew for the DoNotSchedule hostname constraint; 1 = pass. */
+int or_spread_filter(const or_group_node* g, const kg_pod* pod, int eligible, int64_t min_match);
+/* PodTopologySpread Score (scoring.go Score) before normalisation: int64(cnt · log(F + 2) + (maxSkew − 1)) for the
+ * ScheduleAnyway hostname constraint, F = the number of filtered nodes; 0 without one. */
+int64_t or_spread_raw(int64_t cnt, const kg_pod* pod, int64_t n_feasible);
+/* PodTopologySpread NormalizeScore: MaxNodeScore · (max + min − s) / max, MaxNodeScore when max == 0. */
+int64_t or_spread_normalize(int64_t raw, int64_t mn, int64_t mx);
+/* InterPodAffinity Filter (filtering.go Filter): required affinity (the conjunction group, or the first pod of a
+ * series: no pod in the cluster matches and the pod matches its own terms), required anti-affinity, existing pods'
+ * anti-affinity; 1 = pass.  total[k] = pods in the cluster matching group k. */
+int or_interpod_filter(const or_group_node* g, const kg_pod* pod, const int64_t* total);
+/* InterPodAffinity Score (scoring.go processExistingPod summed per node) before normalisation. */
+int64_t or_interpod_raw(const or_group_node* g, const kg_pod* pod);
+/* InterPodAffinity NormalizeScore: int64(MaxNodeScore · float64(s − min) / float64(max − min)), 0 when max == min. */
+int64_t or_interpod_normalize(int64_t raw, int64_t mn, int64_t mx);
+
 #ifdef __cplusplus
 }
 #endif

@@ -98,7 +98,21 @@ def lib():
         L.or_schedule_resv.argtypes = [vp, i64, vp, vp, vp, vp, i64, vp, i64, vp, vp, vp]
         L.or_schedule_resv.restype = i
         L.or_schedule_resv_full.argtypes = [vp, i64, vp, vp, vp, vp, vp, vp, i64, i64, vp, i64, i, vp, vp, vp, vp,
-                                            vp, vp, vp, vp]
+                                            vp, vp, vp, vp, vp]
+        L.or_groups_apply.argtypes = [vp, vp, i, i64]
+        L.or_groups_apply.restype = None
+        L.or_spread_filter.argtypes = [vp, vp, i, i64]
+        L.or_spread_filter.restype = i
+        L.or_spread_raw.argtypes = [i64, vp, i64]
+        L.or_spread_raw.restype = i64
+        L.or_spread_normalize.argtypes = [i64, i64, i64]
+        L.or_spread_normalize.restype = i64
+        L.or_interpod_filter.argtypes = [vp, vp, vp]
+        L.or_interpod_filter.restype = i
+        L.or_interpod_raw.argtypes = [vp, vp]
+        L.or_interpod_raw.restype = i64
+        L.or_interpod_normalize.argtypes = [i64, i64, i64]
+        L.or_interpod_normalize.restype = i64
         L.or_schedule_resv_full.restype = i
         L.or_quota_admit.argtypes = [vp, vp]
         L.or_quota_admit.restype = i
@@ -191,8 +205,28 @@ def unreserve(cfg, st, pod, node: int, numa_buf=None, devices=None, rsv=None, qu
 p = abi.ptr
 
 
+# (ABI 12) or_group_node: per node and match group, pods matching / required anti-affinity terms / symmetric weights
+GROUP_DTYPE = np.dtype([("cnt", np.int32, (abi.MAX_MATCH_GROUPS,)), ("anti", np.int32, (abi.MAX_MATCH_GROUPS,)),
+                        ("symw", np.int32, (abi.MAX_MATCH_GROUPS,))])
+
+
+def groups_init(n_nodes: int, pods=None, node_idx=None, hard_weight: int = 1) -> np.ndarray:
+    """or_group_node[n_nodes] with `pods` on nodes `node_idx` added (or_groups_apply, NodeInfo.AddPod)."""
+    g = np.zeros(max(n_nodes, 1), dtype=GROUP_DTYPE)
+    if pods is not None:
+        pods = np.ascontiguousarray(pods, dtype=abi.POD_DTYPE)
+        for k in range(len(pods)):
+            groups_apply(g, int(node_idx[k]), pods[k:k + 1], 1, hard_weight)
+    return g
+
+
+def groups_apply(g, node: int, pod, sign: int, hard_weight: int = 1):
+    row = g[node:node + 1]
+    lib().or_groups_apply(p(row), p(np.ascontiguousarray(pod, dtype=abi.POD_DTYPE)), sign, hard_weight)
+
+
 def schedule_resv(cfg, nodes, metrics, st, rsv, pods, now_ns: int, devices=None, quotas=None, n_threads: int = 1,
-                  with_minors: bool = False, numa_buf=None, with_numa: bool = False, preds=None):
+                  with_minors: bool = False, numa_buf=None, with_numa: bool = False, preds=None, groups=None):
     """Sequential FIFO scheduling through the per-pod exact loop: NodeResourcesFit + LoadAware + Reservation
     [+ DeviceShare + NodeNUMAResource + ElasticQuota + TaintToleration / NodeAffinity over `preds` (NODE_PRED_DTYPE
     rows) + BalancedAllocation] (st, rsv, devices, numa_buf, quotas mutated; the node loop of each
@@ -209,7 +243,8 @@ def schedule_resv(cfg, nodes, metrics, st, rsv, pods, now_ns: int, devices=None,
     rc = lib().or_schedule_resv_full(p(cfg), len(nodes), p(nodes), p(metrics), p(st), p(rsv), p(devices), p(quotas),
                                      nq, len(pods), p(pods), now_ns, n_threads, p(out_node), p(out_score), p(out_slot),
                                      p(out_minors), p(numa_buf), p(cpus), p(nalloc),
-                                     p(None if preds is None else np.ascontiguousarray(preds, dtype=abi.NODE_PRED_DTYPE)))
+                                     p(None if preds is None else np.ascontiguousarray(preds, dtype=abi.NODE_PRED_DTYPE)),
+                                     p(groups))
     if rc != 0:
         raise RuntimeError(f"oracle or_schedule_resv_full failed: {rc}")
     out = (out_node[:len(pods)], out_score[:len(pods)], out_slot[:len(pods)])

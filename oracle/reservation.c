@@ -216,15 +216,22 @@ int or_schedule_resv(const kg_config* cfg, int64_t n_nodes, const kg_node* nodes
                      or_node_state* st, kg_node_reservations* rsv, int64_t n_pods, const kg_pod* pods, int64_t now,
                      int32_t* out_node, int64_t* out_score, int32_t* out_slot) {
   return or_schedule_resv_full(cfg, n_nodes, nodes, metrics, st, rsv, NULL, NULL, 0, n_pods, pods, now, 1, out_node,
-                               out_score, out_slot, NULL, NULL, NULL, NULL, NULL);
+                               out_score, out_slot, NULL, NULL, NULL, NULL, NULL, NULL);
 }
 
 int or_schedule_resv_full(const kg_config* cfg, int64_t n_nodes, const kg_node* nodes, const kg_node_metric* metrics,
                           or_node_state* st, kg_node_reservations* rsv, kg_node_device* dev, kg_quota* quotas,
                           int64_t n_quotas, int64_t n_pods, const kg_pod* pods, int64_t now, int n_threads,
                           int32_t* out_node, int64_t* out_score, int32_t* out_slot, int32_t* out_minors,
-                          void* numa_states, uint64_t* out_cpus, int64_t* out_numa, const kg_node_predicates* preds) {
+                          void* numa_states, uint64_t* out_cpus, int64_t* out_numa, const kg_node_predicates* preds,
+                          void* groups) {
   const size_t nn = (size_t)(n_nodes > 0 ? n_nodes : 1);
+  or_group_node* grp = (or_group_node*)groups;
+  const int spread_on = grp && (cfg->spread_filter || cfg->spread_score);
+  const int ipa_on = grp && (cfg->interpod_filter || cfg->interpod_score);
+  int64_t* scnt = (int64_t*)calloc(nn, sizeof(int64_t)); /* PodTopologySpread: the soft constraint's count */
+  int64_t* iraw = (int64_t*)calloc(nn, sizeof(int64_t)); /* InterPodAffinity raw Score */
+  if (!scnt || !iraw) { free(scnt); free(iraw); return KG_E_NOMEM; }
   or_numa_node* numa = (or_numa_node*)numa_states;
   const int numa_on = numa && (cfg->numa_filter || cfg->numa_score);
   or_hint* aff = numa_on ? (or_hint*)calloc(nn, sizeof(or_hint)) : NULL;
@@ -281,6 +288,20 @@ int or_schedule_resv_full(const kg_config* cfg, int64_t n_nodes, const kg_node* 
     const int ds_blocks_nomination = ds_on && cfg->ds_filter && !dsp.skip;
     or_numa_pod npod;
     if (numa_on) or_numa_pod_init(cfg, pod, &npod);
+    /* PodTopologySpread PreFilter (common.go calPreFilterState): the minimum match count over the nodes passing the
+     * pod's nodeSelector / required node affinity (MaxInt32 when none); InterPodAffinity PreFilter: the cluster-wide
+     * count of pods matching each group (len(affinityCounts) == 0 ⇔ no pod matches the required terms) */
+    int64_t min_match = INT32_MAX, total[KG_MAX_MATCH_GROUPS] = {0};
+    if ((spread_on && cfg->spread_filter && pod->spread_hard_group > 0) || (ipa_on && cfg->interpod_filter)) {
+      for (int64_t i = 0; i < n_nodes; i++) {
+        if (!(nodes[i].flags & KG_NODE_VALID)) continue;
+        for (int k = 0; k < KG_MAX_MATCH_GROUPS; k++) total[k] += grp[i].cnt[k];
+        if (spread_on && pod->spread_hard_group > 0 && or_affinity_filter(preds ? &preds[i] : &zero_pred, pod)) {
+          const int64_t c = grp[i].cnt[pod->spread_hard_group - 1];
+          if (c < min_match) min_match = c;
+        }
+      }
+    }
     int err = 0;
 #pragma omp parallel for schedule(dynamic, chunk) num_threads(n_threads) reduction(min : err)
     for (int64_t i = 0; i < n_nodes; i++) {
@@ -315,7 +336,13 @@ int or_schedule_resv_full(const kg_config* cfg, int64_t n_nodes, const kg_node* 
             !or_numa_filter(cfg, &numa[i], &npod, &aff[i], rs.requested[KG_RES_CPU], nd->allocatable[KG_RES_CPU]))
           continue;
       }
+      if (spread_on && cfg->spread_filter &&
+          !or_spread_filter(&grp[i], pod, or_affinity_filter(np, pod), min_match))
+        continue;
+      if (ipa_on && cfg->interpod_filter && !or_interpod_filter(&grp[i], pod, total)) continue;
       feas[i] = 1;
+      scnt[i] = (spread_on && pod->spread_soft_group > 0) ? grp[i].cnt[pod->spread_soft_group - 1] : 0;
+      iraw[i] = ipa_on ? or_interpod_raw(&grp[i], pod) : 0;
       int64_t t = 0;
       if (cfg->fit_score) t += cfg->weight_fit * or_fit_score(cfg, nd, &rs, pod);
       if (cfg->la_score) {
@@ -348,6 +375,19 @@ int or_schedule_resv_full(const kg_config* cfg, int64_t n_nodes, const kg_node* 
     for (int64_t i = 0; i < n_nodes; i++)
       if (feas[i] && order[i] != 0 && best_order > order[i]) { best_order = order[i]; pref = i; }
     int64_t mx = 0, mds = 0, mt = 0, ma = 0;
+    /* PodTopologySpread / InterPodAffinity NormalizeScore inputs over the filtered nodes: the raw spread score is
+     * monotone in the count, so its extremes are those of the count */
+    int64_t n_feas = 0, smin = INT64_MAX, smax = INT64_MIN, imin = INT64_MAX, imax = INT64_MIN;
+    for (int64_t i = 0; i < n_nodes; i++) {
+      if (!feas[i]) continue;
+      n_feas++;
+      if (scnt[i] < smin) smin = scnt[i];
+      if (scnt[i] > smax) smax = scnt[i];
+      if (iraw[i] < imin) imin = iraw[i];
+      if (iraw[i] > imax) imax = iraw[i];
+    }
+    const int64_t sraw_min = n_feas ? or_spread_raw(smin, pod, n_feas) : 0;
+    const int64_t sraw_max = n_feas ? or_spread_raw(smax, pod, n_feas) : 0;
     for (int64_t i = 0; i < n_nodes; i++) {
       if (!feas[i]) continue;
       if (tcnt[i] > mt) mt = tcnt[i];
@@ -367,6 +407,9 @@ int or_schedule_resv_full(const kg_config* cfg, int64_t n_nodes, const kg_node* 
       /* TaintToleration NormalizeScore (reverse) and NodeAffinity NormalizeScore × weight */
       if (cfg->taint_score) t += cfg->weight_taint * or_normalize_default(tcnt[i], mt, 1);
       if (cfg->affinity_score) t += cfg->weight_affinity * or_normalize_default(asum[i], ma, 0);
+      if (spread_on && cfg->spread_score)
+        t += cfg->weight_spread * or_spread_normalize(or_spread_raw(scnt[i], pod, n_feas), sraw_min, sraw_max);
+      if (ipa_on && cfg->interpod_score) t += cfg->weight_interpod * or_interpod_normalize(iraw[i], imin, imax);
       if (t > win_total) { win_total = t; win = i; }
     }
     /* Reserve in the profile's order (scheduler-config.yaml:92-98): NodeNUMAResource (the exact cpuset), then
@@ -410,9 +453,11 @@ int or_schedule_resv_full(const kg_config* cfg, int64_t n_nodes, const kg_node* 
         if (out_slot) out_slot[p] = nom[win];
       }
       if (quota) or_quota_charge(quota, pod);
+      if (grp) or_groups_apply(&grp[win], pod, 1, cfg->hard_pod_affinity_weight);
     }
   }
   free(feas); free(base); free(raw); free(dsraw); free(order); free(nom); free(aff); free(tcnt); free(asum);
+  free(scnt); free(iraw);
   return rc;
 }
 

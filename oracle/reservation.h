@@ -61,14 +61,16 @@ int or_schedule_resv(const kg_config* cfg, int64_t n_nodes, const kg_node* nodes
                      int32_t* out_node, int64_t* out_score, int32_t* out_slot);
 
 /* The exact per-pod cycle (C5, the shipped profile, TaintToleration / NodeAffinity / BalancedAllocation when the
- * config enables them, over `preds`, NULL = no predicates / taints): NodeResourcesFit + LoadAwareScheduling + Reservation + DeviceShare (+ ElasticQuota admission when
+ * config enables them, over `preds`, NULL = no predicates / taints; (ABI 12) PodTopologySpread / InterPodAffinity over
+ * `groups` = or_group_node[n_nodes] (defaults.h), NULL = none — mutated by Reserve): NodeResourcesFit + LoadAwareScheduling + Reservation + DeviceShare (+ ElasticQuota admission when
  * pods carry quota_id).  `dev` / `quotas` may be NULL.  The node loop of every pod runs on n_threads OpenMP threads
  * (Parallelizer chunking); reductions and Reserve are sequential.  out_minors (nullable) = DeviceShare's minors. */
 int or_schedule_resv_full(const kg_config* cfg, int64_t n_nodes, const kg_node* nodes, const kg_node_metric* metrics,
                           or_node_state* st, kg_node_reservations* rsv, kg_node_device* dev, kg_quota* quotas,
                           int64_t n_quotas, int64_t n_pods, const kg_pod* pods, int64_t now, int n_threads,
                           int32_t* out_node, int64_t* out_score, int32_t* out_slot, int32_t* out_minors,
-                          void* numa_states, uint64_t* out_cpus, int64_t* out_numa, const kg_node_predicates* preds);
+                          void* numa_states, uint64_t* out_cpus, int64_t* out_numa, const kg_node_predicates* preds,
+                          void* groups);
 
 /* Golden-case entry (flat): explicit nodeReservationState (pod_requested, r_allocated, restored pod count) as the
  * reference tests build it.  out[0] = filter pass, out[1] = nominated slot, out[2] = Score (before normalize). */

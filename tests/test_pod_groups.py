@@ -1,0 +1,292 @@
+"""(ABI 12) PodTopologySpread and InterPodAffinity with topologyKey kubernetes.io/hostname on the exact per-pod pass.
+
+The reference runs both from k8s.io/kubernetes v1.24.15 (not vendored): the oracle restates the published plugins
+(oracle/defaults.c) and is pinned by hand-derived cases below ("parity unpinned" against the reference beyond them;
+the only reference-held anchor is frameworkext/debug_test.go:91-174, where PodTopologySpread contributes 200 = weight 2
+× MaxNodeScore to every node of a pod without soft constraints — test_spread_score_without_constraint_is_max).
+Bar for the device: bit-exact placements, totals and the final per-node group counters against the oracle."""
+import math
+
+import numpy as np
+import pytest
+
+from koordinator_amd import Engine, abi, framework as F, synth
+from koordinator_amd.predicates import PodGroupTable
+from oracle import oracle
+
+SPREAD_ONLY = F.Profile(filter=(F.NODE_RESOURCES_FIT, F.POD_TOPOLOGY_SPREAD),
+                        score={F.NODE_RESOURCES_FIT: 1, F.POD_TOPOLOGY_SPREAD: 2})
+IPA_ONLY = F.Profile(filter=(F.NODE_RESOURCES_FIT, F.INTER_POD_AFFINITY),
+                     score={F.NODE_RESOURCES_FIT: 1, F.INTER_POD_AFFINITY: 1})
+STOCK = F.Profile(filter=(F.NODE_RESOURCES_FIT, F.LOAD_AWARE, F.TAINT_TOLERATION, F.NODE_AFFINITY,
+                          F.POD_TOPOLOGY_SPREAD, F.INTER_POD_AFFINITY),
+                  score={F.NODE_RESOURCES_FIT: 1, F.LOAD_AWARE: 1, F.TAINT_TOLERATION: 1, F.NODE_AFFINITY: 1,
+                         F.BALANCED_ALLOCATION: 1, F.POD_TOPOLOGY_SPREAD: 2, F.INTER_POD_AFFINITY: 1})
+
+
+def _grp(**kw):
+    g = np.zeros(1, dtype=oracle.GROUP_DTYPE)
+    for k, v in kw.items():
+        g[k][0, :len(v)] = v
+    return g
+
+
+def _gpod(**kw):
+    p = np.zeros(1, dtype=abi.POD_DTYPE)
+    for k, v in kw.items():
+        p[k] = v
+    return p
+
+
+# ---- hand-derived cases of the restated plugins ----------------------------------------------------------------
+def test_spread_filter_cases():
+    """filtering.go: skew = matchNum + selfMatch − minMatchNum > maxSkew rejects; a node outside the eligible set
+    counts 0 matches."""
+    L = oracle.lib()
+    pod = _gpod(match_groups=1, spread_hard_group=1, spread_hard_max_skew=1)
+    for cnt, elig, mn, want in [(0, 1, 0, 1), (1, 1, 0, 0), (2, 1, 1, 0), (1, 1, 1, 1), (5, 0, 0, 1), (2, 1, 2, 1), (3, 1, 2, 0)]:
+        assert L.or_spread_filter(oracle.p(_grp(cnt=[cnt])), oracle.p(pod), elig, mn) == want, (cnt, elig, mn)
+    other = _gpod(match_groups=2, spread_hard_group=1, spread_hard_max_skew=1)  # the pod does not match its selector
+    assert L.or_spread_filter(oracle.p(_grp(cnt=[1])), oracle.p(other), 1, 0) == 1
+
+
+def test_spread_score_cases():
+    """scoring.go: counts [0, 1, 3] over 3 filtered nodes, maxSkew 1: weight log(5) → raw [0, 1, 4], normalized
+    100 · (4 + 0 − s) / 4 = [100, 75, 0]."""
+    L = oracle.lib()
+    pod = _gpod(spread_soft_group=1, spread_soft_max_skew=1)
+    raw = [L.or_spread_raw(c, oracle.p(pod), 3) for c in (0, 1, 3)]
+    assert raw == [0, int(1 * math.log(5)), int(3 * math.log(5))] == [0, 1, 4]
+    assert [L.or_spread_normalize(r, 0, 4) for r in raw] == [100, 75, 0]
+    skew3 = _gpod(spread_soft_group=1, spread_soft_max_skew=3)  # + (maxSkew − 1) before the truncation
+    assert L.or_spread_raw(2, oracle.p(skew3), 10) == int(2 * math.log(12) + 2)
+
+
+def test_spread_score_without_constraint_is_max():
+    """A pod without a ScheduleAnyway constraint: Score 0 everywhere, NormalizeScore gives MaxNodeScore (the 200 of
+    debug_test.go:140-144 = weight 2 × 100)."""
+    L = oracle.lib()
+    pod = _gpod()
+    assert L.or_spread_raw(7, oracle.p(pod), 4) == 0
+    assert 2 * L.or_spread_normalize(0, 0, 0) == 200
+
+
+def test_interpod_filter_cases():
+    L = oracle.lib()
+    tot = np.zeros(abi.MAX_MATCH_GROUPS, dtype=np.int64)
+    # required anti-affinity to group 0: a node holding a matching pod rejects
+    anti = _gpod(pod_anti_affinity=1)
+    assert L.or_interpod_filter(oracle.p(_grp(cnt=[1])), oracle.p(anti), oracle.p(tot)) == 0
+    assert L.or_interpod_filter(oracle.p(_grp(cnt=[0])), oracle.p(anti), oracle.p(tot)) == 1
+    # an existing pod's anti-affinity term of a group the incoming pod matches
+    mine = _gpod(match_groups=2)
+    assert L.or_interpod_filter(oracle.p(_grp(anti=[0, 1])), oracle.p(mine), oracle.p(tot)) == 0
+    assert L.or_interpod_filter(oracle.p(_grp(anti=[1, 0])), oracle.p(mine), oracle.p(tot)) == 1
+    # required affinity to group 2: needs a matching pod on the node; the first pod of a series (no pod in the
+    # cluster matches and the pod matches its own terms) passes anywhere
+    aff = _gpod(pod_affinity_group=3, match_groups=4)
+    assert L.or_interpod_filter(oracle.p(_grp(cnt=[0, 0, 1])), oracle.p(aff), oracle.p(tot)) == 1
+    assert L.or_interpod_filter(oracle.p(_grp()), oracle.p(aff), oracle.p(tot)) == 1  # first of a series
+    tot[2] = 1
+    assert L.or_interpod_filter(oracle.p(_grp()), oracle.p(aff), oracle.p(tot)) == 0
+    tot[2] = 0
+    stranger = _gpod(pod_affinity_group=3, match_groups=0)  # does not match its own terms
+    assert L.or_interpod_filter(oracle.p(_grp()), oracle.p(stranger), oracle.p(tot)) == 0
+
+
+def test_interpod_score_cases():
+    """processExistingPod summed on one node: the pod's preferred affinity (+10 × 2 matching pods) and anti-affinity
+    (−5 × 1), plus the node's pods' terms matching the pod (symmetric weights 7); min-max normalisation in float64."""
+    L = oracle.lib()
+    pod = _gpod(match_groups=0b100, n_pod_preferred=2, pod_preferred_group=[1, 2, 0, 0],
+                pod_preferred_weight=[10, -5, 0, 0])
+    g = _grp(cnt=[2, 1, 0], symw=[100, 100, 7])
+    assert L.or_interpod_raw(oracle.p(g), oracle.p(pod)) == 20 - 5 + 7
+    assert [L.or_interpod_normalize(r, -5, 10) for r in (-5, 0, 10)] == [0, int(100.0 * (5 / 15)), 100]
+    assert L.or_interpod_normalize(3, 3, 3) == 0
+
+
+def test_groups_apply_counts_terms():
+    g = np.zeros(1, dtype=oracle.GROUP_DTYPE)
+    pod = _gpod(match_groups=0b11, pod_anti_affinity=0b100, pod_affinity_terms=0b1000, n_pod_preferred=1,
+                pod_preferred_group=[2, 0, 0, 0], pod_preferred_weight=[-30, 0, 0, 0])
+    oracle.groups_apply(g, 0, pod, 1, hard_weight=5)
+    assert list(g["cnt"][0, :4]) == [1, 1, 0, 0] and list(g["anti"][0, :4]) == [0, 0, 1, 0]
+    assert list(g["symw"][0, :4]) == [0, -30, 0, 5]
+    oracle.groups_apply(g, 0, pod, -1, hard_weight=5)
+    assert not g["cnt"].any() and not g["anti"].any() and not g["symw"].any()
+
+
+# ---- composed scheduling on the oracle: the plugins' visible effects ---------------------------------------------
+def _flat(n, cpu="64", mem="256Gi"):
+    nodes = np.concatenate([F.make_node({"cpu": cpu, "memory": mem}) for _ in range(n)])
+    metrics = np.concatenate([F.make_node_metric(present=False, node_usage=None) for _ in range(n)])
+    return synth.Cluster(nodes, metrics, np.zeros(0, dtype=abi.POD_DTYPE), np.zeros(0, dtype=np.int32), 10**18)
+
+
+def _run_oracle(cfg, cluster, pods, preds=None, n_threads=4):
+    st = oracle.states(cluster.n)
+    oracle.add_pods(cfg, st, cluster.existing_pods, cluster.existing_node)
+    g = oracle.groups_init(cluster.n, cluster.existing_pods, cluster.existing_node,
+                           int(cfg["hard_pod_affinity_weight"][0]))
+    node, score, _ = oracle.schedule_resv(cfg, cluster.nodes, cluster.metrics, st, None, pods, cluster.now_ns,
+                                          n_threads=n_threads, preds=preds, groups=g)
+    return node, score, st, g
+
+
+def _replicas(n, table, **kw):
+    pods = np.concatenate([F.make_pod(requests={"cpu": "1", "memory": "1Gi"}) for _ in range(n)])
+    for j in range(n):
+        table.fill_pod(pods[j:j + 1], {"app": "web"}, "default", **kw)
+    return pods
+
+
+def test_oracle_hard_spread_round_robin():
+    """maxSkew 1 on four equal nodes: each pod lands on an emptiest node, lowest index first."""
+    t = PodGroupTable()
+    sel = {"matchLabels": {"app": "web"}}
+    pods = _replicas(8, t, spread=[{"maxSkew": 1, "labelSelector": sel}])
+    node, _, _, g = _run_oracle(F.build_config(profile=SPREAD_ONLY), _flat(4), pods)
+    assert list(node) == [0, 1, 2, 3, 0, 1, 2, 3]
+    assert list(g["cnt"][:4, 0]) == [2, 2, 2, 2]
+
+
+def test_oracle_anti_affinity_one_per_node():
+    t = PodGroupTable()
+    sel = {"matchLabels": {"app": "web"}}
+    pods = _replicas(5, t, required_anti_affinity=[{"labelSelector": sel}])
+    node, _, _, _ = _run_oracle(F.build_config(profile=IPA_ONLY), _flat(3), pods)
+    assert sorted(node[:3]) == [0, 1, 2] and list(node[3:]) == [-1, -1]
+
+
+def test_oracle_affinity_follows_the_first_pod():
+    """The first pod of a series passes anywhere (no pod matches, it matches its own term); the rest must share a
+    node with a matching pod, and the preferred weight of the symmetric term keeps them together."""
+    t = PodGroupTable()
+    sel = {"matchLabels": {"app": "web"}}
+    pods = _replicas(4, t, required_affinity=[{"labelSelector": sel}])
+    node, _, _, _ = _run_oracle(F.build_config(profile=IPA_ONLY), _flat(6), pods)
+    assert (node == node[0]).all() and node[0] >= 0
+
+
+def test_oracle_preferred_anti_affinity_spreads():
+    t = PodGroupTable()
+    sel = {"matchLabels": {"app": "web"}}
+    pods = _replicas(3, t, preferred_anti_affinity=[{"weight": 100, "podAffinityTerm": {"labelSelector": sel}}])
+    node, _, _, _ = _run_oracle(F.build_config(profile=IPA_ONLY), _flat(3), pods)
+    assert sorted(node) == [0, 1, 2]
+
+
+def test_pod_group_table_compiles_selectors():
+    t = PodGroupTable()
+    g1 = t.group({"matchLabels": {"app": "web"}}, ("default",))
+    g2 = t.group({"matchExpressions": [{"key": "tier", "operator": "In", "values": ["fe", "be"]}]}, ("default", "x"))
+    g3 = t.group(None, ("default",))  # nil selector matches nothing
+    both = t.conjunction([g1, g2])
+    assert t.matches(g1, {"app": "web"}, "default") and not t.matches(g1, {"app": "web"}, "other")
+    assert t.matches(g2, {"tier": "be"}, "x") and not t.matches(g2, {}, "x")
+    assert not t.matches(g3, {"app": "web"}, "default")
+    assert t.matches(both, {"app": "web", "tier": "fe"}, "default") and not t.matches(both, {"app": "web"}, "default")
+    pod = np.zeros(1, dtype=abi.POD_DTYPE)
+    t.fill_pod(pod, {"app": "web", "tier": "fe"}, "default",
+               required_affinity=[{"labelSelector": {"matchLabels": {"app": "web"}}},
+                                  {"labelSelector": {"matchExpressions": [{"key": "tier", "operator": "In",
+                                                                           "values": ["fe", "be"]}]},
+                                   "namespaces": ["default", "x"]}])
+    assert pod["pod_affinity_group"][0] == both
+    assert pod["pod_affinity_terms"][0] == (1 << (g1 - 1)) | (1 << (g2 - 1))
+    assert (pod["match_groups"][0] >> (both - 1)) & 1
+    with pytest.raises(NotImplementedError):
+        t.fill_pod(pod, {}, "default", spread=[{"maxSkew": 1, "topologyKey": "topology.kubernetes.io/zone",
+                                                "labelSelector": {}}])
+
+
+# ---- device vs oracle -------------------------------------------------------------------------------------------
+def _world(n_nodes, n_pods, seed, with_preds=True):
+    cluster = synth.make_cluster(n_nodes, seed=seed)
+    synth.make_pod_groups(cluster.existing_pods, seed=seed + 3)
+    pods = synth.make_pods(n_pods, seed=seed + 1)
+    synth.make_pod_groups(pods, seed=seed + 4)
+    preds = synth.make_predicates(n_nodes, pods, seed=seed + 2)[1] if with_preds else None
+    return cluster, pods, preds
+
+
+def _device(cfg, cluster, pods, preds, calls=1):
+    with Engine(cfg, cluster.n) as e:
+        synth.load_into(e, cluster)
+        if preds is not None:
+            e.upsert_predicates(preds)
+        e.stage(pods)
+        bounds = np.linspace(0, len(pods), calls + 1).astype(int)
+        for a, b in zip(bounds[:-1], bounds[1:]):
+            e.schedule_staged(int(a), int(b - a))
+        node, score = e.fetch(0, len(pods))
+        groups = e.read_pod_groups()
+        state = e.read_state()
+    return node, score, groups, state
+
+
+def _check(cfg, cluster, pods, preds, calls=1):
+    want, want_score, st, g = _run_oracle(cfg, cluster, pods, preds, n_threads=8)
+    node, score, (cnt, anti, symw), state = _device(cfg, cluster, pods, preds, calls)
+    bad = np.nonzero((node != want) | (score != want_score))[0]
+    assert len(bad) == 0, f"first mismatch at pod {bad[0]}: gpu ({node[bad[0]]}, {score[bad[0]]}) " \
+                          f"oracle ({want[bad[0]]}, {want_score[bad[0]]})"
+    assert np.array_equal(cnt, g["cnt"][:cluster.n]) and np.array_equal(anti, g["anti"][:cluster.n])
+    assert np.array_equal(symw, g["symw"][:cluster.n])
+    assert np.array_equal(state["requested_cpu"], st["requested"][:, abi.RES_CPU])
+    return want
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,profile", [("spread", SPREAD_ONLY), ("interpod", IPA_ONLY), ("stock", STOCK)])
+def test_device_matches_oracle(name, profile):
+    cluster, pods, preds = _world(2000, 600, 61)
+    node = _check(F.build_config(profile=profile), cluster, pods, preds, calls=2)
+    assert (node >= 0).mean() > 0.5
+
+
+@pytest.mark.gpu
+def test_device_matches_oracle_10k_nodes():
+    """The verdict's bar: both plugins in the stock profile at 10k nodes (HardPodAffinityWeight 3)."""
+    cluster, pods, preds = _world(10_000, 400, 71)
+    _check(F.build_config(profile=STOCK, hard_pod_affinity_weight=3), cluster, pods, preds, calls=3)
+
+
+@pytest.mark.gpu
+def test_device_single_pod_calls_and_unreserve():
+    """One pod per call, then Unreserve of every other placed pod: the group counters go back exactly."""
+    cfg = F.build_config(profile=STOCK)
+    cluster, pods, preds = _world(500, 120, 81)
+    want = _check(cfg, cluster, pods, preds, calls=120)
+    with Engine(cfg, cluster.n) as e:
+        synth.load_into(e, cluster)
+        e.upsert_predicates(preds)
+        e.stage(pods)
+        e.schedule_staged(0, len(pods))
+        before = e.read_pod_groups()
+        mask = (np.arange(len(pods)) % 2 == 0).astype(np.uint8)
+        e.unreserve(0, len(pods), mask)
+        after = e.read_pod_groups()
+    g = oracle.groups_init(cluster.n, cluster.existing_pods, cluster.existing_node)
+    for j in np.nonzero(want >= 0)[0]:
+        if not mask[j]:
+            oracle.groups_apply(g, int(want[j]), pods[j:j + 1], 1)
+    assert not np.array_equal(before[0], after[0])
+    assert np.array_equal(after[0], g["cnt"][:cluster.n]) and np.array_equal(after[2], g["symw"][:cluster.n])
+
+
+@pytest.mark.gpu
+def test_pods_add_remove_feed_the_counters():
+    cfg = F.build_config(profile=STOCK)
+    cluster, pods, preds = _world(300, 50, 91)
+    g = oracle.groups_init(cluster.n, cluster.existing_pods, cluster.existing_node)
+    with Engine(cfg, cluster.n) as e:
+        synth.load_into(e, cluster)
+        cnt, anti, symw = e.read_pod_groups()
+        assert np.array_equal(cnt, g["cnt"][:cluster.n]) and np.array_equal(anti, g["anti"][:cluster.n])
+        assert np.array_equal(symw, g["symw"][:cluster.n])
+        e.remove_pods(cluster.existing_pods[:100], cluster.existing_node[:100])
+        for k in range(100):
+            oracle.groups_apply(g, int(cluster.existing_node[k]), cluster.existing_pods[k:k + 1], -1)
+        assert np.array_equal(e.read_pod_groups()[0], g["cnt"][:cluster.n])
