@@ -370,8 +370,8 @@ def main():
         if work.numa is not None:
             algo += n_local * (144.0 + 104.0) + pods_per_launch * n_local * 4.0
         B = pods_per_launch
-    else:
-        algo = n_local * B_NODE + B * nt * 8 * 8.0 + B * 96.0
+    else:  # (r4) one top-8 list per (pod, tile group of 4 tiles) written
+        algo = n_local * B_NODE + B * (-(-nt // 4)) * 8 * 8.0 + B * 96.0
     dom_ms = live.get(dom, {}).get("avg_ms") or isolated[dom][0]
     achieved = algo / (dom_ms * 1e-3) / 1e9
     per_eval = B * n_local * B_NODE / (dom_ms * 1e-3) / 1e9  # §8d per-evaluation accounting (one table read per pod)

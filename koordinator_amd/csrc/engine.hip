@@ -580,6 +580,149 @@ __global__ __launch_bounds__(kMergeThreads) void merge_round(DevTable T, EvalPar
   KG_STAMP(1, 14);
 }
 
+// ---- (r4) round kernel 2b: per-pod merge on one wavefront (eval_round's tile-group lists) ---------------------
+// The same record as merge_round<false> (kC largest keys sorted, strict bound ub, the kStaged best rows), with no block
+// barrier: lane l holds lists l, l + 64, … (L per lane, ≤ 64·L lists) in registers.
+//  * ub_in = max over full lists of their minimum; every key below it is useless to the resolver, which stops once
+//    its best candidate falls below ub ≥ ub_in, so those keys are dropped before the selection.
+//  * τ = the largest score with count(score ≥ τ) ≥ kC (a ballot-sum binary search over the score bits), the first
+//    `need` keys of score τ in list order (lists by index, then position: ascending node index, as for tile lists) —
+//    i.e. the kC largest keys.
+//  * compaction into LDS by a wave prefix sum, a rank sort of ≤ kC keys, then the staged rows.
+__device__ __forceinline__ uint32_t wave_excl_prefix_u32(uint32_t v) { return wave_prefix_sum_u32(v) - v; }
+
+template <int L>
+__global__ __launch_bounds__(kWave * 4) void merge_wave(DevTable T, EvalParams P, const uint64_t* __restrict__ in,
+                                                        int64_t pod_stride, int n_lists, int nb,
+                                                        const int32_t* __restrict__ poison,
+                                                        uint64_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint64_t s_sel[4][kC];
+  const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
+  const int pod = blockIdx.x * 4 + wave;
+  if (*poison || pod >= nb) return;  // no block barrier below: a wave may leave alone
+  KG_STAMP(1, 0);
+  const uint64_t* base = in + (size_t)pod * pod_stride;
+  uint64_t k[L][kR];
+  uint64_t ub_in = 0;
+#pragma unroll
+  for (int i = 0; i < L; ++i) {
+    const int l = lane + kWave * i;
+    if (l < n_lists) {
+      const ulonglong2* src = reinterpret_cast<const ulonglong2*>(base + (size_t)l * kR);
+#pragma unroll
+      for (int r = 0; r < kR / 2; ++r) {
+        const ulonglong2 v = src[r];
+        k[i][2 * r] = v.x;
+        k[i][2 * r + 1] = v.y;
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < kR; ++r) k[i][r] = 0;
+    }
+    // a full list (kR keys, sorted descending) bounds its unseen nodes by its last key
+    ub_in = k[i][kR - 1] > ub_in ? k[i][kR - 1] : ub_in;
+  }
+  ub_in = wave_max_u64_dpp(ub_in);
+  ub_in = readlane_u64(ub_in, kWave - 1);
+  KG_STAMP(1, 1);
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < L; ++i)
+#pragma unroll
+    for (int r = 0; r < kR; ++r) {
+      if (k[i][r] < ub_in) k[i][r] = 0;
+      c += k[i][r] != 0;
+    }
+  const uint32_t total = wave_sum_u32(c);
+  const bool all = total <= (uint32_t)kC;
+  uint32_t tau = 0, need = kC;
+  if (!all) {
+    uint32_t cur = 0;
+    for (int b = P.score_bits; b >= 0; --b) {
+      const uint32_t cand = cur | (1u << b);
+      uint32_t n = 0;
+#pragma unroll
+      for (int i = 0; i < L; ++i)
+#pragma unroll
+        for (int r = 0; r < kR; ++r) n += k[i][r] != 0 && (uint32_t)(k[i][r] >> 32) >= cand;
+      if (wave_sum_u32(n) >= (uint32_t)kC) cur = cand;
+    }
+    tau = cur;
+    uint32_t a = 0;
+#pragma unroll
+    for (int i = 0; i < L; ++i)
+#pragma unroll
+      for (int r = 0; r < kR; ++r) a += k[i][r] != 0 && (uint32_t)(k[i][r] >> 32) > tau;
+    need = (uint32_t)kC - wave_sum_u32(a);
+  }
+  KG_STAMP(1, 2);
+  // selection with tie ranks in list order (i-major, then lane, then position) and the best key left out
+  uint32_t tie_base = 0, mycnt = 0;
+  uint64_t next = 0;
+  uint32_t selm[L];
+#pragma unroll
+  for (int i = 0; i < L; ++i) {
+    uint32_t ties = 0;
+    if (!all) {
+#pragma unroll
+      for (int r = 0; r < kR; ++r) ties += k[i][r] != 0 && (uint32_t)(k[i][r] >> 32) == tau;
+    }
+    uint32_t tr = tie_base + wave_excl_prefix_u32(ties);
+    tie_base += wave_sum_u32(ties);
+    uint32_t m = 0;
+#pragma unroll
+    for (int r = 0; r < kR; ++r) {
+      const uint64_t v = k[i][r];
+      const uint32_t sc = (uint32_t)(v >> 32);
+      const bool tie = !all && v != 0 && sc == tau;
+      const bool sel = v != 0 && (all || sc > tau || (tie && tr < need));
+      tr += tie;
+      m |= (uint32_t)sel << r;
+      if (v != 0 && !sel) next = v > next ? v : next;
+    }
+    selm[i] = m;
+    mycnt += __popc(m);
+  }
+  const uint32_t n_sel = wave_sum_u32(mycnt);
+  uint32_t off = wave_excl_prefix_u32(mycnt);
+  next = wave_max_u64_dpp(next);
+  next = readlane_u64(next, kWave - 1);
+  uint64_t* sel = s_sel[wave];
+#pragma unroll
+  for (int i = 0; i < L; ++i)
+#pragma unroll
+    for (int r = 0; r < kR; ++r)
+      if ((selm[i] >> r) & 1u) sel[off++] = k[i][r];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  KG_STAMP(1, 13);
+  // rank sort of the ≤ kC selected keys (unique): position = number of larger keys
+  const uint64_t v = lane < (int)n_sel ? sel[lane] : 0;
+  int rank = 0;
+  const ulonglong2* s2 = reinterpret_cast<const ulonglong2*>(sel);
+  for (int q = 0; q < ((int)n_sel + 1) / 2; ++q) {
+    const ulonglong2 x = s2[q];  // broadcast LDS reads
+    rank += (x.x > v) + (2 * q + 1 < (int)n_sel && x.y > v);
+  }
+  uint64_t* o = out + (size_t)pod * kCandStride;
+  if (lane < (int)n_sel) o[rank] = v;
+  else o[lane] = 0;
+  if (lane == 0) {
+    const uint64_t ub_sel = next ? next + 1 : 0;
+    o[kC] = ub_in > ub_sel ? ub_in : ub_sel;
+  }
+  if (lane < (int)n_sel && rank < kStaged && key_node(v) < (uint32_t)T.cap) {
+    const EvalRow er = make_eval_row(load_row(T, key_node(v)), P);
+    uint64_t words[kEvalRowWords];
+    __builtin_memcpy(words, &er, sizeof(er));
+    uint64_t* dst = o + kRecRows + rank * kEvalRowWords;
+#pragma unroll
+    for (int w = 0; w < kEvalRowWords; ++w) dst[w] = words[w];
+  }
+  KG_STAMP(1, 14);
+}
+
 // ---- round kernel 3: FIFO resolve (one wavefront, modified rows in registers) ---------------------------
 // One wavefront replays the round's pods [first, first + nb) in queue order against the merged candidates.
 // The "modified set" of pod j = every node assumed by an earlier pod of this round or by the n_prev rounds before
@@ -3831,9 +3974,28 @@ uint64_t* gathered_slot(kg_engine* e, const RoundGeom& g, int slot) {
   return e->gathered.p + (size_t)slot * e->n_ranks * g.B * kCandStride;
 }
 
+// KG_MERGE=block: the block-per-pod merge_round for eval_round's lists too (A/B measurements only)
+bool merge_block() {
+  static const bool on = std::getenv("KG_MERGE") && std::string(std::getenv("KG_MERGE")) == "block";
+  return on;
+}
+
 void launch_merge_local(kg_engine* e, const RoundGeom& g, int nb, int slot, hipStream_t st, uint32_t* done = nullptr) {
   uint64_t* dst = e->n_ranks > 1 ? gathered_slot(e, g, slot) + (size_t)e->rank * g.B * kCandStride : cand_slot(e, g, slot);
   const int nl = eval_lists(e, g);
+  if (!e->numa_on && !e->ds_on && !done && !merge_block()) {  // (r4) one wavefront per pod
+    const unsigned blocks = (unsigned)((nb + 3) / 4);
+    const int64_t ps = (int64_t)nl * kR;
+    if (nl <= kWave)
+      merge_wave<1><<<blocks, kWave * 4, 0, st>>>(e->T, e->P, lists_slot(e, g, slot), ps, nl, nb, poison_ptr(e), dst);
+    else if (nl <= 2 * kWave)
+      merge_wave<2><<<blocks, kWave * 4, 0, st>>>(e->T, e->P, lists_slot(e, g, slot), ps, nl, nb, poison_ptr(e), dst);
+    else if (nl <= 4 * kWave)
+      merge_wave<4><<<blocks, kWave * 4, 0, st>>>(e->T, e->P, lists_slot(e, g, slot), ps, nl, nb, poison_ptr(e), dst);
+    else
+      merge_wave<8><<<blocks, kWave * 4, 0, st>>>(e->T, e->P, lists_slot(e, g, slot), ps, nl, nb, poison_ptr(e), dst);
+    return;
+  }
   merge_round<false><<<nb, kMergeThreads, 0, st>>>(e->T, e->P, lists_slot(e, g, slot), (int64_t)nl * kR, kR, nl, kR,
                                                    nb, poison_ptr(e), dst,
                                                    e->n_ranks > 1 ? nullptr : done);

@@ -30,6 +30,30 @@ def _free_port():
         return s.getsockname()[1]
 
 
+RSV_PROFILE = F.Profile(filter=(F.NODE_RESOURCES_FIT, F.LOAD_AWARE, F.RESERVATION),
+                        score={F.NODE_RESOURCES_FIT: 1, F.LOAD_AWARE: 1, F.RESERVATION: 5000})
+SHIPPED_PROFILE = F.Profile(filter=(F.NODE_RESOURCES_FIT, F.LOAD_AWARE, F.NODE_NUMA_RESOURCE, F.DEVICE_SHARE,
+                                    F.RESERVATION),
+                            score={F.NODE_RESOURCES_FIT: 1, F.LOAD_AWARE: 1, F.NODE_NUMA_RESOURCE: 1,
+                                   F.DEVICE_SHARE: 1, F.RESERVATION: 5000})
+
+
+def _exact_case(kind):
+    """(r4) the exact profiles, which run as replicas on every rank: Reservation, and the shipped profile
+    (NUMA + DeviceShare + Reservation + ElasticQuota)."""
+    if kind == "rsv":
+        cfg = F.build_config(profile=RSV_PROFILE)
+        cluster, rsv = synth.make_rsv_cluster(1500, seed=961)
+        return cfg, dict(cluster=cluster, rsv=rsv, pods=synth.make_rsv_pods(800, seed=962))
+    cfg = F.build_config(profile=SHIPPED_PROFILE,
+                         la=F.LoadAwareSchedulingArgs(filter_expired_node_metrics=False,
+                                                      node_metric_expiration_seconds=300))
+    cluster, numa, dev, rsv = synth.make_shipped_cluster(600, seed=971)
+    pods = synth.make_shipped_pods(500, seed=972)
+    return cfg, dict(cluster=cluster, numa=numa, dev=dev, rsv=rsv, pods=pods,
+                     quotas=synth.make_c5_quotas(pods, seed=973))
+
+
 def _case(kind):
     if kind == "ds":
         cfg = F.build_config(profile=DS_PROFILE, batch_pods=32, pods_per_wave=4)
@@ -58,8 +82,27 @@ def _rank_main(rank, world, port, kind, out_dir):
             calls[0] += 1
             return torch.cat(parts).numpy()
 
-        cfg, cluster, pods, dev = _case(kind)
         ex = HostExchange(allgather)
+        if kind in ("rsv", "shipped"):
+            cfg, w = _exact_case(kind)
+            cluster, pods = w["cluster"], w["pods"]
+            with Engine(cfg, cluster.n, rank=rank, n_ranks=world, exchange=ex) as e:
+                if kind == "rsv":
+                    synth.load_rsv_into(e, cluster, w["rsv"])
+                else:
+                    synth.load_shipped_into(e, cluster, w["numa"], w["dev"], w["rsv"], w["quotas"])
+                e.stage(pods)
+                half = len(pods) // 2
+                e.schedule_staged(0, half)
+                e.schedule_staged(half, len(pods) - half)
+                node, score = e.fetch(0, len(pods))
+                np.save(os.path.join(out_dir, f"node{rank}.npy"), node)
+                np.save(os.path.join(out_dir, f"score{rank}.npy"), score)
+                np.save(os.path.join(out_dir, f"slot{rank}.npy"), e.fetch_reservations(0, len(pods)))
+                np.save(os.path.join(out_dir, f"cpu{rank}.npy"), e.read_state()["requested_cpu"])
+            assert ex.error is None, ex.error
+            return
+        cfg, cluster, pods, dev = _case(kind)
         with Engine(cfg, cluster.n, rank=rank, n_ranks=world, exchange=ex) as e:
             if dev is not None:
                 synth.load_gpu_into(e, cluster, dev)
@@ -104,4 +147,32 @@ def test_two_process_gloo_engine(tmp_path, kind):
         assert int(np.load(tmp_path / f"calls{r}.npy")[0]) > 0  # the rounds really exchanged through gloo
         if want_minors is not None:
             np.testing.assert_array_equal(np.load(tmp_path / f"minors{r}.npy"), want_minors)
+    assert (want >= 0).mean() > 0.3
+
+
+@pytest.mark.parametrize("kind", ["rsv", "shipped"])
+def test_two_process_gloo_exact_profiles(tmp_path, kind):
+    """The exact profiles on two ranks: every rank a full replica resolving the same FIFO order with no exchange
+     — both ranks' placements, totals, reservation slots and node state equal the oracle's."""
+    world = 2
+    mp.spawn(_rank_main, args=(world, _free_port(), kind, str(tmp_path)), nprocs=world, join=True)
+    cfg, w = _exact_case(kind)
+    cluster, pods = w["cluster"], w["pods"]
+    st = oracle.states(cluster.n)
+    oracle.add_pods(cfg, st, cluster.existing_pods, cluster.existing_node)
+    if kind == "rsv":
+        want, want_score, want_slot = oracle.schedule_resv(cfg, cluster.nodes, cluster.metrics, st, w["rsv"].copy(),
+                                                           pods, cluster.now_ns, n_threads=8)
+    else:
+        want, want_score, want_slot = oracle.schedule_resv(cfg, cluster.nodes, cluster.metrics, st, w["rsv"].copy(),
+                                                           pods, cluster.now_ns, devices=w["dev"].copy(),
+                                                           quotas=w["quotas"].copy(), n_threads=8,
+                                                           numa_buf=oracle.numa_states(w["numa"]))
+    for r in range(world):
+        node = np.load(tmp_path / f"node{r}.npy")
+        bad = np.nonzero(node != want)[0]
+        assert bad.size == 0, f"rank {r}: first mismatch at pod {bad[0]}: {node[bad[0]]} vs oracle {want[bad[0]]}"
+        np.testing.assert_array_equal(np.load(tmp_path / f"score{r}.npy"), want_score)
+        np.testing.assert_array_equal(np.load(tmp_path / f"slot{r}.npy"), want_slot)
+        np.testing.assert_array_equal(np.load(tmp_path / f"cpu{r}.npy"), st["requested"][:, 0])
     assert (want >= 0).mean() > 0.3
