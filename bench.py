@@ -54,6 +54,7 @@ WORKLOADS = {
     "c5ds": (50_000, 10_000, 32, 4, 2_000),
     "c5r": (50_000, 10_000, 32, 4, 2_000),
     "shipped": (50_000, 5_000, 32, 4, 1_000),
+    "stock": (10_000, 2_000, 32, 8, 500),
 }
 
 
@@ -133,7 +134,7 @@ class Work:
     def __init__(self, name, nodes, cfg):
         from koordinator_amd import synth
         self.name, self.cfg = name, cfg
-        self.numa = self.devices = self.rsv = self.quotas = None
+        self.numa = self.devices = self.rsv = self.quotas = self.preds = None
         S = synth
         if name == "c5":
             self.seed = S.BASE_SEED + 10
@@ -155,6 +156,12 @@ class Work:
             self.seed = S.BASE_SEED + 8
             self.cluster, self.rsv = S.make_rsv_cluster(nodes, seed=self.seed)
             self.make_pods = S.make_rsv_pods
+        elif name == "stock":  # (r4) the upstream defaults + hostname PodTopologySpread / InterPodAffinity
+            self.seed = S.BASE_SEED + 19
+            self.cluster = S.make_cluster(nodes, seed=self.seed)
+            S.make_pod_groups(self.cluster.existing_pods, seed=self.seed + 3)
+            self.preds = S.make_predicates(nodes, S.make_pods(0), seed=self.seed + 2)[1]  # labels + taints
+            self.make_pods = lambda n, seed: S.make_pod_groups(S.make_pods(n, seed=seed), seed=seed + 4)
         else:  # c1, c3: Fit + LoadAware
             self.seed = S.BASE_SEED + (1 if name == "c1" else 3)
             self.cluster = S.make_cluster(nodes, seed=self.seed)
@@ -180,6 +187,8 @@ class Work:
             synth.load_rsv_into(e, self.cluster, self.rsv)
         else:
             synth.load_into(e, self.cluster)
+        if self.preds is not None:
+            e.upsert_predicates(self.preds)
 
     def oracle_run(self, pods, threads):
         """(node idx, oracle name) of the oracle's sequential FIFO run over `pods` from the initial state."""
@@ -187,6 +196,11 @@ class Work:
         cl, cfg = self.cluster, self.cfg
         st = oracle.states(cl.n)
         oracle.add_pods(cfg, st, cl.existing_pods, cl.existing_node)
+        if self.name == "stock":
+            g = oracle.groups_init(cl.n, cl.existing_pods, cl.existing_node)
+            on, _, _ = oracle.schedule_resv(cfg, cl.nodes, cl.metrics, st, None, pods, cl.now_ns, n_threads=threads,
+                                            preds=self.preds, groups=g)
+            return on, "oracle/reservation.c or_schedule_resv_full with defaults.c pod groups (Parallelizer chunking)"
         if self.rsv is not None:
             on, _, _ = oracle.schedule_resv(cfg, cl.nodes, cl.metrics, st, self.rsv.copy(), pods, cl.now_ns,
                                             devices=None if self.devices is None else self.devices.copy(),
@@ -265,6 +279,11 @@ def main():
     elif wl == "c5r":  # shipped weights: Reservation 5000 (config/manager/scheduler-config.yaml:90-91)
         profile = F.Profile(filter=(F.NODE_RESOURCES_FIT, F.LOAD_AWARE, F.RESERVATION),
                             score={F.NODE_RESOURCES_FIT: 1, F.LOAD_AWARE: 1, F.RESERVATION: 5000})
+    elif wl == "stock":  # k8s v1.24 v1beta2 default weights + LoadAware; hostname spread / inter-pod affinity
+        profile = F.Profile(filter=(F.NODE_RESOURCES_FIT, F.LOAD_AWARE, F.TAINT_TOLERATION, F.NODE_AFFINITY,
+                                    F.POD_TOPOLOGY_SPREAD, F.INTER_POD_AFFINITY),
+                            score={F.NODE_RESOURCES_FIT: 1, F.LOAD_AWARE: 1, F.TAINT_TOLERATION: 1, F.NODE_AFFINITY: 1,
+                                   F.BALANCED_ALLOCATION: 1, F.POD_TOPOLOGY_SPREAD: 2, F.INTER_POD_AFFINITY: 1})
     la = None
     if wl == "shipped":  # config/manager/scheduler-config.yaml:29-117: plugins, weights and LoadAware args
         profile = F.Profile(filter=(F.NODE_RESOURCES_FIT, F.LOAD_AWARE, F.NODE_NUMA_RESOURCE, F.DEVICE_SHARE,
@@ -343,7 +362,7 @@ def main():
                        "note": "kg_pods_schedule_staged(count=1) continuing the staged queue after the timed region; "
                                "kg_pods_schedule(1 host pod) on a fresh engine: decode + upload + schedule + result"})
     # isolated replays of one round's kernels (warm caches, no concurrency) for comparison
-    rsv_path = wl in ("c5r", "c5", "shipped")
+    rsv_path = wl in ("c5r", "c5", "shipped", "stock")
     names = (("rsv_eval", "rsv_select") if rsv_path else
              ("eval_round", "merge_round", "resolve_round") + (("ds_max_round", "ds_norm_reduce") if wl == "c5ds" else ()))
     isolated = {name: e.bench_kernel(which, args.kernel_iters) for which, name in enumerate(names)}
@@ -351,12 +370,16 @@ def main():
     # roofline kernel: the wide pass — the only kernel whose work scales with node evaluations.  One launch
     # processes the round's B pods against every node row of this rank's shard, reading each row once:
     # algorithmic bytes = rows × b_node + the candidate lists written + the pods read.
-    dom = {"c5ds": "ds_max_round", "c5r": "rsv_eval", "c5": "rsv_eval", "shipped": "rsv_eval"}.get(wl, "eval_round")
+    dom = {"c5ds": "ds_max_round", "c5r": "rsv_eval", "c5": "rsv_eval", "shipped": "rsv_eval",
+           "stock": "rsv_eval"}.get(wl, "eval_round")
     n_local = -(-cluster.n // d.world)
     nt = max(1, -(-n_local // 256))
     B = 1 if rsv_path else args.batch
     if wl == "c5ds":  # ds_max_round also reads the 272-B GPU row and writes a 4-B packed value per (pod, node)
         algo = n_local * (B_NODE + 272.0) + B * n_local * 4.0 + B * nt * 8.0
+    elif wl == "stock":  # one pod per exact pass (rsv_eval): per node the Fit / LoadAware columns, the 32-B NodePred,
+        # ~4 group counters, and the 8 + 4 + 8 B of values it writes
+        algo = n_local * (B_NODE + 32.0 + 16.0 + 20.0)
     elif rsv_path:  # the exact wide pass (xr_eval, live time folded under "rsv_eval"): one launch scores the round's
         # pods (kXrPods = 32, or fewer) against every node.  Per launch: the node columns + rsv_n once, the 192-B slot
         # rows of nodes holding reservations, the 272-B GPU row per node when the round has device pods, the NUMA rows
@@ -370,8 +393,8 @@ def main():
         if work.numa is not None:
             algo += n_local * (144.0 + 104.0) + pods_per_launch * n_local * 4.0
         B = pods_per_launch
-    else:  # (r4) one top-8 list per (pod, tile group of 4 tiles) written
-        algo = n_local * B_NODE + B * (-(-nt // 4)) * 8 * 8.0 + B * 96.0
+    else:  # (r4) one top-8 list per (pod, tile group of 4 tiles) written from 64 tiles on, per tile below
+        algo = n_local * B_NODE + B * (-(-nt // 4) if nt >= 64 else nt) * 8 * 8.0 + B * 96.0
     dom_ms = live.get(dom, {}).get("avg_ms") or isolated[dom][0]
     achieved = algo / (dom_ms * 1e-3) / 1e9
     per_eval = B * n_local * B_NODE / (dom_ms * 1e-3) / 1e9  # §8d per-evaluation accounting (one table read per pod)
@@ -411,7 +434,8 @@ def main():
                                                    for r in ("r04", "r03", "r02")) if os.path.exists(f)),
                                       os.path.join(ROOT, "profiles", "r02", f"traffic_{wl}.json"))
     # live timing folds every wide pass under one name: the kernel rocprof sees
-    pmc_name = {"c4": "eval_round_numa", "c5": "xr_eval", "c5r": "xr_eval", "shipped": "xr_eval"}.get(wl, dom)
+    pmc_name = {"c4": "eval_round_numa", "c5": "xr_eval", "c5r": "xr_eval", "shipped": "xr_eval",
+                "stock": "rsv_eval"}.get(wl, dom)
     traffic, traffic_src, rocprof_ns = (pmc_traffic(tfile, pmc_name, cluster.n, args.batch, args.pods_per_wave,
                                                     args.depth) if d.world == 1 else (None, None, None))
     # period decomposition of the round pipeline (Fit + LoadAware / DeviceShare round profiles): per round, the serial
@@ -462,6 +486,11 @@ def main():
             "c5r": "C5 (Reservation part): %d nodes (30%% with 1-4 reservations), %d-pod FIFO queue (20%% "
                    "reservation-owned), NodeResourcesFit+LoadAwareScheduling+Reservation (w 5000), batched exact "
                    "rounds of 32 pods, %d pods per step",
+            "stock": "k8s v1.24 default profile + LoadAware: %d nodes (labels, NoSchedule / PreferNoSchedule taints), "
+                     "%d-pod FIFO queue of 8 deployments in 4 teams (40%% DoNotSchedule / 50%% ScheduleAnyway hostname "
+                     "spread, 15%% required anti-affinity, 10%% required affinity, 30%% preferred terms), NodeResourcesFit"
+                     "+LoadAware+TaintToleration+NodeAffinity+BalancedAllocation+PodTopologySpread(w2)+InterPodAffinity, "
+                     "one pod per exact pass, %d pods per step",
         }[wl] % (cluster.n, total, args.pods_per_step)
         out = {
             "metric": {"c3": "pods scheduled/sec at 100k nodes (node-evals/sec alongside)",
@@ -472,7 +501,9 @@ def main():
                        "c5ds": "pods scheduled/sec, DeviceShare GPU-share profile (node-evals/sec alongside)",
                        "c5r": "pods scheduled/sec, Reservation profile (node-evals/sec alongside)",
                        "c5": "pods scheduled/sec, Reservation+DeviceShare+ElasticQuota profile (node-evals/sec "
-                             "alongside)"}[wl],
+                             "alongside)",
+                       "stock": "pods scheduled/sec, default plugins + hostname PodTopologySpread / InterPodAffinity "
+                                "(node-evals/sec alongside)"}[wl],
             "value": pods_s,
             "unit": "pods/s",
             "n_gpus": d.world,

@@ -151,8 +151,8 @@ __device__ __forceinline__ void select_write(const uint32_t (&v)[kNPT], const ui
 // (they would stay live across the wide loop and halve its occupancy).
 __device__ __forceinline__ void eval_tile_exact(const DevTable& T, const DevPod* __restrict__ pods, int64_t first,
                                              int p0, int p1, int tile, int64_t node_base, int64_t n_local,
-                                             const EvalParams& P, uint64_t* __restrict__ out, int vbits,
-                                             const int64_t* __restrict__ paux) {
+                                             const EvalParams& P, uint64_t* __restrict__ out, int64_t out_stride,
+                                             int vbits, const int64_t* __restrict__ paux) {
   const int lane = threadIdx.x % kWave;
   uint32_t gidx[kNPT];
 #pragma unroll
@@ -169,7 +169,7 @@ __device__ __forceinline__ void eval_tile_exact(const DevTable& T, const DevPod*
       if (P.fit_filter && (p.flags & P_AUX) && v[j] && !aux_fits(T, node_base + local, paux + (size_t)(first + pi) * kAux))
         v[j] = 0;
     }
-    select_write(v, gidx, vbits, out + (size_t)(pi - p0) * kR, lane);
+    select_write(v, gidx, vbits, out + (size_t)(pi - p0) * out_stride, lane);
   }
 }
 
@@ -177,8 +177,8 @@ __device__ __forceinline__ void eval_tile_exact(const DevTable& T, const DevPod*
 template <int PF>
 __device__ __forceinline__ void eval_tile(const DevTable& T, const DevPod* __restrict__ pods, int64_t first, int p0,
                                           int p1, int tile, int64_t node_base, int64_t n_local, const EvalParams& P,
-                                          uint64_t* __restrict__ out, int vbits, const int64_t* __restrict__ paux,
-                                          int lane) {
+                                          uint64_t* __restrict__ out, int64_t out_stride, int vbits,
+                                          const int64_t* __restrict__ paux, int lane) {
 
   HotRow rows[kNPT];
   uint32_t gidx[kNPT];
@@ -208,7 +208,7 @@ __device__ __forceinline__ void eval_tile(const DevTable& T, const DevPod* __res
   KG_STAMP(0, 1);
   // a row outside eval_hot's exact domain anywhere in the tile: the whole tile takes the exact path
   if (__ballot(rare)) {
-    eval_tile_exact(T, pods, first, p0, p1, tile, node_base, n_local, P, out, vbits, paux);
+    eval_tile_exact(T, pods, first, p0, p1, tile, node_base, n_local, P, out, out_stride, vbits, paux);
     return;
   }
   for (int pi = p0; pi < p1; ++pi) {
@@ -227,7 +227,7 @@ __device__ __forceinline__ void eval_tile(const DevTable& T, const DevPod* __res
           if (v[j] && !aux_fits(T, gidx[j], rq)) v[j] = 0;
       }
     }
-    select_write(v, gidx, vbits, out + (size_t)(pi - p0) * kR, lane);
+    select_write(v, gidx, vbits, out + (size_t)(pi - p0) * out_stride, lane);
   }
 }
 
@@ -237,7 +237,7 @@ __global__ __launch_bounds__(kWave* kEvalWaves) void eval_round(DevTable T, cons
                                                                   int64_t node_base, int64_t n_local, int nt_local,
                                                                   EvalParams P, uint64_t* __restrict__ lists,
                                                                   const int32_t* __restrict__ poison,
-                                                                  const int64_t* __restrict__ paux) {
+                                                                  const int64_t* __restrict__ paux, int combine) {
   KG_STAMP(0, 0);
   if (*poison) return;
   const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
@@ -254,9 +254,16 @@ __global__ __launch_bounds__(kWave* kEvalWaves) void eval_round(DevTable T, cons
   const int vbits = P.score_bits + 1;  // v = total + 1 ≤ 2^score_bits
   // (r4) each wave's per-pod tile top-kR goes to LDS; the block then combines its kEvalWaves tiles into one
   // top-kR list per (pod, tile group) — a quarter of the candidate lists for the merge to read and rank
+  // (a shard of fewer than kCombineTiles tiles keeps one list per tile: a pod's record needs kC candidates)
   extern __shared__ __attribute__((aligned(16))) uint64_t s_lists[];  // [kEvalWaves][pods_per_wave][kR]
+  if (!combine) {
+    if (tile < nt_local)
+      eval_tile<PF>(T, pods, first, p0, p1, tile, node_base, n_local, P, lists + ((size_t)p0 * nt_local + tile) * kR,
+                    (int64_t)nt_local * kR, vbits, paux, lane);
+    return;
+  }
   uint64_t* my_l = s_lists + (size_t)wave * pods_per_wave * kR;
-  if (tile < nt_local) eval_tile<PF>(T, pods, first, p0, p1, tile, node_base, n_local, P, my_l, vbits, paux, lane);
+  if (tile < nt_local) eval_tile<PF>(T, pods, first, p0, p1, tile, node_base, n_local, P, my_l, kR, vbits, paux, lane);
   else
     for (int q = lane; q < (p1 - p0) * kR; q += kWave) my_l[q] = 0;
   __syncthreads();
@@ -3945,6 +3952,8 @@ uint64_t* lists_slot(kg_engine* e, const RoundGeom& g, int slot) {
   return e->lists.p + (size_t)slot * g.B * g.nt_local * kR;
 }
 
+constexpr int kCombineTiles = 64;  // combined lists from 64 tiles on (16 group lists = 128 keys ≥ kC per pod)
+bool eval_combine(const RoundGeom& g) { return g.nt_local >= kCombineTiles; }
 void launch_eval(kg_engine* e, const RoundGeom& g, int64_t first, int nb, int slot, hipStream_t st) {
   if (e->numa_on) {  // one block per (tile, pod group)
     const dim3 grid((unsigned)(g.nt_local * ((nb + g.ppw - 1) / g.ppw)));
@@ -3957,7 +3966,8 @@ void launch_eval(kg_engine* e, const RoundGeom& g, int64_t first, int nb, int sl
   eval_round<X><<<eval_grid(g, nb), kWave * kEvalWaves, eval_lds_bytes(g), st>>>(e->T, e->pods.p, first, nb,   \
                                                                                 g.ppw, g.base,                   \
                                                                  g.n_local, g.nt_local, e->P,             \
-                                                                 lists_slot(e, g, slot), poison_ptr(e), e->paux.p)
+                                                                 lists_slot(e, g, slot), poison_ptr(e), e->paux.p, \
+                                                                 eval_combine(g) ? 1 : 0)
   KG_PF_SWITCH(profile_bits(e->P), KG_EVAL)
 #undef KG_EVAL
 }
@@ -3965,7 +3975,7 @@ void launch_eval(kg_engine* e, const RoundGeom& g, int64_t first, int nb, int sl
 // candidate lists per pod of the round's wide pass: eval_round writes one per tile group of kEvalWaves tiles, the
 // NUMA and DeviceShare passes one per tile
 int eval_lists(kg_engine* e, const RoundGeom& g) {
-  return (e->numa_on || e->ds_on) ? g.nt_local : (g.nt_local + kEvalWaves - 1) / kEvalWaves;
+  return (e->numa_on || e->ds_on || !eval_combine(g)) ? g.nt_local : (g.nt_local + kEvalWaves - 1) / kEvalWaves;
 }
 
 // local merge: this rank's tile lists → per-pod record (single rank: the final candidates)
