@@ -589,7 +589,7 @@ __global__ __launch_bounds__(kMergeThreads) void merge_round(DevTable T, EvalPar
 
 // ---- (r4) round kernel 2b: per-pod merge on one wavefront (eval_round's tile-group lists) ---------------------
 // The same record as merge_round<false> (kC largest keys sorted, strict bound ub, the kStaged best rows), with no block
-// barrier: lane l holds lists l, l + 64, … (L per lane, ≤ 64·L lists) in registers.
+// barrier: lane l holds lists l, l + 64, … (L per lane, ≤ 64·L lists; tile lists or tile-group lists) in registers.
 //  * ub_in = max over full lists of their minimum; every key below it is useless to the resolver, which stops once
 //    its best candidate falls below ub ≥ ub_in, so those keys are dropped before the selection.
 //  * τ = the largest score with count(score ≥ τ) ≥ kC (a ballot-sum binary search over the score bits), the first
@@ -626,8 +626,16 @@ __global__ __launch_bounds__(kWave * 4) void merge_wave(DevTable T, EvalParams P
 #pragma unroll
       for (int r = 0; r < kR; ++r) k[i][r] = 0;
     }
-    // a full list (kR keys, sorted descending) bounds its unseen nodes by its last key
-    ub_in = k[i][kR - 1] > ub_in ? k[i][kR - 1] : ub_in;
+    // a full list (kR keys: a tile list in node order, or a sorted tile-group list) bounds its unseen nodes by its
+    // minimum
+    uint64_t mn = ~0ull;
+    int cnt = 0;
+#pragma unroll
+    for (int r = 0; r < kR; ++r) {
+      cnt += k[i][r] != 0;
+      mn = k[i][r] != 0 && k[i][r] < mn ? k[i][r] : mn;
+    }
+    if (cnt == kR) ub_in = mn > ub_in ? mn : ub_in;
   }
   ub_in = wave_max_u64_dpp(ub_in);
   ub_in = readlane_u64(ub_in, kWave - 1);
