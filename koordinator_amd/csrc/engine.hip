@@ -39,6 +39,17 @@ namespace {
 
 constexpr int kNPT = 4;               // nodes per lane in an eval tile
 constexpr int kTile = kWave * kNPT;   // 256 nodes per tile
+// (r4) eval_round's own geometry: kENPT nodes per lane, kEW tiles (waves) per block = 1,024-node tile groups.
+// KG_EVAL_NPT=4 restores the round-3 shape (4 waves of 256-node tiles)
+#ifndef KG_EVAL_NPT
+#define KG_EVAL_NPT 2
+#endif
+#ifndef KG_EVAL_EW
+#define KG_EVAL_EW (16 / KG_EVAL_NPT)
+#endif
+constexpr int kENPT = KG_EVAL_NPT;
+constexpr int kETile = kWave * kENPT;
+constexpr int kEW = KG_EVAL_EW;
 constexpr int kR = 8;                 // candidates kept per (pod, tile)
 constexpr int kEvalWaves = 4;         // waves (tiles) per eval block
 constexpr int kMaxB = 64;             // modified rows are held one per lane of the resolver wave
@@ -96,37 +107,38 @@ typedef const __attribute__((address_space(1))) void* global_cvoid_ptr;
 // Per (pod, tile): the tile's top-kR packed keys from v[j] = feasible ? total + 1 : 0 (one value per node, so a
 // compare needs no feasibility mask).  τ = the largest v with count(v ≥ τ) ≥ kR, one ballot per value bit;
 // ties at τ go to the lowest node index (register j, then lane).  Writes the list in ascending node order.
-__device__ __forceinline__ void select_write(const uint32_t (&v)[kNPT], const uint32_t (&gidx)[kNPT], int vbits,
+template <int NPT>
+__device__ __forceinline__ void select_write(const uint32_t (&v)[NPT], const uint32_t (&gidx)[NPT], int vbits,
                                              uint64_t* __restrict__ out, int lane) {
-  uint64_t fm[kNPT], sel[kNPT];
+  uint64_t fm[NPT], sel[NPT];
   int nfeas = 0;
 #pragma unroll
-  for (int j = 0; j < kNPT; ++j) {
+  for (int j = 0; j < NPT; ++j) {
     fm[j] = __ballot(v[j] != 0);
     nfeas += __popcll(fm[j]);
   }
   if (nfeas <= kR) {
 #pragma unroll
-    for (int j = 0; j < kNPT; ++j) sel[j] = fm[j];
+    for (int j = 0; j < NPT; ++j) sel[j] = fm[j];
   } else {
     uint32_t cur = 0;
     for (int b = vbits - 1; b >= 0; --b) {
       const uint32_t c = cur | (1u << b);
       int cnt = 0;
 #pragma unroll
-      for (int j = 0; j < kNPT; ++j) cnt += __popcll(__ballot(v[j] >= c));
+      for (int j = 0; j < NPT; ++j) cnt += __popcll(__ballot(v[j] >= c));
       if (cnt >= kR) cur = c;
     }
     int need = kR;
-    uint64_t eq[kNPT];
+    uint64_t eq[NPT];
 #pragma unroll
-    for (int j = 0; j < kNPT; ++j) {
+    for (int j = 0; j < NPT; ++j) {
       sel[j] = __ballot(v[j] > cur);
       eq[j] = __ballot(v[j] == cur);
       need -= __popcll(sel[j]);
     }
 #pragma unroll
-    for (int j = 0; j < kNPT; ++j) {
+    for (int j = 0; j < NPT; ++j) {
       uint64_t m = eq[j];
       while (need > 0 && m) {
         const uint64_t low = m & (~m + 1);
@@ -139,7 +151,7 @@ __device__ __forceinline__ void select_write(const uint32_t (&v)[kNPT], const ui
   const uint64_t lane_lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   int base = 0;
 #pragma unroll
-  for (int j = 0; j < kNPT; ++j) {
+  for (int j = 0; j < NPT; ++j) {
     if ((sel[j] >> lane) & 1) out[base + __popcll(sel[j] & lane_lt)] = make_key(v[j] - 1, gidx[j]);
     base += __popcll(sel[j]);
   }
@@ -149,20 +161,21 @@ __device__ __forceinline__ void select_write(const uint32_t (&v)[kNPT], const ui
 // A tile holding a row outside eval_hot's exact domain: the reference-shaped int64 path for every pod (rare).
 // The row index is laundered inside the loop so the compiler cannot hoist the 19 column addresses out of it
 // (they would stay live across the wide loop and halve its occupancy).
+template <int NPT>
 __device__ __forceinline__ void eval_tile_exact(const DevTable& T, const DevPod* __restrict__ pods, int64_t first,
                                              int p0, int p1, int tile, int64_t node_base, int64_t n_local,
                                              const EvalParams& P, uint64_t* __restrict__ out, int64_t out_stride,
                                              int vbits, const int64_t* __restrict__ paux) {
   const int lane = threadIdx.x % kWave;
-  uint32_t gidx[kNPT];
+  uint32_t gidx[NPT];
 #pragma unroll
-  for (int j = 0; j < kNPT; ++j) gidx[j] = (uint32_t)(node_base + (int64_t)tile * kTile + j * kWave + lane);
+  for (int j = 0; j < NPT; ++j) gidx[j] = (uint32_t)(node_base + (int64_t)tile * (kWave * NPT) + j * kWave + lane);
   for (int pi = p0; pi < p1; ++pi) {
     const DevPod p = pods[first + pi];
-    uint32_t v[kNPT];
+    uint32_t v[NPT];
 #pragma unroll
-    for (int j = 0; j < kNPT; ++j) {
-      int64_t local = (int64_t)tile * kTile + j * kWave + lane;
+    for (int j = 0; j < NPT; ++j) {
+      int64_t local = (int64_t)tile * (kWave * NPT) + j * kWave + lane;
       asm volatile("" : "+v"(local));
       int64_t t = 0;
       v[j] = (local < n_local && eval_node(load_row(T, node_base + local), p, P, t)) ? (uint32_t)t + 1u : 0u;
@@ -174,32 +187,32 @@ __device__ __forceinline__ void eval_tile_exact(const DevTable& T, const DevPod*
 }
 
 // one wave's tile for pods [p0, p1): its kR best packed keys per pod into out[(pi - p0) * kR ..]
-template <int PF>
+template <int PF, int NPT>
 __device__ __forceinline__ void eval_tile(const DevTable& T, const DevPod* __restrict__ pods, int64_t first, int p0,
                                           int p1, int tile, int64_t node_base, int64_t n_local, const EvalParams& P,
                                           uint64_t* __restrict__ out, int64_t out_stride, int vbits,
                                           const int64_t* __restrict__ paux, int lane) {
 
-  HotRow rows[kNPT];
-  uint32_t gidx[kNPT];
+  HotRow rows[NPT];
+  uint32_t gidx[NPT];
   bool rare = false;
   {  // every column load of the tile's rows issued before any is used (a row past the shard reads the shard's last
      // row — row 0 for an empty shard — and is masked invalid): one wait for the tile instead of a wait per
      // conditional load
-    HotCols c[kNPT];
-    int64_t ii[kNPT];
+    HotCols c[NPT];
+    int64_t ii[NPT];
 #pragma unroll
-    for (int j = 0; j < kNPT; ++j) {
-      const int64_t local = (int64_t)tile * kTile + j * kWave + lane;
+    for (int j = 0; j < NPT; ++j) {
+      const int64_t local = (int64_t)tile * (kWave * NPT) + j * kWave + lane;
       gidx[j] = (uint32_t)(node_base + local);
       ii[j] = local < n_local ? node_base + local : (n_local > 0 ? node_base + n_local - 1 : 0);
       load_hot_cols<PF>(T, ii[j], c[j]);
     }
 #pragma unroll
-    for (int j = 0; j < kNPT; ++j) load_hot_la_alloc<PF>(T, ii[j], c[j]);
+    for (int j = 0; j < NPT; ++j) load_hot_la_alloc<PF>(T, ii[j], c[j]);
 #pragma unroll
-    for (int j = 0; j < kNPT; ++j) {
-      const int64_t local = (int64_t)tile * kTile + j * kWave + lane;
+    for (int j = 0; j < NPT; ++j) {
+      const int64_t local = (int64_t)tile * (kWave * NPT) + j * kWave + lane;
       rows[j] = hot_from_cols<PF>(c[j], P);
       if (local >= n_local) rows[j].flags = 0;  // not F_VALID → never feasible
       rare |= (rows[j].flags & F_RARE) != 0;
@@ -208,14 +221,14 @@ __device__ __forceinline__ void eval_tile(const DevTable& T, const DevPod* __res
   KG_STAMP(0, 1);
   // a row outside eval_hot's exact domain anywhere in the tile: the whole tile takes the exact path
   if (__ballot(rare)) {
-    eval_tile_exact(T, pods, first, p0, p1, tile, node_base, n_local, P, out, out_stride, vbits, paux);
+    eval_tile_exact<NPT>(T, pods, first, p0, p1, tile, node_base, n_local, P, out, out_stride, vbits, paux);
     return;
   }
   for (int pi = p0; pi < p1; ++pi) {
     const DevPod p = pods[first + pi];
-    uint32_t v[kNPT];
+    uint32_t v[NPT];
 #pragma unroll
-    for (int j = 0; j < kNPT; ++j) {
+    for (int j = 0; j < NPT; ++j) {
       uint32_t t = 0;
       v[j] = eval_hot<PF>(rows[j], p, P, t) ? t + 1u : 0u;
     }
@@ -223,7 +236,7 @@ __device__ __forceinline__ void eval_tile(const DevTable& T, const DevPod* __res
       if (p.flags & P_AUX) {
         const int64_t* rq = paux + (size_t)(first + pi) * kAux;
 #pragma unroll
-        for (int j = 0; j < kNPT; ++j)
+        for (int j = 0; j < NPT; ++j)
           if (v[j] && !aux_fits(T, gidx[j], rq)) v[j] = 0;
       }
     }
@@ -231,8 +244,18 @@ __device__ __forceinline__ void eval_tile(const DevTable& T, const DevPod* __res
   }
 }
 
+// 4 waves per SIMD for the 2-node shape: all of the C3 grid (3,136 waves) resident at once (KG_EVAL_WPE=0: the
+// compiler's choice, 130 VGPRs and 3 waves per SIMD)
+#ifndef KG_EVAL_WPE
+#define KG_EVAL_WPE (KG_EVAL_NPT == 2 ? 4 : 0)
+#endif
+#if KG_EVAL_WPE > 0
+#define KG_EVAL_ATTR __attribute__((amdgpu_waves_per_eu(KG_EVAL_WPE)))
+#else
+#define KG_EVAL_ATTR
+#endif
 template <int PF>
-__global__ __launch_bounds__(kWave* kEvalWaves) void eval_round(DevTable T, const DevPod* __restrict__ pods,
+__global__ __launch_bounds__(kWave* kEW) KG_EVAL_ATTR void eval_round(DevTable T, const DevPod* __restrict__ pods,
                                                                   int64_t first, int nb, int pods_per_wave,
                                                                   int64_t node_base, int64_t n_local, int nt_local,
                                                                   EvalParams P, uint64_t* __restrict__ lists,
@@ -247,36 +270,36 @@ __global__ __launch_bounds__(kWave* kEvalWaves) void eval_round(DevTable T, cons
   const int n_pg = (nb + pods_per_wave - 1) / pods_per_wave;
   const uint32_t nwg = gridDim.x, bid = blockIdx.x, xcd = bid % 8u, q = nwg / 8u, r = nwg % 8u;
   const uint32_t wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8u;
-  const int tile0 = (int)(wgid / (uint32_t)n_pg) * kEvalWaves, tile = tile0 + wave;
+  const int tile0 = (int)(wgid / (uint32_t)n_pg) * kEW, tile = tile0 + wave;
   const int p0 = (int)(wgid % (uint32_t)n_pg) * pods_per_wave;
   if (tile0 >= nt_local || p0 >= nb) return;  // block-uniform
   const int p1 = (p0 + pods_per_wave) < nb ? (p0 + pods_per_wave) : nb;
   const int vbits = P.score_bits + 1;  // v = total + 1 ≤ 2^score_bits
-  // (r4) each wave's per-pod tile top-kR goes to LDS; the block then combines its kEvalWaves tiles into one
+  // (r4) each wave's per-pod tile top-kR goes to LDS; the block then combines its kEW tiles into one
   // top-kR list per (pod, tile group) — a quarter of the candidate lists for the merge to read and rank
   // (a shard of fewer than kCombineTiles tiles keeps one list per tile: a pod's record needs kC candidates)
-  extern __shared__ __attribute__((aligned(16))) uint64_t s_lists[];  // [kEvalWaves][pods_per_wave][kR]
+  extern __shared__ __attribute__((aligned(16))) uint64_t s_lists[];  // [kEW][pods_per_wave][kR]
   if (!combine) {
     if (tile < nt_local)
-      eval_tile<PF>(T, pods, first, p0, p1, tile, node_base, n_local, P, lists + ((size_t)p0 * nt_local + tile) * kR,
+      eval_tile<PF, kENPT>(T, pods, first, p0, p1, tile, node_base, n_local, P, lists + ((size_t)p0 * nt_local + tile) * kR,
                     (int64_t)nt_local * kR, vbits, paux, lane);
     return;
   }
   uint64_t* my_l = s_lists + (size_t)wave * pods_per_wave * kR;
-  if (tile < nt_local) eval_tile<PF>(T, pods, first, p0, p1, tile, node_base, n_local, P, my_l, kR, vbits, paux, lane);
+  if (tile < nt_local) eval_tile<PF, kENPT>(T, pods, first, p0, p1, tile, node_base, n_local, P, my_l, kR, vbits, paux, lane);
   else
     for (int q = lane; q < (p1 - p0) * kR; q += kWave) my_l[q] = 0;
   __syncthreads();
-  // group list = the kR largest of the block's kEvalWaves·kR keys, in descending key order (within one score:
+  // group list = the kR largest of the block's kEW·kR keys, in descending key order (within one score:
   // ascending node index, as the merge's tie rule reads lists); a full group list's minimum bounds every key the
   // block left out, as a full tile list's did (a full tile list's kR keys are all in the union)
-  const int ng_local = (nt_local + kEvalWaves - 1) / kEvalWaves, grp = tile0 / kEvalWaves;
-  static_assert(kEvalWaves * kR <= kWave, "one key per lane");
-  for (int pl = wave; pl < p1 - p0; pl += kEvalWaves) {
-    const uint64_t key = lane < kEvalWaves * kR ? s_lists[((size_t)(lane / kR) * pods_per_wave + pl) * kR + lane % kR] : 0;
+  const int ng_local = (nt_local + kEW - 1) / kEW, grp = tile0 / kEW;
+  static_assert(kEW * kR <= kWave, "one key per lane");
+  for (int pl = wave; pl < p1 - p0; pl += kEW) {
+    const uint64_t key = lane < kEW * kR ? s_lists[((size_t)(lane / kR) * pods_per_wave + pl) * kR + lane % kR] : 0;
     int rank = 0;
 #pragma unroll
-    for (int w = 0; w < kEvalWaves; ++w) {
+    for (int w = 0; w < kEW; ++w) {
       const ulonglong2* l2 = reinterpret_cast<const ulonglong2*>(s_lists + ((size_t)w * pods_per_wave + pl) * kR);
 #pragma unroll
       for (int q = 0; q < kR / 2; ++q) {
@@ -3890,6 +3913,8 @@ void mirror_unassign(kg_engine* e, int64_t i, int64_t uid, const int64_t est[2])
 struct RoundGeom {
   int64_t N, shard, base, n_local;
   int nt_local, B, ppw, bitmap_words;
+  int nte;     // (r4) eval_round tiles of kETile nodes in this shard
+  int nl_max;  // list slots per pod in the lists buffer: max(nt_local, nte)
   int depth;  // rounds in flight: eval(r) reads the table right after resolve(r - depth) (1 = unpipelined)
 };
 
@@ -3900,6 +3925,8 @@ RoundGeom geometry(const kg_engine* e) {
   g.base = std::min<int64_t>(g.N, (int64_t)e->rank * g.shard);
   g.n_local = std::min<int64_t>(g.shard, g.N - g.base);
   g.nt_local = (int)std::max<int64_t>(1, (g.shard + kTile - 1) / kTile);
+  g.nte = (int)std::max<int64_t>(1, (g.shard + kETile - 1) / kETile);
+  g.nl_max = std::max(g.nt_local, g.nte);
   g.B = (int)(e->cfg.batch_pods > 0 ? e->cfg.batch_pods : 32);
   g.ppw = (int)(e->cfg.pods_per_wave > 0 ? std::min<int64_t>(e->cfg.pods_per_wave, g.B) : 8);
   g.bitmap_words = (int)(((std::max<int64_t>(g.N, 1) + 127) / 128) * 4);  // whole 16-B stores
@@ -3925,7 +3952,11 @@ size_t resolve_numa_lds_bytes(const RoundGeom& g, int nb) {
 }
 NumaTable numa_table(kg_engine* e) { return NumaTable{e->numa_s.p, e->numa_m.p}; }
 
-size_t eval_lds_bytes(const RoundGeom& g) { return (size_t)kEvalWaves * g.ppw * kR * 8; }
+size_t eval_lds_bytes(const RoundGeom& g) { return (size_t)kEW * g.ppw * kR * 8; }
+// eval_round's 1-D grid: tile groups of kEW tiles × pod groups, swizzled over XCDs inside the kernel
+dim3 eval_grid_e(const RoundGeom& g, int nb) {
+  return dim3((unsigned)(((g.nte + kEW - 1) / kEW) * ((nb + g.ppw - 1) / g.ppw)));
+}
 dim3 eval_grid(const RoundGeom& g, int nb) {
   // 1-D grid: tile groups × pod groups, swizzled over XCDs inside eval_round
   return dim3((unsigned)(((g.nt_local + kEvalWaves - 1) / kEvalWaves) * ((nb + g.ppw - 1) / g.ppw)));
@@ -3957,11 +3988,11 @@ int profile_bits(const EvalParams& P) {
 
 int32_t* poison_ptr(kg_engine* e) { return reinterpret_cast<int32_t*>(e->cursor.p + 3); }
 uint64_t* lists_slot(kg_engine* e, const RoundGeom& g, int slot) {
-  return e->lists.p + (size_t)slot * g.B * g.nt_local * kR;
+  return e->lists.p + (size_t)slot * g.B * g.nl_max * kR;
 }
 
-constexpr int kCombineTiles = 64;  // combined lists from 64 tiles on (16 group lists = 128 keys ≥ kC per pod)
-bool eval_combine(const RoundGeom& g) { return g.nt_local >= kCombineTiles; }
+constexpr int kCombineTiles = 16 * kEW;  // combined lists from 16 tile groups on (128 keys ≥ kC per pod)
+bool eval_combine(const RoundGeom& g) { return g.nte >= kCombineTiles; }
 void launch_eval(kg_engine* e, const RoundGeom& g, int64_t first, int nb, int slot, hipStream_t st) {
   if (e->numa_on) {  // one block per (tile, pod group)
     const dim3 grid((unsigned)(g.nt_local * ((nb + g.ppw - 1) / g.ppw)));
@@ -3971,9 +4002,9 @@ void launch_eval(kg_engine* e, const RoundGeom& g, int64_t first, int nb, int sl
     return;
   }
 #define KG_EVAL(X)                                                                                        \
-  eval_round<X><<<eval_grid(g, nb), kWave * kEvalWaves, eval_lds_bytes(g), st>>>(e->T, e->pods.p, first, nb,   \
+  eval_round<X><<<eval_grid_e(g, nb), kWave * kEW, eval_lds_bytes(g), st>>>(e->T, e->pods.p, first, nb,       \
                                                                                 g.ppw, g.base,                   \
-                                                                 g.n_local, g.nt_local, e->P,             \
+                                                                 g.n_local, g.nte, e->P,                  \
                                                                  lists_slot(e, g, slot), poison_ptr(e), e->paux.p, \
                                                                  eval_combine(g) ? 1 : 0)
   KG_PF_SWITCH(profile_bits(e->P), KG_EVAL)
@@ -3983,7 +4014,8 @@ void launch_eval(kg_engine* e, const RoundGeom& g, int64_t first, int nb, int sl
 // candidate lists per pod of the round's wide pass: eval_round writes one per tile group of kEvalWaves tiles, the
 // NUMA and DeviceShare passes one per tile
 int eval_lists(kg_engine* e, const RoundGeom& g) {
-  return (e->numa_on || e->ds_on || !eval_combine(g)) ? g.nt_local : (g.nt_local + kEvalWaves - 1) / kEvalWaves;
+  if (e->numa_on || e->ds_on) return g.nt_local;
+  return eval_combine(g) ? (g.nte + kEW - 1) / kEW : g.nte;
 }
 
 // local merge: this rank's tile lists → per-pod record (single rank: the final candidates)
@@ -4266,7 +4298,7 @@ int prepare_rounds(kg_engine* e, RoundGeom& g) {
     return fail(KG_E_UNSUPPORTED, "resolver LDS %zu B > %zu B: a smaller batch_pods", mw_lds_bytes(g.B), kMaxLds);
   const size_t D = (size_t)g.depth;
   const size_t lists_n = e->lists.n;
-  if (int rc = e->lists.ensure(D * g.B * g.nt_local * kR)) return rc;
+  if (int rc = e->lists.ensure(D * g.B * g.nl_max * kR)) return rc;
   if (e->lists.n != lists_n)  // fresh lists hold no keys (DeviceShare rounds merge every one of the B slots)
     HIP_TRY(hipMemsetAsync(e->lists.p, 0, e->lists.n * 8, e->stream));
   const size_t cand_n = e->cand.n;
