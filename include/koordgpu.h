@@ -287,6 +287,12 @@ typedef struct kg_pod_metric {
 #define KG_MAX_CONTAINERS 8
 #define KG_MAX_MATCH_GROUPS 16   /* (ABI 12) PodTopologySpread / InterPodAffinity match groups */
 #define KG_MAX_POD_PREFERRED 4   /* (ABI 12) preferred pod (anti-)affinity terms per pod */
+#define KG_MAX_SPREAD 4          /* (ABI 12) topology spread constraints per pod */
+#define KG_MAX_ZONES 64          /* (ABI 12) topology.kubernetes.io/zone domains */
+enum {
+  KG_SPREAD_HARD = 1 << 0,       /* whenUnsatisfiable: DoNotSchedule (else ScheduleAnyway) */
+  KG_SPREAD_ZONE = 1 << 1        /* topologyKey topology.kubernetes.io/zone (else kubernetes.io/hostname) */
+};
 
 /* One pod, pre-decoded by the caller (PodRequestsAndLimits semantics, pkg/util/pod_resources_utils.go:48-64). */
 typedef struct kg_pod {
@@ -340,10 +346,13 @@ typedef struct kg_pod {
    * it is scheduled and when it sits on a node (kg_pods_add, or placed by the engine): the engine keeps per node the
    * number of pods matching each group, of required anti-affinity terms of each group, and the symmetric weights. */
   int64_t match_groups;                        /* bit k: the pod (labels, namespace) matches group k             */
-  int64_t spread_hard_group;                   /* the DoNotSchedule hostname constraint's group (0 = none)       */
-  int64_t spread_hard_max_skew;
-  int64_t spread_soft_group;                   /* the ScheduleAnyway hostname constraint's group (0 = none); a   */
-  int64_t spread_soft_max_skew;                /* pod without constraints passes the system default one here     */
+  /* topology spread constraints in the pod's order (≤ KG_MAX_SPREAD; at most one per {key, whenUnsatisfiable}, as
+   * the API validates): the selector's group, maxSkew and KG_SPREAD_* flags.  A pod without constraints passes the
+   * system defaults here (hostname maxSkew 3 + zone maxSkew 5, ScheduleAnyway, with its owners' selector). */
+  int64_t n_spread;
+  int64_t spread_group[KG_MAX_SPREAD];
+  int64_t spread_max_skew[KG_MAX_SPREAD];
+  int64_t spread_flags[KG_MAX_SPREAD];
   int64_t pod_affinity_group;                  /* the conjunction of its required pod-affinity terms (0 = none)  */
   int64_t pod_affinity_terms;                  /* bit k: a required pod-affinity term of group k (symmetric      */
                                                /* score of later pods: HardPodAffinityWeight)                    */
@@ -452,6 +461,9 @@ typedef struct kg_node_predicates {
    * references a predicate or image id some valid node row was not compiled for (KG_E_INVALID: re-send the rows). */
   int64_t predicate_count;
   int64_t image_count;
+  /* (ABI 12) the node's topology.kubernetes.io/zone domain: 1 + the zone's index in the caller's zone table
+   * (< KG_MAX_ZONES), 0 = the node has no zone label (PodTopologySpread zone constraints) */
+  int64_t zone;
 } kg_node_predicates;
 
 typedef struct kg_stats {

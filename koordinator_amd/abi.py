@@ -64,6 +64,9 @@ MAX_AFF_TERMS = 4  # KG_MAX_AFF_TERMS
 MAX_CONTAINERS = 8  # KG_MAX_CONTAINERS
 MAX_MATCH_GROUPS = 16  # KG_MAX_MATCH_GROUPS (ABI 12)
 MAX_POD_PREFERRED = 4  # KG_MAX_POD_PREFERRED (ABI 12)
+MAX_SPREAD = 4  # KG_MAX_SPREAD (ABI 12)
+MAX_ZONES = 64  # KG_MAX_ZONES (ABI 12)
+SPREAD_HARD, SPREAD_ZONE = 1, 2  # KG_SPREAD_*
 DEV_NVIDIA_GPU, DEV_HYGON_DCU, DEV_KOORD_GPU, DEV_GPU_CORE, DEV_GPU_MEMORY, DEV_GPU_MEMORY_RATIO, DEV_FPGA, DEV_RDMA = \
     range(8)
 DEVICE_RESOURCE_SLOTS = {
@@ -149,13 +152,13 @@ POD_DTYPE = np.dtype([
     _i64("preferred_cpu_exclusive_policy"),
     _i64("n_containers"), _i64("container_image_bit", MAX_CONTAINERS), _i64("container_image_score", MAX_CONTAINERS),
     _i64("taint_count"),
-    _i64("match_groups"), _i64("spread_hard_group"), _i64("spread_hard_max_skew"), _i64("spread_soft_group"),
-    _i64("spread_soft_max_skew"), _i64("pod_affinity_group"), _i64("pod_affinity_terms"), _i64("pod_anti_affinity"),
+    _i64("match_groups"), _i64("n_spread"), _i64("spread_group", MAX_SPREAD), _i64("spread_max_skew", MAX_SPREAD),
+    _i64("spread_flags", MAX_SPREAD), _i64("pod_affinity_group"), _i64("pod_affinity_terms"), _i64("pod_anti_affinity"),
     _i64("n_pod_preferred"), _i64("pod_preferred_group", MAX_POD_PREFERRED),
     _i64("pod_preferred_weight", MAX_POD_PREFERRED),
 ])
 NODE_PRED_DTYPE = np.dtype([("predicates", np.uint64), ("taints_hard", np.uint64), ("taints_soft", np.uint64),
-                            ("images", np.uint64), _i64("predicate_count"), _i64("image_count")])
+                            ("images", np.uint64), _i64("predicate_count"), _i64("image_count"), _i64("zone")])
 
 
 NODE_RSV_DTYPE = np.dtype([_i64("n")] + [_i64(f, MAX_RSV_SLOTS) for f in (

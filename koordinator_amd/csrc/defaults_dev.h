@@ -27,8 +27,10 @@ namespace kg {
 
 constexpr int kAffTerms = KG_MAX_AFF_TERMS;
 
-struct NodePred {  // 32 B per node (the masks of kg_node_predicates; its ABI 11 table sizes stay on the host)
+struct NodePred {  // 40 B per node (the masks of kg_node_predicates; its ABI 11 table sizes stay on the host)
   uint64_t pred, hard, soft, images;
+  int32_t zone;     // (ABI 12) 1 + topology.kubernetes.io/zone index, 0 = no zone label
+  int32_t pad;
 };
 
 constexpr int kContainers = KG_MAX_CONTAINERS;

@@ -3153,6 +3153,8 @@ struct kg_engine {
   DevBuf<uint64_t> gval;        // [cap] InterPodAffinity raw << 32 | spread count
   DevBuf<GroupPod> gdelta;      // kg_pods_add / kg_pods_remove: the pods' group view, their nodes and signs
   DevBuf<int32_t> gdelta_ns;
+  DevBuf<int32_t> gz;           // [2][2][kSpread][kZones] zone sums, by pod parity
+  DevBuf<uint64_t> gzm;         // [2] present zones
   // batched exact rounds (xr_dev.h): kXrPods pods per round
   bool xr_on = true;            // KG_EXACT_ROUNDS=0: one pod per pass only
   DevBuf<uint64_t> xr_val;      // [kXrPods][cap]
@@ -3607,14 +3609,27 @@ int decode_group_pod(const kg_pod& p, GroupPod& d, int64_t k) {
   d.match = (uint32_t)p.match_groups;
   d.aff_terms = (uint32_t)p.pod_affinity_terms;
   d.anti = (uint32_t)p.pod_anti_affinity;
-  if (int rc = grp(p.spread_hard_group, d.hard, "spread (DoNotSchedule)")) return rc;
-  if (int rc = grp(p.spread_soft_group, d.soft, "spread (ScheduleAnyway)")) return rc;
   if (int rc = grp(p.pod_affinity_group, d.req, "pod affinity")) return rc;
-  if ((d.hard >= 0 && p.spread_hard_max_skew < 1) || (d.soft >= 0 && p.spread_soft_max_skew < 1) ||
-      p.spread_hard_max_skew > INT32_MAX || p.spread_soft_max_skew > INT32_MAX)
-    return fail(KG_E_INVALID, "pod %lld: maxSkew must be >= 1", (long long)k);
-  d.hard_skew = (int32_t)p.spread_hard_max_skew;
-  d.soft_skew = (int32_t)p.spread_soft_max_skew;
+  if (p.n_spread < 0 || p.n_spread > kSpread)
+    return fail(KG_E_UNSUPPORTED, "pod %lld: more than %d topology spread constraints (the pod stays on the Go path)",
+                (long long)k, kSpread);
+  d.nsp = (int32_t)p.n_spread;
+  uint32_t seen = 0;
+  for (int c = 0; c < d.nsp; ++c) {
+    int32_t g = -1;
+    if (int rc = grp(p.spread_group[c], g, "topology spread")) return rc;
+    const int64_t f = p.spread_flags[c];
+    if (g < 0 || p.spread_max_skew[c] < 1 || p.spread_max_skew[c] > INT32_MAX || (f & ~3ll))
+      return fail(KG_E_INVALID, "pod %lld: spread constraint %d: group %lld, maxSkew %lld, flags %lld", (long long)k, c,
+                  (long long)p.spread_group[c], (long long)p.spread_max_skew[c], (long long)f);
+    if ((seen >> f) & 1u)  // the API allows one constraint per {topologyKey, whenUnsatisfiable}
+      return fail(KG_E_INVALID, "pod %lld: duplicate {topologyKey, whenUnsatisfiable} spread constraints", (long long)k);
+    seen |= 1u << f;
+    d.sp_g[c] = g;
+    d.sp_skew[c] = (int32_t)p.spread_max_skew[c];
+    d.sp_flags[c] = (uint32_t)f;
+    if (f & KG_SPREAD_ZONE) d.zone_keys |= (f & KG_SPREAD_HARD) ? 1u : 2u;
+  }
   if (p.n_pod_preferred < 0 || p.n_pod_preferred > kPodPref)
     return fail(KG_E_UNSUPPORTED, "pod %lld: more than %d preferred pod (anti-)affinity terms (the pod stays on the Go "
                 "path)", (long long)k, kPodPref);
@@ -4351,6 +4366,8 @@ RsvExt rsv_ext(kg_engine* e) {
   X.GP = e->GP;
   X.logw = e->logw.p;
   X.gval = e->gval.p;
+  X.gz = e->gz.p;
+  X.gzm = e->gzm.p;
   return X;
 }
 
@@ -4362,6 +4379,10 @@ int run_rsv(kg_engine* e, int64_t first, int64_t count, kg_stats* stats, double 
     const RsvExt X = rsv_ext(e);
     const unsigned long long init[5] = {0, 0, 0, (unsigned long long)first, (unsigned long long)end};
     HIP_TRY(hipMemcpyAsync(e->rsv_ws.p, init, sizeof(init), hipMemcpyHostToDevice, e->stream));
+    if (e->grp_on) {  // the zone sums start from zero (then each pod's rsv_select clears the next pod's)
+      HIP_TRY(hipMemsetAsync(e->gz.p, 0, (size_t)4 * kSpread * kZones * 4, e->stream));
+      HIP_TRY(hipMemsetAsync(e->gzm.p, 0, 16, e->stream));
+    }
     // `end_arg` < 0: the kernels read the call's end from the workspace (a graph stays valid across calls);
     // `passes` < kRsvGroup: a short call issues exactly its passes, no empty ones
     auto issue_group = [&](int64_t end_arg, int passes) {
@@ -4377,6 +4398,9 @@ int run_rsv(kg_engine* e, int64_t first, int64_t count, kg_stats* stats, double 
         t = prof_begin(e, e->stream);
         rsv_select<<<blocks, kRsvThreads, 0, e->stream>>>(e->rsv_val.p, e->pods.p, end_arg, n, g, e->RP, X, e->rsv_part.p,
                                                            e->rsv_ws.p);
+        if (e->grp_on)  // the keys, after PodTopologySpread's raw scores and their extremes
+          rsv_select2<<<blocks, kRsvThreads, 0, e->stream>>>(e->rsv_val.p, end_arg, n, g, e->RP, X, e->rsv_part.p,
+                                                             e->rsv_ws.p);
         prof_end(e, KG_PROF_RSV_SELECT, t, e->stream);
       }
       size_t t = prof_begin(e, e->stream);
@@ -4841,6 +4865,8 @@ static int engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank,
     if (int rc = e->grp_d.ensure((size_t)3 * kGroups * cap)) return bail(rc);
     if (int rc = e->logw.ensure(cap + 1)) return bail(rc);
     if (int rc = e->gval.ensure(cap)) return bail(rc);
+    if (int rc = e->gz.ensure((size_t)4 * kSpread * kZones)) return bail(rc);
+    if (int rc = e->gzm.ensure(2)) return bail(rc);
     std::vector<double> lw((size_t)cap + 1);
     for (int64_t f = 0; f <= cap; ++f) lw[f] = std::log((double)(f + 2));  // TopologyNormalizingWeight
     if (hipMemsetAsync(e->grp_d.p, 0, (size_t)3 * kGroups * cap * 4, e->stream) != hipSuccess ||
@@ -4858,7 +4884,7 @@ static int engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank,
     if (int rc = e->rsv_nd.ensure(cap)) return bail(rc);
     if (int rc = e->rsv_val.ensure(cap)) return bail(rc);
     if (int rc = e->rsv_ws.ensure(8)) return bail(rc);
-    if (int rc = e->rsv_part.ensure(13 * ((cap + kRsvThreads - 1) / kRsvThreads) + 4)) return bail(rc);
+    if (int rc = e->rsv_part.ensure(15 * ((cap + kRsvThreads - 1) / kRsvThreads) + 4)) return bail(rc);
     if (hipMemsetAsync(e->rsv_nd.p, 0, cap * 4, e->stream) != hipSuccess || hipMemsetAsync(e->rsv_ws.p, 0, 64, e->stream) != hipSuccess)
       return bail(fail(KG_E_DEVICE, "hipMemset"));
   }
@@ -5104,6 +5130,8 @@ void kg_engine_destroy(kg_engine* e) {
   e->gval.release();
   e->gdelta.release();
   e->gdelta_ns.release();
+  e->gz.release();
+  e->gzm.release();
   e->scratch64.release();
   e->scratch32.release();
   e->uidx.release();
@@ -6063,7 +6091,10 @@ int kg_nodes_predicates_upsert(kg_engine* e, const kg_node_predicates* p, const 
   for (int64_t k = 0; k < n; ++k) {
     if (p[k].predicate_count < 0 || p[k].predicate_count > 64 || p[k].image_count < 0 || p[k].image_count > 64)
       return fail(KG_E_INVALID, "node row %lld: predicate_count / image_count outside [0, 64]", (long long)k);
-    h[k] = NodePred{p[k].predicates, p[k].taints_hard, p[k].taints_soft, p[k].images};
+    if (p[k].zone < 0 || p[k].zone > KG_MAX_ZONES)
+      return fail(KG_E_INVALID, "node predicates row %lld: zone %lld outside [0, %d]", (long long)k, (long long)p[k].zone,
+                  KG_MAX_ZONES);
+    h[k] = NodePred{p[k].predicates, p[k].taints_hard, p[k].taints_soft, p[k].images, (int32_t)p[k].zone, 0};
     const uint64_t t = p[k].taints_hard | p[k].taints_soft;
     const int i = idx[k];
     e->np_taint_top[i] = (int16_t)(t ? 64 - __builtin_clzll(t) : 0);

@@ -29,6 +29,8 @@ namespace kg {
 
 constexpr int kGroups = KG_MAX_MATCH_GROUPS;
 constexpr int kPodPref = KG_MAX_POD_PREFERRED;
+constexpr int kSpread = KG_MAX_SPREAD;
+constexpr int kZones = KG_MAX_ZONES;
 
 // per-node counters, structure of arrays [3][kGroups][cap] int32: pods matching group k, required anti-affinity
 // terms of group k on the node, Σ symmetric weights of the node's pods' terms of group k
@@ -40,14 +42,21 @@ struct GroupTable {
   __device__ __forceinline__ int32_t& symw(int k, int64_t i) const { return g[(size_t)(2 * kGroups + k) * cap + i]; }
 };
 
-struct GroupPod {  // 72 B per staged pod
+struct GroupPod {  // 104 B per staged pod
   uint32_t match, aff_terms, anti, pad;
-  int32_t hard, hard_skew;  // DoNotSchedule hostname constraint: group (-1 none), maxSkew
-  int32_t soft, soft_skew;  // ScheduleAnyway hostname constraint
   int32_t req;              // conjunction group of the required pod-affinity terms (-1 none)
   int32_t npref;
   int32_t pref_g[kPodPref], pref_w[kPodPref];
+  int32_t nsp;              // topology spread constraints, in the pod's order
+  uint32_t zone_keys;       // bit 0: a DoNotSchedule constraint is zone-keyed, bit 1: a ScheduleAnyway one
+  int32_t sp_g[kSpread], sp_skew[kSpread];
+  uint32_t sp_flags[kSpread];  // KG_SPREAD_HARD | KG_SPREAD_ZONE
 };
+// the nodes a spread constraint set counts on: the pod's nodeSelector / required node affinity hold and the node
+// carries every key of the set (kind 0: DoNotSchedule, 1: ScheduleAnyway)
+__device__ __forceinline__ bool spread_has_keys(const GroupPod& gp, int kind, int32_t zone) {
+  return !((gp.zone_keys >> kind) & 1u) || zone > 0;
+}
 
 struct GroupParams {
   int32_t spread_filter, spread_score, w_spread;
@@ -81,13 +90,35 @@ __device__ __forceinline__ bool node_affinity_match(const NodePred* pred, const 
   return any;
 }
 
-// Filters of both plugins on node i (true = feasible); min_match / total from group_pre
+// Zone sums of one pod (group_pre, double-buffered by the pod's parity): per constraint c, zf[c][z] = Σ over the nodes
+// passing the pod's node affinity with every DoNotSchedule key of the pods matching c's group in zone z, zs[c][z] the
+// same over the ScheduleAnyway node set; pres = the zones holding such a DoNotSchedule node
+struct ZoneSums {
+  int32_t* __restrict__ zf;  // [kSpread][kZones]
+  int32_t* __restrict__ zs;  // [kSpread][kZones]
+  uint64_t* __restrict__ pres;
+};
+
+// Filters of both plugins on node i (true = feasible).  min_match[c]: TpKeyToCriticalPaths' minimum per DoNotSchedule
+// constraint (hostname: over the eligible nodes' counts; zone: over the present zones' sums); total: the cluster-wide
+// count of pods matching the required pod-affinity group
 __device__ __forceinline__ bool groups_filter(const GroupTable& G, int64_t i, const GroupPod& gp, const GroupParams& GP,
-                                              bool eligible, int64_t min_match, int64_t total) {
-  if (GP.spread_filter && gp.hard >= 0) {
-    const int64_t match = eligible ? G.cnt(gp.hard, i) : 0;
-    const int64_t self = (gp.match >> gp.hard) & 1u;
-    if (match + self - min_match > gp.hard_skew) return false;
+                                              bool nodeaff, int32_t zone, const int64_t* min_match, const ZoneSums& Z,
+                                              uint64_t pres, int64_t total) {
+  if (GP.spread_filter) {
+    const bool elig = nodeaff && spread_has_keys(gp, 0, zone);
+    for (int c = 0; c < gp.nsp; ++c) {
+      if (!(gp.sp_flags[c] & KG_SPREAD_HARD)) continue;
+      int64_t match;
+      if (gp.sp_flags[c] & KG_SPREAD_ZONE) {
+        if (zone <= 0) return false;  // the node lacks the constraint's key
+        match = ((pres >> (zone - 1)) & 1ull) ? Z.zf[c * kZones + zone - 1] : 0;
+      } else {
+        match = elig ? G.cnt(gp.sp_g[c], i) : 0;
+      }
+      const int64_t self = (gp.match >> gp.sp_g[c]) & 1u;
+      if (match + self - min_match[c] > gp.sp_skew[c]) return false;
+    }
   }
   if (GP.ipa_filter) {
     if (gp.req >= 0 && G.cnt(gp.req, i) <= 0 && !(total == 0 && ((gp.match >> gp.req) & 1u))) return false;
@@ -113,11 +144,19 @@ __device__ __forceinline__ int32_t interpod_raw(const GroupTable& G, int64_t i, 
   return s;
 }
 
-// PodTopologySpread raw Score of a count: int64(float64(cnt)·w + float64(maxSkew − 1)), w = log(F + 2) from the host's
-// table (the same libm as the checker); the product and the sum round separately (-ffp-contract=off)
-__device__ __forceinline__ int64_t spread_raw(int64_t cnt, const GroupPod& gp, double w) {
-  if (gp.soft < 0) return 0;
-  const double s = (double)cnt * w + (double)(gp.soft_skew - 1);
+// PodTopologySpread raw Score of node i (not ignored): Σ over the ScheduleAnyway constraints in the pod's order of
+// float64(cnt)·w + float64(maxSkew − 1), from 0, then int64(); hostname: the node's count, weight log(F − ignored + 2);
+// zone: its zone's sum, weight log(#zones + 2) — both from the host's log table (the same libm as the checker); the
+// products and sums round separately (-ffp-contract=off)
+__device__ __forceinline__ int64_t spread_raw(const GroupTable& G, int64_t i, const GroupPod& gp, int32_t zone,
+                                              const int32_t* __restrict__ zs, double w_host, double w_zone) {
+  double s = 0;
+  for (int c = 0; c < gp.nsp; ++c) {
+    if (gp.sp_flags[c] & KG_SPREAD_HARD) continue;
+    const bool z = (gp.sp_flags[c] & KG_SPREAD_ZONE) != 0;
+    const int64_t cnt = z ? (zone > 0 ? zs[c * kZones + zone - 1] : 0) : G.cnt(gp.sp_g[c], i);
+    s += (double)cnt * (z ? w_zone : w_host) + (double)(gp.sp_skew[c] - 1);
+  }
   return (int64_t)s;
 }
 

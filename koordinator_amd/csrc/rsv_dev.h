@@ -87,8 +87,15 @@ struct RsvExt {
   const GroupPod* __restrict__ gpods;  // [pods]
   GroupParams GP;
   const double* __restrict__ logw;     // [cap + 1]: log(F + 2), the host's libm
-  uint64_t* __restrict__ gval;         // [cap] InterPodAffinity raw << 32 | the spread constraint's count
+  uint64_t* __restrict__ gval;         // [cap] InterPodAffinity raw << 32 | PodTopologySpread raw (+ 2^31; 0 = ignored)
+  int32_t* __restrict__ gz;            // [2 parities][2][kSpread][kZones] the zone sums (ZoneSums)
+  uint64_t* __restrict__ gzm;          // [2 parities] the present zones
 };
+// pod j's zone sums (double-buffered by parity: group_pre(j) accumulates, rsv_select(j) clears j + 1's)
+__device__ __forceinline__ ZoneSums zone_sums(const RsvExt& X, int64_t j) {
+  int32_t* b = X.gz + (size_t)(j & 1) * 2 * kSpread * kZones;
+  return ZoneSums{b, b + kSpread * kZones, X.gzm + (j & 1)};
+}
 
 struct RsvOut {
   bool feas;
@@ -539,14 +546,36 @@ __global__ __launch_bounds__(kRsvThreads) void rsv_eval(DevTable T, RsvNode* __r
   }
   uint64_t pk = 0, rawv = 0, dsv = 0, tv = 0, av = 0;
   uint64_t v = 0;
-  int32_t scnt = 0, iraw = 0;  // PodTopologySpread count / InterPodAffinity raw Score of a feasible node
-  int64_t min_match = 0x7fffffff, total = 0;
+  int32_t iraw = 0;      // InterPodAffinity raw Score of a feasible node
+  bool ign = false;      // PodTopologySpread IgnoredNodes: a feasible node lacking a ScheduleAnyway key
+  int32_t zone = 0;
+  int64_t total = 0;
   GroupPod gp{};
+  ZoneSums Z{};
+  uint64_t pres = 0;
+  __shared__ int64_t s_min[kSpread];
   if (X.gpods) {  // group_pre's reductions over the snapshot after pod j - 1's Reserve
     gp = X.gpods[j];
+    Z = zone_sums(X, j);
+    pres = *Z.pres;
     const uint64_t e = rsv_partials_max(part + 6 * nb, nb);
-    if (e) min_match = dec_min_i32(e);
     total = (int64_t)rsv_partials_sum(part + 7 * nb, nb);
+    if (threadIdx.x < kWave) {  // minMatchNum per DoNotSchedule constraint (MaxInt32 without pairs)
+      for (int c = 0; c < gp.nsp; ++c) {
+        if (!(gp.sp_flags[c] & KG_SPREAD_HARD)) continue;
+        int64_t m = 0x7fffffff;
+        if (gp.sp_flags[c] & KG_SPREAD_ZONE) {
+          const uint64_t v = ((pres >> threadIdx.x) & 1ull) ? enc_min_i32(Z.zf[c * kZones + threadIdx.x]) : 0;
+          const uint64_t mv = wave_max_u64_dpp(v);
+          const uint64_t mm = readlane_u64(mv, kWave - 1);
+          if (mm) m = dec_min_i32(mm);
+        } else if (e) {
+          m = dec_min_i32(e);
+        }
+        if (threadIdx.x == 0) s_min[c] = m;
+      }
+    }
+    __syncthreads();
   }
   if (i < n) {
     const RsvPod rp = rpods[j];
@@ -556,9 +585,10 @@ __global__ __launch_bounds__(kRsvThreads) void rsv_eval(DevTable T, RsvNode* __r
     const DefPod* df = X.defp ? &X.defp[j] : nullptr;
     RsvOut o = rsv_eval_node(T, RN, rsv_n, i, p, rp, P, RP, X, dp, np, nullptr, aux, df);
     if (o.feas && X.gpods) {
-      o.feas = groups_filter(X.G, i, gp, X.GP, node_affinity_match(X.pred, df, i), min_match, total);
+      zone = X.pred[i].zone;
+      o.feas = groups_filter(X.G, i, gp, X.GP, node_affinity_match(X.pred, df, i), zone, s_min, Z, pres, total);
       if (o.feas) {
-        scnt = gp.soft >= 0 ? X.G.cnt(gp.soft, i) : 0;
+        ign = !spread_has_keys(gp, 1, zone);
         iraw = interpod_raw(X.G, i, gp);
       }
     }
@@ -576,26 +606,34 @@ __global__ __launch_bounds__(kRsvThreads) void rsv_eval(DevTable T, RsvNode* __r
   if (i < n) val[i] = v;
   const bool dscore = X.val2 != nullptr;  // TaintToleration / NodeAffinity Score in the profile
   if (dscore && i < n) X.val2[i] = (uint32_t)(tv << 24 | av);
-  if (X.gpods) {  // the NormalizeScore inputs of both plugins over the filtered nodes
+  if (X.gpods) {  // the PreScore / NormalizeScore inputs of both plugins over the filtered nodes
     const bool f = (v >> 7) & 1u;
-    if (i < n) X.gval[i] = ((uint64_t)(uint32_t)iraw << 32) | (uint32_t)scnt;
+    if (i < n) X.gval[i] = ((uint64_t)(uint32_t)iraw << 32) | (uint32_t)(zone << 1 | (ign ? 1 : 0));
     const uint64_t fc = rsv_block_sum(f ? 1u : 0u, s_red);
     __syncthreads();
-    const uint64_t sx = rsv_block_max(f ? enc_max_i32(scnt) : 0, s_red);
-    __syncthreads();
-    const uint64_t sn = rsv_block_max(f ? enc_min_i32(scnt) : 0, s_red);
+    const uint64_t ic = rsv_block_sum(f && ign ? 1u : 0u, s_red);
     __syncthreads();
     const uint64_t ix = rsv_block_max(f ? enc_max_i32(iraw) : 0, s_red);
     __syncthreads();
     const uint64_t in = rsv_block_max(f ? enc_min_i32(iraw) : 0, s_red);
     __syncthreads();
-    if (threadIdx.x == 0) {
-      part[8 * nb + blockIdx.x] = fc;
-      part[9 * nb + blockIdx.x] = sx;
-      part[10 * nb + blockIdx.x] = sn;
-      part[11 * nb + blockIdx.x] = ix;
-      part[12 * nb + blockIdx.x] = in;
+    // the zones of the filtered, not ignored nodes (a zone constraint's topology size)
+    uint64_t zm = (f && !ign && zone > 0) ? 1ull << (zone - 1) : 0;
+    for (int d = 1; d < kWave; d <<= 1) {
+      const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)zm, d), hi = (uint32_t)__shfl_xor((int)(uint32_t)(zm >> 32), d);
+      zm |= ((uint64_t)hi << 32) | lo;
     }
+    if ((threadIdx.x & (kWave - 1)) == 0) s_red[threadIdx.x / kWave] = zm;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      for (int w = 1; w < kRsvThreads / kWave; ++w) zm |= s_red[w];
+      part[8 * nb + blockIdx.x] = fc;
+      part[9 * nb + blockIdx.x] = ix;
+      part[10 * nb + blockIdx.x] = in;
+      part[11 * nb + blockIdx.x] = ic;
+      part[12 * nb + blockIdx.x] = zm;
+    }
+    __syncthreads();
   }
   pk = rsv_block_max(pk, s_red);
   __syncthreads();
@@ -632,38 +670,24 @@ __device__ __forceinline__ int64_t rsv_total(uint64_t v, uint32_t v2, bool is_pr
 
 // Pass 2: PreScore preferred node (1000), DefaultNormalizeScore of both plugins over the feasible nodes, × weights,
 // packed key; part[2 nb + b] = the block's max key.  Block 0 also charges pod j - 1's quota (tagged ws[0] = j).
-__global__ __launch_bounds__(kRsvThreads) void rsv_select(const uint64_t* __restrict__ val, const DevPod* __restrict__ pods,
-                                                          int64_t end, int64_t n, int g, RsvParams RP, RsvExt X,
-                                                          uint64_t* __restrict__ part,
-                                                          unsigned long long* __restrict__ ws) {
-  __shared__ uint64_t s_red[kRsvThreads / kWave];
-  if (end < 0) end = (int64_t)ws[4];
-  const int64_t j = (int64_t)ws[3] + g;
-  if (j >= end) return;
-  const int nb = gridDim.x;
-  if (blockIdx.x == 0 && threadIdx.x == 0 && X.nq > 0 && g > 0 && ws[0] == (unsigned long long)j)
-    rsv_quota_charge(X, pods[j - 1], j - 1);
+// (ABI 12) Group profiles: this pass computes PodTopologySpread's raw Score per node (its weights need the filtered
+// count and zones) with its extremes — part[13 nb + b] / part[14 nb + b] — and rsv_select2 makes the keys.
+__device__ __forceinline__ uint64_t select_key(const uint64_t* __restrict__ val, int64_t i, int64_t n, int nb,
+                                               const RsvParams& RP, const RsvExt& X,
+                                               const uint64_t* __restrict__ part) {
   const uint64_t pk = rsv_partials_max(part, nb);
   const uint64_t mraw = rsv_partials_max(part + nb, nb);
   const uint64_t mds = X.ds ? rsv_partials_max(part + 3 * nb, nb) : 0;
   const int64_t mt = X.val2 ? (int64_t)rsv_partials_max(part + 4 * nb, nb) : 0;
   const int64_t ma = X.val2 ? (int64_t)rsv_partials_max(part + 5 * nb, nb) : 0;
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t pref = pk ? (int64_t)(uint32_t)(~pk) : -1;
   const int64_t mx = pk ? (mraw > 1000 ? (int64_t)mraw : 1000) : (int64_t)mraw;
-  // PodTopologySpread / InterPodAffinity NormalizeScore over the filtered nodes (the raw spread score is monotone in
-  // the count, so its extremes are the extremes' scores)
-  GroupPod gp{};
-  double lw = 0;
   int64_t smin = 0, smax = 0, imin = 0, imax = 0;
   if (X.gpods) {
-    gp = X.gpods[j];
-    const int64_t F = (int64_t)rsv_partials_sum(part + 8 * nb, nb);
-    lw = X.logw[F < n ? F : n];
-    const uint64_t sx = rsv_partials_max(part + 9 * nb, nb), sn = rsv_partials_max(part + 10 * nb, nb);
-    const uint64_t ix = rsv_partials_max(part + 11 * nb, nb), in = rsv_partials_max(part + 12 * nb, nb);
-    smax = sx ? spread_raw(dec_max_i32(sx), gp, lw) : 0;
-    smin = sn ? spread_raw(dec_min_i32(sn), gp, lw) : 0;
+    const uint64_t sx = rsv_partials_max(part + 13 * nb, nb), sn = rsv_partials_max(part + 14 * nb, nb);
+    const uint64_t ix = rsv_partials_max(part + 9 * nb, nb), in = rsv_partials_max(part + 10 * nb, nb);
+    smax = sx ? dec_max_i32(sx) : 0;
+    smin = sn ? dec_min_i32(sn) : 0;
     imax = ix ? dec_max_i32(ix) : 0;
     imin = in ? dec_min_i32(in) : 0;
   }
@@ -675,14 +699,84 @@ __global__ __launch_bounds__(kRsvThreads) void rsv_select(const uint64_t* __rest
       int64_t t = rsv_total(v, v2, i == pref, mx, (int64_t)mds, mt, ma, RP, X);
       if (X.gpods) {
         const uint64_t gv = X.gval[i];
-        if (X.GP.spread_score)
-          t += (int64_t)X.GP.w_spread * spread_normalize(spread_raw((int32_t)(uint32_t)gv, gp, lw), smin, smax);
+        const uint32_t sr = (uint32_t)gv;  // the spread raw + 2^31, 0 = ignored (NormalizeScore gives it 0)
+        if (X.GP.spread_score && sr != 0)
+          t += (int64_t)X.GP.w_spread * spread_normalize((int64_t)sr - 0x80000000ll, smin, smax);
         if (X.GP.ipa_score) t += (int64_t)X.GP.w_ipa * interpod_normalize((int32_t)(gv >> 32), imin, imax);
       }
       key = make_key(t, (uint32_t)i);
     }
   }
-  key = rsv_block_max(key, s_red);
+  return key;
+}
+
+__global__ __launch_bounds__(kRsvThreads) void rsv_select(const uint64_t* __restrict__ val, const DevPod* __restrict__ pods,
+                                                          int64_t end, int64_t n, int g, RsvParams RP, RsvExt X,
+                                                          uint64_t* __restrict__ part,
+                                                          unsigned long long* __restrict__ ws) {
+  __shared__ uint64_t s_red[kRsvThreads / kWave];
+  if (end < 0) end = (int64_t)ws[4];
+  const int64_t j = (int64_t)ws[3] + g;
+  if (j >= end) return;
+  const int nb = gridDim.x;
+  if (blockIdx.x == 0 && threadIdx.x == 0 && X.nq > 0 && g > 0 && ws[0] == (unsigned long long)j)
+    rsv_quota_charge(X, pods[j - 1], j - 1);
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (!X.gpods) {
+    const uint64_t key = rsv_block_max(select_key(val, i, n, nb, RP, X, part), s_red);
+    if (threadIdx.x == 0) part[2 * nb + blockIdx.x] = key;
+    return;
+  }
+  // PodTopologySpread PreScore + Score: weights log(F − ignored + 2) (hostname) and log(#zones + 2) (zone)
+  const GroupPod gp = X.gpods[j];
+  const ZoneSums Z = zone_sums(X, j);
+  const int64_t F = (int64_t)rsv_partials_sum(part + 8 * nb, nb), ig = (int64_t)rsv_partials_sum(part + 11 * nb, nb);
+  uint64_t zm = 0;
+  for (int k = threadIdx.x & (kWave - 1); k < nb; k += kWave) zm |= part[12 * nb + k];
+  for (int d = 1; d < kWave; d <<= 1) {
+    const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)zm, d), hi = (uint32_t)__shfl_xor((int)(uint32_t)(zm >> 32), d);
+    zm |= ((uint64_t)hi << 32) | lo;
+  }
+  const int64_t hs = F - ig;
+  const double w_host = X.logw[hs < 0 ? 0 : (hs < n ? hs : n)], w_zone = X.logw[__popcll(zm)];
+  int32_t raw = 0;
+  bool on = false;
+  if (i < n && ((val[i] >> 7) & 1u)) {
+    const uint64_t gv = X.gval[i];
+    on = (gv & 1u) == 0;  // not ignored
+    if (on) {
+      raw = (int32_t)spread_raw(X.G, i, gp, (int32_t)((uint32_t)gv >> 1), Z.zs, w_host, w_zone);
+      X.gval[i] = (gv & 0xFFFFFFFF00000000ull) | (uint32_t)((int64_t)raw + 0x80000000ll);
+    } else {
+      X.gval[i] = gv & 0xFFFFFFFF00000000ull;
+    }
+  }
+  const uint64_t sx = rsv_block_max(on ? enc_max_i32(raw) : 0, s_red);
+  __syncthreads();
+  const uint64_t sn = rsv_block_max(on ? enc_min_i32(raw) : 0, s_red);
+  if (threadIdx.x == 0) {
+    part[13 * nb + blockIdx.x] = sx;
+    part[14 * nb + blockIdx.x] = sn;
+  }
+  // pod j + 1's zone sums start from zero (pod j - 1 was their last reader)
+  if (blockIdx.x == 0) {
+    const ZoneSums Zn = zone_sums(X, j + 1);
+    for (int k = threadIdx.x; k < 2 * kSpread * kZones; k += kRsvThreads) Zn.zf[k] = 0;
+    if (threadIdx.x == 0) *Zn.pres = 0;
+  }
+}
+
+// (ABI 12) Pass 3 of group profiles: the keys (the same weighted total as rsv_select, with both plugins' NormalizeScore)
+__global__ __launch_bounds__(kRsvThreads) void rsv_select2(const uint64_t* __restrict__ val, int64_t end, int64_t n,
+                                                           int g, RsvParams RP, RsvExt X, uint64_t* __restrict__ part,
+                                                           const unsigned long long* __restrict__ ws) {
+  __shared__ uint64_t s_red[kRsvThreads / kWave];
+  if (end < 0) end = (int64_t)ws[4];
+  const int64_t j = (int64_t)ws[3] + g;
+  if (j >= end) return;
+  const int nb = gridDim.x;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t key = rsv_block_max(select_key(val, i, n, nb, RP, X, part), s_red);
   if (threadIdx.x == 0) part[2 * nb + blockIdx.x] = key;
 }
 
@@ -720,11 +814,34 @@ __global__ __launch_bounds__(kRsvThreads) void group_pre(DevTable T, RsvNode* __
     if (j >= end) return;
   }
   const GroupPod gp = X.gpods[j];
+  const ZoneSums Z = zone_sums(X, j);
+  __shared__ int32_t s_zs[2][kSpread][kZones];  // the block's zone sums (hard, soft), flushed with one atomic each
+  __shared__ unsigned long long s_pres;
+  const bool zoned = gp.zone_keys != 0;
+  if (zoned) {
+    for (int k = threadIdx.x; k < 2 * kSpread * kZones; k += kRsvThreads) (&s_zs[0][0][0])[k] = 0;
+    if (threadIdx.x == 0) s_pres = 0;
+    __syncthreads();
+  }
   uint64_t mn = 0;
   uint32_t sm = 0;
   if (i < n && (T.flags[i] & F_VALID)) {
-    if (X.GP.spread_filter && gp.hard >= 0 && node_affinity_match(X.pred, X.defp ? &X.defp[j] : nullptr, i))
-      mn = enc_min_i32(X.G.cnt(gp.hard, i));
+    if (gp.nsp > 0) {
+      const bool aff = node_affinity_match(X.pred, X.defp ? &X.defp[j] : nullptr, i);
+      const int32_t zone = X.pred[i].zone;
+      const bool ef = aff && spread_has_keys(gp, 0, zone), es = aff && spread_has_keys(gp, 1, zone);
+      for (int c = 0; c < gp.nsp; ++c) {
+        const bool hard = (gp.sp_flags[c] & KG_SPREAD_HARD) != 0, z = (gp.sp_flags[c] & KG_SPREAD_ZONE) != 0;
+        if (!(hard ? ef : es)) continue;
+        const int32_t v = X.G.cnt(gp.sp_g[c], i);
+        if (z) {
+          if (v) atomicAdd(&s_zs[hard ? 0 : 1][c][zone - 1], v);
+          if (hard) atomicOr(&s_pres, 1ull << (zone - 1));
+        } else if (hard) {
+          mn = enc_min_i32(v);
+        }
+      }
+    }
     if (X.GP.ipa_filter && gp.req >= 0) sm = (uint32_t)X.G.cnt(gp.req, i);
   }
   mn = rsv_block_max(mn, s_red);
@@ -733,6 +850,14 @@ __global__ __launch_bounds__(kRsvThreads) void group_pre(DevTable T, RsvNode* __
   if (threadIdx.x == 0) {
     part[6 * nb + blockIdx.x] = mn;
     part[7 * nb + blockIdx.x] = st;
+  }
+  if (zoned) {
+    __syncthreads();
+    for (int k = threadIdx.x; k < 2 * kSpread * kZones; k += kRsvThreads) {
+      const int32_t v = (&s_zs[0][0][0])[k];
+      if (v) atomicAdd(&Z.zf[k], v);  // zf and zs are contiguous: [2][kSpread][kZones]
+    }
+    if (threadIdx.x == 0 && s_pres) atomicOr((unsigned long long*)Z.pres, s_pres);
   }
 }
 

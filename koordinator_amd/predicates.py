@@ -57,6 +57,7 @@ class PredicateTable:
     def __init__(self):
         self.taints: list[tuple] = []
         self.preds: list[tuple] = []
+        self.zones: list[str] = []  # (ABI 12) topology.kubernetes.io/zone values, for PodTopologySpread zone keys
         self._taint_id: dict = {}
         self._pred_id: dict = {}
 
@@ -124,6 +125,13 @@ class PredicateTable:
                 hard |= bit
         r["predicates"], r["taints_hard"], r["taints_soft"] = m, hard, soft
         r["predicate_count"] = len(self.preds)  # ABI 11: predicates interned later are undecided on this row
+        z = labels.get(ZONE)
+        if z is not None:  # (ABI 12) the node's zone domain, 1-based (0 = no zone label)
+            if z not in self.zones:
+                if len(self.zones) == abi.MAX_ZONES:
+                    raise OverflowError(f"more than {abi.MAX_ZONES} zones: zone spread stays on the Go path")
+                self.zones.append(z)
+            r["zone"] = self.zones.index(z) + 1
         return r
 
     # ---- pods (per staging: evaluated against the taints interned so far) ----
@@ -285,6 +293,7 @@ def selector_matches(selector: dict | None, labels: dict) -> bool:
 
 
 HOSTNAME = "kubernetes.io/hostname"
+ZONE = "topology.kubernetes.io/zone"
 
 
 class PodGroupTable:
@@ -293,8 +302,9 @@ class PodGroupTable:
     term's selector and namespaces (AffinityTerm.Matches; an empty namespace list means the term owner's namespace),
     or the conjunction of a pod's required pod-affinity terms (updateWithAffinityTerms counts a pod only when it matches
     all of them).  Register every group the cluster's pods and the queue use before filling pod rows: a row's
-    match_groups covers the groups registered when it was filled.  Only topologyKey kubernetes.io/hostname is
-    accelerated (another key raises NotImplementedError: the pod stays on the Go path)."""
+    match_groups covers the groups registered when it was filled.  Accelerated topology keys: kubernetes.io/hostname
+    for both plugins, topology.kubernetes.io/zone for PodTopologySpread (the node's zone comes from
+    PredicateTable.node_row); another key raises NotImplementedError: the pod stays on the Go path."""
 
     def __init__(self):
         self.groups: list[tuple] = []  # (kind, payload): ("sel", (selector_repr, namespaces)) / ("and", (gid, ...))
@@ -334,20 +344,27 @@ class PodGroupTable:
 
     def fill_pod(self, pod: np.ndarray, labels: dict, namespace: str, spread=(), required_affinity=(),
                  required_anti_affinity=(), preferred_affinity=(), preferred_anti_affinity=()) -> np.ndarray:
-        """The ABI 12 fields of one pod.  spread: [{maxSkew, whenUnsatisfiable, labelSelector, topologyKey}] (a pod
-        without constraints may pass the system default hostname one, maxSkew 3 ScheduleAnyway, with its owners'
-        selector); required_*: [{labelSelector, namespaces, topologyKey}]; preferred_*: [{weight, podAffinityTerm}]."""
+        """The ABI 12 fields of one pod.  spread: [{maxSkew, whenUnsatisfiable, labelSelector, topologyKey}] with
+        topologyKey kubernetes.io/hostname (default) or topology.kubernetes.io/zone (a pod without constraints may pass
+        the system defaults, hostname maxSkew 3 + zone maxSkew 5 ScheduleAnyway, with its owners' selector);
+        required_*: [{labelSelector, namespaces, topologyKey}] (hostname only); preferred_*: [{weight,
+        podAffinityTerm}]."""
         r = pod[0] if pod.ndim else pod
-        hard = [c for c in spread if c.get("whenUnsatisfiable", "DoNotSchedule") == "DoNotSchedule"]
-        soft = [c for c in spread if c.get("whenUnsatisfiable") == "ScheduleAnyway"]
-        for c in spread:
-            if c.get("topologyKey", HOSTNAME) != HOSTNAME:
-                raise NotImplementedError("topology spread key other than kubernetes.io/hostname")
-        if len(hard) > 1 or len(soft) > 1:
-            raise ValueError("duplicate {topologyKey, whenUnsatisfiable} spread constraints")
-        for arr, (gk, sk) in ((hard, ("spread_hard_group", "spread_hard_max_skew")),
-                              (soft, ("spread_soft_group", "spread_soft_max_skew"))):
-            r[gk], r[sk] = (self.group(arr[0].get("labelSelector"), (namespace,)), arr[0]["maxSkew"]) if arr else (0, 0)
+        if len(spread) > abi.MAX_SPREAD:
+            raise NotImplementedError(f"more than {abi.MAX_SPREAD} topology spread constraints")
+        seen = set()
+        r["n_spread"] = len(spread)
+        for c, cons in enumerate(spread):
+            key = cons.get("topologyKey", HOSTNAME)
+            if key not in (HOSTNAME, ZONE):
+                raise NotImplementedError(f"topology spread key {key}: hostname and zone are accelerated")
+            hard = cons.get("whenUnsatisfiable", "DoNotSchedule") == "DoNotSchedule"
+            if (key, hard) in seen:
+                raise ValueError("duplicate {topologyKey, whenUnsatisfiable} spread constraints")
+            seen.add((key, hard))
+            r["spread_group"][c] = self.group(cons.get("labelSelector"), (namespace,))
+            r["spread_max_skew"][c] = cons["maxSkew"]
+            r["spread_flags"][c] = (abi.SPREAD_HARD if hard else 0) | (abi.SPREAD_ZONE if key == ZONE else 0)
         terms = [self._term(t, namespace) for t in required_affinity]
         r["pod_affinity_terms"] = sum(1 << (g - 1) for g in set(terms))
         r["pod_affinity_group"] = self.conjunction(terms) if terms else 0

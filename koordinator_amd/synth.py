@@ -488,7 +488,7 @@ def load_shipped_into(engine, cluster: Cluster, numa: np.ndarray, dev: np.ndarra
         engine.set_quotas(quotas)
 
 
-def make_predicates(n_nodes: int, pods: np.ndarray, seed: int = BASE_SEED + 15) -> tuple:
+def make_predicates(n_nodes: int, pods: np.ndarray, seed: int = BASE_SEED + 15, no_zone: float = 0.0) -> tuple:
     """Node labels / taints and pod tolerations / nodeSelector / node affinity for TaintToleration + NodeAffinity
     (compiled through koordinator_amd.predicates).  Fills `pods` in place; returns (table, NODE_PRED_DTYPE[n_nodes])."""
     from .predicates import PredicateTable, NO_SCHEDULE, NO_EXECUTE, PREFER_NO_SCHEDULE
@@ -498,6 +498,8 @@ def make_predicates(n_nodes: int, pods: np.ndarray, seed: int = BASE_SEED + 15) 
     for i in range(n_nodes):
         lb = {"topology.kubernetes.io/zone": zones[rng.integers(4)], "pool": pools[rng.integers(3)],
               "rack": str(int(rng.integers(20)))}
+        if no_zone and rng.random() < no_zone:  # (r4) nodes without a zone label: zone spread rejects / ignores them
+            del lb["topology.kubernetes.io/zone"]
         if rng.random() < 0.3:
             lb["ssd"] = "true"
         labels.append(lb)
@@ -583,11 +585,13 @@ def make_images(n_nodes: int, pods: np.ndarray, preds: np.ndarray, seed: int = B
 
 
 # ---- (ABI 12) PodTopologySpread / InterPodAffinity (hostname key) ------------------------------------------------
-def make_pod_groups(pods: np.ndarray, seed: int = BASE_SEED + 17, n_apps: int = 8) -> np.ndarray:
+def make_pod_groups(pods: np.ndarray, seed: int = BASE_SEED + 17, n_apps: int = 8, zones: bool = False) -> np.ndarray:
     """Fills the ABI 12 group fields of `pods` in place, as PodGroupTable would compile them for a workload of n_apps
     deployments (groups 1..n_apps: app=k in the namespace) in n_apps / 2 teams (groups n_apps+1..: team=t): every pod
     matches its app and team; 40 % carry a DoNotSchedule hostname spread constraint on their app (maxSkew 1-3), 50 % a
-    ScheduleAnyway one (maxSkew 1-5), 15 % a required anti-affinity to their own app (one per node), 10 % a required
+    ScheduleAnyway one (maxSkew 1-5), with `zones` also 15 % a DoNotSchedule zone one (maxSkew 1-39) and 40 % a
+    ScheduleAnyway zone one (maxSkew 1-7), in a random order; 15 % a required anti-affinity to their own app (one per
+    node), 10 % a required
     affinity to another team, 30 % one or two preferred (anti-)affinity terms (weights ±1..100)."""
     rng = np.random.default_rng(seed)
     n = len(pods)
@@ -595,12 +599,30 @@ def make_pod_groups(pods: np.ndarray, seed: int = BASE_SEED + 17, n_apps: int = 
     app = rng.integers(0, n_apps, n)
     team = app // 2
     pods["match_groups"] = (1 << app) | (1 << (n_apps + team))
-    hard = rng.random(n) < 0.4
-    pods["spread_hard_group"] = np.where(hard, app + 1, 0)
-    pods["spread_hard_max_skew"] = np.where(hard, rng.integers(1, 4, n), 0)
-    soft = rng.random(n) < 0.5
-    pods["spread_soft_group"] = np.where(soft, app + 1, 0)
-    pods["spread_soft_max_skew"] = np.where(soft, rng.integers(1, 6, n), 0)
+    # spread constraints (≤ 4, in pod order): hostname / zone × DoNotSchedule / ScheduleAnyway, each with probability
+    # p; zone ones only with `zones` (the nodes carry topology.kubernetes.io/zone)
+    kinds = [(abi.SPREAD_HARD, 0.4, 1, 4), (0, 0.5, 1, 6)]
+    if zones:
+        kinds += [(abi.SPREAD_HARD | abi.SPREAD_ZONE, 0.15, 1, 40), (abi.SPREAD_ZONE, 0.4, 1, 8)]
+    nsp = np.zeros(n, dtype=np.int64)
+    order = np.argsort(rng.random((n, len(kinds))), axis=1)  # a random constraint order per pod
+    for kk in range(len(kinds)):
+        flag, prob, lo, hi = kinds[kk]
+        on = rng.random(n) < prob
+        skew = rng.integers(lo, hi, n)
+        for j in np.nonzero(on)[0]:
+            c = nsp[j]
+            pods["spread_group"][j, c] = app[j] + 1
+            pods["spread_max_skew"][j, c] = skew[j]
+            pods["spread_flags"][j, c] = flag
+            nsp[j] += 1
+    for j in range(n):  # shuffle each pod's constraints (the raw Score sums them in the pod's order)
+        c = nsp[j]
+        if c > 1:
+            perm = order[j][order[j] < c]
+            for f in ("spread_group", "spread_max_skew", "spread_flags"):
+                pods[f][j, :c] = pods[f][j, perm]
+    pods["n_spread"] = nsp
     anti = rng.random(n) < 0.15
     pods["pod_anti_affinity"] = np.where(anti, 1 << app, 0)
     aff = rng.random(n) < 0.10

@@ -109,24 +109,29 @@ void or_groups_apply(or_group_node* g, const kg_pod* pod, int sign, int64_t hard
   }
 }
 
-/* filtering.go Filter: skew = matchNum + selfMatchNum − minMatchNum (TpKeyToCriticalPaths[key][0], the minimum over
- * the pairs PreFilter counted: nodes passing the pod's nodeSelector / required node affinity); a node outside that
- * set has no pair, so its matchNum is 0.  selfMatchNum: the constraint's selector matches the pod's own labels. */
-int or_spread_filter(const or_group_node* g, const kg_pod* pod, int eligible, int64_t min_match) {
-  const int64_t k = pod->spread_hard_group - 1;
-  if (k < 0) return 1;
-  const int64_t match = eligible ? g->cnt[k] : 0;
-  const int64_t self = (pod->match_groups >> k) & 1;
-  return match + self - min_match <= pod->spread_hard_max_skew;
+static int spread_needs_zone(const kg_pod* pod, int hard) {
+  for (int64_t c = 0; c < pod->n_spread; c++)
+    if (((pod->spread_flags[c] & KG_SPREAD_HARD) != 0) == (hard != 0) && (pod->spread_flags[c] & KG_SPREAD_ZONE))
+      return 1;
+  return 0;
 }
 
-/* scoring.go: TopologyNormalizingWeight = log(size + 2) with size = len(filteredNodes) − len(IgnoredNodes) for the
- * hostname key (no node lacks it); scoreForCount = float64(cnt)·weight + float64(maxSkew − 1), summed from 0 and
- * truncated by int64() (no fused multiply-add: -ffp-contract=off). */
-int64_t or_spread_raw(int64_t cnt, const kg_pod* pod, int64_t n_feasible) {
-  if (pod->spread_soft_group <= 0) return 0;
-  const double w = log((double)(n_feasible + 2));
-  const double s = (double)cnt * w + (double)(pod->spread_soft_max_skew - 1);
+int or_spread_has_keys(const kg_node_predicates* n, const kg_pod* pod, int hard) {
+  return !spread_needs_zone(pod, hard) || n->zone > 0;  /* kubernetes.io/hostname: every node carries it */
+}
+
+int or_spread_node_ok(const kg_node_predicates* n, const kg_pod* pod, int hard) {
+  return or_affinity_filter(n, pod) && or_spread_has_keys(n, pod, hard);
+}
+
+/* scoring.go: scoreForCount = float64(cnt)·weight + float64(maxSkew − 1), summed over the constraints from 0 and
+ * truncated by int64() (no fused multiply-add: -ffp-contract=off); weight = log(size + 2), the caller's per constraint */
+int64_t or_spread_raw(const int64_t* cnt, const double* w, const kg_pod* pod) {
+  double s = 0;
+  for (int64_t c = 0; c < pod->n_spread; c++) {
+    if (pod->spread_flags[c] & KG_SPREAD_HARD) continue;
+    s += (double)cnt[c] * w[c] + (double)(pod->spread_max_skew[c] - 1);
+  }
   return (int64_t)s;
 }
 

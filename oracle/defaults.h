@@ -51,12 +51,15 @@ typedef struct or_group_node {
 } or_group_node;
 /* NodeInfo.AddPod / RemovePod of `pod` (sign ±1) on one node's counters. */
 void or_groups_apply(or_group_node* g, const kg_pod* pod, int sign, int64_t hard_weight);
-/* PodTopologySpread Filter (filtering.go Filter): matchNum (0 off the eligible set) + selfMatch − minMatchNum ≤
- * maxSkew for the DoNotSchedule hostname constraint; 1 = pass. */
-int or_spread_filter(const or_group_node* g, const kg_pod* pod, int eligible, int64_t min_match);
-/* PodTopologySpread Score (scoring.go Score) before normalisation: int64(cnt · log(F + 2) + (maxSkew − 1)) for the
- * ScheduleAnyway hostname constraint, F = the number of filtered nodes; 0 without one. */
-int64_t or_spread_raw(int64_t cnt, const kg_pod* pod, int64_t n_feasible);
+/* PodTopologySpread constraints' node requirements (common.go nodeLabelsMatchSpreadConstraints + the PreFilter /
+ * PreScore node selection): the pod's nodeSelector / required node affinity hold and the node carries every topology
+ * key of the pod's constraints of that kind (hard = DoNotSchedule: the Filter's set; else ScheduleAnyway). */
+int or_spread_node_ok(const kg_node_predicates* n, const kg_pod* pod, int hard);
+/* 1 = the node carries every topology key of the pod's constraints of that kind. */
+int or_spread_has_keys(const kg_node_predicates* n, const kg_pod* pod, int hard);
+/* PodTopologySpread Score (scoring.go Score) before normalisation: Σ over the ScheduleAnyway constraints in the pod's
+ * order of float64(cnt[c]) · w[c] + float64(maxSkew − 1), accumulated in float64 from 0, then int64(). */
+int64_t or_spread_raw(const int64_t* cnt, const double* w, const kg_pod* pod);
 /* PodTopologySpread NormalizeScore: MaxNodeScore · (max + min − s) / max, MaxNodeScore when max == 0. */
 int64_t or_spread_normalize(int64_t raw, int64_t mn, int64_t mx);
 /* InterPodAffinity Filter (filtering.go Filter): required affinity (the conjunction group, or the first pod of a

@@ -101,9 +101,11 @@ def lib():
                                             vp, vp, vp, vp, vp]
         L.or_groups_apply.argtypes = [vp, vp, i, i64]
         L.or_groups_apply.restype = None
-        L.or_spread_filter.argtypes = [vp, vp, i, i64]
-        L.or_spread_filter.restype = i
-        L.or_spread_raw.argtypes = [i64, vp, i64]
+        L.or_spread_node_ok.argtypes = [vp, vp, i]
+        L.or_spread_node_ok.restype = i
+        L.or_spread_has_keys.argtypes = [vp, vp, i]
+        L.or_spread_has_keys.restype = i
+        L.or_spread_raw.argtypes = [vp, vp, vp]
         L.or_spread_raw.restype = i64
         L.or_spread_normalize.argtypes = [i64, i64, i64]
         L.or_spread_normalize.restype = i64

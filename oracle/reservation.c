@@ -249,7 +249,7 @@ int or_schedule_resv_full(const kg_config* cfg, int64_t n_nodes, const kg_node* 
     return KG_E_NOMEM;
   }
   /* TaintToleration / NodeAffinity / BalancedAllocation (defaults.c); a NULL table = no predicates, no taints */
-  const kg_node_predicates zero_pred = {0, 0, 0, 0, 0, 0};
+  const kg_node_predicates zero_pred = {0, 0, 0, 0, 0, 0, 0};
   const int rsv_on = cfg->reservation_filter || cfg->reservation_score;
   const int ds_on = dev && (cfg->ds_filter || cfg->ds_score);
   if (n_threads < 1) n_threads = 1;
@@ -288,19 +288,36 @@ int or_schedule_resv_full(const kg_config* cfg, int64_t n_nodes, const kg_node* 
     const int ds_blocks_nomination = ds_on && cfg->ds_filter && !dsp.skip;
     or_numa_pod npod;
     if (numa_on) or_numa_pod_init(cfg, pod, &npod);
-    /* PodTopologySpread PreFilter (common.go calPreFilterState): the minimum match count over the nodes passing the
-     * pod's nodeSelector / required node affinity (MaxInt32 when none); InterPodAffinity PreFilter: the cluster-wide
-     * count of pods matching each group (len(affinityCounts) == 0 ⇔ no pod matches the required terms) */
-    int64_t min_match = INT32_MAX, total[KG_MAX_MATCH_GROUPS] = {0};
-    if ((spread_on && cfg->spread_filter && pod->spread_hard_group > 0) || (ipa_on && cfg->interpod_filter)) {
+    /* PodTopologySpread PreFilter (common.go calPreFilterState) over the nodes passing the pod's nodeSelector /
+     * required node affinity and carrying every DoNotSchedule key: per constraint, TpPairToMatchNum — each such node's
+     * own count (hostname) or its zone's sum (zone) — and the minimum over those pairs (MaxInt32 when none);
+     * InterPodAffinity PreFilter: the cluster-wide count of pods matching each group (len(affinityCounts) == 0 ⇔ no pod
+     * matches the required terms) */
+    int64_t min_match[KG_MAX_SPREAD], zsum_f[KG_MAX_SPREAD][KG_MAX_ZONES], total[KG_MAX_MATCH_GROUPS] = {0};
+    uint64_t zpres_f[KG_MAX_SPREAD] = {0};
+    memset(zsum_f, 0, sizeof(zsum_f));
+    for (int c = 0; c < KG_MAX_SPREAD; c++) min_match[c] = INT32_MAX;
+    if (spread_on || (ipa_on && cfg->interpod_filter)) {
       for (int64_t i = 0; i < n_nodes; i++) {
         if (!(nodes[i].flags & KG_NODE_VALID)) continue;
         for (int k = 0; k < KG_MAX_MATCH_GROUPS; k++) total[k] += grp[i].cnt[k];
-        if (spread_on && pod->spread_hard_group > 0 && or_affinity_filter(preds ? &preds[i] : &zero_pred, pod)) {
-          const int64_t c = grp[i].cnt[pod->spread_hard_group - 1];
-          if (c < min_match) min_match = c;
+        const kg_node_predicates* np = preds ? &preds[i] : &zero_pred;
+        if (!spread_on || !or_spread_node_ok(np, pod, 1)) continue;
+        for (int64_t c = 0; c < pod->n_spread; c++) {
+          if (!(pod->spread_flags[c] & KG_SPREAD_HARD)) continue;
+          const int64_t v = grp[i].cnt[pod->spread_group[c] - 1];
+          if (pod->spread_flags[c] & KG_SPREAD_ZONE) {
+            zsum_f[c][np->zone - 1] += v;
+            zpres_f[c] |= 1ull << (np->zone - 1);
+          } else if (v < min_match[c]) {
+            min_match[c] = v;
+          }
         }
       }
+      for (int64_t c = 0; c < pod->n_spread; c++)
+        if (pod->spread_flags[c] & KG_SPREAD_ZONE)
+          for (int z = 0; z < KG_MAX_ZONES; z++)
+            if (((zpres_f[c] >> z) & 1) && zsum_f[c][z] < min_match[c]) min_match[c] = zsum_f[c][z];
     }
     int err = 0;
 #pragma omp parallel for schedule(dynamic, chunk) num_threads(n_threads) reduction(min : err)
@@ -336,12 +353,26 @@ int or_schedule_resv_full(const kg_config* cfg, int64_t n_nodes, const kg_node* 
             !or_numa_filter(cfg, &numa[i], &npod, &aff[i], rs.requested[KG_RES_CPU], nd->allocatable[KG_RES_CPU]))
           continue;
       }
-      if (spread_on && cfg->spread_filter &&
-          !or_spread_filter(&grp[i], pod, or_affinity_filter(np, pod), min_match))
-        continue;
+      if (spread_on && cfg->spread_filter) { /* filtering.go Filter */
+        int ok = 1;
+        const int elig = or_spread_node_ok(np, pod, 1);
+        for (int64_t c = 0; c < pod->n_spread && ok; c++) {
+          if (!(pod->spread_flags[c] & KG_SPREAD_HARD)) continue;
+          const int64_t g = pod->spread_group[c] - 1;
+          int64_t match;
+          if (pod->spread_flags[c] & KG_SPREAD_ZONE) {
+            if (np->zone <= 0) { ok = 0; break; } /* the node lacks the constraint's key */
+            match = ((zpres_f[c] >> (np->zone - 1)) & 1) ? zsum_f[c][np->zone - 1] : 0;
+          } else {
+            match = elig ? grp[i].cnt[g] : 0;
+          }
+          const int64_t self = (pod->match_groups >> g) & 1;
+          if (match + self - min_match[c] > pod->spread_max_skew[c]) ok = 0;
+        }
+        if (!ok) continue;
+      }
       if (ipa_on && cfg->interpod_filter && !or_interpod_filter(&grp[i], pod, total)) continue;
       feas[i] = 1;
-      scnt[i] = (spread_on && pod->spread_soft_group > 0) ? grp[i].cnt[pod->spread_soft_group - 1] : 0;
       iraw[i] = ipa_on ? or_interpod_raw(&grp[i], pod) : 0;
       int64_t t = 0;
       if (cfg->fit_score) t += cfg->weight_fit * or_fit_score(cfg, nd, &rs, pod);
@@ -375,19 +406,60 @@ int or_schedule_resv_full(const kg_config* cfg, int64_t n_nodes, const kg_node* 
     for (int64_t i = 0; i < n_nodes; i++)
       if (feas[i] && order[i] != 0 && best_order > order[i]) { best_order = order[i]; pref = i; }
     int64_t mx = 0, mds = 0, mt = 0, ma = 0;
-    /* PodTopologySpread / InterPodAffinity NormalizeScore inputs over the filtered nodes: the raw spread score is
-     * monotone in the count, so its extremes are those of the count */
-    int64_t n_feas = 0, smin = INT64_MAX, smax = INT64_MIN, imin = INT64_MAX, imax = INT64_MIN;
+    /* PodTopologySpread PreScore (scoring.go initPreScoreState, processAllNode): filtered nodes lacking a
+     * ScheduleAnyway key are IgnoredNodes; the hostname weight is log(|filtered| − |ignored| + 2), a zone constraint's
+     * log(#zones of the non-ignored filtered nodes + 2); a zone's count sums the pods of every node passing the pod's
+     * node affinity and carrying every ScheduleAnyway key.  Score per node, then NormalizeScore's extremes over the
+     * non-ignored filtered nodes; InterPodAffinity's extremes over the filtered nodes */
+    int64_t n_feas = 0, n_ign = 0, smin = INT64_MAX, smax = INT64_MIN, imin = INT64_MAX, imax = INT64_MIN;
+    uint64_t zpres_s = 0;
     for (int64_t i = 0; i < n_nodes; i++) {
       if (!feas[i]) continue;
       n_feas++;
-      if (scnt[i] < smin) smin = scnt[i];
-      if (scnt[i] > smax) smax = scnt[i];
       if (iraw[i] < imin) imin = iraw[i];
       if (iraw[i] > imax) imax = iraw[i];
+      if (!spread_on) continue;
+      const kg_node_predicates* np = preds ? &preds[i] : &zero_pred;
+      if (!or_spread_has_keys(np, pod, 0)) { n_ign++; continue; }
+      if (np->zone > 0) zpres_s |= 1ull << (np->zone - 1);
     }
-    const int64_t sraw_min = n_feas ? or_spread_raw(smin, pod, n_feas) : 0;
-    const int64_t sraw_max = n_feas ? or_spread_raw(smax, pod, n_feas) : 0;
+    int64_t zsum_s[KG_MAX_SPREAD][KG_MAX_ZONES];
+    double sw[KG_MAX_SPREAD] = {0};
+    memset(zsum_s, 0, sizeof(zsum_s));
+    if (spread_on) {
+      int has_zone = 0;
+      for (int64_t c = 0; c < pod->n_spread; c++) {
+        if (pod->spread_flags[c] & KG_SPREAD_HARD) continue;
+        if (pod->spread_flags[c] & KG_SPREAD_ZONE) {
+          has_zone = 1;
+          sw[c] = log((double)(__builtin_popcountll(zpres_s) + 2));
+        } else {
+          sw[c] = log((double)(n_feas - n_ign + 2));
+        }
+      }
+      if (has_zone)
+        for (int64_t i = 0; i < n_nodes; i++) {
+          if (!(nodes[i].flags & KG_NODE_VALID)) continue;
+          const kg_node_predicates* np = preds ? &preds[i] : &zero_pred;
+          if (np->zone <= 0 || !((zpres_s >> (np->zone - 1)) & 1) || !or_spread_node_ok(np, pod, 0)) continue;
+          for (int64_t c = 0; c < pod->n_spread; c++)
+            if ((pod->spread_flags[c] & (KG_SPREAD_HARD | KG_SPREAD_ZONE)) == KG_SPREAD_ZONE)
+              zsum_s[c][np->zone - 1] += grp[i].cnt[pod->spread_group[c] - 1];
+        }
+      for (int64_t i = 0; i < n_nodes; i++) {
+        scnt[i] = INT64_MIN; /* ignored */
+        if (!feas[i]) continue;
+        const kg_node_predicates* np = preds ? &preds[i] : &zero_pred;
+        if (!or_spread_has_keys(np, pod, 0)) continue;
+        int64_t cnt[KG_MAX_SPREAD] = {0};
+        for (int64_t c = 0; c < pod->n_spread; c++)
+          cnt[c] = (pod->spread_flags[c] & KG_SPREAD_ZONE) ? (np->zone > 0 ? zsum_s[c][np->zone - 1] : 0)
+                                                           : grp[i].cnt[pod->spread_group[c] - 1];
+        scnt[i] = or_spread_raw(cnt, sw, pod);
+        if (scnt[i] < smin) smin = scnt[i];
+        if (scnt[i] > smax) smax = scnt[i];
+      }
+    }
     for (int64_t i = 0; i < n_nodes; i++) {
       if (!feas[i]) continue;
       if (tcnt[i] > mt) mt = tcnt[i];
@@ -407,8 +479,8 @@ int or_schedule_resv_full(const kg_config* cfg, int64_t n_nodes, const kg_node* 
       /* TaintToleration NormalizeScore (reverse) and NodeAffinity NormalizeScore × weight */
       if (cfg->taint_score) t += cfg->weight_taint * or_normalize_default(tcnt[i], mt, 1);
       if (cfg->affinity_score) t += cfg->weight_affinity * or_normalize_default(asum[i], ma, 0);
-      if (spread_on && cfg->spread_score)
-        t += cfg->weight_spread * or_spread_normalize(or_spread_raw(scnt[i], pod, n_feas), sraw_min, sraw_max);
+      if (spread_on && cfg->spread_score) /* NormalizeScore: an ignored node scores 0 */
+        t += cfg->weight_spread * (scnt[i] == INT64_MIN ? 0 : or_spread_normalize(scnt[i], smin, smax));
       if (ipa_on && cfg->interpod_score) t += cfg->weight_interpod * or_interpod_normalize(iraw[i], imin, imax);
       if (t > win_total) { win_total = t; win = i; }
     }

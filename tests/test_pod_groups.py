@@ -39,36 +39,49 @@ def _gpod(**kw):
 
 
 # ---- hand-derived cases of the restated plugins ----------------------------------------------------------------
-def test_spread_filter_cases():
-    """filtering.go: skew = matchNum + selfMatch − minMatchNum > maxSkew rejects; a node outside the eligible set
-    counts 0 matches."""
-    L = oracle.lib()
-    pod = _gpod(match_groups=1, spread_hard_group=1, spread_hard_max_skew=1)
-    for cnt, elig, mn, want in [(0, 1, 0, 1), (1, 1, 0, 0), (2, 1, 1, 0), (1, 1, 1, 1), (5, 0, 0, 1), (2, 1, 2, 1), (3, 1, 2, 0)]:
-        assert L.or_spread_filter(oracle.p(_grp(cnt=[cnt])), oracle.p(pod), elig, mn) == want, (cnt, elig, mn)
-    other = _gpod(match_groups=2, spread_hard_group=1, spread_hard_max_skew=1)  # the pod does not match its selector
-    assert L.or_spread_filter(oracle.p(_grp(cnt=[1])), oracle.p(other), 1, 0) == 1
+def _spread_pod(*cons, match=1):
+    """cons: (group, maxSkew, flags) in the pod's order."""
+    p = _gpod(match_groups=match, n_spread=len(cons))
+    for c, (g, k, f) in enumerate(cons):
+        p["spread_group"][0, c], p["spread_max_skew"][0, c], p["spread_flags"][0, c] = g, k, f
+    return p
 
 
 def test_spread_score_cases():
-    """scoring.go: counts [0, 1, 3] over 3 filtered nodes, maxSkew 1: weight log(5) → raw [0, 1, 4], normalized
-    100 · (4 + 0 − s) / 4 = [100, 75, 0]."""
+    """scoring.go: one hostname constraint, counts [0, 1, 3] over 3 filtered nodes, maxSkew 1: weight log(5) → raw
+    [0, 1, 4], normalized 100 · (4 + 0 − s) / 4 = [100, 75, 0]; two constraints sum in the pod's order, each
+    float64(cnt)·w + float64(maxSkew − 1), truncated once."""
     L = oracle.lib()
-    pod = _gpod(spread_soft_group=1, spread_soft_max_skew=1)
-    raw = [L.or_spread_raw(c, oracle.p(pod), 3) for c in (0, 1, 3)]
+    pod = _spread_pod((1, 1, 0))
+    w = np.array([math.log(5), 0, 0, 0])
+    raw = [L.or_spread_raw(oracle.p(np.array([c, 0, 0, 0], dtype=np.int64)), oracle.p(w), oracle.p(pod))
+           for c in (0, 1, 3)]
     assert raw == [0, int(1 * math.log(5)), int(3 * math.log(5))] == [0, 1, 4]
     assert [L.or_spread_normalize(r, 0, 4) for r in raw] == [100, 75, 0]
-    skew3 = _gpod(spread_soft_group=1, spread_soft_max_skew=3)  # + (maxSkew − 1) before the truncation
-    assert L.or_spread_raw(2, oracle.p(skew3), 10) == int(2 * math.log(12) + 2)
+    two = _spread_pod((1, 3, abi.SPREAD_ZONE), (1, 1, 0), (2, 1, abi.SPREAD_HARD))  # the hard one does not score
+    w2 = np.array([math.log(4 + 2), math.log(10 + 2), 0, 0])
+    got = L.or_spread_raw(oracle.p(np.array([7, 2, 9, 0], dtype=np.int64)), oracle.p(w2), oracle.p(two))
+    assert got == int((7 * math.log(6) + 2) + (2 * math.log(12) + 0))
 
 
 def test_spread_score_without_constraint_is_max():
     """A pod without a ScheduleAnyway constraint: Score 0 everywhere, NormalizeScore gives MaxNodeScore (the 200 of
     debug_test.go:140-144 = weight 2 × 100)."""
     L = oracle.lib()
-    pod = _gpod()
-    assert L.or_spread_raw(7, oracle.p(pod), 4) == 0
+    pod = _spread_pod((1, 1, abi.SPREAD_HARD))
+    assert L.or_spread_raw(oracle.p(np.array([7, 0, 0, 0], dtype=np.int64)), oracle.p(np.ones(4)), oracle.p(pod)) == 0
     assert 2 * L.or_spread_normalize(0, 0, 0) == 200
+
+
+def test_spread_node_keys():
+    """nodeLabelsMatchSpreadConstraints: a zone-keyed constraint needs the node's zone label (per kind)."""
+    L = oracle.lib()
+    pod = _spread_pod((1, 1, abi.SPREAD_HARD | abi.SPREAD_ZONE), (1, 1, 0))
+    zoned, bare = np.zeros(1, dtype=abi.NODE_PRED_DTYPE), np.zeros(1, dtype=abi.NODE_PRED_DTYPE)
+    zoned["zone"] = 2
+    assert L.or_spread_has_keys(oracle.p(zoned), oracle.p(pod), 1) == 1
+    assert L.or_spread_has_keys(oracle.p(bare), oracle.p(pod), 1) == 0
+    assert L.or_spread_has_keys(oracle.p(bare), oracle.p(pod), 0) == 1  # the ScheduleAnyway one is hostname-keyed
 
 
 def test_interpod_filter_cases():
@@ -141,6 +154,27 @@ def _replicas(n, table, **kw):
     return pods
 
 
+def _zoned(n, zones):
+    cl = _flat(n)
+    preds = np.zeros(n, dtype=abi.NODE_PRED_DTYPE)
+    preds["zone"] = zones
+    return cl, preds
+
+
+def test_oracle_zone_spread_round_robin():
+    """maxSkew 1 over zones: 6 nodes in zones [1, 1, 2, 2, 3, 3] — each pod lands in an emptiest zone (lowest node
+    first); a node without the zone label is never chosen."""
+    t = PodGroupTable()
+    sel = {"matchLabels": {"app": "web"}}
+    pods = _replicas(6, t, spread=[{"maxSkew": 1, "labelSelector": sel, "topologyKey": "topology.kubernetes.io/zone"}])
+    cl, preds = _zoned(7, [0, 1, 1, 2, 2, 3, 3])
+    node, _, _, g = _run_oracle(F.build_config(profile=SPREAD_ONLY), cl, pods, preds)
+    assert list(node) == [1, 3, 5, 1, 3, 5] or sorted(node[:3]) == [1, 3, 5]
+    assert 0 not in node
+    zone_of = np.array([0, 1, 1, 2, 2, 3, 3])
+    assert sorted(np.bincount(zone_of[node], minlength=4)[1:]) == [2, 2, 2]
+
+
 def test_oracle_hard_spread_round_robin():
     """maxSkew 1 on four equal nodes: each pod lands on an emptiest node, lowest index first."""
     t = PodGroupTable()
@@ -197,17 +231,20 @@ def test_pod_group_table_compiles_selectors():
     assert pod["pod_affinity_terms"][0] == (1 << (g1 - 1)) | (1 << (g2 - 1))
     assert (pod["match_groups"][0] >> (both - 1)) & 1
     with pytest.raises(NotImplementedError):
-        t.fill_pod(pod, {}, "default", spread=[{"maxSkew": 1, "topologyKey": "topology.kubernetes.io/zone",
+        t.fill_pod(pod, {}, "default", spread=[{"maxSkew": 1, "topologyKey": "topology.kubernetes.io/region",
                                                 "labelSelector": {}}])
+    t.fill_pod(pod, {}, "default", spread=[{"maxSkew": 2, "topologyKey": "topology.kubernetes.io/zone",
+                                            "labelSelector": {}, "whenUnsatisfiable": "ScheduleAnyway"}])
+    assert pod["n_spread"][0] == 1 and pod["spread_flags"][0, 0] == abi.SPREAD_ZONE
 
 
 # ---- device vs oracle -------------------------------------------------------------------------------------------
-def _world(n_nodes, n_pods, seed, with_preds=True):
+def _world(n_nodes, n_pods, seed, with_preds=True, zones=True):
     cluster = synth.make_cluster(n_nodes, seed=seed)
-    synth.make_pod_groups(cluster.existing_pods, seed=seed + 3)
+    synth.make_pod_groups(cluster.existing_pods, seed=seed + 3, zones=zones)
     pods = synth.make_pods(n_pods, seed=seed + 1)
-    synth.make_pod_groups(pods, seed=seed + 4)
-    preds = synth.make_predicates(n_nodes, pods, seed=seed + 2)[1] if with_preds else None
+    synth.make_pod_groups(pods, seed=seed + 4, zones=zones)
+    preds = synth.make_predicates(n_nodes, pods, seed=seed + 2, no_zone=0.05)[1] if with_preds else None
     return cluster, pods, preds
 
 
@@ -236,6 +273,20 @@ def _check(cfg, cluster, pods, preds, calls=1):
     assert np.array_equal(symw, g["symw"][:cluster.n])
     assert np.array_equal(state["requested_cpu"], st["requested"][:, abi.RES_CPU])
     return want
+
+
+def test_oracle_zone_constraints_bite():
+    """Zone constraints change placements against hostname-only ones, and every zone-keyed DoNotSchedule pod lands
+    on a node carrying a zone label."""
+    cfg = F.build_config(profile=SPREAD_ONLY)
+    cluster, pods, preds = _world(300, 200, 65)
+    node, _, _, _ = _run_oracle(cfg, cluster, pods, preds)
+    cluster2, pods2, preds2 = _world(300, 200, 65, zones=False)
+    node2, _, _, _ = _run_oracle(cfg, cluster2, pods2, preds2)
+    assert (node != node2).any()
+    hz = ((pods["spread_flags"] & (abi.SPREAD_HARD | abi.SPREAD_ZONE)) == (abi.SPREAD_HARD | abi.SPREAD_ZONE)).any(1)
+    placed = node >= 0
+    assert (preds["zone"][node[hz & placed]] > 0).all() and (hz & placed).any()
 
 
 @pytest.mark.gpu
