@@ -360,6 +360,12 @@ typedef struct kg_pod {
   int64_t n_pod_preferred;                     /* preferred pod (anti-)affinity terms (≤ KG_MAX_POD_PREFERRED)   */
   int64_t pod_preferred_group[KG_MAX_POD_PREFERRED];
   int64_t pod_preferred_weight[KG_MAX_POD_PREFERRED];  /* + affinity weight, − anti-affinity weight           */
+  /* InterPodAffinity terms with topologyKey topology.kubernetes.io/zone (the fields above are kubernetes.io/hostname
+   * terms): required affinity terms (bit k: a term of group k; the conjunction stays pod_affinity_group), required
+   * anti-affinity terms, and bit t: preferred term t is zone-keyed */
+  int64_t pod_affinity_terms_zone;
+  int64_t pod_anti_affinity_zone;
+  int64_t pod_preferred_zone;
 } kg_pod;
 
 /* pod reservation flags */
@@ -630,8 +636,10 @@ int kg_pods_filter_preemption(kg_engine* e, const kg_pod* pod, int32_t node_idx,
  * group k, [n][k] layout of KG_MAX_MATCH_GROUPS int32 each — pods matching group k (countPodsMatchSelector),
  * required anti-affinity terms of group k held by the node's pods (existingAntiAffinityCounts), and the symmetric
  * score weight of the node's pods' terms of group k (processExistingPod: preferred ± weight, required affinity ×
- * HardPodAffinityWeight).  Maintained from kg_pods_add / kg_pods_remove, Reserve and Unreserve. */
-int kg_nodes_read_pod_groups(kg_engine* e, int32_t* match_count, int32_t* anti_count, int32_t* sym_weight);
+ * HardPodAffinityWeight); anti_zone / sym_zone: the same for the node's pods' zone-keyed terms (NULL = skip).
+ * Maintained from kg_pods_add / kg_pods_remove, Reserve and Unreserve. */
+int kg_nodes_read_pod_groups(kg_engine* e, int32_t* match_count, int32_t* anti_count, int32_t* sym_weight,
+                             int32_t* anti_zone, int32_t* sym_zone);
 
 /* ElasticQuota admission (engines whose pods carry quota_id): replaces the quota table (n ≤ KG_MAX_QUOTAS).
  * Every scheduled pod runs PreFilter's check (used + request ≤ used_limit over the pod's cpu/memory requests; for

@@ -156,6 +156,7 @@ POD_DTYPE = np.dtype([
     _i64("spread_flags", MAX_SPREAD), _i64("pod_affinity_group"), _i64("pod_affinity_terms"), _i64("pod_anti_affinity"),
     _i64("n_pod_preferred"), _i64("pod_preferred_group", MAX_POD_PREFERRED),
     _i64("pod_preferred_weight", MAX_POD_PREFERRED),
+    _i64("pod_affinity_terms_zone"), _i64("pod_anti_affinity_zone"), _i64("pod_preferred_zone"),
 ])
 NODE_PRED_DTYPE = np.dtype([("predicates", np.uint64), ("taints_hard", np.uint64), ("taints_soft", np.uint64),
                             ("images", np.uint64), _i64("predicate_count"), _i64("image_count"), _i64("zone")])
@@ -285,7 +286,7 @@ def load_library(path: str | None = None):
         "kg_debug_numa_merge": (i, [vp, vp, i64, vp]),
         "kg_pods_evaluate_reservation": (i, [vp, vp, vp]),
         "kg_pods_filter_preemption": (i, [vp, vp, ctypes.c_int32, vp, vp, i64, vp]),
-        "kg_nodes_read_pod_groups": (i, [vp, vp, vp, vp]),
+        "kg_nodes_read_pod_groups": (i, [vp, vp, vp, vp, vp, vp]),
         "kg_nodes_predicates_upsert": (i, [vp, vp, vp, i64]),
         "kg_engine_create_hosted": (i, [vp, i64, i, i, EXCHANGE_FN, vp, ctypes.POINTER(vp)]),
     }

@@ -3147,7 +3147,7 @@ struct kg_engine {
   // (ABI 12) PodTopologySpread / InterPodAffinity, hostname key (groups_dev.h): one pod per exact pass
   bool grp_on = false;
   GroupParams GP{};
-  DevBuf<int32_t> grp_d;        // [3][kGroups][cap] per-node group counters
+  DevBuf<int32_t> grp_d;        // [kGroupArrays][kGroups][cap] per-node group counters
   DevBuf<GroupPod> gpods;       // [staged + kMaxB]
   DevBuf<double> logw;          // [cap + 1] log(F + 2)
   DevBuf<uint64_t> gval;        // [cap] InterPodAffinity raw << 32 | spread count
@@ -3604,12 +3604,18 @@ int decode_group_pod(const kg_pod& p, GroupPod& d, int64_t k) {
     return 0;
   };
   const uint64_t all = kGroups >= 64 ? ~0ull : ((1ull << kGroups) - 1);
-  if (((uint64_t)p.match_groups | (uint64_t)p.pod_affinity_terms | (uint64_t)p.pod_anti_affinity) & ~all)
+  if (((uint64_t)p.match_groups | (uint64_t)p.pod_affinity_terms | (uint64_t)p.pod_anti_affinity |
+       (uint64_t)p.pod_affinity_terms_zone | (uint64_t)p.pod_anti_affinity_zone) & ~all)
     return fail(KG_E_INVALID, "pod %lld: a group bit beyond %d", (long long)k, kGroups);
   d.match = (uint32_t)p.match_groups;
   d.aff_terms = (uint32_t)p.pod_affinity_terms;
   d.anti = (uint32_t)p.pod_anti_affinity;
+  d.aff_terms_z = (uint32_t)p.pod_affinity_terms_zone;
+  d.anti_z = (uint32_t)p.pod_anti_affinity_zone;
   if (int rc = grp(p.pod_affinity_group, d.req, "pod affinity")) return rc;
+  if ((d.req >= 0) != ((d.aff_terms | d.aff_terms_z) != 0))
+    return fail(KG_E_INVALID, "pod %lld: required pod affinity needs both its conjunction group and its terms",
+                (long long)k);
   if (p.n_spread < 0 || p.n_spread > kSpread)
     return fail(KG_E_UNSUPPORTED, "pod %lld: more than %d topology spread constraints (the pod stays on the Go path)",
                 (long long)k, kSpread);
@@ -3644,6 +3650,9 @@ int decode_group_pod(const kg_pod& p, GroupPod& d, int64_t k) {
     d.pref_g[t] = g;
     d.pref_w[t] = (int32_t)w;
   }
+  if ((uint64_t)p.pod_preferred_zone >> d.npref)
+    return fail(KG_E_INVALID, "pod %lld: pod_preferred_zone bit beyond n_pod_preferred", (long long)k);
+  d.pref_zone = (uint32_t)p.pod_preferred_zone;
   return 0;
 }
 
@@ -4380,7 +4389,7 @@ int run_rsv(kg_engine* e, int64_t first, int64_t count, kg_stats* stats, double 
     const unsigned long long init[5] = {0, 0, 0, (unsigned long long)first, (unsigned long long)end};
     HIP_TRY(hipMemcpyAsync(e->rsv_ws.p, init, sizeof(init), hipMemcpyHostToDevice, e->stream));
     if (e->grp_on) {  // the zone sums start from zero (then each pod's rsv_select clears the next pod's)
-      HIP_TRY(hipMemsetAsync(e->gz.p, 0, (size_t)4 * kSpread * kZones * 4, e->stream));
+      HIP_TRY(hipMemsetAsync(e->gz.p, 0, (size_t)2 * kZoneSumWords * 4, e->stream));
       HIP_TRY(hipMemsetAsync(e->gzm.p, 0, 16, e->stream));
     }
     // `end_arg` < 0: the kernels read the call's end from the workspace (a graph stays valid across calls);
@@ -4862,14 +4871,14 @@ static int engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank,
                       (int32_t)(c.interpod_filter != 0), (int32_t)(c.interpod_score != 0), (int32_t)c.weight_interpod,
                       (int32_t)c.hard_pod_affinity_weight, 0};
   if (e->grp_on) {
-    if (int rc = e->grp_d.ensure((size_t)3 * kGroups * cap)) return bail(rc);
+    if (int rc = e->grp_d.ensure((size_t)kGroupArrays * kGroups * cap)) return bail(rc);
     if (int rc = e->logw.ensure(cap + 1)) return bail(rc);
     if (int rc = e->gval.ensure(cap)) return bail(rc);
-    if (int rc = e->gz.ensure((size_t)4 * kSpread * kZones)) return bail(rc);
+    if (int rc = e->gz.ensure((size_t)2 * kZoneSumWords)) return bail(rc);
     if (int rc = e->gzm.ensure(2)) return bail(rc);
     std::vector<double> lw((size_t)cap + 1);
     for (int64_t f = 0; f <= cap; ++f) lw[f] = std::log((double)(f + 2));  // TopologyNormalizingWeight
-    if (hipMemsetAsync(e->grp_d.p, 0, (size_t)3 * kGroups * cap * 4, e->stream) != hipSuccess ||
+    if (hipMemsetAsync(e->grp_d.p, 0, (size_t)kGroupArrays * kGroups * cap * 4, e->stream) != hipSuccess ||
         hipMemcpyAsync(e->logw.p, lw.data(), lw.size() * 8, hipMemcpyHostToDevice, e->stream) != hipSuccess ||
         hipStreamSynchronize(e->stream) != hipSuccess)
       return bail(fail(KG_E_DEVICE, "group tables"));
@@ -5247,6 +5256,7 @@ static int pods_delta(kg_engine* e, const kg_pod* pods, const int32_t* node_idx,
     std::vector<int32_t> hn((size_t)(2 * n));
     for (int64_t k = 0; k < n; ++k) {
       if (int rc = decode_group_pod(pods[k], hg[k], k)) return rc;
+      if (hg[k].aff_terms_z | hg[k].anti_z | hg[k].pref_zone) e->GP.ipa_zone = 1;  // sticky: zone channels on
       hn[k] = (int32_t)node_idx[k];
       hn[n + k] = sign;
     }
@@ -5408,8 +5418,10 @@ int kg_pods_stage(kg_engine* e, const kg_pod* pods, int64_t n) {
   }
   if (e->grp_on) {  // PodTopologySpread / InterPodAffinity view of the pods
     std::vector<GroupPod> hg(std::max<int64_t>(n, 1));
-    for (int64_t k = 0; k < n; ++k)
+    for (int64_t k = 0; k < n; ++k) {
       if (int rc = decode_group_pod(pods[k], hg[k], k)) return rc;
+      if (hg[k].aff_terms_z | hg[k].anti_z | hg[k].pref_zone) e->GP.ipa_zone = 1;  // sticky: zone channels on
+    }
     if (int rc = e->gpods.ensure(n + kMaxB)) return rc;
     if (n > 0) HIP_TRY(hipMemcpyAsync(e->gpods.p, hg.data(), n * sizeof(GroupPod), hipMemcpyHostToDevice, e->stream));
   }
@@ -6160,16 +6172,17 @@ int kg_nodes_read_reservations(kg_engine* e, int64_t* allocated_cpu, int64_t* al
   return 0;
 }
 
-int kg_nodes_read_pod_groups(kg_engine* e, int32_t* match_count, int32_t* anti_count, int32_t* sym_weight) {
+int kg_nodes_read_pod_groups(kg_engine* e, int32_t* match_count, int32_t* anti_count, int32_t* sym_weight,
+                             int32_t* anti_zone, int32_t* sym_zone) {
   if (!e) return fail(KG_E_INVALID, "engine is NULL");
   if (!e->grp_on) return fail(KG_E_INVALID, "the profile enables neither PodTopologySpread nor InterPodAffinity");
   const int64_t n = e->n_nodes, cap = e->capacity;
   if (n == 0) return 0;
-  std::vector<int32_t> h((size_t)3 * kGroups * cap);
+  std::vector<int32_t> h((size_t)kGroupArrays * kGroups * cap);
   HIP_TRY(hipMemcpyAsync(h.data(), e->grp_d.p, h.size() * 4, hipMemcpyDeviceToHost, e->stream));
   HIP_TRY(hipStreamSynchronize(e->stream));
-  int32_t* outs[3] = {match_count, anti_count, sym_weight};
-  for (int a = 0; a < 3; ++a)
+  int32_t* outs[kGroupArrays] = {match_count, anti_count, sym_weight, anti_zone, sym_zone};
+  for (int a = 0; a < kGroupArrays; ++a)
     if (outs[a])
       for (int64_t i = 0; i < n; ++i)
         for (int k = 0; k < kGroups; ++k) outs[a][i * kGroups + k] = h[((size_t)a * kGroups + k) * cap + i];

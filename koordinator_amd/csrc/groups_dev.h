@@ -31,19 +31,25 @@ constexpr int kGroups = KG_MAX_MATCH_GROUPS;
 constexpr int kPodPref = KG_MAX_POD_PREFERRED;
 constexpr int kSpread = KG_MAX_SPREAD;
 constexpr int kZones = KG_MAX_ZONES;
+constexpr int kGroupArrays = 5;
+constexpr int kIpaZoneCh = 4;  // InterPodAffinity zone channels (ZoneSums::zi)
 
-// per-node counters, structure of arrays [3][kGroups][cap] int32: pods matching group k, required anti-affinity
-// terms of group k on the node, Σ symmetric weights of the node's pods' terms of group k
+// per-node counters, structure of arrays [kGroupArrays][kGroups][cap] int32: pods matching group k, required
+// anti-affinity terms of group k on the node, Σ symmetric weights of the node's pods' terms of group k; the last two
+// again for the node's pods' zone-keyed terms
 struct GroupTable {
   int32_t* __restrict__ g;
   int64_t cap;
   __device__ __forceinline__ int32_t& cnt(int k, int64_t i) const { return g[(size_t)k * cap + i]; }
   __device__ __forceinline__ int32_t& anti(int k, int64_t i) const { return g[(size_t)(kGroups + k) * cap + i]; }
   __device__ __forceinline__ int32_t& symw(int k, int64_t i) const { return g[(size_t)(2 * kGroups + k) * cap + i]; }
+  __device__ __forceinline__ int32_t& anti_z(int k, int64_t i) const { return g[(size_t)(3 * kGroups + k) * cap + i]; }
+  __device__ __forceinline__ int32_t& symw_z(int k, int64_t i) const { return g[(size_t)(4 * kGroups + k) * cap + i]; }
 };
 
-struct GroupPod {  // 104 B per staged pod
-  uint32_t match, aff_terms, anti, pad;
+struct GroupPod {  // 112 B per staged pod
+  uint32_t match, aff_terms, anti, anti_z;  // hostname-keyed required terms; anti_z: zone-keyed anti-affinity terms
+  uint32_t aff_terms_z, pref_zone;          // zone-keyed required affinity terms; bit t: preferred term t zone-keyed
   int32_t req;              // conjunction group of the required pod-affinity terms (-1 none)
   int32_t npref;
   int32_t pref_g[kPodPref], pref_w[kPodPref];
@@ -62,7 +68,7 @@ struct GroupParams {
   int32_t spread_filter, spread_score, w_spread;
   int32_t ipa_filter, ipa_score, w_ipa;
   int32_t hard_w;
-  int32_t pad;
+  int32_t ipa_zone;  // some pod carries zone-keyed InterPodAffinity terms: group_pre builds the zone channels
 };
 
 // NodeInfo.AddPod / RemovePod (sign ±1) of a pod's group contributions on node i (atomics: the delta pass applies
@@ -72,9 +78,12 @@ __device__ __forceinline__ void group_apply(const GroupTable& G, int64_t i, cons
   for (int k = 0; k < kGroups; ++k) {
     if ((gp.match >> k) & 1u) atomicAdd(&G.cnt(k, i), sign);
     if ((gp.anti >> k) & 1u) atomicAdd(&G.anti(k, i), sign);
+    if ((gp.anti_z >> k) & 1u) atomicAdd(&G.anti_z(k, i), sign);
     if (hard_w > 0 && ((gp.aff_terms >> k) & 1u)) atomicAdd(&G.symw(k, i), sign * hard_w);
+    if (hard_w > 0 && ((gp.aff_terms_z >> k) & 1u)) atomicAdd(&G.symw_z(k, i), sign * hard_w);
   }
-  for (int t = 0; t < gp.npref; ++t) atomicAdd(&G.symw(gp.pref_g[t], i), sign * gp.pref_w[t]);
+  for (int t = 0; t < gp.npref; ++t)
+    atomicAdd((gp.pref_zone >> t) & 1u ? &G.symw_z(gp.pref_g[t], i) : &G.symw(gp.pref_g[t], i), sign * gp.pref_w[t]);
 }
 
 // PodMatchesNodeSelectorAndAffinityTerms: the pod's nodeSelector and required node affinity (the NodeAffinity Filter
@@ -92,12 +101,41 @@ __device__ __forceinline__ bool node_affinity_match(const NodePred* pred, const 
 
 // Zone sums of one pod (group_pre, double-buffered by the pod's parity): per constraint c, zf[c][z] = Σ over the nodes
 // passing the pod's node affinity with every DoNotSchedule key of the pods matching c's group in zone z, zs[c][z] the
-// same over the ScheduleAnyway node set; pres = the zones holding such a DoNotSchedule node
+// same over the ScheduleAnyway node set; pres = the zones holding such a DoNotSchedule node.  zi: InterPodAffinity's
+// topologyToMatchedTermCount maps for the zone key, summed over the valid nodes carrying a zone label:
+//   zi[0][z] pods matching the required affinity conjunction (affinityCounts),
+//   zi[1][z] pods matching one of the pod's zone-keyed anti-affinity groups (antiAffinityCounts, > 0 test only),
+//   zi[2][z] zone-keyed required anti-affinity terms of existing pods the pod matches (existingAntiAffinityCounts),
+//   zi[3][z] topologyScore: the pod's zone-keyed preferred terms × matching pods + existing pods' zone-keyed terms
+//            the pod matches
+constexpr int kZoneSumWords = (2 * kSpread + kIpaZoneCh) * kZones;
 struct ZoneSums {
   int32_t* __restrict__ zf;  // [kSpread][kZones]
   int32_t* __restrict__ zs;  // [kSpread][kZones]
+  int32_t* __restrict__ zi;  // [kIpaZoneCh][kZones]
   uint64_t* __restrict__ pres;
 };
+
+// node i's contribution to the zone channels (group_pre; the node is valid and carries a zone label)
+__device__ __forceinline__ void ipa_zone_terms(const GroupTable& G, int64_t i, const GroupPod& gp, int32_t c[kIpaZoneCh]) {
+  c[0] = gp.req >= 0 && gp.aff_terms_z ? G.cnt(gp.req, i) : 0;
+  c[1] = c[2] = c[3] = 0;
+  for (int t = 0; t < gp.npref; ++t)
+    if ((gp.pref_zone >> t) & 1u) c[3] += gp.pref_w[t] * G.cnt(gp.pref_g[t], i);
+  uint32_t a = gp.anti_z;
+  while (a) {
+    const int k = __builtin_ctz(a);
+    a &= a - 1;
+    c[1] += G.cnt(k, i);
+  }
+  uint32_t m = gp.match;
+  while (m) {
+    const int k = __builtin_ctz(m);
+    m &= m - 1;
+    c[2] += G.anti_z(k, i);
+    c[3] += G.symw_z(k, i);
+  }
+}
 
 // Filters of both plugins on node i (true = feasible).  min_match[c]: TpKeyToCriticalPaths' minimum per DoNotSchedule
 // constraint (hostname: over the eligible nodes' counts; zone: over the present zones' sums); total: the cluster-wide
@@ -121,20 +159,27 @@ __device__ __forceinline__ bool groups_filter(const GroupTable& G, int64_t i, co
     }
   }
   if (GP.ipa_filter) {
-    if (gp.req >= 0 && G.cnt(gp.req, i) <= 0 && !(total == 0 && ((gp.match >> gp.req) & 1u))) return false;
+    if (gp.req >= 0) {  // satisfyPodAffinity: every term's key on the node, then its pair's count
+      if (gp.aff_terms_z && zone <= 0) return false;
+      const bool exist = (!gp.aff_terms || G.cnt(gp.req, i) > 0) && (!gp.aff_terms_z || Z.zi[zone - 1] > 0);
+      if (!exist && !(total == 0 && ((gp.match >> gp.req) & 1u))) return false;
+    }
     for (int k = 0; k < kGroups; ++k) {
       if (((gp.anti >> k) & 1u) && G.cnt(k, i) > 0) return false;
       if (((gp.match >> k) & 1u) && G.anti(k, i) > 0) return false;
     }
+    if (GP.ipa_zone && zone > 0 && (Z.zi[kZones + zone - 1] > 0 || Z.zi[2 * kZones + zone - 1] > 0)) return false;
   }
   return true;
 }
 
 // InterPodAffinity raw Score on node i: the pod's preferred terms against the node's matching pods, plus the node's
 // pods' terms the pod matches
-__device__ __forceinline__ int32_t interpod_raw(const GroupTable& G, int64_t i, const GroupPod& gp) {
-  int32_t s = 0;
-  for (int t = 0; t < gp.npref; ++t) s += gp.pref_w[t] * G.cnt(gp.pref_g[t], i);
+__device__ __forceinline__ int32_t interpod_raw(const GroupTable& G, int64_t i, const GroupPod& gp, int32_t zone,
+                                              const ZoneSums& Z) {
+  int32_t s = zone > 0 ? Z.zi[3 * kZones + zone - 1] : 0;  // the zone key's topologyScore
+  for (int t = 0; t < gp.npref; ++t)
+    if (!((gp.pref_zone >> t) & 1u)) s += gp.pref_w[t] * G.cnt(gp.pref_g[t], i);
   uint32_t m = gp.match;
   while (m) {
     const int k = __builtin_ctz(m);

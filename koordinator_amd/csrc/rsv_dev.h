@@ -88,13 +88,13 @@ struct RsvExt {
   GroupParams GP;
   const double* __restrict__ logw;     // [cap + 1]: log(F + 2), the host's libm
   uint64_t* __restrict__ gval;         // [cap] InterPodAffinity raw << 32 | PodTopologySpread raw (+ 2^31; 0 = ignored)
-  int32_t* __restrict__ gz;            // [2 parities][2][kSpread][kZones] the zone sums (ZoneSums)
+  int32_t* __restrict__ gz;            // [2 parities][kZoneSumWords] the zone sums (ZoneSums)
   uint64_t* __restrict__ gzm;          // [2 parities] the present zones
 };
 // pod j's zone sums (double-buffered by parity: group_pre(j) accumulates, rsv_select(j) clears j + 1's)
 __device__ __forceinline__ ZoneSums zone_sums(const RsvExt& X, int64_t j) {
-  int32_t* b = X.gz + (size_t)(j & 1) * 2 * kSpread * kZones;
-  return ZoneSums{b, b + kSpread * kZones, X.gzm + (j & 1)};
+  int32_t* b = X.gz + (size_t)(j & 1) * kZoneSumWords;
+  return ZoneSums{b, b + kSpread * kZones, b + 2 * kSpread * kZones, X.gzm + (j & 1)};
 }
 
 struct RsvOut {
@@ -589,7 +589,7 @@ __global__ __launch_bounds__(kRsvThreads) void rsv_eval(DevTable T, RsvNode* __r
       o.feas = groups_filter(X.G, i, gp, X.GP, node_affinity_match(X.pred, df, i), zone, s_min, Z, pres, total);
       if (o.feas) {
         ign = !spread_has_keys(gp, 1, zone);
-        iraw = interpod_raw(X.G, i, gp);
+        iraw = interpod_raw(X.G, i, gp, zone, Z);
       }
     }
     if (o.feas) {
@@ -761,7 +761,7 @@ __global__ __launch_bounds__(kRsvThreads) void rsv_select(const uint64_t* __rest
   // pod j + 1's zone sums start from zero (pod j - 1 was their last reader)
   if (blockIdx.x == 0) {
     const ZoneSums Zn = zone_sums(X, j + 1);
-    for (int k = threadIdx.x; k < 2 * kSpread * kZones; k += kRsvThreads) Zn.zf[k] = 0;
+    for (int k = threadIdx.x; k < kZoneSumWords; k += kRsvThreads) Zn.zf[k] = 0;
     if (threadIdx.x == 0) *Zn.pres = 0;
   }
 }
@@ -784,7 +784,8 @@ __global__ __launch_bounds__(kRsvThreads) void rsv_select2(const uint64_t* __res
 // groups: the thread owning the winner row), then the reductions pod j's Filters need over the snapshot after it:
 // part[6 nb + b] = min over the block's valid nodes passing the pod's nodeSelector / required node affinity of the
 // DoNotSchedule constraint's count (enc_min_i32; 0 = none: MaxInt32), part[7 nb + b] = Σ over valid nodes of pods
-// matching the required pod-affinity group.
+// matching the required pod-affinity group (only those carrying a zone label when every required term is zone-keyed:
+// affinityCounts then has no hostname pairs); the zone sums (ZoneSums) with one atomic per block and nonzero word.
 __global__ __launch_bounds__(kRsvThreads) void group_pre(DevTable T, RsvNode* __restrict__ RN,
                                                          const DevPod* __restrict__ pods, int64_t end, int64_t n,
                                                          int g, RsvExt X, const uint64_t* __restrict__ val,
@@ -815,11 +816,11 @@ __global__ __launch_bounds__(kRsvThreads) void group_pre(DevTable T, RsvNode* __
   }
   const GroupPod gp = X.gpods[j];
   const ZoneSums Z = zone_sums(X, j);
-  __shared__ int32_t s_zs[2][kSpread][kZones];  // the block's zone sums (hard, soft), flushed with one atomic each
+  __shared__ int32_t s_zs[kZoneSumWords];  // the block's zone sums, flushed with one atomic each
   __shared__ unsigned long long s_pres;
-  const bool zoned = gp.zone_keys != 0;
+  const bool zoned = gp.zone_keys != 0 || X.GP.ipa_zone;
   if (zoned) {
-    for (int k = threadIdx.x; k < 2 * kSpread * kZones; k += kRsvThreads) (&s_zs[0][0][0])[k] = 0;
+    for (int k = threadIdx.x; k < kZoneSumWords; k += kRsvThreads) s_zs[k] = 0;
     if (threadIdx.x == 0) s_pres = 0;
     __syncthreads();
   }
@@ -835,14 +836,22 @@ __global__ __launch_bounds__(kRsvThreads) void group_pre(DevTable T, RsvNode* __
         if (!(hard ? ef : es)) continue;
         const int32_t v = X.G.cnt(gp.sp_g[c], i);
         if (z) {
-          if (v) atomicAdd(&s_zs[hard ? 0 : 1][c][zone - 1], v);
+          if (v) atomicAdd(&s_zs[((hard ? 0 : kSpread) + c) * kZones + zone - 1], v);
           if (hard) atomicOr(&s_pres, 1ull << (zone - 1));
         } else if (hard) {
           mn = enc_min_i32(v);
         }
       }
     }
-    if (X.GP.ipa_filter && gp.req >= 0) sm = (uint32_t)X.G.cnt(gp.req, i);
+    const int32_t zone = X.pred[i].zone;
+    if (X.GP.ipa_filter && gp.req >= 0 && (gp.aff_terms || zone > 0)) sm = (uint32_t)X.G.cnt(gp.req, i);
+    if (X.GP.ipa_zone && zone > 0) {
+      int32_t c[kIpaZoneCh];
+      ipa_zone_terms(X.G, i, gp, c);
+#pragma unroll
+      for (int h = 0; h < kIpaZoneCh; ++h)
+        if (c[h]) atomicAdd(&s_zs[(2 * kSpread + h) * kZones + zone - 1], c[h]);
+    }
   }
   mn = rsv_block_max(mn, s_red);
   __syncthreads();
@@ -853,9 +862,9 @@ __global__ __launch_bounds__(kRsvThreads) void group_pre(DevTable T, RsvNode* __
   }
   if (zoned) {
     __syncthreads();
-    for (int k = threadIdx.x; k < 2 * kSpread * kZones; k += kRsvThreads) {
-      const int32_t v = (&s_zs[0][0][0])[k];
-      if (v) atomicAdd(&Z.zf[k], v);  // zf and zs are contiguous: [2][kSpread][kZones]
+    for (int k = threadIdx.x; k < kZoneSumWords; k += kRsvThreads) {
+      const int32_t v = s_zs[k];
+      if (v) atomicAdd(&Z.zf[k], v);  // zf, zs and zi are contiguous
     }
     if (threadIdx.x == 0 && s_pres) atomicOr((unsigned long long*)Z.pres, s_pres);
   }

@@ -193,13 +193,14 @@ class Engine:
         check(self.lib, self.lib.kg_nodes_read_reservations(self.h, *[ptr(o) for o in out]))
         return tuple(out)
 
-    def read_pod_groups(self):
-        """(ABI 12) per node and match group: (pods matching, required anti-affinity terms, symmetric weight),
-        int32[n, KG_MAX_MATCH_GROUPS] each, from the device (kg_nodes_read_pod_groups)."""
+    def read_pod_groups(self, zone: bool = False):
+        """(ABI 12) per node and match group: (pods matching, required anti-affinity terms, symmetric weight) — and,
+        with zone, the zone-keyed terms' (anti-affinity, symmetric weight) — int32[n, KG_MAX_MATCH_GROUPS] each, from
+        the device (kg_nodes_read_pod_groups)."""
         n = self.num_nodes
-        out = [np.zeros((n, abi.MAX_MATCH_GROUPS), dtype=np.int32) for _ in range(3)]
+        out = [np.zeros((n, abi.MAX_MATCH_GROUPS), dtype=np.int32) for _ in range(5)]
         check(self.lib, self.lib.kg_nodes_read_pod_groups(self.h, *[ptr(o) for o in out]))
-        return tuple(out)
+        return tuple(out[:3]) if not zone else tuple(out)
 
     def fetch_reservations(self, first: int, count: int) -> np.ndarray:
         """int32[count]: the reservation slot Reserve assumed each staged pod into (-1 = none)."""

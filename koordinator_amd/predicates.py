@@ -303,8 +303,8 @@ class PodGroupTable:
     or the conjunction of a pod's required pod-affinity terms (updateWithAffinityTerms counts a pod only when it matches
     all of them).  Register every group the cluster's pods and the queue use before filling pod rows: a row's
     match_groups covers the groups registered when it was filled.  Accelerated topology keys: kubernetes.io/hostname
-    for both plugins, topology.kubernetes.io/zone for PodTopologySpread (the node's zone comes from
-    PredicateTable.node_row); another key raises NotImplementedError: the pod stays on the Go path."""
+    and topology.kubernetes.io/zone for both plugins (the node's zone comes from PredicateTable.node_row); another
+    key raises NotImplementedError: the pod stays on the Go path."""
 
     def __init__(self):
         self.groups: list[tuple] = []  # (kind, payload): ("sel", (selector_repr, namespaces)) / ("and", (gid, ...))
@@ -337,17 +337,23 @@ class PodGroupTable:
     def match_mask(self, labels: dict, namespace: str) -> int:
         return sum(1 << (g - 1) for g in range(1, len(self.groups) + 1) if self.matches(g, labels, namespace))
 
-    def _term(self, t: dict, namespace: str) -> int:
-        if t.get("topologyKey", HOSTNAME) != HOSTNAME:
-            raise NotImplementedError("pod affinity topologyKey other than kubernetes.io/hostname")
-        return self.group(t.get("labelSelector"), t.get("namespaces") or (namespace,))
+    def _term(self, t: dict, namespace: str) -> tuple[int, bool]:
+        """(group id, zone-keyed) of one pod (anti-)affinity term."""
+        key = t.get("topologyKey", HOSTNAME)
+        if key not in (HOSTNAME, ZONE):
+            raise NotImplementedError(f"pod affinity topologyKey {key}: hostname and zone are accelerated")
+        return self.group(t.get("labelSelector"), t.get("namespaces") or (namespace,)), key == ZONE
+
+    @staticmethod
+    def _mask(terms, zone: bool) -> int:
+        return sum(1 << (g - 1) for g in {g for g, z in terms if z == zone})
 
     def fill_pod(self, pod: np.ndarray, labels: dict, namespace: str, spread=(), required_affinity=(),
                  required_anti_affinity=(), preferred_affinity=(), preferred_anti_affinity=()) -> np.ndarray:
         """The ABI 12 fields of one pod.  spread: [{maxSkew, whenUnsatisfiable, labelSelector, topologyKey}] with
         topologyKey kubernetes.io/hostname (default) or topology.kubernetes.io/zone (a pod without constraints may pass
         the system defaults, hostname maxSkew 3 + zone maxSkew 5 ScheduleAnyway, with its owners' selector);
-        required_*: [{labelSelector, namespaces, topologyKey}] (hostname only); preferred_*: [{weight,
+        required_*: [{labelSelector, namespaces, topologyKey}] (hostname or zone); preferred_*: [{weight,
         podAffinityTerm}]."""
         r = pod[0] if pod.ndim else pod
         if len(spread) > abi.MAX_SPREAD:
@@ -366,15 +372,19 @@ class PodGroupTable:
             r["spread_max_skew"][c] = cons["maxSkew"]
             r["spread_flags"][c] = (abi.SPREAD_HARD if hard else 0) | (abi.SPREAD_ZONE if key == ZONE else 0)
         terms = [self._term(t, namespace) for t in required_affinity]
-        r["pod_affinity_terms"] = sum(1 << (g - 1) for g in set(terms))
-        r["pod_affinity_group"] = self.conjunction(terms) if terms else 0
-        r["pod_anti_affinity"] = sum(1 << (self._term(t, namespace) - 1) for t in required_anti_affinity)
+        r["pod_affinity_terms"] = self._mask(terms, False)
+        r["pod_affinity_terms_zone"] = self._mask(terms, True)
+        r["pod_affinity_group"] = self.conjunction([g for g, _ in terms]) if terms else 0
+        anti = [self._term(t, namespace) for t in required_anti_affinity]
+        r["pod_anti_affinity"] = self._mask(anti, False)
+        r["pod_anti_affinity_zone"] = self._mask(anti, True)
         pref = [(self._term(t["podAffinityTerm"], namespace), t["weight"]) for t in preferred_affinity]
         pref += [(self._term(t["podAffinityTerm"], namespace), -t["weight"]) for t in preferred_anti_affinity]
         if len(pref) > abi.MAX_POD_PREFERRED:
             raise NotImplementedError(f"more than {abi.MAX_POD_PREFERRED} preferred pod affinity terms")
         r["n_pod_preferred"] = len(pref)
-        for t, (g, w) in enumerate(pref):
+        r["pod_preferred_zone"] = sum(1 << t for t, ((_, z), _) in enumerate(pref) if z)
+        for t, ((g, _), w) in enumerate(pref):
             r["pod_preferred_group"][t], r["pod_preferred_weight"][t] = g, w
         r["match_groups"] = self.match_mask(labels, namespace)
         return pod

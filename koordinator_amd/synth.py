@@ -585,14 +585,18 @@ def make_images(n_nodes: int, pods: np.ndarray, preds: np.ndarray, seed: int = B
 
 
 # ---- (ABI 12) PodTopologySpread / InterPodAffinity (hostname key) ------------------------------------------------
-def make_pod_groups(pods: np.ndarray, seed: int = BASE_SEED + 17, n_apps: int = 8, zones: bool = False) -> np.ndarray:
+def make_pod_groups(pods: np.ndarray, seed: int = BASE_SEED + 17, n_apps: int = 8, zones: bool = False,
+                    ipa_zones: bool | None = None) -> np.ndarray:
     """Fills the ABI 12 group fields of `pods` in place, as PodGroupTable would compile them for a workload of n_apps
     deployments (groups 1..n_apps: app=k in the namespace) in n_apps / 2 teams (groups n_apps+1..: team=t): every pod
     matches its app and team; 40 % carry a DoNotSchedule hostname spread constraint on their app (maxSkew 1-3), 50 % a
     ScheduleAnyway one (maxSkew 1-5), with `zones` also 15 % a DoNotSchedule zone one (maxSkew 1-39) and 40 % a
     ScheduleAnyway zone one (maxSkew 1-7), in a random order; 15 % a required anti-affinity to their own app (one per
     node), 10 % a required
-    affinity to another team, 30 % one or two preferred (anti-)affinity terms (weights ±1..100)."""
+    affinity to another team, 30 % one or two preferred (anti-)affinity terms (weights ±1..100).  ipa_zones (default:
+    `zones`) re-keys InterPodAffinity terms to topology.kubernetes.io/zone: a third of the required anti-affinity pods
+    (one per zone, or a node without the label), half of the required affinity pods (a fifth of them with both keys),
+    half of the preferred terms."""
     rng = np.random.default_rng(seed)
     n = len(pods)
     n_teams = n_apps // 2
@@ -637,4 +641,14 @@ def make_pod_groups(pods: np.ndarray, seed: int = BASE_SEED + 17, n_apps: int = 
         w = rng.integers(1, 101, n) * np.where(rng.random(n) < 0.4, -1, 1)
         pods["pod_preferred_group"][:, t] = np.where(on, g, 0)
         pods["pod_preferred_weight"][:, t] = np.where(on, w, 0)
+    if zones if ipa_zones is None else ipa_zones:
+        za = anti & (rng.random(n) < 1 / 3)
+        pods["pod_anti_affinity_zone"] = np.where(za, pods["pod_anti_affinity"], 0)
+        pods["pod_anti_affinity"] = np.where(za, 0, pods["pod_anti_affinity"])
+        kind = rng.random(n)  # < 0.4: zone only, < 0.5: both keys
+        terms = pods["pod_affinity_terms"].copy()
+        pods["pod_affinity_terms_zone"] = np.where(aff & (kind < 0.5), terms, 0)
+        pods["pod_affinity_terms"] = np.where(aff & (kind < 0.4), 0, terms)
+        pz = (rng.random((n, 2)) < 0.5) & (npref[:, None] > np.arange(2))
+        pods["pod_preferred_zone"] = pz[:, 0] * 1 + pz[:, 1] * 2
     return pods

@@ -2,6 +2,7 @@
 #include "defaults.h"
 
 #include <math.h>
+#include <string.h>
 
 /* taint_toleration.go Filter: v1helper.FindMatchingUntoleratedTaint(node.Spec.Taints, pod.Spec.Tolerations,
  * effect ∈ {NoSchedule, NoExecute}); a taint id carries its effect, so "tolerated" is per id. */
@@ -90,7 +91,7 @@ int64_t or_normalize_default(int64_t score, int64_t max_count, int reverse) {
   return reverse ? 100 - s : s;
 }
 
-/* ---- (ABI 12) PodTopologySpread / InterPodAffinity, topologyKey kubernetes.io/hostname ---------------------------- */
+/* ---- (ABI 12) PodTopologySpread / InterPodAffinity, topologyKey kubernetes.io/hostname or zone -------------------- */
 
 /* The counters a pod contributes to its node: countPodsMatchSelector (podtopologyspread/common.go, and the
  * interpodaffinity PreFilter / PreScore matches of existing pods against the incoming pod's terms) counts it in every
@@ -101,12 +102,39 @@ void or_groups_apply(or_group_node* g, const kg_pod* pod, int sign, int64_t hard
   for (int k = 0; k < KG_MAX_MATCH_GROUPS; k++) {
     if ((pod->match_groups >> k) & 1) g->cnt[k] += sign;
     if ((pod->pod_anti_affinity >> k) & 1) g->anti[k] += sign;
+    if ((pod->pod_anti_affinity_zone >> k) & 1) g->anti_z[k] += sign;
     if (hard_weight > 0 && ((pod->pod_affinity_terms >> k) & 1)) g->symw[k] += sign * (int32_t)hard_weight;
+    if (hard_weight > 0 && ((pod->pod_affinity_terms_zone >> k) & 1)) g->symw_z[k] += sign * (int32_t)hard_weight;
   }
   for (int64_t t = 0; t < pod->n_pod_preferred; t++) {
     const int64_t k = pod->pod_preferred_group[t] - 1;
-    if (k >= 0 && k < KG_MAX_MATCH_GROUPS) g->symw[k] += sign * (int32_t)pod->pod_preferred_weight[t];
+    if (k < 0 || k >= KG_MAX_MATCH_GROUPS) continue;
+    int32_t* w = ((pod->pod_preferred_zone >> t) & 1) ? &g->symw_z[k] : &g->symw[k];
+    *w += sign * (int32_t)pod->pod_preferred_weight[t];
   }
+}
+
+/* filtering.go getTPMapMatchingIncomingAffinityAntiAffinity / getExistingAntiAffinityCounts and scoring.go PreScore,
+ * zone key: every existing pod on a node with the zone label adds its matches to the node's zone pair; a required
+ * affinity match needs all the pod's terms (updateWithAffinityTerms); hostname terms make a pair on every node. */
+void or_ipa_zones_add(or_ipa_zones* z, const or_group_node* g, int32_t zone, const kg_pod* pod) {
+  const int64_t a = pod->pod_affinity_group - 1;
+  if (a >= 0 && pod->pod_affinity_terms && g->cnt[a] > 0) z->entries = 1;  /* a hostname pair */
+  if (zone <= 0) return;
+  if (a >= 0 && pod->pod_affinity_terms_zone) {
+    z->aff[zone - 1] += g->cnt[a];
+    if (z->aff[zone - 1] > 0) z->entries = 1;
+  }
+  for (int k = 0; k < KG_MAX_MATCH_GROUPS; k++) {
+    if ((pod->pod_anti_affinity_zone >> k) & 1) z->anti_in[zone - 1] += g->cnt[k];
+    if ((pod->match_groups >> k) & 1) {
+      z->anti_ex[zone - 1] += g->anti_z[k];
+      z->score[zone - 1] += g->symw_z[k];
+    }
+  }
+  for (int64_t t = 0; t < pod->n_pod_preferred; t++)
+    if ((pod->pod_preferred_zone >> t) & 1)
+      z->score[zone - 1] += pod->pod_preferred_weight[t] * (int64_t)g->cnt[pod->pod_preferred_group[t] - 1];
 }
 
 static int spread_needs_zone(const kg_pod* pod, int hard) {
@@ -140,23 +168,29 @@ int64_t or_spread_normalize(int64_t raw, int64_t mn, int64_t mx) {
   return 100 * (mx + mn - raw) / mx;
 }
 
-int or_interpod_filter(const or_group_node* g, const kg_pod* pod, const int64_t* total) {
+int or_interpod_filter(const or_group_node* g, const kg_pod* pod, int32_t zone, const or_ipa_zones* z) {
   const int64_t a = pod->pod_affinity_group - 1;
-  if (a >= 0 && g->cnt[a] <= 0) {  /* satisfyPodAffinity */
-    if (!(total[a] == 0 && ((pod->match_groups >> a) & 1))) return 0;
+  if (a >= 0) {  /* satisfyPodAffinity: every term's topology key on the node, then each term's pair count */
+    if (pod->pod_affinity_terms_zone && zone <= 0) return 0;
+    int exist = 1;
+    if (pod->pod_affinity_terms && g->cnt[a] <= 0) exist = 0;
+    if (pod->pod_affinity_terms_zone && z->aff[zone - 1] <= 0) exist = 0;
+    if (!exist && !(!z->entries && ((pod->match_groups >> a) & 1))) return 0;
   }
   for (int k = 0; k < KG_MAX_MATCH_GROUPS; k++) {
     if (((pod->pod_anti_affinity >> k) & 1) && g->cnt[k] > 0) return 0;  /* satisfyPodAntiAffinity */
     if (((pod->match_groups >> k) & 1) && g->anti[k] > 0) return 0;      /* satisfyExistingPodsAntiAffinity */
   }
+  if (zone > 0 && (z->anti_in[zone - 1] > 0 || z->anti_ex[zone - 1] > 0)) return 0;  /* the zone pairs */
   return 1;
 }
 
-int64_t or_interpod_raw(const or_group_node* g, const kg_pod* pod) {
-  int64_t s = 0;
+int64_t or_interpod_raw(const or_group_node* g, const kg_pod* pod, int32_t zone, const or_ipa_zones* z) {
+  int64_t s = zone > 0 ? z->score[zone - 1] : 0;
   for (int64_t t = 0; t < pod->n_pod_preferred; t++) {
     const int64_t k = pod->pod_preferred_group[t] - 1;
-    if (k >= 0 && k < KG_MAX_MATCH_GROUPS) s += pod->pod_preferred_weight[t] * (int64_t)g->cnt[k];
+    if (k >= 0 && k < KG_MAX_MATCH_GROUPS && !((pod->pod_preferred_zone >> t) & 1))
+      s += pod->pod_preferred_weight[t] * (int64_t)g->cnt[k];
   }
   for (int k = 0; k < KG_MAX_MATCH_GROUPS; k++)
     if ((pod->match_groups >> k) & 1) s += g->symw[k];

@@ -40,15 +40,29 @@ int64_t or_balanced_score(int64_t alloc_cpu, int64_t alloc_mem, int64_t req_cpu,
 /* DefaultNormalizeScore(MaxNodeScore, reverse) of one score against the maximum over the scored nodes. */
 int64_t or_normalize_default(int64_t score, int64_t max_count, int reverse);
 
-/* (ABI 12) PodTopologySpread / InterPodAffinity with topologyKey kubernetes.io/hostname (k8s v1.24.15
- * podtopologyspread/{common,filtering,scoring}.go, interpodaffinity/{filtering,scoring}.go; not vendored, restated as
- * published — "parity unpinned" beyond tests/test_pod_groups.py's hand-derived cases).  Each node is its own
- * topology domain, so the plugins' per-domain maps become per-node counters over the caller's match groups. */
+/* (ABI 12) PodTopologySpread / InterPodAffinity with topologyKey kubernetes.io/hostname or topology.kubernetes.io/zone
+ * (k8s v1.24.15 podtopologyspread/{common,filtering,scoring}.go, interpodaffinity/{filtering,scoring}.go; not
+ * vendored, restated as published — "parity unpinned" beyond tests/test_pod_groups.py's hand-derived cases).  With
+ * the hostname key each node is its own topology domain, so the plugins' per-domain maps become per-node counters
+ * over the caller's match groups; zone-keyed maps are sums of those counters over a zone's nodes. */
 typedef struct or_group_node {
-  int32_t cnt[KG_MAX_MATCH_GROUPS];   /* pods on the node matching group k (countPodsMatchSelector)        */
-  int32_t anti[KG_MAX_MATCH_GROUPS];  /* required anti-affinity terms of group k held by the node's pods   */
-  int32_t symw[KG_MAX_MATCH_GROUPS];  /* Σ symmetric weights of the node's pods' terms of group k          */
+  int32_t cnt[KG_MAX_MATCH_GROUPS];     /* pods on the node matching group k (countPodsMatchSelector)        */
+  int32_t anti[KG_MAX_MATCH_GROUPS];    /* required anti-affinity terms of group k held by the node's pods   */
+  int32_t symw[KG_MAX_MATCH_GROUPS];    /* Σ symmetric weights of the node's pods' terms of group k          */
+  int32_t anti_z[KG_MAX_MATCH_GROUPS];  /* the same two for the node's pods' zone-keyed terms               */
+  int32_t symw_z[KG_MAX_MATCH_GROUPS];
 } or_group_node;
+/* InterPodAffinity's zone-keyed topologyToMatchedTermCount maps of one incoming pod (interpodaffinity PreFilter /
+ * PreScore over every node carrying the zone label), indexed by zone − 1; entries = len(affinityCounts) ≠ 0. */
+typedef struct or_ipa_zones {
+  int64_t aff[KG_MAX_ZONES];      /* affinityCounts[zone]: pods matching every required affinity term          */
+  int64_t anti_in[KG_MAX_ZONES];  /* antiAffinityCounts[zone] of the pod's zone-keyed required anti terms      */
+  int64_t anti_ex[KG_MAX_ZONES];  /* existingAntiAffinityCounts[zone]: existing pods' zone anti terms vs pod   */
+  int64_t score[KG_MAX_ZONES];    /* topologyScore[zone]                                                       */
+  int64_t entries;                /* affinityCounts has a pair (hostname or zone)                              */
+} or_ipa_zones;
+/* Adds one valid node's counters (zone = 1 + zone id, 0 = no zone label) to `pod`'s maps (zeroed by the caller). */
+void or_ipa_zones_add(or_ipa_zones* z, const or_group_node* g, int32_t zone, const kg_pod* pod);
 /* NodeInfo.AddPod / RemovePod of `pod` (sign ±1) on one node's counters. */
 void or_groups_apply(or_group_node* g, const kg_pod* pod, int sign, int64_t hard_weight);
 /* PodTopologySpread constraints' node requirements (common.go nodeLabelsMatchSpreadConstraints + the PreFilter /
@@ -65,9 +79,9 @@ int64_t or_spread_normalize(int64_t raw, int64_t mn, int64_t mx);
 /* InterPodAffinity Filter (filtering.go Filter): required affinity (the conjunction group, or the first pod of a
  * series: no pod in the cluster matches and the pod matches its own terms), required anti-affinity, existing pods'
  * anti-affinity; 1 = pass.  total[k] = pods in the cluster matching group k. */
-int or_interpod_filter(const or_group_node* g, const kg_pod* pod, const int64_t* total);
-/* InterPodAffinity Score (scoring.go processExistingPod summed per node) before normalisation. */
-int64_t or_interpod_raw(const or_group_node* g, const kg_pod* pod);
+int or_interpod_filter(const or_group_node* g, const kg_pod* pod, int32_t zone, const or_ipa_zones* z);
+/* InterPodAffinity Score (scoring.go Score: the node's hostname pair plus its zone pair) before normalisation. */
+int64_t or_interpod_raw(const or_group_node* g, const kg_pod* pod, int32_t zone, const or_ipa_zones* z);
 /* InterPodAffinity NormalizeScore: int64(MaxNodeScore · float64(s − min) / float64(max − min)), 0 when max == min. */
 int64_t or_interpod_normalize(int64_t raw, int64_t mn, int64_t mx);
 

@@ -109,9 +109,11 @@ def lib():
         L.or_spread_raw.restype = i64
         L.or_spread_normalize.argtypes = [i64, i64, i64]
         L.or_spread_normalize.restype = i64
-        L.or_interpod_filter.argtypes = [vp, vp, vp]
+        L.or_ipa_zones_add.argtypes = [vp, vp, ctypes.c_int32, vp]
+        L.or_ipa_zones_add.restype = None
+        L.or_interpod_filter.argtypes = [vp, vp, ctypes.c_int32, vp]
         L.or_interpod_filter.restype = i
-        L.or_interpod_raw.argtypes = [vp, vp]
+        L.or_interpod_raw.argtypes = [vp, vp, ctypes.c_int32, vp]
         L.or_interpod_raw.restype = i64
         L.or_interpod_normalize.argtypes = [i64, i64, i64]
         L.or_interpod_normalize.restype = i64
@@ -208,8 +210,10 @@ p = abi.ptr
 
 
 # (ABI 12) or_group_node: per node and match group, pods matching / required anti-affinity terms / symmetric weights
-GROUP_DTYPE = np.dtype([("cnt", np.int32, (abi.MAX_MATCH_GROUPS,)), ("anti", np.int32, (abi.MAX_MATCH_GROUPS,)),
-                        ("symw", np.int32, (abi.MAX_MATCH_GROUPS,))])
+GROUP_DTYPE = np.dtype([(f, np.int32, (abi.MAX_MATCH_GROUPS,)) for f in ("cnt", "anti", "symw", "anti_z", "symw_z")])
+# or_ipa_zones: one incoming pod's zone-keyed InterPodAffinity maps (defaults.h)
+IPA_ZONES_DTYPE = np.dtype([(f, np.int64, (abi.MAX_ZONES,)) for f in ("aff", "anti_in", "anti_ex", "score")]
+                           + [("entries", np.int64)])
 
 
 def groups_init(n_nodes: int, pods=None, node_idx=None, hard_weight: int = 1) -> np.ndarray:

@@ -291,17 +291,19 @@ int or_schedule_resv_full(const kg_config* cfg, int64_t n_nodes, const kg_node* 
     /* PodTopologySpread PreFilter (common.go calPreFilterState) over the nodes passing the pod's nodeSelector /
      * required node affinity and carrying every DoNotSchedule key: per constraint, TpPairToMatchNum — each such node's
      * own count (hostname) or its zone's sum (zone) — and the minimum over those pairs (MaxInt32 when none);
-     * InterPodAffinity PreFilter: the cluster-wide count of pods matching each group (len(affinityCounts) == 0 ⇔ no pod
-     * matches the required terms) */
-    int64_t min_match[KG_MAX_SPREAD], zsum_f[KG_MAX_SPREAD][KG_MAX_ZONES], total[KG_MAX_MATCH_GROUPS] = {0};
+     * InterPodAffinity PreFilter / PreScore: the pod's topology-pair maps (or_ipa_zones: the zone pairs and whether
+     * affinityCounts has any pair) */
+    int64_t min_match[KG_MAX_SPREAD], zsum_f[KG_MAX_SPREAD][KG_MAX_ZONES];
     uint64_t zpres_f[KG_MAX_SPREAD] = {0};
+    or_ipa_zones ipz;
+    memset(&ipz, 0, sizeof(ipz));
     memset(zsum_f, 0, sizeof(zsum_f));
     for (int c = 0; c < KG_MAX_SPREAD; c++) min_match[c] = INT32_MAX;
-    if (spread_on || (ipa_on && cfg->interpod_filter)) {
+    if (spread_on || ipa_on) {
       for (int64_t i = 0; i < n_nodes; i++) {
         if (!(nodes[i].flags & KG_NODE_VALID)) continue;
-        for (int k = 0; k < KG_MAX_MATCH_GROUPS; k++) total[k] += grp[i].cnt[k];
         const kg_node_predicates* np = preds ? &preds[i] : &zero_pred;
+        if (ipa_on) or_ipa_zones_add(&ipz, &grp[i], np->zone, pod);
         if (!spread_on || !or_spread_node_ok(np, pod, 1)) continue;
         for (int64_t c = 0; c < pod->n_spread; c++) {
           if (!(pod->spread_flags[c] & KG_SPREAD_HARD)) continue;
@@ -371,9 +373,9 @@ int or_schedule_resv_full(const kg_config* cfg, int64_t n_nodes, const kg_node* 
         }
         if (!ok) continue;
       }
-      if (ipa_on && cfg->interpod_filter && !or_interpod_filter(&grp[i], pod, total)) continue;
+      if (ipa_on && cfg->interpod_filter && !or_interpod_filter(&grp[i], pod, np->zone, &ipz)) continue;
       feas[i] = 1;
-      iraw[i] = ipa_on ? or_interpod_raw(&grp[i], pod) : 0;
+      iraw[i] = ipa_on ? or_interpod_raw(&grp[i], pod, np->zone, &ipz) : 0;
       int64_t t = 0;
       if (cfg->fit_score) t += cfg->weight_fit * or_fit_score(cfg, nd, &rs, pod);
       if (cfg->la_score) {

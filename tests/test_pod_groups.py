@@ -1,4 +1,5 @@
-"""(ABI 12) PodTopologySpread and InterPodAffinity with topologyKey kubernetes.io/hostname on the exact per-pod pass.
+"""(ABI 12) PodTopologySpread and InterPodAffinity with topologyKey kubernetes.io/hostname or topology.kubernetes.io/zone
+on the exact per-pod pass.
 
 The reference runs both from k8s.io/kubernetes v1.24.15 (not vendored): the oracle restates the published plugins
 (oracle/defaults.c) and is pinned by hand-derived cases below ("parity unpinned" against the reference beyond them;
@@ -84,27 +85,76 @@ def test_spread_node_keys():
     assert L.or_spread_has_keys(oracle.p(bare), oracle.p(pod), 0) == 1  # the ScheduleAnyway one is hostname-keyed
 
 
+def _zones(**kw):
+    z = np.zeros(1, dtype=oracle.IPA_ZONES_DTYPE)
+    for k, v in kw.items():
+        if k == "entries":
+            z[k] = v
+        else:
+            z[k][0, :len(v)] = v
+    return z
+
+
 def test_interpod_filter_cases():
     L = oracle.lib()
-    tot = np.zeros(abi.MAX_MATCH_GROUPS, dtype=np.int64)
+    none = _zones()
+    f = lambda g, pod, zone=0, z=none: L.or_interpod_filter(oracle.p(g), oracle.p(pod), zone, oracle.p(z))
     # required anti-affinity to group 0: a node holding a matching pod rejects
     anti = _gpod(pod_anti_affinity=1)
-    assert L.or_interpod_filter(oracle.p(_grp(cnt=[1])), oracle.p(anti), oracle.p(tot)) == 0
-    assert L.or_interpod_filter(oracle.p(_grp(cnt=[0])), oracle.p(anti), oracle.p(tot)) == 1
+    assert f(_grp(cnt=[1]), anti) == 0
+    assert f(_grp(cnt=[0]), anti) == 1
     # an existing pod's anti-affinity term of a group the incoming pod matches
     mine = _gpod(match_groups=2)
-    assert L.or_interpod_filter(oracle.p(_grp(anti=[0, 1])), oracle.p(mine), oracle.p(tot)) == 0
-    assert L.or_interpod_filter(oracle.p(_grp(anti=[1, 0])), oracle.p(mine), oracle.p(tot)) == 1
-    # required affinity to group 2: needs a matching pod on the node; the first pod of a series (no pod in the
-    # cluster matches and the pod matches its own terms) passes anywhere
-    aff = _gpod(pod_affinity_group=3, match_groups=4)
-    assert L.or_interpod_filter(oracle.p(_grp(cnt=[0, 0, 1])), oracle.p(aff), oracle.p(tot)) == 1
-    assert L.or_interpod_filter(oracle.p(_grp()), oracle.p(aff), oracle.p(tot)) == 1  # first of a series
-    tot[2] = 1
-    assert L.or_interpod_filter(oracle.p(_grp()), oracle.p(aff), oracle.p(tot)) == 0
-    tot[2] = 0
-    stranger = _gpod(pod_affinity_group=3, match_groups=0)  # does not match its own terms
-    assert L.or_interpod_filter(oracle.p(_grp()), oracle.p(stranger), oracle.p(tot)) == 0
+    assert f(_grp(anti=[0, 1]), mine) == 0
+    assert f(_grp(anti=[1, 0]), mine) == 1
+    # required affinity to group 2: needs a matching pod on the node; the first pod of a series (affinityCounts
+    # empty and the pod matches its own terms) passes anywhere
+    aff = _gpod(pod_affinity_group=3, pod_affinity_terms=4, match_groups=4)
+    assert f(_grp(cnt=[0, 0, 1]), aff) == 1
+    assert f(_grp(), aff) == 1  # first of a series
+    assert f(_grp(), aff, 0, _zones(entries=1)) == 0
+    stranger = _gpod(pod_affinity_group=3, pod_affinity_terms=4, match_groups=0)  # does not match its own terms
+    assert f(_grp(), stranger) == 0
+
+
+def test_interpod_zone_filter_cases():
+    """Zone-keyed terms: satisfyPodAffinity needs the node's zone label (even for the first pod of a series) and its
+    zone pair's count; anti-affinity pairs reject every node of the zone; a node without the label has no pair."""
+    L = oracle.lib()
+    f = lambda g, pod, zone, z: L.or_interpod_filter(oracle.p(g), oracle.p(pod), zone, oracle.p(z))
+    aff = _gpod(pod_affinity_group=1, pod_affinity_terms_zone=1, match_groups=1)
+    assert f(_grp(), aff, 2, _zones(aff=[0, 3], entries=1)) == 1  # zone 2 holds 3 matching pods
+    assert f(_grp(), aff, 1, _zones(aff=[0, 3], entries=1)) == 0
+    assert f(_grp(), aff, 1, _zones()) == 1  # first of a series, in a labelled zone
+    assert f(_grp(), aff, 0, _zones()) == 0  # "All topology labels must exist on the node"
+    both = _gpod(pod_affinity_group=1, pod_affinity_terms=1, pod_affinity_terms_zone=1, match_groups=1)
+    assert f(_grp(cnt=[1]), both, 1, _zones(aff=[1], entries=1)) == 1
+    assert f(_grp(cnt=[0]), both, 1, _zones(aff=[1], entries=1)) == 0  # the hostname pair is empty
+    anti = _gpod(pod_anti_affinity_zone=2)
+    assert f(_grp(), anti, 1, _zones(anti_in=[1])) == 0
+    assert f(_grp(), anti, 2, _zones(anti_in=[1])) == 1
+    assert f(_grp(), anti, 0, _zones(anti_in=[1])) == 1
+    assert f(_grp(), _gpod(match_groups=1), 3, _zones(anti_ex=[0, 0, 2])) == 0
+
+
+def test_interpod_zone_maps():
+    """or_ipa_zones_add: the zone pairs sum the nodes' counters; affinityCounts' emptiness sees hostname pairs on any
+    node and zone pairs only on labelled nodes."""
+    L = oracle.lib()
+    pod = _gpod(pod_affinity_group=1, pod_affinity_terms_zone=1, pod_anti_affinity_zone=2, match_groups=0b100,
+                n_pod_preferred=2, pod_preferred_group=[1, 2, 0, 0], pod_preferred_weight=[10, -5, 0, 0],
+                pod_preferred_zone=0b10)
+    z = _zones()
+    for g, zone in ((_grp(cnt=[1, 2, 0], anti_z=[0, 0, 1], symw_z=[0, 0, 4]), 1), (_grp(cnt=[0, 1]), 1),
+                    (_grp(cnt=[5, 5], anti_z=[0, 0, 9]), 0)):
+        L.or_ipa_zones_add(oracle.p(z), oracle.p(g), zone, oracle.p(pod))
+    assert z["aff"][0, 0] == 1 and z["anti_in"][0, 0] == 3 and z["anti_ex"][0, 0] == 1
+    assert z["score"][0, 0] == -5 * 3 + 4 and z["entries"][0] == 1  # only the zone-keyed preferred term
+    z0 = _zones()
+    L.or_ipa_zones_add(oracle.p(z0), oracle.p(_grp(cnt=[5])), 0, oracle.p(pod))
+    assert z0["entries"][0] == 0  # an unlabelled node makes no zone pair
+    raw = L.or_interpod_raw(oracle.p(_grp(cnt=[2, 7])), oracle.p(pod), 1, oracle.p(z))
+    assert raw == 10 * 2 + (-5 * 3 + 4)  # hostname term on the node + the zone pair
 
 
 def test_interpod_score_cases():
@@ -114,7 +164,7 @@ def test_interpod_score_cases():
     pod = _gpod(match_groups=0b100, n_pod_preferred=2, pod_preferred_group=[1, 2, 0, 0],
                 pod_preferred_weight=[10, -5, 0, 0])
     g = _grp(cnt=[2, 1, 0], symw=[100, 100, 7])
-    assert L.or_interpod_raw(oracle.p(g), oracle.p(pod)) == 20 - 5 + 7
+    assert L.or_interpod_raw(oracle.p(g), oracle.p(pod), 0, oracle.p(_zones())) == 20 - 5 + 7
     assert [L.or_interpod_normalize(r, -5, 10) for r in (-5, 0, 10)] == [0, int(100.0 * (5 / 15)), 100]
     assert L.or_interpod_normalize(3, 3, 3) == 0
 
@@ -128,6 +178,11 @@ def test_groups_apply_counts_terms():
     assert list(g["symw"][0, :4]) == [0, -30, 0, 5]
     oracle.groups_apply(g, 0, pod, -1, hard_weight=5)
     assert not g["cnt"].any() and not g["anti"].any() and not g["symw"].any()
+    zp = _gpod(match_groups=1, pod_anti_affinity_zone=0b10, pod_affinity_terms_zone=0b100, n_pod_preferred=2,
+               pod_preferred_group=[4, 4, 0, 0], pod_preferred_weight=[3, -2, 0, 0], pod_preferred_zone=0b10)
+    oracle.groups_apply(g, 0, zp, 1, hard_weight=5)
+    assert list(g["anti_z"][0, :4]) == [0, 1, 0, 0] and list(g["anti"][0, :4]) == [0, 0, 0, 0]
+    assert list(g["symw_z"][0, :4]) == [0, 0, 5, -2] and list(g["symw"][0, :4]) == [0, 0, 0, 3]
 
 
 # ---- composed scheduling on the oracle: the plugins' visible effects ---------------------------------------------
@@ -211,6 +266,47 @@ def test_oracle_preferred_anti_affinity_spreads():
     assert sorted(node) == [0, 1, 2]
 
 
+ZONE = "topology.kubernetes.io/zone"
+WEB = {"matchLabels": {"app": "web"}}
+ZONE_WORLDS = {  # (nodes' zones, replicas, PodGroupTable.fill_pod keywords) of the zone-keyed InterPodAffinity cases
+    "anti": ([1, 1, 2, 2, 3, 3, 0, 0], 6, dict(required_anti_affinity=[{"labelSelector": WEB, "topologyKey": ZONE}])),
+    "affinity": ([0, 1, 1, 2, 2, 3, 3], 5, dict(required_affinity=[{"labelSelector": WEB, "topologyKey": ZONE}])),
+    "preferred": ([1, 2, 3, 1, 2, 3], 6, dict(preferred_anti_affinity=[
+        {"weight": 100, "podAffinityTerm": {"labelSelector": WEB, "topologyKey": ZONE}}])),
+}
+
+
+def _zone_world(name):
+    zones, n, kw = ZONE_WORLDS[name]
+    cl, preds = _zoned(len(zones), zones)
+    return cl, _replicas(n, PodGroupTable(), **kw), preds, np.array(zones)
+
+
+def test_oracle_zone_anti_affinity_one_per_zone():
+    """Required anti-affinity with the zone key: one replica per zone, then the nodes without a zone label (the
+    term has no pair there) take the rest."""
+    cl, pods, preds, zone = _zone_world("anti")
+    node, _, _, g = _run_oracle(F.build_config(profile=IPA_ONLY), cl, pods, preds)
+    assert (node >= 0).all()
+    assert sorted(zone[node[:3]]) == [1, 2, 3] and (zone[node[3:]] == 0).all()
+    assert list(g["anti_z"][:, 0]) == list(np.bincount(node, minlength=len(zone)))
+
+
+def test_oracle_zone_affinity_follows_the_first_pod():
+    """Required affinity with the zone key: the first pod of the series goes to a labelled node, the rest to its
+    zone (any node of it), never to the node without the label."""
+    cl, pods, preds, zone = _zone_world("affinity")
+    node, _, _, _ = _run_oracle(F.build_config(profile=IPA_ONLY), cl, pods, preds)
+    assert (node > 0).all() and (zone[node] == zone[node[0]]).all()
+    assert len(set(node)) == 2  # NodeResourcesFit spreads them over the zone's two nodes
+
+
+def test_oracle_zone_preferred_anti_affinity_spreads_zones():
+    cl, pods, preds, zone = _zone_world("preferred")
+    node, _, _, _ = _run_oracle(F.build_config(profile=IPA_ONLY), cl, pods, preds)
+    assert sorted(zone[node[:3]]) == [1, 2, 3] and sorted(np.bincount(zone[node])[1:]) == [2, 2, 2]
+
+
 def test_pod_group_table_compiles_selectors():
     t = PodGroupTable()
     g1 = t.group({"matchLabels": {"app": "web"}}, ("default",))
@@ -258,19 +354,20 @@ def _device(cfg, cluster, pods, preds, calls=1):
         for a, b in zip(bounds[:-1], bounds[1:]):
             e.schedule_staged(int(a), int(b - a))
         node, score = e.fetch(0, len(pods))
-        groups = e.read_pod_groups()
+        groups = e.read_pod_groups(zone=True)
         state = e.read_state()
     return node, score, groups, state
 
 
 def _check(cfg, cluster, pods, preds, calls=1):
     want, want_score, st, g = _run_oracle(cfg, cluster, pods, preds, n_threads=8)
-    node, score, (cnt, anti, symw), state = _device(cfg, cluster, pods, preds, calls)
+    node, score, (cnt, anti, symw, anti_z, symw_z), state = _device(cfg, cluster, pods, preds, calls)
     bad = np.nonzero((node != want) | (score != want_score))[0]
     assert len(bad) == 0, f"first mismatch at pod {bad[0]}: gpu ({node[bad[0]]}, {score[bad[0]]}) " \
                           f"oracle ({want[bad[0]]}, {want_score[bad[0]]})"
     assert np.array_equal(cnt, g["cnt"][:cluster.n]) and np.array_equal(anti, g["anti"][:cluster.n])
     assert np.array_equal(symw, g["symw"][:cluster.n])
+    assert np.array_equal(anti_z, g["anti_z"][:cluster.n]) and np.array_equal(symw_z, g["symw_z"][:cluster.n])
     assert np.array_equal(state["requested_cpu"], st["requested"][:, abi.RES_CPU])
     return want
 
@@ -295,6 +392,15 @@ def test_device_matches_oracle(name, profile):
     cluster, pods, preds = _world(2000, 600, 61)
     node = _check(F.build_config(profile=profile), cluster, pods, preds, calls=2)
     assert (node >= 0).mean() > 0.5
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", sorted(ZONE_WORLDS))
+def test_device_zone_interpod_cases(name):
+    """The zone-keyed InterPodAffinity worlds above, on the device (one pod per call and one call for all)."""
+    cl, pods, preds, _ = _zone_world(name)
+    for calls in (1, len(pods)):
+        _check(F.build_config(profile=IPA_ONLY), cl, pods, preds, calls)
 
 
 @pytest.mark.gpu
