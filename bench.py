@@ -11,7 +11,8 @@ ingested, pod queue staged); PCIe-inclusive timing of kg_pods_schedule is report
 Other workloads (--workload): c1 (500 nodes, 5k pods: the reference's CPU-runnable case), c2 (10k nodes, 100k pods),
 c4 (NodeNUMAResource), c5 (Reservation + DeviceShare + ElasticQuota, 50k nodes), c5ds / c5r (its DeviceShare /
 Reservation halves), shipped (the reference's shipped profile, config/manager/scheduler-config.yaml:66-117:
-LoadAware + NodeNUMAResource + DeviceShare + Reservation + ElasticQuota on 256-cpu NUMA nodes with 8 GPUs).
+LoadAware + NodeNUMAResource + DeviceShare + Reservation + ElasticQuota on 256-cpu NUMA nodes with 8 GPUs), stock / stockz
+(the k8s v1.24 default profile + LoadAware with hostname / also zone-keyed PodTopologySpread and InterPodAffinity).
 
 Single-pod calls (the drop-in's scheduleOne, framework_extender_factory.go:156-185): after the timed region
 `--single-pod-calls` more queued pods are scheduled one kg_pods_schedule_staged call each, and the same number through
@@ -55,6 +56,7 @@ WORKLOADS = {
     "c5r": (50_000, 10_000, 32, 4, 2_000),
     "shipped": (50_000, 5_000, 32, 4, 1_000),
     "stock": (10_000, 2_000, 32, 8, 500),
+    "stockz": (10_000, 2_000, 32, 8, 500),
 }
 
 
@@ -156,12 +158,14 @@ class Work:
             self.seed = S.BASE_SEED + 8
             self.cluster, self.rsv = S.make_rsv_cluster(nodes, seed=self.seed)
             self.make_pods = S.make_rsv_pods
-        elif name == "stock":  # (r4) the upstream defaults + hostname PodTopologySpread / InterPodAffinity
+        elif name in ("stock", "stockz"):  # (r4) the upstream defaults + PodTopologySpread / InterPodAffinity
+            z = name == "stockz"  # stockz: zone-keyed constraints and terms too, 5 % of nodes without a zone label
             self.seed = S.BASE_SEED + 19
             self.cluster = S.make_cluster(nodes, seed=self.seed)
-            S.make_pod_groups(self.cluster.existing_pods, seed=self.seed + 3)
-            self.preds = S.make_predicates(nodes, S.make_pods(0), seed=self.seed + 2)[1]  # labels + taints
-            self.make_pods = lambda n, seed: S.make_pod_groups(S.make_pods(n, seed=seed), seed=seed + 4)
+            S.make_pod_groups(self.cluster.existing_pods, seed=self.seed + 3, zones=z)
+            self.preds = S.make_predicates(nodes, S.make_pods(0), seed=self.seed + 2,
+                                           no_zone=0.05 if z else 0.0)[1]  # labels + taints
+            self.make_pods = lambda n, seed: S.make_pod_groups(S.make_pods(n, seed=seed), seed=seed + 4, zones=z)
         else:  # c1, c3: Fit + LoadAware
             self.seed = S.BASE_SEED + (1 if name == "c1" else 3)
             self.cluster = S.make_cluster(nodes, seed=self.seed)
@@ -196,7 +200,7 @@ class Work:
         cl, cfg = self.cluster, self.cfg
         st = oracle.states(cl.n)
         oracle.add_pods(cfg, st, cl.existing_pods, cl.existing_node)
-        if self.name == "stock":
+        if self.name in ("stock", "stockz"):
             g = oracle.groups_init(cl.n, cl.existing_pods, cl.existing_node)
             on, _, _ = oracle.schedule_resv(cfg, cl.nodes, cl.metrics, st, None, pods, cl.now_ns, n_threads=threads,
                                             preds=self.preds, groups=g)
@@ -279,7 +283,7 @@ def main():
     elif wl == "c5r":  # shipped weights: Reservation 5000 (config/manager/scheduler-config.yaml:90-91)
         profile = F.Profile(filter=(F.NODE_RESOURCES_FIT, F.LOAD_AWARE, F.RESERVATION),
                             score={F.NODE_RESOURCES_FIT: 1, F.LOAD_AWARE: 1, F.RESERVATION: 5000})
-    elif wl == "stock":  # k8s v1.24 v1beta2 default weights + LoadAware; hostname spread / inter-pod affinity
+    elif wl in ("stock", "stockz"):  # k8s v1.24 v1beta2 default weights + LoadAware; hostname spread / inter-pod affinity
         profile = F.Profile(filter=(F.NODE_RESOURCES_FIT, F.LOAD_AWARE, F.TAINT_TOLERATION, F.NODE_AFFINITY,
                                     F.POD_TOPOLOGY_SPREAD, F.INTER_POD_AFFINITY),
                             score={F.NODE_RESOURCES_FIT: 1, F.LOAD_AWARE: 1, F.TAINT_TOLERATION: 1, F.NODE_AFFINITY: 1,
@@ -362,7 +366,7 @@ def main():
                        "note": "kg_pods_schedule_staged(count=1) continuing the staged queue after the timed region; "
                                "kg_pods_schedule(1 host pod) on a fresh engine: decode + upload + schedule + result"})
     # isolated replays of one round's kernels (warm caches, no concurrency) for comparison
-    rsv_path = wl in ("c5r", "c5", "shipped", "stock")
+    rsv_path = wl in ("c5r", "c5", "shipped", "stock", "stockz")
     names = (("rsv_eval", "rsv_select") if rsv_path else
              ("eval_round", "merge_round", "resolve_round") + (("ds_max_round", "ds_norm_reduce") if wl == "c5ds" else ()))
     isolated = {name: e.bench_kernel(which, args.kernel_iters) for which, name in enumerate(names)}
@@ -371,13 +375,13 @@ def main():
     # processes the round's B pods against every node row of this rank's shard, reading each row once:
     # algorithmic bytes = rows × b_node + the candidate lists written + the pods read.
     dom = {"c5ds": "ds_max_round", "c5r": "rsv_eval", "c5": "rsv_eval", "shipped": "rsv_eval",
-           "stock": "rsv_eval"}.get(wl, "eval_round")
+           "stock": "rsv_eval", "stockz": "rsv_eval"}.get(wl, "eval_round")
     n_local = -(-cluster.n // d.world)
     nt = max(1, -(-n_local // 256))
     B = 1 if rsv_path else args.batch
     if wl == "c5ds":  # ds_max_round also reads the 272-B GPU row and writes a 4-B packed value per (pod, node)
         algo = n_local * (B_NODE + 272.0) + B * n_local * 4.0 + B * nt * 8.0
-    elif wl == "stock":  # one pod per exact pass (rsv_eval): per node the Fit / LoadAware columns, the 32-B NodePred,
+    elif wl in ("stock", "stockz"):  # one pod per exact pass (rsv_eval): per node the Fit / LoadAware columns, the 32-B NodePred,
         # ~4 group counters, and the 8 + 4 + 8 B of values it writes
         algo = n_local * (B_NODE + 32.0 + 16.0 + 20.0)
     elif rsv_path:  # the exact wide pass (xr_eval, live time folded under "rsv_eval"): one launch scores the round's
@@ -435,7 +439,7 @@ def main():
                                       os.path.join(ROOT, "profiles", "r02", f"traffic_{wl}.json"))
     # live timing folds every wide pass under one name: the kernel rocprof sees
     pmc_name = {"c4": "eval_round_numa", "c5": "xr_eval", "c5r": "xr_eval", "shipped": "xr_eval",
-                "stock": "rsv_eval"}.get(wl, dom)
+                "stock": "rsv_eval", "stockz": "rsv_eval"}.get(wl, dom)
     traffic, traffic_src, rocprof_ns = (pmc_traffic(tfile, pmc_name, cluster.n, args.batch, args.pods_per_wave,
                                                     args.depth) if d.world == 1 else (None, None, None))
     # period decomposition of the round pipeline (Fit + LoadAware / DeviceShare round profiles): per round, the serial
@@ -491,6 +495,11 @@ def main():
                      "spread, 15%% required anti-affinity, 10%% required affinity, 30%% preferred terms), NodeResourcesFit"
                      "+LoadAware+TaintToleration+NodeAffinity+BalancedAllocation+PodTopologySpread(w2)+InterPodAffinity, "
                      "one pod per exact pass, %d pods per step",
+            "stockz": "k8s v1.24 default profile + LoadAware with zone keys: %d nodes in 4 zones (5%% without the zone "
+                      "label), %d-pod FIFO queue of 8 deployments in 4 teams (hostname and zone spread constraints in "
+                      "random order; a third of required anti-affinity, half of required affinity and half of "
+                      "preferred terms zone-keyed), the stock profile's plugins and weights, one pod per exact pass, "
+                      "%d pods per step",
         }[wl] % (cluster.n, total, args.pods_per_step)
         out = {
             "metric": {"c3": "pods scheduled/sec at 100k nodes (node-evals/sec alongside)",
@@ -503,7 +512,9 @@ def main():
                        "c5": "pods scheduled/sec, Reservation+DeviceShare+ElasticQuota profile (node-evals/sec "
                              "alongside)",
                        "stock": "pods scheduled/sec, default plugins + hostname PodTopologySpread / InterPodAffinity "
-                                "(node-evals/sec alongside)"}[wl],
+                                "(node-evals/sec alongside)",
+                       "stockz": "pods scheduled/sec, default plugins + hostname / zone PodTopologySpread / "
+                                 "InterPodAffinity (node-evals/sec alongside)"}[wl],
             "value": pods_s,
             "unit": "pods/s",
             "n_gpus": d.world,
