@@ -366,6 +366,15 @@ typedef struct kg_pod {
   int64_t pod_affinity_terms_zone;
   int64_t pod_anti_affinity_zone;
   int64_t pod_preferred_zone;
+  /* (ABI 12) the required reservation affinity of a KG_POD_RSV_AFFINITY pod (GetRequiredReservationAffinity,
+   * pkg/util/reservation/reservation.go:444-489), over the caller's predicate table evaluated on each slot's labels
+   * (kg_node_reservations.predicates): matchReservation (reservation/transformer.go:348-372) also needs every
+   * predicate of reservation_selector (ReservationSelector) and, when n_reservation_terms > 0, one of the
+   * ReservationSelectorTerms (each: every listed predicate; 0 = an empty term, matching nothing).  All zero: the
+   * owner groups alone decide, as before. */
+  uint64_t reservation_selector;
+  int64_t n_reservation_terms;
+  uint64_t reservation_terms[KG_MAX_AFF_TERMS];
 } kg_pod;
 
 /* pod reservation flags */
@@ -396,6 +405,9 @@ typedef struct kg_node_reservations {
   int64_t allocate_once[KG_MAX_RSV_SLOTS];     /* IsAllocateOnce                                               */
   int64_t available[KG_MAX_RSV_SLOTS];         /* IsAvailable && ParseError == nil                             */
   int64_t unschedulable[KG_MAX_RSV_SLOTS];     /* IsUnschedulable                                              */
+  uint64_t predicates[KG_MAX_RSV_SLOTS];       /* (ABI 12) the caller's predicate bits over the node's labels  */
+                                               /* overlaid with the reservation's (matchReservation's fakeNode, */
+                                               /* transformer.go:357-369); read for reservation-affinity pods    */
 } kg_node_reservations;
 
 /* One ElasticQuota as the plugin's PreFilter snapshot sees it (plugin.go:211-256) over KG_QUOTA_RES resources: cpu

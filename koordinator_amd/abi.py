@@ -157,6 +157,7 @@ POD_DTYPE = np.dtype([
     _i64("n_pod_preferred"), _i64("pod_preferred_group", MAX_POD_PREFERRED),
     _i64("pod_preferred_weight", MAX_POD_PREFERRED),
     _i64("pod_affinity_terms_zone"), _i64("pod_anti_affinity_zone"), _i64("pod_preferred_zone"),
+    ("reservation_selector", np.uint64), _i64("n_reservation_terms"), ("reservation_terms", np.uint64, (MAX_AFF_TERMS,)),
 ])
 NODE_PRED_DTYPE = np.dtype([("predicates", np.uint64), ("taints_hard", np.uint64), ("taints_soft", np.uint64),
                             ("images", np.uint64), _i64("predicate_count"), _i64("image_count"), _i64("zone")])
@@ -164,7 +165,7 @@ NODE_PRED_DTYPE = np.dtype([("predicates", np.uint64), ("taints_hard", np.uint64
 
 NODE_RSV_DTYPE = np.dtype([_i64("n")] + [_i64(f, MAX_RSV_SLOTS) for f in (
     "owner", "allocatable_cpu", "allocatable_mem", "allocated_cpu", "allocated_mem", "assigned", "order", "policy",
-    "allocate_once", "available", "unschedulable")])
+    "allocate_once", "available", "unschedulable")] + [("predicates", np.uint64, (MAX_RSV_SLOTS,))])
 
 QUOTA_DTYPE = np.dtype([_i64("used", QUOTA_RES), _i64("non_preemptible_used", QUOTA_RES), _i64("used_limit", QUOTA_RES),
                         _i64("min", QUOTA_RES)])

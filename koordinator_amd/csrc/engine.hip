@@ -4641,7 +4641,22 @@ int decode_node_rsv(const kg_node_reservations& r, RsvNode& d, int32_t& ns) {
     d.order[s] = (int32_t)r.order[s];
     d.meta[s] = (r.available[s] ? RS_AVAIL : 0u) | (r.allocate_once[s] ? RS_ONCE : 0u) |
                 (r.unschedulable[s] ? RS_UNSCHED : 0u) | ((uint32_t)r.policy[s] << 4);
+    d.pred[s] = r.predicates[s];
   }
+  return 0;
+}
+
+// the Reservation view of one pod: owner groups, the required-affinity flag and (ABI 12) its selector / terms
+int decode_rsv_pod(const kg_pod& p, RsvPod& d, int64_t k) {
+  std::memset(&d, 0, sizeof(d));
+  if (p.n_reservation_terms < 0 || p.n_reservation_terms > KG_MAX_AFF_TERMS)
+    return fail(KG_E_UNSUPPORTED, "pod %lld: more than %d reservation affinity terms (the pod stays on the Go path)",
+                (long long)k, KG_MAX_AFF_TERMS);
+  d.owner_mask = (uint64_t)p.reservation_owner_mask;
+  d.flags = (p.reservation_flags & KG_POD_RSV_AFFINITY) ? RP_AFFINITY : 0u;
+  d.nterms = (uint32_t)p.n_reservation_terms;
+  d.sel = p.reservation_selector;
+  for (int t = 0; t < d.nterms; ++t) d.terms[t] = p.reservation_terms[t];
   return 0;
 }
 
@@ -5427,11 +5442,8 @@ int kg_pods_stage(kg_engine* e, const kg_pod* pods, int64_t n) {
   }
   {  // exact-pass records (the Reservation view of every pod; single-pod calls of any profile use the pass)
     std::vector<RsvPod> hr(std::max<int64_t>(n, 1));
-    for (int64_t k = 0; k < n; ++k) {
-      hr[k].owner_mask = (uint64_t)pods[k].reservation_owner_mask;
-      hr[k].flags = (pods[k].reservation_flags & KG_POD_RSV_AFFINITY) ? RP_AFFINITY : 0u;
-      hr[k].pad = 0;
-    }
+    for (int64_t k = 0; k < n; ++k)
+      if (int rc = decode_rsv_pod(pods[k], hr[k], k)) return rc;
     if (int rc = e->rpods.ensure(n + kMaxB)) return rc;
     if (int rc = e->out_rslot.ensure(n + kMaxB)) return rc;
     if (n > 0) HIP_TRY(hipMemcpyAsync(e->rpods.p, hr.data(), n * sizeof(RsvPod), hipMemcpyHostToDevice, e->stream));
@@ -5839,7 +5851,7 @@ int kg_quotas_read(kg_engine* e, kg_quota* out, int64_t n) {
 // Reservation profile: which 0 = rsv_eval, 1 = rsv_select, replayed on the first staged pod (neither kernel
 // changes node state; the cursor words are reset afterwards).  Algorithmic bytes of rsv_eval per launch: SURVEY
 // §8d's 76 B of Fit + LoadAware columns per node, the 4-B slot count and the 8-B packed value written, plus the
-// 192-B slot record of every node that has reservations; rsv_select reads the 8-B packed value per node.
+// 224-B slot record of every node that has reservations; rsv_select reads the 8-B packed value per node.
 static int bench_rsv(kg_engine* e, int which, int iters, double* avg_ms, double* algo_bytes) {
   if (iters <= 0 || which < 0 || which > 1) return fail(KG_E_INVALID, "bad argument");
   if (e->n_staged <= 0) return fail(KG_E_INVALID, "stage a pod queue first");
@@ -6198,7 +6210,8 @@ int kg_pods_evaluate_reservation(kg_engine* e, const kg_pod* pod, int64_t* out) 
   if (int rc = sync_static(e)) return rc;
   DevPod d;
   if (int rc = decode_pod(e, *pod, d)) return rc;
-  RsvPod rp{(uint64_t)pod->reservation_owner_mask, (pod->reservation_flags & KG_POD_RSV_AFFINITY) ? RP_AFFINITY : 0u, 0};
+  RsvPod rp;
+  if (int rc = decode_rsv_pod(*pod, rp, 0)) return rc;
   DsPod dsp{};
   dsp.skip = 1;
   if (e->ds_on)
@@ -6243,7 +6256,8 @@ int kg_pods_filter_preemption(kg_engine* e, const kg_pod* pod, int32_t node_idx,
   DevPod d;
   if (int rc = decode_pod(e, *pod, d)) return rc;
   if (d.flags & P_AUX) return fail(KG_E_UNSUPPORTED, "preemption dry run: ephemeral-storage / scalar requests");
-  const RsvPod rp{(uint64_t)pod->reservation_owner_mask, (pod->reservation_flags & KG_POD_RSV_AFFINITY) ? RP_AFFINITY : 0u, 0};
+  RsvPod rp;
+  if (int rc = decode_rsv_pod(*pod, rp, 0)) return rc;
   std::vector<Victim> hv((size_t)std::max<int64_t>(n_victims, 1));
   for (int64_t k = 0; k < n_victims; ++k) {
     DevPod v;

@@ -40,19 +40,33 @@ constexpr uint32_t RS_AVAIL = 1u << 0, RS_ONCE = 1u << 1, RS_UNSCHED = 1u << 2; 
 constexpr uint32_t RP_AFFINITY = 1u << 0;
 constexpr int64_t kDefaultMilliCpu = 100, kDefaultMemory = 200ll << 20;  // schedutil.GetNonzeroRequests defaults
 
-struct RsvNode {  // 192 B: one node's slots, read only for nodes with slots (rsv_n[i] > 0)
+struct RsvNode {  // 224 B: one node's slots, read only for nodes with slots (rsv_n[i] > 0)
   int64_t alloc_cpu[kRsvSlots], alloc_mem[kRsvSlots];    // ReservationInfo.Allocatable (0 = key absent)
   int64_t allocd_cpu[kRsvSlots], allocd_mem[kRsvSlots];  // ReservationInfo.Allocated
   int32_t owner[kRsvSlots], assigned[kRsvSlots], order[kRsvSlots];  // owner group 0..63
   uint32_t meta[kRsvSlots];
+  uint64_t pred[kRsvSlots];  // predicate bits over the node's labels overlaid with the reservation's
 };
-static_assert(sizeof(RsvNode) == 192, "RsvNode layout");
+static_assert(sizeof(RsvNode) == 224, "RsvNode layout");
 
-struct RsvPod {
+struct RsvPod {  // 56 B
   uint64_t owner_mask;  // bit g: the pod matches the owners of owner group g
   uint32_t flags;
-  uint32_t pad;
+  uint32_t nterms;      // required reservation affinity: ReservationSelectorTerms (0 = absent)
+  uint64_t sel;         // ReservationSelector predicates (all must hold)
+  uint64_t terms[KG_MAX_AFF_TERMS];
 };
+
+// RequiredReservationAffinity.Match (pkg/util/reservation/reservation.go:476-489) on a slot's fakeNode labels
+__device__ __forceinline__ bool rsv_affinity_match(const RsvPod& rp, uint64_t pred) {
+  if (!(rp.flags & RP_AFFINITY)) return true;
+  if ((pred & rp.sel) != rp.sel) return false;
+  if (rp.nterms == 0) return true;
+  bool any = false;
+#pragma unroll
+  for (int k = 0; k < KG_MAX_AFF_TERMS; ++k) any |= k < (int)rp.nterms && rp.terms[k] != 0 && (pred & rp.terms[k]) == rp.terms[k];
+  return any;
+}
 
 struct RsvParams {
   int32_t filter, score, weight, pad;
@@ -156,7 +170,8 @@ __device__ __forceinline__ void rsv_restore(const RsvNode& rn, int ns, const Rsv
     const uint32_t m = rn.meta[s];
     if (!(m & RS_AVAIL) || ((m & RS_ONCE) && rn.assigned[s] > 0)) continue;  // transformer.go:101-110
     // ReservationInfo.Match → MatchReservationOwners, decoded per owner group into the pod's mask
-    if (((rp.owner_mask >> (rn.owner[s] & 63)) & 1u) && !(m & RS_UNSCHED)) mm |= 1u << s;
+    if (((rp.owner_mask >> (rn.owner[s] & 63)) & 1u) && !(m & RS_UNSCHED) && rsv_affinity_match(rp, rn.pred[s]))
+      mm |= 1u << s;
     else if (rn.assigned[s] > 0) um |= 1u << s;
   }
   has_state = (mm | um) != 0 && !((rp.flags & RP_AFFINITY) && mm == 0);  // transformer.go:127-136

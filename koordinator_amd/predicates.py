@@ -199,6 +199,45 @@ class PredicateTable:
             row["preferred_weights"][k] = w
         return pod
 
+    # ---- (ABI 12) reservation affinity (matchReservation, reservation/transformer.go:348-372) ----
+    def reservation_predicates(self, node_labels: dict | None, reservation_labels: dict | None,
+                               reservation_name: str = "") -> int:
+        """kg_node_reservations.predicates of one slot: the predicate bits over matchReservation's fakeNode — named
+        after the reservation, the node's labels overlaid with the reservation's.  Like node rows, a slot decides the
+        predicates interned before it: intern the queue's reservation affinities first, or re-send the slots."""
+        labels = dict(node_labels or {})
+        labels.update(reservation_labels or {})
+        m = 0
+        for k, pr in enumerate(self.preds):
+            if self._holds(pr, labels, reservation_name):
+                m |= 1 << k
+        return m
+
+    def fill_reservation_affinity(self, pod: np.ndarray, selector: dict | None = None,
+                                  required_terms: list | None = None) -> np.ndarray:
+        """The pod's required reservation affinity (apiext.ReservationAffinity; GetRequiredReservationAffinity,
+        pkg/util/reservation/reservation.go:450-474): reservationSelector {key: value} and the
+        ReservationSelectorTerms of requiredDuringScheduling (None = not set; [] = set with no terms, matching
+        nothing).  Neither set: no affinity.  Sets KG_POD_RSV_AFFINITY when either is (in place; returns it)."""
+        row = pod[0] if pod.shape else pod
+        sel = 0
+        for k, v in (selector or {}).items():
+            sel |= 1 << self.pred_id("label", k, "In", (v,))
+        row["reservation_selector"] = sel
+        row["n_reservation_terms"] = 0
+        row["reservation_terms"][:] = 0
+        if required_terms is not None:
+            if len(required_terms) > abi.MAX_AFF_TERMS:
+                raise OverflowError("more than 4 reservation affinity terms: the pod stays on the Go path")
+            terms = [self._term_mask(t) for t in required_terms] or [0]
+            row["n_reservation_terms"] = len(terms)
+            row["reservation_terms"][:len(terms)] = terms
+        flags = int(row["reservation_flags"]) & ~abi.POD_RSV_AFFINITY
+        if selector or required_terms is not None:
+            flags |= abi.POD_RSV_AFFINITY
+        row["reservation_flags"] = flags
+        return pod
+
 
 def normalized_image_name(name: str) -> str:
     """imagelocality normalizedImageName (v1.24.15): no tag after the last '/' → ':latest' appended."""

@@ -397,6 +397,35 @@ def make_rsv_pods(n_pods: int, seed: int = BASE_SEED + 9, base: np.ndarray | Non
     return p
 
 
+def add_reservation_affinity(rsv: np.ndarray, pods: np.ndarray, seed: int = BASE_SEED + 23) -> None:
+    """(ABI 12) Labels and required reservation affinities, in place: each node gets topology.kubernetes.io/zone
+    z0..z3, each reservation reservation-type ∈ {a, b, c} (a fifth also zone = its own "z-pinned" value, overlaying the
+    node's); half of the pods with a required reservation affinity carry a reservationSelector on reservation-type
+    and a third of the others ReservationSelectorTerms (type In {a, b} / zone In {z0, z1}, ORed) — compiled through
+    PredicateTable as a caller would (affinities interned first, then the slots' fakeNode predicates)."""
+    from .predicates import PredicateTable, ZONE
+    rng = np.random.default_rng(seed)
+    t = PredicateTable()
+    aff = np.nonzero(pods["reservation_flags"] & abi.POD_RSV_AFFINITY)[0]
+    kind = rng.random(len(aff))
+    for j, k in zip(aff, kind):
+        if k < 0.5:
+            t.fill_reservation_affinity(pods[j:j + 1], selector={"reservation-type": "abc"[rng.integers(3)]})
+        elif k < 0.67:
+            t.fill_reservation_affinity(pods[j:j + 1], required_terms=[
+                {"matchExpressions": [{"key": "reservation-type", "operator": "In", "values": ["a", "b"]}]},
+                {"matchExpressions": [{"key": ZONE, "operator": "In", "values": ["z0", "z1"]}]}])
+    n = len(rsv)
+    zone = rng.integers(0, 4, n)
+    for i in np.nonzero(rsv["n"] > 0)[0]:
+        node_labels = {ZONE: f"z{zone[i]}"}
+        for s in range(int(rsv["n"][i])):
+            labels = {"reservation-type": "abc"[rng.integers(3)]}
+            if rng.random() < 0.2:
+                labels[ZONE] = "z-pinned"
+            rsv["predicates"][i, s] = t.reservation_predicates(node_labels, labels, f"r-{i}-{s}")
+
+
 def load_rsv_into(engine, cluster: Cluster, rsv: np.ndarray):
     load_into(engine, cluster)
     engine.upsert_reservations(rsv)

@@ -24,12 +24,28 @@ static int slot_usable(const kg_node_reservations* r, int s) {
   return 1;
 }
 
+/* RequiredReservationAffinity.Match (pkg/util/reservation/reservation.go:476-489) on matchReservation's fakeNode — the
+ * node's labels overlaid with the reservation's (transformer.go:353-369) — as the caller's predicate bits of the slot:
+ * the ReservationSelector's predicates all hold, and one ReservationSelectorTerm holds when any are given (an empty
+ * term matches nothing, nodeaffinity.NodeSelector) */
+static int affinity_matches(const kg_pod* pod, uint64_t pred) {
+  if (!(pod->reservation_flags & KG_POD_RSV_AFFINITY)) return 1;
+  if ((pred & pod->reservation_selector) != pod->reservation_selector) return 0;
+  if (pod->n_reservation_terms <= 0) return 1;
+  for (int64_t t = 0; t < pod->n_reservation_terms && t < KG_MAX_AFF_TERMS; t++) {
+    const uint64_t term = pod->reservation_terms[t];
+    if (term != 0 && (pred & term) == term) return 1;
+  }
+  return 0;
+}
+
 static int pod_matches(const kg_pod* pod, const kg_node_reservations* r, int s) {
-  /* ReservationInfo.Match → MatchReservationOwners (reservation_info.go:231-236) decoded per owner group: bit g of
-   * the pod's mask; !IsUnschedulable (transformer.go:112); the affinity selector matches every reservation of the
-   * owner group */
+  /* matchReservation (transformer.go:348-372): ReservationInfo.Match → MatchReservationOwners
+   * (reservation_info.go:231-236) decoded per owner group — bit g of the pod's mask —, !IsUnschedulable
+   * (transformer.go:112), and the pod's required reservation affinity on the slot's labels */
   const int64_t g = r->owner[s];
-  return g >= 0 && g < KG_MAX_OWNER_GROUPS && (((uint64_t)pod->reservation_owner_mask >> g) & 1u) && !r->unschedulable[s];
+  return g >= 0 && g < KG_MAX_OWNER_GROUPS && (((uint64_t)pod->reservation_owner_mask >> g) & 1u) &&
+         !r->unschedulable[s] && affinity_matches(pod, r->predicates[s]);
 }
 
 /* GetNonzeroRequests of the reserve pod (requests = Allocatable): an absent key takes the default */

@@ -68,10 +68,14 @@ CASES += [
 
 # BeforePreFilter's restore (transformer.go:49-346): one node, its bound pods (cpu cores, memory GiB; "reserve" = a
 # reservation's reserve pod) and reservation slots, the pod's owner-group mask / required-affinity flag, and the
-# restored node (transformer_test.go assertions).  Owner groups: the caller decodes ReservationInfo.Match — and, when
-# the pod has a reservation affinity, the affinity selector over the reservation's labels (matchReservation,
-# transformer.go:348-372) — into the pod's mask.  Test_matchReservation (:348) exercises only that caller-side label
-# matching and is not an engine case.
+# restored node (transformer_test.go assertions).  Owner groups: the caller decodes ReservationInfo.Match into the pod's
+# mask.  (ABI 12) A required reservation affinity travels as predicates: "rsv_affinity" = the pod's
+# reservationSelector / ReservationSelectorTerms, "node_labels" / "slot_labels" = matchReservation's fakeNode
+# (transformer.go:348-372), compiled through PredicateTable by the test.
+AFF_A_TRUE = {"terms": [{"matchExpressions": [{"key": "reservation-a", "operator": "In", "values": ["true"]}]}]}
+AFF_A_FALSE = {"terms": [{"matchExpressions": [{"key": "reservation-a", "operator": "In", "values": ["false"]}]}]}
+AFF_TYPE = {"terms": [{"matchExpressions": [{"key": "reservation-type", "operator": "In",
+                                             "values": ["reservation-test"]}]}]}
 RESTORE = [
     dict(ref="transformer_test.go:41 TestRestoreReservation", node=[32, 64],
          pods=[[4, 8, 0], [8, 16, 0], [12, 24, 1], [8, 16, 1], [4, 8, 0]],
@@ -81,12 +85,24 @@ RESTORE = [
          want=dict(has_state=1, matched=0b10, requested_cpu=24000, requested_mem=48 * GI, nonzero_cpu=24000,
                    nonzero_mem=48 * GI, num_pods=4, pod_requested_cpu=32000, pod_requested_mem=64 * GI)),
     dict(ref="transformer_test.go:510 pod has no reservation affinity", node=[32, 64], pods=[[8, 16, 1]],
-         slots=[dict(slot(8, 16), owner=0, allocate_once=1)], mask=1, affinity=0, want=dict(has_state=1)),
+         slots=[dict(slot(8, 16), owner=0, allocate_once=1)], mask=1, affinity=0,
+         node_labels={"test": "true"}, slot_labels=[{"reservation-a": "true"}], want=dict(has_state=1, matched=1)),
     dict(ref="transformer_test.go:514 pod has reservation affinity and matched", node=[32, 64], pods=[[8, 16, 1]],
-         slots=[dict(slot(8, 16), owner=0, allocate_once=1)], mask=1, affinity=1, want=dict(has_state=1)),
+         slots=[dict(slot(8, 16), owner=0, allocate_once=1)], mask=1, affinity=1, rsv_affinity=AFF_A_TRUE,
+         node_labels={"test": "true"}, slot_labels=[{"reservation-a": "true"}], want=dict(has_state=1, matched=1)),
     dict(ref="transformer_test.go:533 pod has reservation affinity but failed to match", node=[32, 64],
-         pods=[[8, 16, 1]], slots=[dict(slot(8, 16), owner=0, allocate_once=1)], mask=0, affinity=1,
-         want=dict(has_state=0)),
+         pods=[[8, 16, 1]], slots=[dict(slot(8, 16), owner=0, allocate_once=1)], mask=1, affinity=1,
+         rsv_affinity=AFF_A_FALSE, node_labels={"test": "true"}, slot_labels=[{"reservation-a": "true"}],
+         want=dict(has_state=0, matched=0)),
+    # Test_matchReservation (transformer_test.go:348-442) through the restore: the pod matches the owners; with the
+    # affinity term on the reservation's own label it still matches (both "want: true")
+    dict(ref="transformer_test.go:356 only match reservation owners", node=[32, 64], pods=[[8, 16, 1]],
+         slots=[dict(slot(8, 16), owner=0, allocate_once=0)], mask=1, affinity=0,
+         slot_labels=[{}], want=dict(has_state=1, matched=1)),
+    dict(ref="transformer_test.go:379 match reservation owners and match reservation affinity", node=[32, 64],
+         pods=[[8, 16, 1]], slots=[dict(slot(8, 16), owner=0, allocate_once=0)], mask=1, affinity=1,
+         rsv_affinity=AFF_TYPE, slot_labels=[{"reservation-type": "reservation-test"}],
+         want=dict(has_state=1, matched=1)),
 ]
 
 if __name__ == "__main__":
@@ -96,7 +112,6 @@ if __name__ == "__main__":
                    "restore": RESTORE,
                    "skipped": [{"ref": "nominator_test.go:110 reserve pod",
                                 "reason": "scheduling a reserve pod stays on the Go path"},
-                               {"ref": "transformer_test.go:348 Test_matchReservation",
-                                "reason": "caller-side label-selector matching (decoded into reservation_owner_mask)"}]},
+                               ]},
                   f, indent=1)
     print(f"wrote {len(CASES)} cases to {out}")

@@ -63,6 +63,18 @@ def test_schedule_parity_owner_heavy_small_cluster():
     assert (node < 0).any() and (slot >= 0).any()
 
 
+def test_schedule_parity_reservation_affinity_selectors():
+    """(ABI 12) Required reservation affinities narrower than the owner groups: reservationSelector and
+    ReservationSelectorTerms over the slots' fakeNode labels (synth.add_reservation_affinity)."""
+    cluster, rsv = synth.make_rsv_cluster(600, seed=71)
+    pods = synth.make_rsv_pods(1500, seed=72)
+    pods["reservation_flags"] = np.where(pods["reservation_owner_mask"] != 0, abi.POD_RSV_AFFINITY, 0)
+    synth.add_reservation_affinity(rsv, pods, seed=73)
+    assert (pods["reservation_selector"] != 0).any() and (pods["n_reservation_terms"] > 0).any()
+    node, slot = check(F.build_config(profile=PROFILE), cluster, rsv, pods, chunks=2)
+    assert (slot >= 0).sum() > 10
+
+
 def test_schedule_parity_filter_only_and_plugin_off():
     cluster, rsv = synth.make_rsv_cluster(500, seed=61)
     pods = synth.make_rsv_pods(800, seed=62)

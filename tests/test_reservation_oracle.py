@@ -49,3 +49,31 @@ def test_reserve_bookkeeping_and_affinity():
                                       minlength=cluster.n * abi.MAX_RSV_SLOTS).reshape(cluster.n, -1))
     aff = (pods["reservation_flags"] & abi.POD_RSV_AFFINITY) != 0
     assert ((slot >= 0) | (node < 0))[aff].all()  # required affinity: placed only through a reservation
+
+
+def _affinity_ok(pod, pred):
+    """RequiredReservationAffinity.Match on a slot's predicate bits (the restatement the engine and oracle share)."""
+    if not pod["reservation_flags"] & abi.POD_RSV_AFFINITY:
+        return True
+    sel = int(pod["reservation_selector"])
+    if pred & sel != sel:
+        return False
+    n = int(pod["n_reservation_terms"])
+    return n == 0 or any(int(t) != 0 and pred & int(t) == int(t) for t in pod["reservation_terms"][:n])
+
+
+def test_reservation_affinity_selectors_bite():
+    """(ABI 12) Selectors narrower than the owner groups change the matched reservations: placements differ from the
+    owner-only run, and every pod assumed into a slot satisfies its affinity on that slot's fakeNode predicates."""
+    cluster, rsv = synth.make_rsv_cluster(300, seed=81)
+    pods = synth.make_rsv_pods(900, seed=82)
+    pods["reservation_flags"] = np.where(pods["reservation_owner_mask"] != 0, abi.POD_RSV_AFFINITY, 0)
+    cfg = F.build_config(profile=PROFILE)
+    base_node, _, base_slot, _, _ = run(cfg, cluster, rsv, pods)
+    synth.add_reservation_affinity(rsv, pods, seed=83)
+    node, _, slot, _, _ = run(cfg, cluster, rsv, pods)
+    assert (node != base_node).any() or (slot != base_slot).any()
+    placed = np.nonzero(slot >= 0)[0]
+    assert len(placed) > 5
+    for j in placed:
+        assert _affinity_ok(pods[j], int(rsv["predicates"][node[j], slot[j]]))

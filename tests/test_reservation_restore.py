@@ -11,6 +11,7 @@ import pytest
 
 import golden_cases as G
 from koordinator_amd import Engine, abi, framework as F
+from koordinator_amd.predicates import PredicateTable
 from oracle import oracle
 
 GI = 1 << 30
@@ -38,11 +39,26 @@ def _pods(spec):
     return np.concatenate(out) if out else np.zeros(0, dtype=abi.POD_DTYPE)
 
 
-def _pod(c):
+def _pod(c, table=None):
     p = F.make_pod({})
     p["reservation_owner_mask"] = c["mask"]
     p["reservation_flags"] = abi.POD_RSV_AFFINITY if c["affinity"] else 0
+    if table is not None and c.get("rsv_affinity"):
+        a = c["rsv_affinity"]
+        table.fill_reservation_affinity(p, selector=a.get("selector"), required_terms=a.get("terms"))
     return p
+
+
+def _case(c):
+    """(pod, slots) of a restore case; a case with labels compiles the pod's reservation affinity and then the slots'
+    fakeNode predicates through one PredicateTable (ABI 12)."""
+    table = PredicateTable() if "slot_labels" in c else None
+    pod = _pod(c, table)
+    slots = _slots(c["slots"])
+    if table is not None:
+        for s, labels in enumerate(c["slot_labels"]):
+            slots[0]["predicates"][s] = table.reservation_predicates(c.get("node_labels"), labels, f"r{s}")
+    return pod, slots
 
 
 def _node(c):
@@ -55,7 +71,8 @@ def test_restore_oracle(c):
     st = oracle.states(1)
     pods = _pods(c["pods"])
     oracle.add_pods(cfg, st, pods, np.zeros(len(pods), np.int32))
-    got = oracle.rsv_restore(_slots(c["slots"]), st, _pod(c))
+    pod, slots = _case(c)
+    got = oracle.rsv_restore(slots, st, pod)
     for k, v in c["want"].items():
         assert got[k] == v, (c["ref"], k)
 
@@ -67,8 +84,9 @@ def test_restore_device(c):
         e.upsert_nodes(_node(c))
         pods = _pods(c["pods"])
         e.add_pods(pods, np.zeros(len(pods), np.int32))
-        e.upsert_reservations(_slots(c["slots"]))
-        ev = e.evaluate_reservation(_pod(c))
+        pod, slots = _case(c)
+        e.upsert_reservations(slots)
+        ev = e.evaluate_reservation(pod)
     for k, v in c["want"].items():
         assert int(ev[k][0]) == v, (c["ref"], k)
 
