@@ -375,11 +375,20 @@ typedef struct kg_pod {
   uint64_t reservation_selector;
   int64_t n_reservation_terms;
   uint64_t reservation_terms[KG_MAX_AFF_TERMS];
+  /* (ABI 12) scheduling a Reservation: a staged pod with KG_POD_RESERVE is the reservation's reserve pod
+   * (reservationutil.IsReservePod): it matches no reservation (transformer.go:112), and Reservation.Filter
+   * (reservation/plugin.go:324-350) pins it to the reservation's node and rejects nodes holding an available
+   * reservation whose allocate policy conflicts with its own (Default never coexists with another policy); a
+   * KG_POD_RSV_OPERATING pod (IsReservationOperatingMode) takes that conflict check with the Aligned policy.
+   * Its Reservation Score is MinNodeScore (scoring.go:104-106). */
+  int64_t reserve_allocate_policy;             /* the reservation's Spec.AllocatePolicy: KG_RSV_POLICY_*          */
+  int64_t reserve_node;                        /* 1 + index of GetReservePodNodeName's node; 0 = not pinned       */
 } kg_pod;
 
 /* pod reservation flags */
 enum {
-  KG_POD_RSV_AFFINITY = 1 << 0   /* GetRequiredReservationAffinity != nil: must allocate from a reservation */
+  KG_POD_RSV_AFFINITY = 1 << 0,  /* GetRequiredReservationAffinity != nil: must allocate from a reservation */
+  KG_POD_RSV_OPERATING = 1 << 1  /* (ABI 12) apiext.IsReservationOperatingMode: Filter's allocate-policy check */
 };
 
 /* Reservation slots of one node as reservationCache holds them (frameworkext/reservation_info.go:79-99,

@@ -39,7 +39,7 @@ MAX_QUOTAS = 64
 ABI_VERSION = 12
 MAX_RSV_SLOTS = 4
 RSV_POLICY = {"Default": 0, "Aligned": 1, "Restricted": 2}
-POD_RSV_AFFINITY = 1
+POD_RSV_AFFINITY, POD_RSV_OPERATING = 1, 2
 PROF_KINDS = 16
 PROF_NAMES = {0: "eval_round", 1: "merge_round", 2: "resolve_round", 3: "ds_max_round", 4: "ds_norm_reduce",
               5: "rsv_eval", 6: "rsv_select", 7: "rsv_apply"}
@@ -158,6 +158,7 @@ POD_DTYPE = np.dtype([
     _i64("pod_preferred_weight", MAX_POD_PREFERRED),
     _i64("pod_affinity_terms_zone"), _i64("pod_anti_affinity_zone"), _i64("pod_preferred_zone"),
     ("reservation_selector", np.uint64), _i64("n_reservation_terms"), ("reservation_terms", np.uint64, (MAX_AFF_TERMS,)),
+    _i64("reserve_allocate_policy"), _i64("reserve_node"),
 ])
 NODE_PRED_DTYPE = np.dtype([("predicates", np.uint64), ("taints_hard", np.uint64), ("taints_soft", np.uint64),
                             ("images", np.uint64), _i64("predicate_count"), _i64("image_count"), _i64("zone")])

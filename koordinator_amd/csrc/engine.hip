@@ -4653,7 +4653,17 @@ int decode_rsv_pod(const kg_pod& p, RsvPod& d, int64_t k) {
     return fail(KG_E_UNSUPPORTED, "pod %lld: more than %d reservation affinity terms (the pod stays on the Go path)",
                 (long long)k, KG_MAX_AFF_TERMS);
   d.owner_mask = (uint64_t)p.reservation_owner_mask;
-  d.flags = (p.reservation_flags & KG_POD_RSV_AFFINITY) ? RP_AFFINITY : 0u;
+  d.flags = ((p.reservation_flags & KG_POD_RSV_AFFINITY) ? RP_AFFINITY : 0u) |
+            ((p.flags & KG_POD_RESERVE) ? RP_RESERVE : 0u) | ((p.reservation_flags & KG_POD_RSV_OPERATING) ? RP_OPERATING : 0u);
+  d.policy = (p.flags & KG_POD_RESERVE) ? (int32_t)p.reserve_allocate_policy : KG_RSV_POLICY_ALIGNED;
+  d.pin = -1;
+  if (p.flags & KG_POD_RESERVE) {
+    if (p.reserve_allocate_policy < KG_RSV_POLICY_DEFAULT || p.reserve_allocate_policy > KG_RSV_POLICY_RESTRICTED)
+      return fail(KG_E_INVALID, "pod %lld: reserve_allocate_policy %lld", (long long)k, (long long)p.reserve_allocate_policy);
+    if (p.reserve_node < 0 || p.reserve_node > INT32_MAX)
+      return fail(KG_E_INVALID, "pod %lld: reserve_node %lld", (long long)k, (long long)p.reserve_node);
+    d.pin = (int32_t)p.reserve_node - 1;
+  }
   d.nterms = (uint32_t)p.n_reservation_terms;
   d.sel = p.reservation_selector;
   for (int t = 0; t < d.nterms; ++t) d.terms[t] = p.reservation_terms[t];
@@ -5442,8 +5452,12 @@ int kg_pods_stage(kg_engine* e, const kg_pod* pods, int64_t n) {
   }
   {  // exact-pass records (the Reservation view of every pod; single-pod calls of any profile use the pass)
     std::vector<RsvPod> hr(std::max<int64_t>(n, 1));
-    for (int64_t k = 0; k < n; ++k)
+    for (int64_t k = 0; k < n; ++k) {
       if (int rc = decode_rsv_pod(pods[k], hr[k], k)) return rc;
+      if ((pods[k].flags & KG_POD_RESERVE) && (e->numa_on || e->ds_on))
+        return fail(KG_E_UNSUPPORTED, "pod %lld: scheduling a reserve pod with NodeNUMAResource / DeviceShare in the "
+                    "profile (their reserve-pod paths keep the Go plugins)", (long long)k);
+    }
     if (int rc = e->rpods.ensure(n + kMaxB)) return rc;
     if (int rc = e->out_rslot.ensure(n + kMaxB)) return rc;
     if (n > 0) HIP_TRY(hipMemcpyAsync(e->rpods.p, hr.data(), n * sizeof(RsvPod), hipMemcpyHostToDevice, e->stream));
@@ -6258,6 +6272,8 @@ int kg_pods_filter_preemption(kg_engine* e, const kg_pod* pod, int32_t node_idx,
   if (d.flags & P_AUX) return fail(KG_E_UNSUPPORTED, "preemption dry run: ephemeral-storage / scalar requests");
   RsvPod rp;
   if (int rc = decode_rsv_pod(*pod, rp, 0)) return rc;
+  if (rp.flags & (RP_RESERVE | RP_OPERATING))
+    return fail(KG_E_UNSUPPORTED, "preemption dry run for a reserve pod / reservation operating mode keeps the Go path");
   std::vector<Victim> hv((size_t)std::max<int64_t>(n_victims, 1));
   for (int64_t k = 0; k < n_victims; ++k) {
     DevPod v;

@@ -37,7 +37,7 @@ namespace kg {
 
 constexpr int kRsvSlots = KG_MAX_RSV_SLOTS;
 constexpr uint32_t RS_AVAIL = 1u << 0, RS_ONCE = 1u << 1, RS_UNSCHED = 1u << 2;  // policy in bits 4..5
-constexpr uint32_t RP_AFFINITY = 1u << 0;
+constexpr uint32_t RP_AFFINITY = 1u << 0, RP_RESERVE = 1u << 1, RP_OPERATING = 1u << 2;
 constexpr int64_t kDefaultMilliCpu = 100, kDefaultMemory = 200ll << 20;  // schedutil.GetNonzeroRequests defaults
 
 struct RsvNode {  // 224 B: one node's slots, read only for nodes with slots (rsv_n[i] > 0)
@@ -49,12 +49,14 @@ struct RsvNode {  // 224 B: one node's slots, read only for nodes with slots (rs
 };
 static_assert(sizeof(RsvNode) == 224, "RsvNode layout");
 
-struct RsvPod {  // 56 B
+struct RsvPod {  // 64 B
   uint64_t owner_mask;  // bit g: the pod matches the owners of owner group g
-  uint32_t flags;
+  uint32_t flags;       // RP_*
   uint32_t nterms;      // required reservation affinity: ReservationSelectorTerms (0 = absent)
   uint64_t sel;         // ReservationSelector predicates (all must hold)
   uint64_t terms[KG_MAX_AFF_TERMS];
+  int32_t policy;       // RP_RESERVE: the reservation's allocate policy; RP_OPERATING: Aligned
+  int32_t pin;          // RP_RESERVE: the node GetReservePodNodeName names (-1 = none)
 };
 
 // RequiredReservationAffinity.Match (pkg/util/reservation/reservation.go:476-489) on a slot's fakeNode labels
@@ -170,7 +172,9 @@ __device__ __forceinline__ void rsv_restore(const RsvNode& rn, int ns, const Rsv
     const uint32_t m = rn.meta[s];
     if (!(m & RS_AVAIL) || ((m & RS_ONCE) && rn.assigned[s] > 0)) continue;  // transformer.go:101-110
     // ReservationInfo.Match → MatchReservationOwners, decoded per owner group into the pod's mask
-    if (((rp.owner_mask >> (rn.owner[s] & 63)) & 1u) && !(m & RS_UNSCHED) && rsv_affinity_match(rp, rn.pred[s]))
+    // a reserve pod matches no reservation (transformer.go:112 isReservedPod)
+    if (!(rp.flags & RP_RESERVE) && ((rp.owner_mask >> (rn.owner[s] & 63)) & 1u) && !(m & RS_UNSCHED) &&
+        rsv_affinity_match(rp, rn.pred[s]))
       mm |= 1u << s;
     else if (rn.assigned[s] > 0) um |= 1u << s;
   }
@@ -241,6 +245,17 @@ __device__ __forceinline__ RsvOut rsv_eval_node(const DevTable& T, const RsvNode
     dbg->pod_req_cpu = has_state ? pr_c : 0, dbg->pod_req_mem = has_state ? pr_m : 0;
   }
   if (dbg && df && !defaults_filter(npd, *df, X.DF)) return o;
+  // Reservation.Filter of a reserve pod / a pod in reservation operating mode (plugin.go:324-350): the reservation's
+  // node, and no available reservation whose allocate policy conflicts (Default coexists with no other policy)
+  if (RP.filter && (rp.flags & (RP_RESERVE | RP_OPERATING))) {
+    if ((rp.flags & RP_RESERVE) && rp.pin >= 0 && i != rp.pin) return o;
+#pragma unroll
+    for (int s = 0; s < kRsvSlots; ++s) {
+      if (s >= ns || !(rn.meta[s] & RS_AVAIL)) continue;
+      const int32_t ps = (int32_t)((rn.meta[s] >> 4) & 3);
+      if ((rp.policy == KG_RSV_POLICY_DEFAULT || ps == KG_RSV_POLICY_DEFAULT) && rp.policy != ps) return o;
+    }
+  }
   int64_t t = 0;
   if (!eval_node(r, p, P, t)) return o;  // NodeResourcesFit + LoadAware on the restored NodeInfo
   // fitsRequest over ephemeral-storage and the scalar resources the pod requests (reservation/plugin.go:469-479)
@@ -264,7 +279,8 @@ __device__ __forceinline__ RsvOut rsv_eval_node(const DevTable& T, const RsvNode
       if (fits) sat |= 1u << s;
     }
   }
-  if (RP.filter && (rp.flags & RP_AFFINITY) && sat == 0) return o;  // plugin.go:361-364, 423-426
+  // plugin.go:361-364, 423-426 (a reserve pod skips this part of the Filter, :357)
+  if (RP.filter && (rp.flags & RP_AFFINITY) && !(rp.flags & RP_RESERVE) && sat == 0) return o;
   int64_t dsraw = 0;
   if (X.ds && dp && !dp->skip) {  // DeviceShare Filter + raw Score (node level: no device-holding reservations)
     if (!ds_eval(X.ds[i], *dp, X.DP, dsraw)) return o;

@@ -122,6 +122,8 @@ def lib():
         L.or_quota_admit.restype = i
         L.or_rsv_case_flat.argtypes = [vp, i64, vp, i64, vp, vp, i, vp, vp]
         L.or_rsv_case_flat.restype = None
+        L.or_rsv_policy_filter.argtypes = [vp, i64, vp]
+        L.or_rsv_policy_filter.restype = i
         L.or_filter_preemption.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, i64, i64]
         L.or_filter_preemption.restype = i64
         for f, res in (("or_taint_filter", i), ("or_taint_count", i64), ("or_affinity_filter", i),

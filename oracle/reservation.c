@@ -44,8 +44,28 @@ static int pod_matches(const kg_pod* pod, const kg_node_reservations* r, int s) 
    * (reservation_info.go:231-236) decoded per owner group — bit g of the pod's mask —, !IsUnschedulable
    * (transformer.go:112), and the pod's required reservation affinity on the slot's labels */
   const int64_t g = r->owner[s];
+  if (pod->flags & KG_POD_RESERVE) return 0; /* isReservedPod: a reserve pod matches no reservation (:112) */
   return g >= 0 && g < KG_MAX_OWNER_GROUPS && (((uint64_t)pod->reservation_owner_mask >> g) & 1u) &&
          !r->unschedulable[s] && affinity_matches(pod, r->predicates[s]);
+}
+
+/* Reservation.Filter of a reserve pod or a pod in reservation operating mode (reservation/plugin.go:324-350): the
+ * reservation's node name, then forEachAvailableReservationOnNode — Default coexists with no other allocate policy
+ * (a reserve pod brings its reservation's policy, operating mode Aligned).  1 = pass. */
+int or_rsv_policy_filter(const kg_pod* pod, int64_t node_idx, const kg_node_reservations* r) {
+  const int reserve = (pod->flags & KG_POD_RESERVE) != 0;
+  if (!reserve && !(pod->reservation_flags & KG_POD_RSV_OPERATING)) return 1;
+  int64_t pol = KG_RSV_POLICY_ALIGNED;
+  if (reserve) {
+    if (pod->reserve_node > 0 && pod->reserve_node - 1 != node_idx) return 0;
+    pol = pod->reserve_allocate_policy;
+  }
+  if (!r) return 1;
+  for (int64_t s = 0; s < r->n; s++) {
+    if (!r->available[s]) continue;
+    if ((pol == KG_RSV_POLICY_DEFAULT || r->policy[s] == KG_RSV_POLICY_DEFAULT) && pol != r->policy[s]) return 0;
+  }
+  return 1;
 }
 
 /* GetNonzeroRequests of the reserve pod (requests = Allocatable): an absent key takes the default */
@@ -159,6 +179,7 @@ int or_rsv_filter_with(const kg_pod* pod, int64_t allowed_pods, const int64_t al
 
 int or_rsv_filter(const kg_pod* pod, int64_t allowed_pods, const int64_t alloc[2], const or_rsv_node* ns,
                   const kg_node_reservations* r) {
+  if (pod->flags & KG_POD_RESERVE) return 1; /* the matched-reservation part skips reserve pods (plugin.go:357) */
   const int required = (pod->reservation_flags & KG_POD_RSV_AFFINITY) != 0;
   if (ns->n_matched == 0 || !ns->has_state) return required ? 0 : 1;
   return or_rsv_filter_with(pod, allowed_pods, alloc, ns, r, ns->matched, ns->n_matched, required);
@@ -361,6 +382,7 @@ int or_schedule_resv_full(const kg_config* cfg, int64_t n_nodes, const kg_node* 
         if (f < 0) { err = f; continue; }
         if (f != 0) continue;
       }
+      if (cfg->reservation_filter && !or_rsv_policy_filter(pod, i, rsv_on ? &rsv[i] : NULL)) continue;
       if (cfg->reservation_filter && !or_rsv_filter(pod, nd->allowed_pods, alloc, &ns, &rsv[i])) continue;
       if (ds_on && cfg->ds_filter && !or_ds_filter(&dev[i], &dsp)) continue;
       /* NodeNUMAResource Filter (nodenumaresource/plugin.go:276-334) on the restored NodeInfo; the reserve pods hold

@@ -42,6 +42,8 @@ int or_rsv_fits_node(const kg_pod* pod, int64_t allowed_pods, const int64_t allo
 int or_rsv_filter_with(const kg_pod* pod, int64_t allowed_pods, const int64_t alloc[2], const or_rsv_node* ns,
                        const kg_node_reservations* r, const int32_t* slots, int n_slots, int required);
 /* Filter for a non-reserve pod (plugin.go:357-378, preemption maps empty). */
+/* (ABI 12) Reservation.Filter of a reserve pod / reservation operating mode (plugin.go:324-350): 1 = pass */
+int or_rsv_policy_filter(const kg_pod* pod, int64_t node_idx, const kg_node_reservations* r);
 int or_rsv_filter(const kg_pod* pod, int64_t allowed_pods, const int64_t alloc[2], const or_rsv_node* ns,
                   const kg_node_reservations* r);
 /* scoreReservation (scoring.go:183-203) of slot s. */
