@@ -417,6 +417,8 @@ typedef struct kg_node_reservations {
   uint64_t predicates[KG_MAX_RSV_SLOTS];       /* (ABI 12) the caller's predicate bits over the node's labels  */
                                                /* overlaid with the reservation's (matchReservation's fakeNode, */
                                                /* transformer.go:357-369); read for reservation-affinity pods    */
+  int64_t predicate_count;                     /* predicate ids decided in `predicates` (as node rows, ABI 11): */
+                                               /* a queue using a later id is refused until the slots are re-sent */
 } kg_node_reservations;
 
 /* One ElasticQuota as the plugin's PreFilter snapshot sees it (plugin.go:211-256) over KG_QUOTA_RES resources: cpu

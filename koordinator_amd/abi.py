@@ -166,7 +166,8 @@ NODE_PRED_DTYPE = np.dtype([("predicates", np.uint64), ("taints_hard", np.uint64
 
 NODE_RSV_DTYPE = np.dtype([_i64("n")] + [_i64(f, MAX_RSV_SLOTS) for f in (
     "owner", "allocatable_cpu", "allocatable_mem", "allocated_cpu", "allocated_mem", "assigned", "order", "policy",
-    "allocate_once", "available", "unschedulable")] + [("predicates", np.uint64, (MAX_RSV_SLOTS,))])
+    "allocate_once", "available", "unschedulable")] + [("predicates", np.uint64, (MAX_RSV_SLOTS,)),
+                                                        _i64("predicate_count")])
 
 QUOTA_DTYPE = np.dtype([_i64("used", QUOTA_RES), _i64("non_preemptible_used", QUOTA_RES), _i64("used_limit", QUOTA_RES),
                         _i64("min", QUOTA_RES)])

@@ -3142,6 +3142,9 @@ struct kg_engine {
   bool np_dirty = true;
   int64_t np_taint_top_max = 0, np_pred_cnt_min = 64, np_img_cnt_min = 64;
   int64_t sq_taint_min = 64, sq_pred_top = 0, sq_img_top = 0;
+  std::vector<int16_t> rsv_pcnt;                // (ABI 12) per node: predicates its slots were compiled against (64: no slots)
+  int64_t rsv_pcnt_min = 64, sq_rsv_top = 0;    // min over the nodes; the staged reservation affinities' top id + 1
+  bool rsv_pdirty = false;
   DevBuf<DefPod> defpods;       // [staged + kMaxB]
   DevBuf<uint32_t> rsv_val2;    // [cap] raw taint count << 24 | raw affinity sum (their Scores on)
   // (ABI 12) PodTopologySpread / InterPodAffinity, hostname key (groups_dev.h): one pod per exact pass
@@ -4620,6 +4623,8 @@ int run_xr(kg_engine* e, int64_t first, int64_t count, kg_stats* stats, double t
 int decode_node_rsv(const kg_node_reservations& r, RsvNode& d, int32_t& ns) {
   std::memset(&d, 0, sizeof(d));
   if (r.n < 0 || r.n > KG_MAX_RSV_SLOTS) return fail(KG_E_INVALID, "reservation slot count %lld", (long long)r.n);
+  if (r.predicate_count < 0 || r.predicate_count > 64)
+    return fail(KG_E_INVALID, "reservation predicate_count %lld outside [0, 64]", (long long)r.predicate_count);
   ns = (int32_t)r.n;
   for (int s = 0; s < ns; ++s) {
     if (r.allocatable_cpu[s] < 0 || r.allocatable_mem[s] < 0 || r.allocatable_cpu[s] > (int64_t(1) << 40) ||
@@ -4644,6 +4649,14 @@ int decode_node_rsv(const kg_node_reservations& r, RsvNode& d, int32_t& ns) {
     d.pred[s] = r.predicates[s];
   }
   return 0;
+}
+
+// 1 + the highest predicate id a pod's reservation affinity uses (0: none)
+int64_t rsv_pred_top(const RsvPod& d) {
+  if (!(d.flags & RP_AFFINITY) || (d.flags & RP_RESERVE)) return 0;
+  uint64_t used = d.sel;
+  for (uint32_t t = 0; t < d.nterms; ++t) used |= d.terms[t];
+  return used ? 64 - __builtin_clzll(used) : 0;
 }
 
 // the Reservation view of one pod: owner groups, the required-affinity flag and (ABI 12) its selector / terms
@@ -5452,12 +5465,15 @@ int kg_pods_stage(kg_engine* e, const kg_pod* pods, int64_t n) {
   }
   {  // exact-pass records (the Reservation view of every pod; single-pod calls of any profile use the pass)
     std::vector<RsvPod> hr(std::max<int64_t>(n, 1));
+    int64_t rtop = 0;
     for (int64_t k = 0; k < n; ++k) {
       if (int rc = decode_rsv_pod(pods[k], hr[k], k)) return rc;
+      rtop = std::max<int64_t>(rtop, rsv_pred_top(hr[k]));
       if ((pods[k].flags & KG_POD_RESERVE) && (e->numa_on || e->ds_on))
         return fail(KG_E_UNSUPPORTED, "pod %lld: scheduling a reserve pod with NodeNUMAResource / DeviceShare in the "
                     "profile (their reserve-pod paths keep the Go plugins)", (long long)k);
     }
+    e->sq_rsv_top = rtop;
     if (int rc = e->rpods.ensure(n + kMaxB)) return rc;
     if (int rc = e->out_rslot.ensure(n + kMaxB)) return rc;
     if (n > 0) HIP_TRY(hipMemcpyAsync(e->rpods.p, hr.data(), n * sizeof(RsvPod), hipMemcpyHostToDevice, e->stream));
@@ -5523,11 +5539,29 @@ static int check_predicate_tables(kg_engine* e) {
   return 0;
 }
 
+// (ABI 12) the same rule for the reservation slots' fakeNode predicates (kg_node_reservations.predicate_count)
+static int check_rsv_predicates(kg_engine* e, int64_t top) {
+  if (top == 0) return 0;
+  if (e->rsv_pdirty) {
+    int64_t pc = 64;
+    for (int64_t i = 0; i < std::min<int64_t>(e->n_nodes, (int64_t)e->rsv_pcnt.size()); ++i)
+      pc = std::min<int64_t>(pc, e->rsv_pcnt[i]);
+    e->rsv_pcnt_min = pc;
+    e->rsv_pdirty = false;
+  }
+  if (top > e->rsv_pcnt_min)
+    return fail(KG_E_INVALID, "Reservation affinity: a pod uses predicate %lld but reservation slots were compiled "
+                "against %lld predicates: re-send the reservations", (long long)top - 1, (long long)e->rsv_pcnt_min);
+  return 0;
+}
+
 static int schedule_staged_impl(kg_engine* e, int64_t first, int64_t count, kg_stats* stats) {
   if (!e) return fail(KG_E_INVALID, "engine is NULL");
   if (first < 0 || count < 0 || first + count > e->n_staged) return fail(KG_E_INVALID, "staged range");
   if (count > 0)
     if (int rc = check_predicate_tables(e)) return rc;
+  if (count > 0)
+    if (int rc = check_rsv_predicates(e, e->sq_rsv_top)) return rc;
   const double t0 = now_s();
   // the exact per-pod pass: its profiles, and calls of at most kExactSmall pods of any profile (the drop-in's per-pod
   // scheduleOne): one pass costs less than a round's eval + merge + resolve when a round would hold one pod
@@ -6163,6 +6197,9 @@ int kg_nodes_reservation_upsert(kg_engine* e, const kg_node_reservations* r, con
     if (idx[k] < 0 || idx[k] >= e->capacity) return fail(KG_E_INVALID, "node index %d outside capacity", idx[k]);
     if (int rc = decode_node_rsv(r[k], h[k], hn[k])) return rc;
   }
+  if ((int64_t)e->rsv_pcnt.size() < e->capacity) e->rsv_pcnt.assign(e->capacity, 64);
+  for (int64_t k = 0; k < n; ++k) e->rsv_pcnt[idx[k]] = (int16_t)(r[k].n > 0 ? r[k].predicate_count : 64);
+  e->rsv_pdirty = true;
   DevBuf<uint8_t> b;
   if (int rc = b.ensure(n * (sizeof(RsvNode) + 8))) return rc;
   RsvNode* dd = reinterpret_cast<RsvNode*>(b.p);
@@ -6226,6 +6263,7 @@ int kg_pods_evaluate_reservation(kg_engine* e, const kg_pod* pod, int64_t* out) 
   if (int rc = decode_pod(e, *pod, d)) return rc;
   RsvPod rp;
   if (int rc = decode_rsv_pod(*pod, rp, 0)) return rc;
+  if (int rc = check_rsv_predicates(e, rsv_pred_top(rp))) return rc;
   DsPod dsp{};
   dsp.skip = 1;
   if (e->ds_on)

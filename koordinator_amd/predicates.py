@@ -204,7 +204,9 @@ class PredicateTable:
                                reservation_name: str = "") -> int:
         """kg_node_reservations.predicates of one slot: the predicate bits over matchReservation's fakeNode — named
         after the reservation, the node's labels overlaid with the reservation's.  Like node rows, a slot decides the
-        predicates interned before it: intern the queue's reservation affinities first, or re-send the slots."""
+        predicates interned before it: intern the queue's reservation affinities first, set the row's
+        predicate_count to len(self.preds), and re-send the slots after the table grows (the engine refuses a queue
+        using a later predicate)."""
         labels = dict(node_labels or {})
         labels.update(reservation_labels or {})
         m = 0

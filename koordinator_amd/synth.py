@@ -424,6 +424,7 @@ def add_reservation_affinity(rsv: np.ndarray, pods: np.ndarray, seed: int = BASE
             if rng.random() < 0.2:
                 labels[ZONE] = "z-pinned"
             rsv["predicates"][i, s] = t.reservation_predicates(node_labels, labels, f"r-{i}-{s}")
+        rsv["predicate_count"][i] = len(t.preds)  # ABI 12: the predicates the slots were compiled against
 
 
 def load_rsv_into(engine, cluster: Cluster, rsv: np.ndarray):

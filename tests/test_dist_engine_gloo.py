@@ -38,9 +38,23 @@ SHIPPED_PROFILE = F.Profile(filter=(F.NODE_RESOURCES_FIT, F.LOAD_AWARE, F.NODE_N
                                    F.DEVICE_SHARE: 1, F.RESERVATION: 5000})
 
 
+STOCK_PROFILE = F.Profile(filter=(F.NODE_RESOURCES_FIT, F.LOAD_AWARE, F.TAINT_TOLERATION, F.NODE_AFFINITY,
+                                  F.POD_TOPOLOGY_SPREAD, F.INTER_POD_AFFINITY),
+                          score={F.NODE_RESOURCES_FIT: 1, F.LOAD_AWARE: 1, F.TAINT_TOLERATION: 1, F.NODE_AFFINITY: 1,
+                                 F.BALANCED_ALLOCATION: 1, F.POD_TOPOLOGY_SPREAD: 2, F.INTER_POD_AFFINITY: 1})
+
+
 def _exact_case(kind):
-    """(r4) the exact profiles, which run as replicas on every rank: Reservation, and the shipped profile
-    (NUMA + DeviceShare + Reservation + ElasticQuota)."""
+    """(r4) the exact profiles, which run as replicas on every rank: Reservation, the shipped profile
+    (NUMA + DeviceShare + Reservation + ElasticQuota), and the upstream defaults with hostname / zone
+    PodTopologySpread and InterPodAffinity (the per-pod pass)."""
+    if kind == "stock":
+        cfg = F.build_config(profile=STOCK_PROFILE)
+        cluster = synth.make_cluster(800, seed=981)
+        synth.make_pod_groups(cluster.existing_pods, seed=984, zones=True)
+        pods = synth.make_pod_groups(synth.make_pods(300, seed=982), seed=985, zones=True)
+        preds = synth.make_predicates(800, pods, seed=983, no_zone=0.05)[1]
+        return cfg, dict(cluster=cluster, pods=pods, preds=preds)
     if kind == "rsv":
         cfg = F.build_config(profile=RSV_PROFILE)
         cluster, rsv = synth.make_rsv_cluster(1500, seed=961)
@@ -83,12 +97,15 @@ def _rank_main(rank, world, port, kind, out_dir):
             return torch.cat(parts).numpy()
 
         ex = HostExchange(allgather)
-        if kind in ("rsv", "shipped"):
+        if kind in ("rsv", "shipped", "stock"):
             cfg, w = _exact_case(kind)
             cluster, pods = w["cluster"], w["pods"]
             with Engine(cfg, cluster.n, rank=rank, n_ranks=world, exchange=ex) as e:
                 if kind == "rsv":
                     synth.load_rsv_into(e, cluster, w["rsv"])
+                elif kind == "stock":
+                    synth.load_into(e, cluster)
+                    e.upsert_predicates(w["preds"])
                 else:
                     synth.load_shipped_into(e, cluster, w["numa"], w["dev"], w["rsv"], w["quotas"])
                 e.stage(pods)
@@ -150,7 +167,7 @@ def test_two_process_gloo_engine(tmp_path, kind):
     assert (want >= 0).mean() > 0.3
 
 
-@pytest.mark.parametrize("kind", ["rsv", "shipped"])
+@pytest.mark.parametrize("kind", ["rsv", "shipped", "stock"])
 def test_two_process_gloo_exact_profiles(tmp_path, kind):
     """The exact profiles on two ranks: every rank a full replica resolving the same FIFO order with no exchange
      — both ranks' placements, totals, reservation slots and node state equal the oracle's."""
@@ -160,7 +177,11 @@ def test_two_process_gloo_exact_profiles(tmp_path, kind):
     cluster, pods = w["cluster"], w["pods"]
     st = oracle.states(cluster.n)
     oracle.add_pods(cfg, st, cluster.existing_pods, cluster.existing_node)
-    if kind == "rsv":
+    if kind == "stock":
+        g = oracle.groups_init(cluster.n, cluster.existing_pods, cluster.existing_node)
+        want, want_score, want_slot = oracle.schedule_resv(cfg, cluster.nodes, cluster.metrics, st, None, pods,
+                                                           cluster.now_ns, n_threads=8, preds=w["preds"], groups=g)
+    elif kind == "rsv":
         want, want_score, want_slot = oracle.schedule_resv(cfg, cluster.nodes, cluster.metrics, st, w["rsv"].copy(),
                                                            pods, cluster.now_ns, n_threads=8)
     else:

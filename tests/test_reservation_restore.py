@@ -58,6 +58,7 @@ def _case(c):
     if table is not None:
         for s, labels in enumerate(c["slot_labels"]):
             slots[0]["predicates"][s] = table.reservation_predicates(c.get("node_labels"), labels, f"r{s}")
+        slots[0]["predicate_count"] = len(table.preds)
     return pod, slots
 
 

@@ -118,3 +118,21 @@ def test_reserve_pods_device_matches_oracle(seed):
     cluster, rsv, pods, res = _mixed_world(seed)
     node, slot = check(F.build_config(profile=PROFILE), cluster, rsv, pods, chunks=2)
     assert (node[res] >= 0).any() and (slot[res] == -1).all()
+
+
+@pytest.mark.gpu
+def test_reservation_affinity_refused_against_older_slots():
+    """(ABI 12) A queue whose reservation affinity uses a predicate the slots were not compiled against is refused
+    (kg_node_reservations.predicate_count, like the node rows' ABI 11 check)."""
+    from koordinator_amd.predicates import PredicateTable
+    cluster, rsv = synth.make_rsv_cluster(50, seed=5)
+    pods = synth.make_rsv_pods(20, seed=6)
+    t = PredicateTable()
+    pods["reservation_flags"] = abi.POD_RSV_AFFINITY
+    t.fill_reservation_affinity(pods[0:1], selector={"reservation-type": "a"})
+    rsv["predicate_count"] = 0  # compiled before the predicate existed
+    with Engine(F.build_config(profile=PROFILE), cluster.n) as e:
+        synth.load_rsv_into(e, cluster, rsv)
+        e.stage(pods)
+        with pytest.raises(abi.KoordGPUError, match="re-send the reservations"):
+            e.schedule_staged(0, len(pods))
