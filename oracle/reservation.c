@@ -209,6 +209,7 @@ int64_t or_rsv_node_order(const or_rsv_node* ns, const kg_node_reservations* r) 
 
 int or_rsv_nominate(const kg_pod* pod, int64_t allowed_pods, const int64_t alloc[2], const or_rsv_node* ns,
                     const kg_node_reservations* r) {
+  if (pod->flags & KG_POD_RESERVE) return -1; /* NominateReservation: none for a reserve pod (nominator.go:77) */
   if (!ns->has_state || ns->n_matched == 0) return -1;
   int32_t cand[KG_MAX_RSV_SLOTS];
   int n = 0;

@@ -56,6 +56,12 @@ CASES = [
 # listed reservation; node Status empty, pod 2C4G (`reservations` order = slot order).  "reserve pod" (:169) is out of
 # scope: reserve pods themselves are scheduled on the Go path.
 CASES += [
+    dict(ref="nominator_test.go:110 reserve pod", pod=[0, 0], slots=[], has_state=0, **EMPTY_NODE, want_nominated=-1,
+         reserve=1),
+    # derived from nominator.go:77 (a reserve pod nominates nothing) with the :253 reservations on the node: not a
+    # reference table row
+    dict(ref="nominator.go:77 reserve pod beside matching reservations (derived)", pod=[2000, 4 * GI],
+         slots=[R4C8G, R2C4G], has_state=1, **EMPTY_NODE, want_nominated=-1, reserve=1),
     dict(ref="nominator_test.go:121 node without reservations", pod=[2000, 4 * GI], slots=[], has_state=0, **EMPTY_NODE,
          want_nominated=-1),
     dict(ref="nominator_test.go:126 preferred reservation", pod=[2000, 4 * GI],
@@ -110,8 +116,6 @@ if __name__ == "__main__":
     with open(out, "w") as f:
         json.dump({"source": "hhyasdf/koordinator pkg/scheduler/plugins/reservation tests", "cases": CASES,
                    "restore": RESTORE,
-                   "skipped": [{"ref": "nominator_test.go:110 reserve pod",
-                                "reason": "scheduling a reserve pod stays on the Go path"},
-                               ]},
+                   "skipped": []},
                   f, indent=1)
     print(f"wrote {len(CASES)} cases to {out}")

@@ -29,6 +29,8 @@ def test_reservation_golden(case):
     pod["requests"][0], pod["requests"][1] = case["pod"]
     pod["reservation_owner_mask"] = 1
     pod["reservation_flags"] = abi.POD_RSV_AFFINITY if case.get("affinity") else 0
+    if case.get("reserve"):
+        pod["flags"] |= abi.POD_RESERVE
     ok, nom, score = oracle.rsv_case(pod, case["allowed_pods"], case["alloc"], case["num_pods"],
                                      case["pod_requested"], case["r_allocated"], case["has_state"],
                                      rsv_row(case["slots"]))

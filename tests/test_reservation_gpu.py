@@ -103,4 +103,6 @@ def test_golden_cases_place_like_the_oracle(case):
     pod["priority_class"] = abi.PRIO_PROD
     pod["reservation_owner_mask"] = 1
     pod["reservation_flags"] = abi.POD_RSV_AFFINITY if case.get("affinity") else 0
+    if case.get("reserve"):
+        pod["flags"] |= abi.POD_RESERVE
     check(F.build_config(profile=PROFILE), cluster, rsv, pod)

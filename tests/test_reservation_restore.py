@@ -110,6 +110,8 @@ def test_nominate_device(c):
         e.upsert_reservations(_slots(slots))
         pod = F.make_pod({"cpu": f"{c['pod'][0]}m", "memory": str(c["pod"][1])})
         pod["reservation_owner_mask"] = 1
+        if c.get("reserve"):
+            pod["flags"] |= abi.POD_RESERVE
         ev = e.evaluate_reservation(pod)
     assert int(ev["nominated"][0]) == c["want_nominated"], c["ref"]
 
