@@ -385,14 +385,14 @@ def main():
         # ~4 group counters, and the 8 + 4 + 8 B of values it writes
         algo = n_local * (B_NODE + 32.0 + 16.0 + 20.0)
     elif rsv_path:  # the exact wide pass (xr_eval, live time folded under "rsv_eval"): one launch scores the round's
-        # pods (kXrPods = 32, or fewer) against every node.  Per launch: the node columns + rsv_n once, the 224-B slot
+        # pods (kXrPods = 32, or fewer) against every node.  Per launch: the node columns + rsv_n once, the 192-B slot
         # rows of nodes holding reservations, the 272-B GPU row per node when the round has device pods, the NUMA rows
         # (NumaStatic 144 B + NodeAllocation 104 B), and per (pod, node) the 8-B packed value (+ 4-B NUMA affinity)
         ev = live.get("rsv_eval", {})
         pods_per_launch = (n_prof / ev["launches"]) if ev.get("launches") else 1.0
         prof_pods = pods[total:total + n_prof] if n_prof > 0 else pods[:1]
         has_dev = work.devices is not None and bool(prof_pods["device_requests"].any())
-        algo = n_local * (B_NODE + 4) + int((work.rsv["n"] > 0).sum()) * 224.0 + (n_local * 272.0 if has_dev else 0.0)
+        algo = n_local * (B_NODE + 4) + int((work.rsv["n"] > 0).sum()) * 192.0 + (n_local * 272.0 if has_dev else 0.0)
         algo += pods_per_launch * n_local * 8.0
         if work.numa is not None:
             algo += n_local * (144.0 + 104.0) + pods_per_launch * n_local * 4.0

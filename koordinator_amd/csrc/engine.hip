@@ -2612,7 +2612,7 @@ struct Victim {
   int32_t nonzero;  // !quotav1.IsZero(PodRequestsAndLimits): RemovePod records it
 };
 __global__ void filter_pod_preempt(DevTable T, const RsvNode* __restrict__ RN, const int32_t* __restrict__ rsv_n,
-                                   int64_t i, const DevPod* __restrict__ pod, RsvPod rp, EvalParams P, RsvParams RP,
+                                   const uint64_t* __restrict__ rsv_pred, int64_t i, const DevPod* __restrict__ pod, RsvPod rp, EvalParams P, RsvParams RP,
                                    int rsv_on, const Victim* __restrict__ vic, int64_t n_vic, int32_t* __restrict__ out) {
   if (blockIdx.x != 0 || threadIdx.x != 0) return;
   const DevPod p = *pod;
@@ -2629,7 +2629,7 @@ __global__ void filter_pod_preempt(DevTable T, const RsvNode* __restrict__ RN, c
   RsvNode rn;
   if (ns > 0) {
     rn = RN[i];
-    rsv_restore(rn, ns, rp, r, mm, nm, pr_c, pr_m, ra_c, ra_m, has_state);
+    rsv_restore(rn, ns, rp, rsv_pred + (size_t)i * kRsvSlots, r, mm, nm, pr_c, pr_m, ra_c, ra_m, has_state);
   }
   int64_t pre_c = 0, pre_m = 0, rr_c[kRsvSlots] = {}, rr_m[kRsvSlots] = {};
   bool pre_set = false;
@@ -3118,6 +3118,7 @@ struct kg_engine {
   DevBuf<uint32_t> numa_aff;  // exact pass: the NUMA affinity Filter stored per node for the pass's pod
   RsvParams RP{};
   DevBuf<RsvNode> rsv_d;
+  DevBuf<uint64_t> rsv_pd;      // [cap][kRsvSlots] (ABI 12) the slots' fakeNode predicates
   DevBuf<int32_t> rsv_nd;       // slots in use per node
   DevBuf<RsvPod> rpods;
   DevBuf<int32_t> out_rslot;    // [staged + kMaxB]
@@ -4380,6 +4381,7 @@ RsvExt rsv_ext(kg_engine* e) {
   X.gval = e->gval.p;
   X.gz = e->gz.p;
   X.gzm = e->gzm.p;
+  X.rsv_pred = e->rsv_pd.p;
   return X;
 }
 
@@ -4646,7 +4648,6 @@ int decode_node_rsv(const kg_node_reservations& r, RsvNode& d, int32_t& ns) {
     d.order[s] = (int32_t)r.order[s];
     d.meta[s] = (r.available[s] ? RS_AVAIL : 0u) | (r.allocate_once[s] ? RS_ONCE : 0u) |
                 (r.unschedulable[s] ? RS_UNSCHED : 0u) | ((uint32_t)r.policy[s] << 4);
-    d.pred[s] = r.predicates[s];
   }
   return 0;
 }
@@ -4929,10 +4930,12 @@ static int engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank,
       if (int rc = e->numa_aff.ensure(cap)) return bail(rc);
     if (int rc = e->rsv_d.ensure(cap)) return bail(rc);
     if (int rc = e->rsv_nd.ensure(cap)) return bail(rc);
+    if (int rc = e->rsv_pd.ensure((size_t)kRsvSlots * cap)) return bail(rc);
     if (int rc = e->rsv_val.ensure(cap)) return bail(rc);
     if (int rc = e->rsv_ws.ensure(8)) return bail(rc);
     if (int rc = e->rsv_part.ensure(15 * ((cap + kRsvThreads - 1) / kRsvThreads) + 4)) return bail(rc);
-    if (hipMemsetAsync(e->rsv_nd.p, 0, cap * 4, e->stream) != hipSuccess || hipMemsetAsync(e->rsv_ws.p, 0, 64, e->stream) != hipSuccess)
+    if (hipMemsetAsync(e->rsv_nd.p, 0, cap * 4, e->stream) != hipSuccess || hipMemsetAsync(e->rsv_ws.p, 0, 64, e->stream) != hipSuccess ||
+        hipMemsetAsync(e->rsv_pd.p, 0, (size_t)kRsvSlots * cap * 8, e->stream) != hipSuccess)
       return bail(fail(KG_E_DEVICE, "hipMemset"));
   }
   {
@@ -5150,6 +5153,7 @@ void kg_engine_destroy(kg_engine* e) {
   e->dsval.release();
   e->rsv_d.release();
   e->rsv_nd.release();
+  e->rsv_pd.release();
   e->rpods.release();
   e->out_rslot.release();
   e->rsv_val.release();
@@ -5899,7 +5903,7 @@ int kg_quotas_read(kg_engine* e, kg_quota* out, int64_t n) {
 // Reservation profile: which 0 = rsv_eval, 1 = rsv_select, replayed on the first staged pod (neither kernel
 // changes node state; the cursor words are reset afterwards).  Algorithmic bytes of rsv_eval per launch: SURVEY
 // §8d's 76 B of Fit + LoadAware columns per node, the 4-B slot count and the 8-B packed value written, plus the
-// 224-B slot record of every node that has reservations; rsv_select reads the 8-B packed value per node.
+// 192-B slot record of every node that has reservations; rsv_select reads the 8-B packed value per node.
 static int bench_rsv(kg_engine* e, int which, int iters, double* avg_ms, double* algo_bytes) {
   if (iters <= 0 || which < 0 || which > 1) return fail(KG_E_INVALID, "bad argument");
   if (e->n_staged <= 0) return fail(KG_E_INVALID, "stage a pod queue first");
@@ -6200,15 +6204,22 @@ int kg_nodes_reservation_upsert(kg_engine* e, const kg_node_reservations* r, con
   if ((int64_t)e->rsv_pcnt.size() < e->capacity) e->rsv_pcnt.assign(e->capacity, 64);
   for (int64_t k = 0; k < n; ++k) e->rsv_pcnt[idx[k]] = (int16_t)(r[k].n > 0 ? r[k].predicate_count : 64);
   e->rsv_pdirty = true;
+  std::vector<uint64_t> hp((size_t)n * kRsvSlots);
+  for (int64_t k = 0; k < n; ++k)
+    for (int s = 0; s < kRsvSlots; ++s) hp[(size_t)k * kRsvSlots + s] = s < r[k].n ? r[k].predicates[s] : 0;
   DevBuf<uint8_t> b;
-  if (int rc = b.ensure(n * (sizeof(RsvNode) + 8))) return rc;
-  RsvNode* dd = reinterpret_cast<RsvNode*>(b.p);
-  int32_t* dn = reinterpret_cast<int32_t*>(b.p + n * sizeof(RsvNode));
+  const size_t pb = (size_t)n * kRsvSlots * 8;
+  if (int rc = b.ensure(pb + n * (sizeof(RsvNode) + 8))) return rc;
+  uint64_t* dp = reinterpret_cast<uint64_t*>(b.p);
+  RsvNode* dd = reinterpret_cast<RsvNode*>(b.p + pb);
+  int32_t* dn = reinterpret_cast<int32_t*>(b.p + pb + n * sizeof(RsvNode));
   int32_t* di = dn + n;
+  HIP_TRY(hipMemcpyAsync(dp, hp.data(), pb, hipMemcpyHostToDevice, e->stream));
   HIP_TRY(hipMemcpyAsync(dd, h.data(), n * sizeof(RsvNode), hipMemcpyHostToDevice, e->stream));
   HIP_TRY(hipMemcpyAsync(dn, hn.data(), n * 4, hipMemcpyHostToDevice, e->stream));
   HIP_TRY(hipMemcpyAsync(di, idx, n * 4, hipMemcpyHostToDevice, e->stream));
-  scatter_rsv<<<(unsigned)((n + 255) / 256), 256, 0, e->stream>>>(e->rsv_d.p, e->rsv_nd.p, dd, dn, di, n);
+  scatter_rsv<<<(unsigned)((n + 255) / 256), 256, 0, e->stream>>>(e->rsv_d.p, e->rsv_nd.p, e->rsv_pd.p, dd, dn, dp, di,
+                                                                  n);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(e->stream));
   b.release();
@@ -6329,7 +6340,7 @@ int kg_pods_filter_preemption(kg_engine* e, const kg_pod* pod, int32_t node_idx,
   int32_t* go = reinterpret_cast<int32_t*>(e->scratch64.p + kPodWords + vw);
   HIP_TRY(hipMemcpyAsync(gp, &d, sizeof(d), hipMemcpyHostToDevice, e->stream));
   if (n_victims > 0) HIP_TRY(hipMemcpyAsync(gv, hv.data(), (size_t)n_victims * sizeof(Victim), hipMemcpyHostToDevice, e->stream));
-  filter_pod_preempt<<<1, kWave, 0, e->stream>>>(e->T, e->rsv_d.p, e->rsv_nd.p, node_idx, gp, rp, e->P, e->RP,
+  filter_pod_preempt<<<1, kWave, 0, e->stream>>>(e->T, e->rsv_d.p, e->rsv_nd.p, e->rsv_pd.p, node_idx, gp, rp, e->P, e->RP,
                                                  e->rsv_on ? 1 : 0, gv, n_victims, go);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpyAsync(out_reject, go, 4, hipMemcpyDeviceToHost, e->stream));

@@ -40,14 +40,15 @@ constexpr uint32_t RS_AVAIL = 1u << 0, RS_ONCE = 1u << 1, RS_UNSCHED = 1u << 2; 
 constexpr uint32_t RP_AFFINITY = 1u << 0, RP_RESERVE = 1u << 1, RP_OPERATING = 1u << 2;
 constexpr int64_t kDefaultMilliCpu = 100, kDefaultMemory = 200ll << 20;  // schedutil.GetNonzeroRequests defaults
 
-struct RsvNode {  // 224 B: one node's slots, read only for nodes with slots (rsv_n[i] > 0)
+struct RsvNode {  // 192 B: one node's slots, read only for nodes with slots (rsv_n[i] > 0)
   int64_t alloc_cpu[kRsvSlots], alloc_mem[kRsvSlots];    // ReservationInfo.Allocatable (0 = key absent)
   int64_t allocd_cpu[kRsvSlots], allocd_mem[kRsvSlots];  // ReservationInfo.Allocated
   int32_t owner[kRsvSlots], assigned[kRsvSlots], order[kRsvSlots];  // owner group 0..63
   uint32_t meta[kRsvSlots];
-  uint64_t pred[kRsvSlots];  // predicate bits over the node's labels overlaid with the reservation's
 };
-static_assert(sizeof(RsvNode) == 224, "RsvNode layout");
+static_assert(sizeof(RsvNode) == 192, "RsvNode layout");
+// (ABI 12) the slots' fakeNode predicate bits live in their own [cap][kRsvSlots] array (RsvExt::rsv_pred), read only
+// for a pod whose reservation affinity has a selector or terms: the slot record the resolvers copy stays 192 B
 
 struct RsvPod {  // 64 B
   uint64_t owner_mask;  // bit g: the pod matches the owners of owner group g
@@ -105,6 +106,7 @@ struct RsvExt {
   const double* __restrict__ logw;     // [cap + 1]: log(F + 2), the host's libm
   uint64_t* __restrict__ gval;         // [cap] InterPodAffinity raw << 32 | PodTopologySpread raw (+ 2^31; 0 = ignored)
   int32_t* __restrict__ gz;            // [2 parities][kZoneSumWords] the zone sums (ZoneSums)
+  const uint64_t* __restrict__ rsv_pred;  // [cap][kRsvSlots] the slots' fakeNode predicates (reservation affinity)
   uint64_t* __restrict__ gzm;          // [2 parities] the present zones
 };
 // pod j's zone sums (double-buffered by parity: group_pre(j) accumulates, rsv_select(j) clears j + 1's)
@@ -162,7 +164,8 @@ struct RsvDbg {
 // BeforePreFilter's restore of one node for one pod (transformer.go:100-189): the matched slots' reserve pods leave
 // NodeInfo (restoreMatchedReservation :240-263), the unmatched assigned ones leave and return as their remainders
 // (restoreUnmatchedReservations :265-291); pr_* = nodeReservationState.podRequested, ra_* = Σ matched Allocated.
-__device__ __forceinline__ void rsv_restore(const RsvNode& rn, int ns, const RsvPod& rp, Row& r, uint32_t& mm, int& nm,
+__device__ __forceinline__ void rsv_restore(const RsvNode& rn, int ns, const RsvPod& rp, const uint64_t* pred_row,
+                                            Row& r, uint32_t& mm, int& nm,
                                             int64_t& pr_c, int64_t& pr_m, int64_t& ra_c, int64_t& ra_m,
                                             bool& has_state) {
   uint32_t um = 0;
@@ -174,7 +177,8 @@ __device__ __forceinline__ void rsv_restore(const RsvNode& rn, int ns, const Rsv
     // ReservationInfo.Match → MatchReservationOwners, decoded per owner group into the pod's mask
     // a reserve pod matches no reservation (transformer.go:112 isReservedPod)
     if (!(rp.flags & RP_RESERVE) && ((rp.owner_mask >> (rn.owner[s] & 63)) & 1u) && !(m & RS_UNSCHED) &&
-        rsv_affinity_match(rp, rn.pred[s]))
+        (!(rp.flags & RP_AFFINITY) || (rp.sel == 0 && rp.nterms == 0) ||
+         rsv_affinity_match(rp, pred_row ? pred_row[s] : 0ull)))
       mm |= 1u << s;
     else if (rn.assigned[s] > 0) um |= 1u << s;
   }
@@ -236,7 +240,9 @@ __device__ __forceinline__ RsvOut rsv_eval_node(const DevTable& T, const RsvNode
   RsvNode rn_copy;
   if (kSlotsInRegs && ns > 0) rn_copy = RN[i];
   const RsvNode& rn = kSlotsInRegs ? rn_copy : RN[i];
-  if (ns > 0) rsv_restore(rn, ns, rp, r, mm, nm, pr_c, pr_m, ra_c, ra_m, has_state);
+  if (ns > 0)
+    rsv_restore(rn, ns, rp, X.rsv_pred ? X.rsv_pred + (size_t)i * kRsvSlots : nullptr, r, mm, nm, pr_c, pr_m, ra_c,
+                ra_m, has_state);
   if (dbg) {
     dbg->matched = mm;
     dbg->has_state = has_state ? 1 : 0;
@@ -929,12 +935,15 @@ __global__ __launch_bounds__(kWave) void rsv_apply(DevTable T, RsvNode* __restri
   ws[3] = (unsigned long long)(base + g_last + 1);
 }
 
-__global__ void scatter_rsv(RsvNode* __restrict__ RN, int32_t* __restrict__ rsv_n, const RsvNode* __restrict__ s,
-                            const int32_t* __restrict__ ns, const int32_t* __restrict__ idx, int64_t n) {
+__global__ void scatter_rsv(RsvNode* __restrict__ RN, int32_t* __restrict__ rsv_n, uint64_t* __restrict__ pred,
+                            const RsvNode* __restrict__ s, const int32_t* __restrict__ ns,
+                            const uint64_t* __restrict__ sp, const int32_t* __restrict__ idx, int64_t n) {
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= n) return;
   RN[idx[k]] = s[k];
   rsv_n[idx[k]] = ns[k];
+#pragma unroll
+  for (int q = 0; q < kRsvSlots; ++q) pred[(size_t)idx[k] * kRsvSlots + q] = sp[(size_t)k * kRsvSlots + q];
 }
 
 }  // namespace kg
