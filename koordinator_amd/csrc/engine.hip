@@ -2612,7 +2612,7 @@ struct Victim {
   int32_t nonzero;  // !quotav1.IsZero(PodRequestsAndLimits): RemovePod records it
 };
 __global__ void filter_pod_preempt(DevTable T, const RsvNode* __restrict__ RN, const int32_t* __restrict__ rsv_n,
-                                   const uint64_t* __restrict__ rsv_pred, int64_t i, const DevPod* __restrict__ pod, RsvPod rp, EvalParams P, RsvParams RP,
+                                   const uint64_t* __restrict__ rsv_pred, const RsvSel* __restrict__ rsel, int64_t i, const DevPod* __restrict__ pod, RsvPod rp, EvalParams P, RsvParams RP,
                                    int rsv_on, const Victim* __restrict__ vic, int64_t n_vic, int32_t* __restrict__ out) {
   if (blockIdx.x != 0 || threadIdx.x != 0) return;
   const DevPod p = *pod;
@@ -2629,7 +2629,8 @@ __global__ void filter_pod_preempt(DevTable T, const RsvNode* __restrict__ RN, c
   RsvNode rn;
   if (ns > 0) {
     rn = RN[i];
-    rsv_restore(rn, ns, rp, rsv_pred + (size_t)i * kRsvSlots, r, mm, nm, pr_c, pr_m, ra_c, ra_m, has_state);
+    rsv_restore(rn, ns, rp, rsv_pred + (size_t)i * kRsvSlots, (rp.flags & RP_SEL) ? rsel : nullptr, r, mm, nm, pr_c,
+                pr_m, ra_c, ra_m, has_state);
   }
   int64_t pre_c = 0, pre_m = 0, rr_c[kRsvSlots] = {}, rr_m[kRsvSlots] = {};
   bool pre_set = false;
@@ -3121,6 +3122,7 @@ struct kg_engine {
   DevBuf<uint64_t> rsv_pd;      // [cap][kRsvSlots] (ABI 12) the slots' fakeNode predicates
   DevBuf<int32_t> rsv_nd;       // slots in use per node
   DevBuf<RsvPod> rpods;
+  DevBuf<RsvSel> rsel;          // (ABI 12) [staged + kMaxB] reservation-affinity selectors (RsvPod::aux)
   DevBuf<int32_t> out_rslot;    // [staged + kMaxB]
   DevBuf<uint64_t> rsv_val;     // [capacity] packed per-node pass-1 values
   DevBuf<unsigned long long> rsv_ws;  // [8]: [3] = pod cursor, [4] = the call's end (graph launches)
@@ -4382,6 +4384,7 @@ RsvExt rsv_ext(kg_engine* e) {
   X.gz = e->gz.p;
   X.gzm = e->gzm.p;
   X.rsv_pred = e->rsv_pd.p;
+  X.rsv_sel = e->rsel.p;
   return X;
 }
 
@@ -4653,34 +4656,40 @@ int decode_node_rsv(const kg_node_reservations& r, RsvNode& d, int32_t& ns) {
 }
 
 // 1 + the highest predicate id a pod's reservation affinity uses (0: none)
-int64_t rsv_pred_top(const RsvPod& d) {
-  if (!(d.flags & RP_AFFINITY) || (d.flags & RP_RESERVE)) return 0;
-  uint64_t used = d.sel;
-  for (uint32_t t = 0; t < d.nterms; ++t) used |= d.terms[t];
+int64_t rsv_pred_top(const RsvPod& d, const RsvSel& c) {
+  if (!(d.flags & RP_SEL)) return 0;
+  uint64_t used = c.sel;
+  for (uint32_t t = 0; t < c.nterms; ++t) used |= c.terms[t];
   return used ? 64 - __builtin_clzll(used) : 0;
 }
 
-// the Reservation view of one pod: owner groups, the required-affinity flag and (ABI 12) its selector / terms
-int decode_rsv_pod(const kg_pod& p, RsvPod& d, int64_t k) {
+// the Reservation view of one pod: owner groups, the required-affinity flag and (ABI 12) its selector / terms (RP_SEL:
+// the caller points aux at where it stores `c`), the reserve pod's node and allocate policy
+int decode_rsv_pod(const kg_pod& p, RsvPod& d, RsvSel& c, int64_t k) {
   std::memset(&d, 0, sizeof(d));
+  std::memset(&c, 0, sizeof(c));
   if (p.n_reservation_terms < 0 || p.n_reservation_terms > KG_MAX_AFF_TERMS)
     return fail(KG_E_UNSUPPORTED, "pod %lld: more than %d reservation affinity terms (the pod stays on the Go path)",
                 (long long)k, KG_MAX_AFF_TERMS);
   d.owner_mask = (uint64_t)p.reservation_owner_mask;
   d.flags = ((p.reservation_flags & KG_POD_RSV_AFFINITY) ? RP_AFFINITY : 0u) |
             ((p.flags & KG_POD_RESERVE) ? RP_RESERVE : 0u) | ((p.reservation_flags & KG_POD_RSV_OPERATING) ? RP_OPERATING : 0u);
-  d.policy = (p.flags & KG_POD_RESERVE) ? (int32_t)p.reserve_allocate_policy : KG_RSV_POLICY_ALIGNED;
-  d.pin = -1;
+  d.aux = -1;
   if (p.flags & KG_POD_RESERVE) {
     if (p.reserve_allocate_policy < KG_RSV_POLICY_DEFAULT || p.reserve_allocate_policy > KG_RSV_POLICY_RESTRICTED)
       return fail(KG_E_INVALID, "pod %lld: reserve_allocate_policy %lld", (long long)k, (long long)p.reserve_allocate_policy);
     if (p.reserve_node < 0 || p.reserve_node > INT32_MAX)
       return fail(KG_E_INVALID, "pod %lld: reserve_node %lld", (long long)k, (long long)p.reserve_node);
-    d.pin = (int32_t)p.reserve_node - 1;
+    d.aux = (int32_t)p.reserve_node - 1;
+    d.flags |= (uint32_t)p.reserve_allocate_policy << RP_POLICY_SHIFT;
+  } else {
+    d.flags |= (uint32_t)KG_RSV_POLICY_ALIGNED << RP_POLICY_SHIFT;  // operating mode checks as Aligned
+    c.nterms = (uint32_t)p.n_reservation_terms;
+    c.sel = p.reservation_selector;
+    for (uint32_t t = 0; t < c.nterms; ++t) c.terms[t] = p.reservation_terms[t];
+    // a reserve pod matches no reservation, so its selectors are never read
+    if ((d.flags & RP_AFFINITY) && (c.sel != 0 || c.nterms != 0)) d.flags |= RP_SEL;
   }
-  d.nterms = (uint32_t)p.n_reservation_terms;
-  d.sel = p.reservation_selector;
-  for (int t = 0; t < d.nterms; ++t) d.terms[t] = p.reservation_terms[t];
   return 0;
 }
 
@@ -5154,6 +5163,7 @@ void kg_engine_destroy(kg_engine* e) {
   e->rsv_d.release();
   e->rsv_nd.release();
   e->rsv_pd.release();
+  e->rsel.release();
   e->rpods.release();
   e->out_rslot.release();
   e->rsv_val.release();
@@ -5469,10 +5479,12 @@ int kg_pods_stage(kg_engine* e, const kg_pod* pods, int64_t n) {
   }
   {  // exact-pass records (the Reservation view of every pod; single-pod calls of any profile use the pass)
     std::vector<RsvPod> hr(std::max<int64_t>(n, 1));
+    std::vector<RsvSel> hs(std::max<int64_t>(n, 1));
     int64_t rtop = 0;
     for (int64_t k = 0; k < n; ++k) {
-      if (int rc = decode_rsv_pod(pods[k], hr[k], k)) return rc;
-      rtop = std::max<int64_t>(rtop, rsv_pred_top(hr[k]));
+      if (int rc = decode_rsv_pod(pods[k], hr[k], hs[k], k)) return rc;
+      if (hr[k].flags & RP_SEL) hr[k].aux = (int32_t)k;
+      rtop = std::max<int64_t>(rtop, rsv_pred_top(hr[k], hs[k]));
       if ((pods[k].flags & KG_POD_RESERVE) && (e->numa_on || e->ds_on))
         return fail(KG_E_UNSUPPORTED, "pod %lld: scheduling a reserve pod with NodeNUMAResource / DeviceShare in the "
                     "profile (their reserve-pod paths keep the Go plugins)", (long long)k);
@@ -5481,6 +5493,8 @@ int kg_pods_stage(kg_engine* e, const kg_pod* pods, int64_t n) {
     if (int rc = e->rpods.ensure(n + kMaxB)) return rc;
     if (int rc = e->out_rslot.ensure(n + kMaxB)) return rc;
     if (n > 0) HIP_TRY(hipMemcpyAsync(e->rpods.p, hr.data(), n * sizeof(RsvPod), hipMemcpyHostToDevice, e->stream));
+    if (int rc = e->rsel.ensure(n + kMaxB)) return rc;
+    if (n > 0) HIP_TRY(hipMemcpyAsync(e->rsel.p, hs.data(), n * sizeof(RsvSel), hipMemcpyHostToDevice, e->stream));
     HIP_TRY(hipMemsetAsync(e->out_rslot.p, 0xff, (n + kMaxB) * 4, e->stream));
   }
   HIP_TRY(hipStreamSynchronize(e->stream));
@@ -6273,8 +6287,10 @@ int kg_pods_evaluate_reservation(kg_engine* e, const kg_pod* pod, int64_t* out) 
   DevPod d;
   if (int rc = decode_pod(e, *pod, d)) return rc;
   RsvPod rp;
-  if (int rc = decode_rsv_pod(*pod, rp, 0)) return rc;
-  if (int rc = check_rsv_predicates(e, rsv_pred_top(rp))) return rc;
+  RsvSel rs;
+  if (int rc = decode_rsv_pod(*pod, rp, rs, 0)) return rc;
+  if (int rc = check_rsv_predicates(e, rsv_pred_top(rp, rs))) return rc;
+  if (rp.flags & RP_SEL) rp.aux = 0;  // the scratch copy below
   DsPod dsp{};
   dsp.skip = 1;
   if (e->ds_on)
@@ -6286,7 +6302,8 @@ int kg_pods_evaluate_reservation(kg_engine* e, const kg_pod* pod, int64_t* out) 
   if (n == 0) return 0;
   const int64_t words = (int64_t)KG_RSV_EVAL_WORDS * n;
   const int64_t pw = kPodWords + (int64_t)(sizeof(RsvPod) / 8) + kDsPodWords + kNumaPodWords;
-  if (int rc = e->scratch64.ensure(words + pw)) return rc;
+  if (int rc = e->scratch64.ensure(words + pw + sizeof(RsvSel) / 8)) return rc;
+  RsvSel* gs = reinterpret_cast<RsvSel*>(e->scratch64.p + words + pw);
   DevPod* gp = reinterpret_cast<DevPod*>(e->scratch64.p + words);
   RsvPod* gr = reinterpret_cast<RsvPod*>(e->scratch64.p + words + kPodWords);
   DsPod* gd = reinterpret_cast<DsPod*>(e->scratch64.p + words + kPodWords + sizeof(RsvPod) / 8);
@@ -6295,7 +6312,9 @@ int kg_pods_evaluate_reservation(kg_engine* e, const kg_pod* pod, int64_t* out) 
   HIP_TRY(hipMemcpyAsync(gr, &rp, sizeof(rp), hipMemcpyHostToDevice, e->stream));
   HIP_TRY(hipMemcpyAsync(gd, &dsp, sizeof(dsp), hipMemcpyHostToDevice, e->stream));
   HIP_TRY(hipMemcpyAsync(gn, &np, sizeof(np), hipMemcpyHostToDevice, e->stream));
+  HIP_TRY(hipMemcpyAsync(gs, &rs, sizeof(rs), hipMemcpyHostToDevice, e->stream));
   RsvExt X = rsv_ext(e);
+  X.rsv_sel = gs;
   X.aff = nullptr;  // no pass affinity store: this is not a scheduling pass
   evaluate_pod_rsv<<<(unsigned)((n + 255) / 256), 256, 0, e->stream>>>(e->T, e->rsv_d.p, e->rsv_nd.p, gp, gr,
                                                                        e->ds_on ? gd : nullptr,
@@ -6320,7 +6339,10 @@ int kg_pods_filter_preemption(kg_engine* e, const kg_pod* pod, int32_t node_idx,
   if (int rc = decode_pod(e, *pod, d)) return rc;
   if (d.flags & P_AUX) return fail(KG_E_UNSUPPORTED, "preemption dry run: ephemeral-storage / scalar requests");
   RsvPod rp;
-  if (int rc = decode_rsv_pod(*pod, rp, 0)) return rc;
+  RsvSel rs;
+  if (int rc = decode_rsv_pod(*pod, rp, rs, 0)) return rc;
+  if (int rc = check_rsv_predicates(e, rsv_pred_top(rp, rs))) return rc;
+  if (rp.flags & RP_SEL) rp.aux = 0;
   if (rp.flags & (RP_RESERVE | RP_OPERATING))
     return fail(KG_E_UNSUPPORTED, "preemption dry run for a reserve pod / reservation operating mode keeps the Go path");
   std::vector<Victim> hv((size_t)std::max<int64_t>(n_victims, 1));
@@ -6334,13 +6356,15 @@ int kg_pods_filter_preemption(kg_engine* e, const kg_pod* pod, int32_t node_idx,
     hv[k] = Victim{v.req_cpu, v.req_mem, v.nz_cpu, v.nz_mem, s, nz ? 1 : 0};
   }
   const size_t vw = (hv.size() * sizeof(Victim) + 7) / 8;
-  if (int rc = e->scratch64.ensure(kPodWords + vw + 1)) return rc;
+  if (int rc = e->scratch64.ensure(kPodWords + vw + 1 + sizeof(RsvSel) / 8)) return rc;
   DevPod* gp = reinterpret_cast<DevPod*>(e->scratch64.p);
   Victim* gv = reinterpret_cast<Victim*>(e->scratch64.p + kPodWords);
   int32_t* go = reinterpret_cast<int32_t*>(e->scratch64.p + kPodWords + vw);
+  RsvSel* gs = reinterpret_cast<RsvSel*>(e->scratch64.p + kPodWords + vw + 1);
   HIP_TRY(hipMemcpyAsync(gp, &d, sizeof(d), hipMemcpyHostToDevice, e->stream));
+  HIP_TRY(hipMemcpyAsync(gs, &rs, sizeof(rs), hipMemcpyHostToDevice, e->stream));
   if (n_victims > 0) HIP_TRY(hipMemcpyAsync(gv, hv.data(), (size_t)n_victims * sizeof(Victim), hipMemcpyHostToDevice, e->stream));
-  filter_pod_preempt<<<1, kWave, 0, e->stream>>>(e->T, e->rsv_d.p, e->rsv_nd.p, e->rsv_pd.p, node_idx, gp, rp, e->P, e->RP,
+  filter_pod_preempt<<<1, kWave, 0, e->stream>>>(e->T, e->rsv_d.p, e->rsv_nd.p, e->rsv_pd.p, gs, node_idx, gp, rp, e->P, e->RP,
                                                  e->rsv_on ? 1 : 0, gv, n_victims, go);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpyAsync(out_reject, go, 4, hipMemcpyDeviceToHost, e->stream));

@@ -37,7 +37,8 @@ namespace kg {
 
 constexpr int kRsvSlots = KG_MAX_RSV_SLOTS;
 constexpr uint32_t RS_AVAIL = 1u << 0, RS_ONCE = 1u << 1, RS_UNSCHED = 1u << 2;  // policy in bits 4..5
-constexpr uint32_t RP_AFFINITY = 1u << 0, RP_RESERVE = 1u << 1, RP_OPERATING = 1u << 2;
+constexpr uint32_t RP_AFFINITY = 1u << 0, RP_RESERVE = 1u << 1, RP_OPERATING = 1u << 2, RP_SEL = 1u << 3;
+constexpr int RP_POLICY_SHIFT = 8;  // flags bits 8..9: the allocate policy of a reserve / operating-mode pod
 constexpr int64_t kDefaultMilliCpu = 100, kDefaultMemory = 200ll << 20;  // schedutil.GetNonzeroRequests defaults
 
 struct RsvNode {  // 192 B: one node's slots, read only for nodes with slots (rsv_n[i] > 0)
@@ -50,24 +51,26 @@ static_assert(sizeof(RsvNode) == 192, "RsvNode layout");
 // (ABI 12) the slots' fakeNode predicate bits live in their own [cap][kRsvSlots] array (RsvExt::rsv_pred), read only
 // for a pod whose reservation affinity has a selector or terms: the slot record the resolvers copy stays 192 B
 
-struct RsvPod {  // 64 B
+struct RsvPod {  // 16 B: what every evaluation of the pod reads
   uint64_t owner_mask;  // bit g: the pod matches the owners of owner group g
-  uint32_t flags;       // RP_*
-  uint32_t nterms;      // required reservation affinity: ReservationSelectorTerms (0 = absent)
-  uint64_t sel;         // ReservationSelector predicates (all must hold)
+  uint32_t flags;       // RP_* | allocate policy << RP_POLICY_SHIFT
+  int32_t aux;          // RP_RESERVE: the node GetReservePodNodeName names (-1 = none); RP_SEL: its RsvSel index
+};
+// (ABI 12) a required reservation affinity's selector / terms, read only by pods with RP_SEL (RsvExt::rsv_sel)
+struct RsvSel {  // 48 B
+  uint64_t sel;     // ReservationSelector predicates (all must hold)
   uint64_t terms[KG_MAX_AFF_TERMS];
-  int32_t policy;       // RP_RESERVE: the reservation's allocate policy; RP_OPERATING: Aligned
-  int32_t pin;          // RP_RESERVE: the node GetReservePodNodeName names (-1 = none)
+  uint32_t nterms;  // ReservationSelectorTerms (0 = absent)
+  uint32_t pad;
 };
 
 // RequiredReservationAffinity.Match (pkg/util/reservation/reservation.go:476-489) on a slot's fakeNode labels
-__device__ __forceinline__ bool rsv_affinity_match(const RsvPod& rp, uint64_t pred) {
-  if (!(rp.flags & RP_AFFINITY)) return true;
-  if ((pred & rp.sel) != rp.sel) return false;
-  if (rp.nterms == 0) return true;
+__device__ __forceinline__ bool rsv_affinity_match(const RsvSel& c, uint64_t pred) {
+  if ((pred & c.sel) != c.sel) return false;
+  if (c.nterms == 0) return true;
   bool any = false;
 #pragma unroll
-  for (int k = 0; k < KG_MAX_AFF_TERMS; ++k) any |= k < (int)rp.nterms && rp.terms[k] != 0 && (pred & rp.terms[k]) == rp.terms[k];
+  for (int k = 0; k < KG_MAX_AFF_TERMS; ++k) any |= k < (int)c.nterms && c.terms[k] != 0 && (pred & c.terms[k]) == c.terms[k];
   return any;
 }
 
@@ -107,6 +110,7 @@ struct RsvExt {
   uint64_t* __restrict__ gval;         // [cap] InterPodAffinity raw << 32 | PodTopologySpread raw (+ 2^31; 0 = ignored)
   int32_t* __restrict__ gz;            // [2 parities][kZoneSumWords] the zone sums (ZoneSums)
   const uint64_t* __restrict__ rsv_pred;  // [cap][kRsvSlots] the slots' fakeNode predicates (reservation affinity)
+  const RsvSel* __restrict__ rsv_sel;     // [pods] the RP_SEL pods' selectors / terms (RsvPod::aux)
   uint64_t* __restrict__ gzm;          // [2 parities] the present zones
 };
 // pod j's zone sums (double-buffered by parity: group_pre(j) accumulates, rsv_select(j) clears j + 1's)
@@ -165,7 +169,7 @@ struct RsvDbg {
 // NodeInfo (restoreMatchedReservation :240-263), the unmatched assigned ones leave and return as their remainders
 // (restoreUnmatchedReservations :265-291); pr_* = nodeReservationState.podRequested, ra_* = Σ matched Allocated.
 __device__ __forceinline__ void rsv_restore(const RsvNode& rn, int ns, const RsvPod& rp, const uint64_t* pred_row,
-                                            Row& r, uint32_t& mm, int& nm,
+                                            const RsvSel* sel, Row& r, uint32_t& mm, int& nm,
                                             int64_t& pr_c, int64_t& pr_m, int64_t& ra_c, int64_t& ra_m,
                                             bool& has_state) {
   uint32_t um = 0;
@@ -177,8 +181,8 @@ __device__ __forceinline__ void rsv_restore(const RsvNode& rn, int ns, const Rsv
     // ReservationInfo.Match → MatchReservationOwners, decoded per owner group into the pod's mask
     // a reserve pod matches no reservation (transformer.go:112 isReservedPod)
     if (!(rp.flags & RP_RESERVE) && ((rp.owner_mask >> (rn.owner[s] & 63)) & 1u) && !(m & RS_UNSCHED) &&
-        (!(rp.flags & RP_AFFINITY) || (rp.sel == 0 && rp.nterms == 0) ||
-         rsv_affinity_match(rp, pred_row ? pred_row[s] : 0ull)))
+        (!(rp.flags & RP_AFFINITY) || !(rp.flags & RP_SEL) ||
+         (sel && rsv_affinity_match(*sel, pred_row ? pred_row[s] : 0ull))))
       mm |= 1u << s;
     else if (rn.assigned[s] > 0) um |= 1u << s;
   }
@@ -241,8 +245,9 @@ __device__ __forceinline__ RsvOut rsv_eval_node(const DevTable& T, const RsvNode
   if (kSlotsInRegs && ns > 0) rn_copy = RN[i];
   const RsvNode& rn = kSlotsInRegs ? rn_copy : RN[i];
   if (ns > 0)
-    rsv_restore(rn, ns, rp, X.rsv_pred ? X.rsv_pred + (size_t)i * kRsvSlots : nullptr, r, mm, nm, pr_c, pr_m, ra_c,
-                ra_m, has_state);
+    rsv_restore(rn, ns, rp, X.rsv_pred ? X.rsv_pred + (size_t)i * kRsvSlots : nullptr,
+                (rp.flags & RP_SEL) && X.rsv_sel ? X.rsv_sel + rp.aux : nullptr, r, mm, nm, pr_c, pr_m, ra_c, ra_m,
+                has_state);
   if (dbg) {
     dbg->matched = mm;
     dbg->has_state = has_state ? 1 : 0;
@@ -254,12 +259,13 @@ __device__ __forceinline__ RsvOut rsv_eval_node(const DevTable& T, const RsvNode
   // Reservation.Filter of a reserve pod / a pod in reservation operating mode (plugin.go:324-350): the reservation's
   // node, and no available reservation whose allocate policy conflicts (Default coexists with no other policy)
   if (RP.filter && (rp.flags & (RP_RESERVE | RP_OPERATING))) {
-    if ((rp.flags & RP_RESERVE) && rp.pin >= 0 && i != rp.pin) return o;
+    if ((rp.flags & RP_RESERVE) && rp.aux >= 0 && i != rp.aux) return o;
+    const int32_t pol = (int32_t)((rp.flags >> RP_POLICY_SHIFT) & 3);
 #pragma unroll
     for (int s = 0; s < kRsvSlots; ++s) {
       if (s >= ns || !(rn.meta[s] & RS_AVAIL)) continue;
       const int32_t ps = (int32_t)((rn.meta[s] >> 4) & 3);
-      if ((rp.policy == KG_RSV_POLICY_DEFAULT || ps == KG_RSV_POLICY_DEFAULT) && rp.policy != ps) return o;
+      if ((pol == KG_RSV_POLICY_DEFAULT || ps == KG_RSV_POLICY_DEFAULT) && pol != ps) return o;
     }
   }
   int64_t t = 0;
