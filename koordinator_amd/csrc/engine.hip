@@ -3147,6 +3147,7 @@ struct kg_engine {
   int64_t sq_taint_min = 64, sq_pred_top = 0, sq_img_top = 0;
   std::vector<int16_t> rsv_pcnt;                // (ABI 12) per node: predicates its slots were compiled against (64: no slots)
   int64_t rsv_pcnt_min = 64, sq_rsv_top = 0;    // min over the nodes; the staged reservation affinities' top id + 1
+  bool rsv_ext_q = false;                       // the queue holds reserve / operating-mode / selector pods: per-pod pass
   bool rsv_pdirty = false;
   DevBuf<DefPod> defpods;       // [staged + kMaxB]
   DevBuf<uint32_t> rsv_val2;    // [cap] raw taint count << 24 | raw affinity sum (their Scores on)
@@ -5481,15 +5482,18 @@ int kg_pods_stage(kg_engine* e, const kg_pod* pods, int64_t n) {
     std::vector<RsvPod> hr(std::max<int64_t>(n, 1));
     std::vector<RsvSel> hs(std::max<int64_t>(n, 1));
     int64_t rtop = 0;
+    bool ext = false;
     for (int64_t k = 0; k < n; ++k) {
       if (int rc = decode_rsv_pod(pods[k], hr[k], hs[k], k)) return rc;
       if (hr[k].flags & RP_SEL) hr[k].aux = (int32_t)k;
+      ext |= (hr[k].flags & (RP_RESERVE | RP_OPERATING | RP_SEL)) != 0;
       rtop = std::max<int64_t>(rtop, rsv_pred_top(hr[k], hs[k]));
       if ((pods[k].flags & KG_POD_RESERVE) && (e->numa_on || e->ds_on))
         return fail(KG_E_UNSUPPORTED, "pod %lld: scheduling a reserve pod with NodeNUMAResource / DeviceShare in the "
                     "profile (their reserve-pod paths keep the Go plugins)", (long long)k);
     }
     e->sq_rsv_top = rtop;
+    e->rsv_ext_q = ext;
     if (int rc = e->rpods.ensure(n + kMaxB)) return rc;
     if (int rc = e->out_rslot.ensure(n + kMaxB)) return rc;
     if (n > 0) HIP_TRY(hipMemcpyAsync(e->rpods.p, hr.data(), n * sizeof(RsvPod), hipMemcpyHostToDevice, e->stream));
@@ -5585,7 +5589,8 @@ static int schedule_staged_impl(kg_engine* e, int64_t first, int64_t count, kg_s
   // scheduleOne): one pass costs less than a round's eval + merge + resolve when a round would hold one pod
   // (PodTopologySpread / InterPodAffinity profiles: one pod per pass — the batched rounds' stop rules do not cover
   // their cluster-wide minimum / count and min-max normalisation)
-  if (e->exact_on && e->xr_on && !e->grp_on && count >= kXrMin && e->n_nodes > 0) return run_xr(e, first, count, stats, t0);
+  if (e->exact_on && e->xr_on && !e->grp_on && !e->rsv_ext_q && count >= kXrMin && e->n_nodes > 0)
+    return run_xr(e, first, count, stats, t0);
   if (e->exact_on || (count <= kExactSmall && e->n_ranks == 1)) return run_rsv(e, first, count, stats, t0);
   RoundGeom g;
   if (int rc = prepare_rounds(e, g)) return rc;

@@ -168,6 +168,8 @@ struct RsvDbg {
 // BeforePreFilter's restore of one node for one pod (transformer.go:100-189): the matched slots' reserve pods leave
 // NodeInfo (restoreMatchedReservation :240-263), the unmatched assigned ones leave and return as their remainders
 // (restoreUnmatchedReservations :265-291); pr_* = nodeReservationState.podRequested, ra_* = Σ matched Allocated.
+// kExt = false (the batched exact rounds, which never see reserve / operating-mode / selector pods): owner groups only
+template <bool kExt = true>
 __device__ __forceinline__ void rsv_restore(const RsvNode& rn, int ns, const RsvPod& rp, const uint64_t* pred_row,
                                             const RsvSel* sel, Row& r, uint32_t& mm, int& nm,
                                             int64_t& pr_c, int64_t& pr_m, int64_t& ra_c, int64_t& ra_m,
@@ -180,10 +182,12 @@ __device__ __forceinline__ void rsv_restore(const RsvNode& rn, int ns, const Rsv
     if (!(m & RS_AVAIL) || ((m & RS_ONCE) && rn.assigned[s] > 0)) continue;  // transformer.go:101-110
     // ReservationInfo.Match → MatchReservationOwners, decoded per owner group into the pod's mask
     // a reserve pod matches no reservation (transformer.go:112 isReservedPod)
-    if (!(rp.flags & RP_RESERVE) && ((rp.owner_mask >> (rn.owner[s] & 63)) & 1u) && !(m & RS_UNSCHED) &&
-        (!(rp.flags & RP_AFFINITY) || !(rp.flags & RP_SEL) ||
-         (sel && rsv_affinity_match(*sel, pred_row ? pred_row[s] : 0ull))))
-      mm |= 1u << s;
+    bool match = ((rp.owner_mask >> (rn.owner[s] & 63)) & 1u) && !(m & RS_UNSCHED);
+    if (kExt)
+      match = match && !(rp.flags & RP_RESERVE) &&
+              (!(rp.flags & RP_AFFINITY) || !(rp.flags & RP_SEL) ||
+               (sel && rsv_affinity_match(*sel, pred_row ? pred_row[s] : 0ull)));
+    if (match) mm |= 1u << s;
     else if (rn.assigned[s] > 0) um |= 1u << s;
   }
   has_state = (mm | um) != 0 && !((rp.flags & RP_AFFINITY) && mm == 0);  // transformer.go:127-136
@@ -219,7 +223,10 @@ __device__ __forceinline__ void rsv_restore(const RsvNode& rn, int ns, const Rsv
     }
 }
 
-template <bool kSlotsInRegs = true>  // false: the slot record is read where used (the wide exact pass, register-bound)
+// kSlotsInRegs = false: the slot record is read where used (the wide exact pass, register-bound); kExt = false: no
+// reserve-pod / operating-mode / reservation-selector logic (the batched exact rounds; the host routes queues holding
+// such pods to the per-pod pass)
+template <bool kSlotsInRegs = true, bool kExt = true>
 __device__ __forceinline__ RsvOut rsv_eval_node(const DevTable& T, const RsvNode* __restrict__ RN,
                                                 const int32_t* __restrict__ rsv_n, int64_t i, const DevPod& p,
                                                 const RsvPod& rp, const EvalParams& P, const RsvParams& RP,
@@ -245,7 +252,7 @@ __device__ __forceinline__ RsvOut rsv_eval_node(const DevTable& T, const RsvNode
   if (kSlotsInRegs && ns > 0) rn_copy = RN[i];
   const RsvNode& rn = kSlotsInRegs ? rn_copy : RN[i];
   if (ns > 0)
-    rsv_restore(rn, ns, rp, X.rsv_pred ? X.rsv_pred + (size_t)i * kRsvSlots : nullptr,
+    rsv_restore<kExt>(rn, ns, rp, X.rsv_pred ? X.rsv_pred + (size_t)i * kRsvSlots : nullptr,
                 (rp.flags & RP_SEL) && X.rsv_sel ? X.rsv_sel + rp.aux : nullptr, r, mm, nm, pr_c, pr_m, ra_c, ra_m,
                 has_state);
   if (dbg) {
@@ -258,7 +265,7 @@ __device__ __forceinline__ RsvOut rsv_eval_node(const DevTable& T, const RsvNode
   if (dbg && df && !defaults_filter(npd, *df, X.DF)) return o;
   // Reservation.Filter of a reserve pod / a pod in reservation operating mode (plugin.go:324-350): the reservation's
   // node, and no available reservation whose allocate policy conflicts (Default coexists with no other policy)
-  if (RP.filter && (rp.flags & (RP_RESERVE | RP_OPERATING))) {
+  if (kExt && RP.filter && (rp.flags & (RP_RESERVE | RP_OPERATING))) {
     if ((rp.flags & RP_RESERVE) && rp.aux >= 0 && i != rp.aux) return o;
     const int32_t pol = (int32_t)((rp.flags >> RP_POLICY_SHIFT) & 3);
 #pragma unroll
@@ -292,7 +299,7 @@ __device__ __forceinline__ RsvOut rsv_eval_node(const DevTable& T, const RsvNode
     }
   }
   // plugin.go:361-364, 423-426 (a reserve pod skips this part of the Filter, :357)
-  if (RP.filter && (rp.flags & RP_AFFINITY) && !(rp.flags & RP_RESERVE) && sat == 0) return o;
+  if (RP.filter && (rp.flags & RP_AFFINITY) && !(kExt && (rp.flags & RP_RESERVE)) && sat == 0) return o;
   int64_t dsraw = 0;
   if (X.ds && dp && !dp->skip) {  // DeviceShare Filter + raw Score (node level: no device-holding reservations)
     if (!ds_eval(X.ds[i], *dp, X.DP, dsraw)) return o;

@@ -90,7 +90,7 @@ __global__ __launch_bounds__(kTile) void xr_eval(DevTable T, const RsvNode* __re
       const DefPod* df = (XF & XF_DEF) ? &X.defp[j] : nullptr;
       RsvExt Xk = X;
       Xk.aff = X.aff ? affk + (size_t)k * stride : nullptr;  // rsv_eval_node stores the NUMA affinity per node
-      const RsvOut o = rsv_eval_node<false>(T, RN, rsv_n, i, p, rp, P, RP, Xk, dp, np, nullptr, aux, df);
+      const RsvOut o = rsv_eval_node<false, false>(T, RN, rsv_n, i, p, rp, P, RP, Xk, dp, np, nullptr, aux, df);
       uint64_t v = 0;
       uint32_t v2 = 0;
       if (o.feas) {
@@ -471,7 +471,7 @@ __global__ __launch_bounds__(kWave) void xr_resolve(DevTable T, RsvNode* __restr
     uint64_t cv = 0;
     uint32_t cv2 = 0;
     if (lane < nM) {
-      cur = rsv_eval_node(T, RN, rsv_n, midx, p, rp, P, RP, X, dp, np, nullptr, aux, df);  // X.aff[midx] = pod j's
+      cur = rsv_eval_node<true, false>(T, RN, rsv_n, midx, p, rp, P, RP, X, dp, np, nullptr, aux, df);  // X.aff[midx] = pod j's
       if (cur.feas) cv = rsv_pack(cur), cv2 = ((uint32_t)cur.tcnt << 24) | (uint32_t)cur.asum;
     }
     KG_POD_SUB(j, 0);
