@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define KG_ABI_VERSION 12
+#define KG_ABI_VERSION 13
 
 /* ---- resource slots (fixed order) ------------------------------------------------------- */
 enum {
@@ -291,7 +291,13 @@ typedef struct kg_pod_metric {
 #define KG_MAX_ZONES 64          /* (ABI 12) topology.kubernetes.io/zone domains */
 enum {
   KG_SPREAD_HARD = 1 << 0,       /* whenUnsatisfiable: DoNotSchedule (else ScheduleAnyway) */
-  KG_SPREAD_ZONE = 1 << 1        /* topologyKey topology.kubernetes.io/zone (else kubernetes.io/hostname) */
+  KG_SPREAD_ZONE = 1 << 1,       /* topologyKey topology.kubernetes.io/zone (else kubernetes.io/hostname) */
+  /* (ABI 13) the constraint is one of the plugin's system defaults, applied because the pod has no constraints of its
+   * own (podtopologyspread PreScore: requireAllTopologies = len(pod.Spec.TopologySpreadConstraints) > 0 ||
+   * !systemDefaulted).  Set on every constraint of such a pod or on none; only with ScheduleAnyway.  Scoring then
+   * ignores no node: a filtered node without the zone label skips that constraint's term and adds the empty zone value
+   * to the constraint's topology size (scoring.go initPreScoreState, Score). */
+  KG_SPREAD_SYSTEM_DEFAULT = 1 << 2
 };
 
 /* One pod, pre-decoded by the caller (PodRequestsAndLimits semantics, pkg/util/pod_resources_utils.go:48-64). */
@@ -348,7 +354,8 @@ typedef struct kg_pod {
   int64_t match_groups;                        /* bit k: the pod (labels, namespace) matches group k             */
   /* topology spread constraints in the pod's order (≤ KG_MAX_SPREAD; at most one per {key, whenUnsatisfiable}, as
    * the API validates): the selector's group, maxSkew and KG_SPREAD_* flags.  A pod without constraints passes the
-   * system defaults here (hostname maxSkew 3 + zone maxSkew 5, ScheduleAnyway, with its owners' selector). */
+   * system defaults here (hostname maxSkew 3 + zone maxSkew 5, ScheduleAnyway, with its owners' selector), each flagged
+   * KG_SPREAD_SYSTEM_DEFAULT (ABI 13; before, such nodes were treated as if requireAllTopologies held). */
   int64_t n_spread;
   int64_t spread_group[KG_MAX_SPREAD];
   int64_t spread_max_skew[KG_MAX_SPREAD];

@@ -36,7 +36,7 @@ POD_TAINT_TABLE = 64
 MAX_OWNER_GROUPS = 64
 QUOTA_RES = 8
 MAX_QUOTAS = 64
-ABI_VERSION = 12
+ABI_VERSION = 13
 MAX_RSV_SLOTS = 4
 RSV_POLICY = {"Default": 0, "Aligned": 1, "Restricted": 2}
 POD_RSV_AFFINITY, POD_RSV_OPERATING = 1, 2
@@ -66,7 +66,7 @@ MAX_MATCH_GROUPS = 16  # KG_MAX_MATCH_GROUPS (ABI 12)
 MAX_POD_PREFERRED = 4  # KG_MAX_POD_PREFERRED (ABI 12)
 MAX_SPREAD = 4  # KG_MAX_SPREAD (ABI 12)
 MAX_ZONES = 64  # KG_MAX_ZONES (ABI 12)
-SPREAD_HARD, SPREAD_ZONE = 1, 2  # KG_SPREAD_*
+SPREAD_HARD, SPREAD_ZONE, SPREAD_SYSTEM_DEFAULT = 1, 2, 4  # KG_SPREAD_* (SYSTEM_DEFAULT: ABI 13)
 DEV_NVIDIA_GPU, DEV_HYGON_DCU, DEV_KOORD_GPU, DEV_GPU_CORE, DEV_GPU_MEMORY, DEV_GPU_MEMORY_RATIO, DEV_FPGA, DEV_RDMA = \
     range(8)
 DEVICE_RESOURCE_SLOTS = {

@@ -67,6 +67,32 @@ static_assert(kRecRows + kStaged * kEvalRowWords <= kCandStride, "record layout"
 
 thread_local std::string g_err;
 
+// (r5) Go's math.Log (src/math/log.go; amd64 archLog evaluates the same expression, no FMA contraction), in plain IEEE
+// double arithmetic (this file builds with -ffp-contract=off).  PodTopologySpread's topologyNormalizingWeight is
+// math.Log(size + 2), truncated after a multiply-add, so the weight table is built with Go's algorithm, not libm's
+// (the oracle's or_go_log is the same restatement; tests/test_go_log.py lists where glibc's log differs).
+double go_log(double x) {
+  const double Ln2Hi = 6.93147180369123816490e-01, Ln2Lo = 1.90821492927058770002e-10;
+  const double L1 = 6.666666666666735130e-01, L2 = 3.999999999940941908e-01, L3 = 2.857142874366239149e-01,
+               L4 = 2.222219843214978396e-01, L5 = 1.818357216161805012e-01, L6 = 1.531383769920937332e-01,
+               L7 = 1.479819860511658591e-01;
+  if (std::isnan(x) || (std::isinf(x) && x > 0)) return x;
+  if (x < 0) return std::nan("");
+  if (x == 0) return -HUGE_VAL;
+  int ki = 0;
+  double f1 = std::frexp(x, &ki);
+  if (f1 < 0.70710678118654752440) {  // math.Sqrt2 / 2
+    f1 *= 2;
+    ki--;
+  }
+  const double f = f1 - 1, k = (double)ki;
+  const double s = f / (2 + f), s2 = s * s, s4 = s2 * s2;
+  const double t1 = s2 * (L1 + s4 * (L3 + s4 * (L5 + s4 * L7)));
+  const double t2 = s4 * (L2 + s4 * (L4 + s4 * L6));
+  const double R = t1 + t2, hfsq = 0.5 * f * f;
+  return k * Ln2Hi - ((hfsq - (s * (hfsq + R) + k * Ln2Lo)) - f);
+}
+
 int fail(int code, const char* fmt, ...) {
   char buf[512];
   va_list ap;
@@ -244,6 +270,48 @@ __device__ __forceinline__ void eval_tile(const DevTable& T, const DevPod* __res
   }
 }
 
+template <int L>
+__device__ __forceinline__ void merge_pod(const DevTable& T, const EvalParams& P, const uint64_t* __restrict__ base,
+                                          int n_lists, uint64_t* sel, uint64_t* __restrict__ o, int lane);
+
+// (r5) The merge fused into the wide pass's tail.  Every block of a pod group publishes its lists (its stores drained,
+// the XCD L2 written back: the guide's release form) and takes a ticket; the block drawing the group's last ticket
+// acquires and merges the group's pods into their records, one pod per wave (merge_pod, as the merge_wave kernel
+// does), then resets the ticket for the slot's next round (stream order: that round's kernel starts after this one
+// ends).  n_lists ≤ 2·kWave (the caller's condition).  A round poisoned mid-launch can leave a partial count: the
+// batch is abandoned then, and every batch starts from zeroed tickets.
+__device__ __forceinline__ void merge_tail(const DevTable& T, const EvalParams& P, const uint64_t* __restrict__ lists,
+                                           int n_lists, int p0, int p1, int ppw, int n_tg, uint32_t* __restrict__ tickets,
+                                           uint64_t* __restrict__ records, uint64_t* s_lds) {
+  __shared__ uint32_t s_last;
+  const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    uint32_t* t = tickets + p0 / ppw;
+    const uint32_t old = __hip_atomic_fetch_add(t, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t last = old + 1 == (uint32_t)n_tg ? 1u : 0u;
+    if (last) {
+      __hip_atomic_store(t, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    s_last = last;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  const int64_t pstride = (int64_t)n_lists * kR;
+  uint64_t* sel = s_lds + (size_t)wave * kC;  // the block's list staging is free again: kEW·kC words (host-sized)
+  for (int pl = wave; pl < p1 - p0; pl += kEW) {
+    const uint64_t* base = lists + (size_t)(p0 + pl) * pstride;
+    uint64_t* o = records + (size_t)(p0 + pl) * kCandStride;
+    if (n_lists <= kWave) merge_pod<1>(T, P, base, n_lists, sel, o, lane);
+    else merge_pod<2>(T, P, base, n_lists, sel, o, lane);
+  }
+}
+
 // 4 waves per SIMD for the 2-node shape: all of the C3 grid (3,136 waves) resident at once (KG_EVAL_WPE=0: the
 // compiler's choice, 130 VGPRs and 3 waves per SIMD)
 #ifndef KG_EVAL_WPE
@@ -260,7 +328,9 @@ __global__ __launch_bounds__(kWave* kEW) KG_EVAL_ATTR void eval_round(DevTable T
                                                                   int64_t node_base, int64_t n_local, int nt_local,
                                                                   EvalParams P, uint64_t* __restrict__ lists,
                                                                   const int32_t* __restrict__ poison,
-                                                                  const int64_t* __restrict__ paux, int combine) {
+                                                                  const int64_t* __restrict__ paux, int combine,
+                                                                  uint32_t* __restrict__ tickets,
+                                                                  uint64_t* __restrict__ records) {
   KG_STAMP(0, 0);
   if (*poison) return;
   const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
@@ -279,10 +349,12 @@ __global__ __launch_bounds__(kWave* kEW) KG_EVAL_ATTR void eval_round(DevTable T
   // top-kR list per (pod, tile group) — a quarter of the candidate lists for the merge to read and rank
   // (a shard of fewer than kCombineTiles tiles keeps one list per tile: a pod's record needs kC candidates)
   extern __shared__ __attribute__((aligned(16))) uint64_t s_lists[];  // [kEW][pods_per_wave][kR]
+  const int ng_local = (nt_local + kEW - 1) / kEW, grp = tile0 / kEW;
   if (!combine) {
     if (tile < nt_local)
       eval_tile<PF, kENPT>(T, pods, first, p0, p1, tile, node_base, n_local, P, lists + ((size_t)p0 * nt_local + tile) * kR,
                     (int64_t)nt_local * kR, vbits, paux, lane);
+    if (tickets) merge_tail(T, P, lists, nt_local, p0, p1, pods_per_wave, ng_local, tickets, records, s_lists);
     return;
   }
   uint64_t* my_l = s_lists + (size_t)wave * pods_per_wave * kR;
@@ -293,7 +365,6 @@ __global__ __launch_bounds__(kWave* kEW) KG_EVAL_ATTR void eval_round(DevTable T
   // group list = the kR largest of the block's kEW·kR keys, in descending key order (within one score:
   // ascending node index, as the merge's tie rule reads lists); a full group list's minimum bounds every key the
   // block left out, as a full tile list's did (a full tile list's kR keys are all in the union)
-  const int ng_local = (nt_local + kEW - 1) / kEW, grp = tile0 / kEW;
   static_assert(kEW * kR <= kWave, "one key per lane");
   for (int pl = wave; pl < p1 - p0; pl += kEW) {
     const uint64_t key = lane < kEW * kR ? s_lists[((size_t)(lane / kR) * pods_per_wave + pl) * kR + lane % kR] : 0;
@@ -312,6 +383,7 @@ __global__ __launch_bounds__(kWave* kEW) KG_EVAL_ATTR void eval_round(DevTable T
     if (key != 0 && rank < kR) out[rank] = key;
     if (lane >= nnz && lane < kR) out[lane] = 0;
   }
+  if (tickets) merge_tail(T, P, lists, ng_local, p0, p1, pods_per_wave, ng_local, tickets, records, s_lists);
   KG_STAMP(0, 31);
 }
 
@@ -349,8 +421,7 @@ __global__ __launch_bounds__(kMergeThreads) void merge_round(DevTable T, EvalPar
                                                              const uint64_t* __restrict__ in, int64_t pod_stride,
                                                              int64_t list_stride, int n_lists, int list_len,
                                                              int nb, const int32_t* __restrict__ poison,
-                                                             uint64_t* __restrict__ out,
-                                                             uint32_t* __restrict__ done_cnt) {
+                                                             uint64_t* __restrict__ out) {
   __shared__ uint32_t hist[1 << kHistBits];
   __shared__ __attribute__((aligned(16))) uint64_t sel[kC];
   __shared__ uint64_t red64[kMergeThreads / kWave];
@@ -360,12 +431,7 @@ __global__ __launch_bounds__(kMergeThreads) void merge_round(DevTable T, EvalPar
   KG_STAMP(1, 0);
   const int pod = blockIdx.x;
   const int tid = threadIdx.x, lane = tid % kWave, wave = tid / kWave;
-  // done_cnt (round engines): every block of the grid counts itself once its record is written (or skipped), so the
-  // round's resolver — dispatched ahead on its own stream — knows when the records are there
-  if (*poison || pod >= nb) {
-    if (tid == 0 && done_cnt) atomicAdd(done_cnt, 1u);
-    return;
-  }
+  if (*poison || pod >= nb) return;
   const uint64_t* base = in + (size_t)pod * pod_stride;
 
   // Keys held in registers: thread t owns chunks c = t + kMergeThreads*i of 8 consecutive keys (chunk order
@@ -602,11 +668,6 @@ __global__ __launch_bounds__(kMergeThreads) void merge_round(DevTable T, EvalPar
       for (int w = 0; w < kEvalRowWords; ++w) dst[w] = words[w];
     }
   }
-  if (done_cnt) {
-    __threadfence();
-    __syncthreads();
-    if (tid == 0) atomicAdd(done_cnt, 1u);
-  }
   KG_STAMP(1, 14);
 }
 
@@ -621,17 +682,17 @@ __global__ __launch_bounds__(kMergeThreads) void merge_round(DevTable T, EvalPar
 //  * compaction into LDS by a wave prefix sum, a rank sort of ≤ kC keys, then the staged rows.
 __device__ __forceinline__ uint32_t wave_excl_prefix_u32(uint32_t v) { return wave_prefix_sum_u32(v) - v; }
 
+// One pod's record from its n_lists candidate lists at base (list l at base + l·kR), by one wavefront; sel = kC words of
+// this wave's LDS, o = the record.  Shared by merge_wave and (r5) eval_round's fused tail (opt-in).
+// (r5) Per-step costs measured in-kernel at C3 size (KG_STAMPS, profiles/r05/stamps_merge*.txt) drove the layout: the
+// staged rows of the 3 best keys are requested first (a knock-out wave max), so their HBM latency overlaps the
+// selection instead of ending the kernel; the threshold τ is a bisection over the live score range with ballot
+// popcounts (no DPP sums); the rank sort reads the zero-padded selection with all its broadcast loads in flight.
+__device__ __forceinline__ uint32_t ballot_count(bool c) { return (uint32_t)__popcll(__ballot(c)); }
+
 template <int L>
-__global__ __launch_bounds__(kWave * 4) void merge_wave(DevTable T, EvalParams P, const uint64_t* __restrict__ in,
-                                                        int64_t pod_stride, int n_lists, int nb,
-                                                        const int32_t* __restrict__ poison,
-                                                        uint64_t* __restrict__ out) {
-  __shared__ __attribute__((aligned(16))) uint64_t s_sel[4][kC];
-  const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
-  const int pod = blockIdx.x * 4 + wave;
-  if (*poison || pod >= nb) return;  // no block barrier below: a wave may leave alone
-  KG_STAMP(1, 0);
-  const uint64_t* base = in + (size_t)pod * pod_stride;
+__device__ __forceinline__ void merge_pod(const DevTable& T, const EvalParams& P, const uint64_t* __restrict__ base,
+                                          int n_lists, uint64_t* sel, uint64_t* __restrict__ o, int lane) {
   uint64_t k[L][kR];
   uint64_t ub_in = 0;
 #pragma unroll
@@ -660,38 +721,63 @@ __global__ __launch_bounds__(kWave * 4) void merge_wave(DevTable T, EvalParams P
     }
     if (cnt == kR) ub_in = mn > ub_in ? mn : ub_in;
   }
-  ub_in = wave_max_u64_dpp(ub_in);
-  ub_in = readlane_u64(ub_in, kWave - 1);
+  ub_in = wave_max_key(ub_in);
   KG_STAMP(1, 1);
+  // keys below ub_in can never be listed (ub_in bounds them already); the 3 best keys' rows go out to HBM now
+  uint64_t top[kStaged];
+  {
+    uint64_t bound = ~0ull;
+#pragma unroll
+    for (int q = 0; q < kStaged; ++q) {
+      uint64_t m = 0;
+#pragma unroll
+      for (int i = 0; i < L; ++i)
+#pragma unroll
+        for (int r = 0; r < kR; ++r) {
+          if (q == 0 && k[i][r] < ub_in) k[i][r] = 0;
+          m = k[i][r] < bound && k[i][r] > m ? k[i][r] : m;
+        }
+      top[q] = wave_max_key(m);
+      bound = top[q] ? top[q] : 1;  // 1: nothing below an empty maximum (every later top is 0)
+    }
+  }
+  const uint64_t my_top = lane == 0 ? top[0] : lane == 1 ? top[1] : top[2];
+  const bool stage = lane < kStaged && my_top != 0 && key_node(my_top) < (uint32_t)T.cap;
+  Row srow;
+  if (stage) srow = load_row(T, key_node(my_top));  // consumed at the end: its latency overlaps the selection
+  uint32_t sc[L][kR];  // score + 1 of a live key, 0 for a dropped one
   uint32_t c = 0;
 #pragma unroll
   for (int i = 0; i < L; ++i)
 #pragma unroll
     for (int r = 0; r < kR; ++r) {
-      if (k[i][r] < ub_in) k[i][r] = 0;
+      sc[i][r] = k[i][r] ? (uint32_t)(k[i][r] >> 32) + 1u : 0u;
       c += k[i][r] != 0;
     }
   const uint32_t total = wave_sum_u32(c);
   const bool all = total <= (uint32_t)kC;
   uint32_t tau = 0, need = kC;
   if (!all) {
-    uint32_t cur = 0;
-    for (int b = P.score_bits; b >= 0; --b) {
-      const uint32_t cand = cur | (1u << b);
+    // τ = the largest t with count(sc ≥ t) ≥ kC, bisected over (lo, hi]: count(sc ≥ lo) = total ≥ kC holds at lo = 1,
+    // and no key reaches the best key's score + 2
+    uint32_t lo = 1, hi = (uint32_t)(top[0] >> 32) + 2;
+    while (hi - lo > 1) {
+      const uint32_t mid = lo + (hi - lo) / 2;
       uint32_t n = 0;
 #pragma unroll
       for (int i = 0; i < L; ++i)
 #pragma unroll
-        for (int r = 0; r < kR; ++r) n += k[i][r] != 0 && (uint32_t)(k[i][r] >> 32) >= cand;
-      if (wave_sum_u32(n) >= (uint32_t)kC) cur = cand;
+        for (int r = 0; r < kR; ++r) n += ballot_count(sc[i][r] >= mid);
+      if (n >= (uint32_t)kC) lo = mid;
+      else hi = mid;
     }
-    tau = cur;
+    tau = lo;
     uint32_t a = 0;
 #pragma unroll
     for (int i = 0; i < L; ++i)
 #pragma unroll
-      for (int r = 0; r < kR; ++r) a += k[i][r] != 0 && (uint32_t)(k[i][r] >> 32) > tau;
-    need = (uint32_t)kC - wave_sum_u32(a);
+      for (int r = 0; r < kR; ++r) a += ballot_count(sc[i][r] > tau);
+    need = (uint32_t)kC - a;
   }
   KG_STAMP(1, 2);
   // selection with tie ranks in list order (i-major, then lane, then position) and the best key left out
@@ -703,7 +789,7 @@ __global__ __launch_bounds__(kWave * 4) void merge_wave(DevTable T, EvalParams P
     uint32_t ties = 0;
     if (!all) {
 #pragma unroll
-      for (int r = 0; r < kR; ++r) ties += k[i][r] != 0 && (uint32_t)(k[i][r] >> 32) == tau;
+      for (int r = 0; r < kR; ++r) ties += sc[i][r] == tau;
     }
     uint32_t tr = tie_base + wave_excl_prefix_u32(ties);
     tie_base += wave_sum_u32(ties);
@@ -711,54 +797,64 @@ __global__ __launch_bounds__(kWave * 4) void merge_wave(DevTable T, EvalParams P
 #pragma unroll
     for (int r = 0; r < kR; ++r) {
       const uint64_t v = k[i][r];
-      const uint32_t sc = (uint32_t)(v >> 32);
-      const bool tie = !all && v != 0 && sc == tau;
-      const bool sel = v != 0 && (all || sc > tau || (tie && tr < need));
+      const bool tie = !all && sc[i][r] == tau;
+      const bool sl = sc[i][r] != 0 && (all || sc[i][r] > tau || (tie && tr < need));
       tr += tie;
-      m |= (uint32_t)sel << r;
-      if (v != 0 && !sel) next = v > next ? v : next;
+      m |= (uint32_t)sl << r;
+      if (v != 0 && !sl) next = v > next ? v : next;
     }
     selm[i] = m;
     mycnt += __popc(m);
   }
   const uint32_t n_sel = wave_sum_u32(mycnt);
   uint32_t off = wave_excl_prefix_u32(mycnt);
-  next = wave_max_u64_dpp(next);
-  next = readlane_u64(next, kWave - 1);
-  uint64_t* sel = s_sel[wave];
+  next = wave_max_key(next);
 #pragma unroll
   for (int i = 0; i < L; ++i)
 #pragma unroll
     for (int r = 0; r < kR; ++r)
       if ((selm[i] >> r) & 1u) sel[off++] = k[i][r];
+  if (lane >= (int)n_sel) sel[lane] = 0;  // zero padding: the rank sort reads all kC slots
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   KG_STAMP(1, 13);
-  // rank sort of the ≤ kC selected keys (unique): position = number of larger keys
-  const uint64_t v = lane < (int)n_sel ? sel[lane] : 0;
+  // rank sort of the ≤ kC selected keys (unique, 0-padded): position = number of larger keys
+  const uint64_t v = sel[lane];
   int rank = 0;
   const ulonglong2* s2 = reinterpret_cast<const ulonglong2*>(sel);
-  for (int q = 0; q < ((int)n_sel + 1) / 2; ++q) {
+#pragma unroll
+  for (int q = 0; q < kC / 2; ++q) {
     const ulonglong2 x = s2[q];  // broadcast LDS reads
-    rank += (x.x > v) + (2 * q + 1 < (int)n_sel && x.y > v);
+    rank += (x.x > v) + (x.y > v);
   }
-  uint64_t* o = out + (size_t)pod * kCandStride;
-  if (lane < (int)n_sel) o[rank] = v;
-  else o[lane] = 0;
+  o[lane < (int)n_sel ? rank : lane] = lane < (int)n_sel ? v : 0;
   if (lane == 0) {
     const uint64_t ub_sel = next ? next + 1 : 0;
     o[kC] = ub_in > ub_sel ? ub_in : ub_sel;
   }
-  if (lane < (int)n_sel && rank < kStaged && key_node(v) < (uint32_t)T.cap) {
-    const EvalRow er = make_eval_row(load_row(T, key_node(v)), P);
+  if (stage) {  // lane q holds the q-th best key's row: rank q of the record
+    const EvalRow er = make_eval_row(srow, P);
     uint64_t words[kEvalRowWords];
     __builtin_memcpy(words, &er, sizeof(er));
-    uint64_t* dst = o + kRecRows + rank * kEvalRowWords;
+    uint64_t* dst = o + kRecRows + lane * kEvalRowWords;
 #pragma unroll
     for (int w = 0; w < kEvalRowWords; ++w) dst[w] = words[w];
   }
   KG_STAMP(1, 14);
+}
+
+template <int L>
+__global__ __launch_bounds__(kWave * 4) void merge_wave(DevTable T, EvalParams P, const uint64_t* __restrict__ in,
+                                                        int64_t pod_stride, int n_lists, int nb,
+                                                        const int32_t* __restrict__ poison,
+                                                        uint64_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint64_t s_sel[4][kC];
+  const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
+  const int pod = blockIdx.x * 4 + wave;
+  if (*poison || pod >= nb) return;  // no block barrier below: a wave may leave alone
+  KG_STAMP(1, 0);
+  merge_pod<L>(T, P, in + (size_t)pod * pod_stride, n_lists, s_sel[wave], out + (size_t)pod * kCandStride, lane);
 }
 
 // ---- round kernel 3: FIFO resolve (one wavefront, modified rows in registers) ---------------------------
@@ -803,22 +899,14 @@ __device__ __forceinline__ int mod_insert(uint32_t* h, uint32_t node, int slot) 
 
 // End of a resolver: every store of this wave visible device-wide, then ctl[4] = seq (agent-scope release) for
 // the next round's resolver, which may already be resident on another round stream.
+// (r5) Release only (the guide's producer form): this wave's stores drained, the XCD L2 written back, the wait after
+// the write-back kept by inline asm (the compiler may drop it), then a relaxed flag store.  The acq_rel
+// __threadfence() it replaces also invalidated the L2 — a cost on the serial chain that nothing after it needs.
 __device__ __forceinline__ void publish_round(int64_t* ctl, int64_t seq) {
-  __threadfence();
-  if (threadIdx.x == 0) __hip_atomic_store(&ctl[4], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// The round's records: each merge_round block adds 1 to *rec_cnt once its record is written; the resolver, dispatched
-// ahead on its own stream, waits for the batch's cumulative count (nullptr: stream order already guarantees them).
-// Bounded spin: 1 = timed out (reported as a device error).
-__device__ __forceinline__ int wait_records(const uint32_t* rec_cnt, uint32_t target) {
-  if (!rec_cnt) return 0;
-  int64_t it = 0;
-  while (__hip_atomic_load(rec_cnt, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < target) {
-    __builtin_amdgcn_s_sleep(1);
-    if (++it > kSpinLimit) return 1;
-  }
-  return 0;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (threadIdx.x == 0) __hip_atomic_store(&ctl[4], seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // exact key of one modified row for pod p (0 = filtered out).  A row outside eval_fast's domain takes the
@@ -1008,24 +1096,12 @@ __global__ __launch_bounds__(kWave) void resolve_round(DevTable T0, const DevPod
                                                         int32_t* __restrict__ modlists, int slot, int depth,
                                                         int n_prev, int32_t* __restrict__ poison, int64_t seq,
                                                         int wait, QuotaRow* __restrict__ quotas, int nq,
-                                                        const int64_t* __restrict__ paux,
-                                                        const uint32_t* __restrict__ rec_cnt, uint32_t rec_target) {
+                                                        const int64_t* __restrict__ paux) {
   extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
   KG_STAMP(2, 0);
   const int lane = threadIdx.x;
   // the serial chain outranks the wide pass's waves when they share a SIMD
   __builtin_amdgcn_s_setprio(3);
-  {
-    int to = 0;
-    if (lane == 0) to = wait_records(rec_cnt, rec_target);
-    to = __builtin_amdgcn_readfirstlane(to);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    if (to) {
-      if (lane == 0) ctl[5] = 1, *poison = 1;
-      publish_round(ctl, seq);
-      return;
-    }
-  }
   uint64_t* s_cand = smem;                                            // [nb][kCandStride]
   uint64_t* s_podw = s_cand + (size_t)nb * kCandStride;               // [nb] DevPod (kPodWords words)
   uint64_t* s_par = s_podw + (size_t)nb * kPodWords;                  // [kParWords] EvalParams (rare-path copy)
@@ -1357,23 +1433,11 @@ __global__ __launch_bounds__(kMwThreads) void resolve_mw(DevTable T0, const DevP
                                                          int32_t* __restrict__ modlists, int slot, int depth,
                                                          int n_prev, int32_t* __restrict__ poison, int64_t seq,
                                                          int wait, QuotaRow* __restrict__ quotas, int nq,
-                                                         const int64_t* __restrict__ paux,
-                                                         const uint32_t* __restrict__ rec_cnt, uint32_t rec_target) {
+                                                         const int64_t* __restrict__ paux) {
   extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
   KG_STAMP(2, 0);
   const MwLayout L = mw_layout(nb);
   const int tid = threadIdx.x, lane = tid % kWave, wave = tid / kWave;
-  {  // every wave waits for the round's records itself (a timeout is the same on every wave: the round is abandoned)
-    int to = 0;
-    if (lane == 0) to = wait_records(rec_cnt, rec_target);
-    to = __builtin_amdgcn_readfirstlane(to);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    if (to) {
-      if (tid == 0) ctl[5] = 1, *poison = 1;
-      if (wave == 0) publish_round(ctl, seq);
-      return;
-    }
-  }
   if (wave == 0) __builtin_amdgcn_s_setprio(3);  // the chain first, then its helpers, then any wide-pass wave
   else __builtin_amdgcn_s_setprio(2);
   uint64_t* s_cand = smem + L.cand;
@@ -1946,21 +2010,9 @@ __global__ __launch_bounds__(kWave) void resolve_round_numa(DevTable T, NumaTabl
                                                              uint64_t* __restrict__ out_cpus,
                                                              int64_t* __restrict__ out_nrec, int bitmap_words,
                                                              int32_t* __restrict__ poison, int64_t seq,
-                                                             QuotaRow* __restrict__ quotas, int nq,
-                                                             const uint32_t* __restrict__ rec_cnt, uint32_t rec_target) {
+                                                             QuotaRow* __restrict__ quotas, int nq) {
   extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
   const int lane = threadIdx.x;
-  {
-    int to = 0;
-    if (lane == 0) to = wait_records(rec_cnt, rec_target);
-    to = __builtin_amdgcn_readfirstlane(to);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    if (to) {
-      if (lane == 0) ctl[5] = 1, *poison = 1;
-      publish_round(ctl, seq);
-      return;
-    }
-  }
   uint64_t* s_cand = smem;                                    // [nb][kCandStride]
   uint64_t* s_podw = s_cand + (size_t)nb * kCandStride;       // [nb] DevPod
   uint64_t* s_npw = s_podw + (size_t)nb * kPodWords;          // [nb] NumaPod
@@ -3070,18 +3122,11 @@ struct kg_engine {
                               // [6] pods re-scored on the chain, [7] chain waits on a helper, [8] resolver active
                               // time (s_memrealtime ticks)
   DevBuf<int32_t> modlists;   // [kMaxDepth][kModListStride]: rows each round modified ([0] = count), by round slot
+  DevBuf<uint32_t> tickets;   // (r5) [kMaxDepth][kMaxB]: fused-merge tickets per (round slot, pod group)
   // round r runs on rs[r % D] (eval → merge → [RCCL on comms[r % D]] → resolve); `stream` runs ingest
   hipStream_t rs[kMaxDepth] = {};
   ncclComm_t comms[kMaxDepth] = {};  // comms[0] = comm; one communicator per round stream
   hipEvent_t ev_res[kMaxDepth] = {};
-  // (r4) round r's wide pass and merge run on es[r % D], its resolver on rs[r % D]: the resolver is dispatched as soon
-  // as resolve(r - D) is done — long before its records exist — and waits on the device for merge(r)'s blocks
-  // (mcnt[r % D]) and for resolve(r - 1) (the sequence word).  Same-stream resolvers were dispatched only after their
-  // merge, when the next round's wide pass could already fill every CU, and a multi-wave resolver then waited for a
-  // whole CU to drain.  eval(r) waits for resolve(r - D) through ev_done[r % D].
-  hipStream_t es[kMaxDepth] = {};
-  hipEvent_t ev_done[kMaxDepth] = {};
-  DevBuf<uint32_t> mcnt;  // [kMaxDepth] merge blocks done per round slot (cumulative over a batch)
   DevBuf<RowDelta> deltas;
   DevBuf<int64_t> scratch64;
   DevBuf<int32_t> scratch32;
@@ -3631,10 +3676,16 @@ int decode_group_pod(const kg_pod& p, GroupPod& d, int64_t k) {
   for (int c = 0; c < d.nsp; ++c) {
     int32_t g = -1;
     if (int rc = grp(p.spread_group[c], g, "topology spread")) return rc;
-    const int64_t f = p.spread_flags[c];
-    if (g < 0 || p.spread_max_skew[c] < 1 || p.spread_max_skew[c] > INT32_MAX || (f & ~3ll))
+    const int64_t fa = p.spread_flags[c], f = fa & 3ll;
+    if (g < 0 || p.spread_max_skew[c] < 1 || p.spread_max_skew[c] > INT32_MAX || (fa & ~7ll))
       return fail(KG_E_INVALID, "pod %lld: spread constraint %d: group %lld, maxSkew %lld, flags %lld", (long long)k, c,
-                  (long long)p.spread_group[c], (long long)p.spread_max_skew[c], (long long)f);
+                  (long long)p.spread_group[c], (long long)p.spread_max_skew[c], (long long)fa);
+    // (ABI 13) system defaults: every constraint of the pod or none, ScheduleAnyway only
+    const bool sd = (fa & KG_SPREAD_SYSTEM_DEFAULT) != 0;
+    if (sd != ((p.spread_flags[0] & KG_SPREAD_SYSTEM_DEFAULT) != 0) || (sd && (f & KG_SPREAD_HARD)))
+      return fail(KG_E_INVALID, "pod %lld: KG_SPREAD_SYSTEM_DEFAULT on some constraints only, or on a DoNotSchedule one",
+                  (long long)k);
+    if (sd) d.zone_keys |= kSpreadSysDefault;
     if ((seen >> f) & 1u)  // the API allows one constraint per {topologyKey, whenUnsatisfiable}
       return fail(KG_E_INVALID, "pod %lld: duplicate {topologyKey, whenUnsatisfiable} spread constraints", (long long)k);
     seen |= 1u << f;
@@ -3983,7 +4034,7 @@ size_t resolve_numa_lds_bytes(const RoundGeom& g, int nb) {
 }
 NumaTable numa_table(kg_engine* e) { return NumaTable{e->numa_s.p, e->numa_m.p}; }
 
-size_t eval_lds_bytes(const RoundGeom& g) { return (size_t)kEW * g.ppw * kR * 8; }
+size_t eval_lds_bytes(const RoundGeom& g) { return (size_t)kEW * std::max(g.ppw * kR, kC) * 8; }
 // eval_round's 1-D grid: tile groups of kEW tiles × pod groups, swizzled over XCDs inside the kernel
 dim3 eval_grid_e(const RoundGeom& g, int nb) {
   return dim3((unsigned)(((g.nte + kEW - 1) / kEW) * ((nb + g.ppw - 1) / g.ppw)));
@@ -3998,12 +4049,10 @@ int profile_bits(const EvalParams& P) {
          (P.la_score ? PF_LA_SCORE : 0) | (P.la_score && P.la_prod_score ? PF_LA_PROD : 0);
 }
 
-#ifdef KG_DEV_PF  // iteration builds only (make dev): one profile instantiated, every other one refused at run time
+#ifdef KG_DEV_PF  // iteration builds only (make dev): one profile instantiated; engine_create refuses every other one
 #define KG_PF_SWITCH(pf, CALL) \
   if ((pf) == KG_DEV_PF) {     \
     CALL(KG_DEV_PF);           \
-  } else {                     \
-    std::abort();              \
   }
 #else
 #define KG_PF_SWITCH(pf, CALL)                                                                   \
@@ -4024,7 +4073,19 @@ uint64_t* lists_slot(kg_engine* e, const RoundGeom& g, int slot) {
 
 constexpr int kCombineTiles = 16 * kEW;  // combined lists from 16 tile groups on (128 keys ≥ kC per pod)
 bool eval_combine(const RoundGeom& g) { return g.nte >= kCombineTiles; }
-void launch_eval(kg_engine* e, const RoundGeom& g, int64_t first, int nb, int slot, hipStream_t st) {
+int eval_lists(kg_engine* e, const RoundGeom& g);
+uint64_t* cand_slot(kg_engine* e, const RoundGeom& g, int slot);
+bool merge_block();
+// (r5) KG_FUSE=1: the merge fused into eval_round's tail (merge_tail; one rank, the Fit + LoadAware round engine,
+// ≤ 2·kWave lists per pod, ≤ 131k nodes).  A/B option only: measured at C3 the tail merge made eval + merge 2.5 µs
+// longer than the two launches (40.8 vs 28.0 + 10.2 µs, profiles/r05/timeline_*.txt) — the boundary it removes costs
+// ~0.9 µs (scripts/micro/handoff.hip) and every block pays a release before its ticket.
+bool fused_merge(kg_engine* e, const RoundGeom& g) {
+  static const bool on = std::getenv("KG_FUSE") && std::string(std::getenv("KG_FUSE")) == "1";
+  return on && e->n_ranks == 1 && !e->numa_on && !e->ds_on && !merge_block() && eval_lists(e, g) <= 2 * kWave;
+}
+uint32_t* tickets_slot(kg_engine* e, int slot) { return e->tickets.p + (size_t)slot * kMaxB; }
+void launch_eval(kg_engine* e, const RoundGeom& g, int64_t first, int nb, int slot, hipStream_t st, bool fuse = false) {
   if (e->numa_on) {  // one block per (tile, pod group)
     const dim3 grid((unsigned)(g.nt_local * ((nb + g.ppw - 1) / g.ppw)));
     eval_round_numa<<<grid, kWave * kEvalWaves, 0, st>>>(e->T, numa_table(e), e->pods.p, e->npods.p, first, nb,
@@ -4037,7 +4098,9 @@ void launch_eval(kg_engine* e, const RoundGeom& g, int64_t first, int nb, int sl
                                                                                 g.ppw, g.base,                   \
                                                                  g.n_local, g.nte, e->P,                  \
                                                                  lists_slot(e, g, slot), poison_ptr(e), e->paux.p, \
-                                                                 eval_combine(g) ? 1 : 0)
+                                                                 eval_combine(g) ? 1 : 0,                          \
+                                                                 fuse ? tickets_slot(e, slot) : nullptr,           \
+                                                                 cand_slot(e, g, slot))
   KG_PF_SWITCH(profile_bits(e->P), KG_EVAL)
 #undef KG_EVAL
 }
@@ -4061,10 +4124,10 @@ bool merge_block() {
   return on;
 }
 
-void launch_merge_local(kg_engine* e, const RoundGeom& g, int nb, int slot, hipStream_t st, uint32_t* done = nullptr) {
+void launch_merge_local(kg_engine* e, const RoundGeom& g, int nb, int slot, hipStream_t st) {
   uint64_t* dst = e->n_ranks > 1 ? gathered_slot(e, g, slot) + (size_t)e->rank * g.B * kCandStride : cand_slot(e, g, slot);
   const int nl = eval_lists(e, g);
-  if (!e->numa_on && !e->ds_on && !done && !merge_block()) {  // (r4) one wavefront per pod
+  if (!e->numa_on && !e->ds_on && !merge_block()) {  // (r4) one wavefront per pod
     const unsigned blocks = (unsigned)((nb + 3) / 4);
     const int64_t ps = (int64_t)nl * kR;
     if (nl <= kWave)
@@ -4078,14 +4141,13 @@ void launch_merge_local(kg_engine* e, const RoundGeom& g, int nb, int slot, hipS
     return;
   }
   merge_round<false><<<nb, kMergeThreads, 0, st>>>(e->T, e->P, lists_slot(e, g, slot), (int64_t)nl * kR, kR, nl, kR,
-                                                   nb, poison_ptr(e), dst,
-                                                   e->n_ranks > 1 ? nullptr : done);
+                                                   nb, poison_ptr(e), dst);
 }
 
-void launch_merge_ranks(kg_engine* e, const RoundGeom& g, int nb, int slot, hipStream_t st, uint32_t* done = nullptr) {
+void launch_merge_ranks(kg_engine* e, const RoundGeom& g, int nb, int slot, hipStream_t st) {
   merge_round<true><<<nb, kMergeThreads, 0, st>>>(e->T, e->P, gathered_slot(e, g, slot), kCandStride,
                                                   (int64_t)g.B * kCandStride, e->n_ranks, kC, nb, poison_ptr(e),
-                                                  cand_slot(e, g, slot), done);
+                                                  cand_slot(e, g, slot));
 }
 
 // KG_RESOLVER=mw: the look-ahead resolve_mw (A/B measurements only).  The single-wave resolve_round is the default:
@@ -4096,14 +4158,14 @@ bool resolver_one_wave() {
 }
 
 void launch_resolve(kg_engine* e, const RoundGeom& g, int64_t first, int nb, int slot, int n_prev,
-                    int64_t seq, int wait, hipStream_t st, const uint32_t* rec_cnt = nullptr, uint32_t rec_target = 0) {
+                    int64_t seq, int wait, hipStream_t st) {
   if (e->numa_on) {
     resolve_round_numa<<<1, kWave, resolve_numa_lds_bytes(g, nb), st>>>(e->T, numa_table(e), e->pods.p, e->npods.p,
                                                                         e->cursor.p, first, nb, cand_slot(e, g, slot),
                                                                         e->P, e->NP, e->out_keys.p, e->out_cpus.p,
                                                                         e->out_nrec.p,
                                                                         g.bitmap_words, poison_ptr(e), seq, e->quotas.p,
-                                                                        e->nq, rec_cnt, rec_target);
+                                                                        e->nq);
     return;
   }
 #define KG_RESOLVE_T(X, Q)                                                                                       \
@@ -4111,15 +4173,14 @@ void launch_resolve(kg_engine* e, const RoundGeom& g, int64_t first, int nb, int
                                                                   cand_slot(e, g, slot), e->P, e->out_keys.p,       \
                                                                   g.bitmap_words, e->modlists.p, slot, g.depth,     \
                                                                   n_prev, poison_ptr(e), seq, wait, e->quotas.p,    \
-                                                                  e->nq, e->paux.p, rec_cnt, rec_target)
+                                                                  e->nq, e->paux.p)
 #define KG_RESOLVE(X) KG_RESOLVE_T(X, false)
 #define KG_RESOLVE_Q(X) KG_RESOLVE_T(X, true)
 #define KG_RESOLVE_MW_T(X, Q)                                                                                   \
   resolve_mw<X, Q><<<1, kMwThreads, mw_lds_bytes(nb), st>>>(e->T, e->pods.p, e->cursor.p, first, nb,              \
                                                             cand_slot(e, g, slot), e->P, e->out_keys.p,         \
                                                             e->modlists.p, slot, g.depth, n_prev, poison_ptr(e), \
-                                                            seq, wait, e->quotas.p, e->nq, e->paux.p, rec_cnt,   \
-                                                            rec_target)
+                                                            seq, wait, e->quotas.p, e->nq, e->paux.p)
 #define KG_RESOLVE_MW(X) KG_RESOLVE_MW_T(X, false)
 #define KG_RESOLVE_MW_Q(X) KG_RESOLVE_MW_T(X, true)
   if (!resolver_one_wave()) {
@@ -4195,14 +4256,14 @@ int rank_allgather(kg_engine* e, uint64_t* all, size_t cnt, int slot, hipStream_
 }
 
 // merge → [all-gather + merge of the rank records] of one round, on stream st
-int launch_merge(kg_engine* e, const RoundGeom& g, int nb, int slot, hipStream_t st, uint32_t* done = nullptr) {
-  launch_merge_local(e, g, nb, slot, st, done);
+int launch_merge(kg_engine* e, const RoundGeom& g, int nb, int slot, hipStream_t st) {
+  launch_merge_local(e, g, nb, slot, st);
   HIP_TRY(hipGetLastError());
   if (e->n_ranks > 1) {
     const size_t cnt = (size_t)g.B * kCandStride;
     uint64_t* all = gathered_slot(e, g, slot);
     if (int rc = rank_allgather(e, all, cnt, slot, st)) return rc;
-    launch_merge_ranks(e, g, nb, slot, st, done);
+    launch_merge_ranks(e, g, nb, slot, st);
     HIP_TRY(hipGetLastError());
   }
   return 0;
@@ -4219,7 +4280,9 @@ int launch_merge(kg_engine* e, const RoundGeom& g, int nb, int slot, hipStream_t
 // than the early dispatch saves)
 int run_batch(kg_engine* e, const RoundGeom& g, int64_t cur, int64_t end, int64_t n_rounds) {
   const int D = g.depth;
+  const bool fuse = fused_merge(e, g);
   HIP_TRY(hipMemsetAsync(e->cursor.p + 3, 0, 3 * 8, e->rs[0]));  // poison, resolver sequence, device error
+  if (fuse) HIP_TRY(hipMemsetAsync(e->tickets.p, 0, (size_t)kMaxDepth * kMaxB * 4, e->rs[0]));
   if (D > 1) {  // the other round streams must not start before that reset
     HIP_TRY(hipEventRecord(e->ev_res[0], e->rs[0]));
     for (int k = 1; k < D; ++k) HIP_TRY(hipStreamWaitEvent(e->rs[k], e->ev_res[0], 0));
@@ -4230,12 +4293,14 @@ int run_batch(kg_engine* e, const RoundGeom& g, int64_t cur, int64_t end, int64_
     const int slot = (int)(r % D);
     hipStream_t st = e->rs[slot];
     size_t t = prof_begin(e, st);
-    launch_eval(e, g, first, nb, slot, st);
+    launch_eval(e, g, first, nb, slot, st, fuse);
     HIP_TRY(hipGetLastError());
     prof_end(e, KG_PROF_EVAL, t, st);
-    t = prof_begin(e, st);
-    if (int rc = launch_merge(e, g, nb, slot, st)) return rc;
-    prof_end(e, KG_PROF_MERGE, t, st);
+    if (!fuse) {
+      t = prof_begin(e, st);
+      if (int rc = launch_merge(e, g, nb, slot, st)) return rc;
+      prof_end(e, KG_PROF_MERGE, t, st);
+    }
     const int n_prev = (int)std::min<int64_t>(r, D - 1);
     t = prof_begin(e, st);
     launch_resolve(e, g, first, nb, slot, n_prev, r + 1, D > 1 && r > 0, st);
@@ -4545,7 +4610,7 @@ int run_xr(kg_engine* e, int64_t first, int64_t count, kg_stats* stats, double t
     xr_select<<<eval_blocks, kWave * kEvalWaves, 0, e->stream>>>(val, val2, n, nt, stride, vbits, e->RP, X,
                                                                e->xr_norm_d.p, e->xr_lists.p, e->rsv_ws.p);
     merge_round<false><<<kXrPods, kMergeThreads, 0, e->stream>>>(e->T, e->P, e->xr_lists.p, (int64_t)nt * kR, kR, nt,
-                                                                 kR, kXrPods, poison, e->xr_cand.p, nullptr);
+                                                                 kR, kXrPods, poison, e->xr_cand.p);
     prof_end(e, KG_PROF_RSV_SELECT, t, e->stream);
     t = prof_begin(e, e->stream);
 #define KG_XR_RESOLVE(XF)                                                                                      \
@@ -4834,9 +4899,6 @@ static int engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank,
         return bail(fail(KG_E_DEVICE, "hipStreamCreateWithPriority"));
       if (hipEventCreateWithFlags(&e->ev_res[k], hipEventDisableTiming) != hipSuccess)
         return bail(fail(KG_E_DEVICE, "hipEventCreate"));
-      if (hipStreamCreateWithPriority(&e->es[k], hipStreamNonBlocking, hi) != hipSuccess ||
-          hipEventCreateWithFlags(&e->ev_done[k], hipEventDisableTiming) != hipSuccess)
-        return bail(fail(KG_E_DEVICE, "hipStreamCreateWithPriority / hipEventCreate"));
     }
   }
   // 12 int64 columns + inv_mem[2] (f64) + the kAux resources' Allocatable / Requested
@@ -4867,8 +4929,9 @@ static int engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank,
   if (int rc = e->cursor.ensure(16)) return bail(rc);
   if (hipMemsetAsync(e->cursor.p, 0, 16 * 8, e->stream) != hipSuccess) return bail(fail(KG_E_DEVICE, "hipMemset"));
   if (int rc = e->modlists.ensure(kMaxDepth * kModListStride)) return bail(rc);
-  if (int rc = e->mcnt.ensure(kMaxDepth)) return bail(rc);
   if (hipMemsetAsync(e->modlists.p, 0, kMaxDepth * kModListStride * 4, e->stream) != hipSuccess) return bail(fail(KG_E_DEVICE, "hipMemset"));
+  if (int rc = e->tickets.ensure(kMaxDepth * kMaxB)) return bail(rc);
+  if (hipMemsetAsync(e->tickets.p, 0, kMaxDepth * kMaxB * 4, e->stream) != hipSuccess) return bail(fail(KG_E_DEVICE, "hipMemset"));
   e->nodes.assign(cap, kg_node{});
   e->metrics.assign(cap, kg_node_metric{});
   e->folded_usage.assign(2 * cap, 0);
@@ -4926,7 +4989,7 @@ static int engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank,
     if (int rc = e->gz.ensure((size_t)2 * kZoneSumWords)) return bail(rc);
     if (int rc = e->gzm.ensure(2)) return bail(rc);
     std::vector<double> lw((size_t)cap + 1);
-    for (int64_t f = 0; f <= cap; ++f) lw[f] = std::log((double)(f + 2));  // TopologyNormalizingWeight
+    for (int64_t f = 0; f <= cap; ++f) lw[f] = go_log((double)(f + 2));  // TopologyNormalizingWeight (Go's Log)
     if (hipMemsetAsync(e->grp_d.p, 0, (size_t)kGroupArrays * kGroups * cap * 4, e->stream) != hipSuccess ||
         hipMemcpyAsync(e->logw.p, lw.data(), lw.size() * 8, hipMemcpyHostToDevice, e->stream) != hipSuccess ||
         hipStreamSynchronize(e->stream) != hipSuccess)
@@ -5033,6 +5096,11 @@ static int engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank,
     e->P.inv_fit_ws[2] = wm > 0 ? 1.0f / wm : 0.0f;
     e->P.inv_fit_ws[3] = wc + wm > 0 ? 1.0f / (wc + wm) : 0.0f;
   }
+#ifdef KG_DEV_PF  // (r5) an iteration build refuses other profiles here, as a product build refuses what it lacks
+  if (profile_bits(e->P) != KG_DEV_PF)
+    return bail(fail(KG_E_UNSUPPORTED, "iteration build (KG_DEV_PF=%d): profile %d is not compiled in", KG_DEV_PF,
+                     profile_bits(e->P)));
+#endif
   {
     const int lds = (int)kMaxLds;
     hipError_t fe = hipSuccess;
@@ -5120,8 +5188,6 @@ void kg_engine_destroy(kg_engine* e) {
   if (e->stream) (void)hipStreamSynchronize(e->stream);
   for (int k = 0; k < kMaxDepth; ++k)
     if (e->rs[k]) (void)hipStreamSynchronize(e->rs[k]);
-  for (int k = 0; k < kMaxDepth; ++k)
-    if (e->es[k]) (void)hipStreamSynchronize(e->es[k]);
   if (e->lb_ready) (void)hipEventDestroy(e->lb_ready);
   if (e->lb_done) (void)hipEventDestroy(e->lb_done);
   for (int k = 1; k < kMaxDepth; ++k)
@@ -5139,12 +5205,10 @@ void kg_engine_destroy(kg_engine* e) {
   e->out_keys.release();
   e->cursor.release();
   e->modlists.release();
-  e->mcnt.release();
+  e->tickets.release();
   for (int k = 0; k < kMaxDepth; ++k) {
     if (e->ev_res[k]) (void)hipEventDestroy(e->ev_res[k]);
     if (e->rs[k]) (void)hipStreamDestroy(e->rs[k]);
-    if (e->ev_done[k]) (void)hipEventDestroy(e->ev_done[k]);
-    if (e->es[k]) (void)hipStreamDestroy(e->es[k]);
   }
   e->deltas.release();
   e->numa_s.release();
@@ -5273,14 +5337,33 @@ int kg_node_metrics_update(kg_engine* e, const kg_node_metric* m, const int32_t*
 
 static int pods_delta(kg_engine* e, const kg_pod* pods, const int32_t* node_idx, int64_t n, int sign) {
   if (!e || (n > 0 && (!pods || !node_idx))) return fail(KG_E_INVALID, "null argument");
-  if (sign < 0)  // a delete may name a pod this engine placed
-    if (int rc = flush_placements(e)) return rc;
+  // (r5) every pod is decoded and validated — node index, requests, group fields — before any host or device
+  // state changes, so a refused call leaves the engine as it was and may be retried
   std::vector<RowDelta> d(n);
+  std::vector<DevPod> dp((size_t)n);
   for (int64_t k = 0; k < n; ++k) {
     const int64_t i = node_idx[k];
     if (i < 0 || i >= e->capacity) return fail(KG_E_INVALID, "node index %lld", (long long)i);
-    DevPod p;
-    if (int rc = decode_pod(e, pods[k], p)) return rc;
+    if (int rc = decode_pod(e, pods[k], dp[k])) return rc;
+  }
+  std::vector<GroupPod> hg;
+  std::vector<int32_t> hn;
+  bool ipa_zone = false;
+  if (e->grp_on && n > 0) {
+    hg.resize((size_t)n);
+    hn.resize((size_t)(2 * n));
+    for (int64_t k = 0; k < n; ++k) {
+      if (int rc = decode_group_pod(pods[k], hg[k], k)) return rc;
+      ipa_zone |= (hg[k].aff_terms_z | hg[k].anti_z | hg[k].pref_zone) != 0;
+      hn[k] = (int32_t)node_idx[k];
+      hn[n + k] = sign;
+    }
+  }
+  if (sign < 0)  // a delete may name a pod this engine placed
+    if (int rc = flush_placements(e)) return rc;
+  for (int64_t k = 0; k < n; ++k) {
+    const int64_t i = node_idx[k];
+    const DevPod& p = dp[k];
     RowDelta& x = d[k];
     x.idx = i;
     x.d[0] = sign * p.req_cpu;
@@ -5305,14 +5388,7 @@ static int pods_delta(kg_engine* e, const kg_pod* pods, const int32_t* node_idx,
     }
   }
   if (e->grp_on && n > 0) {  // the nodes' pod-group counters (NodeInfo.AddPod / RemovePod of the pods' labels / terms)
-    std::vector<GroupPod> hg((size_t)n);
-    std::vector<int32_t> hn((size_t)(2 * n));
-    for (int64_t k = 0; k < n; ++k) {
-      if (int rc = decode_group_pod(pods[k], hg[k], k)) return rc;
-      if (hg[k].aff_terms_z | hg[k].anti_z | hg[k].pref_zone) e->GP.ipa_zone = 1;  // sticky: zone channels on
-      hn[k] = (int32_t)node_idx[k];
-      hn[n + k] = sign;
-    }
+    if (ipa_zone) e->GP.ipa_zone = 1;  // sticky: zone channels on
     if (int rc = e->gdelta.ensure(n)) return rc;
     if (int rc = e->gdelta_ns.ensure(2 * n)) return rc;
     HIP_TRY(hipMemcpyAsync(e->gdelta.p, hg.data(), n * sizeof(GroupPod), hipMemcpyHostToDevice, e->stream));
@@ -6358,6 +6434,9 @@ int kg_pods_filter_preemption(kg_engine* e, const kg_pod* pod, int32_t node_idx,
     if (s < -1 || s >= KG_MAX_RSV_SLOTS) return fail(KG_E_INVALID, "victim %lld: reservation slot %d", (long long)k, s);
     bool nz = false;
     for (int q = 0; q < KG_RES_MAX; ++q) nz |= victims[k].requests[q] != 0;
+    // (r5) RemovePod returns before counting a reserve pod (reservation/plugin.go:286): the framework still
+    // removes it from the NodeInfo copy, but it never becomes preemptible
+    if (victims[k].flags & KG_POD_RESERVE) nz = false;
     hv[k] = Victim{v.req_cpu, v.req_mem, v.nz_cpu, v.nz_mem, s, nz ? 1 : 0};
   }
   const size_t vw = (hv.size() * sizeof(Victim) + 7) / 8;

@@ -54,7 +54,8 @@ struct GroupPod {  // 112 B per staged pod
   int32_t npref;
   int32_t pref_g[kPodPref], pref_w[kPodPref];
   int32_t nsp;              // topology spread constraints, in the pod's order
-  uint32_t zone_keys;       // bit 0: a DoNotSchedule constraint is zone-keyed, bit 1: a ScheduleAnyway one
+  uint32_t zone_keys;       // bit 0: a DoNotSchedule constraint is zone-keyed, bit 1: a ScheduleAnyway one,
+                            // bit 2 (kSpreadSysDefault): the constraints are the plugin's system defaults
   int32_t sp_g[kSpread], sp_skew[kSpread];
   uint32_t sp_flags[kSpread];  // KG_SPREAD_HARD | KG_SPREAD_ZONE
 };
@@ -63,6 +64,11 @@ struct GroupPod {  // 112 B per staged pod
 __device__ __forceinline__ bool spread_has_keys(const GroupPod& gp, int kind, int32_t zone) {
   return !((gp.zone_keys >> kind) & 1u) || zone > 0;
 }
+// (ABI 13) requireAllTopologies = len(pod.Spec.TopologySpreadConstraints) > 0 || !systemDefaulted (podtopologyspread
+// PreScore): a system-defaulted pod ignores no node; a filtered node without the zone label skips that constraint's
+// Score term and adds the empty zone value to the constraint's topology size
+constexpr uint32_t kSpreadSysDefault = 1u << 2;
+__device__ __forceinline__ bool spread_sysdef(const GroupPod& gp) { return (gp.zone_keys & kSpreadSysDefault) != 0; }
 
 struct GroupParams {
   int32_t spread_filter, spread_score, w_spread;
@@ -191,15 +197,16 @@ __device__ __forceinline__ int32_t interpod_raw(const GroupTable& G, int64_t i, 
 
 // PodTopologySpread raw Score of node i (not ignored): Σ over the ScheduleAnyway constraints in the pod's order of
 // float64(cnt)·w + float64(maxSkew − 1), from 0, then int64(); hostname: the node's count, weight log(F − ignored + 2);
-// zone: its zone's sum, weight log(#zones + 2) — both from the host's log table (the same libm as the checker); the
-// products and sums round separately (-ffp-contract=off)
+// zone: its zone's sum, weight log(#zones + 2) — both from the host's table of Go's math.Log (r5); the products and
+// sums round separately (-ffp-contract=off)
 __device__ __forceinline__ int64_t spread_raw(const GroupTable& G, int64_t i, const GroupPod& gp, int32_t zone,
                                               const int32_t* __restrict__ zs, double w_host, double w_zone) {
   double s = 0;
   for (int c = 0; c < gp.nsp; ++c) {
     if (gp.sp_flags[c] & KG_SPREAD_HARD) continue;
     const bool z = (gp.sp_flags[c] & KG_SPREAD_ZONE) != 0;
-    const int64_t cnt = z ? (zone > 0 ? zs[c * kZones + zone - 1] : 0) : G.cnt(gp.sp_g[c], i);
+    if (z && zone <= 0) continue;  // Score: no label, no term (reached only by a system-defaulted pod, ABI 13)
+    const int64_t cnt = z ? zs[c * kZones + zone - 1] : G.cnt(gp.sp_g[c], i);
     s += (double)cnt * (z ? w_zone : w_host) + (double)(gp.sp_skew[c] - 1);
   }
   return (int64_t)s;

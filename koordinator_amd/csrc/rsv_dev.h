@@ -638,7 +638,7 @@ __global__ __launch_bounds__(kRsvThreads) void rsv_eval(DevTable T, RsvNode* __r
       zone = X.pred[i].zone;
       o.feas = groups_filter(X.G, i, gp, X.GP, node_affinity_match(X.pred, df, i), zone, s_min, Z, pres, total);
       if (o.feas) {
-        ign = !spread_has_keys(gp, 1, zone);
+        ign = !spread_sysdef(gp) && !spread_has_keys(gp, 1, zone);
         iraw = interpod_raw(X.G, i, gp, zone, Z);
       }
     }
@@ -661,7 +661,9 @@ __global__ __launch_bounds__(kRsvThreads) void rsv_eval(DevTable T, RsvNode* __r
     if (i < n) X.gval[i] = ((uint64_t)(uint32_t)iraw << 32) | (uint32_t)(zone << 1 | (ign ? 1 : 0));
     const uint64_t fc = rsv_block_sum(f ? 1u : 0u, s_red);
     __syncthreads();
-    const uint64_t ic = rsv_block_sum(f && ign ? 1u : 0u, s_red);
+    // ignored nodes; for a system-defaulted pod (none ignored), the filtered nodes without a zone label (the empty
+    // zone value's domain)
+    const uint64_t ic = rsv_block_sum(f && (spread_sysdef(gp) ? zone <= 0 : ign) ? 1u : 0u, s_red);
     __syncthreads();
     const uint64_t ix = rsv_block_max(f ? enc_max_i32(iraw) : 0, s_red);
     __syncthreads();
@@ -787,8 +789,9 @@ __global__ __launch_bounds__(kRsvThreads) void rsv_select(const uint64_t* __rest
     const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)zm, d), hi = (uint32_t)__shfl_xor((int)(uint32_t)(zm >> 32), d);
     zm |= ((uint64_t)hi << 32) | lo;
   }
-  const int64_t hs = F - ig;
-  const double w_host = X.logw[hs < 0 ? 0 : (hs < n ? hs : n)], w_zone = X.logw[__popcll(zm)];
+  const bool sd = spread_sysdef(gp);  // (ABI 13) part[11] counts the filtered nodes without a zone label instead
+  const int64_t hs = sd ? F : F - ig;
+  const double w_host = X.logw[hs < 0 ? 0 : (hs < n ? hs : n)], w_zone = X.logw[__popcll(zm) + (sd && ig > 0 ? 1 : 0)];
   int32_t raw = 0;
   bool on = false;
   if (i < n && ((val[i] >> 7) & 1u)) {

@@ -390,13 +390,21 @@ class PodGroupTable:
         return sum(1 << (g - 1) for g in {g for g, z in terms if z == zone})
 
     def fill_pod(self, pod: np.ndarray, labels: dict, namespace: str, spread=(), required_affinity=(),
-                 required_anti_affinity=(), preferred_affinity=(), preferred_anti_affinity=()) -> np.ndarray:
+                 required_anti_affinity=(), preferred_affinity=(), preferred_anti_affinity=(),
+                 system_default_selector=None) -> np.ndarray:
         """The ABI 12 fields of one pod.  spread: [{maxSkew, whenUnsatisfiable, labelSelector, topologyKey}] with
-        topologyKey kubernetes.io/hostname (default) or topology.kubernetes.io/zone (a pod without constraints may pass
-        the system defaults, hostname maxSkew 3 + zone maxSkew 5 ScheduleAnyway, with its owners' selector);
-        required_*: [{labelSelector, namespaces, topologyKey}] (hostname or zone); preferred_*: [{weight,
-        podAffinityTerm}]."""
+        topologyKey kubernetes.io/hostname (default) or topology.kubernetes.io/zone; required_*: [{labelSelector,
+        namespaces, topologyKey}] (hostname or zone); preferred_*: [{weight, podAffinityTerm}].
+        (ABI 13) system_default_selector: a pod without constraints of its own, under a PodTopologySpread configured
+        with the system defaults (defaultingType System), gets them here — hostname maxSkew 3 + zone maxSkew 5,
+        ScheduleAnyway, on its owners' selector (buildDefaultConstraints) — flagged KG_SPREAD_SYSTEM_DEFAULT, so scoring
+        ignores no node (requireAllTopologies false)."""
         r = pod[0] if pod.ndim else pod
+        if not spread and system_default_selector is not None:
+            spread = [dict(maxSkew=3, whenUnsatisfiable="ScheduleAnyway", labelSelector=system_default_selector,
+                           topologyKey=HOSTNAME, _system=True),
+                      dict(maxSkew=5, whenUnsatisfiable="ScheduleAnyway", labelSelector=system_default_selector,
+                           topologyKey=ZONE, _system=True)]
         if len(spread) > abi.MAX_SPREAD:
             raise NotImplementedError(f"more than {abi.MAX_SPREAD} topology spread constraints")
         seen = set()
@@ -411,8 +419,14 @@ class PodGroupTable:
             seen.add((key, hard))
             r["spread_group"][c] = self.group(cons.get("labelSelector"), (namespace,))
             r["spread_max_skew"][c] = cons["maxSkew"]
-            r["spread_flags"][c] = (abi.SPREAD_HARD if hard else 0) | (abi.SPREAD_ZONE if key == ZONE else 0)
+            r["spread_flags"][c] = ((abi.SPREAD_HARD if hard else 0) | (abi.SPREAD_ZONE if key == ZONE else 0) |
+                                    (abi.SPREAD_SYSTEM_DEFAULT if cons.get("_system") else 0))
         terms = [self._term(t, namespace) for t in required_affinity]
+        if len(set(terms)) != len(terms):
+            # (r5) the ABI carries required terms as a group bitmask; upstream processExistingPod adds
+            # HardPodAffinityWeight once per term, so two terms with the same selector, namespaces and key would score
+            # differently: such a pod stays on the Go path
+            raise NotImplementedError("two required pod-affinity terms with the same selector, namespaces and key")
         r["pod_affinity_terms"] = self._mask(terms, False)
         r["pod_affinity_terms_zone"] = self._mask(terms, True)
         r["pod_affinity_group"] = self.conjunction([g for g, _ in terms]) if terms else 0

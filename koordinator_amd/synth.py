@@ -616,7 +616,7 @@ def make_images(n_nodes: int, pods: np.ndarray, preds: np.ndarray, seed: int = B
 
 # ---- (ABI 12) PodTopologySpread / InterPodAffinity (hostname key) ------------------------------------------------
 def make_pod_groups(pods: np.ndarray, seed: int = BASE_SEED + 17, n_apps: int = 8, zones: bool = False,
-                    ipa_zones: bool | None = None) -> np.ndarray:
+                    ipa_zones: bool | None = None, system_default: float = 0.0) -> np.ndarray:
     """Fills the ABI 12 group fields of `pods` in place, as PodGroupTable would compile them for a workload of n_apps
     deployments (groups 1..n_apps: app=k in the namespace) in n_apps / 2 teams (groups n_apps+1..: team=t): every pod
     matches its app and team; 40 % carry a DoNotSchedule hostname spread constraint on their app (maxSkew 1-3), 50 % a
@@ -656,6 +656,18 @@ def make_pod_groups(pods: np.ndarray, seed: int = BASE_SEED + 17, n_apps: int = 
             perm = order[j][order[j] < c]
             for f in ("spread_group", "spread_max_skew", "spread_flags"):
                 pods[f][j, :c] = pods[f][j, perm]
+    # (ABI 13) a fraction of the pods without constraints of their own get the plugin's system defaults on their app
+    # (hostname maxSkew 3 + zone maxSkew 5, ScheduleAnyway, flagged KG_SPREAD_SYSTEM_DEFAULT); drawn after everything
+    # above so the rest of the workload is unchanged
+    if system_default > 0:
+        sd = (nsp == 0) & (np.random.default_rng(seed + 991).random(n) < system_default)
+        for j in np.nonzero(sd)[0]:
+            cons = [(0, 3)] + ([(abi.SPREAD_ZONE, 5)] if zones else [])
+            for c, (flag, skew) in enumerate(cons):
+                pods["spread_group"][j, c] = app[j] + 1
+                pods["spread_max_skew"][j, c] = skew
+                pods["spread_flags"][j, c] = flag | abi.SPREAD_SYSTEM_DEFAULT
+            nsp[j] = len(cons)
     pods["n_spread"] = nsp
     anti = rng.random(n) < 0.15
     pods["pod_anti_affinity"] = np.where(anti, 1 << app, 0)

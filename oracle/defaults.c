@@ -148,16 +148,51 @@ int or_spread_has_keys(const kg_node_predicates* n, const kg_pod* pod, int hard)
   return !spread_needs_zone(pod, hard) || n->zone > 0;  /* kubernetes.io/hostname: every node carries it */
 }
 
+/* (ABI 13) requireAllTopologies = len(pod.Spec.TopologySpreadConstraints) > 0 || !systemDefaulted (podtopologyspread
+ * PreScore, k8s v1.24.15): false when the pod's constraints are the plugin's system defaults */
+int or_spread_system_default(const kg_pod* pod) {
+  return pod->n_spread > 0 && (pod->spread_flags[0] & KG_SPREAD_SYSTEM_DEFAULT) != 0;
+}
+
 int or_spread_node_ok(const kg_node_predicates* n, const kg_pod* pod, int hard) {
   return or_affinity_filter(n, pod) && or_spread_has_keys(n, pod, hard);
 }
 
 /* scoring.go: scoreForCount = float64(cnt)·weight + float64(maxSkew − 1), summed over the constraints from 0 and
  * truncated by int64() (no fused multiply-add: -ffp-contract=off); weight = log(size + 2), the caller's per constraint */
+/* (r5) Go's math.Log (go1.18+ src/math/log.go `log`, the FreeBSD e_log.c algorithm; on amd64 `archLog` in log_amd64.s
+ * evaluates the same expression in the same order with SSE2 scalar ops, and the Go compiler never contracts a*b+c
+ * into an FMA on amd64), restated here in plain IEEE double arithmetic (-ffp-contract=off).  PodTopologySpread's
+ * topologyNormalizingWeight(size) = math.Log(float64(size + 2)) (podtopologyspread/scoring.go, k8s v1.24.15) feeds
+ * int64(cnt·w + maxSkew − 1), so a one-ulp difference from glibc's log() could move a truncation: the oracle and the
+ * engine both compute the weight with this function (tests/test_go_log.py compares it with glibc over [0, 1M]). */
+double or_go_log(double x) {
+  static const double Ln2Hi = 6.93147180369123816490e-01, Ln2Lo = 1.90821492927058770002e-10;
+  static const double L1 = 6.666666666666735130e-01, L2 = 3.999999999940941908e-01, L3 = 2.857142874366239149e-01,
+                      L4 = 2.222219843214978396e-01, L5 = 1.818357216161805012e-01, L6 = 1.531383769920937332e-01,
+                      L7 = 1.479819860511658591e-01;
+  if (isnan(x) || isinf(x)) return x > 0 || isnan(x) ? x : NAN;
+  if (x < 0) return NAN;
+  if (x == 0) return -INFINITY;
+  int ki = 0;
+  double f1 = frexp(x, &ki); /* Go's Frexp: f1 in [0.5, 1), the same for every finite non-zero x (subnormals too) */
+  if (f1 < 0.70710678118654752440 /* math.Sqrt2 / 2 as a float64 constant */) {
+    f1 *= 2;
+    ki--;
+  }
+  const double f = f1 - 1, k = (double)ki;
+  const double s = f / (2 + f), s2 = s * s, s4 = s2 * s2;
+  const double t1 = s2 * (L1 + s4 * (L3 + s4 * (L5 + s4 * L7)));
+  const double t2 = s4 * (L2 + s4 * (L4 + s4 * L6));
+  const double R = t1 + t2, hfsq = 0.5 * f * f;
+  return k * Ln2Hi - ((hfsq - (s * (hfsq + R) + k * Ln2Lo)) - f);
+}
+
 int64_t or_spread_raw(const int64_t* cnt, const double* w, const kg_pod* pod) {
   double s = 0;
   for (int64_t c = 0; c < pod->n_spread; c++) {
     if (pod->spread_flags[c] & KG_SPREAD_HARD) continue;
+    if (cnt[c] < 0) continue; /* (ABI 13) Score: `if tpVal, ok := node.Labels[c.TopologyKey]; ok` — no label, no term */
     s += (double)cnt[c] * w[c] + (double)(pod->spread_max_skew[c] - 1);
   }
   return (int64_t)s;

@@ -73,6 +73,10 @@ int or_spread_node_ok(const kg_node_predicates* n, const kg_pod* pod, int hard);
 int or_spread_has_keys(const kg_node_predicates* n, const kg_pod* pod, int hard);
 /* PodTopologySpread Score (scoring.go Score) before normalisation: Σ over the ScheduleAnyway constraints in the pod's
  * order of float64(cnt[c]) · w[c] + float64(maxSkew − 1), accumulated in float64 from 0, then int64(). */
+/* (ABI 13) the pod's spread constraints are the plugin's system defaults: requireAllTopologies is false */
+int or_spread_system_default(const kg_pod* pod);
+/* (r5) Go's math.Log restated (amd64: no FMA contraction); the PodTopologySpread weight uses it. */
+double or_go_log(double x);
 int64_t or_spread_raw(const int64_t* cnt, const double* w, const kg_pod* pod);
 /* PodTopologySpread NormalizeScore: MaxNodeScore · (max + min − s) / max, MaxNodeScore when max == 0. */
 int64_t or_spread_normalize(int64_t raw, int64_t mn, int64_t mx);

@@ -452,7 +452,11 @@ int or_schedule_resv_full(const kg_config* cfg, int64_t n_nodes, const kg_node* 
      * log(#zones of the non-ignored filtered nodes + 2); a zone's count sums the pods of every node passing the pod's
      * node affinity and carrying every ScheduleAnyway key.  Score per node, then NormalizeScore's extremes over the
      * non-ignored filtered nodes; InterPodAffinity's extremes over the filtered nodes */
+    /* (ABI 13) a system-defaulted pod (requireAllTopologies false) ignores no node: a filtered node without the zone
+     * label adds the empty zone value as one more domain of a zone constraint (zone_empty) */
+    const int sysdef = spread_on && or_spread_system_default(pod);
     int64_t n_feas = 0, n_ign = 0, smin = INT64_MAX, smax = INT64_MIN, imin = INT64_MAX, imax = INT64_MIN;
+    int zone_empty = 0;
     uint64_t zpres_s = 0;
     for (int64_t i = 0; i < n_nodes; i++) {
       if (!feas[i]) continue;
@@ -461,8 +465,9 @@ int or_schedule_resv_full(const kg_config* cfg, int64_t n_nodes, const kg_node* 
       if (iraw[i] > imax) imax = iraw[i];
       if (!spread_on) continue;
       const kg_node_predicates* np = preds ? &preds[i] : &zero_pred;
-      if (!or_spread_has_keys(np, pod, 0)) { n_ign++; continue; }
+      if (!sysdef && !or_spread_has_keys(np, pod, 0)) { n_ign++; continue; }
       if (np->zone > 0) zpres_s |= 1ull << (np->zone - 1);
+      else zone_empty = 1;
     }
     int64_t zsum_s[KG_MAX_SPREAD][KG_MAX_ZONES];
     double sw[KG_MAX_SPREAD] = {0};
@@ -473,9 +478,9 @@ int or_schedule_resv_full(const kg_config* cfg, int64_t n_nodes, const kg_node* 
         if (pod->spread_flags[c] & KG_SPREAD_HARD) continue;
         if (pod->spread_flags[c] & KG_SPREAD_ZONE) {
           has_zone = 1;
-          sw[c] = log((double)(__builtin_popcountll(zpres_s) + 2));
+          sw[c] = or_go_log((double)(__builtin_popcountll(zpres_s) + (sysdef ? zone_empty : 0) + 2));
         } else {
-          sw[c] = log((double)(n_feas - n_ign + 2));
+          sw[c] = or_go_log((double)(n_feas - n_ign + 2));
         }
       }
       if (has_zone)
@@ -491,10 +496,10 @@ int or_schedule_resv_full(const kg_config* cfg, int64_t n_nodes, const kg_node* 
         scnt[i] = INT64_MIN; /* ignored */
         if (!feas[i]) continue;
         const kg_node_predicates* np = preds ? &preds[i] : &zero_pred;
-        if (!or_spread_has_keys(np, pod, 0)) continue;
+        if (!sysdef && !or_spread_has_keys(np, pod, 0)) continue;
         int64_t cnt[KG_MAX_SPREAD] = {0};
         for (int64_t c = 0; c < pod->n_spread; c++)
-          cnt[c] = (pod->spread_flags[c] & KG_SPREAD_ZONE) ? (np->zone > 0 ? zsum_s[c][np->zone - 1] : 0)
+          cnt[c] = (pod->spread_flags[c] & KG_SPREAD_ZONE) ? (np->zone > 0 ? zsum_s[c][np->zone - 1] : -1)
                                                            : grp[i].cnt[pod->spread_group[c] - 1];
         scnt[i] = or_spread_raw(cnt, sw, pod);
         if (scnt[i] < smin) smin = scnt[i];
@@ -637,6 +642,7 @@ int64_t or_filter_preemption(const kg_config* cfg, const kg_node* node, const kg
     int nz = 0; /* !quotav1.IsZero(podRequests): every requested resource counts, not only cpu / memory */
     for (int q = 0; q < KG_RES_MAX; q++) nz |= v->requests[q] != 0;
     if (!nz) continue;
+    if (v->flags & KG_POD_RESERVE) continue; /* RemovePod (plugin.go:286): a reserve pod is never preemptible */
     const int s = victim_slot ? victim_slot[k] : -1;
     if (s >= 0 && s < KG_MAX_RSV_SLOTS) {
       pre_rr[s][0] += v->requests[KG_RES_CPU];

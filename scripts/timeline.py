@@ -11,9 +11,9 @@ import numpy as np
 
 
 def short(n):
-    for k in ("eval_round", "merge_round", "resolve_round"):
+    for k in ("eval_round", "merge_round", "resolve_round", "merge_wave"):
         if k in n:
-            return k
+            return "merge_round" if k == "merge_wave" else k
     return None
 
 
@@ -27,6 +27,8 @@ for r in rows:
         by[k].append((int(r.get("Dispatch_Id", 0)), int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
 for k in by:
     by[k].sort()
+if len(by.get("merge_round", [])) < len(by["eval_round"]) // 2:  # (r5) merge fused into eval_round's tail: a zero-length merge at the eval's end
+    by["merge_round"] = [(d, e, e) for d, _, e in by["eval_round"]]
 E, M, R = (np.array([(s, e) for _, s, e in by[k]], dtype=np.float64) / 1e3 for k in ("eval_round", "merge_round",
                                                                                       "resolve_round"))
 n = min(len(E), len(M), len(R))

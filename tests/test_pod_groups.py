@@ -230,6 +230,39 @@ def test_oracle_zone_spread_round_robin():
     assert sorted(np.bincount(zone_of[node], minlength=4)[1:]) == [2, 2, 2]
 
 
+def test_oracle_system_default_constraints_ignore_no_node():
+    """(ABI 13) requireAllTopologies = len(pod.Spec.TopologySpreadConstraints) > 0 || !systemDefaulted
+    (podtopologyspread PreScore, k8s v1.24.15).  Three equal nodes in zones [1, 2, none] holding 2 / 0 / 1 pods of the
+    app; a pod of the app with the system defaults (hostname maxSkew 3 + zone maxSkew 5, ScheduleAnyway).  Hand-derived:
+    * system-defaulted: no node ignored; hostname weight log(3 + 2), zone weight log(#{zone 1, zone 2, ""} + 2) =
+      log 5; the zone sums count only nodes carrying the key (zone 1: 2, zone 2: 0); raw node 0 = int(2w+2 + 2w+4) = 12,
+      node 1 = int(2 + 4) = 6, node 2 (no zone label: hostname term only) = int(w + 2) = 3; normalized 100·(15 − s)/12
+      = [25, 75, 100]; Fit 99 everywhere (1m / 1Mi pods) → totals 99 + 2·[25, 75, 100]: node 2 wins with 299;
+    * the same constraints given by the pod itself: node 2 is ignored (0), weights log(2 + 2), raw [11, 6] →
+      normalized [54, 100] → node 1 wins with 299."""
+    t = PodGroupTable()
+    sel = {"matchLabels": {"app": "web"}}
+    t.group(sel, ("default",))  # the group exists before the existing pods' match bits are compiled
+    cl, preds = _zoned(3, [1, 2, 0])
+
+    def tiny(n, **kw):
+        pods = np.concatenate([F.make_pod(requests={"cpu": "1m", "memory": "1Mi"}) for _ in range(n)])
+        for j in range(n):
+            t.fill_pod(pods[j:j + 1], {"app": "web"}, "default", **kw)
+        return pods
+
+    cl = synth.Cluster(cl.nodes, cl.metrics, tiny(3), np.array([0, 0, 2], dtype=np.int32), cl.now_ns)
+    sysdef = tiny(1, system_default_selector=sel)
+    assert (sysdef["spread_flags"][0, :2] & abi.SPREAD_SYSTEM_DEFAULT).all()
+    own = sysdef.copy()
+    own["spread_flags"] &= ~abi.SPREAD_SYSTEM_DEFAULT
+    cfg = F.build_config(profile=SPREAD_ONLY)
+    node, score, _, _ = _run_oracle(cfg, cl, sysdef, preds)
+    assert (int(node[0]), int(score[0])) == (2, 299)
+    node, score, _, _ = _run_oracle(cfg, cl, own, preds)
+    assert (int(node[0]), int(score[0])) == (1, 299)
+
+
 def test_oracle_hard_spread_round_robin():
     """maxSkew 1 on four equal nodes: each pod lands on an emptiest node, lowest index first."""
     t = PodGroupTable()
@@ -334,6 +367,18 @@ def test_pod_group_table_compiles_selectors():
     assert pod["n_spread"][0] == 1 and pod["spread_flags"][0, 0] == abi.SPREAD_ZONE
 
 
+def test_duplicate_required_affinity_terms_stay_on_go_path():
+    """(r5) Upstream adds HardPodAffinityWeight once per required term (processExistingPod); the ABI's
+    group bitmask would count two identical terms once, so PodGroupTable refuses such a pod."""
+    t = PodGroupTable()
+    pod = F.make_pod(requests={"cpu": "1"})
+    term = {"labelSelector": {"matchLabels": {"app": "db"}}, "topologyKey": "kubernetes.io/hostname"}
+    with pytest.raises(NotImplementedError):
+        t.fill_pod(pod, {"app": "web"}, "default", required_affinity=[term, dict(term)])
+    t.fill_pod(pod, {"app": "web"}, "default", required_affinity=[term])  # one term is fine
+    assert pod["pod_affinity_terms"][0] != 0
+
+
 # ---- device vs oracle -------------------------------------------------------------------------------------------
 def _world(n_nodes, n_pods, seed, with_preds=True, zones=True):
     cluster = synth.make_cluster(n_nodes, seed=seed)
@@ -401,6 +446,21 @@ def test_device_zone_interpod_cases(name):
     cl, pods, preds, _ = _zone_world(name)
     for calls in (1, len(pods)):
         _check(F.build_config(profile=IPA_ONLY), cl, pods, preds, calls)
+
+
+@pytest.mark.gpu
+def test_device_system_default_constraints():
+    """(ABI 13) A third of the pods without constraints of their own carry the system defaults (hostname + zone,
+    ScheduleAnyway, KG_SPREAD_SYSTEM_DEFAULT) on a cluster where 5 % of the nodes lack the zone label: device vs oracle
+    bit-exact, in one call and one pod per call."""
+    cluster = synth.make_cluster(1500, seed=131)
+    synth.make_pod_groups(cluster.existing_pods, seed=134, zones=True)
+    pods = synth.make_pods(300, seed=132)
+    synth.make_pod_groups(pods, seed=135, zones=True, system_default=0.35)
+    assert ((pods["spread_flags"][:, 0] & abi.SPREAD_SYSTEM_DEFAULT) != 0).sum() > 20
+    preds = synth.make_predicates(1500, pods, seed=133, no_zone=0.05)[1]
+    for calls in (1, 300):
+        _check(F.build_config(profile=STOCK), cluster, pods, preds, calls)
 
 
 @pytest.mark.gpu

@@ -310,3 +310,42 @@ def test_gpu_pods_metric_sequence():
         bad = np.nonzero(got2 != want2)[0]
         assert bad.size == 0, f"first mismatch at pod {bad[:5]}: gpu {got2[bad[:5]]} oracle {want2[bad[:5]]}"
         np.testing.assert_array_equal(score2, want2_score)
+
+
+@pytest.mark.gpu
+def test_refused_pods_add_leaves_state_unchanged():
+    """(r5) kg_pods_add validates every pod — its group fields included — before it changes any state: a
+    call refused for a bad group bit leaves the podAssignCache mirror, the node table and the group counters as they
+    were, so the retried call gives exactly the state of an engine that only saw the valid call."""
+    prof = F.Profile(filter=(F.NODE_RESOURCES_FIT, F.LOAD_AWARE, F.POD_TOPOLOGY_SPREAD),
+                     score={F.NODE_RESOURCES_FIT: 1, F.LOAD_AWARE: 1, F.POD_TOPOLOGY_SPREAD: 2})
+    cfg = F.build_config(profile=prof)
+    cl, pms = _pm_cluster(200, 990)
+    pm_nodes = sorted(pms)[:4]
+    add = _queue(4, 991, 1 << 42)
+    add["match_groups"] = 1
+    bad = add.copy()
+    bad["match_groups"][3] = 1 << 40  # a group bit beyond the 16 groups: KG_E_INVALID
+    idx = np.array(pm_nodes, dtype=np.int32)
+    probe = _queue(300, 992, 1 << 43)
+    out = []
+    for refused_first in (True, False):
+        with Engine(cfg, cl.n) as e:
+            synth.load_into(e, cl)
+            for i, pm in pms.items():
+                e.set_pods_metric(i, pm)
+            if refused_first:
+                with pytest.raises(abi.KoordGPUError):
+                    e.add_pods(bad, idx)
+            e.add_pods(add, idx)
+            st = e.read_state()
+            grp = e.read_pod_groups()
+            node, score, _ = e.schedule(probe)
+            out.append((st, grp, node, score))
+    (s1, g1, n1, sc1), (s2, g2, n2, sc2) = out
+    for k in s1:
+        np.testing.assert_array_equal(s1[k], s2[k], err_msg=k)
+    for a, b in zip(g1, g2):
+        np.testing.assert_array_equal(a, b)
+    np.testing.assert_array_equal(n1, n2)
+    np.testing.assert_array_equal(sc1, sc2)

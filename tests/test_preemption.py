@@ -34,12 +34,14 @@ def _victims(spec):
     """[(cpu_m, mem, slot)] -> (POD_DTYPE[k], int32[k]): slot -1 = the victim was not allocated from a reservation
     (RemovePod adds it to preemptible), s >= 0 = from slot s (preemptibleInRRs[s])."""
     v = np.zeros(len(spec), dtype=abi.POD_DTYPE)
-    for k, (c, m, _) in enumerate(spec):
+    for k, (c, m, *_rest) in enumerate(spec):
         req = {"cpu": f"{c}m"} if c else {}
         if m:
             req["memory"] = str(m)
         v[k] = F.make_pod(requests=req, limits=req)[0]
-    return v, np.array([s for _, _, s in spec], dtype=np.int32)
+        if _rest[1:] == ["reserve"]:  # a reservation's reserve pod (RemovePod skips it: plugin.go:286)
+            v[k]["flags"] |= abi.POD_RESERVE
+    return v, np.array([t[2] for t in spec], dtype=np.int32)
 
 
 def _rsv(policy, owner, alloc_cpu, allocd_cpu, assigned):
@@ -67,6 +69,13 @@ CASES = [
          pod=(4000, 0, False), victims=[(2000, 0, -1)], want=REJ),
     dict(ref="plugin_test.go:636 preemption but no preemptible resources", **_UNMATCHED,
          pod=(4000, 0, False), victims=[], want=0),
+    # (r5) plugin.go:286: RemovePod returns before counting a reserve pod.  The victim still leaves the
+    # NodeInfo copy (NodeResourcesFit passes), but it adds nothing to preemptible: fitsNode needs 32 − 2 + 4 ≤ 32 and
+    # rejects, where two ordinary 2-cpu victims make 32 − 4 + 4 and pass (the :594 row split in two)
+    dict(ref="plugin.go:286 RemovePod skips a reserve-pod victim", **_UNMATCHED,
+         pod=(4000, 0, False), victims=[(2000, 0, -1), (2000, 0, -1, "reserve")], want=REJ),
+    dict(ref="plugin.go:286-control two ordinary victims", **_UNMATCHED,
+         pod=(4000, 0, False), victims=[(2000, 0, -1), (2000, 0, -1)], want=0),
     dict(ref="plugin_test.go:867 default reservations with preemption", requested=36000, **_DEFAULT,
          pod=(4000, 0, False), victims=[(4000, 0, 0)], want=0),
     dict(ref="plugin_test.go:912 default reservations, preempt from reservation and node", requested=38000,
@@ -116,7 +125,8 @@ def test_oracle_reference_tables(case):
 def test_oracle_restore_reproduces_the_tables_state():
     """The restore of the golden NodeInfo gives the state the reference tests write: podRequested 32 (unmatched) /
     36 / 38 cpu and rAllocated 6 cpu with the one matched reservation."""
-    for case in (CASES[0], CASES[3], CASES[4]):
+    by = {c["ref"].split(" ", 1)[0]: c for c in CASES}
+    for case in (by["plugin_test.go:594"], by["plugin_test.go:867"], by["plugin_test.go:912"]):
         cluster, rsv, pod, _, _ = golden_cluster(case)
         st = oracle.states(1)
         oracle.add_pods(F.build_config(profile=RSV_ONLY), st, cluster.existing_pods, cluster.existing_node)
