@@ -426,6 +426,15 @@ typedef struct kg_node_reservations {
                                                /* transformer.go:357-369); read for reservation-affinity pods    */
   int64_t predicate_count;                     /* predicate ids decided in `predicates` (as node rows, ABI 11): */
                                                /* a queue using a later id is refused until the slots are re-sent */
+  /* (ABI 13) DeviceShare: the GPUs each reservation holds.  gpu_alloc = nodeDevice.getUsed(reserve pod), the
+   * reservation's allocatable per minor; gpu_allocated = the allocations of its assigned pods on those minors
+   * (appendAllocatedByHints, deviceshare/reservation.go:133-160).  [slot][minor][0..2] = gpu-core, gpu-memory (bytes),
+   * gpu-memory-ratio.  gpu_minors[s] = 0: the reservation holds no GPU (RestoreReservation drops it).  Both are in
+   * kg_node_device.used already (the reserve pod and the assigned pods are bound pods of the node); Reserve / Unreserve
+   * keep gpu_allocated current. */
+  int64_t gpu_minors[KG_MAX_RSV_SLOTS];        /* bit m: minor m is in the reserve pod's allocation             */
+  int64_t gpu_alloc[KG_MAX_RSV_SLOTS][KG_MAX_MINORS][3];
+  int64_t gpu_allocated[KG_MAX_RSV_SLOTS][KG_MAX_MINORS][3];
 } kg_node_reservations;
 
 /* One ElasticQuota as the plugin's PreFilter snapshot sees it (plugin.go:211-256) over KG_QUOTA_RES resources: cpu
@@ -635,6 +644,9 @@ int kg_nodes_reservation_upsert(kg_engine* e, const kg_node_reservations* r, con
 int kg_nodes_predicates_upsert(kg_engine* e, const kg_node_predicates* p, const int32_t* idx, int64_t n);
 /* Reads the DEVICE reservation slots: allocated cpu / memory and assigned count, KG_MAX_RSV_SLOTS per node. */
 int kg_nodes_read_reservations(kg_engine* e, int64_t* allocated_cpu, int64_t* allocated_mem, int64_t* assigned);
+/* (ABI 13) Reads the DEVICE reservation slots' gpu_allocated, [n_nodes][KG_MAX_RSV_SLOTS][KG_MAX_MINORS][3] (zeros
+ * for slots holding no GPU, or when DeviceShare is off). */
+int kg_nodes_read_reservation_gpus(kg_engine* e, int64_t* gpu_allocated);
 /* The reservation slot Reserve assumed each staged pod [first, first+count) into (-1 = none). */
 int kg_results_fetch_reservations(kg_engine* e, int64_t first, int64_t count, int32_t* out_slot);
 

@@ -78,7 +78,7 @@ DEVICE_RESOURCE_SLOTS = {
 
 
 def _i64(name, n=None):
-    return (name, np.int64) if n is None else (name, np.int64, (n,))
+    return (name, np.int64) if n is None else (name, np.int64, n if isinstance(n, tuple) else (n,))
 
 
 CONFIG_DTYPE = np.dtype([
@@ -167,7 +167,11 @@ NODE_PRED_DTYPE = np.dtype([("predicates", np.uint64), ("taints_hard", np.uint64
 NODE_RSV_DTYPE = np.dtype([_i64("n")] + [_i64(f, MAX_RSV_SLOTS) for f in (
     "owner", "allocatable_cpu", "allocatable_mem", "allocated_cpu", "allocated_mem", "assigned", "order", "policy",
     "allocate_once", "available", "unschedulable")] + [("predicates", np.uint64, (MAX_RSV_SLOTS,)),
-                                                        _i64("predicate_count")])
+                                                        _i64("predicate_count"),
+                                                        # (ABI 13) GPUs held per reservation
+                                                        _i64("gpu_minors", MAX_RSV_SLOTS),
+                                                        _i64("gpu_alloc", (MAX_RSV_SLOTS, MAX_MINORS, 3)),
+                                                        _i64("gpu_allocated", (MAX_RSV_SLOTS, MAX_MINORS, 3))])
 
 QUOTA_DTYPE = np.dtype([_i64("used", QUOTA_RES), _i64("non_preemptible_used", QUOTA_RES), _i64("used_limit", QUOTA_RES),
                         _i64("min", QUOTA_RES)])
@@ -206,6 +210,7 @@ EXPORTED_SYMBOLS = (
     "kg_nodes_numa_upsert", "kg_nodes_read_numa", "kg_results_fetch_cpusets", "kg_pods_evaluate_numa",
     "kg_nodes_device_upsert", "kg_nodes_read_device", "kg_results_fetch_devices", "kg_pods_evaluate_device",
     "kg_quotas_set", "kg_quotas_read", "kg_nodes_reservation_upsert", "kg_nodes_read_reservations",
+    "kg_nodes_read_reservation_gpus",
     "kg_results_fetch_reservations", "kg_profile_enable", "kg_profile_read", "kg_loopback_create",
     "kg_loopback_destroy", "kg_engine_create_loopback", "kg_pods_unreserve", "kg_engine_set_clock",
     "kg_node_pods_metric_set", "kg_debug_numa_merge", "kg_pods_evaluate_reservation", "kg_nodes_predicates_upsert",
@@ -221,11 +226,18 @@ LIB_PATH = os.environ.get("KOORDGPU_LIB") or os.path.join(PKG_DIR, "libkoordgpu.
 _lib = None
 
 
+class _ArrayPtr(ctypes.c_void_p):
+    """A c_void_p that keeps its array alive: `ptr(np.ascontiguousarray(x))` passes a temporary, which would otherwise
+    be freed as soon as ptr() returns, leaving the call a dangling pointer."""
+
+
 def ptr(a):
-    """Pointer to a numpy array's data (None for None)."""
+    """Pointer to a numpy array's data (None for None); the array lives as long as the pointer object."""
     if a is None:
         return None
-    return ctypes.c_void_p(a.ctypes.data)
+    q = _ArrayPtr(a.ctypes.data)
+    q._array = a
+    return q
 
 
 def load_library(path: str | None = None):
@@ -278,6 +290,7 @@ def load_library(path: str | None = None):
         "kg_quotas_read": (i, [vp, vp, i64]),
         "kg_nodes_reservation_upsert": (i, [vp, vp, vp, i64]),
         "kg_nodes_read_reservations": (i, [vp, vp, vp, vp]),
+        "kg_nodes_read_reservation_gpus": (i, [vp, vp]),
         "kg_results_fetch_reservations": (i, [vp, i64, i64, vp]),
         "kg_profile_enable": (i, [vp, i]),
         "kg_profile_read": (i, [vp, vp, vp]),

@@ -2798,12 +2798,13 @@ __global__ void unreserve_pods(DevTable T, const DevPod* __restrict__ pods, cons
                                int32_t* __restrict__ out_minors, RsvNode* __restrict__ RN, int32_t* __restrict__ out_rslot,
                                QuotaRow* __restrict__ quotas, int nq, const int64_t* __restrict__ qdev,
                                const int64_t* __restrict__ paux, GroupTable G, const GroupPod* __restrict__ gpods,
-                               int hard_w) {
+                               int hard_w, RsvGpu* __restrict__ rg) {
   if (blockIdx.x != 0 || threadIdx.x != 0) return;
   for (int64_t k = 0; k < n; ++k) {
     const int64_t j = idx[k];
     const uint64_t key = out_keys[j];
     if (key == 0) continue;
+    const int32_t gm = ds ? out_minors[j] : 0;  // the DeviceShare allocation, before it is cleared below
     const uint32_t w = key_node(key);
     const DevPod p = pods[j];
     Row r = load_row(T, w);  // NodeInfo.RemovePod + podAssignCache.unAssign (pod_assign_cache.go:119-131)
@@ -2849,6 +2850,10 @@ __global__ void unreserve_pods(DevTable T, const DevPod* __restrict__ pods, cons
     if (RN && out_rslot[j] >= 0) {  // reservation/plugin.go:561-583 → RemoveAssignedPod (reservation_info.go:328-339)
       const int s = out_rslot[j];
       RsvNode& rn = RN[w];
+      // (ABI 13) its allocation on a GPU-holding reservation's minors leaves the restore's `allocated`
+      // (deviceshare/reservation.go:150-155)
+      if (rg && gm > 0 && (rn.meta[s] & RS_GPU))
+        rsv_gpu_assign(rg[(size_t)w * kRsvSlots + s], ds_instance(ds[w], dpods[j]), gm, -1);
       if (rn.assigned[s] > 0) {
         if (rn.alloc_cpu[s] > 0) rn.allocd_cpu[s] = rn.allocd_cpu[s] > p.req_cpu ? rn.allocd_cpu[s] - p.req_cpu : 0;
         if (rn.alloc_mem[s] > 0) rn.allocd_mem[s] = rn.allocd_mem[s] > p.req_mem ? rn.allocd_mem[s] - p.req_mem : 0;
@@ -3164,6 +3169,9 @@ struct kg_engine {
   DevBuf<uint32_t> numa_aff;  // exact pass: the NUMA affinity Filter stored per node for the pass's pod
   RsvParams RP{};
   DevBuf<RsvNode> rsv_d;
+  DevBuf<RsvGpu> rsv_g;                         // (ABI 13) [cap][kRsvSlots] GPU holdings, allocated at the first GPU slot
+  std::vector<uint8_t> rsv_gnode;               // per node: it has an RS_GPU slot
+  int64_t rgpu_nodes = 0;                       // nodes with an RS_GPU slot (> 0 routes queues to the per-pod pass)
   DevBuf<uint64_t> rsv_pd;      // [cap][kRsvSlots] (ABI 12) the slots' fakeNode predicates
   DevBuf<int32_t> rsv_nd;       // slots in use per node
   DevBuf<RsvPod> rpods;
@@ -4451,6 +4459,9 @@ RsvExt rsv_ext(kg_engine* e) {
   X.gzm = e->gzm.p;
   X.rsv_pred = e->rsv_pd.p;
   X.rsv_sel = e->rsel.p;
+  X.rgpu = e->ds_on && e->rgpu_nodes > 0 ? e->rsv_g.p : nullptr;
+  X.rpods = e->rpods.p;
+  X.rsv_n = e->rsv_nd.p;
   return X;
 }
 
@@ -4691,8 +4702,9 @@ int run_xr(kg_engine* e, int64_t first, int64_t count, kg_stats* stats, double t
   return 0;
 }
 
-int decode_node_rsv(const kg_node_reservations& r, RsvNode& d, int32_t& ns) {
+int decode_node_rsv(const kg_node_reservations& r, RsvNode& d, int32_t& ns, RsvGpu* g, bool ds_on) {
   std::memset(&d, 0, sizeof(d));
+  std::memset(g, 0, sizeof(RsvGpu) * kRsvSlots);
   if (r.n < 0 || r.n > KG_MAX_RSV_SLOTS) return fail(KG_E_INVALID, "reservation slot count %lld", (long long)r.n);
   if (r.predicate_count < 0 || r.predicate_count > 64)
     return fail(KG_E_INVALID, "reservation predicate_count %lld outside [0, 64]", (long long)r.predicate_count);
@@ -4717,6 +4729,29 @@ int decode_node_rsv(const kg_node_reservations& r, RsvNode& d, int32_t& ns) {
     d.order[s] = (int32_t)r.order[s];
     d.meta[s] = (r.available[s] ? RS_AVAIL : 0u) | (r.allocate_once[s] ? RS_ONCE : 0u) |
                 (r.unschedulable[s] ? RS_UNSCHED : 0u) | ((uint32_t)r.policy[s] << 4);
+    // (ABI 13) the GPUs the reservation holds (DeviceShare only reads them)
+    if (r.gpu_minors[s] < 0 || r.gpu_minors[s] >= (int64_t(1) << kMinors))
+      return fail(KG_E_INVALID, "reservation slot %d: gpu_minors outside [0, 2^%d)", s, kMinors);
+    if (r.gpu_minors[s] == 0 || !ds_on) continue;
+    RsvGpu& G = g[s];
+    G.minors = (uint32_t)r.gpu_minors[s];
+    for (int m = 0; m < kMinors; ++m)
+      for (int q = 0; q < 3; ++q) {
+        const int64_t lim = q == 1 ? (int64_t(1) << 46) : (int64_t(1) << 30);
+        const int64_t A = r.gpu_alloc[s][m][q], a = r.gpu_allocated[s][m][q];
+        if (A < 0 || a < 0 || A > lim || a > lim)
+          return fail(KG_E_UNSUPPORTED, "reservation slot %d minor %d: gpu allocatable / allocated outside [0, %s]", s,
+                      m, q == 1 ? "2^46" : "2^30");
+      }
+    for (int m = 0; m < kMinors; ++m) {
+      G.acore[m] = (int32_t)r.gpu_alloc[s][m][0];
+      G.amem[m] = r.gpu_alloc[s][m][1];
+      G.aratio[m] = (int32_t)r.gpu_alloc[s][m][2];
+      G.dcore[m] = (int32_t)r.gpu_allocated[s][m][0];
+      G.dmem[m] = r.gpu_allocated[s][m][1];
+      G.dratio[m] = (int32_t)r.gpu_allocated[s][m][2];
+    }
+    d.meta[s] |= RS_GPU;
   }
   return 0;
 }
@@ -5226,6 +5261,7 @@ void kg_engine_destroy(kg_engine* e) {
   e->dsnorm_all.release();
   e->dsval.release();
   e->rsv_d.release();
+  e->rsv_g.release();
   e->rsv_nd.release();
   e->rsv_pd.release();
   e->rsel.release();
@@ -5445,7 +5481,7 @@ int kg_pods_unreserve(kg_engine* e, int64_t first, int64_t count, const uint8_t*
                                         e->rsv_on ? e->rsv_d.p : nullptr, e->out_rslot.p, e->quotas.p, e->nq,
                                         (e->ds_on || e->rsv_on) ? e->qdev.p : nullptr, e->paux.p,
                                         GroupTable{e->grp_d.p, e->capacity}, e->grp_on ? e->gpods.p : nullptr,
-                                        e->GP.hard_w);
+                                        e->GP.hard_w, e->rsv_on && e->ds_on && e->rgpu_nodes > 0 ? e->rsv_g.p : nullptr);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(e->stream));
   e->eph_dirty |= e->eph_any;  // a release may end an ephemeral-storage overcommit
@@ -5665,7 +5701,8 @@ static int schedule_staged_impl(kg_engine* e, int64_t first, int64_t count, kg_s
   // scheduleOne): one pass costs less than a round's eval + merge + resolve when a round would hold one pod
   // (PodTopologySpread / InterPodAffinity profiles: one pod per pass — the batched rounds' stop rules do not cover
   // their cluster-wide minimum / count and min-max normalisation)
-  if (e->exact_on && e->xr_on && !e->grp_on && !e->rsv_ext_q && count >= kXrMin && e->n_nodes > 0)
+  // (ABI 13) GPU-holding reservations: the per-pod pass (the batched rounds keep no DeviceShare restore)
+  if (e->exact_on && e->xr_on && !e->grp_on && !e->rsv_ext_q && e->rgpu_nodes == 0 && count >= kXrMin && e->n_nodes > 0)
     return run_xr(e, first, count, stats, t0);
   if (e->exact_on || (count <= kExactSmall && e->n_ranks == 1)) return run_rsv(e, first, count, stats, t0);
   RoundGeom g;
@@ -6292,9 +6329,24 @@ int kg_nodes_reservation_upsert(kg_engine* e, const kg_node_reservations* r, con
   if (n == 0) return 0;
   std::vector<RsvNode> h(n);
   std::vector<int32_t> hn(n);
+  std::vector<RsvGpu> hg((size_t)n * kRsvSlots);
+  bool any_gpu = false;
   for (int64_t k = 0; k < n; ++k) {
     if (idx[k] < 0 || idx[k] >= e->capacity) return fail(KG_E_INVALID, "node index %d outside capacity", idx[k]);
-    if (int rc = decode_node_rsv(r[k], h[k], hn[k])) return rc;
+    if (int rc = decode_node_rsv(r[k], h[k], hn[k], hg.data() + (size_t)k * kRsvSlots, e->ds_on)) return rc;
+    for (int s = 0; s < hn[k]; ++s) any_gpu |= (h[k].meta[s] & RS_GPU) != 0;
+  }
+  // (ABI 13) the GPU holdings: allocated (zeroed) at the first GPU-holding slot, then scattered with every upsert
+  if (any_gpu && !e->rsv_g.p) {
+    if (int rc = e->rsv_g.ensure((size_t)kRsvSlots * e->capacity)) return rc;
+    HIP_TRY(hipMemsetAsync(e->rsv_g.p, 0, sizeof(RsvGpu) * kRsvSlots * (size_t)e->capacity, e->stream));
+  }
+  if ((int64_t)e->rsv_gnode.size() < e->capacity) e->rsv_gnode.assign(e->capacity, 0);
+  for (int64_t k = 0; k < n; ++k) {
+    bool g = false;
+    for (int s = 0; s < hn[k]; ++s) g |= (h[k].meta[s] & RS_GPU) != 0;
+    e->rgpu_nodes += (int64_t)g - (int64_t)e->rsv_gnode[idx[k]];
+    e->rsv_gnode[idx[k]] = g ? 1 : 0;
   }
   if ((int64_t)e->rsv_pcnt.size() < e->capacity) e->rsv_pcnt.assign(e->capacity, 64);
   for (int64_t k = 0; k < n; ++k) e->rsv_pcnt[idx[k]] = (int16_t)(r[k].n > 0 ? r[k].predicate_count : 64);
@@ -6316,8 +6368,39 @@ int kg_nodes_reservation_upsert(kg_engine* e, const kg_node_reservations* r, con
   scatter_rsv<<<(unsigned)((n + 255) / 256), 256, 0, e->stream>>>(e->rsv_d.p, e->rsv_nd.p, e->rsv_pd.p, dd, dn, dp, di,
                                                                   n);
   HIP_TRY(hipGetLastError());
+  DevBuf<RsvGpuNode> bg;
+  if (e->rsv_g.p) {
+    if (int rc = bg.ensure(n)) return rc;
+    HIP_TRY(hipMemcpyAsync(bg.p, hg.data(), n * sizeof(RsvGpuNode), hipMemcpyHostToDevice, e->stream));
+    scatter_rows<RsvGpuNode><<<(unsigned)((n + 255) / 256), 256, 0, e->stream>>>(
+        reinterpret_cast<RsvGpuNode*>(e->rsv_g.p), bg.p, di, n);
+    HIP_TRY(hipGetLastError());
+  }
   HIP_TRY(hipStreamSynchronize(e->stream));
   b.release();
+  bg.release();
+  return 0;
+}
+
+int kg_nodes_read_reservation_gpus(kg_engine* e, int64_t* gpu_allocated) {
+  if (!e || !gpu_allocated) return fail(KG_E_INVALID, "null argument");
+  if (!e->rsv_on) return fail(KG_E_INVALID, "the profile does not enable Reservation");
+  const int64_t n = e->n_nodes;
+  const size_t per = (size_t)KG_MAX_RSV_SLOTS * KG_MAX_MINORS * 3;
+  std::memset(gpu_allocated, 0, (size_t)n * per * 8);
+  if (n == 0 || !e->rsv_g.p) return 0;
+  std::vector<RsvGpu> h((size_t)n * kRsvSlots);
+  HIP_TRY(hipMemcpyAsync(h.data(), e->rsv_g.p, h.size() * sizeof(RsvGpu), hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  for (int64_t i = 0; i < n; ++i)
+    for (int s = 0; s < kRsvSlots; ++s)
+      for (int m = 0; m < kMinors; ++m) {
+        const RsvGpu& g = h[(size_t)i * kRsvSlots + s];
+        int64_t* o = gpu_allocated + (size_t)i * per + ((size_t)s * KG_MAX_MINORS + m) * 3;
+        o[0] = g.dcore[m];
+        o[1] = g.dmem[m];
+        o[2] = g.dratio[m];
+      }
   return 0;
 }
 

@@ -37,6 +37,7 @@ namespace kg {
 
 constexpr int kRsvSlots = KG_MAX_RSV_SLOTS;
 constexpr uint32_t RS_AVAIL = 1u << 0, RS_ONCE = 1u << 1, RS_UNSCHED = 1u << 2;  // policy in bits 4..5
+constexpr uint32_t RS_GPU = 1u << 3;  // (ABI 13) the reservation holds GPUs: its RsvGpu row is live
 constexpr uint32_t RP_AFFINITY = 1u << 0, RP_RESERVE = 1u << 1, RP_OPERATING = 1u << 2, RP_SEL = 1u << 3;
 constexpr int RP_POLICY_SHIFT = 8;  // flags bits 8..9: the allocate policy of a reserve / operating-mode pod
 constexpr int64_t kDefaultMilliCpu = 100, kDefaultMemory = 200ll << 20;  // schedutil.GetNonzeroRequests defaults
@@ -78,6 +79,27 @@ struct RsvParams {
   int32_t filter, score, weight, pad;
 };
 
+// (ABI 13) One reservation's GPU holding (deviceshare/reservation.go:133-160): the reserve pod's allocation per minor
+// (the reservation's allocatable) and the allocations of its assigned pods on those minors (appendAllocatedByHints).
+// 272 B per slot, [cap][kRsvSlots]; read only for a pod with device requests on a node with an RS_GPU slot.
+struct RsvGpu {
+  int32_t acore[kMinors], aratio[kMinors];  // allocatable: gpu-core, gpu-memory-ratio
+  int32_t dcore[kMinors], dratio[kMinors];  // allocated by the assigned pods
+  int64_t amem[kMinors], dmem[kMinors];     // gpu-memory bytes
+  uint32_t minors;                          // the reserve pod's minors
+  uint32_t pad[3];
+};
+static_assert(sizeof(RsvGpu) == 272, "RsvGpu layout");
+struct RsvGpuNode {  // one node's slots (the upsert's scatter row)
+  RsvGpu s[kRsvSlots];
+};
+__device__ __forceinline__ int64_t rg_a(const RsvGpu& g, int m, int q) {
+  return q == 0 ? (int64_t)g.acore[m] : (q == 1 ? g.amem[m] : (int64_t)g.aratio[m]);
+}
+__device__ __forceinline__ int64_t rg_d(const RsvGpu& g, int m, int q) {
+  return q == 0 ? (int64_t)g.dcore[m] : (q == 1 ? g.dmem[m] : (int64_t)g.dratio[m]);
+}
+
 // DeviceShare + ElasticQuota context of the C5 pass (ds = nullptr: no DeviceShare in the profile; nq = 0: no quotas)
 struct RsvExt {
   const DsNode* __restrict__ ds;       // [cap] node devices (deviceUsed updated by Reserve)
@@ -112,6 +134,11 @@ struct RsvExt {
   const uint64_t* __restrict__ rsv_pred;  // [cap][kRsvSlots] the slots' fakeNode predicates (reservation affinity)
   const RsvSel* __restrict__ rsv_sel;     // [pods] the RP_SEL pods' selectors / terms (RsvPod::aux)
   uint64_t* __restrict__ gzm;          // [2 parities] the present zones
+  // (ABI 13) reservations holding GPUs (rgpu = nullptr: none in the cluster, or DeviceShare / Reservation off); the
+  // Reserve re-runs the winner's restore, so it needs the pod's Reservation view and the slot counts
+  RsvGpu* __restrict__ rgpu;           // [cap][kRsvSlots]
+  const RsvPod* __restrict__ rpods;    // [pods]
+  const int32_t* __restrict__ rsv_n;   // [cap]
 };
 // pod j's zone sums (double-buffered by parity: group_pre(j) accumulates, rsv_select(j) clears j + 1's)
 __device__ __forceinline__ ZoneSums zone_sums(const RsvExt& X, int64_t j) {
@@ -173,7 +200,7 @@ template <bool kExt = true>
 __device__ __forceinline__ void rsv_restore(const RsvNode& rn, int ns, const RsvPod& rp, const uint64_t* pred_row,
                                             const RsvSel* sel, Row& r, uint32_t& mm, int& nm,
                                             int64_t& pr_c, int64_t& pr_m, int64_t& ra_c, int64_t& ra_m,
-                                            bool& has_state) {
+                                            bool& has_state, uint32_t* um_out = nullptr) {
   uint32_t um = 0;
 #pragma unroll
   for (int s = 0; s < kRsvSlots; ++s) {
@@ -191,6 +218,7 @@ __device__ __forceinline__ void rsv_restore(const RsvNode& rn, int ns, const Rsv
     else if (rn.assigned[s] > 0) um |= 1u << s;
   }
   has_state = (mm | um) != 0 && !((rp.flags & RP_AFFINITY) && mm == 0);  // transformer.go:127-136
+  if (um_out) *um_out = has_state ? um : 0u;
   if (!has_state) return;
 #pragma unroll
   for (int s = 0; s < kRsvSlots; ++s)
@@ -223,6 +251,99 @@ __device__ __forceinline__ void rsv_restore(const RsvNode& rn, int ns, const Rsv
     }
 }
 
+// ---- (ABI 13) DeviceShare with reservations holding GPUs --------------------------------------------------------
+// The plugin's restore of one node for one pod (RestoreReservation + mergeReservationAllocations, reservation.go:84-171)
+// over the GPU-holding slots of the Reservation restore's matched (mt) / unmatched (um) lists.  The preemptible maps it
+// builds are evaluated per (minor, resource) where used instead of materialized:
+//   node view   (Filter fallback, Score / Reserve without a nominated GPU reservation):
+//               mergedUnmatchedUsed + mergedMatchedAllocatable
+//   slot view s (tryAllocateFromReservation / scoreWithReservation of matched slot s):
+//               mergedUnmatchedUsed + mergedMatchedAllocated + remained(s)
+// with mergedUnmatchedUsed = Σ_unmatched min(allocatable, allocated) (allocatable − remained), remained =
+// SubtractWithNonNegativeResult(allocatable, allocated).  calcFreeWithPreemptible (device_cache.go:314-342) then gives
+// free = total − max(0, used − preemptible), non-negative, on every minor; a Restricted slot's second Allocate sees only
+// its own minors with their remained resources (requiredDeviceResources, calcRequiredDeviceResources).
+struct DsrCtx {
+  const RsvGpu* g;  // the node's [kRsvSlots] rows
+  uint32_t um, mt;  // GPU-holding unmatched / matched slots
+};
+__device__ __forceinline__ int64_t dsr_pre(const DsrCtx& c, int m, int q, int slot) {
+  int64_t v = 0;
+#pragma unroll
+  for (int s = 0; s < kRsvSlots; ++s) {
+    if (!(((c.um | c.mt) >> s) & 1u)) continue;
+    const int64_t A = rg_a(c.g[s], m, q), a = rg_d(c.g[s], m, q);
+    if ((c.um >> s) & 1u) v += A < a ? A : a;
+    else v += slot < 0 ? A : a;
+  }
+  if (slot >= 0) v += rsv_nn(rg_a(c.g[slot], m, q), rg_d(c.g[slot], m, q));
+  return v;
+}
+__device__ __forceinline__ int64_t ds_tot(const DsNode& d, int m, int q) {
+  return q == 0 ? (int64_t)d.tcore[m] : (q == 1 ? d.tmem[m] : (int64_t)d.tratio[m]);
+}
+__device__ __forceinline__ int64_t ds_used(const DsNode& d, int m, int q) {
+  return q == 0 ? (int64_t)d.ucore[m] : (q == 1 ? d.umem[m] : (int64_t)d.uratio[m]);
+}
+// the free resources of minor m in a view (slot < 0: the node view; rr: a Restricted slot's required view)
+__device__ __forceinline__ void dsr_free(const DsNode& d, const DsrCtx& c, int m, int slot, bool rr, int64_t f[3]) {
+#pragma unroll
+  for (int q = 0; q < 3; ++q)
+    f[q] = rr ? rsv_nn(rg_a(c.g[slot], m, q), rg_d(c.g[slot], m, q))
+              : rsv_nn(ds_tot(d, m, q), rsv_nn(ds_used(d, m, q), dsr_pre(c, m, q, slot)));
+}
+struct DsrView {
+  bool any;    // some minor of the view has free resources (nodeDevice.filter keeps the GPU type)
+  int nfit;    // minors the per-instance request fits (within `req` when set)
+  int64_t T[3], F[3];
+};
+__device__ __forceinline__ DsrView dsr_view(const DsNode& d, const DsInst& in, const DsrCtx& c, int slot, bool rr,
+                                           uint32_t req) {
+  DsrView v{false, 0, {0, 0, 0}, {0, 0, 0}};
+  const uint32_t minors = rr ? c.g[slot].minors & (uint32_t)d.present : (uint32_t)d.present;
+  for (int m = 0; m < kMinors; ++m) {
+    if (!((minors >> m) & 1u)) continue;
+    int64_t f[3];
+    dsr_free(d, c, m, slot, rr, f);
+    const bool nz = (f[0] | f[1] | f[2]) != 0;
+    v.any |= nz;
+    v.nfit += (nz && (!req || ((req >> m) & 1u)) && in.core <= f[0] && in.mem <= f[1] && in.ratio <= f[2]) ? 1 : 0;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      v.T[q] += ds_tot(d, m, q);
+      v.F[q] += f[q];
+    }
+  }
+  return v;
+}
+__device__ __forceinline__ int64_t dsr_score(const DsrView& v, const DsInst& in, const DsParams& P) {
+  if (!v.any) return 0;
+  int64_t num = 0, ws = 0;
+  const bool most = P.most != 0;
+  ds_term(P.w_core, v.T[0], v.F[0], in.core, num, ws, most);
+  ds_term(P.w_mem, v.T[1], v.F[1], in.mem, num, ws, most);
+  ds_term(P.w_ratio, v.T[2], v.F[2], in.ratio, num, ws, most);
+  return ws ? div_small(num, ws) : 0;
+}
+// tryAllocateFromReservation([s]) feasibility (reservation.go:196-236): Default / Aligned — Allocate(nil, preferred,
+// nil, preemptible); Restricted — with required = preferred = the slot's minors, then again on its remained resources
+__device__ __forceinline__ bool dsr_slot_ok(const DsNode& d, const DsInst& in, const DsrCtx& c, int s, bool restricted) {
+  if (!restricted) {
+    const DsrView v = dsr_view(d, in, c, s, false, 0u);
+    return v.any && v.nfit >= in.count;
+  }
+  const uint32_t req = c.g[s].minors;
+  const DsrView v1 = dsr_view(d, in, c, s, false, req);
+  if (!(v1.any && v1.nfit >= in.count)) return false;
+  const DsrView v2 = dsr_view(d, in, c, s, true, req);
+  return v2.any && v2.nfit >= in.count;
+}
+// scoreWithReservation of slot s (reservation.go:246-272): the required view for Restricted, else the slot view
+__device__ __forceinline__ int64_t dsr_slot_score(const DsNode& d, const DsInst& in, const DsrCtx& c, int s,
+                                                  bool restricted, const DsParams& P) {
+  return dsr_score(dsr_view(d, in, c, s, restricted, 0u), in, P);
+}
+
 // kSlotsInRegs = false: the slot record is read where used (the wide exact pass, register-bound); kExt = false: no
 // reserve-pod / operating-mode / reservation-selector logic (the batched exact rounds; the host routes queues holding
 // such pods to the per-pod pass)
@@ -242,6 +363,7 @@ __device__ __forceinline__ RsvOut rsv_eval_node(const DevTable& T, const RsvNode
   Row r = load_row(T, i);
   const int ns = rsv_n[i];
   uint32_t mm = 0;  // matched slots
+  uint32_t um = 0;  // unmatched slots with assigned pods (the restore's unmatched list)
   int nm = 0;
   int64_t pr_c = 0, pr_m = 0, ra_c = 0, ra_m = 0;
   bool has_state = false;
@@ -254,7 +376,7 @@ __device__ __forceinline__ RsvOut rsv_eval_node(const DevTable& T, const RsvNode
   if (ns > 0)
     rsv_restore<kExt>(rn, ns, rp, X.rsv_pred ? X.rsv_pred + (size_t)i * kRsvSlots : nullptr,
                 (rp.flags & RP_SEL) && X.rsv_sel ? X.rsv_sel + rp.aux : nullptr, r, mm, nm, pr_c, pr_m, ra_c, ra_m,
-                has_state);
+                has_state, &um);
   if (dbg) {
     dbg->matched = mm;
     dbg->has_state = has_state ? 1 : 0;
@@ -301,10 +423,42 @@ __device__ __forceinline__ RsvOut rsv_eval_node(const DevTable& T, const RsvNode
   // plugin.go:361-364, 423-426 (a reserve pod skips this part of the Filter, :357)
   if (RP.filter && (rp.flags & RP_AFFINITY) && !(kExt && (rp.flags & RP_RESERVE)) && sat == 0) return o;
   int64_t dsraw = 0;
-  if (X.ds && dp && !dp->skip) {  // DeviceShare Filter + raw Score (node level: no device-holding reservations)
-    if (!ds_eval(X.ds[i], *dp, X.DP, dsraw)) return o;
-    // DeviceShare.FilterReservation rejects every reservation for a pod that requests devices
-    if (X.DP.filter) sat = 0;
+  // (ABI 13) DeviceShare with the node's GPU-holding reservations (reservation.go, plugin.go:280-330): dsr = the
+  // plugin keeps a restore state here; dsok = the GPU-holding matched slots it can allocate from (FilterReservation)
+  bool dsr = false;
+  uint32_t dsok = 0;
+  DsrCtx dc{nullptr, 0u, 0u};
+  DsInst din{0, 0, 0, 0, 0};
+  if (X.ds && dp && !dp->skip) {
+    const DsNode& d = X.ds[i];
+    uint32_t gslots = 0;
+    if (kExt && X.rgpu && has_state)  // the batched exact rounds never see GPU reservations (host routing)
+#pragma unroll
+      for (int s = 0; s < kRsvSlots; ++s) gslots |= (s < ns && (rn.meta[s] & RS_GPU)) ? (1u << s) : 0u;
+    dsr = (gslots & (mm | um)) != 0 && !dp->error && d.has_device;
+    if (!dsr) {  // the node-level Filter + raw Score
+      if (!ds_eval(d, *dp, X.DP, dsraw)) return o;
+    } else {
+      din = ds_instance(d, *dp);
+      if (!din.ok) return o;
+      dc = DsrCtx{X.rgpu + (size_t)i * kRsvSlots, um & gslots, mm & gslots};
+#pragma unroll
+      for (int s = 0; s < kRsvSlots; ++s)
+        if (((dc.mt >> s) & 1u) &&
+            dsr_slot_ok(d, din, dc, s, ((rn.meta[s] >> 4) & 3) == KG_RSV_POLICY_RESTRICTED))
+          dsok |= 1u << s;
+      // Filter: a matched GPU reservation that fits, else (unless the pod requires a reservation) the node with every
+      // matched reservation's allocatable returned
+      bool pass = dsok != 0;
+      if (!pass && !(dc.mt != 0 && (rp.flags & RP_AFFINITY))) {
+        const DsrView v = dsr_view(d, din, dc, -1, false, 0u);
+        pass = v.any && v.nfit >= din.count;
+      }
+      if (X.DP.filter && !pass) return o;
+    }
+    // FilterReservation: a pod with device requests can use only a GPU-holding reservation DeviceShare can allocate
+    // from (plugin.go:333-380: "no relevant Reservation information" for the others)
+    sat &= dsok;
   }
   if (X.ns && np) {  // NodeNUMAResource Filter + Score on the restored NodeInfo; Reserve reuses the stored affinity
     const NumaView nv = make_view(X.ns + i, X.nm + i, X.NP);
@@ -343,12 +497,27 @@ __device__ __forceinline__ RsvOut rsv_eval_node(const DevTable& T, const RsvNode
 #pragma unroll
     for (int s = 0; s < kRsvSlots; ++s) ssc[s] = (sat >> s & 1) ? rsv_score_slot(rn, s, p) : 0;
     if (pick < 0) {
+      // (ABI 13) prioritizeReservations sums every reservation score plugin: DeviceShare's ScoreReservation
+      // (scoreWithNominatedReservation) normalized by DefaultReservationNormalizeScore over the candidates
+      int32_t dnorm[kRsvSlots] = {0, 0, 0, 0};
+      if (dsr && sat) {
+        int64_t dsc[kRsvSlots] = {0, 0, 0, 0}, dmax = 0;
+#pragma unroll
+        for (int s = 0; s < kRsvSlots; ++s)
+          if (sat >> s & 1) {
+            dsc[s] = dsr_slot_score(X.ds[i], din, dc, s, ((rn.meta[s] >> 4) & 3) == KG_RSV_POLICY_RESTRICTED, X.DP);
+            dmax = dsc[s] > dmax ? dsc[s] : dmax;
+          }
+        if (dmax > 0)
+#pragma unroll
+          for (int s = 0; s < kRsvSlots; ++s) dnorm[s] = (sat >> s & 1) ? (int32_t)div_small(100 * dsc[s], dmax) : 0;
+      }
       int32_t best = -1;
 #pragma unroll
       for (int s = 0; s < kRsvSlots; ++s)
         if (sat >> s & 1) {
-          if (ssc[s] > best) {  // prioritizeReservations + sort (unstable; pinned: lowest slot on ties)
-            best = ssc[s];
+          if (ssc[s] + dnorm[s] > best) {  // prioritizeReservations + sort (unstable; pinned: lowest slot on ties)
+            best = ssc[s] + dnorm[s];
             pick = s;
           }
         }
@@ -359,6 +528,14 @@ __device__ __forceinline__ RsvOut rsv_eval_node(const DevTable& T, const RsvNode
     for (int s = 0; s < kRsvSlots; ++s)
       if (s == pick) raw = ssc[s];
     o.raw = raw;
+  }
+  if (dsr && X.DP.score) {  // Score (scoring.go:34-89): the nominated reservation's, else the node view's
+    const DsNode& d = X.ds[i];
+    if (o.nom >= 0 && ((dc.mt >> o.nom) & 1u))
+      dsraw = dsr_slot_score(d, din, dc, o.nom, ((rn.meta[o.nom] >> 4) & 3) == KG_RSV_POLICY_RESTRICTED, X.DP);
+    else
+      dsraw = dsr_score(dsr_view(d, din, dc, -1, false, 0u), din, X.DP);
+    o.dsraw = (int32_t)dsraw;
   }
   return o;
 }
@@ -447,6 +624,92 @@ __device__ __forceinline__ int32_t rsv_ds_reserve(DsNode& dn, const DsPod& dp, c
   return (int32_t)taken;
 }
 
+// (ABI 13) Allocate over a view (device_allocator.go:89-129, 384-454 + sortDeviceResourcesByMinor): the first `count`
+// fitting minors in (preferred first, scoreDevice desc, minor asc) order, within `req` when set.  -1 = Insufficient.
+__device__ __forceinline__ int32_t dsr_allocate(const DsNode& d, const DsInst& in, const DsrCtx& c, int slot, bool rr,
+                                                uint32_t req, uint32_t pref, const DsParams& P) {
+  const uint32_t minors = rr ? c.g[slot].minors & (uint32_t)d.present : (uint32_t)d.present;
+  int64_t sc[kMinors];
+  uint32_t fit = 0;
+  bool any = false;
+  const bool most = P.most != 0;
+  for (int m = 0; m < kMinors; ++m) {
+    sc[m] = 0;
+    if (!((minors >> m) & 1u)) continue;
+    int64_t f[3];
+    dsr_free(d, c, m, slot, rr, f);
+    const bool nz = (f[0] | f[1] | f[2]) != 0;
+    any |= nz;
+    if (nz && (!req || ((req >> m) & 1u)) && in.core <= f[0] && in.mem <= f[1] && in.ratio <= f[2]) fit |= 1u << m;
+    int64_t num = 0, ws = 0;  // scoreDevice (scoring.go:183-203)
+    ds_term(P.w_core, ds_tot(d, m, 0), f[0], in.core, num, ws, most);
+    ds_term(P.w_mem, ds_tot(d, m, 1), f[1], in.mem, num, ws, most);
+    ds_term(P.w_ratio, ds_tot(d, m, 2), f[2], in.ratio, num, ws, most);
+    sc[m] = ws ? div_small(num, ws) : 0;
+  }
+  if (!any || __popc(fit) < in.count) return -1;
+  uint32_t taken = 0;
+  for (int k = 0; k < in.count; ++k) {
+    int best = -1;
+    for (int m = 0; m < kMinors; ++m) {
+      if (!(((fit & ~taken) >> m) & 1u)) continue;
+      if (best < 0) {
+        best = m;
+        continue;
+      }
+      const int pm = (pref >> m) & 1, pb = (pref >> best) & 1;
+      if (pm > pb || (pm == pb && sc[m] > sc[best])) best = m;
+    }
+    taken |= 1u << best;
+  }
+  return (int32_t)taken;
+}
+
+// (ABI 13) DeviceShare Reserve with the node's GPU-holding reservations (plugin.go:388-437): the nominated reservation
+// alone (allocateWithNominatedReservation → tryAllocateFromReservation, not required; none for a reserve pod), else the
+// node view; updateCacheUsed adds the per-instance request to the allocated minors.  -1 = no allocation.
+__device__ __forceinline__ int32_t rsv_ds_reserve_gpu(DsNode& dn, const DsPod& dp, const DsParams& DP, const DsrCtx& c,
+                                                      int nominated, bool restricted, bool reserve_pod) {
+  if (dp.skip || !dn.has_device) return 0;
+  if (dp.error) return -1;
+  const DsInst in = ds_instance(dn, dp);
+  if (!in.ok) return -1;
+  int32_t mask = -1;
+  if (nominated >= 0 && ((c.mt >> nominated) & 1u) && !reserve_pod) {
+    const uint32_t pref = c.g[nominated].minors;
+    if (restricted) {
+      const DsrView v1 = dsr_view(dn, in, c, nominated, false, pref);
+      if (v1.any && v1.nfit >= in.count) mask = dsr_allocate(dn, in, c, nominated, true, pref, pref, DP);
+    } else {
+      mask = dsr_allocate(dn, in, c, nominated, false, 0u, pref, DP);
+    }
+  }
+  if (mask < 0) mask = dsr_allocate(dn, in, c, -1, false, 0u, 0u, DP);
+  if (mask <= 0) return mask;
+#pragma unroll
+  for (int m = 0; m < kMinors; ++m)
+    if ((mask >> m) & 1) {
+      dn.ucore[m] += (int32_t)in.core;
+      dn.uratio[m] += (int32_t)in.ratio;
+      dn.umem[m] += in.mem;
+    }
+  return mask;
+}
+
+// the pod's allocation on reservation slot s's minors (appendAllocatedByHints): sign +1 when assumed into it, −1 when
+// it leaves (SubtractWithNonNegativeResult)
+__device__ __forceinline__ void rsv_gpu_assign(RsvGpu& g, const DsInst& in, int32_t mask, int sign) {
+  const uint32_t mm = (uint32_t)mask & g.minors;
+  for (int m = 0; m < kMinors; ++m) {
+    if (!((mm >> m) & 1u)) continue;
+    const int64_t c = (int64_t)g.dcore[m] + sign * in.core, r = (int64_t)g.dratio[m] + sign * in.ratio,
+                  b = g.dmem[m] + sign * in.mem;
+    g.dcore[m] = (int32_t)(c > 0 ? c : 0);
+    g.dratio[m] = (int32_t)(r > 0 ? r : 0);
+    g.dmem[m] = b > 0 ? b : 0;
+  }
+}
+
 __device__ __forceinline__ void rsv_quota_charge(const RsvExt& X, const DevPod& p, int64_t j) {
   if (X.nq == 0 || p.quota < 0) return;
   quota_row_charge(X.quotas[p.quota], quota_req(p, X.qdev + (size_t)j * kQuotaRes), (p.flags & P_NONPREEMPT) != 0);
@@ -480,9 +743,38 @@ __device__ __forceinline__ bool rsv_reserve(const DevTable& T, RsvNode* __restri
     }
   }
   KG_LANE_SUB(diag_j, 1);
+  int32_t gpu_minors = 0;  // (ABI 13) the DeviceShare allocation, for the reservation's allocated GPUs below
   if (DS && X.ds) {
     DsNode dn = X.ds[w];
-    const int32_t minors = rsv_ds_reserve(dn, X.dpods[j], X.DP);
+    int32_t minors = 0;
+    bool done = false;
+    // (ABI 13) the winner's DeviceShare restore again (reservation.go:118-171) when it holds GPU reservations
+    if (X.rgpu && X.rsv_n && X.rpods && !X.dpods[j].skip) {
+      const int ns = X.rsv_n[w];
+      uint32_t gslots = 0;
+      for (int s = 0; s < kRsvSlots; ++s) gslots |= (s < ns && (RN[w].meta[s] & RS_GPU)) ? (1u << s) : 0u;
+      if (gslots) {
+        const RsvNode rn = RN[w];
+        const RsvPod rp = X.rpods[j];
+        Row rr = load_row(T, w);
+        uint32_t mm = 0, um = 0;
+        int nm = 0;
+        int64_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+        bool hs = false;
+        rsv_restore<true>(rn, ns, rp, X.rsv_pred ? X.rsv_pred + (size_t)w * kRsvSlots : nullptr,
+                          (rp.flags & RP_SEL) && X.rsv_sel ? X.rsv_sel + rp.aux : nullptr, rr, mm, nm, a0, a1, a2, a3,
+                          hs, &um);
+        if (hs && (gslots & (mm | um))) {
+          const DsrCtx c{X.rgpu + (size_t)w * kRsvSlots, um & gslots, mm & gslots};
+          const int nom = (int)(v & 7) - 1;
+          minors = rsv_ds_reserve_gpu(dn, X.dpods[j], X.DP, c, nom,
+                                      nom >= 0 && ((rn.meta[nom] >> 4) & 3) == KG_RSV_POLICY_RESTRICTED,
+                                      (rp.flags & RP_RESERVE) != 0);
+          done = true;
+        }
+      }
+    }
+    if (!done) minors = rsv_ds_reserve(dn, X.dpods[j], X.DP);
     KG_LANE_SUB(diag_j, 2);
     if (minors < 0) {
       X.out_minors[j] = 0;
@@ -490,6 +782,7 @@ __device__ __forceinline__ bool rsv_reserve(const DevTable& T, RsvNode* __restri
     }
     if (minors) const_cast<DsNode*>(X.ds)[w] = dn;
     X.out_minors[j] = minors;
+    gpu_minors = minors;
   }
   if (NUMA && X.ns) {
     X.nm[w] = nmw;
@@ -526,6 +819,9 @@ __device__ __forceinline__ bool rsv_reserve(const DevTable& T, RsvNode* __restri
     if (RN[w].alloc_cpu[slot] > 0) RN[w].allocd_cpu[slot] += p.req_cpu;
     if (RN[w].alloc_mem[slot] > 0) RN[w].allocd_mem[slot] += p.req_mem;
     RN[w].assigned[slot] += 1;
+    // (ABI 13) the reservation's allocated GPUs: the pod's allocation on its minors
+    if (DS && X.rgpu && gpu_minors > 0 && (RN[w].meta[slot] & RS_GPU))
+      rsv_gpu_assign(X.rgpu[(size_t)w * kRsvSlots + slot], ds_instance(X.ds[w], X.dpods[j]), gpu_minors, +1);
   }
   slot_out = slot;
   KG_LANE_SUB(diag_j, 5);

@@ -193,6 +193,13 @@ class Engine:
         check(self.lib, self.lib.kg_nodes_read_reservations(self.h, *[ptr(o) for o in out]))
         return tuple(out)
 
+    def read_reservation_gpus(self):
+        """(ABI 13) the reservation slots' gpu_allocated, int64[n, KG_MAX_RSV_SLOTS, KG_MAX_MINORS, 3], from the device
+        (kg_nodes_read_reservation_gpus)."""
+        out = np.zeros((self.num_nodes, abi.MAX_RSV_SLOTS, abi.MAX_MINORS, 3), dtype=np.int64)
+        check(self.lib, self.lib.kg_nodes_read_reservation_gpus(self.h, ptr(out)))
+        return out
+
     def read_pod_groups(self, zone: bool = False):
         """(ABI 12) per node and match group: (pods matching, required anti-affinity terms, symmetric weight) — and,
         with zone, the zone-keyed terms' (anti-affinity, symmetric weight) — int32[n, KG_MAX_MATCH_GROUPS] each, from

@@ -436,12 +436,51 @@ def load_rsv_into(engine, cluster: Cluster, rsv: np.ndarray):
 N_QUOTAS = 16
 
 
-def make_c5_cluster(n_nodes: int, seed: int = BASE_SEED + 10) -> tuple:
+def make_c5_cluster(n_nodes: int, seed: int = BASE_SEED + 10, gpu_rsv_frac: float = 0.0) -> tuple:
     """(Cluster, kg_node_device[n], kg_node_reservations[n]) for config C5 as one profile: make_gpu_cluster's GPU nodes
-    with make_rsv_cluster's reservations on top (cpu / memory reservations; the reserve pods in NodeInfo)."""
+    with make_rsv_cluster's reservations on top (cpu / memory reservations; the reserve pods in NodeInfo).
+    gpu_rsv_frac > 0 (ABI 13): that fraction of the reservations on nodes with a Device object also hold GPUs
+    (add_gpu_reservations)."""
     cluster, dev = make_gpu_cluster(n_nodes, seed=seed)
     cluster, rsv = make_rsv_cluster(n_nodes, seed=seed + 1, cluster=cluster)
+    if gpu_rsv_frac > 0:
+        add_gpu_reservations(dev, rsv, gpu_rsv_frac, seed=seed + 3)
     return cluster, dev, rsv
+
+
+def add_gpu_reservations(dev: np.ndarray, rsv: np.ndarray, frac: float, seed: int = BASE_SEED + 24) -> None:
+    """(ABI 13) Reservations holding GPUs, in place: `frac` of the reservations on nodes with a Device object get a
+    reserve pod allocation of 1–2 healthy minors, gpu-memory-ratio ∈ {25, 50, 100} each (gpu-core the same, gpu-memory
+    the ratio's bytes); each of the reservation's assigned pods used a quarter of it on its first minor, half of them
+    on the second too (appendAllocatedByHints: the allocations inside the reservation's minors).  Every allocation
+    is added to the node's deviceUsed, as the bound reserve pod and assigned pods are in nodeDevice.deviceUsed; a minor
+    may end up over-used (used > total), which calcFreeWithPreemptible clamps."""
+    rng = np.random.default_rng(seed)
+    S = abi.MAX_RSV_SLOTS
+    for i in np.nonzero((rsv["n"] > 0) & (dev["has_device"] != 0))[0]:
+        ok = np.nonzero(dev["healthy"][i] & dev["present"][i])[0]
+        if len(ok) == 0:
+            continue
+        for s in range(int(rsv["n"][i])):
+            if rng.random() >= frac:
+                continue
+            k = 1 if rng.random() < 0.7 or len(ok) < 2 else 2
+            minors = rng.choice(ok, k, replace=False)
+            ratio = int(rng.choice([25, 50, 100]))
+            for m in minors:
+                rsv["gpu_alloc"][i, s, m] = (ratio, ratio * GPU_MEM // 100, ratio)
+            rsv["gpu_minors"][i, s] = int(sum(1 << int(m) for m in minors))
+            a = rsv["gpu_allocated"][i, s]
+            for q in range(int(rsv["assigned"][i, s])):
+                share = ratio // 4
+                for t, m in enumerate(minors):
+                    if t == 0 or q % 2 == 0:
+                        a[m] += (share, share * GPU_MEM // 100, share)
+            for m in range(abi.MAX_MINORS):
+                al, ad = rsv["gpu_alloc"][i, s, m], rsv["gpu_allocated"][i, s, m]
+                dev["used_core"][i, m] += al[0] + ad[0]
+                dev["used_memory"][i, m] += al[1] + ad[1]
+                dev["used_ratio"][i, m] += al[2] + ad[2]
 
 
 def make_c5_pods(n_pods: int, seed: int = BASE_SEED + 11) -> np.ndarray:

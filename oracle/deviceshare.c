@@ -13,6 +13,7 @@ static int valid_percentage(int64_t v) { return !(v > 100 && v % 100 != 0); }
  * ConvertDeviceRequest (:181-192, mapper table :92-149) */
 int or_ds_pod_init(const kg_pod* pod, or_ds_pod* out) {
   memset(out, 0, sizeof(*out));
+  out->reserve = (pod->flags & KG_POD_RESERVE) != 0;
   const int64_t* q = pod->device_requests;
   for (int r = 0; r < KG_DEV_RES_MAX; r++)
     if (q[r] < 0) { out->error = 1; return 0; }
@@ -225,4 +226,292 @@ int or_ds_instance_flat(const kg_node_device* d, const or_ds_pod* p, int64_t* ou
   const or_ds_inst in = or_ds_instance(d, p);
   out[0] = in.count; out[1] = in.core; out[2] = in.mem; out[3] = in.ratio;
   return in.ok;
+}
+
+/* ===================================================================================================================
+ * (ABI 13) Reservations that hold GPUs (deviceshare/reservation.go, plugin.go:280-459, scoring.go:34-160,
+ * device_allocator.go:89-129, device_cache.go:314-391, device_resources.go:47-208).  Device resources are kept per minor
+ * as {gpu-core, gpu-memory, gpu-memory-ratio}; a minor absent from a map holds zeros, which every formula below
+ * treats exactly as the reference treats an absent key / minor (SubtractWithNonNegativeResult, appendAllocated,
+ * calcFreeWithPreemptible's merge, LessThanOrEqual over the free resources' keys — all three keys are present on a
+ * healthy GPU).
+ * =================================================================================================================== */
+
+static int64_t mn64(int64_t a, int64_t b) { return a < b ? a : b; }
+
+/* RestoreReservation + mergeReservationAllocations (reservation.go:84-171) over the GPU-holding slots of the
+ * Reservation restore's matched / unmatched lists: remained = SubtractWithNonNegativeResult(allocatable, allocated);
+ * mergedUnmatchedUsed += allocatable − remained (= min(allocatable, allocated)); mergedMatchedAllocatable /
+ * mergedMatchedAllocated += allocatable / allocated */
+void or_ds_rsv_init(const kg_node_reservations* r, const int32_t* matched, int n_matched, const int32_t* unmatched,
+                    int n_unmatched, or_ds_rsv* out) {
+  memset(out, 0, sizeof(*out));
+  if (!r) return;
+  for (int k = 0; k < n_unmatched; k++) {
+    const int s = unmatched[k];
+    if (!r->gpu_minors[s]) continue;
+    for (int m = 0; m < KG_MAX_MINORS; m++)
+      for (int q = 0; q < 3; q++) out->unm_used[m][q] += mn64(r->gpu_alloc[s][m][q], r->gpu_allocated[s][m][q]);
+  }
+  for (int k = 0; k < n_matched; k++) {
+    const int s = matched[k];
+    if (!r->gpu_minors[s]) continue;
+    out->matched[out->n_matched++] = s;
+    for (int m = 0; m < KG_MAX_MINORS; m++)
+      for (int q = 0; q < 3; q++) {
+        out->mat_alloc[m][q] += r->gpu_alloc[s][m][q];
+        out->mat_allocd[m][q] += r->gpu_allocated[s][m][q];
+      }
+  }
+}
+
+/* calcFreeWithPreemptible (device_cache.go:314-342): free = SubtractWithNonNegativeResult(total,
+ * SubtractWithNonNegativeResult(used, preemptible)) on every minor (a minor without preemptible keeps total − used) */
+static int64_t free_pre(const kg_node_device* d, int m, int q, const int64_t (*pre)[3]) {
+  const int64_t u = sub0(used(d, m, q), pre ? pre[m][q] : 0);
+  return sub0(tot(d, m, q), u);
+}
+
+/* AutopilotAllocator.Allocate / score over a filtered nodeDevice (device_allocator.go:89-155, 499-522): the minors and
+ * free resources it sees — every listed minor with the preemptible-merged free, or, with requiredDeviceResources
+ * (a Restricted reservation), only the reservation's minors with their remained resources.  Returns 0 when the GPU
+ * type is dropped (nodeDevice.filter: free resources all zero). */
+static int dsr_view(const kg_node_device* d, const int64_t (*pre)[3], uint32_t rr_minors, const int64_t (*rr)[3],
+                    int64_t fr[KG_MAX_MINORS][3], uint32_t* minors) {
+  *minors = 0;
+  int any = 0;
+  for (int m = 0; m < KG_MAX_MINORS; m++) {
+    for (int q = 0; q < 3; q++) fr[m][q] = 0;
+    if (!d->present[m]) continue;
+    if (rr) {
+      if (!((rr_minors >> m) & 1u)) continue;
+      for (int q = 0; q < 3; q++) fr[m][q] = rr[m][q];
+    } else {
+      for (int q = 0; q < 3; q++) fr[m][q] = free_pre(d, m, q, pre);
+    }
+    *minors |= 1u << m;
+    any |= fr[m][0] != 0 || fr[m][1] != 0 || fr[m][2] != 0;
+  }
+  return any;
+}
+
+/* Allocate(required, preferred, requiredDeviceResources, preemptible): defaultAllocateDevices over the view — pairs in
+ * sortDeviceResourcesByMinor order (preferred first, then scoreDevice desc when a scorer is set — Reserve and Score,
+ * not Filter —, then minor asc), skipping minors outside `required`, all-zero minors and minors the per-instance request
+ * does not fit; the first desiredCount.  Returns the minor mask, -1 = Insufficient. */
+int32_t or_ds_allocate(const kg_node_device* d, const or_ds_pod* p, uint32_t required, uint32_t preferred,
+                       uint32_t rr_minors, const int64_t (*rr)[3], const int64_t (*pre)[3], int scored, int strategy,
+                       const int64_t w[3]) {
+  if (p->skip || !d->has_device) return 0;
+  if (p->error) return -1;
+  const or_ds_inst in = or_ds_instance(d, p);
+  if (!in.ok) return -1;
+  int64_t fr[KG_MAX_MINORS][3];
+  uint32_t minors = 0;
+  if (!dsr_view(d, pre, rr_minors, rr, fr, &minors)) return -1;
+  int order[KG_MAX_MINORS], n = 0;
+  int64_t sc[KG_MAX_MINORS] = {0};
+  for (int m = 0; m < KG_MAX_MINORS; m++) {
+    if (!((minors >> m) & 1u)) continue;
+    if (scored) {
+      const int64_t total[3] = {tot(d, m, 0), tot(d, m, 1), tot(d, m, 2)};
+      const int64_t req[3] = {in.core, in.mem, in.ratio};
+      sc[m] = scorer(strategy, w, total, fr[m], req);
+    }
+    const int pm = (preferred >> m) & 1;
+    int k = n++;
+    while (k > 0) {
+      const int o = order[k - 1], po = (preferred >> o) & 1;
+      if (po > pm || (po == pm && sc[o] >= sc[m])) break; /* earlier minors win ties (minor asc) */
+      order[k] = o;
+      k--;
+    }
+    order[k] = m;
+  }
+  int32_t mask = 0;
+  int got = 0;
+  for (int k = 0; k < n && got < in.count; k++) {
+    const int m = order[k];
+    if (required && !((required >> m) & 1u)) continue;
+    if (fr[m][0] == 0 && fr[m][1] == 0 && fr[m][2] == 0) continue;
+    if (!(in.core <= fr[m][0] && in.mem <= fr[m][1] && in.ratio <= fr[m][2])) continue;
+    mask |= 1 << m;
+    got++;
+  }
+  return got < in.count ? -1 : mask;
+}
+
+/* AutopilotAllocator.score over the view: scoreNode(request, Σ total, Σ free) of the minors it lists (0 when the type
+ * is dropped) */
+int64_t or_ds_score_view(const kg_node_device* d, const or_ds_pod* p, uint32_t rr_minors, const int64_t (*rr)[3],
+                         const int64_t (*pre)[3], int strategy, const int64_t w[3]) {
+  if (p->skip || p->error || !d->has_device) return 0;
+  const or_ds_inst in = or_ds_instance(d, p);
+  if (!in.ok) return 0;
+  int64_t fr[KG_MAX_MINORS][3];
+  uint32_t minors = 0;
+  if (!dsr_view(d, pre, rr_minors, rr, fr, &minors)) return 0;
+  int64_t total[3] = {0, 0, 0}, free_[3] = {0, 0, 0};
+  for (int m = 0; m < KG_MAX_MINORS; m++) {
+    if (!((minors >> m) & 1u)) continue;
+    for (int q = 0; q < 3; q++) {
+      total[q] += tot(d, m, q);
+      free_[q] += fr[m][q];
+    }
+  }
+  const int64_t req[3] = {in.core, in.mem, in.ratio};
+  return scorer(strategy, w, total, free_, req);
+}
+
+/* the preemptible map of one matched reservation s (tryAllocateFromReservation / scoreWithReservation):
+ * mergedUnmatchedUsed + mergedMatchedAllocated + remained(s) (preemptibleInRR: no preemption here) */
+static void dsr_pre_slot(const kg_node_reservations* r, const or_ds_rsv* st, int s, int64_t pre[KG_MAX_MINORS][3],
+                         int64_t rem[KG_MAX_MINORS][3]) {
+  for (int m = 0; m < KG_MAX_MINORS; m++)
+    for (int q = 0; q < 3; q++) {
+      rem[m][q] = sub0(r->gpu_alloc[s][m][q], r->gpu_allocated[s][m][q]);
+      pre[m][q] = st->unm_used[m][q] + st->mat_allocd[m][q] + rem[m][q];
+    }
+}
+
+/* tryAllocateFromReservation (reservation.go:173-244) over the given GPU-holding matched slots, in order:
+ * Default / Aligned: Allocate(nil, preferred = the slot's minors, nil, preemptible); Restricted: the same with required =
+ * preferred, and then once more with requiredDeviceResources = the slot's remained (calcRequiredDeviceResources: all
+ * zero when nothing remains).  Returns the satisfied slot (its allocation in *mask), -1 none satisfied. */
+int or_ds_try_rsv(const kg_node_device* d, const or_ds_pod* p, const kg_node_reservations* r, const or_ds_rsv* st,
+                  const int32_t* slots, int n_slots, int scored, int strategy, const int64_t w[3], int32_t* mask) {
+  for (int k = 0; k < n_slots; k++) {
+    const int s = slots[k];
+    int64_t pre[KG_MAX_MINORS][3], rem[KG_MAX_MINORS][3];
+    dsr_pre_slot(r, st, s, pre, rem);
+    const uint32_t pref = (uint32_t)r->gpu_minors[s];
+    int32_t got;
+    if (r->policy[s] == KG_RSV_POLICY_RESTRICTED) {
+      if (or_ds_allocate(d, p, pref, pref, 0, NULL, (const int64_t(*)[3])pre, 0, strategy, w) < 0) continue;
+      got = or_ds_allocate(d, p, pref, pref, pref, (const int64_t(*)[3])rem, (const int64_t(*)[3])pre, scored,
+                           strategy, w);
+    } else {
+      got = or_ds_allocate(d, p, 0, pref, 0, NULL, (const int64_t(*)[3])pre, scored, strategy, w);
+    }
+    if (got >= 0) {
+      if (mask) *mask = got;
+      return s;
+    }
+  }
+  return -1;
+}
+
+/* the preemptible map of the node-level fallback: mergedUnmatchedUsed + mergedMatchedAllocatable */
+static void dsr_pre_node(const or_ds_rsv* st, int64_t pre[KG_MAX_MINORS][3]) {
+  for (int m = 0; m < KG_MAX_MINORS; m++)
+    for (int q = 0; q < 3; q++) pre[m][q] = st->unm_used[m][q] + st->mat_alloc[m][q];
+}
+
+/* Filter (plugin.go:280-330): tryAllocateFromReservation over every GPU-holding matched slot (requiredFromReservation =
+ * the pod's required reservation affinity), else Allocate on the node with every matched reservation's allocatable
+ * returned.  1 = pass. */
+int or_ds_filter_rsv(const kg_node_device* d, const or_ds_pod* p, const kg_node_reservations* r, const or_ds_rsv* st,
+                     int required_from_rsv) {
+  if (p->skip) return 1;
+  if (p->error || !d->has_device) return 0;
+  if (st->n_matched > 0) {
+    int32_t mask = 0;
+    if (or_ds_try_rsv(d, p, r, st, st->matched, st->n_matched, 0, 0, NULL, &mask) >= 0) return 1;
+    if (required_from_rsv) return 0;
+  }
+  int64_t pre[KG_MAX_MINORS][3];
+  dsr_pre_node(st, pre);
+  return or_ds_allocate(d, p, 0, 0, 0, NULL, (const int64_t(*)[3])pre, 0, 0, NULL) >= 0;
+}
+
+/* FilterReservation (plugin.go:333-380) of slot s: a pod with device requests can use only a reservation the restore
+ * holds GPUs for ("impossible, there is no relevant Reservation information" otherwise); tryAllocateFromReservation
+ * with that slot alone, requiredFromReservation = true.  1 = pass. */
+int or_ds_filter_reservation(const kg_node_device* d, const or_ds_pod* p, const kg_node_reservations* r,
+                             const or_ds_rsv* st, int s) {
+  if (p->skip) return 1;
+  if (!d->has_device) return 1; /* nodeDeviceInfo == nil: nil */
+  int in_state = 0;
+  for (int k = 0; k < st->n_matched; k++) in_state |= st->matched[k] == s;
+  if (!in_state) return 0;
+  const int32_t one = s;
+  return or_ds_try_rsv(d, p, r, st, &one, 1, 0, 0, NULL, NULL) >= 0;
+}
+
+/* scoreWithReservation (reservation.go:246-272) of slot s: score(requiredDeviceResources = remained for Restricted,
+ * preemptible of the slot) — ScoreReservation, and Score for the nominated reservation */
+int64_t or_ds_score_slot(const kg_node_device* d, const or_ds_pod* p, const kg_node_reservations* r,
+                         const or_ds_rsv* st, int s, int strategy, const int64_t w[3]) {
+  if (p->skip || !d->has_device) return 0;
+  int in_state = 0;
+  for (int k = 0; k < st->n_matched; k++) in_state |= st->matched[k] == s;
+  if (!in_state) return 0;
+  int64_t pre[KG_MAX_MINORS][3], rem[KG_MAX_MINORS][3];
+  dsr_pre_slot(r, st, s, pre, rem);
+  if (r->policy[s] == KG_RSV_POLICY_RESTRICTED)
+    return or_ds_score_view(d, p, (uint32_t)r->gpu_minors[s], (const int64_t(*)[3])rem, (const int64_t(*)[3])pre,
+                            strategy, w);
+  return or_ds_score_view(d, p, 0, NULL, (const int64_t(*)[3])pre, strategy, w);
+}
+
+/* Score (scoring.go:34-89): the nominated reservation's score when one is nominated, else the node's with every
+ * matched reservation's allocatable returned */
+int64_t or_ds_score_rsv(const kg_node_device* d, const or_ds_pod* p, const kg_node_reservations* r,
+                        const or_ds_rsv* st, int nominated, int strategy, const int64_t w[3]) {
+  if (p->skip || p->error || !d->has_device) return 0;
+  if (nominated >= 0) {
+    int in_state = 0;
+    for (int k = 0; k < st->n_matched; k++) in_state |= st->matched[k] == nominated;
+    if (in_state) return or_ds_score_slot(d, p, r, st, nominated, strategy, w);
+  }
+  int64_t pre[KG_MAX_MINORS][3];
+  dsr_pre_node(st, pre);
+  return or_ds_score_view(d, p, 0, NULL, (const int64_t(*)[3])pre, strategy, w);
+}
+
+/* Reserve (plugin.go:388-437): allocateWithNominatedReservation (the nominated slot alone, not required), else Allocate
+ * on the node with the matched reservations' allocatable returned; updateCacheUsed adds the per-instance request to
+ * every allocated minor.  Returns the minor mask (0: nothing to allocate), -1 on failure. */
+int32_t or_ds_reserve_rsv(kg_node_device* d, const or_ds_pod* p, const kg_node_reservations* r, const or_ds_rsv* st,
+                          int nominated, int strategy, const int64_t w[3]) {
+  if (p->skip || !d->has_device) return 0;
+  if (p->error) return -1;
+  int32_t mask = -1;
+  if (nominated >= 0 && !(p->reserve)) {
+    int in_state = 0;
+    for (int k = 0; k < st->n_matched; k++) in_state |= st->matched[k] == nominated;
+    if (in_state) {
+      const int32_t one = nominated;
+      if (or_ds_try_rsv(d, p, r, st, &one, 1, 1, strategy, w, &mask) < 0) mask = -1;
+    }
+  }
+  if (mask < 0) {
+    int64_t pre[KG_MAX_MINORS][3];
+    dsr_pre_node(st, pre);
+    mask = or_ds_allocate(d, p, 0, 0, 0, NULL, (const int64_t(*)[3])pre, 1, strategy, w);
+  }
+  if (mask <= 0) return mask;
+  const or_ds_inst in = or_ds_instance(d, p);
+  for (int m = 0; m < KG_MAX_MINORS; m++) {
+    if (!((mask >> m) & 1)) continue;
+    d->used_core[m] += in.core;
+    d->used_memory[m] += in.mem;
+    d->used_ratio[m] += in.ratio;
+  }
+  return mask;
+}
+
+/* the allocation of a pod assumed into slot s, on the reservation's minors (appendAllocatedByHints): sign ±1 */
+void or_ds_rsv_assign(kg_node_reservations* r, int s, const kg_node_device* d, const or_ds_pod* p, int32_t mask,
+                      int sign) {
+  if (s < 0 || !r->gpu_minors[s] || mask <= 0) return;
+  const or_ds_inst in = or_ds_instance(d, p);
+  const int64_t v[3] = {in.core, in.mem, in.ratio};
+  for (int m = 0; m < KG_MAX_MINORS; m++) {
+    if (!((mask >> m) & 1) || !((r->gpu_minors[s] >> m) & 1)) continue;
+    for (int q = 0; q < 3; q++) {
+      const int64_t x = r->gpu_allocated[s][m][q] + sign * v[q];
+      r->gpu_allocated[s][m][q] = sign > 0 ? x : (x > 0 ? x : 0);
+    }
+  }
 }

@@ -10,7 +10,8 @@
  *   device_cache.go:124-174,314-391,505-523  updateCacheUsed/resetDeviceFree/calcFreeWithPreemptible/filter/build
  *   device_resources.go:164-208  scoreDevices + sortDeviceResourcesByMinor (score desc, minor asc)
  *   scoring.go:34-97,183-308   Score, NormalizeScore (DefaultNormalizeScore), scoreDevice/scoreNode, scorers
- * Scope: the GPU device type without hints, joint allocation, VFs, NUMA affinity, reservations or preemption.
+ * Scope: the GPU device type without hints, joint allocation, VFs, NUMA affinity or preemption; (ABI 13) reservations
+ * that hold GPUs (reservation.go RestoreReservation / tryAllocateFromReservation / scoreWithReservation).
  * Map-order pins: fillGPUTotalMem takes the lowest healthy minor (the reference iterates a Go map; every GPU of
  * a node is the same model, device_cache.go comment at devicehandler_gpu.go:69-70).
  */
@@ -26,6 +27,7 @@ extern "C" {
 /* DeviceShare preFilterState for the GPU device type (preparePod, utils.go:204-230) */
 typedef struct or_ds_pod {
   int skip;          /* no device request: Filter passes, Score 0                         */
+  int reserve;       /* (ABI 13) a reservation's reserve pod: allocateWithNominatedReservation skips it */
   int error;         /* PreFilter UnschedulableAndUnresolvable: invalid request           */
   int unsupported;   /* rdma / fpga requests: outside the restated scope                  */
   int has_mem;       /* the converted request names gpu-memory (else gpu-memory-ratio)   */
@@ -61,6 +63,36 @@ int64_t or_ds_score_minor(const kg_node_device* d, int minor, const or_ds_pod* p
 void or_default_normalize(int64_t* scores, int64_t n);
 /* Python binding helper: or_ds_instance → {count, core, mem, ratio}; returns ok */
 int or_ds_instance_flat(const kg_node_device* d, const or_ds_pod* p, int64_t* out);
+
+/* (ABI 13) reservations holding GPUs: the DeviceShare restore of one node for one pod (reservation.go:84-171) */
+typedef struct or_ds_rsv {
+  int n_matched;
+  int32_t matched[KG_MAX_RSV_SLOTS];        /* GPU-holding matched slots, in the Reservation restore's order */
+  int64_t unm_used[KG_MAX_MINORS][3];       /* mergedUnmatchedUsed                                           */
+  int64_t mat_allocd[KG_MAX_MINORS][3];     /* mergedMatchedAllocated                                        */
+  int64_t mat_alloc[KG_MAX_MINORS][3];      /* mergedMatchedAllocatable                                      */
+} or_ds_rsv;
+void or_ds_rsv_init(const kg_node_reservations* r, const int32_t* matched, int n_matched, const int32_t* unmatched,
+                    int n_unmatched, or_ds_rsv* out);
+int32_t or_ds_allocate(const kg_node_device* d, const or_ds_pod* p, uint32_t required, uint32_t preferred,
+                       uint32_t rr_minors, const int64_t (*rr)[3], const int64_t (*pre)[3], int scored, int strategy,
+                       const int64_t w[3]);
+int64_t or_ds_score_view(const kg_node_device* d, const or_ds_pod* p, uint32_t rr_minors, const int64_t (*rr)[3],
+                         const int64_t (*pre)[3], int strategy, const int64_t w[3]);
+int or_ds_try_rsv(const kg_node_device* d, const or_ds_pod* p, const kg_node_reservations* r, const or_ds_rsv* st,
+                  const int32_t* slots, int n_slots, int scored, int strategy, const int64_t w[3], int32_t* mask);
+int or_ds_filter_rsv(const kg_node_device* d, const or_ds_pod* p, const kg_node_reservations* r, const or_ds_rsv* st,
+                     int required_from_rsv);
+int or_ds_filter_reservation(const kg_node_device* d, const or_ds_pod* p, const kg_node_reservations* r,
+                             const or_ds_rsv* st, int s);
+int64_t or_ds_score_slot(const kg_node_device* d, const or_ds_pod* p, const kg_node_reservations* r,
+                         const or_ds_rsv* st, int s, int strategy, const int64_t w[3]);
+int64_t or_ds_score_rsv(const kg_node_device* d, const or_ds_pod* p, const kg_node_reservations* r,
+                        const or_ds_rsv* st, int nominated, int strategy, const int64_t w[3]);
+int32_t or_ds_reserve_rsv(kg_node_device* d, const or_ds_pod* p, const kg_node_reservations* r, const or_ds_rsv* st,
+                          int nominated, int strategy, const int64_t w[3]);
+void or_ds_rsv_assign(kg_node_reservations* r, int s, const kg_node_device* d, const or_ds_pod* p, int32_t mask,
+                      int sign);
 
 #ifdef __cplusplus
 }

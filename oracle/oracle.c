@@ -572,6 +572,9 @@ int or_unreserve(const kg_config* cfg, or_node_state* st, void* numa_states, kg_
     or_ds_pod dsp;
     if (or_ds_pod_init(pod, &dsp) != 0) return KG_E_INVALID;
     or_ds_release(&dev[node], &dsp, minors);
+    /* (ABI 13) the pod leaves the reservation's AssignedPods: its allocation on the reservation's minors leaves the
+     * restore's `allocated` (deviceshare/reservation.go:150-155) */
+    if (rsv && slot >= 0) or_ds_rsv_assign(&rsv[node], slot, &dev[node], &dsp, minors, -1);
   }
   if (rsv && slot >= 0) or_rsv_forget(&rsv[node], slot, pod); /* reservation/plugin.go:561-583 */
   if (quotas && pod->quota_id > 0) { /* elasticquota/plugin.go:348-360 → UnreservePod (addUsedNonNegativeNoLock) */

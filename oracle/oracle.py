@@ -95,6 +95,20 @@ def lib():
         L.or_ds_memory_ratio_to_bytes.restype = i64
         L.or_ds_instance_flat.argtypes = [vp, vp, vp]
         L.or_ds_instance_flat.restype = i
+        L.or_ds_rsv_init.argtypes = [vp, vp, i, vp, i, vp]
+        L.or_ds_rsv_init.restype = None
+        L.or_ds_try_rsv.argtypes = [vp, vp, vp, vp, vp, i, i, i, vp, vp]
+        L.or_ds_try_rsv.restype = i
+        L.or_ds_filter_rsv.argtypes = [vp, vp, vp, vp, i]
+        L.or_ds_filter_rsv.restype = i
+        L.or_ds_filter_reservation.argtypes = [vp, vp, vp, vp, i]
+        L.or_ds_filter_reservation.restype = i
+        L.or_ds_score_slot.argtypes = [vp, vp, vp, vp, i, i, vp]
+        L.or_ds_score_slot.restype = i64
+        L.or_ds_score_rsv.argtypes = [vp, vp, vp, vp, i, i, vp]
+        L.or_ds_score_rsv.restype = i64
+        L.or_ds_reserve_rsv.argtypes = [vp, vp, vp, vp, i, i, vp]
+        L.or_ds_reserve_rsv.restype = ctypes.c_int32
         L.or_schedule_resv.argtypes = [vp, i64, vp, vp, vp, vp, i64, vp, i64, vp, vp, vp]
         L.or_schedule_resv.restype = i
         L.or_schedule_resv_full.argtypes = [vp, i64, vp, vp, vp, vp, vp, vp, i64, i64, vp, i64, i, vp, vp, vp, vp,
@@ -138,8 +152,12 @@ def lib():
     return _lib
 
 
-DS_POD_DTYPE = np.dtype([("skip", np.int32), ("error", np.int32), ("unsupported", np.int32), ("has_mem", np.int32),
-                         ("core", np.int64), ("mem", np.int64), ("ratio", np.int64)])
+DS_POD_DTYPE = np.dtype([("skip", np.int32), ("reserve", np.int32), ("error", np.int32), ("unsupported", np.int32),
+                         ("has_mem", np.int32), ("core", np.int64), ("mem", np.int64), ("ratio", np.int64)], align=True)
+# (ABI 13) or_ds_rsv: the DeviceShare restore of one node (oracle/deviceshare.h)
+DS_RSV_DTYPE = np.dtype([("n_matched", np.int32), ("matched", np.int32, (abi.MAX_RSV_SLOTS,)),
+                         ("unm_used", np.int64, (abi.MAX_MINORS, 3)), ("mat_allocd", np.int64, (abi.MAX_MINORS, 3)),
+                         ("mat_alloc", np.int64, (abi.MAX_MINORS, 3))], align=True)
 
 
 def ds_pod(pod) -> np.ndarray:
@@ -169,6 +187,51 @@ def ds_reserve(cfg, dev, pod) -> int:
     """Reserve on one node (mutates `dev`, a 1-element NODE_DEVICE array): minor bitmask, 0 none, -1 failure."""
     w = np.ascontiguousarray(cfg["ds_scoring_weights"].reshape(3), dtype=np.int64)
     return int(lib().or_ds_reserve(p(dev), p(ds_pod(pod)), int(cfg["ds_scoring_strategy"]), p(w)))
+
+
+def _w(cfg):
+    return np.ascontiguousarray(cfg["ds_scoring_weights"].reshape(3), dtype=np.int64)
+
+
+def ds_rsv_init(rsv, matched=(), unmatched=()) -> np.ndarray:
+    """(ABI 13) the DeviceShare restore of one node over its GPU-holding slots (or_ds_rsv_init): `matched` /
+    `unmatched` are the Reservation restore's slot lists, in order."""
+    out = np.zeros(1, dtype=DS_RSV_DTYPE)
+    m = np.ascontiguousarray(matched, dtype=np.int32)
+    u = np.ascontiguousarray(unmatched, dtype=np.int32)
+    r = np.ascontiguousarray(np.asarray(rsv, dtype=abi.NODE_RSV_DTYPE).reshape(1))
+    lib().or_ds_rsv_init(p(r), p(m), len(m), p(u), len(u), p(out))
+    return out
+
+
+def ds_try_rsv(cfg, dev, pod, rsv, st, slots, scored=True):
+    """tryAllocateFromReservation over `slots` (or_ds_try_rsv): (satisfied slot or -1, minor mask)."""
+    mask = np.zeros(1, dtype=np.int32)
+    sl = np.ascontiguousarray(slots, dtype=np.int32)
+    r = np.ascontiguousarray(np.asarray(rsv, dtype=abi.NODE_RSV_DTYPE).reshape(1))
+    s = lib().or_ds_try_rsv(p(np.ascontiguousarray(dev)), p(ds_pod(pod)), p(r), p(st), p(sl), len(sl), int(scored),
+                            int(cfg["ds_scoring_strategy"]), p(_w(cfg)), p(mask))
+    return int(s), int(mask[0])
+
+
+def ds_filter_rsv(dev, pod, rsv, st, required_from_rsv=False) -> bool:
+    r = np.ascontiguousarray(np.asarray(rsv, dtype=abi.NODE_RSV_DTYPE).reshape(1))
+    return bool(lib().or_ds_filter_rsv(p(np.ascontiguousarray(dev)), p(ds_pod(pod)), p(r), p(st),
+                                       int(required_from_rsv)))
+
+
+def ds_score_slot(cfg, dev, pod, rsv, st, s) -> int:
+    """ScoreReservation of slot s (or_ds_score_slot, scoreWithReservation)."""
+    r = np.ascontiguousarray(np.asarray(rsv, dtype=abi.NODE_RSV_DTYPE).reshape(1))
+    return int(lib().or_ds_score_slot(p(np.ascontiguousarray(dev)), p(ds_pod(pod)), p(r), p(st), int(s),
+                                      int(cfg["ds_scoring_strategy"]), p(_w(cfg))))
+
+
+def ds_reserve_rsv(cfg, dev, pod, rsv, st, nominated) -> int:
+    """Reserve with the node's GPU reservations (mutates `dev`): minor bitmask, 0 none, -1 failure."""
+    r = np.ascontiguousarray(np.asarray(rsv, dtype=abi.NODE_RSV_DTYPE).reshape(1))
+    return int(lib().or_ds_reserve_rsv(p(dev), p(ds_pod(pod)), p(r), p(st), int(nominated),
+                                       int(cfg["ds_scoring_strategy"]), p(_w(cfg))))
 
 
 NUMA_ALLOC_WORDS = 1 + 2 * abi.MAX_NUMA  # per-pod NUMA allocation record (oracle/numa.h OR_NUMA_ALLOC_WORDS)

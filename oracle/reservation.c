@@ -86,13 +86,14 @@ void or_rsv_restore(const kg_node_reservations* r, const or_node_state* st, cons
   out->nonzero[1] = st->nonzero[1];
   out->num_pods = st->num_pods;
   if (!r) return;
-  int32_t unmatched[KG_MAX_RSV_SLOTS];
+  int32_t* unmatched = out->unmatched;
   int n_unmatched = 0;
   for (int s = 0; s < (int)r->n; s++) {
     if (!slot_usable(r, s)) continue;
     if (pod_matches(pod, r, s)) out->matched[out->n_matched++] = s;
     else if (r->assigned[s] > 0) unmatched[n_unmatched++] = s;
   }
+  out->n_unmatched = n_unmatched;
   if (out->n_matched == 0 && n_unmatched == 0) return;
   /* reservationAffinity != nil && no matched: the node is not processed (transformer.go:134-136) */
   if ((pod->reservation_flags & KG_POD_RSV_AFFINITY) && out->n_matched == 0) return;
@@ -209,15 +210,25 @@ int64_t or_rsv_node_order(const or_rsv_node* ns, const kg_node_reservations* r) 
 
 int or_rsv_nominate(const kg_pod* pod, int64_t allowed_pods, const int64_t alloc[2], const or_rsv_node* ns,
                     const kg_node_reservations* r) {
+  return or_rsv_nominate_ds(pod, allowed_pods, alloc, ns, r, NULL, NULL, NULL, 0, NULL);
+}
+
+int or_rsv_nominate_ds(const kg_pod* pod, int64_t allowed_pods, const int64_t alloc[2], const or_rsv_node* ns,
+                       const kg_node_reservations* r, const kg_node_device* dev, const struct or_ds_pod* dsp,
+                       const struct or_ds_rsv* dst, int strategy, const int64_t w[3]) {
   if (pod->flags & KG_POD_RESERVE) return -1; /* NominateReservation: none for a reserve pod (nominator.go:77) */
   if (!ns->has_state || ns->n_matched == 0) return -1;
+  const int ds = dev && dsp && dst && !dsp->skip;
   int32_t cand[KG_MAX_RSV_SLOTS];
   int n = 0;
   for (int k = 0; k < ns->n_matched; k++) {
     const int s = ns->matched[k];
     /* FilterReservation (plugin.go:492-519): AllocateOnce already excluded; filterWithReservations([s], true) */
     const int32_t one = s;
-    if (or_rsv_filter_with(pod, allowed_pods, alloc, ns, r, &one, 1, 1)) cand[n++] = s;
+    if (!or_rsv_filter_with(pod, allowed_pods, alloc, ns, r, &one, 1, 1)) continue;
+    /* (ABI 13) DeviceShare.FilterReservation (deviceshare/plugin.go:333-380) */
+    if (ds && !or_ds_filter_reservation(dev, dsp, r, dst, s)) continue;
+    cand[n++] = s;
   }
   if (n == 0) return -1;
   int64_t best_order = INT64_MAX;
@@ -227,9 +238,17 @@ int or_rsv_nominate(const kg_pod* pod, int64_t allowed_pods, const int64_t alloc
     if (o != 0 && best_order > o) { best_order = o; pick = cand[k]; }
   }
   if (pick >= 0) return pick;
+  /* prioritizeReservations: Σ over the reservation score plugins — Reservation (no normalizer) + DeviceShare
+   * (scoreWithNominatedReservation, then DefaultReservationNormalizeScore: 100·s / max over the candidates) */
+  int64_t dsc[KG_MAX_RSV_SLOTS] = {0}, dmax = 0;
+  if (ds)
+    for (int k = 0; k < n; k++) {
+      dsc[k] = or_ds_score_slot(dev, dsp, r, dst, cand[k], strategy, w);
+      if (dsc[k] > dmax) dmax = dsc[k];
+    }
   int64_t best = -1;
   for (int k = 0; k < n; k++) {
-    const int64_t sc = or_rsv_score_slot(pod, r, cand[k]);
+    const int64_t sc = or_rsv_score_slot(pod, r, cand[k]) + (dmax > 0 ? 100 * dsc[k] / dmax : 0);
     if (sc > best) { best = sc; pick = cand[k]; } /* sort.Slice unstable → pinned: lowest slot on ties */
   }
   return pick;
@@ -320,10 +339,11 @@ int or_schedule_resv_full(const kg_config* cfg, int64_t n_nodes, const kg_node* 
       or_ds_pod_init(pod, &dsp);
       if (dsp.unsupported) { rc = KG_E_UNSUPPORTED; break; }
     }
-    /* DeviceShare.FilterReservation (deviceshare/plugin.go:462-486): a pod with device requests can only use a
-     * reservation DeviceShare restored device state for; the reservations here hold none, so it is rejected and no
-     * reservation is nominated for such a pod (NominateReservation skips failing reservations, nominator.go:99-105) */
-    const int ds_blocks_nomination = ds_on && cfg->ds_filter && !dsp.skip;
+    /* (ABI 13) DeviceShare with reservations holding GPUs: the plugin's restore per node (or_ds_rsv_init over the
+     * Reservation restore's matched / unmatched slots), its Filter / FilterReservation / ScoreReservation / Score /
+     * Reserve (deviceshare.c) */
+    const int ds_rsv = ds_on && !dsp.skip;
+    const int required_from_rsv = (pod->reservation_flags & KG_POD_RSV_AFFINITY) != 0;
     or_numa_pod npod;
     if (numa_on) or_numa_pod_init(cfg, pod, &npod);
     /* PodTopologySpread PreFilter (common.go calPreFilterState) over the nodes passing the pod's nodeSelector /
@@ -385,7 +405,12 @@ int or_schedule_resv_full(const kg_config* cfg, int64_t n_nodes, const kg_node* 
       }
       if (cfg->reservation_filter && !or_rsv_policy_filter(pod, i, rsv_on ? &rsv[i] : NULL)) continue;
       if (cfg->reservation_filter && !or_rsv_filter(pod, nd->allowed_pods, alloc, &ns, &rsv[i])) continue;
-      if (ds_on && cfg->ds_filter && !or_ds_filter(&dev[i], &dsp)) continue;
+      or_ds_rsv dst;
+      memset(&dst, 0, sizeof(dst));
+      if (ds_rsv && rsv_on && ns.has_state)
+        or_ds_rsv_init(&rsv[i], ns.matched, ns.n_matched, ns.unmatched, ns.n_unmatched, &dst);
+      if (ds_on && cfg->ds_filter && !or_ds_filter_rsv(&dev[i], &dsp, rsv_on ? &rsv[i] : NULL, &dst, required_from_rsv))
+        continue;
       /* NodeNUMAResource Filter (nodenumaresource/plugin.go:276-334) on the restored NodeInfo; the reserve pods hold
        * no cpuset, so its RestoreReservation (nodenumaresource/reservation.go) restores nothing */
       if (numa_on) {
@@ -435,11 +460,16 @@ int or_schedule_resv_full(const kg_config* cfg, int64_t n_nodes, const kg_node* 
       tcnt[i] = cfg->taint_score ? or_taint_count(np, pod) : 0;
       asum[i] = cfg->affinity_score ? or_affinity_sum(np, pod) : 0;
       base[i] = t;
-      nom[i] = (rsv_on && !ds_blocks_nomination) ? or_rsv_nominate(pod, nd->allowed_pods, alloc, &ns, &rsv[i]) : -1;
+      nom[i] = rsv_on ? or_rsv_nominate_ds(pod, nd->allowed_pods, alloc, &ns, &rsv[i], ds_on ? &dev[i] : NULL,
+                                           ds_on ? &dsp : NULL, ds_on ? &dst : NULL, (int)cfg->ds_scoring_strategy,
+                                           cfg->ds_scoring_weights)
+                      : -1;
       raw[i] = nom[i] >= 0 ? or_rsv_score_slot(pod, &rsv[i], nom[i]) : 0;
       order[i] = ns.has_state ? or_rsv_node_order(&ns, &rsv[i]) : INT64_MAX;
       dsraw[i] = (ds_on && cfg->ds_score && !dsp.skip)
-                     ? or_ds_score(&dev[i], &dsp, (int)cfg->ds_scoring_strategy, cfg->ds_scoring_weights) : 0;
+                     ? or_ds_score_rsv(&dev[i], &dsp, rsv_on ? &rsv[i] : NULL, &dst, nom[i],
+                                       (int)cfg->ds_scoring_strategy, cfg->ds_scoring_weights)
+                     : 0;
     }
     if (err) { rc = err; break; }
     /* PreScore preferredNode (scoring.go:89-99): smallest order, first (lowest index) feasible node */
@@ -546,7 +576,16 @@ int or_schedule_resv_full(const kg_config* cfg, int64_t n_nodes, const kg_node* 
     }
     int32_t minors = 0;
     if (win >= 0 && ds_on && !dsp.skip) {
-      minors = or_ds_reserve(&dev[win], &dsp, (int)cfg->ds_scoring_strategy, cfg->ds_scoring_weights);
+      /* the winner's DeviceShare restore again (the per-node state of the Filter pass above) */
+      or_rsv_node wns;
+      or_ds_rsv wdst;
+      memset(&wdst, 0, sizeof(wdst));
+      if (rsv_on) {
+        or_rsv_restore(&rsv[win], &st[win], pod, &wns);
+        if (wns.has_state) or_ds_rsv_init(&rsv[win], wns.matched, wns.n_matched, wns.unmatched, wns.n_unmatched, &wdst);
+      }
+      minors = or_ds_reserve_rsv(&dev[win], &dsp, rsv_on ? &rsv[win] : NULL, &wdst, rsv_on ? nom[win] : -1,
+                                 (int)cfg->ds_scoring_strategy, cfg->ds_scoring_weights);
       if (minors < 0) {
         minors = 0;
         if (numa_on) numa[win] = numa_save;
@@ -568,6 +607,8 @@ int or_schedule_resv_full(const kg_config* cfg, int64_t n_nodes, const kg_node* 
         if (r->allocatable_cpu[s] > 0) r->allocated_cpu[s] += pod->requests[KG_RES_CPU];
         if (r->allocatable_mem[s] > 0) r->allocated_mem[s] += pod->requests[KG_RES_MEMORY];
         r->assigned[s] += 1;
+        /* (ABI 13) the reservation's allocated GPUs: the pod's allocation on the reservation's minors */
+        if (ds_on && minors > 0) or_ds_rsv_assign(r, s, &dev[win], &dsp, minors, 1);
         if (out_slot) out_slot[p] = nom[win];
       }
       if (quota) or_quota_charge(quota, pod);

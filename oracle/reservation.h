@@ -30,6 +30,8 @@ typedef struct or_rsv_node {
   int64_t r_allocated[2];            /* Σ matched Allocated                                                 */
   int64_t requested[2], nonzero[2];  /* restored NodeInfo.Requested / NonZeroRequested                      */
   int64_t num_pods;                  /* restored len(NodeInfo.Pods)                                         */
+  int32_t n_unmatched;               /* (ABI 13) the restore's unmatched list (usable, not matched, assigned) */
+  int32_t unmatched[KG_MAX_RSV_SLOTS];
 } or_rsv_node;
 
 /* BeforePreFilter for one node (transformer.go:100-189). */
@@ -52,6 +54,15 @@ int64_t or_rsv_score_slot(const kg_pod* pod, const kg_node_reservations* r, int 
  * filter and ScoreReservation as the only reservation scorer; ties on score → lowest slot.  Returns slot or -1. */
 int or_rsv_nominate(const kg_pod* pod, int64_t allowed_pods, const int64_t alloc[2], const or_rsv_node* ns,
                     const kg_node_reservations* r);
+/* (ABI 13) NominateReservation with DeviceShare as a reservation filter / score plugin (plugin.go:333-380,
+ * scoring.go:99-127): a pod with device requests may be nominated only to a GPU-holding reservation DeviceShare can
+ * allocate from; the prioritization sums Reservation's ScoreReservation and DeviceShare's, the latter normalized by
+ * DefaultReservationNormalizeScore (frameworkext/framework_extender.go:379-432).  dsp / dev / dst NULL = no DeviceShare. */
+struct or_ds_pod;
+struct or_ds_rsv;
+int or_rsv_nominate_ds(const kg_pod* pod, int64_t allowed_pods, const int64_t alloc[2], const or_rsv_node* ns,
+                       const kg_node_reservations* r, const kg_node_device* dev, const struct or_ds_pod* dsp,
+                       const struct or_ds_rsv* dst, int strategy, const int64_t w[3]);
 /* findMostPreferredReservationByOrder over the matched slots (scoring.go:162-181): INT64_MAX if none. */
 int64_t or_rsv_node_order(const or_rsv_node* ns, const kg_node_reservations* r);
 

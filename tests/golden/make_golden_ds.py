@@ -140,6 +140,119 @@ CASES = [
 ]
 
 
+
+# ---- (ABI 13) reservations holding GPUs (reservation.go) ----
+# A reservation slot: policy, the minors the reserve pod holds with its allocation per minor (allocatable: core, ratio,
+# memory bytes) and the allocations of its assigned pods on those minors (allocated; absent = none).  The node's `used`
+# includes the reserve pod's and the assigned pods' allocations, as nodeDevice.deviceUsed does.
+def slot(policy="Default", alloc=None, allocated=None):
+    return {"policy": policy, "alloc": alloc or {}, "allocated": allocated or {}}
+
+
+HALF, QUARTER = (50, 50, 4 * GI), (25, 25, 2 * GI)
+
+
+def two_8g(used0=(0, 0, 0), used1=(0, 0, 0)):
+    return {"has_device": True, "gpus": [gpu(0, mem=8 * GI, used=used0), gpu(1, mem=8 * GI, used=used1)]}
+
+
+HALF_POD = {"koordinator.sh/gpu-core": 50, "koordinator.sh/gpu-memory": 4 * GI}  # podRequestsHalfGPU
+FULL8, FULL16 = (100, 100, 8 * GI), (100, 100, 16 * GI)
+
+CASES += [
+    # ---- reservation_test.go Test_Plugin_ReservationRestore (:38): mergeReservationAllocations of one matched slot ----
+    {"kind": "rsv_restore", "name": "restore_matched_with_assigned_pod", "source": "reservation_test.go:38-222",
+     "slot": slot(alloc={1: FULL8}, allocated={1: HALF}),
+     "want": {"mat_alloc": {1: FULL8}, "mat_allocd": {1: HALF}, "remained": {1: HALF}}},
+    # ---- reservation_test.go Test_tryAllocateFromReservation (:224): one matched slot, no scorer; node = 2 GPUs of
+    # 100 / 8Gi / 100 with the case's deviceUsed ----
+    {"kind": "rsv_try", "name": "no_matched_reservations", "source": "reservation_test.go:308-319",
+     "node": two_8g(), "slot": None, "pod": HALF_POD, "required": False, "want_minors": None,
+     "want_unschedulable": False},
+    {"kind": "rsv_try", "name": "default_policy", "source": "reservation_test.go:321-352",
+     "node": two_8g(), "slot": slot(alloc={0: QUARTER}), "pod": HALF_POD, "required": False, "want_minors": [0],
+     "want_unschedulable": False},
+    # the test's hand-built restore state carries remained = 50 % with allocated = 25 %; RestoreReservation computes
+    # remained = allocatable − allocated (25 %), which gives the same allocation (preemptible 50 % vs 75 % of a minor
+    # used 50 %: free 100 % either way)
+    {"kind": "rsv_try", "name": "default_policy_required", "source": "reservation_test.go:354-396",
+     "node": two_8g(used0=HALF), "slot": slot(alloc={0: HALF}, allocated={0: QUARTER}), "pod": HALF_POD,
+     "required": True, "want_minors": [0], "want_unschedulable": False},
+    {"kind": "rsv_try", "name": "default_policy_required_reservation_empty", "source": "reservation_test.go:398-440",
+     "node": two_8g(used0=(150, 150, 12 * GI)), "slot": slot(alloc={0: HALF}, allocated={0: HALF}), "pod": HALF_POD,
+     "required": True, "want_minors": [1], "want_unschedulable": False},
+    {"kind": "rsv_try", "name": "aligned_policy", "source": "reservation_test.go:442-486",
+     "node": two_8g(used0=FULL8, used1=FULL8), "slot": slot("Aligned", alloc={0: HALF}), "pod": HALF_POD,
+     "required": False, "want_minors": [0], "want_unschedulable": False},
+    {"kind": "rsv_try", "name": "aligned_bigger_request_no_node_remaining", "source": "reservation_test.go:488-527",
+     "node": two_8g(used0=FULL8, used1=FULL8), "slot": slot("Aligned", alloc={0: HALF}),
+     "pod": {"koordinator.sh/gpu-core": 60, "koordinator.sh/gpu-memory": 5 * GI}, "required": True,
+     "want_minors": None, "want_unschedulable": True},
+    {"kind": "rsv_try", "name": "aligned_remaining_little", "source": "reservation_test.go:529-570",
+     "node": two_8g(used0=(125, 125, 10 * GI), used1=FULL8), "slot": slot("Aligned", alloc={0: HALF},
+                                                                          allocated={0: QUARTER}),
+     "pod": {"koordinator.sh/gpu-core": 30, "koordinator.sh/gpu-memory": 1 * GI}, "required": True,
+     "want_minors": None, "want_unschedulable": True},
+    {"kind": "rsv_try", "name": "restricted_policy", "source": "reservation_test.go:572-616",
+     "node": two_8g(used0=FULL8, used1=FULL8), "slot": slot("Restricted", alloc={0: HALF}), "pod": HALF_POD,
+     "required": False, "want_minors": [0], "want_unschedulable": False},
+    {"kind": "rsv_try", "name": "restricted_node_remains_reservation_not", "source": "reservation_test.go:618-654",
+     "node": two_8g(used0=(75, 75, 6 * GI), used1=FULL8), "slot": slot("Restricted", alloc={0: HALF},
+                                                                       allocated={0: QUARTER}),
+     "pod": HALF_POD, "required": True, "want_minors": None, "want_unschedulable": True},
+    # ---- plugin_test.go Test_Plugin_Filter (:869) with a matched reservation (no reservation affinity) ----
+    {"kind": "rsv_filter", "name": "filter_allocate_from_reserved", "source": "plugin_test.go:1670-1737",
+     "node": {"has_device": True, "gpus": [gpu(0, used=FULL16)]}, "slot": slot(alloc={0: FULL16}),
+     "pod": {"koordinator.sh/gpu-core": 100, "koordinator.sh/gpu-memory-ratio": 100}, "want_filter": True},
+    {"kind": "rsv_filter", "name": "filter_reserved_remaining_zero", "source": "plugin_test.go:1739-1835",
+     "node": {"has_device": True, "gpus": [gpu(0, used=FULL16), gpu(1)]}, "slot": slot(alloc={0: (0, 0, 0)}),
+     "pod": {"koordinator.sh/gpu-core": 100, "koordinator.sh/gpu-memory-ratio": 100}, "want_filter": True},
+    # ---- plugin_test.go Test_Plugin_FilterReservation (:1905): GPUs minor 1, 2 of 100 / 8Gi / 100; the reservation
+    # holds minor 1; then a pod assigned to it takes minors 1 and 2 (only minor 1 counts as its allocated) ----
+    {"kind": "rsv_filter_reservation", "name": "filter_reservation_free", "source": "plugin_test.go:1935-2006",
+     "node": {"has_device": True, "gpus": [gpu(1, mem=8 * GI, used=FULL8), gpu(2, mem=8 * GI)]},
+     "slot": slot(alloc={1: FULL8}), "pod": {"koordinator.sh/gpu": 100}, "want_filter": True},
+    {"kind": "rsv_filter_reservation", "name": "filter_reservation_exhausted", "source": "plugin_test.go:2008-2046",
+     "node": {"has_device": True, "gpus": [gpu(1, mem=8 * GI, used=(200, 200, 16 * GI)),
+                                           gpu(2, mem=8 * GI, used=FULL8)]},
+     "slot": slot(alloc={1: FULL8}, allocated={1: FULL8}), "pod": {"koordinator.sh/gpu": 100}, "want_filter": False},
+    # ---- plugin_test.go Test_Plugin_Reserve (:2049) "reserve from reservation": the nominated reservation ----
+    {"kind": "rsv_reserve", "name": "reserve_from_reservation", "source": "plugin_test.go:2937-3009",
+     "node": {"has_device": True, "gpus": [gpu(0, used=FULL16)]}, "slot": slot(alloc={0: FULL16}),
+     "pod": {"koordinator.sh/gpu-core": 100, "koordinator.sh/gpu-memory-ratio": 100}, "strategy": "LeastAllocated",
+     "want_minors": [0], "want_instance": {"core": 100, "ratio": 100, "memory": 16 * GI}},
+    # ---- scoring_test.go TestScoreReservation (:579): one GPU of 100 / 16Gi / 100, used = deviceUsed + the reserve
+    # pod's allocation (updatePod); pod gpu-core 50 + gpu-memory-ratio 50 ----
+    {"kind": "rsv_score", "name": "score_default_least", "source": "scoring_test.go:647-679",
+     "node": {"has_device": True, "gpus": [gpu(0, used=(75, 75, 16 * GI))]}, "slot": slot(alloc={0: (50, 50, 12 * GI)}),
+     "pod": {"koordinator.sh/gpu-core": 50, "koordinator.sh/gpu-memory-ratio": 50}, "strategy": "LeastAllocated",
+     "want_score": 25},
+    {"kind": "rsv_score", "name": "score_default_most", "source": "scoring_test.go:681-714",
+     "node": {"has_device": True, "gpus": [gpu(0, used=(75, 75, 12 * GI))]}, "slot": slot(alloc={0: (50, 50, 8 * GI)}),
+     "pod": {"koordinator.sh/gpu-core": 50, "koordinator.sh/gpu-memory-ratio": 50}, "strategy": "MostAllocated",
+     "want_score": 75},
+    {"kind": "rsv_score", "name": "score_aligned_least", "source": "scoring_test.go:716-749",
+     "node": {"has_device": True, "gpus": [gpu(0, used=(75, 75, 12 * GI))]},
+     "slot": slot("Aligned", alloc={0: (50, 50, 8 * GI)}),
+     "pod": {"koordinator.sh/gpu-core": 50, "koordinator.sh/gpu-memory-ratio": 50}, "strategy": "LeastAllocated",
+     "want_score": 25},
+    {"kind": "rsv_score", "name": "score_aligned_most", "source": "scoring_test.go:751-784",
+     "node": {"has_device": True, "gpus": [gpu(0, used=(75, 75, 12 * GI))]},
+     "slot": slot("Aligned", alloc={0: (50, 50, 8 * GI)}),
+     "pod": {"koordinator.sh/gpu-core": 50, "koordinator.sh/gpu-memory-ratio": 50}, "strategy": "MostAllocated",
+     "want_score": 75},
+    {"kind": "rsv_score", "name": "score_restricted_least", "source": "scoring_test.go:786-819",
+     "node": {"has_device": True, "gpus": [gpu(0, used=(50, 50, 8 * GI))]},
+     "slot": slot("Restricted", alloc={0: (50, 50, 8 * GI)}),
+     "pod": {"koordinator.sh/gpu-core": 50, "koordinator.sh/gpu-memory-ratio": 50}, "strategy": "LeastAllocated",
+     "want_score": 0},
+    {"kind": "rsv_score", "name": "score_restricted_most", "source": "scoring_test.go:821-854",
+     "node": {"has_device": True, "gpus": [gpu(0, used=(50, 50, 8 * GI))]},
+     "slot": slot("Restricted", alloc={0: (50, 50, 8 * GI)}),
+     "pod": {"koordinator.sh/gpu-core": 50, "koordinator.sh/gpu-memory-ratio": 50}, "strategy": "MostAllocated",
+     "want_score": 100},
+]
+
 # Cases of those tables outside the accelerated scope (the engine refuses such pods / states with KG_E_UNSUPPORTED, so
 # the Go path keeps them), with the reason:
 SKIPPED = [
@@ -150,12 +263,14 @@ SKIPPED = [
      "reason": "FPGA requests (not accelerated)"},
     {"source": "plugin_test.go:1595-1668", "name": "allocate from preemptible",
      "reason": "preemptible devices of a nominated preemption (preemption is out of scope)"},
-    {"source": "plugin_test.go:1670-1835", "name": "allocate from reserved / remaining of reserved are zero",
-     "reason": "reservations holding GPU devices (device reservation restore is not accelerated)"},
     {"source": "scoring_test.go:1115-1127", "name": "scoreDevice completely used",
      "reason": "free 0: the pod does not fit, so Score is never called for it in a scheduling cycle"},
-    {"source": "scoring_test.go:579-1090", "name": "TestScoreReservation",
-     "reason": "reservations holding GPU devices (not accelerated)"},
+    {"source": "scoring_test.go:856-952", "name": "TestScoreReservation: aligned / restricted policy and preemptible",
+     "reason": "preemptible devices of a nominated preemption (preemption is out of scope)"},
+    {"source": "scoring_test.go:954-1001", "name": "TestScoreReservation: multi resources and MostAllocated",
+     "reason": "RDMA requests (not accelerated)"},
+    {"source": "plugin_test.go:2856-2935", "name": "Test_Plugin_Reserve: reserve from preemptible",
+     "reason": "preemptible devices of a nominated preemption (preemption is out of scope)"},
 ]
 
 
