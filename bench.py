@@ -323,10 +323,12 @@ def main():
     t0 = time.perf_counter()
     rounds = 0
     active_s = 0.0  # resolvers' in-kernel active time (after the chain wait; s_memrealtime), round profiles
+    slow_pods = 0.0  # resolver diagnostics: pods that re-scored modified rows (the chain's slow path)
     for k in range(args.steps):
         st = e.schedule_staged(k * args.pods_per_step, args.pods_per_step)
         rounds += int(st["device_batches"])
         active_s += float(st["reserved"][2])
+        slow_pods += float(st["reserved"][0])
         if d.rank == 0:
             print(f"[bench] step {k + 1}/{args.steps} done", file=sys.stderr, flush=True)
     t1 = time.perf_counter()
@@ -459,6 +461,7 @@ def main():
                   "resolver_share": active_s / elapsed if active_s > 0 else None,
                   "eval_us": ev_ms * 1e3 if ev_ms else None, "merge_us": mg_ms * 1e3 if mg_ms else None,
                   "depth": depth,
+                  "slow_pod_frac": slow_pods / total if total else None,
                   "eval_stream_share": ((ev_ms or 0) + (mg_ms or 0)) * 1e-3 / (depth * per) if ev_ms else None,
                   "dominant": ("resolver" if active_s > 0 and active_s / elapsed >= ((ev_ms or 0) + (mg_ms or 0)) * 1e-3
                                / (depth * per) else "eval_stream"),

@@ -181,6 +181,7 @@ def test_gpu_reservation_unreserve_interleaved():
         oracle.unreserve(cfg, st, pods[j], w1[j], devices=d, rsv=r, quotas=q, minors=m1[j], slot=s1[j])
     gs = (s1 >= 0) & (rsv["gpu_minors"][np.maximum(w1, 0), np.maximum(s1, 0)] != 0)
     assert (m & gs & (m1 != 0)).any()
+    mid_gpu = np.where((r["gpu_minors"] != 0)[:, :, None, None], r["gpu_allocated"], 0)  # after the Unreserve
     w2, ws2, s2, m2 = oracle.schedule_resv(cfg, cluster.nodes, cluster.metrics, st, r, pods[a:], cluster.now_ns,
                                            devices=d, quotas=q, n_threads=8, with_minors=True)
     with Engine(cfg, cluster.n) as e:
@@ -190,8 +191,7 @@ def test_gpu_reservation_unreserve_interleaved():
         g1, _ = e.fetch(0, a)
         assert np.array_equal(g1, w1) and np.array_equal(e.fetch_devices(0, a), m1)
         e.unreserve(0, a, m)
-        want_gpu = np.where((r["gpu_minors"] != 0)[:, :, None, None], r["gpu_allocated"], 0)
-        assert np.array_equal(e.read_reservation_gpus(), want_gpu)
+        assert np.array_equal(e.read_reservation_gpus(), mid_gpu)
         e.schedule_staged(a, len(pods) - a)
         g2, gs2 = e.fetch(a, len(pods) - a)
         assert np.array_equal(g2, w2) and np.array_equal(gs2, ws2)
