@@ -452,7 +452,7 @@ def main():
         per = elapsed / rounds
         ev_ms = live.get("eval_round", {}).get("avg_ms") or live.get("ds_max_round", {}).get("avg_ms")
         mg_ms = live.get("merge_round", {}).get("avg_ms")
-        depth = args.depth or (1 if wl == "c4" or wl == "c5ds" else 2)
+        depth = args.depth or (1 if wl == "c5ds" else 2)
         res_us = active_s / rounds * 1e6
         # the resolver's algorithmic bytes per launch: the round's records and pods (LDS-DMA) + the rows it writes back
         res_bytes = B * (1024.0 + 96.0) + B * 80.0

@@ -2010,7 +2010,9 @@ __global__ __launch_bounds__(kWave) void resolve_round_numa(DevTable T, NumaTabl
                                                              uint64_t* __restrict__ out_cpus,
                                                              int64_t* __restrict__ out_nrec, int bitmap_words,
                                                              int32_t* __restrict__ poison, int64_t seq,
-                                                             QuotaRow* __restrict__ quotas, int nq) {
+                                                             QuotaRow* __restrict__ quotas, int nq,
+                                                             int32_t* __restrict__ modlists, int slot, int depth,
+                                                             int n_prev, int wait) {
   extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
   const int lane = threadIdx.x;
   uint64_t* s_cand = smem;                                    // [nb][kCandStride]
@@ -2018,7 +2020,8 @@ __global__ __launch_bounds__(kWave) void resolve_round_numa(DevTable T, NumaTabl
   uint64_t* s_npw = s_podw + (size_t)nb * kPodWords;          // [nb] NumaPod
   uint64_t* s_nsw = s_npw + (size_t)nb * kNumaPodWords;       // [kWave] NumaStatic of the modified rows
   uint64_t* s_nmw = s_nsw + (size_t)kWave * kNumaStaticWords; // [kWave] NumaMut of the modified rows
-  uint32_t* bitmap = reinterpret_cast<uint32_t*>(s_nmw + (size_t)kWave * kNumaMutWords);
+  uint32_t* s_prevn = reinterpret_cast<uint32_t*>(s_nmw + (size_t)kWave * kNumaMutWords);  // [kWave] earlier winners
+  uint32_t* bitmap = s_prevn + kWave;
   for (int w = lane; w < nb * kCandStride; w += kWave) s_cand[w] = cand[w];
   {
     const uint64_t* pw = reinterpret_cast<const uint64_t*>(pods + first);
@@ -2028,7 +2031,25 @@ __global__ __launch_bounds__(kWave) void resolve_round_numa(DevTable T, NumaTabl
   }
   for (int w = lane; w < bitmap_words; w += kWave) bitmap[w] = 0;
   __syncthreads();
-  if (*poison || ctl[0] != first) {
+  // (r5) pipelined rounds: chain on the previous round's resolver (its rows, cursor, poison and winner list are
+  // published with a release of ctl[4] = its sequence number); bounded spin, as resolve_round
+  int timed_out = 0;
+  if (wait) {
+    if (lane == 0) {
+      int64_t it = 0;
+      while (__hip_atomic_load(&ctl[4], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < seq - 1) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++it > kSpinLimit) {
+          timed_out = 1;
+          break;
+        }
+      }
+    }
+    timed_out = __builtin_amdgcn_readfirstlane(timed_out);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
+  if (timed_out || *poison || ctl[0] != first) {
+    if (lane == 0 && timed_out) ctl[5] = 1;
     publish_round(ctl, seq);
     return;
   }
@@ -2044,6 +2065,37 @@ __global__ __launch_bounds__(kWave) void resolve_round_numa(DevTable T, NumaTabl
   bool touched = false;
   uint64_t my_out = 0;
   int nM = 0, consumed = 0;
+  {  // the rows the n_prev earlier rounds modified (snapshot-stale: NUMA is not monotone, so every modified row is
+     // re-scored for every pod anyway): de-duplicated into slots [0, nM), read after the chain wait
+    int n = 0;
+    for (int d = 1; d <= n_prev; ++d) {
+      const int32_t* ml = modlists + (size_t)(((slot - d) % depth + depth) % depth) * kModListStride;
+      const int c = ml[0];
+      for (int t = lane; t < c; t += kWave) s_prevn[n + t] = (uint32_t)ml[1 + t];
+      n += c;
+    }
+    __syncthreads();
+    const uint32_t node = lane < n ? s_prevn[lane] : 0xFFFFFFFFu;
+    bool dup = false;
+    for (int k = 0; k < n; ++k) dup |= lane > k && node == (uint32_t)__builtin_amdgcn_readlane((int)node, k);
+    const bool keep = lane < n && !dup;
+    const uint64_t km = __ballot(keep);
+    const uint64_t lane_lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    const int sl = __popcll(km & lane_lt);
+    __syncthreads();
+    if (keep) s_prevn[sl] = node;
+    __syncthreads();
+    nM = __popcll(km);
+    if (lane < nM) {
+      midx = s_prevn[lane];
+      mrow = load_row(T, midx);
+      s_ns[lane] = NT.s[midx];
+      s_nm[lane] = NT.m[midx];
+      mv = make_view(&s_ns[lane], &s_nm[lane], NP);
+      atomicOr(&bitmap[midx >> 5], 1u << (midx & 31));
+    }
+    __syncthreads();
+  }
   DevQuota ql = quota_load(quotas, nq, lane);
   for (int j = 0; j < nb; ++j) {
     const uint64_t key = s_cand[(size_t)j * kCandStride + lane];
@@ -2166,6 +2218,14 @@ __global__ __launch_bounds__(kWave) void resolve_round_numa(DevTable T, NumaTabl
   }
   if (lane < consumed) out_keys[first + lane] = my_out;
   quota_store(quotas, nq, lane, ql);
+  {  // this round's modified rows (its placed pods' nodes; duplicates allowed) for the next rounds
+    const bool mine = lane < consumed && my_out != 0;
+    const uint64_t bm = __ballot(mine);
+    const uint64_t lane_lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    int32_t* my_mod = modlists + (size_t)slot * kModListStride;
+    if (mine) my_mod[1 + __popcll(bm & lane_lt)] = (int32_t)key_node(my_out);
+    if (lane == 0) my_mod[0] = __popcll(bm);
+  }
   if (lane == 0) {
     ctl[0] = first + consumed;
     ctl[1] += 1;
@@ -4025,7 +4085,13 @@ RoundGeom geometry(const kg_engine* e) {
   int d = (int)(e->cfg.pipeline_depth > 0 ? e->cfg.pipeline_depth : 2);
   d = std::min(d, kMaxDepth);
   while (d > 1 && d * g.B > kMaxMod) --d;
-  g.depth = e->P.monotone ? d : 1;
+  // (r5) the NUMA rounds pipeline too: their resolver re-scores every row modified since the snapshot (the earlier
+  // rounds' winners included) for every pod, so no monotonicity is needed; its slots are one wave's lanes, one of
+  // them spare for the best unmodified candidate
+  const bool numa_rounds = e->numa_on && !e->ds_on && !e->rsv_on;
+  if (numa_rounds)
+    while (d > 1 && d * g.B >= kWave) --d;
+  g.depth = (e->P.monotone || numa_rounds) ? d : 1;
   if (e->numa_on) g.ppw = std::min(g.ppw, kNumaPpw);  // eval_round_numa parks ≤ kNumaPpw pods' values in LDS
   if (e->ds_on) g.ppw = std::min(g.ppw, kDsPpw);      // the DeviceShare passes keep ≤ kDsPpw pods in registers
   return g;
@@ -4038,7 +4104,7 @@ size_t resolve_lds_bytes(const RoundGeom& g, int nb) {
 constexpr size_t kMaxLds = 160 * 1024;
 size_t resolve_numa_lds_bytes(const RoundGeom& g, int nb) {
   return ((size_t)nb * (kCandStride + kPodWords + kNumaPodWords) + (size_t)kWave * (kNumaStaticWords + kNumaMutWords)) * 8 +
-         (size_t)g.bitmap_words * 4;
+         (size_t)kWave * 4 + (size_t)g.bitmap_words * 4;
 }
 NumaTable numa_table(kg_engine* e) { return NumaTable{e->numa_s.p, e->numa_m.p}; }
 
@@ -4173,7 +4239,8 @@ void launch_resolve(kg_engine* e, const RoundGeom& g, int64_t first, int nb, int
                                                                         e->P, e->NP, e->out_keys.p, e->out_cpus.p,
                                                                         e->out_nrec.p,
                                                                         g.bitmap_words, poison_ptr(e), seq, e->quotas.p,
-                                                                        e->nq);
+                                                                        e->nq, e->modlists.p, slot, g.depth, n_prev,
+                                                                        wait);
     return;
   }
 #define KG_RESOLVE_T(X, Q)                                                                                       \

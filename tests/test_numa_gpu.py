@@ -173,6 +173,18 @@ def test_c4_schedule_parity(batch):
     assert (cpus != 0).any()
 
 
+@pytest.mark.parametrize("batch,depth", [(16, 2), (16, 3), (8, 4), (15, 3)])
+def test_c4_pipelined_parity(batch, depth):
+    """(r5) Pipelined NUMA rounds: the resolver re-scores every row the earlier rounds in flight modified (their
+    winner lists), so depth 2..4 stays bit-exact although NodeNUMAResource is not monotone."""
+    cfg = F.build_config(profile=FULL_PROFILE, batch_pods=batch, pods_per_wave=min(8, batch), pipeline_depth=depth)
+    cluster, numa = synth.make_numa_cluster(700, seed=synth.BASE_SEED + 142)
+    pods = synth.make_numa_pods(2000, seed=synth.BASE_SEED + 143)
+    node, cpus = _numa_parity(cfg, cluster, numa, pods)
+    assert (node >= 0).mean() > 0.5
+    assert (cpus != 0).any()
+
+
 @pytest.mark.parametrize("variant", ["score_only", "most_allocated", "numa_only_spread_default"])
 def test_c4_profile_variants(variant):
     if variant == "score_only":
