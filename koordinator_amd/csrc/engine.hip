@@ -147,13 +147,36 @@ __device__ __forceinline__ void select_write(const uint32_t (&v)[NPT], const uin
 #pragma unroll
     for (int j = 0; j < NPT; ++j) sel[j] = fm[j];
   } else {
-    uint32_t cur = 0;
-    for (int b = vbits - 1; b >= 0; --b) {
-      const uint32_t c = cur | (1u << b);
-      int cnt = 0;
+    // (r5) τ from the tile's maximum first: the kR best of 64·NPT values usually lie within kSelWin of it, where
+    // log2(kSelWin) bisection steps suffice; otherwise the full vbits-step bisection (both give the same τ)
+    constexpr uint32_t kSelWin = 16;
+    uint32_t vm = 0;
 #pragma unroll
-      for (int j = 0; j < NPT; ++j) cnt += __popcll(__ballot(v[j] >= c));
-      if (cnt >= kR) cur = c;
+    for (int j = 0; j < NPT; ++j) vm = v[j] > vm ? v[j] : vm;
+    const uint32_t top = wave_max_u32(vm);
+    const uint32_t lo = top > kSelWin ? top - (kSelWin - 1) : 1u;
+    int cnt_lo = 0;
+#pragma unroll
+    for (int j = 0; j < NPT; ++j) cnt_lo += __popcll(__ballot(v[j] >= lo));
+    uint32_t cur = 0;
+    if (cnt_lo >= kR) {  // τ ∈ [lo, top]
+      cur = lo;
+#pragma unroll
+      for (int b = 3; b >= 0; --b) {
+        const uint32_t c = cur + (1u << b);
+        int cnt = 0;
+#pragma unroll
+        for (int j = 0; j < NPT; ++j) cnt += __popcll(__ballot(v[j] >= c));
+        if (c <= top && cnt >= kR) cur = c;
+      }
+    } else {
+      for (int b = vbits - 1; b >= 0; --b) {
+        const uint32_t c = cur | (1u << b);
+        int cnt = 0;
+#pragma unroll
+        for (int j = 0; j < NPT; ++j) cnt += __popcll(__ballot(v[j] >= c));
+        if (cnt >= kR) cur = c;
+      }
     }
     int need = kR;
     uint64_t eq[NPT];
@@ -163,15 +186,14 @@ __device__ __forceinline__ void select_write(const uint32_t (&v)[NPT], const uin
       eq[j] = __ballot(v[j] == cur);
       need -= __popcll(sel[j]);
     }
+    // ties at τ in (register j, lane) order: a lane's rank among them is a masked bit count, no peeling loop
+    const uint64_t lane_lt0 = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    int base = 0;
 #pragma unroll
     for (int j = 0; j < NPT; ++j) {
-      uint64_t m = eq[j];
-      while (need > 0 && m) {
-        const uint64_t low = m & (~m + 1);
-        sel[j] |= low;
-        m ^= low;
-        --need;
-      }
+      const int r = base + __popcll(eq[j] & lane_lt0);
+      sel[j] |= __ballot(((eq[j] >> lane) & 1ull) && r < need);
+      base += __popcll(eq[j]);
     }
   }
   const uint64_t lane_lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
