@@ -3306,6 +3306,8 @@ struct kg_engine {
   DevBuf<uint64_t> xr_norm_d;   // [kXrPods][kXrNorm]
   DevBuf<uint64_t> xr_lists;    // [kXrPods][tiles][kR]
   DevBuf<uint64_t> xr_cand;     // [kXrPods][kCandStride]
+  DevBuf<uint64_t> xr_norm_all; // (r5) [n_ranks][kXrPods][kXrNorm]: every rank's shard statistics (several ranks)
+  DevBuf<uint64_t> xr_rec_all;  // (r5) [n_ranks][kXrPods][kCandStride]: every rank's merged record (several ranks)
   hipGraphExec_t xr_exec = nullptr;  // kXrGraphRounds rounds
   std::vector<unsigned char> xr_exec_sig;
   double xr_avg = kXrPods;      // pods a round consumed on average (sizes the launches between host checks)
@@ -4685,8 +4687,12 @@ int run_xr(kg_engine* e, int64_t first, int64_t count, kg_stats* stats, double t
   const RsvExt X = rsv_ext(e);
   const unsigned long long init[8] = {0, 0, 0, (unsigned long long)first, (unsigned long long)end, 0, 0, 0};
   HIP_TRY(hipMemcpyAsync(e->rsv_ws.p, init, sizeof(init), hipMemcpyHostToDevice, e->stream));
-  const unsigned eval_blocks = (unsigned)(((nt + kEvalWaves - 1) / kEvalWaves) * (kXrPods / kXrPpw));
-  const unsigned xr_eval_blocks = (unsigned)nt * (kXrPods / kXrEvalPpw);
+  // (r5) several ranks: this rank's range of tiles (an empty range keeps one tile past the table: every node masked)
+  const int R = e->n_ranks, tpr = (nt + R - 1) / R, tile_base = e->rank * tpr;
+  const int ntl = std::max(1, std::min(tpr, nt - tile_base));
+  const int64_t lo = std::min<int64_t>(n, (int64_t)tile_base * kTile), hi = std::min<int64_t>(n, (int64_t)(tile_base + ntl) * kTile);
+  const unsigned eval_blocks = (unsigned)(((ntl + kEvalWaves - 1) / kEvalWaves) * (kXrPods / kXrPpw));
+  const unsigned xr_eval_blocks = (unsigned)ntl * (kXrPods / kXrEvalPpw);
   const int vbits = e->P.score_bits + 1;
   const int bitmap_words = (int)((n + 31) / 32);
   const int xf = (X.ns ? XF_NUMA : 0) | (X.ds ? XF_DS : 0) | (X.defp ? XF_DEF : 0);
@@ -4696,21 +4702,45 @@ int run_xr(kg_engine* e, int64_t first, int64_t count, kg_stats* stats, double t
   uint64_t* val = e->xr_val.p;
   uint32_t* val2 = e->def_score ? e->xr_val2.p : nullptr;
   uint32_t* affk = e->numa_on ? e->xr_aff.p : nullptr;
-  auto issue_round = [&]() {
+  const size_t norm_words = (size_t)kXrPods * kXrNorm, rec_words = (size_t)kXrPods * kCandStride;
+  if (R > 1) {
+    if (int rc = e->xr_norm_all.ensure(norm_words * R)) return rc;
+    if (int rc = e->xr_rec_all.ensure(rec_words * R)) return rc;
+  }
+  auto issue_round = [&]() -> int {
     size_t t = prof_begin(e, e->stream);
 #define KG_XR_EVAL(XF)                                                                                        \
-  xr_eval<XF><<<xr_eval_blocks, kTile, 0, e->stream>>>(e->T, e->rsv_d.p, e->rsv_nd.p, e->pods.p, e->rpods.p, n, nt, \
-                                                       stride, e->P, e->RP, X, val, val2, affk, e->xr_part.p,     \
-                                                       e->rsv_ws.p)
+  xr_eval<XF><<<xr_eval_blocks, kTile, 0, e->stream>>>(e->T, e->rsv_d.p, e->rsv_nd.p, e->pods.p, e->rpods.p, n, ntl, \
+                                                       tile_base, stride, e->P, e->RP, X, val, val2, affk,          \
+                                                       e->xr_part.p, e->rsv_ws.p)
     KG_XF_SWITCH(xf, KG_XR_EVAL);
 #undef KG_XR_EVAL
     prof_end(e, KG_PROF_RSV_EVAL, t, e->stream);
     t = prof_begin(e, e->stream);
-    xr_norm<<<kXrPods, 256, 0, e->stream>>>(e->xr_part.p, nt, e->xr_norm_d.p, e->rsv_ws.p);
-    xr_select<<<eval_blocks, kWave * kEvalWaves, 0, e->stream>>>(val, val2, n, nt, stride, vbits, e->RP, X,
+    if (R > 1) {  // the shard's statistics → every rank's → the global maxima and holder counts
+      uint64_t* mine = e->xr_norm_all.p + norm_words * e->rank;
+      xr_norm<<<kXrPods, 256, 0, e->stream>>>(e->xr_part.p, ntl, mine, e->rsv_ws.p);
+      if (int rc = rank_allgather(e, e->xr_norm_all.p, norm_words, 0, e->stream)) return rc;
+      xr_norm_combine<<<1, kXrPods * kXrNorm, 0, e->stream>>>(e->xr_norm_all.p, R, e->xr_norm_d.p, e->rsv_ws.p);
+    } else {
+      xr_norm<<<kXrPods, 256, 0, e->stream>>>(e->xr_part.p, ntl, e->xr_norm_d.p, e->rsv_ws.p);
+    }
+    xr_select<<<eval_blocks, kWave * kEvalWaves, 0, e->stream>>>(val, val2, n, ntl, tile_base, stride, vbits, e->RP, X,
                                                                e->xr_norm_d.p, e->xr_lists.p, e->rsv_ws.p);
-    merge_round<false><<<kXrPods, kMergeThreads, 0, e->stream>>>(e->T, e->P, e->xr_lists.p, (int64_t)nt * kR, kR, nt,
-                                                                 kR, kXrPods, poison, e->xr_cand.p);
+    uint64_t* rec = R > 1 ? e->xr_rec_all.p + rec_words * e->rank : e->xr_cand.p;
+    merge_round<false><<<kXrPods, kMergeThreads, 0, e->stream>>>(e->T, e->P, e->xr_lists.p, (int64_t)ntl * kR, kR, ntl,
+                                                                 kR, kXrPods, poison, rec);
+    if (R > 1) {  // every rank's record → the global record; the other shards' candidates evaluated here
+      if (int rc = rank_allgather(e, e->xr_rec_all.p, rec_words, 0, e->stream)) return rc;
+      merge_round<true><<<kXrPods, kMergeThreads, 0, e->stream>>>(e->T, e->P, e->xr_rec_all.p, kCandStride, rec_words,
+                                                                  R, kC, kXrPods, poison, e->xr_cand.p);
+#define KG_XR_FILL(XF)                                                                                              \
+  xr_fill<XF><<<kXrPods * kXrPods, kWave, 0, e->stream>>>(e->T, e->rsv_d.p, e->rsv_nd.p, e->pods.p, e->rpods.p, n, lo, \
+                                                          hi, stride, e->P, e->RP, X, e->xr_cand.p, val, val2, affk,  \
+                                                          e->rsv_ws.p)
+      KG_XF_SWITCH(xf, KG_XR_FILL);
+#undef KG_XR_FILL
+    }
     prof_end(e, KG_PROF_RSV_SELECT, t, e->stream);
     t = prof_begin(e, e->stream);
 #define KG_XR_RESOLVE(XF)                                                                                      \
@@ -4720,9 +4750,10 @@ int run_xr(kg_engine* e, int64_t first, int64_t count, kg_stats* stats, double t
     KG_XF_SWITCH(xf, KG_XR_RESOLVE);
 #undef KG_XR_RESOLVE
     prof_end(e, KG_PROF_RSV_APPLY, t, e->stream);
+    return 0;
   };
   static const bool no_graph = std::getenv("KG_RSV_NO_GRAPH") && std::getenv("KG_RSV_NO_GRAPH")[0] == '1';
-  if (!no_graph && !e->prof_on) {  // the instantiated graph of kXrGraphRounds rounds, keyed on its launch arguments
+  if (!no_graph && !e->prof_on && R == 1) {  // the instantiated graph of kXrGraphRounds rounds, keyed on its launch arguments
     std::vector<unsigned char> sig;
     auto put = [&](const void* q, size_t len) {
       const unsigned char* b = static_cast<const unsigned char*>(q);
@@ -4741,7 +4772,7 @@ int run_xr(kg_engine* e, int64_t first, int64_t count, kg_stats* stats, double t
       e->xr_exec = nullptr;
       hipGraph_t gr = nullptr;
       HIP_TRY(hipStreamBeginCapture(e->stream, hipStreamCaptureModeThreadLocal));
-      for (int r = 0; r < kXrGraphRounds; ++r) issue_round();
+      for (int r = 0; r < kXrGraphRounds; ++r) (void)issue_round();
       const hipError_t ce = hipStreamEndCapture(e->stream, &gr);
       if (ce != hipSuccess) return fail(KG_E_DEVICE, "hipStreamEndCapture: %s", hipGetErrorString(ce));
       const hipError_t ie = hipGraphInstantiate(&e->xr_exec, gr, nullptr, nullptr, 0);
@@ -4760,7 +4791,7 @@ int run_xr(kg_engine* e, int64_t first, int64_t count, kg_stats* stats, double t
     const double per = std::max(1.0, e->xr_avg);
     int64_t rounds = (int64_t)std::ceil((double)(end - cursor) / per);
     rounds = std::max<int64_t>(1, std::min<int64_t>(rounds, kMaxBatchRounds));
-    if (e->xr_exec && !e->prof_on) {
+    if (e->xr_exec && !e->prof_on && R == 1) {
       const int64_t graphs = (rounds + kXrGraphRounds - 1) / kXrGraphRounds;
       for (int64_t g = 0; g < graphs; ++g) {
         const hipError_t ge = hipGraphLaunch(e->xr_exec, e->stream);
@@ -4768,7 +4799,8 @@ int run_xr(kg_engine* e, int64_t first, int64_t count, kg_stats* stats, double t
       }
       rounds = graphs * kXrGraphRounds;
     } else {
-      for (int64_t r = 0; r < rounds; ++r) issue_round();
+      for (int64_t r = 0; r < rounds; ++r)  // (several ranks: every rank issues the same rounds, so the collectives pair)
+        if (int rc = issue_round()) return rc;
       HIP_TRY(hipGetLastError());
     }
     launched += rounds;
@@ -5370,6 +5402,8 @@ void kg_engine_destroy(kg_engine* e) {
   e->xr_norm_d.release();
   e->xr_lists.release();
   e->xr_cand.release();
+  e->xr_norm_all.release();
+  e->xr_rec_all.release();
   e->rsv_ws.release();
   e->rsv_part.release();
   e->npred.release();

@@ -17,6 +17,11 @@
 //              was modified (the holder count says so); the preferred node neither moves nor changes; and the best
 //              candidate is ≥ ub.  Otherwise the round stops before pod j and the next round starts there.
 // The first pod of a round always resolves (nothing modified yet), so every round makes progress.
+// (r5) Several ranks: each rank evaluates its own range of tiles (xr_eval / xr_select over tiles [tile_base,
+// tile_base + nt)), the per-pod statistics and the merged records are all-gathered (xr_norm_combine, merge_round<true>),
+// and xr_fill evaluates, on this rank's replica of the round-start table, the candidates of the merged records that
+// lie in other ranks' shards — the only nodes outside the shard whose round-start values the resolver reads (a
+// winner and every modified row is a listed candidate).  The table and the resolver stay replicated.
 #pragma once
 
 constexpr int kXrPods = 32;      // pods per round (< kWave: one modified row per resolver lane)
@@ -60,10 +65,10 @@ constexpr int kXrEvalPpw = 2;
 template <int XF>
 __global__ __launch_bounds__(kTile) void xr_eval(DevTable T, const RsvNode* __restrict__ RN,
                                                  const int32_t* __restrict__ rsv_n, const DevPod* __restrict__ pods,
-                                                 const RsvPod* __restrict__ rpods, int64_t n, int nt, int64_t stride,
-                                                 EvalParams P, RsvParams RP, RsvExt X, uint64_t* __restrict__ val,
-                                                 uint32_t* __restrict__ val2, uint32_t* __restrict__ affk,
-                                                 uint64_t* __restrict__ part,
+                                                 const RsvPod* __restrict__ rpods, int64_t n, int nt, int tile_base,
+                                                 int64_t stride, EvalParams P, RsvParams RP, RsvExt X,
+                                                 uint64_t* __restrict__ val, uint32_t* __restrict__ val2,
+                                                 uint32_t* __restrict__ affk, uint64_t* __restrict__ part,
                                                  const unsigned long long* __restrict__ ws) {
   __shared__ uint64_t s_st[kTile / kWave][kXrNorm];
   int64_t first;
@@ -76,7 +81,7 @@ __global__ __launch_bounds__(kTile) void xr_eval(DevTable T, const RsvNode* __re
   if (tile >= nt || p0 >= nb) return;  // block-uniform
   const int tid = threadIdx.x, lane = tid % kWave, wave = tid / kWave;
   const int p1 = p0 + kXrEvalPpw < nb ? p0 + kXrEvalPpw : nb;
-  const int64_t i = (int64_t)tile * kTile + tid;
+  const int64_t i = (int64_t)(tile_base + tile) * kTile + tid;  // nt tiles of this rank's shard
   for (int k = p0; k < p1; ++k) {
     const int64_t j = first + k;
     uint64_t pk = 0;
@@ -183,6 +188,65 @@ __global__ __launch_bounds__(256) void xr_norm(const uint64_t* __restrict__ part
   }
 }
 
+// several ranks: the global statistics per pod from the ranks' all-gathered xr_norm values ([n_ranks][kXrPods][kXrNorm]):
+// the preferred key's maximum, and per normalised Score the max of M + 1 with the holders summed over the ranks at it
+__global__ __launch_bounds__(kXrPods* kXrNorm) void xr_norm_combine(const uint64_t* __restrict__ all, int n_ranks,
+                                                                     uint64_t* __restrict__ norm,
+                                                                     const unsigned long long* __restrict__ ws) {
+  int64_t first;
+  int nb;
+  if (!xr_range(ws, first, nb)) return;
+  const int t = threadIdx.x, k = t / kXrNorm, q = t % kXrNorm;
+  if (k >= nb) return;
+  uint64_t r = 0;
+  uint32_t M = 0, C = 0;
+  for (int rk = 0; rk < n_ranks; ++rk) {
+    const uint64_t v = all[((size_t)rk * kXrPods + k) * kXrNorm + q];
+    if (q == 0) {
+      r = v > r ? v : r;
+    } else {
+      const uint32_t vm = (uint32_t)(v >> 32), vc = (uint32_t)v;
+      C = vm > M ? vc : C + (vm == M ? vc : 0u);
+      M = vm > M ? vm : M;
+    }
+  }
+  norm[(size_t)k * kXrNorm + q] = q == 0 ? r : ((uint64_t)M << 32) | C;
+}
+
+// several ranks: the round-start values (val, val2, the NUMA affinity) of pod k on every candidate of the merged
+// records that lies outside this rank's node range [lo, hi).  Block (k, j) = pod k on the kC entries of pod j's record,
+// one per lane; a node listed by several records is evaluated once per record, each time to the same values.
+template <int XF>
+__global__ __launch_bounds__(kWave) void xr_fill(DevTable T, const RsvNode* __restrict__ RN,
+                                                 const int32_t* __restrict__ rsv_n, const DevPod* __restrict__ pods,
+                                                 const RsvPod* __restrict__ rpods, int64_t n, int64_t lo, int64_t hi,
+                                                 int64_t stride, EvalParams P, RsvParams RP, RsvExt X,
+                                                 const uint64_t* __restrict__ cand, uint64_t* __restrict__ val,
+                                                 uint32_t* __restrict__ val2, uint32_t* __restrict__ affk,
+                                                 const unsigned long long* __restrict__ ws) {
+  int64_t first;
+  int nb;
+  if (!xr_range(ws, first, nb)) return;
+  const int k = blockIdx.x / kXrPods, jr = blockIdx.x % kXrPods, lane = threadIdx.x;
+  if (k >= nb || jr >= nb) return;
+  const uint64_t key = cand[(size_t)jr * kCandStride + lane];
+  if (key == 0) return;
+  const int64_t i = (int64_t)key_node(key);
+  if ((i >= lo && i < hi) || i >= n) return;
+  const int64_t j = first + k;
+  const DevPod p = pods[j];
+  const RsvPod rp = rpods[j];
+  const DsPod* dp = (XF & XF_DS) ? &X.dpods[j] : nullptr;
+  const NumaPod* np = (XF & XF_NUMA) ? &X.npods[j] : nullptr;
+  const int64_t* aux = (X.paux && (p.flags & P_AUX)) ? X.paux + (size_t)j * kAux : nullptr;
+  const DefPod* df = (XF & XF_DEF) ? &X.defp[j] : nullptr;
+  RsvExt Xk = X;
+  Xk.aff = X.aff ? affk + (size_t)k * stride : nullptr;
+  const RsvOut o = rsv_eval_node<false, false>(T, RN, rsv_n, i, p, rp, P, RP, Xk, dp, np, nullptr, aux, df);
+  val[(size_t)k * stride + i] = o.feas ? rsv_pack(o) : 0;
+  if (val2) val2[(size_t)k * stride + i] = o.feas ? (((uint32_t)o.tcnt << 24) | (uint32_t)o.asum) : 0u;
+}
+
 struct XrNorms {
   int64_t pref;             // the PreScore preferred node (-1 = none)
   int64_t mx, mds, mt, ma;  // the normalisation maxima rsv_total takes
@@ -202,7 +266,7 @@ __device__ __forceinline__ XrNorms xr_norms(const uint64_t* __restrict__ nk) {
 
 __global__ __launch_bounds__(kWave* kEvalWaves) void xr_select(const uint64_t* __restrict__ val,
                                                                const uint32_t* __restrict__ val2, int64_t n, int nt,
-                                                               int64_t stride, int vbits, RsvParams RP, RsvExt X,
+                                                               int tile_base, int64_t stride, int vbits, RsvParams RP, RsvExt X,
                                                                const uint64_t* __restrict__ norm,
                                                                uint64_t* __restrict__ lists,
                                                                const unsigned long long* __restrict__ ws) {
@@ -216,7 +280,7 @@ __global__ __launch_bounds__(kWave* kEvalWaves) void xr_select(const uint64_t* _
   const int p1 = p0 + kXrPpw < nb ? p0 + kXrPpw : nb;
   uint32_t gidx[kNPT];
 #pragma unroll
-  for (int q = 0; q < kNPT; ++q) gidx[q] = (uint32_t)((int64_t)tile * kTile + q * kWave + lane);
+  for (int q = 0; q < kNPT; ++q) gidx[q] = (uint32_t)((int64_t)(tile_base + tile) * kTile + q * kWave + lane);
   for (int k = p0; k < p1; ++k) {
     const XrNorms N = xr_norms(norm + (size_t)k * kXrNorm);
     uint32_t v[kNPT];

@@ -117,6 +117,7 @@ def _rank_main(rank, world, port, kind, out_dir):
                 np.save(os.path.join(out_dir, f"score{rank}.npy"), score)
                 np.save(os.path.join(out_dir, f"slot{rank}.npy"), e.fetch_reservations(0, len(pods)))
                 np.save(os.path.join(out_dir, f"cpu{rank}.npy"), e.read_state()["requested_cpu"])
+                np.save(os.path.join(out_dir, f"calls{rank}.npy"), np.array([calls[0]]))
             assert ex.error is None, ex.error
             return
         cfg, cluster, pods, dev = _case(kind)
@@ -169,8 +170,11 @@ def test_two_process_gloo_engine(tmp_path, kind):
 
 @pytest.mark.parametrize("kind", ["rsv", "shipped", "stock"])
 def test_two_process_gloo_exact_profiles(tmp_path, kind):
-    """The exact profiles on two ranks: every rank a full replica resolving the same FIFO order with no exchange
-     — both ranks' placements, totals, reservation slots and node state equal the oracle's."""
+    """The exact profiles on two ranks.  Reservation and the shipped profile run the batched exact rounds
+    sharded by node range: each rank evaluates its half of the tiles, the per-pod statistics and merged records go
+    through the exchange every round, and the other half's candidates are evaluated on the rank's replica (xr_fill).
+    The stock profile (PodTopologySpread / InterPodAffinity: the per-pod pass) stays a replica on every rank.  Both
+    ranks' placements, totals, reservation slots and node state equal the oracle's."""
     world = 2
     mp.spawn(_rank_main, args=(world, _free_port(), kind, str(tmp_path)), nprocs=world, join=True)
     cfg, w = _exact_case(kind)
@@ -196,4 +200,9 @@ def test_two_process_gloo_exact_profiles(tmp_path, kind):
         np.testing.assert_array_equal(np.load(tmp_path / f"score{r}.npy"), want_score)
         np.testing.assert_array_equal(np.load(tmp_path / f"slot{r}.npy"), want_slot)
         np.testing.assert_array_equal(np.load(tmp_path / f"cpu{r}.npy"), st["requested"][:, 0])
+        calls = int(np.load(tmp_path / f"calls{r}.npy")[0])
+        if kind == "stock":
+            assert calls == 0  # replicas: nothing to exchange
+        else:
+            assert calls >= 2 * 10, calls  # two exchanges per exact round, ≥ 10 rounds for these queues
     assert (want >= 0).mean() > 0.3

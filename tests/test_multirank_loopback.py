@@ -144,12 +144,15 @@ C5_PROFILE = F.Profile(filter=(F.NODE_RESOURCES_FIT, F.LOAD_AWARE, F.RESERVATION
                        score={F.NODE_RESOURCES_FIT: 1, F.LOAD_AWARE: 1, F.RESERVATION: 5000, F.DEVICE_SHARE: 1})
 
 
-def test_reservation_profile_ranks_replicated():
-    """C5 as one profile (Reservation + DeviceShare + ElasticQuota) on 2 ranks: the exact profiles run as replicas
-    (every rank evaluates its full table and resolves the same FIFO order), so every rank's placements,
-    reservation slots, GPU minors and quota charges equal the oracle's."""
+@pytest.mark.parametrize("n_ranks,n_nodes", [(2, 2000), (3, 2000), (3, 500)])
+def test_reservation_profile_ranks_sharded(n_ranks, n_nodes):
+    """C5 as one profile (Reservation + DeviceShare + ElasticQuota) on several ranks: (r5) the batched exact rounds
+    sharded by tile range — each rank evaluates its tiles, the per-pod statistics and merged records are exchanged
+    every round, and the other shards' listed candidates are evaluated on the rank's replica — so
+    every rank's placements, reservation slots, GPU minors and quota charges equal the oracle's.  500 nodes = 2 tiles
+    over 3 ranks: the last rank's shard is empty."""
     cfg = F.build_config(profile=C5_PROFILE)
-    cluster, dev, rsv = synth.make_c5_cluster(2000, seed=961)
+    cluster, dev, rsv = synth.make_c5_cluster(n_nodes, seed=961)
     pods = synth.make_c5_pods(1500, seed=962)
     quotas = synth.make_c5_quotas(pods, seed=963)
     st = oracle.states(cluster.n)
@@ -158,12 +161,40 @@ def test_reservation_profile_ranks_replicated():
     want, want_score, want_slot, want_minors = oracle.schedule_resv(cfg, cluster.nodes, cluster.metrics, st, r, pods,
                                                                     cluster.now_ns, devices=d, quotas=q, n_threads=8,
                                                                     with_minors=True)
-    out = run_ranks(cfg, 2, cluster.n, lambda e: synth.load_c5_into(e, cluster, dev, rsv, quotas), pods, chunks=2,
-                    fetch=lambda e: (e.fetch_reservations(0, len(pods)), e.fetch_devices(0, len(pods)),
-                                     e.read_quotas(len(quotas))))
+    out = run_ranks(cfg, n_ranks, cluster.n, lambda e: synth.load_c5_into(e, cluster, dev, rsv, quotas), pods,
+                    chunks=2, fetch=lambda e: (e.fetch_reservations(0, len(pods)), e.fetch_devices(0, len(pods)),
+                                               e.read_quotas(len(quotas))))
     same_on_every_rank(out, want, want_score, st)
-    for rk in range(2):
+    for rk in range(n_ranks):
         slot, minors, qq = out[rk][3]
         assert np.array_equal(slot, want_slot), rk
         assert np.array_equal(minors, want_minors), rk
         assert np.array_equal(qq, q), rk
+
+
+SHIPPED_PROFILE = F.Profile(filter=(F.NODE_RESOURCES_FIT, F.LOAD_AWARE, F.NODE_NUMA_RESOURCE, F.DEVICE_SHARE,
+                                    F.RESERVATION),
+                            score={F.NODE_RESOURCES_FIT: 1, F.LOAD_AWARE: 1, F.NODE_NUMA_RESOURCE: 1,
+                                   F.DEVICE_SHARE: 1, F.RESERVATION: 5000})
+
+
+def test_shipped_profile_ranks_sharded():
+    """The shipped profile (NUMA + DeviceShare + Reservation + ElasticQuota) on 4 ranks of sharded exact rounds: the
+    NUMA affinity of another shard's candidate comes from xr_fill on the rank's replica."""
+    cfg = F.build_config(profile=SHIPPED_PROFILE,
+                         la=F.LoadAwareSchedulingArgs(filter_expired_node_metrics=False,
+                                                      node_metric_expiration_seconds=300))
+    cluster, numa, dev, rsv = synth.make_shipped_cluster(1100, seed=1971)
+    pods = synth.make_shipped_pods(700, seed=1972)
+    quotas = synth.make_c5_quotas(pods, seed=1973)
+    st = oracle.states(cluster.n)
+    oracle.add_pods(cfg, st, cluster.existing_pods, cluster.existing_node)
+    want, want_score, want_slot = oracle.schedule_resv(cfg, cluster.nodes, cluster.metrics, st, rsv.copy(), pods,
+                                                       cluster.now_ns, devices=dev.copy(), quotas=quotas.copy(),
+                                                       n_threads=8, numa_buf=oracle.numa_states(numa))
+    out = run_ranks(cfg, 4, cluster.n, lambda e: synth.load_shipped_into(e, cluster, numa, dev, rsv, quotas), pods,
+                    chunks=2, fetch=lambda e: e.fetch_reservations(0, len(pods)))
+    same_on_every_rank(out, want, want_score, st)
+    for rk in range(4):
+        assert np.array_equal(out[rk][3], want_slot), rk
+    assert (want >= 0).mean() > 0.3
