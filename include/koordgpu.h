@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define KG_ABI_VERSION 13
+#define KG_ABI_VERSION 14
 
 /* ---- resource slots (fixed order) ------------------------------------------------------- */
 enum {
@@ -127,8 +127,10 @@ enum {
   KG_REJECT_RESERVATION = 1 << 8,   /* (ABI 11) Reservation Filter (kg_pods_filter_preemption): preemption failed /
                                        no reservation meets the requirements / reservation affinity */
   KG_REJECT_SPREAD = 1 << 9,        /* (ABI 12) PodTopologySpread: DoNotSchedule constraint's skew exceeded   */
-  KG_REJECT_INTERPOD = 1 << 10      /* (ABI 12) InterPodAffinity: affinity / anti-affinity / existing pods'
+  KG_REJECT_INTERPOD = 1 << 10,     /* (ABI 12) InterPodAffinity: affinity / anti-affinity / existing pods'
                                        anti-affinity rules not matched                                          */
+  KG_REJECT_NO_VICTIMS = 1 << 11    /* (ABI 14) kg_pods_select_victims: the candidate has no potential victims
+                                       ("No victims found on node": UnschedulableAndUnresolvable)              */
 };
 
 /* node flags */
@@ -670,9 +672,30 @@ int kg_pods_evaluate_reservation(kg_engine* e, const kg_pod* pod, int64_t* out);
  * node's reservation slot it was allocated from; NULL = none).  The Reservation Filter then fits the pod against them
  * (plugin.go:357-428, fitsNode :433-482).  out_reject: 0 = every enabled Filter passes, else KG_REJECT_* bits.
  * Profiles with NodeResourcesFit / LoadAwareScheduling / Reservation; NodeNUMAResource, DeviceShare and the upstream
- * defaults are refused (KG_E_UNSUPPORTED: the victims' cpusets / devices / labels are not modelled here). */
+ * defaults are refused (KG_E_UNSUPPORTED: the victims' cpusets / devices / labels are not modelled here).  (ABI 14)
+ * Pods and victims with ephemeral-storage / scalar requests are accepted. */
 int kg_pods_filter_preemption(kg_engine* e, const kg_pod* pod, int32_t node_idx, const kg_pod* victims,
                               const int32_t* victim_slot, int64_t n_victims, int32_t* out_reject);
+
+/* (ABI 14) The preemption dry run over many candidate nodes in ONE launch: SelectVictimsOnNode for every candidate
+ * (DryRunPreemption's per-node step: koordinator's elasticquota/preempt.go:111-215 and the k8s defaultpreemption
+ * plugin run the same loop), one device thread per candidate c = node node_idx[c]:
+ *   - its potential victims are victims[victim_offsets[c] .. victim_offsets[c + 1]) in the caller's reprieve order —
+ *     the caller's canPreempt selection (priority, quota), util.MoreImportantPod sort and filterPodsWithPDBViolation
+ *     split: PDB-violating victims first (pdb_violating[k] = 1; NULL = none), each group most important first;
+ *     victim_slot[k] as for kg_pods_filter_preemption (NULL = none);
+ *   - the device removes them all (NodeInfo.RemovePod + the Reservation plugin's RemovePod) and runs the Filters:
+ *     out_reject[c] = 0 or KG_REJECT_* bits (KG_REJECT_NO_VICTIMS for a candidate without potential victims);
+ *   - when they pass, it reprieves each victim in order: adds it back (AddPodInfo + AddPod), re-runs the Filters and
+ *     removes it again when the pod no longer fits: out_victim[k] = 1 for a victim kept, 0 for one reprieved (and for
+ *     every entry of a candidate whose Filters failed); out_violating[c] = numViolatingVictim.
+ * Nominated pods are not added (the engine holds no nominator).  Same profiles and refusals as
+ * kg_pods_filter_preemption; ephemeral-storage and scalar requests are carried in NodeResourcesFit and in fitsNode's
+ * EphemeralStorage / ScalarResources terms (reservation/plugin.go:471-479) by both entry points since ABI 14. */
+int kg_pods_select_victims(kg_engine* e, const kg_pod* pod, int64_t n_candidates, const int32_t* node_idx,
+                           const int64_t* victim_offsets, const kg_pod* victims, const int32_t* victim_slot,
+                           const uint8_t* pdb_violating, int32_t* out_reject, uint8_t* out_victim,
+                           int32_t* out_violating);
 
 /* (ABI 12) PodTopologySpread / InterPodAffinity state (engines whose profile enables either): per node and match
  * group k, [n][k] layout of KG_MAX_MATCH_GROUPS int32 each — pods matching group k (countPodsMatchSelector),

@@ -2737,88 +2737,151 @@ __global__ void evaluate_pod_rsv(DevTable T, const RsvNode* __restrict__ RN, con
   w[15] = 0;
 }
 
-// kg_pods_filter_preemption: the preemption dry run's Filter of one pod on one node (one thread): the restored node
-// minus the victims (NodeInfo.RemovePod), NodeResourcesFit + LoadAware on it, and the Reservation Filter with the
-// victims' requests as preemptible (reservation/plugin.go:284-310 RemovePod, :357-428 Filter, :433-482 fitsNode)
+// The preemption dry run on the device (kg_pods_filter_preemption, r5 kg_pods_select_victims): a candidate node's
+// restored NodeInfo copy minus its victims (NodeInfo.RemovePod) with the Reservation plugin's PreFilterExtensions
+// (reservation/plugin.go:253-310: RemovePod adds a non-reserve victim's non-zero requests to state.preemptible[node], or
+// to preemptibleInRRs[node][its reservation]; AddPod subtracts them again; either sets the map entry), then the pod's
+// Filters on it: NodeResourcesFit + LoadAware (eval_node), the ephemeral-storage / scalar fit on the victim-free
+// Requested, and the Reservation Filter with the preemptible amounts (:357-428, fitsNode :433-482).
 struct Victim {
   int64_t req_cpu, req_mem, nz_cpu, nz_mem;
-  int32_t slot;     // the node's reservation slot the victim was allocated from, -1 = none
-  int32_t nonzero;  // !quotav1.IsZero(PodRequestsAndLimits): RemovePod records it
+  int64_t aux[kAux];  // ephemeral-storage and the scalar resources (KG_RES_EPHEMERAL ..)
+  int32_t slot;       // the node's reservation slot the victim was allocated from, -1 = none
+  int32_t nonzero;    // counted by RemovePod / AddPod: !quotav1.IsZero(PodRequestsAndLimits) and not a reserve pod
 };
-__global__ void filter_pod_preempt(DevTable T, const RsvNode* __restrict__ RN, const int32_t* __restrict__ rsv_n,
-                                   const uint64_t* __restrict__ rsv_pred, const RsvSel* __restrict__ rsel, int64_t i, const DevPod* __restrict__ pod, RsvPod rp, EvalParams P, RsvParams RP,
-                                   int rsv_on, const Victim* __restrict__ vic, int64_t n_vic, int32_t* __restrict__ out) {
-  if (blockIdx.x != 0 || threadIdx.x != 0) return;
-  const DevPod p = *pod;
-  Row r = load_row(T, i);
-  if (!(r.flags & F_VALID)) {
-    *out = KG_REJECT_INVALID_NODE;
-    return;
-  }
-  uint32_t mm = 0;
-  int nm = 0;
-  int64_t pr_c = 0, pr_m = 0, ra_c = 0, ra_m = 0;
-  bool has_state = false;
-  const int ns = rsv_on ? rsv_n[i] : 0;
+struct PreNode {
+  Row r;
   RsvNode rn;
+  uint32_t mm;
+  int nm;
+  int64_t pr_c, pr_m, ra_c, ra_m;
+  bool has_state;
+  int64_t aux_req[kAux];                          // Requested of the aux resources, victims removed
+  int64_t pre_c, pre_m, pre_aux[kAux];            // state.preemptible[node]
+  int64_t rr_c[kRsvSlots], rr_m[kRsvSlots], rr_aux[kRsvSlots][kAux];  // preemptibleInRRs[node][slot]
+  bool pre_set;
+  uint32_t rr_set;
+};
+
+// BeforePreFilter's restore of node i for the pod (the same rsv_restore as the scheduling passes); false: invalid node
+__device__ bool pre_node_init(PreNode& S, const DevTable& T, const RsvNode* __restrict__ RN,
+                              const int32_t* __restrict__ rsv_n, const uint64_t* __restrict__ rsv_pred,
+                              const RsvSel* __restrict__ rsel, int64_t i, const RsvPod& rp, int rsv_on) {
+  S.r = load_row(T, i);
+  if (!(S.r.flags & F_VALID)) return false;
+  S.mm = 0;
+  S.nm = 0;
+  S.pr_c = S.pr_m = S.ra_c = S.ra_m = 0;
+  S.has_state = false;
+  const int ns = rsv_on ? rsv_n[i] : 0;
   if (ns > 0) {
-    rn = RN[i];
-    rsv_restore(rn, ns, rp, rsv_pred + (size_t)i * kRsvSlots, (rp.flags & RP_SEL) ? rsel : nullptr, r, mm, nm, pr_c,
-                pr_m, ra_c, ra_m, has_state);
+    S.rn = RN[i];
+    rsv_restore(S.rn, ns, rp, rsv_pred + (size_t)i * kRsvSlots, (rp.flags & RP_SEL) ? rsel : nullptr, S.r, S.mm, S.nm,
+                S.pr_c, S.pr_m, S.ra_c, S.ra_m, S.has_state);
   }
-  int64_t pre_c = 0, pre_m = 0, rr_c[kRsvSlots] = {}, rr_m[kRsvSlots] = {};
-  bool pre_set = false;
-  uint32_t rr_set = 0;
-  for (int64_t k = 0; k < n_vic; ++k) {
-    const Victim v = vic[k];
-    r.req_cpu -= v.req_cpu;
-    r.req_mem -= v.req_mem;
-    r.nz_cpu -= v.nz_cpu;
-    r.nz_mem -= v.nz_mem;
-    r.num_pods -= 1;
-    if (!v.nonzero) continue;
-    if (v.slot >= 0 && v.slot < kRsvSlots) {
-      rr_c[v.slot] += v.req_cpu;
-      rr_m[v.slot] += v.req_mem;
-      rr_set |= 1u << v.slot;
-    } else {
-      pre_c += v.req_cpu;
-      pre_m += v.req_mem;
-      pre_set = true;
-    }
+#pragma unroll
+  for (int q = 0; q < kAux; ++q) {
+    S.aux_req[q] = T.aux ? T.aux[(size_t)(kAux + q) * T.cap + i] : 0;
+    S.pre_aux[q] = 0;
   }
+  S.pre_c = S.pre_m = 0;
+  for (int s = 0; s < kRsvSlots; ++s) {
+    S.rr_c[s] = S.rr_m[s] = 0;
+#pragma unroll
+    for (int q = 0; q < kAux; ++q) S.rr_aux[s][q] = 0;
+  }
+  S.pre_set = false;
+  S.rr_set = 0;
+  return true;
+}
+
+// sign +1: NodeInfo.RemovePod + RemovePod; −1: NodeInfo.AddPodInfo + AddPod
+__device__ __forceinline__ void pre_node_apply(PreNode& S, const Victim& v, int64_t sign) {
+  S.r.req_cpu -= sign * v.req_cpu;
+  S.r.req_mem -= sign * v.req_mem;
+  S.r.nz_cpu -= sign * v.nz_cpu;
+  S.r.nz_mem -= sign * v.nz_mem;
+  S.r.num_pods -= sign;
+#pragma unroll
+  for (int q = 0; q < kAux; ++q) S.aux_req[q] -= sign * v.aux[q];
+  if (!v.nonzero) return;
+  if (v.slot >= 0 && v.slot < kRsvSlots) {
+    S.rr_c[v.slot] += sign * v.req_cpu;
+    S.rr_m[v.slot] += sign * v.req_mem;
+#pragma unroll
+    for (int q = 0; q < kAux; ++q) S.rr_aux[v.slot][q] += sign * v.aux[q];
+    S.rr_set |= 1u << v.slot;
+  } else {
+    S.pre_c += sign * v.req_cpu;
+    S.pre_m += sign * v.req_mem;
+#pragma unroll
+    for (int q = 0; q < kAux; ++q) S.pre_aux[q] += sign * v.aux[q];
+    S.pre_set = true;
+  }
+}
+
+// the pod's Filters on the candidate's current NodeInfo copy: 0 or KG_REJECT_* bits.  rq: the pod's kAux requests.
+__device__ uint32_t pre_node_filter(const DevTable& T, const PreNode& S, int64_t i, const DevPod& p,
+                                    const int64_t (&rq)[kAux], const RsvPod& rp, const EvalParams& P,
+                                    const RsvParams& RP, int rsv_on) {
   uint32_t rej = 0;
   int64_t t = 0;
-  (void)eval_node(r, p, P, t, &rej);  // NodeResourcesFit + LoadAware Filter verdicts on the victim-free NodeInfo
+  Row r = S.r;
+  r.flags &= ~F_EPH_OVER;  // recomputed below from the victim-free Requested
+  (void)eval_node(r, p, P, t, &rej);  // NodeResourcesFit + LoadAware Filter verdicts
+  bool any_aux = false;
+#pragma unroll
+  for (int q = 0; q < kAux; ++q) any_aux |= rq[q] != 0;
+  const bool zero = (p.flags & P_ZERO_REQ) != 0;
+  if (P.fit_filter && !zero && T.aux) {  // fitsRequest: ephemeral-storage always, a scalar only when requested
+#pragma unroll
+    for (int q = 0; q < kAux; ++q)
+      if ((q == 0 || rq[q] != 0) && rq[q] > T.aux[(size_t)q * T.cap + i] - S.aux_req[q]) rej |= KG_REJECT_FIT_OTHER;
+  }
   if (rsv_on && RP.filter) {
+    const RsvNode& rn = S.rn;
     const bool required = (rp.flags & RP_AFFINITY) != 0;
-    const bool zero = p.req_cpu == 0 && p.req_mem == 0;
-    // fitsNode with rInfo = slot s (s < 0: nil) and preemptible (pc, pm); a node without state has no podRequested
-    auto fits_node = [&](int s, int64_t pc, int64_t pm) {
-      if (r.num_pods - nm + 1 > r.alloc_pods) return false;
-      if (zero) return true;
+    const bool rzero = p.req_cpu == 0 && p.req_mem == 0 && !any_aux;
+    // fitsNode with rInfo = slot s (s < 0: nil) and preemptible (pc, pm, pa); a node without state has no podRequested.
+    // A reservation holds cpu / memory only (its Allocatable / Allocated of the aux resources are 0), and
+    // podRequested's aux part is the node's Requested at restore time (T.aux), which the victims do not change.
+    auto fits_node = [&](int s, int64_t pc, int64_t pm, const int64_t* pa) {
+      if (r.num_pods - S.nm + 1 > r.alloc_pods) return false;
+      if (rzero) return true;
       const int64_t rc = s >= 0 ? rsv_nn(rn.alloc_cpu[s], rn.allocd_cpu[s]) : 0;
       const int64_t rm = s >= 0 ? rsv_nn(rn.alloc_mem[s], rn.allocd_mem[s]) : 0;
-      const int64_t prc = has_state ? pr_c : 0, prm = has_state ? pr_m : 0;
-      return !(p.req_cpu > r.alloc_cpu - (prc - rc - ra_c - pc)) && !(p.req_mem > r.alloc_mem - (prm - rm - ra_m - pm));
+      const int64_t prc = S.has_state ? S.pr_c : 0, prm = S.has_state ? S.pr_m : 0;
+      if (p.req_cpu > r.alloc_cpu - (prc - rc - S.ra_c - pc)) return false;
+      if (p.req_mem > r.alloc_mem - (prm - rm - S.ra_m - pm)) return false;
+      if (T.aux) {
+        for (int q = 0; q < kAux; ++q) {
+          if (q > 0 && rq[q] == 0) continue;  // ScalarResources: the pod's request keys only
+          const int64_t pra = S.has_state ? T.aux[(size_t)(kAux + q) * T.cap + i] : 0;
+          if (rq[q] > T.aux[(size_t)q * T.cap + i] - (pra - pa[q])) return false;
+        }
+      }
+      return true;
     };
     bool ok = true;
-    if (mm == 0 || !has_state) {
+    if (S.mm == 0 || !S.has_state) {
       if (required) ok = false;
-      else if (pre_set || rr_set) ok = fits_node(-1, pre_c, pre_m);
+      else if (S.pre_set || S.rr_set) ok = fits_node(-1, S.pre_c, S.pre_m, S.pre_aux);
     } else {
       const bool kc = (p.flags & P_CPU_KEY) != 0, km = (p.flags & P_MEM_KEY) != 0;
       bool sat = false;
       for (int s = 0; s < kRsvSlots && !sat; ++s) {
-        if (!(mm >> s & 1)) continue;
+        if (!(S.mm >> s & 1)) continue;
         const bool hc = rn.alloc_cpu[s] > 0, hm = rn.alloc_mem[s] > 0;
         if (!((kc && hc) || (km && hm))) continue;  // Intersection(rInfo.ResourceNames, pod request names) empty
-        const bool fits = fits_node(s, rr_c[s] + pre_c, rr_m[s] + pre_m);
+        int64_t pa[kAux];
+#pragma unroll
+        for (int q = 0; q < kAux; ++q) pa[q] = S.rr_aux[s][q] + S.pre_aux[q];
+        const bool fits = fits_node(s, S.rr_c[s] + S.pre_c, S.rr_m[s] + S.pre_m, pa);
         if (((rn.meta[s] >> 4) & 3) == KG_RSV_POLICY_RESTRICTED) {
           int64_t ac = rn.allocd_cpu[s], am = rn.allocd_mem[s];
-          if (rr_set >> s & 1) {  // Allocated − preemptibleInRR, non-negative, masked to the reservation's keys
-            ac = hc ? rsv_nn(ac, rr_c[s]) : 0;
-            am = hm ? rsv_nn(am, rr_m[s]) : 0;
+          if (S.rr_set >> s & 1) {  // Allocated − preemptibleInRR, non-negative, masked to the reservation's keys
+            ac = hc ? rsv_nn(ac, S.rr_c[s]) : 0;
+            am = hm ? rsv_nn(am, S.rr_m[s]) : 0;
           }
           const int64_t rc = rsv_nn(rn.alloc_cpu[s], ac), rm = rsv_nn(rn.alloc_mem[s], am);
           sat = fits && (!hc || !kc || p.req_cpu <= rc) && (!hm || !km || p.req_mem <= rm);
@@ -2830,7 +2893,72 @@ __global__ void filter_pod_preempt(DevTable T, const RsvNode* __restrict__ RN, c
     }
     if (!ok) rej |= KG_REJECT_RESERVATION;
   }
-  *out = (int32_t)rej;
+  return rej;
+}
+
+// kg_pods_filter_preemption: one (pod, node) with every victim removed (one thread)
+__global__ void filter_pod_preempt(DevTable T, const RsvNode* __restrict__ RN, const int32_t* __restrict__ rsv_n,
+                                   const uint64_t* __restrict__ rsv_pred, const RsvSel* __restrict__ rsel, int64_t i,
+                                   const DevPod* __restrict__ pod, const int64_t* __restrict__ pod_aux, RsvPod rp,
+                                   EvalParams P, RsvParams RP, int rsv_on, const Victim* __restrict__ vic,
+                                   int64_t n_vic, int32_t* __restrict__ out) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  PreNode S;
+  if (!pre_node_init(S, T, RN, rsv_n, rsv_pred, rsel, i, rp, rsv_on)) {
+    *out = KG_REJECT_INVALID_NODE;
+    return;
+  }
+  const DevPod p = *pod;
+  int64_t rq[kAux];
+#pragma unroll
+  for (int q = 0; q < kAux; ++q) rq[q] = pod_aux[q];
+  for (int64_t k = 0; k < n_vic; ++k) pre_node_apply(S, vic[k], 1);
+  *out = (int32_t)pre_node_filter(T, S, i, p, rq, rp, P, RP, rsv_on);
+}
+
+// (r5) kg_pods_select_victims: SelectVictimsOnNode for every candidate (one thread per candidate, the victims in the
+// caller's reprieve order): remove every potential victim, Filter, then reprieve them one by one (add back, Filter,
+// remove again as a victim when the pod no longer fits).  elasticquota/preempt.go:111-215; k8s defaultpreemption.
+__global__ void select_victims(DevTable T, const RsvNode* __restrict__ RN, const int32_t* __restrict__ rsv_n,
+                               const uint64_t* __restrict__ rsv_pred, const RsvSel* __restrict__ rsel,
+                               const DevPod* __restrict__ pod, const int64_t* __restrict__ pod_aux, RsvPod rp,
+                               EvalParams P, RsvParams RP, int rsv_on, int64_t n_cand, const int32_t* __restrict__ nodes,
+                               const int64_t* __restrict__ off, const Victim* __restrict__ vic,
+                               const uint8_t* __restrict__ violating, int32_t* __restrict__ out_reject,
+                               uint8_t* __restrict__ out_victim, int32_t* __restrict__ out_violating) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= n_cand) return;
+  const int64_t i = nodes[c], k0 = off[c], k1 = off[c + 1];
+  for (int64_t k = k0; k < k1; ++k) out_victim[k] = 0;
+  out_violating[c] = 0;
+  PreNode S;
+  if (!pre_node_init(S, T, RN, rsv_n, rsv_pred, rsel, i, rp, rsv_on)) {
+    out_reject[c] = KG_REJECT_INVALID_NODE;
+    return;
+  }
+  if (k1 == k0) {  // "No victims found on node": UnschedulableAndUnresolvable, the node is not evaluated
+    out_reject[c] = KG_REJECT_NO_VICTIMS;
+    return;
+  }
+  const DevPod p = *pod;
+  int64_t rq[kAux];
+#pragma unroll
+  for (int q = 0; q < kAux; ++q) rq[q] = pod_aux[q];
+  for (int64_t k = k0; k < k1; ++k) pre_node_apply(S, vic[k], 1);
+  const uint32_t rej = pre_node_filter(T, S, i, p, rq, rp, P, RP, rsv_on);
+  out_reject[c] = (int32_t)rej;
+  if (rej) return;
+  int32_t nv = 0;
+  for (int64_t k = k0; k < k1; ++k) {  // reprievePod, in order
+    const Victim v = vic[k];
+    pre_node_apply(S, v, -1);
+    if (pre_node_filter(T, S, i, p, rq, rp, P, RP, rsv_on) != 0) {
+      pre_node_apply(S, v, 1);
+      out_victim[k] = 1;
+      nv += violating && violating[k] ? 1 : 0;
+    }
+  }
+  out_violating[c] = nv;
 }
 
 // Scatter of upserted device rows
@@ -6613,26 +6741,22 @@ int kg_pods_evaluate_reservation(kg_engine* e, const kg_pod* pod, int64_t* out) 
   return 0;
 }
 
-int kg_pods_filter_preemption(kg_engine* e, const kg_pod* pod, int32_t node_idx, const kg_pod* victims,
-                              const int32_t* victim_slot, int64_t n_victims, int32_t* out_reject) {
-  if (!e || !pod || !out_reject || n_victims < 0 || (n_victims > 0 && !victims)) return fail(KG_E_INVALID, "null argument");
-  if (node_idx < 0 || node_idx >= e->n_nodes) return fail(KG_E_INVALID, "node index %d outside [0, %lld)", node_idx,
-                                                           (long long)e->n_nodes);
+// the pod and its victims of one dry-run call, decoded and checked (the shared front half of the two entry points)
+static int preempt_prepare(kg_engine* e, const kg_pod* pod, const kg_pod* victims, const int32_t* victim_slot,
+                           int64_t n_victims, DevPod& d, RsvPod& rp, RsvSel& rs, int64_t (&rq)[kAux],
+                           std::vector<Victim>& hv) {
   if (e->numa_on || e->ds_on || e->def_on)
     return fail(KG_E_UNSUPPORTED, "preemption dry run: NodeNUMAResource / DeviceShare / the upstream defaults keep the "
                 "Go path (the victims' cpusets, devices and labels are not modelled)");
   if (int rc = sync_static(e)) return rc;
-  DevPod d;
   if (int rc = decode_pod(e, *pod, d)) return rc;
-  if (d.flags & P_AUX) return fail(KG_E_UNSUPPORTED, "preemption dry run: ephemeral-storage / scalar requests");
-  RsvPod rp;
-  RsvSel rs;
+  for (int q = 0; q < kAux; ++q) rq[q] = pod->requests[kAuxFirst + q];
   if (int rc = decode_rsv_pod(*pod, rp, rs, 0)) return rc;
   if (int rc = check_rsv_predicates(e, rsv_pred_top(rp, rs))) return rc;
   if (rp.flags & RP_SEL) rp.aux = 0;
   if (rp.flags & (RP_RESERVE | RP_OPERATING))
     return fail(KG_E_UNSUPPORTED, "preemption dry run for a reserve pod / reservation operating mode keeps the Go path");
-  std::vector<Victim> hv((size_t)std::max<int64_t>(n_victims, 1));
+  hv.resize((size_t)std::max<int64_t>(n_victims, 1));
   for (int64_t k = 0; k < n_victims; ++k) {
     DevPod v;
     if (int rc = decode_pod(e, victims[k], v)) return rc;
@@ -6643,21 +6767,113 @@ int kg_pods_filter_preemption(kg_engine* e, const kg_pod* pod, int32_t node_idx,
     // (r5) RemovePod returns before counting a reserve pod (reservation/plugin.go:286): the framework still
     // removes it from the NodeInfo copy, but it never becomes preemptible
     if (victims[k].flags & KG_POD_RESERVE) nz = false;
-    hv[k] = Victim{v.req_cpu, v.req_mem, v.nz_cpu, v.nz_mem, s, nz ? 1 : 0};
+    Victim w{v.req_cpu, v.req_mem, v.nz_cpu, v.nz_mem, {}, s, nz ? 1 : 0};
+    for (int q = 0; q < kAux; ++q) w.aux[q] = victims[k].requests[kAuxFirst + q];
+    hv[k] = w;
   }
+  return 0;
+}
+
+int kg_pods_filter_preemption(kg_engine* e, const kg_pod* pod, int32_t node_idx, const kg_pod* victims,
+                              const int32_t* victim_slot, int64_t n_victims, int32_t* out_reject) {
+  if (!e || !pod || !out_reject || n_victims < 0 || (n_victims > 0 && !victims)) return fail(KG_E_INVALID, "null argument");
+  if (node_idx < 0 || node_idx >= e->n_nodes) return fail(KG_E_INVALID, "node index %d outside [0, %lld)", node_idx,
+                                                           (long long)e->n_nodes);
+  DevPod d;
+  RsvPod rp;
+  RsvSel rs;
+  int64_t rq[kAux];
+  std::vector<Victim> hv;
+  if (int rc = preempt_prepare(e, pod, victims, victim_slot, n_victims, d, rp, rs, rq, hv)) return rc;
   const size_t vw = (hv.size() * sizeof(Victim) + 7) / 8;
-  if (int rc = e->scratch64.ensure(kPodWords + vw + 1 + sizeof(RsvSel) / 8)) return rc;
+  if (int rc = e->scratch64.ensure(kPodWords + kAux + vw + 1 + sizeof(RsvSel) / 8)) return rc;
   DevPod* gp = reinterpret_cast<DevPod*>(e->scratch64.p);
-  Victim* gv = reinterpret_cast<Victim*>(e->scratch64.p + kPodWords);
-  int32_t* go = reinterpret_cast<int32_t*>(e->scratch64.p + kPodWords + vw);
-  RsvSel* gs = reinterpret_cast<RsvSel*>(e->scratch64.p + kPodWords + vw + 1);
+  int64_t* ga = reinterpret_cast<int64_t*>(e->scratch64.p + kPodWords);
+  Victim* gv = reinterpret_cast<Victim*>(e->scratch64.p + kPodWords + kAux);
+  int32_t* go = reinterpret_cast<int32_t*>(e->scratch64.p + kPodWords + kAux + vw);
+  RsvSel* gs = reinterpret_cast<RsvSel*>(e->scratch64.p + kPodWords + kAux + vw + 1);
   HIP_TRY(hipMemcpyAsync(gp, &d, sizeof(d), hipMemcpyHostToDevice, e->stream));
+  HIP_TRY(hipMemcpyAsync(ga, rq, sizeof(rq), hipMemcpyHostToDevice, e->stream));
   HIP_TRY(hipMemcpyAsync(gs, &rs, sizeof(rs), hipMemcpyHostToDevice, e->stream));
   if (n_victims > 0) HIP_TRY(hipMemcpyAsync(gv, hv.data(), (size_t)n_victims * sizeof(Victim), hipMemcpyHostToDevice, e->stream));
-  filter_pod_preempt<<<1, kWave, 0, e->stream>>>(e->T, e->rsv_d.p, e->rsv_nd.p, e->rsv_pd.p, gs, node_idx, gp, rp, e->P, e->RP,
-                                                 e->rsv_on ? 1 : 0, gv, n_victims, go);
+  filter_pod_preempt<<<1, kWave, 0, e->stream>>>(e->T, e->rsv_d.p, e->rsv_nd.p, e->rsv_pd.p, gs, node_idx, gp, ga, rp,
+                                                 e->P, e->RP, e->rsv_on ? 1 : 0, gv, n_victims, go);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpyAsync(out_reject, go, 4, hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  return 0;
+}
+
+int kg_pods_select_victims(kg_engine* e, const kg_pod* pod, int64_t n_candidates, const int32_t* node_idx,
+                           const int64_t* victim_offsets, const kg_pod* victims, const int32_t* victim_slot,
+                           const uint8_t* pdb_violating, int32_t* out_reject, uint8_t* out_victim,
+                           int32_t* out_violating) {
+  if (!e || !pod || n_candidates < 0 || (n_candidates > 0 && (!node_idx || !victim_offsets || !out_reject ||
+                                                              !out_violating)))
+    return fail(KG_E_INVALID, "null argument");
+  if (n_candidates == 0) return 0;
+  if (victim_offsets[0] != 0) return fail(KG_E_INVALID, "victim_offsets[0] must be 0");
+  for (int64_t c = 0; c < n_candidates; ++c) {
+    if (node_idx[c] < 0 || node_idx[c] >= e->n_nodes)
+      return fail(KG_E_INVALID, "candidate %lld: node index %d outside [0, %lld)", (long long)c, node_idx[c],
+                  (long long)e->n_nodes);
+    if (victim_offsets[c + 1] < victim_offsets[c])
+      return fail(KG_E_INVALID, "victim_offsets decrease at candidate %lld", (long long)c);
+  }
+  const int64_t nv = victim_offsets[n_candidates];
+  if (nv > 0 && (!victims || !out_victim)) return fail(KG_E_INVALID, "null argument");
+  DevPod d;
+  RsvPod rp;
+  RsvSel rs;
+  int64_t rq[kAux];
+  std::vector<Victim> hv;
+  if (int rc = preempt_prepare(e, pod, victims, victim_slot, nv, d, rp, rs, rq, hv)) return rc;
+  // one device buffer: pod, pod aux, RsvSel, victims, offsets, nodes, violating flags, then the outputs
+  auto words = [](size_t bytes) { return (bytes + 7) / 8; };
+  const size_t w_pod = kPodWords, w_aux = kAux, w_sel = words(sizeof(RsvSel)), w_vic = words(hv.size() * sizeof(Victim));
+  const size_t w_off = (size_t)n_candidates + 1, w_nodes = words((size_t)n_candidates * 4),
+               w_viol = words((size_t)std::max<int64_t>(nv, 1)), w_rej = words((size_t)n_candidates * 4),
+               w_out = words((size_t)std::max<int64_t>(nv, 1)), w_nvio = words((size_t)n_candidates * 4);
+  size_t o = 0;
+  const size_t o_pod = o; o += w_pod;
+  const size_t o_aux = o; o += w_aux;
+  const size_t o_sel = o; o += w_sel;
+  const size_t o_vic = o; o += w_vic;
+  const size_t o_off = o; o += w_off;
+  const size_t o_nodes = o; o += w_nodes;
+  const size_t o_viol = o; o += w_viol;
+  const size_t o_rej = o; o += w_rej;
+  const size_t o_out = o; o += w_out;
+  const size_t o_nvio = o; o += w_nvio;
+  if (int rc = e->scratch64.ensure(o)) return rc;
+  int64_t* b = e->scratch64.p;
+  HIP_TRY(hipMemcpyAsync(b + o_pod, &d, sizeof(d), hipMemcpyHostToDevice, e->stream));
+  HIP_TRY(hipMemcpyAsync(b + o_aux, rq, sizeof(rq), hipMemcpyHostToDevice, e->stream));
+  HIP_TRY(hipMemcpyAsync(b + o_sel, &rs, sizeof(rs), hipMemcpyHostToDevice, e->stream));
+  if (nv > 0) HIP_TRY(hipMemcpyAsync(b + o_vic, hv.data(), (size_t)nv * sizeof(Victim), hipMemcpyHostToDevice, e->stream));
+  HIP_TRY(hipMemcpyAsync(b + o_off, victim_offsets, w_off * 8, hipMemcpyHostToDevice, e->stream));
+  HIP_TRY(hipMemcpyAsync(b + o_nodes, node_idx, (size_t)n_candidates * 4, hipMemcpyHostToDevice, e->stream));
+  const uint8_t* gviol = nullptr;
+  if (pdb_violating && nv > 0) {
+    HIP_TRY(hipMemcpyAsync(b + o_viol, pdb_violating, (size_t)nv, hipMemcpyHostToDevice, e->stream));
+    gviol = reinterpret_cast<const uint8_t*>(b + o_viol);
+  }
+  const unsigned blocks = (unsigned)((n_candidates + kWave - 1) / kWave);
+  select_victims<<<blocks, kWave, 0, e->stream>>>(e->T, e->rsv_d.p, e->rsv_nd.p, e->rsv_pd.p,
+                                                  reinterpret_cast<const RsvSel*>(b + o_sel),
+                                                  reinterpret_cast<const DevPod*>(b + o_pod),
+                                                  reinterpret_cast<const int64_t*>(b + o_aux), rp, e->P, e->RP,
+                                                  e->rsv_on ? 1 : 0, n_candidates,
+                                                  reinterpret_cast<const int32_t*>(b + o_nodes),
+                                                  reinterpret_cast<const int64_t*>(b + o_off),
+                                                  reinterpret_cast<const Victim*>(b + o_vic), gviol,
+                                                  reinterpret_cast<int32_t*>(b + o_rej),
+                                                  reinterpret_cast<uint8_t*>(b + o_out),
+                                                  reinterpret_cast<int32_t*>(b + o_nvio));
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(out_reject, b + o_rej, (size_t)n_candidates * 4, hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipMemcpyAsync(out_violating, b + o_nvio, (size_t)n_candidates * 4, hipMemcpyDeviceToHost, e->stream));
+  if (nv > 0) HIP_TRY(hipMemcpyAsync(out_victim, b + o_out, (size_t)nv, hipMemcpyDeviceToHost, e->stream));
   HIP_TRY(hipStreamSynchronize(e->stream));
   return 0;
 }

@@ -354,6 +354,36 @@ class Engine:
                                                            ptr(sl) if sl is not None else None, len(victims), ptr(out)))
         return int(out[0])
 
+    def select_victims(self, pod: np.ndarray, nodes, victims_per_node, slots_per_node=None, violating_per_node=None):
+        """SelectVictimsOnNode on every candidate node in one launch (kg_pods_select_victims).  victims_per_node[c]:
+        candidate c's potential victims (POD_DTYPE) in reprieve order; slots / violating: per-victim reservation slot
+        (-1 none) and PDB-violating flag.  Returns (reject int32[C], victim bool arrays per candidate, violating int32[C])."""
+        pod = np.ascontiguousarray(np.asarray(pod, dtype=abi.POD_DTYPE).reshape(1))
+        nodes = np.ascontiguousarray(nodes, dtype=np.int32)
+        counts = np.array([len(v) for v in victims_per_node], dtype=np.int64)
+        off = np.zeros(len(nodes) + 1, dtype=np.int64)
+        off[1:] = np.cumsum(counts)
+        nv = int(off[-1])
+        vic = np.zeros(max(nv, 1), dtype=abi.POD_DTYPE)
+        if nv:
+            vic[:nv] = np.concatenate([np.asarray(v, dtype=abi.POD_DTYPE).reshape(-1) for v in victims_per_node])
+        sl = vio = None
+        if slots_per_node is not None and nv:
+            sl = np.ascontiguousarray(np.concatenate([np.asarray(s, dtype=np.int32).reshape(-1)
+                                                      for s in slots_per_node]))
+        if violating_per_node is not None and nv:
+            vio = np.ascontiguousarray(np.concatenate([np.asarray(s, dtype=np.uint8).reshape(-1)
+                                                       for s in violating_per_node]))
+        rej = np.zeros(max(len(nodes), 1), dtype=np.int32)
+        kept = np.zeros(max(nv, 1), dtype=np.uint8)
+        nvio = np.zeros(max(len(nodes), 1), dtype=np.int32)
+        check(self.lib, self.lib.kg_pods_select_victims(self.h, ptr(pod), len(nodes), ptr(nodes), ptr(off), ptr(vic),
+                                                        ptr(sl) if sl is not None else None,
+                                                        ptr(vio) if vio is not None else None, ptr(rej), ptr(kept),
+                                                        ptr(nvio)))
+        return (rej[:len(nodes)], [kept[off[c]:off[c + 1]].astype(bool) for c in range(len(nodes))],
+                nvio[:len(nodes)])
+
     def evaluate_reservation(self, pod: np.ndarray) -> dict:
         """The exact pass's evaluation of one pod on every node (kg_pods_evaluate_reservation): per node pass,
         nominated slot, raw Reservation score, restore state (has_state, matched slots, restored Requested /

@@ -140,6 +140,8 @@ def lib():
         L.or_rsv_policy_filter.restype = i
         L.or_filter_preemption.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, i64, i64]
         L.or_filter_preemption.restype = i64
+        L.or_select_victims.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i64, vp, vp]
+        L.or_select_victims.restype = i64
         for f, res in (("or_taint_filter", i), ("or_taint_count", i64), ("or_affinity_filter", i),
                        ("or_affinity_sum", i64), ("or_image_score", i64)):
             getattr(L, f).argtypes = [vp, vp]
@@ -353,6 +355,23 @@ def filter_preemption(cfg, node, metric, state, rsv, pod, victims, slots, now_ns
                                           p(c(rsv, abi.NODE_RSV_DTYPE)) if rsv is not None else None,
                                           p(c(pod, abi.POD_DTYPE)), p(v) if len(v) else None, p(sl) if len(v) else None,
                                           len(v), now_ns))
+
+
+def select_victims(cfg, node, metric, state, rsv, pod, victims, slots, violating, now_ns: int):
+    """or_select_victims: SelectVictimsOnNode of one candidate → (reject bits, bool[k] victim kept, numViolating)."""
+    c = lambda a, dt: np.ascontiguousarray(np.asarray(a, dtype=dt).reshape(-1))
+    v = c(victims, abi.POD_DTYPE)
+    n = len(v)
+    sl = c(slots if slots is not None else -np.ones(n), np.int32)
+    vio = c(violating if violating is not None else np.zeros(n), np.uint8)
+    kept = np.zeros(max(n, 1), dtype=np.uint8)
+    nv = np.zeros(1, dtype=np.int32)
+    rej = int(lib().or_select_victims(p(cfg), p(c(node, abi.NODE_DTYPE)), p(c(metric, abi.METRIC_DTYPE)),
+                                      p(np.ascontiguousarray(state[:1])),
+                                      p(c(rsv, abi.NODE_RSV_DTYPE)) if rsv is not None else None,
+                                      p(c(pod, abi.POD_DTYPE)), p(v) if n else None, p(sl) if n else None,
+                                      p(vio) if n else None, n, now_ns, p(kept), p(nv)))
+    return rej, kept[:n].astype(bool), int(nv[0])
 
 
 def rsv_restore(rsv, st, pod) -> dict:

@@ -637,94 +637,116 @@ void or_rsv_restore_flat(const kg_node_reservations* r, const or_node_state* st,
   out[9] = ns.r_allocated[0], out[10] = ns.r_allocated[1];
 }
 
-/* fitsNode (plugin.go:433-482) with rInfo = slot s (s < 0: nil) and a preemptible amount.  `np` = len(NodeInfo.Pods)
- * of the NodeInfo the Filter sees (victims removed); podRequested / rAllocated are nodeReservationState's, which the
- * victims' removal does not touch (a node without state has none: zero). */
-static int fits_node_pre(const kg_pod* pod, int64_t allowed_pods, const int64_t alloc[2], const or_rsv_node* ns,
-                         int64_t np, const kg_node_reservations* r, int s, const int64_t pre[2]) {
-  if (np - ns->n_matched + 1 > allowed_pods) return 0;
-  const int64_t pc = pod->requests[KG_RES_CPU], pm = pod->requests[KG_RES_MEMORY];
-  if (pc == 0 && pm == 0) return 1;
+/* The preemption dry run's per-candidate state: the restored NodeInfo copy minus the removed victims and the
+ * Reservation plugin's preemptible maps (PreFilterExtensions RemovePod / AddPod, reservation/plugin.go:253-310: a
+ * non-reserve victim with non-zero requests adds (RemovePod) or subtracts (AddPod) its requests — every resource, so
+ * ephemeral-storage and the scalars too — to state.preemptible[node] or preemptibleInRRs[node][its reservation]; either
+ * call sets the map entry, which then stays non-empty). */
+typedef struct {
+  or_node_state rs;   /* the NodeInfo copy the Filters see */
+  or_rsv_node ns;     /* nodeReservationState (restore-time podRequested / rAllocated, untouched by the victims) */
+  int64_t pre[KG_RES_MAX], pre_rr[KG_MAX_RSV_SLOTS][KG_RES_MAX];
+  int pre_set, pre_rr_set;
+} pre_node;
+
+static void pre_node_init(pre_node* S, const kg_config* cfg, const or_node_state* st, const kg_node_reservations* rsv,
+                          const kg_pod* pod) {
+  const int rsv_on = cfg->reservation_filter || cfg->reservation_score;
+  memset(S, 0, sizeof(*S));
+  or_rsv_restore(rsv_on ? rsv : NULL, st, pod, &S->ns);
+  S->rs = *st;
+  S->rs.requested[KG_RES_CPU] = S->ns.requested[0];
+  S->rs.requested[KG_RES_MEMORY] = S->ns.requested[1];
+  S->rs.nonzero[0] = S->ns.nonzero[0];
+  S->rs.nonzero[1] = S->ns.nonzero[1];
+  S->rs.num_pods = S->ns.num_pods;
+}
+
+/* sign +1: NodeInfo.RemovePod + RemovePod; -1: NodeInfo.AddPodInfo + AddPod */
+static void pre_node_apply(pre_node* S, const kg_pod* v, int slot, int64_t sign) {
+  for (int q = 0; q < KG_RES_MAX; q++) S->rs.requested[q] -= sign * v->requests[q];
+  S->rs.nonzero[0] -= sign * v->nonzero_requests[0];
+  S->rs.nonzero[1] -= sign * v->nonzero_requests[1];
+  S->rs.num_pods -= sign;
+  int nz = 0; /* !quotav1.IsZero(podRequests): every requested resource counts, not only cpu / memory */
+  for (int q = 0; q < KG_RES_MAX; q++) nz |= v->requests[q] != 0;
+  if (!nz) return;
+  if (v->flags & KG_POD_RESERVE) return; /* RemovePod / AddPod (plugin.go:254,286): a reserve pod is never preemptible */
+  if (slot >= 0 && slot < KG_MAX_RSV_SLOTS) {
+    for (int q = 0; q < KG_RES_MAX; q++) S->pre_rr[slot][q] += sign * v->requests[q];
+    S->pre_rr_set |= 1 << slot;
+  } else {
+    for (int q = 0; q < KG_RES_MAX; q++) S->pre[q] += sign * v->requests[q];
+    S->pre_set = 1;
+  }
+}
+
+/* fitsNode (plugin.go:433-482) with rInfo = slot s (s < 0: nil) and a preemptible amount over every resource.  `np` =
+ * len(NodeInfo.Pods) of the NodeInfo the Filter sees (victims removed); podRequested / rAllocated are
+ * nodeReservationState's, which the victims' removal does not touch (a node without state has none: zero).  A
+ * reservation holds cpu / memory only, so its remained / allocated amounts of the other resources are 0, and
+ * podRequested's are the node's Requested at restore time (`st0`). */
+static int fits_node_pre(const kg_pod* pod, const kg_node* node, const or_node_state* st0, const or_rsv_node* ns,
+                         int64_t np, const kg_node_reservations* r, int s, const int64_t pre[KG_RES_MAX]) {
+  if (np - ns->n_matched + 1 > node->allowed_pods) return 0;
+  int zero = 1;
+  for (int q = 0; q < KG_RES_MAX; q++) zero &= pod->requests[q] == 0;
+  if (zero) return 1;
   int64_t rc = 0, rm = 0;
   if (s >= 0) {
     rc = sub_nn(r->allocatable_cpu[s], r->allocated_cpu[s]);
     rm = sub_nn(r->allocatable_mem[s], r->allocated_mem[s]);
   }
   const int64_t prc = ns->has_state ? ns->pod_requested[0] : 0, prm = ns->has_state ? ns->pod_requested[1] : 0;
-  if (pc > alloc[0] - (prc - rc - ns->r_allocated[0] - pre[0])) return 0;
-  if (pm > alloc[1] - (prm - rm - ns->r_allocated[1] - pre[1])) return 0;
+  if (pod->requests[KG_RES_CPU] > node->allocatable[KG_RES_CPU] - (prc - rc - ns->r_allocated[0] - pre[KG_RES_CPU]))
+    return 0;
+  if (pod->requests[KG_RES_MEMORY] > node->allocatable[KG_RES_MEMORY] - (prm - rm - ns->r_allocated[1] - pre[KG_RES_MEMORY]))
+    return 0;
+  /* EphemeralStorage always (:471), then `for rName, rQuant := range podRequest.ScalarResources` (:475-479) */
+  for (int q = KG_RES_EPHEMERAL; q <= KG_RES_MID_MEMORY; q++) {
+    if (q > KG_RES_EPHEMERAL && pod->requests[q] == 0) continue;
+    const int64_t pr = ns->has_state ? st0->requested[q] : 0;
+    if (pod->requests[q] > node->allocatable[q] - (pr - pre[q])) return 0;
+  }
   return 1;
 }
 
-int64_t or_filter_preemption(const kg_config* cfg, const kg_node* node, const kg_node_metric* metric,
-                             const or_node_state* st, const kg_node_reservations* rsv, const kg_pod* pod,
-                             const kg_pod* victims, const int32_t* victim_slot, int64_t n_victims, int64_t now) {
-  if (!(node->flags & KG_NODE_VALID)) return KG_REJECT_INVALID_NODE;
+/* the pod's Filters on the candidate's current NodeInfo copy: 0, KG_REJECT_* bits, or < 0 (an oracle error) */
+static int64_t pre_node_filter(const kg_config* cfg, const kg_node* node, const kg_node_metric* metric,
+                               const or_node_state* st0, const kg_node_reservations* rsv, const kg_pod* pod,
+                               const pre_node* S, int64_t now) {
   const int rsv_on = cfg->reservation_filter || cfg->reservation_score;
-  or_rsv_node ns;
-  or_rsv_restore(rsv_on ? rsv : NULL, st, pod, &ns);
-  /* the NodeInfo copy the dry run filters on: the restored node minus the victims (NodeInfo.RemovePod) */
-  or_node_state rs = *st;
-  rs.requested[KG_RES_CPU] = ns.requested[0];
-  rs.requested[KG_RES_MEMORY] = ns.requested[1];
-  rs.nonzero[0] = ns.nonzero[0];
-  rs.nonzero[1] = ns.nonzero[1];
-  rs.num_pods = ns.num_pods;
-  int64_t pre[2] = {0, 0}, pre_rr[KG_MAX_RSV_SLOTS][2];
-  int pre_set = 0, pre_rr_set = 0;
-  memset(pre_rr, 0, sizeof(pre_rr));
-  for (int64_t k = 0; k < n_victims; k++) {
-    const kg_pod* v = &victims[k];
-    rs.requested[KG_RES_CPU] -= v->requests[KG_RES_CPU];
-    rs.requested[KG_RES_MEMORY] -= v->requests[KG_RES_MEMORY];
-    rs.nonzero[0] -= v->nonzero_requests[0];
-    rs.nonzero[1] -= v->nonzero_requests[1];
-    rs.num_pods -= 1;
-    int nz = 0; /* !quotav1.IsZero(podRequests): every requested resource counts, not only cpu / memory */
-    for (int q = 0; q < KG_RES_MAX; q++) nz |= v->requests[q] != 0;
-    if (!nz) continue;
-    if (v->flags & KG_POD_RESERVE) continue; /* RemovePod (plugin.go:286): a reserve pod is never preemptible */
-    const int s = victim_slot ? victim_slot[k] : -1;
-    if (s >= 0 && s < KG_MAX_RSV_SLOTS) {
-      pre_rr[s][0] += v->requests[KG_RES_CPU];
-      pre_rr[s][1] += v->requests[KG_RES_MEMORY];
-      pre_rr_set |= 1 << s;
-    } else {
-      pre[0] += v->requests[KG_RES_CPU];
-      pre[1] += v->requests[KG_RES_MEMORY];
-      pre_set = 1;
-    }
-  }
   int64_t rej = 0;
-  if (cfg->fit_filter) rej |= or_fit_filter(node, &rs, pod);
+  if (cfg->fit_filter) rej |= or_fit_filter(node, &S->rs, pod);
   if (cfg->la_filter) {
     const int f = or_loadaware_filter(cfg, node, metric, pod, now);
     if (f < 0) return f;
     if (f) rej |= KG_REJECT_LOADAWARE;
   }
   if (rsv_on && cfg->reservation_filter) {
+    const or_rsv_node* ns = &S->ns;
     const int required = (pod->reservation_flags & KG_POD_RSV_AFFINITY) != 0;
-    const int64_t alloc[2] = {node->allocatable[KG_RES_CPU], node->allocatable[KG_RES_MEMORY]};
     int ok = 1;
-    if (ns.n_matched == 0 || !ns.has_state) {
+    if (ns->n_matched == 0 || !ns->has_state) {
       if (required) ok = 0;
-      else if (pre_set || pre_rr_set) ok = fits_node_pre(pod, node->allowed_pods, alloc, &ns, rs.num_pods, rsv, -1, pre);
+      else if (S->pre_set || S->pre_rr_set) ok = fits_node_pre(pod, node, st0, ns, S->rs.num_pods, rsv, -1, S->pre);
     } else {
       const int64_t pc = pod->requests[KG_RES_CPU], pm = pod->requests[KG_RES_MEMORY];
       const int kc = or_pod_cpu_key(pod), km = or_pod_mem_key(pod);
       int satisfied = 0;
-      for (int k = 0; k < ns.n_matched && !satisfied; k++) {
-        const int s = ns.matched[k];
+      for (int k = 0; k < ns->n_matched && !satisfied; k++) {
+        const int s = ns->matched[k];
         const int hc = rsv->allocatable_cpu[s] > 0, hm = rsv->allocatable_mem[s] > 0;
         if (!((kc && hc) || (km && hm))) continue;
-        const int64_t p2[2] = {pre_rr[s][0] + pre[0], pre_rr[s][1] + pre[1]};
-        const int fits = fits_node_pre(pod, node->allowed_pods, alloc, &ns, rs.num_pods, rsv, s, p2);
+        int64_t p2[KG_RES_MAX]; /* framework.NewResource(preemptibleInRR) + preemptible[node] */
+        for (int q = 0; q < KG_RES_MAX; q++) p2[q] = S->pre_rr[s][q] + S->pre[q];
+        const int fits = fits_node_pre(pod, node, st0, ns, S->rs.num_pods, rsv, s, p2);
         if (rsv->policy[s] == KG_RSV_POLICY_RESTRICTED) {
           /* Allocated − preemptibleInRR (non-negative, masked to the reservation's keys) when that map is set */
           int64_t ac = rsv->allocated_cpu[s], am = rsv->allocated_mem[s];
-          if ((pre_rr_set >> s) & 1) {
-            ac = hc ? sub_nn(ac, pre_rr[s][0]) : 0;
-            am = hm ? sub_nn(am, pre_rr[s][1]) : 0;
+          if ((S->pre_rr_set >> s) & 1) {
+            ac = hc ? sub_nn(ac, S->pre_rr[s][KG_RES_CPU]) : 0;
+            am = hm ? sub_nn(am, S->pre_rr[s][KG_RES_MEMORY]) : 0;
           }
           const int64_t rc = sub_nn(rsv->allocatable_cpu[s], ac), rm = sub_nn(rsv->allocatable_mem[s], am);
           if ((!hc || !kc || pc <= rc) && (!hm || !km || pm <= rm) && fits) satisfied = 1;
@@ -737,4 +759,47 @@ int64_t or_filter_preemption(const kg_config* cfg, const kg_node* node, const kg
     if (!ok) rej |= KG_REJECT_RESERVATION;
   }
   return rej;
+}
+
+int64_t or_filter_preemption(const kg_config* cfg, const kg_node* node, const kg_node_metric* metric,
+                             const or_node_state* st, const kg_node_reservations* rsv, const kg_pod* pod,
+                             const kg_pod* victims, const int32_t* victim_slot, int64_t n_victims, int64_t now) {
+  if (!(node->flags & KG_NODE_VALID)) return KG_REJECT_INVALID_NODE;
+  pre_node S;
+  pre_node_init(&S, cfg, st, rsv, pod);
+  for (int64_t k = 0; k < n_victims; k++) pre_node_apply(&S, &victims[k], victim_slot ? victim_slot[k] : -1, 1);
+  return pre_node_filter(cfg, node, metric, st, rsv, pod, &S, now);
+}
+
+/* SelectVictimsOnNode (elasticquota/preempt.go:111-215; k8s defaultpreemption) of one candidate node, the potential
+ * victims given in reprieve order (PDB-violating first, each group by util.MoreImportantPod — the caller's sort and
+ * filterPodsWithPDBViolation): remove them all, Filter (none: "No victims found" → KG_REJECT_NO_VICTIMS), then
+ * reprieve each in order — add it back, Filter, remove it again as a victim when the pod no longer fits (:175-213).
+ * out_victim[k] = 1 for a victim kept; *out_violating = the PDB-violating victims kept.  Returns the first Filter's
+ * status (0 = a candidate), or < 0 on an oracle error. */
+int64_t or_select_victims(const kg_config* cfg, const kg_node* node, const kg_node_metric* metric,
+                          const or_node_state* st, const kg_node_reservations* rsv, const kg_pod* pod,
+                          const kg_pod* victims, const int32_t* victim_slot, const uint8_t* violating,
+                          int64_t n_victims, int64_t now, uint8_t* out_victim, int32_t* out_violating) {
+  for (int64_t k = 0; k < n_victims; k++) out_victim[k] = 0;
+  *out_violating = 0;
+  if (!(node->flags & KG_NODE_VALID)) return KG_REJECT_INVALID_NODE;
+  if (n_victims == 0) return KG_REJECT_NO_VICTIMS;
+  pre_node S;
+  pre_node_init(&S, cfg, st, rsv, pod);
+  for (int64_t k = 0; k < n_victims; k++) pre_node_apply(&S, &victims[k], victim_slot ? victim_slot[k] : -1, 1);
+  const int64_t rej = pre_node_filter(cfg, node, metric, st, rsv, pod, &S, now);
+  if (rej != 0) return rej;
+  for (int64_t k = 0; k < n_victims; k++) {
+    const int slot = victim_slot ? victim_slot[k] : -1;
+    pre_node_apply(&S, &victims[k], slot, -1);
+    const int64_t f = pre_node_filter(cfg, node, metric, st, rsv, pod, &S, now);
+    if (f < 0) return f;
+    if (f != 0) {
+      pre_node_apply(&S, &victims[k], slot, 1);
+      out_victim[k] = 1;
+      if (violating && violating[k]) *out_violating += 1;
+    }
+  }
+  return 0;
 }

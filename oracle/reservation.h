@@ -97,12 +97,19 @@ void or_rsv_restore_flat(const kg_node_reservations* r, const or_node_state* st,
  * with the victims removed): NodeInfo.RemovePod of each victim, and Reservation's PreFilterExtensions.RemovePod
  * (plugin.go:284-310) adding each victim's requests to state.preemptible[node] (victim_slot[k] < 0) or to
  * state.preemptibleInRRs[node][slot] — a victim with all-zero requests is skipped.  Then the pod's Filters on that
- * node: NodeResourcesFit (cpu / memory / pods), LoadAwareScheduling, and the Reservation Filter (plugin.go:357-428)
+ * node: NodeResourcesFit (cpu / memory / pods / ephemeral-storage / scalars), LoadAwareScheduling, and the Reservation Filter (plugin.go:357-428)
  * with the preemptible amounts in fitsNode (:433-482) and the Restricted policy's Allocated (:404-413).  Returns the
  * KG_REJECT_* bits (0 = every Filter passes).  Profiles: Fit / LoadAware / Reservation. */
 int64_t or_filter_preemption(const kg_config* cfg, const kg_node* node, const kg_node_metric* metric,
                              const or_node_state* st, const kg_node_reservations* rsv, const kg_pod* pod,
                              const kg_pod* victims, const int32_t* victim_slot, int64_t n_victims, int64_t now);
+/* (r5) SelectVictimsOnNode of one candidate (elasticquota/preempt.go:111-215): the potential victims in reprieve
+ * order are removed, the Filters run (none: KG_REJECT_NO_VICTIMS), then each victim is reprieved in order (added
+ * back, kept as a victim when the pod no longer fits).  out_victim[k], *out_violating as kg_pods_select_victims. */
+int64_t or_select_victims(const kg_config* cfg, const kg_node* node, const kg_node_metric* metric,
+                          const or_node_state* st, const kg_node_reservations* rsv, const kg_pod* pod,
+                          const kg_pod* victims, const int32_t* victim_slot, const uint8_t* violating,
+                          int64_t n_victims, int64_t now, uint8_t* out_victim, int32_t* out_violating);
 
 #ifdef __cplusplus
 }

@@ -197,3 +197,171 @@ def test_device_matches_oracle_random(seed):
                 assert got == want, (prof, j, i, k, got, want)
                 seen.add(want)
         assert len(seen) > 1  # both verdicts occur
+
+
+# ---- (r5) SelectVictimsOnNode over many candidates in one launch (kg_pods_select_victims) -------------------------
+# The reprieve loop (elasticquota/preempt.go:111-215, the k8s defaultpreemption loop) has no table of its own in the
+# reference; its per-step Filter is the one the tables above pin.  The known answers below are derived by hand from
+# preempt.go's loop.
+
+
+def _select_oracle(cfg, cluster, rsv, pod, vic, slots, violating, node=0):
+    st = oracle.states(cluster.n)
+    oracle.add_pods(cfg, st, cluster.existing_pods, cluster.existing_node)
+    return oracle.select_victims(cfg, cluster.nodes[node], cluster.metrics[node], st[node:node + 1],
+                                 rsv[node] if rsv is not None else None, pod, vic, slots, violating, cluster.now_ns)
+
+
+FIT_ONLY = F.Profile(filter=(F.NODE_RESOURCES_FIT,), score={F.NODE_RESOURCES_FIT: 1})
+
+
+def _fit_cluster(spec, alloc_cpu="8", eph=None):
+    node = F.make_node({"cpu": alloc_cpu, "memory": "8Gi", **({"ephemeral-storage": eph} if eph else {})})
+    vic = np.zeros(len(spec), dtype=abi.POD_DTYPE)
+    for k, (c, e) in enumerate(spec):
+        req = {"cpu": f"{c}m"}
+        if e:
+            req["ephemeral-storage"] = str(e)
+        vic[k] = F.make_pod(requests=req, limits=req)[0]
+    cluster = synth.Cluster(node, F.make_node_metric(present=False, node_usage=None), vic,
+                            np.zeros(len(vic), dtype=np.int32), 10**18)
+    return cluster, vic
+
+
+def test_oracle_select_victims_reprieve_order():
+    """8-cpu node holding victims 3 / 3 / 2 cpu (reprieve order), pod 4 cpu: all removed → fits; v0 reprieved (3 + 4 ≤
+    8), v1 stays a victim (6 + 4 > 8), v2 stays a victim (3 + 2 + 4 > 8).  v1 is PDB-violating → numViolating 1."""
+    cfg = F.build_config(profile=FIT_ONLY)
+    cluster, vic = _fit_cluster([(3000, 0), (3000, 0), (2000, 0)])
+    rej, kept, nv = _select_oracle(cfg, cluster, None, _pod(4000), vic, None, [0, 1, 0])
+    assert rej == 0 and kept.tolist() == [False, True, True] and nv == 1
+    # a different order reprieves differently: 2 first (2 + 4 ≤ 8), then each 3 overflows (5 + 4, 5 + 4)
+    rej, kept, nv = _select_oracle(cfg, cluster, None, _pod(4000), vic[[2, 0, 1]], None, None)
+    assert rej == 0 and kept.tolist() == [False, True, True] and nv == 0
+    # a 1-cpu pod: everything is reprieved but the last (3 + 3 + 2 + 1 > 8)
+    rej, kept, nv = _select_oracle(cfg, cluster, None, _pod(1000), vic, None, None)
+    assert rej == 0 and kept.tolist() == [False, False, True]
+
+
+def test_oracle_select_victims_no_victims_and_unfit():
+    cfg = F.build_config(profile=FIT_ONLY)
+    cluster, vic = _fit_cluster([(3000, 0)])
+    assert _select_oracle(cfg, cluster, None, _pod(4000), vic[:0], None, None)[0] == abi.REJECT_NO_VICTIMS
+    rej, kept, _ = _select_oracle(cfg, cluster, None, _pod(9000), vic, None, None)  # 9 > 8 even on an empty node
+    assert rej & abi.REJECT_FIT_CPU and not kept.any()
+
+
+def test_oracle_select_victims_ephemeral():
+    """ephemeral-storage (ABI 14): 10 GB node, victims 6 GB / 3 GB, pod 5 GB + 1 cpu: v0 stays (6 + 5 > 10), v1 is
+    reprieved (3 + 5 ≤ 10)."""
+    cfg = F.build_config(profile=FIT_ONLY)
+    cluster, vic = _fit_cluster([(1000, 6 * 10**9), (1000, 3 * 10**9)], eph="10G")
+    pod = F.make_pod(requests={"cpu": "1", "ephemeral-storage": str(5 * 10**9)})
+    pod["reservation_owner_mask"] = 1
+    rej, kept, _ = _select_oracle(cfg, cluster, None, pod, vic, None, None)
+    assert rej == 0 and kept.tolist() == [True, False]
+
+
+def test_oracle_preemption_reservation_fits_node_ephemeral():
+    """fitsNode's EphemeralStorage term (plugin.go:471): an unmatched reservation's node with ephemeral-storage
+    Requested 9 GB of 10 GB; the pod asks 3 GB.  Preempting a 1 GB victim (preemptible 1 GB) still rejects
+    (3 > 10 − (9 − 1)); a 2 GB victim passes (3 ≤ 10 − (9 − 2))."""
+    cfg = F.build_config(profile=RSV_ONLY)
+    node = F.make_node({"cpu": "32", "memory": "32Gi", "ephemeral-storage": "10G"}, allowed_pods=100)
+    for ve, want in ((1 * 10**9, REJ), (2 * 10**9, 0)):
+        v = F.make_pod(requests={"cpu": "1", "ephemeral-storage": str(ve)})
+        filler = F.make_pod(requests={"cpu": "30", "ephemeral-storage": str(9 * 10**9 - ve)})
+        existing = np.concatenate([filler, v])
+        cluster = synth.Cluster(node, F.make_node_metric(present=False, node_usage=None), existing,
+                                np.zeros(2, dtype=np.int32), 10**18)
+        rsv = _rsv(abi.RSV_POLICY["Default"], 5, 4000, 4000, 1)
+        pod = F.make_pod(requests={"cpu": "1", "ephemeral-storage": str(3 * 10**9)})
+        pod["reservation_owner_mask"] = 1
+        assert oracle_verdict(cfg, cluster, rsv, pod, v, np.array([-1], np.int32)) == want, ve
+
+
+def _random_candidates(cluster, rsv, rng, n_cand, aux=False):
+    """per candidate node: a random subset of its pods in random reprieve order, random slots and PDB flags"""
+    nodes = rng.choice(cluster.n, size=n_cand, replace=False).astype(np.int32)
+    vics, slots, viol = [], [], []
+    for i in nodes:
+        on = np.nonzero(cluster.existing_node == i)[0]
+        k = int(rng.integers(0, len(on) + 1))
+        pick = rng.permutation(on)[:k]
+        vics.append(cluster.existing_pods[pick])
+        ns = int(rsv["n"][i]) if rsv is not None else 0
+        slots.append(np.where((rng.random(k) < 0.4) & (ns > 0), rng.integers(0, max(ns, 1), k), -1).astype(np.int32))
+        viol.append((rng.random(k) < 0.3).astype(np.uint8))
+    return nodes, vics, slots, viol
+
+
+def _with_ephemeral(cluster, rng):
+    """ephemeral-storage on every node (100 GB) and on ~half of the pods (1-20 GB)"""
+    cluster.nodes["allocatable"][:, abi.RES_EPHEMERAL] = 100 * 10**9
+    pods = cluster.existing_pods
+    m = rng.random(len(pods)) < 0.5
+    pods["requests"][m, abi.RES_EPHEMERAL] = rng.integers(1, 21, int(m.sum())) * 10**9
+    return cluster
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [1, 2])
+def test_device_select_victims_matches_oracle(seed):
+    """One kg_pods_select_victims launch per pod over 48 candidate nodes of a random Reservation cluster (every policy,
+    owned / affinity pods), random victim subsets in random reprieve order with reservation slots and PDB flags, half
+    of the pods and victims carrying ephemeral-storage: per candidate the Filter status, the victims kept and
+    numViolatingVictim equal the oracle's, for the Reservation-only profile and Fit + LoadAware + Reservation."""
+    rng = np.random.default_rng(70 + seed)
+    cluster, rsv = synth.make_rsv_cluster(96, seed=910 + seed)
+    cluster = _with_ephemeral(cluster, rng)
+    pods = synth.make_rsv_pods(24, seed=960 + seed)
+    em = rng.random(len(pods)) < 0.5
+    pods["requests"][em, abi.RES_EPHEMERAL] = rng.integers(1, 40, int(em.sum())) * 10**9
+    stats = {"kept": 0, "reprieved": 0, "rejected": 0, "none": 0}
+    for prof in (RSV_ONLY, PROFILE):
+        cfg = F.build_config(profile=prof)
+        st = oracle.states(cluster.n)
+        oracle.add_pods(cfg, st, cluster.existing_pods, cluster.existing_node)
+        with Engine(cfg, cluster.n) as e:
+            synth.load_rsv_into(e, cluster, rsv)
+            for j in range(len(pods)):
+                nodes, vics, slots, viol = _random_candidates(cluster, rsv, rng, 48)
+                rej, kept, nvio = e.select_victims(pods[j:j + 1], nodes, vics, slots, viol)
+                for c, i in enumerate(nodes):
+                    w_rej, w_kept, w_nv = oracle.select_victims(cfg, cluster.nodes[i], cluster.metrics[i],
+                                                                st[i:i + 1], rsv[i], pods[j:j + 1], vics[c], slots[c],
+                                                                viol[c], cluster.now_ns)
+                    assert (rej[c], kept[c].tolist(), nvio[c]) == (w_rej, w_kept.tolist(), w_nv), (prof, j, c, i)
+                    if w_rej == abi.REJECT_NO_VICTIMS:
+                        stats["none"] += 1
+                    elif w_rej:
+                        stats["rejected"] += 1
+                    else:
+                        stats["kept"] += int(w_kept.sum())
+                        stats["reprieved"] += int((~w_kept).sum())
+    assert all(v > 0 for v in stats.values()), stats
+
+
+@pytest.mark.gpu
+def test_device_select_victims_10k_nodes():
+    """One launch over every node of a 10k-node Fit + LoadAware cluster with each node's pods as its potential
+    victims (the §8 scale: DryRunPreemption over all candidates), against the oracle on a sample of 400 candidates."""
+    cluster = synth.make_cluster(10000, seed=4242)
+    rng = np.random.default_rng(4243)
+    cfg = F.build_config()
+    pod = F.make_pod(requests={"cpu": "24", "memory": "48Gi"})
+    st = oracle.states(cluster.n)
+    oracle.add_pods(cfg, st, cluster.existing_pods, cluster.existing_node)
+    order = np.argsort(cluster.existing_node, kind="stable")
+    bounds = np.searchsorted(cluster.existing_node[order], np.arange(cluster.n + 1))
+    nodes = np.arange(cluster.n, dtype=np.int32)
+    vics = [cluster.existing_pods[order[bounds[i]:bounds[i + 1]]] for i in range(cluster.n)]
+    with Engine(cfg, cluster.n) as e:
+        synth.load_into(e, cluster)
+        rej, kept, nvio = e.select_victims(pod, nodes, vics)
+    sample = rng.choice(cluster.n, 400, replace=False)
+    for i in sample:
+        w_rej, w_kept, w_nv = oracle.select_victims(cfg, cluster.nodes[i], cluster.metrics[i], st[i:i + 1], None, pod,
+                                                    vics[i], None, None, cluster.now_ns)
+        assert (rej[i], kept[i].tolist(), nvio[i]) == (w_rej, w_kept.tolist(), w_nv), i
+    assert (rej == 0).sum() > 100 and sum(int(k.sum()) for k in kept) > 0
