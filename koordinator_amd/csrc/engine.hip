@@ -5851,9 +5851,8 @@ int kg_pods_stage(kg_engine* e, const kg_pod* pods, int64_t n) {
       if (hr[k].flags & RP_SEL) hr[k].aux = (int32_t)k;
       ext |= (hr[k].flags & (RP_RESERVE | RP_OPERATING | RP_SEL)) != 0;
       rtop = std::max<int64_t>(rtop, rsv_pred_top(hr[k], hs[k]));
-      if ((pods[k].flags & KG_POD_RESERVE) && (e->numa_on || e->ds_on))
-        return fail(KG_E_UNSUPPORTED, "pod %lld: scheduling a reserve pod with NodeNUMAResource / DeviceShare in the "
-                    "profile (their reserve-pod paths keep the Go plugins)", (long long)k);
+      // (r5) reserve pods in NodeNUMAResource / DeviceShare profiles: matched to no reservation and never nominated,
+      // they take both plugins' plain paths (nodenumaresource/plugin.go:515, deviceshare/reservation.go:301, :342)
     }
     e->sq_rsv_top = rtop;
     e->rsv_ext_q = ext;

@@ -362,14 +362,16 @@ int64_t or_fit_score(const kg_config* cfg, const kg_node* node, const or_node_st
   return node_score / weight_sum;
 }
 
-/* upstream NodeInfo.AddPod/RemovePod + LoadAware Reserve/Unreserve → podAssignCache.assign/unAssign
- * (load_aware.go:260-267, pod_assign_cache.go:53-80) with the estimate taken at Score time (:359). */
-void or_apply_pod(const kg_config* cfg, or_node_state* st, const kg_pod* pod, int sign) {
+/* upstream NodeInfo.AddPod/RemovePod + podAssignCache.assign/unAssign (pod_assign_cache.go:53-80) with the estimate
+ * taken at Score time (load_aware.go:359).  informer = 1: the pod informer's add / delete (OnAdd / OnDelete), which a
+ * reserve pod never reaches (a Reservation is not a Pod object); 0: LoadAware Reserve / Unreserve
+ * (load_aware.go:260-267), which assign / unAssign every scheduled pod, a reserve pod included. */
+static void apply_pod(const kg_config* cfg, or_node_state* st, const kg_pod* pod, int sign, int informer) {
   for (int r = 0; r < KG_RES_MAX; r++) st->requested[r] += sign * pod->requests[r];
   st->nonzero[0] += sign * pod->nonzero_requests[0];
   st->nonzero[1] += sign * pod->nonzero_requests[1];
   st->num_pods += sign;
-  if (pod->flags & KG_POD_RESERVE) return; /* reserve pods never reach podAssignCache (pod informer only) */
+  if (informer && (pod->flags & KG_POD_RESERVE)) return;
   int64_t est[2];
   or_estimate_pod(cfg, pod, est);
   for (int r = 0; r < 2; r++) {
@@ -377,6 +379,9 @@ void or_apply_pod(const kg_config* cfg, or_node_state* st, const kg_pod* pod, in
     if (pod->priority_class == KG_PRIO_PROD) st->la_est_prod[r] += sign * est[r];
   }
 }
+
+void or_apply_pod(const kg_config* cfg, or_node_state* st, const kg_pod* pod, int sign) { apply_pod(cfg, st, pod, sign, 1); }
+void or_assume_pod(const kg_config* cfg, or_node_state* st, const kg_pod* pod, int sign) { apply_pod(cfg, st, pod, sign, 0); }
 
 void or_states_init(int64_t n_nodes, or_node_state* st) { memset(st, 0, sizeof(*st) * (size_t)n_nodes); }
 
@@ -562,7 +567,7 @@ int or_unreserve(const kg_config* cfg, or_node_state* st, void* numa_states, kg_
                  const uint64_t* cpus, const int64_t* numa_alloc, int32_t minors, int32_t slot) {
   if (node < 0) return 0;
   if (pod->quota_id > n_quotas) return KG_E_INVALID;
-  or_apply_pod(cfg, &st[node], pod, -1); /* NodeInfo.RemovePod + podAssignCache.unAssign */
+  or_assume_pod(cfg, &st[node], pod, -1); /* NodeInfo.RemovePod + LoadAware Unreserve (unAssign) */
   if (numa_states && (cfg->numa_filter || cfg->numa_score) && cpus && numa_alloc) {
     or_cpuset cs;
     for (int w = 0; w < OR_CPUSET_WORDS; w++) cs.w[w] = cpus[w];
@@ -691,7 +696,7 @@ int or_schedule_full(const kg_config* cfg, int64_t n_nodes, const kg_node* nodes
       for (int w = 0; w < OR_CPUSET_WORDS; w++) out_cpus[p * OR_CPUSET_WORDS + w] = cpus.w[w];
     out_node[p] = (int32_t)best;
     out_score[p] = best >= 0 ? best_score : 0;
-    if (best >= 0) or_apply_pod(cfg, &st[best], &pods[p], +1); /* assume + Reserve */
+    if (best >= 0) or_assume_pod(cfg, &st[best], &pods[p], +1); /* assume + Reserve */
     if (best >= 0 && quota) or_quota_charge(quota, &pods[p]);
   }
   if (n_threads > 1) {

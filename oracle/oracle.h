@@ -66,6 +66,8 @@ int64_t or_least_requested_score(int64_t requested, int64_t capacity);
 
 /* Assume/AddPod + podAssignCache.assign for one pod onto one node state. sign=+1 add, -1 remove. */
 void or_apply_pod(const kg_config* cfg, or_node_state* st, const kg_pod* pod, int sign);
+/* the same at Reserve / Unreserve: LoadAware assigns every scheduled pod, a reserve pod included */
+void or_assume_pod(const kg_config* cfg, or_node_state* st, const kg_pod* pod, int sign);
 
 /* Sequential FIFO scheduling of `n_pods` over `n_nodes` (percentageOfNodesToScore=100, ties → lowest index).
  * `st` is updated in place (assume).  n_threads>1 splits every per-pod Filter and Score pass over threads

@@ -598,7 +598,7 @@ int or_schedule_resv_full(const kg_config* cfg, int64_t n_nodes, const kg_node* 
     out_score[p] = win >= 0 ? win_total : 0;
     if (out_minors) out_minors[p] = minors;
     if (win >= 0) {
-      or_apply_pod(cfg, &st[win], pod, 1);
+      or_assume_pod(cfg, &st[win], pod, 1); /* assume + LoadAware Reserve (a reserve pod too) */
       if (rsv_on && nom[win] >= 0) {
         /* Reserve → reservationCache.assumePod → AddAssignedPod (reservation_info.go:317-326) */
         kg_node_reservations* r = &rsv[win];

@@ -228,3 +228,46 @@ def test_evaluate_reservation_matches_oracle_loop_first_pod():
     total = ev["base"] + (5000 * (100 * raw // mx) if mx > 0 else 0) + (100 * ev["ds_raw"] // mds if mds > 0 else 0)
     total = np.where(feas, total, -1)
     assert int(np.argmax(total)) == w["node"][0] and int(total.max()) == w["score"][0]
+
+
+def reserve_pod_workload(n_nodes, n_pods, seed):
+    """(r5) the shipped world with 10 % reserve pods (random allocate policy, a third pinned to a node; no quota) and
+    5 % reservation operating-mode pods.  A reserve pod matches no reservation (transformer.go:112), is never
+    nominated, and takes NodeNUMAResource's and DeviceShare's own paths like any pod
+    (nodenumaresource/plugin.go:515 getReservationReservedCPUs → none; deviceshare/reservation.go:301, :342 → none):
+    its cpuset and minors come from the node's free CPUs / GPUs, and the unmatched reservations' held GPUs stay held."""
+    cluster, numa, dev, rsv, pods, quotas = workload(n_nodes, n_pods, seed)
+    rng = np.random.default_rng(seed + 7)
+    res = rng.random(n_pods) < 0.10
+    pods["flags"] = np.where(res, pods["flags"] | abi.POD_RESERVE, pods["flags"])
+    pods["reserve_allocate_policy"] = np.where(res, rng.integers(0, 3, n_pods), 0)
+    pin = res & (rng.random(n_pods) < 1 / 3)
+    pods["reserve_node"] = np.where(pin, rng.integers(0, n_nodes, n_pods) + 1, 0)
+    pods["quota_id"] = np.where(res, 0, pods["quota_id"])
+    op = ~res & (rng.random(n_pods) < 0.05)
+    pods["reservation_flags"] = np.where(op, pods["reservation_flags"] | abi.POD_RSV_OPERATING,
+                                         pods["reservation_flags"])
+    return cluster, numa, dev, rsv, pods, quotas, res
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n_nodes,n_pods,seed,chunks", [(600, 900, 171, 2), (80, 600, 172, 1)])
+def test_shipped_profile_reserve_pods(n_nodes, n_pods, seed, chunks):
+    """(r5) Scheduling Reservations under the shipped profile: device vs oracle bit-exact with reserve pods in the
+    queue (placement, totals, slots, cpusets, minors and every state table, as check() compares)."""
+    cluster, numa, dev, rsv, pods, quotas, res = reserve_pod_workload(n_nodes, n_pods, seed)
+    g, _ = check(config(), cluster, numa, dev, rsv, pods, quotas, chunks)
+    placed = g["node"] >= 0
+    assert (placed & res).any() and (g["slot"][res] == -1).all()
+    assert (g["cpus"][res & placed].any(axis=1)).any() or (g["minors"][res & placed] != 0).any()
+
+
+def test_oracle_shipped_reserve_pods():
+    """The oracle side of the same queue: reserve pods are placed, never assumed into a slot, pinned ones land on
+    their node, and some take a cpuset or GPUs."""
+    cluster, numa, dev, rsv, pods, quotas, res = reserve_pod_workload(300, 600, 173)
+    w = oracle_run(config(), cluster, numa, dev, rsv, pods, quotas)
+    node, slot = w["node"], w["slot"]
+    assert (node[res] >= 0).any() and (slot[res] == -1).all()
+    pinned = res & (pods["reserve_node"] > 0) & (node >= 0)
+    assert (node[pinned] == pods["reserve_node"][pinned] - 1).all()
