@@ -1241,7 +1241,11 @@ __global__ __launch_bounds__(kWave) void resolve_round(DevTable T0, const DevPod
     const uint32_t word_n = bitmap[key_n ? key_node(key_n) >> 5 : 0u];
     const uint64_t ub_n = s_cand[(size_t)j1 * kCandStride + kC];
     const uint64_t key_nn = s_cand[(size_t)j2 * kCandStride + lane];
-    const DevPod p = s_pods[j];  // (r4) from the LDS copy: a scalar load on the chain made every LDS wait wait for it
+    // (r4) the pod from the LDS copy: a scalar load on the chain made every LDS wait wait for it.  (r5) Read only where
+    // it is used — the slow path (and the assume that follows it) or the quota check: on the fast path (the listed
+    // winner is unmodified) its 96-byte load and the wait for it sat in front of the ballot of every pod.
+    DevPod p;
+    if (QUOTA) p = s_pods[j];
     const uint32_t node = key_node(key);  // key 0 → node 0xFFFFFFFF: masked below
     const bool unmod = (key != 0) & !((word >> (node & 31)) & 1u) & (node != last_w);
     bool placed = false;
@@ -1254,6 +1258,7 @@ __global__ __launch_bounds__(kWave) void resolve_round(DevTable T0, const DevPod
       KG_POD_SUB(j, 0);
       bool from_mod = false;
       if (nM > 0 && pos > 0) {  // a modified node is listed above e: re-score the modified rows exactly
+        if (!QUOTA) p = s_pods[j];
         ++n_slow;
         diag |= 1;
         const bool aux = (PF & PF_FIT_FILTER) && (p.flags & P_AUX);  // ephemeral-storage / scalar requests
