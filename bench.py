@@ -531,8 +531,11 @@ def main():
             "data": "synthetic (SURVEY §8d generator, seed %d)" % work.seed,
             "config": {"workload": desc, "nodes": cluster.n, "pods": total, "batch_pods": args.batch,
                        "pods_per_wave": args.pods_per_wave, "pipeline_depth": args.depth or "default",
-                       "parallelism": (("replicas x%d (exact profile: every rank evaluates its full replica, no "
-                                        "exchange)" % d.world) if rsv_path else
+                       "parallelism": (("replicas x%d (per-pod exact pass: every rank evaluates its full replica, "
+                                        "no exchange)" % d.world) if wl in ("stock", "stockz") else
+                                       ("node-sharded exact rounds x%d (replicated table; per round an RCCL "
+                                        "all-gather of the pod statistics and of the merged records)" % d.world)
+                                       if rsv_path else
                                        "node-sharded x%d (replicated table, RCCL all-gather)" % d.world)},
             "node_evals_per_sec": pods_s * cluster.n,
             "placed": placed,

@@ -185,6 +185,17 @@ def test_c4_pipelined_parity(batch, depth):
     assert (cpus != 0).any()
 
 
+def test_c4_full_size_parity():
+    """(r5) C4 at its bench size on the device: 10k two-socket 256-cpu nodes, the bench geometry
+    (16 pods per round, depth 2), 3,000 queued pods — placements, totals, cpusets, the NodeAllocation state and the
+    node table all equal the oracle's (the bench line checks the first 2k placements only)."""
+    cfg = F.build_config(profile=FULL_PROFILE, batch_pods=16, pods_per_wave=1, pipeline_depth=2)
+    cluster, numa = synth.make_numa_cluster(10_000, seed=synth.BASE_SEED + 242)
+    pods = synth.make_numa_pods(3000, seed=synth.BASE_SEED + 243)
+    node, cpus = _numa_parity(cfg, cluster, numa, pods)
+    assert (node >= 0).mean() > 0.9 and (cpus != 0).any(axis=1).sum() > 1000
+
+
 @pytest.mark.parametrize("variant", ["score_only", "most_allocated", "numa_only_spread_default"])
 def test_c4_profile_variants(variant):
     if variant == "score_only":
