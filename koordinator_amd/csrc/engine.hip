@@ -51,6 +51,11 @@ constexpr int kENPT = KG_EVAL_NPT;
 constexpr int kETile = kWave * kENPT;
 constexpr int kEW = KG_EVAL_EW;
 constexpr int kR = 8;                 // candidates kept per (pod, tile)
+#ifndef KG_GROUP_KEYS
+#define KG_GROUP_KEYS 8
+#endif
+constexpr int kRG = KG_GROUP_KEYS;    // (r5) candidates kept per (pod, tile group of kEW tiles): the merge's input
+static_assert(kRG % 2 == 0 && kRG <= kR, "group lists: an even count of at most kR keys");
 constexpr int kEvalWaves = 4;         // waves (tiles) per eval block
 constexpr int kMaxB = 64;             // modified rows are held one per lane of the resolver wave
 constexpr int kC = 64;                // merged candidates per pod (> any modified-set size: kC > kMaxB - 1)
@@ -292,7 +297,7 @@ __device__ __forceinline__ void eval_tile(const DevTable& T, const DevPod* __res
   }
 }
 
-template <int L>
+template <int L, int LL>
 __device__ __forceinline__ void merge_pod(const DevTable& T, const EvalParams& P, const uint64_t* __restrict__ base,
                                           int n_lists, uint64_t* sel, uint64_t* __restrict__ o, int lane);
 
@@ -302,6 +307,7 @@ __device__ __forceinline__ void merge_pod(const DevTable& T, const EvalParams& P
 // does), then resets the ticket for the slot's next round (stream order: that round's kernel starts after this one
 // ends).  n_lists ≤ 2·kWave (the caller's condition).  A round poisoned mid-launch can leave a partial count: the
 // batch is abandoned then, and every batch starts from zeroed tickets.
+template <int LL>
 __device__ __forceinline__ void merge_tail(const DevTable& T, const EvalParams& P, const uint64_t* __restrict__ lists,
                                            int n_lists, int p0, int p1, int ppw, int n_tg, uint32_t* __restrict__ tickets,
                                            uint64_t* __restrict__ records, uint64_t* s_lds) {
@@ -324,13 +330,13 @@ __device__ __forceinline__ void merge_tail(const DevTable& T, const EvalParams& 
   }
   __syncthreads();
   if (!s_last) return;
-  const int64_t pstride = (int64_t)n_lists * kR;
+  const int64_t pstride = (int64_t)n_lists * LL;
   uint64_t* sel = s_lds + (size_t)wave * kC;  // the block's list staging is free again: kEW·kC words (host-sized)
   for (int pl = wave; pl < p1 - p0; pl += kEW) {
     const uint64_t* base = lists + (size_t)(p0 + pl) * pstride;
     uint64_t* o = records + (size_t)(p0 + pl) * kCandStride;
-    if (n_lists <= kWave) merge_pod<1>(T, P, base, n_lists, sel, o, lane);
-    else merge_pod<2>(T, P, base, n_lists, sel, o, lane);
+    if (n_lists <= kWave) merge_pod<1, LL>(T, P, base, n_lists, sel, o, lane);
+    else merge_pod<2, LL>(T, P, base, n_lists, sel, o, lane);
   }
 }
 
@@ -376,7 +382,7 @@ __global__ __launch_bounds__(kWave* kEW) KG_EVAL_ATTR void eval_round(DevTable T
     if (tile < nt_local)
       eval_tile<PF, kENPT>(T, pods, first, p0, p1, tile, node_base, n_local, P, lists + ((size_t)p0 * nt_local + tile) * kR,
                     (int64_t)nt_local * kR, vbits, paux, lane);
-    if (tickets) merge_tail(T, P, lists, nt_local, p0, p1, pods_per_wave, ng_local, tickets, records, s_lists);
+    if (tickets) merge_tail<kR>(T, P, lists, nt_local, p0, p1, pods_per_wave, ng_local, tickets, records, s_lists);
     return;
   }
   uint64_t* my_l = s_lists + (size_t)wave * pods_per_wave * kR;
@@ -401,11 +407,11 @@ __global__ __launch_bounds__(kWave* kEW) KG_EVAL_ATTR void eval_round(DevTable T
       }
     }
     const int nnz = __popcll(__ballot(key != 0));
-    uint64_t* out = lists + ((size_t)(p0 + pl) * ng_local + grp) * kR;
-    if (key != 0 && rank < kR) out[rank] = key;
-    if (lane >= nnz && lane < kR) out[lane] = 0;
+    uint64_t* out = lists + ((size_t)(p0 + pl) * ng_local + grp) * kRG;  // the kRG best (a full list still bounds)
+    if (key != 0 && rank < kRG) out[rank] = key;
+    if (lane >= nnz && lane < kRG) out[lane] = 0;
   }
-  if (tickets) merge_tail(T, P, lists, ng_local, p0, p1, pods_per_wave, ng_local, tickets, records, s_lists);
+  if (tickets) merge_tail<kRG>(T, P, lists, ng_local, p0, p1, pods_per_wave, ng_local, tickets, records, s_lists);
   KG_STAMP(0, 31);
 }
 
@@ -712,36 +718,36 @@ __device__ __forceinline__ uint32_t wave_excl_prefix_u32(uint32_t v) { return wa
 // popcounts (no DPP sums); the rank sort reads the zero-padded selection with all its broadcast loads in flight.
 __device__ __forceinline__ uint32_t ballot_count(bool c) { return (uint32_t)__popcll(__ballot(c)); }
 
-template <int L>
+template <int L, int LL>
 __device__ __forceinline__ void merge_pod(const DevTable& T, const EvalParams& P, const uint64_t* __restrict__ base,
                                           int n_lists, uint64_t* sel, uint64_t* __restrict__ o, int lane) {
-  uint64_t k[L][kR];
+  uint64_t k[L][LL];
   uint64_t ub_in = 0;
 #pragma unroll
   for (int i = 0; i < L; ++i) {
     const int l = lane + kWave * i;
     if (l < n_lists) {
-      const ulonglong2* src = reinterpret_cast<const ulonglong2*>(base + (size_t)l * kR);
+      const ulonglong2* src = reinterpret_cast<const ulonglong2*>(base + (size_t)l * LL);
 #pragma unroll
-      for (int r = 0; r < kR / 2; ++r) {
+      for (int r = 0; r < LL / 2; ++r) {
         const ulonglong2 v = src[r];
         k[i][2 * r] = v.x;
         k[i][2 * r + 1] = v.y;
       }
     } else {
 #pragma unroll
-      for (int r = 0; r < kR; ++r) k[i][r] = 0;
+      for (int r = 0; r < LL; ++r) k[i][r] = 0;
     }
-    // a full list (kR keys: a tile list in node order, or a sorted tile-group list) bounds its unseen nodes by its
+    // a full list (LL keys: a tile list in node order, or a sorted tile-group list) bounds its unseen nodes by its
     // minimum
     uint64_t mn = ~0ull;
     int cnt = 0;
 #pragma unroll
-    for (int r = 0; r < kR; ++r) {
+    for (int r = 0; r < LL; ++r) {
       cnt += k[i][r] != 0;
       mn = k[i][r] != 0 && k[i][r] < mn ? k[i][r] : mn;
     }
-    if (cnt == kR) ub_in = mn > ub_in ? mn : ub_in;
+    if (cnt == LL) ub_in = mn > ub_in ? mn : ub_in;
   }
   ub_in = wave_max_key(ub_in);
   KG_STAMP(1, 1);
@@ -755,7 +761,7 @@ __device__ __forceinline__ void merge_pod(const DevTable& T, const EvalParams& P
 #pragma unroll
       for (int i = 0; i < L; ++i)
 #pragma unroll
-        for (int r = 0; r < kR; ++r) {
+        for (int r = 0; r < LL; ++r) {
           if (q == 0 && k[i][r] < ub_in) k[i][r] = 0;
           m = k[i][r] < bound && k[i][r] > m ? k[i][r] : m;
         }
@@ -767,12 +773,12 @@ __device__ __forceinline__ void merge_pod(const DevTable& T, const EvalParams& P
   const bool stage = lane < kStaged && my_top != 0 && key_node(my_top) < (uint32_t)T.cap;
   Row srow;
   if (stage) srow = load_row(T, key_node(my_top));  // consumed at the end: its latency overlaps the selection
-  uint32_t sc[L][kR];  // score + 1 of a live key, 0 for a dropped one
+  uint32_t sc[L][LL];  // score + 1 of a live key, 0 for a dropped one
   uint32_t c = 0;
 #pragma unroll
   for (int i = 0; i < L; ++i)
 #pragma unroll
-    for (int r = 0; r < kR; ++r) {
+    for (int r = 0; r < LL; ++r) {
       sc[i][r] = k[i][r] ? (uint32_t)(k[i][r] >> 32) + 1u : 0u;
       c += k[i][r] != 0;
     }
@@ -789,7 +795,7 @@ __device__ __forceinline__ void merge_pod(const DevTable& T, const EvalParams& P
 #pragma unroll
       for (int i = 0; i < L; ++i)
 #pragma unroll
-        for (int r = 0; r < kR; ++r) n += ballot_count(sc[i][r] >= mid);
+        for (int r = 0; r < LL; ++r) n += ballot_count(sc[i][r] >= mid);
       if (n >= (uint32_t)kC) lo = mid;
       else hi = mid;
     }
@@ -798,7 +804,7 @@ __device__ __forceinline__ void merge_pod(const DevTable& T, const EvalParams& P
 #pragma unroll
     for (int i = 0; i < L; ++i)
 #pragma unroll
-      for (int r = 0; r < kR; ++r) a += ballot_count(sc[i][r] > tau);
+      for (int r = 0; r < LL; ++r) a += ballot_count(sc[i][r] > tau);
     need = (uint32_t)kC - a;
   }
   KG_STAMP(1, 2);
@@ -811,13 +817,13 @@ __device__ __forceinline__ void merge_pod(const DevTable& T, const EvalParams& P
     uint32_t ties = 0;
     if (!all) {
 #pragma unroll
-      for (int r = 0; r < kR; ++r) ties += sc[i][r] == tau;
+      for (int r = 0; r < LL; ++r) ties += sc[i][r] == tau;
     }
     uint32_t tr = tie_base + wave_excl_prefix_u32(ties);
     tie_base += wave_sum_u32(ties);
     uint32_t m = 0;
 #pragma unroll
-    for (int r = 0; r < kR; ++r) {
+    for (int r = 0; r < LL; ++r) {
       const uint64_t v = k[i][r];
       const bool tie = !all && sc[i][r] == tau;
       const bool sl = sc[i][r] != 0 && (all || sc[i][r] > tau || (tie && tr < need));
@@ -834,7 +840,7 @@ __device__ __forceinline__ void merge_pod(const DevTable& T, const EvalParams& P
 #pragma unroll
   for (int i = 0; i < L; ++i)
 #pragma unroll
-    for (int r = 0; r < kR; ++r)
+    for (int r = 0; r < LL; ++r)
       if ((selm[i] >> r) & 1u) sel[off++] = k[i][r];
   if (lane >= (int)n_sel) sel[lane] = 0;  // zero padding: the rank sort reads all kC slots
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -866,7 +872,7 @@ __device__ __forceinline__ void merge_pod(const DevTable& T, const EvalParams& P
   KG_STAMP(1, 14);
 }
 
-template <int L>
+template <int L, int LL>
 __global__ __launch_bounds__(kWave * 4) void merge_wave(DevTable T, EvalParams P, const uint64_t* __restrict__ in,
                                                         int64_t pod_stride, int n_lists, int nb,
                                                         const int32_t* __restrict__ poison,
@@ -876,7 +882,7 @@ __global__ __launch_bounds__(kWave * 4) void merge_wave(DevTable T, EvalParams P
   const int pod = blockIdx.x * 4 + wave;
   if (*poison || pod >= nb) return;  // no block barrier below: a wave may leave alone
   KG_STAMP(1, 0);
-  merge_pod<L>(T, P, in + (size_t)pod * pod_stride, n_lists, s_sel[wave], out + (size_t)pod * kCandStride, lane);
+  merge_pod<L, LL>(T, P, in + (size_t)pod * pod_stride, n_lists, s_sel[wave], out + (size_t)pod * kCandStride, lane);
 }
 
 // ---- round kernel 3: FIFO resolve (one wavefront, modified rows in registers) ---------------------------
@@ -4358,20 +4364,30 @@ bool merge_block() {
 void launch_merge_local(kg_engine* e, const RoundGeom& g, int nb, int slot, hipStream_t st) {
   uint64_t* dst = e->n_ranks > 1 ? gathered_slot(e, g, slot) + (size_t)e->rank * g.B * kCandStride : cand_slot(e, g, slot);
   const int nl = eval_lists(e, g);
+  // eval_round's tile-group lists hold kRG keys, its tile lists (a shard of fewer than kCombineTiles tiles) and the
+  // NUMA / DeviceShare passes' lists kR
+  const bool grp = !e->numa_on && !e->ds_on && eval_combine(g);
+  const int ll = grp ? kRG : kR;
   if (!e->numa_on && !e->ds_on && !merge_block()) {  // (r4) one wavefront per pod
     const unsigned blocks = (unsigned)((nb + 3) / 4);
-    const int64_t ps = (int64_t)nl * kR;
-    if (nl <= kWave)
-      merge_wave<1><<<blocks, kWave * 4, 0, st>>>(e->T, e->P, lists_slot(e, g, slot), ps, nl, nb, poison_ptr(e), dst);
-    else if (nl <= 2 * kWave)
-      merge_wave<2><<<blocks, kWave * 4, 0, st>>>(e->T, e->P, lists_slot(e, g, slot), ps, nl, nb, poison_ptr(e), dst);
-    else if (nl <= 4 * kWave)
-      merge_wave<4><<<blocks, kWave * 4, 0, st>>>(e->T, e->P, lists_slot(e, g, slot), ps, nl, nb, poison_ptr(e), dst);
-    else
-      merge_wave<8><<<blocks, kWave * 4, 0, st>>>(e->T, e->P, lists_slot(e, g, slot), ps, nl, nb, poison_ptr(e), dst);
+    const int64_t ps = (int64_t)nl * ll;
+#define KG_MW(LW, LLV) \
+  merge_wave<LW, LLV><<<blocks, kWave * 4, 0, st>>>(e->T, e->P, lists_slot(e, g, slot), ps, nl, nb, poison_ptr(e), dst)
+#define KG_MW_L(LLV)                    \
+  if (nl <= kWave) KG_MW(1, LLV);       \
+  else if (nl <= 2 * kWave) KG_MW(2, LLV); \
+  else if (nl <= 4 * kWave) KG_MW(4, LLV); \
+  else KG_MW(8, LLV);
+    if (grp) {
+      KG_MW_L(kRG)
+    } else {
+      KG_MW_L(kR)
+    }
+#undef KG_MW_L
+#undef KG_MW
     return;
   }
-  merge_round<false><<<nb, kMergeThreads, 0, st>>>(e->T, e->P, lists_slot(e, g, slot), (int64_t)nl * kR, kR, nl, kR,
+  merge_round<false><<<nb, kMergeThreads, 0, st>>>(e->T, e->P, lists_slot(e, g, slot), (int64_t)nl * ll, ll, nl, ll,
                                                    nb, poison_ptr(e), dst);
 }
 
