@@ -340,6 +340,11 @@ __device__ __forceinline__ void merge_tail(const DevTable& T, const EvalParams& 
   }
 }
 
+// (r5) the fused merge tail (KG_FUSE=1 at run time) is compiled into eval_round only with -DKG_FUSE_TAIL=1: measured
+// slower (fused_merge below), and its merge code raised the wide pass's scalar-register pressure
+#ifndef KG_FUSE_TAIL
+#define KG_FUSE_TAIL 0
+#endif
 // 4 waves per SIMD for the 2-node shape: all of the C3 grid (3,136 waves) resident at once (KG_EVAL_WPE=0: the
 // compiler's choice, 130 VGPRs and 3 waves per SIMD)
 #ifndef KG_EVAL_WPE
@@ -382,7 +387,9 @@ __global__ __launch_bounds__(kWave* kEW) KG_EVAL_ATTR void eval_round(DevTable T
     if (tile < nt_local)
       eval_tile<PF, kENPT>(T, pods, first, p0, p1, tile, node_base, n_local, P, lists + ((size_t)p0 * nt_local + tile) * kR,
                     (int64_t)nt_local * kR, vbits, paux, lane);
+#if KG_FUSE_TAIL
     if (tickets) merge_tail<kR>(T, P, lists, nt_local, p0, p1, pods_per_wave, ng_local, tickets, records, s_lists);
+#endif
     return;
   }
   uint64_t* my_l = s_lists + (size_t)wave * pods_per_wave * kR;
@@ -411,7 +418,9 @@ __global__ __launch_bounds__(kWave* kEW) KG_EVAL_ATTR void eval_round(DevTable T
     if (key != 0 && rank < kRG) out[rank] = key;
     if (lane >= nnz && lane < kRG) out[lane] = 0;
   }
+#if KG_FUSE_TAIL
   if (tickets) merge_tail<kRG>(T, P, lists, ng_local, p0, p1, pods_per_wave, ng_local, tickets, records, s_lists);
+#endif
   KG_STAMP(0, 31);
 }
 
@@ -4318,7 +4327,7 @@ bool merge_block();
 // longer than the two launches (40.8 vs 28.0 + 10.2 µs, profiles/r05/timeline_*.txt) — the boundary it removes costs
 // ~0.9 µs (scripts/micro/handoff.hip) and every block pays a release before its ticket.
 bool fused_merge(kg_engine* e, const RoundGeom& g) {
-  static const bool on = std::getenv("KG_FUSE") && std::string(std::getenv("KG_FUSE")) == "1";
+  static const bool on = KG_FUSE_TAIL && std::getenv("KG_FUSE") && std::string(std::getenv("KG_FUSE")) == "1";
   return on && e->n_ranks == 1 && !e->numa_on && !e->ds_on && !merge_block() && eval_lists(e, g) <= 2 * kWave;
 }
 uint32_t* tickets_slot(kg_engine* e, int slot) { return e->tickets.p + (size_t)slot * kMaxB; }
