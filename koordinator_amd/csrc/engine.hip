@@ -240,7 +240,7 @@ __device__ __forceinline__ void eval_tile_exact(const DevTable& T, const DevPod*
 }
 
 // one wave's tile for pods [p0, p1): its kR best packed keys per pod into out[(pi - p0) * kR ..]
-template <int PF, int NPT>
+template <int PF, int NPT, bool AUX>
 __device__ __forceinline__ void eval_tile(const DevTable& T, const DevPod* __restrict__ pods, int64_t first, int p0,
                                           int p1, int tile, int64_t node_base, int64_t n_local, const EvalParams& P,
                                           uint64_t* __restrict__ out, int64_t out_stride, int vbits,
@@ -285,7 +285,9 @@ __device__ __forceinline__ void eval_tile(const DevTable& T, const DevPod* __res
       uint32_t t = 0;
       v[j] = eval_hot<PF>(rows[j], p, P, t) ? t + 1u : 0u;
     }
-    if constexpr ((PF & PF_FIT_FILTER) != 0) {  // ephemeral-storage / scalar requests: the Allocatable-Requested columns
+    // ephemeral-storage / scalar requests: the Allocatable-Requested columns.  (r5) Compiled only into the AUX
+    // instantiation (a staged queue holding such a pod): the check cost the common kernel 20 VGPRs
+    if constexpr (AUX && (PF & PF_FIT_FILTER) != 0) {
       if (p.flags & P_AUX) {
         const int64_t* rq = paux + (size_t)(first + pi) * kAux;
 #pragma unroll
@@ -355,7 +357,7 @@ __device__ __forceinline__ void merge_tail(const DevTable& T, const EvalParams& 
 #else
 #define KG_EVAL_ATTR
 #endif
-template <int PF>
+template <int PF, bool AUX>
 __global__ __launch_bounds__(kWave* kEW) KG_EVAL_ATTR void eval_round(DevTable T, const DevPod* __restrict__ pods,
                                                                   int64_t first, int nb, int pods_per_wave,
                                                                   int64_t node_base, int64_t n_local, int nt_local,
@@ -385,7 +387,7 @@ __global__ __launch_bounds__(kWave* kEW) KG_EVAL_ATTR void eval_round(DevTable T
   const int ng_local = (nt_local + kEW - 1) / kEW, grp = tile0 / kEW;
   if (!combine) {
     if (tile < nt_local)
-      eval_tile<PF, kENPT>(T, pods, first, p0, p1, tile, node_base, n_local, P, lists + ((size_t)p0 * nt_local + tile) * kR,
+      eval_tile<PF, kENPT, AUX>(T, pods, first, p0, p1, tile, node_base, n_local, P, lists + ((size_t)p0 * nt_local + tile) * kR,
                     (int64_t)nt_local * kR, vbits, paux, lane);
 #if KG_FUSE_TAIL
     if (tickets) merge_tail<kR>(T, P, lists, nt_local, p0, p1, pods_per_wave, ng_local, tickets, records, s_lists);
@@ -393,7 +395,7 @@ __global__ __launch_bounds__(kWave* kEW) KG_EVAL_ATTR void eval_round(DevTable T
     return;
   }
   uint64_t* my_l = s_lists + (size_t)wave * pods_per_wave * kR;
-  if (tile < nt_local) eval_tile<PF, kENPT>(T, pods, first, p0, p1, tile, node_base, n_local, P, my_l, kR, vbits, paux, lane);
+  if (tile < nt_local) eval_tile<PF, kENPT, AUX>(T, pods, first, p0, p1, tile, node_base, n_local, P, my_l, kR, vbits, paux, lane);
   else
     for (int q = lane; q < (p1 - p0) * kR; q += kWave) my_l[q] = 0;
   __syncthreads();
@@ -3431,6 +3433,7 @@ struct kg_engine {
   std::vector<int16_t> rsv_pcnt;                // (ABI 12) per node: predicates its slots were compiled against (64: no slots)
   int64_t rsv_pcnt_min = 64, sq_rsv_top = 0;    // min over the nodes; the staged reservation affinities' top id + 1
   bool rsv_ext_q = false;                       // the queue holds reserve / operating-mode / selector pods: per-pod pass
+  bool aux_q = false;  // (r5) a staged pod requests ephemeral-storage / a scalar resource: eval_round<PF, true>
   bool rsv_pdirty = false;
   DevBuf<DefPod> defpods;       // [staged + kMaxB]
   DevBuf<uint32_t> rsv_val2;    // [cap] raw taint count << 24 | raw affinity sum (their Scores on)
@@ -4331,6 +4334,27 @@ bool fused_merge(kg_engine* e, const RoundGeom& g) {
   return on && e->n_ranks == 1 && !e->numa_on && !e->ds_on && !merge_block() && eval_lists(e, g) <= 2 * kWave;
 }
 uint32_t* tickets_slot(kg_engine* e, int slot) { return e->tickets.p + (size_t)slot * kMaxB; }
+// (r5) eval_round<PF, AUX>: the ephemeral-storage / scalar check only in the instantiation a queue with such a pod
+// runs (profiles with NodeResourcesFit's Filter)
+template <int X>
+void launch_eval_round(kg_engine* e, const RoundGeom& g, int64_t first, int nb, int slot, hipStream_t st, bool fuse) {
+  auto go = [&](auto kern) {
+    kern<<<eval_grid_e(g, nb), kWave * kEW, eval_lds_bytes(g), st>>>(e->T, e->pods.p, first, nb, g.ppw, g.base,
+                                                                    g.n_local, g.nte, e->P, lists_slot(e, g, slot),
+                                                                    poison_ptr(e), e->paux.p,
+                                                                    eval_combine(g) ? 1 : 0,
+                                                                    fuse ? tickets_slot(e, slot) : nullptr,
+                                                                    cand_slot(e, g, slot));
+  };
+  if constexpr ((X & PF_FIT_FILTER) != 0) {
+    if (e->aux_q) {
+      go(eval_round<X, true>);
+      return;
+    }
+  }
+  go(eval_round<X, false>);
+}
+
 void launch_eval(kg_engine* e, const RoundGeom& g, int64_t first, int nb, int slot, hipStream_t st, bool fuse = false) {
   if (e->numa_on) {  // one block per (tile, pod group)
     const dim3 grid((unsigned)(g.nt_local * ((nb + g.ppw - 1) / g.ppw)));
@@ -4339,14 +4363,7 @@ void launch_eval(kg_engine* e, const RoundGeom& g, int64_t first, int nb, int sl
                                                                       e->NP, lists_slot(e, g, slot), poison_ptr(e));
     return;
   }
-#define KG_EVAL(X)                                                                                        \
-  eval_round<X><<<eval_grid_e(g, nb), kWave * kEW, eval_lds_bytes(g), st>>>(e->T, e->pods.p, first, nb,       \
-                                                                                g.ppw, g.base,                   \
-                                                                 g.n_local, g.nte, e->P,                  \
-                                                                 lists_slot(e, g, slot), poison_ptr(e), e->paux.p, \
-                                                                 eval_combine(g) ? 1 : 0,                          \
-                                                                 fuse ? tickets_slot(e, slot) : nullptr,           \
-                                                                 cand_slot(e, g, slot))
+#define KG_EVAL(X) launch_eval_round<X>(e, g, first, nb, slot, st, fuse)
   KG_PF_SWITCH(profile_bits(e->P), KG_EVAL)
 #undef KG_EVAL
 }
@@ -5784,9 +5801,13 @@ int kg_pods_stage(kg_engine* e, const kg_pod* pods, int64_t n) {
                   (long long)pods[k].quota_id, e->nq);
   }
   std::vector<DevPod> h(std::max<int64_t>(n, 1));
-  for (int64_t k = 0; k < n; ++k)
+  bool aux_q = false;
+  for (int64_t k = 0; k < n; ++k) {
     if (int rc = decode_pod(e, pods[k], h[k])) return rc;
+    aux_q |= (h[k].flags & P_AUX) != 0;
+  }
   if (int rc = flush_placements(e)) return rc;  // before the staged queue is replaced
+  e->aux_q = aux_q;
   e->staged_info.resize((size_t)n);
   for (int64_t k = 0; k < n; ++k)
     e->staged_info[k] = kg_engine::AssignedPod{pods[k].uid, 0, {h[k].est_cpu, h[k].est_mem}, (h[k].flags & P_PROD) ? 1 : 0};
