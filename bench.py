@@ -49,7 +49,7 @@ B_NODE = 76.0          # SURVEY §8d b_node for Fit + LoadAware: bytes of node c
 WORKLOADS = {
     "c1": (500, 5_000, 32, 8, 5_000),
     "c2": (10_000, 10_000, 32, 8, 10_000),
-    "c3": (100_000, 100_000, 32, 8, 10_000),
+    "c3": (100_000, 100_000, 38, 8, 10_000),  # (r5) B = 38: the resolver and the eval→merge chain balance
     "c4": (10_000, 10_000, 16, 1, 2_000),
     "c5": (50_000, 10_000, 32, 4, 2_000),
     "c5ds": (50_000, 10_000, 32, 4, 2_000),
