@@ -1127,6 +1127,8 @@ __device__ __forceinline__ void mod_row_settle(ModRow& R, const uint64_t* s_cand
   }
 }
 
+constexpr int kBank1Probe = 8;  // modified keys above e matched against bank 1 before re-scoring it
+
 template <int PF, bool QUOTA>
 __global__ __launch_bounds__(kWave) void resolve_round(DevTable T0, const DevPod* __restrict__ pods,
                                                         int64_t* __restrict__ ctl, int64_t first, int nb,
@@ -1286,7 +1288,16 @@ __global__ __launch_bounds__(kWave) void resolve_round(DevTable T0, const DevPod
         if (lane == 0) KG_LANE_SUB(j, 1);
         if (aux && mk && !mod_aux_fits(table_at(T0), R0.node, rq, j, my_out, s_pods, paux + (size_t)first * kAux))
           mk = 0;
-        if (nM > kWave) {
+        // (r5) bank 1 only when one of its rows is listed above e: a modified row listed below e, or not listed, reads
+        // at most its listed key / ub (monotone profile), so it cannot beat e (≥ ub).  The ≤ kBank1Probe modified
+        // keys above e are matched against bank 1's nodes (past that, both banks as before).
+        bool need1 = nM > kWave;
+        if (need1 && pos <= kBank1Probe) {
+          uint64_t hit = 0;
+          for (int q = 0; q < pos; ++q) hit |= __ballot(R1.node == key_node(readlane_u64(key, q)));
+          need1 = hit != 0;
+        }
+        if (need1) {
           mod_row_settle<PF>(R1, s_cand, s_pods, T0, P);
           uint64_t k1 = mod_row_key<PF>(R1, p, P, s_par);
           if (aux && k1 && !mod_aux_fits(table_at(T0), R1.node, rq, j, my_out, s_pods, paux + (size_t)first * kAux))
