@@ -65,7 +65,7 @@ def same_on_every_rank(out, want_node, want_score, st):
         assert np.array_equal(state["num_pods"], st["num_pods"]), r
 
 
-@pytest.mark.parametrize("n_ranks,depth,batch", [(2, 1, 32), (2, 2, 32), (3, 2, 16), (4, 0, 32)])
+@pytest.mark.parametrize("n_ranks,depth,batch", [(2, 1, 32), (2, 2, 32), (3, 2, 16), (4, 0, 32), (2, 2, 38)])
 def test_fit_loadaware_ranks(n_ranks, depth, batch):
     cluster = synth.make_cluster(3000, seed=901 + n_ranks)
     pods = synth.make_pods(6000, seed=902 + depth)
