@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define KG_ABI_VERSION 14
+#define KG_ABI_VERSION 15
 
 /* ---- resource slots (fixed order) ------------------------------------------------------- */
 enum {
@@ -437,6 +437,16 @@ typedef struct kg_node_reservations {
   int64_t gpu_minors[KG_MAX_RSV_SLOTS];        /* bit m: minor m is in the reserve pod's allocation             */
   int64_t gpu_alloc[KG_MAX_RSV_SLOTS][KG_MAX_MINORS][3];
   int64_t gpu_allocated[KG_MAX_RSV_SLOTS][KG_MAX_MINORS][3];
+  /* (ABI 15) NodeNUMAResource: the cpuset each reservation holds.  cpus = resourceManager.GetAllocatedCPUSet(node,
+   * reservation UID), the reserve pod's allocation; cpus_assigned = the union of GetAllocatedCPUSet(node, pod.UID) over
+   * the reservation's AssignedPods.  RestoreReservation (nodenumaresource/reservation.go:76-113) gives a pod matching
+   * the reservation reservedCPUs = cpus − cpus_assigned, which getResourceOptions (plugin.go:482-505, 513-535) offers
+   * to the pod nominated into it as preferredCPUs / reusable NUMA cpu at Score and Reserve.  Both sets are in
+   * kg_node_numa.allocated_cpus already (the resource manager's allocatedCPUs); a cpu of cpus ∩ cpus_assigned has
+   * RefCount 2 there (node_allocation.go:76-103).  Reserve / Unreserve keep cpus_assigned current.  All zero: the
+   * reservation holds no cpuset. */
+  uint64_t cpus[KG_MAX_RSV_SLOTS][KG_MAX_CPUS / 64];
+  uint64_t cpus_assigned[KG_MAX_RSV_SLOTS][KG_MAX_CPUS / 64];
 } kg_node_reservations;
 
 /* One ElasticQuota as the plugin's PreFilter snapshot sees it (plugin.go:211-256) over KG_QUOTA_RES resources: cpu

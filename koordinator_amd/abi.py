@@ -36,7 +36,7 @@ POD_TAINT_TABLE = 64
 MAX_OWNER_GROUPS = 64
 QUOTA_RES = 8
 MAX_QUOTAS = 64
-ABI_VERSION = 14
+ABI_VERSION = 15
 MAX_RSV_SLOTS = 4
 RSV_POLICY = {"Default": 0, "Aligned": 1, "Restricted": 2}
 POD_RSV_AFFINITY, POD_RSV_OPERATING = 1, 2
@@ -172,7 +172,10 @@ NODE_RSV_DTYPE = np.dtype([_i64("n")] + [_i64(f, MAX_RSV_SLOTS) for f in (
                                                         # (ABI 13) GPUs held per reservation
                                                         _i64("gpu_minors", MAX_RSV_SLOTS),
                                                         _i64("gpu_alloc", (MAX_RSV_SLOTS, MAX_MINORS, 3)),
-                                                        _i64("gpu_allocated", (MAX_RSV_SLOTS, MAX_MINORS, 3))])
+                                                        _i64("gpu_allocated", (MAX_RSV_SLOTS, MAX_MINORS, 3)),
+                                                        # (ABI 15) cpusets held per reservation / its assigned pods'
+                                                        ("cpus", np.uint64, (MAX_RSV_SLOTS, MAX_CPUS // 64)),
+                                                        ("cpus_assigned", np.uint64, (MAX_RSV_SLOTS, MAX_CPUS // 64))])
 
 QUOTA_DTYPE = np.dtype([_i64("used", QUOTA_RES), _i64("non_preemptible_used", QUOTA_RES), _i64("used_limit", QUOTA_RES),
                         _i64("min", QUOTA_RES)])

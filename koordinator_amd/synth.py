@@ -115,6 +115,21 @@ def make_pods(n_pods: int, seed: int = BASE_SEED + 1) -> np.ndarray:
     return p
 
 
+POD_STREAM_CHUNK = 1 << 16
+
+
+def make_pods_stream(n_pods: int, seed: int = BASE_SEED + 1) -> np.ndarray:
+    """(r6) The `make_pods` distribution, prefix-stable: chunk k of 65,536 pods is `make_pods(65536)` seeded with
+    SeedSequence([seed, k]), so the first m pods are the same whatever `n_pods` is.  The C3 bench and the 1M-pod
+    parity test draw their queue here, which lets one committed oracle fixture (tests/golden/c3_queue.npz) cover any
+    prefix the bench times."""
+    k = -(-n_pods // POD_STREAM_CHUNK)
+    parts = [make_pods(POD_STREAM_CHUNK, seed=np.random.SeedSequence([seed, i])) for i in range(k)]
+    if not parts:
+        return np.zeros(0, dtype=abi.POD_DTYPE)
+    return np.concatenate(parts)[:n_pods]
+
+
 def load_into(engine, cluster: Cluster):
     """Informer-order ingest: nodes, NodeMetrics, then the already-assigned pods."""
     engine.upsert_nodes(cluster.nodes)

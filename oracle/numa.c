@@ -522,6 +522,28 @@ void or_numa_node_init(or_numa_node* n, const kg_node_numa* s) {
     n->excl_pcpu.w[i] = s->exclusive_pcpu_cpus[i] & s->allocated_cpus[i];
     n->excl_numa.w[i] = s->exclusive_numa_cpus[i] & s->allocated_cpus[i];
   }
+  for (int c = 0; c < KG_MAX_CPUS; c++) n->ref[c] = (uint8_t)cs_has(&n->allocated, c);
+  n->refs_ready = 0;
+}
+
+/* (r6) A cpu a reservation holds (GetAllocatedCPUSet(node, reservation UID)) that one of its assigned pods took from
+ * the reservation's reserved cpus was added twice (addPodAllocation, node_allocation.go:76-103): RefCount 2. */
+void or_numa_rsv_refs(or_numa_node* n, const kg_node_reservations* r) {
+  if (n->refs_ready || !r) return;
+  n->refs_ready = 1;
+  for (int s = 0; s < (int)r->n && s < KG_MAX_RSV_SLOTS; s++)
+    for (int c = 0; c < KG_MAX_CPUS; c++)
+      if (((r->cpus[s][c >> 6] >> (c & 63)) & 1u) && ((r->cpus_assigned[s][c >> 6] >> (c & 63)) & 1u) &&
+          n->ref[c] == 1)
+        n->ref[c] = 2;
+}
+
+/* (r6) RestoreReservation (nodenumaresource/reservation.go:76-113): the reservation's allocated cpus, minus each
+ * assigned pod's (allocatedCPUs.Difference(podCPUs) over rInfo.AssignedPods) */
+or_cpuset or_numa_rsv_reserved(const kg_node_reservations* r, int s) {
+  or_cpuset c;
+  for (int w = 0; w < OR_CPUSET_WORDS; w++) c.w[w] = r->cpus[s][w] & ~r->cpus_assigned[s][w];
+  return c;
 }
 
 /* AllowUseCPUSet (util.go:42-49) + PreFilter (plugin.go:220-270) */
@@ -529,13 +551,14 @@ void or_numa_pod_init(const kg_config* cfg, const kg_pod* pod, or_numa_pod* p) {
   memset(p, 0, sizeof(*p));
   p->req_cpu = pod->requests[KG_RES_CPU];
   p->req_mem = pod->requests[KG_RES_MEMORY];
+  const int allow = (pod->qos == KG_QOS_LSE || pod->qos == KG_QOS_LSR) && pod->priority_class == KG_PRIO_PROD;
+  p->allow_cpuset = allow; /* PreRestoreReservation (reservation.go:68-74) */
   int zero = 1;
   for (int r = 0; r < KG_RES_MAX; r++) zero &= pod->requests[r] == 0;
   if (zero) {
     p->skip = 1;
     return;
   }
-  const int allow = (pod->qos == KG_QOS_LSE || pod->qos == KG_QOS_LSR) && pod->priority_class == KG_PRIO_PROD;
   if (!allow) return;
   int bind = (int)pod->preferred_cpu_bind_policy;
   if (bind == KG_BIND_NONE || bind == KG_BIND_DEFAULT) bind = (int)cfg->numa_default_cpu_bind_policy;
@@ -580,6 +603,22 @@ static or_cpuset available_cpus(const or_numa_node* n) {
   return cs_andnot(cs_andnot(n->topo.all, n->allocated), n->reserved);
 }
 
+/* (r6) getAvailableCPUs (node_allocation.go:133-153) with preferredCPUs, maxRefCount 1: on a copy of the allocated
+ * CPUInfos every preferred cpu's RefCount drops by one (deleted at 0); the cpus still at RefCount ≥ maxRefCount are
+ * unavailable, and so are the kubelet-reserved ones.  *held = the copy's cpus (the allocateInfo CPUDetails). */
+static or_cpuset available_pref(const or_numa_node* n, const or_cpuset* pref, or_cpuset* held) {
+  or_cpuset h = cs_empty();
+  for (int c = 0; c < KG_MAX_CPUS; c++) {
+    int r = n->ref[c];
+    if (pref && r > 0 && cs_has(pref, c)) r--;
+    if (r >= 1) cs_add(&h, c);
+  }
+  if (held) *held = h;
+  return cs_andnot(cs_andnot(n->topo.all, h), n->reserved);
+}
+
+static int cs_nonempty(const or_cpuset* s) { return s && cs_size(s) > 0; }
+
 /* extension.Amplify (apis/extension/node_resource_amplification.go:170-175) */
 static int64_t amplify(int64_t origin, double ratio) {
   if (ratio <= 1) return origin;
@@ -605,10 +644,25 @@ static int64_t numa_allocated_cpu(const or_numa_node* n, int i) {
   return c;
 }
 
-/* getAvailableNUMANodeResources (node_allocation.go:155-177), no reusable resources (no reservations) */
-static void numa_available(const or_numa_node* n, int64_t avail_cpu[], int64_t avail_mem[]) {
+/* (r6) getResourceOptions' reusableResources (plugin.go:482-493): per NUMA node holding a preferred cpu (CPUDetails.
+ * KeepOnly), Amplify(its preferred cpus × 1000) of cpu; 0 elsewhere */
+static int64_t reusable_cpu(const or_numa_node* n, const or_cpuset* pref, int i) {
+  if (!cs_nonempty(pref)) return 0;
+  const or_cpuset in = cs_and(cs_and(*pref, n->topo.all), cpus_in_numa(&n->topo, i));
+  const int k = cs_size(&in);
+  return k > 0 ? amplify((int64_t)k * 1000, n->cpu_amp) : 0;
+}
+
+/* allocatedResources[i] cpu after SubtractWithNonNegativeResult(allocatedRes, reusableResources[i]) (:166) */
+static int64_t numa_allocated_cpu_pref(const or_numa_node* n, const or_cpuset* pref, int i) {
+  const int64_t ac = numa_allocated_cpu(n, i) - reusable_cpu(n, pref, i);
+  return ac > 0 ? ac : 0;
+}
+
+/* getAvailableNUMANodeResources (node_allocation.go:155-177); (r6) with the reusable cpu of preferred cpus */
+static void numa_available(const or_numa_node* n, const or_cpuset* pref, int64_t avail_cpu[], int64_t avail_mem[]) {
   for (int i = 0; i < n->num_numa; i++) {
-    const int64_t ac = numa_allocated_cpu(n, i);
+    const int64_t ac = n->numa_alloc_present[i] ? numa_allocated_cpu_pref(n, pref, i) : 0;
     const int64_t am = n->numa_alloc_present[i] ? n->numa_alloc_mem[i] : 0;
     avail_cpu[i] = n->numa_cpu[i] - ac > 0 ? n->numa_cpu[i] - ac : 0;
     avail_mem[i] = n->numa_mem[i] - am > 0 ? n->numa_mem[i] - am : 0;
@@ -669,7 +723,7 @@ static int numa_hints(const kg_config* cfg, const or_numa_node* n, const or_numa
   if (bind < 0) return -1; /* getResourceOptions error */
   if (n->num_numa == 0) return -1;
   int64_t avail_cpu[KG_MAX_NUMA], avail_mem[KG_MAX_NUMA];
-  numa_available(n, avail_cpu, avail_mem);
+  numa_available(n, NULL, avail_cpu, avail_mem);
   if (p->request_cpu_bind && p->required_policy != KG_BIND_NONE) trim_numa(n, bind, avail_cpu);
   const int req_c = p->req_cpu > 0, req_m = p->req_mem > 0; /* keys of PodRequestsAndLimits */
   int min_c = n->num_numa, min_m = n->num_numa;
@@ -862,17 +916,41 @@ static or_cpuset excl_seed(const or_numa_node* n, const or_numa_pod* p) {
   return cs_empty();
 }
 
+/* takePreferredCPUs (cpu_accumulator.go:33-85): the preferred cpus among the available ones first (as many as are
+ * needed, one takeCPUs over them), then the rest from the other available cpus */
+static int take_preferred(const or_topology* t, or_cpuset avail, const or_cpuset* pref, int needed, int bind,
+                          int strategy, int excl, or_cpuset seed, or_cpuset* out) {
+  or_cpuset result = cs_empty();
+  const or_cpuset pc = pref ? cs_and(avail, *pref) : cs_empty();
+  if (cs_size(&pc) > 0) {
+    const int k = needed < cs_size(&pc) ? needed : cs_size(&pc);
+    if (or_take_cpus_ex(t, pc, k, bind, strategy, excl, seed, &result) != 0) return -1;
+    needed -= cs_size(&result);
+    avail = cs_andnot(avail, pc);
+  }
+  if (needed > 0) {
+    or_cpuset got;
+    if (or_take_cpus_ex(t, avail, needed, bind, strategy, excl, seed, &got) != 0) return -1;
+    result = cs_or(result, got);
+  }
+  *out = result;
+  return 0;
+}
+
+/* resourceManager.Allocate (resource_manager.go:171-360); (r6) pref = ResourceOptions.preferredCPUs (the nominated
+ * reservation's reserved cpus; NULL / empty = none), which also makes its NUMA cpu reusable */
 static int allocate(const kg_config* cfg, const or_numa_node* n, const or_numa_pod* p, const or_hint* hint,
-                    numa_alloc* res, or_cpuset* cpus) {
+                    const or_cpuset* pref, numa_alloc* res, or_cpuset* cpus) {
   res->n = 0;
   *cpus = cs_empty();
+  if (!cs_nonempty(pref)) pref = NULL;
   const int bind = preferred_bind(n, p->preferred_policy);
   if (bind < 0) return -1; /* getResourceOptions error */
   if (!hint->nil) {
     /* allocateResourcesByHint (:195-250) */
     if (n->num_numa == 0) return -1;
     int64_t avail_cpu[KG_MAX_NUMA], avail_mem[KG_MAX_NUMA];
-    numa_available(n, avail_cpu, avail_mem);
+    numa_available(n, pref, avail_cpu, avail_mem);
     /* a cpu-bind pod splits its ORIGINAL (un-amplified) requests (:205-210: options.originalRequests); any other
      * pod's requests are never amplified, so the plain request is right for both */
     int64_t rq_c = p->req_cpu, rq_m = p->req_mem;
@@ -902,12 +980,15 @@ static int allocate(const kg_config* cfg, const or_numa_node* n, const or_numa_p
     if ((inter_c && rq_c != 0) || (inter_m && rq_m != 0)) return -1; /* Insufficient NUMA cpu/memory */
   }
   if (p->request_cpu_bind) {
-    /* allocateCPUSet (:273-360) */
-    or_cpuset avail = available_cpus(n);
+    /* allocateCPUSet (:273-360): GetAvailableCPUs(node, preferredCPUs), then per NUMA node of the allocation (or once)
+     * takePreferredCPUs */
+    or_cpuset held = n->allocated;
+    or_cpuset avail = pref ? available_pref(n, pref, &held) : available_cpus(n);
     const int required = p->required_policy != KG_BIND_NONE;
     if (required) avail = or_filter_required(&n->topo, avail, bind);
     if (cs_size(&avail) < p->num_cpus_needed) return -1;
     const int strategy = allocate_strategy(cfg, n);
+    const or_cpuset seed = cs_and(excl_seed(n, p), held); /* the allocateInfo the accumulator seeds from */
     int needed = p->num_cpus_needed;
     or_cpuset result = cs_empty();
     if (res->n > 0) {
@@ -917,8 +998,7 @@ static int allocate(const kg_config* cfg, const or_numa_node* n, const or_numa_p
         const int node_need = (int)(res->cpu[k] / 1000);
         if (node_need < num) num = node_need;
         or_cpuset got;
-        if (or_take_cpus_ex(&n->topo, in_node, num, bind, strategy, p->excl_policy, excl_seed(n, p), &got) != 0)
-          return -1;
+        if (take_preferred(&n->topo, in_node, pref, num, bind, strategy, p->excl_policy, seed, &got) != 0) return -1;
         result = cs_or(result, got);
       }
       needed -= cs_size(&result);
@@ -926,8 +1006,8 @@ static int allocate(const kg_config* cfg, const or_numa_node* n, const or_numa_p
     }
     if (needed > 0) {
       or_cpuset got;
-      if (or_take_cpus_ex(&n->topo, cs_andnot(avail, result), needed, bind, strategy, p->excl_policy,
-                          excl_seed(n, p), &got) != 0)
+      if (take_preferred(&n->topo, cs_andnot(avail, result), pref, needed, bind, strategy, p->excl_policy, seed,
+                         &got) != 0)
         return -1;
       result = cs_or(result, got);
     }
@@ -966,7 +1046,7 @@ int or_numa_filter(const kg_config* cfg, const or_numa_node* n, const or_numa_po
       numa_alloc res;
       or_cpuset cpus;
       const or_hint none = {1, 0, 0, 0};
-      if (allocate(cfg, n, p, &none, &res, &cpus) != 0) return 0;
+      if (allocate(cfg, n, p, &none, NULL, &res, &cpus) != 0) return 0;
     }
   }
   if (policy != KG_NUMA_POLICY_NONE) {
@@ -980,23 +1060,33 @@ int or_numa_filter(const kg_config* cfg, const or_numa_node* n, const or_numa_po
     *affinity = best;
     numa_alloc res;
     or_cpuset cpus;
-    if (allocate(cfg, n, p, &best, &res, &cpus) != 0) return 0;
+    if (allocate(cfg, n, p, &best, NULL, &res, &cpus) != 0) return 0;
   }
   return 1;
 }
 
 int64_t or_numa_score(const kg_config* cfg, const or_numa_node* n, const or_numa_pod* p, const or_hint* affinity,
                       int64_t node_req_cpu, int64_t node_req_mem, int64_t node_alloc_cpu, int64_t node_alloc_mem) {
+  return or_numa_score_pref(cfg, n, p, affinity, NULL, node_req_cpu, node_req_mem, node_alloc_cpu, node_alloc_mem);
+}
+
+int64_t or_numa_score_pref(const kg_config* cfg, const or_numa_node* n, const or_numa_pod* p, const or_hint* affinity,
+                           const or_cpuset* pref, int64_t node_req_cpu, int64_t node_req_mem, int64_t node_alloc_cpu,
+                           int64_t node_alloc_mem) {
   const int64_t w[2] = {cfg->numa_scoring_weights[0], cfg->numa_scoring_weights[1]};
   const int strategy = (int)cfg->numa_scoring_strategy;
   const int policy = n->numa_policy;
+  if (!cs_nonempty(pref)) pref = NULL;
   if (skip_the_node(p, policy)) {
     if (p->skip) return 0;
     /* scoreWithAmplifiedCPUs (:95-120): getResourceOptions needs a valid topology */
     if (preferred_bind(n, p->preferred_policy) < 0) return 0;
     int64_t rc = node_req_cpu;
     if (p->req_cpu != 0 && n->cpu_amp > 1) { /* the cpuset part of Requested counts amplified */
-      const int64_t am = (int64_t)cs_size(&n->allocated) * 1000;
+      /* GetAvailableCPUs(node, preferredCPUs): the allocated CPUDetails after the preferred cpus' RefCount drop */
+      or_cpuset held = n->allocated;
+      if (pref) available_pref(n, pref, &held);
+      const int64_t am = (int64_t)cs_size(&held) * 1000;
       rc = rc - am + amplify(am, n->cpu_amp);
     }
     return scorer(strategy, w, rc, node_req_mem, node_alloc_cpu, node_alloc_mem, p->req_cpu, p->req_mem);
@@ -1004,15 +1094,15 @@ int64_t or_numa_score(const kg_config* cfg, const or_numa_node* n, const or_numa
   if (p->request_cpu_bind && (!n->has_topology || !n->valid_topology)) return 0;
   numa_alloc res;
   or_cpuset cpus;
-  if (allocate(cfg, n, p, affinity, &res, &cpus) != 0) return 0;
+  if (allocate(cfg, n, p, affinity, pref, &res, &cpus) != 0) return 0;
   /* calculateAllocatableAndRequested (:122-168) */
   int64_t alloc_c, alloc_m, req_c, req_m;
   if (res.n > 0) {
     alloc_c = alloc_m = req_c = req_m = 0;
     for (int k = 0; k < res.n; k++) {
       const int i = res.numa[k];
-      if (n->numa_alloc_present[i]) {
-        req_c += numa_allocated_cpu(n, i);
+      if (n->numa_alloc_present[i]) { /* getAvailableNUMANodeResources' totalAllocated, reusable subtracted */
+        req_c += numa_allocated_cpu_pref(n, pref, i);
         req_m += n->numa_alloc_mem[i];
       }
       alloc_c += n->numa_cpu[i];
@@ -1024,19 +1114,35 @@ int64_t or_numa_score(const kg_config* cfg, const or_numa_node* n, const or_numa
     req_c = node_req_cpu;
     req_m = node_req_mem;
   }
-  if (cs_size(&cpus) > 0) req_c = amplify((int64_t)cs_size(&n->allocated) * 1000, n->cpu_amp);
+  if (cs_size(&cpus) > 0) {
+    /* getAvailableCPUs with preferred = preferredCPUs − the pod's cpus: the allocated CPUDetails' size */
+    or_cpuset held = n->allocated;
+    if (pref) {
+      const or_cpuset rest = cs_andnot(*pref, cpus);
+      available_pref(n, &rest, &held);
+    }
+    req_c = amplify((int64_t)cs_size(&held) * 1000, n->cpu_amp);
+  }
   return scorer(strategy, w, req_c, req_m, alloc_c, alloc_m, opt_req_cpu(n, p), p->req_mem);
 }
 
 int or_numa_reserve(const kg_config* cfg, or_numa_node* n, const or_numa_pod* p, const or_hint* affinity,
                     or_cpuset* cpus, int64_t* alloc) {
+  return or_numa_reserve_pref(cfg, n, p, affinity, NULL, cpus, alloc);
+}
+
+int or_numa_reserve_pref(const kg_config* cfg, or_numa_node* n, const or_numa_pod* p, const or_hint* affinity,
+                         const or_cpuset* pref, or_cpuset* cpus, int64_t* alloc) {
   *cpus = cs_empty();
   if (alloc) memset(alloc, 0, sizeof(int64_t) * OR_NUMA_ALLOC_WORDS);
   if (skip_the_node(p, n->numa_policy)) return 0;
   if (p->request_cpu_bind && (!n->has_topology || !n->valid_topology)) return -1;
   numa_alloc res;
-  if (allocate(cfg, n, p, affinity, &res, cpus) != 0) return -1;
-  /* resourceManager.Update → addPodAllocation (node_allocation.go:76-103): the pod's cpus carry its exclusive policy */
+  if (allocate(cfg, n, p, affinity, pref, &res, cpus) != 0) return -1;
+  /* resourceManager.Update → addPodAllocation (node_allocation.go:76-103): RefCount + 1 per cpu, which takes the pod's
+   * exclusive policy */
+  for (int c = 0; c < KG_MAX_CPUS; c++)
+    if (cs_has(cpus, c) && n->ref[c] < 255) n->ref[c]++;
   n->allocated = cs_or(n->allocated, *cpus);
   n->excl_pcpu = cs_andnot(n->excl_pcpu, *cpus);
   n->excl_numa = cs_andnot(n->excl_numa, *cpus);
@@ -1059,10 +1165,12 @@ int or_numa_reserve(const kg_config* cfg, or_numa_node* n, const or_numa_pod* p,
 /* resourceManager.Release → NodeAllocation.release (node_allocation.go:105-131): the pod's cpus leave the
  * allocated set (maxRefCount 1) and its NUMANodeResources are subtracted (SubtractWithNonNegativeResult). */
 void or_numa_release(or_numa_node* n, const or_cpuset* cpus, const int64_t* alloc) {
-  for (int w = 0; w < OR_CPUSET_WORDS; w++) {
-    n->allocated.w[w] &= ~cpus->w[w];
-    n->excl_pcpu.w[w] &= ~cpus->w[w]; /* RefCount 0: the CPUInfo (and its policy) is deleted */
-    n->excl_numa.w[w] &= ~cpus->w[w];
+  for (int c = 0; c < KG_MAX_CPUS; c++) {
+    if (!cs_has(cpus, c) || n->ref[c] == 0) continue;
+    if (--n->ref[c] > 0) continue; /* (r6) still held (its reservation): the CPUInfo stays, policy and all */
+    cs_del(&n->allocated, c);
+    cs_del(&n->excl_pcpu, c); /* RefCount 0: the CPUInfo (and its policy) is deleted */
+    cs_del(&n->excl_numa, c);
   }
   for (int i = 0; i < KG_MAX_NUMA; i++) {
     if (!((alloc[0] >> i) & 1)) continue;
@@ -1193,4 +1301,58 @@ int or_debug_single_numa_filter(int nl, const int32_t* counts, const int64_t* hi
     }
   }
   return 0;
+}
+
+/* (r6) Test hooks for NodeNUMAResource with reservation cpusets (golden tables of node_allocation_test.go,
+ * cpu_accumulator_test.go and plugin_test.go).  getAvailableCPUs with preferred cpus on a node whose allocated cpus
+ * all have RefCount 1: writes the available cpus. */
+void or_numa_available_pref_flat(const kg_node_numa* node, const uint64_t* preferred, uint64_t* out) {
+  or_numa_node n;
+  or_numa_node_init(&n, node);
+  or_cpuset pref;
+  for (int w = 0; w < OR_CPUSET_WORDS; w++) pref.w[w] = preferred[w];
+  const or_cpuset a = available_pref(&n, &pref, NULL);
+  for (int w = 0; w < OR_CPUSET_WORDS; w++) out[w] = a.w[w];
+}
+
+/* takePreferredCPUs (cpu_accumulator.go:33-85) on buildCPUTopologyForTest(sockets, nps, cpn, cpc), no exclusive
+ * policy; 0 ok, -1 error */
+int or_take_preferred_flat(int sockets, int nodes_per_socket, int cores_per_node, int cpus_per_core,
+                           const uint64_t* available, const uint64_t* preferred, int needed, int bind_policy,
+                           int strategy, uint64_t* out) {
+  or_topology t;
+  or_topology_build(&t, sockets, nodes_per_socket, cores_per_node, cpus_per_core);
+  or_cpuset a, pref, r;
+  for (int w = 0; w < OR_CPUSET_WORDS; w++) {
+    a.w[w] = available[w];
+    pref.w[w] = preferred[w];
+  }
+  const int rc = take_preferred(&t, a, &pref, needed, bind_policy, strategy, KG_EXCL_NONE, cs_empty(), &r);
+  for (int w = 0; w < OR_CPUSET_WORDS; w++) out[w] = rc == 0 ? r.w[w] : 0;
+  return rc;
+}
+
+/* Reserve of one pod on one node whose reservation slot 0 (rsv) holds cpus, the pod nominated into it: the node's
+ * allocated cpus and the reservation's RefCounts as the reference's NodeAllocation holds them, the preferred cpus from
+ * RestoreReservation.  Writes the chosen cpuset; 0 ok, -1 failure. */
+int or_numa_reserve_rsv_flat(const kg_config* cfg, const kg_node_numa* node, const kg_node_reservations* rsv,
+                             const kg_pod* pod, uint64_t* cpuset) {
+  or_numa_node n;
+  or_numa_node_init(&n, node);
+  or_numa_rsv_refs(&n, rsv);
+  or_numa_pod p;
+  or_numa_pod_init(cfg, pod, &p);
+  or_hint h;
+  or_numa_filter(cfg, &n, &p, &h, 0, INT64_MAX / 4);
+  const or_cpuset pref = or_numa_rsv_reserved(rsv, 0);
+  or_cpuset cs;
+  const int rc = or_numa_reserve_pref(cfg, &n, &p, &h, p.allow_cpuset ? &pref : NULL, &cs, NULL);
+  for (int w = 0; w < OR_CPUSET_WORDS; w++) cpuset[w] = cs.w[w];
+  return rc;
+}
+
+/* RestoreReservation's reservedCPUs of slot s as words (plugin_test.go TestRestoreReservation) */
+void or_numa_rsv_reserved_flat(const kg_node_reservations* r, int s, uint64_t* out) {
+  const or_cpuset c = or_numa_rsv_reserved(r, s);
+  for (int w = 0; w < OR_CPUSET_WORDS; w++) out[w] = c.w[w];
 }

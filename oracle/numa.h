@@ -26,7 +26,9 @@ typedef struct {
   or_cpuset all;
 } or_topology;
 
-/* One node's NodeNUMAResource state: TopologyOptions + NodeAllocation (maxRefCount 1). */
+/* One node's NodeNUMAResource state: TopologyOptions + NodeAllocation (maxRefCount 1).  (r6) `ref` is each cpu's
+ * CPUInfo.RefCount (node_allocation.go:76-131): 1 per holder — a pod or a reservation (its reserve pod) — so a cpu a
+ * pod took from its reservation's reserved cpus has RefCount 2; `allocated` is the set with RefCount ≥ 1. */
 typedef struct {
   int has_topology, valid_topology;
   or_topology topo;
@@ -40,6 +42,8 @@ typedef struct {
   or_cpuset excl_pcpu, excl_numa; /* allocated cpus whose CPUInfo.ExclusivePolicy is PCPULevel / NUMANodeLevel */
   int64_t numa_alloc_cpu[KG_MAX_NUMA], numa_alloc_mem[KG_MAX_NUMA];
   int numa_alloc_present[KG_MAX_NUMA]; /* allocatedResources[numa] exists */
+  uint8_t ref[KG_MAX_CPUS];            /* (r6) CPUInfo.RefCount                                     */
+  int refs_ready;                      /* (r6) the reservations' RefCount-2 cpus were counted         */
 } or_numa_node;
 
 /* NodeNUMAResource preFilterState (plugin.go:177-186, PreFilter :220-270) */
@@ -50,6 +54,7 @@ typedef struct {
   int num_cpus_needed;
   int excl_policy;          /* preferredCPUExclusivePolicy (KG_EXCL_*) */
   int64_t req_cpu, req_mem; /* PodRequestsAndLimits cpu (milli) / memory */
+  int allow_cpuset;         /* (r6) AllowUseCPUSet (util.go:42-49): PreRestoreReservation's skip = !allow_cpuset */
 } or_numa_pod;
 
 /* the affinity the topology manager stores for a node (store.SetAffinity, manager.go:73) */
@@ -85,6 +90,18 @@ int64_t or_numa_score(const kg_config* cfg, const or_numa_node* n, const or_numa
 int or_numa_reserve(const kg_config* cfg, or_numa_node* n, const or_numa_pod* p, const or_hint* affinity,
                     or_cpuset* cpus, int64_t* alloc);
 void or_numa_release(or_numa_node* n, const or_cpuset* cpus, const int64_t* alloc);
+
+/* (r6) NodeNUMAResource with reservations holding cpusets (nodenumaresource/reservation.go, plugin.go:465-535).
+ * pref = the nominated reservation's reservedCPUs (getReservationReservedCPUs), NULL or empty = none. */
+int64_t or_numa_score_pref(const kg_config* cfg, const or_numa_node* n, const or_numa_pod* p, const or_hint* affinity,
+                           const or_cpuset* pref, int64_t node_req_cpu, int64_t node_req_mem, int64_t node_alloc_cpu,
+                           int64_t node_alloc_mem);
+int or_numa_reserve_pref(const kg_config* cfg, or_numa_node* n, const or_numa_pod* p, const or_hint* affinity,
+                         const or_cpuset* pref, or_cpuset* cpus, int64_t* alloc);
+/* RefCount 2 for the cpus a reservation holds that one of its assigned pods holds too (once per state) */
+void or_numa_rsv_refs(or_numa_node* n, const kg_node_reservations* r);
+/* RestoreReservation's reservedCPUs of reservation slot s (reservation.go:76-113): its cpuset minus its assigned pods' */
+or_cpuset or_numa_rsv_reserved(const kg_node_reservations* r, int s);
 
 #ifdef __cplusplus
 }

@@ -569,6 +569,7 @@ int or_unreserve(const kg_config* cfg, or_node_state* st, void* numa_states, kg_
   if (pod->quota_id > n_quotas) return KG_E_INVALID;
   or_assume_pod(cfg, &st[node], pod, -1); /* NodeInfo.RemovePod + LoadAware Unreserve (unAssign) */
   if (numa_states && (cfg->numa_filter || cfg->numa_score) && cpus && numa_alloc) {
+    if (rsv) or_numa_rsv_refs(&((or_numa_node*)numa_states)[node], &rsv[node]);
     or_cpuset cs;
     for (int w = 0; w < OR_CPUSET_WORDS; w++) cs.w[w] = cpus[w];
     or_numa_release(&((or_numa_node*)numa_states)[node], &cs, numa_alloc); /* nodenumaresource/plugin.go:417-425 */
@@ -582,6 +583,8 @@ int or_unreserve(const kg_config* cfg, or_node_state* st, void* numa_states, kg_
     if (rsv && slot >= 0) or_ds_rsv_assign(&rsv[node], slot, &dev[node], &dsp, minors, -1);
   }
   if (rsv && slot >= 0) or_rsv_forget(&rsv[node], slot, pod); /* reservation/plugin.go:561-583 */
+  if (rsv && slot >= 0 && cpus) /* (ABI 15) the pod leaves the reservation's AssignedPods: its cpus are reserved again */
+    for (int w = 0; w < OR_CPUSET_WORDS; w++) rsv[node].cpus_assigned[slot][w] &= ~cpus[w];
   if (quotas && pod->quota_id > 0) { /* elasticquota/plugin.go:348-360 → UnreservePod (addUsedNonNegativeNoLock) */
     kg_quota* q = &quotas[pod->quota_id - 1];
     int64_t req[KG_QUOTA_RES];

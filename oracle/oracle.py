@@ -42,6 +42,15 @@ def lib():
         L = ctypes.CDLL(LIB)
         vp, i64, i = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int
         L.or_estimate_pod.argtypes = [vp, vp, vp]
+        # (r6) NodeNUMAResource with reservation cpusets
+        L.or_numa_available_pref_flat.argtypes = [vp, vp, vp]
+        L.or_numa_available_pref_flat.restype = None
+        L.or_take_preferred_flat.argtypes = [i, i, i, i, vp, vp, i, i, i, vp]
+        L.or_take_preferred_flat.restype = i
+        L.or_numa_reserve_rsv_flat.argtypes = [vp, vp, vp, vp, vp]
+        L.or_numa_reserve_rsv_flat.restype = i
+        L.or_numa_rsv_reserved_flat.argtypes = [vp, i, vp]
+        L.or_numa_rsv_reserved_flat.restype = None
         L.or_la_node_terms.argtypes = [vp, vp, vp, ctypes.c_int64, vp, ctypes.c_int64, vp]
         L.or_la_node_terms.restype = None
         L.or_estimate_node.argtypes = [vp, i]
@@ -528,6 +537,43 @@ def take_cpus(topology, available, needed: int, bind_policy: str, strategy: str,
     if rc != 0:
         return None
     return [64 * w + b for w in range(len(out)) for b in range(64) if (int(out[w]) >> b) & 1]
+
+
+def _cpu_list(words):
+    return [64 * w + b for w in range(len(words)) for b in range(64) if (int(words[w]) >> b) & 1]
+
+
+def numa_available_pref(node_numa, preferred):
+    """(r6) getAvailableCPUs with preferred cpus (node_allocation.go:133-153) on a node whose allocated cpus have
+    RefCount 1: the available cpu list."""
+    out = np.zeros(abi.MAX_CPUS // 64, dtype=np.uint64)
+    lib().or_numa_available_pref_flat(p(np.ascontiguousarray(node_numa)), p(_cpu_words(preferred)), p(out))
+    return _cpu_list(out)
+
+
+def take_preferred(topology, available, preferred, needed: int, bind_policy: str, strategy: str):
+    """(r6) takePreferredCPUs (cpu_accumulator.go:33-85): the cpu list or None on error."""
+    out = np.zeros(abi.MAX_CPUS // 64, dtype=np.uint64)
+    rc = lib().or_take_preferred_flat(*topology, p(_cpu_words(available)), p(_cpu_words(preferred)), needed,
+                                      abi.BIND[bind_policy], abi.STRATEGY[strategy], p(out))
+    return None if rc != 0 else _cpu_list(out)
+
+
+def numa_rsv_reserved(rsv, slot: int):
+    """(r6) RestoreReservation's reservedCPUs of one slot (nodenumaresource/reservation.go:76-113)."""
+    out = np.zeros(abi.MAX_CPUS // 64, dtype=np.uint64)
+    lib().or_numa_rsv_reserved_flat(p(np.ascontiguousarray(np.asarray(rsv, dtype=abi.NODE_RSV_DTYPE).reshape(1))),
+                                    int(slot), p(out))
+    return _cpu_list(out)
+
+
+def numa_reserve_rsv(cfg, node_numa, rsv, pod):
+    """(r6) Reserve of a pod nominated into reservation slot 0, which holds cpus: (0 / -1, chosen cpu list)."""
+    out = np.zeros(abi.MAX_CPUS // 64, dtype=np.uint64)
+    rc = lib().or_numa_reserve_rsv_flat(p(cfg), p(np.ascontiguousarray(node_numa)),
+                                        p(np.ascontiguousarray(np.asarray(rsv, dtype=abi.NODE_RSV_DTYPE).reshape(1))),
+                                        p(np.ascontiguousarray(pod)), p(out))
+    return rc, _cpu_list(out)
 
 
 def numa_eval(cfg, node_numa, pod, node_requested=(0, 0), node_allocatable=(0, 0)):

@@ -309,6 +309,9 @@ int or_schedule_resv_full(const kg_config* cfg, int64_t n_nodes, const kg_node* 
   const kg_node_predicates zero_pred = {0, 0, 0, 0, 0, 0, 0};
   const int rsv_on = cfg->reservation_filter || cfg->reservation_score;
   const int ds_on = dev && (cfg->ds_filter || cfg->ds_score);
+  /* (r6) the cpus a reservation and one of its assigned pods both hold have RefCount 2 in NodeAllocation */
+  if (numa_on && rsv_on)
+    for (int64_t i = 0; i < n_nodes; i++) or_numa_rsv_refs(&numa[i], &rsv[i]);
   if (n_threads < 1) n_threads = 1;
   /* chunkSizeFor (pkg/util/parallelize/parallelism.go:35-46) with parallelism = n_threads */
   int64_t chunk = (int64_t)sqrt((double)n_nodes), lim = n_nodes / n_threads + 1;
@@ -447,10 +450,12 @@ int or_schedule_resv_full(const kg_config* cfg, int64_t n_nodes, const kg_node* 
         if (sc < 0) { err = (int)sc; continue; }
         t += cfg->weight_loadaware * sc;
       }
-      if (numa_on && cfg->numa_score) /* scoring.go:55-93 on the restored NodeInfo with the stored affinity */
-        t += cfg->weight_numa * or_numa_score(cfg, &numa[i], &npod, &aff[i], rs.requested[KG_RES_CPU],
-                                              rs.requested[KG_RES_MEMORY], nd->allocatable[KG_RES_CPU],
-                                              nd->allocatable[KG_RES_MEMORY]);
+      int64_t nsc = 0;
+      if (numa_on && cfg->numa_score) { /* scoring.go:55-93 on the restored NodeInfo with the stored affinity */
+        nsc = or_numa_score(cfg, &numa[i], &npod, &aff[i], rs.requested[KG_RES_CPU], rs.requested[KG_RES_MEMORY],
+                            nd->allocatable[KG_RES_CPU], nd->allocatable[KG_RES_MEMORY]);
+        t += cfg->weight_numa * nsc;
+      }
       if (cfg->balanced_score)
         t += cfg->weight_balanced * or_balanced_score(nd->allocatable[KG_RES_CPU], nd->allocatable[KG_RES_MEMORY],
                                                       rs.requested[KG_RES_CPU], rs.requested[KG_RES_MEMORY],
@@ -465,6 +470,16 @@ int or_schedule_resv_full(const kg_config* cfg, int64_t n_nodes, const kg_node* 
                                            cfg->ds_scoring_weights)
                       : -1;
       raw[i] = nom[i] >= 0 ? or_rsv_score_slot(pod, &rsv[i], nom[i]) : 0;
+      /* (r6) NodeNUMAResource Score after the PreScore nomination: getResourceOptions offers the nominated
+       * reservation's reserved cpus (getReservationReservedCPUs, plugin.go:513-535; RestoreReservation
+       * reservation.go:76-113, skipped unless AllowUseCPUSet) as preferredCPUs / reusable NUMA cpu */
+      if (numa_on && cfg->numa_score && nom[i] >= 0 && npod.allow_cpuset && !(pod->flags & KG_POD_RESERVE)) {
+        const or_cpuset pref = or_numa_rsv_reserved(&rsv[i], nom[i]);
+        const int64_t psc = or_numa_score_pref(cfg, &numa[i], &npod, &aff[i], &pref, rs.requested[KG_RES_CPU],
+                                               rs.requested[KG_RES_MEMORY], nd->allocatable[KG_RES_CPU],
+                                               nd->allocatable[KG_RES_MEMORY]);
+        base[i] += cfg->weight_numa * (psc - nsc);
+      }
       order[i] = ns.has_state ? or_rsv_node_order(&ns, &rsv[i]) : INT64_MAX;
       dsraw[i] = (ds_on && cfg->ds_score && !dsp.skip)
                      ? or_ds_score_rsv(&dev[i], &dsp, rsv_on ? &rsv[i] : NULL, &dst, nom[i],
@@ -569,7 +584,12 @@ int or_schedule_resv_full(const kg_config* cfg, int64_t n_nodes, const kg_node* 
     int64_t nalloc[OR_NUMA_ALLOC_WORDS] = {0};
     if (win >= 0 && numa_on) {
       numa_save = numa[win];
-      if (or_numa_reserve(cfg, &numa[win], &npod, &aff[win], &cpus, nalloc) != 0) {
+      /* (r6) the nominated reservation's reserved cpus are Reserve's preferredCPUs too (getResourceOptions) */
+      or_cpuset pref;
+      memset(&pref, 0, sizeof(pref));
+      if (rsv_on && nom[win] >= 0 && npod.allow_cpuset && !(pod->flags & KG_POD_RESERVE))
+        pref = or_numa_rsv_reserved(&rsv[win], nom[win]);
+      if (or_numa_reserve_pref(cfg, &numa[win], &npod, &aff[win], &pref, &cpus, nalloc) != 0) {
         numa[win] = numa_save;
         win = -1;
       }
@@ -609,6 +629,11 @@ int or_schedule_resv_full(const kg_config* cfg, int64_t n_nodes, const kg_node* 
         r->assigned[s] += 1;
         /* (ABI 13) the reservation's allocated GPUs: the pod's allocation on the reservation's minors */
         if (ds_on && minors > 0) or_ds_rsv_assign(r, s, &dev[win], &dsp, minors, 1);
+        /* (ABI 15) an assigned pod's cpus leave the reservation's reserved cpus at the next RestoreReservation */
+        int holds = 0;
+        for (int w = 0; w < OR_CPUSET_WORDS; w++) holds |= r->cpus[s][w] != 0;
+        if (numa_on && holds)
+          for (int w = 0; w < OR_CPUSET_WORDS; w++) r->cpus_assigned[s][w] |= cpus.w[w];
         if (out_slot) out_slot[p] = nom[win];
       }
       if (quota) or_quota_charge(quota, pod);
