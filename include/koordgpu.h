@@ -657,8 +657,14 @@ int kg_nodes_predicates_upsert(kg_engine* e, const kg_node_predicates* p, const 
 /* Reads the DEVICE reservation slots: allocated cpu / memory and assigned count, KG_MAX_RSV_SLOTS per node. */
 int kg_nodes_read_reservations(kg_engine* e, int64_t* allocated_cpu, int64_t* allocated_mem, int64_t* assigned);
 /* (ABI 13) Reads the DEVICE reservation slots' gpu_allocated, [n_nodes][KG_MAX_RSV_SLOTS][KG_MAX_MINORS][3] (zeros
- * for slots holding no GPU, or when DeviceShare is off). */
+ * for slots holding no GPU, or when DeviceShare is off; a re-upserted node's slots that no longer hold GPUs read zero).
+ * KG_E_INVALID when the profile does not enable Reservation. */
 int kg_nodes_read_reservation_gpus(kg_engine* e, int64_t* gpu_allocated);
+/* (ABI 15) Reads the DEVICE reservation slots' cpus_assigned, [n_nodes][KG_MAX_RSV_SLOTS][KG_MAX_CPUS / 64] (zeros for
+ * slots holding no cpuset, or when NodeNUMAResource is off); KG_E_INVALID when the profile does not enable Reservation.
+ * Replaces the reference's read of reservationRestoreStateData through resourceManager.GetAllocatedCPUSet
+ * (nodenumaresource/reservation.go:84-101). */
+int kg_nodes_read_reservation_cpus(kg_engine* e, uint64_t* cpus_assigned);
 /* The reservation slot Reserve assumed each staged pod [first, first+count) into (-1 = none). */
 int kg_results_fetch_reservations(kg_engine* e, int64_t first, int64_t count, int32_t* out_slot);
 

@@ -214,7 +214,7 @@ EXPORTED_SYMBOLS = (
     "kg_nodes_numa_upsert", "kg_nodes_read_numa", "kg_results_fetch_cpusets", "kg_pods_evaluate_numa",
     "kg_nodes_device_upsert", "kg_nodes_read_device", "kg_results_fetch_devices", "kg_pods_evaluate_device",
     "kg_quotas_set", "kg_quotas_read", "kg_nodes_reservation_upsert", "kg_nodes_read_reservations",
-    "kg_nodes_read_reservation_gpus",
+    "kg_nodes_read_reservation_gpus", "kg_nodes_read_reservation_cpus",
     "kg_results_fetch_reservations", "kg_profile_enable", "kg_profile_read", "kg_loopback_create",
     "kg_loopback_destroy", "kg_engine_create_loopback", "kg_pods_unreserve", "kg_engine_set_clock",
     "kg_node_pods_metric_set", "kg_debug_numa_merge", "kg_pods_evaluate_reservation", "kg_nodes_predicates_upsert",
@@ -296,6 +296,7 @@ def load_library(path: str | None = None):
         "kg_nodes_reservation_upsert": (i, [vp, vp, vp, i64]),
         "kg_nodes_read_reservations": (i, [vp, vp, vp, vp]),
         "kg_nodes_read_reservation_gpus": (i, [vp, vp]),
+        "kg_nodes_read_reservation_cpus": (i, [vp, vp]),
         "kg_results_fetch_reservations": (i, [vp, i64, i64, vp]),
         "kg_profile_enable": (i, [vp, i]),
         "kg_profile_read": (i, [vp, vp, vp]),

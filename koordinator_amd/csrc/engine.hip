@@ -3041,7 +3041,7 @@ __global__ void unreserve_pods(DevTable T, const DevPod* __restrict__ pods, cons
                                int32_t* __restrict__ out_minors, RsvNode* __restrict__ RN, int32_t* __restrict__ out_rslot,
                                QuotaRow* __restrict__ quotas, int nq, const int64_t* __restrict__ qdev,
                                const int64_t* __restrict__ paux, GroupTable G, const GroupPod* __restrict__ gpods,
-                               int hard_w, RsvGpu* __restrict__ rg) {
+                               int hard_w, RsvGpu* __restrict__ rg, RsvCpu* __restrict__ rcs) {
   if (blockIdx.x != 0 || threadIdx.x != 0) return;
   for (int64_t k = 0; k < n; ++k) {
     const int64_t j = idx[k];
@@ -3065,11 +3065,19 @@ __global__ void unreserve_pods(DevTable T, const DevPod* __restrict__ pods, cons
     if (gpods) group_apply(G, w, gpods[j], -1, hard_w);  // the node's pod-group counters
     if (p.flags & P_AUX)  // ephemeral-storage / scalar Requested
       for (int q = 0; q < kAux; ++q) T.aux[(size_t)(kAux + q) * T.cap + w] -= paux[(size_t)j * kAux + q];
+    uint64_t pc[kCpuWords] = {0, 0, 0, 0};  // the pod's cpuset, before it is cleared below
     if (nm) {  // nodenumaresource/plugin.go:417-425
       uint64_t* c = out_cpus + (size_t)j * kCpuWords;
       int64_t* rec = out_nrec + (size_t)j * kNumaRecWords;
+      // (ABI 15) the cpus the node's reservations hold keep RefCount 1 (the reservation's)
+      uint64_t keep[kCpuWords] = {0, 0, 0, 0};
+      if (rcs && RN)
+        for (int s = 0; s < kRsvSlots; ++s)
+          if (RN[w].meta[s] & RS_CPUS)
+            for (int q = 0; q < kCpuWords; ++q) keep[q] |= rcs[(size_t)w * kRsvSlots + s].r[q];
+      for (int q = 0; q < kCpuWords; ++q) pc[q] = c[q];
       NumaMut m = nm[w];
-      numa_release(m, c, rec);
+      numa_release(m, c, rec, keep);
       nm[w] = m;
       for (int q = 0; q < kCpuWords; ++q) c[q] = 0;
       for (int q = 0; q < kNumaRecWords; ++q) rec[q] = 0;
@@ -3097,6 +3105,9 @@ __global__ void unreserve_pods(DevTable T, const DevPod* __restrict__ pods, cons
       // (deviceshare/reservation.go:150-155)
       if (rg && gm > 0 && (rn.meta[s] & RS_GPU))
         rsv_gpu_assign(rg[(size_t)w * kRsvSlots + s], ds_instance(ds[w], dpods[j]), gm, -1);
+      // (ABI 15) the pod leaves AssignedPods: its cpus are the reservation's reserved cpus again
+      if (rcs && (rn.meta[s] & RS_CPUS))
+        for (int q = 0; q < kCpuWords; ++q) rcs[(size_t)w * kRsvSlots + s].u[q] &= ~pc[q];
       if (rn.assigned[s] > 0) {
         if (rn.alloc_cpu[s] > 0) rn.allocd_cpu[s] = rn.allocd_cpu[s] > p.req_cpu ? rn.allocd_cpu[s] - p.req_cpu : 0;
         if (rn.alloc_mem[s] > 0) rn.allocd_mem[s] = rn.allocd_mem[s] > p.req_mem ? rn.allocd_mem[s] - p.req_mem : 0;
@@ -3415,6 +3426,9 @@ struct kg_engine {
   DevBuf<RsvGpu> rsv_g;                         // (ABI 13) [cap][kRsvSlots] GPU holdings, allocated at the first GPU slot
   std::vector<uint8_t> rsv_gnode;               // per node: it has an RS_GPU slot
   int64_t rgpu_nodes = 0;                       // nodes with an RS_GPU slot (> 0 routes queues to the per-pod pass)
+  DevBuf<RsvCpu> rsv_c;                         // (ABI 15) [cap][kRsvSlots] cpusets, allocated at the first cpu slot
+  std::vector<uint8_t> rsv_cnode;               // per node: it has an RS_CPUS slot
+  int64_t rcpu_nodes = 0;                       // nodes with an RS_CPUS slot (> 0 routes queues to the per-pod pass)
   DevBuf<uint64_t> rsv_pd;      // [cap][kRsvSlots] (ABI 12) the slots' fakeNode predicates
   DevBuf<int32_t> rsv_nd;       // slots in use per node
   DevBuf<RsvPod> rpods;
@@ -3780,13 +3794,14 @@ int decode_numa_pod(const kg_config& c, const kg_pod& p, NumaPod& d) {
     return fail(KG_E_INVALID, "pod cpu exclusive policy");
   d.req_cpu = p.requests[KG_RES_CPU];
   d.req_mem = p.requests[KG_RES_MEMORY];
+  d.allow = (p.qos == KG_QOS_LSE || p.qos == KG_QOS_LSR) && p.priority_class == KG_PRIO_PROD;  // PreRestoreReservation
   bool zero = true;
   for (int r = 0; r < KG_RES_MAX; ++r) zero &= p.requests[r] == 0;
   if (zero) {
     d.skip = 1;
     return 0;
   }
-  if (!((p.qos == KG_QOS_LSE || p.qos == KG_QOS_LSR) && p.priority_class == KG_PRIO_PROD)) return 0;
+  if (!d.allow) return 0;
   int bind = (int)p.preferred_cpu_bind_policy;
   if (bind == KG_BIND_NONE || bind == KG_BIND_DEFAULT) bind = (int)c.numa_default_cpu_bind_policy;
   int required = (int)p.required_cpu_bind_policy;
@@ -4739,6 +4754,7 @@ RsvExt rsv_ext(kg_engine* e) {
   X.rgpu = e->ds_on && e->rgpu_nodes > 0 ? e->rsv_g.p : nullptr;
   X.rpods = e->rpods.p;
   X.rsv_n = e->rsv_nd.p;
+  X.rcpu = e->numa_on && e->rcpu_nodes > 0 ? e->rsv_c.p : nullptr;
   return X;
 }
 
@@ -5009,9 +5025,11 @@ int run_xr(kg_engine* e, int64_t first, int64_t count, kg_stats* stats, double t
   return 0;
 }
 
-int decode_node_rsv(const kg_node_reservations& r, RsvNode& d, int32_t& ns, RsvGpu* g, bool ds_on) {
+int decode_node_rsv(const kg_node_reservations& r, RsvNode& d, int32_t& ns, RsvGpu* g, bool ds_on, RsvCpu* c,
+                    bool numa_on) {
   std::memset(&d, 0, sizeof(d));
   std::memset(g, 0, sizeof(RsvGpu) * kRsvSlots);
+  std::memset(c, 0, sizeof(RsvCpu) * kRsvSlots);
   if (r.n < 0 || r.n > KG_MAX_RSV_SLOTS) return fail(KG_E_INVALID, "reservation slot count %lld", (long long)r.n);
   if (r.predicate_count < 0 || r.predicate_count > 64)
     return fail(KG_E_INVALID, "reservation predicate_count %lld outside [0, 64]", (long long)r.predicate_count);
@@ -5036,6 +5054,16 @@ int decode_node_rsv(const kg_node_reservations& r, RsvNode& d, int32_t& ns, RsvG
     d.order[s] = (int32_t)r.order[s];
     d.meta[s] = (r.available[s] ? RS_AVAIL : 0u) | (r.allocate_once[s] ? RS_ONCE : 0u) |
                 (r.unschedulable[s] ? RS_UNSCHED : 0u) | ((uint32_t)r.policy[s] << 4);
+    // (ABI 15) the cpuset the reservation holds and its assigned pods' (NodeNUMAResource only reads them)
+    uint64_t any = 0;
+    for (int w = 0; w < kCpuWords; ++w) any |= r.cpus[s][w];
+    if (any && numa_on) {
+      for (int w = 0; w < kCpuWords; ++w) {
+        c[s].r[w] = r.cpus[s][w];
+        c[s].u[w] = r.cpus_assigned[s][w];
+      }
+      d.meta[s] |= RS_CPUS;
+    }
     // (ABI 13) the GPUs the reservation holds (DeviceShare only reads them)
     if (r.gpu_minors[s] < 0 || r.gpu_minors[s] >= (int64_t(1) << kMinors))
       return fail(KG_E_INVALID, "reservation slot %d: gpu_minors outside [0, 2^%d)", s, kMinors);
@@ -5790,7 +5818,8 @@ int kg_pods_unreserve(kg_engine* e, int64_t first, int64_t count, const uint8_t*
                                         e->rsv_on ? e->rsv_d.p : nullptr, e->out_rslot.p, e->quotas.p, e->nq,
                                         (e->ds_on || e->rsv_on) ? e->qdev.p : nullptr, e->paux.p,
                                         GroupTable{e->grp_d.p, e->capacity}, e->grp_on ? e->gpods.p : nullptr,
-                                        e->GP.hard_w, e->rsv_on && e->ds_on && e->rgpu_nodes > 0 ? e->rsv_g.p : nullptr);
+                                        e->GP.hard_w, e->rsv_on && e->ds_on && e->rgpu_nodes > 0 ? e->rsv_g.p : nullptr,
+                                        e->rsv_on && e->numa_on && e->rcpu_nodes > 0 ? e->rsv_c.p : nullptr);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(e->stream));
   e->eph_dirty |= e->eph_any;  // a release may end an ephemeral-storage overcommit
@@ -6014,7 +6043,9 @@ static int schedule_staged_impl(kg_engine* e, int64_t first, int64_t count, kg_s
   // (PodTopologySpread / InterPodAffinity profiles: one pod per pass — the batched rounds' stop rules do not cover
   // their cluster-wide minimum / count and min-max normalisation)
   // (ABI 13) GPU-holding reservations: the per-pod pass (the batched rounds keep no DeviceShare restore)
-  if (e->exact_on && e->xr_on && !e->grp_on && !e->rsv_ext_q && e->rgpu_nodes == 0 && count >= kXrMin && e->n_nodes > 0)
+  // (ABI 15) reservations holding cpusets: the per-pod pass too (the batched rounds compile the preferred-cpu path out)
+  if (e->exact_on && e->xr_on && !e->grp_on && !e->rsv_ext_q && e->rgpu_nodes == 0 && e->rcpu_nodes == 0 &&
+      count >= kXrMin && e->n_nodes > 0)
     return run_xr(e, first, count, stats, t0);
   if (e->exact_on || (count <= kExactSmall && e->n_ranks == 1)) return run_rsv(e, first, count, stats, t0);
   RoundGeom g;
@@ -6642,11 +6673,29 @@ int kg_nodes_reservation_upsert(kg_engine* e, const kg_node_reservations* r, con
   std::vector<RsvNode> h(n);
   std::vector<int32_t> hn(n);
   std::vector<RsvGpu> hg((size_t)n * kRsvSlots);
-  bool any_gpu = false;
+  std::vector<RsvCpu> hc((size_t)n * kRsvSlots);
+  bool any_gpu = false, any_cpu = false;
   for (int64_t k = 0; k < n; ++k) {
     if (idx[k] < 0 || idx[k] >= e->capacity) return fail(KG_E_INVALID, "node index %d outside capacity", idx[k]);
-    if (int rc = decode_node_rsv(r[k], h[k], hn[k], hg.data() + (size_t)k * kRsvSlots, e->ds_on)) return rc;
-    for (int s = 0; s < hn[k]; ++s) any_gpu |= (h[k].meta[s] & RS_GPU) != 0;
+    if (int rc = decode_node_rsv(r[k], h[k], hn[k], hg.data() + (size_t)k * kRsvSlots, e->ds_on,
+                                 hc.data() + (size_t)k * kRsvSlots, e->numa_on))
+      return rc;
+    for (int s = 0; s < hn[k]; ++s) {
+      any_gpu |= (h[k].meta[s] & RS_GPU) != 0;
+      any_cpu |= (h[k].meta[s] & RS_CPUS) != 0;
+    }
+  }
+  // (ABI 15) the cpusets: allocated (zeroed) at the first cpu-holding slot, then scattered with every upsert
+  if (any_cpu && !e->rsv_c.p) {
+    if (int rc = e->rsv_c.ensure((size_t)kRsvSlots * e->capacity)) return rc;
+    HIP_TRY(hipMemsetAsync(e->rsv_c.p, 0, sizeof(RsvCpu) * kRsvSlots * (size_t)e->capacity, e->stream));
+  }
+  if ((int64_t)e->rsv_cnode.size() < e->capacity) e->rsv_cnode.assign(e->capacity, 0);
+  for (int64_t k = 0; k < n; ++k) {
+    bool c = false;
+    for (int s = 0; s < hn[k]; ++s) c |= (h[k].meta[s] & RS_CPUS) != 0;
+    e->rcpu_nodes += (int64_t)c - (int64_t)e->rsv_cnode[idx[k]];
+    e->rsv_cnode[idx[k]] = c ? 1 : 0;
   }
   // (ABI 13) the GPU holdings: allocated (zeroed) at the first GPU-holding slot, then scattered with every upsert
   if (any_gpu && !e->rsv_g.p) {
@@ -6688,9 +6737,34 @@ int kg_nodes_reservation_upsert(kg_engine* e, const kg_node_reservations* r, con
         reinterpret_cast<RsvGpuNode*>(e->rsv_g.p), bg.p, di, n);
     HIP_TRY(hipGetLastError());
   }
+  DevBuf<RsvCpuNode> bc;
+  if (e->rsv_c.p) {
+    if (int rc = bc.ensure(n)) return rc;
+    HIP_TRY(hipMemcpyAsync(bc.p, hc.data(), n * sizeof(RsvCpuNode), hipMemcpyHostToDevice, e->stream));
+    scatter_rows<RsvCpuNode><<<(unsigned)((n + 255) / 256), 256, 0, e->stream>>>(
+        reinterpret_cast<RsvCpuNode*>(e->rsv_c.p), bc.p, di, n);
+    HIP_TRY(hipGetLastError());
+  }
   HIP_TRY(hipStreamSynchronize(e->stream));
   b.release();
   bg.release();
+  bc.release();
+  return 0;
+}
+
+int kg_nodes_read_reservation_cpus(kg_engine* e, uint64_t* cpus_assigned) {
+  if (!e || !cpus_assigned) return fail(KG_E_INVALID, "null argument");
+  if (!e->rsv_on) return fail(KG_E_INVALID, "the profile does not enable Reservation");
+  const int64_t n = e->n_nodes;
+  const size_t per = (size_t)KG_MAX_RSV_SLOTS * kCpuWords;
+  std::memset(cpus_assigned, 0, (size_t)n * per * 8);
+  if (n == 0 || !e->rsv_c.p) return 0;
+  std::vector<RsvCpu> h((size_t)n * kRsvSlots);
+  HIP_TRY(hipMemcpyAsync(h.data(), e->rsv_c.p, h.size() * sizeof(RsvCpu), hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  for (int64_t i = 0; i < n; ++i)
+    for (int s = 0; s < kRsvSlots; ++s)
+      for (int w = 0; w < kCpuWords; ++w) cpus_assigned[(size_t)i * per + (size_t)s * kCpuWords + w] = h[(size_t)i * kRsvSlots + s].u[w];
   return 0;
 }
 

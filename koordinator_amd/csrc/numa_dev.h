@@ -9,7 +9,9 @@
 //   frameworkext/topologymanager/policy*.go   mergeFilteredHints + best-effort / restricted / single-numa-node
 // CPU sets are 256-bit masks in buildCPUTopology numbering (cpu = ((socket·nps + node)·cpn + core)·cpc + t), so a
 // NUMA node, a socket and a core are contiguous cpu ranges.  Scope: ≤ 4 NUMA nodes, cpus per core 1 or 2,
-// maxRefCount 1, no reservations, exclusive policy None (validated at ingest); cpu amplification included.
+// maxRefCount 1; cpu amplification and exclusive policies included.  (r6) Reservations that hold cpusets
+// (nodenumaresource/reservation.go, plugin.go:465-535): a pod nominated into one gets its reserved cpus as
+// preferredCPUs at Score and Reserve (numa_alloc_pref / numa_score_pref / numa_reserve_pref below).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -59,7 +61,7 @@ struct NumaPod {
   int32_t skip, prefilter_error, cpu_bind, required;  // required/preferred: KG_BIND_*
   int32_t preferred, needed;
   int32_t excl;  // preferredCPUExclusivePolicy (KG_EXCL_*)
-  int32_t pad;
+  int32_t allow;  // (r6) AllowUseCPUSet (util.go:42-49): RestoreReservation restores reserved cpus only for such pods
 };
 static_assert(sizeof(NumaPod) == 48, "NumaPod layout");
 
@@ -1093,17 +1095,174 @@ __device__ __forceinline__ bool numa_reserve(const NumaStatic& s, NumaMut& m, co
   return true;
 }
 
+// ---------------------------------------------------------------------------------------------------------
+// (r6) Reservations holding cpusets.  getResourceOptions (plugin.go:465-510) gives a pod nominated into a reservation
+// preferredCPUs P = the reservation's reserved cpus (RestoreReservation: its cpuset minus its assigned pods', every one
+// of them held by the reservation alone, RefCount 1) and reusableResources = Amplify(|P on NUMA node i| × 1000) of cpu
+// per NUMA node holding some.  GetAvailableCPUs(P) drops P's RefCounts to 0, so P is available and its cpus leave the
+// allocated CPUDetails; getAvailableNUMANodeResources subtracts the reusable cpu from allocatedResources (≥ 0).
+// ---------------------------------------------------------------------------------------------------------
+// the view with P: the reusable cpu off each NUMA node's allocated cpu (the counts of `v` are not used with P)
+__device__ __forceinline__ NumaView view_with_pref(NumaView v, const NumaStatic& s, const CpuSet& P) {
+  const Topo t = make_topo(s);
+  const CpuSet pin = cs_and(P, t.all());
+#pragma unroll
+  for (int i = 0; i < kNumaMax; ++i) {
+    const int k = cs_count(cs_and(pin, t.node_cpus(i)));
+    const int64_t reusable = k > 0 ? amplify((int64_t)k * 1000, v.amp) : 0;
+    const int64_t ac = v.alloc_cpu[i] - reusable;
+    v.alloc_cpu[i] = ac > 0 ? ac : 0;  // 0 stays 0 for a NUMA node without an allocatedResources entry
+  }
+  return v;
+}
+
+// takePreferredCPUs (cpu_accumulator.go:33-85): up to `needed` cpus from the preferred ones among `in` (one takeCPUs
+// over them), then the rest from the others — one inlined take_cpus in a two-pass loop
+__device__ __forceinline__ bool take_preferred(const Topo& t, const CpuSet& in, const CpuSet& P, int needed, int bind,
+                                               int strategy, CpuSet& out, int excl, const CpuSet& seed) {
+  out = cs_zero();
+  const CpuSet pc = cs_and(in, P);
+  const int np = cs_count(pc);
+  for (int ph = 0; ph < 2; ++ph) {
+    if (ph == 0 && np == 0) continue;
+    if (ph == 1 && needed <= 0) break;
+    const CpuSet set = ph == 0 ? pc : cs_andnot(in, pc);
+    const int k = ph == 0 ? (needed < np ? needed : np) : needed;
+    CpuSet one;
+    if (!take_cpus(t, set, k, bind, strategy, one, excl, seed)) return false;
+    out = cs_or(out, one);
+    needed -= cs_count(one);
+  }
+  return true;
+}
+
+// resourceManager.Allocate (resource_manager.go:171-360) with preferredCPUs P, exact: allocateResourcesByHint on the
+// reusable-adjusted view `vp`, then allocateCPUSet — GetAvailableCPUs(P), the required-policy filter, per NUMA node of
+// the allocation (or once) takePreferredCPUs, satisfiedRequiredCPUBindPolicy.  The accumulator's exclusive seed is
+// the allocated CPUDetails after P's RefCount drop.
+__device__ __forceinline__ bool numa_alloc_pref(const NumaStatic& s, const NumaMut& m, const NumaView& vp,
+                                                const NumaPod& p, const NumaHint& aff, const CpuSet& P, NumaAlloc& a,
+                                                CpuSet& cpus) {
+  cpus = cs_zero();
+  a.res = 0;
+  const int bind = numa_pref_bind(vp, p.preferred);
+  if (bind < 0) return false;
+  if (!aff.nil && !alloc_by_hint(vp, p, aff.mask, a)) return false;
+  if (!p.cpu_bind) return true;
+  const Topo t = make_topo(s);
+  CpuSet held, avail = t.all(), seed;
+#pragma unroll
+  for (int w = 0; w < kCpuWords; ++w) {
+    held.w[w] = m.allocated[w] & ~P.w[w];
+    avail.w[w] &= ~(held.w[w] | s.reserved[w]);
+    seed.w[w] = (p.excl == KG_EXCL_PCPU_LEVEL ? m.excl_pcpu[w] : p.excl == KG_EXCL_NUMA_NODE_LEVEL ? m.excl_numa[w] : 0ull) &
+                held.w[w];
+  }
+  if (p.required != 0) avail = filter_required(t, avail, bind);
+  if (cs_count(avail) < p.needed) return false;
+  const int parts = a.res ? kNumaMax : 1;
+  for (int i = 0; i < parts; ++i) {
+    if (a.res && !((a.res >> i) & 1u)) continue;
+    const CpuSet in = a.res ? cs_and(avail, t.node_cpus(i)) : avail;
+    int num = p.needed;
+    if (a.res) {
+      num = cs_count(in);
+      const int want = (int)(a.cpu[i] / 1000);
+      if (want < num) num = want;
+    }
+    CpuSet one;
+    if (!take_preferred(t, in, P, num, bind, vp.strategy, one, p.excl, seed)) return false;
+    cpus = cs_or(cpus, one);
+  }
+  if (cs_count(cpus) != p.needed) return false;  // "not enough cpus available to satisfy request"
+  if (p.required != 0) {
+    if (bind == 2 && t.cpc > 1 && cs_count(full_core_cpus(t, cpus)) != cs_count(cpus)) return false;
+    if (bind == 3 && cs_count(first_cpu_per_core(t, cpus)) != cs_count(cpus)) return false;
+  }
+  return true;
+}
+
+// NodeNUMAResource.Score with preferredCPUs P (scoring.go:55-168): v = the node's plain view
+__device__ __forceinline__ int64_t numa_score_pref(const NumaStatic& s, const NumaMut& m, const NumaView& v,
+                                                   const NumaPod& p, const NumaParams& NP, const NumaHint& aff,
+                                                   const CpuSet& P, int64_t node_req_cpu, int64_t node_req_mem,
+                                                   int64_t node_alloc_cpu, int64_t node_alloc_mem) {
+  int64_t ac = node_alloc_cpu, am = node_alloc_mem, rc = node_req_cpu, rm = node_req_mem, pc = p.req_cpu;
+  CpuSet alloc;
+#pragma unroll
+  for (int w = 0; w < kCpuWords; ++w) alloc.w[w] = m.allocated[w];
+  if (skip_the_node(p, v.policy)) {
+    if (p.skip) return 0;
+    if (numa_pref_bind(v, p.preferred) < 0) return 0;
+    if (p.req_cpu != 0 && v.amp > 1.0) {  // scoreWithAmplifiedCPUs: GetAvailableCPUs(node, P)'s allocated CPUDetails
+      const int64_t an = (int64_t)cs_count(cs_andnot(alloc, P)) * 1000;
+      rc = rc - an + amplify(an, v.amp);
+    }
+  } else {
+    if (p.cpu_bind && !v.valid) return 0;
+    const NumaView vp = view_with_pref(v, s, P);
+    NumaAlloc a;
+    CpuSet c;
+    if (!numa_alloc_pref(s, m, vp, p, aff, P, a, c)) return 0;
+    if (a.res) {  // calculateAllocatableAndRequested: totalAllocated with the reusable cpu subtracted
+      ac = am = rc = rm = 0;
+#pragma unroll
+      for (int i = 0; i < kNumaMax; ++i)
+        if ((a.res >> i) & 1u) {
+          rc += vp.alloc_cpu[i];
+          rm += vp.alloc_mem[i];
+          ac += vp.numa_cpu[i];
+          am += vp.numa_mem[i];
+        }
+    }
+    // getAvailableCPUs with preferred = P − the pod's cpus: the allocated CPUDetails' size
+    if (p.cpu_bind) rc = amplify((int64_t)cs_count(cs_andnot(alloc, cs_andnot(P, c))) * 1000, v.amp);
+    pc = opt_cpu(v, p);
+  }
+  return numa_scorer(NP.node_strategy, NP.w_cpu, NP.w_mem, rc, rm, ac, am, pc, p.req_mem);
+}
+
+// NodeNUMAResource.Reserve with preferredCPUs P (plugin.go:375-415 → Allocate → addPodAllocation); as numa_reserve
+__device__ __forceinline__ bool numa_reserve_pref(const NumaStatic& s, NumaMut& m, const NumaView& v, const NumaPod& p,
+                                                  const NumaHint& aff, const CpuSet& P, CpuSet& cpus, NumaAlloc& rec) {
+  cpus = cs_zero();
+  rec.res = 0;
+  if (skip_the_node(p, v.policy)) return true;
+  if (p.cpu_bind && !v.valid) return false;
+  NumaAlloc a;
+  if (!numa_alloc_pref(s, m, view_with_pref(v, s, P), p, aff, P, a, cpus)) return false;
+#pragma unroll
+  for (int w = 0; w < kCpuWords; ++w) {
+    m.allocated[w] |= cpus.w[w];
+    m.excl_pcpu[w] = (m.excl_pcpu[w] & ~cpus.w[w]) | (p.excl == KG_EXCL_PCPU_LEVEL ? cpus.w[w] : 0ull);
+    m.excl_numa[w] = (m.excl_numa[w] & ~cpus.w[w]) | (p.excl == KG_EXCL_NUMA_NODE_LEVEL ? cpus.w[w] : 0ull);
+  }
+#pragma unroll
+  for (int i = 0; i < kNumaMax; ++i)
+    if ((a.res >> i) & 1u) {
+      m.alloc_cpu[i] += a.cpu[i];
+      m.alloc_mem[i] += a.mem[i];
+    }
+  m.present |= a.res;
+  rec = a;
+  return true;
+}
+
 // per-pod NUMA allocation record (kg_pods_unreserve): [0] NUMA-node mask, [1 + i] cpu, [1 + kNumaMax + i] memory
 constexpr int kNumaRecWords = 1 + 2 * kNumaMax;
 
 // resourceManager.Release → NodeAllocation.release (node_allocation.go:105-131): the pod's cpus leave the
 // allocated set (maxRefCount 1), its NUMANodeResources are subtracted with a non-negative result
-__device__ __forceinline__ void numa_release(NumaMut& m, const uint64_t* cpus, const int64_t* rec) {
+// (r6) `keep`: the cpus the node's reservations hold — a pod's cpu among them keeps RefCount 1 (the reservation's), so
+// it stays allocated with its CPUInfo (node_allocation.go:115-126)
+__device__ __forceinline__ void numa_release(NumaMut& m, const uint64_t* cpus, const int64_t* rec,
+                                             const uint64_t* keep = nullptr) {
 #pragma unroll
   for (int w = 0; w < kCpuWords; ++w) {
-    m.allocated[w] &= ~cpus[w];
-    m.excl_pcpu[w] &= ~cpus[w];  // RefCount 0: the CPUInfo and its policy are deleted
-    m.excl_numa[w] &= ~cpus[w];
+    const uint64_t gone = cpus[w] & ~(keep ? keep[w] : 0ull);
+    m.allocated[w] &= ~gone;
+    m.excl_pcpu[w] &= ~gone;  // RefCount 0: the CPUInfo and its policy are deleted
+    m.excl_numa[w] &= ~gone;
   }
 #pragma unroll
   for (int i = 0; i < kNumaMax; ++i)

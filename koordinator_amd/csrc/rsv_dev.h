@@ -38,6 +38,7 @@ namespace kg {
 constexpr int kRsvSlots = KG_MAX_RSV_SLOTS;
 constexpr uint32_t RS_AVAIL = 1u << 0, RS_ONCE = 1u << 1, RS_UNSCHED = 1u << 2;  // policy in bits 4..5
 constexpr uint32_t RS_GPU = 1u << 3;  // (ABI 13) the reservation holds GPUs: its RsvGpu row is live
+constexpr uint32_t RS_CPUS = 1u << 6;  // (ABI 15) the reservation holds a cpuset: its RsvCpu row is live
 constexpr uint32_t RP_AFFINITY = 1u << 0, RP_RESERVE = 1u << 1, RP_OPERATING = 1u << 2, RP_SEL = 1u << 3;
 constexpr int RP_POLICY_SHIFT = 8;  // flags bits 8..9: the allocate policy of a reserve / operating-mode pod
 constexpr int64_t kDefaultMilliCpu = 100, kDefaultMemory = 200ll << 20;  // schedutil.GetNonzeroRequests defaults
@@ -100,6 +101,24 @@ __device__ __forceinline__ int64_t rg_d(const RsvGpu& g, int m, int q) {
   return q == 0 ? (int64_t)g.dcore[m] : (q == 1 ? g.dmem[m] : (int64_t)g.dratio[m]);
 }
 
+// (ABI 15) One reservation's cpuset (NodeNUMAResource): `r` = GetAllocatedCPUSet(node, reservation UID), `u` = the union
+// of its assigned pods' cpusets.  RestoreReservation's reserved cpus are r − u (nodenumaresource/reservation.go:76-113).
+// 64 B per slot, [cap][kRsvSlots]; read only for a cpuset-capable pod nominated into an RS_CPUS slot, and by Unreserve.
+struct RsvCpu {
+  uint64_t r[kCpuWords];
+  uint64_t u[kCpuWords];
+};
+static_assert(sizeof(RsvCpu) == 64, "RsvCpu layout");
+struct RsvCpuNode {  // one node's slots (the upsert's scatter row)
+  RsvCpu s[kRsvSlots];
+};
+__device__ __forceinline__ CpuSet rsv_reserved_cpus(const RsvCpu& c) {
+  CpuSet p;
+#pragma unroll
+  for (int w = 0; w < kCpuWords; ++w) p.w[w] = c.r[w] & ~c.u[w];
+  return p;
+}
+
 // DeviceShare + ElasticQuota context of the C5 pass (ds = nullptr: no DeviceShare in the profile; nq = 0: no quotas)
 struct RsvExt {
   const DsNode* __restrict__ ds;       // [cap] node devices (deviceUsed updated by Reserve)
@@ -139,6 +158,8 @@ struct RsvExt {
   RsvGpu* __restrict__ rgpu;           // [cap][kRsvSlots]
   const RsvPod* __restrict__ rpods;    // [pods]
   const int32_t* __restrict__ rsv_n;   // [cap]
+  // (ABI 15) reservations holding cpusets (rcpu = nullptr: none in the cluster, or NodeNUMAResource / Reservation off)
+  RsvCpu* __restrict__ rcpu;           // [cap][kRsvSlots]
 };
 // pod j's zone sums (double-buffered by parity: group_pre(j) accumulates, rsv_select(j) clears j + 1's)
 __device__ __forceinline__ ZoneSums zone_sums(const RsvExt& X, int64_t j) {
@@ -460,13 +481,13 @@ __device__ __forceinline__ RsvOut rsv_eval_node(const DevTable& T, const RsvNode
     // from (plugin.go:333-380: "no relevant Reservation information" for the others)
     sat &= dsok;
   }
+  int64_t nsc = 0;        // NodeNUMAResource's Score without preferred cpus
+  NumaHint naff{0, 1, 0, 0};
   if (X.ns && np) {  // NodeNUMAResource Filter + Score on the restored NodeInfo; Reserve reuses the stored affinity
     const NumaView nv = make_view(X.ns + i, X.nm + i, X.NP);
-    int64_t sc = 0;
-    NumaHint aff;
-    if (!numa_eval(nv, *np, X.NP, r.req_cpu, r.req_mem, r.alloc_cpu, r.alloc_mem, sc, aff)) return o;
-    if (X.NP.score) t += sc * X.NP.weight;
-    if (X.aff) X.aff[i] = aff.nil ? 0x100u : aff.mask;
+    if (!numa_eval(nv, *np, X.NP, r.req_cpu, r.req_mem, r.alloc_cpu, r.alloc_mem, nsc, naff)) return o;
+    if (X.NP.score) t += nsc * X.NP.weight;
+    if (X.aff) X.aff[i] = naff.nil ? 0x100u : naff.mask;
   }
   if (df) {  // BalancedAllocation on the restored NodeInfo; the two normalised raw Scores
     if (X.DF.bal) t += X.DF.w_bal * balanced_score(r.alloc_cpu, r.alloc_mem, r.req_cpu, r.req_mem, p.req_cpu, p.req_mem, X.DF);
@@ -528,6 +549,17 @@ __device__ __forceinline__ RsvOut rsv_eval_node(const DevTable& T, const RsvNode
     for (int s = 0; s < kRsvSlots; ++s)
       if (s == pick) raw = ssc[s];
     o.raw = raw;
+    // (ABI 15) NodeNUMAResource Score runs after the PreScore nomination: a cpuset-capable pod nominated into a
+    // reservation holding cpus gets its reserved cpus as preferredCPUs (getReservationReservedCPUs, plugin.go:513-535)
+    if (kExt && X.rcpu && X.ns && np && X.NP.score && np->allow && pick >= 0 && (rn.meta[pick] & RS_CPUS)) {
+      const CpuSet P = rsv_reserved_cpus(X.rcpu[(size_t)i * kRsvSlots + pick]);
+      if (cs_count(P) > 0) {
+        const NumaView nv = make_view(X.ns + i, X.nm + i, X.NP);
+        const int64_t psc = numa_score_pref(X.ns[i], X.nm[i], nv, *np, X.NP, naff, P, r.req_cpu, r.req_mem,
+                                            r.alloc_cpu, r.alloc_mem);
+        o.base += (psc - nsc) * X.NP.weight;
+      }
+    }
   }
   if (dsr && X.DP.score) {  // Score (scoring.go:34-89): the nominated reservation's, else the node view's
     const DsNode& d = X.ds[i];
@@ -731,13 +763,20 @@ __device__ __forceinline__ bool rsv_reserve(const DevTable& T, RsvNode* __restri
   CpuSet cpus = cs_zero();
   NumaAlloc rec;
   rec.res = 0;
+  const int32_t nom_slot = (int32_t)(v & 7) - 1;  // the slot PreScore nominated on the winner (-1: none)
   if (NUMA && X.ns) {
     const NumaStatic nsw = X.ns[w];
     nmw = X.nm[w];
     const NumaView nv = make_view(&nsw, &nmw, X.NP);
     const uint32_t a = X.aff[w];
     const NumaHint aff{a & 0xFFu, (int)((a >> 8) & 1u), 0, 0};
-    if (!numa_reserve(nsw, nmw, nv, X.npods[j], aff, cpus, rec)) {
+    // (ABI 15) the nominated reservation's reserved cpus are Reserve's preferredCPUs too (getResourceOptions)
+    CpuSet P = cs_zero();
+    if (X.rcpu && nom_slot >= 0 && X.npods[j].allow && (RN[w].meta[nom_slot] & RS_CPUS))
+      P = rsv_reserved_cpus(X.rcpu[(size_t)w * kRsvSlots + nom_slot]);
+    const bool ok = cs_count(P) > 0 ? numa_reserve_pref(nsw, nmw, nv, X.npods[j], aff, P, cpus, rec)
+                                    : numa_reserve(nsw, nmw, nv, X.npods[j], aff, cpus, rec);
+    if (!ok) {
       if (X.out_minors) X.out_minors[j] = 0;
       return false;
     }
@@ -822,6 +861,12 @@ __device__ __forceinline__ bool rsv_reserve(const DevTable& T, RsvNode* __restri
     // (ABI 13) the reservation's allocated GPUs: the pod's allocation on its minors
     if (DS && X.rgpu && gpu_minors > 0 && (RN[w].meta[slot] & RS_GPU))
       rsv_gpu_assign(X.rgpu[(size_t)w * kRsvSlots + slot], ds_instance(X.ds[w], X.dpods[j]), gpu_minors, +1);
+    // (ABI 15) an assigned pod's cpus leave the reservation's reserved cpus at the next RestoreReservation
+    if (NUMA && X.rcpu && X.ns && (RN[w].meta[slot] & RS_CPUS)) {
+      RsvCpu& rc = X.rcpu[(size_t)w * kRsvSlots + slot];
+#pragma unroll
+      for (int q = 0; q < kCpuWords; ++q) rc.u[q] |= cpus.w[q];
+    }
   }
   slot_out = slot;
   KG_LANE_SUB(diag_j, 5);

@@ -200,6 +200,13 @@ class Engine:
         check(self.lib, self.lib.kg_nodes_read_reservation_gpus(self.h, ptr(out)))
         return out
 
+    def read_reservation_cpus(self):
+        """(ABI 15) the reservation slots' cpus_assigned, uint64[n, KG_MAX_RSV_SLOTS, 4], from the device
+        (kg_nodes_read_reservation_cpus)."""
+        out = np.zeros((self.num_nodes, abi.MAX_RSV_SLOTS, abi.MAX_CPUS // 64), dtype=np.uint64)
+        check(self.lib, self.lib.kg_nodes_read_reservation_cpus(self.h, ptr(out)))
+        return out
+
     def read_pod_groups(self, zone: bool = False):
         """(ABI 12) per node and match group: (pods matching, required anti-affinity terms, symmetric weight) — and,
         with zone, the zone-keyed terms' (anti-affinity, symmetric weight) — int32[n, KG_MAX_MATCH_GROUPS] each, from

@@ -551,6 +551,52 @@ def make_shipped_cluster(n_nodes: int, seed: int = BASE_SEED + 13) -> tuple:
     return cluster, numa, dev, rsv
 
 
+def add_cpuset_reservations(numa: np.ndarray, rsv: np.ndarray, frac: float = 0.3,
+                            seed: int = BASE_SEED + 25) -> int:
+    """(ABI 15) Reservations holding cpusets, in place: `frac` of the reservations with a whole-core cpu allocatable on
+    nodes with a valid topology get a reserve pod cpuset of that many cpus — whole free cores (neither allocated nor
+    kubelet-reserved) at random positions — added to the node's NodeAllocation (allocated cpus; allocatedResources cpu
+    of their NUMA nodes, as make_numa_cluster accounts bound cpuset pods).  The reservation's assigned pods hold the
+    first ⌊assigned·|R|/4⌋ of those cpus (cpus_assigned, RefCount 2 in NodeAllocation), and a tenth of the reservations
+    hand one more single cpu to them (a half core stays reserved, the FullPCPUs edge of takePreferredCPUs).  Returns the
+    number of cpuset reservations."""
+    rng = np.random.default_rng(seed)
+    made = 0
+    for i in np.nonzero((rsv["n"] > 0) & (numa["has_topology"] != 0))[0]:
+        total = int(numa["sockets"][i] * numa["nodes_per_socket"][i] * numa["cores_per_node"][i] *
+                    numa["cpus_per_core"][i])
+        cpc = int(numa["cpus_per_core"][i])
+        per_numa = total // max(int(numa["num_numa"][i]), 1)
+        for s in range(int(rsv["n"][i])):
+            need = int(rsv["allocatable_cpu"][i, s]) // 1000
+            if need == 0 or need * 1000 != rsv["allocatable_cpu"][i, s] or need % cpc or rng.random() >= frac:
+                continue
+            held = np.zeros(total, dtype=bool)
+            for w in range(4):
+                a = int(numa["allocated_cpus"][i, w]) | int(numa["reserved_cpus"][i, w])
+                for b in range(64):
+                    if 64 * w + b < total and (a >> b) & 1:
+                        held[64 * w + b] = True
+            free_cores = np.flatnonzero(~held.reshape(-1, cpc).any(axis=1))
+            if len(free_cores) < need // cpc:
+                continue
+            cores = np.sort(rng.choice(free_cores, need // cpc, replace=False))
+            cpus = (cores[:, None] * cpc + np.arange(cpc)[None, :]).ravel()
+            for c in cpus:
+                rsv["cpus"][i, s, c // 64] |= np.uint64(1) << np.uint64(c % 64)
+                numa["allocated_cpus"][i, c // 64] |= np.uint64(1) << np.uint64(c % 64)
+            z = int(numa["num_numa"][i])
+            if z > 0:
+                numa["numa_alloc_cpu"][i, :z] += np.bincount(cpus // per_numa, minlength=z)[:z] * 1000
+            k = int(rsv["assigned"][i, s]) * len(cpus) // 4
+            if k > 0 and rng.random() < 0.1:
+                k += 1
+            for c in cpus[:min(k, len(cpus))]:
+                rsv["cpus_assigned"][i, s, c // 64] |= np.uint64(1) << np.uint64(c % 64)
+            made += 1
+    return made
+
+
 def make_shipped_pods(n_pods: int, seed: int = BASE_SEED + 14) -> np.ndarray:
     """The shipped profile's queue: make_numa_pods' LSR / LSE cpuset and LS / BE pods, 30 % also requesting GPU share
     (make_gpu_pods), 20 % owned by reservation owner groups (make_rsv_pods) and 80 % in one of N_QUOTAS quotas."""
