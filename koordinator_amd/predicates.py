@@ -400,7 +400,12 @@ class PodGroupTable:
         ScheduleAnyway, on its owners' selector (buildDefaultConstraints) — flagged KG_SPREAD_SYSTEM_DEFAULT, so scoring
         ignores no node (requireAllTopologies false)."""
         r = pod[0] if pod.ndim else pod
-        if not spread and system_default_selector is not None:
+        # buildDefaultConstraints returns no constraints when DefaultSelector is empty (selector.Empty(): a pod
+        # without owners — no matchLabels, no matchExpressions)
+        sel = system_default_selector
+        empty = sel is not None and not (sel.get("matchLabels") or sel.get("matchExpressions") or
+                                         {k: v for k, v in sel.items() if k not in ("matchLabels", "matchExpressions")})
+        if not spread and sel is not None and not empty:
             spread = [dict(maxSkew=3, whenUnsatisfiable="ScheduleAnyway", labelSelector=system_default_selector,
                            topologyKey=HOSTNAME, _system=True),
                       dict(maxSkew=5, whenUnsatisfiable="ScheduleAnyway", labelSelector=system_default_selector,

@@ -1356,3 +1356,24 @@ void or_numa_rsv_reserved_flat(const kg_node_reservations* r, int s, uint64_t* o
   const or_cpuset c = or_numa_rsv_reserved(r, s);
   for (int w = 0; w < OR_CPUSET_WORDS; w++) out[w] = c.w[w];
 }
+
+/* (r6) The NodeAllocation of node i as a kg_node_numa row's mutable fields (allocated cpus, their exclusive policies,
+ * allocatedResources), written over `row`: what a caller re-sends with a rewritten NodeResourceTopology
+ * (topology_eventhandler.go:62-113 updates TopologyOptions; the NodeAllocation stays). */
+void or_numa_state_export(const void* states, int64_t i, kg_node_numa* row) {
+  const or_numa_node* s = &((const or_numa_node*)states)[i];
+  for (int w = 0; w < OR_CPUSET_WORDS; w++) {
+    row->allocated_cpus[w] = s->allocated.w[w];
+    row->exclusive_pcpu_cpus[w] = s->excl_pcpu.w[w];
+    row->exclusive_numa_cpus[w] = s->excl_numa.w[w];
+  }
+  for (int k = 0; k < KG_MAX_NUMA; k++) {
+    row->numa_alloc_cpu[k] = s->numa_alloc_cpu[k];
+    row->numa_alloc_mem[k] = s->numa_alloc_mem[k];
+  }
+}
+
+/* (r6) Re-initialise node i's state from a row (the NodeResourceTopology / NodeAllocation upsert) */
+void or_numa_state_set(void* states, int64_t i, const kg_node_numa* row) {
+  or_numa_node_init(&((or_numa_node*)states)[i], row);
+}

@@ -51,6 +51,10 @@ def lib():
         L.or_numa_reserve_rsv_flat.restype = i
         L.or_numa_rsv_reserved_flat.argtypes = [vp, i, vp]
         L.or_numa_rsv_reserved_flat.restype = None
+        L.or_numa_state_export.argtypes = [vp, i64, vp]
+        L.or_numa_state_export.restype = None
+        L.or_numa_state_set.argtypes = [vp, i64, vp]
+        L.or_numa_state_set.restype = None
         L.or_la_node_terms.argtypes = [vp, vp, vp, ctypes.c_int64, vp, ctypes.c_int64, vp]
         L.or_la_node_terms.restype = None
         L.or_estimate_node.argtypes = [vp, i]
@@ -487,6 +491,18 @@ def numa_states(nodes_numa: np.ndarray) -> np.ndarray:
     buf = np.zeros(max(len(nodes_numa), 1) * size, dtype=np.uint8)
     lib().or_numa_states_init(p(nodes_numa), len(nodes_numa), p(buf))
     return buf
+
+
+def numa_state_export(buf: np.ndarray, i: int, row: np.ndarray) -> np.ndarray:
+    """(r6) kg_node_numa row `row` (static fields) with node i's current NodeAllocation from the oracle state."""
+    out = np.ascontiguousarray(np.array(row, dtype=abi.NODE_NUMA_DTYPE).reshape(1))
+    lib().or_numa_state_export(p(buf), int(i), p(out))
+    return out
+
+
+def numa_state_set(buf: np.ndarray, i: int, row: np.ndarray):
+    """(r6) node i's oracle state re-initialised from a kg_node_numa row (an upsert)."""
+    lib().or_numa_state_set(p(buf), int(i), p(np.ascontiguousarray(np.array(row, dtype=abi.NODE_NUMA_DTYPE).reshape(1))))
 
 
 def numa_state_read(buf: np.ndarray, n: int):

@@ -218,3 +218,31 @@ def test_gpu_holdings_validated_at_upsert():
         bad["gpu_alloc"][0, 0, 0] = (-1, 0, 0)
         with pytest.raises(abi.KoordGPUError):
             e.upsert_reservations(bad, idx=np.array([0], dtype=np.int32))
+
+
+@pytest.mark.gpu
+def test_read_reservation_gpus_zero_after_reupsert_without_gpus():
+    """ Re-upserting a node whose reservations no longer hold GPUs zeroes its rows: the read-back is zero
+    there; a profile without Reservation refuses the read (KG_E_INVALID, as koordgpu.h documents)."""
+    cfg = F.build_config(profile=PROFILE)
+    cluster, dev, rsv, pods, _ = workload(60, 10, 62, frac=1.0, quotas=False)
+    held = np.flatnonzero((rsv["gpu_minors"] != 0).any(axis=1))
+    assert held.size > 0
+    with Engine(cfg, cluster.n) as e:
+        synth.load_c5_into(e, cluster, dev, rsv, None)
+        before = e.read_reservation_gpus()
+        i = int(held[0])
+        assert before[i].any() or not rsv["gpu_allocated"][i].any()
+        row = rsv[i:i + 1].copy()
+        row["gpu_minors"] = 0
+        row["gpu_alloc"] = 0
+        row["gpu_allocated"] = 0
+        e.upsert_reservations(row, idx=np.array([i], dtype=np.int32))
+        after = e.read_reservation_gpus()
+        assert not after[i].any()
+        others = np.arange(cluster.n) != i
+        assert np.array_equal(after[others], before[others])
+    no_rsv = F.Profile(filter=(F.NODE_RESOURCES_FIT, F.DEVICE_SHARE), score={F.NODE_RESOURCES_FIT: 1})
+    with Engine(F.build_config(profile=no_rsv), cluster.n) as e:
+        with pytest.raises(abi.KoordGPUError):
+            e.read_reservation_gpus()

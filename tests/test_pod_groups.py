@@ -263,6 +263,22 @@ def test_oracle_system_default_constraints_ignore_no_node():
     assert (int(node[0]), int(score[0])) == (1, 299)
 
 
+def test_system_default_without_owners_adds_no_constraints():
+    """ buildDefaultConstraints returns nil when DefaultSelector is empty (a pod without owners): the
+    system defaults add no constraint, so the pod is not spread against every pod of the namespace."""
+    t = PodGroupTable()
+    for sel in ({}, {"matchLabels": {}}, {"matchLabels": {}, "matchExpressions": []}):
+        pod = F.make_pod(requests={"cpu": "1m", "memory": "1Mi"})
+        t.fill_pod(pod, {"app": "web"}, "default", system_default_selector=sel)
+        assert int(pod["n_spread"][0]) == 0 and not pod["spread_flags"].any()
+    pod = F.make_pod(requests={"cpu": "1m", "memory": "1Mi"})
+    t.fill_pod(pod, {"app": "web"}, "default", system_default_selector={"matchLabels": {"app": "web"}})
+    assert int(pod["n_spread"][0]) == 2
+    cl, preds = _zoned(3, [1, 2, 0])
+    node, _, _, _ = _run_oracle(F.build_config(profile=SPREAD_ONLY), cl, F.make_pod(requests={"cpu": "1m"}), preds)
+    assert node[0] == 0  # no constraint: the equal nodes tie, lowest index
+
+
 def test_oracle_hard_spread_round_robin():
     """maxSkew 1 on four equal nodes: each pod lands on an emptiest node, lowest index first."""
     t = PodGroupTable()
