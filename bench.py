@@ -24,9 +24,11 @@ bracketing every launch on its own stream, kg_profile_enable) — the roofline's
 with the committed oracle fixture of the whole queue (tests/golden/c3_queue.npz); (3) the CPU baseline (the oracle, the same
 algorithm in C) is timed on a bounded sample with 16 threads and with 1 thread.
 
-N>1 (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): the node table is replicated
-and its evaluation sharded over ranks; candidate lists are exchanged with RCCL all-gather over xGMI.  Total
-work is fixed as N grows → "scaling": "strong".
+N>1 (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): the node table is replicated on every
+rank; with --multi-rank shard its evaluation is sharded over ranks and candidate lists are exchanged with an RCCL
+all-gather over xGMI each round; with replica every rank schedules the whole queue on its own table; auto (default)
+lets the engine choose from the DESIGN §6 model (replicas below 262,144 nodes for the round profiles).  Total work is
+fixed as N grows → "scaling": "strong".
 
 Prints ONE JSON line on rank 0 (contract in the task statement).
 """
@@ -84,6 +86,9 @@ def parse():
                     help="PMC summary (scripts/pmc_summary.py) of the same workload: per-launch HBM bytes "
                          "(default profiles/r02/traffic_<workload>.json)")
     ap.add_argument("--check", type=int, default=None, help="verify the first N placements against the oracle")
+    ap.add_argument("--multi-rank", choices=("auto", "shard", "replica"), default="auto",
+                    help="N>1: node-sharded evaluation with a per-round exchange, every rank a replica of one GPU, or "
+                         "the engine's choice from its model (DESIGN §6)")
     ap.add_argument("--single-pod-calls", type=int, default=200, help="single-pod scheduling calls timed one by one "
                     "after the timed region (0 = skip)")
     return ap.parse_args()
@@ -324,7 +329,7 @@ def main():
                                    F.RESERVATION: 5000})
         la = F.LoadAwareSchedulingArgs(filter_expired_node_metrics=False, node_metric_expiration_seconds=300)
     cfg = framework.build_config(batch_pods=args.batch, pods_per_wave=args.pods_per_wave, device_id=d.local_rank,
-                                 profile=profile, pipeline_depth=args.depth, la=la)
+                                 profile=profile, pipeline_depth=args.depth, la=la, multi_rank=args.multi_rank)
     work = Work(wl, args.nodes, cfg)
     cluster = work.cluster
     total = args.steps * args.pods_per_step
@@ -346,6 +351,7 @@ def main():
             ew.schedule_staged(0, len(wp))
 
     e = engine()
+    shard_ranks, replica_ranks = e.ranks  # (r6) the engine's resolved multi-rank mode
     e.stage(pods)
     d.barrier()
     t0 = time.perf_counter()
@@ -464,6 +470,15 @@ def main():
         if args.cpu_nproc and nproc > threads:  # §8d: the Parallelizer widened to every host thread as well
             mn, dtn, _ = cpu_sample(work, pods[:total], args.cpu_seconds / 2, nproc)
             cpu["nproc_threads"] = {"value": mn / dtn, "threads": nproc, "sample_pods": mn}
+        elif nproc > threads:
+            # (r6) the GPU box gives one GPU a 16-thread CPU share (nproc shows the whole machine), so the default run
+            # does not start nproc threads; the nproc-wide Parallelizer is bounded above by linear scaling of the
+            # 16-thread rate (measured 1 → 16 threads: the efficiency below)
+            cpu["nproc_threads_linear_bound"] = {
+                "value": m / dt * nproc / threads, "threads": nproc,
+                "note": "upper bound: the %d-thread rate scaled linearly to nproc (the measured 1 -> %d-thread "
+                        "efficiency is %.2f); --cpu-nproc measures it when the box's CPU share allows"
+                        % (threads, threads, (m / dt) / (m1 / dt1) / threads)}
 
     tfile = args.traffic_file or next((f for f in (os.path.join(ROOT, "profiles", r, f"traffic_{wl}.json")
                                                    for r in ("r05", "r04", "r03", "r02")) if os.path.exists(f)),
@@ -499,6 +514,19 @@ def main():
                                         if active_s > 0 else None),
                   "note": "resolver_share = in-kernel active time / wall time of the timed steps (the serial chain "
                           "sets the period when it is near 1); eval_stream_share = (eval + merge) / (depth x period)"}
+    if d.world == 1:
+        parallelism = "1 GPU"
+    elif replica_ranks > 1:
+        parallelism = ("replicas x%d (multi_rank %s: every rank schedules the whole queue on its own full table, no "
+                       "exchange; the sharding model of DESIGN §6 predicts no gain at %d nodes)"
+                       % (d.world, args.multi_rank, cluster.n))
+    elif wl in ("stock", "stockz"):
+        parallelism = ("replicas x%d (per-pod exact pass: every rank evaluates its full replica, no exchange)" % d.world)
+    elif rsv_path:
+        parallelism = ("node-sharded exact rounds x%d (replicated table; per round an RCCL all-gather of the pod "
+                       "statistics and of the merged records)" % shard_ranks)
+    else:
+        parallelism = "node-sharded x%d (replicated table, RCCL all-gather)" % shard_ranks
     if d.rank == 0:
         pods_s = total / elapsed
         desc = {
@@ -560,12 +588,7 @@ def main():
             "data": "synthetic (SURVEY §8d generator, seed %d)" % work.seed,
             "config": {"workload": desc, "nodes": cluster.n, "pods": total, "batch_pods": args.batch,
                        "pods_per_wave": args.pods_per_wave, "pipeline_depth": args.depth or "default",
-                       "parallelism": (("replicas x%d (per-pod exact pass: every rank evaluates its full replica, "
-                                        "no exchange)" % d.world) if wl in ("stock", "stockz") else
-                                       ("node-sharded exact rounds x%d (replicated table; per round an RCCL "
-                                        "all-gather of the pod statistics and of the merged records)" % d.world)
-                                       if rsv_path else
-                                       "node-sharded x%d (replicated table, RCCL all-gather)" % d.world)},
+                       "parallelism": parallelism},
             "node_evals_per_sec": pods_s * cluster.n,
             "placed": placed,
             "device_rounds": rounds,

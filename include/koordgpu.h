@@ -236,8 +236,13 @@ typedef struct kg_config {
   int64_t interpod_score;                      /* InterPodAffinity at Score (min-max NormalizeScore)             */
   int64_t weight_interpod;
   int64_t hard_pod_affinity_weight;            /* InterPodAffinityArgs.HardPodAffinityWeight (default 1)         */
-  int64_t reserved[2];
+  /* (ABI 15) several ranks (kg_engine_create n_ranks > 1): KG_MULTI_RANK_SHARD evaluates a node shard per rank and
+   * exchanges each round's candidates; KG_MULTI_RANK_REPLICA makes every rank a replica of one GPU (the whole table, no
+   * exchange, the same placements); AUTO shards only tables large enough for it to pay. */
+  int64_t multi_rank_mode;
+  int64_t reserved[1];
 } kg_config;
+enum { KG_MULTI_RANK_AUTO = 0, KG_MULTI_RANK_SHARD = 1, KG_MULTI_RANK_REPLICA = 2 };
 
 /* One node (snapshot index = position given by the caller). */
 typedef struct kg_node {
@@ -612,6 +617,9 @@ int kg_pods_schedule_staged(kg_engine* e, int64_t first, int64_t count, kg_stats
 int kg_results_fetch(kg_engine* e, int64_t first, int64_t count, int32_t* out_node_idx, int64_t* out_score);
 
 int64_t kg_engine_num_nodes(const kg_engine* e);
+/* (ABI 15) The ranks the engine shards node evaluation over (1 = unsharded) and, for a replica, the ranks of the
+ * caller's group it replicates (1 otherwise): kg_config.multi_rank_mode resolved at kg_engine_create. */
+int kg_engine_ranks(const kg_engine* e, int64_t* shard_ranks, int64_t* replica_ranks);
 /* Reads the DEVICE copy of the mutable node state: NodeInfo.Requested{cpu,mem}, NonZeroRequested{cpu,mem},
  * pod count and the LoadAware estimated usage Σ EstimatePod over the assign cache (all pods / prod pods).
  * Any output may be NULL. */

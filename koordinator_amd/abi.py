@@ -44,6 +44,7 @@ PROF_KINDS = 16
 PROF_NAMES = {0: "eval_round", 1: "merge_round", 2: "resolve_round", 3: "ds_max_round", 4: "ds_norm_reduce",
               5: "rsv_eval", 6: "rsv_select", 7: "rsv_apply"}
 MAX_NUMA, MAX_CPUS = 4, 256
+MULTI_RANK = {"auto": 0, "shard": 1, "replica": 2}  # (ABI 15) kg_config.multi_rank_mode
 QOS = {"": 0, "LSE": 1, "LSR": 2, "LS": 3, "BE": 4, "SYSTEM": 5}
 BIND = {"": 0, "Default": 1, "FullPCPUs": 2, "SpreadByPCPUs": 3, "ConstrainedBurst": 4}
 EXCL = {"": 0, "None": 0, "PCPULevel": 1, "NUMANodeLevel": 2}  # CPUExclusivePolicy
@@ -110,7 +111,7 @@ CONFIG_DTYPE = np.dtype([
     _i64("image_score"), _i64("weight_image"),
     _i64("spread_filter"), _i64("spread_score"), _i64("weight_spread"),
     _i64("interpod_filter"), _i64("interpod_score"), _i64("weight_interpod"), _i64("hard_pod_affinity_weight"),
-    _i64("reserved", 2),
+    _i64("multi_rank_mode"), _i64("reserved", 1),
 ])
 
 NODE_DTYPE = np.dtype([
@@ -214,7 +215,7 @@ EXPORTED_SYMBOLS = (
     "kg_nodes_numa_upsert", "kg_nodes_read_numa", "kg_results_fetch_cpusets", "kg_pods_evaluate_numa",
     "kg_nodes_device_upsert", "kg_nodes_read_device", "kg_results_fetch_devices", "kg_pods_evaluate_device",
     "kg_quotas_set", "kg_quotas_read", "kg_nodes_reservation_upsert", "kg_nodes_read_reservations",
-    "kg_nodes_read_reservation_gpus", "kg_nodes_read_reservation_cpus",
+    "kg_nodes_read_reservation_gpus", "kg_nodes_read_reservation_cpus", "kg_engine_ranks",
     "kg_results_fetch_reservations", "kg_profile_enable", "kg_profile_read", "kg_loopback_create",
     "kg_loopback_destroy", "kg_engine_create_loopback", "kg_pods_unreserve", "kg_engine_set_clock",
     "kg_node_pods_metric_set", "kg_debug_numa_merge", "kg_pods_evaluate_reservation", "kg_nodes_predicates_upsert",
@@ -297,6 +298,7 @@ def load_library(path: str | None = None):
         "kg_nodes_read_reservations": (i, [vp, vp, vp, vp]),
         "kg_nodes_read_reservation_gpus": (i, [vp, vp]),
         "kg_nodes_read_reservation_cpus": (i, [vp, vp]),
+        "kg_engine_ranks": (i, [vp, vp, vp]),
         "kg_results_fetch_reservations": (i, [vp, i64, i64, vp]),
         "kg_profile_enable": (i, [vp, i]),
         "kg_profile_read": (i, [vp, vp, vp]),

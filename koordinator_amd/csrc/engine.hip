@@ -3426,6 +3426,7 @@ struct kg_engine {
   DevBuf<RsvGpu> rsv_g;                         // (ABI 13) [cap][kRsvSlots] GPU holdings, allocated at the first GPU slot
   std::vector<uint8_t> rsv_gnode;               // per node: it has an RS_GPU slot
   int64_t rgpu_nodes = 0;                       // nodes with an RS_GPU slot (> 0 routes queues to the per-pod pass)
+  int replica_ranks = 1;                        // (r6) ranks of the caller's group when this engine runs as a replica
   DevBuf<RsvCpu> rsv_c;                         // (ABI 15) [cap][kRsvSlots] cpusets, allocated at the first cpu slot
   std::vector<uint8_t> rsv_cnode;               // per node: it has an RS_CPUS slot
   int64_t rcpu_nodes = 0;                       // nodes with an RS_CPUS slot (> 0 routes queues to the per-pod pass)
@@ -5232,6 +5233,10 @@ int kg_nccl_unique_id(void* out128) {
   return 0;
 }
 
+// (r6) auto multi-rank mode: the smallest tables worth sharding (DESIGN.md §6 model)
+constexpr int64_t kShardMinNodes = 262144;      // round profiles: one GPU's wide pass > exchange + second merge
+constexpr int64_t kShardMinNodesExact = 32768;  // batched exact rounds of NodeNUMAResource / DeviceShare profiles
+
 static int engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank, int n_ranks, const void* nccl_id,
                          kg_loopback* lb, kg_engine** out, kg_exchange_fn xfn = nullptr, void* xuser = nullptr) {
   if (!out) return fail(KG_E_INVALID, "out is NULL");
@@ -5331,10 +5336,27 @@ static int engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank,
               c.image_score || e->grp_on;
   e->def_score = c.taint_score || c.affinity_score;
   e->exact_on = e->rsv_on || (e->numa_on && e->ds_on) || e->def_on;
-  // Exact profiles (Reservation, NodeNUMAResource + DeviceShare, the upstream defaults) on several ranks run as
-  // replicas: every rank evaluates its full replica of the table and resolves the same FIFO order, so no exchange is
-  // needed and every rank holds the same placements (the exact rounds' stop rule reads the round-start
-  // values of the modified rows, which a node-sharded pass would hold on another rank only).
+  // (r6) Several ranks: node-sharded evaluation with a per-round exchange, or every rank a replica of one GPU (its own
+  // full table, the same FIFO resolve, no exchange).  The replicated single-wave resolver bounds the period at any
+  // rank count, and sharding adds the all-gather and a second merge to the critical cycle (DESIGN.md §6, r5 numbers),
+  // so it pays only where one GPU's wide pass is long: auto shards the round profiles from kShardMinNodes nodes and
+  // the batched exact rounds of NodeNUMAResource / DeviceShare profiles from kShardMinNodesExact.  Either way every
+  // rank holds the same placements.
+  if (c.multi_rank_mode < KG_MULTI_RANK_AUTO || c.multi_rank_mode > KG_MULTI_RANK_REPLICA)
+    return bail(fail(KG_E_INVALID, "multi_rank_mode %lld", (long long)c.multi_rank_mode));
+  if (n_ranks > 1) {
+    const bool heavy_exact = e->exact_on && !e->grp_on && (e->numa_on || e->ds_on);
+    const bool shard = c.multi_rank_mode == KG_MULTI_RANK_SHARD ||
+                       (c.multi_rank_mode == KG_MULTI_RANK_AUTO &&
+                        capacity_nodes >= (e->exact_on ? (heavy_exact ? kShardMinNodesExact : INT64_MAX) : kShardMinNodes));
+    if (!shard) {  // a replica: the engine of one GPU (no collective, no exchange)
+      e->replica_ranks = n_ranks;
+      e->rank = rank = 0;
+      e->n_ranks = n_ranks = 1;
+      lb = nullptr;
+      xfn = nullptr;
+    }
+  }
   e->DF = DefParams{(int32_t)(c.taint_filter != 0), (int32_t)(c.taint_score != 0), (int32_t)c.weight_taint,
                     (int32_t)(c.affinity_filter != 0), (int32_t)(c.affinity_score != 0), (int32_t)c.weight_affinity,
                     (int32_t)(c.balanced_score != 0), (int32_t)c.weight_balanced,
@@ -5514,6 +5536,13 @@ static int engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank,
   // deltas — the node usage vanished from la_used (GPUTEST_r03, test_schedule_parity_round_shapes[16-4]).
   if (hipStreamSynchronize(e->stream) != hipSuccess) return bail(fail(KG_E_DEVICE, "engine initialisation"));
   *out = e;
+  return 0;
+}
+
+int kg_engine_ranks(const kg_engine* e, int64_t* shard_ranks, int64_t* replica_ranks) {
+  if (!e) return fail(KG_E_INVALID, "engine is NULL");
+  if (shard_ranks) *shard_ranks = e->n_ranks;
+  if (replica_ranks) *replica_ranks = e->replica_ranks;
   return 0;
 }
 

@@ -308,6 +308,13 @@ class Engine:
 
     # -- introspection -----------------------------------------------------------------------------------
     @property
+    def ranks(self) -> tuple:
+        """(ABI 15) (ranks node evaluation is sharded over, ranks this engine replicates) — kg_engine_ranks."""
+        s, r = ctypes.c_int64(), ctypes.c_int64()
+        check(self.lib, self.lib.kg_engine_ranks(self.h, ctypes.byref(s), ctypes.byref(r)))
+        return int(s.value), int(r.value)
+
+    @property
     def num_nodes(self) -> int:
         return int(self.lib.kg_engine_num_nodes(self.h))
 

@@ -92,8 +92,10 @@ def build_config(la: LoadAwareSchedulingArgs | None = None, fit: NodeResourcesFi
                  profile: Profile | None = None, batch_pods: int = 32, pods_per_wave: int = 8,
                  device_id: int = -1, numa: NodeNUMAResourceArgs | None = None,
                  deviceshare: DeviceShareArgs | None = None, pipeline_depth: int = 0,
-                 balanced_resources: tuple = ("cpu", "memory"), hard_pod_affinity_weight: int = 1) -> np.ndarray:
-    """kg_config of a profile.  balanced_resources: NodeResourcesBalancedAllocationArgs.resources (v1beta2 default
+                 balanced_resources: tuple = ("cpu", "memory"), hard_pod_affinity_weight: int = 1,
+                 multi_rank: str = "auto") -> np.ndarray:
+    """kg_config of a profile.  multi_rank (ABI 15): "shard" / "replica" / "auto" — how an engine of several ranks
+    splits the work (kg_config.multi_rank_mode).  balanced_resources: NodeResourcesBalancedAllocationArgs.resources (v1beta2 default
     cpu + memory, weight 1 each; the weights do not enter the two-resource std).  hard_pod_affinity_weight:
     InterPodAffinityArgs.HardPodAffinityWeight (v1beta2 default 1)."""
     la = la or LoadAwareSchedulingArgs()
@@ -161,6 +163,7 @@ def build_config(la: LoadAwareSchedulingArgs | None = None, fit: NodeResourcesFi
     r["interpod_score"] = int(INTER_POD_AFFINITY in profile.score)
     r["weight_interpod"] = int(profile.score.get(INTER_POD_AFFINITY, 0))
     r["hard_pod_affinity_weight"] = hard_pod_affinity_weight
+    r["multi_rank_mode"] = abi.MULTI_RANK[multi_rank]
     r["ds_scoring_strategy"] = abi.STRATEGY[ds.scoring_strategy]
     r["ds_scoring_weights"] = [ds.scoring_resources.get("koordinator.sh/gpu-core", 0),
                                ds.scoring_resources.get("koordinator.sh/gpu-memory", 0),

@@ -49,17 +49,17 @@ def _exact_case(kind):
     (NUMA + DeviceShare + Reservation + ElasticQuota), and the upstream defaults with hostname / zone
     PodTopologySpread and InterPodAffinity (the per-pod pass)."""
     if kind == "stock":
-        cfg = F.build_config(profile=STOCK_PROFILE)
+        cfg = F.build_config(multi_rank="shard", profile=STOCK_PROFILE)
         cluster = synth.make_cluster(800, seed=981)
         synth.make_pod_groups(cluster.existing_pods, seed=984, zones=True)
         pods = synth.make_pod_groups(synth.make_pods(300, seed=982), seed=985, zones=True)
         preds = synth.make_predicates(800, pods, seed=983, no_zone=0.05)[1]
         return cfg, dict(cluster=cluster, pods=pods, preds=preds)
     if kind == "rsv":
-        cfg = F.build_config(profile=RSV_PROFILE)
+        cfg = F.build_config(multi_rank="shard", profile=RSV_PROFILE)
         cluster, rsv = synth.make_rsv_cluster(1500, seed=961)
         return cfg, dict(cluster=cluster, rsv=rsv, pods=synth.make_rsv_pods(800, seed=962))
-    cfg = F.build_config(profile=SHIPPED_PROFILE,
+    cfg = F.build_config(multi_rank="shard", profile=SHIPPED_PROFILE,
                          la=F.LoadAwareSchedulingArgs(filter_expired_node_metrics=False,
                                                       node_metric_expiration_seconds=300))
     cluster, numa, dev, rsv = synth.make_shipped_cluster(600, seed=971)
@@ -70,11 +70,11 @@ def _exact_case(kind):
 
 def _case(kind):
     if kind == "ds":
-        cfg = F.build_config(profile=DS_PROFILE, batch_pods=32, pods_per_wave=4)
+        cfg = F.build_config(multi_rank="shard", profile=DS_PROFILE, batch_pods=32, pods_per_wave=4)
         cluster, dev = synth.make_gpu_cluster(1200, seed=951)
         pods = synth.make_gpu_pods(1500, seed=952)
         return cfg, cluster, pods, dev
-    cfg = F.build_config(batch_pods=32, pods_per_wave=8, pipeline_depth=2)
+    cfg = F.build_config(multi_rank="shard", batch_pods=32, pods_per_wave=8, pipeline_depth=2)
     cluster = synth.make_cluster(2000, seed=941)
     pods = synth.make_pods(3000, seed=942)
     return cfg, cluster, pods, None

@@ -43,11 +43,18 @@ def test_rsv_filter_device(c):
 def test_rsv_filter_reservation_device(c):
     """FilterReservation: the pod is nominated into the GPU-holding reservation exactly when DeviceShare can allocate
     from it (a device pod never nominates one it cannot)."""
-    e, _, _, pod = engine_case(c)
+    from oracle import oracle
+    e, dev, r, pod = engine_case(c)
     with e:
         ev = e.evaluate_reservation(pod)
-    assert ev["pass"][0] == 1, c["source"]
-    assert (ev["nominated"][0] == 0) == c["want_filter"], c["source"]
+    # the node-level Filter (the reference test calls FilterReservation alone): device = oracle; an exhausted
+    # reservation on a node with nothing else free fails both
+    st = oracle.ds_rsv_init(r, matched=[0])
+    assert bool(ev["pass"][0]) == oracle.ds_filter_rsv(dev, pod, r, st, False), c["source"]
+    if ev["pass"][0]:
+        assert (ev["nominated"][0] == 0) == c["want_filter"], c["source"]
+    else:
+        assert not c["want_filter"], c["source"]
 
 
 @pytest.mark.parametrize("c", TG._cases(("rsv_score",)), ids=TG._id)

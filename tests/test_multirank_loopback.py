@@ -69,7 +69,7 @@ def same_on_every_rank(out, want_node, want_score, st):
 def test_fit_loadaware_ranks(n_ranks, depth, batch):
     cluster = synth.make_cluster(3000, seed=901 + n_ranks)
     pods = synth.make_pods(6000, seed=902 + depth)
-    cfg = F.build_config(batch_pods=batch, pods_per_wave=8, pipeline_depth=depth)
+    cfg = F.build_config(multi_rank="shard", batch_pods=batch, pods_per_wave=8, pipeline_depth=depth)
     st = oracle.states(cluster.n)
     oracle.add_pods(cfg, st, cluster.existing_pods, cluster.existing_node)
     want, want_score = oracle.schedule(cfg, cluster.nodes, cluster.metrics, st, pods, cluster.now_ns, 8)
@@ -88,7 +88,7 @@ def test_fit_loadaware_ranks_with_quotas_and_ragged_shards():
     quotas["used_limit"] = -1
     quotas["min"] = -1
     quotas["used_limit"][:, 0] = pods["requests"][:, 0].sum() // 8
-    cfg = F.build_config()
+    cfg = F.build_config(multi_rank="shard")
     st = oracle.states(cluster.n)
     oracle.add_pods(cfg, st, cluster.existing_pods, cluster.existing_node)
     q = quotas.copy()
@@ -107,7 +107,7 @@ def test_fit_loadaware_ranks_with_quotas_and_ragged_shards():
 
 
 def test_numa_ranks():
-    cfg = F.build_config(profile=NUMA_PROFILE, batch_pods=16, pods_per_wave=1)
+    cfg = F.build_config(multi_rank="shard", profile=NUMA_PROFILE, batch_pods=16, pods_per_wave=1)
     cluster, numa = synth.make_numa_cluster(600, seed=921)
     pods = synth.make_numa_pods(1500, seed=922)
     st = oracle.states(cluster.n)
@@ -123,7 +123,7 @@ def test_numa_ranks():
 
 
 def test_deviceshare_ranks():
-    cfg = F.build_config(profile=DS_PROFILE, batch_pods=32, pods_per_wave=4)
+    cfg = F.build_config(multi_rank="shard", profile=DS_PROFILE, batch_pods=32, pods_per_wave=4)
     cluster, dev = synth.make_gpu_cluster(1500, seed=931)
     pods = synth.make_gpu_pods(3000, seed=932)
     st = oracle.states(cluster.n)
@@ -151,7 +151,7 @@ def test_reservation_profile_ranks_sharded(n_ranks, n_nodes):
     every round, and the other shards' listed candidates are evaluated on the rank's replica — so
     every rank's placements, reservation slots, GPU minors and quota charges equal the oracle's.  500 nodes = 2 tiles
     over 3 ranks: the last rank's shard is empty."""
-    cfg = F.build_config(profile=C5_PROFILE)
+    cfg = F.build_config(multi_rank="shard", profile=C5_PROFILE)
     cluster, dev, rsv = synth.make_c5_cluster(n_nodes, seed=961)
     pods = synth.make_c5_pods(1500, seed=962)
     quotas = synth.make_c5_quotas(pods, seed=963)
@@ -181,7 +181,7 @@ SHIPPED_PROFILE = F.Profile(filter=(F.NODE_RESOURCES_FIT, F.LOAD_AWARE, F.NODE_N
 def test_shipped_profile_ranks_sharded():
     """The shipped profile (NUMA + DeviceShare + Reservation + ElasticQuota) on 4 ranks of sharded exact rounds: the
     NUMA affinity of another shard's candidate comes from xr_fill on the rank's replica."""
-    cfg = F.build_config(profile=SHIPPED_PROFILE,
+    cfg = F.build_config(multi_rank="shard", profile=SHIPPED_PROFILE,
                          la=F.LoadAwareSchedulingArgs(filter_expired_node_metrics=False,
                                                       node_metric_expiration_seconds=300))
     cluster, numa, dev, rsv = synth.make_shipped_cluster(1100, seed=1971)
@@ -198,3 +198,33 @@ def test_shipped_profile_ranks_sharded():
     for rk in range(4):
         assert np.array_equal(out[rk][3], want_slot), rk
     assert (want >= 0).mean() > 0.3
+
+
+def test_auto_multi_rank_runs_small_tables_as_replicas():
+    """(r6) kg_config.multi_rank_mode AUTO: below the sharding threshold an engine of a 2-rank group is a
+    replica of one GPU — it shards nothing, never calls the exchange, and places exactly as one GPU does; SHARD forces
+    the exchange at the same size."""
+    from koordinator_amd.engine import HostExchange
+    cluster = synth.make_cluster(3000, seed=991)
+    pods = synth.make_pods(1500, seed=992)
+    calls = [0]
+
+    def allgather(buf):
+        calls[0] += 1
+        return np.concatenate([buf, buf])
+
+    one = F.build_config(batch_pods=32)
+    with Engine(one, cluster.n) as e:
+        synth.load_into(e, cluster)
+        want = e.schedule(pods)[:2]
+    ex = HostExchange(allgather)
+    with Engine(F.build_config(batch_pods=32, multi_rank="auto"), cluster.n, rank=1, n_ranks=2, exchange=ex) as e:
+        assert e.ranks == (1, 2)
+        synth.load_into(e, cluster)
+        got = e.schedule(pods)[:2]
+    assert calls[0] == 0 and ex.error is None
+    np.testing.assert_array_equal(got[0], want[0])
+    np.testing.assert_array_equal(got[1], want[1])
+    with Engine(F.build_config(batch_pods=32, multi_rank="shard"), cluster.n, rank=0, n_ranks=2,
+                exchange=HostExchange(allgather)) as e:
+        assert e.ranks == (2, 1)
