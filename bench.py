@@ -151,11 +151,12 @@ class Work:
         elif name == "shipped":
             self.seed = S.BASE_SEED + 13
             self.cluster, self.numa, self.devices, self.rsv = S.make_shipped_cluster(nodes, seed=self.seed)
-            self.make_pods = S.make_shipped_pods
+            # (r6) prefix-stable queues (C4, shipped): the committed oracle fixture covers any prefix --steps times
+            self.make_pods = lambda n, seed: S.make_stream(S.make_shipped_pods, n, seed)
         elif name == "c4":
             self.seed = S.BASE_SEED + 4
             self.cluster, self.numa = S.make_numa_cluster(nodes, seed=self.seed)
-            self.make_pods = S.make_numa_pods
+            self.make_pods = lambda n, seed: S.make_stream(S.make_numa_pods, n, seed)
         elif name == "c5ds":
             self.seed = S.BASE_SEED + 6
             self.cluster, self.devices = S.make_gpu_cluster(nodes, seed=self.seed)
@@ -178,11 +179,15 @@ class Work:
             # (r6) C3's queue is prefix-stable, so the committed oracle fixture covers whatever prefix --steps times
             self.make_pods = S.make_pods_stream if name == "c3" else S.make_pods
 
+    QUOTA_BASIS = 25_000  # (r6) shipped: quotas sized on the queue's first 25k pods, whatever --steps (fixture-stable)
+
     def set_queue(self, pods):
         """ElasticQuota groups sized on the queue's demand (C5: 16 groups whose limits run out mid-queue)."""
         from koordinator_amd import synth
-        if self.name in ("c5", "shipped"):
+        if self.name == "c5":
             self.quotas = synth.make_c5_quotas(pods, seed=self.seed + 2)
+        elif self.name == "shipped":
+            self.quotas = synth.make_c5_quotas(pods[:self.QUOTA_BASIS], seed=self.seed + 2)
 
     def load(self, e):
         from koordinator_amd import synth
@@ -231,14 +236,15 @@ class Work:
         return on, "oracle/oracle.c or_schedule (Parallelizer chunking)"
 
 
-FIXTURES = {"c3": "c3_queue.npz"}  # (r6) the oracle's schedule of the whole queue, tests/golden/make_*_fixture.py
+# (r6) the oracle's schedule of the whole queue: tests/golden/make_c3_fixture.py, make_bench_fixture.py
+FIXTURES = {"c3": "c3_queue.npz", "c4": "c4_queue.npz", "shipped": "shipped_queue.npz"}
 
 
 def fixture_check(wl, n_nodes, pods, node_idx, score, total):
     """(r6) Compare the first `total` placements and totals with the committed oracle fixture of this workload's queue
     (outside the timed region).  The fixture holds the oracle's sequential schedule of the same seeded queue; its
-    per-100k-segment digests prove the queue is the one this run generated.  Returns (ok, pods checked, source) or
-    None when no fixture covers this run."""
+    per-segment digests prove the queue is the one this run generated.  Returns (ok, pods checked, source, totals
+    compared) or None when no fixture covers this run."""
     import hashlib
     name = FIXTURES.get(wl)
     path = os.path.join(ROOT, "tests", "golden", name) if name else None
@@ -252,9 +258,41 @@ def fixture_check(wl, n_nodes, pods, node_idx, score, total):
     for s in range(total // seg):
         if hashlib.sha256(np.ascontiguousarray(pods[s * seg:(s + 1) * seg]).tobytes()).hexdigest() != str(z["seg_sha"][s]):
             return None
-    ok = bool(np.array_equal(z["node"][:total], node_idx[:total]) and
-              np.array_equal(z["score"][:total].astype(np.int64), score[:total]))
-    return ok, total, f"tests/golden/{name} ({meta['oracle']}, {meta['pods']} pods)"
+    ok = bool(np.array_equal(z["node"][:total], node_idx[:total]))
+    if "score" in z.files:  # C3: the totals too; C4 / shipped fixtures hold the placements
+        ok = ok and bool(np.array_equal(z["score"][:total].astype(np.int64), score[:total]))
+    return ok, total, f"tests/golden/{name} ({meta['oracle']}, {meta['pods']} pods)", "score" in z.files
+
+
+def workload_profile(wl):
+    """(profile, LoadAwareSchedulingArgs) of a workload (None = the engine defaults)."""
+    from koordinator_amd import framework as F
+    profile = None
+    if wl == "c4":
+        profile = F.Profile(filter=(F.NODE_RESOURCES_FIT, F.LOAD_AWARE, F.NODE_NUMA_RESOURCE),
+                            score={F.NODE_RESOURCES_FIT: 1, F.LOAD_AWARE: 1, F.NODE_NUMA_RESOURCE: 1})
+    elif wl == "c5ds":  # shipped weights: DeviceShare 1 (config/manager/scheduler-config.yaml:82-91)
+        profile = F.Profile(filter=(F.NODE_RESOURCES_FIT, F.LOAD_AWARE, F.DEVICE_SHARE),
+                            score={F.NODE_RESOURCES_FIT: 1, F.LOAD_AWARE: 1, F.DEVICE_SHARE: 1})
+    elif wl == "c5":  # one profile: Reservation 5000, DeviceShare 1, ElasticQuota admission (PreFilter only)
+        profile = F.Profile(filter=(F.NODE_RESOURCES_FIT, F.LOAD_AWARE, F.RESERVATION, F.DEVICE_SHARE),
+                            score={F.NODE_RESOURCES_FIT: 1, F.LOAD_AWARE: 1, F.RESERVATION: 5000, F.DEVICE_SHARE: 1})
+    elif wl == "c5r":  # shipped weights: Reservation 5000 (config/manager/scheduler-config.yaml:90-91)
+        profile = F.Profile(filter=(F.NODE_RESOURCES_FIT, F.LOAD_AWARE, F.RESERVATION),
+                            score={F.NODE_RESOURCES_FIT: 1, F.LOAD_AWARE: 1, F.RESERVATION: 5000})
+    elif wl in ("stock", "stockz"):  # k8s v1.24 v1beta2 default weights + LoadAware; hostname spread / inter-pod affinity
+        profile = F.Profile(filter=(F.NODE_RESOURCES_FIT, F.LOAD_AWARE, F.TAINT_TOLERATION, F.NODE_AFFINITY,
+                                    F.POD_TOPOLOGY_SPREAD, F.INTER_POD_AFFINITY),
+                            score={F.NODE_RESOURCES_FIT: 1, F.LOAD_AWARE: 1, F.TAINT_TOLERATION: 1, F.NODE_AFFINITY: 1,
+                                   F.BALANCED_ALLOCATION: 1, F.POD_TOPOLOGY_SPREAD: 2, F.INTER_POD_AFFINITY: 1})
+    la = None
+    if wl == "shipped":  # config/manager/scheduler-config.yaml:29-117: plugins, weights and LoadAware args
+        profile = F.Profile(filter=(F.NODE_RESOURCES_FIT, F.LOAD_AWARE, F.NODE_NUMA_RESOURCE, F.DEVICE_SHARE,
+                                    F.RESERVATION),
+                            score={F.NODE_RESOURCES_FIT: 1, F.LOAD_AWARE: 1, F.NODE_NUMA_RESOURCE: 1, F.DEVICE_SHARE: 1,
+                                   F.RESERVATION: 5000})
+        la = F.LoadAwareSchedulingArgs(filter_expired_node_metrics=False, node_metric_expiration_seconds=300)
+    return profile, la
 
 
 def cpu_sample(work, pods, budget_s, threads):
@@ -302,32 +340,7 @@ def main():
     args.check = check0 if args.check is None else args.check
     if wl == "c1" and args.steps == 10:
         args.steps = 1  # the whole 5k-pod queue of config 1
-    F = framework
-    profile = None
-    if wl == "c4":
-        profile = F.Profile(filter=(F.NODE_RESOURCES_FIT, F.LOAD_AWARE, F.NODE_NUMA_RESOURCE),
-                            score={F.NODE_RESOURCES_FIT: 1, F.LOAD_AWARE: 1, F.NODE_NUMA_RESOURCE: 1})
-    elif wl == "c5ds":  # shipped weights: DeviceShare 1 (config/manager/scheduler-config.yaml:82-91)
-        profile = F.Profile(filter=(F.NODE_RESOURCES_FIT, F.LOAD_AWARE, F.DEVICE_SHARE),
-                            score={F.NODE_RESOURCES_FIT: 1, F.LOAD_AWARE: 1, F.DEVICE_SHARE: 1})
-    elif wl == "c5":  # one profile: Reservation 5000, DeviceShare 1, ElasticQuota admission (PreFilter only)
-        profile = F.Profile(filter=(F.NODE_RESOURCES_FIT, F.LOAD_AWARE, F.RESERVATION, F.DEVICE_SHARE),
-                            score={F.NODE_RESOURCES_FIT: 1, F.LOAD_AWARE: 1, F.RESERVATION: 5000, F.DEVICE_SHARE: 1})
-    elif wl == "c5r":  # shipped weights: Reservation 5000 (config/manager/scheduler-config.yaml:90-91)
-        profile = F.Profile(filter=(F.NODE_RESOURCES_FIT, F.LOAD_AWARE, F.RESERVATION),
-                            score={F.NODE_RESOURCES_FIT: 1, F.LOAD_AWARE: 1, F.RESERVATION: 5000})
-    elif wl in ("stock", "stockz"):  # k8s v1.24 v1beta2 default weights + LoadAware; hostname spread / inter-pod affinity
-        profile = F.Profile(filter=(F.NODE_RESOURCES_FIT, F.LOAD_AWARE, F.TAINT_TOLERATION, F.NODE_AFFINITY,
-                                    F.POD_TOPOLOGY_SPREAD, F.INTER_POD_AFFINITY),
-                            score={F.NODE_RESOURCES_FIT: 1, F.LOAD_AWARE: 1, F.TAINT_TOLERATION: 1, F.NODE_AFFINITY: 1,
-                                   F.BALANCED_ALLOCATION: 1, F.POD_TOPOLOGY_SPREAD: 2, F.INTER_POD_AFFINITY: 1})
-    la = None
-    if wl == "shipped":  # config/manager/scheduler-config.yaml:29-117: plugins, weights and LoadAware args
-        profile = F.Profile(filter=(F.NODE_RESOURCES_FIT, F.LOAD_AWARE, F.NODE_NUMA_RESOURCE, F.DEVICE_SHARE,
-                                    F.RESERVATION),
-                            score={F.NODE_RESOURCES_FIT: 1, F.LOAD_AWARE: 1, F.NODE_NUMA_RESOURCE: 1, F.DEVICE_SHARE: 1,
-                                   F.RESERVATION: 5000})
-        la = F.LoadAwareSchedulingArgs(filter_expired_node_metrics=False, node_metric_expiration_seconds=300)
+    profile, la = workload_profile(wl)
     cfg = framework.build_config(batch_pods=args.batch, pods_per_wave=args.pods_per_wave, device_id=d.local_rank,
                                  profile=profile, pipeline_depth=args.depth, la=la, multi_rank=args.multi_rank)
     work = Work(wl, args.nodes, cfg)
@@ -617,7 +630,7 @@ def main():
                              (check is not False) and (fx is None or fx[0])),
             "oracle_check_pods": max(min(args.check, total) if args.check else 0, fx[1] if fx else 0),
             "oracle_check_live_pods": min(args.check, total) if args.check else 0,
-            "oracle_check_fixture": ({"ok": fx[0], "pods": fx[1], "placements_and_totals": True, "source": fx[2]}
+            "oracle_check_fixture": ({"ok": fx[0], "pods": fx[1], "placements_and_totals": fx[3], "source": fx[2]}
                                      if fx else None),
         }
         print(json.dumps(out), flush=True)

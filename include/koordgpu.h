@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define KG_ABI_VERSION 15
+#define KG_ABI_VERSION 16
 
 /* ---- resource slots (fixed order) ------------------------------------------------------- */
 enum {
@@ -129,8 +129,11 @@ enum {
   KG_REJECT_SPREAD = 1 << 9,        /* (ABI 12) PodTopologySpread: DoNotSchedule constraint's skew exceeded   */
   KG_REJECT_INTERPOD = 1 << 10,     /* (ABI 12) InterPodAffinity: affinity / anti-affinity / existing pods'
                                        anti-affinity rules not matched                                          */
-  KG_REJECT_NO_VICTIMS = 1 << 11    /* (ABI 14) kg_pods_select_victims: the candidate has no potential victims
+  KG_REJECT_NO_VICTIMS = 1 << 11,   /* (ABI 14) kg_pods_select_victims: the candidate has no potential victims
                                        ("No victims found on node": UnschedulableAndUnresolvable)              */
+  KG_REJECT_TAINT = 1 << 12,        /* (ABI 16) TaintToleration (preemption dry run): an untolerated taint    */
+  KG_REJECT_NODE_AFFINITY = 1 << 13 /* (ABI 16) NodeAffinity (preemption dry run): nodeSelector / required
+                                       terms do not match                                                      */
 };
 
 /* node flags */
@@ -695,11 +698,20 @@ int kg_pods_evaluate_reservation(kg_engine* e, const kg_pod* pod, int64_t* out);
  * state.preemptible[node], or to state.preemptibleInRRs[node][its reservation] when victim_slot[k] >= 0 names the
  * node's reservation slot it was allocated from; NULL = none).  The Reservation Filter then fits the pod against them
  * (plugin.go:357-428, fitsNode :433-482).  out_reject: 0 = every enabled Filter passes, else KG_REJECT_* bits.
- * Profiles with NodeResourcesFit / LoadAwareScheduling / Reservation; NodeNUMAResource, DeviceShare and the upstream
- * defaults are refused (KG_E_UNSUPPORTED: the victims' cpusets / devices / labels are not modelled here).  (ABI 14)
- * Pods and victims with ephemeral-storage / scalar requests are accepted. */
+ * Profiles with NodeResourcesFit / LoadAwareScheduling / Reservation; (ABI 14) pods and victims with ephemeral-storage
+ * / scalar requests are accepted.  (ABI 16) The other accelerated Filters run in the dry run too:
+ *   - NodeNUMAResource: no PreFilterExtensions (nodenumaresource/plugin.go:272-274), so the victims' cpusets stay
+ *     allocated in the node's NodeAllocation; its Filter reads the victim-free NodeInfo.Requested (filterAmplifiedCPUs);
+ *   - DeviceShare: AddPod / RemovePod (deviceshare/plugin.go:163-278) move a victim's GPU allocation (victim_minors[k] =
+ *     the minors it holds on the node, its per-instance share = its device request as Reserve allocated it; NULL or 0
+ *     = none) into state.preemptibleDevices[node] unless it is a reserve pod or was allocated from a reservation
+ *     (victim_slot[k] >= 0); Filter allocates against free = total − max(0, used − preemptible)
+ *     (calcFreeWithPreemptible, device_cache.go:314-342).  Engines whose reservations hold GPUs are refused;
+ *   - TaintToleration / NodeAffinity: node-static (KG_REJECT_TAINT / KG_REJECT_NODE_AFFINITY).
+ * PodTopologySpread / InterPodAffinity profiles are refused (KG_E_UNSUPPORTED). */
 int kg_pods_filter_preemption(kg_engine* e, const kg_pod* pod, int32_t node_idx, const kg_pod* victims,
-                              const int32_t* victim_slot, int64_t n_victims, int32_t* out_reject);
+                              const int32_t* victim_slot, const int32_t* victim_minors, int64_t n_victims,
+                              int32_t* out_reject);
 
 /* (ABI 14) The preemption dry run over many candidate nodes in ONE launch: SelectVictimsOnNode for every candidate
  * (DryRunPreemption's per-node step: koordinator's elasticquota/preempt.go:111-215 and the k8s defaultpreemption
@@ -707,7 +719,7 @@ int kg_pods_filter_preemption(kg_engine* e, const kg_pod* pod, int32_t node_idx,
  *   - its potential victims are victims[victim_offsets[c] .. victim_offsets[c + 1]) in the caller's reprieve order —
  *     the caller's canPreempt selection (priority, quota), util.MoreImportantPod sort and filterPodsWithPDBViolation
  *     split: PDB-violating victims first (pdb_violating[k] = 1; NULL = none), each group most important first;
- *     victim_slot[k] as for kg_pods_filter_preemption (NULL = none);
+ *     victim_slot[k] and victim_minors[k] as for kg_pods_filter_preemption (NULL = none);
  *   - the device removes them all (NodeInfo.RemovePod + the Reservation plugin's RemovePod) and runs the Filters:
  *     out_reject[c] = 0 or KG_REJECT_* bits (KG_REJECT_NO_VICTIMS for a candidate without potential victims);
  *   - when they pass, it reprieves each victim in order: adds it back (AddPodInfo + AddPod), re-runs the Filters and
@@ -718,8 +730,8 @@ int kg_pods_filter_preemption(kg_engine* e, const kg_pod* pod, int32_t node_idx,
  * EphemeralStorage / ScalarResources terms (reservation/plugin.go:471-479) by both entry points since ABI 14. */
 int kg_pods_select_victims(kg_engine* e, const kg_pod* pod, int64_t n_candidates, const int32_t* node_idx,
                            const int64_t* victim_offsets, const kg_pod* victims, const int32_t* victim_slot,
-                           const uint8_t* pdb_violating, int32_t* out_reject, uint8_t* out_victim,
-                           int32_t* out_violating);
+                           const int32_t* victim_minors, const uint8_t* pdb_violating, int32_t* out_reject,
+                           uint8_t* out_victim, int32_t* out_violating);
 
 /* (ABI 12) PodTopologySpread / InterPodAffinity state (engines whose profile enables either): per node and match
  * group k, [n][k] layout of KG_MAX_MATCH_GROUPS int32 each — pods matching group k (countPodsMatchSelector),

@@ -36,7 +36,7 @@ POD_TAINT_TABLE = 64
 MAX_OWNER_GROUPS = 64
 QUOTA_RES = 8
 MAX_QUOTAS = 64
-ABI_VERSION = 15
+ABI_VERSION = 16
 MAX_RSV_SLOTS = 4
 RSV_POLICY = {"Default": 0, "Aligned": 1, "Restricted": 2}
 POD_RSV_AFFINITY, POD_RSV_OPERATING = 1, 2
@@ -60,6 +60,8 @@ REJECT_RESERVATION = 256  # Reservation Filter (kg_pods_filter_preemption)
 REJECT_SPREAD = 512  # (ABI 12) PodTopologySpread
 REJECT_INTERPOD = 1024  # (ABI 12) InterPodAffinity
 REJECT_NO_VICTIMS = 2048  # (ABI 14) kg_pods_select_victims: the candidate has no potential victims
+REJECT_TAINT = 4096  # (ABI 16) TaintToleration in the preemption dry run
+REJECT_NODE_AFFINITY = 8192  # (ABI 16) NodeAffinity in the preemption dry run
 # DeviceShare device resources (KG_DEV_*)
 DEV_RES_MAX, MAX_MINORS = 8, 8
 MAX_AFF_TERMS = 4  # KG_MAX_AFF_TERMS
@@ -309,8 +311,8 @@ def load_library(path: str | None = None):
         "kg_engine_set_clock": (i, [vp, i64]),
         "kg_debug_numa_merge": (i, [vp, vp, i64, vp]),
         "kg_pods_evaluate_reservation": (i, [vp, vp, vp]),
-        "kg_pods_filter_preemption": (i, [vp, vp, ctypes.c_int32, vp, vp, i64, vp]),
-        "kg_pods_select_victims": (i, [vp, vp, i64, vp, vp, vp, vp, vp, vp, vp, vp]),
+        "kg_pods_filter_preemption": (i, [vp, vp, ctypes.c_int32, vp, vp, vp, i64, vp]),
+        "kg_pods_select_victims": (i, [vp, vp, i64, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
         "kg_nodes_read_pod_groups": (i, [vp, vp, vp, vp, vp, vp]),
         "kg_nodes_predicates_upsert": (i, [vp, vp, vp, i64]),
         "kg_engine_create_hosted": (i, [vp, i64, i, i, EXCHANGE_FN, vp, ctypes.POINTER(vp)]),

@@ -2781,6 +2781,22 @@ struct Victim {
   int64_t aux[kAux];  // ephemeral-storage and the scalar resources (KG_RES_EPHEMERAL ..)
   int32_t slot;       // the node's reservation slot the victim was allocated from, -1 = none
   int32_t nonzero;    // counted by RemovePod / AddPod: !quotav1.IsZero(PodRequestsAndLimits) and not a reserve pod
+  int32_t dminors;    // (r6) the GPU minors of its DeviceShare allocation (nodeDevice.getUsed of the victim), 0 = none
+  int32_t reserve;    // (r6) a reserve pod (DeviceShare's AddPod / RemovePod return before counting it)
+  DsPod dp;           // (r6) its DeviceShare request (the per-instance allocation on each minor, ds_instance)
+};
+// (r6) the dry run's Filters of the other accelerated plugins (nullptr: the plugin is not in the profile)
+struct PreExt {
+  const NumaStatic* __restrict__ ns;  // NodeNUMAResource: no PreFilterExtensions (plugin.go:272-274), so the victims'
+  const NumaMut* __restrict__ nm;     // cpusets stay allocated; its Filter reads the victim-free NodeInfo.Requested
+  NumaParams NP;
+  NumaPod np;
+  const DsNode* __restrict__ ds;      // DeviceShare: AddPod / RemovePod (deviceshare/plugin.go:163-278) move the
+  DsParams DP;                        // victims' allocations in / out of preemptibleDevices[node]
+  DsPod dp;
+  const NodePred* __restrict__ pred;  // TaintToleration / NodeAffinity: node-static Filters
+  DefParams DF;
+  DefPod df;
 };
 struct PreNode {
   Row r;
@@ -2794,6 +2810,7 @@ struct PreNode {
   int64_t rr_c[kRsvSlots], rr_m[kRsvSlots], rr_aux[kRsvSlots][kAux];  // preemptibleInRRs[node][slot]
   bool pre_set;
   uint32_t rr_set;
+  int64_t dpre[kMinors][3];  // (r6) DeviceShare preemptibleDevices[node]: gpu-core, gpu-memory, gpu-memory-ratio
 };
 
 // BeforePreFilter's restore of node i for the pod (the same rsv_restore as the scheduling passes); false: invalid node
@@ -2825,11 +2842,28 @@ __device__ bool pre_node_init(PreNode& S, const DevTable& T, const RsvNode* __re
   }
   S.pre_set = false;
   S.rr_set = 0;
+#pragma unroll
+  for (int m = 0; m < kMinors; ++m) S.dpre[m][0] = S.dpre[m][1] = S.dpre[m][2] = 0;
   return true;
 }
 
 // sign +1: NodeInfo.RemovePod + RemovePod; −1: NodeInfo.AddPodInfo + AddPod
-__device__ __forceinline__ void pre_node_apply(PreNode& S, const Victim& v, int64_t sign) {
+__device__ __forceinline__ void pre_node_apply(PreNode& S, const Victim& v, int64_t sign, const PreExt* X = nullptr,
+                                               int64_t i = 0) {
+  // (r6) DeviceShare's RemovePod / AddPod (deviceshare/plugin.go:163-278): a victim outside any reservation (rInfo nil)
+  // moves its allocation into / out of preemptibleDevices[node] (appendAllocated / subtractAllocated), unless it is a
+  // reserve pod or the preemptor requests no devices (state.skip)
+  if (X && X->ds && !X->dp.skip && v.dminors != 0 && !v.reserve && v.slot < 0) {
+    const DsInst in = ds_instance(X->ds[i], v.dp);
+    if (in.ok)
+#pragma unroll
+      for (int m = 0; m < kMinors; ++m)
+        if ((v.dminors >> m) & 1) {
+          S.dpre[m][0] += sign * in.core;
+          S.dpre[m][1] += sign * in.mem;
+          S.dpre[m][2] += sign * in.ratio;
+        }
+  }
   S.r.req_cpu -= sign * v.req_cpu;
   S.r.req_mem -= sign * v.req_mem;
   S.r.nz_cpu -= sign * v.nz_cpu;
@@ -2856,7 +2890,7 @@ __device__ __forceinline__ void pre_node_apply(PreNode& S, const Victim& v, int6
 // the pod's Filters on the candidate's current NodeInfo copy: 0 or KG_REJECT_* bits.  rq: the pod's kAux requests.
 __device__ uint32_t pre_node_filter(const DevTable& T, const PreNode& S, int64_t i, const DevPod& p,
                                     const int64_t (&rq)[kAux], const RsvPod& rp, const EvalParams& P,
-                                    const RsvParams& RP, int rsv_on) {
+                                    const RsvParams& RP, int rsv_on, const PreExt* X = nullptr) {
   uint32_t rej = 0;
   int64_t t = 0;
   Row r = S.r;
@@ -2926,6 +2960,42 @@ __device__ uint32_t pre_node_filter(const DevTable& T, const PreNode& S, int64_t
     }
     if (!ok) rej |= KG_REJECT_RESERVATION;
   }
+  if (X) {
+    if (X->pred) {  // TaintToleration / NodeAffinity Filter (defaults_filter, split into their reject bits)
+      const NodePred n = X->pred[i];
+      const DefPod& d = X->df;
+      if (X->DF.taint_filter && (n.hard & ~d.tol) != 0) rej |= KG_REJECT_TAINT;
+      if (X->DF.aff_filter) {
+        bool ok = (n.pred & d.sel) == d.sel;
+        if (ok && d.nreq > 0) {
+          bool any = false;
+#pragma unroll
+          for (int k = 0; k < kAffTerms; ++k) any |= k < d.nreq && term_holds(n.pred, d.req[k]);
+          ok = any;
+        }
+        if (!ok) rej |= KG_REJECT_NODE_AFFINITY;
+      }
+    }
+    if (X->ns && X->NP.filter) {  // NodeNUMAResource Filter on the node's own NodeAllocation, victim-free Requested
+      const NumaView v = make_view(X->ns + i, X->nm + i, X->NP);
+      NumaHint aff;
+      if (!numa_filter(v, X->np, X->NP, aff, S.r.req_cpu, S.r.alloc_cpu)) rej |= KG_REJECT_NUMA;
+    }
+    if (X->ds && X->DP.filter && !X->dp.skip) {
+      // calcFreeWithPreemptible (device_cache.go:314-342): free = total − max(0, used − preemptible) on every minor
+      DsNode d = X->ds[i];
+#pragma unroll
+      for (int m = 0; m < kMinors; ++m) {
+        const int64_t c = (int64_t)d.ucore[m] - S.dpre[m][0], b = d.umem[m] - S.dpre[m][1],
+                      r = (int64_t)d.uratio[m] - S.dpre[m][2];
+        d.ucore[m] = (int32_t)(c > 0 ? c : 0);
+        d.umem[m] = b > 0 ? b : 0;
+        d.uratio[m] = (int32_t)(r > 0 ? r : 0);
+      }
+      int64_t raw = 0;
+      if (!ds_eval(d, X->dp, X->DP, raw)) rej |= KG_REJECT_DEVICE;
+    }
+  }
   return rej;
 }
 
@@ -2934,7 +3004,7 @@ __global__ void filter_pod_preempt(DevTable T, const RsvNode* __restrict__ RN, c
                                    const uint64_t* __restrict__ rsv_pred, const RsvSel* __restrict__ rsel, int64_t i,
                                    const DevPod* __restrict__ pod, const int64_t* __restrict__ pod_aux, RsvPod rp,
                                    EvalParams P, RsvParams RP, int rsv_on, const Victim* __restrict__ vic,
-                                   int64_t n_vic, int32_t* __restrict__ out) {
+                                   int64_t n_vic, int32_t* __restrict__ out, PreExt X) {
   if (blockIdx.x != 0 || threadIdx.x != 0) return;
   PreNode S;
   if (!pre_node_init(S, T, RN, rsv_n, rsv_pred, rsel, i, rp, rsv_on)) {
@@ -2945,8 +3015,8 @@ __global__ void filter_pod_preempt(DevTable T, const RsvNode* __restrict__ RN, c
   int64_t rq[kAux];
 #pragma unroll
   for (int q = 0; q < kAux; ++q) rq[q] = pod_aux[q];
-  for (int64_t k = 0; k < n_vic; ++k) pre_node_apply(S, vic[k], 1);
-  *out = (int32_t)pre_node_filter(T, S, i, p, rq, rp, P, RP, rsv_on);
+  for (int64_t k = 0; k < n_vic; ++k) pre_node_apply(S, vic[k], 1, &X, i);
+  *out = (int32_t)pre_node_filter(T, S, i, p, rq, rp, P, RP, rsv_on, &X);
 }
 
 // (r5) kg_pods_select_victims: SelectVictimsOnNode for every candidate (one thread per candidate, the victims in the
@@ -2958,7 +3028,7 @@ __global__ void select_victims(DevTable T, const RsvNode* __restrict__ RN, const
                                EvalParams P, RsvParams RP, int rsv_on, int64_t n_cand, const int32_t* __restrict__ nodes,
                                const int64_t* __restrict__ off, const Victim* __restrict__ vic,
                                const uint8_t* __restrict__ violating, int32_t* __restrict__ out_reject,
-                               uint8_t* __restrict__ out_victim, int32_t* __restrict__ out_violating) {
+                               uint8_t* __restrict__ out_victim, int32_t* __restrict__ out_violating, PreExt X) {
   const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= n_cand) return;
   const int64_t i = nodes[c], k0 = off[c], k1 = off[c + 1];
@@ -2977,16 +3047,16 @@ __global__ void select_victims(DevTable T, const RsvNode* __restrict__ RN, const
   int64_t rq[kAux];
 #pragma unroll
   for (int q = 0; q < kAux; ++q) rq[q] = pod_aux[q];
-  for (int64_t k = k0; k < k1; ++k) pre_node_apply(S, vic[k], 1);
-  const uint32_t rej = pre_node_filter(T, S, i, p, rq, rp, P, RP, rsv_on);
+  for (int64_t k = k0; k < k1; ++k) pre_node_apply(S, vic[k], 1, &X, i);
+  const uint32_t rej = pre_node_filter(T, S, i, p, rq, rp, P, RP, rsv_on, &X);
   out_reject[c] = (int32_t)rej;
   if (rej) return;
   int32_t nv = 0;
   for (int64_t k = k0; k < k1; ++k) {  // reprievePod, in order
     const Victim v = vic[k];
-    pre_node_apply(S, v, -1);
-    if (pre_node_filter(T, S, i, p, rq, rp, P, RP, rsv_on) != 0) {
-      pre_node_apply(S, v, 1);
+    pre_node_apply(S, v, -1, &X, i);
+    if (pre_node_filter(T, S, i, p, rq, rp, P, RP, rsv_on, &X) != 0) {
+      pre_node_apply(S, v, 1, &X, i);
       out_victim[k] = 1;
       nv += violating && violating[k] ? 1 : 0;
     }
@@ -6043,6 +6113,27 @@ static int check_predicate_tables(kg_engine* e) {
   return 0;
 }
 
+// one pod (the preemption dry run's) against the node rows' tables, as check_predicate_tables does for a staged queue
+static int check_pod_tables(kg_engine* e, const kg_pod& q) {
+  const int64_t st = e->sq_taint_min, sp = e->sq_pred_top, si = e->sq_img_top;
+  int64_t tmin = 64, ptop = 0, itop = 0;
+  if (q.flags & KG_POD_TAINT_TABLE) {
+    if (q.taint_count < 0 || q.taint_count > 64) return fail(KG_E_INVALID, "pod: taint_count");
+    tmin = q.taint_count;
+  }
+  uint64_t used = q.node_selector;
+  for (int t = 0; t < KG_MAX_AFF_TERMS; ++t) {
+    if (t < q.n_required_terms) used |= q.required_terms[t];
+    if (t < q.n_preferred_terms) used |= q.preferred_terms[t];
+  }
+  ptop = used ? 64 - __builtin_clzll(used) : 0;
+  for (int c = 0; c < KG_MAX_CONTAINERS && c < q.n_containers; ++c) itop = std::max<int64_t>(itop, q.container_image_bit[c] + 1);
+  e->sq_taint_min = tmin, e->sq_pred_top = ptop, e->sq_img_top = itop;
+  const int rc = check_predicate_tables(e);
+  e->sq_taint_min = st, e->sq_pred_top = sp, e->sq_img_top = si;
+  return rc;
+}
+
 // (ABI 12) the same rule for the reservation slots' fakeNode predicates (kg_node_reservations.predicate_count)
 static int check_rsv_predicates(kg_engine* e, int64_t top) {
   if (top == 0) return 0;
@@ -6905,13 +6996,19 @@ int kg_pods_evaluate_reservation(kg_engine* e, const kg_pod* pod, int64_t* out) 
   return 0;
 }
 
-// the pod and its victims of one dry-run call, decoded and checked (the shared front half of the two entry points)
+// the pod and its victims of one dry-run call, decoded and checked (the shared front half of the two entry points).
+// (r6) NodeNUMAResource, DeviceShare and TaintToleration / NodeAffinity run in the dry run too (PreExt); refused:
+// PodTopologySpread / InterPodAffinity (their PreFilterExtensions move cluster-wide counters) and DeviceShare with
+// reservations that hold GPUs (preemptibleInRRs of devices).
 static int preempt_prepare(kg_engine* e, const kg_pod* pod, const kg_pod* victims, const int32_t* victim_slot,
-                           int64_t n_victims, DevPod& d, RsvPod& rp, RsvSel& rs, int64_t (&rq)[kAux],
-                           std::vector<Victim>& hv) {
-  if (e->numa_on || e->ds_on || e->def_on)
-    return fail(KG_E_UNSUPPORTED, "preemption dry run: NodeNUMAResource / DeviceShare / the upstream defaults keep the "
-                "Go path (the victims' cpusets, devices and labels are not modelled)");
+                           const int32_t* victim_minors, int64_t n_victims, DevPod& d, RsvPod& rp, RsvSel& rs,
+                           int64_t (&rq)[kAux], std::vector<Victim>& hv, PreExt& X) {
+  if (e->grp_on)
+    return fail(KG_E_UNSUPPORTED, "preemption dry run: PodTopologySpread / InterPodAffinity keep the Go path (their "
+                "AddPod / RemovePod move cluster-wide counters)");
+  if (e->ds_on && e->rsv_on && e->rgpu_nodes > 0)
+    return fail(KG_E_UNSUPPORTED, "preemption dry run: DeviceShare with reservations that hold GPUs keeps the Go path "
+                "(preemptibleInRRs of devices)");
   if (int rc = sync_static(e)) return rc;
   if (int rc = decode_pod(e, *pod, d)) return rc;
   for (int q = 0; q < kAux; ++q) rq[q] = pod->requests[kAuxFirst + q];
@@ -6920,26 +7017,58 @@ static int preempt_prepare(kg_engine* e, const kg_pod* pod, const kg_pod* victim
   if (rp.flags & RP_SEL) rp.aux = 0;
   if (rp.flags & (RP_RESERVE | RP_OPERATING))
     return fail(KG_E_UNSUPPORTED, "preemption dry run for a reserve pod / reservation operating mode keeps the Go path");
+  X = PreExt{};
+  X.dp.skip = 1;
+  if (e->numa_on) {
+    if (int rc = decode_numa_pod(e->cfg, *pod, X.np)) return rc;
+    X.ns = e->numa_s.p, X.nm = e->numa_m.p, X.NP = e->NP;
+  }
+  if (e->ds_on) {
+    if (int rc = decode_ds_pod(*pod, X.dp)) return rc;
+    X.ds = e->ds_d.p, X.DP = e->DP;
+  } else {
+    for (int r = 0; r < KG_DEV_RES_MAX; ++r)
+      if (pod->device_requests[r] != 0 && e->cfg.fit_filter)
+        return fail(KG_E_UNSUPPORTED, "the pod requests devices; the profile has no DeviceShare");
+  }
+  if (e->def_on) {
+    if (int rc = decode_def_pod(*pod, X.df, 0)) return rc;
+    if (int rc = check_pod_tables(e, *pod)) return rc;
+    X.pred = e->npred.p, X.DF = e->DF;
+  }
   hv.resize((size_t)std::max<int64_t>(n_victims, 1));
   for (int64_t k = 0; k < n_victims; ++k) {
     DevPod v;
     if (int rc = decode_pod(e, victims[k], v)) return rc;
     const int32_t s = victim_slot ? victim_slot[k] : -1;
     if (s < -1 || s >= KG_MAX_RSV_SLOTS) return fail(KG_E_INVALID, "victim %lld: reservation slot %d", (long long)k, s);
+    const int32_t m = victim_minors ? victim_minors[k] : 0;
+    if (m < 0 || m >= (1 << kMinors)) return fail(KG_E_INVALID, "victim %lld: minors 0x%x", (long long)k, m);
     bool nz = false;
     for (int q = 0; q < KG_RES_MAX; ++q) nz |= victims[k].requests[q] != 0;
     // (r5) RemovePod returns before counting a reserve pod (reservation/plugin.go:286): the framework still
     // removes it from the NodeInfo copy, but it never becomes preemptible
-    if (victims[k].flags & KG_POD_RESERVE) nz = false;
-    Victim w{v.req_cpu, v.req_mem, v.nz_cpu, v.nz_mem, {}, s, nz ? 1 : 0};
+    const bool reserve = (victims[k].flags & KG_POD_RESERVE) != 0;
+    if (reserve) nz = false;
+    Victim w{};
+    w.req_cpu = v.req_cpu, w.req_mem = v.req_mem, w.nz_cpu = v.nz_cpu, w.nz_mem = v.nz_mem;
+    w.slot = s, w.nonzero = nz ? 1 : 0, w.reserve = reserve ? 1 : 0;
     for (int q = 0; q < kAux; ++q) w.aux[q] = victims[k].requests[kAuxFirst + q];
+    w.dp.skip = 1;
+    if (e->ds_on && m != 0) {
+      if (int rc = decode_ds_pod(victims[k], w.dp)) return rc;
+      if (w.dp.skip || w.dp.error)
+        return fail(KG_E_INVALID, "victim %lld holds minors 0x%x but requests no valid GPU share", (long long)k, m);
+      w.dminors = m;
+    }
     hv[k] = w;
   }
   return 0;
 }
 
 int kg_pods_filter_preemption(kg_engine* e, const kg_pod* pod, int32_t node_idx, const kg_pod* victims,
-                              const int32_t* victim_slot, int64_t n_victims, int32_t* out_reject) {
+                              const int32_t* victim_slot, const int32_t* victim_minors, int64_t n_victims,
+                              int32_t* out_reject) {
   if (!e || !pod || !out_reject || n_victims < 0 || (n_victims > 0 && !victims)) return fail(KG_E_INVALID, "null argument");
   if (node_idx < 0 || node_idx >= e->n_nodes) return fail(KG_E_INVALID, "node index %d outside [0, %lld)", node_idx,
                                                            (long long)e->n_nodes);
@@ -6948,7 +7077,8 @@ int kg_pods_filter_preemption(kg_engine* e, const kg_pod* pod, int32_t node_idx,
   RsvSel rs;
   int64_t rq[kAux];
   std::vector<Victim> hv;
-  if (int rc = preempt_prepare(e, pod, victims, victim_slot, n_victims, d, rp, rs, rq, hv)) return rc;
+  PreExt X;
+  if (int rc = preempt_prepare(e, pod, victims, victim_slot, victim_minors, n_victims, d, rp, rs, rq, hv, X)) return rc;
   const size_t vw = (hv.size() * sizeof(Victim) + 7) / 8;
   if (int rc = e->scratch64.ensure(kPodWords + kAux + vw + 1 + sizeof(RsvSel) / 8)) return rc;
   DevPod* gp = reinterpret_cast<DevPod*>(e->scratch64.p);
@@ -6961,7 +7091,7 @@ int kg_pods_filter_preemption(kg_engine* e, const kg_pod* pod, int32_t node_idx,
   HIP_TRY(hipMemcpyAsync(gs, &rs, sizeof(rs), hipMemcpyHostToDevice, e->stream));
   if (n_victims > 0) HIP_TRY(hipMemcpyAsync(gv, hv.data(), (size_t)n_victims * sizeof(Victim), hipMemcpyHostToDevice, e->stream));
   filter_pod_preempt<<<1, kWave, 0, e->stream>>>(e->T, e->rsv_d.p, e->rsv_nd.p, e->rsv_pd.p, gs, node_idx, gp, ga, rp,
-                                                 e->P, e->RP, e->rsv_on ? 1 : 0, gv, n_victims, go);
+                                                 e->P, e->RP, e->rsv_on ? 1 : 0, gv, n_victims, go, X);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpyAsync(out_reject, go, 4, hipMemcpyDeviceToHost, e->stream));
   HIP_TRY(hipStreamSynchronize(e->stream));
@@ -6970,7 +7100,7 @@ int kg_pods_filter_preemption(kg_engine* e, const kg_pod* pod, int32_t node_idx,
 
 int kg_pods_select_victims(kg_engine* e, const kg_pod* pod, int64_t n_candidates, const int32_t* node_idx,
                            const int64_t* victim_offsets, const kg_pod* victims, const int32_t* victim_slot,
-                           const uint8_t* pdb_violating, int32_t* out_reject, uint8_t* out_victim,
+                           const int32_t* victim_minors, const uint8_t* pdb_violating, int32_t* out_reject, uint8_t* out_victim,
                            int32_t* out_violating) {
   if (!e || !pod || n_candidates < 0 || (n_candidates > 0 && (!node_idx || !victim_offsets || !out_reject ||
                                                               !out_violating)))
@@ -6991,7 +7121,8 @@ int kg_pods_select_victims(kg_engine* e, const kg_pod* pod, int64_t n_candidates
   RsvSel rs;
   int64_t rq[kAux];
   std::vector<Victim> hv;
-  if (int rc = preempt_prepare(e, pod, victims, victim_slot, nv, d, rp, rs, rq, hv)) return rc;
+  PreExt X;
+  if (int rc = preempt_prepare(e, pod, victims, victim_slot, victim_minors, nv, d, rp, rs, rq, hv, X)) return rc;
   // one device buffer: pod, pod aux, RsvSel, victims, offsets, nodes, violating flags, then the outputs
   auto words = [](size_t bytes) { return (bytes + 7) / 8; };
   const size_t w_pod = kPodWords, w_aux = kAux, w_sel = words(sizeof(RsvSel)), w_vic = words(hv.size() * sizeof(Victim));
@@ -7033,7 +7164,7 @@ int kg_pods_select_victims(kg_engine* e, const kg_pod* pod, int64_t n_candidates
                                                   reinterpret_cast<const Victim*>(b + o_vic), gviol,
                                                   reinterpret_cast<int32_t*>(b + o_rej),
                                                   reinterpret_cast<uint8_t*>(b + o_out),
-                                                  reinterpret_cast<int32_t*>(b + o_nvio));
+                                                  reinterpret_cast<int32_t*>(b + o_nvio), X);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpyAsync(out_reject, b + o_rej, (size_t)n_candidates * 4, hipMemcpyDeviceToHost, e->stream));
   HIP_TRY(hipMemcpyAsync(out_violating, b + o_nvio, (size_t)n_candidates * 4, hipMemcpyDeviceToHost, e->stream));

@@ -357,21 +357,26 @@ class Engine:
         check(self.lib, self.lib.kg_debug_eval_paths(self.h, ptr(out)))
         return int(out[0])
 
-    def filter_preemption(self, pod: np.ndarray, node: int, victims: np.ndarray, slots=None) -> int:
+    def filter_preemption(self, pod: np.ndarray, node: int, victims: np.ndarray, slots=None, minors=None) -> int:
         """The preemption dry run's Filter of `pod` on node `node` with `victims` removed (kg_pods_filter_preemption):
-        KG_REJECT_* bits, 0 = fits.  slots[k]: the node's reservation slot victim k was allocated from (-1 = none)."""
+        KG_REJECT_* bits, 0 = fits.  slots[k]: the node's reservation slot victim k was allocated from (-1 = none);
+        minors[k]: the GPU minors (bitmask) its DeviceShare allocation holds on the node (0 = none)."""
         pod = np.ascontiguousarray(np.asarray(pod, dtype=abi.POD_DTYPE).reshape(1))
         victims = np.ascontiguousarray(np.asarray(victims, dtype=abi.POD_DTYPE).reshape(-1))
         sl = None if slots is None else np.ascontiguousarray(slots, dtype=np.int32)
+        mi = None if minors is None else np.ascontiguousarray(minors, dtype=np.int32)
         out = np.zeros(1, dtype=np.int32)
         check(self.lib, self.lib.kg_pods_filter_preemption(self.h, ptr(pod), int(node), ptr(victims) if len(victims) else None,
-                                                           ptr(sl) if sl is not None else None, len(victims), ptr(out)))
+                                                           ptr(sl) if sl is not None else None,
+                                                           ptr(mi) if mi is not None else None, len(victims), ptr(out)))
         return int(out[0])
 
-    def select_victims(self, pod: np.ndarray, nodes, victims_per_node, slots_per_node=None, violating_per_node=None):
+    def select_victims(self, pod: np.ndarray, nodes, victims_per_node, slots_per_node=None, violating_per_node=None,
+                       minors_per_node=None):
         """SelectVictimsOnNode on every candidate node in one launch (kg_pods_select_victims).  victims_per_node[c]:
-        candidate c's potential victims (POD_DTYPE) in reprieve order; slots / violating: per-victim reservation slot
-        (-1 none) and PDB-violating flag.  Returns (reject int32[C], victim bool arrays per candidate, violating int32[C])."""
+        candidate c's potential victims (POD_DTYPE) in reprieve order; slots / violating / minors: per-victim reservation
+        slot (-1 none), PDB-violating flag and GPU minors.  Returns (reject int32[C], victim bool arrays per candidate,
+        violating int32[C])."""
         pod = np.ascontiguousarray(np.asarray(pod, dtype=abi.POD_DTYPE).reshape(1))
         nodes = np.ascontiguousarray(nodes, dtype=np.int32)
         counts = np.array([len(v) for v in victims_per_node], dtype=np.int64)
@@ -381,7 +386,10 @@ class Engine:
         vic = np.zeros(max(nv, 1), dtype=abi.POD_DTYPE)
         if nv:
             vic[:nv] = np.concatenate([np.asarray(v, dtype=abi.POD_DTYPE).reshape(-1) for v in victims_per_node])
-        sl = vio = None
+        sl = vio = mi = None
+        if minors_per_node is not None and nv:
+            mi = np.ascontiguousarray(np.concatenate([np.asarray(s, dtype=np.int32).reshape(-1)
+                                                      for s in minors_per_node]))
         if slots_per_node is not None and nv:
             sl = np.ascontiguousarray(np.concatenate([np.asarray(s, dtype=np.int32).reshape(-1)
                                                       for s in slots_per_node]))
@@ -393,6 +401,7 @@ class Engine:
         nvio = np.zeros(max(len(nodes), 1), dtype=np.int32)
         check(self.lib, self.lib.kg_pods_select_victims(self.h, ptr(pod), len(nodes), ptr(nodes), ptr(off), ptr(vic),
                                                         ptr(sl) if sl is not None else None,
+                                                        ptr(mi) if mi is not None else None,
                                                         ptr(vio) if vio is not None else None, ptr(rej), ptr(kept),
                                                         ptr(nvio)))
         return (rej[:len(nodes)], [kept[off[c]:off[c + 1]].astype(bool) for c in range(len(nodes))],

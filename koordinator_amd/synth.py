@@ -130,6 +130,17 @@ def make_pods_stream(n_pods: int, seed: int = BASE_SEED + 1) -> np.ndarray:
     return np.concatenate(parts)[:n_pods]
 
 
+def make_stream(make, n_pods: int, seed: int, chunk: int = POD_STREAM_CHUNK) -> np.ndarray:
+    """(r6) Any queue generator made prefix-stable: chunk k of `chunk` pods is make(chunk, seed=s_k) with s_k an int
+    drawn from SeedSequence([seed, k]).  The C4 / shipped benches draw their queues here so one committed oracle
+    fixture (tests/golden/make_bench_fixture.py) covers every prefix they time."""
+    k = -(-n_pods // chunk)
+    parts = [make(chunk, seed=int(np.random.SeedSequence([seed, i]).generate_state(1)[0])) for i in range(k)]
+    if not parts:
+        return np.zeros(0, dtype=abi.POD_DTYPE)
+    return np.concatenate(parts)[:n_pods]
+
+
 def load_into(engine, cluster: Cluster):
     """Informer-order ingest: nodes, NodeMetrics, then the already-assigned pods."""
     engine.upsert_nodes(cluster.nodes)

@@ -151,9 +151,9 @@ def lib():
         L.or_rsv_case_flat.restype = None
         L.or_rsv_policy_filter.argtypes = [vp, i64, vp]
         L.or_rsv_policy_filter.restype = i
-        L.or_filter_preemption.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, i64, i64]
+        L.or_filter_preemption.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, i64, i64, vp]
         L.or_filter_preemption.restype = i64
-        L.or_select_victims.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i64, vp, vp]
+        L.or_select_victims.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i64, vp, vp, vp]
         L.or_select_victims.restype = i64
         for f, res in (("or_taint_filter", i), ("or_taint_count", i64), ("or_affinity_filter", i),
                        ("or_affinity_sum", i64), ("or_image_score", i64)):
@@ -358,19 +358,37 @@ def rsv_case(pod, allowed_pods, alloc, num_pods, pod_requested, r_allocated, has
     return int(out[0]), int(out[1]), int(out[2])
 
 
-def filter_preemption(cfg, node, metric, state, rsv, pod, victims, slots, now_ns: int) -> int:
-    """or_filter_preemption: the preemption dry run's Filter (KG_REJECT_* bits) of one pod on one node."""
+def _pre_ext(numa, dev, pred, minors, n):
+    """or_pre_ext {numa, dev, pred, victim_minors} (r6): None members = not in the profile / none.  Returns the struct
+    (a ctypes array of 4 pointers) and the arrays it points into (kept alive by the caller)."""
+    c = lambda a, dt: np.ascontiguousarray(np.asarray(a, dtype=dt).reshape(-1))
+    keep = [c(numa, abi.NODE_NUMA_DTYPE) if numa is not None else None,
+            c(dev, abi.NODE_DEVICE_DTYPE) if dev is not None else None,
+            c(pred, abi.NODE_PRED_DTYPE) if pred is not None else None,
+            c(minors, np.int32) if minors is not None and n else None]
+    if all(k is None for k in keep):
+        return None, keep
+    x = (ctypes.c_void_p * 4)(*[k.ctypes.data if k is not None else None for k in keep])
+    return x, keep
+
+
+def filter_preemption(cfg, node, metric, state, rsv, pod, victims, slots, now_ns: int, numa=None, dev=None, pred=None,
+                      minors=None) -> int:
+    """or_filter_preemption: the preemption dry run's Filter (KG_REJECT_* bits) of one pod on one node; (r6) numa /
+    dev / pred = the node's NodeNUMAResource / DeviceShare / predicate rows, minors[k] = victim k's GPU minors."""
     c = lambda a, dt: np.ascontiguousarray(np.asarray(a, dtype=dt).reshape(-1))
     v = c(victims, abi.POD_DTYPE)
     sl = c(slots if slots is not None else -np.ones(len(v)), np.int32)
+    x, _keep = _pre_ext(numa, dev, pred, minors, len(v))
     return int(lib().or_filter_preemption(p(cfg), p(c(node, abi.NODE_DTYPE)), p(c(metric, abi.METRIC_DTYPE)),
                                           p(np.ascontiguousarray(state[:1])),
                                           p(c(rsv, abi.NODE_RSV_DTYPE)) if rsv is not None else None,
                                           p(c(pod, abi.POD_DTYPE)), p(v) if len(v) else None, p(sl) if len(v) else None,
-                                          len(v), now_ns))
+                                          len(v), now_ns, ctypes.cast(x, ctypes.c_void_p) if x is not None else None))
 
 
-def select_victims(cfg, node, metric, state, rsv, pod, victims, slots, violating, now_ns: int):
+def select_victims(cfg, node, metric, state, rsv, pod, victims, slots, violating, now_ns: int, numa=None, dev=None,
+                   pred=None, minors=None):
     """or_select_victims: SelectVictimsOnNode of one candidate → (reject bits, bool[k] victim kept, numViolating)."""
     c = lambda a, dt: np.ascontiguousarray(np.asarray(a, dtype=dt).reshape(-1))
     v = c(victims, abi.POD_DTYPE)
@@ -379,11 +397,13 @@ def select_victims(cfg, node, metric, state, rsv, pod, victims, slots, violating
     vio = c(violating if violating is not None else np.zeros(n), np.uint8)
     kept = np.zeros(max(n, 1), dtype=np.uint8)
     nv = np.zeros(1, dtype=np.int32)
+    x, _keep = _pre_ext(numa, dev, pred, minors, n)
     rej = int(lib().or_select_victims(p(cfg), p(c(node, abi.NODE_DTYPE)), p(c(metric, abi.METRIC_DTYPE)),
                                       p(np.ascontiguousarray(state[:1])),
                                       p(c(rsv, abi.NODE_RSV_DTYPE)) if rsv is not None else None,
                                       p(c(pod, abi.POD_DTYPE)), p(v) if n else None, p(sl) if n else None,
-                                      p(vio) if n else None, n, now_ns, p(kept), p(nv)))
+                                      p(vio) if n else None, n, now_ns, p(kept), p(nv),
+                                      ctypes.cast(x, ctypes.c_void_p) if x is not None else None))
     return rej, kept[:n].astype(bool), int(nv[0])
 
 

@@ -666,16 +666,21 @@ void or_rsv_restore_flat(const kg_node_reservations* r, const or_node_state* st,
  * Reservation plugin's preemptible maps (PreFilterExtensions RemovePod / AddPod, reservation/plugin.go:253-310: a
  * non-reserve victim with non-zero requests adds (RemovePod) or subtracts (AddPod) its requests — every resource, so
  * ephemeral-storage and the scalars too — to state.preemptible[node] or preemptibleInRRs[node][its reservation]; either
- * call sets the map entry, which then stays non-empty). */
+ * call sets the map entry, which then stays non-empty).  (r6) DeviceShare's preemptibleDevices[node] per minor. */
 typedef struct {
   or_node_state rs;   /* the NodeInfo copy the Filters see */
   or_rsv_node ns;     /* nodeReservationState (restore-time podRequested / rAllocated, untouched by the victims) */
   int64_t pre[KG_RES_MAX], pre_rr[KG_MAX_RSV_SLOTS][KG_RES_MAX];
   int pre_set, pre_rr_set;
+  const or_pre_ext* x;
+  or_ds_pod dsp;                        /* the preemptor's DeviceShare preFilterState */
+  int64_t dpre[KG_MAX_MINORS][3];       /* preemptibleDevices[node]: gpu-core, gpu-memory, gpu-memory-ratio */
+  or_numa_node nn;                      /* the node's NodeAllocation (victims' cpusets kept) */
+  or_numa_pod np;
 } pre_node;
 
 static void pre_node_init(pre_node* S, const kg_config* cfg, const or_node_state* st, const kg_node_reservations* rsv,
-                          const kg_pod* pod) {
+                          const kg_pod* pod, const or_pre_ext* x) {
   const int rsv_on = cfg->reservation_filter || cfg->reservation_score;
   memset(S, 0, sizeof(*S));
   or_rsv_restore(rsv_on ? rsv : NULL, st, pod, &S->ns);
@@ -685,10 +690,31 @@ static void pre_node_init(pre_node* S, const kg_config* cfg, const or_node_state
   S->rs.nonzero[0] = S->ns.nonzero[0];
   S->rs.nonzero[1] = S->ns.nonzero[1];
   S->rs.num_pods = S->ns.num_pods;
+  S->x = x;
+  S->dsp.skip = 1;
+  if (x && x->dev) or_ds_pod_init(pod, &S->dsp);
+  if (x && x->numa) {
+    or_numa_node_init(&S->nn, x->numa);
+    or_numa_pod_init(cfg, pod, &S->np);
+  }
 }
 
 /* sign +1: NodeInfo.RemovePod + RemovePod; -1: NodeInfo.AddPodInfo + AddPod */
-static void pre_node_apply(pre_node* S, const kg_pod* v, int slot, int64_t sign) {
+static void pre_node_apply(pre_node* S, const kg_pod* v, int slot, int32_t minors, int64_t sign) {
+  /* (r6) DeviceShare AddPod / RemovePod: reserve pods and state.skip return first; no allocation on the node
+   * (getUsed empty) returns; a victim allocated from a reservation goes to preemptibleInRRs */
+  if (S->x && S->x->dev && !S->dsp.skip && minors != 0 && !(v->flags & KG_POD_RESERVE) && slot < 0) {
+    or_ds_pod vp;
+    or_ds_pod_init(v, &vp);
+    const or_ds_inst in = or_ds_instance(S->x->dev, &vp);
+    if (in.ok)
+      for (int m = 0; m < KG_MAX_MINORS; m++)
+        if ((minors >> m) & 1) {
+          S->dpre[m][0] += sign * in.core;
+          S->dpre[m][1] += sign * in.mem;
+          S->dpre[m][2] += sign * in.ratio;
+        }
+  }
   for (int q = 0; q < KG_RES_MAX; q++) S->rs.requested[q] -= sign * v->requests[q];
   S->rs.nonzero[0] -= sign * v->nonzero_requests[0];
   S->rs.nonzero[1] -= sign * v->nonzero_requests[1];
@@ -783,16 +809,36 @@ static int64_t pre_node_filter(const kg_config* cfg, const kg_node* node, const 
     }
     if (!ok) rej |= KG_REJECT_RESERVATION;
   }
+  const or_pre_ext* x = S->x;
+  if (x && x->pred) {
+    if (cfg->taint_filter && !or_taint_filter(x->pred, pod)) rej |= KG_REJECT_TAINT;
+    if (cfg->affinity_filter && !or_affinity_filter(x->pred, pod)) rej |= KG_REJECT_NODE_AFFINITY;
+  }
+  if (x && x->numa && cfg->numa_filter) {
+    or_hint aff;
+    if (!or_numa_filter(cfg, &S->nn, &S->np, &aff, S->rs.requested[KG_RES_CPU], node->allocatable[KG_RES_CPU]))
+      rej |= KG_REJECT_NUMA;
+  }
+  if (x && x->dev && cfg->ds_filter && !S->dsp.skip) {
+    /* Filter without GPU-holding reservations: Allocate(nil, nil, nil, preemptibleDevices[node]); a node without a
+     * Device object rejects a device pod (NodeResourcesFit on the device resources, as or_ds_filter) */
+    const int ok = !S->dsp.error && x->dev->has_device &&
+                   or_ds_allocate(x->dev, &S->dsp, 0, 0, 0, NULL, (const int64_t(*)[3])S->dpre, 0, 0, NULL) >= 0;
+    if (!ok) rej |= KG_REJECT_DEVICE;
+  }
   return rej;
 }
 
 int64_t or_filter_preemption(const kg_config* cfg, const kg_node* node, const kg_node_metric* metric,
                              const or_node_state* st, const kg_node_reservations* rsv, const kg_pod* pod,
-                             const kg_pod* victims, const int32_t* victim_slot, int64_t n_victims, int64_t now) {
+                             const kg_pod* victims, const int32_t* victim_slot, int64_t n_victims, int64_t now,
+                             const or_pre_ext* ext) {
   if (!(node->flags & KG_NODE_VALID)) return KG_REJECT_INVALID_NODE;
   pre_node S;
-  pre_node_init(&S, cfg, st, rsv, pod);
-  for (int64_t k = 0; k < n_victims; k++) pre_node_apply(&S, &victims[k], victim_slot ? victim_slot[k] : -1, 1);
+  pre_node_init(&S, cfg, st, rsv, pod, ext);
+  const int32_t* vm = ext ? ext->victim_minors : NULL;
+  for (int64_t k = 0; k < n_victims; k++)
+    pre_node_apply(&S, &victims[k], victim_slot ? victim_slot[k] : -1, vm ? vm[k] : 0, 1);
   return pre_node_filter(cfg, node, metric, st, rsv, pod, &S, now);
 }
 
@@ -805,23 +851,27 @@ int64_t or_filter_preemption(const kg_config* cfg, const kg_node* node, const kg
 int64_t or_select_victims(const kg_config* cfg, const kg_node* node, const kg_node_metric* metric,
                           const or_node_state* st, const kg_node_reservations* rsv, const kg_pod* pod,
                           const kg_pod* victims, const int32_t* victim_slot, const uint8_t* violating,
-                          int64_t n_victims, int64_t now, uint8_t* out_victim, int32_t* out_violating) {
+                          int64_t n_victims, int64_t now, uint8_t* out_victim, int32_t* out_violating,
+                          const or_pre_ext* ext) {
   for (int64_t k = 0; k < n_victims; k++) out_victim[k] = 0;
   *out_violating = 0;
   if (!(node->flags & KG_NODE_VALID)) return KG_REJECT_INVALID_NODE;
   if (n_victims == 0) return KG_REJECT_NO_VICTIMS;
   pre_node S;
-  pre_node_init(&S, cfg, st, rsv, pod);
-  for (int64_t k = 0; k < n_victims; k++) pre_node_apply(&S, &victims[k], victim_slot ? victim_slot[k] : -1, 1);
+  pre_node_init(&S, cfg, st, rsv, pod, ext);
+  const int32_t* vm = ext ? ext->victim_minors : NULL;
+  for (int64_t k = 0; k < n_victims; k++)
+    pre_node_apply(&S, &victims[k], victim_slot ? victim_slot[k] : -1, vm ? vm[k] : 0, 1);
   const int64_t rej = pre_node_filter(cfg, node, metric, st, rsv, pod, &S, now);
   if (rej != 0) return rej;
   for (int64_t k = 0; k < n_victims; k++) {
     const int slot = victim_slot ? victim_slot[k] : -1;
-    pre_node_apply(&S, &victims[k], slot, -1);
+    const int32_t mk = vm ? vm[k] : 0;
+    pre_node_apply(&S, &victims[k], slot, mk, -1);
     const int64_t f = pre_node_filter(cfg, node, metric, st, rsv, pod, &S, now);
     if (f < 0) return f;
     if (f != 0) {
-      pre_node_apply(&S, &victims[k], slot, 1);
+      pre_node_apply(&S, &victims[k], slot, mk, 1);
       out_victim[k] = 1;
       if (violating && violating[k]) *out_violating += 1;
     }

@@ -93,23 +93,42 @@ void or_rsv_case_flat(const kg_pod* pod, int64_t allowed_pods, const int64_t all
 
 void or_rsv_restore_flat(const kg_node_reservations* r, const or_node_state* st, const kg_pod* pod, int64_t* out);
 
+/* (r6) The dry run's other Filters (NULL members: the plugin has no data for the node / is not in the profile):
+ *   numa  the node's NodeNUMAResource view — no PreFilterExtensions (nodenumaresource/plugin.go:272-274): the victims'
+ *         cpusets stay allocated; the Filter (plugin.go:276-334) reads the victim-free NodeInfo.Requested cpu;
+ *   dev   the node's GPUs — DeviceShare's RemovePod / AddPod (deviceshare/plugin.go:163-278) append / subtract a victim's
+ *         allocation (victim_minors[k], its per-instance share) to state.preemptibleDevices[node] unless it is a reserve
+ *         pod, requests nothing the preemptor's state tracks (state.skip) or was allocated from a reservation (its GPUs
+ *         go to preemptibleInRRs, which only GPU-holding reservations read); Filter (:280-330) allocates with free =
+ *         total − max(0, used − preemptible) (calcFreeWithPreemptible, device_cache.go:314-342);
+ *   pred  the node's taints / labels — TaintToleration and NodeAffinity Filters (node-static). */
+typedef struct or_pre_ext {
+  const kg_node_numa* numa;
+  const kg_node_device* dev;
+  const kg_node_predicates* pred;
+  const int32_t* victim_minors;
+} or_pre_ext;
+
 /* Preemption dry run (defaultpreemption SelectVictimsOnNode → RunFilterPluginsWithNominatedPods on a NodeInfo copy
  * with the victims removed): NodeInfo.RemovePod of each victim, and Reservation's PreFilterExtensions.RemovePod
  * (plugin.go:284-310) adding each victim's requests to state.preemptible[node] (victim_slot[k] < 0) or to
  * state.preemptibleInRRs[node][slot] — a victim with all-zero requests is skipped.  Then the pod's Filters on that
  * node: NodeResourcesFit (cpu / memory / pods / ephemeral-storage / scalars), LoadAwareScheduling, and the Reservation Filter (plugin.go:357-428)
- * with the preemptible amounts in fitsNode (:433-482) and the Restricted policy's Allocated (:404-413).  Returns the
- * KG_REJECT_* bits (0 = every Filter passes).  Profiles: Fit / LoadAware / Reservation. */
+ * with the preemptible amounts in fitsNode (:433-482) and the Restricted policy's Allocated (:404-413); (r6) with `ext`
+ * NodeNUMAResource, DeviceShare, TaintToleration and NodeAffinity as or_pre_ext says.  Returns the KG_REJECT_* bits
+ * (0 = every Filter passes). */
 int64_t or_filter_preemption(const kg_config* cfg, const kg_node* node, const kg_node_metric* metric,
                              const or_node_state* st, const kg_node_reservations* rsv, const kg_pod* pod,
-                             const kg_pod* victims, const int32_t* victim_slot, int64_t n_victims, int64_t now);
+                             const kg_pod* victims, const int32_t* victim_slot, int64_t n_victims, int64_t now,
+                             const or_pre_ext* ext);
 /* (r5) SelectVictimsOnNode of one candidate (elasticquota/preempt.go:111-215): the potential victims in reprieve
  * order are removed, the Filters run (none: KG_REJECT_NO_VICTIMS), then each victim is reprieved in order (added
  * back, kept as a victim when the pod no longer fits).  out_victim[k], *out_violating as kg_pods_select_victims. */
 int64_t or_select_victims(const kg_config* cfg, const kg_node* node, const kg_node_metric* metric,
                           const or_node_state* st, const kg_node_reservations* rsv, const kg_pod* pod,
                           const kg_pod* victims, const int32_t* victim_slot, const uint8_t* violating,
-                          int64_t n_victims, int64_t now, uint8_t* out_victim, int32_t* out_violating);
+                          int64_t n_victims, int64_t now, uint8_t* out_victim, int32_t* out_violating,
+                          const or_pre_ext* ext);
 
 #ifdef __cplusplus
 }
