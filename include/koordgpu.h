@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define KG_ABI_VERSION 16
+#define KG_ABI_VERSION 17
 
 /* ---- resource slots (fixed order) ------------------------------------------------------- */
 enum {
@@ -97,8 +97,8 @@ enum {
   KG_DEV_GPU_CORE = 3,          /* koordinator.sh/gpu-core (percentage)                */
   KG_DEV_GPU_MEMORY = 4,        /* koordinator.sh/gpu-memory (bytes)                   */
   KG_DEV_GPU_MEMORY_RATIO = 5,  /* koordinator.sh/gpu-memory-ratio (percentage)        */
-  KG_DEV_FPGA = 6,              /* koordinator.sh/fpga (not accelerated)               */
-  KG_DEV_RDMA = 7,              /* koordinator.sh/rdma (not accelerated)               */
+  KG_DEV_FPGA = 6,              /* koordinator.sh/fpga (percentage; (ABI 17) accelerated) */
+  KG_DEV_RDMA = 7,              /* koordinator.sh/rdma (percentage; (ABI 17) accelerated) */
   KG_DEV_RES_MAX = 8
 };
 #define KG_MAX_MINORS 8         /* GPU minors per node */
@@ -243,6 +243,9 @@ typedef struct kg_config {
    * exchanges each round's candidates; KG_MULTI_RANK_REPLICA makes every rank a replica of one GPU (the whole table, no
    * exchange, the same placements); AUTO shards only tables large enough for it to pay. */
   int64_t multi_rank_mode;
+  /* (ABI 17) DeviceShareArgs.ScoringStrategy.Resources weights of koordinator.sh/rdma and koordinator.sh/fpga (the
+   * scorer of the RDMA / FPGA device types; v1beta2 default 1 each) */
+  int64_t ds_scoring_weights_x[2];
   int64_t reserved[1];
 } kg_config;
 enum { KG_MULTI_RANK_AUTO = 0, KG_MULTI_RANK_SHARD = 1, KG_MULTI_RANK_REPLICA = 2 };
@@ -476,12 +479,21 @@ typedef struct kg_quota {
  * an unhealthy device has empty resources) + nodeDevice.deviceUsed from the pods already bound there.
  * has_device = 0: no Device object for the node (the plugin passes such nodes; NodeResourcesFit on the
  * device extended resources, whose allocatable is then 0, rejects device pods). */
+/* (ABI 17) the device types of the default handler (deviceshare/devicehandler_default.go): RDMA, FPGA */
+#define KG_DEV_XTYPES 2
+enum { KG_XTYPE_RDMA = 0, KG_XTYPE_FPGA = 1 };
 typedef struct kg_node_device {
   int64_t has_device;
   int64_t present[KG_MAX_MINORS];              /* a GPU DeviceInfo with this minor exists             */
   int64_t healthy[KG_MAX_MINORS];
   int64_t total_core[KG_MAX_MINORS], total_memory[KG_MAX_MINORS], total_ratio[KG_MAX_MINORS];
   int64_t used_core[KG_MAX_MINORS], used_memory[KG_MAX_MINORS], used_ratio[KG_MAX_MINORS];
+  /* (ABI 17) RDMA / FPGA DeviceInfos (type KG_XTYPE_*): listed minors, health, the type's one resource
+   * (koordinator.sh/rdma, koordinator.sh/fpga: percentage per device) and its deviceUsed */
+  int64_t x_present[KG_DEV_XTYPES][KG_MAX_MINORS];
+  int64_t x_healthy[KG_DEV_XTYPES][KG_MAX_MINORS];
+  int64_t x_total[KG_DEV_XTYPES][KG_MAX_MINORS];
+  int64_t x_used[KG_DEV_XTYPES][KG_MAX_MINORS];
 } kg_node_device;
 
 /* NodeNUMAResource view of one node: TopologyOptions (topology_options.go:40-48, from the
@@ -654,6 +666,12 @@ int kg_nodes_read_device(kg_engine* e, int64_t* used_core, int64_t* used_memory,
 /* The GPU minors DeviceShare Reserve allocated to staged pods [first, first+count): a bitmask per pod (0 = none);
  * every chosen minor received the pod's per-instance request (CalcDesiredRequestsAndCount). */
 int kg_results_fetch_devices(kg_engine* e, int64_t first, int64_t count, int32_t* out_minor_mask);
+/* (ABI 17) The RDMA / FPGA minors Reserve allocated to staged pods [first, first+count): out[k·KG_DEV_XTYPES + t] = the
+ * bitmask of type t for pod first + k (the default handler's allocation: every chosen minor received the per-instance
+ * request, devicehandler_default.go:45-92, device_allocator.go:384-454). */
+int kg_results_fetch_devices_x(kg_engine* e, int64_t first, int64_t count, int32_t* out_minor_masks);
+/* (ABI 17) Reads the device's RDMA / FPGA deviceUsed: [node][KG_DEV_XTYPES][KG_MAX_MINORS]. */
+int kg_nodes_read_device_x(kg_engine* e, int64_t* x_used);
 /* DeviceShare Filter + Score of one pod on every node slot, the plugin alone: out_pass 1/0 and the raw
  * (un-normalized) score, 0 where Filter rejects. */
 int kg_pods_evaluate_device(kg_engine* e, const kg_pod* pod, int32_t* out_pass, int64_t* out_score);
@@ -702,9 +720,10 @@ int kg_pods_evaluate_reservation(kg_engine* e, const kg_pod* pod, int64_t* out);
  * / scalar requests are accepted.  (ABI 16) The other accelerated Filters run in the dry run too:
  *   - NodeNUMAResource: no PreFilterExtensions (nodenumaresource/plugin.go:272-274), so the victims' cpusets stay
  *     allocated in the node's NodeAllocation; its Filter reads the victim-free NodeInfo.Requested (filterAmplifiedCPUs);
- *   - DeviceShare: AddPod / RemovePod (deviceshare/plugin.go:163-278) move a victim's GPU allocation (victim_minors[k] =
- *     the minors it holds on the node, its per-instance share = its device request as Reserve allocated it; NULL or 0
- *     = none) into state.preemptibleDevices[node] unless it is a reserve pod or was allocated from a reservation
+ *   - DeviceShare: AddPod / RemovePod (deviceshare/plugin.go:163-278) move a victim's device allocation (victim_minors[k]
+ *     = the minors it holds on the node — GPU bits 0-7, (ABI 17) RDMA bits 8-15, FPGA bits 16-23 —, its per-instance
+ *     share = its device request as Reserve allocated it; NULL or 0 = none) into state.preemptibleDevices[node] unless
+ *     it is a reserve pod or was allocated from a reservation
  *     (victim_slot[k] >= 0); Filter allocates against free = total − max(0, used − preemptible)
  *     (calcFreeWithPreemptible, device_cache.go:314-342).  Engines whose reservations hold GPUs are refused;
  *   - TaintToleration / NodeAffinity: node-static (KG_REJECT_TAINT / KG_REJECT_NODE_AFFINITY).

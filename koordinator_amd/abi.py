@@ -36,7 +36,7 @@ POD_TAINT_TABLE = 64
 MAX_OWNER_GROUPS = 64
 QUOTA_RES = 8
 MAX_QUOTAS = 64
-ABI_VERSION = 16
+ABI_VERSION = 17
 MAX_RSV_SLOTS = 4
 RSV_POLICY = {"Default": 0, "Aligned": 1, "Restricted": 2}
 POD_RSV_AFFINITY, POD_RSV_OPERATING = 1, 2
@@ -64,6 +64,7 @@ REJECT_TAINT = 4096  # (ABI 16) TaintToleration in the preemption dry run
 REJECT_NODE_AFFINITY = 8192  # (ABI 16) NodeAffinity in the preemption dry run
 # DeviceShare device resources (KG_DEV_*)
 DEV_RES_MAX, MAX_MINORS = 8, 8
+DEV_XTYPES, XTYPE_RDMA, XTYPE_FPGA = 2, 0, 1  # (ABI 17) the default handler's device types
 MAX_AFF_TERMS = 4  # KG_MAX_AFF_TERMS
 MAX_CONTAINERS = 8  # KG_MAX_CONTAINERS
 MAX_MATCH_GROUPS = 16  # KG_MAX_MATCH_GROUPS (ABI 12)
@@ -113,7 +114,7 @@ CONFIG_DTYPE = np.dtype([
     _i64("image_score"), _i64("weight_image"),
     _i64("spread_filter"), _i64("spread_score"), _i64("weight_spread"),
     _i64("interpod_filter"), _i64("interpod_score"), _i64("weight_interpod"), _i64("hard_pod_affinity_weight"),
-    _i64("multi_rank_mode"), _i64("reserved", 1),
+    _i64("multi_rank_mode"), _i64("ds_scoring_weights_x", 2), _i64("reserved", 1),
 ])
 
 NODE_DTYPE = np.dtype([
@@ -187,6 +188,9 @@ NODE_DEVICE_DTYPE = np.dtype([
     _i64("has_device"), _i64("present", MAX_MINORS), _i64("healthy", MAX_MINORS),
     _i64("total_core", MAX_MINORS), _i64("total_memory", MAX_MINORS), _i64("total_ratio", MAX_MINORS),
     _i64("used_core", MAX_MINORS), _i64("used_memory", MAX_MINORS), _i64("used_ratio", MAX_MINORS),
+    # (ABI 17) RDMA / FPGA DeviceInfos [XTYPE_RDMA, XTYPE_FPGA][minor]
+    _i64("x_present", (DEV_XTYPES, MAX_MINORS)), _i64("x_healthy", (DEV_XTYPES, MAX_MINORS)),
+    _i64("x_total", (DEV_XTYPES, MAX_MINORS)), _i64("x_used", (DEV_XTYPES, MAX_MINORS)),
 ])
 
 NODE_NUMA_DTYPE = np.dtype([
@@ -216,6 +220,7 @@ EXPORTED_SYMBOLS = (
     "kg_debug_fast_lrs",
     "kg_nodes_numa_upsert", "kg_nodes_read_numa", "kg_results_fetch_cpusets", "kg_pods_evaluate_numa",
     "kg_nodes_device_upsert", "kg_nodes_read_device", "kg_results_fetch_devices", "kg_pods_evaluate_device",
+    "kg_results_fetch_devices_x", "kg_nodes_read_device_x",
     "kg_quotas_set", "kg_quotas_read", "kg_nodes_reservation_upsert", "kg_nodes_read_reservations",
     "kg_nodes_read_reservation_gpus", "kg_nodes_read_reservation_cpus", "kg_engine_ranks",
     "kg_results_fetch_reservations", "kg_profile_enable", "kg_profile_read", "kg_loopback_create",
@@ -293,6 +298,8 @@ def load_library(path: str | None = None):
         "kg_nodes_device_upsert": (i, [vp, vp, vp, i64]),
         "kg_nodes_read_device": (i, [vp, vp, vp, vp]),
         "kg_results_fetch_devices": (i, [vp, i64, i64, vp]),
+        "kg_results_fetch_devices_x": (i, [vp, i64, i64, vp]),
+        "kg_nodes_read_device_x": (i, [vp, vp]),
         "kg_pods_evaluate_device": (i, [vp, vp, vp, vp]),
         "kg_quotas_set": (i, [vp, vp, i64]),
         "kg_quotas_read": (i, [vp, vp, i64]),

@@ -2737,11 +2737,15 @@ __global__ __launch_bounds__(kWave) void resolve_round_ds(DevTable T, DsTable DT
 
 // kg_pods_evaluate_device: DeviceShare Filter + raw Score of one pod on every node (the plugin alone)
 __global__ void evaluate_pod_ds(DsTable DT, const DsPod* __restrict__ pod, int64_t n, DsParams DP,
-                                int32_t* __restrict__ pass, int64_t* __restrict__ score) {
+                                int32_t* __restrict__ pass, int64_t* __restrict__ score,
+                                const DsXNode* __restrict__ dsx) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  int64_t raw = 0;
-  const bool ok = ds_eval(DT.d[i], *pod, DP, raw);
+  int64_t raw = 0, xraw = 0;
+  const DsNode& d = DT.d[i];
+  // (ABI 17) the RDMA / FPGA types too: AutopilotAllocator allocates every requested type, score sums them
+  const bool ok = ds_eval(d, *pod, DP, raw) && ds_eval_x(dsx[i], d.has_device != 0, *pod, DP, xraw);
+  raw += xraw;
   pass[i] = ok ? 1 : 0;
   score[i] = ok ? raw : 0;
 }
@@ -2781,7 +2785,8 @@ struct Victim {
   int64_t aux[kAux];  // ephemeral-storage and the scalar resources (KG_RES_EPHEMERAL ..)
   int32_t slot;       // the node's reservation slot the victim was allocated from, -1 = none
   int32_t nonzero;    // counted by RemovePod / AddPod: !quotav1.IsZero(PodRequestsAndLimits) and not a reserve pod
-  int32_t dminors;    // (r6) the GPU minors of its DeviceShare allocation (nodeDevice.getUsed of the victim), 0 = none
+  int32_t dminors;    // (r6) the minors of its DeviceShare allocation (nodeDevice.getUsed of the victim), 0 = none: GPU
+                      // bits 0-7, (ABI 17) RDMA 8-15, FPGA 16-23
   int32_t reserve;    // (r6) a reserve pod (DeviceShare's AddPod / RemovePod return before counting it)
   DsPod dp;           // (r6) its DeviceShare request (the per-instance allocation on each minor, ds_instance)
 };
@@ -2792,7 +2797,8 @@ struct PreExt {
   NumaParams NP;
   NumaPod np;
   const DsNode* __restrict__ ds;      // DeviceShare: AddPod / RemovePod (deviceshare/plugin.go:163-278) move the
-  DsParams DP;                        // victims' allocations in / out of preemptibleDevices[node]
+  const DsXNode* __restrict__ dsx;    // victims' allocations in / out of preemptibleDevices[node] ((ABI 17) RDMA /
+  DsParams DP;                        // FPGA too)
   DsPod dp;
   const NodePred* __restrict__ pred;  // TaintToleration / NodeAffinity: node-static Filters
   DefParams DF;
@@ -2811,6 +2817,7 @@ struct PreNode {
   bool pre_set;
   uint32_t rr_set;
   int64_t dpre[kMinors][3];  // (r6) DeviceShare preemptibleDevices[node]: gpu-core, gpu-memory, gpu-memory-ratio
+  int32_t xpre[kXTypes][kMinors];  // (ABI 17) and its RDMA / FPGA part
 };
 
 // BeforePreFilter's restore of node i for the pod (the same rsv_restore as the scheduling passes); false: invalid node
@@ -2844,6 +2851,10 @@ __device__ bool pre_node_init(PreNode& S, const DevTable& T, const RsvNode* __re
   S.rr_set = 0;
 #pragma unroll
   for (int m = 0; m < kMinors; ++m) S.dpre[m][0] = S.dpre[m][1] = S.dpre[m][2] = 0;
+#pragma unroll
+  for (int t = 0; t < kXTypes; ++t)
+#pragma unroll
+    for (int m = 0; m < kMinors; ++m) S.xpre[t][m] = 0;
   return true;
 }
 
@@ -2854,15 +2865,26 @@ __device__ __forceinline__ void pre_node_apply(PreNode& S, const Victim& v, int6
   // moves its allocation into / out of preemptibleDevices[node] (appendAllocated / subtractAllocated), unless it is a
   // reserve pod or the preemptor requests no devices (state.skip)
   if (X && X->ds && !X->dp.skip && v.dminors != 0 && !v.reserve && v.slot < 0) {
-    const DsInst in = ds_instance(X->ds[i], v.dp);
+    const int32_t gm = v.dminors & 0xFF;
+    const DsInst in = gm && !v.dp.nogpu ? ds_instance(X->ds[i], v.dp) : DsInst{0, 0, 0, 0, 0};
     if (in.ok)
 #pragma unroll
       for (int m = 0; m < kMinors; ++m)
-        if ((v.dminors >> m) & 1) {
+        if ((gm >> m) & 1) {
           S.dpre[m][0] += sign * in.core;
           S.dpre[m][1] += sign * in.mem;
           S.dpre[m][2] += sign * in.ratio;
         }
+#pragma unroll
+    for (int t = 0; t < kXTypes; ++t) {  // (ABI 17) its RDMA / FPGA minors: the per-instance request on each
+      const uint32_t xm = ((uint32_t)v.dminors >> (8 * (t + 1))) & 0xFFu;
+      if (!xm || v.dp.xq[t] == 0) continue;
+      int32_t count, per;
+      dsx_inst(v.dp.xq[t], count, per);
+#pragma unroll
+      for (int m = 0; m < kMinors; ++m)
+        if ((xm >> m) & 1u) S.xpre[t][m] += (int32_t)sign * per;
+    }
   }
   S.r.req_cpu -= sign * v.req_cpu;
   S.r.req_mem -= sign * v.req_mem;
@@ -2994,6 +3016,9 @@ __device__ uint32_t pre_node_filter(const DevTable& T, const PreNode& S, int64_t
       }
       int64_t raw = 0;
       if (!ds_eval(d, X->dp, X->DP, raw)) rej |= KG_REJECT_DEVICE;
+      else if (X->dsx && (X->dp.xq[0] | X->dp.xq[1]) &&
+               !ds_eval_x(X->dsx[i], d.has_device != 0, X->dp, X->DP, raw, S.xpre))
+        rej |= KG_REJECT_DEVICE;
     }
   }
   return rej;
@@ -3079,6 +3104,12 @@ __global__ void scatter_ds(DsTable DT, const DsNode* __restrict__ s, const int32
   if (k >= n) return;
   DT.d[idx[k]] = s[k];
 }
+__global__ void scatter_dsx(DsXNode* __restrict__ dst, const DsXNode* __restrict__ s, const int32_t* __restrict__ idx,
+                            int64_t n) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  dst[idx[k]] = s[k];
+}
 
 // kg_pods_evaluate: one pod, every node, per-plugin outputs.
 __global__ void evaluate_pod(DevTable T, const DevPod* __restrict__ pod, int64_t n, EvalParams P,
@@ -3111,13 +3142,14 @@ __global__ void unreserve_pods(DevTable T, const DevPod* __restrict__ pods, cons
                                int32_t* __restrict__ out_minors, RsvNode* __restrict__ RN, int32_t* __restrict__ out_rslot,
                                QuotaRow* __restrict__ quotas, int nq, const int64_t* __restrict__ qdev,
                                const int64_t* __restrict__ paux, GroupTable G, const GroupPod* __restrict__ gpods,
-                               int hard_w, RsvGpu* __restrict__ rg, RsvCpu* __restrict__ rcs) {
+                               int hard_w, RsvGpu* __restrict__ rg, RsvCpu* __restrict__ rcs,
+                               DsXNode* __restrict__ dsx) {
   if (blockIdx.x != 0 || threadIdx.x != 0) return;
   for (int64_t k = 0; k < n; ++k) {
     const int64_t j = idx[k];
     const uint64_t key = out_keys[j];
     if (key == 0) continue;
-    const int32_t gm = ds ? out_minors[j] : 0;  // the DeviceShare allocation, before it is cleared below
+    const int32_t gm = ds ? (out_minors[j] & 0xFF) : 0;  // the DeviceShare GPU allocation, before it is cleared below
     const uint32_t w = key_node(key);
     const DevPod p = pods[j];
     Row r = load_row(T, w);  // NodeInfo.RemovePod + podAssignCache.unAssign (pod_assign_cache.go:119-131)
@@ -3155,10 +3187,10 @@ __global__ void unreserve_pods(DevTable T, const DevPod* __restrict__ pods, cons
     if (ds && out_minors[j]) {  // deviceshare/plugin.go:440-455, SubtractWithNonNegativeResult per minor
       const DsPod dp = dpods[j];
       DsNode dn = ds[w];
-      if (!dp.skip && !dp.error && dn.has_device) {
+      if (!dp.skip && !dp.error && !dp.nogpu && dn.has_device && gm) {
         const DsInst in = ds_instance(dn, dp);
         for (int m = 0; m < kMinors; ++m) {
-          if (!((out_minors[j] >> m) & 1)) continue;
+          if (!((gm >> m) & 1)) continue;
           const int64_t c = dn.ucore[m] - in.core, q = dn.uratio[m] - in.ratio, b = dn.umem[m] - in.mem;
           dn.ucore[m] = (int32_t)(c > 0 ? c : 0);
           dn.uratio[m] = (int32_t)(q > 0 ? q : 0);
@@ -3166,6 +3198,8 @@ __global__ void unreserve_pods(DevTable T, const DevPod* __restrict__ pods, cons
         }
         ds[w] = dn;
       }
+      // (ABI 17) the RDMA / FPGA minors of the packed record
+      if (dsx && ((uint32_t)out_minors[j] >> 8)) ds_release_x(dsx[w], dp, out_minors[j]);
       out_minors[j] = 0;
     }
     if (RN && out_rslot[j] >= 0) {  // reservation/plugin.go:561-583 → RemoveAssignedPod (reservation_info.go:328-339)
@@ -3475,6 +3509,8 @@ struct kg_engine {
   DsParams DP{};
   DevBuf<DsNode> ds_d;
   std::vector<DsNode> ds_host;
+  DevBuf<DsXNode> dsx_d;                         // (ABI 17) RDMA / FPGA devices [cap]
+  bool dsx_q = false;                            // (ABI 17) the staged queue holds RDMA / FPGA requests: per-pod pass
   DevBuf<DsPod> dpods;
   DevBuf<int32_t> out_minors;  // [staged + kMaxB]
   DevBuf<uint64_t> dsmax;      // [B][nt_local]
@@ -4059,16 +4095,23 @@ int decode_ds_pod(const kg_pod& p, DsPod& d) {
   const int64_t* q = p.device_requests;
   for (int r = 0; r < KG_DEV_RES_MAX; ++r)
     if (q[r] < 0) return fail(KG_E_INVALID, "negative device request");
-  if (q[KG_DEV_FPGA] || q[KG_DEV_RDMA]) return fail(KG_E_UNSUPPORTED, "FPGA / RDMA device requests are not accelerated");
+  auto pct_ok = [](int64_t v) { return !(v > 100 && v % 100 != 0); };
+  // (ABI 17) RDMA / FPGA (utils.go:47-58: one resource each, ValidatePercentageResource): the default handler's types
+  const int64_t xq[kXTypes] = {q[KG_DEV_RDMA], q[KG_DEV_FPGA]};
+  for (int t = 0; t < kXTypes; ++t) {
+    if (xq[t] > (1 << 20)) return fail(KG_E_UNSUPPORTED, "RDMA / FPGA request beyond the accelerated range");
+    if (xq[t] && !pct_ok(xq[t])) d.error = 1;  // "invalid resource unit"
+    d.xq[t] = (int32_t)xq[t];
+  }
   enum { NV = 1, DCU = 2, KG = 4, CORE = 8, MEM = 16, RATIO = 32 };
   unsigned comb = 0;
   for (int r = 0; r < 6; ++r)
     if (q[r]) comb |= 1u << r;  // KG_DEV_* order = flag order
   if (!comb) {
-    d.skip = 1;
+    d.nogpu = 1;
+    d.skip = (xq[0] | xq[1]) == 0 ? 1 : 0;  // state.skip: no device request of any type
     return 0;
   }
-  auto pct_ok = [](int64_t v) { return !(v > 100 && v % 100 != 0); };
   if ((q[KG_DEV_KOORD_GPU] && !pct_ok(q[KG_DEV_KOORD_GPU])) || (q[KG_DEV_GPU_CORE] && !pct_ok(q[KG_DEV_GPU_CORE])) ||
       (q[KG_DEV_GPU_MEMORY_RATIO] && !pct_ok(q[KG_DEV_GPU_MEMORY_RATIO]))) {
     d.error = 1;
@@ -4091,7 +4134,19 @@ int decode_ds_pod(const kg_pod& p, DsPod& d) {
 }
 
 // One node's Device object + deviceUsed → device row (buildDeviceResources, device_cache.go:505-523)
-int decode_node_device(const kg_node_device& n, DsNode& d) {
+int decode_node_device(const kg_node_device& n, DsNode& d, DsXNode& x) {
+  std::memset(&x, 0, sizeof(x));
+  if (n.has_device)  // (ABI 17) RDMA / FPGA DeviceInfos (buildDeviceResources: an unhealthy device has no resources)
+    for (int t = 0; t < kXTypes; ++t)
+      for (int m = 0; m < KG_MAX_MINORS; ++m) {
+        if (!n.x_present[t][m]) continue;
+        if (n.x_total[t][m] < 0 || n.x_used[t][m] < 0) return fail(KG_E_INVALID, "negative device quantity");
+        if (n.x_total[t][m] >= (1 << 30) || n.x_used[t][m] >= (1 << 30))
+          return fail(KG_E_UNSUPPORTED, "device quantity beyond the accelerated range");
+        x.listed[t] |= 1u << m;
+        x.t[t][m] = n.x_healthy[t][m] ? (int32_t)n.x_total[t][m] : 0;
+        x.u[t][m] = (int32_t)n.x_used[t][m];
+      }
   std::memset(&d, 0, sizeof(d));
   d.first = -1;
   d.has_device = n.has_device ? 1 : 0;
@@ -4795,6 +4850,7 @@ constexpr int64_t kExactSmall = 2;  // schedule calls of at most this many pods 
 RsvExt rsv_ext(kg_engine* e) {
   RsvExt X;
   X.ds = e->ds_on ? e->ds_d.p : nullptr;
+  X.dsx = e->ds_on ? e->dsx_d.p : nullptr;
   X.dpods = e->ds_on ? e->dpods.p : nullptr;
   X.DP = e->DP;
   X.quotas = e->quotas.p;
@@ -5513,7 +5569,12 @@ static int engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank,
   e->DP.w_mem = (int32_t)c.ds_scoring_weights[1];
   e->DP.w_ratio = (int32_t)c.ds_scoring_weights[2];
   e->DP.most = (int32_t)(c.ds_scoring_strategy == KG_STRATEGY_MOST_ALLOCATED);
+  e->DP.w_x[KG_XTYPE_RDMA] = (int32_t)c.ds_scoring_weights_x[KG_XTYPE_RDMA];
+  e->DP.w_x[KG_XTYPE_FPGA] = (int32_t)c.ds_scoring_weights_x[KG_XTYPE_FPGA];
   if (e->ds_on) {
+    if (int rc = e->dsx_d.ensure(cap)) return bail(rc);
+    if (hipMemsetAsync(e->dsx_d.p, 0, cap * sizeof(DsXNode), e->stream) != hipSuccess)
+      return bail(fail(KG_E_DEVICE, "hipMemset"));
     if (int rc = e->ds_d.ensure(cap)) return bail(rc);
     e->ds_host.assign(cap, DsNode{});
     for (auto& d : e->ds_host) d.first = -1;
@@ -5686,6 +5747,7 @@ void kg_engine_destroy(kg_engine* e) {
   e->out_cpus.release();
   e->out_nrec.release();
   e->ds_d.release();
+  e->dsx_d.release();
   e->quotas.release();
   e->qdev.release();
   e->dpods.release();
@@ -5918,7 +5980,8 @@ int kg_pods_unreserve(kg_engine* e, int64_t first, int64_t count, const uint8_t*
                                         (e->ds_on || e->rsv_on) ? e->qdev.p : nullptr, e->paux.p,
                                         GroupTable{e->grp_d.p, e->capacity}, e->grp_on ? e->gpods.p : nullptr,
                                         e->GP.hard_w, e->rsv_on && e->ds_on && e->rgpu_nodes > 0 ? e->rsv_g.p : nullptr,
-                                        e->rsv_on && e->numa_on && e->rcpu_nodes > 0 ? e->rsv_c.p : nullptr);
+                                        e->rsv_on && e->numa_on && e->rcpu_nodes > 0 ? e->rsv_c.p : nullptr,
+                                        e->ds_on ? e->dsx_d.p : nullptr);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(e->stream));
   e->eph_dirty |= e->eph_any;  // a release may end an ephemeral-storage overcommit
@@ -5981,10 +6044,13 @@ int kg_pods_stage(kg_engine* e, const kg_pod* pods, int64_t n) {
     HIP_TRY(hipMemsetAsync(e->out_nrec.p, 0, (n + kMaxB) * kNumaRecWords * 8, e->stream));
   }
   std::vector<DsPod> hd;
+  e->dsx_q = false;
   if (e->ds_on) {
     hd.resize(std::max<int64_t>(n, 1));
-    for (int64_t k = 0; k < n; ++k)
+    for (int64_t k = 0; k < n; ++k) {
       if (int rc = decode_ds_pod(pods[k], hd[k])) return rc;
+      e->dsx_q |= (hd[k].xq[0] | hd[k].xq[1]) != 0;  // (ABI 17) RDMA / FPGA pods take the per-pod pass
+    }
     if (int rc = e->dpods.ensure(n + kMaxB)) return rc;
     if (int rc = e->out_minors.ensure(n + kMaxB)) return rc;
     if (n > 0) HIP_TRY(hipMemcpyAsync(e->dpods.p, hd.data(), n * sizeof(DsPod), hipMemcpyHostToDevice, e->stream));
@@ -6164,10 +6230,17 @@ static int schedule_staged_impl(kg_engine* e, int64_t first, int64_t count, kg_s
   // their cluster-wide minimum / count and min-max normalisation)
   // (ABI 13) GPU-holding reservations: the per-pod pass (the batched rounds keep no DeviceShare restore)
   // (ABI 15) reservations holding cpusets: the per-pod pass too (the batched rounds compile the preferred-cpu path out)
-  if (e->exact_on && e->xr_on && !e->grp_on && !e->rsv_ext_q && e->rgpu_nodes == 0 && e->rcpu_nodes == 0 &&
-      count >= kXrMin && e->n_nodes > 0)
+  // (ABI 17) RDMA / FPGA requests: the per-pod pass (the batched rounds and the round engine carry the GPU type only)
+  if (e->dsx_q && count > 0) {
+    if (e->rsv_on && e->rgpu_nodes > 0)
+      return fail(KG_E_UNSUPPORTED, "RDMA / FPGA requests with reservations that hold GPUs keep the Go path");
+    if (!e->exact_on && e->n_ranks > 1)
+      return fail(KG_E_UNSUPPORTED, "RDMA / FPGA requests on a multi-rank round-engine profile keep the Go path");
+  }
+  if (e->exact_on && e->xr_on && !e->grp_on && !e->rsv_ext_q && !e->dsx_q && e->rgpu_nodes == 0 &&
+      e->rcpu_nodes == 0 && count >= kXrMin && e->n_nodes > 0)
     return run_xr(e, first, count, stats, t0);
-  if (e->exact_on || (count <= kExactSmall && e->n_ranks == 1)) return run_rsv(e, first, count, stats, t0);
+  if (e->exact_on || e->dsx_q || (count <= kExactSmall && e->n_ranks == 1)) return run_rsv(e, first, count, stats, t0);
   RoundGeom g;
   if (int rc = prepare_rounds(e, g)) return rc;
   const int64_t end = first + count;
@@ -6393,17 +6466,22 @@ int kg_nodes_device_upsert(kg_engine* e, const kg_node_device* dev, const int32_
   if (!e->ds_on) return fail(KG_E_INVALID, "the profile does not enable DeviceShare");
   if (n == 0) return 0;
   std::vector<DsNode> h(n);
+  std::vector<DsXNode> hx(n);
   for (int64_t k = 0; k < n; ++k) {
     if (idx[k] < 0 || idx[k] >= e->capacity) return fail(KG_E_INVALID, "node index %d outside capacity", idx[k]);
-    if (int rc = decode_node_device(dev[k], h[k])) return rc;
+    if (int rc = decode_node_device(dev[k], h[k], hx[k])) return rc;
   }
   DevBuf<uint8_t> b;
-  if (int rc = b.ensure(n * (sizeof(DsNode) + 4))) return rc;
+  if (int rc = b.ensure(n * (sizeof(DsNode) + sizeof(DsXNode) + 4))) return rc;
   DsNode* dd = reinterpret_cast<DsNode*>(b.p);
-  int32_t* di = reinterpret_cast<int32_t*>(b.p + n * sizeof(DsNode));
+  DsXNode* dx = reinterpret_cast<DsXNode*>(b.p + n * sizeof(DsNode));
+  int32_t* di = reinterpret_cast<int32_t*>(b.p + n * (sizeof(DsNode) + sizeof(DsXNode)));
   HIP_TRY(hipMemcpyAsync(dd, h.data(), n * sizeof(DsNode), hipMemcpyHostToDevice, e->stream));
+  HIP_TRY(hipMemcpyAsync(dx, hx.data(), n * sizeof(DsXNode), hipMemcpyHostToDevice, e->stream));
   HIP_TRY(hipMemcpyAsync(di, idx, n * 4, hipMemcpyHostToDevice, e->stream));
   scatter_ds<<<(unsigned)((n + 255) / 256), 256, 0, e->stream>>>(DsTable{e->ds_d.p}, dd, di, n);
+  HIP_TRY(hipGetLastError());
+  scatter_dsx<<<(unsigned)((n + 255) / 256), 256, 0, e->stream>>>(e->dsx_d.p, dx, di, n);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(e->stream));
   b.release();
@@ -6437,7 +6515,39 @@ int kg_results_fetch_devices(kg_engine* e, int64_t first, int64_t count, int32_t
   if (count > 0) {
     HIP_TRY(hipMemcpyAsync(out_minor_mask, e->out_minors.p + first, count * 4, hipMemcpyDeviceToHost, e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
+    for (int64_t k = 0; k < count; ++k) out_minor_mask[k] &= 0xFF;  // the GPU byte of the packed record
   }
+  return 0;
+}
+
+int kg_results_fetch_devices_x(kg_engine* e, int64_t first, int64_t count, int32_t* out) {
+  if (!e || (count > 0 && !out)) return fail(KG_E_INVALID, "null argument");
+  if (first < 0 || count < 0 || first + count > e->n_staged) return fail(KG_E_INVALID, "staged range");
+  if (!e->ds_on) {
+    std::memset(out, 0, (size_t)count * kXTypes * 4);
+    return 0;
+  }
+  if (count > 0) {
+    std::vector<int32_t> h((size_t)count);
+    HIP_TRY(hipMemcpyAsync(h.data(), e->out_minors.p + first, count * 4, hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    for (int64_t k = 0; k < count; ++k)
+      for (int t = 0; t < kXTypes; ++t) out[k * kXTypes + t] = ((uint32_t)h[k] >> (8 * (t + 1))) & 0xFFu;
+  }
+  return 0;
+}
+
+int kg_nodes_read_device_x(kg_engine* e, int64_t* x_used) {
+  if (!e || !x_used) return fail(KG_E_INVALID, "null argument");
+  if (!e->ds_on) return fail(KG_E_INVALID, "the profile does not enable DeviceShare");
+  const int64_t n = e->n_nodes;
+  if (n == 0) return 0;
+  std::vector<DsXNode> h(n);
+  HIP_TRY(hipMemcpyAsync(h.data(), e->dsx_d.p, n * sizeof(DsXNode), hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  for (int64_t i = 0; i < n; ++i)
+    for (int t = 0; t < kXTypes; ++t)
+      for (int m = 0; m < KG_MAX_MINORS; ++m) x_used[(i * kXTypes + t) * KG_MAX_MINORS + m] = h[i].u[t][m];
   return 0;
 }
 
@@ -6453,7 +6563,7 @@ int kg_pods_evaluate_device(kg_engine* e, const kg_pod* pod, int32_t* out_pass, 
   DsPod* d = reinterpret_cast<DsPod*>(e->scratch64.p + n);
   HIP_TRY(hipMemcpyAsync(d, &dp, sizeof(dp), hipMemcpyHostToDevice, e->stream));
   evaluate_pod_ds<<<(unsigned)((n + 255) / 256), 256, 0, e->stream>>>(DsTable{e->ds_d.p}, d, n, e->DP, e->scratch32.p,
-                                                                      e->scratch64.p);
+                                                                      e->scratch64.p, e->dsx_d.p);
   HIP_TRY(hipGetLastError());
   std::vector<int32_t> ps(n);
   std::vector<int64_t> sc(n);
@@ -7025,7 +7135,7 @@ static int preempt_prepare(kg_engine* e, const kg_pod* pod, const kg_pod* victim
   }
   if (e->ds_on) {
     if (int rc = decode_ds_pod(*pod, X.dp)) return rc;
-    X.ds = e->ds_d.p, X.DP = e->DP;
+    X.ds = e->ds_d.p, X.dsx = e->dsx_d.p, X.DP = e->DP;
   } else {
     for (int r = 0; r < KG_DEV_RES_MAX; ++r)
       if (pod->device_requests[r] != 0 && e->cfg.fit_filter)
@@ -7043,7 +7153,7 @@ static int preempt_prepare(kg_engine* e, const kg_pod* pod, const kg_pod* victim
     const int32_t s = victim_slot ? victim_slot[k] : -1;
     if (s < -1 || s >= KG_MAX_RSV_SLOTS) return fail(KG_E_INVALID, "victim %lld: reservation slot %d", (long long)k, s);
     const int32_t m = victim_minors ? victim_minors[k] : 0;
-    if (m < 0 || m >= (1 << kMinors)) return fail(KG_E_INVALID, "victim %lld: minors 0x%x", (long long)k, m);
+    if (m < 0 || m >= (1 << (8 * (1 + kXTypes)))) return fail(KG_E_INVALID, "victim %lld: minors 0x%x", (long long)k, m);
     bool nz = false;
     for (int q = 0; q < KG_RES_MAX; ++q) nz |= victims[k].requests[q] != 0;
     // (r5) RemovePod returns before counting a reserve pod (reservation/plugin.go:286): the framework still

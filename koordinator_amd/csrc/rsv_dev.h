@@ -122,6 +122,7 @@ __device__ __forceinline__ CpuSet rsv_reserved_cpus(const RsvCpu& c) {
 // DeviceShare + ElasticQuota context of the C5 pass (ds = nullptr: no DeviceShare in the profile; nq = 0: no quotas)
 struct RsvExt {
   const DsNode* __restrict__ ds;       // [cap] node devices (deviceUsed updated by Reserve)
+  DsXNode* __restrict__ dsx;           // (ABI 17) [cap] RDMA / FPGA devices (per-pod pass only)
   const DsPod* __restrict__ dpods;     // [pods] DeviceShare preFilterState
   DsParams DP;
   QuotaRow* __restrict__ quotas;       // [nq]
@@ -480,6 +481,15 @@ __device__ __forceinline__ RsvOut rsv_eval_node(const DevTable& T, const RsvNode
     // FilterReservation: a pod with device requests can use only a GPU-holding reservation DeviceShare can allocate
     // from (plugin.go:333-380: "no relevant Reservation information" for the others)
     sat &= dsok;
+    // (ABI 17) the RDMA / FPGA types of the request (the host routes such queues here and refuses them next to
+    // GPU-holding reservations): Allocate needs every requested type, Score sums them
+    if constexpr (kExt) {
+      if (X.dsx && (dp->xq[0] | dp->xq[1])) {
+        int64_t xraw = 0;
+        if (!ds_eval_x(X.dsx[i], d.has_device != 0, *dp, X.DP, xraw)) return o;
+        dsraw += xraw;
+      }
+    }
   }
   int64_t nsc = 0;        // NodeNUMAResource's Score without preferred cpus
   NumaHint naff{0, 1, 0, 0};
@@ -624,6 +634,7 @@ __device__ __forceinline__ uint64_t rsv_partials_sum(const uint64_t* __restrict_
 __device__ __forceinline__ int32_t rsv_ds_reserve(DsNode& dn, const DsPod& dp, const DsParams& DP) {
   if (dp.skip || !dn.has_device) return 0;
   if (dp.error) return -1;
+  if (dp.nogpu) return 0;  // (ABI 17) only RDMA / FPGA requests: no GPU minor
   const DsInst in = ds_instance(dn, dp);
   if (!in.ok) return -1;
   int64_t sc[kMinors];
@@ -704,6 +715,7 @@ __device__ __forceinline__ int32_t rsv_ds_reserve_gpu(DsNode& dn, const DsPod& d
                                                       int nominated, bool restricted, bool reserve_pod) {
   if (dp.skip || !dn.has_device) return 0;
   if (dp.error) return -1;
+  if (dp.nogpu) return 0;  // (ABI 17) only RDMA / FPGA requests: no GPU minor
   const DsInst in = ds_instance(dn, dp);
   if (!in.ok) return -1;
   int32_t mask = -1;
@@ -815,12 +827,21 @@ __device__ __forceinline__ bool rsv_reserve(const DevTable& T, RsvNode* __restri
     }
     if (!done) minors = rsv_ds_reserve(dn, X.dpods[j], X.DP);
     KG_LANE_SUB(diag_j, 2);
-    if (minors < 0) {
+    // (ABI 17) the RDMA / FPGA types, on a copy: every requested type is allocated or none is
+    int32_t xminors = 0;
+    DsXNode xn;
+    const bool xreq = X.dsx && (X.dpods[j].xq[0] | X.dpods[j].xq[1]);
+    if (xreq && minors >= 0) {
+      xn = X.dsx[w];
+      xminors = ds_reserve_x(xn, dn.has_device != 0, X.dpods[j], X.DP);
+    }
+    if (minors < 0 || xminors < 0) {
       X.out_minors[j] = 0;
       return false;
     }
     if (minors) const_cast<DsNode*>(X.ds)[w] = dn;
-    X.out_minors[j] = minors;
+    if (xminors) X.dsx[w] = xn;
+    X.out_minors[j] = minors | xminors;
     gpu_minors = minors;
   }
   if (NUMA && X.ns) {

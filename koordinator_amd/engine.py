@@ -293,6 +293,18 @@ class Engine:
         check(self.lib, self.lib.kg_results_fetch_devices(self.h, int(first), int(count), ptr(out)))
         return out
 
+    def fetch_devices_x(self, first: int, count: int) -> np.ndarray:
+        """int32[count, 2]: the RDMA / FPGA minor bitmasks DeviceShare Reserve allocated to each staged pod (ABI 17)."""
+        out = np.zeros((count, abi.DEV_XTYPES), dtype=np.int32)
+        check(self.lib, self.lib.kg_results_fetch_devices_x(self.h, int(first), int(count), ptr(out)))
+        return out
+
+    def read_devices_x(self) -> np.ndarray:
+        """int64[n, 2, 8]: the RDMA / FPGA deviceUsed from the device (ABI 17)."""
+        out = np.zeros((self.num_nodes, abi.DEV_XTYPES, abi.MAX_MINORS), dtype=np.int64)
+        check(self.lib, self.lib.kg_nodes_read_device_x(self.h, ptr(out)))
+        return out
+
     def read_devices(self):
         """(used core, used memory, used ratio), int64[n, 8] each, from the device."""
         n = self.num_nodes

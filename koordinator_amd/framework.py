@@ -168,6 +168,8 @@ def build_config(la: LoadAwareSchedulingArgs | None = None, fit: NodeResourcesFi
     r["ds_scoring_weights"] = [ds.scoring_resources.get("koordinator.sh/gpu-core", 0),
                                ds.scoring_resources.get("koordinator.sh/gpu-memory", 0),
                                ds.scoring_resources.get("koordinator.sh/gpu-memory-ratio", 0)]
+    r["ds_scoring_weights_x"] = [ds.scoring_resources.get("koordinator.sh/rdma", 0),
+                                 ds.scoring_resources.get("koordinator.sh/fpga", 0)]
     return c
 
 
@@ -289,12 +291,21 @@ def cpuset_of(words) -> list:
     return out
 
 
-def make_node_device(gpus: list | None = None, has_device: bool = True) -> np.ndarray:
+def make_node_device(gpus: list | None = None, has_device: bool = True, rdma: list | None = None,
+                     fpga: list | None = None) -> np.ndarray:
     """DeviceShare view of one node: gpus = [{"minor": m, "healthy": True, "total": {core, memory, ratio},
-    "used": {core, memory, ratio}}, ...] in koordinator.sh/gpu-* units (core / ratio percent, memory bytes)."""
+    "used": {core, memory, ratio}}, ...] in koordinator.sh/gpu-* units (core / ratio percent, memory bytes).
+    (ABI 17) rdma / fpga = [{"minor": m, "healthy": True, "total": percent, "used": percent}, ...]."""
     d = np.zeros(1, dtype=abi.NODE_DEVICE_DTYPE)
     r = d[0]
     r["has_device"] = int(has_device)
+    for t, devs in ((abi.XTYPE_RDMA, rdma), (abi.XTYPE_FPGA, fpga)):
+        for g in devs or []:
+            m = int(g["minor"])
+            r["x_present"][t, m] = 1
+            r["x_healthy"][t, m] = int(g.get("healthy", True))
+            r["x_total"][t, m] = int(g.get("total", 0))
+            r["x_used"][t, m] = int(g.get("used", 0))
     for g in gpus or []:
         m = int(g["minor"])
         r["present"][m] = 1

@@ -315,6 +315,32 @@ def make_gpu_pods(n_pods: int, seed: int = BASE_SEED + 7, base: np.ndarray | Non
     return p
 
 
+def add_x_devices(dev: np.ndarray, frac: float = 0.5, seed: int = BASE_SEED + 26) -> None:
+    """(ABI 17) RDMA / FPGA devices, in place: `frac` of the nodes with a Device object get 1–4 RDMA NICs and, half of
+    them, 1–2 FPGAs at minors 0.., each koordinator.sh/rdma / fpga 100 with 0–100 % (steps of 25) used, 2 % unhealthy."""
+    rng = np.random.default_rng(seed)
+    for i in np.nonzero(dev["has_device"] != 0)[0]:
+        if rng.random() >= frac:
+            continue
+        for t, k in ((abi.XTYPE_RDMA, int(rng.integers(1, 5))), (abi.XTYPE_FPGA, int(rng.integers(1, 3)) * int(rng.random() < 0.5))):
+            for m in range(k):
+                dev["x_present"][i, t, m] = 1
+                dev["x_healthy"][i, t, m] = int(rng.random() >= 0.02)
+                dev["x_total"][i, t, m] = 100
+                dev["x_used"][i, t, m] = int(rng.integers(0, 5)) * 25
+
+
+def add_x_requests(pods: np.ndarray, frac: float = 0.3, seed: int = BASE_SEED + 27) -> None:
+    """(ABI 17) RDMA / FPGA requests, in place: `frac` of the pods request koordinator.sh/rdma ∈ {25, 50, 100, 200}
+    (a fifth of them also koordinator.sh/fpga 50 or 100), with or without a GPU share."""
+    rng = np.random.default_rng(seed)
+    n = len(pods)
+    x = rng.random(n) < frac
+    pods["device_requests"][:, abi.DEV_RDMA] = np.where(x, rng.choice([25, 50, 100, 200], n), 0)
+    f = x & (rng.random(n) < 0.2)
+    pods["device_requests"][:, abi.DEV_FPGA] = np.where(f, rng.choice([50, 100], n), 0)
+
+
 def load_gpu_into(engine, cluster: Cluster, dev: np.ndarray):
     load_into(engine, cluster)
     engine.upsert_devices(dev)

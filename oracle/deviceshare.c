@@ -17,12 +17,20 @@ int or_ds_pod_init(const kg_pod* pod, or_ds_pod* out) {
   const int64_t* q = pod->device_requests;
   for (int r = 0; r < KG_DEV_RES_MAX; r++)
     if (q[r] < 0) { out->error = 1; return 0; }
-  if (q[KG_DEV_FPGA] != 0 || q[KG_DEV_RDMA] != 0) out->unsupported = 1;
+  /* (ABI 17) RDMA / FPGA: one resource per type (DeviceResourceNames, utils.go:47-58), ValidatePercentageResource */
+  out->xq[KG_XTYPE_RDMA] = q[KG_DEV_RDMA];
+  out->xq[KG_XTYPE_FPGA] = q[KG_DEV_FPGA];
+  for (int t = 0; t < KG_DEV_XTYPES; t++)
+    if (out->xq[t] && !valid_percentage(out->xq[t])) out->error = 1; /* "invalid resource unit" */
   static const int flag_of[6] = {F_NVIDIA, F_DCU, F_KGPU, F_CORE, F_MEM, F_RATIO};
   unsigned comb = 0;
   for (int r = 0; r < 6; r++)
     if (q[r] != 0) comb |= (unsigned)flag_of[r]; /* quotav1.RemoveZeros */
-  if (comb == 0) { out->skip = !out->unsupported; return 0; }
+  if (comb == 0) {
+    out->nogpu = 1;
+    out->skip = out->xq[0] == 0 && out->xq[1] == 0; /* state.skip: no request of any device type */
+    return 0;
+  }
   if ((q[KG_DEV_KOORD_GPU] && !valid_percentage(q[KG_DEV_KOORD_GPU])) ||
       (q[KG_DEV_GPU_CORE] && !valid_percentage(q[KG_DEV_GPU_CORE])) ||
       (q[KG_DEV_GPU_MEMORY_RATIO] && !valid_percentage(q[KG_DEV_GPU_MEMORY_RATIO]))) {
@@ -111,6 +119,8 @@ int or_ds_filter(const kg_node_device* d, const or_ds_pod* p) {
   if (p->skip) return 1;
   if (p->error) return 0;
   if (!d->has_device) return 0;
+  if (!or_dsx_filter(d, p, NULL)) return 0; /* (ABI 17) every requested type must allocate */
+  if (p->nogpu) return 1;
   const or_ds_inst in = or_ds_instance(d, p);
   if (!in.ok) return 0;
   if (all_free_zero(d)) return 0; /* nodeDevice.filter drops the type (device_cache.go:358-360) */
@@ -145,7 +155,7 @@ static int64_t scorer(int strategy, const int64_t w[3], const int64_t total[3], 
 }
 
 int64_t or_ds_score(const kg_node_device* d, const or_ds_pod* p, int strategy, const int64_t w[3]) {
-  if (p->skip || p->error || !d->has_device) return 0;
+  if (p->skip || p->error || !d->has_device || p->nogpu) return 0;
   const or_ds_inst in = or_ds_instance(d, p);
   if (!in.ok || all_free_zero(d)) return 0;
   int64_t total[3] = {0, 0, 0}, free_[3] = {0, 0, 0};
@@ -172,6 +182,7 @@ int64_t or_ds_score_minor(const kg_node_device* d, int m, const or_ds_pod* p, co
 int32_t or_ds_reserve(kg_node_device* d, const or_ds_pod* p, int strategy, const int64_t w[3]) {
   if (p->skip || !d->has_device) return 0;
   if (p->error) return -1;
+  if (p->nogpu) return 0;
   const or_ds_inst in = or_ds_instance(d, p);
   if (!in.ok || all_free_zero(d)) return -1;
   /* scoreDevices → sortDeviceResourcesByMinor (score desc, minor asc) → first `count` that fit */
@@ -203,6 +214,9 @@ int32_t or_ds_reserve(kg_node_device* d, const or_ds_pod* p, int strategy, const
 
 void or_ds_release(kg_node_device* d, const or_ds_pod* p, int32_t minors) {
   if (p->skip || !d->has_device || p->error) return;
+  or_dsx_release(d, p, minors); /* (ABI 17) the RDMA / FPGA bytes of the packed mask */
+  minors &= 0xFF;
+  if (p->nogpu || !minors) return;
   const or_ds_inst in = or_ds_instance(d, p); /* the per-instance request Reserve added (node totals only) */
   for (int m = 0; m < KG_MAX_MINORS; m++) {
     if (!(minors >> m & 1)) continue;
@@ -219,6 +233,132 @@ void or_default_normalize(int64_t* s, int64_t n) {
     if (s[i] > mx) mx = s[i];
   if (mx == 0) return;
   for (int64_t i = 0; i < n; i++) s[i] = 100 * s[i] / mx;
+}
+
+/* ---- (ABI 17) RDMA / FPGA: DefaultDeviceHandler (devicehandler_default.go:45-92) without hints ------------------
+ * CalcDesiredRequestsAndCount: a request q > 100 and a multiple of 100 is q / 100 instances of 100, else one of q;
+ * "Insufficient %s devices" when the node lists no device of the type.  deviceTotal of an unhealthy device is an empty
+ * ResourceList (device_cache.go:513-515); free = SubtractWithNonNegativeResult(total, used − preemptible). */
+static void x_inst(int64_t q, int* count, int64_t* per) {
+  const int multi = q > 100 && q % 100 == 0;
+  *count = multi ? (int)(q / 100) : 1;
+  *per = multi ? 100 : q;
+}
+static int64_t xtot(const kg_node_device* d, int t, int m) {
+  return d->x_present[t][m] && d->x_healthy[t][m] ? d->x_total[t][m] : 0;
+}
+static int64_t xfree(const kg_node_device* d, int t, int m, const int64_t (*pre)[KG_MAX_MINORS]) {
+  return sub0(xtot(d, t, m), sub0(d->x_used[t][m], pre ? pre[t][m] : 0));
+}
+static int x_listed(const kg_node_device* d, int t) {
+  for (int m = 0; m < KG_MAX_MINORS; m++)
+    if (d->x_present[t][m]) return 1;
+  return 0;
+}
+/* the scorer over the type's one resource: the other configured resources see a zero total (skipped), so the weighted
+ * mean is the resource's own least / most requested score when its weight is set, 0 otherwise (scoring.go:183-304) */
+static int64_t x_scorer(int strategy, int64_t w, int64_t total, int64_t free_, int64_t req) {
+  if (w == 0 || total == 0) return 0;
+  const int64_t rq = total >= free_ ? total - free_ + req : total;
+  const int64_t s = strategy == KG_STRATEGY_MOST_ALLOCATED ? most_requested(rq, total) : least_requested(rq, total);
+  return s * w / w;
+}
+
+int or_dsx_filter(const kg_node_device* d, const or_ds_pod* p, const int64_t (*pre)[KG_MAX_MINORS]) {
+  if (p->skip) return 1;
+  if (p->error) return 0;
+  for (int t = 0; t < KG_DEV_XTYPES; t++) {
+    if (!p->xq[t]) continue;
+    if (!d->has_device || !x_listed(d, t)) return 0;
+    int count;
+    int64_t per;
+    x_inst(p->xq[t], &count, &per);
+    int any = 0, n = 0;
+    for (int m = 0; m < KG_MAX_MINORS; m++) {
+      if (!d->x_present[t][m]) continue;
+      const int64_t f = xfree(d, t, m, pre);
+      any |= f != 0;
+      n += f != 0 && per <= f; /* defaultAllocateDevices: skip zero free, LessThanOrEqual(request, free) */
+    }
+    if (!any || n < count) return 0; /* nodeDevice.filter drops an all-zero type; "Insufficient %s devices" */
+  }
+  return 1;
+}
+
+int64_t or_dsx_score(const kg_node_device* d, const or_ds_pod* p, int strategy, const int64_t w[KG_DEV_XTYPES]) {
+  if (p->skip || p->error || !d->has_device) return 0;
+  int64_t sum = 0;
+  for (int t = 0; t < KG_DEV_XTYPES; t++) {
+    if (!p->xq[t] || !x_listed(d, t)) continue;
+    int count;
+    int64_t per, T = 0, F = 0;
+    x_inst(p->xq[t], &count, &per);
+    for (int m = 0; m < KG_MAX_MINORS; m++) {
+      if (!d->x_present[t][m]) continue;
+      T += xtot(d, t, m);
+      F += xfree(d, t, m, NULL);
+    }
+    sum += x_scorer(strategy, w[t], T, F, per); /* AutopilotAllocator.score: finalScore += per type */
+  }
+  return sum;
+}
+
+int32_t or_dsx_reserve(kg_node_device* d, const or_ds_pod* p, int strategy, const int64_t w[KG_DEV_XTYPES]) {
+  if (p->skip || !d->has_device) return 0;
+  if (p->error) return -1;
+  int32_t taken[KG_DEV_XTYPES] = {0, 0};
+  for (int t = 0; t < KG_DEV_XTYPES; t++) {
+    if (!p->xq[t]) continue;
+    if (!x_listed(d, t)) return -1;
+    int count;
+    int64_t per;
+    x_inst(p->xq[t], &count, &per);
+    /* scoreDevices → sortDeviceResourcesByMinor (score desc, minor asc) → the first `count` that fit */
+    int order[KG_MAX_MINORS], n = 0, any = 0;
+    int64_t sc[KG_MAX_MINORS];
+    for (int m = 0; m < KG_MAX_MINORS; m++) {
+      if (!d->x_present[t][m]) continue;
+      const int64_t f = xfree(d, t, m, NULL);
+      any |= f != 0;
+      sc[m] = x_scorer(strategy, w[t], xtot(d, t, m), f, per);
+      int k = n++;
+      while (k > 0 && sc[order[k - 1]] < sc[m]) { order[k] = order[k - 1]; k--; }
+      order[k] = m;
+    }
+    if (!any) return -1;
+    int got = 0;
+    for (int k = 0; k < n && got < count; k++) {
+      const int m = order[k];
+      const int64_t f = xfree(d, t, m, NULL);
+      if (f == 0 || per > f) continue;
+      taken[t] |= 1 << m;
+      got++;
+    }
+    if (got < count) return -1;
+  }
+  int32_t out = 0;
+  for (int t = 0; t < KG_DEV_XTYPES; t++) {
+    if (!taken[t]) continue;
+    int count;
+    int64_t per;
+    x_inst(p->xq[t], &count, &per);
+    for (int m = 0; m < KG_MAX_MINORS; m++)
+      if ((taken[t] >> m) & 1) d->x_used[t][m] += per; /* updateCacheUsed */
+    out |= taken[t] << (8 * (t + 1));
+  }
+  return out;
+}
+
+void or_dsx_release(kg_node_device* d, const or_ds_pod* p, int32_t packed) {
+  for (int t = 0; t < KG_DEV_XTYPES; t++) {
+    const int32_t mk = (int32_t)(((uint32_t)packed >> (8 * (t + 1))) & 0xFFu);
+    if (!mk || !p->xq[t]) continue;
+    int count;
+    int64_t per;
+    x_inst(p->xq[t], &count, &per);
+    for (int m = 0; m < KG_MAX_MINORS; m++)
+      if ((mk >> m) & 1) d->x_used[t][m] = sub0(d->x_used[t][m], per);
+  }
 }
 
 /* flat helper for the Python binding: CalcDesiredRequestsAndCount → out = {count, core, mem, ratio} */
@@ -304,6 +444,7 @@ int32_t or_ds_allocate(const kg_node_device* d, const or_ds_pod* p, uint32_t req
                        const int64_t w[3]) {
   if (p->skip || !d->has_device) return 0;
   if (p->error) return -1;
+  if (p->nogpu) return 0; /* (ABI 17) only RDMA / FPGA: no GPU minor */
   const or_ds_inst in = or_ds_instance(d, p);
   if (!in.ok) return -1;
   int64_t fr[KG_MAX_MINORS][3];
@@ -345,7 +486,7 @@ int32_t or_ds_allocate(const kg_node_device* d, const or_ds_pod* p, uint32_t req
  * is dropped) */
 int64_t or_ds_score_view(const kg_node_device* d, const or_ds_pod* p, uint32_t rr_minors, const int64_t (*rr)[3],
                          const int64_t (*pre)[3], int strategy, const int64_t w[3]) {
-  if (p->skip || p->error || !d->has_device) return 0;
+  if (p->skip || p->error || !d->has_device || p->nogpu) return 0;
   const or_ds_inst in = or_ds_instance(d, p);
   if (!in.ok) return 0;
   int64_t fr[KG_MAX_MINORS][3];
@@ -414,6 +555,8 @@ int or_ds_filter_rsv(const kg_node_device* d, const or_ds_pod* p, const kg_node_
                      int required_from_rsv) {
   if (p->skip) return 1;
   if (p->error || !d->has_device) return 0;
+  if (!or_dsx_filter(d, p, NULL)) return 0; /* (ABI 17) the RDMA / FPGA types (no GPU-holding reservation with them) */
+  if (p->nogpu) return 1;
   if (st->n_matched > 0) {
     int32_t mask = 0;
     if (or_ds_try_rsv(d, p, r, st, st->matched, st->n_matched, 0, 0, NULL, &mask) >= 0) return 1;
@@ -458,7 +601,7 @@ int64_t or_ds_score_slot(const kg_node_device* d, const or_ds_pod* p, const kg_n
  * matched reservation's allocatable returned */
 int64_t or_ds_score_rsv(const kg_node_device* d, const or_ds_pod* p, const kg_node_reservations* r,
                         const or_ds_rsv* st, int nominated, int strategy, const int64_t w[3]) {
-  if (p->skip || p->error || !d->has_device) return 0;
+  if (p->skip || p->error || !d->has_device || p->nogpu) return 0;
   if (nominated >= 0) {
     int in_state = 0;
     for (int k = 0; k < st->n_matched; k++) in_state |= st->matched[k] == nominated;
@@ -476,6 +619,7 @@ int32_t or_ds_reserve_rsv(kg_node_device* d, const or_ds_pod* p, const kg_node_r
                           int nominated, int strategy, const int64_t w[3]) {
   if (p->skip || !d->has_device) return 0;
   if (p->error) return -1;
+  if (p->nogpu) return 0;
   int32_t mask = -1;
   if (nominated >= 0 && !(p->reserve)) {
     int in_state = 0;
@@ -504,6 +648,7 @@ int32_t or_ds_reserve_rsv(kg_node_device* d, const or_ds_pod* p, const kg_node_r
 /* the allocation of a pod assumed into slot s, on the reservation's minors (appendAllocatedByHints): sign ±1 */
 void or_ds_rsv_assign(kg_node_reservations* r, int s, const kg_node_device* d, const or_ds_pod* p, int32_t mask,
                       int sign) {
+  mask &= 0xFF; /* the GPU byte of a packed mask */
   if (s < 0 || !r->gpu_minors[s] || mask <= 0) return;
   const or_ds_inst in = or_ds_instance(d, p);
   const int64_t v[3] = {in.core, in.mem, in.ratio};

@@ -11,7 +11,10 @@
  *   device_resources.go:164-208  scoreDevices + sortDeviceResourcesByMinor (score desc, minor asc)
  *   scoring.go:34-97,183-308   Score, NormalizeScore (DefaultNormalizeScore), scoreDevice/scoreNode, scorers
  * Scope: the GPU device type without hints, joint allocation, VFs, NUMA affinity or preemption; (ABI 13) reservations
- * that hold GPUs (reservation.go RestoreReservation / tryAllocateFromReservation / scoreWithReservation).
+ * that hold GPUs (reservation.go RestoreReservation / tryAllocateFromReservation / scoreWithReservation); (ABI 17) the
+ * RDMA / FPGA types of devicehandler_default.go (one percentage resource each, no hints), allocated alongside the GPU
+ * type: Filter needs every requested type, Score sums the types (device_allocator.go:92-129, 333-454, 499-522).
+ * Minor masks of a pod are packed: GPU bits 0-7, RDMA 8-15, FPGA 16-23.
  * Map-order pins: fillGPUTotalMem takes the lowest healthy minor (the reference iterates a Go map; every GPU of
  * a node is the same model, device_cache.go comment at devicehandler_gpu.go:69-70).
  */
@@ -26,12 +29,14 @@ extern "C" {
 
 /* DeviceShare preFilterState for the GPU device type (preparePod, utils.go:204-230) */
 typedef struct or_ds_pod {
-  int skip;          /* no device request: Filter passes, Score 0                         */
+  int skip;          /* no device request of any type (state.skip): Filter passes, Score 0 */
   int reserve;       /* (ABI 13) a reservation's reserve pod: allocateWithNominatedReservation skips it */
   int error;         /* PreFilter UnschedulableAndUnresolvable: invalid request           */
-  int unsupported;   /* rdma / fpga requests: outside the restated scope                  */
+  int unsupported;   /* unused since ABI 17 (RDMA / FPGA are restated)                    */
   int has_mem;       /* the converted request names gpu-memory (else gpu-memory-ratio)   */
   int64_t core, mem, ratio;
+  int nogpu;         /* (ABI 17) no GPU-type request (only RDMA / FPGA)                   */
+  int64_t xq[KG_DEV_XTYPES]; /* (ABI 17) koordinator.sh/rdma, koordinator.sh/fpga (0 = none) */
 } or_ds_pod;
 
 /* per-instance request on one node (CalcDesiredRequestsAndCount) */
@@ -56,6 +61,12 @@ int64_t or_ds_score(const kg_node_device* d, const or_ds_pod* p, int strategy, c
 /* Reserve: allocates minors (defaultAllocateDevices order) and adds the per-instance request to their used
  * resources.  Returns the minor bitmask (0 = no allocation needed: skip / no Device object), -1 on failure. */
 int32_t or_ds_reserve(kg_node_device* d, const or_ds_pod* p, int strategy, const int64_t w[3]);
+/* (ABI 17) the RDMA / FPGA part alone: Filter (pre = the types' preemptible amounts per minor, NULL none), raw Score,
+ * Reserve (the packed RDMA / FPGA masks, -1 = Insufficient; deviceUsed updated only on success) and Unreserve */
+int or_dsx_filter(const kg_node_device* d, const or_ds_pod* p, const int64_t (*pre)[KG_MAX_MINORS]);
+int64_t or_dsx_score(const kg_node_device* d, const or_ds_pod* p, int strategy, const int64_t w[KG_DEV_XTYPES]);
+int32_t or_dsx_reserve(kg_node_device* d, const or_ds_pod* p, int strategy, const int64_t w[KG_DEV_XTYPES]);
+void or_dsx_release(kg_node_device* d, const or_ds_pod* p, int32_t packed);
 /* scoreDevice for one minor (scoring.go:183-203) */
 int64_t or_ds_score_minor(const kg_node_device* d, int minor, const or_ds_pod* p, const or_ds_inst* in,
                           int strategy, const int64_t w[3]);

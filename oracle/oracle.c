@@ -457,7 +457,10 @@ static void eval_score(sched_ctx* c, int64_t i) {
                                           c->st[i].requested[KG_RES_MEMORY], c->nodes[i].allocatable[KG_RES_CPU],
                                           c->nodes[i].allocatable[KG_RES_MEMORY]);
   if (c->dev) c->ds_raw[i] = cfg->ds_score ? or_ds_score(&c->dev[i], &c->ds_pod, (int)cfg->ds_scoring_strategy,
-                                                         cfg->ds_scoring_weights) : 0;
+                                                         cfg->ds_scoring_weights) +
+                                                 or_dsx_score(&c->dev[i], &c->ds_pod, (int)cfg->ds_scoring_strategy,
+                                                              cfg->ds_scoring_weights_x)
+                                           : 0;
   c->total[i] = t;
 }
 
@@ -682,6 +685,16 @@ int or_schedule_full(const kg_config* cfg, int64_t n_nodes, const kg_node* nodes
     int32_t minors = 0;
     if (best >= 0 && c.dev) {
       minors = or_ds_reserve(&c.dev[best], &c.ds_pod, (int)cfg->ds_scoring_strategy, cfg->ds_scoring_weights);
+      if (minors >= 0) { /* (ABI 17) the RDMA / FPGA types: all of them or none (the GPU part is given back) */
+        const int32_t xm = or_dsx_reserve(&c.dev[best], &c.ds_pod, (int)cfg->ds_scoring_strategy,
+                                          cfg->ds_scoring_weights_x);
+        if (xm < 0) {
+          or_ds_release(&c.dev[best], &c.ds_pod, minors);
+          minors = -1;
+        } else {
+          minors |= xm;
+        }
+      }
       if (minors < 0) {
         /* DeviceShare Reserve failed: RunReservePluginsUnreserve releases NodeNUMAResource's allocation too */
         minors = 0;

@@ -102,6 +102,14 @@ def lib():
         L.or_ds_score.restype = i64
         L.or_ds_reserve.argtypes = [vp, vp, i, vp]
         L.or_ds_reserve.restype = ctypes.c_int32
+        L.or_dsx_filter.argtypes = [vp, vp, vp]
+        L.or_dsx_filter.restype = i
+        L.or_dsx_score.argtypes = [vp, vp, i, vp]
+        L.or_dsx_score.restype = i64
+        L.or_dsx_reserve.argtypes = [vp, vp, i, vp]
+        L.or_dsx_reserve.restype = ctypes.c_int32
+        L.or_ds_release.argtypes = [vp, vp, ctypes.c_int32]
+        L.or_ds_release.restype = None
         L.or_ds_memory_bytes_to_ratio.argtypes = [i64, i64]
         L.or_ds_memory_bytes_to_ratio.restype = i64
         L.or_ds_memory_ratio_to_bytes.argtypes = [i64, i64]
@@ -168,7 +176,8 @@ def lib():
 
 
 DS_POD_DTYPE = np.dtype([("skip", np.int32), ("reserve", np.int32), ("error", np.int32), ("unsupported", np.int32),
-                         ("has_mem", np.int32), ("core", np.int64), ("mem", np.int64), ("ratio", np.int64)], align=True)
+                         ("has_mem", np.int32), ("core", np.int64), ("mem", np.int64), ("ratio", np.int64),
+                         ("nogpu", np.int32), ("xq", np.int64, (abi.DEV_XTYPES,))], align=True)
 # (ABI 13) or_ds_rsv: the DeviceShare restore of one node (oracle/deviceshare.h)
 DS_RSV_DTYPE = np.dtype([("n_matched", np.int32), ("matched", np.int32, (abi.MAX_RSV_SLOTS,)),
                          ("unm_used", np.int64, (abi.MAX_MINORS, 3)), ("mat_allocd", np.int64, (abi.MAX_MINORS, 3)),
@@ -193,15 +202,37 @@ def ds_filter(dev, pod) -> bool:
     return bool(lib().or_ds_filter(p(np.ascontiguousarray(dev)), p(ds_pod(pod))))
 
 
+def _wx(cfg):
+    return np.ascontiguousarray(cfg["ds_scoring_weights_x"].reshape(abi.DEV_XTYPES), dtype=np.int64)
+
+
 def ds_score(cfg, dev, pod) -> int:
+    """The plugin's raw Score: the GPU type's + (ABI 17) the RDMA / FPGA types' (AutopilotAllocator.score sums them)."""
     w = np.ascontiguousarray(cfg["ds_scoring_weights"].reshape(3), dtype=np.int64)
-    return int(lib().or_ds_score(p(np.ascontiguousarray(dev)), p(ds_pod(pod)), int(cfg["ds_scoring_strategy"]), p(w)))
+    d, dp = p(np.ascontiguousarray(dev)), p(ds_pod(pod))
+    return int(lib().or_ds_score(d, dp, int(cfg["ds_scoring_strategy"]), p(w))) + \
+        int(lib().or_dsx_score(d, dp, int(cfg["ds_scoring_strategy"]), p(_wx(cfg))))
 
 
 def ds_reserve(cfg, dev, pod) -> int:
-    """Reserve on one node (mutates `dev`, a 1-element NODE_DEVICE array): minor bitmask, 0 none, -1 failure."""
+    """Reserve on one node (mutates `dev`, a 1-element NODE_DEVICE array): the packed minor bitmask (GPU bits 0-7,
+    (ABI 17) RDMA 8-15, FPGA 16-23), 0 none, -1 failure (nothing allocated)."""
     w = np.ascontiguousarray(cfg["ds_scoring_weights"].reshape(3), dtype=np.int64)
-    return int(lib().or_ds_reserve(p(dev), p(ds_pod(pod)), int(cfg["ds_scoring_strategy"]), p(w)))
+    dp = ds_pod(pod)
+    m = int(lib().or_ds_reserve(p(dev), p(dp), int(cfg["ds_scoring_strategy"]), p(w)))
+    if m < 0:
+        return m
+    x = int(lib().or_dsx_reserve(p(dev), p(dp), int(cfg["ds_scoring_strategy"]), p(_wx(cfg))))
+    if x < 0:
+        lib().or_ds_release(p(dev), p(dp), m)
+        return -1
+    return m | x
+
+
+def dsx_filter(dev, pod, pre=None) -> bool:
+    """(ABI 17) the RDMA / FPGA part of the Filter; pre = int64[2, 8] preemptible amounts per type and minor."""
+    pr = None if pre is None else np.ascontiguousarray(pre, dtype=np.int64).reshape(abi.DEV_XTYPES, abi.MAX_MINORS)
+    return bool(lib().or_dsx_filter(p(np.ascontiguousarray(dev)), p(ds_pod(pod)), p(pr) if pr is not None else None))
 
 
 def _w(cfg):

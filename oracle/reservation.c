@@ -483,7 +483,8 @@ int or_schedule_resv_full(const kg_config* cfg, int64_t n_nodes, const kg_node* 
       order[i] = ns.has_state ? or_rsv_node_order(&ns, &rsv[i]) : INT64_MAX;
       dsraw[i] = (ds_on && cfg->ds_score && !dsp.skip)
                      ? or_ds_score_rsv(&dev[i], &dsp, rsv_on ? &rsv[i] : NULL, &dst, nom[i],
-                                       (int)cfg->ds_scoring_strategy, cfg->ds_scoring_weights)
+                                       (int)cfg->ds_scoring_strategy, cfg->ds_scoring_weights) +
+                           or_dsx_score(&dev[i], &dsp, (int)cfg->ds_scoring_strategy, cfg->ds_scoring_weights_x)
                      : 0;
     }
     if (err) { rc = err; break; }
@@ -606,6 +607,15 @@ int or_schedule_resv_full(const kg_config* cfg, int64_t n_nodes, const kg_node* 
       }
       minors = or_ds_reserve_rsv(&dev[win], &dsp, rsv_on ? &rsv[win] : NULL, &wdst, rsv_on ? nom[win] : -1,
                                  (int)cfg->ds_scoring_strategy, cfg->ds_scoring_weights);
+      if (minors >= 0) { /* (ABI 17) the RDMA / FPGA types: all of them or none */
+        const int32_t xm = or_dsx_reserve(&dev[win], &dsp, (int)cfg->ds_scoring_strategy, cfg->ds_scoring_weights_x);
+        if (xm < 0) {
+          or_ds_release(&dev[win], &dsp, minors);
+          minors = -1;
+        } else {
+          minors |= xm;
+        }
+      }
       if (minors < 0) {
         minors = 0;
         if (numa_on) numa[win] = numa_save;
@@ -675,6 +685,7 @@ typedef struct {
   const or_pre_ext* x;
   or_ds_pod dsp;                        /* the preemptor's DeviceShare preFilterState */
   int64_t dpre[KG_MAX_MINORS][3];       /* preemptibleDevices[node]: gpu-core, gpu-memory, gpu-memory-ratio */
+  int64_t xpre[KG_DEV_XTYPES][KG_MAX_MINORS]; /* (ABI 17) its RDMA / FPGA part */
   or_numa_node nn;                      /* the node's NodeAllocation (victims' cpusets kept) */
   or_numa_pod np;
 } pre_node;
@@ -706,7 +717,7 @@ static void pre_node_apply(pre_node* S, const kg_pod* v, int slot, int32_t minor
   if (S->x && S->x->dev && !S->dsp.skip && minors != 0 && !(v->flags & KG_POD_RESERVE) && slot < 0) {
     or_ds_pod vp;
     or_ds_pod_init(v, &vp);
-    const or_ds_inst in = or_ds_instance(S->x->dev, &vp);
+    const or_ds_inst in = (minors & 0xFF) && !vp.nogpu ? or_ds_instance(S->x->dev, &vp) : (or_ds_inst){0, 0, 0, 0, 0};
     if (in.ok)
       for (int m = 0; m < KG_MAX_MINORS; m++)
         if ((minors >> m) & 1) {
@@ -714,6 +725,14 @@ static void pre_node_apply(pre_node* S, const kg_pod* v, int slot, int32_t minor
           S->dpre[m][1] += sign * in.mem;
           S->dpre[m][2] += sign * in.ratio;
         }
+    /* (ABI 17) its RDMA / FPGA minors (bytes 1 and 2 of the packed mask): the per-instance request on each */
+    for (int t = 0; t < KG_DEV_XTYPES; t++) {
+      const int32_t xm = (int32_t)(((uint32_t)minors >> (8 * (t + 1))) & 0xFFu);
+      if (!xm || !vp.xq[t]) continue;
+      const int64_t q = vp.xq[t], per = (q > 100 && q % 100 == 0) ? 100 : q;
+      for (int m = 0; m < KG_MAX_MINORS; m++)
+        if ((xm >> m) & 1) S->xpre[t][m] += sign * per;
+    }
   }
   for (int q = 0; q < KG_RES_MAX; q++) S->rs.requested[q] -= sign * v->requests[q];
   S->rs.nonzero[0] -= sign * v->nonzero_requests[0];
@@ -823,7 +842,8 @@ static int64_t pre_node_filter(const kg_config* cfg, const kg_node* node, const 
     /* Filter without GPU-holding reservations: Allocate(nil, nil, nil, preemptibleDevices[node]); a node without a
      * Device object rejects a device pod (NodeResourcesFit on the device resources, as or_ds_filter) */
     const int ok = !S->dsp.error && x->dev->has_device &&
-                   or_ds_allocate(x->dev, &S->dsp, 0, 0, 0, NULL, (const int64_t(*)[3])S->dpre, 0, 0, NULL) >= 0;
+                   or_ds_allocate(x->dev, &S->dsp, 0, 0, 0, NULL, (const int64_t(*)[3])S->dpre, 0, 0, NULL) >= 0 &&
+                   or_dsx_filter(x->dev, &S->dsp, (const int64_t(*)[KG_MAX_MINORS])S->xpre);
     if (!ok) rej |= KG_REJECT_DEVICE;
   }
   return rej;

@@ -175,7 +175,8 @@ def test_unsupported_requests_fail_loudly():
     cfg = F.build_config(profile=PROFILE)
     with Engine(cfg, 4) as e:
         with pytest.raises(KoordGPUError) as ei:
-            e.stage(F.make_pod({"cpu": "1"}, devices={"koordinator.sh/rdma": 50}))
+            # (ABI 17) RDMA / FPGA are accelerated; a request beyond the accelerated range is still refused
+            e.stage(F.make_pod({"cpu": "1"}, devices={"koordinator.sh/rdma": 1 << 21}))
         assert ei.value.code == abi.E_UNSUPPORTED
     with Engine(F.build_config(), 4) as e:  # no DeviceShare in the profile: device requests are refused
         with pytest.raises(KoordGPUError):
