@@ -494,7 +494,7 @@ def main():
                         % (threads, threads, (m / dt) / (m1 / dt1) / threads)}
 
     tfile = args.traffic_file or next((f for f in (os.path.join(ROOT, "profiles", r, f"traffic_{wl}.json")
-                                                   for r in ("r05", "r04", "r03", "r02")) if os.path.exists(f)),
+                                                   for r in ("r06", "r05", "r04", "r03", "r02")) if os.path.exists(f)),
                                       os.path.join(ROOT, "profiles", "r02", f"traffic_{wl}.json"))
     # live timing folds every wide pass under one name: the kernel rocprof sees
     pmc_name = {"c4": "eval_round_numa", "c5": "xr_eval", "c5r": "xr_eval", "shipped": "xr_eval",
