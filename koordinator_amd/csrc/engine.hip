@@ -4885,12 +4885,29 @@ RsvExt rsv_ext(kg_engine* e) {
   return X;
 }
 
+// the rsv_eval variant for the pass's extension pointers (RSV_F_*: plugins absent from the profile compile out)
+int rsv_eval_flags(const RsvExt& X) {
+  return (X.dsx || X.rcpu ? RSV_F_XF : 0) | (X.ns ? RSV_F_NUMA : 0) | (X.ds ? RSV_F_DS : 0);
+}
+using RsvEvalFn = decltype(&rsv_eval<0>);
+RsvEvalFn rsv_eval_kernel(int f) {
+  switch (f) {  // the combinations a profile yields (XF needs NUMA or DeviceShare); the rest take the full kernel
+    case 0: return rsv_eval<0>;
+    case RSV_F_NUMA: return rsv_eval<RSV_F_NUMA>;
+    case RSV_F_DS: return rsv_eval<RSV_F_DS>;
+    case RSV_F_NUMA | RSV_F_DS: return rsv_eval<RSV_F_NUMA | RSV_F_DS>;
+    default: return rsv_eval<RSV_F_XF | RSV_F_NUMA | RSV_F_DS>;
+  }
+}
+
 int run_rsv(kg_engine* e, int64_t first, int64_t count, kg_stats* stats, double t0) {
   if (int rc = sync_static(e)) return rc;
   const int64_t n = e->n_nodes, end = first + count;
   if (count > 0 && n > 0) {
     const unsigned blocks = (unsigned)((n + kRsvThreads - 1) / kRsvThreads);
-    const RsvExt X = rsv_ext(e);
+    RsvExt X = rsv_ext(e);
+    if (!e->dsx_q) X.dsx = nullptr;  // (r6) no RDMA / FPGA request staged: the lean rsv_eval variant (part of the graph key)
+    const int rf = rsv_eval_flags(X);
     const unsigned long long init[5] = {0, 0, 0, (unsigned long long)first, (unsigned long long)end};
     HIP_TRY(hipMemcpyAsync(e->rsv_ws.p, init, sizeof(init), hipMemcpyHostToDevice, e->stream));
     if (e->grp_on) {  // the zone sums start from zero (then each pod's rsv_select clears the next pod's)
@@ -4905,9 +4922,9 @@ int run_rsv(kg_engine* e, int64_t first, int64_t count, kg_stats* stats, double 
         if (e->grp_on)  // Reserve of the previous pod + the group reductions this pod's Filters need
           group_pre<<<blocks, kRsvThreads, 0, e->stream>>>(e->T, e->rsv_d.p, e->pods.p, end_arg, n, g, X, e->rsv_val.p,
                                                            e->rsv_part.p, e->out_keys.p, e->out_rslot.p, e->rsv_ws.p);
-        rsv_eval<<<blocks, kRsvThreads, 0, e->stream>>>(e->T, e->rsv_d.p, e->rsv_nd.p, e->pods.p, e->rpods.p, end_arg, n,
-                                                         g, e->P, e->RP, X, e->rsv_val.p, e->rsv_part.p, e->out_keys.p,
-                                                         e->out_rslot.p, e->rsv_ws.p);
+        rsv_eval_kernel(rf)<<<blocks, kRsvThreads, 0, e->stream>>>(
+            e->T, e->rsv_d.p, e->rsv_nd.p, e->pods.p, e->rpods.p, end_arg, n, g, e->P, e->RP, X, e->rsv_val.p,
+            e->rsv_part.p, e->out_keys.p, e->out_rslot.p, e->rsv_ws.p);
         prof_end(e, KG_PROF_RSV_EVAL, t, e->stream);
         t = prof_begin(e, e->stream);
         rsv_select<<<blocks, kRsvThreads, 0, e->stream>>>(e->rsv_val.p, e->pods.p, end_arg, n, g, e->RP, X, e->rsv_part.p,
@@ -6622,20 +6639,22 @@ static int bench_rsv(kg_engine* e, int which, int iters, double* avg_ms, double*
   const unsigned blocks = (unsigned)((n + kRsvThreads - 1) / kRsvThreads);
   const unsigned long long zero[4] = {0, 0, 0, 0};
   HIP_TRY(hipMemcpyAsync(e->rsv_ws.p, zero, 32, hipMemcpyHostToDevice, e->stream));
-  const RsvExt X = rsv_ext(e);
+  RsvExt X = rsv_ext(e);
+  if (!e->dsx_q) X.dsx = nullptr;  // the variant run_rsv launches
+  const int rf = rsv_eval_flags(X);
   auto launch = [&]() {
     if (which == 0)
-      rsv_eval<<<blocks, kRsvThreads, 0, e->stream>>>(e->T, e->rsv_d.p, e->rsv_nd.p, e->pods.p, e->rpods.p,
-                                                       e->n_staged, n, 0, e->P, e->RP, X, e->rsv_val.p, e->rsv_part.p,
-                                                       e->out_keys.p, e->out_rslot.p, e->rsv_ws.p);
+      rsv_eval_kernel(rf)<<<blocks, kRsvThreads, 0, e->stream>>>(
+          e->T, e->rsv_d.p, e->rsv_nd.p, e->pods.p, e->rpods.p, e->n_staged, n, 0, e->P, e->RP, X, e->rsv_val.p,
+          e->rsv_part.p, e->out_keys.p, e->out_rslot.p, e->rsv_ws.p);
     else
       rsv_select<<<blocks, kRsvThreads, 0, e->stream>>>(e->rsv_val.p, e->pods.p, e->n_staged, n, 0, e->RP, X, e->rsv_part.p,
                                                          e->rsv_ws.p);
   };
   if (which == 1)  // rsv_select needs the packed values and partials of a real pass
-    rsv_eval<<<blocks, kRsvThreads, 0, e->stream>>>(e->T, e->rsv_d.p, e->rsv_nd.p, e->pods.p, e->rpods.p,
-                                                     e->n_staged, n, 0, e->P, e->RP, X, e->rsv_val.p, e->rsv_part.p,
-                                                     e->out_keys.p, e->out_rslot.p, e->rsv_ws.p);
+    rsv_eval_kernel(rf)<<<blocks, kRsvThreads, 0, e->stream>>>(
+        e->T, e->rsv_d.p, e->rsv_nd.p, e->pods.p, e->rpods.p, e->n_staged, n, 0, e->P, e->RP, X, e->rsv_val.p,
+        e->rsv_part.p, e->out_keys.p, e->out_rslot.p, e->rsv_ws.p);
   launch();  // warm
   hipEvent_t a, b;
   HIP_TRY(hipEventCreate(&a));

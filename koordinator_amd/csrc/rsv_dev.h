@@ -368,8 +368,9 @@ __device__ __forceinline__ int64_t dsr_slot_score(const DsNode& d, const DsInst&
 
 // kSlotsInRegs = false: the slot record is read where used (the wide exact pass, register-bound); kExt = false: no
 // reserve-pod / operating-mode / reservation-selector logic (the batched exact rounds; the host routes queues holding
-// such pods to the per-pod pass)
-template <bool kSlotsInRegs = true, bool kExt = true>
+// such pods to the per-pod pass); kXF = false: no RDMA / FPGA evaluation and no reserved-cpus NodeNUMAResource Score
+// (the host picks it when the queue holds no RDMA / FPGA request and no reservation holds cpus: fewer registers)
+template <bool kSlotsInRegs = true, bool kExt = true, bool kXF = true, bool kNuma = true, bool kDs = true>
 __device__ __forceinline__ RsvOut rsv_eval_node(const DevTable& T, const RsvNode* __restrict__ RN,
                                                 const int32_t* __restrict__ rsv_n, int64_t i, const DevPod& p,
                                                 const RsvPod& rp, const EvalParams& P, const RsvParams& RP,
@@ -451,7 +452,7 @@ __device__ __forceinline__ RsvOut rsv_eval_node(const DevTable& T, const RsvNode
   uint32_t dsok = 0;
   DsrCtx dc{nullptr, 0u, 0u};
   DsInst din{0, 0, 0, 0, 0};
-  if (X.ds && dp && !dp->skip) {
+  if (kDs && X.ds && dp && !dp->skip) {
     const DsNode& d = X.ds[i];
     uint32_t gslots = 0;
     if (kExt && X.rgpu && has_state)  // the batched exact rounds never see GPU reservations (host routing)
@@ -483,7 +484,7 @@ __device__ __forceinline__ RsvOut rsv_eval_node(const DevTable& T, const RsvNode
     sat &= dsok;
     // (ABI 17) the RDMA / FPGA types of the request (the host routes such queues here and refuses them next to
     // GPU-holding reservations): Allocate needs every requested type, Score sums them
-    if constexpr (kExt) {
+    if constexpr (kExt && kXF) {
       if (X.dsx && (dp->xq[0] | dp->xq[1])) {
         int64_t xraw = 0;
         if (!ds_eval_x(X.dsx[i], d.has_device != 0, *dp, X.DP, xraw)) return o;
@@ -493,7 +494,7 @@ __device__ __forceinline__ RsvOut rsv_eval_node(const DevTable& T, const RsvNode
   }
   int64_t nsc = 0;        // NodeNUMAResource's Score without preferred cpus
   NumaHint naff{0, 1, 0, 0};
-  if (X.ns && np) {  // NodeNUMAResource Filter + Score on the restored NodeInfo; Reserve reuses the stored affinity
+  if (kNuma && X.ns && np) {  // NodeNUMAResource Filter + Score on the restored NodeInfo; Reserve reuses the stored affinity
     const NumaView nv = make_view(X.ns + i, X.nm + i, X.NP);
     if (!numa_eval(nv, *np, X.NP, r.req_cpu, r.req_mem, r.alloc_cpu, r.alloc_mem, nsc, naff)) return o;
     if (X.NP.score) t += nsc * X.NP.weight;
@@ -561,7 +562,7 @@ __device__ __forceinline__ RsvOut rsv_eval_node(const DevTable& T, const RsvNode
     o.raw = raw;
     // (ABI 15) NodeNUMAResource Score runs after the PreScore nomination: a cpuset-capable pod nominated into a
     // reservation holding cpus gets its reserved cpus as preferredCPUs (getReservationReservedCPUs, plugin.go:513-535)
-    if (kExt && X.rcpu && X.ns && np && X.NP.score && np->allow && pick >= 0 && (rn.meta[pick] & RS_CPUS)) {
+    if (kExt && kXF && kNuma && X.rcpu && X.ns && np && X.NP.score && np->allow && pick >= 0 && (rn.meta[pick] & RS_CPUS)) {
       const CpuSet P = rsv_reserved_cpus(X.rcpu[(size_t)i * kRsvSlots + pick]);
       if (cs_count(P) > 0) {
         const NumaView nv = make_view(X.ns + i, X.nm + i, X.NP);
@@ -571,7 +572,7 @@ __device__ __forceinline__ RsvOut rsv_eval_node(const DevTable& T, const RsvNode
       }
     }
   }
-  if (dsr && X.DP.score) {  // Score (scoring.go:34-89): the nominated reservation's, else the node view's
+  if (kDs && dsr && X.DP.score) {  // Score (scoring.go:34-89): the nominated reservation's, else the node view's
     const DsNode& d = X.ds[i];
     if (o.nom >= 0 && ((dc.mt >> o.nom) & 1u))
       dsraw = dsr_slot_score(d, din, dc, o.nom, ((rn.meta[o.nom] >> 4) & 3) == KG_RSV_POLICY_RESTRICTED, X.DP);
@@ -762,7 +763,7 @@ __device__ __forceinline__ void rsv_quota_charge(const RsvExt& X, const DevPod& 
 // Reserve of pod j on its winner row w: DeviceShare first (a failure un-assumes the pod: nothing is placed), then
 // NodeInfo + LoadAware assign cache and reservationCache.assumePod on the slot nominated there
 // (reservation_info.go:317-326).  Called by the one thread that owns row w.  Returns false when not placed.
-template <bool NUMA = true, bool DS = true>  // compile-time: the profile's plugins (batched exact rounds)
+template <bool NUMA = true, bool DS = true, bool kXF = true>  // compile-time: the profile's plugins (see rsv_eval_node)
 __device__ __forceinline__ bool rsv_reserve(const DevTable& T, RsvNode* __restrict__ RN, int64_t w, uint64_t v,
                                             const DevPod& p, const RsvExt& X, int64_t j, int32_t& slot_out,
                                             int diag_j = -1) {
@@ -784,7 +785,7 @@ __device__ __forceinline__ bool rsv_reserve(const DevTable& T, RsvNode* __restri
     const NumaHint aff{a & 0xFFu, (int)((a >> 8) & 1u), 0, 0};
     // (ABI 15) the nominated reservation's reserved cpus are Reserve's preferredCPUs too (getResourceOptions)
     CpuSet P = cs_zero();
-    if (X.rcpu && nom_slot >= 0 && X.npods[j].allow && (RN[w].meta[nom_slot] & RS_CPUS))
+    if (kXF && X.rcpu && nom_slot >= 0 && X.npods[j].allow && (RN[w].meta[nom_slot] & RS_CPUS))
       P = rsv_reserved_cpus(X.rcpu[(size_t)w * kRsvSlots + nom_slot]);
     const bool ok = cs_count(P) > 0 ? numa_reserve_pref(nsw, nmw, nv, X.npods[j], aff, P, cpus, rec)
                                     : numa_reserve(nsw, nmw, nv, X.npods[j], aff, cpus, rec);
@@ -830,7 +831,7 @@ __device__ __forceinline__ bool rsv_reserve(const DevTable& T, RsvNode* __restri
     // (ABI 17) the RDMA / FPGA types, on a copy: every requested type is allocated or none is
     int32_t xminors = 0;
     DsXNode xn;
-    const bool xreq = X.dsx && (X.dpods[j].xq[0] | X.dpods[j].xq[1]);
+    const bool xreq = kXF && X.dsx && (X.dpods[j].xq[0] | X.dpods[j].xq[1]);
     if (xreq && minors >= 0) {
       xn = X.dsx[w];
       xminors = ds_reserve_x(xn, dn.has_device != 0, X.dpods[j], X.DP);
@@ -883,7 +884,7 @@ __device__ __forceinline__ bool rsv_reserve(const DevTable& T, RsvNode* __restri
     if (DS && X.rgpu && gpu_minors > 0 && (RN[w].meta[slot] & RS_GPU))
       rsv_gpu_assign(X.rgpu[(size_t)w * kRsvSlots + slot], ds_instance(X.ds[w], X.dpods[j]), gpu_minors, +1);
     // (ABI 15) an assigned pod's cpus leave the reservation's reserved cpus at the next RestoreReservation
-    if (NUMA && X.rcpu && X.ns && (RN[w].meta[slot] & RS_CPUS)) {
+    if (kXF && NUMA && X.rcpu && X.ns && (RN[w].meta[slot] & RS_CPUS)) {
       RsvCpu& rc = X.rcpu[(size_t)w * kRsvSlots + slot];
 #pragma unroll
       for (int q = 0; q < kCpuWords; ++q) rc.u[q] |= cpus.w[q];
@@ -904,6 +905,9 @@ __device__ __forceinline__ bool rsv_reserve(const DevTable& T, RsvNode* __restri
 // pods < j - 1 (pod j - 2 was charged by rsv_select(j - 1)); pod j - 1's charge is added here explicitly when it was
 // placed (g > 0; a group's last pod is charged by rsv_apply itself), and written into the rows by rsv_select(j), when
 // no pass reads them (ws[0] = j tags it).
+// F = RSV_F_* bits, compile-time: kernels without the plugins the profile lacks need fewer registers
+constexpr int RSV_F_XF = 1, RSV_F_NUMA = 2, RSV_F_DS = 4;  // XF: X.dsx or X.rcpu set (see rsv_eval_node)
+template <int F>
 __global__ __launch_bounds__(kRsvThreads) void rsv_eval(DevTable T, RsvNode* __restrict__ RN,
                                                         const int32_t* __restrict__ rsv_n,
                                                         const DevPod* __restrict__ pods,
@@ -926,7 +930,9 @@ __global__ __launch_bounds__(kRsvThreads) void rsv_eval(DevTable T, RsvNode* __r
     if (!X.gpods && (i == w || (w < 0 && i == 0))) {
       int32_t slot = -1;
       bool placed = false;
-      if (w >= 0) placed = rsv_reserve(T, RN, w, val[w], pods[j - 1], X, j - 1, slot);
+      if (w >= 0) placed = rsv_reserve<(F & RSV_F_NUMA) != 0, (F & RSV_F_DS) != 0, (F & RSV_F_XF) != 0>(T, RN, w, val[w],
+                                                                                              pods[j - 1], X, j - 1,
+                                                                                              slot);
       out_keys[j - 1] = placed ? k : 0;
       out_slot[j - 1] = slot;
       if (placed && X.nq > 0 && pods[j - 1].quota >= 0) {
@@ -995,7 +1001,8 @@ __global__ __launch_bounds__(kRsvThreads) void rsv_eval(DevTable T, RsvNode* __r
     const NumaPod* np = X.ns ? &X.npods[j] : nullptr;
     const int64_t* aux = (X.paux && (p.flags & P_AUX)) ? X.paux + (size_t)j * kAux : nullptr;
     const DefPod* df = X.defp ? &X.defp[j] : nullptr;
-    RsvOut o = rsv_eval_node(T, RN, rsv_n, i, p, rp, P, RP, X, dp, np, nullptr, aux, df);
+    RsvOut o = rsv_eval_node<true, true, (F & RSV_F_XF) != 0, (F & RSV_F_NUMA) != 0, (F & RSV_F_DS) != 0>(
+        T, RN, rsv_n, i, p, rp, P, RP, X, dp, np, nullptr, aux, df);
     if (o.feas && X.gpods) {
       zone = X.pred[i].zone;
       o.feas = groups_filter(X.G, i, gp, X.GP, node_affinity_match(X.pred, df, i), zone, s_min, Z, pres, total);
