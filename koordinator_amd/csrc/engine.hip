@@ -2291,6 +2291,395 @@ __global__ __launch_bounds__(kWave) void resolve_round_numa(DevTable T, NumaTabl
   publish_round(ctl, seq);
 }
 
+// (r6) Two-wave NUMA resolver: resolve_round_numa's chain split over the two waves of one workgroup.  Per pod j,
+// phase A runs on both waves at once:
+//   wave 0 (scorer):   pod j's exact key on every modified row (their committed states, i.e. after Reserve of pod
+//                      j - 2) and the best unmodified candidate e's Filter (its affinity), e's row staged in the spare
+//                      slot nM; keys and affinities go to LDS;
+//   wave 1 (reserver): Reserve of pod j - 1 on its winner's slot (wave-uniform, on a copy), then pod j's exact key on
+//                      that slot's new state — the one row whose state the scorer has not seen;
+// after a barrier, phase B on the reserver: commit Reserve(j - 1)'s row, then pod j's decision (ElasticQuota admission,
+// the early round end, e against the modified rows, the slot adopting e); a second barrier ends the pod.  The serial
+// chain per pod becomes max(scorer, Reserve + one row) instead of their sum.  Same results as
+// resolve_round_numa: the scorer's key of Reserve(j - 1)'s slot is replaced by the reserver's, every other slot's state
+// is the one a sequential resolver would see.
+constexpr int kRowWords = (int)(sizeof(Row) / 8);
+static_assert(sizeof(Row) % 8 == 0, "Row in 8-byte words");
+constexpr int kNuma2Threads = 2 * kWave;
+size_t numa2_extra_lds_bytes() {  // beyond resolve_numa_lds_bytes: slot Rows, reserver's NumaMut, keys, affinities, words
+  return ((size_t)kWave * (kRowWords + 1 + 2) + kNumaMutWords + 4) * 8 + (size_t)kWave * 4 * 2 + 16 * 4;
+}
+// the rows of each pod's first kNumaPre candidates, read into LDS once per round (after the chain wait, so an unmodified
+// row's copy is current): the best unmodified candidate's staging then reads LDS instead of HBM on the serial path
+constexpr int kNumaPre = 2;
+constexpr int kPreWords = kRowWords + kNumaStaticWords + kNumaMutWords;
+size_t numa2_pre_lds_bytes(int nb) { return (size_t)nb * kNumaPre * kPreWords * 8; }
+
+__global__ __launch_bounds__(kNuma2Threads) void resolve_round_numa2(DevTable T, NumaTable NT,
+                                                                      const DevPod* __restrict__ pods,
+                                                                      const NumaPod* __restrict__ npods,
+                                                                      int64_t* __restrict__ ctl, int64_t first, int nb,
+                                                                      const uint64_t* __restrict__ cand, EvalParams P,
+                                                                      NumaParams NP, uint64_t* __restrict__ out_keys,
+                                                                      uint64_t* __restrict__ out_cpus,
+                                                                      int64_t* __restrict__ out_nrec, int bitmap_words,
+                                                                      int32_t* __restrict__ poison, int64_t seq,
+                                                                      QuotaRow* __restrict__ quotas, int nq,
+                                                                      int32_t* __restrict__ modlists, int slot,
+                                                                      int depth, int n_prev, int wait, int npre) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
+  const int tid = threadIdx.x, wave = tid / kWave, lane = tid % kWave;
+  uint64_t* s_cand = smem;                                     // [nb][kCandStride]
+  uint64_t* s_podw = s_cand + (size_t)nb * kCandStride;        // [nb] DevPod
+  uint64_t* s_npw = s_podw + (size_t)nb * kPodWords;           // [nb] NumaPod
+  uint64_t* s_nsw = s_npw + (size_t)nb * kNumaPodWords;        // [kWave] NumaStatic of the slots
+  uint64_t* s_nmw = s_nsw + (size_t)kWave * kNumaStaticWords;  // [kWave] NumaMut of the slots (committed)
+  uint64_t* s_roww = s_nmw + (size_t)kWave * kNumaMutWords;    // [kWave] Row of the slots (committed)
+  uint64_t* s_rnmw = s_roww + (size_t)kWave * kRowWords;       // the reserver's NumaMut after its Reserve
+  uint64_t* s_key = s_rnmw + kNumaMutWords;                    // [kWave] the scorer's keys of the current pod
+  uint64_t* s_affw = s_key + kWave;                            // [kWave][2] the scorer's affinities (NumaHint)
+  uint64_t* s_misc = s_affw + (size_t)kWave * 2;               // [4]: 0 = the current pod's e key (0 = none)
+  uint32_t* s_ver = reinterpret_cast<uint32_t*>(s_misc + 4);   // [kWave] slot state versions
+  uint32_t* s_node = s_ver + kWave;                            // [kWave] node of each slot
+  int32_t* s_c = reinterpret_cast<int32_t*>(s_node + kWave);   // [16] 0 nM, 1 stop, 4 timed out, 5 abort
+  uint32_t* bitmap = reinterpret_cast<uint32_t*>(s_c + 16);
+  uint32_t* s_prevn = bitmap + bitmap_words;                   // [kWave] earlier rounds' winners (prologue)
+  uint64_t* s_pre = reinterpret_cast<uint64_t*>(s_prevn + kWave);  // [nb][npre] Row, NumaStatic, NumaMut
+  for (int w = tid; w < nb * kCandStride; w += kNuma2Threads) s_cand[w] = cand[w];
+  {
+    const uint64_t* pw = reinterpret_cast<const uint64_t*>(pods + first);
+    for (int w = tid; w < nb * kPodWords; w += kNuma2Threads) s_podw[w] = pw[w];
+    const uint64_t* nw = reinterpret_cast<const uint64_t*>(npods + first);
+    for (int w = tid; w < nb * kNumaPodWords; w += kNuma2Threads) s_npw[w] = nw[w];
+  }
+  for (int w = tid; w < bitmap_words; w += kNuma2Threads) bitmap[w] = 0;
+  if (tid < kWave) s_ver[tid] = 0;
+  if (tid < 16) s_c[tid] = 0;
+  __syncthreads();
+  if (tid == 0) {  // (r5) pipelined rounds: chain on the previous round's resolver (bounded spin, as resolve_round)
+    int timed_out = 0;
+    if (wait) {
+      int64_t it = 0;
+      while (__hip_atomic_load(&ctl[4], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < seq - 1) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++it > kSpinLimit) {
+          timed_out = 1;
+          break;
+        }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    s_c[4] = timed_out;
+    s_c[5] = (timed_out || *poison || ctl[0] != first) ? 1 : 0;
+  }
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  if (s_c[5]) {
+    if (tid == 0 && s_c[4]) ctl[5] = 1;
+    publish_round(ctl, seq);
+    return;
+  }
+  const uint64_t t_active = __builtin_amdgcn_s_memrealtime();
+  for (int x = tid; x < nb * npre; x += kNuma2Threads) {  // the candidates' rows (one entry per thread)
+    const uint64_t key = s_cand[(size_t)(x / npre) * kCandStride + x % npre];
+    if (key == 0) continue;
+    const uint32_t m = key_node(key);
+    uint64_t* e = s_pre + (size_t)x * kPreWords;
+    *reinterpret_cast<Row*>(e) = load_row(T, m);
+    *reinterpret_cast<NumaStatic*>(e + kRowWords) = NT.s[m];
+    *reinterpret_cast<NumaMut*>(e + kRowWords + kNumaStaticWords) = NT.m[m];
+  }
+  const DevPod* s_pods = reinterpret_cast<const DevPod*>(s_podw);
+  const NumaPod* s_np = reinterpret_cast<const NumaPod*>(s_npw);
+  NumaStatic* s_ns = reinterpret_cast<NumaStatic*>(s_nsw);
+  NumaMut* s_nm = reinterpret_cast<NumaMut*>(s_nmw);
+  Row* s_row = reinterpret_cast<Row*>(s_roww);
+  NumaMut* s_rnm = reinterpret_cast<NumaMut*>(s_rnmw);
+  // the rows the n_prev earlier rounds modified, de-duplicated into slots [0, nM) by wave 0 (as resolve_round_numa)
+  {
+    int n = 0;
+    for (int d = 1; d <= n_prev; ++d) {
+      const int32_t* ml = modlists + (size_t)(((slot - d) % depth + depth) % depth) * kModListStride;
+      const int c = ml[0];
+      if (wave == 0)
+        for (int t = lane; t < c; t += kWave) s_prevn[n + t] = (uint32_t)ml[1 + t];
+      n += c;
+    }
+    __syncthreads();
+    const uint32_t node = (wave == 0 && lane < n) ? s_prevn[lane] : 0xFFFFFFFFu;
+    bool dup = false;
+    if (wave == 0)
+      for (int k = 0; k < n; ++k) dup |= lane > k && node == (uint32_t)__builtin_amdgcn_readlane((int)node, k);
+    const bool keep = wave == 0 && lane < n && !dup;
+    const uint64_t km = __ballot(keep);
+    const uint64_t lane_lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    __syncthreads();
+    if (keep) s_prevn[__popcll(km & lane_lt)] = node;
+    __syncthreads();
+    if (wave == 0) {
+      const int nM0 = __popcll(km);
+      if (lane < nM0) {
+        const uint32_t m = s_prevn[lane];
+        s_node[lane] = m;
+        s_row[lane] = load_row(T, m);
+        s_ns[lane] = NT.s[m];
+        s_nm[lane] = NT.m[m];
+        atomicOr(&bitmap[m >> 5], 1u << (m & 31));
+      }
+      if (lane == 0) s_c[0] = nM0;
+    }
+    __syncthreads();
+  }
+  // scorer state (wave 0, lane = slot): the slot's node, Row and view, and the version they were built from
+  uint32_t midx = 0xFFFFFFFFu, myver = 0;
+  Row mrow;
+  mrow.flags = 0;
+  NumaView mv;
+  if (wave == 0 && lane < s_c[0]) {
+    midx = s_node[lane];
+    mrow = s_row[lane];
+    mv = make_view(&s_ns[lane], &s_nm[lane], NP);
+  }
+  // reserver state (wave 1, uniform but my_out / quota lanes): the pending Reserve and the commit of the last one
+  bool r_pend = false;
+  int r_j = 0, r_slot = -1;
+  uint64_t r_best = 0;
+  NumaHint r_aff{0, 1, 0, 0};
+  bool r_placed = false;  // this pod's phase A placed pod r_j (commit in phase B)
+  int c_slot = -1;        // the slot that Reserve changed
+  Row r_row;
+  r_row.flags = 0;
+  uint64_t r_key = 0;           // pod j's key on c_slot's new state
+  NumaHint r_aff2{0, 1, 0, 0};  // its affinity
+  uint64_t touch = 0;           // slots with committed Reserves (written back at the end)
+  uint64_t my_out = 0;
+  int consumed = 0;
+  DevQuota ql = quota_load(quotas, nq, wave == 1 ? lane : kWave);
+  bool stop = false;
+  for (int j = 0; j <= nb; ++j) {
+    const bool live = j < nb && !stop;
+#ifdef KG_STAMPS  // per pod: scorer phase A start / end, reserver phase A start / after Reserve / end, phase B end
+#define KG_N2_STAMP(k) \
+    if (lane == 0 && j < 64) g_pod_diag[j][k] = __builtin_amdgcn_s_memtime()
+#define KG_N2_SUB(k) \
+    if (lane == 0 && j < 64) g_lane_diag[j][k] = __builtin_amdgcn_s_memtime()
+#else
+#define KG_N2_STAMP(k)
+#define KG_N2_SUB(k)
+#endif
+    if (wave == 0) {
+      KG_N2_STAMP(0);
+    } else {
+      KG_N2_STAMP(2);
+    }
+    // ---- phase A ----
+    if (wave == 0) {
+      if (live) {
+        const int nM = s_c[0];
+        if (lane < nM && s_ver[lane] != myver) {  // the reserver committed a Reserve on this slot
+          myver = s_ver[lane];
+          mrow = s_row[lane];
+          mv = make_view(&s_ns[lane], &s_nm[lane], NP);
+        }
+        KG_N2_SUB(0);
+        const uint64_t key = s_cand[(size_t)j * kCandStride + lane];
+        const uint32_t node = key_node(key);
+        const bool unmod = (key != 0) && !((bitmap[node >> 5] >> (node & 31)) & 1u);
+        const uint64_t um = __ballot(unmod);
+        const int pos = um ? (int)__builtin_ctzll(um) : kC;
+        const uint64_t ekey = um ? readlane_u64(key, pos) : 0;
+        const bool stage = um && nM < kWave;
+        if (stage && pos < npre) {  // e's row from the round's LDS copy: the wave copies it into the spare slot nM
+          const uint64_t* e = s_pre + ((size_t)j * npre + pos) * kPreWords;
+          for (int w = lane; w < kPreWords; w += kWave) {
+            const uint64_t v = e[w];
+            if (w < kRowWords) s_roww[(size_t)nM * kRowWords + w] = v;
+            else if (w < kRowWords + kNumaStaticWords) s_nsw[(size_t)nM * kNumaStaticWords + (w - kRowWords)] = v;
+            else s_nmw[(size_t)nM * kNumaMutWords + (w - kRowWords - kNumaStaticWords)] = v;
+          }
+          if (lane == nM) {  // its Filter gives the affinity Reserve needs (read from the copy: no cross-lane wait)
+            midx = key_node(ekey);
+            mrow = *reinterpret_cast<const Row*>(e);
+            s_node[nM] = midx;
+            myver = s_ver[nM];
+            mv = make_view(reinterpret_cast<const NumaStatic*>(e + kRowWords),
+                           reinterpret_cast<const NumaMut*>(e + kRowWords + kNumaStaticWords), NP);
+          }
+        } else if (stage && lane == nM) {  // e's row into the spare slot: its Filter gives the affinity Reserve needs
+          const uint32_t en = key_node(ekey);
+          midx = en;
+          mrow = load_row(T, en);
+          s_ns[nM] = NT.s[en];
+          s_nm[nM] = NT.m[en];
+          s_row[nM] = mrow;
+          s_node[nM] = en;
+          myver = s_ver[nM];
+          mv = make_view(&s_ns[nM], &s_nm[nM], NP);
+        }
+        const DevPod p = s_pods[j];
+        const NumaPod np = s_np[j];
+        uint64_t mk = 0;
+        NumaHint maff{0, 1, 0, 0};
+        KG_N2_SUB(1);
+        if (lane < nM || (stage && lane == nM)) {
+          int64_t t = 0;
+          if (eval_node_numa(mrow, mv, p, np, P, NP, t, maff) && lane < nM) mk = make_key(t, midx);
+        }
+        KG_N2_SUB(2);
+        if (lane <= nM && lane < kWave) {
+          s_key[lane] = mk;
+          s_affw[2 * lane] = (uint64_t)maff.mask | ((uint64_t)(uint32_t)maff.nil << 32);
+          s_affw[2 * lane + 1] = (uint64_t)(uint32_t)maff.preferred | ((uint64_t)(uint32_t)maff.score << 32);
+        }
+        if (lane == 0) s_misc[0] = ekey;
+      }
+      KG_N2_STAMP(1);
+    } else {
+      r_placed = false;
+      if (r_pend) {  // Reserve of pod r_j on slot r_slot (wave-uniform on copies; lane 0 writes the records)
+        r_pend = false;
+        const DevPod p = s_pods[r_j];
+        const NumaPod np = s_np[r_j];
+        const NumaStatic ns = s_ns[r_slot];
+        NumaMut nm = s_nm[r_slot];
+        const NumaView ov = make_view(&s_ns[r_slot], &s_nm[r_slot], NP);
+        CpuSet cpus;
+        NumaAlloc rec;
+        r_placed = numa_reserve(ns, nm, ov, np, r_aff, cpus, rec);
+        if (r_placed) {
+          c_slot = r_slot;
+          r_row = s_row[r_slot];
+          r_row.req_cpu += p.req_cpu;  // assume: NodeInfo.AddPod + LoadAware assign cache
+          r_row.req_mem += p.req_mem;
+          r_row.nz_cpu += p.nz_cpu;
+          r_row.nz_mem += p.nz_mem;
+          r_row.la_used_cpu += p.est_cpu;
+          r_row.la_used_mem += p.est_mem;
+          if (p.flags & P_PROD) {
+            r_row.la_pused_cpu += p.est_cpu;
+            r_row.la_pused_mem += p.est_mem;
+          }
+          r_row.num_pods += 1;
+          *s_rnm = nm;  // every lane writes the same (uniform) state and reads back its own write
+          if (lane == 0) {
+#pragma unroll
+            for (int q = 0; q < kCpuWords; ++q) out_cpus[(size_t)(first + r_j) * kCpuWords + q] = cpus.w[q];
+            int64_t* r = out_nrec + (size_t)(first + r_j) * kNumaRecWords;
+            r[0] = rec.res;
+#pragma unroll
+            for (int i = 0; i < kNumaMax; ++i) {
+              r[1 + i] = ((rec.res >> i) & 1u) ? rec.cpu[i] : 0;
+              r[1 + kNumaMax + i] = ((rec.res >> i) & 1u) ? rec.mem[i] : 0;
+            }
+          }
+          if (nq > 0) quota_charge(ql, p, lane);
+          KG_N2_STAMP(3);
+          if (live) {  // pod j's key on the new state (the scorer saw the state before this Reserve)
+            const NumaView nv = make_view(&s_ns[r_slot], s_rnm, NP);
+            int64_t t = 0;
+            r_aff2 = NumaHint{0, 1, 0, 0};
+            r_key = eval_node_numa(r_row, nv, s_pods[j], s_np[j], P, NP, t, r_aff2)
+                        ? make_key(t, s_node[r_slot]) : 0;
+          }
+        }
+        my_out = lane == r_j ? (r_placed ? r_best : 0) : my_out;
+      }
+      KG_N2_STAMP(4);
+    }
+    __syncthreads();
+    // ---- phase B (reserver) ----
+    if (wave == 1) {
+      if (r_placed) {  // commit Reserve(r_j): the scorer rebuilds this slot from LDS at its next pod
+        if (lane == 0) {
+          s_nm[c_slot] = *s_rnm;
+          s_row[c_slot] = r_row;
+          s_ver[c_slot] += 1;
+        }
+        touch |= 1ull << c_slot;
+      }
+      if (live) {
+        const DevPod p = s_pods[j];
+        const int nM = s_c[0];
+        if (nq > 0 && !quota_admit(ql, p)) {  // ElasticQuota PreFilter rejects
+          my_out = lane == j ? 0 : my_out;
+          ++consumed;
+        } else {
+          const uint64_t ekey = s_misc[0];
+          const uint64_t ub = s_cand[(size_t)j * kCandStride + kC];
+          uint64_t mk = lane < nM ? s_key[lane] : 0;
+          if (r_placed && lane == c_slot) mk = r_key;  // the slot Reserve(j - 1) changed
+          const uint64_t mbest = wave_max_key(mk);
+          const uint64_t best = mbest > ekey ? mbest : ekey;
+          if (best < ub) {
+            stop = true;
+            if (lane == 0) s_c[1] = 1;
+          } else {
+            ++consumed;
+            if (best == 0) {
+              my_out = lane == j ? 0 : my_out;
+            } else {
+              const uint32_t w = key_node(best);
+              const uint64_t hit = __ballot(lane < nM && s_node[lane] == w);
+              const int owner = hit ? (int)__builtin_ctzll(hit) : nM;
+              if (!hit) {  // w = e, staged in slot nM: the slot becomes a modified row
+                if (lane == 0) {
+                  bitmap[w >> 5] |= 1u << (w & 31);
+                  s_c[0] = nM + 1;
+                }
+              }
+              if (r_placed && owner == c_slot) {
+                r_aff = r_aff2;
+              } else {
+                const uint64_t a0 = s_affw[2 * owner], a1 = s_affw[2 * owner + 1];
+                r_aff = NumaHint{(uint32_t)a0, (int)(uint32_t)(a0 >> 32), (int)(uint32_t)a1, (int)(uint32_t)(a1 >> 32)};
+              }
+              r_pend = true;
+              r_j = j;
+              r_slot = owner;
+              r_best = best;
+            }
+          }
+        }
+      }
+    }
+    if (wave == 1) {
+      KG_N2_STAMP(5);
+    }
+    __syncthreads();
+    stop = s_c[1] != 0;
+    if (!live) break;
+#undef KG_N2_STAMP
+#undef KG_N2_SUB
+  }
+  // write-back (reserver): the committed slots' rows, placements, quota, this round's modified-row list
+  if (wave == 1) {
+    if (lane < s_c[0] && ((touch >> lane) & 1ull)) {
+      const uint32_t m = s_node[lane];
+      store_mutable(T, m, s_row[lane]);
+      NT.m[m] = s_nm[lane];
+    }
+    if (lane < consumed) out_keys[first + lane] = my_out;
+    quota_store(quotas, nq, lane, ql);
+    const bool mine = lane < consumed && my_out != 0;
+    const uint64_t bm = __ballot(mine);
+    const uint64_t lane_lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    int32_t* my_mod = modlists + (size_t)slot * kModListStride;
+    if (mine) my_mod[1 + __popcll(bm & lane_lt)] = (int32_t)key_node(my_out);
+    if (lane == 0) {
+      my_mod[0] = __popcll(bm);
+      ctl[0] = first + consumed;
+      ctl[1] += 1;
+      ctl[2] += consumed;
+      if (consumed < nb) *poison = 1;
+      ctl[8] += (int64_t)(__builtin_amdgcn_s_memrealtime() - t_active);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  __syncthreads();
+  publish_round(ctl, seq);
+}
+
 // kg_pods_evaluate_numa: NodeNUMAResource Filter + Score of one pod on every node (the plugin alone)
 __global__ void evaluate_pod_numa(DevTable T, NumaTable NT, const DevPod* __restrict__ pod,
                                   const NumaPod* __restrict__ npod, int64_t n, NumaParams NP,
@@ -4584,7 +4973,16 @@ bool resolver_one_wave() {
 
 void launch_resolve(kg_engine* e, const RoundGeom& g, int64_t first, int nb, int slot, int n_prev,
                     int64_t seq, int wait, hipStream_t st) {
-  if (e->numa_on) {
+  // (r6) the two-wave resolver by default; KG_NUMA_RESOLVER=1 keeps the one-wave chain (A/B runs)
+  static const bool numa_one_wave = std::getenv("KG_NUMA_RESOLVER") && std::getenv("KG_NUMA_RESOLVER")[0] == '1';
+  const size_t lds2 = resolve_numa_lds_bytes(g, nb) + numa2_extra_lds_bytes();
+  if (e->numa_on && !numa_one_wave && lds2 <= kMaxLds) {
+    const bool pre = lds2 + numa2_pre_lds_bytes(nb) <= kMaxLds;
+    resolve_round_numa2<<<1, kNuma2Threads, lds2 + (pre ? numa2_pre_lds_bytes(nb) : 0), st>>>(
+        e->T, numa_table(e), e->pods.p, e->npods.p, e->cursor.p, first, nb, cand_slot(e, g, slot), e->P, e->NP,
+        e->out_keys.p, e->out_cpus.p, e->out_nrec.p, g.bitmap_words, poison_ptr(e), seq, e->quotas.p, e->nq,
+        e->modlists.p, slot, g.depth, n_prev, wait, pre ? kNumaPre : 0);
+  } else if (e->numa_on) {
     resolve_round_numa<<<1, kWave, resolve_numa_lds_bytes(g, nb), st>>>(e->T, numa_table(e), e->pods.p, e->npods.p,
                                                                         e->cursor.p, first, nb, cand_slot(e, g, slot),
                                                                         e->P, e->NP, e->out_keys.p, e->out_cpus.p,
@@ -5623,7 +6021,10 @@ static int engine_create(const kg_config* cfg, int64_t capacity_nodes, int rank,
       return bail(fail(KG_E_DEVICE, "hipMemset"));
     const int lds = (int)(kMaxNodes / 8 + ((size_t)kMaxB * (kCandStride + kPodWords + kNumaPodWords) +
                                            (size_t)kWave * (kNumaStaticWords + kNumaMutWords)) * 8);
-    if (hipFuncSetAttribute((const void*)resolve_round_numa, hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess)
+    if (hipFuncSetAttribute((const void*)resolve_round_numa, hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess ||
+        hipFuncSetAttribute((const void*)resolve_round_numa2, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)std::min<size_t>(lds + numa2_extra_lds_bytes() + numa2_pre_lds_bytes(kMaxB), kMaxLds)) !=
+            hipSuccess)
       return bail(fail(KG_E_DEVICE, "hipFuncSetAttribute(resolve_round_numa LDS)"));
   }
   e->P.inv_la_wsum = 1.0f / (float)e->P.la_wsum;

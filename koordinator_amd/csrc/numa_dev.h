@@ -305,10 +305,10 @@ __device__ __forceinline__ CpuSet spread_first_k(const Topo& t, const CpuSet& s,
   return cs_or(first, lowest_k(cs_andnot(s, first), k - nf));
 }
 
-// Inlined into callers that run it wave-uniformly (every lane with the same node and pod): the masks, counts and group
-// keys then live in scalar registers and the branches are scalar (s_and_b64 / s_bcnt1 / s_cselect), instead of one
-// active lane issuing the 64-bit mask arithmetic as vector instructions through a call frame in scratch.
-__device__ __forceinline__ bool take_cpus(const Topo& t, const CpuSet& available, int needed, int bind, int strategy,
+// (r6) Not inlined: one shared copy.  Measured on MI355X (scripts/micro/numa_eval.hip, C4 rows, wave-uniform Reserve):
+// the inlined copies (an earlier round's choice, to keep the masks in scalar registers) cost 27.9 k cycles per cpuset
+// Reserve against 16.0 k for the call; the call's 64-bit mask arithmetic is vector but the body is a third the size.
+__device__ __attribute__((noinline)) bool take_cpus(const Topo& t, const CpuSet& available, int needed, int bind, int strategy,
                                           CpuSet& out, int excl, const CpuSet& seed) {
   Acc a;
   a.t = t;
@@ -714,6 +714,27 @@ __device__ __forceinline__ NumaHint merge_hints(uint32_t def, const HintList L0,
   const bool nilb = nl > 1 ? L1.nil != 0 : true;
   const uint32_t q0 = preferred_positions(L0), q1 = nl > 1 ? preferred_positions(L1) : 1u;
   KG_COUNT(0);
+  // (r6) Single-NUMA fast path, exact: when every preferred hint of both lists is a single-NUMA mask (positions 0-3,
+  // mask_at(k) = 1 << k: every pod whose request fits one NUMA node), pass 0's non-empty merges are the NUMA nodes in
+  // both lists, met in ascending order, all preferred, each scored with its own mask; the fold takes the first and
+  // then replaces it only on a higher score (a wider mask is never narrower) — the first of the highest score.  Only
+  // those ≤ 4 scores are computed, not the pass's ≤ 16 iterations with a divergent score inside.
+  if (!L0.nil && (nl == 1 || !L1.nil) && !(q0 & ~0xFu) && (nl == 1 || !(q1 & ~0xFu))) {
+    const uint32_t c = q0 & (nl > 1 ? q1 : 0xFu);
+    if (c) {
+      int bi = 0, bs = -1;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if ((c >> i) & 1u) {
+          const int sc = score_of(1u << i);
+          if (sc > bs) {
+            bs = sc;
+            bi = i;
+          }
+        }
+      return NumaHint{1u << bi, 0, 1, bs};
+    }
+  }
 #pragma unroll 1
   for (int pass = 0; pass < 2; ++pass) {
     if (pass == 1) KG_COUNT(1);

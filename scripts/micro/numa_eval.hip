@@ -125,6 +125,50 @@ __global__ __launch_bounds__(64) void k_numa(const NumaStatic* __restrict__ S, c
   if (lane < R) res[((size_t)P * 64 + lane) * 2] = rc;  // keep the view rebuilds live
 }
 
+// MODE 6 / 7: interference of two waves in one workgroup (blockDim 128 / 256): wave 0 evaluates the R rows as k_numa
+// MODE 0's eval, the second wave (wave 1 for 6, wave 2 for 7) evaluates row 0 wave-uniformly at the same time; each
+// wave's cycles per pod go to cyc[j*3] (wave 0) and cyc[j*3+1] (second wave)
+template <int MODE>
+__global__ __launch_bounds__(256) void k_pair(const NumaStatic* __restrict__ S, const NumaMut* __restrict__ M,
+                                              const int64_t* __restrict__ nr, int R, const NumaPod* __restrict__ pods,
+                                              int P, NumaParams NP, uint64_t* __restrict__ cyc,
+                                              int64_t* __restrict__ res) {
+  __shared__ NumaStatic s_s[64];
+  __shared__ NumaMut s_m[64];
+  const int wave = threadIdx.x / 64, lane = threadIdx.x % 64;
+  const int second = MODE == 6 ? 1 : 2;
+  if (threadIdx.x < R) {
+    s_s[threadIdx.x] = S[threadIdx.x];
+    s_m[threadIdx.x] = M[threadIdx.x];
+  }
+  __syncthreads();
+  const int row = wave == 0 ? lane : 0;
+  const bool act = (wave == 0 && lane < R) || wave == second;
+  NumaView v;
+  int64_t rc = 0, rm = 0, ac = 0, am = 0;
+  if (act) {
+    v = make_view(&s_s[row], &s_m[row], NP);
+    rc = nr[row * 4], rm = nr[row * 4 + 1], ac = nr[row * 4 + 2], am = nr[row * 4 + 3];
+  }
+  int64_t acc = 0;
+  for (int j = 0; j < P; ++j) {
+    __syncthreads();
+    if (wave != 0 && wave != second) continue;
+    const NumaPod p = pods[j];
+    const uint64_t t0 = clk();
+    int64_t sc = 0;
+    NumaHint aff{0, 1, 0, 0};
+    bool ok = false;
+    if (act) ok = numa_eval(v, p, NP, rc, rm, ac, am, sc, aff);
+    const uint64_t bm = __ballot(ok);
+    asm volatile("" ::"s"(bm));
+    const uint64_t t1 = clk();
+    acc += sc + aff.mask;
+    if (lane == 0) cyc[(size_t)j * 3 + (wave == 0 ? 0 : 1)] = t1 - t0;
+  }
+  if (act) res[threadIdx.x] = acc;
+}
+
 static int decode_pod(const kg_pod& p, int default_bind, NumaPod& d) {
   std::memset(&d, 0, sizeof(d));
   d.req_cpu = p.requests[KG_RES_CPU];
@@ -233,6 +277,8 @@ extern "C" int micro_numa(const kg_node_numa* nodes, const int64_t* node_req, in
       case 3: KG_MICRO(3); break;
       case 4: KG_MICRO(4); break;
       case 5: KG_MICRO(5); break;
+      case 6: k_pair<6><<<1, 128>>>(dS, dM, dR, R, dP, P, NP, dC, dRes); break;
+      case 7: k_pair<7><<<1, 256>>>(dS, dM, dR, R, dP, P, NP, dC, dRes); break;
       default: KG_MICRO(0); break;
     }
 #undef KG_MICRO

@@ -33,10 +33,10 @@ cpuset = np.isin(pods["qos"], [abi.QOS["LSR"], abi.QOS["LSE"]]) & (pods["request
     (pods["requests"][:, abi.RES_CPU] > 0)
 
 out = []
-MODES = {1: "admit only", 2: "filter only", 3: "score only (nil affinity)", 4: "reserve = feasible only",
+MODES = {6: "pair: waves 0 + 1", 7: "pair: waves 0 + 2", 1: "admit only", 2: "filter only", 3: "score only (nil affinity)", 4: "reserve = feasible only",
          5: "reserve = take_cpus only"}
 for lib_path in sys.argv[1:]:
-  for mode in [0] + ([1, 2, 3, 4, 5] if os.environ.get("MODES") else []):
+  for mode in [0] + [int(m) for m in os.environ.get("MODES", "").split(",") if m]:
       lib = ctypes.CDLL(os.path.abspath(lib_path))
       cyc = np.zeros((P, 3), dtype=np.uint64)
       res = np.zeros((P, 64, 2), dtype=np.int64)
@@ -46,6 +46,10 @@ for lib_path in sys.argv[1:]:
                           ctypes.c_int(int(cfg["numa_default_cpu_bind_policy"])), p(cyc), p(res), p(cps),
                             ctypes.c_int(mode))
       assert rc == 0, rc
+      if mode >= 6:
+          print(f"{lib_path} [{MODES[mode]}]: R={R} P={P}  wave 0 eval mean {cyc[:, 0].astype(float).mean():.0f} | "
+                f"second wave (one row, uniform) eval mean {cyc[:, 1].astype(float).mean():.0f}")
+          continue
       ok = (cps[:, 4] >> 1) & 1
       placed = cps[:, 4] & 1
       e = cyc[:, 0].astype(np.float64)
