@@ -2306,13 +2306,18 @@ __global__ __launch_bounds__(kWave) void resolve_round_numa(DevTable T, NumaTabl
 constexpr int kRowWords = (int)(sizeof(Row) / 8);
 static_assert(sizeof(Row) % 8 == 0, "Row in 8-byte words");
 constexpr int kNuma2Threads = 2 * kWave;
-size_t numa2_extra_lds_bytes() {  // beyond resolve_numa_lds_bytes: slot Rows, reserver's NumaMut, keys, affinities, words
-  return ((size_t)kWave * (kRowWords + 1 + 2) + kNumaMutWords + 4) * 8 + (size_t)kWave * 4 * 2 + 16 * 4;
+// (r6) a row's view (make_view, ~3-4 k cycles on one lane) is built once per state and shared through LDS: the
+// reserver publishes the view of the state it commits, the scorer the views of the rows it stages
+constexpr int kViewWords = (int)(sizeof(NumaView) / 8);
+static_assert(sizeof(NumaView) % 8 == 0, "NumaView in 8-byte words");
+size_t numa2_extra_lds_bytes() {  // beyond resolve_numa_lds_bytes: slot Rows and views, reserver's NumaMut, keys, ...
+  return ((size_t)kWave * (kRowWords + kViewWords + 1 + 2) + kNumaMutWords + 4) * 8 + (size_t)kWave * 4 * 2 + 16 * 4;
 }
-// the rows of each pod's first kNumaPre candidates, read into LDS once per round (after the chain wait, so an unmodified
-// row's copy is current): the best unmodified candidate's staging then reads LDS instead of HBM on the serial path
+// the rows (and views) of each pod's first kNumaPre candidates, read into LDS once per round (after the chain wait, so
+// an unmodified row's copy is current): the best unmodified candidate's staging then reads LDS instead of HBM and
+// rebuilding its view on the serial path
 constexpr int kNumaPre = 2;
-constexpr int kPreWords = kRowWords + kNumaStaticWords + kNumaMutWords;
+constexpr int kPreWords = kRowWords + kNumaStaticWords + kNumaMutWords + kViewWords;
 size_t numa2_pre_lds_bytes(int nb) { return (size_t)nb * kNumaPre * kPreWords * 8; }
 
 __global__ __launch_bounds__(kNuma2Threads) void resolve_round_numa2(DevTable T, NumaTable NT,
@@ -2335,7 +2340,8 @@ __global__ __launch_bounds__(kNuma2Threads) void resolve_round_numa2(DevTable T,
   uint64_t* s_nsw = s_npw + (size_t)nb * kNumaPodWords;        // [kWave] NumaStatic of the slots
   uint64_t* s_nmw = s_nsw + (size_t)kWave * kNumaStaticWords;  // [kWave] NumaMut of the slots (committed)
   uint64_t* s_roww = s_nmw + (size_t)kWave * kNumaMutWords;    // [kWave] Row of the slots (committed)
-  uint64_t* s_rnmw = s_roww + (size_t)kWave * kRowWords;       // the reserver's NumaMut after its Reserve
+  uint64_t* s_vieww = s_roww + (size_t)kWave * kRowWords;      // [kWave] view of each slot's current state
+  uint64_t* s_rnmw = s_vieww + (size_t)kWave * kViewWords;     // the reserver's NumaMut after its Reserve
   uint64_t* s_key = s_rnmw + kNumaMutWords;                    // [kWave] the scorer's keys of the current pod
   uint64_t* s_affw = s_key + kWave;                            // [kWave][2] the scorer's affinities (NumaHint)
   uint64_t* s_misc = s_affw + (size_t)kWave * 2;               // [4]: 0 = the current pod's e key (0 = none)
@@ -2344,7 +2350,7 @@ __global__ __launch_bounds__(kNuma2Threads) void resolve_round_numa2(DevTable T,
   int32_t* s_c = reinterpret_cast<int32_t*>(s_node + kWave);   // [16] 0 nM, 1 stop, 4 timed out, 5 abort
   uint32_t* bitmap = reinterpret_cast<uint32_t*>(s_c + 16);
   uint32_t* s_prevn = bitmap + bitmap_words;                   // [kWave] earlier rounds' winners (prologue)
-  uint64_t* s_pre = reinterpret_cast<uint64_t*>(s_prevn + kWave);  // [nb][npre] Row, NumaStatic, NumaMut
+  uint64_t* s_pre = reinterpret_cast<uint64_t*>(s_prevn + kWave);  // [nb][npre] Row, NumaStatic, NumaMut, view
   for (int w = tid; w < nb * kCandStride; w += kNuma2Threads) s_cand[w] = cand[w];
   {
     const uint64_t* pw = reinterpret_cast<const uint64_t*>(pods + first);
@@ -2386,8 +2392,11 @@ __global__ __launch_bounds__(kNuma2Threads) void resolve_round_numa2(DevTable T,
     const uint32_t m = key_node(key);
     uint64_t* e = s_pre + (size_t)x * kPreWords;
     *reinterpret_cast<Row*>(e) = load_row(T, m);
-    *reinterpret_cast<NumaStatic*>(e + kRowWords) = NT.s[m];
-    *reinterpret_cast<NumaMut*>(e + kRowWords + kNumaStaticWords) = NT.m[m];
+    NumaStatic* es = reinterpret_cast<NumaStatic*>(e + kRowWords);
+    NumaMut* em = reinterpret_cast<NumaMut*>(e + kRowWords + kNumaStaticWords);
+    *es = NT.s[m];
+    *em = NT.m[m];
+    *reinterpret_cast<NumaView*>(e + kRowWords + kNumaStaticWords + kNumaMutWords) = make_view(es, em, NP);
   }
   const DevPod* s_pods = reinterpret_cast<const DevPod*>(s_podw);
   const NumaPod* s_np = reinterpret_cast<const NumaPod*>(s_npw);
@@ -2395,6 +2404,7 @@ __global__ __launch_bounds__(kNuma2Threads) void resolve_round_numa2(DevTable T,
   NumaMut* s_nm = reinterpret_cast<NumaMut*>(s_nmw);
   Row* s_row = reinterpret_cast<Row*>(s_roww);
   NumaMut* s_rnm = reinterpret_cast<NumaMut*>(s_rnmw);
+  NumaView* s_view = reinterpret_cast<NumaView*>(s_vieww);
   // the rows the n_prev earlier rounds modified, de-duplicated into slots [0, nM) by wave 0 (as resolve_round_numa)
   {
     int n = 0;
@@ -2439,6 +2449,7 @@ __global__ __launch_bounds__(kNuma2Threads) void resolve_round_numa2(DevTable T,
     midx = s_node[lane];
     mrow = s_row[lane];
     mv = make_view(&s_ns[lane], &s_nm[lane], NP);
+    s_view[lane] = mv;
   }
   // reserver state (wave 1, uniform but my_out / quota lanes): the pending Reserve and the commit of the last one
   bool r_pend = false;
@@ -2449,6 +2460,7 @@ __global__ __launch_bounds__(kNuma2Threads) void resolve_round_numa2(DevTable T,
   int c_slot = -1;        // the slot that Reserve changed
   Row r_row;
   r_row.flags = 0;
+  NumaView r_view;  // the view of c_slot's state after the last placed Reserve (published at its commit)
   uint64_t r_key = 0;           // pod j's key on c_slot's new state
   NumaHint r_aff2{0, 1, 0, 0};  // its affinity
   uint64_t touch = 0;           // slots with committed Reserves (written back at the end)
@@ -2476,10 +2488,10 @@ __global__ __launch_bounds__(kNuma2Threads) void resolve_round_numa2(DevTable T,
     if (wave == 0) {
       if (live) {
         const int nM = s_c[0];
-        if (lane < nM && s_ver[lane] != myver) {  // the reserver committed a Reserve on this slot
+        if (lane < nM && s_ver[lane] != myver) {  // the reserver committed a Reserve on this slot (and its view)
           myver = s_ver[lane];
           mrow = s_row[lane];
-          mv = make_view(&s_ns[lane], &s_nm[lane], NP);
+          mv = s_view[lane];
         }
         KG_N2_SUB(0);
         const uint64_t key = s_cand[(size_t)j * kCandStride + lane];
@@ -2491,19 +2503,20 @@ __global__ __launch_bounds__(kNuma2Threads) void resolve_round_numa2(DevTable T,
         const bool stage = um && nM < kWave;
         if (stage && pos < npre) {  // e's row from the round's LDS copy: the wave copies it into the spare slot nM
           const uint64_t* e = s_pre + ((size_t)j * npre + pos) * kPreWords;
+          constexpr int kS = kRowWords, kM = kS + kNumaStaticWords, kV = kM + kNumaMutWords;
           for (int w = lane; w < kPreWords; w += kWave) {
             const uint64_t v = e[w];
-            if (w < kRowWords) s_roww[(size_t)nM * kRowWords + w] = v;
-            else if (w < kRowWords + kNumaStaticWords) s_nsw[(size_t)nM * kNumaStaticWords + (w - kRowWords)] = v;
-            else s_nmw[(size_t)nM * kNumaMutWords + (w - kRowWords - kNumaStaticWords)] = v;
+            if (w < kS) s_roww[(size_t)nM * kRowWords + w] = v;
+            else if (w < kM) s_nsw[(size_t)nM * kNumaStaticWords + (w - kS)] = v;
+            else if (w < kV) s_nmw[(size_t)nM * kNumaMutWords + (w - kM)] = v;
+            else s_vieww[(size_t)nM * kViewWords + (w - kV)] = v;
           }
           if (lane == nM) {  // its Filter gives the affinity Reserve needs (read from the copy: no cross-lane wait)
             midx = key_node(ekey);
             mrow = *reinterpret_cast<const Row*>(e);
             s_node[nM] = midx;
             myver = s_ver[nM];
-            mv = make_view(reinterpret_cast<const NumaStatic*>(e + kRowWords),
-                           reinterpret_cast<const NumaMut*>(e + kRowWords + kNumaStaticWords), NP);
+            mv = *reinterpret_cast<const NumaView*>(e + kV);
           }
         } else if (stage && lane == nM) {  // e's row into the spare slot: its Filter gives the affinity Reserve needs
           const uint32_t en = key_node(ekey);
@@ -2515,6 +2528,7 @@ __global__ __launch_bounds__(kNuma2Threads) void resolve_round_numa2(DevTable T,
           s_node[nM] = en;
           myver = s_ver[nM];
           mv = make_view(&s_ns[nM], &s_nm[nM], NP);
+          s_view[nM] = mv;
         }
         const DevPod p = s_pods[j];
         const NumaPod np = s_np[j];
@@ -2542,7 +2556,8 @@ __global__ __launch_bounds__(kNuma2Threads) void resolve_round_numa2(DevTable T,
         const NumaPod np = s_np[r_j];
         const NumaStatic ns = s_ns[r_slot];
         NumaMut nm = s_nm[r_slot];
-        const NumaView ov = make_view(&s_ns[r_slot], &s_nm[r_slot], NP);
+        // the slot's current view, published with its state (this wave's commit, or the scorer's staging of e)
+        const NumaView ov = s_view[r_slot];
         CpuSet cpus;
         NumaAlloc rec;
         r_placed = numa_reserve(ns, nm, ov, np, r_aff, cpus, rec);
@@ -2574,11 +2589,11 @@ __global__ __launch_bounds__(kNuma2Threads) void resolve_round_numa2(DevTable T,
           }
           if (nq > 0) quota_charge(ql, p, lane);
           KG_N2_STAMP(3);
+          r_view = make_view(&s_ns[r_slot], s_rnm, NP);
           if (live) {  // pod j's key on the new state (the scorer saw the state before this Reserve)
-            const NumaView nv = make_view(&s_ns[r_slot], s_rnm, NP);
             int64_t t = 0;
             r_aff2 = NumaHint{0, 1, 0, 0};
-            r_key = eval_node_numa(r_row, nv, s_pods[j], s_np[j], P, NP, t, r_aff2)
+            r_key = eval_node_numa(r_row, r_view, s_pods[j], s_np[j], P, NP, t, r_aff2)
                         ? make_key(t, s_node[r_slot]) : 0;
           }
         }
@@ -2593,6 +2608,7 @@ __global__ __launch_bounds__(kNuma2Threads) void resolve_round_numa2(DevTable T,
         if (lane == 0) {
           s_nm[c_slot] = *s_rnm;
           s_row[c_slot] = r_row;
+          s_view[c_slot] = r_view;
           s_ver[c_slot] += 1;
         }
         touch |= 1ull << c_slot;
