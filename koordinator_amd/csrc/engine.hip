@@ -4989,10 +4989,13 @@ bool resolver_one_wave() {
 
 void launch_resolve(kg_engine* e, const RoundGeom& g, int64_t first, int nb, int slot, int n_prev,
                     int64_t seq, int wait, hipStream_t st) {
-  // (r6) the two-wave resolver by default; KG_NUMA_RESOLVER=1 keeps the one-wave chain (A/B runs)
+  // (r6) the two-wave resolver on one rank; KG_NUMA_RESOLVER=1 keeps the one-wave chain (A/B runs).  Several ranks
+  // keep the one-wave chain: in the one-process loopback mode (tests/test_multirank_loopback.py) the ranks' round
+  // streams share the process's 4 hardware queues, and the two-wave kernel's chain wait once outlasted its spin limit
+  // there (test_numa_ranks, r6) — the one-wave kernel is the measured-safe choice for that mode
   static const bool numa_one_wave = std::getenv("KG_NUMA_RESOLVER") && std::getenv("KG_NUMA_RESOLVER")[0] == '1';
   const size_t lds2 = resolve_numa_lds_bytes(g, nb) + numa2_extra_lds_bytes();
-  if (e->numa_on && !numa_one_wave && lds2 <= kMaxLds) {
+  if (e->numa_on && !numa_one_wave && e->n_ranks == 1 && lds2 <= kMaxLds) {
     const bool pre = lds2 + numa2_pre_lds_bytes(nb) <= kMaxLds;
     resolve_round_numa2<<<1, kNuma2Threads, lds2 + (pre ? numa2_pre_lds_bytes(nb) : 0), st>>>(
         e->T, numa_table(e), e->pods.p, e->npods.p, e->cursor.p, first, nb, cand_slot(e, g, slot), e->P, e->NP,
