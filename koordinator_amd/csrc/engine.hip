@@ -4989,13 +4989,14 @@ bool resolver_one_wave() {
 
 void launch_resolve(kg_engine* e, const RoundGeom& g, int64_t first, int nb, int slot, int n_prev,
                     int64_t seq, int wait, hipStream_t st) {
-  // (r6) the two-wave resolver on one rank; KG_NUMA_RESOLVER=1 keeps the one-wave chain (A/B runs).  Several ranks
-  // keep the one-wave chain: in the one-process loopback mode (tests/test_multirank_loopback.py) the ranks' round
-  // streams share the process's 4 hardware queues, and the two-wave kernel's chain wait once outlasted its spin limit
-  // there (test_numa_ranks, r6) — the one-wave kernel is the measured-safe choice for that mode
+  // (r6) the two-wave resolver while the engine's round streams have hardware queues of their own (one rank, depth
+  // ≤ 3: with the main stream ≤ 4 streams, GPU_MAX_HW_QUEUES); KG_NUMA_RESOLVER=1 keeps the one-wave chain (A/B runs).
+  // Where streams share a queue — depth 4, or several loopback ranks in one process — the two-wave kernel's chain
+  // wait outlasted its spin limit in r6 (test_c4_pipelined_parity[8-4], test_numa_ranks); the one-wave kernel is the
+  // measured-safe choice there
   static const bool numa_one_wave = std::getenv("KG_NUMA_RESOLVER") && std::getenv("KG_NUMA_RESOLVER")[0] == '1';
   const size_t lds2 = resolve_numa_lds_bytes(g, nb) + numa2_extra_lds_bytes();
-  if (e->numa_on && !numa_one_wave && e->n_ranks == 1 && lds2 <= kMaxLds) {
+  if (e->numa_on && !numa_one_wave && e->n_ranks == 1 && g.depth <= 3 && lds2 <= kMaxLds) {
     const bool pre = lds2 + numa2_pre_lds_bytes(nb) <= kMaxLds;
     resolve_round_numa2<<<1, kNuma2Threads, lds2 + (pre ? numa2_pre_lds_bytes(nb) : 0), st>>>(
         e->T, numa_table(e), e->pods.p, e->npods.p, e->cursor.p, first, nb, cand_slot(e, g, slot), e->P, e->NP,
