@@ -5307,16 +5307,22 @@ RsvExt rsv_ext(kg_engine* e) {
 int rsv_eval_flags(const RsvExt& X) {
   return (X.dsx || X.rcpu ? RSV_F_XF : 0) | (X.ns ? RSV_F_NUMA : 0) | (X.ds ? RSV_F_DS : 0);
 }
-using RsvEvalFn = decltype(&rsv_eval<0>);
-RsvEvalFn rsv_eval_kernel(int f) {
-  switch (f) {  // the combinations a profile yields (XF needs NUMA or DeviceShare); the rest take the full kernel
-    case 0: return rsv_eval<0>;
-    case RSV_F_NUMA: return rsv_eval<RSV_F_NUMA>;
-    case RSV_F_DS: return rsv_eval<RSV_F_DS>;
-    case RSV_F_NUMA | RSV_F_DS: return rsv_eval<RSV_F_NUMA | RSV_F_DS>;
-    default: return rsv_eval<RSV_F_XF | RSV_F_NUMA | RSV_F_DS>;
+// the combinations a profile yields (XF needs NUMA or DeviceShare); the rest take the full kernel
+#define KG_RSV_VARIANT(K, f)                                           \
+  switch (f) {                                                        \
+    case 0: return K<0>;                                              \
+    case RSV_F_NUMA: return K<RSV_F_NUMA>;                            \
+    case RSV_F_DS: return K<RSV_F_DS>;                                \
+    case RSV_F_NUMA | RSV_F_DS: return K<RSV_F_NUMA | RSV_F_DS>;      \
+    default: return K<RSV_F_XF | RSV_F_NUMA | RSV_F_DS>;              \
   }
-}
+using RsvEvalFn = decltype(&rsv_eval<0>);
+RsvEvalFn rsv_eval_kernel(int f) { KG_RSV_VARIANT(rsv_eval, f) }
+using GroupPreFn = decltype(&group_pre<0>);
+GroupPreFn group_pre_kernel(int f) { KG_RSV_VARIANT(group_pre, f) }
+using RsvApplyFn = decltype(&rsv_apply<0>);
+RsvApplyFn rsv_apply_kernel(int f) { KG_RSV_VARIANT(rsv_apply, f) }
+#undef KG_RSV_VARIANT
 
 int run_rsv(kg_engine* e, int64_t first, int64_t count, kg_stats* stats, double t0) {
   if (int rc = sync_static(e)) return rc;
@@ -5338,7 +5344,7 @@ int run_rsv(kg_engine* e, int64_t first, int64_t count, kg_stats* stats, double 
       for (int g = 0; g < passes; ++g) {
         size_t t = prof_begin(e, e->stream);
         if (e->grp_on)  // Reserve of the previous pod + the group reductions this pod's Filters need
-          group_pre<<<blocks, kRsvThreads, 0, e->stream>>>(e->T, e->rsv_d.p, e->pods.p, end_arg, n, g, X, e->rsv_val.p,
+          group_pre_kernel(rf)<<<blocks, kRsvThreads, 0, e->stream>>>(e->T, e->rsv_d.p, e->pods.p, end_arg, n, g, X, e->rsv_val.p,
                                                            e->rsv_part.p, e->out_keys.p, e->out_rslot.p, e->rsv_ws.p);
         rsv_eval_kernel(rf)<<<blocks, kRsvThreads, 0, e->stream>>>(
             e->T, e->rsv_d.p, e->rsv_nd.p, e->pods.p, e->rpods.p, end_arg, n, g, e->P, e->RP, X, e->rsv_val.p,
@@ -5353,7 +5359,7 @@ int run_rsv(kg_engine* e, int64_t first, int64_t count, kg_stats* stats, double 
         prof_end(e, KG_PROF_RSV_SELECT, t, e->stream);
       }
       size_t t = prof_begin(e, e->stream);
-      rsv_apply<<<1, kWave, 0, e->stream>>>(e->T, e->rsv_d.p, e->rsv_val.p, e->pods.p, end_arg, (int)blocks, passes - 1,
+      rsv_apply_kernel(rf)<<<1, kWave, 0, e->stream>>>(e->T, e->rsv_d.p, e->rsv_val.p, e->pods.p, end_arg, (int)blocks, passes - 1,
                                             X, e->rsv_part.p, e->out_keys.p, e->out_rslot.p, e->rsv_ws.p);
       prof_end(e, KG_PROF_RSV_APPLY, t, e->stream);
     };

@@ -1208,6 +1208,7 @@ __global__ __launch_bounds__(kRsvThreads) void rsv_select2(const uint64_t* __res
 // DoNotSchedule constraint's count (enc_min_i32; 0 = none: MaxInt32), part[7 nb + b] = Σ over valid nodes of pods
 // matching the required pod-affinity group (only those carrying a zone label when every required term is zone-keyed:
 // affinityCounts then has no hostname pairs); the zone sums (ZoneSums) with one atomic per block and nonzero word.
+template <int F>  // RSV_F_* (as rsv_eval): the Reserve compiled for the profile's plugins only
 __global__ __launch_bounds__(kRsvThreads) void group_pre(DevTable T, RsvNode* __restrict__ RN,
                                                          const DevPod* __restrict__ pods, int64_t end, int64_t n,
                                                          int g, RsvExt X, const uint64_t* __restrict__ val,
@@ -1226,7 +1227,10 @@ __global__ __launch_bounds__(kRsvThreads) void group_pre(DevTable T, RsvNode* __
     if (i == w || (w < 0 && i == 0)) {
       int32_t slot = -1;
       bool placed = false;
-      if (w >= 0) placed = rsv_reserve(T, RN, w, val[w], pods[j - 1], X, j - 1, slot);
+      if (w >= 0)
+        placed = rsv_reserve<(F & RSV_F_NUMA) != 0, (F & RSV_F_DS) != 0, (F & RSV_F_XF) != 0>(T, RN, w, val[w],
+                                                                                              pods[j - 1], X, j - 1,
+                                                                                              slot);
       out_keys[j - 1] = placed ? k : 0;
       out_slot[j - 1] = slot;
       if (placed && X.nq > 0 && pods[j - 1].quota >= 0) {
@@ -1294,6 +1298,7 @@ __global__ __launch_bounds__(kRsvThreads) void group_pre(DevTable T, RsvNode* __
 
 // End of a group of kRsvGroup pods (one wave): Reserve of the group's last pod (cursor + g_last) with its quota
 // charge, and the cursor advance.  Pods past `end` are skipped.
+template <int F>  // RSV_F_* (as rsv_eval)
 __global__ __launch_bounds__(kWave) void rsv_apply(DevTable T, RsvNode* __restrict__ RN,
                                                    const uint64_t* __restrict__ val, const DevPod* __restrict__ pods,
                                                    int64_t end, int nb, int g_last, RsvExt X,
@@ -1311,7 +1316,8 @@ __global__ __launch_bounds__(kWave) void rsv_apply(DevTable T, RsvNode* __restri
     bool placed = false;
     if (k) {
       const int64_t w = (int64_t)key_node(k);
-      placed = rsv_reserve(T, RN, w, val[w], pods[j], X, j, slot);
+      placed = rsv_reserve<(F & RSV_F_NUMA) != 0, (F & RSV_F_DS) != 0, (F & RSV_F_XF) != 0>(T, RN, w, val[w], pods[j],
+                                                                                            X, j, slot);
     }
     out_keys[j] = placed ? k : 0;
     out_slot[j] = slot;
