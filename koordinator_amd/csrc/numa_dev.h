@@ -322,6 +322,26 @@ __device__ __attribute__((noinline)) bool take_cpus(const Topo& t, const CpuSet&
   if (a.needed < 1) return true;
   if (a.needed > cs_count(a.avail)) return false;
   const bool full = bind == 2;
+  // (r6) One NUMA node, exact shortcut: Reserve calls this per NUMA node of the hint, so the available cpus usually lie
+  // in one node.  Then freeCoresInNode (no exclusive policy: one pass, nothing excluded) lists that node alone, and
+  // when its whole-core cpus cover the request the first branch below takes the lowest `needed` of them — taken here
+  // without the eight-group orders.  Any other case runs the full accumulator.
+  if ((full || t.cpc == 1) && a.excl == KG_EXCL_NONE && a.needed <= t.per_node()) {
+    int lo = -1, hi = -1;
+#pragma unroll
+    for (int w = 0; w < kCpuWords; ++w)
+      if (a.avail.w[w]) {
+        if (lo < 0) lo = 64 * w + __builtin_ctzll(a.avail.w[w]);
+        hi = 64 * w + 63 - __builtin_clzll(a.avail.w[w]);
+      }
+    if (lo >= 0 && t.node_of(lo) == t.node_of(hi)) {
+      const CpuSet fc = full_core_cpus(t, a.avail);
+      if (cs_count(fc) >= a.needed) {
+        out = lowest_k(fc, a.needed);
+        return true;
+      }
+    }
+  }
   uint64_t k[8];
   if (full || t.cpc == 1) {
     if (a.needed <= t.per_node()) {
