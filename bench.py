@@ -55,11 +55,11 @@ WORKLOADS = {
     "c2": (10_000, 10_000, 32, 8, 10_000),
     "c3": (100_000, 100_000, 38, 8, 10_000),  # (r5) B = 38: the resolver and the eval→merge chain balance
     "c4": (10_000, 10_000, 16, 1, 2_000),
-    "c5": (50_000, 10_000, 32, 4, 2_000),
-    "c5ds": (50_000, 10_000, 32, 4, 2_000),
-    "c5r": (50_000, 10_000, 32, 4, 2_000),
+    "c5": (50_000, 10_000, 32, 4, 10_000),    # (r6) the first step's 10k pods checked against the live oracle
+    "c5ds": (50_000, 10_000, 32, 4, 10_000),
+    "c5r": (50_000, 10_000, 32, 4, 10_000),
     "shipped": (50_000, 5_000, 32, 4, 1_000),
-    "stock": (10_000, 2_000, 32, 8, 500),
+    "stock": (10_000, 2_000, 32, 8, 2_000),
     "stockz": (10_000, 2_000, 32, 8, 500),
 }
 
